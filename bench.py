@@ -1,0 +1,127 @@
+#!/usr/bin/env python3
+"""Headline benchmark: DPOTRF GFLOP/s, N=65536, NB=512, on 1/2/4/8 MI355X.
+
+Metric and config are the ones named in BASELINE.json.  One process per GPU
+(``torch.distributed.run --nproc-per-node N``; RCCL over xGMI), 2-D
+block-cyclic P x Q grid (8 -> 2x4, 4 -> 2x2, 2 -> 1x2, 1 -> 1x1).  The input is
+the reference's SPD test matrix ``dplghe(bump=N, seed=3872)`` (synthetic, LCG
+generated on the GPU, bit-identical to the reference generator).
+
+A "step" = restore A from a pristine device copy + one full distributed
+Cholesky factorisation (the restore is timed too -- conservative).  W untimed
+warm-up steps, then exactly K timed steps bracketed by barrier + device
+synchronize on both sides; the max time over ranks is reported.  Flops are
+FLOPS_DPOTRF(N) = N^3/3 + N^2/2 + N/6 per step (src/flops.h), as in the
+reference harness (tests/common.h:136-137, 268-277).  Strong scaling: N is
+fixed as the GPU count grows.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+BASELINE_METRIC = "GFLOP/s DPOTRF N=64k NB=512 at 1/2/4/8 MI355X; % of fp64 MFMA peak"
+FP64_PEAK_GFLOPS = 78600.0  # per MI355X, datasheet
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("-N", "--N", type=int, default=65536)
+    ap.add_argument("--nb", type=int, default=512)
+    ap.add_argument("-P", type=int, default=None)
+    ap.add_argument("--check", action="store_true", help="verify the factorisation after the timed steps")
+    ap.add_argument("--trace", default=None, help="write a Chrome trace of one step to this file")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import dplasma_amd as dp
+
+    P = args.P
+    if P is None:
+        P = {1: 1, 2: 1, 4: 2, 8: 2}.get(world, None)
+    ctx = dp.init(P=P)
+    rank = ctx.rank
+    N, NB = args.N, args.nb
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N, name="A", uplo=dp.dplasmaLower)
+    dp.dplghe(ctx, float(N), dp.dplasmaLower, A, 3872)
+    A0 = A.data.clone()
+    ctx.sync()
+    t0 = time.perf_counter()
+    tp = dp.dpotrf_New(ctx, dp.dplasmaLower, A)
+    t_enq = time.perf_counter() - t0
+    flops = tp.flops
+
+    def step():
+        A.data.copy_(A0)
+        tp.info.zero_()
+        tp.run(ctx)
+
+    for _ in range(args.warmup):
+        step()
+    tp.complete(ctx)
+    ctx.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.sync()
+    ctx.barrier()
+    t1 = time.perf_counter()
+    info = tp.complete(ctx)
+    el = torch.tensor([t1 - t0], dtype=torch.float64, device=ctx.device)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    ms = elapsed / args.steps * 1e3
+    gflops = flops * args.steps / elapsed / 1e9
+    ok = None
+    if args.check:
+        A_orig = A.like()
+        A_orig.data.copy_(A0)
+        ok, res = dp.check_potrf(ctx, dp.dplasmaLower, A, A_orig, verbose=True)
+    if rank == 0:
+        print(f"[****] TIME(s) {ms / 1e3:12.5f} : dpotrf PxQxg= {ctx.P:3d} {ctx.Q:<3d} 1 NB= {NB:4d} N= {N:7d} : "
+              f"{gflops / world:14f} gflops/gpu - ENQ {t_enq:.3f} info={info}", file=sys.stderr)
+        out = {
+            "metric": BASELINE_METRIC,
+            "value": round(gflops, 2),
+            "unit": "GFLOP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "fp64",
+            "data": "synthetic (dplghe SPD, bump=N, seed=3872; random-init, LCG generated on GPU)",
+            "pct_fp64_peak": round(100.0 * gflops / (FP64_PEAK_GFLOPS * world), 2),
+            "info": info,
+            "check": ok,
+            "config": {"model": "dpotrf (lower, 2D block-cyclic tiles)", "N": N, "NB": NB, "global_batch": 1,
+                       "seq_len": N, "parallelism": f"{ctx.P}x{ctx.Q} block-cyclic (one rank per GPU)"},
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

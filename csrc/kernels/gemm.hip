@@ -1,0 +1,416 @@
+// Batched tile GEMM engine: C_item = beta*C_item + alpha * sum_kt opA(A_kt) * opB(B_kt)
+//
+// This is the flop engine of every dplasma_amd algorithm (the role cublasZgemm
+// plays inside the reference's JDF CUDA bodies, e.g. src/zpotrf_L.jdf:432-471,
+// src/zgemm_NN_summa.jdf:209-242, src/zgetrf_nopiv.jdf:198-235).  Instead of one
+// vendor call per tile, one launch covers every output tile of a step:
+//
+//   * each GemmItem names one C tile and a run of KPair records (the k-tiles to
+//     contract), so a whole local SUMMA/GEMM, or one Cholesky trailing update,
+//     is a single launch;
+//   * f64 uses v_mfma_f64_16x16x4_f64, f32 uses v_mfma_f32_16x16x4_f32:
+//     256-thread workgroups, 128x128 C sub-tile per workgroup, 4 waves in 2x2,
+//     64x64 per wave = 4x4 MFMA blocks, BK=16 k-steps double-buffered in LDS
+//     (row stride 144 elements => conflict-free ds_read_b64 halves);
+//   * operand roles are swapped inside the MFMA (D = opB^T * opA^T) so the
+//     accumulator's lane index runs along C's rows, i.e. along the contiguous
+//     direction of column-major tiles: epilogue stores are 128-B segments;
+//   * accumulators are initialised with beta*C (C is read once, up front, its
+//     latency overlapping the first operand loads) and alpha is folded into the
+//     A staging, so the epilogue is a pure store;
+//   * blockIdx is remapped XCD-aware so the 16 sub-tiles of a 512x512 tile and
+//     neighbouring tiles of a tile-row share one XCD's L2.
+// Complex precisions use a generic LDS-tiled FMA kernel (same item protocol).
+#include "common.h"
+
+struct KPair {
+  long long a_off, b_off;
+  int k;
+  int pad;
+};
+struct GemmItemK {
+  long long c_off;
+  int kt_beg, kt_cnt;  // run of KPair records
+  int m, n;
+  int flags;           // bits 0-1: C write mask (0 full, 1 lower, 2 upper)
+  int pad;
+};
+
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+template <typename T> struct MF;
+template <> struct MF<double> {
+  typedef d4_t acc_t;
+  typedef d2v vec_t;
+  static constexpr int VEC = 2;
+  static __device__ inline acc_t mma(double a, double b, acc_t c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+  }
+  // row (within a 16x16 block, along the D "row" axis) held by lane l, register r
+  static __device__ inline int drow(int l, int r) { return (l >> 4) + 4 * r; }
+};
+template <> struct MF<float> {
+  typedef f4_t acc_t;
+  typedef f4v vec_t;
+  static constexpr int VEC = 4;
+  static __device__ inline acc_t mma(float a, float b, acc_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+  static __device__ inline int drow(int l, int r) { return (l >> 4) * 4 + r; }
+};
+
+#define GBM 128
+#define GBN 128
+#define GBK 16
+#define GLS 144
+
+template <typename T, bool TA, bool TB>
+__global__ __launch_bounds__(256, 2) void k_gemm_mfma(const GemmItemK* __restrict__ items,
+                                                      const KPair* __restrict__ kps, int nsm, int nsn,
+                                                      int nwg, T alpha, const T* __restrict__ A, int lda,
+                                                      const T* __restrict__ B, int ldb, T beta,
+                                                      T* __restrict__ C, int ldc, int vec_ok) {
+  typedef MF<T> M_;
+  typedef typename M_::acc_t acc_t;
+  typedef typename M_::vec_t vec_t;
+  constexpr int VEC = M_::VEC;
+  constexpr int NLD = (GBM * GBK) / (VEC * 256);  // 16-byte loads per thread per operand per k-step
+  __shared__ T sm[2][2][GBK][GLS];
+
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int per = nsm * nsn;
+  const GemmItemK it = items[wg / per];
+  const int sub = wg % per;
+  const int m0 = (sub % nsm) * GBM, n0 = (sub / nsm) * GBN;
+  const int Mt = it.m, Nt = it.n;
+  if (m0 >= Mt || n0 >= Nt) return;
+  const int uplo = it.flags & 3;
+  if (uplo == 1 && n0 >= m0 + GBM) return;
+  if (uplo == 2 && m0 >= n0 + GBN) return;
+
+  T* Cb = C + it.c_off;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int wm = w & 1, wn = w >> 1;
+  const bool fullmn = vec_ok && (m0 + GBM <= Mt) && (n0 + GBN <= Nt);
+
+  acc_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int mm = m0 + wm * 64 + i * 16 + (l & 15);
+        const int nn = n0 + wn * 64 + j * 16 + M_::drow(l, r);
+        T v = T(0);
+        if (beta != T(0) && mm < Mt && nn < Nt) v = beta * Cb[mm + (long long)nn * ldc];
+        acc[i][j][r] = v;
+      }
+
+  // flatten the (k-tile, k-block) iteration space
+  int nsteps = 0;
+  for (int t = 0; t < it.kt_cnt; ++t) nsteps += (kps[it.kt_beg + t].k + GBK - 1) / GBK;
+
+  vec_t ra[NLD], rb[NLD];
+  int ld_kt = it.kt_beg, ld_k0 = 0;  // position of the next load
+  KPair kp;
+  kp.a_off = 0; kp.b_off = 0; kp.k = 0;
+  if (it.kt_cnt > 0) kp = kps[ld_kt];
+
+  auto load = [&](void) {
+    const T* Ab = A + kp.a_off;
+    const T* Bb = B + kp.b_off;
+    const int Kt = kp.k;
+    const bool fk = fullmn && (ld_k0 + GBK <= Kt);
+#pragma unroll
+    for (int q = 0; q < NLD; ++q) {
+      const int c = tid + 256 * q;
+      // ---- A: op(A)(i, k), i in [0,128), k in [0,16)
+      if (!TA) {
+        const int kk = c / (GBM / VEC), i = (c % (GBM / VEC)) * VEC;
+        const T* src = Ab + (m0 + i) + (long long)(ld_k0 + kk) * lda;
+        if (fk) {
+          ra[q] = *(const vec_t*)src;
+        } else {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e)
+            ra[q][e] = (m0 + i + e < Mt && ld_k0 + kk < Kt) ? src[e] : T(0);
+        }
+      } else {
+        const int i = c / (GBK / VEC), kk = (c % (GBK / VEC)) * VEC;
+        const T* src = Ab + (ld_k0 + kk) + (long long)(m0 + i) * lda;
+        if (fk) {
+          ra[q] = *(const vec_t*)src;
+        } else {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e)
+            ra[q][e] = (m0 + i < Mt && ld_k0 + kk + e < Kt) ? src[e] : T(0);
+        }
+      }
+      // ---- B: op(B)(k, j)
+      if (TB) {
+        const int kk = c / (GBN / VEC), j = (c % (GBN / VEC)) * VEC;
+        const T* src = Bb + (n0 + j) + (long long)(ld_k0 + kk) * ldb;
+        if (fk) {
+          rb[q] = *(const vec_t*)src;
+        } else {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e)
+            rb[q][e] = (n0 + j + e < Nt && ld_k0 + kk < Kt) ? src[e] : T(0);
+        }
+      } else {
+        const int j = c / (GBK / VEC), kk = (c % (GBK / VEC)) * VEC;
+        const T* src = Bb + (ld_k0 + kk) + (long long)(n0 + j) * ldb;
+        if (fk) {
+          rb[q] = *(const vec_t*)src;
+        } else {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e)
+            rb[q][e] = (n0 + j < Nt && ld_k0 + kk + e < Kt) ? src[e] : T(0);
+        }
+      }
+    }
+    // advance
+    ld_k0 += GBK;
+    if (ld_k0 >= Kt) {
+      ld_k0 = 0;
+      ++ld_kt;
+      if (ld_kt < it.kt_beg + it.kt_cnt) kp = kps[ld_kt];
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < NLD; ++q) {
+      const int c = tid + 256 * q;
+      if (!TA) {
+        const int kk = c / (GBM / VEC), i = (c % (GBM / VEC)) * VEC;
+        vec_t v = ra[q] * alpha;
+        *(vec_t*)&sm[buf][0][kk][i] = v;
+      } else {
+        const int i = c / (GBK / VEC), kk = (c % (GBK / VEC)) * VEC;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) sm[buf][0][kk + e][i] = ra[q][e] * alpha;
+      }
+      if (TB) {
+        const int kk = c / (GBN / VEC), j = (c % (GBN / VEC)) * VEC;
+        *(vec_t*)&sm[buf][1][kk][j] = rb[q];
+      } else {
+        const int j = c / (GBK / VEC), kk = (c % (GBK / VEC)) * VEC;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) sm[buf][1][kk + e][j] = rb[q][e];
+      }
+    }
+  };
+
+  if (nsteps > 0) {
+    load();
+    store(0);
+  }
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < nsteps) load();
+#pragma unroll
+    for (int kq = 0; kq < GBK / 4; ++kq) {
+      const int kr = kq * 4 + (l >> 4);
+      T a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = sm[cur][0][kr][wm * 64 + i * 16 + (l & 15)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = sm[cur][1][kr][wn * 64 + j * 16 + (l & 15)];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = M_::mma(b[j], a[i], acc[i][j]);
+    }
+    if (s + 1 < nsteps) store(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int mm = m0 + wm * 64 + i * 16 + (l & 15);
+        const int nn = n0 + wn * 64 + j * 16 + M_::drow(l, r);
+        bool ok = mm < Mt && nn < Nt;
+        if (uplo == 1) ok = ok && (mm >= nn);
+        if (uplo == 2) ok = ok && (mm <= nn);
+        if (ok) Cb[mm + (long long)nn * ldc] = acc[i][j][r];
+      }
+}
+
+// ------------------------------------------------------------------ generic
+// 64x64 C tile per 256-thread workgroup, 4x4 outputs per thread, BK=16.
+// OPA/OPB: 0 = N, 1 = T, 2 = C (conjugate transpose).
+template <typename T, int OPA, int OPB>
+__global__ __launch_bounds__(256) void k_gemm_generic(const GemmItemK* __restrict__ items,
+                                                      const KPair* __restrict__ kps, int nsm, int nsn,
+                                                      int nwg, T alpha, const T* __restrict__ A, int lda,
+                                                      const T* __restrict__ B, int ldb, T beta,
+                                                      T* __restrict__ C, int ldc) {
+  constexpr int BM = 64, BN = 64, BK = 16;
+  __shared__ T As[BK][BM + 1];
+  __shared__ T Bs[BK][BN + 1];
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int per = nsm * nsn;
+  const GemmItemK it = items[wg / per];
+  const int sub = wg % per;
+  const int m0 = (sub % nsm) * BM, n0 = (sub / nsm) * BN;
+  const int Mt = it.m, Nt = it.n;
+  if (m0 >= Mt || n0 >= Nt) return;
+  const int uplo = it.flags & 3;
+  if (uplo == 1 && n0 >= m0 + BM) return;
+  if (uplo == 2 && m0 >= n0 + BN) return;
+  T* Cb = C + it.c_off;
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  T acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = ST<T>::zero();
+
+  for (int t = 0; t < it.kt_cnt; ++t) {
+    const KPair kp = kps[it.kt_beg + t];
+    const T* Ab = A + kp.a_off;
+    const T* Bb = B + kp.b_off;
+    for (int k0 = 0; k0 < kp.k; k0 += BK) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e = tid + 256 * q;
+        int i, kk;
+        if (OPA == 0) { i = e & 63; kk = e >> 6; } else { kk = e & 15; i = e >> 4; }
+        T v = ST<T>::zero();
+        if (m0 + i < Mt && k0 + kk < kp.k) {
+          v = (OPA == 0) ? Ab[(m0 + i) + (long long)(k0 + kk) * lda]
+                         : Ab[(k0 + kk) + (long long)(m0 + i) * lda];
+          if (OPA == 2) v = conj_(v);
+        }
+        As[kk][i] = mul(alpha, v);
+        int j;
+        if (OPB == 0) { kk = e & 15; j = e >> 4; } else { j = e & 63; kk = e >> 6; }
+        T u = ST<T>::zero();
+        if (n0 + j < Nt && k0 + kk < kp.k) {
+          u = (OPB == 0) ? Bb[(k0 + kk) + (long long)(n0 + j) * ldb]
+                         : Bb[(n0 + j) + (long long)(k0 + kk) * ldb];
+          if (OPB == 2) u = conj_(u);
+        }
+        Bs[kk][j] = u;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int kk = 0; kk < BK; ++kk) {
+        T a[4], b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = As[kk][tx + 16 * i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = Bs[kk][ty + 16 * j];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = fma_(a[i], b[j], acc[i][j]);
+      }
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int mm = m0 + tx + 16 * i, nn = n0 + ty + 16 * j;
+      bool ok = mm < Mt && nn < Nt;
+      if (uplo == 1) ok = ok && (mm >= nn);
+      if (uplo == 2) ok = ok && (mm <= nn);
+      if (ok) {
+        T* p = Cb + mm + (long long)nn * ldc;
+        T v = acc[i][j];
+        if (!is_zero(beta)) v = add(v, mul(beta, *p));
+        *p = v;
+      }
+    }
+}
+
+// ------------------------------------------------------------------ launchers
+static inline int op_code(int trans) { return trans == DPL_NOTRANS ? 0 : (trans == DPL_TRANS ? 1 : 2); }
+
+template <typename T>
+static int launch_mfma(int opa, int opb, int nitems, const GemmItemK* items, const KPair* kps, int max_m,
+                       int max_n, T alpha, const T* A, int lda, const T* B, int ldb, T beta, T* C, int ldc,
+                       int vec_ok, hipStream_t st) {
+  const int nsm = cdiv(max_m, GBM), nsn = cdiv(max_n, GBN);
+  const long long nwgl = (long long)nitems * nsm * nsn;
+  if (nwgl <= 0) return 0;
+  if (nwgl > 0x7fffffffLL) return -1;
+  const int nwg = (int)nwgl;
+  dim3 g(nwg), b(256);
+  const bool ta = opa != 0, tb = opb != 0;
+  if (!ta && !tb) hipLaunchKernelGGL((k_gemm_mfma<T, false, false>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc, vec_ok);
+  else if (!ta && tb) hipLaunchKernelGGL((k_gemm_mfma<T, false, true>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc, vec_ok);
+  else if (ta && !tb) hipLaunchKernelGGL((k_gemm_mfma<T, true, false>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc, vec_ok);
+  else hipLaunchKernelGGL((k_gemm_mfma<T, true, true>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc, vec_ok);
+  return (int)hipGetLastError();
+}
+
+template <typename T, int OA, int OB>
+static void lg1(dim3 g, hipStream_t st, const GemmItemK* items, const KPair* kps, int nsm, int nsn, int nwg,
+                T alpha, const T* A, int lda, const T* B, int ldb, T beta, T* C, int ldc) {
+  hipLaunchKernelGGL((k_gemm_generic<T, OA, OB>), g, dim3(256), 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B,
+                     ldb, beta, C, ldc);
+}
+
+template <typename T>
+static int launch_generic(int opa, int opb, int nitems, const GemmItemK* items, const KPair* kps, int max_m,
+                          int max_n, T alpha, const T* A, int lda, const T* B, int ldb, T beta, T* C, int ldc,
+                          hipStream_t st) {
+  const int nsm = cdiv(max_m, 64), nsn = cdiv(max_n, 64);
+  const long long nwgl = (long long)nitems * nsm * nsn;
+  if (nwgl <= 0) return 0;
+  if (nwgl > 0x7fffffffLL) return -1;
+  const int nwg = (int)nwgl;
+  dim3 g(nwg);
+#define G_(a, b) \
+  if (opa == a && opb == b) lg1<T, a, b>(g, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc);
+  G_(0, 0) G_(0, 1) G_(0, 2) G_(1, 0) G_(1, 1) G_(1, 2) G_(2, 0) G_(2, 1) G_(2, 2)
+#undef G_
+  return (int)hipGetLastError();
+}
+
+// alpha/beta: host pointers to one scalar of the launch precision (complex = 2 reals)
+// force_generic: route real precisions through the FMA kernel (testing / A-B).
+DPL_API int dpl_gemm_batched(int prec, int transA, int transB, int nitems, const void* items, const void* kpairs,
+                             int max_m, int max_n, const void* alpha, const void* A, int lda, const void* B,
+                             int ldb, const void* beta, void* C, int ldc, int vec_ok, int force_generic,
+                             hipStream_t st) {
+  const int oa = op_code(transA), ob = op_code(transB);
+  const GemmItemK* it = (const GemmItemK*)items;
+  const KPair* kp = (const KPair*)kpairs;
+  switch (prec) {
+    case DPL_D:
+      if (!force_generic)
+        return launch_mfma<double>(oa, ob, nitems, it, kp, max_m, max_n, *(const double*)alpha, (const double*)A,
+                                   lda, (const double*)B, ldb, *(const double*)beta, (double*)C, ldc, vec_ok, st);
+      return launch_generic<double>(oa, ob, nitems, it, kp, max_m, max_n, *(const double*)alpha, (const double*)A,
+                                    lda, (const double*)B, ldb, *(const double*)beta, (double*)C, ldc, st);
+    case DPL_S:
+      if (!force_generic)
+        return launch_mfma<float>(oa, ob, nitems, it, kp, max_m, max_n, *(const float*)alpha, (const float*)A, lda,
+                                  (const float*)B, ldb, *(const float*)beta, (float*)C, ldc, vec_ok, st);
+      return launch_generic<float>(oa, ob, nitems, it, kp, max_m, max_n, *(const float*)alpha, (const float*)A, lda,
+                                   (const float*)B, ldb, *(const float*)beta, (float*)C, ldc, st);
+    case DPL_C:
+      return launch_generic<hipFloatComplex>(oa, ob, nitems, it, kp, max_m, max_n,
+                                             *(const hipFloatComplex*)alpha, (const hipFloatComplex*)A, lda,
+                                             (const hipFloatComplex*)B, ldb, *(const hipFloatComplex*)beta,
+                                             (hipFloatComplex*)C, ldc, st);
+    case DPL_Z:
+      return launch_generic<hipDoubleComplex>(oa, ob, nitems, it, kp, max_m, max_n,
+                                              *(const hipDoubleComplex*)alpha, (const hipDoubleComplex*)A, lda,
+                                              (const hipDoubleComplex*)B, ldb, *(const hipDoubleComplex*)beta,
+                                              (hipDoubleComplex*)C, ldc, st);
+  }
+  return -2;
+}

@@ -1,0 +1,76 @@
+"""Public API: ``op``, ``op_New``, ``op_Destruct`` and precision-prefixed aliases.
+
+Mirrors ``src/include/dplasma/dplasma_z.h:18-353``: e.g. ``dpotrf(ctx, uplo, A)``
+is the blocking call (returns info), ``dpotrf_New`` returns a taskpool that can
+be queued with other taskpools before one ``ctx.wait()``, ``dpotrf_Destruct``
+releases it.  The precision prefix is checked against the descriptor dtype.
+"""
+from __future__ import annotations
+
+import functools
+
+from .constants import DTYPE_PREC
+from .models import aux as _aux
+from .models import check as _check
+from .models import gemm as _gemm
+from .models import potrf as _potrf
+from .models import redistribute as _redis
+
+__all__ = []
+
+# generic (precision-agnostic) entry points
+_GENERIC = {
+    "potrf": _potrf.potrf, "potrf_New": _potrf.potrf_New,
+    "gemm": _gemm.gemm, "gemm_New": _gemm.gemm_New,
+    "plrnt": _aux.plrnt, "plrnt_New": _aux.plrnt_New,
+    "plghe": _aux.plghe, "plghe_New": _aux.plghe_New,
+    "plgsy": _aux.plgsy, "plgsy_New": _aux.plgsy_New,
+    "laset": _aux.laset, "laset_New": _aux.laset_New,
+    "lacpy": _aux.lacpy, "lacpy_New": _aux.lacpy_New,
+    "geadd": _aux.geadd, "geadd_New": _aux.geadd_New,
+    "tradd": _aux.tradd,
+    "lascal": _aux.lascal, "lascal_New": _aux.lascal_New,
+    "lange": _aux.lange, "lansy": _aux.lansy, "lanhe": _aux.lanhe, "lantr": _aux.lantr,
+    "check_potrf": _check.check_potrf, "check_axmb": _check.check_axmb,
+    "redistribute": _redis.redistribute,
+}
+
+
+def _destruct(tp):
+    if tp is not None:
+        tp.destruct()
+
+
+def _register(name, fn):
+    globals()[name] = fn
+    __all__.append(name)
+
+
+def _prec_checked(prec, fn):
+    @functools.wraps(fn)
+    def wrapper(ctx, *args, **kw):
+        for a in args:
+            dt = getattr(a, "dtype", None)
+            if dt is not None and hasattr(a, "mb"):
+                if DTYPE_PREC.get(dt) != prec:
+                    raise TypeError(f"{prec}{fn.__name__}: descriptor {a.name} has precision {DTYPE_PREC.get(dt)}")
+                break
+        return fn(ctx, *args, **kw)
+    return wrapper
+
+
+def register_op(name, fn):
+    """Register a generic op and its s/d/c/z aliases (+ _Destruct for _New ops)."""
+    _register(name, fn)
+    if name.endswith("_New"):
+        base = name[:-4]
+        _register(base + "_Destruct", _destruct)
+    for p in "sdcz":
+        alias = p + name
+        _register(alias, _prec_checked(p, fn))
+        if name.endswith("_New"):
+            _register(p + name[:-4] + "_Destruct", _destruct)
+
+
+for _n, _f in _GENERIC.items():
+    register_op(_n, _f)

@@ -1,0 +1,146 @@
+"""Execution context: the analogue of ``parsec_init``/``parsec_context_t``.
+
+One process per GPU (``torch.distributed`` over RCCL on GPU, gloo on CPU).
+The context owns
+
+* the P x Q process grid (rank = prow*Q + pcol) and the row/column
+  sub-communicators used for panel broadcasts (created once, like PaRSEC's
+  remote-dependency engine communicator ``parsec_remote_dep_set_ctx``,
+  ``src/scalapack_wrappers/dplasma_wrapper_parsec_init.c:112-114``);
+* the device and its HIP streams: a high-priority ``panel`` stream for the
+  critical-path tasks (POTRF/TRSM/panel broadcast), an ``update`` stream for
+  the bulk trailing updates, and an ``aux`` stream;
+* the native task runtime handle (``dplasma_amd.runtime``) and the per-call
+  option registry (``dplasma_info``).
+
+The taskpool lifecycle mirrors the reference: ``X_New`` builds a taskpool
+(nothing runs), ``ctx.add_taskpool(tp)`` enqueues it, ``ctx.start()`` /
+``ctx.wait()`` execute it (``src/dplasmaaux.h:98-102``).
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+def _default_grid(world: int):
+    P = int(math.isqrt(world))
+    while world % P:
+        P -= 1
+    return P, world // P
+
+
+class Context:
+    def __init__(self, nb_cores: Optional[int] = None, device=None, P: Optional[int] = None, Q: Optional[int] = None,
+                 gpus: Optional[int] = None, verbose: int = 0):
+        self.distributed = dist.is_available() and dist.is_initialized()
+        self.rank = dist.get_rank() if self.distributed else 0
+        self.world = dist.get_world_size() if self.distributed else 1
+        self.verbose = verbose
+        if P is None and Q is None:
+            P, Q = _default_grid(self.world)
+        elif P is None:
+            P = self.world // Q
+        elif Q is None:
+            Q = self.world // P
+        if P * Q != self.world:
+            raise ValueError(f"grid {P}x{Q} does not match world size {self.world}")
+        self.P, self.Q = P, Q
+        self.myrow, self.mycol = self.rank // Q, self.rank % Q
+        # device selection: one GPU per rank (LOCAL_RANK), or CPU
+        if device is None:
+            want_gpu = (gpus is None or gpus > 0) and torch.cuda.is_available()
+            if want_gpu:
+                lr = int(os.environ.get("LOCAL_RANK", self.rank % max(1, torch.cuda.device_count())))
+                device = torch.device("cuda", lr)
+            else:
+                device = torch.device("cpu")
+        self.device = torch.device(device)
+        self.is_gpu = self.device.type == "cuda"
+        self.nb_cores = nb_cores or int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        if self.is_gpu:
+            torch.cuda.set_device(self.device)
+            lo, hi = torch.cuda.Stream.priority_range()
+            self.streams = {
+                "panel": torch.cuda.Stream(device=self.device, priority=hi),
+                "update": torch.cuda.Stream(device=self.device, priority=lo),
+                "aux": torch.cuda.Stream(device=self.device, priority=lo),
+            }
+        else:
+            self.streams = {}
+        self._groups_built = False
+        self.row_group = None
+        self.col_group = None
+        self.row_ranks: List[int] = [self.myrow * Q + c for c in range(Q)]
+        self.col_ranks: List[int] = [r * Q + self.mycol for r in range(P)]
+        self._build_groups()
+        self._queue = []
+        self.profiling = None  # utils.trace.Tracer when enabled
+        from .utils.info import Info
+        self.info = Info()
+
+    # ------------------------------------------------------------------ comms
+    def _build_groups(self):
+        if not self.distributed or self.world == 1:
+            return
+        # every rank must create every group, in the same order
+        rows, cols = [], []
+        for r in range(self.P):
+            ranks = [r * self.Q + c for c in range(self.Q)]
+            rows.append(dist.new_group(ranks) if self.Q > 1 else None)
+        for c in range(self.Q):
+            ranks = [r * self.Q + c for r in range(self.P)]
+            cols.append(dist.new_group(ranks) if self.P > 1 else None)
+        self.row_group = rows[self.myrow]
+        self.col_group = cols[self.mycol]
+        self._groups_built = True
+
+    def barrier(self):
+        if self.distributed and self.world > 1:
+            if self.is_gpu:
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+    def sync(self):
+        if self.is_gpu:
+            torch.cuda.synchronize(self.device)
+
+    def stream(self, name: str):
+        return self.streams.get(name)
+
+    # ------------------------------------------------------------------ taskpools
+    def add_taskpool(self, tp):
+        self._queue.append(tp)
+
+    def start(self):
+        for tp in self._queue:
+            tp.run(self)
+
+    def wait(self):
+        for tp in self._queue:
+            tp.complete(self)
+        self._queue = []
+
+    def __repr__(self):
+        return f"Context(rank={self.rank}/{self.world}, grid={self.P}x{self.Q}, device={self.device})"
+
+
+_DEFAULT: Optional[Context] = None
+
+
+def init(nb_cores=None, device=None, P=None, Q=None, gpus=None, verbose=0) -> Context:
+    """Create (or return) the default context -- ``parsec_init`` analogue."""
+    global _DEFAULT
+    _DEFAULT = Context(nb_cores=nb_cores, device=device, P=P, Q=Q, gpus=gpus, verbose=verbose)
+    return _DEFAULT
+
+
+def fini(ctx: Optional[Context] = None):
+    global _DEFAULT
+    if ctx is None or ctx is _DEFAULT:
+        _DEFAULT = None

@@ -1,0 +1,119 @@
+"""Distributed GEMM: C = alpha op(A) op(B) + beta C.
+
+Reference: ``src/zgemm_wrapper.c`` dispatching to the default
+(``zgemm_{NN,NT,TN,TT}.jdf``), SUMMA (``zgemm_*_summa.jdf``: RING_A/RING_B
+rings along process rows/columns with look-ahead CTLs, :91-207) and the
+out-of-GPU-memory variant (``zgemm_NN_gpu.jdf``).
+
+MI355X design:
+* Single rank: the whole product is ONE launch of the batched MFMA GEMM
+  engine -- every local C tile is an item whose k-loop runs over all k tiles
+  inside the kernel (no per-k launches, C read and written exactly once).
+* P x Q ranks (SUMMA): K is cut into chunks of ``kc`` tile columns; for each
+  chunk one planned all-to-all (``parallel.exchange``) delivers the A tiles of
+  my C rows and the B tiles of my C columns (any transpose, any distribution),
+  then one GEMM launch accumulates the chunk.  Chunks are double-buffered: the
+  exchange of chunk s+1 (panel stream) overlaps the GEMM of chunk s (update
+  stream).  With 288 GB of HBM per GPU the default chunk is large (fewer,
+  larger collectives), see ``DPLASMA:GEMM:kc``.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..constants import dplasmaNoTrans
+from ..ops import tile_ops as ops
+from ..ops.batch import MASK_LOWER, MASK_UPPER, GemmBatch
+from ..parallel.exchange import ExchangePlan
+from ..runtime import Taskpool
+from ..utils.flops import flops
+
+
+def _check(transA, transB, A, B, C):
+    am, ak = (A.m, A.n) if transA == dplasmaNoTrans else (A.n, A.m)
+    bk, bn = (B.m, B.n) if transB == dplasmaNoTrans else (B.n, B.m)
+    if am != C.m or bn != C.n or ak != bk:
+        raise ValueError(f"gemm: size mismatch op(A)={am}x{ak} op(B)={bk}x{bn} C={C.m}x{C.n}")
+    return ak
+
+
+def _a_tile(transA, m, k):
+    return (m, k) if transA == dplasmaNoTrans else (k, m)
+
+
+def _b_tile(transB, k, n):
+    return (k, n) if transB == dplasmaNoTrans else (n, k)
+
+
+def gemm_New(ctx, transA, transB, alpha, A, B, beta, C, c_mask=None, kc=None, name="gemm") -> Taskpool:
+    """c_mask(m, n) -> MASK_* restricts the update of C tile (m,n) to a triangle (used by herk/syrk)."""
+    K = _check(transA, transB, A, B, C)
+    tp = Taskpool(name, ctx)
+    tp.flops = flops(C.prec, "gemm", C.m, C.n, K)
+    kt = (K + A.nb - 1) // A.nb if transA == dplasmaNoTrans else (K + A.mb - 1) // A.mb
+    # tile size along k (op(A) columns)
+    def kext(k):
+        return A.tile_cols(k) if transA == dplasmaNoTrans else A.tile_rows(k)
+    ctiles = [(m, n) for (m, n) in C.local_tiles() if c_mask is None or c_mask(m, n) is not None]
+    if kt == 0 or not ctiles:
+        if beta != 1.0 and ctiles:
+            from .aux import lascal_New
+            return lascal_New(ctx, 123, beta, C)
+        return tp.finish_build()
+    if ctx.world == 1:
+        gb = GemmBatch()
+        for (m, n) in ctiles:
+            kp = [(A.offset(*_a_tile(transA, m, k)), B.offset(*_b_tile(transB, k, n)), kext(k)) for k in range(kt)]
+            gb.add(C.offset(m, n), C.tile_rows(m), C.tile_cols(n), kp, c_mask(m, n) if c_mask else 0)
+        gb.finalize()
+        tp.task("GEMM", "update", lambda: ops.gemm(transA, transB, alpha, A.data, A.ld, B.data, B.ld, beta, C.data,
+                                                     C.ld, gb))
+        return tp.finish_build()
+    # ---------------- SUMMA over k chunks
+    if kc is None:
+        kc = ctx.info.get_int("DPLASMA:GEMM:kc", 0) or max(1, min(kt, 8))
+    nchunks = (kt + kc - 1) // kc
+    mats = [A, B]
+    bufs = []
+    prev_gemm = {}
+    for s in range(nchunks):
+        ks = list(range(s * kc, min(kt, (s + 1) * kc)))
+        needs = {}
+        for r in range(ctx.world):
+            pr, pc = r // C.Q, r % C.Q
+            rows = [m for m in range(C.mt) if C.grid.prow(m + C.it0) == pr]
+            cols = [n for n in range(C.nt) if C.grid.pcol(n + C.jt0) == pc]
+            lst = []
+            for m in rows:
+                for k in ks:
+                    lst.append((0,) + _a_tile(transA, m, k))
+            for n in cols:
+                for k in ks:
+                    lst.append((1,) + _b_tile(transB, k, n))
+            needs[r] = lst
+        plan = ExchangePlan(ctx, mats, needs, C.dtype, C.device)
+        if len(bufs) < 2:
+            bufs.append(plan.new_recv_buffer())
+        buf = bufs[s % 2]
+        if buf.numel() < max(plan.nrecv, 1) * plan.nbe:
+            buf = plan.new_recv_buffer()
+            bufs[s % 2] = buf
+        gb = GemmBatch()
+        for (m, n) in ctiles:
+            kp = [(plan.offset(0, *_a_tile(transA, m, k)), plan.offset(1, *_b_tile(transB, k, n)), kext(k))
+                  for k in ks]
+            gb.add(C.offset(m, n), C.tile_rows(m), C.tile_cols(n), kp, c_mask(m, n) if c_mask else 0)
+        gb.finalize()
+        t_ex = tp.task(f"EXCH({s})", "panel", lambda plan=plan, buf=buf: plan.run(buf), [prev_gemm.get(s - 2)],
+                       prio=2)
+        b_eff = beta if s == 0 else 1.0
+        prev_gemm[s] = tp.task(
+            f"GEMM({s})", "update",
+            lambda gb=gb, buf=buf, b_eff=b_eff, plan=plan: ops.gemm(transA, transB, alpha, buf, plan.ld, buf, plan.ld, b_eff,
+                                                          C.data, C.ld, gb), [t_ex], prio=1)
+    tp._buffers = bufs
+    return tp.finish_build()
+
+
+def gemm(ctx, transA, transB, alpha, A, B, beta, C, **kw):
+    return gemm_New(ctx, transA, transB, alpha, A, B, beta, C, **kw).execute(ctx)

@@ -1,0 +1,120 @@
+"""ctypes binding of the in-tree HIP kernel library ``lib/libdplasma_kernels.so``.
+
+The library is built by ``tools/build.py`` (``hipcc --offload-arch=gfx950``).
+On a GPU box the native path is mandatory: if a CUDA/HIP tensor reaches a
+kernel wrapper and the library cannot be loaded we raise instead of silently
+falling back to PyTorch/rocBLAS (no vendor-BLAS fallback, BASELINE.json).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+
+import torch
+
+from ..constants import DTYPE_CODE
+
+_LIBDIR = Path(__file__).resolve().parents[1] / "lib"
+_LIB = None
+_LOCK = threading.Lock()
+
+c_int, c_ll, c_ull, c_vp = ctypes.c_int, ctypes.c_longlong, ctypes.c_ulonglong, ctypes.c_void_p
+
+_SIGS = {
+    # prec, transA, transB, nitems, items, kpairs, max_m, max_n, alpha*, A, lda, B, ldb, beta*, C, ldc, vec_ok, generic, stream
+    "dpl_gemm_batched": [c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_int, c_vp,
+                         c_vp, c_int, c_int, c_int, c_vp],
+    # prec, uplo, n, A, a_off, lda, info*, info_base, stream
+    "dpl_potrf_tile": [c_int, c_int, c_int, c_vp, c_ll, c_int, c_vp, c_int, c_vp],
+    # prec, side, uplo, trans, diag, nitems, items, max_m, max_n, alpha*, A, lda, B, ldb, stream
+    "dpl_trsm_batched": [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_int,
+                         c_vp],
+    # prec, kind, nitems, items, mmax, nmax, A, lda, gM, seed, bump*, stream
+    "dpl_generate": [c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_int, c_ll, c_ull, c_vp, c_vp],
+    # prec, part, nitems, items, mmax, nmax, alpha*, beta*, A, lda, stream
+    "dpl_laset": [c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp],
+    # prec, part, trans, nitems, items, mmax, nmax, alpha*, A, lda, beta*, B, ldb, copy, stream
+    "dpl_geadd": [c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp],
+    # prec, part, nitems, items, mmax, nmax, alpha*, A, lda, stream
+    "dpl_lascal": [c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp],
+    # prec, kind, part, unit, nitems, items, A, lda, out, ostride, stream
+    "dpl_tile_norm": [c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_int, c_vp],
+}
+_OPTIONAL = set()
+
+
+def lib_path() -> Path:
+    return _LIBDIR / "libdplasma_kernels.so"
+
+
+def load(build_if_missing: bool = True):
+    """Load (building first if needed) the kernel library; returns the CDLL."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        p = lib_path()
+        if not p.exists() and build_if_missing and os.environ.get("DPLASMA_NO_BUILD") != "1":
+            import importlib.util
+            spec = importlib.util.spec_from_file_location("dplasma_build", _LIBDIR.parents[1] / "tools" / "build.py")
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            mod.build_kernels()
+        lib = ctypes.CDLL(str(p))
+        for name, args in _SIGS.items():
+            try:
+                f = getattr(lib, name)
+            except AttributeError:
+                if name in _OPTIONAL:
+                    continue
+                raise
+            f.argtypes = args
+            f.restype = c_int
+        _LIB = lib
+        return lib
+
+
+def available() -> bool:
+    try:
+        load()
+        return True
+    except Exception:
+        return False
+
+
+def stream_ptr(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+class Scalar:
+    """Host-side scalar of a given dtype, passed by pointer (complex = 2 reals)."""
+
+    __slots__ = ("buf",)
+
+    def __init__(self, value, dtype: torch.dtype):
+        if dtype in (torch.complex64, torch.complex128):
+            v = complex(value)
+            t = ctypes.c_float if dtype == torch.complex64 else ctypes.c_double
+            self.buf = (t * 2)(v.real, v.imag)
+        elif dtype == torch.float32:
+            self.buf = ctypes.c_float(float(value.real if isinstance(value, complex) else value))
+        else:
+            self.buf = ctypes.c_double(float(value.real if isinstance(value, complex) else value))
+
+    @property
+    def ptr(self):
+        return ctypes.cast(ctypes.pointer(self.buf), c_vp)
+
+
+def prec_code(dtype: torch.dtype) -> int:
+    return DTYPE_CODE[dtype]
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"dplasma_amd kernel {what} failed with code {rc}")

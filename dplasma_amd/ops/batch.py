@@ -1,0 +1,110 @@
+"""Item batches: the unit of work handed to one batched kernel launch.
+
+A batch is built once (host numpy records, ``ENQ`` phase) and uploaded once
+per device; executing it is a single kernel launch on GPU, or a loop of
+PyTorch tile operations on the CPU reference path.  The record layouts match
+``csrc/kernels/common.h`` / ``gemm.hip`` exactly.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+GEMM_ITEM = np.dtype([("c_off", "<i8"), ("kt_beg", "<i4"), ("kt_cnt", "<i4"), ("m", "<i4"), ("n", "<i4"),
+                      ("flags", "<i4"), ("pad", "<i4")])
+KPAIR = np.dtype([("a_off", "<i8"), ("b_off", "<i8"), ("k", "<i4"), ("pad", "<i4")])
+TILE_ITEM = np.dtype([("a_off", "<i8"), ("b_off", "<i8"), ("m", "<i4"), ("n", "<i4"), ("gi", "<i4"), ("gj", "<i4")])
+assert GEMM_ITEM.itemsize == 32 and KPAIR.itemsize == 24 and TILE_ITEM.itemsize == 32
+
+MASK_FULL, MASK_LOWER, MASK_UPPER = 0, 1, 2
+
+
+class _Uploadable:
+    def __init__(self):
+        self._dev = {}
+
+    def _upload(self, arr: np.ndarray, device: torch.device) -> torch.Tensor:
+        key = (id(arr), str(device))
+        t = self._dev.get(key)
+        if t is None:
+            host = torch.from_numpy(arr.view(np.uint8).copy())
+            if device.type == "cuda":
+                host = host.pin_memory()
+                t = host.to(device, non_blocking=True)
+            else:
+                t = host
+            self._dev[key] = t
+        return t
+
+
+class GemmBatch(_Uploadable):
+    """C_i = beta*C_i + alpha * sum_j opA(A_ij) opB(B_ij) over a list of C tiles."""
+
+    def __init__(self):
+        super().__init__()
+        self._items = []
+        self._kps = []
+        self.items = None
+        self.kpairs = None
+        self.max_m = self.max_n = 0
+        self.vec_ok = True
+        self.flops_mnk = 0.0
+
+    def add(self, c_off: int, m: int, n: int, kpairs, mask: int = MASK_FULL):
+        """kpairs: iterable of (a_off, b_off, k)."""
+        kp = list(kpairs)
+        beg = len(self._kps)
+        for (a, b, k) in kp:
+            self._kps.append((a, b, k, 0))
+            if a % 2 or b % 2:
+                self.vec_ok = False
+            self.flops_mnk += float(m) * n * k
+        self._items.append((c_off, beg, len(kp), m, n, mask, 0))
+        if c_off % 2:
+            self.vec_ok = False
+        self.max_m = max(self.max_m, m)
+        self.max_n = max(self.max_n, n)
+        return self
+
+    def __len__(self):
+        return len(self._items) if self.items is None else len(self.items)
+
+    def finalize(self):
+        if self.items is None:
+            self.items = np.array(self._items, dtype=GEMM_ITEM)
+            self.kpairs = np.array(self._kps if self._kps else [(0, 0, 0, 0)], dtype=KPAIR)
+            self._items = self._kps = None
+        return self
+
+    def device_arrays(self, device):
+        self.finalize()
+        return self._upload(self.items, device), self._upload(self.kpairs, device)
+
+
+class TileBatch(_Uploadable):
+    """List of tiles (a_off, b_off, m, n, global row, global col) for map/trsm/norm launches."""
+
+    def __init__(self):
+        super().__init__()
+        self._items = []
+        self.items = None
+        self.max_m = self.max_n = 0
+
+    def add(self, a_off: int, m: int, n: int, gi: int = 0, gj: int = 0, b_off: int = 0):
+        self._items.append((a_off, b_off, m, n, gi, gj))
+        self.max_m = max(self.max_m, m)
+        self.max_n = max(self.max_n, n)
+        return self
+
+    def __len__(self):
+        return len(self._items) if self.items is None else len(self.items)
+
+    def finalize(self):
+        if self.items is None:
+            self.items = np.array(self._items if self._items else [], dtype=TILE_ITEM)
+            self._items = None
+        return self
+
+    def device_array(self, device):
+        self.finalize()
+        return self._upload(self.items, device)

@@ -1,0 +1,291 @@
+"""Batched tile operations: one entry point per CORE kernel family.
+
+Each function takes base tensors (a descriptor's local storage or a panel
+buffer), leading dimensions and an item batch, and runs either
+
+* the native HIP/CDNA4 kernel (``lib/libdplasma_kernels.so``) on the current
+  torch stream when the data lives on a GPU -- a single launch per batch; or
+* the CPU reference path (PyTorch CPU ops on tile views -- the analogue of the
+  reference's ``CORE_z*`` CBLAS/LAPACKE wrappers, ``src/cores/core_zgemm.c:90``,
+  ``core_zpotrf.c:68`` ...) when the data lives in host memory.
+
+GPU tensors never fall back to PyTorch/rocBLAS: a missing or failing kernel
+raises.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..constants import (dplasmaConjTrans, dplasmaLeft, dplasmaLower, dplasmaNoTrans, dplasmaTrans, dplasmaUnit,
+                         dplasmaUpper)
+from ..utils import lcg
+from . import _lib
+from .batch import MASK_LOWER, MASK_UPPER, GemmBatch, TileBatch
+
+FORCE_GENERIC_GEMM = False  # testing knob: route real GEMMs through the FMA kernel
+
+
+def _view(base: torch.Tensor, off: int, rows: int, cols: int, ld: int) -> torch.Tensor:
+    return torch.as_strided(base, (rows, cols), (1, ld), int(off))
+
+
+def _op(x: torch.Tensor, trans: int) -> torch.Tensor:
+    if trans == dplasmaNoTrans:
+        return x
+    if trans == dplasmaTrans:
+        return x.transpose(0, 1)
+    return x.conj().transpose(0, 1)
+
+
+def _is_gpu(t: torch.Tensor) -> bool:
+    return t.device.type == "cuda"
+
+
+# ----------------------------------------------------------------------------- GEMM
+def gemm(transA: int, transB: int, alpha, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, beta,
+         C: torch.Tensor, ldc: int, batch: GemmBatch):
+    """For every item: C = beta*C + alpha * sum_k opA(A_k) opB(B_k) (masked to a triangle if asked)."""
+    batch.finalize()
+    if len(batch) == 0:
+        return
+    if _is_gpu(C):
+        lib = _lib.load()
+        items, kps = batch.device_arrays(C.device)
+        vec_ok = int(batch.vec_ok and lda % 2 == 0 and ldb % 2 == 0 and A.data_ptr() % 16 == 0
+                     and B.data_ptr() % 16 == 0)
+        rc = lib.dpl_gemm_batched(_lib.prec_code(C.dtype), transA, transB, len(batch.items), items.data_ptr(),
+                                  kps.data_ptr(), batch.max_m, batch.max_n, _lib.Scalar(alpha, C.dtype).ptr,
+                                  A.data_ptr(), lda, B.data_ptr(), ldb, _lib.Scalar(beta, C.dtype).ptr,
+                                  C.data_ptr(), ldc, vec_ok, int(FORCE_GENERIC_GEMM), _lib.stream_ptr())
+        _lib.check(rc, "gemm_batched")
+        return
+    for it in batch.items:
+        m, n = int(it["m"]), int(it["n"])
+        c = _view(C, it["c_off"], m, n, ldc)
+        acc = None
+        for kp in batch.kpairs[it["kt_beg"]:it["kt_beg"] + it["kt_cnt"]]:
+            k = int(kp["k"])
+            a = _view(A, kp["a_off"], m, k, lda) if transA == dplasmaNoTrans else _op(_view(A, kp["a_off"], k, m, lda), transA)
+            b = _view(B, kp["b_off"], k, n, ldb) if transB == dplasmaNoTrans else _op(_view(B, kp["b_off"], n, k, ldb), transB)
+            p = a @ b
+            acc = p if acc is None else acc + p
+        new = c * beta if beta != 0 else torch.zeros_like(c)
+        if acc is not None:
+            new = new + alpha * acc
+        mask = int(it["flags"]) & 3
+        if mask == MASK_LOWER:
+            new = torch.where(torch.ones(m, n, dtype=torch.bool).tril(), new, c)
+        elif mask == MASK_UPPER:
+            new = torch.where(torch.ones(m, n, dtype=torch.bool).triu(), new, c)
+        c.copy_(new)
+
+
+# ----------------------------------------------------------------------------- POTRF
+def potrf_tile(uplo: int, A: torch.Tensor, off: int, n: int, lda: int, info: torch.Tensor, info_base: int):
+    """Cholesky of one diagonal tile in place; ``info`` (int32 tensor, 1 elem) gets base + first bad col."""
+    if n <= 0:
+        return
+    if _is_gpu(A):
+        lib = _lib.load()
+        rc = lib.dpl_potrf_tile(_lib.prec_code(A.dtype), uplo, n, A.data_ptr(), int(off), lda, info.data_ptr(),
+                                int(info_base), _lib.stream_ptr())
+        _lib.check(rc, "potrf_tile")
+        return
+    t = _view(A, off, n, n, lda)
+    upper = uplo == dplasmaUpper
+    src = t.triu() if upper else t.tril()
+    herm = src + _op(src, dplasmaConjTrans) - torch.diag_embed(torch.diagonal(src))
+    if herm.is_complex():
+        herm = herm - 1j * torch.diag_embed(torch.diagonal(herm).imag)
+    L, inf = torch.linalg.cholesky_ex(herm, upper=upper)
+    bad = int(inf)
+    if bad > 0:
+        if int(info[0]) == 0:
+            info[0] = info_base + bad
+        # mimic LAPACK: factor up to the failing column, keep what we have
+    keep = torch.ones(n, n, dtype=torch.bool).triu() if upper else torch.ones(n, n, dtype=torch.bool).tril()
+    t.copy_(torch.where(keep, L, t))
+
+
+# ----------------------------------------------------------------------------- TRSM
+def trsm(side: int, uplo: int, trans: int, diag: int, alpha, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int,
+         batch: TileBatch):
+    """For every item: solve op(T) X = alpha B (left) or X op(T) = alpha B (right) in place in B.
+
+    item.a_off -> triangular tile in ``A``; item.b_off -> B tile; item m, n = B extent.
+    """
+    batch.finalize()
+    if len(batch) == 0:
+        return
+    if _is_gpu(B):
+        lib = _lib.load()
+        items = batch.device_array(B.device)
+        rc = lib.dpl_trsm_batched(_lib.prec_code(B.dtype), side, uplo, trans, diag, len(batch.items),
+                                  items.data_ptr(), batch.max_m, batch.max_n, _lib.Scalar(alpha, B.dtype).ptr,
+                                  A.data_ptr(), lda, B.data_ptr(), ldb, _lib.stream_ptr())
+        _lib.check(rc, "trsm_batched")
+        return
+    left = side == dplasmaLeft
+    for it in batch.items:
+        m, n = int(it["m"]), int(it["n"])
+        k = m if left else n
+        t = _view(A, it["a_off"], k, k, lda)
+        t = t.tril() if uplo == dplasmaLower else t.triu()
+        if diag == dplasmaUnit:
+            t = t - torch.diag_embed(torch.diagonal(t)) + torch.eye(k, dtype=t.dtype)
+        opt = _op(t, trans)
+        upper = (uplo == dplasmaUpper) != (trans != dplasmaNoTrans)
+        b = _view(B, it["b_off"], m, n, ldb)
+        x = torch.linalg.solve_triangular(opt, alpha * b, upper=upper, left=left)
+        b.copy_(x)
+
+
+# ----------------------------------------------------------------------------- generators
+GEN_KIND = {"rnt": 0, "ghe": 1, "gsy": 2}
+
+
+def generate(kind: str, A: torch.Tensor, lda: int, batch: TileBatch, gM: int, seed: int, bump=0.0):
+    """Fill tiles with plrnt / plghe / plgsy values (bit-identical CPU/GPU)."""
+    batch.finalize()
+    if len(batch) == 0:
+        return
+    if _is_gpu(A):
+        lib = _lib.load()
+        items = batch.device_array(A.device)
+        rc = lib.dpl_generate(_lib.prec_code(A.dtype), GEN_KIND[kind], len(batch.items), items.data_ptr(),
+                              batch.max_m, batch.max_n, A.data_ptr(), lda, int(gM), int(seed) & (2**64 - 1),
+                              _lib.Scalar(bump, A.dtype).ptr, _lib.stream_ptr())
+        _lib.check(rc, "generate")
+        return
+    cplx = A.is_complex()
+    for it in batch.items:
+        m, n = int(it["m"]), int(it["n"])
+        blk = lcg.generate_block(kind, int(it["gi"]), int(it["gj"]), m, n, gM, seed, cplx, bump)
+        _view(A, it["a_off"], m, n, lda).copy_(torch.from_numpy(np.ascontiguousarray(blk)).to(A.dtype))
+
+
+# ----------------------------------------------------------------------------- maps
+# element selections (global coordinates); the kernels take the same codes
+PART_FULL, PART_LOWER, PART_UPPER, PART_SLOWER, PART_SUPPER, PART_DIAG = 0, 1, 2, 3, 4, 5
+_PART = {0: 0, 1: 1, 2: 2, 3: 3, 4: 4, 5: 5, dplasmaLower: 1, dplasmaUpper: 2, 123: 0}
+
+
+def _part_mask(it, m, n, part):
+    I = torch.arange(m).view(-1, 1) + int(it["gi"])
+    J = torch.arange(n).view(1, -1) + int(it["gj"])
+    if part == 1:
+        return I >= J
+    if part == 2:
+        return I <= J
+    if part == 3:
+        return I > J
+    if part == 4:
+        return I < J
+    if part == 5:
+        return I == J
+    return torch.ones(m, n, dtype=torch.bool)
+
+
+def laset(uplo: int, alpha, beta, A: torch.Tensor, lda: int, batch: TileBatch):
+    """Off-diagonal (global) entries := alpha, diagonal := beta, on the uplo part."""
+    batch.finalize()
+    if len(batch) == 0:
+        return
+    part = _PART.get(uplo, 0)
+    if _is_gpu(A):
+        rc = _lib.load().dpl_laset(_lib.prec_code(A.dtype), part, len(batch.items), batch.device_array(A.device).data_ptr(),
+                                   batch.max_m, batch.max_n, _lib.Scalar(alpha, A.dtype).ptr,
+                                   _lib.Scalar(beta, A.dtype).ptr, A.data_ptr(), lda, _lib.stream_ptr())
+        _lib.check(rc, "laset")
+        return
+    for it in batch.items:
+        m, n = int(it["m"]), int(it["n"])
+        v = _view(A, it["a_off"], m, n, lda)
+        I = torch.arange(m).view(-1, 1) + int(it["gi"])
+        J = torch.arange(n).view(1, -1) + int(it["gj"])
+        val = torch.where(I == J, torch.tensor(beta, dtype=A.dtype), torch.tensor(alpha, dtype=A.dtype))
+        v.copy_(torch.where(_part_mask(it, m, n, part), val, v))
+
+
+def geadd(uplo: int, trans: int, alpha, A: torch.Tensor, lda: int, beta, B: torch.Tensor, ldb: int,
+          batch: TileBatch, copy: bool = False):
+    """B = alpha*op(A) + beta*B (or B = op(A) when copy) on the uplo part; item a_off/b_off per tile."""
+    batch.finalize()
+    if len(batch) == 0:
+        return
+    part = _PART.get(uplo, 0)
+    if _is_gpu(B):
+        rc = _lib.load().dpl_geadd(_lib.prec_code(B.dtype), part, trans, len(batch.items),
+                                   batch.device_array(B.device).data_ptr(), batch.max_m, batch.max_n,
+                                   _lib.Scalar(alpha, B.dtype).ptr, A.data_ptr(), lda, _lib.Scalar(beta, B.dtype).ptr,
+                                   B.data_ptr(), ldb, int(copy), _lib.stream_ptr())
+        _lib.check(rc, "geadd")
+        return
+    for it in batch.items:
+        m, n = int(it["m"]), int(it["n"])
+        a = _view(A, it["a_off"], m, n, lda) if trans == dplasmaNoTrans else _op(_view(A, it["a_off"], n, m, lda), trans)
+        b = _view(B, it["b_off"], m, n, ldb)
+        new = a.clone() if copy else (alpha * a + (beta * b if beta != 0 else 0))
+        b.copy_(torch.where(_part_mask(it, m, n, part), new, b))
+
+
+def lascal(uplo: int, alpha, A: torch.Tensor, lda: int, batch: TileBatch):
+    batch.finalize()
+    if len(batch) == 0:
+        return
+    part = _PART.get(uplo, 0)
+    if _is_gpu(A):
+        rc = _lib.load().dpl_lascal(_lib.prec_code(A.dtype), part, len(batch.items),
+                                    batch.device_array(A.device).data_ptr(), batch.max_m, batch.max_n,
+                                    _lib.Scalar(alpha, A.dtype).ptr, A.data_ptr(), lda, _lib.stream_ptr())
+        _lib.check(rc, "lascal")
+        return
+    for it in batch.items:
+        m, n = int(it["m"]), int(it["n"])
+        a = _view(A, it["a_off"], m, n, lda)
+        a.copy_(torch.where(_part_mask(it, m, n, part), alpha * a, a))
+
+
+# ----------------------------------------------------------------------------- norms
+NORM_MAX, NORM_COLSUM, NORM_ROWSUM, NORM_SSQ = 0, 1, 2, 3
+
+
+def tile_norm(kind: int, uplo: int, unit: bool, A: torch.Tensor, lda: int, batch: TileBatch) -> torch.Tensor:
+    """Per-tile norm partials (float64, on A's device).
+
+    MAX -> (ntiles,); COLSUM -> (ntiles, max_n); ROWSUM -> (ntiles, max_m); SSQ -> (ntiles, 2) (scale, ssq).
+    """
+    batch.finalize()
+    nt = len(batch)
+    ostride = {NORM_MAX: 1, NORM_COLSUM: max(batch.max_n, 1), NORM_ROWSUM: max(batch.max_m, 1), NORM_SSQ: 2}[kind]
+    out = torch.zeros(nt, ostride, dtype=torch.float64, device=A.device)
+    if nt == 0:
+        return out
+    part = _PART.get(uplo, 0)
+    if _is_gpu(A):
+        rc = _lib.load().dpl_tile_norm(_lib.prec_code(A.dtype), kind, part, int(unit), nt,
+                                       batch.device_array(A.device).data_ptr(), A.data_ptr(), lda, out.data_ptr(),
+                                       ostride, _lib.stream_ptr())
+        _lib.check(rc, "tile_norm")
+        return out
+    for i, it in enumerate(batch.items):
+        m, n = int(it["m"]), int(it["n"])
+        a = _view(A, it["a_off"], m, n, lda).abs().to(torch.float64)
+        mk = _part_mask(it, m, n, part)
+        a = torch.where(mk, a, torch.zeros((), dtype=torch.float64))
+        if unit:
+            I = torch.arange(m).view(-1, 1) + int(it["gi"])
+            J = torch.arange(n).view(1, -1) + int(it["gj"])
+            a = torch.where((I == J) & mk, torch.ones((), dtype=torch.float64), a)
+        if kind == NORM_MAX:
+            out[i, 0] = a.max() if a.numel() else 0
+        elif kind == NORM_COLSUM:
+            out[i, :n] = a.sum(0)
+        elif kind == NORM_ROWSUM:
+            out[i, :m] = a.sum(1)
+        else:
+            mx = a.max() if a.numel() else torch.tensor(0.0, dtype=torch.float64)
+            out[i, 0] = mx
+            out[i, 1] = ((a / mx) ** 2).sum() if mx > 0 else 0.0
+    return out

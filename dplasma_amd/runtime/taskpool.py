@@ -1,0 +1,134 @@
+"""Taskpools: the executable form of an algorithm (``X_New`` result).
+
+An algorithm is compiled at ``_New`` time into a list of *tasks*; each task
+is a coarse unit (one batched kernel launch, one panel kernel, one
+collective) bound to a stream class (``panel``/``update``/``aux``) with
+explicit dependencies on earlier tasks.  Execution enqueues every task in
+program order on its stream, inserting HIP event waits only for
+cross-stream edges, so the whole factorisation is queued asynchronously and
+the GPU runs ahead of the host (the HIP-native replacement for PaRSEC's
+ready-queue dispatch).  The dependency bookkeeping, event
+management and optional tracing are done by the native engine
+(``dplasma_amd.runtime.engine``) when available, by the pure-Python loop
+below otherwise; on CPU tasks simply run in order.
+
+Timing protocol (reference ``tests/common.h:252-277``): building the
+taskpool is ENQ, ``run`` + ``complete`` is PROG, ``destruct`` is DEST.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional, Sequence
+
+import torch
+
+
+@dataclass
+class Task:
+    tid: int
+    name: str
+    stream: str
+    fn: Callable[[], None]
+    deps: List[int] = field(default_factory=list)
+    prio: int = 0
+    needs_event: bool = False
+
+
+class Taskpool:
+    def __init__(self, name: str, ctx=None):
+        self.name = name
+        self.ctx = ctx
+        self.tasks: List[Task] = []
+        self.flops = 0.0
+        self._on_complete: List[Callable] = []
+        self._result = None
+        self.t_enq = time.perf_counter()
+        self.t_prog = None
+        self.trace = None
+        self.native = None  # compiled native program (runtime.engine)
+
+    # ------------------------------------------------------------------ build
+    def task(self, name: str, stream: str, fn: Callable[[], None], deps: Sequence[Optional[int]] = (),
+             prio: int = 0) -> int:
+        tid = len(self.tasks)
+        dd = [d for d in deps if d is not None]
+        for d in dd:
+            if d >= tid:
+                raise ValueError("dependencies must point to earlier tasks")
+            if self.tasks[d].stream != stream:
+                self.tasks[d].needs_event = True
+        self.tasks.append(Task(tid, name, stream, fn, dd, prio))
+        return tid
+
+    def on_complete(self, fn: Callable):
+        self._on_complete.append(fn)
+
+    def finish_build(self):
+        self.t_enq = time.perf_counter() - self.t_enq
+        return self
+
+    # ------------------------------------------------------------------ execute
+    def run(self, ctx=None):
+        ctx = ctx or self.ctx
+        t0 = time.perf_counter()
+        if ctx is not None and ctx.is_gpu:
+            from . import engine
+            if engine.available():
+                engine.run_gpu(self, ctx)
+            else:
+                self._run_gpu_py(ctx)
+        else:
+            for t in self.tasks:
+                t.fn()
+        self._t_run = t0
+
+    def _run_gpu_py(self, ctx):
+        cur = torch.cuda.current_stream(ctx.device)
+        start = torch.cuda.Event()
+        start.record(cur)
+        used = {t.stream for t in self.tasks}
+        for s in used:
+            ctx.streams[s].wait_event(start)
+        events = {}
+        for t in self.tasks:
+            s = ctx.streams[t.stream]
+            for d in t.deps:
+                if self.tasks[d].stream != t.stream:
+                    s.wait_event(events[d])
+            with torch.cuda.stream(s):
+                t.fn()
+            if t.needs_event:
+                ev = torch.cuda.Event()
+                ev.record(s)
+                events[t.tid] = ev
+        for s in used:
+            ev = torch.cuda.Event()
+            ev.record(ctx.streams[s])
+            cur.wait_event(ev)
+
+    def complete(self, ctx=None):
+        ctx = ctx or self.ctx
+        if ctx is not None and ctx.is_gpu:
+            torch.cuda.current_stream(ctx.device).synchronize()
+        res = None
+        for fn in self._on_complete:
+            r = fn()
+            if r is not None:
+                res = r
+        self._result = res
+        self.t_prog = time.perf_counter() - getattr(self, "_t_run", time.perf_counter())
+        return res
+
+    def execute(self, ctx=None):
+        """Blocking run (add + start + wait)."""
+        self.run(ctx)
+        return self.complete(ctx)
+
+    @property
+    def result(self):
+        return self._result
+
+    def destruct(self):
+        self.tasks = []
+        self._on_complete = []

@@ -1,0 +1,181 @@
+"""GPU numerics: every HIP kernel vs the CPU/PyTorch fp64 reference of the same op."""
+import pytest
+import torch
+
+import dplasma_amd as dp
+from dplasma_amd.ops import _lib
+from dplasma_amd.ops import tile_ops as ops
+from dplasma_amd.ops.batch import TileBatch
+from helpers import DTYPES, rel_err, tol
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gctx():
+    _lib.load()
+    return dp.init(device="cuda:0")
+
+
+@pytest.fixture(scope="module")
+def cctx():
+    return dp.Context(device="cpu")
+
+
+def test_native_library_loaded(gctx):
+    maps = open("/proc/self/maps").read()
+    assert "libdplasma_kernels.so" in maps
+
+
+def _pair(gctx, cctx, dt, mb, nb, m, n, storage=dp.STORAGE_TILE):
+    G = dp.block_cyclic(gctx, dt, mb, nb, m, n, storage=storage)
+    C = dp.block_cyclic(cctx, dt, mb, nb, m, n, storage=storage)
+    return G, C
+
+
+@pytest.mark.parametrize("prec", list("sdcz"))
+@pytest.mark.parametrize("kind", ["rnt", "ghe", "gsy"])
+def test_generators_bit_identical(gctx, cctx, prec, kind):
+    dt = DTYPES[prec]
+    G, C = _pair(gctx, cctx, dt, 37, 37, 150, 150)
+    for ctx, X in ((gctx, G), (cctx, C)):
+        if kind == "rnt":
+            dp.plrnt(ctx, X, 3872)
+        elif kind == "ghe":
+            dp.plghe(ctx, 150.0, dp.dplasmaUpperLower, X, 3872)
+        else:
+            dp.plgsy(ctx, 150.0, dp.dplasmaUpperLower, X, 3872)
+    torch.cuda.synchronize()
+    assert torch.equal(G.to_dense_local(), C.to_dense_local())
+
+
+@pytest.mark.parametrize("prec", list("sdcz"))
+@pytest.mark.parametrize("ta,tb", [(111, 111), (111, 112), (112, 111), (112, 112), (113, 111), (111, 113)])
+@pytest.mark.parametrize("dims", [(300, 280, 256, 128), (106, 283, 97, 56), (512, 512, 512, 512)])
+def test_gemm(gctx, cctx, prec, ta, tb, dims):
+    if prec in "sd" and (ta == 113 or tb == 113):
+        pytest.skip("conj == trans for real")
+    dt = DTYPES[prec]
+    M, N, K, NB = dims
+    am, an = (M, K) if ta == 111 else (K, M)
+    bm, bn = (K, N) if tb == 111 else (N, K)
+    res = []
+    for ctx in (gctx, cctx):
+        A = dp.block_cyclic(ctx, dt, NB, NB, am, an)
+        B = dp.block_cyclic(ctx, dt, NB, NB, bm, bn)
+        C = dp.block_cyclic(ctx, dt, NB, NB, M, N)
+        dp.plrnt(ctx, A, 3872)
+        dp.plrnt(ctx, B, 4674)
+        dp.plrnt(ctx, C, 2873)
+        dp.gemm(ctx, ta, tb, 0.51, A, B, -0.42, C)
+        res.append(C.to_dense_local())
+    assert rel_err(res[0], res[1]) < tol(dt)
+
+
+def test_gemm_generic_path_matches_mfma(gctx):
+    M = 384
+    outs = []
+    for gen in (False, True):
+        ops.FORCE_GENERIC_GEMM = gen
+        A = dp.block_cyclic(gctx, torch.float64, 128, 128, M, M)
+        B = dp.block_cyclic(gctx, torch.float64, 128, 128, M, M)
+        C = dp.block_cyclic(gctx, torch.float64, 128, 128, M, M)
+        dp.plrnt(gctx, A, 1)
+        dp.plrnt(gctx, B, 2)
+        dp.gemm(gctx, 111, 112, 1.0, A, B, 0.0, C)
+        outs.append(C.to_dense_local())
+    ops.FORCE_GENERIC_GEMM = False
+    assert rel_err(outs[0], outs[1]) < 1e-13
+
+
+def test_mfma_layout_identity(gctx):
+    """A = I with an asymmetric B catches transposed accumulator layouts."""
+    n = 256
+    A = dp.block_cyclic(gctx, torch.float64, n, n, n, n)
+    B = dp.block_cyclic(gctx, torch.float64, n, n, n, n)
+    C = dp.block_cyclic(gctx, torch.float64, n, n, n, n)
+    A.from_dense(torch.eye(n, dtype=torch.float64))
+    b = torch.arange(n * n, dtype=torch.float64).view(n, n) * 0.001 + torch.arange(n).view(n, 1) * 7.0
+    B.from_dense(b)
+    dp.gemm(gctx, 111, 111, 1.0, A, B, 0.0, C)
+    assert torch.equal(C.to_dense_local(), b)
+
+
+@pytest.mark.parametrize("prec", list("sdcz"))
+@pytest.mark.parametrize("side", [dp.dplasmaLeft, dp.dplasmaRight])
+@pytest.mark.parametrize("uplo", [dp.dplasmaLower, dp.dplasmaUpper])
+@pytest.mark.parametrize("trans", [dp.dplasmaNoTrans, dp.dplasmaTrans, dp.dplasmaConjTrans])
+@pytest.mark.parametrize("diag", [dp.dplasmaNonUnit, dp.dplasmaUnit])
+def test_trsm_tile(gctx, cctx, prec, side, uplo, trans, diag):
+    dt = DTYPES[prec]
+    m, n = 150, 93
+    k = m if side == dp.dplasmaLeft else n
+    outs = []
+    for ctx in (gctx, cctx):
+        T = dp.block_cyclic(ctx, dt, k, k, k, k)
+        dp.plghe(ctx, float(k), dp.dplasmaUpperLower, T, 11)  # well conditioned
+        B = dp.block_cyclic(ctx, dt, m, n, m, n)
+        dp.plrnt(ctx, B, 12)
+        tb = TileBatch().add(0, m, n, b_off=0)
+        ops.trsm(side, uplo, trans, diag, 0.7, T.data, T.ld, B.data, B.ld, tb)
+        outs.append(B.to_dense_local())
+    assert rel_err(outs[0], outs[1]) < tol(dt) * 10
+
+
+@pytest.mark.parametrize("prec", list("sdcz"))
+@pytest.mark.parametrize("uplo", [dp.dplasmaLower, dp.dplasmaUpper])
+@pytest.mark.parametrize("dims", [(378, 93), (1024, 256), (600, 512)])
+def test_potrf(gctx, prec, uplo, dims):
+    dt = DTYPES[prec]
+    N, NB = dims
+    A = dp.block_cyclic(gctx, dt, NB, NB, N, N)
+    dp.plghe(gctx, float(N), uplo, A, 3872)
+    A0 = A.like()
+    dp.lacpy(gctx, dp.dplasmaUpperLower, A, A0)
+    info = dp.potrf(gctx, uplo, A)
+    assert info == 0
+    ok, res = dp.check_potrf(gctx, uplo, A, A0)
+    assert ok, res
+
+
+def test_potrf_matches_cpu(gctx, cctx):
+    N, NB = 700, 128
+    outs = []
+    for ctx in (gctx, cctx):
+        A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+        dp.plghe(ctx, float(N), dp.dplasmaLower, A, 3872)
+        dp.potrf(ctx, dp.dplasmaLower, A)
+        outs.append(A.to_dense_local().tril())
+    assert rel_err(outs[0], outs[1]) < 1e-12
+
+
+def test_potrf_info_gpu(gctx):
+    N, NB = 256, 64
+    A = dp.block_cyclic(gctx, torch.float64, NB, NB, N, N)
+    dp.plghe(gctx, 0.0, dp.dplasmaLower, A, 1)
+    assert dp.potrf(gctx, dp.dplasmaLower, A) > 0
+
+
+@pytest.mark.parametrize("norm", [dp.dplasmaMaxNorm, dp.dplasmaOneNorm, dp.dplasmaInfNorm, dp.dplasmaFrobeniusNorm])
+def test_norms(gctx, cctx, norm):
+    vals = []
+    for ctx in (gctx, cctx):
+        A = dp.block_cyclic(ctx, torch.complex128, 40, 40, 130, 130)
+        dp.plghe(ctx, 2.0, dp.dplasmaUpperLower, A, 9)
+        vals.append((dp.lange(ctx, norm, A), dp.lanhe(ctx, norm, dp.dplasmaLower, A)))
+    assert abs(vals[0][0] - vals[1][0]) <= 1e-12 * vals[1][0]
+    assert abs(vals[0][1] - vals[1][1]) <= 1e-12 * vals[1][1]
+
+
+def test_lapack_storage_gemm(gctx, cctx):
+    outs = []
+    for ctx in (gctx, cctx):
+        A = dp.block_cyclic(ctx, torch.float64, 64, 64, 200, 150, storage=dp.STORAGE_LAPACK, lld=203)
+        B = dp.block_cyclic(ctx, torch.float64, 64, 64, 150, 170, storage=dp.STORAGE_LAPACK)
+        C = dp.block_cyclic(ctx, torch.float64, 64, 64, 200, 170)
+        dp.plrnt(ctx, A, 1)
+        dp.plrnt(ctx, B, 2)
+        dp.plrnt(ctx, C, 3)
+        dp.gemm(ctx, 111, 111, 1.5, A, B, 0.5, C)
+        outs.append(C.to_dense_local())
+    assert rel_err(outs[0], outs[1]) < 1e-12

@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""Build the native parts of dplasma_amd in-tree.
+
+* ``dplasma_amd/lib/libdplasma_kernels.so`` -- every HIP/CDNA4 kernel (gfx950),
+  compiled with ``hipcc --offload-arch=gfx950`` (one object per ``.hip`` file,
+  rebuilt only when the source or a header changed).
+* ``dplasma_amd/lib/_dplasma_rt*.so`` -- the C++ task runtime (DAG engine,
+  DTD front end, schedulers, tracing) as a pybind11 module.
+
+Usage: ``python tools/build.py [--force] [-j N]``.  Called by
+``__graft_entry__.build()`` and imported lazily by ``dplasma_amd.ops._lib``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+KSRC = ROOT / "csrc" / "kernels"
+RSRC = ROOT / "csrc" / "runtime"
+OUT = ROOT / "dplasma_amd" / "lib"
+BUILD = ROOT / "build" / "obj"
+ARCH = os.environ.get("DPLASMA_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _newer(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(" ".join(map(str, cmd)) + "\n" + r.stdout + r.stderr)
+        raise RuntimeError(f"build step failed: {cmd[0]} {cmd[-1]}")
+    return r
+
+
+def build_kernels(force=False, jobs=8) -> Path:
+    OUT.mkdir(parents=True, exist_ok=True)
+    BUILD.mkdir(parents=True, exist_ok=True)
+    headers = sorted(KSRC.glob("*.h"))
+    srcs = sorted(KSRC.glob("*.hip"))
+    objs = []
+    todo = []
+    for s in srcs:
+        o = BUILD / (s.stem + ".o")
+        objs.append(o)
+        if force or _newer(o, [s, *headers]):
+            todo.append((s, o))
+
+    def comp(so):
+        s, o = so
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
+              "-munsafe-fp-atomics", "-c", str(s), "-o", str(o)])
+        return s.name
+
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+            for name in ex.map(comp, todo):
+                print(f"[build] compiled {name}", flush=True)
+    lib = OUT / "libdplasma_kernels.so"
+    if force or todo or _newer(lib, objs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(lib)])
+        print(f"[build] linked {lib.relative_to(ROOT)}", flush=True)
+    return lib
+
+
+def build_runtime(force=False) -> Path | None:
+    srcs = sorted(RSRC.glob("*.cpp"))
+    if not srcs:
+        return None
+    import pybind11
+
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    lib = OUT / f"_dplasma_rt{suffix}"
+    headers = sorted(RSRC.glob("*.h"))
+    if not force and not _newer(lib, [*srcs, *headers]):
+        return lib
+    inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", f"-I{RSRC}",
+           "-I/opt/rocm/include"]
+    cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-D__HIP_PLATFORM_AMD__",
+           *inc, *map(str, srcs), "-o", str(lib), "-L/opt/rocm/lib", "-lamdhip64", "-lpthread",
+           "-Wl,-rpath,/opt/rocm/lib"]
+    _run(cmd)
+    print(f"[build] linked {lib.relative_to(ROOT)}", flush=True)
+    return lib
+
+
+def build_all(force=False, jobs=8):
+    k = build_kernels(force=force, jobs=jobs)
+    r = build_runtime(force=force)
+    return k, r
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
+    a = ap.parse_args()
+    build_all(force=a.force, jobs=a.j)
