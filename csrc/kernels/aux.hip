@@ -57,10 +57,12 @@ __device__ inline T rnd_at(long long I, long long J, long long gM, unsigned long
 // sequential LCG (one skip-ahead per run).
 #define SEG 16
 template <typename T>
-__global__ __launch_bounds__(256) void k_generate(const TileItem* __restrict__ items, int nseg_max, int nmax, T* A,
-                                                  int lda, long long gM, unsigned long long seed, int kind, T bump) {
+__global__ __launch_bounds__(256) void k_generate(const TileItem* __restrict__ items, int nitems, int nseg_max,
+                                                  int nmax, T* A, int lda, long long gM, unsigned long long seed,
+                                                  int kind, T bump) {
   const int per_item = nseg_max * nmax;
   const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= (long long)nitems * per_item) return;  // tail of the last block
   const int item = (int)(gid / per_item);
   const int r = (int)(gid % per_item);
   const int seg = r % nseg_max, j = r / nseg_max;
@@ -116,10 +118,11 @@ __device__ inline bool in_part(int part, long long I, long long J) {
   }
 }
 template <typename T>
-__global__ __launch_bounds__(256) void k_laset(const TileItem* __restrict__ items, int mmax, int nmax, T* A, int lda,
+__global__ __launch_bounds__(256) void k_laset(const TileItem* __restrict__ items, int nitems, int mmax, int nmax, T* A, int lda,
                                                int part, T alpha, T beta) {
   const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
   const int per = mmax * nmax;
+  if (gid >= (long long)nitems * per) return;  // tail of the last block
   const int item = (int)(gid / per), r = (int)(gid % per);
   const int i = r % mmax, j = r / mmax;
   const TileItem it = items[item];
@@ -130,11 +133,12 @@ __global__ __launch_bounds__(256) void k_laset(const TileItem* __restrict__ item
 }
 // B = alpha * op(A) + beta * B on the part; trans: 0 N, 1 T, 2 C (A item tile is op-sized source)
 template <typename T>
-__global__ __launch_bounds__(256) void k_geadd(const TileItem* __restrict__ items, int mmax, int nmax, const T* A,
+__global__ __launch_bounds__(256) void k_geadd(const TileItem* __restrict__ items, int nitems, int mmax, int nmax, const T* A,
                                                int lda, T* B, int ldb, int part, int trans, T alpha, T beta,
                                                int copy) {
   const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
   const int per = mmax * nmax;
+  if (gid >= (long long)nitems * per) return;  // tail of the last block
   const int item = (int)(gid / per), r = (int)(gid % per);
   const int i = r % mmax, j = r / mmax;
   const TileItem it = items[item];
@@ -150,10 +154,11 @@ __global__ __launch_bounds__(256) void k_geadd(const TileItem* __restrict__ item
   *pb = v;
 }
 template <typename T>
-__global__ __launch_bounds__(256) void k_lascal(const TileItem* __restrict__ items, int mmax, int nmax, T* A, int lda,
+__global__ __launch_bounds__(256) void k_lascal(const TileItem* __restrict__ items, int nitems, int mmax, int nmax, T* A, int lda,
                                                 int part, T alpha) {
   const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
   const int per = mmax * nmax;
+  if (gid >= (long long)nitems * per) return;  // tail of the last block
   const int item = (int)(gid / per), r = (int)(gid % per);
   const int i = r % mmax, j = r / mmax;
   const TileItem it = items[item];
@@ -253,7 +258,7 @@ DPL_API int dpl_generate(int prec, int kind, int nitems, const void* items, int 
   const int nseg = cdiv(mmax, SEG);
   const long long total = (long long)nitems * nseg * nmax;
   const int blocks = (int)((total + 255) / 256);
-  DISPATCH(prec, hipLaunchKernelGGL((k_generate<T>), dim3(blocks), dim3(256), 0, st, (const TileItem*)items, nseg,
+  DISPATCH(prec, hipLaunchKernelGGL((k_generate<T>), dim3(blocks), dim3(256), 0, st, (const TileItem*)items, nitems, nseg,
                                     nmax, (T*)A, lda, gM, seed, kind, *(const T*)bump));
   return (int)hipGetLastError();
 }
@@ -263,7 +268,7 @@ DPL_API int dpl_laset(int prec, int part, int nitems, const void* items, int mma
   if (nitems <= 0) return 0;
   const long long total = (long long)nitems * mmax * nmax;
   const int blocks = (int)((total + 255) / 256);
-  DISPATCH(prec, hipLaunchKernelGGL((k_laset<T>), dim3(blocks), dim3(256), 0, st, (const TileItem*)items, mmax, nmax,
+  DISPATCH(prec, hipLaunchKernelGGL((k_laset<T>), dim3(blocks), dim3(256), 0, st, (const TileItem*)items, nitems, mmax, nmax,
                                     (T*)A, lda, part, *(const T*)alpha, *(const T*)beta));
   return (int)hipGetLastError();
 }
@@ -276,7 +281,7 @@ DPL_API int dpl_geadd(int prec, int part, int trans, int nitems, const void* ite
   const long long total = (long long)nitems * mmax * nmax;
   const int blocks = (int)((total + 255) / 256);
   const int tr = trans == DPL_NOTRANS ? 0 : (trans == DPL_TRANS ? 1 : 2);
-  DISPATCH(prec, hipLaunchKernelGGL((k_geadd<T>), dim3(blocks), dim3(256), 0, st, (const TileItem*)items, mmax, nmax,
+  DISPATCH(prec, hipLaunchKernelGGL((k_geadd<T>), dim3(blocks), dim3(256), 0, st, (const TileItem*)items, nitems, mmax, nmax,
                                     (const T*)A, lda, (T*)B, ldb, part, tr, *(const T*)alpha, *(const T*)beta, copy));
   return (int)hipGetLastError();
 }
@@ -286,7 +291,7 @@ DPL_API int dpl_lascal(int prec, int part, int nitems, const void* items, int mm
   if (nitems <= 0) return 0;
   const long long total = (long long)nitems * mmax * nmax;
   const int blocks = (int)((total + 255) / 256);
-  DISPATCH(prec, hipLaunchKernelGGL((k_lascal<T>), dim3(blocks), dim3(256), 0, st, (const TileItem*)items, mmax,
+  DISPATCH(prec, hipLaunchKernelGGL((k_lascal<T>), dim3(blocks), dim3(256), 0, st, (const TileItem*)items, nitems, mmax,
                                     nmax, (T*)A, lda, part, *(const T*)alpha));
   return (int)hipGetLastError();
 }

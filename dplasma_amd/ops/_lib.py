@@ -108,7 +108,10 @@ class Scalar:
 
     @property
     def ptr(self):
-        return ctypes.cast(ctypes.pointer(self.buf), c_vp)
+        # NOTE: the Scalar object must stay referenced until the C call returns;
+        # callers bind it to a local name first (a temporary may be collected
+        # and its buffer reused before the launcher dereferences it).
+        return ctypes.c_void_p(ctypes.addressof(self.buf))
 
 
 def prec_code(dtype: torch.dtype) -> int:

@@ -22,6 +22,7 @@ MASK_FULL, MASK_LOWER, MASK_UPPER = 0, 1, 2
 class _Uploadable:
     def __init__(self):
         self._dev = {}
+        self._host = {}
 
     def _upload(self, arr: np.ndarray, device: torch.device) -> torch.Tensor:
         key = (id(arr), str(device))
@@ -31,6 +32,9 @@ class _Uploadable:
             if device.type == "cuda":
                 host = host.pin_memory()
                 t = host.to(device, non_blocking=True)
+                # keep the pinned staging buffer for the batch's lifetime: the
+                # async H2D copy must never read a recycled host block
+                self._host[key] = host
             else:
                 t = host
             self._dev[key] = t

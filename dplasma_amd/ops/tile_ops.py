@@ -54,10 +54,10 @@ def gemm(transA: int, transB: int, alpha, A: torch.Tensor, lda: int, B: torch.Te
         items, kps = batch.device_arrays(C.device)
         vec_ok = int(batch.vec_ok and lda % 2 == 0 and ldb % 2 == 0 and A.data_ptr() % 16 == 0
                      and B.data_ptr() % 16 == 0)
+        sa, sb = _lib.Scalar(alpha, C.dtype), _lib.Scalar(beta, C.dtype)
         rc = lib.dpl_gemm_batched(_lib.prec_code(C.dtype), transA, transB, len(batch.items), items.data_ptr(),
-                                  kps.data_ptr(), batch.max_m, batch.max_n, _lib.Scalar(alpha, C.dtype).ptr,
-                                  A.data_ptr(), lda, B.data_ptr(), ldb, _lib.Scalar(beta, C.dtype).ptr,
-                                  C.data_ptr(), ldc, vec_ok, int(FORCE_GENERIC_GEMM), _lib.stream_ptr())
+                                  kps.data_ptr(), batch.max_m, batch.max_n, sa.ptr, A.data_ptr(), lda, B.data_ptr(),
+                                  ldb, sb.ptr, C.data_ptr(), ldc, vec_ok, int(FORCE_GENERIC_GEMM), _lib.stream_ptr())
         _lib.check(rc, "gemm_batched")
         return
     for it in batch.items:
@@ -121,9 +121,10 @@ def trsm(side: int, uplo: int, trans: int, diag: int, alpha, A: torch.Tensor, ld
     if _is_gpu(B):
         lib = _lib.load()
         items = batch.device_array(B.device)
+        sa = _lib.Scalar(alpha, B.dtype)
         rc = lib.dpl_trsm_batched(_lib.prec_code(B.dtype), side, uplo, trans, diag, len(batch.items),
-                                  items.data_ptr(), batch.max_m, batch.max_n, _lib.Scalar(alpha, B.dtype).ptr,
-                                  A.data_ptr(), lda, B.data_ptr(), ldb, _lib.stream_ptr())
+                                  items.data_ptr(), batch.max_m, batch.max_n, sa.ptr, A.data_ptr(), lda,
+                                  B.data_ptr(), ldb, _lib.stream_ptr())
         _lib.check(rc, "trsm_batched")
         return
     left = side == dplasmaLeft
@@ -153,9 +154,10 @@ def generate(kind: str, A: torch.Tensor, lda: int, batch: TileBatch, gM: int, se
     if _is_gpu(A):
         lib = _lib.load()
         items = batch.device_array(A.device)
+        sb = _lib.Scalar(bump, A.dtype)
         rc = lib.dpl_generate(_lib.prec_code(A.dtype), GEN_KIND[kind], len(batch.items), items.data_ptr(),
                               batch.max_m, batch.max_n, A.data_ptr(), lda, int(gM), int(seed) & (2**64 - 1),
-                              _lib.Scalar(bump, A.dtype).ptr, _lib.stream_ptr())
+                              sb.ptr, _lib.stream_ptr())
         _lib.check(rc, "generate")
         return
     cplx = A.is_complex()
@@ -194,9 +196,10 @@ def laset(uplo: int, alpha, beta, A: torch.Tensor, lda: int, batch: TileBatch):
         return
     part = _PART.get(uplo, 0)
     if _is_gpu(A):
-        rc = _lib.load().dpl_laset(_lib.prec_code(A.dtype), part, len(batch.items), batch.device_array(A.device).data_ptr(),
-                                   batch.max_m, batch.max_n, _lib.Scalar(alpha, A.dtype).ptr,
-                                   _lib.Scalar(beta, A.dtype).ptr, A.data_ptr(), lda, _lib.stream_ptr())
+        sa, sb = _lib.Scalar(alpha, A.dtype), _lib.Scalar(beta, A.dtype)
+        rc = _lib.load().dpl_laset(_lib.prec_code(A.dtype), part, len(batch.items),
+                                   batch.device_array(A.device).data_ptr(), batch.max_m, batch.max_n, sa.ptr, sb.ptr,
+                                   A.data_ptr(), lda, _lib.stream_ptr())
         _lib.check(rc, "laset")
         return
     for it in batch.items:
@@ -216,10 +219,10 @@ def geadd(uplo: int, trans: int, alpha, A: torch.Tensor, lda: int, beta, B: torc
         return
     part = _PART.get(uplo, 0)
     if _is_gpu(B):
+        sa, sb = _lib.Scalar(alpha, B.dtype), _lib.Scalar(beta, B.dtype)
         rc = _lib.load().dpl_geadd(_lib.prec_code(B.dtype), part, trans, len(batch.items),
-                                   batch.device_array(B.device).data_ptr(), batch.max_m, batch.max_n,
-                                   _lib.Scalar(alpha, B.dtype).ptr, A.data_ptr(), lda, _lib.Scalar(beta, B.dtype).ptr,
-                                   B.data_ptr(), ldb, int(copy), _lib.stream_ptr())
+                                   batch.device_array(B.device).data_ptr(), batch.max_m, batch.max_n, sa.ptr,
+                                   A.data_ptr(), lda, sb.ptr, B.data_ptr(), ldb, int(copy), _lib.stream_ptr())
         _lib.check(rc, "geadd")
         return
     for it in batch.items:
@@ -236,9 +239,10 @@ def lascal(uplo: int, alpha, A: torch.Tensor, lda: int, batch: TileBatch):
         return
     part = _PART.get(uplo, 0)
     if _is_gpu(A):
+        sa = _lib.Scalar(alpha, A.dtype)
         rc = _lib.load().dpl_lascal(_lib.prec_code(A.dtype), part, len(batch.items),
-                                    batch.device_array(A.device).data_ptr(), batch.max_m, batch.max_n,
-                                    _lib.Scalar(alpha, A.dtype).ptr, A.data_ptr(), lda, _lib.stream_ptr())
+                                    batch.device_array(A.device).data_ptr(), batch.max_m, batch.max_n, sa.ptr,
+                                    A.data_ptr(), lda, _lib.stream_ptr())
         _lib.check(rc, "lascal")
         return
     for it in batch.items:
