@@ -28,9 +28,9 @@ _SIGS = {
                          c_vp, c_int, c_int, c_int, c_vp],
     # prec, uplo, n, A, a_off, lda, info*, info_base, stream
     "dpl_potrf_tile": [c_int, c_int, c_int, c_vp, c_ll, c_int, c_vp, c_int, c_vp],
-    # prec, side, uplo, trans, diag, nitems, items, max_m, max_n, alpha*, A, lda, B, ldb, stream
+    # prec, side, uplo, trans, diag, nitems, items, max_m, max_n, alpha*, A, lda, B, ldb, ntri, tri_off, work, stream
     "dpl_trsm_batched": [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_int,
-                         c_vp],
+                         c_int, c_vp, c_vp, c_vp],
     # prec, kind, nitems, items, mmax, nmax, A, lda, gM, seed, bump*, stream
     "dpl_generate": [c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_int, c_ll, c_ull, c_vp, c_vp],
     # prec, part, nitems, items, mmax, nmax, alpha*, beta*, A, lda, stream

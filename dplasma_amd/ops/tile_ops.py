@@ -109,6 +109,118 @@ def potrf_tile(uplo: int, A: torch.Tensor, off: int, n: int, lda: int, info: tor
 
 
 # ----------------------------------------------------------------------------- TRSM
+class _TrsmGroup:
+    """Items sharing one triangle order: device items (gi = triangle index), triangle offsets, scratch."""
+
+    def __init__(self, items, device, dtype, npos):
+        tris = sorted({int(a) for a in items["a_off"]})
+        idx = {a: i for i, a in enumerate(tris)}
+        items = items.copy()
+        items["gi"] = [idx[int(a)] for a in items["a_off"]]
+        self.items = items
+        self.max_m = int(items["m"].max())
+        self.max_n = int(items["n"].max())
+        self.ntri = len(tris)
+        self.items_dev = torch.from_numpy(items.view(np.uint8).copy()).to(device)
+        self.tri_dev = torch.tensor(tris, dtype=torch.int64, device=device)
+        nJ = (npos + 15) // 16
+        self.work = torch.empty(self.ntri * nJ * 256, dtype=dtype, device=device)
+
+
+def _trsm_groups(batch, side, B):
+    key = (str(B.device), side, B.dtype)
+    cache = getattr(batch, "_trsm_cache", None)
+    if cache is None:
+        cache = batch._trsm_cache = {}
+    g = cache.get(key)
+    if g is None:
+        its = batch.items
+        npos = its["m"] if side == dplasmaLeft else its["n"]
+        g = [_TrsmGroup(its[npos == v], B.device, B.dtype, int(v)) for v in sorted(set(int(x) for x in npos))]
+        cache[key] = g
+    return g
+
+
+TRSM_INVERSE_MIN_TILES = 8  # batches at least this large use inverse + MFMA GEMM
+
+
+def _use_inverse(batch, side, B) -> bool:
+    import os
+    thr = int(os.environ.get("DPLASMA_TRSM_INVERSE_MIN_TILES", TRSM_INVERSE_MIN_TILES))
+    if thr <= 0 or len(batch) < thr or B.dtype not in (torch.float64, torch.float32):
+        return False
+    tris = set(int(a) for a in batch.items["a_off"])
+    return len(tris) == 1
+
+
+_IDENT = {}
+
+
+def _identity(n, dtype, device):
+    key = (n, dtype, str(device))
+    t = _IDENT.get(key)
+    if t is None:
+        t = torch.eye(n, dtype=dtype, device=device).t().contiguous().view(-1)  # column-major
+        _IDENT[key] = t
+    return t
+
+
+class _InvPlan:
+    """Per-batch resources for TRSM = apply(op(T)^-1): inverse buffer, copy and GEMM batches."""
+
+    def __init__(self, batch, side, B):
+        its = batch.items
+        npos = int(its["m"].max()) if side == dplasmaLeft else int(its["n"].max())
+        self.n = npos
+        self.inv = torch.empty(npos * npos, dtype=B.dtype, device=B.device)
+        self.inv_batch = TileBatch().add(int(its["a_off"][0]), npos, npos, b_off=0).finalize()
+        # scratch copy of B, one slot per item (ld = max rows)
+        self.ld = int(its["m"].max())
+        slot = self.ld * int(its["n"].max())
+        self.scratch = torch.empty(max(1, len(its)) * slot, dtype=B.dtype, device=B.device)
+        self.copy = TileBatch()
+        self.gemm = GemmBatch()
+        for j, it in enumerate(its):
+            m, n = int(it["m"]), int(it["n"])
+            self.copy.add(int(it["b_off"]), m, n, b_off=j * slot)
+            if side == dplasmaLeft:   # B = Inv * S
+                self.gemm.add(int(it["b_off"]), m, n, [(0, j * slot, m)])
+            else:                     # B = S * Inv
+                self.gemm.add(int(it["b_off"]), m, n, [(j * slot, 0, n)])
+        self.copy.finalize()
+        self.gemm.finalize()
+
+
+def _trsm_via_inverse(side, uplo, trans, diag, alpha, A, lda, B, ldb, batch):
+    plan = getattr(batch, "_inv_plan", None)
+    if plan is None or plan.inv.device != B.device or plan.inv.dtype != B.dtype:
+        plan = batch._inv_plan = _InvPlan(batch, side, B)
+    n = plan.n
+    inv2 = plan.inv
+    inv2.copy_(_identity(n, B.dtype, B.device))
+    # inv := op(T)^-1 by solving against the identity (strip kernel, n/16 workgroups)
+    trsm_strip(side, uplo, trans, diag, 1.0, A, lda, inv2, n, plan.inv_batch)
+    # scratch = B ; B = alpha * op-applied product
+    geadd(0, dplasmaNoTrans, 1.0, B, ldb, 0.0, plan.scratch, plan.ld, plan.copy, copy=True)
+    if side == dplasmaLeft:
+        gemm(dplasmaNoTrans, dplasmaNoTrans, alpha, inv2, n, plan.scratch, plan.ld, 0.0, B, ldb, plan.gemm)
+    else:
+        gemm(dplasmaNoTrans, dplasmaNoTrans, alpha, plan.scratch, plan.ld, inv2, n, 0.0, B, ldb, plan.gemm)
+
+
+def trsm_strip(side, uplo, trans, diag, alpha, A, lda, B, ldb, batch):
+    """The strip kernel only (no inverse path)."""
+    lib = _lib.load()
+    batch.finalize()
+    for sub in _trsm_groups(batch, side, B):
+        sa = _lib.Scalar(alpha, B.dtype)
+        rc = lib.dpl_trsm_batched(_lib.prec_code(B.dtype), side, uplo, trans, diag, len(sub.items),
+                                  sub.items_dev.data_ptr(), sub.max_m, sub.max_n, sa.ptr, A.data_ptr(), lda,
+                                  B.data_ptr(), ldb, sub.ntri, sub.tri_dev.data_ptr(), sub.work.data_ptr(),
+                                  _lib.stream_ptr())
+        _lib.check(rc, "trsm_batched")
+
+
 def trsm(side: int, uplo: int, trans: int, diag: int, alpha, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int,
          batch: TileBatch):
     """For every item: solve op(T) X = alpha B (left) or X op(T) = alpha B (right) in place in B.
@@ -120,12 +232,15 @@ def trsm(side: int, uplo: int, trans: int, diag: int, alpha, A: torch.Tensor, ld
         return
     if _is_gpu(B):
         lib = _lib.load()
-        items = batch.device_array(B.device)
-        sa = _lib.Scalar(alpha, B.dtype)
-        rc = lib.dpl_trsm_batched(_lib.prec_code(B.dtype), side, uplo, trans, diag, len(batch.items),
-                                  items.data_ptr(), batch.max_m, batch.max_n, sa.ptr, A.data_ptr(), lda,
-                                  B.data_ptr(), ldb, _lib.stream_ptr())
-        _lib.check(rc, "trsm_batched")
+        if _use_inverse(batch, side, B):
+            return _trsm_via_inverse(side, uplo, trans, diag, alpha, A, lda, B, ldb, batch)
+        for sub in _trsm_groups(batch, side, B):
+            sa = _lib.Scalar(alpha, B.dtype)
+            rc = lib.dpl_trsm_batched(_lib.prec_code(B.dtype), side, uplo, trans, diag, len(sub.items),
+                                      sub.items_dev.data_ptr(), sub.max_m, sub.max_n, sa.ptr, A.data_ptr(), lda,
+                                      B.data_ptr(), ldb, sub.ntri, sub.tri_dev.data_ptr(), sub.work.data_ptr(),
+                                      _lib.stream_ptr())
+            _lib.check(rc, "trsm_batched")
         return
     left = side == dplasmaLeft
     for it in batch.items:
