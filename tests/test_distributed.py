@@ -1,0 +1,100 @@
+"""Multi-rank (gloo, CPU) tests: distributed algorithms match the single-rank result."""
+import pytest
+import torch
+
+from helpers import run_distributed
+
+
+def _potrf_worker(rank, world, P, N, NB, uplo, prec):
+    import dplasma_amd as dp
+    ctx = dp.init(device="cpu", P=P)
+    dt = dp.PREC_DTYPE[prec]
+    A = dp.block_cyclic(ctx, dt, NB, NB, N, N)
+    dp.plghe(ctx, float(N), uplo, A, 3872)
+    A0 = A.like()
+    dp.lacpy(ctx, dp.dplasmaUpperLower, A, A0)
+    info = dp.potrf(ctx, uplo, A)
+    ok, res = dp.check_potrf(ctx, uplo, A, A0)
+    return info, ok, res, A.to_dense_local()
+
+
+@pytest.mark.parametrize("world,P", [(2, 1), (2, 2), (4, 2), (3, 1)])
+@pytest.mark.parametrize("uplo", [122, 121])
+def test_potrf_distributed(world, P, uplo):
+    N, NB = 150, 19
+    out = run_distributed(_potrf_worker, world, P, N, NB, uplo, "d")
+    full = sum(out[r][3] for r in range(world))
+    for r in range(world):
+        info, ok, res, _ = out[r]
+        assert info == 0 and ok, (r, res)
+    # compare with the single-rank factor
+    import dplasma_amd as dp
+    ctx = dp.Context(device="cpu")
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+    dp.plghe(ctx, float(N), uplo, A, 3872)
+    dp.potrf(ctx, uplo, A)
+    ref = A.to_dense_local()
+    tri = (lambda x: x.tril()) if uplo == 122 else (lambda x: x.triu())
+    assert (tri(full) - tri(ref)).abs().max() < 1e-12
+
+
+def _gemm_worker(rank, world, P, ta, tb, kc):
+    import dplasma_amd as dp
+    ctx = dp.init(device="cpu", P=P)
+    M, N, K, NB = 70, 55, 63, 16
+    am, an = (M, K) if ta == 111 else (K, M)
+    bm, bn = (K, N) if tb == 111 else (N, K)
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, am, an)
+    B = dp.block_cyclic(ctx, torch.float64, NB, NB, bm, bn)
+    C = dp.block_cyclic(ctx, torch.float64, NB, NB, M, N)
+    dp.plrnt(ctx, A, 3872)
+    dp.plrnt(ctx, B, 4674)
+    dp.plrnt(ctx, C, 2873)
+    dp.gemm(ctx, ta, tb, 0.51, A, B, -0.42, C, kc=kc)
+    return C.to_dense_local()
+
+
+@pytest.mark.parametrize("world,P", [(2, 1), (4, 2)])
+@pytest.mark.parametrize("ta,tb", [(111, 111), (112, 111), (111, 112), (112, 112)])
+def test_gemm_summa(world, P, ta, tb):
+    out = run_distributed(_gemm_worker, world, P, ta, tb, 2)
+    full = sum(out[r] for r in range(world))
+    ref = _gemm_worker(0, 1, 1, ta, tb, None) if False else None
+    import dplasma_amd as dp
+    ctx = dp.Context(device="cpu")
+    M, N, K, NB = 70, 55, 63, 16
+    am, an = (M, K) if ta == 111 else (K, M)
+    bm, bn = (K, N) if tb == 111 else (N, K)
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, am, an)
+    B = dp.block_cyclic(ctx, torch.float64, NB, NB, bm, bn)
+    C = dp.block_cyclic(ctx, torch.float64, NB, NB, M, N)
+    dp.plrnt(ctx, A, 3872)
+    dp.plrnt(ctx, B, 4674)
+    dp.plrnt(ctx, C, 2873)
+    a, b, c = A.to_dense_local(), B.to_dense_local(), C.to_dense_local()
+    op = lambda x, t: x if t == 111 else x.T
+    ref = 0.51 * op(a, ta) @ op(b, tb) - 0.42 * c
+    assert (full - ref).abs().max() < 1e-12
+
+
+def _norm_worker(rank, world, P):
+    import dplasma_amd as dp
+    ctx = dp.init(device="cpu", P=P)
+    A = dp.block_cyclic(ctx, torch.float64, 10, 10, 47, 38)
+    dp.plrnt(ctx, A, 7)
+    return [dp.lange(ctx, n, A) for n in (dp.dplasmaMaxNorm, dp.dplasmaOneNorm, dp.dplasmaInfNorm,
+                                          dp.dplasmaFrobeniusNorm)]
+
+
+def test_norms_distributed():
+    out = run_distributed(_norm_worker, 4, 2)
+    ref = _norm_worker(0, 1, 1) if False else None
+    import dplasma_amd as dp
+    ctx = dp.Context(device="cpu")
+    A = dp.block_cyclic(ctx, torch.float64, 10, 10, 47, 38)
+    dp.plrnt(ctx, A, 7)
+    a = A.to_dense_local()
+    ref = [a.abs().max().item(), a.abs().sum(0).max().item(), a.abs().sum(1).max().item(), a.norm().item()]
+    for r in range(4):
+        for g, e in zip(out[r], ref):
+            assert abs(g - e) <= 1e-12 * e
