@@ -11,6 +11,8 @@ import functools
 
 from .constants import DTYPE_PREC
 from .models import aux as _aux
+from .models import blas3 as _blas3
+from .models import cholesky as _chol
 from .models import check as _check
 from .models import gemm as _gemm
 from .models import potrf as _potrf
@@ -33,6 +35,23 @@ _GENERIC = {
     "lange": _aux.lange, "lansy": _aux.lansy, "lanhe": _aux.lanhe, "lantr": _aux.lantr,
     "check_potrf": _check.check_potrf, "check_axmb": _check.check_axmb,
     "redistribute": _redis.redistribute,
+    "trsm": _blas3.trsm, "trsm_New": _blas3.trsm_New,
+    "trmm": _blas3.trmm, "trmm_New": _blas3.trmm_New,
+    "symm": _blas3.symm, "symm_New": _blas3.symm_New,
+    "hemm": _blas3.hemm, "hemm_New": _blas3.hemm_New,
+    "syrk": _blas3.syrk, "syrk_New": _blas3.syrk_New,
+    "herk": _blas3.herk, "herk_New": _blas3.herk_New,
+    "syr2k": _blas3.syr2k, "syr2k_New": _blas3.syr2k_New,
+    "her2k": _blas3.her2k, "her2k_New": _blas3.her2k_New,
+    "gerc": _blas3.gerc, "gerc_New": _blas3.gerc_New,
+    "geru": _blas3.geru, "geru_New": _blas3.geru_New,
+    "potrs": _chol.potrs, "potrs_New": _chol.potrs_New,
+    "posv": _chol.posv, "posv_New": _chol.posv_New,
+    "trtri": _chol.trtri, "trtri_New": _chol.trtri_New,
+    "lauum": _chol.lauum, "lauum_New": _chol.lauum_New,
+    "potri": _chol.potri, "potri_New": _chol.potri_New,
+    "poinv": _chol.poinv, "poinv_New": _chol.poinv_New,
+    "compose": _chol.compose,
 }
 
 

@@ -408,3 +408,45 @@ def tile_norm(kind: int, uplo: int, unit: bool, A: torch.Tensor, lda: int, batch
             out[i, 0] = mx
             out[i, 1] = ((a / mx) ** 2).sum() if mx > 0 else 0.0
     return out
+
+
+# ----------------------------------------------------------------------------- composite tile ops
+def trtri_tile(uplo: int, diag: int, A: torch.Tensor, off: int, n: int, lda: int):
+    """In-place inverse of the uplo triangle of one tile (CORE_ztrtri)."""
+    if n <= 0:
+        return
+    if not _is_gpu(A):
+        t = _view(A, off, n, n, lda)
+        tri = t.tril() if uplo == dplasmaLower else t.triu()
+        if diag == dplasmaUnit:
+            tri = tri - torch.diag_embed(torch.diagonal(tri)) + torch.eye(n, dtype=t.dtype)
+        inv = torch.linalg.solve_triangular(tri, torch.eye(n, dtype=t.dtype), upper=(uplo == dplasmaUpper))
+        keep = torch.ones(n, n, dtype=torch.bool)
+        keep = keep.tril(-1 if diag == dplasmaUnit else 0) if uplo == dplasmaLower else keep.triu(
+            1 if diag == dplasmaUnit else 0)
+        t.copy_(torch.where(keep, inv, t))
+        return
+    scratch = torch.eye(n, dtype=A.dtype, device=A.device).t().contiguous().view(-1)
+    tb = TileBatch().add(int(off), n, n, b_off=0).finalize()
+    trsm_strip(dplasmaLeft, uplo, dplasmaNoTrans, diag, 1.0, A, lda, scratch, n, tb)
+    part = (3 if diag == dplasmaUnit else 1) if uplo == dplasmaLower else (4 if diag == dplasmaUnit else 2)
+    cb = TileBatch().add(0, n, n, b_off=int(off)).finalize()
+    geadd(part, dplasmaNoTrans, 1.0, scratch, n, 0.0, A, lda, cb, copy=True)
+
+
+def lauum_tile(uplo: int, A: torch.Tensor, off: int, n: int, lda: int):
+    """In-place L^H L (lower) or U U^H (upper) of one tile (CORE_zlauum)."""
+    if n <= 0:
+        return
+    T = torch.zeros(n * n, dtype=A.dtype, device=A.device)
+    W = torch.zeros(n * n, dtype=A.dtype, device=A.device)
+    part = 1 if uplo == dplasmaLower else 2
+    cb = TileBatch().add(int(off), n, n, b_off=0).finalize()
+    geadd(part, dplasmaNoTrans, 1.0, A, lda, 0.0, T, n, cb, copy=True)
+    gb = GemmBatch().add(0, n, n, [(0, 0, n)], MASK_LOWER if uplo == dplasmaLower else MASK_UPPER).finalize()
+    if uplo == dplasmaLower:
+        gemm(dplasmaConjTrans, dplasmaNoTrans, 1.0, T, n, T, n, 0.0, W, n, gb)
+    else:
+        gemm(dplasmaNoTrans, dplasmaConjTrans, 1.0, T, n, T, n, 0.0, W, n, gb)
+    back = TileBatch().add(0, n, n, b_off=int(off)).finalize()
+    geadd(part, dplasmaNoTrans, 1.0, W, n, 0.0, A, lda, back, copy=True)

@@ -70,21 +70,23 @@ class ExchangePlan:
         for tb in self.pack.values():
             tb.finalize()
         self.dtype, self.device = dtype, device
-        self.sendbuf = torch.zeros(max(self.nsend, 1) * nbe, dtype=dtype, device=device)
+        self.sendbuf = None  # allocated per run (stream-ordered caching allocator reuse)
 
     def new_recv_buffer(self) -> torch.Tensor:
-        return torch.zeros(max(self.nrecv, 1) * self.nbe, dtype=self.dtype, device=self.device)
+        return torch.empty(max(self.nrecv, 1) * self.nbe, dtype=self.dtype, device=self.device)
 
     def offset(self, mid: int, m: int, n: int) -> int:
         return self.slot[(mid, m, n)]
 
     def run(self, recv: torch.Tensor):
         """Pack + all-to-all into ``recv`` (on the current stream)."""
+        self.sendbuf = torch.empty(max(self.nsend, 1) * self.nbe, dtype=self.dtype, device=self.device)
         for mid, tb in self.pack.items():
             M = self.mats[mid]
             ops.geadd(0, dplasmaNoTrans, 1.0, M.data, M.ld, 0.0, self.sendbuf, self.ld, tb, copy=True)
         if self.ctx.world == 1:
             recv[: self.nrecv * self.nbe].copy_(self.sendbuf[: self.nsend * self.nbe])
+            self.sendbuf = None
             return
         nbe = self.nbe
         out_splits = [c * nbe for c in self.recv_counts]
@@ -92,3 +94,4 @@ class ExchangePlan:
         w = dist.all_to_all_single(recv[: self.nrecv * nbe], self.sendbuf[: self.nsend * nbe], out_splits,
                                    in_splits, async_op=True)
         w.wait()
+        self.sendbuf = None

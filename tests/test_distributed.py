@@ -98,3 +98,37 @@ def test_norms_distributed():
     for r in range(4):
         for g, e in zip(out[r], ref):
             assert abs(g - e) <= 1e-12 * e
+
+
+def _blas3_worker(rank, world, P):
+    import dplasma_amd as dp
+    ctx = dp.init(device="cpu", P=P)
+    out = {}
+    A = dp.block_cyclic(ctx, torch.float64, 12, 12, 50, 50)
+    dp.plghe(ctx, 50.0, dp.dplasmaUpperLower, A, 3)
+    for side in (141, 142):
+        for uplo in (121, 122):
+            for trans in (111, 112):
+                B = dp.block_cyclic(ctx, torch.float64, 12, 12, 50, 37 if side == 141 else 50)
+                if side == 142:
+                    B = dp.block_cyclic(ctx, torch.float64, 12, 12, 37, 50)
+                dp.plrnt(ctx, B, 4)
+                dp.trsm(ctx, side, uplo, trans, 131, 0.5, A, B)
+                out[("trsm", side, uplo, trans)] = B.to_dense_local()
+    A2 = dp.block_cyclic(ctx, torch.float64, 12, 12, 50, 50)
+    dp.plghe(ctx, 50.0, dp.dplasmaUpperLower, A2, 5)
+    dp.poinv(ctx, 122, A2)
+    out["poinv"] = A2.to_dense_local()
+    C = dp.block_cyclic(ctx, torch.float64, 12, 12, 50, 50)
+    dp.plrnt(ctx, C, 6)
+    dp.hemm(ctx, 141, 122, 1.0, A, C, 0.0, A2)
+    out["hemm"] = A2.to_dense_local()
+    return out
+
+
+def test_blas3_distributed_matches_single():
+    res = run_distributed(_blas3_worker, 4, 2)
+    single = _blas3_worker(0, 1, 1)
+    for key in single:
+        full = sum(res[r][key] for r in range(4))
+        assert (full - single[key]).abs().max() < 1e-10, key

@@ -179,3 +179,34 @@ def test_lapack_storage_gemm(gctx, cctx):
         dp.gemm(ctx, 111, 111, 1.5, A, B, 0.5, C)
         outs.append(C.to_dense_local())
     assert rel_err(outs[0], outs[1]) < 1e-12
+
+
+def test_blas3_gpu_matches_cpu(gctx, cctx):
+    outs = []
+    for ctx in (gctx, cctx):
+        r = {}
+        A = dp.block_cyclic(ctx, torch.float64, 64, 64, 300, 300)
+        dp.plghe(ctx, 300.0, dp.dplasmaUpperLower, A, 3)
+        for side in (141, 142):
+            for uplo in (121, 122):
+                for trans in (111, 113):
+                    B = dp.block_cyclic(ctx, torch.float64, 64, 64, 300, 200) if side == 141 else \
+                        dp.block_cyclic(ctx, torch.float64, 64, 64, 200, 300)
+                    dp.plrnt(ctx, B, 4)
+                    dp.trsm(ctx, side, uplo, trans, 131, 0.5, A, B)
+                    r[("trsm", side, uplo, trans)] = B.to_dense_local()
+                    dp.plrnt(ctx, B, 4)
+                    dp.trmm(ctx, side, uplo, trans, 132, 0.5, A, B)
+                    r[("trmm", side, uplo, trans)] = B.to_dense_local()
+        A2 = dp.block_cyclic(ctx, torch.complex128, 64, 64, 256, 256)
+        dp.plghe(ctx, 256.0, dp.dplasmaUpperLower, A2, 5)
+        assert dp.poinv(ctx, dp.dplasmaLower, A2) == 0
+        r["poinv"] = A2.to_dense_local().tril()
+        C = dp.block_cyclic(ctx, torch.complex128, 64, 64, 256, 100)
+        dp.plrnt(ctx, C, 6)
+        D = dp.block_cyclic(ctx, torch.complex128, 64, 64, 256, 256)
+        dp.herk(ctx, dp.dplasmaLower, dp.dplasmaNoTrans, 1.0, C, 0.0, D)
+        r["herk"] = D.to_dense_local().tril()
+        outs.append(r)
+    for k in outs[1]:
+        assert rel_err(outs[0][k], outs[1][k]) < 1e-10, k
