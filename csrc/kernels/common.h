@@ -78,6 +78,11 @@ __device__ inline float absv(float a) { return fabsf(a); }
 __device__ inline double absv(double a) { return fabs(a); }
 __device__ inline float absv(hipFloatComplex a) { return hypotf(a.x, a.y); }
 __device__ inline double absv(hipDoubleComplex a) { return hypot(a.x, a.y); }
+// LAPACK i?amax magnitude: |re| + |im| for complex (cabs1)
+__device__ inline float abs1(float a) { return fabsf(a); }
+__device__ inline double abs1(double a) { return fabs(a); }
+__device__ inline float abs1(hipFloatComplex a) { return fabsf(a.x) + fabsf(a.y); }
+__device__ inline double abs1(hipDoubleComplex a) { return fabs(a.x) + fabs(a.y); }
 __device__ inline float realv(float a) { return a; }
 __device__ inline double realv(double a) { return a; }
 __device__ inline float realv(hipFloatComplex a) { return a.x; }

@@ -13,6 +13,7 @@ from .constants import DTYPE_PREC
 from .models import aux as _aux
 from .models import blas3 as _blas3
 from .models import cholesky as _chol
+from .models import lu as _lu
 from .models import check as _check
 from .models import gemm as _gemm
 from .models import potrf as _potrf
@@ -52,6 +53,11 @@ _GENERIC = {
     "potri": _chol.potri, "potri_New": _chol.potri_New,
     "poinv": _chol.poinv, "poinv_New": _chol.poinv_New,
     "compose": _chol.compose,
+    "getrf_nopiv": _lu.getrf_nopiv, "getrf_nopiv_New": _lu.getrf_nopiv_New,
+    "getrf_1d": _lu.getrf_1d, "getrf_1d_New": _lu.getrf_1d_New, "getrf": _lu.getrf,
+    "laswp": _lu.laswp, "getrs": _lu.getrs, "gesv_1d": _lu.gesv_1d, "gesv": _lu.gesv_1d,
+    "getrs_nopiv": _lu.getrs_nopiv, "gesv_nopiv": _lu.gesv_nopiv,
+    "ipiv_descriptor": _lu.ipiv_descriptor,
 }
 
 

@@ -75,7 +75,7 @@ class TiledMatrix:
         if mb <= 0 or nb <= 0:
             raise ValueError("tile sizes must be positive")
         self.dtype = dtype
-        self.prec = DTYPE_PREC[dtype]
+        self.prec = DTYPE_PREC.get(dtype, 'i')  # integer descriptors (IPIV) use 'i'
         self.mb, self.nb = mb, nb
         self.lm, self.ln = lm, ln          # full matrix extent
         self.lmt, self.lnt = _cdiv(lm, mb), _cdiv(ln, nb)

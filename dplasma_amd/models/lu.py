@@ -1,0 +1,313 @@
+"""LU factorizations and solves.
+
+Reference: ``src/zgetrf_nopiv.jdf`` (zgetrf_nopiv(k) :46, ztrsm_l :86, ztrsm_u
+:128, zgemm :169), ``src/zgetrf_1d.jdf`` (partial pivoting with a
+multithreaded panel, :70-359; ``src/zgetrf_1d_wrapper.c:82``), ``src/zlaswp.jdf``
+/ ``zlaswp_wrapper.c`` and the ScaLAPACK-style drivers getrs / gesv.
+
+MI355X design:
+* getrf_nopiv: TileProgram stages per step (tile LU kernel, two batched TRSM
+  launches, one MFMA GEMM launch) on any P x Q grid.
+* getrf_1d (partial pivoting): 1-D block-cyclic column distribution (P = 1,
+  exactly the reference's "1d" variant): the panel's owner assembles the tile
+  column into one contiguous tall panel, factors it with the pivoting panel
+  kernel (workgroup-wide argmax in LDS), and broadcasts factor + pivots to the
+  other ranks; every rank applies the net row permutation to its local columns
+  with two row-gather launches, then one TRSM launch and one MFMA GEMM launch
+  update its trailing tiles.  Pivots are returned LAPACK-style (global,
+  1-based, sequential interchanges) in a 1 x min(M,N) IPIV descriptor.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..constants import (DPLASMA_ERR_NOT_SUPPORTED, dplasmaLeft, dplasmaLower, dplasmaNoTrans, dplasmaNonUnit,
+                         dplasmaRight, dplasmaTrans, dplasmaConjTrans, dplasmaUnit, dplasmaUpper)
+from ..descriptor import TiledMatrix
+from ..ops import tile_ops as ops
+from ..ops.batch import GemmBatch, TileBatch
+from ..parallel import comm
+from ..runtime import Taskpool
+from ..runtime.tileprog import TileProgram
+from ..utils.flops import flops
+from . import blas3
+
+N_ = dplasmaNoTrans
+
+
+# ----------------------------------------------------------------------------- no pivoting
+def _tile_lu_nopiv(A, key, info, base):
+    def fn(res):
+        b, off, ld = res[key]
+        m, n = A.tile_rows(key[1]), A.tile_cols(key[2])
+        ops.getrf_panel(b, off, m, n, ld, None, info, base, pivot=False)
+    return fn
+
+
+def getrf_nopiv_New(ctx, A, info_out=None):
+    prog = TileProgram(ctx, "getrf_nopiv")
+    prog.flops = flops(A.prec, "getrf", A.m, A.n)
+    info = torch.zeros(1, dtype=torch.int32, device=A.device)
+    kt = min(A.mt, A.nt)
+    for k in range(kt):
+        s = prog.stage(f"getrf({k})")
+        s.batch_fn([(A, k, k)], [], _tile_lu_nopiv(A, (prog.mid(A), k, k), info, k * A.mb))
+        s = prog.stage(f"trsm({k})")
+        for m in range(k + 1, A.mt):
+            s.trsm(dplasmaRight, dplasmaUpper, N_, dplasmaNonUnit, 1.0, (A, k, k), (A, m, k))
+        for n in range(k + 1, A.nt):
+            s.trsm(dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, (A, k, k), (A, k, n))
+        s = prog.stage(f"gemm({k})")
+        for m in range(k + 1, A.mt):
+            for n in range(k + 1, A.nt):
+                s.gemm((A, m, n), [((A, m, k), N_, (A, k, n), N_)], alpha=-1.0, beta=1.0)
+    tp = prog.compile()
+    tp.info = info
+
+    def _done():
+        v = info.clone()
+        comm.allreduce(v, op=torch.distributed.ReduceOp.MAX)
+        r = int(v.item())
+        if info_out is not None:
+            info_out[0] = r
+        return r
+    tp.on_complete(_done)
+    return tp
+
+
+def getrf_nopiv(ctx, A):
+    return getrf_nopiv_New(ctx, A).execute(ctx)
+
+
+# ----------------------------------------------------------------------------- pivot helpers
+def ipiv_descriptor(ctx, A, name="IPIV") -> TiledMatrix:
+    """1 x min(M,N) int32 descriptor (tiles 1 x nb) on the context grid."""
+    k = min(A.m, A.n)
+    return TiledMatrix(torch.int32, 1, A.nb, 1, k, P=1, Q=ctx.world, rank=ctx.rank, device=A.device, name=name)
+
+
+def _perm_from_swaps(piv: np.ndarray, nrows: int) -> np.ndarray:
+    """Sequential interchanges i <-> piv[i] (0-based, rows of a panel) -> perm with new[r] = old[perm[r]]."""
+    perm = np.arange(nrows)
+    for i, p in enumerate(piv):
+        if p != i:
+            perm[i], perm[p] = perm[p], perm[i]
+    return perm
+
+
+def _row_pairs(M: TiledMatrix, rows_dst, rows_src, coltiles, dst_off_fn=None, src_off_fn=None):
+    """RowPair records for rows (global element row indices) across the given local column tiles."""
+    out = []
+    for n in coltiles:
+        for d, s in zip(rows_dst, rows_src):
+            od = dst_off_fn(d, n) if dst_off_fn else M.offset(d // M.mb, n) + d % M.mb
+            os_ = src_off_fn(s, n) if src_off_fn else M.offset(s // M.mb, n) + s % M.mb
+            out.append((od, os_))
+    return np.array(out, dtype=ops.ROW_PAIR)
+
+
+class _Getrf1D:
+    """Per-step closures of the 1-D partial-pivoting LU."""
+
+    def __init__(self, ctx, A, IPIV, info):
+        self.ctx, self.A, self.IPIV, self.info = ctx, A, IPIV, info
+        self.dev = A.device
+        mb, nb = A.mb, A.nb
+        self.kt = min(A.mt, A.nt)
+        self.pbuf = torch.zeros(A.m * nb, dtype=A.dtype, device=self.dev)
+        self.piv_dev = torch.zeros(nb, dtype=torch.int32, device=self.dev)
+        self.ipiv_all = torch.zeros(min(A.m, A.n), dtype=torch.int32, device=self.dev)
+
+    def step(self, k):
+        A, ctx = self.A, self.ctx
+        mb = A.mb
+        kb = A.tile_cols(k)
+        r0 = k * mb
+        mp = A.m - r0                      # panel rows
+        owner = A.grid.pcol(k + A.jt0)
+        me_owner = A.col_is_local(k)
+        pv = self.pbuf[: mp * kb]
+        # --- 1. assemble + factor the panel on its owner
+        if me_owner:
+            tb = TileBatch()
+            for m in range(k, A.mt):
+                tb.add(A.offset(m, k), A.tile_rows(m), kb, b_off=(m - k) * mb)
+            tb.finalize()
+            ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, pv, mp, tb, copy=True)
+            ops.getrf_panel(pv, 0, mp, kb, mp, self.piv_dev, self.info, r0, pivot=True)
+            # write the factored panel back
+            back = TileBatch()
+            for m in range(k, A.mt):
+                back.add((m - k) * mb, A.tile_rows(m), kb, b_off=A.offset(m, k))
+            back.finalize()
+            ops.geadd(0, N_, 1.0, pv, mp, 0.0, A.data, A.ld, back, copy=True)
+        # --- 2. broadcast factored panel + pivots (world == process row for P = 1)
+        if ctx.world > 1:
+            comm.bcast(pv, owner, ctx.row_group)
+            comm.bcast(self.piv_dev, owner, ctx.row_group)
+        # --- 3. apply the net permutation to local columns != k
+        piv = self.piv_dev[: min(mp, kb)].cpu().numpy()  # small D2H (pivots drive the row moves)
+        self.ipiv_all[r0: r0 + len(piv)] = torch.from_numpy(piv.astype(np.int32) + r0 + 1).to(self.dev)
+        perm = _perm_from_swaps(piv, mp)
+        moved = np.nonzero(perm != np.arange(mp))[0]
+        cols = [n for n in range(A.nt) if n != k and A.col_is_local(n)]
+        if len(moved) and cols:
+            dst_rows = moved + r0
+            src_rows = perm[moved] + r0
+            full = [n for n in cols if A.tile_cols(n) == A.nb]
+            ragged = [n for n in cols if A.tile_cols(n) != A.nb]
+            nmv = len(moved)
+            tmp = torch.empty(max(1, nmv * len(cols)) * A.nb, dtype=A.dtype, device=self.dev)
+            for group in (full, ragged):
+                if not group:
+                    continue
+                w = A.tile_cols(group[0])
+                # gather sources into tmp (row-major-ish: row i of column tile j at (j*nmv + i), stride nmv*len)
+                ld_t = nmv * len(group)
+                pairs_in = []
+                pairs_out = []
+                for j, n in enumerate(group):
+                    for i in range(nmv):
+                        s = int(src_rows[i])
+                        d = int(dst_rows[i])
+                        pairs_in.append((j * nmv + i, A.offset(s // mb, n) + s % mb))
+                        pairs_out.append((A.offset(d // mb, n) + d % mb, j * nmv + i))
+                ops.row_gather(tmp, A.data, np.array(pairs_in, dtype=ops.ROW_PAIR), w, ld_t, A.ld)
+                ops.row_gather(A.data, tmp, np.array(pairs_out, dtype=ops.ROW_PAIR), w, A.ld, ld_t)
+        # --- 4. U row block: A(k, n) = L(k,k)^-1 A(k, n), n > k local
+        trail = [n for n in range(k + 1, A.nt) if A.col_is_local(n)]
+        if trail:
+            tb = TileBatch()
+            for n in trail:
+                tb.add(0, kb, A.tile_cols(n), b_off=A.offset(k, n))
+            tb.finalize()
+            ops.trsm(dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, pv, mp, A.data, A.ld, tb)
+            # --- 5. trailing update A(m, n) -= L(m, k) U(k, n)
+            if k + 1 < A.mt:
+                gb = GemmBatch()
+                for n in trail:
+                    for m in range(k + 1, A.mt):
+                        gb.add(A.offset(m, n), A.tile_rows(m), A.tile_cols(n),
+                               [((m - k) * mb, A.offset(k, n), kb)])
+                gb.finalize()
+                ops.gemm(N_, N_, -1.0, pv, mp, A.data, A.ld, 1.0, A.data, A.ld, gb)
+
+
+def getrf_1d_New(ctx, A, IPIV, info_out=None):
+    if ctx.world > 1 and A.P != 1:
+        raise NotImplementedError("getrf_1d requires a 1-D (P = 1) column distribution; "
+                                  "use getrf_nopiv or a 1 x Q grid")
+    tp = Taskpool("getrf_1d", ctx)
+    tp.flops = flops(A.prec, "getrf", A.m, A.n)
+    info = torch.zeros(1, dtype=torch.int32, device=A.device)
+    st = _Getrf1D(ctx, A, IPIV, info)
+    prev = None
+    for k in range(st.kt):
+        prev = tp.task(f"getrf1d({k})", "update", (lambda k=k: st.step(k)), [prev])
+    tp._state = st
+
+    def _done():
+        # IPIV descriptor: every tile owner writes its piece (values are replicated)
+        for (m, n) in IPIV.local_tiles():
+            c0 = n * IPIV.nb
+            IPIV.tile(m, n).copy_(st.ipiv_all[c0: c0 + IPIV.tile_cols(n)].view(1, -1).to(IPIV.device))
+        v = info.clone()
+        comm.allreduce(v, op=torch.distributed.ReduceOp.MAX)
+        r = int(v.item())
+        if info_out is not None:
+            info_out[0] = r
+        return r
+    tp.on_complete(_done)
+    tp.ipiv_all = st.ipiv_all
+    return tp.finish_build()
+
+
+def getrf_1d(ctx, A, IPIV):
+    return getrf_1d_New(ctx, A, IPIV).execute(ctx)
+
+
+getrf = getrf_1d
+
+
+# ----------------------------------------------------------------------------- LASWP / GETRS / GESV
+def _gather_ipiv(ctx, IPIV) -> np.ndarray:
+    k = IPIV.n
+    full = torch.zeros(k, dtype=torch.int32, device=IPIV.device)
+    for (m, n) in IPIV.local_tiles():
+        c0 = n * IPIV.nb
+        full[c0: c0 + IPIV.tile_cols(n)] = IPIV.tile(m, n).view(-1)
+    if ctx.world > 1:
+        comm.allreduce(full)
+    return full.cpu().numpy()
+
+
+def laswp(ctx, A, IPIV, inc=1):
+    """Apply the row interchanges of IPIV (1-based, sequential) to A, forward (inc>0) or backward."""
+    if ctx.world > 1 and A.P != 1:
+        raise NotImplementedError("laswp on P > 1 grids is not supported in this release")
+    piv = _gather_ipiv(ctx, IPIV) - 1
+    perm = np.arange(A.m)
+    seq = range(len(piv)) if inc > 0 else range(len(piv) - 1, -1, -1)
+    for i in seq:
+        p = int(piv[i])
+        if p != i:
+            perm[i], perm[p] = perm[p], perm[i]
+    moved = np.nonzero(perm != np.arange(A.m))[0]
+    cols = [n for n in range(A.nt) if A.col_is_local(n)]
+    if not len(moved) or not cols:
+        return 0
+    tmp = torch.empty(len(moved) * len(cols) * A.nb, dtype=A.dtype, device=A.device)
+    for group in ([n for n in cols if A.tile_cols(n) == A.nb], [n for n in cols if A.tile_cols(n) != A.nb]):
+        if not group:
+            continue
+        w = A.tile_cols(group[0])
+        ld_t = len(moved) * len(group)
+        pin, pout = [], []
+        for j, n in enumerate(group):
+            for i, d in enumerate(moved):
+                s = int(perm[d])
+                pin.append((j * len(moved) + i, A.offset(s // A.mb, n) + s % A.mb))
+                pout.append((A.offset(int(d) // A.mb, n) + int(d) % A.mb, j * len(moved) + i))
+        ops.row_gather(tmp, A.data, np.array(pin, dtype=ops.ROW_PAIR), w, ld_t, A.ld)
+        ops.row_gather(A.data, tmp, np.array(pout, dtype=ops.ROW_PAIR), w, A.ld, ld_t)
+    if A.device.type == "cuda":
+        torch.cuda.synchronize(A.device)
+    return 0
+
+
+def getrs(ctx, trans, A, IPIV, B):
+    """Solve op(A) X = B with the getrf_1d factorization (A = P L U)."""
+    if trans == N_:
+        laswp(ctx, B, IPIV, 1)
+        blas3.trsm(ctx, dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, A, B)
+        blas3.trsm(ctx, dplasmaLeft, dplasmaUpper, N_, dplasmaNonUnit, 1.0, A, B)
+    else:
+        blas3.trsm(ctx, dplasmaLeft, dplasmaUpper, trans, dplasmaNonUnit, 1.0, A, B)
+        blas3.trsm(ctx, dplasmaLeft, dplasmaLower, trans, dplasmaUnit, 1.0, A, B)
+        laswp(ctx, B, IPIV, -1)
+    return 0
+
+
+def gesv_1d(ctx, A, IPIV, B):
+    info = getrf_1d(ctx, A, IPIV)
+    if info != 0:
+        return info
+    return getrs(ctx, N_, A, IPIV, B)
+
+
+def getrs_nopiv(ctx, trans, A, B):
+    if trans == N_:
+        blas3.trsm(ctx, dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, A, B)
+        blas3.trsm(ctx, dplasmaLeft, dplasmaUpper, N_, dplasmaNonUnit, 1.0, A, B)
+    else:
+        blas3.trsm(ctx, dplasmaLeft, dplasmaUpper, trans, dplasmaNonUnit, 1.0, A, B)
+        blas3.trsm(ctx, dplasmaLeft, dplasmaLower, trans, dplasmaUnit, 1.0, A, B)
+    return 0
+
+
+def gesv_nopiv(ctx, A, B):
+    info = getrf_nopiv(ctx, A)
+    if info != 0:
+        return info
+    return getrs_nopiv(ctx, N_, A, B)

@@ -39,6 +39,10 @@ _SIGS = {
     "dpl_geadd": [c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp],
     # prec, part, nitems, items, mmax, nmax, alpha*, A, lda, stream
     "dpl_lascal": [c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp],
+    # prec, m, n, A, a_off, lda, ipiv*, info*, info_base, pivot, stream
+    "dpl_getrf_panel": [c_int, c_int, c_int, c_vp, c_ll, c_int, c_vp, c_vp, c_int, c_int, c_vp],
+    # prec, dst, src, rows, nrows, ncols, ld_dst, ld_src, stream
+    "dpl_row_gather": [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],
     # prec, kind, part, unit, nitems, items, A, lda, out, ostride, stream
     "dpl_tile_norm": [c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_int, c_vp],
 }

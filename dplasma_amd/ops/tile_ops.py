@@ -450,3 +450,59 @@ def lauum_tile(uplo: int, A: torch.Tensor, off: int, n: int, lda: int):
         gemm(dplasmaNoTrans, dplasmaConjTrans, 1.0, T, n, T, n, 0.0, W, n, gb)
     back = TileBatch().add(0, n, n, b_off=int(off)).finalize()
     geadd(part, dplasmaNoTrans, 1.0, W, n, 0.0, A, lda, back, copy=True)
+
+
+# ----------------------------------------------------------------------------- LU primitives
+def getrf_panel(A: torch.Tensor, off: int, m: int, n: int, lda: int, ipiv: torch.Tensor, info: torch.Tensor,
+                info_base: int, pivot: bool = True):
+    """LU of an m x n column-major panel in place; ipiv (int32, >= min(m,n)) gets 0-based panel rows."""
+    if m <= 0 or n <= 0:
+        return
+    if _is_gpu(A):
+        rc = _lib.load().dpl_getrf_panel(_lib.prec_code(A.dtype), m, n, A.data_ptr(), int(off), lda,
+                                         ipiv.data_ptr() if ipiv is not None else None, info.data_ptr(),
+                                         int(info_base), int(pivot), _lib.stream_ptr())
+        _lib.check(rc, "getrf_panel")
+        return
+    P = _view(A, off, m, n, lda)
+    kmax = min(m, n)
+    if pivot:
+        LU, piv, inf = torch.linalg.lu_factor_ex(P.clone())
+        P.copy_(LU)
+        if ipiv is not None:
+            ipiv[:kmax] = (piv[:kmax] - 1).to(torch.int32)
+        bad = int(inf)
+        if bad > 0 and int(info[0]) == 0:
+            info[0] = info_base + bad
+        return
+    for j in range(kmax):
+        d = P[j, j]
+        if d == 0:
+            if int(info[0]) == 0:
+                info[0] = info_base + j + 1
+            continue
+        P[j + 1:, j] /= d
+        if j + 1 < n:
+            P[j + 1:, j + 1:] -= torch.outer(P[j + 1:, j], P[j, j + 1:])
+    if ipiv is not None:
+        ipiv[:kmax] = torch.arange(kmax, dtype=torch.int32)
+
+
+ROW_PAIR = np.dtype([("dst", "<i8"), ("src", "<i8")])
+
+
+def row_gather(dst: torch.Tensor, src: torch.Tensor, pairs: np.ndarray, ncols: int, ld_dst: int, ld_src: int,
+               _cache={}):
+    """dst row at pairs[i].dst := src row at pairs[i].src (ncols elements each, column strides ld_*)."""
+    if len(pairs) == 0 or ncols <= 0:
+        return
+    if _is_gpu(dst):
+        dev = torch.from_numpy(np.ascontiguousarray(pairs).view(np.uint8).copy()).to(dst.device, non_blocking=False)
+        rc = _lib.load().dpl_row_gather(_lib.prec_code(dst.dtype), dst.data_ptr(), src.data_ptr(), dev.data_ptr(),
+                                        len(pairs), ncols, ld_dst, ld_src, _lib.stream_ptr())
+        _lib.check(rc, "row_gather")
+        return
+    for p in pairs:
+        d = torch.as_strided(dst, (ncols,), (ld_dst,), int(p["dst"]))
+        s = torch.as_strided(src, (ncols,), (ld_src,), int(p["src"]))
+        d.copy_(s)

@@ -210,3 +210,21 @@ def test_blas3_gpu_matches_cpu(gctx, cctx):
         outs.append(r)
     for k in outs[1]:
         assert rel_err(outs[0][k], outs[1][k]) < 1e-10, k
+
+
+@pytest.mark.parametrize("prec", list("sdz"))
+def test_lu_gpu(gctx, cctx, prec):
+    dt = DTYPES[prec]
+    N, NB = 300, 64
+    outs = []
+    for ctx in (gctx, cctx):
+        A = dp.block_cyclic(ctx, dt, NB, NB, N, N)
+        dp.plrnt(ctx, A, 3872)
+        IPIV = dp.ipiv_descriptor(ctx, A)
+        assert dp.getrf_1d(ctx, A, IPIV) == 0
+        B = dp.block_cyclic(ctx, dt, NB, NB, N, N)
+        dp.plghe(ctx, float(N), dp.dplasmaUpperLower, B, 5)
+        assert dp.getrf_nopiv(ctx, B) == 0
+        outs.append((A.to_dense_local(), B.to_dense_local()))
+    assert rel_err(outs[0][0], outs[1][0]) < tol(dt) * 100
+    assert rel_err(outs[0][1], outs[1][1]) < tol(dt) * 100
