@@ -96,6 +96,12 @@ template <> __device__ inline float from_real<float>(float r) { return r; }
 template <> __device__ inline double from_real<double>(double r) { return r; }
 template <> __device__ inline hipFloatComplex from_real<hipFloatComplex>(float r) { return make_hipFloatComplex(r, 0.f); }
 template <> __device__ inline hipDoubleComplex from_real<hipDoubleComplex>(double r) { return make_hipDoubleComplex(r, 0.); }
+// scalar from (re, im); the imaginary part is dropped for real types
+template <typename T> __device__ inline T make_sc(typename ST<T>::real re, typename ST<T>::real im);
+template <> __device__ inline float make_sc<float>(float re, float) { return re; }
+template <> __device__ inline double make_sc<double>(double re, double) { return re; }
+template <> __device__ inline hipFloatComplex make_sc<hipFloatComplex>(float re, float im) { return make_hipFloatComplex(re, im); }
+template <> __device__ inline hipDoubleComplex make_sc<hipDoubleComplex>(double re, double im) { return make_hipDoubleComplex(re, im); }
 __device__ inline float divv(float a, float b) { return a / b; }
 __device__ inline double divv(double a, double b) { return a / b; }
 __device__ inline hipFloatComplex divv(hipFloatComplex a, hipFloatComplex b) { return hipCdivf(a, b); }

@@ -1,0 +1,11 @@
+// pybind11 entry point of the native runtime module ``dplasma_amd.lib._dplasma_rt``.
+#include <pybind11/pybind11.h>
+
+namespace py = pybind11;
+
+void register_dag(py::module_& m);
+
+PYBIND11_MODULE(_dplasma_rt, m) {
+  m.doc() = "dplasma_amd native runtime: tile-DAG analysis";
+  register_dag(m);
+}

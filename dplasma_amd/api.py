@@ -14,6 +14,7 @@ from .models import aux as _aux
 from .models import blas3 as _blas3
 from .models import cholesky as _chol
 from .models import lu as _lu
+from .models import qr as _qr
 from .models import check as _check
 from .models import gemm as _gemm
 from .models import potrf as _potrf
@@ -58,6 +59,11 @@ _GENERIC = {
     "laswp": _lu.laswp, "getrs": _lu.getrs, "gesv_1d": _lu.gesv_1d, "gesv": _lu.gesv_1d,
     "getrs_nopiv": _lu.getrs_nopiv, "gesv_nopiv": _lu.gesv_nopiv,
     "ipiv_descriptor": _lu.ipiv_descriptor,
+    # QR / LQ (flat trees)
+    "geqrf": _qr.geqrf, "geqrf_New": _qr.geqrf_New, "gelqf": _qr.gelqf, "gelqf_New": _qr.gelqf_New,
+    "unmqr": _qr.unmqr, "unmqr_New": _qr.unmqr_New, "unmlq": _qr.unmlq, "unmlq_New": _qr.unmlq_New,
+    "ungqr": _qr.ungqr, "ungqr_New": _qr.ungqr_New, "unglq": _qr.unglq, "unglq_New": _qr.unglq_New,
+    "geqrs": _qr.geqrs, "gelqs": _qr.gelqs, "gels": _qr.gels,
 }
 
 

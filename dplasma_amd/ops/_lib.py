@@ -43,6 +43,11 @@ _SIGS = {
     "dpl_getrf_panel": [c_int, c_int, c_int, c_vp, c_ll, c_int, c_vp, c_vp, c_int, c_int, c_vp],
     # prec, dst, src, rows, nrows, ncols, ld_dst, ld_src, stream
     "dpl_row_gather": [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp],
+    # QR / LQ tile kernels on DAG items (csrc/kernels/qr.hip)
+    "dpl_geqrt": [c_int, c_int, c_vp, c_int, c_int, c_int, c_vp],
+    "dpl_unmqr": [c_int, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "dpl_tsqrt": [c_int, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp],
+    "dpl_tsmqr": [c_int, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     # prec, kind, part, unit, nitems, items, A, lda, out, ostride, stream
     "dpl_tile_norm": [c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_int, c_vp],
 }

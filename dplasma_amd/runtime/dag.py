@@ -1,0 +1,470 @@
+"""Tile-task DAGs executed as level-synchronous batched launches.
+
+This is dplasma_amd's counterpart of the reference's two task-graph front
+ends -- the PTG/JDF algorithms (e.g. ``src/zgeqrf.jdf``, ``src/zgeqrf_param.jdf``,
+``src/zgetrf_incpiv.jdf``) and the DTD insert-task interface
+(``parsec_dtd_insert_task`` as used by ``src/dtd_wrappers/``) -- redesigned for
+MI355X:
+
+* An algorithm inserts tile tasks in *program order* (DTD semantics), each
+  naming the tiles it reads and writes.  Insertion is vectorised: one call adds
+  a whole numpy array of tasks of one kind.
+* ``compile()`` computes every task's dependency *level* in native code
+  (``csrc/runtime/dag.cpp``: RAW/WAR/WAW hazards per tile).  All tasks of one
+  kind in one level are independent, so they become ONE batched kernel launch
+  -- thousands of tile updates per launch instead of one tiny launch per task,
+  which is what it takes to fill 256 CUs.
+* Distributed (one process per GPU): a task executes on the home rank of its
+  designated tile (owner-computes, like the JDF's ``: descA(m, n)`` affinity).
+  Other tiles it touches are fetched into a per-rank slot arena before the
+  level (cached per tile version, so a panel's V/T tiles are fetched once per
+  rank, not once per update) and tiles it modifies are written back to their
+  home after the level.  Each level's traffic is ONE ``all_to_all_single``
+  (RCCL p2p over xGMI), planned identically on every rank from replicated
+  metadata; levels without traffic do no collective at all.
+
+Items carry absolute device addresses (``DAG_ITEM``, 64 bytes, layout of
+``QrItem`` in ``csrc/kernels/qr.hip``) so one launch can mix tiles living in
+descriptor storage and in the slot arena.  All items are built and uploaded
+once at compile time ("ENQ" phase, excluded from timing as in
+``tests/common.h:252-277``).
+"""
+from __future__ import annotations
+
+from collections import defaultdict
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..constants import STORAGE_TILE
+from .taskpool import Taskpool
+
+DAG_ITEM = np.dtype([("p0", "<u8"), ("p1", "<u8"), ("p2", "<u8"), ("p3", "<u8"),
+                     ("ld0", "<i4"), ("ld1", "<i4"), ("ld2", "<i4"), ("ld3", "<i4"),
+                     ("m", "<i4"), ("n", "<i4"), ("k", "<i4"), ("pad", "<i4")])
+assert DAG_ITEM.itemsize == 64
+
+R, W, RW = 1, 2, 3
+
+_MID_SHIFT, _M_SHIFT = 44, 22
+_MASK22 = (1 << 22) - 1
+
+
+def _root(M):
+    while getattr(M, "_parent", None) is not None:
+        M = M._parent
+    return M
+
+
+@dataclass
+class Kind:
+    """A tile-kernel family usable in a DAG.
+
+    roles: tuple of (role name, access mode, item pointer slot 0..3)
+    exec_role: index of the role whose home rank executes the task
+    gpu(items_dev_ptr, nitems, stream_ptr): one batched launch
+    cpu(refs, ext): reference execution of one task; refs[r] = (tensor, offset, ld)
+    """
+    name: str
+    roles: Tuple[Tuple[str, int, int], ...]
+    exec_role: int
+    gpu: Callable
+    cpu: Callable
+    flops: Optional[Callable] = None  # ext (n, 3) int array -> total flops
+    prio: int = 0                     # launch order within a level (lower first)
+
+
+def _lib_rt():
+    try:
+        from ..lib import _dplasma_rt as rt  # type: ignore
+        return rt
+    except Exception:
+        return None
+
+
+def _levels_py(ops, modes):
+    st = {}
+    out = np.zeros(len(ops), dtype=np.int32)
+    for t in range(len(ops)):
+        L = 0
+        for k, md in zip(ops[t], modes[t]):
+            if not md or k not in st:
+                continue
+            lw, mr = st[k]
+            if lw >= L:
+                L = lw + 1
+            if (md & 2) and mr >= L:
+                L = mr + 1
+        out[t] = L
+        for k, md in zip(ops[t], modes[t]):
+            if not md:
+                continue
+            lw, mr = st.get(k, (-1, -1))
+            st[k] = (L, -1) if md & 2 else (lw, max(mr, L))
+    return out
+
+
+def _versions_py(ops, modes):
+    ver = defaultdict(int)
+    out = np.full(ops.shape, -1, dtype=np.int32)
+    for t in range(len(ops)):
+        for r in range(ops.shape[1]):
+            if modes[t, r]:
+                out[t, r] = ver[ops[t, r]]
+        for r in range(ops.shape[1]):
+            if modes[t, r] & 2:
+                ver[ops[t, r]] += 1
+    return out
+
+
+class TileDAG:
+    """Program-order tile task graph (see module docstring)."""
+
+    def __init__(self, ctx, name: str):
+        self.ctx = ctx
+        self.name = name
+        self.mats: List = []        # root descriptors, index = matrix id
+        self._mid: Dict[int, int] = {}
+        self.kinds: List[Kind] = []
+        self._kid: Dict[str, int] = {}
+        self._chunks = []           # (kind id, ops (n, R) int64, ext (n, 3) int32)
+        self.flops = 0.0
+        self.info = None
+
+    # ------------------------------------------------------------ registration
+    def mat(self, M) -> int:
+        """Register a descriptor (or a view of one); returns the root's matrix id."""
+        Rt = _root(M)
+        k = id(Rt)
+        if k not in self._mid:
+            self._mid[k] = len(self.mats)
+            self.mats.append(Rt)
+        return self._mid[k]
+
+    def keys(self, M, m, n) -> np.ndarray:
+        """Tile keys of view tiles (m, n) of M (scalars or arrays)."""
+        mid = self.mat(M)
+        gm = np.asarray(m, dtype=np.int64) + M.it0
+        gn = np.asarray(n, dtype=np.int64) + M.jt0
+        return (np.int64(mid) << _MID_SHIFT) | (gm << _M_SHIFT) | gn
+
+    def kind(self, K: Kind) -> int:
+        if K.name not in self._kid:
+            self._kid[K.name] = len(self.kinds)
+            self.kinds.append(K)
+        return self._kid[K.name]
+
+    def add(self, K: Kind, ops, ext):
+        """Append tasks of kind K in program order.
+
+        ops: (n, len(K.roles)) tile keys (-1 for an unused optional role); ext: (n, 3) ints."""
+        ops = np.atleast_2d(np.asarray(ops, dtype=np.int64))
+        ext = np.atleast_2d(np.asarray(ext, dtype=np.int32))
+        if ops.size == 0:
+            return
+        if ops.shape[1] != len(K.roles) or ext.shape != (ops.shape[0], 3):
+            raise ValueError(f"{K.name}: bad task array shapes {ops.shape} {ext.shape}")
+        kid = self.kind(K)
+        self._chunks.append((kid, ops, ext))
+        if K.flops is not None:
+            self.flops += float(K.flops(ext))
+
+    # ------------------------------------------------------------ geometry helpers
+    def _home(self, keys: np.ndarray) -> np.ndarray:
+        mid = keys >> _MID_SHIFT
+        gm = (keys >> _M_SHIFT) & _MASK22
+        gn = keys & _MASK22
+        out = np.zeros(keys.shape, dtype=np.int64)
+        for i, M in enumerate(self.mats):
+            sel = mid == i
+            if not sel.any():
+                continue
+            g = M.grid
+            pr = (gm[sel] // g.kp + g.ip) % g.P
+            pc = (gn[sel] // g.kq + g.jq) % g.Q
+            out[sel] = pr * g.Q + pc
+        return out
+
+    def _local_offsets(self, keys: np.ndarray) -> np.ndarray:
+        """Element offsets of home-local tiles in their root descriptor storage."""
+        mid = keys >> _MID_SHIFT
+        gm = (keys >> _M_SHIFT) & _MASK22
+        gn = keys & _MASK22
+        out = np.zeros(keys.shape, dtype=np.int64)
+        for i, M in enumerate(self.mats):
+            sel = mid == i
+            if not sel.any():
+                continue
+            lrow = np.full(M.lmt, -1, dtype=np.int64)
+            lcol = np.full(M.lnt, -1, dtype=np.int64)
+            for t, k in M.lrow.items():
+                lrow[t] = k
+            for t, k in M.lcol.items():
+                lcol[t] = k
+            il, jl = lrow[gm[sel]], lcol[gn[sel]]
+            if (il < 0).any() or (jl < 0).any():
+                raise RuntimeError("tile is not local to this rank")
+            if M.storage == STORAGE_TILE:
+                out[sel] = (jl * M.llmt + il) * M.mb * M.nb
+            else:
+                out[sel] = il * M.mb + jl * M.nb * M.ld
+        return out
+
+    # ------------------------------------------------------------ compile
+    def compile(self) -> Taskpool:
+        ctx = self.ctx
+        me, world = ctx.rank, ctx.world
+        tp = Taskpool(self.name, ctx)
+        tp.flops = self.flops
+        if not self._chunks:
+            return tp.finish_build()
+        nR = max(len(self.kinds[k].roles) for k, _, _ in self._chunks)
+        ntask = sum(len(o) for _, o, _ in self._chunks)
+        ops = np.full((ntask, nR), -1, dtype=np.int64)
+        modes = np.zeros((ntask, nR), dtype=np.uint8)
+        kid = np.zeros(ntask, dtype=np.int32)
+        ext = np.zeros((ntask, 3), dtype=np.int32)
+        p = 0
+        for k, o, e in self._chunks:
+            n = len(o)
+            K = self.kinds[k]
+            ops[p:p + n, :o.shape[1]] = o
+            for r, (_, md, _) in enumerate(K.roles):
+                modes[p:p + n, r] = np.where(o[:, r] >= 0, md, 0)
+            kid[p:p + n] = k
+            ext[p:p + n] = e
+            p += n
+        self._chunks = []
+        rt = _lib_rt()
+        level = rt.dag_levels(ops, modes) if rt is not None else _levels_py(ops, modes)
+        nlev = int(level.max()) + 1
+        # executor rank per task
+        exec_key = ops[np.arange(ntask), np.array([self.kinds[k].exec_role for k in range(len(self.kinds))])[kid]]
+        exe = self._home(exec_key) if world > 1 else np.zeros(ntask, dtype=np.int64)
+
+        # ---------------- remote-tile plan (identical on every rank)
+        fetch_at = defaultdict(list)   # level -> rows (src, dst, key)
+        wback_at = defaultdict(list)
+        slot_of: Dict[int, int] = {}
+        if world > 1:
+            used = modes > 0
+            t_idx, r_idx = np.nonzero(used)
+            akeys = ops[t_idx, r_idx]
+            home = self._home(akeys)
+            aexe = exe[t_idx]
+            rem = home != aexe
+            if rem.any():
+                ver = rt.dag_versions(ops, modes) if rt is not None else _versions_py(ops, modes)
+                t_r, r_r = t_idx[rem], r_idx[rem]
+                k_r, h_r, e_r = akeys[rem], home[rem], aexe[rem]
+                v_r = ver[t_r, r_r].astype(np.int64)
+                w_r = (modes[t_r, r_r] & 2) > 0
+                l_r = level[t_r].astype(np.int64)
+                order = np.lexsort((l_r, k_r, e_r))
+                t_r, k_r, h_r, e_r, v_r, w_r, l_r = (x[order] for x in (t_r, k_r, h_r, e_r, v_r, w_r, l_r))
+                first = np.ones(len(k_r), dtype=bool)
+                first[1:] = (k_r[1:] != k_r[:-1]) | (e_r[1:] != e_r[:-1])
+                have = np.empty(len(k_r), dtype=np.int64)
+                have[1:] = v_r[:-1] + w_r[:-1]
+                need = first | (v_r != np.where(first, -1, have))
+                for i in np.nonzero(need)[0]:
+                    fetch_at[int(l_r[i])].append((int(h_r[i]), int(e_r[i]), int(k_r[i])))
+                for i in np.nonzero(w_r)[0]:
+                    wback_at[int(l_r[i])].append((int(e_r[i]), int(h_r[i]), int(k_r[i])))
+                mine = np.unique(k_r[e_r == me])
+                for s, k in enumerate(mine.tolist()):
+                    slot_of[k] = s
+        # slot arena (one slot per remote tile this rank touches)
+        nbe = max(M.mb * M.nb for M in self.mats)
+        dtype = self.mats[0].dtype
+        for M in self.mats:
+            if M.dtype != dtype:
+                raise TypeError("all matrices of a DAG must share one dtype")
+        device = ctx.device
+        self.arena = torch.zeros(max(len(slot_of), 1) * nbe, dtype=dtype, device=device) if slot_of else None
+        bases = [M.data for M in self.mats] + ([self.arena] if self.arena is not None else [])
+        esize = torch.empty(0, dtype=dtype).element_size()
+
+        def resolve(keys):
+            """keys (n,) -> (base index, element offset, ld) arrays for this rank."""
+            keys = np.asarray(keys, dtype=np.int64)
+            mid = (keys >> _MID_SHIFT).astype(np.int64)
+            bidx = mid.copy()
+            off = np.zeros(len(keys), dtype=np.int64)
+            ld = np.zeros(len(keys), dtype=np.int32)
+            loc = (self._home(keys) == me) if world > 1 else np.ones(len(keys), dtype=bool)
+            if loc.any():
+                off[loc] = self._local_offsets(keys[loc])
+                ld[loc] = np.array([self.mats[i].ld for i in range(len(self.mats))], dtype=np.int32)[mid[loc]]
+            if (~loc).any():
+                sl = np.array([slot_of[int(k)] for k in keys[~loc]], dtype=np.int64)
+                off[~loc] = sl * nbe
+                bidx[~loc] = len(self.mats)
+                ld[~loc] = np.array([self.mats[i].mb for i in range(len(self.mats))], dtype=np.int32)[mid[~loc]]
+            return bidx, off, ld
+
+        # ---------------- my launches, grouped by (level, kind prio, kind)
+        mine_t = np.nonzero(exe == me)[0] if world > 1 else np.arange(ntask)
+        order = np.lexsort((mine_t, kid[mine_t], np.array([self.kinds[k].prio for k in range(len(self.kinds))])[kid[mine_t]],
+                            level[mine_t]))
+        mine_t = mine_t[order]
+        launches = defaultdict(list)  # level -> [(kind, item slice / cpu refs)]
+        all_items = []
+        nitems_total = 0
+        if len(mine_t):
+            lv, kk = level[mine_t], kid[mine_t]
+            brk = np.nonzero((lv[1:] != lv[:-1]) | (kk[1:] != kk[:-1]))[0] + 1
+            starts = np.concatenate([[0], brk])
+            ends = np.concatenate([brk, [len(mine_t)]])
+            items = np.zeros(len(mine_t), dtype=DAG_ITEM)
+            ptrs = [b.data_ptr() for b in bases]
+            refs_all = []
+            for r in range(nR):
+                keys = ops[mine_t, r]
+                ok = keys >= 0
+                b = np.full(len(keys), -1, dtype=np.int64)
+                o = np.zeros(len(keys), dtype=np.int64)
+                l = np.zeros(len(keys), dtype=np.int32)
+                if ok.any():
+                    b[ok], o[ok], l[ok] = resolve(keys[ok])
+                refs_all.append((b, o, l))
+            # role -> pointer slot per kind
+            for s, e in zip(starts, ends):
+                K = self.kinds[int(kk[s])]
+                seg = items[s:e]
+                for r, (_, _, slot) in enumerate(K.roles):
+                    b, o, l = (x[s:e] for x in refs_all[r])
+                    addr = np.array([ptrs[int(bi)] if bi >= 0 else 0 for bi in b], dtype=np.uint64) + \
+                        (o * esize).astype(np.uint64)
+                    addr[b < 0] = 0
+                    seg[f"p{slot}"] = addr
+                    seg[f"ld{slot}"] = l
+                seg["m"], seg["n"], seg["k"] = ext[mine_t[s:e], 0], ext[mine_t[s:e], 1], ext[mine_t[s:e], 2]
+                cpu_refs = None
+                if device.type != "cuda":
+                    cpu_refs = [[(bases[int(refs_all[r][0][i])] if refs_all[r][0][i] >= 0 else None,
+                                  int(refs_all[r][1][i]), int(refs_all[r][2][i])) for r in range(len(K.roles))]
+                                for i in range(s, e)]
+                launches[int(lv[s])].append((K, int(s), int(e - s), cpu_refs, ext[mine_t[s:e]]))
+            all_items = items
+            nitems_total = len(items)
+        dev_items = None
+        if device.type == "cuda" and nitems_total:
+            host = torch.from_numpy(all_items.view(np.uint8).copy()).pin_memory()
+            dev_items = host.to(device, non_blocking=True)
+            self._host_items = host
+        self.dev_items = dev_items
+
+        # ---------------- exchange plans
+        def xplan(rows, fetch: bool):
+            """rows: (src, dst, key) for one level -> my pack/unpack lists and split sizes."""
+            rows = sorted(rows, key=lambda x: (x[0], x[1], x[2]))
+            sends = [r for r in rows if r[0] == me]
+            recvs = [r for r in rows if r[1] == me]
+            sc = [0] * world
+            rc = [0] * world
+            for s_, d_, _ in sends:
+                sc[d_] += nbe
+            for s_, d_, _ in recvs:
+                rc[s_] += nbe
+            if fetch:   # home storage -> arena slot
+                pk = [k for (_, _, k) in sends]
+                uk = [k for (_, _, k) in recvs]
+                return (pk, True), (uk, False), sc, rc
+            # write-back: arena slot -> home storage
+            return ([k for (_, _, k) in sends], False), ([k for (_, _, k) in recvs], True), sc, rc
+
+        def copy_plan(keys, from_home: bool, to_buf: bool):
+            """Batched tile copies between (home storage | arena) and a contiguous buffer."""
+            from ..ops.batch import TileBatch
+            groups = {}
+            if not keys:
+                return []
+            b, o, l = resolve(np.array(keys, dtype=np.int64))
+            for i, k in enumerate(keys):
+                mid = k >> _MID_SHIFT
+                M = self.mats[mid]
+                gm, gn = (k >> _M_SHIFT) & _MASK22, k & _MASK22
+                rows = min(M.mb, M.lm - gm * M.mb)
+                cols = min(M.nb, M.ln - gn * M.nb)
+                g = groups.setdefault((int(b[i]), int(l[i]), M.mb), TileBatch())
+                g.add(int(o[i]), rows, cols, b_off=i * nbe)
+            return [(bi, ldx, mb, tb.finalize()) for (bi, ldx, mb), tb in groups.items()]
+
+        xch = {}
+        for L in range(nlev):
+            for phase, rows in (("f", fetch_at.get(L)), ("w", wback_at.get(L))):
+                if not rows:
+                    continue
+                (pk, _), (uk, _), sc, rc = xplan(rows, phase == "f")
+                xch[(L, phase)] = (copy_plan(pk, phase == "f", True), copy_plan(uk, phase == "w", False), sc, rc)
+        self._bases = bases
+        prog = _DagProgram(self, nlev, launches, xch, nbe, dtype, device)
+        tp.task(self.name, "update", prog.run)
+        tp.dag = prog
+        return tp.finish_build()
+
+
+class _DagProgram:
+    def __init__(self, dag: TileDAG, nlev, launches, xch, nbe, dtype, device):
+        self.dag = dag
+        self.nlev = nlev
+        self.launches = launches
+        self.xch = xch
+        self.nbe = nbe
+        self.dtype, self.device = dtype, device
+        self.nlaunch = sum(len(v) for v in launches.values())
+
+    def _exchange(self, plan):
+        from ..constants import dplasmaNoTrans
+        from ..ops import tile_ops as ops
+        pack, unpack, sc, rc = plan
+        bases = self.dag._bases
+        nbe = self.nbe
+        sendbuf = torch.empty(sum(sc), dtype=self.dtype, device=self.device)
+        recvbuf = torch.empty(sum(rc), dtype=self.dtype, device=self.device)
+        for bi, ld, mb, tb in pack:   # tile (base, off, ld) -> sendbuf[i*nbe] (ld = mb)
+            ops.geadd(0, dplasmaNoTrans, 1.0, bases[bi], ld, 0.0, sendbuf, mb, tb, copy=True)
+        # every rank joins: the plan exists on all ranks whenever the level has any traffic
+        dist.all_to_all_single(recvbuf, sendbuf, output_split_sizes=rc, input_split_sizes=sc)
+        for bi, ld, mb, tb in unpack:  # recvbuf[i*nbe] -> tile
+            _swap_copy(ops, recvbuf, mb, bases[bi], ld, tb)
+
+    def run(self):
+        dag = self.dag
+        dev_items = dag.dev_items
+        stream = None
+        if self.device.type == "cuda":
+            from ..ops import _lib
+            stream = _lib.stream_ptr()
+        for L in range(self.nlev):
+            x = self.xch.get((L, "f"))
+            if x is not None:
+                self._exchange(x)
+            for (K, start, n, cpu_refs, ext) in self.launches.get(L, ()):
+                if dev_items is not None:
+                    K.gpu(dev_items.data_ptr() + start * DAG_ITEM.itemsize, n, stream)
+                else:
+                    for refs, e in zip(cpu_refs, ext):
+                        K.cpu(refs, (int(e[0]), int(e[1]), int(e[2])))
+            x = self.xch.get((L, "w"))
+            if x is not None:
+                self._exchange(x)
+
+
+def _swap_copy(ops, src, src_ld, dst, dst_ld, tb):
+    """Copy tiles src[b_off] (ld src_ld) -> dst[a_off] (ld dst_ld) for a TileBatch keyed (a=dst, b=src)."""
+    from ..ops.batch import TileBatch
+    from ..constants import dplasmaNoTrans
+    sw = getattr(tb, "_swapped", None)
+    if sw is None:
+        sw = TileBatch()
+        tb.finalize()
+        for it in tb.items:
+            sw.add(int(it["b_off"]), int(it["m"]), int(it["n"]), b_off=int(it["a_off"]))
+        sw.finalize()
+        tb._swapped = sw
+    ops.geadd(0, dplasmaNoTrans, 1.0, src, src_ld, 0.0, dst, dst_ld, sw, copy=True)

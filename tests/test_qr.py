@@ -1,0 +1,253 @@
+"""QR / LQ family: factorizations, Q generation/application, least squares.
+
+Checks follow the reference's testing_zgeqrf.c:221-303 (||I - Q^H Q|| and
+||A - Q R|| / ||A||) and testing_zgels.c; the GPU variants compare the HIP
+kernels against the CPU reference path of the same algorithm.
+"""
+import pytest
+import torch
+
+import dplasma_amd as dp
+from helpers import DTYPES, rel_err, run_distributed
+
+EPS = {"s": 1e-5, "c": 1e-5, "d": 1e-13, "z": 1e-13}
+
+
+def _mk(ctx, dt, M, N, NB, seed, **kw):
+    A = dp.block_cyclic(ctx, dt, NB, NB, M, N, **kw)
+    dp.plrnt(ctx, A, seed)
+    return A
+
+
+def _T(ctx, A, ib):
+    return dp.block_cyclic(ctx, A.dtype, ib, A.nb, A.mt * ib, A.nt * A.nb)
+
+
+def _qr_check(ctx, prec, M, N, NB, IB, lq=False):
+    dt = DTYPES[prec]
+    A = _mk(ctx, dt, M, N, NB, 3872)
+    a = A.to_dense_local().cpu()
+    T = _T(ctx, A, IB)
+    K = min(M, N)
+    if not lq:
+        dp.geqrf(ctx, A, T)
+        Q = dp.block_cyclic(ctx, dt, NB, NB, M, K)
+        dp.ungqr(ctx, A, T, Q)
+        q = Q.to_dense_local().cpu()
+        r = torch.triu(A.to_dense_local().cpu()[:K])
+        orth = (q.conj().T @ q - torch.eye(K, dtype=dt)).abs().max().item()
+        rec = (q @ r - a).abs().max().item() / a.abs().max().item()
+    else:
+        dp.gelqf(ctx, A, T)
+        Q = dp.block_cyclic(ctx, dt, NB, NB, K, N)
+        dp.unglq(ctx, A, T, Q)
+        q = Q.to_dense_local().cpu()
+        l_ = torch.tril(A.to_dense_local().cpu()[:, :K])
+        orth = (q @ q.conj().T - torch.eye(K, dtype=dt)).abs().max().item()
+        rec = (l_ @ q - a).abs().max().item() / a.abs().max().item()
+    lim = EPS[prec] * max(M, N)
+    assert orth < lim, orth
+    assert rec < lim, rec
+    return A, T
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return dp.init(device="cpu")
+
+
+@pytest.mark.parametrize("prec", list("sdcz"))
+@pytest.mark.parametrize("shape", [(40, 24, 8, 4), (37, 23, 8, 3), (30, 30, 10, 4)])
+def test_geqrf(ctx, prec, shape):
+    _qr_check(ctx, prec, *shape)
+
+
+@pytest.mark.parametrize("prec", list("dz"))
+@pytest.mark.parametrize("shape", [(24, 40, 8, 4), (23, 37, 8, 3)])
+def test_gelqf(ctx, prec, shape):
+    _qr_check(ctx, prec, *shape, lq=True)
+
+
+def _dense_q(ctx, A, T, lq):
+    """Full square orthogonal factor Q (M x M for QR, N x N for LQ)."""
+    n = A.m if not lq else A.n
+    Q = dp.block_cyclic(ctx, A.dtype, A.mb, A.nb, n, n)
+    (dp.unglq if lq else dp.ungqr)(ctx, A, T, Q)
+    return Q.to_dense_local().cpu()
+
+
+@pytest.mark.parametrize("prec", list("dz"))
+@pytest.mark.parametrize("lq", [False, True])
+def test_unmqr_unmlq_variants(ctx, prec, lq):
+    dt = DTYPES[prec]
+    M, N, NB, IB = (36, 20, 8, 4) if not lq else (20, 36, 8, 4)
+    A = _mk(ctx, dt, M, N, NB, 11)
+    T = _T(ctx, A, IB)
+    (dp.gelqf if lq else dp.geqrf)(ctx, A, T)
+    q = _dense_q(ctx, A, T, lq)
+    n = q.shape[0]
+    for side in (dp.dplasmaLeft, dp.dplasmaRight):
+        for trans in (dp.dplasmaNoTrans, dp.dplasmaConjTrans):
+            shp = (n, 13) if side == dp.dplasmaLeft else (13, n)
+            C = _mk(ctx, dt, shp[0], shp[1], NB, 5)
+            c = C.to_dense_local().cpu()
+            (dp.unmlq if lq else dp.unmqr)(ctx, side, trans, A, T, C)
+            op = q if trans == dp.dplasmaNoTrans else q.conj().T
+            ref = op @ c if side == dp.dplasmaLeft else c @ op
+            assert rel_err(C.to_dense_local().cpu(), ref) < 1e-12, (side, trans)
+
+
+@pytest.mark.parametrize("prec", list("dz"))
+def test_gels_overdetermined(ctx, prec):
+    dt = DTYPES[prec]
+    M, N, NB, IB, NRHS = 45, 21, 8, 4, 5
+    A = _mk(ctx, dt, M, N, NB, 1)
+    a = A.to_dense_local()
+    B = _mk(ctx, dt, M, NRHS, NB, 2)
+    b = B.to_dense_local()
+    T = _T(ctx, A, IB)
+    dp.gels(ctx, dp.dplasmaNoTrans, A, T, B)
+    x = B.to_dense_local()[:N]
+    ref = torch.linalg.lstsq(a, b).solution
+    assert rel_err(x, ref) < 1e-11
+
+
+@pytest.mark.parametrize("prec", list("dz"))
+def test_gels_underdetermined(ctx, prec):
+    dt = DTYPES[prec]
+    M, N, NB, IB, NRHS = 19, 42, 8, 4, 3
+    A = _mk(ctx, dt, M, N, NB, 1)
+    a = A.to_dense_local()
+    B = _mk(ctx, dt, N, NRHS, NB, 2)
+    b = B.to_dense_local()[:M]
+    T = _T(ctx, A, IB)
+    dp.gels(ctx, dp.dplasmaNoTrans, A, T, B)
+    x = B.to_dense_local()
+    ref = torch.linalg.pinv(a) @ b  # minimum-norm solution
+    assert rel_err(x, ref) < 1e-11
+
+
+def test_dag_levels_native_matches_python():
+    import numpy as np
+    from dplasma_amd.runtime import dag as D
+    rt = D._lib_rt()
+    rng = np.random.default_rng(0)
+    ops = rng.integers(0, 12, size=(300, 3)).astype(np.int64)
+    modes = rng.integers(0, 4, size=(300, 3)).astype(np.uint8)
+    lp = D._levels_py(ops, modes)
+    vp = D._versions_py(ops, modes)
+    if rt is not None:
+        assert (rt.dag_levels(ops, modes) == lp).all()
+        assert (rt.dag_versions(ops, modes) == vp).all()
+    # every hazard is respected: a writer is strictly after every earlier access of its tiles
+    last = {}
+    for t in range(len(ops)):
+        for k, md in zip(ops[t], modes[t]):
+            if not md:
+                continue
+            for (pl, pm) in last.get(k, []):
+                if (md & 2) or (pm & 2):
+                    assert lp[t] > pl
+        for k, md in zip(ops[t], modes[t]):
+            if md:
+                last.setdefault(k, []).append((lp[t], md))
+
+
+# ----------------------------------------------------------------------------- distributed
+def _qr_worker(rank, world, P, lq):
+    import dplasma_amd as dp
+    ctx = dp.init(device="cpu", P=P)
+    dt = torch.float64
+    M, N, NB, IB = (44, 28, 8, 4) if not lq else (28, 44, 8, 4)
+    A = dp.block_cyclic(ctx, dt, NB, NB, M, N)
+    dp.plrnt(ctx, A, 3872)
+    T = dp.block_cyclic(ctx, dt, IB, NB, A.mt * IB, A.nt * NB)
+    (dp.gelqf if lq else dp.geqrf)(ctx, A, T)
+    K = min(M, N)
+    Q = dp.block_cyclic(ctx, dt, NB, NB, M if not lq else K, K if not lq else N)
+    (dp.unglq if lq else dp.ungqr)(ctx, A, T, Q)
+    C = dp.block_cyclic(ctx, dt, NB, NB, M if not lq else N, 9)
+    dp.plrnt(ctx, C, 17)
+    (dp.unmlq if lq else dp.unmqr)(ctx, dp.dplasmaLeft, dp.dplasmaConjTrans, A, T, C)
+    return A.to_dense_local(), T.to_dense_local(), Q.to_dense_local(), C.to_dense_local()
+
+
+@pytest.mark.parametrize("world,P,lq", [(2, 1, False), (2, 2, False), (4, 2, False), (3, 3, True), (4, 2, True)])
+def test_qr_distributed(world, P, lq):
+    out = run_distributed(_qr_worker, world, P, lq)
+    r = _qr_worker(0, 1, 1, lq)  # single-process run of the same algorithm on the same data
+    for i in range(4):
+        full = sum(out[k][i] for k in range(world))
+        assert rel_err(full, r[i]) < 1e-12, i
+
+
+# ----------------------------------------------------------------------------- GPU (HIP kernels)
+@pytest.fixture(scope="module")
+def gctx():
+    return dp.init(device="cuda:0")
+
+
+def _dense(M):
+    return M.to_dense_local().cpu()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", list("sdcz"))
+@pytest.mark.parametrize("lq", [False, True])
+def test_gpu_qr_matches_cpu(gctx, ctx, prec, lq):
+    """Same algorithm on GPU (HIP kernels) and CPU (reference path): factors must agree."""
+    dt = DTYPES[prec]
+    M, N, NB, IB = (200, 136, 32, 8) if not lq else (136, 200, 32, 8)
+    out = []
+    for c in (gctx, ctx):
+        A = _mk(c, dt, M, N, NB, 3872)
+        T = _T(c, A, IB)
+        (dp.gelqf if lq else dp.geqrf)(c, A, T)
+        out.append((_dense(A), _dense(T)))
+    tol_ = 1e-4 if prec in "sc" else 1e-11
+    assert rel_err(out[0][0], out[1][0]) < tol_
+    assert rel_err(out[0][1], out[1][1]) < tol_ * 10
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", list("dz"))
+@pytest.mark.parametrize("shape", [(520, 300, 64, 16), (300, 300, 96, 32), (256, 512, 64, 32)])
+def test_gpu_qr_orthogonality(gctx, prec, shape):
+    M, N, NB, IB = shape
+    _qr_check(gctx, prec, M, N, NB, IB, lq=M < N)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lq", [False, True])
+def test_gpu_unmqr_variants(gctx, lq):
+    dt = torch.complex128
+    M, N, NB, IB = (160, 96, 32, 8) if not lq else (96, 160, 32, 8)
+    A = _mk(gctx, dt, M, N, NB, 11)
+    T = _T(gctx, A, IB)
+    (dp.gelqf if lq else dp.geqrf)(gctx, A, T)
+    q = _dense_q(gctx, A, T, lq)
+    n = q.shape[0]
+    for side in (dp.dplasmaLeft, dp.dplasmaRight):
+        for trans in (dp.dplasmaNoTrans, dp.dplasmaConjTrans):
+            shp = (n, 40) if side == dp.dplasmaLeft else (40, n)
+            C = _mk(gctx, dt, shp[0], shp[1], NB, 5)
+            c = _dense(C)
+            (dp.unmlq if lq else dp.unmqr)(gctx, side, trans, A, T, C)
+            op = q if trans == dp.dplasmaNoTrans else q.conj().T
+            ref = op @ c if side == dp.dplasmaLeft else c @ op
+            assert rel_err(_dense(C), ref) < 1e-12, (side, trans)
+
+
+@pytest.mark.gpu
+def test_gpu_gels(gctx):
+    dt = torch.float64
+    for (M, N) in ((300, 170), (170, 300)):
+        A = _mk(gctx, dt, M, N, 64, 1)
+        a = _dense(A)
+        B = _mk(gctx, dt, max(M, N), 7, 64, 2)
+        b = _dense(B)[:M]
+        T = _T(gctx, A, 16)
+        dp.gels(gctx, dp.dplasmaNoTrans, A, T, B)
+        x = _dense(B)[:N]
+        ref = torch.linalg.lstsq(a, b).solution if M >= N else torch.linalg.pinv(a) @ b
+        assert rel_err(x, ref) < 1e-10
