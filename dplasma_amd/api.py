@@ -15,6 +15,7 @@ from .models import blas3 as _blas3
 from .models import cholesky as _chol
 from .models import lu as _lu
 from .models import qr as _qr
+from .models import qrtree as _qrtree
 from .models import check as _check
 from .models import gemm as _gemm
 from .models import potrf as _potrf
@@ -64,6 +65,14 @@ _GENERIC = {
     "unmqr": _qr.unmqr, "unmqr_New": _qr.unmqr_New, "unmlq": _qr.unmlq, "unmlq_New": _qr.unmlq_New,
     "ungqr": _qr.ungqr, "ungqr_New": _qr.ungqr_New, "unglq": _qr.unglq, "unglq_New": _qr.unglq_New,
     "geqrs": _qr.geqrs, "gelqs": _qr.gelqs, "gels": _qr.gels,
+    # hierarchical QR / LQ (reduction trees)
+    "geqrf_param": _qr.geqrf_param, "geqrf_param_New": _qr.geqrf_param_New,
+    "gelqf_param": _qr.gelqf_param, "gelqf_param_New": _qr.gelqf_param_New,
+    "unmqr_param": _qr.unmqr_param, "unmqr_param_New": _qr.unmqr_param_New,
+    "unmlq_param": _qr.unmlq_param, "unmlq_param_New": _qr.unmlq_param_New,
+    "ungqr_param": _qr.ungqr_param, "ungqr_param_New": _qr.ungqr_param_New,
+    "unglq_param": _qr.unglq_param, "unglq_param_New": _qr.unglq_param_New,
+    "geqrs_param": _qr.geqrs_param, "gelqs_param": _qr.gelqs_param,
 }
 
 
@@ -105,3 +114,8 @@ def register_op(name, fn):
 
 for _n, _f in _GENERIC.items():
     register_op(_n, _f)
+
+# precision-independent helpers (QR trees: src/include/dplasma/qr_param.h)
+for _n in ("hqr_init", "systolic_init", "svd_init", "qrtree_check", "QRTree", "HQRTree", "SystolicTree", "SVDTree",
+           "FlatTree", "FLAT_TREE", "GREEDY_TREE", "FIBONACCI_TREE", "BINARY_TREE", "GREEDY1P_TREE"):
+    _register("dplasma_" + _n if _n.endswith("_TREE") else _n, getattr(_qrtree, _n))

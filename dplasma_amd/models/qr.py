@@ -28,7 +28,7 @@ from ..ops.batch import TileBatch
 from ..runtime.dag import TileDAG
 from ..runtime.taskpool import Taskpool
 from ..utils.flops import flops
-from . import aux, blas3
+from . import aux, blas3, qrtree
 from .cholesky import _Seq
 
 
@@ -63,63 +63,74 @@ def _check_square_tiles(A):
 
 
 # ----------------------------------------------------------------------------- task sequences
-def _factor(dag: TileDAG, X: _L, TT: _L, kd):
-    """Flat-tree tile QR of the logical matrix X (zgeqrf.jdf task order)."""
+def _runs(kills):
+    """Split a panel's kill list into maximal runs of one kernel class (TS / TT)."""
+    out = []
+    for (p, m, t) in kills:
+        cls = "ts" if t == qrtree.KILLED_BY_TS else "tt"
+        if out and out[-1][0] == cls:
+            out[-1][1].append(p)
+            out[-1][2].append(m)
+        else:
+            out.append((cls, [p], [m]))
+    return [(c, np.array(p, dtype=np.int64), np.array(m, dtype=np.int64)) for c, p, m in out]
+
+
+def _factor(dag: TileDAG, X: _L, TS: _L, TT: _L, kd, tree):
+    """Tile QR of the logical matrix X along the elimination plan of ``tree``.
+
+    Per panel k (zgeqrf.jdf / zgeqrf_param.jdf task classes): GEQRT on every
+    head row, UNMQR of the head rows' trailing tiles, then the kills in plan
+    order (TSQRT/TTQRT on the panel, TSMQR/TTMQR on the trailing tiles)."""
     MT, NT = X.mt, X.nt
     for k in range(min(MT, NT)):
-        rk, ck = int(X.rows(k)), int(X.cols(k))
-        akk, tkk = X.keys(dag, k, k), TT.keys(dag, k, k)
-        dag.add(kd["geqrt"], [[akk, tkk]], [[rk, ck, 0]])
+        ck = int(X.cols(k))
+        heads = np.array(tree.heads(k), dtype=np.int64)
         ns = np.arange(k + 1, NT)
+        dag.add(kd["geqrt"], np.stack([X.keys(dag, heads, k), TS.keys(dag, heads, k)], 1),
+                np.stack([X.rows(heads), np.full(len(heads), ck), np.zeros(len(heads), dtype=np.int64)], 1))
         if len(ns):
-            dag.add(kd["unmqr_h"], np.stack([X.keys(dag, k, ns), np.full(len(ns), akk), np.full(len(ns), tkk)], 1),
-                    np.stack([np.full(len(ns), rk), X.cols(ns), np.full(len(ns), min(rk, ck))], 1))
-        ms = np.arange(k + 1, MT)
-        if not len(ms):
-            continue
-        dag.add(kd["tsqrt"], np.stack([np.full(len(ms), akk), X.keys(dag, ms, k), TT.keys(dag, ms, k)], 1),
-                np.stack([X.rows(ms), np.full(len(ms), ck), np.zeros(len(ms), dtype=np.int64)], 1))
-        if len(ns):
-            mm, nn = np.meshgrid(ms, ns, indexing="ij")
-            mm, nn = mm.ravel(), nn.ravel()
-            dag.add(kd["tsmqr_h"], np.stack([X.keys(dag, k, nn), X.keys(dag, mm, nn), X.keys(dag, mm, k),
-                                            TT.keys(dag, mm, k)], 1),
-                    np.stack([X.rows(mm), X.cols(nn), np.full(len(mm), ck)], 1))
+            hh, nn = (x.ravel() for x in np.meshgrid(heads, ns, indexing="ij"))
+            dag.add(kd["unmqr_h"], np.stack([X.keys(dag, hh, nn), X.keys(dag, hh, k), TS.keys(dag, hh, k)], 1),
+                    np.stack([X.rows(hh), X.cols(nn), np.minimum(X.rows(hh), ck)], 1))
+        for cls, pv, vm in _runs(tree.kills(k)):
+            Tm = TS if cls == "ts" else TT
+            dag.add(kd[cls + "qrt"], np.stack([X.keys(dag, pv, k), X.keys(dag, vm, k), Tm.keys(dag, vm, k)], 1),
+                    np.stack([X.rows(vm), np.full(len(vm), ck), np.zeros(len(vm), dtype=np.int64)], 1))
+            if len(ns):
+                ii, nn = (x.ravel() for x in np.meshgrid(np.arange(len(vm)), ns, indexing="ij"))
+                dag.add(kd[cls + "mqr_h"], np.stack([X.keys(dag, pv[ii], nn), X.keys(dag, vm[ii], nn),
+                                                    X.keys(dag, vm[ii], k), Tm.keys(dag, vm[ii], k)], 1),
+                        np.stack([X.rows(vm[ii]), X.cols(nn), np.full(len(ii), ck)], 1))
 
 
-def _apply(dag: TileDAG, X: _L, TT: _L, C: _L, kd, conjtrans: bool, K: int = None):
-    """C := Q^H C (conjtrans) or Q C, Q from _factor(X): the zunmqr_LC / zunmqr_LN sequences."""
-    MT = X.mt
+def _apply(dag: TileDAG, X: _L, TS: _L, TT: _L, C: _L, kd, conjtrans: bool, tree, K: int = None):
+    """C := Q^H C (conjtrans) or Q C, Q from _factor(X, tree) (zunmqr_L{C,N}[_param].jdf)."""
     K = min(X.mt, X.nt) if K is None else K
     NTc = C.nt
     ns = np.arange(NTc)
-    ks = range(K) if conjtrans else range(K - 1, -1, -1)
     sfx = "_h" if conjtrans else ""
-    for k in ks:
-        rk, ck = int(X.rows(k)), int(X.cols(k))
-        akk, tkk = X.keys(dag, k, k), TT.keys(dag, k, k)
-        ms = np.arange(k + 1, MT)
-        if not conjtrans:
-            ms = ms[::-1]
+    for k in (range(K) if conjtrans else range(K - 1, -1, -1)):
+        ck = int(X.cols(k))
+        heads = np.array(tree.heads(k), dtype=np.int64)
 
         def unm():
-            dag.add(kd["unmqr" + sfx],
-                    np.stack([C.keys(dag, k, ns), np.full(NTc, akk), np.full(NTc, tkk)], 1),
-                    np.stack([np.full(NTc, int(C.rows(k))), C.cols(ns), np.full(NTc, min(rk, ck))], 1))
+            hh, nn = (x.ravel() for x in np.meshgrid(heads, ns, indexing="ij"))
+            dag.add(kd["unmqr" + sfx], np.stack([C.keys(dag, hh, nn), X.keys(dag, hh, k), TS.keys(dag, hh, k)], 1),
+                    np.stack([C.rows(hh), C.cols(nn), np.minimum(X.rows(hh), ck)], 1))
 
-        def tsm():
-            if not len(ms):
-                return
-            mm, nn = np.meshgrid(ms, ns, indexing="ij")
-            mm, nn = mm.ravel(), nn.ravel()
-            dag.add(kd["tsmqr" + sfx], np.stack([C.keys(dag, k, nn), C.keys(dag, mm, nn), X.keys(dag, mm, k),
-                                                TT.keys(dag, mm, k)], 1),
-                    np.stack([C.rows(mm), C.cols(nn), np.full(len(mm), ck)], 1))
-        if conjtrans:
-            unm()
-            tsm()
+        runs = _runs(tree.kills(k))
+        if not conjtrans:
+            runs = [(c, p[::-1], m[::-1]) for (c, p, m) in runs[::-1]]
         else:
-            tsm()
+            unm()
+        for cls, pv, vm in runs:
+            Tm = TS if cls == "ts" else TT
+            ii, nn = (x.ravel() for x in np.meshgrid(np.arange(len(vm)), ns, indexing="ij"))
+            dag.add(kd[cls + "mqr" + sfx], np.stack([C.keys(dag, pv[ii], nn), C.keys(dag, vm[ii], nn),
+                                                    X.keys(dag, vm[ii], k), Tm.keys(dag, vm[ii], k)], 1),
+                    np.stack([C.rows(vm[ii]), C.cols(nn), np.full(len(ii), ck)], 1))
+        if not conjtrans:
             unm()
 
 
@@ -142,7 +153,7 @@ def geqrf_New(ctx, A, T) -> Taskpool:
     _check_square_tiles(A)
     _check_T(A, T)
     dag = TileDAG(ctx, "geqrf")
-    _factor(dag, _L(A), _L(T), _kinds(A, T, False))
+    _factor(dag, _L(A), _L(T), _L(T), _kinds(A, T, False), qrtree.FlatTree(A.mt, A.nt))
     dag.flops = flops(A.prec, "geqrf", A.m, A.n)
     return dag.compile()
 
@@ -157,7 +168,7 @@ def gelqf_New(ctx, A, T) -> Taskpool:
     _check_square_tiles(A)
     _check_T(A, T)
     dag = TileDAG(ctx, "gelqf")
-    _factor(dag, _L(A, True), _L(T, True), _kinds(A, T, True))
+    _factor(dag, _L(A, True), _L(T, True), _L(T, True), _kinds(A, T, True), qrtree.FlatTree(A.nt, A.mt))
     dag.flops = flops(A.prec, "gelqf", A.m, A.n)
     return dag.compile()
 
@@ -178,7 +189,11 @@ def _norm_trans(A, trans):
     return trans
 
 
-def _unm(ctx, name, side, trans, A, T, C, lq: bool):
+def _flat(A, lq):
+    return qrtree.FlatTree(A.nt, A.mt) if lq else qrtree.FlatTree(A.mt, A.nt)
+
+
+def _unm(ctx, name, side, trans, A, T, C, lq: bool, tree=None, TT=None):
     _check_square_tiles(A)
     trans = _norm_trans(A, trans)
     if side not in (dplasmaLeft, dplasmaRight):
@@ -193,7 +208,8 @@ def _unm(ctx, name, side, trans, A, T, C, lq: bool):
     X = _L(A, lq)
     dag = TileDAG(ctx, name)
     K = min(A.mt, A.nt)
-    _apply(dag, X, _L(T, lq), _L(C, c_t), _kinds(A, T, lq, c_t), qh, K)
+    _apply(dag, X, _L(T, lq), _L(TT if TT is not None else T, lq), _L(C, c_t), _kinds(A, T, lq, c_t), qh,
+           tree or _flat(A, lq), K)
     dag.flops = flops(A.prec, "unmqr", C.m, C.n, min(A.m, A.n), side == dplasmaLeft)
     return dag.compile()
 
@@ -219,12 +235,13 @@ def unmlq(ctx, side, trans, A, T, C):
 
 
 # ----------------------------------------------------------------------------- UNGQR / UNGLQ
-def _ung(ctx, name, A, T, Q, lq: bool):
+def _ung(ctx, name, A, T, Q, lq: bool, tree=None, TT=None):
     _check_square_tiles(A)
     init = aux.laset_New(ctx, dplasmaUpperLower, 0.0, 1.0, Q)
     dag = TileDAG(ctx, name)
     K = min(A.mt, A.nt)
-    _apply(dag, _L(A, lq), _L(T, lq), _L(Q, lq), _kinds(A, T, lq, lq), False, K)
+    _apply(dag, _L(A, lq), _L(T, lq), _L(TT if TT is not None else T, lq), _L(Q, lq), _kinds(A, T, lq, lq), False,
+           tree or _flat(A, lq), K)
     if lq:
         dag.flops = flops(A.prec, "unglq", Q.m, Q.n, min(A.m, A.n))
     else:
@@ -313,4 +330,107 @@ def gels(ctx, trans, A, T, B):
     unmlq(ctx, dplasmaLeft, dplasmaNoTrans, A, T, B)
     blas3.trsm(ctx, dplasmaLeft, dplasmaLower, dplasmaConjTrans, dplasmaNonUnit, 1.0, A.submatrix(0, 0, M, M),
                B.submatrix(0, 0, M, B.n))
+    return 0
+
+
+# ----------------------------------------------------------------------------- hierarchical (tree-parameterised) variants
+def _check_tree(A, tree, lq):
+    mt, nt = (A.nt, A.mt) if lq else (A.mt, A.nt)
+    if tree.mt != mt or tree.nt != nt:
+        raise ValueError(f"qrtree built for {tree.mt}x{tree.nt} tiles, matrix has {mt}x{nt}")
+
+
+def geqrf_param_New(ctx, tree, A, TS, TT) -> Taskpool:
+    """Hierarchical QR driven by a reduction tree (dplasma_zgeqrf_param_New, src/zgeqrf_param_wrapper.c).
+
+    TS receives the T factors of GEQRT/TSQRT, TT those of TTQRT."""
+    _check_square_tiles(A)
+    _check_T(A, TS)
+    _check_T(A, TT)
+    _check_tree(A, tree, False)
+    dag = TileDAG(ctx, "geqrf_param")
+    _factor(dag, _L(A), _L(TS), _L(TT), _kinds(A, TS, False), tree)
+    dag.flops = flops(A.prec, "geqrf", A.m, A.n)
+    return dag.compile()
+
+
+def geqrf_param(ctx, tree, A, TS, TT):
+    geqrf_param_New(ctx, tree, A, TS, TT).execute(ctx)
+    return 0
+
+
+def gelqf_param_New(ctx, tree, A, TS, TT) -> Taskpool:
+    """Hierarchical LQ (dplasma_zgelqf_param_New); ``tree`` built with trans=ConjTrans."""
+    _check_square_tiles(A)
+    _check_T(A, TS)
+    _check_T(A, TT)
+    _check_tree(A, tree, True)
+    dag = TileDAG(ctx, "gelqf_param")
+    _factor(dag, _L(A, True), _L(TS, True), _L(TT, True), _kinds(A, TS, True), tree)
+    dag.flops = flops(A.prec, "gelqf", A.m, A.n)
+    return dag.compile()
+
+
+def gelqf_param(ctx, tree, A, TS, TT):
+    gelqf_param_New(ctx, tree, A, TS, TT).execute(ctx)
+    return 0
+
+
+def unmqr_param_New(ctx, side, trans, tree, A, TS, TT, C) -> Taskpool:
+    _check_tree(A, tree, False)
+    return _unm(ctx, "unmqr_param", side, trans, A, TS, C, lq=False, tree=tree, TT=TT)
+
+
+def unmqr_param(ctx, side, trans, tree, A, TS, TT, C):
+    unmqr_param_New(ctx, side, trans, tree, A, TS, TT, C).execute(ctx)
+    return 0
+
+
+def unmlq_param_New(ctx, side, trans, tree, A, TS, TT, C) -> Taskpool:
+    _check_tree(A, tree, True)
+    return _unm(ctx, "unmlq_param", side, trans, A, TS, C, lq=True, tree=tree, TT=TT)
+
+
+def unmlq_param(ctx, side, trans, tree, A, TS, TT, C):
+    unmlq_param_New(ctx, side, trans, tree, A, TS, TT, C).execute(ctx)
+    return 0
+
+
+def ungqr_param_New(ctx, tree, A, TS, TT, Q) -> Taskpool:
+    _check_tree(A, tree, False)
+    return _ung(ctx, "ungqr_param", A, TS, Q, lq=False, tree=tree, TT=TT)
+
+
+def ungqr_param(ctx, tree, A, TS, TT, Q):
+    ungqr_param_New(ctx, tree, A, TS, TT, Q).execute(ctx)
+    return 0
+
+
+def unglq_param_New(ctx, tree, A, TS, TT, Q) -> Taskpool:
+    _check_tree(A, tree, True)
+    return _ung(ctx, "unglq_param", A, TS, Q, lq=True, tree=tree, TT=TT)
+
+
+def unglq_param(ctx, tree, A, TS, TT, Q):
+    unglq_param_New(ctx, tree, A, TS, TT, Q).execute(ctx)
+    return 0
+
+
+def geqrs_param(ctx, tree, A, TS, TT, B):
+    """Least squares after geqrf_param (dplasma_zgeqrs_param)."""
+    unmqr_param(ctx, dplasmaLeft, dplasmaConjTrans, tree, A, TS, TT, B)
+    N = A.n
+    blas3.trsm(ctx, dplasmaLeft, dplasmaUpper, dplasmaNoTrans, dplasmaNonUnit, 1.0, A.submatrix(0, 0, N, N),
+               B.submatrix(0, 0, N, B.n))
+    return 0
+
+
+def gelqs_param(ctx, tree, A, TS, TT, B):
+    """Minimum-norm solve after gelqf_param (dplasma_zgelqs_param)."""
+    M = A.m
+    blas3.trsm(ctx, dplasmaLeft, dplasmaLower, dplasmaNoTrans, dplasmaNonUnit, 1.0, A.submatrix(0, 0, M, M),
+               B.submatrix(0, 0, M, B.n))
+    if A.n > M:
+        _zero_rows(ctx, B, M)
+    unmlq_param(ctx, dplasmaLeft, dplasmaConjTrans, tree, A, TS, TT, B)
     return 0

@@ -251,3 +251,126 @@ def test_gpu_gels(gctx):
         x = _dense(B)[:N]
         ref = torch.linalg.lstsq(a, b).solution if M >= N else torch.linalg.pinv(a) @ b
         assert rel_err(x, ref) < 1e-10
+
+
+# ----------------------------------------------------------------------------- QR trees / HQR
+def test_qrtree_validity_sweep():
+    """Exhaustive sweep of tree parameters (tests/TestsQRPivgen.cmake analogue)."""
+    import itertools
+    from dplasma_amd.models import qrtree as Q
+    for mt, nt in ((7, 4), (12, 12), (5, 9), (16, 3), (1, 1)):
+        for ll, hl, a, p, dom, rr in itertools.product(range(5), range(5), (1, 2, 3, 8), (1, 2, 3), (0, 1), (0, 1)):
+            Q.HQRTree(mt, nt, ll, hl, a, p, dom, rr).check()
+        for p, q in itertools.product((1, 2, 3), (1, 2, 4)):
+            Q.SystolicTree(mt, nt, p, q).check()
+        Q.SVDTree(mt, nt, 1, 2, 4, 1).check()
+        Q.FlatTree(mt, nt).check()
+
+
+def test_qrtree_queries():
+    from dplasma_amd.models import qrtree as Q
+    t = Q.HQRTree(8, 4, Q.GREEDY_TREE, Q.FLAT_TREE, a=2, p=2)
+    k = 0
+    assert t.getnbgeqrf(k) == len(t.heads(k))
+    for i in range(t.getnbgeqrf(k)):
+        assert t.geti(k, t.getm(k, i)) == i
+    for m in range(1, 8):
+        p = t.currpiv(k, m)
+        # m appears in p's kill sequence, walkable with nextpiv / prevpiv
+        seq, x = [], t.nextpiv(k, p, t.mt)
+        while x != t.mt:
+            seq.append(x)
+            x = t.nextpiv(k, p, x)
+        assert m in seq
+        back, x = [], t.prevpiv(k, p, p)
+        while x != t.mt:
+            back.append(x)
+            x = t.prevpiv(k, p, x)
+        assert back[::-1] == seq
+    assert t.gettype(0, 2) == Q.KILLED_BY_TS and t.gettype(0, 1) == Q.KILLED_BY_DISTTREE
+    # systolic matches the reference's closed forms (dplasma_systolic_qr.c:56-99)
+    s = Q.SystolicTree(10, 10, p=2, q=2)
+    for k in range(10):
+        for m in range(k + 1, 10):
+            exp_t = 0 if m >= k + 4 else (1 if m >= k + 2 else 3)
+            exp_p = (m - k) % 4 + k if exp_t == 0 else ((m - k) % 2 + k if exp_t == 1 else k)
+            assert s.gettype(k, m) == exp_t and s.currpiv(k, m) == exp_p
+    assert Q.HQRTree(32, 4, Q.BINARY_TREE, Q.BINARY_TREE, 1, 1).depth(0) < Q.FlatTree(32, 4).depth(0)
+
+
+def _hqr_run(c, dt, lq, treeargs, M, N, NB, IB):
+    A = _mk(c, dt, M, N, NB, 77)
+    a = _dense(A)
+    TS = _T(c, A, IB)
+    TT = _T(c, A, IB)
+    tree = dp.hqr_init(dp.dplasmaConjTrans if lq else dp.dplasmaNoTrans, A, *treeargs)
+    (dp.gelqf_param if lq else dp.geqrf_param)(c, tree, A, TS, TT)
+    K = min(M, N)
+    Qm = dp.block_cyclic(c, dt, NB, NB, M if not lq else K, K if not lq else N)
+    (dp.unglq_param if lq else dp.ungqr_param)(c, tree, A, TS, TT, Qm)
+    q = _dense(Qm)
+    if not lq:
+        r = torch.triu(_dense(A)[:K])
+        e1 = (q.conj().T @ q - torch.eye(K, dtype=dt)).abs().max().item()
+        e2 = (q @ r - a).abs().max().item() / a.abs().max().item()
+    else:
+        l_ = torch.tril(_dense(A)[:, :K])
+        e1 = (q @ q.conj().T - torch.eye(K, dtype=dt)).abs().max().item()
+        e2 = (l_ @ q - a).abs().max().item() / a.abs().max().item()
+    return e1, e2, A, tree, TS, TT
+
+
+@pytest.mark.parametrize("prec", list("dz"))
+@pytest.mark.parametrize("lq", [False, True])
+@pytest.mark.parametrize("treeargs", [(1, 0, 2, 3), (3, 3, 1, 2), (2, 1, 3, 2, True), (0, 4, 2, 2, False, True)])
+def test_hqr(ctx, prec, lq, treeargs):
+    M, N = (70, 40) if not lq else (40, 70)
+    e1, e2, *_ = _hqr_run(ctx, DTYPES[prec], lq, treeargs, M, N, 8, 4)
+    assert e1 < 1e-13 and e2 < 1e-13
+
+
+def test_hqr_unmqr_and_solve(ctx):
+    dt = torch.float64
+    e1, e2, A, tree, TS, TT = _hqr_run(ctx, dt, False, (1, 3, 2, 2), 60, 30, 8, 4)
+    B = _mk(ctx, dt, 60, 4, 8, 9)
+    b = _dense(B)
+    A2 = _mk(ctx, dt, 60, 30, 8, 77)
+    dp.geqrs_param(ctx, tree, A, TS, TT, B)
+    ref = torch.linalg.lstsq(_dense(A2), b).solution
+    assert rel_err(_dense(B)[:30], ref) < 1e-11
+
+
+def _hqr_worker(rank, world, P):
+    import dplasma_amd as dp
+    ctx = dp.init(device="cpu", P=P)
+    dt = torch.float64
+    A = dp.block_cyclic(ctx, dt, 8, 8, 68, 36)
+    dp.plrnt(ctx, A, 3)
+    TS = dp.block_cyclic(ctx, dt, 4, 8, A.mt * 4, A.nt * 8)
+    TT = dp.block_cyclic(ctx, dt, 4, 8, A.mt * 4, A.nt * 8)
+    tree = dp.hqr_init(dp.dplasmaNoTrans, A, dp.dplasma_GREEDY_TREE, dp.dplasma_BINARY_TREE, 2, 2)
+    dp.geqrf_param(ctx, tree, A, TS, TT)
+    C = dp.block_cyclic(ctx, dt, 8, 8, 68, 10)
+    dp.plrnt(ctx, C, 5)
+    dp.unmqr_param(ctx, dp.dplasmaLeft, dp.dplasmaConjTrans, tree, A, TS, TT, C)
+    return A.to_dense_local(), TS.to_dense_local(), TT.to_dense_local(), C.to_dense_local()
+
+
+@pytest.mark.parametrize("world,P", [(2, 2), (4, 2)])
+def test_hqr_distributed(world, P):
+    out = run_distributed(_hqr_worker, world, P)
+    r = _hqr_worker(0, 1, 1)
+    for i in range(4):
+        assert rel_err(sum(out[k][i] for k in range(world)), r[i]) < 1e-12, i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", list("sdcz"))
+@pytest.mark.parametrize("lq", [False, True])
+def test_gpu_hqr(gctx, ctx, prec, lq):
+    dt = DTYPES[prec]
+    M, N = (300, 160) if not lq else (160, 300)
+    res = [_hqr_run(c, dt, lq, (1, 3, 2, 2), M, N, 32, 8) for c in (gctx, ctx)]
+    lim = 1e-4 if prec in "sc" else 1e-12
+    assert res[0][0] < lim and res[0][1] < lim
+    assert rel_err(_dense(res[0][2]), _dense(res[1][2])) < lim * 10

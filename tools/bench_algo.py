@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Quick single-GPU timing of one algorithm (factorizations beyond the headline bench).
+
+python tools/bench_algo.py geqrf -N 8192 --nb 256 --ib 32 [--tree hqr] [--runs 2]
+Prints the reference-style line ``[****] TIME(s) ... : X gflops``.
+"""
+import argparse
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+import torch
+
+import dplasma_amd as dp
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("op")
+    ap.add_argument("-N", type=int, default=8192)
+    ap.add_argument("-M", type=int, default=0)
+    ap.add_argument("--nb", type=int, default=256)
+    ap.add_argument("--ib", type=int, default=32)
+    ap.add_argument("--runs", type=int, default=2)
+    ap.add_argument("--prec", default="d")
+    ap.add_argument("--tree", default="flat")
+    a = ap.parse_args()
+    ctx = dp.init(device="cuda:0")
+    dt = {"s": torch.float32, "d": torch.float64, "c": torch.complex64, "z": torch.complex128}[a.prec]
+    M = a.M or a.N
+    N = a.N
+    for r in range(a.runs):
+        A = dp.block_cyclic(ctx, dt, a.nb, a.nb, M, N)
+        dp.plrnt(ctx, A, 3872)
+        if a.op in ("geqrf", "gelqf"):
+            TS = dp.block_cyclic(ctx, dt, a.ib, a.nb, A.mt * a.ib, A.nt * a.nb)
+            TT = dp.block_cyclic(ctx, dt, a.ib, a.nb, A.mt * a.ib, A.nt * a.nb)
+            t0 = time.perf_counter()
+            if a.tree == "flat":
+                tp = (dp.geqrf_New if a.op == "geqrf" else dp.gelqf_New)(ctx, A, TS)
+            else:
+                tree = dp.hqr_init(dp.dplasmaNoTrans if a.op == "geqrf" else dp.dplasmaConjTrans, A,
+                                   dp.dplasma_GREEDY_TREE, dp.dplasma_GREEDY_TREE, 4, 1)
+                tp = (dp.geqrf_param_New if a.op == "geqrf" else dp.gelqf_param_New)(ctx, tree, A, TS, TT)
+        elif a.op == "getrf_nopiv":
+            dp.plghe(ctx, float(N), dp.dplasmaUpperLower, A, 3872)
+            t0 = time.perf_counter()
+            tp = dp.getrf_nopiv_New(ctx, A)
+        elif a.op == "getrf_1d":
+            IPIV = dp.ipiv_descriptor(ctx, A)
+            t0 = time.perf_counter()
+            tp = dp.getrf_1d_New(ctx, A, IPIV)
+        else:
+            raise SystemExit(f"unknown op {a.op}")
+        torch.cuda.synchronize()
+        t_enq = time.perf_counter() - t0
+        t1 = time.perf_counter()
+        tp.run(ctx)
+        torch.cuda.synchronize()
+        tp.complete(ctx)
+        t = time.perf_counter() - t1
+        nl = getattr(getattr(tp, "dag", None), "nlaunch", None)
+        print(f"[****] TIME(s) {t:12.5f} : {a.op}\tPxQxg= 1 1 1 NB= {a.nb} N= {N} M= {M} : "
+              f"{tp.flops / t / 1e9:14.3f} gflops - ENQ {t_enq:.3f}s launches {nl}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
