@@ -91,9 +91,9 @@ __global__ __launch_bounds__(QT) void k_geqrt(const QrItem* __restrict__ items, 
   __shared__ T s_tau[64];
   const QrItem it = items[blockIdx.x];
   const int m = it.m, n = it.n, kk = min(m, n), tid = threadIdx.x;
-  T* Ab = (T*)it.a1;
+  T* Ab = (T*)it.a2;  // A travels in the A2 slot (shared item layout with qr_mfma.hip)
   T* Tb = (T*)it.t;
-  const int ao = it.lda1, ldt = it.ldt;
+  const int ao = it.lda2, ldt = it.ldt;
   for (int i0 = 0; i0 < kk; i0 += ib) {
     const int sb = min(ib, kk - i0);
     for (int j = i0; j < i0 + sb; ++j) {
@@ -206,10 +206,10 @@ __global__ __launch_bounds__(QT) void k_unmqr(const QrItem* __restrict__ items, 
   __shared__ T Tl[64][65];
   const QrItem it = items[blockIdx.x];
   const int m = it.m, nc = it.n, kk = it.k, tid = threadIdx.x;
-  T* Cb = (T*)it.a1;
+  T* Cb = (T*)it.a2;  // C travels in the A2 slot (shared item layout with the MFMA kernel)
   const T* Vb = (const T*)it.v;
   const T* Tb = (const T*)it.t;
-  const int ldc = it.lda1, ldv = it.ldv, ldt = it.ldt;
+  const int ldc = it.lda2, ldv = it.ldv, ldt = it.ldt;
   const int nblk = (kk + ib - 1) / ib;
   for (int bi = 0; bi < nblk; ++bi) {
     const int blk = conjtrans ? bi : nblk - 1 - bi;

@@ -48,6 +48,11 @@ _SIGS = {
     "dpl_unmqr": [c_int, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "dpl_tsqrt": [c_int, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp],
     "dpl_tsmqr": [c_int, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
+    # prec, nitems, items, max_n, a_tr, v_tr, ib, conjtrans, mode, stream
+    "dpl_qr_apply_mfma": [c_int, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "dpl_qr_apply_mfma_ok": [c_int, c_int, c_int],
+    # prec, nitems, items, a_tr, ib, ts, tri, stream
+    "dpl_qr_panel_mfma": [c_int, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp],
     # prec, kind, part, unit, nitems, items, A, lda, out, ostride, stream
     "dpl_tile_norm": [c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_int, c_vp],
 }

@@ -168,6 +168,9 @@ def _ref_tsmqr(A1, A2, V2, T, ib, k, conjtrans, tri):
 
 
 # ----------------------------------------------------------------------------- kinds
+USE_MFMA_APPLY = True  # real precisions, m <= 256, ib <= 32: csrc/kernels/qr_mfma.hip
+
+
 def view_flags(dtype: torch.dtype, transposed: bool):
     """(tr, cj) of a tile view: the tile itself, or its conjugate transpose."""
     return (1, 1 if dtype.is_complex else 0) if transposed else (0, 0)
@@ -194,9 +197,20 @@ def kinds(dtype: torch.dtype, ib: int, av=(0, 0), vv=None):
     out = {}
     pre = f"qr{tr}{cj}{vtr}{vcj}_"
 
-    def mk(name, roles, exec_role, cfn, cname, flags, prio):
-        def gpu(items_ptr, n, stream):
-            rc = getattr(_lib.load(), cname)(prec, n, items_ptr, *flags, stream)
+    def mk(name, roles, exec_role, cfn, cname, flags, prio, fast=None, panel=None):
+        """fast = (mode, conjtrans): eligible for the MFMA reflector-application kernel;
+        panel = (ts, tri): eligible for the MFMA panel kernel."""
+        def gpu(items_ptr, n, stream, emax):
+            lib = _lib.load()
+            if fast is not None and USE_MFMA_APPLY and lib.dpl_qr_apply_mfma_ok(prec, emax[0], ib):
+                rc = lib.dpl_qr_apply_mfma(prec, n, items_ptr, emax[1], tr, vtr, ib, fast[1], fast[0], stream)
+                _lib.check(rc, "qr_apply_mfma")
+                return
+            if panel is not None and USE_MFMA_APPLY and lib.dpl_qr_apply_mfma_ok(prec, emax[0], ib):
+                rc = lib.dpl_qr_panel_mfma(prec, n, items_ptr, tr, ib, panel[0], panel[1], stream)
+                _lib.check(rc, "qr_panel_mfma")
+                return
+            rc = getattr(lib, cname)(prec, n, items_ptr, *flags, stream)
             _lib.check(rc, cname)
         out[name] = Kind(pre + name + f"_{prec}_{ib}", roles, exec_role, gpu, cfn, prio=prio)
 
@@ -209,7 +223,7 @@ def kinds(dtype: torch.dtype, ib: int, av=(0, 0), vv=None):
         _ref_geqrt(A, Tw, ib)
         _store(refs[0], A, tr, cj)
         Tt.copy_(Tw)
-    mk("geqrt", (("A", RW, 0), ("T", RW, 3)), 0, c_geqrt, "dpl_geqrt", (tr, cj, ib), 0)
+    mk("geqrt", (("A", RW, 1), ("T", RW, 3)), 0, c_geqrt, "dpl_geqrt", (tr, cj, ib), 0, panel=(0, 0))
 
     for conjtrans in (0, 1):
         def c_unmqr(refs, ext, conjtrans=conjtrans):
@@ -219,8 +233,8 @@ def kinds(dtype: torch.dtype, ib: int, av=(0, 0), vv=None):
             Tt = torch.as_strided(refs[2][0], (ib, k), (1, refs[2][2]), refs[2][1])
             _ref_unmqr(C, V, Tt.clone(), ib, k, conjtrans)
             _store(refs[0], C, tr, cj)
-        mk("unmqr" + ("_h" if conjtrans else ""), (("C", RW, 0), ("V", R, 2), ("T", R, 3)), 0, c_unmqr,
-           "dpl_unmqr", (tr, cj, vtr, vcj, ib, conjtrans), 1)
+        mk("unmqr" + ("_h" if conjtrans else ""), (("C", RW, 1), ("V", R, 2), ("T", R, 3)), 0, c_unmqr,
+           "dpl_unmqr", (tr, cj, vtr, vcj, ib, conjtrans), 1, fast=(2, conjtrans))
 
     for tri in (0, 1):
         def c_tsqrt(refs, ext, tri=tri):
@@ -235,7 +249,7 @@ def kinds(dtype: torch.dtype, ib: int, av=(0, 0), vv=None):
             _store(refs[1], A2, tr, cj, torch.triu(torch.ones(m, n, dtype=torch.bool)) if tri else None)
             Tt.copy_(Tw)
         mk(("tt" if tri else "ts") + "qrt", (("A1", RW, 0), ("A2", RW, 1), ("T", RW, 3)), 1, c_tsqrt,
-           "dpl_tsqrt", (tr, cj, ib, tri), 0)
+           "dpl_tsqrt", (tr, cj, ib, tri), 0, panel=(1, tri))
         for conjtrans in (0, 1):
             def c_tsmqr(refs, ext, tri=tri, conjtrans=conjtrans):
                 m, n, k = ext
@@ -248,6 +262,6 @@ def kinds(dtype: torch.dtype, ib: int, av=(0, 0), vv=None):
                 _store(refs[1], A2, tr, cj)
             mk(("tt" if tri else "ts") + "mqr" + ("_h" if conjtrans else ""),
                (("A1", RW, 0), ("A2", RW, 1), ("V", R, 2), ("T", R, 3)), 1, c_tsmqr,
-               "dpl_tsmqr", (tr, cj, vtr, vcj, ib, conjtrans, tri), 1)
+               "dpl_tsmqr", (tr, cj, vtr, vcj, ib, conjtrans, tri), 1, fast=(tri, conjtrans))
     return out
 

@@ -65,7 +65,7 @@ class Kind:
 
     roles: tuple of (role name, access mode, item pointer slot 0..3)
     exec_role: index of the role whose home rank executes the task
-    gpu(items_dev_ptr, nitems, stream_ptr): one batched launch
+    gpu(items_dev_ptr, nitems, stream_ptr, emax): one batched launch; emax = max (m, n, k) over the items
     cpu(refs, ext): reference execution of one task; refs[r] = (tensor, offset, ld)
     """
     name: str
@@ -348,7 +348,8 @@ class TileDAG:
                     cpu_refs = [[(bases[int(refs_all[r][0][i])] if refs_all[r][0][i] >= 0 else None,
                                   int(refs_all[r][1][i]), int(refs_all[r][2][i])) for r in range(len(K.roles))]
                                 for i in range(s, e)]
-                launches[int(lv[s])].append((K, int(s), int(e - s), cpu_refs, ext[mine_t[s:e]]))
+                ex = ext[mine_t[s:e]]
+                launches[int(lv[s])].append((K, int(s), int(e - s), cpu_refs, ex, tuple(int(x) for x in ex.max(0))))
             all_items = items
             nitems_total = len(items)
         dev_items = None
@@ -444,9 +445,9 @@ class _DagProgram:
             x = self.xch.get((L, "f"))
             if x is not None:
                 self._exchange(x)
-            for (K, start, n, cpu_refs, ext) in self.launches.get(L, ()):
+            for (K, start, n, cpu_refs, ext, emax) in self.launches.get(L, ()):
                 if dev_items is not None:
-                    K.gpu(dev_items.data_ptr() + start * DAG_ITEM.itemsize, n, stream)
+                    K.gpu(dev_items.data_ptr() + start * DAG_ITEM.itemsize, n, stream, emax)
                 else:
                     for refs, e in zip(cpu_refs, ext):
                         K.cpu(refs, (int(e[0]), int(e[1]), int(e[2])))
