@@ -69,9 +69,11 @@ template <> struct QMF<float> {
 // upper-triangular T block.  A1 == nullptr: no A1 term (UNMQR / GEQRT mode).
 // Caller guarantees Vs/Ts/A2s are complete (barrier before the call); returns
 // after a barrier with A2s updated.
+// a1pre: the A1 values of this lane's W entries, already loaded (or nullptr: load here).
 template <typename T>
 __device__ inline void apply_block(T (*A2s)[QM_LDM], const T (*Vs)[QM_LDM], T (*Ws)[QM_LDW], const T (*Ts)[QM_LDW],
-                                   int mp, int sb, int conjtrans, T* A1, int lda1, View2 va, int i0, int c0, int cw) {
+                                   int mp, int sb, int conjtrans, T* A1, int lda1, View2 va, int i0, int c0, int cw,
+                                   const T* a1pre = nullptr) {
   typedef QMF<T> M_;
   typedef typename M_::acc_t acc_t;
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
@@ -80,11 +82,27 @@ __device__ inline void apply_block(T (*A2s)[QM_LDM], const T (*Vs)[QM_LDM], T (*
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int a = ta + (l & 15), c = tc + M_::drow(l, r);
-    acc[r] = (A1 && a < sb && c < cw) ? vld(A1, lda1, va, i0 + a, c0 + c) : T(0);
+    acc[r] = a1pre ? a1pre[r] : ((A1 && a < sb && c < cw) ? vld(A1, lda1, va, i0 + a, c0 + c) : T(0));
   }
-  for (int r0 = 0; r0 < mp; r0 += 4) {
-    const int rr = r0 + (l >> 4);
-    acc = M_::mma(A2s[tc + (l & 15)][rr], Vs[ta + (l & 15)][rr], acc);
+  {
+    // four independent accumulation chains over the row range (more MFMA/LDS overlap)
+    acc_t acc1, acc2, acc3;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc1[r] = acc2[r] = acc3[r] = T(0);
+    int r0 = 0;
+    for (; r0 + 16 <= mp; r0 += 16) {
+      const int rr = r0 + (l >> 4);
+      const T x0 = A2s[tc + (l & 15)][rr], y0 = Vs[ta + (l & 15)][rr];
+      const T x1 = A2s[tc + (l & 15)][rr + 4], y1 = Vs[ta + (l & 15)][rr + 4];
+      const T x2 = A2s[tc + (l & 15)][rr + 8], y2 = Vs[ta + (l & 15)][rr + 8];
+      const T x3 = A2s[tc + (l & 15)][rr + 12], y3 = Vs[ta + (l & 15)][rr + 12];
+      acc = M_::mma(x0, y0, acc);
+      acc1 = M_::mma(x1, y1, acc1);
+      acc2 = M_::mma(x2, y2, acc2);
+      acc3 = M_::mma(x3, y3, acc3);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] += acc1[r] + acc2[r] + acc3[r];
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) Ws[tc + M_::drow(l, r)][ta + (l & 15)] = acc[r];
@@ -104,7 +122,7 @@ __device__ inline void apply_block(T (*A2s)[QM_LDM], const T (*Vs)[QM_LDM], T (*
       const int a = ta + (l & 15), c = tc + M_::drow(l, r);
       Ws[c][a] = t2[r];
       if (A1 && a < sb && c < cw) {
-        const T old = vld(A1, lda1, va, i0 + a, c0 + c);
+        const T old = a1pre ? a1pre[r] : vld(A1, lda1, va, i0 + a, c0 + c);
         vst(A1, lda1, va, i0 + a, c0 + c, old - t2[r]);
       }
     }
@@ -151,9 +169,12 @@ __device__ inline void load_T(T (*Ts)[QM_LDW], const T* Tt, int ldt, int i0, int
 }
 
 // mode: 0 TS (A1 present, V2 full), 1 TT (A1 present, V2 upper), 2 UNMQR (no A1, V unit lower)
+// The next IB block's V, T and A1 values are prefetched into registers while
+// the current block computes (one wave per SIMD: registers are plentiful).
 template <typename T>
 __global__ __launch_bounds__(256, 1) void k_qr_apply_mfma(const QrItemM* __restrict__ items, int nchunk, int nwg,
                                                           View2 va, View2 vv, int ib, int conjtrans, int mode) {
+  typedef QMF<T> M_;
   __shared__ T A2s[QM_CW][QM_LDM];
   __shared__ T Vs[QM_IB][QM_LDM];
   __shared__ T Ws[QM_CW][QM_LDW];
@@ -165,30 +186,67 @@ __global__ __launch_bounds__(256, 1) void k_qr_apply_mfma(const QrItemM* __restr
   const int c0 = chunk * QM_CW;
   if (c0 >= it.n) return;
   const int cw = min(QM_CW, it.n - c0);
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   T* A1 = mode == 2 ? nullptr : (T*)it.a1;
   T* A2 = (T*)it.a2;
   const T* V = (const T*)it.v;
+  const T* Tt = (const T*)it.t;
   const int mp = (m + 15) & ~15;  // rows padded to 16
-  load_chunk(A2s, A2, it.lda2, va, m, mp, c0, cw);
   const int nblk = (kk + ib - 1) / ib;
-  for (int bi = 0; bi < nblk; ++bi) {
+  const int ta = (w & 1) * 16, tc = (w >> 1) * 16;
+  T vreg[QM_IB * QM_MR / 256];
+  T treg[QM_IB * QM_IB / 256];
+  T areg[4];
+  auto fetch = [&](int bi) {
     const int blk = conjtrans ? bi : nblk - 1 - bi;
     const int i0 = blk * ib, sb = min(ib, kk - i0);
-    for (int e = tid; e < QM_IB * mp; e += 256) {
+#pragma unroll
+    for (int q = 0; q < QM_IB * QM_MR / 256; ++q) {
+      const int e = tid + 256 * q;
       const int a = e / mp, r = e % mp;
       T x = T(0);
-      if (a < sb && r < m) {
+      if (e < QM_IB * mp && a < sb && r < m) {
         const int ag = i0 + a;
         if (mode == 0) x = vld(V, it.ldv, vv, r, ag);
         else if (mode == 1) x = (r <= ag) ? vld(V, it.ldv, vv, r, ag) : T(0);
         else x = (r == ag) ? T(1) : (r > ag ? vld(V, it.ldv, vv, r, ag) : T(0));
       }
-      Vs[a][r] = x;
+      vreg[q] = x;
     }
-    load_T(Ts, (const T*)it.t, it.ldt, i0, sb);
+#pragma unroll
+    for (int q = 0; q < QM_IB * QM_IB / 256; ++q) {
+      const int e = tid + 256 * q;
+      const int col = e / QM_IB, row = e % QM_IB;
+      treg[q] = (row <= col && col < sb) ? Tt[row + (long long)(i0 + col) * it.ldt] : T(0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int a = ta + (l & 15), c = tc + M_::drow(l, r);
+      areg[r] = (A1 && a < sb && c < cw) ? vld(A1, it.lda1, va, i0 + a, c0 + c) : T(0);
+    }
+  };
+  fetch(0);
+  load_chunk(A2s, A2, it.lda2, va, m, mp, c0, cw);
+  for (int bi = 0; bi < nblk; ++bi) {
+    const int blk = conjtrans ? bi : nblk - 1 - bi;
+    const int i0 = blk * ib, sb = min(ib, kk - i0);
+    // registers -> LDS (the previous block finished with Vs / Ts: apply_block ends with a barrier)
+#pragma unroll
+    for (int q = 0; q < QM_IB * QM_MR / 256; ++q) {
+      const int e = tid + 256 * q;
+      if (e < QM_IB * mp) Vs[e / mp][e % mp] = vreg[q];
+    }
+#pragma unroll
+    for (int q = 0; q < QM_IB * QM_IB / 256; ++q) {
+      const int e = tid + 256 * q;
+      Ts[e / QM_IB][e % QM_IB] = treg[q];
+    }
+    T a1cur[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a1cur[r] = areg[r];
     __syncthreads();
-    apply_block(A2s, Vs, Ws, Ts, mp, sb, conjtrans, A1, it.lda1, va, i0, c0, cw);
+    if (bi + 1 < nblk) fetch(bi + 1);  // in flight during this block's MFMA work
+    apply_block(A2s, Vs, Ws, Ts, mp, sb, conjtrans, A1, it.lda1, va, i0, c0, cw, a1cur);
   }
   store_chunk(A2s, A2, it.lda2, va, m, mp, c0, cw);
 }
@@ -212,23 +270,39 @@ __device__ inline T block_sum(T x, T* red4) {
 }
 
 // Factor one IB-column block held in Vs (column a = global column i0+a of the tile).
-//   geqrt (A1 == nullptr): rows r >= i0+a of column a form [alpha; x]; R part above.
-//   tsqrt: alpha = R1[a][a] (the A1 block, rows/cols i0..), x = Vs[a][0..mrows(a))
-//          with mrows(a) = tri ? min(m, i0+a+1) : m.
-// taus -> tau[a].  Reductions: (column c, row segment) partial sums in Red[8][33].
+//   geqrt (ts=false): column j's reflector acts on rows >= jr = i0+j: alpha = A(jr, j),
+//          x = rows > jr; the R part lies above.
+//   tsqrt: alpha = R1[j][j] (A1 diagonal block), x = Vs[j][0..re) with
+//          re = tri ? min(m, jr+1) : m.
+// Two barriers per column: phase 1 computes, per (column c, row segment), the
+// partial dot products d_c = sum x_r A(r, c) -- c = j gives ||x||^2 -- and
+// snapshots A(jr, c); phase 2 lets every thread derive tau / scale redundantly
+// and apply  A(r, c) -= v_r f_c  with  f_c = tau (A(jr, c) + scale d_c),
+// v_r = scale x_r, while the column-j threads scale x in place.  A segment's
+// rows belong to one wave, so a wave reads x_r before it overwrites it.
 template <typename T>
 __device__ inline void factor_block(T (*Vs)[QM_LDM], T (*R1)[QM_LDW], T (*Red)[33], T* tau, T* red4, int m, int i0,
                                     int sb, bool ts, bool tri) {
   const int tid = threadIdx.x;
-  const int cidx = tid & 31, seg = tid >> 5;
+  const int c = tid & 31, seg = tid >> 5;
+  (void)red4;
   for (int j = 0; j < sb; ++j) {
-    const int jr = i0 + j;                       // geqrt: pivot row of column j
-    const int rb = ts ? 0 : jr + 1;              // first row of x
+    const int jr = i0 + j;
+    const int rb = ts ? 0 : jr + 1;
     const int re = ts ? (tri ? min(m, jr + 1) : m) : m;
-    T part = T(0);
-    for (int r = rb + tid; r < re; r += 256) part += Vs[j][r] * Vs[j][r];
-    const T xn2 = block_sum(part, red4);
-    const T alpha = ts ? R1[j][j] : Vs[j][jr];
+    const int cc = j + c;
+    // ---- phase 1
+    T p = T(0);
+    if (cc < sb)
+      for (int r = rb + seg; r < re; r += 8) p += Vs[j][r] * Vs[cc][r];
+    Red[seg][c] = p;
+    if (seg == 0 && cc < sb) Red[8][c] = ts ? R1[j][cc] : Vs[cc][jr];
+    __syncthreads();
+    // ---- phase 2 (every thread: tau, scale)
+    T xn2 = T(0);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) xn2 += Red[q][0];
+    const T alpha = Red[8][0];
     T beta = alpha, tj = T(0), scal = T(0);
     if (xn2 != T(0)) {
       const T nrm = sqrt(alpha * alpha + xn2);
@@ -236,37 +310,28 @@ __device__ inline void factor_block(T (*Vs)[QM_LDM], T (*R1)[QM_LDW], T (*Red)[3
       tj = (beta - alpha) / beta;
       scal = T(1) / (alpha - beta);
     }
-    for (int r = rb + tid; r < re; r += 256) Vs[j][r] *= scal;
-    if (tid == 0) {
-      tau[j] = tj;
-      if (ts) R1[j][j] = beta;
-      else Vs[j][jr] = beta;
+    if (c != 0 && cc < sb) {
+      T d = T(0);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) d += Red[q][c];
+      const T f = tj * (Red[8][c] + scal * d);
+      const T fs = f * scal;
+      for (int r = rb + seg; r < re; r += 8) Vs[cc][r] -= Vs[j][r] * fs;
+      if (seg == 0) {
+        if (ts) R1[j][cc] -= f;
+        else Vs[cc][jr] -= f;
+      }
+    }
+    // after the reconvergence point: every lane of this wave has read x_r already
+    if (c == 0) {
+      for (int r = rb + seg; r < re; r += 8) Vs[j][r] *= scal;
+      if (seg == 0) {
+        tau[j] = tj;
+        if (ts) R1[j][j] = beta;
+        else Vs[j][jr] = beta;
+      }
     }
     __syncthreads();
-    // w_c = [R1(j,c)] + sum_r v_r A(r, c) for c in (j, sb); v has an implicit 1 at row jr (geqrt)
-    if (j + 1 < sb) {
-      T p = T(0);
-      const int c = j + 1 + cidx;
-      if (c < sb) {
-        for (int r = rb + seg; r < re; r += 8) p += Vs[j][r] * Vs[c][r];
-      }
-      Red[seg][cidx] = p;
-      __syncthreads();
-      if (tid < 32 && j + 1 + tid < sb) {
-        const int cc = j + 1 + tid;
-        T s = ts ? R1[j][cc] : Vs[cc][jr];
-        for (int q = 0; q < 8; ++q) s += Red[q][tid];
-        Red[8][tid] = tj * s;  // f_c = tau * w_c
-        if (ts) R1[j][cc] -= tj * s;
-        else Vs[cc][jr] -= tj * s;
-      }
-      __syncthreads();
-      for (int e = tid; e < (sb - j - 1) * (re - rb); e += 256) {
-        const int cc = j + 1 + e / (re - rb), r = rb + e % (re - rb);
-        Vs[cc][r] -= Vs[j][r] * Red[8][cc - j - 1];
-      }
-      __syncthreads();
-    }
   }
 }
 

@@ -98,9 +98,86 @@ py::array_t<int32_t> dag_versions(py::array_t<int64_t, py::array::c_style | py::
   return out;
 }
 
+// Full schedule analysis: levels, bottom levels (longest path to a sink) and
+// the deduplicated dependency edges.  Edges always point from an earlier to a
+// later task in program order, so the reverse program order is a reverse
+// topological order for the bottom-level pass.
+py::tuple dag_schedule(py::array_t<int64_t, py::array::c_style | py::array::forcecast> ops,
+                       py::array_t<uint8_t, py::array::c_style | py::array::forcecast> modes) {
+  if (ops.ndim() != 2 || modes.ndim() != 2 || ops.shape(0) != modes.shape(0) || ops.shape(1) != modes.shape(1))
+    throw std::invalid_argument("dag_schedule: ops and modes must be (ntasks, nroles) arrays of equal shape");
+  const int64_t n = ops.shape(0), R = ops.shape(1);
+  auto o = ops.unchecked<2>();
+  auto md = modes.unchecked<2>();
+  struct St {
+    int64_t writer = -1;           // last writing task
+    std::vector<int64_t> readers;  // readers since that write
+  };
+  std::vector<int32_t> level(n, 0), blevel(n, 0);
+  std::vector<int64_t> esrc, edst;
+  {
+    py::gil_scoped_release rel;
+    std::unordered_map<int64_t, St> st;
+    st.reserve(static_cast<size_t>(std::min<int64_t>(n * 2 + 16, 1 << 24)));
+    std::vector<int64_t> preds;
+    esrc.reserve(n * 3);
+    edst.reserve(n * 3);
+    for (int64_t t = 0; t < n; ++t) {
+      preds.clear();
+      for (int64_t r = 0; r < R; ++r) {
+        const uint8_t m = md(t, r);
+        if (!m) continue;
+        auto it = st.find(o(t, r));
+        if (it == st.end()) continue;
+        if (it->second.writer >= 0) preds.push_back(it->second.writer);
+        if (m & 2)
+          for (int64_t q : it->second.readers) preds.push_back(q);
+      }
+      std::sort(preds.begin(), preds.end());
+      preds.erase(std::unique(preds.begin(), preds.end()), preds.end());
+      int32_t L = 0;
+      for (int64_t p : preds) {
+        if (p == t) continue;
+        L = std::max(L, level[p] + 1);
+        esrc.push_back(p);
+        edst.push_back(t);
+      }
+      level[t] = L;
+      for (int64_t r = 0; r < R; ++r) {
+        const uint8_t m = md(t, r);
+        if (!m) continue;
+        St& s = st[o(t, r)];
+        if (m & 2) {
+          s.writer = t;
+          s.readers.clear();
+        } else {
+          s.readers.push_back(t);
+        }
+      }
+    }
+    // bottom levels: iterate edges in reverse destination order
+    std::vector<int64_t> order(esrc.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = static_cast<int64_t>(i);
+    // edges were appended grouped by increasing destination: walking them backwards is reverse-topological
+    for (int64_t i = static_cast<int64_t>(esrc.size()) - 1; i >= 0; --i) {
+      const int64_t s = esrc[i], d = edst[i];
+      blevel[s] = std::max(blevel[s], blevel[d] + 1);
+    }
+  }
+  py::array_t<int32_t> lv(n), bl(n);
+  py::array_t<int64_t> es(static_cast<int64_t>(esrc.size())), ed(static_cast<int64_t>(edst.size()));
+  std::copy(level.begin(), level.end(), lv.mutable_data());
+  std::copy(blevel.begin(), blevel.end(), bl.mutable_data());
+  std::copy(esrc.begin(), esrc.end(), es.mutable_data());
+  std::copy(edst.begin(), edst.end(), ed.mutable_data());
+  return py::make_tuple(lv, bl, es, ed);
+}
+
 }  // namespace
 
 void register_dag(py::module_& m) {
+  m.def("dag_schedule", &dag_schedule, py::arg("ops"), py::arg("modes"),
+        "(level, bottom level, edge sources, edge destinations) of a program-order tile DAG");
   m.def("dag_levels", &dag_levels, py::arg("ops"), py::arg("modes"),
         "Level (0-based) of every task of a program-order tile DAG under RAW/WAR/WAW hazards");
   m.def("dag_versions", &dag_versions, py::arg("ops"), py::arg("modes"),

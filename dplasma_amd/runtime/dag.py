@@ -49,6 +49,9 @@ assert DAG_ITEM.itemsize == 64
 
 R, W, RW = 1, 2, 3
 
+MULTISTREAM = True  # single-GPU DAGs: critical-path stream + bulk stream
+CRIT_SLACK = 0      # tasks with at most this much slack (levels) go to the critical stream
+
 _MID_SHIFT, _M_SHIFT = 44, 22
 _MASK22 = (1 << 22) - 1
 
@@ -239,7 +242,15 @@ class TileDAG:
             p += n
         self._chunks = []
         rt = _lib_rt()
-        level = rt.dag_levels(ops, modes) if rt is not None else _levels_py(ops, modes)
+        # single process on a GPU: dataflow over two streams (critical path / bulk)
+        multistream = world == 1 and ctx.device.type == "cuda" and rt is not None and MULTISTREAM
+        crit = None
+        if multistream:
+            level, blevel, esrc, edst = rt.dag_schedule(ops, modes)
+            depth = level.astype(np.int64) + blevel
+            crit = (depth.max() - depth) <= CRIT_SLACK
+        else:
+            level = rt.dag_levels(ops, modes) if rt is not None else _levels_py(ops, modes)
         nlev = int(level.max()) + 1
         # executor rank per task
         exec_key = ops[np.arange(ntask), np.array([self.kinds[k].exec_role for k in range(len(self.kinds))])[kid]]
@@ -306,21 +317,23 @@ class TileDAG:
                 ld[~loc] = np.array([self.mats[i].mb for i in range(len(self.mats))], dtype=np.int32)[mid[~loc]]
             return bidx, off, ld
 
-        # ---------------- my launches, grouped by (level, kind prio, kind)
+        # ---------------- my launches, grouped by (level, critical first, kind prio, kind)
         mine_t = np.nonzero(exe == me)[0] if world > 1 else np.arange(ntask)
-        order = np.lexsort((mine_t, kid[mine_t], np.array([self.kinds[k].prio for k in range(len(self.kinds))])[kid[mine_t]],
-                            level[mine_t]))
+        prio = np.array([self.kinds[k].prio for k in range(len(self.kinds))])[kid[mine_t]]
+        cflag = (~crit[mine_t]).astype(np.int64) if crit is not None else np.zeros(len(mine_t), dtype=np.int64)
+        order = np.lexsort((mine_t, kid[mine_t], prio, cflag, level[mine_t]))
         mine_t = mine_t[order]
-        launches = defaultdict(list)  # level -> [(kind, item slice / cpu refs)]
+        groups = []  # execution order: dict(K, start, n, cpu_refs, ext, emax, level, stream)
         all_items = []
         nitems_total = 0
         if len(mine_t):
             lv, kk = level[mine_t], kid[mine_t]
-            brk = np.nonzero((lv[1:] != lv[:-1]) | (kk[1:] != kk[:-1]))[0] + 1
+            cf = cflag[order]
+            brk = np.nonzero((lv[1:] != lv[:-1]) | (kk[1:] != kk[:-1]) | (cf[1:] != cf[:-1]))[0] + 1
             starts = np.concatenate([[0], brk])
             ends = np.concatenate([brk, [len(mine_t)]])
             items = np.zeros(len(mine_t), dtype=DAG_ITEM)
-            ptrs = [b.data_ptr() for b in bases]
+            ptr_arr = np.array([b.data_ptr() for b in bases] + [0], dtype=np.uint64)
             refs_all = []
             for r in range(nR):
                 keys = ops[mine_t, r]
@@ -331,14 +344,13 @@ class TileDAG:
                 if ok.any():
                     b[ok], o[ok], l[ok] = resolve(keys[ok])
                 refs_all.append((b, o, l))
-            # role -> pointer slot per kind
-            for s, e in zip(starts, ends):
+            gid_of_task = np.zeros(ntask, dtype=np.int64)
+            for g, (s, e) in enumerate(zip(starts, ends)):
                 K = self.kinds[int(kk[s])]
                 seg = items[s:e]
                 for r, (_, _, slot) in enumerate(K.roles):
                     b, o, l = (x[s:e] for x in refs_all[r])
-                    addr = np.array([ptrs[int(bi)] if bi >= 0 else 0 for bi in b], dtype=np.uint64) + \
-                        (o * esize).astype(np.uint64)
+                    addr = ptr_arr[b] + (o * esize).astype(np.uint64)  # b == -1 -> trailing 0 entry
                     addr[b < 0] = 0
                     seg[f"p{slot}"] = addr
                     seg[f"ld{slot}"] = l
@@ -349,7 +361,25 @@ class TileDAG:
                                   int(refs_all[r][1][i]), int(refs_all[r][2][i])) for r in range(len(K.roles))]
                                 for i in range(s, e)]
                 ex = ext[mine_t[s:e]]
-                launches[int(lv[s])].append((K, int(s), int(e - s), cpu_refs, ex, tuple(int(x) for x in ex.max(0))))
+                gid_of_task[mine_t[s:e]] = g
+                groups.append(dict(K=K, start=int(s), n=int(e - s), cpu_refs=cpu_refs, ext=ex,
+                                   emax=tuple(int(x) for x in ex.max(0)), level=int(lv[s]),
+                                   stream="panel" if (multistream and cf[s] == 0) else "update",
+                                   waits=[], record=False))
+            if multistream and len(esrc):
+                gs, gd = gid_of_task[esrc], gid_of_task[edst]
+                st_code = np.array([0 if g["stream"] == "panel" else 1 for g in groups], dtype=np.int64)
+                sel = st_code[gs] != st_code[gd]
+                if sel.any():
+                    pairs = np.unique(np.stack([gd[sel], gs[sel]], 1), axis=0)
+                    # per destination group, only the latest source group of the other stream matters
+                    last = {}
+                    for d, s_ in pairs:
+                        if s_ > last.get(int(d), -1):
+                            last[int(d)] = int(s_)
+                    for d, s_ in last.items():
+                        groups[d]["waits"].append(s_)
+                        groups[s_]["record"] = True
             all_items = items
             nitems_total = len(items)
         dev_items = None
@@ -403,28 +433,31 @@ class TileDAG:
                 (pk, _), (uk, _), sc, rc = xplan(rows, phase == "f")
                 xch[(L, phase)] = (copy_plan(pk, phase == "f", True), copy_plan(uk, phase == "w", False), sc, rc)
         self._bases = bases
-        prog = _DagProgram(self, nlev, launches, xch, nbe, dtype, device)
+        prog = _DagProgram(self, nlev, groups, xch, nbe, dtype, device, multistream)
         tp.task(self.name, "update", prog.run)
         tp.dag = prog
         return tp.finish_build()
 
 
 class _DagProgram:
-    def __init__(self, dag: TileDAG, nlev, launches, xch, nbe, dtype, device):
+    def __init__(self, dag: TileDAG, nlev, groups, xch, nbe, dtype, device, multistream):
         self.dag = dag
         self.nlev = nlev
-        self.launches = launches
+        self.groups = groups
+        self.by_level = defaultdict(list)
+        for i, g in enumerate(groups):
+            self.by_level[g["level"]].append(i)
         self.xch = xch
         self.nbe = nbe
         self.dtype, self.device = dtype, device
-        self.nlaunch = sum(len(v) for v in launches.values())
+        self.multistream = multistream
+        self.nlaunch = len(groups)
 
     def _exchange(self, plan):
         from ..constants import dplasmaNoTrans
         from ..ops import tile_ops as ops
         pack, unpack, sc, rc = plan
         bases = self.dag._bases
-        nbe = self.nbe
         sendbuf = torch.empty(sum(sc), dtype=self.dtype, device=self.device)
         recvbuf = torch.empty(sum(rc), dtype=self.dtype, device=self.device)
         for bi, ld, mb, tb in pack:   # tile (base, off, ld) -> sendbuf[i*nbe] (ld = mb)
@@ -434,9 +467,19 @@ class _DagProgram:
         for bi, ld, mb, tb in unpack:  # recvbuf[i*nbe] -> tile
             _swap_copy(ops, recvbuf, mb, bases[bi], ld, tb)
 
+    def _launch(self, g, dev_items, stream_ptr):
+        K = g["K"]
+        if dev_items is not None:
+            K.gpu(dev_items.data_ptr() + g["start"] * DAG_ITEM.itemsize, g["n"], stream_ptr, g["emax"])
+        else:
+            for refs, e in zip(g["cpu_refs"], g["ext"]):
+                K.cpu(refs, (int(e[0]), int(e[1]), int(e[2])))
+
     def run(self):
         dag = self.dag
         dev_items = dag.dev_items
+        if self.multistream and dev_items is not None:
+            return self._run_streams(dev_items)
         stream = None
         if self.device.type == "cuda":
             from ..ops import _lib
@@ -445,15 +488,37 @@ class _DagProgram:
             x = self.xch.get((L, "f"))
             if x is not None:
                 self._exchange(x)
-            for (K, start, n, cpu_refs, ext, emax) in self.launches.get(L, ()):
-                if dev_items is not None:
-                    K.gpu(dev_items.data_ptr() + start * DAG_ITEM.itemsize, n, stream, emax)
-                else:
-                    for refs, e in zip(cpu_refs, ext):
-                        K.cpu(refs, (int(e[0]), int(e[1]), int(e[2])))
+            for gi in self.by_level.get(L, ()):
+                self._launch(self.groups[gi], dev_items, stream)
             x = self.xch.get((L, "w"))
             if x is not None:
                 self._exchange(x)
+
+    def _run_streams(self, dev_items):
+        """Dataflow over two streams: zero-slack (critical-path) groups on a
+        high-priority stream, bulk groups on the other; cross-stream group
+        dependencies become event waits."""
+        ctx = self.dag.ctx
+        cur = torch.cuda.current_stream(ctx.device)
+        streams = {"panel": ctx.streams["panel"], "update": ctx.streams["update"]}
+        start = torch.cuda.Event()
+        start.record(cur)
+        for s in streams.values():
+            s.wait_event(start)
+        events = {}
+        for gi, g in enumerate(self.groups):
+            s = streams[g["stream"]]
+            for w in g["waits"]:
+                s.wait_event(events[w])
+            self._launch(g, dev_items, s.cuda_stream)
+            if g["record"]:
+                ev = torch.cuda.Event()
+                ev.record(s)
+                events[gi] = ev
+        for s in streams.values():
+            ev = torch.cuda.Event()
+            ev.record(s)
+            cur.wait_event(ev)
 
 
 def _swap_copy(ops, src, src_ld, dst, dst_ld, tb):
