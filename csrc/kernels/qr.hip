@@ -27,8 +27,10 @@ struct QrItem {
   long long a1, a2, v, t;  // addresses of A (or A1), A2, V (V2), T tile
   int lda1, lda2, ldv, ldt;
   int m, n, k, pad;        // problem extents (meaning per kernel)
+  long long p4, p5;        // extra operand slots (DAG_ITEM tail, unused here)
+  int ld4, ld5, aux0, aux1;
 };
-static_assert(sizeof(QrItem) == 64, "QrItem layout");
+static_assert(sizeof(QrItem) == 96, "QrItem layout = DAG_ITEM");
 
 template <typename T>
 __device__ inline T vget(const T* b, int ld, View v, int i, int j) {

@@ -29,7 +29,10 @@ struct QrItemM {
   long long a1, a2, v, t;
   int lda1, lda2, ldv, ldt;
   int m, n, k, pad;
+  long long p4, p5;
+  int ld4, ld5, aux0, aux1;
 };
+static_assert(sizeof(QrItemM) == 96, "QrItemM layout = DAG_ITEM");
 
 template <typename T>
 __device__ inline T vld(const T* b, int ld, View2 v, int i, int j) {

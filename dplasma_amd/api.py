@@ -14,6 +14,7 @@ from .models import aux as _aux
 from .models import blas3 as _blas3
 from .models import cholesky as _chol
 from .models import lu as _lu
+from .models import lu_incpiv as _lui
 from .models import qr as _qr
 from .models import qrtree as _qrtree
 from .models import check as _check
@@ -60,6 +61,11 @@ _GENERIC = {
     "laswp": _lu.laswp, "getrs": _lu.getrs, "gesv_1d": _lu.gesv_1d, "gesv": _lu.gesv_1d,
     "getrs_nopiv": _lu.getrs_nopiv, "gesv_nopiv": _lu.gesv_nopiv,
     "ipiv_descriptor": _lu.ipiv_descriptor,
+    # LU with incremental pivoting
+    "getrf_incpiv": _lui.getrf_incpiv, "getrf_incpiv_New": _lui.getrf_incpiv_New,
+    "trsmpl_incpiv": _lui.trsmpl_incpiv, "trsmpl_incpiv_New": _lui.trsmpl_incpiv_New,
+    "gesv_incpiv": _lui.gesv_incpiv,
+    "incpiv_L_descriptor": _lui.L_descriptor, "incpiv_ipiv_descriptor": _lui.ipiv_descriptor,
     # QR / LQ (flat trees)
     "geqrf": _qr.geqrf, "geqrf_New": _qr.geqrf_New, "gelqf": _qr.gelqf, "gelqf_New": _qr.gelqf_New,
     "unmqr": _qr.unmqr, "unmqr_New": _qr.unmqr_New, "unmlq": _qr.unmlq, "unmlq_New": _qr.unmlq_New,

@@ -53,6 +53,11 @@ _SIGS = {
     "dpl_qr_apply_mfma_ok": [c_int, c_int, c_int],
     # prec, nitems, items, a_tr, ib, ts, tri, stream
     "dpl_qr_panel_mfma": [c_int, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp],
+    # LU incremental pivoting on DAG items (csrc/kernels/lu_incpiv.hip)
+    "dpl_getrf_tile": [c_int, c_int, c_vp, c_vp, c_vp],               # prec, n, items, info*, stream
+    "dpl_gessm": [c_int, c_int, c_vp, c_int, c_vp],                   # prec, n, items, max_n, stream
+    "dpl_ssssm": [c_int, c_int, c_vp, c_int, c_int, c_int, c_vp],     # + ib, NB
+    "dpl_tstrf": [c_int, c_int, c_vp, c_int, c_int, c_int, c_vp, c_vp],  # prec, n, items, ib, NB, max_m, info*, stream
     # prec, kind, part, unit, nitems, items, A, lda, out, ostride, stream
     "dpl_tile_norm": [c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_int, c_vp],
 }
@@ -88,8 +93,21 @@ def load(build_if_missing: bool = True):
                 raise
             f.argtypes = args
             f.restype = c_int
-        _LIB = lib
-        return lib
+        _LIB = _Declared(lib)
+        return _LIB
+
+
+class _Declared:
+    """Exposes only the exports listed in _SIGS: calling an export without a
+    declared signature would pass 64-bit pointers as C ints."""
+
+    def __init__(self, lib):
+        self._lib = lib
+
+    def __getattr__(self, name):
+        if name not in _SIGS:
+            raise AttributeError(f"{name}: no ctypes signature declared in dplasma_amd/ops/_lib.py")
+        return getattr(self._lib, name)
 
 
 def available() -> bool:

@@ -23,8 +23,8 @@ MI355X:
   (RCCL p2p over xGMI), planned identically on every rank from replicated
   metadata; levels without traffic do no collective at all.
 
-Items carry absolute device addresses (``DAG_ITEM``, 64 bytes, layout of
-``QrItem`` in ``csrc/kernels/qr.hip``) so one launch can mix tiles living in
+Items carry absolute device addresses (``DAG_ITEM``, 96 bytes: six operand
+slots, layout of ``QrItem`` in ``csrc/kernels/qr.hip``) so one launch can mix tiles living in
 descriptor storage and in the slot arena.  All items are built and uploaded
 once at compile time ("ENQ" phase, excluded from timing as in
 ``tests/common.h:252-277``).
@@ -44,8 +44,10 @@ from .taskpool import Taskpool
 
 DAG_ITEM = np.dtype([("p0", "<u8"), ("p1", "<u8"), ("p2", "<u8"), ("p3", "<u8"),
                      ("ld0", "<i4"), ("ld1", "<i4"), ("ld2", "<i4"), ("ld3", "<i4"),
-                     ("m", "<i4"), ("n", "<i4"), ("k", "<i4"), ("pad", "<i4")])
-assert DAG_ITEM.itemsize == 64
+                     ("m", "<i4"), ("n", "<i4"), ("k", "<i4"), ("pad", "<i4"),
+                     ("p4", "<u8"), ("p5", "<u8"),
+                     ("ld4", "<i4"), ("ld5", "<i4"), ("aux0", "<i4"), ("aux1", "<i4")])
+assert DAG_ITEM.itemsize == 96
 
 R, W, RW = 1, 2, 3
 
@@ -66,7 +68,7 @@ def _root(M):
 class Kind:
     """A tile-kernel family usable in a DAG.
 
-    roles: tuple of (role name, access mode, item pointer slot 0..3)
+    roles: tuple of (role name, access mode, item pointer slot 0..5)
     exec_role: index of the role whose home rank executes the task
     gpu(items_dev_ptr, nitems, stream_ptr, emax): one batched launch; emax = max (m, n, k) over the items
     cpu(refs, ext): reference execution of one task; refs[r] = (tensor, offset, ld)
@@ -286,18 +288,30 @@ class TileDAG:
                 for i in np.nonzero(w_r)[0]:
                     wback_at[int(l_r[i])].append((int(e_r[i]), int(h_r[i]), int(k_r[i])))
                 mine = np.unique(k_r[e_r == me])
-                for s, k in enumerate(mine.tolist()):
-                    slot_of[k] = s
-        # slot arena (one slot per remote tile this rank touches)
-        nbe = max(M.mb * M.nb for M in self.mats)
-        dtype = self.mats[0].dtype
-        for M in self.mats:
-            if M.dtype != dtype:
-                raise TypeError("all matrices of a DAG must share one dtype")
+                cnt = defaultdict(int)
+                for k in mine.tolist():
+                    dt = self.mats[k >> _MID_SHIFT].dtype
+                    slot_of[k] = cnt[dt]
+                    cnt[dt] += 1
+        # slot arenas: one per dtype (IPIV-like integer descriptors get their own),
+        # one slot per remote tile this rank touches
+        dtypes = sorted({M.dtype for M in self.mats}, key=str)
+        nbe_of = {dt: max(M.mb * M.nb for M in self.mats if M.dtype == dt) for dt in dtypes}
+        nslots = defaultdict(int)
+        for k, s_ in slot_of.items():
+            dt = self.mats[k >> _MID_SHIFT].dtype
+            nslots[dt] = max(nslots[dt], s_ + 1)
         device = ctx.device
-        self.arena = torch.zeros(max(len(slot_of), 1) * nbe, dtype=dtype, device=device) if slot_of else None
-        bases = [M.data for M in self.mats] + ([self.arena] if self.arena is not None else [])
-        esize = torch.empty(0, dtype=dtype).element_size()
+        self.arenas = {dt: torch.zeros(nslots[dt] * nbe_of[dt], dtype=dt, device=device) for dt in dtypes
+                       if nslots[dt]}
+        arena_base = {}
+        bases = [M.data for M in self.mats]
+        for dt, ar in self.arenas.items():
+            arena_base[dt] = len(bases)
+            bases.append(ar)
+        esz = np.array([b.element_size() for b in bases] + [0], dtype=np.uint64)
+        mat_dt = [M.dtype for M in self.mats]
+        dtype = self.mats[0].dtype
 
         def resolve(keys):
             """keys (n,) -> (base index, element offset, ld) arrays for this rank."""
@@ -311,9 +325,10 @@ class TileDAG:
                 off[loc] = self._local_offsets(keys[loc])
                 ld[loc] = np.array([self.mats[i].ld for i in range(len(self.mats))], dtype=np.int32)[mid[loc]]
             if (~loc).any():
-                sl = np.array([slot_of[int(k)] for k in keys[~loc]], dtype=np.int64)
-                off[~loc] = sl * nbe
-                bidx[~loc] = len(self.mats)
+                rk = keys[~loc]
+                dts = [mat_dt[int(k >> _MID_SHIFT)] for k in rk]
+                off[~loc] = np.array([slot_of[int(k)] * nbe_of[dt] for k, dt in zip(rk, dts)], dtype=np.int64)
+                bidx[~loc] = np.array([arena_base[dt] for dt in dts], dtype=np.int64)
                 ld[~loc] = np.array([self.mats[i].mb for i in range(len(self.mats))], dtype=np.int32)[mid[~loc]]
             return bidx, off, ld
 
@@ -350,7 +365,7 @@ class TileDAG:
                 seg = items[s:e]
                 for r, (_, _, slot) in enumerate(K.roles):
                     b, o, l = (x[s:e] for x in refs_all[r])
-                    addr = ptr_arr[b] + (o * esize).astype(np.uint64)  # b == -1 -> trailing 0 entry
+                    addr = ptr_arr[b] + o.astype(np.uint64) * esz[b]  # b == -1 -> trailing 0 entries
                     addr[b < 0] = 0
                     seg[f"p{slot}"] = addr
                     seg[f"ld{slot}"] = l
@@ -389,9 +404,9 @@ class TileDAG:
             self._host_items = host
         self.dev_items = dev_items
 
-        # ---------------- exchange plans
-        def xplan(rows, fetch: bool):
-            """rows: (src, dst, key) for one level -> my pack/unpack lists and split sizes."""
+        # ---------------- exchange plans (one all_to_all per level, phase and dtype)
+        def xplan(rows, nbe):
+            """rows: (src, dst, key) -> my send keys, my receive keys, split sizes (elements)."""
             rows = sorted(rows, key=lambda x: (x[0], x[1], x[2]))
             sends = [r for r in rows if r[0] == me]
             recvs = [r for r in rows if r[1] == me]
@@ -401,26 +416,25 @@ class TileDAG:
                 sc[d_] += nbe
             for s_, d_, _ in recvs:
                 rc[s_] += nbe
-            if fetch:   # home storage -> arena slot
-                pk = [k for (_, _, k) in sends]
-                uk = [k for (_, _, k) in recvs]
-                return (pk, True), (uk, False), sc, rc
-            # write-back: arena slot -> home storage
-            return ([k for (_, _, k) in sends], False), ([k for (_, _, k) in recvs], True), sc, rc
+            return [k for (_, _, k) in sends], [k for (_, _, k) in recvs], sc, rc
 
-        def copy_plan(keys, from_home: bool, to_buf: bool):
-            """Batched tile copies between (home storage | arena) and a contiguous buffer."""
+        def copy_plan(keys, nbe):
+            """Tile copies between their current place (home storage | arena) and a buffer."""
             from ..ops.batch import TileBatch
             groups = {}
             if not keys:
                 return []
             b, o, l = resolve(np.array(keys, dtype=np.int64))
             for i, k in enumerate(keys):
-                mid = k >> _MID_SHIFT
-                M = self.mats[mid]
+                M = self.mats[k >> _MID_SHIFT]
                 gm, gn = (k >> _M_SHIFT) & _MASK22, k & _MASK22
-                rows = min(M.mb, M.lm - gm * M.mb)
-                cols = min(M.nb, M.ln - gn * M.nb)
+                if M.storage == STORAGE_TILE:
+                    # full physical tile: kernels may use storage past a ragged edge
+                    # (TSTRF writes one pivot per panel column into an IPIV tile)
+                    rows, cols = M.mb, M.nb
+                else:
+                    rows = min(M.mb, M.lm - gm * M.mb)
+                    cols = min(M.nb, M.ln - gn * M.nb)
                 g = groups.setdefault((int(b[i]), int(l[i]), M.mb), TileBatch())
                 g.add(int(o[i]), rows, cols, b_off=i * nbe)
             return [(bi, ldx, mb, tb.finalize()) for (bi, ldx, mb), tb in groups.items()]
@@ -430,17 +444,23 @@ class TileDAG:
             for phase, rows in (("f", fetch_at.get(L)), ("w", wback_at.get(L))):
                 if not rows:
                     continue
-                (pk, _), (uk, _), sc, rc = xplan(rows, phase == "f")
-                xch[(L, phase)] = (copy_plan(pk, phase == "f", True), copy_plan(uk, phase == "w", False), sc, rc)
+                plans = []
+                for dt in dtypes:
+                    r_dt = [r for r in rows if mat_dt[r[2] >> _MID_SHIFT] == dt]
+                    if not r_dt:
+                        continue
+                    pk, uk, sc, rc = xplan(r_dt, nbe_of[dt])
+                    plans.append((dt, copy_plan(pk, nbe_of[dt]), copy_plan(uk, nbe_of[dt]), sc, rc))
+                xch[(L, phase)] = plans
         self._bases = bases
-        prog = _DagProgram(self, nlev, groups, xch, nbe, dtype, device, multistream)
+        prog = _DagProgram(self, nlev, groups, xch, dtype, device, multistream)
         tp.task(self.name, "update", prog.run)
         tp.dag = prog
         return tp.finish_build()
 
 
 class _DagProgram:
-    def __init__(self, dag: TileDAG, nlev, groups, xch, nbe, dtype, device, multistream):
+    def __init__(self, dag: TileDAG, nlev, groups, xch, dtype, device, multistream):
         self.dag = dag
         self.nlev = nlev
         self.groups = groups
@@ -448,24 +468,21 @@ class _DagProgram:
         for i, g in enumerate(groups):
             self.by_level[g["level"]].append(i)
         self.xch = xch
-        self.nbe = nbe
         self.dtype, self.device = dtype, device
         self.multistream = multistream
         self.nlaunch = len(groups)
 
-    def _exchange(self, plan):
-        from ..constants import dplasmaNoTrans
-        from ..ops import tile_ops as ops
-        pack, unpack, sc, rc = plan
+    def _exchange(self, plans):
         bases = self.dag._bases
-        sendbuf = torch.empty(sum(sc), dtype=self.dtype, device=self.device)
-        recvbuf = torch.empty(sum(rc), dtype=self.dtype, device=self.device)
-        for bi, ld, mb, tb in pack:   # tile (base, off, ld) -> sendbuf[i*nbe] (ld = mb)
-            ops.geadd(0, dplasmaNoTrans, 1.0, bases[bi], ld, 0.0, sendbuf, mb, tb, copy=True)
-        # every rank joins: the plan exists on all ranks whenever the level has any traffic
-        dist.all_to_all_single(recvbuf, sendbuf, output_split_sizes=rc, input_split_sizes=sc)
-        for bi, ld, mb, tb in unpack:  # recvbuf[i*nbe] -> tile
-            _swap_copy(ops, recvbuf, mb, bases[bi], ld, tb)
+        for dt, pack, unpack, sc, rc in plans:
+            sendbuf = torch.empty(sum(sc), dtype=dt, device=self.device)
+            recvbuf = torch.empty(sum(rc), dtype=dt, device=self.device)
+            for bi, ld, mb, tb in pack:   # tile (base, off, ld) -> sendbuf[i*nbe] (ld = mb)
+                copy_tiles(bases[bi], ld, sendbuf, mb, tb, to_b=True)
+            # every rank joins: the plan exists on all ranks whenever the level has this traffic
+            dist.all_to_all_single(recvbuf, sendbuf, output_split_sizes=rc, input_split_sizes=sc)
+            for bi, ld, mb, tb in unpack:  # recvbuf[i*nbe] -> tile
+                copy_tiles(bases[bi], ld, recvbuf, mb, tb, to_b=False)
 
     def _launch(self, g, dev_items, stream_ptr):
         K = g["K"]
@@ -521,16 +538,30 @@ class _DagProgram:
             cur.wait_event(ev)
 
 
-def _swap_copy(ops, src, src_ld, dst, dst_ld, tb):
-    """Copy tiles src[b_off] (ld src_ld) -> dst[a_off] (ld dst_ld) for a TileBatch keyed (a=dst, b=src)."""
-    from ..ops.batch import TileBatch
+def copy_tiles(A, lda, B, ldb, tb, to_b: bool):
+    """Copy the tiles of a TileBatch (a_off in A, b_off in B) A -> B (to_b) or B -> A.
+
+    Floating-point tiles use the batched copy kernel; integer tiles (pivot
+    vectors) are tiny and copied with tensor views."""
     from ..constants import dplasmaNoTrans
-    sw = getattr(tb, "_swapped", None)
-    if sw is None:
-        sw = TileBatch()
-        tb.finalize()
-        for it in tb.items:
-            sw.add(int(it["b_off"]), int(it["m"]), int(it["n"]), b_off=int(it["a_off"]))
-        sw.finalize()
-        tb._swapped = sw
-    ops.geadd(0, dplasmaNoTrans, 1.0, src, src_ld, 0.0, dst, dst_ld, sw, copy=True)
+    from ..ops import tile_ops as ops
+    from ..ops.batch import TileBatch
+    tb.finalize()
+    if A.dtype.is_floating_point or A.dtype.is_complex:
+        if to_b:
+            ops.geadd(0, dplasmaNoTrans, 1.0, A, lda, 0.0, B, ldb, tb, copy=True)
+            return
+        sw = getattr(tb, "_swapped", None)
+        if sw is None:
+            sw = TileBatch()
+            for it in tb.items:
+                sw.add(int(it["b_off"]), int(it["m"]), int(it["n"]), b_off=int(it["a_off"]))
+            sw.finalize()
+            tb._swapped = sw
+        ops.geadd(0, dplasmaNoTrans, 1.0, B, ldb, 0.0, A, lda, sw, copy=True)
+        return
+    for it in tb.items:
+        m, n = int(it["m"]), int(it["n"])
+        a = torch.as_strided(A, (m, n), (1, lda), int(it["a_off"]))
+        b = torch.as_strided(B, (m, n), (1, ldb), int(it["b_off"]))
+        (b if to_b else a).copy_(a if to_b else b)
