@@ -61,6 +61,9 @@ _GENERIC = {
     "laswp": _lu.laswp, "getrs": _lu.getrs, "gesv_1d": _lu.gesv_1d, "gesv": _lu.gesv_1d,
     "getrs_nopiv": _lu.getrs_nopiv, "gesv_nopiv": _lu.gesv_nopiv,
     "ipiv_descriptor": _lu.ipiv_descriptor,
+    "getrf_ptgpanel": _lu.getrf_ptgpanel, "getrf_ptgpanel_New": _lu.getrf_ptgpanel_New,
+    "trsmpl_ptgpanel": _lu.trsmpl_ptgpanel, "ptgpanel_ipiv_descriptor": _lu.ptgpanel_ipiv_descriptor,
+    "gerfs": _lu.gerfs,
     # LU with incremental pivoting
     "getrf_incpiv": _lui.getrf_incpiv, "getrf_incpiv_New": _lui.getrf_incpiv_New,
     "trsmpl_incpiv": _lui.trsmpl_incpiv, "trsmpl_incpiv_New": _lui.trsmpl_incpiv_New,

@@ -27,6 +27,8 @@ from ..constants import (DPLASMA_ERR_NOT_SUPPORTED, dplasmaLeft, dplasmaLower, d
 from ..descriptor import TiledMatrix
 from ..ops import tile_ops as ops
 from ..ops.batch import GemmBatch, TileBatch
+import torch.distributed as dist
+
 from ..parallel import comm
 from ..runtime import Taskpool
 from ..runtime.tileprog import TileProgram
@@ -194,10 +196,212 @@ class _Getrf1D:
                 ops.gemm(N_, N_, -1.0, pv, mp, A.data, A.ld, 1.0, A.data, A.ld, gb)
 
 
+def _permute_rows_2d(ctx, A, dst_rows, src_rows, coltiles):
+    """A[dst_rows[i], tiles] := A_old[src_rows[i], tiles] (global element rows of the view) on a P x Q grid.
+
+    Rows live on process rows ``prow(row // mb)``; for one process column all
+    ranks agree on the move lists (they depend only on the replicated pivots),
+    so moves across process rows are ONE all-to-all inside the process-column
+    group (RCCL p2p), local moves are two row-gather launches.  All sources are
+    read before any destination is written (the moves form a permutation)."""
+    if len(dst_rows) == 0:
+        return
+    mb, nb = A.mb, A.nb
+    g, myrow = A.grid, A.myrow
+    P = g.P
+    prow = lambda r: g.prow(r // mb + A.it0)  # noqa: E731
+    coltiles = list(coltiles)
+    dst_p = np.array([prow(int(r)) for r in dst_rows])
+    src_p = np.array([prow(int(r)) for r in src_rows])
+    local = np.nonzero((dst_p == myrow) & (src_p == myrow))[0]
+    sends = [np.nonzero((src_p == myrow) & (dst_p == q))[0] for q in range(P)]
+    recvs = [np.nonzero((dst_p == myrow) & (src_p == q))[0] for q in range(P)]
+    for q in range(P):
+        if q == myrow:
+            sends[q] = recvs[q] = np.zeros(0, dtype=np.int64)
+    cross = P > 1 and any(((src_p != dst_p)).tolist())
+    nct = len(coltiles)
+
+    def off(r, n):
+        return A.offset(r // mb, n) + r % mb
+
+    def pairs(idx_rows, slot0, to_buf):
+        """(row_gather pairs per width group): slot j holds one tile row of nb elements."""
+        out = {}
+        for j, r in enumerate(idx_rows):
+            for c, n in enumerate(coltiles):
+                w = A.tile_cols(n)
+                slot = (slot0 + j * nct + c) * nb
+                pr = (slot, off(int(r), n)) if to_buf else (off(int(r), n), slot)
+                out.setdefault(w, []).append(pr)
+        return {w: np.array(v, dtype=ops.ROW_PAIR) for w, v in out.items()}
+
+    dev, dt = A.device, A.dtype
+    tmp = torch.empty(max(1, len(local) * nct) * nb, dtype=dt, device=dev)
+    if len(local) and nct:
+        for w, pr in pairs(src_rows[local], 0, True).items():
+            ops.row_gather(tmp, A.data, pr, w, 1, A.ld)
+    if cross:
+        scount = [len(s) * nct * nb for s in sends]
+        rcount = [len(r) * nct * nb for r in recvs]
+        sbuf = torch.empty(sum(scount), dtype=dt, device=dev)
+        rbuf = torch.empty(sum(rcount), dtype=dt, device=dev)
+        slot = 0
+        for q in range(P):
+            if len(sends[q]) and nct:
+                for w, pr in pairs(src_rows[sends[q]], slot, True).items():
+                    ops.row_gather(sbuf, A.data, pr, w, 1, A.ld)
+            slot += len(sends[q]) * nct
+        dist.all_to_all_single(rbuf, sbuf, output_split_sizes=rcount, input_split_sizes=scount,
+                               group=ctx.col_group)
+    if len(local) and nct:
+        for w, pr in pairs(dst_rows[local], 0, False).items():
+            ops.row_gather(A.data, tmp, pr, w, A.ld, 1)
+    if cross:
+        slot = 0
+        for q in range(P):
+            if len(recvs[q]) and nct:
+                for w, pr in pairs(dst_rows[recvs[q]], slot, False).items():
+                    ops.row_gather(A.data, rbuf, pr, w, A.ld, 1)
+            slot += len(recvs[q]) * nct
+
+
+class _GetrfPtg:
+    """Partial-pivoting LU on a P x Q grid (getrf_ptgpanel role, src/zgetrf_ptgpanel.jdf).
+
+    Step k: the panel's tiles are summed into one buffer inside their process
+    column (all-reduce over P ranks) and factored redundantly there (pivot
+    search over the whole column, ``GETRF_MAX/RDC/SND`` of the reference); the
+    factored panel and pivots are broadcast along process rows; interchanges
+    cross process rows through one all-to-all per process column (``SWAP_*``);
+    the U block row is solved where it lives, broadcast down process columns,
+    and the trailing update is one batched GEMM launch per rank."""
+
+    def __init__(self, ctx, A, info):
+        self.ctx, self.A, self.info = ctx, A, info
+        self.dev = A.device
+        self.kt = min(A.mt, A.nt)
+        self.pbuf = torch.zeros(A.m * A.nb, dtype=A.dtype, device=self.dev)
+        self.piv_dev = torch.zeros(A.nb, dtype=torch.int32, device=self.dev)
+        self.ipiv_all = torch.zeros(min(A.m, A.n), dtype=torch.int32, device=self.dev)
+        ncol = sum(A.tile_cols(n) for n in range(A.nt) if A.col_is_local(n))
+        self.ubuf = torch.zeros(max(1, A.nb * max(ncol, 1)), dtype=A.dtype, device=self.dev)
+
+    def step(self, k):
+        A, ctx = self.A, self.ctx
+        g = A.grid
+        mb = A.mb
+        kb = A.tile_cols(k)
+        r0 = k * mb
+        mp = A.m - r0
+        pc = g.pcol(k + A.jt0)
+        pv = self.pbuf[: mp * kb]
+        # --- 1. panel: sum the column's pieces inside process column pc, factor redundantly
+        if A.col_is_local(k):
+            pv.zero_()
+            mine = [m for m in range(k, A.mt) if A.row_is_local(m)]
+            if mine:
+                tb = TileBatch()
+                for m in mine:
+                    tb.add(A.offset(m, k), A.tile_rows(m), kb, b_off=(m - k) * mb)
+                ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, pv, mp, tb.finalize(), copy=True)
+            if g.P > 1:
+                dist.all_reduce(pv, group=ctx.col_group)
+            ops.getrf_panel(pv, 0, mp, kb, mp, self.piv_dev, self.info, r0, pivot=True)
+            if mine:
+                back = TileBatch()
+                for m in mine:
+                    back.add((m - k) * mb, A.tile_rows(m), kb, b_off=A.offset(m, k))
+                ops.geadd(0, N_, 1.0, pv, mp, 0.0, A.data, A.ld, back.finalize(), copy=True)
+        # --- 2. factored panel + pivots along process rows
+        if g.Q > 1:
+            root = g.rank(A.myrow, pc)
+            comm.bcast(pv, root, ctx.row_group)
+            comm.bcast(self.piv_dev, root, ctx.row_group)
+        piv = self.piv_dev[: min(mp, kb)].cpu().numpy()
+        self.ipiv_all[r0: r0 + len(piv)] = torch.from_numpy(piv.astype(np.int32) + r0 + 1).to(self.dev)
+        # --- 3. interchanges on every column but k
+        perm = _perm_from_swaps(piv, mp)
+        moved = np.nonzero(perm != np.arange(mp))[0]
+        cols = [n for n in range(A.nt) if n != k and A.col_is_local(n)]
+        _permute_rows_2d(ctx, A, moved + r0, perm[moved] + r0, cols)
+        # --- 4. U block row where it lives
+        trail = [n for n in range(k + 1, A.nt) if A.col_is_local(n)]
+        if not trail:
+            return
+        if A.row_is_local(k):
+            tb = TileBatch()
+            for n in trail:
+                tb.add(0, kb, A.tile_cols(n), b_off=A.offset(k, n))
+            ops.trsm(dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, pv, mp, A.data, A.ld, tb.finalize())
+        if k + 1 >= A.mt:
+            return
+        # --- 5. U block row down the process column (packed kb x sum(cols))
+        ub = self.ubuf
+        uoff, c = {}, 0
+        for n in trail:
+            uoff[n] = c * kb
+            c += A.tile_cols(n)
+        if A.row_is_local(k):
+            tb = TileBatch()
+            for n in trail:
+                tb.add(A.offset(k, n), kb, A.tile_cols(n), b_off=uoff[n])
+            ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, ub, kb, tb.finalize(), copy=True)
+        if g.P > 1:
+            comm.bcast(ub[: c * kb], g.rank(g.prow(k + A.it0), A.mycol), ctx.col_group)
+        # --- 6. trailing update A(m, n) -= L(m, k) U(k, n)
+        rows = [m for m in range(k + 1, A.mt) if A.row_is_local(m)]
+        if rows:
+            gb = GemmBatch()
+            for n in trail:
+                for m in rows:
+                    gb.add(A.offset(m, n), A.tile_rows(m), A.tile_cols(n), [((m - k) * mb, uoff[n], kb)])
+            ops.gemm(N_, N_, -1.0, pv, mp, ub, kb, 1.0, A.data, A.ld, gb.finalize())
+
+
+def getrf_ptgpanel_New(ctx, A, IPIV, info_out=None):
+    """Partial-pivoting LU on any P x Q grid (dplasma_zgetrf_ptgpanel_New).
+
+    IPIV: P x min(M,N) int32 with 1 x NB tiles (one replicated row per process
+    row, tests/testing_zgetrf_ptgpanel.c:55-58) or the 1-D ``ipiv_descriptor``."""
+    tp = Taskpool("getrf_ptgpanel", ctx)
+    tp.flops = flops(A.prec, "getrf", A.m, A.n)
+    info = torch.zeros(1, dtype=torch.int32, device=A.device)
+    st = _GetrfPtg(ctx, A, info)
+    prev = None
+    for k in range(st.kt):
+        prev = tp.task(f"getrf_ptg({k})", "update", (lambda k=k: st.step(k)), [prev])
+    tp._state = st
+
+    def _done():
+        for (m, n) in IPIV.local_tiles():
+            c0 = n * IPIV.nb
+            IPIV.tile(m, n).copy_(st.ipiv_all[c0: c0 + IPIV.tile_cols(n)].view(1, -1).to(IPIV.device))
+        v = info.clone()
+        comm.allreduce(v, op=torch.distributed.ReduceOp.MAX)
+        r = int(v.item())
+        if info_out is not None:
+            info_out[0] = r
+        return r
+    tp.on_complete(_done)
+    tp.ipiv_all = st.ipiv_all
+    return tp.finish_build()
+
+
+def getrf_ptgpanel(ctx, A, IPIV):
+    return getrf_ptgpanel_New(ctx, A, IPIV).execute(ctx)
+
+
+def ptgpanel_ipiv_descriptor(ctx, A, name="IPIV") -> TiledMatrix:
+    """P x min(M,N) int32, 1 x NB tiles: one replicated pivot row per process row."""
+    k = min(A.m, A.n)
+    return TiledMatrix(torch.int32, 1, A.nb, A.grid.P, k, P=A.grid.P, Q=A.grid.Q, rank=ctx.rank, device=A.device,
+                       name=name)
+
+
 def getrf_1d_New(ctx, A, IPIV, info_out=None):
     if ctx.world > 1 and A.P != 1:
-        raise NotImplementedError("getrf_1d requires a 1-D (P = 1) column distribution; "
-                                  "use getrf_nopiv or a 1 x Q grid")
+        return getrf_ptgpanel_New(ctx, A, IPIV, info_out)  # 2-D grid: the P x Q variant
     tp = Taskpool("getrf_1d", ctx)
     tp.flops = flops(A.prec, "getrf", A.m, A.n)
     info = torch.zeros(1, dtype=torch.int32, device=A.device)
@@ -235,6 +439,8 @@ def _gather_ipiv(ctx, IPIV) -> np.ndarray:
     k = IPIV.n
     full = torch.zeros(k, dtype=torch.int32, device=IPIV.device)
     for (m, n) in IPIV.local_tiles():
+        if m != 0:  # ptgpanel IPIV: one replicated row per process row
+            continue
         c0 = n * IPIV.nb
         full[c0: c0 + IPIV.tile_cols(n)] = IPIV.tile(m, n).view(-1)
     if ctx.world > 1:
@@ -243,9 +449,10 @@ def _gather_ipiv(ctx, IPIV) -> np.ndarray:
 
 
 def laswp(ctx, A, IPIV, inc=1):
-    """Apply the row interchanges of IPIV (1-based, sequential) to A, forward (inc>0) or backward."""
-    if ctx.world > 1 and A.P != 1:
-        raise NotImplementedError("laswp on P > 1 grids is not supported in this release")
+    """Apply the row interchanges of IPIV (1-based, sequential) to A, forward (inc>0) or backward.
+
+    Any P x Q grid: rows crossing process rows move with one all-to-all per
+    process column (_permute_rows_2d)."""
     piv = _gather_ipiv(ctx, IPIV) - 1
     perm = np.arange(A.m)
     seq = range(len(piv)) if inc > 0 else range(len(piv) - 1, -1, -1)
@@ -255,24 +462,29 @@ def laswp(ctx, A, IPIV, inc=1):
             perm[i], perm[p] = perm[p], perm[i]
     moved = np.nonzero(perm != np.arange(A.m))[0]
     cols = [n for n in range(A.nt) if A.col_is_local(n)]
-    if not len(moved) or not cols:
-        return 0
-    tmp = torch.empty(len(moved) * len(cols) * A.nb, dtype=A.dtype, device=A.device)
-    for group in ([n for n in cols if A.tile_cols(n) == A.nb], [n for n in cols if A.tile_cols(n) != A.nb]):
-        if not group:
-            continue
-        w = A.tile_cols(group[0])
-        ld_t = len(moved) * len(group)
-        pin, pout = [], []
-        for j, n in enumerate(group):
-            for i, d in enumerate(moved):
-                s = int(perm[d])
-                pin.append((j * len(moved) + i, A.offset(s // A.mb, n) + s % A.mb))
-                pout.append((A.offset(int(d) // A.mb, n) + int(d) % A.mb, j * len(moved) + i))
-        ops.row_gather(tmp, A.data, np.array(pin, dtype=ops.ROW_PAIR), w, ld_t, A.ld)
-        ops.row_gather(A.data, tmp, np.array(pout, dtype=ops.ROW_PAIR), w, A.ld, ld_t)
+    _permute_rows_2d(ctx, A, moved, perm[moved], cols)
     if A.device.type == "cuda":
         torch.cuda.synchronize(A.device)
+    return 0
+
+
+def trsmpl_ptgpanel(ctx, A, IPIV, B):
+    """B := L^-1 P B with the getrf_ptgpanel factors (dplasma_ztrsmpl_ptgpanel)."""
+    laswp(ctx, B, IPIV, 1)
+    blas3.trsm(ctx, dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, A, B)
+    return 0
+
+
+def gerfs(ctx, A, LU, IPIV, B, X, iters=2):
+    """Iterative refinement X += (LU)^-1 (B - A X) (dplasma_zgerfs role)."""
+    from . import aux
+    from .gemm import gemm
+    R = B.like(name="R")
+    for _ in range(iters):
+        aux.lacpy(ctx, 123, B, R)  # dplasmaUpperLower
+        gemm(ctx, N_, N_, -1.0, A, X, 1.0, R)
+        getrs(ctx, N_, LU, IPIV, R)
+        aux.geadd(ctx, N_, 1.0, R, 1.0, X)
     return 0
 
 

@@ -80,3 +80,84 @@ def test_lu_distributed():
     assert (full - a1).abs().max() < 1e-12
     assert (out[0][2] == piv1).all()
     assert (full2 - b1).abs().max() < 1e-12
+
+
+# ----------------------------------------------------------------------------- 2-D partial pivoting (ptgpanel)
+def _ptg_worker(rank, world, P, N, NB):
+    import dplasma_amd as dp
+    ctx = dp.init(device="cpu", P=P)
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+    dp.plrnt(ctx, A, 11)
+    IPIV = dp.ptgpanel_ipiv_descriptor(ctx, A)
+    info = dp.getrf_ptgpanel(ctx, A, IPIV)
+    from dplasma_amd.models.lu import _gather_ipiv
+    B = dp.block_cyclic(ctx, torch.float64, NB, NB, N, 3)
+    dp.plrnt(ctx, B, 12)
+    dp.trsmpl_ptgpanel(ctx, A, IPIV, B)
+    dp.trsm(ctx, dp.dplasmaLeft, dp.dplasmaUpper, dp.dplasmaNoTrans, dp.dplasmaNonUnit, 1.0, A, B)
+    return info, A.to_dense_local(), _gather_ipiv(ctx, IPIV), B.to_dense_local()
+
+
+@pytest.mark.parametrize("world,P", [(2, 2), (4, 2), (3, 3), (4, 4)])
+def test_getrf_ptgpanel_distributed(world, P):
+    N, NB = 90, 16
+    out = run_distributed(_ptg_worker, world, P, N, NB)
+    ctx = dp.init(device="cpu")
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+    dp.plrnt(ctx, A, 11)
+    a = A.to_dense_local()
+    B = dp.block_cyclic(ctx, torch.float64, NB, NB, N, 3)
+    dp.plrnt(ctx, B, 12)
+    b = B.to_dense_local()
+    lu, piv = torch.linalg.lu_factor(a)
+    assert all(out[r][0] == 0 for r in range(world))
+    full = sum(out[r][1] for r in range(world))
+    assert rel_err(full, lu) < 1e-12
+    assert (torch.from_numpy(out[0][2]).long() == piv.long()).all()
+    x = sum(out[r][3] for r in range(world))
+    assert rel_err(x, torch.linalg.solve(a, b)) < 1e-11
+
+
+def test_getrf_ptgpanel_single(ctx):
+    N, NB = 70, 16
+    A = dp.block_cyclic(ctx, torch.complex128, NB, NB, N, N)
+    dp.plrnt(ctx, A, 5)
+    a = A.to_dense_local()
+    IPIV = dp.ptgpanel_ipiv_descriptor(ctx, A)
+    assert dp.getrf_ptgpanel(ctx, A, IPIV) == 0
+    lu, piv = torch.linalg.lu_factor(a)
+    assert rel_err(A.to_dense_local(), lu) < 1e-12
+
+
+def test_gerfs(ctx):
+    N, NB = 60, 16
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+    dp.plrnt(ctx, A, 5)
+    LU = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+    dp.lacpy(ctx, dp.dplasmaUpperLower, A, LU)
+    B = dp.block_cyclic(ctx, torch.float64, NB, NB, N, 2)
+    dp.plrnt(ctx, B, 6)
+    X = dp.block_cyclic(ctx, torch.float64, NB, NB, N, 2)
+    dp.lacpy(ctx, dp.dplasmaUpperLower, B, X)
+    IPIV = dp.ipiv_descriptor(ctx, A)
+    assert dp.gesv(ctx, LU, IPIV, X) == 0
+    dp.gerfs(ctx, A, LU, IPIV, B, X)
+    ref = torch.linalg.solve(A.to_dense_local(), B.to_dense_local())
+    assert rel_err(X.to_dense_local(), ref) < 1e-13
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", list("dz"))
+def test_gpu_getrf_ptgpanel(prec):
+    gctx = dp.init(device="cuda:0")
+    dt = DTYPES[prec]
+    N, NB = 700, 128
+    A = dp.block_cyclic(gctx, dt, NB, NB, N, N)
+    dp.plrnt(gctx, A, 9)
+    a = A.to_dense_local().cpu()
+    IPIV = dp.ptgpanel_ipiv_descriptor(gctx, A)
+    assert dp.getrf_ptgpanel(gctx, A, IPIV) == 0
+    lu, piv = torch.linalg.lu_factor(a)
+    assert rel_err(A.to_dense_local().cpu(), lu) < 1e-11
+    from dplasma_amd.models.lu import _gather_ipiv
+    assert (torch.from_numpy(_gather_ipiv(gctx, IPIV)).long() == piv.long()).all()
