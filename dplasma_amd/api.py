@@ -14,6 +14,7 @@ from .models import aux as _aux
 from .models import blas3 as _blas3
 from .models import cholesky as _chol
 from .models import lu as _lu
+from .models import generators as _gen
 from .models import lu_incpiv as _lui
 from .models import qr as _qr
 from .models import qrtree as _qrtree
@@ -37,6 +38,8 @@ _GENERIC = {
     "tradd": _aux.tradd,
     "lascal": _aux.lascal, "lascal_New": _aux.lascal_New,
     "lange": _aux.lange, "lansy": _aux.lansy, "lanhe": _aux.lanhe, "lantr": _aux.lantr,
+    "lanm2": _aux.lanm2, "print": _aux.print_matrix, "apply": _aux.apply, "map2": _aux.map2,
+    "pltmg": _gen.pltmg, "latms": _gen.latms,
     "check_potrf": _check.check_potrf, "check_axmb": _check.check_axmb,
     "redistribute": _redis.redistribute,
     "trsm": _blas3.trsm, "trsm_New": _blas3.trsm_New,
@@ -128,3 +131,8 @@ for _n, _f in _GENERIC.items():
 for _n in ("hqr_init", "systolic_init", "svd_init", "qrtree_check", "QRTree", "HQRTree", "SystolicTree", "SVDTree",
            "FlatTree", "FLAT_TREE", "GREEDY_TREE", "FIBONACCI_TREE", "BINARY_TREE", "GREEDY1P_TREE"):
     _register("dplasma_" + _n if _n.endswith("_TREE") else _n, getattr(_qrtree, _n))
+
+# LAWN-263 matrix type codes (src/include/dplasma/constants.h:163-207)
+for _n in dir(_gen):
+    if _n.startswith("dplasmaMatrix"):
+        _register(_n, getattr(_gen, _n))

@@ -20,8 +20,8 @@ import math
 
 import torch
 
-from ..constants import (dplasmaFrobeniusNorm, dplasmaInfNorm, dplasmaLower, dplasmaMaxNorm, dplasmaNoTrans,
-                         dplasmaOneNorm, dplasmaTrans, dplasmaUnit, dplasmaUpper, dplasmaUpperLower)
+from ..constants import (dplasmaConjTrans, dplasmaFrobeniusNorm, dplasmaInfNorm, dplasmaLower, dplasmaMaxNorm,
+                         dplasmaNoTrans, dplasmaOneNorm, dplasmaTrans, dplasmaUnit, dplasmaUpper, dplasmaUpperLower)
 from ..ops import tile_ops as ops
 from ..ops.batch import TileBatch
 from ..parallel import comm
@@ -61,8 +61,23 @@ def plgsy_New(ctx, bump, uplo: int, A, seed: int) -> Taskpool:
     return _single(ctx, "plgsy", lambda: ops.generate("gsy", A.data, A.ld, tb, A.m, seed, bump))
 
 
-def plrnt(ctx, A, seed: int):
-    return plrnt_New(ctx, A, seed).execute(ctx)
+def plrnt(ctx, *args):
+    """plrnt(ctx, A, seed) or the reference form plrnt(ctx, diagdom, A, seed) (src/zplrnt_wrapper.c:191).
+
+    diagdom: add max(M,N) (real) / (M+N-1) + i max(M,N) (complex) to the
+    diagonal, making the matrix diagonally dominant (zplrnt_wrapper.c:45-60)."""
+    if len(args) == 3:
+        diagdom, A, seed = args
+    else:
+        (A, seed), diagdom = args, 0
+    plrnt_New(ctx, A, seed).execute(ctx)
+    if diagdom:
+        mx = max(A.m, A.n)
+        alpha = complex(A.m + A.n - 1, mx) if A.dtype.is_complex else float(mx)
+        for (m, n) in A.local_tiles():
+            if m + A.it0 == n + A.jt0:
+                A.tile(m, n).diagonal().add_(alpha)
+    return 0
 
 
 def plghe(ctx, bump, uplo, A, seed):
@@ -244,3 +259,90 @@ def lansy(ctx, norm, uplo, A, hermitian=False) -> float:
 
 def lanhe(ctx, norm, uplo, A) -> float:
     return lansy(ctx, norm, uplo, A, hermitian=True)
+
+
+# ----------------------------------------------------------------------------- apply / map2 (user tile operators)
+def apply(ctx, uplo, A, op, op_args=None):
+    """Run ``op(tile, uplo, m, n, op_args)`` on every local tile of the uplo part (parsec_apply_New).
+
+    ``tile`` is a (rows x cols) column-major view of the tile's storage on the
+    tile's device; the operator may modify it in place."""
+    for (m, n) in A.local_tiles(uplo if uplo in (dplasmaLower, dplasmaUpper) else dplasmaUpperLower):
+        t_uplo = uplo if m == n else dplasmaUpperLower
+        op(A.tile(m, n), t_uplo, m, n, op_args)
+    return 0
+
+
+def map2(ctx, uplo, trans, A, B, op, op_args=None):
+    """``op(tileA, tileB, uplo, m, n, op_args)`` on every local tile pair (dplasma_map2, src/map2.jdf).
+
+    trans != NoTrans pairs B(m, n) with op(A)(m, n) = A(n, m)^T/^H: A is first
+    redistributed transposed onto B's distribution."""
+    if trans != dplasmaNoTrans:
+        from .redistribute import transpose_into
+        A = transpose_into(ctx, A, trans)
+    for (m, n) in B.local_tiles(uplo if uplo in (dplasmaLower, dplasmaUpper) else dplasmaUpperLower):
+        t_uplo = uplo if m == n else dplasmaUpperLower
+        op(A.tile(m, n), B.tile(m, n), t_uplo, m, n, op_args)
+    return 0
+
+
+# ----------------------------------------------------------------------------- 2-norm estimate
+def lanm2(ctx, A, info=None, tol=1e-10, maxiter=500) -> float:
+    """Estimate ||A||_2 by power iteration on A^H A (dplasma_zlanm2, src/zlanm2.jdf:53-653).
+
+    Every product is a distributed tile GEMM; returns the estimate and, if
+    ``info`` (a list) is given, stores the iteration count (negative if the
+    iteration did not converge)."""
+    from .gemm import gemm_New
+    X = A.__class__(A.dtype, A.nb, 1, A.n, 1, P=A.grid.P, Q=A.grid.Q, rank=A.rank, device=A.device, name="x")
+    Y = A.__class__(A.dtype, A.mb, 1, A.m, 1, P=A.grid.P, Q=A.grid.Q, rank=A.rank, device=A.device, name="y")
+    ct = dplasmaConjTrans if A.dtype.is_complex else dplasmaTrans
+    laset(ctx, dplasmaUpperLower, 1.0 / math.sqrt(max(A.n, 1)), 1.0 / math.sqrt(max(A.n, 1)), X)
+    # the two products are compiled once and re-executed every iteration
+    ax = gemm_New(ctx, dplasmaNoTrans, dplasmaNoTrans, 1.0, A, X, 0.0, Y)
+    ahy = gemm_New(ctx, ct, dplasmaNoTrans, 1.0, A, Y, 0.0, X)
+    e, e0, it = 0.0, -1.0, 0
+    while it < maxiter and abs(e - e0) > tol * max(e, 1e-300):
+        e0 = e
+        ax.execute(ctx)
+        ahy.execute(ctx)
+        nx = lange(ctx, dplasmaFrobeniusNorm, X)
+        ny = lange(ctx, dplasmaFrobeniusNorm, Y)
+        if nx == 0.0 or ny == 0.0:
+            e = 0.0
+            break
+        e = nx / ny
+        lascal(ctx, dplasmaUpperLower, 1.0 / nx, X)
+        it += 1
+    if info is not None:
+        info.append(it if abs(e - e0) <= tol * max(e, 1e-300) else -it)
+    return e
+
+
+# ----------------------------------------------------------------------------- print
+def print_matrix(ctx, uplo, A, file=None) -> int:
+    """Print the uplo part of A tile by tile (dplasma_zprint, src/zprint.jdf PRINT_F/L/U).
+
+    Local tiles are collected on rank 0 and printed in (m, n) order."""
+    import sys
+    out = file or sys.stdout
+    dense = A.to_dense_local()
+    if ctx.world > 1:
+        import torch.distributed as dist
+        parts = [None] * ctx.world
+        dist.all_gather_object(parts, dense)
+        dense = sum(parts)
+    if ctx.rank != 0:
+        return 0
+    for n in range(A.nt):
+        for m in range(A.mt):
+            if (uplo == dplasmaLower and m < n) or (uplo == dplasmaUpper and m > n):
+                continue
+            r0, c0 = m * A.mb, n * A.nb
+            t = dense[r0:r0 + A.tile_rows(m), c0:c0 + A.tile_cols(n)]
+            print(f"{A.name}({m},{n}) [{t.shape[0]}x{t.shape[1]}]", file=out)
+            for i in range(t.shape[0]):
+                print("  " + " ".join(f"{complex(v):.6g}" if t.is_complex() else f"{float(v): .6e}" for v in t[i]),
+                      file=out)
+    return 0

@@ -55,7 +55,9 @@ def gemm_New(ctx, transA, transB, alpha, A, B, beta, C, c_mask=None, kc=None, na
     def kext(k):
         return A.tile_cols(k) if transA == dplasmaNoTrans else A.tile_rows(k)
     ctiles = [(m, n) for (m, n) in C.local_tiles() if c_mask is None or c_mask(m, n) is not None]
-    if kt == 0 or not ctiles:
+    # distributed: a rank without C tiles may still own A/B tiles others need, so it
+    # must join every exchange -- only kt == 0 (identical on all ranks) skips them
+    if kt == 0 or (not ctiles and ctx.world == 1):
         if beta != 1.0 and ctiles:
             from .aux import lascal_New
             return lascal_New(ctx, 123, beta, C)
