@@ -42,20 +42,25 @@ def main():
     ap.add_argument("-P", type=int, default=None)
     ap.add_argument("--check", action="store_true", help="verify the factorisation after the timed steps")
     ap.add_argument("--trace", default=None, help="write a Chrome trace of one step to this file")
+    ap.add_argument("--cpu", action="store_true",
+                    help="dry run of the same multi-rank path on CPU ranks (gloo) -- plumbing tests only")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.cpu:
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import dplasma_amd as dp
 
     P = args.P
     if P is None:
         P = {1: 1, 2: 1, 4: 2, 8: 2}.get(world, None)
-    ctx = dp.init(P=P)
+    ctx = dp.init(P=P, device="cpu") if args.cpu else dp.init(P=P)
     rank = ctx.rank
     N, NB = args.N, args.nb
     A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N, name="A", uplo=dp.dplasmaLower)
