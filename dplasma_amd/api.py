@@ -136,3 +136,12 @@ for _n in ("hqr_init", "systolic_init", "svd_init", "qrtree_check", "QRTree", "H
 for _n in dir(_gen):
     if _n.startswith("dplasmaMatrix"):
         _register(_n, getattr(_gen, _n))
+
+# DTD insert-task front end (parsec_dtd_* surface) and the DTD Cholesky (src/dtd_wrappers/zpotrf.c)
+from .runtime import dtd  # noqa: E402
+from .models import dtd_potrf as _dtdp  # noqa: E402
+register_op("potrf_dtd", _dtdp.potrf_dtd)
+register_op("potrf_dtd_New", _dtdp.potrf_dtd_New)
+for _n in ("taskpool_new", "tile_of", "INPUT", "OUTPUT", "INOUT", "AFFINITY", "VALUE", "SCRATCH", "PUSHOUT"):
+    _register("dtd_" + _n, getattr(dtd, _n))
+_register("dtd", dtd)

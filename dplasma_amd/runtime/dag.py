@@ -80,6 +80,9 @@ class Kind:
     cpu: Callable
     flops: Optional[Callable] = None  # ext (n, 3) int array -> total flops
     prio: int = 0                     # launch order within a level (lower first)
+    # DTD-style task class: body(*tile_views, *pyargs) runs once per task (on the
+    # level's stream) instead of one batched launch; gpu/cpu are then unused
+    body: Optional[Callable] = None
 
 
 def _lib_rt():
@@ -162,22 +165,32 @@ class TileDAG:
             self.kinds.append(K)
         return self._kid[K.name]
 
-    def add(self, K: Kind, ops, ext):
+    def add(self, K: Kind, ops, ext, pyargs=None):
         """Append tasks of kind K in program order.
 
-        ops: (n, len(K.roles)) tile keys (-1 for an unused optional role); ext: (n, 3) ints."""
+        ops: (n, len(K.roles)) tile keys (-1 for an unused optional role); ext: (n, 3) ints;
+        pyargs: optional per-task tuples of Python values passed to a ``body`` kind."""
         ops = np.atleast_2d(np.asarray(ops, dtype=np.int64))
         ext = np.atleast_2d(np.asarray(ext, dtype=np.int32))
         if ops.size == 0:
             return
         if ops.shape[1] != len(K.roles) or ext.shape != (ops.shape[0], 3):
             raise ValueError(f"{K.name}: bad task array shapes {ops.shape} {ext.shape}")
+        if pyargs is not None and len(pyargs) != len(ops):
+            raise ValueError("one pyargs tuple per task")
         kid = self.kind(K)
-        self._chunks.append((kid, ops, ext))
+        self._chunks.append((kid, ops, ext, list(pyargs) if pyargs is not None else None))
         if K.flops is not None:
             self.flops += float(K.flops(ext))
 
     # ------------------------------------------------------------ geometry helpers
+    def _tile_shape(self, key: int):
+        if key < 0:
+            return (0, 0)
+        M = self.mats[key >> _MID_SHIFT]
+        gm, gn = (key >> _M_SHIFT) & _MASK22, key & _MASK22
+        return (min(M.mb, M.lm - gm * M.mb), min(M.nb, M.ln - gn * M.nb))
+
     def _home(self, keys: np.ndarray) -> np.ndarray:
         mid = keys >> _MID_SHIFT
         gm = (keys >> _M_SHIFT) & _MASK22
@@ -226,14 +239,15 @@ class TileDAG:
         tp.flops = self.flops
         if not self._chunks:
             return tp.finish_build()
-        nR = max(len(self.kinds[k].roles) for k, _, _ in self._chunks)
-        ntask = sum(len(o) for _, o, _ in self._chunks)
+        nR = max(len(self.kinds[c[0]].roles) for c in self._chunks)
+        ntask = sum(len(c[1]) for c in self._chunks)
         ops = np.full((ntask, nR), -1, dtype=np.int64)
         modes = np.zeros((ntask, nR), dtype=np.uint8)
         kid = np.zeros(ntask, dtype=np.int32)
         ext = np.zeros((ntask, 3), dtype=np.int32)
+        pyargs_all = None
         p = 0
-        for k, o, e in self._chunks:
+        for k, o, e, pa in self._chunks:
             n = len(o)
             K = self.kinds[k]
             ops[p:p + n, :o.shape[1]] = o
@@ -241,6 +255,10 @@ class TileDAG:
                 modes[p:p + n, r] = np.where(o[:, r] >= 0, md, 0)
             kid[p:p + n] = k
             ext[p:p + n] = e
+            if pa is not None:
+                if pyargs_all is None:
+                    pyargs_all = [()] * ntask
+                pyargs_all[p:p + n] = pa
             p += n
         self._chunks = []
         rt = _lib_rt()
@@ -371,13 +389,18 @@ class TileDAG:
                     seg[f"ld{slot}"] = l
                 seg["m"], seg["n"], seg["k"] = ext[mine_t[s:e], 0], ext[mine_t[s:e], 1], ext[mine_t[s:e], 2]
                 cpu_refs = None
-                if device.type != "cuda":
+                if device.type != "cuda" or K.body is not None:
                     cpu_refs = [[(bases[int(refs_all[r][0][i])] if refs_all[r][0][i] >= 0 else None,
                                   int(refs_all[r][1][i]), int(refs_all[r][2][i])) for r in range(len(K.roles))]
                                 for i in range(s, e)]
                 ex = ext[mine_t[s:e]]
                 gid_of_task[mine_t[s:e]] = g
-                groups.append(dict(K=K, start=int(s), n=int(e - s), cpu_refs=cpu_refs, ext=ex,
+                pyargs = [pyargs_all[int(t)] for t in mine_t[s:e]] if pyargs_all is not None else None
+                shapes = None
+                if K.body is not None:
+                    shapes = [[self._tile_shape(int(ops[t, r])) for r in range(len(K.roles))] for t in mine_t[s:e]]
+                groups.append(dict(K=K, start=int(s), n=int(e - s), cpu_refs=cpu_refs, ext=ex, pyargs=pyargs,
+                                   shapes=shapes,
                                    emax=tuple(int(x) for x in ex.max(0)), level=int(lv[s]),
                                    stream="panel" if (multistream and cf[s] == 0) else "update",
                                    waits=[], record=False))
@@ -484,13 +507,33 @@ class _DagProgram:
             for bi, ld, mb, tb in unpack:  # recvbuf[i*nbe] -> tile
                 copy_tiles(bases[bi], ld, recvbuf, mb, tb, to_b=False)
 
-    def _launch(self, g, dev_items, stream_ptr):
+    def _launch(self, g, dev_items, stream_ptr, stream_obj=None):
         K = g["K"]
+        if K.body is not None:
+            self._run_bodies(g, stream_obj)
+            return
         if dev_items is not None:
             K.gpu(dev_items.data_ptr() + g["start"] * DAG_ITEM.itemsize, g["n"], stream_ptr, g["emax"])
         else:
             for refs, e in zip(g["cpu_refs"], g["ext"]):
                 K.cpu(refs, (int(e[0]), int(e[1]), int(e[2])))
+
+    def _run_bodies(self, g, stream_obj):
+        """DTD task class: one call per task on tile views (tensor views of tile storage)."""
+        K = g["K"]
+        pyargs = g["pyargs"] or [()] * g["n"]
+
+        def go():
+            for refs, shp, pa in zip(g["cpu_refs"], g["shapes"], pyargs):
+                views = []
+                for (base, off, ld), (r, c) in zip(refs, shp):
+                    views.append(None if base is None else torch.as_strided(base, (r, c), (1, ld), off))
+                K.body(*views, *pa)
+        if stream_obj is not None:
+            with torch.cuda.stream(stream_obj):
+                go()
+        else:
+            go()
 
     def run(self):
         dag = self.dag
@@ -527,7 +570,7 @@ class _DagProgram:
             s = streams[g["stream"]]
             for w in g["waits"]:
                 s.wait_event(events[w])
-            self._launch(g, dev_items, s.cuda_stream)
+            self._launch(g, dev_items, s.cuda_stream, s)
             if g["record"]:
                 ev = torch.cuda.Event()
                 ev.record(s)
