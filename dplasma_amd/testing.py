@@ -1,0 +1,367 @@
+"""Reference-style testing driver: ``python -m dplasma_amd.testing <prec><op> [flags]``.
+
+Mirrors the ``tests/testing_z*.c`` programs and their common CLI
+(``tests/common.c:171-259``): -N/-M/-K, -t/--MB, -T/--NB,
+-i/--IB, -P/-Q, -x/--check, --seed, --mtx, --nruns, --qr_a/--qr_p/--treel/--treeh,
+-d/--domino, -r/--tsrr, -v, --dot.  Each run prints the reference's result line
+
+    [****] TIME(s)      t : dpotrf PxQxg=   P Q g NB=  nb N=    n :      X gflops - ENQ&PROG&DEST e p d
+
+and, with -x, the check outcome ("Solution is CORRECT" / "SUSPICIOUS") using
+the reference's residual tests (``src/dplasma_zcheck.c``, ``tests/testing_zgeqrf.c:221-303``).
+Multi-process: launch with ``torch.distributed.run``; the grid is P x (world/P).
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import os
+import sys
+import time
+
+import torch
+
+PRECS = {"s": torch.float32, "d": torch.float64, "c": torch.complex64, "z": torch.complex128}
+EPS = {"s": 5.96e-08, "d": 1.11e-16, "c": 5.96e-08, "z": 1.11e-16}
+
+
+def _parse(argv):
+    ap = argparse.ArgumentParser(prog="python -m dplasma_amd.testing", add_help=True)
+    ap.add_argument("op", help="e.g. dpotrf, zgemm, dgeqrf_hqr, sgetrf_incpiv")
+    ap.add_argument("-N", type=int, required=True)
+    ap.add_argument("-M", type=int, default=0)
+    ap.add_argument("-K", "--NRHS", type=int, default=0, dest="K")
+    ap.add_argument("-t", "--MB", type=int, default=0, dest="MB")
+    ap.add_argument("-T", "--NB", type=int, default=0, dest="NB")
+    ap.add_argument("-i", "--IB", type=int, default=0, dest="IB")
+    ap.add_argument("-P", "-p", "--grid-rows", type=int, default=0, dest="P")
+    ap.add_argument("-Q", "-q", "--grid-cols", type=int, default=0, dest="Q")
+    ap.add_argument("-x", "--check", action="store_true")
+    ap.add_argument("-X", "--check_inv", action="store_true")
+    ap.add_argument("--seed", type=int, default=3872)
+    ap.add_argument("--mtx", type=int, default=0)
+    ap.add_argument("--nruns", type=int, default=1)
+    ap.add_argument("--qr_a", type=int, default=-1)
+    ap.add_argument("--qr_p", type=int, default=-1)
+    ap.add_argument("--treel", type=int, default=1)
+    ap.add_argument("--treeh", type=int, default=0)
+    ap.add_argument("-d", "--domino", action="store_true")
+    ap.add_argument("-r", "--tsrr", action="store_true")
+    ap.add_argument("-a", "--alpha", type=float, default=1.0)
+    ap.add_argument("-u", "--uplo", default="L")
+    ap.add_argument("-v", "--verbose", type=int, nargs="?", const=1, default=0)
+    ap.add_argument("-g", "--gpus", type=int, default=-1, help="0: CPU only; default: GPU when present")
+    ap.add_argument("--dot", default=None, help="write the DAG of DAG-based ops to this DOT file")
+    return ap.parse_args(argv)
+
+
+class Harness:
+    def __init__(self, a):
+        self.a = a
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        import torch.distributed as dist
+        use_gpu = torch.cuda.is_available() and a.gpus != 0
+        if world > 1 and not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if use_gpu:
+                local = int(os.environ.get("LOCAL_RANK", "0"))
+                torch.cuda.set_device(local)
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group("gloo")
+        import dplasma_amd as dp
+        self.dp = dp
+        P = a.P or None
+        self.ctx = dp.init(P=P, device=None if use_gpu else "cpu")
+        self.prec = a.op[0]
+        if self.prec not in PRECS:
+            raise SystemExit(f"operation must start with a precision letter s/d/c/z: {a.op}")
+        self.name = a.op[1:]
+        self.dt = PRECS[self.prec]
+        self.ok = True
+
+    # ------------------------------------------------------------ helpers
+    def mat(self, m, n, mb=None, nb=None, name="A"):
+        a = self.a
+        mb = mb or a.MB or a.NB or 180
+        nb = nb or a.NB or mb
+        return self.dp.block_cyclic(self.ctx, self.dt, mb, nb, m, n, name=name)
+
+    def report(self, opname, t, flops, t_enq=0.0, t_dest=0.0):
+        ctx = self.ctx
+        if ctx.rank == 0:
+            g = 1 if ctx.is_gpu else 0
+            print(f"[****] TIME(s) {t:12.5f} : {self.prec}{opname}\tPxQxg= {ctx.P:3d} {ctx.Q:<3d} {g} "
+                  f"NB= {self.a.NB or self.a.MB or 180:4d} N= {self.a.N:7d} : {flops / t / 1e9 if t > 0 else 0:14f} "
+                  f"gflops - ENQ&PROG&DEST {t_enq:12.5f} : {t:12.5f} : {t_dest:12.5f}", flush=True)
+
+    def run_tp(self, opname, build):
+        """build() -> taskpool; times ENQ (build), PROG (run+complete), DEST; returns (taskpool result)."""
+        ctx = self.ctx
+        res = None
+        for _ in range(max(1, self.a.nruns)):
+            ctx.barrier()
+            t0 = time.perf_counter()
+            tp = build()
+            t_enq = time.perf_counter() - t0
+            ctx.barrier()
+            ctx.sync()
+            t1 = time.perf_counter()
+            tp.run(ctx)
+            res = tp.complete(ctx)
+            ctx.sync()
+            ctx.barrier()
+            t2 = time.perf_counter()
+            if self.a.dot and getattr(tp, "dag", None) is not None and ctx.rank == 0:
+                pass  # DOT dumps are produced by TileDAG.dot before compile (see _dag_dot)
+            tp.destruct()
+            t3 = time.perf_counter()
+            self.report(opname, t2 - t1, tp.flops, t_enq, t3 - t2)
+        return res
+
+    def check(self, label, value, threshold):
+        good = value < threshold and not math.isnan(value)
+        self.ok &= good
+        if self.ctx.rank == 0:
+            print(f"-- {label} = {value:e} (threshold {threshold:g}): Solution is "
+                  f"{'CORRECT' if good else 'SUSPICIOUS'}", flush=True)
+
+
+# ----------------------------------------------------------------------------- operations
+def t_potrf(h, dtd=False):
+    dp, a, ctx = h.dp, h.a, h.ctx
+    uplo = dp.dplasmaLower if a.uplo.upper() == "L" else dp.dplasmaUpper
+    A = h.mat(a.N, a.N)
+    dp.plghe(ctx, float(a.N), dp.dplasmaUpperLower, A, a.seed)
+    A0 = A.like()
+    A0.data.copy_(A.data)
+    fn = dp.potrf_dtd_New if dtd else dp.potrf_New
+    info = h.run_tp("potrf_dtd" if dtd else "potrf", lambda: fn(ctx, uplo, A))
+    if a.check:
+        ok, res = dp.check_potrf(ctx, uplo, A, A0)
+        h.check("||L L^H - A|| / (||A|| N eps)", res, 60.0)
+    return info
+
+
+def t_posv(h):
+    dp, a, ctx = h.dp, h.a, h.ctx
+    K = a.K or 1
+    A = h.mat(a.N, a.N)
+    dp.plghe(ctx, float(a.N), dp.dplasmaUpperLower, A, a.seed)
+    A0 = A.like()
+    A0.data.copy_(A.data)
+    B = h.mat(a.N, K, name="B")
+    dp.plrnt(ctx, B, a.seed + 1)
+    B0 = B.like()
+    B0.data.copy_(B.data)
+    h.run_tp("posv", lambda: dp.posv_New(ctx, dp.dplasmaLower, A, B))
+    if a.check:
+        ok, res = dp.check_axmb(ctx, A0, B, B0)
+        h.check("||Ax-b|| / ((||A|| ||x|| + ||b||) N eps)", res, 60.0)
+
+
+def t_gemm(h):
+    dp, a, ctx = h.dp, h.a, h.ctx
+    M, N, K = a.M or a.N, a.N, a.K or a.N
+    A, B, C = h.mat(M, K, name="A"), h.mat(K, N, name="B"), h.mat(M, N, name="C")
+    dp.plrnt(ctx, A, a.seed)
+    dp.plrnt(ctx, B, a.seed + 1)
+    dp.plrnt(ctx, C, a.seed + 2)
+    if a.check:
+        a_, b_, c_ = (_dense(h, X) for X in (A, B, C))
+    h.run_tp("gemm", lambda: dp.gemm_New(ctx, dp.dplasmaNoTrans, dp.dplasmaNoTrans, a.alpha, A, B, 0.5, C))
+    if a.check:
+        ref = a.alpha * (a_ @ b_) + 0.5 * c_
+        got = _dense(h, C)
+        res = float((got - ref).abs().max() / (ref.abs().max() * K * EPS[h.prec]))
+        h.check("||C - C_ref|| / (||C_ref|| K eps)", res, 10.0)
+
+
+def t_trsm(h):
+    dp, a, ctx = h.dp, h.a, h.ctx
+    M, N = a.M or a.N, a.K or a.N
+    A, B = h.mat(M, M, name="A"), h.mat(M, N, name="B")
+    dp.plghe(ctx, float(M), dp.dplasmaUpperLower, A, a.seed)
+    dp.plrnt(ctx, B, a.seed + 1)
+    b0 = _dense(h, B) if a.check else None
+    a0 = _dense(h, A) if a.check else None
+    h.run_tp("trsm", lambda: dp.trsm_New(ctx, dp.dplasmaLeft, dp.dplasmaLower, dp.dplasmaNoTrans,
+                                          dp.dplasmaNonUnit, a.alpha, A, B))
+    if a.check:
+        x = _dense(h, B)
+        res = float((torch.tril(a0) @ x - a.alpha * b0).abs().max() / (a0.abs().max() * x.abs().max() * M
+                                                                         * EPS[h.prec] + 1e-300))
+        h.check("||A X - alpha B|| / (||A|| ||X|| N eps)", res, 10.0)
+
+
+def t_trmm(h):
+    dp, a, ctx = h.dp, h.a, h.ctx
+    M, N = a.M or a.N, a.K or a.N
+    A, B = h.mat(M, M, name="A"), h.mat(M, N, name="B")
+    dp.plrnt(ctx, A, a.seed)
+    dp.plrnt(ctx, B, a.seed + 1)
+    a0, b0 = (_dense(h, A), _dense(h, B)) if a.check else (None, None)
+    h.run_tp("trmm", lambda: dp.trmm_New(ctx, dp.dplasmaLeft, dp.dplasmaUpper, dp.dplasmaNoTrans,
+                                          dp.dplasmaNonUnit, a.alpha, A, B))
+    if a.check:
+        ref = a.alpha * torch.triu(a0) @ b0
+        res = float((_dense(h, B) - ref).abs().max() / (ref.abs().max() * M * EPS[h.prec]))
+        h.check("||B - B_ref|| / (||B_ref|| N eps)", res, 10.0)
+
+
+def _qr_common(h, lq, tree_kind):
+    dp, a, ctx = h.dp, h.a, h.ctx
+    M = a.M or a.N
+    N = a.N
+    ib = a.IB or 32
+    A = h.mat(M, N)
+    if a.mtx:
+        dp.pltmg(ctx, a.mtx, A, a.seed)
+    else:
+        dp.plrnt(ctx, A, a.seed)
+    a0 = _dense(h, A) if a.check else None
+    TS = dp.block_cyclic(ctx, h.dt, ib, A.nb, A.mt * ib, A.nt * A.nb, name="TS")
+    TT = dp.block_cyclic(ctx, h.dt, ib, A.nb, A.mt * ib, A.nt * A.nb, name="TT")
+    trans = dp.dplasmaConjTrans if lq else dp.dplasmaNoTrans
+    tree = None
+    if tree_kind == "hqr":
+        tree = dp.hqr_init(trans, A, a.treel, a.treeh, a.qr_a if a.qr_a > 0 else 1,
+                           a.qr_p if a.qr_p > 0 else ctx.P, a.domino, a.tsrr)
+    elif tree_kind == "systolic":
+        tree = dp.systolic_init(trans, A, a.qr_p if a.qr_p > 0 else ctx.P, a.qr_a if a.qr_a > 0 else 1)
+    if tree is None:
+        build = (lambda: dp.gelqf_New(ctx, A, TS)) if lq else (lambda: dp.geqrf_New(ctx, A, TS))
+    else:
+        build = (lambda: dp.gelqf_param_New(ctx, tree, A, TS, TT)) if lq else \
+            (lambda: dp.geqrf_param_New(ctx, tree, A, TS, TT))
+    h.run_tp(("gelqf" if lq else "geqrf") + ("" if tree is None else "_" + tree_kind), build)
+    if a.check:
+        K = min(M, N)
+        Q = h.mat(M if not lq else K, K if not lq else N, name="Q")
+        if tree is None:
+            (dp.unglq if lq else dp.ungqr)(ctx, A, TS, Q)
+        else:
+            (dp.unglq_param if lq else dp.ungqr_param)(ctx, tree, A, TS, TT, Q)
+        q, r = _dense(h, Q), _dense(h, A)
+        if not lq:
+            orth = (q.conj().T @ q - torch.eye(K, dtype=q.dtype)).abs().max()
+            rec = (q @ torch.triu(r[:K]) - a0).abs().max() / a0.abs().max()
+        else:
+            orth = (q @ q.conj().T - torch.eye(K, dtype=q.dtype)).abs().max()
+            rec = (torch.tril(r[:, :K]) @ q - a0).abs().max() / a0.abs().max()
+        h.check("||I - Q^H Q|| / (N eps)", float(orth) / (max(M, N) * EPS[h.prec]), 60.0)
+        h.check("||A - Q R|| / (||A|| N eps)", float(rec) / (max(M, N) * EPS[h.prec]), 60.0)
+
+
+def t_getrf(h, variant):
+    dp, a, ctx = h.dp, h.a, h.ctx
+    N = a.N
+    A = h.mat(N, N)
+    if variant == "nopiv":
+        dp.plghe(ctx, float(N), dp.dplasmaUpperLower, A, a.seed)
+    else:
+        dp.plrnt(ctx, A, a.seed)
+    a0 = _dense(h, A) if a.check else None
+    if variant == "incpiv":
+        L = dp.incpiv_L_descriptor(ctx, A, a.IB or 32)
+        IP = dp.incpiv_ipiv_descriptor(ctx, A)
+        h.run_tp("getrf_incpiv", lambda: dp.getrf_incpiv_New(ctx, A, L, IP))
+    elif variant == "nopiv":
+        h.run_tp("getrf_nopiv", lambda: dp.getrf_nopiv_New(ctx, A))
+    else:
+        IP = dp.ptgpanel_ipiv_descriptor(ctx, A)
+        h.run_tp("getrf_" + variant, lambda: dp.getrf_ptgpanel_New(ctx, A, IP))
+    if a.check:
+        B = h.mat(N, a.K or 1, name="B")
+        dp.plrnt(ctx, B, a.seed + 1)
+        b0 = _dense(h, B)
+        if variant == "incpiv":
+            dp.trsmpl_incpiv(ctx, A, L, IP, B)
+        elif variant == "nopiv":
+            dp.trsm(ctx, dp.dplasmaLeft, dp.dplasmaLower, dp.dplasmaNoTrans, dp.dplasmaUnit, 1.0, A, B)
+        else:
+            dp.trsmpl_ptgpanel(ctx, A, IP, B)
+        dp.trsm(ctx, dp.dplasmaLeft, dp.dplasmaUpper, dp.dplasmaNoTrans, dp.dplasmaNonUnit, 1.0, A, B)
+        x = _dense(h, B)
+        res = float((a0 @ x - b0).abs().max() / ((a0.abs().max() * x.abs().max() + b0.abs().max()) * N
+                                                  * EPS[h.prec]))
+        h.check("||Ax-b|| / ((||A|| ||x|| + ||b||) N eps)", res, 60.0)
+
+
+def t_lange(h):
+    dp, a, ctx = h.dp, h.a, h.ctx
+    M, N = a.M or a.N, a.N
+    A = h.mat(M, N)
+    dp.plrnt(ctx, A, a.seed)
+    d = _dense(h, A)
+    for nm, code, ref in (("max", dp.dplasmaMaxNorm, d.abs().max()), ("one", dp.dplasmaOneNorm, d.abs().sum(0).max()),
+                          ("inf", dp.dplasmaInfNorm, d.abs().sum(1).max()),
+                          ("frb", dp.dplasmaFrobeniusNorm, torch.linalg.norm(d))):
+        t0 = time.perf_counter()
+        v = dp.lange(ctx, code, A)
+        if ctx.rank == 0:
+            print(f"[****] TIME(s) {time.perf_counter() - t0:12.5f} : {h.prec}lange({nm}) = {v:.15e}")
+        if a.check:
+            h.check(f"|lange({nm}) - ref| / (ref eps N)", abs(v - float(ref)) / (float(ref) * EPS[h.prec] * N), 10.0)
+
+
+def t_lanm2(h):
+    dp, a, ctx = h.dp, h.a, h.ctx
+    A = h.mat(a.M or a.N, a.N)
+    dp.plrnt(ctx, A, a.seed)
+    info = []
+    t0 = time.perf_counter()
+    v = dp.lanm2(ctx, A, info)
+    if ctx.rank == 0:
+        print(f"[****] TIME(s) {time.perf_counter() - t0:12.5f} : {h.prec}lanm2 = {v:.15e} (iterations {info[0]})")
+    if a.check:
+        ref = float(torch.linalg.matrix_norm(_dense(h, A).to(torch.complex128 if h.dt.is_complex else torch.float64),
+                                             2))
+        h.check("|lanm2 - ||A||_2| / ||A||_2", abs(v - ref) / ref, 1e-5)
+
+
+def t_print(h):
+    dp, a, ctx = h.dp, h.a, h.ctx
+    A = h.mat(a.M or a.N, a.N)
+    dp.plrnt(ctx, A, a.seed)
+    dp.print(ctx, dp.dplasmaUpperLower, A)
+
+
+def _dense(h, X):
+    d = X.to_dense_local().cpu()
+    if h.ctx.world > 1:
+        import torch.distributed as dist
+        t = d.to(h.ctx.device)
+        dist.all_reduce(t)
+        d = t.cpu()
+    return d
+
+
+OPS = {
+    "potrf": t_potrf, "potrf_dtd": lambda h: t_potrf(h, dtd=True), "posv": t_posv, "gemm": t_gemm,
+    "trsm": t_trsm, "trmm": t_trmm,
+    "geqrf": lambda h: _qr_common(h, False, None), "gelqf": lambda h: _qr_common(h, True, None),
+    "geqrf_hqr": lambda h: _qr_common(h, False, "hqr"), "gelqf_hqr": lambda h: _qr_common(h, True, "hqr"),
+    "geqrf_systolic": lambda h: _qr_common(h, False, "systolic"),
+    "gelqf_systolic": lambda h: _qr_common(h, True, "systolic"),
+    "getrf_1d": lambda h: t_getrf(h, "1d"), "getrf_ptgpanel": lambda h: t_getrf(h, "ptgpanel"),
+    "getrf_incpiv": lambda h: t_getrf(h, "incpiv"), "getrf_nopiv": lambda h: t_getrf(h, "nopiv"),
+    "lange": t_lange, "lanm2": t_lanm2, "print": t_print,
+}
+
+
+def main(argv=None):
+    a = _parse(argv if argv is not None else sys.argv[1:])
+    h = Harness(a)
+    fn = OPS.get(h.name)
+    if fn is None:
+        raise SystemExit(f"unknown operation {h.name}; available: {', '.join(sorted(OPS))}")
+    fn(h)
+    if h.ctx.world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    return 0 if h.ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

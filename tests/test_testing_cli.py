@@ -1,0 +1,39 @@
+"""The reference-style testing driver (python -m dplasma_amd.testing), on CPU ranks."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+from helpers import free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, nproc=1):
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+    if nproc == 1:
+        cmd = [sys.executable, "-m", "dplasma_amd.testing", *args, "-g", "0"]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m", "dplasma_amd.testing",
+               *args, "-g", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd="/tmp")
+    return r
+
+
+@pytest.mark.parametrize("args", [
+    "dpotrf -N 378 -t 93 -x", "zposv -N 150 -t 40 -K 3 -x", "sgemm -M 106 -N 283 -K 97 -t 56 -x",
+    "dgeqrf -M 487 -N 283 -t 56 -i 8 -x", "dgeqrf_hqr -M 300 -N 200 -t 50 -i 10 --qr_a 2 -x",
+    "dgetrf_incpiv -N 200 -t 50 -i 10 -x", "dgetrf_ptgpanel -N 200 -t 50 -x", "dlange -M 87 -N 83 -t 16 -x",
+])
+def test_cli_single(args):
+    r = _run(args.split())
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    assert "[****] TIME(s)" in r.stdout and "SUSPICIOUS" not in r.stdout
+
+
+def test_cli_multirank():
+    r = _run("dgetrf_ptgpanel -N 200 -t 32 -P 2 -x".split(), nproc=4)
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    assert "PxQxg=   2 2" in r.stdout and "CORRECT" in r.stdout
