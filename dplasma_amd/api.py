@@ -145,3 +145,7 @@ register_op("potrf_dtd_New", _dtdp.potrf_dtd_New)
 for _n in ("taskpool_new", "tile_of", "INPUT", "OUTPUT", "INOUT", "AFFINITY", "VALUE", "SCRATCH", "PUSHOUT"):
     _register("dtd_" + _n, getattr(dtd, _n))
 _register("dtd", dtd)
+
+# ScaLAPACK-compatible shims (src/scalapack_wrappers): dp.scalapack.pdgemm_ ...
+from . import scalapack  # noqa: E402
+_register("scalapack", scalapack)
