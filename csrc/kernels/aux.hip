@@ -169,6 +169,28 @@ __global__ __launch_bounds__(256) void k_lascal(const TileItem* __restrict__ ite
   *p = mul(alpha, *p);
 }
 
+// ---------------------------------------------------------------- diagonal scaling (LDL^H family)
+// B(i, j) := B(i, j) / d, with d the diagonal of the tile at D + item.a_off:
+// cols != 0: d = D(j, j) (B := B D^-1, CORE_ztrmdm / hetrf), else d = D(i, i) (B := D^-1 B, CORE_ztrdsm).
+// item.b_off addresses the B tile; gi/gj its global coordinates for the part mask.
+template <typename T>
+__global__ __launch_bounds__(256) void k_diag_scale(const TileItem* __restrict__ items, int nitems, int mmax,
+                                                    int nmax, const T* __restrict__ D, int ldd, T* B, int ldb,
+                                                    int part, int cols) {
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int per = mmax * nmax;
+  if (gid >= (long long)nitems * per) return;
+  const int item = (int)(gid / per), r = (int)(gid % per);
+  const int i = r % mmax, j = r / mmax;
+  const TileItem it = items[item];
+  if (i >= it.m || j >= it.n) return;
+  if (!in_part(part, it.gi + i, it.gj + j)) return;
+  const int q = cols ? j : i;
+  const T d = D[it.a_off + q + (long long)q * ldd];
+  T* p = B + it.b_off + i + (long long)j * ldb;
+  *p = divv(*p, d);
+}
+
 // ---------------------------------------------------------------- norms
 // kind 0: max |a| -> out[item]
 // kind 1: column sums of |a| -> out[item*ostride + j]
@@ -293,6 +315,16 @@ DPL_API int dpl_lascal(int prec, int part, int nitems, const void* items, int mm
   const int blocks = (int)((total + 255) / 256);
   DISPATCH(prec, hipLaunchKernelGGL((k_lascal<T>), dim3(blocks), dim3(256), 0, st, (const TileItem*)items, nitems, mmax,
                                     nmax, (T*)A, lda, part, *(const T*)alpha));
+  return (int)hipGetLastError();
+}
+
+DPL_API int dpl_diag_scale(int prec, int part, int cols, int nitems, const void* items, int mmax, int nmax,
+                           const void* D, int ldd, void* B, int ldb, hipStream_t st) {
+  if (nitems <= 0) return 0;
+  const long long total = (long long)nitems * mmax * nmax;
+  const int blocks = (int)((total + 255) / 256);
+  DISPATCH(prec, hipLaunchKernelGGL((k_diag_scale<T>), dim3(blocks), dim3(256), 0, st, (const TileItem*)items, nitems,
+                                    mmax, nmax, (const T*)D, ldd, (T*)B, ldb, part, cols));
   return (int)hipGetLastError();
 }
 

@@ -149,3 +149,11 @@ _register("dtd", dtd)
 # ScaLAPACK-compatible shims (src/scalapack_wrappers): dp.scalapack.pdgemm_ ...
 from . import scalapack  # noqa: E402
 _register("scalapack", scalapack)
+
+# LDL^H without pivoting + random butterfly transformation (src/zhetrf.jdf, zhebut/zgebut/zgebmm, ztrdsm, ztrmdm)
+from .models import ldl as _ldl  # noqa: E402
+for _n, _f in (("hetrf", _ldl.hetrf), ("hetrf_New", _ldl.hetrf_New), ("trdsm", _ldl.trdsm),
+               ("trdsm_New", _ldl.trdsm_New), ("trmdm", _ldl.trmdm), ("trmdm_New", _ldl.trmdm_New),
+               ("hetrs", _ldl.hetrs), ("hebut", _ldl.hebut), ("gebut", _ldl.gebut), ("gebmm", _ldl.gebmm)):
+    register_op(_n, _f)
+_register("butterfly_vectors", _ldl.butterfly_vectors)

@@ -58,6 +58,8 @@ _SIGS = {
     "dpl_gessm": [c_int, c_int, c_vp, c_int, c_vp],                   # prec, n, items, max_n, stream
     "dpl_ssssm": [c_int, c_int, c_vp, c_int, c_int, c_int, c_vp],     # + ib, NB
     "dpl_tstrf": [c_int, c_int, c_vp, c_int, c_int, c_int, c_vp, c_vp],  # prec, n, items, ib, NB, max_m, info*, stream
+    # prec, part, cols, nitems, items, mmax, nmax, D, ldd, B, ldb, stream
+    "dpl_diag_scale": [c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp],
     # prec, kind, part, unit, nitems, items, A, lda, out, ostride, stream
     "dpl_tile_norm": [c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_int, c_vp],
 }

@@ -506,3 +506,25 @@ def row_gather(dst: torch.Tensor, src: torch.Tensor, pairs: np.ndarray, ncols: i
         d = torch.as_strided(dst, (ncols,), (ld_dst,), int(p["dst"]))
         s = torch.as_strided(src, (ncols,), (ld_src,), int(p["src"]))
         d.copy_(s)
+
+
+# ----------------------------------------------------------------------------- diagonal scaling (LDL^H)
+def diag_scale(part: int, cols: bool, D: torch.Tensor, ldd: int, B: torch.Tensor, ldb: int, batch: TileBatch):
+    """B_tile(i, j) /= d (d = D_tile(j, j) if cols else D_tile(i, i)) on the part mask; a_off -> D tile, b_off -> B tile."""
+    batch.finalize()
+    if len(batch) == 0:
+        return
+    p = _PART.get(part, 0)
+    if _is_gpu(B):
+        rc = _lib.load().dpl_diag_scale(_lib.prec_code(B.dtype), p, int(cols), len(batch.items),
+                                        batch.device_array(B.device).data_ptr(), batch.max_m, batch.max_n,
+                                        D.data_ptr(), ldd, B.data_ptr(), ldb, _lib.stream_ptr())
+        _lib.check(rc, "diag_scale")
+        return
+    for it in batch.items:
+        m, n = int(it["m"]), int(it["n"])
+        b = _view(B, it["b_off"], m, n, ldb)
+        k = n if cols else m
+        d = torch.as_strided(D, (k,), (ldd + 1,), int(it["a_off"]))
+        new = b / (d.view(1, -1) if cols else d.view(-1, 1))
+        b.copy_(torch.where(_part_mask(it, m, n, p), new, b))
