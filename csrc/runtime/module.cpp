@@ -4,8 +4,10 @@
 namespace py = pybind11;
 
 void register_dag(py::module_& m);
+void register_band(py::module_& m);
 
 PYBIND11_MODULE(_dplasma_rt, m) {
-  m.doc() = "dplasma_amd native runtime: tile-DAG analysis";
+  m.doc() = "dplasma_amd native runtime: tile-DAG analysis, band reductions";
   register_dag(m);
+  register_band(m);
 }

@@ -157,3 +157,14 @@ for _n, _f in (("hetrf", _ldl.hetrf), ("hetrf_New", _ldl.hetrf_New), ("trdsm", _
                ("hetrs", _ldl.hetrs), ("hebut", _ldl.hebut), ("gebut", _ldl.gebut), ("gebmm", _ldl.gebmm)):
     register_op(_n, _f)
 _register("butterfly_vectors", _ldl.butterfly_vectors)
+
+# Eigenvalues / singular values: two-sided band reductions (src/zherbt_*.jdf, zgebrd_ge2gb.jdf), band ->
+# tridiagonal bulge chase (src/zhbrdt.jdf, native C++), heev NoVec driver (src/zheev_wrapper.c)
+from .models import eigen as _eig  # noqa: E402
+for _n, _f in (("herbt", _eig.herbt), ("herbt_New", _eig.herbt_New), ("heev", _eig.heev), ("heev_New", _eig.heev_New),
+               ("gebrd_ge2gb", _eig.gebrd_ge2gb), ("gebrd_ge2gb_New", _eig.gebrd_ge2gb_New),
+               ("gebrd_ge2gbx", _eig.gebrd_ge2gbx), ("gebrd_ge2gbx_New", _eig.gebrd_ge2gbx_New)):
+    register_op(_n, _f)
+for _n in ("hbrdt", "diag_band_to_rect", "sterf", "band_singular_values", "eigvalsh", "gesvd_values"):
+    _register(_n, getattr(_eig, _n))
+_register("eigen_T", _eig.T_descriptor)

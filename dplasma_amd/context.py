@@ -60,6 +60,9 @@ class Context:
             else:
                 device = torch.device("cpu")
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            lr = int(os.environ.get("LOCAL_RANK", self.rank % max(1, torch.cuda.device_count())))
+            self.device = torch.device("cuda", lr)
         self.is_gpu = self.device.type == "cuda"
         self.nb_cores = nb_cores or int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
         if self.is_gpu:

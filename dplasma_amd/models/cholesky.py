@@ -43,6 +43,10 @@ class _Seq(Taskpool):
     def complete(self, ctx=None):
         r = self.parts[-1].complete(ctx or self.ctx)
         res = self.parts[self._rf]._result if self._rf < len(self.parts) - 1 else r
+        for fn in self._on_complete:
+            v = fn()
+            if v is not None:
+                res = v
         self._result = res
         return res
 

@@ -76,14 +76,16 @@ def _runs(kills):
     return [(c, np.array(p, dtype=np.int64), np.array(m, dtype=np.int64)) for c, p, m in out]
 
 
-def _factor(dag: TileDAG, X: _L, TS: _L, TT: _L, kd, tree):
-    """Tile QR of the logical matrix X along the elimination plan of ``tree``.
+def _factor(dag: TileDAG, X: _L, TS: _L, TT: _L, kd, tree, ks=None):
+    """Tile QR of the logical matrix X along the elimination plan of ``tree``
+    (only the panels in ``ks`` if given: one-sided panel steps of the
+    two-sided band reductions in models/eigen.py).
 
     Per panel k (zgeqrf.jdf / zgeqrf_param.jdf task classes): GEQRT on every
     head row, UNMQR of the head rows' trailing tiles, then the kills in plan
     order (TSQRT/TTQRT on the panel, TSMQR/TTMQR on the trailing tiles)."""
     MT, NT = X.mt, X.nt
-    for k in range(min(MT, NT)):
+    for k in (range(min(MT, NT)) if ks is None else ks):
         ck = int(X.cols(k))
         heads = np.array(tree.heads(k), dtype=np.int64)
         ns = np.arange(k + 1, NT)
@@ -104,13 +106,17 @@ def _factor(dag: TileDAG, X: _L, TS: _L, TT: _L, kd, tree):
                         np.stack([X.rows(vm[ii]), X.cols(nn), np.full(len(ii), ck)], 1))
 
 
-def _apply(dag: TileDAG, X: _L, TS: _L, TT: _L, C: _L, kd, conjtrans: bool, tree, K: int = None):
-    """C := Q^H C (conjtrans) or Q C, Q from _factor(X, tree) (zunmqr_L{C,N}[_param].jdf)."""
+def _apply(dag: TileDAG, X: _L, TS: _L, TT: _L, C: _L, kd, conjtrans: bool, tree, K: int = None, ks=None,
+           n0: int = 0):
+    """C := Q^H C (conjtrans) or Q C, Q from _factor(X, tree) (zunmqr_L{C,N}[_param].jdf).
+    ``ks``: apply only these panels' reflectors; ``n0``: only C's columns n0.. ."""
     K = min(X.mt, X.nt) if K is None else K
     NTc = C.nt
-    ns = np.arange(NTc)
+    ns = np.arange(n0, NTc)
     sfx = "_h" if conjtrans else ""
-    for k in (range(K) if conjtrans else range(K - 1, -1, -1)):
+    if ks is None:
+        ks = range(K) if conjtrans else range(K - 1, -1, -1)
+    for k in ks:
         ck = int(X.cols(k))
         heads = np.array(tree.heads(k), dtype=np.int64)
 

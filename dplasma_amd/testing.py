@@ -327,6 +327,65 @@ def t_print(h):
     dp.print(ctx, dp.dplasmaUpperLower, A)
 
 
+def t_heev(h):
+    """testing_zheev.c: eigenvalues of a Hermitian matrix vs LAPACK on the original."""
+    dp, a, ctx = h.dp, h.a, h.ctx
+    uplo = dp.dplasmaLower if a.uplo.upper() == "L" else dp.dplasmaUpper
+    A = h.mat(a.N, a.N)
+    dp.plghe(ctx, 0.0, dp.dplasmaUpperLower, A, a.seed)
+    a0 = _dense(h, A) if a.check else None
+    W = torch.zeros(a.N, dtype=torch.float64)
+    ib = a.IB or min(32, A.nb)
+    h.run_tp("heev", lambda: dp.heev_New(ctx, dp.dplasmaNoVec, uplo, A, W, ib=ib))
+    if a.check:
+        ref = torch.linalg.eigvalsh(a0.to(torch.complex128 if h.dt.is_complex else torch.float64))
+        res = float((W - ref).abs().max() / (ref.abs().max() * a.N * EPS[h.prec]))
+        h.check("max|w - w_lapack| / (||A|| N eps)", res, 60.0)
+
+
+def t_gebrd_ge2gb(h):
+    """testing_zgebrd_ge2gb.c: reduction to band bidiagonal; check its singular values."""
+    dp, a, ctx = h.dp, h.a, h.ctx
+    M, N = max(a.M or a.N, a.N), a.N
+    A = h.mat(M, N)
+    dp.plrnt(ctx, A, a.seed)
+    a0 = _dense(h, A) if a.check else None
+    ib = a.IB or min(32, A.nb)
+    tp_box = []
+
+    def build():
+        tp = dp.gebrd_ge2gb_New(ctx, ib, A)
+        tp_box.append(tp)
+        return tp
+    h.run_tp("gebrd_ge2gb", build)
+    if a.check:
+        s = torch.from_numpy(dp.band_singular_values(tp_box[-1].band, A.nb).copy())
+        ref = torch.linalg.svdvals(a0.to(torch.complex128 if h.dt.is_complex else torch.float64))
+        res = float((s - ref).abs().max() / (ref.max() * max(M, N) * EPS[h.prec]))
+        h.check("max|sigma - sigma_lapack| / (||A|| N eps)", res, 60.0)
+
+
+def t_hetrf(h):
+    """testing_zhebut.c: RBT + LDL^H without pivoting, then solve."""
+    dp, a, ctx = h.dp, h.a, h.ctx
+    K = a.K or 1
+    A = h.mat(a.N, a.N)
+    dp.plghe(ctx, float(a.N), dp.dplasmaUpperLower, A, a.seed)
+    a0 = _dense(h, A) if a.check else None
+    B = h.mat(a.N, K, name="B")
+    dp.plrnt(ctx, B, a.seed + 1)
+    b0 = _dense(h, B) if a.check else None
+    levels = 2 if a.N % 4 == 0 else 0
+    U = dp.hebut(ctx, A, levels) if levels else None
+    h.run_tp("hetrf", lambda: dp.hetrf_New(ctx, A))
+    dp.hetrs(ctx, A, B, U)
+    if a.check:
+        x = _dense(h, B)
+        res = float((a0 @ x - b0).abs().max() / ((a0.abs().max() * x.abs().max() + b0.abs().max()) * a.N
+                                                  * EPS[h.prec]))
+        h.check("||Ax-b|| / ((||A|| ||x|| + ||b||) N eps)", res, 60.0)
+
+
 def _dense(h, X):
     d = X.to_dense_local().cpu()
     if h.ctx.world > 1:
@@ -347,6 +406,7 @@ OPS = {
     "getrf_1d": lambda h: t_getrf(h, "1d"), "getrf_ptgpanel": lambda h: t_getrf(h, "ptgpanel"),
     "getrf_incpiv": lambda h: t_getrf(h, "incpiv"), "getrf_nopiv": lambda h: t_getrf(h, "nopiv"),
     "lange": t_lange, "lanm2": t_lanm2, "print": t_print,
+    "heev": t_heev, "gebrd_ge2gb": t_gebrd_ge2gb, "hetrf": t_hetrf, "hebut": t_hetrf,
 }
 
 

@@ -110,6 +110,30 @@ def fmuls_heev(n): return 2.0 / 3.0 * float(n) ** 3
 fadds_heev = fmuls_heev
 
 
+def fmuls_hetrd(n):
+    n = float(n)
+    return n * (n * (2.0 / 3.0 * n + 2.5) - 1.0 / 6.0)
+
+
+def fadds_hetrd(n):
+    n = float(n)
+    return n * (n * (2.0 / 3.0 * n + 1.0) - 8.0 / 3.0)
+
+
+def fmuls_gebrd(m, n):
+    m, n = float(m), float(n)
+    if m < n:
+        m, n = n, m
+    return n * (n * (2.0 * m - 2.0 / 3.0 * n + 2.0) + 20.0 / 3.0)
+
+
+def fadds_gebrd(m, n):
+    m, n = float(m), float(n)
+    if m < n:
+        m, n = n, m
+    return n * (n * (2.0 * m - 2.0 / 3.0 * n + 1.0) - m + 5.0 / 3.0)
+
+
 _OPS = {
     "gemm": (fmuls_gemm, fadds_gemm), "gemv": (fmuls_gemv, fadds_gemv),
     "symm": (fmuls_symm, fadds_symm), "hemm": (fmuls_symm, fadds_symm),
@@ -124,6 +148,7 @@ _OPS = {
     "ungqr": (fmuls_ungqr, fadds_ungqr), "unglq": (fmuls_ungqr, fadds_ungqr),
     "unmqr": (fmuls_unmqr, fadds_unmqr), "unmlq": (fmuls_unmqr, fadds_unmqr),
     "geqrs": (fmuls_geqrs, fadds_geqrs), "heev": (fmuls_heev, fadds_heev),
+    "hetrd": (fmuls_hetrd, fadds_hetrd), "herbt": (fmuls_hetrd, fadds_hetrd), "gebrd": (fmuls_gebrd, fadds_gebrd),
 }
 
 

@@ -1,0 +1,159 @@
+"""Eigenvalue / singular value pipeline: herbt, hbrdt (native bulge chase), heev, gebrd_ge2gb(x).
+
+Mirrors tests/testing_zheev.c (eigenvalues of the reduced matrix vs LAPACK on the
+original), testing_zhbrdt.c and testing_zgebrd_ge2gb.c of the reference; the
+LAPACK side is torch.linalg.eigvalsh / svdvals in float64 / complex128."""
+import numpy as np
+import pytest
+import torch
+
+import dplasma_amd as dp
+from dplasma_amd.models import eigen, qrtree
+from helpers import DTYPES, run_distributed
+
+TOL = {"s": 2e-4, "d": 1e-11, "c": 2e-4, "z": 1e-11}
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return dp.init(device="cpu")
+
+
+def _herm(N, dt, seed):
+    g = torch.Generator().manual_seed(seed)
+    M = torch.randn(N, N, dtype=torch.complex128 if dt.is_complex else torch.float64, generator=g)
+    return M + M.conj().T
+
+
+def _load(ctx, M, dt, NB, part=None):
+    A = dp.block_cyclic(ctx, dt, NB, NB, M.shape[0], M.shape[1])
+    src = M if part is None else part(M)
+    A.from_dense(src.to(dt))
+    return A
+
+
+def test_native_hbrdt_matches_dense():
+    rng = np.random.default_rng(3)
+    for n, b, cplx in ((40, 4, False), (33, 7, True), (64, 1, False), (5, 8, False)):
+        M = rng.standard_normal((n, n)) + (1j * rng.standard_normal((n, n)) if cplx else 0)
+        M = M + M.conj().T
+        Bm = np.tril(np.triu(M, -b), b)
+        ab = np.zeros((b + 1, n), dtype=M.dtype)
+        for d in range(min(b + 1, n)):
+            ab[d, :n - d] = np.diagonal(Bm, -d)
+        d, e = eigen.hbrdt(None, ab, b)
+        w = eigen.sterf(d, e)
+        assert np.abs(w - np.linalg.eigvalsh(Bm)).max() < 1e-12 * max(1.0, np.abs(w).max())
+
+
+def test_band_singular_values():
+    rng = np.random.default_rng(4)
+    n, kd = 37, 5
+    B = np.triu(np.tril(rng.standard_normal((n, n)), kd))
+    ab = np.zeros((kd + 1, n))
+    for s in range(kd + 1):
+        ab[kd - s, s:] = np.diagonal(B, s)
+    assert np.abs(eigen.band_singular_values(ab, kd) - np.linalg.svd(B, compute_uv=False)).max() < 1e-12
+
+
+@pytest.mark.parametrize("prec", list("sdcz"))
+@pytest.mark.parametrize("uplo", ["L", "U"])
+def test_heev(ctx, prec, uplo):
+    dt = DTYPES[prec]
+    N, NB = 75, 16
+    M = _herm(N, dt, 11)
+    lo = uplo == "L"
+    A = _load(ctx, M, dt, NB, torch.tril if lo else torch.triu)
+    W = torch.zeros(N, dtype=torch.float64)
+    assert dp.heev(ctx, dp.dplasmaNoVec, dp.dplasmaLower if lo else dp.dplasmaUpper, A, W, ib=8) == 0
+    ref = torch.linalg.eigvalsh(M.to(dt).to(M.dtype)).numpy()
+    assert np.abs(W.numpy() - ref).max() < TOL[prec] * np.abs(ref).max()
+
+
+def test_heev_rejects_vectors(ctx):
+    A = dp.block_cyclic(ctx, torch.float64, 8, 8, 16, 16)
+    with pytest.raises(NotImplementedError):
+        dp.heev(ctx, dp.dplasmaVec, dp.dplasmaLower, A, torch.zeros(16))
+
+
+def test_herbt_band_is_similar(ctx):
+    """After herbt the band (from the tiles) has the spectrum of A and everything else is reflector storage."""
+    N, NB = 64, 16
+    M = _herm(N, torch.float64, 5)
+    A = _load(ctx, M, torch.float64, NB, torch.tril)
+    T = eigen.T_descriptor(A, 4)
+    dp.herbt(ctx, dp.dplasmaLower, 4, A, T)
+    ab = eigen.diag_band_to_rect(ctx, A)
+    B = np.zeros((N, N))
+    for d in range(NB + 1):
+        B[np.arange(d, N), np.arange(N - d)] = ab[d, :N - d]
+    B = B + np.tril(B, -1).T
+    assert np.abs(np.linalg.eigvalsh(B) - torch.linalg.eigvalsh(M).numpy()).max() < 1e-11
+
+
+@pytest.mark.parametrize("prec", list("dz"))
+@pytest.mark.parametrize("shape", [(96, 96), (110, 80)])
+def test_ge2gb_singular_values(ctx, prec, shape):
+    dt = DTYPES[prec]
+    m, n = shape
+    NB = 16
+    g = torch.Generator().manual_seed(7)
+    G = torch.randn(m, n, dtype=dt, generator=g)
+    A = _load(ctx, G, dt, NB)
+    Band = dp.TiledMatrix(dt, NB + 1, NB, NB + 1, n, device="cpu")
+    ab = dp.gebrd_ge2gb(ctx, 8, A, Band)
+    assert torch.allclose(Band.to_dense_local(), torch.from_numpy(ab))
+    s = eigen.band_singular_values(ab, NB)
+    assert np.abs(s - torch.linalg.svdvals(G).numpy()).max() < 1e-11 * s.max()
+
+
+def test_ge2gbx_hierarchical_trees(ctx):
+    m, n, NB = 128, 96, 16
+    G = torch.randn(m, n, dtype=torch.float64, generator=torch.Generator().manual_seed(9))
+    A = _load(ctx, G, torch.float64, NB)
+    T = [eigen.T_descriptor(A, 4) for _ in range(4)]
+    qt = qrtree.hqr_init(dp.dplasmaNoTrans, A, qrtree.GREEDY_TREE, qrtree.FLAT_TREE, 2, 1)
+    lt = qrtree.FlatTree(A.nt - 1, A.mt)
+    ab = dp.gebrd_ge2gbx(ctx, 4, qt, lt, A, *T)
+    s = eigen.band_singular_values(ab, NB)
+    assert np.abs(s - torch.linalg.svdvals(G).numpy()).max() < 1e-11 * s.max()
+
+
+def _worker(rank, world, P):
+    ctx = dp.init(device="cpu", P=P)
+    N, NB = 70, 16
+    M = _herm(N, torch.complex128, 21)
+    A = dp.block_cyclic(ctx, torch.complex128, NB, NB, N, N)
+    A.from_dense(torch.tril(M))
+    W = torch.zeros(N, dtype=torch.float64)
+    dp.heev(ctx, dp.dplasmaNoVec, dp.dplasmaLower, A, W, ib=8)
+    G = torch.randn(80, 64, dtype=torch.float64, generator=torch.Generator().manual_seed(2))
+    B = dp.block_cyclic(ctx, torch.float64, NB, NB, 80, 64)
+    B.from_dense(G)
+    s = eigen.gesvd_values(ctx, B, ib=8)
+    return (float(np.abs(W.numpy() - torch.linalg.eigvalsh(M).numpy()).max()),
+            float(np.abs(s - torch.linalg.svdvals(G).numpy()).max()))
+
+
+def test_eigen_distributed(ctx):
+    for e_heev, e_svd in run_distributed(_worker, 4, 2).values():
+        assert e_heev < 1e-11 and e_svd < 1e-11
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", list("dz"))
+def test_gpu_heev_ge2gb(prec):
+    dt = DTYPES[prec]
+    g = dp.init(device="cuda")
+    N, NB = 512, 64
+    M = _herm(N, dt, 13)
+    A = dp.block_cyclic(g, dt, NB, NB, N, N)
+    A.from_dense(torch.tril(M).to(dt))
+    W = torch.zeros(N, dtype=torch.float64)
+    dp.heev(g, dp.dplasmaNoVec, dp.dplasmaLower, A, W, ib=32)
+    assert np.abs(W.numpy() - torch.linalg.eigvalsh(M).numpy()).max() < 1e-10 * N
+    G = torch.randn(640, N, dtype=dt, generator=torch.Generator().manual_seed(3))
+    B = dp.block_cyclic(g, dt, NB, NB, 640, N)
+    B.from_dense(G)
+    s = eigen.gesvd_values(g, B, ib=32)
+    assert np.abs(s - torch.linalg.svdvals(G).numpy()).max() < 1e-10 * s.max()

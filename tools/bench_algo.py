@@ -52,6 +52,17 @@ def main():
             IPIV = dp.ipiv_descriptor(ctx, A)
             t0 = time.perf_counter()
             tp = dp.getrf_1d_New(ctx, A, IPIV)
+        elif a.op in ("herbt", "heev"):
+            dp.plghe(ctx, 0.0, dp.dplasmaLower, A, 3872)
+            t0 = time.perf_counter()
+            if a.op == "herbt":
+                tp = dp.herbt_New(ctx, dp.dplasmaLower, a.ib, A, dp.eigen_T(A, a.ib))
+            else:
+                W = torch.zeros(N, dtype=torch.float64)
+                tp = dp.heev_New(ctx, dp.dplasmaNoVec, dp.dplasmaLower, A, W, ib=a.ib)
+        elif a.op == "gebrd_ge2gb":
+            t0 = time.perf_counter()
+            tp = dp.gebrd_ge2gb_New(ctx, a.ib, A)
         else:
             raise SystemExit(f"unknown op {a.op}")
         torch.cuda.synchronize()

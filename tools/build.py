@@ -87,7 +87,7 @@ def build_runtime(force=False) -> Path | None:
         return lib
     inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", f"-I{RSRC}",
            "-I/opt/rocm/include"]
-    cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-D__HIP_PLATFORM_AMD__",
+    cmd = ["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-D__HIP_PLATFORM_AMD__",
            *inc, *map(str, srcs), "-o", str(lib), "-L/opt/rocm/lib", "-lamdhip64", "-lpthread",
            "-Wl,-rpath,/opt/rocm/lib"]
     _run(cmd)
