@@ -168,3 +168,27 @@ for _n, _f in (("herbt", _eig.herbt), ("herbt_New", _eig.herbt_New), ("heev", _e
 for _n in ("hbrdt", "diag_band_to_rect", "sterf", "band_singular_values", "eigvalsh", "gesvd_values"):
     _register(_n, getattr(_eig, _n))
 _register("eigen_T", _eig.T_descriptor)
+
+# Tracing / profiling (PaRSEC profiling + --dot + DPLASMA_TRACE_KERNELS analogues) and dplasma_info_t options
+from .utils import trace as _trace  # noqa: E402
+from .utils import info as _info  # noqa: E402
+for _n in ("profiling_start", "profiling_stop", "Tracer"):
+    _register(_n, getattr(_trace, _n))
+
+
+def dot_start(ctx, path):
+    """Append the DOT graph of every tile DAG compiled from now on to ``path`` (``--dot``)."""
+    open(path, "w").close()
+    ctx.dot_file = path
+
+
+def dot_stop(ctx):
+    ctx.dot_file = None
+
+
+_register("dot_start", dot_start)
+_register("dot_stop", dot_stop)
+_register("Info", _info.Info)
+_register("info_create", _info.info_create)
+for _n in ("set", "get", "get_nkeys", "get_nthkey", "delete", "free"):
+    _register("info_" + _n, (lambda m: (lambda inf, *a: getattr(inf, m)(*a)))(_n))

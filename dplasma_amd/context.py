@@ -83,6 +83,10 @@ class Context:
         self._build_groups()
         self._queue = []
         self.profiling = None  # utils.trace.Tracer when enabled
+        self.dot_file = os.environ.get("DPLASMA_DOT") or None  # DOT dump of every compiled tile DAG
+        if os.environ.get("DPLASMA_PROFILE"):
+            from .utils.trace import Tracer
+            self.profiling = Tracer(self)
         from .utils.info import Info
         self.info = Info()
 
@@ -145,5 +149,9 @@ def init(nb_cores=None, device=None, P=None, Q=None, gpus=None, verbose=0) -> Co
 
 def fini(ctx: Optional[Context] = None):
     global _DEFAULT
+    c = ctx or _DEFAULT
+    path = os.environ.get("DPLASMA_PROFILE")
+    if c is not None and c.profiling is not None and path:
+        c.profiling.dump(path if c.world == 1 else path)
     if ctx is None or ctx is _DEFAULT:
         _DEFAULT = None

@@ -40,6 +40,7 @@ import torch
 import torch.distributed as dist
 
 from ..constants import STORAGE_TILE
+from ..utils import trace
 from .taskpool import Taskpool
 
 DAG_ITEM = np.dtype([("p0", "<u8"), ("p1", "<u8"), ("p2", "<u8"), ("p3", "<u8"),
@@ -272,6 +273,9 @@ class TileDAG:
         else:
             level = rt.dag_levels(ops, modes) if rt is not None else _levels_py(ops, modes)
         nlev = int(level.max()) + 1
+        dot = getattr(ctx, "dot_file", None)
+        if dot and me == 0:
+            self._write_dot(dot, ops, modes, kid, level)
         # executor rank per task
         exec_key = ops[np.arange(ntask), np.array([self.kinds[k].exec_role for k in range(len(self.kinds))])[kid]]
         exe = self._home(exec_key) if world > 1 else np.zeros(ntask, dtype=np.int64)
@@ -482,6 +486,31 @@ class TileDAG:
         return tp.finish_build()
 
 
+    def _write_dot(self, path, ops, modes, kid, level, max_tasks: int = 20000):
+        """Append this DAG (tasks as nodes labelled kind(m,n), RAW/WAR/WAW edges, ranked by
+        level) to a DOT file -- the ``--dot`` / ``parsec_dot`` dump of the reference."""
+        rt = _lib_rt()
+        n = len(kid)
+        if rt is None or n > max_tasks:
+            with open(path, "a") as f:
+                f.write(f"// {self.name}: {n} tasks, not dumped (limit {max_tasks})\n")
+            return
+        _, _, esrc, edst = rt.dag_schedule(ops, modes)
+        ex = np.array([self.kinds[k].exec_role for k in range(len(self.kinds))])[kid]
+        key = ops[np.arange(n), ex]
+        name = self.name.replace('"', "")
+        with open(path, "a") as f:
+            f.write(f'digraph "{name}" {{\n  rankdir=TB; node [shape=box, fontsize=9];\n')
+            for t in range(n):
+                k = int(key[t])
+                nm = self.kinds[int(kid[t])].name
+                m, c = (k >> _M_SHIFT) & _MASK22, k & _MASK22
+                f.write(f'  t{t} [label="{nm}({m},{c})\\nL{int(level[t])}"];\n')
+            for a, b in zip(esrc.tolist(), edst.tolist()):
+                f.write(f"  t{a} -> t{b};\n")
+            f.write("}\n")
+
+
 class _DagProgram:
     def __init__(self, dag: TileDAG, nlev, groups, xch, dtype, device, multistream):
         self.dag = dag
@@ -495,7 +524,11 @@ class _DagProgram:
         self.multistream = multistream
         self.nlaunch = len(groups)
 
-    def _exchange(self, plans):
+    def _exchange(self, plans, level=-1):
+        with trace.span(self.dag.ctx, f"{self.dag.name}:exchange", "comm", args={"level": level}):
+            self._exchange_now(plans)
+
+    def _exchange_now(self, plans):
         bases = self.dag._bases
         for dt, pack, unpack, sc, rc in plans:
             sendbuf = torch.empty(sum(sc), dtype=dt, device=self.device)
@@ -508,6 +541,11 @@ class _DagProgram:
                 copy_tiles(bases[bi], ld, recvbuf, mb, tb, to_b=False)
 
     def _launch(self, g, dev_items, stream_ptr, stream_obj=None):
+        with trace.span(self.dag.ctx, g["K"].name, "dag", stream_obj,
+                        {"level": g["level"], "tasks": g["n"], "dag": self.dag.name}):
+            self._launch_now(g, dev_items, stream_ptr, stream_obj)
+
+    def _launch_now(self, g, dev_items, stream_ptr, stream_obj=None):
         K = g["K"]
         if K.body is not None:
             self._run_bodies(g, stream_obj)
@@ -547,12 +585,12 @@ class _DagProgram:
         for L in range(self.nlev):
             x = self.xch.get((L, "f"))
             if x is not None:
-                self._exchange(x)
+                self._exchange(x, L)
             for gi in self.by_level.get(L, ()):
                 self._launch(self.groups[gi], dev_items, stream)
             x = self.xch.get((L, "w"))
             if x is not None:
-                self._exchange(x)
+                self._exchange(x, L)
 
     def _run_streams(self, dev_items):
         """Dataflow over two streams: zero-slack (critical-path) groups on a

@@ -70,7 +70,12 @@ class Taskpool:
 
     # ------------------------------------------------------------------ execute
     def run(self, ctx=None):
+        from ..utils import trace
         ctx = ctx or self.ctx
+        with trace.span(ctx, self.name, "taskpool", args={"tasks": len(self.tasks), "gflop": self.flops / 1e9}):
+            self._run(ctx)
+
+    def _run(self, ctx):
         t0 = time.perf_counter()
         if ctx is not None and ctx.is_gpu:
             from . import engine

@@ -32,6 +32,7 @@ from ..constants import dplasmaNoTrans
 from ..ops import tile_ops as ops
 from ..ops.batch import GemmBatch, TileBatch
 from ..parallel.exchange import ExchangePlan
+from ..utils import trace
 from .taskpool import Taskpool
 
 Key = Tuple[int, int, int]  # (matrix id, m, n)
@@ -277,6 +278,11 @@ class _StageRunner:
         self.launches.append(("map", ("lascal", 0, beta, out[0], tb)))
 
     def run(self):
+        with trace.span(self.prog.ctx, f"{self.prog.name}:{self.st.name}", "stage",
+                        args={"launches": len(self.launches), "exchange": self.plan is not None}):
+            self._run()
+
+    def _run(self):
         mats = self.prog.mats
         if self.plan is not None:
             self.buf = self.plan.new_recv_buffer()

@@ -52,6 +52,7 @@ def _parse(argv):
     ap.add_argument("-v", "--verbose", type=int, nargs="?", const=1, default=0)
     ap.add_argument("-g", "--gpus", type=int, default=-1, help="0: CPU only; default: GPU when present")
     ap.add_argument("--dot", default=None, help="write the DAG of DAG-based ops to this DOT file")
+    ap.add_argument("--trace", default=None, help="write a Chrome trace (all ranks) of the timed runs to this file")
     return ap.parse_args(argv)
 
 
@@ -79,6 +80,10 @@ class Harness:
         self.name = a.op[1:]
         self.dt = PRECS[self.prec]
         self.ok = True
+        if a.dot:
+            dp.dot_start(self.ctx, a.dot)
+        if a.trace:
+            dp.profiling_start(self.ctx)
 
     # ------------------------------------------------------------ helpers
     def mat(self, m, n, mb=None, nb=None, name="A"):
@@ -112,8 +117,9 @@ class Harness:
             ctx.sync()
             ctx.barrier()
             t2 = time.perf_counter()
-            if self.a.dot and getattr(tp, "dag", None) is not None and ctx.rank == 0:
-                pass  # DOT dumps are produced by TileDAG.dot before compile (see _dag_dot)
+            if ctx.profiling is not None:
+                ctx.profiling.save_info(f"{opname}:TIME_ELAPSED", t2 - t1)
+                ctx.profiling.save_info(f"{opname}:GFLOPS", tp.flops / max(t2 - t1, 1e-12) / 1e9)
             tp.destruct()
             t3 = time.perf_counter()
             self.report(opname, t2 - t1, tp.flops, t_enq, t3 - t2)
@@ -417,6 +423,10 @@ def main(argv=None):
     if fn is None:
         raise SystemExit(f"unknown operation {h.name}; available: {', '.join(sorted(OPS))}")
     fn(h)
+    if a.trace:
+        tr = h.dp.profiling_stop(h.ctx, a.trace)
+        if h.ctx.rank == 0 and a.verbose:
+            tr.print_summary()
     if h.ctx.world > 1:
         import torch.distributed as dist
         dist.barrier()
