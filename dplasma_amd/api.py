@@ -192,3 +192,14 @@ _register("Info", _info.Info)
 _register("info_create", _info.info_create)
 for _n in ("set", "get", "get_nkeys", "get_nthkey", "delete", "free"):
     _register("info_" + _n, (lambda m: (lambda inf, *a: getattr(inf, m)(*a)))(_n))
+
+# Hybrid LU-QR (src/zgetrf_qrf.jdf, ztrsmpl_qrf.jdf, include/dplasma/lu_qr.h criteria)
+from .models import lu_qr as _luqr  # noqa: E402
+for _n, _f in (("getrf_qrf", _luqr.getrf_qrf), ("getrf_qrf_New", _luqr.getrf_qrf_New),
+               ("trsmpl_qrf", _luqr.trsmpl_qrf), ("trsmpl_qrf_New", _luqr.trsmpl_qrf_New),
+               ("gesv_qrf", _luqr.gesv_qrf)):
+    register_op(_n, _f)
+_register("qrf_ipiv_descriptor", _luqr.qrf_ipiv_descriptor)
+for _n in ("DEFAULT_CRITERIUM", "HIGHAM_CRITERIUM", "MUMPS_CRITERIUM", "LU_ONLY_CRITERIUM", "QR_ONLY_CRITERIUM",
+           "RANDOM_CRITERIUM", "HIGHAM_SUM_CRITERIUM", "HIGHAM_MAX_CRITERIUM", "HIGHAM_MOY_CRITERIUM"):
+    _register(_n, getattr(_luqr, _n))

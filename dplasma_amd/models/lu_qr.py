@@ -1,0 +1,354 @@
+"""Hybrid LU-QR factorization (per panel: a stable-enough LU step, else an HQR step).
+
+Reference: ``src/zgetrf_qrf.jdf`` (LU part: ``zgetrf`` / ``swptrsm_u`` /
+``ztrsm_l`` / ``zgemm`` :77-276; QR part ``zgeqrt`` / ``zunmqr`` / ``zttqrt`` /
+``zttmqr`` :277-640; decision: ``copypanel`` :645, ``zlufacto`` :739,
+``reduce_norm`` :847, ``setchoice`` :937-1150, ``selector`` :1193),
+``src/ztrsmpl_qrf.jdf``, ``src/zgetrf_qrf_wrapper.c`` (random LU table
+``dplasma_genrandom_lutab``), ``src/include/dplasma/lu_qr.h`` (criteria) and
+``tests/testing_zgetrf_qrf.c`` (trsmpl_qrf + trsm(U) solve check).
+
+Semantics (as the reference): at step k the *diagonal domain* is the set of
+panel tiles m = k, k+p, k+2p, ... (p = process-grid rows: the tiles that live
+with the diagonal tile).  They are stacked and factored by LU with partial
+pivoting; a criterion then compares a measure of that factorization with the
+off-domain tiles of the panel:
+
+=====================  =========================================================
+DEFAULT (0)            alternate: LU on odd steps
+HIGHAM (1)             alpha * cond(U_kk) > sum_i ||A_ik||_1
+MUMPS (2)              alpha * max|A_kk(:,j)| >= max_i max|A_ik(:,j)| for all j
+LU_ONLY / QR_ONLY      always LU / always QR
+RANDOM (5)             lu_tab from a balanced random split with alpha % LU steps
+HIGHAM_SUM/MAX/MOY     alpha / ||(L U)_kk^-1||_1 > sum / max / mean of ||A_ik||_1
+=====================  =========================================================
+
+alpha = 0 forces QR, alpha >= 9999999999 forces LU, a singular domain forces QR.
+An LU step swaps rows inside the domain stack of every trailing column, solves
+A(k, n) with L_kk, the off-domain A(m, k) with U_kk (no pivoting across
+domains -- what the criterion guards) and updates the trailing matrix; a QR
+step is one panel of hierarchical QR on the given tree.  lu_tab[k] records the
+choice (1 = LU); IPIV(k, k) holds the domain pivots (1-based rows of the stack).
+
+MI355X design: the domain LU runs on a contiguous copy of the stacked domain
+tiles on the diagonal owner (the GPU panel kernel), so A's panel is untouched
+until the decision -- the QR fallback needs no restore copy.  The decision is
+one small allreduce (criterion values + pivots + info) per step; the LU step is
+a TileProgram (row moves with the row-gather kernel, then batched TRSM and
+MFMA GEMM launches) and the QR step a one-panel tile DAG (GEQRT / TTQRT /
+TSMQR / TTMQR batched kernels, models/qr.py).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..constants import dplasmaLeft, dplasmaLower, dplasmaNoTrans, dplasmaNonUnit, dplasmaRight, dplasmaUnit, dplasmaUpper
+from ..descriptor import TiledMatrix
+from ..ops import qr_ops
+from ..ops import tile_ops as ops
+from ..parallel import comm
+from ..runtime.dag import TileDAG
+from ..runtime.taskpool import Taskpool
+from ..runtime.tileprog import TileProgram
+from ..utils.flops import flops
+from . import qr, qrtree
+from .lu import _perm_from_swaps, _permute_rows_2d
+
+DEFAULT_CRITERIUM = 0
+HIGHAM_CRITERIUM = 1
+MUMPS_CRITERIUM = 2
+LU_ONLY_CRITERIUM = 3
+QR_ONLY_CRITERIUM = 4
+RANDOM_CRITERIUM = 5
+HIGHAM_SUM_CRITERIUM = 6
+HIGHAM_MAX_CRITERIUM = 7
+HIGHAM_MOY_CRITERIUM = 8
+_HIGHAMS = (HIGHAM_CRITERIUM, HIGHAM_SUM_CRITERIUM, HIGHAM_MAX_CRITERIUM, HIGHAM_MOY_CRITERIUM)
+
+N_ = dplasmaNoTrans
+
+
+def qrf_ipiv_descriptor(ctx, A, name="IPIV") -> TiledMatrix:
+    """Pivot storage aligned with A: tile (k, k) (mb ints) holds step k's domain pivots."""
+    return TiledMatrix(torch.int32, A.mb, 1, A.mt * A.mb, A.nt, P=A.grid.P, Q=A.grid.Q, rank=A.rank,
+                       device=A.device, name=name)
+
+
+def genrandom_lutab(lu_tab, deb, fin, nb_lu, rec_depth=0):
+    """Balanced recursive split of nb_lu LU steps over [deb, fin] (dplasma_genrandom_lutab)."""
+    if deb == fin:
+        lu_tab[deb] = int(nb_lu != 0)
+        return
+    n = fin - deb + 1
+    new_fin = deb - 1 + n // 2 if n % 2 == 0 else deb - 1 + (fin - deb) // 2 + (rec_depth % 2)
+    new_nb = nb_lu // 2 if nb_lu % 2 == 0 else (nb_lu - 1) // 2 + (rec_depth % 2)
+    genrandom_lutab(lu_tab, deb, new_fin, new_nb, rec_depth + 1)
+    genrandom_lutab(lu_tab, new_fin + 1, fin, nb_lu - new_nb, rec_depth + 1)
+
+
+def _lapack(name, arr):
+    from scipy.linalg import lapack
+    return lapack.get_lapack_funcs((name,), (arr,))[0]
+
+
+class _Step:
+    """Shared per-step geometry."""
+
+    def __init__(self, A, k, p):
+        self.k = k
+        self.dom = list(range(k, A.mt, p))
+        self.off = [m for m in range(k + 1, A.mt) if (m - k) % p]
+        self.rows = [A.tile_rows(m) for m in self.dom]
+        self.M = sum(self.rows)
+        self.ncol = A.tile_cols(k)
+        self.kmax = min(self.M, self.ncol)
+        self.owner = A.rank_of(k, k)
+        # global element rows of the stacked domain, in stack order
+        self.grow = np.concatenate([np.arange(m * A.mb, m * A.mb + r) for m, r in zip(self.dom, self.rows)])
+
+
+class _GetrfQrf(Taskpool):
+    def __init__(self, ctx, tree, A, IPIV, TS, TT, criteria, alpha, lu_tab, info, p):
+        super().__init__("getrf_qrf", ctx)
+        self.tree, self.A, self.IPIV, self.TS, self.TT = tree, A, IPIV, TS, TT
+        self.criteria, self.alpha = criteria, float(alpha)
+        self.minMNT = min(A.mt, A.nt)
+        self.lu_tab = lu_tab if lu_tab is not None else [0] * self.minMNT
+        self.info_out = info
+        self.p = p or A.grid.P
+        self.kd = qr_ops.kinds(A.dtype, TS.mb, (0, 0), (0, 0))
+        self.flops = flops(A.prec, "getrf", A.m, A.n)
+        if criteria == RANDOM_CRITERIUM:
+            genrandom_lutab(self.lu_tab, 0, self.minMNT - 1, int(round(self.minMNT * self.alpha / 100.0)), 0)
+        self.finish_build()
+
+    # ------------------------------------------------------------------ one panel
+    def _domain_lu(self, st: _Step):
+        """Stacked LU of the domain on the diagonal owner -> (buffer, ipiv, info, W0, colmax)."""
+        A = self.A
+        buf = torch.empty(st.ncol * st.M, dtype=A.dtype, device=A.device)
+        view = torch.as_strided(buf, (st.M, st.ncol), (1, st.M))
+        r0 = 0
+        for m, r in zip(st.dom, st.rows):
+            view[r0:r0 + r].copy_(A.tile(m, st.k))
+            r0 += r
+        colmax = None
+        if self.criteria == MUMPS_CRITERIUM:
+            colmax = A.tile(st.k, st.k)[:st.ncol, :st.ncol].abs().amax(0).double().cpu().numpy()
+        ipiv = torch.zeros(max(st.kmax, 1), dtype=torch.int32, device=A.device)
+        info = torch.zeros(1, dtype=torch.int32, device=A.device)
+        ops.getrf_panel(buf, 0, st.M, st.ncol, st.M, ipiv, info, 0, pivot=True)
+        w0 = 0.0
+        bad = int(info.item()) != 0
+        if not bad and self.criteria in _HIGHAMS:
+            lu = view[:st.ncol, :st.ncol].cpu().numpy()
+            lu = np.asfortranarray(lu.astype(np.complex128 if A.dtype.is_complex else np.float64))
+            if self.criteria == HIGHAM_CRITERIUM:
+                rc, _ = _lapack("trcon", lu)(lu, norm="1", uplo="U", diag="N")
+                w0 = 1.0 / rc if rc > 0 else np.inf
+            else:
+                rc, _ = _lapack("gecon", lu)(lu, 1.0, norm="1")
+                w0 = float(rc)
+        return buf, view, ipiv, bad, w0, colmax
+
+    def _offdomain_norms(self, st: _Step):
+        """Local partial (sum, max, count) of off-domain tile 1-norms, or per-column max (MUMPS)."""
+        A = self.A
+        s, mx, cnt = 0.0, 0.0, 0
+        cm = np.zeros(A.nb)
+        for m in st.off:
+            if not A.is_local(m, st.k):
+                continue
+            t = A.tile(m, st.k)
+            if self.criteria == MUMPS_CRITERIUM:
+                c = t.abs().amax(0).double().cpu().numpy()
+                cm[:len(c)] = np.maximum(cm[:len(c)], c)
+            else:
+                v = float(t.abs().sum(0).max())
+                s, mx, cnt = s + v, max(mx, v), cnt + 1
+        return s, mx, cm
+
+    def _decide(self, st: _Step, mine):
+        """Collective decision: every rank returns the same (do_lu, ipiv)."""
+        A, ctx = self.A, self.ctx
+        me = ctx.rank
+        s, mx, cm = self._offdomain_norms(st)
+        nb = A.nb
+        # SUM vector: [w0, bad, offsum, ipiv(nb), colmax_diag(nb)]; MAX vector: [offmax, colmax_off(nb)]
+        vs = torch.zeros(3 + 2 * nb, dtype=torch.float64)
+        vm = torch.zeros(1 + nb, dtype=torch.float64)
+        if me == st.owner:
+            _, _, ipiv, bad, w0, colmax = mine
+            vs[0], vs[1] = (0.0 if bad else w0), float(bad)
+            vs[3:3 + st.kmax] = ipiv[:st.kmax].double().cpu()
+            if colmax is not None:
+                vs[3 + nb:3 + nb + len(colmax)] = torch.from_numpy(colmax)
+        vs[2] = s
+        vm[0] = mx
+        vm[1:] = torch.from_numpy(cm)
+        if ctx.world > 1:
+            dv = ctx.device
+            a, b = vs.to(dv), vm.to(dv)
+            comm.allreduce(a)
+            comm.allreduce(b, op=torch.distributed.ReduceOp.MAX)
+            vs, vm = a.cpu(), b.cpu()
+        w0, bad, offsum, offmax = float(vs[0]), vs[1] > 0, float(vs[2]), float(vm[0])
+        ipiv = vs[3:3 + st.kmax].round().to(torch.int64).numpy()
+        k, alpha, crit = st.k, self.alpha, self.criteria
+        if bad:
+            cond = 0
+        elif crit in (HIGHAM_CRITERIUM, HIGHAM_SUM_CRITERIUM):
+            cond = int(alpha * w0 > offsum)
+        elif crit == HIGHAM_MAX_CRITERIUM:
+            cond = int(alpha * w0 > offmax)
+        elif crit == HIGHAM_MOY_CRITERIUM:
+            nt_ = A.mt - k
+            nout = nt_ - (nt_ + self.p - 1) // self.p
+            cond = int(alpha * w0 > (offsum / nout if nout else 0.0))
+        elif crit == MUMPS_CRITERIUM:
+            diag = vs[3 + nb:3 + nb + st.ncol].numpy()
+            off = vm[1:1 + st.ncol].numpy()
+            cond = int(bool(np.all(alpha * diag >= off)))
+        elif crit == LU_ONLY_CRITERIUM:
+            cond = 1
+        elif crit == QR_ONLY_CRITERIUM:
+            cond = 0
+        elif crit == RANDOM_CRITERIUM:
+            cond = int(self.lu_tab[k])
+        else:
+            cond = k % 2
+        if not bad:
+            if alpha == 0:
+                cond = 0
+            if alpha >= 9999999999:
+                cond = 1
+        return cond, ipiv
+
+    def _lu_step(self, st: _Step, mine, ipiv):
+        A, ctx, k = self.A, self.ctx, st.k
+        if ctx.rank == st.owner:
+            buf, view, _, _, _, _ = mine
+            r0 = 0
+            for m, r in zip(st.dom, st.rows):
+                A.tile(m, k).copy_(view[r0:r0 + r])
+                r0 += r
+        if self.IPIV.is_local(k, k):
+            t = self.IPIV.tile(k, k)
+            t.zero_()
+            t[:st.kmax, 0] = torch.from_numpy(ipiv + 1).to(torch.int32).to(t.device)
+        # row interchanges inside the domain stack of the trailing columns (all on k's process row)
+        perm = _perm_from_swaps(ipiv, st.M)
+        mv = np.nonzero(perm != np.arange(st.M))[0]
+        trail = [n for n in range(k + 1, A.nt) if A.col_is_local(n)]
+        _permute_rows_2d(ctx, A, st.grow[mv], st.grow[perm[mv]], trail)
+        prog = TileProgram(ctx, f"getrf_qrf_lu({k})")
+        s = prog.stage("trsm")
+        for n in range(k + 1, A.nt):
+            s.trsm(dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, (A, k, k), (A, k, n))
+        for m in st.off:
+            s.trsm(dplasmaRight, dplasmaUpper, N_, dplasmaNonUnit, 1.0, (A, k, k), (A, m, k))
+        if k + 1 < A.nt:
+            s = prog.stage("gemm")
+            for m in range(k + 1, A.mt):
+                for n in range(k + 1, A.nt):
+                    s.gemm((A, m, n), [((A, m, k), N_, (A, k, n), N_)], alpha=-1.0, beta=1.0)
+        prog.compile().execute(ctx)
+
+    def _qr_step(self, st: _Step):
+        A, ctx, k = self.A, self.ctx, st.k
+        if self.IPIV.is_local(k, k):
+            self.IPIV.tile(k, k).zero_()
+        dag = TileDAG(ctx, f"getrf_qrf_qr({k})")
+        qr._factor(dag, qr._L(A), qr._L(self.TS), qr._L(self.TT), self.kd, self.tree, ks=[k])
+        dag.compile().execute(ctx)
+
+    def run(self, ctx=None):
+        import time
+        self._t_run = time.perf_counter()
+        A = self.A
+        ctx = self.ctx
+        for k in range(self.minMNT):
+            st = _Step(A, k, self.p)
+            mine = self._domain_lu(st) if ctx.rank == st.owner else None
+            cond, ipiv = self._decide(st, mine)
+            self.lu_tab[k] = cond
+            if cond:
+                self._lu_step(st, mine, ipiv)
+            else:
+                self._qr_step(st)
+        if self.info_out is not None:
+            self.info_out[0] = 0
+
+    def complete(self, ctx=None):
+        if self.ctx.is_gpu:
+            torch.cuda.current_stream(self.ctx.device).synchronize()
+        self._result = 0
+        return 0
+
+
+def getrf_qrf_New(ctx, qrtree_, A, IPIV, TS, TT, criteria=DEFAULT_CRITERIUM, alpha=1.0, lu_tab=None, INFO=None,
+                  p=None):
+    """Hybrid LU-QR factorization (dplasma_zgetrf_qrf_New).  ``p``: domain period (default: grid rows)."""
+    qr._check_square_tiles(A)
+    if TS.nb != A.nb or TT.nb != A.nb:
+        raise ValueError("TS/TT must have tiles of ib x nb")
+    return _GetrfQrf(ctx, qrtree_, A, IPIV, TS, TT, criteria, alpha, lu_tab, INFO, p)
+
+
+def getrf_qrf(ctx, qrtree_, A, IPIV, TS, TT, criteria=DEFAULT_CRITERIUM, alpha=1.0, lu_tab=None, INFO=None, p=None):
+    getrf_qrf_New(ctx, qrtree_, A, IPIV, TS, TT, criteria, alpha, lu_tab, INFO, p).execute(ctx)
+    return 0
+
+
+def trsmpl_qrf(ctx, qrtree_, A, IPIV, B, TS, TT, lu_tab, p=None):
+    """Apply the hybrid factorization's L / Q^H to B: B := (L_k or Q_k)^-1 ... B (dplasma_ztrsmpl_qrf);
+    then solve with the upper triangle of A (trsm Left Upper NoTrans NonUnit) to get x."""
+    p = p or A.grid.P
+    kd = qr_ops.kinds(A.dtype, TS.mb, (0, 0), (0, 0))
+    for k in range(min(A.mt, A.nt)):
+        if lu_tab[k]:
+            st = _Step(A, k, p)
+            piv = torch.zeros(A.mb, dtype=torch.float64)
+            if IPIV.is_local(k, k):
+                piv[:] = IPIV.tile(k, k)[:, 0].double().cpu()
+            if ctx.world > 1:
+                d = piv.to(ctx.device)
+                comm.allreduce(d)
+                piv = d.cpu()
+            ipiv = piv[:st.kmax].round().to(torch.int64).numpy() - 1
+            perm = _perm_from_swaps(ipiv, st.M)
+            mv = np.nonzero(perm != np.arange(st.M))[0]
+            cols = [n for n in range(B.nt) if B.col_is_local(n)]
+            _permute_rows_2d(ctx, B, st.grow[mv], st.grow[perm[mv]], cols)
+            prog = TileProgram(ctx, f"trsmpl_qrf_lu({k})")
+            s = prog.stage("trsm")
+            for n in range(B.nt):
+                s.trsm(dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, (A, k, k), (B, k, n))
+            if k + 1 < B.mt:
+                s = prog.stage("gemm")
+                for m in range(k + 1, B.mt):
+                    for n in range(B.nt):
+                        s.gemm((B, m, n), [((A, m, k), N_, (B, k, n), N_)], alpha=-1.0, beta=1.0)
+            prog.compile().execute(ctx)
+        else:
+            dag = TileDAG(ctx, f"trsmpl_qrf_qr({k})")
+            qr._apply(dag, qr._L(A), qr._L(TS), qr._L(TT), qr._L(B), kd, True, qrtree_, ks=[k])
+            dag.compile().execute(ctx)
+    return 0
+
+
+def trsmpl_qrf_New(ctx, qrtree_, A, IPIV, B, TS, TT, lu_tab, p=None) -> Taskpool:
+    tp = Taskpool("trsmpl_qrf", ctx)
+    tp.task("trsmpl_qrf", "update", lambda: trsmpl_qrf(ctx, qrtree_, A, IPIV, B, TS, TT, lu_tab, p))
+    return tp.finish_build()
+
+
+def gesv_qrf(ctx, qrtree_, A, IPIV, TS, TT, B, criteria=DEFAULT_CRITERIUM, alpha=1.0, p=None):
+    """Convenience driver: hybrid factorization + solve (as tests/testing_zgetrf_qrf.c checks it)."""
+    from . import blas3
+    lu_tab = [0] * min(A.mt, A.nt)
+    getrf_qrf(ctx, qrtree_, A, IPIV, TS, TT, criteria, alpha, lu_tab, None, p)
+    trsmpl_qrf(ctx, qrtree_, A, IPIV, B, TS, TT, lu_tab, p)
+    blas3.trsm(ctx, dplasmaLeft, dplasmaUpper, N_, dplasmaNonUnit, 1.0, A, B)
+    return lu_tab

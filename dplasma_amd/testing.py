@@ -52,6 +52,7 @@ def _parse(argv):
     ap.add_argument("-v", "--verbose", type=int, nargs="?", const=1, default=0)
     ap.add_argument("-g", "--gpus", type=int, default=-1, help="0: CPU only; default: GPU when present")
     ap.add_argument("--dot", default=None, help="write the DAG of DAG-based ops to this DOT file")
+    ap.add_argument("--criteria", type=int, default=0, help="LU-QR criterion (include/dplasma/lu_qr.h)")
     ap.add_argument("--trace", default=None, help="write a Chrome trace (all ranks) of the timed runs to this file")
     return ap.parse_args(argv)
 
@@ -392,6 +393,34 @@ def t_hetrf(h):
         h.check("||Ax-b|| / ((||A|| ||x|| + ||b||) N eps)", res, 60.0)
 
 
+def t_getrf_qrf(h):
+    """testing_zgetrf_qrf.c: hybrid LU-QR, then trsmpl_qrf + trsm(U) solve check."""
+    dp, a, ctx = h.dp, h.a, h.ctx
+    A = h.mat(a.N, a.N)
+    dp.plrnt(ctx, A, a.seed)
+    a0 = _dense(h, A) if a.check else None
+    ib = a.IB or min(32, A.nb)
+    TS = h.mat(A.mt * ib, a.N, mb=ib, nb=A.nb, name="TS")
+    TT = h.mat(A.mt * ib, a.N, mb=ib, nb=A.nb, name="TT")
+    IP = dp.qrf_ipiv_descriptor(ctx, A)
+    tree = dp.hqr_init(dp.dplasmaNoTrans, A, a.treel, a.treeh, a.qr_a if a.qr_a > 0 else 1,
+                       a.qr_p if a.qr_p > 0 else ctx.P, a.domino, a.tsrr)
+    lu_tab = [0] * min(A.mt, A.nt)
+    h.run_tp("getrf_qrf", lambda: dp.getrf_qrf_New(ctx, tree, A, IP, TS, TT, a.criteria, a.alpha, lu_tab))
+    if ctx.rank == 0:
+        print(f"-- lu_tab: {' '.join(map(str, lu_tab))}  ({sum(lu_tab)} LU / {len(lu_tab)} steps)")
+    if a.check:
+        B = h.mat(a.N, a.K or 1, name="B")
+        dp.plrnt(ctx, B, a.seed + 1)
+        b0 = _dense(h, B)
+        dp.trsmpl_qrf(ctx, tree, A, IP, B, TS, TT, lu_tab)
+        dp.trsm(ctx, dp.dplasmaLeft, dp.dplasmaUpper, dp.dplasmaNoTrans, dp.dplasmaNonUnit, 1.0, A, B)
+        x = _dense(h, B)
+        res = float((a0 @ x - b0).abs().max() / ((a0.abs().max() * x.abs().max() + b0.abs().max()) * a.N
+                                                  * EPS[h.prec]))
+        h.check("||Ax-b|| / ((||A|| ||x|| + ||b||) N eps)", res, 60.0)
+
+
 def _dense(h, X):
     d = X.to_dense_local().cpu()
     if h.ctx.world > 1:
@@ -412,7 +441,7 @@ OPS = {
     "getrf_1d": lambda h: t_getrf(h, "1d"), "getrf_ptgpanel": lambda h: t_getrf(h, "ptgpanel"),
     "getrf_incpiv": lambda h: t_getrf(h, "incpiv"), "getrf_nopiv": lambda h: t_getrf(h, "nopiv"),
     "lange": t_lange, "lanm2": t_lanm2, "print": t_print,
-    "heev": t_heev, "gebrd_ge2gb": t_gebrd_ge2gb, "hetrf": t_hetrf, "hebut": t_hetrf,
+    "getrf_qrf": t_getrf_qrf, "heev": t_heev, "gebrd_ge2gb": t_gebrd_ge2gb, "hetrf": t_hetrf, "hebut": t_hetrf,
 }
 
 
