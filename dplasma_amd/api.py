@@ -203,3 +203,30 @@ _register("qrf_ipiv_descriptor", _luqr.qrf_ipiv_descriptor)
 for _n in ("DEFAULT_CRITERIUM", "HIGHAM_CRITERIUM", "MUMPS_CRITERIUM", "LU_ONLY_CRITERIUM", "QR_ONLY_CRITERIUM",
            "RANDOM_CRITERIUM", "HIGHAM_SUM_CRITERIUM", "HIGHAM_MAX_CRITERIUM", "HIGHAM_MOY_CRITERIUM"):
     _register(_n, getattr(_luqr, _n))
+
+# Memory-bounded GEMM with host-resident operands (src/zgemm_NN_gpu.jdf)
+from .models import gemm_ooc as _gooc  # noqa: E402
+register_op("gemm_gpu", _gooc.gemm_gpu)
+register_op("gemm_gpu_New", _gooc.gemm_gpu_New)
+
+# GER (src/zger.jdf), HETRD = h2b + b2s (src/zhetrd_wrapper.c), setrecursive hints
+from .models import blas3 as _b3  # noqa: E402
+for _n in ("gerc", "gerc_New", "geru", "geru_New"):
+    register_op(_n, getattr(_b3, _n))
+register_op("ger", _b3.geru)
+register_op("ger_New", _b3.geru_New)
+for _n in ("hetrd", "hetrd_h2b_New", "hetrd_b2s"):
+    register_op(_n, getattr(_eig, _n))
+
+
+def _setrecursive(tp, hnb):
+    """dplasma_z{potrf,geqrf}_setrecursive(tp, hnb): the reference splits large CPU tile tasks into
+    sub-DAGs of hnb tiles.  On MI355X every tile kernel is already a multi-wavefront workgroup
+    program over the whole tile (and tiles of one level are batched into one launch), so the
+    hint is recorded on the taskpool (``tp.recursive_nb``) and has no further effect."""
+    tp.recursive_nb = int(hnb)
+    return 0
+
+
+for _op in ("potrf", "geqrf"):
+    register_op(_op + "_setrecursive", _setrecursive)

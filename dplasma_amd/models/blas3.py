@@ -294,3 +294,27 @@ def gerc(ctx, alpha, X, Y, A):
 
 def geru(ctx, alpha, X, Y, A):
     return geru_New(ctx, alpha, X, Y, A).execute(ctx)
+
+
+# ----------------------------------------------------------------------------- GER
+def gerc_New(ctx, alpha, X, Y, A):
+    """A := alpha x y^H + A (dplasma_zgerc_New, src/zger.jdf): X is M x 1, Y is N x 1 -- a K = 1 GEMM."""
+    from .gemm import gemm_New
+    return gemm_New(ctx, dplasmaNoTrans, dplasmaConjTrans if A.dtype.is_complex else dplasmaTrans, alpha, X, Y, 1.0,
+                    A, name="ger")
+
+
+def geru_New(ctx, alpha, X, Y, A):
+    """A := alpha x y^T + A (dplasma_zgeru_New)."""
+    from .gemm import gemm_New
+    return gemm_New(ctx, dplasmaNoTrans, dplasmaTrans, alpha, X, Y, 1.0, A, name="ger")
+
+
+def gerc(ctx, alpha, X, Y, A):
+    gerc_New(ctx, alpha, X, Y, A).execute(ctx)
+    return 0
+
+
+def geru(ctx, alpha, X, Y, A):
+    geru_New(ctx, alpha, X, Y, A).execute(ctx)
+    return 0

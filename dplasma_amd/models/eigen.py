@@ -341,3 +341,34 @@ def gesvd_values(ctx, A, ib: int = None) -> np.ndarray:
     ib = ib or min(32, A.nb)
     ab = gebrd_ge2gb(ctx, ib, A)
     return band_singular_values(ab, A.nb)
+
+
+# ----------------------------------------------------------------------------- HETRD (h2b + b2s)
+def hetrd_h2b_New(ctx, uplo, ib, A, T):
+    """Hermitian -> band (src/zhetrd_h2b_L.jdf): the herbt reduction."""
+    return herbt_New(ctx, uplo, ib, A, T)
+
+
+def hetrd_b2s(ctx, DE, b: int = None):
+    """Band -> tridiagonal in place on a band descriptor DE ((nb+1) x N, LAPACK lower band
+    storage; src/zhetrd_b2s.jdf): on exit row 0 holds d, row 1 holds e, the rest is zero.
+    Returns (d, e)."""
+    ab = _band_from_descriptor(ctx, DE)
+    d, e = _rt().hbrdt(np.asfortranarray(ab), ab.shape[0] - 1 if b is None else int(b))
+    out = np.zeros_like(ab)
+    out[0, :len(d)] = d
+    out[1, :len(e)] = e
+    src = torch.from_numpy(out)
+    for (m, n) in DE.local_tiles():
+        t = DE.tile(m, n)
+        r0, c0 = m * DE.mb, n * DE.nb
+        t.copy_(src[r0:r0 + t.shape[0], c0:c0 + t.shape[1]].to(t.device))
+    return d, e
+
+
+def hetrd(ctx, uplo, ib, A, DE, T):
+    """A = Q T Q^H with T real symmetric tridiagonal (dplasma_zhetrd, src/zhetrd_wrapper.c):
+    h2b on A, band -> DE (diag_band_to_rect), b2s on DE.  Returns (d, e)."""
+    herbt(ctx, uplo, ib, A, T)
+    diag_band_to_rect(ctx, A, DE, uplo=dplasmaLower)
+    return hetrd_b2s(ctx, DE, A.nb)

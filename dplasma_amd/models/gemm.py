@@ -46,8 +46,16 @@ def _b_tile(transB, k, n):
 
 
 def gemm_New(ctx, transA, transB, alpha, A, B, beta, C, c_mask=None, kc=None, name="gemm") -> Taskpool:
-    """c_mask(m, n) -> MASK_* restricts the update of C tile (m,n) to a triangle (used by herk/syrk)."""
+    """c_mask(m, n) -> MASK_* restricts the update of C tile (m,n) to a triangle (used by herk/syrk).
+
+    Host-resident operands with a GPU context dispatch to the memory-bounded
+    streaming variant (models/gemm_ooc.py), like dplasma_zgemm_New_ex picks the
+    GPU variant when the active set exceeds GPU memory (src/zgemm_wrapper.c:455-486)."""
     K = _check(transA, transB, A, B, C)
+    if (ctx.is_gpu and ctx.world == 1 and c_mask is None and C.device.type == "cpu"
+            and A.device.type == "cpu" and B.device.type == "cpu"):
+        from .gemm_ooc import gemm_gpu_New
+        return gemm_gpu_New(ctx, transA, transB, alpha, A, B, beta, C)
     tp = Taskpool(name, ctx)
     tp.flops = flops(C.prec, "gemm", C.m, C.n, K)
     kt = (K + A.nb - 1) // A.nb if transA == dplasmaNoTrans else (K + A.mb - 1) // A.mb

@@ -157,3 +157,20 @@ def test_gpu_heev_ge2gb(prec):
     B.from_dense(G)
     s = eigen.gesvd_values(g, B, ib=32)
     assert np.abs(s - torch.linalg.svdvals(G).numpy()).max() < 1e-10 * s.max()
+
+
+@pytest.mark.parametrize("prec", list("dz"))
+def test_hetrd_h2b_b2s(ctx, prec):
+    """dplasma_zhetrd: h2b + diag_band_to_rect + b2s; the tridiagonal (d, e) in DE has A's spectrum."""
+    dt = DTYPES[prec]
+    N, NB = 72, 16
+    M = _herm(N, dt, 17)
+    A = _load(ctx, M, dt, NB, torch.tril)
+    T = eigen.T_descriptor(A, 4)
+    DE = dp.TiledMatrix(dt, NB + 1, NB, NB + 1, N, device="cpu")
+    d, e = dp.hetrd(ctx, dp.dplasmaLower, 4, A, DE, T)
+    de = DE.to_dense_local()
+    assert np.allclose(de[0].real.numpy(), d) and np.allclose(de[1, :N - 1].real.numpy(), e)
+    assert float(de[2:].abs().max()) == 0.0
+    Tm = np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
+    assert np.abs(np.linalg.eigvalsh(Tm) - torch.linalg.eigvalsh(M).numpy()).max() < 1e-11
