@@ -63,7 +63,22 @@ template <> struct MF<float> {
 #define GBM 128
 #define GBN 128
 #define GBK 16
-#define GLS 144
+
+// LDS image of one operand block: [GBK][row-stride] per buffer.
+//  f64: no padding, column index XOR-swizzled by ((kk >> 1) & 7) << 2.  Fragment reads (16
+//       consecutive columns of row kr + the same of row kr+1 per 32 lanes) stay a permutation
+//       of whole 16-column groups in opposite bank halves, and the transposed stores of a
+//       k-contiguous operand (8 lanes = rows 0,2,..,14 of one column) land on 8 distinct
+//       bank pairs -- conflict-free both ways (padding alone cannot do both for b64).
+//  f32: padded row stride 144, no swizzle.
+template <typename T> struct LdsL {
+  static constexpr int LS = 144;
+  static __device__ inline int at(int kk, int col) { return kk * LS + col; }
+};
+template <> struct LdsL<double> {
+  static constexpr int LS = 128;
+  static __device__ inline int at(int kk, int col) { return kk * LS + (col ^ (((kk >> 1) & 7) << 2)); }
+};
 
 template <typename T, bool TA, bool TB>
 __global__ __launch_bounds__(256, 2) void k_gemm_mfma(const GemmItemK* __restrict__ items,
@@ -76,7 +91,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm_mfma(const GemmItemK* __restric
   typedef typename M_::vec_t vec_t;
   constexpr int VEC = M_::VEC;
   constexpr int NLD = (GBM * GBK) / (VEC * 256);  // 16-byte loads per thread per operand per k-step
-  __shared__ T sm[2][2][GBK][GLS];
+  typedef LdsL<T> L_;
+  constexpr int OPB_ = GBK * L_::LS;  // one operand image
+  __shared__ T sm[2 * 2 * OPB_];      // [buf][operand][GBK x LS]
 
   const int wg = xcd_remap(blockIdx.x, nwg);
   const int per = nsm * nsn;
@@ -93,20 +110,6 @@ __global__ __launch_bounds__(256, 2) void k_gemm_mfma(const GemmItemK* __restric
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   const int wm = w & 1, wn = w >> 1;
   const bool fullmn = vec_ok && (m0 + GBM <= Mt) && (n0 + GBN <= Nt);
-
-  acc_t acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int mm = m0 + wm * 64 + i * 16 + (l & 15);
-        const int nn = n0 + wn * 64 + j * 16 + M_::drow(l, r);
-        T v = T(0);
-        if (beta != T(0) && mm < Mt && nn < Nt) v = beta * Cb[mm + (long long)nn * ldc];
-        acc[i][j][r] = v;
-      }
 
   // flatten the (k-tile, k-block) iteration space
   int nsteps = 0;
@@ -180,68 +183,416 @@ __global__ __launch_bounds__(256, 2) void k_gemm_mfma(const GemmItemK* __restric
     }
   };
   auto store = [&](int buf) {
+    T* sa = sm + (2 * buf) * OPB_;
+    T* sb = sa + OPB_;
 #pragma unroll
     for (int q = 0; q < NLD; ++q) {
       const int c = tid + 256 * q;
       if (!TA) {
         const int kk = c / (GBM / VEC), i = (c % (GBM / VEC)) * VEC;
         vec_t v = ra[q] * alpha;
-        *(vec_t*)&sm[buf][0][kk][i] = v;
+        *(vec_t*)&sa[L_::at(kk, i)] = v;
       } else {
         const int i = c / (GBK / VEC), kk = (c % (GBK / VEC)) * VEC;
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) sm[buf][0][kk + e][i] = ra[q][e] * alpha;
+        for (int e = 0; e < VEC; ++e) sa[L_::at(kk + e, i)] = ra[q][e] * alpha;
       }
       if (TB) {
         const int kk = c / (GBN / VEC), j = (c % (GBN / VEC)) * VEC;
-        *(vec_t*)&sm[buf][1][kk][j] = rb[q];
+        *(vec_t*)&sb[L_::at(kk, j)] = rb[q];
       } else {
         const int j = c / (GBK / VEC), kk = (c % (GBK / VEC)) * VEC;
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) sm[buf][1][kk + e][j] = rb[q][e];
+        for (int e = 0; e < VEC; ++e) sb[L_::at(kk + e, j)] = rb[q][e];
       }
     }
   };
+  // MFMA fragments of k-quad kq: a[i] = op(A)(wm*64 + i*16 + l%16, kq*4 + l/16), b[j] likewise
+  auto frag = [&](int buf, int kq, T* a, T* b) {
+    const T* sa = sm + (2 * buf) * OPB_;
+    const T* sb = sa + OPB_;
+    const int kr = kq * 4 + (l >> 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = sa[L_::at(kr, wm * 64 + i * 16 + (l & 15))];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = sb[L_::at(kr, wn * 64 + j * 16 + (l & 15))];
+  };
 
-  if (nsteps > 0) {
-    load();
-    store(0);
+  // first operand block in flight before the C prologue so both latencies overlap
+  if (nsteps > 0) load();
+  // C sub-tile origin of this lane: row mrow + i*16, columns ncol + j*16 + drow(l, r)
+  const int mrow = m0 + wm * 64 + (l & 15);
+  const int ncol = n0 + wn * 64;
+  const bool fullc = (m0 + GBM <= Mt) && (n0 + GBN <= Nt);
+  acc_t acc[4][4];
+  if (beta == T(0)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = T(0);
+  } else if (fullc) {
+    // interior sub-tile: 64 independent loads in flight, one wait (the first MFMA's)
+    const T* cp = Cb + mrow + (long long)ncol * ldc;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc[i][j][r] = cp[i * 16 + (long long)(j * 16 + M_::drow(l, r)) * ldc];
+    // always scale (even by 1): consuming the C values here makes the waitcnt pass drain
+    // them before the main loop; left pending, they are carried into the loop and every
+    // iteration's MFMAs wait on the freshly issued prefetch (vmcnt is a plain counter)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] *= beta;
+  } else {
+    // ragged edge: clamp the address, select the value (no per-element branches)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int mm = mrow + i * 16, nn = ncol + j * 16 + M_::drow(l, r);
+          const bool in = mm < Mt && nn < Nt;
+          const T v = Cb[(in ? mm : 0) + (long long)(in ? nn : 0) * ldc];
+          acc[i][j][r] = in ? beta * v : T(0);
+        }
   }
-  __syncthreads();
+
+  if (nsteps > 0) store(0);
+  if (nsteps > 1) load();
+  // Pipeline (per k-step s): barrier -> fragments of quad 0 -> write block s+1 (loaded during
+  // step s-1) into the other buffer -> issue the global loads of block s+2 -> 16 MFMAs per
+  // quad with the next quad's fragments in flight.  The LDS writes and the global loads both
+  // hide behind the step's 64 MFMAs/wave instead of sitting between the MFMAs and the barrier.
   for (int s = 0; s < nsteps; ++s) {
     const int cur = s & 1;
-    if (s + 1 < nsteps) load();
+    __syncthreads();
+    T a[2][4], b[2][4];
+    frag(cur, 0, a[0], b[0]);
+    if (s + 1 < nsteps) store(cur ^ 1);
+    if (s + 2 < nsteps) load();
 #pragma unroll
     for (int kq = 0; kq < GBK / 4; ++kq) {
-      const int kr = kq * 4 + (l >> 4);
-      T a[4], b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = sm[cur][0][kr][wm * 64 + i * 16 + (l & 15)];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = sm[cur][1][kr][wn * 64 + j * 16 + (l & 15)];
+      if (kq + 1 < GBK / 4) frag(cur, kq + 1, a[(kq + 1) & 1], b[(kq + 1) & 1]);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = M_::mma(b[j], a[i], acc[i][j]);
+        for (int j = 0; j < 4; ++j) acc[i][j] = M_::mma(b[kq & 1][j], a[kq & 1][i], acc[i][j]);
     }
-    if (s + 1 < nsteps) store(cur ^ 1);
-    __syncthreads();
   }
 
-  // epilogue
+  // epilogue: interior sub-tiles off the diagonal store unconditionally
+  const bool diag = (uplo == 1 && n0 + GBN > m0) || (uplo == 2 && m0 + GBM > n0);
+  if (fullc && !diag) {
+    T* cp = Cb + mrow + (long long)ncol * ldc;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int mm = m0 + wm * 64 + i * 16 + (l & 15);
-        const int nn = n0 + wn * 64 + j * 16 + M_::drow(l, r);
-        bool ok = mm < Mt && nn < Nt;
-        if (uplo == 1) ok = ok && (mm >= nn);
-        if (uplo == 2) ok = ok && (mm <= nn);
-        if (ok) Cb[mm + (long long)nn * ldc] = acc[i][j][r];
+        for (int r = 0; r < 4; ++r)
+          cp[i * 16 + (long long)(j * 16 + M_::drow(l, r)) * ldc] = acc[i][j][r];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int mm = mrow + i * 16, nn = ncol + j * 16 + M_::drow(l, r);
+          bool ok = mm < Mt && nn < Nt;
+          if (uplo == 1) ok = ok && (mm >= nn);
+          if (uplo == 2) ok = ok && (mm <= nn);
+          if (ok) Cb[mm + (long long)nn * ldc] = acc[i][j][r];
+        }
+  }
+}
+
+// ------------------------------------------------------------------ full-tile fast path
+// Used when every item of the launch is a whole number of 128x128 sub-tiles and every k-run a
+// multiple of GBK (e.g. all NB=512 Cholesky / SUMMA updates).  Differences from k_gemm_mfma:
+//  * no bounds logic anywhere in the k-loop;
+//  * operands are fetched with buffer loads: the per-thread byte offset is loop-invariant (VGPR),
+//    the k-advance is a scalar soffset and the k-tile base lives in the SGPR resource, so the
+//    loop carries no 64-bit VALU address arithmetic;
+//  * alpha is applied once in the epilogue (acc starts at (beta/alpha) C), not per staged block;
+//  * k-contiguous operands (A^T / B untransposed) are fetched with 16 consecutive lanes on 16
+//    different rows/columns so their transposed LDS stores hit 16 distinct bank slots; all LDS
+//    images use the padded stride 144 (fragment reads of rows kr / kr+1 in opposite bank halves).
+#define FLS 144
+
+__device__ inline __amdgpu_buffer_rsrc_t mk_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+
+template <typename T> struct BufLd;
+template <> struct BufLd<double> {
+  typedef d2v vec_t;
+  static __device__ inline vec_t ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(vec_t, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+  }
+};
+template <> struct BufLd<float> {
+  typedef f4v vec_t;
+  static __device__ inline vec_t ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(vec_t, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+  }
+};
+
+template <typename T, bool TA, bool TB>
+__global__ __launch_bounds__(256, 2) void k_gemm_full(const GemmItemK* __restrict__ items,
+                                                      const KPair* __restrict__ kps, int nsm, int nsn,
+                                                      int nwg, T alpha, const T* __restrict__ A, int lda,
+                                                      const T* __restrict__ B, int ldb, T beta,
+                                                      T* __restrict__ C, int ldc) {
+  typedef MF<T> M_;
+  typedef typename M_::acc_t acc_t;
+  typedef typename M_::vec_t vec_t;
+  constexpr int VEC = M_::VEC;
+  constexpr int NLD = (GBM * GBK) / (VEC * 256);
+  constexpr int KG = GBK / VEC;      // 16-byte k-groups per row of a k-contiguous operand
+  constexpr int OPB_ = GBK * FLS;
+  __shared__ T sm[2 * 2 * OPB_];     // [buf][operand][GBK x FLS]
+
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int per = nsm * nsn;
+  const GemmItemK it = items[wg / per];
+  const int sub = wg % per;
+  const int m0 = (sub % nsm) * GBM, n0 = (sub / nsm) * GBN;
+  const int Mt = it.m, Nt = it.n;
+  if (m0 >= Mt || n0 >= Nt) return;
+  const int uplo = it.flags & 3;
+  if (uplo == 1 && n0 >= m0 + GBM) return;
+  if (uplo == 2 && m0 >= n0 + GBN) return;
+
+  T* Cb = C + it.c_off;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int wm = w & 1, wn = w >> 1;
+
+  int nsteps = 0;
+  for (int t = 0; t < it.kt_cnt; ++t) nsteps += kps[it.kt_beg + t].k / GBK;
+
+  // ---- loop-invariant per-thread fetch offset (bytes) and LDS destination of the q=0 vector;
+  // the q-th vector (thread c + 256q) is a fixed stride away: scalar for the fetch, immediate in LDS
+  int voa, vob, lda0, ldb0;
+  {
+    const int c = tid;
+    if (!TA) {  // op(A)(i, k) = A[i + k*lda]: 16-byte vectors along i
+      const int kk = c / (GBM / VEC), i = (c % (GBM / VEC)) * VEC;
+      voa = (i + kk * lda) * (int)sizeof(T);
+      lda0 = kk * FLS + i;
+    } else {    // op(A)(i, k) = A[k + i*lda]: 16 consecutive lanes on 16 different i
+      const int i = (c & 15) | ((c / (16 * KG)) << 4), kk = ((c >> 4) % KG) * VEC;
+      voa = (kk + i * lda) * (int)sizeof(T);
+      lda0 = kk * FLS + i;
+    }
+    if (TB) {   // op(B)(k, j) = B[j + k*ldb]
+      const int kk = c / (GBN / VEC), j = (c % (GBN / VEC)) * VEC;
+      vob = (j + kk * ldb) * (int)sizeof(T);
+      ldb0 = kk * FLS + j;
+    } else {    // op(B)(k, j) = B[k + j*ldb]
+      const int j = (c & 15) | ((c / (16 * KG)) << 4), kk = ((c >> 4) % KG) * VEC;
+      vob = (kk + j * ldb) * (int)sizeof(T);
+      ldb0 = kk * FLS + j;
+    }
+  }
+  constexpr int LQA = TA ? 16 * VEC : 2 * VEC * FLS;   // LDS stride between q and q+1
+  constexpr int LQB = TB ? 2 * VEC * FLS : 16 * VEC;
+  const int GQA = (TA ? 16 * VEC : 2 * VEC) * lda * (int)sizeof(T);  // fetch stride (bytes)
+  const int GQB = (TB ? 2 * VEC : 16 * VEC) * ldb * (int)sizeof(T);
+  // scalar k-position of the next fetch
+  int ld_kt = it.kt_beg, ld_k0 = 0, ld_K = 0;
+  __amdgpu_buffer_rsrc_t ra_rs = mk_rsrc(A), rb_rs = mk_rsrc(B);
+  auto set_kt = [&]() {
+    const KPair kp = kps[ld_kt];
+    ld_K = kp.k;
+    ra_rs = mk_rsrc(A + kp.a_off + (TA ? (long long)m0 * lda : (long long)m0));
+    rb_rs = mk_rsrc(B + kp.b_off + (TB ? (long long)n0 : (long long)n0 * ldb));
+  };
+  if (nsteps > 0) set_kt();
+  vec_t ra[NLD], rb[NLD];
+  // fetch(): issue the block at the current position; advance(): step it (scalar), clamped at
+  // the last block so the loop can fetch unconditionally (surplus fetches are never stored)
+  auto fetch = [&]() {
+    const int sa = (TA ? ld_k0 : ld_k0 * lda) * (int)sizeof(T);
+    const int sb = (TB ? ld_k0 * ldb : ld_k0) * (int)sizeof(T);
+#pragma unroll
+    for (int q = 0; q < NLD; ++q) {
+      ra[q] = BufLd<T>::ld(ra_rs, voa, sa + q * GQA);
+      rb[q] = BufLd<T>::ld(rb_rs, vob, sb + q * GQB);
+    }
+  };
+  auto advance = [&]() {
+    if (ld_k0 + GBK < ld_K) {
+      ld_k0 += GBK;
+    } else if (ld_kt + 1 < it.kt_beg + it.kt_cnt) {
+      ++ld_kt;
+      ld_k0 = 0;
+      set_kt();
+    }
+  };
+  auto load = [&]() {
+    fetch();
+    advance();
+  };
+  auto store = [&](int buf) {
+    T* sa = sm + (2 * buf) * OPB_;
+    T* sb = sa + OPB_;
+#pragma unroll
+    for (int q = 0; q < NLD; ++q) {
+      if (!TA) {
+        *(vec_t*)&sa[lda0 + q * LQA] = ra[q];
+      } else {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) sa[lda0 + q * LQA + e * FLS] = ra[q][e];
       }
+      if (TB) {
+        *(vec_t*)&sb[ldb0 + q * LQB] = rb[q];
+      } else {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) sb[ldb0 + q * LQB + e * FLS] = rb[q][e];
+      }
+    }
+  };
+  auto frag = [&](int buf, int kq, T* a, T* b) {
+    const T* sa = sm + (2 * buf) * OPB_;
+    const T* sb = sa + OPB_;
+    const int kr = kq * 4 + (l >> 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = sa[kr * FLS + wm * 64 + i * 16 + (l & 15)];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = sb[kr * FLS + wn * 64 + j * 16 + (l & 15)];
+  };
+
+  if (nsteps > 0) load();
+  // ---- C prologue: acc = (beta/alpha) C, finished by one multiply with alpha in the epilogue
+  const int mrow = m0 + wm * 64 + (l & 15);
+  const int ncol = n0 + wn * 64;
+  T* cp = Cb + mrow + (long long)ncol * ldc;
+  acc_t acc[4][4];
+  if (beta == T(0)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = T(0);
+  } else {
+    const T bs = beta / alpha;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = cp[i * 16 + (long long)(j * 16 + M_::drow(l, r)) * ldc];
+    // consume the C values here so the waitcnt pass drains them before the loop (vmcnt is a counter)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] *= bs;
+  }
+  if (nsteps > 0) store(0);
+  if (nsteps > 1) load();
+  // One basic block per k-step: barrier, then the step's 64 MFMAs/wave with the LDS writes of
+  // block s+1, the buffer fetches of block s+2 and the fragment reads of quads 1..3 interleaved
+  // one memory instruction per MFMA (sched_group_barrier), then the scalar advance.
+  constexpr int NW = (TA ? NLD * VEC : NLD) + (TB ? NLD : NLD * VEC);  // LDS stores per step
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    __syncthreads();
+    T a[3][4], b[3][4];
+    frag(cur, 0, a[0], b[0]);
+    store(cur ^ 1);
+    frag(cur, 1, a[1], b[1]);
+    fetch();
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = M_::mma(b[0][j], a[0][i], acc[i][j]);
+    frag(cur, 2, a[2], b[2]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = M_::mma(b[1][j], a[1][i], acc[i][j]);
+    frag(cur, 3, a[0], b[0]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = M_::mma(b[2][j], a[2][i], acc[i][j]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = M_::mma(b[0][j], a[0][i], acc[i][j]);
+    // schedule: [quad-0 reads] then MFMA-paced: NW stores, 4 reads (q1), 2*NLD fetches,
+    // pad to 24, 4 reads (q2), pad to 40, 4 reads (q3), rest
+    constexpr int M1 = NW + 4 + 2 * NLD;            // MFMAs paced by stores / q1 reads / fetches
+    constexpr int P1 = M1 < 24 ? 24 - M1 : 0;
+    constexpr int M2 = M1 + P1 + 4;
+    constexpr int P2 = M2 < 40 ? 40 - M2 : 0;
+    constexpr int M3 = M2 + P2 + 4;
+    static_assert(M3 < 64, "schedule overflows the step's MFMAs");
+    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+#pragma unroll
+    for (int v = 0; v < 2 * NLD; ++v) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    }
+    if (P1 > 0) __builtin_amdgcn_sched_group_barrier(0x008, P1, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    if (P2 > 0) __builtin_amdgcn_sched_group_barrier(0x008, P2, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 64 - M3, 0);
+    advance();
+  }
+
+  const bool diag = (uplo == 1 && n0 + GBN > m0) || (uplo == 2 && m0 + GBM > n0);
+  if (!diag) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cp[i * 16 + (long long)(j * 16 + M_::drow(l, r)) * ldc] = alpha * acc[i][j][r];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int mm = mrow + i * 16, nn = ncol + j * 16 + M_::drow(l, r);
+          const bool ok = (uplo == 1) ? (mm >= nn) : (mm <= nn);
+          if (ok) Cb[mm + (long long)nn * ldc] = alpha * acc[i][j][r];
+        }
+  }
 }
 
 // ------------------------------------------------------------------ generic
@@ -341,6 +692,11 @@ template <typename T>
 static int launch_mfma(int opa, int opb, int nitems, const GemmItemK* items, const KPair* kps, int max_m,
                        int max_n, T alpha, const T* A, int lda, const T* B, int ldb, T beta, T* C, int ldc,
                        int vec_ok, hipStream_t st) {
+  // vec_ok bit 1: every item is whole 128x128 sub-tiles with k-runs multiple of GBK (host-checked)
+  // (32-bit buffer offsets: the furthest fetch is < (GBM + GBK) leading dimensions away)
+  const bool full = (vec_ok & 2) && (vec_ok & 1) && alpha != T(0) &&
+                    (long long)(GBM + GBK) * (lda > ldb ? lda : ldb) * (long long)sizeof(T) < (1LL << 30);
+  vec_ok &= 1;
   const int nsm = cdiv(max_m, GBM), nsn = cdiv(max_n, GBN);
   const long long nwgl = (long long)nitems * nsm * nsn;
   if (nwgl <= 0) return 0;
@@ -348,6 +704,13 @@ static int launch_mfma(int opa, int opb, int nitems, const GemmItemK* items, con
   const int nwg = (int)nwgl;
   dim3 g(nwg), b(256);
   const bool ta = opa != 0, tb = opb != 0;
+  if (full) {
+    if (!ta && !tb) hipLaunchKernelGGL((k_gemm_full<T, false, false>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc);
+    else if (!ta && tb) hipLaunchKernelGGL((k_gemm_full<T, false, true>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc);
+    else if (ta && !tb) hipLaunchKernelGGL((k_gemm_full<T, true, false>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc);
+    else hipLaunchKernelGGL((k_gemm_full<T, true, true>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc);
+    return (int)hipGetLastError();
+  }
   if (!ta && !tb) hipLaunchKernelGGL((k_gemm_mfma<T, false, false>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc, vec_ok);
   else if (!ta && tb) hipLaunchKernelGGL((k_gemm_mfma<T, false, true>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc, vec_ok);
   else if (ta && !tb) hipLaunchKernelGGL((k_gemm_mfma<T, true, false>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc, vec_ok);

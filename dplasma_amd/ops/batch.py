@@ -52,6 +52,8 @@ class GemmBatch(_Uploadable):
         self.kpairs = None
         self.max_m = self.max_n = 0
         self.vec_ok = True
+        self.full = True   # every item whole 128x128 sub-tiles, every k-run a multiple of 16
+        self._align = 0    # OR of all element offsets (vector-alignment test per dtype)
         self.flops_mnk = 0.0
 
     def add(self, c_off: int, m: int, n: int, kpairs, mask: int = MASK_FULL):
@@ -62,16 +64,26 @@ class GemmBatch(_Uploadable):
             self._kps.append((a, b, k, 0))
             if a % 2 or b % 2:
                 self.vec_ok = False
+            self._align |= int(a) | int(b)
+            if k % 16:
+                self.full = False
             self.flops_mnk += float(m) * n * k
+        if m % 128 or n % 128:
+            self.full = False
         self._items.append((c_off, beg, len(kp), m, n, mask, 0))
         if c_off % 2:
             self.vec_ok = False
+        self._align |= int(c_off)
         self.max_m = max(self.max_m, m)
         self.max_n = max(self.max_n, n)
         return self
 
     def __len__(self):
         return len(self._items) if self.items is None else len(self.items)
+
+    def aligned(self, elems: int) -> bool:
+        """All A/B/C offsets are multiples of ``elems`` elements."""
+        return self._align % elems == 0
 
     def finalize(self):
         if self.items is None:

@@ -52,8 +52,11 @@ def gemm(transA: int, transB: int, alpha, A: torch.Tensor, lda: int, B: torch.Te
     if _is_gpu(C):
         lib = _lib.load()
         items, kps = batch.device_arrays(C.device)
-        vec_ok = int(batch.vec_ok and lda % 2 == 0 and ldb % 2 == 0 and A.data_ptr() % 16 == 0
+        ve = max(1, 16 // C.element_size())   # elements per 16-byte vector
+        vec_ok = int(batch.aligned(ve) and lda % ve == 0 and ldb % ve == 0 and A.data_ptr() % 16 == 0
                      and B.data_ptr() % 16 == 0)
+        if vec_ok and batch.full:
+            vec_ok |= 2
         sa, sb = _lib.Scalar(alpha, C.dtype), _lib.Scalar(beta, C.dtype)
         rc = lib.dpl_gemm_batched(_lib.prec_code(C.dtype), transA, transB, len(batch.items), items.data_ptr(),
                                   kps.data_ptr(), batch.max_m, batch.max_n, sa.ptr, A.data_ptr(), lda, B.data_ptr(),

@@ -228,3 +228,42 @@ def test_lu_gpu(gctx, cctx, prec):
         outs.append((A.to_dense_local(), B.to_dense_local()))
     assert rel_err(outs[0][0], outs[1][0]) < tol(dt) * 100
     assert rel_err(outs[0][1], outs[1][1]) < tol(dt) * 100
+
+
+@pytest.mark.parametrize("prec", list("sd"))
+@pytest.mark.parametrize("ta,tb", [(111, 111), (111, 112), (112, 111), (112, 112)])
+@pytest.mark.parametrize("mask,alpha,beta", [(0, -1.0, 1.0), (1, -1.0, 1.0), (2, 0.5, -0.3), (0, 2.0, 0.0)])
+def test_gemm_full_tile_path(gctx, prec, ta, tb, mask, alpha, beta):
+    """Whole-128-sub-tile batches take the branch-free buffer-load kernel (k_gemm_full): check it
+    against torch for every transpose pair, triangular write masks and alpha/beta folding."""
+    from dplasma_amd.ops.batch import GemmBatch
+    dt = DTYPES[prec]
+    nb, kt = 256, 3
+    torch.manual_seed(7)
+    A = torch.randn(nb * kt * nb, dtype=dt, device="cuda")       # kt tiles nb x nb, ld = nb
+    B = torch.randn(nb * kt * nb, dtype=dt, device="cuda")
+    C = torch.randn(2 * nb * nb, dtype=dt, device="cuda")        # 2 tiles
+    C0 = C.clone()
+    gb = GemmBatch()
+    for t in range(2):
+        gb.add(t * nb * nb, nb, nb, [(q * nb * nb, ((q + t) % kt) * nb * nb, nb) for q in range(kt)], mask)
+    assert gb.full
+    ops.gemm(ta, tb, alpha, A, nb, B, nb, beta, C, nb, gb)
+    torch.cuda.synchronize()
+
+    def tile(X, i):
+        return X[i * nb * nb:(i + 1) * nb * nb].view(nb, nb).t().double()   # column-major view
+    for t in range(2):
+        acc = torch.zeros(nb, nb, dtype=torch.float64, device="cuda")
+        for q in range(kt):
+            a = tile(A, q) if ta == 111 else tile(A, q).t()
+            b = tile(B, (q + t) % kt) if tb == 111 else tile(B, (q + t) % kt).t()
+            acc += a @ b
+        ref = beta * tile(C0, t) + alpha * acc
+        keep = tile(C0, t)
+        if mask == 1:
+            ref = torch.where(torch.ones(nb, nb, dtype=torch.bool, device="cuda").tril(), ref, keep)
+        elif mask == 2:
+            ref = torch.where(torch.ones(nb, nb, dtype=torch.bool, device="cuda").triu(), ref, keep)
+        got = tile(C, t)
+        assert (got - ref).abs().max().item() / ref.abs().max().item() < (1e-12 if prec == "d" else 1e-4)

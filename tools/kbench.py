@@ -74,8 +74,23 @@ def bench_gemm(ctx, nb=512, grid=(1, 4, 16, 64)):
                                     C.data, C.ld, gb))
         fl = 2.0 * n * n * nb
         print(f"gemm NT tiles={g}x{g} k={nb}: {t:9.1f} us ({fl / t / 1e3:8.1f} GF/s)", flush=True)
+    # trailing-update shapes with k aggregated over several panels (deferred updates)
+    for kd in (2, 4):
+        g = 32
+        n = nb * g
+        A = dp.block_cyclic(ctx, torch.float64, nb, nb, n, nb * kd)
+        C = dp.block_cyclic(ctx, torch.float64, nb, nb, n, n)
+        dp.plrnt(ctx, A, 1)
+        gb = GemmBatch()
+        for nn in range(g):
+            for mm in range(g):
+                gb.add(C.offset(mm, nn), nb, nb, [(A.offset(mm, q), A.offset(nn, q), nb) for q in range(kd)])
+        t = timeit(lambda: ops.gemm(dp.dplasmaNoTrans, dp.dplasmaConjTrans, -1.0, A.data, A.ld, A.data, A.ld, 1.0,
+                                    C.data, C.ld, gb))
+        fl = 2.0 * n * n * nb * kd
+        print(f"gemm NT tiles={g}x{g} k={nb * kd}: {t:9.1f} us ({fl / t / 1e3:8.1f} GF/s)", flush=True)
     # one big multi-k GEMM (SUMMA single rank)
-    for n in (8192, 16384):
+    for n in [int(x) for x in os.environ.get("KBENCH_GEMM_N", "8192,16384").split(",")]:
         A = dp.block_cyclic(ctx, torch.float64, nb, nb, n, n)
         B = dp.block_cyclic(ctx, torch.float64, nb, nb, n, n)
         C = dp.block_cyclic(ctx, torch.float64, nb, nb, n, n)
