@@ -8,23 +8,23 @@ all-reduce).
 MI355X design (not a translation of the JDF):
 
 * The factorisation is compiled (``potrf_New``) into a short program of
-  coarse tasks per step k, right-looking with look-ahead 1:
+  coarse tasks, right-looking over blocks of D panels (deferred updates):
 
     panel stream  : POTRF(k) -> bcast diag tile down the owner column ->
                     TRSM of the local panel tiles (ONE batched launch) ->
-                    pack + row broadcast + column all-gather of the panel
-    update stream : UPDCOL(k)  trailing update of tile column k+1 (one launch)
-                    UPDREST(k) trailing update of every other local tile
-                               (one launch of the MFMA GEMM engine over all
-                               local (m, n) tiles, diagonal tiles masked lower)
+                    pack + row broadcast + column all-gather of the panel ->
+                    NEAR(k): panel k updates the rest of its block
+    update stream : NEXT(b)  block b's D panels update block b+1 (k = D*NB)
+                    REST(b)  ... and every local tile beyond it (one launch of
+                             the MFMA GEMM engine, diagonal tiles masked)
 
-  POTRF(k+1) depends only on UPDCOL(k), so the k+1 panel (on the
-  high-priority stream) overlaps UPDREST(k) -- the critical-path/lookahead
-  structure the reference obtains with priorities (zpotrf_L.jdf:58-69).
+  Block b+1's panels depend only on NEXT(b), so they (high-priority stream)
+  overlap REST(b) -- the critical-path/lookahead structure the reference
+  obtains with priorities (zpotrf_L.jdf:58-69).
 * Tiles stay resident in HBM; the panel travels once per step over RCCL/xGMI:
   the owner column broadcasts its pieces along process rows and every
   process column all-gathers them, so each rank ends with the full panel in
-  a double-buffered contiguous slab (buffer k%2).
+  a contiguous slab (G[block parity][panel in block]).
 * Single rank: no copies at all -- the panel is read in place.
 """
 from __future__ import annotations
@@ -47,8 +47,28 @@ class _Panel:
         self.base, self.ld, self.off = base, ld, off_fn
 
 
-def potrf_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
-    """Build the Cholesky taskpool for the ``uplo`` triangle of square matrix A."""
+POTRF_DEFER = 4            # panels aggregated per deferred trailing update (k = 4*NB)
+POTRF_DEFER_MIN_TILES = 24 # below this many trailing tile-columns: plain look-ahead-1 (D = 1)
+
+
+def _defer_depth(nt_left: int, D: int, min_tiles: int) -> int:
+    return D if nt_left >= min_tiles else 1
+
+
+def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
+    """Build the Cholesky taskpool for the ``uplo`` triangle of square matrix A.
+
+    Blocked right-looking schedule with deferred (aggregated) trailing updates:
+    panels are processed in blocks of D tile-columns (``defer``, default
+    ``POTRF_DEFER``; D = 1 once fewer than ``POTRF_DEFER_MIN_TILES`` columns
+    remain).  Inside a block each panel k updates the rest of its own block at
+    once (NEAR(k), panel stream, critical path).  The D panels of a block then
+    update the next block (NEXT(b), critical path of the next block) and every
+    column beyond it (REST(b), which overlaps the next block's panels) in single
+    launches whose k-runs are D*NB long: the MFMA engine runs at its large-k rate
+    (74 vs 70 TF/s at k=512 on MI355X) and every trailing tile is read and
+    written once per block instead of once per panel.
+    """
     if uplo not in (dplasmaLower, dplasmaUpper):
         raise ValueError("potrf: illegal uplo")
     if A.m != A.n or A.mb != A.nb:
@@ -64,6 +84,19 @@ def potrf_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     distributed = ctx.world > 1
     P, Q = A.P, A.Q
     myrow, mycol = A.myrow, A.mycol
+    import os
+    if defer is None:
+        defer = int(os.environ.get("DPLASMA_POTRF_DEFER", POTRF_DEFER))
+    D = max(1, int(defer))
+    min_tiles = int(os.environ.get("DPLASMA_POTRF_DEFER_MIN_TILES", POTRF_DEFER_MIN_TILES))
+
+    # block partition of the tile columns
+    blocks = []
+    c = 0
+    while c < nt:
+        d = _defer_depth(nt - c, D, min_tiles)
+        blocks.append((c, min(nt, c + d)))
+        c += d
 
     # "panel coordinate": lower -> tile (i, k); upper -> tile (k, i)
     def tcoord(i, k):
@@ -82,7 +115,7 @@ def potrf_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
 
     my_cross = mycol if lower else myrow
 
-    # distributed panel buffers: G[2][nlines][maxcnt][nbe]
+    # distributed panel buffers: G[2 (block parity)][D (panel in block)][nlines][maxcnt][nbe]
     if distributed:
         maxcnt = 0
         for k in range(nt):
@@ -91,121 +124,148 @@ def potrf_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                 cnt[owner_of_panel_line(i)] += 1
             maxcnt = max(maxcnt, max(cnt) if cnt else 0)
         maxcnt = max(maxcnt, 1)
-        G = torch.zeros(2, nlines, maxcnt, nbe, dtype=A.dtype, device=dev)
+        G = torch.zeros(2, D, nlines, maxcnt, nbe, dtype=A.dtype, device=dev)
         dbuf = torch.zeros(nbe, dtype=A.dtype, device=dev)
         tp._buffers = (G, dbuf)
 
     tri_mask = MASK_LOWER if lower else MASK_UPPER
-    prev_col = None   # task id of UPDCOL(k-1)
-    last_upd = {}     # k -> last update-stream task of step k (guards panel buffer reuse)
-    prev_panel = None
-    for k in range(nt):
-        kb = A.tile_rows(k)
-        dk = tcoord(k, k)
-        own_diag = A.is_local(*dk)
-        in_panel_cross = (panel_owner_cross(k) == my_cross)
-        # ---------------- POTRF(k)
-        t_potrf = None
-        if own_diag:
-            off = A.offset(*dk)
+    tA, tB = (dplasmaNoTrans, dplasmaConjTrans) if lower else (dplasmaConjTrans, dplasmaNoTrans)
+    panels = {}       # k -> _Panel (where panel k's tiles live for the updates)
 
-            def f_potrf(off=off, kb=kb, k=k):
-                ops.potrf_tile(uplo, A.data, off, kb, A.ld, info, k * A.mb)
-            t_potrf = tp.task(f"POTRF({k})", "panel", f_potrf, [prev_col], prio=3)
-        # ---------------- local panel tiles (i > k) of my process row/col
-        mine = [i for i in range(k + 1, nt) if in_panel_cross and owner_of_panel_line(i) == my_line]
-        # ---------------- diag tile to the panel owners (column for lower) and TRSM
-        t_trsm = None
-        if in_panel_cross:
-            if distributed and nlines > 1:
-                src = A.grid.rank(*((owner_of_panel_line(k), panel_owner_cross(k)) if lower
-                                    else (panel_owner_cross(k), owner_of_panel_line(k))))
-                dk_off = A.offset(*dk) if own_diag else None
-
-                def f_dbcast(dk_off=dk_off, src=src, kb=kb):
-                    if dk_off is not None:
-                        dv = torch.as_strided(dbuf, (kb, kb), (1, A.mb), 0)
-                        dv.copy_(torch.as_strided(A.data, (kb, kb), (1, A.ld), dk_off))
-                    comm.bcast(dbuf, src, line_group)
-                t_db = tp.task(f"DBCAST({k})", "panel", f_dbcast, [t_potrf, prev_col], prio=3)
-                tri_base, tri_ld, tri_off = dbuf, A.mb, 0
-            else:
-                t_db = t_potrf
-                tri_base, tri_ld, tri_off = A.data, A.ld, A.offset(*dk)
-            if mine:
-                tb = TileBatch()
-                for i in mine:
-                    c = tcoord(i, k)
-                    tb.add(tri_off, A.tile_rows(c[0]), A.tile_cols(c[1]), b_off=A.offset(*c))
-                tb.finalize()
-                side = dplasmaRight if lower else dplasmaLeft
-
-                def f_trsm(tb=tb, tri_base=tri_base, tri_ld=tri_ld, side=side):
-                    ops.trsm(side, uplo, dplasmaConjTrans, dplasmaNonUnit, 1.0, tri_base, tri_ld, A.data, A.ld, tb)
-                t_trsm = tp.task(f"TRSM({k})", "panel", f_trsm, [t_db, prev_col], prio=2)
-        # ---------------- panel distribution
-        if k == nt - 1:
-            break
-        if distributed:
-            par = k % 2
-            lines_cnt = [0] * nlines
-            idx_in_line = {}
-            for i in range(k + 1, nt):
-                ln = owner_of_panel_line(i)
-                idx_in_line[i] = lines_cnt[ln]
-                lines_cnt[ln] += 1
-            my_cnt = lines_cnt[my_line]
-            pack = None
-            if in_panel_cross and mine:
-                pb = TileBatch()
-                for j, i in enumerate(mine):
-                    c = tcoord(i, k)
-                    pb.add(A.offset(*c), A.tile_rows(c[0]), A.tile_cols(c[1]),
-                           b_off=((par * nlines + my_line) * maxcnt + j) * nbe)
-                pack = pb.finalize()
-            root = A.grid.rank(*((my_line, panel_owner_cross(k)) if lower else (panel_owner_cross(k), my_line)))
-
-            def f_comm(pack=pack, par=par, my_cnt=my_cnt, root=root):
-                if pack is not None:
-                    # local slab -> G[par][my_line] (ld = mb)
-                    ops.geadd(0, dplasmaNoTrans, 1.0, A.data, A.ld, 0.0, G, A.mb, pack, copy=True)
-                if my_cnt > 0 and cross_group is not None:
-                    comm.bcast(G[par, my_line, :my_cnt], root, cross_group)
-                if line_group is not None:
-                    comm.allgather_inplace(G[par], my_line, line_group)
-            deps = [t_trsm, prev_col, prev_panel, last_upd.get(k - 2)]
-            t_panel = tp.task(f"PANEL_COMM({k})", "panel", f_comm, deps, prio=2)
-
-            def poff(i, par=par, idx_in_line=idx_in_line):
-                return ((par * nlines + owner_of_panel_line(i)) * maxcnt + idx_in_line[i]) * nbe
-            panel = _Panel(G, A.mb, poff)
-        else:
-            t_panel = t_trsm if t_trsm is not None else t_potrf
-            panel = _Panel(A.data, A.ld, lambda i, k=k: A.offset(*tcoord(i, k)))
-        prev_panel = t_panel
-        # ---------------- trailing update: tiles (m, n) with k < n <= m (lower)
-        col_b, rest_b = GemmBatch(), GemmBatch()
-        for n_ in range(k + 1, nt):
+    def add_update(batch, ks, ncols):
+        """Trailing tiles (m, n), n in ncols, m >= n (lower), updated by the panels ks."""
+        for n_ in ncols:
             for m_ in range(n_, nt):
-                c = (m_, n_) if lower else (n_, m_)
-                if not A.is_local(*c):
+                cc = (m_, n_) if lower else (n_, m_)
+                if not A.is_local(*cc):
                     continue
-                kp = [(panel.off(c[0] if lower else c[0]), panel.off(c[1]), kb)]
-                b = col_b if n_ == k + 1 else rest_b
-                b.add(A.offset(*c), A.tile_rows(c[0]), A.tile_cols(c[1]), kp, tri_mask if m_ == n_ else 0)
-        col_b.finalize()
-        rest_b.finalize()
-        tA, tB = (dplasmaNoTrans, dplasmaConjTrans) if lower else (dplasmaConjTrans, dplasmaNoTrans)
+                # lower: C(m,n) -= L(m,k) L(n,k)^H ; upper: C(n,m) -= U(k,n)^H U(k,m)
+                kp = [(panels[k].off(cc[0]), panels[k].off(cc[1]), A.tile_rows(k)) for k in ks]
+                batch.add(A.offset(*cc), A.tile_rows(cc[0]), A.tile_cols(cc[1]), kp,
+                          tri_mask if m_ == n_ else 0)
+        return batch.finalize()
 
-        def f_upd(batch, panel=panel, tA=tA, tB=tB):
-            ops.gemm(tA, tB, -1.0, panel.base, panel.ld, panel.base, panel.ld, 1.0, A.data, A.ld, batch)
-        t_col = None
-        if len(col_b):
-            t_col = tp.task(f"UPDCOL({k})", "update", lambda b=col_b, f=f_upd: f(b), [t_panel], prio=2)
-            last_upd[k] = t_col
-        if len(rest_b):
-            last_upd[k] = tp.task(f"UPDREST({k})", "update", lambda b=rest_b, f=f_upd: f(b), [t_panel], prio=1)
-        prev_col = t_col
+    def f_upd(batch, base, ld):
+        ops.gemm(tA, tB, -1.0, base, ld, base, ld, 1.0, A.data, A.ld, batch)
+
+    gate = None        # task the next POTRF must follow (NEAR(k-1) or NEXT(b-1))
+    last_upd = {}      # block -> last update-stream task reading its panels
+    last_panel = None  # last panel-stream communication task
+    for b, (c0, c1) in enumerate(blocks):
+        par = b % 2
+        for k in range(c0, c1):
+            kb = A.tile_rows(k)
+            dk = tcoord(k, k)
+            own_diag = A.is_local(*dk)
+            in_panel_cross = (panel_owner_cross(k) == my_cross)
+            # ---------------- POTRF(k)
+            t_potrf = None
+            if own_diag:
+                off = A.offset(*dk)
+
+                def f_potrf(off=off, kb=kb, k=k):
+                    ops.potrf_tile(uplo, A.data, off, kb, A.ld, info, k * A.mb)
+                t_potrf = tp.task(f"POTRF({k})", "panel", f_potrf, [gate], prio=3)
+            # ---------------- local panel tiles (i > k) of my process row/col
+            mine = [i for i in range(k + 1, nt) if in_panel_cross and owner_of_panel_line(i) == my_line]
+            # ---------------- diag tile to the panel owners (column for lower) and TRSM
+            t_trsm = None
+            if in_panel_cross:
+                if distributed and nlines > 1:
+                    src = A.grid.rank(*((owner_of_panel_line(k), panel_owner_cross(k)) if lower
+                                        else (panel_owner_cross(k), owner_of_panel_line(k))))
+                    dk_off = A.offset(*dk) if own_diag else None
+
+                    def f_dbcast(dk_off=dk_off, src=src, kb=kb):
+                        if dk_off is not None:
+                            dv = torch.as_strided(dbuf, (kb, kb), (1, A.mb), 0)
+                            dv.copy_(torch.as_strided(A.data, (kb, kb), (1, A.ld), dk_off))
+                        comm.bcast(dbuf, src, line_group)
+                    t_db = tp.task(f"DBCAST({k})", "panel", f_dbcast, [t_potrf, gate], prio=3)
+                    tri_base, tri_ld, tri_off = dbuf, A.mb, 0
+                else:
+                    t_db = t_potrf
+                    tri_base, tri_ld, tri_off = A.data, A.ld, A.offset(*dk)
+                if mine:
+                    tb = TileBatch()
+                    for i in mine:
+                        cc = tcoord(i, k)
+                        tb.add(tri_off, A.tile_rows(cc[0]), A.tile_cols(cc[1]), b_off=A.offset(*cc))
+                    tb.finalize()
+                    side = dplasmaRight if lower else dplasmaLeft
+
+                    def f_trsm(tb=tb, tri_base=tri_base, tri_ld=tri_ld, side=side):
+                        ops.trsm(side, uplo, dplasmaConjTrans, dplasmaNonUnit, 1.0, tri_base, tri_ld, A.data, A.ld,
+                                 tb)
+                    t_trsm = tp.task(f"TRSM({k})", "panel", f_trsm, [t_db, gate], prio=2)
+            if k == nt - 1:
+                break
+            # ---------------- panel distribution
+            if distributed:
+                slot = k - c0
+                lines_cnt = [0] * nlines
+                idx_in_line = {}
+                for i in range(k + 1, nt):
+                    ln = owner_of_panel_line(i)
+                    idx_in_line[i] = lines_cnt[ln]
+                    lines_cnt[ln] += 1
+                my_cnt = lines_cnt[my_line]
+                Gk = G[par, slot]
+                pack = None
+                if in_panel_cross and mine:
+                    pb = TileBatch()
+                    for j, i in enumerate(mine):
+                        cc = tcoord(i, k)
+                        pb.add(A.offset(*cc), A.tile_rows(cc[0]), A.tile_cols(cc[1]),
+                               b_off=(((par * D + slot) * nlines + my_line) * maxcnt + j) * nbe)
+                    pack = pb.finalize()
+                root = A.grid.rank(*((my_line, panel_owner_cross(k)) if lower else (panel_owner_cross(k), my_line)))
+
+                def f_comm(pack=pack, Gk=Gk, my_cnt=my_cnt, root=root):
+                    if pack is not None:
+                        # local slab -> G[par][slot][my_line] (ld = mb)
+                        ops.geadd(0, dplasmaNoTrans, 1.0, A.data, A.ld, 0.0, G, A.mb, pack, copy=True)
+                    if my_cnt > 0 and cross_group is not None:
+                        comm.bcast(Gk[my_line, :my_cnt], root, cross_group)
+                    if line_group is not None:
+                        comm.allgather_inplace(Gk, my_line, line_group)
+                # G[par] is reused by block b+2: its previous readers (NEXT/REST of block b-2) must be done
+                t_panel = tp.task(f"PANEL_COMM({k})", "panel", f_comm,
+                                  [t_trsm, gate, last_panel, last_upd.get(b - 2)], prio=2)
+                last_panel = t_panel
+
+                def poff(i, par=par, slot=slot, idx_in_line=idx_in_line):
+                    return ((((par * D + slot) * nlines + owner_of_panel_line(i)) * maxcnt + idx_in_line[i]) * nbe)
+                panels[k] = _Panel(G, A.mb, poff)
+            else:
+                t_panel = t_trsm if t_trsm is not None else t_potrf
+                panels[k] = _Panel(A.data, A.ld, lambda i, k=k: A.offset(*tcoord(i, k)))
+            base, ld = panels[k].base, panels[k].ld
+            # ---------------- NEAR(k): the rest of this block, right now (panel stream)
+            near = add_update(GemmBatch(), [k], range(k + 1, c1))
+            if len(near):
+                gate = tp.task(f"NEAR({k})", "panel", lambda bt=near, bs=base, l=ld: f_upd(bt, bs, l),
+                               [t_panel, gate], prio=2)
+            else:
+                gate = t_panel if t_panel is not None else gate
+        if c1 >= nt:
+            break
+        # ---------------- block b's panels update the next block (critical) and the rest (bulk)
+        ks = list(range(c0, c1))
+        n0, n1 = blocks[b + 1]
+        base, ld = panels[c0].base, panels[c0].ld
+        nxt = add_update(GemmBatch(), ks, range(n0, n1))
+        rest = add_update(GemmBatch(), ks, range(n1, nt))
+        deps = [gate, last_panel]
+        t_next = None
+        if len(nxt):
+            t_next = tp.task(f"NEXT({b})", "update", lambda bt=nxt, bs=base, l=ld: f_upd(bt, bs, l), deps, prio=2)
+            last_upd[b] = t_next
+        if len(rest):
+            last_upd[b] = tp.task(f"REST({b})", "update", lambda bt=rest, bs=base, l=ld: f_upd(bt, bs, l), deps,
+                                  prio=1)
+        # the next block's first POTRF follows NEXT(b) (and, for this rank, the block's NEARs)
+        gate = t_next if t_next is not None else gate
 
     def _done():
         v = info.clone()

@@ -29,6 +29,20 @@ def free_port():
     return p
 
 
+def _plain(x, to_np=True):
+    """Results cross the process boundary by value: tensors as numpy arrays (a tensor sent through
+    an mp.Queue is shared by file descriptor and races with the exiting child)."""
+    if to_np and isinstance(x, torch.Tensor):
+        return ("__tensor__", x.detach().cpu().numpy().copy())
+    if not to_np and isinstance(x, tuple) and len(x) == 2 and x[0] == "__tensor__":
+        return torch.from_numpy(x[1])
+    if isinstance(x, (list, tuple)):
+        return type(x)(_plain(v, to_np) for v in x)
+    if isinstance(x, dict):
+        return {k: _plain(v, to_np) for k, v in x.items()}
+    return x
+
+
 def _worker(rank, world, port, fn, args, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -36,7 +50,7 @@ def _worker(rank, world, port, fn, args, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         r = fn(rank, world, *args)
-        q.put((rank, "ok", r))
+        q.put((rank, "ok", _plain(r)))
     except Exception as e:  # pragma: no cover - reported to parent
         import traceback
         q.put((rank, "err", traceback.format_exc()))
@@ -58,7 +72,7 @@ def run_distributed(fn, world, *args, timeout=240):
             rank, status, r = q.get(timeout=timeout)
             if status != "ok":
                 raise RuntimeError(f"rank {rank} failed:\n{r}")
-            out[rank] = r
+            out[rank] = _plain(r, to_np=False)
     finally:
         for p in procs:
             p.join(timeout=30)

@@ -38,6 +38,29 @@ def test_potrf_distributed(world, P, uplo):
     assert (tri(full) - tri(ref)).abs().max() < 1e-12
 
 
+@pytest.mark.parametrize("world,P", [(2, 1), (4, 2)])
+@pytest.mark.parametrize("uplo", [122, 121])
+@pytest.mark.parametrize("defer", [2, 3])
+def test_potrf_distributed_deferred(world, P, uplo, defer, monkeypatch):
+    """Blocks of D panels with aggregated NEXT/REST updates (k = D*NB), on a ragged last tile."""
+    monkeypatch.setenv("DPLASMA_POTRF_DEFER", str(defer))
+    monkeypatch.setenv("DPLASMA_POTRF_DEFER_MIN_TILES", "3")
+    N, NB = 150, 17
+    out = run_distributed(_potrf_worker, world, P, N, NB, uplo, "d")
+    full = sum(out[r][3] for r in range(world))
+    for r in range(world):
+        info, ok, res, _ = out[r]
+        assert info == 0 and ok, (r, res)
+    import dplasma_amd as dp
+    ctx = dp.Context(device="cpu")
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+    dp.plghe(ctx, float(N), uplo, A, 3872)
+    dp.potrf(ctx, uplo, A)
+    ref = A.to_dense_local()
+    tri = (lambda x: x.tril()) if uplo == 122 else (lambda x: x.triu())
+    assert (tri(full) - tri(ref)).abs().max() < 1e-12
+
+
 def _gemm_worker(rank, world, P, ta, tb, kc):
     import dplasma_amd as dp
     ctx = dp.init(device="cpu", P=P)

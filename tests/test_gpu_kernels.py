@@ -138,6 +138,23 @@ def test_potrf(gctx, prec, uplo, dims):
     assert ok, res
 
 
+@pytest.mark.parametrize("uplo", [dp.dplasmaLower, dp.dplasmaUpper])
+@pytest.mark.parametrize("N,NB,defer", [(3072, 256, 4), (2900, 256, 3), (6144, 512, 4)])
+def test_potrf_deferred_blocks(gctx, uplo, N, NB, defer, monkeypatch):
+    """Deferred trailing updates (blocks of D panels, k = D*NB) incl. a ragged last tile."""
+    monkeypatch.setenv("DPLASMA_POTRF_DEFER", str(defer))
+    monkeypatch.setenv("DPLASMA_POTRF_DEFER_MIN_TILES", "3")
+    A = dp.block_cyclic(gctx, torch.float64, NB, NB, N, N)
+    dp.plghe(gctx, float(N), uplo, A, 3872)
+    A0 = A.like()
+    dp.lacpy(gctx, dp.dplasmaUpperLower, A, A0)
+    tp = dp.potrf_New(gctx, uplo, A)
+    assert any(t.name.startswith("REST(") for t in tp.tasks)
+    assert tp.execute(gctx) == 0
+    ok, res = dp.check_potrf(gctx, uplo, A, A0)
+    assert ok, res
+
+
 def test_potrf_matches_cpu(gctx, cctx):
     N, NB = 700, 128
     outs = []

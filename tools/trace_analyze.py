@@ -42,11 +42,12 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--from-kernel", default="k_potrf")
     ap.add_argument("--engine", default="k_gemm")
+    ap.add_argument("--skip", type=int, default=0, help="start at the (skip+1)-th --from-kernel dispatch")
     args = ap.parse_args()
     rows = list(csv.DictReader(open(args.trace)))
     ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows]
     ks.sort()
-    t0 = next(s for s, e, n in ks if args.from_kernel in n)
+    t0 = [s for s, e, n in ks if args.from_kernel in n][args.skip]
     win = [(s, e, n) for s, e, n in ks if s >= t0]
     t1 = max(e for s, e, n in win)
     wall = t1 - t0
