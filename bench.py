@@ -52,6 +52,12 @@ def main():
         local = int(os.environ.get("LOCAL_RANK", "0"))
         if args.cpu:
             dist.init_process_group("gloo")
+        elif os.environ.get("DPLASMA_DIST_BACKEND") == "gloo":
+            # rehearsal of the multi-rank GPU path on fewer GPUs than ranks (gloo moves GPU tensors
+            # through the host); ranks share devices round-robin
+            local %= torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
         else:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))

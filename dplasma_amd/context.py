@@ -55,13 +55,15 @@ class Context:
         if device is None:
             want_gpu = (gpus is None or gpus > 0) and torch.cuda.is_available()
             if want_gpu:
-                lr = int(os.environ.get("LOCAL_RANK", self.rank % max(1, torch.cuda.device_count())))
+                nd = max(1, torch.cuda.device_count())
+                lr = int(os.environ.get("LOCAL_RANK", self.rank % nd)) % nd
                 device = torch.device("cuda", lr)
             else:
                 device = torch.device("cpu")
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
-            lr = int(os.environ.get("LOCAL_RANK", self.rank % max(1, torch.cuda.device_count())))
+            nd = max(1, torch.cuda.device_count())
+            lr = int(os.environ.get("LOCAL_RANK", self.rank % nd)) % nd
             self.device = torch.device("cuda", lr)
         self.is_gpu = self.device.type == "cuda"
         self.nb_cores = nb_cores or int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))

@@ -32,12 +32,16 @@ def bcast(t: torch.Tensor, src_global: int, group) -> None:
     w.wait()
 
 
+def _nccl() -> bool:
+    return dist.get_backend() == "nccl"
+
+
 def allgather_inplace(out: torch.Tensor, my_index: int, group) -> None:
     """out is [n_in_group, ...] contiguous; slot my_index already holds my contribution."""
     if group is None:
         return
     inp = out[my_index]
-    if out.device.type == "cuda":
+    if out.device.type == "cuda" and _nccl():
         w = dist.all_gather_into_tensor(out.view(-1), inp.reshape(-1).clone() if False else inp.reshape(-1),
                                         group=group, async_op=True)
         w.wait()
