@@ -1,0 +1,282 @@
+// Device-resident partial-pivoting LU building blocks (no host round trip per step).
+//
+// Reference roles: CORE_zgetrf_rectil / _reclap -- the recursive, multithreaded panel of
+// src/cores/core_zgetrf_rectil.c:120-279 (spin barriers + shared amax arrays between
+// threads), the GETRF_MAX / GETRF_RDC / GETRF_SND pivot search of
+// src/zgetrf_ptgpanel.jdf:206-590, and CORE_zlaswp / zlaswp_ontile (core_zlaswp.c:62-224).
+//
+// MI355X design:
+//  * The tall panel (m up to 64k rows x NB columns, column-major, one buffer) is factored by a
+//    recursive LU (host-side recursion in dplasma_amd.ops: halves -> laswp + TRSM + MFMA GEMM);
+//    its base case is a column block of <= 64 columns handled by dpl_lu_block, which issues one
+//    launch per column.  Launch j, over every row of the panel (256 rows per workgroup, one row
+//    per thread, coalesced column-major reads):
+//      1. applies column j-1: l = a(r, j-1) / a(j-1, j-1); a(r, j-1) = l;
+//         a(r, c) -= l * a(j-1, c) for the block's columns c > j-1   (rank-1 update)
+//      2. computes the workgroup's |max| of column j over its rows,
+//      3. the LAST workgroup to finish (agent-scope release / ticket / acquire, per
+//         cdna_hip_programming.md G16) reduces the partial maxima, records the pivot and swaps
+//         the two rows across the block -- so the pivot search never leaves the GPU and the
+//         next launch sees the swapped rows (kernel boundary).
+//  * Trailing interchanges: dpl_piv_moves turns the sequential swaps (LAPACK ipiv) into the
+//    net list of moved rows on the device (one thread, LDS hash of displaced rows), and
+//    dpl_rows_gather / dpl_rows_scatter move those rows across any set of local tile columns
+//    through a staging buffer (the rows' owners contribute, others write zeros, so on a P x Q
+//    grid one all-reduce of the staging buffer inside the process column completes the
+//    exchange -- SWAP_COLLECT / SWAP_SND of the reference without host planning).
+#include "common.h"
+
+#define LUR 256        // rows per workgroup (one per thread)
+#define LU_MAXBW 64    // widest base block
+
+template <typename T>
+__device__ inline void last_wg_fence_ticket(int* cnt, int nwg, bool& last) {
+  __shared__ int s_last;
+  // every wave's stores are issued and drained before the workgroup's ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (t == nwg - 1);
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  last = s_last;
+}
+
+// One column step of the blocked panel LU (see header).  Rows [row0, m) take part; row0 = j
+// (rows above j are final).  Block columns [c0, cend); j in [c0, cend]:
+//   j > c0   : apply column j-1 (scale + rank-1 update of columns j..cend-1)
+//   j < cend : pivot search on column j, last workgroup swaps rows j <-> p over [c0, cend)
+template <typename T>
+__global__ __launch_bounds__(LUR) void k_lu_col(T* __restrict__ A, int ld, int m, int c0, int cend, int j,
+                                                int* __restrict__ ipiv, typename ST<T>::real* __restrict__ wsv,
+                                                int* __restrict__ wsi, int* __restrict__ cnt, int* __restrict__ info,
+                                                int info_base, int pivot) {
+  typedef typename ST<T>::real R;
+  const int tid = threadIdx.x;
+  const int r = j + blockIdx.x * LUR + tid;
+  const bool in = r < m;
+  // ---- 1. rank-1 update with column j-1 (pivot row j-1 is final)
+  if (j > c0 && in) {
+    const int jp = j - 1;
+    const T d = A[jp + (long long)jp * ld];
+    T l = A[r + (long long)jp * ld];
+    if (!is_zero(d)) l = divv(l, d);
+    A[r + (long long)jp * ld] = l;
+    for (int c = j; c < cend; ++c) {
+      const T u = A[jp + (long long)c * ld];
+      A[r + (long long)c * ld] = sub(A[r + (long long)c * ld], mul(l, u));
+    }
+  }
+  if (j >= cend || !pivot) {
+    if (j < cend && !pivot && blockIdx.x == 0 && tid == 0) {
+      ipiv[j] = j;
+      if (is_zero(A[j + (long long)j * ld]) && info) atomicCAS(info, 0, info_base + j + 1);
+    }
+    return;
+  }
+  // ---- 2. workgroup |max| of column j (ties -> smallest row, LAPACK i?amax)
+  __shared__ R sv[LUR];
+  __shared__ int si[LUR];
+  sv[tid] = in ? abs1(A[r + (long long)j * ld]) : R(-1);
+  si[tid] = in ? r : 0x7fffffff;
+  __syncthreads();
+  for (int s = LUR / 2; s > 0; s >>= 1) {
+    if (tid < s) {
+      const R a = sv[tid], b = sv[tid + s];
+      if (b > a || (b == a && si[tid + s] < si[tid])) { sv[tid] = b; si[tid] = si[tid + s]; }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    wsv[blockIdx.x] = sv[0];
+    wsi[blockIdx.x] = si[0];
+  }
+  // ---- 3. last workgroup: global pivot, swap rows over the block
+  bool last;
+  last_wg_fence_ticket<T>(cnt, gridDim.x, last);
+  if (!last) return;
+  R best = R(-1);
+  int bi = 0x7fffffff;
+  for (int b = tid; b < (int)gridDim.x; b += LUR) {
+    const R v = wsv[b];   // plain loads after the agent-scope acquire
+    const int i = wsi[b];
+    if (v > best || (v == best && i < bi)) { best = v; bi = i; }
+  }
+  sv[tid] = best;
+  si[tid] = bi;
+  __syncthreads();
+  for (int s = LUR / 2; s > 0; s >>= 1) {
+    if (tid < s) {
+      const R a = sv[tid], b = sv[tid + s];
+      if (b > a || (b == a && si[tid + s] < si[tid])) { sv[tid] = b; si[tid] = si[tid + s]; }
+    }
+    __syncthreads();
+  }
+  const int p = si[0];
+  if (p != j) {
+    for (int c = c0 + tid; c < cend; c += LUR) {
+      const T t = A[j + (long long)c * ld];
+      A[j + (long long)c * ld] = A[p + (long long)c * ld];
+      A[p + (long long)c * ld] = t;
+    }
+  }
+  if (tid == 0) {
+    ipiv[j] = p;
+    if (sv[0] == R(0) && info) atomicCAS(info, 0, info_base + j + 1);
+    *cnt = 0;  // ready for the next launch (kernel boundary orders it)
+  }
+}
+
+// Sequential interchanges rows i <-> ipiv[i], i in [i0, i1), on columns [ca, cb) of the panel.
+template <typename T>
+__global__ __launch_bounds__(64) void k_laswp_panel(T* __restrict__ A, int ld, int ca, int cb,
+                                                    const int* __restrict__ ipiv, int i0, int i1) {
+  const int c = ca + blockIdx.x * 64 + threadIdx.x;
+  if (c >= cb) return;
+  T* col = A + (long long)c * ld;
+  for (int i = i0; i < i1; ++i) {
+    const int p = ipiv[i];
+    if (p != i) {
+      const T t = col[i];
+      col[i] = col[p];
+      col[p] = t;
+    }
+  }
+}
+
+// Net row moves of the sequential interchanges ipiv[0..kb) (panel-relative rows): after the
+// swaps, row dst[t] holds the former row src[t]; cnt[0] = number of moved rows (<= 2 kb).
+// One thread: the top kb rows in an LDS array, displaced rows below kb in an LDS hash table.
+#define HSZ 4096
+__global__ __launch_bounds__(64) void k_piv_moves(const int* __restrict__ ipiv, int kb, int* __restrict__ dst,
+                                                  int* __restrict__ src, int* __restrict__ cnt) {
+  __shared__ int top[1024];
+  __shared__ int hkey[HSZ], hval[HSZ];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kb; i += 64) top[i] = i;
+  for (int i = tid; i < HSZ; i += 64) hkey[i] = -1;
+  __syncthreads();
+  if (tid != 0) return;
+  auto slot = [&](int row) -> int {
+    unsigned h = ((unsigned)row * 2654435761u) & (HSZ - 1);
+    while (hkey[h] != -1 && hkey[h] != row) h = (h + 1) & (HSZ - 1);
+    return (int)h;
+  };
+  for (int i = 0; i < kb; ++i) {
+    const int p = ipiv[i];
+    if (p == i) continue;
+    const int a = top[i];
+    int b;
+    if (p < kb) {
+      b = top[p];
+      top[p] = a;
+    } else {
+      const int h = slot(p);
+      if (hkey[h] == -1) { hkey[h] = p; hval[h] = p; }
+      b = hval[h];
+      hval[h] = a;
+    }
+    top[i] = b;
+  }
+  int n = 0;
+  for (int i = 0; i < kb; ++i)
+    if (top[i] != i) { dst[n] = i; src[n] = top[i]; ++n; }
+  for (int h = 0; h < HSZ; ++h)
+    if (hkey[h] != -1 && hval[h] != hkey[h]) { dst[n] = hkey[h]; src[n] = hval[h]; ++n; }
+  cnt[0] = n;
+}
+
+// Row moves across local tile columns of a tiled matrix.  Global view row R = r0 + rel lives in
+// view tile-row R / mb at local offset rowoff[R / mb] (+ R % mb); -1 = not on this rank.
+// Column c of the flattened set: tile t = c / nb (coloff[t], ncols[t]), element c % nb.
+// gather : buf[t_row * ldb + c] = A[src row] (0 if the row is not local)
+// scatter: A[dst row] = buf[...] (only if the row is local)
+template <typename T, bool GATHER>
+__global__ __launch_bounds__(256) void k_rows_move(T* __restrict__ A, int ld, int mb, int r0,
+                                                   const long long* __restrict__ rowoff, int nrt,
+                                                   const long long* __restrict__ coloff, const int* __restrict__ ncols,
+                                                   int nct, int nb, const int* __restrict__ rows,
+                                                   const int* __restrict__ cnt, T* __restrict__ buf, int ldb) {
+  const int t = blockIdx.y;
+  if (t >= cnt[0]) return;
+  const int R = r0 + rows[t];
+  const int rt = R / mb;
+  const long long ro = (rt < nrt) ? rowoff[rt] : -1;
+  const int W = nct * nb;
+  for (int c = blockIdx.x * 256 + threadIdx.x; c < W; c += gridDim.x * 256) {
+    const int ct = c / nb, cc = c % nb;
+    if (cc >= ncols[ct]) continue;
+    const long long a = ro + (R % mb) + coloff[ct] + (long long)cc * ld;
+    if (GATHER) {
+      buf[(long long)c * ldb + t] = (ro >= 0) ? A[a] : ST<T>::zero();
+    } else if (ro >= 0) {
+      A[a] = buf[(long long)c * ldb + t];
+    }
+  }
+}
+
+#define DISPATCH(prec, CALL)                                          \
+  switch (prec) {                                                     \
+    case DPL_S: { typedef float T; CALL; } break;                     \
+    case DPL_D: { typedef double T; CALL; } break;                    \
+    case DPL_C: { typedef hipFloatComplex T; CALL; } break;           \
+    case DPL_Z: { typedef hipDoubleComplex T; CALL; } break;          \
+    default: return -2;                                               \
+  }
+
+// Factor block columns [c0, cend) of the panel A (m rows, ld) with partial pivoting (or none):
+// cend - c0 + 1 launches of k_lu_col.  ws: >= 2*ceil(m/256) 8-byte words + 1 int counter
+// (zero on first use; each launch leaves it zero).
+DPL_API int dpl_lu_block(int prec, void* A, int ld, int m, int c0, int cend, int* ipiv, void* ws, int* cnt,
+                         int* info, int info_base, int pivot, hipStream_t st) {
+  if (cend - c0 > LU_MAXBW || c0 >= cend || m <= c0) return cend <= c0 ? 0 : -3;
+  const int maxwg = (m + LUR - 1) / LUR;
+  for (int j = c0; j <= cend; ++j) {
+    const int rows = m - j;
+    if (rows <= 0) break;
+    const int nwg = (rows + LUR - 1) / LUR;
+    DISPATCH(prec, {
+      typedef typename ST<T>::real R;
+      hipLaunchKernelGGL((k_lu_col<T>), dim3(nwg), dim3(LUR), 0, st, (T*)A, ld, m, c0, cend, j, ipiv, (R*)ws,
+                         (int*)((R*)ws + maxwg), cnt, info, info_base, pivot);
+    });
+  }
+  return (int)hipGetLastError();
+}
+
+DPL_API int dpl_laswp_panel(int prec, void* A, int ld, int ca, int cb, const int* ipiv, int i0, int i1,
+                            hipStream_t st) {
+  if (cb <= ca || i1 <= i0) return 0;
+  DISPATCH(prec, hipLaunchKernelGGL((k_laswp_panel<T>), dim3((cb - ca + 63) / 64), dim3(64), 0, st, (T*)A, ld, ca,
+                                    cb, ipiv, i0, i1));
+  return (int)hipGetLastError();
+}
+
+DPL_API int dpl_piv_moves(const int* ipiv, int kb, int* dst, int* src, int* cnt, hipStream_t st) {
+  if (kb > 1024) return -3;
+  hipLaunchKernelGGL(k_piv_moves, dim3(1), dim3(64), 0, st, ipiv, kb, dst, src, cnt);
+  return (int)hipGetLastError();
+}
+
+DPL_API int dpl_rows_move(int prec, int gather, void* A, int ld, int mb, int r0, const long long* rowoff, int nrt,
+                          const long long* coloff, const int* ncols, int nct, int nb, const int* rows,
+                          const int* cnt, int maxcnt, void* buf, int ldb, hipStream_t st) {
+  if (nct <= 0 || maxcnt <= 0) return 0;
+  const int W = nct * nb;
+  dim3 g((W + 255) / 256 > 32 ? 32 : (W + 255) / 256, maxcnt);
+  if (gather) {
+    DISPATCH(prec, hipLaunchKernelGGL((k_rows_move<T, true>), g, dim3(256), 0, st, (T*)A, ld, mb, r0, rowoff, nrt,
+                                      coloff, ncols, nct, nb, rows, cnt, (T*)buf, ldb));
+  } else {
+    DISPATCH(prec, hipLaunchKernelGGL((k_rows_move<T, false>), g, dim3(256), 0, st, (T*)A, ld, mb, r0, rowoff, nrt,
+                                      coloff, ncols, nct, nb, rows, cnt, (T*)buf, ldb));
+  }
+  return (int)hipGetLastError();
+}

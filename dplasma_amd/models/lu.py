@@ -109,91 +109,147 @@ def _row_pairs(M: TiledMatrix, rows_dst, rows_src, coltiles, dst_off_fn=None, sr
     return np.array(out, dtype=ops.ROW_PAIR)
 
 
-class _Getrf1D:
-    """Per-step closures of the 1-D partial-pivoting LU."""
+class _GetrfDev:
+    """Partial-pivoting LU, device-resident (getrf_1d on 1 x Q grids, getrf_ptgpanel on P x Q).
 
-    def __init__(self, ctx, A, IPIV, info):
-        self.ctx, self.A, self.IPIV, self.info = ctx, A, IPIV, info
-        self.dev = A.device
+    Step k (every batch and panel plan is built once, here; a run only launches):
+      1. the panel's process column assembles the tall panel (its tiles summed over the P
+         process rows -> replicated) and factors it with the recursive device LU
+         (ops.PanelLU: dgetrf2 halves, <=64-column blocks with an on-device multi-workgroup
+         pivot search -- GETRF_MAX / RDC / SND of src/zgetrf_ptgpanel.jdf:206-590);
+      2. factored panel + pivots travel along process rows (RCCL broadcast);
+      3. the net row moves are derived on the device (ops.piv_moves) and applied to every
+         local tile column through a staging buffer, summed over the process column when
+         P > 1 (SWAP_COLLECT / SWAP_SND, :825-978) -- no host round trip, no host planning;
+      4. the U block row is solved where it lives and broadcast down process columns;
+      5. one batched MFMA GEMM launch updates the trailing tiles."""
+
+    def __init__(self, ctx, A, info):
+        self.ctx, self.A, self.info = ctx, A, info
+        dev = self.dev = A.device
         mb, nb = A.mb, A.nb
+        g = A.grid
         self.kt = min(A.mt, A.nt)
-        self.pbuf = torch.zeros(A.m * nb, dtype=A.dtype, device=self.dev)
-        self.piv_dev = torch.zeros(nb, dtype=torch.int32, device=self.dev)
-        self.ipiv_all = torch.zeros(min(A.m, A.n), dtype=torch.int32, device=self.dev)
+        self.pbuf = torch.zeros(max(1, A.m * nb), dtype=A.dtype, device=dev)
+        self.piv_dev = torch.zeros(nb, dtype=torch.int32, device=dev)
+        self.ipiv_all = torch.zeros(max(1, min(A.m, A.n)), dtype=torch.int32, device=dev)
+        self.ws = torch.zeros(2 * ((A.m + 255) // 256) + 8, dtype=torch.float64, device=dev)
+        self.cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.mdst = torch.zeros(2 * nb, dtype=torch.int32, device=dev)
+        self.msrc = torch.zeros(2 * nb, dtype=torch.int32, device=dev)
+        self.mcnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        # row / column offset tables of the local tiles (offset(m, n) = rowoff[m] + coloff[n])
+        lrows = [m for m in range(A.mt) if A.row_is_local(m)]
+        lcols = [n for n in range(A.nt) if A.col_is_local(n)]
+        self.lcols = lcols
+        if lrows and lcols:
+            mr, nr = lrows[0], lcols[0]
+            base = A.offset(mr, nr)
+            rowoff = [A.offset(m, nr) - base if A.row_is_local(m) else -1 for m in range(A.mt)]
+            coloff = [A.offset(mr, n) for n in lcols]
+            self.rowoff = torch.tensor(rowoff, dtype=torch.int64, device=dev)
+            self.coloff = torch.tensor(coloff, dtype=torch.int64, device=dev)
+            self.ncols = torch.tensor([A.tile_cols(n) for n in lcols], dtype=torch.int32, device=dev)
+            width = len(lcols) * nb
+            self.tmp = torch.zeros(2 * nb * width, dtype=A.dtype, device=dev)
+        else:
+            self.rowoff = self.coloff = self.ncols = self.tmp = None
+        ncol_loc = sum(A.tile_cols(n) for n in lcols)
+        self.ubuf = torch.zeros(max(1, nb * max(ncol_loc, 1)), dtype=A.dtype, device=dev)
+        self.plan = [self._build(k) for k in range(self.kt)]
 
-    def step(self, k):
-        A, ctx = self.A, self.ctx
+    def _build(self, k):
+        A = self.A
         mb = A.mb
         kb = A.tile_cols(k)
         r0 = k * mb
-        mp = A.m - r0                      # panel rows
-        owner = A.grid.pcol(k + A.jt0)
-        me_owner = A.col_is_local(k)
-        pv = self.pbuf[: mp * kb]
-        # --- 1. assemble + factor the panel on its owner
-        if me_owner:
-            tb = TileBatch()
-            for m in range(k, A.mt):
-                tb.add(A.offset(m, k), A.tile_rows(m), kb, b_off=(m - k) * mb)
-            tb.finalize()
-            ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, pv, mp, tb, copy=True)
-            ops.getrf_panel(pv, 0, mp, kb, mp, self.piv_dev, self.info, r0, pivot=True)
-            # write the factored panel back
-            back = TileBatch()
-            for m in range(k, A.mt):
-                back.add((m - k) * mb, A.tile_rows(m), kb, b_off=A.offset(m, k))
-            back.finalize()
-            ops.geadd(0, N_, 1.0, pv, mp, 0.0, A.data, A.ld, back, copy=True)
-        # --- 2. broadcast factored panel + pivots (world == process row for P = 1)
-        if ctx.world > 1:
-            comm.bcast(pv, owner, ctx.row_group)
-            comm.bcast(self.piv_dev, owner, ctx.row_group)
-        # --- 3. apply the net permutation to local columns != k
-        piv = self.piv_dev[: min(mp, kb)].cpu().numpy()  # small D2H (pivots drive the row moves)
-        self.ipiv_all[r0: r0 + len(piv)] = torch.from_numpy(piv.astype(np.int32) + r0 + 1).to(self.dev)
-        perm = _perm_from_swaps(piv, mp)
-        moved = np.nonzero(perm != np.arange(mp))[0]
-        cols = [n for n in range(A.nt) if n != k and A.col_is_local(n)]
-        if len(moved) and cols:
-            dst_rows = moved + r0
-            src_rows = perm[moved] + r0
-            full = [n for n in cols if A.tile_cols(n) == A.nb]
-            ragged = [n for n in cols if A.tile_cols(n) != A.nb]
-            nmv = len(moved)
-            tmp = torch.empty(max(1, nmv * len(cols)) * A.nb, dtype=A.dtype, device=self.dev)
-            for group in (full, ragged):
-                if not group:
-                    continue
-                w = A.tile_cols(group[0])
-                # gather sources into tmp (row-major-ish: row i of column tile j at (j*nmv + i), stride nmv*len)
-                ld_t = nmv * len(group)
-                pairs_in = []
-                pairs_out = []
-                for j, n in enumerate(group):
-                    for i in range(nmv):
-                        s = int(src_rows[i])
-                        d = int(dst_rows[i])
-                        pairs_in.append((j * nmv + i, A.offset(s // mb, n) + s % mb))
-                        pairs_out.append((A.offset(d // mb, n) + d % mb, j * nmv + i))
-                ops.row_gather(tmp, A.data, np.array(pairs_in, dtype=ops.ROW_PAIR), w, ld_t, A.ld)
-                ops.row_gather(A.data, tmp, np.array(pairs_out, dtype=ops.ROW_PAIR), w, A.ld, ld_t)
-        # --- 4. U row block: A(k, n) = L(k,k)^-1 A(k, n), n > k local
+        mp = A.m - r0
+        st = {"kb": kb, "r0": r0, "mp": mp, "kmin": min(mp, kb)}
+        if A.col_is_local(k):
+            mine = [m for m in range(k, A.mt) if A.row_is_local(m)]
+            if mine:
+                tb, back = TileBatch(), TileBatch()
+                for m in mine:
+                    tb.add(A.offset(m, k), A.tile_rows(m), kb, b_off=(m - k) * mb)
+                    back.add((m - k) * mb, A.tile_rows(m), kb, b_off=A.offset(m, k))
+                st["gather"], st["back"] = tb.finalize(), back.finalize()
+            st["plu"] = ops.PanelLU(self.pbuf, mp, mp, kb, pivot=True)
         trail = [n for n in range(k + 1, A.nt) if A.col_is_local(n)]
-        if trail:
+        st["trail"] = trail
+        if trail and A.row_is_local(k):
             tb = TileBatch()
             for n in trail:
                 tb.add(0, kb, A.tile_cols(n), b_off=A.offset(k, n))
-            tb.finalize()
-            ops.trsm(dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, pv, mp, A.data, A.ld, tb)
-            # --- 5. trailing update A(m, n) -= L(m, k) U(k, n)
-            if k + 1 < A.mt:
+            st["trsm"] = tb.finalize()
+        if trail and k + 1 < A.mt:
+            uoff, c = {}, 0
+            for n in trail:
+                uoff[n] = c * kb
+                c += A.tile_cols(n)
+            st["ulen"] = c * kb
+            if A.row_is_local(k):
+                tb = TileBatch()
+                for n in trail:
+                    tb.add(A.offset(k, n), kb, A.tile_cols(n), b_off=uoff[n])
+                st["upack"] = tb.finalize()
+            rows = [m for m in range(k + 1, A.mt) if A.row_is_local(m)]
+            if rows:
                 gb = GemmBatch()
                 for n in trail:
-                    for m in range(k + 1, A.mt):
-                        gb.add(A.offset(m, n), A.tile_rows(m), A.tile_cols(n),
-                               [((m - k) * mb, A.offset(k, n), kb)])
-                gb.finalize()
-                ops.gemm(N_, N_, -1.0, pv, mp, A.data, A.ld, 1.0, A.data, A.ld, gb)
+                    for m in rows:
+                        gb.add(A.offset(m, n), A.tile_rows(m), A.tile_cols(n), [((m - k) * mb, uoff[n], kb)])
+                st["gemm"] = gb.finalize()
+        return st
+
+    def step(self, k):
+        A, ctx = self.A, self.ctx
+        g = A.grid
+        st = self.plan[k]
+        kb, r0, mp, kmin = st["kb"], st["r0"], st["mp"], st["kmin"]
+        pc = g.pcol(k + A.jt0)
+        pv = self.pbuf[: mp * kb]
+        # --- 1. panel (process column pc): assemble, replicate over P, factor on the device
+        if A.col_is_local(k):
+            if g.P > 1:
+                pv.zero_()
+            if "gather" in st:
+                ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, pv, mp, st["gather"], copy=True)
+            if g.P > 1:
+                dist.all_reduce(pv, group=ctx.col_group)
+            st["plu"].run(self.piv_dev, self.ws, self.cnt, self.info, r0)
+        # --- 2. factored panel + pivots along process rows
+        if g.Q > 1:
+            root = g.rank(A.myrow, pc)
+            comm.bcast(pv, root, ctx.row_group)
+            comm.bcast(self.piv_dev, root, ctx.row_group)
+        self.ipiv_all[r0: r0 + kmin].copy_(self.piv_dev[:kmin] + (r0 + 1))
+        # --- 3. row interchanges on every local column (the panel column is rewritten below)
+        if self.tmp is not None:
+            ops.piv_moves(self.piv_dev, kmin, self.mdst, self.msrc, self.mcnt)
+            ldb = 2 * A.nb
+            ops.rows_move(True, A.data, A.ld, A.mb, r0, self.rowoff, self.coloff, self.ncols, A.nb, self.msrc,
+                          self.mcnt, ldb, self.tmp, ldb)
+            if g.P > 1:
+                dist.all_reduce(self.tmp, group=ctx.col_group)
+            ops.rows_move(False, A.data, A.ld, A.mb, r0, self.rowoff, self.coloff, self.ncols, A.nb, self.mdst,
+                          self.mcnt, ldb, self.tmp, ldb)
+        if "back" in st:
+            ops.geadd(0, N_, 1.0, pv, mp, 0.0, A.data, A.ld, st["back"], copy=True)
+        # --- 4. U block row where it lives, then down the process column
+        if not st["trail"]:
+            return
+        if "trsm" in st:
+            ops.trsm(dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, pv, mp, A.data, A.ld, st["trsm"])
+        if "ulen" not in st:
+            return
+        ub = self.ubuf
+        if "upack" in st:
+            ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, ub, kb, st["upack"], copy=True)
+        if g.P > 1:
+            comm.bcast(ub[: st["ulen"]], g.rank(g.prow(k + A.it0), A.mycol), ctx.col_group)
+        # --- 5. trailing update A(m, n) -= L(m, k) U(k, n)
+        if "gemm" in st:
+            ops.gemm(N_, N_, -1.0, pv, mp, ub, kb, 1.0, A.data, A.ld, st["gemm"])
 
 
 def _permute_rows_2d(ctx, A, dst_rows, src_rows, coltiles):
@@ -266,99 +322,6 @@ def _permute_rows_2d(ctx, A, dst_rows, src_rows, coltiles):
             slot += len(recvs[q]) * nct
 
 
-class _GetrfPtg:
-    """Partial-pivoting LU on a P x Q grid (getrf_ptgpanel role, src/zgetrf_ptgpanel.jdf).
-
-    Step k: the panel's tiles are summed into one buffer inside their process
-    column (all-reduce over P ranks) and factored redundantly there (pivot
-    search over the whole column, ``GETRF_MAX/RDC/SND`` of the reference); the
-    factored panel and pivots are broadcast along process rows; interchanges
-    cross process rows through one all-to-all per process column (``SWAP_*``);
-    the U block row is solved where it lives, broadcast down process columns,
-    and the trailing update is one batched GEMM launch per rank."""
-
-    def __init__(self, ctx, A, info):
-        self.ctx, self.A, self.info = ctx, A, info
-        self.dev = A.device
-        self.kt = min(A.mt, A.nt)
-        self.pbuf = torch.zeros(A.m * A.nb, dtype=A.dtype, device=self.dev)
-        self.piv_dev = torch.zeros(A.nb, dtype=torch.int32, device=self.dev)
-        self.ipiv_all = torch.zeros(min(A.m, A.n), dtype=torch.int32, device=self.dev)
-        ncol = sum(A.tile_cols(n) for n in range(A.nt) if A.col_is_local(n))
-        self.ubuf = torch.zeros(max(1, A.nb * max(ncol, 1)), dtype=A.dtype, device=self.dev)
-
-    def step(self, k):
-        A, ctx = self.A, self.ctx
-        g = A.grid
-        mb = A.mb
-        kb = A.tile_cols(k)
-        r0 = k * mb
-        mp = A.m - r0
-        pc = g.pcol(k + A.jt0)
-        pv = self.pbuf[: mp * kb]
-        # --- 1. panel: sum the column's pieces inside process column pc, factor redundantly
-        if A.col_is_local(k):
-            pv.zero_()
-            mine = [m for m in range(k, A.mt) if A.row_is_local(m)]
-            if mine:
-                tb = TileBatch()
-                for m in mine:
-                    tb.add(A.offset(m, k), A.tile_rows(m), kb, b_off=(m - k) * mb)
-                ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, pv, mp, tb.finalize(), copy=True)
-            if g.P > 1:
-                dist.all_reduce(pv, group=ctx.col_group)
-            ops.getrf_panel(pv, 0, mp, kb, mp, self.piv_dev, self.info, r0, pivot=True)
-            if mine:
-                back = TileBatch()
-                for m in mine:
-                    back.add((m - k) * mb, A.tile_rows(m), kb, b_off=A.offset(m, k))
-                ops.geadd(0, N_, 1.0, pv, mp, 0.0, A.data, A.ld, back.finalize(), copy=True)
-        # --- 2. factored panel + pivots along process rows
-        if g.Q > 1:
-            root = g.rank(A.myrow, pc)
-            comm.bcast(pv, root, ctx.row_group)
-            comm.bcast(self.piv_dev, root, ctx.row_group)
-        piv = self.piv_dev[: min(mp, kb)].cpu().numpy()
-        self.ipiv_all[r0: r0 + len(piv)] = torch.from_numpy(piv.astype(np.int32) + r0 + 1).to(self.dev)
-        # --- 3. interchanges on every column but k
-        perm = _perm_from_swaps(piv, mp)
-        moved = np.nonzero(perm != np.arange(mp))[0]
-        cols = [n for n in range(A.nt) if n != k and A.col_is_local(n)]
-        _permute_rows_2d(ctx, A, moved + r0, perm[moved] + r0, cols)
-        # --- 4. U block row where it lives
-        trail = [n for n in range(k + 1, A.nt) if A.col_is_local(n)]
-        if not trail:
-            return
-        if A.row_is_local(k):
-            tb = TileBatch()
-            for n in trail:
-                tb.add(0, kb, A.tile_cols(n), b_off=A.offset(k, n))
-            ops.trsm(dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, pv, mp, A.data, A.ld, tb.finalize())
-        if k + 1 >= A.mt:
-            return
-        # --- 5. U block row down the process column (packed kb x sum(cols))
-        ub = self.ubuf
-        uoff, c = {}, 0
-        for n in trail:
-            uoff[n] = c * kb
-            c += A.tile_cols(n)
-        if A.row_is_local(k):
-            tb = TileBatch()
-            for n in trail:
-                tb.add(A.offset(k, n), kb, A.tile_cols(n), b_off=uoff[n])
-            ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, ub, kb, tb.finalize(), copy=True)
-        if g.P > 1:
-            comm.bcast(ub[: c * kb], g.rank(g.prow(k + A.it0), A.mycol), ctx.col_group)
-        # --- 6. trailing update A(m, n) -= L(m, k) U(k, n)
-        rows = [m for m in range(k + 1, A.mt) if A.row_is_local(m)]
-        if rows:
-            gb = GemmBatch()
-            for n in trail:
-                for m in rows:
-                    gb.add(A.offset(m, n), A.tile_rows(m), A.tile_cols(n), [((m - k) * mb, uoff[n], kb)])
-            ops.gemm(N_, N_, -1.0, pv, mp, ub, kb, 1.0, A.data, A.ld, gb.finalize())
-
-
 def getrf_ptgpanel_New(ctx, A, IPIV, info_out=None):
     """Partial-pivoting LU on any P x Q grid (dplasma_zgetrf_ptgpanel_New).
 
@@ -367,7 +330,7 @@ def getrf_ptgpanel_New(ctx, A, IPIV, info_out=None):
     tp = Taskpool("getrf_ptgpanel", ctx)
     tp.flops = flops(A.prec, "getrf", A.m, A.n)
     info = torch.zeros(1, dtype=torch.int32, device=A.device)
-    st = _GetrfPtg(ctx, A, info)
+    st = _GetrfDev(ctx, A, info)
     prev = None
     for k in range(st.kt):
         prev = tp.task(f"getrf_ptg({k})", "update", (lambda k=k: st.step(k)), [prev])
@@ -405,7 +368,7 @@ def getrf_1d_New(ctx, A, IPIV, info_out=None):
     tp = Taskpool("getrf_1d", ctx)
     tp.flops = flops(A.prec, "getrf", A.m, A.n)
     info = torch.zeros(1, dtype=torch.int32, device=A.device)
-    st = _Getrf1D(ctx, A, IPIV, info)
+    st = _GetrfDev(ctx, A, info)
     prev = None
     for k in range(st.kt):
         prev = tp.task(f"getrf1d({k})", "update", (lambda k=k: st.step(k)), [prev])

@@ -62,6 +62,16 @@ _SIGS = {
     "dpl_diag_scale": [c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp],
     # prec, kind, part, unit, nitems, items, A, lda, out, ostride, stream
     "dpl_tile_norm": [c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_int, c_vp],
+    # device-resident pivoting LU (lu_piv.hip)
+    # prec, A, ld, m, c0, cend, ipiv, ws, cnt, info, info_base, pivot, stream
+    "dpl_lu_block": [c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp],
+    # prec, A, ld, ca, cb, ipiv, i0, i1, stream
+    "dpl_laswp_panel": [c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp],
+    # ipiv, kb, dst, src, cnt, stream
+    "dpl_piv_moves": [c_vp, c_int, c_vp, c_vp, c_vp, c_vp],
+    # prec, gather, A, ld, mb, r0, rowoff, nrt, coloff, ncols, nct, nb, rows, cnt, maxcnt, buf, ldb, stream
+    "dpl_rows_move": [c_int, c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp,
+                      c_int, c_vp, c_int, c_vp],
 }
 _OPTIONAL = set()
 

@@ -531,3 +531,160 @@ def diag_scale(part: int, cols: bool, D: torch.Tensor, ldd: int, B: torch.Tensor
         d = torch.as_strided(D, (k,), (ldd + 1,), int(it["a_off"]))
         new = b / (d.view(1, -1) if cols else d.view(-1, 1))
         b.copy_(torch.where(_part_mask(it, m, n, p), new, b))
+
+
+# ----------------------------------------------------------------------------- device-pivoting LU
+LU_BW = 64   # base block width of the recursive panel LU (lu_piv.hip LU_MAXBW)
+
+
+def lu_block(P: torch.Tensor, ld: int, m: int, c0: int, cend: int, ipiv: torch.Tensor, ws: torch.Tensor,
+             cnt: torch.Tensor, info: torch.Tensor, info_base: int, pivot: bool = True):
+    """Unblocked LU with partial pivoting of panel columns [c0, cend), rows [c0, m) of the column-major
+    buffer P (ld): swaps only inside the block columns, ipiv[j] = panel-relative pivot row."""
+    if cend <= c0 or m <= c0:
+        return
+    if _is_gpu(P):
+        rc = _lib.load().dpl_lu_block(_lib.prec_code(P.dtype), P.data_ptr(), ld, m, c0, cend, ipiv.data_ptr(),
+                                      ws.data_ptr(), cnt.data_ptr(), info.data_ptr(), int(info_base), int(pivot),
+                                      _lib.stream_ptr())
+        _lib.check(rc, "lu_block")
+        return
+    A = torch.as_strided(P, (m, cend), (1, ld), 0)
+    for j in range(c0, min(cend, m)):
+        col = A[j:, j]
+        p = j + int(torch.argmax(col.abs() if not col.is_complex() else col.real.abs() + col.imag.abs())) \
+            if pivot else j
+        ipiv[j] = p
+        if p != j:
+            t = A[j, c0:cend].clone()
+            A[j, c0:cend] = A[p, c0:cend]
+            A[p, c0:cend] = t
+        d = A[j, j]
+        if d == 0:
+            if int(info[0]) == 0:
+                info[0] = info_base + j + 1
+        else:
+            A[j + 1:, j] /= d
+        if j + 1 < cend:
+            A[j + 1:, j + 1:cend] -= torch.outer(A[j + 1:, j], A[j, j + 1:cend])
+
+
+def laswp_panel(P: torch.Tensor, ld: int, ca: int, cb: int, ipiv: torch.Tensor, i0: int, i1: int):
+    """Sequential row interchanges i <-> ipiv[i] (i in [i0, i1)) on columns [ca, cb) of panel P."""
+    if cb <= ca or i1 <= i0:
+        return
+    if _is_gpu(P):
+        rc = _lib.load().dpl_laswp_panel(_lib.prec_code(P.dtype), P.data_ptr(), ld, ca, cb, ipiv.data_ptr(), i0, i1,
+                                         _lib.stream_ptr())
+        _lib.check(rc, "laswp_panel")
+        return
+    nrow = int(ipiv[i0:i1].max()) + 1 if i1 > i0 else 0
+    A = torch.as_strided(P, (max(nrow, i1), cb - ca), (1, ld), ca * ld)
+    for i in range(i0, i1):
+        p = int(ipiv[i])
+        if p != i:
+            t = A[i].clone()
+            A[i] = A[p]
+            A[p] = t
+
+
+def piv_moves(ipiv: torch.Tensor, kb: int, dst: torch.Tensor, src: torch.Tensor, cnt: torch.Tensor):
+    """Net row moves of the sequential interchanges ipiv[:kb]: row dst[t] receives former row src[t]."""
+    if _is_gpu(ipiv):
+        rc = _lib.load().dpl_piv_moves(ipiv.data_ptr(), kb, dst.data_ptr(), src.data_ptr(), cnt.data_ptr(),
+                                       _lib.stream_ptr())
+        _lib.check(rc, "piv_moves")
+        return
+    cur = {}
+    for i in range(kb):
+        p = int(ipiv[i])
+        if p != i:
+            a, b = cur.get(i, i), cur.get(p, p)
+            cur[i], cur[p] = b, a
+    moves = sorted((d, s_) for d, s_ in cur.items() if d != s_)
+    for t, (d, s_) in enumerate(moves):
+        dst[t] = d
+        src[t] = s_
+    cnt[0] = len(moves)
+
+
+def rows_move(gather: bool, A: torch.Tensor, ld: int, mb: int, r0: int, rowoff: torch.Tensor, coloff: torch.Tensor,
+              ncols: torch.Tensor, nb: int, rows: torch.Tensor, cnt: torch.Tensor, maxcnt: int, buf: torch.Tensor,
+              ldb: int):
+    """gather: buf[t, c] = A[r0 + rows[t], col c] (0 where the row is not local);
+    scatter: A[r0 + rows[t], col c] = buf[t, c] where local.  Columns: the flattened local tile
+    columns (coloff[j], ncols[j]); buf is column-major with leading dimension ldb."""
+    nct = int(coloff.numel())
+    if nct == 0:
+        return
+    if _is_gpu(A):
+        rc = _lib.load().dpl_rows_move(_lib.prec_code(A.dtype), int(gather), A.data_ptr(), ld, mb, r0,
+                                       rowoff.data_ptr(), int(rowoff.numel()), coloff.data_ptr(), ncols.data_ptr(),
+                                       nct, nb, rows.data_ptr(), cnt.data_ptr(), maxcnt, buf.data_ptr(), ldb,
+                                       _lib.stream_ptr())
+        _lib.check(rc, "rows_move")
+        return
+    n = int(cnt[0])
+    for t in range(n):
+        R = r0 + int(rows[t])
+        ro = int(rowoff[R // mb]) if R // mb < rowoff.numel() else -1
+        for j in range(nct):
+            w = int(ncols[j])
+            if w == 0:
+                continue
+            bv = torch.as_strided(buf, (w,), (ldb,), j * nb * ldb + t)
+            if ro < 0:
+                if gather:
+                    bv.zero_()
+                continue
+            av = torch.as_strided(A, (w,), (ld,), ro + R % mb + int(coloff[j]))
+            if gather:
+                bv.copy_(av)
+            else:
+                av.copy_(bv)
+
+
+class PanelLU:
+    """Recursive LU with partial pivoting of one tall column-major panel (m x n, ld), device-resident:
+    halves until <= LU_BW columns (lu_block), then laswp + TRSM + MFMA GEMM to join the halves
+    (the dgetrf2 recursion; reference CORE_zgetrf_rectil's role).  The TRSM / GEMM batches of
+    every recursion node are built once here and re-used by every run."""
+
+    def __init__(self, buf: torch.Tensor, ld: int, m: int, n: int, pivot: bool = True):
+        self.buf, self.ld, self.m, self.n, self.pivot = buf, ld, m, n, pivot
+        self.plan = []
+        kf = min(m, n)
+        self._rec(0, kf)
+        if n > kf:   # wide panel: the columns past the last row only get the swaps and U = L^-1 A
+            self.plan.append(("laswp", kf, n, 0, kf))
+            self.plan.append(("trsm", TileBatch().add(0, kf, n - kf, b_off=kf * ld).finalize()))
+
+    def _rec(self, c0: int, n: int):
+        ld, m = self.ld, self.m
+        if n <= LU_BW:
+            self.plan.append(("block", c0, c0 + n))
+            return
+        n1 = (n // 2 + 15) // 16 * 16
+        self._rec(c0, n1)
+        c1 = c0 + n1
+        self.plan.append(("laswp", c1, c0 + n, c0, c1))
+        tb = TileBatch().add(c0 + c0 * ld, n1, n - n1, b_off=c0 + c1 * ld).finalize()
+        self.plan.append(("trsm", tb))
+        if m > c1:
+            gb = GemmBatch().add(c1 + c1 * ld, m - c1, n - n1, [(c1 + c0 * ld, c0 + c1 * ld, n1)]).finalize()
+            self.plan.append(("gemm", gb))
+        self._rec(c1, n - n1)
+        self.plan.append(("laswp", c0, c1, c1, c0 + n))
+
+    def run(self, ipiv: torch.Tensor, ws: torch.Tensor, cnt: torch.Tensor, info: torch.Tensor, info_base: int):
+        P, ld, m = self.buf, self.ld, self.m
+        for op in self.plan:
+            if op[0] == "block":
+                lu_block(P, ld, m, op[1], op[2], ipiv, ws, cnt, info, info_base, self.pivot)
+            elif op[0] == "laswp":
+                if self.pivot:
+                    laswp_panel(P, ld, op[1], op[2], ipiv, op[3], op[4])
+            elif op[0] == "trsm":
+                trsm(dplasmaLeft, dplasmaLower, dplasmaNoTrans, dplasmaUnit, 1.0, P, ld, P, ld, op[1])
+            else:
+                gemm(dplasmaNoTrans, dplasmaNoTrans, -1.0, P, ld, P, ld, 1.0, P, ld, op[1])

@@ -29,13 +29,18 @@ def free_port():
     return p
 
 
+class _TensorBox:
+    def __init__(self, arr):
+        self.arr = arr
+
+
 def _plain(x, to_np=True):
     """Results cross the process boundary by value: tensors as numpy arrays (a tensor sent through
     an mp.Queue is shared by file descriptor and races with the exiting child)."""
     if to_np and isinstance(x, torch.Tensor):
-        return ("__tensor__", x.detach().cpu().numpy().copy())
-    if not to_np and isinstance(x, tuple) and len(x) == 2 and x[0] == "__tensor__":
-        return torch.from_numpy(x[1])
+        return _TensorBox(x.detach().cpu().numpy().copy())
+    if not to_np and isinstance(x, _TensorBox):
+        return torch.from_numpy(x.arr)
     if isinstance(x, (list, tuple)):
         return type(x)(_plain(v, to_np) for v in x)
     if isinstance(x, dict):

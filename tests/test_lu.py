@@ -147,17 +147,16 @@ def test_gerfs(ctx):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("prec", list("dz"))
-def test_gpu_getrf_ptgpanel(prec):
+@pytest.mark.parametrize("prec,N,NB", [("d", 700, 128), ("z", 700, 128), ("d", 3000, 512), ("s", 1100, 256)])
+def test_gpu_getrf_ptgpanel(prec, N, NB):
     gctx = dp.init(device="cuda:0")
     dt = DTYPES[prec]
-    N, NB = 700, 128
     A = dp.block_cyclic(gctx, dt, NB, NB, N, N)
     dp.plrnt(gctx, A, 9)
     a = A.to_dense_local().cpu()
     IPIV = dp.ptgpanel_ipiv_descriptor(gctx, A)
     assert dp.getrf_ptgpanel(gctx, A, IPIV) == 0
     lu, piv = torch.linalg.lu_factor(a)
-    assert rel_err(A.to_dense_local().cpu(), lu) < 1e-11
+    assert rel_err(A.to_dense_local().cpu(), lu) < (1e-3 if prec == "s" else 1e-11)
     from dplasma_amd.models.lu import _gather_ipiv
     assert (torch.from_numpy(_gather_ipiv(gctx, IPIV)).long() == piv.long()).all()

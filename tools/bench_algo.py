@@ -48,6 +48,22 @@ def main():
             dp.plghe(ctx, float(N), dp.dplasmaUpperLower, A, 3872)
             t0 = time.perf_counter()
             tp = dp.getrf_nopiv_New(ctx, A)
+        elif a.op == "getrf_ptgpanel":
+            IPIV = dp.ptgpanel_ipiv_descriptor(ctx, A)
+            t0 = time.perf_counter()
+            tp = dp.getrf_ptgpanel_New(ctx, A, IPIV)
+        elif a.op == "getrf_incpiv":
+            L = dp.incpiv_L_descriptor(ctx, A, a.ib)
+            IPIV = dp.incpiv_ipiv_descriptor(ctx, A)
+            t0 = time.perf_counter()
+            tp = dp.getrf_incpiv_New(ctx, A, L, IPIV)
+        elif a.op == "gemm":
+            B = dp.block_cyclic(ctx, dt, a.nb, a.nb, N, N)
+            C = dp.block_cyclic(ctx, dt, a.nb, a.nb, M, N)
+            dp.plrnt(ctx, B, 4674)
+            dp.plrnt(ctx, C, 2873)
+            t0 = time.perf_counter()
+            tp = dp.gemm_New(ctx, dp.dplasmaNoTrans, dp.dplasmaNoTrans, 0.51, A, B, -0.42, C)
         elif a.op == "getrf_1d":
             IPIV = dp.ipiv_descriptor(ctx, A)
             t0 = time.perf_counter()
