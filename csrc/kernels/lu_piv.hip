@@ -222,6 +222,149 @@ __global__ __launch_bounds__(256) void k_rows_move(T* __restrict__ A, int ld, in
   }
 }
 
+// ---------------------------------------------------------------- persistent block LU
+// Same block factorisation as k_lu_col, in ONE launch with the block's rows resident in LDS:
+// G workgroups (<= one per CU), workgroup w owns panel rows [c0 + w R, c0 + (w+1) R) x the
+// block's BW columns (R <= 256 rows, one per thread; R x BW x 8 B <= 128 KiB of LDS).
+// Per column j, ONE grid barrier: before it every workgroup publishes its local |max| with
+// that row's BW values (the candidate pivot row) and the owner of row j publishes row j;
+// after it every workgroup reduces the G candidates (same answer everywhere), takes the winner
+// as the new row j and the owner of the pivot row takes the old row j -- the interchange needs
+// no second hand-off.  Barrier: monotonic agent-scope counter (release fence -> arrive ->
+// relaxed poll with s_sleep -> acquire fence; MI355X_MICROARCH.md barrier-counter), published
+// data double-buffered by column parity.  Rank-1 updates run on the LDS copy.
+#define PLR 256
+#define PBW 64
+// Bounded spin: if the grid is not co-resident (e.g. several processes share the device) the
+// barrier gives up after ~2 s, flags info = -1000 and lets the kernel drain instead of hanging.
+template <typename T>
+__device__ inline void grid_sync_counter(int* cnt, int target, int* info) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ULL) {  // 100 MHz clock: 2 s
+        if (info) atomicExch(info, -1000);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+template <typename T>
+__global__ __launch_bounds__(PLR) void k_lu_block_persist(T* __restrict__ A, int ld, int m, int c0, int cend, int R,
+                                                          int* __restrict__ ipiv, T* __restrict__ cand,
+                                                          double* __restrict__ pval, int* __restrict__ pidx,
+                                                          int* __restrict__ cnt, int* __restrict__ info,
+                                                          int info_base) {
+  __shared__ T tile[PBW * PLR];      // column-major: tile[c * R + r]
+  __shared__ T prow[PBW], oldj[PBW];
+  __shared__ double sv[PLR];
+  __shared__ int si[PLR];
+  const int G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
+  const int BW = cend - c0;
+  const int rbase = c0 + w * R;
+  const int nr = max(0, min(R, m - rbase));   // rows owned
+  // ---- load the block rows
+  for (int e = tid; e < BW * R; e += PLR) {
+    const int c = e / R, r = e % R;
+    if (r < nr) tile[c * R + r] = A[(rbase + r) + (long long)(c0 + c) * ld];
+  }
+  __syncthreads();
+  const int r = tid, g = rbase + tid;
+  const bool own = r < nr;
+  for (int cj = 0; cj < BW; ++cj) {
+    const int j = c0 + cj;
+    const int par = cj & 1;
+    // ---- 1. apply column cj-1 (pivot row in prow)
+    if (cj > 0 && own && g >= j) {
+      const T d = prow[cj - 1];
+      T l = tile[(cj - 1) * R + r];
+      if (!is_zero(d)) l = divv(l, d);
+      tile[(cj - 1) * R + r] = l;
+      for (int c = cj; c < BW; ++c) tile[c * R + r] = sub(tile[c * R + r], mul(l, prow[c]));
+    }
+    __syncthreads();
+    // ---- 2. local |max| of column cj over rows >= j; publish it with its row, and row j
+    sv[tid] = (own && g >= j) ? (double)abs1(tile[cj * R + r]) : -1.0;
+    si[tid] = (own && g >= j) ? g : 0x7fffffff;
+    __syncthreads();
+    for (int st = PLR / 2; st > 0; st >>= 1) {
+      if (tid < st) {
+        const double a = sv[tid], b = sv[tid + st];
+        if (b > a || (b == a && si[tid + st] < si[tid])) { sv[tid] = b; si[tid] = si[tid + st]; }
+      }
+      __syncthreads();
+    }
+    const int lw = si[0];
+    if (tid == 0) {
+      pval[par * G + w] = sv[0];
+      pidx[par * G + w] = lw;
+    }
+    if (lw != 0x7fffffff && tid < BW) cand[((long long)par * G + w) * PBW + tid] = tile[tid * R + (lw - rbase)];
+    if (j >= rbase && j < rbase + nr && tid < BW)
+      cand[((long long)2 * G + par) * PBW + tid] = tile[tid * R + (j - rbase)];
+    grid_sync_counter<T>(cnt, (cj + 1) * G, info);
+    // ---- 3. global pivot (every workgroup reduces the same G candidates)
+    {
+      double best = -1.0;
+      int bi = 0x7fffffff, bw = 0;
+      for (int b = tid; b < G; b += PLR) {
+        const double v = pval[par * G + b];
+        const int i = pidx[par * G + b];
+        if (v > best || (v == best && i < bi)) { best = v; bi = i; bw = b; }
+      }
+      sv[tid] = best;
+      si[tid] = bi;
+      __syncthreads();
+      __shared__ int swin[PLR];
+      swin[tid] = bw;
+      __syncthreads();
+      for (int st = PLR / 2; st > 0; st >>= 1) {
+        if (tid < st) {
+          const double a = sv[tid], b = sv[tid + st];
+          if (b > a || (b == a && si[tid + st] < si[tid])) { sv[tid] = b; si[tid] = si[tid + st]; swin[tid] = swin[tid + st]; }
+        }
+        __syncthreads();
+      }
+      const int p = si[0], pw = swin[0];
+      if (tid < BW) {
+        prow[tid] = cand[((long long)par * G + pw) * PBW + tid];
+        oldj[tid] = cand[((long long)2 * G + par) * PBW + tid];
+      }
+      __syncthreads();
+      // interchange rows j <-> p on the LDS copies
+      if (tid < BW) {
+        if (j >= rbase && j < rbase + nr) tile[tid * R + (j - rbase)] = prow[tid];
+        if (p != j && p >= rbase && p < rbase + nr) tile[tid * R + (p - rbase)] = oldj[tid];
+      }
+      if (w == 0 && tid == 0) {
+        ipiv[j] = p;
+        if (sv[0] == 0.0 && info) atomicCAS(info, 0, info_base + j + 1);
+      }
+      __syncthreads();
+    }
+  }
+  // ---- last column: scale below the diagonal
+  if (own && g >= cend) {
+    const T d = prow[BW - 1];
+    T l = tile[(BW - 1) * R + r];
+    if (!is_zero(d)) l = divv(l, d);
+    tile[(BW - 1) * R + r] = l;
+  }
+  __syncthreads();
+  for (int e = tid; e < BW * R; e += PLR) {
+    const int c = e / R, rr = e % R;
+    if (rr < nr) A[(rbase + rr) + (long long)(c0 + c) * ld] = tile[c * R + rr];
+  }
+}
+
 #define DISPATCH(prec, CALL)                                          \
   switch (prec) {                                                     \
     case DPL_S: { typedef float T; CALL; } break;                     \
@@ -234,9 +377,48 @@ __global__ __launch_bounds__(256) void k_rows_move(T* __restrict__ A, int ld, in
 // Factor block columns [c0, cend) of the panel A (m rows, ld) with partial pivoting (or none):
 // cend - c0 + 1 launches of k_lu_col.  ws: >= 2*ceil(m/256) 8-byte words + 1 int counter
 // (zero on first use; each launch leaves it zero).
+static int g_num_cus = 0;
+
+// ws layout (bytes): [0, 8*2*G) pval, then 4*2*G pidx, then 8-aligned candidate rows
+// (3 * G * PBW * sizeof(T) <= 3 * 256 * 64 * 16 B); callers size it with dpl_lu_block_ws_bytes.
+DPL_API long long dpl_lu_block_ws_bytes(int m) {
+  const int maxwg = (m + LUR - 1) / LUR;
+  long long a = 16LL * (maxwg > 256 ? maxwg : 256) + 64;
+  return a + 3LL * 256 * PBW * 16 + 64;
+}
+
 DPL_API int dpl_lu_block(int prec, void* A, int ld, int m, int c0, int cend, int* ipiv, void* ws, int* cnt,
                          int* info, int info_base, int pivot, hipStream_t st) {
   if (cend - c0 > LU_MAXBW || c0 >= cend || m <= c0) return cend <= c0 ? 0 : -3;
+  // persistent single-launch path: real precisions, rows fit one per thread in <= #CU workgroups
+  if (g_num_cus == 0) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (g_num_cus <= 0) g_num_cus = 1;
+  }
+  const int rows = m - c0;
+  const int gmax = g_num_cus < 256 ? g_num_cus : 256;
+  if (pivot && (prec == DPL_D || prec == DPL_S) && rows <= gmax * PLR && cend - c0 <= PBW) {
+    int G = (rows + 127) / 128;                 // aim at ~128 rows per workgroup
+    if (G > gmax) G = gmax;
+    if (G < 1) G = 1;
+    const int R = (rows + G - 1) / G;
+    if (R <= PLR) {
+      char* b = (char*)ws;
+      double* pval = (double*)b;
+      int* pidx = (int*)(b + 8LL * 2 * 256);
+      void* cand = (void*)(b + 8LL * 2 * 256 + 4LL * 2 * 256 + 64);
+      hipMemsetAsync(cnt, 0, sizeof(int), st);
+      if (prec == DPL_D)
+        hipLaunchKernelGGL((k_lu_block_persist<double>), dim3(G), dim3(PLR), 0, st, (double*)A, ld, m, c0, cend, R,
+                           ipiv, (double*)cand, pval, pidx, cnt, info, info_base);
+      else
+        hipLaunchKernelGGL((k_lu_block_persist<float>), dim3(G), dim3(PLR), 0, st, (float*)A, ld, m, c0, cend, R,
+                           ipiv, (float*)cand, pval, pidx, cnt, info, info_base);
+      return (int)hipGetLastError();
+    }
+  }
   const int maxwg = (m + LUR - 1) / LUR;
   for (int j = c0; j <= cend; ++j) {
     const int rows = m - j;

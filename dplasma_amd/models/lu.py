@@ -133,7 +133,7 @@ class _GetrfDev:
         self.pbuf = torch.zeros(max(1, A.m * nb), dtype=A.dtype, device=dev)
         self.piv_dev = torch.zeros(nb, dtype=torch.int32, device=dev)
         self.ipiv_all = torch.zeros(max(1, min(A.m, A.n)), dtype=torch.int32, device=dev)
-        self.ws = torch.zeros(2 * ((A.m + 255) // 256) + 8, dtype=torch.float64, device=dev)
+        self.ws = ops.lu_workspace(A.m, dev)
         self.cnt = torch.zeros(1, dtype=torch.int32, device=dev)
         self.mdst = torch.zeros(2 * nb, dtype=torch.int32, device=dev)
         self.msrc = torch.zeros(2 * nb, dtype=torch.int32, device=dev)

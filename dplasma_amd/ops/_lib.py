@@ -67,6 +67,7 @@ _SIGS = {
     "dpl_lu_block": [c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp],
     # prec, A, ld, ca, cb, ipiv, i0, i1, stream
     "dpl_laswp_panel": [c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp],
+    "dpl_lu_block_ws_bytes": [c_int],
     # ipiv, kb, dst, src, cnt, stream
     "dpl_piv_moves": [c_vp, c_int, c_vp, c_vp, c_vp, c_vp],
     # prec, gather, A, ld, mb, r0, rowoff, nrt, coloff, ncols, nct, nb, rows, cnt, maxcnt, buf, ldb, stream

@@ -537,6 +537,15 @@ def diag_scale(part: int, cols: bool, D: torch.Tensor, ldd: int, B: torch.Tensor
 LU_BW = 64   # base block width of the recursive panel LU (lu_piv.hip LU_MAXBW)
 
 
+def lu_workspace(m: int, device) -> torch.Tensor:
+    """Scratch for lu_block / PanelLU on panels of up to m rows (pivot candidates, barrier data)."""
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        nbytes = int(_lib.load().dpl_lu_block_ws_bytes(int(m)))
+        return torch.zeros(nbytes // 8 + 8, dtype=torch.float64, device=dev)
+    return torch.zeros(8, dtype=torch.float64)
+
+
 def lu_block(P: torch.Tensor, ld: int, m: int, c0: int, cend: int, ipiv: torch.Tensor, ws: torch.Tensor,
              cnt: torch.Tensor, info: torch.Tensor, info_base: int, pivot: bool = True):
     """Unblocked LU with partial pivoting of panel columns [c0, cend), rows [c0, m) of the column-major

@@ -286,7 +286,8 @@ def test_gemm_full_tile_path(gctx, prec, ta, tb, mask, alpha, beta):
         assert (got - ref).abs().max().item() / ref.abs().max().item() < (1e-12 if prec == "d" else 1e-4)
 
 
-@pytest.mark.parametrize("m,n", [(2000, 128), (4096, 512), (1500, 200), (512, 512), (300, 512)])
+@pytest.mark.parametrize("m,n", [(2000, 128), (4096, 512), (1500, 200), (512, 512), (300, 512), (70000, 128),
+                                 (40000, 64)])
 def test_panel_lu_device(gctx, m, n):
     """Recursive device-resident panel LU (<=64-column blocks with the multi-workgroup on-device
     pivot search) against LAPACK partial pivoting (torch.linalg.lu_factor on the CPU)."""
@@ -295,7 +296,7 @@ def test_panel_lu_device(gctx, m, n):
     a = torch.randn(m, n, dtype=torch.float64)
     P = a.t().contiguous().view(-1).cuda()          # column-major
     ipiv = torch.zeros(n, dtype=torch.int32, device="cuda")
-    ws = torch.zeros(2 * ((m + 255) // 256) + 8, dtype=torch.float64, device="cuda")
+    ws = ops.lu_workspace(m, "cuda")
     cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
     info = torch.zeros(1, dtype=torch.int32, device="cuda")
     plu = ops.PanelLU(P, ld, m, n)
