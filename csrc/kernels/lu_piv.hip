@@ -157,10 +157,10 @@ __global__ __launch_bounds__(64) void k_laswp_panel(T* __restrict__ A, int ld, i
 #define HSZ 4096
 __global__ __launch_bounds__(64) void k_piv_moves(const int* __restrict__ ipiv, int kb, int* __restrict__ dst,
                                                   int* __restrict__ src, int* __restrict__ cnt) {
-  __shared__ int top[1024];
+  __shared__ int top[1024], pv[1024];
   __shared__ int hkey[HSZ], hval[HSZ];
   const int tid = threadIdx.x;
-  for (int i = tid; i < kb; i += 64) top[i] = i;
+  for (int i = tid; i < kb; i += 64) { top[i] = i; pv[i] = ipiv[i]; }
   for (int i = tid; i < HSZ; i += 64) hkey[i] = -1;
   __syncthreads();
   if (tid != 0) return;
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(64) void k_piv_moves(const int* __restrict__ ipiv, 
     return (int)h;
   };
   for (int i = 0; i < kb; ++i) {
-    const int p = ipiv[i];
+    const int p = pv[i];
     if (p == i) continue;
     const int a = top[i];
     int b;
@@ -204,16 +204,26 @@ __global__ __launch_bounds__(256) void k_rows_move(T* __restrict__ A, int ld, in
                                                    const long long* __restrict__ coloff, const int* __restrict__ ncols,
                                                    int nct, int nb, const int* __restrict__ rows,
                                                    const int* __restrict__ cnt, T* __restrict__ buf, int ldb) {
-  const int t = blockIdx.y;
-  if (t >= cnt[0]) return;
-  const int R = r0 + rows[t];
-  const int rt = R / mb;
-  const long long ro = (rt < nrt) ? rowoff[rt] : -1;
+  // lanes run along the move list (64 moves per wave): the staging buffer is column-major in t
+  // and the moved rows are mostly runs of consecutive rows (the top kb rows), so both sides of
+  // the copy coalesce; the 4 waves of a workgroup take different columns.
+  const int n = cnt[0];
+  const int t = blockIdx.y * 64 + (threadIdx.x & 63);
+  if (blockIdx.y * 64 >= n) return;
+  const bool tin = t < n;
+  int R = 0, rt = 0;
+  long long ro = -1;
+  if (tin) {
+    R = r0 + rows[t];
+    rt = R / mb;
+    ro = (rt < nrt) ? rowoff[rt] : -1;
+  }
+  const long long rbase = ro + (R % mb);
   const int W = nct * nb;
-  for (int c = blockIdx.x * 256 + threadIdx.x; c < W; c += gridDim.x * 256) {
+  for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < W; c += gridDim.x * 4) {
     const int ct = c / nb, cc = c % nb;
-    if (cc >= ncols[ct]) continue;
-    const long long a = ro + (R % mb) + coloff[ct] + (long long)cc * ld;
+    if (!tin || cc >= ncols[ct]) continue;
+    const long long a = rbase + coloff[ct] + (long long)cc * ld;
     if (GATHER) {
       buf[(long long)c * ldb + t] = (ro >= 0) ? A[a] : ST<T>::zero();
     } else if (ro >= 0) {
@@ -237,12 +247,13 @@ __global__ __launch_bounds__(256) void k_rows_move(T* __restrict__ A, int ld, in
 #define PBW 64
 // Bounded spin: if the grid is not co-resident (e.g. several processes share the device) the
 // barrier gives up after ~2 s, flags info = -1000 and lets the kernel drain instead of hanging.
-template <typename T>
+// Every byte handed across the barrier is written and read with agent-scope relaxed atomics
+// (sc1: coherent past the per-XCD L2s) and drained (vmcnt(0)) before the arrival, so the
+// barrier itself needs no cache-maintenance fences (MI355X_MICROARCH.md handoff rows).
 __device__ inline void grid_sync_counter(int* cnt, int target, int* info) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -252,9 +263,25 @@ __device__ inline void grid_sync_counter(int* cnt, int target, int* info) {
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
+}
+
+template <typename T> __device__ inline void st_sc1(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T> __device__ inline T ld_sc1(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// wave-level argmax (|v| desc, row asc) with DPP-free shuffles, then across the 4 waves in LDS
+__device__ inline void wave_argmax(double& v, int& i) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double v2 = __shfl_xor(v, o, 64);
+    const int i2 = __shfl_xor(i, o, 64);
+    if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
+  }
 }
 
 template <typename T>
@@ -292,51 +319,52 @@ __global__ __launch_bounds__(PLR) void k_lu_block_persist(T* __restrict__ A, int
     }
     __syncthreads();
     // ---- 2. local |max| of column cj over rows >= j; publish it with its row, and row j
-    sv[tid] = (own && g >= j) ? (double)abs1(tile[cj * R + r]) : -1.0;
-    si[tid] = (own && g >= j) ? g : 0x7fffffff;
+    double v = (own && g >= j) ? (double)abs1(tile[cj * R + r]) : -1.0;
+    int vi = (own && g >= j) ? g : 0x7fffffff;
+    wave_argmax(v, vi);
+    if ((tid & 63) == 0) { sv[tid >> 6] = v; si[tid >> 6] = vi; }
     __syncthreads();
-    for (int st = PLR / 2; st > 0; st >>= 1) {
-      if (tid < st) {
-        const double a = sv[tid], b = sv[tid + st];
-        if (b > a || (b == a && si[tid + st] < si[tid])) { sv[tid] = b; si[tid] = si[tid + st]; }
-      }
-      __syncthreads();
+    if (tid < 64) {
+      v = tid < PLR / 64 ? sv[tid] : -1.0;
+      vi = tid < PLR / 64 ? si[tid] : 0x7fffffff;
+      wave_argmax(v, vi);
+      if (tid == 0) { sv[0] = v; si[0] = vi; }
     }
+    __syncthreads();
     const int lw = si[0];
     if (tid == 0) {
-      pval[par * G + w] = sv[0];
-      pidx[par * G + w] = lw;
+      st_sc1(&pval[par * G + w], sv[0]);
+      st_sc1(&pidx[par * G + w], lw);
     }
-    if (lw != 0x7fffffff && tid < BW) cand[((long long)par * G + w) * PBW + tid] = tile[tid * R + (lw - rbase)];
+    if (lw != 0x7fffffff && tid < BW) st_sc1(&cand[((long long)par * G + w) * PBW + tid], tile[tid * R + (lw - rbase)]);
     if (j >= rbase && j < rbase + nr && tid < BW)
-      cand[((long long)2 * G + par) * PBW + tid] = tile[tid * R + (j - rbase)];
-    grid_sync_counter<T>(cnt, (cj + 1) * G, info);
+      st_sc1(&cand[((long long)2 * G + par) * PBW + tid], tile[tid * R + (j - rbase)]);
+    grid_sync_counter(cnt, (cj + 1) * G, info);
     // ---- 3. global pivot (every workgroup reduces the same G candidates)
     {
       double best = -1.0;
       int bi = 0x7fffffff, bw = 0;
       for (int b = tid; b < G; b += PLR) {
-        const double v = pval[par * G + b];
-        const int i = pidx[par * G + b];
-        if (v > best || (v == best && i < bi)) { best = v; bi = i; bw = b; }
+        const double pv_ = ld_sc1(&pval[par * G + b]);
+        const int pi_ = ld_sc1(&pidx[par * G + b]);
+        if (pv_ > best || (pv_ == best && pi_ < bi)) { best = pv_; bi = pi_; bw = b; }
       }
-      sv[tid] = best;
-      si[tid] = bi;
+      // the winning workgroup travels with the row index (row -> owner is rbase arithmetic)
+      wave_argmax(best, bi);
+      if ((tid & 63) == 0) { sv[tid >> 6] = best; si[tid >> 6] = bi; }
       __syncthreads();
-      __shared__ int swin[PLR];
-      swin[tid] = bw;
-      __syncthreads();
-      for (int st = PLR / 2; st > 0; st >>= 1) {
-        if (tid < st) {
-          const double a = sv[tid], b = sv[tid + st];
-          if (b > a || (b == a && si[tid + st] < si[tid])) { sv[tid] = b; si[tid] = si[tid + st]; swin[tid] = swin[tid + st]; }
-        }
-        __syncthreads();
+      if (tid < 64) {
+        best = tid < PLR / 64 ? sv[tid] : -1.0;
+        bi = tid < PLR / 64 ? si[tid] : 0x7fffffff;
+        wave_argmax(best, bi);
+        if (tid == 0) { sv[0] = best; si[0] = bi; }
       }
-      const int p = si[0], pw = swin[0];
+      __syncthreads();
+      (void)bw;
+      const int p = si[0], pw = (p - c0) / R;
       if (tid < BW) {
-        prow[tid] = cand[((long long)par * G + pw) * PBW + tid];
-        oldj[tid] = cand[((long long)2 * G + par) * PBW + tid];
+        prow[tid] = ld_sc1(&cand[((long long)par * G + pw) * PBW + tid]);
+        oldj[tid] = ld_sc1(&cand[((long long)2 * G + par) * PBW + tid]);
       }
       __syncthreads();
       // interchange rows j <-> p on the LDS copies
@@ -400,7 +428,7 @@ DPL_API int dpl_lu_block(int prec, void* A, int ld, int m, int c0, int cend, int
   const int rows = m - c0;
   const int gmax = g_num_cus < 256 ? g_num_cus : 256;
   if (pivot && (prec == DPL_D || prec == DPL_S) && rows <= gmax * PLR && cend - c0 <= PBW) {
-    int G = (rows + 127) / 128;                 // aim at ~128 rows per workgroup
+    int G = (rows + 255) / 256;                 // ~256 rows per workgroup: fewest barrier arrivals
     if (G > gmax) G = gmax;
     if (G < 1) G = 1;
     const int R = (rows + G - 1) / G;
@@ -452,7 +480,8 @@ DPL_API int dpl_rows_move(int prec, int gather, void* A, int ld, int mb, int r0,
                           const int* cnt, int maxcnt, void* buf, int ldb, hipStream_t st) {
   if (nct <= 0 || maxcnt <= 0) return 0;
   const int W = nct * nb;
-  dim3 g((W + 255) / 256 > 32 ? 32 : (W + 255) / 256, maxcnt);
+  const int gx = (W + 3) / 4 > 2048 ? 2048 : (W + 3) / 4;
+  dim3 g(gx, (maxcnt + 63) / 64);
   if (gather) {
     DISPATCH(prec, hipLaunchKernelGGL((k_rows_move<T, true>), g, dim3(256), 0, st, (T*)A, ld, mb, r0, rowoff, nrt,
                                       coloff, ncols, nct, nb, rows, cnt, (T*)buf, ldb));
