@@ -1,0 +1,207 @@
+// C ABI of dplasma_amd: embeds CPython and forwards each dplasma_<p><op>() to the framework.
+//
+// The reference exposes its algorithms as C functions over parsec_context_t and
+// parsec_tiled_matrix_t (src/include/dplasma/dplasma_z.h).  Here the handles are Python objects
+// (dplasma_amd.context.Context, dplasma_amd.descriptor.TiledMatrix) owned by this library; every
+// call takes the GIL, converts the C arguments, calls dplasma_amd.capi.call() and returns int /
+// double.  Works inside an existing interpreter too (then Py_Initialize is skipped).
+#include "capi_bridge.h"
+
+#include <dlfcn.h>
+
+#include <cmath>
+#include <cstdlib>
+#include <string>
+
+struct dplasma_context_s { PyObject* obj; };
+struct dplasma_desc_s { PyObject* obj; };
+
+static PyObject* g_capi = nullptr;   // module dplasma_amd.capi
+static thread_local std::string g_err;
+
+static void keep_error() {
+  if (!PyErr_Occurred()) return;
+  PyObject *t, *v, *tb;
+  PyErr_Fetch(&t, &v, &tb);
+  PyObject* s = v ? PyObject_Str(v) : nullptr;
+  g_err = s ? PyUnicode_AsUTF8(s) : "python error";
+  Py_XDECREF(s);
+  Py_XDECREF(t);
+  Py_XDECREF(v);
+  Py_XDECREF(tb);
+}
+
+// repository root = <dir of libdplasma.so>/../.. (dplasma_amd/lib/libdplasma.so)
+static std::string lib_root() {
+  Dl_info info;
+  if (dladdr((void*)&lib_root, &info) && info.dli_fname) {
+    std::string p(info.dli_fname);
+    for (int up = 0; up < 3; ++up) {
+      const size_t s = p.find_last_of('/');
+      if (s == std::string::npos) return ".";
+      p = p.substr(0, s);
+    }
+    return p;
+  }
+  return ".";
+}
+
+static bool ensure_python() {
+  if (!Py_IsInitialized()) {
+    Py_InitializeEx(0);
+    PyEval_SaveThread();   // release the GIL; every entry point takes it with PyGILState_Ensure
+  }
+  if (g_capi) return true;
+  PyGILState_STATE st = PyGILState_Ensure();
+  const char* env = std::getenv("DPLASMA_ROOT");
+  const std::string root = env ? env : lib_root();
+  PyObject* sys_path = PySys_GetObject("path");  // borrowed
+  PyObject* r = PyUnicode_FromString(root.c_str());
+  if (sys_path && r) PyList_Insert(sys_path, 0, r);
+  Py_XDECREF(r);
+  g_capi = PyImport_ImportModule("dplasma_amd.capi");
+  if (!g_capi) keep_error();
+  PyGILState_Release(st);
+  return g_capi != nullptr;
+}
+
+PyObject* dpl_arg_desc(const dplasma_desc_t* d) {
+  if (!d) { Py_RETURN_NONE; }
+  Py_INCREF(d->obj);
+  return d->obj;
+}
+PyObject* dpl_arg_int(long long v) { return PyLong_FromLongLong(v); }
+PyObject* dpl_arg_u64(unsigned long long v) { return PyLong_FromUnsignedLongLong(v); }
+PyObject* dpl_arg_real(double v) { return PyFloat_FromDouble(v); }
+PyObject* dpl_arg_cplx(dplasma_complex64_t v) { return PyComplex_FromDoubles(__real__ v, __imag__ v); }
+PyObject* dpl_arg_cplx(dplasma_complex32_t v) { return PyComplex_FromDoubles(__real__ v, __imag__ v); }
+
+static PyObject* call_obj(dplasma_context_t* ctx, const char* fname, const char* opname,
+                          std::initializer_list<PyObject*> args) {
+  const size_t n = args.size() + (ctx ? 1 : 0) + (opname ? 1 : 0);
+  PyObject* tup = PyTuple_New((Py_ssize_t)n);
+  size_t i = 0;
+  if (ctx) { Py_INCREF(ctx->obj); PyTuple_SET_ITEM(tup, i++, ctx->obj); }
+  if (opname) PyTuple_SET_ITEM(tup, i++, PyUnicode_FromString(opname));
+  bool bad = false;
+  for (PyObject* a : args) {
+    if (!a) { bad = true; a = Py_None; Py_INCREF(a); }
+    PyTuple_SET_ITEM(tup, i++, a);
+  }
+  PyObject* res = nullptr;
+  if (!bad) {
+    PyObject* f = PyObject_GetAttrString(g_capi, fname);
+    if (f) res = PyObject_CallObject(f, tup);
+    Py_XDECREF(f);
+  }
+  Py_DECREF(tup);
+  if (!res) keep_error();
+  return res;
+}
+
+int dpl_call_int(dplasma_context_t* ctx, const char* name, std::initializer_list<PyObject*> args) {
+  PyGILState_STATE st = PyGILState_Ensure();
+  g_err.clear();
+  PyObject* r = call_obj(ctx, "call", name, args);
+  int v = -1;
+  if (r) { v = (int)PyLong_AsLong(r); if (PyErr_Occurred()) { PyErr_Clear(); v = (int)PyFloat_AsDouble(r); } }
+  Py_XDECREF(r);
+  PyGILState_Release(st);
+  return v;
+}
+
+double dpl_call_real(dplasma_context_t* ctx, const char* name, std::initializer_list<PyObject*> args) {
+  PyGILState_STATE st = PyGILState_Ensure();
+  g_err.clear();
+  PyObject* r = call_obj(ctx, "call", name, args);
+  double v = r ? PyFloat_AsDouble(r) : NAN;
+  Py_XDECREF(r);
+  PyGILState_Release(st);
+  return v;
+}
+
+extern "C" {
+
+DPL_CAPI const char* dplasma_last_error(void) { return g_err.c_str(); }
+
+DPL_CAPI dplasma_context_t* dplasma_init(int nb_cores, int gpus) {
+  if (!ensure_python()) return nullptr;
+  PyGILState_STATE st = PyGILState_Ensure();
+  PyObject* o = call_obj(nullptr, "init", nullptr, {PyLong_FromLong(nb_cores), PyLong_FromLong(gpus)});
+  dplasma_context_t* c = nullptr;
+  if (o) { c = new dplasma_context_s; c->obj = o; }
+  PyGILState_Release(st);
+  return c;
+}
+
+DPL_CAPI void dplasma_fini(dplasma_context_t* ctx) {
+  if (!ctx) return;
+  PyGILState_STATE st = PyGILState_Ensure();
+  PyObject* r = call_obj(ctx, "fini", nullptr, {});
+  Py_XDECREF(r);
+  Py_DECREF(ctx->obj);
+  PyGILState_Release(st);
+  delete ctx;
+}
+
+static int ctx_attr(const dplasma_context_t* ctx, const char* a) {
+  if (!ctx) return -1;
+  PyGILState_STATE st = PyGILState_Ensure();
+  PyObject* v = PyObject_GetAttrString(ctx->obj, a);
+  const int r = v ? (int)PyLong_AsLong(v) : -1;
+  Py_XDECREF(v);
+  PyGILState_Release(st);
+  return r;
+}
+DPL_CAPI int dplasma_context_rank(const dplasma_context_t* ctx) { return ctx_attr(ctx, "rank"); }
+DPL_CAPI int dplasma_context_world(const dplasma_context_t* ctx) { return ctx_attr(ctx, "world"); }
+
+DPL_CAPI dplasma_desc_t* dplasma_desc_block_cyclic(dplasma_context_t* ctx, int prec, int mb, int nb, int m, int n,
+                                                   int P, int Q, dplasma_enum_t uplo) {
+  PyGILState_STATE st = PyGILState_Ensure();
+  PyObject* o = call_obj(ctx, "desc_block_cyclic", nullptr,
+                         {PyLong_FromLong(prec), PyLong_FromLong(mb), PyLong_FromLong(nb), PyLong_FromLong(m),
+                          PyLong_FromLong(n), PyLong_FromLong(P), PyLong_FromLong(Q), PyLong_FromLong(uplo)});
+  dplasma_desc_t* d = nullptr;
+  if (o) { d = new dplasma_desc_s; d->obj = o; }
+  PyGILState_Release(st);
+  return d;
+}
+
+DPL_CAPI dplasma_desc_t* dplasma_desc_ipiv(dplasma_context_t* ctx, int mb, int nb, int m, int n, int P, int Q) {
+  PyGILState_STATE st = PyGILState_Ensure();
+  PyObject* o = call_obj(ctx, "desc_int", nullptr,
+                         {PyLong_FromLong(mb), PyLong_FromLong(nb), PyLong_FromLong(m), PyLong_FromLong(n),
+                          PyLong_FromLong(P), PyLong_FromLong(Q)});
+  dplasma_desc_t* d = nullptr;
+  if (o) { d = new dplasma_desc_s; d->obj = o; }
+  PyGILState_Release(st);
+  return d;
+}
+
+DPL_CAPI void dplasma_desc_destroy(dplasma_desc_t* A) {
+  if (!A) return;
+  PyGILState_STATE st = PyGILState_Ensure();
+  Py_DECREF(A->obj);
+  PyGILState_Release(st);
+  delete A;
+}
+
+static int desc_io(const dplasma_desc_t* A, const void* host, int lda, const char* fn) {
+  PyGILState_STATE st = PyGILState_Ensure();
+  PyObject* r = call_obj(nullptr, fn, nullptr,
+                         {dpl_arg_desc(A), PyLong_FromUnsignedLongLong((unsigned long long)(uintptr_t)host),
+                          PyLong_FromLong(lda)});
+  const int v = r ? (int)PyLong_AsLong(r) : -1;
+  Py_XDECREF(r);
+  PyGILState_Release(st);
+  return v;
+}
+DPL_CAPI int dplasma_desc_set_lapack(dplasma_desc_t* A, const void* host, int lda) {
+  return desc_io(A, host, lda, "desc_set_lapack");
+}
+DPL_CAPI int dplasma_desc_get_lapack(const dplasma_desc_t* A, void* host, int lda) {
+  return desc_io(A, host, lda, "desc_get_lapack");
+}
+
+}  // extern "C"

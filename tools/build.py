@@ -95,9 +95,28 @@ def build_runtime(force=False) -> Path | None:
     return lib
 
 
+def build_capi(force=False) -> Path | None:
+    """libdplasma.so: the C ABI (capi/include/dplasma.h) -- embeds CPython, forwards to dplasma_amd."""
+    csrc = ROOT / "capi"
+    srcs = sorted(csrc.glob("*.cpp"))
+    if not srcs:
+        return None
+    lib = OUT / "libdplasma.so"
+    if not force and not _newer(lib, [*srcs, *csrc.glob("*.h")]):
+        return lib
+    pyinc = sysconfig.get_paths()["include"]
+    libdir = sysconfig.get_config_var("LIBDIR") or "/usr/lib"
+    ver = sysconfig.get_config_var("LDVERSION") or sysconfig.get_python_version()
+    _run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", f"-I{pyinc}", f"-I{csrc}",
+          *map(str, srcs), "-o", str(lib), f"-L{libdir}", f"-lpython{ver}", "-ldl", f"-Wl,-rpath,{libdir}"])
+    print(f"[build] linked {lib.relative_to(ROOT)}", flush=True)
+    return lib
+
+
 def build_all(force=False, jobs=8):
     k = build_kernels(force=force, jobs=jobs)
     r = build_runtime(force=force)
+    build_capi(force=force)
     return k, r
 
 
