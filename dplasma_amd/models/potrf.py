@@ -22,9 +22,10 @@ MI355X design (not a translation of the JDF):
   overlap REST(b) -- the critical-path/lookahead structure the reference
   obtains with priorities (zpotrf_L.jdf:58-69).
 * Tiles stay resident in HBM; the panel travels once per step over RCCL/xGMI:
-  the owner column broadcasts its pieces along process rows and every
-  process column all-gathers them, so each rank ends with the full panel in
-  a contiguous slab (G[block parity][panel in block]).
+  the owner column broadcasts its pieces along process rows (each rank needs
+  every panel tile of its own rows), then inside each process column only the
+  tiles that column needs as the second GEMM operand are all-gathered -- a
+  rank receives (nt-k)/P + (nt-k)(P-1)/(PQ) tiles per panel, not (nt-k).
 * Single rank: no copies at all -- the panel is read in place.
 """
 from __future__ import annotations
@@ -115,18 +116,30 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
 
     my_cross = mycol if lower else myrow
 
-    # distributed panel buffers: G[2 (block parity)][D (panel in block)][nlines][maxcnt][nbe]
+    def cross_of(i):  # process col (lower) / row (upper) of panel tile i's "other" index
+        return A.grid.pcol(i + A.jt0) if lower else A.grid.prow(i + A.it0)
+
+    # Distributed panel buffers, one flat tensor GX; per (block parity, panel in block) a slab of
+    #   G [nlines][maxcnt][nbe]: every line's panel tiles (my line arrives by the row broadcast)
+    #   X [nlines][maxsub][nbe]: of every line, only the tiles my process column/row needs as the
+    #                            second GEMM operand (cross_of(i) == my_cross), all-gathered
+    # so each rank receives (nt-k)/P + (nt-k)(P-1)/(PQ) tiles per panel instead of (nt-k).
     if distributed:
-        maxcnt = 0
+        maxcnt = maxsub = 1
         for k in range(nt):
-            cnt = [0] * nlines
+            cnt, sub = [0] * nlines, [0] * nlines
             for i in range(k + 1, nt):
-                cnt[owner_of_panel_line(i)] += 1
+                ln = owner_of_panel_line(i)
+                cnt[ln] += 1
+                if cross_of(i) == my_cross:
+                    sub[ln] += 1
             maxcnt = max(maxcnt, max(cnt) if cnt else 0)
-        maxcnt = max(maxcnt, 1)
-        G = torch.zeros(2, D, nlines, maxcnt, nbe, dtype=A.dtype, device=dev)
+            maxsub = max(maxsub, max(sub) if sub else 0)
+        SG, SX = nlines * maxcnt * nbe, nlines * maxsub * nbe
+        slab = SG + SX
+        GX = torch.zeros(2 * D * slab, dtype=A.dtype, device=dev)
         dbuf = torch.zeros(nbe, dtype=A.dtype, device=dev)
-        tp._buffers = (G, dbuf)
+        tp._buffers = (GX, dbuf)
 
     tri_mask = MASK_LOWER if lower else MASK_UPPER
     tA, tB = (dplasmaNoTrans, dplasmaConjTrans) if lower else (dplasmaConjTrans, dplasmaNoTrans)
@@ -203,40 +216,60 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
             # ---------------- panel distribution
             if distributed:
                 slot = k - c0
+                o = (par * D + slot) * slab
                 lines_cnt = [0] * nlines
-                idx_in_line = {}
+                sub_cnt = [0] * nlines
+                idx_in_line, idx_in_sub = {}, {}
                 for i in range(k + 1, nt):
                     ln = owner_of_panel_line(i)
                     idx_in_line[i] = lines_cnt[ln]
                     lines_cnt[ln] += 1
+                    if cross_of(i) == my_cross:
+                        idx_in_sub[i] = sub_cnt[ln]
+                        sub_cnt[ln] += 1
                 my_cnt = lines_cnt[my_line]
-                Gk = G[par, slot]
+                Gk = GX[o: o + SG].view(nlines, maxcnt, nbe)
+                Xk = GX[o + SG: o + slab].view(nlines, maxsub, nbe)
                 pack = None
                 if in_panel_cross and mine:
                     pb = TileBatch()
                     for j, i in enumerate(mine):
                         cc = tcoord(i, k)
                         pb.add(A.offset(*cc), A.tile_rows(cc[0]), A.tile_cols(cc[1]),
-                               b_off=(((par * D + slot) * nlines + my_line) * maxcnt + j) * nbe)
+                               b_off=o + (my_line * maxcnt + j) * nbe)
                     pack = pb.finalize()
+                # my line's tiles wanted by my line_group mates -> X[my_line] (device copy)
+                subpack = None
+                if line_group is not None and sub_cnt[my_line]:
+                    sb = TileBatch()
+                    for i, t in idx_in_sub.items():
+                        if owner_of_panel_line(i) == my_line:
+                            sb.add(o + (my_line * maxcnt + idx_in_line[i]) * nbe, A.mb, A.nb,
+                                   b_off=o + SG + (my_line * maxsub + t) * nbe)
+                    subpack = sb.finalize()
                 root = A.grid.rank(*((my_line, panel_owner_cross(k)) if lower else (panel_owner_cross(k), my_line)))
 
-                def f_comm(pack=pack, Gk=Gk, my_cnt=my_cnt, root=root):
+                def f_comm(pack=pack, subpack=subpack, Gk=Gk, Xk=Xk, my_cnt=my_cnt, root=root):
                     if pack is not None:
-                        # local slab -> G[par][slot][my_line] (ld = mb)
-                        ops.geadd(0, dplasmaNoTrans, 1.0, A.data, A.ld, 0.0, G, A.mb, pack, copy=True)
+                        # local slab -> G[my_line] (ld = mb)
+                        ops.geadd(0, dplasmaNoTrans, 1.0, A.data, A.ld, 0.0, GX, A.mb, pack, copy=True)
                     if my_cnt > 0 and cross_group is not None:
                         comm.bcast(Gk[my_line, :my_cnt], root, cross_group)
                     if line_group is not None:
-                        comm.allgather_inplace(Gk, my_line, line_group)
-                # G[par] is reused by block b+2: its previous readers (NEXT/REST of block b-2) must be done
+                        if subpack is not None:
+                            ops.geadd(0, dplasmaNoTrans, 1.0, GX, A.mb, 0.0, GX, A.mb, subpack, copy=True)
+                        comm.allgather_inplace(Xk, my_line, line_group)
+                # GX slab (par) is reused by block b+2: its previous readers (NEXT/REST of b-2) must be done
                 t_panel = tp.task(f"PANEL_COMM({k})", "panel", f_comm,
                                   [t_trsm, gate, last_panel, last_upd.get(b - 2)], prio=2)
                 last_panel = t_panel
 
-                def poff(i, par=par, slot=slot, idx_in_line=idx_in_line):
-                    return ((((par * D + slot) * nlines + owner_of_panel_line(i)) * maxcnt + idx_in_line[i]) * nbe)
-                panels[k] = _Panel(G, A.mb, poff)
+                def poff(i, o=o, idx_in_line=idx_in_line, idx_in_sub=idx_in_sub):
+                    ln = owner_of_panel_line(i)
+                    if ln == my_line:
+                        return o + (ln * maxcnt + idx_in_line[i]) * nbe
+                    return o + SG + (ln * maxsub + idx_in_sub[i]) * nbe
+                panels[k] = _Panel(GX, A.mb, poff)
             else:
                 t_panel = t_trsm if t_trsm is not None else t_potrf
                 panels[k] = _Panel(A.data, A.ld, lambda i, k=k: A.offset(*tcoord(i, k)))
