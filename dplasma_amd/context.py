@@ -96,14 +96,25 @@ class Context:
     def _build_groups(self):
         if not self.distributed or self.world == 1:
             return
-        # every rank must create every group, in the same order
+        # every rank must create every group, in the same order.  On RCCL the panel traffic
+        # (broadcasts / all-gathers of the factorisations' critical path) runs on high-priority
+        # streams so its kernels are dispatched ahead of the bulk trailing-update GEMM workgroups.
+        kw = {}
+        if dist.get_backend() == "nccl":
+            try:
+                from torch.distributed import ProcessGroupNCCL
+                opts = ProcessGroupNCCL.Options()
+                opts.is_high_priority_stream = True
+                kw["pg_options"] = opts
+            except Exception:  # pragma: no cover - older torch
+                kw = {}
         rows, cols = [], []
         for r in range(self.P):
             ranks = [r * self.Q + c for c in range(self.Q)]
-            rows.append(dist.new_group(ranks) if self.Q > 1 else None)
+            rows.append(dist.new_group(ranks, **kw) if self.Q > 1 else None)
         for c in range(self.Q):
             ranks = [r * self.Q + c for r in range(self.P)]
-            cols.append(dist.new_group(ranks) if self.P > 1 else None)
+            cols.append(dist.new_group(ranks, **kw) if self.P > 1 else None)
         self.row_group = rows[self.myrow]
         self.col_group = cols[self.mycol]
         self._groups_built = True
