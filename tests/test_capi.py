@@ -40,3 +40,15 @@ def test_capi_cpu(tmp_path):
 def test_capi_gpu(tmp_path):
     out = _run(_build(tmp_path), 1, 1000, 256)
     assert "dpotrf N=1000" in out
+
+
+def test_capi_info(tmp_path):
+    """dplasma_info_t (native, no interpreter): the checks of the reference's testing_info.c."""
+    if not os.path.exists(os.path.join(LIB, "libdplasma.so")):
+        _build(tmp_path)
+    exe = str(tmp_path / "test_info")
+    subprocess.run(["gcc", "-O1", "-o", exe, os.path.join(ROOT, "tests", "capi", "test_info.c"),
+                    "-I" + os.path.join(ROOT, "capi", "include"), "-L" + LIB, "-ldplasma",
+                    "-Wl,-rpath," + LIB], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "INFO OK" in r.stdout, r.stdout + r.stderr
