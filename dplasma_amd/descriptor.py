@@ -204,9 +204,12 @@ class TiledMatrix:
 
     def like(self, dtype=None, storage=None, alloc=True, name=None, lm=None, ln=None) -> "TiledMatrix":
         """Same distribution/tiling, new storage (full matrix, not a view)."""
+        st = storage or self.storage
+        # same LAPACK layout (leading dimension) when the storage kind and extent are kept
+        lld = self.ld if (st == STORAGE_LAPACK and self.storage == STORAGE_LAPACK and lm is None) else None
         return TiledMatrix(dtype or self.dtype, self.mb, self.nb, lm or self.m, ln or self.n, P=self.grid.P,
                            Q=self.grid.Q, kp=self.grid.kp, kq=self.grid.kq, ip=self.grid.ip, jq=self.grid.jq,
-                           rank=self.rank, device=self.device, storage=storage or self.storage,
+                           rank=self.rank, device=self.device, storage=st, lld=lld,
                            uplo=self.uplo, alloc=alloc, name=name or self.name)
 
     # ------------------------------------------------------------ host helpers (tests / checks)

@@ -54,6 +54,20 @@ def _parse(argv):
     ap.add_argument("--dot", default=None, help="write the DAG of DAG-based ops to this DOT file")
     ap.add_argument("--criteria", type=int, default=0, help="LU-QR criterion (include/dplasma/lu_qr.h)")
     ap.add_argument("--trace", default=None, help="write a Chrome trace (all ranks) of the timed runs to this file")
+    # remaining flags of tests/common.c:171-259
+    ap.add_argument("-s", "--kp", "--SMB", type=int, default=1, dest="kp", help="k-cyclic repetition over rows")
+    ap.add_argument("-S", "--kq", "--SNB", type=int, default=1, dest="kq", help="k-cyclic repetition over cols")
+    ap.add_argument("-A", "--LDA", type=int, default=0, dest="LDA", help="LAPACK storage with this local lld")
+    ap.add_argument("-B", "--LDB", type=int, default=0, dest="LDB")
+    ap.add_argument("-C", "--LDC", type=int, default=0, dest="LDC")
+    ap.add_argument("-b", "--sync", action="store_true", help="synchronise (barrier) around every phase")
+    ap.add_argument("-y", "--butlvl", type=int, default=0, help="butterfly level (hebut/gebut)")
+    ap.add_argument("-z", "--HNB", "--HMB", type=int, default=0, dest="HNB",
+                    help="recursive sub-tile size hint (dplasma_z*_setrecursive)")
+    ap.add_argument("-c", "--cores", type=int, default=0, help="host worker threads (CPU path)")
+    ap.add_argument("-m", "--thread_multi", action="store_true", help="accepted for compatibility")
+    ap.add_argument("-o", "--scheduler", default="", help="accepted for compatibility (LFQ/LTQ/AP/LHQ/GD/PBQ/IP/RND): "
+                    "the stream-program executor has one schedule -- critical path on the high-priority stream")
     return ap.parse_args(argv)
 
 
@@ -74,7 +88,11 @@ class Harness:
         import dplasma_amd as dp
         self.dp = dp
         P = a.P or None
-        self.ctx = dp.init(P=P, device=None if use_gpu else "cpu")
+        if a.cores > 0:
+            torch.set_num_threads(a.cores)
+        self.ctx = dp.init(P=P, device=None if use_gpu else "cpu", nb_cores=a.cores or None)
+        if a.scheduler and a.verbose:
+            print(f"#+++++ scheduler {a.scheduler}: stream-program executor (fixed priority streams)", flush=True)
         self.prec = a.op[0]
         if self.prec not in PRECS:
             raise SystemExit(f"operation must start with a precision letter s/d/c/z: {a.op}")
@@ -91,7 +109,11 @@ class Harness:
         a = self.a
         mb = mb or a.MB or a.NB or 180
         nb = nb or a.NB or mb
-        return self.dp.block_cyclic(self.ctx, self.dt, mb, nb, m, n, name=name)
+        lld = {"A": a.LDA, "B": a.LDB, "C": a.LDC}.get(name, 0)
+        kw = {"kp": a.kp, "kq": a.kq}
+        if lld:
+            kw.update(storage=self.dp.STORAGE_LAPACK, lld=lld)
+        return self.dp.block_cyclic(self.ctx, self.dt, mb, nb, m, n, name=name, **kw)
 
     def report(self, opname, t, flops, t_enq=0.0, t_dest=0.0):
         ctx = self.ctx

@@ -26,6 +26,8 @@ def _run(args, nproc=1):
     "dpotrf -N 378 -t 93 -x", "zposv -N 150 -t 40 -K 3 -x", "sgemm -M 106 -N 283 -K 97 -t 56 -x",
     "dgeqrf -M 487 -N 283 -t 56 -i 8 -x", "dgeqrf_hqr -M 300 -N 200 -t 50 -i 10 --qr_a 2 -x",
     "dgetrf_incpiv -N 200 -t 50 -i 10 -x", "dgetrf_ptgpanel -N 200 -t 50 -x", "dlange -M 87 -N 83 -t 16 -x",
+    # the remaining common.c flags: LAPACK storage (-A lld), cores, scheduler name, recursive hint, sync
+    "dpotrf -N 300 -t 64 -A 320 -c 2 -o LFQ -z 32 -b -x", "dgemm -M 90 -N 70 -K 50 -t 16 -A 100 -B 60 -C 100 -x",
 ])
 def test_cli_single(args):
     r = _run(args.split())
@@ -37,3 +39,10 @@ def test_cli_multirank():
     r = _run("dgetrf_ptgpanel -N 200 -t 32 -P 2 -x".split(), nproc=4)
     assert r.returncode == 0, r.stdout + r.stderr[-2000:]
     assert "PxQxg=   2 2" in r.stdout and "CORRECT" in r.stdout
+
+
+def test_cli_kcyclic_multirank():
+    """k-cyclic distribution (-s/-S: KP x KQ repetition) on a 2 x 2 grid."""
+    r = _run("dpotrf -N 256 -t 32 -P 2 -s 2 -S 2 -x".split(), nproc=4)
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    assert "CORRECT" in r.stdout and "SUSPICIOUS" not in r.stdout
