@@ -28,7 +28,7 @@ from ..ops.batch import TileBatch
 from ..runtime.dag import TileDAG
 from ..runtime.taskpool import Taskpool
 from ..utils.flops import flops
-from . import aux, blas3, qrtree
+from . import aux, blas3, qr_panel, qrtree
 from .cholesky import _Seq
 
 
@@ -158,6 +158,9 @@ def geqrf_New(ctx, A, T) -> Taskpool:
     """Tile QR factorization A = Q R (dplasma_zgeqrf_New, src/zgeqrf_wrapper.c:130)."""
     _check_square_tiles(A)
     _check_T(A, T)
+    flat = qrtree.FlatTree(A.mt, A.nt)
+    if qr_panel.usable(A, flat):
+        return qr_panel.factor_New(ctx, A, T, T, flat, "geqrf")
     dag = TileDAG(ctx, "geqrf")
     _factor(dag, _L(A), _L(T), _L(T), _kinds(A, T, False), qrtree.FlatTree(A.mt, A.nt))
     dag.flops = flops(A.prec, "geqrf", A.m, A.n)
@@ -211,6 +214,8 @@ def _unm(ctx, name, side, trans, A, T, C, lq: bool, tree=None, TT=None):
     c_t = side == dplasmaRight
     if c_t:
         qh = not qh  # C op(Q) = (op(Q)^H C^H)^H
+    if not lq and qr_panel.usable(A, tree or _flat(A, lq)):
+        return qr_panel.apply_New(ctx, side, trans, A, T, TT if TT is not None else T, C, tree or _flat(A, lq), name)
     X = _L(A, lq)
     dag = TileDAG(ctx, name)
     K = min(A.mt, A.nt)
@@ -244,6 +249,11 @@ def unmlq(ctx, side, trans, A, T, C):
 def _ung(ctx, name, A, T, Q, lq: bool, tree=None, TT=None):
     _check_square_tiles(A)
     init = aux.laset_New(ctx, dplasmaUpperLower, 0.0, 1.0, Q)
+    if not lq and qr_panel.usable(A, tree or _flat(A, lq)):
+        app = qr_panel.apply_New(ctx, dplasmaLeft, dplasmaNoTrans, A, T, TT if TT is not None else T, Q,
+                                 tree or _flat(A, lq), name)
+        app.flops = flops(A.prec, "ungqr", Q.m, Q.n, min(A.m, A.n))
+        return _Seq(name, ctx, [init, app])
     dag = TileDAG(ctx, name)
     K = min(A.mt, A.nt)
     _apply(dag, _L(A, lq), _L(T, lq), _L(TT if TT is not None else T, lq), _L(Q, lq), _kinds(A, T, lq, lq), False,
@@ -354,6 +364,8 @@ def geqrf_param_New(ctx, tree, A, TS, TT) -> Taskpool:
     _check_T(A, TS)
     _check_T(A, TT)
     _check_tree(A, tree, False)
+    if qr_panel.usable(A, tree):
+        return qr_panel.factor_New(ctx, A, TS, TT, tree, "geqrf_param")
     dag = TileDAG(ctx, "geqrf_param")
     _factor(dag, _L(A), _L(TS), _L(TT), _kinds(A, TS, False), tree)
     dag.flops = flops(A.prec, "geqrf", A.m, A.n)

@@ -1,0 +1,434 @@
+"""Stacked-domain Householder QR: the MI355X engine of geqrf / geqrf_param on a 1 x 1 grid.
+
+Reference: ``src/zgeqrf.jdf`` (flat TS tree: zgeqrt(k) :98, zunmqr(k,n) :198, ztsqrt(k,m) :314,
+ztsmqr(k,m,n) :443), ``src/zgeqrf_param.jdf`` (trees: TS domains + TT kills), ``src/zunmqr_*.jdf``,
+``src/zungqr*.jdf``.
+
+Why a different kernel decomposition than the tile DAG of models/qr.py: a TS chain (GEQRT on
+the head, then TSQRT of every row of the domain, one after the other) is a sequence of
+single-workgroup, column-at-a-time kernels -- latency bound on a 256-CU part (measured: 2.6 ms
+per 256-column TSQRT launch, 54-60 % of a 16k factorisation, profiles/README.md).  Here a TS
+domain is factored as ONE stacked tall panel by a persistent kernel that spreads the rows over
+every CU (ops.qr_panel -> csrc/kernels/qr_panel.hip), and its trailing update is three batched
+MFMA GEMM launches of the whole remaining matrix:
+
+    W = V^T C   (split over the domain rows, partials summed)     W' = T^T W     C -= V W'
+
+Storage format (what unmqr / ungqr / geqrs / gels of this package consume; real precisions):
+  * every TS domain D = [h, m1, m2, ...] of panel k (the head and the rows it TS-kills, in kill
+    order) -- for the flat tree the whole panel -- holds the Householder QR of the stacked rows
+    [A(h,k); A(m1,k); ...]: R in the upper triangle of A(h,k), V below the diagonal of A(h,k)
+    and in the full tiles A(m_i,k) (LAPACK dgeqrf layout for the domain); TS(h,k) holds the
+    IB x IB diagonal blocks of the domain's compact-WY T (LAPACK dgeqrt's T layout);
+  * every TT kill (p, m) of the tree is the Householder QR of the stacked R factors [R_p; R_m]:
+    R into A(p,k)'s upper triangle, V2 (upper triangular) into A(m,k)'s upper triangle, T blocks
+    in TT(m,k) -- the same places the reference's TTQRT uses;
+  * per panel, all domains come first, then the TT kills in plan order.
+The full T of a reflector set is rebuilt from V and its diagonal blocks when Q is applied.
+
+Lookahead (single-domain trees, e.g. the flat tree or HQR with one domain per process row):
+the panel stream factors panel k+1 right after applying Q_k^T to column k+1, while the update
+stream applies Q_k^T to columns k+2.. (the reference's priority-driven lookahead, done with
+two HIP streams of different priority).
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+
+import numpy as np
+import torch
+
+from ..constants import dplasmaConjTrans, dplasmaLeft, dplasmaNoTrans, dplasmaTrans
+from ..ops import tile_ops as ops
+from ..ops.batch import GemmBatch, TileBatch
+from ..runtime.taskpool import Taskpool
+from ..utils.flops import flops
+from . import qrtree
+
+N_, T_ = dplasmaNoTrans, dplasmaTrans
+PART_FULL, PART_UPPER, PART_SLOWER, PART_DIAG = 0, 2, 3, 5
+
+_ENGINE = [os.environ.get("DPLASMA_QR_ENGINE", "panel")]
+
+
+@contextlib.contextmanager
+def engine(name: str):
+    """Temporarily select the QR engine ("panel" or "tile") -- tests use it to run the tile
+    algorithm on one process as the reference of a distributed run."""
+    old = _ENGINE[0]
+    _ENGINE[0] = name
+    try:
+        yield
+    finally:
+        _ENGINE[0] = old
+
+
+def _rup(x, m):
+    return (x + m - 1) // m * m
+
+
+# ----------------------------------------------------------------------------- plans
+def step_plan(tree, k):
+    """(domains, tt_kills) of panel k: domains = [[head, ts victims...], ...], tt = [(p, m), ...];
+    None when a TS kill's pivot is not a head (not expressible as stacked domains)."""
+    heads = list(tree.heads(k))
+    doms = {h: [h] for h in heads}
+    tts = []
+    for (p, m, t) in tree.kills(k):
+        if t == qrtree.KILLED_BY_TS:
+            if p not in doms:
+                return None
+            doms[p].append(m)
+        else:
+            tts.append((p, m))
+    return [doms[h] for h in heads], tts
+
+
+def usable(A, tree=None) -> bool:
+    """The stacked-domain engine handles this factorisation (and therefore owns its format)."""
+    if _ENGINE[0] != "panel":
+        return False
+    if A.dtype not in (torch.float32, torch.float64):
+        return False
+    if A.grid.P != 1 or A.grid.Q != 1 or A.mb != A.nb or A.nb > ops.QR_PANEL_MAXW:
+        return False
+    if A.device.type == "cuda" and A.m > ops.qr_panel_max_rows(A.device):
+        return False
+    if tree is not None:
+        if any(step_plan(tree, k) is None for k in range(min(A.mt, A.nt))):
+            return False
+    return True
+
+
+def _sequence(A, tree):
+    """Factorisation order: [("dom", k, rows) | ("tt", k, p, m)] over all panels."""
+    seq = []
+    for k in range(min(A.mt, A.nt)):
+        doms, tts = step_plan(tree, k)
+        seq += [("dom", k, d) for d in doms]
+        seq += [("tt", k, p, m) for (p, m) in tts]
+    return seq
+
+
+# ----------------------------------------------------------------------------- batched updates
+class _Left:
+    """C(rows, cols) := op(Q)^T-style block reflector application from the left:
+    W = V^T C (split over S row groups, partials summed), W' = op(T) W, C -= V W'."""
+
+    def __init__(self, C, rows, voff, kf, cols, target_wg=512):
+        self.kf = kf
+        woff, c = {}, 0
+        for n in cols:
+            woff[n] = c * kf
+            c += C.tile_cols(n)
+        self.wlen = c * kf
+        nrow = len(rows)
+        wg = max(1, len(cols) * max(1, kf // 128) * max(1, C.nb // 128))
+        self.S = S = max(1, min(nrow, -(-target_wg // wg)))
+        g1, g2, g3 = GemmBatch(), GemmBatch(), GemmBatch()
+        for s, grp in enumerate(np.array_split(np.arange(nrow), S)):
+            for n in cols:
+                g1.add(s * self.wlen + woff[n], kf, C.tile_cols(n),
+                       [(voff[i], C.offset(rows[i], n), C.tile_rows(rows[i])) for i in grp])
+        for n in cols:
+            g2.add(woff[n], kf, C.tile_cols(n), [(0, woff[n], kf)])
+            for i, r in enumerate(rows):
+                g3.add(C.offset(r, n), C.tile_rows(r), C.tile_cols(n), [(voff[i], woff[n], kf)])
+        self.g1, self.g2, self.g3 = g1.finalize(), g2.finalize(), g3.finalize()
+        self.empty = not cols or not rows
+
+    def run(self, C, V, ldv, Tm, ldt, Wp, W, W2, qt: bool):
+        if self.empty:
+            return
+        kf, L = self.kf, self.wlen
+        ops.gemm(T_, N_, 1.0, V, ldv, C.data, C.ld, 0.0, Wp, kf, self.g1)
+        if self.S > 1:
+            torch.sum(Wp[: self.S * L].view(self.S, L), 0, out=W[:L])
+            src = W
+        else:
+            src = Wp
+        ops.gemm(T_ if qt else N_, N_, 1.0, Tm, ldt, src, kf, 0.0, W2, kf, self.g2)
+        ops.gemm(N_, N_, -1.0, V, ldv, W2, kf, 1.0, C.data, C.ld, self.g3)
+
+
+class _Right:
+    """C(rows, cols) := C op(Q) (cols = the reflector rows): W = C V, W' = W op(T), C -= W' V^T."""
+
+    def __init__(self, C, crows, vcols, voff, kf, target_wg=512):
+        self.kf = kf
+        roff, c = {}, 0
+        for i in crows:
+            roff[i] = c
+            c += C.tile_rows(i)
+        self.ldw = max(1, _rup(c, 16))
+        self.wlen = self.ldw * kf
+        ncol = len(vcols)
+        wg = max(1, len(crows) * max(1, kf // 128) * max(1, C.mb // 128))
+        self.S = S = max(1, min(ncol, -(-target_wg // wg)))
+        g1, g2, g3 = GemmBatch(), GemmBatch(), GemmBatch()
+        for s, grp in enumerate(np.array_split(np.arange(ncol), S)):
+            for i in crows:
+                g1.add(s * self.wlen + roff[i], C.tile_rows(i), kf,
+                       [(C.offset(i, vcols[j]), voff[j], C.tile_cols(vcols[j])) for j in grp])
+        for i in crows:
+            g2.add(roff[i], C.tile_rows(i), kf, [(roff[i], 0, kf)])
+            for j, n in enumerate(vcols):
+                g3.add(C.offset(i, n), C.tile_rows(i), C.tile_cols(n), [(roff[i], voff[j], kf)])
+        self.g1, self.g2, self.g3 = g1.finalize(), g2.finalize(), g3.finalize()
+        self.empty = not crows or not vcols
+
+    def run(self, C, V, ldv, Tm, ldt, Wp, W, W2, qt: bool):
+        if self.empty:
+            return
+        kf, L, ldw = self.kf, self.wlen, self.ldw
+        ops.gemm(N_, N_, 1.0, C.data, C.ld, V, ldv, 0.0, Wp, ldw, self.g1)
+        if self.S > 1:
+            torch.sum(Wp[: self.S * L].view(self.S, L), 0, out=W[:L])
+            src = W
+        else:
+            src = Wp
+        ops.gemm(N_, T_ if qt else N_, 1.0, src, ldw, Tm, ldt, 0.0, W2, ldw, self.g2)
+        ops.gemm(N_, T_, -1.0, W2, ldw, V, ldv, 1.0, C.data, C.ld, self.g3)
+
+
+def _work_buffers(updates, dtype, device):
+    """Wp (split partials), W (their sum), W2 sized for a list of _Left/_Right plans."""
+    n1 = max([u.S * u.wlen for u in updates] + [1])
+    n2 = max([u.wlen for u in updates] + [1])
+    z = lambda n: torch.zeros(n, dtype=dtype, device=device)  # noqa: E731
+    return z(n1), z(n2), z(n2)
+
+
+# ----------------------------------------------------------------------------- T storage
+def _store_T(Tm, ldt, kf, Td, row, k):
+    """Diagonal IB x IB blocks of the kf x kf T into tile Td(row, k) (dgeqrt layout)."""
+    ib = Td.mb
+    base, ld = Td.offset(row, k), Td.ld
+    nfull = kf // ib
+    if nfull:
+        src = torch.as_strided(Tm, (nfull, ib, ib), (ib * ldt + ib, 1, ldt), 0)
+        dst = torch.as_strided(Td.data, (nfull, ib, ib), (ib * ld, 1, ld), base)
+        dst.copy_(src)
+    r = kf - nfull * ib
+    if r:
+        c0 = nfull * ib
+        src = torch.as_strided(Tm, (r, r), (1, ldt), c0 * ldt + c0)
+        torch.as_strided(Td.data, (r, r), (1, ld), base + c0 * ld).copy_(src)
+
+
+def _rebuild_T(V, ldv, M, kf, Td, row, k, out, ldt):
+    """Full compact-WY T from the stored diagonal blocks and V (coupling -T11 V1^T V2 T22)."""
+    ib = Td.mb
+    Tf = torch.zeros(kf, kf, dtype=V.dtype, device=V.device)
+    for b0 in range(0, kf, ib):
+        bs = min(ib, kf - b0)
+        Tf[b0:b0 + bs, b0:b0 + bs] = torch.triu(Td.tile(row, k)[:bs, b0:b0 + bs])
+    if kf > ib:
+        Vv = torch.as_strided(V, (M, kf), (1, ldv), 0)
+        Gm = Vv.T @ Vv
+        for b0 in range(ib, kf, ib):
+            bs = min(ib, kf - b0)
+            Tf[:b0, b0:b0 + bs] = -(Tf[:b0, :b0] @ Gm[:b0, b0:b0 + bs]) @ Tf[b0:b0 + bs, b0:b0 + bs]
+    torch.as_strided(out, (kf, kf), (1, ldt), 0).copy_(Tf)
+
+
+# ----------------------------------------------------------------------------- factorisation
+class _Factor:
+    def __init__(self, ctx, A, TS, TT, tree):
+        self.ctx, self.A, self.TS, self.TT = ctx, A, TS, TT
+        dev, dt = A.device, A.dtype
+        nb = A.nb
+        self.kt = min(A.mt, A.nt)
+        self.plans = [step_plan(tree, k) for k in range(self.kt)]
+        self.simple = all(len(d) == 1 and not t for d, t in self.plans)
+        self.ldp = max(16, _rup(A.m, 16))
+        nbuf = 2 if self.simple else 1
+        self.P = [torch.zeros(self.ldp * nb, dtype=dt, device=dev) for _ in range(nbuf)]
+        self.V = [torch.zeros(self.ldp * nb, dtype=dt, device=dev) for _ in range(nbuf)]
+        self.Tm = [torch.zeros(nb * nb, dtype=dt, device=dev) for _ in range(nbuf)]
+        self.ws = ops.qr_panel_workspace(nb, nb, dt, dev)
+        self.info = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.steps = [self._build(k) for k in range(self.kt)]
+        ups = [u for st in self.steps for e in st for u in (e.get("next"), e.get("rest"), e.get("upd")) if u]
+        if self.simple:
+            self.wn = _work_buffers([e["next"] for st in self.steps for e in st if e.get("next")], dt, dev)
+            self.wr = _work_buffers([e["rest"] for st in self.steps for e in st if e.get("rest")], dt, dev)
+        else:
+            self.wr = _work_buffers(ups, dt, dev)
+
+    def _entry(self, k, rows, tt):
+        A = self.A
+        kb = A.tile_cols(k)
+        voff, c = [], 0
+        for r in rows:
+            voff.append(c)
+            c += A.tile_rows(r)
+        M = c
+        e = {"rows": rows, "voff": voff, "M": M, "kb": kb, "kf": min(M, kb), "tt": tt, "ld": max(16, _rup(M, 16))}
+        g, back = TileBatch(), TileBatch()
+        part = PART_UPPER if tt else PART_FULL
+        for r, o in zip(rows, voff):
+            g.add(A.offset(r, k), A.tile_rows(r), kb, b_off=o)
+            back.add(o, A.tile_rows(r), kb, b_off=A.offset(r, k))
+        e["gather"], e["back"], e["part"] = g.finalize(), back.finalize(), part
+        return e
+
+    def _build(self, k):
+        A = self.A
+        doms, tts = self.plans[k]
+        out = []
+        cols = list(range(k + 1, A.nt))
+        for d in doms:
+            e = self._entry(k, d, False)
+            if self.simple:
+                e["next"] = _Left(A, d, e["voff"], e["kf"], cols[:1]) if cols else None
+                e["rest"] = _Left(A, d, e["voff"], e["kf"], cols[1:]) if len(cols) > 1 else None
+            else:
+                e["upd"] = _Left(A, d, e["voff"], e["kf"], cols) if cols else None
+            out.append(e)
+        for (p, m) in tts:
+            e = self._entry(k, [p, m], True)
+            e["upd"] = _Left(A, [p, m], e["voff"], e["kf"], cols) if cols else None
+            out.append(e)
+        return out
+
+    def panel(self, k, e, buf):
+        """Assemble, factor, write back, store T of one domain / TT stack."""
+        A = self.A
+        P, V, Tm = self.P[buf], self.V[buf], self.Tm[buf]
+        ld, M, kb, kf = e["ld"], e["M"], e["kb"], e["kf"]
+        if e["tt"]:
+            P[: ld * kb].zero_()
+        ops.geadd(e["part"], N_, 1.0, A.data, A.ld, 0.0, P, ld, e["gather"], copy=True)
+        ops.qr_panel(P, ld, M, kb, kf, V, ld, Tm, A.nb, self.ws, self.info)
+        ops.geadd(e["part"], N_, 1.0, P, ld, 0.0, A.data, A.ld, e["back"], copy=True)
+        if e["tt"]:
+            _store_T(Tm, A.nb, kf, self.TT, e["rows"][1], k)
+        else:
+            _store_T(Tm, A.nb, kf, self.TS, e["rows"][0], k)
+
+    def apply(self, e, upd, buf, work):
+        if upd is None:
+            return
+        upd.run(self.A, self.V[buf], e["ld"], self.Tm[buf], self.A.nb, *work, qt=True)
+
+    def step_general(self, k):
+        for e in self.steps[k]:
+            self.panel(k, e, 0)
+            self.apply(e, e.get("upd"), 0, self.wr)
+
+
+def factor_New(ctx, A, TS, TT, tree, name="geqrf") -> Taskpool:
+    """Build the taskpool of the stacked-domain QR (see module docstring)."""
+    tp = Taskpool(name, ctx)
+    tp.flops = flops(A.prec, "geqrf", A.m, A.n)
+    st = _Factor(ctx, A, TS, TT, tree)
+    if st.simple:
+        prev_next = prev_rest = prev_rest2 = None
+        for k in range(st.kt):
+            e = st.steps[k][0]
+            buf = k % 2
+            pan = tp.task(f"qr_panel({k})", "panel", (lambda k=k, e=e, b=buf: st.panel(k, e, b)),
+                          [prev_next, prev_rest2])
+            nxt = None
+            if e.get("next"):
+                nxt = tp.task(f"qr_next({k})", "panel", (lambda e=e, b=buf: st.apply(e, e["next"], b, st.wn)),
+                              [pan, prev_rest])
+            rst = None
+            if e.get("rest"):
+                rst = tp.task(f"qr_rest({k})", "update", (lambda e=e, b=buf: st.apply(e, e["rest"], b, st.wr)),
+                              [pan, prev_rest])
+            prev_next, prev_rest2, prev_rest = nxt or pan, prev_rest, rst or prev_rest
+    else:
+        prev = None
+        for k in range(st.kt):
+            prev = tp.task(f"qr_step({k})", "update", (lambda k=k: st.step_general(k)), [prev])
+    tp._state = st
+
+    def _done():
+        v = int(st.info.item())
+        if v != 0:
+            raise RuntimeError(f"QR panel kernel reported {v} (grid barrier timeout: is the device shared?)")
+        return 0
+    tp.on_complete(_done)
+    return tp.finish_build()
+
+
+# ----------------------------------------------------------------------------- applications
+class _Apply:
+    """C := op(Q) C or C op(Q) with Q in the stacked-domain format (unmqr / ungqr)."""
+
+    def __init__(self, ctx, side, trans, A, TS, TT, C, tree):
+        self.A, self.TS, self.TT, self.C = A, TS, TT, C
+        dev, dt = A.device, A.dtype
+        self.left = side == dplasmaLeft
+        self.qt = trans in (dplasmaTrans, dplasmaConjTrans)
+        asc = (self.left and self.qt) or (not self.left and not self.qt)
+        seq = _sequence(A, tree)
+        self.seq = seq if asc else seq[::-1]
+        self.ldv = max(16, _rup(A.m, 16))
+        self.V = torch.zeros(self.ldv * A.nb, dtype=dt, device=dev)
+        self.Tm = torch.zeros(A.nb * A.nb, dtype=dt, device=dev)
+        self.items = [self._build(s) for s in self.seq]
+        self.work = _work_buffers([it["upd"] for it in self.items if it["upd"]], dt, dev)
+
+    def _build(self, s):
+        A, C = self.A, self.C
+        k = s[1]
+        tt = s[0] == "tt"
+        rows = [s[2], s[3]] if tt else s[2]
+        kb = A.tile_cols(k)
+        voff, c = [], 0
+        for r in rows:
+            voff.append(c)
+            c += A.tile_rows(r)
+        M, kf = c, min(c, kb)
+        it = {"k": k, "tt": tt, "rows": rows, "M": M, "kf": kf}
+        # V gather batches: copy part (dom head: strictly lower / victims: full; TT: upper of m) + unit diagonal
+        cp, dg = TileBatch(), TileBatch()
+        if tt:
+            dg.add(0, A.tile_rows(rows[0]), kf)
+            cp.add(A.offset(rows[1], k), A.tile_rows(rows[1]), kf, b_off=voff[1])
+            it["cp"] = [(PART_UPPER, cp.finalize())]
+        else:
+            dg.add(0, A.tile_rows(rows[0]), kf)
+            head, rest = TileBatch(), TileBatch()
+            head.add(A.offset(rows[0], k), A.tile_rows(rows[0]), kf, b_off=0)
+            for r, o in zip(rows[1:], voff[1:]):
+                rest.add(A.offset(r, k), A.tile_rows(r), kf, b_off=o)
+            it["cp"] = [(PART_SLOWER, head.finalize()), (PART_FULL, rest.finalize())]
+        it["diag"] = dg.finalize()
+        if self.left:
+            cols = list(range(C.nt))
+            it["upd"] = _Left(C, rows, voff, kf, cols)
+        else:
+            it["upd"] = _Right(C, list(range(C.mt)), rows, voff, kf)
+        return it
+
+    def run_item(self, it):
+        A = self.A
+        V, ld, kf = self.V, self.ldv, it["kf"]
+        V[: ld * kf].zero_()
+        for part, b in it["cp"]:
+            if len(b):
+                ops.geadd(part, N_, 1.0, A.data, A.ld, 0.0, V, ld, b, copy=True)
+        ops.laset(PART_DIAG, 0.0, 1.0, V, ld, it["diag"])
+        Td, row = (self.TT, it["rows"][1]) if it["tt"] else (self.TS, it["rows"][0])
+        _rebuild_T(V, ld, it["M"], kf, Td, row, it["k"], self.Tm, A.nb)
+        it["upd"].run(self.C, V, ld, self.Tm, A.nb, *self.work, qt=self.qt)
+
+    def run(self):
+        for it in self.items:
+            self.run_item(it)
+
+
+def apply_New(ctx, side, trans, A, TS, TT, C, tree, name="unmqr") -> Taskpool:
+    if C.dtype != A.dtype or (side == dplasmaLeft and C.mb != A.mb) or (side != dplasmaLeft and C.nb != A.mb):
+        raise ValueError("C must share A's precision and tiling along the reflector dimension")
+    tp = Taskpool(name, ctx)
+    tp.flops = flops(A.prec, "unmqr", C.m, C.n, min(A.m, A.n), side == dplasmaLeft)
+    st = _Apply(ctx, side, trans, A, TS, TT, C, tree)
+    tp.task(name, "update", st.run, [])
+    tp._state = st
+    return tp.finish_build()

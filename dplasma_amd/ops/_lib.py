@@ -68,6 +68,10 @@ _SIGS = {
     # prec, A, ld, ca, cb, ipiv, i0, i1, stream
     "dpl_laswp_panel": [c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp],
     "dpl_lu_block_ws_bytes": [c_int],
+    # Householder panel (qr_panel.hip): prec, P, ldp, M, nc, kf, V, ldv, Tm, ldt, ws, info, stream
+    "dpl_qr_panel": [c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp],
+    "dpl_qr_panel_ws_bytes": [c_int, c_int, c_int],
+    "dpl_qr_panel_max_rows": [],
     # ipiv, kb, dst, src, cnt, stream
     "dpl_piv_moves": [c_vp, c_int, c_vp, c_vp, c_vp, c_vp],
     # prec, gather, A, ld, mb, r0, rowoff, nrt, coloff, ncols, nct, nb, rows, cnt, maxcnt, buf, ldb, stream

@@ -534,6 +534,64 @@ def diag_scale(part: int, cols: bool, D: torch.Tensor, ldd: int, B: torch.Tensor
 
 
 # ----------------------------------------------------------------------------- device-pivoting LU
+QR_PANEL_MAXW = 256   # widest panel of the single-launch Householder panel kernel (qr_panel.hip QP_R)
+
+
+def qr_panel_max_rows(device) -> int:
+    """Tallest panel the persistent QR panel kernel factors in one launch (one workgroup per CU)."""
+    if torch.device(device).type == "cuda":
+        return int(_lib.load().dpl_qr_panel_max_rows())
+    return 1 << 62
+
+
+def qr_panel_workspace(nc: int, kf: int, dtype: torch.dtype, device) -> torch.Tensor:
+    """Scratch for qr_panel on panels of nc columns (kf reflectors): reduction partials + barrier."""
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        nbytes = int(_lib.load().dpl_qr_panel_ws_bytes(_lib.prec_code(dtype), int(nc), int(kf)))
+        return torch.zeros(nbytes // 8 + 8, dtype=torch.float64, device=dev)
+    return torch.zeros(8, dtype=torch.float64)
+
+
+def _larft_cpu(V: torch.Tensor, tau: torch.Tensor) -> torch.Tensor:
+    """Compact-WY T (upper triangular, dlarft forward/columnwise) of explicit reflectors V."""
+    k = V.shape[1]
+    T = torch.zeros(k, k, dtype=V.dtype)
+    G = V.T @ V
+    for j in range(k):
+        T[j, j] = tau[j]
+        if j:
+            T[:j, j] = -tau[j] * (T[:j, :j] @ G[:j, j])
+    return T
+
+
+def qr_panel(P: torch.Tensor, ldp: int, M: int, nc: int, kf: int, V: torch.Tensor, ldv: int, Tm: torch.Tensor,
+             ldt: int, ws: torch.Tensor, info: torch.Tensor):
+    """Householder QR of the column-major M x nc panel P (ld ldp), first kf columns (real precisions).
+
+    P := R (upper) + V (strictly lower) with the remaining nc - kf columns updated by Q^T;
+    V := the kf reflectors explicitly (unit diagonal, zeros above); Tm(0:kf, 0:kf) := the
+    compact-WY T (upper part; the strictly lower part is not written).  GPU: one persistent
+    launch (csrc/kernels/qr_panel.hip); CPU: LAPACK geqrf through torch + dlarft."""
+    if kf <= 0:
+        return
+    if _is_gpu(P):
+        rc = _lib.load().dpl_qr_panel(_lib.prec_code(P.dtype), P.data_ptr(), ldp, M, nc, kf, V.data_ptr(), ldv,
+                                      Tm.data_ptr(), ldt, ws.data_ptr(), info.data_ptr(), _lib.stream_ptr())
+        _lib.check(rc, "qr_panel")
+        return
+    A = torch.as_strided(P, (M, nc), (1, ldp), 0)
+    a, tau = torch.geqrf(A[:, :kf].clone())
+    Vx = torch.tril(a, -1) + torch.eye(M, kf, dtype=P.dtype)
+    T = _larft_cpu(Vx, tau)
+    if nc > kf:
+        A[:, kf:] -= Vx @ (T.T @ (Vx.T @ A[:, kf:]))
+    A[:, :kf] = a
+    torch.as_strided(V, (M, kf), (1, ldv), 0).copy_(Vx)
+    tv = torch.as_strided(Tm, (kf, kf), (1, ldt), 0)
+    tv.copy_(torch.where(torch.ones(kf, kf, dtype=torch.bool).triu(), T, tv))
+
+
 LU_BW = 64   # base block width of the recursive panel LU (lu_piv.hip LU_MAXBW)
 
 

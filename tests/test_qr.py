@@ -8,6 +8,7 @@ import pytest
 import torch
 
 import dplasma_amd as dp
+from dplasma_amd.models import qr_panel
 from helpers import DTYPES, rel_err, run_distributed
 
 EPS = {"s": 1e-5, "c": 1e-5, "d": 1e-13, "z": 1e-13}
@@ -175,7 +176,8 @@ def _qr_worker(rank, world, P, lq):
 @pytest.mark.parametrize("world,P,lq", [(2, 1, False), (2, 2, False), (4, 2, False), (3, 3, True), (4, 2, True)])
 def test_qr_distributed(world, P, lq):
     out = run_distributed(_qr_worker, world, P, lq)
-    r = _qr_worker(0, 1, 1, lq)  # single-process run of the same algorithm on the same data
+    with qr_panel.engine("tile"):  # single-process run of the same (tile) algorithm on the same data
+        r = _qr_worker(0, 1, 1, lq)
     for i in range(4):
         full = sum(out[k][i] for k in range(world))
         assert rel_err(full, r[i]) < 1e-12, i
@@ -359,7 +361,8 @@ def _hqr_worker(rank, world, P):
 @pytest.mark.parametrize("world,P", [(2, 2), (4, 2)])
 def test_hqr_distributed(world, P):
     out = run_distributed(_hqr_worker, world, P)
-    r = _hqr_worker(0, 1, 1)
+    with qr_panel.engine("tile"):
+        r = _hqr_worker(0, 1, 1)
     for i in range(4):
         assert rel_err(sum(out[k][i] for k in range(world)), r[i]) < 1e-12, i
 
@@ -374,3 +377,88 @@ def test_gpu_hqr(gctx, ctx, prec, lq):
     lim = 1e-4 if prec in "sc" else 1e-12
     assert res[0][0] < lim and res[0][1] < lim
     assert rel_err(_dense(res[0][2]), _dense(res[1][2])) < lim * 10
+
+
+# ----------------------------------------------------------------------------- stacked-domain engine
+def _panel_case(device, dt, M, nc, kf, ld, seed):
+    from dplasma_amd.ops import tile_ops as ops
+    g = torch.Generator().manual_seed(seed)
+    Pc = torch.randn(M, nc, generator=g, dtype=torch.float64)
+    P = torch.zeros(ld * nc, dtype=dt, device=device)
+    torch.as_strided(P, (M, nc), (1, ld), 0).copy_(Pc.to(dt))
+    V = torch.zeros(ld * kf, dtype=dt, device=device)
+    Tm = torch.zeros(kf * kf, dtype=dt, device=device)
+    ws = ops.qr_panel_workspace(nc, kf, dt, device)
+    info = torch.zeros(1, dtype=torch.int32, device=device)
+    ops.qr_panel(P, ld, M, nc, kf, V, ld, Tm, kf, ws, info)
+    out = (torch.as_strided(P, (M, nc), (1, ld), 0).cpu().double(), torch.as_strided(V, (M, kf), (1, ld), 0).cpu().double(),
+           torch.as_strided(Tm, (kf, kf), (1, kf), 0).cpu().double())
+    return Pc, out, int(info.item())
+
+
+@pytest.mark.parametrize("M,nc,kf", [(40, 16, 16), (23, 30, 23), (70, 40, 40)])
+def test_qr_panel_op_cpu(M, nc, kf):
+    """The panel op's CPU path: Q = I - V T V^T is orthogonal and Q^T P0 = [R; 0] (+ updated columns)."""
+    P0, (P, V, T), _ = _panel_case("cpu", torch.float64, M, nc, kf, M + 5, 1)
+    Q = torch.eye(M, dtype=torch.float64) - V @ T @ V.T
+    assert (Q.T @ Q - torch.eye(M, dtype=torch.float64)).abs().max() < 1e-13
+    R = torch.triu(P[:, :kf])
+    ref = Q.T @ P0
+    assert rel_err(torch.triu(ref[:, :kf]), R) < 1e-13
+    if M > kf:
+        assert ref[kf:, :kf].abs().max() < 1e-12
+    if nc > kf:
+        assert rel_err(ref[:, kf:], P[:, kf:]) < 1e-13
+
+
+@pytest.mark.parametrize("M,N,NB,IB,tree", [(96, 64, 16, 4, None), (90, 90, 16, 8, None), (100, 48, 16, 4, (1, 1, 2, 1)),
+                                            (100, 48, 16, 4, (0, 3, 3, 1)), (64, 96, 16, 4, None)])
+def test_qr_panel_engine_cpu(ctx, M, N, NB, IB, tree):
+    """geqrf / geqrf_param through the stacked-domain engine: factors, Q and its applications."""
+    dt = torch.float64
+    A = _mk(ctx, dt, M, N, NB, 5)
+    a = _dense(A)
+    TS, TT = _T(ctx, A, IB), _T(ctx, A, IB)
+    tr = dp.hqr_init(dp.dplasmaNoTrans, A, *tree) if tree else None
+    assert qr_panel.usable(A, tr or dp.models.qrtree.FlatTree(A.mt, A.nt))
+    if tr is None:
+        dp.geqrf(ctx, A, TS)
+    else:
+        dp.geqrf_param(ctx, tr, A, TS, TT)
+    K = min(M, N)
+    Q = dp.block_cyclic(ctx, dt, NB, NB, M, M)
+    if tr is None:
+        dp.ungqr(ctx, A, TS, Q)
+    else:
+        dp.ungqr_param(ctx, tr, A, TS, TT, Q)
+    q = _dense(Q)
+    assert (q.T @ q - torch.eye(M, dtype=dt)).abs().max() < 1e-13
+    assert rel_err(q[:, :K] @ torch.triu(_dense(A)[:K]), a) < 1e-13
+    for side in (dp.dplasmaLeft, dp.dplasmaRight):
+        for trans in (dp.dplasmaNoTrans, dp.dplasmaTrans):
+            shp = (M, 11) if side == dp.dplasmaLeft else (11, M)
+            C = _mk(ctx, dt, shp[0], shp[1], NB, 9)
+            c = _dense(C)
+            if tr is None:
+                dp.unmqr(ctx, side, trans, A, TS, C)
+            else:
+                dp.unmqr_param(ctx, side, trans, tr, A, TS, TT, C)
+            op = q if trans == dp.dplasmaNoTrans else q.T
+            ref = op @ c if side == dp.dplasmaLeft else c @ op
+            assert rel_err(_dense(C), ref) < 1e-12, (side, trans)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", ["d", "s"])
+@pytest.mark.parametrize("M,nc,kf", [(300, 64, 64), (1000, 256, 256), (256, 256, 256), (513, 200, 200), (70, 100, 70),
+                                     (5000, 256, 256), (40000, 256, 256), (65536, 128, 128)])
+def test_gpu_qr_panel_kernel(prec, M, nc, kf):
+    """Persistent HIP panel kernel vs the LAPACK path of the same op (same sign conventions)."""
+    dt = DTYPES[prec]
+    ld = M + 7
+    P0, g, info = _panel_case("cuda", dt, M, nc, kf, ld, M + nc)
+    assert info == 0
+    _, c, _ = _panel_case("cpu", torch.float64, M, nc, kf, ld, M + nc)
+    tol = 1e-10 if prec == "d" else 2e-3
+    for i, (x, y) in enumerate(zip(g, c)):
+        assert rel_err(x, y) < tol, i

@@ -26,8 +26,14 @@ def main():
     ap.add_argument("--runs", type=int, default=2)
     ap.add_argument("--prec", default="d")
     ap.add_argument("--tree", default="flat")
+    ap.add_argument("--qr-a", type=int, default=0, help="HQR TS domain size in tiles (0: one domain per process row)")
+    ap.add_argument("--qr-llvl", type=int, default=1, help="HQR low-level tree (0 flat, 1 greedy, 2 fibonacci, 3 binary)")
+    ap.add_argument("--qr-hlvl", type=int, default=1, help="HQR high-level tree")
+    ap.add_argument("--engine", default="panel", help="QR engine: panel (stacked domains) or tile")
     a = ap.parse_args()
     ctx = dp.init(device="cuda:0")
+    from dplasma_amd.models import qr_panel
+    qr_panel._ENGINE[0] = a.engine
     dt = {"s": torch.float32, "d": torch.float64, "c": torch.complex64, "z": torch.complex128}[a.prec]
     M = a.M or a.N
     N = a.N
@@ -41,8 +47,10 @@ def main():
             if a.tree == "flat":
                 tp = (dp.geqrf_New if a.op == "geqrf" else dp.gelqf_New)(ctx, A, TS)
             else:
-                tree = dp.hqr_init(dp.dplasmaNoTrans if a.op == "geqrf" else dp.dplasmaConjTrans, A,
-                                   dp.dplasma_GREEDY_TREE, dp.dplasma_GREEDY_TREE, 4, 1)
+                tr_ = dp.dplasmaNoTrans if a.op == "geqrf" else dp.dplasmaConjTrans
+                rows = A.mt if a.op == "geqrf" else A.nt
+                P_ = ctx.P if a.op == "geqrf" else ctx.Q
+                tree = dp.hqr_init(tr_, A, a.qr_llvl, a.qr_hlvl, a.qr_a or -(-rows // P_), P_)
                 tp = (dp.geqrf_param_New if a.op == "geqrf" else dp.gelqf_param_New)(ctx, tree, A, TS, TT)
         elif a.op == "getrf_nopiv":
             dp.plghe(ctx, float(N), dp.dplasmaUpperLower, A, 3872)
