@@ -51,32 +51,51 @@ template <> struct QPM<float> {
 template <typename T>
 __global__ __launch_bounds__(256, 1) void k_qr_panel_persist(T* __restrict__ P, int ldp, int M, int nc, int kf, int R,
                                                              T* __restrict__ V, int ldv, T* __restrict__ Tm, int ldt,
-                                                             T* __restrict__ part1, T* __restrict__ part2,
-                                                             T* __restrict__ Yg, T* __restrict__ Xc,
-                                                             int* __restrict__ cnt, int* __restrict__ info) {
+                                                             T* __restrict__ part1, T* __restrict__ rowj,
+                                                             T* __restrict__ part2, T* __restrict__ Yg,
+                                                             T* __restrict__ Xc, int* __restrict__ cnt,
+                                                             int* __restrict__ info, long long* __restrict__ prof) {
   typedef QPM<T> MM;
   typedef typename MM::acc_t acc_t;
-  __shared__ T Ab[QP_B][QP_LD];   // current block columns (later: explicit V_b)
-  __shared__ T Xs[QP_B][QP_LD];   // streamed chunk of other columns
+  __shared__ T Ab[QP_B][QP_LD];     // finished block columns (R / beta / V), later explicit V_b
+  __shared__ T Xs[QP_B][QP_LD];     // explicit V_b during the column steps, later streamed chunks
   __shared__ T Ts[QP_B][QP_B + 1];  // T_b, Ts[col][row]
-  __shared__ T Ws[QP_B][QP_WL];   // Y / T_b^T Y chunk, Ws[col][k]
+  __shared__ T Ws[QP_B][QP_WL];     // Gram block / Y chunk / T_b^T Y chunk, Ws[col][k]
   __shared__ T red[8][QP_B + 1];
   __shared__ T fin[2 * QP_B];
-  __shared__ T ff[QP_B], tv[QP_B];
+  __shared__ T ff[QP_B], taus[QP_B];
   const int G = gridDim.x, w = blockIdx.x, tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
   const int rbase = w * R;
   const int nr = max(0, min(R, M - rbase));
   const int R16 = (nr + 15) & ~15;
+  const int grow = rbase + tid;
+  const bool rowok = tid < nr;
   int nsync = 0;
   const int nblk = (kf + QP_B - 1) / QP_B;
+  // optional phase timers (workgroup 0, 100 MHz ticks): 0 column-step compute, 1 column barrier,
+  // 2 partial reduction, 3 Y partials, 4 Y barriers + reduction + T_b, 5 trailing update, 6 T coupling
+  const bool tprof = prof != nullptr && w == 0 && tid == 0;
+  unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tlast = tprof ? __builtin_amdgcn_s_memrealtime() : 0;
+#define QP_TICK(slot)                                                \
+  if (tprof) {                                                       \
+    const unsigned long long tn_ = __builtin_amdgcn_s_memrealtime(); \
+    tacc[slot] += tn_ - tlast;                                       \
+    tlast = tn_;                                                     \
+  }
 
   for (int b = 0; b < nblk; ++b) {
     const int b0 = b * QP_B;
-    const int cb = min(QP_B, nc - b0);   // block columns held in LDS
+    const int cb = min(QP_B, nc - b0);   // block columns
     const int bw = min(QP_B, kf - b0);   // of which reflectors
-    for (int e = tid; e < QP_B * R16; e += 256) {
-      const int c = e / R16, r = e % R16;
-      Ab[c][r] = (c < cb && r < nr) ? P[(rbase + r) + (long long)(b0 + c) * ldp] : T(0);
+    // The thread owning local row tid keeps the row's block in registers, rotated so that the
+    // active column is always a[0] (static register indices only).
+    T a[QP_B];
+#pragma unroll
+    for (int c = 0; c < QP_B; ++c) a[c] = (rowok && c < cb) ? P[grow + (long long)(b0 + c) * ldp] : T(0);
+    for (int e = tid; e < QP_B * QP_LD; e += 256) {
+      (&Xs[0][0])[e] = T(0);
+      (&Ab[0][0])[e] = T(0);
     }
     for (int e = tid; e < QP_B * (QP_B + 1); e += 256) (&Ts[0][0])[e] = T(0);
     __syncthreads();
@@ -84,42 +103,78 @@ __global__ __launch_bounds__(256, 1) void k_qr_panel_persist(T* __restrict__ P, 
     for (int jj = 0; jj < bw; ++jj) {
       const int j = b0 + jj;
       const int par = nsync & 1;
+      const int sh = QP_B - jj;  // live slots: slot s is column jj + s
       {
-        const int c = tid & 31, g = tid >> 5;
-        const int rs = j + 1 - rbase;  // first local row strictly below the diagonal
-        T s = T(0);
-        if (c < cb)
-          for (int rl = g; rl < nr; rl += 8)
-            if (rl >= rs) s += Ab[jj][rl] * Ab[c][rl];
-        red[g][c] = s;
+        // x = A(r > j, j) against every live column, then a wave transpose-reduction:
+        // lane l ends with the wave's sum for slot l >> 1
+        const T x = (rowok && grow > j) ? a[0] : T(0);
+        T v[QP_B];
+#pragma unroll
+        for (int s = 0; s < QP_B; ++s) v[s] = s < sh ? x * a[s] : T(0);
+#pragma unroll
+        for (int wdt = QP_B / 2, m = 32; wdt >= 1; wdt >>= 1, m >>= 1) {
+          const bool hi = (l & m) != 0;
+#pragma unroll
+          for (int i = 0; i < wdt; ++i) {
+            const T send = hi ? v[i] : v[wdt + i];
+            const T keep = hi ? v[wdt + i] : v[i];
+            v[i] = keep + __shfl_xor(send, m, 64);
+          }
+        }
+        v[0] += __shfl_xor(v[0], 1, 64);
+        if ((l & 1) == 0) red[wv][l >> 1] = v[0];
+        if (rowok && grow == j) {
+          T* rj = rowj + par * QP_B;
+#pragma unroll
+          for (int s = 0; s < QP_B; ++s)
+            if (s < sh) st_sc1(&rj[s], a[s]);
+        }
+      }
+      __syncthreads();
+      if (tid < QP_B) {
+        const T d = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+        st_sc1(&part1[((long long)par * G + w) * QP_B + tid], d);
+      }
+      QP_TICK(0);
+      if (G > 1) {
+        ++nsync;
+        grid_sync_counter(cnt, nsync * G, info);
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      QP_TICK(1);
+      {
+        // thread (slot s, group q) sums partials q, q+8, ... (up to 16 loads in flight)
+        const int s = tid & 31, q = tid >> 5;
+        T acc = T(0);
+        if (s < sh) {
+          const T* src = part1 + (long long)par * G * QP_B + s;
+          for (int base = q; base < G; base += 8 * 16) {
+            T t[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+              const int bb = base + 8 * u;
+              t[u] = bb < G ? ld_sc1(&src[(long long)bb * QP_B]) : T(0);
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) acc += t[u];
+          }
+        }
+        red[q][s] = acc;
+        if (tid < QP_B) fin[QP_B + tid] = tid < sh ? ld_sc1(&rowj[par * QP_B + tid]) : T(0);
       }
       __syncthreads();
       if (tid < QP_B) {
         T d = T(0);
 #pragma unroll
-        for (int g = 0; g < 8; ++g) d += red[g][tid];
-        const bool own = j >= rbase && j < rbase + nr;
-        const T rv = (own && tid < cb) ? Ab[tid][j - rbase] : T(0);
-        T* pp = part1 + ((long long)par * G + w) * (2 * QP_B);
-        st_sc1(&pp[tid], d);
-        st_sc1(&pp[QP_B + tid], rv);
-      }
-      ++nsync;
-      grid_sync_counter(cnt, nsync * G, info);
-      {
-        const int v = tid & 63, q = tid >> 6;
-        T s = T(0);
-        for (int bb = q; bb < G; bb += 4) s += ld_sc1(&part1[((long long)par * G + bb) * (2 * QP_B) + v]);
-        (&red[0][0])[q * 64 + v] = s;
+        for (int q = 0; q < 8; ++q) d += red[q][tid];
+        fin[tid] = d;
       }
       __syncthreads();
-      if (tid < 2 * QP_B) {
-        const T* rf = &red[0][0];
-        fin[tid] = (rf[tid] + rf[64 + tid]) + (rf[128 + tid] + rf[192 + tid]);
-      }
-      __syncthreads();
-      // dlarfg (every thread derives the same scalars)
-      const T alpha = fin[QP_B + jj], x2 = fin[jj];
+      QP_TICK(2);
+      // dlarfg (every thread derives the same scalars); slot 0 is column jj
+      const T alpha = fin[QP_B], x2 = fin[0];
       T beta, tau, scale;
       if (x2 == T(0)) {
         beta = alpha;
@@ -132,68 +187,63 @@ __global__ __launch_bounds__(256, 1) void k_qr_panel_persist(T* __restrict__ P, 
         scale = T(1) / (alpha - beta);
       }
       if (tid < QP_B) {
-        const T t = fin[QP_B + tid] + scale * fin[tid];   // v^T A(:, tid) (c > jj), V(:, tid)^T v (c < jj)
-        ff[tid] = (tid > jj && tid < cb) ? tau * t : T(0);
-        tv[tid] = tid < jj ? t : T(0);
+        ff[tid] = (tid >= 1 && tid < sh && jj + tid < cb) ? tau * (fin[QP_B + tid] + scale * fin[tid]) : T(0);
+        if (tid == 0) taus[jj] = tau;
       }
       __syncthreads();
-      if (tid < jj) {
-        T z = T(0);
-        for (int k = tid; k < jj; ++k) z += Ts[k][tid] * tv[k];
-        Ts[jj][tid] = -tau * z;
-      } else if (tid == jj) {
-        Ts[jj][jj] = tau;
+      if (rowok) {
+        const T x = a[0];
+        const T vr = grow > j ? scale * x : (grow == j ? T(1) : T(0));
+#pragma unroll
+        for (int s = 1; s < QP_B; ++s) a[s] -= vr * ff[s];
+        Ab[jj][tid] = grow < j ? x : (grow == j ? beta : vr);
+        Xs[jj][tid] = vr;
       }
-      if (tid < nr) {
-        const int grow = rbase + tid;
-        if (grow > j) {
-          const T vr = scale * Ab[jj][tid];
-          Ab[jj][tid] = vr;
-          for (int c = jj + 1; c < cb; ++c) Ab[c][tid] -= vr * ff[c];
-        } else if (grow == j) {
-          Ab[jj][tid] = beta;
-          for (int c = jj + 1; c < cb; ++c) Ab[c][tid] -= ff[c];
-        }
-      }
-      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < QP_B - 1; ++s) a[s] = a[s + 1];
+      a[QP_B - 1] = T(0);
     }
-    // ------------------------------------------------------------ block results
-    if (w == 0)
-      for (int e = tid; e < bw * bw; e += 256) {
-        const int i = e % bw, c = e / bw;
-        st_sc1(&Tm[(b0 + i) + (long long)(b0 + c) * ldt], i <= c ? Ts[c][i] : T(0));
-      }
-    for (int e = tid; e < cb * R16; e += 256) {
-      const int c = e / R16, r = e % R16;
-      const int grow = rbase + r, gc = b0 + c;
-      const T a = Ab[c][r];
-      T vex = T(0);
-      if (r < nr) {
-        P[grow + (long long)gc * ldp] = a;
-        if (c < bw) {
-          vex = grow > gc ? a : (grow == gc ? T(1) : T(0));
-          V[grow + (long long)gc * ldv] = vex;
-        }
-      }
-      Ab[c][r] = vex;
-    }
+    // non-reflector block columns (kf < nc): still in registers, rotated by bw
+    if (rowok)
+#pragma unroll
+      for (int s = 0; s < QP_B; ++s)
+        if (s < cb - bw) Ab[(bw + s) & (QP_B - 1)][tid] = a[s];
     __syncthreads();
-    const int nA = nc - b0 - cb;   // trailing panel columns
-    const int nX = b0 + nA;        // columns of [V_prev | A_rest]
-    if (nX <= 0) continue;
+    // ------------------------------------------------------------ block results (row per thread)
+    if (rowok) {
+#pragma unroll
+      for (int c = 0; c < QP_B; ++c) {
+        if (c < cb) P[grow + (long long)(b0 + c) * ldp] = Ab[c][tid];
+        if (c < bw) V[grow + (long long)(b0 + c) * ldv] = Xs[c][tid];
+      }
+    }
+    if (tid < R16)
+      for (int c = 0; c < QP_B; ++c) Ab[c][tid] = c < bw ? Xs[c][tid] : T(0);
+    __syncthreads();
+    // ------------------------------------------------------------ Y partials: V_b^T [V_b | V_prev | A_rest]
+    const int nA = nc - b0 - cb;
+    const int nX = QP_B + b0 + nA;
     const bool act = rbase + nr > b0;
     const long long E = (long long)QP_B * nX;
-    // ------------------------------------------------------------ Y partials (MFMA, K = own rows)
     for (int x0 = 0; x0 < nX; x0 += QP_B) {
       const int cw = min(QP_B, nX - x0);
+      T* pw = part2 + (long long)w * E;
       if (act) {
-        for (int e = tid; e < QP_B * R16; e += 256) {
-          const int c = e / R16, r = e % R16;
-          const int grow = rbase + r, xc = x0 + c;
-          T v = T(0);
-          if (c < cw && r < nr && grow >= b0)
-            v = xc < b0 ? V[grow + (long long)xc * ldv] : P[grow + (long long)(cb + xc) * ldp];
-          Xs[c][r] = v;
+        if (tid < R16) {
+          // chunks never straddle the V_b | V_prev | A_rest boundaries (b0 is a multiple of 32)
+          const bool live = rowok && grow >= b0;
+          if (x0 < QP_B) {
+            for (int c = 0; c < QP_B; ++c) Xs[c][tid] = Ab[c][tid];
+          } else {
+            const T* src = x0 < QP_B + b0 ? V + grow + (long long)(x0 - QP_B) * ldv
+                                          : P + grow + (long long)(cb + x0 - QP_B) * ldp;
+            const long long ld = x0 < QP_B + b0 ? ldv : ldp;
+            T t[QP_B];
+#pragma unroll
+            for (int c = 0; c < QP_B; ++c) t[c] = (live && c < cw) ? src[c * ld] : T(0);
+#pragma unroll
+            for (int c = 0; c < QP_B; ++c) Xs[c][tid] = t[c];
+          }
         }
         __syncthreads();
         const int pt = wv & 1, qt = wv >> 1;
@@ -207,7 +257,6 @@ __global__ __launch_bounds__(256, 1) void k_qr_panel_persist(T* __restrict__ P, 
           a2 = MM::mma(Ab[pt * 16 + (l & 15)][rr + 8], Xs[qt * 16 + (l & 15)][rr + 8], a2);
           a3 = MM::mma(Ab[pt * 16 + (l & 15)][rr + 12], Xs[qt * 16 + (l & 15)][rr + 12], a3);
         }
-        T* pw = part2 + (long long)w * E;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int p = pt * 16 + MM::drow(l, r), q = qt * 16 + (l & 15);
@@ -215,14 +264,26 @@ __global__ __launch_bounds__(256, 1) void k_qr_panel_persist(T* __restrict__ P, 
         }
         __syncthreads();
       } else {
-        T* pw = part2 + (long long)w * E;
-        for (int e = tid; e < QP_B * cw; e += 256) st_sc1(&pw[(long long)(e / cw) * nX + x0 + e % cw], T(0));
+        for (int p = wv; p < QP_B; p += 4)
+          if (l < cw) st_sc1(&pw[(long long)p * nX + x0 + l], T(0));
       }
     }
+    QP_TICK(3);
     ++nsync;
     grid_sync_counter(cnt, nsync * G, info);
-    // ------------------------------------------------------------ Y = sum of partials (slice per workgroup)
-    {
+    // ------------------------------------------------------------ Y = sum of partials
+    if (G <= 8) {
+      // few partials: thread per entry, no LDS round
+      const long long epw = (E + G - 1) / G;
+      const long long e_beg = (long long)w * epw, e_end = min(E, e_beg + epw);
+      for (long long e = e_beg + tid; e < e_end; e += 256) {
+        T y = T(0);
+        for (int bb = 0; bb < G; ++bb) y += ld_sc1(&part2[(long long)bb * E + e]);
+        st_sc1(&Yg[e], y);
+        const int p = (int)(e / nX), xc = (int)(e - (long long)p * nX);
+        if (xc >= QP_B && xc < QP_B + b0) st_sc1(&Xc[((long long)b * QP_B + p) * kf + xc - QP_B], y);
+      }
+    } else {
       const long long epw = (E + G - 1) / G;
       const long long e_beg = (long long)w * epw, e_end = min(E, e_beg + epw);
       for (long long base = e_beg; base < e_end; base += 32) {
@@ -238,26 +299,54 @@ __global__ __launch_bounds__(256, 1) void k_qr_panel_persist(T* __restrict__ P, 
 #pragma unroll
           for (int gg = 0; gg < 8; ++gg) y += red[gg][tid];
           st_sc1(&Yg[e], y);
-          const int p = (int)(e / nX), xc = (int)(e % nX);
-          if (xc < b0) st_sc1(&Xc[((long long)b * QP_B + p) * kf + xc], y);
+          const int p = (int)(e / nX), xc = (int)(e - (long long)p * nX);
+          if (xc >= QP_B && xc < QP_B + b0) st_sc1(&Xc[((long long)b * QP_B + p) * kf + xc - QP_B], y);
         }
         __syncthreads();
       }
     }
     ++nsync;
     grid_sync_counter(cnt, nsync * G, info);
+    // ------------------------------------------------------------ T_b from taus and the Gram block
+    for (int e = tid; e < QP_B * QP_B; e += 256) {
+      const int c = e >> 5, k = e & 31;
+      Ws[c][k] = ld_sc1(&Yg[(long long)k * nX + c]);   // G_b(k, c) = v_k^T v_c
+    }
+    __syncthreads();
+    if (tid < bw) {
+      // lane i builds row i of T_b: T(i, j) = -tau_j sum_{k=i}^{j-1} T(i, k) G(k, j)
+      const int i = tid;
+      Ts[i][i] = taus[i];
+      for (int jc = i + 1; jc < bw; ++jc) {
+        T z = T(0);
+        for (int k = i; k < jc; ++k) z += Ts[k][i] * Ws[jc][k];
+        Ts[jc][i] = -taus[jc] * z;
+      }
+    }
+    __syncthreads();
+    if (w == 0)
+      for (int e = tid; e < bw * bw; e += 256) {
+        const int c = e / bw, i = e - c * bw;
+        st_sc1(&Tm[(b0 + i) + (long long)(b0 + c) * ldt], i <= c ? Ts[c][i] : T(0));
+      }
+    QP_TICK(4);
     // ------------------------------------------------------------ A_rest -= V_b (T_b^T Y)
     if (nA > 0 && act) {
+      const int ycol0 = QP_B + b0;
       for (int a0 = 0; a0 < nA; a0 += QP_B) {
         const int cw = min(QP_B, nA - a0);
         for (int e = tid; e < QP_B * QP_B; e += 256) {
-          const int q = e / QP_B, i = e % QP_B;
-          Ws[q][i] = q < cw ? ld_sc1(&Yg[(long long)i * nX + b0 + a0 + q]) : T(0);
+          const int q = e >> 5, i = e & 31;
+          Ws[q][i] = q < cw ? ld_sc1(&Yg[(long long)i * nX + ycol0 + a0 + q]) : T(0);
         }
-        for (int e = tid; e < QP_B * R16; e += 256) {
-          const int c = e / R16, r = e % R16;
-          const int grow = rbase + r;
-          Xs[c][r] = (c < cw && r < nr && grow >= b0) ? P[grow + (long long)(b0 + cb + a0 + c) * ldp] : T(0);
+        if (tid < R16) {
+          const bool live = rowok && grow >= b0;
+          const T* src = P + grow + (long long)(b0 + cb + a0) * ldp;
+          T t[QP_B];
+#pragma unroll
+          for (int c = 0; c < QP_B; ++c) t[c] = (live && c < cw) ? src[(long long)c * ldp] : T(0);
+#pragma unroll
+          for (int c = 0; c < QP_B; ++c) Xs[c][tid] = t[c];
         }
         __syncthreads();
         T o[4];
@@ -293,58 +382,71 @@ __global__ __launch_bounds__(256, 1) void k_qr_panel_persist(T* __restrict__ P, 
           for (int r = 0; r < 4; ++r) Xs[qt * 16 + (l & 15)][rt * 16 + MM::drow(l, r)] = acc[r];
         }
         __syncthreads();
-        for (int e = tid; e < cw * R16; e += 256) {
-          const int c = e / R16, r = e % R16;
-          const int grow = rbase + r;
-          if (r < nr && grow >= b0) P[grow + (long long)(b0 + cb + a0 + c) * ldp] = Xs[c][r];
+        if (rowok && grow >= b0) {
+          T* dst = P + grow + (long long)(b0 + cb + a0) * ldp;
+#pragma unroll
+          for (int c = 0; c < QP_B; ++c)
+            if (c < cw) dst[(long long)c * ldp] = Xs[c][tid];
         }
         __syncthreads();
       }
     }
+    QP_TICK(5);
   }
   // ------------------------------------------------------------ off-diagonal T blocks
+  // T(i, blk) = -T(i, 0:b0) Z, Z = X_b T_b, X_b = V_prev^T V_b; workgroup w owns T rows w, w+G, ...
   if (nblk > 1) {
     ++nsync;
     grid_sync_counter(cnt, nsync * G, info);
     for (int b = 1; b < nblk; ++b) {
       const int b0 = b * QP_B, bw = min(QP_B, kf - b0);
-      if (w >= b0) continue;   // owns no T row above this block
+      if (w >= b0) continue;
       for (int e = tid; e < QP_B * QP_B; e += 256) {
-        const int c = e / QP_B, k = e % QP_B;
+        const int c = e >> 5, k = e & 31;
         Ts[c][k] = (k <= c && c < bw) ? ld_sc1(&Tm[(b0 + k) + (long long)(b0 + c) * ldt]) : T(0);
       }
-      for (int e = tid; e < QP_B * b0; e += 256) {
-        const int k = e / b0, j = e % b0;
-        Ab[k][j] = k < bw ? ld_sc1(&Xc[((long long)b * QP_B + k) * kf + j]) : T(0);
-      }
+      if (tid < b0)
+        for (int k = 0; k < QP_B; ++k) Ab[k][tid] = k < bw ? ld_sc1(&Xc[((long long)b * QP_B + k) * kf + tid]) : T(0);
       __syncthreads();
-      // Z(j, c) = sum_k X(j, k) T_b(k, c), X = V_prev^T V_b
-      for (int e = tid; e < QP_B * b0; e += 256) {
-        const int c = e / b0, j = e % b0;
-        T z = T(0);
-        for (int k = 0; k <= c; ++k) z += Ab[k][j] * Ts[c][k];
-        Xs[c][j] = z;
-      }
+      if (tid < b0)
+        for (int c = 0; c < QP_B; ++c) {
+          T z = T(0);
+          for (int k = 0; k <= c; ++k) z += Ab[k][tid] * Ts[c][k];
+          Xs[c][tid] = z;   // Z(j = tid, c)
+        }
       __syncthreads();
-      T* trow = &Ws[0][0];
-      for (int i = w; i < b0; i += G) {
-        for (int j = tid; j < b0; j += 256) trow[j] = j >= i ? ld_sc1(&Tm[i + (long long)j * ldt]) : T(0);
+      // own rows, 4 at a time: stage T(i, 0:b0) in LDS, then thread (c, row, half) sums over j
+      const int nown = (b0 - w + G - 1) / G;
+      T* trow = &Ws[0][0];   // [4][b0]
+      for (int o0 = 0; o0 < nown; o0 += 4) {
+        for (int e = tid; e < 4 * b0; e += 256) {
+          const int oi = e / b0, jx = e - oi * b0;
+          const int i = w + (o0 + oi) * G;
+          trow[e] = (o0 + oi < nown && jx >= i) ? ld_sc1(&Tm[i + (long long)jx * ldt]) : T(0);
+        }
         __syncthreads();
-        const int c = tid & 31, g = tid >> 5;
-        T s = T(0);
-        for (int j = i + g; j < b0; j += 8) s += trow[j] * Xs[c][j];
-        red[g][c] = s;
+        {
+          const int c = tid & 31, oi = (tid >> 5) & 3, hh = tid >> 7;
+          const int i = w + (o0 + oi) * G;
+          T s = T(0);
+          if (o0 + oi < nown)
+            for (int jx = i + hh; jx < b0; jx += 2) s += trow[oi * b0 + jx] * Xs[c][jx];
+          red[hh * 4 + oi][c] = s;
+        }
         __syncthreads();
-        if (tid < bw) {
-          T t = T(0);
-#pragma unroll
-          for (int gg = 0; gg < 8; ++gg) t += red[gg][tid];
-          st_sc1(&Tm[i + (long long)(b0 + tid) * ldt], -t);
+        if (tid < 128) {
+          const int c = tid & 31, oi = tid >> 5;
+          const int i = w + (o0 + oi) * G;
+          if (o0 + oi < nown && c < bw) st_sc1(&Tm[i + (long long)(b0 + c) * ldt], -(red[oi][c] + red[4 + oi][c]));
         }
         __syncthreads();
       }
     }
   }
+  QP_TICK(6);
+  if (tprof)
+    for (int i = 0; i < 8; ++i) prof[i] += (long long)tacc[i];
+#undef QP_TICK
 }
 
 static int g_qp_cus = 0;
@@ -359,15 +461,31 @@ static int qp_cus() {
   return g_qp_cus;
 }
 
+static long long* g_qp_prof = nullptr;
+// Debug: accumulate workgroup 0's phase timers (8 x int64, 100 MHz ticks) into dev_ptr (nullptr: off).
+DPL_API int dpl_qr_panel_set_prof(void* dev_ptr) {
+  g_qp_prof = (long long*)dev_ptr;
+  return 0;
+}
+
 static inline long long qp_align(long long x) { return (x + 255) & ~255LL; }
 
-// Workspace layout (bytes, 256-aligned parts): part1 [2][256][64], part2 [256][32*nc], Yg [32*nc],
-// Xc [nblk][32][kf] elements of the precision, then the barrier counter.
-DPL_API long long dpl_qr_panel_ws_bytes(int prec, int nc, int kf) {
-  const long long es = prec == DPL_D ? 8 : 4;
+// Workspace layout (bytes, 256-aligned parts): part1 [2][256][32], rowj [2][32], part2 [256][32*(nc+32)],
+// Yg [32*(nc+32)], Xc [nblk][32][kf] elements of the precision, then the barrier counter.
+static inline void qp_layout(long long es, int nc, int kf, long long off[6]) {
   const long long nblk = (kf + QP_B - 1) / QP_B;
-  return qp_align(es * 2 * 256 * 2 * QP_B) + qp_align(es * 256LL * QP_B * nc) + qp_align(es * QP_B * nc) +
-         qp_align(es * nblk * QP_B * kf) + 256;
+  off[0] = 0;
+  off[1] = off[0] + qp_align(es * 2 * 256 * QP_B);
+  off[2] = off[1] + qp_align(es * 2 * QP_B);
+  off[3] = off[2] + qp_align(es * 256LL * QP_B * (nc + QP_B));
+  off[4] = off[3] + qp_align(es * QP_B * (nc + QP_B));
+  off[5] = off[4] + qp_align(es * nblk * QP_B * kf);
+}
+
+DPL_API long long dpl_qr_panel_ws_bytes(int prec, int nc, int kf) {
+  long long off[6];
+  qp_layout(prec == DPL_D ? 8 : 4, nc, kf, off);
+  return off[5] + 256;
 }
 
 // Largest panel height the single-launch kernel takes (one workgroup per CU, <= 256 rows each).
@@ -383,26 +501,19 @@ DPL_API int dpl_qr_panel(int prec, void* P, int ldp, int M, int nc, int kf, void
   if (G > cus) return -4;
   if (G < 1) G = 1;
   const int R = (M + G - 1) / G;
-  const long long es = prec == DPL_D ? 8 : 4;
-  const long long nblk = (kf + QP_B - 1) / QP_B;
+  long long off[6];
+  qp_layout(prec == DPL_D ? 8 : 4, nc, kf, off);
   char* b = (char*)ws;
-  void* part1 = b;
-  b += qp_align(es * 2 * 256 * 2 * QP_B);
-  void* part2 = b;
-  b += qp_align(es * 256LL * QP_B * nc);
-  void* Yg = b;
-  b += qp_align(es * QP_B * nc);
-  void* Xc = b;
-  b += qp_align(es * nblk * QP_B * kf);
-  int* cnt = (int*)b;
+  void *part1 = b + off[0], *rowj = b + off[1], *part2 = b + off[2], *Yg = b + off[3], *Xc = b + off[4];
+  int* cnt = (int*)(b + off[5]);
   hipMemsetAsync(cnt, 0, sizeof(int), st);
   if (prec == DPL_D)
     hipLaunchKernelGGL((k_qr_panel_persist<double>), dim3(G), dim3(256), 0, st, (double*)P, ldp, M, nc, kf, R,
-                       (double*)V, ldv, (double*)Tm, ldt, (double*)part1, (double*)part2, (double*)Yg, (double*)Xc,
-                       cnt, info);
+                       (double*)V, ldv, (double*)Tm, ldt, (double*)part1, (double*)rowj, (double*)part2, (double*)Yg, (double*)Xc,
+                       cnt, info, g_qp_prof);
   else
     hipLaunchKernelGGL((k_qr_panel_persist<float>), dim3(G), dim3(256), 0, st, (float*)P, ldp, M, nc, kf, R,
-                       (float*)V, ldv, (float*)Tm, ldt, (float*)part1, (float*)part2, (float*)Yg, (float*)Xc, cnt,
-                       info);
+                       (float*)V, ldv, (float*)Tm, ldt, (float*)part1, (float*)rowj, (float*)part2, (float*)Yg, (float*)Xc, cnt,
+                       info, g_qp_prof);
   return (int)hipGetLastError();
 }

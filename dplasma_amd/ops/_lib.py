@@ -72,6 +72,7 @@ _SIGS = {
     "dpl_qr_panel": [c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp],
     "dpl_qr_panel_ws_bytes": [c_int, c_int, c_int],
     "dpl_qr_panel_max_rows": [],
+    "dpl_qr_panel_set_prof": [c_vp],
     # ipiv, kb, dst, src, cnt, stream
     "dpl_piv_moves": [c_vp, c_int, c_vp, c_vp, c_vp, c_vp],
     # prec, gather, A, ld, mb, r0, rowoff, nrt, coloff, ncols, nct, nb, rows, cnt, maxcnt, buf, ldb, stream
