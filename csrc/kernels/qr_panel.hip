@@ -49,7 +49,8 @@ template <> struct QPM<float> {
 // mma(x, y, acc): D(p, q) += sum_k x(p, k) y(q, k); input lane l carries p (resp. q) = l & 15,
 // k = l >> 4; output acc[r] of lane l is D(drow(l, r), l & 15).
 template <typename T>
-__global__ __launch_bounds__(256, 1) void k_qr_panel_persist(T* __restrict__ P, int ldp, int M, int nc, int kf, int R,
+__global__ __launch_bounds__(256, 1) void k_qr_panel_persist(T* __restrict__ P0, int ldp, int rbl, long long rstride,
+                                                             int M, int nc, int kf, int R,
                                                              T* __restrict__ V, int ldv, T* __restrict__ Tm, int ldt,
                                                              T* __restrict__ part1, T* __restrict__ rowj,
                                                              T* __restrict__ part2, T* __restrict__ Yg,
@@ -70,6 +71,9 @@ __global__ __launch_bounds__(256, 1) void k_qr_panel_persist(T* __restrict__ P, 
   const int R16 = (nr + 15) & ~15;
   const int grow = rbase + tid;
   const bool rowok = tid < nr;
+  // row grow of the panel starts at P: panel rows come in blocks of rbl rows rstride apart
+  // (tile-storage panels are addressed in place; contiguous panels pass rbl >= M)
+  T* const P = P0 + (long long)(grow / rbl) * rstride + (grow % rbl) - grow;
   int nsync = 0;
   const int nblk = (kf + QP_B - 1) / QP_B;
   // optional phase timers (workgroup 0, 100 MHz ticks): 0 column-step compute, 1 column barrier,
@@ -491,11 +495,20 @@ DPL_API long long dpl_qr_panel_ws_bytes(int prec, int nc, int kf) {
 // Largest panel height the single-launch kernel takes (one workgroup per CU, <= 256 rows each).
 DPL_API int dpl_qr_panel_max_rows() { return qp_cus() * QP_R; }
 
-DPL_API int dpl_qr_panel(int prec, void* P, int ldp, int M, int nc, int kf, void* V, int ldv, void* Tm, int ldt,
-                         void* ws, int* info, hipStream_t st) {
+// P: column-major panel (ld ldp); rbl > 0 && rbl < M: rows come in blocks of rbl rows that are
+// rstride elements apart (tile storage: rbl = mb, rstride = mb * nb, ldp = mb).
+DPL_API int dpl_qr_panel(int prec, void* P, int ldp, int rbl, long long rstride, int M, int nc, int kf, void* V,
+                         int ldv, void* Tm, int ldt, void* ws, int* info, hipStream_t st) {
   if (kf <= 0) return 0;
   if (prec != DPL_D && prec != DPL_S) return -2;
-  if (kf > M || kf > nc || kf > QP_R || ldp < M || ldv < M || ldt < kf) return -3;
+  if (rbl <= 0 || rbl >= M) {
+    rbl = 1 << 30;
+    rstride = 0;
+    if (ldp < M) return -3;
+  } else if (ldp < rbl) {
+    return -3;
+  }
+  if (kf > M || kf > nc || kf > QP_R || ldv < M || ldt < kf) return -3;
   const int cus = qp_cus();
   int G = (M + QP_R - 1) / QP_R;
   if (G > cus) return -4;
@@ -508,12 +521,55 @@ DPL_API int dpl_qr_panel(int prec, void* P, int ldp, int M, int nc, int kf, void
   int* cnt = (int*)(b + off[5]);
   hipMemsetAsync(cnt, 0, sizeof(int), st);
   if (prec == DPL_D)
-    hipLaunchKernelGGL((k_qr_panel_persist<double>), dim3(G), dim3(256), 0, st, (double*)P, ldp, M, nc, kf, R,
+    hipLaunchKernelGGL((k_qr_panel_persist<double>), dim3(G), dim3(256), 0, st, (double*)P, ldp, rbl, rstride, M, nc, kf, R,
                        (double*)V, ldv, (double*)Tm, ldt, (double*)part1, (double*)rowj, (double*)part2, (double*)Yg, (double*)Xc,
                        cnt, info, g_qp_prof);
   else
-    hipLaunchKernelGGL((k_qr_panel_persist<float>), dim3(G), dim3(256), 0, st, (float*)P, ldp, M, nc, kf, R,
+    hipLaunchKernelGGL((k_qr_panel_persist<float>), dim3(G), dim3(256), 0, st, (float*)P, ldp, rbl, rstride, M, nc, kf, R,
                        (float*)V, ldv, (float*)Tm, ldt, (float*)part1, (float*)rowj, (float*)part2, (float*)Yg, (float*)Xc, cnt,
                        info, g_qp_prof);
+  return (int)hipGetLastError();
+}
+
+// dst[i] = sum_s src[s * stride + i], i < L: the split-K partials of the QR trailing GEMMs
+// (wide grid, 2 elements per thread, S loads in flight per thread).
+template <typename T>
+__global__ __launch_bounds__(256) void k_sum_partials(const T* __restrict__ src, long long stride, int S, long long L,
+                                                     T* __restrict__ dst) {
+  const long long i = 2 * ((long long)blockIdx.x * 256 + threadIdx.x);
+  if (i >= L) return;
+  const bool two = i + 1 < L;
+  T a0 = T(0), a1 = T(0), b0 = T(0), b1 = T(0);
+  int s = 0;
+  for (; s + 1 < S; s += 2) {
+    const T* p = src + (long long)s * stride + i;
+    a0 += p[0];
+    b0 += p[stride];
+    if (two) {
+      a1 += p[1];
+      b1 += p[stride + 1];
+    }
+  }
+  if (s < S) {
+    const T* p = src + (long long)s * stride + i;
+    a0 += p[0];
+    if (two) a1 += p[1];
+  }
+  dst[i] = a0 + b0;
+  if (two) dst[i + 1] = a1 + b1;
+}
+
+DPL_API int dpl_sum_partials(int prec, const void* src, long long stride, int S, long long L, void* dst,
+                             hipStream_t st) {
+  if (L <= 0 || S <= 0) return 0;
+  const unsigned nblk = (unsigned)((L + 511) / 512);
+  if (prec == DPL_D)
+    hipLaunchKernelGGL((k_sum_partials<double>), dim3(nblk), dim3(256), 0, st, (const double*)src, stride, S, L,
+                       (double*)dst);
+  else if (prec == DPL_S)
+    hipLaunchKernelGGL((k_sum_partials<float>), dim3(nblk), dim3(256), 0, st, (const float*)src, stride, S, L,
+                       (float*)dst);
+  else
+    return -2;
   return (int)hipGetLastError();
 }

@@ -144,7 +144,7 @@ class _Left:
         kf, L = self.kf, self.wlen
         ops.gemm(T_, N_, 1.0, V, ldv, C.data, C.ld, 0.0, Wp, kf, self.g1)
         if self.S > 1:
-            torch.sum(Wp[: self.S * L].view(self.S, L), 0, out=W[:L])
+            ops.sum_partials(Wp, L, self.S, L, W)
             src = W
         else:
             src = Wp
@@ -184,7 +184,7 @@ class _Right:
         kf, L, ldw = self.kf, self.wlen, self.ldw
         ops.gemm(N_, N_, 1.0, C.data, C.ld, V, ldv, 0.0, Wp, ldw, self.g1)
         if self.S > 1:
-            torch.sum(Wp[: self.S * L].view(self.S, L), 0, out=W[:L])
+            ops.sum_partials(Wp, L, self.S, L, W)
             src = W
         else:
             src = Wp
@@ -272,6 +272,13 @@ class _Factor:
             g.add(A.offset(r, k), A.tile_rows(r), kb, b_off=o)
             back.add(o, A.tile_rows(r), kb, b_off=A.offset(r, k))
         e["gather"], e["back"], e["part"] = g.finalize(), back.finalize(), part
+        # a domain of consecutive tile rows is factored in place (no gather / scatter copies)
+        e["direct"] = None
+        if not tt and list(rows) == list(range(rows[0], rows[0] + len(rows))):
+            if A.storage == "tile" or A.ld == A.mb:
+                e["direct"] = (A.mb, A.mb, A.mb * A.nb, A.offset(rows[0], k))
+            else:
+                e["direct"] = (A.ld, 0, 0, A.offset(rows[0], k))
         return e
 
     def _build(self, k):
@@ -298,11 +305,16 @@ class _Factor:
         A = self.A
         P, V, Tm = self.P[buf], self.V[buf], self.Tm[buf]
         ld, M, kb, kf = e["ld"], e["M"], e["kb"], e["kf"]
-        if e["tt"]:
-            P[: ld * kb].zero_()
-        ops.geadd(e["part"], N_, 1.0, A.data, A.ld, 0.0, P, ld, e["gather"], copy=True)
-        ops.qr_panel(P, ld, M, kb, kf, V, ld, Tm, A.nb, self.ws, self.info)
-        ops.geadd(e["part"], N_, 1.0, P, ld, 0.0, A.data, A.ld, e["back"], copy=True)
+        if e["direct"] is not None:
+            ldp, rbl, rstride, poff = e["direct"]
+            ops.qr_panel(A.data, ldp, M, kb, kf, V, ld, Tm, A.nb, self.ws, self.info, rbl=rbl, rstride=rstride,
+                         poff=poff)
+        else:
+            if e["tt"]:
+                P[: ld * kb].zero_()
+            ops.geadd(e["part"], N_, 1.0, A.data, A.ld, 0.0, P, ld, e["gather"], copy=True)
+            ops.qr_panel(P, ld, M, kb, kf, V, ld, Tm, A.nb, self.ws, self.info)
+            ops.geadd(e["part"], N_, 1.0, P, ld, 0.0, A.data, A.ld, e["back"], copy=True)
         if e["tt"]:
             _store_T(Tm, A.nb, kf, self.TT, e["rows"][1], k)
         else:

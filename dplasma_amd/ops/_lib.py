@@ -68,8 +68,11 @@ _SIGS = {
     # prec, A, ld, ca, cb, ipiv, i0, i1, stream
     "dpl_laswp_panel": [c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp],
     "dpl_lu_block_ws_bytes": [c_int],
-    # Householder panel (qr_panel.hip): prec, P, ldp, M, nc, kf, V, ldv, Tm, ldt, ws, info, stream
-    "dpl_qr_panel": [c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_vp],
+    # Householder panel (qr_panel.hip): prec, P, ldp, rbl, rstride, M, nc, kf, V, ldv, Tm, ldt, ws, info, stream
+    "dpl_qr_panel": [c_int, c_vp, c_int, c_int, c_ll, c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_vp,
+                     c_vp],
+    # prec, src, stride, S, L, dst, stream
+    "dpl_sum_partials": [c_int, c_vp, c_ll, c_int, c_ll, c_vp, c_vp],
     "dpl_qr_panel_ws_bytes": [c_int, c_int, c_int],
     "dpl_qr_panel_max_rows": [],
     "dpl_qr_panel_set_prof": [c_vp],

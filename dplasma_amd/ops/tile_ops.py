@@ -565,20 +565,46 @@ def _larft_cpu(V: torch.Tensor, tau: torch.Tensor) -> torch.Tensor:
     return T
 
 
+def sum_partials(src: torch.Tensor, stride: int, S: int, L: int, dst: torch.Tensor):
+    """dst[:L] = sum over s < S of src[s*stride : s*stride + L] (split-K partials)."""
+    if _is_gpu(dst):
+        rc = _lib.load().dpl_sum_partials(_lib.prec_code(dst.dtype), src.data_ptr(), int(stride), int(S), int(L),
+                                          dst.data_ptr(), _lib.stream_ptr())
+        _lib.check(rc, "sum_partials")
+        return
+    torch.sum(torch.as_strided(src, (S, L), (stride, 1), 0), 0, out=dst[:L])
+
+
 def qr_panel(P: torch.Tensor, ldp: int, M: int, nc: int, kf: int, V: torch.Tensor, ldv: int, Tm: torch.Tensor,
-             ldt: int, ws: torch.Tensor, info: torch.Tensor):
+             ldt: int, ws: torch.Tensor, info: torch.Tensor, rbl: int = 0, rstride: int = 0, poff: int = 0):
     """Householder QR of the column-major M x nc panel P (ld ldp), first kf columns (real precisions).
 
     P := R (upper) + V (strictly lower) with the remaining nc - kf columns updated by Q^T;
     V := the kf reflectors explicitly (unit diagonal, zeros above); Tm(0:kf, 0:kf) := the
     compact-WY T (upper part; the strictly lower part is not written).  GPU: one persistent
-    launch (csrc/kernels/qr_panel.hip); CPU: LAPACK geqrf through torch + dlarft."""
+    launch (csrc/kernels/qr_panel.hip); CPU: LAPACK geqrf through torch + dlarft.
+    The panel starts at element poff of P; 0 < rbl < M: its rows come in blocks of rbl rows,
+    rstride elements apart (a column of tiles in TILE storage, addressed in place, ldp = mb)."""
     if kf <= 0:
         return
     if _is_gpu(P):
-        rc = _lib.load().dpl_qr_panel(_lib.prec_code(P.dtype), P.data_ptr(), ldp, M, nc, kf, V.data_ptr(), ldv,
-                                      Tm.data_ptr(), ldt, ws.data_ptr(), info.data_ptr(), _lib.stream_ptr())
+        rc = _lib.load().dpl_qr_panel(_lib.prec_code(P.dtype), P.data_ptr() + poff * P.element_size(), ldp, int(rbl),
+                                      int(rstride), M, nc, kf, V.data_ptr(), ldv, Tm.data_ptr(), ldt, ws.data_ptr(),
+                                      info.data_ptr(), _lib.stream_ptr())
         _lib.check(rc, "qr_panel")
+        return
+    if 0 < rbl < M or poff:
+        if not 0 < rbl < M:
+            rbl, rstride = M, 0
+        blocks = [torch.as_strided(P, (min(rbl, M - r0), nc), (1, ldp), poff + (r0 // rbl) * rstride)
+                  for r0 in range(0, M, rbl)]
+        tmp = torch.cat(blocks, 0).T.contiguous().view(-1)   # column-major M x nc
+        qr_panel(tmp, M, M, nc, kf, V, ldv, Tm, ldt, ws, info)
+        res = torch.as_strided(tmp, (M, nc), (1, M), 0)
+        r0 = 0
+        for blk in blocks:
+            blk.copy_(res[r0:r0 + blk.shape[0]])
+            r0 += blk.shape[0]
         return
     A = torch.as_strided(P, (M, nc), (1, ldp), 0)
     a, tau = torch.geqrf(A[:, :kf].clone())

@@ -411,12 +411,13 @@ def test_qr_panel_op_cpu(M, nc, kf):
         assert rel_err(ref[:, kf:], P[:, kf:]) < 1e-13
 
 
-@pytest.mark.parametrize("M,N,NB,IB,tree", [(96, 64, 16, 4, None), (90, 90, 16, 8, None), (100, 48, 16, 4, (1, 1, 2, 1)),
-                                            (100, 48, 16, 4, (0, 3, 3, 1)), (64, 96, 16, 4, None)])
-def test_qr_panel_engine_cpu(ctx, M, N, NB, IB, tree):
+@pytest.mark.parametrize("M,N,NB,IB,tree,st", [(96, 64, 16, 4, None, "tile"), (90, 90, 16, 8, None, "tile"),
+                                               (100, 48, 16, 4, (1, 1, 2, 1), "tile"), (100, 48, 16, 4, (0, 3, 3, 1), "tile"),
+                                               (64, 96, 16, 4, None, "tile"), (90, 70, 16, 4, None, "lapack")])
+def test_qr_panel_engine_cpu(ctx, M, N, NB, IB, tree, st):
     """geqrf / geqrf_param through the stacked-domain engine: factors, Q and its applications."""
     dt = torch.float64
-    A = _mk(ctx, dt, M, N, NB, 5)
+    A = _mk(ctx, dt, M, N, NB, 5, storage=st)
     a = _dense(A)
     TS, TT = _T(ctx, A, IB), _T(ctx, A, IB)
     tr = dp.hqr_init(dp.dplasmaNoTrans, A, *tree) if tree else None
