@@ -84,11 +84,14 @@ class Taskpool:
             else:
                 self._run_gpu_py(ctx)
         else:
+            from ..utils import trace
             for t in self.tasks:
-                t.fn()
+                with trace.span(ctx, t.name, t.stream, gpu=False):
+                    t.fn()
         self._t_run = t0
 
     def _run_gpu_py(self, ctx):
+        from ..utils import trace
         cur = torch.cuda.current_stream(ctx.device)
         start = torch.cuda.Event()
         start.record(cur)
@@ -101,7 +104,7 @@ class Taskpool:
             for d in t.deps:
                 if self.tasks[d].stream != t.stream:
                     s.wait_event(events[d])
-            with torch.cuda.stream(s):
+            with torch.cuda.stream(s), trace.span(ctx, t.name, t.stream, s):
                 t.fn()
             if t.needs_event:
                 ev = torch.cuda.Event()

@@ -9,6 +9,7 @@ import pytest
 import torch
 
 import dplasma_amd as dp
+from dplasma_amd.models import qr_panel
 from helpers import run_distributed
 
 
@@ -26,23 +27,27 @@ def _qr(ctx, N=48, NB=16):
 
 def test_trace_records_launches(ctx, tmp_path):
     tr = dp.profiling_start(ctx)
-    _qr(ctx)
+    _qr(ctx)                      # stacked-domain engine: panel / next / rest tasks
+    with qr_panel.engine("tile"):
+        _qr(ctx)                  # tile DAG: one launch per kernel kind and level
     tr.save_info("N", 48)
     dp.profiling_stop(ctx, str(tmp_path / "t.json"))
     d = json.load(open(tmp_path / "t.json"))
     names = {e["name"] for e in d["traceEvents"] if e.get("ph") == "X"}
     assert "geqrf" in names
+    assert any("qr_panel" in n for n in names) and any("qr_rest" in n for n in names)
     assert any("geqrt" in n for n in names) and any("tsmqr" in n for n in names)
     assert d["otherData"]["N"] == 48
     s = tr.summary()
-    assert s["geqrf"]["count"] == 1 and s["geqrf"]["total_us"] > 0
+    assert s["geqrf"]["count"] >= 2 and s["geqrf"]["total_us"] > 0
     assert ctx.profiling is None
 
 
 def test_dot_dump(ctx, tmp_path):
     p = str(tmp_path / "g.dot")
     dp.dot_start(ctx, p)
-    _qr(ctx)
+    with qr_panel.engine("tile"):   # DOT dumps are of tile DAGs
+        _qr(ctx)
     dp.dot_stop(ctx)
     txt = open(p).read()
     assert txt.startswith('digraph "geqrf"') and "->" in txt and "geqrt" in txt
