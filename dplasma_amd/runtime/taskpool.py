@@ -79,14 +79,14 @@ class Taskpool:
         t0 = time.perf_counter()
         if ctx is not None and ctx.is_gpu:
             from . import engine
-            if engine.available():
+            if engine.available() and getattr(ctx, "profiling", None) is None:
                 engine.run_gpu(self, ctx)
             else:
                 self._run_gpu_py(ctx)
         else:
             from ..utils import trace
             for t in self.tasks:
-                with trace.span(ctx, t.name, t.stream, gpu=False):
+                with trace.span(ctx, t.name, "task", gpu=False):
                     t.fn()
         self._t_run = t0
 
@@ -104,7 +104,7 @@ class Taskpool:
             for d in t.deps:
                 if self.tasks[d].stream != t.stream:
                     s.wait_event(events[d])
-            with torch.cuda.stream(s), trace.span(ctx, t.name, t.stream, s):
+            with torch.cuda.stream(s), trace.span(ctx, t.name, "task", s):
                 t.fn()
             if t.needs_event:
                 ev = torch.cuda.Event()

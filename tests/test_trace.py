@@ -103,6 +103,6 @@ def test_gpu_trace_streams(tmp_path):
     dp.profiling_stop(g, str(tmp_path / "g.json"))
     d = json.load(open(tmp_path / "g.json"))
     ev = [e for e in d["traceEvents"] if e.get("ph") == "X"]
-    tracks = {e["tid"] for e in ev if e["cat"] == "dag"}
+    tracks = {e["tid"] for e in ev if e["cat"] in ("dag", "task")}
     assert {"panel", "update"} <= tracks
     assert all(e["dur"] >= 0 for e in ev)
