@@ -1,4 +1,4 @@
-"""Stacked-domain Householder QR: the MI355X engine of geqrf / geqrf_param on a 1 x 1 grid.
+"""Stacked-domain Householder QR: the MI355X engine of geqrf / geqrf_param on 1 x Q grids.
 
 Reference: ``src/zgeqrf.jdf`` (flat TS tree: zgeqrt(k) :98, zunmqr(k,n) :198, ztsqrt(k,m) :314,
 ztsmqr(k,m,n) :443), ``src/zgeqrf_param.jdf`` (trees: TS domains + TT kills), ``src/zunmqr_*.jdf``,
@@ -26,6 +26,10 @@ Storage format (what unmqr / ungqr / geqrs / gels of this package consume; real 
   * per panel, all domains come first, then the TT kills in plan order.
 The full T of a reflector set is rebuilt from V and its diagonal blocks when Q is applied.
 
+1 x Q grids (single-domain plans): the owner of panel column k factors it and broadcasts V and T
+along the process row (RCCL); every rank applies them to its own columns.  For Q-side applications
+from the right the partial W = C V is all-reduced along the row.
+
 Lookahead (single-domain trees, e.g. the flat tree or HQR with one domain per process row):
 the panel stream factors panel k+1 right after applying Q_k^T to column k+1, while the update
 stream applies Q_k^T to columns k+2.. (the reference's priority-driven lookahead, done with
@@ -42,6 +46,7 @@ import torch
 from ..constants import dplasmaConjTrans, dplasmaLeft, dplasmaNoTrans, dplasmaTrans
 from ..ops import tile_ops as ops
 from ..ops.batch import GemmBatch, TileBatch
+from ..parallel import comm
 from ..runtime.taskpool import Taskpool
 from ..utils.flops import flops
 from . import qrtree
@@ -91,12 +96,16 @@ def usable(A, tree=None) -> bool:
         return False
     if A.dtype not in (torch.float32, torch.float64):
         return False
-    if A.grid.P != 1 or A.grid.Q != 1 or A.mb != A.nb or A.nb > ops.QR_PANEL_MAXW:
+    if A.grid.P != 1 or A.grid.kq != 1 or A.mb != A.nb or A.nb > ops.QR_PANEL_MAXW:
         return False
     if A.device.type == "cuda" and A.m > ops.qr_panel_max_rows(A.device):
         return False
     if tree is not None:
-        if any(step_plan(tree, k) is None for k in range(min(A.mt, A.nt))):
+        plans = [step_plan(tree, k) for k in range(min(A.mt, A.nt))]
+        if any(p is None for p in plans):
+            return False
+        # 1 x Q grids: one domain per panel and no TT kills (the panel column is one rank's)
+        if A.grid.Q > 1 and any(len(d) != 1 or t for d, t in plans):
             return False
     return True
 
@@ -138,7 +147,7 @@ class _Left:
         self.g1, self.g2, self.g3 = g1.finalize(), g2.finalize(), g3.finalize()
         self.empty = not cols or not rows
 
-    def run(self, C, V, ldv, Tm, ldt, Wp, W, W2, qt: bool):
+    def run(self, C, V, ldv, Tm, ldt, Wp, W, W2, qt: bool, group=None):
         if self.empty:
             return
         kf, L = self.kf, self.wlen
@@ -155,7 +164,7 @@ class _Left:
 class _Right:
     """C(rows, cols) := C op(Q) (cols = the reflector rows): W = C V, W' = W op(T), C -= W' V^T."""
 
-    def __init__(self, C, crows, vcols, voff, kf, target_wg=512):
+    def __init__(self, C, crows, vcols, voff, kf, target_wg=512, split=True):
         self.kf = kf
         roff, c = {}, 0
         for i in crows:
@@ -165,7 +174,7 @@ class _Right:
         self.wlen = self.ldw * kf
         ncol = len(vcols)
         wg = max(1, len(crows) * max(1, kf // 128) * max(1, C.mb // 128))
-        self.S = S = max(1, min(ncol, -(-target_wg // wg)))
+        self.S = S = max(1, min(ncol, -(-target_wg // wg))) if split else 1
         g1, g2, g3 = GemmBatch(), GemmBatch(), GemmBatch()
         for s, grp in enumerate(np.array_split(np.arange(ncol), S)):
             for i in crows:
@@ -177,11 +186,24 @@ class _Right:
                 g3.add(C.offset(i, n), C.tile_rows(i), C.tile_cols(n), [(roff[i], voff[j], kf)])
         self.g1, self.g2, self.g3 = g1.finalize(), g2.finalize(), g3.finalize()
         self.empty = not crows or not vcols
+        self.nocols = not vcols
 
-    def run(self, C, V, ldv, Tm, ldt, Wp, W, W2, qt: bool):
+    def run(self, C, V, ldv, Tm, ldt, Wp, W, W2, qt: bool, group=None):
+        kf, L, ldw = self.kf, self.wlen, self.ldw
+        if group is not None:
+            # 1 x Q grid: the reflector rows are C's columns, spread over the process row
+            if self.nocols:
+                Wp[:L].zero_()
+            else:
+                ops.gemm(N_, N_, 1.0, C.data, C.ld, V, ldv, 0.0, Wp, ldw, self.g1)
+            comm.allreduce(Wp[:L], group=group)
+            if self.empty:
+                return
+            ops.gemm(N_, T_ if qt else N_, 1.0, Wp, ldw, Tm, ldt, 0.0, W2, ldw, self.g2)
+            ops.gemm(N_, T_, -1.0, W2, ldw, V, ldv, 1.0, C.data, C.ld, self.g3)
+            return
         if self.empty:
             return
-        kf, L, ldw = self.kf, self.wlen, self.ldw
         ops.gemm(N_, N_, 1.0, C.data, C.ld, V, ldv, 0.0, Wp, ldw, self.g1)
         if self.S > 1:
             ops.sum_partials(Wp, L, self.S, L, W)
@@ -240,6 +262,7 @@ class _Factor:
         dev, dt = A.device, A.dtype
         nb = A.nb
         self.kt = min(A.mt, A.nt)
+        self.dist = A.grid.Q > 1   # 1 x Q grid: the panel owner broadcasts V and T along the row
         self.plans = [step_plan(tree, k) for k in range(self.kt)]
         self.simple = all(len(d) == 1 and not t for d, t in self.plans)
         self.ldp = max(16, _rup(A.m, 16))
@@ -265,7 +288,10 @@ class _Factor:
             voff.append(c)
             c += A.tile_rows(r)
         M = c
-        e = {"rows": rows, "voff": voff, "M": M, "kb": kb, "kf": min(M, kb), "tt": tt, "ld": max(16, _rup(M, 16))}
+        e = {"rows": rows, "voff": voff, "M": M, "kb": kb, "kf": min(M, kb), "tt": tt, "ld": max(16, _rup(M, 16)),
+             "own": A.col_is_local(k), "root": A.grid.rank(0, A.grid.pcol(k + A.jt0)), "direct": None}
+        if not e["own"]:
+            return e
         g, back = TileBatch(), TileBatch()
         part = PART_UPPER if tt else PART_FULL
         for r, o in zip(rows, voff):
@@ -273,7 +299,6 @@ class _Factor:
             back.add(o, A.tile_rows(r), kb, b_off=A.offset(r, k))
         e["gather"], e["back"], e["part"] = g.finalize(), back.finalize(), part
         # a domain of consecutive tile rows is factored in place (no gather / scatter copies)
-        e["direct"] = None
         if not tt and list(rows) == list(range(rows[0], rows[0] + len(rows))):
             if A.storage == "tile" or A.ld == A.mb:
                 e["direct"] = (A.mb, A.mb, A.mb * A.nb, A.offset(rows[0], k))
@@ -285,12 +310,14 @@ class _Factor:
         A = self.A
         doms, tts = self.plans[k]
         out = []
-        cols = list(range(k + 1, A.nt))
+        cols = [n for n in range(k + 1, A.nt) if A.col_is_local(n)]
         for d in doms:
             e = self._entry(k, d, False)
             if self.simple:
-                e["next"] = _Left(A, d, e["voff"], e["kf"], cols[:1]) if cols else None
-                e["rest"] = _Left(A, d, e["voff"], e["kf"], cols[1:]) if len(cols) > 1 else None
+                nxt = [n for n in cols if n == k + 1]
+                rest = [n for n in cols if n != k + 1]
+                e["next"] = _Left(A, d, e["voff"], e["kf"], nxt) if nxt else None
+                e["rest"] = _Left(A, d, e["voff"], e["kf"], rest) if rest else None
             else:
                 e["upd"] = _Left(A, d, e["voff"], e["kf"], cols) if cols else None
             out.append(e)
@@ -305,6 +332,9 @@ class _Factor:
         A = self.A
         P, V, Tm = self.P[buf], self.V[buf], self.Tm[buf]
         ld, M, kb, kf = e["ld"], e["M"], e["kb"], e["kf"]
+        if not e["own"]:
+            self._bcast(e, V, Tm)
+            return
         if e["direct"] is not None:
             ldp, rbl, rstride, poff = e["direct"]
             ops.qr_panel(A.data, ldp, M, kb, kf, V, ld, Tm, A.nb, self.ws, self.info, rbl=rbl, rstride=rstride,
@@ -319,6 +349,12 @@ class _Factor:
             _store_T(Tm, A.nb, kf, self.TT, e["rows"][1], k)
         else:
             _store_T(Tm, A.nb, kf, self.TS, e["rows"][0], k)
+        self._bcast(e, V, Tm)
+
+    def _bcast(self, e, V, Tm):
+        if self.dist:
+            comm.bcast(V[: e["ld"] * e["kf"]], e["root"], self.ctx.row_group)
+            comm.bcast(Tm, e["root"], self.ctx.row_group)
 
     def apply(self, e, upd, buf, work):
         if upd is None:
@@ -372,7 +408,8 @@ class _Apply:
     """C := op(Q) C or C op(Q) with Q in the stacked-domain format (unmqr / ungqr)."""
 
     def __init__(self, ctx, side, trans, A, TS, TT, C, tree):
-        self.A, self.TS, self.TT, self.C = A, TS, TT, C
+        self.ctx, self.A, self.TS, self.TT, self.C = ctx, A, TS, TT, C
+        self.dist = A.grid.Q > 1
         dev, dt = A.device, A.dtype
         self.left = side == dplasmaLeft
         self.qt = trans in (dplasmaTrans, dplasmaConjTrans)
@@ -396,7 +433,16 @@ class _Apply:
             voff.append(c)
             c += A.tile_rows(r)
         M, kf = c, min(c, kb)
-        it = {"k": k, "tt": tt, "rows": rows, "M": M, "kf": kf}
+        it = {"k": k, "tt": tt, "rows": rows, "M": M, "kf": kf, "own": A.col_is_local(k),
+              "root": A.grid.rank(0, A.grid.pcol(k + A.jt0))}
+        if self.left:
+            it["upd"] = _Left(C, rows, voff, kf, [n for n in range(C.nt) if C.col_is_local(n)])
+        else:
+            loc = [j for j, r in enumerate(rows) if C.col_is_local(r)]
+            it["upd"] = _Right(C, list(range(C.mt)), [rows[j] for j in loc], [voff[j] for j in loc], kf,
+                               split=not self.dist)
+        if not it["own"]:
+            return it
         # V gather batches: copy part (dom head: strictly lower / victims: full; TT: upper of m) + unit diagonal
         cp, dg = TileBatch(), TileBatch()
         if tt:
@@ -411,24 +457,24 @@ class _Apply:
                 rest.add(A.offset(r, k), A.tile_rows(r), kf, b_off=o)
             it["cp"] = [(PART_SLOWER, head.finalize()), (PART_FULL, rest.finalize())]
         it["diag"] = dg.finalize()
-        if self.left:
-            cols = list(range(C.nt))
-            it["upd"] = _Left(C, rows, voff, kf, cols)
-        else:
-            it["upd"] = _Right(C, list(range(C.mt)), rows, voff, kf)
         return it
 
     def run_item(self, it):
         A = self.A
         V, ld, kf = self.V, self.ldv, it["kf"]
-        V[: ld * kf].zero_()
-        for part, b in it["cp"]:
-            if len(b):
-                ops.geadd(part, N_, 1.0, A.data, A.ld, 0.0, V, ld, b, copy=True)
-        ops.laset(PART_DIAG, 0.0, 1.0, V, ld, it["diag"])
-        Td, row = (self.TT, it["rows"][1]) if it["tt"] else (self.TS, it["rows"][0])
-        _rebuild_T(V, ld, it["M"], kf, Td, row, it["k"], self.Tm, A.nb)
-        it["upd"].run(self.C, V, ld, self.Tm, A.nb, *self.work, qt=self.qt)
+        if it["own"]:
+            V[: ld * kf].zero_()
+            for part, b in it["cp"]:
+                if len(b):
+                    ops.geadd(part, N_, 1.0, A.data, A.ld, 0.0, V, ld, b, copy=True)
+            ops.laset(PART_DIAG, 0.0, 1.0, V, ld, it["diag"])
+            Td, row = (self.TT, it["rows"][1]) if it["tt"] else (self.TS, it["rows"][0])
+            _rebuild_T(V, ld, it["M"], kf, Td, row, it["k"], self.Tm, A.nb)
+        if self.dist:
+            comm.bcast(V[: ld * kf], it["root"], self.ctx.row_group)
+            comm.bcast(self.Tm, it["root"], self.ctx.row_group)
+        it["upd"].run(self.C, V, ld, self.Tm, A.nb, *self.work, qt=self.qt,
+                      group=self.ctx.row_group if self.dist else None)
 
     def run(self):
         for it in self.items:

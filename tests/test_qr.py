@@ -176,7 +176,9 @@ def _qr_worker(rank, world, P, lq):
 @pytest.mark.parametrize("world,P,lq", [(2, 1, False), (2, 2, False), (4, 2, False), (3, 3, True), (4, 2, True)])
 def test_qr_distributed(world, P, lq):
     out = run_distributed(_qr_worker, world, P, lq)
-    with qr_panel.engine("tile"):  # single-process run of the same (tile) algorithm on the same data
+    # single-process run of the same algorithm on the same data: 1 x Q grids take the
+    # stacked-domain engine (real QR), P > 1 grids the tile algorithm
+    with qr_panel.engine("panel" if P == 1 else "tile"):
         r = _qr_worker(0, 1, 1, lq)
     for i in range(4):
         full = sum(out[k][i] for k in range(world))
@@ -463,3 +465,48 @@ def test_gpu_qr_panel_kernel(prec, M, nc, kf):
     tol = 1e-10 if prec == "d" else 2e-3
     for i, (x, y) in enumerate(zip(g, c)):
         assert rel_err(x, y) < tol, i
+
+
+def _qrp_worker(rank, world, P):
+    """Stacked-domain engine on a 1 x Q grid (flat and one-domain HQR trees)."""
+    import dplasma_amd as dp
+    ctx = dp.init(device="cpu", P=P)
+    dt = torch.float64
+    M, N, NB, IB = 72, 56, 8, 4
+    out = []
+    for use_tree in (False, True):
+        A = dp.block_cyclic(ctx, dt, NB, NB, M, N)
+        dp.plrnt(ctx, A, 3872)
+        TS = dp.block_cyclic(ctx, dt, IB, NB, A.mt * IB, A.nt * NB)
+        TT = dp.block_cyclic(ctx, dt, IB, NB, A.mt * IB, A.nt * NB)
+        tree = dp.hqr_init(dp.dplasmaNoTrans, A, 1, 1, A.mt, 1) if use_tree else None
+        assert qr_panel.usable(A, tree or dp.models.qrtree.FlatTree(A.mt, A.nt))
+        if use_tree:
+            dp.geqrf_param(ctx, tree, A, TS, TT)
+        else:
+            dp.geqrf(ctx, A, TS)
+        Q = dp.block_cyclic(ctx, dt, NB, NB, M, M)
+        C1 = dp.block_cyclic(ctx, dt, NB, NB, M, 20)
+        C2 = dp.block_cyclic(ctx, dt, NB, NB, 12, M)
+        dp.plrnt(ctx, C1, 5)
+        dp.plrnt(ctx, C2, 6)
+        if use_tree:
+            dp.ungqr_param(ctx, tree, A, TS, TT, Q)
+            dp.unmqr_param(ctx, dp.dplasmaLeft, dp.dplasmaTrans, tree, A, TS, TT, C1)
+            dp.unmqr_param(ctx, dp.dplasmaRight, dp.dplasmaNoTrans, tree, A, TS, TT, C2)
+        else:
+            dp.ungqr(ctx, A, TS, Q)
+            dp.unmqr(ctx, dp.dplasmaLeft, dp.dplasmaTrans, A, TS, C1)
+            dp.unmqr(ctx, dp.dplasmaRight, dp.dplasmaNoTrans, A, TS, C2)
+        out += [A.to_dense_local(), TS.to_dense_local(), Q.to_dense_local(), C1.to_dense_local(),
+                C2.to_dense_local()]
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_qr_panel_engine_1xq(world):
+    out = run_distributed(_qrp_worker, world, 1)
+    r = _qrp_worker(0, 1, 1)
+    for i in range(len(r)):
+        full = sum(out[k][i] for k in range(world))
+        assert rel_err(full, r[i]) < 1e-12, i
