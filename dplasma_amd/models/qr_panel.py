@@ -121,31 +121,46 @@ def _sequence(A, tree):
 
 
 # ----------------------------------------------------------------------------- batched updates
+def _offsets(C, rows, cols):
+    """off[i, j] = C.offset(rows[i], cols[j]) (tile offsets are additive in row and column)."""
+    rows, cols = list(rows), list(cols)
+    R = np.array([C.offset(r, cols[0]) for r in rows], dtype=np.int64)
+    Cc = np.array([C.offset(rows[0], n) for n in cols], dtype=np.int64) - R[0]
+    return R[:, None] + Cc[None, :]
+
+
 class _Left:
     """C(rows, cols) := op(Q)^T-style block reflector application from the left:
-    W = V^T C (split over S row groups, partials summed), W' = op(T) W, C -= V W'."""
+    W = V^T C (split over S row groups, partials summed), W' = op(T) W, C -= V W'.
+    Batches are built with whole-array numpy operations (millions of tiles at 64k)."""
 
     def __init__(self, C, rows, voff, kf, cols, target_wg=512):
         self.kf = kf
-        woff, c = {}, 0
-        for n in cols:
-            woff[n] = c * kf
-            c += C.tile_cols(n)
-        self.wlen = c * kf
-        nrow = len(rows)
-        wg = max(1, len(cols) * max(1, kf // 128) * max(1, C.nb // 128))
+        self.empty = not cols or not rows
+        self.S, self.wlen = 1, 0
+        if self.empty:
+            return
+        rows, cols = list(rows), list(cols)
+        voff = np.asarray(voff, dtype=np.int64)
+        hr = np.array([C.tile_rows(r) for r in rows], dtype=np.int64)
+        wn = np.array([C.tile_cols(n) for n in cols], dtype=np.int64)
+        woff = kf * np.concatenate([[0], np.cumsum(wn)[:-1]])
+        self.wlen = int(wn.sum()) * kf
+        nrow, ncol = len(rows), len(cols)
+        off = _offsets(C, rows, cols)
+        wg = max(1, ncol * max(1, kf // 128) * max(1, C.nb // 128))
         self.S = S = max(1, min(nrow, -(-target_wg // wg)))
         g1, g2, g3 = GemmBatch(), GemmBatch(), GemmBatch()
-        for s, grp in enumerate(np.array_split(np.arange(nrow), S)):
-            for n in cols:
-                g1.add(s * self.wlen + woff[n], kf, C.tile_cols(n),
-                       [(voff[i], C.offset(rows[i], n), C.tile_rows(rows[i])) for i in grp])
-        for n in cols:
-            g2.add(woff[n], kf, C.tile_cols(n), [(0, woff[n], kf)])
-            for i, r in enumerate(rows):
-                g3.add(C.offset(r, n), C.tile_rows(r), C.tile_cols(n), [(voff[i], woff[n], kf)])
+        grps = np.array_split(np.arange(nrow), S)
+        g1.add_arrays((np.arange(S, dtype=np.int64)[:, None] * self.wlen + woff[None, :]).ravel(), kf, np.tile(wn, S),
+                      np.repeat([len(g) for g in grps], ncol),
+                      np.concatenate([np.tile(voff[g], ncol) for g in grps]),
+                      np.concatenate([off[g, :].T.ravel() for g in grps]),
+                      np.concatenate([np.tile(hr[g], ncol) for g in grps]))
+        g2.add_arrays(woff, kf, wn, 1, 0, woff, kf)
+        g3.add_arrays(off.T.ravel(), np.tile(hr, ncol), np.repeat(wn, nrow), 1, np.tile(voff, ncol),
+                      np.repeat(woff, nrow), kf)
         self.g1, self.g2, self.g3 = g1.finalize(), g2.finalize(), g3.finalize()
-        self.empty = not cols or not rows
 
     def run(self, C, V, ldv, Tm, ldt, Wp, W, W2, qt: bool, group=None):
         if self.empty:
@@ -166,27 +181,33 @@ class _Right:
 
     def __init__(self, C, crows, vcols, voff, kf, target_wg=512, split=True):
         self.kf = kf
-        roff, c = {}, 0
-        for i in crows:
-            roff[i] = c
-            c += C.tile_rows(i)
-        self.ldw = max(1, _rup(c, 16))
+        crows, vcols = list(crows), list(vcols)
+        hc = np.array([C.tile_rows(i) for i in crows], dtype=np.int64)
+        roff = np.concatenate([[0], np.cumsum(hc)[:-1]]).astype(np.int64)
+        self.ldw = max(1, _rup(int(hc.sum()), 16))
         self.wlen = self.ldw * kf
-        ncol = len(vcols)
-        wg = max(1, len(crows) * max(1, kf // 128) * max(1, C.mb // 128))
-        self.S = S = max(1, min(ncol, -(-target_wg // wg))) if split else 1
-        g1, g2, g3 = GemmBatch(), GemmBatch(), GemmBatch()
-        for s, grp in enumerate(np.array_split(np.arange(ncol), S)):
-            for i in crows:
-                g1.add(s * self.wlen + roff[i], C.tile_rows(i), kf,
-                       [(C.offset(i, vcols[j]), voff[j], C.tile_cols(vcols[j])) for j in grp])
-        for i in crows:
-            g2.add(roff[i], C.tile_rows(i), kf, [(roff[i], 0, kf)])
-            for j, n in enumerate(vcols):
-                g3.add(C.offset(i, n), C.tile_rows(i), C.tile_cols(n), [(roff[i], voff[j], kf)])
-        self.g1, self.g2, self.g3 = g1.finalize(), g2.finalize(), g3.finalize()
         self.empty = not crows or not vcols
         self.nocols = not vcols
+        self.S = 1
+        if self.empty:
+            return
+        voff = np.asarray(voff, dtype=np.int64)
+        wc = np.array([C.tile_cols(n) for n in vcols], dtype=np.int64)
+        ncol, nrow = len(vcols), len(crows)
+        off = _offsets(C, crows, vcols)
+        wg = max(1, nrow * max(1, kf // 128) * max(1, C.mb // 128))
+        self.S = S = max(1, min(ncol, -(-target_wg // wg))) if split else 1
+        g1, g2, g3 = GemmBatch(), GemmBatch(), GemmBatch()
+        grps = np.array_split(np.arange(ncol), S)
+        g1.add_arrays((np.arange(S, dtype=np.int64)[:, None] * self.wlen + roff[None, :]).ravel(), np.tile(hc, S), kf,
+                      np.repeat([len(g) for g in grps], nrow),
+                      np.concatenate([off[:, g].ravel() for g in grps]),
+                      np.concatenate([np.tile(voff[g], nrow) for g in grps]),
+                      np.concatenate([np.tile(wc[g], nrow) for g in grps]))
+        g2.add_arrays(roff, hc, kf, 1, roff, 0, kf)
+        g3.add_arrays(off.ravel(), np.repeat(hc, ncol), np.tile(wc, nrow), 1, np.repeat(roff, ncol),
+                      np.tile(voff, nrow), kf)
+        self.g1, self.g2, self.g3 = g1.finalize(), g2.finalize(), g3.finalize()
 
     def run(self, C, V, ldv, Tm, ldt, Wp, W, W2, qt: bool, group=None):
         kf, L, ldw = self.kf, self.wlen, self.ldw

@@ -78,8 +78,44 @@ class GemmBatch(_Uploadable):
         self.max_n = max(self.max_n, n)
         return self
 
+    def add_arrays(self, c_off, m, n, kt_cnt, a_off, b_off, k, mask: int = MASK_FULL):
+        """Vectorised add: items (c_off[i], m[i], n[i]) with kt_cnt[i] consecutive K-pairs taken from
+        (a_off, b_off, k) in item order -- one numpy pass for millions of items."""
+        c_off, m, n, kt_cnt = (np.asarray(x, dtype=np.int64).ravel() for x in (c_off, m, n, kt_cnt))
+        a_off, b_off, k = (np.asarray(x, dtype=np.int64).ravel() for x in (a_off, b_off, k))
+        ni = len(c_off)
+        if ni == 0:
+            return self
+        m, n, kt_cnt = (np.broadcast_to(x, (ni,)) for x in (m, n, kt_cnt))
+        nk = int(kt_cnt.sum())
+        k = np.broadcast_to(k, (nk,))
+        beg = len(self._kps) + sum(len(c) for c in getattr(self, "_kp_chunks", [])) + np.concatenate(
+            [[0], np.cumsum(kt_cnt)[:-1]])
+        items = np.zeros(ni, dtype=GEMM_ITEM)
+        items["c_off"], items["kt_beg"], items["kt_cnt"] = c_off, beg, kt_cnt
+        items["m"], items["n"], items["flags"] = m, n, mask
+        kps = np.zeros(nk, dtype=KPAIR)
+        kps["a_off"], kps["b_off"], kps["k"] = a_off, b_off, k
+        if not hasattr(self, "_item_chunks"):
+            self._item_chunks, self._kp_chunks = [], []
+        self._item_chunks.append(items)
+        self._kp_chunks.append(kps)
+        if (a_off % 2).any() or (b_off % 2).any() or (c_off % 2).any():
+            self.vec_ok = False
+        self._align |= int(np.bitwise_or.reduce(np.concatenate([a_off, b_off, c_off])))
+        if (k % 16).any() or (m % 128).any() or (n % 128).any():
+            self.full = False
+        # flops: sum over items of m*n*sum(k of its pairs)
+        ksum = np.add.reduceat(k, np.concatenate([[0], np.cumsum(kt_cnt)[:-1]])) if nk else np.zeros(ni)
+        self.flops_mnk += float((m.astype(np.float64) * n * ksum).sum())
+        self.max_m = max(self.max_m, int(m.max()))
+        self.max_n = max(self.max_n, int(n.max()))
+        return self
+
     def __len__(self):
-        return len(self._items) if self.items is None else len(self.items)
+        if self.items is not None:
+            return len(self.items)
+        return len(self._items) + sum(len(c) for c in getattr(self, "_item_chunks", []))
 
     def aligned(self, elems: int) -> bool:
         """All A/B/C offsets are multiples of ``elems`` elements."""
@@ -87,8 +123,17 @@ class GemmBatch(_Uploadable):
 
     def finalize(self):
         if self.items is None:
-            self.items = np.array(self._items, dtype=GEMM_ITEM)
-            self.kpairs = np.array(self._kps if self._kps else [(0, 0, 0, 0)], dtype=KPAIR)
+            chunks_i = getattr(self, "_item_chunks", [])
+            chunks_k = getattr(self, "_kp_chunks", [])
+            if chunks_i:
+                if self._items:
+                    raise RuntimeError("GemmBatch: mixing add() after add_arrays() is not supported")
+                self.items = np.concatenate(chunks_i)
+                self.kpairs = np.concatenate(chunks_k) if sum(len(c) for c in chunks_k) else np.zeros(1, dtype=KPAIR)
+                self._item_chunks = self._kp_chunks = []
+            else:
+                self.items = np.array(self._items, dtype=GEMM_ITEM)
+                self.kpairs = np.array(self._kps if self._kps else [(0, 0, 0, 0)], dtype=KPAIR)
             self._items = self._kps = None
         return self
 
