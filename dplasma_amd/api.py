@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import functools
 
-from .constants import DTYPE_PREC
+from .constants import DTYPE_PREC, dplasmaLeft, dplasmaNoTrans, dplasmaNonUnit, dplasmaUpper
 from .models import aux as _aux
 from .models import blas3 as _blas3
 from .models import cholesky as _chol
@@ -230,3 +230,46 @@ def _setrecursive(tp, hnb):
 
 for _op in ("potrf", "geqrf"):
     register_op(_op + "_setrecursive", _setrecursive)
+
+
+# Recursive-hint and synchronous variants of dplasma_z.h:68-83 (zpotrf_rec, zgeqrf_rec, zpoinv_sync,
+# zgetrs_incpiv) and the per-precision band -> tridiagonal bulge chase (zhbrdt).
+def potrf_rec(ctx, uplo, A, hmb):
+    """dplasma_zpotrf_rec: Cholesky with the recursive-subtask hint (see _setrecursive)."""
+    from .models import potrf as _pf
+    tp = _pf.potrf_New(ctx, uplo, A)
+    _setrecursive(tp, hmb)
+    return tp.execute(ctx)
+
+
+def geqrf_rec(ctx, A, T, hnb):
+    """dplasma_zgeqrf_rec: QR with the recursive-subtask hint (see _setrecursive)."""
+    tp = _qr.geqrf_New(ctx, A, T)
+    _setrecursive(tp, hnb)
+    tp.execute(ctx)
+    return 0
+
+
+def poinv_sync(ctx, uplo, A):
+    """dplasma_zpoinv_sync: A := inv(A) as three blocking steps (potrf, trtri, lauum)."""
+    from .models import potrf as _pf
+    info = _pf.potrf(ctx, uplo, A)
+    if info:
+        return info
+    _chol.trtri(ctx, uplo, dplasmaNonUnit, A)
+    _chol.lauum(ctx, uplo, A)
+    return 0
+
+
+def getrs_incpiv(ctx, trans, A, L, IPIV, B):
+    """dplasma_zgetrs_incpiv: solve after getrf_incpiv (NoTrans only, as in the reference)."""
+    if trans != dplasmaNoTrans:
+        raise ValueError("getrs_incpiv: only trans = NoTrans is supported (as in the reference)")
+    _lui.trsmpl_incpiv(ctx, A, L, IPIV, B)
+    _b3.trsm(ctx, dplasmaLeft, dplasmaUpper, dplasmaNoTrans, dplasmaNonUnit, 1.0, A, B)
+    return 0
+
+
+for _n, _f in (("potrf_rec", potrf_rec), ("geqrf_rec", geqrf_rec), ("poinv_sync", poinv_sync),
+               ("getrs_incpiv", getrs_incpiv), ("hbrdt", _eig.hbrdt)):
+    register_op(_n, _f)

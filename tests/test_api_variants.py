@@ -1,0 +1,65 @@
+"""Recursive-hint / synchronous entry points of dplasma_z.h:68-83 (zpotrf_rec, zgeqrf_rec,
+zpoinv_sync, zgetrs_incpiv) against their plain counterparts."""
+import pytest
+import torch
+
+import dplasma_amd as dp
+from helpers import rel_err
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return dp.init(device="cpu")
+
+
+def _spd(ctx, N, NB, seed=7):
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+    dp.plghe(ctx, float(N), dp.dplasmaLower, A, seed)
+    return A
+
+
+def test_potrf_rec_matches_potrf(ctx):
+    A, B = _spd(ctx, 60, 16), _spd(ctx, 60, 16)
+    assert dp.dpotrf_rec(ctx, dp.dplasmaLower, A, 4) == 0
+    assert dp.dpotrf(ctx, dp.dplasmaLower, B) == 0
+    assert rel_err(torch.tril(A.to_dense_local()), torch.tril(B.to_dense_local())) < 1e-14
+
+
+def test_geqrf_rec(ctx):
+    A = dp.block_cyclic(ctx, torch.float64, 16, 16, 64, 48)
+    dp.plrnt(ctx, A, 3)
+    a = A.to_dense_local().clone()
+    T = dp.block_cyclic(ctx, torch.float64, 4, 16, A.mt * 4, 48)
+    assert dp.dgeqrf_rec(ctx, A, T, 2) == 0
+    Q = dp.block_cyclic(ctx, torch.float64, 16, 16, 64, 48)
+    dp.dungqr(ctx, A, T, Q)
+    q = Q.to_dense_local()
+    assert rel_err(q @ torch.triu(A.to_dense_local()[:48]), a) < 1e-13
+
+
+def test_poinv_sync(ctx):
+    N = 48
+    A = _spd(ctx, N, 16)
+    a = A.to_dense_local().clone()
+    a = torch.tril(a) + torch.tril(a, -1).T
+    assert dp.dpoinv_sync(ctx, dp.dplasmaLower, A) == 0
+    inv = torch.tril(A.to_dense_local())
+    inv = inv + torch.tril(inv, -1).T
+    assert rel_err(inv @ a, torch.eye(N, dtype=torch.float64)) < 1e-12
+
+
+def test_getrs_incpiv(ctx):
+    N, NB, IB = 64, 16, 4
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+    dp.plrnt(ctx, A, 3)
+    a = A.to_dense_local().clone()
+    B = dp.block_cyclic(ctx, torch.float64, NB, NB, N, 3)
+    dp.plrnt(ctx, B, 4)
+    b = B.to_dense_local().clone()
+    L = dp.incpiv_L_descriptor(ctx, A, IB)
+    IP = dp.incpiv_ipiv_descriptor(ctx, A)
+    assert dp.dgetrf_incpiv(ctx, A, L, IP) == 0
+    assert dp.dgetrs_incpiv(ctx, dp.dplasmaNoTrans, A, L, IP, B) == 0
+    assert rel_err(a @ B.to_dense_local(), b) < 1e-12
+    with pytest.raises(ValueError):
+        dp.dgetrs_incpiv(ctx, dp.dplasmaTrans, A, L, IP, B)
