@@ -50,6 +50,12 @@ class _Panel:
 
 POTRF_DEFER = 4            # panels aggregated per deferred trailing update (k = 4*NB)
 POTRF_DEFER_MIN_TILES = 24 # below this many trailing tile-columns: plain look-ahead-1 (D = 1)
+# Diagonal-tile kernel: "single" = one-workgroup left-looking kernel, "blocked" = 128-wide
+# right-looking steps over several workgroups.  Measured on MI355X (profiles/r1_potrf_tile_kernels.txt):
+# 577 vs 625 us for a 512 tile in isolation, but DPOTRF 32k (the per-GPU share of 64k on 8 GPUs)
+# 53.0 vs 56.7 TF/s -- its extra launches contend with the bulk update -- so "single" everywhere;
+# "auto" = blocked when distributed.
+POTRF_TILE = "single"
 
 
 def _defer_depth(nt_left: int, D: int, min_tiles: int) -> int:
@@ -90,6 +96,11 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
         defer = int(os.environ.get("DPLASMA_POTRF_DEFER", POTRF_DEFER))
     D = max(1, int(defer))
     min_tiles = int(os.environ.get("DPLASMA_POTRF_DEFER_MIN_TILES", POTRF_DEFER_MIN_TILES))
+    tile_kind = os.environ.get("DPLASMA_POTRF_TILE", POTRF_TILE)
+    if tile_kind not in ("auto", "single", "blocked"):
+        raise ValueError(f"DPLASMA_POTRF_TILE={tile_kind!r}: expected auto, single or blocked")
+    potrf_diag = ops.potrf_tile_blocked if tile_kind == "blocked" or (tile_kind == "auto" and distributed) \
+        else ops.potrf_tile
 
     # block partition of the tile columns
     blocks = []
@@ -177,7 +188,7 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                 off = A.offset(*dk)
 
                 def f_potrf(off=off, kb=kb, k=k):
-                    ops.potrf_tile(uplo, A.data, off, kb, A.ld, info, k * A.mb)
+                    potrf_diag(uplo, A.data, off, kb, A.ld, info, k * A.mb)
                 t_potrf = tp.task(f"POTRF({k})", "panel", f_potrf, [gate], prio=3)
             # ---------------- local panel tiles (i > k) of my process row/col
             mine = [i for i in range(k + 1, nt) if in_panel_cross and owner_of_panel_line(i) == my_line]

@@ -92,3 +92,19 @@ def test_lantr(ctx):
     t = a.tril()
     t.fill_diagonal_(1.0)
     assert abs(dp.lantr(ctx, dp.dplasmaOneNorm, dp.dplasmaLower, dp.dplasmaUnit, A) - t.abs().sum(0).max().item()) < 1e-12
+
+
+@pytest.mark.parametrize("prec", list("dz"))
+@pytest.mark.parametrize("uplo", [dp.dplasmaLower, dp.dplasmaUpper])
+def test_potrf_blocked_tile_kernel(ctx, prec, uplo, monkeypatch):
+    """Diagonal tiles factored as 128-wide right-looking steps (POTRF + TRSM + masked GEMM)."""
+    monkeypatch.setenv("DPLASMA_POTRF_TILE", "blocked")
+    dt = DTYPES[prec]
+    N, NB = 700, 300   # tiles of 300 -> steps 128, 128, 44; ragged 100 last tile
+    A = dp.block_cyclic(ctx, dt, NB, NB, N, N)
+    dp.plghe(ctx, float(N), uplo, A, 3872)
+    A0 = A.like()
+    dp.lacpy(ctx, dp.dplasmaUpperLower, A, A0)
+    assert dp.potrf(ctx, uplo, A) == 0
+    ok, res = dp.check_potrf(ctx, uplo, A, A0)
+    assert ok, res

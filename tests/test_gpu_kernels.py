@@ -324,3 +324,20 @@ def test_piv_moves_device(gctx):
         n = int(c[0])
         outs.append(sorted(zip(d[:n].cpu().tolist(), s[:n].cpu().tolist())))
     assert outs[0] == outs[1]
+
+
+@pytest.mark.parametrize("prec", list("dz"))
+@pytest.mark.parametrize("uplo", [dp.dplasmaLower, dp.dplasmaUpper])
+@pytest.mark.parametrize("dims", [(1024, 512), (1100, 300)])
+def test_potrf_blocked_tile_kernel(gctx, prec, uplo, dims, monkeypatch):
+    """Diagonal tiles as 128-wide POTRF + TRSM + masked MFMA GEMM steps (distributed default)."""
+    monkeypatch.setenv("DPLASMA_POTRF_TILE", "blocked")
+    dt = DTYPES[prec]
+    N, NB = dims
+    A = dp.block_cyclic(gctx, dt, NB, NB, N, N)
+    dp.plghe(gctx, float(N), uplo, A, 3872)
+    A0 = A.like()
+    dp.lacpy(gctx, dp.dplasmaUpperLower, A, A0)
+    assert dp.potrf(gctx, uplo, A) == 0
+    ok, res = dp.check_potrf(gctx, uplo, A, A0)
+    assert ok, res
