@@ -129,6 +129,48 @@ def _versions_py(ops, modes):
     return out
 
 
+# Reference task costs (JDF ``SIMCOST``): zgeqrf.jdf:105,207,323,454 and zgeqrf_param.jdf:69,147,
+# 213,313 (TT kernels cost 2 / 6 instead of the TS 6 / 12).  Other kinds cost 1.
+REFERENCE_SIMCOST = {"geqrt": 4, "unmqr": 6, "tsqrt": 6, "ttqrt": 2, "tsmqr": 12, "ttmqr": 6}
+
+
+def _kernel_of(kind_name: str) -> str:
+    """Kernel family of a kind name: "qr0000_tsmqr_h_3_32" -> "tsmqr", "incpiv_getrf_d" -> "getrf"."""
+    parts = kind_name.split("_")
+    return parts[1] if len(parts) > 1 else kind_name
+
+
+def simulation_date(ops: np.ndarray, modes: np.ndarray, kid: np.ndarray, kind_names: Sequence[str],
+                    cost=None) -> float:
+    """Critical-path length of a tile DAG with per-kind task costs: the analogue of PaRSEC's
+    simulation date (``parsec_getsimulationdate``, printed by ``tests/testing_zgeqrf_systolic.c:139-150``,
+    ``testing_zgelqf.c:97-99``).  A task starts when the last writer of every tile it touches has
+    finished (dataflow: RAW and in-place RW chains; reads do not order later writes, as PTG data
+    versions do not) and ends ``cost`` later; the date is the latest end.  ``cost``: dict kernel
+    family -> cost (default ``REFERENCE_SIMCOST``) or callable(kind name) -> cost."""
+    table = REFERENCE_SIMCOST if cost is None else cost
+    if callable(table):
+        kc = [float(table(n)) for n in kind_names]
+    else:
+        kc = [float(table.get(_kernel_of(n), 1.0)) for n in kind_names]
+    done: Dict[int, float] = {}
+    end = 0.0
+    for t in range(len(ops)):
+        start = 0.0
+        for k, md in zip(ops[t], modes[t]):
+            if md:
+                d = done.get(int(k))
+                if d is not None and d > start:
+                    start = d
+        fin = start + kc[int(kid[t])]
+        for k, md in zip(ops[t], modes[t]):
+            if md & W:
+                done[int(k)] = fin
+        if fin > end:
+            end = fin
+    return end
+
+
 class TileDAG:
     """Program-order tile task graph (see module docstring)."""
 
@@ -262,6 +304,8 @@ class TileDAG:
                 pyargs_all[p:p + n] = pa
             p += n
         self._chunks = []
+        names = [K.name for K in self.kinds]
+        tp.simulation_date = lambda cost=None: simulation_date(ops, modes, kid, names, cost)
         rt = _lib_rt()
         # single process on a GPU: dataflow over two streams (critical path / bulk)
         multistream = world == 1 and ctx.device.type == "cuda" and rt is not None and MULTISTREAM

@@ -53,6 +53,9 @@ def _parse(argv):
     ap.add_argument("-g", "--gpus", type=int, default=-1, help="0: CPU only; default: GPU when present")
     ap.add_argument("--dot", default=None, help="write the DAG of DAG-based ops to this DOT file")
     ap.add_argument("--criteria", type=int, default=0, help="LU-QR criterion (include/dplasma/lu_qr.h)")
+    ap.add_argument("--sim", action="store_true",
+                    help="print the simulation date (critical path with the reference SIMCOST task costs) of "
+                         "tile-DAG algorithms, as PaRSEC simulation builds do")
     ap.add_argument("--trace", default=None, help="write a Chrome trace (all ranks) of the timed runs to this file")
     # remaining flags of tests/common.c:171-259
     ap.add_argument("-s", "--kp", "--SMB", type=int, default=1, dest="kp", help="k-cyclic repetition over rows")
@@ -132,6 +135,11 @@ class Harness:
             t0 = time.perf_counter()
             tp = build()
             t_enq = time.perf_counter() - t0
+            if getattr(self.a, "sim", False) and ctx.rank == 0:
+                sim = getattr(tp, "simulation_date", None)
+                print(f"{self.prec}{opname} simulation M= {self.a.M or self.a.N} N= {self.a.N} "
+                      f"NB= {self.a.NB or self.a.MB} : {sim() if sim else 'n/a (not a tile-DAG taskpool)'}",
+                      flush=True)
             ctx.barrier()
             ctx.sync()
             t1 = time.perf_counter()

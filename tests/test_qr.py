@@ -510,3 +510,26 @@ def test_qr_panel_engine_1xq(world):
     for i in range(len(r)):
         full = sum(out[k][i] for k in range(world))
         assert rel_err(full, r[i]) < 1e-12, i
+
+
+@pytest.mark.parametrize("mt,nt,flat,greedy", [(1, 1, 4, 4), (2, 1, 10, 6), (2, 2, 26, 20), (4, 4, 86, 64),
+                                               (16, 2, 196, 54)])
+def test_qr_simulation_date(mt, nt, flat, greedy):
+    """Critical path of the tile QR DAG with the reference SIMCOST weights (geqrt 4, unmqr 6,
+    tsqrt 6 / ttqrt 2, tsmqr 12 / ttmqr 6).  Small cases by hand: 2x1 flat = geqrt + tsqrt = 10,
+    greedy = max(geqrt, geqrt) + ttqrt = 6; 2x2 flat = geqrt, then unmqr || tsqrt, tsmqr, geqrt = 26."""
+    from dplasma_amd.models import qr_panel
+    ctx = dp.init(device="cpu")
+    NB, ib = 16, 4
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, mt * NB, nt * NB)
+    TS = dp.block_cyclic(ctx, torch.float64, ib, NB, mt * ib, nt * NB)
+    TT = TS.like()
+    with qr_panel.engine("tile"):
+        assert dp.geqrf_New(ctx, A, TS).simulation_date() == flat
+        tree = dp.hqr_init(dp.dplasmaNoTrans, A, 2, 0, 1, 1, False, False)   # greedy low-level tree
+        assert dp.geqrf_param_New(ctx, tree, A, TS, TT).simulation_date() == greedy
+        # the systolic tree with one domain reduces to the flat TS tree
+        assert dp.geqrf_param_New(ctx, dp.systolic_init(dp.dplasmaNoTrans, A, 1, 1), A, TS, TT) \
+            .simulation_date() == flat
+        # unit costs: the date is the DAG depth
+        assert dp.geqrf_New(ctx, A, TS).simulation_date(lambda name: 1) >= mt + nt - 1

@@ -46,3 +46,14 @@ def test_cli_kcyclic_multirank():
     r = _run("dpotrf -N 256 -t 32 -P 2 -s 2 -S 2 -x".split(), nproc=4)
     assert r.returncode == 0, r.stdout + r.stderr[-2000:]
     assert "CORRECT" in r.stdout and "SUSPICIOUS" not in r.stdout
+
+
+def test_cli_simulation_date():
+    """--sim prints the critical path of tile-DAG algorithms with the reference SIMCOST weights
+    (the reference prints parsec_getsimulationdate in simulation builds)."""
+    env_args = ["dgeqrf", "-M", "64", "-N", "64", "-t", "32", "-i", "8", "--sim"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT, DPLASMA_QR_ENGINE="tile")
+    r = subprocess.run([sys.executable, "-m", "dplasma_amd.testing", *env_args, "-g", "0"], capture_output=True,
+                       text=True, timeout=600, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr
+    assert "dgeqrf simulation M= 64 N= 64 NB= 32 : 26.0" in r.stdout, r.stdout
