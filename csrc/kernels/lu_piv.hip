@@ -135,10 +135,73 @@ __global__ __launch_bounds__(LUR) void k_lu_col(T* __restrict__ A, int ld, int m
   }
 }
 
-// Sequential interchanges rows i <-> ipiv[i], i in [i0, i1), on columns [ca, cb) of the panel.
+// Net effect of the sequential LAPACK interchanges r <-> pv[r - i0] (r in [i0, i0 + k), pv[.] >= r):
+// afterwards row dst[t] holds the former row src[t], t < return value (<= 2k moves).
+// Content-parallel replay: every involved row's CONTENT (rows i0..i0+k-1 and each distinct
+// pv[j] >= i0 + k) is tracked by its own thread through all k swaps -- k steps of a few VALU ops
+// per content with the swap pair read as an LDS broadcast, instead of one lane chasing the swaps
+// through LDS / global memory (a dependent-latency chain of ~k * 4 round trips).
+// NT threads, CPT contents per thread (2k <= NT * CPT); pv is in LDS; wtot = NT/64 LDS ints.
+template <int NT, int CPT>
+__device__ int net_moves(const int* pv, int i0, int k, int* dst, int* src, int* wtot) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int start[CPT], pos[CPT];
+  bool act[CPT];
+#pragma unroll
+  for (int u = 0; u < CPT; ++u) {
+    const int c = u * NT + tid;
+    start[u] = -1;
+    act[u] = false;
+    if (c < k) {
+      start[u] = i0 + c;
+      act[u] = true;
+    } else if (c < 2 * k) {
+      const int p = pv[c - k];
+      if (p >= i0 + k) { start[u] = p; act[u] = true; }
+    }
+    pos[u] = start[u];
+  }
+  for (int i = 0; i < k; ++i) {
+    const int p = pv[i], r = i0 + i;
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+      if (u * NT >= 2 * k) break;       // uniform: no contents left in this slot
+      const int j = u * NT + tid - k;   // content index among the pivot rows (>= 0 for those)
+      if (j > i && p == start[u]) act[u] = false;   // row p is already tracked by an earlier pivot
+      pos[u] = pos[u] == r ? p : (pos[u] == p ? r : pos[u]);
+    }
+  }
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int n = 0;
+#pragma unroll
+  for (int u = 0; u < CPT; ++u) {
+    if (u * NT >= 2 * k) break;
+    const bool mv = act[u] && pos[u] != start[u];
+    const unsigned long long m = __ballot(mv);
+    if (lane == 0) wtot[w] = __popcll(m);
+    __syncthreads();
+    int off = n, tot = 0;
+#pragma unroll
+    for (int v = 0; v < NT / 64; ++v) {
+      const int x = wtot[v];
+      off += v < w ? x : 0;
+      tot += x;
+    }
+    if (mv) {
+      const int t = off + __popcll(m & below);
+      dst[t] = pos[u];
+      src[t] = start[u];
+    }
+    n += tot;
+    __syncthreads();
+  }
+  return n;
+}
+
+// Sequential interchanges (fallback for i1 - i0 > 512): one thread per column replays the swaps.
 template <typename T>
-__global__ __launch_bounds__(64) void k_laswp_panel(T* __restrict__ A, int ld, int ca, int cb,
-                                                    const int* __restrict__ ipiv, int i0, int i1) {
+__global__ __launch_bounds__(64) void k_laswp_seq(T* __restrict__ A, int ld, int ca, int cb,
+                                                  const int* __restrict__ ipiv, int i0, int i1) {
   const int c = ca + blockIdx.x * 64 + threadIdx.x;
   if (c >= cb) return;
   T* col = A + (long long)c * ld;
@@ -152,46 +215,38 @@ __global__ __launch_bounds__(64) void k_laswp_panel(T* __restrict__ A, int ld, i
   }
 }
 
-// Net row moves of the sequential interchanges ipiv[0..kb) (panel-relative rows): after the
-// swaps, row dst[t] holds the former row src[t]; cnt[0] = number of moved rows (<= 2 kb).
-// One thread: the top kb rows in an LDS array, displaced rows below kb in an LDS hash table.
-#define HSZ 4096
-__global__ __launch_bounds__(64) void k_piv_moves(const int* __restrict__ ipiv, int kb, int* __restrict__ dst,
-                                                  int* __restrict__ src, int* __restrict__ cnt) {
-  __shared__ int top[1024], pv[1024];
-  __shared__ int hkey[HSZ], hval[HSZ];
-  const int tid = threadIdx.x;
-  for (int i = tid; i < kb; i += 64) { top[i] = i; pv[i] = ipiv[i]; }
-  for (int i = tid; i < HSZ; i += 64) hkey[i] = -1;
+// Interchanges rows i <-> ipiv[i], i in [i0, i1) (i1 - i0 <= 512), on columns [ca, cb) of the
+// panel: every workgroup derives the net moves in LDS (net_moves), then each wave moves its
+// columns -- all reads of a column land in LDS before its writes (no chain through memory).
+#define LSW_COLS 16
+template <typename T>
+__global__ __launch_bounds__(512) void k_laswp_panel(T* __restrict__ A, int ld, int ca, int cb,
+                                                     const int* __restrict__ ipiv, int i0, int i1) {
+  __shared__ int pv[512], mdst[1024], msrc[1024], wtot[8];
+  __shared__ T vals[4][1024];
+  const int k = i1 - i0, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < k; i += 512) pv[i] = ipiv[i0 + i];
   __syncthreads();
-  if (tid != 0) return;
-  auto slot = [&](int row) -> int {
-    unsigned h = ((unsigned)row * 2654435761u) & (HSZ - 1);
-    while (hkey[h] != -1 && hkey[h] != row) h = (h + 1) & (HSZ - 1);
-    return (int)h;
-  };
-  for (int i = 0; i < kb; ++i) {
-    const int p = pv[i];
-    if (p == i) continue;
-    const int a = top[i];
-    int b;
-    if (p < kb) {
-      b = top[p];
-      top[p] = a;
-    } else {
-      const int h = slot(p);
-      if (hkey[h] == -1) { hkey[h] = p; hval[h] = p; }
-      b = hval[h];
-      hval[h] = a;
-    }
-    top[i] = b;
+  const int n = net_moves<512, 2>(pv, i0, k, mdst, msrc, wtot);
+  if (w >= 4) return;
+  for (int cc = w; cc < LSW_COLS; cc += 4) {
+    const int c = ca + blockIdx.x * LSW_COLS + cc;
+    if (c >= cb) break;
+    T* col = A + (long long)c * ld;
+    for (int t = lane; t < n; t += 64) vals[w][t] = col[msrc[t]];
+    for (int t = lane; t < n; t += 64) col[mdst[t]] = vals[w][t];
   }
-  int n = 0;
-  for (int i = 0; i < kb; ++i)
-    if (top[i] != i) { dst[n] = i; src[n] = top[i]; ++n; }
-  for (int h = 0; h < HSZ; ++h)
-    if (hkey[h] != -1 && hval[h] != hkey[h]) { dst[n] = hkey[h]; src[n] = hval[h]; ++n; }
-  cnt[0] = n;
+}
+
+// Net row moves of the sequential interchanges ipiv[0..kb) (panel-relative rows, kb <= 1024):
+// row dst[t] holds the former row src[t]; cnt[0] = number of moved rows (<= 2 kb).
+__global__ __launch_bounds__(1024) void k_piv_moves(const int* __restrict__ ipiv, int kb, int* __restrict__ dst,
+                                                    int* __restrict__ src, int* __restrict__ cnt) {
+  __shared__ int pv[1024], wtot[16];
+  for (int i = threadIdx.x; i < kb; i += 1024) pv[i] = ipiv[i];
+  __syncthreads();
+  const int n = net_moves<1024, 2>(pv, 0, kb, dst, src, wtot);
+  if (threadIdx.x == 0) cnt[0] = n;
 }
 
 // Row moves across local tile columns of a tiled matrix.  Global view row R = r0 + rel lives in
@@ -436,14 +491,19 @@ DPL_API int dpl_lu_block(int prec, void* A, int ld, int m, int c0, int cend, int
 DPL_API int dpl_laswp_panel(int prec, void* A, int ld, int ca, int cb, const int* ipiv, int i0, int i1,
                             hipStream_t st) {
   if (cb <= ca || i1 <= i0) return 0;
-  DISPATCH(prec, hipLaunchKernelGGL((k_laswp_panel<T>), dim3((cb - ca + 63) / 64), dim3(64), 0, st, (T*)A, ld, ca,
-                                    cb, ipiv, i0, i1));
+  if (i1 - i0 > 512) {
+    DISPATCH(prec, hipLaunchKernelGGL((k_laswp_seq<T>), dim3((cb - ca + 63) / 64), dim3(64), 0, st, (T*)A, ld, ca,
+                                      cb, ipiv, i0, i1));
+    return (int)hipGetLastError();
+  }
+  DISPATCH(prec, hipLaunchKernelGGL((k_laswp_panel<T>), dim3((cb - ca + LSW_COLS - 1) / LSW_COLS), dim3(512), 0, st,
+                                    (T*)A, ld, ca, cb, ipiv, i0, i1));
   return (int)hipGetLastError();
 }
 
 DPL_API int dpl_piv_moves(const int* ipiv, int kb, int* dst, int* src, int* cnt, hipStream_t st) {
   if (kb > 1024) return -3;
-  hipLaunchKernelGGL(k_piv_moves, dim3(1), dim3(64), 0, st, ipiv, kb, dst, src, cnt);
+  hipLaunchKernelGGL(k_piv_moves, dim3(1), dim3(1024), 0, st, ipiv, kb, dst, src, cnt);
   return (int)hipGetLastError();
 }
 

@@ -19,6 +19,9 @@ MI355X design:
 """
 from __future__ import annotations
 
+import bisect
+import os
+
 import numpy as np
 import torch
 
@@ -135,9 +138,11 @@ class _GetrfDev:
         self.ipiv_all = torch.zeros(max(1, min(A.m, A.n)), dtype=torch.int32, device=dev)
         self.ws = ops.lu_workspace(A.m, dev)
         self.cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.mdst = torch.zeros(2 * nb, dtype=torch.int32, device=dev)
-        self.msrc = torch.zeros(2 * nb, dtype=torch.int32, device=dev)
-        self.mcnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        # move lists double-buffered by step parity: step k+2 must not overwrite the lists the
+        # side stream is still applying to the left (already factored) columns of step k
+        self.mdst = torch.zeros(2, 2 * nb, dtype=torch.int32, device=dev)
+        self.msrc = torch.zeros(2, 2 * nb, dtype=torch.int32, device=dev)
+        self.mcnt = torch.zeros(2, 1, dtype=torch.int32, device=dev)
         # row / column offset tables of the local tiles (offset(m, n) = rowoff[m] + coloff[n])
         lrows = [m for m in range(A.mt) if A.row_is_local(m)]
         lcols = [n for n in range(A.nt) if A.col_is_local(n)]
@@ -154,6 +159,20 @@ class _GetrfDev:
             self.tmp = torch.zeros(2 * nb * width, dtype=A.dtype, device=dev)
         else:
             self.rowoff = self.coloff = self.ncols = self.tmp = None
+        # P == 1, opt-in (DPLASMA_LU_SIDE_SWAPS=1): the interchanges of the already factored
+        # columns (tile columns < k) are off the critical path -- only LAPACK's final L needs
+        # them -- so they can run on a low-priority side stream (zgetrf_1d.jdf applies them as
+        # separate SWAP tasks).  Measured on one MI355X (profiles/r1_lu_side_swaps.txt): the
+        # split moves contend with the trailing GEMM and the persistent panel kernel, the sum of
+        # row-move time grows 82 -> 132 ms at N=32k and the factorisation is no faster, so the
+        # default keeps one exchange per step.  P > 1 always keeps one summed exchange.
+        self.side = None
+        if self.tmp is not None and A.grid.P == 1 and dev.type == "cuda" and \
+                os.environ.get("DPLASMA_LU_SIDE_SWAPS", "0") == "1":
+            self.side = torch.cuda.Stream(device=dev, priority=0)
+            self.tmp_l = torch.zeros_like(self.tmp)
+            self.ev_side = [None, None]
+        self.nleft = [bisect.bisect_left(lcols, k) for k in range(min(A.mt, A.nt))]
         ncol_loc = sum(A.tile_cols(n) for n in lcols)
         self.ubuf = torch.zeros(max(1, nb * max(ncol_loc, 1)), dtype=A.dtype, device=dev)
         self.plan = [self._build(k) for k in range(self.kt)]
@@ -225,14 +244,36 @@ class _GetrfDev:
         self.ipiv_all[r0: r0 + kmin].copy_(self.piv_dev[:kmin] + (r0 + 1))
         # --- 3. row interchanges on every local column (the panel column is rewritten below)
         if self.tmp is not None:
-            ops.piv_moves(self.piv_dev, kmin, self.mdst, self.msrc, self.mcnt)
+            par = k & 1
+            mdst, msrc, mcnt = self.mdst[par], self.msrc[par], self.mcnt[par]
             ldb = 2 * A.nb
-            ops.rows_move(True, A.data, A.ld, A.mb, r0, self.rowoff, self.coloff, self.ncols, A.nb, self.msrc,
-                          self.mcnt, ldb, self.tmp, ldb)
+            nl = self.nleft[k] if self.side is not None else 0
+            cur = torch.cuda.current_stream() if self.side is not None else None
+            if cur is not None and self.ev_side[par] is not None:
+                cur.wait_event(self.ev_side[par])      # step k-2's side moves have read these lists
+            ops.piv_moves(self.piv_dev, kmin, mdst, msrc, mcnt)
+            if nl:
+                ev = torch.cuda.Event()
+                ev.record(cur)                           # lists ready, left columns final (back(k-1))
+                with torch.cuda.stream(self.side):
+                    self.side.wait_event(ev)
+                    cl, nc = self.coloff[:nl], self.ncols[:nl]
+                    ops.rows_move(True, A.data, A.ld, A.mb, r0, self.rowoff, cl, nc, A.nb, msrc, mcnt, ldb,
+                                  self.tmp_l, ldb)
+                    ops.rows_move(False, A.data, A.ld, A.mb, r0, self.rowoff, cl, nc, A.nb, mdst, mcnt, ldb,
+                                  self.tmp_l, ldb)
+                    self.ev_side[par] = torch.cuda.Event()
+                    self.ev_side[par].record(self.side)
+            cr, nr = self.coloff[nl:], self.ncols[nl:]
+            ops.rows_move(True, A.data, A.ld, A.mb, r0, self.rowoff, cr, nr, A.nb, msrc, mcnt, ldb, self.tmp, ldb)
             if g.P > 1:
                 dist.all_reduce(self.tmp, group=ctx.col_group)
-            ops.rows_move(False, A.data, A.ld, A.mb, r0, self.rowoff, self.coloff, self.ncols, A.nb, self.mdst,
-                          self.mcnt, ldb, self.tmp, ldb)
+            ops.rows_move(False, A.data, A.ld, A.mb, r0, self.rowoff, cr, nr, A.nb, mdst, mcnt, ldb, self.tmp, ldb)
+            if cur is not None and k == self.kt - 1:
+                for e in self.ev_side:                   # join: the factorisation ends with L final
+                    if e is not None:
+                        cur.wait_event(e)
+                self.ev_side = [None, None]
         if "back" in st:
             ops.geadd(0, N_, 1.0, pv, mp, 0.0, A.data, A.ld, st["back"], copy=True)
         # --- 4. U block row where it lives, then down the process column

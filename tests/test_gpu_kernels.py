@@ -247,6 +247,23 @@ def test_lu_gpu(gctx, cctx, prec):
     assert rel_err(outs[0][1], outs[1][1]) < tol(dt) * 100
 
 
+@pytest.mark.parametrize("side", ["0", "1"])
+def test_getrf_side_swaps(gctx, cctx, side, monkeypatch):
+    """Partial-pivoting LU with the left-column interchanges on the side stream (opt-in) and
+    without: same factors and pivots as the CPU path."""
+    monkeypatch.setenv("DPLASMA_LU_SIDE_SWAPS", side)
+    N, NB = 1100, 128
+    outs = []
+    for ctx in (gctx, cctx):
+        A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+        dp.plrnt(ctx, A, 3872)
+        IPIV = dp.ipiv_descriptor(ctx, A)
+        assert dp.getrf_1d(ctx, A, IPIV) == 0
+        outs.append((A.to_dense_local(), IPIV.to_dense_local()))
+    assert torch.equal(outs[0][1].cpu(), outs[1][1].cpu())
+    assert rel_err(outs[0][0], outs[1][0]) < 1e-11
+
+
 @pytest.mark.parametrize("prec", list("sd"))
 @pytest.mark.parametrize("ta,tb", [(111, 111), (111, 112), (112, 111), (112, 112)])
 @pytest.mark.parametrize("mask,alpha,beta", [(0, -1.0, 1.0), (1, -1.0, 1.0), (2, 0.5, -0.3), (0, 2.0, 0.0)])
@@ -324,6 +341,25 @@ def test_piv_moves_device(gctx):
         n = int(c[0])
         outs.append(sorted(zip(d[:n].cpu().tolist(), s[:n].cpu().tolist())))
     assert outs[0] == outs[1]
+
+
+@pytest.mark.parametrize("prec", list("dz"))
+@pytest.mark.parametrize("seg", [(0, 64), (64, 320), (100, 356), (0, 600)])
+def test_laswp_panel_device(gctx, prec, seg):
+    """Panel interchanges on the device (content-parallel net moves; > 512 swaps: sequential
+    fallback) vs the host replay of the same LAPACK ipiv segment."""
+    torch.manual_seed(7)
+    i0, i1 = seg
+    m, ld, ncols = 3000, 3008, 77
+    ipiv = torch.tensor([int(torch.randint(i, min(m, i + (4 if i % 3 else m)), (1,))) for i in range(i1)],
+                        dtype=torch.int32)
+    P = torch.randn(ld * (ncols + 3), dtype=DTYPES[prec])
+    outs = []
+    for dev in ("cuda", "cpu"):
+        X = P.clone().to(dev)
+        ops.laswp_panel(X, ld, 2, 2 + ncols, ipiv.to(dev), i0, i1)
+        outs.append(X.cpu())
+    assert torch.equal(outs[0], outs[1])
 
 
 @pytest.mark.parametrize("prec", list("dz"))
