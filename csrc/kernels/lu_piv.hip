@@ -288,6 +288,42 @@ __global__ __launch_bounds__(256) void k_rows_move(T* __restrict__ A, int ld, in
   }
 }
 
+// In-place row permutation on one process (P == 1): row r0 + dst[t] := former row r0 + src[t] over
+// every local tile column, without the staging buffer of k_rows_move (no gather/scatter round trip
+// through HBM, one launch).  Each wave owns whole columns: it reads all moved elements of its column
+// into LDS before writing any of them (the moves form a permutation of the involved rows).
+template <typename T>
+__global__ __launch_bounds__(256) void k_rows_permute(T* __restrict__ A, int ld, int mb, int r0,
+                                                      const long long* __restrict__ rowoff, int nrt,
+                                                      const long long* __restrict__ coloff,
+                                                      const int* __restrict__ ncols, int nct, int nb,
+                                                      const int* __restrict__ dst, const int* __restrict__ src,
+                                                      const int* __restrict__ cnt) {
+  __shared__ long long so[1024], dof[1024];
+  __shared__ T vals[4][1024];
+  const int n = min(cnt[0], 1024);
+  for (int t = threadIdx.x; t < n; t += 256) {
+    const int Rs = r0 + src[t], Rd = r0 + dst[t];
+    const int ts = Rs / mb, td = Rd / mb;
+    const long long bs = ts < nrt ? rowoff[ts] : -1, bd = td < nrt ? rowoff[td] : -1;
+    const bool ok = bs >= 0 && bd >= 0;
+    so[t] = ok ? bs + Rs % mb : -1;
+    dof[t] = ok ? bd + Rd % mb : -1;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int W = nct * nb;
+  for (int c = blockIdx.x * 4 + w; c < W; c += gridDim.x * 4) {
+    const int ct = c / nb, cc = c % nb;
+    if (cc >= ncols[ct]) continue;
+    const long long co = coloff[ct] + (long long)cc * ld;
+    for (int t = lane; t < n; t += 64)
+      if (so[t] >= 0) vals[w][t] = A[so[t] + co];
+    for (int t = lane; t < n; t += 64)
+      if (dof[t] >= 0) A[dof[t] + co] = vals[w][t];
+  }
+}
+
 // ---------------------------------------------------------------- persistent block LU
 // Same block factorisation as k_lu_col, in ONE launch with the block's rows resident in LDS:
 // G workgroups (<= one per CU), workgroup w owns panel rows [c0 + w R, c0 + (w+1) R) x the
@@ -521,5 +557,17 @@ DPL_API int dpl_rows_move(int prec, int gather, void* A, int ld, int mb, int r0,
     DISPATCH(prec, hipLaunchKernelGGL((k_rows_move<T, false>), g, dim3(256), 0, st, (T*)A, ld, mb, r0, rowoff, nrt,
                                       coloff, ncols, nct, nb, rows, cnt, (T*)buf, ldb));
   }
+  return (int)hipGetLastError();
+}
+
+DPL_API int dpl_rows_permute(int prec, void* A, int ld, int mb, int r0, const long long* rowoff, int nrt,
+                             const long long* coloff, const int* ncols, int nct, int nb, const int* dst,
+                             const int* src, const int* cnt, int maxcnt, hipStream_t st) {
+  if (nct <= 0 || maxcnt <= 0) return 0;
+  if (maxcnt > 1024) return -3;
+  const int W = nct * nb;
+  const int gx = (W + 3) / 4 > 4096 ? 4096 : (W + 3) / 4;
+  DISPATCH(prec, hipLaunchKernelGGL((k_rows_permute<T>), dim3(gx), dim3(256), 0, st, (T*)A, ld, mb, r0, rowoff, nrt,
+                                    coloff, ncols, nct, nb, dst, src, cnt));
   return (int)hipGetLastError();
 }

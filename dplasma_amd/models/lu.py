@@ -166,6 +166,7 @@ class _GetrfDev:
         # split moves contend with the trailing GEMM and the persistent panel kernel, the sum of
         # row-move time grows 82 -> 132 ms at N=32k and the factorisation is no faster, so the
         # default keeps one exchange per step.  P > 1 always keeps one summed exchange.
+        self.inplace_moves = os.environ.get("DPLASMA_LU_INPLACE_MOVES", "1") != "0"
         self.side = None
         if self.tmp is not None and A.grid.P == 1 and dev.type == "cuda" and \
                 os.environ.get("DPLASMA_LU_SIDE_SWAPS", "0") == "1":
@@ -265,10 +266,16 @@ class _GetrfDev:
                     self.ev_side[par] = torch.cuda.Event()
                     self.ev_side[par].record(self.side)
             cr, nr = self.coloff[nl:], self.ncols[nl:]
-            ops.rows_move(True, A.data, A.ld, A.mb, r0, self.rowoff, cr, nr, A.nb, msrc, mcnt, ldb, self.tmp, ldb)
-            if g.P > 1:
-                dist.all_reduce(self.tmp, group=ctx.col_group)
-            ops.rows_move(False, A.data, A.ld, A.mb, r0, self.rowoff, cr, nr, A.nb, mdst, mcnt, ldb, self.tmp, ldb)
+            if g.P == 1 and self.inplace_moves and ldb <= 1024:
+                # one process: in-place permutation, no staging round trip through HBM
+                ops.rows_permute(A.data, A.ld, A.mb, r0, self.rowoff, cr, nr, A.nb, mdst, msrc, mcnt, ldb)
+            else:
+                ops.rows_move(True, A.data, A.ld, A.mb, r0, self.rowoff, cr, nr, A.nb, msrc, mcnt, ldb, self.tmp,
+                              ldb)
+                if g.P > 1:
+                    dist.all_reduce(self.tmp, group=ctx.col_group)
+                ops.rows_move(False, A.data, A.ld, A.mb, r0, self.rowoff, cr, nr, A.nb, mdst, mcnt, ldb, self.tmp,
+                              ldb)
             if cur is not None and k == self.kt - 1:
                 for e in self.ev_side:                   # join: the factorisation ends with L final
                     if e is not None:

@@ -82,6 +82,8 @@ _SIGS = {
     # prec, gather, A, ld, mb, r0, rowoff, nrt, coloff, ncols, nct, nb, rows, cnt, maxcnt, buf, ldb, stream
     "dpl_rows_move": [c_int, c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp,
                       c_int, c_vp, c_int, c_vp],
+    "dpl_rows_permute": [c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp,
+                         c_int, c_vp],
 }
 _OPTIONAL = set()
 

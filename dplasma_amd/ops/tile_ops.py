@@ -770,6 +770,24 @@ def piv_moves(ipiv: torch.Tensor, kb: int, dst: torch.Tensor, src: torch.Tensor,
     cnt[0] = len(moves)
 
 
+def rows_permute(A: torch.Tensor, ld: int, mb: int, r0: int, rowoff: torch.Tensor, coloff: torch.Tensor,
+                 ncols: torch.Tensor, nb: int, dst: torch.Tensor, src: torch.Tensor, cnt: torch.Tensor, maxcnt: int):
+    """In place, one process: A[r0 + dst[t], col c] := old A[r0 + src[t], col c] on the flattened local
+    tile columns (coloff[j], ncols[j]) -- rows_move gather + scatter without the staging buffer."""
+    nct = int(coloff.numel())
+    if nct == 0:
+        return
+    if _is_gpu(A):
+        rc = _lib.load().dpl_rows_permute(_lib.prec_code(A.dtype), A.data_ptr(), ld, mb, r0, rowoff.data_ptr(),
+                                          int(rowoff.numel()), coloff.data_ptr(), ncols.data_ptr(), nct, nb,
+                                          dst.data_ptr(), src.data_ptr(), cnt.data_ptr(), maxcnt, _lib.stream_ptr())
+        _lib.check(rc, "rows_permute")
+        return
+    buf = torch.zeros(maxcnt * nct * nb, dtype=A.dtype, device=A.device)
+    rows_move(True, A, ld, mb, r0, rowoff, coloff, ncols, nb, src, cnt, maxcnt, buf, maxcnt)
+    rows_move(False, A, ld, mb, r0, rowoff, coloff, ncols, nb, dst, cnt, maxcnt, buf, maxcnt)
+
+
 def rows_move(gather: bool, A: torch.Tensor, ld: int, mb: int, r0: int, rowoff: torch.Tensor, coloff: torch.Tensor,
               ncols: torch.Tensor, nb: int, rows: torch.Tensor, cnt: torch.Tensor, maxcnt: int, buf: torch.Tensor,
               ldb: int):

@@ -247,11 +247,13 @@ def test_lu_gpu(gctx, cctx, prec):
     assert rel_err(outs[0][1], outs[1][1]) < tol(dt) * 100
 
 
-@pytest.mark.parametrize("side", ["0", "1"])
-def test_getrf_side_swaps(gctx, cctx, side, monkeypatch):
-    """Partial-pivoting LU with the left-column interchanges on the side stream (opt-in) and
-    without: same factors and pivots as the CPU path."""
+@pytest.mark.parametrize("side,inplace", [("0", "1"), ("0", "0"), ("1", "1")])
+def test_getrf_side_swaps(gctx, cctx, side, inplace, monkeypatch):
+    """Partial-pivoting LU with the left-column interchanges on the side stream (opt-in) or not,
+    row moves in place (k_rows_permute, default on one process) or staged (k_rows_move): same
+    factors and pivots as the CPU path."""
     monkeypatch.setenv("DPLASMA_LU_SIDE_SWAPS", side)
+    monkeypatch.setenv("DPLASMA_LU_INPLACE_MOVES", inplace)
     N, NB = 1100, 128
     outs = []
     for ctx in (gctx, cctx):
