@@ -335,3 +335,13 @@ DPL_API int dpl_tile_norm(int prec, int kind, int part, int unit, int nitems, co
                                     (const T*)A, lda, part, unit, kind, out, ostride));
   return (int)hipGetLastError();
 }
+
+// Stream restricted to a CU subset (CDNA CU masking): bit i of mask[i / 32] enables CU i.  Used to
+// give the latency-bound diagonal-tile Cholesky its own CU(s), away from the CU-saturating trailing
+// GEMM it would otherwise share SIMDs with.
+DPL_API int dpl_stream_cumask(const unsigned* mask, int nwords, void** out) {
+  hipStream_t s = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, mask);
+  *out = (void*)s;
+  return (int)e;
+}

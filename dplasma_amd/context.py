@@ -75,6 +75,9 @@ class Context:
                 "update": torch.cuda.Stream(device=self.device, priority=lo),
                 "aux": torch.cuda.Stream(device=self.device, priority=lo),
             }
+            ndiag = int(os.environ.get("DPLASMA_DIAG_CUS", "0"))
+            if ndiag > 0:
+                self._reserve_cus(ndiag)
         else:
             self.streams = {}
         self._groups_built = False
@@ -91,6 +94,30 @@ class Context:
             self.profiling = Tracer(self)
         from .utils.info import Info
         self.info = Info()
+
+    def _reserve_cus(self, ndiag: int):
+        """Opt-in (DPLASMA_DIAG_CUS=n): a "diag" stream on CUs [0, n) for the latency-bound
+        diagonal-tile factorisations and an "update" stream on the other CUs, so the single-
+        workgroup tile kernel does not share SIMDs with the trailing-update GEMM (HIP CU masks)."""
+        import ctypes
+        from .ops import _lib
+        ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+        nw = (ncu + 31) // 32
+        diag, upd = [0] * nw, [0] * nw
+        for c in range(ncu):
+            if c < ndiag:
+                diag[c // 32] |= 1 << (c % 32)
+            else:
+                upd[c // 32] |= 1 << (c % 32)
+        lib = _lib.load()
+        made = {}
+        for name, m in (("diag", diag), ("update", upd)):
+            arr = (ctypes.c_uint * nw)(*m)
+            out = ctypes.c_void_p()
+            rc = lib.dpl_stream_cumask(ctypes.cast(arr, ctypes.c_void_p), nw, ctypes.byref(out))
+            _lib.check(rc, "stream_cumask")
+            made[name] = torch.cuda.ExternalStream(out.value, device=self.device)
+        self.streams.update(made)
 
     # ------------------------------------------------------------------ comms
     def _build_groups(self):

@@ -82,6 +82,8 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
         raise ValueError("potrf: A must be square with square tiles")
     lower = uplo == dplasmaLower
     tp = Taskpool("potrf", ctx)
+    # diagonal tiles on the CU-reserved stream when DPLASMA_DIAG_CUS is set (context._reserve_cus)
+    diag_stream = "diag" if "diag" in getattr(ctx, "streams", {}) else "panel"
     tp.flops = flops(A.prec, "potrf", A.n)
     nt = A.nt
     dev = A.device
@@ -189,7 +191,7 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
 
                 def f_potrf(off=off, kb=kb, k=k):
                     potrf_diag(uplo, A.data, off, kb, A.ld, info, k * A.mb)
-                t_potrf = tp.task(f"POTRF({k})", "panel", f_potrf, [gate], prio=3)
+                t_potrf = tp.task(f"POTRF({k})", diag_stream, f_potrf, [gate], prio=3)
             # ---------------- local panel tiles (i > k) of my process row/col
             mine = [i for i in range(k + 1, nt) if in_panel_cross and owner_of_panel_line(i) == my_line]
             # ---------------- diag tile to the panel owners (column for lower) and TRSM

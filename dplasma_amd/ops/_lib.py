@@ -82,6 +82,7 @@ _SIGS = {
     # prec, gather, A, ld, mb, r0, rowoff, nrt, coloff, ncols, nct, nb, rows, cnt, maxcnt, buf, ldb, stream
     "dpl_rows_move": [c_int, c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp,
                       c_int, c_vp, c_int, c_vp],
+    "dpl_stream_cumask": [c_vp, c_int, c_vp],
     "dpl_rows_permute": [c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp,
                          c_int, c_vp],
 }
