@@ -11,6 +11,8 @@
 // (src/cores/random.h:20-41) bit for bit: every element's value depends only on
 // its GLOBAL (row, col) and the seed, so a matrix generated on any P x Q grid,
 // any tile size, on GPU or CPU, is identical (SURVEY.md §2.4 "RNG").
+#include <algorithm>
+
 #include "common.h"
 
 #define RND64_A 6364136223846793005ULL
@@ -57,11 +59,10 @@ __device__ inline T rnd_at(long long I, long long J, long long gM, unsigned long
 // sequential LCG (one skip-ahead per run).
 #define SEG 16
 template <typename T>
-__global__ __launch_bounds__(256) void k_generate(const TileItem* __restrict__ items, int nitems, int nseg_max,
+__device__ inline void k_generate_one(long long gid, const TileItem* __restrict__ items, int nitems, int nseg_max,
                                                   int nmax, T* A, int lda, long long gM, unsigned long long seed,
                                                   int kind, T bump) {
   const int per_item = nseg_max * nmax;
-  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
   if (gid >= (long long)nitems * per_item) return;  // tail of the last block
   const int item = (int)(gid / per_item);
   const int r = (int)(gid % per_item);
@@ -103,6 +104,17 @@ __global__ __launch_bounds__(256) void k_generate(const TileItem* __restrict__ i
     col[i] = v;
   }
 }
+template <typename T>
+__global__ __launch_bounds__(256) void k_generate(const TileItem* __restrict__ items, int nitems, int nseg_max,
+                                                  int nmax, T* A, int lda, long long gM, unsigned long long seed,
+                                                  int kind, T bump) {
+  // grid-stride: a launch covers at most 2^28 work-items (HSA grid sizes are 32-bit)
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long gid = (long long)blockIdx.x * 256 + threadIdx.x;; gid += stride) {
+    if (gid >= (long long)nitems * nseg_max * nmax) return;
+    k_generate_one<T>(gid, items, nitems, nseg_max, nmax, A, lda, gM, seed, kind, bump);
+  }
+}
 
 // ---------------------------------------------------------------- laset / lacpy / geadd / lascal
 // part: 0 full, 1 lower incl diag, 2 upper incl diag, 3 strictly lower,
@@ -118,9 +130,8 @@ __device__ inline bool in_part(int part, long long I, long long J) {
   }
 }
 template <typename T>
-__global__ __launch_bounds__(256) void k_laset(const TileItem* __restrict__ items, int nitems, int mmax, int nmax, T* A, int lda,
+__device__ inline void k_laset_one(long long gid, const TileItem* __restrict__ items, int nitems, int mmax, int nmax, T* A, int lda,
                                                int part, T alpha, T beta) {
-  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
   const int per = mmax * nmax;
   if (gid >= (long long)nitems * per) return;  // tail of the last block
   const int item = (int)(gid / per), r = (int)(gid % per);
@@ -131,12 +142,21 @@ __global__ __launch_bounds__(256) void k_laset(const TileItem* __restrict__ item
   if (!in_part(part, I, J)) return;
   A[it.a_off + i + (long long)j * lda] = (I == J) ? beta : alpha;
 }
+template <typename T>
+__global__ __launch_bounds__(256) void k_laset(const TileItem* __restrict__ items, int nitems, int mmax, int nmax, T* A, int lda,
+                                               int part, T alpha, T beta) {
+  // grid-stride: a launch covers at most 2^28 work-items (HSA grid sizes are 32-bit)
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long gid = (long long)blockIdx.x * 256 + threadIdx.x;; gid += stride) {
+    if (gid >= (long long)nitems * mmax * nmax) return;
+    k_laset_one<T>(gid, items, nitems, mmax, nmax, A, lda, part, alpha, beta);
+  }
+}
 // B = alpha * op(A) + beta * B on the part; trans: 0 N, 1 T, 2 C (A item tile is op-sized source)
 template <typename T>
-__global__ __launch_bounds__(256) void k_geadd(const TileItem* __restrict__ items, int nitems, int mmax, int nmax, const T* A,
+__device__ inline void k_geadd_one(long long gid, const TileItem* __restrict__ items, int nitems, int mmax, int nmax, const T* A,
                                                int lda, T* B, int ldb, int part, int trans, T alpha, T beta,
                                                int copy) {
-  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
   const int per = mmax * nmax;
   if (gid >= (long long)nitems * per) return;  // tail of the last block
   const int item = (int)(gid / per), r = (int)(gid % per);
@@ -154,9 +174,19 @@ __global__ __launch_bounds__(256) void k_geadd(const TileItem* __restrict__ item
   *pb = v;
 }
 template <typename T>
-__global__ __launch_bounds__(256) void k_lascal(const TileItem* __restrict__ items, int nitems, int mmax, int nmax, T* A, int lda,
+__global__ __launch_bounds__(256) void k_geadd(const TileItem* __restrict__ items, int nitems, int mmax, int nmax, const T* A,
+                                               int lda, T* B, int ldb, int part, int trans, T alpha, T beta,
+                                               int copy) {
+  // grid-stride: a launch covers at most 2^28 work-items (HSA grid sizes are 32-bit)
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long gid = (long long)blockIdx.x * 256 + threadIdx.x;; gid += stride) {
+    if (gid >= (long long)nitems * mmax * nmax) return;
+    k_geadd_one<T>(gid, items, nitems, mmax, nmax, A, lda, B, ldb, part, trans, alpha, beta, copy);
+  }
+}
+template <typename T>
+__device__ inline void k_lascal_one(long long gid, const TileItem* __restrict__ items, int nitems, int mmax, int nmax, T* A, int lda,
                                                 int part, T alpha) {
-  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
   const int per = mmax * nmax;
   if (gid >= (long long)nitems * per) return;  // tail of the last block
   const int item = (int)(gid / per), r = (int)(gid % per);
@@ -168,16 +198,25 @@ __global__ __launch_bounds__(256) void k_lascal(const TileItem* __restrict__ ite
   T* p = A + it.a_off + i + (long long)j * lda;
   *p = mul(alpha, *p);
 }
+template <typename T>
+__global__ __launch_bounds__(256) void k_lascal(const TileItem* __restrict__ items, int nitems, int mmax, int nmax, T* A, int lda,
+                                                int part, T alpha) {
+  // grid-stride: a launch covers at most 2^28 work-items (HSA grid sizes are 32-bit)
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long gid = (long long)blockIdx.x * 256 + threadIdx.x;; gid += stride) {
+    if (gid >= (long long)nitems * mmax * nmax) return;
+    k_lascal_one<T>(gid, items, nitems, mmax, nmax, A, lda, part, alpha);
+  }
+}
 
 // ---------------------------------------------------------------- diagonal scaling (LDL^H family)
 // B(i, j) := B(i, j) / d, with d the diagonal of the tile at D + item.a_off:
 // cols != 0: d = D(j, j) (B := B D^-1, CORE_ztrmdm / hetrf), else d = D(i, i) (B := D^-1 B, CORE_ztrdsm).
 // item.b_off addresses the B tile; gi/gj its global coordinates for the part mask.
 template <typename T>
-__global__ __launch_bounds__(256) void k_diag_scale(const TileItem* __restrict__ items, int nitems, int mmax,
+__device__ inline void k_diag_scale_one(long long gid, const TileItem* __restrict__ items, int nitems, int mmax,
                                                     int nmax, const T* __restrict__ D, int ldd, T* B, int ldb,
                                                     int part, int cols) {
-  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
   const int per = mmax * nmax;
   if (gid >= (long long)nitems * per) return;
   const int item = (int)(gid / per), r = (int)(gid % per);
@@ -189,6 +228,17 @@ __global__ __launch_bounds__(256) void k_diag_scale(const TileItem* __restrict__
   const T d = D[it.a_off + q + (long long)q * ldd];
   T* p = B + it.b_off + i + (long long)j * ldb;
   *p = divv(*p, d);
+}
+template <typename T>
+__global__ __launch_bounds__(256) void k_diag_scale(const TileItem* __restrict__ items, int nitems, int mmax,
+                                                    int nmax, const T* __restrict__ D, int ldd, T* B, int ldb,
+                                                    int part, int cols) {
+  // grid-stride: a launch covers at most 2^28 work-items (HSA grid sizes are 32-bit)
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long gid = (long long)blockIdx.x * 256 + threadIdx.x;; gid += stride) {
+    if (gid >= (long long)nitems * mmax * nmax) return;
+    k_diag_scale_one<T>(gid, items, nitems, mmax, nmax, D, ldd, B, ldb, part, cols);
+  }
 }
 
 // ---------------------------------------------------------------- norms
@@ -279,7 +329,7 @@ DPL_API int dpl_generate(int prec, int kind, int nitems, const void* items, int 
   if (nitems <= 0) return 0;
   const int nseg = cdiv(mmax, SEG);
   const long long total = (long long)nitems * nseg * nmax;
-  const int blocks = (int)((total + 255) / 256);
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 1LL << 20);
   DISPATCH(prec, hipLaunchKernelGGL((k_generate<T>), dim3(blocks), dim3(256), 0, st, (const TileItem*)items, nitems, nseg,
                                     nmax, (T*)A, lda, gM, seed, kind, *(const T*)bump));
   return (int)hipGetLastError();
@@ -289,7 +339,7 @@ DPL_API int dpl_laset(int prec, int part, int nitems, const void* items, int mma
                       const void* beta, void* A, int lda, hipStream_t st) {
   if (nitems <= 0) return 0;
   const long long total = (long long)nitems * mmax * nmax;
-  const int blocks = (int)((total + 255) / 256);
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 1LL << 20);
   DISPATCH(prec, hipLaunchKernelGGL((k_laset<T>), dim3(blocks), dim3(256), 0, st, (const TileItem*)items, nitems, mmax, nmax,
                                     (T*)A, lda, part, *(const T*)alpha, *(const T*)beta));
   return (int)hipGetLastError();
@@ -301,7 +351,7 @@ DPL_API int dpl_geadd(int prec, int part, int trans, int nitems, const void* ite
                       hipStream_t st) {
   if (nitems <= 0) return 0;
   const long long total = (long long)nitems * mmax * nmax;
-  const int blocks = (int)((total + 255) / 256);
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 1LL << 20);
   const int tr = trans == DPL_NOTRANS ? 0 : (trans == DPL_TRANS ? 1 : 2);
   DISPATCH(prec, hipLaunchKernelGGL((k_geadd<T>), dim3(blocks), dim3(256), 0, st, (const TileItem*)items, nitems, mmax, nmax,
                                     (const T*)A, lda, (T*)B, ldb, part, tr, *(const T*)alpha, *(const T*)beta, copy));
@@ -312,7 +362,7 @@ DPL_API int dpl_lascal(int prec, int part, int nitems, const void* items, int mm
                        void* A, int lda, hipStream_t st) {
   if (nitems <= 0) return 0;
   const long long total = (long long)nitems * mmax * nmax;
-  const int blocks = (int)((total + 255) / 256);
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 1LL << 20);
   DISPATCH(prec, hipLaunchKernelGGL((k_lascal<T>), dim3(blocks), dim3(256), 0, st, (const TileItem*)items, nitems, mmax,
                                     nmax, (T*)A, lda, part, *(const T*)alpha));
   return (int)hipGetLastError();
@@ -322,7 +372,7 @@ DPL_API int dpl_diag_scale(int prec, int part, int cols, int nitems, const void*
                            const void* D, int ldd, void* B, int ldb, hipStream_t st) {
   if (nitems <= 0) return 0;
   const long long total = (long long)nitems * mmax * nmax;
-  const int blocks = (int)((total + 255) / 256);
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 1LL << 20);
   DISPATCH(prec, hipLaunchKernelGGL((k_diag_scale<T>), dim3(blocks), dim3(256), 0, st, (const TileItem*)items, nitems,
                                     mmax, nmax, (const T*)D, ldd, (T*)B, ldb, part, cols));
   return (int)hipGetLastError();

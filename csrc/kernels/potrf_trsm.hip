@@ -392,11 +392,24 @@ static int potrf_launch(int uplo, int n, T* A, int lda, int* info, int info_base
   return (int)hipGetLastError();
 }
 
+// fp64 tiles with n <= 512 go to the multi-workgroup dataflow kernel (potrf_rb.hip) unless
+// dpl_potrf_tile_set_kind(1) selects the single-workgroup kernel (ablation / comparison).
+DPL_API int dpl_potrf_tile_rb(int uplo, int n, double* A, int lda, int* info, int info_base, hipStream_t st);
+static int g_potrf_kind = 0;
+DPL_API int dpl_potrf_tile_set_kind(int kind) {
+  const int old = g_potrf_kind;
+  g_potrf_kind = kind;
+  return old;
+}
+
 DPL_API int dpl_potrf_tile(int prec, int uplo, int n, void* A, long long a_off, int lda, int* info, int info_base,
                            hipStream_t st) {
   switch (prec) {
     case DPL_S: return potrf_launch<float>(uplo, n, (float*)A + a_off, lda, info, info_base, st);
-    case DPL_D: return potrf_launch<double>(uplo, n, (double*)A + a_off, lda, info, info_base, st);
+    case DPL_D:
+      if (g_potrf_kind == 0 && n <= 512)
+        return dpl_potrf_tile_rb(uplo, n, (double*)A + a_off, lda, info, info_base, st);
+      return potrf_launch<double>(uplo, n, (double*)A + a_off, lda, info, info_base, st);
     case DPL_C: return potrf_launch<hipFloatComplex>(uplo, n, (hipFloatComplex*)A + a_off, lda, info, info_base, st);
     case DPL_Z: return potrf_launch<hipDoubleComplex>(uplo, n, (hipDoubleComplex*)A + a_off, lda, info, info_base, st);
   }

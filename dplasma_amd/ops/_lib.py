@@ -68,7 +68,8 @@ _SIGS = {
     # prec, A, ld, ca, cb, ipiv, i0, i1, stream
     "dpl_laswp_panel": [c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp],
     "dpl_lu_block_ws_bytes": [c_int],
-    "dpl_debug_set_phase_mask": [c_int],   # tile POTRF phase ablation (tools/gpu/potrf_tile_phases.py)
+    "dpl_debug_set_phase_mask": [c_int],
+    "dpl_potrf_tile_set_kind": [c_int],    # 0 = dataflow multi-WG (fp64, n <= 512), 1 = single-WG kernel   # tile POTRF phase ablation (tools/gpu/potrf_tile_phases.py)
     # Householder panel (qr_panel.hip): prec, P, ldp, rbl, rstride, M, nc, kf, V, ldv, Tm, ldt, ws, info, stream
     "dpl_qr_panel": [c_int, c_vp, c_int, c_int, c_ll, c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_vp,
                      c_vp],

@@ -1,0 +1,112 @@
+"""Diagonal-tile Cholesky kernels on the GPU against a plain PyTorch fp64 reference.
+
+Covers the multi-workgroup dataflow kernel (csrc/kernels/potrf_rb.hip, fp64 n <= 512) and the
+single-workgroup kernel it replaces (potrf_trsm.hip), both through ``ops.potrf_tile``:
+odd sizes (identity padding of the last 32-row block), lower/upper storage, a leading dimension
+larger than n, the untouched opposite triangle, LAPACK's info convention on a non-SPD tile, and
+repeated launches while a large GEMM keeps every CU busy on another stream (the workgroup
+hand-offs must hold under uneven load).
+"""
+import pytest
+import torch
+
+from dplasma_amd.constants import dplasmaLower, dplasmaUpper
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    from dplasma_amd.ops import _lib
+    return _lib.load()
+
+
+def _spd(n, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    M = torch.randn(n, n, dtype=torch.float64, generator=g)
+    return (M @ M.T + n * torch.eye(n, dtype=torch.float64)).cuda()
+
+
+def _run(kind, uplo, S, lda, info_base=0):
+    from dplasma_amd.ops import tile_ops as ops
+    n = S.shape[0]
+    buf = torch.full((lda * n,), 7.0, dtype=torch.float64, device="cuda")
+    view = torch.as_strided(buf, (n, n), (1, lda), 0)
+    view.copy_(S)
+    info = torch.zeros(1, dtype=torch.int32, device="cuda")
+    old = _lib().dpl_potrf_tile_set_kind(kind)
+    try:
+        ops.potrf_tile(uplo, buf, 0, n, lda, info, info_base)
+        torch.cuda.synchronize()
+    finally:
+        _lib().dpl_potrf_tile_set_kind(old)
+    return view.clone(), int(info.item()), buf
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("uplo", [dplasmaLower, dplasmaUpper])
+@pytest.mark.parametrize("n", [1, 31, 32, 33, 100, 256, 480, 511, 512])
+def test_potrf_tile_vs_torch(kind, uplo, n):
+    S = _spd(n, seed=n)
+    lda = n + 9
+    out, info, _ = _run(kind, uplo, S, lda)
+    assert info == 0
+    Lref = torch.linalg.cholesky(S)
+    if uplo == dplasmaLower:
+        got, other, ref_other = out.tril(), out.triu(1), S.triu(1)
+        ref = Lref
+    else:
+        got, other, ref_other = out.triu(), out.tril(-1), S.tril(-1)
+        ref = Lref.T
+    err = (got - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-13, err
+    # the opposite strict triangle is never written
+    assert torch.equal(other, ref_other)
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("bad", [0, 5, 31, 32, 200, 511])
+def test_potrf_tile_info(kind, bad):
+    n = 512
+    S = _spd(n, seed=3)
+    # make the leading minor of order bad+1 indefinite: the first failing column is `bad`
+    L = torch.linalg.cholesky(S)
+    S = S.clone()
+    S[bad, bad] -= 2 * (L[bad, bad] ** 2)
+    _, info, _ = _run(kind, dplasmaLower, S, n, info_base=1000)
+    assert info == 1000 + bad + 1
+
+
+def test_potrf_tile_under_load():
+    """Repeated dataflow-kernel launches on a high-priority stream while a big MFMA GEMM occupies
+    every CU on another stream: every factorisation must be exact."""
+    from dplasma_amd.ops import tile_ops as ops
+    from dplasma_amd.ops.batch import GemmBatch
+    n, lda = 512, 512
+    S = _spd(n, seed=11)
+    Lref = torch.linalg.cholesky(S)
+    N = 8192
+    big = torch.randn(3 * N * N, dtype=torch.float64, device="cuda")
+    gb = GemmBatch()
+    for i in range(0, N, 512):
+        for j in range(0, N, 512):
+            gb.add(2 * N * N + i + j * N, 512, 512, [(i, N * N + j * N, N)], 0)
+    gb.finalize()
+    lo = torch.cuda.Stream(priority=0)
+    hi = torch.cuda.Stream(priority=-1)
+    reps = 24
+    bufs = [torch.empty(n * lda, dtype=torch.float64, device="cuda") for _ in range(reps)]
+    infos = torch.zeros(reps, dtype=torch.int32, device="cuda")
+    for b in bufs:
+        torch.as_strided(b, (n, n), (1, lda), 0).copy_(S)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(lo):
+        from dplasma_amd.constants import dplasmaNoTrans
+        ops.gemm(dplasmaNoTrans, dplasmaNoTrans, 1.0, big, N, big, N, 0.0, big, N, gb)
+    with torch.cuda.stream(hi):
+        for r in range(reps):
+            ops.potrf_tile(dplasmaLower, bufs[r], 0, n, lda, infos[r:r + 1], 0)
+    torch.cuda.synchronize()
+    assert int(infos.abs().max().item()) == 0
+    for b in bufs:
+        got = torch.as_strided(b, (n, n), (1, lda), 0).tril()
+        assert (got - Lref).abs().max().item() < 1e-12
