@@ -48,10 +48,13 @@ constexpr int PSTRIDE = 32;       // ints between flags (one 128-B line each)
 constexpr int NSLOT = 8;          // workspaces (concurrent launches on different streams)
 
 struct RbWork {
-  double* Z;    // [MAXB][BLK]        inv(L(k,k)), T-layout
+  double* M;    // [MAXB][BLK]        M_k, column-major: inv(L(k,k)) = diag(S_k) M_k
+  double* S;    // [MAXB][RB]         S_k
   double* Lp;   // [MAXB][MAXB][BLK]  L(i,k), T-layout
   int* prog;    // [MAXB * PSTRIDE]   epoch * 64 + number of published steps
 };
+// caller-visible copy of (M, S) for the panel TRSM (dpl_trsm_rb): MAXB * (BLK + RB) doubles
+constexpr int ZBUF = MAXB * (BLK + RB);
 
 __device__ inline int tl_index(int rho, int gam) {  // T-layout index of element (rho, gam) of a block
   const int q = ((rho >> 4) << 1) | (gam >> 4), g = gam & 15;
@@ -95,6 +98,13 @@ __device__ inline void spin_until(const int* flag, int target, int* info) {
 
 __device__ inline void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// 16-byte write-through store (global_store_dwordx4 sc1); drained by drain_stores()
+__device__ inline void st_sc1_x2(double* p, double a, double b) {
+  typedef double d2_t __attribute__((ext_vector_type(2)));
+  const d2_t v = {a, b};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
 // acc += sum_u Y(u) X(u): A operand Y, B operand X (T-layout chunks)
 template <int NU>
 __device__ inline d4_t mfma_chunks(const double* y, const double* x, d4_t acc) {
@@ -105,15 +115,19 @@ __device__ inline d4_t mfma_chunks(const double* y, const double* x, d4_t acc) {
 
 // T-layout offset of (row half h, k-chunk u) for this lane
 __device__ inline int qoff(int h, int u, int l) { return ((h * 2 + (u >> 2)) * 4 + (u & 3)) * 64 + l; }
-// column-major 32x32 scratch with an XOR swizzle (conflict-free column writes by 32 lanes)
-__device__ inline int sidx(int row, int col) { return col * RB + (row ^ col); }
+
+// optional phase timestamps (s_memrealtime, 100 MHz): trace[64 * wg + slot]
+#define RB_TRACE(slot)                                                                  \
+  do {                                                                                  \
+    if (trace && l == 0) trace[64 * i + (slot)] = __builtin_amdgcn_s_memrealtime();     \
+  } while (0)
 
 template <bool LOWER>
 __global__ __launch_bounds__(256) void k_potrf_rb(double* __restrict__ A, int n, int lda, int* __restrict__ info,
-                                                  int info_base, RbWork ws, int epoch) {
-  __shared__ double Tb[BLK];  // C(i,k) fully updated: input of step k's TRSM
-  __shared__ double Xb[BLK];  // L(i,k) of the current step; later the diagonal block
-  __shared__ double Sc[BLK];  // 32x32 scratch of the diagonal factorisation (sidx layout)
+                                                  int info_base, RbWork ws, int epoch,
+                                                  unsigned long long* __restrict__ trace) {
+  __shared__ double Tb[BLK];  // C(i,k) fully updated: input of step k's TRSM; finally C(i,i)
+  __shared__ double Xb[BLK];  // L(i,k) of the current step
   const int i = blockIdx.x;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int a = w >> 1, b = w & 1;                       // this wave's quadrant of off-diagonal blocks
@@ -125,6 +139,7 @@ __global__ __launch_bounds__(256) void k_potrf_rb(double* __restrict__ A, int n,
     return (rho < n && gam < n) ? A[gidx(rho, gam)] : (rho == gam ? 1.0 : 0.0);
   };
   const int rho_a = RB * i + 16 * a + (l & 15);  // global row of this lane in off-diagonal quadrants
+  if (w == 0) RB_TRACE(0);
 
   // ---- initial state: diagonal quadrants in registers, C(i,0) staged for the first TRSM
   d4_t dg = {0, 0, 0, 0};
@@ -142,18 +157,21 @@ __global__ __launch_bounds__(256) void k_potrf_rb(double* __restrict__ A, int n,
     // ---- wait for Z_k = inv(L(k,k))
     if (tid == 0) spin_until(ws.prog + k * PSTRIDE, base + k + 1, info);
     __syncthreads();
-    // ---- L(i,k) = C(i,k) Z_k^T (Z lower: chunks u < 4(b+1))
+    if (w == 0) RB_TRACE(1 + 3 * k);
+    // ---- L(i,k) = C(i,k) Z_k^T,  Z_k = diag(S_k) M_k  (M lower: chunks u < 4(b+1))
     d4_t acc = {0, 0, 0, 0};
     {
-      const double* Zk = ws.Z + (size_t)k * BLK;
+      const double* Mk = ws.M + (size_t)k * BLK;
       double y[8], x[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        y[u] = (u < 4 * (b + 1)) ? ld_sc1(Zk + qoff(b, u, l)) : 0.0;
+        y[u] = (u < 4 * (b + 1)) ? ld_sc1(Mk + (4 * u + (l >> 4)) * RB + 16 * b + (l & 15)) : 0.0;
         x[u] = Tb[qoff(a, u, l)];
       }
       if (b == 0) acc = mfma_chunks<4>(y, x, acc);
       else acc = mfma_chunks<8>(y, x, acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] *= ld_sc1(ws.S + (size_t)k * RB + 16 * b + (l >> 4) + 4 * r);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -161,8 +179,10 @@ __global__ __launch_bounds__(256) void k_potrf_rb(double* __restrict__ A, int n,
       if (rho_a < n) A[gidx(rho_a, RB * k + 16 * b + (l >> 4) + 4 * r)] = acc[r];  // final L(i,k)
     }
     __syncthreads();  // L(i,k) complete in LDS; Tb free
-    // ---- wave 3 publishes L(i,k) for the workgroups below (write-through, drained, flagged)
-    if (w == 3) {
+    if (w == 0) RB_TRACE(2 + 3 * k);
+    // ---- wave 3 publishes L(i,k) for the workgroups below (write-through, drained, flagged);
+    // L(i,i-1) is published later, beside the diagonal factorisation
+    if (w == 3 && k + 1 < i) {
       double* dst = ws.Lp + ((size_t)i * MAXB + k) * BLK;
 #pragma unroll
       for (int e = 0; e < 16; ++e) st_sc1(dst + e * 64 + l, Xb[e * 64 + l]);
@@ -220,77 +240,87 @@ __global__ __launch_bounds__(256) void k_potrf_rb(double* __restrict__ A, int n,
       }
       dg = mfma_chunks<8>(yd, xd, dg);
     }
+    if (w == 0) RB_TRACE(3 + 3 * k);
     // the next step starts with a workgroup barrier (after its Z poll)
   }
   __syncthreads();
   if (w < 3) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) Xb[((qa_d * 2 + qb_d) * 4 + r) * 64 + l] = dg[r];
+    for (int r = 0; r < 4; ++r) Tb[((qa_d * 2 + qb_d) * 4 + r) * 64 + l] = dg[r];
   }
   __syncthreads();
 
+  if (w == 3 && i > 0) {  // publish L(i,i-1) while wave 0 factors the diagonal block
+    double* dst = ws.Lp + ((size_t)i * MAXB + (i - 1)) * BLK;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) st_sc1(dst + e * 64 + l, Xb[e * 64 + l]);
+    drain_stores();
+    if (l == 0) st_sc1(ws.prog + i * PSTRIDE, base + i);
+    drain_stores();
+  }
   // ---- step i: Cholesky + inverse of the 32x32 diagonal block on wave 0.
   // Lanes 0..31 hold the columns of the symmetric block, lanes 32..63 the columns of M (initially
   // I).  Step c: the pivot d_c and column c are broadcast from lane c (readlane); every A column
   // j > c and every M column receives  col[t] -= A(t,c) * (col[c] / d_c),  t > c  -- the same
   // instruction for both halves, so the row operations that reduce A also build M with
   // M A M^T = D; then L = M^{-1} D^{1/2} (read off the reduced columns) and inv(L) = D^{-1/2} M
-  // come out of one pass with no separate substitution.
-  if (w != 0) return;
+  // come out of one pass with no separate substitution.  M (exact zeros above the diagonal) and
+  // S = D^{-1/2} are published as they are; consumers scale their products by S.
   const int j = l & 31;
   const bool mhalf = l >= RB;
   double col[RB];
+  double s = 0.0;
+  if (w == 0) {
+    RB_TRACE(49);
 #pragma unroll
-  for (int p = 0; p < RB; ++p)
-    col[p] = mhalf ? ((p == j) ? 1.0 : 0.0) : ((p >= j) ? Xb[tl_index(p, j)] : Xb[tl_index(j, p)]);
+    for (int p = 0; p < RB; ++p)
+      col[p] = mhalf ? ((p == j) ? 1.0 : 0.0) : ((p >= j) ? Tb[tl_index(p, j)] : Tb[tl_index(j, p)]);
 #pragma unroll
-  for (int c = 0; c < RB; ++c) {
-    const double d = readlane_d(col[c], c);
-    double akc[RB];
+    for (int c = 0; c < RB; ++c) {
+      const double d = readlane_d(col[c], c);
+      double akc[RB];
 #pragma unroll
-    for (int p = c + 1; p < RB; ++p) akc[p] = readlane_d(col[p], c);
-    const double t = col[c] * rcp_d(d);
-    if (l > c) {
+      for (int p = c + 1; p < RB; ++p) akc[p] = readlane_d(col[p], c);
+      const double t = col[c] * rcp_d(d);
+      if (l > c) {
 #pragma unroll
-      for (int p = c + 1; p < RB; ++p) col[p] = fma(-akc[p], t, col[p]);
+        for (int p = c + 1; p < RB; ++p) col[p] = fma(-akc[p], t, col[p]);
+      }
+    }
+    // lane j < 32: pivot d_j = col[j] (frozen since step j); L(p, j) = col[p] / sqrt(d_j), p >= j
+    double dj = 1.0;
+#pragma unroll
+    for (int p = 0; p < RB; ++p)
+      if (p == j) dj = col[p];
+    const bool bad = !mhalf && !(dj > 0.0);
+    const unsigned long long bm = __ballot(bad ? 1 : 0);
+    if (bm != 0 && l == 0 && info) {
+      const int c = __ffsll((long long)bm);  // first failing column + 1
+      if (RB * i + c - 1 < n) atomicCAS(info, 0, info_base + RB * i + c);
+    }
+    RB_TRACE(50);
+    s = rsqrt_d(dj);
+    if (mhalf) {
+      double* Mi = ws.M + (size_t)i * BLK + j * RB;
+#pragma unroll
+      for (int p = 0; p < RB; p += 2) st_sc1_x2(Mi + p, col[p], col[p + 1]);
+    } else {
+      st_sc1(ws.S + (size_t)i * RB + j, s);
+    }
+    drain_stores();
+  }
+  __syncthreads();  // wave 0 (M, S) and wave 3 (L(i,i-1)) drained
+  if (tid == 0) st_sc1(ws.prog + i * PSTRIDE, base + i + 1);
+  if (w == 0) {
+    RB_TRACE(51);
+    if (!mhalf) {
+#pragma unroll
+      for (int p = 0; p < RB; ++p) {
+        const int rho = RB * i + p;
+        if (p >= j && rho < n) A[gidx(rho, RB * i + j)] = col[p] * s;  // final L(i,i)
+      }
     }
   }
-  // lane j < 32: pivot d_j = col[j] (frozen since step j); L(p, j) = col[p] / sqrt(d_j), p >= j
-  double dj = 1.0;
-#pragma unroll
-  for (int p = 0; p < RB; ++p)
-    if (p == j) dj = col[p];
-  const bool bad = !mhalf && !(dj > 0.0);
-  const unsigned long long bm = __ballot(bad ? 1 : 0);
-  if (bm != 0 && l == 0 && info) {
-    const int c = __ffsll((long long)bm);  // first failing column + 1
-    if (RB * i + c - 1 < n) atomicCAS(info, 0, info_base + RB * i + c);
-  }
-  const double s = rsqrt_d(dj);
-  if (!mhalf) {
-#pragma unroll
-    for (int p = 0; p < RB; ++p) {
-      const int rho = RB * i + p;
-      if (p >= j && rho < n) A[gidx(rho, RB * i + j)] = col[p] * s;  // final L(i,i)
-    }
-  } else {
-    // inv(L)(p, j) = M(p, j) / sqrt(d_p)
-#pragma unroll
-    for (int p = 0; p < RB; ++p) Sc[sidx(p, j)] = (p >= j) ? col[p] * readlane_d(s, p) : 0.0;
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-  // publish Z_i in T-layout (write-through), drain, flag
-  double* Zi = ws.Z + (size_t)i * BLK;
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int rho = 16 * (q >> 1) + (l & 15), gam = 16 * (q & 1) + (l >> 4) + 4 * r;
-      st_sc1(Zi + (q * 4 + r) * 64 + l, Sc[sidx(rho, gam)]);
-    }
-  drain_stores();
-  if (l == 0) st_sc1(ws.prog + i * PSTRIDE, base + i + 1);
 }
 
 std::mutex g_mu;
@@ -306,7 +336,8 @@ int get_ws(RbWork* out, int* epoch, hipStream_t st) {
   if (!g_have[dev]) {
     for (int s = 0; s < NSLOT; ++s) {
       RbWork& w = g_ws[dev][s];
-      HIP_CHECK_RET(hipMalloc((void**)&w.Z, sizeof(double) * MAXB * BLK));
+      HIP_CHECK_RET(hipMalloc((void**)&w.M, sizeof(double) * MAXB * BLK));
+      HIP_CHECK_RET(hipMalloc((void**)&w.S, sizeof(double) * MAXB * RB));
       HIP_CHECK_RET(hipMalloc((void**)&w.Lp, sizeof(double) * MAXB * MAXB * BLK));
       HIP_CHECK_RET(hipMalloc((void**)&w.prog, sizeof(int) * MAXB * PSTRIDE));
       HIP_CHECK_RET(hipMemset(w.prog, 0, sizeof(int) * MAXB * PSTRIDE));
@@ -323,20 +354,216 @@ int get_ws(RbWork* out, int* epoch, hipStream_t st) {
   *epoch = (int)(g_launch & 0x1ffffff);
   return 0;
 }
+unsigned long long* g_trace = nullptr;
 }  // namespace
 
+// debug: record per-workgroup phase timestamps of the next launches into buf (64 x 8 B per WG)
+DPL_API int dpl_potrf_rb_set_trace(void* buf) {
+  g_trace = (unsigned long long*)buf;
+  return 0;
+}
+
 // Cholesky of one n x n fp64 tile (n <= 512) in place; returns -3 when the shape is not supported.
-DPL_API int dpl_potrf_tile_rb(int uplo, int n, double* A, int lda, int* info, int info_base, hipStream_t st) {
+// zbuf (optional, ZBUF doubles): receives (M_k, S_k) of every diagonal 32-block for dpl_trsm_rb.
+DPL_API int dpl_potrf_tile_rbz(int uplo, int n, double* A, int lda, int* info, int info_base, double* zbuf,
+                               hipStream_t st) {
   if (n <= 0) return 0;
   if (n > RB * MAXB) return -3;
   RbWork ws;
   int epoch = 0;
   const int rc = get_ws(&ws, &epoch, st);
   if (rc) return rc;
+  if (zbuf) {
+    ws.M = zbuf;
+    ws.S = zbuf + MAXB * BLK;
+  }
   const int nblk = cdiv(n, RB);
   if (uplo == DPL_LOWER)
-    hipLaunchKernelGGL((k_potrf_rb<true>), dim3(nblk), dim3(256), 0, st, A, n, lda, info, info_base, ws, epoch);
+    hipLaunchKernelGGL((k_potrf_rb<true>), dim3(nblk), dim3(256), 0, st, A, n, lda, info, info_base, ws, epoch, g_trace);
   else
-    hipLaunchKernelGGL((k_potrf_rb<false>), dim3(nblk), dim3(256), 0, st, A, n, lda, info, info_base, ws, epoch);
+    hipLaunchKernelGGL((k_potrf_rb<false>), dim3(nblk), dim3(256), 0, st, A, n, lda, info, info_base, ws, epoch, g_trace);
+  return (int)hipGetLastError();
+}
+
+DPL_API int dpl_potrf_tile_rb(int uplo, int n, double* A, int lda, int* info, int info_base, hipStream_t st) {
+  return dpl_potrf_tile_rbz(uplo, n, A, lda, info, info_base, nullptr, st);
+}
+
+// ================================================================== panel TRSM on the (M, S) blocks
+// B := B L^{-T} for every 16-row strip of the panel tiles below a diagonal tile factored by
+// k_potrf_rb (or prepared by k_trsm_rb_prep): the right-looking block substitution of the same
+// dataflow, without waiting -- every (M_k, S_k) and L(j,k) is final when this launch starts.
+// One wave per 16-row strip and no barrier at all: the strip (16 x 512) stays in the wave's
+// registers for the whole solve, as the T-layout quadrants of its <= 16 column blocks -- the
+// accumulator layout of the MFMA products is also the B-operand layout of the next ones, so
+// L(R,k) = C(R,k) M_k^T diag(S_k) feeds the updates C(R,j) -= L(R,k) L(j,k)^T straight from
+// registers.  L(j,k) is read from the factored tile (L2-resident, shared by every strip).
+// Reference role: the potrf_ztrsm tasks (src/zpotrf_L.jdf:194-243).
+constexpr int TR_ROWS = 16;
+#ifndef TR_GRP
+#define TR_GRP 3  // update blocks whose operands are fetched together
+#endif
+struct RbItem {
+  long long b_off;  // element offset of the strip in B
+  int rows;         // <= TR_ROWS
+  int pad;
+};
+
+template <bool LOWER, int NBLK>  // NBLK = ceil(n / 32): static, so the strip never needs runtime guards
+__global__ __launch_bounds__(64) void k_trsm_rb(const RbItem* __restrict__ items, int n,
+                                                const double* __restrict__ Lt, int ldl,
+                                                const double* __restrict__ zb, double* __restrict__ B, int ldb) {
+  const RbItem it = items[blockIdx.x];
+  const int l = threadIdx.x;
+  const long long sib = LOWER ? 1 : ldb, sjb = LOWER ? ldb : 1;
+  const long long sil = LOWER ? 1 : ldl, sjl = LOWER ? ldl : 1;
+  const int row = l & 15;
+  const bool rok = row < it.rows;
+  double* Bb = B + it.b_off;
+  const double* Sz = zb + MAXB * BLK;
+  // operands of the next solve / update are fetched one operation ahead (software pipeline)
+  auto load_m = [&](int k, double* m) {  // M_k rows of both halves (12 chunks) + the 8 S values
+    const double* Mk = zb + (size_t)k * BLK;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) m[u] = Mk[(4 * u + (l >> 4)) * RB + (l & 15)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) m[4 + u] = Mk[(4 * u + (l >> 4)) * RB + 16 + (l & 15)];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) m[12 + q] = Sz[k * RB + 16 * (q >> 2) + (l >> 4) + 4 * (q & 3)];
+  };
+  auto load_y = [&](int k, int jb, double* y) {  // L(jb, k), both row halves, T-layout chunks
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int lr = RB * jb + 16 * h + (l & 15);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) y[8 * h + u] = (lr < n) ? Lt[lr * sil + (RB * k + 4 * u + (l >> 4)) * sjl] : 0.0;
+    }
+  };
+  d4_t C[NBLK][2];
+#pragma unroll
+  for (int jb = 0; jb < NBLK; ++jb)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = RB * jb + 16 * h + (l >> 4) + 4 * r;
+        C[jb][h][r] = (rok && col < n) ? Bb[row * sib + col * sjb] : 0.0;
+      }
+  double mc[20];
+#pragma unroll
+  for (int k = 0; k < NBLK; ++k) {
+    load_m(k, mc);
+    // L(R,k) = C(R,k) M_k^T diag(S_k)
+    double x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = C[k][u >> 2][u & 3];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      d4_t acc = {0, 0, 0, 0};
+      if (h == 0) acc = mfma_chunks<4>(mc, x, acc);
+      else acc = mfma_chunks<8>(mc + 4, x, acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = 16 * h + (l >> 4) + 4 * r;
+        acc[r] *= mc[12 + 4 * h + r];
+        if (rok && RB * k + c < n) Bb[row * sib + (RB * k + c) * sjb] = acc[r];  // final L(R,k)
+      }
+      C[k][h] = acc;
+    }
+    double xm[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xm[u] = -C[k][u >> 2][u & 3];
+    // updates in groups of TR_GRP blocks: the group's operand loads are all in flight together
+#pragma unroll
+    for (int j0 = k + 1; j0 < NBLK; j0 += TR_GRP) {
+      double y[TR_GRP][16];
+#pragma unroll
+      for (int g = 0; g < TR_GRP; ++g)
+        if (j0 + g < NBLK) load_y(k, j0 + g, y[g]);
+#pragma unroll
+      for (int g = 0; g < TR_GRP; ++g)
+        if (j0 + g < NBLK) {
+          C[j0 + g][0] = mfma_chunks<8>(y[g], xm, C[j0 + g][0]);
+          C[j0 + g][1] = mfma_chunks<8>(y[g] + 8, xm, C[j0 + g][1]);
+        }
+    }
+  }
+}
+
+// (M_k, S_k) of every 32x32 diagonal block of a factored tile L (for ranks that received L):
+// row elimination of L_kk applied to I (M L_kk = diag(L_kk)), so inv(L_kk) = diag(1 / L_kk(p,p)) M.
+template <bool LOWER>
+__global__ __launch_bounds__(64) void k_trsm_rb_prep(int n, const double* __restrict__ Lt, int ldl,
+                                                     double* __restrict__ zb) {
+  const int k = blockIdx.x, l = threadIdx.x;
+  const long long sil = LOWER ? 1 : ldl, sjl = LOWER ? ldl : 1;
+  const int j = l & 31;
+  const bool mhalf = l >= RB;
+  double col[RB];
+#pragma unroll
+  for (int p = 0; p < RB; ++p) {
+    const int gr = RB * k + p, gc = RB * k + j;
+    const double v = (gr < n && gc < n) ? Lt[gr * sil + gc * sjl] : (gr == gc ? 1.0 : 0.0);
+    col[p] = mhalf ? ((p == j) ? 1.0 : 0.0) : ((p >= j) ? v : 0.0);
+  }
+#pragma unroll
+  for (int c = 0; c < RB; ++c) {
+    const double d = readlane_d(col[c], c);
+    double akc[RB];
+#pragma unroll
+    for (int p = c + 1; p < RB; ++p) akc[p] = readlane_d(col[p], c);
+    const double t = col[c] * rcp_d(d);
+    if (mhalf) {
+#pragma unroll
+      for (int p = c + 1; p < RB; ++p) col[p] = fma(-akc[p], t, col[p]);
+    }
+  }
+  double dj = 1.0;
+#pragma unroll
+  for (int p = 0; p < RB; ++p)
+    if (p == j) dj = col[p];
+  if (mhalf) {
+    double* Mk = zb + (size_t)k * BLK + j * RB;
+#pragma unroll
+    for (int p = 0; p < RB; ++p) Mk[p] = col[p];
+  } else {
+    zb[MAXB * BLK + k * RB + j] = rcp_d(dj);
+  }
+}
+
+DPL_API int dpl_potrf_zbuf_size() { return ZBUF; }
+
+DPL_API int dpl_trsm_rb_prep(int uplo, int n, const double* L, int ldl, double* zbuf, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (n > RB * MAXB) return -3;
+  const int nblk = cdiv(n, RB);
+  if (uplo == DPL_LOWER)
+    hipLaunchKernelGGL((k_trsm_rb_prep<true>), dim3(nblk), dim3(64), 0, st, n, L, ldl, zbuf);
+  else
+    hipLaunchKernelGGL((k_trsm_rb_prep<false>), dim3(nblk), dim3(64), 0, st, n, L, ldl, zbuf);
+  return (int)hipGetLastError();
+}
+
+// items: device RbItem[nrb] (16-row strips of the panel tiles, offsets relative to B)
+DPL_API int dpl_trsm_rb(int uplo, int n, const double* L, int ldl, const double* zbuf, int nrb, const void* items,
+                        double* B, int ldb, hipStream_t st) {
+  if (n <= 0 || nrb <= 0) return 0;
+  if (n > RB * MAXB) return -3;
+  const int nblk = cdiv(n, RB);
+  const RbItem* it = (const RbItem*)items;
+#define TRSM_RB_CASE(NB_)                                                                              \
+  case NB_:                                                                                            \
+    if (uplo == DPL_LOWER)                                                                             \
+      hipLaunchKernelGGL((k_trsm_rb<true, NB_>), dim3(nrb), dim3(64), 0, st, it, n, L, ldl, zbuf, B, ldb);  \
+    else                                                                                               \
+      hipLaunchKernelGGL((k_trsm_rb<false, NB_>), dim3(nrb), dim3(64), 0, st, it, n, L, ldl, zbuf, B, ldb); \
+    break;
+  switch (nblk) {
+    TRSM_RB_CASE(1) TRSM_RB_CASE(2) TRSM_RB_CASE(3) TRSM_RB_CASE(4) TRSM_RB_CASE(5) TRSM_RB_CASE(6)
+    TRSM_RB_CASE(7) TRSM_RB_CASE(8) TRSM_RB_CASE(9) TRSM_RB_CASE(10) TRSM_RB_CASE(11) TRSM_RB_CASE(12)
+    TRSM_RB_CASE(13) TRSM_RB_CASE(14) TRSM_RB_CASE(15) TRSM_RB_CASE(16)
+    default: return -3;
+  }
+#undef TRSM_RB_CASE
   return (int)hipGetLastError();
 }

@@ -154,6 +154,13 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
         dbuf = torch.zeros(nbe, dtype=A.dtype, device=dev)
         tp._buffers = (GX, dbuf)
 
+    # fp64 tiles <= 512 on the GPU: dataflow tile POTRF + register-resident panel TRSM sharing the
+    # inverted diagonal 32-blocks (csrc/kernels/potrf_rb.hip); zbufs alternate with k's parity
+    use_rb = ops.rb_ok(A.data, A.mb) and A.mb == A.nb
+    if use_rb:
+        zsz = ops.rb_zbuf_size()
+        zbufs = torch.empty(2 * zsz, dtype=torch.float64, device=dev)
+        tp._zbufs = zbufs
     tri_mask = MASK_LOWER if lower else MASK_UPPER
     tA, tB = (dplasmaNoTrans, dplasmaConjTrans) if lower else (dplasmaConjTrans, dplasmaNoTrans)
     panels = {}       # k -> _Panel (where panel k's tiles live for the updates)
@@ -190,7 +197,11 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                 off = A.offset(*dk)
 
                 def f_potrf(off=off, kb=kb, k=k):
-                    potrf_diag(uplo, A.data, off, kb, A.ld, info, k * A.mb)
+                    if use_rb:
+                        ops.potrf_tile(uplo, A.data, off, kb, A.ld, info, k * A.mb,
+                                       zbuf=zbufs[(k % 2) * zsz:(k % 2 + 1) * zsz])
+                    else:
+                        potrf_diag(uplo, A.data, off, kb, A.ld, info, k * A.mb)
                 t_potrf = tp.task(f"POTRF({k})", diag_stream, f_potrf, [gate], prio=3)
             # ---------------- local panel tiles (i > k) of my process row/col
             mine = [i for i in range(k + 1, nt) if in_panel_cross and owner_of_panel_line(i) == my_line]
@@ -212,7 +223,19 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                 else:
                     t_db = t_potrf
                     tri_base, tri_ld, tri_off = A.data, A.ld, A.offset(*dk)
-                if mine:
+                if mine and use_rb:
+                    # row blocks of the panel tiles (lower: rows of L(i,k); upper: columns of U(k,i))
+                    rbp = ops.RbPanel(uplo, [(A.offset(*tcoord(i, k)),
+                                              A.tile_rows(i) if lower else A.tile_cols(i)) for i in mine], A.ld)
+                    zk = zbufs[(k % 2) * zsz:(k % 2 + 1) * zsz]
+
+                    def f_trsm(rbp=rbp, tri_base=tri_base, tri_ld=tri_ld, tri_off=tri_off, kb=kb, zk=zk,
+                               own=own_diag and tri_base is A.data):
+                        if not own:  # the diagonal tile arrived by broadcast: invert its 32-blocks here
+                            ops.trsm_rb_prep(uplo, kb, tri_base, tri_off, tri_ld, zk)
+                        ops.trsm_rb(uplo, kb, tri_base, tri_off, tri_ld, zk, rbp, A.data, A.ld)
+                    t_trsm = tp.task(f"TRSM({k})", "panel", f_trsm, [t_db, gate], prio=2)
+                elif mine:
                     tb = TileBatch()
                     for i in mine:
                         cc = tcoord(i, k)

@@ -86,14 +86,23 @@ def gemm(transA: int, transB: int, alpha, A: torch.Tensor, lda: int, B: torch.Te
 
 
 # ----------------------------------------------------------------------------- POTRF
-def potrf_tile(uplo: int, A: torch.Tensor, off: int, n: int, lda: int, info: torch.Tensor, info_base: int):
-    """Cholesky of one diagonal tile in place; ``info`` (int32 tensor, 1 elem) gets base + first bad col."""
+def potrf_tile(uplo: int, A: torch.Tensor, off: int, n: int, lda: int, info: torch.Tensor, info_base: int,
+               zbuf: torch.Tensor = None):
+    """Cholesky of one diagonal tile in place; ``info`` (int32 tensor, 1 elem) gets base + first bad col.
+
+    ``zbuf`` (fp64 GPU tiles with n <= 512, see :func:`rb_zbuf`): also receive the inverted
+    diagonal 32-blocks for :func:`trsm_rb`."""
     if n <= 0:
         return
     if _is_gpu(A):
         lib = _lib.load()
-        rc = lib.dpl_potrf_tile(_lib.prec_code(A.dtype), uplo, n, A.data_ptr(), int(off), lda, info.data_ptr(),
-                                int(info_base), _lib.stream_ptr())
+        if zbuf is not None:
+            assert rb_ok(A, n) and zbuf.dtype == torch.float64 and zbuf.numel() >= rb_zbuf_size()
+            rc = lib.dpl_potrf_tile_rbz(uplo, n, A.data_ptr() + 8 * int(off), lda, info.data_ptr(), int(info_base),
+                                        zbuf.data_ptr(), _lib.stream_ptr())
+        else:
+            rc = lib.dpl_potrf_tile(_lib.prec_code(A.dtype), uplo, n, A.data_ptr(), int(off), lda, info.data_ptr(),
+                                    int(info_base), _lib.stream_ptr())
         _lib.check(rc, "potrf_tile")
         return
     t = _view(A, off, n, n, lda)
@@ -178,6 +187,63 @@ def potrf_tile_blocked(uplo: int, A: torch.Tensor, off: int, n: int, lda: int, i
             continue
         trsm(side, uplo, dplasmaConjTrans, dplasmaNonUnit, 1.0, V, lda, V, lda, tb)
         gemm(tA, tB, -1.0, V, lda, V, lda, 1.0, V, lda, gb)
+
+
+# ----------------------------------------------------------------------------- POTRF panel TRSM (rb)
+RB_ROWS = 16  # strip height of the panel TRSM kernel (csrc/kernels/potrf_rb.hip k_trsm_rb)
+_RB_ITEM = np.dtype([("b_off", np.int64), ("rows", np.int32), ("pad", np.int32)])
+
+
+def rb_ok(A: torch.Tensor, n: int) -> bool:
+    """fp64 GPU tiles of order <= 512 use the dataflow POTRF / panel-TRSM kernels."""
+    return _is_gpu(A) and A.dtype == torch.float64 and 0 < n <= 512
+
+
+def rb_zbuf_size() -> int:
+    return int(_lib.load().dpl_potrf_zbuf_size())
+
+
+class RbPanel:
+    """16-row strips of the panel tiles B_i (m_i x n) solved by :func:`trsm_rb`: for lower storage a
+    strip is 16 consecutive rows of a tile (offset b_off + r); for upper storage (B_i = A(k, i),
+    solved from the left) the same thing on the transposed view (16 consecutive columns)."""
+
+    def __init__(self, uplo: int, tiles, ldb: int):
+        rows = []
+        for b_off, m in tiles:
+            for r0 in range(0, m, RB_ROWS):
+                off = b_off + (r0 if uplo == dplasmaLower else r0 * ldb)
+                rows.append((off, min(RB_ROWS, m - r0), 0))
+        self.items = np.array(rows, dtype=_RB_ITEM)
+        self._dev = {}
+
+    def __len__(self):
+        return len(self.items)
+
+    def device(self, dev):
+        key = str(dev)
+        t = self._dev.get(key)
+        if t is None:
+            t = self._dev[key] = torch.from_numpy(self.items.view(np.uint8).copy()).to(dev)
+        return t
+
+
+def trsm_rb_prep(uplo: int, n: int, L: torch.Tensor, l_off: int, ldl: int, zbuf: torch.Tensor):
+    """Inverted diagonal 32-blocks of an already factored tile (ranks that received it)."""
+    rc = _lib.load().dpl_trsm_rb_prep(uplo, n, L.data_ptr() + 8 * int(l_off), ldl, zbuf.data_ptr(),
+                                      _lib.stream_ptr())
+    _lib.check(rc, "trsm_rb_prep")
+
+
+def trsm_rb(uplo: int, n: int, L: torch.Tensor, l_off: int, ldl: int, zbuf: torch.Tensor, panel: RbPanel,
+            B: torch.Tensor, ldb: int):
+    """Panel solve of the Cholesky step: B_i := B_i L^{-H} (lower) / U^{-H} B_i (upper) for every panel
+    tile of ``panel``, L the factored n x n tile at L[l_off] and ``zbuf`` its inverted 32-blocks."""
+    if len(panel) == 0:
+        return
+    rc = _lib.load().dpl_trsm_rb(uplo, n, L.data_ptr() + 8 * int(l_off), ldl, zbuf.data_ptr(), len(panel),
+                                 panel.device(B.device).data_ptr(), B.data_ptr(), ldb, _lib.stream_ptr())
+    _lib.check(rc, "trsm_rb")
 
 
 # ----------------------------------------------------------------------------- TRSM

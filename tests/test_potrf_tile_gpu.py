@@ -110,3 +110,49 @@ def test_potrf_tile_under_load():
     for b in bufs:
         got = torch.as_strided(b, (n, n), (1, lda), 0).tril()
         assert (got - Lref).abs().max().item() < 1e-12
+
+
+@pytest.mark.parametrize("uplo", [dplasmaLower, dplasmaUpper])
+@pytest.mark.parametrize("n", [512, 100, 32])
+@pytest.mark.parametrize("prep", [False, True])
+def test_trsm_rb_panel(uplo, n, prep):
+    """Panel solve of the Cholesky step (k_trsm_rb) against torch.linalg.solve_triangular, with the
+    inverted diagonal blocks from the tile factorisation itself or from k_trsm_rb_prep."""
+    from dplasma_amd.ops import tile_ops as ops
+    S = _spd(n, seed=7 + n)
+    ms = [n, 77, n, 1]
+    ld = n + sum(ms) + 5
+    g = torch.Generator(device="cpu").manual_seed(n)
+    Bs = [torch.randn(m, n, dtype=torch.float64, generator=g).cuda() for m in ms]  # lower view: m x n
+    # storage: tile 0 = diagonal, then the panel tiles (lower: below it; upper: to its right)
+    buf = torch.zeros(ld * (n * 5 + 100), dtype=torch.float64, device="cuda")
+    def view(off, r, c):
+        return torch.as_strided(buf, (r, c), (1, ld), off)
+    view(0, n, n).copy_(S)
+    offs, tiles = [], []
+    if uplo == dplasmaLower:
+        r0 = n
+        for B, m in zip(Bs, ms):
+            view(r0, m, n).copy_(B)
+            offs.append(r0); tiles.append((r0, m)); r0 += m
+    else:
+        c0 = n
+        for B, m in zip(Bs, ms):
+            view(c0 * ld, n, m).copy_(B.T)
+            offs.append(c0 * ld); tiles.append((c0 * ld, m)); c0 += m
+    info = torch.zeros(1, dtype=torch.int32, device="cuda")
+    zbuf = torch.zeros(ops.rb_zbuf_size(), dtype=torch.float64, device="cuda")
+    ops.potrf_tile(uplo, buf, 0, n, ld, info, 0, zbuf=zbuf)
+    if prep:
+        zbuf.fill_(float("nan"))
+        ops.trsm_rb_prep(uplo, n, buf, 0, ld, zbuf)
+    panel = ops.RbPanel(uplo, tiles, ld)
+    ops.trsm_rb(uplo, n, buf, 0, ld, zbuf, panel, buf, ld)
+    torch.cuda.synchronize()
+    assert int(info.item()) == 0
+    L = torch.linalg.cholesky(S)
+    for B, m, off in zip(Bs, ms, offs):
+        ref = torch.linalg.solve_triangular(L, B.T, upper=False).T  # B L^{-T}
+        got = view(off, m, n) if uplo == dplasmaLower else view(off, n, m).T
+        err = (got - ref).abs().max().item() / max(1.0, ref.abs().max().item())
+        assert err < 1e-12, (m, err)
