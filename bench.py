@@ -45,6 +45,7 @@ def main():
     ap.add_argument("-P", type=int, default=None)
     ap.add_argument("--no-check", dest="check", action="store_false",
                     help="skip the (untimed, default-on) residual check of the last factorisation")
+    ap.add_argument("--check", dest="check", action="store_true", help="(default) verify the last factorisation")
     ap.add_argument("--trace", default=None, help="write a Chrome trace of one step to this file")
     ap.add_argument("--cpu", action="store_true",
                     help="dry run of the same multi-rank path on CPU ranks (gloo) -- plumbing tests only")

@@ -13,13 +13,12 @@
 #include <cstdlib>
 #include <string>
 
-struct dplasma_context_s { PyObject* obj; };
-struct dplasma_desc_s { PyObject* obj; };
-
 static PyObject* g_capi = nullptr;   // module dplasma_amd.capi
 static thread_local std::string g_err;
 
-static void keep_error() {
+void dpl_keep_error();
+static void keep_error() { dpl_keep_error(); }
+void dpl_keep_error() {
   if (!PyErr_Occurred()) return;
   PyObject *t, *v, *tb;
   PyErr_Fetch(&t, &v, &tb);
@@ -46,6 +45,8 @@ static std::string lib_root() {
   return ".";
 }
 
+static bool ensure_python();
+bool dpl_ensure_python() { return ensure_python(); }
 static bool ensure_python() {
   if (!Py_IsInitialized()) {
     Py_InitializeEx(0);
@@ -76,8 +77,16 @@ PyObject* dpl_arg_real(double v) { return PyFloat_FromDouble(v); }
 PyObject* dpl_arg_cplx(dplasma_complex64_t v) { return PyComplex_FromDoubles(__real__ v, __imag__ v); }
 PyObject* dpl_arg_cplx(dplasma_complex32_t v) { return PyComplex_FromDoubles(__real__ v, __imag__ v); }
 
+PyObject* dpl_arg_ptr(const void* p) { return PyLong_FromUnsignedLongLong((unsigned long long)(uintptr_t)p); }
+PyObject* dpl_arg_str(const char* s, int len) { return PyUnicode_FromStringAndSize(s ? s : "", s ? len : 0); }
+
 static PyObject* call_obj(dplasma_context_t* ctx, const char* fname, const char* opname,
                           std::initializer_list<PyObject*> args) {
+  if (!g_capi) {  // dplasma_amd could not be imported (or the interpreter is not up)
+    for (PyObject* a : args) Py_XDECREF(a);
+    if (g_err.empty()) g_err = "dplasma_amd is not initialised (dplasma_init failed or was not called)";
+    return nullptr;
+  }
   const size_t n = args.size() + (ctx ? 1 : 0) + (opname ? 1 : 0);
   PyObject* tup = PyTuple_New((Py_ssize_t)n);
   size_t i = 0;
@@ -100,6 +109,7 @@ static PyObject* call_obj(dplasma_context_t* ctx, const char* fname, const char*
 }
 
 int dpl_call_int(dplasma_context_t* ctx, const char* name, std::initializer_list<PyObject*> args) {
+  dpl_ensure_python();
   PyGILState_STATE st = PyGILState_Ensure();
   g_err.clear();
   PyObject* r = call_obj(ctx, "call", name, args);
@@ -111,6 +121,7 @@ int dpl_call_int(dplasma_context_t* ctx, const char* name, std::initializer_list
 }
 
 double dpl_call_real(dplasma_context_t* ctx, const char* name, std::initializer_list<PyObject*> args) {
+  dpl_ensure_python();
   PyGILState_STATE st = PyGILState_Ensure();
   g_err.clear();
   PyObject* r = call_obj(ctx, "call", name, args);
@@ -120,12 +131,87 @@ double dpl_call_real(dplasma_context_t* ctx, const char* name, std::initializer_
   return v;
 }
 
+PyObject* dpl_call_fn(const char* fname, std::initializer_list<PyObject*> args) {
+  g_err.clear();
+  return call_obj(nullptr, fname, nullptr, args);
+}
+
+dplasma_taskpool_t* dpl_call_new(dplasma_context_t* ctx, const char* name, std::initializer_list<PyObject*> args) {
+  g_err.clear();
+  PyObject* o = call_obj(ctx, "new", name, args);
+  if (!o) return nullptr;
+  dplasma_taskpool_t* tp = new dplasma_taskpool_s;
+  tp->obj = o;
+  return tp;
+}
+
 extern "C" {
 
 DPL_CAPI const char* dplasma_last_error(void) { return g_err.c_str(); }
 
+// ---- taskpool lifecycle (dplasma_<p><op>_New / _Destruct, parsec_context_add_taskpool / start / wait)
+DPL_CAPI void dplasma_taskpool_free(dplasma_taskpool_t* tp) {
+  if (!tp) return;
+  DplGil g;
+  PyObject* r = call_obj(nullptr, "destruct", nullptr, {(Py_INCREF(tp->obj), tp->obj)});
+  Py_XDECREF(r);
+  Py_DECREF(tp->obj);
+  delete tp;
+}
+
+DPL_CAPI int dplasma_context_add_taskpool(dplasma_context_t* ctx, dplasma_taskpool_t* tp) {
+  if (!ctx || !tp) return -1;
+  DplGil g;
+  g_err.clear();
+  PyObject* r = call_obj(ctx, "add_taskpool", nullptr, {(Py_INCREF(tp->obj), tp->obj)});
+  const int v = r ? 0 : -1;
+  Py_XDECREF(r);
+  return v;
+}
+
+static int ctx_call(dplasma_context_t* ctx, const char* fn) {
+  if (!ctx) return -1;
+  DplGil g;
+  g_err.clear();
+  PyObject* r = call_obj(ctx, fn, nullptr, {});
+  const int v = r ? (int)PyLong_AsLong(r) : -1;
+  Py_XDECREF(r);
+  return v;
+}
+DPL_CAPI int dplasma_context_start(dplasma_context_t* ctx) { return ctx_call(ctx, "start"); }
+DPL_CAPI int dplasma_context_wait(dplasma_context_t* ctx) { return ctx_call(ctx, "wait"); }
+
+// info / result of a completed taskpool (what the blocking call would have returned)
+DPL_CAPI int dplasma_taskpool_result(const dplasma_taskpool_t* tp) {
+  if (!tp) return -1;
+  DplGil g;
+  g_err.clear();
+  PyObject* r = call_obj(nullptr, "tp_result", nullptr, {(Py_INCREF(tp->obj), tp->obj)});
+  const int v = r ? (int)PyLong_AsLong(r) : -1;
+  Py_XDECREF(r);
+  return v;
+}
+
+// descriptor over caller-owned memory in ScaLAPACK / LAPACK local layout (column-major, lld):
+// on_device != 0 -> a device pointer of the context's GPU (zero copy), else host memory.
+DPL_CAPI dplasma_desc_t* dplasma_desc_block_cyclic_lapack(dplasma_context_t* ctx, int prec, int mb, int nb, int m,
+                                                          int n, int P, int Q, int ip, int jq, void* data, int lld,
+                                                          int on_device) {
+  DplGil g;
+  g_err.clear();
+  PyObject* o = call_obj(ctx, "desc_lapack", nullptr,
+                         {PyLong_FromLong(prec), PyLong_FromLong(mb), PyLong_FromLong(nb), PyLong_FromLong(m),
+                          PyLong_FromLong(n), PyLong_FromLong(P), PyLong_FromLong(Q), PyLong_FromLong(ip),
+                          PyLong_FromLong(jq), dpl_arg_ptr(data), PyLong_FromLong(lld), PyLong_FromLong(on_device)});
+  if (!o) return nullptr;
+  dplasma_desc_t* d = new dplasma_desc_s;
+  d->obj = o;
+  return d;
+}
+
 DPL_CAPI dplasma_context_t* dplasma_init(int nb_cores, int gpus) {
   if (!ensure_python()) return nullptr;
+  dpl_ensure_python();
   PyGILState_STATE st = PyGILState_Ensure();
   PyObject* o = call_obj(nullptr, "init", nullptr, {PyLong_FromLong(nb_cores), PyLong_FromLong(gpus)});
   dplasma_context_t* c = nullptr;
@@ -136,6 +222,7 @@ DPL_CAPI dplasma_context_t* dplasma_init(int nb_cores, int gpus) {
 
 DPL_CAPI void dplasma_fini(dplasma_context_t* ctx) {
   if (!ctx) return;
+  dpl_ensure_python();
   PyGILState_STATE st = PyGILState_Ensure();
   PyObject* r = call_obj(ctx, "fini", nullptr, {});
   Py_XDECREF(r);
@@ -146,6 +233,7 @@ DPL_CAPI void dplasma_fini(dplasma_context_t* ctx) {
 
 static int ctx_attr(const dplasma_context_t* ctx, const char* a) {
   if (!ctx) return -1;
+  dpl_ensure_python();
   PyGILState_STATE st = PyGILState_Ensure();
   PyObject* v = PyObject_GetAttrString(ctx->obj, a);
   const int r = v ? (int)PyLong_AsLong(v) : -1;
@@ -158,6 +246,7 @@ DPL_CAPI int dplasma_context_world(const dplasma_context_t* ctx) { return ctx_at
 
 DPL_CAPI dplasma_desc_t* dplasma_desc_block_cyclic(dplasma_context_t* ctx, int prec, int mb, int nb, int m, int n,
                                                    int P, int Q, dplasma_enum_t uplo) {
+  dpl_ensure_python();
   PyGILState_STATE st = PyGILState_Ensure();
   PyObject* o = call_obj(ctx, "desc_block_cyclic", nullptr,
                          {PyLong_FromLong(prec), PyLong_FromLong(mb), PyLong_FromLong(nb), PyLong_FromLong(m),
@@ -169,6 +258,7 @@ DPL_CAPI dplasma_desc_t* dplasma_desc_block_cyclic(dplasma_context_t* ctx, int p
 }
 
 DPL_CAPI dplasma_desc_t* dplasma_desc_ipiv(dplasma_context_t* ctx, int mb, int nb, int m, int n, int P, int Q) {
+  dpl_ensure_python();
   PyGILState_STATE st = PyGILState_Ensure();
   PyObject* o = call_obj(ctx, "desc_int", nullptr,
                          {PyLong_FromLong(mb), PyLong_FromLong(nb), PyLong_FromLong(m), PyLong_FromLong(n),
@@ -181,6 +271,7 @@ DPL_CAPI dplasma_desc_t* dplasma_desc_ipiv(dplasma_context_t* ctx, int mb, int n
 
 DPL_CAPI void dplasma_desc_destroy(dplasma_desc_t* A) {
   if (!A) return;
+  dpl_ensure_python();
   PyGILState_STATE st = PyGILState_Ensure();
   Py_DECREF(A->obj);
   PyGILState_Release(st);
@@ -188,6 +279,7 @@ DPL_CAPI void dplasma_desc_destroy(dplasma_desc_t* A) {
 }
 
 static int desc_io(const dplasma_desc_t* A, const void* host, int lda, const char* fn) {
+  dpl_ensure_python();
   PyGILState_STATE st = PyGILState_Ensure();
   PyObject* r = call_obj(nullptr, fn, nullptr,
                          {dpl_arg_desc(A), PyLong_FromUnsignedLongLong((unsigned long long)(uintptr_t)host),

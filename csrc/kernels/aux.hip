@@ -395,3 +395,5 @@ DPL_API int dpl_stream_cumask(const unsigned* mask, int nwords, void** out) {
   *out = (void*)s;
   return (int)e;
 }
+
+DPL_API int dpl_stream_destroy(void* s) { return (int)hipStreamDestroy((hipStream_t)s); }

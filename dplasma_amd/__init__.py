@@ -10,7 +10,7 @@ Layout:
   ops/       HIP/CDNA4 tile kernels (batched) + CPU reference tile kernels
   models/    algorithm families (Cholesky, LU, QR, BLAS3, norms, generators ...)
   parallel/  process grid communication (RCCL/xGMI via torch.distributed)
-  runtime/   taskpools, stream-program executor, native engine bridge, DTD
+  runtime/   taskpools, stream-program executor, tile DAGs (native level analysis), DTD
   utils/     flops, LCG generators, options, tracing
 """
 from .constants import *  # noqa: F401,F403

@@ -96,9 +96,11 @@ class Context:
         self.info = Info()
 
     def _reserve_cus(self, ndiag: int):
-        """Opt-in (DPLASMA_DIAG_CUS=n): a "diag" stream on CUs [0, n) for the latency-bound
-        diagonal-tile factorisations and an "update" stream on the other CUs, so the single-
-        workgroup tile kernel does not share SIMDs with the trailing-update GEMM (HIP CU masks)."""
+        """Opt-in (DPLASMA_DIAG_CUS=n), POTRF only: a "diag" stream on CUs [0, n) for the
+        latency-bound diagonal-tile factorisations and a "potrf_update" stream on the other CUs
+        for POTRF's bulk trailing updates, so the tile kernel does not share SIMDs with the GEMM
+        (HIP CU masks).  The shared "update" stream stays unmasked: the persistent LU / QR panel
+        kernels size their grids for every CU and must not run on a masked stream."""
         import ctypes
         from .ops import _lib
         ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
@@ -111,13 +113,26 @@ class Context:
                 upd[c // 32] |= 1 << (c % 32)
         lib = _lib.load()
         made = {}
-        for name, m in (("diag", diag), ("update", upd)):
+        for name, m in (("diag", diag), ("potrf_update", upd)):
             arr = (ctypes.c_uint * nw)(*m)
             out = ctypes.c_void_p()
             rc = lib.dpl_stream_cumask(ctypes.cast(arr, ctypes.c_void_p), nw, ctypes.byref(out))
             _lib.check(rc, "stream_cumask")
             made[name] = torch.cuda.ExternalStream(out.value, device=self.device)
         self.streams.update(made)
+        self._owned_streams = [s.cuda_stream for s in made.values()]
+
+    def release(self):
+        """Destroy the HIP streams this context created itself (CU-masked ones)."""
+        owned = getattr(self, "_owned_streams", [])
+        if owned:
+            from .ops import _lib
+            torch.cuda.synchronize(self.device)
+            for name in ("diag", "potrf_update"):
+                self.streams.pop(name, None)
+            for s in owned:
+                _lib.load().dpl_stream_destroy(s)
+            self._owned_streams = []
 
     # ------------------------------------------------------------------ comms
     def _build_groups(self):
@@ -193,5 +208,7 @@ def fini(ctx: Optional[Context] = None):
     path = os.environ.get("DPLASMA_PROFILE")
     if c is not None and c.profiling is not None and path:
         c.profiling.dump(path if c.world == 1 else path)
+    if c is not None:
+        c.release()
     if ctx is None or ctx is _DEFAULT:
         _DEFAULT = None

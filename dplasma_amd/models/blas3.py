@@ -270,33 +270,6 @@ def her2k(ctx, uplo, trans, alpha, A, B, beta, C):
 
 
 # ----------------------------------------------------------------------------- GER
-def _ger_New(ctx, alpha, X, Y, A, conj):
-    """A := alpha x y^H + A (gerc) / alpha x y^T + A (geru); X is m x 1, Y is n x 1."""
-    prog = TileProgram(ctx, "gerc" if conj else "geru")
-    prog.flops = 8.0 * A.m * A.n if A.dtype.is_complex else 2.0 * A.m * A.n
-    s = prog.stage("ger")
-    for (m, n) in _all_tiles(A):
-        s.gemm((A, m, n), [((X, m, 0), N_, (Y, n, 0), C_ if conj else T_)], alpha=alpha, beta=1.0)
-    return prog.compile()
-
-
-def gerc_New(ctx, alpha, X, Y, A):
-    return _ger_New(ctx, alpha, X, Y, A, True)
-
-
-def geru_New(ctx, alpha, X, Y, A):
-    return _ger_New(ctx, alpha, X, Y, A, False)
-
-
-def gerc(ctx, alpha, X, Y, A):
-    return gerc_New(ctx, alpha, X, Y, A).execute(ctx)
-
-
-def geru(ctx, alpha, X, Y, A):
-    return geru_New(ctx, alpha, X, Y, A).execute(ctx)
-
-
-# ----------------------------------------------------------------------------- GER
 def gerc_New(ctx, alpha, X, Y, A):
     """A := alpha x y^H + A (dplasma_zgerc_New, src/zger.jdf): X is M x 1, Y is N x 1 -- a K = 1 GEMM."""
     from .gemm import gemm_New

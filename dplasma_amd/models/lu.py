@@ -370,6 +370,23 @@ def _permute_rows_2d(ctx, A, dst_rows, src_rows, coltiles):
             slot += len(recvs[q]) * nct
 
 
+def _reduce_info(info: torch.Tensor) -> int:
+    """Combine the per-rank LU info: a negative code on ANY rank (-1000: a persistent panel
+    kernel's grid barrier timed out, the factorisation is corrupt) raises; otherwise the smallest
+    positive singular-pivot index wins (LAPACK reports the first zero pivot)."""
+    v = info.to(torch.int64)
+    neg = torch.where(v < 0, v, torch.zeros_like(v))
+    comm.allreduce(neg, op=torch.distributed.ReduceOp.MIN)
+    if int(neg.item()) < 0:
+        raise RuntimeError(f"getrf: panel kernel failed on some rank (info={int(neg.item())}): the grid of "
+                           "the persistent panel kernel was not co-resident")
+    big = torch.iinfo(torch.int64).max
+    pos = torch.where(v > 0, v, torch.full_like(v, big))
+    comm.allreduce(pos, op=torch.distributed.ReduceOp.MIN)
+    r = int(pos.item())
+    return 0 if r == big else r
+
+
 def getrf_ptgpanel_New(ctx, A, IPIV, info_out=None):
     """Partial-pivoting LU on any P x Q grid (dplasma_zgetrf_ptgpanel_New).
 
@@ -388,9 +405,7 @@ def getrf_ptgpanel_New(ctx, A, IPIV, info_out=None):
         for (m, n) in IPIV.local_tiles():
             c0 = n * IPIV.nb
             IPIV.tile(m, n).copy_(st.ipiv_all[c0: c0 + IPIV.tile_cols(n)].view(1, -1).to(IPIV.device))
-        v = info.clone()
-        comm.allreduce(v, op=torch.distributed.ReduceOp.MAX)
-        r = int(v.item())
+        r = _reduce_info(info)
         if info_out is not None:
             info_out[0] = r
         return r
@@ -427,9 +442,7 @@ def getrf_1d_New(ctx, A, IPIV, info_out=None):
         for (m, n) in IPIV.local_tiles():
             c0 = n * IPIV.nb
             IPIV.tile(m, n).copy_(st.ipiv_all[c0: c0 + IPIV.tile_cols(n)].view(1, -1).to(IPIV.device))
-        v = info.clone()
-        comm.allreduce(v, op=torch.distributed.ReduceOp.MAX)
-        r = int(v.item())
+        r = _reduce_info(info)
         if info_out is not None:
             info_out[0] = r
         return r

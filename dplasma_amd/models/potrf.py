@@ -84,6 +84,7 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
     tp = Taskpool("potrf", ctx)
     # diagonal tiles on the CU-reserved stream when DPLASMA_DIAG_CUS is set (context._reserve_cus)
     diag_stream = "diag" if "diag" in getattr(ctx, "streams", {}) else "panel"
+    upd_stream = "potrf_update" if "potrf_update" in getattr(ctx, "streams", {}) else "update"
     tp.flops = flops(A.prec, "potrf", A.n)
     nt = A.nt
     dev = A.device
@@ -328,10 +329,10 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
         deps = [gate, last_panel]
         t_next = None
         if len(nxt):
-            t_next = tp.task(f"NEXT({b})", "update", lambda bt=nxt, bs=base, l=ld: f_upd(bt, bs, l), deps, prio=2)
+            t_next = tp.task(f"NEXT({b})", upd_stream, lambda bt=nxt, bs=base, l=ld: f_upd(bt, bs, l), deps, prio=2)
             last_upd[b] = t_next
         if len(rest):
-            last_upd[b] = tp.task(f"REST({b})", "update", lambda bt=rest, bs=base, l=ld: f_upd(bt, bs, l), deps,
+            last_upd[b] = tp.task(f"REST({b})", upd_stream, lambda bt=rest, bs=base, l=ld: f_upd(bt, bs, l), deps,
                                   prio=1)
         # the next block's first POTRF follows NEXT(b) (and, for this rank, the block's NEARs)
         gate = t_next if t_next is not None else gate

@@ -90,6 +90,7 @@ _SIGS = {
     "dpl_rows_move": [c_int, c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp,
                       c_int, c_vp, c_int, c_vp],
     "dpl_stream_cumask": [c_vp, c_int, c_vp],
+    "dpl_stream_destroy": [c_vp],
     "dpl_rows_permute": [c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp,
                          c_int, c_vp],
 }

@@ -21,10 +21,6 @@ import torch
 import torch.distributed as dist
 
 
-def _group_rank0(group) -> None:
-    return None
-
-
 def bcast(t: torch.Tensor, src_global: int, group) -> None:
     if group is None:
         return
@@ -42,7 +38,7 @@ def allgather_inplace(out: torch.Tensor, my_index: int, group) -> None:
         return
     inp = out[my_index]
     if out.device.type == "cuda" and _nccl():
-        w = dist.all_gather_into_tensor(out.view(-1), inp.reshape(-1).clone() if False else inp.reshape(-1),
+        w = dist.all_gather_into_tensor(out.view(-1), inp.reshape(-1),
                                         group=group, async_op=True)
         w.wait()
     else:

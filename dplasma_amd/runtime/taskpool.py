@@ -7,10 +7,10 @@ explicit dependencies on earlier tasks.  Execution enqueues every task in
 program order on its stream, inserting HIP event waits only for
 cross-stream edges, so the whole factorisation is queued asynchronously and
 the GPU runs ahead of the host (the HIP-native replacement for PaRSEC's
-ready-queue dispatch).  The dependency bookkeeping, event
-management and optional tracing are done by the native engine
-(``dplasma_amd.runtime.engine``) when available, by the pure-Python loop
-below otherwise; on CPU tasks simply run in order.
+ready-queue dispatch).  The dependency bookkeeping and event
+management are done by the loop in ``_run_gpu_py`` (task bodies are Python
+callables that enqueue native kernels through ctypes); on CPU tasks simply
+run in order.
 
 Timing protocol (reference ``tests/common.h:252-277``): building the
 taskpool is ENQ, ``run`` + ``complete`` is PROG, ``destruct`` is DEST.
@@ -46,7 +46,6 @@ class Taskpool:
         self.t_enq = time.perf_counter()
         self.t_prog = None
         self.trace = None
-        self.native = None  # compiled native program (runtime.engine)
 
     # ------------------------------------------------------------------ build
     def task(self, name: str, stream: str, fn: Callable[[], None], deps: Sequence[Optional[int]] = (),
@@ -78,11 +77,7 @@ class Taskpool:
     def _run(self, ctx):
         t0 = time.perf_counter()
         if ctx is not None and ctx.is_gpu:
-            from . import engine
-            if engine.available() and getattr(ctx, "profiling", None) is None:
-                engine.run_gpu(self, ctx)
-            else:
-                self._run_gpu_py(ctx)
+            self._run_gpu_py(ctx)
         else:
             from ..utils import trace
             for t in self.tasks:

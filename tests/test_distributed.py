@@ -82,7 +82,6 @@ def _gemm_worker(rank, world, P, ta, tb, kc):
 def test_gemm_summa(world, P, ta, tb):
     out = run_distributed(_gemm_worker, world, P, ta, tb, 2)
     full = sum(out[r] for r in range(world))
-    ref = _gemm_worker(0, 1, 1, ta, tb, None) if False else None
     import dplasma_amd as dp
     ctx = dp.Context(device="cpu")
     M, N, K, NB = 70, 55, 63, 16
@@ -111,7 +110,6 @@ def _norm_worker(rank, world, P):
 
 def test_norms_distributed():
     out = run_distributed(_norm_worker, 4, 2)
-    ref = _norm_worker(0, 1, 1) if False else None
     import dplasma_amd as dp
     ctx = dp.Context(device="cpu")
     A = dp.block_cyclic(ctx, torch.float64, 10, 10, 47, 38)

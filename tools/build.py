@@ -4,8 +4,9 @@
 * ``dplasma_amd/lib/libdplasma_kernels.so`` -- every HIP/CDNA4 kernel (gfx950),
   compiled with ``hipcc --offload-arch=gfx950`` (one object per ``.hip`` file,
   rebuilt only when the source or a header changed).
-* ``dplasma_amd/lib/_dplasma_rt*.so`` -- the C++ task runtime (DAG engine,
-  DTD front end, schedulers, tracing) as a pybind11 module.
+* ``dplasma_amd/lib/_dplasma_rt*.so`` -- the C++ runtime helpers as a pybind11
+  module: tile-DAG level analysis / critical-path priorities (``dag.cpp``) and
+  the band bulge-chasing kernels of the eigen/SVD reductions (``band.cpp``).
 
 Usage: ``python tools/build.py [--force] [-j N]``.  Called by
 ``__graft_entry__.build()`` and imported lazily by ``dplasma_amd.ops._lib``.
@@ -113,10 +114,24 @@ def build_capi(force=False) -> Path | None:
     return lib
 
 
+def build_tools(force=False) -> Path | None:
+    """tools/gemmpeak/mfma_peak: the fp64/fp32 MFMA and VALU peak microbenchmark (built from source,
+    never committed)."""
+    src = ROOT / "tools" / "gemmpeak" / "mfma_peak.hip"
+    if not src.exists():
+        return None
+    exe = src.with_suffix("")
+    if force or _newer(exe, [src]):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", str(src), "-o", str(exe)])
+        print(f"[build] built {exe.relative_to(ROOT)}", flush=True)
+    return exe
+
+
 def build_all(force=False, jobs=8):
     k = build_kernels(force=force, jobs=jobs)
     r = build_runtime(force=force)
     build_capi(force=force)
+    build_tools(force=force)
     return k, r
 
 
