@@ -34,7 +34,10 @@ void dpl_keep_error() {
 static std::string lib_root() {
   Dl_info info;
   if (dladdr((void*)&lib_root, &info) && info.dli_fname) {
-    std::string p(info.dli_fname);
+    // resolve symlinks: an installed prefix links lib/libdplasma.so -> lib/dplasma_amd/lib/libdplasma.so
+    char* real = realpath(info.dli_fname, nullptr);
+    std::string p(real ? real : info.dli_fname);
+    free(real);
     for (int up = 0; up < 3; ++up) {
       const size_t s = p.find_last_of('/');
       if (s == std::string::npos) return ".";

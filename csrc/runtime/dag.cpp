@@ -16,160 +16,67 @@
 #include <algorithm>
 #include <cstdint>
 #include <stdexcept>
-#include <unordered_map>
+#include <string>
 #include <vector>
 
 namespace py = pybind11;
 
+#include "dag_core.h"
+
 namespace {
 
-struct TileState {
-  int32_t last_write = -1;  // level of the last writer
-  int32_t max_read = -1;    // max level of readers since that write
-};
+using I64 = py::array_t<int64_t, py::array::c_style | py::array::forcecast>;
+using U8 = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
 
-// modes: 0 = unused slot, 1 = read, 2 = write, 3 = read+write
-py::array_t<int32_t> dag_levels(py::array_t<int64_t, py::array::c_style | py::array::forcecast> ops,
-                                py::array_t<uint8_t, py::array::c_style | py::array::forcecast> modes) {
+void check_shapes(const I64& ops, const U8& modes, const char* who) {
   if (ops.ndim() != 2 || modes.ndim() != 2 || ops.shape(0) != modes.shape(0) || ops.shape(1) != modes.shape(1))
-    throw std::invalid_argument("dag_levels: ops and modes must be (ntasks, nroles) arrays of equal shape");
+    throw std::invalid_argument(std::string(who) + ": ops and modes must be (ntasks, nroles) arrays of equal shape");
+}
+
+py::array_t<int32_t> dag_levels(I64 ops, U8 modes) {
+  check_shapes(ops, modes, "dag_levels");
   const int64_t n = ops.shape(0), R = ops.shape(1);
-  auto o = ops.unchecked<2>();
-  auto md = modes.unchecked<2>();
   py::array_t<int32_t> out(n);
-  auto lv = out.mutable_unchecked<1>();
-  std::unordered_map<int64_t, TileState> st;
-  st.reserve(static_cast<size_t>(std::min<int64_t>(n * 2 + 16, 1 << 24)));
+  const int64_t* o = ops.data();
+  const uint8_t* m = modes.data();
+  int32_t* lv = out.mutable_data();
   {
     py::gil_scoped_release rel;
-    for (int64_t t = 0; t < n; ++t) {
-      int32_t L = 0;
-      for (int64_t r = 0; r < R; ++r) {
-        const uint8_t m = md(t, r);
-        if (!m) continue;
-        auto it = st.find(o(t, r));
-        if (it == st.end()) continue;
-        const TileState& s = it->second;
-        if (s.last_write >= L) L = s.last_write + 1;        // RAW / WAW
-        if ((m & 2) && s.max_read >= L) L = s.max_read + 1;  // WAR
-      }
-      lv(t) = L;
-      for (int64_t r = 0; r < R; ++r) {
-        const uint8_t m = md(t, r);
-        if (!m) continue;
-        TileState& s = st[o(t, r)];
-        if (m & 2) {
-          s.last_write = L;
-          s.max_read = -1;
-        } else if (L > s.max_read) {
-          s.max_read = L;
-        }
-      }
-    }
+    dpl_dag::levels(o, m, n, R, lv);
   }
   return out;
 }
 
-// Versioned tile accesses for the distributed plan.  For every (task, role)
-// access returns the version of the tile it touches (0 = initial data, v = the
-// state after the v-th writing task).  Readers see the current version; a
-// writing access also reports the version it reads (it produces version+1).
-py::array_t<int32_t> dag_versions(py::array_t<int64_t, py::array::c_style | py::array::forcecast> ops,
-                                  py::array_t<uint8_t, py::array::c_style | py::array::forcecast> modes) {
+py::array_t<int32_t> dag_versions(I64 ops, U8 modes) {
+  check_shapes(ops, modes, "dag_versions");
   const int64_t n = ops.shape(0), R = ops.shape(1);
-  auto o = ops.unchecked<2>();
-  auto md = modes.unchecked<2>();
   py::array_t<int32_t> out({n, R});
-  auto v = out.mutable_unchecked<2>();
-  std::unordered_map<int64_t, int32_t> ver;
+  const int64_t* o = ops.data();
+  const uint8_t* m = modes.data();
+  int32_t* v = out.mutable_data();
   {
     py::gil_scoped_release rel;
-    for (int64_t t = 0; t < n; ++t) {
-      for (int64_t r = 0; r < R; ++r) {
-        v(t, r) = -1;
-        if (!md(t, r)) continue;
-        auto it = ver.find(o(t, r));
-        v(t, r) = it == ver.end() ? 0 : it->second;
-      }
-      for (int64_t r = 0; r < R; ++r)
-        if (md(t, r) & 2) ver[o(t, r)] += 1;
-    }
+    dpl_dag::versions(o, m, n, R, v);
   }
   return out;
 }
 
-// Full schedule analysis: levels, bottom levels (longest path to a sink) and
-// the deduplicated dependency edges.  Edges always point from an earlier to a
-// later task in program order, so the reverse program order is a reverse
-// topological order for the bottom-level pass.
-py::tuple dag_schedule(py::array_t<int64_t, py::array::c_style | py::array::forcecast> ops,
-                       py::array_t<uint8_t, py::array::c_style | py::array::forcecast> modes) {
-  if (ops.ndim() != 2 || modes.ndim() != 2 || ops.shape(0) != modes.shape(0) || ops.shape(1) != modes.shape(1))
-    throw std::invalid_argument("dag_schedule: ops and modes must be (ntasks, nroles) arrays of equal shape");
+py::tuple dag_schedule(I64 ops, U8 modes) {
+  check_shapes(ops, modes, "dag_schedule");
   const int64_t n = ops.shape(0), R = ops.shape(1);
-  auto o = ops.unchecked<2>();
-  auto md = modes.unchecked<2>();
-  struct St {
-    int64_t writer = -1;           // last writing task
-    std::vector<int64_t> readers;  // readers since that write
-  };
-  std::vector<int32_t> level(n, 0), blevel(n, 0);
-  std::vector<int64_t> esrc, edst;
+  dpl_dag::Schedule S;
+  const int64_t* o = ops.data();
+  const uint8_t* m = modes.data();
   {
     py::gil_scoped_release rel;
-    std::unordered_map<int64_t, St> st;
-    st.reserve(static_cast<size_t>(std::min<int64_t>(n * 2 + 16, 1 << 24)));
-    std::vector<int64_t> preds;
-    esrc.reserve(n * 3);
-    edst.reserve(n * 3);
-    for (int64_t t = 0; t < n; ++t) {
-      preds.clear();
-      for (int64_t r = 0; r < R; ++r) {
-        const uint8_t m = md(t, r);
-        if (!m) continue;
-        auto it = st.find(o(t, r));
-        if (it == st.end()) continue;
-        if (it->second.writer >= 0) preds.push_back(it->second.writer);
-        if (m & 2)
-          for (int64_t q : it->second.readers) preds.push_back(q);
-      }
-      std::sort(preds.begin(), preds.end());
-      preds.erase(std::unique(preds.begin(), preds.end()), preds.end());
-      int32_t L = 0;
-      for (int64_t p : preds) {
-        if (p == t) continue;
-        L = std::max(L, level[p] + 1);
-        esrc.push_back(p);
-        edst.push_back(t);
-      }
-      level[t] = L;
-      for (int64_t r = 0; r < R; ++r) {
-        const uint8_t m = md(t, r);
-        if (!m) continue;
-        St& s = st[o(t, r)];
-        if (m & 2) {
-          s.writer = t;
-          s.readers.clear();
-        } else {
-          s.readers.push_back(t);
-        }
-      }
-    }
-    // bottom levels: iterate edges in reverse destination order
-    std::vector<int64_t> order(esrc.size());
-    for (size_t i = 0; i < order.size(); ++i) order[i] = static_cast<int64_t>(i);
-    // edges were appended grouped by increasing destination: walking them backwards is reverse-topological
-    for (int64_t i = static_cast<int64_t>(esrc.size()) - 1; i >= 0; --i) {
-      const int64_t s = esrc[i], d = edst[i];
-      blevel[s] = std::max(blevel[s], blevel[d] + 1);
-    }
+    S = dpl_dag::schedule(o, m, n, R);
   }
   py::array_t<int32_t> lv(n), bl(n);
-  py::array_t<int64_t> es(static_cast<int64_t>(esrc.size())), ed(static_cast<int64_t>(edst.size()));
-  std::copy(level.begin(), level.end(), lv.mutable_data());
-  std::copy(blevel.begin(), blevel.end(), bl.mutable_data());
-  std::copy(esrc.begin(), esrc.end(), es.mutable_data());
-  std::copy(edst.begin(), edst.end(), ed.mutable_data());
+  py::array_t<int64_t> es(static_cast<int64_t>(S.esrc.size())), ed(static_cast<int64_t>(S.edst.size()));
+  std::copy(S.level.begin(), S.level.end(), lv.mutable_data());
+  std::copy(S.blevel.begin(), S.blevel.end(), bl.mutable_data());
+  std::copy(S.esrc.begin(), S.esrc.end(), es.mutable_data());
+  std::copy(S.edst.begin(), S.edst.end(), ed.mutable_data());
   return py::make_tuple(lv, bl, es, ed);
 }
 

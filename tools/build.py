@@ -127,6 +127,41 @@ def build_tools(force=False) -> Path | None:
     return exe
 
 
+SAN_FLAGS = {
+    "asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer"],
+    "tsan": ["-fsanitize=thread"],
+}
+
+
+def build_sanitized(kinds=("asan", "tsan")) -> dict:
+    """Debug/sanitizer builds of the host-native code (reference configure --enable-debug modes,
+    configure:81-90): the runtime cores (csrc/runtime/*_core.h) driven by
+    tests/native/test_runtime_core.cpp, and the native dplasma_info_t of the C ABI driven by
+    tests/capi/test_info.c.  GPU sanitizers are not used (host code only)."""
+    out = ROOT / "build" / "sanitize"
+    out.mkdir(parents=True, exist_ok=True)
+    pyinc = sysconfig.get_paths()["include"]
+    made = {}
+    for kind in kinds:
+        fl = ["-O1", "-g", *SAN_FLAGS[kind]]
+        exe = out / f"test_runtime_core_{kind}"
+        src = ROOT / "tests" / "native" / "test_runtime_core.cpp"
+        deps = [src, *RSRC.glob("*_core.h")]
+        if _newer(exe, deps):
+            _run(["g++", "-std=c++17", *fl, f"-I{RSRC}", str(src), "-o", str(exe), "-lpthread"])
+        made[f"runtime_{kind}"] = exe
+        if kind == "asan":
+            exe2 = out / "test_info_asan"
+            deps2 = [ROOT / "capi" / "dplasma_info.cpp", ROOT / "tests" / "capi" / "test_info.c"]
+            if _newer(exe2, deps2):
+                obj = out / "test_info.o"
+                _run(["gcc", *fl, f"-I{ROOT / 'capi' / 'include'}", "-c", str(deps2[1]), "-o", str(obj)])
+                _run(["g++", "-std=c++17", *fl, f"-I{pyinc}", f"-I{ROOT / 'capi'}", str(deps2[0]), str(obj), "-o",
+                      str(exe2)])
+            made["info_asan"] = exe2
+    return made
+
+
 def build_all(force=False, jobs=8):
     k = build_kernels(force=force, jobs=jobs)
     r = build_runtime(force=force)
@@ -139,5 +174,9 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--sanitize", action="store_true", help="also build the ASan/UBSan/TSan host test drivers")
     a = ap.parse_args()
     build_all(force=a.force, jobs=a.j)
+    if a.sanitize:
+        for k, v in build_sanitized().items():
+            print(f"[build] sanitizer driver {k}: {v.relative_to(ROOT)}")
