@@ -14,8 +14,9 @@ MI355X design:
   my C rows and the B tiles of my C columns (any transpose, any distribution),
   then one GEMM launch accumulates the chunk.  Chunks are double-buffered: the
   exchange of chunk s+1 (panel stream) overlaps the GEMM of chunk s (update
-  stream).  With 288 GB of HBM per GPU the default chunk is large (fewer,
-  larger collectives), see ``DPLASMA:GEMM:kc``.
+  stream); ``DPLASMA:GEMM:look_ahead`` chunks may be in flight (default from
+  utils.aux.gemm_lookahead).  With 288 GB of HBM per GPU the default chunk is
+  large (fewer, larger collectives), see ``DPLASMA:GEMM:kc``.
 """
 from __future__ import annotations
 
@@ -83,6 +84,15 @@ def gemm_New(ctx, transA, transB, alpha, A, B, beta, C, c_mask=None, kc=None, na
     if kc is None:
         kc = ctx.info.get_int("DPLASMA:GEMM:kc", 0) or max(1, min(kt, 8))
     nchunks = (kt + kc - 1) // kc
+    # look-ahead: chunks whose exchange may run ahead of the GEMM consuming the oldest one
+    # (reference DPLASMA:GEMM:GPU:look_ahead, src/zgemm_wrapper.c:289-296; the SUMMA look-ahead
+    # CTLs of zgemm_NN_summa.jdf); one receive buffer per chunk in flight
+    from ..utils.aux import gemm_lookahead
+    la = ctx.info.get_int("DPLASMA:GEMM:look_ahead", 0) or ctx.info.get_int("DPLASMA:GEMM:GPU:look_ahead", 0) \
+        or gemm_lookahead(ctx, C)
+    if la <= 0:
+        raise ValueError("DPLASMA:GEMM:look_ahead must be 1 or more")
+    nbuf = min(nchunks, la + 1)
     mats = [A, B]
     bufs = []
     prev_gemm = {}
@@ -102,19 +112,19 @@ def gemm_New(ctx, transA, transB, alpha, A, B, beta, C, c_mask=None, kc=None, na
                     lst.append((1,) + _b_tile(transB, k, n))
             needs[r] = lst
         plan = ExchangePlan(ctx, mats, needs, C.dtype, C.device)
-        if len(bufs) < 2:
+        if len(bufs) < nbuf:
             bufs.append(plan.new_recv_buffer())
-        buf = bufs[s % 2]
+        buf = bufs[s % nbuf]
         if buf.numel() < max(plan.nrecv, 1) * plan.nbe:
             buf = plan.new_recv_buffer()
-            bufs[s % 2] = buf
+            bufs[s % nbuf] = buf
         gb = GemmBatch()
         for (m, n) in ctiles:
             kp = [(plan.offset(0, *_a_tile(transA, m, k)), plan.offset(1, *_b_tile(transB, k, n)), kext(k))
                   for k in ks]
             gb.add(C.offset(m, n), C.tile_rows(m), C.tile_cols(n), kp, c_mask(m, n) if c_mask else 0)
         gb.finalize()
-        t_ex = tp.task(f"EXCH({s})", "panel", lambda plan=plan, buf=buf: plan.run(buf), [prev_gemm.get(s - 2)],
+        t_ex = tp.task(f"EXCH({s})", "panel", lambda plan=plan, buf=buf: plan.run(buf), [prev_gemm.get(s - nbuf)],
                        prio=2)
         b_eff = beta if s == 0 else 1.0
         prev_gemm[s] = tp.task(

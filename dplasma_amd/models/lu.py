@@ -115,17 +115,29 @@ def _row_pairs(M: TiledMatrix, rows_dst, rows_src, coltiles, dst_off_fn=None, sr
 class _GetrfDev:
     """Partial-pivoting LU, device-resident (getrf_1d on 1 x Q grids, getrf_ptgpanel on P x Q).
 
-    Step k (every batch and panel plan is built once, here; a run only launches):
-      1. the panel's process column assembles the tall panel (its tiles summed over the P
-         process rows -> replicated) and factors it with the recursive device LU
-         (ops.PanelLU: dgetrf2 halves, <=64-column blocks with an on-device multi-workgroup
-         pivot search -- GETRF_MAX / RDC / SND of src/zgetrf_ptgpanel.jdf:206-590);
-      2. factored panel + pivots travel along process rows (RCCL broadcast);
-      3. the net row moves are derived on the device (ops.piv_moves) and applied to every
-         local tile column through a staging buffer, summed over the process column when
-         P > 1 (SWAP_COLLECT / SWAP_SND, :825-978) -- no host round trip, no host planning;
-      4. the U block row is solved where it lives and broadcast down process columns;
-      5. one batched MFMA GEMM launch updates the trailing tiles."""
+    Step k is four tasks (every batch and panel plan is built once, here; a run only launches):
+      PANEL(k)  [panel stream]  the panel's process column gathers the tall panel -- each process
+                row contributes only its own tiles (one all-gather of M x NB / P per rank instead
+                of the former all-reduce of the whole zero-padded panel) -- and factors it with the
+                recursive device LU (ops.PanelLU: dgetrf2 halves, <=64-column blocks with an
+                on-device multi-workgroup pivot search -- GETRF_MAX / RDC / SND of
+                src/zgetrf_ptgpanel.jdf:206-590), then factored panel + pivots travel along
+                process rows (RCCL broadcast);
+      SWAP(k)   [update stream] net row moves derived on the device (ops.piv_moves) applied to every
+                local tile column (SWAP_COLLECT / SWAP_SND, :825-978; summed over the process column
+                when P > 1), L written back, the U block row solved where it lives and broadcast
+                down process columns;
+      NEXT(k)   [panel stream]  the trailing update of tile column k+1 only;
+      REST(k)   [update stream] the trailing update of every column beyond it.
+    PANEL(k+1) needs only NEXT(k), so with look-ahead (default; DPLASMA_LU_LOOKAHEAD=0 turns it
+    off) the next panel factorisation overlaps REST(k) -- the reference's lookahead through
+    priorities.  Panel buffers alternate with k's parity (REST(k) still reads panel k).
+
+    Why the panel travels whole: partial pivoting identical to one process needs, per column, a
+    max-reduction over the process column followed by the pivot row; done as collectives that is
+    NB dependent RCCL calls per panel (512 x ~15 us = 7.7 ms at NB = 512) against ~1 ms to move a
+    64k x 512 panel once over xGMI, so the panel is gathered once and factored redundantly by
+    every process row of the column (same pivots everywhere, no further panel traffic)."""
 
     def __init__(self, ctx, A, info):
         self.ctx, self.A, self.info = ctx, A, info
@@ -133,7 +145,9 @@ class _GetrfDev:
         mb, nb = A.mb, A.nb
         g = A.grid
         self.kt = min(A.mt, A.nt)
-        self.pbuf = torch.zeros(max(1, A.m * nb), dtype=A.dtype, device=dev)
+        self.lookahead = os.environ.get("DPLASMA_LU_LOOKAHEAD", "1") != "0"
+        self.pbufs = [torch.zeros(max(1, A.m * nb), dtype=A.dtype, device=dev)
+                      for _ in range(2 if self.lookahead else 1)]
         self.piv_dev = torch.zeros(nb, dtype=torch.int32, device=dev)
         self.ipiv_all = torch.zeros(max(1, min(A.m, A.n)), dtype=torch.int32, device=dev)
         self.ws = ops.lu_workspace(A.m, dev)
@@ -176,7 +190,17 @@ class _GetrfDev:
         self.nleft = [bisect.bisect_left(lcols, k) for k in range(min(A.mt, A.nt))]
         ncol_loc = sum(A.tile_cols(n) for n in lcols)
         self.ubuf = torch.zeros(max(1, nb * max(ncol_loc, 1)), dtype=A.dtype, device=dev)
+        # P > 1: per-step panel gather buffer [P][maxrows x nb] (every process row's panel tiles)
+        self.gbuf = None
+        if g.P > 1:
+            maxrows = 0
+            for k in range(self.kt):
+                for q in range(g.P):
+                    maxrows = max(maxrows, sum(A.tile_rows(m) for m in range(k, A.mt) if g.prow(m + A.it0) == q))
+            self.gmax = max(1, maxrows)
+            self.gbuf = torch.zeros(g.P * self.gmax * nb, dtype=A.dtype, device=dev)
         self.plan = [self._build(k) for k in range(self.kt)]
+        self.bytes_panel = [0] * self.kt   # elements this rank sends per step (panel gather)
 
     def _build(self, k):
         A = self.A
@@ -185,6 +209,8 @@ class _GetrfDev:
         r0 = k * mb
         mp = A.m - r0
         st = {"kb": kb, "r0": r0, "mp": mp, "kmin": min(mp, kb)}
+        g = A.grid
+        st["pv"] = self.pbufs[k % len(self.pbufs)]
         if A.col_is_local(k):
             mine = [m for m in range(k, A.mt) if A.row_is_local(m)]
             if mine:
@@ -193,7 +219,26 @@ class _GetrfDev:
                     tb.add(A.offset(m, k), A.tile_rows(m), kb, b_off=(m - k) * mb)
                     back.add((m - k) * mb, A.tile_rows(m), kb, b_off=A.offset(m, k))
                 st["gather"], st["back"] = tb.finalize(), back.finalize()
-            st["plu"] = ops.PanelLU(self.pbuf, mp, mp, kb, pivot=True)
+            if g.P > 1:
+                # pack my panel tiles into my slot of the gather buffer, unpack every slot into the panel
+                gm, slot = self.gmax, g.P
+                pack, unpack = TileBatch(), TileBatch()
+                sent = 0
+                for q in range(slot):
+                    r = 0
+                    for m in range(k, A.mt):
+                        if g.prow(m + A.it0) != q:
+                            continue
+                        base = q * gm * kb + r
+                        if q == A.myrow:
+                            pack.add(A.offset(m, k), A.tile_rows(m), kb, b_off=base)
+                            sent += A.tile_rows(m) * kb
+                        unpack.add(base, A.tile_rows(m), kb, b_off=(m - k) * mb)
+                        r += A.tile_rows(m)
+                st["gpack"] = pack.finalize() if len(pack) else None
+                st["gunpack"] = unpack.finalize()
+                st["gsent"] = sent
+            st["plu"] = ops.PanelLU(st["pv"], mp, mp, kb, pivot=True)
         trail = [n for n in range(k + 1, A.nt) if A.col_is_local(n)]
         st["trail"] = trail
         if trail and A.row_is_local(k):
@@ -214,36 +259,58 @@ class _GetrfDev:
                 st["upack"] = tb.finalize()
             rows = [m for m in range(k + 1, A.mt) if A.row_is_local(m)]
             if rows:
-                gb = GemmBatch()
+                nxt, rest = GemmBatch(), GemmBatch()
                 for n in trail:
                     for m in rows:
-                        gb.add(A.offset(m, n), A.tile_rows(m), A.tile_cols(n), [((m - k) * mb, uoff[n], kb)])
-                st["gemm"] = gb.finalize()
+                        (nxt if n == k + 1 else rest).add(A.offset(m, n), A.tile_rows(m), A.tile_cols(n),
+                                                          [((m - k) * mb, uoff[n], kb)])
+                st["gemm_next"] = nxt.finalize() if len(nxt) else None
+                st["gemm_rest"] = rest.finalize() if len(rest) else None
         return st
 
     def step(self, k):
+        """The whole step in order (no look-ahead)."""
+        self.panel(k)
+        self.swap(k)
+        self.next(k)
+        self.rest(k)
+
+    def panel(self, k):
         A, ctx = self.A, self.ctx
         g = A.grid
         st = self.plan[k]
         kb, r0, mp, kmin = st["kb"], st["r0"], st["mp"], st["kmin"]
         pc = g.pcol(k + A.jt0)
-        pv = self.pbuf[: mp * kb]
-        # --- 1. panel (process column pc): assemble, replicate over P, factor on the device
+        pv = st["pv"][: mp * kb]
+        # --- gather the panel in its process column (each process row sends only its own tiles)
         if A.col_is_local(k):
             if g.P > 1:
-                pv.zero_()
-            if "gather" in st:
+                gv = self.gbuf[: g.P * self.gmax * kb].view(g.P, self.gmax * kb)
+                if st["gpack"] is not None:
+                    ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, self.gbuf, self.gmax, st["gpack"], copy=True)
+                comm.allgather_inplace(gv, A.myrow, ctx.col_group)
+                ops.geadd(0, N_, 1.0, self.gbuf, self.gmax, 0.0, pv, mp, st["gunpack"], copy=True)
+                self.bytes_panel[k] = st["gsent"]
+            elif "gather" in st:
                 ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, pv, mp, st["gather"], copy=True)
-            if g.P > 1:
-                dist.all_reduce(pv, group=ctx.col_group)
             st["plu"].run(self.piv_dev, self.ws, self.cnt, self.info, r0)
-        # --- 2. factored panel + pivots along process rows
+        # --- factored panel + pivots along process rows
         if g.Q > 1:
             root = g.rank(A.myrow, pc)
             comm.bcast(pv, root, ctx.row_group)
             comm.bcast(self.piv_dev, root, ctx.row_group)
         self.ipiv_all[r0: r0 + kmin].copy_(self.piv_dev[:kmin] + (r0 + 1))
-        # --- 3. row interchanges on every local column (the panel column is rewritten below)
+        if self.tmp is not None:   # net moves of this step's interchanges (lists double-buffered by parity)
+            par = k & 1
+            ops.piv_moves(self.piv_dev, kmin, self.mdst[par], self.msrc[par], self.mcnt[par])
+
+    def swap(self, k):
+        A, ctx = self.A, self.ctx
+        g = A.grid
+        st = self.plan[k]
+        kb, r0, mp = st["kb"], st["r0"], st["mp"]
+        pv = st["pv"][: mp * kb]
+        # --- row interchanges on every local column (the panel column is rewritten below)
         if self.tmp is not None:
             par = k & 1
             mdst, msrc, mcnt = self.mdst[par], self.msrc[par], self.mcnt[par]
@@ -252,7 +319,6 @@ class _GetrfDev:
             cur = torch.cuda.current_stream() if self.side is not None else None
             if cur is not None and self.ev_side[par] is not None:
                 cur.wait_event(self.ev_side[par])      # step k-2's side moves have read these lists
-            ops.piv_moves(self.piv_dev, kmin, mdst, msrc, mcnt)
             if nl:
                 ev = torch.cuda.Event()
                 ev.record(cur)                           # lists ready, left columns final (back(k-1))
@@ -283,7 +349,7 @@ class _GetrfDev:
                 self.ev_side = [None, None]
         if "back" in st:
             ops.geadd(0, N_, 1.0, pv, mp, 0.0, A.data, A.ld, st["back"], copy=True)
-        # --- 4. U block row where it lives, then down the process column
+        # --- U block row where it lives, then down the process column
         if not st["trail"]:
             return
         if "trsm" in st:
@@ -295,9 +361,32 @@ class _GetrfDev:
             ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, ub, kb, st["upack"], copy=True)
         if g.P > 1:
             comm.bcast(ub[: st["ulen"]], g.rank(g.prow(k + A.it0), A.mycol), ctx.col_group)
-        # --- 5. trailing update A(m, n) -= L(m, k) U(k, n)
-        if "gemm" in st:
-            ops.gemm(N_, N_, -1.0, pv, mp, ub, kb, 1.0, A.data, A.ld, st["gemm"])
+
+    def _update(self, k, key):
+        st = self.plan[k]
+        gb = st.get(key)
+        if gb is not None:   # trailing update A(m, n) -= L(m, k) U(k, n)
+            ops.gemm(N_, N_, -1.0, st["pv"], st["mp"], self.ubuf, st["kb"], 1.0, self.A.data, self.A.ld, gb)
+
+    def next(self, k):
+        self._update(k, "gemm_next")
+
+    def rest(self, k):
+        self._update(k, "gemm_rest")
+
+    def add_tasks(self, tp, tag):
+        """PANEL/SWAP/NEXT/REST tasks of every step; with look-ahead PANEL(k+1) overlaps REST(k)."""
+        if not self.lookahead:
+            prev = None
+            for k in range(self.kt):
+                prev = tp.task(f"{tag}({k})", "update", (lambda k=k: self.step(k)), [prev])
+            return
+        nxt = rest = None
+        for k in range(self.kt):
+            t_p = tp.task(f"PANEL({k})", "panel", (lambda k=k: self.panel(k)), [nxt], prio=3)
+            t_s = tp.task(f"SWAP({k})", "update", (lambda k=k: self.swap(k)), [t_p, rest], prio=2)
+            nxt = tp.task(f"NEXT({k})", "panel", (lambda k=k: self.next(k)), [t_s], prio=2)
+            rest = tp.task(f"REST({k})", "update", (lambda k=k: self.rest(k)), [t_s], prio=1)
 
 
 def _permute_rows_2d(ctx, A, dst_rows, src_rows, coltiles):
@@ -396,9 +485,7 @@ def getrf_ptgpanel_New(ctx, A, IPIV, info_out=None):
     tp.flops = flops(A.prec, "getrf", A.m, A.n)
     info = torch.zeros(1, dtype=torch.int32, device=A.device)
     st = _GetrfDev(ctx, A, info)
-    prev = None
-    for k in range(st.kt):
-        prev = tp.task(f"getrf_ptg({k})", "update", (lambda k=k: st.step(k)), [prev])
+    st.add_tasks(tp, "getrf_ptg")
     tp._state = st
 
     def _done():
@@ -432,9 +519,7 @@ def getrf_1d_New(ctx, A, IPIV, info_out=None):
     tp.flops = flops(A.prec, "getrf", A.m, A.n)
     info = torch.zeros(1, dtype=torch.int32, device=A.device)
     st = _GetrfDev(ctx, A, info)
-    prev = None
-    for k in range(st.kt):
-        prev = tp.task(f"getrf1d({k})", "update", (lambda k=k: st.step(k)), [prev])
+    st.add_tasks(tp, "getrf1d")
     tp._state = st
 
     def _done():

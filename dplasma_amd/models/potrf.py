@@ -85,6 +85,14 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
     # diagonal tiles on the CU-reserved stream when DPLASMA_DIAG_CUS is set (context._reserve_cus)
     diag_stream = "diag" if "diag" in getattr(ctx, "streams", {}) else "panel"
     upd_stream = "potrf_update" if "potrf_update" in getattr(ctx, "streams", {}) else "update"
+    # PRI_CHANGE ({S,D,C,Z}POTRF env, reference zpotrf_wrapper.c:201-203): the last PRI_CHANGE
+    # panels issue their critical-path tasks at normal priority (update stream) instead of the
+    # high-priority panel stream; 0 (default) keeps every panel on the panel stream
+    from ..utils.aux import get_priority_limit
+    pri_change = get_priority_limit("POTRF", A)
+
+    def pstream(k, default):
+        return upd_stream if (pri_change > 0 and k >= A.nt - pri_change) else default
     tp.flops = flops(A.prec, "potrf", A.n)
     nt = A.nt
     dev = A.device
@@ -203,7 +211,7 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                                        zbuf=zbufs[(k % 2) * zsz:(k % 2 + 1) * zsz])
                     else:
                         potrf_diag(uplo, A.data, off, kb, A.ld, info, k * A.mb)
-                t_potrf = tp.task(f"POTRF({k})", diag_stream, f_potrf, [gate], prio=3)
+                t_potrf = tp.task(f"POTRF({k})", pstream(k, diag_stream), f_potrf, [gate], prio=3)
             # ---------------- local panel tiles (i > k) of my process row/col
             mine = [i for i in range(k + 1, nt) if in_panel_cross and owner_of_panel_line(i) == my_line]
             # ---------------- diag tile to the panel owners (column for lower) and TRSM
@@ -219,7 +227,7 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                             dv = torch.as_strided(dbuf, (kb, kb), (1, A.mb), 0)
                             dv.copy_(torch.as_strided(A.data, (kb, kb), (1, A.ld), dk_off))
                         comm.bcast(dbuf, src, line_group)
-                    t_db = tp.task(f"DBCAST({k})", "panel", f_dbcast, [t_potrf, gate], prio=3)
+                    t_db = tp.task(f"DBCAST({k})", pstream(k, "panel"), f_dbcast, [t_potrf, gate], prio=3)
                     tri_base, tri_ld, tri_off = dbuf, A.mb, 0
                 else:
                     t_db = t_potrf
@@ -235,7 +243,7 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                         if not own:  # the diagonal tile arrived by broadcast: invert its 32-blocks here
                             ops.trsm_rb_prep(uplo, kb, tri_base, tri_off, tri_ld, zk)
                         ops.trsm_rb(uplo, kb, tri_base, tri_off, tri_ld, zk, rbp, A.data, A.ld)
-                    t_trsm = tp.task(f"TRSM({k})", "panel", f_trsm, [t_db, gate], prio=2)
+                    t_trsm = tp.task(f"TRSM({k})", pstream(k, "panel"), f_trsm, [t_db, gate], prio=2)
                 elif mine:
                     tb = TileBatch()
                     for i in mine:
@@ -247,7 +255,7 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                     def f_trsm(tb=tb, tri_base=tri_base, tri_ld=tri_ld, side=side):
                         ops.trsm(side, uplo, dplasmaConjTrans, dplasmaNonUnit, 1.0, tri_base, tri_ld, A.data, A.ld,
                                  tb)
-                    t_trsm = tp.task(f"TRSM({k})", "panel", f_trsm, [t_db, gate], prio=2)
+                    t_trsm = tp.task(f"TRSM({k})", pstream(k, "panel"), f_trsm, [t_db, gate], prio=2)
             if k == nt - 1:
                 break
             # ---------------- panel distribution
@@ -297,7 +305,7 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                             ops.geadd(0, dplasmaNoTrans, 1.0, GX, A.mb, 0.0, GX, A.mb, subpack, copy=True)
                         comm.allgather_inplace(Xk, my_line, line_group)
                 # GX slab (par) is reused by block b+2: its previous readers (NEXT/REST of b-2) must be done
-                t_panel = tp.task(f"PANEL_COMM({k})", "panel", f_comm,
+                t_panel = tp.task(f"PANEL_COMM({k})", pstream(k, "panel"), f_comm,
                                   [t_trsm, gate, last_panel, last_upd.get(b - 2)], prio=2)
                 last_panel = t_panel
 
@@ -314,7 +322,7 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
             # ---------------- NEAR(k): the rest of this block, right now (panel stream)
             near = add_update(GemmBatch(), [k], range(k + 1, c1))
             if len(near):
-                gate = tp.task(f"NEAR({k})", "panel", lambda bt=near, bs=base, l=ld: f_upd(bt, bs, l),
+                gate = tp.task(f"NEAR({k})", pstream(k, "panel"), lambda bt=near, bs=base, l=ld: f_upd(bt, bs, l),
                                [t_panel, gate], prio=2)
             else:
                 gate = t_panel if t_panel is not None else gate
