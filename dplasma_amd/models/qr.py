@@ -161,6 +161,7 @@ def geqrf_New(ctx, A, T) -> Taskpool:
     flat = qrtree.FlatTree(A.mt, A.nt)
     if qr_panel.usable(A, flat):
         return qr_panel.factor_New(ctx, A, T, T, flat, "geqrf")
+    T.full_T = {}   # tile engine: the panel engine's kept T factors no longer describe T
     dag = TileDAG(ctx, "geqrf")
     _factor(dag, _L(A), _L(T), _L(T), _kinds(A, T, False), qrtree.FlatTree(A.mt, A.nt))
     dag.flops = flops(A.prec, "geqrf", A.m, A.n)
@@ -366,6 +367,7 @@ def geqrf_param_New(ctx, tree, A, TS, TT) -> Taskpool:
     _check_tree(A, tree, False)
     if qr_panel.usable(A, tree):
         return qr_panel.factor_New(ctx, A, TS, TT, tree, "geqrf_param")
+    TS.full_T, TT.full_T = {}, {}   # tile engine: drop the panel engine's kept T factors
     dag = TileDAG(ctx, "geqrf_param")
     _factor(dag, _L(A), _L(TS), _L(TT), _kinds(A, TS, False), tree)
     dag.flops = flops(A.prec, "geqrf", A.m, A.n)

@@ -260,20 +260,49 @@ def _store_T(Tm, ldt, kf, Td, row, k):
         torch.as_strided(Td.data, (r, r), (1, ld), base + c0 * ld).copy_(src)
 
 
+def _keep_full_T(Tm, ldt, kf, Td, row, k):
+    """Keep the whole compact-WY T of a factored domain / TT stack next to its reference-layout
+    diagonal blocks (Td.full_T[(row, k)], nb x nb per panel: 2 MiB at NB = 512), so the apply
+    (unmqr / ungqr / geqrs / gels) reuses it instead of rebuilding the coupling blocks."""
+    store = getattr(Td, "full_T", None)
+    if store is None:
+        store = Td.full_T = {}
+    t = store.get((row, k))
+    if t is None or t.numel() < kf * kf or t.device != Tm.device:
+        t = store[(row, k)] = torch.empty(kf * kf, dtype=Tm.dtype, device=Tm.device)
+    torch.as_strided(t, (kf, kf), (1, kf), 0).copy_(torch.as_strided(Tm, (kf, kf), (1, ldt), 0))
+
+
 def _rebuild_T(V, ldv, M, kf, Td, row, k, out, ldt):
-    """Full compact-WY T from the stored diagonal blocks and V (coupling -T11 V1^T V2 T22)."""
+    """Full compact-WY T: the copy kept by the factorisation when there is one, else rebuilt from
+    the stored diagonal IB blocks and V (coupling T12 = -T11 (V1^H V2) T22, block column by block
+    column) with the batched MFMA GEMM engine -- no vendor BLAS on the device path."""
+    kept = getattr(Td, "full_T", {}).get((row, k))
+    dst = torch.as_strided(out, (kf, kf), (1, ldt), 0)
+    if kept is not None and kept.device == out.device and kept.numel() >= kf * kf:
+        dst.copy_(torch.as_strided(kept, (kf, kf), (1, kf), 0))
+        return
     ib = Td.mb
-    Tf = torch.zeros(kf, kf, dtype=V.dtype, device=V.device)
+    dst.zero_()
     for b0 in range(0, kf, ib):
         bs = min(ib, kf - b0)
-        Tf[b0:b0 + bs, b0:b0 + bs] = torch.triu(Td.tile(row, k)[:bs, b0:b0 + bs])
-    if kf > ib:
-        Vv = torch.as_strided(V, (M, kf), (1, ldv), 0)
-        Gm = Vv.T @ Vv
-        for b0 in range(ib, kf, ib):
-            bs = min(ib, kf - b0)
-            Tf[:b0, b0:b0 + bs] = -(Tf[:b0, :b0] @ Gm[:b0, b0:b0 + bs]) @ Tf[b0:b0 + bs, b0:b0 + bs]
-    torch.as_strided(out, (kf, kf), (1, ldt), 0).copy_(Tf)
+        dst[b0:b0 + bs, b0:b0 + bs] = torch.triu(Td.tile(row, k)[:bs, b0:b0 + bs])
+    if kf <= ib:
+        return
+    ct = dplasmaConjTrans if V.dtype.is_complex else dplasmaTrans
+    G = torch.empty(kf * kf, dtype=V.dtype, device=V.device)   # G = V^H V  (kf x kf, ld kf)
+    X = torch.empty(kf * ib, dtype=V.dtype, device=V.device)   # X = T(:b0, :b0) G(:b0, b0:b0+bs)
+    gb = GemmBatch()
+    gb.add(0, kf, kf, [(0, 0, M)])
+    ops.gemm(ct, N_, 1.0, V, ldv, V, ldv, 0.0, G, kf, gb)
+    for b0 in range(ib, kf, ib):
+        bs = min(ib, kf - b0)
+        g1 = GemmBatch()
+        g1.add(0, b0, bs, [(0, b0 * kf, b0)])                  # X = T11 G(:b0, b0:)
+        ops.gemm(N_, N_, 1.0, out, ldt, G, kf, 0.0, X, b0, g1)
+        g2 = GemmBatch()
+        g2.add(b0 * ldt, b0, bs, [(0, b0 + b0 * ldt, bs)])     # T(:b0, b0:) = -X T22
+        ops.gemm(N_, N_, -1.0, X, b0, out, ldt, 0.0, out, ldt, g2)
 
 
 # ----------------------------------------------------------------------------- factorisation
@@ -368,8 +397,10 @@ class _Factor:
             ops.geadd(e["part"], N_, 1.0, P, ld, 0.0, A.data, A.ld, e["back"], copy=True)
         if e["tt"]:
             _store_T(Tm, A.nb, kf, self.TT, e["rows"][1], k)
+            _keep_full_T(Tm, A.nb, kf, self.TT, e["rows"][1], k)
         else:
             _store_T(Tm, A.nb, kf, self.TS, e["rows"][0], k)
+            _keep_full_T(Tm, A.nb, kf, self.TS, e["rows"][0], k)
         self._bcast(e, V, Tm)
 
     def _bcast(self, e, V, Tm):

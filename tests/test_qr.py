@@ -533,3 +533,32 @@ def test_qr_simulation_date(mt, nt, flat, greedy):
             .simulation_date() == flat
         # unit costs: the date is the DAG depth
         assert dp.geqrf_New(ctx, A, TS).simulation_date(lambda name: 1) >= mt + nt - 1
+
+
+def _kept_vs_rebuilt(c, dt):
+    """ungqr with the T kept by the stacked-domain factorisation vs with T rebuilt from the stored
+    diagonal blocks and V (MFMA GEMM engine on the GPU): same Q."""
+    M, N, NB, IB = 300, 200, 64, 16
+    with qr_panel.engine("panel"):
+        A = dp.block_cyclic(c, dt, NB, NB, M, N)
+        dp.plrnt(c, A, 3872)
+        T = dp.block_cyclic(c, dt, IB, NB, A.mt * IB, A.nt * NB)
+        dp.geqrf(c, A, T)
+        assert getattr(T, "full_T", None)
+        Q1 = dp.block_cyclic(c, dt, NB, NB, M, N)
+        dp.ungqr(c, A, T, Q1)
+        T.full_T = {}
+        Q2 = dp.block_cyclic(c, dt, NB, NB, M, N)
+        dp.ungqr(c, A, T, Q2)
+    return rel_err(_dense(Q2), _dense(Q1))
+
+
+@pytest.mark.parametrize("prec", ["d", "s"])   # the stacked-domain engine is real-precision only
+def test_qr_kept_T_matches_rebuilt(ctx, prec):
+    assert _kept_vs_rebuilt(ctx, DTYPES[prec]) < (1e-4 if prec == "s" else 1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", ["d", "s"])
+def test_gpu_qr_kept_T_matches_rebuilt(gctx, prec):
+    assert _kept_vs_rebuilt(gctx, DTYPES[prec]) < (1e-4 if prec == "s" else 1e-11)
