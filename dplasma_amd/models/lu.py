@@ -129,9 +129,8 @@ class _GetrfDev:
                 down process columns;
       NEXT(k)   [panel stream]  the trailing update of tile column k+1 only;
       REST(k)   [update stream] the trailing update of every column beyond it.
-    PANEL(k+1) needs only NEXT(k), so with look-ahead (default; DPLASMA_LU_LOOKAHEAD=0 turns it
-    off) the next panel factorisation overlaps REST(k) -- the reference's lookahead through
-    priorities.  Panel buffers alternate with k's parity (REST(k) still reads panel k).
+    PANEL(k+1) needs only NEXT(k), so with look-ahead (DPLASMA_LU_LOOKAHEAD=1) the next panel
+    factorisation overlaps REST(k) -- the reference's lookahead through priorities.  Panel buffers alternate with k's parity (REST(k) still reads panel k).
 
     Why the panel travels whole: partial pivoting identical to one process needs, per column, a
     max-reduction over the process column followed by the pivot row; done as collectives that is
@@ -145,7 +144,11 @@ class _GetrfDev:
         mb, nb = A.mb, A.nb
         g = A.grid
         self.kt = min(A.mt, A.nt)
-        self.lookahead = os.environ.get("DPLASMA_LU_LOOKAHEAD", "1") != "0"
+        # look-ahead is opt-in: measured on one MI355X (profiles/r2_lu_lookahead.txt) the persistent
+        # grid-barrier panel kernel beside the REST GEMM slows from ~0.5 to ~1.2 ms per 64-column
+        # block (its workgroups share CUs with GEMM waves), which eats the overlap: DGETRF 32k
+        # 28.2 -> 27.1 TF/s, 64k 48.1 -> 47.2 TF/s with look-ahead on
+        self.lookahead = os.environ.get("DPLASMA_LU_LOOKAHEAD", "0") == "1"
         self.pbufs = [torch.zeros(max(1, A.m * nb), dtype=A.dtype, device=dev)
                       for _ in range(2 if self.lookahead else 1)]
         self.piv_dev = torch.zeros(nb, dtype=torch.int32, device=dev)
