@@ -20,7 +20,7 @@
 //     A staging, so the epilogue is a pure store;
 //   * blockIdx is remapped XCD-aware so the 16 sub-tiles of a 512x512 tile and
 //     neighbouring tiles of a tile-row share one XCD's L2.
-// Complex precisions use a generic LDS-tiled FMA kernel (same item protocol).
+// Complex precisions run on the matrix cores too (zgemm.hip, four real MFMA products per complex one).
 #include "common.h"
 
 struct KPair {
@@ -742,8 +742,13 @@ static int launch_generic(int opa, int opb, int nitems, const GemmItemK* items, 
   return (int)hipGetLastError();
 }
 
+// complex precisions on the matrix cores (zgemm.hip)
+DPL_API int dpl_cgemm_mfma(int prec, int opa, int opb, int nitems, const void* items, const void* kpairs, int max_m,
+                           int max_n, const void* alpha, const void* A, int lda, const void* B, int ldb,
+                           const void* beta, void* C, int ldc, hipStream_t st);
+
 // alpha/beta: host pointers to one scalar of the launch precision (complex = 2 reals)
-// force_generic: route real precisions through the FMA kernel (testing / A-B).
+// force_generic: route every precision through the FMA kernel (testing / A-B).
 DPL_API int dpl_gemm_batched(int prec, int transA, int transB, int nitems, const void* items, const void* kpairs,
                              int max_m, int max_n, const void* alpha, const void* A, int lda, const void* B,
                              int ldb, const void* beta, void* C, int ldc, int vec_ok, int force_generic,
@@ -765,11 +770,17 @@ DPL_API int dpl_gemm_batched(int prec, int transA, int transB, int nitems, const
       return launch_generic<float>(oa, ob, nitems, it, kp, max_m, max_n, *(const float*)alpha, (const float*)A, lda,
                                    (const float*)B, ldb, *(const float*)beta, (float*)C, ldc, st);
     case DPL_C:
+      if (!force_generic)
+        return dpl_cgemm_mfma(prec, oa, ob, nitems, items, kpairs, max_m, max_n, alpha, A, lda, B, ldb, beta, C, ldc,
+                              st);
       return launch_generic<hipFloatComplex>(oa, ob, nitems, it, kp, max_m, max_n,
                                              *(const hipFloatComplex*)alpha, (const hipFloatComplex*)A, lda,
                                              (const hipFloatComplex*)B, ldb, *(const hipFloatComplex*)beta,
                                              (hipFloatComplex*)C, ldc, st);
     case DPL_Z:
+      if (!force_generic)
+        return dpl_cgemm_mfma(prec, oa, ob, nitems, items, kpairs, max_m, max_n, alpha, A, lda, B, ldb, beta, C, ldc,
+                              st);
       return launch_generic<hipDoubleComplex>(oa, ob, nitems, it, kp, max_m, max_n,
                                               *(const hipDoubleComplex*)alpha, (const hipDoubleComplex*)A, lda,
                                               (const hipDoubleComplex*)B, ldb, *(const hipDoubleComplex*)beta,

@@ -285,7 +285,8 @@ TRSM_INVERSE_MIN_TILES = 8  # batches at least this large use inverse + MFMA GEM
 def _use_inverse(batch, side, B) -> bool:
     import os
     thr = int(os.environ.get("DPLASMA_TRSM_INVERSE_MIN_TILES", TRSM_INVERSE_MIN_TILES))
-    if thr <= 0 or len(batch) < thr or B.dtype not in (torch.float64, torch.float32):
+    if thr <= 0 or len(batch) < thr or B.dtype not in (torch.float64, torch.float32, torch.complex128,
+                                                       torch.complex64):
         return False
     tris = set(int(a) for a in batch.items["a_off"])
     return len(tris) == 1
