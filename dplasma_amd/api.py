@@ -220,10 +220,12 @@ for _n in ("hetrd", "hetrd_h2b_New", "hetrd_b2s"):
 
 
 def _setrecursive(tp, hnb):
-    """dplasma_z{potrf,geqrf}_setrecursive(tp, hnb): the reference splits large CPU tile tasks into
-    sub-DAGs of hnb tiles.  On MI355X every tile kernel is already a multi-wavefront workgroup
-    program over the whole tile (and tiles of one level are batched into one launch), so the
-    hint is recorded on the taskpool (``tp.recursive_nb``) and has no further effect."""
+    """dplasma_z{potrf,geqrf}_setrecursive(tp, hnb): split large tile tasks into sub-taskpools of
+    hnb x hnb tiles (reference parsec_recursivecall, src/zpotrf_L.jdf:148-172).  POTRF runs each
+    diagonal-tile factorisation as a recursive potrf_New on the re-tiled tile (models/potrf.py
+    _recursive_potrf).  QR keeps its panel kernels: the stacked-domain engine factors a whole
+    panel per launch and the tile engine's GEQRT already blocks by IB (the T tile's mb), so the
+    hint is recorded on geqrf taskpools (``tp.recursive_nb``) without changing their schedule."""
     tp.recursive_nb = int(hnb)
     return 0
 

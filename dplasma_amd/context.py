@@ -175,6 +175,19 @@ class Context:
     def stream(self, name: str):
         return self.streams.get(name)
 
+    def local(self) -> "Context":
+        """A one-process view of this context (same device, streams and options, no communicators):
+        the context of recursive sub-taskpools that run inside one task of this rank
+        (reference: parsec_recursivecall, src/zpotrf_L.jdf:148-172)."""
+        c = object.__new__(Context)
+        c.__dict__.update(self.__dict__)
+        c.distributed, c.rank, c.world = False, 0, 1
+        c.P, c.Q, c.myrow, c.mycol = 1, 1, 0, 0
+        c.row_group = c.col_group = None
+        c.row_ranks, c.col_ranks = [0], [0]
+        c._queue = []
+        return c
+
     # ------------------------------------------------------------------ taskpools
     def add_taskpool(self, tp):
         self._queue.append(tp)

@@ -202,6 +202,15 @@ class TiledMatrix:
         v._parent = self
         return v
 
+    def tile_desc(self, m: int, n: int, hnb: int) -> "TiledMatrix":
+        """One-process descriptor over local tile (m, n) itself, tiled hnb x hnb (LAPACK storage,
+        ld = this descriptor's ld, sharing storage): the operand of a recursive sub-taskpool
+        (reference: the small_descA of parsec_recursivecall, src/zpotrf_L.jdf:148-172)."""
+        r, c = self.tile_rows(m), self.tile_cols(n)
+        off = self.offset(m, n)
+        return TiledMatrix(self.dtype, hnb, hnb, r, c, device=self.device, storage=STORAGE_LAPACK, lld=self.ld,
+                           uplo=self.uplo, data=self.data[off:], name=f"{self.name}({m},{n})")
+
     def like(self, dtype=None, storage=None, alloc=True, name=None, lm=None, ln=None) -> "TiledMatrix":
         """Same distribution/tiling, new storage (full matrix, not a view)."""
         st = storage or self.storage

@@ -80,6 +80,12 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
         raise ValueError("potrf: illegal uplo")
     if A.m != A.n or A.mb != A.nb:
         raise ValueError("potrf: A must be square with square tiles")
+    # memory-capped variant: a host-resident matrix on a GPU context, or an explicit arena cap
+    # (reference: the device memory manager's bounded block pool, tests/Testings.cmake:147)
+    if ctx.world == 1 and ((ctx.is_gpu and A.data.device.type == "cpu")
+                           or ctx.info.get_int("DPLASMA:GPU:number_of_blocks", 0) > 0):
+        from .potrf_ooc import potrf_ooc_New
+        return potrf_ooc_New(ctx, uplo, A)
     lower = uplo == dplasmaLower
     tp = Taskpool("potrf", ctx)
     # diagonal tiles on the CU-reserved stream when DPLASMA_DIAG_CUS is set (context._reserve_cus)
@@ -205,8 +211,11 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
             if own_diag:
                 off = A.offset(*dk)
 
-                def f_potrf(off=off, kb=kb, k=k):
-                    if use_rb:
+                def f_potrf(off=off, kb=kb, k=k, dk=dk):
+                    hnb = getattr(tp, "recursive_nb", 0)
+                    if hnb and hnb < kb:
+                        _recursive_potrf(tp, ctx, uplo, A, dk, hnb, info, k * A.mb)
+                    elif use_rb:
                         ops.potrf_tile(uplo, A.data, off, kb, A.ld, info, k * A.mb,
                                        zbuf=zbufs[(k % 2) * zsz:(k % 2 + 1) * zsz])
                     else:
@@ -240,7 +249,8 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
 
                     def f_trsm(rbp=rbp, tri_base=tri_base, tri_ld=tri_ld, tri_off=tri_off, kb=kb, zk=zk,
                                own=own_diag and tri_base is A.data):
-                        if not own:  # the diagonal tile arrived by broadcast: invert its 32-blocks here
+                        rec = 0 < getattr(tp, "recursive_nb", 0) < kb   # sub-taskpool left no zbuf
+                        if rec or not own:  # the diagonal tile came by broadcast: invert its 32-blocks here
                             ops.trsm_rb_prep(uplo, kb, tri_base, tri_off, tri_ld, zk)
                         ops.trsm_rb(uplo, kb, tri_base, tri_off, tri_ld, zk, rbp, A.data, A.ld)
                     t_trsm = tp.task(f"TRSM({k})", pstream(k, "panel"), f_trsm, [t_db, gate], prio=2)
@@ -355,6 +365,24 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
         return r
     tp.on_complete(_done)
     return tp.finish_build()
+
+
+def _recursive_potrf(tp, ctx, uplo, A, dk, hnb, info, info_base):
+    """POTRF(k) as a sub-taskpool: the diagonal tile re-tiled hnb x hnb and factored by potrf_New on a
+    one-process view of the context, inside the POTRF task (reference: parsec_recursivecall when
+    the tile is larger than smallnb, src/zpotrf_L.jdf:148-172).  Sub-taskpools are built once per
+    tile and reused; their info is folded into the parent's as base + iinfo."""
+    subs = tp.__dict__.setdefault("_rec_subs", {})
+    key = (dk, hnb)
+    sub = subs.get(key)
+    if sub is None:
+        lctx = ctx.local()
+        sub = subs[key] = (potrf_New(lctx, uplo, A.tile_desc(dk[0], dk[1], hnb)), lctx)
+    stp, lctx = sub
+    stp.info.zero_()
+    stp.run(lctx)
+    si = stp.info
+    info.copy_(torch.where((info == 0) & (si > 0), si + info_base, info))
 
 
 def potrf(ctx, uplo: int, A) -> int:
