@@ -295,7 +295,8 @@ __global__ __launch_bounds__(PT) void k_potrf_ll(T* __restrict__ A, int n, int s
       Blk16<T> a0;
       a0.zero();
       if (j0 > 0 && (pmask & 2)) {
-        auto X = [&](int b, int i, int p) -> T { return LD(j0 + i, p); };
+        // rows past the last (partial) column block are outside the tile: never read them
+        auto X = [&](int b, int i, int p) -> T { return (i < jb) ? LD(j0 + i, p) : ST<T>::zero(); };
         if (STAGE_Y) add_rows<T>(&a0, 1, X, Ystage, 0, j0);
         else add_rows<T>(&a0, 1, X, Yglob, 0, j0);
       }
