@@ -86,6 +86,12 @@ class Context:
         self.row_ranks: List[int] = [self.myrow * Q + c for c in range(Q)]
         self.col_ranks: List[int] = [r * Q + self.mycol for r in range(P)]
         self._build_groups()
+        if self.distributed and self.world > 1 and self.is_gpu and dist.get_backend() == "nccl":
+            # bring the default communicator up on every rank now: the dataflow transport's grouped
+            # send/recv (parallel.p2p) run on it and involve only the ranks with traffic, which must
+            # never be the call that creates it
+            t = torch.zeros(1, device=self.device)
+            dist.all_reduce(t)
         self._queue = []
         self.profiling = None  # utils.trace.Tracer when enabled
         self.dot_file = os.environ.get("DPLASMA_DOT") or None  # DOT dump of every compiled tile DAG

@@ -16,12 +16,15 @@ MI355X:
   which is what it takes to fill 256 CUs.
 * Distributed (one process per GPU): a task executes on the home rank of its
   designated tile (owner-computes, like the JDF's ``: descA(m, n)`` affinity).
-  Other tiles it touches are fetched into a per-rank slot arena before the
-  level (cached per tile version, so a panel's V/T tiles are fetched once per
-  rank, not once per update) and tiles it modifies are written back to their
-  home after the level.  Each level's traffic is ONE ``all_to_all_single``
-  (RCCL p2p over xGMI), planned identically on every rank from replicated
-  metadata; levels without traffic do no collective at all.
+  Other tiles it touches are fetched into a per-rank slot arena (cached per
+  tile version, so a panel's V/T tiles are fetched once per rank, not once per
+  update) straight from the rank holding that version (its home, or the remote
+  executor that produced it), and tiles it modifies are written back to their
+  home.  Transport is dataflow (``parallel.p2p``): each edge is issued right
+  after the level that makes it final, as grouped RCCL send/recv with only the
+  peers involved, on a communication stream, and the compute stream waits only
+  before the first level that reads it -- the PTG remote dependencies of
+  ``src/zgeqrf.jdf:84-121`` without a runtime message engine.
 
 Items carry absolute device addresses (``DAG_ITEM``, 96 bytes: six operand
 slots, layout of ``QrItem`` in ``csrc/kernels/qr.hip``) so one launch can mix tiles living in
@@ -325,8 +328,10 @@ class TileDAG:
         exe = self._home(exec_key) if world > 1 else np.zeros(ntask, dtype=np.int64)
 
         # ---------------- remote-tile plan (identical on every rank)
-        fetch_at = defaultdict(list)   # level -> rows (src, dst, key)
-        wback_at = defaultdict(list)
+        # rows (src, dst, key, version, need level, issue point, phase): fetches of a tile version
+        # into the executor's slot arena, straight from the rank holding it (its home, or the
+        # remote executor that produced it), and write-backs of remotely written tiles to their home
+        xrows = None
         slot_of: Dict[int, int] = {}
         if world > 1:
             used = modes > 0
@@ -334,14 +339,18 @@ class TileDAG:
             akeys = ops[t_idx, r_idx]
             home = self._home(akeys)
             aexe = exe[t_idx]
+            alev = level[t_idx].astype(np.int64)
+            awr = (modes[t_idx, r_idx] & 2) > 0
             rem = home != aexe
+            self._local_access = (akeys[aexe == me], alev[aexe == me], awr[aexe == me])
             if rem.any():
                 ver = rt.dag_versions(ops, modes) if rt is not None else _versions_py(ops, modes)
-                t_r, r_r = t_idx[rem], r_idx[rem]
-                k_r, h_r, e_r = akeys[rem], home[rem], aexe[rem]
-                v_r = ver[t_r, r_r].astype(np.int64)
-                w_r = (modes[t_r, r_r] & 2) > 0
-                l_r = level[t_r].astype(np.int64)
+                aver = ver[t_idx, r_idx].astype(np.int64)
+                # producer (level, executor) of every written version: version v+1 comes from the
+                # task that wrote while seeing version v
+                wk, wv, wl, we = akeys[awr], aver[awr], alev[awr], aexe[awr]
+                t_r, k_r, h_r, e_r = t_idx[rem], akeys[rem], home[rem], aexe[rem]
+                v_r, w_r, l_r = aver[rem], awr[rem], alev[rem]
                 order = np.lexsort((l_r, k_r, e_r))
                 t_r, k_r, h_r, e_r, v_r, w_r, l_r = (x[order] for x in (t_r, k_r, h_r, e_r, v_r, w_r, l_r))
                 first = np.ones(len(k_r), dtype=bool)
@@ -349,10 +358,35 @@ class TileDAG:
                 have = np.empty(len(k_r), dtype=np.int64)
                 have[1:] = v_r[:-1] + w_r[:-1]
                 need = first | (v_r != np.where(first, -1, have))
-                for i in np.nonzero(need)[0]:
-                    fetch_at[int(l_r[i])].append((int(h_r[i]), int(e_r[i]), int(k_r[i])))
-                for i in np.nonzero(w_r)[0]:
-                    wback_at[int(l_r[i])].append((int(e_r[i]), int(h_r[i]), int(k_r[i])))
+                prev_l = np.full(len(k_r), -1, dtype=np.int64)
+                prev_l[1:] = np.where(first[1:], -1, l_r[:-1])
+                fi = np.nonzero(need)[0]
+                fk, fv, fl = k_r[fi], v_r[fi], l_r[fi]
+                # producer of version fv (fv == 0: the initial data at home, available at the start)
+                prod_l = np.full(len(fi), -1, dtype=np.int64)
+                src = h_r[fi].copy()
+                if len(wk) and (fv > 0).any():
+                    uk = np.unique(np.concatenate([wk, fk]))
+                    VS = np.int64(int(max(wv.max(), fv.max())) + 2)
+                    code_w = np.searchsorted(uk, wk).astype(np.int64) * VS + wv
+                    ow = np.argsort(code_w)
+                    code_w = code_w[ow]
+                    sel = fv > 0
+                    code_q = np.searchsorted(uk, fk[sel]).astype(np.int64) * VS + (fv[sel] - 1)
+                    pos = np.searchsorted(code_w, code_q)
+                    pos = np.minimum(pos, len(code_w) - 1)
+                    okp = code_w[pos] == code_q
+                    if not okp.all():
+                        raise RuntimeError(f"{self.name}: producer of a fetched tile version not found")
+                    prod_l[sel] = wl[ow][pos]
+                    src[sel] = we[ow][pos]
+                point = np.maximum(prod_l, prev_l[fi])
+                dst = e_r[fi]
+                direct = src != dst   # the producer itself is the executor: its slot already holds it
+                f_rows = np.stack([src, dst, fk, fl, point, np.zeros(len(fi), np.int64)], 1)[direct]
+                wi = np.nonzero(w_r)[0]
+                w_rows = np.stack([e_r[wi], h_r[wi], k_r[wi], l_r[wi], l_r[wi], np.ones(len(wi), np.int64)], 1)
+                xrows = np.concatenate([f_rows, w_rows]) if len(w_rows) else f_rows
                 mine = np.unique(k_r[e_r == me])
                 cnt = defaultdict(int)
                 for k in mine.tolist():
@@ -475,58 +509,77 @@ class TileDAG:
             self._host_items = host
         self.dev_items = dev_items
 
-        # ---------------- exchange plans (one all_to_all per level, phase and dtype)
-        def xplan(rows, nbe):
-            """rows: (src, dst, key) -> my send keys, my receive keys, split sizes (elements)."""
-            rows = sorted(rows, key=lambda x: (x[0], x[1], x[2]))
-            sends = [r for r in rows if r[0] == me]
-            recvs = [r for r in rows if r[1] == me]
-            sc = [0] * world
-            rc = [0] * world
-            for s_, d_, _ in sends:
-                sc[d_] += nbe
-            for s_, d_, _ in recvs:
-                rc[s_] += nbe
-            return [k for (_, _, k) in sends], [k for (_, _, k) in recvs], sc, rc
+        # ---------------- dataflow exchanges (parallel.p2p): one per (issue point, phase, dtype),
+        # planned identically on every rank; each rank keeps only the peers it has traffic with
+        transport = None
+        if xrows is not None and len(xrows):
+            from ..parallel.p2p import Transport, Xfer, first_after
+            transport = Transport(ctx, self.name, lambda: self._bases)
+            lk, ll, lw = self._local_access
+            wk_me, wl_me = lk[lw], ll[lw]
 
-        def copy_plan(keys, nbe):
-            """Tile copies between their current place (home storage | arena) and a buffer."""
-            from ..ops.batch import TileBatch
-            groups = {}
-            if not keys:
-                return []
-            b, o, l = resolve(np.array(keys, dtype=np.int64))
-            for i, k in enumerate(keys):
-                M = self.mats[k >> _MID_SHIFT]
-                gm, gn = (k >> _M_SHIFT) & _MASK22, k & _MASK22
-                if M.storage == STORAGE_TILE:
-                    # full physical tile: kernels may use storage past a ragged edge
-                    # (TSTRF writes one pivot per panel column into an IPIV tile)
-                    rows, cols = M.mb, M.nb
-                else:
-                    rows = min(M.mb, M.lm - gm * M.mb)
-                    cols = min(M.nb, M.ln - gn * M.nb)
-                g = groups.setdefault((int(b[i]), int(l[i]), M.mb), TileBatch())
-                g.add(int(o[i]), rows, cols, b_off=i * nbe)
-            return [(bi, ldx, mb, tb.finalize()) for (bi, ldx, mb), tb in groups.items()]
+            def tref(keys):
+                b, o, l = resolve(np.asarray(keys, dtype=np.int64))
+                out = []
+                for i, k in enumerate(keys):
+                    M = self.mats[int(k) >> _MID_SHIFT]
+                    gm, gn = (int(k) >> _M_SHIFT) & _MASK22, int(k) & _MASK22
+                    if M.storage == STORAGE_TILE:
+                        # full physical tile: kernels may use storage past a ragged edge
+                        # (TSTRF writes one pivot per panel column into an IPIV tile)
+                        rows, cols = M.mb, M.nb
+                    else:
+                        rows, cols = min(M.mb, M.lm - gm * M.mb), min(M.nb, M.ln - gn * M.nb)
+                    out.append((int(b[i]), int(o[i]), int(l[i]), rows, cols, M.mb))
+                return out
 
-        xch = {}
-        for L in range(nlev):
-            for phase, rows in (("f", fetch_at.get(L)), ("w", wback_at.get(L))):
-                if not rows:
+            mid_dt = np.array([dtypes.index(M.dtype) for M in self.mats], dtype=np.int64)
+            xdt = mid_dt[xrows[:, 2] >> _MID_SHIFT]
+            # global order: issue point, write-backs before fetches, dtype, then peers / key
+            gkey = np.stack([xrows[:, 4], 1 - xrows[:, 5], xdt], 1)
+            order = np.lexsort((xrows[:, 2], xrows[:, 1], xrows[:, 0], gkey[:, 2], gkey[:, 1], gkey[:, 0]))
+            xrows, gkey = xrows[order], gkey[order]
+            brk = np.nonzero((gkey[1:] != gkey[:-1]).any(1))[0] + 1
+            starts = np.concatenate([[0], brk])
+            ends = np.concatenate([brk, [len(xrows)]])
+            transport.n_global = len(starts)
+            for xid, (a, b_) in enumerate(zip(starts, ends)):
+                rows = xrows[a:b_]
+                sm = rows[rows[:, 0] == me]
+                rm = rows[rows[:, 1] == me]
+                if not len(sm) and not len(rm):
                     continue
-                plans = []
-                for dt in dtypes:
-                    r_dt = [r for r in rows if mat_dt[r[2] >> _MID_SHIFT] == dt]
-                    if not r_dt:
-                        continue
-                    pk, uk, sc, rc = xplan(r_dt, nbe_of[dt])
-                    plans.append((dt, copy_plan(pk, nbe_of[dt]), copy_plan(uk, nbe_of[dt]), sc, rc))
-                xch[(L, phase)] = plans
+                dt = dtypes[int(gkey[a, 2])]
+                point = int(gkey[a, 0])
+                wb = gkey[a, 1] == 0
+                sends, recvs = defaultdict(list), defaultdict(list)
+                if len(sm):
+                    for (dst_r, k), ref in zip(sm[:, [1, 2]].tolist(), tref(sm[:, 2])):
+                        sends[dst_r].append(ref)
+                if len(rm):
+                    for (src_r, k), ref in zip(rm[:, [0, 2]].tolist(), tref(rm[:, 2])):
+                        recvs[src_r].append(ref)
+                x = Xfer(xid, dt, nbe_of[dt], sends, recvs, label=f"{'w' if wb else 'f'}@{point}")
+                need = None
+                if len(rm):
+                    if wb:   # write-back into my storage: first later level of mine touching the tile
+                        nx = first_after(lk, ll, rm[:, 2], np.full(len(rm), point), nlev)
+                        nx = nx[nx >= 0]
+                        need = int(nx.min()) if len(nx) else None
+                    else:
+                        need = int(rm[:, 3].min())
+                guard = None
+                if len(sm):      # first later level of mine overwriting a tile this exchange packs
+                    gx = first_after(wk_me, wl_me, sm[:, 2], np.full(len(sm), point), nlev)
+                    gx = gx[gx >= 0]
+                    guard = int(gx.min()) if len(gx) else None
+                transport.add(x, point, need, guard)
+        self.transport = transport
         self._bases = bases
-        prog = _DagProgram(self, nlev, groups, xch, dtype, device, multistream)
+        prog = _DagProgram(self, nlev, groups, transport, dtype, device, multistream)
         tp.task(self.name, "update", prog.run)
         tp.dag = prog
+        tp.transport = transport
         return tp.finish_build()
 
 
@@ -556,33 +609,17 @@ class TileDAG:
 
 
 class _DagProgram:
-    def __init__(self, dag: TileDAG, nlev, groups, xch, dtype, device, multistream):
+    def __init__(self, dag: TileDAG, nlev, groups, transport, dtype, device, multistream):
         self.dag = dag
         self.nlev = nlev
         self.groups = groups
         self.by_level = defaultdict(list)
         for i, g in enumerate(groups):
             self.by_level[g["level"]].append(i)
-        self.xch = xch
+        self.transport = transport
         self.dtype, self.device = dtype, device
         self.multistream = multistream
         self.nlaunch = len(groups)
-
-    def _exchange(self, plans, level=-1):
-        with trace.span(self.dag.ctx, f"{self.dag.name}:exchange", "comm", args={"level": level}):
-            self._exchange_now(plans)
-
-    def _exchange_now(self, plans):
-        bases = self.dag._bases
-        for dt, pack, unpack, sc, rc in plans:
-            sendbuf = torch.empty(sum(sc), dtype=dt, device=self.device)
-            recvbuf = torch.empty(sum(rc), dtype=dt, device=self.device)
-            for bi, ld, mb, tb in pack:   # tile (base, off, ld) -> sendbuf[i*nbe] (ld = mb)
-                copy_tiles(bases[bi], ld, sendbuf, mb, tb, to_b=True)
-            # every rank joins: the plan exists on all ranks whenever the level has this traffic
-            dist.all_to_all_single(recvbuf, sendbuf, output_split_sizes=rc, input_split_sizes=sc)
-            for bi, ld, mb, tb in unpack:  # recvbuf[i*nbe] -> tile
-                copy_tiles(bases[bi], ld, recvbuf, mb, tb, to_b=False)
 
     def _launch(self, g, dev_items, stream_ptr, stream_obj=None):
         with trace.span(self.dag.ctx, g["K"].name, "dag", stream_obj,
@@ -622,19 +659,23 @@ class _DagProgram:
         dev_items = dag.dev_items
         if self.multistream and dev_items is not None:
             return self._run_streams(dev_items)
-        stream = None
+        stream = sobj = None
         if self.device.type == "cuda":
             from ..ops import _lib
             stream = _lib.stream_ptr()
+            sobj = torch.cuda.current_stream(self.device)
+        tr = self.transport
+        if tr is not None:
+            tr.start(sobj)
         for L in range(self.nlev):
-            x = self.xch.get((L, "f"))
-            if x is not None:
-                self._exchange(x, L)
+            if tr is not None:
+                tr.before(L, sobj)
             for gi in self.by_level.get(L, ()):
                 self._launch(self.groups[gi], dev_items, stream)
-            x = self.xch.get((L, "w"))
-            if x is not None:
-                self._exchange(x, L)
+            if tr is not None:
+                tr.after(L, sobj)
+        if tr is not None:
+            tr.finish(sobj)
 
     def _run_streams(self, dev_items):
         """Dataflow over two streams: zero-slack (critical-path) groups on a
@@ -663,30 +704,4 @@ class _DagProgram:
             cur.wait_event(ev)
 
 
-def copy_tiles(A, lda, B, ldb, tb, to_b: bool):
-    """Copy the tiles of a TileBatch (a_off in A, b_off in B) A -> B (to_b) or B -> A.
-
-    Floating-point tiles use the batched copy kernel; integer tiles (pivot
-    vectors) are tiny and copied with tensor views."""
-    from ..constants import dplasmaNoTrans
-    from ..ops import tile_ops as ops
-    from ..ops.batch import TileBatch
-    tb.finalize()
-    if A.dtype.is_floating_point or A.dtype.is_complex:
-        if to_b:
-            ops.geadd(0, dplasmaNoTrans, 1.0, A, lda, 0.0, B, ldb, tb, copy=True)
-            return
-        sw = getattr(tb, "_swapped", None)
-        if sw is None:
-            sw = TileBatch()
-            for it in tb.items:
-                sw.add(int(it["b_off"]), int(it["m"]), int(it["n"]), b_off=int(it["a_off"]))
-            sw.finalize()
-            tb._swapped = sw
-        ops.geadd(0, dplasmaNoTrans, 1.0, B, ldb, 0.0, A, lda, sw, copy=True)
-        return
-    for it in tb.items:
-        m, n = int(it["m"]), int(it["n"])
-        a = torch.as_strided(A, (m, n), (1, lda), int(it["a_off"]))
-        b = torch.as_strided(B, (m, n), (1, ldb), int(it["b_off"]))
-        (b if to_b else a).copy_(a if to_b else b)
+from ..parallel.p2p import copy_tiles  # noqa: E402,F401  (re-export)

@@ -14,10 +14,13 @@ for one-process-per-GPU execution with batched kernels:
 * Reads see the values left by previous stages (stages are the dependency
   frontier -- the analogue of a DAG level).
 * For every stage the builder computes, for every rank, which input tiles it
-  does not own.  Execution runs ONE planned all-to-all
-  (``parallel.exchange``: RCCL over xGMI / gloo) and then ONE batched kernel
-  launch per (op kind, operand sources) group -- e.g. all GEMM updates of a
-  step in a single MFMA launch.
+  does not own.  They travel as ONE dataflow exchange per stage
+  (``parallel.p2p``: grouped RCCL send/recv with only the peers involved, on a
+  communication stream) issued right after the last stage that writes any of
+  them -- so it overlaps the stages in between -- and received in place into
+  one of ``RING`` pre-allocated receive slabs; the stage then runs ONE batched
+  kernel launch per (op kind, operand sources) group -- e.g. all GEMM updates
+  of a step in a single MFMA launch.
 * On a single rank there is no exchange at all and every operand is read in
   place.
 """
@@ -26,12 +29,12 @@ from __future__ import annotations
 from collections import defaultdict
 from typing import Callable, Dict, List, Optional, Tuple
 
+import numpy as np
 import torch
 
 from ..constants import dplasmaNoTrans
 from ..ops import tile_ops as ops
 from ..ops.batch import GemmBatch, TileBatch
-from ..parallel.exchange import ExchangePlan
 from ..utils import trace
 from .taskpool import Taskpool
 
@@ -137,38 +140,142 @@ class TileProgram:
         tp.flops = self.flops
         distributed = ctx.world > 1
         dtype = self.mats[0].dtype if self.mats else torch.float64
-        device = ctx.device
-        prev = None
-        for st in self.stages:
-            if not st.ops:
-                continue
-            plan = None
-            if distributed:
-                needs = defaultdict(list)
-                seen = defaultdict(set)
-                for op in st.ops:
-                    o = self._owner(op.out)
-                    for k in op.ins:
-                        if self._owner(k) != o and k not in seen[o]:
-                            seen[o].add(k)
-                            needs[o].append(k)
-                if any(needs.values()):
-                    plan = ExchangePlan(ctx, self.mats, dict(needs), dtype, device)
+        stages = [st for st in self.stages if st.ops]
+        self.transport = None
+        layouts: List[Optional[_RecvLayout]] = [None] * len(stages)
+        if distributed and stages:
+            self.transport = self._plan_transport(stages, layouts, dtype)
+        runners = []
+        for si, st in enumerate(stages):
             my_ops = [op for op in st.ops if self._owner(op.out) == me]
-            runner = _StageRunner(self, st, my_ops, plan)
-            prev = tp.task(st.name, "update", runner.run, [prev])
+            runners.append(_StageRunner(self, st, my_ops, layouts[si]))
+        tr = self.transport
+        prev = None
+        for si, runner in enumerate(runners):
+            def fn(si=si, runner=runner, last=(si == len(runners) - 1)):
+                s = torch.cuda.current_stream(ctx.device) if ctx.is_gpu else None
+                if tr is not None:
+                    if si == 0:
+                        tr.start(s)
+                    tr.before(si, s)
+                    runner.buf = self._ring[si % len(self._ring)] if self._ring else None
+                runner.run()
+                if tr is not None:
+                    tr.after(si, s)
+                    if last:
+                        tr.finish(s)
+            prev = tp.task(runner.st.name, "update", fn, [prev])
+        tp.transport = tr
         return tp.finish_build()
+
+    RING = 3   # receive slabs in flight: a stage's operands may arrive up to RING-1 stages early
+
+    def _plan_transport(self, stages, layouts, dtype):
+        """Dataflow exchanges (parallel.p2p): stage s's remote operands travel in one exchange
+        issued right after the last stage that writes any of them (and no earlier than stage
+        s - RING, whose receive slab it reuses), received in place into the slab."""
+        from ..parallel.p2p import Transport, Xfer, first_after
+        ctx, me, world = self.ctx, self.ctx.rank, self.ctx.world
+        mb = max(M.mb for M in self.mats)
+        nb = max(M.nb for M in self.mats)
+        nbe = mb * nb
+        K = self.RING
+        nmat = len(self.mats)
+        last_w: Dict[Key, int] = {}
+        my_writes_k, my_writes_s = [], []
+        kid: Dict[Key, int] = {}
+
+        def kcode(key):
+            c = kid.get(key)
+            if c is None:
+                c = kid[key] = len(kid)
+            return c
+        plans = []
+        for si, st in enumerate(stages):
+            needs = defaultdict(list)
+            seen = defaultdict(set)
+            ready = -1
+            for op in st.ops:
+                o = self._owner(op.out)
+                for k in op.ins:
+                    if self._owner(k) != o and k not in seen[o]:
+                        seen[o].add(k)
+                        needs[o].append(k)
+                        ready = max(ready, last_w.get(k, -1))
+            for op in st.ops:
+                last_w[op.out] = si
+                if self._owner(op.out) == me:
+                    my_writes_k.append(kcode(op.out))
+                    my_writes_s.append(si)
+            if any(needs.values()):
+                plans.append((si, dict(needs), max(ready, si - K)))
+        tr = Transport(ctx, self.name, lambda: [M.data for M in self.mats] + list(self._ring))
+        maxrecv = 0
+        wk = np.array(my_writes_k, dtype=np.int64)
+        ws = np.array(my_writes_s, dtype=np.int64)
+        for si, needs, point in plans:
+            lay = _RecvLayout(self.mats, needs.get(me, []), mb, nbe, self._owner)
+            layouts[si] = lay
+            maxrecv = max(maxrecv, lay.nrecv)
+            sends = defaultdict(list)
+            for d in range(world):
+                for key in needs.get(d, []):
+                    if self._owner(key) == me and d != me:
+                        M = self.mats[key[0]]
+                        sends[d].append((key[0], M.offset(key[1], key[2]), M.ld, M.tile_rows(key[1]),
+                                         M.tile_cols(key[2]), mb))
+            recvs = defaultdict(list)
+            for key in needs.get(me, []):
+                M = self.mats[key[0]]
+                recvs[self._owner(key)].append((nmat + si % K, lay.slot[key], mb, M.tile_rows(key[1]),
+                                                M.tile_cols(key[2]), mb))
+            x = Xfer(si, dtype, nbe, sends, recvs, label=f"{self.name}:{si}",
+                     recv_into=(nmat + si % K, 0))
+            guard = None
+            if x.send_peers:
+                sk = np.array([kcode(key) for d in sends for key in
+                               [k for k in needs.get(d, []) if self._owner(k) == me]], dtype=np.int64)
+                gx = first_after(wk, ws, sk, np.full(len(sk), point), len(stages))
+                gx = gx[gx >= 0]
+                guard = int(gx.min()) if len(gx) else None
+            tr.add(x, point, si if x.recv_peers else None, guard)
+        tr.n_global = len(plans)
+        ring = min(K, len(stages))
+        self._ring = [torch.empty(max(1, maxrecv) * nbe, dtype=dtype, device=ctx.device) for _ in range(ring)] \
+            if maxrecv else []
+        return tr
 
     def execute(self):
         return self.compile().execute(self.ctx)
 
 
+class _RecvLayout:
+    """Where a stage's remote operands sit in its receive slab: by source rank, in need order,
+    one mb x nb slot each (ld = mb) -- the layout the exchange receives in place."""
+
+    def __init__(self, mats, mine: List[Key], mb: int, nbe: int, owner):
+        self.ld = mb
+        by_src = defaultdict(list)
+        for key in mine:
+            by_src[owner(key)].append(key)
+        self.slot: Dict[Key, int] = {}
+        pos = 0
+        for s in sorted(by_src):
+            for key in by_src[s]:
+                self.slot[key] = pos * nbe
+                pos += 1
+        self.nrecv = pos
+
+    def offset(self, mid: int, m: int, n: int) -> int:
+        return self.slot[(mid, m, n)]
+
+
 class _StageRunner:
     """Resolves operand locations and groups the rank's ops into batched launches."""
 
-    def __init__(self, prog: TileProgram, st: Stage, my_ops: List[_Op], plan: Optional[ExchangePlan]):
+    def __init__(self, prog: TileProgram, st: Stage, my_ops: List[_Op], plan: Optional["_RecvLayout"]):
         self.prog, self.st, self.plan = prog, st, plan
-        self.buf = None  # receive slab, allocated per run
+        self.buf = None  # this stage's receive slab (set by the program before each run)
         self.launches = []
         mats = prog.mats
 
@@ -284,9 +391,6 @@ class _StageRunner:
 
     def _run(self):
         mats = self.prog.mats
-        if self.plan is not None:
-            self.buf = self.plan.new_recv_buffer()
-            self.plan.run(self.buf)
         B = self._base_of
         for kind, p in self.launches:
             if kind == "gemm":
@@ -328,4 +432,3 @@ class _StageRunner:
             elif kind == "batch":
                 fn, res = p
                 fn({k: (B(v[0]), v[1], v[2]) for k, v in res.items()})
-        self.buf = None
