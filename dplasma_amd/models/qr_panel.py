@@ -90,13 +90,17 @@ def step_plan(tree, k):
     return [doms[h] for h in heads], tts
 
 
+def _prow(A, m):
+    return A.grid.prow(m + A.it0)
+
+
 def usable(A, tree=None) -> bool:
     """The stacked-domain engine handles this factorisation (and therefore owns its format)."""
     if _ENGINE[0] != "panel":
         return False
     if A.dtype not in (torch.float32, torch.float64):
         return False
-    if A.grid.P != 1 or A.grid.kq != 1 or A.mb != A.nb or A.nb > ops.QR_PANEL_MAXW:
+    if A.grid.kq != 1 or A.mb != A.nb or A.nb > ops.QR_PANEL_MAXW:
         return False
     if A.device.type == "cuda" and A.m > ops.qr_panel_max_rows(A.device):
         return False
@@ -104,8 +108,9 @@ def usable(A, tree=None) -> bool:
         plans = [step_plan(tree, k) for k in range(min(A.mt, A.nt))]
         if any(p is None for p in plans):
             return False
-        # 1 x Q grids: one domain per panel and no TT kills (the panel column is one rank's)
-        if A.grid.Q > 1 and any(len(d) != 1 or t for d, t in plans):
+        # distributed grids: every TS domain lives on one process row (its owner factors it with no
+        # communication); TT kills may cross process rows (exchange of R / V2 / partial W)
+        if A.grid.P > 1 and any(len({_prow(A, r) for r in d}) != 1 for dd, _ in plans for d in dd):
             return False
     return True
 
@@ -162,7 +167,7 @@ class _Left:
                       np.repeat(woff, nrow), kf)
         self.g1, self.g2, self.g3 = g1.finalize(), g2.finalize(), g3.finalize()
 
-    def run(self, C, V, ldv, Tm, ldt, Wp, W, W2, qt: bool, group=None):
+    def run(self, C, V, ldv, Tm, ldt, Wp, W, W2, qt: bool, group=None, reduce=None):
         if self.empty:
             return
         kf, L = self.kf, self.wlen
@@ -172,6 +177,8 @@ class _Left:
             src = W
         else:
             src = Wp
+        if reduce is not None:   # reflector rows split over two process rows: add the partner's part
+            reduce(src[:L])
         ops.gemm(T_ if qt else N_, N_, 1.0, Tm, ldt, src, kf, 0.0, W2, kf, self.g2)
         ops.gemm(N_, N_, -1.0, V, ldv, W2, kf, 1.0, C.data, C.ld, self.g3)
 
@@ -312,14 +319,24 @@ class _Factor:
         dev, dt = A.device, A.dtype
         nb = A.nb
         self.kt = min(A.mt, A.nt)
-        self.dist = A.grid.Q > 1   # 1 x Q grid: the panel owner broadcasts V and T along the row
+        # distributed: V and T travel along the process row(s) of the reflector rows (RCCL);
+        # TT kills across process rows exchange R / V2 / T and the partial W between the two rows
+        self.dist = ctx.world > 1
         self.plans = [step_plan(tree, k) for k in range(self.kt)]
-        self.simple = all(len(d) == 1 and not t for d, t in self.plans)
+        for k, (doms, tts) in enumerate(self.plans):
+            for d in doms:
+                if TS.rank_of(d[0], k) != A.rank_of(d[0], k):
+                    raise ValueError("geqrf: TS must be distributed like A (tile rows and columns)")
+            for (pp, m) in tts:
+                if TT.rank_of(m, k) != A.rank_of(m, k):
+                    raise ValueError("geqrf: TT must be distributed like A (tile rows and columns)")
+        self.simple = all(len(d) == 1 and not t for d, t in self.plans) and A.grid.P == 1
         self.ldp = max(16, _rup(A.m, 16))
         nbuf = 2 if self.simple else 1
         self.P = [torch.zeros(self.ldp * nb, dtype=dt, device=dev) for _ in range(nbuf)]
         self.V = [torch.zeros(self.ldp * nb, dtype=dt, device=dev) for _ in range(nbuf)]
         self.Tm = [torch.zeros(nb * nb, dtype=dt, device=dev) for _ in range(nbuf)]
+        self.R = torch.zeros(nb * nb, dtype=dt, device=dev)     # cross-row TT: the partner's tile
         self.ws = ops.qr_panel_workspace(nb, nb, dt, dev)
         self.info = torch.zeros(1, dtype=torch.int32, device=dev)
         self.steps = [self._build(k) for k in range(self.kt)]
@@ -329,27 +346,51 @@ class _Factor:
             self.wr = _work_buffers([e["rest"] for st in self.steps for e in st if e.get("rest")], dt, dev)
         else:
             self.wr = _work_buffers(ups, dt, dev)
+        self.xtmp = torch.zeros(max([u.wlen for u in ups] + [1]), dtype=dt, device=dev)
 
     def _entry(self, k, rows, tt):
         A = self.A
+        g = A.grid
         kb = A.tile_cols(k)
         voff, c = [], 0
         for r in rows:
             voff.append(c)
             c += A.tile_rows(r)
         M = c
+        pc = g.pcol(k + A.jt0)
+        rp = _prow(A, rows[0])
+        rm = _prow(A, rows[1]) if tt else rp
         e = {"rows": rows, "voff": voff, "M": M, "kb": kb, "kf": min(M, kb), "tt": tt, "ld": max(16, _rup(M, 16)),
-             "own": A.col_is_local(k), "root": A.grid.rank(0, A.grid.pcol(k + A.jt0)), "direct": None}
+             "root": g.rank(rp, pc), "rp": rp, "rm": rm, "cross": rm != rp, "direct": None,
+             "partner": g.rank(rm, pc)}
+        # ranks of the reflector rows' process row(s) take part; the root factors
+        e["own"] = A.rank == e["root"]
+        e["is_partner"] = e["cross"] and A.rank == e["partner"]
+        e["myline"] = A.myrow in (rp, rm)
+        if e["cross"] and e["myline"]:
+            other = rm if A.myrow == rp else rp
+            e["peer"] = g.rank(other, A.mycol)      # the same process column in the other row
+        if e["is_partner"]:
+            m = rows[1]
+            rb = TileBatch().add(A.offset(m, k), A.tile_rows(m), kb, b_off=0)
+            e["r_out"] = rb.finalize()   # A(m,k) -> R buffer (ld = tile rows); upper part is R_m
+            vb = TileBatch().add(voff[1], A.tile_rows(m), kb, b_off=A.offset(m, k))
+            e["v_back"] = vb.finalize()  # V2 (upper) -> A(m,k)
         if not e["own"]:
             return e
-        g, back = TileBatch(), TileBatch()
+        g_, back = TileBatch(), TileBatch()
         part = PART_UPPER if tt else PART_FULL
-        for r, o in zip(rows, voff):
-            g.add(A.offset(r, k), A.tile_rows(r), kb, b_off=o)
+        for j, (r, o) in enumerate(zip(rows, voff)):
+            if e["cross"] and j == 1:
+                continue
+            g_.add(A.offset(r, k), A.tile_rows(r), kb, b_off=o)
             back.add(o, A.tile_rows(r), kb, b_off=A.offset(r, k))
-        e["gather"], e["back"], e["part"] = g.finalize(), back.finalize(), part
-        # a domain of consecutive tile rows is factored in place (no gather / scatter copies)
-        if not tt and list(rows) == list(range(rows[0], rows[0] + len(rows))):
+        e["gather"], e["back"], e["part"] = g_.finalize(), back.finalize(), part
+        if e["cross"]:
+            rin = TileBatch().add(0, A.tile_rows(rows[1]), kb, b_off=voff[1])
+            e["r_in"] = rin.finalize()   # R buffer -> P (upper part)
+        # a domain of consecutive tile rows stored contiguously is factored in place
+        if not tt and list(rows) == list(range(rows[0], rows[0] + len(rows))) and g.P == 1:
             if A.storage == "tile" or A.ld == A.mb:
                 e["direct"] = (A.mb, A.mb, A.mb * A.nb, A.offset(rows[0], k))
             else:
@@ -369,11 +410,17 @@ class _Factor:
                 e["next"] = _Left(A, d, e["voff"], e["kf"], nxt) if nxt else None
                 e["rest"] = _Left(A, d, e["voff"], e["kf"], rest) if rest else None
             else:
-                e["upd"] = _Left(A, d, e["voff"], e["kf"], cols) if cols else None
+                e["upd"] = _Left(A, d, e["voff"], e["kf"], cols) if (cols and e["myline"]) else None
             out.append(e)
         for (p, m) in tts:
             e = self._entry(k, [p, m], True)
-            e["upd"] = _Left(A, [p, m], e["voff"], e["kf"], cols) if cols else None
+            if not (cols and e["myline"]):
+                e["upd"] = None
+            elif e["cross"]:   # only my process row's reflector row: partial W summed with the peer
+                j = 0 if A.myrow == e["rp"] else 1
+                e["upd"] = _Left(A, [e["rows"][j]], [e["voff"][j]], e["kf"], cols)
+            else:
+                e["upd"] = _Left(A, [p, m], e["voff"], e["kf"], cols)
             out.append(e)
         return out
 
@@ -382,8 +429,21 @@ class _Factor:
         A = self.A
         P, V, Tm = self.P[buf], self.V[buf], self.Tm[buf]
         ld, M, kb, kf = e["ld"], e["M"], e["kb"], e["kf"]
+        if e["is_partner"]:
+            # cross-row TT, partner side: R_m to the root, V2 and T back, V2 into A(m,k)
+            m = e["rows"][1]
+            rows_m = A.tile_rows(m)
+            ops.geadd(PART_FULL, N_, 1.0, A.data, A.ld, 0.0, self.R, rows_m, e["r_out"], copy=True)
+            comm.p2p(sends=[(self.R[: rows_m * kb], e["root"])])
+            comm.p2p(recvs=[(V[: ld * kf], e["root"]), (Tm, e["root"])])
+            ops.geadd(PART_UPPER, N_, 1.0, V, ld, 0.0, A.data, A.ld, e["v_back"], copy=True)
+            _store_T(Tm, A.nb, kf, self.TT, m, k)
+            _keep_full_T(Tm, A.nb, kf, self.TT, m, k)
+            self._bcast(e, V, Tm, e["partner"])
+            return
         if not e["own"]:
-            self._bcast(e, V, Tm)
+            if e["myline"]:
+                self._bcast(e, V, Tm, e["root"] if A.myrow == e["rp"] else e["partner"])
             return
         if e["direct"] is not None:
             ldp, rbl, rstride, poff = e["direct"]
@@ -393,25 +453,35 @@ class _Factor:
             if e["tt"]:
                 P[: ld * kb].zero_()
             ops.geadd(e["part"], N_, 1.0, A.data, A.ld, 0.0, P, ld, e["gather"], copy=True)
+            if e["cross"]:
+                rows_m = A.tile_rows(e["rows"][1])
+                comm.p2p(recvs=[(self.R[: rows_m * kb], e["partner"])])
+                ops.geadd(PART_UPPER, N_, 1.0, self.R, rows_m, 0.0, P, ld, e["r_in"], copy=True)
             ops.qr_panel(P, ld, M, kb, kf, V, ld, Tm, A.nb, self.ws, self.info)
             ops.geadd(e["part"], N_, 1.0, P, ld, 0.0, A.data, A.ld, e["back"], copy=True)
-        if e["tt"]:
+        if e["cross"]:
+            comm.p2p(sends=[(V[: ld * kf], e["partner"]), (Tm, e["partner"])])
+        elif e["tt"]:
             _store_T(Tm, A.nb, kf, self.TT, e["rows"][1], k)
             _keep_full_T(Tm, A.nb, kf, self.TT, e["rows"][1], k)
         else:
             _store_T(Tm, A.nb, kf, self.TS, e["rows"][0], k)
             _keep_full_T(Tm, A.nb, kf, self.TS, e["rows"][0], k)
-        self._bcast(e, V, Tm)
+        self._bcast(e, V, Tm, e["root"])
 
-    def _bcast(self, e, V, Tm):
-        if self.dist:
-            comm.bcast(V[: e["ld"] * e["kf"]], e["root"], self.ctx.row_group)
-            comm.bcast(Tm, e["root"], self.ctx.row_group)
+    def _bcast(self, e, V, Tm, root):
+        """V and T along my process row (from the rank of my row that holds them)."""
+        if self.dist and self.A.grid.Q > 1:
+            comm.bcast(V[: e["ld"] * e["kf"]], root, self.ctx.row_group)
+            comm.bcast(Tm, root, self.ctx.row_group)
 
     def apply(self, e, upd, buf, work):
         if upd is None:
             return
-        upd.run(self.A, self.V[buf], e["ld"], self.Tm[buf], self.A.nb, *work, qt=True)
+        red = None
+        if e.get("cross"):
+            red = lambda w, peer=e["peer"]: comm.exchange_add(w, peer, self.xtmp)  # noqa: E731
+        upd.run(self.A, self.V[buf], e["ld"], self.Tm[buf], self.A.nb, *work, qt=True, reduce=red)
 
     def step_general(self, k):
         for e in self.steps[k]:
@@ -457,14 +527,24 @@ def factor_New(ctx, A, TS, TT, tree, name="geqrf") -> Taskpool:
 
 # ----------------------------------------------------------------------------- applications
 class _Apply:
-    """C := op(Q) C or C op(Q) with Q in the stacked-domain format (unmqr / ungqr)."""
+    """C := op(Q) C or C op(Q) with Q in the stacked-domain format (unmqr / ungqr).
+
+    P x Q grids: the reflectors of an item are built by the rank holding their storage (the domain
+    owner; for a TT kill the owner of A(m,k), whose upper triangle is V2) and travel along the
+    process row(s) of the reflector rows (left side; a cross-row TT also goes to the other row's
+    panel-column rank, and the two rows sum their partial W pairwise) or to every rank (right side:
+    the reflector rows are C's columns, the partial W is all-reduced along each process row)."""
 
     def __init__(self, ctx, side, trans, A, TS, TT, C, tree):
         self.ctx, self.A, self.TS, self.TT, self.C = ctx, A, TS, TT, C
-        self.dist = A.grid.Q > 1
+        self.dist = ctx.world > 1
+        self.pq = A.grid.P > 1
         dev, dt = A.device, A.dtype
         self.left = side == dplasmaLeft
         self.qt = trans in (dplasmaTrans, dplasmaConjTrans)
+        if self.pq and self.left and (C.grid.P != A.grid.P or any(
+                C.grid.prow(m + C.it0) != _prow(A, m) for m in range(min(C.mt, A.mt)))):
+            raise ValueError("unmqr: C's tile rows must be distributed like A's")
         asc = (self.left and self.qt) or (not self.left and not self.qt)
         seq = _sequence(A, tree)
         self.seq = seq if asc else seq[::-1]
@@ -472,10 +552,13 @@ class _Apply:
         self.V = torch.zeros(self.ldv * A.nb, dtype=dt, device=dev)
         self.Tm = torch.zeros(A.nb * A.nb, dtype=dt, device=dev)
         self.items = [self._build(s) for s in self.seq]
-        self.work = _work_buffers([it["upd"] for it in self.items if it["upd"]], dt, dev)
+        ups = [it["upd"] for it in self.items if it["upd"]]
+        self.work = _work_buffers(ups, dt, dev)
+        self.xtmp = torch.zeros(max([u.wlen for u in ups] + [1]), dtype=dt, device=dev)
 
     def _build(self, s):
         A, C = self.A, self.C
+        g = A.grid
         k = s[1]
         tt = s[0] == "tt"
         rows = [s[2], s[3]] if tt else s[2]
@@ -485,13 +568,27 @@ class _Apply:
             voff.append(c)
             c += A.tile_rows(r)
         M, kf = c, min(c, kb)
-        it = {"k": k, "tt": tt, "rows": rows, "M": M, "kf": kf, "own": A.col_is_local(k),
-              "root": A.grid.rank(0, A.grid.pcol(k + A.jt0))}
+        pc = g.pcol(k + A.jt0)
+        rp = _prow(A, rows[0])
+        rm = _prow(A, rows[1]) if tt else rp
+        holder = g.rank(rm, pc)
+        it = {"k": k, "tt": tt, "rows": rows, "M": M, "kf": kf, "own": A.rank == holder, "root": holder,
+              "rp": rp, "rm": rm, "cross": rm != rp, "relay": g.rank(rp, pc), "upd": None}
+        mycols = [n for n in range(C.nt) if C.col_is_local(n)]
         if self.left:
-            it["upd"] = _Left(C, rows, voff, kf, [n for n in range(C.nt) if C.col_is_local(n)])
+            if not self.pq:
+                it["upd"] = _Left(C, rows, voff, kf, mycols)
+            elif C.myrow in (rp, rm) and mycols:
+                if it["cross"]:
+                    j = 0 if C.myrow == rp else 1
+                    it["upd"] = _Left(C, [rows[j]], [voff[j]], kf, mycols)
+                    it["peer"] = g.rank(rm if j == 0 else rp, C.mycol)
+                else:
+                    it["upd"] = _Left(C, rows, voff, kf, mycols)
         else:
             loc = [j for j, r in enumerate(rows) if C.col_is_local(r)]
-            it["upd"] = _Right(C, list(range(C.mt)), [rows[j] for j in loc], [voff[j] for j in loc], kf,
+            myrows = [i for i in range(C.mt) if C.row_is_local(i)]
+            it["upd"] = _Right(C, myrows, [rows[j] for j in loc], [voff[j] for j in loc], kf,
                                split=not self.dist)
         if not it["own"]:
             return it
@@ -511,6 +608,30 @@ class _Apply:
         it["diag"] = dg.finalize()
         return it
 
+    def _deliver(self, it, V, ld, kf):
+        """V and T from the holder to every rank whose part of C they update."""
+        A, ctx = self.A, self.ctx
+        if not self.dist:
+            return
+        v = V[: ld * kf]
+        if not self.pq:                       # 1 x Q: along the (only) process row
+            comm.bcast(v, it["root"], ctx.row_group)
+            comm.bcast(self.Tm, it["root"], ctx.row_group)
+            return
+        if not self.left:                     # reflector rows = C's columns: every rank
+            comm.bcast(v, it["root"], None, world=True)
+            comm.bcast(self.Tm, it["root"], None, world=True)
+            return
+        if it["cross"]:                       # the other row's panel-column rank relays to its row
+            if A.rank == it["root"]:
+                comm.p2p(sends=[(v, it["relay"]), (self.Tm, it["relay"])])
+            elif A.rank == it["relay"]:
+                comm.p2p(recvs=[(v, it["root"]), (self.Tm, it["root"])])
+        if A.myrow in (it["rp"], it["rm"]) and A.grid.Q > 1:
+            src = it["root"] if A.myrow == it["rm"] else it["relay"]
+            comm.bcast(v, src, ctx.row_group)
+            comm.bcast(self.Tm, src, ctx.row_group)
+
     def run_item(self, it):
         A = self.A
         V, ld, kf = self.V, self.ldv, it["kf"]
@@ -522,11 +643,17 @@ class _Apply:
             ops.laset(PART_DIAG, 0.0, 1.0, V, ld, it["diag"])
             Td, row = (self.TT, it["rows"][1]) if it["tt"] else (self.TS, it["rows"][0])
             _rebuild_T(V, ld, it["M"], kf, Td, row, it["k"], self.Tm, A.nb)
-        if self.dist:
-            comm.bcast(V[: ld * kf], it["root"], self.ctx.row_group)
-            comm.bcast(self.Tm, it["root"], self.ctx.row_group)
-        it["upd"].run(self.C, V, ld, self.Tm, A.nb, *self.work, qt=self.qt,
-                      group=self.ctx.row_group if self.dist else None)
+        self._deliver(it, V, ld, kf)
+        if it["upd"] is None:
+            return
+        red = None
+        if self.left and it.get("peer") is not None:
+            red = lambda w, peer=it["peer"]: comm.exchange_add(w, peer, self.xtmp)  # noqa: E731
+        if self.left:
+            it["upd"].run(self.C, V, ld, self.Tm, A.nb, *self.work, qt=self.qt, reduce=red)
+        else:
+            it["upd"].run(self.C, V, ld, self.Tm, A.nb, *self.work, qt=self.qt,
+                          group=self.ctx.row_group if (self.dist and A.grid.Q > 1) else None)
 
     def run(self):
         for it in self.items:

@@ -21,8 +21,12 @@ import torch
 import torch.distributed as dist
 
 
-def bcast(t: torch.Tensor, src_global: int, group) -> None:
-    if group is None:
+def bcast(t: torch.Tensor, src_global: int, group, world: bool = False) -> None:
+    """Broadcast from global rank src_global over ``group`` (None: nothing to do -- unless ``world``,
+    then over every rank)."""
+    if group is None and not world:
+        return
+    if world and not (dist.is_initialized() and dist.get_world_size() > 1):
         return
     w = dist.broadcast(t, src=src_global, group=group, async_op=True)
     w.wait()
@@ -52,3 +56,32 @@ def allreduce(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None) -> None:
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return
     dist.all_reduce(t, op=op, group=group)
+
+
+def p2p(sends=(), recvs=()) -> None:
+    """Grouped point-to-point transfer: sends / recvs are lists of (tensor, global peer rank).
+
+    RCCL: one grouped send/recv call (every pair on its own xGMI link); the current stream waits
+    for the transfer.  gloo: CUDA tensors are staged through host memory (gloo moves host buffers)."""
+    sends, recvs = list(sends), list(recvs)
+    if not sends and not recvs:
+        return
+    if _nccl():
+        ops = [dist.P2POp(dist.isend, t, p) for t, p in sends] + [dist.P2POp(dist.irecv, t, p) for t, p in recvs]
+        for w in dist.batch_isend_irecv(ops) or ():
+            w.wait()
+        return
+    host_r = [(t, t.cpu() if t.device.type != "cpu" else t) for t, _ in recvs]
+    works = [dist.isend(t.cpu() if t.device.type != "cpu" else t, p) for t, p in sends]
+    works += [dist.irecv(h, p) for (_, h), (_, p) in zip(host_r, recvs)]
+    for w in works:
+        w.wait()
+    for t, h in host_r:
+        if h is not t:
+            t.copy_(h)
+
+
+def exchange_add(t: torch.Tensor, peer: int, tmp: torch.Tensor) -> None:
+    """t += (peer's t): symmetric pairwise sum through one send/recv pair (tmp: same size as t)."""
+    p2p([(t, peer)], [(tmp[: t.numel()], peer)])
+    t.add_(tmp[: t.numel()])

@@ -344,8 +344,9 @@ def test_hqr_unmqr_and_solve(ctx):
     assert rel_err(_dense(B)[:30], ref) < 1e-11
 
 
-def _hqr_worker(rank, world, P):
+def _hqr_worker(rank, world, P, engine="panel"):
     import dplasma_amd as dp
+    from dplasma_amd.models import qr_panel
     ctx = dp.init(device="cpu", P=P)
     dt = torch.float64
     A = dp.block_cyclic(ctx, dt, 8, 8, 68, 36)
@@ -353,19 +354,28 @@ def _hqr_worker(rank, world, P):
     TS = dp.block_cyclic(ctx, dt, 4, 8, A.mt * 4, A.nt * 8)
     TT = dp.block_cyclic(ctx, dt, 4, 8, A.mt * 4, A.nt * 8)
     tree = dp.hqr_init(dp.dplasmaNoTrans, A, dp.dplasma_GREEDY_TREE, dp.dplasma_BINARY_TREE, 2, 2)
-    dp.geqrf_param(ctx, tree, A, TS, TT)
-    C = dp.block_cyclic(ctx, dt, 8, 8, 68, 10)
-    dp.plrnt(ctx, C, 5)
-    dp.unmqr_param(ctx, dp.dplasmaLeft, dp.dplasmaConjTrans, tree, A, TS, TT, C)
-    return A.to_dense_local(), TS.to_dense_local(), TT.to_dense_local(), C.to_dense_local()
+    with qr_panel.engine(engine):
+        assert qr_panel.usable(A, tree) == (engine == "panel")
+        dp.geqrf_param(ctx, tree, A, TS, TT)
+        C = dp.block_cyclic(ctx, dt, 8, 8, 68, 10)
+        dp.plrnt(ctx, C, 5)
+        dp.unmqr_param(ctx, dp.dplasmaLeft, dp.dplasmaConjTrans, tree, A, TS, TT, C)
+        D = dp.block_cyclic(ctx, dt, 8, 8, 9, 68)
+        dp.plrnt(ctx, D, 6)
+        dp.unmqr_param(ctx, dp.dplasmaRight, dp.dplasmaNoTrans, tree, A, TS, TT, D)
+    return A.to_dense_local(), TS.to_dense_local(), TT.to_dense_local(), C.to_dense_local(), D.to_dense_local()
 
 
-@pytest.mark.parametrize("world,P", [(2, 2), (4, 2)])
-def test_hqr_distributed(world, P):
-    out = run_distributed(_hqr_worker, world, P)
-    with qr_panel.engine("tile"):
-        r = _hqr_worker(0, 1, 1)
-    for i in range(4):
+@pytest.mark.parametrize("world,P,engine", [(2, 2, "tile"), (4, 2, "tile"), (2, 2, "panel"), (4, 2, "panel"),
+                                            (8, 2, "panel")])
+def test_hqr_distributed(world, P, engine):
+    """geqrf_param + unmqr_param (left and right) on P x Q grids match one process with the same
+    engine: the tile DAG, or the stacked-domain engine (process-row TS domains, cross-row TT kills
+    exchanging R / V2 / T and the partial W)."""
+    out = run_distributed(_hqr_worker, world, P, engine)
+    with qr_panel.engine(engine):
+        r = _hqr_worker(0, 1, 1, engine)
+    for i in range(5):
         assert rel_err(sum(out[k][i] for k in range(world)), r[i]) < 1e-12, i
 
 
@@ -562,3 +572,43 @@ def test_qr_kept_T_matches_rebuilt(ctx, prec):
 @pytest.mark.parametrize("prec", ["d", "s"])
 def test_gpu_qr_kept_T_matches_rebuilt(gctx, prec):
     assert _kept_vs_rebuilt(gctx, DTYPES[prec]) < (1e-4 if prec == "s" else 1e-11)
+
+
+def _hqr_check_worker(rank, world, P, treeargs, M, N, NB, IB):
+    import dplasma_amd as dp
+    from dplasma_amd.models import qr_panel
+    ctx = dp.init(device="cpu", P=P)
+    dt = torch.float64
+    A = dp.block_cyclic(ctx, dt, NB, NB, M, N)
+    dp.plrnt(ctx, A, 3872)
+    TS = dp.block_cyclic(ctx, dt, IB, NB, A.mt * IB, A.nt * NB)
+    TT = dp.block_cyclic(ctx, dt, IB, NB, A.mt * IB, A.nt * NB)
+    tree = dp.hqr_init(dp.dplasmaNoTrans, A, *treeargs)
+    used = qr_panel.usable(A, tree)
+    dp.geqrf_param(ctx, tree, A, TS, TT)
+    K = min(M, N)
+    Q = dp.block_cyclic(ctx, dt, NB, NB, M, K)
+    dp.ungqr_param(ctx, tree, A, TS, TT, Q)
+    B = dp.block_cyclic(ctx, dt, NB, NB, M, 3)
+    dp.plrnt(ctx, B, 11)
+    dp.geqrs_param(ctx, tree, A, TS, TT, B)
+    return used, A.to_dense_local(), Q.to_dense_local(), B.to_dense_local()
+
+
+@pytest.mark.parametrize("world,P,treeargs", [(4, 2, (0, 0, 3, 2)), (4, 2, (1, 3, 2, 2)), (8, 2, (1, 0, 4, 2)),
+                                              (8, 4, (3, 1, 2, 4))])
+def test_hqr_engine_distributed_checks(world, P, treeargs):
+    """The reference's testing_zgeqrf_hqr checks on P x Q grids with the stacked-domain engine:
+    ||I - Q^T Q||, ||A - Q R|| / ||A|| and the least-squares solve, from the distributed factors."""
+    M, N, NB, IB = 96, 56, 8, 4
+    out = run_distributed(_hqr_check_worker, world, P, treeargs, M, N, NB, IB)
+    assert all(out[r][0] for r in range(world))   # the distributed engine ran
+    R = torch.triu(sum(out[r][1] for r in range(world))[:N])
+    Qd = sum(out[r][2] for r in range(world))
+    X = sum(out[r][3] for r in range(world))[:N]
+    ctx = dp.Context(device="cpu")
+    A0 = _mk(ctx, torch.float64, M, N, NB, 3872).to_dense_local()
+    B0 = _mk(ctx, torch.float64, M, 3, NB, 11).to_dense_local()
+    assert (Qd.T @ Qd - torch.eye(N, dtype=torch.float64)).abs().max() < 1e-13
+    assert (Qd @ R - A0).abs().max() / A0.abs().max() < 1e-13
+    assert rel_err(X, torch.linalg.lstsq(A0, B0).solution) < 1e-11
