@@ -142,6 +142,10 @@ from .runtime import dtd  # noqa: E402
 from .models import dtd_potrf as _dtdp  # noqa: E402
 register_op("potrf_dtd", _dtdp.potrf_dtd)
 register_op("potrf_dtd_New", _dtdp.potrf_dtd_New)
+register_op("potrf_dtd_untied", _dtdp.potrf_dtd_untied)
+register_op("gemm_dtd", _dtdp.gemm_dtd)
+register_op("gemm_dtd_New", _dtdp.gemm_dtd_New)
+register_op("potrf_dtd_untied_New", _dtdp.potrf_dtd_untied_New)
 for _n in ("taskpool_new", "tile_of", "INPUT", "OUTPUT", "INOUT", "AFFINITY", "VALUE", "SCRATCH", "PUSHOUT"):
     _register("dtd_" + _n, getattr(dtd, _n))
 _register("dtd", dtd)

@@ -52,14 +52,10 @@ def _gemm_body(ta, tb_, alpha, beta, mask):
     return body
 
 
-def potrf_dtd_New(ctx, uplo, A):
-    """Tile Cholesky through DTD insert_task (returns a compiled taskpool; result() = info)."""
-    if A.mb != A.nb:
-        raise ValueError("square tiles required")
-    info = torch.zeros(1, dtype=torch.int32, device=A.device)
+def _insert_potrf(tp, uplo, A, info):
+    """The tile Cholesky as DTD tasks, with the reference's flushes (testing_zpotrf_dtd_untied.c)."""
     bases = [k * A.mb for k in range(A.mt)]
     ct = dplasmaConjTrans if A.dtype.is_complex else dplasmaTrans
-    tp = dtd.taskpool_new(ctx, "potrf_dtd")
     potrf = tp.task_class("potrf", _potrf_body(uplo, info, bases))
     if uplo == dplasmaLower:
         trsm = tp.task_class("trsm", _trsm_body(dplasmaRight, dplasmaLower, ct))
@@ -71,13 +67,15 @@ def potrf_dtd_New(ctx, uplo, A):
         gemm = tp.task_class("gemm", _gemm_body(ct, dplasmaNoTrans, -1.0, 1.0, 0))
     T = dtd.tile_of
     In, InOut, Aff = dtd.INPUT, dtd.INOUT, dtd.AFFINITY
+    total = A.mt
     for k in range(A.mt):
-        tp.insert_task(potrf, (T(A, k, k), InOut | Aff), k)
+        tp.insert_task(potrf, (T(A, k, k), InOut | Aff), k, priority=(total - k) ** 3)
         for m in range(k + 1, A.mt):
             if uplo == dplasmaLower:
                 tp.insert_task(trsm, (T(A, k, k), In), (T(A, m, k), InOut | Aff))
             else:
                 tp.insert_task(trsm, (T(A, k, k), In), (T(A, k, m), InOut | Aff))
+        tp.data_flush(T(A, k, k))
         for m in range(k + 1, A.mt):
             if uplo == dplasmaLower:
                 tp.insert_task(herk, (T(A, m, k), In), (T(A, m, k), In), (T(A, m, m), InOut | Aff))
@@ -87,18 +85,110 @@ def potrf_dtd_New(ctx, uplo, A):
                 tp.insert_task(herk, (T(A, k, m), In), (T(A, k, m), In), (T(A, m, m), InOut | Aff))
                 for n in range(k + 1, m):
                     tp.insert_task(gemm, (T(A, k, n), In), (T(A, k, m), In), (T(A, n, m), InOut | Aff))
+            tp.data_flush(T(A, m, k) if uplo == dplasmaLower else T(A, k, m))
     tp.flops = flops(A.prec, "potrf", A.m)
-    ctp = tp.compile()
+    tp.data_flush_all(A)
 
+
+def _info_reducer(ctx, info):
     def _done():
         v = info.clone()
         if ctx.world > 1:
             import torch.distributed as dist
             dist.all_reduce(v, op=dist.ReduceOp.MAX)
         return int(v.item())
-    ctp.on_complete(_done)
+    return _done
+
+
+def potrf_dtd_New(ctx, uplo, A):
+    """Tile Cholesky through DTD insert_task (deferred: a compiled taskpool; result() = info)."""
+    if A.mb != A.nb:
+        raise ValueError("square tiles required")
+    info = torch.zeros(1, dtype=torch.int32, device=A.device)
+    tp = dtd.taskpool_new(ctx, "potrf_dtd", window=0)
+    _insert_potrf(tp, uplo, A, info)
+    ctp = tp.compile()
+    ctp.on_complete(_info_reducer(ctx, info))
     return ctp
 
 
-def potrf_dtd(ctx, uplo, A):
-    return potrf_dtd_New(ctx, uplo, A).execute(ctx)
+def potrf_dtd(ctx, uplo, A, window=None):
+    """Blocking DTD Cholesky: windows of inserted tasks run while insertion continues."""
+    if A.mb != A.nb:
+        raise ValueError("square tiles required")
+    info = torch.zeros(1, dtype=torch.int32, device=A.device)
+    tp = dtd.taskpool_new(ctx, "potrf_dtd", window=window)
+    tp.on_complete(_info_reducer(ctx, info))
+    _insert_potrf(tp, uplo, A, info)
+    r = tp.wait()
+    potrf_dtd.last = tp
+    return r
+
+
+def potrf_dtd_untied(ctx, uplo, A, window=None):
+    """The reference's untied variant (tests/testing_zpotrf_dtd_untied.c): ONE task is inserted, and
+    its body inserts the whole Cholesky into the taskpool it runs in (single process)."""
+    if ctx.world > 1:
+        raise NotImplementedError("untied DTD insertion needs a single process")
+    info = torch.zeros(1, dtype=torch.int32, device=A.device)
+    tp = dtd.taskpool_new(ctx, "potrf_dtd_untied", window=window)
+    tp.on_complete(_info_reducer(ctx, info))
+
+    def inserter(a00):
+        _insert_potrf(tp, uplo, A, info)
+    tp.insert_task(tp.task_class("insert_tasks", inserter), (dtd.tile_of(A, 0, 0), dtd.INPUT))
+    tp.data_flush()
+    r = tp.wait()
+    potrf_dtd_untied.last = tp
+    return r
+
+
+# ----------------------------------------------------------------------------- GEMM
+def gemm_dtd(ctx, transA, transB, alpha, A, B, beta, C, window=None):
+    """C = alpha op(A) op(B) + beta C through DTD insert_task (tests/testing_zgemm_dtd.c: one GEMM task
+    per (m, n, k), the C tile's owner computes; k runs in order on each C tile)."""
+    Ka = A.nt if transA == dplasmaNoTrans else A.mt
+    tp = dtd.taskpool_new(ctx, "gemm_dtd", window=window)
+    bodies = {}
+
+    def body_for(beta_k):
+        b = bodies.get(beta_k)
+        if b is None:
+            b = bodies[beta_k] = tp.task_class(f"gemm_b{beta_k}", _gemm_body(transA, transB, alpha, beta_k, 0))
+        return b
+    T = dtd.tile_of
+    In, InOut, Aff = dtd.INPUT, dtd.INOUT, dtd.AFFINITY
+    for m in range(C.mt):
+        for n in range(C.nt):
+            for k in range(Ka):
+                ta = T(A, m, k) if transA == dplasmaNoTrans else T(A, k, m)
+                tb = T(B, k, n) if transB == dplasmaNoTrans else T(B, n, k)
+                tp.insert_task(body_for(beta if k == 0 else 1.0), (ta, In), (tb, In), (T(C, m, n), InOut | Aff))
+    tp.flops = flops(C.prec, "gemm", C.m, C.n, A.n if transA == dplasmaNoTrans else A.m)
+    tp.data_flush_all(C)
+    tp.wait()
+    gemm_dtd.last = tp
+    return 0
+
+
+def _blocking_New(name, ctx, fn, flops_):
+    """A taskpool whose run inserts and executes a windowed DTD algorithm (insertion inside the timed
+    region, concurrent with execution -- the reference's testing_z*_dtd drivers)."""
+    from ..runtime.taskpool import Taskpool
+    tp = Taskpool(name, ctx)
+    tp.flops = flops_
+    box = {}
+    tp.task(name, "update", lambda: box.__setitem__("r", fn()))
+    tp.on_complete(lambda: box.get("r"))
+    return tp.finish_build()
+
+
+def potrf_dtd_untied_New(ctx, uplo, A, window=None):
+    return _blocking_New("potrf_dtd_untied", ctx, lambda: potrf_dtd_untied(ctx, uplo, A, window),
+                         flops(A.prec, "potrf", A.m))
+
+
+def gemm_dtd_New(ctx, transA, transB, alpha, A, B, beta, C, window=None):
+    K = A.n if transA == dplasmaNoTrans else A.m
+    return _blocking_New("gemm_dtd", ctx, lambda: gemm_dtd(ctx, transA, transB, alpha, A, B, beta, C, window),
+                         flops(C.prec, "gemm", C.m, C.n, K))

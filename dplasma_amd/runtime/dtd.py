@@ -7,15 +7,27 @@ Reference surface (SURVEY.md §2.2 "DTD"): ``parsec_dtd_taskpool_new``,
 ``parsec_dtd_data_flush(_all)`` -- used by ``src/dtd_wrappers/zpotrf.c:151-171``
 and ``tests/testing_zpotrf_dtd.c:74-311``.
 
-Design: inserted tasks go, in program order, into a :class:`TileDAG`; their
-tile arguments become the DAG roles (access mode from the flags) and every
-other argument is passed through by value.  Executing the taskpool runs the
-DAG with the dataflow executor (levels, critical-path stream, distributed
-fetch/write-back), and each task body is called with tensor views of its
-tiles on the tile's device -- so a body that calls dplasma_amd tile kernels
-(or any torch op) runs on the GPU stream the runtime chose.  Tasks execute on
-the rank owning the AFFINITY tile (default: the first written tile), exactly
-the DTD placement rule.
+Design: inserted tasks go, in program order, into a *window*; their tile
+arguments become DAG roles (access mode from the flags) and every other
+argument is passed through by value.  When the window holds ``window`` tasks
+(``parsec_dtd_window_size``; ``DPLASMA_DTD_WINDOW``, default 4096) it is
+compiled into a :class:`TileDAG` and launched at once -- on the GPU the
+launches are asynchronous, so insertion of the next window overlaps the
+execution of the previous one, as PaRSEC's DTD engine runs tasks while the
+application is still inserting.  Consecutive windows are ordered by the
+stream (and, distributed, by each window's write-backs), so program-order
+semantics hold across window boundaries.  Each task body is called with tensor
+views of its tiles on the tile's device -- a body that calls dplasma_amd tile
+kernels (or any torch op) runs on the GPU stream the runtime chose.  Tasks
+execute on the rank owning the AFFINITY tile (default: the first written
+tile), exactly the DTD placement rule.
+
+``data_flush(tile | M)`` launches the pending window: every tile it wrote is
+back at its home, and the remote copies of windows older than the last two are
+released (``parsec_dtd_data_flush``: the bound on memory).  Bodies may insert
+further tasks into the taskpool they run in ("untied" tasks,
+``tests/testing_zpotrf_dtd_untied.c``): those land after everything inserted
+so far and run in a later window (single process).
 
 A task class may instead provide a batched ``Kind`` (``task_class(kind=...)``):
 then all ready tasks of that class in a level become one kernel launch.
@@ -56,15 +68,29 @@ class TaskClass:
 
 
 class DTDTaskpool:
-    """``parsec_dtd_taskpool_new`` analogue; compile with :meth:`compile` or run with :meth:`execute`."""
+    """``parsec_dtd_taskpool_new`` analogue: insert tasks, then :meth:`wait` (or :meth:`execute`)."""
 
-    def __init__(self, ctx, name: str = "dtd"):
+    KEEP = 2   # windows whose remote copies stay alive (older ones are released on flush)
+
+    def __init__(self, ctx, name: str = "dtd", window: Optional[int] = None):
+        import os
         self.ctx = ctx
         self.name = name
-        self.dag = TileDAG(ctx, name)
+        # window = 0: deferred -- nothing runs until compile() / wait() (the _New taskpools)
+        w = int(os.environ.get("DPLASMA_DTD_WINDOW", 4096)) if window is None else int(window)
+        self.window = w if w > 0 else float("inf")
+        self._new_dag()
         self._kinds: Dict[tuple, Kind] = {}
         self.ntasks = 0
         self.flops = 0.0
+        self.pending = 0
+        self.windows_run = 0          # windows launched so far (insertion continues meanwhile)
+        self._live: List[tuple] = []  # (compiled taskpool, completion event) of recent windows
+        self._running = False
+        self._on_complete: List[Callable] = []
+
+    def _new_dag(self):
+        self.dag = TileDAG(self.ctx, f"{self.name}[{getattr(self, 'windows_run', 0)}]")
 
     def task_class(self, name: str, body: Callable, kind: Optional[Kind] = None) -> TaskClass:
         return TaskClass(name, body, kind)
@@ -78,10 +104,13 @@ class DTDTaskpool:
             self._kinds[key] = K
         return K
 
-    def insert_task(self, fn, *args, name: Optional[str] = None, flops: float = 0.0):
+    def insert_task(self, fn, *args, name: Optional[str] = None, flops: float = 0.0, priority: int = 0):
         """Insert one task.  ``args`` mixes tile arguments ``(tile_of(A, m, n), INPUT|INOUT|OUTPUT[|AFFINITY])``
         (or a bare TileRef, read-only) and plain values; the body is called as
-        ``fn(*tile_views, *values)`` with tiles first, in argument order."""
+        ``fn(*tile_views, *values)`` with tiles first, in argument order.  ``priority`` is accepted
+        for API parity (within a window, tasks of one level run in one batch)."""
+        if self._running and self.ctx.world > 1:
+            raise RuntimeError("DTD: inserting from a task body is supported on a single process")
         tc = fn if isinstance(fn, TaskClass) else TaskClass(name or getattr(fn, "__name__", "task"), fn)
         tiles, modes, values = [], [], []
         affinity = None
@@ -110,24 +139,81 @@ class DTDTaskpool:
         keys = [int(self.dag.keys(t.M, t.m, t.n)) for t in tiles]
         self.dag.add(K, [keys], [[0, 0, 0]], pyargs=[tuple(values)])
         self.ntasks += 1
+        self.pending += 1
         self.flops += flops
+        if self.pending >= self.window and not self._running:
+            self._launch()
 
-    def data_flush(self, M=None):
-        """parsec_dtd_data_flush(_all): data is always written back to its home
-        tile by the end of a run, so this only documents the intent."""
+    # ------------------------------------------------------------------ execution
+    def _launch(self):
+        """Compile the pending window and start it (asynchronous on the GPU)."""
+        while self.pending:
+            dag, self.pending = self.dag, 0
+            self.windows_run += 1
+            self._new_dag()
+            tp = dag.compile()
+            self._running = True
+            try:
+                tp.run(self.ctx)
+            finally:
+                self._running = False
+            ev = None
+            if self.ctx.is_gpu:
+                import torch
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.ctx.device))
+            self._live.append((tp, ev))
+            if self.pending < self.window:   # tasks inserted by bodies wait for the next trigger
+                break
+
+    def _release(self, keep: int):
+        while len(self._live) > keep:
+            tp, ev = self._live.pop(0)
+            if ev is not None:
+                ev.synchronize()
+            tp.destruct()
+
+    def data_flush(self, tile=None):
+        """parsec_dtd_data_flush(_all): launch what is pending (the data goes home) and release the
+        remote copies of older windows.  Deferred taskpools (window 0) flush at the end of their run."""
+        if self.window == float("inf"):
+            return 0
+        self._launch()
+        self._release(self.KEEP)
         return 0
 
     data_flush_all = data_flush
 
+    def on_complete(self, fn: Callable):
+        self._on_complete.append(fn)
+
+    def wait(self):
+        """parsec_dtd_taskpool_wait: run everything inserted (including tasks inserted by bodies)."""
+        while self.pending:
+            self._launch()
+        if self.ctx.is_gpu:
+            import torch
+            torch.cuda.current_stream(self.ctx.device).synchronize()
+        self._release(0)
+        res = None
+        for fn in self._on_complete:
+            r = fn()
+            if r is not None:
+                res = r
+        return res
+
     def compile(self):
-        self.dag.flops = self.flops
-        tp = self.dag.compile()
+        """The pending tasks as one compiled (re-runnable) taskpool: the _New form of a DTD algorithm."""
+        dag, self.pending = self.dag, 0
+        self._new_dag()
+        dag.flops = self.flops
+        tp = dag.compile()
         tp.ntasks = self.ntasks
         return tp
 
     def execute(self):
-        return self.compile().execute(self.ctx)
+        return self.wait()
 
 
-def taskpool_new(ctx, name: str = "dtd") -> DTDTaskpool:
-    return DTDTaskpool(ctx, name)
+def taskpool_new(ctx, name: str = "dtd", window: Optional[int] = None) -> DTDTaskpool:
+    return DTDTaskpool(ctx, name, window)

@@ -165,15 +165,16 @@ class Harness:
 
 
 # ----------------------------------------------------------------------------- operations
-def t_potrf(h, dtd=False):
+def t_potrf(h, dtd=False, untied=False):
     dp, a, ctx = h.dp, h.a, h.ctx
     uplo = dp.dplasmaLower if a.uplo.upper() == "L" else dp.dplasmaUpper
     A = h.mat(a.N, a.N)
     dp.plghe(ctx, float(a.N), dp.dplasmaUpperLower, A, a.seed)
     A0 = A.like()
     A0.data.copy_(A.data)
-    fn = dp.potrf_dtd_New if dtd else dp.potrf_New
-    info = h.run_tp("potrf_dtd" if dtd else "potrf", lambda: fn(ctx, uplo, A))
+    fn = dp.potrf_dtd_untied_New if untied else (dp.potrf_dtd_New if dtd else dp.potrf_New)
+    name = "potrf_dtd_untied" if untied else ("potrf_dtd" if dtd else "potrf")
+    info = h.run_tp(name, lambda: fn(ctx, uplo, A))
     if a.check:
         ok, res = dp.check_potrf(ctx, uplo, A, A0)
         h.check("||L L^H - A|| / (||A|| N eps)", res, 60.0)
@@ -197,7 +198,7 @@ def t_posv(h):
         h.check("||Ax-b|| / ((||A|| ||x|| + ||b||) N eps)", res, 60.0)
 
 
-def t_gemm(h):
+def t_gemm(h, dtd=False):
     dp, a, ctx = h.dp, h.a, h.ctx
     M, N, K = a.M or a.N, a.N, a.K or a.N
     A, B, C = h.mat(M, K, name="A"), h.mat(K, N, name="B"), h.mat(M, N, name="C")
@@ -206,7 +207,8 @@ def t_gemm(h):
     dp.plrnt(ctx, C, a.seed + 2)
     if a.check:
         a_, b_, c_ = (_dense(h, X) for X in (A, B, C))
-    h.run_tp("gemm", lambda: dp.gemm_New(ctx, dp.dplasmaNoTrans, dp.dplasmaNoTrans, a.alpha, A, B, 0.5, C))
+    fn = dp.gemm_dtd_New if dtd else dp.gemm_New
+    h.run_tp("gemm_dtd" if dtd else "gemm", lambda: fn(ctx, dp.dplasmaNoTrans, dp.dplasmaNoTrans, a.alpha, A, B, 0.5, C))
     if a.check:
         ref = a.alpha * (a_ @ b_) + 0.5 * c_
         got = _dense(h, C)
@@ -463,6 +465,7 @@ def _dense(h, X):
 
 OPS = {
     "potrf": t_potrf, "potrf_dtd": lambda h: t_potrf(h, dtd=True), "posv": t_posv, "gemm": t_gemm,
+    "potrf_dtd_untied": lambda h: t_potrf(h, untied=True), "gemm_dtd": lambda h: t_gemm(h, dtd=True),
     "trsm": t_trsm, "trmm": t_trmm,
     "geqrf": lambda h: _qr_common(h, False, None), "gelqf": lambda h: _qr_common(h, True, None),
     "geqrf_hqr": lambda h: _qr_common(h, False, "hqr"), "gelqf_hqr": lambda h: _qr_common(h, True, "hqr"),

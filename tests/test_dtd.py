@@ -50,18 +50,62 @@ def test_potrf_dtd(ctx, uplo, dt):
         assert rel_err(torch.triu(got), L.conj().T) < 1e-12
 
 
-def _worker(rank, world, P):
+@pytest.mark.parametrize("window", [1, 7, 40])
+def test_potrf_dtd_windows_overlap_insertion(ctx, window):
+    """Windowed DTD: windows launch while insertion continues (windows_run grows with the task
+    count), data_flush keeps at most KEEP windows of remote copies, the result is unchanged."""
+    N, NB = 90, 16
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+    dp.plghe(ctx, float(N), dp.dplasmaUpperLower, A, 5)
+    L = torch.linalg.cholesky(A.to_dense_local())
+    assert potrf_dtd(ctx, dp.dplasmaLower, A, window=window) == 0
+    tp = potrf_dtd.last
+    assert tp.windows_run >= tp.ntasks // window // 2 and tp.windows_run > 1
+    assert len(tp._live) == 0
+    assert rel_err(torch.tril(A.to_dense_local()), L) < 1e-12
+
+
+def test_potrf_dtd_untied(ctx):
+    """One inserted task inserts the whole factorisation from its body (testing_zpotrf_dtd_untied.c)."""
+    from dplasma_amd.models.dtd_potrf import potrf_dtd_untied
+    N, NB = 80, 16
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+    dp.plghe(ctx, float(N), dp.dplasmaUpperLower, A, 8)
+    L = torch.linalg.cholesky(A.to_dense_local())
+    assert potrf_dtd_untied(ctx, dp.dplasmaLower, A, window=9) == 0
+    assert potrf_dtd_untied.last.ntasks > 1 and potrf_dtd_untied.last.windows_run > 2
+    assert rel_err(torch.tril(A.to_dense_local()), L) < 1e-12
+
+
+@pytest.mark.parametrize("ta,tb", [(111, 111), (112, 111), (111, 113)])
+def test_gemm_dtd(ctx, ta, tb):
+    """tests/testing_zgemm_dtd.c: GEMM through insert_task matches the dense product."""
+    from dplasma_amd.models.dtd_potrf import gemm_dtd
+    M, N, K, NB = 50, 40, 36, 8
+    dt = torch.complex128 if tb == 113 else torch.float64
+    A = dp.block_cyclic(ctx, dt, NB, NB, *((M, K) if ta == 111 else (K, M)))
+    B = dp.block_cyclic(ctx, dt, NB, NB, *((K, N) if tb == 111 else (N, K)))
+    C = dp.block_cyclic(ctx, dt, NB, NB, M, N)
+    for X, s in ((A, 1), (B, 2), (C, 3)):
+        dp.plrnt(ctx, X, s)
+    a, b, c = A.to_dense_local(), B.to_dense_local(), C.to_dense_local()
+    op = lambda x, t: x if t == 111 else (x.T if t == 112 else x.conj().T)  # noqa: E731
+    gemm_dtd(ctx, ta, tb, 0.5, A, B, -0.25, C, window=13)
+    assert rel_err(C.to_dense_local(), 0.5 * op(a, ta) @ op(b, tb) - 0.25 * c) < 1e-12
+
+
+def _worker(rank, world, P, window=None):
     import dplasma_amd as dp
     from dplasma_amd.models.dtd_potrf import potrf_dtd
     ctx = dp.init(device="cpu", P=P)
     A = dp.block_cyclic(ctx, torch.float64, 16, 16, 70, 70)
     dp.plghe(ctx, 70.0, dp.dplasmaUpperLower, A, 3)
-    return potrf_dtd(ctx, dp.dplasmaLower, A), A.to_dense_local()
+    return potrf_dtd(ctx, dp.dplasmaLower, A, window=window), A.to_dense_local()
 
 
-@pytest.mark.parametrize("world,P", [(2, 1), (4, 2)])
-def test_potrf_dtd_distributed(world, P):
-    out = run_distributed(_worker, world, P)
+@pytest.mark.parametrize("world,P,window", [(2, 1, None), (4, 2, None), (4, 2, 11)])
+def test_potrf_dtd_distributed(world, P, window):
+    out = run_distributed(_worker, world, P, window)
     ctx = dp.init(device="cpu")
     A = dp.block_cyclic(ctx, torch.float64, 16, 16, 70, 70)
     dp.plghe(ctx, 70.0, dp.dplasmaUpperLower, A, 3)

@@ -28,6 +28,8 @@ def _run(args, nproc=1):
     "dgetrf_incpiv -N 200 -t 50 -i 10 -x", "dgetrf_ptgpanel -N 200 -t 50 -x", "dlange -M 87 -N 83 -t 16 -x",
     # the remaining common.c flags: LAPACK storage (-A lld), cores, scheduler name, recursive hint, sync
     "dpotrf -N 300 -t 64 -A 320 -c 2 -o LFQ -z 32 -b -x", "dgemm -M 90 -N 70 -K 50 -t 16 -A 100 -B 60 -C 100 -x",
+    # DTD drivers (testing_zpotrf_dtd, testing_zpotrf_dtd_untied, testing_zgemm_dtd)
+    "dpotrf_dtd -N 200 -t 32 -x", "dpotrf_dtd_untied -N 200 -t 32 -x", "dgemm_dtd -M 90 -N 70 -K 50 -t 16 -x",
 ])
 def test_cli_single(args):
     r = _run(args.split())
