@@ -80,9 +80,35 @@ py::tuple dag_schedule(I64 ops, U8 modes) {
   return py::make_tuple(lv, bl, es, ed);
 }
 
+py::array_t<int64_t> dag_list_schedule(I64 pred_ptr, I64 pred_idx, py::array_t<int32_t, py::array::c_style |
+                                        py::array::forcecast> prio, int policy, uint64_t seed) {
+  const int64_t n = prio.shape(0);
+  if (pred_ptr.ndim() != 1 || pred_ptr.shape(0) != n + 1)
+    throw std::invalid_argument("dag_list_schedule: pred_ptr must have ntasks + 1 entries");
+  const int64_t* pp = pred_ptr.data();
+  const int64_t* pi = pred_idx.data();
+  if (pp[0] != 0 || pp[n] != pred_idx.shape(0))
+    throw std::invalid_argument("dag_list_schedule: pred_ptr does not describe pred_idx");
+  for (int64_t e = 0; e < pred_idx.shape(0); ++e)
+    if (pi[e] < 0 || pi[e] >= n) throw std::invalid_argument("dag_list_schedule: predecessor out of range");
+  std::vector<int64_t> order;
+  {
+    py::gil_scoped_release rel;
+    order = dpl_dag::list_schedule(n, pp, pi, prio.data(), policy, seed);
+  }
+  if (static_cast<int64_t>(order.size()) != n) throw std::invalid_argument("dag_list_schedule: the graph has a cycle");
+  py::array_t<int64_t> out(n);
+  std::copy(order.begin(), order.end(), out.mutable_data());
+  return out;
+}
+
 }  // namespace
 
 void register_dag(py::module_& m) {
+  m.def("dag_list_schedule", &dag_list_schedule, py::arg("pred_ptr"), py::arg("pred_idx"), py::arg("prio"),
+        py::arg("policy"), py::arg("seed") = 0,
+        "Issue order of a task graph under a ready-queue policy (0 program, 1 priority, 2 inverse "
+        "priority, 3 FIFO, 4 LIFO, 5 random)");
   m.def("dag_schedule", &dag_schedule, py::arg("ops"), py::arg("modes"),
         "(level, bottom level, edge sources, edge destinations) of a program-order tile DAG");
   m.def("dag_levels", &dag_levels, py::arg("ops"), py::arg("modes"),

@@ -119,4 +119,71 @@ inline Schedule schedule(const int64_t* ops, const uint8_t* modes, int64_t n, in
   return S;
 }
 
+// ---------------------------------------------------------------- ready-queue list scheduler
+// The issue order of a task graph under one of the reference's scheduler policies (PaRSEC's
+// "-o" choice, tests/common.c): tasks become ready when all predecessors are issued and are taken
+// from the ready set by the policy's key.  pred_ptr / pred_idx: CSR predecessor lists (any order).
+enum Policy : int {
+  POL_PROGRAM = 0,  // program order (default)
+  POL_PRIO = 1,     // highest priority first, ties in program order (lfq, ltq, pbq, lhq, spq, ap)
+  POL_INVPRIO = 2,  // lowest priority first (ip)
+  POL_FIFO = 3,     // breadth first: in order of readiness (gd, global dequeue)
+  POL_LIFO = 4,     // depth first: most recently readied first (ll, local LIFO)
+  POL_RANDOM = 5    // uniformly random among ready tasks (rnd), seeded
+};
+
+inline std::vector<int64_t> list_schedule(int64_t n, const int64_t* pred_ptr, const int64_t* pred_idx,
+                                          const int32_t* prio, int policy, uint64_t seed) {
+  std::vector<int64_t> order;
+  order.reserve(static_cast<size_t>(n));
+  std::vector<int64_t> npred(static_cast<size_t>(n)), succ_ptr(static_cast<size_t>(n) + 1, 0);
+  for (int64_t t = 0; t < n; ++t) {
+    npred[t] = pred_ptr[t + 1] - pred_ptr[t];
+    for (int64_t e = pred_ptr[t]; e < pred_ptr[t + 1]; ++e) ++succ_ptr[pred_idx[e] + 1];
+  }
+  for (int64_t t = 0; t < n; ++t) succ_ptr[t + 1] += succ_ptr[t];
+  std::vector<int64_t> succ(static_cast<size_t>(succ_ptr[n])), fill(succ_ptr.begin(), succ_ptr.end() - 1);
+  for (int64_t t = 0; t < n; ++t)
+    for (int64_t e = pred_ptr[t]; e < pred_ptr[t + 1]; ++e) succ[fill[pred_idx[e]]++] = t;
+  // ready set: a max-heap on (key, -tid) -- the key encodes the policy
+  uint64_t rng = seed * 6364136223846793005ULL + 1442695040888963407ULL;
+  int64_t stamp = 0;
+  struct Item {
+    int64_t k1, k2, tid;
+    bool operator<(const Item& o) const {
+      if (k1 != o.k1) return k1 < o.k1;
+      if (k2 != o.k2) return k2 < o.k2;
+      return tid > o.tid;  // smaller tid wins ties
+    }
+  };
+  std::vector<Item> heap;
+  auto push = [&](int64_t t) {
+    Item it{0, 0, t};
+    switch (policy) {
+      case POL_PRIO: it.k1 = prio[t]; break;
+      case POL_INVPRIO: it.k1 = -static_cast<int64_t>(prio[t]); break;
+      case POL_FIFO: it.k1 = -(stamp++); break;
+      case POL_LIFO: it.k1 = stamp++; break;
+      case POL_RANDOM:
+        rng = rng * 6364136223846793005ULL + 1442695040888963407ULL;
+        it.k1 = static_cast<int64_t>(rng >> 17);
+        break;
+      default: it.k1 = -t; break;
+    }
+    heap.push_back(it);
+    std::push_heap(heap.begin(), heap.end());
+  };
+  for (int64_t t = 0; t < n; ++t)
+    if (npred[t] == 0) push(t);
+  while (!heap.empty()) {
+    std::pop_heap(heap.begin(), heap.end());
+    const int64_t t = heap.back().tid;
+    heap.pop_back();
+    order.push_back(t);
+    for (int64_t e = succ_ptr[t]; e < succ_ptr[t + 1]; ++e)
+      if (--npred[succ[e]] == 0) push(succ[e]);
+  }
+  return order;  // shorter than n only if the graph has a cycle
+}
+
 }  // namespace dpl_dag

@@ -93,6 +93,9 @@ class Context:
             t = torch.zeros(1, device=self.device)
             dist.all_reduce(t)
         self._queue = []
+        # ready-queue policy of single-process taskpools (the reference's -o scheduler choice)
+        self.scheduler = os.environ.get("DPLASMA_SCHEDULER", "") or None
+        self.sched_seed = 0
         self.profiling = None  # utils.trace.Tracer when enabled
         self.dot_file = os.environ.get("DPLASMA_DOT") or None  # DOT dump of every compiled tile DAG
         if os.environ.get("DPLASMA_PROFILE"):

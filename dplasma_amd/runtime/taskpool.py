@@ -12,6 +12,16 @@ management are done by the loop in ``_run_gpu_py`` (task bodies are Python
 callables that enqueue native kernels through ctypes); on CPU tasks simply
 run in order.
 
+Issue order: program order by default; a context scheduler policy
+(``ctx.scheduler``: the reference's ``-o`` choice -- lfq, ltq, ap, lhq, spq, pbq
+(priority first), ip (inverse priority), gd (FIFO), ll (LIFO), rnd) makes the
+native ready-queue list scheduler (``csrc/runtime/dag_core.h`` ``list_schedule``)
+pick the order in which ready tasks are enqueued, by their ``prio``.  Every
+order it produces is a topological order, so stream order plus the cross-stream
+events keep the dataflow intact.  Multi-process taskpools always issue in
+program order: their communication tasks must reach every rank in the same
+order.
+
 Timing protocol (reference ``tests/common.h:252-277``): building the
 taskpool is ENQ, ``run`` + ``complete`` is PROG, ``destruct`` is DEST.
 """
@@ -21,7 +31,19 @@ import time
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional, Sequence
 
+import numpy as np
 import torch
+
+# scheduler names (PaRSEC's -o) -> list_schedule policy codes
+SCHED_POLICY = {"": 0, "po": 0, "program": 0, "lfq": 1, "ltq": 1, "ap": 1, "lhq": 1, "spq": 1, "pbq": 1,
+                "ip": 2, "gd": 3, "ll": 4, "rnd": 5}
+
+
+def policy_code(name) -> int:
+    key = (name or "").strip().lower()
+    if key not in SCHED_POLICY:
+        raise ValueError(f"unknown scheduler {name!r} (known: {', '.join(sorted(k for k in SCHED_POLICY if k))})")
+    return SCHED_POLICY[key]
 
 
 @dataclass
@@ -80,10 +102,35 @@ class Taskpool:
             self._run_gpu_py(ctx)
         else:
             from ..utils import trace
-            for t in self.tasks:
+            for ti in self.issue_order(ctx):
+                t = self.tasks[ti]
                 with trace.span(ctx, t.name, "task", gpu=False):
                     t.fn()
         self._t_run = t0
+
+    def issue_order(self, ctx=None) -> List[int]:
+        """Task issue order under the context's scheduler policy (see module docstring)."""
+        ctx = ctx or self.ctx
+        n = len(self.tasks)
+        pol = policy_code(getattr(ctx, "scheduler", None)) if ctx is not None else 0
+        if pol == 0 or n < 2 or (ctx is not None and ctx.world > 1):
+            return list(range(n))
+        cache = self.__dict__.setdefault("_orders", {})
+        if pol in cache:
+            return cache[pol]
+        from .dag import _lib_rt
+        rt = _lib_rt()
+        if rt is None:
+            return list(range(n))
+        ptr = np.zeros(n + 1, dtype=np.int64)
+        for t in self.tasks:
+            ptr[t.tid + 1] = len(t.deps)
+        ptr = np.cumsum(ptr)
+        idx = np.array([d for t in self.tasks for d in t.deps], dtype=np.int64)
+        prio = np.array([t.prio for t in self.tasks], dtype=np.int32)
+        order = [int(x) for x in rt.dag_list_schedule(ptr, idx, prio, pol, int(getattr(ctx, "sched_seed", 0)))]
+        cache[pol] = order
+        return order
 
     def _run_gpu_py(self, ctx):
         from ..utils import trace
@@ -94,7 +141,8 @@ class Taskpool:
         for s in used:
             ctx.streams[s].wait_event(start)
         events = {}
-        for t in self.tasks:
+        for ti in self.issue_order(ctx):
+            t = self.tasks[ti]
             s = ctx.streams[t.stream]
             for d in t.deps:
                 if self.tasks[d].stream != t.stream:

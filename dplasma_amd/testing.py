@@ -69,8 +69,9 @@ def _parse(argv):
                     help="recursive sub-tile size hint (dplasma_z*_setrecursive)")
     ap.add_argument("-c", "--cores", type=int, default=0, help="host worker threads (CPU path)")
     ap.add_argument("-m", "--thread_multi", action="store_true", help="accepted for compatibility")
-    ap.add_argument("-o", "--scheduler", default="", help="accepted for compatibility (LFQ/LTQ/AP/LHQ/GD/PBQ/IP/RND): "
-                    "the stream-program executor has one schedule -- critical path on the high-priority stream")
+    ap.add_argument("-o", "--scheduler", default="", help="ready-queue policy of the task issue order "
+                    "(LFQ/LTQ/AP/LHQ/SPQ/PBQ: priority first, IP: inverse priority, GD: FIFO, LL: LIFO, RND: random; "
+                    "default: program order); multi-process runs issue in program order")
     return ap.parse_args(argv)
 
 
@@ -94,8 +95,12 @@ class Harness:
         if a.cores > 0:
             torch.set_num_threads(a.cores)
         self.ctx = dp.init(P=P, device=None if use_gpu else "cpu", nb_cores=a.cores or None)
-        if a.scheduler and a.verbose:
-            print(f"#+++++ scheduler {a.scheduler}: stream-program executor (fixed priority streams)", flush=True)
+        if a.scheduler:
+            from .runtime.taskpool import policy_code
+            policy_code(a.scheduler)   # unknown names fail here
+            self.ctx.scheduler = a.scheduler
+            if a.verbose:
+                print(f"#+++++ scheduler {a.scheduler}: native ready-queue issue order", flush=True)
         self.prec = a.op[0]
         if self.prec not in PRECS:
             raise SystemExit(f"operation must start with a precision letter s/d/c/z: {a.op}")

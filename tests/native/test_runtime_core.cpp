@@ -105,8 +105,34 @@ template <typename T> void test_band(int64_t n, int64_t b) {
   for (int64_t i = 0; i + 1 < n; ++i) CHECK(e1[i] == e4[i]);
 }
 
+// list scheduler: every policy gives a topological order of the Cholesky DAG's edges
+static void test_list_schedule() {
+  const int nt = 6;
+  std::vector<int64_t> ops;
+  std::vector<uint8_t> modes;
+  std::vector<int> kind;
+  chol_dag(nt, ops, modes, kind);
+  const int64_t n = (int64_t)kind.size(), R = 3;
+  const dpl_dag::Schedule S = dpl_dag::schedule(ops.data(), modes.data(), n, R);
+  std::vector<int64_t> ptr(n + 1, 0), idx(S.edst.size());
+  for (int64_t d : S.edst) ++ptr[d + 1];
+  for (int64_t t = 0; t < n; ++t) ptr[t + 1] += ptr[t];
+  std::vector<int64_t> fill(ptr.begin(), ptr.end() - 1);
+  for (size_t e = 0; e < S.esrc.size(); ++e) idx[fill[S.edst[e]]++] = S.esrc[e];
+  std::vector<int32_t> prio(n);
+  for (int64_t t = 0; t < n; ++t) prio[t] = S.blevel[t];
+  for (int pol = 0; pol < 6; ++pol) {
+    const std::vector<int64_t> order = dpl_dag::list_schedule(n, ptr.data(), idx.data(), prio.data(), pol, 7);
+    CHECK((int64_t)order.size() == n);
+    std::vector<int64_t> pos(n, -1);
+    for (int64_t i = 0; i < (int64_t)order.size(); ++i) pos[order[i]] = i;
+    for (size_t e = 0; e < S.esrc.size(); ++e) CHECK(pos[S.esrc[e]] < pos[S.edst[e]]);
+  }
+}
+
 int main() {
   test_dag();
+  test_list_schedule();
   test_band<double>(257, 8);
   test_band<std::complex<double>>(200, 5);
   // concurrent independent reductions (thread-safety of the core under TSan)
