@@ -344,7 +344,9 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
         base, ld = panels[c0].base, panels[c0].ld
         nxt = add_update(GemmBatch(), ks, range(n0, n1))
         rest = add_update(GemmBatch(), ks, range(n1, nt))
-        deps = [gate, last_panel]
+        # the previous block's bulk update touched every column beyond it: explicit WAW/RAW edge
+        # (stream order alone would hold it only under program-order issue, see runtime.taskpool)
+        deps = [gate, last_panel, last_upd.get(b - 1)]
         t_next = None
         if len(nxt):
             t_next = tp.task(f"NEXT({b})", upd_stream, lambda bt=nxt, bs=base, l=ld: f_upd(bt, bs, l), deps, prio=2)

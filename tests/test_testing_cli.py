@@ -29,6 +29,7 @@ def _run(args, nproc=1):
     # the remaining common.c flags: LAPACK storage (-A lld), cores, scheduler name, recursive hint, sync
     "dpotrf -N 300 -t 64 -A 320 -c 2 -o LFQ -z 32 -b -x", "dgemm -M 90 -N 70 -K 50 -t 16 -A 100 -B 60 -C 100 -x",
     # DTD drivers (testing_zpotrf_dtd, testing_zpotrf_dtd_untied, testing_zgemm_dtd)
+    "dpotrf -N 300 -t 32 -o LL -x", "dgetrf_1d -N 200 -t 32 -o RND -x", "dgeqrf -M 300 -N 200 -t 40 -i 8 -o IP -x",
     "dpotrf_dtd -N 200 -t 32 -x", "dpotrf_dtd_untied -N 200 -t 32 -x", "dgemm_dtd -M 90 -N 70 -K 50 -t 16 -x",
 ])
 def test_cli_single(args):
