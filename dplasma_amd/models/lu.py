@@ -132,7 +132,13 @@ class _GetrfDev:
     PANEL(k+1) needs only NEXT(k), so with look-ahead (DPLASMA_LU_LOOKAHEAD=1) the next panel
     factorisation overlaps REST(k) -- the reference's lookahead through priorities.  Panel buffers alternate with k's parity (REST(k) still reads panel k).
 
-    Why the panel travels whole: partial pivoting identical to one process needs, per column, a
+    Panel modes for P > 1 (``DPLASMA_LU_PANEL``): "gather" (default, below) or "percol" -- the
+    reference's distributed pivoting: each process row factors only its own panel rows, each
+    column's pivot comes from one all-gather of the P local candidates (|value|, row, candidate row,
+    current diagonal row: GETRF_MAX + RDC), the two rows of an interchange are replaced in place
+    (SND), and the trailing row moves travel only between the process rows involved.
+
+    Why the panel travels whole by default: partial pivoting identical to one process needs, per column, a
     max-reduction over the process column followed by the pivot row; done as collectives that is
     NB dependent RCCL calls per panel (512 x ~15 us = 7.7 ms at NB = 512) against ~1 ms to move a
     64k x 512 panel once over xGMI, so the panel is gathered once and factored redundantly by
@@ -202,8 +208,22 @@ class _GetrfDev:
                     maxrows = max(maxrows, sum(A.tile_rows(m) for m in range(k, A.mt) if g.prow(m + A.it0) == q))
             self.gmax = max(1, maxrows)
             self.gbuf = torch.zeros(g.P * self.gmax * nb, dtype=A.dtype, device=dev)
+        # P > 1 panel mode: "gather" (default) -- the panel's process column all-gathers the tall panel
+        # and every process row factors it redundantly (one collective per panel); "percol" -- the
+        # reference's distributed pivoting (zgetrf_ptgpanel.jdf GETRF_MAX / RDC / SND): each process
+        # row keeps its own panel rows, every column's pivot is chosen by one small all-gather of the
+        # local candidates (value, row, candidate row, current diagonal row) and only the two rows of
+        # an interchange move; O(NB (NB + P)) elements per panel instead of O(M NB / P)
+        self.panel_mode = os.environ.get("DPLASMA_LU_PANEL", "gather")
+        if self.panel_mode not in ("gather", "percol"):
+            raise ValueError(f"DPLASMA_LU_PANEL={self.panel_mode!r}: expected gather or percol")
+        self.percol = self.panel_mode == "percol" and g.P > 1
         self.plan = [self._build(k) for k in range(self.kt)]
-        self.bytes_panel = [0] * self.kt   # elements this rank sends per step (panel gather)
+        self.bytes_panel = [0] * self.kt   # elements this rank sends per step (panel exchange)
+        if self.percol:
+            mlmax = max([st.get("Ml", 0) for st in self.plan] + [1])
+            self.lpbuf = torch.zeros(mlmax * nb, dtype=A.dtype, device=dev)
+            self.xbuf = torch.zeros(g.P * (2 + 2 * nb), dtype=A.dtype, device=dev)
 
     def _build(self, k):
         A = self.A
@@ -242,6 +262,20 @@ class _GetrfDev:
                 st["gunpack"] = unpack.finalize()
                 st["gsent"] = sent
             st["plu"] = ops.PanelLU(st["pv"], mp, mp, kb, pivot=True)
+            if g.P > 1:
+                # percol mode: my panel rows, contiguous (ld = Ml), and their global row indices
+                lg, lu_ = TileBatch(), TileBatch()
+                grow, r = [], 0
+                mine = [m for m in range(k, A.mt) if A.row_is_local(m)]
+                Ml = sum(A.tile_rows(m) for m in mine)
+                for m in mine:
+                    lg.add(A.offset(m, k), A.tile_rows(m), kb, b_off=r)
+                    lu_.add(r, A.tile_rows(m), kb, b_off=(m - k) * mb)
+                    grow += list(range(m * mb, m * mb + A.tile_rows(m)))
+                    r += A.tile_rows(m)
+                st["Ml"] = Ml
+                st["lgather"], st["lunpack"] = lg.finalize(), lu_.finalize()
+                st["grow"] = grow
         trail = [n for n in range(k + 1, A.nt) if A.col_is_local(n)]
         st["trail"] = trail
         if trail and A.row_is_local(k):
@@ -286,7 +320,9 @@ class _GetrfDev:
         pc = g.pcol(k + A.jt0)
         pv = st["pv"][: mp * kb]
         # --- gather the panel in its process column (each process row sends only its own tiles)
-        if A.col_is_local(k):
+        if A.col_is_local(k) and self.percol:
+            self._panel_percol(k)
+        elif A.col_is_local(k):
             if g.P > 1:
                 gv = self.gbuf[: g.P * self.gmax * kb].view(g.P, self.gmax * kb)
                 if st["gpack"] is not None:
@@ -307,6 +343,66 @@ class _GetrfDev:
             par = k & 1
             ops.piv_moves(self.piv_dev, kmin, self.mdst[par], self.msrc[par], self.mcnt[par])
 
+    def _panel_percol(self, k):
+        """Distributed partial pivoting of panel k inside its process column (see panel_mode)."""
+        A, ctx = self.A, self.ctx
+        g = A.grid
+        st = self.plan[k]
+        kb, r0, kmin, Ml = st["kb"], st["r0"], st["kmin"], st["Ml"]
+        W = 2 + 2 * kb
+        lp = self.lpbuf
+        if Ml:
+            ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, lp, Ml, st["lgather"], copy=True)
+        L = torch.as_strided(lp, (Ml, kb), (1, max(Ml, 1)), 0)
+        grow = st["grow"]
+        where = {gr: i for i, gr in enumerate(grow)}
+        diag_owner = A.row_is_local(k)
+        diag_rank = g.prow(k + A.it0)
+        xb = self.xbuf[: g.P * W].view(g.P, W)
+        cplx = A.dtype.is_complex
+        crit = (lambda x: x.real.abs() + x.imag.abs()) if cplx else (lambda x: x.abs())  # noqa: E731 (i?amax)
+        piv = [0] * kmin
+        bad = 0
+        for j in range(kmin):
+            lo = j if diag_owner else 0          # rows still eligible: global index >= r0 + j
+            mine = xb[A.myrow]
+            mine.zero_()
+            mine[0] = -1.0
+            if Ml > lo:
+                c = crit(L[lo:, j])
+                i = int(torch.argmax(c).item())   # first maximum, as i?amax
+                mine[0] = c[i]
+                mine[1] = float(grow[lo + i])
+                mine[2:2 + kb] = L[lo + i, :]
+            if diag_owner:
+                mine[2 + kb:] = L[j, :]
+            comm.allgather_inplace(xb, A.myrow, ctx.col_group)
+            hv = xb[:, :2].real.cpu().tolist() if cplx else xb[:, :2].cpu().tolist()
+            best = max(range(g.P), key=lambda q: (hv[q][0], -hv[q][1]))
+            pg = int(hv[best][1])
+            u = xb[best, 2:2 + kb].clone()
+            piv[j] = pg - r0
+            if pg != r0 + j:
+                d = xb[diag_rank, 2 + kb:]
+                if pg in where:
+                    L[where[pg], :] = d
+                if diag_owner:
+                    L[j, :] = u
+            b0 = j + 1 if diag_owner else 0
+            if u[j] == 0:
+                bad = bad or (r0 + j + 1)
+                continue
+            if Ml > b0:
+                L[b0:, j] /= u[j]
+                if j + 1 < kb:
+                    L[b0:, j + 1:] -= torch.outer(L[b0:, j], u[j + 1:])
+        self.bytes_panel[k] = kmin * W
+        if bad and int(self.info.item()) == 0:
+            self.info.fill_(bad)
+        if Ml:
+            ops.geadd(0, N_, 1.0, lp, Ml, 0.0, st["pv"], st["mp"], st["lunpack"], copy=True)
+        self.piv_dev[:kmin] = torch.tensor(piv, dtype=torch.int32, device=self.piv_dev.device)
+
     def swap(self, k):
         A, ctx = self.A, self.ctx
         g = A.grid
@@ -314,7 +410,15 @@ class _GetrfDev:
         kb, r0, mp = st["kb"], st["r0"], st["mp"]
         pv = st["pv"][: mp * kb]
         # --- row interchanges on every local column (the panel column is rewritten below)
-        if self.tmp is not None:
+        if self.percol and self.tmp is not None:
+            # pivots are on the host in this mode: only the rows that cross process rows travel,
+            # between the two process rows involved (one all-to-all of exact sizes per column group)
+            piv = self.piv_dev[: st["kmin"]].cpu().numpy()
+            perm = _perm_from_swaps(piv, mp)
+            moved = np.nonzero(perm != np.arange(mp))[0]
+            if len(moved):
+                _permute_rows_2d(ctx, A, r0 + moved, r0 + perm[moved], self.lcols)
+        elif self.tmp is not None:
             par = k & 1
             mdst, msrc, mcnt = self.mdst[par], self.msrc[par], self.mcnt[par]
             ldb = 2 * A.nb

@@ -120,3 +120,55 @@ def test_getrf_ptgpanel_2x4():
         pc = k % 4
         sent = [out[r][3][k] for r in range(8) if out[r][4] == pc]
         assert sum(sent) == (N - k * NB) * NB, (k, sent)
+
+
+def _getrf_percol_w(rank, world, N, NB, P, prec):
+    import os
+    os.environ["DPLASMA_LU_PANEL"] = "percol"
+    return _getrf_prec_w(rank, world, N, NB, P, prec)
+
+
+def _getrf_prec_w(rank, world, N, NB, P, prec):
+    import dplasma_amd as dp
+    ctx = dp.init(device="cpu", P=P)
+    dt = dp.PREC_DTYPE[prec]
+    A = dp.block_cyclic(ctx, dt, NB, NB, N, N)
+    dp.plrnt(ctx, A, 3872)
+    IPIV = dp.ptgpanel_ipiv_descriptor(ctx, A)
+    tp = dp.getrf_ptgpanel_New(ctx, A, IPIV)
+    info = tp.execute(ctx)
+    from dplasma_amd.models.lu import _gather_ipiv
+    piv = _gather_ipiv(ctx, IPIV)
+    st = tp._state
+    return info, A.to_dense_local(), piv, list(st.bytes_panel), ctx.mycol, st.percol
+
+
+@pytest.mark.parametrize("world,P,prec", [(2, 2, "d"), (4, 2, "d"), (8, 2, "d"), (4, 4, "z"), (2, 1, "d")])
+def test_getrf_ptgpanel_percol(world, P, prec):
+    """Distributed pivoting (zgetrf_ptgpanel.jdf GETRF_MAX / RDC / SND): every process row keeps its
+    own panel rows and each column's pivot comes from one small all-gather of the local candidates.
+    Pivots are identical to one process and the per-panel traffic of a rank is O(NB (NB + P))
+    elements, independent of M (the gather mode sends M NB / P)."""
+    N, NB = 176, 16
+    out = run_distributed(_getrf_percol_w, world, N, NB, P, prec)
+    import dplasma_amd as dp
+    ctx = dp.Context(device="cpu")
+    A = dp.block_cyclic(ctx, dp.PREC_DTYPE[prec], NB, NB, N, N)
+    dp.plrnt(ctx, A, 3872)
+    IP = dp.ipiv_descriptor(ctx, A)
+    assert dp.getrf_1d(ctx, A, IP) == 0
+    from dplasma_amd.models.lu import _gather_ipiv
+    piv1 = _gather_ipiv(ctx, IP)
+    full = sum(out[r][1] for r in range(world))
+    for r in range(world):
+        assert out[r][0] == 0 and out[r][5] == (P > 1)
+        assert np.array_equal(out[r][2], piv1)
+    assert (full - A.to_dense_local()).abs().max() < 1e-10
+    if P > 1:
+        Q = world // P
+        nt = N // NB
+        for k in range(nt):
+            sent = [out[r][3][k] for r in range(world) if out[r][4] == k % Q]
+            assert max(sent) == NB * (2 + 2 * NB), (k, sent)          # per column: value, row, 2 rows
+            if N - k * NB > P * (2 * NB + 2):                        # tall panels: less than gathering
+                assert max(sent) < (N - k * NB) * NB // P
