@@ -56,6 +56,8 @@ POTRF_DEFER_MIN_TILES = 24 # below this many trailing tile-columns: plain look-a
 # 53.0 vs 56.7 TF/s -- its extra launches contend with the bulk update -- so "single" everywhere;
 # "auto" = blocked when distributed.
 POTRF_TILE = "single"
+POTRF_LOOKAHEAD = 1
+POTRF_TRSM = "rb"
 
 
 def _defer_depth(nt_left: int, D: int, min_tiles: int) -> int:
@@ -113,6 +115,18 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
         defer = int(os.environ.get("DPLASMA_POTRF_DEFER", POTRF_DEFER))
     D = max(1, int(defer))
     min_tiles = int(os.environ.get("DPLASMA_POTRF_DEFER_MIN_TILES", POTRF_DEFER_MIN_TILES))
+    # look-ahead depth: 1 -- NEXT(b) follows the whole bulk update REST(b-1) on the update stream;
+    # 2 -- REST(b) is split into NEXT2(b) (the columns of block b+2) and REST2(b) (beyond), NEXT(b)
+    # moves to the panel stream and needs only NEXT2(b-1): the bulk update gets two blocks of slack
+    la = int(os.environ.get("DPLASMA_POTRF_LOOKAHEAD", POTRF_LOOKAHEAD))
+    if la not in (1, 2):
+        raise ValueError("DPLASMA_POTRF_LOOKAHEAD must be 1 or 2")
+    nslab = 1 + la          # panel slabs in flight (distributed): block b+nslab reuses block b's
+    # panel TRSM: "rb" (register-resident strips on the tile kernel's inverted 32-blocks) or "gemm"
+    # (inverse of the diagonal tile + one MFMA GEMM launch: bulk-efficient beside the trailing GEMM)
+    trsm_kind = os.environ.get("DPLASMA_POTRF_TRSM", POTRF_TRSM)
+    if trsm_kind not in ("rb", "gemm"):
+        raise ValueError("DPLASMA_POTRF_TRSM must be rb or gemm")
     tile_kind = os.environ.get("DPLASMA_POTRF_TILE", POTRF_TILE)
     if tile_kind not in ("auto", "single", "blocked"):
         raise ValueError(f"DPLASMA_POTRF_TILE={tile_kind!r}: expected auto, single or blocked")
@@ -165,7 +179,7 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
             maxsub = max(maxsub, max(sub) if sub else 0)
         SG, SX = nlines * maxcnt * nbe, nlines * maxsub * nbe
         slab = SG + SX
-        GX = torch.zeros(2 * D * slab, dtype=A.dtype, device=dev)
+        GX = torch.zeros(nslab * D * slab, dtype=A.dtype, device=dev)
         dbuf = torch.zeros(nbe, dtype=A.dtype, device=dev)
         tp._buffers = (GX, dbuf)
 
@@ -198,9 +212,10 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
 
     gate = None        # task the next POTRF must follow (NEAR(k-1) or NEXT(b-1))
     last_upd = {}      # block -> last update-stream task reading its panels
+    nxt2_of, rest_of = {}, {}   # look-ahead 2: block -> NEXT2 / REST2 task (REST2: last bulk task)
     last_panel = None  # last panel-stream communication task
     for b, (c0, c1) in enumerate(blocks):
-        par = b % 2
+        par = b % nslab
         for k in range(c0, c1):
             kb = A.tile_rows(k)
             dk = tcoord(k, k)
@@ -241,7 +256,7 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                 else:
                     t_db = t_potrf
                     tri_base, tri_ld, tri_off = A.data, A.ld, A.offset(*dk)
-                if mine and use_rb:
+                if mine and use_rb and trsm_kind == "rb":
                     # row blocks of the panel tiles (lower: rows of L(i,k); upper: columns of U(k,i))
                     rbp = ops.RbPanel(uplo, [(A.offset(*tcoord(i, k)),
                                               A.tile_rows(i) if lower else A.tile_cols(i)) for i in mine], A.ld)
@@ -316,7 +331,7 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                         comm.allgather_inplace(Xk, my_line, line_group)
                 # GX slab (par) is reused by block b+2: its previous readers (NEXT/REST of b-2) must be done
                 t_panel = tp.task(f"PANEL_COMM({k})", pstream(k, "panel"), f_comm,
-                                  [t_trsm, gate, last_panel, last_upd.get(b - 2)], prio=2)
+                                  [t_trsm, gate, last_panel, last_upd.get(b - nslab)], prio=2)
                 last_panel = t_panel
 
                 def poff(i, o=o, idx_in_line=idx_in_line, idx_in_sub=idx_in_sub):
@@ -342,19 +357,45 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
         ks = list(range(c0, c1))
         n0, n1 = blocks[b + 1]
         base, ld = panels[c0].base, panels[c0].ld
+        if la == 1:
+            nxt = add_update(GemmBatch(), ks, range(n0, n1))
+            rest = add_update(GemmBatch(), ks, range(n1, nt))
+            # the previous block's bulk update touched every column beyond it: explicit WAW/RAW edge
+            # (stream order alone would hold it only under program-order issue, see runtime.taskpool)
+            deps = [gate, last_panel, last_upd.get(b - 1)]
+            t_next = None
+            if len(nxt):
+                t_next = tp.task(f"NEXT({b})", upd_stream, lambda bt=nxt, bs=base, l=ld: f_upd(bt, bs, l), deps,
+                                 prio=2)
+                last_upd[b] = t_next
+            if len(rest):
+                last_upd[b] = tp.task(f"REST({b})", upd_stream, lambda bt=rest, bs=base, l=ld: f_upd(bt, bs, l),
+                                      deps, prio=1)
+            # the next block's first POTRF follows NEXT(b) (and, for this rank, the block's NEARs)
+            gate = t_next if t_next is not None else gate
+            continue
+        n2 = blocks[b + 2][1] if b + 2 < len(blocks) else nt
         nxt = add_update(GemmBatch(), ks, range(n0, n1))
-        rest = add_update(GemmBatch(), ks, range(n1, nt))
-        # the previous block's bulk update touched every column beyond it: explicit WAW/RAW edge
-        # (stream order alone would hold it only under program-order issue, see runtime.taskpool)
-        deps = [gate, last_panel, last_upd.get(b - 1)]
+        nxt2 = add_update(GemmBatch(), ks, range(n1, n2))
+        rest = add_update(GemmBatch(), ks, range(n2, nt))
+        # NEXT(b): critical (panel stream); block b+1's columns were last updated by NEXT2(b-1) and,
+        # before that, by REST2(b-2) (ordered before NEXT2(b-1) on the update stream)
         t_next = None
         if len(nxt):
-            t_next = tp.task(f"NEXT({b})", upd_stream, lambda bt=nxt, bs=base, l=ld: f_upd(bt, bs, l), deps, prio=2)
-            last_upd[b] = t_next
+            t_next = tp.task(f"NEXT({b})", pstream(c1, "panel"), lambda bt=nxt, bs=base, l=ld: f_upd(bt, bs, l),
+                             [gate, last_panel, nxt2_of.get(b - 1), rest_of.get(b - 2)], prio=2)
+        # NEXT2(b) / REST2(b): bulk (update stream); block b+2's columns and beyond were last updated
+        # by REST2(b-1)
+        prev_bulk = rest_of.get(b - 1)
+        if len(nxt2):
+            nxt2_of[b] = tp.task(f"NEXT2({b})", upd_stream, lambda bt=nxt2, bs=base, l=ld: f_upd(bt, bs, l),
+                                 [gate, last_panel, prev_bulk], prio=1)
         if len(rest):
-            last_upd[b] = tp.task(f"REST({b})", upd_stream, lambda bt=rest, bs=base, l=ld: f_upd(bt, bs, l), deps,
-                                  prio=1)
-        # the next block's first POTRF follows NEXT(b) (and, for this rank, the block's NEARs)
+            rest_of[b] = tp.task(f"REST2({b})", upd_stream, lambda bt=rest, bs=base, l=ld: f_upd(bt, bs, l),
+                                 [gate, last_panel, prev_bulk, nxt2_of.get(b)], prio=0)
+        else:
+            rest_of[b] = nxt2_of.get(b, prev_bulk)
+        last_upd[b] = rest_of[b] if rest_of[b] is not None else t_next
         gate = t_next if t_next is not None else gate
 
     def _done():

@@ -40,9 +40,11 @@ def test_potrf_distributed(world, P, uplo):
 
 @pytest.mark.parametrize("world,P", [(2, 1), (4, 2)])
 @pytest.mark.parametrize("uplo", [122, 121])
-@pytest.mark.parametrize("defer", [2, 3])
-def test_potrf_distributed_deferred(world, P, uplo, defer, monkeypatch):
-    """Blocks of D panels with aggregated NEXT/REST updates (k = D*NB), on a ragged last tile."""
+@pytest.mark.parametrize("defer,la", [(2, 1), (3, 1), (2, 2), (1, 2)])
+def test_potrf_distributed_deferred(world, P, uplo, defer, la, monkeypatch):
+    """Blocks of D panels with aggregated NEXT/REST updates (k = D*NB), on a ragged last tile;
+    look-ahead 2 splits the bulk update (NEXT2 / REST2, three panel slabs in flight)."""
+    monkeypatch.setenv("DPLASMA_POTRF_LOOKAHEAD", str(la))
     monkeypatch.setenv("DPLASMA_POTRF_DEFER", str(defer))
     monkeypatch.setenv("DPLASMA_POTRF_DEFER_MIN_TILES", "3")
     N, NB = 150, 17
