@@ -46,6 +46,9 @@ constexpr int MAXB = 16;          // at most 16 row blocks (n <= 512)
 constexpr int BLK = RB * RB;      // doubles per block
 constexpr int PSTRIDE = 32;       // ints between flags (one 128-B line each)
 constexpr int NSLOT = 8;          // workspaces (concurrent launches on different streams)
+#ifndef RB_PRIO
+#define RB_PRIO 3                 // wave priority of the critical-path kernels (0..3)
+#endif
 
 struct RbWork {
   double* M;    // [MAXB][BLK]        M_k, column-major: inv(L(k,k)) = diag(S_k) M_k
@@ -128,6 +131,9 @@ __global__ __launch_bounds__(256) void k_potrf_rb(double* __restrict__ A, int n,
                                                   unsigned long long* __restrict__ trace) {
   __shared__ double Tb[BLK];  // C(i,k) fully updated: input of step k's TRSM; finally C(i,i)
   __shared__ double Xb[BLK];  // L(i,k) of the current step
+  // critical path: win the SIMD's issue arbitration against co-resident trailing-update GEMM waves
+  // (priority, then age -- MI355X_MICROARCH.md "Two waves per SIMD"); a scalar, wave-uniform op
+  __builtin_amdgcn_s_setprio(RB_PRIO);
   const int i = blockIdx.x;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int a = w >> 1, b = w & 1;                       // this wave's quadrant of off-diagonal blocks
@@ -413,6 +419,7 @@ template <bool LOWER, int NBLK>  // NBLK = ceil(n / 32): static, so the strip ne
 __global__ __launch_bounds__(64) void k_trsm_rb(const RbItem* __restrict__ items, int n,
                                                 const double* __restrict__ Lt, int ldl,
                                                 const double* __restrict__ zb, double* __restrict__ B, int ldb) {
+  __builtin_amdgcn_s_setprio(RB_PRIO);
   const RbItem it = items[blockIdx.x];
   const int l = threadIdx.x;
   const long long sib = LOWER ? 1 : ldb, sjb = LOWER ? ldb : 1;
@@ -495,6 +502,7 @@ __global__ __launch_bounds__(64) void k_trsm_rb(const RbItem* __restrict__ items
 template <bool LOWER>
 __global__ __launch_bounds__(64) void k_trsm_rb_prep(int n, const double* __restrict__ Lt, int ldl,
                                                      double* __restrict__ zb) {
+  __builtin_amdgcn_s_setprio(RB_PRIO);
   const int k = blockIdx.x, l = threadIdx.x;
   const long long sil = LOWER ? 1 : ldl, sjl = LOWER ? ldl : 1;
   const int j = l & 31;

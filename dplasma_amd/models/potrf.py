@@ -91,7 +91,12 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
     lower = uplo == dplasmaLower
     tp = Taskpool("potrf", ctx)
     # diagonal tiles on the CU-reserved stream when DPLASMA_DIAG_CUS is set (context._reserve_cus)
+    import os
     diag_stream = "diag" if "diag" in getattr(ctx, "streams", {}) else "panel"
+    # the panel TRSM joins the diagonal tile on the CU-reserved stream (DPLASMA_POTRF_DIAG_TRSM=0: on
+    # the shared panel stream): both are latency-bound chains that slow 7-28x beside GEMM waves
+    # (profiles/r2_potrf16k_timeline.txt)
+    trsm_stream = diag_stream if os.environ.get("DPLASMA_POTRF_DIAG_TRSM", "1") == "1" else "panel"
     upd_stream = "potrf_update" if "potrf_update" in getattr(ctx, "streams", {}) else "update"
     # PRI_CHANGE ({S,D,C,Z}POTRF env, reference zpotrf_wrapper.c:201-203): the last PRI_CHANGE
     # panels issue their critical-path tasks at normal priority (update stream) instead of the
@@ -110,7 +115,6 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
     distributed = ctx.world > 1
     P, Q = A.P, A.Q
     myrow, mycol = A.myrow, A.mycol
-    import os
     if defer is None:
         defer = int(os.environ.get("DPLASMA_POTRF_DEFER", POTRF_DEFER))
     D = max(1, int(defer))
@@ -268,7 +272,7 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                         if rec or not own:  # the diagonal tile came by broadcast: invert its 32-blocks here
                             ops.trsm_rb_prep(uplo, kb, tri_base, tri_off, tri_ld, zk)
                         ops.trsm_rb(uplo, kb, tri_base, tri_off, tri_ld, zk, rbp, A.data, A.ld)
-                    t_trsm = tp.task(f"TRSM({k})", pstream(k, "panel"), f_trsm, [t_db, gate], prio=2)
+                    t_trsm = tp.task(f"TRSM({k})", pstream(k, trsm_stream), f_trsm, [t_db, gate], prio=2)
                 elif mine:
                     tb = TileBatch()
                     for i in mine:
@@ -280,7 +284,7 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                     def f_trsm(tb=tb, tri_base=tri_base, tri_ld=tri_ld, side=side):
                         ops.trsm(side, uplo, dplasmaConjTrans, dplasmaNonUnit, 1.0, tri_base, tri_ld, A.data, A.ld,
                                  tb)
-                    t_trsm = tp.task(f"TRSM({k})", pstream(k, "panel"), f_trsm, [t_db, gate], prio=2)
+                    t_trsm = tp.task(f"TRSM({k})", pstream(k, trsm_stream), f_trsm, [t_db, gate], prio=2)
             if k == nt - 1:
                 break
             # ---------------- panel distribution
