@@ -126,15 +126,13 @@ __device__ inline int qoff(int h, int u, int l) { return ((h * 2 + (u >> 2)) * 4
   } while (0)
 
 template <bool LOWER>
-__global__ __launch_bounds__(256) void k_potrf_rb(double* __restrict__ A, int n, int lda, int* __restrict__ info,
-                                                  int info_base, RbWork ws, int epoch,
-                                                  unsigned long long* __restrict__ trace) {
+__device__ inline void rb_tile_body(double* __restrict__ A, int n, int lda, int* __restrict__ info, int info_base,
+                                    const RbWork& ws, int epoch, unsigned long long* __restrict__ trace, const int i) {
   __shared__ double Tb[BLK];  // C(i,k) fully updated: input of step k's TRSM; finally C(i,i)
   __shared__ double Xb[BLK];  // L(i,k) of the current step
   // critical path: win the SIMD's issue arbitration against co-resident trailing-update GEMM waves
   // (priority, then age -- MI355X_MICROARCH.md "Two waves per SIMD"); a scalar, wave-uniform op
   __builtin_amdgcn_s_setprio(RB_PRIO);
-  const int i = blockIdx.x;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int a = w >> 1, b = w & 1;                       // this wave's quadrant of off-diagonal blocks
   const int qa_d = (w == 0) ? 0 : 1, qb_d = (w == 2) ? 1 : 0;  // diagonal quadrant of waves 0..2
@@ -329,6 +327,13 @@ __global__ __launch_bounds__(256) void k_potrf_rb(double* __restrict__ A, int n,
   }
 }
 
+template <bool LOWER>
+__global__ __launch_bounds__(256) void k_potrf_rb(double* __restrict__ A, int n, int lda, int* __restrict__ info,
+                                                  int info_base, RbWork ws, int epoch,
+                                                  unsigned long long* __restrict__ trace) {
+  rb_tile_body<LOWER>(A, n, lda, info, info_base, ws, epoch, trace, blockIdx.x);
+}
+
 std::mutex g_mu;
 RbWork g_ws[64][NSLOT];
 bool g_have[64] = {};
@@ -394,6 +399,11 @@ DPL_API int dpl_potrf_tile_rbz(int uplo, int n, double* A, int lda, int* info, i
 DPL_API int dpl_potrf_tile_rb(int uplo, int n, double* A, int lda, int* info, int info_base, hipStream_t st) {
   return dpl_potrf_tile_rbz(uplo, n, A, lda, info, info_base, nullptr, st);
 }
+
+// Fused tile Cholesky + panel solve (k_potrf_trsm_rb): the tile at A, the panel strips in B
+// (device RbItem[nrb], offsets relative to B); zbuf (optional) receives (M, S) as in dpl_potrf_tile_rbz.
+DPL_API int dpl_potrf_trsm_rb(int uplo, int n, double* A, int lda, int* info, int info_base, double* zbuf, int nrb,
+                              const void* items, double* B, int ldb, hipStream_t st);
 
 // ================================================================== panel TRSM on the (M, S) blocks
 // B := B L^{-T} for every 16-row strip of the panel tiles below a diagonal tile factored by
@@ -497,6 +507,120 @@ __global__ __launch_bounds__(64) void k_trsm_rb(const RbItem* __restrict__ items
   }
 }
 
+// ================================================================== fused tile POTRF + panel TRSM
+// One launch: workgroups 0..NBLK-1 factor the diagonal tile exactly as k_potrf_rb; every further
+// workgroup solves four 16-row strips of the panel (one per wave) *along the factorisation
+// wavefront*: strip step k starts as soon as (M_k, S_k) and the blocks L(j,k), j > k, are published
+// (the same epoch-tagged flags the tile workgroups hand off with), reading them write-through from
+// the workspace.  The panel solve therefore overlaps the tile factorisation instead of following
+// it, and its workgroups are dispatched while the tile is still being factored -- beside a bulk
+// GEMM the separate TRSM launch waited ~1 ms for free slots (profiles/r2_potrf16k_timeline.txt).
+// Deadlock-free for the same reason as the tile kernel: a workgroup only ever waits on workgroups
+// with a smaller index (in-order dispatch); every spin is bounded.
+#ifndef TR_GRP_FUSED
+#define TR_GRP_FUSED 2  // fewer operand registers than k_trsm_rb: the fused kernel also holds the tile path
+#endif
+// one step k of a strip (compile-time k: the register arrays are indexed statically, and the
+// bounded flag spin cannot keep the compiler from unrolling the step sequence)
+template <bool LOWER, int NBLK, int K>
+__device__ __forceinline__ void rb_strip_step(d4_t (&C)[NBLK][2], const RbWork& ws, int base, int* __restrict__ info,
+                                              double* __restrict__ Bb, long long sib, long long sjb, bool rok,
+                                              int row, int n, int l) {
+  if constexpr (K < NBLK) {
+    // (M_K, S_K) and every L(j,K), j > K, published
+    if (l == 0) {
+#pragma nounroll
+      for (int j = K; j < NBLK; ++j) spin_until(ws.prog + j * PSTRIDE, base + K + 1, info);
+    }
+    __builtin_amdgcn_wave_barrier();
+    double mc[20];
+    const double* Mk = ws.M + (size_t)K * BLK;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) mc[u] = ld_sc1(Mk + (4 * u + (l >> 4)) * RB + (l & 15));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) mc[4 + u] = ld_sc1(Mk + (4 * u + (l >> 4)) * RB + 16 + (l & 15));
+#pragma unroll
+    for (int q = 0; q < 8; ++q) mc[12 + q] = ld_sc1(ws.S + (size_t)K * RB + 16 * (q >> 2) + (l >> 4) + 4 * (q & 3));
+    // L(R,K) = C(R,K) M_K^T diag(S_K)
+    double x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = C[K][u >> 2][u & 3];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      d4_t acc = {0, 0, 0, 0};
+      if (h == 0) acc = mfma_chunks<4>(mc, x, acc);
+      else acc = mfma_chunks<8>(mc + 4, x, acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = 16 * h + (l >> 4) + 4 * r;
+        acc[r] *= mc[12 + 4 * h + r];
+        if (rok && RB * K + c < n) Bb[row * sib + (RB * K + c) * sjb] = acc[r];  // final L(R,K)
+      }
+      C[K][h] = acc;
+    }
+    double xm[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xm[u] = -C[K][u >> 2][u & 3];
+    // C(R,j) -= L(R,K) L(j,K)^T: L(j,K) from the workspace (T-layout, both row halves)
+#pragma unroll
+    for (int j0 = K + 1; j0 < NBLK; j0 += TR_GRP_FUSED) {
+      double y[TR_GRP_FUSED][16];
+#pragma unroll
+      for (int g = 0; g < TR_GRP_FUSED; ++g)
+        if (j0 + g < NBLK) {
+          const double* Yp = ws.Lp + ((size_t)(j0 + g) * MAXB + K) * BLK;
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) y[g][8 * h + u] = ld_sc1(Yp + qoff(h, u, l));
+        }
+#pragma unroll
+      for (int g = 0; g < TR_GRP_FUSED; ++g)
+        if (j0 + g < NBLK) {
+          C[j0 + g][0] = mfma_chunks<8>(y[g], xm, C[j0 + g][0]);
+          C[j0 + g][1] = mfma_chunks<8>(y[g] + 8, xm, C[j0 + g][1]);
+        }
+    }
+    rb_strip_step<LOWER, NBLK, K + 1>(C, ws, base, info, Bb, sib, sjb, rok, row, n, l);
+  }
+}
+
+template <bool LOWER, int NBLK>
+__device__ inline void rb_strip_dataflow(const RbItem it, int n, const RbWork& ws, int base, int* __restrict__ info,
+                                         double* __restrict__ B, int ldb) {
+  const int l = threadIdx.x & 63;
+  const long long sib = LOWER ? 1 : ldb, sjb = LOWER ? ldb : 1;
+  const int row = l & 15;
+  const bool rok = row < it.rows;
+  double* Bb = B + it.b_off;
+  d4_t C[NBLK][2];
+#pragma unroll
+  for (int jb = 0; jb < NBLK; ++jb)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = RB * jb + 16 * h + (l >> 4) + 4 * r;
+        C[jb][h][r] = (rok && col < n) ? Bb[row * sib + col * sjb] : 0.0;
+      }
+  rb_strip_step<LOWER, NBLK, 0>(C, ws, base, info, Bb, sib, sjb, rok, row, n, l);
+}
+
+template <bool LOWER, int NBLK>
+__global__ __launch_bounds__(256) void k_potrf_trsm_rb(double* __restrict__ A, int n, int lda, int* __restrict__ info,
+                                                       int info_base, RbWork ws, int epoch,
+                                                       const RbItem* __restrict__ items, int nrb,
+                                                       double* __restrict__ B, int ldb) {
+  if (blockIdx.x < NBLK) {
+    rb_tile_body<LOWER>(A, n, lda, info, info_base, ws, epoch, nullptr, blockIdx.x);
+    return;
+  }
+  __builtin_amdgcn_s_setprio(RB_PRIO);
+  const int strip = (blockIdx.x - NBLK) * 4 + (threadIdx.x >> 6);
+  if (strip >= nrb) return;
+  rb_strip_dataflow<LOWER, NBLK>(items[strip], n, ws, epoch * 64, info, B, ldb);
+}
+
 // (M_k, S_k) of every 32x32 diagonal block of a factored tile L (for ranks that received L):
 // row elimination of L_kk applied to I (M L_kk = diag(L_kk)), so inv(L_kk) = diag(1 / L_kk(p,p)) M.
 template <bool LOWER>
@@ -573,5 +697,41 @@ DPL_API int dpl_trsm_rb(int uplo, int n, const double* L, int ldl, const double*
     default: return -3;
   }
 #undef TRSM_RB_CASE
+  return (int)hipGetLastError();
+}
+
+DPL_API int dpl_potrf_trsm_rb(int uplo, int n, double* A, int lda, int* info, int info_base, double* zbuf, int nrb,
+                              const void* items, double* B, int ldb, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (n > RB * MAXB) return -3;
+  if (nrb <= 0) return dpl_potrf_tile_rbz(uplo, n, A, lda, info, info_base, zbuf, st);
+  RbWork ws;
+  int epoch = 0;
+  const int rc = get_ws(&ws, &epoch, st);
+  if (rc) return rc;
+  if (zbuf) {
+    ws.M = zbuf;
+    ws.S = zbuf + MAXB * BLK;
+  }
+  const int nblk = cdiv(n, RB);
+  const dim3 grid(nblk + cdiv(nrb, 4));
+  const RbItem* it = (const RbItem*)items;
+#define POTRF_TRSM_CASE(NB_)                                                                              \
+  case NB_:                                                                                               \
+    if (uplo == DPL_LOWER)                                                                                \
+      hipLaunchKernelGGL((k_potrf_trsm_rb<true, NB_>), grid, dim3(256), 0, st, A, n, lda, info, info_base, ws, \
+                         epoch, it, nrb, B, ldb);                                                         \
+    else                                                                                                  \
+      hipLaunchKernelGGL((k_potrf_trsm_rb<false, NB_>), grid, dim3(256), 0, st, A, n, lda, info, info_base, ws, \
+                         epoch, it, nrb, B, ldb);                                                         \
+    break;
+  switch (nblk) {
+    POTRF_TRSM_CASE(1) POTRF_TRSM_CASE(2) POTRF_TRSM_CASE(3) POTRF_TRSM_CASE(4) POTRF_TRSM_CASE(5)
+    POTRF_TRSM_CASE(6) POTRF_TRSM_CASE(7) POTRF_TRSM_CASE(8) POTRF_TRSM_CASE(9) POTRF_TRSM_CASE(10)
+    POTRF_TRSM_CASE(11) POTRF_TRSM_CASE(12) POTRF_TRSM_CASE(13) POTRF_TRSM_CASE(14) POTRF_TRSM_CASE(15)
+    POTRF_TRSM_CASE(16)
+    default: return -3;
+  }
+#undef POTRF_TRSM_CASE
   return (int)hipGetLastError();
 }

@@ -57,7 +57,7 @@ POTRF_DEFER_MIN_TILES = 24 # below this many trailing tile-columns: plain look-a
 # "auto" = blocked when distributed.
 POTRF_TILE = "single"
 POTRF_LOOKAHEAD = 1
-POTRF_TRSM = "rb"
+POTRF_TRSM = "rb"   # "fused": the diagonal owner factors its tile and solves its panel strips in one launch
 
 
 def _defer_depth(nt_left: int, D: int, min_tiles: int) -> int:
@@ -129,8 +129,8 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
     # panel TRSM: "rb" (register-resident strips on the tile kernel's inverted 32-blocks) or "gemm"
     # (inverse of the diagonal tile + one MFMA GEMM launch: bulk-efficient beside the trailing GEMM)
     trsm_kind = os.environ.get("DPLASMA_POTRF_TRSM", POTRF_TRSM)
-    if trsm_kind not in ("rb", "gemm"):
-        raise ValueError("DPLASMA_POTRF_TRSM must be rb or gemm")
+    if trsm_kind not in ("rb", "gemm", "fused"):
+        raise ValueError("DPLASMA_POTRF_TRSM must be rb, fused or gemm")
     tile_kind = os.environ.get("DPLASMA_POTRF_TILE", POTRF_TILE)
     if tile_kind not in ("auto", "single", "blocked"):
         raise ValueError(f"DPLASMA_POTRF_TILE={tile_kind!r}: expected auto, single or blocked")
@@ -230,10 +230,24 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
             if own_diag:
                 off = A.offset(*dk)
 
-                def f_potrf(off=off, kb=kb, k=k, dk=dk):
+                fused_rbp = None
+                if use_rb and trsm_kind == "fused" and in_panel_cross:
+                    mine_k = [i for i in range(k + 1, nt) if owner_of_panel_line(i) == my_line]
+                    if mine_k:
+                        fused_rbp = ops.RbPanel(uplo, [(A.offset(*tcoord(i, k)), A.tile_rows(i) if lower
+                                                        else A.tile_cols(i)) for i in mine_k], A.ld)
+
+                def f_potrf(off=off, kb=kb, k=k, dk=dk, frbp=fused_rbp):
                     hnb = getattr(tp, "recursive_nb", 0)
                     if hnb and hnb < kb:
                         _recursive_potrf(tp, ctx, uplo, A, dk, hnb, info, k * A.mb)
+                        if frbp is not None:   # the sub-taskpool left no zbuf: solve the panel apart
+                            zk = zbufs[(k % 2) * zsz:(k % 2 + 1) * zsz]
+                            ops.trsm_rb_prep(uplo, kb, A.data, off, A.ld, zk)
+                            ops.trsm_rb(uplo, kb, A.data, off, A.ld, zk, frbp, A.data, A.ld)
+                    elif frbp is not None:
+                        ops.potrf_trsm_rb(uplo, kb, A.data, off, A.ld, info, k * A.mb,
+                                          zbufs[(k % 2) * zsz:(k % 2 + 1) * zsz], frbp, A.data, A.ld)
                     elif use_rb:
                         ops.potrf_tile(uplo, A.data, off, kb, A.ld, info, k * A.mb,
                                        zbuf=zbufs[(k % 2) * zsz:(k % 2 + 1) * zsz])
@@ -260,7 +274,9 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                 else:
                     t_db = t_potrf
                     tri_base, tri_ld, tri_off = A.data, A.ld, A.offset(*dk)
-                if mine and use_rb and trsm_kind == "rb":
+                if mine and own_diag and use_rb and trsm_kind == "fused":
+                    t_trsm = t_potrf          # solved by the fused POTRF launch
+                elif mine and use_rb and trsm_kind in ("rb", "fused"):
                     # row blocks of the panel tiles (lower: rows of L(i,k); upper: columns of U(k,i))
                     rbp = ops.RbPanel(uplo, [(A.offset(*tcoord(i, k)),
                                               A.tile_rows(i) if lower else A.tile_cols(i)) for i in mine], A.ld)

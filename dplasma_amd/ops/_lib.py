@@ -73,6 +73,8 @@ _SIGS = {
     "dpl_potrf_rb_set_trace": [c_vp],
     # dataflow tile POTRF + panel TRSM (potrf_rb.hip): uplo, n, A, lda, info*, info_base, zbuf, stream
     "dpl_potrf_tile_rbz": [c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_vp],
+    # uplo, n, A, lda, info, info_base, zbuf, nrb, items, B, ldb, stream: fused tile POTRF + panel TRSM
+    "dpl_potrf_trsm_rb": [c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp],
     "dpl_potrf_zbuf_size": [],
     "dpl_trsm_rb_prep": [c_int, c_int, c_vp, c_int, c_vp, c_vp],                    # uplo, n, L, ldl, zbuf, stream
     "dpl_trsm_rb": [c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp],  # + nrb, items, B, ldb      # debug: per-workgroup phase timestamps of the dataflow kernel    # 0 = dataflow multi-WG (fp64, n <= 512), 1 = single-WG kernel   # tile POTRF phase ablation (tools/gpu/potrf_tile_phases.py)

@@ -228,6 +228,17 @@ class RbPanel:
         return t
 
 
+def potrf_trsm_rb(uplo: int, n: int, A: torch.Tensor, off: int, lda: int, info: torch.Tensor, info_base: int,
+                  zbuf: torch.Tensor, panel: "RbPanel", B: torch.Tensor, ldb: int):
+    """Fused diagonal-tile Cholesky + panel solve (k_potrf_trsm_rb): the tile at A[off] is factored
+    and the strips of ``panel`` (in B) are solved along the factorisation wavefront in ONE launch."""
+    assert rb_ok(A, n) and zbuf.dtype == torch.float64 and zbuf.numel() >= rb_zbuf_size()
+    rc = _lib.load().dpl_potrf_trsm_rb(uplo, n, A.data_ptr() + 8 * int(off), lda, info.data_ptr(), int(info_base),
+                                       zbuf.data_ptr(), len(panel), panel.device(B.device).data_ptr() if len(panel)
+                                       else None, B.data_ptr(), ldb, _lib.stream_ptr())
+    _lib.check(rc, "potrf_trsm_rb")
+
+
 def trsm_rb_prep(uplo: int, n: int, L: torch.Tensor, l_off: int, ldl: int, zbuf: torch.Tensor):
     """Inverted diagonal 32-blocks of an already factored tile (ranks that received it)."""
     rc = _lib.load().dpl_trsm_rb_prep(uplo, n, L.data_ptr() + 8 * int(l_off), ldl, zbuf.data_ptr(),

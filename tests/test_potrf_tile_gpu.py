@@ -114,7 +114,7 @@ def test_potrf_tile_under_load():
 
 @pytest.mark.parametrize("uplo", [dplasmaLower, dplasmaUpper])
 @pytest.mark.parametrize("n", [512, 100, 32])
-@pytest.mark.parametrize("prep", [False, True])
+@pytest.mark.parametrize("prep", [False, True, "fused"])
 def test_trsm_rb_panel(uplo, n, prep):
     """Panel solve of the Cholesky step (k_trsm_rb) against torch.linalg.solve_triangular, with the
     inverted diagonal blocks from the tile factorisation itself or from k_trsm_rb_prep."""
@@ -142,17 +142,44 @@ def test_trsm_rb_panel(uplo, n, prep):
             offs.append(c0 * ld); tiles.append((c0 * ld, m)); c0 += m
     info = torch.zeros(1, dtype=torch.int32, device="cuda")
     zbuf = torch.zeros(ops.rb_zbuf_size(), dtype=torch.float64, device="cuda")
-    ops.potrf_tile(uplo, buf, 0, n, ld, info, 0, zbuf=zbuf)
-    if prep:
-        zbuf.fill_(float("nan"))
-        ops.trsm_rb_prep(uplo, n, buf, 0, ld, zbuf)
     panel = ops.RbPanel(uplo, tiles, ld)
-    ops.trsm_rb(uplo, n, buf, 0, ld, zbuf, panel, buf, ld)
+    if prep == "fused":   # one launch: tile factorisation + panel strips along its wavefront
+        ops.potrf_trsm_rb(uplo, n, buf, 0, ld, info, 0, zbuf, panel, buf, ld)
+    else:
+        ops.potrf_tile(uplo, buf, 0, n, ld, info, 0, zbuf=zbuf)
+        if prep:
+            zbuf.fill_(float("nan"))
+            ops.trsm_rb_prep(uplo, n, buf, 0, ld, zbuf)
+        ops.trsm_rb(uplo, n, buf, 0, ld, zbuf, panel, buf, ld)
     torch.cuda.synchronize()
     assert int(info.item()) == 0
     L = torch.linalg.cholesky(S)
+    tri = view(0, n, n).tril() if uplo == dplasmaLower else view(0, n, n).triu().T
+    assert (tri - L).abs().max().item() < 1e-12 * max(1.0, L.abs().max().item())
     for B, m, off in zip(Bs, ms, offs):
         ref = torch.linalg.solve_triangular(L, B.T, upper=False).T  # B L^{-T}
         got = view(off, m, n) if uplo == dplasmaLower else view(off, n, m).T
         err = (got - ref).abs().max().item() / max(1.0, ref.abs().max().item())
         assert err < 1e-12, (m, err)
+
+
+@pytest.mark.parametrize("uplo", [dplasmaLower, dplasmaUpper])
+@pytest.mark.parametrize("N,NB", [(4096, 512), (3000, 384), (2048, 256)])
+def test_potrf_fused_trsm(uplo, N, NB, monkeypatch):
+    """Whole DPOTRF with the fused tile + panel-solve launch (DPLASMA_POTRF_TRSM=fused) passes the
+    reference check (src/dplasma_zcheck.c check_zpotrf) and matches the default two-launch path."""
+    import dplasma_amd as dp
+    ctx = dp.init(device="cuda:0")
+    out = {}
+    for kind in ("rb", "fused"):
+        monkeypatch.setenv("DPLASMA_POTRF_TRSM", kind)
+        A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+        dp.dplghe(ctx, float(N), uplo, A, 3872)
+        A0 = A.like()
+        dp.lacpy(ctx, dp.dplasmaUpperLower, A, A0)
+        assert dp.dpotrf(ctx, uplo, A) == 0
+        ok, res = dp.check_potrf(ctx, uplo, A, A0)
+        assert ok, (kind, res)
+        out[kind] = A.to_dense_local()
+    tri = (lambda x: x.tril()) if uplo == dplasmaLower else (lambda x: x.triu())
+    assert (tri(out["rb"]) - tri(out["fused"])).abs().max().item() < 1e-10
