@@ -215,25 +215,203 @@ class QRTree:
         return f"QRTree({self.name}, mt={self.mt}, nt={self.nt}, a={self.a}, p={self.p})"
 
 
+def _lowbit_piv(d: int) -> int:
+    """Binary tree over offsets: offset d > 0 is killed by d minus its lowest set bit."""
+    return d - (d & -d)
+
+
+def _fib_piv(d: int) -> int:
+    """Fibonacci (order 1) tree over offsets: groups of 1, 2, 3, ... consecutive offsets, each
+    offset killed by the one ``group size`` above it (dplasma_hqr.c fibonacci ipiv, first column)."""
+    f, start = 1, 1
+    while d >= start + f:
+        start += f
+        f += 1
+    return d - f
+
+
+def _greedy_low_table(ldd: int, min_mn: int, p: int, a: int):
+    """Pivot domain index of domain j at panel k for process row r, tab[r][k][j], of the reference's
+    coarse-grained greedy low-level tree (dplasma_hqr.c hqr_low_greedy_init, non-domino): per panel
+    column, half of the domains still to be annihilated are killed by the ones just above them,
+    columns advancing as soon as their predecessor has produced enough triangles.  Re-implemented
+    here because identical elimination trees are the point (the tree defines the V/T layout)."""
+    pa = p * a
+    tab = [[[0] * ldd for _ in range(min_mn)] for _ in range(p)]
+    for r in range(p):
+        todo = []
+        for k in range(min_mn):
+            v = max(ldd - (k + p - 1 - r) // pa, 0)
+            if v == 0:
+                break
+            todo.append(v)
+        lmin = len(todo)
+        if lmin == 0:
+            continue
+        nt_ = [0] * lmin
+        nz = [0] * lmin
+        nt_[0] = ldd
+        k = first = 0
+        guard = 0
+        while not (nt_[lmin - 1] == todo[lmin - 1] and nz[lmin - 1] + 1 == nt_[lmin - 1]) and first < lmin:
+            guard += 1
+            if guard > 10 * (ldd + 2) * (lmin + 2):
+                raise RuntimeError("greedy tree schedule did not converge")
+            h = (nt_[k] - nz[k]) // 2
+            if h == 0:
+                while first < lmin and nt_[first] == todo[first] and nz[first] + 1 == nt_[first]:
+                    if first < lmin - 1 and first % pa != (a - 1) * p + r:
+                        nt_[first + 1] += 1
+                    first += 1
+                k = first
+                continue
+            if k < lmin - 1:
+                nt_[k + 1] += h
+            top = ldd - nz[k] - 1
+            for j in range(top, top - h, -1):
+                tab[r][k][j] = j - h
+            nz[k] += h
+            k += 1
+            if k > lmin - 1:
+                k = first
+    return tab
+
+
+def _greedy_high_table(mt: int, min_mn: int, p: int):
+    """tab[k][d]: pivot row of band row k+d at panel k of the reference's greedy high-level tree
+    (dplasma_hqr.c hqr_high_greedy_init)."""
+    tab = [[0] * p for _ in range(min_mn)]
+    nt_ = [0] * min_mn
+    nz = [0] * min_mn
+    nt_[0] = mt
+    nz[0] = max(mt - p, 0)
+    for k in range(1, min_mn):
+        nt_[k] = nz[k] = max(mt - k - p, 0)
+    k = first = 0
+    guard = 0
+    while not (nt_[min_mn - 1] == mt - (min_mn - 1) and nz[min_mn - 1] + 1 == nt_[min_mn - 1]) and first < min_mn:
+        guard += 1
+        if guard > 10 * (mt + 2) * (min_mn + 2):
+            raise RuntimeError("greedy tree schedule did not converge")
+        h = (nt_[k] - nz[k]) // 2
+        if h == 0:
+            while first < min_mn and nt_[first] == mt - first and nz[first] + 1 == nt_[first]:
+                first += 1
+            k = first
+            continue
+        top = mt - nz[k] - 1
+        nz[k] += h
+        if k < min_mn - 1:
+            nt_[k + 1] = nz[k]
+        for j in range(top, top - h, -1):
+            tab[k][j - k] = j - h
+        k += 1
+        if k > min_mn - 1:
+            k = first
+    return tab
+
+
 class HQRTree(QRTree):
     """Hierarchical tree (dplasma_hqr_init, src/dplasma_hqr.c:1670-1948).
 
-    Rows of panel k are grouped by "process row" ``m % p``; inside a process
-    row, consecutive local rows form TS domains of ``a`` tiles (flat TS tree,
-    no communication); the domain heads are reduced by the low-level tree
-    ``llvl`` (local TT kernels); the process-row survivors are reduced by the
-    high-level tree ``hlvl`` (distributed TT kernels, one tile-row exchange per
-    elimination).  ``domino``: the high level is a flat TT chain (type 2),
-    which pipelines consecutive panels; ``tsrr``: TS domains are formed
-    round-robin over the local rows instead of contiguously."""
+    Rows of panel k are grouped by "process row" ``m % p``.  Reference semantics (gettype /
+    currpiv, dplasma_hqr.c:299-322, 1241-1311), reproduced exactly for the non-domino, non-tsrr trees:
+    the p rows [k, k+p) are the distributed (type 3) rows, reduced by the high-level tree ``hlvl``;
+    below them, TS domains are the GLOBALLY aligned groups of ``a`` consecutive local rows
+    ((m / p) / a is the domain index), each killed by its first row (type 1) -- except the domain
+    containing the diagonal macro-tile, whose rows the type-3 row of their process row kills; the
+    domain heads of a process row are reduced by the low-level tree ``llvl`` over domain indices
+    (flat, binary, fibonacci and greedy as the reference defines them; greedy1p uses the per-panel
+    greedy shape).  ``domino``: the high level is a flat TT chain (type 2) pipelining consecutive
+    panels; ``tsrr``: TS domains formed round-robin over the local rows (both per-panel shapes)."""
 
     def __init__(self, mt, nt, llvl=GREEDY_TREE, hlvl=FLAT_TREE, a=1, p=1, domino=False, tsrr=False):
         self.llvl, self.hlvl, self.domino, self.tsrr = llvl, hlvl, bool(domino), bool(tsrr)
         a = max(1, min(a, mt)) if a > 0 else 1
         p = max(1, p)
+        self._min_mn = min(mt, nt)
+        self._ldd = -(-mt // (p * a))
+        self._glow = _greedy_low_table(self._ldd, self._min_mn, p, a) if llvl == GREEDY_TREE else None
+        self._ghigh = _greedy_high_table(mt, self._min_mn, p) if hlvl == GREEDY_TREE and p > 1 else None
         super().__init__(mt, nt, a, p, "hqr")
 
     def _plan(self, k):
+        if self.domino or self.tsrr:
+            return self._plan_local(k)
+        return self._plan_aligned(k)
+
+    def _low_piv(self, k, r, j, k_a):
+        """Pivot domain index of domain j (> k_a) of process row r at panel k."""
+        t = self.llvl
+        if t == FLAT_TREE:
+            return k_a
+        if t == BINARY_TREE:
+            return k_a + _lowbit_piv(j - k_a)
+        if t == FIBONACCI_TREE:
+            return k_a + _fib_piv(j - k_a)
+        if t == GREEDY_TREE:
+            return self._glow[r][k][j]
+        return None   # greedy1p: per-panel shape
+
+    def _high_piv(self, k, m):
+        t, d = self.hlvl, m - k
+        if t == FLAT_TREE:
+            return k
+        if t == BINARY_TREE:
+            return k + _lowbit_piv(d)
+        if t == FIBONACCI_TREE:
+            return k + _fib_piv(d)
+        if t == GREEDY_TREE:
+            return self._ghigh[k][d]
+        return None
+
+    def _plan_aligned(self, k):
+        a, p, mt = self.a, self.p, self.mt
+        pa = p * a
+        tmpk = k // pa
+        band = [m for m in range(k, min(mt, k + p))]          # type 3 rows, one per process row
+        t_of = {m % p: m for m in band}
+        heads, ts, low, high = list(band), [], [], []
+        by_res = {r: [] for r in t_of}                        # aligned heads (type 1) per process row
+        for m in range(k + p, mt):
+            r, li = m % p, m // p
+            if li % a == 0:
+                heads.append(m)
+                by_res[r].append(m)
+            else:
+                idx = li // a
+                ts.append((t_of[r] if idx == tmpk else idx * pa + r, m, KILLED_BY_TS))
+        for r, hs in by_res.items():
+            if not hs:
+                continue
+            k_a = (k + p - 1 - r) // p // a
+            doms = [t_of[r]] + hs
+            idx_of = {m: (k_a if m == t_of[r] else m // pa) for m in doms}
+            row_of = {idx_of[m]: m for m in doms}
+            pairs = []
+            for m in sorted(hs, reverse=True):
+                j = idx_of[m]
+                pj = self._low_piv(k, r, j, k_a)
+                if pj is None:
+                    pairs = None
+                    break
+                pairs.append((row_of.get(pj, t_of[r]), m))
+            if pairs is None:
+                pairs = tree_pairs(doms, self.llvl)
+            low += [(pv, m, KILLED_BY_LOCALTREE) for (pv, m) in pairs]
+        hp = []
+        for m in sorted(band[1:], reverse=True):
+            pv = self._high_piv(k, m)
+            if pv is None:
+                hp = None
+                break
+            hp.append((pv, m))
+        if hp is None:
+            hp = tree_pairs(band, self.hlvl)
+        high = [(pv, m, KILLED_BY_DISTTREE) for (pv, m) in hp]
+        return heads, ts + low + high
+
+    def _plan_local(self, k):
         a, p = self.a, self.p
         heads, kills = [], []
         roots = []
