@@ -53,7 +53,7 @@ def gemm_New(ctx, transA, transB, alpha, A, B, beta, C, c_mask=None, kc=None, na
     streaming variant (models/gemm_ooc.py), like dplasma_zgemm_New_ex picks the
     GPU variant when the active set exceeds GPU memory (src/zgemm_wrapper.c:455-486)."""
     K = _check(transA, transB, A, B, C)
-    if (ctx.is_gpu and ctx.world == 1 and c_mask is None and C.device.type == "cpu"
+    if (ctx.is_gpu and c_mask is None and C.device.type == "cpu"
             and A.device.type == "cpu" and B.device.type == "cpu"):
         from .gemm_ooc import gemm_gpu_New
         return gemm_gpu_New(ctx, transA, transB, alpha, A, B, beta, C)

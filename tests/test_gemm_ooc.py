@@ -54,3 +54,40 @@ def test_gpu_gemm_dispatches_host_operands():
     assert tp.name == "gemm_gpu"
     tp.execute(g)
     assert (C.to_dense_local() - ref).abs().max() < 1e-11
+
+
+def _dist_ooc_worker(rank, world, P, ta, tb, bcd):
+    import dplasma_amd as dp
+    ctx = dp.init(device="cpu", P=P)
+    for key, v in zip(("b", "c", "d"), bcd):
+        ctx.info.set(f"DPLASMA:GEMM:GPU:{key}", v)
+    M, N, K, NB = 70, 52, 61, 8
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, *((M, K) if ta == 0 else (K, M)))
+    B = dp.block_cyclic(ctx, torch.float64, NB, NB, *((K, N) if tb == 0 else (N, K)))
+    C = dp.block_cyclic(ctx, torch.float64, NB, NB, M, N)
+    for X, s in ((A, 1), (B, 2), (C, 3)):
+        dp.plrnt(ctx, X, s)
+    tp = dp.gemm_gpu_New(ctx, T[ta], T[tb], 0.5, A, B, -2.0, C, allow_cpu=True)
+    tp.execute(ctx)
+    return C.to_dense_local(), tp.bytes_recv
+
+
+@pytest.mark.parametrize("world,P,ta,tb,bcd", [(4, 2, 0, 0, (3, 2, 2)), (4, 2, 1, 0, (2, 4, 3)), (2, 1, 0, 1, (4, 3, 1)),
+                                               (3, 3, 1, 1, (5, 5, 4))])
+def test_gemm_ooc_distributed(world, P, ta, tb, bcd):
+    """Host-resident operands on a P x Q grid (zgemm_NN_gpu.jdf's super-blocks with GLOBAL barriers):
+    global b x c blocks of C, K in chunks of d tiles, only the tiles other ranks own are exchanged."""
+    from helpers import run_distributed
+    out = run_distributed(_dist_ooc_worker, world, P, ta, tb, bcd)
+    ctx = dp.init(device="cpu")
+    M, N, K, NB = 70, 52, 61, 8
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, *((M, K) if ta == 0 else (K, M)))
+    B = dp.block_cyclic(ctx, torch.float64, NB, NB, *((K, N) if tb == 0 else (N, K)))
+    C = dp.block_cyclic(ctx, torch.float64, NB, NB, M, N)
+    for X, s in ((A, 1), (B, 2), (C, 3)):
+        dp.plrnt(ctx, X, s)
+    op = lambda x, t: x if t == 0 else x.t()  # noqa: E731
+    ref = 0.5 * op(A.to_dense_local(), ta) @ op(B.to_dense_local(), tb) - 2.0 * C.to_dense_local()
+    full = sum(out[r][0] for r in range(world))
+    assert (full - ref).abs().max() < 1e-10
+    assert all(out[r][1] > 0 for r in range(world))   # every rank received remote operand tiles
