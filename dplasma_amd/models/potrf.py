@@ -185,7 +185,8 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
         slab = SG + SX
         GX = torch.zeros(nslab * D * slab, dtype=A.dtype, device=dev)
         dbuf = torch.zeros(nbe, dtype=A.dtype, device=dev)
-        tp._buffers = (GX, dbuf)
+        dpack = torch.zeros(A.mb * (A.mb + 1) // 2, dtype=A.dtype, device=dev)
+        tp._buffers = (GX, dbuf, dpack)
 
     # fp64 tiles <= 512 on the GPU: dataflow tile POTRF + register-resident panel TRSM sharing the
     # inverted diagonal 32-blocks (csrc/kernels/potrf_rb.hip); zbufs alternate with k's parity
@@ -265,10 +266,9 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                     dk_off = A.offset(*dk) if own_diag else None
 
                     def f_dbcast(dk_off=dk_off, src=src, kb=kb):
-                        if dk_off is not None:
-                            dv = torch.as_strided(dbuf, (kb, kb), (1, A.mb), 0)
-                            dv.copy_(torch.as_strided(A.data, (kb, kb), (1, A.ld), dk_off))
-                        comm.bcast(dbuf, src, line_group)
+                        # only the factor's triangle travels (the reference's LOWER/UPPER tile shapes)
+                        comm.bcast_tri(dbuf, 0, A.data if dk_off is not None else None, dk_off or 0, kb, A.ld,
+                                       A.mb, lower, src, line_group, pack=dpack)
                     t_db = tp.task(f"DBCAST({k})", pstream(k, "panel"), f_dbcast, [t_potrf, gate], prio=3)
                     tri_base, tri_ld, tri_off = dbuf, A.mb, 0
                 else:

@@ -470,10 +470,13 @@ class _Factor:
         self._bcast(e, V, Tm, e["root"])
 
     def _bcast(self, e, V, Tm, root):
-        """V and T along my process row (from the rank of my row that holds them)."""
+        """V and T along my process row (from the rank of my row that holds them); T is upper
+        triangular and only its triangle travels."""
         if self.dist and self.A.grid.Q > 1:
             comm.bcast(V[: e["ld"] * e["kf"]], root, self.ctx.row_group)
-            comm.bcast(Tm, root, self.ctx.row_group)
+            nb = self.A.nb
+            comm.bcast_tri(Tm, 0, Tm if self.A.rank == root else None, 0, e["kf"], nb, nb, False, root,
+                           self.ctx.row_group)
 
     def apply(self, e, upd, buf, work):
         if upd is None:
@@ -614,9 +617,11 @@ class _Apply:
         if not self.dist:
             return
         v = V[: ld * kf]
+        nb = A.nb
         if not self.pq:                       # 1 x Q: along the (only) process row
             comm.bcast(v, it["root"], ctx.row_group)
-            comm.bcast(self.Tm, it["root"], ctx.row_group)
+            comm.bcast_tri(self.Tm, 0, self.Tm if A.rank == it["root"] else None, 0, kf, nb, nb, False,
+                           it["root"], ctx.row_group)
             return
         if not self.left:                     # reflector rows = C's columns: every rank
             comm.bcast(v, it["root"], None, world=True)
@@ -630,7 +635,8 @@ class _Apply:
         if A.myrow in (it["rp"], it["rm"]) and A.grid.Q > 1:
             src = it["root"] if A.myrow == it["rm"] else it["relay"]
             comm.bcast(v, src, ctx.row_group)
-            comm.bcast(self.Tm, src, ctx.row_group)
+            comm.bcast_tri(self.Tm, 0, self.Tm if A.rank == src else None, 0, kf, nb, nb, False, src,
+                           ctx.row_group)
 
     def run_item(self, it):
         A = self.A

@@ -85,3 +85,36 @@ def exchange_add(t: torch.Tensor, peer: int, tmp: torch.Tensor) -> None:
     """t += (peer's t): symmetric pairwise sum through one send/recv pair (tmp: same size as t)."""
     p2p([(t, peer)], [(tmp[: t.numel()], peer)])
     t.add_(tmp[: t.numel()])
+
+
+_TRI_IDX = {}
+
+
+def _tri_index(n: int, ld: int, lower: bool, device) -> torch.Tensor:
+    """Element offsets (column-major, leading dimension ld) of the lower / upper triangle of an n x n
+    block, diagonal included -- n (n + 1) / 2 entries."""
+    key = (n, ld, lower, str(device))
+    t = _TRI_IDX.get(key)
+    if t is None:
+        r = torch.arange(n).view(-1, 1)
+        c = torch.arange(n).view(1, -1)
+        mask = (r >= c) if lower else (r <= c)
+        off = (r + c * ld).expand(n, n)
+        t = _TRI_IDX[key] = off.t()[mask.t()].contiguous().to(device)   # column by column
+    return t
+
+
+def bcast_tri(dst: torch.Tensor, dst_off: int, src: Optional[torch.Tensor], src_off: int, n: int, ld_src: int,
+              ld_dst: int, lower: bool, root: int, group, pack: Optional[torch.Tensor] = None) -> None:
+    """Broadcast only the lower / upper triangle of an n x n block (the reference's LOWER_TILE /
+    UPPER_TILE arena shapes: half the bytes of the full tile).  The root reads its block from
+    ``src[src_off]`` (leading dimension ld_src); every rank (root included) gets the triangle in
+    ``dst[dst_off]`` (ld_dst); the rest of the destination block is not written."""
+    if group is None:
+        return
+    nt = n * (n + 1) // 2
+    buf = pack[:nt] if pack is not None else torch.empty(nt, dtype=dst.dtype, device=dst.device)
+    if src is not None:
+        buf.copy_(src.view(-1)[src_off + _tri_index(n, ld_src, lower, src.device)])
+    bcast(buf, root, group)
+    dst.view(-1)[dst_off + _tri_index(n, ld_dst, lower, dst.device)] = buf
