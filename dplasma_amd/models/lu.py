@@ -51,6 +51,30 @@ def _tile_lu_nopiv(A, key, info, base):
 
 
 def getrf_nopiv_New(ctx, A, info_out=None):
+    """LU without pivoting (dplasma_zgetrf_nopiv_New, src/zgetrf_nopiv.jdf): the partial-pivoting
+    engine's PANEL / SWAP / NEXT / REST task structure with a non-pivoting panel (recursive device
+    LU on the tall panel, one TRSM launch for the U block row, MFMA GEMM trailing updates) on square
+    tiles; other tilings run the tile program below."""
+    if A.mb != A.nb:
+        return _getrf_nopiv_tiles_New(ctx, A, info_out)
+    tp = Taskpool("getrf_nopiv", ctx)
+    tp.flops = flops(A.prec, "getrf", A.m, A.n)
+    info = torch.zeros(1, dtype=torch.int32, device=A.device)
+    st = _GetrfDev(ctx, A, info, pivot=False)
+    st.add_tasks(tp, "getrf_nopiv")
+    tp._state = st
+    tp.info = info
+
+    def _done():
+        r = _reduce_info(info)
+        if info_out is not None:
+            info_out[0] = r
+        return r
+    tp.on_complete(_done)
+    return tp.finish_build()
+
+
+def _getrf_nopiv_tiles_New(ctx, A, info_out=None):
     prog = TileProgram(ctx, "getrf_nopiv")
     prog.flops = flops(A.prec, "getrf", A.m, A.n)
     info = torch.zeros(1, dtype=torch.int32, device=A.device)
@@ -144,8 +168,9 @@ class _GetrfDev:
     64k x 512 panel once over xGMI, so the panel is gathered once and factored redundantly by
     every process row of the column (same pivots everywhere, no further panel traffic)."""
 
-    def __init__(self, ctx, A, info):
+    def __init__(self, ctx, A, info, pivot: bool = True):
         self.ctx, self.A, self.info = ctx, A, info
+        self.pivot = pivot   # False: getrf_nopiv (same task structure, no interchanges)
         dev = self.dev = A.device
         mb, nb = A.mb, A.nb
         g = A.grid
@@ -217,7 +242,7 @@ class _GetrfDev:
         self.panel_mode = os.environ.get("DPLASMA_LU_PANEL", "gather")
         if self.panel_mode not in ("gather", "percol"):
             raise ValueError(f"DPLASMA_LU_PANEL={self.panel_mode!r}: expected gather or percol")
-        self.percol = self.panel_mode == "percol" and g.P > 1
+        self.percol = self.panel_mode == "percol" and g.P > 1 and pivot
         self.plan = [self._build(k) for k in range(self.kt)]
         self.bytes_panel = [0] * self.kt   # elements this rank sends per step (panel exchange)
         if self.percol:
@@ -261,7 +286,7 @@ class _GetrfDev:
                 st["gpack"] = pack.finalize() if len(pack) else None
                 st["gunpack"] = unpack.finalize()
                 st["gsent"] = sent
-            st["plu"] = ops.PanelLU(st["pv"], mp, mp, kb, pivot=True)
+            st["plu"] = ops.PanelLU(st["pv"], mp, mp, kb, pivot=self.pivot)
             if g.P > 1:
                 # percol mode: my panel rows, contiguous (ld = Ml), and their global row indices
                 lg, lu_ = TileBatch(), TileBatch()
@@ -337,7 +362,10 @@ class _GetrfDev:
         if g.Q > 1:
             root = g.rank(A.myrow, pc)
             comm.bcast(pv, root, ctx.row_group)
-            comm.bcast(self.piv_dev, root, ctx.row_group)
+            if self.pivot:
+                comm.bcast(self.piv_dev, root, ctx.row_group)
+        if not self.pivot:
+            return
         self.ipiv_all[r0: r0 + kmin].copy_(self.piv_dev[:kmin] + (r0 + 1))
         if self.tmp is not None:   # net moves of this step's interchanges (lists double-buffered by parity)
             par = k & 1
@@ -410,7 +438,9 @@ class _GetrfDev:
         kb, r0, mp = st["kb"], st["r0"], st["mp"]
         pv = st["pv"][: mp * kb]
         # --- row interchanges on every local column (the panel column is rewritten below)
-        if self.percol and self.tmp is not None:
+        if not self.pivot:
+            pass
+        elif self.percol and self.tmp is not None:
             # pivots are on the host in this mode: only the rows that cross process rows travel,
             # between the two process rows involved (one all-to-all of exact sizes per column group)
             piv = self.piv_dev[: st["kmin"]].cpu().numpy()
