@@ -160,3 +160,38 @@ def test_gpu_getrf_ptgpanel(prec, N, NB):
     assert rel_err(A.to_dense_local().cpu(), lu) < (1e-3 if prec == "s" else 1e-11)
     from dplasma_amd.models.lu import _gather_ipiv
     assert (torch.from_numpy(_gather_ipiv(gctx, IPIV)).long() == piv.long()).all()
+
+
+def _nopiv_worker(rank, world, P):
+    import dplasma_amd as dp
+    ctx = dp.init(device="cpu", P=P)
+    N, NB = 96, 16
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+    dp.plghe(ctx, float(N), dp.dplasmaUpperLower, A, 5)
+    return dp.getrf_nopiv(ctx, A), A.to_dense_local()
+
+
+@pytest.mark.parametrize("world,P", [(4, 2), (2, 2)])
+def test_getrf_nopiv_2d(world, P):
+    """getrf_nopiv on P x Q grids (device LU engine, gathered non-pivoting panel) = one process."""
+    out = run_distributed(_nopiv_worker, world, P)
+    info, ref = _nopiv_worker(0, 1, 1)
+    assert info == 0 and all(out[r][0] == 0 for r in range(world))
+    assert (sum(out[r][1] for r in range(world)) - ref).abs().max() < 1e-12
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec,N,NB", [("d", 3000, 512), ("z", 700, 128), ("s", 1100, 256)])
+def test_gpu_getrf_nopiv(prec, N, NB):
+    """The non-pivoting LU on the GPU (recursive device panel without pivot search) against
+    torch's factorisation of the same diagonally dominant matrix: ||L U - A|| / ||A||."""
+    g = dp.init(device="cuda:0")
+    dt = DTYPES[prec]
+    A = dp.block_cyclic(g, dt, NB, NB, N, N)
+    dp.plghe(g, float(N), dp.dplasmaUpperLower, A, 5)
+    a = A.to_dense_local().cpu().to(torch.complex128 if dt.is_complex else torch.float64)
+    assert dp.getrf_nopiv(g, A) == 0
+    lu = A.to_dense_local().cpu().to(a.dtype)
+    L = torch.tril(lu, -1) + torch.eye(N, dtype=a.dtype)
+    err = ((L @ torch.triu(lu) - a).abs().max() / a.abs().max()).item()
+    assert err < (1e-4 if prec in "sc" else 1e-12), err
