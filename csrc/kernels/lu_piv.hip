@@ -478,6 +478,71 @@ DPL_API long long dpl_lu_block_ws_bytes(int m) {
   return a + 3LL * 256 * PBW * 16 + 64;
 }
 
+// ------------------------------------------------------------------ no-pivot block LU
+// Columns [c0, cend) (<= 64), rows [c0, m) of P, without pivoting (CORE_zgetrf_nopiv's role): the
+// bw x bw top block is tiny, so every workgroup factors it redundantly in LDS (bw dependent steps on
+// 256 threads) and then solves its own 256 rows as L21 = A21 U11^-1 by forward substitution, one
+// row per thread -- no grid-wide synchronisation at all (the pivoting path needs one grid barrier per
+// column for the pivot search; without pivots the rows are independent given U11).
+constexpr int NPB = 64;
+template <typename T>
+__global__ __launch_bounds__(256) void k_lu_nopiv_block(T* __restrict__ A, int ld, int m, int c0, int cend,
+                                                        int* __restrict__ info, int info_base) {
+  __shared__ T U[NPB][NPB + 1];
+  const int tid = threadIdx.x;
+  const int bw = cend - c0;
+  const int top = min(bw, m - c0);
+  for (int e = tid; e < top * bw; e += 256) {
+    const int r = e % top, c = e / top;
+    U[r][c] = A[(long long)(c0 + r) + (long long)(c0 + c) * ld];
+  }
+  __syncthreads();
+  int bad = 0;
+  for (int j = 0; j < top; ++j) {
+    const T d = U[j][j];
+    if (is_zero(d)) {
+      if (!bad) bad = j + 1;
+      __syncthreads();
+      continue;
+    }
+    for (int e = tid; e < (top - j - 1) * (bw - j); e += 256) {
+      const int r = j + 1 + e % (top - j - 1), c = j + e / (top - j - 1);
+      if (c == j) U[r][j] = divv(U[r][j], d);
+    }
+    __syncthreads();
+    for (int e = tid; e < (top - j - 1) * (bw - j - 1); e += 256) {
+      const int r = j + 1 + e % (top - j - 1), c = j + 1 + e / (top - j - 1);
+      U[r][c] = sub(U[r][c], mul(U[r][j], U[j][c]));
+    }
+    __syncthreads();
+  }
+  if (blockIdx.x == 0) {
+    for (int e = tid; e < top * bw; e += 256) {
+      const int r = e % top, c = e / top;
+      A[(long long)(c0 + r) + (long long)(c0 + c) * ld] = U[r][c];
+    }
+    if (tid == 0 && bad && info && *info == 0) *info = info_base + c0 + bad;
+  }
+  // rows below the top block: x := x U11^-1
+  const int r = c0 + top + blockIdx.x * 256 + tid;
+  if (r >= m) return;
+  T x[NPB];
+#pragma unroll
+  for (int c = 0; c < NPB; ++c) x[c] = (c < bw) ? A[(long long)r + (long long)(c0 + c) * ld] : ST<T>::zero();
+#pragma unroll
+  for (int c = 0; c < NPB; ++c) {
+    if (c < bw) {
+      T v = x[c];
+#pragma unroll
+      for (int i = 0; i < c; ++i) v = sub(v, mul(x[i], U[i][c]));
+      x[c] = (c < top && !is_zero(U[c][c])) ? divv(v, U[c][c]) : v;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NPB; ++c)
+    if (c < bw) A[(long long)r + (long long)(c0 + c) * ld] = x[c];
+}
+
 DPL_API int dpl_lu_block(int prec, void* A, int ld, int m, int c0, int cend, int* ipiv, void* ws, int* cnt,
                          int* info, int info_base, int pivot, hipStream_t st) {
   if (cend - c0 > LU_MAXBW || c0 >= cend || m <= c0) return cend <= c0 ? 0 : -3;
@@ -509,6 +574,13 @@ DPL_API int dpl_lu_block(int prec, void* A, int ld, int m, int c0, int cend, int
                            ipiv, (float*)cand, pval, pidx, cnt, info, info_base);
       return (int)hipGetLastError();
     }
+  }
+  if (!pivot && cend - c0 <= NPB) {
+    const int rows_below = m - c0 - ((cend - c0) < (m - c0) ? (cend - c0) : (m - c0));
+    const int G = rows_below > 0 ? (rows_below + 255) / 256 : 1;
+    DISPATCH(prec, hipLaunchKernelGGL((k_lu_nopiv_block<T>), dim3(G), dim3(256), 0, st, (T*)A, ld, m, c0, cend, info,
+                                      info_base));
+    return (int)hipGetLastError();
   }
   const int maxwg = (m + LUR - 1) / LUR;
   for (int j = c0; j <= cend; ++j) {

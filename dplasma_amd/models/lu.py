@@ -286,7 +286,17 @@ class _GetrfDev:
                 st["gpack"] = pack.finalize() if len(pack) else None
                 st["gunpack"] = unpack.finalize()
                 st["gsent"] = sent
-            st["plu"] = ops.PanelLU(st["pv"], mp, mp, kb, pivot=self.pivot)
+            if self.pivot:
+                st["plu"] = ops.PanelLU(st["pv"], mp, mp, kb, pivot=True)
+            else:
+                # no pivoting: only the diagonal block needs the recursive LU; the rows below are
+                # L21 = A21 U11^-1, one TRSM launch (no grid barrier over the tall panel)
+                st["plu"] = ops.PanelLU(st["pv"], mp, kb, kb, pivot=False)
+                if mp > kb:
+                    tb = TileBatch()
+                    for r in range(kb, mp, mb):
+                        tb.add(0, min(mb, mp - r), kb, b_off=r)
+                    st["l21"] = tb.finalize()
             if g.P > 1:
                 # percol mode: my panel rows, contiguous (ld = Ml), and their global row indices
                 lg, lu_ = TileBatch(), TileBatch()
@@ -358,6 +368,8 @@ class _GetrfDev:
             elif "gather" in st:
                 ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, pv, mp, st["gather"], copy=True)
             st["plu"].run(self.piv_dev, self.ws, self.cnt, self.info, r0)
+            if "l21" in st:
+                ops.trsm(dplasmaRight, dplasmaUpper, N_, dplasmaNonUnit, 1.0, pv, mp, pv, mp, st["l21"])
         # --- factored panel + pivots along process rows
         if g.Q > 1:
             root = g.rank(A.myrow, pc)
