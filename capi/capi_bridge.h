@@ -8,9 +8,14 @@
 typedef int dplasma_enum_t;
 typedef __complex__ float dplasma_complex32_t;    // ABI of C's float _Complex
 typedef __complex__ double dplasma_complex64_t;   // ABI of C's double _Complex
-struct dplasma_context_s { PyObject* obj; };
-struct dplasma_desc_s { PyObject* obj; };
-struct dplasma_taskpool_s { PyObject* obj; };
+// Python-backed handles carry obj; handles of a native context (dplasma_init_native, native.cpp)
+// carry nat instead and never touch the interpreter
+struct NatCtx;
+struct NatDesc;
+struct NatProgram;
+struct dplasma_context_s { PyObject* obj = nullptr; NatCtx* nat = nullptr; };
+struct dplasma_desc_s { PyObject* obj = nullptr; NatDesc* nat = nullptr; };
+struct dplasma_taskpool_s { PyObject* obj = nullptr; NatProgram* nat = nullptr; };
 typedef struct dplasma_context_s dplasma_context_t;
 typedef struct dplasma_desc_s dplasma_desc_t;
 typedef struct dplasma_taskpool_s dplasma_taskpool_t;
@@ -46,3 +51,32 @@ dplasma_taskpool_t* dpl_call_new(dplasma_context_t* ctx, const char* name, std::
 // dplasma_amd.capi.call(ctx, name, *args) -> int / double (errors: -1 / NaN, message kept)
 int dpl_call_int(dplasma_context_t* ctx, const char* name, std::initializer_list<PyObject*> args);
 double dpl_call_real(dplasma_context_t* ctx, const char* name, std::initializer_list<PyObject*> args);
+
+// error message of the calling thread (dplasma_last_error)
+void dpl_set_error(const char* msg);
+
+// ---- native single-GPU engine (native.cpp)
+bool dpl_native(const dplasma_context_t* ctx);
+int nat_unsupported(const char* op);
+NatProgram* nat_potrf(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* A);
+NatProgram* nat_potrs(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* A, dplasma_desc_t* B);
+NatProgram* nat_posv(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* A, dplasma_desc_t* B);
+NatProgram* nat_gemm(dplasma_context_t* ctx, int prec, int tA, int tB, const void* alpha, dplasma_desc_t* A,
+                     dplasma_desc_t* B, const void* beta, dplasma_desc_t* C);
+NatProgram* nat_trsm(dplasma_context_t* ctx, int prec, int side, int uplo, int trans, int diag, const void* alpha,
+                     dplasma_desc_t* A, dplasma_desc_t* B);
+NatProgram* nat_plghe(dplasma_context_t* ctx, int prec, double bump, int uplo, dplasma_desc_t* A,
+                      unsigned long long seed);
+NatProgram* nat_plrnt(dplasma_context_t* ctx, int prec, int diagdom, dplasma_desc_t* A, unsigned long long seed);
+int nat_execute(dplasma_context_t* ctx, NatProgram* P);     // run + wait + info, frees P
+dplasma_taskpool_t* nat_wrap(NatProgram* P);
+void nat_fini(dplasma_context_t* ctx);
+dplasma_desc_t* nat_desc(dplasma_context_t* ctx, int prec, int mb, int nb, int m, int n, int P, int Q, void* data,
+                         int lld, int on_device);
+void nat_desc_free(dplasma_desc_t* A);
+int nat_desc_io(const dplasma_desc_t* A, void* host, int lda, bool to_device);
+int nat_add(dplasma_context_t* ctx, dplasma_taskpool_t* tp);
+int nat_start(dplasma_context_t* ctx);
+int nat_wait(dplasma_context_t* ctx);
+int nat_result(const dplasma_taskpool_t* tp);
+void nat_free(dplasma_taskpool_t* tp);

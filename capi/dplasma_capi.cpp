@@ -15,6 +15,7 @@
 
 static PyObject* g_capi = nullptr;   // module dplasma_amd.capi
 static thread_local std::string g_err;
+void dpl_set_error(const char* msg) { g_err = msg ? msg : ""; }
 
 void dpl_keep_error();
 static void keep_error() { dpl_keep_error(); }
@@ -152,9 +153,17 @@ extern "C" {
 
 DPL_CAPI const char* dplasma_last_error(void) { return g_err.c_str(); }
 
+// 1 once the embedded interpreter is up (never on a program that only uses native contexts)
+DPL_CAPI int dplasma_python_active(void) { return Py_IsInitialized() ? 1 : 0; }
+
 // ---- taskpool lifecycle (dplasma_<p><op>_New / _Destruct, parsec_context_add_taskpool / start / wait)
 DPL_CAPI void dplasma_taskpool_free(dplasma_taskpool_t* tp) {
   if (!tp) return;
+  if (tp->nat) {
+    nat_free(tp);
+    delete tp;
+    return;
+  }
   DplGil g;
   PyObject* r = call_obj(nullptr, "destruct", nullptr, {(Py_INCREF(tp->obj), tp->obj)});
   Py_XDECREF(r);
@@ -164,6 +173,7 @@ DPL_CAPI void dplasma_taskpool_free(dplasma_taskpool_t* tp) {
 
 DPL_CAPI int dplasma_context_add_taskpool(dplasma_context_t* ctx, dplasma_taskpool_t* tp) {
   if (!ctx || !tp) return -1;
+  if (ctx->nat) return nat_add(ctx, tp);
   DplGil g;
   g_err.clear();
   PyObject* r = call_obj(ctx, "add_taskpool", nullptr, {(Py_INCREF(tp->obj), tp->obj)});
@@ -174,6 +184,7 @@ DPL_CAPI int dplasma_context_add_taskpool(dplasma_context_t* ctx, dplasma_taskpo
 
 static int ctx_call(dplasma_context_t* ctx, const char* fn) {
   if (!ctx) return -1;
+  if (ctx->nat) return fn[0] == 's' ? nat_start(ctx) : nat_wait(ctx);
   DplGil g;
   g_err.clear();
   PyObject* r = call_obj(ctx, fn, nullptr, {});
@@ -187,6 +198,7 @@ DPL_CAPI int dplasma_context_wait(dplasma_context_t* ctx) { return ctx_call(ctx,
 // info / result of a completed taskpool (what the blocking call would have returned)
 DPL_CAPI int dplasma_taskpool_result(const dplasma_taskpool_t* tp) {
   if (!tp) return -1;
+  if (tp->nat) return nat_result(tp);
   DplGil g;
   g_err.clear();
   PyObject* r = call_obj(nullptr, "tp_result", nullptr, {(Py_INCREF(tp->obj), tp->obj)});
@@ -200,6 +212,10 @@ DPL_CAPI int dplasma_taskpool_result(const dplasma_taskpool_t* tp) {
 DPL_CAPI dplasma_desc_t* dplasma_desc_block_cyclic_lapack(dplasma_context_t* ctx, int prec, int mb, int nb, int m,
                                                           int n, int P, int Q, int ip, int jq, void* data, int lld,
                                                           int on_device) {
+  if (dpl_native(ctx)) {
+    if (ip != 0 || jq != 0) { g_err = "native descriptor: ip = jq = 0 (one process)"; return nullptr; }
+    return nat_desc(ctx, prec, mb, nb, m, n, P, Q, data, lld, on_device);
+  }
   DplGil g;
   g_err.clear();
   PyObject* o = call_obj(ctx, "desc_lapack", nullptr,
@@ -225,6 +241,11 @@ DPL_CAPI dplasma_context_t* dplasma_init(int nb_cores, int gpus) {
 
 DPL_CAPI void dplasma_fini(dplasma_context_t* ctx) {
   if (!ctx) return;
+  if (ctx->nat) {
+    nat_fini(ctx);
+    delete ctx;
+    return;
+  }
   dpl_ensure_python();
   PyGILState_STATE st = PyGILState_Ensure();
   PyObject* r = call_obj(ctx, "fini", nullptr, {});
@@ -236,6 +257,7 @@ DPL_CAPI void dplasma_fini(dplasma_context_t* ctx) {
 
 static int ctx_attr(const dplasma_context_t* ctx, const char* a) {
   if (!ctx) return -1;
+  if (ctx->nat) return a[0] == 'r' ? 0 : 1;   // rank 0 of a world of 1
   dpl_ensure_python();
   PyGILState_STATE st = PyGILState_Ensure();
   PyObject* v = PyObject_GetAttrString(ctx->obj, a);
@@ -249,6 +271,7 @@ DPL_CAPI int dplasma_context_world(const dplasma_context_t* ctx) { return ctx_at
 
 DPL_CAPI dplasma_desc_t* dplasma_desc_block_cyclic(dplasma_context_t* ctx, int prec, int mb, int nb, int m, int n,
                                                    int P, int Q, dplasma_enum_t uplo) {
+  if (dpl_native(ctx)) return nat_desc(ctx, prec, mb, nb, m, n, P, Q, nullptr, 0, 1);
   dpl_ensure_python();
   PyGILState_STATE st = PyGILState_Ensure();
   PyObject* o = call_obj(ctx, "desc_block_cyclic", nullptr,
@@ -261,6 +284,7 @@ DPL_CAPI dplasma_desc_t* dplasma_desc_block_cyclic(dplasma_context_t* ctx, int p
 }
 
 DPL_CAPI dplasma_desc_t* dplasma_desc_ipiv(dplasma_context_t* ctx, int mb, int nb, int m, int n, int P, int Q) {
+  if (dpl_native(ctx)) { nat_unsupported("desc_ipiv"); return nullptr; }
   dpl_ensure_python();
   PyGILState_STATE st = PyGILState_Ensure();
   PyObject* o = call_obj(ctx, "desc_int", nullptr,
@@ -274,6 +298,11 @@ DPL_CAPI dplasma_desc_t* dplasma_desc_ipiv(dplasma_context_t* ctx, int mb, int n
 
 DPL_CAPI void dplasma_desc_destroy(dplasma_desc_t* A) {
   if (!A) return;
+  if (A->nat) {
+    nat_desc_free(A);
+    delete A;
+    return;
+  }
   dpl_ensure_python();
   PyGILState_STATE st = PyGILState_Ensure();
   Py_DECREF(A->obj);
@@ -282,6 +311,7 @@ DPL_CAPI void dplasma_desc_destroy(dplasma_desc_t* A) {
 }
 
 static int desc_io(const dplasma_desc_t* A, const void* host, int lda, const char* fn) {
+  if (A && A->nat) return nat_desc_io(A, const_cast<void*>(host), lda, fn[5] == 's');
   dpl_ensure_python();
   PyGILState_STATE st = PyGILState_Ensure();
   PyObject* r = call_obj(nullptr, fn, nullptr,

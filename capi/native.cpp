@@ -1,0 +1,769 @@
+// Interpreter-free single-GPU engine behind the C ABI (dplasma_init_native).
+//
+// The default C ABI (dplasma_capi.cpp) embeds CPython and forwards every call to dplasma_amd.  A
+// native context never starts the interpreter: descriptors are LAPACK-layout device buffers, the
+// algorithms below are compiled into stream programs here in C++ and their tasks launch the HIP
+// kernels of libdplasma_kernels.so directly (the same kernels, batch records and schedules as the
+// Python builders: models/potrf.py, models/gemm.py, models/blas3.py, models/aux.py).
+//
+// Runtime: a program is a list of tasks, each bound to one of the context's two HIP streams
+// ("panel", high priority: the critical path; "update", low priority: bulk trailing updates)
+// with explicit dependencies on earlier tasks; running it enqueues every task in order and
+// inserts a HIP event wait only for cross-stream edges (the PaRSEC dataflow of the reference's
+// JDF taskpools -- src/zpotrf_L.jdf:93-188 -- as stream order + events, no host round trips).
+// Batch records (GemmItemK / KPair / TileItem / RbItem) are built and uploaded once, when the
+// program is built (dplasma_<p><op>_New), so a run only launches kernels.
+//
+// Scope: one process, one GPU; s/d/c/z potrf, potrs, posv, gemm, trsm (all 8 side/uplo/trans
+// variants), plghe, plrnt.  Every other entry point returns an error on a native context.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "capi_bridge.h"
+
+extern "C" {  // csrc/kernels (libdplasma_kernels.so)
+int dpl_gemm_batched(int prec, int transA, int transB, int nitems, const void* items, const void* kpairs, int max_m,
+                     int max_n, const void* alpha, const void* A, int lda, const void* B, int ldb, const void* beta,
+                     void* C, int ldc, int vec_ok, int force_generic, hipStream_t st);
+int dpl_potrf_tile(int prec, int uplo, int n, void* A, long long a_off, int lda, int* info, int info_base,
+                   hipStream_t st);
+int dpl_potrf_tile_rbz(int uplo, int n, double* A, int lda, int* info, int info_base, double* zbuf, hipStream_t st);
+int dpl_potrf_zbuf_size();
+int dpl_trsm_rb(int uplo, int n, const double* L, int ldl, const double* zbuf, int nrb, const void* items, double* B,
+                int ldb, hipStream_t st);
+int dpl_trsm_batched(int prec, int side, int uplo, int trans, int diag, int nitems, const void* items, int max_m,
+                     int max_n, const void* alpha, const void* A, int lda, void* B, int ldb, int ntri,
+                     const void* tri_off, void* work, hipStream_t st);
+int dpl_generate(int prec, int kind, int nitems, const void* items, int mmax, int nmax, void* A, int lda,
+                 long long gM, unsigned long long seed, const void* bump, hipStream_t st);
+}
+
+namespace {
+
+enum { NOTRANS = 111, TRANS = 112, CONJTRANS = 113, UPPER = 121, LOWER = 122, UPPERLOWER = 123, NONUNIT = 131,
+       LEFT = 141, RIGHT = 142 };
+enum { P_S = 2, P_D = 3, P_C = 4, P_Z = 5 };
+
+// kernel records (csrc/kernels/common.h, gemm.hip, potrf_rb.hip)
+struct GemmItemK { long long c_off; int kt_beg, kt_cnt, m, n, flags, pad; };
+struct KPair { long long a_off, b_off; int k, pad; };
+struct TileItem { long long a_off, b_off; int m, n, gi, gj; };
+struct RbItem { long long b_off; int rows, pad; };
+static_assert(sizeof(GemmItemK) == 32 && sizeof(KPair) == 24 && sizeof(TileItem) == 32 && sizeof(RbItem) == 16,
+              "kernel record layouts");
+
+int esize(int prec) { return prec == P_S ? 4 : prec == P_Z ? 16 : 8; }
+bool prec_ok(int prec) { return prec >= P_S && prec <= P_Z; }
+
+// one scalar of a precision (complex = two reals), as the kernels' host API takes it
+struct Scalar {
+  alignas(16) unsigned char b[16] = {};   // read as hipDoubleComplex (16-byte aligned loads)
+  Scalar(int prec, double re, double im = 0.0) {
+    if (prec == P_S || prec == P_C) {
+      float v[2] = {(float)re, (float)im};
+      std::memcpy(b, v, prec == P_S ? 4 : 8);
+    } else {
+      double v[2] = {re, im};
+      std::memcpy(b, v, prec == P_D ? 8 : 16);
+    }
+  }
+  Scalar(int prec, const void* p) { std::memcpy(b, p, esize(prec)); }
+  const void* ptr() const { return b; }
+};
+
+struct DevMem {
+  void* p = nullptr;
+  ~DevMem() {
+    if (p) (void)hipFree(p);
+  }
+};
+using DevPtr = std::shared_ptr<DevMem>;
+
+DevPtr dev_alloc(size_t bytes, bool zero) {
+  auto d = std::make_shared<DevMem>();
+  if (bytes == 0) bytes = 16;
+  if (hipMalloc(&d->p, bytes) != hipSuccess) return nullptr;
+  if (zero && hipMemset(d->p, 0, bytes) != hipSuccess) return nullptr;
+  return d;
+}
+
+template <typename R>
+DevPtr dev_upload(const std::vector<R>& v) {
+  auto d = dev_alloc(v.size() * sizeof(R), false);
+  if (d && !v.empty() && hipMemcpy(d->p, v.data(), v.size() * sizeof(R), hipMemcpyHostToDevice) != hipSuccess)
+    return nullptr;
+  return d;
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------------------- handles
+struct NatCtx {
+  int device = 0;
+  hipStream_t st[2] = {nullptr, nullptr};   // 0: panel (high priority), 1: update
+  hipEvent_t join[2] = {nullptr, nullptr};
+  std::vector<NatProgram*> queue;
+};
+
+struct NatDesc {
+  NatCtx* ctx = nullptr;
+  int prec = P_D, es = 8, mb = 0, nb = 0, m = 0, n = 0, mt = 0, nt = 0, lld = 0;
+  char* data = nullptr;
+  bool owned = false;
+  NatDesc() = default;
+  NatDesc(const NatDesc&) = delete;             // owns its buffer: never copied (nor captured by value)
+  NatDesc& operator=(const NatDesc&) = delete;
+  long long off(int i, int j) const { return (long long)i * mb + (long long)j * nb * lld; }
+  int rows(int i) const { return std::min(mb, m - i * mb); }
+  int cols(int j) const { return std::min(nb, n - j * nb); }
+  ~NatDesc() {
+    if (owned && data) (void)hipFree(data);
+  }
+};
+
+struct NatTask {
+  int stream;
+  std::vector<int> deps;
+  std::function<int(hipStream_t)> fn;
+  bool event = false;
+};
+
+struct NatProgram {
+  NatCtx* ctx = nullptr;
+  std::string name;
+  std::vector<NatTask> tasks;
+  std::vector<hipEvent_t> ev;
+  std::vector<DevPtr> keep;      // batch records and scratch referenced by the tasks
+  DevPtr info;                   // device int: first failing column (LAPACK info), 0 if none
+  int result = 0;
+  bool enqueued = false;
+
+  int task(int stream, std::function<int(hipStream_t)> fn, std::initializer_list<int> deps) {
+    NatTask t;
+    t.stream = stream;
+    t.fn = std::move(fn);
+    const int id = (int)tasks.size();
+    for (int d : deps) {
+      if (d < 0 || d >= id) continue;
+      t.deps.push_back(d);
+      if (tasks[d].stream != stream) tasks[d].event = true;
+    }
+    tasks.push_back(std::move(t));
+    return id;
+  }
+
+  // enqueue every task (stream order + events for cross-stream edges); the program starts after
+  // everything already queued on both streams (join events) -- programs compose in call order
+  int run() {
+    if (ev.empty()) {
+      ev.assign(tasks.size(), nullptr);
+      for (size_t i = 0; i < tasks.size(); ++i)
+        if (tasks[i].event && hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) return -1;
+    }
+    for (int s = 0; s < 2; ++s)
+      if (hipEventRecord(ctx->join[s], ctx->st[s]) != hipSuccess) return -1;
+    for (int s = 0; s < 2; ++s)
+      if (hipStreamWaitEvent(ctx->st[s], ctx->join[1 - s], 0) != hipSuccess) return -1;
+    // info is written by panel-stream tasks only (tile factorisations)
+    if (info && hipMemsetAsync(info->p, 0, sizeof(int), ctx->st[0]) != hipSuccess) return -1;
+    for (size_t i = 0; i < tasks.size(); ++i) {
+      NatTask& t = tasks[i];
+      hipStream_t s = ctx->st[t.stream];
+      for (int d : t.deps)
+        if (tasks[d].stream != t.stream && hipStreamWaitEvent(s, ev[d], 0) != hipSuccess) return -1;
+      const int rc = t.fn(s);
+      if (rc != 0) return rc;
+      if (t.event && hipEventRecord(ev[i], s) != hipSuccess) return -1;
+    }
+    enqueued = true;
+    return 0;
+  }
+
+  int wait() {
+    for (int s = 0; s < 2; ++s)
+      if (hipStreamSynchronize(ctx->st[s]) != hipSuccess) return -1;
+    result = 0;
+    if (info && hipMemcpy(&result, info->p, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    enqueued = false;
+    return 0;
+  }
+
+  ~NatProgram() {
+    for (hipEvent_t e : ev)
+      if (e) (void)hipEventDestroy(e);
+  }
+};
+
+namespace {
+
+// ----------------------------------------------------------------------------- batches
+struct Gemm {
+  std::vector<GemmItemK> it;
+  std::vector<KPair> kp;
+  int max_m = 0, max_n = 0;
+  bool full = true;
+  long long align = 0;
+  DevPtr d_it, d_kp;
+
+  void add(long long c, int m, int n, const std::vector<KPair>& pairs, int mask) {
+    GemmItemK g{c, (int)kp.size(), (int)pairs.size(), m, n, mask, 0};
+    for (const KPair& p : pairs) {
+      kp.push_back(p);
+      align |= p.a_off | p.b_off;
+      if (p.k % 16) full = false;
+    }
+    if (m % 128 || n % 128) full = false;
+    align |= c;
+    it.push_back(g);
+    max_m = std::max(max_m, m);
+    max_n = std::max(max_n, n);
+  }
+  bool empty() const { return it.empty(); }
+  bool upload(NatProgram& P) {
+    if (kp.empty()) kp.push_back(KPair{0, 0, 0, 0});
+    d_it = dev_upload(it);
+    d_kp = dev_upload(kp);
+    if (!d_it || !d_kp) return false;
+    P.keep.push_back(d_it);
+    P.keep.push_back(d_kp);
+    return true;
+  }
+  int launch(int prec, int ta, int tb, const Scalar& alpha, const void* A, int lda, const void* B, int ldb,
+             const Scalar& beta, void* C, int ldc, hipStream_t st) const {
+    if (it.empty()) return 0;
+    const int ve = std::max(1, 16 / esize(prec));
+    int vec = (align % ve == 0 && lda % ve == 0 && ldb % ve == 0 && (uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0)
+                  ? 1 : 0;
+    if (vec && full) vec |= 2;
+    return dpl_gemm_batched(prec, ta, tb, (int)it.size(), d_it->p, d_kp->p, max_m, max_n, alpha.ptr(), A, lda, B,
+                            ldb, beta.ptr(), C, ldc, vec, 0, st);
+  }
+};
+
+// items sharing ONE triangular tile (dpl_trsm_batched with ntri = 1)
+struct Trsm1 {
+  std::vector<TileItem> it;
+  int max_m = 0, max_n = 0, npos = 0;
+  DevPtr d_it, d_tri, d_work;
+  long long tri = 0;
+  void add(long long b_off, int m, int n) {
+    it.push_back(TileItem{tri, b_off, m, n, 0, 0});
+    max_m = std::max(max_m, m);
+    max_n = std::max(max_n, n);
+  }
+  bool upload(NatProgram& P, int prec, int side) {
+    npos = side == LEFT ? max_m : max_n;
+    d_it = dev_upload(it);
+    d_tri = dev_upload(std::vector<long long>{tri});
+    d_work = dev_alloc((size_t)((npos + 15) / 16) * 256 * esize(prec), false);
+    if (!d_it || !d_tri || !d_work) return false;
+    P.keep.push_back(d_it);
+    P.keep.push_back(d_tri);
+    P.keep.push_back(d_work);
+    return true;
+  }
+  int launch(int prec, int side, int uplo, int trans, int diag, const Scalar& alpha, const void* A, int lda, void* B,
+             int ldb, hipStream_t st) const {
+    if (it.empty()) return 0;
+    return dpl_trsm_batched(prec, side, uplo, trans, diag, (int)it.size(), d_it->p, max_m, max_n, alpha.ptr(), A, lda,
+                            B, ldb, 1, d_tri->p, d_work->p, st);
+  }
+};
+
+NatProgram* fail(NatProgram* P, const std::string& msg) {
+  delete P;
+  dpl_set_error(msg.c_str());
+  return nullptr;
+}
+
+NatProgram* new_program(NatCtx* c, const char* name, bool with_info) {
+  NatProgram* P = new NatProgram;
+  P->ctx = c;
+  P->name = name;
+  if (with_info) P->info = dev_alloc(sizeof(int), true);
+  return P;
+}
+
+int env_int(const char* k, int dflt) {
+  const char* v = std::getenv(k);
+  return v && *v ? std::atoi(v) : dflt;
+}
+
+// ----------------------------------------------------------------------------- POTRF
+// models/potrf.py on one process: blocks of D panels; per panel POTRF(k) and its panel TRSM on the
+// panel stream, NEAR(k) (the rest of the block) right after; per block NEXT (the next block's
+// columns, K = D*nb) and REST (everything beyond) on the update stream; the next block's first
+// POTRF follows NEXT.  fp64 tiles <= 512: dataflow tile kernel + register-resident panel TRSM
+// sharing the inverted 32-blocks (potrf_rb.hip); other precisions: tile POTRF + batched TRSM.
+bool add_potrf(NatProgram& P, int uplo, NatDesc& A) {
+  const int prec = A.prec, nt = A.nt;
+  const bool lower = uplo == LOWER;
+  const int D = std::max(1, env_int("DPLASMA_POTRF_DEFER", 4));
+  const int min_tiles = env_int("DPLASMA_POTRF_DEFER_MIN_TILES", 24);
+  const bool rb = prec == P_D && A.mb == A.nb && A.mb <= 512;
+  const int zsz = rb ? dpl_potrf_zbuf_size() : 0;
+  DevPtr zb;
+  if (rb) {
+    zb = dev_alloc((size_t)2 * zsz * sizeof(double), false);
+    if (!zb) return false;
+    P.keep.push_back(zb);
+  }
+  auto tc = [&](int i, int k) { return lower ? std::make_pair(i, k) : std::make_pair(k, i); };
+  const int tri_mask = lower ? 1 : 2;
+  const int tA = lower ? NOTRANS : CONJTRANS, tB = lower ? CONJTRANS : NOTRANS;
+  const Scalar m_one(prec, -1.0), one(prec, 1.0);
+  char* base = A.data;
+  const int ld = A.lld, mbA = A.mb;
+  int* info = (int*)P.info->p;
+
+  auto update = [&](const std::vector<int>& ks, int n0, int n1) {
+    auto g = std::make_shared<Gemm>();
+    for (int n_ = n0; n_ < n1; ++n_)
+      for (int m_ = n_; m_ < nt; ++m_) {
+        const auto cc = lower ? std::make_pair(m_, n_) : std::make_pair(n_, m_);
+        std::vector<KPair> kp;
+        for (int k : ks) {
+          const auto a = tc(cc.first, k), b = tc(cc.second, k);
+          kp.push_back(KPair{A.off(a.first, a.second), A.off(b.first, b.second), A.rows(k), 0});
+        }
+        g->add(A.off(cc.first, cc.second), A.rows(cc.first), A.cols(cc.second), kp, m_ == n_ ? tri_mask : 0);
+      }
+    return g;
+  };
+  auto gemm_task = [&](std::shared_ptr<Gemm> g) {
+    return [=](hipStream_t s) { return g->launch(prec, tA, tB, m_one, base, ld, base, ld, one, base, ld, s); };
+  };
+
+  std::vector<std::pair<int, int>> blocks;
+  for (int c = 0; c < nt;) {
+    const int d = nt - c >= min_tiles ? D : 1;
+    blocks.emplace_back(c, std::min(nt, c + d));
+    c += d;
+  }
+  int gate = -1, last_upd = -1;
+  for (size_t b = 0; b < blocks.size(); ++b) {
+    const int c0 = blocks[b].first, c1 = blocks[b].second;
+    for (int k = c0; k < c1; ++k) {
+      const int kb = A.rows(k);
+      const long long dk = A.off(k, k);
+      double* zk = rb ? (double*)zb->p + (size_t)(k % 2) * zsz : nullptr;
+      int t_potrf;
+      if (rb)
+        t_potrf = P.task(0, [=](hipStream_t s) {
+          return dpl_potrf_tile_rbz(uplo, kb, (double*)base + dk, ld, info, k * mbA, zk, s);
+        }, {gate});
+      else
+        t_potrf = P.task(0, [=](hipStream_t s) {
+          return dpl_potrf_tile(prec, uplo, kb, base, dk, ld, info, k * mbA, s);
+        }, {gate});
+      int t_trsm = t_potrf;
+      if (k + 1 < nt) {
+        if (rb) {
+          std::vector<RbItem> strips;
+          for (int i = k + 1; i < nt; ++i) {
+            const auto cc = tc(i, k);
+            const int ext = lower ? A.rows(i) : A.cols(i);
+            for (int r0 = 0; r0 < ext; r0 += 16)
+              strips.push_back(RbItem{A.off(cc.first, cc.second) + (lower ? r0 : (long long)r0 * ld),
+                                      std::min(16, ext - r0), 0});
+          }
+          DevPtr d = dev_upload(strips);
+          if (!d) return false;
+          P.keep.push_back(d);
+          const int nrb = (int)strips.size();
+          t_trsm = P.task(0, [=](hipStream_t s) {
+            return dpl_trsm_rb(uplo, kb, (double*)base + dk, ld, zk, nrb, d->p, (double*)base, ld, s);
+          }, {t_potrf, gate});
+        } else {
+          auto tr = std::make_shared<Trsm1>();
+          tr->tri = dk;
+          for (int i = k + 1; i < nt; ++i) {
+            const auto cc = tc(i, k);
+            tr->add(A.off(cc.first, cc.second), A.rows(cc.first), A.cols(cc.second));
+          }
+          const int side = lower ? RIGHT : LEFT;
+          if (!tr->upload(P, prec, side)) return false;
+          t_trsm = P.task(0, [=](hipStream_t s) {
+            return tr->launch(prec, side, uplo, CONJTRANS, NONUNIT, one, base, ld, base, ld, s);
+          }, {t_potrf, gate});
+        }
+      }
+      if (k == nt - 1) break;
+      auto near = update({k}, k + 1, c1);
+      if (!near->empty()) {
+        if (!near->upload(P)) return false;
+        gate = P.task(0, gemm_task(near), {t_trsm, gate});
+      } else {
+        gate = t_trsm;
+      }
+    }
+    if (c1 >= nt) break;
+    std::vector<int> ks;
+    for (int k = c0; k < c1; ++k) ks.push_back(k);
+    const int n0 = blocks[b + 1].first, n1 = blocks[b + 1].second;
+    auto nxt = update(ks, n0, n1), rest = update(ks, n1, nt);
+    int t_next = -1;
+    if (!nxt->empty()) {
+      if (!nxt->upload(P)) return false;
+      t_next = P.task(1, gemm_task(nxt), {gate, last_upd});
+      last_upd = t_next;
+    }
+    if (!rest->empty()) {
+      if (!rest->upload(P)) return false;
+      last_upd = P.task(1, gemm_task(rest), {gate, last_upd});
+    }
+    if (t_next >= 0) gate = t_next;
+  }
+  return true;
+}
+
+// ----------------------------------------------------------------------------- TRSM
+// op(A) X = alpha B (left) / X op(A) = alpha B (right), tile by tile (models/blas3.py): solve one
+// block row (left) / column (right) of B against the diagonal tile, then update the blocks still
+// to be solved with one GEMM launch (beta = alpha on the first step, 1 afterwards).
+bool add_trsm(NatProgram& P, int side, int uplo, int trans, int diag, const Scalar& alpha, NatDesc& A, NatDesc& B,
+              int stream) {
+  const int prec = B.prec;
+  const bool left = side == LEFT, notrans = trans == NOTRANS;
+  const int nk = left ? B.mt : B.nt;
+  // effective lower (forward) for left: lower & notrans or upper & trans; right is the mirror
+  const bool forward = left ? ((uplo == LOWER) == notrans) : ((uplo == UPPER) == notrans);
+  std::vector<int> order;
+  for (int i = 0; i < nk; ++i) order.push_back(forward ? i : nk - 1 - i);
+  const Scalar one(prec, 1.0), m_one(prec, -1.0);
+  char* a = A.data;
+  char* bb = B.data;
+  const int lda = A.lld, ldb = B.lld;
+  int prev = -1;
+  for (int s = 0; s < nk; ++s) {
+    const int k = order[s];
+    const Scalar ak = s == 0 ? alpha : one;
+    auto tr = std::make_shared<Trsm1>();
+    tr->tri = A.off(k, k);
+    if (left)
+      for (int n = 0; n < B.nt; ++n) tr->add(B.off(k, n), B.rows(k), B.cols(n));
+    else
+      for (int m = 0; m < B.mt; ++m) tr->add(B.off(m, k), B.rows(m), B.cols(k));
+    if (!tr->upload(P, prec, side)) return false;
+    prev = P.task(stream, [=](hipStream_t st) {
+      return tr->launch(prec, side, uplo, trans, diag, ak, a, lda, bb, ldb, st);
+    }, {prev});
+    if (s + 1 == nk) break;
+    auto g = std::make_shared<Gemm>();
+    for (int r = s + 1; r < nk; ++r) {
+      const int i = order[r];
+      if (left) {   // B(i, n) = ak B(i, n) - op(A)(i, k) X(k, n)
+        const long long ao = notrans ? A.off(i, k) : A.off(k, i);
+        for (int n = 0; n < B.nt; ++n)
+          g->add(B.off(i, n), B.rows(i), B.cols(n), {KPair{ao, B.off(k, n), B.rows(k), 0}}, 0);
+      } else {      // B(m, i) = ak B(m, i) - X(m, k) op(A)(k, i)
+        const long long ao = notrans ? A.off(k, i) : A.off(i, k);
+        for (int m = 0; m < B.mt; ++m)
+          g->add(B.off(m, i), B.rows(m), B.cols(i), {KPair{B.off(m, k), ao, B.cols(k), 0}}, 0);
+      }
+    }
+    if (!g->upload(P)) return false;
+    if (left)
+      prev = P.task(stream, [=](hipStream_t st) {
+        return g->launch(prec, notrans ? NOTRANS : trans, NOTRANS, m_one, a, lda, bb, ldb, ak, bb, ldb, st);
+      }, {prev});
+    else
+      prev = P.task(stream, [=](hipStream_t st) {
+        return g->launch(prec, NOTRANS, notrans ? NOTRANS : trans, m_one, bb, ldb, a, lda, ak, bb, ldb, st);
+      }, {prev});
+  }
+  return true;
+}
+
+bool add_potrs(NatProgram& P, int uplo, NatDesc& A, NatDesc& B) {
+  const Scalar one(B.prec, 1.0);
+  if (uplo == LOWER)
+    return add_trsm(P, LEFT, LOWER, NOTRANS, NONUNIT, one, A, B, 1) &&
+           add_trsm(P, LEFT, LOWER, CONJTRANS, NONUNIT, one, A, B, 1);
+  return add_trsm(P, LEFT, UPPER, CONJTRANS, NONUNIT, one, A, B, 1) &&
+         add_trsm(P, LEFT, UPPER, NOTRANS, NONUNIT, one, A, B, 1);
+}
+
+bool same_ctx(NatCtx* c, std::initializer_list<const NatDesc*> ds, int prec) {
+  for (const NatDesc* d : ds)
+    if (!d || d->ctx != c || d->prec != prec) return false;
+  return true;
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------------------- builders (capi_bridge.h)
+NatProgram* nat_potrf(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* dA) {
+  NatCtx* c = ctx->nat;
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!same_ctx(c, {A}, prec)) return fail(nullptr, "potrf: descriptor of another context or precision");
+  if (A->m != A->n || A->mb != A->nb || (uplo != LOWER && uplo != UPPER))
+    return fail(nullptr, "potrf: square matrix with square tiles and uplo Lower/Upper required");
+  NatProgram* P = new_program(c, "potrf", true);
+  if (!P->info || !add_potrf(*P, uplo, *A)) return fail(P, "potrf: device allocation failed");
+  return P;
+}
+
+NatProgram* nat_potrs(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* dA, dplasma_desc_t* dB) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *B = dB ? dB->nat : nullptr;
+  if (!same_ctx(c, {A, B}, prec) || A->m != A->n || B->m != A->n || B->mb != A->nb)
+    return fail(nullptr, "potrs: descriptors do not conform");
+  NatProgram* P = new_program(c, "potrs", false);
+  if (!add_potrs(*P, uplo, *A, *B)) return fail(P, "potrs: device allocation failed");
+  return P;
+}
+
+NatProgram* nat_posv(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* dA, dplasma_desc_t* dB) {
+  NatProgram* P = nat_potrf(ctx, prec, uplo, dA);
+  if (!P) return nullptr;
+  NatDesc *A = dA->nat, *B = dB ? dB->nat : nullptr;
+  if (!same_ctx(ctx->nat, {B}, prec) || B->m != A->n || B->mb != A->nb)
+    return fail(P, "posv: right-hand side does not conform");
+  if (!add_potrs(*P, uplo, *A, *B)) return fail(P, "posv: device allocation failed");
+  return P;
+}
+
+NatProgram* nat_gemm(dplasma_context_t* ctx, int prec, int tA, int tB, const void* alpha, dplasma_desc_t* dA,
+                     dplasma_desc_t* dB, const void* beta, dplasma_desc_t* dC) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *B = dB ? dB->nat : nullptr, *C = dC ? dC->nat : nullptr;
+  if (!same_ctx(c, {A, B, C}, prec)) return fail(nullptr, "gemm: descriptors of another context or precision");
+  const int am = tA == NOTRANS ? A->m : A->n, ak = tA == NOTRANS ? A->n : A->m;
+  const int bk = tB == NOTRANS ? B->m : B->n, bn = tB == NOTRANS ? B->n : B->m;
+  const int akb = tA == NOTRANS ? A->nb : A->mb, bkb = tB == NOTRANS ? B->mb : B->nb;
+  if (am != C->m || bn != C->n || ak != bk || akb != bkb || (tA == NOTRANS ? A->mb : A->nb) != C->mb ||
+      (tB == NOTRANS ? B->nb : B->mb) != C->nb)
+    return fail(nullptr, "gemm: operands do not conform");
+  NatProgram* P = new_program(c, "gemm", false);
+  auto g = std::make_shared<Gemm>();
+  const int kt = (ak + akb - 1) / akb;
+  for (int n = 0; n < C->nt; ++n)
+    for (int m = 0; m < C->mt; ++m) {
+      std::vector<KPair> kp;
+      for (int k = 0; k < kt; ++k) {
+        const long long ao = tA == NOTRANS ? A->off(m, k) : A->off(k, m);
+        const long long bo = tB == NOTRANS ? B->off(k, n) : B->off(n, k);
+        kp.push_back(KPair{ao, bo, tA == NOTRANS ? A->cols(k) : A->rows(k), 0});
+      }
+      g->add(C->off(m, n), C->rows(m), C->cols(n), kp, 0);
+    }
+  if (!g->upload(*P)) return fail(P, "gemm: device allocation failed");
+  const Scalar al(prec, alpha), be(prec, beta);
+  char *a = A->data, *b = B->data, *cc = C->data;
+  const int lda = A->lld, ldb = B->lld, ldc = C->lld;
+  P->task(1, [=](hipStream_t s) { return g->launch(prec, tA, tB, al, a, lda, b, ldb, be, cc, ldc, s); }, {});
+  return P;
+}
+
+NatProgram* nat_trsm(dplasma_context_t* ctx, int prec, int side, int uplo, int trans, int diag, const void* alpha,
+                     dplasma_desc_t* dA, dplasma_desc_t* dB) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *B = dB ? dB->nat : nullptr;
+  if (!same_ctx(c, {A, B}, prec)) return fail(nullptr, "trsm: descriptors of another context or precision");
+  const int order = side == LEFT ? B->m : B->n;
+  if (A->m != A->n || A->m != order || A->mb != A->nb || (side == LEFT ? B->mb : B->nb) != A->nb)
+    return fail(nullptr, "trsm: operands do not conform");
+  NatProgram* P = new_program(c, "trsm", false);
+  if (!add_trsm(*P, side, uplo, trans, diag, Scalar(prec, alpha), *A, *B, 1))
+    return fail(P, "trsm: device allocation failed");
+  return P;
+}
+
+static NatProgram* generator(dplasma_context_t* ctx, int prec, int kind, int uplo, const Scalar& bump,
+                             dplasma_desc_t* dA, unsigned long long seed, const char* name) {
+  NatCtx* c = ctx->nat;
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!same_ctx(c, {A}, prec)) return fail(nullptr, std::string(name) + ": descriptor of another context");
+  NatProgram* P = new_program(c, name, false);
+  std::vector<TileItem> it;
+  int mm = 0, nn = 0;
+  for (int n = 0; n < A->nt; ++n)
+    for (int m = 0; m < A->mt; ++m) {
+      if ((uplo == LOWER && m < n) || (uplo == UPPER && m > n)) continue;
+      it.push_back(TileItem{A->off(m, n), 0, A->rows(m), A->cols(n), m * A->mb, n * A->nb});
+      mm = std::max(mm, A->rows(m));
+      nn = std::max(nn, A->cols(n));
+    }
+  DevPtr d = dev_upload(it);
+  if (!d) return fail(P, std::string(name) + ": device allocation failed");
+  P->keep.push_back(d);
+  const int ni = (int)it.size(), lda = A->lld;
+  const long long gM = A->m;
+  char* base = A->data;
+  P->task(1, [=](hipStream_t s) {
+    return dpl_generate(prec, kind, ni, d->p, mm, nn, base, lda, gM, seed, bump.ptr(), s);
+  }, {});
+  return P;
+}
+
+NatProgram* nat_plghe(dplasma_context_t* ctx, int prec, double bump, int uplo, dplasma_desc_t* A,
+                      unsigned long long seed) {
+  return generator(ctx, prec, 1, uplo, Scalar(prec, bump), A, seed, "plghe");
+}
+
+NatProgram* nat_plrnt(dplasma_context_t* ctx, int prec, int diagdom, dplasma_desc_t* A, unsigned long long seed) {
+  if (diagdom) return fail(nullptr, "plrnt: diagdom is not available on a native context");
+  return generator(ctx, prec, 0, UPPERLOWER, Scalar(prec, 0.0), A, seed, "plrnt");
+}
+
+// ----------------------------------------------------------------------------- execution
+int nat_execute(dplasma_context_t* ctx, NatProgram* P) {
+  if (!P) return -1;
+  int rc = P->run();
+  if (rc == 0) rc = P->wait();
+  const int res = rc == 0 ? P->result : -1;
+  if (rc != 0) dpl_set_error(("native " + P->name + ": kernel launch failed").c_str());
+  (void)ctx;
+  delete P;
+  return res;
+}
+
+dplasma_taskpool_t* nat_wrap(NatProgram* P) {
+  if (!P) return nullptr;
+  dplasma_taskpool_t* tp = new dplasma_taskpool_s;
+  tp->nat = P;
+  return tp;
+}
+
+int nat_unsupported(const char* op) {
+  dpl_set_error((std::string(op) + ": not available on a native context (dplasma_init_native)").c_str());
+  return -1;
+}
+
+bool dpl_native(const dplasma_context_t* ctx) { return ctx && ctx->nat; }
+
+extern "C" {
+
+DPL_CAPI dplasma_context_t* dplasma_init_native(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+    dpl_set_error("dplasma_init_native: no such GPU");
+    return nullptr;
+  }
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  NatCtx* c = new NatCtx;
+  c->device = device;
+  int lo = 0, hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+  if (hipStreamCreateWithPriority(&c->st[0], hipStreamNonBlocking, hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->st[1], hipStreamNonBlocking, lo) != hipSuccess ||
+      hipEventCreateWithFlags(&c->join[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->join[1], hipEventDisableTiming) != hipSuccess) {
+    dpl_set_error("dplasma_init_native: stream creation failed");
+    delete c;
+    return nullptr;
+  }
+  dplasma_context_t* ctx = new dplasma_context_s;
+  ctx->nat = c;
+  return ctx;
+}
+
+}  // extern "C"
+
+void nat_fini(dplasma_context_t* ctx) {
+  NatCtx* c = ctx->nat;
+  for (int s = 0; s < 2; ++s) {
+    if (c->st[s]) {
+      (void)hipStreamSynchronize(c->st[s]);
+      (void)hipStreamDestroy(c->st[s]);
+    }
+    if (c->join[s]) (void)hipEventDestroy(c->join[s]);
+  }
+  delete c;
+}
+
+dplasma_desc_t* nat_desc(dplasma_context_t* ctx, int prec, int mb, int nb, int m, int n, int P, int Q, void* data,
+                         int lld, int on_device) {
+  if (!prec_ok(prec) || mb <= 0 || nb <= 0 || m < 0 || n < 0 || P > 1 || Q > 1) {
+    dpl_set_error("native descriptor: one process (P = Q = 1), positive tile sizes, s/d/c/z");
+    return nullptr;
+  }
+  if (data && !on_device) {
+    dpl_set_error("native descriptor: caller memory must be device memory of the context's GPU");
+    return nullptr;
+  }
+  NatDesc* d = new NatDesc;
+  d->ctx = ctx->nat;
+  d->prec = prec;
+  d->es = esize(prec);
+  d->mb = mb;
+  d->nb = nb;
+  d->m = m;
+  d->n = n;
+  d->mt = (m + mb - 1) / mb;
+  d->nt = (n + nb - 1) / nb;
+  if (data) {
+    if (lld < std::max(1, m)) {
+      delete d;
+      dpl_set_error("native descriptor: lld < m");
+      return nullptr;
+    }
+    d->data = (char*)data;
+    d->lld = lld;
+  } else {
+    d->lld = std::max(16, (m + 15) / 16 * 16);   // 128-byte aligned columns for the vector paths
+    void* p = nullptr;
+    const size_t bytes = (size_t)d->lld * std::max(1, n) * d->es;
+    if (hipMalloc(&p, bytes) != hipSuccess || hipMemset(p, 0, bytes) != hipSuccess) {
+      delete d;
+      dpl_set_error("native descriptor: device allocation failed");
+      return nullptr;
+    }
+    d->data = (char*)p;
+    d->owned = true;
+  }
+  dplasma_desc_t* h = new dplasma_desc_s;
+  h->nat = d;
+  return h;
+}
+
+void nat_desc_free(dplasma_desc_t* A) { delete A->nat; }
+
+int nat_desc_io(const dplasma_desc_t* A, void* host, int lda, bool to_device) {
+  const NatDesc* d = A->nat;
+  if (lda < std::max(1, d->m)) return nat_unsupported("desc_set/get_lapack: lda < m");
+  for (int s = 0; s < 2; ++s)
+    if (hipStreamSynchronize(d->ctx->st[s]) != hipSuccess) return -1;
+  const size_t w = (size_t)d->m * d->es;
+  if (w == 0 || d->n == 0) return 0;
+  const hipError_t e = to_device ? hipMemcpy2D(d->data, (size_t)d->lld * d->es, host, (size_t)lda * d->es, w, d->n,
+                                               hipMemcpyHostToDevice)
+                                 : hipMemcpy2D(host, (size_t)lda * d->es, d->data, (size_t)d->lld * d->es, w, d->n,
+                                               hipMemcpyDeviceToHost);
+  return e == hipSuccess ? 0 : -1;
+}
+
+int nat_add(dplasma_context_t* ctx, dplasma_taskpool_t* tp) {
+  if (!tp->nat || tp->nat->ctx != ctx->nat) return nat_unsupported("add_taskpool: taskpool of another context");
+  ctx->nat->queue.push_back(tp->nat);
+  return 0;
+}
+
+int nat_start(dplasma_context_t* ctx) {
+  for (NatProgram* P : ctx->nat->queue)
+    if (!P->enqueued && P->run() != 0) return -1;
+  return 0;
+}
+
+int nat_wait(dplasma_context_t* ctx) {
+  int rc = nat_start(ctx);
+  for (NatProgram* P : ctx->nat->queue)
+    if (P->enqueued && P->wait() != 0) rc = -1;
+  ctx->nat->queue.clear();
+  return rc;
+}
+
+int nat_result(const dplasma_taskpool_t* tp) { return tp->nat->result; }
+
+void nat_free(dplasma_taskpool_t* tp) {
+  if (tp->nat->enqueued) (void)tp->nat->wait();
+  delete tp->nat;
+}

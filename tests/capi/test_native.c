@@ -1,0 +1,291 @@
+/* Interpreter-free C ABI (dplasma_init_native, capi/native.cpp) on one GPU: Cholesky / solve / GEMM /
+ * TRSM against host reference arithmetic, the taskpool lifecycle, an unsupported call, and a
+ * check that the embedded interpreter was never started.
+ * usage: test_native [N_bench]   (N_bench > 0: also time dpotrf at N_bench, NB = 512) */
+#include <complex.h>
+#include <execinfo.h>
+#include <math.h>
+#include <signal.h>
+#include <unistd.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "dplasma.h"
+
+static int fails = 0;
+#define CHECK(c, ...)                         \
+  do {                                        \
+    if (!(c)) {                               \
+      printf("FAIL %s:%d ", __FILE__, __LINE__); \
+      printf(__VA_ARGS__);                    \
+      printf("\n");                           \
+      fails++;                                \
+    }                                         \
+  } while (0)
+
+static double now(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
+static dplasma_desc_t *dmat(dplasma_context_t *ctx, int prec, int nb, int m, int n) {
+  dplasma_desc_t *A = dplasma_desc_block_cyclic(ctx, prec, nb, nb, m, n, 1, 1, dplasmaUpperLower);
+  if (!A) printf("desc: %s\n", dplasma_last_error());
+  return A;
+}
+
+/* ||A0 - L L^T||_max / (n ||A0||_max) on the lower triangle (A0 lower holds the input) */
+static double chol_resid_d(const double *A0, const double *L, int n) {
+  double err = 0, nrm = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = j; i < n; ++i) {
+      double s = 0;
+      for (int k = 0; k <= j; ++k) s += L[i + (size_t)k * n] * L[j + (size_t)k * n];
+      err = fmax(err, fabs(A0[i + (size_t)j * n] - s));
+      nrm = fmax(nrm, fabs(A0[i + (size_t)j * n]));
+    }
+  return err / (n * nrm);
+}
+
+static void test_dpotrf_posv(dplasma_context_t *ctx) {
+  const int n = 1200, nb = 256, nrhs = 70;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, n, n);
+  dplasma_desc_t *B = dmat(ctx, dplasmaRealDouble, nb, n, nrhs);
+  double *A0 = malloc(sizeof(double) * n * n), *L = malloc(sizeof(double) * n * n);
+  double *B0 = malloc(sizeof(double) * n * nrhs), *X = malloc(sizeof(double) * n * nrhs);
+  CHECK(A && B, "descriptors");
+  CHECK(dplasma_dplghe(ctx, (double)n, dplasmaLower, A, 3872) == 0, "dplghe: %s", dplasma_last_error());
+  CHECK(dplasma_desc_get_lapack(A, A0, n) == 0, "get A0");
+  int info = dplasma_dpotrf(ctx, dplasmaLower, A);
+  CHECK(info == 0, "dpotrf info %d (%s)", info, dplasma_last_error());
+  dplasma_desc_get_lapack(A, L, n);
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < j; ++i) L[i + (size_t)j * n] = 0.0;
+  const double r = chol_resid_d(A0, L, n);
+  printf("dpotrf n=%d nb=%d residual %.3e\n", n, nb, r);
+  CHECK(r < 1e-14, "dpotrf residual %.3e", r);
+
+  /* posv on a fresh copy of A: A0 x = b */
+  CHECK(dplasma_dplghe(ctx, (double)n, dplasmaLower, A, 3872) == 0, "dplghe 2");
+  CHECK(dplasma_dplrnt(ctx, 0, B, 51) == 0, "dplrnt: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(B, B0, n);
+  info = dplasma_dposv(ctx, dplasmaLower, A, B);
+  CHECK(info == 0, "dposv info %d (%s)", info, dplasma_last_error());
+  dplasma_desc_get_lapack(B, X, n);
+  double err = 0, bn = 0;
+  for (int c = 0; c < nrhs; ++c)
+    for (int i = 0; i < n; ++i) {
+      double s = 0;
+      for (int k = 0; k < n; ++k) {
+        const double a = i >= k ? A0[i + (size_t)k * n] : A0[k + (size_t)i * n];
+        s += a * X[k + (size_t)c * n];
+      }
+      err = fmax(err, fabs(s - B0[i + (size_t)c * n]));
+      bn = fmax(bn, fabs(B0[i + (size_t)c * n]));
+    }
+  printf("dposv n=%d nrhs=%d ||Ax-b||/||b|| %.3e\n", n, nrhs, err / bn);
+  CHECK(err / bn < 1e-12, "dposv residual %.3e", err / bn);
+  free(A0), free(L), free(B0), free(X);
+  dplasma_desc_destroy(A);
+  dplasma_desc_destroy(B);
+}
+
+static void test_dgemm(dplasma_context_t *ctx) {
+  const int M = 300, N = 200, K = 250, nb = 128;
+  /* C = alpha A^T B + beta C, A is K x M */
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, K, M), *B = dmat(ctx, dplasmaRealDouble, nb, K, N);
+  dplasma_desc_t *C = dmat(ctx, dplasmaRealDouble, nb, M, N);
+  dplasma_dplrnt(ctx, 0, A, 1);
+  dplasma_dplrnt(ctx, 0, B, 2);
+  dplasma_dplrnt(ctx, 0, C, 3);
+  double *a = malloc(sizeof(double) * K * M), *b = malloc(sizeof(double) * K * N), *c = malloc(sizeof(double) * M * N);
+  double *r = malloc(sizeof(double) * M * N);
+  dplasma_desc_get_lapack(A, a, K);
+  dplasma_desc_get_lapack(B, b, K);
+  dplasma_desc_get_lapack(C, c, M);
+  const double alpha = 1.5, beta = -0.5;
+  CHECK(dplasma_dgemm(ctx, dplasmaTrans, dplasmaNoTrans, alpha, A, B, beta, C) == 0, "dgemm: %s",
+        dplasma_last_error());
+  dplasma_desc_get_lapack(C, r, M);
+  double err = 0;
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i < M; ++i) {
+      double s = 0;
+      for (int k = 0; k < K; ++k) s += a[k + (size_t)i * K] * b[k + (size_t)j * K];
+      err = fmax(err, fabs(alpha * s + beta * c[i + (size_t)j * M] - r[i + (size_t)j * M]));
+    }
+  printf("dgemm TN %dx%dx%d max error %.3e\n", M, N, K, err);
+  CHECK(err < 1e-12, "dgemm error %.3e", err);
+  free(a), free(b), free(c), free(r);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(B), dplasma_desc_destroy(C);
+}
+
+/* op(T) X = alpha B (left) / X op(T) = alpha B (right) for the given variant; T = plghe (well conditioned) */
+static void test_dtrsm(dplasma_context_t *ctx, int side, int uplo, int trans) {
+  const int n = 400, nrhs = 150, nb = 128;
+  const int bm = side == dplasmaLeft ? n : nrhs, bn = side == dplasmaLeft ? nrhs : n;
+  dplasma_desc_t *T = dmat(ctx, dplasmaRealDouble, nb, n, n), *B = dmat(ctx, dplasmaRealDouble, nb, bm, bn);
+  dplasma_dplghe(ctx, (double)n, dplasmaUpperLower, T, 7);
+  dplasma_dplrnt(ctx, 0, B, 8);
+  double *t = malloc(sizeof(double) * n * n), *b0 = malloc(sizeof(double) * bm * bn), *x = malloc(sizeof(double) * bm * bn);
+  dplasma_desc_get_lapack(T, t, n);
+  dplasma_desc_get_lapack(B, b0, bm);
+  const double alpha = 2.0;
+  CHECK(dplasma_dtrsm(ctx, side, uplo, trans, dplasmaNonUnit, alpha, T, B) == 0, "dtrsm: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(B, x, bm);
+  /* op(T) element (i, k) of the triangle */
+#define TR(i, k) (((uplo == dplasmaLower) ? ((i) >= (k)) : ((i) <= (k))) ? t[(i) + (size_t)(k) * n] : 0.0)
+#define OPT(i, k) (trans == dplasmaNoTrans ? TR(i, k) : TR(k, i))
+  double err = 0;
+  for (int j = 0; j < bn; ++j)
+    for (int i = 0; i < bm; ++i) {
+      double s = 0;
+      if (side == dplasmaLeft)
+        for (int k = 0; k < n; ++k) s += OPT(i, k) * x[k + (size_t)j * bm];
+      else
+        for (int k = 0; k < n; ++k) s += x[i + (size_t)k * bm] * OPT(k, j);
+      err = fmax(err, fabs(s - alpha * b0[i + (size_t)j * bm]));
+    }
+#undef OPT
+#undef TR
+  printf("dtrsm side=%d uplo=%d trans=%d residual %.3e\n", side, uplo, trans, err);
+  CHECK(err < 1e-10, "dtrsm residual %.3e", err);
+  free(t), free(b0), free(x);
+  dplasma_desc_destroy(T), dplasma_desc_destroy(B);
+}
+
+static void test_zpotrf_spotrf(dplasma_context_t *ctx) {
+  const int n = 300, nb = 128;
+  dplasma_desc_t *A = dmat(ctx, dplasmaComplexDouble, nb, n, n);
+  double complex *A0 = malloc(sizeof(double complex) * n * n), *L = malloc(sizeof(double complex) * n * n);
+  CHECK(dplasma_zplghe(ctx, (double)n, dplasmaLower, A, 11) == 0, "zplghe: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(A, A0, n);
+  int info = dplasma_zpotrf(ctx, dplasmaLower, A);
+  CHECK(info == 0, "zpotrf info %d (%s)", info, dplasma_last_error());
+  dplasma_desc_get_lapack(A, L, n);
+  double err = 0, nrm = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = j; i < n; ++i) {
+      double complex s = 0;
+      for (int k = 0; k <= j; ++k) s += L[i + (size_t)k * n] * conj(L[j + (size_t)k * n]);
+      err = fmax(err, cabs(A0[i + (size_t)j * n] - s));
+      nrm = fmax(nrm, cabs(A0[i + (size_t)j * n]));
+    }
+  printf("zpotrf n=%d residual %.3e\n", n, err / (n * nrm));
+  CHECK(err / (n * nrm) < 1e-14, "zpotrf residual");
+  free(A0), free(L);
+  dplasma_desc_destroy(A);
+
+  dplasma_desc_t *S = dmat(ctx, dplasmaRealFloat, nb, n, n);
+  float *s0 = malloc(sizeof(float) * n * n), *sl = malloc(sizeof(float) * n * n);
+  dplasma_splghe(ctx, (double)n, dplasmaUpper, S, 12);
+  dplasma_desc_get_lapack(S, s0, n);
+  info = dplasma_spotrf(ctx, dplasmaUpper, S);
+  CHECK(info == 0, "spotrf info %d (%s)", info, dplasma_last_error());
+  dplasma_desc_get_lapack(S, sl, n);
+  err = 0, nrm = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i <= j; ++i) {   /* A = U^T U on the upper triangle */
+      double s = 0;
+      for (int k = 0; k <= i; ++k) s += (double)sl[k + (size_t)i * n] * sl[k + (size_t)j * n];
+      err = fmax(err, fabs(s0[i + (size_t)j * n] - s));
+      nrm = fmax(nrm, fabs(s0[i + (size_t)j * n]));
+    }
+  printf("spotrf upper n=%d residual %.3e\n", n, err / (n * nrm));
+  CHECK(err / (n * nrm) < 1e-6, "spotrf residual");
+  free(s0), free(sl);
+  dplasma_desc_destroy(S);
+}
+
+static void test_taskpools(dplasma_context_t *ctx) {
+  const int n = 1024, nb = 256;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, n, n), *B = dmat(ctx, dplasmaRealDouble, nb, n, n);
+  dplasma_dplghe(ctx, (double)n, dplasmaLower, A, 5);
+  dplasma_dplghe(ctx, (double)n, dplasmaLower, B, 5);
+  /* make B indefinite at column 700: info = 701 */
+  double *h = malloc(sizeof(double) * n * n);
+  dplasma_desc_get_lapack(B, h, n);
+  h[700 + (size_t)700 * n] = -1.0e6;
+  dplasma_desc_set_lapack(B, h, n);
+  dplasma_taskpool_t *t1 = dplasma_dpotrf_New(ctx, dplasmaLower, A), *t2 = dplasma_dpotrf_New(ctx, dplasmaLower, B);
+  CHECK(t1 && t2, "dpotrf_New: %s", dplasma_last_error());
+  dplasma_context_add_taskpool(ctx, t1);
+  dplasma_context_add_taskpool(ctx, t2);
+  CHECK(dplasma_context_start(ctx) == 0, "start");
+  CHECK(dplasma_context_wait(ctx) == 0, "wait");
+  CHECK(dplasma_taskpool_result(t1) == 0, "t1 info %d", dplasma_taskpool_result(t1));
+  CHECK(dplasma_taskpool_result(t2) == 701, "t2 info %d (expected 701)", dplasma_taskpool_result(t2));
+  printf("taskpools: info %d, %d\n", dplasma_taskpool_result(t1), dplasma_taskpool_result(t2));
+  /* re-run a built taskpool on a fresh matrix */
+  dplasma_dplghe(ctx, (double)n, dplasmaLower, A, 5);
+  dplasma_context_add_taskpool(ctx, t1);
+  dplasma_context_wait(ctx);
+  CHECK(dplasma_taskpool_result(t1) == 0, "t1 rerun");
+  dplasma_dpotrf_Destruct(t1);
+  dplasma_dpotrf_Destruct(t2);
+  free(h);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(B);
+}
+
+static void bench(dplasma_context_t *ctx, int n) {
+  const int nb = 512;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, n, n);
+  dplasma_desc_t *A0 = dmat(ctx, dplasmaRealDouble, nb, n, n);
+  dplasma_dplghe(ctx, (double)n, dplasmaLower, A0, 3872);
+  dplasma_taskpool_t *tp = dplasma_dpotrf_New(ctx, dplasmaLower, A);
+  const double fl = (double)n * n * n / 3.0 + (double)n * n / 2.0 + n / 6.0;
+  for (int r = 0; r < 4; ++r) {
+    dplasma_dplghe(ctx, (double)n, dplasmaLower, A, 3872);
+    const double t0 = now();
+    dplasma_context_add_taskpool(ctx, tp);
+    dplasma_context_wait(ctx);
+    const double t = now() - t0;
+    printf("[****] TIME(s) %12.5f : dpotrf native N= %d NB= %d : %14.3f gflops info=%d\n", t, n, nb, fl / t / 1e9,
+           dplasma_taskpool_result(tp));
+  }
+  dplasma_dpotrf_Destruct(tp);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(A0);
+}
+
+static void on_fault(int sig) {
+  void *fr[64];
+  const int n = backtrace(fr, 64);
+  dprintf(2, "fatal signal %d, backtrace:\n", sig);
+  backtrace_symbols_fd(fr, n, 2);
+  _exit(128 + sig);
+}
+
+int main(int argc, char **argv) {
+  setvbuf(stdout, NULL, _IONBF, 0);
+  signal(SIGSEGV, on_fault);
+  dplasma_context_t *ctx = dplasma_init_native(0);
+  if (!ctx) {
+    printf("dplasma_init_native failed: %s\n", dplasma_last_error());
+    return 2;
+  }
+  CHECK(dplasma_context_world(ctx) == 1 && dplasma_context_rank(ctx) == 0, "rank/world");
+  printf("native context up\n");
+  test_dpotrf_posv(ctx);
+  test_dgemm(ctx);
+  test_dtrsm(ctx, dplasmaLeft, dplasmaLower, dplasmaNoTrans);
+  test_dtrsm(ctx, dplasmaLeft, dplasmaUpper, dplasmaTrans);
+  test_dtrsm(ctx, dplasmaRight, dplasmaUpper, dplasmaNoTrans);
+  test_dtrsm(ctx, dplasmaRight, dplasmaLower, dplasmaTrans);
+  test_zpotrf_spotrf(ctx);
+  test_taskpools(ctx);
+  /* an operation without a native implementation fails cleanly */
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
+  CHECK(dplasma_dgeqrf(ctx, A, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");
+  dplasma_desc_destroy(A);
+  if (argc > 1 && atoi(argv[1]) > 0) bench(ctx, atoi(argv[1]));
+  CHECK(dplasma_python_active() == 0, "the interpreter was started");
+  dplasma_fini(ctx);
+  if (fails)
+    printf("native C ABI: %d FAILED\n", fails);
+  else
+    printf("native C ABI: all passed\n");
+  return fails ? 1 : 0;
+}

@@ -96,3 +96,35 @@ def test_capi_exports():
               "pdgemm_", "pdpotrf_", "pdgetrf_", "pdtrsm_", "pdtrmm_", "pdlatsqr_", "pzgemm_", "pspotrf_",
               "parsec_init_wrapper_", "parsec_fini_wrapper_", "numroc_", "descinit_"):
         assert s in syms, s
+
+
+def _build_native(tmp_path):
+    _build(tmp_path)
+    exe = str(tmp_path / "test_native")
+    subprocess.run(["gcc", "-O2", "-o", exe, os.path.join(ROOT, "tests", "capi", "test_native.c"),
+                    "-I" + os.path.join(ROOT, "capi", "include"), "-L" + LIB, "-ldplasma", "-lm",
+                    "-Wl,-rpath," + LIB], check=True)
+    return exe
+
+
+def test_capi_native_no_gpu(tmp_path):
+    """dplasma_init_native without a GPU fails cleanly (no interpreter started, error message kept)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present: covered by test_capi_native_gpu")
+    env = dict(os.environ)
+    env.pop("PYTHONPATH", None)
+    r = subprocess.run([_build_native(tmp_path)], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 2, r.stdout + r.stderr
+    assert "dplasma_init_native failed" in r.stdout
+
+
+@pytest.mark.gpu
+def test_capi_native_gpu(tmp_path):
+    """Interpreter-free C ABI on one GPU (capi/native.cpp): potrf / posv / gemm / 4 trsm variants / z and s
+    potrf / taskpool lifecycle against host arithmetic; dplasma_python_active() stays 0."""
+    env = dict(os.environ)
+    env.pop("PYTHONPATH", None)
+    r = subprocess.run([_build_native(tmp_path)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "native C ABI: all passed" in r.stdout

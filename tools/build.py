@@ -103,13 +103,17 @@ def build_capi(force=False) -> Path | None:
     if not srcs:
         return None
     lib = OUT / "libdplasma.so"
-    if not force and not _newer(lib, [*srcs, *csrc.glob("*.h")]):
+    kern = OUT / "libdplasma_kernels.so"
+    if not force and not _newer(lib, [*srcs, *csrc.glob("*.h"), kern]):
         return lib
     pyinc = sysconfig.get_paths()["include"]
     libdir = sysconfig.get_config_var("LIBDIR") or "/usr/lib"
     ver = sysconfig.get_config_var("LDVERSION") or sysconfig.get_python_version()
-    _run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", f"-I{pyinc}", f"-I{csrc}",
-          *map(str, srcs), "-o", str(lib), f"-L{libdir}", f"-lpython{ver}", "-ldl", f"-Wl,-rpath,{libdir}"])
+    # native.cpp (interpreter-free engine) calls the HIP runtime and the kernel library directly
+    _run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-D__HIP_PLATFORM_AMD__",
+          f"-I{pyinc}", f"-I{csrc}", "-I/opt/rocm/include", *map(str, srcs), "-o", str(lib), f"-L{libdir}",
+          f"-lpython{ver}", f"-L{OUT}", "-ldplasma_kernels", "-L/opt/rocm/lib", "-lamdhip64", "-ldl",
+          f"-Wl,-rpath,{libdir}", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath,/opt/rocm/lib"])
     print(f"[build] linked {lib.relative_to(ROOT)}", flush=True)
     return lib
 
