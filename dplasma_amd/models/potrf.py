@@ -134,8 +134,12 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
     tile_kind = os.environ.get("DPLASMA_POTRF_TILE", POTRF_TILE)
     if tile_kind not in ("auto", "single", "blocked"):
         raise ValueError(f"DPLASMA_POTRF_TILE={tile_kind!r}: expected auto, single or blocked")
-    potrf_diag = ops.potrf_tile_blocked if tile_kind == "blocked" or (tile_kind == "auto" and distributed) \
-        else ops.potrf_tile
+    # auto: the single-workgroup tile kernel only where nothing better exists -- fp64 uses the dataflow
+    # kernel (use_rb below); distributed runs and the other precisions take nb-wide MFMA sub-steps
+    # (a complex 512 tile on one workgroup is ~10 ms: zpotrf 32k 33.0 -> 47.2 TF/s with sub-steps,
+    # profiles/r2_zpotrf_tile.txt)
+    potrf_diag = ops.potrf_tile_blocked if tile_kind == "blocked" or (
+        tile_kind == "auto" and (distributed or A.dtype != torch.float64)) else ops.potrf_tile
 
     # block partition of the tile columns
     blocks = []
