@@ -486,7 +486,13 @@ static inline void qp_layout(long long es, int nc, int kf, long long off[6]) {
   off[5] = off[4] + qp_align(es * nblk * QP_B * kf);
 }
 
+// complex precisions: qr_panel_z.hip (16-column blocks, VALU block products)
+DPL_API long long dpl_qr_panel_z_ws_bytes(int prec, int nc, int kf);
+DPL_API int dpl_qr_panel_z(int prec, void* P, int ldp, int rbl, long long rstride, int M, int nc, int kf, void* V,
+                           int ldv, void* Tm, int ldt, void* ws, int* info, hipStream_t st);
+
 DPL_API long long dpl_qr_panel_ws_bytes(int prec, int nc, int kf) {
+  if (prec == DPL_Z || prec == DPL_C) return dpl_qr_panel_z_ws_bytes(prec, nc, kf);
   long long off[6];
   qp_layout(prec == DPL_D ? 8 : 4, nc, kf, off);
   return off[5] + 256;
@@ -500,6 +506,7 @@ DPL_API int dpl_qr_panel_max_rows() { return qp_cus() * QP_R; }
 DPL_API int dpl_qr_panel(int prec, void* P, int ldp, int rbl, long long rstride, int M, int nc, int kf, void* V,
                          int ldv, void* Tm, int ldt, void* ws, int* info, hipStream_t st) {
   if (kf <= 0) return 0;
+  if (prec == DPL_Z || prec == DPL_C) return dpl_qr_panel_z(prec, P, ldp, rbl, rstride, M, nc, kf, V, ldv, Tm, ldt, ws, info, st);
   if (prec != DPL_D && prec != DPL_S) return -2;
   if (rbl <= 0 || rbl >= M) {
     rbl = 1 << 30;
@@ -562,6 +569,11 @@ __global__ __launch_bounds__(256) void k_sum_partials(const T* __restrict__ src,
 DPL_API int dpl_sum_partials(int prec, const void* src, long long stride, int S, long long L, void* dst,
                              hipStream_t st) {
   if (L <= 0 || S <= 0) return 0;
+  if (prec == DPL_Z || prec == DPL_C) {   // complex sums are sums of (re, im) pairs
+    prec = prec == DPL_Z ? DPL_D : DPL_S;
+    stride *= 2;
+    L *= 2;
+  }
   const unsigned nblk = (unsigned)((L + 511) / 512);
   if (prec == DPL_D)
     hipLaunchKernelGGL((k_sum_partials<double>), dim3(nblk), dim3(256), 0, st, (const double*)src, stride, S, L,

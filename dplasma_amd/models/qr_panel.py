@@ -51,7 +51,8 @@ from ..runtime.taskpool import Taskpool
 from ..utils.flops import flops
 from . import qrtree
 
-N_, T_ = dplasmaNoTrans, dplasmaTrans
+# T_ is the adjoint: V^H / T^H for complex (the GEMM engine treats ConjTrans as Trans for real types)
+N_, T_ = dplasmaNoTrans, dplasmaConjTrans
 PART_FULL, PART_UPPER, PART_SLOWER, PART_DIAG = 0, 2, 3, 5
 
 _ENGINE = [os.environ.get("DPLASMA_QR_ENGINE", "panel")]
@@ -98,7 +99,7 @@ def usable(A, tree=None) -> bool:
     """The stacked-domain engine handles this factorisation (and therefore owns its format)."""
     if _ENGINE[0] != "panel":
         return False
-    if A.dtype not in (torch.float32, torch.float64):
+    if A.dtype not in (torch.float32, torch.float64, torch.complex64, torch.complex128):
         return False
     if A.grid.kq != 1 or A.mb != A.nb or A.nb > ops.QR_PANEL_MAXW:
         return False

@@ -704,7 +704,7 @@ def _larft_cpu(V: torch.Tensor, tau: torch.Tensor) -> torch.Tensor:
     """Compact-WY T (upper triangular, dlarft forward/columnwise) of explicit reflectors V."""
     k = V.shape[1]
     T = torch.zeros(k, k, dtype=V.dtype)
-    G = V.T @ V
+    G = V.mH @ V
     for j in range(k):
         T[j, j] = tau[j]
         if j:
@@ -724,9 +724,9 @@ def sum_partials(src: torch.Tensor, stride: int, S: int, L: int, dst: torch.Tens
 
 def qr_panel(P: torch.Tensor, ldp: int, M: int, nc: int, kf: int, V: torch.Tensor, ldv: int, Tm: torch.Tensor,
              ldt: int, ws: torch.Tensor, info: torch.Tensor, rbl: int = 0, rstride: int = 0, poff: int = 0):
-    """Householder QR of the column-major M x nc panel P (ld ldp), first kf columns (real precisions).
+    """Householder QR of the column-major M x nc panel P (ld ldp), first kf columns (s/d/c/z).
 
-    P := R (upper) + V (strictly lower) with the remaining nc - kf columns updated by Q^T;
+    P := R (upper) + V (strictly lower) with the remaining nc - kf columns updated by Q^H;
     V := the kf reflectors explicitly (unit diagonal, zeros above); Tm(0:kf, 0:kf) := the
     compact-WY T (upper part; the strictly lower part is not written).  GPU: one persistent
     launch (csrc/kernels/qr_panel.hip); CPU: LAPACK geqrf through torch + dlarft.
@@ -758,7 +758,7 @@ def qr_panel(P: torch.Tensor, ldp: int, M: int, nc: int, kf: int, V: torch.Tenso
     Vx = torch.tril(a, -1) + torch.eye(M, kf, dtype=P.dtype)
     T = _larft_cpu(Vx, tau)
     if nc > kf:
-        A[:, kf:] -= Vx @ (T.T @ (Vx.T @ A[:, kf:]))
+        A[:, kf:] -= Vx @ (T.mH @ (Vx.mH @ A[:, kf:]))
     A[:, :kf] = a
     torch.as_strided(V, (M, kf), (1, ldv), 0).copy_(Vx)
     tv = torch.as_strided(Tm, (kf, kf), (1, ldt), 0)
