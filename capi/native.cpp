@@ -355,14 +355,51 @@ bool add_potrf(NatProgram& P, int uplo, NatDesc& A) {
       const long long dk = A.off(k, k);
       double* zk = rb ? (double*)zb->p + (size_t)(k % 2) * zsz : nullptr;
       int t_potrf;
-      if (rb)
+      if (rb) {
         t_potrf = P.task(0, [=](hipStream_t s) {
           return dpl_potrf_tile_rbz(uplo, kb, (double*)base + dk, ld, info, k * mbA, zk, s);
         }, {gate});
-      else
-        t_potrf = P.task(0, [=](hipStream_t s) {
-          return dpl_potrf_tile(prec, uplo, kb, base, dk, ld, info, k * mbA, s);
-        }, {gate});
+      } else {
+        // other precisions: nb-wide sub-steps (tile POTRF, batched TRSM, masked MFMA GEMM) as
+        // ops.potrf_tile_blocked -- a single workgroup on a whole complex 512 tile is ~10 ms
+        const int sb = 128;
+        auto at = [&](int i, int j) { return dk + (lower ? (long long)i + (long long)j * ld : (long long)j + (long long)i * ld); };
+        int prev = gate;
+        for (int j0 = 0; j0 < kb; j0 += sb) {
+          const int jb = std::min(sb, kb - j0);
+          const long long dj = at(j0, j0);
+          prev = P.task(0, [=](hipStream_t s) {
+            return dpl_potrf_tile(prec, uplo, jb, base, dj, ld, info, k * mbA + j0, s);
+          }, {prev});
+          if (j0 + jb >= kb) break;
+          auto tr = std::make_shared<Trsm1>();
+          tr->tri = dj;
+          auto g = std::make_shared<Gemm>();
+          for (int i0 = j0 + jb; i0 < kb; i0 += sb) {
+            const int ib = std::min(sb, kb - i0);
+            if (lower) tr->add(at(i0, j0), ib, jb);
+            else tr->add(at(i0, j0), jb, ib);
+          }
+          for (int c0_ = j0 + jb; c0_ < kb; c0_ += sb) {
+            const int cbw = std::min(sb, kb - c0_);
+            for (int r0 = c0_; r0 < kb; r0 += sb) {
+              const int rbw = std::min(sb, kb - r0);
+              const int mask = r0 == c0_ ? tri_mask : 0;
+              if (lower)   // C(r, c) -= L(r, j) L(c, j)^H
+                g->add(at(r0, c0_), rbw, cbw, {KPair{at(r0, j0), at(c0_, j0), jb, 0}}, mask);
+              else         // C(c, r) -= U(j, c)^H U(j, r)
+                g->add(at(r0, c0_), cbw, rbw, {KPair{at(c0_, j0), at(r0, j0), jb, 0}}, mask);
+            }
+          }
+          const int side = lower ? RIGHT : LEFT;
+          if (!tr->upload(P, prec, side) || !g->upload(P)) return false;
+          prev = P.task(0, [=](hipStream_t s) {
+            return tr->launch(prec, side, uplo, CONJTRANS, NONUNIT, one, base, ld, base, ld, s);
+          }, {prev});
+          prev = P.task(0, gemm_task(g), {prev});
+        }
+        t_potrf = prev;
+      }
       int t_trsm = t_potrf;
       if (k + 1 < nt) {
         if (rb) {

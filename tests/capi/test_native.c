@@ -158,7 +158,8 @@ static void test_dtrsm(dplasma_context_t *ctx, int side, int uplo, int trans) {
 }
 
 static void test_zpotrf_spotrf(dplasma_context_t *ctx) {
-  const int n = 300, nb = 128;
+  /* tiles wider than the 128-wide sub-steps of the non-fp64 diagonal tiles, ragged edges */
+  int n = 700, nb = 300;
   dplasma_desc_t *A = dmat(ctx, dplasmaComplexDouble, nb, n, n);
   double complex *A0 = malloc(sizeof(double complex) * n * n), *L = malloc(sizeof(double complex) * n * n);
   CHECK(dplasma_zplghe(ctx, (double)n, dplasmaLower, A, 11) == 0, "zplghe: %s", dplasma_last_error());
@@ -179,6 +180,7 @@ static void test_zpotrf_spotrf(dplasma_context_t *ctx) {
   free(A0), free(L);
   dplasma_desc_destroy(A);
 
+  n = 600, nb = 256;
   dplasma_desc_t *S = dmat(ctx, dplasmaRealFloat, nb, n, n);
   float *s0 = malloc(sizeof(float) * n * n), *sl = malloc(sizeof(float) * n * n);
   dplasma_splghe(ctx, (double)n, dplasmaUpper, S, 12);
