@@ -348,11 +348,10 @@ template <> struct BufLd<float> {
 };
 
 template <typename T, bool TA, bool TB>
-__global__ __launch_bounds__(256, 2) void k_gemm_full(const GemmItemK* __restrict__ items,
-                                                      const KPair* __restrict__ kps, int nsm, int nsn,
-                                                      int nwg, T alpha, const T* __restrict__ A, int lda,
-                                                      const T* __restrict__ B, int ldb, T beta,
-                                                      T* __restrict__ C, int ldc) {
+__device__ __forceinline__ void gemm_full_tile(const int wg, const GemmItemK* __restrict__ items,
+                                               const KPair* __restrict__ kps, int nsm, int nsn, T alpha,
+                                               const T* __restrict__ A, int lda, const T* __restrict__ B,
+                                               int ldb, T beta, T* __restrict__ C, int ldc) {
   typedef MF<T> M_;
   typedef typename M_::acc_t acc_t;
   typedef typename M_::vec_t vec_t;
@@ -362,7 +361,6 @@ __global__ __launch_bounds__(256, 2) void k_gemm_full(const GemmItemK* __restric
   constexpr int OPB_ = GBK * FLS;
   __shared__ T sm[2 * 2 * OPB_];     // [buf][operand][GBK x FLS]
 
-  const int wg = xcd_remap(blockIdx.x, nwg);
   const int per = nsm * nsn;
   const GemmItemK it = items[wg / per];
   const int sub = wg % per;
@@ -595,6 +593,29 @@ __global__ __launch_bounds__(256, 2) void k_gemm_full(const GemmItemK* __restric
   }
 }
 
+// One 128x128 output sub-tile per workgroup (PERSIST = false: grid = every sub-tile), or a capped
+// grid that walks the sub-tiles grid-stride (PERSIST = true, dpl_gemm_set_wg_cap): a bulk update
+// launched that way never holds more than the cap's workgroup slots, so latency-bound critical-path
+// kernels on a high-priority stream find free CUs at once instead of queueing behind ~0.5 ms
+// GEMM workgroups (profiles/r2_potrf16k_timeline.txt).  The cap is a multiple of the 8 XCDs, so a
+// workgroup keeps its XCD's share of xcd_remap's tile order on every pass.
+template <typename T, bool TA, bool TB, bool PERSIST>
+__global__ __launch_bounds__(256, 2) void k_gemm_full(const GemmItemK* __restrict__ items,
+                                                      const KPair* __restrict__ kps, int nsm, int nsn,
+                                                      int nwg, T alpha, const T* __restrict__ A, int lda,
+                                                      const T* __restrict__ B, int ldb, T beta,
+                                                      T* __restrict__ C, int ldc) {
+  if (!PERSIST) {
+    gemm_full_tile<T, TA, TB>(xcd_remap(blockIdx.x, nwg), items, kps, nsm, nsn, alpha, A, lda, B, ldb, beta, C,
+                              ldc);
+    return;
+  }
+  for (int b = blockIdx.x; b < nwg; b += gridDim.x) {
+    gemm_full_tile<T, TA, TB>(xcd_remap(b, nwg), items, kps, nsm, nsn, alpha, A, lda, B, ldb, beta, C, ldc);
+    __syncthreads();   // the next sub-tile's first LDS stores must not overtake this one's last reads
+  }
+}
+
 // ------------------------------------------------------------------ generic
 // 64x64 C tile per 256-thread workgroup, 4x4 outputs per thread, BK=16.
 // OPA/OPB: 0 = N, 1 = T, 2 = C (conjugate transpose).
@@ -688,6 +709,17 @@ __global__ __launch_bounds__(256) void k_gemm_generic(const GemmItemK* __restric
 // ------------------------------------------------------------------ launchers
 static inline int op_code(int trans) { return trans == DPL_NOTRANS ? 0 : (trans == DPL_TRANS ? 1 : 2); }
 
+// Workgroup cap of the next full-tile MFMA launches (0 = none): set around a bulk trailing update
+// by the host program that wants CUs kept free for its critical path.  Host-thread state, like the
+// current stream: the task programs issue from one thread.
+static int g_gemm_wg_cap = 0;
+DPL_API int dpl_gemm_set_wg_cap(int cap) {
+  const int old = g_gemm_wg_cap;
+  g_gemm_wg_cap = cap > 0 ? (cap / 8) * 8 : 0;
+  if (cap > 0 && g_gemm_wg_cap == 0) g_gemm_wg_cap = 8;
+  return old;
+}
+
 template <typename T>
 static int launch_mfma(int opa, int opb, int nitems, const GemmItemK* items, const KPair* kps, int max_m,
                        int max_n, T alpha, const T* A, int lda, const T* B, int ldb, T beta, T* C, int ldc,
@@ -705,10 +737,19 @@ static int launch_mfma(int opa, int opb, int nitems, const GemmItemK* items, con
   dim3 g(nwg), b(256);
   const bool ta = opa != 0, tb = opb != 0;
   if (full) {
-    if (!ta && !tb) hipLaunchKernelGGL((k_gemm_full<T, false, false>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc);
-    else if (!ta && tb) hipLaunchKernelGGL((k_gemm_full<T, false, true>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc);
-    else if (ta && !tb) hipLaunchKernelGGL((k_gemm_full<T, true, false>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc);
-    else hipLaunchKernelGGL((k_gemm_full<T, true, true>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc);
+    const int cap = g_gemm_wg_cap;
+    if (cap > 0 && nwg > cap) {
+      g = dim3(cap);
+      if (!ta && !tb) hipLaunchKernelGGL((k_gemm_full<T, false, false, true>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc);
+      else if (!ta && tb) hipLaunchKernelGGL((k_gemm_full<T, false, true, true>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc);
+      else if (ta && !tb) hipLaunchKernelGGL((k_gemm_full<T, true, false, true>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc);
+      else hipLaunchKernelGGL((k_gemm_full<T, true, true, true>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc);
+      return (int)hipGetLastError();
+    }
+    if (!ta && !tb) hipLaunchKernelGGL((k_gemm_full<T, false, false, false>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc);
+    else if (!ta && tb) hipLaunchKernelGGL((k_gemm_full<T, false, true, false>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc);
+    else if (ta && !tb) hipLaunchKernelGGL((k_gemm_full<T, true, false, false>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc);
+    else hipLaunchKernelGGL((k_gemm_full<T, true, true, false>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc);
     return (int)hipGetLastError();
   }
   if (!ta && !tb) hipLaunchKernelGGL((k_gemm_mfma<T, false, false>), g, b, 0, st, items, kps, nsm, nsn, nwg, alpha, A, lda, B, ldb, beta, C, ldc, vec_ok);

@@ -58,6 +58,10 @@ POTRF_DEFER_MIN_TILES = 24 # below this many trailing tile-columns: plain look-a
 POTRF_TILE = "single"
 POTRF_LOOKAHEAD = 1
 POTRF_TRSM = "rb"   # "fused": the diagonal owner factors its tile and solves its panel strips in one launch
+# CUs kept free of the bulk trailing updates (REST / NEXT2 / REST2 run as capped grid-stride GEMM
+# launches of 2 x (CUs - reserve) workgroups, ops.gemm_wg_cap): the panel chain's kernels find idle
+# CUs instead of waiting for GEMM workgroups to retire.  (single process, distributed)
+POTRF_RESERVE = (0, 0)
 
 
 def _defer_depth(nt_left: int, D: int, min_tiles: int) -> int:
@@ -218,6 +222,16 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
 
     def f_upd(batch, base, ld):
         ops.gemm(tA, tB, -1.0, base, ld, base, ld, 1.0, A.data, A.ld, batch)
+
+    reserve = int(os.environ.get("DPLASMA_POTRF_RESERVE", POTRF_RESERVE[1 if distributed else 0]))
+    bulk_cap = 0
+    if reserve > 0 and ctx.is_gpu:
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        bulk_cap = 2 * max(8, ncu - reserve)      # k_gemm_full holds 2 workgroups per CU
+
+    def f_bulk(batch, base, ld):
+        with ops.gemm_wg_cap(bulk_cap):
+            f_upd(batch, base, ld)
 
     gate = None        # task the next POTRF must follow (NEAR(k-1) or NEXT(b-1))
     last_upd = {}      # block -> last update-stream task reading its panels
@@ -393,7 +407,7 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                                  prio=2)
                 last_upd[b] = t_next
             if len(rest):
-                last_upd[b] = tp.task(f"REST({b})", upd_stream, lambda bt=rest, bs=base, l=ld: f_upd(bt, bs, l),
+                last_upd[b] = tp.task(f"REST({b})", upd_stream, lambda bt=rest, bs=base, l=ld: f_bulk(bt, bs, l),
                                       deps, prio=1)
             # the next block's first POTRF follows NEXT(b) (and, for this rank, the block's NEARs)
             gate = t_next if t_next is not None else gate
@@ -412,10 +426,10 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
         # by REST2(b-1)
         prev_bulk = rest_of.get(b - 1)
         if len(nxt2):
-            nxt2_of[b] = tp.task(f"NEXT2({b})", upd_stream, lambda bt=nxt2, bs=base, l=ld: f_upd(bt, bs, l),
+            nxt2_of[b] = tp.task(f"NEXT2({b})", upd_stream, lambda bt=nxt2, bs=base, l=ld: f_bulk(bt, bs, l),
                                  [gate, last_panel, prev_bulk], prio=1)
         if len(rest):
-            rest_of[b] = tp.task(f"REST2({b})", upd_stream, lambda bt=rest, bs=base, l=ld: f_upd(bt, bs, l),
+            rest_of[b] = tp.task(f"REST2({b})", upd_stream, lambda bt=rest, bs=base, l=ld: f_bulk(bt, bs, l),
                                  [gate, last_panel, prev_bulk, nxt2_of.get(b)], prio=0)
         else:
             rest_of[b] = nxt2_of.get(b, prev_bulk)

@@ -44,6 +44,27 @@ def _is_gpu(t: torch.Tensor) -> bool:
 
 
 # ----------------------------------------------------------------------------- GEMM
+class gemm_wg_cap:
+    """``with gemm_wg_cap(n):`` -- full-tile MFMA GEMM launches issued inside hold at most n workgroup
+    slots (grid-stride over their sub-tiles; 0 = uncapped).  A bulk trailing update launched that way
+    leaves CUs free for the latency-bound critical-path kernels of a high-priority stream
+    (``dpl_gemm_set_wg_cap``, csrc/kernels/gemm.hip).  No effect on the CPU path."""
+
+    def __init__(self, n: int):
+        self.n = int(n)
+        self.old = 0
+
+    def __enter__(self):
+        if self.n > 0 and torch.cuda.is_available():
+            self.old = _lib.load().dpl_gemm_set_wg_cap(self.n)
+        return self
+
+    def __exit__(self, *exc):
+        if self.n > 0 and torch.cuda.is_available():
+            _lib.load().dpl_gemm_set_wg_cap(self.old)
+        return False
+
+
 def gemm(transA: int, transB: int, alpha, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, beta,
          C: torch.Tensor, ldc: int, batch: GemmBatch):
     """For every item: C = beta*C + alpha * sum_k opA(A_k) opB(B_k) (masked to a triangle if asked)."""

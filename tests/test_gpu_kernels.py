@@ -379,3 +379,30 @@ def test_potrf_blocked_tile_kernel(gctx, prec, uplo, dims, monkeypatch):
     assert dp.potrf(gctx, uplo, A) == 0
     ok, res = dp.check_potrf(gctx, uplo, A, A0)
     assert ok, res
+
+
+@pytest.mark.parametrize("prec", list("sd"))
+@pytest.mark.parametrize("ta,tb", [(111, 111), (111, 112), (112, 111), (112, 112)])
+@pytest.mark.parametrize("cap", [8, 24])
+def test_gemm_full_capped_grid(gctx, prec, ta, tb, cap):
+    """Capped grid-stride k_gemm_full (ops.gemm_wg_cap, the bulk-update mode that keeps CUs free for
+    the critical path): each workgroup walks several sub-tiles; the result is bit-identical to the
+    one-sub-tile-per-workgroup launch (same per-tile arithmetic), triangle masks included."""
+    from dplasma_amd.ops.batch import GemmBatch
+    dt = DTYPES[prec]
+    nb, kt = 512, 2
+    torch.manual_seed(11)
+    A = torch.randn(nb * kt * nb, dtype=dt, device="cuda")
+    B = torch.randn(nb * kt * nb, dtype=dt, device="cuda")
+    C = torch.randn(3 * nb * nb, dtype=dt, device="cuda")
+    gb = GemmBatch()
+    for t in range(3):
+        gb.add(t * nb * nb, nb, nb, [(q * nb * nb, ((q + t) % kt) * nb * nb, nb) for q in range(kt)], t % 2)
+    assert gb.full
+    ref = C.clone()
+    ops.gemm(ta, tb, -1.0, A, nb, B, nb, 1.0, ref, nb, gb)
+    with ops.gemm_wg_cap(cap):
+        ops.gemm(ta, tb, -1.0, A, nb, B, nb, 1.0, C, nb, gb)
+    assert _lib.load().dpl_gemm_set_wg_cap(0) == 0      # the context manager restored "uncapped"
+    torch.cuda.synchronize()
+    assert torch.equal(C, ref)
