@@ -146,6 +146,11 @@ register_op("potrf_dtd_untied", _dtdp.potrf_dtd_untied)
 register_op("gemm_dtd", _dtdp.gemm_dtd)
 register_op("gemm_dtd_New", _dtdp.gemm_dtd_New)
 register_op("potrf_dtd_untied_New", _dtdp.potrf_dtd_untied_New)
+# DTD tile QR and incremental-pivoting LU (tests/testing_zgeqrf_dtd[_untied].c, testing_zgetrf_incpiv_dtd.c)
+from .models import dtd_factor as _dtdf  # noqa: E402
+for _n in ("geqrf_dtd", "geqrf_dtd_New", "geqrf_dtd_untied", "geqrf_dtd_untied_New", "getrf_incpiv_dtd",
+           "getrf_incpiv_dtd_New"):
+    register_op(_n, getattr(_dtdf, _n))
 for _n in ("taskpool_new", "tile_of", "INPUT", "OUTPUT", "INOUT", "AFFINITY", "VALUE", "SCRATCH", "PUSHOUT"):
     _register("dtd_" + _n, getattr(dtd, _n))
 _register("dtd", dtd)

@@ -108,6 +108,12 @@ def _sym_diag_copy(prog, A, uplo, Sym, trans_other, name="sym"):
     s = prog.stage(name + "_mirror")
     for k in range(kt):
         s.copy((A, k, k), (Sym, k, k), part=P_SUPPER if uplo == dplasmaLower else P_SLOWER, trans=trans_other)
+    if trans_other == C_ and A.dtype.is_complex:
+        # Hermitian: the imaginary parts of the diagonal are taken as zero (BLAS zhemm / zherk semantics):
+        # diag := (diag + conj(diag)) / 2
+        s = prog.stage(name + "_realdiag")
+        for k in range(kt):
+            s.geadd((Sym, k, k), (Sym, k, k), 0.5, 0.5, part=P_DIAG, trans=C_)
 
 
 # ----------------------------------------------------------------------------- TRMM

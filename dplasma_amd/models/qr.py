@@ -140,6 +140,12 @@ def _apply(dag: TileDAG, X: _L, TS: _L, TT: _L, C: _L, kd, conjtrans: bool, tree
             unm()
 
 
+def _panel_format(A, T, tree):
+    """The apply must use the stacked-domain engine: it can handle A and T was written by it (the tile
+    engines -- PTG-style DAG or DTD -- mark their per-tile TSQRT layout with qr_format = "tile")."""
+    return qr_panel.usable(A, tree) and getattr(T, "qr_format", "panel") == "panel"
+
+
 def _kinds(A, T, logical_t, c_t=None):
     fa = qr_ops.view_flags(A.dtype, logical_t)
     fc = fa if c_t is None else qr_ops.view_flags(A.dtype, c_t)
@@ -162,6 +168,7 @@ def geqrf_New(ctx, A, T) -> Taskpool:
     if qr_panel.usable(A, flat):
         return qr_panel.factor_New(ctx, A, T, T, flat, "geqrf")
     T.full_T = {}   # tile engine: the panel engine's kept T factors no longer describe T
+    T.qr_format = "tile"
     dag = TileDAG(ctx, "geqrf")
     _factor(dag, _L(A), _L(T), _L(T), _kinds(A, T, False), qrtree.FlatTree(A.mt, A.nt))
     dag.flops = flops(A.prec, "geqrf", A.m, A.n)
@@ -215,7 +222,7 @@ def _unm(ctx, name, side, trans, A, T, C, lq: bool, tree=None, TT=None):
     c_t = side == dplasmaRight
     if c_t:
         qh = not qh  # C op(Q) = (op(Q)^H C^H)^H
-    if not lq and qr_panel.usable(A, tree or _flat(A, lq)):
+    if not lq and _panel_format(A, T, tree or _flat(A, lq)):
         return qr_panel.apply_New(ctx, side, trans, A, T, TT if TT is not None else T, C, tree or _flat(A, lq), name)
     X = _L(A, lq)
     dag = TileDAG(ctx, name)
@@ -250,7 +257,7 @@ def unmlq(ctx, side, trans, A, T, C):
 def _ung(ctx, name, A, T, Q, lq: bool, tree=None, TT=None):
     _check_square_tiles(A)
     init = aux.laset_New(ctx, dplasmaUpperLower, 0.0, 1.0, Q)
-    if not lq and qr_panel.usable(A, tree or _flat(A, lq)):
+    if not lq and _panel_format(A, T, tree or _flat(A, lq)):
         app = qr_panel.apply_New(ctx, dplasmaLeft, dplasmaNoTrans, A, T, TT if TT is not None else T, Q,
                                  tree or _flat(A, lq), name)
         app.flops = flops(A.prec, "ungqr", Q.m, Q.n, min(A.m, A.n))
@@ -368,6 +375,7 @@ def geqrf_param_New(ctx, tree, A, TS, TT) -> Taskpool:
     if qr_panel.usable(A, tree):
         return qr_panel.factor_New(ctx, A, TS, TT, tree, "geqrf_param")
     TS.full_T, TT.full_T = {}, {}   # tile engine: drop the panel engine's kept T factors
+    TS.qr_format = TT.qr_format = "tile"
     dag = TileDAG(ctx, "geqrf_param")
     _factor(dag, _L(A), _L(TS), _L(TT), _kinds(A, TS, False), tree)
     dag.flops = flops(A.prec, "geqrf", A.m, A.n)

@@ -497,6 +497,7 @@ def factor_New(ctx, A, TS, TT, tree, name="geqrf") -> Taskpool:
     """Build the taskpool of the stacked-domain QR (see module docstring)."""
     tp = Taskpool(name, ctx)
     tp.flops = flops(A.prec, "geqrf", A.m, A.n)
+    TS.qr_format = TT.qr_format = "panel"
     st = _Factor(ctx, A, TS, TT, tree)
     if st.simple:
         prev_next = prev_rest = prev_rest2 = None

@@ -253,7 +253,9 @@ def t_trmm(h):
         h.check("||B - B_ref|| / (||B_ref|| N eps)", res, 10.0)
 
 
-def _qr_common(h, lq, tree_kind):
+def _qr_common(h, lq, tree_kind, dtd=None):
+    """testing_zgeqrf[_hqr|_systolic|_dtd|_dtd_untied|_rd].c and the LQ twins; dtd: "tied" / "untied" /
+    "rd" (recursive-subtask hint, dplasma_zgeqrf_setrecursive)."""
     dp, a, ctx = h.dp, h.a, h.ctx
     M = a.M or a.N
     N = a.N
@@ -273,12 +275,21 @@ def _qr_common(h, lq, tree_kind):
                            a.qr_p if a.qr_p > 0 else ctx.P, a.domino, a.tsrr)
     elif tree_kind == "systolic":
         tree = dp.systolic_init(trans, A, a.qr_p if a.qr_p > 0 else ctx.P, a.qr_a if a.qr_a > 0 else 1)
-    if tree is None:
+    if dtd in ("tied", "untied"):
+        build = (lambda: dp.geqrf_dtd_New(ctx, A, TS)) if dtd == "tied" else \
+            (lambda: dp.geqrf_dtd_untied_New(ctx, A, TS))
+    elif dtd == "rd":
+        def build():
+            tp = dp.geqrf_New(ctx, A, TS)
+            dp.geqrf_setrecursive(tp, a.HNB or max(1, A.nb // 2))
+            return tp
+    elif tree is None:
         build = (lambda: dp.gelqf_New(ctx, A, TS)) if lq else (lambda: dp.geqrf_New(ctx, A, TS))
     else:
         build = (lambda: dp.gelqf_param_New(ctx, tree, A, TS, TT)) if lq else \
             (lambda: dp.geqrf_param_New(ctx, tree, A, TS, TT))
-    h.run_tp(("gelqf" if lq else "geqrf") + ("" if tree is None else "_" + tree_kind), build)
+    label = {"tied": "_dtd", "untied": "_dtd_untied", "rd": "_rd"}.get(dtd, "" if tree is None else "_" + tree_kind)
+    h.run_tp(("gelqf" if lq else "geqrf") + label, build)
     if a.check:
         K = min(M, N)
         Q = h.mat(M if not lq else K, K if not lq else N, name="Q")
@@ -306,10 +317,11 @@ def t_getrf(h, variant):
     else:
         dp.plrnt(ctx, A, a.seed)
     a0 = _dense(h, A) if a.check else None
-    if variant == "incpiv":
+    if variant in ("incpiv", "incpiv_dtd"):
         L = dp.incpiv_L_descriptor(ctx, A, a.IB or 32)
         IP = dp.incpiv_ipiv_descriptor(ctx, A)
-        h.run_tp("getrf_incpiv", lambda: dp.getrf_incpiv_New(ctx, A, L, IP))
+        fn = dp.getrf_incpiv_dtd_New if variant == "incpiv_dtd" else dp.getrf_incpiv_New
+        h.run_tp("getrf_" + variant, lambda: fn(ctx, A, L, IP))
     elif variant == "nopiv":
         h.run_tp("getrf_nopiv", lambda: dp.getrf_nopiv_New(ctx, A))
     else:
@@ -319,7 +331,7 @@ def t_getrf(h, variant):
         B = h.mat(N, a.K or 1, name="B")
         dp.plrnt(ctx, B, a.seed + 1)
         b0 = _dense(h, B)
-        if variant == "incpiv":
+        if variant in ("incpiv", "incpiv_dtd"):
             dp.trsmpl_incpiv(ctx, A, L, IP, B)
         elif variant == "nopiv":
             dp.trsm(ctx, dp.dplasmaLeft, dp.dplasmaLower, dp.dplasmaNoTrans, dp.dplasmaUnit, 1.0, A, B)
@@ -458,6 +470,257 @@ def t_getrf_qrf(h):
         h.check("||Ax-b|| / ((||A|| ||x|| + ||b||) N eps)", res, 60.0)
 
 
+# ----------------------------------------------------------------------------- level-3 BLAS (reference comparison)
+def _uplo(h):
+    return h.dp.dplasmaLower if h.a.uplo.upper() == "L" else h.dp.dplasmaUpper
+
+
+def _full_from(d, lower, herm):
+    """The symmetric / Hermitian matrix whose `lower` (or upper) triangle is stored in d."""
+    t = torch.tril(d) if lower else torch.triu(d)
+    o = (torch.tril(d, -1) if lower else torch.triu(d, 1)).T
+    full = t + (o.conj() if herm else o)
+    if herm and full.is_complex():
+        full.diagonal().imag.zero_()
+    return full
+
+
+def _blas_check(h, got, ref, K):
+    res = float((got - ref).abs().max() / (ref.abs().max() * max(K, 1) * EPS[h.prec] + 1e-300))
+    h.check("||C - C_ref|| / (||C_ref|| K eps)", res, 10.0)
+
+
+def t_hemm(h, herm=True):
+    """testing_zhemm.c / testing_zsymm.c: C = alpha A B + beta C, A Hermitian/symmetric (left side)."""
+    dp, a, ctx = h.dp, h.a, h.ctx
+    M, N = a.M or a.N, a.N
+    uplo = _uplo(h)
+    A, B, C = h.mat(M, M, name="A"), h.mat(M, N, name="B"), h.mat(M, N, name="C")
+    dp.plrnt(ctx, A, a.seed)
+    dp.plrnt(ctx, B, a.seed + 1)
+    dp.plrnt(ctx, C, a.seed + 2)
+    if a.check:
+        a_, b_, c_ = (_dense(h, X) for X in (A, B, C))
+    fn = dp.hemm_New if herm else dp.symm_New
+    h.run_tp("hemm" if herm else "symm", lambda: fn(ctx, dp.dplasmaLeft, uplo, a.alpha, A, B, 0.5, C))
+    if a.check:
+        ref = a.alpha * (_full_from(a_, uplo == dp.dplasmaLower, herm) @ b_) + 0.5 * c_
+        _blas_check(h, _dense(h, C), ref, M)
+
+
+def t_herk(h, herm=True, two=False):
+    """testing_z{herk,syrk,her2k,syr2k}.c: C = alpha A A^H (+ B A^H ...) + beta C on the `uplo` triangle."""
+    dp, a, ctx = h.dp, h.a, h.ctx
+    N, K = a.N, a.K or a.N
+    uplo = _uplo(h)
+    A, C = h.mat(N, K, name="A"), h.mat(N, N, name="C")
+    B = h.mat(N, K, name="B") if two else None
+    dp.plrnt(ctx, A, a.seed)
+    if two:
+        dp.plrnt(ctx, B, a.seed + 1)
+    dp.plghe(ctx, 0.0, dp.dplasmaUpperLower, C, a.seed + 2)
+    if a.check:
+        a_, c_ = _dense(h, A), _dense(h, C)
+        b_ = _dense(h, B) if two else None
+    op = (lambda x: x.conj().T) if herm else (lambda x: x.T)
+    name = ("her2k" if two else "herk") if herm else ("syr2k" if two else "syrk")
+    fn = getattr(dp, name + "_New")
+    if two:
+        h.run_tp(name, lambda: fn(ctx, uplo, dp.dplasmaNoTrans, a.alpha, A, B, 0.5, C))
+    else:
+        h.run_tp(name, lambda: fn(ctx, uplo, dp.dplasmaNoTrans, a.alpha, A, 0.5, C))
+    if a.check:
+        prod = a_ @ op(b_) + b_ @ op(a_) if two else a_ @ op(a_)
+        ref = a.alpha * prod + 0.5 * c_
+        mask = torch.ones(N, N, dtype=torch.bool)
+        mask = torch.tril(mask) if uplo == dp.dplasmaLower else torch.triu(mask)
+        got = _dense(h, C)
+        _blas_check(h, torch.where(mask, got, torch.zeros_like(got)), torch.where(mask, ref, torch.zeros_like(ref)),
+                    K)
+
+
+def t_geadd(h):
+    """testing_zgeadd.c: B = alpha op(A) + beta B."""
+    dp, a, ctx = h.dp, h.a, h.ctx
+    M, N = a.M or a.N, a.N
+    A, B = h.mat(M, N, name="A"), h.mat(M, N, name="B")
+    dp.plrnt(ctx, A, a.seed)
+    dp.plrnt(ctx, B, a.seed + 1)
+    if a.check:
+        a_, b_ = _dense(h, A), _dense(h, B)
+    h.run_tp("geadd", lambda: dp.geadd_New(ctx, dp.dplasmaNoTrans, a.alpha, A, 0.5, B))
+    if a.check:
+        _blas_check(h, _dense(h, B), a.alpha * a_ + 0.5 * b_, 1)
+
+
+# ----------------------------------------------------------------------------- inverses
+def t_trtri(h):
+    """testing_ztrtri.c: inverse of a triangular matrix, ||I - A^-1 A||."""
+    dp, a, ctx = h.dp, h.a, h.ctx
+    uplo = _uplo(h)
+    A = h.mat(a.N, a.N)
+    dp.plghe(ctx, float(a.N), dp.dplasmaUpperLower, A, a.seed)
+    a0 = _dense(h, A) if a.check else None
+    h.run_tp("trtri", lambda: dp.trtri_New(ctx, uplo, dp.dplasmaNonUnit, A))
+    if a.check:
+        tri = torch.tril if uplo == dp.dplasmaLower else torch.triu
+        res = float((tri(_dense(h, A)) @ tri(a0) - torch.eye(a.N, dtype=a0.dtype)).abs().max()
+                    / (a.N * EPS[h.prec]))
+        h.check("||I - A^-1 A|| / (N eps)", res, 60.0 * float(tri(a0).abs().max()))
+
+
+def t_poinv(h):
+    """testing_zpoinv.c: inverse of an SPD matrix (potrf + trtri + lauum in one taskpool)."""
+    dp, a, ctx = h.dp, h.a, h.ctx
+    uplo = _uplo(h)
+    A = h.mat(a.N, a.N)
+    dp.plghe(ctx, float(a.N), dp.dplasmaUpperLower, A, a.seed)
+    a0 = _dense(h, A) if a.check else None
+    h.run_tp("poinv", lambda: dp.poinv_New(ctx, uplo, A))
+    if a.check:
+        inv = _full_from(_dense(h, A), uplo == dp.dplasmaLower, True)
+        res = float((inv @ a0 - torch.eye(a.N, dtype=a0.dtype)).abs().max()
+                    / (a0.abs().max() * inv.abs().max() * a.N * EPS[h.prec]))
+        h.check("||I - A^-1 A|| / (||A|| ||A^-1|| N eps)", res, 60.0)
+
+
+# ----------------------------------------------------------------------------- Q applications
+def t_unmqr(h, lq, tree_kind):
+    """testing_zunm{qr,lq}[_hqr|_systolic].c: C := op(Q) C and C op(Q) checked against the explicit Q."""
+    dp, a, ctx = h.dp, h.a, h.ctx
+    M = a.M or a.N
+    N = a.N
+    K = a.K or N
+    ib = a.IB or 32
+    A = h.mat(M, N)
+    dp.plrnt(ctx, A, a.seed)
+    TS = dp.block_cyclic(ctx, h.dt, ib, A.nb, A.mt * ib, A.nt * A.nb, name="TS")
+    TT = dp.block_cyclic(ctx, h.dt, ib, A.nb, A.mt * ib, A.nt * A.nb, name="TT")
+    trans_t = dp.dplasmaConjTrans if lq else dp.dplasmaNoTrans
+    tree = None
+    if tree_kind == "hqr":
+        tree = dp.hqr_init(trans_t, A, a.treel, a.treeh, a.qr_a if a.qr_a > 0 else 1,
+                           a.qr_p if a.qr_p > 0 else ctx.P, a.domino, a.tsrr)
+    elif tree_kind == "systolic":
+        tree = dp.systolic_init(trans_t, A, a.qr_p if a.qr_p > 0 else ctx.P, a.qr_a if a.qr_a > 0 else 1)
+    if tree is None:
+        (dp.gelqf if lq else dp.geqrf)(ctx, A, TS)
+    else:
+        (dp.gelqf_param if lq else dp.geqrf_param)(ctx, tree, A, TS, TT)
+    nq = N if lq else M          # Q is nq x nq
+    Qm = h.mat(nq, nq, name="Q")
+    if tree is None:
+        (dp.unglq if lq else dp.ungqr)(ctx, A, TS, Qm)
+    else:
+        (dp.unglq_param if lq else dp.ungqr_param)(ctx, tree, A, TS, TT, Qm)
+    q = _dense(h, Qm)
+    name = ("unmlq" if lq else "unmqr") + ("" if tree is None else "_" + tree_kind)
+    for side in (dp.dplasmaLeft, dp.dplasmaRight):
+        for trans in (dp.dplasmaNoTrans, dp.dplasmaConjTrans):
+            C = h.mat(nq, K, name="C") if side == dp.dplasmaLeft else h.mat(K, nq, name="C")
+            dp.plrnt(ctx, C, a.seed + 3)
+            c0 = _dense(h, C)
+            if tree is None:
+                build = lambda C=C, s=side, t=trans: (dp.unmlq_New if lq else dp.unmqr_New)(ctx, s, t, A, TS, C)  # noqa: E731
+            else:
+                build = lambda C=C, s=side, t=trans: (dp.unmlq_param_New if lq else dp.unmqr_param_New)(  # noqa: E731
+                    ctx, s, t, tree, A, TS, TT, C)
+            h.run_tp(name, build)
+            if a.check:
+                op = q if trans == dp.dplasmaNoTrans else q.conj().T
+                ref = op @ c0 if side == dp.dplasmaLeft else c0 @ op
+                res = float((_dense(h, C) - ref).abs().max() / (c0.abs().max() * nq * EPS[h.prec]))
+                h.check(f"||{'L' if side == dp.dplasmaLeft else 'R'}{'N' if trans == dp.dplasmaNoTrans else 'C'}: "
+                        f"op(Q) C - ref|| / (||C|| N eps)", res, 60.0)
+
+
+# ----------------------------------------------------------------------------- solvers and reductions
+def t_gesv_incpiv(h):
+    """testing_zgesv_incpiv.c: A X = B with incremental-pivoting LU."""
+    dp, a, ctx = h.dp, h.a, h.ctx
+    N, K = a.N, a.K or 1
+    A = h.mat(N, N)
+    dp.plrnt(ctx, A, a.seed)
+    B = h.mat(N, K, name="B")
+    dp.plrnt(ctx, B, a.seed + 1)
+    a0, b0 = (_dense(h, A), _dense(h, B)) if a.check else (None, None)
+    L = dp.incpiv_L_descriptor(ctx, A, a.IB or 32)
+    IP = dp.incpiv_ipiv_descriptor(ctx, A)
+    t0 = time.perf_counter()
+    info = dp.gesv_incpiv(ctx, A, L, IP, B)
+    ctx.sync()
+    from .utils.flops import flops
+    h.report("gesv_incpiv", time.perf_counter() - t0, flops(A.prec, "getrf", N, N)
+             + 2 * flops(A.prec, "trsm", True, N, K))
+    if a.check:
+        x = _dense(h, B)
+        res = float((a0 @ x - b0).abs().max() / ((a0.abs().max() * x.abs().max() + b0.abs().max()) * N
+                                                  * EPS[h.prec]))
+        h.check("||Ax-b|| / ((||A|| ||x|| + ||b||) N eps)", res, 60.0)
+    return info
+
+
+def t_gesvd(h):
+    """testing_zgesvd.c: singular values through the two-stage reduction (ge2gb to band, then the band
+    bidiagonal's singular values) against LAPACK on the original matrix."""
+    t_gebrd_ge2gb(h)
+
+
+def t_hbrdt(h):
+    """testing_zhbrdt.c: Hermitian band -> real tridiagonal (bulge chasing); eigenvalues preserved."""
+    dp, a, ctx = h.dp, h.a, h.ctx
+    N = a.N
+    b = a.NB or a.MB or 8
+    g = torch.Generator().manual_seed(a.seed)
+    rdt = torch.float64
+    dt = torch.complex128 if h.dt.is_complex else torch.float64
+    dense = torch.randn(N, N, generator=g, dtype=rdt)
+    if dt.is_complex:
+        dense = torch.complex(dense, torch.randn(N, N, generator=g, dtype=rdt))
+    dense = torch.tril(torch.triu(dense, -b), 0)
+    herm = dense + torch.tril(dense, -1).conj().T
+    herm.diagonal().imag.zero_() if dt.is_complex else None
+    band = torch.zeros(b + 1, N, dtype=dt)
+    for j in range(N):
+        for i in range(j, min(N, j + b + 1)):
+            band[i - j, j] = herm[i, j]
+    t0 = time.perf_counter()
+    d, e = dp.hbrdt(ctx, band.numpy(), b)
+    h.report("hbrdt", time.perf_counter() - t0, 6.0 * N * N * b)
+    if a.check:
+        T = torch.diag(torch.as_tensor(d, dtype=rdt)) + torch.diag(torch.as_tensor(e, dtype=rdt).abs(), -1) \
+            + torch.diag(torch.as_tensor(e, dtype=rdt).abs(), 1)
+        w, ref = torch.linalg.eigvalsh(T), torch.linalg.eigvalsh(herm)
+        res = float((w - ref).abs().max() / (ref.abs().max() * N * EPS["d"]))
+        h.check("max|w(T) - w(A)| / (||A|| N eps)", res, 60.0)
+
+
+def t_pivgen(h):
+    """testing_zpivgen.c / TestsQRPivgen.cmake: validate the QR elimination trees (every tile killed once,
+    by a live pivot, in a consistent order) over the low/high-level trees, domain sizes and domino."""
+    dp, a, ctx = h.dp, h.a, h.ctx
+    M, N = a.M or a.N, a.N
+    A = h.mat(M, N)
+    bad = 0
+    count = 0
+    t0 = time.perf_counter()
+    for llvl in (0, 1, 2, 3, 4):
+        for hlvl in (0, 1, 2, 3):
+            for qa in (1, 2, 4):
+                for dom in (False, True):
+                    tree = dp.hqr_init(dp.dplasmaNoTrans, A, llvl, hlvl, qa, a.qr_p if a.qr_p > 0 else 2, dom,
+                                       a.tsrr)
+                    count += 1
+                    bad += int(dp.qrtree_check(A, tree) != 0)
+    for p in (1, 2, 3):
+        count += 1
+        bad += int(dp.qrtree_check(A, dp.systolic_init(dp.dplasmaNoTrans, A, p, 1)) != 0)
+    h.report("pivgen", time.perf_counter() - t0, 0.0)
+    if ctx.rank == 0:
+        print(f"[****] pivgen: {count} trees checked on {A.mt} x {A.nt} tiles, {bad} invalid", flush=True)
+    h.check("invalid trees", float(bad), 0.5)
+
+
 def _dense(h, X):
     d = X.to_dense_local().cpu()
     if h.ctx.world > 1:
@@ -480,6 +743,22 @@ OPS = {
     "getrf_incpiv": lambda h: t_getrf(h, "incpiv"), "getrf_nopiv": lambda h: t_getrf(h, "nopiv"),
     "lange": t_lange, "lanm2": t_lanm2, "print": t_print,
     "getrf_qrf": t_getrf_qrf, "heev": t_heev, "gebrd_ge2gb": t_gebrd_ge2gb, "hetrf": t_hetrf, "hebut": t_hetrf,
+    # DTD / recursive QR and DTD incremental-pivoting LU
+    "geqrf_dtd": lambda h: _qr_common(h, False, None, "tied"),
+    "geqrf_dtd_untied": lambda h: _qr_common(h, False, None, "untied"),
+    "geqrf_rd": lambda h: _qr_common(h, False, None, "rd"),
+    "getrf_incpiv_dtd": lambda h: t_getrf(h, "incpiv_dtd"),
+    # level-3 BLAS against a dense reference
+    "hemm": t_hemm, "symm": lambda h: t_hemm(h, herm=False),
+    "herk": t_herk, "syrk": lambda h: t_herk(h, herm=False),
+    "her2k": lambda h: t_herk(h, two=True), "syr2k": lambda h: t_herk(h, herm=False, two=True),
+    "geadd": t_geadd, "trtri": t_trtri, "poinv": t_poinv,
+    # Q applications
+    "unmqr": lambda h: t_unmqr(h, False, None), "unmlq": lambda h: t_unmqr(h, True, None),
+    "unmqr_hqr": lambda h: t_unmqr(h, False, "hqr"), "unmlq_hqr": lambda h: t_unmqr(h, True, "hqr"),
+    "unmqr_systolic": lambda h: t_unmqr(h, False, "systolic"),
+    "unmlq_systolic": lambda h: t_unmqr(h, True, "systolic"),
+    "gesv_incpiv": t_gesv_incpiv, "gesvd": t_gesvd, "hbrdt": t_hbrdt, "pivgen": t_pivgen,
 }
 
 

@@ -31,6 +31,19 @@ def _run(args, nproc=1):
     # DTD drivers (testing_zpotrf_dtd, testing_zpotrf_dtd_untied, testing_zgemm_dtd)
     "dpotrf -N 300 -t 32 -o LL -x", "dgetrf_1d -N 200 -t 32 -o RND -x", "dgeqrf -M 300 -N 200 -t 40 -i 8 -o IP -x",
     "dpotrf_dtd -N 200 -t 32 -x", "dpotrf_dtd_untied -N 200 -t 32 -x", "dgemm_dtd -M 90 -N 70 -K 50 -t 16 -x",
+    # DTD QR / incpiv LU, recursive QR (testing_zgeqrf_dtd[_untied], testing_zgetrf_incpiv_dtd, testing_zgeqrf_rd)
+    "dgeqrf_dtd -M 150 -N 118 -t 32 -i 8 -x", "zgeqrf_dtd_untied -M 120 -N 90 -t 32 -i 8 -x",
+    "dgetrf_incpiv_dtd -N 150 -t 32 -i 8 -x", "dgeqrf_rd -M 200 -N 150 -t 50 -i 10 -z 25 -x",
+    # level-3 BLAS vs a dense reference, inverses
+    "zhemm -M 90 -N 70 -t 16 -x", "dsymm -M 90 -N 70 -t 16 -u U -x", "zherk -N 90 -K 50 -t 16 -u U -x",
+    "ssyrk -N 70 -K 40 -t 16 -x", "zher2k -N 90 -K 50 -t 16 -x", "dsyr2k -N 90 -K 50 -t 16 -u U -x",
+    "dgeadd -M 90 -N 70 -t 16 -x", "ztrtri -N 150 -t 32 -u U -x", "dpoinv -N 150 -t 32 -x",
+    # Q applications (all four side / trans combinations against the explicit Q)
+    "dunmqr -M 120 -N 90 -K 40 -t 24 -i 8 -x", "zunmlq -M 90 -N 120 -K 40 -t 24 -i 8 -x",
+    "dunmqr_hqr -M 150 -N 90 -K 30 -t 24 -i 8 --qr_a 2 -x", "dunmlq_systolic -M 90 -N 150 -K 30 -t 24 -i 8 -x",
+    # solvers, reductions, QR tree validation
+    "dgesv_incpiv -N 150 -t 32 -i 8 -K 3 -x", "dgesvd -M 150 -N 120 -t 24 -x", "zhbrdt -N 60 -t 6 -x",
+    "dpivgen -M 400 -N 200 -t 20",
 ])
 def test_cli_single(args):
     r = _run(args.split())
@@ -42,6 +55,13 @@ def test_cli_multirank():
     r = _run("dgetrf_ptgpanel -N 200 -t 32 -P 2 -x".split(), nproc=4)
     assert r.returncode == 0, r.stdout + r.stderr[-2000:]
     assert "PxQxg=   2 2" in r.stdout and "CORRECT" in r.stdout
+
+
+def test_cli_unmqr_hqr_multirank():
+    """Q application with an HQR tree on a 2 x 1 grid (testing_zunmqr_hqr with -P 2)."""
+    r = _run("dunmqr_hqr -M 160 -N 96 -K 40 -t 16 -i 8 -P 2 --qr_a 2 -x".split(), nproc=2)
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    assert "CORRECT" in r.stdout and "SUSPICIOUS" not in r.stdout
 
 
 def test_cli_kcyclic_multirank():
