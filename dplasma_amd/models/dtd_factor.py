@@ -4,53 +4,27 @@ Reference: ``tests/testing_zgeqrf_dtd.c`` / ``testing_zgeqrf_dtd_untied.c`` (GEQ
 TSMQR tasks inserted in loop order on A and the T tiles, the untied variant inserting from inside a
 task) and ``tests/testing_zgetrf_incpiv_dtd.c`` (GETRF / GESSM / TSTRF / SSSSM on A, L and IPIV).
 
-Each task body runs ONE item of the same batched tile kernels the PTG-style tile DAGs use
-(``ops/qr_ops.py``, ``ops/lu_incpiv_ops.py``: HIP launches on the GPU, the PyTorch transcription on
-the CPU), so the DTD factorizations store exactly what the tile engines store: V and T in the
-reference's per-tile TSQRT layout, L / IPIV in the incremental-pivoting layout that
-``trsmpl_incpiv`` consumes.
+The task classes carry the batched tile kinds of the PTG-style tile DAGs (``ops/qr_ops.py``,
+``ops/lu_incpiv_ops.py``: HIP launches on the GPU, the PyTorch transcription on the CPU): the ready
+tasks of one class in a window level run as ONE launch, and the DTD factorizations store exactly what
+the tile engines store -- V and T in the reference's per-tile TSQRT layout, L / IPIV in the
+incremental-pivoting layout that ``trsmpl_incpiv`` consumes.
 """
 from __future__ import annotations
 
-import numpy as np
 import torch
 
-from ..ops import _lib, lu_incpiv_ops, qr_ops
+from ..ops import lu_incpiv_ops, qr_ops
 from ..runtime import dtd
-from ..runtime.dag import DAG_ITEM
 from ..utils.flops import flops
-from .dtd_potrf import _blocking_New, _info_reducer, tile_args
-
-
-def _run_kind(K, views, ext):
-    """One task of a batched tile kind: ``views[r]`` is the tile of role r, ``ext`` its (m, n, k)."""
-    ext = tuple(int(x) for x in ext)
-    if views[0].device.type == "cuda":
-        it = np.zeros(1, dtype=DAG_ITEM)
-        for (_, _, slot), v in zip(K.roles, views):
-            b, off, ld = tile_args(v)
-            it[f"p{slot}"] = b.data_ptr() + off * v.element_size()
-            it[f"ld{slot}"] = ld
-        it["m"], it["n"], it["k"] = ext
-        d = torch.from_numpy(it.view(np.uint8).copy()).to(views[0].device)
-        K.gpu(d.data_ptr(), 1, _lib.stream_ptr(), ext)
-        d.record_stream(torch.cuda.current_stream())   # the record lives until the launch has read it
-        return
-    K.cpu([tile_args(v) for v in views], ext)
-
-
-def _body(K):
-    def body(*args):
-        n = len(K.roles)
-        _run_kind(K, args[:n], args[n])
-    return body
+from .dtd_potrf import _blocking_New, _info_reducer
 
 
 # ----------------------------------------------------------------------------- QR
 def _insert_geqrf(tp, A, T):
     """Flat-tree tile QR (zgeqrf.jdf task classes) as DTD tasks on A and T (ib x nb tiles)."""
     kd = qr_ops.kinds(A.dtype, T.mb, qr_ops.view_flags(A.dtype, False), qr_ops.view_flags(A.dtype, False))
-    tc = {k: tp.task_class(k, _body(kd[k])) for k in ("geqrt", "unmqr_h", "tsqrt", "tsmqr_h")}
+    tc = {k: tp.task_class(k, kind=kd[k]) for k in ("geqrt", "unmqr_h", "tsqrt", "tsmqr_h")}
     Tl = dtd.tile_of
     In, InOut, Aff = dtd.INPUT, dtd.INOUT, dtd.AFFINITY
     for k in range(min(A.mt, A.nt)):
@@ -125,7 +99,7 @@ def geqrf_dtd_untied_New(ctx, A, T, window=None):
 def _insert_getrf_incpiv(tp, A, L, IPIV, info):
     """zgetrf_incpiv.jdf task classes as DTD tasks (tests/testing_zgetrf_incpiv_dtd.c)."""
     kd = lu_incpiv_ops.kinds(A.dtype, L.mb, A.nb, info)
-    tc = {k: tp.task_class(k, _body(kd[k])) for k in ("getrf", "gessm", "tstrf", "ssssm")}
+    tc = {k: tp.task_class(k, kind=kd[k]) for k in ("getrf", "gessm", "tstrf", "ssssm")}
     Tl = dtd.tile_of
     In, InOut, Aff = dtd.INPUT, dtd.INOUT, dtd.AFFINITY
     for k in range(min(A.mt, A.nt)):

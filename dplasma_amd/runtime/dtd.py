@@ -34,6 +34,7 @@ then all ready tasks of that class in a level become one kernel launch.
 """
 from __future__ import annotations
 
+import dataclasses
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional
 
@@ -92,7 +93,7 @@ class DTDTaskpool:
     def _new_dag(self):
         self.dag = TileDAG(self.ctx, f"{self.name}[{getattr(self, 'windows_run', 0)}]")
 
-    def task_class(self, name: str, body: Callable, kind: Optional[Kind] = None) -> TaskClass:
+    def task_class(self, name: str, body: Optional[Callable] = None, kind: Optional[Kind] = None) -> TaskClass:
         return TaskClass(name, body, kind)
 
     def _kind_for(self, tc: TaskClass, modes: tuple, affinity: int) -> Kind:
@@ -103,6 +104,18 @@ class DTDTaskpool:
             K = Kind(f"dtd:{tc.name}:{len(self._kinds)}", roles, affinity, None, None, body=tc.body)
             self._kinds[key] = K
         return K
+
+    def _batched_kind(self, tc: TaskClass, modes: tuple, affinity: int) -> Kind:
+        K = tc.kind
+        if len(modes) != len(K.roles) or any(md != r[1] for md, r in zip(modes, K.roles)):
+            raise ValueError(f"DTD task class {tc.name}: tile access modes {modes} do not match kind {K.name}")
+        if affinity == K.exec_role:
+            return K
+        key = (id(tc), "exec", affinity)
+        Ka = self._kinds.get(key)
+        if Ka is None:
+            Ka = self._kinds[key] = dataclasses.replace(K, name=f"{K.name}@{affinity}", exec_role=affinity)
+        return Ka
 
     def insert_task(self, fn, *args, name: Optional[str] = None, flops: float = 0.0, priority: int = 0):
         """Insert one task.  ``args`` mixes tile arguments ``(tile_of(A, m, n), INPUT|INOUT|OUTPUT[|AFFINITY])``
@@ -135,9 +148,16 @@ class DTDTaskpool:
         if affinity is None:
             written = [i for i, md in enumerate(modes) if md & 2]
             affinity = written[0] if written else 0
-        K = self._kind_for(tc, tuple(modes), affinity)
         keys = [int(self.dag.keys(t.M, t.m, t.n)) for t in tiles]
-        self.dag.add(K, [keys], [[0, 0, 0]], pyargs=[tuple(values)])
+        if tc.kind is not None:
+            # batched tile kind: the values are the task's (m, n, k) extents; every ready task of the
+            # class in a level becomes one launch
+            K = self._batched_kind(tc, tuple(modes), affinity)
+            ext = [int(x) for x in (values[0] if values else (0, 0, 0))]
+            self.dag.add(K, [keys], [ext])
+        else:
+            K = self._kind_for(tc, tuple(modes), affinity)
+            self.dag.add(K, [keys], [[0, 0, 0]], pyargs=[tuple(values)])
         self.ntasks += 1
         self.pending += 1
         self.flops += flops
