@@ -68,6 +68,18 @@ NatProgram* nat_trsm(dplasma_context_t* ctx, int prec, int side, int uplo, int t
 NatProgram* nat_plghe(dplasma_context_t* ctx, int prec, double bump, int uplo, dplasma_desc_t* A,
                       unsigned long long seed);
 NatProgram* nat_plrnt(dplasma_context_t* ctx, int prec, int diagdom, dplasma_desc_t* A, unsigned long long seed);
+NatProgram* nat_herk(dplasma_context_t* ctx, int prec, int uplo, int trans, double alpha, dplasma_desc_t* A,
+                     double beta, dplasma_desc_t* C);
+NatProgram* nat_syrk(dplasma_context_t* ctx, int prec, int uplo, int trans, const void* alpha, dplasma_desc_t* A,
+                     const void* beta, dplasma_desc_t* C);
+NatProgram* nat_geadd(dplasma_context_t* ctx, int prec, int trans, const void* alpha, dplasma_desc_t* A,
+                      const void* beta, dplasma_desc_t* B);
+NatProgram* nat_tradd(dplasma_context_t* ctx, int prec, int uplo, int trans, const void* alpha, dplasma_desc_t* A,
+                      const void* beta, dplasma_desc_t* B);
+NatProgram* nat_lacpy(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* A, dplasma_desc_t* B);
+NatProgram* nat_laset(dplasma_context_t* ctx, int prec, int uplo, const void* alpha, const void* beta,
+                      dplasma_desc_t* A);
+NatProgram* nat_lascal(dplasma_context_t* ctx, int prec, int uplo, const void* alpha, dplasma_desc_t* A);
 int nat_execute(dplasma_context_t* ctx, NatProgram* P);     // run + wait + info, frees P
 dplasma_taskpool_t* nat_wrap(NatProgram* P);
 void nat_fini(dplasma_context_t* ctx);

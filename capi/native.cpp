@@ -15,7 +15,8 @@
 // program is built (dplasma_<p><op>_New), so a run only launches kernels.
 //
 // Scope: one process, one GPU; s/d/c/z potrf, potrs, posv, gemm, trsm (all 8 side/uplo/trans
-// variants), plghe, plrnt.  Every other entry point returns an error on a native context.
+// variants), herk / syrk, the element-wise maps (geadd, tradd, lacpy, laset, lascal), plghe, plrnt.
+// Every other entry point returns an error on a native context.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -43,6 +44,12 @@ int dpl_trsm_batched(int prec, int side, int uplo, int trans, int diag, int nite
                      const void* tri_off, void* work, hipStream_t st);
 int dpl_generate(int prec, int kind, int nitems, const void* items, int mmax, int nmax, void* A, int lda,
                  long long gM, unsigned long long seed, const void* bump, hipStream_t st);
+int dpl_laset(int prec, int part, int nitems, const void* items, int mmax, int nmax, const void* alpha,
+              const void* beta, void* A, int lda, hipStream_t st);
+int dpl_geadd(int prec, int part, int trans, int nitems, const void* items, int mmax, int nmax, const void* alpha,
+              const void* A, int lda, const void* beta, void* B, int ldb, int copy, hipStream_t st);
+int dpl_lascal(int prec, int part, int nitems, const void* items, int mmax, int nmax, const void* alpha, void* A,
+               int lda, hipStream_t st);
 }
 
 namespace {
@@ -611,6 +618,156 @@ NatProgram* nat_trsm(dplasma_context_t* ctx, int prec, int side, int uplo, int t
   NatProgram* P = new_program(c, "trsm", false);
   if (!add_trsm(*P, side, uplo, trans, diag, Scalar(prec, alpha), *A, *B, 1))
     return fail(P, "trsm: device allocation failed");
+  return P;
+}
+
+// ----------------------------------------------------------------------------- HERK / SYRK
+// C = alpha op(A) op(A)^{H|T} + beta C on the uplo triangle (models/blas3.py): one launch of the MFMA
+// GEMM engine over every tile of the triangle, k-runs over A's tile columns (rows for trans), the
+// diagonal tiles masked to their triangle.
+static NatProgram* rank_k(dplasma_context_t* ctx, int prec, int uplo, int trans, const Scalar& alpha,
+                          dplasma_desc_t* dA, const Scalar& beta, dplasma_desc_t* dC, bool herm, const char* name) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *C = dC ? dC->nat : nullptr;
+  if (!same_ctx(c, {A, C}, prec)) return fail(nullptr, std::string(name) + ": descriptors of another context");
+  const bool nt = trans == NOTRANS;
+  const int an = nt ? A->m : A->n, ak = nt ? A->n : A->m, akb = nt ? A->nb : A->mb;
+  if ((uplo != LOWER && uplo != UPPER) || C->m != C->n || an != C->m || C->mb != C->nb ||
+      (nt ? A->mb : A->nb) != C->mb)
+    return fail(nullptr, std::string(name) + ": operands do not conform");
+  const int ct = herm ? CONJTRANS : TRANS;
+  NatProgram* P = new_program(c, name, false);
+  auto g = std::make_shared<Gemm>();
+  const int kt = (ak + akb - 1) / akb;
+  for (int n = 0; n < C->nt; ++n)
+    for (int m = 0; m < C->mt; ++m) {
+      if ((uplo == LOWER && m < n) || (uplo == UPPER && m > n)) continue;
+      std::vector<KPair> kp;
+      for (int k = 0; k < kt; ++k)   // C(m,n) += op(A)(m,k) op(A)(n,k)^H
+        kp.push_back(KPair{nt ? A->off(m, k) : A->off(k, m), nt ? A->off(n, k) : A->off(k, n),
+                           nt ? A->cols(k) : A->rows(k), 0});
+      g->add(C->off(m, n), C->rows(m), C->cols(n), kp, m == n ? (uplo == LOWER ? 1 : 2) : 0);
+    }
+  if (!g->upload(*P)) return fail(P, std::string(name) + ": device allocation failed");
+  char *a = A->data, *cc = C->data;
+  const int lda = A->lld, ldc = C->lld;
+  const int ta = nt ? NOTRANS : ct, tb = nt ? ct : NOTRANS;
+  P->task(1, [=](hipStream_t s) { return g->launch(prec, ta, tb, alpha, a, lda, a, lda, beta, cc, ldc, s); }, {});
+  return P;
+}
+
+NatProgram* nat_herk(dplasma_context_t* ctx, int prec, int uplo, int trans, double alpha, dplasma_desc_t* A,
+                     double beta, dplasma_desc_t* C) {
+  if (prec != P_C && prec != P_Z) return fail(nullptr, "herk: complex precisions only");
+  return rank_k(ctx, prec, uplo, trans, Scalar(prec, alpha), A, Scalar(prec, beta), C, true, "herk");
+}
+
+NatProgram* nat_syrk(dplasma_context_t* ctx, int prec, int uplo, int trans, const void* alpha, dplasma_desc_t* A,
+                     const void* beta, dplasma_desc_t* C) {
+  return rank_k(ctx, prec, uplo, trans, Scalar(prec, alpha), A, Scalar(prec, beta), C, false, "syrk");
+}
+
+// ----------------------------------------------------------------------------- element-wise maps
+// geadd / tradd / lacpy / laset / lascal (models/aux.py): one grid-stride launch over the tiles that
+// meet the uplo part; the kernels mask by GLOBAL element coordinates (TileItem gi / gj), so a diagonal
+// tile is cut at the matrix diagonal exactly as the reference's map2 LOWER / UPPER tasks do.
+static int part_of(int uplo) { return uplo == LOWER ? 1 : uplo == UPPER ? 2 : 0; }
+
+struct MapBatch {
+  std::vector<TileItem> it;
+  int mm = 0, nn = 0;
+  DevPtr d;
+  // the tiles of B (optionally paired with op(A)'s source tile) touching the uplo part
+  void build(const NatDesc& B, int uplo, const NatDesc* A, int trans) {
+    for (int n = 0; n < B.nt; ++n)
+      for (int m = 0; m < B.mt; ++m) {
+        if ((uplo == LOWER && m < n) || (uplo == UPPER && m > n)) continue;
+        const long long ao = A ? (trans == NOTRANS ? A->off(m, n) : A->off(n, m)) : B.off(m, n);
+        it.push_back(TileItem{A ? ao : B.off(m, n), B.off(m, n), B.rows(m), B.cols(n), m * B.mb, n * B.nb});
+        mm = std::max(mm, B.rows(m));
+        nn = std::max(nn, B.cols(n));
+      }
+  }
+  bool upload(NatProgram& P) {
+    if (it.empty()) return true;
+    d = dev_upload(it);
+    if (!d) return false;
+    P.keep.push_back(d);
+    return true;
+  }
+  int n() const { return (int)it.size(); }
+  const void* items() const { return d ? d->p : nullptr; }
+};
+
+static NatProgram* map_add(dplasma_context_t* ctx, int prec, int uplo, int trans, const Scalar& alpha,
+                           dplasma_desc_t* dA, const Scalar& beta, dplasma_desc_t* dB, int copy, const char* name) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *B = dB ? dB->nat : nullptr;
+  if (!same_ctx(c, {A, B}, prec)) return fail(nullptr, std::string(name) + ": descriptors of another context");
+  const bool nt = trans == NOTRANS;
+  if ((nt ? A->m : A->n) != B->m || (nt ? A->n : A->m) != B->n || (nt ? A->mb : A->nb) != B->mb ||
+      (nt ? A->nb : A->mb) != B->nb)
+    return fail(nullptr, std::string(name) + ": operands do not conform");
+  NatProgram* P = new_program(c, name, false);
+  auto mb = std::make_shared<MapBatch>();
+  mb->build(*B, uplo, A, trans);
+  if (!mb->upload(*P)) return fail(P, std::string(name) + ": device allocation failed");
+  const int part = part_of(uplo), lda = A->lld, ldb = B->lld;
+  const char* a = A->data;
+  char* b = B->data;
+  P->task(1, [=](hipStream_t s) {
+    return dpl_geadd(prec, part, trans, mb->n(), mb->items(), mb->mm, mb->nn, alpha.ptr(), a, lda, beta.ptr(), b,
+                     ldb, copy, s);
+  }, {});
+  return P;
+}
+
+NatProgram* nat_geadd(dplasma_context_t* ctx, int prec, int trans, const void* alpha, dplasma_desc_t* A,
+                      const void* beta, dplasma_desc_t* B) {
+  return map_add(ctx, prec, UPPERLOWER, trans, Scalar(prec, alpha), A, Scalar(prec, beta), B, 0, "geadd");
+}
+
+NatProgram* nat_tradd(dplasma_context_t* ctx, int prec, int uplo, int trans, const void* alpha, dplasma_desc_t* A,
+                      const void* beta, dplasma_desc_t* B) {
+  return map_add(ctx, prec, uplo, trans, Scalar(prec, alpha), A, Scalar(prec, beta), B, 0, "tradd");
+}
+
+NatProgram* nat_lacpy(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* A, dplasma_desc_t* B) {
+  return map_add(ctx, prec, uplo, NOTRANS, Scalar(prec, 1.0), A, Scalar(prec, 0.0), B, 1, "lacpy");
+}
+
+NatProgram* nat_laset(dplasma_context_t* ctx, int prec, int uplo, const void* alpha, const void* beta,
+                      dplasma_desc_t* dA) {
+  NatCtx* c = ctx->nat;
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!same_ctx(c, {A}, prec)) return fail(nullptr, "laset: descriptor of another context");
+  NatProgram* P = new_program(c, "laset", false);
+  auto mb = std::make_shared<MapBatch>();
+  mb->build(*A, uplo, nullptr, NOTRANS);
+  if (!mb->upload(*P)) return fail(P, "laset: device allocation failed");
+  const Scalar al(prec, alpha), be(prec, beta);
+  const int part = part_of(uplo), lda = A->lld;
+  char* a = A->data;
+  P->task(1, [=](hipStream_t s) {
+    return dpl_laset(prec, part, mb->n(), mb->items(), mb->mm, mb->nn, al.ptr(), be.ptr(), a, lda, s);
+  }, {});
+  return P;
+}
+
+NatProgram* nat_lascal(dplasma_context_t* ctx, int prec, int uplo, const void* alpha, dplasma_desc_t* dA) {
+  NatCtx* c = ctx->nat;
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!same_ctx(c, {A}, prec)) return fail(nullptr, "lascal: descriptor of another context");
+  NatProgram* P = new_program(c, "lascal", false);
+  auto mb = std::make_shared<MapBatch>();
+  mb->build(*A, uplo, nullptr, NOTRANS);
+  if (!mb->upload(*P)) return fail(P, "lascal: device allocation failed");
+  const Scalar al(prec, alpha);
+  const int part = part_of(uplo), lda = A->lld;
+  char* a = A->data;
+  P->task(1, [=](hipStream_t s) {
+    return dpl_lascal(prec, part, mb->n(), mb->items(), mb->mm, mb->nn, al.ptr(), a, lda, s);
+  }, {});
   return P;
 }
 

@@ -123,6 +123,103 @@ static void test_dgemm(dplasma_context_t *ctx) {
   dplasma_desc_destroy(A), dplasma_desc_destroy(B), dplasma_desc_destroy(C);
 }
 
+/* dsyrk (lower, A^T A) and zherk (upper, A A^H) against host sums; ragged 300 / 200 with nb 128 */
+static void test_rank_k(dplasma_context_t *ctx) {
+  const int N = 300, K = 200, nb = 128;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, K, N), *C = dmat(ctx, dplasmaRealDouble, nb, N, N);
+  dplasma_dplrnt(ctx, 0, A, 7);
+  dplasma_dplrnt(ctx, 0, C, 8);
+  double *a = malloc(sizeof(double) * K * N), *c = malloc(sizeof(double) * N * N), *r = malloc(sizeof(double) * N * N);
+  dplasma_desc_get_lapack(A, a, K);
+  dplasma_desc_get_lapack(C, c, N);
+  CHECK(dplasma_dsyrk(ctx, dplasmaLower, dplasmaTrans, 0.5, A, 2.0, C) == 0, "dsyrk: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(C, r, N);
+  double err = 0;
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i < N; ++i) {
+      double ref = c[i + (size_t)j * N];
+      if (i >= j) {
+        double s = 0;
+        for (int k = 0; k < K; ++k) s += a[k + (size_t)i * K] * a[k + (size_t)j * K];
+        ref = 0.5 * s + 2.0 * ref;
+      }
+      err = fmax(err, fabs(ref - r[i + (size_t)j * N]));   /* the upper part must be untouched */
+    }
+  printf("dsyrk LT %dx%d max error %.3e\n", N, K, err);
+  CHECK(err < 1e-12, "dsyrk error %.3e", err);
+  free(a), free(c), free(r);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(C);
+
+  dplasma_desc_t *Z = dmat(ctx, dplasmaComplexDouble, nb, N, K), *W = dmat(ctx, dplasmaComplexDouble, nb, N, N);
+  dplasma_zplrnt(ctx, 0, Z, 9);
+  dplasma_zplghe(ctx, 0.0, dplasmaUpperLower, W, 10);
+  double complex *z = malloc(sizeof(double complex) * N * K), *w = malloc(sizeof(double complex) * N * N);
+  double complex *q = malloc(sizeof(double complex) * N * N);
+  dplasma_desc_get_lapack(Z, z, N);
+  dplasma_desc_get_lapack(W, w, N);
+  CHECK(dplasma_zherk(ctx, dplasmaUpper, dplasmaNoTrans, -1.0, Z, 0.5, W) == 0, "zherk: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(W, q, N);
+  err = 0;
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i <= j; ++i) {
+      double complex s = 0;
+      for (int k = 0; k < K; ++k) s += z[i + (size_t)k * N] * conj(z[j + (size_t)k * N]);
+      err = fmax(err, cabs(-s + 0.5 * w[i + (size_t)j * N] - q[i + (size_t)j * N]));
+    }
+  printf("zherk UN %dx%d max error %.3e\n", N, K, err);
+  CHECK(err < 1e-11, "zherk error %.3e", err);
+  free(z), free(w), free(q);
+  dplasma_desc_destroy(Z), dplasma_desc_destroy(W);
+}
+
+/* element-wise maps: dgeadd (B = 2 A^T - B), dtradd (lower), dlacpy (upper), dlaset (lower), dlascal */
+static void test_maps(dplasma_context_t *ctx) {
+  const int M = 260, N = 190, nb = 64;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, N, M), *B = dmat(ctx, dplasmaRealDouble, nb, M, N);
+  dplasma_desc_t *S = dmat(ctx, dplasmaRealDouble, nb, M, M), *T = dmat(ctx, dplasmaRealDouble, nb, M, M);
+  dplasma_dplrnt(ctx, 0, A, 21);
+  dplasma_dplrnt(ctx, 0, B, 22);
+  dplasma_dplrnt(ctx, 0, S, 23);
+  dplasma_dplrnt(ctx, 0, T, 24);
+  double *a = malloc(sizeof(double) * N * M), *b = malloc(sizeof(double) * M * N), *r = malloc(sizeof(double) * M * N);
+  double *s0 = malloc(sizeof(double) * M * M), *t0 = malloc(sizeof(double) * M * M), *t1 = malloc(sizeof(double) * M * M);
+  dplasma_desc_get_lapack(A, a, N);
+  dplasma_desc_get_lapack(B, b, M);
+  dplasma_desc_get_lapack(S, s0, M);
+  dplasma_desc_get_lapack(T, t0, M);
+  CHECK(dplasma_dgeadd(ctx, dplasmaTrans, 2.0, A, -1.0, B) == 0, "dgeadd: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(B, r, M);
+  double err = 0;
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i < M; ++i) err = fmax(err, fabs(2.0 * a[j + (size_t)i * N] - b[i + (size_t)j * M] - r[i + (size_t)j * M]));
+  CHECK(err < 1e-14, "dgeadd error %.3e", err);
+  /* T := S on the upper triangle (lacpy), T := 3 S + T on the lower (tradd), T := -2 T (lascal) */
+  CHECK(dplasma_dlacpy(ctx, dplasmaUpper, S, T) == 0, "dlacpy: %s", dplasma_last_error());
+  CHECK(dplasma_dtradd(ctx, dplasmaLower, dplasmaNoTrans, 3.0, S, 1.0, T) == 0, "dtradd: %s", dplasma_last_error());
+  CHECK(dplasma_dlascal(ctx, dplasmaUpperLower, -2.0, T) == 0, "dlascal: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(T, t1, M);
+  err = 0;
+  for (int j = 0; j < M; ++j)
+    for (int i = 0; i < M; ++i) {
+      const double sv = s0[i + (size_t)j * M], tv = t0[i + (size_t)j * M];
+      double ref = i < j ? sv : (i == j ? sv + 3.0 * sv : tv + 3.0 * sv);
+      err = fmax(err, fabs(-2.0 * ref - t1[i + (size_t)j * M]));
+    }
+  CHECK(err < 1e-13, "lacpy/tradd/lascal error %.3e", err);
+  CHECK(dplasma_dlaset(ctx, dplasmaLower, 0.25, 4.0, T) == 0, "dlaset: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(T, t0, M);
+  err = 0;
+  for (int j = 0; j < M; ++j)
+    for (int i = 0; i < M; ++i) {
+      const double ref = i > j ? 0.25 : (i == j ? 4.0 : t1[i + (size_t)j * M]);
+      err = fmax(err, fabs(ref - t0[i + (size_t)j * M]));
+    }
+  CHECK(err == 0, "dlaset error %.3e", err);
+  printf("native maps (geadd, lacpy, tradd, lascal, laset) ok\n");
+  free(a), free(b), free(r), free(s0), free(t0), free(t1);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(B), dplasma_desc_destroy(S), dplasma_desc_destroy(T);
+}
+
 /* op(T) X = alpha B (left) / X op(T) = alpha B (right) for the given variant; T = plghe (well conditioned) */
 static void test_dtrsm(dplasma_context_t *ctx, int side, int uplo, int trans) {
   const int n = 400, nrhs = 150, nb = 128;
@@ -277,6 +374,8 @@ int main(int argc, char **argv) {
   test_dtrsm(ctx, dplasmaRight, dplasmaUpper, dplasmaNoTrans);
   test_dtrsm(ctx, dplasmaRight, dplasmaLower, dplasmaTrans);
   test_zpotrf_spotrf(ctx);
+  test_rank_k(ctx);
+  test_maps(ctx);
   test_taskpools(ctx);
   /* an operation without a native implementation fails cleanly */
   dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
