@@ -80,6 +80,8 @@ NatProgram* nat_lacpy(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t
 NatProgram* nat_laset(dplasma_context_t* ctx, int prec, int uplo, const void* alpha, const void* beta,
                       dplasma_desc_t* A);
 NatProgram* nat_lascal(dplasma_context_t* ctx, int prec, int uplo, const void* alpha, dplasma_desc_t* A);
+double nat_lange(dplasma_context_t* ctx, int prec, int ntype, dplasma_desc_t* A);   // NAN + error on failure
+double nat_lantr(dplasma_context_t* ctx, int prec, int ntype, int uplo, int diag, dplasma_desc_t* A);
 int nat_execute(dplasma_context_t* ctx, NatProgram* P);     // run + wait + info, frees P
 dplasma_taskpool_t* nat_wrap(NatProgram* P);
 void nat_fini(dplasma_context_t* ctx);

@@ -15,11 +15,13 @@
 // program is built (dplasma_<p><op>_New), so a run only launches kernels.
 //
 // Scope: one process, one GPU; s/d/c/z potrf, potrs, posv, gemm, trsm (all 8 side/uplo/trans
-// variants), herk / syrk, the element-wise maps (geadd, tradd, lacpy, laset, lascal), plghe, plrnt.
+// variants), herk / syrk, the element-wise maps (geadd, tradd, lacpy, laset, lascal), the norms lange /
+// lantr, plghe, plrnt.
 // Every other entry point returns an error on a native context.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -50,6 +52,8 @@ int dpl_geadd(int prec, int part, int trans, int nitems, const void* items, int 
               const void* A, int lda, const void* beta, void* B, int ldb, int copy, hipStream_t st);
 int dpl_lascal(int prec, int part, int nitems, const void* items, int mmax, int nmax, const void* alpha, void* A,
                int lda, hipStream_t st);
+int dpl_tile_norm(int prec, int kind, int part, int unit, int nitems, const void* items, const void* A, int lda,
+                  double* out, int ostride, hipStream_t st);
 }
 
 namespace {
@@ -769,6 +773,85 @@ NatProgram* nat_lascal(dplasma_context_t* ctx, int prec, int uplo, const void* a
     return dpl_lascal(prec, part, mb->n(), mb->items(), mb->mm, mb->nn, al.ptr(), a, lda, s);
   }, {});
   return P;
+}
+
+// ----------------------------------------------------------------------------- norms
+// lange / lantr (models/aux.py): one dpl_tile_norm launch gives per-tile partials (max, column sums,
+// row sums or a scaled sum of squares), combined on the host -- the reference's STEP1..STEP4 reduction
+// of zlange_*_cyclic.jdf on one process.
+enum { NORM_ONE = 171, NORM_FRB = 174, NORM_INF = 175, NORM_MAX = 177, UNIT = 132 };
+
+static double norm_tiles(NatDesc& A, int ntype, int uplo, bool unit, hipStream_t st, bool& ok) {
+  ok = false;
+  const int kind = ntype == NORM_MAX ? 0 : ntype == NORM_ONE ? 1 : ntype == NORM_INF ? 2 : ntype == NORM_FRB ? 3 : -1;
+  if (kind < 0) return 0.0;
+  std::vector<TileItem> it;
+  std::vector<std::pair<int, int>> mn;
+  int mm = 0, nn = 0;
+  for (int n = 0; n < A.nt; ++n)
+    for (int m = 0; m < A.mt; ++m) {
+      if ((uplo == LOWER && m < n) || (uplo == UPPER && m > n)) continue;
+      it.push_back(TileItem{A.off(m, n), 0, A.rows(m), A.cols(n), m * A.mb, n * A.nb});
+      mn.emplace_back(m, n);
+      mm = std::max(mm, A.rows(m));
+      nn = std::max(nn, A.cols(n));
+    }
+  if (it.empty()) { ok = true; return 0.0; }
+  const int os = kind == 0 ? 1 : kind == 1 ? nn : kind == 2 ? mm : 2;
+  DevPtr d = dev_upload(it), out = dev_alloc(sizeof(double) * it.size() * os, true);
+  if (!d || !out) return 0.0;
+  if (dpl_tile_norm(A.prec, kind, part_of(uplo), unit ? 1 : 0, (int)it.size(), d->p, A.data, A.lld,
+                    (double*)out->p, os, st) != 0)
+    return 0.0;
+  std::vector<double> h(it.size() * os);
+  if (hipStreamSynchronize(st) != hipSuccess ||
+      hipMemcpy(h.data(), out->p, sizeof(double) * h.size(), hipMemcpyDeviceToHost) != hipSuccess)
+    return 0.0;
+  ok = true;
+  double r = 0.0;
+  if (kind == 0) {
+    for (double v : h) r = std::max(r, v);
+  } else if (kind == 3) {   // (scale, ssq) per tile -> sqrt(sum scale^2 ssq), rescaled by the largest scale
+    double big = 0.0;
+    for (size_t t = 0; t < it.size(); ++t) big = std::max(big, h[2 * t]);
+    if (big > 0) {
+      for (size_t t = 0; t < it.size(); ++t) {
+        const double q = h[2 * t] / big;
+        r += q * q * h[2 * t + 1];
+      }
+      r = big * std::sqrt(r);
+    }
+  } else {                  // column (one) / row (inf) sums over the tiles of a tile column / row
+    std::vector<double> acc(kind == 1 ? A.n : A.m, 0.0);
+    for (size_t t = 0; t < it.size(); ++t) {
+      const int base = kind == 1 ? mn[t].second * A.nb : mn[t].first * A.mb;
+      const int len = kind == 1 ? A.cols(mn[t].second) : A.rows(mn[t].first);
+      for (int j = 0; j < len; ++j) acc[base + j] += h[t * os + j];
+    }
+    for (double v : acc) r = std::max(r, v);
+  }
+  return r;
+}
+
+double nat_lange(dplasma_context_t* ctx, int prec, int ntype, dplasma_desc_t* dA) {
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!same_ctx(ctx->nat, {A}, prec)) { dpl_set_error("lange: descriptor of another context"); return NAN; }
+  bool ok;
+  const double r = norm_tiles(*A, ntype, UPPERLOWER, false, ctx->nat->st[1], ok);
+  if (!ok) { dpl_set_error("lange: unsupported norm or kernel failure"); return NAN; }
+  return r;
+}
+
+double nat_lantr(dplasma_context_t* ctx, int prec, int ntype, int uplo, int diag, dplasma_desc_t* dA) {
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!same_ctx(ctx->nat, {A}, prec) || (uplo != LOWER && uplo != UPPER)) {
+    dpl_set_error("lantr: bad descriptor or uplo");
+    return NAN;
+  }
+  bool ok;
+  const double r = norm_tiles(*A, ntype, uplo, diag == UNIT, ctx->nat->st[1], ok);
+  if (!ok) { dpl_set_error("lantr: unsupported norm or kernel failure"); return NAN; }
+  return r;
 }
 
 static NatProgram* generator(dplasma_context_t* ctx, int prec, int kind, int uplo, const Scalar& bump,

@@ -220,6 +220,49 @@ static void test_maps(dplasma_context_t *ctx) {
   dplasma_desc_destroy(A), dplasma_desc_destroy(B), dplasma_desc_destroy(S), dplasma_desc_destroy(T);
 }
 
+/* dlange (max / one / inf / Frobenius) and zlantr (lower, unit) against host loops; ragged tiles */
+static void test_norms(dplasma_context_t *ctx) {
+  const int M = 300, N = 170, nb = 64;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, M, N);
+  dplasma_dplrnt(ctx, 0, A, 31);
+  double *a = malloc(sizeof(double) * M * N);
+  dplasma_desc_get_lapack(A, a, M);
+  double mx = 0, one = 0, inf = 0, fr = 0;
+  double *rs = calloc(M, sizeof(double));
+  for (int j = 0; j < N; ++j) {
+    double cs = 0;
+    for (int i = 0; i < M; ++i) {
+      const double v = fabs(a[i + (size_t)j * M]);
+      mx = fmax(mx, v), cs += v, rs[i] += v, fr += v * v;
+    }
+    one = fmax(one, cs);
+  }
+  for (int i = 0; i < M; ++i) inf = fmax(inf, rs[i]);
+  fr = sqrt(fr);
+  const double g[4] = {dplasma_dlange(ctx, dplasmaMaxNorm, A), dplasma_dlange(ctx, dplasmaOneNorm, A),
+                       dplasma_dlange(ctx, dplasmaInfNorm, A), dplasma_dlange(ctx, dplasmaFrobeniusNorm, A)};
+  const double r[4] = {mx, one, inf, fr};
+  for (int q = 0; q < 4; ++q) CHECK(fabs(g[q] - r[q]) <= 1e-13 * r[q], "dlange kind %d: %.15e vs %.15e", q, g[q], r[q]);
+  free(a), free(rs);
+  dplasma_desc_destroy(A);
+
+  dplasma_desc_t *Z = dmat(ctx, dplasmaComplexDouble, nb, N, N);
+  dplasma_zplrnt(ctx, 0, Z, 32);
+  double complex *z = malloc(sizeof(double complex) * N * N);
+  dplasma_desc_get_lapack(Z, z, N);
+  double one_z = 0;
+  for (int j = 0; j < N; ++j) {
+    double cs = 1.0;   /* unit diagonal */
+    for (int i = j + 1; i < N; ++i) cs += cabs(z[i + (size_t)j * N]);
+    one_z = fmax(one_z, cs);
+  }
+  const double gz = dplasma_zlantr(ctx, dplasmaOneNorm, dplasmaLower, dplasmaUnit, Z);
+  CHECK(fabs(gz - one_z) <= 1e-13 * one_z, "zlantr one: %.15e vs %.15e", gz, one_z);
+  printf("native norms (dlange max/one/inf/frb, zlantr) ok\n");
+  free(z);
+  dplasma_desc_destroy(Z);
+}
+
 /* op(T) X = alpha B (left) / X op(T) = alpha B (right) for the given variant; T = plghe (well conditioned) */
 static void test_dtrsm(dplasma_context_t *ctx, int side, int uplo, int trans) {
   const int n = 400, nrhs = 150, nb = 128;
@@ -376,6 +419,7 @@ int main(int argc, char **argv) {
   test_zpotrf_spotrf(ctx);
   test_rank_k(ctx);
   test_maps(ctx);
+  test_norms(ctx);
   test_taskpools(ctx);
   /* an operation without a native implementation fails cleanly */
   dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
