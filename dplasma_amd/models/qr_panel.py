@@ -135,13 +135,20 @@ def _offsets(C, rows, cols):
     return R[:, None] + Cc[None, :]
 
 
+# W = V^T C is split over S row groups (partials summed) until a launch has about this many
+# 128 x 128 output workgroups (DPLASMA_QR_SPLIT_WG)
+QR_SPLIT_TARGET_WG = int(os.environ.get("DPLASMA_QR_SPLIT_WG", 512))
+
+
 class _Left:
     """C(rows, cols) := op(Q)^T-style block reflector application from the left:
     W = V^T C (split over S row groups, partials summed), W' = op(T) W, C -= V W'.
     Batches are built with whole-array numpy operations (millions of tiles at 64k)."""
 
-    def __init__(self, C, rows, voff, kf, cols, target_wg=512):
+    def __init__(self, C, rows, voff, kf, cols, target_wg=None):
         self.kf = kf
+        if target_wg is None:
+            target_wg = QR_SPLIT_TARGET_WG
         self.empty = not cols or not rows
         self.S, self.wlen = 1, 0
         if self.empty:
@@ -187,8 +194,10 @@ class _Left:
 class _Right:
     """C(rows, cols) := C op(Q) (cols = the reflector rows): W = C V, W' = W op(T), C -= W' V^T."""
 
-    def __init__(self, C, crows, vcols, voff, kf, target_wg=512, split=True):
+    def __init__(self, C, crows, vcols, voff, kf, target_wg=None, split=True):
         self.kf = kf
+        if target_wg is None:
+            target_wg = QR_SPLIT_TARGET_WG
         crows, vcols = list(crows), list(vcols)
         hc = np.array([C.tile_rows(i) for i in crows], dtype=np.int64)
         roff = np.concatenate([[0], np.cumsum(hc)[:-1]]).astype(np.int64)
