@@ -18,7 +18,7 @@ def _potrf_worker(rank, world, P, N, NB, uplo, prec):
     return info, ok, res, A.to_dense_local()
 
 
-@pytest.mark.parametrize("world,P", [(2, 1), (2, 2), (4, 2), (3, 1)])
+@pytest.mark.parametrize("world,P", [(2, 1), (2, 2), (4, 2), (3, 1), (4, 4)])
 @pytest.mark.parametrize("uplo", [122, 121])
 def test_potrf_distributed(world, P, uplo):
     N, NB = 150, 19
