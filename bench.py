@@ -3,7 +3,8 @@
 
 Metric and config are the ones named in BASELINE.json.  One process per GPU
 (``torch.distributed.run --nproc-per-node N``; RCCL over xGMI), 2-D
-block-cyclic P x Q grid (8 -> 2x4 as BASELINE.json names it, 4 -> 4x1, 2 -> 2x1, 1 -> 1x1).  The input is
+block-cyclic P x Q grid (8 -> 2x4 as BASELINE.json names it; 2 and 4 -> the whole panel axis:
+P x 1 for lower, 1 x Q for upper).  The input is
 the reference's SPD test matrix ``dplghe(bump=N, seed=3872)`` (synthetic, LCG
 generated on the GPU, bit-identical to the reference generator).
 
@@ -43,6 +44,8 @@ def main():
     ap.add_argument("-N", "--N", type=int, default=65536)
     ap.add_argument("--nb", type=int, default=512)
     ap.add_argument("-P", type=int, default=None)
+    ap.add_argument("--uplo", choices=("L", "U"), default="L",
+                    help="triangle factored (the reference's testing_zpotrf.c defaults to Upper)")
     ap.add_argument("--no-check", dest="check", action="store_false",
                     help="skip the (untimed, default-on) residual check of the last factorisation")
     ap.add_argument("--check", dest="check", action="store_true", help="(default) verify the last factorisation")
@@ -70,20 +73,27 @@ def main():
 
     P = args.P
     if P is None:
-        # lower Cholesky: a P x 1 grid splits the panel TRSM over P ranks and replaces the row broadcast
-        # of the panel by one all-gather ((P-1)/P of it per rank, vs all of it for the 1 x 2 non-owner)
-        # -- tools/sim_potrf.py: 2x1 88 % vs 1x2 75 %, 4x1 59 % vs 2x2 54 % scaling efficiency; 8 GPUs
-        # keep the configuration BASELINE.json names (2 x 4)
-        P = {1: 1, 2: 2, 4: 4, 8: 2}.get(world, None)
+        # The panel of lower Cholesky is a tile column (spread over the P process rows), that of upper a
+        # tile row (spread over the Q columns).  A grid whose panel axis holds every rank (P x 1 for
+        # lower, 1 x Q for upper) splits the panel TRSM over all of them and moves the panel by one
+        # all-gather instead of a broadcast to ranks that own none of it -- tools/sim_potrf.py: 88 vs 75 %
+        # on 2 GPUs, 59 vs 54 % on 4.  8 GPUs keep the grid BASELINE.json names (2 x 4).
+        if world == 8:
+            P = 2
+        elif world in (2, 4):
+            P = world if args.uplo == "L" else 1
+        else:
+            P = None
     ctx = dp.init(P=P, device="cpu") if args.cpu else dp.init(P=P)
     rank = ctx.rank
     N, NB = args.N, args.nb
-    A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N, name="A", uplo=dp.dplasmaLower)
-    dp.dplghe(ctx, float(N), dp.dplasmaLower, A, 3872)
+    uplo = dp.dplasmaLower if args.uplo == "L" else dp.dplasmaUpper
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N, name="A", uplo=uplo)
+    dp.dplghe(ctx, float(N), uplo, A, 3872)
     A0 = A.data.clone()
     ctx.sync()
     t0 = time.perf_counter()
-    tp = dp.dpotrf_New(ctx, dp.dplasmaLower, A)
+    tp = dp.dpotrf_New(ctx, uplo, A)
     t_enq = time.perf_counter() - t0
     flops = tp.flops
 
@@ -124,7 +134,7 @@ def main():
         A_orig = A.like()
         A_orig.data.copy_(A0)
         del A0
-        ok, res = dp.check_potrf(ctx, dp.dplasmaLower, A, A_orig, verbose=(rank == 0))
+        ok, res = dp.check_potrf(ctx, uplo, A, A_orig, verbose=(rank == 0))
         t_check = time.perf_counter() - tc
         del A_orig
     if rank == 0:
@@ -149,7 +159,7 @@ def main():
             "residual": res,
             "check_s": round(t_check, 2) if args.check else None,
             "enq_s": round(t_enq, 3),
-            "config": {"model": "dpotrf (lower, 2D block-cyclic tiles)", "N": N, "NB": NB, "global_batch": 1,
+            "config": {"model": f"dpotrf ({'lower' if args.uplo == 'L' else 'upper'}, 2D block-cyclic tiles)", "N": N, "NB": NB, "global_batch": 1,
                        "seq_len": N, "parallelism": f"{ctx.P}x{ctx.Q} block-cyclic (one rank per GPU)"},
         }
         print(json.dumps(out), flush=True)
