@@ -152,6 +152,8 @@ def main():
     ap.add_argument("--lat", type=float, default=20.0, help="us per message")
     ap.add_argument("-D", type=int, default=4)
     ap.add_argument("--calibrate", action="store_true")
+    ap.add_argument("--uplo", choices=("L", "U"), default="L",
+                    help="U: upper Cholesky on P x Q is lower on Q x P (its panel is a tile row, spread over Q)")
     a = ap.parse_args()
     m = Model(bw=a.bw * 1e9, lat=a.lat * 1e-6)
     fl = lambda n: n ** 3 / 3 + n ** 2 / 2 + n / 6  # noqa: E731
@@ -163,7 +165,7 @@ def main():
     base = None
     for g in a.grids.split(","):
         P, Q = (int(x) for x in g.split("x"))
-        s = simulate(a.N, a.nb, P, Q, m, a.D)
+        s = simulate(a.N, a.nb, *((P, Q) if a.uplo == "L" else (Q, P)), m, a.D)
         tf = fl(a.N) / s / 1e12
         base = base or tf
         print(f"{P}x{Q} N={a.N}: model {s * 1e3:8.1f} ms  {tf:6.1f} TF/s  {100 * tf / (P * Q * PEAK / 1e12):5.1f}% of "
