@@ -56,6 +56,9 @@ assert DAG_ITEM.itemsize == 96
 R, W, RW = 1, 2, 3
 
 MULTISTREAM = True  # single-GPU DAGs: critical-path stream + bulk stream
+# DPLASMA_PTG_TO_DTD=1: every tile DAG is re-executed through the DTD front end (TileDAG._ptg_to_dtd)
+import os as _os  # noqa: E402
+PTG_TO_DTD = [_os.environ.get("DPLASMA_PTG_TO_DTD", "0") == "1"]
 CRIT_SLACK = 0      # tasks with at most this much slack (levels) go to the critical stream
 
 _MID_SHIFT, _M_SHIFT = 44, 22
@@ -187,6 +190,7 @@ class TileDAG:
         self._chunks = []           # (kind id, ops (n, R) int64, ext (n, 3) int32)
         self.flops = 0.0
         self.info = None
+        self.no_dtd = False         # the DTD engine's own windows (never re-routed through DTD)
 
     # ------------------------------------------------------------ registration
     def mat(self, M) -> int:
@@ -278,9 +282,41 @@ class TileDAG:
         return out
 
     # ------------------------------------------------------------ compile
+    def _ptg_to_dtd(self) -> Optional[Taskpool]:
+        """Re-execute this task graph through the DTD front end (the reference's ``--mca mca_pins
+        ptg_to_dtd`` test mode, tests/Testings.cmake:7,11-12,33-36): every task is inserted in program
+        order with its tiles' access modes and the executing role as AFFINITY, and the dependencies
+        are rediscovered by the DTD engine.  None when a task cannot be expressed (Python-body kinds
+        or optional roles left empty): the graph then runs as built."""
+        from . import dtd
+        if any(self.kinds[k].body is not None or (o < 0).any() for k, o, _, _ in self._chunks):
+            return None
+        dt = dtd.DTDTaskpool(self.ctx, self.name + "[ptg_to_dtd]", window=0)
+        mask = (1 << 22) - 1
+        for k, o, e, _ in self._chunks:
+            K = self.kinds[k]
+            tc = dt.task_class(K.name, kind=K)
+            for t in range(len(o)):
+                args = []
+                for r, key in enumerate(o[t]):
+                    key = int(key)
+                    ref = dtd.tile_of(self.mats[key >> _MID_SHIFT], (key >> _M_SHIFT) & mask, key & mask)
+                    args.append((ref, K.roles[r][1] | (dtd.AFFINITY if r == K.exec_role else 0)))
+                dt.insert_task(tc, *args, tuple(int(x) for x in e[t]))
+        self._chunks = []
+        dt.flops = self.flops
+        tp = dt.compile()
+        tp.name = self.name
+        tp.ptg_to_dtd = True
+        return tp
+
     def compile(self) -> Taskpool:
         ctx = self.ctx
         me, world = ctx.rank, ctx.world
+        if PTG_TO_DTD[0] and not self.no_dtd and self._chunks:
+            tp = self._ptg_to_dtd()
+            if tp is not None:
+                return tp
         tp = Taskpool(self.name, ctx)
         tp.flops = self.flops
         if not self._chunks:

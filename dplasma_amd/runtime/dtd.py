@@ -92,6 +92,7 @@ class DTDTaskpool:
 
     def _new_dag(self):
         self.dag = TileDAG(self.ctx, f"{self.name}[{getattr(self, 'windows_run', 0)}]")
+        self.dag.no_dtd = True
 
     def task_class(self, name: str, body: Optional[Callable] = None, kind: Optional[Kind] = None) -> TaskClass:
         return TaskClass(name, body, kind)

@@ -69,6 +69,9 @@ def _parse(argv):
                     help="recursive sub-tile size hint (dplasma_z*_setrecursive)")
     ap.add_argument("-c", "--cores", type=int, default=0, help="host worker threads (CPU path)")
     ap.add_argument("-m", "--thread_multi", action="store_true", help="accepted for compatibility")
+    ap.add_argument("--ptg-to-dtd", "--ptg_to_dtd", action="store_true", dest="ptg_to_dtd",
+                    help="re-execute every tile-DAG algorithm through the DTD front end (the reference's "
+                         "--mca mca_pins ptg_to_dtd)")
     ap.add_argument("-o", "--scheduler", default="", help="ready-queue policy of the task issue order "
                     "(LFQ/LTQ/AP/LHQ/SPQ/PBQ: priority first, IP: inverse priority, GD: FIFO, LL: LIFO, RND: random; "
                     "default: program order); multi-process runs issue in program order")
@@ -91,6 +94,9 @@ class Harness:
                 dist.init_process_group("gloo")
         import dplasma_amd as dp
         self.dp = dp
+        if a.ptg_to_dtd:
+            from .runtime import dag as _dag
+            _dag.PTG_TO_DTD[0] = True
         P = a.P or None
         if a.cores > 0:
             torch.set_num_threads(a.cores)

@@ -44,6 +44,8 @@ def _run(args, nproc=1):
     # solvers, reductions, QR tree validation
     "dgesv_incpiv -N 150 -t 32 -i 8 -K 3 -x", "dgesvd -M 150 -N 120 -t 24 -x", "zhbrdt -N 60 -t 6 -x",
     "dpivgen -M 400 -N 200 -t 20",
+    # PTG -> DTD re-execution of the tile-DAG algorithms (the reference's --mca mca_pins ptg_to_dtd)
+    "dgetrf_incpiv -N 150 -t 32 -i 8 -x --ptg-to-dtd", "zgelqf -M 100 -N 150 -t 25 -i 5 -x --ptg-to-dtd",
 ])
 def test_cli_single(args):
     r = _run(args.split())
