@@ -457,15 +457,39 @@ __global__ __launch_bounds__(64) void k_trsm_rb(const RbItem* __restrict__ items
     }
   };
   d4_t C[NBLK][2];
+  // Upper: a strip row is a COLUMN of U(k, i) (contiguous in memory) and the T-layout's 16 row lanes
+  // would stride by ldb (32-byte segments).  Stage each 16 x 32 block through LDS instead: lane l
+  // moves 8 consecutive elements of strip row l / 4 (4 lanes = one 256-byte run), then reads its
+  // T-layout values back (row stride 33 doubles: conflict-free).
+  __shared__ double stg[LOWER ? 1 : TR_ROWS * 33];
+  const int srow = l >> 2, scol = (l & 3) * 8;
+  const bool sok = srow < it.rows;
+  if constexpr (LOWER) {
 #pragma unroll
-  for (int jb = 0; jb < NBLK; ++jb)
+    for (int jb = 0; jb < NBLK; ++jb)
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+      for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int col = RB * jb + 16 * h + (l >> 4) + 4 * r;
-        C[jb][h][r] = (rok && col < n) ? Bb[row * sib + col * sjb] : 0.0;
+        for (int r = 0; r < 4; ++r) {
+          const int col = RB * jb + 16 * h + (l >> 4) + 4 * r;
+          C[jb][h][r] = (rok && col < n) ? Bb[row * sib + col * sjb] : 0.0;
+        }
+  } else {
+#pragma unroll
+    for (int jb = 0; jb < NBLK; ++jb) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int col = RB * jb + scol + e;
+        stg[srow * 33 + scol + e] = (sok && col < n) ? Bb[(long long)srow * ldb + col] : 0.0;
       }
+      __syncthreads();
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) C[jb][h][r] = rok ? stg[row * 33 + 16 * h + (l >> 4) + 4 * r] : 0.0;
+      __syncthreads();
+    }
+  }
   double mc[20];
 #pragma unroll
   for (int k = 0; k < NBLK; ++k) {
@@ -483,9 +507,22 @@ __global__ __launch_bounds__(64) void k_trsm_rb(const RbItem* __restrict__ items
       for (int r = 0; r < 4; ++r) {
         const int c = 16 * h + (l >> 4) + 4 * r;
         acc[r] *= mc[12 + 4 * h + r];
-        if (rok && RB * k + c < n) Bb[row * sib + (RB * k + c) * sjb] = acc[r];  // final L(R,k)
+        if constexpr (LOWER) {
+          if (rok && RB * k + c < n) Bb[row * sib + (RB * k + c) * sjb] = acc[r];  // final L(R,k)
+        } else {
+          stg[row * 33 + c] = acc[r];
+        }
       }
       C[k][h] = acc;
+    }
+    if constexpr (!LOWER) {  // final U(k, R) columns: back through LDS, 256-byte runs per strip row
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int col = RB * k + scol + e;
+        if (sok && col < n) Bb[(long long)srow * ldb + col] = stg[srow * 33 + scol + e];
+      }
+      __syncthreads();
     }
     double xm[8];
 #pragma unroll
