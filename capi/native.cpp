@@ -800,6 +800,8 @@ static double norm_tiles(NatDesc& A, int ntype, int uplo, bool unit, hipStream_t
   const int os = kind == 0 ? 1 : kind == 1 ? nn : kind == 2 ? mm : 2;
   DevPtr d = dev_upload(it), out = dev_alloc(sizeof(double) * it.size() * os, true);
   if (!d || !out) return 0.0;
+  // the norm reads A after everything already queued on the context (both streams)
+  if (hipDeviceSynchronize() != hipSuccess) return 0.0;
   if (dpl_tile_norm(A.prec, kind, part_of(uplo), unit ? 1 : 0, (int)it.size(), d->p, A.data, A.lld,
                     (double*)out->p, os, st) != 0)
     return 0.0;

@@ -34,6 +34,7 @@ once at compile time ("ENQ" phase, excluded from timing as in
 """
 from __future__ import annotations
 
+import os
 from collections import defaultdict
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -57,8 +58,7 @@ R, W, RW = 1, 2, 3
 
 MULTISTREAM = True  # single-GPU DAGs: critical-path stream + bulk stream
 # DPLASMA_PTG_TO_DTD=1: every tile DAG is re-executed through the DTD front end (TileDAG._ptg_to_dtd)
-import os as _os  # noqa: E402
-PTG_TO_DTD = [_os.environ.get("DPLASMA_PTG_TO_DTD", "0") == "1"]
+PTG_TO_DTD = [os.environ.get("DPLASMA_PTG_TO_DTD", "0") == "1"]
 CRIT_SLACK = 0      # tasks with at most this much slack (levels) go to the critical stream
 
 _MID_SHIFT, _M_SHIFT = 44, 22

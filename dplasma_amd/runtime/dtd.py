@@ -95,6 +95,9 @@ class DTDTaskpool:
         self.dag.no_dtd = True
 
     def task_class(self, name: str, body: Optional[Callable] = None, kind: Optional[Kind] = None) -> TaskClass:
+        """A task class with a Python ``body`` (called per task with its tile views and values) or a
+        batched tile ``kind``: its tasks then pass exactly the kind's roles as tile arguments (same
+        access modes) and their (m, n, k) extents as the only value."""
         return TaskClass(name, body, kind)
 
     def _kind_for(self, tc: TaskClass, modes: tuple, affinity: int) -> Kind:
