@@ -68,6 +68,8 @@ NatProgram* nat_trsm(dplasma_context_t* ctx, int prec, int side, int uplo, int t
 NatProgram* nat_plghe(dplasma_context_t* ctx, int prec, double bump, int uplo, dplasma_desc_t* A,
                       unsigned long long seed);
 NatProgram* nat_plrnt(dplasma_context_t* ctx, int prec, int diagdom, dplasma_desc_t* A, unsigned long long seed);
+NatProgram* nat_plgsy(dplasma_context_t* ctx, int prec, const void* bump, int uplo, dplasma_desc_t* A,
+                      unsigned long long seed);
 NatProgram* nat_herk(dplasma_context_t* ctx, int prec, int uplo, int trans, double alpha, dplasma_desc_t* A,
                      double beta, dplasma_desc_t* C);
 NatProgram* nat_syrk(dplasma_context_t* ctx, int prec, int uplo, int trans, const void* alpha, dplasma_desc_t* A,

@@ -16,7 +16,7 @@
 //
 // Scope: one process, one GPU; s/d/c/z potrf, potrs, posv, gemm, trsm (all 8 side/uplo/trans
 // variants), herk / syrk, the element-wise maps (geadd, tradd, lacpy, laset, lascal), the norms lange /
-// lantr, plghe, plrnt.
+// lantr, plghe, plgsy, plrnt.
 // Every other entry point returns an error on a native context.
 #include <hip/hip_runtime.h>
 
@@ -886,6 +886,11 @@ static NatProgram* generator(dplasma_context_t* ctx, int prec, int kind, int upl
 NatProgram* nat_plghe(dplasma_context_t* ctx, int prec, double bump, int uplo, dplasma_desc_t* A,
                       unsigned long long seed) {
   return generator(ctx, prec, 1, uplo, Scalar(prec, bump), A, seed, "plghe");
+}
+
+NatProgram* nat_plgsy(dplasma_context_t* ctx, int prec, const void* bump, int uplo, dplasma_desc_t* A,
+                      unsigned long long seed) {
+  return generator(ctx, prec, 2, uplo, Scalar(prec, bump), A, seed, "plgsy");
 }
 
 NatProgram* nat_plrnt(dplasma_context_t* ctx, int prec, int diagdom, dplasma_desc_t* A, unsigned long long seed) {

@@ -259,6 +259,16 @@ static void test_norms(dplasma_context_t *ctx) {
   const double gz = dplasma_zlantr(ctx, dplasmaOneNorm, dplasmaLower, dplasmaUnit, Z);
   CHECK(fabs(gz - one_z) <= 1e-13 * one_z, "zlantr one: %.15e vs %.15e", gz, one_z);
   printf("native norms (dlange max/one/inf/frb, zlantr) ok\n");
+  /* dplgsy == dplghe for a real matrix (same LCG stream, same bump on the diagonal) */
+  dplasma_desc_t *G1 = dmat(ctx, dplasmaRealDouble, nb, 150, 150), *G2 = dmat(ctx, dplasmaRealDouble, nb, 150, 150);
+  CHECK(dplasma_dplgsy(ctx, 7.0, dplasmaUpperLower, G1, 41) == 0, "dplgsy: %s", dplasma_last_error());
+  CHECK(dplasma_dplghe(ctx, 7.0, dplasmaUpperLower, G2, 41) == 0, "dplghe: %s", dplasma_last_error());
+  double *g1 = malloc(sizeof(double) * 150 * 150), *g2 = malloc(sizeof(double) * 150 * 150);
+  dplasma_desc_get_lapack(G1, g1, 150);
+  dplasma_desc_get_lapack(G2, g2, 150);
+  CHECK(memcmp(g1, g2, sizeof(double) * 150 * 150) == 0, "dplgsy differs from dplghe");
+  free(g1), free(g2);
+  dplasma_desc_destroy(G1), dplasma_desc_destroy(G2);
   free(z);
   dplasma_desc_destroy(Z);
 }
