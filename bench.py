@@ -36,6 +36,31 @@ BASELINE_METRIC = "GFLOP/s DPOTRF N=64k NB=512 at 1/2/4/8 MI355X; % of fp64 MFMA
 FP64_PEAK_GFLOPS = 78600.0  # per MI355X, datasheet
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn_ranks(n: int, cpu: bool) -> int:
+    """``--gpus N`` without a launcher: run this same command under ``torch.distributed.run`` with N
+    ranks (127.0.0.1 rendezvous) as a child process; returns its exit status.  Refuses (non-zero)
+    when fewer than N GPUs are visible -- a silent 1-GPU number reported as N would be invalid.
+    ``torch.cuda.device_count()`` does not initialise the GPU, so no exec/fork hazard here."""
+    import subprocess
+    if not cpu:
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} requested but only {have} GPU(s) are visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -54,7 +79,15 @@ def main():
                     help="dry run of the same multi-rank path on CPU ranks (gloo) -- plumbing tests only")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        sys.exit(f"bench.py: --gpus must be >= 1 (got {args.gpus})")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: start one rank per GPU ourselves (a child torch.distributed.run, before any GPU
+        # call in this process) and exit with its status
+        sys.exit(_spawn_ranks(args.gpus, args.cpu))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         local = int(os.environ.get("LOCAL_RANK", "0"))
