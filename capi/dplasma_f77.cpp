@@ -114,6 +114,18 @@ DPL_CAPI int dplasma_blacs_gridinit(dplasma_context_t* ctx) {
   return v;
 }
 
+// p?latsqr_ workspace size, as the reference wrapper reports it (dplasma_wrapper_pdlatsqr.c:257-258):
+// NB_A * (mloc + nloc + NB_A), local extents from numroc over the BLACS grid of DESCA
+static int latsqr_work(const int* desca) {
+  int ctxt = desca[1], nprow = 1, npcol = 1, myrow = 0, mycol = 0;
+  blacs_gridinfo_(&ctxt, &nprow, &npcol, &myrow, &mycol);
+  if (nprow < 1 || npcol < 1 || myrow < 0 || mycol < 0) nprow = npcol = 1, myrow = mycol = 0;
+  int gm = desca[2], gn = desca[3], mb = desca[4], nb = desca[5], rsrc = desca[6], csrc = desca[7];
+  const int mloc = numroc_(&gm, &mb, &myrow, &rsrc, &nprow);
+  const int nloc = numroc_(&gn, &nb, &mycol, &csrc, &npcol);
+  return nb * (mloc + nloc + nb);
+}
+
 // ---- p?gemm_, p?potrf_, p?getrf_, p?trsm_, p?trmm_, p?latsqr_
 #define DPL_F77_PREC(P, T)                                                                                      \
   DPL_CAPI void p##P##gemm_(const char* transa, const char* transb, int* m, int* n, int* k, T* alpha, T* a,      \
@@ -143,9 +155,14 @@ DPL_CAPI int dplasma_blacs_gridinit(dplasma_context_t* ctx) {
                          iv(ia), iv(ja), desc_list(desca), dpl_arg_ptr(b), iv(ib), iv(jb), desc_list(descb)});   \
   }                                                                                                              \
   DPL_CAPI void p##P##latsqr_(int* m, int* n, T* a, int* ia, int* ja, int* desca, T* tau, T* work, int* lwork,   \
-                              int* info) { DplGil g;                                                             \
-    (void)work;                                                                                                  \
-    (void)lwork;                                                                                                 \
+                              int* info) {                                                                     \
+    *info = 0;                                                                                                   \
+    if (*m == 0 || *n == 0) return;                                                                              \
+    /* optimal workspace NB_A * (Mp0 + Nq0 + NB_A) in WORK(1); LWORK = -1 is a pure query */                     \
+    const int lw = latsqr_work(desca);                                                                           \
+    if (work) work[0] = (T)lw;                                                                                   \
+    if (*lwork == -1) return;                                                                                    \
+    DplGil g;                                                                                                    \
     *info = f77("p" #P "latsqr_", {iv(m), iv(n), dpl_arg_ptr(a), iv(ia), iv(ja), desc_list(desca),               \
                                    dpl_arg_ptr(tau)});                                                           \
   }

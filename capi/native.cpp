@@ -477,7 +477,7 @@ bool add_potrf(NatProgram& P, int uplo, NatDesc& A) {
 // block row (left) / column (right) of B against the diagonal tile, then update the blocks still
 // to be solved with one GEMM launch (beta = alpha on the first step, 1 afterwards).
 bool add_trsm(NatProgram& P, int side, int uplo, int trans, int diag, const Scalar& alpha, NatDesc& A, NatDesc& B,
-              int stream) {
+              int stream, int first_dep = -1) {
   const int prec = B.prec;
   const bool left = side == LEFT, notrans = trans == NOTRANS;
   const int nk = left ? B.mt : B.nt;
@@ -489,7 +489,7 @@ bool add_trsm(NatProgram& P, int side, int uplo, int trans, int diag, const Scal
   char* a = A.data;
   char* bb = B.data;
   const int lda = A.lld, ldb = B.lld;
-  int prev = -1;
+  int prev = first_dep;   // the first solve follows this task (e.g. the factorisation's last one)
   for (int s = 0; s < nk; ++s) {
     const int k = order[s];
     const Scalar ak = s == 0 ? alpha : one;
@@ -530,13 +530,22 @@ bool add_trsm(NatProgram& P, int side, int uplo, int trans, int diag, const Scal
   return true;
 }
 
-bool add_potrs(NatProgram& P, int uplo, NatDesc& A, NatDesc& B) {
+// first_dep: the task the solves must follow (posv: the factorisation's last panel-stream task; the
+// solves run on the update stream, so stream order covers the factorisation's update-stream tasks)
+bool add_potrs(NatProgram& P, int uplo, NatDesc& A, NatDesc& B, int first_dep = -1) {
   const Scalar one(B.prec, 1.0);
   if (uplo == LOWER)
-    return add_trsm(P, LEFT, LOWER, NOTRANS, NONUNIT, one, A, B, 1) &&
+    return add_trsm(P, LEFT, LOWER, NOTRANS, NONUNIT, one, A, B, 1, first_dep) &&
            add_trsm(P, LEFT, LOWER, CONJTRANS, NONUNIT, one, A, B, 1);
-  return add_trsm(P, LEFT, UPPER, CONJTRANS, NONUNIT, one, A, B, 1) &&
+  return add_trsm(P, LEFT, UPPER, CONJTRANS, NONUNIT, one, A, B, 1, first_dep) &&
          add_trsm(P, LEFT, UPPER, NOTRANS, NONUNIT, one, A, B, 1);
+}
+
+// last task of a program on a stream (-1: none)
+int last_on(const NatProgram& P, int stream) {
+  for (int i = (int)P.tasks.size() - 1; i >= 0; --i)
+    if (P.tasks[i].stream == stream) return i;
+  return -1;
 }
 
 bool same_ctx(NatCtx* c, std::initializer_list<const NatDesc*> ds, int prec) {
@@ -575,7 +584,9 @@ NatProgram* nat_posv(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t*
   NatDesc *A = dA->nat, *B = dB ? dB->nat : nullptr;
   if (!same_ctx(ctx->nat, {B}, prec) || B->m != A->n || B->mb != A->nb)
     return fail(P, "posv: right-hand side does not conform");
-  if (!add_potrs(*P, uplo, *A, *B)) return fail(P, "posv: device allocation failed");
+  // the solves (update stream) start after the factorisation's last panel-stream task (POTRF / TRSM /
+  // NEAR of the last tiles): without this edge they could read A(nt-1, nt-1) before it is factored
+  if (!add_potrs(*P, uplo, *A, *B, last_on(*P, 0))) return fail(P, "posv: device allocation failed");
   return P;
 }
 
@@ -656,7 +667,25 @@ static NatProgram* rank_k(dplasma_context_t* ctx, int prec, int uplo, int trans,
   char *a = A->data, *cc = C->data;
   const int lda = A->lld, ldc = C->lld;
   const int ta = nt ? NOTRANS : ct, tb = nt ? ct : NOTRANS;
-  P->task(1, [=](hipStream_t s) { return g->launch(prec, ta, tb, alpha, a, lda, a, lda, beta, cc, ldc, s); }, {});
+  const int t = P->task(1, [=](hipStream_t s) { return g->launch(prec, ta, tb, alpha, a, lda, a, lda, beta, cc, ldc, s); }, {});
+  if (herm) {
+    // Hermitian rank-k (zherk): C's diagonal is real.  diag := (diag + conj(diag)) / 2 on the
+    // diagonal tiles (geadd, diagonal part, conjugate transpose of the tile onto itself)
+    std::vector<TileItem> d;
+    int mm = 0;
+    for (int k = 0; k < C->mt && k < C->nt; ++k) {
+      d.push_back(TileItem{C->off(k, k), C->off(k, k), C->rows(k), C->cols(k), k * C->mb, k * C->nb});
+      mm = std::max(mm, std::max(C->rows(k), C->cols(k)));
+    }
+    DevPtr dd = dev_upload(d);
+    if (!dd) return fail(P, std::string(name) + ": device allocation failed");
+    P->keep.push_back(dd);
+    const Scalar half(prec, 0.5);
+    const int n = (int)d.size();
+    P->task(1, [=](hipStream_t s) {
+      return dpl_geadd(prec, 5, CONJTRANS, n, dd->p, mm, mm, half.ptr(), cc, ldc, half.ptr(), cc, ldc, 0, s);
+    }, {t});
+  }
   return P;
 }
 
@@ -903,8 +932,14 @@ int nat_execute(dplasma_context_t* ctx, NatProgram* P) {
   if (!P) return -1;
   int rc = P->run();
   if (rc == 0) rc = P->wait();
-  const int res = rc == 0 ? P->result : -1;
+  int res = rc == 0 ? P->result : -1;
   if (rc != 0) dpl_set_error(("native " + P->name + ": kernel launch failed").c_str());
+  else if (res < 0) {
+    // the dataflow tile kernels report a bounded-spin timeout (or another internal failure) as a
+    // negative info: never a numerical result, always an error
+    dpl_set_error(("native " + P->name + ": tile kernel failure (info " + std::to_string(res) + ")").c_str());
+    res = -1;
+  }
   (void)ctx;
   delete P;
   return res;
@@ -1048,6 +1083,10 @@ int nat_wait(dplasma_context_t* ctx) {
 int nat_result(const dplasma_taskpool_t* tp) { return tp->nat->result; }
 
 void nat_free(dplasma_taskpool_t* tp) {
-  if (tp->nat->enqueued) (void)tp->nat->wait();
-  delete tp->nat;
+  NatProgram* P = tp->nat;
+  if (P->enqueued) (void)P->wait();
+  // a taskpool added but destroyed before dplasma_context_wait must leave its context's queue
+  auto& q = P->ctx->queue;
+  q.erase(std::remove(q.begin(), q.end(), P), q.end());
+  delete P;
 }

@@ -45,7 +45,7 @@ constexpr int RB = 32;            // row-block height
 constexpr int MAXB = 16;          // at most 16 row blocks (n <= 512)
 constexpr int BLK = RB * RB;      // doubles per block
 constexpr int PSTRIDE = 32;       // ints between flags (one 128-B line each)
-constexpr int NSLOT = 8;          // workspaces (concurrent launches on different streams)
+constexpr int NSLOT = 8;          // workspaces, one per stream that launches the kernel (get_ws)
 #ifndef RB_PRIO
 #define RB_PRIO 3                 // wave priority of the critical-path kernels (0..3)
 #endif
@@ -338,6 +338,9 @@ std::mutex g_mu;
 RbWork g_ws[64][NSLOT];
 bool g_have[64] = {};
 unsigned int g_launch = 0;
+hipStream_t g_slot_stream[64][NSLOT] = {};
+bool g_slot_used[64][NSLOT] = {};
+unsigned int g_slot_tick[64][NSLOT] = {};
 
 int get_ws(RbWork* out, int* epoch, hipStream_t st) {
   int dev = 0;
@@ -361,7 +364,23 @@ int get_ws(RbWork* out, int* epoch, hipStream_t st) {
     for (int s = 0; s < NSLOT; ++s) HIP_CHECK_RET(hipMemset(g_ws[dev][s].prog, 0, sizeof(int) * MAXB * PSTRIDE));
     ++g_launch;
   }
-  *out = g_ws[dev][g_launch % NSLOT];
+  // One workspace per stream: launches on one stream are serialised, so they can share it; launches
+  // on different streams (which may run concurrently, the whole program being enqueued ahead) never
+  // do.  Beyond NSLOT streams the least recently used stream's slot is recycled after that stream
+  // has drained (a host wait, only when more than NSLOT streams launch tile kernels).
+  int slot = -1, lru = 0;
+  for (int s = 0; s < NSLOT; ++s) {
+    if (g_slot_stream[dev][s] == st && g_slot_used[dev][s]) slot = s;
+    if (!g_slot_used[dev][s] || (g_slot_used[dev][lru] && g_slot_tick[dev][s] < g_slot_tick[dev][lru])) lru = s;
+  }
+  if (slot < 0) {
+    slot = lru;
+    if (g_slot_used[dev][slot]) (void)hipStreamSynchronize(g_slot_stream[dev][slot]);  // may be destroyed: ignore
+    g_slot_stream[dev][slot] = st;
+    g_slot_used[dev][slot] = true;
+  }
+  g_slot_tick[dev][slot] = g_launch;
+  *out = g_ws[dev][slot];
   *epoch = (int)(g_launch & 0x1ffffff);
   return 0;
 }

@@ -441,6 +441,10 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
         if distributed:
             comm.allreduce(v, op=torch.distributed.ReduceOp.MAX)
         r = int(v.item())
+        if r < 0:
+            # the dataflow tile kernels report a bounded-spin timeout as a negative info (-1000): an
+            # execution failure, never a numerical result
+            raise RuntimeError(f"potrf: tile kernel failure (info {r})")
         if info_out is not None:
             info_out[0] = r
         return r

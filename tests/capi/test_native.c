@@ -93,6 +93,36 @@ static void test_dpotrf_posv(dplasma_context_t *ctx) {
   dplasma_desc_destroy(B);
 }
 
+/* posv on a single tile (n <= nb): the solves must wait for the tile factorisation (one POTRF and two
+ * TRSM tasks on different streams) */
+static void test_dposv_one_tile(dplasma_context_t *ctx) {
+  const int n = 200, nb = 256, nrhs = 9;
+  for (int rep = 0; rep < 3; ++rep) {
+    dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, n, n), *B = dmat(ctx, dplasmaRealDouble, nb, n, nrhs);
+    double *A0 = malloc(sizeof(double) * n * n), *B0 = malloc(sizeof(double) * n * nrhs);
+    double *X = malloc(sizeof(double) * n * nrhs);
+    dplasma_dplghe(ctx, (double)n, dplasmaLower, A, 11 + rep);
+    dplasma_dplrnt(ctx, 0, B, 12 + rep);
+    dplasma_desc_get_lapack(A, A0, n);
+    dplasma_desc_get_lapack(B, B0, n);
+    const int info = dplasma_dposv(ctx, dplasmaLower, A, B);
+    CHECK(info == 0, "dposv (one tile) info %d (%s)", info, dplasma_last_error());
+    dplasma_desc_get_lapack(B, X, n);
+    double err = 0, bn = 0;
+    for (int c = 0; c < nrhs; ++c)
+      for (int i = 0; i < n; ++i) {
+        double s = 0;
+        for (int k = 0; k < n; ++k) s += (i >= k ? A0[i + (size_t)k * n] : A0[k + (size_t)i * n]) * X[k + (size_t)c * n];
+        err = fmax(err, fabs(s - B0[i + (size_t)c * n]));
+        bn = fmax(bn, fabs(B0[i + (size_t)c * n]));
+      }
+    if (rep == 0) printf("dposv one tile n=%d nb=%d ||Ax-b||/||b|| %.3e\n", n, nb, err / bn);
+    CHECK(err / bn < 1e-12, "dposv (one tile) residual %.3e", err / bn);
+    free(A0), free(B0), free(X);
+    dplasma_desc_destroy(A), dplasma_desc_destroy(B);
+  }
+}
+
 static void test_dgemm(dplasma_context_t *ctx) {
   const int M = 300, N = 200, K = 250, nb = 128;
   /* C = alpha A^T B + beta C, A is K x M */
@@ -168,6 +198,8 @@ static void test_rank_k(dplasma_context_t *ctx) {
     }
   printf("zherk UN %dx%d max error %.3e\n", N, K, err);
   CHECK(err < 1e-11, "zherk error %.3e", err);
+  for (int i = 0; i < N; ++i)   /* Hermitian rank-k: a real diagonal, exactly */
+    CHECK(cimag(q[i + (size_t)i * N]) == 0.0, "zherk diagonal (%d) imaginary part %.3e", i, cimag(q[i + (size_t)i * N]));
   free(z), free(w), free(q);
   dplasma_desc_destroy(Z), dplasma_desc_destroy(W);
 }
@@ -421,6 +453,7 @@ int main(int argc, char **argv) {
   CHECK(dplasma_context_world(ctx) == 1 && dplasma_context_rank(ctx) == 0, "rank/world");
   printf("native context up\n");
   test_dpotrf_posv(ctx);
+  test_dposv_one_tile(ctx);
   test_dgemm(ctx);
   test_dtrsm(ctx, dplasmaLeft, dplasmaLower, dplasmaNoTrans);
   test_dtrsm(ctx, dplasmaLeft, dplasmaUpper, dplasmaTrans);

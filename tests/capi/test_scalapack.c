@@ -126,6 +126,33 @@ int main(int argc, char **argv) {
     }
   printf("pdgetrf_ info=%d err=%.3e\n", info, e);
   ok &= info == 0 && e < 1e-11;
+  /* pdlatsqr_: workspace query (LWORK = -1) then the factorisation; the query must not touch A */
+  {
+    double *q = malloc(sizeof(double) * N * N), *tau = malloc(sizeof(double) * N), w1 = -1.0;
+    int mq = N, nq = N, lwork = -1;
+    memcpy(q, a0, sizeof(double) * N * N);
+    pdlatsqr_(&mq, &nq, q, &one, &one, desca, tau, &w1, &lwork, &info);
+    const double want = (double)NB * (N + N + NB);
+    int same = memcmp(q, a0, sizeof(double) * N * N) == 0;
+    printf("pdlatsqr_ query info=%d work(1)=%.0f (want %.0f) A untouched=%d\n", info, w1, want, same);
+    ok &= info == 0 && w1 == want && same;
+    lwork = (int)w1;
+    double *work = malloc(sizeof(double) * lwork);
+    pdlatsqr_(&mq, &nq, q, &one, &one, desca, tau, work, &lwork, &info);
+    /* R^T R = A0^T A0 (R: upper triangle of the result) */
+    double e = 0, d = 0;
+    for (int j = 0; j < N; ++j)
+      for (int i = 0; i <= j; ++i) {
+        double s = 0, t = 0;
+        for (int k = 0; k <= i; ++k) s += q[k + (size_t)i * N] * q[k + (size_t)j * N];
+        for (int k = 0; k < N; ++k) t += a0[k + (size_t)i * N] * a0[k + (size_t)j * N];
+        e = fmax(e, fabs(s - t));
+        d = fmax(d, fabs(t));
+      }
+    printf("pdlatsqr_ info=%d |R'R - A'A|/|A'A| %.3e\n", info, e / d);
+    ok &= info == 0 && e / d < 1e-12;
+    free(q), free(tau), free(work);
+  }
   blacs_gridexit_(&ictxt);
   parsec_fini_wrapper_();
   printf("%s\n", ok ? "SCALAPACK OK" : "SCALAPACK FAIL");
