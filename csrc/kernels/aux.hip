@@ -397,3 +397,19 @@ DPL_API int dpl_stream_cumask(const unsigned* mask, int nwords, void** out) {
 }
 
 DPL_API int dpl_stream_destroy(void* s) { return (int)hipStreamDestroy((hipStream_t)s); }
+
+// Busy wait of a fixed wall-clock duration on a stream (tools/replay_potrf.py: stands in for an
+// RCCL transfer of modelled duration -- occupying, like the RCCL kernel it replaces, nwg workgroup
+// slots).  wall_clock64(): the 100 MHz constant-rate counter; bounded to 1 s.
+__global__ __launch_bounds__(64) void k_delay(unsigned long long ticks) {
+  const unsigned long long t0 = wall_clock64();
+  if (ticks > 100000000ull) ticks = 100000000ull;
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+DPL_API int dpl_delay(double us, int nwg, hipStream_t st) {
+  if (us <= 0.0) return 0;
+  const unsigned long long ticks = (unsigned long long)(us * 100.0);   // 10 ns per tick
+  hipLaunchKernelGGL(k_delay, dim3(nwg < 1 ? 1 : nwg), dim3(64), 0, st, ticks);
+  return (int)hipGetLastError();
+}

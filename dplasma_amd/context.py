@@ -83,6 +83,8 @@ class Context:
         self._groups_built = False
         self.row_group = None
         self.col_group = None
+        self.urgent_group = None
+        self.bulk_groups = []
         self.row_ranks: List[int] = [self.myrow * Q + c for c in range(Q)]
         self.col_ranks: List[int] = [r * Q + self.mycol for r in range(P)]
         self._build_groups()
@@ -131,17 +133,57 @@ class Context:
         self.streams.update(made)
         self._owned_streams = [s.cuda_stream for s in made.values()]
 
+    @staticmethod
+    def reserve_mask(ncu: int, reserve: int):
+        """CU indices left to a bulk stream when ``reserve`` CUs are kept free for the critical path,
+        spread evenly over the chip: 8 XCDs, and whichever way the HIP CU-mask bits map onto them
+        (contiguous runs of ncu/8 or interleaved by index mod 8), every XCD keeps reserve/8 free CUs
+        -- a workgroup of a critical-path kernel dealt to any XCD finds one."""
+        per = ncu // 8
+        r = max(0, min(per - 1, (reserve + 7) // 8))
+        free = set()
+        for x in range(8):
+            for t in range(r):
+                # column x*per + x + 8t: one per residue class mod 8 in each contiguous run
+                free.add(x * per + (x + 8 * t) % per)
+        return [c for c in range(ncu) if c not in free]
+
+    def bulk_stream(self, reserve: int):
+        """A low-priority stream restricted to all CUs but ``reserve`` (see ``reserve_mask``); cached
+        per reserve.  reserve <= 0 or no GPU: the plain ``update`` stream."""
+        if reserve <= 0 or not self.is_gpu:
+            return "update"
+        name = f"bulk{reserve}"
+        if name in self.streams:
+            return name
+        import ctypes
+        from .ops import _lib
+        ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+        nw = (ncu + 31) // 32
+        words = [0] * nw
+        for c in self.reserve_mask(ncu, reserve):
+            words[c // 32] |= 1 << (c % 32)
+        arr = (ctypes.c_uint * nw)(*words)
+        out = ctypes.c_void_p()
+        lib = _lib.load()
+        _lib.check(lib.dpl_stream_cumask(ctypes.cast(arr, ctypes.c_void_p), nw, ctypes.byref(out)), "stream_cumask")
+        self.streams[name] = torch.cuda.ExternalStream(out.value, device=self.device)
+        self._owned_streams = getattr(self, "_owned_streams", []) + [out.value]
+        self._owned_names = getattr(self, "_owned_names", []) + [name]
+        return name
+
     def release(self):
         """Destroy the HIP streams this context created itself (CU-masked ones)."""
         owned = getattr(self, "_owned_streams", [])
         if owned:
             from .ops import _lib
             torch.cuda.synchronize(self.device)
-            for name in ("diag", "potrf_update"):
+            for name in ("diag", "potrf_update", *getattr(self, "_owned_names", [])):
                 self.streams.pop(name, None)
             for s in owned:
                 _lib.load().dpl_stream_destroy(s)
             self._owned_streams = []
+            self._owned_names = []
 
     # ------------------------------------------------------------------ comms
     def _build_groups(self):
@@ -168,6 +210,19 @@ class Context:
             cols.append(dist.new_group(ranks, **kw) if self.P > 1 else None)
         self.row_group = rows[self.myrow]
         self.col_group = cols[self.mycol]
+        # world-wide communicators of the dataflow tile transport (parallel.comm.start_p2p): one for
+        # critical-path (look-ahead) traffic on high-priority RCCL streams and DPLASMA_BULK_GROUPS for
+        # bulk traffic -- a communicator's operations are serialised on its stream, so bulk transfers
+        # of consecutive panels (different roots, different xGMI links) only overlap on different ones
+        nb = max(1, int(os.environ.get("DPLASMA_BULK_GROUPS", "2")))
+        self.urgent_group = dist.new_group(list(range(self.world)), **kw)
+        self.bulk_groups = [dist.new_group(list(range(self.world))) for _ in range(nb)]
+        if dist.get_backend() == "nccl" and self.is_gpu:
+            # create every communicator now, on every rank (a point-to-point batch that involves only
+            # some ranks must never be the call that initialises one)
+            t = torch.zeros(1, device=self.device)
+            for g in [self.urgent_group, *self.bulk_groups, *[x for x in rows + cols if x is not None]]:
+                dist.all_reduce(t, group=g)
         self._groups_built = True
 
     def barrier(self):
@@ -193,6 +248,7 @@ class Context:
         c.distributed, c.rank, c.world = False, 0, 1
         c.P, c.Q, c.myrow, c.mycol = 1, 1, 0, 0
         c.row_group = c.col_group = None
+        c.urgent_group, c.bulk_groups = None, []
         c.row_ranks, c.col_ranks = [0], [0]
         c._queue = []
         return c

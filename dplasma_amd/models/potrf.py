@@ -30,6 +30,8 @@ MI355X design (not a translation of the JDF):
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..constants import (STORAGE_TILE, dplasmaConjTrans, dplasmaLeft, dplasmaLower, dplasmaNoTrans, dplasmaNonUnit,
@@ -92,10 +94,14 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                            or ctx.info.get_int("DPLASMA:GPU:number_of_blocks", 0) > 0):
         from .potrf_ooc import potrf_ooc_New
         return potrf_ooc_New(ctx, uplo, A)
+    if ctx.world > 1 and os.environ.get("DPLASMA_POTRF_DIST", "p2p") != "collective":
+        # distributed: point-to-point dataflow panel transport (models/potrf_dist.py);
+        # DPLASMA_POTRF_DIST=collective keeps the row-broadcast + column-all-gather schedule below
+        from .potrf_dist import potrf_dist_New
+        return potrf_dist_New(ctx, uplo, A, info_out)
     lower = uplo == dplasmaLower
     tp = Taskpool("potrf", ctx)
     # diagonal tiles on the CU-reserved stream when DPLASMA_DIAG_CUS is set (context._reserve_cus)
-    import os
     diag_stream = "diag" if "diag" in getattr(ctx, "streams", {}) else "panel"
     # the panel TRSM joins the diagonal tile on the CU-reserved stream (DPLASMA_POTRF_DIAG_TRSM=0: on
     # the shared panel stream): both are latency-bound chains that slow 7-28x beside GEMM waves

@@ -1,0 +1,439 @@
+"""Distributed Cholesky (P x Q > 1 processes): dataflow panel transport.
+
+Reference: ``src/zpotrf_L.jdf`` / ``zpotrf_U.jdf`` -- every edge from ``potrf_ztrsm(m,k)`` to a
+``potrf_zherk`` / ``potrf_zgemm`` of another rank is a message sent by PaRSEC's remote-dependency
+engine as soon as the TRSM finishes, with the panel tasks marked ``high_priority`` (:93,:194,:306)
+and the look-ahead expressed by the priority formulas (:58-69).
+
+MI355X design.  The schedule is the single-process one of ``models/potrf.py`` (blocks of D panels:
+per panel POTRF -> panel TRSM -> NEAR; per block NEXT (the next block, critical) and REST (bulk),
+optionally look-ahead 2), but the panel now travels *point to point from its producers* instead of
+through a row broadcast followed by a column all-gather:
+
+* the owner of panel tile (i, k) (a rank of process column pcol(k), lower) sends it directly to
+  every rank that needs it -- the ranks of its process row (row operand: the whole piece, one
+  contiguous message, the piece being packed sorted by destination column) and, in the other
+  process rows, the ranks of column pcol(i) (column operand: a contiguous sub-range).  One hop, no
+  relay, each pair on its own xGMI link;
+* destinations are split by urgency: a rank that owns a column of the look-ahead window (the rest of
+  the block and the next block: NEAR / NEXT) gets its tiles on the high-priority ``urgent``
+  communicator, every other rank on a ``bulk`` communicator (``k mod DPLASMA_BULK_GROUPS``, so the
+  bulk transfers of consecutive panels -- different roots -- overlap).  Each rank issues, per panel
+  and communicator, ONE grouped send/recv batch (sends and receives together: no ordering deadlock);
+* the receiving side waits where the data is consumed: NEAR / NEXT make the panel stream wait for the
+  urgent batch, REST makes the bulk stream wait for both -- never the host, never the producer's
+  stream;
+* the bulk trailing updates can run on a CU-masked stream that leaves ``DPLASMA_POTRF_BULK_RESERVE``
+  CUs (spread over the 8 XCDs) to the critical path and the RCCL kernels (``Context.bulk_stream``).
+
+The diagonal tile's triangle goes to the other ranks of the panel column on the urgent communicator
+(the reference's LOWER/UPPER tile shapes: half the bytes).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from ..constants import dplasmaConjTrans, dplasmaLeft, dplasmaLower, dplasmaNoTrans, dplasmaNonUnit, dplasmaRight
+from ..ops import tile_ops as ops
+from ..ops.batch import MASK_LOWER, MASK_UPPER, GemmBatch, TileBatch
+from ..parallel import comm
+from ..runtime import Taskpool
+from ..utils.flops import flops
+
+# distributed defaults (tools/replay_potrf.py decides them, profiles/r3_potrf_replay*.txt)
+DIST_DEFER = 2
+DIST_LOOKAHEAD = 2
+DIST_BULK_RESERVE = 0
+
+
+class _Panel:
+    def __init__(self, base, ld, off_fn):
+        self.base, self.ld, self.off = base, ld, off_fn
+
+
+def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
+    lower = uplo == dplasmaLower
+    tp = Taskpool("potrf", ctx)
+    tp.flops = flops(A.prec, "potrf", A.n)
+    nt = A.nt
+    dev = A.device
+    nbe = A.mb * A.nb
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    tp.info = info
+    P, Q = A.P, A.Q
+    env = os.environ
+    D = max(1, int(env.get("DPLASMA_POTRF_DEFER", DIST_DEFER)))
+    min_tiles = int(env.get("DPLASMA_POTRF_DEFER_MIN_TILES", 24))
+    la = int(env.get("DPLASMA_POTRF_LOOKAHEAD", DIST_LOOKAHEAD))
+    if la not in (1, 2):
+        raise ValueError("DPLASMA_POTRF_LOOKAHEAD must be 1 or 2")
+    nslab = 1 + la
+    reserve = int(env.get("DPLASMA_POTRF_BULK_RESERVE", DIST_BULK_RESERVE))
+    upd_stream = ctx.bulk_stream(reserve) if ctx.is_gpu else "update"
+    if ctx.is_gpu and "comm" not in ctx.streams:
+        ctx.streams["comm"] = torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1])
+    urgent_g = ctx.urgent_group
+    bulk_gs = ctx.bulk_groups or [None]
+
+    # ---- axis abstraction: the panel of lower is a tile column spread over process rows ("lines");
+    # upper is the transpose (a tile row spread over process columns)
+    def line(i):
+        return A.grid.prow(i + A.it0) if lower else A.grid.pcol(i + A.jt0)
+
+    def cross(i):
+        return A.grid.pcol(i + A.jt0) if lower else A.grid.prow(i + A.it0)
+
+    def rank_lc(l, c):
+        return A.grid.rank(l, c) if lower else A.grid.rank(c, l)
+
+    def tcoord(i, k):
+        return (i, k) if lower else (k, i)
+
+    my_line = A.myrow if lower else A.mycol
+    my_cross = A.mycol if lower else A.myrow
+    nlines = P if lower else Q
+
+    blocks = []
+    c = 0
+    while c < nt:
+        d = D if nt - c >= min_tiles else 1
+        blocks.append((c, min(nt, c + d)))
+        c += d
+    block_of = {}
+    for b, (c0, c1) in enumerate(blocks):
+        for k in range(c0, c1):
+            block_of[k] = b
+
+    # ---- per panel: every line's tiles sorted by (cross, i) (the packing order of its root)
+    def line_tiles(k):
+        per = [[] for _ in range(nlines)]
+        for i in range(k + 1, nt):
+            per[line(i)].append(i)
+        for l in range(nlines):
+            per[l].sort(key=lambda i: (cross(i), i))
+        return per
+
+    maxcnt = maxsub = 1
+    for k in range(nt):
+        per = line_tiles(k)
+        maxcnt = max(maxcnt, max(len(p) for p in per))
+        maxsub = max(maxsub, max(sum(1 for i in p if cross(i) == my_cross) for p in per))
+    SG, SX = maxcnt * nbe, nlines * maxsub * nbe
+    slab = SG + SX
+    GX = torch.zeros(nslab * D * slab, dtype=A.dtype, device=dev)
+    ntri = A.mb * (A.mb + 1) // 2
+    dsend = torch.zeros(2 * ntri, dtype=A.dtype, device=dev)
+    drecv = torch.zeros(2 * ntri, dtype=A.dtype, device=dev)
+    dbuf = torch.zeros(2 * nbe, dtype=A.dtype, device=dev)
+    tp._buffers = (GX, dsend, drecv, dbuf)
+
+    use_rb = ops.rb_ok(A.data, A.mb) and A.mb == A.nb
+    if use_rb:
+        zsz = ops.rb_zbuf_size()
+        zbufs = torch.empty(2 * zsz, dtype=torch.float64, device=dev)
+        tp._zbufs = zbufs
+    tri_mask = MASK_LOWER if lower else MASK_UPPER
+    tA, tB = (dplasmaNoTrans, dplasmaConjTrans) if lower else (dplasmaConjTrans, dplasmaNoTrans)
+
+    def window(k):
+        """columns updated on the critical path by panel k: the rest of its block and the next one"""
+        b = block_of[k]
+        hi = blocks[b + 1][1] if b + 1 < len(blocks) else nt
+        return range(k + 1, hi)
+
+    def urgent_cross(k):
+        return {cross(j) for j in window(k)}
+
+    panels = {}
+    last_trsm = {}     # k -> TRSM(k) task (the reader of the diagonal receive buffer k % 2)
+    pend = {}          # k -> {"u": Pending, "b": Pending} (this rank's batches of panel k)
+    send_pend = {}     # slot -> list of Pending whose sends read that slab
+    dsend_pend = {}    # k % 2 -> Pending of the diag send reading dsend[k % 2]
+
+    def add_update(batch, ks, ncols):
+        for n_ in ncols:
+            for m_ in range(n_, nt):
+                cc = (m_, n_) if lower else (n_, m_)
+                if not A.is_local(*cc):
+                    continue
+                kp = [(panels[k].off(cc[0]), panels[k].off(cc[1]), A.tile_rows(k)) for k in ks]
+                batch.add(A.offset(*cc), A.tile_rows(cc[0]), A.tile_cols(cc[1]), kp, tri_mask if m_ == n_ else 0)
+        return batch.finalize()
+
+    def f_upd(batch, base, ld):
+        ops.gemm(tA, tB, -1.0, base, ld, base, ld, 1.0, A.data, A.ld, batch)
+
+    def wait_panels(ks):
+        # the consumer's stream waits for the receives of panels ks (never for this rank's sends)
+        for k in ks:
+            comm.finish(pend.get(k, {}).get("r"))
+
+    gate = None
+    last_upd = {}
+    nxt2_of, rest_of = {}, {}
+    last_panel = None
+    slot_readers = {}   # slot -> tasks reading it (updates); the next user of the slot follows them
+    for b, (c0, c1) in enumerate(blocks):
+        par = b % nslab
+        for k in range(c0, c1):
+            kb = A.tile_rows(k)
+            dk = tcoord(k, k)
+            pc = cross(k)
+            in_pc = my_cross == pc
+            diag_line = line(k)
+            own_diag = in_pc and my_line == diag_line
+            per = line_tiles(k)
+            mine = per[my_line] if in_pc else []
+            slot = par * D + (k - c0)
+            o = slot * slab
+            guard = slot_readers.get(slot, [])
+            # ---------------- POTRF(k)
+            t_potrf = None
+            zk = zbufs[(k % 2) * zsz:(k % 2 + 1) * zsz] if use_rb else None
+            if own_diag:
+                off = A.offset(*dk)
+
+                def f_potrf(off=off, kb=kb, k=k, zk=zk):
+                    if use_rb:
+                        ops.potrf_tile(uplo, A.data, off, kb, A.ld, info, k * A.mb, zbuf=zk)
+                    else:
+                        ops.potrf_tile(uplo, A.data, off, kb, A.ld, info, k * A.mb)
+                t_potrf = tp.task(f"POTRF({k})", "panel", f_potrf, [gate], prio=3)
+            # ---------------- diagonal triangle to the other roots of the panel column
+            tri_src = None
+            if in_pc and mine and not own_diag:
+                src = rank_lc(diag_line, pc)
+                par2 = k % 2
+
+                def f_drecv(src=src, par2=par2, k=k, kb=kb):
+                    h = comm.start_p2p(recvs=[(drecv[par2 * ntri:(par2 + 1) * ntri], src)], group=urgent_g,
+                                       hint=("potrf", kb))
+                    pend.setdefault(k, {})["d"] = h
+                # the buffer pair alternates: panel k-2's TRSM must have read it (deps)
+                t_dr = tp.task(f"DRECV({k})", "comm", f_drecv, [last_trsm.get(k - 2)] if k >= 2 else [], prio=3)
+                tri_src = (t_dr, par2)
+            if own_diag:
+                dests = [rank_lc(l, pc) for l in range(nlines) if l != my_line and per[l]]
+                if dests:
+                    par2 = k % 2
+
+                    def f_dsend(dests=dests, par2=par2, off=A.offset(*dk), kb=kb):
+                        comm.finish(dsend_pend.get(par2))
+                        buf = dsend[par2 * ntri:(par2 + 1) * ntri]
+                        buf[: kb * (kb + 1) // 2].copy_(A.data.view(-1)[off + comm._tri_index(kb, A.ld, lower, dev)])
+                        h = comm.start_p2p(sends=[(buf, d) for d in dests], group=urgent_g)
+                        dsend_pend[par2] = h
+                    tp.task(f"DSEND({k})", "panel", f_dsend, [t_potrf], prio=3)
+            # ---------------- TRSM of my tiles of panel k
+            t_trsm = None
+            if mine:
+                if tri_src is not None:
+                    t_dr, par2 = tri_src
+                    tri_base, tri_ld, tri_off = dbuf, A.mb, par2 * nbe
+
+                    def f_unpack(par2=par2, kb=kb, k=k):
+                        comm.finish(pend[k]["d"])
+                        d = dbuf[par2 * nbe:(par2 + 1) * nbe]
+                        d[comm._tri_index(kb, A.mb, lower, dev)] = drecv[par2 * ntri: par2 * ntri + kb * (kb + 1) // 2]
+                    pre = [(f_unpack, t_dr)]
+                else:
+                    tri_base, tri_ld, tri_off = A.data, A.ld, A.offset(*dk)
+                    pre = []
+                if use_rb:
+                    rbp = ops.RbPanel(uplo, [(A.offset(*tcoord(i, k)), A.tile_rows(i) if lower else A.tile_cols(i))
+                                             for i in mine], A.ld)
+
+                    def f_trsm(rbp=rbp, tb_=tri_base, tl=tri_ld, to=tri_off, kb=kb, zk=zk, pre=pre, recv=bool(pre)):
+                        for f, _ in pre:
+                            f()
+                        if recv:
+                            ops.trsm_rb_prep(uplo, kb, tb_, to, tl, zk)
+                        ops.trsm_rb(uplo, kb, tb_, to, tl, zk, rbp, A.data, A.ld)
+                else:
+                    tb = TileBatch()
+                    for i in mine:
+                        cc = tcoord(i, k)
+                        tb.add(tri_off, A.tile_rows(cc[0]), A.tile_cols(cc[1]), b_off=A.offset(*cc))
+                    tb.finalize()
+                    side = dplasmaRight if lower else dplasmaLeft
+
+                    def f_trsm(tb=tb, tb_=tri_base, tl=tri_ld, side=side, pre=pre):
+                        for f, _ in pre:
+                            f()
+                        ops.trsm(side, uplo, dplasmaConjTrans, dplasmaNonUnit, 1.0, tb_, tl, A.data, A.ld, tb)
+                deps = [t_potrf, gate] + [t for _, t in pre]
+                t_trsm = tp.task(f"TRSM({k})", "panel", f_trsm, deps, prio=2)
+                last_trsm[k] = t_trsm
+            if k == nt - 1:
+                break
+            # ---------------- panel k's transport
+            ucross = urgent_cross(k)
+            G = o
+            X = o + SG
+            # my receive layout: G = my line's piece (root's packing order); X[l] = line l's tiles of my cross
+            pos_g = {i: j for j, i in enumerate(per[my_line])}
+            pos_x = {}
+            for l in range(nlines):
+                if l == my_line:
+                    continue
+                sub = sorted(i for i in per[l] if cross(i) == my_cross)
+                for j, i in enumerate(sub):
+                    pos_x[i] = X + (l * maxsub + j) * nbe
+            sends = {"u": [], "b": []}
+            recvs = {"u": [], "b": []}
+            me_urgent = my_cross in ucross
+            if mine:
+                # my piece -> G (packed by cross), then: my line's other crosses get all of it, every
+                # other line's rank of cross c gets the sub-range of cross c
+                for c_ in range(Q if lower else P):
+                    if c_ == my_cross:
+                        continue
+                    kind = "u" if c_ in ucross else "b"
+                    sends[kind].append((G, len(mine), rank_lc(my_line, c_)))
+                for l in range(nlines):
+                    if l == my_line:
+                        continue
+                    cs = {}
+                    for j, i in enumerate(mine):
+                        cs.setdefault(cross(i), []).append(j)
+                    for c_, js in cs.items():
+                        kind = "u" if c_ in ucross else "b"
+                        sends[kind].append((G + js[0] * nbe, len(js), rank_lc(l, c_)))
+            kind_me = "u" if me_urgent else "b"
+            if not in_pc and per[my_line]:
+                recvs[kind_me].append((G, len(per[my_line]), rank_lc(my_line, pc)))
+            for l in range(nlines):
+                if l == my_line:
+                    continue
+                nsub = sum(1 for i in per[l] if cross(i) == my_cross)
+                if nsub:
+                    recvs[kind_me].append((X + l * maxsub * nbe, nsub, rank_lc(l, pc)))
+            pack = None
+            if mine:
+                pb = TileBatch()
+                for j, i in enumerate(mine):
+                    cc = tcoord(i, k)
+                    pb.add(A.offset(*cc), A.tile_rows(cc[0]), A.tile_cols(cc[1]), b_off=G + j * nbe)
+                pack = pb.finalize()
+            bg = bulk_gs[k % len(bulk_gs)]
+            hint_row = ("trsm", len(per[my_line]), kb)
+
+            def f_xfer(pack=pack, sends=sends, recvs=recvs, k=k, slot=slot, bg=bg, hint_row=hint_row):
+                for h in send_pend.pop(slot, []):   # the slab's previous sends have read it
+                    comm.finish(h)
+                if pack is not None:
+                    ops.geadd(0, dplasmaNoTrans, 1.0, A.data, A.ld, 0.0, GX, A.mb, pack, copy=True)
+                hs = {}
+                for kind, grp in (("u", urgent_g), ("b", bg)):
+                    s_ = [(GX[a: a + n * nbe], r) for a, n, r in sends[kind]]
+                    r_ = [(GX[a: a + n * nbe], r) for a, n, r in recvs[kind]]
+                    if s_ or r_:
+                        h = comm.start_p2p(s_, r_, group=grp, hint=hint_row)
+                        if r_:
+                            hs["r"] = h          # the batch carrying my receives (one kind per rank)
+                        if s_:
+                            send_pend.setdefault(slot, []).append(h)
+                pend[k] = {**pend.get(k, {}), **hs}
+            # a root issues after its TRSM (panel stream); a pure receiver on the comm stream, as soon
+            # as the slab is free
+            stream = "panel" if mine else "comm"
+            t_x = tp.task(f"XFER({k})", stream, f_xfer, [t_trsm, *guard], prio=2)
+            last_panel = t_x
+
+            def poff(i, pos_g=pos_g, pos_x=pos_x, G=G):
+                if line(i) == my_line:
+                    return G + pos_g[i] * nbe
+                return pos_x[i]
+            panels[k] = _Panel(GX, A.mb, poff)
+            base, ld = GX, A.mb
+            # ---------------- NEAR(k): the rest of this block (panel stream)
+            near = add_update(GemmBatch(), [k], range(k + 1, c1))
+            if len(near):
+                def f_near(bt=near, k=k):
+                    wait_panels([k])
+                    f_upd(bt, GX, A.mb)
+                gate = tp.task(f"NEAR({k})", "panel", f_near, [t_x, gate], prio=2)
+                slot_readers.setdefault(slot, []).append(gate)
+            else:
+                gate = t_x if t_x is not None else gate
+        if c1 >= nt:
+            break
+        ks = list(range(c0, c1))
+        n0, n1 = blocks[b + 1]
+        my_slots = [par * D + (k - c0) for k in ks]
+        if la == 1:
+            nxt = add_update(GemmBatch(), ks, range(n0, n1))
+            rest = add_update(GemmBatch(), ks, range(n1, nt))
+            deps = [gate, last_panel, last_upd.get(b - 1)]
+            t_next = None
+            if len(nxt):
+                def f_next(bt=nxt, ks=ks):
+                    wait_panels(ks)
+                    f_upd(bt, GX, A.mb)
+                t_next = tp.task(f"NEXT({b})", upd_stream, f_next, deps, prio=2)
+                last_upd[b] = t_next
+            if len(rest):
+                def f_rest(bt=rest, ks=ks):
+                    wait_panels(ks)
+                    f_upd(bt, GX, A.mb)
+                last_upd[b] = tp.task(f"REST({b})", upd_stream, f_rest, deps, prio=1)
+            for s_ in my_slots:
+                slot_readers[s_] = [t for t in (last_upd.get(b), gate) if t is not None]
+            gate = t_next if t_next is not None else gate
+            continue
+        n2 = blocks[b + 2][1] if b + 2 < len(blocks) else nt
+        nxt = add_update(GemmBatch(), ks, range(n0, n1))
+        nxt2 = add_update(GemmBatch(), ks, range(n1, n2))
+        rest = add_update(GemmBatch(), ks, range(n2, nt))
+        t_next = None
+        if len(nxt):
+            def f_next(bt=nxt, ks=ks):
+                wait_panels(ks)
+                f_upd(bt, GX, A.mb)
+            t_next = tp.task(f"NEXT({b})", "panel", f_next,
+                             [gate, last_panel, nxt2_of.get(b - 1), rest_of.get(b - 2)], prio=2)
+        prev_bulk = rest_of.get(b - 1)
+        if len(nxt2):
+            def f_nxt2(bt=nxt2, ks=ks):
+                wait_panels(ks)
+                f_upd(bt, GX, A.mb)
+            nxt2_of[b] = tp.task(f"NEXT2({b})", upd_stream, f_nxt2, [gate, last_panel, prev_bulk], prio=1)
+        if len(rest):
+            def f_rest(bt=rest, ks=ks):
+                wait_panels(ks)
+                f_upd(bt, GX, A.mb)
+            rest_of[b] = tp.task(f"REST2({b})", upd_stream, f_rest, [gate, last_panel, prev_bulk, nxt2_of.get(b)],
+                                 prio=0)
+        else:
+            rest_of[b] = nxt2_of.get(b, prev_bulk)
+        last_upd[b] = rest_of[b] if rest_of[b] is not None else t_next
+        for s_ in my_slots:
+            slot_readers[s_] = [t for t in (last_upd.get(b), t_next, gate) if t is not None]
+        gate = t_next if t_next is not None else gate
+
+    def _done():
+        # every exchange this rank started is complete before the buffers can be reused or freed
+        for d in pend.values():
+            for h in d.values():
+                comm.finish(h)
+        for hs in send_pend.values():
+            for h in hs:
+                comm.finish(h)
+        for h in dsend_pend.values():
+            comm.finish(h)
+        pend.clear()
+        send_pend.clear()
+        dsend_pend.clear()
+        v = info.clone()
+        comm.allreduce(v, op=torch.distributed.ReduceOp.MAX)
+        r = int(v.item())
+        if r < 0:
+            raise RuntimeError(f"potrf: tile kernel failure (info {r})")
+        if info_out is not None:
+            info_out[0] = r
+        return r
+    tp.on_complete(_done)
+    return tp.finish_build()
+

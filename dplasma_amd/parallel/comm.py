@@ -81,6 +81,78 @@ def p2p(sends=(), recvs=()) -> None:
             t.copy_(h)
 
 
+class Pending:
+    """An exchange in flight (``start_p2p``), completed by ``finish`` on the consumer's side.
+    Device transfers (RCCL) are waited for per consumer stream; host ones (gloo) once."""
+    __slots__ = ("works", "host_recvs", "keep", "device", "streams", "done", "meta")
+
+    def __init__(self, works, host_recvs=(), keep=(), device=False, meta=None):
+        self.works, self.host_recvs, self.keep = list(works), list(host_recvs), keep
+        self.device, self.streams, self.done, self.meta = device, set(), False, meta
+
+
+_BACKEND = None   # replaces the torch.distributed transport (tools/replay_potrf.py: modelled xGMI timing)
+
+
+def set_backend(b) -> None:
+    """Install a transport backend with ``start_p2p(sends, recvs, group, hint)`` / ``finish(p)``
+    (None: torch.distributed)."""
+    global _BACKEND
+    _BACKEND = b
+
+
+def start_p2p(sends=(), recvs=(), group=None, hint=None) -> Optional[Pending]:
+    """Issue a grouped point-to-point exchange and return at once.
+
+    sends / recvs: lists of (tensor, global peer rank); ``group``: the process group whose
+    communicator carries it (each group has its own RCCL stream, so exchanges on different groups
+    proceed concurrently -- over different xGMI links when their peers differ).  RCCL: the transfer
+    waits for the current stream's prior work and runs on the group's stream; ``finish`` (issued
+    later, under the consumer's stream) makes that stream -- not the host -- wait.  gloo: CUDA
+    tensors are staged through host memory; ``finish`` waits on the host and unstages.
+    ``hint`` describes the producer's work for a modelling backend; the real transports ignore it."""
+    sends, recvs = list(sends), list(recvs)
+    if not sends and not recvs:
+        return None
+    if _BACKEND is not None:
+        return _BACKEND.start_p2p(sends, recvs, group, hint)
+    if _nccl() and any(t.device.type == "cuda" for t, _ in sends + recvs):
+        ops = [dist.P2POp(dist.isend, t, p, group=group) for t, p in sends]
+        ops += [dist.P2POp(dist.irecv, t, p, group=group) for t, p in recvs]
+        return Pending(dist.batch_isend_irecv(ops) or (), device=True)
+    host_s = [(t.cpu() if t.device.type != "cpu" else t, p) for t, p in sends]
+    host_r = [(t, t.cpu() if t.device.type != "cpu" else t, p) for t, p in recvs]
+    works = [dist.isend(h, p, group=group) for h, p in host_s]
+    works += [dist.irecv(h, p, group=group) for _, h, p in host_r]
+    return Pending(works, [(t, h) for t, h, _ in host_r if h is not t], keep=host_s)
+
+
+def finish(p: Optional[Pending]) -> None:
+    """Complete an exchange from ``start_p2p`` for the caller: RCCL -- the current stream waits for
+    the transfer (once per stream); gloo -- the host waits and unstages (once).  None: no-op."""
+    if p is None or p.done:
+        return
+    if p.device:
+        sid = torch.cuda.current_stream().cuda_stream
+        if sid in p.streams:
+            return
+        p.streams.add(sid)
+        if _BACKEND is not None:
+            _BACKEND.finish(p)
+        else:
+            for w in p.works:
+                w.wait()
+        return
+    if _BACKEND is not None:
+        _BACKEND.finish(p)
+    else:
+        for w in p.works:
+            w.wait()
+        for t, h in p.host_recvs:
+            t.copy_(h)
+    p.done = True
+
+
 def exchange_add(t: torch.Tensor, peer: int, tmp: torch.Tensor) -> None:
     """t += (peer's t): symmetric pairwise sum through one send/recv pair (tmp: same size as t)."""
     p2p([(t, peer)], [(tmp[: t.numel()], peer)])
