@@ -68,23 +68,29 @@ def _insert_potrf(tp, uplo, A, info):
     T = dtd.tile_of
     In, InOut, Aff = dtd.INPUT, dtd.INOUT, dtd.AFFINITY
     total = A.mt
+    # priorities of the reference driver (tests/testing_zpotrf_dtd.c:134-186): cubic in the distance
+    # to the end, the panel first
     for k in range(A.mt):
         tp.insert_task(potrf, (T(A, k, k), InOut | Aff), k, priority=(total - k) ** 3)
         for m in range(k + 1, A.mt):
+            pr = (total - m) ** 3 + 3 * (2 * total - k - m - 1) * (m - k)
             if uplo == dplasmaLower:
-                tp.insert_task(trsm, (T(A, k, k), In), (T(A, m, k), InOut | Aff))
+                tp.insert_task(trsm, (T(A, k, k), In), (T(A, m, k), InOut | Aff), priority=pr)
             else:
-                tp.insert_task(trsm, (T(A, k, k), In), (T(A, k, m), InOut | Aff))
+                tp.insert_task(trsm, (T(A, k, k), In), (T(A, k, m), InOut | Aff), priority=pr)
         tp.data_flush(T(A, k, k))
         for m in range(k + 1, A.mt):
+            pr = (total - m) ** 3 + 3 * (m - k)
             if uplo == dplasmaLower:
-                tp.insert_task(herk, (T(A, m, k), In), (T(A, m, k), In), (T(A, m, m), InOut | Aff))
+                tp.insert_task(herk, (T(A, m, k), In), (T(A, m, k), In), (T(A, m, m), InOut | Aff), priority=pr)
                 for n in range(k + 1, m):
-                    tp.insert_task(gemm, (T(A, m, k), In), (T(A, n, k), In), (T(A, m, n), InOut | Aff))
+                    tp.insert_task(gemm, (T(A, m, k), In), (T(A, n, k), In), (T(A, m, n), InOut | Aff),
+                                   priority=(total - m) ** 3 + 3 * (2 * total - m - n - 3) * (m - n) + 6 * (m - k))
             else:
-                tp.insert_task(herk, (T(A, k, m), In), (T(A, k, m), In), (T(A, m, m), InOut | Aff))
+                tp.insert_task(herk, (T(A, k, m), In), (T(A, k, m), In), (T(A, m, m), InOut | Aff), priority=pr)
                 for n in range(k + 1, m):
-                    tp.insert_task(gemm, (T(A, k, n), In), (T(A, k, m), In), (T(A, n, m), InOut | Aff))
+                    tp.insert_task(gemm, (T(A, k, n), In), (T(A, k, m), In), (T(A, n, m), InOut | Aff),
+                                   priority=(total - m) ** 3 + 3 * (2 * total - m - n - 3) * (m - n) + 6 * (m - k))
             tp.data_flush(T(A, m, k) if uplo == dplasmaLower else T(A, k, m))
     tp.flops = flops(A.prec, "potrf", A.m)
     tp.data_flush_all(A)

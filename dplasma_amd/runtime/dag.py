@@ -191,6 +191,7 @@ class TileDAG:
         self.flops = 0.0
         self.info = None
         self.no_dtd = False         # the DTD engine's own windows (never re-routed through DTD)
+        self._has_prio = False      # some task carries a non-zero priority (add(prio=...))
 
     # ------------------------------------------------------------ registration
     def mat(self, M) -> int:
@@ -215,11 +216,13 @@ class TileDAG:
             self.kinds.append(K)
         return self._kid[K.name]
 
-    def add(self, K: Kind, ops, ext, pyargs=None):
+    def add(self, K: Kind, ops, ext, pyargs=None, prio=None):
         """Append tasks of kind K in program order.
 
         ops: (n, len(K.roles)) tile keys (-1 for an unused optional role); ext: (n, 3) ints;
-        pyargs: optional per-task tuples of Python values passed to a ``body`` kind."""
+        pyargs: optional per-task tuples of Python values passed to a ``body`` kind; prio: optional
+        per-task priorities (the DTD ``priority`` argument: higher first among the ready tasks of a
+        level, and on the high-priority stream when positive)."""
         ops = np.atleast_2d(np.asarray(ops, dtype=np.int64))
         ext = np.atleast_2d(np.asarray(ext, dtype=np.int32))
         if ops.size == 0:
@@ -228,8 +231,12 @@ class TileDAG:
             raise ValueError(f"{K.name}: bad task array shapes {ops.shape} {ext.shape}")
         if pyargs is not None and len(pyargs) != len(ops):
             raise ValueError("one pyargs tuple per task")
+        if prio is not None:
+            prio = np.broadcast_to(np.asarray(prio, dtype=np.int64), (len(ops),)).copy()
+            if prio.any():
+                self._has_prio = True
         kid = self.kind(K)
-        self._chunks.append((kid, ops, ext, list(pyargs) if pyargs is not None else None))
+        self._chunks.append((kid, ops, ext, list(pyargs) if pyargs is not None else None, prio))
         if K.flops is not None:
             self.flops += float(K.flops(ext))
 
@@ -289,11 +296,11 @@ class TileDAG:
         are rediscovered by the DTD engine.  None when a task cannot be expressed (Python-body kinds
         or optional roles left empty): the graph then runs as built."""
         from . import dtd
-        if any(self.kinds[k].body is not None or (o < 0).any() for k, o, _, _ in self._chunks):
+        if any(self.kinds[k].body is not None or (o < 0).any() for k, o, _, _, _ in self._chunks):
             return None
         dt = dtd.DTDTaskpool(self.ctx, self.name + "[ptg_to_dtd]", window=0)
         mask = (1 << 22) - 1
-        for k, o, e, _ in self._chunks:
+        for k, o, e, _, pr in self._chunks:
             K = self.kinds[k]
             tc = dt.task_class(K.name, kind=K)
             for t in range(len(o)):
@@ -302,7 +309,8 @@ class TileDAG:
                     key = int(key)
                     ref = dtd.tile_of(self.mats[key >> _MID_SHIFT], (key >> _M_SHIFT) & mask, key & mask)
                     args.append((ref, K.roles[r][1] | (dtd.AFFINITY if r == K.exec_role else 0)))
-                dt.insert_task(tc, *args, tuple(int(x) for x in e[t]))
+                dt.insert_task(tc, *args, tuple(int(x) for x in e[t]),
+                               priority=int(pr[t]) if pr is not None else 0)
         self._chunks = []
         dt.flops = self.flops
         tp = dt.compile()
@@ -328,8 +336,9 @@ class TileDAG:
         kid = np.zeros(ntask, dtype=np.int32)
         ext = np.zeros((ntask, 3), dtype=np.int32)
         pyargs_all = None
+        tprio = np.zeros(ntask, dtype=np.int64)
         p = 0
-        for k, o, e, pa in self._chunks:
+        for k, o, e, pa, pr in self._chunks:
             n = len(o)
             K = self.kinds[k]
             ops[p:p + n, :o.shape[1]] = o
@@ -337,6 +346,8 @@ class TileDAG:
                 modes[p:p + n, r] = np.where(o[:, r] >= 0, md, 0)
             kid[p:p + n] = k
             ext[p:p + n] = e
+            if pr is not None:
+                tprio[p:p + n] = pr
             if pa is not None:
                 if pyargs_all is None:
                     pyargs_all = [()] * ntask
@@ -468,19 +479,33 @@ class TileDAG:
                 ld[~loc] = np.array([self.mats[i].mb for i in range(len(self.mats))], dtype=np.int32)[mid[~loc]]
             return bidx, off, ld
 
-        # ---------------- my launches, grouped by (level, critical first, kind prio, kind)
+        # ---------------- my launches, grouped by (level, critical first, task priority (higher first),
+        # kind prio, kind)
         mine_t = np.nonzero(exe == me)[0] if world > 1 else np.arange(ntask)
         prio = np.array([self.kinds[k].prio for k in range(len(self.kinds))])[kid[mine_t]]
         cflag = (~crit[mine_t]).astype(np.int64) if crit is not None else np.zeros(len(mine_t), dtype=np.int64)
-        order = np.lexsort((mine_t, kid[mine_t], prio, cflag, level[mine_t]))
+        eff = tprio[mine_t].copy()
+        if self._has_prio and len(mine_t):
+            # a batched kind stays ONE launch per level: its tasks share their highest priority;
+            # Python-body kinds (one call per task) order task by task
+            batched = np.array([self.kinds[k].body is None for k in range(len(self.kinds))])[kid[mine_t]]
+            if batched.any():
+                gk = (level[mine_t].astype(np.int64) * 2 + cflag) * (len(self.kinds) + 1) + kid[mine_t]
+                gmax = {}
+                for g_, v in zip(gk[batched].tolist(), eff[batched].tolist()):
+                    if v > gmax.get(g_, -(1 << 62)):
+                        gmax[g_] = v
+                eff[batched] = np.array([gmax[g_] for g_ in gk[batched].tolist()], dtype=np.int64)
+        order = np.lexsort((mine_t, kid[mine_t], prio, -eff, cflag, level[mine_t]))
         mine_t = mine_t[order]
         groups = []  # execution order: dict(K, start, n, cpu_refs, ext, emax, level, stream)
         all_items = []
         nitems_total = 0
         if len(mine_t):
-            lv, kk = level[mine_t], kid[mine_t]
+            lv, kk, tp_ = level[mine_t], kid[mine_t], eff[order]
             cf = cflag[order]
-            brk = np.nonzero((lv[1:] != lv[:-1]) | (kk[1:] != kk[:-1]) | (cf[1:] != cf[:-1]))[0] + 1
+            brk = np.nonzero((lv[1:] != lv[:-1]) | (kk[1:] != kk[:-1]) | (cf[1:] != cf[:-1]) |
+                             (tp_[1:] != tp_[:-1]))[0] + 1
             starts = np.concatenate([[0], brk])
             ends = np.concatenate([brk, [len(mine_t)]])
             items = np.zeros(len(mine_t), dtype=DAG_ITEM)

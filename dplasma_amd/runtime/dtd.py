@@ -124,8 +124,10 @@ class DTDTaskpool:
     def insert_task(self, fn, *args, name: Optional[str] = None, flops: float = 0.0, priority: int = 0):
         """Insert one task.  ``args`` mixes tile arguments ``(tile_of(A, m, n), INPUT|INOUT|OUTPUT[|AFFINITY])``
         (or a bare TileRef, read-only) and plain values; the body is called as
-        ``fn(*tile_views, *values)`` with tiles first, in argument order.  ``priority`` is accepted
-        for API parity (within a window, tasks of one level run in one batch)."""
+        ``fn(*tile_views, *values)`` with tiles first, in argument order.  ``priority`` (the
+        reference's per-insert priority, tests/testing_zpotrf_dtd.c): among the tasks of a window that
+        are ready together (one DAG level), higher priorities issue first (the stream -- critical path
+        or bulk -- still follows the task's slack in the DAG)."""
         if self._running and self.ctx.world > 1:
             raise RuntimeError("DTD: inserting from a task body is supported on a single process")
         tc = fn if isinstance(fn, TaskClass) else TaskClass(name or getattr(fn, "__name__", "task"), fn)
@@ -158,10 +160,10 @@ class DTDTaskpool:
             # class in a level becomes one launch
             K = self._batched_kind(tc, tuple(modes), affinity)
             ext = [int(x) for x in (values[0] if values else (0, 0, 0))]
-            self.dag.add(K, [keys], [ext])
+            self.dag.add(K, [keys], [ext], prio=[int(priority)])
         else:
             K = self._kind_for(tc, tuple(modes), affinity)
-            self.dag.add(K, [keys], [[0, 0, 0]], pyargs=[tuple(values)])
+            self.dag.add(K, [keys], [[0, 0, 0]], pyargs=[tuple(values)], prio=[int(priority)])
         self.ntasks += 1
         self.pending += 1
         self.flops += flops

@@ -123,3 +123,37 @@ def test_gpu_potrf_dtd():
     a = A.to_dense_local().cpu()
     assert potrf_dtd(g, dp.dplasmaLower, A) == 0
     assert rel_err(torch.tril(A.to_dense_local().cpu()), torch.linalg.cholesky(a)) < 1e-11
+
+
+def test_dtd_priority_orders_ready_tasks(ctx):
+    """insert_task(priority=...) (tests/testing_zpotrf_dtd.c passes one on every insert): tasks that
+    are ready together run highest priority first; program order breaks ties, and dependencies
+    still win over priorities."""
+    A = dp.block_cyclic(ctx, torch.float64, 2, 2, 12, 12)
+    T = dtd.tile_of
+    order = []
+
+    def mark(a, tag):
+        order.append(tag)
+        a.fill_(float(len(order)))
+
+    tp = dtd.taskpool_new(ctx, window=0)
+    prios = [0, 5, 1, 5, -2, 3]
+    for i, p in enumerate(prios):
+        tp.insert_task(mark, (T(A, i, i), dtd.INOUT), i, priority=p)
+    # a dependent low-priority-then-high chain on one tile: order must stay RAW
+    tp.insert_task(mark, (T(A, 0, 1), dtd.INOUT), "dep0", priority=-9)
+    tp.insert_task(mark, (T(A, 0, 1), dtd.INOUT), "dep1", priority=99)
+    tp.compile().execute(ctx)
+    first = [t for t in order if isinstance(t, int) or t == "dep0"]
+    # level 0: the six diagonal tasks and dep0, by priority (ties in program order)
+    assert first == [1, 3, 5, 2, 0, 4, "dep0"]
+    assert order.index("dep1") > order.index("dep0")
+
+    # without priorities: program order
+    order.clear()
+    tp = dtd.taskpool_new(ctx, window=0)
+    for i in range(6):
+        tp.insert_task(mark, (T(A, i, i), dtd.INOUT), i)
+    tp.compile().execute(ctx)
+    assert order == list(range(6))
