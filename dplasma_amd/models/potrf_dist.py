@@ -200,7 +200,7 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                         ops.potrf_tile(uplo, A.data, off, kb, A.ld, info, k * A.mb, zbuf=zk)
                     else:
                         ops.potrf_tile(uplo, A.data, off, kb, A.ld, info, k * A.mb)
-                t_potrf = tp.task(f"POTRF({k})", "panel", f_potrf, [gate], prio=3)
+                t_potrf = tp.task(f"POTRF({k})", "panel", f_potrf, [gate], prio=3, comm=False)
             # ---------------- diagonal triangle to the other roots of the panel column
             tri_src = None
             if in_pc and mine and not own_diag:
@@ -264,7 +264,7 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                             f()
                         ops.trsm(side, uplo, dplasmaConjTrans, dplasmaNonUnit, 1.0, tb_, tl, A.data, A.ld, tb)
                 deps = [t_potrf, gate] + [t for _, t in pre]
-                t_trsm = tp.task(f"TRSM({k})", "panel", f_trsm, deps, prio=2)
+                t_trsm = tp.task(f"TRSM({k})", "panel", f_trsm, deps, prio=2, comm=False)
                 last_trsm[k] = t_trsm
             if k == nt - 1:
                 break
@@ -354,7 +354,7 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                 def f_near(bt=near, k=k):
                     wait_panels([k])
                     f_upd(bt, GX, A.mb)
-                gate = tp.task(f"NEAR({k})", "panel", f_near, [t_x, gate], prio=2)
+                gate = tp.task(f"NEAR({k})", "panel", f_near, [t_x, gate], prio=2, comm=False)
                 slot_readers.setdefault(slot, []).append(gate)
             else:
                 gate = t_x if t_x is not None else gate
@@ -372,13 +372,13 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                 def f_next(bt=nxt, ks=ks):
                     wait_panels(ks)
                     f_upd(bt, GX, A.mb)
-                t_next = tp.task(f"NEXT({b})", upd_stream, f_next, deps, prio=2)
+                t_next = tp.task(f"NEXT({b})", upd_stream, f_next, deps, prio=2, comm=False)
                 last_upd[b] = t_next
             if len(rest):
                 def f_rest(bt=rest, ks=ks):
                     wait_panels(ks)
                     f_upd(bt, GX, A.mb)
-                last_upd[b] = tp.task(f"REST({b})", upd_stream, f_rest, deps, prio=1)
+                last_upd[b] = tp.task(f"REST({b})", upd_stream, f_rest, deps, prio=1, comm=False)
             for s_ in my_slots:
                 slot_readers[s_] = [t for t in (last_upd.get(b), gate) if t is not None]
             gate = t_next if t_next is not None else gate
@@ -393,19 +393,20 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                 wait_panels(ks)
                 f_upd(bt, GX, A.mb)
             t_next = tp.task(f"NEXT({b})", "panel", f_next,
-                             [gate, last_panel, nxt2_of.get(b - 1), rest_of.get(b - 2)], prio=2)
+                             [gate, last_panel, nxt2_of.get(b - 1), rest_of.get(b - 2)], prio=2, comm=False)
         prev_bulk = rest_of.get(b - 1)
         if len(nxt2):
             def f_nxt2(bt=nxt2, ks=ks):
                 wait_panels(ks)
                 f_upd(bt, GX, A.mb)
-            nxt2_of[b] = tp.task(f"NEXT2({b})", upd_stream, f_nxt2, [gate, last_panel, prev_bulk], prio=1)
+            nxt2_of[b] = tp.task(f"NEXT2({b})", upd_stream, f_nxt2, [gate, last_panel, prev_bulk], prio=1,
+                                 comm=False)
         if len(rest):
             def f_rest(bt=rest, ks=ks):
                 wait_panels(ks)
                 f_upd(bt, GX, A.mb)
             rest_of[b] = tp.task(f"REST2({b})", upd_stream, f_rest, [gate, last_panel, prev_bulk, nxt2_of.get(b)],
-                                 prio=0)
+                                 prio=0, comm=False)
         else:
             rest_of[b] = nxt2_of.get(b, prev_bulk)
         last_upd[b] = rest_of[b] if rest_of[b] is not None else t_next

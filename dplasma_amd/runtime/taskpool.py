@@ -55,6 +55,7 @@ class Task:
     deps: List[int] = field(default_factory=list)
     prio: int = 0
     needs_event: bool = False
+    comm: Optional[bool] = None       # issues communication (None: unknown -- treated as True)
 
 
 class Taskpool:
@@ -71,7 +72,10 @@ class Taskpool:
 
     # ------------------------------------------------------------------ build
     def task(self, name: str, stream: str, fn: Callable[[], None], deps: Sequence[Optional[int]] = (),
-             prio: int = 0) -> int:
+             prio: int = 0, comm: Optional[bool] = None) -> int:
+        """Append a task.  ``comm=False`` declares a compute-only task (it may wait for exchanges that
+        its dependencies started, but starts none): on more than one rank only such tasks are
+        reordered by a scheduler policy; every other task keeps its program order."""
         tid = len(self.tasks)
         dd = [d for d in deps if d is not None]
         for d in dd:
@@ -79,7 +83,7 @@ class Taskpool:
                 raise ValueError("dependencies must point to earlier tasks")
             if self.tasks[d].stream != stream:
                 self.tasks[d].needs_event = True
-        self.tasks.append(Task(tid, name, stream, fn, dd, prio))
+        self.tasks.append(Task(tid, name, stream, fn, dd, prio, comm=comm))
         return tid
 
     def on_complete(self, fn: Callable):
@@ -113,7 +117,7 @@ class Taskpool:
         ctx = ctx or self.ctx
         n = len(self.tasks)
         pol = policy_code(getattr(ctx, "scheduler", None)) if ctx is not None else 0
-        if pol == 0 or n < 2 or (ctx is not None and ctx.world > 1):
+        if pol == 0 or n < 2:
             return list(range(n))
         cache = self.__dict__.setdefault("_orders", {})
         if pol in cache:
@@ -122,11 +126,22 @@ class Taskpool:
         rt = _lib_rt()
         if rt is None:
             return list(range(n))
+        multi = ctx is not None and ctx.world > 1
+        deps = [list(t.deps) for t in self.tasks]
+        if multi:
+            # every rank must issue its communication in the same (program) order: chain the tasks
+            # that may communicate; compute-only tasks (comm=False) are free to move by priority
+            prev = None
+            for t in self.tasks:
+                if t.comm is not False:
+                    if prev is not None and prev not in deps[t.tid]:
+                        deps[t.tid].append(prev)
+                    prev = t.tid
         ptr = np.zeros(n + 1, dtype=np.int64)
         for t in self.tasks:
-            ptr[t.tid + 1] = len(t.deps)
+            ptr[t.tid + 1] = len(deps[t.tid])
         ptr = np.cumsum(ptr)
-        idx = np.array([d for t in self.tasks for d in t.deps], dtype=np.int64)
+        idx = np.array([d for dl in deps for d in dl], dtype=np.int64)
         prio = np.array([t.prio for t in self.tasks], dtype=np.int32)
         order = [int(x) for x in rt.dag_list_schedule(ptr, idx, prio, pol, int(getattr(ctx, "sched_seed", 0)))]
         cache[pol] = order

@@ -105,3 +105,33 @@ def test_algorithms_under_every_policy(sched):
     for i, p in enumerate(piv.tolist()):
         perm[[i, p]] = perm[[p, i]]
     assert rel_err(L @ torch.triu(lu), b[perm]) < 1e-12
+
+
+def _potrf_sched_worker(rank, world, P, sched):
+    import dplasma_amd as dp
+    ctx = dp.init(device="cpu", P=P)
+    ctx.scheduler = sched
+    N, NB = 170, 17
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+    dp.plghe(ctx, float(N), dp.dplasmaLower, A, 3872)
+    tp = dp.potrf_New(ctx, dp.dplasmaLower, A)
+    order = tp.issue_order(ctx)
+    moved = order != list(range(len(tp.tasks)))
+    comm_order = [t for t in order if tp.tasks[t].comm is not False]
+    info = tp.execute(ctx)
+    return info, A.to_dense_local(), moved, comm_order == sorted(comm_order)
+
+
+@pytest.mark.parametrize("sched", ["pbq", "ip", "rnd"])
+def test_multirank_potrf_under_policy(sched, monkeypatch):
+    """On more than one rank a scheduler policy reorders the compute-only tasks (comm=False) while
+    the communicating tasks keep their program order on every rank; the factor is bit-identical to
+    the program-order run (reference -o choice, tests/common.c:291-314)."""
+    from helpers import run_distributed
+    monkeypatch.setenv("DPLASMA_POTRF_DEFER_MIN_TILES", "3")
+    ref = run_distributed(_potrf_sched_worker, 4, 2, None)
+    out = run_distributed(_potrf_sched_worker, 4, 2, sched)
+    assert any(out[r][2] for r in range(4)), "the policy never changed the issue order"
+    for r in range(4):
+        assert out[r][0] == 0 and out[r][3]
+        assert torch.equal(out[r][1], ref[r][1]), r

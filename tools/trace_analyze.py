@@ -43,11 +43,24 @@ def main():
     ap.add_argument("--from-kernel", default="k_potrf")
     ap.add_argument("--engine", default="k_gemm")
     ap.add_argument("--skip", type=int, default=0, help="start at the (skip+1)-th --from-kernel dispatch")
+    ap.add_argument("--last", action="store_true", help="start at the last run: the first --from-kernel "
+                    "dispatch after the longest gap with no kernel (a host-side pause between runs)")
+    ap.add_argument("--slices", type=int, default=0, help="also print engine busy / exposed time per time slice")
     args = ap.parse_args()
     rows = list(csv.DictReader(open(args.trace)))
     ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows]
     ks.sort()
-    t0 = [s for s, e, n in ks if args.from_kernel in n][args.skip]
+    starts = [s for s, e, n in ks if args.from_kernel in n]
+    t0 = starts[args.skip]
+    if args.last:
+        # the longest idle gap separates runs; take the first matching dispatch after it
+        best, gap_end = -1, ks[0][0]
+        run_end = ks[0][1]
+        for s, e, n in ks[1:]:
+            if s - run_end > best:
+                best, gap_end = s - run_end, s
+            run_end = max(run_end, e)
+        t0 = min(x for x in starts if x >= gap_end)
     win = [(s, e, n) for s, e, n in ks if s >= t0]
     t1 = max(e for s, e, n in win)
     wall = t1 - t0
@@ -62,6 +75,13 @@ def main():
           f"exposed (no engine kernel running) {(wall - eng) / 1e6:.2f} ms")
     for k, v in sorted(busy.items(), key=lambda x: -x[1]):
         print(f"  {v / 1e6:10.2f} ms  {cnt[k]:6d}x  {k}")
+    if args.slices:
+        w = wall / args.slices
+        print(f"per slice of {w / 1e6:.2f} ms: engine busy / exposed")
+        for i in range(args.slices):
+            a, b = t0 + i * w, t0 + (i + 1) * w
+            e_ = union([(max(s, a), min(e, b)) for s, e, n in win if args.engine in n and e > a and s < b])
+            print(f"  [{i * w / 1e6:7.2f}, {(i + 1) * w / 1e6:7.2f}) ms  engine {e_ / 1e6:6.2f}  exposed {(w - e_) / 1e6:6.2f}")
 
 
 if __name__ == "__main__":
