@@ -155,3 +155,27 @@ def test_blas3_distributed_matches_single():
     for key in single:
         full = sum(res[r][key] for r in range(4))
         assert (full - single[key]).abs().max() < 1e-10, key
+
+
+@pytest.mark.parametrize("world,P", [(2, 1), (2, 2), (4, 2), (8, 2), (3, 1), (4, 4), (6, 2)])
+@pytest.mark.parametrize("uplo", [122, 121])
+@pytest.mark.parametrize("chunk", [1, 3])
+def test_potrf_pipelined(world, P, uplo, chunk, monkeypatch):
+    """One panel per step with the critical path pipelined in chunks of tile rows
+    (models/potrf_dist.py potrf_pipelined_New): TRSM / urgent exchange / NEXT per chunk, bulk
+    exchange for the ranks that do not own the next column; ragged last tile."""
+    monkeypatch.setenv("DPLASMA_POTRF_DEFER", "1")
+    monkeypatch.setenv("DPLASMA_POTRF_CHUNK", str(chunk))
+    N, NB = 170, 17
+    out = run_distributed(_potrf_worker, world, P, N, NB, uplo, "d")
+    full = sum(out[r][3] for r in range(world))
+    for r in range(world):
+        info, ok, res, _ = out[r]
+        assert info == 0 and ok, (r, res)
+    import dplasma_amd as dp
+    ctx = dp.Context(device="cpu")
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+    dp.plghe(ctx, float(N), uplo, A, 3872)
+    dp.potrf(ctx, uplo, A)
+    tri = (lambda x: x.tril()) if uplo == 122 else (lambda x: x.triu())
+    assert (tri(full) - tri(A.to_dense_local())).abs().max() < 1e-12
