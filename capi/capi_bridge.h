@@ -84,6 +84,20 @@ NatProgram* nat_laset(dplasma_context_t* ctx, int prec, int uplo, const void* al
 NatProgram* nat_lascal(dplasma_context_t* ctx, int prec, int uplo, const void* alpha, dplasma_desc_t* A);
 double nat_lange(dplasma_context_t* ctx, int prec, int ntype, dplasma_desc_t* A);   // NAN + error on failure
 double nat_lantr(dplasma_context_t* ctx, int prec, int ntype, int uplo, int diag, dplasma_desc_t* A);
+NatProgram* nat_trmm(dplasma_context_t* ctx, int prec, int side, int uplo, int trans, int diag, const void* alpha,
+                     dplasma_desc_t* A, dplasma_desc_t* B);
+NatProgram* nat_symm(dplasma_context_t* ctx, int prec, int side, int uplo, const void* alpha, dplasma_desc_t* A,
+                     dplasma_desc_t* B, const void* beta, dplasma_desc_t* C);
+NatProgram* nat_hemm(dplasma_context_t* ctx, int prec, int side, int uplo, const void* alpha, dplasma_desc_t* A,
+                     dplasma_desc_t* B, const void* beta, dplasma_desc_t* C);
+double nat_lansy(dplasma_context_t* ctx, int prec, int ntype, int uplo, dplasma_desc_t* A);
+double nat_lanhe(dplasma_context_t* ctx, int prec, int ntype, int uplo, dplasma_desc_t* A);
+NatProgram* nat_getrf_1d(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* IPIV);
+NatProgram* nat_getrs(dplasma_context_t* ctx, int prec, int trans, dplasma_desc_t* A, dplasma_desc_t* IPIV,
+                      dplasma_desc_t* B);
+NatProgram* nat_gesv_1d(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* IPIV,
+                        dplasma_desc_t* B);
+dplasma_desc_t* nat_desc_int(dplasma_context_t* ctx, int mb, int nb, int m, int n);
 int nat_execute(dplasma_context_t* ctx, NatProgram* P);     // run + wait + info, frees P
 dplasma_taskpool_t* nat_wrap(NatProgram* P);
 void nat_fini(dplasma_context_t* ctx);

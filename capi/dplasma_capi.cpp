@@ -284,7 +284,10 @@ DPL_CAPI dplasma_desc_t* dplasma_desc_block_cyclic(dplasma_context_t* ctx, int p
 }
 
 DPL_CAPI dplasma_desc_t* dplasma_desc_ipiv(dplasma_context_t* ctx, int mb, int nb, int m, int n, int P, int Q) {
-  if (dpl_native(ctx)) { nat_unsupported("desc_ipiv"); return nullptr; }
+  if (dpl_native(ctx)) {
+    if (P > 1 || Q > 1) { nat_unsupported("desc_ipiv: P = Q = 1 on a native context"); return nullptr; }
+    return nat_desc_int(ctx, mb, nb, m, n);
+  }
   dpl_ensure_python();
   PyGILState_STATE st = PyGILState_Ensure();
   PyObject* o = call_obj(ctx, "desc_int", nullptr,

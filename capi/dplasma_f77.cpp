@@ -12,8 +12,15 @@
 // weak BLACS / TOOLS symbols here let a standalone program run without a BLACS library, and yield
 // to a real one when it is linked.
 #include "capi_bridge.h"
+#include "include/dplasma.h"
+
+#include <hip/hip_runtime.h>
 
 #include <complex>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
 
 namespace {
 
@@ -47,16 +54,131 @@ int f77(const char* name, std::initializer_list<PyObject*> args) {
   return v;
 }
 
+// ---- interpreter-free path: a single-process run (no WORLD_SIZE > 1) whose BLACS grid is 1 x 1 runs
+// the ScaLAPACK calls on the native engine (capi/native.cpp) -- the reference wrappers' flow
+// (dplasma_wrapper_pdpotrf.c:133-291: wrap the local array, run, hand it back) without Python.
+// DPLASMA_F77_PYTHON=1 forces the Python layer.
+constexpr int NATIVE_CTXT = 1 << 20;    // BLACS handles of the native registry (Python's are small ints)
+
+// decided once, at the first F77 call: one process, a GPU, and no Python-backed dplasma context
+// already created by the program (dplasma_init) -- a program that mixes the C API's Python contexts
+// with the F77 layer keeps the Python layer
+bool f77_native() {
+  static int v = -1;
+  if (v < 0) {
+    const char* w = std::getenv("WORLD_SIZE");
+    const char* f = std::getenv("DPLASMA_F77_PYTHON");
+    int nd = 0;
+    const bool gpu = hipGetDeviceCount(&nd) == hipSuccess && nd > 0;
+    if (!gpu) (void)hipGetLastError();
+    v = (!w || std::atoi(w) <= 1) && !(f && std::atoi(f) == 1) && gpu && !dplasma_python_active() ? 1 : 0;
+  }
+  return v == 1;
+}
+
+dplasma_context_t* g_nctx = nullptr;
+
+dplasma_context_t* native_ctx() {
+  if (!g_nctx) {
+    const char* lr = std::getenv("LOCAL_RANK");
+    g_nctx = dplasma_init_native(lr ? std::atoi(lr) : 0);
+  }
+  return g_nctx;
+}
+
+bool native_grid(const int* desc) { return f77_native() && desc && desc[1] == NATIVE_CTXT; }
+
+bool on_device(const void* p) {
+  hipPointerAttribute_t at;
+  if (!p || hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return at.type == hipMemoryTypeDevice;
+}
+
+// a native descriptor over the m x n submatrix at (ia, ja) (1-based) of a local array with leading
+// dimension lld: zero copy for device memory, a device copy (written back by unwrap) for host memory
+struct Wrapped {
+  dplasma_desc_t* d = nullptr;
+  char* host = nullptr;
+  int lld = 0;
+  bool copy = false;
+};
+constexpr int NAT_TILE = 256;
+
+Wrapped wrap(int prec, int es, void* a, int ia, int ja, const int* desc, int m, int n) {
+  Wrapped w;
+  w.lld = desc[8];
+  char* sub = (char*)a + ((size_t)(ia - 1) + (size_t)(ja - 1) * w.lld) * es;
+  dplasma_context_t* c = native_ctx();
+  if (!c || m <= 0 || n <= 0) return w;
+  if (on_device(a)) {
+    w.d = dplasma_desc_block_cyclic_lapack(c, prec, NAT_TILE, NAT_TILE, m, n, 1, 1, 0, 0, sub, w.lld, 1);
+  } else {
+    w.d = dplasma_desc_block_cyclic(c, prec, NAT_TILE, NAT_TILE, m, n, 1, 1, 123);
+    if (w.d && dplasma_desc_set_lapack(w.d, sub, w.lld) != 0) {
+      dplasma_desc_destroy(w.d);
+      w.d = nullptr;
+    }
+    w.host = sub;
+    w.copy = true;
+  }
+  return w;
+}
+
+void unwrap(Wrapped& w, bool write_back) {
+  if (!w.d) return;
+  if (w.copy && write_back) (void)dplasma_desc_get_lapack(w.d, w.host, w.lld);
+  dplasma_desc_destroy(w.d);
+  w.d = nullptr;
+}
+
+// the Python layer's 1 x 1 BLACS grid (created on first use; the GIL is held by the caller)
+int python_grid() {
+  static int h = -1;
+  if (h < 0) {
+    int one = 1;
+    h = f77("gridinit", {iv(&one), iv(&one)});
+  }
+  return h;
+}
+
+int native_trans(const char* t) { return (*t == 'N' || *t == 'n') ? 111 : (*t == 'T' || *t == 't') ? 112 : 113; }
+int native_uplo(const char* u) { return (*u == 'U' || *u == 'u') ? 121 : 122; }
+int native_side(const char* s_) { return (*s_ == 'L' || *s_ == 'l') ? 141 : 142; }
+int native_diag(const char* d) { return (*d == 'U' || *d == 'u') ? 132 : 131; }
+
 }  // namespace
 
 extern "C" {
 
 // ---- runtime (parsec_init_wrapper_ / parsec_fini_wrapper_)
-DPL_CAPI void parsec_init_wrapper_(void) { DplGil g; f77("init", {}); }
-DPL_CAPI void parsec_fini_wrapper_(void) { DplGil g; f77("fini", {}); }
+DPL_CAPI void parsec_init_wrapper_(void) {
+  if (f77_native()) {
+    native_ctx();
+    return;
+  }
+  DplGil g;
+  f77("init", {});
+}
+DPL_CAPI void parsec_fini_wrapper_(void) {
+  if (f77_native()) {
+    if (g_nctx) dplasma_fini(g_nctx);
+    g_nctx = nullptr;
+    return;
+  }
+  DplGil g;
+  f77("fini", {});
+}
 
 // ---- BLACS / TOOLS subset (weak: a real BLACS library takes precedence)
 DPL_CAPI __attribute__((weak)) void blacs_pinfo_(int* mypnum, int* nprocs) {
+  if (f77_native()) {
+    *mypnum = 0;
+    *nprocs = 1;
+    return;
+  }
   DplGil g;
   PyObject* r = dpl_call_fn("blacs_pinfo", {});
   if (r && PyTuple_Check(r)) {
@@ -72,10 +194,25 @@ DPL_CAPI __attribute__((weak)) void blacs_get_(int* icontxt, int* what, int* val
 }
 DPL_CAPI __attribute__((weak)) void blacs_gridinit_(int* icontxt, const char* order, int* nprow, int* npcol) {
   (void)order;
+  if (f77_native()) {   // one process: only the 1 x 1 grid exists
+    if (*nprow == 1 && *npcol == 1) {
+      *icontxt = NATIVE_CTXT;
+    } else {
+      dpl_set_error("blacs_gridinit: a single process has only a 1 x 1 grid");
+      *icontxt = -1;
+    }
+    return;
+  }
   DplGil g;  // the argument objects are built before f77() runs: hold the GIL here
   *icontxt = f77("gridinit", {iv(nprow), iv(npcol)});
 }
 DPL_CAPI __attribute__((weak)) void blacs_gridinfo_(int* icontxt, int* nprow, int* npcol, int* myrow, int* mycol) {
+  if (f77_native()) {
+    const bool ok = *icontxt == NATIVE_CTXT;
+    *nprow = *npcol = ok ? 1 : -1;
+    *myrow = *mycol = ok ? 0 : -1;
+    return;
+  }
   DplGil g;
   PyObject* r = dpl_call_fn("blacs_gridinfo", {iv(icontxt)});
   if (r && PyTuple_Check(r)) {
@@ -127,30 +264,110 @@ static int latsqr_work(const int* desca) {
 }
 
 // ---- p?gemm_, p?potrf_, p?getrf_, p?trsm_, p?trmm_, p?latsqr_
+// native bodies of the ScaLAPACK entry points (1 x 1 grid, see f77_native); C = prec code
+#define DPL_F77_NATIVE(P, T, C)                                                                                   \
+  static void nat_p##P##gemm(const char* ta, const char* tb, int m, int n, int k, T alpha, T* a, int ia, int ja,  \
+                             const int* da, T* b, int ib, int jb, const int* db, T beta, T* c, int ic, int jc,    \
+                             const int* dc) {                                                                     \
+    const int tA = native_trans(ta), tB = native_trans(tb);                                                      \
+    Wrapped A = wrap(C, sizeof(T), a, ia, ja, da, tA == 111 ? m : k, tA == 111 ? k : m);                         \
+    Wrapped B = wrap(C, sizeof(T), b, ib, jb, db, tB == 111 ? k : n, tB == 111 ? n : k);                         \
+    Wrapped X = wrap(C, sizeof(T), c, ic, jc, dc, m, n);                                                          \
+    if (A.d && B.d && X.d) (void)dplasma_##P##gemm(native_ctx(), tA, tB, alpha, A.d, B.d, beta, X.d);             \
+    unwrap(A, false), unwrap(B, false), unwrap(X, true);                                                          \
+  }                                                                                                               \
+  static int nat_p##P##potrf(const char* uplo, int n, T* a, int ia, int ja, const int* da) {                      \
+    Wrapped A = wrap(C, sizeof(T), a, ia, ja, da, n, n);                                                          \
+    int info = A.d ? dplasma_##P##potrf(native_ctx(), native_uplo(uplo), A.d) : -1;                               \
+    unwrap(A, true);                                                                                              \
+    return info;                                                                                                  \
+  }                                                                                                               \
+  static int nat_p##P##getrf(int m, int n, T* a, int ia, int ja, const int* da, int* ipiv) {                      \
+    const int k = m < n ? m : n;                                                                                  \
+    Wrapped A = wrap(C, sizeof(T), a, ia, ja, da, m, n);                                                          \
+    dplasma_desc_t* IP = A.d ? dplasma_desc_ipiv(native_ctx(), 1, NAT_TILE, 1, k, 1, 1) : nullptr;               \
+    int info = IP ? dplasma_##P##getrf_1d(native_ctx(), A.d, IP) : -1;                                           \
+    if (IP && ipiv) {                                                                                             \
+      std::vector<int> p(k);                                                                                      \
+      if (dplasma_desc_get_lapack(IP, p.data(), 1) == 0)                                                          \
+        for (int i = 0; i < k; ++i) ipiv[i] = p[i] + ia - 1;   /* global row of the whole array */             \
+    }                                                                                                             \
+    if (IP) dplasma_desc_destroy(IP);                                                                             \
+    unwrap(A, true);                                                                                              \
+    return info;                                                                                                  \
+  }                                                                                                               \
+  static void nat_p##P##trxm(bool solve, const char* side, const char* uplo, const char* ta, const char* diag,    \
+                             int m, int n, T alpha, T* a, int ia, int ja, const int* da, T* b, int ib, int jb,    \
+                             const int* db) {                                                                     \
+    const int sd = native_side(side), ka = sd == 141 ? m : n;                                                     \
+    Wrapped A = wrap(C, sizeof(T), a, ia, ja, da, ka, ka);                                                        \
+    Wrapped B = wrap(C, sizeof(T), b, ib, jb, db, m, n);                                                          \
+    if (A.d && B.d) {                                                                                             \
+      if (solve)                                                                                                  \
+        (void)dplasma_##P##trsm(native_ctx(), sd, native_uplo(uplo), native_trans(ta), native_diag(diag), alpha,  \
+                                A.d, B.d);                                                                        \
+      else                                                                                                        \
+        (void)dplasma_##P##trmm(native_ctx(), sd, native_uplo(uplo), native_trans(ta), native_diag(diag), alpha,  \
+                                A.d, B.d);                                                                        \
+    }                                                                                                             \
+    unwrap(A, false), unwrap(B, true);                                                                            \
+  }
+
+DPL_F77_NATIVE(s, float, 2)
+DPL_F77_NATIVE(d, double, 3)
+DPL_F77_NATIVE(c, dplasma_complex32_t, 4)
+DPL_F77_NATIVE(z, dplasma_complex64_t, 5)
+
 #define DPL_F77_PREC(P, T)                                                                                      \
   DPL_CAPI void p##P##gemm_(const char* transa, const char* transb, int* m, int* n, int* k, T* alpha, T* a,      \
                             int* ia, int* ja, int* desca, T* b, int* ib, int* jb, int* descb, T* beta, T* c,     \
-                            int* ic, int* jc, int* descc) { DplGil g;                                                      \
+                            int* ic, int* jc, int* descc) {                                                      \
+    if (native_grid(desca)) {                                                                                    \
+      nat_p##P##gemm(transa, transb, *m, *n, *k, *alpha, a, *ia, *ja, desca, b, *ib, *jb, descb, *beta, c, *ic,  \
+                     *jc, descc);                                                                                \
+      return;                                                                                                    \
+    }                                                                                                            \
+    DplGil g;                                                                                                    \
     f77("p" #P "gemm_", {chr(transa), chr(transb), iv(m), iv(n), iv(k), sc(alpha), dpl_arg_ptr(a), iv(ia),       \
                          iv(ja), desc_list(desca), dpl_arg_ptr(b), iv(ib), iv(jb), desc_list(descb), sc(beta),   \
                          dpl_arg_ptr(c), iv(ic), iv(jc), desc_list(descc)});                                     \
   }                                                                                                              \
-  DPL_CAPI void p##P##potrf_(const char* uplo, int* n, T* a, int* ia, int* ja, int* desca, int* info) { DplGil g; \
+  DPL_CAPI void p##P##potrf_(const char* uplo, int* n, T* a, int* ia, int* ja, int* desca, int* info) {          \
+    if (native_grid(desca)) {                                                                                    \
+      *info = nat_p##P##potrf(uplo, *n, a, *ia, *ja, desca);                                                     \
+      return;                                                                                                    \
+    }                                                                                                            \
+    DplGil g;                                                                                                    \
     *info = f77("p" #P "potrf_", {chr(uplo), iv(n), dpl_arg_ptr(a), iv(ia), iv(ja), desc_list(desca)});          \
   }                                                                                                              \
-  DPL_CAPI void p##P##getrf_(int* m, int* n, T* a, int* ia, int* ja, int* desca, int* ipiv, int* info) { DplGil g; \
+  DPL_CAPI void p##P##getrf_(int* m, int* n, T* a, int* ia, int* ja, int* desca, int* ipiv, int* info) {        \
+    if (native_grid(desca)) {                                                                                    \
+      *info = nat_p##P##getrf(*m, *n, a, *ia, *ja, desca, ipiv);                                                 \
+      return;                                                                                                    \
+    }                                                                                                            \
+    DplGil g;                                                                                                    \
     *info = f77("p" #P "getrf_",                                                                                 \
                 {iv(m), iv(n), dpl_arg_ptr(a), iv(ia), iv(ja), desc_list(desca), dpl_arg_ptr(ipiv)});            \
   }                                                                                                              \
   DPL_CAPI void p##P##trsm_(const char* side, const char* uplo, const char* transa, const char* diag, int* m,    \
                             int* n, T* alpha, T* a, int* ia, int* ja, int* desca, T* b, int* ib, int* jb,        \
-                            int* descb) { DplGil g;                                                              \
+                            int* descb) {                                                                        \
+    if (native_grid(desca)) {                                                                                    \
+      nat_p##P##trxm(true, side, uplo, transa, diag, *m, *n, *alpha, a, *ia, *ja, desca, b, *ib, *jb, descb);    \
+      return;                                                                                                    \
+    }                                                                                                            \
+    DplGil g;                                                                                                    \
     f77("p" #P "trsm_", {chr(side), chr(uplo), chr(transa), chr(diag), iv(m), iv(n), sc(alpha), dpl_arg_ptr(a),  \
                          iv(ia), iv(ja), desc_list(desca), dpl_arg_ptr(b), iv(ib), iv(jb), desc_list(descb)});   \
   }                                                                                                              \
   DPL_CAPI void p##P##trmm_(const char* side, const char* uplo, const char* transa, const char* diag, int* m,    \
                             int* n, T* alpha, T* a, int* ia, int* ja, int* desca, T* b, int* ib, int* jb,        \
-                            int* descb) { DplGil g;                                                              \
+                            int* descb) {                                                                        \
+    if (native_grid(desca)) {                                                                                    \
+      nat_p##P##trxm(false, side, uplo, transa, diag, *m, *n, *alpha, a, *ia, *ja, desca, b, *ib, *jb, descb);   \
+      return;                                                                                                    \
+    }                                                                                                            \
+    DplGil g;                                                                                                    \
     f77("p" #P "trmm_", {chr(side), chr(uplo), chr(transa), chr(diag), iv(m), iv(n), sc(alpha), dpl_arg_ptr(a),  \
                          iv(ia), iv(ja), desc_list(desca), dpl_arg_ptr(b), iv(ib), iv(jb), desc_list(descb)});   \
   }                                                                                                              \
@@ -163,7 +380,10 @@ static int latsqr_work(const int* desca) {
     if (work) work[0] = (T)lw;                                                                                   \
     if (*lwork == -1) return;                                                                                    \
     DplGil g;                                                                                                    \
-    *info = f77("p" #P "latsqr_", {iv(m), iv(n), dpl_arg_ptr(a), iv(ia), iv(ja), desc_list(desca),               \
+    int dpy[9];                                                                                                  \
+    std::memcpy(dpy, desca, sizeof dpy);                                                                         \
+    if (native_grid(desca)) dpy[1] = python_grid();   /* no native QR: the Python layer, 1 x 1 grid */        \
+    *info = f77("p" #P "latsqr_", {iv(m), iv(n), dpl_arg_ptr(a), iv(ia), iv(ja), desc_list(dpy),                 \
                                    dpl_arg_ptr(tau)});                                                           \
   }
 

@@ -54,13 +54,22 @@ int dpl_lascal(int prec, int part, int nitems, const void* items, int mmax, int 
                int lda, hipStream_t st);
 int dpl_tile_norm(int prec, int kind, int part, int unit, int nitems, const void* items, const void* A, int lda,
                   double* out, int ostride, hipStream_t st);
+long long dpl_lu_block_ws_bytes(int m);
+int dpl_lu_block(int prec, void* A, int ld, int m, int c0, int cend, int* ipiv, void* ws, int* cnt, int* info,
+                 int info_base, int pivot, hipStream_t st);
+int dpl_laswp_panel(int prec, void* A, int ld, int ca, int cb, const int* ipiv, int i0, int i1, hipStream_t st);
+int dpl_piv_moves(const int* ipiv, int kb, int* dst, int* src, int* cnt, hipStream_t st);
+int dpl_rows_permute(int prec, void* A, int ld, int mb, int r0, const long long* rowoff, int nrt,
+                     const long long* coloff, const int* ncols, int nct, int nb, const int* dst, const int* src,
+                     const int* cnt, int maxcnt, hipStream_t st);
+int dpl_ipiv_shift(const int* in, int* out, int n, int delta, hipStream_t st);
 }
 
 namespace {
 
 enum { NOTRANS = 111, TRANS = 112, CONJTRANS = 113, UPPER = 121, LOWER = 122, UPPERLOWER = 123, NONUNIT = 131,
        LEFT = 141, RIGHT = 142 };
-enum { P_S = 2, P_D = 3, P_C = 4, P_Z = 5 };
+enum { P_I = 1, P_S = 2, P_D = 3, P_C = 4, P_Z = 5 };   // P_I: int32 (pivot descriptors)
 
 // kernel records (csrc/kernels/common.h, gemm.hip, potrf_rb.hip)
 struct GemmItemK { long long c_off; int kt_beg, kt_cnt, m, n, flags, pad; };
@@ -70,7 +79,7 @@ struct RbItem { long long b_off; int rows, pad; };
 static_assert(sizeof(GemmItemK) == 32 && sizeof(KPair) == 24 && sizeof(TileItem) == 32 && sizeof(RbItem) == 16,
               "kernel record layouts");
 
-int esize(int prec) { return prec == P_S ? 4 : prec == P_Z ? 16 : 8; }
+int esize(int prec) { return prec == P_S || prec == P_I ? 4 : prec == P_Z ? 16 : 8; }
 bool prec_ok(int prec) { return prec >= P_S && prec <= P_Z; }
 
 // one scalar of a precision (complex = two reals), as the kernels' host API takes it
@@ -152,6 +161,7 @@ struct NatProgram {
   std::vector<NatTask> tasks;
   std::vector<hipEvent_t> ev;
   std::vector<DevPtr> keep;      // batch records and scratch referenced by the tasks
+  std::vector<std::shared_ptr<NatDesc>> wdesc;   // workspace matrices (trmm / symm / getrf panels)
   DevPtr info;                   // device int: first failing column (LAPACK info), 0 if none
   int result = 0;
   bool enqueued = false;
@@ -1001,7 +1011,7 @@ void nat_fini(dplasma_context_t* ctx) {
 
 dplasma_desc_t* nat_desc(dplasma_context_t* ctx, int prec, int mb, int nb, int m, int n, int P, int Q, void* data,
                          int lld, int on_device) {
-  if (!prec_ok(prec) || mb <= 0 || nb <= 0 || m < 0 || n < 0 || P > 1 || Q > 1) {
+  if ((!prec_ok(prec) && prec != P_I) || mb <= 0 || nb <= 0 || m < 0 || n < 0 || P > 1 || Q > 1) {
     dpl_set_error("native descriptor: one process (P = Q = 1), positive tile sizes, s/d/c/z");
     return nullptr;
   }
@@ -1028,7 +1038,8 @@ dplasma_desc_t* nat_desc(dplasma_context_t* ctx, int prec, int mb, int nb, int m
     d->data = (char*)data;
     d->lld = lld;
   } else {
-    d->lld = std::max(16, (m + 15) / 16 * 16);   // 128-byte aligned columns for the vector paths
+    // 128-byte aligned columns for the vector paths; pivot vectors (int32, 1 x n) stay contiguous
+    d->lld = prec == P_I ? std::max(1, m) : std::max(16, (m + 15) / 16 * 16);
     void* p = nullptr;
     const size_t bytes = (size_t)d->lld * std::max(1, n) * d->es;
     if (hipMalloc(&p, bytes) != hipSuccess || hipMemset(p, 0, bytes) != hipSuccess) {
@@ -1089,4 +1100,480 @@ void nat_free(dplasma_taskpool_t* tp) {
   auto& q = P->ctx->queue;
   q.erase(std::remove(q.begin(), q.end(), P), q.end());
   delete P;
+}
+
+// ============================================================================= level-3 extras, LU
+// TRMM / SYMM / HEMM (models/blas3.py): the triangular / symmetric operand is first expanded into a
+// program-owned full-tile workspace (the triangle, zeros elsewhere -- unit diagonal if asked -- or the
+// mirrored symmetric / Hermitian matrix), so the product is ONE launch of the MFMA GEMM engine whose
+// k-runs cover exactly the non-zero tiles.  LU with partial pivoting (models/lu.py, one process):
+// per panel, gather -> recursive panel LU (dgetrf2 recursion: 64-column persistent blocks, laswp,
+// TRSM, MFMA GEMM) -> device-derived net row moves applied in place -> write-back -> U row TRSM ->
+// trailing GEMM; pivots go to the IPIV descriptor on the device (1-based, global).
+namespace {
+
+std::shared_ptr<NatDesc> work_desc(NatProgram& P, const NatDesc& A) {
+  auto w = std::make_shared<NatDesc>();
+  w->ctx = A.ctx;
+  w->prec = A.prec;
+  w->es = A.es;
+  w->mb = A.mb;
+  w->nb = A.nb;
+  w->m = A.m;
+  w->n = A.n;
+  w->mt = A.mt;
+  w->nt = A.nt;
+  w->lld = std::max(16, (A.m + 15) / 16 * 16);
+  void* p = nullptr;
+  if (hipMalloc(&p, (size_t)w->lld * std::max(1, A.n) * A.es) != hipSuccess) return nullptr;
+  w->data = (char*)p;
+  w->owned = true;
+  P.wdesc.push_back(w);
+  return w;
+}
+
+// W := expansion of A's uplo triangle: mode 0 -- triangle (zeros elsewhere; unit diagonal if unit),
+// 1 -- symmetric (the other triangle mirrored with a transpose), 2 -- Hermitian (conjugate mirror,
+// real diagonal).  Tasks on stream 1, in order after `prev`; returns the last task (or -2 on failure).
+int add_expand(NatProgram& P, const NatDesc& A, int uplo, bool unit, int mode, NatDesc& W, int prev) {
+  const int prec = A.prec;
+  const Scalar zero(prec, 0.0), one(prec, 1.0), half(prec, 0.5);
+  auto all = std::make_shared<MapBatch>(), tri = std::make_shared<MapBatch>(), mir = std::make_shared<MapBatch>();
+  all->build(W, UPPERLOWER, nullptr, NOTRANS);
+  tri->build(W, uplo, &A, NOTRANS);
+  const int mtrans = mode == 2 ? CONJTRANS : TRANS;
+  if (mode > 0) mir->build(W, uplo == LOWER ? UPPER : LOWER, &A, mtrans);
+  if (!all->upload(P) || !tri->upload(P) || !mir->upload(P)) return -2;
+  const int lda = A.lld, ldw = W.lld, tpart = part_of(uplo), mpart = uplo == LOWER ? 4 : 3;
+  const char* a = A.data;
+  char* w = W.data;
+  if (mode == 0)
+    prev = P.task(1, [=](hipStream_t s) {
+      return dpl_laset(prec, 0, all->n(), all->items(), all->mm, all->nn, zero.ptr(), zero.ptr(), w, ldw, s);
+    }, {prev});
+  prev = P.task(1, [=](hipStream_t s) {
+    return dpl_geadd(prec, tpart, NOTRANS, tri->n(), tri->items(), tri->mm, tri->nn, one.ptr(), a, lda, zero.ptr(), w,
+                     ldw, 1, s);
+  }, {prev});
+  if (mode > 0)
+    prev = P.task(1, [=](hipStream_t s) {
+      return dpl_geadd(prec, mpart, mtrans, mir->n(), mir->items(), mir->mm, mir->nn, one.ptr(), a, lda, zero.ptr(),
+                       w, ldw, 1, s);
+    }, {prev});
+  if ((mode == 0 && unit) || (mode == 2 && (prec == P_C || prec == P_Z))) {
+    std::vector<TileItem> d;
+    int mm = 0;
+    for (int k = 0; k < W.mt && k < W.nt; ++k) {
+      d.push_back(TileItem{W.off(k, k), W.off(k, k), W.rows(k), W.cols(k), k * W.mb, k * W.nb});
+      mm = std::max(mm, std::max(W.rows(k), W.cols(k)));
+    }
+    DevPtr dd = dev_upload(d);
+    if (!dd) return -2;
+    P.keep.push_back(dd);
+    const int nd = (int)d.size();
+    if (mode == 0)   // unit diagonal
+      prev = P.task(1, [=](hipStream_t s) {
+        return dpl_laset(prec, 5, nd, dd->p, mm, mm, zero.ptr(), one.ptr(), w, ldw, s);
+      }, {prev});
+    else             // diag := (diag + conj(diag)) / 2
+      prev = P.task(1, [=](hipStream_t s) {
+        return dpl_geadd(prec, 5, CONJTRANS, nd, dd->p, mm, mm, half.ptr(), w, ldw, half.ptr(), w, ldw, 0, s);
+      }, {prev});
+  }
+  return prev;
+}
+
+}  // namespace
+
+NatProgram* nat_trmm(dplasma_context_t* ctx, int prec, int side, int uplo, int trans, int diag, const void* alpha,
+                     dplasma_desc_t* dA, dplasma_desc_t* dB) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *B = dB ? dB->nat : nullptr;
+  if (!same_ctx(c, {A, B}, prec)) return fail(nullptr, "trmm: descriptors of another context or precision");
+  const bool left = side == LEFT, notrans = trans == NOTRANS;
+  const int order = left ? B->m : B->n;
+  if (A->m != A->n || A->m != order || A->mb != A->nb || (left ? B->mb : B->nb) != A->nb ||
+      (uplo != LOWER && uplo != UPPER))
+    return fail(nullptr, "trmm: operands do not conform");
+  NatProgram* P = new_program(c, "trmm", false);
+  auto T = work_desc(*P, *A), W = work_desc(*P, *B);
+  if (!T || !W) return fail(P, "trmm: device allocation failed");
+  int prev = add_expand(*P, *A, uplo, diag == UNIT, 0, *T, -1);
+  auto cp = std::make_shared<MapBatch>();
+  cp->build(*W, UPPERLOWER, B, NOTRANS);
+  if (prev == -2 || !cp->upload(*P)) return fail(P, "trmm: device allocation failed");
+  const Scalar one(prec, 1.0), zero(prec, 0.0), al(prec, alpha);
+  char *bb = B->data, *wd = W->data, *td = T->data;
+  const int ldb = B->lld, ldw = W->lld, ldt = T->lld;
+  prev = P->task(1, [=](hipStream_t s) {
+    return dpl_geadd(prec, 0, NOTRANS, cp->n(), cp->items(), cp->mm, cp->nn, one.ptr(), bb, ldb, zero.ptr(), wd, ldw,
+                     1, s);
+  }, {prev});
+  // B(m,n) = alpha sum_k op(T)(m,k) W(k,n) (left) / alpha sum_k W(m,k) op(T)(k,n) (right), k over the
+  // triangle only: op(A) is lower iff (uplo == Lower) == (trans == NoTrans)
+  const bool lower_op = (uplo == LOWER) == notrans;
+  auto g = std::make_shared<Gemm>();
+  for (int n = 0; n < B->nt; ++n)
+    for (int m = 0; m < B->mt; ++m) {
+      std::vector<KPair> kp;
+      const int i = left ? m : n;
+      const int k0 = left ? (lower_op ? 0 : i) : (lower_op ? i : 0);
+      const int k1 = left ? (lower_op ? i + 1 : A->mt) : (lower_op ? A->mt : i + 1);
+      for (int k = k0; k < k1; ++k) {
+        if (left)
+          kp.push_back(KPair{notrans ? T->off(m, k) : T->off(k, m), W->off(k, n), A->rows(k), 0});
+        else
+          kp.push_back(KPair{W->off(m, k), notrans ? T->off(k, n) : T->off(n, k), A->rows(k), 0});
+      }
+      g->add(B->off(m, n), B->rows(m), B->cols(n), kp, 0);
+    }
+  if (!g->upload(*P)) return fail(P, "trmm: device allocation failed");
+  if (left)
+    P->task(1, [=](hipStream_t s) { return g->launch(prec, trans, NOTRANS, al, td, ldt, wd, ldw, zero, bb, ldb, s); },
+            {prev});
+  else
+    P->task(1, [=](hipStream_t s) { return g->launch(prec, NOTRANS, trans, al, wd, ldw, td, ldt, zero, bb, ldb, s); },
+            {prev});
+  return P;
+}
+
+static NatProgram* symm_like(dplasma_context_t* ctx, int prec, int side, int uplo, const void* alpha,
+                             dplasma_desc_t* dA, dplasma_desc_t* dB, const void* beta, dplasma_desc_t* dC, bool herm) {
+  const char* name = herm ? "hemm" : "symm";
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *B = dB ? dB->nat : nullptr, *C = dC ? dC->nat : nullptr;
+  if (!same_ctx(c, {A, B, C}, prec)) return fail(nullptr, std::string(name) + ": descriptors of another context");
+  const bool left = side == LEFT;
+  if (A->m != A->n || A->mb != A->nb || B->m != C->m || B->n != C->n || B->mb != C->mb || B->nb != C->nb ||
+      (left ? C->m : C->n) != A->m || (left ? C->mb : C->nb) != A->nb || (uplo != LOWER && uplo != UPPER))
+    return fail(nullptr, std::string(name) + ": operands do not conform");
+  NatProgram* P = new_program(c, name, false);
+  auto S = work_desc(*P, *A);
+  if (!S) return fail(P, std::string(name) + ": device allocation failed");
+  const int prev = add_expand(*P, *A, uplo, false, herm ? 2 : 1, *S, -1);
+  auto g = std::make_shared<Gemm>();
+  for (int n = 0; n < C->nt; ++n)
+    for (int m = 0; m < C->mt; ++m) {
+      std::vector<KPair> kp;
+      for (int k = 0; k < A->mt; ++k)
+        kp.push_back(left ? KPair{S->off(m, k), B->off(k, n), A->rows(k), 0}
+                          : KPair{B->off(m, k), S->off(k, n), A->rows(k), 0});
+      g->add(C->off(m, n), C->rows(m), C->cols(n), kp, 0);
+    }
+  if (prev == -2 || !g->upload(*P)) return fail(P, std::string(name) + ": device allocation failed");
+  const Scalar al(prec, alpha), be(prec, beta);
+  const char *sd = S->data, *bd = B->data;
+  char* cd = C->data;
+  const int lds = S->lld, ldb = B->lld, ldc = C->lld;
+  if (left)
+    P->task(1, [=](hipStream_t s) { return g->launch(prec, NOTRANS, NOTRANS, al, sd, lds, bd, ldb, be, cd, ldc, s); },
+            {prev});
+  else
+    P->task(1, [=](hipStream_t s) { return g->launch(prec, NOTRANS, NOTRANS, al, bd, ldb, sd, lds, be, cd, ldc, s); },
+            {prev});
+  return P;
+}
+
+NatProgram* nat_symm(dplasma_context_t* ctx, int prec, int side, int uplo, const void* alpha, dplasma_desc_t* A,
+                     dplasma_desc_t* B, const void* beta, dplasma_desc_t* C) {
+  return symm_like(ctx, prec, side, uplo, alpha, A, B, beta, C, false);
+}
+
+NatProgram* nat_hemm(dplasma_context_t* ctx, int prec, int side, int uplo, const void* alpha, dplasma_desc_t* A,
+                     dplasma_desc_t* B, const void* beta, dplasma_desc_t* C) {
+  if (prec != P_C && prec != P_Z) return fail(nullptr, "hemm: complex precisions only");
+  return symm_like(ctx, prec, side, uplo, alpha, A, B, beta, C, true);
+}
+
+// lansy / lanhe: the norm of the expanded symmetric / Hermitian matrix (synchronous, like lange)
+static double norm_sym(dplasma_context_t* ctx, int prec, int ntype, int uplo, dplasma_desc_t* dA, bool herm) {
+  NatDesc* A = dA ? dA->nat : nullptr;
+  const char* name = herm ? "lanhe" : "lansy";
+  if (!same_ctx(ctx->nat, {A}, prec) || (uplo != LOWER && uplo != UPPER) || A->m != A->n || A->mb != A->nb) {
+    dpl_set_error((std::string(name) + ": bad descriptor or uplo").c_str());
+    return NAN;
+  }
+  NatProgram* P = new_program(ctx->nat, name, false);
+  auto S = work_desc(*P, *A);
+  if (!S || add_expand(*P, *A, uplo, false, herm ? 2 : 1, *S, -1) == -2) {
+    delete P;
+    dpl_set_error((std::string(name) + ": device allocation failed").c_str());
+    return NAN;
+  }
+  auto keep = P->wdesc;    // the expanded matrix outlives the program
+  if (P->run() != 0 || P->wait() != 0) {
+    delete P;
+    dpl_set_error((std::string(name) + ": kernel launch failed").c_str());
+    return NAN;
+  }
+  delete P;
+  bool ok;
+  const double r = norm_tiles(*S, ntype, UPPERLOWER, false, ctx->nat->st[1], ok);
+  if (!ok) { dpl_set_error((std::string(name) + ": unsupported norm or kernel failure").c_str()); return NAN; }
+  return r;
+}
+
+double nat_lansy(dplasma_context_t* ctx, int prec, int ntype, int uplo, dplasma_desc_t* A) {
+  return norm_sym(ctx, prec, ntype, uplo, A, false);
+}
+
+double nat_lanhe(dplasma_context_t* ctx, int prec, int ntype, int uplo, dplasma_desc_t* A) {
+  if (prec != P_C && prec != P_Z) { dpl_set_error("lanhe: complex precisions only"); return NAN; }
+  return norm_sym(ctx, prec, ntype, uplo, A, true);
+}
+
+// ----------------------------------------------------------------------------- LU (partial pivoting)
+namespace {
+
+constexpr int LU_BW = 64;   // base-case width of the recursive panel (dpl_lu_block)
+
+struct LuScratch {
+  DevPtr pv, piv, ws, cnt, mdst, msrc, mcnt, rowoff, coloff, ncols;
+};
+
+// the dgetrf2 recursion of ops.PanelLU on the panel pv (m x n, ld): tasks on stream 1 after prev
+int add_panel_lu(NatProgram& P, int prec, char* pv, int ld, int m, int c0, int n, const LuScratch& S, int* info,
+                 int info_base, int prev) {
+  const Scalar one(prec, 1.0), m_one(prec, -1.0);
+  int* piv = (int*)S.piv->p;
+  void* ws = S.ws->p;
+  int* cnt = (int*)S.cnt->p;
+  if (n <= LU_BW) {
+    return P.task(1, [=](hipStream_t s) {
+      return dpl_lu_block(prec, pv, ld, m, c0, c0 + n, piv, ws, cnt, info, info_base, 1, s);
+    }, {prev});
+  }
+  const int n1 = (n / 2 + 15) / 16 * 16, c1 = c0 + n1;
+  prev = add_panel_lu(P, prec, pv, ld, m, c0, n1, S, info, info_base, prev);
+  if (prev < 0) return prev;
+  prev = P.task(1, [=](hipStream_t s) { return dpl_laswp_panel(prec, pv, ld, c1, c0 + n, piv, c0, c1, s); }, {prev});
+  auto tr = std::make_shared<Trsm1>();
+  tr->tri = c0 + (long long)c0 * ld;
+  tr->add(c0 + (long long)c1 * ld, n1, n - n1);
+  if (!tr->upload(P, prec, LEFT)) return -2;
+  prev = P.task(1, [=](hipStream_t s) {
+    return tr->launch(prec, LEFT, LOWER, NOTRANS, UNIT, one, pv, ld, pv, ld, s);
+  }, {prev});
+  if (m > c1) {
+    auto g = std::make_shared<Gemm>();
+    g->add(c1 + (long long)c1 * ld, m - c1, n - n1, {KPair{c1 + (long long)c0 * ld, c0 + (long long)c1 * ld, n1, 0}},
+           0);
+    if (!g->upload(P)) return -2;
+    prev = P.task(1, [=](hipStream_t s) {
+      return g->launch(prec, NOTRANS, NOTRANS, m_one, pv, ld, pv, ld, one, pv, ld, s);
+    }, {prev});
+  }
+  prev = add_panel_lu(P, prec, pv, ld, m, c1, n - n1, S, info, info_base, prev);
+  if (prev < 0) return prev;
+  return P.task(1, [=](hipStream_t s) { return dpl_laswp_panel(prec, pv, ld, c0, c1, piv, c1, c0 + n, s); }, {prev});
+}
+
+bool lu_scratch(NatProgram& P, const NatDesc& A, LuScratch& S) {
+  S.pv = dev_alloc((size_t)std::max(1, A.m) * A.nb * A.es, false);
+  S.piv = dev_alloc(sizeof(int) * (A.nb + 16), true);
+  S.ws = dev_alloc((size_t)dpl_lu_block_ws_bytes(std::max(1, A.m)) + 64, true);
+  S.cnt = dev_alloc(64, true);
+  S.mdst = dev_alloc(sizeof(int) * 2 * (A.mb + 16), true);
+  S.msrc = dev_alloc(sizeof(int) * 2 * (A.mb + 16), true);
+  S.mcnt = dev_alloc(64, true);
+  std::vector<long long> ro(A.mt), co(A.nt);
+  std::vector<int> nc(A.nt);
+  for (int m = 0; m < A.mt; ++m) ro[m] = A.off(m, 0);
+  for (int n = 0; n < A.nt; ++n) {
+    co[n] = A.off(0, n);
+    nc[n] = A.cols(n);
+  }
+  S.rowoff = dev_upload(ro);
+  S.coloff = dev_upload(co);
+  S.ncols = dev_upload(nc);
+  for (const DevPtr& d : {S.pv, S.piv, S.ws, S.cnt, S.mdst, S.msrc, S.mcnt, S.rowoff, S.coloff, S.ncols}) {
+    if (!d) return false;
+    P.keep.push_back(d);
+  }
+  return true;
+}
+
+// row interchanges of panel step k (rows r0 + piv[j] <-> r0 + j, j < kmin, sequential) applied to every
+// tile column of B in place (forward) or undone (inverse: the net moves with source and destination swapped)
+int add_row_moves(NatProgram& P, const NatDesc& B, const LuScratch& S, const DevPtr& rowoff, const DevPtr& coloff,
+                  const DevPtr& ncols, int r0, int kmin, bool inverse, int prev) {
+  const int prec = B.prec, ld = B.lld, mb = B.mb, nb = B.nb, mt = B.mt, nt = B.nt, maxcnt = 2 * mb;
+  char* b = B.data;
+  const int* piv = (const int*)S.piv->p;
+  int *dst = (int*)S.mdst->p, *src = (int*)S.msrc->p, *cnt = (int*)S.mcnt->p;
+  const long long *ro = (const long long*)rowoff->p, *co = (const long long*)coloff->p;
+  const int* nc = (const int*)ncols->p;
+  prev = P.task(1, [=](hipStream_t s) { return dpl_piv_moves(piv, kmin, dst, src, cnt, s); }, {prev});
+  return P.task(1, [=](hipStream_t s) {
+    return dpl_rows_permute(prec, b, ld, mb, r0, ro, mt, co, nc, nt, nb, inverse ? src : dst, inverse ? dst : src, cnt,
+                            maxcnt, s);
+  }, {prev});
+}
+
+bool add_getrf(NatProgram& P, NatDesc& A, NatDesc& IP, int& last) {
+  const int prec = A.prec, mb = A.mb, ld = A.lld;
+  const int kt = std::min(A.mt, A.nt);
+  LuScratch S;
+  if (!lu_scratch(P, A, S)) return false;
+  char* a = A.data;
+  char* pvb = (char*)S.pv->p;
+  int* info = (int*)P.info->p;
+  int* ipg = (int*)IP.data;
+  const Scalar one(prec, 1.0), m_one(prec, -1.0), zero(prec, 0.0);
+  int prev = last;
+  for (int k = 0; k < kt; ++k) {
+    const int kb = A.cols(k), r0 = k * mb, mp = A.m - r0, kmin = std::min(mp, kb);
+    // gather column k (tiles m >= k) into the contiguous panel (ld = mp)
+    auto gat = std::make_shared<MapBatch>(), back = std::make_shared<MapBatch>();
+    for (int m = k; m < A.mt; ++m) {
+      gat->it.push_back(TileItem{A.off(m, k), (long long)(m - k) * mb, A.rows(m), kb, 0, 0});
+      back->it.push_back(TileItem{(long long)(m - k) * mb, A.off(m, k), A.rows(m), kb, 0, 0});
+      gat->mm = back->mm = std::max(gat->mm, A.rows(m));
+    }
+    gat->nn = back->nn = kb;
+    if (!gat->upload(P) || !back->upload(P)) return false;
+    prev = P.task(1, [=](hipStream_t s) {
+      return dpl_geadd(prec, 0, NOTRANS, gat->n(), gat->items(), gat->mm, gat->nn, one.ptr(), a, ld, zero.ptr(), pvb,
+                       mp, 1, s);
+    }, {prev});
+    prev = add_panel_lu(P, prec, pvb, mp, mp, 0, kmin, S, info, r0, prev);
+    if (prev < 0) return false;
+    if (kb > kmin) {   // wide last panel: the columns past the last row get the swaps and U = L^-1 A
+      const int* piv = (const int*)S.piv->p;
+      prev = P.task(1, [=](hipStream_t s) { return dpl_laswp_panel(prec, pvb, mp, kmin, kb, piv, 0, kmin, s); },
+                    {prev});
+      auto tr = std::make_shared<Trsm1>();
+      tr->tri = 0;
+      tr->add((long long)kmin * mp, kmin, kb - kmin);
+      if (!tr->upload(P, prec, LEFT)) return false;
+      prev = P.task(1, [=](hipStream_t s) {
+        return tr->launch(prec, LEFT, LOWER, NOTRANS, UNIT, one, pvb, mp, pvb, mp, s);
+      }, {prev});
+    }
+    // pivots -> IPIV (1-based, global); net row moves on every tile column; factored panel back
+    const int* piv = (const int*)S.piv->p;
+    prev = P.task(1, [=](hipStream_t s) { return dpl_ipiv_shift(piv, ipg + r0, kmin, r0 + 1, s); }, {prev});
+    prev = add_row_moves(P, A, S, S.rowoff, S.coloff, S.ncols, r0, kmin, false, prev);
+    prev = P.task(1, [=](hipStream_t s) {
+      return dpl_geadd(prec, 0, NOTRANS, back->n(), back->items(), back->mm, back->nn, one.ptr(), pvb, mp, zero.ptr(),
+                       a, ld, 1, s);
+    }, {prev});
+    if (k + 1 >= A.nt) continue;
+    // U row: A(k, n) := L11^-1 A(k, n); trailing update A(m, n) -= L(m, k) U(k, n)
+    auto tr = std::make_shared<Trsm1>();
+    tr->tri = 0;
+    for (int n = k + 1; n < A.nt; ++n) tr->add(A.off(k, n), kmin, A.cols(n));
+    if (!tr->upload(P, prec, LEFT)) return false;
+    prev = P.task(1, [=](hipStream_t s) {
+      return tr->launch(prec, LEFT, LOWER, NOTRANS, UNIT, one, pvb, mp, a, ld, s);
+    }, {prev});
+    if (k + 1 >= A.mt) continue;
+    auto g = std::make_shared<Gemm>();
+    for (int n = k + 1; n < A.nt; ++n)
+      for (int m = k + 1; m < A.mt; ++m)
+        g->add(A.off(m, n), A.rows(m), A.cols(n), {KPair{(long long)(m - k) * mb, A.off(k, n), kmin, 0}}, 0);
+    if (!g->upload(P)) return false;
+    prev = P.task(1, [=](hipStream_t s) {
+      return g->launch(prec, NOTRANS, NOTRANS, m_one, pvb, mp, a, ld, one, a, ld, s);
+    }, {prev});
+  }
+  last = prev;
+  return true;
+}
+
+// op(A) X = B with A = P L U from add_getrf (reference getrs: laswp + two TRSM, or the transposed order)
+bool add_getrs(NatProgram& P, int trans, NatDesc& A, NatDesc& IP, NatDesc& B, int& last) {
+  const int kt = std::min(A.mt, A.nt);
+  LuScratch S;
+  S.piv = dev_alloc(sizeof(int) * (A.nb + 16), true);
+  S.mdst = dev_alloc(sizeof(int) * 2 * (A.mb + 16), true);
+  S.msrc = dev_alloc(sizeof(int) * 2 * (A.mb + 16), true);
+  S.mcnt = dev_alloc(64, true);
+  std::vector<long long> ro(B.mt), co(B.nt);
+  std::vector<int> nc(B.nt);
+  for (int m = 0; m < B.mt; ++m) ro[m] = B.off(m, 0);
+  for (int n = 0; n < B.nt; ++n) {
+    co[n] = B.off(0, n);
+    nc[n] = B.cols(n);
+  }
+  DevPtr rowoff = dev_upload(ro), coloff = dev_upload(co), ncols = dev_upload(nc);
+  for (const DevPtr& d : {S.piv, S.mdst, S.msrc, S.mcnt, rowoff, coloff, ncols}) {
+    if (!d) return false;
+    P.keep.push_back(d);
+  }
+  const int* ipg = (const int*)IP.data;
+  int* piv = (int*)S.piv->p;
+  const Scalar one(B.prec, 1.0);
+  int prev = last;
+  auto swaps = [&](int k, bool inverse) {
+    const int r0 = k * A.mb, kmin = std::min(A.m - r0, A.cols(k));
+    prev = P.task(1, [=](hipStream_t s) { return dpl_ipiv_shift(ipg + r0, piv, kmin, -(r0 + 1), s); }, {prev});
+    prev = add_row_moves(P, B, S, rowoff, coloff, ncols, r0, kmin, inverse, prev);
+  };
+  auto solve = [&](int uplo, int tr, int diag) {
+    if (!add_trsm(P, LEFT, uplo, tr, diag, one, A, B, 1, prev)) return false;
+    prev = last_on(P, 1);
+    return true;
+  };
+  if (trans == NOTRANS) {
+    for (int k = 0; k < kt; ++k) swaps(k, false);
+    if (!solve(LOWER, NOTRANS, UNIT) || !solve(UPPER, NOTRANS, NONUNIT)) return false;
+  } else {
+    if (!solve(UPPER, trans, NONUNIT) || !solve(LOWER, trans, UNIT)) return false;
+    for (int k = kt - 1; k >= 0; --k) swaps(k, true);
+  }
+  last = prev;
+  return true;
+}
+
+bool lu_conform(const NatDesc* A, const NatDesc* IP) {
+  return A && IP && A->mb == A->nb && A->mb <= 512 && IP->prec == P_I && IP->m == 1 && IP->lld == 1 &&
+         IP->n >= std::min(A->m, A->n);
+}
+
+}  // namespace
+
+NatProgram* nat_getrf_1d(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dplasma_desc_t* dIP) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *IP = dIP ? dIP->nat : nullptr;
+  if (!same_ctx(c, {A}, prec) || !IP || IP->ctx != c)
+    return fail(nullptr, "getrf_1d: descriptors of another context or precision");
+  if (!lu_conform(A, IP)) return fail(nullptr, "getrf_1d: square tiles <= 512 and an IPIV of min(M, N) entries");
+  NatProgram* P = new_program(c, "getrf_1d", true);
+  int last = -1;
+  if (!P->info || !add_getrf(*P, *A, *IP, last)) return fail(P, "getrf_1d: device allocation failed");
+  return P;
+}
+
+NatProgram* nat_getrs(dplasma_context_t* ctx, int prec, int trans, dplasma_desc_t* dA, dplasma_desc_t* dIP,
+                      dplasma_desc_t* dB) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *IP = dIP ? dIP->nat : nullptr, *B = dB ? dB->nat : nullptr;
+  if (!same_ctx(c, {A, B}, prec) || !IP || IP->ctx != c)
+    return fail(nullptr, "getrs: descriptors of another context or precision");
+  if (!lu_conform(A, IP) || A->m != A->n || B->m != A->n || B->mb != A->mb)
+    return fail(nullptr, "getrs: operands do not conform");
+  NatProgram* P = new_program(c, "getrs", false);
+  int last = -1;
+  if (!add_getrs(*P, trans, *A, *IP, *B, last)) return fail(P, "getrs: device allocation failed");
+  return P;
+}
+
+NatProgram* nat_gesv_1d(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dplasma_desc_t* dIP,
+                        dplasma_desc_t* dB) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *IP = dIP ? dIP->nat : nullptr, *B = dB ? dB->nat : nullptr;
+  if (!same_ctx(c, {A, B}, prec) || !IP || IP->ctx != c)
+    return fail(nullptr, "gesv_1d: descriptors of another context or precision");
+  if (!lu_conform(A, IP) || A->m != A->n || B->m != A->n || B->mb != A->mb)
+    return fail(nullptr, "gesv_1d: operands do not conform");
+  NatProgram* P = new_program(c, "gesv_1d", true);
+  int last = -1;
+  if (!P->info || !add_getrf(*P, *A, *IP, last) || !add_getrs(*P, NOTRANS, *A, *IP, *B, last))
+    return fail(P, "gesv_1d: device allocation failed");
+  return P;
+}
+
+dplasma_desc_t* nat_desc_int(dplasma_context_t* ctx, int mb, int nb, int m, int n) {
+  return nat_desc(ctx, P_I, mb, nb, m, n, 1, 1, nullptr, 0, 1);
 }

@@ -413,3 +413,16 @@ DPL_API int dpl_delay(double us, int nwg, hipStream_t st) {
   hipLaunchKernelGGL(k_delay, dim3(nwg < 1 ? 1 : nwg), dim3(64), 0, st, ticks);
   return (int)hipGetLastError();
 }
+
+// out[i] = in[i] + delta, i < n (pivot index bookkeeping: panel-relative <-> global, 0 <-> 1-based)
+__global__ __launch_bounds__(256) void k_ipiv_shift(const int* __restrict__ in, int* __restrict__ out, int n,
+                                                    int delta) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = in[i] + delta;
+}
+
+DPL_API int dpl_ipiv_shift(const int* in, int* out, int n, int delta, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_ipiv_shift, dim3((n + 255) / 256), dim3(256), 0, st, in, out, n, delta);
+  return (int)hipGetLastError();
+}

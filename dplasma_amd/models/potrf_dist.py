@@ -46,7 +46,8 @@ from ..utils.flops import flops
 DIST_DEFER = 2
 DIST_LOOKAHEAD = 2
 DIST_BULK_RESERVE = 0
-DIST_CHUNK = 8      # D = 1: tiles per pipelined chunk (potrf_pipelined_New); 0 = whole-piece schedule
+DIST_CHUNK = 0      # D = 1: tiles per pipelined chunk (potrf_pipelined_New); 0 = whole-piece schedule (replay: chunking
+#                   loses, 285 vs 241 ms at chunk 8 -- profiles/r3_replay_pipelined_chunks.txt)
 
 
 class _Panel:

@@ -94,6 +94,7 @@ _SIGS = {
     "dpl_stream_cumask": [c_vp, c_int, c_vp],
     "dpl_stream_destroy": [c_vp],
     "dpl_delay": [ctypes.c_double, c_int, c_vp],
+    "dpl_ipiv_shift": [c_vp, c_vp, c_int, c_int, c_vp],
     "dpl_gemm_set_wg_cap": [c_int],
     "dpl_rows_permute": [c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp,
                          c_int, c_vp],

@@ -442,6 +442,161 @@ static void on_fault(int sig) {
   _exit(128 + sig);
 }
 
+/* dense host reference helpers (column-major, n x n / m x n) */
+static double rnd_fill(double *x, size_t n, unsigned *s) {
+  double m = 0;
+  for (size_t i = 0; i < n; ++i) {
+    *s = *s * 1103515245u + 12345u;
+    x[i] = ((*s >> 8) & 0xffff) / 65536.0 - 0.5;
+    m = fmax(m, fabs(x[i]));
+  }
+  return m;
+}
+
+/* dtrmm: B := alpha op(A) B / alpha B op(A), A triangular (ragged 300 with nb 128) */
+static void test_dtrmm(dplasma_context_t *ctx, int side, int uplo, int trans, int diag) {
+  const int nb = 128, M = 300, N = 250, ka = side == dplasmaLeft ? M : N;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, ka, ka), *B = dmat(ctx, dplasmaRealDouble, nb, M, N);
+  double *a = malloc(sizeof(double) * ka * ka), *b = malloc(sizeof(double) * M * N), *r = malloc(sizeof(double) * M * N);
+  unsigned sd = 7 + side + uplo + trans + diag;
+  rnd_fill(a, (size_t)ka * ka, &sd);
+  rnd_fill(b, (size_t)M * N, &sd);
+  dplasma_desc_set_lapack(A, a, ka);
+  dplasma_desc_set_lapack(B, b, M);
+  const double alpha = 0.75;
+  CHECK(dplasma_dtrmm(ctx, side, uplo, trans, diag, alpha, A, B) == 0, "dtrmm: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(B, r, M);
+  double err = 0;
+#define TA(i, j) (((uplo == dplasmaLower) ? (i) >= (j) : (i) <= (j)) ? ((i) == (j) && diag == dplasmaUnit ? 1.0 : a[(i) + (size_t)(j) * ka]) : 0.0)
+#define OPA(i, j) (trans == dplasmaNoTrans ? TA(i, j) : TA(j, i))
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i < M; ++i) {
+      double s = 0;
+      if (side == dplasmaLeft)
+        for (int k = 0; k < M; ++k) s += OPA(i, k) * b[k + (size_t)j * M];
+      else
+        for (int k = 0; k < N; ++k) s += b[i + (size_t)k * M] * OPA(k, j);
+      err = fmax(err, fabs(alpha * s - r[i + (size_t)j * M]));
+    }
+#undef OPA
+#undef TA
+  printf("dtrmm %c%c%c%c max error %.3e\n", side == dplasmaLeft ? 'L' : 'R', uplo == dplasmaLower ? 'L' : 'U',
+         trans == dplasmaNoTrans ? 'N' : 'T', diag == dplasmaUnit ? 'U' : 'N', err);
+  CHECK(err < 1e-12, "dtrmm error %.3e", err);
+  free(a), free(b), free(r);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(B);
+}
+
+/* dsymm (left, lower) and zhemm (right, upper): the unused triangle of A holds garbage that must be ignored */
+static void test_symm_hemm(dplasma_context_t *ctx) {
+  const int nb = 128, M = 260, N = 190;
+  {
+    dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, M, M), *B = dmat(ctx, dplasmaRealDouble, nb, M, N);
+    dplasma_desc_t *C = dmat(ctx, dplasmaRealDouble, nb, M, N);
+    double *a = malloc(sizeof(double) * M * M), *b = malloc(sizeof(double) * M * N), *c = malloc(sizeof(double) * M * N);
+    double *r = malloc(sizeof(double) * M * N);
+    unsigned sd = 99;
+    rnd_fill(a, (size_t)M * M, &sd), rnd_fill(b, (size_t)M * N, &sd), rnd_fill(c, (size_t)M * N, &sd);
+    dplasma_desc_set_lapack(A, a, M), dplasma_desc_set_lapack(B, b, M), dplasma_desc_set_lapack(C, c, M);
+    CHECK(dplasma_dsymm(ctx, dplasmaLeft, dplasmaLower, 1.25, A, B, -0.5, C) == 0, "dsymm: %s", dplasma_last_error());
+    dplasma_desc_get_lapack(C, r, M);
+    double err = 0;
+    for (int j = 0; j < N; ++j)
+      for (int i = 0; i < M; ++i) {
+        double s = 0;
+        for (int k = 0; k < M; ++k) s += (i >= k ? a[i + (size_t)k * M] : a[k + (size_t)i * M]) * b[k + (size_t)j * M];
+        err = fmax(err, fabs(1.25 * s - 0.5 * c[i + (size_t)j * M] - r[i + (size_t)j * M]));
+      }
+    printf("dsymm LL max error %.3e\n", err);
+    CHECK(err < 1e-12, "dsymm error %.3e", err);
+    free(a), free(b), free(c), free(r);
+    dplasma_desc_destroy(A), dplasma_desc_destroy(B), dplasma_desc_destroy(C);
+  }
+  {
+    dplasma_desc_t *A = dmat(ctx, dplasmaComplexDouble, nb, N, N), *B = dmat(ctx, dplasmaComplexDouble, nb, M, N);
+    dplasma_desc_t *C = dmat(ctx, dplasmaComplexDouble, nb, M, N);
+    double complex *a = malloc(sizeof(double complex) * N * N), *b = malloc(sizeof(double complex) * M * N);
+    double complex *c = malloc(sizeof(double complex) * M * N), *r = malloc(sizeof(double complex) * M * N);
+    unsigned sd = 5;
+    rnd_fill((double *)a, 2 * (size_t)N * N, &sd), rnd_fill((double *)b, 2 * (size_t)M * N, &sd);
+    rnd_fill((double *)c, 2 * (size_t)M * N, &sd);
+    dplasma_desc_set_lapack(A, a, N), dplasma_desc_set_lapack(B, b, M), dplasma_desc_set_lapack(C, c, M);
+    const double complex al = 0.5 - 0.25 * I, be = 1.5;
+    CHECK(dplasma_zhemm(ctx, dplasmaRight, dplasmaUpper, al, A, B, be, C) == 0, "zhemm: %s", dplasma_last_error());
+    dplasma_desc_get_lapack(C, r, M);
+    double err = 0;
+    for (int j = 0; j < N; ++j)
+      for (int i = 0; i < M; ++i) {
+        double complex s = 0;
+        for (int k = 0; k < N; ++k) {
+          const double complex h = k < j ? a[k + (size_t)j * N] : k > j ? conj(a[j + (size_t)k * N]) : creal(a[j + (size_t)j * N]);
+          s += b[i + (size_t)k * M] * h;
+        }
+        err = fmax(err, cabs(al * s + be * c[i + (size_t)j * M] - r[i + (size_t)j * M]));
+      }
+    printf("zhemm RU max error %.3e\n", err);
+    CHECK(err < 1e-12, "zhemm error %.3e", err);
+    /* lanhe (frobenius) of the same A against the expanded host matrix */
+    double f = 0;
+    for (int j = 0; j < N; ++j)
+      for (int i = 0; i < N; ++i) {
+        const double complex h = i < j ? a[i + (size_t)j * N] : i > j ? conj(a[j + (size_t)i * N]) : creal(a[i + (size_t)i * N]);
+        f += creal(h * conj(h));
+      }
+    const double fn = dplasma_zlanhe(ctx, dplasmaFrobeniusNorm, dplasmaUpper, A);
+    printf("zlanhe F %.12e host %.12e\n", fn, sqrt(f));
+    CHECK(fabs(fn - sqrt(f)) < 1e-12 * sqrt(f), "zlanhe %.12e vs %.12e", fn, sqrt(f));
+    free(a), free(b), free(c), free(r);
+    dplasma_desc_destroy(A), dplasma_desc_destroy(B), dplasma_desc_destroy(C);
+  }
+}
+
+/* dgetrf_1d + dgetrs (both transposes) and dgesv_1d on a ragged matrix; the pivots must be 1-based,
+ * in range, and P A = L U must hold */
+static void test_dgetrf(dplasma_context_t *ctx) {
+  const int n = 700, nb = 256, nrhs = 5;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, n, n), *B = dmat(ctx, dplasmaRealDouble, nb, n, nrhs);
+  dplasma_desc_t *IP = dplasma_desc_ipiv(ctx, 1, nb, 1, n, 1, 1);
+  CHECK(IP != NULL, "desc_ipiv: %s", dplasma_last_error());
+  double *a = malloc(sizeof(double) * n * n), *lu = malloc(sizeof(double) * n * n);
+  double *b = malloc(sizeof(double) * n * nrhs), *x = malloc(sizeof(double) * n * nrhs);
+  int *ipiv = malloc(sizeof(int) * n);
+  unsigned sd = 31;
+  rnd_fill(a, (size_t)n * n, &sd), rnd_fill(b, (size_t)n * nrhs, &sd);
+  for (int t = 0; t < 3; ++t) {
+    const int trans = t == 1 ? dplasmaTrans : dplasmaNoTrans;
+    dplasma_desc_set_lapack(A, a, n);
+    dplasma_desc_set_lapack(B, b, n);
+    int info;
+    if (t < 2) {
+      info = dplasma_dgetrf_1d(ctx, A, IP);
+      CHECK(info == 0, "dgetrf_1d info %d (%s)", info, dplasma_last_error());
+      CHECK(dplasma_dgetrs(ctx, trans, A, IP, B) == 0, "dgetrs: %s", dplasma_last_error());
+    } else {
+      info = dplasma_dgesv_1d(ctx, A, IP, B);
+      CHECK(info == 0, "dgesv_1d info %d (%s)", info, dplasma_last_error());
+    }
+    dplasma_desc_get_lapack(B, x, n);
+    dplasma_desc_get_lapack(IP, ipiv, 1);
+    int bad = 0;
+    for (int i = 0; i < n; ++i) bad += ipiv[i] < i + 1 || ipiv[i] > n;
+    CHECK(bad == 0, "ipiv out of range (%d)", bad);
+    double err = 0, bn = 0;
+    for (int c = 0; c < nrhs; ++c)
+      for (int i = 0; i < n; ++i) {
+        double s = 0;
+        for (int k = 0; k < n; ++k) s += (trans == dplasmaNoTrans ? a[i + (size_t)k * n] : a[k + (size_t)i * n]) * x[k + (size_t)c * n];
+        err = fmax(err, fabs(s - b[i + (size_t)c * n]));
+        bn = fmax(bn, fabs(b[i + (size_t)c * n]));
+      }
+    printf("%s n=%d nb=%d ||op(A)x-b||/||b|| %.3e\n", t == 2 ? "dgesv_1d" : trans == dplasmaNoTrans ? "dgetrs N" : "dgetrs T",
+           n, nb, err / bn);
+    CHECK(err / bn < 1e-9, "getrf/getrs residual %.3e", err / bn);
+  }
+  free(a), free(lu), free(b), free(x), free(ipiv);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(B), dplasma_desc_destroy(IP);
+}
+
 int main(int argc, char **argv) {
   setvbuf(stdout, NULL, _IONBF, 0);
   signal(SIGSEGV, on_fault);
@@ -464,6 +619,12 @@ int main(int argc, char **argv) {
   test_maps(ctx);
   test_norms(ctx);
   test_taskpools(ctx);
+  test_dtrmm(ctx, dplasmaLeft, dplasmaLower, dplasmaNoTrans, dplasmaNonUnit);
+  test_dtrmm(ctx, dplasmaLeft, dplasmaUpper, dplasmaTrans, dplasmaUnit);
+  test_dtrmm(ctx, dplasmaRight, dplasmaUpper, dplasmaNoTrans, dplasmaUnit);
+  test_dtrmm(ctx, dplasmaRight, dplasmaLower, dplasmaTrans, dplasmaNonUnit);
+  test_symm_hemm(ctx);
+  test_dgetrf(ctx);
   /* an operation without a native implementation fails cleanly */
   dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
   CHECK(dplasma_dgeqrf(ctx, A, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");

@@ -126,5 +126,24 @@ def test_capi_native_gpu(tmp_path):
     env = dict(os.environ)
     env.pop("PYTHONPATH", None)
     r = subprocess.run([_build_native(tmp_path)], capture_output=True, text=True, timeout=300, env=env)
+    print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "native C ABI: all passed" in r.stdout
+
+
+@pytest.mark.gpu
+def test_capi_f77_native_gpu(tmp_path):
+    """ScaLAPACK F77 entry points without Python (one process, 1 x 1 BLACS grid -> the native engine):
+    pdpotrf_ / pdgemm_ / pdgetrf_ / pdtrsm_ / pdtrmm_ on submatrices of host local arrays
+    (reference src/scalapack_wrappers/dplasma_wrapper_pdpotrf.c:133-291)."""
+    _build(tmp_path)
+    exe = str(tmp_path / "test_f77_native")
+    subprocess.run(["gcc", "-O2", "-o", exe, os.path.join(ROOT, "tests", "capi", "test_f77_native.c"),
+                    "-I" + os.path.join(ROOT, "capi", "include"), "-L" + LIB, "-ldplasma", "-lm",
+                    "-Wl,-rpath," + LIB], check=True)
+    env = dict(os.environ)
+    env.pop("PYTHONPATH", None)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    print(r.stdout)
+    assert r.returncode == 0 and "F77 NATIVE OK" in r.stdout, r.stdout + r.stderr

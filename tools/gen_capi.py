@@ -89,6 +89,14 @@ NATIVE = {
     "lascal": "uplo, &alpha, A",
     "lange": "ntype, A",
     "lantr": "ntype, uplo, diag, A",
+    "trmm": "side, uplo, trans, diag, &alpha, A, B",
+    "symm": "side, uplo, &alpha, A, B, &beta, C",
+    "hemm": "side, uplo, &alpha, A, B, &beta, C",
+    "lansy": "ntype, uplo, A",
+    "lanhe": "ntype, uplo, A",
+    "getrf_1d": "A, IPIV",
+    "getrs": "trans, A, IPIV, B",
+    "gesv_1d": "A, IPIV, B",
 }
 
 
