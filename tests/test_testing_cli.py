@@ -46,6 +46,8 @@ def _run(args, nproc=1):
     "dpivgen -M 400 -N 200 -t 20",
     # PTG -> DTD re-execution of the tile-DAG algorithms (the reference's --mca mca_pins ptg_to_dtd)
     "dgetrf_incpiv -N 150 -t 32 -i 8 -x --ptg-to-dtd", "zgelqf -M 100 -N 150 -t 25 -i 5 -x --ptg-to-dtd",
+    # several runs: the operands are restored before every run (the reference re-generates them)
+    "dpotrf -N 300 -t 64 -x --nruns 3", "dgetrf_1d -N 200 -t 32 -x --nruns 2", "dgeqrf -M 150 -N 100 -t 32 -i 8 -x --nruns 2",
 ])
 def test_cli_single(args):
     r = _run(args.split())
