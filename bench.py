@@ -89,19 +89,22 @@ def main():
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
     if world > 1:
+        import datetime
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         local = int(os.environ.get("LOCAL_RANK", "0"))
+        # a hung exchange ends the run (non-zero exit) instead of blocking until the driver's limit
+        pg_timeout = datetime.timedelta(seconds=int(os.environ.get("DPLASMA_PG_TIMEOUT", "300")))
         if args.cpu:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=pg_timeout)
         elif os.environ.get("DPLASMA_DIST_BACKEND") == "gloo":
             # rehearsal of the multi-rank GPU path on fewer GPUs than ranks (gloo moves GPU tensors
             # through the host); ranks share devices round-robin
             local %= torch.cuda.device_count()
             torch.cuda.set_device(local)
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=pg_timeout)
         else:
             torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=pg_timeout)
     import dplasma_amd as dp
 
     P = args.P
