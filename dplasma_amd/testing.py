@@ -44,8 +44,9 @@ def _parse(argv):
     ap.add_argument("--qr_a", type=int, default=-1)
     ap.add_argument("--qr_p", type=int, default=-1)
     ap.add_argument("--treel", type=int, default=1)
-    ap.add_argument("--treeh", type=int, default=0)
-    ap.add_argument("-d", "--domino", action="store_true")
+    ap.add_argument("--treeh", type=int, default=-1, help="high-level tree (-1: flat, fibonacci when nt < mt/2)")
+    ap.add_argument("-d", "--domino", type=int, nargs="?", const=1, default=-1,
+                    help="domino coupling of the two trees (-1: on when nt < mt/2, as the reference)")
     ap.add_argument("-r", "--tsrr", action="store_true")
     ap.add_argument("-a", "--alpha", type=float, default=1.0)
     ap.add_argument("-u", "--uplo", default="L")
@@ -287,7 +288,7 @@ def _qr_common(h, lq, tree_kind, dtd=None):
     trans = dp.dplasmaConjTrans if lq else dp.dplasmaNoTrans
     tree = None
     if tree_kind == "hqr":
-        tree = dp.hqr_init(trans, A, a.treel, a.treeh, a.qr_a if a.qr_a > 0 else 1,
+        tree = dp.hqr_init(trans, A, a.treel, a.treeh, a.qr_a,
                            a.qr_p if a.qr_p > 0 else ctx.P, a.domino, a.tsrr)
     elif tree_kind == "systolic":
         tree = dp.systolic_init(trans, A, a.qr_p if a.qr_p > 0 else ctx.P, a.qr_a if a.qr_a > 0 else 1)
@@ -468,7 +469,7 @@ def t_getrf_qrf(h):
     TS = h.mat(A.mt * ib, a.N, mb=ib, nb=A.nb, name="TS")
     TT = h.mat(A.mt * ib, a.N, mb=ib, nb=A.nb, name="TT")
     IP = dp.qrf_ipiv_descriptor(ctx, A)
-    tree = dp.hqr_init(dp.dplasmaNoTrans, A, a.treel, a.treeh, a.qr_a if a.qr_a > 0 else 1,
+    tree = dp.hqr_init(dp.dplasmaNoTrans, A, a.treel, a.treeh, a.qr_a,
                        a.qr_p if a.qr_p > 0 else ctx.P, a.domino, a.tsrr)
     lu_tab = [0] * min(A.mt, A.nt)
     h.run_tp("getrf_qrf", lambda: dp.getrf_qrf_New(ctx, tree, A, IP, TS, TT, a.criteria, a.alpha, lu_tab))
@@ -615,7 +616,7 @@ def t_unmqr(h, lq, tree_kind):
     trans_t = dp.dplasmaConjTrans if lq else dp.dplasmaNoTrans
     tree = None
     if tree_kind == "hqr":
-        tree = dp.hqr_init(trans_t, A, a.treel, a.treeh, a.qr_a if a.qr_a > 0 else 1,
+        tree = dp.hqr_init(trans_t, A, a.treel, a.treeh, a.qr_a,
                            a.qr_p if a.qr_p > 0 else ctx.P, a.domino, a.tsrr)
     elif tree_kind == "systolic":
         tree = dp.systolic_init(trans_t, A, a.qr_p if a.qr_p > 0 else ctx.P, a.qr_a if a.qr_a > 0 else 1)

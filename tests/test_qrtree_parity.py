@@ -1,93 +1,55 @@
-"""HQR elimination trees against the reference's closed-form index functions.
+"""Every QR reduction tree against the reference's own tree code.
 
-Oracle: the type / annihilator formulas of src/dplasma_hqr.c for the non-domino, non-tsrr trees --
-hqr_gettype (:299-322), hqr_currpiv (:1241-1311), the flat and binary low-level trees
-(hqr_low_flat_currpiv :327, hqr_low_binary_currpiv :389) and the flat / binary high-level trees
-(hqr_high_flat_currpiv :912, hqr_high_binary_currpiv :952) -- written out here independently of
-dplasma_amd/models/qrtree.py and compared row by row for a sweep of shapes (the reference's
-pivgen tester, tests/TestsQRPivgen.cmake, checks the same functions for consistency)."""
-import itertools
+tests/fixtures/qrtree_ref.json holds the digest of each tree of the sweep below as computed by the
+reference's dplasma_hqr.c / dplasma_systolic_qr.c compiled into an oracle
+(tools/qrtree_oracle/build.sh, oracle.c; regenerate with ``compare.py --write``).  The digest covers,
+per panel k: the GEQRT rows in getm order and, per row, gettype, currpiv and the complete nextpiv and
+prevpiv chains -- so a tree passes only if every query answers exactly what the reference answers.
+Sweep: tests/TestsQRPivgen.cmake:140-206 style -- HQR (llvl 0-4, hlvl 0-4, a in {1,2,4},
+p in {1,3,5}, domino, tsrr, M in {1,3,4,10,17,25}, N in {1,2,5,13}), the adaptive SVD tree
+(hlvl 0-4, p 1-3, cores, ratio) and the systolic tree.
+"""
+import json
+import os
+import sys
 
 import pytest
 
-from dplasma_amd.models import qrtree as q
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools", "qrtree_oracle"))
+
+import compare  # noqa: E402
+
+from dplasma_amd.models import qrtree as Q  # noqa: E402
+
+REF = json.load(open(os.path.join(ROOT, "tests", "fixtures", "qrtree_ref.json")))["trees"]
 
 
-def ref_type(k, m, a, p):
-    if m < k + p:
-        return 3
-    return 1 if (m // p) % a == 0 else 0
+def _sweep(kind):
+    return [c for c in compare.configs() if c[0] == kind and compare.key(c) in REF]
 
 
-def ref_low(kind, k, m, a, p):
-    """Domain index of the annihilator of domain-head row m (flat / binary low-level trees)."""
-    k_a = (k + p - 1 - m % p) // p // a
-    if kind == q.FLAT_TREE:
-        return k_a
-    m_pa = (m // p) // a
-    d = m_pa - k_a
-    if d == 0:
-        return 0
-    t = 1
-    while d % 2 == 0:
-        d //= 2
-        t *= 2
-    return m_pa - t
+@pytest.mark.parametrize("kind,llvl", [("hqr", l) for l in range(5)] + [("svd", None), ("sys", None)])
+def test_tree_matches_reference(kind, llvl):
+    cfgs = [c for c in _sweep(kind) if llvl is None or c[3] == llvl]
+    assert len(cfgs) > 50
+    bad = [compare.key(c) for c in cfgs if compare.digest(compare.ours(c)) != REF[compare.key(c)]]
+    assert not bad, f"{len(bad)}/{len(cfgs)} trees differ from the reference, e.g. {bad[:5]}"
 
 
-def ref_high(kind, k, m):
-    if kind == q.FLAT_TREE:
-        return k
-    d, t = m - k, 1
-    if d == 0:
-        return 0
-    while d % 2 == 0:
-        d //= 2
-        t *= 2
-    return m - t
-
-
-def ref_currpiv(llvl, hlvl, k, m, a, p):
-    rank = m % p
-    tmpk = k // (p * a)
-    ty = ref_type(k, m, a, p)
-    if ty == 0:
-        tmp = (m // p) // a
-        return k + (m - k) % p if tmp == tmpk else tmp * a * p + rank
-    if ty == 1:
-        tmp = ref_low(llvl, k, m, a, p)
-        return k + (m - k) % p if tmp == tmpk else tmp * a * p + rank
-    return ref_high(hlvl, k, m)
-
-
-@pytest.mark.parametrize("llvl,hlvl", list(itertools.product([q.FLAT_TREE, q.BINARY_TREE],
-                                                             [q.FLAT_TREE, q.BINARY_TREE])))
-def test_hqr_trees_match_reference_formulas(llvl, hlvl):
-    n = 0
-    for mt, nt, a, p in itertools.product([1, 5, 12, 23], [1, 4, 23], [1, 2, 3, 5], [1, 2, 3, 4]):
-        t = q.HQRTree(mt, nt, llvl, hlvl, a, p)
-        t.check()
-        for k in range(min(mt, nt)):
-            for m in range(k + 1, mt):
-                ty = ref_type(k, m, q.HQRTree(mt, nt, llvl, hlvl, a, p).a, p)
-                aa = t.a
-                assert t.gettype(k, m) == ty, (mt, nt, a, p, k, m)
-                assert t.currpiv(k, m) == ref_currpiv(llvl, hlvl, k, m, aa, p), (mt, nt, a, p, k, m, t.kills(k))
-                n += 1
-    assert n > 1000
-
-
-@pytest.mark.parametrize("llvl", [q.FLAT_TREE, q.GREEDY_TREE, q.FIBONACCI_TREE, q.BINARY_TREE, q.GREEDY1P_TREE])
-@pytest.mark.parametrize("hlvl", [q.FLAT_TREE, q.GREEDY_TREE, q.FIBONACCI_TREE, q.BINARY_TREE])
-def test_hqr_every_tree_valid(llvl, hlvl):
-    """Every tree combination is a valid elimination plan (dplasma_qrtree_check) whose TS domains
-    are the globally aligned groups of a local rows and whose pivots sit above their victims."""
-    for mt, nt, a, p in itertools.product([3, 11, 30], [2, 11, 30], [1, 2, 4], [1, 2, 3]):
-        t = q.HQRTree(mt, nt, llvl, hlvl, a, p)
-        t.check()
-        for k in range(min(mt, nt)):
-            for (pv, m, ty) in t.kills(k):
-                assert pv < m
-                if ty == q.KILLED_BY_TS:
-                    assert pv % p == m % p          # TS kills stay inside a process row
-                    assert (m // p) // t.a == (pv // p) // t.a or pv < k + p
+@pytest.mark.parametrize("cfg", ["hqr 25 13 4 2 2 3 1 1", "hqr 17 5 1 3 4 5 0 1", "svd 25 13 0 3 2 1",
+                                 "sys 25 13 4 2"])
+def test_plans_valid(cfg):
+    """The elimination plans derived from the queries are valid programs (every row killed once,
+    after its own kills; TS only onto triangles; currpiv agrees)."""
+    c = cfg.split()
+    kind, args = c[0], list(map(int, c[1:]))
+    if kind == "hqr":
+        t = Q.HQRTree(*args)
+    elif kind == "svd":
+        t = Q.SVDTree(*args)
+    else:
+        t = Q.SystolicTree(*args)
+    t.check()
+    for k in range(min(t.mt, t.nt)):
+        assert sorted(m for _, m, _ in t.kills(k)) == list(range(k + 1, t.mt))

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--qr-a", type=int, default=0, help="HQR TS domain size in tiles (0: one domain per process row)")
     ap.add_argument("--qr-llvl", type=int, default=1, help="HQR low-level tree (0 flat, 1 greedy, 2 fibonacci, 3 binary)")
     ap.add_argument("--qr-hlvl", type=int, default=1, help="HQR high-level tree")
+    ap.add_argument("--qr-domino", type=int, default=-1, help="HQR domino (-1: reference auto)")
+    ap.add_argument("--qr-tsrr", type=int, default=0, help="HQR round-robin TS killers")
     ap.add_argument("--engine", default="panel", help="QR engine: panel (stacked domains) or tile")
     a = ap.parse_args()
     ctx = dp.init(device="cuda:0")
@@ -50,7 +52,8 @@ def main():
                 tr_ = dp.dplasmaNoTrans if a.op == "geqrf" else dp.dplasmaConjTrans
                 rows = A.mt if a.op == "geqrf" else A.nt
                 P_ = ctx.P if a.op == "geqrf" else ctx.Q
-                tree = dp.hqr_init(tr_, A, a.qr_llvl, a.qr_hlvl, a.qr_a or -(-rows // P_), P_)
+                tree = dp.hqr_init(tr_, A, a.qr_llvl, a.qr_hlvl, a.qr_a or -(-rows // P_), P_,
+                                   a.qr_domino, a.qr_tsrr)
                 tp = (dp.geqrf_param_New if a.op == "geqrf" else dp.gelqf_param_New)(ctx, tree, A, TS, TT)
         elif a.op == "getrf_nopiv":
             dp.plghe(ctx, float(N), dp.dplasmaUpperLower, A, 3872)
