@@ -148,12 +148,9 @@ class Context:
                 free.add(x * per + (x + 8 * t) % per)
         return [c for c in range(ncu) if c not in free]
 
-    def bulk_stream(self, reserve: int):
-        """A low-priority stream restricted to all CUs but ``reserve`` (see ``reserve_mask``); cached
-        per reserve.  reserve <= 0 or no GPU: the plain ``update`` stream."""
-        if reserve <= 0 or not self.is_gpu:
-            return "update"
-        name = f"bulk{reserve}"
+    def masked_stream(self, name: str, cus) -> str:
+        """A HIP stream restricted to the CU indices ``cus`` (hipExtStreamCreateWithCUMask), registered
+        as ``name`` and cached; destroyed by ``release``."""
         if name in self.streams:
             return name
         import ctypes
@@ -161,7 +158,7 @@ class Context:
         ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
         nw = (ncu + 31) // 32
         words = [0] * nw
-        for c in self.reserve_mask(ncu, reserve):
+        for c in cus:
             words[c // 32] |= 1 << (c % 32)
         arr = (ctypes.c_uint * nw)(*words)
         out = ctypes.c_void_p()
@@ -171,6 +168,29 @@ class Context:
         self._owned_streams = getattr(self, "_owned_streams", []) + [out.value]
         self._owned_names = getattr(self, "_owned_names", []) + [name]
         return name
+
+    def bulk_stream(self, reserve: int):
+        """A low-priority stream restricted to all CUs but ``reserve`` (see ``reserve_mask``); cached
+        per reserve.  reserve <= 0 or no GPU: the plain ``update`` stream."""
+        if reserve <= 0 or not self.is_gpu:
+            return "update"
+        ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+        return self.masked_stream(f"bulk{reserve}", self.reserve_mask(ncu, reserve))
+
+    def partition_streams(self, reserve: int):
+        """(tile, chain, bulk) stream names for a CU partition: ``tile`` runs on the ``reserve`` CUs kept
+        free by ``reserve_mask`` (the latency-bound diagonal-tile kernels alone on their CUs -- beside a
+        GEMM's waves on the same SIMDs they run ~7x slower, profiles/r3_potrf_tile_cu_partition.txt),
+        ``chain`` and ``bulk`` on the other CUs (the panel solves / look-ahead updates and the trailing
+        update).  reserve <= 0 or no GPU: ("panel", "panel", "update")."""
+        if reserve <= 0 or not self.is_gpu:
+            return "panel", "panel", "update"
+        ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+        keep = self.reserve_mask(ncu, reserve)
+        ks = set(keep)
+        tile = self.masked_stream(f"tile{reserve}", [c for c in range(ncu) if c not in ks])
+        chain = self.masked_stream(f"chain{reserve}", keep)
+        return tile, chain, self.bulk_stream(reserve)
 
     def release(self):
         """Destroy the HIP streams this context created itself (CU-masked ones)."""

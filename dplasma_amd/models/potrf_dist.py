@@ -46,6 +46,7 @@ from ..utils.flops import flops
 DIST_DEFER = 2
 DIST_LOOKAHEAD = 2
 DIST_BULK_RESERVE = 0
+DIST_TILE_CUS = 0   # CUs kept for the diagonal-tile kernels (Context.partition_streams); 0 = no partition
 DIST_CHUNK = 0      # D = 1: tiles per pipelined chunk (potrf_pipelined_New); 0 = whole-piece schedule (replay: chunking
 #                   loses, 285 vs 241 ms at chunk 8 -- profiles/r3_replay_pipelined_chunks.txt)
 
@@ -73,7 +74,16 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
         raise ValueError("DPLASMA_POTRF_LOOKAHEAD must be 1 or 2")
     nslab = 1 + la
     reserve = int(env.get("DPLASMA_POTRF_BULK_RESERVE", DIST_BULK_RESERVE))
-    upd_stream = ctx.bulk_stream(reserve) if ctx.is_gpu else "update"
+    tile_cus = int(env.get("DPLASMA_POTRF_TILE_CUS", DIST_TILE_CUS))
+    if tile_cus > 0 and ctx.is_gpu:
+        # the diagonal tile (and a receiver's (M, S) preparation) on their own CUs, everything else on
+        # the rest: the latency-bound tile kernels never share a SIMD with GEMM waves
+        s_tile, s_chain, upd_stream = ctx.partition_streams(tile_cus)
+        # a CU-masked stream has no priority: by default the chain keeps the high-priority panel stream
+        s_pan = s_chain if env.get("DPLASMA_POTRF_CHAIN_MASKED", "0") == "1" else "panel"
+    else:
+        s_tile = s_pan = "panel"
+        upd_stream = ctx.bulk_stream(reserve) if ctx.is_gpu else "update"
     chunk = int(env.get("DPLASMA_POTRF_CHUNK", DIST_CHUNK))
     if D == 1 and chunk > 0:
         return potrf_pipelined_New(ctx, uplo, A, info_out, chunk)
@@ -205,7 +215,7 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                         ops.potrf_tile(uplo, A.data, off, kb, A.ld, info, k * A.mb, zbuf=zk)
                     else:
                         ops.potrf_tile(uplo, A.data, off, kb, A.ld, info, k * A.mb)
-                t_potrf = tp.task(f"POTRF({k})", "panel", f_potrf, [gate], prio=3, comm=False)
+                t_potrf = tp.task(f"POTRF({k})", s_tile, f_potrf, [gate], prio=3, comm=False)
             # ---------------- diagonal triangle to the other roots of the panel column
             tri_src = None
             if in_pc and mine and not own_diag:
@@ -230,7 +240,7 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                         buf[: kb * (kb + 1) // 2].copy_(A.data.view(-1)[off + comm._tri_index(kb, A.ld, lower, dev)])
                         h = comm.start_p2p(sends=[(buf, d) for d in dests], group=urgent_g)
                         dsend_pend[par2] = h
-                    tp.task(f"DSEND({k})", "panel", f_dsend, [t_potrf], prio=3)
+                    tp.task(f"DSEND({k})", s_tile, f_dsend, [t_potrf], prio=3)
             # ---------------- TRSM of my tiles of panel k
             t_trsm = None
             if mine:
@@ -249,13 +259,19 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                 if use_rb:
                     rbp = ops.RbPanel(uplo, [(A.offset(*tcoord(i, k)), A.tile_rows(i) if lower else A.tile_cols(i))
                                              for i in mine], A.ld)
-
-                    def f_trsm(rbp=rbp, tb_=tri_base, tl=tri_ld, to=tri_off, kb=kb, zk=zk, pre=pre, recv=bool(pre)):
-                        for f, _ in pre:
-                            f()
-                        if recv:
+                    prep = []
+                    if pre:
+                        # a receiver prepares (M, S) of the received triangle on the tile CUs
+                        def f_prep(tb_=tri_base, tl=tri_ld, to=tri_off, kb=kb, zk=zk, pre=pre):
+                            for f, _ in pre:
+                                f()
                             ops.trsm_rb_prep(uplo, kb, tb_, to, tl, zk)
+                        prep = [tp.task(f"PREP({k})", s_tile, f_prep, [gate] + [t for _, t in pre], prio=3,
+                                        comm=False)]
+
+                    def f_trsm(rbp=rbp, tb_=tri_base, tl=tri_ld, to=tri_off, kb=kb, zk=zk):
                         ops.trsm_rb(uplo, kb, tb_, to, tl, zk, rbp, A.data, A.ld)
+                    deps = [t_potrf, gate] + prep
                 else:
                     tb = TileBatch()
                     for i in mine:
@@ -268,8 +284,8 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                         for f, _ in pre:
                             f()
                         ops.trsm(side, uplo, dplasmaConjTrans, dplasmaNonUnit, 1.0, tb_, tl, A.data, A.ld, tb)
-                deps = [t_potrf, gate] + [t for _, t in pre]
-                t_trsm = tp.task(f"TRSM({k})", "panel", f_trsm, deps, prio=2, comm=False)
+                    deps = [t_potrf, gate] + [t for _, t in pre]
+                t_trsm = tp.task(f"TRSM({k})", s_pan, f_trsm, deps, prio=2, comm=False)
                 last_trsm[k] = t_trsm
             if k == nt - 1:
                 break
@@ -343,7 +359,7 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                 pend[k] = {**pend.get(k, {}), **hs}
             # a root issues after its TRSM (panel stream); a pure receiver on the comm stream, as soon
             # as the slab is free
-            stream = "panel" if mine else "comm"
+            stream = s_pan if mine else "comm"
             t_x = tp.task(f"XFER({k})", stream, f_xfer, [t_trsm, *guard], prio=2)
             last_panel = t_x
 
@@ -359,7 +375,7 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                 def f_near(bt=near, k=k):
                     wait_panels([k])
                     f_upd(bt, GX, A.mb)
-                gate = tp.task(f"NEAR({k})", "panel", f_near, [t_x, gate], prio=2, comm=False)
+                gate = tp.task(f"NEAR({k})", s_pan, f_near, [t_x, gate], prio=2, comm=False)
                 slot_readers.setdefault(slot, []).append(gate)
             else:
                 gate = t_x if t_x is not None else gate
@@ -397,7 +413,7 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
             def f_next(bt=nxt, ks=ks):
                 wait_panels(ks)
                 f_upd(bt, GX, A.mb)
-            t_next = tp.task(f"NEXT({b})", "panel", f_next,
+            t_next = tp.task(f"NEXT({b})", s_pan, f_next,
                              [gate, last_panel, nxt2_of.get(b - 1), rest_of.get(b - 2)], prio=2, comm=False)
         prev_bulk = rest_of.get(b - 1)
         if len(nxt2):

@@ -1,8 +1,9 @@
 """Phase timeline of the dataflow diagonal-tile Cholesky (potrf_rb.hip) from its in-kernel
 s_memrealtime stamps (100 MHz): per step k, the Z_k hand-off to WG k+1 and WG k+1's TRSM / SYRK /
-factorisation, i.e. the kernel's critical path.  Alone, and beside an 8192^3 GEMM.
+factorisation, i.e. the kernel's critical path.  Alone, beside an 8192^3 GEMM, and beside the GEMM
+restricted to all CUs but R (R = 16, 32: 2 / 4 per XCD) with the tile kernel on the R reserved CUs.
 
-  python tools/gpu/potrf_rb_trace.py [n]
+  python tools/gpu/potrf_rb_trace.py [n] [R ...]
 """
 import sys
 from pathlib import Path
@@ -14,6 +15,7 @@ from dplasma_amd.constants import dplasmaLower, dplasmaNoTrans  # noqa: E402
 from dplasma_amd.ops import _lib  # noqa: E402
 from dplasma_amd.ops import tile_ops as ops  # noqa: E402
 from dplasma_amd.ops.batch import GemmBatch  # noqa: E402
+from dplasma_amd.context import Context  # noqa: E402
 
 
 def show(tr, nblk, tag):
@@ -33,6 +35,18 @@ def show(tr, nblk, tag):
     print("last WG per-step (poll, trsm, upd):",
           " ".join(f"{float(t[last, 1 + 3 * k]):.0f}/{float(t[last, 2 + 3 * k] - t[last, 1 + 3 * k]):.1f}/"
                    f"{float(t[last, 3 + 3 * k] - t[last, 2 + 3 * k]):.1f}" for k in range(last)))
+
+
+def masked(lib, ncu, cus):
+    import ctypes
+    nw = (ncu + 31) // 32
+    words = [0] * nw
+    for c in cus:
+        words[c // 32] |= 1 << (c % 32)
+    arr = (ctypes.c_uint * nw)(*words)
+    out = ctypes.c_void_p()
+    _lib.check(lib.dpl_stream_cumask(ctypes.cast(arr, ctypes.c_void_p), nw, ctypes.byref(out)), "stream_cumask")
+    return torch.cuda.ExternalStream(out.value)
 
 
 def main():
@@ -55,7 +69,15 @@ def main():
     gb.finalize()
     lo = torch.cuda.Stream(priority=0)
     hi = torch.cuda.Stream(priority=-1)
-    for beside in (False, True):
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    modes = [(False, None, None, "alone"), (True, lo, hi, "beside GEMM")]
+    for R in [int(a) for a in sys.argv[2:]] or [16, 32]:
+        keep = Context.reserve_mask(ncu, R)
+        rsv = [c for c in range(ncu) if c not in set(keep)]
+        modes.append((True, masked(lib, ncu, keep), masked(lib, ncu, rsv),
+                      f"beside GEMM on {len(keep)} CUs, tile on the other {len(rsv)}"))
+        modes.append((True, masked(lib, ncu, keep), hi, f"beside GEMM on {len(keep)} CUs, tile unmasked"))
+    for beside, lo, hi, tag in modes:
         for rep in range(4):
             view.copy_(S)
             torch.cuda.synchronize()
@@ -69,7 +91,7 @@ def main():
                 ops.potrf_tile(dplasmaLower, buf, 0, n, lda, info, 0)
                 lib.dpl_potrf_rb_set_trace(None)
             torch.cuda.synchronize()
-        show(tr.cpu(), nblk, "beside GEMM" if beside else "alone")
+        show(tr.cpu(), nblk, tag)
 
 
 if __name__ == "__main__":

@@ -54,6 +54,7 @@ class ReplayBackend:
             lo, hi = torch.cuda.Stream.priority_range()
             self.hi = hi
             self.remote = torch.cuda.Stream(device=dev, priority=hi)
+            self.remote_potrf = self.remote_trsm = self.remote   # CU-partitioned runs: the rank's own streams
             self.lib = _lib.load()
         self.stats = {"batches": 0, "bytes": 0, "us": 0.0, "proxy_potrf": 0, "proxy_trsm": 0}
         self._scratch = {}
@@ -107,14 +108,15 @@ class ReplayBackend:
         for t, p in list(sends) + list(recvs):
             per_peer[p] = per_peer.get(p, 0) + t.numel() * t.element_size()
         if self.proxies and recvs and not sends and hint is not None:
-            self.remote.wait_event(ev)
-            with torch.cuda.stream(self.remote):
+            rs = self.remote_potrf if hint[0] == "potrf" else self.remote_trsm
+            rs.wait_event(ev)
+            with torch.cuda.stream(rs):
                 if hint[0] == "potrf":
                     self._potrf_proxy(hint[1])
                 elif hint[0] == "trsm":
                     self._trsm_proxy(hint[1], hint[2])
             ev = torch.cuda.Event()
-            ev.record(self.remote)
+            ev.record(rs)
         gs.wait_event(ev)
         us = self.lat + max(per_peer.values()) / self.bw
         _lib.check(self.lib.dpl_delay(float(us), self.nwg, gs.cuda_stream), "delay")
@@ -189,6 +191,11 @@ def main():
     base = dp.init(device="cuda:0")
     be = ReplayBackend(base.device, args.bw, args.lat, args.comm_wg, proxies=not args.no_proxy)
     comm.set_backend(be)
+    tile_cus = int(os.environ.get("DPLASMA_POTRF_TILE_CUS", "0"))
+    if tile_cus > 0:
+        # the remote producers run their tile kernels on their own partition, as this rank does
+        s_tile, s_chain, _ = base.partition_streams(tile_cus)
+        be.remote_potrf, be.remote_trsm = base.streams[s_tile], base.streams[s_chain]
     ranks = range(P * Q) if args.ranks == "all" else [int(x) for x in args.ranks.split(",")]
     fl = dp.flops_of("d", "potrf", args.N) if hasattr(dp, "flops_of") else None
     if fl is None:
