@@ -389,6 +389,98 @@ DPL_API int dpl_tile_norm(int prec, int kind, int part, int unit, int nitems, co
 // Stream restricted to a CU subset (CDNA CU masking): bit i of mask[i / 32] enables CU i.  Used to
 // give the latency-bound diagonal-tile Cholesky its own CU(s), away from the CU-saturating trailing
 // GEMM it would otherwise share SIMDs with.
+// ---------------------------------------------------------------- tile-pair swap-transpose
+// For each item: tile a (m x n at a_off) and tile b (n x m at b_off) become  a <- op(b)^T,
+// b <- op(a)^T  (op = conj when cj, i.e. conjugate transposes); a_off == b_off transposes one square
+// tile in place.  Grid (items, 32x32 sub-blocks of a): workgroup (r, c) exchanges sub-block (r, c) of
+// a with sub-block (c, r) of b through LDS (coalesced 32-wide column reads and writes on both sides;
+// row stride 33: conflict-free transposed reads).  In-place tiles: only r <= c works.
+// Used by the upper Cholesky on one process: A^T (A^H) turns the upper triangle into the lower one,
+// the lower schedule factors it, and the same exchange writes U = L^T (L^H) back while restoring the
+// untouched strictly-lower triangle.
+template <typename T>
+__global__ __launch_bounds__(256) void k_swap_transpose(const TileItem* __restrict__ items, int nbc, T* __restrict__ A,
+                                                        int ld, int cj) {
+  __shared__ T sa[32 * 33], sb[32 * 33];
+  const TileItem it = items[blockIdx.x];
+  const int r = blockIdx.y / nbc, c = blockIdx.y % nbc;
+  if (32 * r >= it.m || 32 * c >= it.n) return;
+  const bool same = it.a_off == it.b_off;
+  if (same && r > c) return;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int ra = 32 * r, ca = 32 * c;                  // sub-block origin in a; in b it is (ca, ra)
+  const int mr = min(32, it.m - ra), nc = min(32, it.n - ca);
+  T* a = A + it.a_off;
+  T* b = A + it.b_off;
+  const bool diag = same && r == c;
+  // sa(i, j) = a(ra + i, ca + j);  sb(j, i) = b(ca + j, ra + i)
+  for (int j = ty; j < 32; j += 8) {
+    if (tx < mr && j < nc) sa[j * 33 + tx] = a[(long long)(ca + j) * ld + ra + tx];
+    if (!diag && tx < nc && j < mr) sb[j * 33 + tx] = b[(long long)(ra + j) * ld + ca + tx];
+  }
+  __syncthreads();
+  const T* src_for_a = diag ? sa : sb;
+  for (int j = ty; j < 32; j += 8) {
+    // a(ra + tx, ca + j) = op(b(ca + j, ra + tx)) = op(sb[tx * 33 + j])   (diag: op(sa[tx * 33 + j]))
+    if (tx < mr && j < nc) {
+      const T v = src_for_a[tx * 33 + j];
+      a[(long long)(ca + j) * ld + ra + tx] = cj ? conj_(v) : v;
+    }
+    // b(ca + tx, ra + j) = op(a(ra + j, ca + tx)) = op(sa[tx * 33 + j])
+    if (!diag && tx < nc && j < mr) {
+      const T v = sa[tx * 33 + j];
+      b[(long long)(ra + j) * ld + ca + tx] = cj ? conj_(v) : v;
+    }
+  }
+}
+
+DPL_API int dpl_swap_transpose(int prec, int nitems, const void* items, int mmax, int nmax, void* A, int ld, int cj,
+                               hipStream_t st) {
+  if (nitems <= 0) return 0;
+  const int nbr = cdiv(mmax, 32), nbc = cdiv(nmax, 32);
+  DISPATCH(prec, hipLaunchKernelGGL((k_swap_transpose<T>), dim3(nitems, nbr * nbc), dim3(256), 0, st,
+                                    (const TileItem*)items, nbc, (T*)A, ld, cj));
+  return (int)hipGetLastError();
+}
+
+// One-way transposed tile copy: for each item, tile y (n x m at b_off in Y) <- op(tile x)^T (x: m x n at
+// a_off in X), op = conj when cj; upper_only writes only y(p, q), p <= q (a diagonal tile whose strictly
+// lower part must stay).  Same LDS-staged 32x32 sub-block scheme as k_swap_transpose, half its traffic.
+template <typename T>
+__global__ __launch_bounds__(256) void k_copy_transpose(const TileItem* __restrict__ items, int nbc,
+                                                        const T* __restrict__ X, int ldx, T* __restrict__ Y, int ldy,
+                                                        int cj, int upper_only) {
+  __shared__ T sa[32 * 33];
+  const TileItem it = items[blockIdx.x];
+  const int r = blockIdx.y / nbc, c = blockIdx.y % nbc;
+  if (32 * r >= it.m || 32 * c >= it.n) return;
+  if (upper_only && c > r) return;             // y block (c, r) lies strictly below the diagonal
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int ra = 32 * r, ca = 32 * c;
+  const int mr = min(32, it.m - ra), nc = min(32, it.n - ca);
+  const T* x = X + it.a_off;
+  T* y = Y + it.b_off;
+  for (int j = ty; j < 32; j += 8)
+    if (tx < mr && j < nc) sa[j * 33 + tx] = x[(long long)(ca + j) * ldx + ra + tx];
+  __syncthreads();
+  for (int j = ty; j < 32; j += 8) {
+    // y(ca + tx, ra + j) = op(x(ra + j, ca + tx)) = op(sa[tx * 33 + j])
+    if (tx < nc && j < mr && (!upper_only || ca + tx <= ra + j)) {
+      const T v = sa[tx * 33 + j];
+      y[(long long)(ra + j) * ldy + ca + tx] = cj ? conj_(v) : v;
+    }
+  }
+}
+
+DPL_API int dpl_copy_transpose(int prec, int nitems, const void* items, int mmax, int nmax, const void* X, int ldx,
+                               void* Y, int ldy, int cj, int upper_only, hipStream_t st) {
+  if (nitems <= 0) return 0;
+  const int nbr = cdiv(mmax, 32), nbc = cdiv(nmax, 32);
+  DISPATCH(prec, hipLaunchKernelGGL((k_copy_transpose<T>), dim3(nitems, nbr * nbc), dim3(256), 0, st,
+                                    (const TileItem*)items, nbc, (const T*)X, ldx, (T*)Y, ldy, cj, upper_only));
+  return (int)hipGetLastError();
+}
+
 DPL_API int dpl_stream_cumask(const unsigned* mask, int nwords, void** out) {
   hipStream_t s = nullptr;
   const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, mask);

@@ -99,8 +99,43 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
         # DPLASMA_POTRF_DIST=collective keeps the row-broadcast + column-all-gather schedule below
         from .potrf_dist import potrf_dist_New
         return potrf_dist_New(ctx, uplo, A, info_out)
+    # Upper on one process: factor A^T (A^H) with the lower schedule (transposed copies in and out,
+    # ops.copy_transpose, overlapped with the factorisation) instead of the upper tile kernels, whose
+    # strips are strided columns of U (16k: native upper 40.1 vs lower 46.7 TF/s,
+    # profiles/r3_potrf_upper_via_lower.txt).  DPLASMA_POTRF_UPPER=native keeps the upper kernels.
+    up_mode = os.environ.get("DPLASMA_POTRF_UPPER", "auto")
+    via_lower = uplo == dplasmaUpper and ctx.world == 1 and (up_mode == "via_lower" or (ctx.is_gpu and up_mode == "auto"))
+    if via_lower:
+        uplo = dplasmaLower
     lower = uplo == dplasmaLower
     tp = Taskpool("potrf", ctx)
+    t_in = t_in1 = None
+    if via_lower:
+        # the lower schedule factors a workspace copy W = A^T (A^H) of the upper triangle; each block of
+        # columns of W goes back into A's upper triangle once factored (A's strictly lower part is never
+        # touched).  One read + one write of the triangle each way, overlapped with the factorisation.
+        cj = A.dtype.is_complex
+        A_user = A
+        A = A_user.like(name="W")
+
+        def xpose(cols, back=False):
+            xb, db = TileBatch(), TileBatch()
+            for j in cols:
+                for i in range(j, A.mt):
+                    if back:
+                        (db if i == j else xb).add(A.offset(i, j), A.tile_rows(i), A.tile_cols(j),
+                                                   b_off=A_user.offset(j, i))
+                    else:
+                        xb.add(A_user.offset(j, i), A_user.tile_rows(j), A_user.tile_cols(i), b_off=A.offset(i, j))
+            xb.finalize()
+            db.finalize()
+            src, dst = (A, A_user) if back else (A_user, A)
+
+            def f(xb=xb, db=db):
+                ops.copy_transpose(src.data, src.ld, dst.data, dst.ld, xb, conj=cj)
+                ops.copy_transpose(src.data, src.ld, dst.data, dst.ld, db, conj=cj, upper_only=True)
+            return f
+        xposed_out = set()
     # diagonal tiles on the CU-reserved stream when DPLASMA_DIAG_CUS is set (context._reserve_cus)
     diag_stream = "diag" if "diag" in getattr(ctx, "streams", {}) else "panel"
     # the panel TRSM joins the diagonal tile on the CU-reserved stream (DPLASMA_POTRF_DIAG_TRSM=0: on
@@ -239,7 +274,13 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
         with ops.gemm_wg_cap(bulk_cap):
             f_upd(batch, base, ld)
 
-    gate = None        # task the next POTRF must follow (NEAR(k-1) or NEXT(b-1))
+    if via_lower:
+        # the first block's columns on the critical stream, the rest beside its panels (bulk stream);
+        # each block's columns go back as soon as its last reader is done (TRANSPOSE_OUT(b) below)
+        t_in = tp.task("TRANSPOSE_IN(0)", "panel", xpose(range(blocks[0][0], blocks[0][1])), [], prio=3, comm=False)
+        if blocks[0][1] < nt:
+            t_in1 = tp.task("TRANSPOSE_IN(1)", upd_stream, xpose(range(blocks[0][1], nt)), [], prio=1, comm=False)
+    gate = t_in        # task the next POTRF must follow (NEAR(k-1) or NEXT(b-1))
     last_upd = {}      # block -> last update-stream task reading its panels
     nxt2_of, rest_of = {}, {}   # look-ahead 2: block -> NEXT2 / REST2 task (REST2: last bulk task)
     last_panel = None  # last panel-stream communication task
@@ -415,6 +456,10 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
             if len(rest):
                 last_upd[b] = tp.task(f"REST({b})", upd_stream, lambda bt=rest, bs=base, l=ld: f_bulk(bt, bs, l),
                                       deps, prio=1)
+            if via_lower:
+                tp.task(f"TRANSPOSE_OUT({b})", upd_stream, xpose(range(c0, c1), back=True),
+                        [t_next, last_upd.get(b), gate, t_in1 if b == 0 else None], prio=0, comm=False)
+                xposed_out.update(range(c0, c1))
             # the next block's first POTRF follows NEXT(b) (and, for this rank, the block's NEARs)
             gate = t_next if t_next is not None else gate
             continue
@@ -440,7 +485,35 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
         else:
             rest_of[b] = nxt2_of.get(b, prev_bulk)
         last_upd[b] = rest_of[b] if rest_of[b] is not None else t_next
+        if via_lower:
+            tp.task(f"TRANSPOSE_OUT({b})", upd_stream, xpose(range(c0, c1), back=True),
+                    [t_next, nxt2_of.get(b), rest_of.get(b), gate, t_in1 if b == 0 else None], prio=0, comm=False)
+            xposed_out.update(range(c0, c1))
         gate = t_next if t_next is not None else gate
+
+    if via_lower:
+        # every root task follows TRANSPOSE_IN(0), the first block's trailing updates TRANSPOSE_IN(1);
+        # the columns not yet transposed back go after every task without a successor
+        for t in tp.tasks:
+            if t.tid in (t_in, t_in1):
+                continue
+            extra = []
+            if not t.deps:
+                extra.append(t_in)
+            if t_in1 is not None and t.name in ("NEXT(0)", "REST(0)", "NEXT2(0)", "REST2(0)"):
+                extra.append(t_in1)
+            for d in extra:
+                if d not in t.deps:
+                    t.deps.append(d)
+                    if tp.tasks[d].stream != t.stream:
+                        tp.tasks[d].needs_event = True
+        has_succ = set()
+        for t in tp.tasks:
+            has_succ.update(t.deps)
+        sinks = [t.tid for t in tp.tasks if t.tid not in has_succ]
+        left = [j for j in range(nt) if j not in xposed_out]
+        if left:
+            tp.task("TRANSPOSE_OUT(end)", "panel", xpose(left, back=True), sinks, prio=0, comm=False)
 
     def _done():
         v = info.clone()

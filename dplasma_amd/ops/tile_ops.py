@@ -519,6 +519,56 @@ def geadd(uplo: int, trans: int, alpha, A: torch.Tensor, lda: int, beta, B: torc
         b.copy_(torch.where(_part_mask(it, m, n, part), new, b))
 
 
+def swap_transpose(A: torch.Tensor, ld: int, batch: TileBatch, conj: bool = False):
+    """Per item: tile a (m x n at a_off) <- op(tile b)^T and tile b (n x m at b_off) <- op(tile a)^T,
+    op = conj if ``conj``; a_off == b_off transposes a square tile in place (csrc/kernels/aux.hip)."""
+    batch.finalize()
+    if len(batch) == 0:
+        return
+    if _is_gpu(A):
+        rc = _lib.load().dpl_swap_transpose(_lib.prec_code(A.dtype), len(batch.items),
+                                            batch.device_array(A.device).data_ptr(), batch.max_m, batch.max_n,
+                                            A.data_ptr(), ld, int(conj), _lib.stream_ptr())
+        _lib.check(rc, "swap_transpose")
+        return
+    for it in batch.items:
+        m, n = int(it["m"]), int(it["n"])
+        a = _view(A, it["a_off"], m, n, ld)
+        b = _view(A, it["b_off"], n, m, ld)
+        na, nb = b.t().clone(), a.t().clone()
+        if conj:
+            na, nb = na.conj(), nb.conj()
+        a.copy_(na)
+        if int(it["a_off"]) != int(it["b_off"]):
+            b.copy_(nb)
+
+
+def copy_transpose(X: torch.Tensor, ldx: int, Y: torch.Tensor, ldy: int, batch: TileBatch, conj: bool = False,
+                   upper_only: bool = False):
+    """Per item: tile y (n x m at b_off in Y) <- op(tile x)^T (x: m x n at a_off in X), op = conj if
+    ``conj``; ``upper_only`` leaves y's strictly lower part alone (csrc/kernels/aux.hip)."""
+    batch.finalize()
+    if len(batch) == 0:
+        return
+    if _is_gpu(Y):
+        rc = _lib.load().dpl_copy_transpose(_lib.prec_code(Y.dtype), len(batch.items),
+                                            batch.device_array(Y.device).data_ptr(), batch.max_m, batch.max_n,
+                                            X.data_ptr(), ldx, Y.data_ptr(), ldy, int(conj), int(upper_only),
+                                            _lib.stream_ptr())
+        _lib.check(rc, "copy_transpose")
+        return
+    for it in batch.items:
+        m, n = int(it["m"]), int(it["n"])
+        x = _view(X, it["a_off"], m, n, ldx).t()
+        if conj:
+            x = x.conj()
+        y = _view(Y, it["b_off"], n, m, ldy)
+        if upper_only:
+            y.copy_(torch.where(torch.ones(n, m, dtype=torch.bool, device=y.device).triu(), x, y))
+        else:
+            y.copy_(x)
+
+
 def lascal(uplo: int, alpha, A: torch.Tensor, lda: int, batch: TileBatch):
     batch.finalize()
     if len(batch) == 0:

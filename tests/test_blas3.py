@@ -164,3 +164,25 @@ def test_trtri_lauum(ctx, uplo, diag):
     ref = t3.conj().T @ t3 if uplo == 122 else t3 @ t3.conj().T
     sel2 = (lambda x: x.tril()) if uplo == 122 else (lambda x: x.triu())
     assert rel_err(sel2(A3.to_dense_local()), sel2(ref)) < 1e-12
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.complex128])
+def test_potrf_upper_via_lower(monkeypatch, dtype):
+    """Upper Cholesky through the transposed lower schedule (one process): same factor as the native
+    upper schedule, strictly-lower triangle untouched."""
+    import dplasma_amd as dp
+    ctx = dp.init(device="cpu")
+    N, NB = 300, 64
+    A = dp.block_cyclic(ctx, dtype, NB, NB, N, N)
+    dp.plghe(ctx, float(N), dp.dplasmaUpperLower, A, 51)
+    dense0 = A.to_dense_local().clone()
+    B = A.like()
+    dp.lacpy(ctx, dp.dplasmaUpperLower, A, B)
+    potrf = dp.zpotrf if dtype.is_complex else dp.dpotrf
+    monkeypatch.setenv("DPLASMA_POTRF_UPPER", "via_lower")
+    assert potrf(ctx, dp.dplasmaUpper, A) == 0
+    monkeypatch.setenv("DPLASMA_POTRF_UPPER", "native")
+    assert potrf(ctx, dp.dplasmaUpper, B) == 0
+    a, b = A.to_dense_local(), B.to_dense_local()
+    assert torch.allclose(torch.triu(a), torch.triu(b), atol=1e-10, rtol=1e-10)
+    assert torch.equal(torch.tril(a, -1), torch.tril(dense0, -1))

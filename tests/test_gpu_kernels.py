@@ -406,3 +406,57 @@ def test_gemm_full_capped_grid(gctx, prec, ta, tb, cap):
     assert _lib.load().dpl_gemm_set_wg_cap(0) == 0      # the context manager restored "uncapped"
     torch.cuda.synchronize()
     assert torch.equal(C, ref)
+
+
+@pytest.mark.parametrize("prec", list("sdcz"))
+@pytest.mark.parametrize("storage", [dp.STORAGE_TILE, dp.STORAGE_LAPACK])
+def test_swap_transpose(gctx, cctx, prec, storage):
+    """ops.swap_transpose (HIP) vs the CPU reference: ragged tiles, in-place diagonal tiles, conj."""
+    from dplasma_amd.ops import tile_ops
+    from dplasma_amd.ops.batch import TileBatch
+    dt = DTYPES[prec]
+    G, C = _pair(gctx, cctx, dt, 96, 96, 333, 333, storage=storage)
+    dp.plrnt(gctx, G, 7)
+    dp.plrnt(cctx, C, 7)
+    for M in (G, C):
+        xb = TileBatch()
+        for j in range(M.nt):
+            for i in range(j, M.mt):
+                xb.add(M.offset(i, j), M.tile_rows(i), M.tile_cols(j), b_off=M.offset(j, i))
+        tile_ops.swap_transpose(M.data, M.ld, xb, conj=dt.is_complex)
+    g, c = G.to_dense_local().cpu(), C.to_dense_local()
+    assert torch.equal(g, c)
+    d0 = dp.block_cyclic(cctx, dt, 96, 96, 333, 333, storage=storage)
+    dp.plrnt(cctx, d0, 7)
+    ref = d0.to_dense_local().t()
+    assert torch.equal(c, ref.conj() if dt.is_complex else ref)
+    # one-way copy: Y's upper tiles <- op(X's lower tiles)^T, diagonal tiles upper part only
+    X, Y = _pair(gctx, cctx, dt, 96, 96, 333, 333, storage=storage)[0], G
+    dp.plrnt(gctx, X, 9)
+    y0 = Y.to_dense_local().clone()
+    xb, db = TileBatch(), TileBatch()
+    for j in range(X.nt):
+        for i in range(j, X.mt):
+            (db if i == j else xb).add(X.offset(i, j), X.tile_rows(i), X.tile_cols(j), b_off=Y.offset(j, i))
+    tile_ops.copy_transpose(X.data, X.ld, Y.data, Y.ld, xb, conj=dt.is_complex)
+    tile_ops.copy_transpose(X.data, X.ld, Y.data, Y.ld, db, conj=dt.is_complex, upper_only=True)
+    xt = X.to_dense_local().t()
+    xt = xt.conj() if dt.is_complex else xt
+    y = Y.to_dense_local()
+    assert torch.equal(torch.triu(y), torch.triu(xt)) and torch.equal(torch.tril(y, -1), torch.tril(y0, -1))
+
+
+@pytest.mark.parametrize("dims", [(378, 93), (2048, 512)])
+def test_potrf_upper_via_lower_gpu(gctx, dims, monkeypatch):
+    """Upper DPOTRF on one GPU runs the transposed lower schedule: residual and untouched lower part."""
+    N, NB = dims
+    monkeypatch.setenv("DPLASMA_POTRF_UPPER", "auto")
+    A = dp.block_cyclic(gctx, torch.float64, NB, NB, N, N)
+    dp.plghe(gctx, float(N), dp.dplasmaUpperLower, A, 3872)
+    A0 = A.like()
+    dp.lacpy(gctx, dp.dplasmaUpperLower, A, A0)
+    low0 = torch.tril(A0.to_dense_local(), -1).cpu()
+    assert dp.dpotrf(gctx, dp.dplasmaUpper, A) == 0
+    ok, res = dp.check_potrf(gctx, dp.dplasmaUpper, A, A0)
+    assert ok, res
+    assert torch.equal(torch.tril(A.to_dense_local(), -1).cpu(), low0)
