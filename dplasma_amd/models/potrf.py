@@ -250,11 +250,13 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
 
     def add_update(batch, ks, ncols):
         """Trailing tiles (m, n), n in ncols, m >= n (lower), updated by the panels ks."""
+        batch.rec = []    # (trailing tile, panel tile rows, panels) for the recursive incarnation
         for n_ in ncols:
             for m_ in range(n_, nt):
                 cc = (m_, n_) if lower else (n_, m_)
                 if not A.is_local(*cc):
                     continue
+                batch.rec.append((cc, m_, n_, list(ks)))
                 # lower: C(m,n) -= L(m,k) L(n,k)^H ; upper: C(n,m) -= U(k,n)^H U(k,m)
                 kp = [(panels[k].off(cc[0]), panels[k].off(cc[1]), A.tile_rows(k)) for k in ks]
                 batch.add(A.offset(*cc), A.tile_rows(cc[0]), A.tile_cols(cc[1]), kp,
@@ -262,6 +264,9 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
         return batch.finalize()
 
     def f_upd(batch, base, ld):
+        if _rec_nb(tp, A) and not distributed:
+            _recursive_update(tp, ctx, uplo, A, batch.rec)
+            return
         ops.gemm(tA, tB, -1.0, base, ld, base, ld, 1.0, A.data, A.ld, batch)
 
     reserve = int(os.environ.get("DPLASMA_POTRF_RESERVE", POTRF_RESERVE[1 if distributed else 0]))
@@ -303,11 +308,14 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                         fused_rbp = ops.RbPanel(uplo, [(A.offset(*tcoord(i, k)), A.tile_rows(i) if lower
                                                         else A.tile_cols(i)) for i in mine_k], A.ld)
 
-                def f_potrf(off=off, kb=kb, k=k, dk=dk, frbp=fused_rbp):
+                def f_potrf(off=off, kb=kb, k=k, dk=dk, frbp=fused_rbp,
+                            mine_k=mine_k if fused_rbp is not None else ()):
                     hnb = getattr(tp, "recursive_nb", 0)
                     if hnb and hnb < kb:
                         _recursive_potrf(tp, ctx, uplo, A, dk, hnb, info, k * A.mb)
-                        if frbp is not None:   # the sub-taskpool left no zbuf: solve the panel apart
+                        if frbp is not None and _rec_nb(tp, A) and not distributed:
+                            _recursive_trsm(tp, ctx, uplo, A, k, mine_k)
+                        elif frbp is not None:   # the sub-taskpool left no zbuf: solve the panel apart
                             zk = zbufs[(k % 2) * zsz:(k % 2 + 1) * zsz]
                             ops.trsm_rb_prep(uplo, kb, A.data, off, A.ld, zk)
                             ops.trsm_rb(uplo, kb, A.data, off, A.ld, zk, frbp, A.data, A.ld)
@@ -348,7 +356,10 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                     zk = zbufs[(k % 2) * zsz:(k % 2 + 1) * zsz]
 
                     def f_trsm(rbp=rbp, tri_base=tri_base, tri_ld=tri_ld, tri_off=tri_off, kb=kb, zk=zk,
-                               own=own_diag and tri_base is A.data):
+                               own=own_diag and tri_base is A.data, k=k, mine=mine):
+                        if _rec_nb(tp, A) and not distributed:
+                            _recursive_trsm(tp, ctx, uplo, A, k, mine)
+                            return
                         rec = 0 < getattr(tp, "recursive_nb", 0) < kb   # sub-taskpool left no zbuf
                         if rec or not own:  # the diagonal tile came by broadcast: invert its 32-blocks here
                             ops.trsm_rb_prep(uplo, kb, tri_base, tri_off, tri_ld, zk)
@@ -362,7 +373,10 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                     tb.finalize()
                     side = dplasmaRight if lower else dplasmaLeft
 
-                    def f_trsm(tb=tb, tri_base=tri_base, tri_ld=tri_ld, side=side):
+                    def f_trsm(tb=tb, tri_base=tri_base, tri_ld=tri_ld, side=side, k=k, mine=mine):
+                        if _rec_nb(tp, A) and not distributed:
+                            _recursive_trsm(tp, ctx, uplo, A, k, mine)
+                            return
                         ops.trsm(side, uplo, dplasmaConjTrans, dplasmaNonUnit, 1.0, tri_base, tri_ld, A.data, A.ld,
                                  tb)
                     t_trsm = tp.task(f"TRSM({k})", pstream(k, trsm_stream), f_trsm, [t_db, gate], prio=2)
@@ -547,6 +561,66 @@ def _recursive_potrf(tp, ctx, uplo, A, dk, hnb, info, info_base):
     stp.run(lctx)
     si = stp.info
     info.copy_(torch.where((info == 0) & (si > 0), si + info_base, info))
+
+
+def _rec_nb(tp, A) -> int:
+    """The recursive-incarnation tile size when dplasma_zpotrf_setrecursive asked for one smaller than
+    the tiles (0: the batched tile kernels)."""
+    h = int(getattr(tp, "recursive_nb", 0) or 0)
+    return h if 0 < h < A.mb else 0
+
+
+def _sub(tp, key, build):
+    subs = tp.__dict__.setdefault("_rec_subs", {})
+    sub = subs.get(key)
+    if sub is None:
+        sub = subs[key] = build()
+    return sub
+
+
+def _recursive_trsm(tp, ctx, uplo, A, k, rows):
+    """TRSM(k) as sub-taskpools: every panel tile solved by trsm_New on hnb x hnb re-tilings of the tile
+    and of the diagonal factor (reference: the RECURSIVE body of potrf_ztrsm, src/zpotrf_L.jdf:245-280)."""
+    from .blas3 import trsm_New
+    hnb = _rec_nb(tp, A)
+    lower = uplo == dplasmaLower
+    side = dplasmaRight if lower else dplasmaLeft
+    for i in rows:
+        cc = (i, k) if lower else (k, i)
+
+        def build(cc=cc):
+            lctx = ctx.local()
+            return trsm_New(lctx, side, uplo, dplasmaConjTrans, dplasmaNonUnit, 1.0, A.tile_desc(k, k, hnb),
+                            A.tile_desc(cc[0], cc[1], hnb)), lctx
+        stp, lctx = _sub(tp, ("trsm", cc, hnb), build)
+        stp.run(lctx)
+
+
+def _recursive_update(tp, ctx, uplo, A, rec):
+    """Trailing updates as sub-taskpools: HERK on diagonal tiles, GEMM elsewhere, on hnb x hnb re-tilings
+    (reference: the RECURSIVE bodies of potrf_zherk / potrf_zgemm, src/zpotrf_L.jdf:351-390,473-520)."""
+    from .blas3 import herk_New
+    from .gemm import gemm_New
+    hnb = _rec_nb(tp, A)
+    lower = uplo == dplasmaLower
+    herk_trans = dplasmaNoTrans if lower else dplasmaConjTrans
+    tA, tB = (dplasmaNoTrans, dplasmaConjTrans) if lower else (dplasmaConjTrans, dplasmaNoTrans)
+    for cc, m_, n_, ks in rec:
+        for k in ks:
+            pm = (m_, k) if lower else (k, m_)
+            pn = (n_, k) if lower else (k, n_)
+
+            def build(cc=cc, pm=pm, pn=pn, diag=(m_ == n_)):
+                lctx = ctx.local()
+                C = A.tile_desc(cc[0], cc[1], hnb)
+                if diag:
+                    return herk_New(lctx, uplo, herk_trans, -1.0, A.tile_desc(*pm, hnb), 1.0, C), lctx
+                # lower: C(m,n) -= L(m,k) L(n,k)^H ; upper: C(n,m) -= U(k,n)^H U(k,m)
+                a, b = (A.tile_desc(*pm, hnb), A.tile_desc(*pn, hnb)) if lower else \
+                    (A.tile_desc(*pn, hnb), A.tile_desc(*pm, hnb))
+                return gemm_New(lctx, tA, tB, -1.0, a, b, 1.0, C), lctx
+            stp, lctx = _sub(tp, ("upd", cc, k, hnb), build)
+            stp.run(lctx)
 
 
 def potrf(ctx, uplo: int, A) -> int:

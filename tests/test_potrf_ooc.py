@@ -51,23 +51,30 @@ def test_potrf_lowmem_gpu():
     assert dp.potrf(ctx, dp.dplasmaLower, A) == 0
 
 
+@pytest.mark.parametrize("uplo", [dp.dplasmaLower, dp.dplasmaUpper])
 @pytest.mark.parametrize("hnb", [16, 24])
-def test_potrf_recursive_cpu(hnb):
-    """setrecursive(hnb): every diagonal-tile factorisation runs as a sub-taskpool of hnb tiles."""
+def test_potrf_recursive_cpu(hnb, uplo):
+    """setrecursive(hnb): every diagonal-tile factorisation, panel solve and trailing update of a tile
+    larger than hnb runs as a sub-taskpool of hnb tiles (POTRF / TRSM / HERK / GEMM incarnations)."""
     ctx = dp.Context(device="cpu")
     N, NB = 200, 64
     A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
-    dp.plghe(ctx, float(N), dp.dplasmaLower, A, 3872)
+    dp.plghe(ctx, float(N), uplo, A, 3872)
     A0 = A.like()
     dp.lacpy(ctx, dp.dplasmaUpperLower, A, A0)
-    tp = dp.dpotrf_New(ctx, dp.dplasmaLower, A)
+    tp = dp.dpotrf_New(ctx, uplo, A)
     dp.dpotrf_setrecursive(tp, hnb)
     assert tp.execute(ctx) == 0
-    ok, res = dp.check_potrf(ctx, dp.dplasmaLower, A, A0)
+    ok, res = dp.check_potrf(ctx, uplo, A, A0)
     assert ok, res
-    assert len(tp._rec_subs) == sum(A.tile_rows(k) > hnb for k in range(A.nt))  # one per large diagonal tile
-    sub = next(iter(tp._rec_subs.values()))[0]
+    subs = tp._rec_subs
+    pot = [k for k in subs if not isinstance(k[0], str)]
+    assert len(pot) == sum(A.tile_rows(k) > hnb for k in range(A.nt))  # one per large diagonal tile
+    assert any(k[0] == "trsm" for k in subs) and any(k[0] == "upd" for k in subs)
+    sub = subs[pot[0]][0]
     assert any(t.name.startswith("POTRF(1)") for t in sub.tasks)   # the tile really was re-tiled
+    names = {type(v[0]).__name__ for v in subs.values()}
+    assert names == {"Taskpool"}
 
 
 def test_potrf_recursive_info_cpu():
@@ -82,15 +89,17 @@ def test_potrf_recursive_info_cpu():
 
 
 @pytest.mark.gpu
-def test_potrf_recursive_gpu():
+@pytest.mark.parametrize("uplo", [dp.dplasmaLower, dp.dplasmaUpper])
+def test_potrf_recursive_gpu(uplo):
     ctx = dp.Context(device="cuda:0")
     N, NB = 2048, 512
     A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
-    dp.plghe(ctx, float(N), dp.dplasmaLower, A, 3872)
+    dp.plghe(ctx, float(N), uplo, A, 3872)
     A0 = A.like()
     dp.lacpy(ctx, dp.dplasmaUpperLower, A, A0)
-    tp = dp.dpotrf_New(ctx, dp.dplasmaLower, A)
+    tp = dp.dpotrf_New(ctx, uplo, A)
     dp.dpotrf_setrecursive(tp, 128)
     assert tp.execute(ctx) == 0
-    ok, res = dp.check_potrf(ctx, dp.dplasmaLower, A, A0)
+    ok, res = dp.check_potrf(ctx, uplo, A, A0)
     assert ok, res
+    assert any(k[0] == "trsm" for k in tp._rec_subs) and any(k[0] == "upd" for k in tp._rec_subs)
