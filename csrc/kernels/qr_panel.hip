@@ -48,14 +48,26 @@ template <> struct QPM<float> {
 
 // mma(x, y, acc): D(p, q) += sum_k x(p, k) y(q, k); input lane l carries p (resp. q) = l & 15,
 // k = l >> 4; output acc[r] of lane l is D(drow(l, r), l & 15).
+// Workspace layout for a G-workgroup panel (bytes, 256-aligned parts): part1 [2][G][32], rowj [2][32],
+// part2 [G][32*(nc+32)], Yg [32*(nc+32)], Xc [nblk][32][kf] elements of the precision, then the barrier counter.
+__host__ __device__ static inline long long qp_align(long long x) { return (x + 255) & ~255LL; }
+__host__ __device__ static inline void qp_layout_g(long long es, int nc, int kf, int G, long long off[6]) {
+  const long long nblk = (kf + QP_B - 1) / QP_B;
+  off[0] = 0;
+  off[1] = off[0] + qp_align(es * 2 * G * QP_B);
+  off[2] = off[1] + qp_align(es * 2 * QP_B);
+  off[3] = off[2] + qp_align(es * (long long)G * QP_B * (nc + QP_B));
+  off[4] = off[3] + qp_align(es * QP_B * (nc + QP_B));
+  off[5] = off[4] + qp_align(es * nblk * QP_B * kf);
+}
+
 template <typename T>
-__global__ __launch_bounds__(256, 1) void k_qr_panel_persist(T* __restrict__ P0, int ldp, int rbl, long long rstride,
-                                                             int M, int nc, int kf, int R,
-                                                             T* __restrict__ V, int ldv, T* __restrict__ Tm, int ldt,
-                                                             T* __restrict__ part1, T* __restrict__ rowj,
-                                                             T* __restrict__ part2, T* __restrict__ Yg,
-                                                             T* __restrict__ Xc, int* __restrict__ cnt,
-                                                             int* __restrict__ info, long long* __restrict__ prof) {
+__device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int rbl, long long rstride, int M, int nc,
+                                              int kf, int R, T* __restrict__ V, int ldv, T* __restrict__ Tm, int ldt,
+                                              T* __restrict__ part1, T* __restrict__ rowj, T* __restrict__ part2,
+                                              T* __restrict__ Yg, T* __restrict__ Xc, int* __restrict__ cnt,
+                                              int* __restrict__ info, long long* __restrict__ prof, const int G_,
+                                              const int w_) {
   typedef QPM<T> MM;
   typedef typename MM::acc_t acc_t;
   __shared__ T Ab[QP_B][QP_LD];     // finished block columns (R / beta / V), later explicit V_b
@@ -65,7 +77,7 @@ __global__ __launch_bounds__(256, 1) void k_qr_panel_persist(T* __restrict__ P0,
   __shared__ T red[8][QP_B + 1];
   __shared__ T fin[2 * QP_B];
   __shared__ T ff[QP_B], taus[QP_B];
-  const int G = gridDim.x, w = blockIdx.x, tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
+  const int G = G_, w = w_, tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
   const int rbase = w * R;
   const int nr = max(0, min(R, M - rbase));
   const int R16 = (nr + 15) & ~15;
@@ -453,6 +465,45 @@ __global__ __launch_bounds__(256, 1) void k_qr_panel_persist(T* __restrict__ P0,
 #undef QP_TICK
 }
 
+template <typename T>
+__global__ __launch_bounds__(256, 1) void k_qr_panel_persist(T* __restrict__ P0, int ldp, int rbl, long long rstride,
+                                                             int M, int nc, int kf, int R,
+                                                             T* __restrict__ V, int ldv, T* __restrict__ Tm, int ldt,
+                                                             T* __restrict__ part1, T* __restrict__ rowj,
+                                                             T* __restrict__ part2, T* __restrict__ Yg,
+                                                             T* __restrict__ Xc, int* __restrict__ cnt,
+                                                             int* __restrict__ info, long long* __restrict__ prof) {
+  qr_panel_body<T>(P0, ldp, rbl, rstride, M, nc, kf, R, V, ldv, Tm, ldt, part1, rowj, part2, Yg, Xc, cnt, info, prof,
+                   gridDim.x, blockIdx.x);
+}
+
+// Several independent panels in ONE launch (the TS domains of one panel step of a hierarchical tree,
+// or the TT stacks of one tree round): panel e owns workgroups [wbase, wbase + G) and its own
+// workspace / barrier counter; every panel's workgroups are co-resident (sum of G <= CUs).
+struct QpItem {
+  void* P0;
+  long long rstride;
+  void* V;
+  void* Tm;
+  char* ws;   // qp_layout_g parts 0..4
+  int* cnt;   // barrier counter (zeroed before every launch)
+  int ldp, rbl, M, nc, kf, R, ldv, ldt, G, wbase;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256, 1) void k_qr_panel_multi(const QpItem* __restrict__ items, int nitems,
+                                                           int* __restrict__ info) {
+  int e = 0;
+  while (e + 1 < nitems && items[e + 1].wbase <= (int)blockIdx.x) ++e;
+  const QpItem it = items[e];
+  long long off[6];
+  qp_layout_g(sizeof(T), it.nc, it.kf, it.G, off);
+  char* b = it.ws;
+  qr_panel_body<T>((T*)it.P0, it.ldp, it.rbl, it.rstride, it.M, it.nc, it.kf, it.R, (T*)it.V, it.ldv, (T*)it.Tm,
+                   it.ldt, (T*)(b + off[0]), (T*)(b + off[1]), (T*)(b + off[2]), (T*)(b + off[3]), (T*)(b + off[4]),
+                   it.cnt, info, nullptr, it.G, (int)blockIdx.x - it.wbase);
+}
+
 static int g_qp_cus = 0;
 static int qp_cus() {
   if (g_qp_cus == 0) {
@@ -472,19 +523,8 @@ DPL_API int dpl_qr_panel_set_prof(void* dev_ptr) {
   return 0;
 }
 
-static inline long long qp_align(long long x) { return (x + 255) & ~255LL; }
-
-// Workspace layout (bytes, 256-aligned parts): part1 [2][256][32], rowj [2][32], part2 [256][32*(nc+32)],
-// Yg [32*(nc+32)], Xc [nblk][32][kf] elements of the precision, then the barrier counter.
-static inline void qp_layout(long long es, int nc, int kf, long long off[6]) {
-  const long long nblk = (kf + QP_B - 1) / QP_B;
-  off[0] = 0;
-  off[1] = off[0] + qp_align(es * 2 * 256 * QP_B);
-  off[2] = off[1] + qp_align(es * 2 * QP_B);
-  off[3] = off[2] + qp_align(es * 256LL * QP_B * (nc + QP_B));
-  off[4] = off[3] + qp_align(es * QP_B * (nc + QP_B));
-  off[5] = off[4] + qp_align(es * nblk * QP_B * kf);
-}
+// single-panel layout: sized for the largest grid (one workgroup per CU, <= 256)
+static inline void qp_layout(long long es, int nc, int kf, long long off[6]) { qp_layout_g(es, nc, kf, 256, off); }
 
 // complex precisions: qr_panel_z.hip (16-column blocks, VALU block products)
 DPL_API long long dpl_qr_panel_z_ws_bytes(int prec, int nc, int kf);
@@ -585,3 +625,27 @@ DPL_API int dpl_sum_partials(int prec, const void* src, long long stride, int S,
     return -2;
   return (int)hipGetLastError();
 }
+
+// Workspace bytes of one panel of a multi launch (G workgroups).
+DPL_API long long dpl_qr_panel_multi_ws_bytes(int prec, int nc, int kf, int G) {
+  long long off[6];
+  qp_layout_g(prec == DPL_D ? 8 : 4, nc, kf, G, off);
+  return off[5] + 256;
+}
+
+// items: device array of n panels (QpItem, validated by the caller: rbl in (0, M) or 1 << 30, G = ceil(M / 256),
+// R = ceil(M / G), wbase = prefix sum of G, sum of G = total <= CUs); the n barrier counters are the
+// ints cnt0[0..n) (each item's cnt points there), zeroed here.  Real precisions only.
+DPL_API int dpl_qr_panel_multi(int prec, int n, int total, const void* items, int* cnt0, int* info, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (prec != DPL_D && prec != DPL_S) return -2;
+  if (total <= 0 || total > qp_cus()) return -4;
+  HIP_CHECK_RET(hipMemsetAsync(cnt0, 0, sizeof(int) * n, st));
+  if (prec == DPL_D)
+    hipLaunchKernelGGL((k_qr_panel_multi<double>), dim3(total), dim3(256), 0, st, (const QpItem*)items, n, info);
+  else
+    hipLaunchKernelGGL((k_qr_panel_multi<float>), dim3(total), dim3(256), 0, st, (const QpItem*)items, n, info);
+  return (int)hipGetLastError();
+}
+
+DPL_API int dpl_qr_panel_item_bytes() { return (int)sizeof(QpItem); }

@@ -191,6 +191,46 @@ class _Left:
         ops.gemm(N_, N_, -1.0, V, ldv, W2, kf, 1.0, C.data, C.ld, self.g3)
 
 
+class _LeftMulti:
+    """The _Left application of several reflector sets on disjoint row sets at once (the TS domains of
+    one panel step, or the TT stacks of one tree round): three GEMM launches for the whole group.
+    parts: (rows, voff (element offsets of each row tile in the V buffer), wbase (offset of the part's
+    W block), tbase (offset of its T in the T buffer)); every part has kf reflectors."""
+
+    def __init__(self, C, parts, kf, cols):
+        self.kf = kf
+        cols = list(cols)
+        self.empty = not cols or not parts
+        self.wlen = 0
+        if self.empty:
+            return
+        wn = np.array([C.tile_cols(n) for n in cols], dtype=np.int64)
+        wloc = kf * np.concatenate([[0], np.cumsum(wn)[:-1]])
+        ncol = len(cols)
+        g1, g2, g3 = GemmBatch(), GemmBatch(), GemmBatch()
+        for rows, voff, wbase, tbase in parts:
+            rows = list(rows)
+            voff = np.asarray(voff, dtype=np.int64)
+            hr = np.array([C.tile_rows(r) for r in rows], dtype=np.int64)
+            nrow = len(rows)
+            off = _offsets(C, rows, cols)
+            woff = wbase + wloc
+            g1.add_arrays(woff, kf, wn, nrow, np.tile(voff, ncol), off.T.ravel(), np.tile(hr, ncol))
+            g2.add_arrays(woff, kf, wn, 1, tbase, woff, kf)
+            g3.add_arrays(off.T.ravel(), np.tile(hr, ncol), np.repeat(wn, nrow), 1, np.tile(voff, ncol),
+                          np.repeat(woff, nrow), kf)
+            self.wlen = max(self.wlen, int(wbase + kf * wn.sum()))
+        self.g1, self.g2, self.g3 = g1.finalize(), g2.finalize(), g3.finalize()
+
+    def run(self, C, V, ldv, Tm, ldt, W, W2, qt: bool):
+        if self.empty:
+            return
+        kf = self.kf
+        ops.gemm(T_, N_, 1.0, V, ldv, C.data, C.ld, 0.0, W, kf, self.g1)
+        ops.gemm(T_ if qt else N_, N_, 1.0, Tm, ldt, W, kf, 0.0, W2, kf, self.g2)
+        ops.gemm(N_, N_, -1.0, V, ldv, W2, kf, 1.0, C.data, C.ld, self.g3)
+
+
 class _Right:
     """C(rows, cols) := C op(Q) (cols = the reflector rows): W = C V, W' = W op(T), C -= W' V^T."""
 
@@ -287,7 +327,7 @@ def _keep_full_T(Tm, ldt, kf, Td, row, k):
     t = store.get((row, k))
     if t is None or t.numel() < kf * kf or t.device != Tm.device:
         t = store[(row, k)] = torch.empty(kf * kf, dtype=Tm.dtype, device=Tm.device)
-    torch.as_strided(t, (kf, kf), (1, kf), 0).copy_(torch.as_strided(Tm, (kf, kf), (1, ldt), 0))
+    t[: kf * kf].view(kf, kf).t().copy_(torch.as_strided(Tm, (kf, kf), (1, ldt), 0))  # t may be a view
 
 
 def _rebuild_T(V, ldv, M, kf, Td, row, k, out, ldt):
@@ -297,7 +337,7 @@ def _rebuild_T(V, ldv, M, kf, Td, row, k, out, ldt):
     kept = getattr(Td, "full_T", {}).get((row, k))
     dst = torch.as_strided(out, (kf, kf), (1, ldt), 0)
     if kept is not None and kept.device == out.device and kept.numel() >= kf * kf:
-        dst.copy_(torch.as_strided(kept, (kf, kf), (1, kf), 0))
+        dst.copy_(kept[: kf * kf].view(kf, kf).t())  # kept may be a view (batched factorisation)
         return
     ib = Td.mb
     dst.zero_()
@@ -341,6 +381,14 @@ class _Factor:
                 if TT.rank_of(m, k) != A.rank_of(m, k):
                     raise ValueError("geqrf: TT must be distributed like A (tile rows and columns)")
         self.simple = all(len(d) == 1 and not t for d, t in self.plans) and A.grid.P == 1
+        # one process, a tree with several domains / TT rounds per panel: every domain of a panel step in
+        # ONE multi-panel launch and one batched update, then each TT round likewise (DPLASMA_QR_BATCHED=0:
+        # entry by entry)
+        self.batched = (not self.simple and not self.dist and A.grid.P == 1 and A.grid.Q == 1
+                        and os.environ.get("DPLASMA_QR_BATCHED", "1") != "0")
+        if self.batched:
+            self._init_batched()
+            return
         self.ldp = max(16, _rup(A.m, 16))
         nbuf = 2 if self.simple else 1
         self.P = [torch.zeros(self.ldp * nb, dtype=dt, device=dev) for _ in range(nbuf)]
@@ -357,6 +405,124 @@ class _Factor:
         else:
             self.wr = _work_buffers(ups, dt, dev)
         self.xtmp = torch.zeros(max([u.wlen for u in ups] + [1]), dtype=dt, device=dev)
+
+    # ------------------------------------------------------------------ batched general trees (P == 1)
+    def _init_batched(self):
+        A, TS, TT = self.A, self.TS, self.TT
+        dev, dt = A.device, A.dtype
+        nb = A.nb
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 256
+        specs = []
+        for k in range(self.kt):
+            doms, tts = self.plans[k]
+            lev, rounds = {}, {}
+            for (p_, m_) in tts:
+                L = max(lev.get(p_, 0), lev.get(m_, 0)) + 1
+                lev[p_] = L
+                rounds.setdefault(L, []).append([p_, m_])
+            cols = list(range(k + 1, A.nt))
+            kgroups = []
+            for kind, members in [("dom", doms)] + [("tt", rounds[L]) for L in sorted(rounds)]:
+                ents = [self._entry(k, list(r), kind == "tt") for r in members]
+                # launches that fit the CUs (every panel's workgroups co-resident), one kf per launch
+                cur, g = [], 0
+                for e in ents:
+                    ge = -(-e["M"] // 256)
+                    if cur and (g + ge > ncu or e["kf"] != cur[0]["kf"]):
+                        kgroups.append((k, kind, cur, cols))
+                        cur, g = [], 0
+                    cur.append(e)
+                    g += ge
+                if cur:
+                    kgroups.append((k, kind, cur, cols))
+            specs.append(kgroups)
+        # buffer sizes over every group
+        need_p = need_w = need_t = 1
+        ncol_el = lambda cols: sum(A.tile_cols(n) for n in cols)  # noqa: E731
+        for kgroups in specs:
+            for (k, kind, ents, cols) in kgroups:
+                ld = max(e["ld"] for e in ents)
+                need_p = max(need_p, len(ents) * ld * nb)
+                need_t = max(need_t, len(ents) * nb * nb)
+                need_w = max(need_w, len(ents) * ents[0]["kf"] * max(1, ncol_el(cols)))
+        self.Pb = torch.zeros(need_p, dtype=dt, device=dev)
+        self.Vb = torch.zeros(need_p, dtype=dt, device=dev)
+        self.Tb = torch.zeros(need_t, dtype=dt, device=dev)
+        self.Wb = torch.zeros(need_w, dtype=dt, device=dev)
+        self.W2b = torch.zeros(need_w, dtype=dt, device=dev)
+        self.info = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.bsteps = [[self._group(*gspec) for gspec in kgroups] for kgroups in specs]
+
+    def _group(self, k, kind, ents, cols):
+        A = self.A
+        nb, kb = A.nb, A.tile_cols(k)
+        tt = kind == "tt"
+        Td = self.TT if tt else self.TS
+        ib = Td.mb
+        kf = ents[0]["kf"]
+        ld = max(e["ld"] for e in ents)
+        wcols = sum(A.tile_cols(n) for n in cols)
+        gi, bi, panels, parts, ti = [], [], [], [], []
+        for j, e in enumerate(ents):
+            pb, vb, tb = j * ld * nb, j * ld * nb, j * nb * nb
+            if e["direct"] is not None:
+                ldp, rbl, rstride, poff = e["direct"]
+                panels.append((A.data, poff, ldp, rbl, rstride, e["M"], kb, kf, self.Vb, vb, ld, self.Tb, tb, nb))
+            else:
+                g_ = e["gather"].items.copy()
+                g_["b_off"] += pb
+                b_ = e["back"].items.copy()
+                b_["a_off"] += pb
+                gi.append(g_)
+                bi.append(b_)
+                panels.append((self.Pb, pb, ld, 0, 0, e["M"], kb, kf, self.Vb, vb, ld, self.Tb, tb, nb))
+            parts.append((e["rows"], vb + np.asarray(e["voff"], dtype=np.int64), j * kf * wcols, tb))
+            row = e["rows"][1] if tt else e["rows"][0]
+            for b0 in range(0, kf, ib):
+                bs = min(ib, kf - b0)
+                ti.append((tb + b0 * nb + b0, Td.offset(row, k) + b0 * Td.ld, bs, bs, 0, 0))
+        def _tb(arrs):
+            if not arrs:
+                return None
+            t = TileBatch()
+            t.items = np.concatenate(arrs)
+            t.max_m, t.max_n = int(t.items["m"].max()), int(t.items["n"].max())
+            return t
+        tst = TileBatch()
+        for (a, b_, m_, n_, _, _) in ti:
+            tst.add(a, m_, n_, b_off=b_)
+        keep = torch.empty(len(ents) * kf * kf, dtype=A.dtype, device=A.device)
+        store = getattr(Td, "full_T", None)
+        if store is None:
+            store = Td.full_T = {}
+        for j, e in enumerate(ents):
+            store[((e["rows"][1] if tt else e["rows"][0]), k)] = keep[j * kf * kf:(j + 1) * kf * kf]
+        return {"tt": tt, "n": len(ents), "ld": ld, "kf": kf, "zero": tt and bool(gi),
+                "plen": len(ents) * ld * nb, "gather": _tb(gi), "back": _tb(bi), "part": PART_UPPER if tt else PART_FULL,
+                "multi": ops.QrPanelMulti(panels, A.dtype, A.device), "Td": Td, "tstore": tst.finalize(),
+                "keep": keep, "upd": _LeftMulti(A, parts, kf, cols)}
+
+    def step_batched(self, k):
+        A = self.A
+        nb = A.nb
+        for g in self.bsteps[k]:
+            if g["zero"]:
+                self.Pb[: g["plen"]].zero_()
+            if g["gather"] is not None:
+                ops.geadd(g["part"], N_, 1.0, A.data, A.ld, 0.0, self.Pb, g["ld"], g["gather"], copy=True)
+            g["multi"].run(self.info)
+            if g["back"] is not None:
+                ops.geadd(g["part"], N_, 1.0, self.Pb, g["ld"], 0.0, A.data, A.ld, g["back"], copy=True)
+            Td = g["Td"]
+            ops.geadd(PART_FULL, N_, 1.0, self.Tb, nb, 0.0, Td.data, Td.ld, g["tstore"], copy=True)
+            n, kf = g["n"], g["kf"]
+            if kf == nb:
+                g["keep"].view(n, kf * kf).copy_(self.Tb[: n * nb * nb].view(n, nb * nb))
+            else:
+                for j in range(n):
+                    torch.as_strided(g["keep"], (kf, kf), (1, kf), j * kf * kf).copy_(
+                        torch.as_strided(self.Tb, (kf, kf), (1, nb), j * nb * nb))
+            g["upd"].run(A, self.Vb, g["ld"], self.Tb, nb, self.Wb, self.W2b, qt=True)
 
     def _entry(self, k, rows, tt):
         A = self.A
@@ -524,6 +690,10 @@ def factor_New(ctx, A, TS, TT, tree, name="geqrf") -> Taskpool:
                 rst = tp.task(f"qr_rest({k})", "update", (lambda e=e, b=buf: st.apply(e, e["rest"], b, st.wr)),
                               [pan, prev_rest])
             prev_next, prev_rest2, prev_rest = nxt or pan, prev_rest, rst or prev_rest
+    elif st.batched:
+        prev = None
+        for k in range(st.kt):
+            prev = tp.task(f"qr_step({k})", "update", (lambda k=k: st.step_batched(k)), [prev])
     else:
         prev = None
         for k in range(st.kt):

@@ -36,6 +36,9 @@ _SIGS = {
     # prec, part, nitems, items, mmax, nmax, alpha*, beta*, A, lda, stream
     "dpl_laset": [c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp],
     # prec, part, trans, nitems, items, mmax, nmax, alpha*, A, lda, beta*, B, ldb, copy, stream
+    "dpl_qr_panel_multi": [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp],
+    "dpl_qr_panel_multi_ws_bytes": [c_int, c_int, c_int, c_int],
+    "dpl_qr_panel_item_bytes": [],
     "dpl_copy_transpose": [c_int, c_int, c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int, c_vp],
     "dpl_swap_transpose": [c_int, c_int, c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp],
     "dpl_geadd": [c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp],

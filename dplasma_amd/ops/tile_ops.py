@@ -771,6 +771,76 @@ def qr_panel_workspace(nc: int, kf: int, dtype: torch.dtype, device) -> torch.Te
     return torch.zeros(8, dtype=torch.float64)
 
 
+QP_ITEM = np.dtype([("P0", "<u8"), ("rstride", "<i8"), ("V", "<u8"), ("Tm", "<u8"), ("ws", "<u8"), ("cnt", "<u8"),
+                    ("ldp", "<i4"), ("rbl", "<i4"), ("M", "<i4"), ("nc", "<i4"), ("kf", "<i4"), ("R", "<i4"),
+                    ("ldv", "<i4"), ("ldt", "<i4"), ("G", "<i4"), ("wbase", "<i4")])
+
+
+class QrPanelMulti:
+    """Several independent Householder panel factorisations in ONE persistent launch (real precisions,
+    GPU; csrc/kernels/qr_panel.hip k_qr_panel_multi): panel e = (P, poff, ldp, rbl, rstride, M, nc, kf,
+    V, voff, ldv, Tm, toff, ldt) with the semantics of ``qr_panel``.  Built once (items uploaded to the
+    device, per-panel workspaces and barrier counters allocated); ``run`` re-launches.  On the CPU (or
+    for complex types, or more workgroups than CUs) the panels are factored one by one by qr_panel."""
+
+    def __init__(self, panels, dtype, device):
+        self.panels = list(panels)
+        self.dtype, self.device = dtype, torch.device(device)
+        self.multi = (self.device.type == "cuda" and dtype in (torch.float32, torch.float64) and len(self.panels) > 0)
+        if not self.multi:
+            self.ws = qr_panel_workspace(max(p[6] for p in self.panels) if self.panels else 1,
+                                         max(p[7] for p in self.panels) if self.panels else 1, dtype, device)
+            return
+        lib = _lib.load()
+        if int(lib.dpl_qr_panel_item_bytes()) != QP_ITEM.itemsize:
+            raise RuntimeError("QrPanelMulti: QpItem layout mismatch")
+        prec, es = _lib.prec_code(dtype), torch.empty(0, dtype=dtype).element_size()
+        n = len(self.panels)
+        Gs = [max(1, -(-p[5] // 256)) for p in self.panels]
+        self.total = sum(Gs)
+        ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+        if self.total > ncu:
+            raise ValueError(f"QrPanelMulti: {self.total} workgroups > {ncu} CUs (split the group)")
+        sizes = [int(lib.dpl_qr_panel_multi_ws_bytes(prec, int(p[6]), int(p[7]), g)) for p, g in zip(self.panels, Gs)]
+        offs = np.concatenate([[0], np.cumsum([(x + 255) // 256 * 256 for x in sizes])]).astype(np.int64)
+        self.wsbuf = torch.zeros(int(offs[-1]) // 8 + 32, dtype=torch.float64, device=self.device)
+        self.cnt = torch.zeros(n, dtype=torch.int32, device=self.device)
+        it = np.zeros(n, dtype=QP_ITEM)
+        wb = 0
+        for e, ((P, poff, ldp, rbl, rstride, M, nc, kf, V, voff, ldv, Tm, toff, ldt), G) in enumerate(
+                zip(self.panels, Gs)):
+            if not 0 < rbl < M:
+                rbl, rstride = 1 << 30, 0
+                if ldp < M:
+                    raise ValueError("QrPanelMulti: ldp < M")
+            if not (0 < kf <= min(M, nc, 256)) or ldv < M or ldt < kf:
+                raise ValueError("QrPanelMulti: bad panel shape")
+            it[e] = (P.data_ptr() + poff * es, rstride, V.data_ptr() + voff * es, Tm.data_ptr() + toff * es,
+                     self.wsbuf.data_ptr() + int(offs[e]), self.cnt.data_ptr() + 4 * e,
+                     ldp, rbl, M, nc, kf, -(-M // G), ldv, ldt, G, wb)
+            wb += G
+        self.items = torch.from_numpy(it.view(np.uint8).copy()).to(self.device)
+
+    def run(self, info: torch.Tensor):
+        if not self.multi:
+            for (P, poff, ldp, rbl, rstride, M, nc, kf, V, voff, ldv, Tm, toff, ldt) in self.panels:
+                if self.device.type == "cuda":
+                    qr_panel(P, ldp, M, nc, kf, V[voff:], ldv, Tm[toff:], ldt, self.ws, info, rbl=rbl,
+                             rstride=rstride, poff=poff)
+                    continue
+                # CPU: qr_panel addresses V / Tm from their first element -- factor into scratch
+                vt = torch.zeros(ldv * kf, dtype=V.dtype)
+                tt = Tm[toff: toff + ldt * kf].clone()
+                qr_panel(P, ldp, M, nc, kf, vt, ldv, tt, ldt, self.ws, info, rbl=rbl, rstride=rstride, poff=poff)
+                V[voff: voff + ldv * kf] = vt
+                Tm[toff: toff + ldt * kf] = tt
+            return
+        rc = _lib.load().dpl_qr_panel_multi(_lib.prec_code(self.dtype), len(self.panels), self.total,
+                                            self.items.data_ptr(), self.cnt.data_ptr(), info.data_ptr(),
+                                            _lib.stream_ptr())
+        _lib.check(rc, "qr_panel_multi")
+
+
 def _larft_cpu(V: torch.Tensor, tau: torch.Tensor) -> torch.Tensor:
     """Compact-WY T (upper triangular, dlarft forward/columnwise) of explicit reflectors V."""
     k = V.shape[1]
