@@ -98,6 +98,13 @@ NatProgram* nat_getrs(dplasma_context_t* ctx, int prec, int trans, dplasma_desc_
 NatProgram* nat_gesv_1d(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* IPIV,
                         dplasma_desc_t* B);
 dplasma_desc_t* nat_desc_int(dplasma_context_t* ctx, int mb, int nb, int m, int n);
+NatProgram* nat_geqrf(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* T);
+NatProgram* nat_unmqr(dplasma_context_t* ctx, int prec, int side, int trans, dplasma_desc_t* A, dplasma_desc_t* T,
+                      dplasma_desc_t* C);
+NatProgram* nat_ungqr(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* T, dplasma_desc_t* Q);
+NatProgram* nat_geqrs(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* T, dplasma_desc_t* B);
+NatProgram* nat_gels(dplasma_context_t* ctx, int prec, int trans, dplasma_desc_t* A, dplasma_desc_t* T,
+                     dplasma_desc_t* B);
 int nat_execute(dplasma_context_t* ctx, NatProgram* P);     // run + wait + info, frees P
 dplasma_taskpool_t* nat_wrap(NatProgram* P);
 void nat_fini(dplasma_context_t* ctx);

@@ -63,6 +63,9 @@ int dpl_rows_permute(int prec, void* A, int ld, int mb, int r0, const long long*
                      const long long* coloff, const int* ncols, int nct, int nb, const int* dst, const int* src,
                      const int* cnt, int maxcnt, hipStream_t st);
 int dpl_ipiv_shift(const int* in, int* out, int n, int delta, hipStream_t st);
+long long dpl_qr_panel_ws_bytes(int prec, int nc, int kf);
+int dpl_qr_panel(int prec, void* P, int ldp, int rbl, long long rstride, int M, int nc, int kf, void* V, int ldv,
+                 void* Tm, int ldt, void* ws, int* info, hipStream_t st);
 }
 
 namespace {
@@ -137,6 +140,10 @@ struct NatDesc {
   int prec = P_D, es = 8, mb = 0, nb = 0, m = 0, n = 0, mt = 0, nt = 0, lld = 0;
   char* data = nullptr;
   bool owned = false;
+  // a T descriptor written by the native geqrf: every panel's full nb x nb compact-WY T (ld nb), the
+  // reference-layout IB x IB diagonal blocks being in the tiles themselves (unmqr / ungqr / gels read it)
+  DevPtr fullT;
+  int fullT_nb = 0, fullT_kt = 0;
   NatDesc() = default;
   NatDesc(const NatDesc&) = delete;             // owns its buffer: never copied (nor captured by value)
   NatDesc& operator=(const NatDesc&) = delete;
@@ -1576,4 +1583,312 @@ NatProgram* nat_gesv_1d(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dp
 
 dplasma_desc_t* nat_desc_int(dplasma_context_t* ctx, int mb, int nb, int m, int n) {
   return nat_desc(ctx, P_I, mb, nb, m, n, 1, 1, nullptr, 0, 1);
+}
+
+// ----------------------------------------------------------------------------- QR (flat TS tree)
+// models/qr_panel.py's single-domain schedule in C++: panel k = rows k*mb.. of tile column k, one persistent
+// Householder launch (dpl_qr_panel, in place in the LAPACK-layout matrix, explicit V in a parity buffer, the
+// full T into the T descriptor's side buffer); NEXT (column k+1) on the panel stream, REST on the update
+// stream, both  C -= V op(T) (V^H C)  as three batched MFMA GEMM launches.
+namespace {
+
+struct QrWork {
+  DevPtr V[2], ws, W[2], W2[2];
+  int ldv = 0;
+};
+
+bool qr_conform(const NatDesc* A, const NatDesc* T) {
+  return A && T && A->mb == A->nb && A->nb <= 256 && T->nb == A->nb && T->mt >= A->mt && T->nt >= A->nt &&
+         T->mb >= 1 && T->mb <= A->nb;
+}
+
+// C(r0 tile.., cols) := op(Q_k) C, Q_k = I - V T V^H (left; qt: T^H); V rows = rows r0*mb.. of C (M rows)
+bool add_left_apply(NatProgram& P, int prec, NatDesc& C, int r0, int M, int kf, char* V, int ldv, char* Tk, int ldt,
+                    bool qt, char* W, char* W2, const std::vector<int>& cols, int stream, int dep, int& out) {
+  out = dep;
+  if (cols.empty() || kf <= 0) return true;
+  const Scalar one(prec, 1.0), zero(prec, 0.0), m_one(prec, -1.0);
+  auto g1 = std::make_shared<Gemm>(), g2 = std::make_shared<Gemm>(), g3 = std::make_shared<Gemm>();
+  long long wo = 0;
+  for (int j : cols) {
+    const int nj = C.cols(j);
+    g1->add(wo, kf, nj, {KPair{0, C.off(r0, j), M, 0}}, 0);
+    g2->add(wo, kf, nj, {KPair{0, wo, kf, 0}}, 0);
+    for (int i = r0; i < C.mt; ++i) g3->add(C.off(i, j), C.rows(i), nj, {KPair{(long long)(i - r0) * C.mb, wo, kf, 0}}, 0);
+    wo += (long long)kf * nj;
+  }
+  if (!g1->upload(P) || !g2->upload(P) || !g3->upload(P)) return false;
+  char* c = C.data;
+  const int ldc = C.lld;
+  int t = P.task(stream, [=](hipStream_t s) {
+    return g1->launch(prec, CONJTRANS, NOTRANS, one, V, ldv, c, ldc, zero, W, kf, s);
+  }, {dep});
+  t = P.task(stream, [=](hipStream_t s) {
+    return g2->launch(prec, qt ? CONJTRANS : NOTRANS, NOTRANS, one, Tk, ldt, W, kf, zero, W2, kf, s);
+  }, {t});
+  out = P.task(stream, [=](hipStream_t s) {
+    return g3->launch(prec, NOTRANS, NOTRANS, m_one, V, ldv, W2, kf, one, c, ldc, s);
+  }, {t});
+  return true;
+}
+
+// C := C op(Q_k) (right): W = C(:, r0..) V, W2 = W op(T), C(:, r0..) -= W2 V^H   (C.nb == the panel's mb)
+bool add_right_apply(NatProgram& P, int prec, NatDesc& C, int r0, int M, int kf, char* V, int ldv, char* Tk, int ldt,
+                     bool qt, char* W, char* W2, int ldw, int stream, int dep, int& out) {
+  out = dep;
+  if (kf <= 0 || C.mt == 0) return true;
+  const Scalar one(prec, 1.0), zero(prec, 0.0), m_one(prec, -1.0);
+  auto g1 = std::make_shared<Gemm>(), g2 = std::make_shared<Gemm>(), g3 = std::make_shared<Gemm>();
+  for (int i = 0; i < C.mt; ++i) {
+    const long long wo = (long long)i * C.mb;
+    g1->add(wo, C.rows(i), kf, {KPair{C.off(i, r0), 0, M, 0}}, 0);
+    g2->add(wo, C.rows(i), kf, {KPair{wo, 0, kf, 0}}, 0);
+    for (int j = r0; j < C.nt; ++j) g3->add(C.off(i, j), C.rows(i), C.cols(j), {KPair{wo, (long long)(j - r0) * C.nb, kf, 0}}, 0);
+  }
+  if (!g1->upload(P) || !g2->upload(P) || !g3->upload(P)) return false;
+  char* c = C.data;
+  const int ldc = C.lld;
+  int t = P.task(stream, [=](hipStream_t s) {
+    return g1->launch(prec, NOTRANS, NOTRANS, one, c, ldc, V, ldv, zero, W, ldw, s);
+  }, {dep});
+  t = P.task(stream, [=](hipStream_t s) {
+    return g2->launch(prec, NOTRANS, qt ? CONJTRANS : NOTRANS, one, W, ldw, Tk, ldt, zero, W2, ldw, s);
+  }, {t});
+  out = P.task(stream, [=](hipStream_t s) {
+    return g3->launch(prec, NOTRANS, CONJTRANS, m_one, W2, ldw, V, ldv, one, c, ldc, s);
+  }, {t});
+  return true;
+}
+
+bool add_geqrf(NatProgram& P, NatDesc& A, NatDesc& T, int& last) {
+  const int prec = A.prec, nb = A.nb, es = A.es;
+  const int kt = std::min(A.mt, A.nt);
+  QrWork Wk;
+  Wk.ldv = std::max(16, (A.m + 15) / 16 * 16);
+  const size_t wlen = (size_t)nb * std::max(1, A.n);
+  for (int b = 0; b < 2; ++b) {
+    Wk.V[b] = dev_alloc((size_t)Wk.ldv * nb * es, true);
+    Wk.W[b] = dev_alloc(wlen * es, false);
+    Wk.W2[b] = dev_alloc(wlen * es, false);
+  }
+  Wk.ws = dev_alloc((size_t)dpl_qr_panel_ws_bytes(prec, nb, nb) + 256, true);
+  T.fullT = dev_alloc((size_t)std::max(1, kt) * nb * nb * es, true);
+  T.fullT_nb = nb;
+  T.fullT_kt = kt;
+  for (const DevPtr& d : {Wk.V[0], Wk.V[1], Wk.W[0], Wk.W[1], Wk.W2[0], Wk.W2[1], Wk.ws, T.fullT}) {
+    if (!d) return false;
+    P.keep.push_back(d);
+  }
+  char* a = A.data;
+  char* tf = (char*)T.fullT->p;
+  char* t = T.data;
+  int* info = (int*)P.info->p;
+  const int lda = A.lld, ldv = Wk.ldv, ldT = T.lld, ib = T.mb;
+  int prev_next = -1, prev_rest = -1, prev_rest2 = -1;
+  for (int k = 0; k < kt; ++k) {
+    const int M = A.m - k * A.mb, kb = A.cols(k), kf = std::min(M, kb), buf = k & 1;
+    char* V = (char*)Wk.V[buf]->p;
+    char* Tk = tf + (size_t)k * nb * nb * es;
+    char* ws = (char*)Wk.ws->p;
+    char* pk = a + A.off(k, k) * es;
+    const int pan = P.task(0, [=](hipStream_t s) {
+      return dpl_qr_panel(prec, pk, lda, 0, 0, M, kb, kf, V, ldv, Tk, nb, ws, info, s);
+    }, {prev_next, prev_rest2});
+    // the reference layout: IB x IB diagonal blocks of T into tile T(k, k)
+    std::vector<TileItem> ti;
+    for (int b0 = 0; b0 < kf; b0 += ib) {
+      const int bs = std::min(ib, kf - b0);
+      ti.push_back(TileItem{(long long)k * nb * nb + b0 + (long long)b0 * nb, T.off(k, k) + (long long)b0 * ldT, bs, bs, 0, 0});
+    }
+    auto d_ti = dev_upload(ti);
+    if (!d_ti) return false;
+    P.keep.push_back(d_ti);
+    const int nti = (int)ti.size();
+    const Scalar one(prec, 1.0), zero(prec, 0.0);
+    int tst = P.task(0, [=](hipStream_t s) {
+      return dpl_geadd(prec, 0, NOTRANS, nti, d_ti->p, ib, ib, one.ptr(), tf, nb, zero.ptr(), t, ldT, 1, s);
+    }, {pan});
+    int nxt = tst, rst = prev_rest;
+    std::vector<int> cn, cr;
+    for (int j = k + 1; j < A.nt; ++j) (j == k + 1 ? cn : cr).push_back(j);
+    if (!add_left_apply(P, prec, A, k, M, kf, V, ldv, Tk, nb, true, (char*)Wk.W[0]->p, (char*)Wk.W2[0]->p, cn, 0,
+                        P.task(0, [](hipStream_t) { return 0; }, {tst, prev_rest}), nxt))
+      return false;
+    if (!cr.empty()) {
+      if (!add_left_apply(P, prec, A, k, M, kf, V, ldv, Tk, nb, true, (char*)Wk.W[1]->p, (char*)Wk.W2[1]->p, cr, 1,
+                          P.task(1, [](hipStream_t) { return 0; }, {pan, prev_rest}), rst))
+        return false;
+    }
+    prev_rest2 = prev_rest;
+    prev_next = nxt;
+    prev_rest = rst;
+  }
+  last = P.task(1, [](hipStream_t) { return 0; }, {prev_next, prev_rest});
+  return true;
+}
+
+// V of panel k rebuilt from A (unit diagonal, zeros above) into V (ld ldv)
+int add_build_v(NatProgram& P, NatDesc& A, int k, char* V, int ldv, int stream, int dep) {
+  const int prec = A.prec, kb = A.cols(k);
+  std::vector<TileItem> it;
+  for (int i = k; i < A.mt; ++i)
+    it.push_back(TileItem{A.off(i, k), (long long)(i - k) * A.mb, A.rows(i), kb, (i - k) * A.mb, 0});
+  std::vector<TileItem> lt;
+  for (const TileItem& x : it) lt.push_back(TileItem{x.b_off, 0, x.m, x.n, x.gi, x.gj});
+  auto d_it = dev_upload(it), d_lt = dev_upload(lt);
+  if (!d_it || !d_lt) return -2;
+  P.keep.push_back(d_it);
+  P.keep.push_back(d_lt);
+  const int n = (int)it.size(), mb = A.mb, lda = A.lld;
+  char* a = A.data;
+  const Scalar zero(prec, 0.0), one(prec, 1.0);
+  int t = P.task(stream, [=](hipStream_t s) {
+    return dpl_laset(prec, 0, n, d_lt->p, mb, kb, zero.ptr(), one.ptr(), V, ldv, s);
+  }, {dep});
+  return P.task(stream, [=](hipStream_t s) {   // part 3: strictly below the (stacked) diagonal
+    return dpl_geadd(prec, 3, NOTRANS, n, d_it->p, mb, kb, one.ptr(), a, lda, zero.ptr(), V, ldv, 1, s);
+  }, {t});
+}
+
+// C := op(Q) C (left) or C op(Q) (right) with Q from the native geqrf (A, T)
+bool add_unmqr(NatProgram& P, int side, int trans, NatDesc& A, NatDesc& T, NatDesc& C, int& last) {
+  const int prec = A.prec, nb = A.nb, es = A.es, kt = std::min(A.mt, A.nt);
+  const bool left = side == LEFT, qt = trans != NOTRANS;
+  const int ldv = std::max(16, (A.m + 15) / 16 * 16);
+  const int ldw = std::max(16, (C.m + 15) / 16 * 16);
+  const size_t wlen = left ? (size_t)nb * std::max(1, C.n) : (size_t)ldw * nb;
+  DevPtr V = dev_alloc((size_t)ldv * nb * es, true), W = dev_alloc(wlen * es, false), W2 = dev_alloc(wlen * es, false);
+  if (!V || !W || !W2) return false;
+  for (const DevPtr& d : {V, W, W2}) P.keep.push_back(d);
+  char* tf = (char*)T.fullT->p;
+  std::vector<int> order;
+  // left: Q^H C applies panel 0 first, Q C the last first; right: C Q panel 0 first, C Q^H the last first
+  const bool forward = left ? qt : !qt;
+  for (int s = 0; s < kt; ++s) order.push_back(forward ? s : kt - 1 - s);
+  int prev = last;
+  for (int k : order) {
+    const int M = A.m - k * A.mb, kf = std::min(M, A.cols(k));
+    prev = add_build_v(P, A, k, (char*)V->p, ldv, 1, prev);
+    if (prev < -1) return false;
+    char* Tk = tf + (size_t)k * nb * nb * es;
+    std::vector<int> cols;
+    for (int j = 0; j < C.nt; ++j) cols.push_back(j);
+    int out = prev;
+    bool ok = left ? add_left_apply(P, prec, C, k, M, kf, (char*)V->p, ldv, Tk, nb, qt, (char*)W->p, (char*)W2->p, cols,
+                                    1, prev, out)
+                   : add_right_apply(P, prec, C, k, M, kf, (char*)V->p, ldv, Tk, nb, qt, (char*)W->p, (char*)W2->p,
+                                     ldw, 1, prev, out);
+    if (!ok) return false;
+    prev = out;
+  }
+  last = prev;
+  return true;
+}
+
+// a non-owning view of the leading r x c part of D (same tiling and storage)
+std::shared_ptr<NatDesc> lead_view(NatDesc& D, int r, int c) {
+  auto v = std::make_shared<NatDesc>();
+  v->ctx = D.ctx;
+  v->prec = D.prec;
+  v->es = D.es;
+  v->mb = D.mb;
+  v->nb = D.nb;
+  v->m = r;
+  v->n = c;
+  v->mt = (r + D.mb - 1) / D.mb;
+  v->nt = (c + D.nb - 1) / D.nb;
+  v->lld = D.lld;
+  v->data = D.data;
+  v->owned = false;
+  return v;
+}
+
+bool has_fullT(const NatDesc& A, const NatDesc& T) {
+  return T.fullT && T.fullT_nb == A.nb && T.fullT_kt >= std::min(A.mt, A.nt);
+}
+
+}  // namespace
+
+NatProgram* nat_geqrf(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dplasma_desc_t* dT) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *T = dT ? dT->nat : nullptr;
+  if (!same_ctx(c, {A, T}, prec)) return fail(nullptr, "geqrf: descriptors of another context or precision");
+  if (!qr_conform(A, T)) return fail(nullptr, "geqrf: square tiles <= 256 and a T of (IB x NB) tiles covering A");
+  NatProgram* P = new_program(c, "geqrf", true);
+  int last = -1;
+  if (!P->info || !add_geqrf(*P, *A, *T, last)) return fail(P, "geqrf: device allocation failed");
+  return P;
+}
+
+NatProgram* nat_unmqr(dplasma_context_t* ctx, int prec, int side, int trans, dplasma_desc_t* dA, dplasma_desc_t* dT,
+                      dplasma_desc_t* dC) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *T = dT ? dT->nat : nullptr, *C = dC ? dC->nat : nullptr;
+  if (!same_ctx(c, {A, T, C}, prec)) return fail(nullptr, "unmqr: descriptors of another context or precision");
+  if (!qr_conform(A, T) || !has_fullT(*A, *T)) return fail(nullptr, "unmqr: T must come from the native geqrf of A");
+  if ((side == LEFT && (C->m != A->m || C->mb != A->mb)) || (side == RIGHT && (C->n != A->m || C->nb != A->mb)))
+    return fail(nullptr, "unmqr: C does not conform to Q");
+  NatProgram* P = new_program(c, "unmqr", false);
+  int last = -1;
+  if (!add_unmqr(*P, side, trans, *A, *T, *C, last)) return fail(P, "unmqr: device allocation failed");
+  return P;
+}
+
+// Q (M x K) := the first K columns of the orthogonal factor: Q = I(:, :K), then Q := Q_geqrf Q
+NatProgram* nat_ungqr(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dplasma_desc_t* dT, dplasma_desc_t* dQ) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *T = dT ? dT->nat : nullptr, *Q = dQ ? dQ->nat : nullptr;
+  if (!same_ctx(c, {A, T, Q}, prec)) return fail(nullptr, "ungqr: descriptors of another context or precision");
+  if (!qr_conform(A, T) || !has_fullT(*A, *T) || Q->m != A->m || Q->mb != A->mb || Q->n > A->m)
+    return fail(nullptr, "ungqr: T from the native geqrf of A, Q with A's rows");
+  NatProgram* P = new_program(c, "ungqr", false);
+  std::vector<TileItem> it;
+  for (int i = 0; i < Q->mt; ++i)
+    for (int j = 0; j < Q->nt; ++j) it.push_back(TileItem{Q->off(i, j), 0, Q->rows(i), Q->cols(j), i * Q->mb, j * Q->nb});
+  auto d_it = dev_upload(it);
+  if (!d_it) return fail(P, "ungqr: device allocation failed");
+  P->keep.push_back(d_it);
+  const int n = (int)it.size(), mb = Q->mb, nb = Q->nb, ldq = Q->lld;
+  char* q = Q->data;
+  const Scalar zero(prec, 0.0), one(prec, 1.0);
+  int last = P->task(1, [=](hipStream_t s) {
+    return dpl_laset(prec, 0, n, d_it->p, mb, nb, zero.ptr(), one.ptr(), q, ldq, s);
+  }, {});
+  if (!add_unmqr(*P, LEFT, NOTRANS, *A, *T, *Q, last)) return fail(P, "ungqr: device allocation failed");
+  return P;
+}
+
+// X = R^{-1} (Q^H B)(0:N) for a factored M >= N matrix (B's first N rows receive X)
+static bool add_geqrs(NatProgram& P, NatDesc& A, NatDesc& T, NatDesc& B, int& last) {
+  if (!add_unmqr(P, LEFT, CONJTRANS, A, T, B, last)) return false;
+  auto R = lead_view(A, A.n, A.n), X = lead_view(B, A.n, B.n);
+  P.wdesc.push_back(R);
+  P.wdesc.push_back(X);
+  return add_trsm(P, LEFT, UPPER, NOTRANS, NONUNIT, Scalar(A.prec, 1.0), *R, *X, 1, last);
+}
+
+NatProgram* nat_geqrs(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dplasma_desc_t* dT, dplasma_desc_t* dB) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *T = dT ? dT->nat : nullptr, *B = dB ? dB->nat : nullptr;
+  if (!same_ctx(c, {A, T, B}, prec)) return fail(nullptr, "geqrs: descriptors of another context or precision");
+  if (!qr_conform(A, T) || !has_fullT(*A, *T) || A->m < A->n || B->m != A->m || B->mb != A->mb)
+    return fail(nullptr, "geqrs: T from the native geqrf of an M >= N matrix A, B with A's rows");
+  NatProgram* P = new_program(c, "geqrs", false);
+  int last = -1;
+  if (!add_geqrs(*P, *A, *T, *B, last)) return fail(P, "geqrs: device allocation failed");
+  return P;
+}
+
+NatProgram* nat_gels(dplasma_context_t* ctx, int prec, int trans, dplasma_desc_t* dA, dplasma_desc_t* dT,
+                     dplasma_desc_t* dB) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *T = dT ? dT->nat : nullptr, *B = dB ? dB->nat : nullptr;
+  if (!same_ctx(c, {A, T, B}, prec)) return fail(nullptr, "gels: descriptors of another context or precision");
+  if (trans != NOTRANS || !qr_conform(A, T) || A->m < A->n || B->m != A->m || B->mb != A->mb)
+    return fail(nullptr, "gels: NoTrans least squares of an M >= N matrix (native engine)");
+  NatProgram* P = new_program(c, "gels", true);
+  int last = -1;
+  if (!P->info || !add_geqrf(*P, *A, *T, last) || !add_geqrs(*P, *A, *T, *B, last))
+    return fail(P, "gels: device allocation failed");
+  return P;
 }

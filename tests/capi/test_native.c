@@ -597,6 +597,93 @@ static void test_dgetrf(dplasma_context_t *ctx) {
   dplasma_desc_destroy(A), dplasma_desc_destroy(B), dplasma_desc_destroy(IP);
 }
 
+/* flat-tree QR family: geqrf, ungqr (thin and full Q), unmqr (left Q^T, right Q), gels */
+static void test_dgeqrf(dplasma_context_t *ctx) {
+  const int m = 700, n = 400, nb = 128, ib = 32, nrhs = 3, p = 50;
+  const int mt = (m + nb - 1) / nb, nt = (n + nb - 1) / nb;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, m, n);
+  dplasma_desc_t *T = dplasma_desc_block_cyclic(ctx, dplasmaRealDouble, ib, nb, mt * ib, nt * nb, 1, 1,
+                                               dplasmaUpperLower);
+  dplasma_desc_t *Q = dmat(ctx, dplasmaRealDouble, nb, m, n), *Qf = dmat(ctx, dplasmaRealDouble, nb, m, m);
+  dplasma_desc_t *C = dmat(ctx, dplasmaRealDouble, nb, m, n), *D = dmat(ctx, dplasmaRealDouble, nb, p, m);
+  dplasma_desc_t *B = dmat(ctx, dplasmaRealDouble, nb, m, nrhs);
+  CHECK(T && Q && Qf && C && D && B, "descriptors: %s", dplasma_last_error());
+  double *a = malloc(sizeof(double) * m * n), *f = malloc(sizeof(double) * m * n), *q = malloc(sizeof(double) * m * n);
+  double *qf = malloc(sizeof(double) * m * m), *c = malloc(sizeof(double) * m * n);
+  double *d = malloc(sizeof(double) * p * m), *dq = malloc(sizeof(double) * p * m);
+  double *b = malloc(sizeof(double) * m * nrhs), *x = malloc(sizeof(double) * m * nrhs);
+  unsigned sd = 77;
+  rnd_fill(a, (size_t)m * n, &sd), rnd_fill(d, (size_t)p * m, &sd), rnd_fill(b, (size_t)m * nrhs, &sd);
+  dplasma_desc_set_lapack(A, a, m);
+  int info = dplasma_dgeqrf(ctx, A, T);
+  CHECK(info == 0, "dgeqrf info %d (%s)", info, dplasma_last_error());
+  dplasma_desc_get_lapack(A, f, m);
+  CHECK(dplasma_dungqr(ctx, A, T, Q) == 0, "dungqr: %s", dplasma_last_error());
+  CHECK(dplasma_dungqr(ctx, A, T, Qf) == 0, "dungqr full: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(Q, q, m);
+  dplasma_desc_get_lapack(Qf, qf, m);
+  double orth = 0, res = 0, an = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < n; ++i) {
+      double s = 0;
+      for (int k = 0; k < m; ++k) s += q[k + (size_t)i * m] * q[k + (size_t)j * m];
+      orth = fmax(orth, fabs(s - (i == j)));
+    }
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < m; ++i) {
+      double s = 0;
+      for (int k = 0; k <= j && k < n; ++k) s += q[i + (size_t)k * m] * f[k + (size_t)j * m];
+      res = fmax(res, fabs(s - a[i + (size_t)j * m]));
+      an = fmax(an, fabs(a[i + (size_t)j * m]));
+    }
+  printf("dgeqrf m=%d n=%d nb=%d ib=%d: ||Q^T Q - I|| %.3e  ||QR - A||/||A|| %.3e\n", m, n, nb, ib, orth, res / an);
+  CHECK(orth < 1e-12 && res / an < 1e-12, "geqrf / ungqr residuals");
+  /* Q^T A0 = [R; 0] */
+  dplasma_desc_set_lapack(C, a, m);
+  CHECK(dplasma_dunmqr(ctx, dplasmaLeft, dplasmaTrans, A, T, C) == 0, "dunmqr L T: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(C, c, m);
+  double e1 = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < m; ++i) e1 = fmax(e1, fabs(c[i + (size_t)j * m] - (i <= j ? f[i + (size_t)j * m] : 0.0)));
+  /* D Q (right, no transpose) against the host product with the full Q */
+  dplasma_desc_set_lapack(D, d, p);
+  CHECK(dplasma_dunmqr(ctx, dplasmaRight, dplasmaNoTrans, A, T, D) == 0, "dunmqr R N: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(D, dq, p);
+  double e2 = 0;
+  for (int j = 0; j < m; ++j)
+    for (int i = 0; i < p; ++i) {
+      double s = 0;
+      for (int k = 0; k < m; ++k) s += d[i + (size_t)k * p] * qf[k + (size_t)j * m];
+      e2 = fmax(e2, fabs(s - dq[i + (size_t)j * p]));
+    }
+  printf("dunmqr: ||Q^T A - R|| / ||A|| %.3e   ||D Q - D*Q|| %.3e\n", e1 / an, e2);
+  CHECK(e1 / an < 1e-12 && e2 < 1e-11, "unmqr residuals");
+  /* least squares: A^T (A x - b) = 0 */
+  dplasma_desc_set_lapack(A, a, m);
+  dplasma_desc_set_lapack(B, b, m);
+  info = dplasma_dgels(ctx, dplasmaNoTrans, A, T, B);
+  CHECK(info == 0, "dgels info %d (%s)", info, dplasma_last_error());
+  dplasma_desc_get_lapack(B, x, m);
+  double ne = 0, bn = 0;
+  for (int r = 0; r < nrhs; ++r) {
+    for (int j = 0; j < n; ++j) {
+      double s = 0;
+      for (int i = 0; i < m; ++i) {
+        double ax = 0;
+        for (int k = 0; k < n; ++k) ax += a[i + (size_t)k * m] * x[k + (size_t)r * m];
+        s += a[i + (size_t)j * m] * (ax - b[i + (size_t)r * m]);
+      }
+      ne = fmax(ne, fabs(s));
+    }
+    for (int i = 0; i < m; ++i) bn = fmax(bn, fabs(b[i + (size_t)r * m]));
+  }
+  printf("dgels: ||A^T (A x - b)|| / (m ||A|| ||b||) %.3e\n", ne / (m * an * bn));
+  CHECK(ne / (m * an * bn) < 1e-12, "gels normal equations %.3e", ne / (m * an * bn));
+  free(a), free(f), free(q), free(qf), free(c), free(d), free(dq), free(b), free(x);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(T), dplasma_desc_destroy(Q), dplasma_desc_destroy(Qf);
+  dplasma_desc_destroy(C), dplasma_desc_destroy(D), dplasma_desc_destroy(B);
+}
+
 int main(int argc, char **argv) {
   setvbuf(stdout, NULL, _IONBF, 0);
   signal(SIGSEGV, on_fault);
@@ -625,9 +712,10 @@ int main(int argc, char **argv) {
   test_dtrmm(ctx, dplasmaRight, dplasmaLower, dplasmaTrans, dplasmaNonUnit);
   test_symm_hemm(ctx);
   test_dgetrf(ctx);
+  test_dgeqrf(ctx);
   /* an operation without a native implementation fails cleanly */
   dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
-  CHECK(dplasma_dgeqrf(ctx, A, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");
+  CHECK(dplasma_dgelqf(ctx, A, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");
   dplasma_desc_destroy(A);
   if (argc > 1 && atoi(argv[1]) > 0) bench(ctx, atoi(argv[1]));
   CHECK(dplasma_python_active() == 0, "the interpreter was started");

@@ -97,6 +97,11 @@ NATIVE = {
     "getrf_1d": "A, IPIV",
     "getrs": "trans, A, IPIV, B",
     "gesv_1d": "A, IPIV, B",
+    "geqrf": "A, T",
+    "unmqr": "side, trans, A, T, C",
+    "ungqr": "A, T, Q",
+    "geqrs": "A, T, B",
+    "gels": "trans, A, T, B",
 }
 
 
