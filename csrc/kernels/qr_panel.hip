@@ -120,6 +120,7 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
       const int j = b0 + jj;
       const int par = nsync & 1;
       const int sh = QP_B - jj;  // live slots: slot s is column jj + s
+      QP_TICK(7);
       {
         // x = A(r > j, j) against every live column, then a wave transpose-reduction:
         // lane l ends with the wave's sum for slot l >> 1

@@ -10,7 +10,8 @@ import torch  # noqa: E402
 from dplasma_amd.ops import _lib  # noqa: E402
 from dplasma_amd.ops import tile_ops as ops  # noqa: E402
 
-NAMES = ["col compute", "col barrier", "col reduce", "Y partials", "Y barriers+sum", "trailing upd", "T coupling"]
+NAMES = ["col dots+reduce", "col barrier", "col reduce", "Y partials", "Y barriers+sum", "trailing upd", "T coupling",
+         "dlarfg+update+block"]
 
 
 def main():
