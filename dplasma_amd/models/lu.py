@@ -29,6 +29,7 @@ from ..constants import (DPLASMA_ERR_NOT_SUPPORTED, dplasmaLeft, dplasmaLower, d
                          dplasmaRight, dplasmaTrans, dplasmaConjTrans, dplasmaUnit, dplasmaUpper)
 from ..descriptor import TiledMatrix
 from ..ops import tile_ops as ops
+from ..ops import lu_dist_ops
 from ..ops.batch import GemmBatch, TileBatch
 import torch.distributed as dist
 
@@ -156,17 +157,16 @@ class _GetrfDev:
     PANEL(k+1) needs only NEXT(k), so with look-ahead (DPLASMA_LU_LOOKAHEAD=1) the next panel
     factorisation overlaps REST(k) -- the reference's lookahead through priorities.  Panel buffers alternate with k's parity (REST(k) still reads panel k).
 
-    Panel modes for P > 1 (``DPLASMA_LU_PANEL``): "gather" (default, below) or "percol" -- the
-    reference's distributed pivoting: each process row factors only its own panel rows, each
-    column's pivot comes from one all-gather of the P local candidates (|value|, row, candidate row,
-    current diagonal row: GETRF_MAX + RDC), the two rows of an interchange are replaced in place
-    (SND), and the trailing row moves travel only between the process rows involved.
-
-    Why the panel travels whole by default: partial pivoting identical to one process needs, per column, a
-    max-reduction over the process column followed by the pivot row; done as collectives that is
-    NB dependent RCCL calls per panel (512 x ~15 us = 7.7 ms at NB = 512) against ~1 ms to move a
-    64k x 512 panel once over xGMI, so the panel is gathered once and factored redundantly by
-    every process row of the column (same pivots everywhere, no further panel traffic)."""
+    Panel modes for P > 1 (``DPLASMA_LU_PANEL``):
+      "dist" (default) -- the reference's distributed pivoting on the GPUs (ops.lu_dist_ops): each
+               process row keeps its own panel rows plus a replica of the diagonal tile rows, and
+               every column's pivot is chosen inside the persistent panel kernel through one
+               cross-process hand-off (IPC-mapped exchange buffers over xGMI, epoch flags): O(NB^2)
+               elements per rank and panel instead of the whole panel, no host round trip;
+      "gather" -- the panel's process column all-gathers the tall panel and every process row
+               factors it redundantly (one collective per panel, O(M NB / P) elements per rank);
+      "percol" -- the distributed pivoting driven from the host (one all-gather and two host
+               syncs per column; kept as the transport-independent reference of "dist")."""
 
     def __init__(self, ctx, A, info, pivot: bool = True):
         self.ctx, self.A, self.info = ctx, A, info
@@ -185,6 +185,17 @@ class _GetrfDev:
         self.piv_dev = torch.zeros(nb, dtype=torch.int32, device=dev)
         self.ipiv_all = torch.zeros(max(1, min(A.m, A.n)), dtype=torch.int32, device=dev)
         self.ws = ops.lu_workspace(A.m, dev)
+        self.panel_mode = os.environ.get("DPLASMA_LU_PANEL", "dist")
+        if self.panel_mode not in ("dist", "gather", "percol"):
+            raise ValueError(f"DPLASMA_LU_PANEL={self.panel_mode!r}: expected dist, gather or percol")
+        self.percol = self.panel_mode == "percol" and g.P > 1 and pivot
+        self.dist = self.panel_mode == "dist" and g.P > 1 and pivot and A.mb == A.nb
+        self.xc = None
+        if self.dist:
+            # exchange buffers of my process column (every rank of the column creates them together)
+            self.xc = lu_dist_ops.PanelXchg(ctx.col_group, A.myrow, g.P, nb, A.dtype, dev)
+            self.dws = lu_dist_ops.dist_workspace(nb, dev)
+            self.tbuf = torch.zeros(max(1, mb * nb), dtype=A.dtype, device=dev)
         self.cnt = torch.zeros(1, dtype=torch.int32, device=dev)
         # move lists double-buffered by step parity: step k+2 must not overwrite the lists the
         # side stream is still applying to the left (already factored) columns of step k
@@ -226,7 +237,7 @@ class _GetrfDev:
         self.ubuf = torch.zeros(max(1, nb * max(ncol_loc, 1)), dtype=A.dtype, device=dev)
         # P > 1: per-step panel gather buffer [P][maxrows x nb] (every process row's panel tiles)
         self.gbuf = None
-        if g.P > 1:
+        if g.P > 1 and not self.dist and not self.percol:
             maxrows = 0
             for k in range(self.kt):
                 for q in range(g.P):
@@ -239,10 +250,6 @@ class _GetrfDev:
         # row keeps its own panel rows, every column's pivot is chosen by one small all-gather of the
         # local candidates (value, row, candidate row, current diagonal row) and only the two rows of
         # an interchange move; O(NB (NB + P)) elements per panel instead of O(M NB / P)
-        self.panel_mode = os.environ.get("DPLASMA_LU_PANEL", "gather")
-        if self.panel_mode not in ("gather", "percol"):
-            raise ValueError(f"DPLASMA_LU_PANEL={self.panel_mode!r}: expected gather or percol")
-        self.percol = self.panel_mode == "percol" and g.P > 1 and pivot
         self.plan = [self._build(k) for k in range(self.kt)]
         self.bytes_panel = [0] * self.kt   # elements this rank sends per step (panel exchange)
         if self.percol:
@@ -259,7 +266,36 @@ class _GetrfDev:
         st = {"kb": kb, "r0": r0, "mp": mp, "kmin": min(mp, kb)}
         g = A.grid
         st["pv"] = self.pbufs[k % len(self.pbufs)]
-        if A.col_is_local(k):
+        # panel buffer layout: row offset of tile row m's L(m, k) and the buffer's leading dimension
+        if self.dist:
+            # [T: replica of the diagonal tile rows][my own tiles below it]
+            tr = A.tile_rows(k)
+            own = [m for m in range(k + 1, A.mt) if A.row_is_local(m)]
+            lay, r, lrel = {k: 0}, tr, []
+            for m in own:
+                lay[m] = r
+                lrel.extend(range((m - k) * mb, (m - k) * mb + A.tile_rows(m)))
+                r += A.tile_rows(m)
+            st["pld"], st["tr"] = r, tr
+        else:
+            lay = {m: (m - k) * mb for m in range(k, A.mt)}
+            st["pld"] = mp
+        if A.col_is_local(k) and self.dist:
+            diag = A.row_is_local(k)
+            tb, back = TileBatch(), TileBatch()
+            for m in ([k] if diag else []) + own:
+                tb.add(A.offset(m, k), A.tile_rows(m), kb, b_off=lay[m])
+                back.add(lay[m], A.tile_rows(m), kb, b_off=A.offset(m, k))
+            st["gather"], st["back"] = tb.finalize(), back.finalize()
+            if diag:
+                st["tpack"] = TileBatch().add(A.offset(k, k), tr, kb, b_off=0).finalize()
+            else:
+                st["tunpack"] = TileBatch().add(0, tr, kb, b_off=0).finalize()
+            st["plu"] = lu_dist_ops.DistPanelLU(st["pv"], r, r, kb, tr, diag, lrel)
+            st["kmin"] = min(st["kmin"], tr)
+            self.bytes_panel_plan = getattr(self, "bytes_panel_plan", {})
+            self.bytes_panel_plan[k] = st["kmin"] * (2 + kb) * (g.P - 1)
+        elif A.col_is_local(k):
             mine = [m for m in range(k, A.mt) if A.row_is_local(m)]
             if mine:
                 tb, back = TileBatch(), TileBatch()
@@ -267,7 +303,7 @@ class _GetrfDev:
                     tb.add(A.offset(m, k), A.tile_rows(m), kb, b_off=(m - k) * mb)
                     back.add((m - k) * mb, A.tile_rows(m), kb, b_off=A.offset(m, k))
                 st["gather"], st["back"] = tb.finalize(), back.finalize()
-            if g.P > 1:
+            if g.P > 1 and self.gbuf is not None:
                 # pack my panel tiles into my slot of the gather buffer, unpack every slot into the panel
                 gm, slot = self.gmax, g.P
                 pack, unpack = TileBatch(), TileBatch()
@@ -335,7 +371,7 @@ class _GetrfDev:
                 for n in trail:
                     for m in rows:
                         (nxt if n == k + 1 else rest).add(A.offset(m, n), A.tile_rows(m), A.tile_cols(n),
-                                                          [((m - k) * mb, uoff[n], kb)])
+                                                          [(lay[m], uoff[n], kb)])
                 st["gemm_next"] = nxt.finalize() if len(nxt) else None
                 st["gemm_rest"] = rest.finalize() if len(rest) else None
         return st
@@ -353,9 +389,11 @@ class _GetrfDev:
         st = self.plan[k]
         kb, r0, mp, kmin = st["kb"], st["r0"], st["mp"], st["kmin"]
         pc = g.pcol(k + A.jt0)
-        pv = st["pv"][: mp * kb]
+        pv = st["pv"][: st["pld"] * kb]
         # --- gather the panel in its process column (each process row sends only its own tiles)
-        if A.col_is_local(k) and self.percol:
+        if A.col_is_local(k) and self.dist:
+            self._panel_dist(k)
+        elif A.col_is_local(k) and self.percol:
             self._panel_percol(k)
         elif A.col_is_local(k):
             if g.P > 1:
@@ -382,6 +420,31 @@ class _GetrfDev:
         if self.tmp is not None:   # net moves of this step's interchanges (lists double-buffered by parity)
             par = k & 1
             ops.piv_moves(self.piv_dev, kmin, self.mdst[par], self.msrc[par], self.mcnt[par])
+
+    def _panel_dist(self, k):
+        """Distributed partial pivoting of panel k on the GPUs of its process column (see panel_mode):
+        the diagonal tile is replicated down the column, then every rank factors its (T + own rows)
+        buffer with the exchange kernel; the pivots come out identical on every rank."""
+        A, ctx = self.A, self.ctx
+        g = A.grid
+        st = self.plan[k]
+        kb, tr, pld = st["kb"], st["tr"], st["pld"]
+        pv = st["pv"]
+        ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, pv, pld, st["gather"], copy=True)
+        tb = self.tbuf[: tr * kb]
+        if "tpack" in st:
+            ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, tb, tr, st["tpack"], copy=True)
+        comm.bcast(tb, g.rank(g.prow(k + A.it0), A.mycol), ctx.col_group)
+        if "tunpack" in st:
+            ops.geadd(0, N_, 1.0, tb, tr, 0.0, pv, pld, st["tunpack"], copy=True)
+        st["plu"].run(self.piv_dev, self.dws, self.cnt, self.info, st["r0"], self.xc)
+        self.bytes_panel[k] = self.bytes_panel_plan[k]
+
+    def close(self):
+        """Release the exchange buffers (every rank, after the last run)."""
+        if self.xc is not None:
+            self.xc.close()
+            self.xc = None
 
     def _panel_percol(self, k):
         """Distributed partial pivoting of panel k inside its process column (see panel_mode)."""
@@ -447,8 +510,8 @@ class _GetrfDev:
         A, ctx = self.A, self.ctx
         g = A.grid
         st = self.plan[k]
-        kb, r0, mp = st["kb"], st["r0"], st["mp"]
-        pv = st["pv"][: mp * kb]
+        kb, r0, mp, pld = st["kb"], st["r0"], st["mp"], st["pld"]
+        pv = st["pv"][: pld * kb]
         # --- row interchanges on every local column (the panel column is rewritten below)
         if not self.pivot:
             pass
@@ -497,12 +560,12 @@ class _GetrfDev:
                         cur.wait_event(e)
                 self.ev_side = [None, None]
         if "back" in st:
-            ops.geadd(0, N_, 1.0, pv, mp, 0.0, A.data, A.ld, st["back"], copy=True)
+            ops.geadd(0, N_, 1.0, pv, pld, 0.0, A.data, A.ld, st["back"], copy=True)
         # --- U block row where it lives, then down the process column
         if not st["trail"]:
             return
         if "trsm" in st:
-            ops.trsm(dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, pv, mp, A.data, A.ld, st["trsm"])
+            ops.trsm(dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, pv, pld, A.data, A.ld, st["trsm"])
         if "ulen" not in st:
             return
         ub = self.ubuf
@@ -515,7 +578,7 @@ class _GetrfDev:
         st = self.plan[k]
         gb = st.get(key)
         if gb is not None:   # trailing update A(m, n) -= L(m, k) U(k, n)
-            ops.gemm(N_, N_, -1.0, st["pv"], st["mp"], self.ubuf, st["kb"], 1.0, self.A.data, self.A.ld, gb)
+            ops.gemm(N_, N_, -1.0, st["pv"], st["pld"], self.ubuf, st["kb"], 1.0, self.A.data, self.A.ld, gb)
 
     def next(self, k):
         self._update(k, "gemm_next")
@@ -646,6 +709,7 @@ def getrf_ptgpanel_New(ctx, A, IPIV, info_out=None):
             info_out[0] = r
         return r
     tp.on_complete(_done)
+    tp.on_destruct(st.close)
     tp.ipiv_all = st.ipiv_all
     return tp.finish_build()
 
@@ -681,6 +745,7 @@ def getrf_1d_New(ctx, A, IPIV, info_out=None):
             info_out[0] = r
         return r
     tp.on_complete(_done)
+    tp.on_destruct(st.close)
     tp.ipiv_all = st.ipiv_all
     return tp.finish_build()
 

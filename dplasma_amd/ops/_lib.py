@@ -101,6 +101,17 @@ _SIGS = {
     "dpl_delay": [ctypes.c_double, c_int, c_vp],
     "dpl_ipiv_shift": [c_vp, c_vp, c_int, c_int, c_vp],
     "dpl_gemm_set_wg_cap": [c_int],
+    # distributed pivoting panel (lu_dist.hip): prec, A, ld, m, c0, cend, kbw, tr, diag, lrel, ipiv, ws, cnt,
+    # peers, P, me, slot_bytes, epoch0, info, info_base, stream
+    "dpl_lu_block_dist": [c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
+                          c_int, c_int, c_int, c_int, c_vp, c_int, c_vp],
+    "dpl_lu_dist_ws_bytes": [c_int],
+    "dpl_lu_dist_slot_bytes": [c_int, c_int],
+    "dpl_xchg_alloc": [c_ll, c_vp, c_vp],
+    "dpl_xchg_open": [c_vp, c_vp],
+    "dpl_xchg_close": [c_vp],
+    "dpl_xchg_free": [c_vp],
+    "dpl_ipc_handle_bytes": [],
     "dpl_rows_permute": [c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp,
                          c_int, c_vp],
 }

@@ -65,6 +65,7 @@ class Taskpool:
         self.tasks: List[Task] = []
         self.flops = 0.0
         self._on_complete: List[Callable] = []
+        self._on_destruct: List[Callable] = []
         self._result = None
         self.t_enq = time.perf_counter()
         self.t_prog = None
@@ -88,6 +89,10 @@ class Taskpool:
 
     def on_complete(self, fn: Callable):
         self._on_complete.append(fn)
+
+    def on_destruct(self, fn: Callable):
+        """Release hook of resources shared with other ranks (called by every rank from destruct)."""
+        self._on_destruct.append(fn)
 
     def finish_build(self):
         self.t_enq = time.perf_counter() - self.t_enq
@@ -196,5 +201,8 @@ class Taskpool:
         return self._result
 
     def destruct(self):
+        for fn in self.__dict__.get("_on_destruct", []):
+            fn()
+        self._on_destruct = []
         self.tasks = []
         self._on_complete = []

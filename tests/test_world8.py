@@ -84,6 +84,8 @@ def test_gemm_summa_2x4_lookahead(la):
 
 
 def _getrf_w(rank, world, N, NB):
+    import os
+    os.environ["DPLASMA_LU_PANEL"] = "gather"
     import dplasma_amd as dp
     ctx = dp.init(device="cpu", P=2)
     A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
@@ -125,6 +127,12 @@ def test_getrf_ptgpanel_2x4():
 def _getrf_percol_w(rank, world, N, NB, P, prec):
     import os
     os.environ["DPLASMA_LU_PANEL"] = "percol"
+    return _getrf_prec_w(rank, world, N, NB, P, prec)
+
+
+def _getrf_dist_w(rank, world, N, NB, P, prec):
+    import os
+    os.environ["DPLASMA_LU_PANEL"] = "dist"
     return _getrf_prec_w(rank, world, N, NB, P, prec)
 
 
@@ -172,3 +180,32 @@ def test_getrf_ptgpanel_percol(world, P, prec):
             assert max(sent) == NB * (2 + 2 * NB), (k, sent)          # per column: value, row, 2 rows
             if N - k * NB > P * (2 * NB + 2):                        # tall panels: less than gathering
                 assert max(sent) < (N - k * NB) * NB // P
+
+
+@pytest.mark.parametrize("world,P,prec", [(2, 2, "d"), (4, 2, "d"), (8, 4, "d"), (4, 4, "z"), (3, 3, "s"), (2, 1, "d")])
+def test_getrf_ptgpanel_dist(world, P, prec):
+    """Default P > 1 panel (ops.lu_dist_ops, zgetrf_ptgpanel.jdf GETRF_MAX / RDC / SND): every process
+    row keeps its own panel rows plus a replica of the diagonal tile; each column's pivot and the
+    winner's whole row travel in one exchange of P candidates.  Pivots are identical to one process;
+    a rank sends kmin x (2 + NB) elements to each of its P - 1 peers per panel, independent of M."""
+    N, NB = 176, 16
+    out = run_distributed(_getrf_dist_w, world, N, NB, P, prec)
+    import dplasma_amd as dp
+    ctx = dp.Context(device="cpu")
+    A = dp.block_cyclic(ctx, dp.PREC_DTYPE[prec], NB, NB, N, N)
+    dp.plrnt(ctx, A, 3872)
+    IP = dp.ipiv_descriptor(ctx, A)
+    assert dp.getrf_1d(ctx, A, IP) == 0
+    from dplasma_amd.models.lu import _gather_ipiv
+    piv1 = _gather_ipiv(ctx, IP)
+    full = sum(out[r][1] for r in range(world))
+    for r in range(world):
+        assert out[r][0] == 0
+        assert np.array_equal(out[r][2], piv1)
+    tol = 1e-3 if prec in ("s", "c") else 1e-10
+    assert (full - A.to_dense_local()).abs().max() < tol
+    if P > 1:
+        Q = world // P
+        for k in range(N // NB):
+            sent = [out[r][3][k] for r in range(world) if out[r][4] == k % Q]
+            assert max(sent) == NB * (2 + NB) * (P - 1), (k, sent)
