@@ -96,6 +96,7 @@ def gemm_New(ctx, transA, transB, alpha, A, B, beta, C, c_mask=None, kc=None, na
     mats = [A, B]
     bufs = []
     prev_gemm = {}
+    plans = []
     for s in range(nchunks):
         ks = list(range(s * kc, min(kt, (s + 1) * kc)))
         needs = {}
@@ -124,14 +125,17 @@ def gemm_New(ctx, transA, transB, alpha, A, B, beta, C, c_mask=None, kc=None, na
                   for k in ks]
             gb.add(C.offset(m, n), C.tile_rows(m), C.tile_cols(n), kp, c_mask(m, n) if c_mask else 0)
         gb.finalize()
-        t_ex = tp.task(f"EXCH({s})", "panel", lambda plan=plan, buf=buf: plan.run(buf), [prev_gemm.get(s - nbuf)],
-                       prio=2)
+        plans.append(plan)
+        # one send slab for every chunk: the exchanges are issued in order on the panel stream
+        t_ex = tp.task(f"EXCH({s})", "panel", lambda plan=plan, buf=buf: plan.run(buf, tp._sendbuf),
+                       [prev_gemm.get(s - nbuf)], prio=2)
         b_eff = beta if s == 0 else 1.0
         prev_gemm[s] = tp.task(
             f"GEMM({s})", "update",
             lambda gb=gb, buf=buf, b_eff=b_eff, plan=plan: ops.gemm(transA, transB, alpha, buf, plan.ld, buf, plan.ld, b_eff,
                                                           C.data, C.ld, gb), [t_ex], prio=1)
     tp._buffers = bufs
+    tp._sendbuf = torch.empty(max([p.nsend for p in plans] + [1]) * plans[0].nbe, dtype=C.dtype, device=C.device)
     return tp.finish_build()
 
 

@@ -101,6 +101,37 @@ def test_gemm_summa(world, P, ta, tb):
     assert (full - ref).abs().max() < 1e-12
 
 
+def _summa_traffic_worker(rank, world, P):
+    import dplasma_amd as dp
+    from dplasma_amd.parallel.exchange import ExchangePlan
+    ctx = dp.init(device="cpu", P=P)
+    A = dp.block_cyclic(ctx, torch.float64, 8, 8, 64, 64)
+    needs = {r: [(0, m, n) for m in range(8) for n in range(8)] for r in range(world)}   # everyone needs all
+    plan = ExchangePlan(ctx, [A], needs, torch.float64, A.device)
+    dp.plrnt(ctx, A, 11)
+    buf = plan.new_recv_buffer()
+    plan.run(buf)
+    own = len(list(A.local_tiles()))
+    # no tile is sent to myself; my own tiles sit after the remote ones, copied straight from A
+    ok = plan.send_counts[ctx.rank] == 0 and plan.recv_counts[ctx.rank] == 0 and plan.nsend == own * (world - 1)
+    ok = ok and plan.nremote == 64 - own
+    got = torch.stack([buf[plan.offset(0, m, n): plan.offset(0, m, n) + 64] for m in range(8) for n in range(8)])
+    return ok, got
+
+
+def test_exchange_plan_no_self_traffic():
+    """SUMMA / redistribution exchange: locally owned tiles never enter the send slab or the all-to-all."""
+    out = run_distributed(_summa_traffic_worker, 4, 2)
+    import dplasma_amd as dp
+    ctx = dp.Context(device="cpu")
+    A = dp.block_cyclic(ctx, torch.float64, 8, 8, 64, 64)
+    dp.plrnt(ctx, A, 11)
+    ref = torch.stack([A.tile(m, n).T.reshape(-1) for m in range(8) for n in range(8)])
+    for r in range(4):
+        assert out[r][0]
+        assert torch.equal(out[r][1], ref)
+
+
 def _norm_worker(rank, world, P):
     import dplasma_amd as dp
     ctx = dp.init(device="cpu", P=P)
