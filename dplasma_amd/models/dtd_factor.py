@@ -23,6 +23,12 @@ from .dtd_potrf import _blocking_New, _info_reducer
 # ----------------------------------------------------------------------------- QR
 def _insert_geqrf(tp, A, T):
     """Flat-tree tile QR (zgeqrf.jdf task classes) as DTD tasks on A and T (ib x nb tiles)."""
+    for _ in _geqrf_steps(tp, A, T):
+        pass
+
+
+def _geqrf_steps(tp, A, T):
+    """Generator form of _insert_geqrf (yields after every inserted task)."""
     kd = qr_ops.kinds(A.dtype, T.mb, qr_ops.view_flags(A.dtype, False), qr_ops.view_flags(A.dtype, False))
     tc = {k: tp.task_class(k, kind=kd[k]) for k in ("geqrt", "unmqr_h", "tsqrt", "tsmqr_h")}
     Tl = dtd.tile_of
@@ -30,19 +36,23 @@ def _insert_geqrf(tp, A, T):
     for k in range(min(A.mt, A.nt)):
         ck, rk = A.tile_cols(k), A.tile_rows(k)
         tp.insert_task(tc["geqrt"], (Tl(A, k, k), InOut | Aff), (Tl(T, k, k), InOut), (rk, ck, 0))
+        yield
         for n in range(k + 1, A.nt):
             # roles C, V, T
             tp.insert_task(tc["unmqr_h"], (Tl(A, k, n), InOut | Aff), (Tl(A, k, k), In), (Tl(T, k, k), In),
                            (rk, A.tile_cols(n), min(rk, ck)))
+            yield
         for m in range(k + 1, A.mt):
             rm = A.tile_rows(m)
             # roles A1, A2, T -- executed where A2 (the killed tile) lives
             tp.insert_task(tc["tsqrt"], (Tl(A, k, k), InOut), (Tl(A, m, k), InOut | Aff), (Tl(T, m, k), InOut),
                            (rm, ck, 0))
+            yield
             for n in range(k + 1, A.nt):
                 # roles A1, A2, V, T
                 tp.insert_task(tc["tsmqr_h"], (Tl(A, k, n), InOut), (Tl(A, m, n), InOut | Aff), (Tl(A, m, k), In),
                                (Tl(T, m, k), In), (rm, A.tile_cols(n), ck))
+                yield
         tp.data_flush(Tl(A, k, k))
     T.full_T = {}   # per-tile T factors (the stacked-domain engine's kept factors do not describe T)
     T.qr_format = "tile"
@@ -69,18 +79,17 @@ def geqrf_dtd(ctx, A, T, window=None):
 
 
 def geqrf_dtd_untied(ctx, A, T, window=None):
-    """Untied variant (tests/testing_zgeqrf_dtd_untied.c): one inserted task inserts the whole QR into the
-    taskpool it runs in (single process)."""
-    if ctx.world > 1:
-        raise NotImplementedError("untied DTD insertion needs a single process")
+    """Untied variant (tests/testing_zgeqrf_dtd_untied.c): one inserted task without data runs on every
+    rank and inserts the whole QR into the taskpool it runs in (AGAIN when the window is nearly full)."""
+    from .dtd_potrf import untied_inserter
     _check_qr(A, T)
     tp = dtd.taskpool_new(ctx, "geqrf_dtd_untied", window=window)
     tp.flops = flops(A.prec, "geqrf", A.m, A.n)
 
-    def inserter(a00):
-        _insert_geqrf(tp, A, T)
-    tp.insert_task(tp.task_class("insert_tasks", inserter), (dtd.tile_of(A, 0, 0), dtd.INPUT))
-    tp.data_flush()
+    def steps():
+        yield from _geqrf_steps(tp, A, T)
+    margin = min(1000, max(1, int(min(tp.window, 1 << 30)) // 4))
+    tp.insert_task(tp.task_class("insert_tasks", untied_inserter(tp, steps(), margin)))
     tp.wait()
     geqrf_dtd_untied.last = tp
     return 0

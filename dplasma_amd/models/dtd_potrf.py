@@ -54,6 +54,13 @@ def _gemm_body(ta, tb_, alpha, beta, mask):
 
 def _insert_potrf(tp, uplo, A, info):
     """The tile Cholesky as DTD tasks, with the reference's flushes (testing_zpotrf_dtd_untied.c)."""
+    for _ in _potrf_steps(tp, uplo, A, info):
+        pass
+
+
+def _potrf_steps(tp, uplo, A, info):
+    """Generator form of _insert_potrf: yields after every inserted task (the untied inserter stops
+    and resumes between any two insertions)."""
     bases = [k * A.mb for k in range(A.mt)]
     ct = dplasmaConjTrans if A.dtype.is_complex else dplasmaTrans
     potrf = tp.task_class("potrf", _potrf_body(uplo, info, bases))
@@ -72,25 +79,31 @@ def _insert_potrf(tp, uplo, A, info):
     # to the end, the panel first
     for k in range(A.mt):
         tp.insert_task(potrf, (T(A, k, k), InOut | Aff), k, priority=(total - k) ** 3)
+        yield
         for m in range(k + 1, A.mt):
             pr = (total - m) ** 3 + 3 * (2 * total - k - m - 1) * (m - k)
             if uplo == dplasmaLower:
                 tp.insert_task(trsm, (T(A, k, k), In), (T(A, m, k), InOut | Aff), priority=pr)
             else:
                 tp.insert_task(trsm, (T(A, k, k), In), (T(A, k, m), InOut | Aff), priority=pr)
+            yield
         tp.data_flush(T(A, k, k))
         for m in range(k + 1, A.mt):
             pr = (total - m) ** 3 + 3 * (m - k)
             if uplo == dplasmaLower:
                 tp.insert_task(herk, (T(A, m, k), In), (T(A, m, k), In), (T(A, m, m), InOut | Aff), priority=pr)
+                yield
                 for n in range(k + 1, m):
                     tp.insert_task(gemm, (T(A, m, k), In), (T(A, n, k), In), (T(A, m, n), InOut | Aff),
                                    priority=(total - m) ** 3 + 3 * (2 * total - m - n - 3) * (m - n) + 6 * (m - k))
+                    yield
             else:
                 tp.insert_task(herk, (T(A, k, m), In), (T(A, k, m), In), (T(A, m, m), InOut | Aff), priority=pr)
+                yield
                 for n in range(k + 1, m):
                     tp.insert_task(gemm, (T(A, k, n), In), (T(A, k, m), In), (T(A, n, m), InOut | Aff),
                                    priority=(total - m) ** 3 + 3 * (2 * total - m - n - 3) * (m - n) + 6 * (m - k))
+                    yield
             tp.data_flush(T(A, m, k) if uplo == dplasmaLower else T(A, k, m))
     tp.flops = flops(A.prec, "potrf", A.m)
     tp.data_flush_all(A)
@@ -131,19 +144,30 @@ def potrf_dtd(ctx, uplo, A, window=None):
     return r
 
 
+def untied_inserter(tp, steps, margin: int = 1000):
+    """Body of the reference's untied inserter task (testing_zpotrf_dtd_untied.c:140-145): insert from
+    the ``steps`` generator; once the window is nearly full, return AGAIN so the runtime launches what
+    was inserted and calls the body again (the generator resumes where it stopped)."""
+    lim = max(1, int(min(tp.window, 1 << 30)) - margin) if tp.window != float("inf") else None
+
+    def body():
+        for _ in steps:
+            if lim is not None and tp.pending >= lim:
+                return dtd.AGAIN
+        return None
+    return body
+
+
 def potrf_dtd_untied(ctx, uplo, A, window=None):
-    """The reference's untied variant (tests/testing_zpotrf_dtd_untied.c): ONE task is inserted, and
-    its body inserts the whole Cholesky into the taskpool it runs in (single process)."""
-    if ctx.world > 1:
-        raise NotImplementedError("untied DTD insertion needs a single process")
+    """The reference's untied variant (tests/testing_zpotrf_dtd_untied.c): ONE task without data is
+    inserted; it runs on every rank and its body inserts the whole Cholesky into the taskpool it runs
+    in, returning AGAIN whenever the window is nearly full."""
     info = torch.zeros(1, dtype=torch.int32, device=A.device)
     tp = dtd.taskpool_new(ctx, "potrf_dtd_untied", window=window)
     tp.on_complete(_info_reducer(ctx, info))
-
-    def inserter(a00):
-        _insert_potrf(tp, uplo, A, info)
-    tp.insert_task(tp.task_class("insert_tasks", inserter), (dtd.tile_of(A, 0, 0), dtd.INPUT))
-    tp.data_flush()
+    margin = min(1000, max(1, int(min(tp.window, 1 << 30)) // 4))
+    tp.insert_task(tp.task_class("insert_task_lower" if uplo == dplasmaLower else "insert_task_upper",
+                                 untied_inserter(tp, _potrf_steps(tp, uplo, A, info), margin)))
     r = tp.wait()
     potrf_dtd_untied.last = tp
     return r

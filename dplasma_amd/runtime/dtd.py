@@ -27,7 +27,14 @@ back at its home, and the remote copies of windows older than the last two are
 released (``parsec_dtd_data_flush``: the bound on memory).  Bodies may insert
 further tasks into the taskpool they run in ("untied" tasks,
 ``tests/testing_zpotrf_dtd_untied.c``): those land after everything inserted
-so far and run in a later window (single process).
+so far and run in a later window.  A task WITHOUT tile arguments has no data to
+follow, so -- as in PaRSEC -- it runs on every rank where it is inserted, at once
+(``insert_task`` calls its body); its insertions are therefore identical on every
+rank and untied insertion works on any number of processes.  A body that returns
+:data:`AGAIN` (``PARSEC_HOOK_RETURN_AGAIN``) is called again after the tasks it
+inserted so far have been launched -- the reference inserter's way of bounding the
+window.  Tile-carrying bodies that insert tasks run only on their executing rank,
+so they are limited to one process.
 
 A task class may instead provide a batched ``Kind`` (``task_class(kind=...)``):
 then all ready tasks of that class in a level become one kernel launch.
@@ -47,6 +54,7 @@ AFFINITY = 8       # flag OR-ed into a tile argument: run the task where this ti
 VALUE = 16         # scalar passed by value (wrapper marker; plain Python values are values too)
 SCRATCH = 32       # temporary passed by value (the body allocates it)
 PUSHOUT = 64       # accepted for API parity: tiles are always written back to their home
+AGAIN = "PARSEC_HOOK_RETURN_AGAIN"   # body return value: call me again once my insertions are launched
 
 
 @dataclass(frozen=True)
@@ -129,7 +137,8 @@ class DTDTaskpool:
         are ready together (one DAG level), higher priorities issue first (the stream -- critical path
         or bulk -- still follows the task's slack in the DAG)."""
         if self._running and self.ctx.world > 1:
-            raise RuntimeError("DTD: inserting from a task body is supported on a single process")
+            raise RuntimeError("DTD: a task with tile arguments inserts only on its executing rank; insert from "
+                               "a task without tiles (it runs on every rank) on more than one process")
         tc = fn if isinstance(fn, TaskClass) else TaskClass(name or getattr(fn, "__name__", "task"), fn)
         tiles, modes, values = [], [], []
         affinity = None
@@ -150,7 +159,10 @@ class DTDTaskpool:
             else:
                 values.append(a)
         if not tiles:
-            raise ValueError("a DTD task needs at least one tile argument")
+            if tc.kind is not None or tc.body is None:
+                raise ValueError("a DTD task without tile arguments needs a Python body")
+            self._run_local(tc, values)
+            return
         if affinity is None:
             written = [i for i, md in enumerate(modes) if md & 2]
             affinity = written[0] if written else 0
@@ -168,6 +180,15 @@ class DTDTaskpool:
         self.pending += 1
         self.flops += flops
         if self.pending >= self.window and not self._running:
+            self._launch()
+
+    def _run_local(self, tc: TaskClass, values):
+        """A task without data: run its body here, on every rank (AGAIN: launch what it inserted, then
+        call it again)."""
+        self.ntasks += 1
+        while tc.body(*values) == AGAIN:
+            if self.window == float("inf"):
+                continue      # deferred taskpool: nothing runs before compile(); keep inserting
             self._launch()
 
     # ------------------------------------------------------------------ execution

@@ -114,6 +114,57 @@ def test_potrf_dtd_distributed(world, P, window):
     assert rel_err(torch.tril(sum(out[r][1] for r in range(world))), L) < 1e-12
 
 
+def _untied_worker(rank, world, P, uplo, window):
+    import dplasma_amd as dp
+    from dplasma_amd.models.dtd_potrf import potrf_dtd_untied
+    ctx = dp.init(device="cpu", P=P)
+    A = dp.block_cyclic(ctx, torch.float64, 16, 16, 70, 70)
+    dp.plghe(ctx, 70.0, dp.dplasmaUpperLower, A, 3)
+    info = potrf_dtd_untied(ctx, uplo, A, window=window)
+    return info, A.to_dense_local(), potrf_dtd_untied.last.windows_run
+
+
+@pytest.mark.parametrize("world,P,uplo,window", [(2, 2, 122, 12), (4, 2, 121, 20), (4, 1, 122, None)])
+def test_potrf_dtd_untied_distributed(world, P, uplo, window):
+    """testing_zpotrf_dtd_untied.c on several processes: the inserter task has no data, runs on every rank
+    and returns AGAIN whenever the window is nearly full; every rank inserts the same tasks."""
+    out = run_distributed(_untied_worker, world, P, uplo, window)
+    ctx = dp.init(device="cpu")
+    A = dp.block_cyclic(ctx, torch.float64, 16, 16, 70, 70)
+    dp.plghe(ctx, 70.0, dp.dplasmaUpperLower, A, 3)
+    L = torch.linalg.cholesky(A.to_dense_local())
+    assert all(out[r][0] == 0 for r in range(world))
+    full = sum(out[r][1] for r in range(world))
+    got = torch.tril(full) if uplo == 122 else torch.triu(full).T
+    assert rel_err(got, L) < 1e-12
+    if window:
+        assert all(out[r][2] > 3 for r in range(world))   # AGAIN re-entered the inserter several times
+
+
+def test_dtd_dataless_task_runs_everywhere_with_again(ctx):
+    """A task without tile arguments runs where it is inserted; AGAIN calls it again after a launch."""
+    from dplasma_amd.runtime import dtd
+    tp = dtd.taskpool_new(ctx, "t", window=4)
+    A = dp.block_cyclic(ctx, torch.float64, 4, 4, 16, 16)
+    calls = []
+
+    def inc(a):
+        a.add_(1.0)
+
+    def inserter(state):
+        calls.append(tp.windows_run)
+        while state[0] < 10:
+            tp.insert_task(inc, (dtd.tile_of(A, state[0] % 4, 0), dtd.INOUT))
+            state[0] += 1
+            if tp.pending >= 3:
+                return dtd.AGAIN
+        return None
+    tp.insert_task(tp.task_class("ins", inserter), [0])
+    tp.wait()
+    assert len(calls) == 4 and calls[0] == 0 and calls[-1] >= 3
+    assert float(A.tile(0, 0).sum()) == 3 * 16 and float(A.tile(1, 0).sum()) == 3 * 16
+
+
 @pytest.mark.gpu
 def test_gpu_potrf_dtd():
     g = dp.init(device="cuda:0")
