@@ -25,6 +25,7 @@ from ..constants import (dplasmaConjTrans, dplasmaLeft, dplasmaLower, dplasmaNoT
 from ..ops import qr_ops
 from ..ops import tile_ops as ops
 from ..ops.batch import TileBatch
+from ..runtime import capped
 from ..runtime.dag import TileDAG
 from ..runtime.taskpool import Taskpool
 from ..utils.flops import flops
@@ -165,7 +166,7 @@ def geqrf_New(ctx, A, T) -> Taskpool:
     _check_square_tiles(A)
     _check_T(A, T)
     flat = qrtree.FlatTree(A.mt, A.nt)
-    if qr_panel.usable(A, flat):
+    if qr_panel.usable(A, flat) and not capped.wanted(ctx, [A, T]):
         return qr_panel.factor_New(ctx, A, T, T, flat, "geqrf")
     T.full_T = {}   # tile engine: the panel engine's kept T factors no longer describe T
     T.qr_format = "tile"
@@ -372,7 +373,7 @@ def geqrf_param_New(ctx, tree, A, TS, TT) -> Taskpool:
     _check_T(A, TS)
     _check_T(A, TT)
     _check_tree(A, tree, False)
-    if qr_panel.usable(A, tree):
+    if qr_panel.usable(A, tree) and not capped.wanted(ctx, [A, TS, TT]):
         return qr_panel.factor_New(ctx, A, TS, TT, tree, "geqrf_param")
     TS.full_T, TT.full_T = {}, {}   # tile engine: drop the panel engine's kept T factors
     TS.qr_format = TT.qr_format = "tile"

@@ -367,6 +367,10 @@ class TileDAG:
         else:
             level = rt.dag_levels(ops, modes) if rt is not None else _levels_py(ops, modes)
         nlev = int(level.max()) + 1
+        from . import capped
+        if capped.wanted(ctx, self.mats):
+            # host-resident operands (or an explicit arena cap): bounded device tile arena, LRU
+            return capped.compile_capped(self, tp, ops, modes, kid, ext, pyargs_all, level, DAG_ITEM)
         dot = getattr(ctx, "dot_file", None)
         if dot and me == 0:
             self._write_dot(dot, ops, modes, kid, level)
