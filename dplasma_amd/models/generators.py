@@ -8,9 +8,11 @@ factors from geqrf/unmqr).  Type codes: ``src/include/dplasma/constants.h:163-20
 Every generator is a function of the GLOBAL element indices (and of the 64-bit
 LCG stream for the random-vector based ones), so the result is identical for
 any tiling or process grid -- the property the reference gets from
-``Rnd64_jump`` (``src/cores/random.h:20-41``).  Tiles are evaluated on the host
-(these are test-matrix utilities, not compute kernels) and copied to their
-owner's device.
+``Rnd64_jump`` (``src/cores/random.h:20-41``).  Formulas are evaluated on the
+matrix's own device, one local tile column at a time (all its local tiles
+stacked); the random base of Demmel / Langou comes from the GPU LCG generator
+(plrnt) and the O(N) random vectors of the vector-based types are generated once
+and moved to the device -- nothing is assembled on the host.
 """
 from __future__ import annotations
 
@@ -128,11 +130,12 @@ def _formula(t, dtype, gM, gN, I, J, seed, cache):
         v = torch.where(I == J, diag, torch.where(I == J - 1, sup, torch.where(I == J + 1, sub,
                                                                                  torch.zeros_like(If))))
         return v.to(cd)
+    dev = I.device
     if t == dplasmaMatrixCompan:
         if "compan" not in cache:
             r = _rand_vec(dtype, gN, seed, row=True)
             v0 = _rand_block(dtype, 1, 0, 0, 1, 1, seed)[0, 0]
-            cache["compan"] = r / v0
+            cache["compan"] = (r / v0).to(dev)
         r = cache["compan"]
         v = torch.where(I == J + 1, torch.ones_like(If), torch.zeros_like(If)).to(cd)
         first = r[J.clamp(max=gN - 1)]
@@ -149,14 +152,18 @@ def _formula(t, dtype, gM, gN, I, J, seed, cache):
         sel = (J >= mn // 4) & (J < mn // 2) & (I >= J)
         return torch.where(sel, base * eps, base)
     if t == dplasmaMatrixCircul:
-        v = cache.setdefault("vec", _rand_vec(dtype, gN, seed))
-        return v[(J - I) % gN]
+        if "vec" not in cache:
+            cache["vec"] = _rand_vec(dtype, gN, seed).to(dev)
+        return cache["vec"][(J - I) % gN]
     if t == dplasmaMatrixFiedler:
-        v = cache.setdefault("vec", _rand_vec(dtype, max(gM, gN), seed))
+        if "vec" not in cache:
+            cache["vec"] = _rand_vec(dtype, max(gM, gN), seed).to(dev)
+        v = cache["vec"]
         return (v[I] - v[J]).abs().to(cd)
     if t == dplasmaMatrixHankel:
-        v = cache.setdefault("vec", _rand_vec(dtype, gM + gN, seed))
-        return v[I + J]
+        if "vec" not in cache:
+            cache["vec"] = _rand_vec(dtype, gM + gN, seed).to(dev)
+        return cache["vec"][I + J]
     if t == dplasmaMatrixChebvand:
         step = 1.0 / (gN - 1.0) if gN > 1 else 0.0
         p = Jf * step
@@ -171,14 +178,22 @@ def _formula(t, dtype, gM, gN, I, J, seed, cache):
         return out.to(cd)
     if t == dplasmaMatrixToeppd:
         if "toeppd" not in cache:
-            W = _rand_block(dtype, 2, 0, 0, 2, gM, seed).real
-            cache["toeppd"] = (W[0] + 0.5, 2 * math.pi * (W[1] + 0.5))
-        w, th = cache["toeppd"]
-        d = (If - Jf).reshape(-1, 1)
-        v = (w.reshape(1, -1) * torch.cos(th.reshape(1, -1) * d)).sum(1).reshape(If.shape)
-        return v.to(cd)
+            # A(i, j) = t(i - j) = sum_k w_k cos(theta_k (i - j)): the 2N - 1 values once, in chunks
+            W = _rand_block(dtype, 2, 0, 0, 2, gM, seed).real.to(dev)
+            w, th = W[0] + 0.5, 2 * math.pi * (W[1] + 0.5)
+            n = max(gM, gN)
+            d = torch.arange(-(n - 1), n, dtype=torch.float64, device=dev)
+            tv = torch.empty_like(d)
+            step = max(1, (1 << 24) // max(1, gM))
+            for a in range(0, len(d), step):
+                tv[a:a + step] = (w.view(1, -1) * torch.cos(th.view(1, -1) * d[a:a + step].view(-1, 1))).sum(1)
+            cache["toeppd"] = (tv, n - 1)
+        tv, z = cache["toeppd"]
+        return tv[(I - J) + z].to(cd)
     if t == dplasmaMatrixHouse:
-        v = cache.setdefault("vec", _rand_vec(dtype, gM, seed))
+        if "vec" not in cache:
+            cache["vec"] = _rand_vec(dtype, gM, seed).to(dev)
+        v = cache["vec"]
         tau = 2.0 / float((v.abs() ** 2).sum())
         return torch.where(I == J, torch.ones_like(If), torch.zeros_like(If)).to(cd) - tau * v[I] * v[J].conj()
     if t == dplasmaMatrixCondex:
@@ -190,7 +205,7 @@ def _formula(t, dtype, gM, gN, I, J, seed, cache):
             i = torch.arange(n, dtype=torch.float64)
             X[:, 2] = ((-1.0) ** i) * (1.0 + i / max(gN - 1, 1))
             Q, _ = torch.linalg.qr(X)
-            cache["condex"] = Q
+            cache["condex"] = Q.to(dev)
         Q = cache["condex"]
         theta = 100.0
         return torch.where(I == J, torch.full_like(If, 1.0 + theta), torch.zeros_like(If)).to(cd) - \
@@ -210,21 +225,34 @@ def pltmg(ctx, mtxtype: int, A, seed: int = 3872):
         return -2
     gM, gN = A.m, A.n
     cache = {}
+    dev = A.device
+    if mtxtype in (dplasmaMatrixDemmel, dplasmaMatrixLangou):
+        plrnt(ctx, A, seed)          # the random base, by the GPU LCG generator, transformed in place
 
     def rand(I, J):
-        i0, j0 = int(I.min()), int(J.min())
-        blk = _rand_block(A.dtype, gM, i0, j0, int(I.max()) - i0 + 1, int(J.max()) - j0 + 1, seed)
-        return blk[I - i0, J - j0]
+        return cache["base"]
     cache["rand"] = rand
+    bycol = {}
     for (m, n) in A.local_tiles():
-        r0, c0 = m * A.mb, n * A.nb
-        rows, cols = A.tile_rows(m), A.tile_cols(n)
-        I = torch.arange(r0, r0 + rows).view(-1, 1).expand(rows, cols)
-        J = torch.arange(c0, c0 + cols).view(1, -1).expand(rows, cols)
+        bycol.setdefault(n, []).append(m)
+    for n, ms in sorted(bycol.items()):
+        # every local tile of tile column n at once: rows stacked, one formula evaluation
+        c0, cols = n * A.nb, A.tile_cols(n)
+        rows = torch.cat([torch.arange(m * A.mb, m * A.mb + A.tile_rows(m), device=dev) for m in ms])
+        I = rows.view(-1, 1).expand(len(rows), cols)
+        J = torch.arange(c0, c0 + cols, device=dev).view(1, -1).expand(len(rows), cols)
+        if "rand" in cache and mtxtype in (dplasmaMatrixDemmel, dplasmaMatrixLangou):
+            cache["base"] = torch.cat([A.tile(m, n) for m in ms]).to(torch.complex128 if A.dtype.is_complex
+                                                                      else torch.float64)
         vals = _formula(mtxtype, A.dtype, gM, gN, I, J, seed, cache)
         if not A.dtype.is_complex and vals.is_complex():
             vals = vals.real
-        A.tile(m, n).copy_(vals.to(A.dtype).to(A.device))
+        vals = vals.to(A.dtype)
+        r = 0
+        for m in ms:
+            h = A.tile_rows(m)
+            A.tile(m, n).copy_(vals[r:r + h])
+            r += h
     if ctx.is_gpu:
         torch.cuda.synchronize(A.device)
     return 0

@@ -95,3 +95,16 @@ def test_generators_distributed(ctx):
     dp.pltmg(ctx, dp.dplasmaMatrixFiedler, A, 4)
     assert rel_err(sum(out[r][0] for r in range(4)), A.to_dense_local()) < 1e-15
     assert abs(out[0][1] - float(torch.linalg.matrix_norm(A.to_dense_local(), 2))) < 1e-6 * out[0][1]
+
+
+@pytest.mark.gpu
+def test_pltmg_gpu_matches_cpu():
+    """pltmg evaluated on the GPU (device formulas, GPU LCG base) equals the CPU evaluation."""
+    cg, cc = dp.init(device="cuda:0"), dp.init(device="cpu")
+    for t in range(43):
+        A = dp.block_cyclic(cg, torch.float64, 16, 16, 72, 72)
+        B = dp.block_cyclic(cc, torch.float64, 16, 16, 72, 72)
+        r1, r2 = dp.pltmg(cg, t, A, 5), dp.pltmg(cc, t, B, 5)
+        assert r1 == r2
+        if r1 == 0:
+            assert (A.to_dense_local().cpu() - B.to_dense_local()).abs().max() < 1e-10, t
