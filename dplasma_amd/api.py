@@ -229,13 +229,19 @@ for _n in ("hetrd", "hetrd_h2b_New", "hetrd_b2s"):
 
 
 def _setrecursive(tp, hnb):
-    """dplasma_z{potrf,geqrf}_setrecursive(tp, hnb): split large tile tasks into sub-taskpools of
-    hnb x hnb tiles (reference parsec_recursivecall, src/zpotrf_L.jdf:148-172).  POTRF runs each
-    diagonal-tile factorisation as a recursive potrf_New on the re-tiled tile (models/potrf.py
-    _recursive_potrf).  QR keeps its panel kernels: the stacked-domain engine factors a whole
-    panel per launch and the tile engine's GEQRT already blocks by IB (the T tile's mb), so the
-    hint is recorded on geqrf taskpools (``tp.recursive_nb``) without changing their schedule."""
+    """dplasma_z{potrf,geqrf}_setrecursive(tp, hnb): split large tile tasks into sub-tasks of hnb
+    (reference parsec_recursivecall, src/zpotrf_L.jdf:148-172, src/zgeqrf.jdf:126-509).  POTRF runs
+    its diagonal tile, panel TRSM and trailing updates as sub-taskpools on hnb x hnb re-tilings
+    (models/potrf.py).  GEQRF / GEQRF_PARAM taskpools are rebuilt in place as the tile engine with
+    recursive task bodies: every GEQRT / TSQRT / UNMQR / TSMQR on hnb-wide column blocks of its tiles
+    (models/qr.py _factor_rec; hnb rounded to a multiple of IB)."""
     tp.recursive_nb = int(hnb)
+    build = getattr(tp, "_rec_build", None)
+    if build is not None and 0 < int(hnb):
+        new = build(int(hnb))
+        keep = tp.name
+        tp.__dict__.update(new.__dict__)
+        tp.name = keep
     return 0
 
 

@@ -107,6 +107,65 @@ def _factor(dag: TileDAG, X: _L, TS: _L, TT: _L, kd, tree, ks=None):
                         np.stack([X.rows(vm[ii]), X.cols(nn), np.full(len(ii), ck)], 1))
 
 
+def _factor_rec(dag: TileDAG, X: _L, TS: _L, TT: _L, kd, tree, hnb: int):
+    """_factor with the reference's RECURSIVE task bodies (src/zgeqrf.jdf:126,220,347,509, under
+    dplasma_zgeqrf_setrecursive): every tile task on tiles wider than ``hnb`` runs as sub-tasks on
+    hnb-wide column blocks of its tiles (zgeqrfr_geqrt / zgeqrfr_tsqrt / zgeqrfr_unmqr / zgeqrfr_tsmqr):
+
+      GEQRT(k)        block j: GEQRT of rows j.. x block j (T columns of block j), UNMQR of rows j..
+                      x the blocks right of it, with block j's reflectors;
+      TSQRT(m, k)     block j: TSQRT of the triangle (j, j) of the head tile over block j of the killed
+                      tile, TSMQR of the head rows j.. / killed tile columns right of block j;
+      UNMQR / TSMQR   independent updates of the hnb-wide column blocks of the updated tiles.
+
+    With hnb a multiple of IB (the T tile height) every sub-task computes exactly the reflectors and
+    T blocks of the whole-tile kernel.  TT kills (triangle on triangle) stay whole-tile tasks."""
+    MT, NT = X.mt, X.nt
+    z = np.zeros(2, dtype=np.int64)
+
+    def blocks(w):
+        return [(c, min(hnb, w - c)) for c in range(0, w, hnb)]
+
+    for k in range(min(MT, NT)):
+        ck = int(X.cols(k))
+        heads = [int(h) for h in tree.heads(k)]
+        ns = list(range(k + 1, NT))
+        for h in heads:
+            rk = int(X.rows(h))
+            for j0, w in blocks(min(ck, rk)):
+                dag.add(kd["geqrt"], [[X.keys(dag, h, k), TS.keys(dag, h, k)]], [[rk - j0, w, 0]],
+                        sub=[[[j0, j0], [0, j0]]])
+                if j0 + w < ck:
+                    dag.add(kd["unmqr_h"], [[X.keys(dag, h, k), X.keys(dag, h, k), TS.keys(dag, h, k)]],
+                            [[rk - j0, ck - j0 - w, min(rk - j0, w)]], sub=[[[j0, j0 + w], [j0, j0], [0, j0]]])
+            for n in ns:
+                cn = int(X.cols(n))
+                for c0, w in blocks(cn):
+                    dag.add(kd["unmqr_h"], [[X.keys(dag, h, n), X.keys(dag, h, k), TS.keys(dag, h, k)]],
+                            [[rk, w, min(rk, ck)]], sub=[[[0, c0], z, z]])
+        for cls, pv, vm in _runs(tree.kills(k)):
+            Tm = TS if cls == "ts" else TT
+            for p_, m_ in zip(pv.tolist(), vm.tolist()):
+                rm = int(X.rows(m_))
+                if cls == "ts":
+                    for j0, w in blocks(ck):
+                        dag.add(kd["tsqrt"], [[X.keys(dag, p_, k), X.keys(dag, m_, k), Tm.keys(dag, m_, k)]],
+                                [[rm, w, 0]], sub=[[[j0, j0], [0, j0], [0, j0]]])
+                        if j0 + w < ck:
+                            dag.add(kd["tsmqr_h"], [[X.keys(dag, p_, k), X.keys(dag, m_, k), X.keys(dag, m_, k),
+                                                     Tm.keys(dag, m_, k)]],
+                                    [[rm, ck - j0 - w, w]], sub=[[[j0, j0 + w], [0, j0 + w], [0, j0], [0, j0]]])
+                else:
+                    dag.add(kd["ttqrt"], [[X.keys(dag, p_, k), X.keys(dag, m_, k), Tm.keys(dag, m_, k)]],
+                            [[rm, ck, 0]])
+                for n in ns:
+                    cn = int(X.cols(n))
+                    for c0, w in blocks(cn):
+                        dag.add(kd[cls + "mqr_h"], [[X.keys(dag, p_, n), X.keys(dag, m_, n), X.keys(dag, m_, k),
+                                                     Tm.keys(dag, m_, k)]],
+                                [[rm, w, ck]], sub=[[[0, c0], [0, c0], z, z]])
+
+
 def _apply(dag: TileDAG, X: _L, TS: _L, TT: _L, C: _L, kd, conjtrans: bool, tree, K: int = None, ks=None,
            n0: int = 0):
     """C := Q^H C (conjtrans) or Q C, Q from _factor(X, tree) (zunmqr_L{C,N}[_param].jdf).
@@ -167,13 +226,31 @@ def geqrf_New(ctx, A, T) -> Taskpool:
     _check_T(A, T)
     flat = qrtree.FlatTree(A.mt, A.nt)
     if qr_panel.usable(A, flat) and not capped.wanted(ctx, [A, T]):
-        return qr_panel.factor_New(ctx, A, T, T, flat, "geqrf")
-    T.full_T = {}   # tile engine: the panel engine's kept T factors no longer describe T
-    T.qr_format = "tile"
-    dag = TileDAG(ctx, "geqrf")
-    _factor(dag, _L(A), _L(T), _L(T), _kinds(A, T, False), qrtree.FlatTree(A.mt, A.nt))
+        tp = qr_panel.factor_New(ctx, A, T, T, flat, "geqrf")
+    else:
+        T.full_T = {}   # tile engine: the panel engine's kept T factors no longer describe T
+        T.qr_format = "tile"
+        dag = TileDAG(ctx, "geqrf")
+        _factor(dag, _L(A), _L(T), _L(T), _kinds(A, T, False), qrtree.FlatTree(A.mt, A.nt))
+        dag.flops = flops(A.prec, "geqrf", A.m, A.n)
+        tp = dag.compile()
+    tp._rec_build = lambda hnb: _recursive_New(ctx, "geqrf", A, T, T, flat, hnb)
+    return tp
+
+
+def _recursive_New(ctx, name, A, TS, TT, tree, hnb):
+    """The tile-engine factorisation with recursive (hnb-wide column block) task bodies -- what
+    dplasma_zgeqrf_setrecursive turns a geqrf taskpool into (see _factor_rec)."""
+    ib = TS.mb
+    hnb = max(ib, (int(hnb) // ib) * ib)
+    TS.full_T, TT.full_T = {}, {}
+    TS.qr_format = TT.qr_format = "tile"
+    dag = TileDAG(ctx, name + "_rec")
+    _factor_rec(dag, _L(A), _L(TS), _L(TT), _kinds(A, TS, False), tree, hnb)
     dag.flops = flops(A.prec, "geqrf", A.m, A.n)
-    return dag.compile()
+    tp = dag.compile()
+    tp.recursive_nb = hnb
+    return tp
 
 
 def geqrf(ctx, A, T):
@@ -374,13 +451,16 @@ def geqrf_param_New(ctx, tree, A, TS, TT) -> Taskpool:
     _check_T(A, TT)
     _check_tree(A, tree, False)
     if qr_panel.usable(A, tree) and not capped.wanted(ctx, [A, TS, TT]):
-        return qr_panel.factor_New(ctx, A, TS, TT, tree, "geqrf_param")
-    TS.full_T, TT.full_T = {}, {}   # tile engine: drop the panel engine's kept T factors
-    TS.qr_format = TT.qr_format = "tile"
-    dag = TileDAG(ctx, "geqrf_param")
-    _factor(dag, _L(A), _L(TS), _L(TT), _kinds(A, TS, False), tree)
-    dag.flops = flops(A.prec, "geqrf", A.m, A.n)
-    return dag.compile()
+        tp = qr_panel.factor_New(ctx, A, TS, TT, tree, "geqrf_param")
+    else:
+        TS.full_T, TT.full_T = {}, {}   # tile engine: drop the panel engine's kept T factors
+        TS.qr_format = TT.qr_format = "tile"
+        dag = TileDAG(ctx, "geqrf_param")
+        _factor(dag, _L(A), _L(TS), _L(TT), _kinds(A, TS, False), tree)
+        dag.flops = flops(A.prec, "geqrf", A.m, A.n)
+        tp = dag.compile()
+    tp._rec_build = lambda hnb: _recursive_New(ctx, "geqrf_param", A, TS, TT, tree, hnb)
+    return tp
 
 
 def geqrf_param(ctx, tree, A, TS, TT):

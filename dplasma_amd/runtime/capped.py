@@ -59,7 +59,7 @@ def wanted(ctx, mats) -> bool:
     return ctx.is_gpu and any(M.data.device.type == "cpu" for M in mats)
 
 
-def compile_capped(dag, tp, ops, modes, kid, ext, pyargs_all, level, item_dtype):
+def compile_capped(dag, tp, ops, modes, kid, ext, pyargs_all, level, item_dtype, sub_all=None):
     """Fill ``tp`` with one task replaying the capped schedule of the DAG (see module docstring)."""
     from .dag import _MASK22, _M_SHIFT, _MID_SHIFT, _DagProgram
     ctx = dag.ctx
@@ -155,6 +155,8 @@ def compile_capped(dag, tp, ops, modes, kid, ext, pyargs_all, level, item_dtype)
                 M = mats[key >> _MID_SHIFT]
                 ar = arenas[M.dtype]
                 off = slot[key] * nbe_of[M.dtype]
+                if sub_all is not None:
+                    off += int(sub_all[t, r, 0]) + int(sub_all[t, r, 1]) * M.mb
                 seg[f"p{sl}"][i] = ar.data_ptr() + off * esz[M.dtype]
                 seg[f"ld{sl}"][i] = M.mb
                 refs.append((ar, off, M.mb))

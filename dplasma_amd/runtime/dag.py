@@ -192,6 +192,7 @@ class TileDAG:
         self.info = None
         self.no_dtd = False         # the DTD engine's own windows (never re-routed through DTD)
         self._has_prio = False      # some task carries a non-zero priority (add(prio=...))
+        self._subs = {}             # chunk index -> (n, R, 2) (row, col) origin of each operand in its tile
 
     # ------------------------------------------------------------ registration
     def mat(self, M) -> int:
@@ -216,13 +217,15 @@ class TileDAG:
             self.kinds.append(K)
         return self._kid[K.name]
 
-    def add(self, K: Kind, ops, ext, pyargs=None, prio=None):
+    def add(self, K: Kind, ops, ext, pyargs=None, prio=None, sub=None):
         """Append tasks of kind K in program order.
 
         ops: (n, len(K.roles)) tile keys (-1 for an unused optional role); ext: (n, 3) ints;
         pyargs: optional per-task tuples of Python values passed to a ``body`` kind; prio: optional
         per-task priorities (the DTD ``priority`` argument: higher first among the ready tasks of a
-        level, and on the high-priority stream when positive)."""
+        level, and on the high-priority stream when positive); sub: optional (n, R, 2) (row, col)
+        origins of the operands inside their tiles -- a task on a sub-block of its tiles (the
+        recursive incarnations); dependencies stay per tile."""
         ops = np.atleast_2d(np.asarray(ops, dtype=np.int64))
         ext = np.atleast_2d(np.asarray(ext, dtype=np.int32))
         if ops.size == 0:
@@ -236,6 +239,10 @@ class TileDAG:
             if prio.any():
                 self._has_prio = True
         kid = self.kind(K)
+        if sub is not None:
+            sub = np.broadcast_to(np.asarray(sub, dtype=np.int64), (ops.shape[0], ops.shape[1], 2)).copy()
+            if sub.any():
+                self._subs[len(self._chunks)] = sub
         self._chunks.append((kid, ops, ext, list(pyargs) if pyargs is not None else None, prio))
         if K.flops is not None:
             self.flops += float(K.flops(ext))
@@ -296,7 +303,7 @@ class TileDAG:
         are rediscovered by the DTD engine.  None when a task cannot be expressed (Python-body kinds
         or optional roles left empty): the graph then runs as built."""
         from . import dtd
-        if any(self.kinds[k].body is not None or (o < 0).any() for k, o, _, _, _ in self._chunks):
+        if self._subs or any(self.kinds[k].body is not None or (o < 0).any() for k, o, _, _, _ in self._chunks):
             return None
         dt = dtd.DTDTaskpool(self.ctx, self.name + "[ptg_to_dtd]", window=0)
         mask = (1 << 22) - 1
@@ -337,11 +344,14 @@ class TileDAG:
         ext = np.zeros((ntask, 3), dtype=np.int32)
         pyargs_all = None
         tprio = np.zeros(ntask, dtype=np.int64)
+        sub_all = np.zeros((ntask, nR, 2), dtype=np.int64) if self._subs else None
         p = 0
-        for k, o, e, pa, pr in self._chunks:
+        for ci, (k, o, e, pa, pr) in enumerate(self._chunks):
             n = len(o)
             K = self.kinds[k]
             ops[p:p + n, :o.shape[1]] = o
+            if ci in self._subs:
+                sub_all[p:p + n, :o.shape[1]] = self._subs[ci]
             for r, (_, md, _) in enumerate(K.roles):
                 modes[p:p + n, r] = np.where(o[:, r] >= 0, md, 0)
             kid[p:p + n] = k
@@ -354,6 +364,7 @@ class TileDAG:
                 pyargs_all[p:p + n] = pa
             p += n
         self._chunks = []
+        self._subs = {}
         names = [K.name for K in self.kinds]
         tp.simulation_date = lambda cost=None: simulation_date(ops, modes, kid, names, cost)
         rt = _lib_rt()
@@ -370,7 +381,7 @@ class TileDAG:
         from . import capped
         if capped.wanted(ctx, self.mats):
             # host-resident operands (or an explicit arena cap): bounded device tile arena, LRU
-            return capped.compile_capped(self, tp, ops, modes, kid, ext, pyargs_all, level, DAG_ITEM)
+            return capped.compile_capped(self, tp, ops, modes, kid, ext, pyargs_all, level, DAG_ITEM, sub_all)
         dot = getattr(ctx, "dot_file", None)
         if dot and me == 0:
             self._write_dot(dot, ops, modes, kid, level)
@@ -523,6 +534,8 @@ class TileDAG:
                 l = np.zeros(len(keys), dtype=np.int32)
                 if ok.any():
                     b[ok], o[ok], l[ok] = resolve(keys[ok])
+                    if sub_all is not None:   # sub-block operands: origin (row, col) inside the tile
+                        o[ok] += sub_all[mine_t, r, 0][ok] + sub_all[mine_t, r, 1][ok] * l[ok].astype(np.int64)
                 refs_all.append((b, o, l))
             gid_of_task = np.zeros(ntask, dtype=np.int64)
             for g, (s, e) in enumerate(zip(starts, ends)):

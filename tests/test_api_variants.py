@@ -63,3 +63,63 @@ def test_getrs_incpiv(ctx):
     assert rel_err(a @ B.to_dense_local(), b) < 1e-12
     with pytest.raises(ValueError):
         dp.dgetrs_incpiv(ctx, dp.dplasmaTrans, A, L, IP, B)
+
+
+@pytest.mark.parametrize("hnb", [4, 8, 12])
+def test_geqrf_setrecursive_tile_bodies(ctx, hnb):
+    """dplasma_zgeqrf_setrecursive: GEQRT / TSQRT / UNMQR / TSMQR run on hnb-wide column blocks of their
+    tiles (zgeqrf.jdf RECURSIVE bodies).  Same reflectors and T blocks as the whole-tile tasks."""
+    from dplasma_amd.models import qr
+    from dplasma_amd.runtime.dag import TileDAG
+    A = dp.block_cyclic(ctx, torch.float64, 16, 16, 80, 48)
+    dp.plrnt(ctx, A, 5)
+    a = A.to_dense_local().clone()
+    T = dp.block_cyclic(ctx, torch.float64, 4, 16, A.mt * 4, 48)
+    tp = dp.dgeqrf_New(ctx, A, T)
+    assert dp.dgeqrf_setrecursive(tp, hnb) == 0 and tp.recursive_nb == hnb
+    assert tp.dag.nlaunch > 20
+    tp.execute(ctx)
+    B = dp.block_cyclic(ctx, torch.float64, 16, 16, 80, 48)
+    dp.plrnt(ctx, B, 5)
+    T2 = dp.block_cyclic(ctx, torch.float64, 4, 16, B.mt * 4, 48)
+    dag = TileDAG(ctx, "geqrf")
+    qr._factor(dag, qr._L(B), qr._L(T2), qr._L(T2), qr._kinds(B, T2, False), qr.qrtree.FlatTree(B.mt, B.nt))
+    dag.compile().execute(ctx)
+    assert rel_err(A.to_dense_local(), B.to_dense_local()) < 1e-13
+    assert rel_err(T.to_dense_local(), T2.to_dense_local()) < 1e-13
+    Q = dp.block_cyclic(ctx, torch.float64, 16, 16, 80, 48)
+    dp.dungqr(ctx, A, T, Q)
+    assert rel_err(Q.to_dense_local() @ torch.triu(A.to_dense_local()[:48]), a) < 1e-13
+
+
+def test_geqrf_param_setrecursive(ctx):
+    """HQR (TS domains + TT tree) with recursive TS bodies: A = QR through ungqr_param."""
+    A = dp.block_cyclic(ctx, torch.float64, 16, 16, 96, 48)
+    dp.plrnt(ctx, A, 9)
+    a = A.to_dense_local().clone()
+    TS = dp.block_cyclic(ctx, torch.float64, 4, 16, A.mt * 4, 48)
+    TT = dp.block_cyclic(ctx, torch.float64, 4, 16, A.mt * 4, 48)
+    tree = dp.hqr_init(dp.dplasmaNoTrans, A, dp.dplasma_GREEDY_TREE, dp.dplasma_FLAT_TREE, 2, 1)
+    tp = dp.dgeqrf_param_New(ctx, tree, A, TS, TT)
+    dp.dgeqrf_setrecursive(tp, 8)
+    tp.execute(ctx)
+    Q = dp.block_cyclic(ctx, torch.float64, 16, 16, 96, 48)
+    dp.dungqr_param(ctx, tree, A, TS, TT, Q)
+    assert rel_err(Q.to_dense_local() @ torch.triu(A.to_dense_local()[:48]), a) < 1e-13
+
+
+@pytest.mark.gpu
+def test_geqrf_setrecursive_gpu():
+    """Recursive QR bodies on the GPU kernels (sub-block operands: item addresses offset inside tiles)."""
+    g = dp.init(device="cuda:0")
+    A = dp.block_cyclic(g, torch.float64, 128, 128, 640, 384)
+    dp.plrnt(g, A, 5)
+    a = A.to_dense_local().clone()
+    T = dp.block_cyclic(g, torch.float64, 32, 128, A.mt * 32, 384)
+    tp = dp.dgeqrf_New(g, A, T)
+    dp.dgeqrf_setrecursive(tp, 64)
+    tp.execute(g)
+    Q = dp.block_cyclic(g, torch.float64, 128, 128, 640, 384)
+    dp.dungqr(g, A, T, Q)
+    r = torch.triu(A.to_dense_local()[:384])
+    assert rel_err(Q.to_dense_local() @ r, a) < 1e-12
