@@ -456,6 +456,125 @@ __global__ __launch_bounds__(PLR) void k_lu_block_persist(T* __restrict__ A, int
   }
 }
 
+// ---------------------------------------------------------------- register-resident block LU
+// Same algorithm and hand-offs as k_lu_block_persist, but every thread keeps ITS ROW of the block in
+// registers (v[c], c < 64, the column loop fully unrolled so every index is static) instead of a
+// 128 KiB LDS tile.  A workgroup then needs ~2 KiB of LDS and <= 256 VGPRs per lane, so it can share
+// a CU with a trailing-update GEMM workgroup (72 KiB LDS, 256 VGPRs): with look-ahead the panel no
+// longer waits for whole CUs to drain of GEMM waves before its grid barrier can complete.
+template <typename T>
+__global__ __launch_bounds__(PLR) void k_lu_block_reg(T* __restrict__ A, int ld, int m, int c0, int cend, int R,
+                                                      int* __restrict__ ipiv, T* __restrict__ cand,
+                                                      double* __restrict__ pval, int* __restrict__ pidx,
+                                                      int* __restrict__ cnt, int* __restrict__ info, int info_base) {
+  __shared__ T prow[PBW], oldj[PBW];
+  __shared__ double sv[PLR / 64];
+  __shared__ int si[PLR / 64];
+  const int G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
+  const int BW = cend - c0;
+  const int rbase = c0 + w * R;
+  const int nr = max(0, min(R, m - rbase));
+  const int g = rbase + tid;
+  const bool own = tid < nr;
+  T v[PBW];
+#pragma unroll
+  for (int c = 0; c < PBW; ++c) v[c] = (own && c < BW) ? A[g + (long long)(c0 + c) * ld] : ST<T>::zero();
+#pragma clang loop unroll(full)
+  for (int cj = 0; cj < PBW; ++cj) {
+    if (cj < BW) {   // uniform; no break, so the loop unrolls and every v[] index is static
+    const int j = c0 + cj;
+    const int par = cj & 1;
+    // ---- 1. apply column cj-1 (pivot row in prow)
+    if (cj > 0 && own && g >= j) {
+      const T d = prow[cj - 1];
+      T l = v[cj - 1];
+      if (!is_zero(d)) l = divv(l, d);
+      v[cj - 1] = l;
+#pragma unroll
+      for (int c = cj; c < PBW; ++c)
+        if (c < BW) v[c] = sub(v[c], mul(l, prow[c]));
+    }
+    // ---- 2. workgroup |max| of column cj over rows >= j
+    double val = (own && g >= j) ? (double)abs1(v[cj]) : -1.0;
+    int vi = (own && g >= j) ? g : 0x7fffffff;
+    wave_argmax(val, vi);
+    if ((tid & 63) == 0) { sv[tid >> 6] = val; si[tid >> 6] = vi; }
+    __syncthreads();
+    double bv = sv[0];
+    int bi = si[0];
+#pragma unroll
+    for (int q = 1; q < PLR / 64; ++q)
+      if (sv[q] > bv || (sv[q] == bv && si[q] < bi)) { bv = sv[q]; bi = si[q]; }
+    if (tid == 0) {
+      st_sc1(&pval[par * G + w], bv);
+      st_sc1(&pidx[par * G + w], bi);
+    }
+    if (own && g == bi) {
+#pragma unroll
+      for (int c = 0; c < PBW; ++c)
+        if (c < BW) st_sc1(&cand[((long long)par * G + w) * PBW + c], v[c]);
+    }
+    if (own && g == j) {
+#pragma unroll
+      for (int c = 0; c < PBW; ++c)
+        if (c < BW) st_sc1(&cand[((long long)2 * G + par) * PBW + c], v[c]);
+    }
+    grid_sync_counter(cnt, (cj + 1) * G, info);
+    // ---- 3. global pivot (every workgroup reduces the same G candidates)
+    double best = -1.0;
+    int bix = 0x7fffffff;
+    for (int b = tid; b < G; b += PLR) {
+      const double pv_ = ld_sc1(&pval[par * G + b]);
+      const int pi_ = ld_sc1(&pidx[par * G + b]);
+      if (pv_ > best || (pv_ == best && pi_ < bix)) { best = pv_; bix = pi_; }
+    }
+    wave_argmax(best, bix);
+    if ((tid & 63) == 0) { sv[tid >> 6] = best; si[tid >> 6] = bix; }
+    __syncthreads();
+    best = sv[0];
+    bix = si[0];
+#pragma unroll
+    for (int q = 1; q < PLR / 64; ++q)
+      if (sv[q] > best || (sv[q] == best && si[q] < bix)) { best = sv[q]; bix = si[q]; }
+    const int p = bix, pw = (p - c0) / R;
+    if (tid < BW) {
+      prow[tid] = ld_sc1(&cand[((long long)par * G + pw) * PBW + tid]);
+      oldj[tid] = ld_sc1(&cand[((long long)2 * G + par) * PBW + tid]);
+    }
+    __syncthreads();
+    if (own && g == j) {
+#pragma unroll
+      for (int c = 0; c < PBW; ++c) v[c] = prow[c];
+    } else if (own && g == p) {
+#pragma unroll
+      for (int c = 0; c < PBW; ++c) v[c] = oldj[c];
+    }
+    if (w == 0 && tid == 0) {
+      ipiv[j] = p;
+      if (best == 0.0 && info) atomicCAS(info, 0, info_base + j + 1);
+    }
+    }
+  }
+  // ---- last column: scale below the diagonal, then the rows go home
+  if (own && g >= cend) {
+    const T d = prow[BW - 1];
+#pragma unroll
+    for (int c = 0; c < PBW; ++c)
+      if (c == BW - 1 && !is_zero(d)) v[c] = divv(v[c], d);
+  }
+#pragma unroll
+  for (int c = 0; c < PBW; ++c)
+    if (own && c < BW) A[g + (long long)(c0 + c) * ld] = v[c];
+}
+
+// block kernel choice for the pivoting persistent path: 1 = register-resident rows (default), 0 = LDS tile
+static int g_lu_kind = 1;
+DPL_API int dpl_lu_block_set_kind(int k) {
+  const int old = g_lu_kind;
+  g_lu_kind = k;
+  return old;
+}
+
 #define DISPATCH(prec, CALL)                                          \
   switch (prec) {                                                     \
     case DPL_S: { typedef float T; CALL; } break;                     \
@@ -566,7 +685,14 @@ DPL_API int dpl_lu_block(int prec, void* A, int ld, int m, int c0, int cend, int
       int* pidx = (int*)(b + 8LL * 2 * 256);
       void* cand = (void*)(b + 8LL * 2 * 256 + 4LL * 2 * 256 + 64);
       hipMemsetAsync(cnt, 0, sizeof(int), st);
-      if (prec == DPL_D)
+      if (g_lu_kind == 1) {
+        if (prec == DPL_D)
+          hipLaunchKernelGGL((k_lu_block_reg<double>), dim3(G), dim3(PLR), 0, st, (double*)A, ld, m, c0, cend, R,
+                             ipiv, (double*)cand, pval, pidx, cnt, info, info_base);
+        else
+          hipLaunchKernelGGL((k_lu_block_reg<float>), dim3(G), dim3(PLR), 0, st, (float*)A, ld, m, c0, cend, R,
+                             ipiv, (float*)cand, pval, pidx, cnt, info, info_base);
+      } else if (prec == DPL_D)
         hipLaunchKernelGGL((k_lu_block_persist<double>), dim3(G), dim3(PLR), 0, st, (double*)A, ld, m, c0, cend, R,
                            ipiv, (double*)cand, pval, pidx, cnt, info, info_base);
       else

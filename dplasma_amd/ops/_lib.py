@@ -101,6 +101,7 @@ _SIGS = {
     "dpl_delay": [ctypes.c_double, c_int, c_vp],
     "dpl_ipiv_shift": [c_vp, c_vp, c_int, c_int, c_vp],
     "dpl_gemm_set_wg_cap": [c_int],
+    "dpl_lu_block_set_kind": [c_int],   # pivoting block kernel: 1 register-resident rows, 0 LDS tile
     # distributed pivoting panel (lu_dist.hip): prec, A, ld, m, c0, cend, kbw, tr, diag, lrel, ipiv, ws, cnt,
     # peers, P, me, slot_bytes, epoch0, info, info_base, stream
     "dpl_lu_block_dist": [c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -148,6 +149,8 @@ def load(build_if_missing: bool = True):
             f.argtypes = args
             f.restype = c_int
         _LIB = _Declared(lib)
+        if os.environ.get("DPLASMA_LU_BLOCK", "reg") == "lds":
+            _LIB.dpl_lu_block_set_kind(0)
         return _LIB
 
 

@@ -4,7 +4,8 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 400 python -u -m pytest tests/test_capped.py tests/test_aux_extra.py tests/test_potrf_ooc.py -m gpu -x -v \
+timeout -k 10 500 python -u -m pytest tests/test_capped.py tests/test_aux_extra.py tests/test_potrf_ooc.py \
+    tests/test_api_variants.py tests/test_lu.py tests/test_lu_qr.py tests/test_gpu_lu_dist.py -m gpu -x -v \
     --timeout 180 --timeout-method thread > gpurun_out/b2_tests.log 2>&1
 rc=$?; grep -E "PASS|FAIL|ERROR|passed|failed" gpurun_out/b2_tests.log | tail -12; echo "tests rc=$rc"
 [ $rc -ne 0 ] && exit $rc
@@ -23,6 +24,12 @@ unset MASTER_ADDR MASTER_PORT WORLD_SIZE DPLASMA_DIST_BACKEND
 timeout -k 10 300 python -m dplasma_amd.testing getrf_qrf -N 16384 -t 512 -x > gpurun_out/b2_luqr.log 2>&1
 rc=$?; grep -E "TIME|SUCC|FAIL|Error" gpurun_out/b2_luqr.log | head -5; echo "getrf_qrf rc=$rc"
 [ $rc -ne 0 ] && exit $rc
+# partial-pivoting LU: register-resident vs LDS block kernel, with and without look-ahead
+for N in 32768 65536; do for K in reg lds; do for LA in 0 1; do
+  DPLASMA_LU_BLOCK=$K DPLASMA_LU_LOOKAHEAD=$LA timeout -k 10 200 python tools/bench_algo.py getrf_1d -N $N --nb 512 --runs 2 \
+      > gpurun_out/b2_lu_${N}_${K}_${LA}.log 2>&1 || { echo "lu $N $K $LA failed"; tail -5 gpurun_out/b2_lu_${N}_${K}_${LA}.log; exit 1; }
+  echo "N=$N block=$K lookahead=$LA: $(grep TIME gpurun_out/b2_lu_${N}_${K}_${LA}.log | tail -1 | cut -c1-150)"
+done; done; done
 timeout -k 10 120 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
     --master-port 29661 tools/gpu/rccl_same_gpu_probe.py > gpurun_out/b2_rccl_probe.log 2>&1
 echo "rccl probe rc=$?"; grep -h "RCCL_SAME_GPU" gpurun_out/b2_rccl_probe.log | head -4
