@@ -21,9 +21,15 @@ import torch
 import torch.distributed as dist
 
 
+def _nbytes(t: torch.Tensor) -> int:
+    return t.numel() * t.element_size()
+
+
 def bcast(t: torch.Tensor, src_global: int, group, world: bool = False) -> None:
     """Broadcast from global rank src_global over ``group`` (None: nothing to do -- unless ``world``,
     then over every rank)."""
+    if _BACKEND is not None and hasattr(_BACKEND, "sync"):
+        return _BACKEND.sync("bcast", _nbytes(t), group)
     if group is None and not world:
         return
     if world and not (dist.is_initialized() and dist.get_world_size() > 1):
@@ -38,6 +44,8 @@ def _nccl() -> bool:
 
 def allgather_inplace(out: torch.Tensor, my_index: int, group) -> None:
     """out is [n_in_group, ...] contiguous; slot my_index already holds my contribution."""
+    if _BACKEND is not None and hasattr(_BACKEND, "sync"):
+        return _BACKEND.sync("allgather", _nbytes(out) - _nbytes(out[my_index]), group)
     if group is None:
         return
     inp = out[my_index]
@@ -53,6 +61,8 @@ def allgather_inplace(out: torch.Tensor, my_index: int, group) -> None:
 
 
 def allreduce(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None) -> None:
+    if _BACKEND is not None and hasattr(_BACKEND, "sync"):
+        return _BACKEND.sync("allreduce", 2 * _nbytes(t), group)
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return
     dist.all_reduce(t, op=op, group=group)
@@ -66,6 +76,11 @@ def p2p(sends=(), recvs=()) -> None:
     sends, recvs = list(sends), list(recvs)
     if not sends and not recvs:
         return
+    if _BACKEND is not None and hasattr(_BACKEND, "sync"):
+        per = {}
+        for t_, p_ in sends + recvs:
+            per[p_] = per.get(p_, 0) + _nbytes(t_)
+        return _BACKEND.sync("p2p", max(per.values()), None)
     if _nccl():
         ops = [dist.P2POp(dist.isend, t, p) for t, p in sends] + [dist.P2POp(dist.irecv, t, p) for t, p in recvs]
         for w in dist.batch_isend_irecv(ops) or ():
@@ -95,8 +110,8 @@ _BACKEND = None   # replaces the torch.distributed transport (tools/replay_potrf
 
 
 def set_backend(b) -> None:
-    """Install a transport backend with ``start_p2p(sends, recvs, group, hint)`` / ``finish(p)``
-    (None: torch.distributed)."""
+    """Install a transport backend with ``start_p2p(sends, recvs, group, hint)`` / ``finish(p)`` and
+    optionally ``sync(kind, critical_bytes, group)`` for the blocking collectives (None: torch.distributed)."""
     global _BACKEND
     _BACKEND = b
 
@@ -182,6 +197,8 @@ def bcast_tri(dst: torch.Tensor, dst_off: int, src: Optional[torch.Tensor], src_
     UPPER_TILE arena shapes: half the bytes of the full tile).  The root reads its block from
     ``src[src_off]`` (leading dimension ld_src); every rank (root included) gets the triangle in
     ``dst[dst_off]`` (ld_dst); the rest of the destination block is not written."""
+    if _BACKEND is not None and hasattr(_BACKEND, "sync"):
+        return _BACKEND.sync("bcast", n * (n + 1) // 2 * dst.element_size(), group)
     if group is None:
         return
     nt = n * (n + 1) // 2

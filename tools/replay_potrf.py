@@ -131,6 +131,25 @@ class ReplayBackend:
         if p.meta is not None:
             torch.cuda.current_stream(self.dev).wait_event(p.meta)
 
+    def sync(self, kind, nbytes, group):
+        """A blocking collective / point-to-point exchange (bcast, allgather, allreduce, p2p): one delay
+        kernel of lat + critical-link bytes / bw on the group's communication stream, waited for by
+        the current stream (the data is not moved)."""
+        self.stats["sync_" + kind] = self.stats.get("sync_" + kind, 0) + 1
+        if self.dev.type != "cuda":
+            return
+        cur = torch.cuda.current_stream(self.dev)
+        gs = self._stream(group)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        gs.wait_event(ev)
+        us = self.lat + nbytes / self.bw
+        _lib.check(self.lib.dpl_delay(float(us), self.nwg, gs.cuda_stream), "delay")
+        end = torch.cuda.Event()
+        end.record(gs)
+        cur.wait_event(end)
+        self.stats["us"] += us
+
 
 def fake_rank_context(base, P, Q, rank):
     """The one-GPU context dressed as rank ``rank`` of a P x Q grid (no process group)."""
