@@ -46,7 +46,13 @@ def main():
     def timed(self, *a, **kw):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        orig(self, *a, **kw)
+        # no host synchronisation inside the panel: torch raises on any synchronizing call
+        # (.item(), .cpu(), blocking copies) while the panel's kernels are issued
+        torch.cuda.set_sync_debug_mode("error" if mode == "ipc" else "default")
+        try:
+            orig(self, *a, **kw)
+        finally:
+            torch.cuda.set_sync_debug_mode("default")
         e1.record()
         times.append((e0, e1, self.kf))
     lu_dist_ops.DistPanelLU.run = timed
@@ -78,6 +84,7 @@ def main():
     dist.all_reduce(flags, op=dist.ReduceOp.MIN)
     print(f"rank {ctx.rank}: lu dist {ctx.P}x{ctx.Q} N={N} NB={NB} exchange={mode}: {t:.3f} s, panels on this rank "
           f"{len(panel_ms)} ({sum(panel_ms):.2f} ms, {1e3 * sum(panel_ms) / max(1, ncol):.2f} us per column), "
+          f"no host sync inside a panel: {mode == 'ipc'}, "
           f"pivots identical to one process: {same}, max |factor diff| {diff:.2e} : "
           f"{'SUCCESS' if ok else 'FAIL'}", flush=True)
     dist.destroy_process_group()
