@@ -567,8 +567,11 @@ __global__ __launch_bounds__(PLR) void k_lu_block_reg(T* __restrict__ A, int ld,
     if (own && c < BW) A[g + (long long)(c0 + c) * ld] = v[c];
 }
 
-// block kernel choice for the pivoting persistent path: 1 = register-resident rows (default), 0 = LDS tile
-static int g_lu_kind = 1;
+// block kernel choice for the pivoting persistent path: 0 = LDS tile (default), 1 = register-resident rows.
+// Measured on one MI355X (profiles/r3_lu_block_reg.txt): the register variant is 30 % slower per column
+// (64 fully unrolled column steps: ~100 KiB of code per launch, instruction-cache bound) and look-ahead
+// does not recover it -- kept opt-in (DPLASMA_LU_BLOCK=reg) as the measured alternative.
+static int g_lu_kind = 0;
 DPL_API int dpl_lu_block_set_kind(int k) {
   const int old = g_lu_kind;
   g_lu_kind = k;

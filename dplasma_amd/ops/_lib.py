@@ -149,8 +149,9 @@ def load(build_if_missing: bool = True):
             f.argtypes = args
             f.restype = c_int
         _LIB = _Declared(lib)
-        if os.environ.get("DPLASMA_LU_BLOCK", "reg") == "lds":
-            _LIB.dpl_lu_block_set_kind(0)
+        # pivoting block kernel: LDS tile (default) or register-resident rows (DPLASMA_LU_BLOCK=reg,
+        # measured slower: profiles/r3_lu_block_reg.txt)
+        _LIB.dpl_lu_block_set_kind(1 if os.environ.get("DPLASMA_LU_BLOCK", "lds") == "reg" else 0)
         return _LIB
 
 

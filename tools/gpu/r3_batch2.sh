@@ -21,7 +21,7 @@ grep -h "^rank" gpurun_out/b2_lud_r0.log gpurun_out/b2_lud_r1.log; echo "lu dist
 [ $rc0 -ne 0 ] && exit $rc0
 unset MASTER_ADDR MASTER_PORT WORLD_SIZE DPLASMA_DIST_BACKEND
 # hybrid LU-QR (reference testing_zgetrf_qrf defaults) and LU variants on one GPU
-timeout -k 10 300 python -m dplasma_amd.testing getrf_qrf -N 16384 -t 512 -x > gpurun_out/b2_luqr.log 2>&1
+timeout -k 10 300 python -m dplasma_amd.testing dgetrf_qrf -N 16384 -t 512 -x > gpurun_out/b2_luqr.log 2>&1
 rc=$?; grep -E "TIME|SUCC|FAIL|Error" gpurun_out/b2_luqr.log | head -5; echo "getrf_qrf rc=$rc"
 [ $rc -ne 0 ] && exit $rc
 # partial-pivoting LU: register-resident vs LDS block kernel, with and without look-ahead
