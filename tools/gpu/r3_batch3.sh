@@ -4,11 +4,6 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-for N in 32768 65536; do for K in reg lds; do for LA in 0 1; do
-  DPLASMA_LU_BLOCK=$K DPLASMA_LU_LOOKAHEAD=$LA timeout -k 10 200 python tools/bench_algo.py getrf_1d -N $N --nb 512 --runs 2 \
-      > gpurun_out/b3_lu_${N}_${K}_${LA}.log 2>&1 || { echo "lu $N $K $LA failed"; tail -5 gpurun_out/b3_lu_${N}_${K}_${LA}.log; exit 1; }
-  echo "N=$N block=$K lookahead=$LA: $(grep TIME gpurun_out/b3_lu_${N}_${K}_${LA}.log | tail -1 | cut -c1-150)"
-done; done; done
 timeout -k 10 300 python -m dplasma_amd.testing dgetrf_qrf -N 16384 -t 512 -x > gpurun_out/b3_luqr.log 2>&1
 rc=$?; grep -E "TIME|SUCC|FAIL|Error" gpurun_out/b3_luqr.log | head -5; echo "getrf_qrf rc=$rc"
 [ $rc -ne 0 ] && exit $rc
