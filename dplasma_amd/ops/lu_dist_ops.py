@@ -172,6 +172,13 @@ class DistPanelLU:
         self._rec(0, self.kf)
         if kb > self.kf:   # wide panel: the columns past the last pivot only get U = L^-1 A
             self.plan.append(("trsm", TileBatch().add(0, self.kf, kb - self.kf, b_off=self.kf * ld).finalize()))
+        if _is_gpu(buf):   # device item arrays now (the _New phase), not inside the first run
+            from .tile_ops import _trsm_groups
+            for op in self.plan:
+                if op[0] == "trsm":
+                    _trsm_groups(op[1], dplasmaLeft, buf)
+                elif op[0] == "gemm":
+                    op[1].device_arrays(buf.device)
 
     def _rec(self, c0: int, n: int):
         ld, m = self.ld, self.m

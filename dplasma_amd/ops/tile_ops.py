@@ -291,8 +291,16 @@ class _TrsmGroup:
         self.max_m = int(items["m"].max())
         self.max_n = int(items["n"].max())
         self.ntri = len(tris)
-        self.items_dev = torch.from_numpy(items.view(np.uint8).copy()).to(device)
-        self.tri_dev = torch.tensor(tris, dtype=torch.int64, device=device)
+        # pinned staging + asynchronous upload (kept alive with the group): building a group inside a
+        # running program must not synchronise the stream
+        dev = torch.device(device)
+        hi = torch.from_numpy(items.view(np.uint8).copy())
+        ht = torch.tensor(tris, dtype=torch.int64)
+        if dev.type == "cuda":
+            hi, ht = hi.pin_memory(), ht.pin_memory()
+        self._host = (hi, ht)
+        self.items_dev = hi.to(dev, non_blocking=True)
+        self.tri_dev = ht.to(dev, non_blocking=True)
         nJ = (npos + 15) // 16
         self.work = torch.empty(self.ntri * nJ * 256, dtype=dtype, device=device)
 
