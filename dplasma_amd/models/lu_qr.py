@@ -118,6 +118,7 @@ class _GetrfQrf(Taskpool):
         self.info_out = info
         self.p = p or A.grid.P
         self.kd = qr_ops.kinds(A.dtype, TS.mb, (0, 0), (0, 0))
+        self._panel_ws = {}
         self.flops = flops(A.prec, "getrf", A.m, A.n)
         if criteria == RANDOM_CRITERIUM:
             genrandom_lutab(self.lu_tab, 0, self.minMNT - 1, int(round(self.minMNT * self.alpha / 100.0)), 0)
@@ -138,7 +139,17 @@ class _GetrfQrf(Taskpool):
             colmax = A.tile(st.k, st.k)[:st.ncol, :st.ncol].abs().amax(0).double().cpu().numpy()
         ipiv = torch.zeros(max(st.kmax, 1), dtype=torch.int32, device=A.device)
         info = torch.zeros(1, dtype=torch.int32, device=A.device)
-        ops.getrf_panel(buf, 0, st.M, st.ncol, st.M, ipiv, info, 0, pivot=True)
+        if A.device.type == "cuda":
+            # the recursive device panel (persistent pivoting block kernels, TRSM / MFMA GEMM joins) --
+            # the same engine as getrf_1d's PANEL task, not a one-workgroup panel
+            key = (st.M, st.ncol)
+            ws = self._panel_ws.get(key)
+            if ws is None:
+                ws = self._panel_ws[key] = (ops.lu_workspace(st.M, A.device),
+                                            torch.zeros(1, dtype=torch.int32, device=A.device))
+            ops.PanelLU(buf, st.M, st.M, st.ncol, pivot=True).run(ipiv, ws[0], ws[1], info, 0)
+        else:
+            ops.getrf_panel(buf, 0, st.M, st.ncol, st.M, ipiv, info, 0, pivot=True)
         w0 = 0.0
         bad = int(info.item()) != 0
         if not bad and self.criteria in _HIGHAMS:
