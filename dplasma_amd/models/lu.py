@@ -630,16 +630,29 @@ def _permute_rows_2d(ctx, A, dst_rows, src_rows, coltiles):
     def off(r, n):
         return A.offset(r // mb, n) + r % mb
 
+    # element offset of (row r, tile column n) = off(r, n0) + colpart(n) - colpart(n0): both storages are
+    # affine in the local tile column index
+    from ..constants import STORAGE_TILE
+    cw = np.array([A.tile_cols(n) for n in coltiles], dtype=np.int64)
+    jl = np.array([A.lcol[n + A.jt0] for n in coltiles], dtype=np.int64)
+    colpart = jl * (A.llmt * A.mb * A.nb if A.storage == STORAGE_TILE else A.nb * A.ld)
+    colpart = colpart - (colpart[0] if len(colpart) else 0)
+
     def pairs(idx_rows, slot0, to_buf):
-        """(row_gather pairs per width group): slot j holds one tile row of nb elements."""
+        """(row_gather pairs per width group): slot j holds one tile row of nb elements (vectorised over
+        rows x tile columns)."""
+        rp = np.array([off(int(r), coltiles[0]) for r in idx_rows], dtype=np.int64)
+        j = np.arange(len(rp), dtype=np.int64)
+        slots = (slot0 + j[:, None] * nct + np.arange(nct, dtype=np.int64)[None, :]) * nb
+        offs = rp[:, None] + colpart[None, :]
         out = {}
-        for j, r in enumerate(idx_rows):
-            for c, n in enumerate(coltiles):
-                w = A.tile_cols(n)
-                slot = (slot0 + j * nct + c) * nb
-                pr = (slot, off(int(r), n)) if to_buf else (off(int(r), n), slot)
-                out.setdefault(w, []).append(pr)
-        return {w: np.array(v, dtype=ops.ROW_PAIR) for w, v in out.items()}
+        for w in np.unique(cw).tolist():
+            sel = np.broadcast_to(cw[None, :] == w, offs.shape)
+            a, b = (slots[sel], offs[sel]) if to_buf else (offs[sel], slots[sel])
+            pr = np.zeros(len(a), dtype=ops.ROW_PAIR)
+            pr[pr.dtype.names[0]], pr[pr.dtype.names[1]] = a, b
+            out[int(w)] = pr
+        return out
 
     dev, dt = A.device, A.dtype
     tmp = torch.empty(max(1, len(local) * nct) * nb, dtype=dt, device=dev)
