@@ -43,7 +43,8 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from ..constants import dplasmaLeft, dplasmaLower, dplasmaNoTrans, dplasmaNonUnit, dplasmaRight, dplasmaUnit, dplasmaUpper
+from ..constants import (dplasmaConjTrans, dplasmaLeft, dplasmaLower, dplasmaNoTrans, dplasmaNonUnit, dplasmaRight,
+                         dplasmaUnit, dplasmaUpper)
 from ..descriptor import TiledMatrix
 from ..ops import qr_ops
 from ..ops import tile_ops as ops
@@ -52,7 +53,7 @@ from ..runtime.dag import TileDAG
 from ..runtime.taskpool import Taskpool
 from ..runtime.tileprog import TileProgram
 from ..utils.flops import flops
-from . import qr, qrtree
+from . import qr, qr_panel, qrtree
 from .lu import _perm_from_swaps, _permute_rows_2d
 
 DEFAULT_CRITERIUM = 0
@@ -119,6 +120,15 @@ class _GetrfQrf(Taskpool):
         self.p = p or A.grid.P
         self.kd = qr_ops.kinds(A.dtype, TS.mb, (0, 0), (0, 0))
         self._panel_ws = {}
+        # QR steps on the stacked-domain engine (models/qr_panel.py: every TS domain of the step's tree
+        # one persistent panel launch, TT kills likewise, MFMA trailing updates) when it handles A and the
+        # tree; T factors then live in its ("panel") format and trsmpl_qrf applies them the same way
+        self.qpf = None
+        if qr_panel.usable(A, tree):
+            self.qpf = qr_panel._Factor(ctx, A, TS, TT, tree)
+            TS.qr_format = TT.qr_format = "panel"
+        else:
+            TS.qr_format = TT.qr_format = "tile"
         self.flops = flops(A.prec, "getrf", A.m, A.n)
         if criteria == RANDOM_CRITERIUM:
             genrandom_lutab(self.lu_tab, 0, self.minMNT - 1, int(round(self.minMNT * self.alpha / 100.0)), 0)
@@ -270,6 +280,18 @@ class _GetrfQrf(Taskpool):
         A, ctx, k = self.A, self.ctx, st.k
         if self.IPIV.is_local(k, k):
             self.IPIV.tile(k, k).zero_()
+        f = self.qpf
+        if f is not None:
+            if f.simple:
+                e = f.steps[k][0]
+                f.panel(k, e, 0)
+                f.apply(e, e.get("next"), 0, f.wn)
+                f.apply(e, e.get("rest"), 0, f.wr)
+            elif f.batched:
+                f.step_batched(k)
+            else:
+                f.step_general(k)
+            return
         dag = TileDAG(ctx, f"getrf_qrf_qr({k})")
         qr._factor(dag, qr._L(A), qr._L(self.TS), qr._L(self.TT), self.kd, self.tree, ks=[k])
         dag.compile().execute(ctx)
@@ -294,6 +316,8 @@ class _GetrfQrf(Taskpool):
     def complete(self, ctx=None):
         if self.ctx.is_gpu:
             torch.cuda.current_stream(self.ctx.device).synchronize()
+        if self.qpf is not None and int(self.qpf.info.item()) != 0:
+            raise RuntimeError(f"getrf_qrf: QR panel kernel reported {int(self.qpf.info.item())}")
         self._result = 0
         return 0
 
@@ -317,8 +341,18 @@ def trsmpl_qrf(ctx, qrtree_, A, IPIV, B, TS, TT, lu_tab, p=None):
     then solve with the upper triangle of A (trsm Left Upper NoTrans NonUnit) to get x."""
     p = p or A.grid.P
     kd = qr_ops.kinds(A.dtype, TS.mb, (0, 0), (0, 0))
+    ap = None
+    if getattr(TS, "qr_format", "tile") == "panel":
+        # QR steps factored by the stacked-domain engine: apply Q_k^H in its format, item by item
+        ap = qr_panel._Apply(ctx, dplasmaLeft, dplasmaConjTrans, A, TS, TT, B, qrtree_)
+        byk = {}
+        for it in ap.items:
+            byk.setdefault(it["k"], []).append(it)
     for k in range(min(A.mt, A.nt)):
-        if lu_tab[k]:
+        if not lu_tab[k] and ap is not None:
+            for it in byk.get(k, ()):
+                ap.run_item(it)
+        elif lu_tab[k]:
             st = _Step(A, k, p)
             piv = torch.zeros(A.mb, dtype=torch.float64)
             if IPIV.is_local(k, k):
