@@ -307,6 +307,11 @@ def fini(ctx: Optional[Context] = None):
     if c is not None and c.profiling is not None and path:
         c.profiling.dump(path if c.world == 1 else path)
     if c is not None:
+        # cached LU exchange buffers (ops.lu_dist_ops): every rank of each process column unmaps them
+        import sys
+        ld = sys.modules.get("dplasma_amd.ops.lu_dist_ops")
+        if ld is not None:
+            ld.release_all()
         c.release()
     if ctx is None or ctx is _DEFAULT:
         _DEFAULT = None

@@ -193,7 +193,7 @@ class _GetrfDev:
         self.xc = None
         if self.dist:
             # exchange buffers of my process column (every rank of the column creates them together)
-            self.xc = lu_dist_ops.PanelXchg(ctx.col_group, A.myrow, g.P, nb, A.dtype, dev)
+            self.xc = lu_dist_ops.panel_xchg(ctx.col_group, A.myrow, g.P, nb, A.dtype, dev)
             self.dws = lu_dist_ops.dist_workspace(nb, dev)
             self.tbuf = torch.zeros(max(1, mb * nb), dtype=A.dtype, device=dev)
         self.cnt = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -441,10 +441,8 @@ class _GetrfDev:
         self.bytes_panel[k] = self.bytes_panel_plan[k]
 
     def close(self):
-        """Release the exchange buffers (every rank, after the last run)."""
-        if self.xc is not None:
-            self.xc.close()
-            self.xc = None
+        """Drop this factorisation's reference to the (cached, re-used) exchange buffers."""
+        self.xc = None
 
     def _panel_percol(self, k):
         """Distributed partial pivoting of panel k inside its process column (see panel_mode)."""

@@ -111,6 +111,26 @@ class PanelXchg:
         self.ok = False
 
 
+_XCHG = {}
+
+
+def panel_xchg(group, me: int, P: int, kbw: int, dtype: torch.dtype, device) -> PanelXchg:
+    """The exchange buffers of a process column, created once per (group, width, dtype) and re-used by
+    every later factorisation (their epochs continue), so repeated LU runs neither re-export IPC
+    handles nor leak mappings.  ``release_all()`` frees them (collective over each column group)."""
+    key = (id(group), me, P, kbw, dtype, str(torch.device(device)))
+    xc = _XCHG.get(key)
+    if xc is None:
+        xc = _XCHG[key] = PanelXchg(group, me, P, kbw, dtype, device)
+    return xc
+
+
+def release_all():
+    """Unmap and free every cached exchange buffer (call on every rank, e.g. before fini)."""
+    for key in list(_XCHG):
+        _XCHG.pop(key).close()
+
+
 def _block_host(P, ld, m, c0, cend, kbw, tr, diag, pos, ipiv, info, info_base, xc: PanelXchg):
     """One block of the distributed panel through per-column all-gathers (same arithmetic as the
     one-process CPU lu_block restricted to the block columns, plus whole-row interchanges)."""
@@ -231,4 +251,4 @@ def kernel_ok(dtype: torch.dtype) -> bool:
     return dtype in (torch.float64, torch.float32)
 
 
-__all__ = ["PanelXchg", "DistPanelLU", "dist_workspace", "kernel_ok"]
+__all__ = ["PanelXchg", "DistPanelLU", "dist_workspace", "kernel_ok", "panel_xchg", "release_all"]
