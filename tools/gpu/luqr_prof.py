@@ -23,7 +23,7 @@ def main():
         TS = dp.block_cyclic(ctx, torch.float64, ib, NB, A.mt * ib, N)
         TT = dp.block_cyclic(ctx, torch.float64, ib, NB, A.mt * ib, N)
         IP = dp.qrf_ipiv_descriptor(ctx, A)
-        tree = dp.hqr_init(dp.dplasmaNoTrans, A, 1, 1, 1, 1, -1, 0)
+        tree = dp.hqr_init(dp.dplasmaNoTrans, A, 1, -1, -1, 1, -1, 0)   # the testing CLI's defaults
         lu_tab = [0] * A.mt
         tp = dp.getrf_qrf_New(ctx, tree, A, IP, TS, TT, 0, 1.0, lu_tab)
         torch.cuda.synchronize()
