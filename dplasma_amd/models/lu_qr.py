@@ -48,6 +48,7 @@ from ..constants import (dplasmaConjTrans, dplasmaLeft, dplasmaLower, dplasmaNoT
 from ..descriptor import TiledMatrix
 from ..ops import qr_ops
 from ..ops import tile_ops as ops
+from ..ops.batch import GemmBatch, TileBatch
 from ..parallel import comm
 from ..runtime.dag import TileDAG
 from ..runtime.taskpool import Taskpool
@@ -120,6 +121,8 @@ class _GetrfQrf(Taskpool):
         self.p = p or A.grid.P
         self.kd = qr_ops.kinds(A.dtype, TS.mb, (0, 0), (0, 0))
         self._panel_ws = {}
+        self._lu_batches = {}
+        self._plu, self._pbuf = {}, None
         # QR steps on the stacked-domain engine (models/qr_panel.py: every TS domain of the step's tree
         # one persistent panel launch, TT kills likewise, MFMA trailing updates) when it handles A and the
         # tree; T factors then live in its ("panel") format and trsmpl_qrf applies them the same way
@@ -138,7 +141,9 @@ class _GetrfQrf(Taskpool):
     def _domain_lu(self, st: _Step):
         """Stacked LU of the domain on the diagonal owner -> (buffer, ipiv, info, W0, colmax)."""
         A = self.A
-        buf = torch.empty(st.ncol * st.M, dtype=A.dtype, device=A.device)
+        if self._pbuf is None:
+            self._pbuf = torch.empty(max(1, A.m * A.nb), dtype=A.dtype, device=A.device)
+        buf = self._pbuf[: st.ncol * st.M]
         view = torch.as_strided(buf, (st.M, st.ncol), (1, st.M))
         r0 = 0
         for m, r in zip(st.dom, st.rows):
@@ -157,7 +162,10 @@ class _GetrfQrf(Taskpool):
             if ws is None:
                 ws = self._panel_ws[key] = (ops.lu_workspace(st.M, A.device),
                                             torch.zeros(1, dtype=torch.int32, device=A.device))
-            ops.PanelLU(buf, st.M, st.M, st.ncol, pivot=True).run(ipiv, ws[0], ws[1], info, 0)
+            plu = self._plu.get(st.k)
+            if plu is None:
+                plu = self._plu[st.k] = ops.PanelLU(buf, st.M, st.M, st.ncol, pivot=True)
+            plu.run(ipiv, ws[0], ws[1], info, 0)
         else:
             ops.getrf_panel(buf, 0, st.M, st.ncol, st.M, ipiv, info, 0, pivot=True)
         w0 = 0.0
@@ -263,6 +271,9 @@ class _GetrfQrf(Taskpool):
         mv = np.nonzero(perm != np.arange(st.M))[0]
         trail = [n for n in range(k + 1, A.nt) if A.col_is_local(n)]
         _permute_rows_2d(ctx, A, st.grow[mv], st.grow[perm[mv]], trail)
+        if ctx.world == 1:
+            self._lu_update_local(st)
+            return
         prog = TileProgram(ctx, f"getrf_qrf_lu({k})")
         s = prog.stage("trsm")
         for n in range(k + 1, A.nt):
@@ -275,6 +286,44 @@ class _GetrfQrf(Taskpool):
                 for n in range(k + 1, A.nt):
                     s.gemm((A, m, n), [((A, m, k), N_, (A, k, n), N_)], alpha=-1.0, beta=1.0)
         prog.compile().execute(ctx)
+
+    def _lu_update_local(self, st: _Step):
+        """One process: the LU step's solves and trailing update as three batched launches (TRSM of
+        row k with L_kk, TRSM of the off-domain tiles with U_kk, one MFMA GEMM batch built with numpy),
+        cached per step across runs -- no per-tile program construction on the critical path."""
+        A, k = self.A, st.k
+        b = self._lu_batches.get(k)
+        if b is None:
+            kb = A.tile_cols(k)
+            dkk = A.offset(k, k)
+            row = TileBatch()
+            for n in range(k + 1, A.nt):
+                row.add(dkk, A.tile_rows(k), A.tile_cols(n), b_off=A.offset(k, n))
+            off = TileBatch()
+            for m in st.off:
+                off.add(dkk, A.tile_rows(m), kb, b_off=A.offset(m, k))
+            gb = None
+            if k + 1 < A.mt and k + 1 < A.nt:
+                ms = np.arange(k + 1, A.mt)
+                ns = np.arange(k + 1, A.nt)
+                ro = np.array([A.offset(m, k) for m in ms], dtype=np.int64)      # column k of every row
+                co = np.array([A.offset(k, n) for n in ns], dtype=np.int64)      # row k of every column
+                cbase = np.array([A.offset(m, k + 1) for m in ms], dtype=np.int64)
+                dcol = co - co[0]                                                 # tile-column stride
+                mm, nn = np.meshgrid(np.arange(len(ms)), np.arange(len(ns)), indexing="ij")
+                c_off = cbase[mm] + dcol[nn]
+                rows = np.array([A.tile_rows(m) for m in ms], dtype=np.int64)[mm]
+                cols = np.array([A.tile_cols(n) for n in ns], dtype=np.int64)[nn]
+                gb = GemmBatch().add_arrays(c_off, rows, cols, 1, ro[mm], co[nn], kb).finalize()
+            b = self._lu_batches[k] = (row.finalize() if len(row) else None, off.finalize() if len(off) else None,
+                                       gb)
+        row, off, gb = b
+        if row is not None:
+            ops.trsm(dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, A.data, A.ld, A.data, A.ld, row)
+        if off is not None:
+            ops.trsm(dplasmaRight, dplasmaUpper, N_, dplasmaNonUnit, 1.0, A.data, A.ld, A.data, A.ld, off)
+        if gb is not None:
+            ops.gemm(N_, N_, -1.0, A.data, A.ld, A.data, A.ld, 1.0, A.data, A.ld, gb)
 
     def _qr_step(self, st: _Step):
         A, ctx, k = self.A, self.ctx, st.k
