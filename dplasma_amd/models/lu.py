@@ -193,7 +193,11 @@ class _GetrfDev:
         self.xc = None
         if self.dist:
             # exchange buffers of my process column (every rank of the column creates them together)
-            self.xc = lu_dist_ops.panel_xchg(ctx.col_group, A.myrow, g.P, nb, A.dtype, dev)
+            # largest (diagonal replica + own rows) panel any rank factors -- the same number on every rank
+            per_row = [0] * g.P
+            for m in range(A.mt):
+                per_row[g.prow(m + A.it0)] += A.tile_rows(m)
+            self.xc = lu_dist_ops.panel_xchg(ctx.col_group, A.myrow, g.P, nb, A.dtype, dev, max(per_row) + mb)
             self.dws = lu_dist_ops.dist_workspace(nb, dev)
             self.tbuf = torch.zeros(max(1, mb * nb), dtype=A.dtype, device=dev)
         self.cnt = torch.zeros(1, dtype=torch.int32, device=dev)

@@ -48,7 +48,7 @@ class PanelXchg:
     sender) of ``{epoch flag, position, |v|, row[kbw]}``, IPC-mapped by every peer.  ``epoch`` counts
     the panel columns factored so far; it advances identically on every rank of the column."""
 
-    def __init__(self, group, me: int, P: int, kbw: int, dtype: torch.dtype, device):
+    def __init__(self, group, me: int, P: int, kbw: int, dtype: torch.dtype, device, max_rows: int = 0):
         self.group, self.me, self.P, self.kbw = group, me, P, kbw
         self.dtype, self.device = dtype, torch.device(device)
         self.epoch = 1
@@ -64,7 +64,11 @@ class PanelXchg:
         handle = (ctypes.c_char * hb)()
         ptr = ctypes.c_void_p()
         torch.cuda.synchronize(self.device)
-        rc = lib.dpl_xchg_alloc(nbytes, ctypes.byref(ptr), handle)
+        # the persistent kernel holds one row per thread on at most one workgroup per CU: a rank whose
+        # panel rows exceed that sends the whole column to the host transport (the choice must agree)
+        ncu = min(256, torch.cuda.get_device_properties(self.device).multi_processor_count)
+        fits = max_rows <= 256 * ncu
+        rc = lib.dpl_xchg_alloc(nbytes, ctypes.byref(ptr), handle) if fits else -4
         mine = bytes(handle) if rc == 0 else b""
         allh = [None] * P
         dist.all_gather_object(allh, (rc, mine), group=group)
@@ -114,14 +118,17 @@ class PanelXchg:
 _XCHG = {}
 
 
-def panel_xchg(group, me: int, P: int, kbw: int, dtype: torch.dtype, device) -> PanelXchg:
+def panel_xchg(group, me: int, P: int, kbw: int, dtype: torch.dtype, device, max_rows: int = 0) -> PanelXchg:
     """The exchange buffers of a process column, created once per (group, width, dtype) and re-used by
     every later factorisation (their epochs continue), so repeated LU runs neither re-export IPC
     handles nor leak mappings.  ``release_all()`` frees them (collective over each column group)."""
-    key = (id(group), me, P, kbw, dtype, str(torch.device(device)))
+    dev = torch.device(device)
+    ncu = min(256, torch.cuda.get_device_properties(dev).multi_processor_count) if dev.type == "cuda" else 256
+    # max_rows is the largest panel of ANY rank (identical everywhere), so every rank picks the same key
+    key = (id(group), me, P, kbw, dtype, str(dev), max_rows <= 256 * ncu)
     xc = _XCHG.get(key)
     if xc is None:
-        xc = _XCHG[key] = PanelXchg(group, me, P, kbw, dtype, device)
+        xc = _XCHG[key] = PanelXchg(group, me, P, kbw, dtype, device, max_rows)
     return xc
 
 
