@@ -347,13 +347,15 @@ __device__ inline void wave_argmax(double& v, int& i) {
   }
 }
 
-template <typename T>
+// BWT: the widest block this instantiation holds (64: 128 KiB LDS tile for fp64; 32: 64 KiB, which leaves
+// room on the CU for one trailing-update GEMM workgroup -- DPLASMA_LU_BW=32, the recursion's base width)
+template <typename T, int BWT>
 __global__ __launch_bounds__(PLR) void k_lu_block_persist(T* __restrict__ A, int ld, int m, int c0, int cend, int R,
                                                           int* __restrict__ ipiv, T* __restrict__ cand,
                                                           double* __restrict__ pval, int* __restrict__ pidx,
                                                           int* __restrict__ cnt, int* __restrict__ info,
                                                           int info_base) {
-  __shared__ T tile[PBW * PLR];      // column-major: tile[c * R + r]
+  __shared__ T tile[BWT * PLR];      // column-major: tile[c * R + r]
   __shared__ T prow[PBW], oldj[PBW];
   __shared__ double sv[PLR];
   __shared__ int si[PLR];
@@ -695,11 +697,18 @@ DPL_API int dpl_lu_block(int prec, void* A, int ld, int m, int c0, int cend, int
         else
           hipLaunchKernelGGL((k_lu_block_reg<float>), dim3(G), dim3(PLR), 0, st, (float*)A, ld, m, c0, cend, R,
                              ipiv, (float*)cand, pval, pidx, cnt, info, info_base);
+      } else if (cend - c0 <= 32) {
+        if (prec == DPL_D)
+          hipLaunchKernelGGL((k_lu_block_persist<double, 32>), dim3(G), dim3(PLR), 0, st, (double*)A, ld, m, c0, cend,
+                             R, ipiv, (double*)cand, pval, pidx, cnt, info, info_base);
+        else
+          hipLaunchKernelGGL((k_lu_block_persist<float, 32>), dim3(G), dim3(PLR), 0, st, (float*)A, ld, m, c0, cend,
+                             R, ipiv, (float*)cand, pval, pidx, cnt, info, info_base);
       } else if (prec == DPL_D)
-        hipLaunchKernelGGL((k_lu_block_persist<double>), dim3(G), dim3(PLR), 0, st, (double*)A, ld, m, c0, cend, R,
+        hipLaunchKernelGGL((k_lu_block_persist<double, 64>), dim3(G), dim3(PLR), 0, st, (double*)A, ld, m, c0, cend, R,
                            ipiv, (double*)cand, pval, pidx, cnt, info, info_base);
       else
-        hipLaunchKernelGGL((k_lu_block_persist<float>), dim3(G), dim3(PLR), 0, st, (float*)A, ld, m, c0, cend, R,
+        hipLaunchKernelGGL((k_lu_block_persist<float, 64>), dim3(G), dim3(PLR), 0, st, (float*)A, ld, m, c0, cend, R,
                            ipiv, (float*)cand, pval, pidx, cnt, info, info_base);
       return (int)hipGetLastError();
     }

@@ -914,7 +914,10 @@ def qr_panel(P: torch.Tensor, ldp: int, M: int, nc: int, kf: int, V: torch.Tenso
     tv.copy_(torch.where(torch.ones(kf, kf, dtype=torch.bool).triu(), T, tv))
 
 
-LU_BW = 64   # base block width of the recursive panel LU (lu_piv.hip LU_MAXBW)
+import os as _os
+# base block width of the recursive panel LU (lu_piv.hip LU_MAXBW = 64); DPLASMA_LU_BW=32 selects the
+# 64 KiB-LDS block kernel, which can share a CU with a trailing-update GEMM workgroup under look-ahead
+LU_BW = int(_os.environ.get("DPLASMA_LU_BW", "64"))
 
 
 def lu_workspace(m: int, device) -> torch.Tensor:
