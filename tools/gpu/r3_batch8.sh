@@ -1,0 +1,17 @@
+#!/bin/bash
+# DGETRF block width 64 vs 32 (the 32-wide block kernel can share CUs with GEMM) x look-ahead; LU-QR profile.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 200 python -u -m pytest tests/test_lu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/b8_tests.log 2>&1
+rc=$?; tail -1 gpurun_out/b8_tests.log; echo "tests rc=$rc"; [ $rc -ne 0 ] && exit $rc
+DPLASMA_LU_BW=32 timeout -k 10 200 python -u -m pytest tests/test_lu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/b8_tests32.log 2>&1
+rc=$?; tail -1 gpurun_out/b8_tests32.log; echo "tests bw32 rc=$rc"; [ $rc -ne 0 ] && exit $rc
+for N in 32768 65536; do for BW in 64 32; do for LA in 0 1; do
+  DPLASMA_LU_BW=$BW DPLASMA_LU_LOOKAHEAD=$LA timeout -k 10 200 python tools/bench_algo.py getrf_1d -N $N --nb 512 --runs 2 \
+      > gpurun_out/b8_lu_${N}_${BW}_${LA}.log 2>&1 || { echo "lu $N $BW $LA failed"; tail -5 gpurun_out/b8_lu_${N}_${BW}_${LA}.log; exit 1; }
+  echo "N=$N bw=$BW lookahead=$LA: $(grep TIME gpurun_out/b8_lu_${N}_${BW}_${LA}.log | tail -1 | cut -c1-150)"
+done; done; done
+timeout -k 10 300 python tools/gpu/luqr_prof.py 32768 256 > gpurun_out/b8_luqr_prof.log 2>&1
+rc=$?; grep "^run" gpurun_out/b8_luqr_prof.log | cut -c1-40; echo "luqr rc=$rc"
+exit 0
