@@ -74,6 +74,14 @@ NatProgram* nat_herk(dplasma_context_t* ctx, int prec, int uplo, int trans, doub
                      double beta, dplasma_desc_t* C);
 NatProgram* nat_syrk(dplasma_context_t* ctx, int prec, int uplo, int trans, const void* alpha, dplasma_desc_t* A,
                      const void* beta, dplasma_desc_t* C);
+NatProgram* nat_her2k(dplasma_context_t* ctx, int prec, int uplo, int trans, const void* alpha, dplasma_desc_t* A,
+                      dplasma_desc_t* B, double beta, dplasma_desc_t* C);
+NatProgram* nat_syr2k(dplasma_context_t* ctx, int prec, int uplo, int trans, const void* alpha, dplasma_desc_t* A,
+                      dplasma_desc_t* B, const void* beta, dplasma_desc_t* C);
+NatProgram* nat_trtri(dplasma_context_t* ctx, int prec, int uplo, int diag, dplasma_desc_t* A);
+NatProgram* nat_lauum(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* A);
+NatProgram* nat_potri(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* A);
+NatProgram* nat_poinv(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* A);
 NatProgram* nat_geadd(dplasma_context_t* ctx, int prec, int trans, const void* alpha, dplasma_desc_t* A,
                       const void* beta, dplasma_desc_t* B);
 NatProgram* nat_tradd(dplasma_context_t* ctx, int prec, int uplo, int trans, const void* alpha, dplasma_desc_t* A,

@@ -657,34 +657,32 @@ NatProgram* nat_trsm(dplasma_context_t* ctx, int prec, int side, int uplo, int t
 // C = alpha op(A) op(A)^{H|T} + beta C on the uplo triangle (models/blas3.py): one launch of the MFMA
 // GEMM engine over every tile of the triangle, k-runs over A's tile columns (rows for trans), the
 // diagonal tiles masked to their triangle.
-static NatProgram* rank_k(dplasma_context_t* ctx, int prec, int uplo, int trans, const Scalar& alpha,
-                          dplasma_desc_t* dA, const Scalar& beta, dplasma_desc_t* dC, bool herm, const char* name) {
-  NatCtx* c = ctx->nat;
-  NatDesc *A = dA ? dA->nat : nullptr, *C = dC ? dC->nat : nullptr;
-  if (!same_ctx(c, {A, C}, prec)) return fail(nullptr, std::string(name) + ": descriptors of another context");
+// C = alpha op(A) op(B)^{H|T} on C's uplo triangle tiles (beta on the first pass); rank-2k adds the
+// swapped product in a second launch.  Tasks on stream 1 after `prev`; returns the last task (-2: failure).
+static int add_rank_k(NatProgram& Pr, int prec, int uplo, int trans, const Scalar& alpha, const NatDesc* A,
+                      const NatDesc* B, const Scalar& beta, NatDesc* C, bool herm, int prev) {
+  NatProgram* P = &Pr;
   const bool nt = trans == NOTRANS;
-  const int an = nt ? A->m : A->n, ak = nt ? A->n : A->m, akb = nt ? A->nb : A->mb;
-  if ((uplo != LOWER && uplo != UPPER) || C->m != C->n || an != C->m || C->mb != C->nb ||
-      (nt ? A->mb : A->nb) != C->mb)
-    return fail(nullptr, std::string(name) + ": operands do not conform");
+  const int ak = nt ? A->n : A->m, akb = nt ? A->nb : A->mb;
   const int ct = herm ? CONJTRANS : TRANS;
-  NatProgram* P = new_program(c, name, false);
   auto g = std::make_shared<Gemm>();
   const int kt = (ak + akb - 1) / akb;
   for (int n = 0; n < C->nt; ++n)
     for (int m = 0; m < C->mt; ++m) {
       if ((uplo == LOWER && m < n) || (uplo == UPPER && m > n)) continue;
       std::vector<KPair> kp;
-      for (int k = 0; k < kt; ++k)   // C(m,n) += op(A)(m,k) op(A)(n,k)^H
-        kp.push_back(KPair{nt ? A->off(m, k) : A->off(k, m), nt ? A->off(n, k) : A->off(k, n),
+      for (int k = 0; k < kt; ++k)   // C(m,n) += op(A)(m,k) op(B)(n,k)^H
+        kp.push_back(KPair{nt ? A->off(m, k) : A->off(k, m), nt ? B->off(n, k) : B->off(k, n),
                            nt ? A->cols(k) : A->rows(k), 0});
       g->add(C->off(m, n), C->rows(m), C->cols(n), kp, m == n ? (uplo == LOWER ? 1 : 2) : 0);
     }
-  if (!g->upload(*P)) return fail(P, std::string(name) + ": device allocation failed");
-  char *a = A->data, *cc = C->data;
-  const int lda = A->lld, ldc = C->lld;
+  if (!g->upload(*P)) return -2;
+  char *a = A->data, *b = B->data, *cc = C->data;
+  const int lda = A->lld, ldb = B->lld, ldc = C->lld;
   const int ta = nt ? NOTRANS : ct, tb = nt ? ct : NOTRANS;
-  const int t = P->task(1, [=](hipStream_t s) { return g->launch(prec, ta, tb, alpha, a, lda, a, lda, beta, cc, ldc, s); }, {});
+  const int t = P->task(1, [=](hipStream_t s) { return g->launch(prec, ta, tb, alpha, a, lda, b, ldb, beta, cc, ldc, s); },
+                        {prev});
+  int last = t;
   if (herm) {
     // Hermitian rank-k (zherk): C's diagonal is real.  diag := (diag + conj(diag)) / 2 on the
     // diagonal tiles (geadd, diagonal part, conjugate transpose of the tile onto itself)
@@ -695,14 +693,50 @@ static NatProgram* rank_k(dplasma_context_t* ctx, int prec, int uplo, int trans,
       mm = std::max(mm, std::max(C->rows(k), C->cols(k)));
     }
     DevPtr dd = dev_upload(d);
-    if (!dd) return fail(P, std::string(name) + ": device allocation failed");
+    if (!dd) return -2;
     P->keep.push_back(dd);
     const Scalar half(prec, 0.5);
     const int n = (int)d.size();
-    P->task(1, [=](hipStream_t s) {
+    last = P->task(1, [=](hipStream_t s) {
       return dpl_geadd(prec, 5, CONJTRANS, n, dd->p, mm, mm, half.ptr(), cc, ldc, half.ptr(), cc, ldc, 0, s);
     }, {t});
   }
+  return last;
+}
+
+static NatProgram* rank_k(dplasma_context_t* ctx, int prec, int uplo, int trans, const Scalar& alpha,
+                          dplasma_desc_t* dA, const Scalar& beta, dplasma_desc_t* dC, bool herm, const char* name) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *C = dC ? dC->nat : nullptr;
+  if (!same_ctx(c, {A, C}, prec)) return fail(nullptr, std::string(name) + ": descriptors of another context");
+  const bool nt = trans == NOTRANS;
+  const int an = nt ? A->m : A->n;
+  if ((uplo != LOWER && uplo != UPPER) || C->m != C->n || an != C->m || C->mb != C->nb ||
+      (nt ? A->mb : A->nb) != C->mb)
+    return fail(nullptr, std::string(name) + ": operands do not conform");
+  NatProgram* P = new_program(c, name, false);
+  if (add_rank_k(*P, prec, uplo, trans, alpha, A, A, beta, C, herm, -1) == -2)
+    return fail(P, std::string(name) + ": device allocation failed");
+  return P;
+}
+
+// C = alpha op(A) op(B)^H + conj(alpha) op(B) op(A)^H + beta C (her2k; syr2k: alpha both times, ^T):
+// two launches of the GEMM engine on the triangle, the second accumulating (src/zher2k_*.jdf)
+static NatProgram* rank_2k(dplasma_context_t* ctx, int prec, int uplo, int trans, const Scalar& alpha,
+                           const Scalar& alpha2, dplasma_desc_t* dA, dplasma_desc_t* dB, const Scalar& beta,
+                           dplasma_desc_t* dC, bool herm, const char* name) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *B = dB ? dB->nat : nullptr, *C = dC ? dC->nat : nullptr;
+  if (!same_ctx(c, {A, B, C}, prec)) return fail(nullptr, std::string(name) + ": descriptors of another context");
+  const bool nt = trans == NOTRANS;
+  if ((uplo != LOWER && uplo != UPPER) || C->m != C->n || (nt ? A->m : A->n) != C->m || A->m != B->m ||
+      A->n != B->n || A->mb != B->mb || A->nb != B->nb || C->mb != C->nb || (nt ? A->mb : A->nb) != C->mb)
+    return fail(nullptr, std::string(name) + ": operands do not conform");
+  NatProgram* P = new_program(c, name, false);
+  const Scalar one(prec, 1.0);
+  int t = add_rank_k(*P, prec, uplo, trans, alpha, A, B, beta, C, false, -1);
+  if (t != -2) t = add_rank_k(*P, prec, uplo, trans, alpha2, B, A, one, C, herm, t);
+  if (t == -2) return fail(P, std::string(name) + ": device allocation failed");
   return P;
 }
 
@@ -715,6 +749,28 @@ NatProgram* nat_herk(dplasma_context_t* ctx, int prec, int uplo, int trans, doub
 NatProgram* nat_syrk(dplasma_context_t* ctx, int prec, int uplo, int trans, const void* alpha, dplasma_desc_t* A,
                      const void* beta, dplasma_desc_t* C) {
   return rank_k(ctx, prec, uplo, trans, Scalar(prec, alpha), A, Scalar(prec, beta), C, false, "syrk");
+}
+
+NatProgram* nat_her2k(dplasma_context_t* ctx, int prec, int uplo, int trans, const void* alpha, dplasma_desc_t* A,
+                      dplasma_desc_t* B, double beta, dplasma_desc_t* C) {
+  if (prec != P_C && prec != P_Z) return fail(nullptr, "her2k: complex precisions only");
+  double a[2] = {0.0, 0.0};
+  if (prec == P_C) {
+    float f[2];
+    std::memcpy(f, alpha, sizeof(f));
+    a[0] = f[0];
+    a[1] = f[1];
+  } else {
+    std::memcpy(a, alpha, sizeof(a));
+  }
+  return rank_2k(ctx, prec, uplo, trans, Scalar(prec, a[0], a[1]), Scalar(prec, a[0], -a[1]), A, B,
+                 Scalar(prec, beta), C, true, "her2k");
+}
+
+NatProgram* nat_syr2k(dplasma_context_t* ctx, int prec, int uplo, int trans, const void* alpha, dplasma_desc_t* A,
+                      dplasma_desc_t* B, const void* beta, dplasma_desc_t* C) {
+  return rank_2k(ctx, prec, uplo, trans, Scalar(prec, alpha), Scalar(prec, alpha), A, B, Scalar(prec, beta), C, false,
+                 "syr2k");
 }
 
 // ----------------------------------------------------------------------------- element-wise maps
@@ -1327,6 +1383,95 @@ double nat_lansy(dplasma_context_t* ctx, int prec, int ntype, int uplo, dplasma_
 double nat_lanhe(dplasma_context_t* ctx, int prec, int ntype, int uplo, dplasma_desc_t* A) {
   if (prec != P_C && prec != P_Z) { dpl_set_error("lanhe: complex precisions only"); return NAN; }
   return norm_sym(ctx, prec, ntype, uplo, A, true);
+}
+
+// ----------------------------------------------------------------------------- TRTRI / LAUUM / POTRI
+// trtri: inv(T) of A's uplo triangle as one blocked TRSM of an identity right-hand side (the MFMA
+// TRSM path: per block row a strip solve + one GEMM), its triangle copied back (strictly, for a unit
+// diagonal).  lauum: L^H L (lower) / U U^H (upper) as one rank-k launch over the triangle of the
+// expanded factor (zeros outside it).  potri = trtri + lauum, poinv = potrf + potri (src/zpotri_wrapper.c,
+// src/zpoinv_wrapper.c: the same algebra as the reference's tile algorithms, batched per launch).
+namespace {
+
+int add_trtri(NatProgram& P, int uplo, int diag, NatDesc& A, int prev) {
+  const int prec = A.prec;
+  auto X = work_desc(P, A);
+  if (!X) return -2;
+  const Scalar zero(prec, 0.0), one(prec, 1.0);
+  auto all = std::make_shared<MapBatch>(), back = std::make_shared<MapBatch>();
+  all->build(*X, UPPERLOWER, nullptr, NOTRANS);
+  back->build(A, uplo, X.get(), NOTRANS);
+  if (!all->upload(P) || !back->upload(P)) return -2;
+  char *xd = X->data, *ad = A.data;
+  const int ldx = X->lld, lda = A.lld;
+  prev = P.task(1, [=](hipStream_t s) {   // X := I
+    return dpl_laset(prec, 0, all->n(), all->items(), all->mm, all->nn, zero.ptr(), one.ptr(), xd, ldx, s);
+  }, {prev});
+  if (!add_trsm(P, LEFT, uplo, NOTRANS, diag, one, A, *X, 1, prev)) return -2;
+  // strictly lower / upper for a unit diagonal (the diagonal of A is not referenced), else with it
+  const int part = uplo == LOWER ? (diag == UNIT ? 3 : 1) : (diag == UNIT ? 4 : 2);
+  return P.task(1, [=](hipStream_t s) {
+    return dpl_geadd(prec, part, NOTRANS, back->n(), back->items(), back->mm, back->nn, one.ptr(), xd, ldx,
+                     zero.ptr(), ad, lda, 1, s);
+  }, {last_on(P, 1)});
+}
+
+int add_lauum(NatProgram& P, int uplo, NatDesc& A, int prev) {
+  const int prec = A.prec;
+  auto T = work_desc(P, A);
+  if (!T) return -2;
+  prev = add_expand(P, A, uplo, false, 0, *T, prev);
+  if (prev == -2) return -2;
+  const Scalar zero(prec, 0.0), one(prec, 1.0);
+  const bool herm = prec == P_C || prec == P_Z;
+  // lower: A = T^H T = op(T) op(T)^H with op = ^H;  upper: A = T T^H
+  const int trans = uplo == LOWER ? (herm ? CONJTRANS : TRANS) : NOTRANS;
+  return add_rank_k(P, prec, uplo, trans, one, T.get(), T.get(), zero, &A, herm, prev);
+}
+
+bool square_tiles(const NatDesc* A, int uplo) {
+  return A && A->m == A->n && A->mb == A->nb && (uplo == LOWER || uplo == UPPER);
+}
+
+}  // namespace
+
+NatProgram* nat_trtri(dplasma_context_t* ctx, int prec, int uplo, int diag, dplasma_desc_t* dA) {
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!same_ctx(ctx->nat, {A}, prec) || !square_tiles(A, uplo))
+    return fail(nullptr, "trtri: square matrix with square tiles and uplo Lower/Upper required");
+  NatProgram* P = new_program(ctx->nat, "trtri", false);
+  if (add_trtri(*P, uplo, diag, *A, -1) == -2) return fail(P, "trtri: device allocation failed");
+  return P;
+}
+
+NatProgram* nat_lauum(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* dA) {
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!same_ctx(ctx->nat, {A}, prec) || !square_tiles(A, uplo))
+    return fail(nullptr, "lauum: square matrix with square tiles and uplo Lower/Upper required");
+  NatProgram* P = new_program(ctx->nat, "lauum", false);
+  if (add_lauum(*P, uplo, *A, -1) == -2) return fail(P, "lauum: device allocation failed");
+  return P;
+}
+
+NatProgram* nat_potri(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* dA) {
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!same_ctx(ctx->nat, {A}, prec) || !square_tiles(A, uplo))
+    return fail(nullptr, "potri: square matrix with square tiles and uplo Lower/Upper required");
+  NatProgram* P = new_program(ctx->nat, "potri", false);
+  int t = add_trtri(*P, uplo, NONUNIT, *A, -1);
+  if (t != -2) t = add_lauum(*P, uplo, *A, t);
+  if (t == -2) return fail(P, "potri: device allocation failed");
+  return P;
+}
+
+NatProgram* nat_poinv(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* dA) {
+  NatProgram* P = nat_potrf(ctx, prec, uplo, dA);
+  if (!P) return nullptr;
+  // the inversion (update stream) starts after the factorisation's last panel-stream task
+  int t = add_trtri(*P, uplo, NONUNIT, *dA->nat, last_on(*P, 0));
+  if (t != -2) t = add_lauum(*P, uplo, *dA->nat, t);
+  if (t == -2) return fail(P, "poinv: device allocation failed");
+  return P;
 }
 
 // ----------------------------------------------------------------------------- LU (partial pivoting)

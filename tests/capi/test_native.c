@@ -684,6 +684,130 @@ static void test_dgeqrf(dplasma_context_t *ctx) {
   dplasma_desc_destroy(C), dplasma_desc_destroy(D), dplasma_desc_destroy(B);
 }
 
+
+/* trtri / lauum / potri / poinv natively: A := inv(A) checked as ||A0 inv(A) - I||; lauum against host
+   L^T L; her2k / syr2k against host rank-2k; the alias entry points (ptgpanel on 1x1, potrf_rec). */
+static void test_inverse_family(dplasma_context_t *ctx) {
+  const int n = 700, nb = 128;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, n, n);
+  double *A0 = malloc(sizeof(double) * n * n), *X = malloc(sizeof(double) * n * n);
+  CHECK(dplasma_dplghe(ctx, (double)n, dplasmaUpperLower, A, 77) == 0, "dplghe: %s", dplasma_last_error());
+  CHECK(dplasma_desc_get_lapack(A, A0, n) == 0, "get A0");
+  CHECK(dplasma_dpoinv(ctx, dplasmaLower, A) == 0, "dpoinv: %s", dplasma_last_error());
+  CHECK(dplasma_desc_get_lapack(A, X, n) == 0, "get X");
+  for (int j = 0; j < n; ++j)   /* symmetric inverse from its lower triangle */
+    for (int i = 0; i < j; ++i) X[i + (size_t)j * n] = X[j + (size_t)i * n];
+  double err = 0;
+  for (int j = 0; j < n; j += 7)
+    for (int i = 0; i < n; ++i) {
+      double s = 0;
+      for (int k = 0; k < n; ++k) s += A0[i + (size_t)k * n] * X[k + (size_t)j * n];
+      err = fmax(err, fabs(s - (i == j ? 1.0 : 0.0)));
+    }
+  CHECK(err < 1e-10, "dpoinv ||A inv(A) - I|| %.3e", err);
+  /* trtri of a unit upper triangle: T inv(T) = I on the upper part */
+  CHECK(dplasma_dplrnt(ctx, 0, A, 5) == 0, "dplrnt");
+  CHECK(dplasma_desc_get_lapack(A, A0, n) == 0, "get T0");
+  CHECK(dplasma_dtrtri(ctx, dplasmaUpper, dplasmaUnit, A) == 0, "dtrtri: %s", dplasma_last_error());
+  CHECK(dplasma_desc_get_lapack(A, X, n) == 0, "get inv");
+  err = 0;
+  for (int j = 0; j < n; j += 5)
+    for (int i = 0; i <= j; ++i) {
+      double s = 0;
+      for (int k = i; k <= j; ++k)
+        s += (k == i ? 1.0 : A0[i + (size_t)k * n]) * (k == j ? 1.0 : X[k + (size_t)j * n]);
+      err = fmax(err, fabs(s - (i == j ? 1.0 : 0.0)));
+    }
+  CHECK(err < 1e-8 * n, "dtrtri unit upper error %.3e", err);
+  /* lauum lower: A := L^T L */
+  CHECK(dplasma_dplrnt(ctx, 0, A, 9) == 0, "dplrnt");
+  CHECK(dplasma_desc_get_lapack(A, A0, n) == 0, "get L0");
+  CHECK(dplasma_dlauum(ctx, dplasmaLower, A) == 0, "dlauum: %s", dplasma_last_error());
+  CHECK(dplasma_desc_get_lapack(A, X, n) == 0, "get LtL");
+  err = 0;
+  double nrm = 0;
+  for (int j = 0; j < n; j += 3)
+    for (int i = j; i < n; ++i) {
+      double s = 0;
+      for (int k = i; k < n; ++k) s += A0[k + (size_t)i * n] * A0[k + (size_t)j * n];
+      err = fmax(err, fabs(X[i + (size_t)j * n] - s));
+      nrm = fmax(nrm, fabs(s));
+    }
+  CHECK(err < 1e-13 * nrm * n, "dlauum error %.3e", err / nrm);
+  dplasma_desc_destroy(A);
+  free(A0);
+  free(X);
+}
+
+static void test_rank_2k(dplasma_context_t *ctx) {
+  const int n = 300, k = 200, nb = 128;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, n, k), *B = dmat(ctx, dplasmaRealDouble, nb, n, k);
+  dplasma_desc_t *C = dmat(ctx, dplasmaRealDouble, nb, n, n);
+  double *a = malloc(sizeof(double) * n * k), *b = malloc(sizeof(double) * n * k);
+  double *c0 = malloc(sizeof(double) * n * n), *c1 = malloc(sizeof(double) * n * n);
+  dplasma_dplrnt(ctx, 0, A, 1);
+  dplasma_dplrnt(ctx, 0, B, 2);
+  dplasma_dplrnt(ctx, 0, C, 3);
+  dplasma_desc_get_lapack(A, a, n);
+  dplasma_desc_get_lapack(B, b, n);
+  dplasma_desc_get_lapack(C, c0, n);
+  CHECK(dplasma_dsyr2k(ctx, dplasmaUpper, dplasmaNoTrans, 0.7, A, B, -0.3, C) == 0, "dsyr2k: %s",
+        dplasma_last_error());
+  dplasma_desc_get_lapack(C, c1, n);
+  double err = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i <= j; ++i) {
+      double s = 0;
+      for (int q = 0; q < k; ++q) s += a[i + (size_t)q * n] * b[j + (size_t)q * n] + b[i + (size_t)q * n] * a[j + (size_t)q * n];
+      err = fmax(err, fabs(c1[i + (size_t)j * n] - (0.7 * s - 0.3 * c0[i + (size_t)j * n])));
+    }
+  CHECK(err < 1e-11, "dsyr2k error %.3e", err);
+  dplasma_desc_destroy(A);
+  dplasma_desc_destroy(B);
+  dplasma_desc_destroy(C);
+  /* zher2k: C = alpha A B^H + conj(alpha) B A^H + beta C, real diagonal */
+  dplasma_desc_t *Z = dmat(ctx, dplasmaComplexDouble, nb, n, k), *Y = dmat(ctx, dplasmaComplexDouble, nb, n, k);
+  dplasma_desc_t *W = dmat(ctx, dplasmaComplexDouble, nb, n, n);
+  double complex *z = malloc(sizeof(double complex) * n * k), *y = malloc(sizeof(double complex) * n * k);
+  double complex *w0 = malloc(sizeof(double complex) * n * n), *w1 = malloc(sizeof(double complex) * n * n);
+  dplasma_zplrnt(ctx, 0, Z, 4);
+  dplasma_zplrnt(ctx, 0, Y, 5);
+  dplasma_zplghe(ctx, 1.0, dplasmaUpperLower, W, 6);
+  dplasma_desc_get_lapack(Z, z, n);
+  dplasma_desc_get_lapack(Y, y, n);
+  dplasma_desc_get_lapack(W, w0, n);
+  const double complex al = 0.5 + 0.25 * I;
+  CHECK(dplasma_zher2k(ctx, dplasmaLower, dplasmaNoTrans, al, Z, Y, 0.5, W) == 0, "zher2k: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(W, w1, n);
+  err = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = j; i < n; ++i) {
+      double complex s = 0;
+      for (int q = 0; q < k; ++q)
+        s += al * z[i + (size_t)q * n] * conj(y[j + (size_t)q * n]) + conj(al) * y[i + (size_t)q * n] * conj(z[j + (size_t)q * n]);
+      err = fmax(err, cabs(w1[i + (size_t)j * n] - (s + 0.5 * w0[i + (size_t)j * n])));
+    }
+  CHECK(err < 1e-11, "zher2k error %.3e", err);
+  for (int i = 0; i < n; ++i) CHECK(cimag(w1[i + (size_t)i * n]) == 0.0, "zher2k diagonal imaginary part");
+  dplasma_desc_destroy(Z);
+  dplasma_desc_destroy(Y);
+  dplasma_desc_destroy(W);
+  free(a); free(b); free(c0); free(c1); free(z); free(y); free(w0); free(w1);
+}
+
+static void test_aliases(dplasma_context_t *ctx) {
+  const int n = 512, nb = 128;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, n, n);
+  dplasma_desc_t *IP = dplasma_desc_ipiv(ctx, 1, nb, 1, n, 1, 1);
+  CHECK(A && IP, "alias descriptors: %s", dplasma_last_error());
+  dplasma_dplrnt(ctx, 0, A, 8);
+  CHECK(dplasma_dgetrf_ptgpanel(ctx, A, IP) == 0, "dgetrf_ptgpanel (1x1 native): %s", dplasma_last_error());
+  dplasma_dplghe(ctx, (double)n, dplasmaLower, A, 3);
+  CHECK(dplasma_dpotrf_rec(ctx, dplasmaLower, A, 64) == 0, "dpotrf_rec (native): %s", dplasma_last_error());
+  dplasma_desc_destroy(A);
+  dplasma_desc_destroy(IP);
+}
+
 int main(int argc, char **argv) {
   setvbuf(stdout, NULL, _IONBF, 0);
   signal(SIGSEGV, on_fault);
@@ -713,6 +837,9 @@ int main(int argc, char **argv) {
   test_symm_hemm(ctx);
   test_dgetrf(ctx);
   test_dgeqrf(ctx);
+  test_inverse_family(ctx);
+  test_rank_2k(ctx);
+  test_aliases(ctx);
   /* an operation without a native implementation fails cleanly */
   dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
   CHECK(dplasma_dgelqf(ctx, A, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");

@@ -102,6 +102,20 @@ NATIVE = {
     "ungqr": "A, T, Q",
     "geqrs": "A, T, B",
     "gels": "trans, A, T, B",
+    "her2k": "uplo, trans, &alpha, A, B, beta, C",
+    "syr2k": "uplo, trans, &alpha, A, B, &beta, C",
+    "trtri": "uplo, diag, A",
+    "lauum": "uplo, A",
+    "potri": "uplo, A",
+    "poinv": "uplo, A",
+}
+# same operation natively under another name: the recursive-size hint only changes the reference's CPU
+# task granularity; a 1 x 1 ptgpanel grid is the 1-D LU; the _sync variant is the blocking call
+NATIVE_ALIAS = {
+    "potrf_rec": ("potrf", "uplo, A"),
+    "geqrf_rec": ("geqrf", "A, T"),
+    "getrf_ptgpanel": ("getrf_1d", "A, IPIV"),
+    "poinv_sync": ("poinv", "uplo, A"),
 }
 
 
@@ -243,11 +257,14 @@ def main():
                     conv.append(f"dpl_arg_{'cplx' if p in 'cz' else 'real'}({nm})")
             call = f'dpl_call_{"int" if ret == "i" else "real"}(ctx, "{p}{op}", {{{", ".join(conv)}}})'
             nat = NATIVE.get(op)
+            nop = op
+            if nat is None and op in NATIVE_ALIAS:
+                nop, nat = NATIVE_ALIAS[op]
             if nat is not None and ret == "r":   # norms: computed and returned directly
-                pre = f"if (dpl_native(ctx)) return nat_{op}(ctx, {PCODE[p]}, {nat}); "
+                pre = f"if (dpl_native(ctx)) return nat_{nop}(ctx, {PCODE[p]}, {nat}); "
                 pre_new = ""
             elif nat is not None:
-                nat_call = f"nat_{op}(ctx, {PCODE[p]}, {nat})"
+                nat_call = f"nat_{nop}(ctx, {PCODE[p]}, {nat})"
                 pre = f"if (dpl_native(ctx)) return nat_execute(ctx, {nat_call}); "
                 pre_new = f"if (dpl_native(ctx)) return nat_wrap({nat_call}); "
             else:
