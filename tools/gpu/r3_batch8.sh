@@ -7,6 +7,8 @@ timeout -k 10 200 python -u -m pytest tests/test_lu.py -m gpu -x -q --timeout 12
 rc=$?; tail -1 gpurun_out/b8_tests.log; echo "tests rc=$rc"; [ $rc -ne 0 ] && exit $rc
 DPLASMA_LU_BW=32 timeout -k 10 200 python -u -m pytest tests/test_lu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/b8_tests32.log 2>&1
 rc=$?; tail -1 gpurun_out/b8_tests32.log; echo "tests bw32 rc=$rc"; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u -m pytest tests/test_capi.py -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/b8_capi.log 2>&1
+rc=$?; grep -E "passed|failed|FAIL" gpurun_out/b8_capi.log | tail -8; echo "capi rc=$rc"; [ $rc -ne 0 ] && exit $rc
 for N in 32768 65536; do for BW in 64 32; do for LA in 0 1; do
   DPLASMA_LU_BW=$BW DPLASMA_LU_LOOKAHEAD=$LA timeout -k 10 200 python tools/bench_algo.py getrf_1d -N $N --nb 512 --runs 2 \
       > gpurun_out/b8_lu_${N}_${BW}_${LA}.log 2>&1 || { echo "lu $N $BW $LA failed"; tail -5 gpurun_out/b8_lu_${N}_${BW}_${LA}.log; exit 1; }
