@@ -390,8 +390,14 @@ class _Factor:
             self._init_batched()
             return
         self.ldp = max(16, _rup(A.m, 16))
-        nbuf = 2 if self.simple else 1
-        self.P = [torch.zeros(self.ldp * nb, dtype=dt, device=dev) for _ in range(nbuf)]
+        # general trees (several domains / TT kills per panel step, or P x Q grids): look-ahead like the
+        # simple path -- every entry's update split into column k+1 (panel stream) and the rest (update
+        # stream), so panel step k+1 overlaps the bulk update of step k; V / T per (step parity, entry)
+        self.la = not self.simple and os.environ.get("DPLASMA_QR_LOOKAHEAD", "1") != "0"
+        nent = max([len(d) + len(t) for d, t in self.plans] + [1])
+        nbuf = 2 if self.simple else (2 * nent if self.la else 1)
+        self.nent = nent
+        self.P = [torch.zeros(self.ldp * nb, dtype=dt, device=dev) for _ in range(1 if self.la else nbuf)]
         self.V = [torch.zeros(self.ldp * nb, dtype=dt, device=dev) for _ in range(nbuf)]
         self.Tm = [torch.zeros(nb * nb, dtype=dt, device=dev) for _ in range(nbuf)]
         self.R = torch.zeros(nb * nb, dtype=dt, device=dev)     # cross-row TT: the partner's tile
@@ -399,12 +405,16 @@ class _Factor:
         self.info = torch.zeros(1, dtype=torch.int32, device=dev)
         self.steps = [self._build(k) for k in range(self.kt)]
         ups = [u for st in self.steps for e in st for u in (e.get("next"), e.get("rest"), e.get("upd")) if u]
-        if self.simple:
-            self.wn = _work_buffers([e["next"] for st in self.steps for e in st if e.get("next")], dt, dev)
-            self.wr = _work_buffers([e["rest"] for st in self.steps for e in st if e.get("rest")], dt, dev)
+        if self.simple or self.la:
+            nx = [e["next"] for st in self.steps for e in st if e.get("next")]
+            rs = [e["rest"] for st in self.steps for e in st if e.get("rest")]
+            self.wn = _work_buffers(nx, dt, dev)
+            self.wr = _work_buffers(rs, dt, dev)
+            self.xtmp_n = torch.zeros(max([u.wlen for u in nx] + [1]), dtype=dt, device=dev)
+            self.xtmp = torch.zeros(max([u.wlen for u in rs] + [1]), dtype=dt, device=dev)
         else:
             self.wr = _work_buffers(ups, dt, dev)
-        self.xtmp = torch.zeros(max([u.wlen for u in ups] + [1]), dtype=dt, device=dev)
+            self.xtmp = torch.zeros(max([u.wlen for u in ups] + [1]), dtype=dt, device=dev)
 
     # ------------------------------------------------------------------ batched general trees (P == 1)
     def _init_batched(self):
@@ -578,32 +588,41 @@ class _Factor:
         doms, tts = self.plans[k]
         out = []
         cols = [n for n in range(k + 1, A.nt) if A.col_is_local(n)]
+        nxt_c = [n for n in cols if n == k + 1]
+        rest_c = [n for n in cols if n != k + 1]
         for d in doms:
             e = self._entry(k, d, False)
             if self.simple:
-                nxt = [n for n in cols if n == k + 1]
-                rest = [n for n in cols if n != k + 1]
-                e["next"] = _Left(A, d, e["voff"], e["kf"], nxt) if nxt else None
-                e["rest"] = _Left(A, d, e["voff"], e["kf"], rest) if rest else None
+                e["next"] = _Left(A, d, e["voff"], e["kf"], nxt_c) if nxt_c else None
+                e["rest"] = _Left(A, d, e["voff"], e["kf"], rest_c) if rest_c else None
+            elif self.la:
+                live = e["myline"]
+                e["next"] = _Left(A, d, e["voff"], e["kf"], nxt_c) if (nxt_c and live) else None
+                e["rest"] = _Left(A, d, e["voff"], e["kf"], rest_c) if (rest_c and live) else None
             else:
                 e["upd"] = _Left(A, d, e["voff"], e["kf"], cols) if (cols and e["myline"]) else None
             out.append(e)
         for (p, m) in tts:
             e = self._entry(k, [p, m], True)
-            if not (cols and e["myline"]):
-                e["upd"] = None
-            elif e["cross"]:   # only my process row's reflector row: partial W summed with the peer
+            if e["cross"] and e["myline"]:   # only my process row's reflector row: partial W summed with the peer
                 j = 0 if A.myrow == e["rp"] else 1
-                e["upd"] = _Left(A, [e["rows"][j]], [e["voff"][j]], e["kf"], cols)
+                rows, voff = [e["rows"][j]], [e["voff"][j]]
             else:
-                e["upd"] = _Left(A, [p, m], e["voff"], e["kf"], cols)
+                rows, voff = [p, m], e["voff"]
+            if self.la:
+                # a cross-row kill sums partial W with the peer: both rows must issue the exchange, so the
+                # next / rest parts exist on both rows whenever the other one has columns there
+                e["next"] = _Left(A, rows, voff, e["kf"], nxt_c) if (e["myline"] and nxt_c) else None
+                e["rest"] = _Left(A, rows, voff, e["kf"], rest_c) if (e["myline"] and rest_c) else None
+            else:
+                e["upd"] = _Left(A, rows, voff, e["kf"], cols) if (cols and e["myline"]) else None
             out.append(e)
         return out
 
-    def panel(self, k, e, buf):
+    def panel(self, k, e, buf, pbuf=None):
         """Assemble, factor, write back, store T of one domain / TT stack."""
         A = self.A
-        P, V, Tm = self.P[buf], self.V[buf], self.Tm[buf]
+        P, V, Tm = self.P[buf if pbuf is None else pbuf], self.V[buf], self.Tm[buf]
         ld, M, kb, kf = e["ld"], e["M"], e["kb"], e["kf"]
         if e["is_partner"]:
             # cross-row TT, partner side: R_m to the root, V2 and T back, V2 into A(m,k)
@@ -654,13 +673,27 @@ class _Factor:
             comm.bcast_tri(Tm, 0, Tm if self.A.rank == root else None, 0, e["kf"], nb, nb, False, root,
                            self.ctx.row_group)
 
-    def apply(self, e, upd, buf, work):
+    def apply(self, e, upd, buf, work, tmp=None):
         if upd is None:
             return
         red = None
         if e.get("cross"):
-            red = lambda w, peer=e["peer"]: comm.exchange_add(w, peer, self.xtmp)  # noqa: E731
+            t = self.xtmp if tmp is None else tmp
+            red = lambda w, peer=e["peer"], t=t: comm.exchange_add(w, peer, t)  # noqa: E731
         upd.run(self.A, self.V[buf], e["ld"], self.Tm[buf], self.A.nb, *work, qt=True, reduce=red)
+
+    # ---- general trees with look-ahead (self.la): V / T of entry i of step k in buffer (k % 2) * nent + i
+    def panels_la(self, k):
+        for i, e in enumerate(self.steps[k]):
+            self.panel(k, e, (k % 2) * self.nent + i, pbuf=0)
+
+    def nexts_la(self, k):
+        for i, e in enumerate(self.steps[k]):
+            self.apply(e, e.get("next"), (k % 2) * self.nent + i, self.wn, self.xtmp_n)
+
+    def rests_la(self, k):
+        for i, e in enumerate(self.steps[k]):
+            self.apply(e, e.get("rest"), (k % 2) * self.nent + i, self.wr, self.xtmp)
 
     def step_general(self, k):
         for e in self.steps[k]:
@@ -694,6 +727,13 @@ def factor_New(ctx, A, TS, TT, tree, name="geqrf") -> Taskpool:
         prev = None
         for k in range(st.kt):
             prev = tp.task(f"qr_step({k})", "update", (lambda k=k: st.step_batched(k)), [prev])
+    elif st.la:
+        prev_next = prev_rest = prev_rest2 = None
+        for k in range(st.kt):
+            pan = tp.task(f"qr_panel({k})", "panel", (lambda k=k: st.panels_la(k)), [prev_next, prev_rest2])
+            nxt = tp.task(f"qr_next({k})", "panel", (lambda k=k: st.nexts_la(k)), [pan, prev_rest])
+            rst = tp.task(f"qr_rest({k})", "update", (lambda k=k: st.rests_la(k)), [pan, prev_rest])
+            prev_next, prev_rest2, prev_rest = nxt, prev_rest, rst
     else:
         prev = None
         for k in range(st.kt):
