@@ -660,7 +660,7 @@ NatProgram* nat_trsm(dplasma_context_t* ctx, int prec, int side, int uplo, int t
 // C = alpha op(A) op(B)^{H|T} on C's uplo triangle tiles (beta on the first pass); rank-2k adds the
 // swapped product in a second launch.  Tasks on stream 1 after `prev`; returns the last task (-2: failure).
 static int add_rank_k(NatProgram& Pr, int prec, int uplo, int trans, const Scalar& alpha, const NatDesc* A,
-                      const NatDesc* B, const Scalar& beta, NatDesc* C, bool herm, int prev) {
+                      const NatDesc* B, const Scalar& beta, NatDesc* C, bool herm, int prev, bool fixdiag = true) {
   NatProgram* P = &Pr;
   const bool nt = trans == NOTRANS;
   const int ak = nt ? A->n : A->m, akb = nt ? A->nb : A->mb;
@@ -683,7 +683,7 @@ static int add_rank_k(NatProgram& Pr, int prec, int uplo, int trans, const Scala
   const int t = P->task(1, [=](hipStream_t s) { return g->launch(prec, ta, tb, alpha, a, lda, b, ldb, beta, cc, ldc, s); },
                         {prev});
   int last = t;
-  if (herm) {
+  if (herm && fixdiag) {
     // Hermitian rank-k (zherk): C's diagonal is real.  diag := (diag + conj(diag)) / 2 on the
     // diagonal tiles (geadd, diagonal part, conjugate transpose of the tile onto itself)
     std::vector<TileItem> d;
@@ -734,8 +734,9 @@ static NatProgram* rank_2k(dplasma_context_t* ctx, int prec, int uplo, int trans
     return fail(nullptr, std::string(name) + ": operands do not conform");
   NatProgram* P = new_program(c, name, false);
   const Scalar one(prec, 1.0);
-  int t = add_rank_k(*P, prec, uplo, trans, alpha, A, B, beta, C, false, -1);
-  if (t != -2) t = add_rank_k(*P, prec, uplo, trans, alpha2, B, A, one, C, herm, t);
+  // both passes use the adjoint for her2k (op(B)^H, op(A)^H); the real diagonal is restored after the second
+  int t = add_rank_k(*P, prec, uplo, trans, alpha, A, B, beta, C, herm, -1, false);
+  if (t != -2) t = add_rank_k(*P, prec, uplo, trans, alpha2, B, A, one, C, herm, t, true);
   if (t == -2) return fail(P, std::string(name) + ": device allocation failed");
   return P;
 }
