@@ -696,6 +696,12 @@ class _Factor:
             self.apply(e, e.get("rest"), (k % 2) * self.nent + i, self.wr, self.xtmp)
 
     def step_general(self, k):
+        """One whole panel step in order (LU-QR's QR steps): look-ahead entries carry next / rest parts."""
+        if self.la:
+            self.panels_la(k)
+            self.nexts_la(k)
+            self.rests_la(k)
+            return
         for e in self.steps[k]:
             self.panel(k, e, 0)
             self.apply(e, e.get("upd"), 0, self.wr)
