@@ -57,6 +57,7 @@ void dpl_set_error(const char* msg);
 
 // ---- native single-GPU engine (native.cpp)
 bool dpl_native(const dplasma_context_t* ctx);
+int nat_ctx_attr(const dplasma_context_t* ctx, bool rank);   // rank / world of a native context
 int nat_unsupported(const char* op);
 NatProgram* nat_potrf(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* A);
 NatProgram* nat_potrs(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* A, dplasma_desc_t* B);

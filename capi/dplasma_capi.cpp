@@ -257,7 +257,7 @@ DPL_CAPI void dplasma_fini(dplasma_context_t* ctx) {
 
 static int ctx_attr(const dplasma_context_t* ctx, const char* a) {
   if (!ctx) return -1;
-  if (ctx->nat) return a[0] == 'r' ? 0 : 1;   // rank 0 of a world of 1
+  if (ctx->nat) return nat_ctx_attr(ctx, a[0] == 'r');
   dpl_ensure_python();
   PyGILState_STATE st = PyGILState_Ensure();
   PyObject* v = PyObject_GetAttrString(ctx->obj, a);

@@ -18,311 +18,13 @@
 // variants), herk / syrk, the element-wise maps (geadd, tradd, lacpy, laset, lascal), the norms lange /
 // lantr, plghe, plgsy, plrnt.
 // Every other entry point returns an error on a native context.
-#include <hip/hip_runtime.h>
+#include "native_comm.h"
+#include "native_internal.h"
 
-#include <algorithm>
-#include <cmath>
-#include <cstdlib>
-#include <cstring>
-#include <functional>
-#include <memory>
-#include <string>
-#include <vector>
-
-#include "capi_bridge.h"
-
-extern "C" {  // csrc/kernels (libdplasma_kernels.so)
-int dpl_gemm_batched(int prec, int transA, int transB, int nitems, const void* items, const void* kpairs, int max_m,
-                     int max_n, const void* alpha, const void* A, int lda, const void* B, int ldb, const void* beta,
-                     void* C, int ldc, int vec_ok, int force_generic, hipStream_t st);
-int dpl_potrf_tile(int prec, int uplo, int n, void* A, long long a_off, int lda, int* info, int info_base,
-                   hipStream_t st);
-int dpl_potrf_tile_rbz(int uplo, int n, double* A, int lda, int* info, int info_base, double* zbuf, hipStream_t st);
-int dpl_potrf_zbuf_size();
-int dpl_trsm_rb(int uplo, int n, const double* L, int ldl, const double* zbuf, int nrb, const void* items, double* B,
-                int ldb, hipStream_t st);
-int dpl_trsm_batched(int prec, int side, int uplo, int trans, int diag, int nitems, const void* items, int max_m,
-                     int max_n, const void* alpha, const void* A, int lda, void* B, int ldb, int ntri,
-                     const void* tri_off, void* work, hipStream_t st);
-int dpl_generate(int prec, int kind, int nitems, const void* items, int mmax, int nmax, void* A, int lda,
-                 long long gM, unsigned long long seed, const void* bump, hipStream_t st);
-int dpl_laset(int prec, int part, int nitems, const void* items, int mmax, int nmax, const void* alpha,
-              const void* beta, void* A, int lda, hipStream_t st);
-int dpl_geadd(int prec, int part, int trans, int nitems, const void* items, int mmax, int nmax, const void* alpha,
-              const void* A, int lda, const void* beta, void* B, int ldb, int copy, hipStream_t st);
-int dpl_lascal(int prec, int part, int nitems, const void* items, int mmax, int nmax, const void* alpha, void* A,
-               int lda, hipStream_t st);
-int dpl_tile_norm(int prec, int kind, int part, int unit, int nitems, const void* items, const void* A, int lda,
-                  double* out, int ostride, hipStream_t st);
-long long dpl_lu_block_ws_bytes(int m);
-int dpl_lu_block(int prec, void* A, int ld, int m, int c0, int cend, int* ipiv, void* ws, int* cnt, int* info,
-                 int info_base, int pivot, hipStream_t st);
-int dpl_laswp_panel(int prec, void* A, int ld, int ca, int cb, const int* ipiv, int i0, int i1, hipStream_t st);
-int dpl_piv_moves(const int* ipiv, int kb, int* dst, int* src, int* cnt, hipStream_t st);
-int dpl_rows_permute(int prec, void* A, int ld, int mb, int r0, const long long* rowoff, int nrt,
-                     const long long* coloff, const int* ncols, int nct, int nb, const int* dst, const int* src,
-                     const int* cnt, int maxcnt, hipStream_t st);
-int dpl_ipiv_shift(const int* in, int* out, int n, int delta, hipStream_t st);
-long long dpl_qr_panel_ws_bytes(int prec, int nc, int kf);
-int dpl_qr_panel(int prec, void* P, int ldp, int rbl, long long rstride, int M, int nc, int kf, void* V, int ldv,
-                 void* Tm, int ldt, void* ws, int* info, hipStream_t st);
-}
-
-namespace {
-
-enum { NOTRANS = 111, TRANS = 112, CONJTRANS = 113, UPPER = 121, LOWER = 122, UPPERLOWER = 123, NONUNIT = 131,
-       LEFT = 141, RIGHT = 142 };
-enum { P_I = 1, P_S = 2, P_D = 3, P_C = 4, P_Z = 5 };   // P_I: int32 (pivot descriptors)
-
-// kernel records (csrc/kernels/common.h, gemm.hip, potrf_rb.hip)
-struct GemmItemK { long long c_off; int kt_beg, kt_cnt, m, n, flags, pad; };
-struct KPair { long long a_off, b_off; int k, pad; };
-struct TileItem { long long a_off, b_off; int m, n, gi, gj; };
-struct RbItem { long long b_off; int rows, pad; };
-static_assert(sizeof(GemmItemK) == 32 && sizeof(KPair) == 24 && sizeof(TileItem) == 32 && sizeof(RbItem) == 16,
-              "kernel record layouts");
-
-int esize(int prec) { return prec == P_S || prec == P_I ? 4 : prec == P_Z ? 16 : 8; }
-bool prec_ok(int prec) { return prec >= P_S && prec <= P_Z; }
-
-// one scalar of a precision (complex = two reals), as the kernels' host API takes it
-struct Scalar {
-  alignas(16) unsigned char b[16] = {};   // read as hipDoubleComplex (16-byte aligned loads)
-  Scalar(int prec, double re, double im = 0.0) {
-    if (prec == P_S || prec == P_C) {
-      float v[2] = {(float)re, (float)im};
-      std::memcpy(b, v, prec == P_S ? 4 : 8);
-    } else {
-      double v[2] = {re, im};
-      std::memcpy(b, v, prec == P_D ? 8 : 16);
-    }
-  }
-  Scalar(int prec, const void* p) { std::memcpy(b, p, esize(prec)); }
-  const void* ptr() const { return b; }
-};
-
-struct DevMem {
-  void* p = nullptr;
-  ~DevMem() {
-    if (p) (void)hipFree(p);
-  }
-};
-using DevPtr = std::shared_ptr<DevMem>;
-
-DevPtr dev_alloc(size_t bytes, bool zero) {
-  auto d = std::make_shared<DevMem>();
-  if (bytes == 0) bytes = 16;
-  if (hipMalloc(&d->p, bytes) != hipSuccess) return nullptr;
-  if (zero && hipMemset(d->p, 0, bytes) != hipSuccess) return nullptr;
-  return d;
-}
-
-template <typename R>
-DevPtr dev_upload(const std::vector<R>& v) {
-  auto d = dev_alloc(v.size() * sizeof(R), false);
-  if (d && !v.empty() && hipMemcpy(d->p, v.data(), v.size() * sizeof(R), hipMemcpyHostToDevice) != hipSuccess)
-    return nullptr;
-  return d;
-}
-
-}  // namespace
-
-// ----------------------------------------------------------------------------- handles
-struct NatCtx {
-  int device = 0;
-  hipStream_t st[2] = {nullptr, nullptr};   // 0: panel (high priority), 1: update
-  hipEvent_t join[2] = {nullptr, nullptr};
-  std::vector<NatProgram*> queue;
-};
-
-struct NatDesc {
-  NatCtx* ctx = nullptr;
-  int prec = P_D, es = 8, mb = 0, nb = 0, m = 0, n = 0, mt = 0, nt = 0, lld = 0;
-  char* data = nullptr;
-  bool owned = false;
-  // a T descriptor written by the native geqrf: every panel's full nb x nb compact-WY T (ld nb), the
-  // reference-layout IB x IB diagonal blocks being in the tiles themselves (unmqr / ungqr / gels read it)
-  DevPtr fullT;
-  int fullT_nb = 0, fullT_kt = 0;
-  NatDesc() = default;
-  NatDesc(const NatDesc&) = delete;             // owns its buffer: never copied (nor captured by value)
-  NatDesc& operator=(const NatDesc&) = delete;
-  long long off(int i, int j) const { return (long long)i * mb + (long long)j * nb * lld; }
-  int rows(int i) const { return std::min(mb, m - i * mb); }
-  int cols(int j) const { return std::min(nb, n - j * nb); }
-  ~NatDesc() {
-    if (owned && data) (void)hipFree(data);
-  }
-};
-
-struct NatTask {
-  int stream;
-  std::vector<int> deps;
-  std::function<int(hipStream_t)> fn;
-  bool event = false;
-};
-
-struct NatProgram {
-  NatCtx* ctx = nullptr;
-  std::string name;
-  std::vector<NatTask> tasks;
-  std::vector<hipEvent_t> ev;
-  std::vector<DevPtr> keep;      // batch records and scratch referenced by the tasks
-  std::vector<std::shared_ptr<NatDesc>> wdesc;   // workspace matrices (trmm / symm / getrf panels)
-  DevPtr info;                   // device int: first failing column (LAPACK info), 0 if none
-  int result = 0;
-  bool enqueued = false;
-
-  int task(int stream, std::function<int(hipStream_t)> fn, std::initializer_list<int> deps) {
-    NatTask t;
-    t.stream = stream;
-    t.fn = std::move(fn);
-    const int id = (int)tasks.size();
-    for (int d : deps) {
-      if (d < 0 || d >= id) continue;
-      t.deps.push_back(d);
-      if (tasks[d].stream != stream) tasks[d].event = true;
-    }
-    tasks.push_back(std::move(t));
-    return id;
-  }
-
-  // enqueue every task (stream order + events for cross-stream edges); the program starts after
-  // everything already queued on both streams (join events) -- programs compose in call order
-  int run() {
-    if (ev.empty()) {
-      ev.assign(tasks.size(), nullptr);
-      for (size_t i = 0; i < tasks.size(); ++i)
-        if (tasks[i].event && hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) return -1;
-    }
-    for (int s = 0; s < 2; ++s)
-      if (hipEventRecord(ctx->join[s], ctx->st[s]) != hipSuccess) return -1;
-    for (int s = 0; s < 2; ++s)
-      if (hipStreamWaitEvent(ctx->st[s], ctx->join[1 - s], 0) != hipSuccess) return -1;
-    // info is written by panel-stream tasks only (tile factorisations)
-    if (info && hipMemsetAsync(info->p, 0, sizeof(int), ctx->st[0]) != hipSuccess) return -1;
-    for (size_t i = 0; i < tasks.size(); ++i) {
-      NatTask& t = tasks[i];
-      hipStream_t s = ctx->st[t.stream];
-      for (int d : t.deps)
-        if (tasks[d].stream != t.stream && hipStreamWaitEvent(s, ev[d], 0) != hipSuccess) return -1;
-      const int rc = t.fn(s);
-      if (rc != 0) return rc;
-      if (t.event && hipEventRecord(ev[i], s) != hipSuccess) return -1;
-    }
-    enqueued = true;
-    return 0;
-  }
-
-  int wait() {
-    for (int s = 0; s < 2; ++s)
-      if (hipStreamSynchronize(ctx->st[s]) != hipSuccess) return -1;
-    result = 0;
-    if (info && hipMemcpy(&result, info->p, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-    enqueued = false;
-    return 0;
-  }
-
-  ~NatProgram() {
-    for (hipEvent_t e : ev)
-      if (e) (void)hipEventDestroy(e);
-  }
-};
 
 namespace {
 
 // ----------------------------------------------------------------------------- batches
-struct Gemm {
-  std::vector<GemmItemK> it;
-  std::vector<KPair> kp;
-  int max_m = 0, max_n = 0;
-  bool full = true;
-  long long align = 0;
-  DevPtr d_it, d_kp;
-
-  void add(long long c, int m, int n, const std::vector<KPair>& pairs, int mask) {
-    GemmItemK g{c, (int)kp.size(), (int)pairs.size(), m, n, mask, 0};
-    for (const KPair& p : pairs) {
-      kp.push_back(p);
-      align |= p.a_off | p.b_off;
-      if (p.k % 16) full = false;
-    }
-    if (m % 128 || n % 128) full = false;
-    align |= c;
-    it.push_back(g);
-    max_m = std::max(max_m, m);
-    max_n = std::max(max_n, n);
-  }
-  bool empty() const { return it.empty(); }
-  bool upload(NatProgram& P) {
-    if (kp.empty()) kp.push_back(KPair{0, 0, 0, 0});
-    d_it = dev_upload(it);
-    d_kp = dev_upload(kp);
-    if (!d_it || !d_kp) return false;
-    P.keep.push_back(d_it);
-    P.keep.push_back(d_kp);
-    return true;
-  }
-  int launch(int prec, int ta, int tb, const Scalar& alpha, const void* A, int lda, const void* B, int ldb,
-             const Scalar& beta, void* C, int ldc, hipStream_t st) const {
-    if (it.empty()) return 0;
-    const int ve = std::max(1, 16 / esize(prec));
-    int vec = (align % ve == 0 && lda % ve == 0 && ldb % ve == 0 && (uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0)
-                  ? 1 : 0;
-    if (vec && full) vec |= 2;
-    return dpl_gemm_batched(prec, ta, tb, (int)it.size(), d_it->p, d_kp->p, max_m, max_n, alpha.ptr(), A, lda, B,
-                            ldb, beta.ptr(), C, ldc, vec, 0, st);
-  }
-};
-
-// items sharing ONE triangular tile (dpl_trsm_batched with ntri = 1)
-struct Trsm1 {
-  std::vector<TileItem> it;
-  int max_m = 0, max_n = 0, npos = 0;
-  DevPtr d_it, d_tri, d_work;
-  long long tri = 0;
-  void add(long long b_off, int m, int n) {
-    it.push_back(TileItem{tri, b_off, m, n, 0, 0});
-    max_m = std::max(max_m, m);
-    max_n = std::max(max_n, n);
-  }
-  bool upload(NatProgram& P, int prec, int side) {
-    npos = side == LEFT ? max_m : max_n;
-    d_it = dev_upload(it);
-    d_tri = dev_upload(std::vector<long long>{tri});
-    d_work = dev_alloc((size_t)((npos + 15) / 16) * 256 * esize(prec), false);
-    if (!d_it || !d_tri || !d_work) return false;
-    P.keep.push_back(d_it);
-    P.keep.push_back(d_tri);
-    P.keep.push_back(d_work);
-    return true;
-  }
-  int launch(int prec, int side, int uplo, int trans, int diag, const Scalar& alpha, const void* A, int lda, void* B,
-             int ldb, hipStream_t st) const {
-    if (it.empty()) return 0;
-    return dpl_trsm_batched(prec, side, uplo, trans, diag, (int)it.size(), d_it->p, max_m, max_n, alpha.ptr(), A, lda,
-                            B, ldb, 1, d_tri->p, d_work->p, st);
-  }
-};
-
-NatProgram* fail(NatProgram* P, const std::string& msg) {
-  delete P;
-  dpl_set_error(msg.c_str());
-  return nullptr;
-}
-
-NatProgram* new_program(NatCtx* c, const char* name, bool with_info) {
-  NatProgram* P = new NatProgram;
-  P->ctx = c;
-  P->name = name;
-  if (with_info) P->info = dev_alloc(sizeof(int), true);
-  return P;
-}
-
-int env_int(const char* k, int dflt) {
-  const char* v = std::getenv(k);
-  return v && *v ? std::atoi(v) : dflt;
-}
 
 // ----------------------------------------------------------------------------- POTRF
 // models/potrf.py on one process: blocks of D panels; per panel POTRF(k) and its panel TRSM on the
@@ -565,10 +267,19 @@ int last_on(const NatProgram& P, int stream) {
   return -1;
 }
 
-bool same_ctx(NatCtx* c, std::initializer_list<const NatDesc*> ds, int prec) {
+// descriptors of context c and precision prec; same_ctx also refuses multi-process contexts (the
+// operations without a distributed builder), same_ctx_dist accepts them
+bool same_ctx_dist(NatCtx* c, std::initializer_list<const NatDesc*> ds, int prec) {
   for (const NatDesc* d : ds)
     if (!d || d->ctx != c || d->prec != prec) return false;
   return true;
+}
+bool same_ctx(NatCtx* c, std::initializer_list<const NatDesc*> ds, int prec) {
+  if (c && c->dist()) {
+    nat_dist_refused = true;
+    return false;
+  }
+  return same_ctx_dist(c, ds, prec);
 }
 
 }  // namespace
@@ -577,9 +288,10 @@ bool same_ctx(NatCtx* c, std::initializer_list<const NatDesc*> ds, int prec) {
 NatProgram* nat_potrf(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* dA) {
   NatCtx* c = ctx->nat;
   NatDesc* A = dA ? dA->nat : nullptr;
-  if (!same_ctx(c, {A}, prec)) return fail(nullptr, "potrf: descriptor of another context or precision");
+  if (!same_ctx_dist(c, {A}, prec)) return fail(nullptr, "potrf: descriptor of another context or precision");
   if (A->m != A->n || A->mb != A->nb || (uplo != LOWER && uplo != UPPER))
     return fail(nullptr, "potrf: square matrix with square tiles and uplo Lower/Upper required");
+  if (c->dist()) return nat_dist_potrf(c, uplo, *A);
   NatProgram* P = new_program(c, "potrf", true);
   if (!P->info || !add_potrf(*P, uplo, *A)) return fail(P, "potrf: device allocation failed");
   return P;
@@ -611,13 +323,14 @@ NatProgram* nat_gemm(dplasma_context_t* ctx, int prec, int tA, int tB, const voi
                      dplasma_desc_t* dB, const void* beta, dplasma_desc_t* dC) {
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *B = dB ? dB->nat : nullptr, *C = dC ? dC->nat : nullptr;
-  if (!same_ctx(c, {A, B, C}, prec)) return fail(nullptr, "gemm: descriptors of another context or precision");
+  if (!same_ctx_dist(c, {A, B, C}, prec)) return fail(nullptr, "gemm: descriptors of another context or precision");
   const int am = tA == NOTRANS ? A->m : A->n, ak = tA == NOTRANS ? A->n : A->m;
   const int bk = tB == NOTRANS ? B->m : B->n, bn = tB == NOTRANS ? B->n : B->m;
   const int akb = tA == NOTRANS ? A->nb : A->mb, bkb = tB == NOTRANS ? B->mb : B->nb;
   if (am != C->m || bn != C->n || ak != bk || akb != bkb || (tA == NOTRANS ? A->mb : A->nb) != C->mb ||
       (tB == NOTRANS ? B->nb : B->mb) != C->nb)
     return fail(nullptr, "gemm: operands do not conform");
+  if (c->dist()) return nat_dist_gemm(c, prec, tA, tB, Scalar(prec, alpha), *A, *B, Scalar(prec, beta), *C);
   NatProgram* P = new_program(c, "gemm", false);
   auto g = std::make_shared<Gemm>();
   const int kt = (ak + akb - 1) / akb;
@@ -789,6 +502,7 @@ struct MapBatch {
     for (int n = 0; n < B.nt; ++n)
       for (int m = 0; m < B.mt; ++m) {
         if ((uplo == LOWER && m < n) || (uplo == UPPER && m > n)) continue;
+        if (!B.local(m, n)) continue;   // (a multi-process context: this rank's tiles)
         const long long ao = A ? (trans == NOTRANS ? A->off(m, n) : A->off(n, m)) : B.off(m, n);
         it.push_back(TileItem{A ? ao : B.off(m, n), B.off(m, n), B.rows(m), B.cols(n), m * B.mb, n * B.nb});
         mm = std::max(mm, B.rows(m));
@@ -810,8 +524,9 @@ static NatProgram* map_add(dplasma_context_t* ctx, int prec, int uplo, int trans
                            dplasma_desc_t* dA, const Scalar& beta, dplasma_desc_t* dB, int copy, const char* name) {
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *B = dB ? dB->nat : nullptr;
-  if (!same_ctx(c, {A, B}, prec)) return fail(nullptr, std::string(name) + ": descriptors of another context");
+  if (!same_ctx_dist(c, {A, B}, prec)) return fail(nullptr, std::string(name) + ": descriptors of another context");
   const bool nt = trans == NOTRANS;
+  if (c->dist() && !nt) return fail(nullptr, std::string(name) + ": transposed operand on a multi-process context");
   if ((nt ? A->m : A->n) != B->m || (nt ? A->n : A->m) != B->n || (nt ? A->mb : A->nb) != B->mb ||
       (nt ? A->nb : A->mb) != B->nb)
     return fail(nullptr, std::string(name) + ": operands do not conform");
@@ -823,6 +538,7 @@ static NatProgram* map_add(dplasma_context_t* ctx, int prec, int uplo, int trans
   const char* a = A->data;
   char* b = B->data;
   P->task(1, [=](hipStream_t s) {
+    if (mb->n() == 0) return 0;
     return dpl_geadd(prec, part, trans, mb->n(), mb->items(), mb->mm, mb->nn, alpha.ptr(), a, lda, beta.ptr(), b,
                      ldb, copy, s);
   }, {});
@@ -847,7 +563,7 @@ NatProgram* nat_laset(dplasma_context_t* ctx, int prec, int uplo, const void* al
                       dplasma_desc_t* dA) {
   NatCtx* c = ctx->nat;
   NatDesc* A = dA ? dA->nat : nullptr;
-  if (!same_ctx(c, {A}, prec)) return fail(nullptr, "laset: descriptor of another context");
+  if (!same_ctx_dist(c, {A}, prec)) return fail(nullptr, "laset: descriptor of another context");
   NatProgram* P = new_program(c, "laset", false);
   auto mb = std::make_shared<MapBatch>();
   mb->build(*A, uplo, nullptr, NOTRANS);
@@ -856,6 +572,7 @@ NatProgram* nat_laset(dplasma_context_t* ctx, int prec, int uplo, const void* al
   const int part = part_of(uplo), lda = A->lld;
   char* a = A->data;
   P->task(1, [=](hipStream_t s) {
+    if (mb->n() == 0) return 0;
     return dpl_laset(prec, part, mb->n(), mb->items(), mb->mm, mb->nn, al.ptr(), be.ptr(), a, lda, s);
   }, {});
   return P;
@@ -864,7 +581,7 @@ NatProgram* nat_laset(dplasma_context_t* ctx, int prec, int uplo, const void* al
 NatProgram* nat_lascal(dplasma_context_t* ctx, int prec, int uplo, const void* alpha, dplasma_desc_t* dA) {
   NatCtx* c = ctx->nat;
   NatDesc* A = dA ? dA->nat : nullptr;
-  if (!same_ctx(c, {A}, prec)) return fail(nullptr, "lascal: descriptor of another context");
+  if (!same_ctx_dist(c, {A}, prec)) return fail(nullptr, "lascal: descriptor of another context");
   NatProgram* P = new_program(c, "lascal", false);
   auto mb = std::make_shared<MapBatch>();
   mb->build(*A, uplo, nullptr, NOTRANS);
@@ -873,6 +590,7 @@ NatProgram* nat_lascal(dplasma_context_t* ctx, int prec, int uplo, const void* a
   const int part = part_of(uplo), lda = A->lld;
   char* a = A->data;
   P->task(1, [=](hipStream_t s) {
+    if (mb->n() == 0) return 0;
     return dpl_lascal(prec, part, mb->n(), mb->items(), mb->mm, mb->nn, al.ptr(), a, lda, s);
   }, {});
   return P;
@@ -894,38 +612,43 @@ static double norm_tiles(NatDesc& A, int ntype, int uplo, bool unit, hipStream_t
   for (int n = 0; n < A.nt; ++n)
     for (int m = 0; m < A.mt; ++m) {
       if ((uplo == LOWER && m < n) || (uplo == UPPER && m > n)) continue;
+      if (!A.local(m, n)) continue;   // a multi-process context: partials of this rank's tiles, combined below
       it.push_back(TileItem{A.off(m, n), 0, A.rows(m), A.cols(n), m * A.mb, n * A.nb});
       mn.emplace_back(m, n);
       mm = std::max(mm, A.rows(m));
       nn = std::max(nn, A.cols(n));
     }
-  if (it.empty()) { ok = true; return 0.0; }
   const int os = kind == 0 ? 1 : kind == 1 ? nn : kind == 2 ? mm : 2;
-  DevPtr d = dev_upload(it), out = dev_alloc(sizeof(double) * it.size() * os, true);
-  if (!d || !out) return 0.0;
-  // the norm reads A after everything already queued on the context (both streams)
-  if (hipDeviceSynchronize() != hipSuccess) return 0.0;
-  if (dpl_tile_norm(A.prec, kind, part_of(uplo), unit ? 1 : 0, (int)it.size(), d->p, A.data, A.lld,
-                    (double*)out->p, os, st) != 0)
-    return 0.0;
   std::vector<double> h(it.size() * os);
-  if (hipStreamSynchronize(st) != hipSuccess ||
-      hipMemcpy(h.data(), out->p, sizeof(double) * h.size(), hipMemcpyDeviceToHost) != hipSuccess)
-    return 0.0;
-  ok = true;
+  // the norm reads A after everything already queued on the context (every stream)
+  if (hipDeviceSynchronize() != hipSuccess) return 0.0;
+  if (!it.empty()) {
+    DevPtr d = dev_upload(it), out = dev_alloc(sizeof(double) * it.size() * os, true);
+    if (!d || !out) return 0.0;
+    if (dpl_tile_norm(A.prec, kind, part_of(uplo), unit ? 1 : 0, (int)it.size(), d->p, A.data, A.lld,
+                      (double*)out->p, os, st) != 0)
+      return 0.0;
+    if (hipStreamSynchronize(st) != hipSuccess ||
+        hipMemcpy(h.data(), out->p, sizeof(double) * h.size(), hipMemcpyDeviceToHost) != hipSuccess)
+      return 0.0;
+  }
+  NatComm* comm = A.ctx->comm;
   double r = 0.0;
   if (kind == 0) {
     for (double v : h) r = std::max(r, v);
+    if (comm && comm->allreduce(&r, 1, true) != 0) return 0.0;
   } else if (kind == 3) {   // (scale, ssq) per tile -> sqrt(sum scale^2 ssq), rescaled by the largest scale
     double big = 0.0;
     for (size_t t = 0; t < it.size(); ++t) big = std::max(big, h[2 * t]);
-    if (big > 0) {
+    if (comm && comm->allreduce(&big, 1, true) != 0) return 0.0;
+    double q2 = 0.0;
+    if (big > 0)
       for (size_t t = 0; t < it.size(); ++t) {
         const double q = h[2 * t] / big;
-        r += q * q * h[2 * t + 1];
+        q2 += q * q * h[2 * t + 1];
       }
-      r = big * std::sqrt(r);
-    }
+    if (comm && comm->allreduce(&q2, 1, false) != 0) return 0.0;
+    r = big > 0 ? big * std::sqrt(q2) : 0.0;
   } else {                  // column (one) / row (inf) sums over the tiles of a tile column / row
     std::vector<double> acc(kind == 1 ? A.n : A.m, 0.0);
     for (size_t t = 0; t < it.size(); ++t) {
@@ -933,14 +656,16 @@ static double norm_tiles(NatDesc& A, int ntype, int uplo, bool unit, hipStream_t
       const int len = kind == 1 ? A.cols(mn[t].second) : A.rows(mn[t].first);
       for (int j = 0; j < len; ++j) acc[base + j] += h[t * os + j];
     }
+    if (comm && !acc.empty() && comm->allreduce(acc.data(), (int)acc.size(), false) != 0) return 0.0;
     for (double v : acc) r = std::max(r, v);
   }
+  ok = true;
   return r;
 }
 
 double nat_lange(dplasma_context_t* ctx, int prec, int ntype, dplasma_desc_t* dA) {
   NatDesc* A = dA ? dA->nat : nullptr;
-  if (!same_ctx(ctx->nat, {A}, prec)) { dpl_set_error("lange: descriptor of another context"); return NAN; }
+  if (!same_ctx_dist(ctx->nat, {A}, prec)) { dpl_set_error("lange: descriptor of another context"); return NAN; }
   bool ok;
   const double r = norm_tiles(*A, ntype, UPPERLOWER, false, ctx->nat->st[1], ok);
   if (!ok) { dpl_set_error("lange: unsupported norm or kernel failure"); return NAN; }
@@ -949,7 +674,7 @@ double nat_lange(dplasma_context_t* ctx, int prec, int ntype, dplasma_desc_t* dA
 
 double nat_lantr(dplasma_context_t* ctx, int prec, int ntype, int uplo, int diag, dplasma_desc_t* dA) {
   NatDesc* A = dA ? dA->nat : nullptr;
-  if (!same_ctx(ctx->nat, {A}, prec) || (uplo != LOWER && uplo != UPPER)) {
+  if (!same_ctx_dist(ctx->nat, {A}, prec) || (uplo != LOWER && uplo != UPPER)) {
     dpl_set_error("lantr: bad descriptor or uplo");
     return NAN;
   }
@@ -963,13 +688,14 @@ static NatProgram* generator(dplasma_context_t* ctx, int prec, int kind, int upl
                              dplasma_desc_t* dA, unsigned long long seed, const char* name) {
   NatCtx* c = ctx->nat;
   NatDesc* A = dA ? dA->nat : nullptr;
-  if (!same_ctx(c, {A}, prec)) return fail(nullptr, std::string(name) + ": descriptor of another context");
+  if (!same_ctx_dist(c, {A}, prec)) return fail(nullptr, std::string(name) + ": descriptor of another context");
   NatProgram* P = new_program(c, name, false);
   std::vector<TileItem> it;
   int mm = 0, nn = 0;
   for (int n = 0; n < A->nt; ++n)
     for (int m = 0; m < A->mt; ++m) {
       if ((uplo == LOWER && m < n) || (uplo == UPPER && m > n)) continue;
+      if (!A->local(m, n)) continue;   // global element coordinates: every rank draws its own tiles
       it.push_back(TileItem{A->off(m, n), 0, A->rows(m), A->cols(n), m * A->mb, n * A->nb});
       mm = std::max(mm, A->rows(m));
       nn = std::max(nn, A->cols(n));
@@ -981,6 +707,7 @@ static NatProgram* generator(dplasma_context_t* ctx, int prec, int kind, int upl
   const long long gM = A->m;
   char* base = A->data;
   P->task(1, [=](hipStream_t s) {
+    if (ni == 0) return 0;
     return dpl_generate(prec, kind, ni, d->p, mm, nn, base, lda, gM, seed, bump.ptr(), s);
   }, {});
   return P;
@@ -1033,9 +760,11 @@ int nat_unsupported(const char* op) {
 
 bool dpl_native(const dplasma_context_t* ctx) { return ctx && ctx->nat; }
 
+int nat_ctx_attr(const dplasma_context_t* ctx, bool rank) { return rank ? ctx->nat->rank : ctx->nat->world; }
+
 extern "C" {
 
-DPL_CAPI dplasma_context_t* dplasma_init_native(int device) {
+static NatCtx* nat_ctx_create(int device) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
     dpl_set_error("dplasma_init_native: no such GPU");
@@ -1046,13 +775,50 @@ DPL_CAPI dplasma_context_t* dplasma_init_native(int device) {
   c->device = device;
   int lo = 0, hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-  if (hipStreamCreateWithPriority(&c->st[0], hipStreamNonBlocking, hi) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->st[1], hipStreamNonBlocking, lo) != hipSuccess ||
-      hipEventCreateWithFlags(&c->join[0], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->join[1], hipEventDisableTiming) != hipSuccess) {
+  bool ok = true;
+  for (int s = 0; s < NAT_NSTREAM; ++s)
+    ok = ok && hipStreamCreateWithPriority(&c->st[s], hipStreamNonBlocking, s == 1 ? lo : hi) == hipSuccess &&
+         hipEventCreateWithFlags(&c->join[s], hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
     dpl_set_error("dplasma_init_native: stream creation failed");
-    delete c;
+    nat_ctx_destroy(c);
     return nullptr;
+  }
+  return c;
+}
+
+DPL_CAPI dplasma_context_t* dplasma_init_native(int device) {
+  NatCtx* c = nat_ctx_create(device);
+  if (!c) return nullptr;
+  dplasma_context_t* ctx = new dplasma_context_s;
+  ctx->nat = c;
+  return ctx;
+}
+
+// one process per GPU of a P x (world / P) grid (the reference's MPI ranks): tiles move between the
+// ranks through RCCL (one GPU per rank) or node-local files (ranks sharing a GPU; one-GPU rehearsals),
+// see native_comm.cpp; rdv_dir is a fresh directory every rank of the job can reach (the rendezvous)
+DPL_CAPI dplasma_context_t* dplasma_init_native_dist(int device, int rank, int world, int P, const char* rdv_dir) {
+  if (world < 1 || rank < 0 || rank >= world || P < 1 || world % P != 0) {
+    dpl_set_error("dplasma_init_native_dist: rank / world / P do not form a P x Q grid");
+    return nullptr;
+  }
+  NatCtx* c = nat_ctx_create(device);
+  if (!c) return nullptr;
+  c->rank = rank;
+  c->world = world;
+  c->P = P;
+  c->Q = world / P;
+  c->myrow = rank / c->Q;
+  c->mycol = rank % c->Q;
+  if (world > 1) {
+    std::string err;
+    c->comm = nat_comm_create(rank, world, device, rdv_dir, err);
+    if (!c->comm) {
+      dpl_set_error(("dplasma_init_native_dist: " + err).c_str());
+      nat_ctx_destroy(c);
+      return nullptr;
+    }
   }
   dplasma_context_t* ctx = new dplasma_context_s;
   ctx->nat = c;
@@ -1061,9 +827,10 @@ DPL_CAPI dplasma_context_t* dplasma_init_native(int device) {
 
 }  // extern "C"
 
-void nat_fini(dplasma_context_t* ctx) {
-  NatCtx* c = ctx->nat;
-  for (int s = 0; s < 2; ++s) {
+void nat_ctx_destroy(NatCtx* c) {
+  if (c->comm) nat_comm_destroy(c->comm);
+  c->comm = nullptr;
+  for (int s = 0; s < NAT_NSTREAM; ++s) {
     if (c->st[s]) {
       (void)hipStreamSynchronize(c->st[s]);
       (void)hipStreamDestroy(c->st[s]);
@@ -1073,10 +840,15 @@ void nat_fini(dplasma_context_t* ctx) {
   delete c;
 }
 
+void nat_fini(dplasma_context_t* ctx) { nat_ctx_destroy(ctx->nat); }
+
 dplasma_desc_t* nat_desc(dplasma_context_t* ctx, int prec, int mb, int nb, int m, int n, int P, int Q, void* data,
                          int lld, int on_device) {
-  if ((!prec_ok(prec) && prec != P_I) || mb <= 0 || nb <= 0 || m < 0 || n < 0 || P > 1 || Q > 1) {
-    dpl_set_error("native descriptor: one process (P = Q = 1), positive tile sizes, s/d/c/z");
+  NatCtx* c = ctx->nat;
+  if (P <= 0 || Q <= 0) P = c->P, Q = c->Q;   // the context's grid
+  if ((!prec_ok(prec) && prec != P_I) || mb <= 0 || nb <= 0 || m < 0 || n < 0 || P != c->P || Q != c->Q) {
+    dpl_set_error("native descriptor: the context's process grid (P = Q = 1 on one process), positive tile "
+                  "sizes, s/d/c/z");
     return nullptr;
   }
   if (data && !on_device) {
@@ -1093,8 +865,14 @@ dplasma_desc_t* nat_desc(dplasma_context_t* ctx, int prec, int mb, int nb, int m
   d->n = n;
   d->mt = (m + mb - 1) / mb;
   d->nt = (n + nb - 1) / nb;
+  d->P = P;
+  d->Q = Q;
+  d->myrow = c->myrow;
+  d->mycol = c->mycol;
+  d->lm = nat_numroc(m, mb, c->myrow, P);
+  d->ln = nat_numroc(n, nb, c->mycol, Q);
   if (data) {
-    if (lld < std::max(1, m)) {
+    if (lld < std::max(1, d->lm)) {
       delete d;
       dpl_set_error("native descriptor: lld < m");
       return nullptr;
@@ -1103,10 +881,13 @@ dplasma_desc_t* nat_desc(dplasma_context_t* ctx, int prec, int mb, int nb, int m
     d->lld = lld;
   } else {
     // 128-byte aligned columns for the vector paths; pivot vectors (int32, 1 x n) stay contiguous
-    d->lld = prec == P_I ? std::max(1, m) : std::max(16, (m + 15) / 16 * 16);
+    d->lld = prec == P_I ? std::max(1, d->lm) : std::max(16, (d->lm + 15) / 16 * 16);
     void* p = nullptr;
-    const size_t bytes = (size_t)d->lld * std::max(1, n) * d->es;
-    if (hipMalloc(&p, bytes) != hipSuccess || hipMemset(p, 0, bytes) != hipSuccess) {
+    const size_t bytes = (size_t)d->lld * std::max(1, d->ln) * d->es;
+    // hipMemset runs on the null stream, which the context's non-blocking streams do not wait for: the zeros
+    // must have landed before any kernel of those streams touches the buffer
+    if (hipMalloc(&p, bytes) != hipSuccess || hipMemset(p, 0, bytes) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {
       delete d;
       dpl_set_error("native descriptor: device allocation failed");
       return nullptr;
@@ -1121,18 +902,30 @@ dplasma_desc_t* nat_desc(dplasma_context_t* ctx, int prec, int mb, int nb, int m
 
 void nat_desc_free(dplasma_desc_t* A) { delete A->nat; }
 
+// host LAPACK-layout matrix (the whole m x n matrix on every rank) <-> this rank's tiles
 int nat_desc_io(const dplasma_desc_t* A, void* host, int lda, bool to_device) {
   const NatDesc* d = A->nat;
   if (lda < std::max(1, d->m)) return nat_unsupported("desc_set/get_lapack: lda < m");
-  for (int s = 0; s < 2; ++s)
+  for (int s = 0; s < NAT_NSTREAM; ++s)
     if (hipStreamSynchronize(d->ctx->st[s]) != hipSuccess) return -1;
-  const size_t w = (size_t)d->m * d->es;
-  if (w == 0 || d->n == 0) return 0;
-  const hipError_t e = to_device ? hipMemcpy2D(d->data, (size_t)d->lld * d->es, host, (size_t)lda * d->es, w, d->n,
-                                               hipMemcpyHostToDevice)
-                                 : hipMemcpy2D(host, (size_t)lda * d->es, d->data, (size_t)d->lld * d->es, w, d->n,
-                                               hipMemcpyDeviceToHost);
-  return e == hipSuccess ? 0 : -1;
+  if (d->m == 0 || d->n == 0) return 0;
+  const size_t hp = (size_t)lda * d->es, dp = (size_t)d->lld * d->es;
+  if (!d->dist()) {
+    const size_t w = (size_t)d->m * d->es;
+    const hipError_t e = to_device ? hipMemcpy2D(d->data, dp, host, hp, w, d->n, hipMemcpyHostToDevice)
+                                   : hipMemcpy2D(host, hp, d->data, dp, w, d->n, hipMemcpyDeviceToHost);
+    return e == hipSuccess ? 0 : -1;
+  }
+  for (int j = d->mycol; j < d->nt; j += d->Q)
+    for (int i = d->myrow; i < d->mt; i += d->P) {
+      char* h = (char*)host + ((size_t)i * d->mb + (size_t)j * d->nb * lda) * d->es;
+      char* g = d->data + d->off(i, j) * d->es;
+      const size_t w = (size_t)d->rows(i) * d->es;
+      const hipError_t e = to_device ? hipMemcpy2D(g, dp, h, hp, w, d->cols(j), hipMemcpyHostToDevice)
+                                     : hipMemcpy2D(h, hp, g, dp, w, d->cols(j), hipMemcpyDeviceToHost);
+      if (e != hipSuccess) return -1;
+    }
+  return 0;
 }
 
 int nat_add(dplasma_context_t* ctx, dplasma_taskpool_t* tp) {

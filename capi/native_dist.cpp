@@ -1,0 +1,274 @@
+// Multi-process native engine: Cholesky and SUMMA GEMM over a P x Q grid of ranks (one process per
+// GPU), compiled in C++ into stream programs exactly like the one-process engine (native.cpp), with the
+// tile traffic as grouped point-to-point exchanges on the context's communication stream
+// (native_comm.h).  No Python anywhere: this is the C library a ScaLAPACK program links against.
+//
+// POTRF (reference: src/zpotrf_L.jdf / zpotrf_U.jdf -- POTRF(k) -> TRSM(m,k) -> HERK/GEMM(m,n,k)
+// with the tiles travelling along the JDF's remote edges):
+//   step k:  POTRF(k) on the owner of the diagonal tile (panel stream)
+//            -> DIAG exchange: the factor to the ranks holding panel tiles (communication stream)
+//            -> TRSM of this rank's panel tiles, one batched launch; pack them into the panel slots
+//            -> PANEL exchange: every panel tile to exactly the ranks whose trailing tiles read it
+//            -> NEXT (the trailing tiles of column k+1, panel stream) and REST (all others, update
+//               stream): one MFMA GEMM launch each, A and B operands read from the panel slots.
+//   Look-ahead 1: POTRF(k+1) needs NEXT(k) and REST(k-1) only, so step k+1's panel, its exchanges and
+//   its TRSM run beside REST(k) -- the critical-path role of the reference's high_priority POTRF /
+//   TRSM classes.  Panel slots are double-buffered by step parity.
+// GEMM (reference: src/zgemm_NN_summa.jdf and the SUMMA variants): per chunk of kc k-steps, the owners
+//   pack their op(A)(m, k) / op(B)(k, n) tiles, one exchange sends each to the ranks holding a C tile of
+//   its block row / column, and one GEMM launch covers every local C tile with k-runs over the chunk;
+//   chunk c+1's pack and exchange overlap chunk c's GEMM (double-buffered).
+#include <algorithm>
+#include <set>
+
+#include "native_comm.h"
+#include "native_internal.h"
+
+namespace {
+
+struct CopyBatch {   // packs local tiles into contiguous slots: one dpl_geadd (copy) launch
+  std::vector<TileItem> it;
+  int mm = 0, nn = 0;
+  DevPtr d;
+  void add(long long src, long long dst, int m, int n) {
+    it.push_back(TileItem{src, dst, m, n, 0, 0});
+    mm = std::max(mm, m);
+    nn = std::max(nn, n);
+  }
+  bool upload(NatProgram& P) {
+    if (it.empty()) return true;
+    d = dev_upload(it);
+    if (!d) return false;
+    P.keep.push_back(d);
+    return true;
+  }
+  int launch(int prec, const char* A, int lda, char* B, int ldb, hipStream_t s) const {
+    if (it.empty()) return 0;
+    const Scalar one(prec, 1.0), zero(prec, 0.0);
+    return dpl_geadd(prec, 0, NOTRANS, (int)it.size(), d->p, mm, nn, one.ptr(), A, lda, zero.ptr(), B, ldb, 1, s);
+  }
+};
+
+// one exchange task: the messages are fixed when the program is built
+int add_exchange(NatProgram& Pr, std::vector<NatMsg> sends, std::vector<NatMsg> recvs, std::initializer_list<int> deps) {
+  if (sends.empty() && recvs.empty()) return -1;
+  NatComm* comm = Pr.ctx->comm;
+  auto s = std::make_shared<std::vector<NatMsg>>(std::move(sends));
+  auto r = std::make_shared<std::vector<NatMsg>>(std::move(recvs));
+  return Pr.task(2, [=](hipStream_t st) { return comm->exchange(*s, *r, st); }, deps);
+}
+
+int either(int a, int b) { return a >= 0 ? a : b; }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------- POTRF
+NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
+  const int prec = A.prec, nt = A.nt, mb = A.mb, es = A.es, me = c->rank, Pg = A.P, Qg = A.Q;
+  const bool lower = uplo == LOWER;
+  NatProgram* Pr = new_program(c, "potrf", true);
+  if (!Pr->info) return fail(Pr, "potrf: device allocation failed");
+  const size_t slot_elems = (size_t)mb * mb;
+  DevPtr W = dev_alloc(2 * (size_t)std::max(1, nt) * slot_elems * es, false);
+  if (!W) return fail(Pr, "potrf: panel slots: device allocation failed");
+  Pr->keep.push_back(W);
+  char* Wb[2] = {(char*)W->p, (char*)W->p + (size_t)nt * slot_elems * es};
+  auto slot = [&](int i) { return (long long)i * (long long)slot_elems; };
+  auto tc = [&](int i, int k) { return lower ? std::make_pair(i, k) : std::make_pair(k, i); };
+  auto own = [&](int i, int k) { const auto t = tc(i, k); return A.owner(t.first, t.second); };
+  // trailing tiles of step k: lower {(m, n): k < n <= m}, upper {(m, n): k < m <= n}; C(m, n) reads
+  // panel tiles m and n, so panel tile i goes to the owners of row i and column i of that set
+  auto consumers = [&](int k, int i) {
+    std::set<int> s;
+    const int a0 = lower ? k + 1 : i, a1 = lower ? i + 1 : nt;     // C(i, n), n in [a0, a1)
+    const int b0 = lower ? i : k + 1, b1 = lower ? nt : i + 1;     // C(m, i), m in [b0, b1)
+    for (int n = a0; n < std::min(a1, a0 + Qg); ++n) s.insert(A.owner(i, n));
+    for (int m = b0; m < std::min(b1, b0 + Pg); ++m) s.insert(A.owner(m, i));
+    return s;
+  };
+  const int tA = lower ? NOTRANS : CONJTRANS, tB = lower ? CONJTRANS : NOTRANS;
+  const int side = lower ? RIGHT : LEFT, tri_mask = lower ? 1 : 2;
+  const Scalar one(prec, 1.0), m_one(prec, -1.0);
+  char* base = A.data;
+  const int ld = A.lld;
+  int* info = (int*)Pr->info->p;
+  const size_t sbytes = slot_elems * es;
+
+  int next_prev = -1;                    // NEXT(k-1) (or the last panel-stream task of step k-1)
+  std::vector<int> rest(nt, -1), xch(nt, -1);   // latest update-stream / communication task after step k
+  for (int k = 0; k < nt; ++k) {
+    const int b = k % 2, kb = A.rows(k);
+    const int rest_km1 = k >= 1 ? rest[k - 1] : -1, rest_km2 = k >= 2 ? rest[k - 2] : -1;
+    const int xch_km2 = k >= 2 ? xch[k - 2] : -1;
+    const int own_k = A.owner(k, k);
+    char* wb = Wb[b];
+    // POTRF(k): the diagonal tile has every update of steps < k (NEXT(k-1) and REST(k-2))
+    int t_diag = -1;
+    if (me == own_k) {
+      const long long dk = A.off(k, k);
+      const int t_potrf = Pr->task(0, [=](hipStream_t s) {
+        return dpl_potrf_tile(prec, uplo, kb, base, dk, ld, info, k * mb, s);
+      }, {next_prev, rest_km2});
+      char* dst = wb + slot(k) * es;   // (run-time lambdas capture values only)
+      t_diag = Pr->task(0, [=](hipStream_t s) {
+        return hipMemcpy2DAsync(dst, (size_t)mb * es, base + dk * es, (size_t)ld * es, (size_t)kb * es, kb,
+                                hipMemcpyDeviceToDevice, s) == hipSuccess ? 0 : -1;
+      }, {t_potrf, xch_km2});
+    }
+    // DIAG exchange: the factor to every other rank holding a panel tile of step k
+    std::set<int> drc;
+    for (int i = k + 1; i < std::min(nt, k + 1 + (lower ? Pg : Qg)); ++i) drc.insert(own(i, k));
+    drc.erase(own_k);
+    std::vector<NatMsg> ds, dr;
+    if (me == own_k)
+      for (int r : drc) ds.push_back(NatMsg{r, wb + slot(k) * es, sbytes});
+    if (drc.count(me)) dr.push_back(NatMsg{own_k, wb + slot(k) * es, sbytes});
+    const int t_xd = add_exchange(*Pr, ds, dr, {t_diag, rest_km2, next_prev, xch_km2});
+    // TRSM of this rank's panel tiles against the factor in slot k, then pack them into their slots
+    auto tr = std::make_shared<Trsm1>();
+    auto pk = std::make_shared<CopyBatch>();
+    tr->tri = slot(k);
+    for (int i = k + 1; i < nt; ++i) {
+      const auto t = tc(i, k);
+      if (!A.local(t.first, t.second)) continue;
+      tr->add(A.off(t.first, t.second), A.rows(t.first), A.cols(t.second));
+      pk->add(A.off(t.first, t.second), slot(i), A.rows(t.first), A.cols(t.second));
+    }
+    int t_pack = -1;
+    if (!tr->it.empty()) {
+      if (!tr->upload(*Pr, prec, side) || !pk->upload(*Pr)) return fail(Pr, "potrf: device allocation failed");
+      const int t_trsm = Pr->task(0, [=](hipStream_t s) {
+        return tr->launch(prec, side, uplo, CONJTRANS, NONUNIT, one, wb, mb, base, ld, s);
+      }, {either(t_xd, t_diag), next_prev, rest_km2});
+      t_pack = Pr->task(0, [=](hipStream_t s) { return pk->launch(prec, base, ld, wb, mb, s); }, {t_trsm, xch_km2});
+    }
+    // PANEL exchange: tile i from its owner to the ranks whose trailing tiles read it (ascending i:
+    // both sides of a pair enumerate their messages in the same order)
+    std::vector<NatMsg> ps, pr;
+    for (int i = k + 1; i < nt; ++i) {
+      const int src = own(i, k);
+      std::set<int> cs = consumers(k, i);
+      cs.erase(src);
+      if (src == me)
+        for (int r : cs) ps.push_back(NatMsg{r, wb + slot(i) * es, sbytes});
+      else if (cs.count(me))
+        pr.push_back(NatMsg{src, wb + slot(i) * es, sbytes});
+    }
+    const int t_xp = add_exchange(*Pr, ps, pr, {t_pack, t_xd, rest_km2, next_prev});
+    // trailing update: NEXT (column / row k+1) on the panel stream, REST on the update stream
+    auto gn = std::make_shared<Gemm>(), gr = std::make_shared<Gemm>();
+    for (int n_ = k + 1; n_ < nt; ++n_)
+      for (int m_ = n_; m_ < nt; ++m_) {
+        const int m = lower ? m_ : n_, n = lower ? n_ : m_;   // C(m, n) in the stored triangle
+        if (!A.local(m, n)) continue;
+        auto& g = (n_ == k + 1) ? gn : gr;
+        g->add(A.off(m, n), A.rows(m), A.cols(n), {KPair{slot(m), slot(n), kb, 0}}, m == n ? tri_mask : 0);
+      }
+    const int t_in = either(t_xp, either(t_pack, t_xd));
+    auto gemm = [=](std::shared_ptr<Gemm> g) {
+      return [=](hipStream_t s) { return g->launch(prec, tA, tB, m_one, wb, mb, wb, mb, one, base, ld, s); };
+    };
+    int t_next = -1;
+    if (!gn->empty()) {
+      if (!gn->upload(*Pr)) return fail(Pr, "potrf: device allocation failed");
+      t_next = Pr->task(0, gemm(gn), {t_in, rest_km1});
+    }
+    int t_rest = -1;
+    if (!gr->empty()) {
+      if (!gr->upload(*Pr)) return fail(Pr, "potrf: device allocation failed");
+      t_rest = Pr->task(1, gemm(gr), {t_in, rest_km1});
+    }
+    next_prev = either(t_next, either(t_pack, either(t_diag, next_prev)));
+    rest[k] = either(t_rest, rest_km1);
+    xch[k] = either(t_xp, either(t_xd, k >= 1 ? xch[k - 1] : -1));
+  }
+  return Pr;
+}
+
+// ----------------------------------------------------------------------------------------------- GEMM
+NatProgram* nat_dist_gemm(NatCtx* c, int prec, int tA, int tB, const Scalar& alpha, NatDesc& A, NatDesc& B,
+                          const Scalar& beta, NatDesc& C) {
+  const int es = C.es, me = c->rank;
+  const bool an = tA == NOTRANS, bn = tB == NOTRANS;
+  const int kt = an ? A.nt : A.mt;
+  NatProgram* Pr = new_program(c, "gemm", false);
+  if (kt == 0) return Pr;
+  const int kc = std::max(1, std::min(kt, env_int("DPLASMA_NATIVE_SUMMA_K", 4)));
+  const size_t sa = (size_t)A.mb * A.nb, sb = (size_t)B.mb * B.nb;   // slots: stored tiles, ld mb
+  DevPtr WA = dev_alloc(2 * (size_t)kc * C.mt * sa * es, false), WB = dev_alloc(2 * (size_t)kc * C.nt * sb * es, false);
+  if (!WA || !WB) return fail(Pr, "gemm: SUMMA slots: device allocation failed");
+  Pr->keep.push_back(WA);
+  Pr->keep.push_back(WB);
+  auto aslot = [&](int kk, int m) { return ((long long)kk * C.mt + m) * (long long)sa; };
+  auto bslot = [&](int kk, int n) { return ((long long)kk * C.nt + n) * (long long)sb; };
+  // ranks holding a C tile of block row m / block column n
+  std::set<int> qs, ps;
+  for (int n = 0; n < std::min(C.nt, C.Q); ++n) qs.insert(n % C.Q);
+  for (int m = 0; m < std::min(C.mt, C.P); ++m) ps.insert(m % C.P);
+  const Scalar one(prec, 1.0);
+  const int nch = (kt + kc - 1) / kc;
+  std::vector<int> gem(nch, -1), xch(nch, -1);
+  for (int ch = 0; ch < nch; ++ch) {
+    const int k0 = ch * kc, k1 = std::min(kt, k0 + kc), b = ch % 2;
+    char* wa = (char*)WA->p + (size_t)b * kc * C.mt * sa * es;
+    char* wb = (char*)WB->p + (size_t)b * kc * C.nt * sb * es;
+    const int g2 = ch >= 2 ? gem[ch - 2] : -1, x2 = ch >= 2 ? xch[ch - 2] : -1;
+    auto pa = std::make_shared<CopyBatch>(), pb = std::make_shared<CopyBatch>();
+    std::vector<NatMsg> snd, rcv;
+    for (int k = k0; k < k1; ++k)
+      for (int m = 0; m < C.mt; ++m) {   // op(A)(m, k): stored tile (m, k) or (k, m)
+        const int si = an ? m : k, sj = an ? k : m, src = A.owner(si, sj);
+        void* p = wa + aslot(k - k0, m) * es;
+        if (src == me) {
+          pa->add(A.off(si, sj), aslot(k - k0, m), A.rows(si), A.cols(sj));
+          for (int q : qs) {
+            const int r = (m % C.P) * C.Q + q;
+            if (r != me) snd.push_back(NatMsg{r, p, sa * es});
+          }
+        } else if (m % C.P == C.myrow && qs.count(C.mycol)) {
+          rcv.push_back(NatMsg{src, p, sa * es});
+        }
+      }
+    for (int k = k0; k < k1; ++k)
+      for (int n = 0; n < C.nt; ++n) {   // op(B)(k, n): stored tile (k, n) or (n, k)
+        const int si = bn ? k : n, sj = bn ? n : k, src = B.owner(si, sj);
+        void* p = wb + bslot(k - k0, n) * es;
+        if (src == me) {
+          pb->add(B.off(si, sj), bslot(k - k0, n), B.rows(si), B.cols(sj));
+          for (int pr : ps) {
+            const int r = pr * C.Q + n % C.Q;
+            if (r != me) snd.push_back(NatMsg{r, p, sb * es});
+          }
+        } else if (n % C.Q == C.mycol && ps.count(C.myrow)) {
+          rcv.push_back(NatMsg{src, p, sb * es});
+        }
+      }
+    if (!pa->upload(*Pr) || !pb->upload(*Pr)) return fail(Pr, "gemm: device allocation failed");
+    const char *a = A.data, *bb = B.data;
+    const int lda = A.lld, ldb = B.lld, amb = A.mb, bmb = B.mb;
+    int t_pack = -1;
+    if (!pa->it.empty() || !pb->it.empty())
+      t_pack = Pr->task(0, [=](hipStream_t s) {
+        const int rc = pa->launch(prec, a, lda, wa, amb, s);
+        return rc ? rc : pb->launch(prec, bb, ldb, wb, bmb, s);
+      }, {g2, x2});
+    const int t_x = add_exchange(*Pr, snd, rcv, {t_pack, g2});
+    xch[ch] = either(t_x, ch >= 1 ? xch[ch - 1] : -1);
+    auto g = std::make_shared<Gemm>();
+    for (int n = C.mycol; n < C.nt; n += C.Q)
+      for (int m = C.myrow; m < C.mt; m += C.P) {
+        std::vector<KPair> kp;
+        for (int k = k0; k < k1; ++k) kp.push_back(KPair{aslot(k - k0, m), bslot(k - k0, n), an ? A.cols(k) : A.rows(k), 0});
+        g->add(C.off(m, n), C.rows(m), C.cols(n), kp, 0);
+      }
+    if (g->empty()) continue;
+    if (!g->upload(*Pr)) return fail(Pr, "gemm: device allocation failed");
+    const Scalar be = ch == 0 ? beta : one;
+    char* cc = C.data;
+    const int ldc = C.lld;
+    gem[ch] = Pr->task(1, [=](hipStream_t s) {
+      return g->launch(prec, tA, tB, alpha, wa, amb, wb, bmb, be, cc, ldc, s);
+    }, {either(t_x, t_pack)});
+  }
+  return Pr;
+}

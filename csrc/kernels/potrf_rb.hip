@@ -356,12 +356,15 @@ int get_ws(RbWork* out, int* epoch, hipStream_t st) {
       HIP_CHECK_RET(hipMalloc((void**)&w.prog, sizeof(int) * MAXB * PSTRIDE));
       HIP_CHECK_RET(hipMemset(w.prog, 0, sizeof(int) * MAXB * PSTRIDE));
     }
+    // null-stream memsets: done before a kernel on a non-blocking stream reads the flags
+    HIP_CHECK_RET(hipDeviceSynchronize());
     g_have[dev] = true;
   }
   ++g_launch;
   if ((g_launch & 0x1ffffff) == 0) {  // epoch wrap (every 2^25 launches): reset every flag
     HIP_CHECK_RET(hipDeviceSynchronize());
     for (int s = 0; s < NSLOT; ++s) HIP_CHECK_RET(hipMemset(g_ws[dev][s].prog, 0, sizeof(int) * MAXB * PSTRIDE));
+    HIP_CHECK_RET(hipDeviceSynchronize());
     ++g_launch;
   }
   // One workspace per stream: launches on one stream are serialised, so they can share it; launches

@@ -1,0 +1,241 @@
+/* Multi-process interpreter-free C ABI (dplasma_init_native_dist, capi/native_dist.cpp): every rank of a
+ * P x Q grid runs the distributed operation and a one-process native context runs the same operation on
+ * the whole matrix; each rank compares ITS tiles of the result (the reference's testing_*.c checks run
+ * per rank on the local tiles too).  Cholesky lower / upper (d, z), SUMMA GEMM (transpose variants, d, z),
+ * a failing factorisation's info on every rank, the norms, the maps, the taskpool lifecycle, and an
+ * operation without a distributed builder (a clean error).
+ * usage: test_native_dist rank world P rdv_dir */
+#include <complex.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "dplasma.h"
+
+static int fails = 0, rank = 0, world = 1, P = 1, Q = 1;
+#define CHECK(c, ...)                                      \
+  do {                                                     \
+    if (!(c)) {                                            \
+      printf("FAIL rank %d %s:%d ", rank, __FILE__, __LINE__); \
+      printf(__VA_ARGS__);                                 \
+      printf("\n");                                        \
+      fails++;                                             \
+    }                                                      \
+  } while (0)
+
+static dplasma_context_t *cd, *c1;
+
+static dplasma_desc_t *mat(dplasma_context_t *ctx, int prec, int nb, int m, int n) {
+  dplasma_desc_t *A = dplasma_desc_block_cyclic(ctx, prec, nb, nb, m, n, 0, 0, dplasmaUpperLower);
+  if (!A) printf("rank %d desc: %s\n", rank, dplasma_last_error());
+  return A;
+}
+
+/* max |X - Y| over this rank's tiles (uplo part: 'L', 'U' or 'A'), relative to max |Y| */
+static double cmp_local(const void *X, const void *Y, int cplx, int m, int n, int nb, char part) {
+  double err = 0, nrm = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < m; ++i) {
+      if ((i / nb) % P != rank / Q || (j / nb) % Q != rank % Q) continue;
+      if ((part == 'L' && i < j) || (part == 'U' && i > j)) continue;
+      const size_t o = i + (size_t)j * m;
+      double d, y;
+      if (cplx) {
+        d = cabs(((const double complex *)X)[o] - ((const double complex *)Y)[o]);
+        y = cabs(((const double complex *)Y)[o]);
+      } else {
+        d = fabs(((const double *)X)[o] - ((const double *)Y)[o]);
+        y = fabs(((const double *)Y)[o]);
+      }
+      if (!(d <= err)) err = d;   /* NaN-propagating */
+      if (y > nrm) nrm = y;
+    }
+  return nrm > 0 ? err / nrm : err;
+}
+
+static void test_potrf(int prec, char uplo, int n, int nb) {
+  const int cplx = prec == dplasmaComplexDouble, es = cplx ? 16 : 8;
+  const dplasma_enum_t u = uplo == 'L' ? dplasmaLower : dplasmaUpper;
+  dplasma_desc_t *A = mat(cd, prec, nb, n, n), *B = mat(c1, prec, nb, n, n);
+  void *X = calloc((size_t)n * n, es), *Y = calloc((size_t)n * n, es);
+  CHECK(A && B, "descriptors");
+  if (!A || !B) return;
+  int r1, r2, i1, i2;
+  if (cplx) {
+    r1 = dplasma_zplghe(cd, (double)n, u, A, 3872);
+    r2 = dplasma_zplghe(c1, (double)n, u, B, 3872);
+    i1 = dplasma_zpotrf(cd, u, A);
+    i2 = dplasma_zpotrf(c1, u, B);
+  } else {
+    r1 = dplasma_dplghe(cd, (double)n, u, A, 3872);
+    r2 = dplasma_dplghe(c1, (double)n, u, B, 3872);
+    i1 = dplasma_dpotrf(cd, u, A);
+    i2 = dplasma_dpotrf(c1, u, B);
+  }
+  CHECK(r1 == 0 && r2 == 0, "plghe: %s", dplasma_last_error());
+  CHECK(i1 == 0 && i2 == 0, "%cpotrf %c info %d / %d: %s", cplx ? 'z' : 'd', uplo, i1, i2, dplasma_last_error());
+  CHECK(dplasma_desc_get_lapack(A, X, n) == 0 && dplasma_desc_get_lapack(B, Y, n) == 0, "get_lapack");
+  const double e = cmp_local(X, Y, cplx, n, n, nb, uplo);
+  CHECK(e < 1e-11, "%cpotrf %c n=%d nb=%d: local tiles differ from one process by %.3e", cplx ? 'z' : 'd', uplo, n,
+        nb, e);
+  if (rank == 0) printf("%cpotrf %c n=%d nb=%d grid %dx%d: max rel diff %.2e\n", cplx ? 'z' : 'd', uplo, n, nb, P, Q, e);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(B);
+  free(X), free(Y);
+}
+
+static void test_gemm(int prec, int ta, int tb, int m, int n, int k, int nb) {
+  const int cplx = prec == dplasmaComplexDouble, es = cplx ? 16 : 8;
+  const int am = ta == dplasmaNoTrans ? m : k, an = ta == dplasmaNoTrans ? k : m;
+  const int bm = tb == dplasmaNoTrans ? k : n, bn = tb == dplasmaNoTrans ? n : k;
+  dplasma_desc_t *A[2], *B[2], *C[2];
+  dplasma_context_t *cx[2] = {cd, c1};
+  int ok = 1;
+  for (int s = 0; s < 2; ++s) {
+    A[s] = mat(cx[s], prec, nb, am, an), B[s] = mat(cx[s], prec, nb, bm, bn), C[s] = mat(cx[s], prec, nb, m, n);
+    ok = ok && A[s] && B[s] && C[s];
+  }
+  CHECK(ok, "descriptors");
+  if (!ok) return;
+  for (int s = 0; s < 2; ++s) {
+    int rc;
+    if (cplx) {
+      rc = dplasma_zplrnt(cx[s], 0, A[s], 11) | dplasma_zplrnt(cx[s], 0, B[s], 12) | dplasma_zplrnt(cx[s], 0, C[s], 13);
+      rc |= dplasma_zgemm(cx[s], ta, tb, 1.5 - 0.25 * I, A[s], B[s], -0.5 + 0.75 * I, C[s]);
+    } else {
+      rc = dplasma_dplrnt(cx[s], 0, A[s], 11) | dplasma_dplrnt(cx[s], 0, B[s], 12) | dplasma_dplrnt(cx[s], 0, C[s], 13);
+      rc |= dplasma_dgemm(cx[s], ta, tb, 1.5, A[s], B[s], -0.5, C[s]);
+    }
+    CHECK(rc == 0, "gemm (%s context): %s", s ? "one-process" : "distributed", dplasma_last_error());
+  }
+  void *X = calloc((size_t)m * n, es), *Y = calloc((size_t)m * n, es);
+  CHECK(dplasma_desc_get_lapack(C[0], X, m) == 0 && dplasma_desc_get_lapack(C[1], Y, m) == 0, "get_lapack");
+  const double e = cmp_local(X, Y, cplx, m, n, nb, 'A');
+  CHECK(e < 1e-12, "%cgemm %d%d %dx%dx%d: local tiles differ by %.3e", cplx ? 'z' : 'd', ta, tb, m, n, k, e);
+  if (rank == 0) printf("%cgemm %d/%d %dx%dx%d grid %dx%d: max rel diff %.2e\n", cplx ? 'z' : 'd', ta, tb, m, n, k, P, Q, e);
+  for (int s = 0; s < 2; ++s) dplasma_desc_destroy(A[s]), dplasma_desc_destroy(B[s]), dplasma_desc_destroy(C[s]);
+  free(X), free(Y);
+}
+
+static void test_failing_potrf(void) {
+  /* a general random matrix is not positive definite: every rank reports the one-process info */
+  const int n = 700, nb = 64;
+  dplasma_desc_t *A = mat(cd, dplasmaRealDouble, nb, n, n), *B = mat(c1, dplasmaRealDouble, nb, n, n);
+  CHECK(A && B, "descriptors");
+  if (!A || !B) return;
+  dplasma_dplrnt(cd, 0, A, 77);
+  dplasma_dplrnt(c1, 0, B, 77);
+  const int i1 = dplasma_dpotrf(cd, dplasmaLower, A), i2 = dplasma_dpotrf(c1, dplasmaLower, B);
+  CHECK(i1 > 0 && i1 == i2, "non-SPD dpotrf info %d, one process %d", i1, i2);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(B);
+}
+
+static void test_norms_maps(void) {
+  const int m = 530, n = 410, nb = 64;
+  dplasma_desc_t *A = mat(cd, dplasmaRealDouble, nb, m, n), *B = mat(c1, dplasmaRealDouble, nb, m, n);
+  dplasma_desc_t *A2 = mat(cd, dplasmaRealDouble, nb, m, n);
+  CHECK(A && B && A2, "descriptors");
+  if (!A || !B || !A2) return;
+  dplasma_dplrnt(cd, 0, A, 5);
+  dplasma_dplrnt(c1, 0, B, 5);
+  {
+    /* host view: this rank's tiles of A against the one-process matrix */
+    double *X = calloc((size_t)m * n, 8), *Y = calloc((size_t)m * n, 8);
+    dplasma_desc_get_lapack(A, X, m);
+    dplasma_desc_get_lapack(B, Y, m);
+    const double e = cmp_local(X, Y, 0, m, n, nb, 'A');
+    double lx = 0, ly = 0;
+    int ix = -1, iy = -1;
+    for (int i = 0; i < m * n; ++i) {
+      if (fabs(Y[i]) > ly) ly = fabs(Y[i]), iy = i;
+      if (((i % m) / nb) % P == rank / Q && ((i / m) / nb) % Q == rank % Q && fabs(X[i]) > lx) lx = fabs(X[i]), ix = i;
+    }
+    CHECK(e == 0, "plrnt: local tiles differ from one process by %.3e", e);
+    printf("rank %d: local max %.15g at (%d,%d); one-process max %.15g at (%d,%d)\n", rank, lx, ix % m, ix / m, ly,
+           iy % m, iy / m);
+    free(X), free(Y);
+  }
+  const int nt[4] = {dplasmaMaxNorm, dplasmaOneNorm, dplasmaInfNorm, dplasmaFrobeniusNorm};
+  for (int t = 0; t < 4; ++t) {
+    const double x = dplasma_dlange(cd, nt[t], A), y = dplasma_dlange(c1, nt[t], B);
+    CHECK(fabs(x - y) <= 1e-12 * y, "dlange %d: %.15g vs one process %.15g", nt[t], x, y);
+  }
+  /* A2 = A; A2 = 2 A2 - A = A; lower part zeroed with diagonal 3: lange max == max(3, max |upper|) */
+  CHECK(dplasma_dlacpy(cd, dplasmaUpperLower, A, A2) == 0, "dlacpy: %s", dplasma_last_error());
+  {
+    double *X = calloc((size_t)m * n, 8), *Y = calloc((size_t)m * n, 8);
+    dplasma_desc_get_lapack(A, X, m);
+    dplasma_desc_get_lapack(A2, Y, m);
+    const double e = cmp_local(Y, X, 0, m, n, nb, 'A');
+    CHECK(e == 0, "lacpy: local tiles differ from A by %.3e", e);
+    free(X), free(Y);
+  }
+  CHECK(dplasma_dgeadd(cd, dplasmaNoTrans, -1.0, A, 2.0, A2) == 0, "dgeadd: %s", dplasma_last_error());
+  const double d = dplasma_dlange(cd, dplasmaFrobeniusNorm, A2), a = dplasma_dlange(cd, dplasmaFrobeniusNorm, A);
+  CHECK(fabs(d - a) <= 1e-12 * a, "lacpy + geadd: |A2|_F %.15g vs |A|_F %.15g", d, a);
+  CHECK(dplasma_dlaset(cd, dplasmaLower, 0.0, 3.0, A2) == 0, "dlaset: %s", dplasma_last_error());
+  CHECK(dplasma_dlaset(c1, dplasmaLower, 0.0, 3.0, B) == 0, "dlaset (one process)");
+  const double l1 = dplasma_dlange(cd, dplasmaOneNorm, A2), l2 = dplasma_dlange(c1, dplasmaOneNorm, B);
+  CHECK(fabs(l1 - l2) <= 1e-12 * l2, "laset + lange one: %.15g vs %.15g", l1, l2);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(B), dplasma_desc_destroy(A2);
+}
+
+static void test_taskpool_and_refusal(void) {
+  const int n = 512, nb = 128;
+  dplasma_desc_t *A = mat(cd, dplasmaRealDouble, nb, n, n), *B = mat(cd, dplasmaRealDouble, nb, n, n);
+  if (!A || !B) { CHECK(0, "descriptors"); return; }
+  dplasma_dplghe(cd, (double)n, dplasmaLower, A, 1);
+  dplasma_taskpool_t *tp = dplasma_dpotrf_New(cd, dplasmaLower, A);
+  CHECK(tp != NULL, "dpotrf_New: %s", dplasma_last_error());
+  if (tp) {
+    CHECK(dplasma_context_add_taskpool(cd, tp) == 0 && dplasma_context_start(cd) == 0 && dplasma_context_wait(cd) == 0,
+          "taskpool lifecycle");
+    CHECK(dplasma_taskpool_result(tp) == 0, "taskpool info %d", dplasma_taskpool_result(tp));
+    dplasma_dpotrf_Destruct(tp);
+  }
+  /* no distributed TRSM builder: a clean error on every rank, the context stays usable */
+  const int rc = dplasma_dtrsm(cd, dplasmaLeft, dplasmaLower, dplasmaNoTrans, dplasmaNonUnit, 1.0, A, B);
+  CHECK(rc != 0 && strstr(dplasma_last_error(), "multi-process"), "dtrsm on a multi-process context: rc %d '%s'", rc,
+        dplasma_last_error());
+  CHECK(dplasma_dlange(cd, dplasmaMaxNorm, A) > 0, "context usable after a refused call");
+  dplasma_desc_destroy(A), dplasma_desc_destroy(B);
+}
+
+int main(int argc, char **argv) {
+  if (argc < 5) {
+    printf("usage: test_native_dist rank world P rdv_dir\n");
+    return 2;
+  }
+  rank = atoi(argv[1]), world = atoi(argv[2]), P = atoi(argv[3]);
+  Q = world / P;
+  cd = dplasma_init_native_dist(0, rank, world, P, argv[4]);
+  c1 = dplasma_init_native(0);
+  if (!cd || !c1) {
+    printf("rank %d: init failed: %s\n", rank, dplasma_last_error());
+    return 2;
+  }
+  CHECK(dplasma_context_rank(cd) == rank && dplasma_context_world(cd) == world, "rank / world of the context");
+  setvbuf(stdout, NULL, _IOLBF, 0);
+  printf("rank %d: contexts up\n", rank);
+  test_potrf(dplasmaRealDouble, 'L', 1100, 128);
+  test_potrf(dplasmaRealDouble, 'U', 1100, 128);
+  test_potrf(dplasmaRealDouble, 'L', 2048, 256);
+  test_potrf(dplasmaComplexDouble, 'L', 600, 96);
+  test_potrf(dplasmaComplexDouble, 'U', 600, 96);
+  test_gemm(dplasmaRealDouble, dplasmaNoTrans, dplasmaNoTrans, 700, 500, 900, 128);
+  test_gemm(dplasmaRealDouble, dplasmaTrans, dplasmaNoTrans, 640, 384, 520, 128);
+  test_gemm(dplasmaRealDouble, dplasmaNoTrans, dplasmaTrans, 300, 700, 257, 64);
+  test_gemm(dplasmaComplexDouble, dplasmaConjTrans, dplasmaTrans, 260, 330, 190, 64);
+  test_failing_potrf();
+  test_norms_maps();
+  test_taskpool_and_refusal();
+  CHECK(!dplasma_python_active(), "the embedded interpreter was started");
+  dplasma_fini(c1);
+  dplasma_fini(cd);
+  if (fails) {
+    printf("rank %d: native dist: %d FAILED\n", rank, fails);
+    return 1;
+  }
+  printf("rank %d: native dist: all passed\n", rank);
+  return 0;
+}

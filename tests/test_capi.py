@@ -147,3 +147,57 @@ def test_capi_f77_native_gpu(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     print(r.stdout)
     assert r.returncode == 0 and "F77 NATIVE OK" in r.stdout, r.stdout + r.stderr
+
+
+def _build_native_dist(tmp_path):
+    _build(tmp_path)
+    exe = str(tmp_path / "test_native_dist")
+    subprocess.run(["gcc", "-O2", "-o", exe, os.path.join(ROOT, "tests", "capi", "test_native_dist.c"),
+                    "-I" + os.path.join(ROOT, "capi", "include"), "-L" + LIB, "-ldplasma", "-lm",
+                    "-Wl,-rpath," + LIB], check=True)
+    return exe
+
+
+def _run_ranks(exe, world, P, rdv, transport="file", timeout=300):
+    """world processes of the C test, one per rank (they share the box's GPU: file transport)."""
+    env = dict(os.environ)
+    env.pop("PYTHONPATH", None)
+    env["DPLASMA_NATIVE_TRANSPORT"] = transport
+    env["DPLASMA_NATIVE_TIMEOUT"] = str(timeout)
+    procs = [subprocess.Popen([exe, str(r), str(world), str(P), str(rdv)], stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True, env=env) for r in range(world)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=timeout + 60)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append((p.returncode, out))
+    return outs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,P", [(2, 2), (2, 1), (4, 2)])
+def test_capi_native_dist_gpu(tmp_path, world, P):
+    """Interpreter-free multi-process C ABI (capi/native_dist.cpp) on P x Q grids of ranks sharing the GPU:
+    distributed potrf (L/U, d/z), SUMMA gemm, info, norms and maps equal the one-process engine's on every
+    rank's tiles; an operation without a distributed builder fails cleanly."""
+    exe = _build_native_dist(tmp_path)
+    outs = _run_ranks(exe, world, P, tmp_path / "rdv")
+    text = "\n".join(o for _, o in outs)
+    print(text)
+    for r, (rc, out) in enumerate(outs):
+        assert rc == 0 and f"rank {r}: native dist: all passed" in out, text
+
+
+def test_capi_native_dist_bad_grid(tmp_path):
+    """dplasma_init_native_dist refuses a world that is not a P x Q grid before touching the transport."""
+    exe = _build_native_dist(tmp_path)
+    env = dict(os.environ)
+    env.pop("PYTHONPATH", None)
+    r = subprocess.run([exe, "0", "3", "2", str(tmp_path / "rdv")], capture_output=True, text=True, timeout=120,
+                       env=env)
+    assert r.returncode == 2, r.stdout + r.stderr
+    assert "init failed" in r.stdout

@@ -165,11 +165,17 @@ def main():
           "void dplasma_fini(dplasma_context_t *ctx);",
           "/* interpreter-free single-GPU context (capi/native.cpp): never starts Python; descriptors are",
           " * LAPACK-layout device buffers (dplasma_desc_block_cyclic allocates, _lapack wraps a device pointer,",
-          " * P = Q = 1); potrf, potrs, posv, gemm, trsm, herk, syrk, geadd, tradd, lacpy, laset, lascal,",
-          " * lange, lantr, plghe, plgsy, plrnt (s/d/c/z, blocking and _New) run natively, every other operation",
-          " * returns an error",
-          " * (dplasma_last_error) */",
+          " * P = Q = 1); the level-3 BLAS, Cholesky / LU / QR families, maps, norms and generators listed in",
+          " * README run natively, every other operation returns an error (dplasma_last_error) */",
           "dplasma_context_t *dplasma_init_native(int device);",
+          "/* interpreter-free multi-process context (capi/native_dist.cpp): rank of world processes, one GPU",
+          " * each, on a P x (world / P) grid (rank = myrow * Q + mycol); descriptors are this rank's tiles of the",
+          " * 2-D block-cyclic distribution in ScaLAPACK local layout, desc_set/get_lapack take the whole matrix;",
+          " * potrf, gemm, plghe / plgsy / plrnt, geadd / tradd / lacpy / laset / lascal and lange / lantr run",
+          " * across the ranks.  Tiles move through RCCL (a GPU per rank) or node-local files (ranks sharing a",
+          " * GPU); DPLASMA_NATIVE_TRANSPORT=rccl|file overrides.  rdv_dir: a fresh directory every rank can",
+          " * reach (NULL: $DPLASMA_NATIVE_RDV) */",
+          "dplasma_context_t *dplasma_init_native_dist(int device, int rank, int world, int P, const char *rdv_dir);",
           "int dplasma_python_active(void);   /* 1 once the embedded interpreter has been started */",
           "int dplasma_context_rank(const dplasma_context_t *ctx);",
           "int dplasma_context_world(const dplasma_context_t *ctx);",
