@@ -16,6 +16,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <complex>
 #include <cstdlib>
 #include <cstring>
@@ -54,35 +55,42 @@ int f77(const char* name, std::initializer_list<PyObject*> args) {
   return v;
 }
 
-// ---- interpreter-free path: a single-process run (no WORLD_SIZE > 1) whose BLACS grid is 1 x 1 runs
-// the ScaLAPACK calls on the native engine (capi/native.cpp) -- the reference wrappers' flow
-// (dplasma_wrapper_pdpotrf.c:133-291: wrap the local array, run, hand it back) without Python.
-// DPLASMA_F77_PYTHON=1 forces the Python layer.
+// ---- interpreter-free path: a single-process run whose BLACS grid is 1 x 1 runs the ScaLAPACK calls on
+// the native engine (capi/native.cpp), and so does a multi-process run (RANK / WORLD_SIZE, one process per
+// GPU) given a rendezvous directory in DPLASMA_NATIVE_RDV: its nprow x npcol BLACS grid becomes a
+// multi-process native context (capi/native_dist.cpp) and p?potrf_ / p?gemm_ run on the ranks' local
+// arrays -- the reference wrappers' flow (dplasma_wrapper_pdpotrf.c:133-291: wrap the local array, run,
+// hand it back) without Python.  DPLASMA_F77_PYTHON=1 forces the Python layer.
 constexpr int NATIVE_CTXT = 1 << 20;    // BLACS handles of the native registry (Python's are small ints)
 
-// decided once, at the first F77 call: one process, a GPU, and no Python-backed dplasma context
-// already created by the program (dplasma_init) -- a program that mixes the C API's Python contexts
-// with the F77 layer keeps the Python layer
+int env_i(const char* k, int d) {
+  const char* v = std::getenv(k);
+  return v && *v ? std::atoi(v) : d;
+}
+int job_world() { return std::max(1, env_i("WORLD_SIZE", 1)); }
+int job_rank() { return env_i("RANK", 0); }
+
+// decided once, at the first F77 call: a GPU, no Python-backed dplasma context already created by the
+// program (dplasma_init) -- a program that mixes the C API's Python contexts with the F77 layer keeps
+// the Python layer -- and, for more than one process, a rendezvous directory
 bool f77_native() {
   static int v = -1;
   if (v < 0) {
-    const char* w = std::getenv("WORLD_SIZE");
     const char* f = std::getenv("DPLASMA_F77_PYTHON");
+    const char* rdv = std::getenv("DPLASMA_NATIVE_RDV");
     int nd = 0;
     const bool gpu = hipGetDeviceCount(&nd) == hipSuccess && nd > 0;
     if (!gpu) (void)hipGetLastError();
-    v = (!w || std::atoi(w) <= 1) && !(f && std::atoi(f) == 1) && gpu && !dplasma_python_active() ? 1 : 0;
+    v = (job_world() <= 1 || (rdv && *rdv)) && !(f && std::atoi(f) == 1) && gpu && !dplasma_python_active() ? 1 : 0;
   }
   return v == 1;
 }
 
 dplasma_context_t* g_nctx = nullptr;
+int g_nprow = 1, g_npcol = 1;   // the native BLACS grid
 
 dplasma_context_t* native_ctx() {
-  if (!g_nctx) {
-    const char* lr = std::getenv("LOCAL_RANK");
-    g_nctx = dplasma_init_native(lr ? std::atoi(lr) : 0);
-  }
+  if (!g_nctx && job_world() <= 1) g_nctx = dplasma_init_native(env_i("LOCAL_RANK", 0));
   return g_nctx;
 }
 
@@ -104,15 +112,49 @@ struct Wrapped {
   char* host = nullptr;
   int lld = 0;
   bool copy = false;
+  void* dev = nullptr;          // multi-process grids: device copy of a host local array (lm x ln, lld)
+  int lm = 0, ln = 0, es = 0;
 };
 constexpr int NAT_TILE = 256;
 
 Wrapped wrap(int prec, int es, void* a, int ia, int ja, const int* desc, int m, int n) {
   Wrapped w;
   w.lld = desc[8];
-  char* sub = (char*)a + ((size_t)(ia - 1) + (size_t)(ja - 1) * w.lld) * es;
   dplasma_context_t* c = native_ctx();
   if (!c || m <= 0 || n <= 0) return w;
+  if (dplasma_context_world(c) > 1) {
+    // P x Q grid: the local array IS this rank's tiles in ScaLAPACK local layout when the operand starts
+    // at (1, 1) of a matrix distributed from process (0, 0) with mb x nb blocks (the tiles)
+    if (ia != 1 || ja != 1 || desc[6] != 0 || desc[7] != 0) {
+      dpl_set_error("native multi-process F77: operands at IA = JA = 1 of matrices distributed from process (0, 0)");
+      return w;
+    }
+    const int mb = desc[4], nb = desc[5], me = dplasma_context_rank(c);
+    const int myrow = me / g_npcol, mycol = me % g_npcol;
+    int zero = 0;
+    int mm = m, nn = n, mbv = mb, nbv = nb, pr = g_nprow, pc = g_npcol, r = myrow, q = mycol;
+    const int lm = numroc_(&mm, &mbv, &r, &zero, &pr), ln = numroc_(&nn, &nbv, &q, &zero, &pc);
+    void* dev = a;
+    if (!on_device(a)) {   // host local array: through a device copy, written back by unwrap
+      dev = nullptr;
+      const size_t bytes = (size_t)w.lld * std::max(1, ln) * es;
+      if (hipMalloc(&dev, bytes) != hipSuccess) return w;
+      if (lm > 0 && ln > 0 &&
+          hipMemcpy2D(dev, (size_t)w.lld * es, a, (size_t)w.lld * es, (size_t)lm * es, ln, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(dev);
+        return w;
+      }
+      w.host = (char*)a;
+      w.copy = true;
+      w.dev = dev;
+      w.lm = lm;
+      w.ln = ln;
+    }
+    w.d = dplasma_desc_block_cyclic_lapack(c, prec, mb, nb, m, n, 0, 0, 0, 0, dev, w.lld, 1);
+    w.es = es;
+    return w;
+  }
+  char* sub = (char*)a + ((size_t)(ia - 1) + (size_t)(ja - 1) * w.lld) * es;
   if (on_device(a)) {
     w.d = dplasma_desc_block_cyclic_lapack(c, prec, NAT_TILE, NAT_TILE, m, n, 1, 1, 0, 0, sub, w.lld, 1);
   } else {
@@ -128,6 +170,16 @@ Wrapped wrap(int prec, int es, void* a, int ia, int ja, const int* desc, int m, 
 }
 
 void unwrap(Wrapped& w, bool write_back) {
+  if (w.dev) {   // multi-process host local array
+    if (write_back && w.d && w.lm > 0 && w.ln > 0)
+      (void)hipMemcpy2D(w.host, (size_t)w.lld * w.es, w.dev, (size_t)w.lld * w.es, (size_t)w.lm * w.es, w.ln,
+                        hipMemcpyDeviceToHost);
+    if (w.d) dplasma_desc_destroy(w.d);
+    (void)hipFree(w.dev);
+    w.d = nullptr;
+    w.dev = nullptr;
+    return;
+  }
   if (!w.d) return;
   if (w.copy && write_back) (void)dplasma_desc_get_lapack(w.d, w.host, w.lld);
   dplasma_desc_destroy(w.d);
@@ -156,7 +208,7 @@ extern "C" {
 // ---- runtime (parsec_init_wrapper_ / parsec_fini_wrapper_)
 DPL_CAPI void parsec_init_wrapper_(void) {
   if (f77_native()) {
-    native_ctx();
+    native_ctx();   // one process; a multi-process context is created by blacs_gridinit_ (it needs the grid)
     return;
   }
   DplGil g;
@@ -175,8 +227,8 @@ DPL_CAPI void parsec_fini_wrapper_(void) {
 // ---- BLACS / TOOLS subset (weak: a real BLACS library takes precedence)
 DPL_CAPI __attribute__((weak)) void blacs_pinfo_(int* mypnum, int* nprocs) {
   if (f77_native()) {
-    *mypnum = 0;
-    *nprocs = 1;
+    *mypnum = job_rank();
+    *nprocs = job_world();
     return;
   }
   DplGil g;
@@ -194,13 +246,21 @@ DPL_CAPI __attribute__((weak)) void blacs_get_(int* icontxt, int* what, int* val
 }
 DPL_CAPI __attribute__((weak)) void blacs_gridinit_(int* icontxt, const char* order, int* nprow, int* npcol) {
   (void)order;
-  if (f77_native()) {   // one process: only the 1 x 1 grid exists
-    if (*nprow == 1 && *npcol == 1) {
-      *icontxt = NATIVE_CTXT;
-    } else {
-      dpl_set_error("blacs_gridinit: a single process has only a 1 x 1 grid");
+  if (f77_native()) {   // the grid must hold every process of the job (one process: 1 x 1)
+    const int world = job_world();
+    if (*nprow < 1 || *npcol < 1 || *nprow * *npcol != world ||
+        (g_nctx && world > 1 && (*nprow != g_nprow || *npcol != g_npcol))) {
+      dpl_set_error("blacs_gridinit: the native grid is nprow x npcol = WORLD_SIZE processes (one grid per job)");
       *icontxt = -1;
+      return;
     }
+    if (world > 1 && !g_nctx) {
+      g_nctx = dplasma_init_native_dist(env_i("LOCAL_RANK", 0), job_rank(), world, *nprow, nullptr);
+      if (!g_nctx) { *icontxt = -1; return; }
+    }
+    g_nprow = *nprow;
+    g_npcol = *npcol;
+    *icontxt = NATIVE_CTXT;
     return;
   }
   DplGil g;  // the argument objects are built before f77() runs: hold the GIL here
@@ -209,8 +269,11 @@ DPL_CAPI __attribute__((weak)) void blacs_gridinit_(int* icontxt, const char* or
 DPL_CAPI __attribute__((weak)) void blacs_gridinfo_(int* icontxt, int* nprow, int* npcol, int* myrow, int* mycol) {
   if (f77_native()) {
     const bool ok = *icontxt == NATIVE_CTXT;
-    *nprow = *npcol = ok ? 1 : -1;
-    *myrow = *mycol = ok ? 0 : -1;
+    const int me = job_world() > 1 ? job_rank() : 0;
+    *nprow = ok ? g_nprow : -1;
+    *npcol = ok ? g_npcol : -1;
+    *myrow = ok ? me / g_npcol : -1;
+    *mycol = ok ? me % g_npcol : -1;
     return;
   }
   DplGil g;
@@ -379,6 +442,11 @@ DPL_F77_NATIVE(z, dplasma_complex64_t, 5)
     const int lw = latsqr_work(desca);                                                                           \
     if (work) work[0] = (T)lw;                                                                                   \
     if (*lwork == -1) return;                                                                                    \
+    if (native_grid(desca) && job_world() > 1) {   /* no native QR on a multi-process grid */                   \
+      dpl_set_error("p?latsqr_: not available on a multi-process native grid");                                   \
+      *info = -1;                                                                                                \
+      return;                                                                                                    \
+    }                                                                                                            \
     DplGil g;                                                                                                    \
     int dpy[9];                                                                                                  \
     std::memcpy(dpy, desca, sizeof dpy);                                                                         \

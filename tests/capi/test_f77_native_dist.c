@@ -1,0 +1,120 @@
+/* ScaLAPACK F77 layer without Python on a P x Q BLACS grid of processes (RANK / WORLD_SIZE,
+ * DPLASMA_NATIVE_RDV; capi/dplasma_f77.cpp -> the multi-process native engine): pdpotrf_ and pdgemm_ on
+ * each rank's ScaLAPACK local arrays (host memory), checked entry by entry against host arithmetic on the
+ * global matrices (every rank holds the formulas); the embedded interpreter must never start.
+ * usage (one process per rank): RANK=r WORLD_SIZE=w test_f77_native_dist nprow */
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "dplasma.h"
+
+static int fails = 0, me = 0;
+#define CHECK(c, ...)                                   \
+  do {                                                  \
+    if (!(c)) {                                         \
+      printf("FAIL rank %d %s:%d ", me, __FILE__, __LINE__); \
+      printf(__VA_ARGS__);                              \
+      printf("\n");                                     \
+      fails++;                                          \
+    }                                                   \
+  } while (0)
+
+static double fa(int i, int j) { return sin(0.37 * i + 1.3 * j) + 0.25 * cos(0.11 * i * j); }
+static double fb(int i, int j) { return cos(0.23 * i - 0.7 * j); }
+static double fc(int i, int j) { return 0.5 * sin(0.05 * (i + 3 * j)); }
+
+int main(int argc, char **argv) {
+  setvbuf(stdout, NULL, _IONBF, 0);
+  const int nprow = argc > 1 ? atoi(argv[1]) : 1;
+  int np, zero = 0, ictxt, P, Q, myrow, mycol, info;
+  parsec_init_wrapper_();
+  blacs_pinfo_(&me, &np);
+  const int npcol = np / nprow;
+  int pr = nprow, pc = npcol;
+  blacs_get_(&zero, &zero, &ictxt);
+  blacs_gridinit_(&ictxt, "R", &pr, &pc);
+  blacs_gridinfo_(&ictxt, &P, &Q, &myrow, &mycol);
+  CHECK(P == nprow && Q == npcol && myrow == me / npcol && mycol == me % npcol, "grid %d x %d at (%d, %d): %s", P, Q,
+        myrow, mycol, dplasma_last_error());
+  if (fails) return 1;
+  const int N = 520, nb = 64;
+  int n = N, nbv = nb, one = 1;
+  const int lm = numroc_(&n, &nbv, &myrow, &zero, &P), ln = numroc_(&n, &nbv, &mycol, &zero, &Q);
+  int lld = lm > 1 ? lm : 1, desc[9];
+  descinit_(desc, &n, &n, &nbv, &nbv, &zero, &zero, &ictxt, &lld, &info);
+  /* local (li, lj) <-> global (i, j) */
+  int *gi = malloc(sizeof(int) * (lm + 1)), *gj = malloc(sizeof(int) * (ln + 1));
+  for (int l = 0; l < lm; ++l) gi[l] = ((l / nb) * P + myrow) * nb + l % nb;
+  for (int l = 0; l < ln; ++l) gj[l] = ((l / nb) * Q + mycol) * nb + l % nb;
+
+  /* ---- pdpotrf_: SPD A = M M^T + N I (M = fa), lower */
+  double *M = malloc(sizeof(double) * N * N), *S = malloc(sizeof(double) * N * N);
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i < N; ++i) M[i + (size_t)j * N] = fa(i, j);
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i < N; ++i) {
+      double s = 0;
+      for (int k = 0; k < N; ++k) s += M[i + (size_t)k * N] * M[j + (size_t)k * N];
+      S[i + (size_t)j * N] = s + (i == j ? N : 0.0);
+    }
+  double *a = malloc(sizeof(double) * lld * (ln > 0 ? ln : 1));
+  for (int lj = 0; lj < ln; ++lj)
+    for (int li = 0; li < lm; ++li) a[li + (size_t)lj * lld] = S[gi[li] + (size_t)gj[lj] * N];
+  pdpotrf_("L", &n, a, &one, &one, desc, &info);
+  CHECK(info == 0, "pdpotrf_ info %d: %s", info, dplasma_last_error());
+  /* host Cholesky of S (in place, lower) */
+  for (int k = 0; k < N; ++k) {
+    double d = sqrt(S[k + (size_t)k * N]);
+    S[k + (size_t)k * N] = d;
+    for (int i = k + 1; i < N; ++i) S[i + (size_t)k * N] /= d;
+    for (int j = k + 1; j < N; ++j)
+      for (int i = j; i < N; ++i) S[i + (size_t)j * N] -= S[i + (size_t)k * N] * S[j + (size_t)k * N];
+  }
+  double e = 0, nrm = 0;
+  for (int lj = 0; lj < ln; ++lj)
+    for (int li = 0; li < lm; ++li)
+      if (gi[li] >= gj[lj]) {
+        const double y = S[gi[li] + (size_t)gj[lj] * N];
+        e = fmax(e, fabs(a[li + (size_t)lj * lld] - y));
+        nrm = fmax(nrm, fabs(y));
+      }
+  printf("rank %d: pdpotrf_ %dx%d grid, local max rel diff %.3e\n", me, P, Q, e / nrm);
+  CHECK(e / nrm < 1e-12, "pdpotrf_ local entries differ by %.3e", e / nrm);
+
+  /* ---- pdgemm_: C = 0.5 A B^T + 2 C */
+  double *A = malloc(sizeof(double) * lld * (ln > 0 ? ln : 1)), *B = malloc(sizeof(double) * lld * (ln > 0 ? ln : 1));
+  double *C = malloc(sizeof(double) * lld * (ln > 0 ? ln : 1));
+  for (int lj = 0; lj < ln; ++lj)
+    for (int li = 0; li < lm; ++li) {
+      A[li + (size_t)lj * lld] = fa(gi[li], gj[lj]);
+      B[li + (size_t)lj * lld] = fb(gi[li], gj[lj]);
+      C[li + (size_t)lj * lld] = fc(gi[li], gj[lj]);
+    }
+  double al = 0.5, be = 2.0;
+  pdgemm_("N", "T", &n, &n, &n, &al, A, &one, &one, desc, B, &one, &one, desc, &be, C, &one, &one, desc);
+  e = 0, nrm = 0;
+  for (int lj = 0; lj < ln; ++lj)
+    for (int li = 0; li < lm; ++li) {
+      double s = 0;
+      for (int k = 0; k < N; ++k) s += fa(gi[li], k) * fb(gj[lj], k);
+      const double y = al * s + be * fc(gi[li], gj[lj]);
+      e = fmax(e, fabs(C[li + (size_t)lj * lld] - y));
+      nrm = fmax(nrm, fabs(y));
+    }
+  printf("rank %d: pdgemm_ %dx%d grid, local max rel diff %.3e\n", me, P, Q, e / nrm);
+  CHECK(e / nrm < 1e-12, "pdgemm_ local entries differ by %.3e", e / nrm);
+  /* no native LU on a multi-process grid: an error, not a wrong answer */
+  int *ipiv = malloc(sizeof(int) * (lm + nb));
+  pdgetrf_(&n, &n, A, &one, &one, desc, ipiv, &info);
+  CHECK(info < 0, "pdgetrf_ on a multi-process native grid returned info %d", info);
+  CHECK(!dplasma_python_active(), "the embedded interpreter was started");
+  parsec_fini_wrapper_();
+  if (fails) {
+    printf("rank %d: F77 NATIVE DIST: %d FAILED\n", me, fails);
+    return 1;
+  }
+  printf("rank %d: F77 NATIVE DIST OK\n", me);
+  return 0;
+}

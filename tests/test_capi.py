@@ -201,3 +201,29 @@ def test_capi_native_dist_bad_grid(tmp_path):
                        env=env)
     assert r.returncode == 2, r.stdout + r.stderr
     assert "init failed" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,nprow", [(2, 1), (4, 2)])
+def test_capi_f77_native_dist_gpu(tmp_path, world, nprow):
+    """ScaLAPACK F77 entry points without Python on a BLACS grid of processes (RANK / WORLD_SIZE and
+    DPLASMA_NATIVE_RDV -> the multi-process native engine): pdpotrf_ / pdgemm_ on every rank's local arrays
+    equal host arithmetic on the global matrices (reference src/scalapack_wrappers/)."""
+    _build(tmp_path)
+    exe = str(tmp_path / "test_f77_native_dist")
+    subprocess.run(["gcc", "-O2", "-o", exe, os.path.join(ROOT, "tests", "capi", "test_f77_native_dist.c"),
+                    "-I" + os.path.join(ROOT, "capi", "include"), "-L" + LIB, "-ldplasma", "-lm",
+                    "-Wl,-rpath," + LIB], check=True)
+    procs = []
+    for r in range(world):
+        env = dict(os.environ)
+        env.pop("PYTHONPATH", None)
+        env.update(RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", DPLASMA_NATIVE_RDV=str(tmp_path / "rdv"),
+                   DPLASMA_NATIVE_TRANSPORT="file", DPLASMA_NATIVE_TIMEOUT="200")
+        procs.append(subprocess.Popen([exe, str(nprow)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                                      env=env))
+    outs = [p.communicate(timeout=300)[0] for p in procs]
+    text = "\n".join(outs)
+    print(text)
+    for r, (p, out) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0 and f"rank {r}: F77 NATIVE DIST OK" in out, text
