@@ -145,6 +145,9 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     tp._buffers = (GX, dsend, drecv, dbuf)
 
     use_rb = ops.rb_ok(A.data, A.mb) and A.mb == A.nb
+    # panel TRSM: "rb" (register-resident strips, k_trsm_rb) or "gemm" (the batched TRSM engine: blocked
+    # substitution on 16-blocks with MFMA updates, workgroups shaped like the bulk GEMM's)
+    trsm_rb = use_rb and env.get("DPLASMA_POTRF_TRSM", "rb") == "rb"
     if use_rb:
         zsz = ops.rb_zbuf_size()
         zbufs = torch.empty(2 * zsz, dtype=torch.float64, device=dev)
@@ -256,7 +259,7 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                 else:
                     tri_base, tri_ld, tri_off = A.data, A.ld, A.offset(*dk)
                     pre = []
-                if use_rb:
+                if trsm_rb:
                     rbp = ops.RbPanel(uplo, [(A.offset(*tcoord(i, k)), A.tile_rows(i) if lower else A.tile_cols(i))
                                              for i in mine], A.ld)
                     prep = []
@@ -536,6 +539,9 @@ def potrf_pipelined_New(ctx, uplo: int, A, info_out=None, chunk: int = 8) -> Tas
     dbuf = torch.zeros(2 * nbe, dtype=A.dtype, device=dev)
     tp._buffers = (GX, dsend, drecv, dbuf)
     use_rb = ops.rb_ok(A.data, A.mb) and A.mb == A.nb
+    # panel TRSM: "rb" (register-resident strips, k_trsm_rb) or "gemm" (the batched TRSM engine: blocked
+    # substitution on 16-blocks with MFMA updates, workgroups shaped like the bulk GEMM's)
+    trsm_rb = use_rb and os.environ.get("DPLASMA_POTRF_TRSM", "rb") == "rb"
     if use_rb:
         zsz = ops.rb_zbuf_size()
         zbufs = torch.empty(2 * zsz, dtype=torch.float64, device=dev)
@@ -668,7 +674,7 @@ def potrf_pipelined_New(ctx, uplo: int, A, info_out=None, chunk: int = 8) -> Tas
                         comm.finish(pend[(k, "d")])
                         d = dbuf[par2 * nbe:(par2 + 1) * nbe]
                         d[comm._tri_index(kb, A.mb, lower, dev)] = drecv[par2 * ntri: par2 * ntri + kb * (kb + 1) // 2]
-                        if use_rb:
+                        if trsm_rb:
                             ops.trsm_rb_prep(uplo, kb, dbuf, par2 * nbe, A.mb, zk)
                     pre.append(f_unpack)
                 if t_dr is not None:
@@ -681,7 +687,7 @@ def potrf_pipelined_New(ctx, uplo: int, A, info_out=None, chunk: int = 8) -> Tas
                     pk.add(A.offset(*cc), A.tile_rows(cc[0]), A.tile_cols(cc[1]), b_off=G + pos_g[i] * nbe)
                     pk.add(A.offset(*cc), A.tile_rows(cc[0]), A.tile_cols(cc[1]), b_off=XS + xs_pos[i] * nbe)
                 pk.finalize()
-                if use_rb:
+                if trsm_rb:
                     rbp = ops.RbPanel(uplo, [(A.offset(*tcoord(i, k)), A.tile_rows(i) if lower else A.tile_cols(i))
                                              for i in ch], A.ld)
 
