@@ -260,6 +260,16 @@ bool add_potrs(NatProgram& P, int uplo, NatDesc& A, NatDesc& B, int first_dep = 
          add_trsm(P, LEFT, UPPER, NOTRANS, NONUNIT, one, A, B, 1);
 }
 
+// the grid version: two distributed solves appended after everything already in the program
+bool add_potrs_dist(NatProgram& P, int uplo, NatDesc& A, NatDesc& B) {
+  const Scalar one(B.prec, 1.0);
+  if (uplo == LOWER)
+    return nat_dist_trsm_into(P, LEFT, LOWER, NOTRANS, NONUNIT, one, A, B) &&
+           nat_dist_trsm_into(P, LEFT, LOWER, CONJTRANS, NONUNIT, one, A, B);
+  return nat_dist_trsm_into(P, LEFT, UPPER, CONJTRANS, NONUNIT, one, A, B) &&
+         nat_dist_trsm_into(P, LEFT, UPPER, NOTRANS, NONUNIT, one, A, B);
+}
+
 // last task of a program on a stream (-1: none)
 int last_on(const NatProgram& P, int stream) {
   for (int i = (int)P.tasks.size() - 1; i >= 0; --i)
@@ -300,10 +310,11 @@ NatProgram* nat_potrf(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t
 NatProgram* nat_potrs(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* dA, dplasma_desc_t* dB) {
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *B = dB ? dB->nat : nullptr;
-  if (!same_ctx(c, {A, B}, prec) || A->m != A->n || B->m != A->n || B->mb != A->nb)
+  if (!same_ctx_dist(c, {A, B}, prec) || A->m != A->n || B->m != A->n || B->mb != A->nb)
     return fail(nullptr, "potrs: descriptors do not conform");
   NatProgram* P = new_program(c, "potrs", false);
-  if (!add_potrs(*P, uplo, *A, *B)) return fail(P, "potrs: device allocation failed");
+  if (!(c->dist() ? add_potrs_dist(*P, uplo, *A, *B) : add_potrs(*P, uplo, *A, *B)))
+    return fail(P, "potrs: device allocation failed");
   return P;
 }
 
@@ -311,8 +322,10 @@ NatProgram* nat_posv(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t*
   NatProgram* P = nat_potrf(ctx, prec, uplo, dA);
   if (!P) return nullptr;
   NatDesc *A = dA->nat, *B = dB ? dB->nat : nullptr;
-  if (!same_ctx(ctx->nat, {B}, prec) || B->m != A->n || B->mb != A->nb)
+  if (!same_ctx_dist(ctx->nat, {B}, prec) || B->m != A->n || B->mb != A->nb)
     return fail(P, "posv: right-hand side does not conform");
+  if (ctx->nat->dist())   // the solves follow the whole factorisation (every stream)
+    return add_potrs_dist(*P, uplo, *A, *B) ? P : fail(P, "posv: device allocation failed");
   // the solves (update stream) start after the factorisation's last panel-stream task (POTRF / TRSM /
   // NEAR of the last tiles): without this edge they could read A(nt-1, nt-1) before it is factored
   if (!add_potrs(*P, uplo, *A, *B, last_on(*P, 0))) return fail(P, "posv: device allocation failed");
@@ -356,11 +369,14 @@ NatProgram* nat_trsm(dplasma_context_t* ctx, int prec, int side, int uplo, int t
                      dplasma_desc_t* dA, dplasma_desc_t* dB) {
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *B = dB ? dB->nat : nullptr;
-  if (!same_ctx(c, {A, B}, prec)) return fail(nullptr, "trsm: descriptors of another context or precision");
+  if (!same_ctx_dist(c, {A, B}, prec)) return fail(nullptr, "trsm: descriptors of another context or precision");
   const int order = side == LEFT ? B->m : B->n;
   if (A->m != A->n || A->m != order || A->mb != A->nb || (side == LEFT ? B->mb : B->nb) != A->nb)
     return fail(nullptr, "trsm: operands do not conform");
   NatProgram* P = new_program(c, "trsm", false);
+  if (c->dist())
+    return nat_dist_trsm_into(*P, side, uplo, trans, diag, Scalar(prec, alpha), *A, *B)
+               ? P : fail(P, "trsm: device allocation failed");
   if (!add_trsm(*P, side, uplo, trans, diag, Scalar(prec, alpha), *A, *B, 1))
     return fail(P, "trsm: device allocation failed");
   return P;
@@ -980,9 +996,10 @@ std::shared_ptr<NatDesc> work_desc(NatProgram& P, const NatDesc& A) {
   w->n = A.n;
   w->mt = A.mt;
   w->nt = A.nt;
-  w->lld = std::max(16, (A.m + 15) / 16 * 16);
+  w->P = A.P, w->Q = A.Q, w->myrow = A.myrow, w->mycol = A.mycol, w->lm = A.lm, w->ln = A.ln;   // A's distribution
+  w->lld = std::max(16, (A.lm + 15) / 16 * 16);
   void* p = nullptr;
-  if (hipMalloc(&p, (size_t)w->lld * std::max(1, A.n) * A.es) != hipSuccess) return nullptr;
+  if (hipMalloc(&p, (size_t)w->lld * std::max(1, A.ln) * A.es) != hipSuccess) return nullptr;
   w->data = (char*)p;
   w->owned = true;
   P.wdesc.push_back(w);
@@ -1006,9 +1023,11 @@ int add_expand(NatProgram& P, const NatDesc& A, int uplo, bool unit, int mode, N
   char* w = W.data;
   if (mode == 0)
     prev = P.task(1, [=](hipStream_t s) {
+      if (all->n() == 0) return 0;
       return dpl_laset(prec, 0, all->n(), all->items(), all->mm, all->nn, zero.ptr(), zero.ptr(), w, ldw, s);
     }, {prev});
   prev = P.task(1, [=](hipStream_t s) {
+    if (tri->n() == 0) return 0;
     return dpl_geadd(prec, tpart, NOTRANS, tri->n(), tri->items(), tri->mm, tri->nn, one.ptr(), a, lda, zero.ptr(), w,
                      ldw, 1, s);
   }, {prev});
@@ -1021,9 +1040,11 @@ int add_expand(NatProgram& P, const NatDesc& A, int uplo, bool unit, int mode, N
     std::vector<TileItem> d;
     int mm = 0;
     for (int k = 0; k < W.mt && k < W.nt; ++k) {
+      if (!W.local(k, k)) continue;
       d.push_back(TileItem{W.off(k, k), W.off(k, k), W.rows(k), W.cols(k), k * W.mb, k * W.nb});
       mm = std::max(mm, std::max(W.rows(k), W.cols(k)));
     }
+    if (d.empty()) return prev;
     DevPtr dd = dev_upload(d);
     if (!dd) return -2;
     P.keep.push_back(dd);
@@ -1046,7 +1067,7 @@ NatProgram* nat_trmm(dplasma_context_t* ctx, int prec, int side, int uplo, int t
                      dplasma_desc_t* dA, dplasma_desc_t* dB) {
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *B = dB ? dB->nat : nullptr;
-  if (!same_ctx(c, {A, B}, prec)) return fail(nullptr, "trmm: descriptors of another context or precision");
+  if (!same_ctx_dist(c, {A, B}, prec)) return fail(nullptr, "trmm: descriptors of another context or precision");
   const bool left = side == LEFT, notrans = trans == NOTRANS;
   const int order = left ? B->m : B->n;
   if (A->m != A->n || A->m != order || A->mb != A->nb || (left ? B->mb : B->nb) != A->nb ||
@@ -1063,9 +1084,15 @@ NatProgram* nat_trmm(dplasma_context_t* ctx, int prec, int side, int uplo, int t
   char *bb = B->data, *wd = W->data, *td = T->data;
   const int ldb = B->lld, ldw = W->lld, ldt = T->lld;
   prev = P->task(1, [=](hipStream_t s) {
+    if (cp->n() == 0) return 0;
     return dpl_geadd(prec, 0, NOTRANS, cp->n(), cp->items(), cp->mm, cp->nn, one.ptr(), bb, ldb, zero.ptr(), wd, ldw,
                      1, s);
   }, {prev});
+  if (c->dist()) {   // the expanded triangle times the copy of B: the SUMMA GEMM over the grid
+    const bool ok = left ? nat_dist_gemm_into(*P, prec, trans, NOTRANS, al, *T, *W, zero, *B)
+                         : nat_dist_gemm_into(*P, prec, NOTRANS, trans, al, *W, *T, zero, *B);
+    return ok ? P : fail(P, "trmm: device allocation failed");
+  }
   // B(m,n) = alpha sum_k op(T)(m,k) W(k,n) (left) / alpha sum_k W(m,k) op(T)(k,n) (right), k over the
   // triangle only: op(A) is lower iff (uplo == Lower) == (trans == NoTrans)
   const bool lower_op = (uplo == LOWER) == notrans;

@@ -186,17 +186,33 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
 }
 
 // ----------------------------------------------------------------------------------------------- GEMM
+static int last_task_on(const NatProgram& P, int stream) {
+  for (int i = (int)P.tasks.size() - 1; i >= 0; --i)
+    if (P.tasks[i].stream == stream) return i;
+  return -1;
+}
+
 NatProgram* nat_dist_gemm(NatCtx* c, int prec, int tA, int tB, const Scalar& alpha, NatDesc& A, NatDesc& B,
                           const Scalar& beta, NatDesc& C) {
+  NatProgram* Pr = new_program(c, "gemm", false);
+  if (!nat_dist_gemm_into(*Pr, prec, tA, tB, alpha, A, B, beta, C)) return fail(Pr, "gemm: device allocation failed");
+  return Pr;
+}
+
+// appended to Pr after everything already in it
+bool nat_dist_gemm_into(NatProgram& PrR, int prec, int tA, int tB, const Scalar& alpha, NatDesc& A, NatDesc& B,
+                        const Scalar& beta, NatDesc& C) {
+  NatProgram* Pr = &PrR;
+  NatCtx* c = Pr->ctx;
   const int es = C.es, me = c->rank;
   const bool an = tA == NOTRANS, bn = tB == NOTRANS;
   const int kt = an ? A.nt : A.mt;
-  NatProgram* Pr = new_program(c, "gemm", false);
-  if (kt == 0) return Pr;
+  if (kt == 0) return true;
+  const int j0 = last_task_on(*Pr, 0), j1 = last_task_on(*Pr, 1), j2 = last_task_on(*Pr, 2);
   const int kc = std::max(1, std::min(kt, env_int("DPLASMA_NATIVE_SUMMA_K", 4)));
   const size_t sa = (size_t)A.mb * A.nb, sb = (size_t)B.mb * B.nb;   // slots: stored tiles, ld mb
   DevPtr WA = dev_alloc(2 * (size_t)kc * C.mt * sa * es, false), WB = dev_alloc(2 * (size_t)kc * C.nt * sb * es, false);
-  if (!WA || !WB) return fail(Pr, "gemm: SUMMA slots: device allocation failed");
+  if (!WA || !WB) return false;
   Pr->keep.push_back(WA);
   Pr->keep.push_back(WB);
   auto aslot = [&](int kk, int m) { return ((long long)kk * C.mt + m) * (long long)sa; };
@@ -243,7 +259,7 @@ NatProgram* nat_dist_gemm(NatCtx* c, int prec, int tA, int tB, const Scalar& alp
           rcv.push_back(NatMsg{src, p, sb * es});
         }
       }
-    if (!pa->upload(*Pr) || !pb->upload(*Pr)) return fail(Pr, "gemm: device allocation failed");
+    if (!pa->upload(*Pr) || !pb->upload(*Pr)) return false;
     const char *a = A.data, *bb = B.data;
     const int lda = A.lld, ldb = B.lld, amb = A.mb, bmb = B.mb;
     int t_pack = -1;
@@ -251,8 +267,8 @@ NatProgram* nat_dist_gemm(NatCtx* c, int prec, int tA, int tB, const Scalar& alp
       t_pack = Pr->task(0, [=](hipStream_t s) {
         const int rc = pa->launch(prec, a, lda, wa, amb, s);
         return rc ? rc : pb->launch(prec, bb, ldb, wb, bmb, s);
-      }, {g2, x2});
-    const int t_x = add_exchange(*Pr, snd, rcv, {t_pack, g2});
+      }, {g2, x2, j0, j1, j2});
+    const int t_x = add_exchange(*Pr, snd, rcv, {t_pack, g2, j0, j1, j2});
     xch[ch] = either(t_x, ch >= 1 ? xch[ch - 1] : -1);
     auto g = std::make_shared<Gemm>();
     for (int n = C.mycol; n < C.nt; n += C.Q)
@@ -262,13 +278,186 @@ NatProgram* nat_dist_gemm(NatCtx* c, int prec, int tA, int tB, const Scalar& alp
         g->add(C.off(m, n), C.rows(m), C.cols(n), kp, 0);
       }
     if (g->empty()) continue;
-    if (!g->upload(*Pr)) return fail(Pr, "gemm: device allocation failed");
+    if (!g->upload(*Pr)) return false;
     const Scalar be = ch == 0 ? beta : one;
     char* cc = C.data;
     const int ldc = C.lld;
     gem[ch] = Pr->task(1, [=](hipStream_t s) {
       return g->launch(prec, tA, tB, alpha, wa, amb, wb, bmb, be, cc, ldc, s);
-    }, {either(t_x, t_pack)});
+    }, {either(t_x, t_pack), j0, j1, j2});
   }
-  return Pr;
+  return true;
+}
+
+// ----------------------------------------------------------------------------------------------- TRSM
+// op(A) X = alpha B (left) / X op(A) = alpha B (right) on the grid (reference: src/ztrsm_LLN.jdf and the
+// other seven variants): per step k of the solve order, the diagonal tile goes to the ranks holding block
+// row (left) / column (right) k of B, they solve it (alpha folded in at the first step) and pack it, one
+// exchange sends the solved tiles and op(A)'s panel tiles to the ranks whose remaining B tiles read them,
+// and one MFMA GEMM launch updates every remaining local tile (beta = the step's alpha, as the
+// one-process engine).  Slots are double-buffered by step parity.  Appended to Pr after everything
+// already in it (posv / potrs).
+bool nat_dist_trsm_into(NatProgram& Pr, int side, int uplo, int trans, int diag, const Scalar& alpha, NatDesc& A,
+                        NatDesc& B) {
+  NatCtx* c = Pr.ctx;
+  const int prec = B.prec, es = B.es, me = c->rank;
+  const bool left = side == LEFT, notrans = trans == NOTRANS;
+  const int nk = left ? B.mt : B.nt;
+  const bool forward = left ? ((uplo == LOWER) == notrans) : ((uplo == UPPER) == notrans);
+  const size_t sa = (size_t)A.mb * A.nb, sbt = (size_t)B.mb * B.nb;
+  const int ns = std::max(B.mt, B.nt);
+  DevPtr W = dev_alloc(2 * (sa + ns * sa + ns * sbt) * es, false);
+  if (!W) return false;
+  Pr.keep.push_back(W);
+  auto dslot = [&](int par) { return (char*)W->p + (size_t)par * (sa + ns * sa + ns * sbt) * es; };
+  auto aoff = [&](int i) { return (long long)(sa + (size_t)i * sa); };                 // elements from dslot
+  auto xoff = [&](int i) { return (long long)(sa + (size_t)ns * sa + (size_t)i * sbt); };
+  // ranks holding B tiles of block row i / block column j
+  std::set<int> bq, bp;
+  for (int j = 0; j < std::min(B.nt, B.Q); ++j) bq.insert(j % B.Q);
+  for (int i = 0; i < std::min(B.mt, B.P); ++i) bp.insert(i % B.P);
+  const Scalar one(prec, 1.0), m_one(prec, -1.0);
+  char* bb = B.data;
+  const int ldb = B.lld, amb = A.mb, bmb = B.mb;
+  // the solve follows everything already in the program (a factorisation, an earlier solve)
+  int j0 = -1, j1 = -1, j2 = -1;
+  for (int i = (int)Pr.tasks.size() - 1; i >= 0; --i) {
+    const int s = Pr.tasks[i].stream;
+    if (s == 0 && j0 < 0) j0 = i;
+    if (s == 1 && j1 < 0) j1 = i;
+    if (s == 2 && j2 < 0) j2 = i;
+  }
+  std::vector<int> gem(nk, -1), xch(nk, -1);
+  int prev_g = -1;
+  for (int s = 0; s < nk; ++s) {
+    const int k = forward ? s : nk - 1 - s, par = s % 2;
+    char* ws = dslot(par);
+    const Scalar ak = s == 0 ? alpha : one;
+    const int g2 = s >= 2 ? gem[s - 2] : -1, x2 = s >= 2 ? xch[s - 2] : -1;
+    const int base_deps[4] = {prev_g, j0, j1, j2};
+    // remaining indices of the solve order after k
+    std::vector<int> rem;
+    for (int r = s + 1; r < nk; ++r) rem.push_back(forward ? r : nk - 1 - r);
+    // diagonal tile -> the ranks holding B's block row / column k
+    std::set<int> drc;
+    if (left) for (int q : bq) drc.insert((k % B.P) * B.Q + q);
+    else for (int p : bp) drc.insert(p * B.Q + k % B.Q);
+    const int od = A.owner(k, k);
+    int t_d = -1;
+    if (me == od && !drc.empty()) {
+      char* dst = ws;
+      const char* src = A.data + A.off(k, k) * es;
+      const int lda = A.lld, rk = A.rows(k), ck = A.cols(k);
+      t_d = Pr.task(0, [=](hipStream_t st) {
+        return hipMemcpy2DAsync(dst, (size_t)amb * es, src, (size_t)lda * es, (size_t)rk * es, ck,
+                                hipMemcpyDeviceToDevice, st) == hipSuccess ? 0 : -1;
+      }, {base_deps[0], base_deps[1], base_deps[2], base_deps[3], g2, x2});
+    }
+    std::vector<NatMsg> ds, dr;
+    if (me == od)
+      for (int r : drc)
+        if (r != me) ds.push_back(NatMsg{r, ws, sa * es});
+    if (me != od && drc.count(me)) dr.push_back(NatMsg{od, ws, sa * es});
+    const int t_xd = add_exchange(Pr, ds, dr, {t_d, base_deps[0], base_deps[1], base_deps[2], base_deps[3], g2, x2});
+    // solve this rank's tiles of block row / column k, pack them into the X slots
+    auto tr = std::make_shared<Trsm1>();
+    auto pk = std::make_shared<CopyBatch>();
+    tr->tri = 0;
+    const int nn = left ? B.nt : B.mt;
+    for (int t = 0; t < nn; ++t) {
+      const int bi = left ? k : t, bj = left ? t : k;
+      if (!B.local(bi, bj)) continue;
+      tr->add(B.off(bi, bj), B.rows(bi), B.cols(bj));
+      pk->add(B.off(bi, bj), xoff(t), B.rows(bi), B.cols(bj));
+    }
+    int t_pack = -1;
+    if (!tr->it.empty()) {
+      if (!tr->upload(Pr, prec, side) || !pk->upload(Pr)) return false;
+      const int t_s = Pr.task(0, [=](hipStream_t st) {
+        return tr->launch(prec, side, uplo, trans, diag, ak, ws, amb, bb, ldb, st);
+      }, {either(t_xd, t_d), base_deps[0], base_deps[1], base_deps[2], base_deps[3]});
+      t_pack = Pr.task(0, [=](hipStream_t st) { return pk->launch(prec, bb, ldb, ws, bmb, st); }, {t_s, g2, x2});
+    }
+    if (rem.empty()) {
+      gem[s] = either(t_pack, prev_g);
+      prev_g = gem[s];
+      xch[s] = either(t_xd, s >= 1 ? xch[s - 1] : -1);
+      continue;
+    }
+    // exchange: solved tiles X(t) and op(A)'s panel tiles (index i in rem) to the ranks that read them
+    std::vector<NatMsg> ps, pr;
+    std::set<int> remset(rem.begin(), rem.end());
+    for (int t = 0; t < nn; ++t) {   // X tile t: left X(k, t) -> ranks (i % P, t % Q), i in rem
+      const int bi = left ? k : t, bj = left ? t : k;
+      const int src = B.owner(bi, bj);
+      std::set<int> cs;
+      for (size_t u = 0; u < rem.size() && u < (size_t)(left ? B.P : B.Q); ++u) {
+        const int i = rem[u];
+        cs.insert(left ? B.owner(i, t) : B.owner(t, i));
+      }
+      cs.erase(src);
+      void* p = ws + xoff(t) * es;
+      if (src == me)
+        for (int r : cs) ps.push_back(NatMsg{r, p, sbt * es});
+      else if (cs.count(me))
+        pr.push_back(NatMsg{src, p, sbt * es});
+    }
+    for (int i : rem) {   // op(A) tile: left op(A)(i, k) -> ranks (i % P, q); right op(A)(k, i) -> ranks (p, i % Q)
+      const int si = left ? (notrans ? i : k) : (notrans ? k : i), sj = left ? (notrans ? k : i) : (notrans ? i : k);
+      const int src = A.owner(si, sj);
+      std::set<int> cs;
+      if (left) for (int q : bq) cs.insert((i % B.P) * B.Q + q);
+      else for (int p : bp) cs.insert(p * B.Q + i % B.Q);
+      void* p = ws + aoff(i) * es;
+      const bool need = cs.count(me) > 0;
+      cs.erase(src);
+      if (src == me) {
+        for (int r : cs) ps.push_back(NatMsg{r, p, sa * es});   // (packed below with the other local tiles)
+      } else if (need) {
+        pr.push_back(NatMsg{src, p, sa * es});
+      }
+    }
+    // pack this rank's op(A) panel tiles that anybody reads
+    auto pa = std::make_shared<CopyBatch>();
+    for (int i : rem) {
+      const int si = left ? (notrans ? i : k) : (notrans ? k : i), sj = left ? (notrans ? k : i) : (notrans ? i : k);
+      if (A.owner(si, sj) == me) pa->add(A.off(si, sj), aoff(i), A.rows(si), A.cols(sj));
+    }
+    int t_pa = -1;
+    if (!pa->it.empty()) {
+      if (!pa->upload(Pr)) return false;
+      const char* ad = A.data;
+      const int lda = A.lld;
+      t_pa = Pr.task(0, [=](hipStream_t st) { return pa->launch(prec, ad, lda, ws, amb, st); }, {g2, x2, t_pack});
+    }
+    const int t_xp = add_exchange(Pr, ps, pr, {t_pack, t_pa, t_xd, g2, x2, base_deps[0], base_deps[1], base_deps[2],
+                                               base_deps[3]});
+    xch[s] = either(t_xp, either(t_xd, s >= 1 ? xch[s - 1] : -1));
+    // update the remaining local tiles: left B(i, t) = ak B(i, t) - op(A)(i, k) X(k, t);
+    // right B(t, i) = ak B(t, i) - X(t, k) op(A)(k, i)
+    auto g = std::make_shared<Gemm>();
+    for (int i : rem)
+      for (int t = 0; t < nn; ++t) {
+        const int bi = left ? i : t, bj = left ? t : i;
+        if (!B.local(bi, bj)) continue;
+        if (left)
+          g->add(B.off(bi, bj), B.rows(bi), B.cols(bj), {KPair{aoff(i), xoff(t), A.rows(k), 0}}, 0);
+        else
+          g->add(B.off(bi, bj), B.rows(bi), B.cols(bj), {KPair{xoff(t), aoff(i), A.rows(k), 0}}, 0);
+      }
+    const int t_in = either(t_xp, either(t_pa, either(t_pack, t_xd)));
+    if (!g->empty()) {
+      if (!g->upload(Pr)) return false;
+      const int ta = left ? (notrans ? NOTRANS : trans) : NOTRANS, tb = left ? NOTRANS : (notrans ? NOTRANS : trans);
+      // both operands live in this parity's slots (offsets from ws): A slots have ld amb, X slots bmb
+      gem[s] = Pr.task(1, [=](hipStream_t st) {
+        return left ? g->launch(prec, ta, tb, m_one, ws, amb, ws, bmb, ak, bb, ldb, st)
+                    : g->launch(prec, ta, tb, m_one, ws, bmb, ws, amb, ak, bb, ldb, st);
+      }, {t_in, prev_g, t_pack});
+    } else {
+      gem[s] = either(t_in, prev_g);
+    }
+    prev_g = gem[s];
+  }
+  return true;
 }

@@ -337,8 +337,8 @@ inline NatProgram* fail(NatProgram* P, const std::string& msg) {
   if (nat_dist_refused) {
     nat_dist_refused = false;
     const std::string op = msg.substr(0, msg.find(':'));
-    dpl_set_error((op + ": not available on a multi-process native context (potrf, gemm, the generators, the "
-                        "element-wise maps and the norms are)").c_str());
+    dpl_set_error((op + ": not available on a multi-process native context (potrf, potrs, posv, gemm, trsm, trmm, "
+                        "the generators, the element-wise maps and the norms are)").c_str());
     return nullptr;
   }
   dpl_set_error(msg.c_str());
@@ -365,3 +365,7 @@ using namespace natk;
 NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A);
 NatProgram* nat_dist_gemm(NatCtx* c, int prec, int tA, int tB, const Scalar& alpha, NatDesc& A, NatDesc& B,
                           const Scalar& beta, NatDesc& C);
+bool nat_dist_gemm_into(NatProgram& Pr, int prec, int tA, int tB, const Scalar& alpha, NatDesc& A, NatDesc& B,
+                        const Scalar& beta, NatDesc& C);
+bool nat_dist_trsm_into(NatProgram& Pr, int side, int uplo, int trans, int diag, const Scalar& alpha, NatDesc& A,
+                        NatDesc& B);

@@ -1,5 +1,5 @@
 /* ScaLAPACK F77 layer without Python on a P x Q BLACS grid of processes (RANK / WORLD_SIZE,
- * DPLASMA_NATIVE_RDV; capi/dplasma_f77.cpp -> the multi-process native engine): pdpotrf_ and pdgemm_ on
+ * DPLASMA_NATIVE_RDV; capi/dplasma_f77.cpp -> the multi-process native engine): pdpotrf_, pdgemm_, pdtrsm_ on
  * each rank's ScaLAPACK local arrays (host memory), checked entry by entry against host arithmetic on the
  * global matrices (every rank holds the formulas); the embedded interpreter must never start.
  * usage (one process per rank): RANK=r WORLD_SIZE=w test_f77_native_dist nprow */
@@ -105,6 +105,28 @@ int main(int argc, char **argv) {
     }
   printf("rank %d: pdgemm_ %dx%d grid, local max rel diff %.3e\n", me, P, Q, e / nrm);
   CHECK(e / nrm < 1e-12, "pdgemm_ local entries differ by %.3e", e / nrm);
+  /* ---- pdtrsm_: X = 2 L^{-1} B0 with L the factor pdpotrf_ left in a (lower), B0 = fb */
+  double *X = malloc(sizeof(double) * lld * (ln > 0 ? ln : 1));
+  for (int lj = 0; lj < ln; ++lj)
+    for (int li = 0; li < lm; ++li) X[li + (size_t)lj * lld] = fb(gi[li], gj[lj]);
+  double two = 2.0;
+  pdtrsm_("L", "L", "N", "N", &n, &n, &two, a, &one, &one, desc, X, &one, &one, desc);
+  double *Xh = malloc(sizeof(double) * N * N);   /* host forward substitution on the global factor S */
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i < N; ++i) {
+      double v = 2.0 * fb(i, j);
+      for (int k = 0; k < i; ++k) v -= S[i + (size_t)k * N] * Xh[k + (size_t)j * N];
+      Xh[i + (size_t)j * N] = v / S[i + (size_t)i * N];
+    }
+  e = 0, nrm = 0;
+  for (int lj = 0; lj < ln; ++lj)
+    for (int li = 0; li < lm; ++li) {
+      const double y = Xh[gi[li] + (size_t)gj[lj] * N];
+      e = fmax(e, fabs(X[li + (size_t)lj * lld] - y));
+      nrm = fmax(nrm, fabs(y));
+    }
+  printf("rank %d: pdtrsm_ %dx%d grid, local max rel diff %.3e\n", me, P, Q, e / nrm);
+  CHECK(e / nrm < 1e-11, "pdtrsm_ local entries differ by %.3e", e / nrm);
   /* no native LU on a multi-process grid: an error, not a wrong answer */
   int *ipiv = malloc(sizeof(int) * (lm + nb));
   pdgetrf_(&n, &n, A, &one, &one, desc, ipiv, &info);

@@ -117,6 +117,74 @@ static void test_gemm(int prec, int ta, int tb, int m, int n, int k, int nb) {
   free(X), free(Y);
 }
 
+/* distributed TRSM / TRMM: every rank's tiles of B equal the one-process engine's (A: the triangle of a
+ * diagonally dominant Hermitian matrix, so every solve is well conditioned) */
+static void test_trxm(int prec, int solve, int side, int uplo, int trans, int diag, int n, int nrhs, int nb) {
+  const int cplx = prec == dplasmaComplexDouble, es = cplx ? 16 : 8;
+  const int bm = side == dplasmaLeft ? n : nrhs, bn = side == dplasmaLeft ? nrhs : n;
+  dplasma_desc_t *A[2], *B[2];
+  dplasma_context_t *cx[2] = {cd, c1};
+  int ok = 1;
+  for (int s = 0; s < 2; ++s) {
+    A[s] = mat(cx[s], prec, nb, n, n), B[s] = mat(cx[s], prec, nb, bm, bn);
+    ok = ok && A[s] && B[s];
+  }
+  CHECK(ok, "descriptors");
+  if (!ok) return;
+  for (int s = 0; s < 2; ++s) {
+    int rc;
+    if (cplx) {
+      rc = dplasma_zplghe(cx[s], (double)n, dplasmaUpperLower, A[s], 21) | dplasma_zplrnt(cx[s], 0, B[s], 22);
+      rc |= solve ? dplasma_ztrsm(cx[s], side, uplo, trans, diag, 0.75 + 0.5 * I, A[s], B[s])
+                  : dplasma_ztrmm(cx[s], side, uplo, trans, diag, 0.75 + 0.5 * I, A[s], B[s]);
+    } else {
+      rc = dplasma_dplghe(cx[s], (double)n, dplasmaUpperLower, A[s], 21) | dplasma_dplrnt(cx[s], 0, B[s], 22);
+      rc |= solve ? dplasma_dtrsm(cx[s], side, uplo, trans, diag, 0.75, A[s], B[s])
+                  : dplasma_dtrmm(cx[s], side, uplo, trans, diag, 0.75, A[s], B[s]);
+    }
+    CHECK(rc == 0, "%s (%s context): %s", solve ? "trsm" : "trmm", s ? "one-process" : "distributed",
+          dplasma_last_error());
+  }
+  void *X = calloc((size_t)bm * bn, es), *Y = calloc((size_t)bm * bn, es);
+  CHECK(dplasma_desc_get_lapack(B[0], X, bm) == 0 && dplasma_desc_get_lapack(B[1], Y, bm) == 0, "get_lapack");
+  const double e = cmp_local(X, Y, cplx, bm, bn, nb, 'A');
+  CHECK(e < 1e-12, "%c%s side %d uplo %d trans %d diag %d: local tiles differ by %.3e", cplx ? 'z' : 'd',
+        solve ? "trsm" : "trmm", side, uplo, trans, diag, e);
+  if (rank == 0)
+    printf("%c%s %d/%d/%d/%d n=%d nrhs=%d grid %dx%d: max rel diff %.2e\n", cplx ? 'z' : 'd', solve ? "trsm" : "trmm",
+           side, uplo, trans, diag, n, nrhs, P, Q, e);
+  for (int s = 0; s < 2; ++s) dplasma_desc_destroy(A[s]), dplasma_desc_destroy(B[s]);
+  free(X), free(Y);
+}
+
+/* distributed posv: the solution's local tiles equal the one-process engine's */
+static void test_posv(int prec, int uplo, int n, int nrhs, int nb) {
+  const int cplx = prec == dplasmaComplexDouble, es = cplx ? 16 : 8;
+  dplasma_desc_t *A[2], *B[2];
+  dplasma_context_t *cx[2] = {cd, c1};
+  int ok = 1;
+  for (int s = 0; s < 2; ++s) {
+    A[s] = mat(cx[s], prec, nb, n, n), B[s] = mat(cx[s], prec, nb, n, nrhs);
+    ok = ok && A[s] && B[s];
+  }
+  CHECK(ok, "descriptors");
+  if (!ok) return;
+  for (int s = 0; s < 2; ++s) {
+    int rc = cplx ? (dplasma_zplghe(cx[s], (double)n, uplo, A[s], 31) | dplasma_zplrnt(cx[s], 0, B[s], 32))
+                  : (dplasma_dplghe(cx[s], (double)n, uplo, A[s], 31) | dplasma_dplrnt(cx[s], 0, B[s], 32));
+    const int info = cplx ? dplasma_zposv(cx[s], uplo, A[s], B[s]) : dplasma_dposv(cx[s], uplo, A[s], B[s]);
+    CHECK(rc == 0 && info == 0, "posv (%s context): info %d %s", s ? "one-process" : "distributed", info,
+          dplasma_last_error());
+  }
+  void *X = calloc((size_t)n * nrhs, es), *Y = calloc((size_t)n * nrhs, es);
+  CHECK(dplasma_desc_get_lapack(B[0], X, n) == 0 && dplasma_desc_get_lapack(B[1], Y, n) == 0, "get_lapack");
+  const double e = cmp_local(X, Y, cplx, n, nrhs, nb, 'A');
+  CHECK(e < 1e-11, "%cposv uplo %d: local solution tiles differ by %.3e", cplx ? 'z' : 'd', uplo, e);
+  if (rank == 0) printf("%cposv %d n=%d nrhs=%d grid %dx%d: max rel diff %.2e\n", cplx ? 'z' : 'd', uplo, n, nrhs, P, Q, e);
+  for (int s = 0; s < 2; ++s) dplasma_desc_destroy(A[s]), dplasma_desc_destroy(B[s]);
+  free(X), free(Y);
+}
+
 static void test_failing_potrf(void) {
   /* a general random matrix is not positive definite: every rank reports the one-process info */
   const int n = 700, nb = 64;
@@ -193,9 +261,9 @@ static void test_taskpool_and_refusal(void) {
     CHECK(dplasma_taskpool_result(tp) == 0, "taskpool info %d", dplasma_taskpool_result(tp));
     dplasma_dpotrf_Destruct(tp);
   }
-  /* no distributed TRSM builder: a clean error on every rank, the context stays usable */
-  const int rc = dplasma_dtrsm(cd, dplasmaLeft, dplasmaLower, dplasmaNoTrans, dplasmaNonUnit, 1.0, A, B);
-  CHECK(rc != 0 && strstr(dplasma_last_error(), "multi-process"), "dtrsm on a multi-process context: rc %d '%s'", rc,
+  /* no distributed SYMM builder: a clean error on every rank, the context stays usable */
+  const int rc = dplasma_dsymm(cd, dplasmaLeft, dplasmaLower, 1.0, A, B, 0.0, B);
+  CHECK(rc != 0 && strstr(dplasma_last_error(), "multi-process"), "dsymm on a multi-process context: rc %d '%s'", rc,
         dplasma_last_error());
   CHECK(dplasma_dlange(cd, dplasmaMaxNorm, A) > 0, "context usable after a refused call");
   dplasma_desc_destroy(A), dplasma_desc_destroy(B);
@@ -226,6 +294,18 @@ int main(int argc, char **argv) {
   test_gemm(dplasmaRealDouble, dplasmaTrans, dplasmaNoTrans, 640, 384, 520, 128);
   test_gemm(dplasmaRealDouble, dplasmaNoTrans, dplasmaTrans, 300, 700, 257, 64);
   test_gemm(dplasmaComplexDouble, dplasmaConjTrans, dplasmaTrans, 260, 330, 190, 64);
+  test_trxm(dplasmaRealDouble, 1, dplasmaLeft, dplasmaLower, dplasmaNoTrans, dplasmaNonUnit, 700, 300, 128);
+  test_trxm(dplasmaRealDouble, 1, dplasmaLeft, dplasmaUpper, dplasmaTrans, dplasmaUnit, 700, 300, 128);
+  test_trxm(dplasmaRealDouble, 1, dplasmaLeft, dplasmaUpper, dplasmaNoTrans, dplasmaNonUnit, 520, 200, 64);
+  test_trxm(dplasmaRealDouble, 1, dplasmaRight, dplasmaLower, dplasmaTrans, dplasmaNonUnit, 520, 330, 64);
+  test_trxm(dplasmaRealDouble, 1, dplasmaRight, dplasmaUpper, dplasmaNoTrans, dplasmaUnit, 520, 330, 64);
+  test_trxm(dplasmaComplexDouble, 1, dplasmaLeft, dplasmaLower, dplasmaConjTrans, dplasmaNonUnit, 300, 170, 64);
+  test_trxm(dplasmaComplexDouble, 1, dplasmaRight, dplasmaLower, dplasmaNoTrans, dplasmaNonUnit, 300, 170, 64);
+  test_trxm(dplasmaRealDouble, 0, dplasmaLeft, dplasmaLower, dplasmaNoTrans, dplasmaUnit, 600, 250, 128);
+  test_trxm(dplasmaRealDouble, 0, dplasmaRight, dplasmaUpper, dplasmaTrans, dplasmaNonUnit, 520, 330, 64);
+  test_posv(dplasmaRealDouble, dplasmaLower, 900, 130, 128);
+  test_posv(dplasmaRealDouble, dplasmaUpper, 900, 130, 128);
+  test_posv(dplasmaComplexDouble, dplasmaLower, 400, 70, 64);
   test_failing_potrf();
   test_norms_maps();
   test_taskpool_and_refusal();
