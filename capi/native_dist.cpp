@@ -93,6 +93,16 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
   const int ld = A.lld;
   int* info = (int*)Pr->info->p;
   const size_t sbytes = slot_elems * es;
+  // fp64 tiles <= 512: the dataflow tile kernel and the register-resident panel solve on its inverted 32-blocks
+  // (potrf_rb.hip, as the one-process engine); receivers invert the received factor's blocks themselves
+  const bool rb = prec == P_D && A.mb == A.nb && A.mb <= 512 && env_int("DPLASMA_NATIVE_RB", 1) == 1;
+  const int zsz = rb ? dpl_potrf_zbuf_size() : 0;
+  DevPtr zb;
+  if (rb) {
+    zb = dev_alloc((size_t)2 * zsz * sizeof(double), false);
+    if (!zb) return fail(Pr, "potrf: device allocation failed");
+    Pr->keep.push_back(zb);
+  }
 
   int next_prev = -1;                    // NEXT(k-1) (or the last panel-stream task of step k-1)
   std::vector<int> rest(nt, -1), xch(nt, -1);   // latest update-stream / communication task after step k
@@ -106,8 +116,10 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
     int t_diag = -1;
     if (me == own_k) {
       const long long dk = A.off(k, k);
+      double* zk = rb ? (double*)zb->p + (size_t)(k % 2) * zsz : nullptr;
       const int t_potrf = Pr->task(0, [=](hipStream_t s) {
-        return dpl_potrf_tile(prec, uplo, kb, base, dk, ld, info, k * mb, s);
+        return rb ? dpl_potrf_tile_rbz(uplo, kb, (double*)base + dk, ld, info, k * mb, zk, s)
+                  : dpl_potrf_tile(prec, uplo, kb, base, dk, ld, info, k * mb, s);
       }, {next_prev, rest_km2});
       char* dst = wb + slot(k) * es;   // (run-time lambdas capture values only)
       t_diag = Pr->task(0, [=](hipStream_t s) {
@@ -135,7 +147,32 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
       pk->add(A.off(t.first, t.second), slot(i), A.rows(t.first), A.cols(t.second));
     }
     int t_pack = -1;
-    if (!tr->it.empty()) {
+    if (!tr->it.empty() && rb) {
+      std::vector<RbItem> strips;   // 16-row strips of this rank's panel tiles (rows of L(i,k) / columns of U(k,i))
+      for (int i = k + 1; i < nt; ++i) {
+        const auto t = tc(i, k);
+        if (!A.local(t.first, t.second)) continue;
+        const int ext = lower ? A.rows(i) : A.cols(i);
+        for (int r0 = 0; r0 < ext; r0 += 16)
+          strips.push_back(RbItem{A.off(t.first, t.second) + (lower ? r0 : (long long)r0 * ld), std::min(16, ext - r0), 0});
+      }
+      DevPtr d = dev_upload(strips);
+      if (!d || !pk->upload(*Pr)) return fail(Pr, "potrf: device allocation failed");
+      Pr->keep.push_back(d);
+      const int nrb = (int)strips.size();
+      double* zk = (double*)zb->p + (size_t)(k % 2) * zsz;
+      const bool own = me == own_k;
+      const double* L = own ? (const double*)base + A.off(k, k) : (const double*)wb + slot(k);
+      const int ldl = own ? ld : mb;
+      const int t_trsm = Pr->task(0, [=](hipStream_t s) {
+        if (!own) {   // the factor came by exchange: invert its 32-blocks here
+          const int rc = dpl_trsm_rb_prep(uplo, kb, L, ldl, zk, s);
+          if (rc) return rc;
+        }
+        return dpl_trsm_rb(uplo, kb, L, ldl, zk, nrb, d->p, (double*)base, ld, s);
+      }, {either(t_xd, t_diag), next_prev, rest_km2});
+      t_pack = Pr->task(0, [=](hipStream_t s) { return pk->launch(prec, base, ld, wb, mb, s); }, {t_trsm, xch_km2});
+    } else if (!tr->it.empty()) {
       if (!tr->upload(*Pr, prec, side) || !pk->upload(*Pr)) return fail(Pr, "potrf: device allocation failed");
       const int t_trsm = Pr->task(0, [=](hipStream_t s) {
         return tr->launch(prec, side, uplo, CONJTRANS, NONUNIT, one, wb, mb, base, ld, s);

@@ -23,6 +23,7 @@ int dpl_potrf_tile(int prec, int uplo, int n, void* A, long long a_off, int lda,
                    hipStream_t st);
 int dpl_potrf_tile_rbz(int uplo, int n, double* A, int lda, int* info, int info_base, double* zbuf, hipStream_t st);
 int dpl_potrf_zbuf_size();
+int dpl_trsm_rb_prep(int uplo, int n, const double* L, int ldl, double* zbuf, hipStream_t st);
 int dpl_trsm_rb(int uplo, int n, const double* L, int ldl, const double* zbuf, int nrb, const void* items, double* B,
                 int ldb, hipStream_t st);
 int dpl_trsm_batched(int prec, int side, int uplo, int trans, int diag, int nitems, const void* items, int max_m,
