@@ -586,7 +586,14 @@ class _GetrfDev:
         self._update(k, "gemm_next")
 
     def rest(self, k):
-        self._update(k, "gemm_rest")
+        # DPLASMA_LU_REST_CAP=n (look-ahead): the bulk update as a grid-stride GEMM of at most n workgroups, so
+        # the next panel's persistent kernel finds room on every CU beside it instead of waiting for drains
+        cap = int(os.environ.get("DPLASMA_LU_REST_CAP", "0")) if self.lookahead else 0
+        if cap > 0:
+            with ops.gemm_wg_cap(cap):
+                self._update(k, "gemm_rest")
+        else:
+            self._update(k, "gemm_rest")
 
     def add_tasks(self, tp, tag):
         """PANEL/SWAP/NEXT/REST tasks of every step; with look-ahead PANEL(k+1) overlaps REST(k)."""
