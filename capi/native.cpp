@@ -394,6 +394,12 @@ static int add_rank_k(NatProgram& Pr, int prec, int uplo, int trans, const Scala
   const bool nt = trans == NOTRANS;
   const int ak = nt ? A->n : A->m, akb = nt ? A->nb : A->mb;
   const int ct = herm ? CONJTRANS : TRANS;
+  if (C->ctx->dist()) {   // the SUMMA GEMM over the grid, restricted to C's triangle
+    if (!nat_dist_gemm_into(Pr, prec, nt ? NOTRANS : ct, nt ? ct : NOTRANS, alpha, *const_cast<NatDesc*>(A),
+                            *const_cast<NatDesc*>(B), beta, *C, uplo))
+      return -2;
+    prev = (int)Pr.tasks.size() - 1;
+  }
   auto g = std::make_shared<Gemm>();
   const int kt = (ak + akb - 1) / akb;
   for (int n = 0; n < C->nt; ++n)
@@ -405,12 +411,15 @@ static int add_rank_k(NatProgram& Pr, int prec, int uplo, int trans, const Scala
                            nt ? A->cols(k) : A->rows(k), 0});
       g->add(C->off(m, n), C->rows(m), C->cols(n), kp, m == n ? (uplo == LOWER ? 1 : 2) : 0);
     }
-  if (!g->upload(*P)) return -2;
   char *a = A->data, *b = B->data, *cc = C->data;
   const int lda = A->lld, ldb = B->lld, ldc = C->lld;
   const int ta = nt ? NOTRANS : ct, tb = nt ? ct : NOTRANS;
-  const int t = P->task(1, [=](hipStream_t s) { return g->launch(prec, ta, tb, alpha, a, lda, b, ldb, beta, cc, ldc, s); },
-                        {prev});
+  int t = prev;
+  if (!C->ctx->dist()) {
+    if (!g->upload(*P)) return -2;
+    t = P->task(1, [=](hipStream_t s) { return g->launch(prec, ta, tb, alpha, a, lda, b, ldb, beta, cc, ldc, s); },
+                {prev});
+  }
   int last = t;
   if (herm && fixdiag) {
     // Hermitian rank-k (zherk): C's diagonal is real.  diag := (diag + conj(diag)) / 2 on the
@@ -418,9 +427,11 @@ static int add_rank_k(NatProgram& Pr, int prec, int uplo, int trans, const Scala
     std::vector<TileItem> d;
     int mm = 0;
     for (int k = 0; k < C->mt && k < C->nt; ++k) {
+      if (!C->local(k, k)) continue;
       d.push_back(TileItem{C->off(k, k), C->off(k, k), C->rows(k), C->cols(k), k * C->mb, k * C->nb});
       mm = std::max(mm, std::max(C->rows(k), C->cols(k)));
     }
+    if (d.empty()) return last;
     DevPtr dd = dev_upload(d);
     if (!dd) return -2;
     P->keep.push_back(dd);
@@ -437,7 +448,7 @@ static NatProgram* rank_k(dplasma_context_t* ctx, int prec, int uplo, int trans,
                           dplasma_desc_t* dA, const Scalar& beta, dplasma_desc_t* dC, bool herm, const char* name) {
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *C = dC ? dC->nat : nullptr;
-  if (!same_ctx(c, {A, C}, prec)) return fail(nullptr, std::string(name) + ": descriptors of another context");
+  if (!same_ctx_dist(c, {A, C}, prec)) return fail(nullptr, std::string(name) + ": descriptors of another context");
   const bool nt = trans == NOTRANS;
   const int an = nt ? A->m : A->n;
   if ((uplo != LOWER && uplo != UPPER) || C->m != C->n || an != C->m || C->mb != C->nb ||
@@ -456,7 +467,7 @@ static NatProgram* rank_2k(dplasma_context_t* ctx, int prec, int uplo, int trans
                            dplasma_desc_t* dC, bool herm, const char* name) {
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *B = dB ? dB->nat : nullptr, *C = dC ? dC->nat : nullptr;
-  if (!same_ctx(c, {A, B, C}, prec)) return fail(nullptr, std::string(name) + ": descriptors of another context");
+  if (!same_ctx_dist(c, {A, B, C}, prec)) return fail(nullptr, std::string(name) + ": descriptors of another context");
   const bool nt = trans == NOTRANS;
   if ((uplo != LOWER && uplo != UPPER) || C->m != C->n || (nt ? A->m : A->n) != C->m || A->m != B->m ||
       A->n != B->n || A->mb != B->mb || A->nb != B->nb || C->mb != C->nb || (nt ? A->mb : A->nb) != C->mb)
@@ -1016,7 +1027,14 @@ int add_expand(NatProgram& P, const NatDesc& A, int uplo, bool unit, int mode, N
   all->build(W, UPPERLOWER, nullptr, NOTRANS);
   tri->build(W, uplo, &A, NOTRANS);
   const int mtrans = mode == 2 ? CONJTRANS : TRANS;
-  if (mode > 0) mir->build(W, uplo == LOWER ? UPPER : LOWER, &A, mtrans);
+  if (mode > 0 && !W.dist()) mir->build(W, uplo == LOWER ? UPPER : LOWER, &A, mtrans);
+  if (mode > 0 && W.dist())   // the grid: diagonal tiles mirror in place, the others through nat_dist_mirror_into
+    for (int k = 0; k < W.mt && k < W.nt; ++k)
+      if (W.local(k, k)) {
+        mir->it.push_back(TileItem{A.off(k, k), W.off(k, k), W.rows(k), W.cols(k), k * W.mb, k * W.nb});
+        mir->mm = std::max(mir->mm, W.rows(k));
+        mir->nn = std::max(mir->nn, W.cols(k));
+      }
   if (!all->upload(P) || !tri->upload(P) || !mir->upload(P)) return -2;
   const int lda = A.lld, ldw = W.lld, tpart = part_of(uplo), mpart = uplo == LOWER ? 4 : 3;
   const char* a = A.data;
@@ -1033,9 +1051,14 @@ int add_expand(NatProgram& P, const NatDesc& A, int uplo, bool unit, int mode, N
   }, {prev});
   if (mode > 0)
     prev = P.task(1, [=](hipStream_t s) {
+      if (mir->n() == 0) return 0;
       return dpl_geadd(prec, mpart, mtrans, mir->n(), mir->items(), mir->mm, mir->nn, one.ptr(), a, lda, zero.ptr(),
                        w, ldw, 1, s);
     }, {prev});
+  if (mode > 0 && W.dist()) {
+    if (!nat_dist_mirror_into(P, A, uplo, mtrans, W)) return -2;
+    prev = (int)P.tasks.size() - 1;
+  }
   if ((mode == 0 && unit) || (mode == 2 && (prec == P_C || prec == P_Z))) {
     std::vector<TileItem> d;
     int mm = 0;
@@ -1126,7 +1149,7 @@ static NatProgram* symm_like(dplasma_context_t* ctx, int prec, int side, int upl
   const char* name = herm ? "hemm" : "symm";
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *B = dB ? dB->nat : nullptr, *C = dC ? dC->nat : nullptr;
-  if (!same_ctx(c, {A, B, C}, prec)) return fail(nullptr, std::string(name) + ": descriptors of another context");
+  if (!same_ctx_dist(c, {A, B, C}, prec)) return fail(nullptr, std::string(name) + ": descriptors of another context");
   const bool left = side == LEFT;
   if (A->m != A->n || A->mb != A->nb || B->m != C->m || B->n != C->n || B->mb != C->mb || B->nb != C->nb ||
       (left ? C->m : C->n) != A->m || (left ? C->mb : C->nb) != A->nb || (uplo != LOWER && uplo != UPPER))
@@ -1135,6 +1158,13 @@ static NatProgram* symm_like(dplasma_context_t* ctx, int prec, int side, int upl
   auto S = work_desc(*P, *A);
   if (!S) return fail(P, std::string(name) + ": device allocation failed");
   const int prev = add_expand(*P, *A, uplo, false, herm ? 2 : 1, *S, -1);
+  if (prev == -2) return fail(P, std::string(name) + ": device allocation failed");
+  if (c->dist()) {   // the expanded operand times B: the SUMMA GEMM over the grid
+    const Scalar al(prec, alpha), be(prec, beta);
+    const bool ok = left ? nat_dist_gemm_into(*P, prec, NOTRANS, NOTRANS, al, *S, *B, be, *C)
+                         : nat_dist_gemm_into(*P, prec, NOTRANS, NOTRANS, al, *B, *S, be, *C);
+    return ok ? P : fail(P, std::string(name) + ": device allocation failed");
+  }
   auto g = std::make_shared<Gemm>();
   for (int n = 0; n < C->nt; ++n)
     for (int m = 0; m < C->mt; ++m) {

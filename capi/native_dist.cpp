@@ -60,6 +60,12 @@ int add_exchange(NatProgram& Pr, std::vector<NatMsg> sends, std::vector<NatMsg> 
 
 int either(int a, int b) { return a >= 0 ? a : b; }
 
+int last_task_on(const NatProgram& P, int stream) {
+  for (int i = (int)P.tasks.size() - 1; i >= 0; --i)
+    if (P.tasks[i].stream == stream) return i;
+  return -1;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------- POTRF
@@ -223,22 +229,18 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
 }
 
 // ----------------------------------------------------------------------------------------------- GEMM
-static int last_task_on(const NatProgram& P, int stream) {
-  for (int i = (int)P.tasks.size() - 1; i >= 0; --i)
-    if (P.tasks[i].stream == stream) return i;
-  return -1;
-}
-
 NatProgram* nat_dist_gemm(NatCtx* c, int prec, int tA, int tB, const Scalar& alpha, NatDesc& A, NatDesc& B,
                           const Scalar& beta, NatDesc& C) {
   NatProgram* Pr = new_program(c, "gemm", false);
-  if (!nat_dist_gemm_into(*Pr, prec, tA, tB, alpha, A, B, beta, C)) return fail(Pr, "gemm: device allocation failed");
+  if (!nat_dist_gemm_into(*Pr, prec, tA, tB, alpha, A, B, beta, C, UPPERLOWER))
+    return fail(Pr, "gemm: device allocation failed");
   return Pr;
 }
 
 // appended to Pr after everything already in it
+// tri: UPPERLOWER (every C tile) or LOWER / UPPER (C's triangle only, diagonal tiles masked -- herk / syrk)
 bool nat_dist_gemm_into(NatProgram& PrR, int prec, int tA, int tB, const Scalar& alpha, NatDesc& A, NatDesc& B,
-                        const Scalar& beta, NatDesc& C) {
+                        const Scalar& beta, NatDesc& C, int tri) {
   NatProgram* Pr = &PrR;
   NatCtx* c = Pr->ctx;
   const int es = C.es, me = c->rank;
@@ -310,9 +312,10 @@ bool nat_dist_gemm_into(NatProgram& PrR, int prec, int tA, int tB, const Scalar&
     auto g = std::make_shared<Gemm>();
     for (int n = C.mycol; n < C.nt; n += C.Q)
       for (int m = C.myrow; m < C.mt; m += C.P) {
+        if ((tri == LOWER && m < n) || (tri == UPPER && m > n)) continue;
         std::vector<KPair> kp;
         for (int k = k0; k < k1; ++k) kp.push_back(KPair{aslot(k - k0, m), bslot(k - k0, n), an ? A.cols(k) : A.rows(k), 0});
-        g->add(C.off(m, n), C.rows(m), C.cols(n), kp, 0);
+        g->add(C.off(m, n), C.rows(m), C.cols(n), kp, m == n && tri != UPPERLOWER ? (tri == LOWER ? 1 : 2) : 0);
       }
     if (g->empty()) continue;
     if (!g->upload(*Pr)) return false;
@@ -496,5 +499,67 @@ bool nat_dist_trsm_into(NatProgram& Pr, int side, int uplo, int trans, int diag,
     }
     prev_g = gem[s];
   }
+  return true;
+}
+
+// ------------------------------------------------------------------------------------- mirror (symm)
+// W(m, n) := op(A(n, m)) for the strict triangle opposite A's stored uplo (op: TRANS / CONJTRANS) on the
+// grid: tiles whose mirror lives on another rank travel in one exchange (every rank walks the stored
+// triangle in the same order, so pairs match), then one transposing copy launch per source buffer.
+bool nat_dist_mirror_into(NatProgram& Pr, const NatDesc& A, int uplo, int mtrans, NatDesc& W) {
+  NatCtx* c = Pr.ctx;
+  const int prec = A.prec, es = A.es, me = c->rank;
+  const size_t st = (size_t)A.mb * A.nb;
+  std::vector<std::pair<int, int>> srcs;   // stored strict-triangle tiles (n, m) in canonical order
+  for (int n = 0; n < A.mt; ++n)
+    for (int m = 0; m < A.nt; ++m)
+      if ((uplo == LOWER && n > m) || (uplo == UPPER && n < m)) srcs.emplace_back(n, m);
+  int nsend = 0, nrecv = 0;
+  for (auto [n, m] : srcs) {
+    const int so = A.owner(n, m), dt = W.owner(m, n);
+    if (so == dt) continue;
+    if (so == me) ++nsend;
+    if (dt == me) ++nrecv;
+  }
+  DevPtr S = dev_alloc((size_t)std::max(1, nsend + nrecv) * st * es, false);
+  if (!S) return false;
+  Pr.keep.push_back(S);
+  char* sb = (char*)S->p;
+  auto pk = std::make_shared<CopyBatch>(), loc = std::make_shared<CopyBatch>(), rc = std::make_shared<CopyBatch>();
+  std::vector<NatMsg> sends, recvs;
+  int is = 0, ir = nsend;
+  for (auto [n, m] : srcs) {
+    const int so = A.owner(n, m), dt = W.owner(m, n);
+    if (so == me && dt == me) {
+      loc->add(A.off(n, m), W.off(m, n), W.rows(m), W.cols(n));   // (transposing copy: dest-sized item)
+    } else if (so == me) {
+      pk->add(A.off(n, m), (long long)is * st, A.rows(n), A.cols(m));
+      sends.push_back(NatMsg{dt, sb + (size_t)is * st * es, st * es});
+      ++is;
+    } else if (dt == me) {
+      rc->add((long long)ir * st, W.off(m, n), W.rows(m), W.cols(n));
+      recvs.push_back(NatMsg{so, sb + (size_t)ir * st * es, st * es});
+      ++ir;
+    }
+  }
+  if (!pk->upload(Pr) || !loc->upload(Pr) || !rc->upload(Pr)) return false;
+  const int j0 = last_task_on(Pr, 0), j1 = last_task_on(Pr, 1), j2 = last_task_on(Pr, 2);
+  const char* a = A.data;
+  char* w = W.data;
+  const int lda = A.lld, ldw = W.lld, mb = A.mb;
+  const Scalar one(prec, 1.0), zero(prec, 0.0);
+  auto tcopy = [=](std::shared_ptr<CopyBatch> b, const char* src, int lds) {
+    return [=](hipStream_t s) {
+      if (b->it.empty()) return 0;
+      return dpl_geadd(prec, 0, mtrans, (int)b->it.size(), b->d->p, b->mm, b->nn, one.ptr(), src, lds, zero.ptr(), w,
+                       ldw, 1, s);
+    };
+  };
+  int t_pk = -1;
+  if (!pk->it.empty())
+    t_pk = Pr.task(0, [=](hipStream_t s) { return pk->launch(prec, a, lda, sb, mb, s); }, {j0, j1, j2});
+  const int t_x = add_exchange(Pr, sends, recvs, {t_pk, j0, j1, j2});
+  int last = Pr.task(1, tcopy(loc, a, lda), {j0, j1, j2});
+  if (!rc->it.empty()) last = Pr.task(1, tcopy(rc, sb, mb), {last, t_x});
   return true;
 }

@@ -338,7 +338,7 @@ inline NatProgram* fail(NatProgram* P, const std::string& msg) {
   if (nat_dist_refused) {
     nat_dist_refused = false;
     const std::string op = msg.substr(0, msg.find(':'));
-    dpl_set_error((op + ": not available on a multi-process native context (potrf, potrs, posv, gemm, trsm, trmm, "
+    dpl_set_error((op + ": not available on a multi-process native context (potrf, potrs, posv, the level-3 BLAS, "
                         "the generators, the element-wise maps and the norms are)").c_str());
     return nullptr;
   }
@@ -367,6 +367,7 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A);
 NatProgram* nat_dist_gemm(NatCtx* c, int prec, int tA, int tB, const Scalar& alpha, NatDesc& A, NatDesc& B,
                           const Scalar& beta, NatDesc& C);
 bool nat_dist_gemm_into(NatProgram& Pr, int prec, int tA, int tB, const Scalar& alpha, NatDesc& A, NatDesc& B,
-                        const Scalar& beta, NatDesc& C);
+                        const Scalar& beta, NatDesc& C, int tri = UPPERLOWER);
+bool nat_dist_mirror_into(NatProgram& Pr, const NatDesc& A, int uplo, int mtrans, NatDesc& W);
 bool nat_dist_trsm_into(NatProgram& Pr, int side, int uplo, int trans, int diag, const Scalar& alpha, NatDesc& A,
                         NatDesc& B);

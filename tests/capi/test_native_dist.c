@@ -185,6 +185,53 @@ static void test_posv(int prec, int uplo, int n, int nrhs, int nb) {
   free(X), free(Y);
 }
 
+/* distributed level-3 BLAS with a symmetric / Hermitian operand or result: local tiles (of C's triangle for
+ * the rank-k updates) equal the one-process engine's.  kind: 0 syrk, 1 herk, 2 syr2k, 3 her2k, 4 symm, 5 hemm */
+static void test_blas3(int kind, int uplo, int trans_or_side, int n, int k, int nb) {
+  const int cplx = kind == 1 || kind == 3 || kind == 5, es = cplx ? 16 : 8, prec = cplx ? dplasmaComplexDouble : dplasmaRealDouble;
+  const int rank_k = kind <= 3, nt = trans_or_side == dplasmaNoTrans;
+  /* rank-k: A, B are n x k (NoTrans) or k x n; symm / hemm: A n x n (side Left) or k x k, B / C n x k */
+  const int am = rank_k ? (nt ? n : k) : (trans_or_side == dplasmaLeft ? n : k);
+  const int an = rank_k ? (nt ? k : n) : am;
+  const int cm = n, cn = rank_k ? n : k;
+  dplasma_desc_t *A[2], *B[2], *C[2];
+  dplasma_context_t *cx[2] = {cd, c1};
+  int ok = 1;
+  for (int s = 0; s < 2; ++s) {
+    A[s] = mat(cx[s], prec, nb, am, an);
+    B[s] = mat(cx[s], prec, nb, rank_k ? am : cm, rank_k ? an : cn);
+    C[s] = mat(cx[s], prec, nb, cm, cn);
+    ok = ok && A[s] && B[s] && C[s];
+  }
+  CHECK(ok, "descriptors");
+  if (!ok) return;
+  for (int s = 0; s < 2; ++s) {
+    int rc = cplx ? (dplasma_zplrnt(cx[s], 0, A[s], 41) | dplasma_zplrnt(cx[s], 0, B[s], 42))
+                  : (dplasma_dplrnt(cx[s], 0, A[s], 41) | dplasma_dplrnt(cx[s], 0, B[s], 42));
+    if (kind == 1 || kind == 3) rc |= dplasma_zplghe(cx[s], 1.0, dplasmaUpperLower, C[s], 43);
+    else if (cplx) rc |= dplasma_zplrnt(cx[s], 0, C[s], 43);
+    else rc |= dplasma_dplrnt(cx[s], 0, C[s], 43);
+    switch (kind) {
+      case 0: rc |= dplasma_dsyrk(cx[s], uplo, trans_or_side, 1.25, A[s], -0.5, C[s]); break;
+      case 1: rc |= dplasma_zherk(cx[s], uplo, trans_or_side, 1.25, A[s], -0.5, C[s]); break;
+      case 2: rc |= dplasma_dsyr2k(cx[s], uplo, trans_or_side, 1.25, A[s], B[s], -0.5, C[s]); break;
+      case 3: rc |= dplasma_zher2k(cx[s], uplo, trans_or_side, 1.25 - 0.5 * I, A[s], B[s], -0.5, C[s]); break;
+      case 4: rc |= dplasma_dsymm(cx[s], trans_or_side, uplo, 1.25, A[s], B[s], -0.5, C[s]); break;
+      default: rc |= dplasma_zhemm(cx[s], trans_or_side, uplo, 1.25 - 0.5 * I, A[s], B[s], -0.5 + 0.25 * I, C[s]); break;
+    }
+    CHECK(rc == 0, "blas3 kind %d (%s context): %s", kind, s ? "one-process" : "distributed", dplasma_last_error());
+  }
+  void *X = calloc((size_t)cm * cn, es), *Y = calloc((size_t)cm * cn, es);
+  CHECK(dplasma_desc_get_lapack(C[0], X, cm) == 0 && dplasma_desc_get_lapack(C[1], Y, cm) == 0, "get_lapack");
+  const char part = rank_k ? (uplo == dplasmaLower ? 'L' : 'U') : 'A';
+  const double e = cmp_local(X, Y, cplx, cm, cn, nb, part);
+  static const char *nm[6] = {"dsyrk", "zherk", "dsyr2k", "zher2k", "dsymm", "zhemm"};
+  CHECK(e < 1e-12, "%s uplo %d %d: local tiles differ by %.3e", nm[kind], uplo, trans_or_side, e);
+  if (rank == 0) printf("%s %d/%d n=%d k=%d grid %dx%d: max rel diff %.2e\n", nm[kind], uplo, trans_or_side, n, k, P, Q, e);
+  for (int s = 0; s < 2; ++s) dplasma_desc_destroy(A[s]), dplasma_desc_destroy(B[s]), dplasma_desc_destroy(C[s]);
+  free(X), free(Y);
+}
+
 static void test_failing_potrf(void) {
   /* a general random matrix is not positive definite: every rank reports the one-process info */
   const int n = 700, nb = 64;
@@ -261,9 +308,9 @@ static void test_taskpool_and_refusal(void) {
     CHECK(dplasma_taskpool_result(tp) == 0, "taskpool info %d", dplasma_taskpool_result(tp));
     dplasma_dpotrf_Destruct(tp);
   }
-  /* no distributed SYMM builder: a clean error on every rank, the context stays usable */
-  const int rc = dplasma_dsymm(cd, dplasmaLeft, dplasmaLower, 1.0, A, B, 0.0, B);
-  CHECK(rc != 0 && strstr(dplasma_last_error(), "multi-process"), "dsymm on a multi-process context: rc %d '%s'", rc,
+  /* no distributed TRTRI builder: a clean error on every rank, the context stays usable */
+  const int rc = dplasma_dtrtri(cd, dplasmaLower, dplasmaNonUnit, A);
+  CHECK(rc != 0 && strstr(dplasma_last_error(), "multi-process"), "dtrtri on a multi-process context: rc %d '%s'", rc,
         dplasma_last_error());
   CHECK(dplasma_dlange(cd, dplasmaMaxNorm, A) > 0, "context usable after a refused call");
   dplasma_desc_destroy(A), dplasma_desc_destroy(B);
@@ -303,6 +350,14 @@ int main(int argc, char **argv) {
   test_trxm(dplasmaComplexDouble, 1, dplasmaRight, dplasmaLower, dplasmaNoTrans, dplasmaNonUnit, 300, 170, 64);
   test_trxm(dplasmaRealDouble, 0, dplasmaLeft, dplasmaLower, dplasmaNoTrans, dplasmaUnit, 600, 250, 128);
   test_trxm(dplasmaRealDouble, 0, dplasmaRight, dplasmaUpper, dplasmaTrans, dplasmaNonUnit, 520, 330, 64);
+  test_blas3(0, dplasmaLower, dplasmaNoTrans, 530, 300, 64);
+  test_blas3(0, dplasmaUpper, dplasmaTrans, 530, 300, 64);
+  test_blas3(1, dplasmaLower, dplasmaConjTrans, 330, 200, 64);
+  test_blas3(2, dplasmaUpper, dplasmaNoTrans, 400, 270, 64);
+  test_blas3(3, dplasmaLower, dplasmaNoTrans, 330, 200, 64);
+  test_blas3(4, dplasmaLower, dplasmaLeft, 450, 310, 64);
+  test_blas3(4, dplasmaUpper, dplasmaRight, 450, 310, 64);
+  test_blas3(5, dplasmaUpper, dplasmaLeft, 300, 170, 64);
   test_posv(dplasmaRealDouble, dplasmaLower, 900, 130, 128);
   test_posv(dplasmaRealDouble, dplasmaUpper, 900, 130, 128);
   test_posv(dplasmaComplexDouble, dplasmaLower, 400, 70, 64);

@@ -12,7 +12,7 @@ for cfg in ${CFGS:-2:2 2:1 4:2}; do
     pids+=($!)
   done
   rc=0; for p in "${pids[@]}"; do wait $p || rc=$?; done
-  echo "world=$W P=$P rc=$rc"; for ((r=0; r<W; r++)); do grep -E "FAIL|passed|failed|diff" gpurun_out/b11_w${W}p${P}_r$r.log | head -20; done
+  echo "world=$W P=$P rc=$rc"; for ((r=0; r<W; r++)); do grep -E "FAIL|passed|failed|diff" gpurun_out/b11_w${W}p${P}_r$r.log | tail -40; done
   [ $rc -ne 0 ] && exit $rc
 done
 exit 0
