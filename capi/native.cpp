@@ -1203,10 +1203,11 @@ NatProgram* nat_hemm(dplasma_context_t* ctx, int prec, int side, int uplo, const
 static double norm_sym(dplasma_context_t* ctx, int prec, int ntype, int uplo, dplasma_desc_t* dA, bool herm) {
   NatDesc* A = dA ? dA->nat : nullptr;
   const char* name = herm ? "lanhe" : "lansy";
-  if (!same_ctx(ctx->nat, {A}, prec) || (uplo != LOWER && uplo != UPPER) || A->m != A->n || A->mb != A->nb) {
+  if (!same_ctx_dist(ctx->nat, {A}, prec) || (uplo != LOWER && uplo != UPPER) || A->m != A->n || A->mb != A->nb) {
     dpl_set_error((std::string(name) + ": bad descriptor or uplo").c_str());
     return NAN;
   }
+  // (a multi-process context: the mirrored triangle is exchanged, then the partial norms all-reduced)
   NatProgram* P = new_program(ctx->nat, name, false);
   auto S = work_desc(*P, *A);
   if (!S || add_expand(*P, *A, uplo, false, herm ? 2 : 1, *S, -1) == -2) {
@@ -1256,15 +1257,19 @@ int add_trtri(NatProgram& P, int uplo, int diag, NatDesc& A, int prev) {
   char *xd = X->data, *ad = A.data;
   const int ldx = X->lld, lda = A.lld;
   prev = P.task(1, [=](hipStream_t s) {   // X := I
+    if (all->n() == 0) return 0;
     return dpl_laset(prec, 0, all->n(), all->items(), all->mm, all->nn, zero.ptr(), one.ptr(), xd, ldx, s);
   }, {prev});
-  if (!add_trsm(P, LEFT, uplo, NOTRANS, diag, one, A, *X, 1, prev)) return -2;
+  if (A.ctx->dist() ? !nat_dist_trsm_into(P, LEFT, uplo, NOTRANS, diag, one, A, *X)
+                    : !add_trsm(P, LEFT, uplo, NOTRANS, diag, one, A, *X, 1, prev))
+    return -2;
   // strictly lower / upper for a unit diagonal (the diagonal of A is not referenced), else with it
   const int part = uplo == LOWER ? (diag == UNIT ? 3 : 1) : (diag == UNIT ? 4 : 2);
   return P.task(1, [=](hipStream_t s) {
+    if (back->n() == 0) return 0;
     return dpl_geadd(prec, part, NOTRANS, back->n(), back->items(), back->mm, back->nn, one.ptr(), xd, ldx,
                      zero.ptr(), ad, lda, 1, s);
-  }, {last_on(P, 1)});
+  }, {last_on(P, 0), last_on(P, 1), last_on(P, 2)});
 }
 
 int add_lauum(NatProgram& P, int uplo, NatDesc& A, int prev) {
@@ -1288,7 +1293,7 @@ bool square_tiles(const NatDesc* A, int uplo) {
 
 NatProgram* nat_trtri(dplasma_context_t* ctx, int prec, int uplo, int diag, dplasma_desc_t* dA) {
   NatDesc* A = dA ? dA->nat : nullptr;
-  if (!same_ctx(ctx->nat, {A}, prec) || !square_tiles(A, uplo))
+  if (!same_ctx_dist(ctx->nat, {A}, prec) || !square_tiles(A, uplo))
     return fail(nullptr, "trtri: square matrix with square tiles and uplo Lower/Upper required");
   NatProgram* P = new_program(ctx->nat, "trtri", false);
   if (add_trtri(*P, uplo, diag, *A, -1) == -2) return fail(P, "trtri: device allocation failed");
@@ -1297,7 +1302,7 @@ NatProgram* nat_trtri(dplasma_context_t* ctx, int prec, int uplo, int diag, dpla
 
 NatProgram* nat_lauum(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* dA) {
   NatDesc* A = dA ? dA->nat : nullptr;
-  if (!same_ctx(ctx->nat, {A}, prec) || !square_tiles(A, uplo))
+  if (!same_ctx_dist(ctx->nat, {A}, prec) || !square_tiles(A, uplo))
     return fail(nullptr, "lauum: square matrix with square tiles and uplo Lower/Upper required");
   NatProgram* P = new_program(ctx->nat, "lauum", false);
   if (add_lauum(*P, uplo, *A, -1) == -2) return fail(P, "lauum: device allocation failed");
@@ -1306,7 +1311,7 @@ NatProgram* nat_lauum(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t
 
 NatProgram* nat_potri(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* dA) {
   NatDesc* A = dA ? dA->nat : nullptr;
-  if (!same_ctx(ctx->nat, {A}, prec) || !square_tiles(A, uplo))
+  if (!same_ctx_dist(ctx->nat, {A}, prec) || !square_tiles(A, uplo))
     return fail(nullptr, "potri: square matrix with square tiles and uplo Lower/Upper required");
   NatProgram* P = new_program(ctx->nat, "potri", false);
   int t = add_trtri(*P, uplo, NONUNIT, *A, -1);

@@ -232,6 +232,35 @@ static void test_blas3(int kind, int uplo, int trans_or_side, int n, int k, int 
   free(X), free(Y);
 }
 
+/* distributed inversions: trtri (via the distributed solve on the identity), lauum (triangle product on C's
+ * triangle), potri and poinv; the stored triangle's local tiles equal the one-process engine's.
+ * kind: 0 trtri, 1 lauum, 2 potri (on a Cholesky factor), 3 poinv */
+static void test_inv(int kind, int uplo, int diag, int n, int nb) {
+  dplasma_desc_t *A[2];
+  dplasma_context_t *cx[2] = {cd, c1};
+  A[0] = mat(cd, dplasmaRealDouble, nb, n, n), A[1] = mat(c1, dplasmaRealDouble, nb, n, n);
+  if (!A[0] || !A[1]) { CHECK(0, "descriptors"); return; }
+  for (int s = 0; s < 2; ++s) {
+    int rc = dplasma_dplghe(cx[s], (double)n, dplasmaUpperLower, A[s], 51);
+    if (kind == 2) rc |= dplasma_dpotrf(cx[s], uplo, A[s]);
+    switch (kind) {
+      case 0: rc |= dplasma_dtrtri(cx[s], uplo, diag, A[s]); break;
+      case 1: rc |= dplasma_dlauum(cx[s], uplo, A[s]); break;
+      case 2: rc |= dplasma_dpotri(cx[s], uplo, A[s]); break;
+      default: rc |= dplasma_dpoinv(cx[s], uplo, A[s]); break;
+    }
+    CHECK(rc == 0, "inversion kind %d (%s context): %s", kind, s ? "one-process" : "distributed", dplasma_last_error());
+  }
+  double *X = calloc((size_t)n * n, 8), *Y = calloc((size_t)n * n, 8);
+  CHECK(dplasma_desc_get_lapack(A[0], X, n) == 0 && dplasma_desc_get_lapack(A[1], Y, n) == 0, "get_lapack");
+  const double e = cmp_local(X, Y, 0, n, n, nb, uplo == dplasmaLower ? 'L' : 'U');
+  static const char *nm[4] = {"dtrtri", "dlauum", "dpotri", "dpoinv"};
+  CHECK(e < 1e-11, "%s uplo %d diag %d: local tiles differ by %.3e", nm[kind], uplo, diag, e);
+  if (rank == 0) printf("%s %d/%d n=%d grid %dx%d: max rel diff %.2e\n", nm[kind], uplo, diag, n, P, Q, e);
+  dplasma_desc_destroy(A[0]), dplasma_desc_destroy(A[1]);
+  free(X), free(Y);
+}
+
 static void test_failing_potrf(void) {
   /* a general random matrix is not positive definite: every rank reports the one-process info */
   const int n = 700, nb = 64;
@@ -288,6 +317,26 @@ static void test_norms_maps(void) {
   CHECK(dplasma_dgeadd(cd, dplasmaNoTrans, -1.0, A, 2.0, A2) == 0, "dgeadd: %s", dplasma_last_error());
   const double d = dplasma_dlange(cd, dplasmaFrobeniusNorm, A2), a = dplasma_dlange(cd, dplasmaFrobeniusNorm, A);
   CHECK(fabs(d - a) <= 1e-12 * a, "lacpy + geadd: |A2|_F %.15g vs |A|_F %.15g", d, a);
+  {   /* symmetric / Hermitian norms of a square matrix's triangle (mirror exchange + all-reduced partials) */
+    const int ns = 450, nbs = 64;
+    dplasma_desc_t *S0 = mat(cd, dplasmaRealDouble, nbs, ns, ns), *S1 = mat(c1, dplasmaRealDouble, nbs, ns, ns);
+    dplasma_desc_t *Z0 = mat(cd, dplasmaComplexDouble, nbs, ns, ns), *Z1 = mat(c1, dplasmaComplexDouble, nbs, ns, ns);
+    if (S0 && S1 && Z0 && Z1) {
+      dplasma_dplrnt(cd, 0, S0, 9), dplasma_dplrnt(c1, 0, S1, 9);
+      dplasma_zplrnt(cd, 0, Z0, 9), dplasma_zplrnt(c1, 0, Z1, 9);
+      for (int t = 0; t < 4; ++t)
+        for (int u = 0; u < 2; ++u) {
+          const int up = u ? dplasmaUpper : dplasmaLower;
+          const double x = dplasma_dlansy(cd, nt[t], up, S0), y = dplasma_dlansy(c1, nt[t], up, S1);
+          CHECK(fabs(x - y) <= 1e-12 * y, "dlansy %d %d: %.15g vs one process %.15g", nt[t], up, x, y);
+          const double zx = dplasma_zlanhe(cd, nt[t], up, Z0), zy = dplasma_zlanhe(c1, nt[t], up, Z1);
+          CHECK(fabs(zx - zy) <= 1e-12 * zy, "zlanhe %d %d: %.15g vs one process %.15g", nt[t], up, zx, zy);
+        }
+    } else {
+      CHECK(0, "descriptors");
+    }
+    dplasma_desc_destroy(S0), dplasma_desc_destroy(S1), dplasma_desc_destroy(Z0), dplasma_desc_destroy(Z1);
+  }
   CHECK(dplasma_dlaset(cd, dplasmaLower, 0.0, 3.0, A2) == 0, "dlaset: %s", dplasma_last_error());
   CHECK(dplasma_dlaset(c1, dplasmaLower, 0.0, 3.0, B) == 0, "dlaset (one process)");
   const double l1 = dplasma_dlange(cd, dplasmaOneNorm, A2), l2 = dplasma_dlange(c1, dplasmaOneNorm, B);
@@ -308,9 +357,9 @@ static void test_taskpool_and_refusal(void) {
     CHECK(dplasma_taskpool_result(tp) == 0, "taskpool info %d", dplasma_taskpool_result(tp));
     dplasma_dpotrf_Destruct(tp);
   }
-  /* no distributed TRTRI builder: a clean error on every rank, the context stays usable */
-  const int rc = dplasma_dtrtri(cd, dplasmaLower, dplasmaNonUnit, A);
-  CHECK(rc != 0 && strstr(dplasma_last_error(), "multi-process"), "dtrtri on a multi-process context: rc %d '%s'", rc,
+  /* no distributed QR builder: a clean error on every rank, the context stays usable */
+  const int rc = dplasma_dgeqrf(cd, A, B);
+  CHECK(rc != 0 && strstr(dplasma_last_error(), "multi-process"), "dgeqrf on a multi-process context: rc %d '%s'", rc,
         dplasma_last_error());
   CHECK(dplasma_dlange(cd, dplasmaMaxNorm, A) > 0, "context usable after a refused call");
   dplasma_desc_destroy(A), dplasma_desc_destroy(B);
@@ -358,6 +407,12 @@ int main(int argc, char **argv) {
   test_blas3(4, dplasmaLower, dplasmaLeft, 450, 310, 64);
   test_blas3(4, dplasmaUpper, dplasmaRight, 450, 310, 64);
   test_blas3(5, dplasmaUpper, dplasmaLeft, 300, 170, 64);
+  test_inv(0, dplasmaLower, dplasmaNonUnit, 520, 64);
+  test_inv(0, dplasmaUpper, dplasmaUnit, 520, 64);
+  test_inv(1, dplasmaLower, dplasmaNonUnit, 450, 64);
+  test_inv(1, dplasmaUpper, dplasmaNonUnit, 450, 64);
+  test_inv(2, dplasmaLower, dplasmaNonUnit, 450, 64);
+  test_inv(3, dplasmaUpper, dplasmaNonUnit, 450, 64);
   test_posv(dplasmaRealDouble, dplasmaLower, 900, 130, 128);
   test_posv(dplasmaRealDouble, dplasmaUpper, 900, 130, 128);
   test_posv(dplasmaComplexDouble, dplasmaLower, 400, 70, 64);
