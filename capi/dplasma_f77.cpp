@@ -352,8 +352,19 @@ static int latsqr_work(const int* desca) {
     int info = IP ? dplasma_##P##getrf_1d(native_ctx(), A.d, IP) : -1;                                           \
     if (IP && ipiv) {                                                                                             \
       std::vector<int> p(k);                                                                                      \
-      if (dplasma_desc_get_lapack(IP, p.data(), 1) == 0)                                                          \
-        for (int i = 0; i < k; ++i) ipiv[i] = p[i] + ia - 1;   /* global row of the whole array */             \
+      if (dplasma_desc_get_lapack(IP, p.data(), 1) == 0) {                                                        \
+        if (dplasma_context_world(native_ctx()) > 1) {   /* ScaLAPACK layout: the entries of my local rows */  \
+          const int mbv = da[4], me = dplasma_context_rank(native_ctx()), myrow = me / g_npcol;                  \
+          int mm = m, mbb = mbv, r = myrow, z = 0, pr = g_nprow;                                                  \
+          const int lm = numroc_(&mm, &mbb, &r, &z, &pr);                                                         \
+          for (int li = 0; li < lm; ++li) {                                                                       \
+            const int gi = ((li / mbv) * g_nprow + myrow) * mbv + li % mbv;                                       \
+            if (gi < k) ipiv[li] = p[gi];                                                                         \
+          }                                                                                                       \
+        } else {                                                                                                  \
+          for (int i = 0; i < k; ++i) ipiv[i] = p[i] + ia - 1;   /* global row of the whole array */           \
+        }                                                                                                         \
+      }                                                                                                           \
     }                                                                                                             \
     if (IP) dplasma_desc_destroy(IP);                                                                             \
     unwrap(A, true);                                                                                              \

@@ -18,6 +18,9 @@
 // variants), herk / syrk, the element-wise maps (geadd, tradd, lacpy, laset, lascal), the norms lange /
 // lantr, plghe, plgsy, plrnt.
 // Every other entry point returns an error on a native context.
+#include <map>
+#include <set>
+
 #include "native_comm.h"
 #include "native_internal.h"
 
@@ -873,7 +876,9 @@ dplasma_desc_t* nat_desc(dplasma_context_t* ctx, int prec, int mb, int nb, int m
                          int lld, int on_device) {
   NatCtx* c = ctx->nat;
   if (P <= 0 || Q <= 0) P = c->P, Q = c->Q;   // the context's grid
-  if ((!prec_ok(prec) && prec != P_I) || mb <= 0 || nb <= 0 || m < 0 || n < 0 || P != c->P || Q != c->Q) {
+  if (prec == P_I) P = Q = 1;   // pivot vectors: replicated on every rank of a grid
+  if ((!prec_ok(prec) && prec != P_I) || mb <= 0 || nb <= 0 || m < 0 || n < 0 ||
+      (prec != P_I && (P != c->P || Q != c->Q))) {
     dpl_set_error("native descriptor: the context's process grid (P = Q = 1 on one process), positive tile "
                   "sizes, s/d/c/z");
     return nullptr;
@@ -894,10 +899,10 @@ dplasma_desc_t* nat_desc(dplasma_context_t* ctx, int prec, int mb, int nb, int m
   d->nt = (n + nb - 1) / nb;
   d->P = P;
   d->Q = Q;
-  d->myrow = c->myrow;
-  d->mycol = c->mycol;
-  d->lm = nat_numroc(m, mb, c->myrow, P);
-  d->ln = nat_numroc(n, nb, c->mycol, Q);
+  d->myrow = P > 1 ? c->myrow : 0;
+  d->mycol = Q > 1 ? c->mycol : 0;
+  d->lm = nat_numroc(m, mb, d->myrow, P);
+  d->ln = nat_numroc(n, nb, d->mycol, Q);
   if (data) {
     if (lld < std::max(1, d->lm)) {
       delete d;
@@ -1489,6 +1494,215 @@ bool add_getrf(NatProgram& P, NatDesc& A, NatDesc& IP, int& last) {
   return true;
 }
 
+// The net row interchanges of one panel step (rows r0 + j <-> r0 + piv[j], j < kmin, in order; piv on the
+// device, 0-based within the panel) applied to every local tile column of B on a grid: planned on the host
+// at run time (one synchronisation), rows that cross process rows travel point to point within the process
+// column, every source row read before any destination is written.  RB: scratch for 2 x (mb + 16) rows.
+int add_rowmoves_dist(NatProgram& P, NatDesc& B, const int* piv, int r0, int kmin, const DevPtr& RB, int prev) {
+  NatComm* comm = P.ctx->comm;
+  const int prec = B.prec, mb = B.mb, ld = B.lld, es = B.es, Pg = B.P, Q = B.Q, ln = B.ln;
+  const int myrow = B.myrow, mycol = B.mycol;
+  char *a = B.data, *rb = (char*)RB->p;
+  const Scalar one(prec, 1.0), zero(prec, 0.0);
+  auto lrow = [=](int r) { return (long long)((r / mb) / Pg) * mb + r % mb; };   // local row of a global row
+  return P.task(1, [=](hipStream_t s) {
+    if (ln == 0 || kmin == 0) return 0;
+    std::vector<int> hp(kmin);
+    if (hipStreamSynchronize(s) != hipSuccess ||
+        hipMemcpy(hp.data(), piv, sizeof(int) * kmin, hipMemcpyDeviceToHost) != hipSuccess)
+      return -1;
+    // row -> row whose content it holds, touched rows only (std::map: references stay valid while the
+    // swaps insert, and every rank walks the moves in the same ascending order)
+    std::map<int, int> content;
+    auto find = [&](int r) -> int& { return content.try_emplace(r, r).first->second; };
+    for (int j = 0; j < kmin; ++j) std::swap(find(r0 + j), find(r0 + hp[j]));
+    std::vector<TileItem> pack, ul, ur;
+    std::vector<NatMsg> snd, rcv;
+    const long long rs = ln;   // one packed row: ln contiguous entries
+    int ns = 0, nr = 0;
+    char* sbuf = rb;
+    char* rbuf = rb + (size_t)2 * (mb + 16) * ln * es;
+    for (const auto& [d, src] : content) {
+      if (d == src) continue;
+      const int pd = (d / mb) % Pg, ps = (src / mb) % Pg;
+      if (ps == myrow) {
+        pack.push_back(TileItem{lrow(src), ns * rs, 1, ln, 0, 0});
+        if (pd == myrow) ul.push_back(TileItem{ns * rs, lrow(d), 1, ln, 0, 0});
+        else snd.push_back(NatMsg{pd * Q + mycol, sbuf + (size_t)ns * rs * es, (size_t)rs * es});
+        ++ns;
+      } else if (pd == myrow) {
+        ur.push_back(TileItem{nr * rs, lrow(d), 1, ln, 0, 0});
+        rcv.push_back(NatMsg{ps * Q + mycol, rbuf + (size_t)nr * rs * es, (size_t)rs * es});
+        ++nr;
+      }
+    }
+    auto launch = [&](const std::vector<TileItem>& it, const char* src, int lds, char* dst, int ldd) -> int {
+      if (it.empty()) return 0;
+      void* d = nullptr;
+      if (hipMalloc(&d, it.size() * sizeof(TileItem)) != hipSuccess) return -1;
+      int rc = hipMemcpy(d, it.data(), it.size() * sizeof(TileItem), hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+      if (rc == 0) rc = dpl_geadd(prec, 0, NOTRANS, (int)it.size(), d, 1, ln, one.ptr(), src, lds, zero.ptr(), dst, ldd, 1, s);
+      if (rc == 0 && hipStreamSynchronize(s) != hipSuccess) rc = -1;
+      (void)hipFree(d);
+      return rc;
+    };
+    int rc = launch(pack, a, ld, sbuf, 1);
+    if (rc == 0) rc = comm->exchange(snd, rcv, s);
+    if (rc == 0) rc = launch(ul, sbuf, 1, a, ld);
+    if (rc == 0) rc = launch(ur, rbuf, 1, a, ld);
+    return rc;
+  }, {prev});
+}
+
+// getrs (NoTrans) on a grid: the pivots of every panel step applied to B's rows, then L (unit) and U solves
+bool add_getrs_dist(NatProgram& P, NatDesc& A, NatDesc& IP, NatDesc& B) {
+  const int kt = std::min(A.mt, A.nt), mb = A.mb;
+  DevPtr RB = dev_alloc((size_t)2 * 2 * (mb + 16) * std::max(1, B.ln) * B.es, false);
+  DevPtr PV = dev_alloc(sizeof(int) * (mb + 16), false);
+  if (!RB || !PV) return false;
+  P.keep.push_back(RB);
+  P.keep.push_back(PV);
+  const int* ipg = (const int*)IP.data;
+  int* pv = (int*)PV->p;
+  int prev = (int)P.tasks.size() - 1;   // after everything so far (a factorisation)
+  for (int k = 0; k < kt; ++k) {
+    const int r0 = k * mb, kmin = std::min(A.m - r0, A.cols(k));
+    // IPIV holds 1-based global rows: back to 0-based within the panel for the planner
+    prev = P.task(1, [=](hipStream_t s) { return dpl_ipiv_shift(ipg + r0, pv, kmin, -(r0 + 1), s); },
+                  {prev, last_on(P, 0), last_on(P, 2)});
+    prev = add_rowmoves_dist(P, B, pv, r0, kmin, RB, prev);
+  }
+  const Scalar one(B.prec, 1.0);
+  return nat_dist_trsm_into(P, LEFT, LOWER, NOTRANS, UNIT, one, A, B) &&
+         nat_dist_trsm_into(P, LEFT, UPPER, NOTRANS, NONUNIT, one, A, B);
+}
+
+// LU with partial pivoting on a P x Q grid (multi-process native context; reference src/zgetrf_1d.jdf /
+// zgetrf_ptgpanel.jdf): per panel step every rank receives the whole panel (one exchange), factors it
+// redundantly with the device recursion above -- identical inputs and deterministic kernels give every rank
+// the same pivots and factors, the role of the reference's distributed pivot search --, applies the net
+// row interchanges to its local tile columns (rows that cross process rows travel point to point within
+// the process column; the moves are planned on the host from the pivots, one synchronisation per panel),
+// writes its panel tiles back, the panel's process row solves its U row, U travels down the process
+// columns, and one MFMA GEMM launch updates the local trailing tiles.  All on one stream, in order.
+bool add_getrf_dist(NatProgram& P, NatDesc& A, NatDesc& IP) {
+  NatCtx* c = P.ctx;
+  NatComm* comm = c->comm;
+  const int prec = A.prec, mb = A.mb, ld = A.lld, es = A.es, me = c->rank, Pg = A.P, Qg = A.Q;
+  const int kt = std::min(A.mt, A.nt), ln = A.ln;
+  LuScratch S;
+  if (!lu_scratch(P, A, S)) return false;
+  const size_t st = (size_t)mb * A.nb;
+  DevPtr TS = dev_alloc((size_t)std::max(1, A.mt) * st * es, false), US = dev_alloc((size_t)std::max(1, A.nt) * st * es, false);
+  DevPtr RB = dev_alloc((size_t)2 * 2 * (mb + 16) * std::max(1, ln) * es, false);   // row-move send / receive rows
+  if (!TS || !US || !RB) return false;
+  for (const DevPtr& d : {TS, US, RB}) P.keep.push_back(d);
+  char *a = A.data, *pvb = (char*)S.pv->p, *ts = (char*)TS->p, *us = (char*)US->p, *rb = (char*)RB->p;
+  int* info = (int*)P.info->p;
+  int* ipg = (int*)IP.data;
+  const int* piv = (const int*)S.piv->p;
+  const Scalar one(prec, 1.0), m_one(prec, -1.0), zero(prec, 0.0);
+  int prev = -1;
+  for (int k = 0; k < kt; ++k) {
+    const int kb = A.cols(k), r0 = k * mb, mp = A.m - r0, kmin = std::min(mp, kb);
+    // ---- 1. the panel to every rank: owners pack, one exchange, scatter into the contiguous panel (ld mp)
+    auto pk = std::make_shared<MapBatch>(), sc = std::make_shared<MapBatch>(), back = std::make_shared<MapBatch>();
+    auto sends = std::make_shared<std::vector<NatMsg>>(), recvs = std::make_shared<std::vector<NatMsg>>();
+    for (int m = k; m < A.mt; ++m) {
+      const int src = A.owner(m, k);
+      char* slot = ts + (size_t)m * st * es;
+      if (src == me) {
+        pk->it.push_back(TileItem{A.off(m, k), (long long)m * (long long)st, A.rows(m), kb, 0, 0});
+        back->it.push_back(TileItem{(long long)(m - k) * mb, A.off(m, k), A.rows(m), kb, 0, 0});
+        for (int r = 0; r < c->world; ++r)
+          if (r != me) sends->push_back(NatMsg{r, slot, st * es});
+      } else {
+        recvs->push_back(NatMsg{src, slot, st * es});
+      }
+      sc->it.push_back(TileItem{(long long)m * (long long)st, (long long)(m - k) * mb, A.rows(m), kb, 0, 0});
+      pk->mm = sc->mm = back->mm = std::max(pk->mm, A.rows(m));
+    }
+    pk->nn = sc->nn = back->nn = kb;
+    if (!pk->upload(P) || !sc->upload(P) || !back->upload(P)) return false;
+    prev = P.task(1, [=](hipStream_t s) {
+      int rc = pk->n() ? dpl_geadd(prec, 0, NOTRANS, pk->n(), pk->items(), pk->mm, pk->nn, one.ptr(), a, ld, zero.ptr(),
+                                   ts, mb, 1, s) : 0;
+      if (rc == 0) rc = comm->exchange(*sends, *recvs, s);
+      if (rc == 0)
+        rc = dpl_geadd(prec, 0, NOTRANS, sc->n(), sc->items(), sc->mm, sc->nn, one.ptr(), ts, mb, zero.ptr(), pvb, mp, 1, s);
+      return rc;
+    }, {prev});
+    // ---- 2. the panel factorisation (every rank, the same result)
+    prev = add_panel_lu(P, prec, pvb, mp, mp, 0, kmin, S, info, r0, prev);
+    if (prev < 0) return false;
+    if (kb > kmin) {
+      prev = P.task(1, [=](hipStream_t s) { return dpl_laswp_panel(prec, pvb, mp, kmin, kb, piv, 0, kmin, s); }, {prev});
+      auto tr = std::make_shared<Trsm1>();
+      tr->tri = 0;
+      tr->add((long long)kmin * mp, kmin, kb - kmin);
+      if (!tr->upload(P, prec, LEFT)) return false;
+      prev = P.task(1, [=](hipStream_t s) { return tr->launch(prec, LEFT, LOWER, NOTRANS, UNIT, one, pvb, mp, pvb, mp, s); },
+                    {prev});
+    }
+    prev = P.task(1, [=](hipStream_t s) { return dpl_ipiv_shift(piv, ipg + r0, kmin, r0 + 1, s); }, {prev});
+    // ---- 3. net row interchanges on this rank's tile columns, planned from the pivots
+    prev = add_rowmoves_dist(P, A, piv, r0, kmin, RB, prev);
+    // ---- 4. my tiles of the factored panel back into A
+    prev = P.task(1, [=](hipStream_t s) {
+      if (back->n() == 0) return 0;
+      return dpl_geadd(prec, 0, NOTRANS, back->n(), back->items(), back->mm, back->nn, one.ptr(), pvb, mp, zero.ptr(),
+                       a, ld, 1, s);
+    }, {prev});
+    if (k + 1 >= A.nt) continue;
+    // ---- 5. U row (the panel's process row) and 6. U down the process columns
+    auto tr = std::make_shared<Trsm1>();
+    auto pu = std::make_shared<MapBatch>();
+    tr->tri = 0;
+    auto usend = std::make_shared<std::vector<NatMsg>>(), urecv = std::make_shared<std::vector<NatMsg>>();
+    for (int n = k + 1; n < A.nt; ++n) {
+      const int src = A.owner(k, n);
+      char* slot = us + (size_t)n * st * es;
+      if (src == me) {
+        tr->add(A.off(k, n), kmin, A.cols(n));
+        pu->it.push_back(TileItem{A.off(k, n), (long long)n * (long long)st, kmin, A.cols(n), 0, 0});
+        pu->mm = std::max(pu->mm, kmin);
+        pu->nn = std::max(pu->nn, A.cols(n));
+      }
+      std::set<int> cs;   // ranks holding trailing tiles (m > k) of tile column n
+      for (int m = k + 1; m < std::min(A.mt, k + 1 + Pg); ++m) cs.insert(A.owner(m, n));
+      cs.erase(src);
+      if (src == me)
+        for (int r : cs) usend->push_back(NatMsg{r, slot, st * es});
+      else if (cs.count(me))
+        urecv->push_back(NatMsg{src, slot, st * es});
+    }
+    if (!tr->it.empty()) {
+      if (!tr->upload(P, prec, LEFT) || !pu->upload(P)) return false;
+      prev = P.task(1, [=](hipStream_t s) {
+        int rc = tr->launch(prec, LEFT, LOWER, NOTRANS, UNIT, one, pvb, mp, a, ld, s);
+        if (rc == 0)
+          rc = dpl_geadd(prec, 0, NOTRANS, pu->n(), pu->items(), pu->mm, pu->nn, one.ptr(), a, ld, zero.ptr(), us, mb, 1, s);
+        return rc;
+      }, {prev});
+    }
+    prev = P.task(1, [=](hipStream_t s) { return comm->exchange(*usend, *urecv, s); }, {prev});
+    // ---- 7. trailing update of my tiles
+    if (k + 1 >= A.mt) continue;
+    auto g = std::make_shared<Gemm>();
+    for (int n = k + 1; n < A.nt; ++n)
+      for (int m = k + 1; m < A.mt; ++m)
+        if (A.local(m, n))
+          g->add(A.off(m, n), A.rows(m), A.cols(n), {KPair{(long long)(m - k) * mb, (long long)n * (long long)st, kmin, 0}},
+                 0);
+    if (g->empty()) continue;
+    if (!g->upload(P)) return false;
+    prev = P.task(1, [=](hipStream_t s) {
+      return g->launch(prec, NOTRANS, NOTRANS, m_one, pvb, mp, us, mb, one, a, ld, s);
+    }, {prev});
+  }
+  return true;
+}
+
 // op(A) X = B with A = P L U from add_getrf (reference getrs: laswp + two TRSM, or the transposed order)
 bool add_getrs(NatProgram& P, int trans, NatDesc& A, NatDesc& IP, NatDesc& B, int& last) {
   const int kt = std::min(A.mt, A.nt);
@@ -1544,12 +1758,13 @@ bool lu_conform(const NatDesc* A, const NatDesc* IP) {
 NatProgram* nat_getrf_1d(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dplasma_desc_t* dIP) {
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *IP = dIP ? dIP->nat : nullptr;
-  if (!same_ctx(c, {A}, prec) || !IP || IP->ctx != c)
+  if (!same_ctx_dist(c, {A}, prec) || !IP || IP->ctx != c)
     return fail(nullptr, "getrf_1d: descriptors of another context or precision");
   if (!lu_conform(A, IP)) return fail(nullptr, "getrf_1d: square tiles <= 512 and an IPIV of min(M, N) entries");
   NatProgram* P = new_program(c, "getrf_1d", true);
   int last = -1;
-  if (!P->info || !add_getrf(*P, *A, *IP, last)) return fail(P, "getrf_1d: device allocation failed");
+  if (!P->info || !(c->dist() ? add_getrf_dist(*P, *A, *IP) : add_getrf(*P, *A, *IP, last)))
+    return fail(P, "getrf_1d: device allocation failed");
   return P;
 }
 
@@ -1557,13 +1772,15 @@ NatProgram* nat_getrs(dplasma_context_t* ctx, int prec, int trans, dplasma_desc_
                       dplasma_desc_t* dB) {
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *IP = dIP ? dIP->nat : nullptr, *B = dB ? dB->nat : nullptr;
-  if (!same_ctx(c, {A, B}, prec) || !IP || IP->ctx != c)
+  if (!same_ctx_dist(c, {A, B}, prec) || !IP || IP->ctx != c)
     return fail(nullptr, "getrs: descriptors of another context or precision");
   if (!lu_conform(A, IP) || A->m != A->n || B->m != A->n || B->mb != A->mb)
     return fail(nullptr, "getrs: operands do not conform");
+  if (c->dist() && trans != NOTRANS) return fail(nullptr, "getrs: a multi-process context solves A X = B only");
   NatProgram* P = new_program(c, "getrs", false);
   int last = -1;
-  if (!add_getrs(*P, trans, *A, *IP, *B, last)) return fail(P, "getrs: device allocation failed");
+  if (!(c->dist() ? add_getrs_dist(*P, *A, *IP, *B) : add_getrs(*P, trans, *A, *IP, *B, last)))
+    return fail(P, "getrs: device allocation failed");
   return P;
 }
 
@@ -1571,14 +1788,15 @@ NatProgram* nat_gesv_1d(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dp
                         dplasma_desc_t* dB) {
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *IP = dIP ? dIP->nat : nullptr, *B = dB ? dB->nat : nullptr;
-  if (!same_ctx(c, {A, B}, prec) || !IP || IP->ctx != c)
+  if (!same_ctx_dist(c, {A, B}, prec) || !IP || IP->ctx != c)
     return fail(nullptr, "gesv_1d: descriptors of another context or precision");
   if (!lu_conform(A, IP) || A->m != A->n || B->m != A->n || B->mb != A->mb)
     return fail(nullptr, "gesv_1d: operands do not conform");
   NatProgram* P = new_program(c, "gesv_1d", true);
   int last = -1;
-  if (!P->info || !add_getrf(*P, *A, *IP, last) || !add_getrs(*P, NOTRANS, *A, *IP, *B, last))
-    return fail(P, "gesv_1d: device allocation failed");
+  const bool ok = c->dist() ? add_getrf_dist(*P, *A, *IP) && add_getrs_dist(*P, *A, *IP, *B)
+                            : add_getrf(*P, *A, *IP, last) && add_getrs(*P, NOTRANS, *A, *IP, *B, last);
+  if (!P->info || !ok) return fail(P, "gesv_1d: device allocation failed");
   return P;
 }
 

@@ -1,5 +1,5 @@
 /* ScaLAPACK F77 layer without Python on a P x Q BLACS grid of processes (RANK / WORLD_SIZE,
- * DPLASMA_NATIVE_RDV; capi/dplasma_f77.cpp -> the multi-process native engine): pdpotrf_, pdgemm_, pdtrsm_ on
+ * DPLASMA_NATIVE_RDV; capi/dplasma_f77.cpp -> the multi-process native engine): pdpotrf_, pdgemm_, pdtrsm_, pdgetrf_ on
  * each rank's ScaLAPACK local arrays (host memory), checked entry by entry against host arithmetic on the
  * global matrices (every rank holds the formulas); the embedded interpreter must never start.
  * usage (one process per rank): RANK=r WORLD_SIZE=w test_f77_native_dist nprow */
@@ -127,10 +127,44 @@ int main(int argc, char **argv) {
     }
   printf("rank %d: pdtrsm_ %dx%d grid, local max rel diff %.3e\n", me, P, Q, e / nrm);
   CHECK(e / nrm < 1e-11, "pdtrsm_ local entries differ by %.3e", e / nrm);
-  /* no native LU on a multi-process grid: an error, not a wrong answer */
+  /* ---- pdgetrf_: LU with partial pivoting of fa on the grid against a host dgetf2 of the global matrix
+   * (IPIV in ScaLAPACK layout: the global pivot row of each local row) */
   int *ipiv = malloc(sizeof(int) * (lm + nb));
+  for (int lj = 0; lj < ln; ++lj)
+    for (int li = 0; li < lm; ++li) A[li + (size_t)lj * lld] = fa(gi[li], gj[lj]);
   pdgetrf_(&n, &n, A, &one, &one, desc, ipiv, &info);
-  CHECK(info < 0, "pdgetrf_ on a multi-process native grid returned info %d", info);
+  CHECK(info == 0, "pdgetrf_ info %d: %s", info, dplasma_last_error());
+  double *G = malloc(sizeof(double) * N * N);
+  int *hp = malloc(sizeof(int) * N);
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i < N; ++i) G[i + (size_t)j * N] = fa(i, j);
+  for (int k = 0; k < N; ++k) {
+    int p = k;
+    for (int i = k + 1; i < N; ++i)
+      if (fabs(G[i + (size_t)k * N]) > fabs(G[p + (size_t)k * N])) p = i;
+    hp[k] = p + 1;
+    if (p != k)
+      for (int j = 0; j < N; ++j) {
+        const double t = G[k + (size_t)j * N];
+        G[k + (size_t)j * N] = G[p + (size_t)j * N];
+        G[p + (size_t)j * N] = t;
+      }
+    for (int i = k + 1; i < N; ++i) G[i + (size_t)k * N] /= G[k + (size_t)k * N];
+    for (int j = k + 1; j < N; ++j)
+      for (int i = k + 1; i < N; ++i) G[i + (size_t)j * N] -= G[i + (size_t)k * N] * G[k + (size_t)j * N];
+  }
+  int piv_ok = 1;
+  for (int li = 0; li < lm; ++li) piv_ok = piv_ok && ipiv[li] == hp[gi[li]];
+  e = 0, nrm = 0;
+  for (int lj = 0; lj < ln; ++lj)
+    for (int li = 0; li < lm; ++li) {
+      const double y = G[gi[li] + (size_t)gj[lj] * N];
+      e = fmax(e, fabs(A[li + (size_t)lj * lld] - y));
+      nrm = fmax(nrm, fabs(y));
+    }
+  printf("rank %d: pdgetrf_ %dx%d grid, pivots %s, local max rel diff %.3e\n", me, P, Q, piv_ok ? "equal" : "DIFFER",
+         e / nrm);
+  CHECK(piv_ok && e / nrm < 1e-10, "pdgetrf_ pivots %d, local entries differ by %.3e", piv_ok, e / nrm);
   CHECK(!dplasma_python_active(), "the embedded interpreter was started");
   parsec_fini_wrapper_();
   if (fails) {

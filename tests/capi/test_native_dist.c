@@ -261,6 +261,57 @@ static void test_inv(int kind, int uplo, int diag, int n, int nb) {
   free(X), free(Y);
 }
 
+/* distributed LU with partial pivoting (getrf_1d) and gesv: the pivots (replicated) and every rank's tiles
+ * of the factors / solution equal the one-process engine's */
+static void test_lu(int prec, int m, int n, int nrhs, int nb) {
+  const int cplx = prec == dplasmaComplexDouble, es = cplx ? 16 : 8, k = m < n ? m : n;
+  dplasma_desc_t *A[2], *IP[2], *B[2] = {NULL, NULL};
+  dplasma_context_t *cx[2] = {cd, c1};
+  int ok = 1;
+  for (int s = 0; s < 2; ++s) {
+    A[s] = mat(cx[s], prec, nb, m, n);
+    IP[s] = dplasma_desc_ipiv(cx[s], 1, nb, 1, k, 1, 1);
+    if (nrhs) B[s] = mat(cx[s], prec, nb, m, nrhs);
+    ok = ok && A[s] && IP[s] && (!nrhs || B[s]);
+  }
+  CHECK(ok, "descriptors: %s", dplasma_last_error());
+  if (!ok) return;
+  for (int s = 0; s < 2; ++s) {
+    int rc = cplx ? dplasma_zplrnt(cx[s], 0, A[s], 61) : dplasma_dplrnt(cx[s], 0, A[s], 61);
+    if (nrhs) rc |= cplx ? dplasma_zplrnt(cx[s], 0, B[s], 62) : dplasma_dplrnt(cx[s], 0, B[s], 62);
+    int info;
+    if (nrhs) info = cplx ? dplasma_zgesv_1d(cx[s], A[s], IP[s], B[s]) : dplasma_dgesv_1d(cx[s], A[s], IP[s], B[s]);
+    else info = cplx ? dplasma_zgetrf_1d(cx[s], A[s], IP[s]) : dplasma_dgetrf_1d(cx[s], A[s], IP[s]);
+    CHECK(rc == 0 && info == 0, "%s (%s context): info %d %s", nrhs ? "gesv" : "getrf", s ? "one-process" : "distributed",
+          info, dplasma_last_error());
+  }
+  int *p0 = calloc(k, sizeof(int)), *p1 = calloc(k, sizeof(int));
+  CHECK(dplasma_desc_get_lapack(IP[0], p0, 1) == 0 && dplasma_desc_get_lapack(IP[1], p1, 1) == 0, "ipiv get");
+  int same = 1;
+  for (int i = 0; i < k; ++i) same = same && p0[i] == p1[i];
+  CHECK(same, "pivots differ from one process");
+  void *X = calloc((size_t)m * n, es), *Y = calloc((size_t)m * n, es);
+  CHECK(dplasma_desc_get_lapack(A[0], X, m) == 0 && dplasma_desc_get_lapack(A[1], Y, m) == 0, "get_lapack");
+  double e = cmp_local(X, Y, cplx, m, n, nb, 'A');
+  CHECK(e < 1e-12, "%cgetrf %dx%d: local factor tiles differ by %.3e", cplx ? 'z' : 'd', m, n, e);
+  if (nrhs) {
+    void *U = calloc((size_t)m * nrhs, es), *V = calloc((size_t)m * nrhs, es);
+    CHECK(dplasma_desc_get_lapack(B[0], U, m) == 0 && dplasma_desc_get_lapack(B[1], V, m) == 0, "get_lapack");
+    const double eb = cmp_local(U, V, cplx, m, nrhs, nb, 'A');
+    CHECK(eb < 1e-11, "%cgesv: local solution tiles differ by %.3e", cplx ? 'z' : 'd', eb);
+    if (eb > e) e = eb;
+    free(U), free(V);
+  }
+  if (rank == 0)
+    printf("%c%s %dx%d nrhs=%d grid %dx%d: pivots %s, max rel diff %.2e\n", cplx ? 'z' : 'd', nrhs ? "gesv" : "getrf", m,
+           n, nrhs, P, Q, same ? "identical" : "DIFFER", e);
+  for (int s = 0; s < 2; ++s) {
+    dplasma_desc_destroy(A[s]), dplasma_desc_destroy(IP[s]);
+    if (B[s]) dplasma_desc_destroy(B[s]);
+  }
+  free(X), free(Y), free(p0), free(p1);
+}
+
 static void test_failing_potrf(void) {
   /* a general random matrix is not positive definite: every rank reports the one-process info */
   const int n = 700, nb = 64;
@@ -413,6 +464,11 @@ int main(int argc, char **argv) {
   test_inv(1, dplasmaUpper, dplasmaNonUnit, 450, 64);
   test_inv(2, dplasmaLower, dplasmaNonUnit, 450, 64);
   test_inv(3, dplasmaUpper, dplasmaNonUnit, 450, 64);
+  test_lu(dplasmaRealDouble, 600, 600, 0, 64);
+  test_lu(dplasmaRealDouble, 700, 500, 0, 64);
+  test_lu(dplasmaRealDouble, 400, 600, 0, 64);
+  test_lu(dplasmaRealDouble, 640, 640, 90, 128);
+  test_lu(dplasmaComplexDouble, 300, 300, 40, 64);
   test_posv(dplasmaRealDouble, dplasmaLower, 900, 130, 128);
   test_posv(dplasmaRealDouble, dplasmaUpper, 900, 130, 128);
   test_posv(dplasmaComplexDouble, dplasmaLower, 400, 70, 64);
