@@ -171,8 +171,10 @@ def main():
           "/* interpreter-free multi-process context (capi/native_dist.cpp): rank of world processes, one GPU",
           " * each, on a P x (world / P) grid (rank = myrow * Q + mycol); descriptors are this rank's tiles of the",
           " * 2-D block-cyclic distribution in ScaLAPACK local layout, desc_set/get_lapack take the whole matrix;",
-          " * potrf, gemm, plghe / plgsy / plrnt, geadd / tradd / lacpy / laset / lascal and lange / lantr run",
-          " * across the ranks.  Tiles move through RCCL (a GPU per rank) or node-local files (ranks sharing a",
+          " * the Cholesky family (potrf / potrs / posv / potri / poinv / trtri / lauum), LU with partial pivoting",
+          " * (getrf_1d / getrs / gesv_1d), the level-3 BLAS (gemm, trsm, trmm, herk / syrk / her2k / syr2k,",
+          " * symm / hemm), the generators, the element-wise maps and the norms run across the ranks; the",
+          " * other operations return an error there.  Tiles move through RCCL (a GPU per rank) or node-local files (ranks sharing a",
           " * GPU); DPLASMA_NATIVE_TRANSPORT=rccl|file overrides.  rdv_dir: a fresh directory every rank can",
           " * reach (NULL: $DPLASMA_NATIVE_RDV) */",
           "dplasma_context_t *dplasma_init_native_dist(int device, int rank, int world, int P, const char *rdv_dir);",
