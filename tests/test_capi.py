@@ -227,3 +227,26 @@ def test_capi_f77_native_dist_gpu(tmp_path, world, nprow):
     print(text)
     for r, (p, out) in enumerate(zip(procs, outs)):
         assert p.returncode == 0 and f"rank {r}: F77 NATIVE DIST OK" in out, text
+
+
+@pytest.mark.gpu
+def test_native_dist_example_gpu(tmp_path):
+    """examples/native_dist_example.c on a 2 x 1 grid of ranks sharing the GPU: distributed posv residual and a
+    timed distributed dpotrf printed in the reference tester's [****] format."""
+    _build(tmp_path)
+    exe = str(tmp_path / "native_dist_example")
+    subprocess.run(["gcc", "-O2", "-o", exe, os.path.join(ROOT, "examples", "native_dist_example.c"),
+                    "-I" + os.path.join(ROOT, "capi", "include"), "-L" + LIB, "-ldplasma", "-lm",
+                    "-Wl,-rpath," + LIB], check=True)
+    procs = []
+    for r in range(2):
+        env = dict(os.environ)
+        env.pop("PYTHONPATH", None)
+        env.update(RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0", DPLASMA_NATIVE_RDV=str(tmp_path / "rdv"),
+                   DPLASMA_NATIVE_TRANSPORT="file", DPLASMA_NATIVE_TIMEOUT="200")
+        procs.append(subprocess.Popen([exe, "2048", "256", "2"], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      text=True, env=env))
+    outs = [p.communicate(timeout=300)[0] for p in procs]
+    print("\n".join(outs))
+    assert all(p.returncode == 0 for p in procs), "\n".join(outs)
+    assert "(ok)" in outs[0] and "[****] TIME(s)" in outs[0]
