@@ -550,28 +550,42 @@ struct MapBatch {
   const void* items() const { return d ? d->p : nullptr; }
 };
 
+namespace {
+std::shared_ptr<NatDesc> work_desc(NatProgram& P, const NatDesc& A);
+}
+
 static NatProgram* map_add(dplasma_context_t* ctx, int prec, int uplo, int trans, const Scalar& alpha,
                            dplasma_desc_t* dA, const Scalar& beta, dplasma_desc_t* dB, int copy, const char* name) {
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *B = dB ? dB->nat : nullptr;
   if (!same_ctx_dist(c, {A, B}, prec)) return fail(nullptr, std::string(name) + ": descriptors of another context");
   const bool nt = trans == NOTRANS;
-  if (c->dist() && !nt) return fail(nullptr, std::string(name) + ": transposed operand on a multi-process context");
   if ((nt ? A->m : A->n) != B->m || (nt ? A->n : A->m) != B->n || (nt ? A->mb : A->nb) != B->mb ||
       (nt ? A->nb : A->mb) != B->nb)
     return fail(nullptr, std::string(name) + ": operands do not conform");
   NatProgram* P = new_program(c, name, false);
+  int trans_eff = trans;
+  const NatDesc* src = A;
+  int first = -1;
+  if (c->dist() && !nt) {   // the grid: op(A) is first transposed tile by tile into B's distribution
+    auto W = work_desc(*P, *B);
+    if (!W || !nat_dist_mirror_into(*P, *A, UPPERLOWER, trans, *W))
+      return fail(P, std::string(name) + ": device allocation failed");
+    src = W.get();
+    trans_eff = NOTRANS;
+    first = (int)P->tasks.size() - 1;
+  }
   auto mb = std::make_shared<MapBatch>();
-  mb->build(*B, uplo, A, trans);
+  mb->build(*B, uplo, src, trans_eff);
   if (!mb->upload(*P)) return fail(P, std::string(name) + ": device allocation failed");
-  const int part = part_of(uplo), lda = A->lld, ldb = B->lld;
-  const char* a = A->data;
+  const int part = part_of(uplo), lda = src->lld, ldb = B->lld;
+  const char* a = src->data;
   char* b = B->data;
   P->task(1, [=](hipStream_t s) {
     if (mb->n() == 0) return 0;
-    return dpl_geadd(prec, part, trans, mb->n(), mb->items(), mb->mm, mb->nn, alpha.ptr(), a, lda, beta.ptr(), b,
+    return dpl_geadd(prec, part, trans_eff, mb->n(), mb->items(), mb->mm, mb->nn, alpha.ptr(), a, lda, beta.ptr(), b,
                      ldb, copy, s);
-  }, {});
+  }, {first, last_on(*P, 0), last_on(*P, 2)});
   return P;
 }
 

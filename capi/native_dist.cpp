@@ -503,7 +503,8 @@ bool nat_dist_trsm_into(NatProgram& Pr, int side, int uplo, int trans, int diag,
 }
 
 // ------------------------------------------------------------------------------------- mirror (symm)
-// W(m, n) := op(A(n, m)) for the strict triangle opposite A's stored uplo (op: TRANS / CONJTRANS) on the
+// W(m, n) := op(A(n, m)) for the strict triangle opposite A's stored uplo (op: TRANS / CONJTRANS) -- or for
+// every tile with uplo = UPPERLOWER (a distributed transpose: geadd / tradd with op(A)) -- on the
 // grid: tiles whose mirror lives on another rank travel in one exchange (every rank walks the stored
 // triangle in the same order, so pairs match), then one transposing copy launch per source buffer.
 bool nat_dist_mirror_into(NatProgram& Pr, const NatDesc& A, int uplo, int mtrans, NatDesc& W) {
@@ -513,7 +514,7 @@ bool nat_dist_mirror_into(NatProgram& Pr, const NatDesc& A, int uplo, int mtrans
   std::vector<std::pair<int, int>> srcs;   // stored strict-triangle tiles (n, m) in canonical order
   for (int n = 0; n < A.mt; ++n)
     for (int m = 0; m < A.nt; ++m)
-      if ((uplo == LOWER && n > m) || (uplo == UPPER && n < m)) srcs.emplace_back(n, m);
+      if ((uplo == LOWER && n > m) || (uplo == UPPER && n < m) || uplo == UPPERLOWER) srcs.emplace_back(n, m);
   int nsend = 0, nrecv = 0;
   for (auto [n, m] : srcs) {
     const int so = A.owner(n, m), dt = W.owner(m, n);

@@ -312,6 +312,38 @@ static void test_lu(int prec, int m, int n, int nrhs, int nb) {
   free(X), free(Y), free(p0), free(p1);
 }
 
+/* transposed maps on the grid (a tile-by-tile distributed transpose): geadd / tradd with op(A) */
+static void test_trans_maps(int cplx, int uplo, int m, int n, int nb) {
+  const int prec = cplx ? dplasmaComplexDouble : dplasmaRealDouble, es = cplx ? 16 : 8;
+  dplasma_desc_t *A[2], *B[2];
+  dplasma_context_t *cx[2] = {cd, c1};
+  int ok = 1;
+  for (int s = 0; s < 2; ++s) {
+    A[s] = mat(cx[s], prec, nb, n, m), B[s] = mat(cx[s], prec, nb, m, n);
+    ok = ok && A[s] && B[s];
+  }
+  CHECK(ok, "descriptors");
+  if (!ok) return;
+  for (int s = 0; s < 2; ++s) {
+    int rc;
+    if (cplx) {
+      rc = dplasma_zplrnt(cx[s], 0, A[s], 71) | dplasma_zplrnt(cx[s], 0, B[s], 72);
+      rc |= dplasma_ztradd(cx[s], uplo, dplasmaConjTrans, 2.0 - 1.0 * I, A[s], -1.0, B[s]);
+    } else {
+      rc = dplasma_dplrnt(cx[s], 0, A[s], 71) | dplasma_dplrnt(cx[s], 0, B[s], 72);
+      rc |= dplasma_dgeadd(cx[s], dplasmaTrans, 2.0, A[s], -1.0, B[s]);
+    }
+    CHECK(rc == 0, "transposed map (%s context): %s", s ? "one-process" : "distributed", dplasma_last_error());
+  }
+  void *X = calloc((size_t)m * n, es), *Y = calloc((size_t)m * n, es);
+  CHECK(dplasma_desc_get_lapack(B[0], X, m) == 0 && dplasma_desc_get_lapack(B[1], Y, m) == 0, "get_lapack");
+  const double e = cmp_local(X, Y, cplx, m, n, nb, 'A');
+  CHECK(e == 0.0, "%s with op(A): local tiles differ by %.3e", cplx ? "ztradd" : "dgeadd", e);
+  if (rank == 0) printf("%s op(A) %dx%d grid %dx%d: max rel diff %.2e\n", cplx ? "ztradd" : "dgeadd", m, n, P, Q, e);
+  for (int s = 0; s < 2; ++s) dplasma_desc_destroy(A[s]), dplasma_desc_destroy(B[s]);
+  free(X), free(Y);
+}
+
 static void test_failing_potrf(void) {
   /* a general random matrix is not positive definite: every rank reports the one-process info */
   const int n = 700, nb = 64;
@@ -472,6 +504,8 @@ int main(int argc, char **argv) {
   test_posv(dplasmaRealDouble, dplasmaLower, 900, 130, 128);
   test_posv(dplasmaRealDouble, dplasmaUpper, 900, 130, 128);
   test_posv(dplasmaComplexDouble, dplasmaLower, 400, 70, 64);
+  test_trans_maps(0, dplasmaUpperLower, 530, 410, 64);
+  test_trans_maps(1, dplasmaLower, 330, 330, 64);
   test_failing_potrf();
   test_norms_maps();
   test_taskpool_and_refusal();
