@@ -930,10 +930,9 @@ dplasma_desc_t* nat_desc(dplasma_context_t* ctx, int prec, int mb, int nb, int m
     d->lld = prec == P_I ? std::max(1, d->lm) : std::max(16, (d->lm + 15) / 16 * 16);
     void* p = nullptr;
     const size_t bytes = (size_t)d->lld * std::max(1, d->ln) * d->es;
-    // hipMemset runs on the null stream, which the context's non-blocking streams do not wait for: the zeros
-    // must have landed before any kernel of those streams touches the buffer
-    if (hipMalloc(&p, bytes) != hipSuccess || hipMemset(p, 0, bytes) != hipSuccess ||
-        hipDeviceSynchronize() != hipSuccess) {
+    // the zeros must have landed before any kernel of the context's non-blocking streams touches the
+    // buffer: a private stream + hipStreamSynchronize (see dpl_zero_sync in csrc/kernels/common.h)
+    if (hipMalloc(&p, bytes) != hipSuccess || nat_zero_sync(p, bytes) != hipSuccess) {
       delete d;
       dpl_set_error("native descriptor: device allocation failed");
       return nullptr;

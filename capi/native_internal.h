@@ -94,12 +94,24 @@ struct DevMem {
 };
 using DevPtr = std::shared_ptr<DevMem>;
 
+// Zero device memory and return once the zeros have landed: a private non-blocking stream and
+// hipStreamSynchronize, never the null stream (a rocprofv3 trace showed null-stream fills completing
+// after a later kernel of a non-blocking stream had started, profiles/r4_potrf_rb_race.txt)
+inline hipError_t nat_zero_sync(void* p, size_t bytes) {
+  hipStream_t s = nullptr;
+  hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(p, 0, bytes, s);
+  const hipError_t e2 = hipStreamSynchronize(s);
+  (void)hipStreamDestroy(s);
+  return e != hipSuccess ? e : e2;
+}
+
 inline DevPtr dev_alloc(size_t bytes, bool zero) {
   auto d = std::make_shared<DevMem>();
   if (bytes == 0) bytes = 16;
   if (hipMalloc(&d->p, bytes) != hipSuccess) return nullptr;
-  // (the null-stream memset completes before the context's non-blocking streams may use the buffer)
-  if (zero && (hipMemset(d->p, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess)) return nullptr;
+  if (zero && nat_zero_sync(d->p, bytes) != hipSuccess) return nullptr;
   return d;
 }
 

@@ -148,3 +148,17 @@ static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
     hipError_t e__ = (x);                             \
     if (e__ != hipSuccess) return (int)e__;           \
   } while (0)
+
+// Zero device memory and return only once the zeros have landed, through a private non-blocking
+// stream and hipStreamSynchronize -- not hipMemset on the null stream + hipDeviceSynchronize, which
+// a rocprofv3 trace showed completing after a later kernel on a non-blocking stream had started
+// (profiles/r4_potrf_rb_race.txt).
+static inline hipError_t dpl_zero_sync(void* p, size_t bytes) {
+  hipStream_t s = nullptr;
+  hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(p, 0, bytes, s);
+  const hipError_t e2 = hipStreamSynchronize(s);
+  (void)hipStreamDestroy(s);
+  return e != hipSuccess ? e : e2;
+}

@@ -286,8 +286,7 @@ DPL_API int dpl_xchg_alloc(long long bytes, void** ptr, void* handle) {
     e = hipMalloc(&p, (size_t)bytes);
     if (e != hipSuccess) return (int)e;
   }
-  e = hipMemset(p, 0, (size_t)bytes);
-  if (e == hipSuccess) e = hipDeviceSynchronize();   // (null stream: done before any peer or stream reads it)
+  e = dpl_zero_sync(p, (size_t)bytes);  // landed before any peer or stream reads it
   if (e != hipSuccess) return (int)e;
   hipIpcMemHandle_t h;
   e = hipIpcGetMemHandle(&h, p);

@@ -18,8 +18,16 @@
 //
 // Only 15 hand-offs sit on the critical path (Z_k -> WG k+1), each followed by one 32x32 TRSM,
 // one SYRK and one 32x32 factorisation.  Workgroups only ever wait on workgroups with a SMALLER
-// index, so the schedule cannot deadlock even if the grid is not co-resident (in-order dispatch);
-// every spin is bounded anyway (info = -1000 after ~2 s).
+// LOGICAL index, and the logical index is a ticket taken with one atomic when the workgroup
+// starts (not blockIdx.x): every workgroup a waiter depends on has therefore already started, so
+// forward progress does not rest on the hardware dispatching blockIdx in order across the 8 XCDs
+// or beside other queues' kernels.  Every spin is bounded anyway (info = -1000 after ~2 s).
+//
+// Flag initialisation is stream-ordered: a workspace slot's flags and ticket are zeroed with
+// hipMemsetAsync on the stream that first launches into it.  (Round 3 zeroed them with
+// hipMemset on the null stream + hipDeviceSynchronize; a rocprofv3 trace of the headline bench,
+// gpurun_out/b4_prof, shows six of those fills executing AFTER the first k_potrf_rb had started
+// on a non-blocking stream -- the kernel's first flags were wiped and its waiters timed out.)
 //
 // Data layout ("T-layout"): a 32x32 block is stored as 4 quadrants x 4 registers x 64 lanes;
 // lane l, register r of quadrant q = (rh, ch) holds element
@@ -55,7 +63,17 @@ struct RbWork {
   double* S;    // [MAXB][RB]         S_k
   double* Lp;   // [MAXB][MAXB][BLK]  L(i,k), T-layout
   int* prog;    // [MAXB * PSTRIDE]   epoch * 64 + number of published steps
+  unsigned* ticket;  // workgroup start tickets (monotonic over the slot's launches)
+  unsigned tbase;    // value of *ticket when this launch's first workgroup starts
 };
+
+// logical workgroup id = order of start (one atomic per workgroup); see the header comment
+__device__ inline int wg_ticket(const RbWork& ws) {
+  __shared__ int sid;
+  if (threadIdx.x == 0) sid = (int)(atomicAdd(ws.ticket, 1u) - ws.tbase);
+  __syncthreads();
+  return sid;
+}
 // caller-visible copy of (M, S) for the panel TRSM (dpl_trsm_rb): MAXB * (BLK + RB) doubles
 constexpr int ZBUF = MAXB * (BLK + RB);
 
@@ -331,7 +349,7 @@ template <bool LOWER>
 __global__ __launch_bounds__(256) void k_potrf_rb(double* __restrict__ A, int n, int lda, int* __restrict__ info,
                                                   int info_base, RbWork ws, int epoch,
                                                   unsigned long long* __restrict__ trace) {
-  rb_tile_body<LOWER>(A, n, lda, info, info_base, ws, epoch, trace, blockIdx.x);
+  rb_tile_body<LOWER>(A, n, lda, info, info_base, ws, epoch, trace, wg_ticket(ws));
 }
 
 std::mutex g_mu;
@@ -340,9 +358,12 @@ bool g_have[64] = {};
 unsigned int g_launch = 0;
 hipStream_t g_slot_stream[64][NSLOT] = {};
 bool g_slot_used[64][NSLOT] = {};
+bool g_slot_zeroed[64][NSLOT] = {};    // flags + ticket zeroed on the slot's current stream
 unsigned int g_slot_tick[64][NSLOT] = {};
+unsigned int g_slot_wgs[64][NSLOT] = {};  // tickets handed out so far (= next launch's tbase)
 
-int get_ws(RbWork* out, int* epoch, hipStream_t st) {
+// nwg: workgroups of the launch that will use the workspace (advances the slot's ticket base)
+int get_ws(RbWork* out, int* epoch, hipStream_t st, int nwg) {
   int dev = 0;
   HIP_CHECK_RET(hipGetDevice(&dev));
   if (dev < 0 || dev >= 64) return -4;
@@ -353,18 +374,17 @@ int get_ws(RbWork* out, int* epoch, hipStream_t st) {
       HIP_CHECK_RET(hipMalloc((void**)&w.M, sizeof(double) * MAXB * BLK));
       HIP_CHECK_RET(hipMalloc((void**)&w.S, sizeof(double) * MAXB * RB));
       HIP_CHECK_RET(hipMalloc((void**)&w.Lp, sizeof(double) * MAXB * MAXB * BLK));
-      HIP_CHECK_RET(hipMalloc((void**)&w.prog, sizeof(int) * MAXB * PSTRIDE));
-      HIP_CHECK_RET(hipMemset(w.prog, 0, sizeof(int) * MAXB * PSTRIDE));
+      // flags, then one 128-byte line for the ticket counter
+      HIP_CHECK_RET(hipMalloc((void**)&w.prog, sizeof(int) * (MAXB + 1) * PSTRIDE));
+      w.ticket = (unsigned*)(w.prog + MAXB * PSTRIDE);
+      g_slot_zeroed[dev][s] = false;
     }
-    // null-stream memsets: done before a kernel on a non-blocking stream reads the flags
-    HIP_CHECK_RET(hipDeviceSynchronize());
     g_have[dev] = true;
   }
   ++g_launch;
-  if ((g_launch & 0x1ffffff) == 0) {  // epoch wrap (every 2^25 launches): reset every flag
+  if ((g_launch & 0x1ffffff) == 0) {  // epoch wrap (every 2^25 launches): every slot re-zeroed on its next use
     HIP_CHECK_RET(hipDeviceSynchronize());
-    for (int s = 0; s < NSLOT; ++s) HIP_CHECK_RET(hipMemset(g_ws[dev][s].prog, 0, sizeof(int) * MAXB * PSTRIDE));
-    HIP_CHECK_RET(hipDeviceSynchronize());
+    for (int s = 0; s < NSLOT; ++s) g_slot_zeroed[dev][s] = false;
     ++g_launch;
   }
   // One workspace per stream: launches on one stream are serialised, so they can share it; launches
@@ -382,8 +402,16 @@ int get_ws(RbWork* out, int* epoch, hipStream_t st) {
     g_slot_stream[dev][slot] = st;
     g_slot_used[dev][slot] = true;
   }
+  RbWork& w = g_ws[dev][slot];
+  if (!g_slot_zeroed[dev][slot]) {  // ordered before this launch by the stream itself
+    HIP_CHECK_RET(hipMemsetAsync(w.prog, 0, sizeof(int) * (MAXB + 1) * PSTRIDE, st));
+    g_slot_wgs[dev][slot] = 0;
+    g_slot_zeroed[dev][slot] = true;
+  }
   g_slot_tick[dev][slot] = g_launch;
-  *out = g_ws[dev][slot];
+  w.tbase = g_slot_wgs[dev][slot];
+  g_slot_wgs[dev][slot] += (unsigned)nwg;
+  *out = w;
   *epoch = (int)(g_launch & 0x1ffffff);
   return 0;
 }
@@ -402,15 +430,15 @@ DPL_API int dpl_potrf_tile_rbz(int uplo, int n, double* A, int lda, int* info, i
                                hipStream_t st) {
   if (n <= 0) return 0;
   if (n > RB * MAXB) return -3;
+  const int nblk = cdiv(n, RB);
   RbWork ws;
   int epoch = 0;
-  const int rc = get_ws(&ws, &epoch, st);
+  const int rc = get_ws(&ws, &epoch, st, nblk);
   if (rc) return rc;
   if (zbuf) {
     ws.M = zbuf;
     ws.S = zbuf + MAXB * BLK;
   }
-  const int nblk = cdiv(n, RB);
   if (uplo == DPL_LOWER)
     hipLaunchKernelGGL((k_potrf_rb<true>), dim3(nblk), dim3(256), 0, st, A, n, lda, info, info_base, ws, epoch, g_trace);
   else
@@ -670,12 +698,13 @@ __global__ __launch_bounds__(256) void k_potrf_trsm_rb(double* __restrict__ A, i
                                                        int info_base, RbWork ws, int epoch,
                                                        const RbItem* __restrict__ items, int nrb,
                                                        double* __restrict__ B, int ldb) {
-  if (blockIdx.x < NBLK) {
-    rb_tile_body<LOWER>(A, n, lda, info, info_base, ws, epoch, nullptr, blockIdx.x);
+  const int id = wg_ticket(ws);
+  if (id < NBLK) {
+    rb_tile_body<LOWER>(A, n, lda, info, info_base, ws, epoch, nullptr, id);
     return;
   }
   __builtin_amdgcn_s_setprio(RB_PRIO);
-  const int strip = (blockIdx.x - NBLK) * 4 + (threadIdx.x >> 6);
+  const int strip = (id - NBLK) * 4 + (threadIdx.x >> 6);
   if (strip >= nrb) return;
   rb_strip_dataflow<LOWER, NBLK>(items[strip], n, ws, epoch * 64, info, B, ldb);
 }
@@ -764,16 +793,16 @@ DPL_API int dpl_potrf_trsm_rb(int uplo, int n, double* A, int lda, int* info, in
   if (n <= 0) return 0;
   if (n > RB * MAXB) return -3;
   if (nrb <= 0) return dpl_potrf_tile_rbz(uplo, n, A, lda, info, info_base, zbuf, st);
+  const int nblk = cdiv(n, RB);
+  const dim3 grid(nblk + cdiv(nrb, 4));
   RbWork ws;
   int epoch = 0;
-  const int rc = get_ws(&ws, &epoch, st);
+  const int rc = get_ws(&ws, &epoch, st, (int)grid.x);
   if (rc) return rc;
   if (zbuf) {
     ws.M = zbuf;
     ws.S = zbuf + MAXB * BLK;
   }
-  const int nblk = cdiv(n, RB);
-  const dim3 grid(nblk + cdiv(nrb, 4));
   const RbItem* it = (const RbItem*)items;
 #define POTRF_TRSM_CASE(NB_)                                                                              \
   case NB_:                                                                                               \
