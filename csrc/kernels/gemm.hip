@@ -21,48 +21,7 @@
 //   * blockIdx is remapped XCD-aware so the 16 sub-tiles of a 512x512 tile and
 //     neighbouring tiles of a tile-row share one XCD's L2.
 // Complex precisions run on the matrix cores too (zgemm.hip, four real MFMA products per complex one).
-#include "common.h"
-
-struct KPair {
-  long long a_off, b_off;
-  int k;
-  int pad;
-};
-struct GemmItemK {
-  long long c_off;
-  int kt_beg, kt_cnt;  // run of KPair records
-  int m, n;
-  int flags;           // bits 0-1: C write mask (0 full, 1 lower, 2 upper)
-  int pad;
-};
-
-typedef double d2v __attribute__((ext_vector_type(2)));
-typedef float f4v __attribute__((ext_vector_type(4)));
-
-template <typename T> struct MF;
-template <> struct MF<double> {
-  typedef d4_t acc_t;
-  typedef d2v vec_t;
-  static constexpr int VEC = 2;
-  static __device__ inline acc_t mma(double a, double b, acc_t c) {
-    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-  }
-  // row (within a 16x16 block, along the D "row" axis) held by lane l, register r
-  static __device__ inline int drow(int l, int r) { return (l >> 4) + 4 * r; }
-};
-template <> struct MF<float> {
-  typedef f4_t acc_t;
-  typedef f4v vec_t;
-  static constexpr int VEC = 4;
-  static __device__ inline acc_t mma(float a, float b, acc_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-  }
-  static __device__ inline int drow(int l, int r) { return (l >> 4) * 4 + r; }
-};
-
-#define GBM 128
-#define GBN 128
-#define GBK 16
+#include "gemm_tile.h"
 
 // LDS image of one operand block: [GBK][row-stride] per buffer.
 //  f64: no padding, column index XOR-swizzled by ((kk >> 1) & 7) << 2.  Fragment reads (16
@@ -317,280 +276,24 @@ __global__ __launch_bounds__(256, 2) void k_gemm_mfma(const GemmItemK* __restric
 }
 
 // ------------------------------------------------------------------ full-tile fast path
-// Used when every item of the launch is a whole number of 128x128 sub-tiles and every k-run a
-// multiple of GBK (e.g. all NB=512 Cholesky / SUMMA updates).  Differences from k_gemm_mfma:
-//  * no bounds logic anywhere in the k-loop;
-//  * operands are fetched with buffer loads: the per-thread byte offset is loop-invariant (VGPR),
-//    the k-advance is a scalar soffset and the k-tile base lives in the SGPR resource, so the
-//    loop carries no 64-bit VALU address arithmetic;
-//  * alpha is applied once in the epilogue (acc starts at (beta/alpha) C), not per staged block;
-//  * k-contiguous operands (A^T / B untransposed) are fetched with 16 consecutive lanes on 16
-//    different rows/columns so their transposed LDS stores hit 16 distinct bank slots; all LDS
-//    images use the padded stride 144 (fragment reads of rows kr / kr+1 in opposite bank halves).
-#define FLS 144
-
-__device__ inline __amdgpu_buffer_rsrc_t mk_rsrc(const void* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
-}
-
-template <typename T> struct BufLd;
-template <> struct BufLd<double> {
-  typedef d2v vec_t;
-  static __device__ inline vec_t ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-    return __builtin_bit_cast(vec_t, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
-  }
-};
-template <> struct BufLd<float> {
-  typedef f4v vec_t;
-  static __device__ inline vec_t ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-    return __builtin_bit_cast(vec_t, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
-  }
-};
-
+// (the sub-tile body lives in gemm_tile.h, shared with the device task runtime)
 template <typename T, bool TA, bool TB>
 __device__ __forceinline__ void gemm_full_tile(const int wg, const GemmItemK* __restrict__ items,
                                                const KPair* __restrict__ kps, int nsm, int nsn, T alpha,
                                                const T* __restrict__ A, int lda, const T* __restrict__ B,
                                                int ldb, T beta, T* __restrict__ C, int ldc) {
-  typedef MF<T> M_;
-  typedef typename M_::acc_t acc_t;
-  typedef typename M_::vec_t vec_t;
-  constexpr int VEC = M_::VEC;
-  constexpr int NLD = (GBM * GBK) / (VEC * 256);
-  constexpr int KG = GBK / VEC;      // 16-byte k-groups per row of a k-contiguous operand
-  constexpr int OPB_ = GBK * FLS;
-  __shared__ T sm[2 * 2 * OPB_];     // [buf][operand][GBK x FLS]
-
+  __shared__ T sm[gemm_lds_elems<T>()];
   const int per = nsm * nsn;
   const GemmItemK it = items[wg / per];
   const int sub = wg % per;
   const int m0 = (sub % nsm) * GBM, n0 = (sub / nsm) * GBN;
-  const int Mt = it.m, Nt = it.n;
-  if (m0 >= Mt || n0 >= Nt) return;
+  if (m0 >= it.m || n0 >= it.n) return;
   const int uplo = it.flags & 3;
   if (uplo == 1 && n0 >= m0 + GBM) return;
   if (uplo == 2 && m0 >= n0 + GBN) return;
-
-  T* Cb = C + it.c_off;
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-  const int wm = w & 1, wn = w >> 1;
-
-  int nsteps = 0;
-  for (int t = 0; t < it.kt_cnt; ++t) nsteps += kps[it.kt_beg + t].k / GBK;
-
-  // ---- loop-invariant per-thread fetch offset (bytes) and LDS destination of the q=0 vector;
-  // the q-th vector (thread c + 256q) is a fixed stride away: scalar for the fetch, immediate in LDS
-  int voa, vob, lda0, ldb0;
-  {
-    const int c = tid;
-    if (!TA) {  // op(A)(i, k) = A[i + k*lda]: 16-byte vectors along i
-      const int kk = c / (GBM / VEC), i = (c % (GBM / VEC)) * VEC;
-      voa = (i + kk * lda) * (int)sizeof(T);
-      lda0 = kk * FLS + i;
-    } else {    // op(A)(i, k) = A[k + i*lda]: 16 consecutive lanes on 16 different i
-      const int i = (c & 15) | ((c / (16 * KG)) << 4), kk = ((c >> 4) % KG) * VEC;
-      voa = (kk + i * lda) * (int)sizeof(T);
-      lda0 = kk * FLS + i;
-    }
-    if (TB) {   // op(B)(k, j) = B[j + k*ldb]
-      const int kk = c / (GBN / VEC), j = (c % (GBN / VEC)) * VEC;
-      vob = (j + kk * ldb) * (int)sizeof(T);
-      ldb0 = kk * FLS + j;
-    } else {    // op(B)(k, j) = B[k + j*ldb]
-      const int j = (c & 15) | ((c / (16 * KG)) << 4), kk = ((c >> 4) % KG) * VEC;
-      vob = (kk + j * ldb) * (int)sizeof(T);
-      ldb0 = kk * FLS + j;
-    }
-  }
-  constexpr int LQA = TA ? 16 * VEC : 2 * VEC * FLS;   // LDS stride between q and q+1
-  constexpr int LQB = TB ? 2 * VEC * FLS : 16 * VEC;
-  const int GQA = (TA ? 16 * VEC : 2 * VEC) * lda * (int)sizeof(T);  // fetch stride (bytes)
-  const int GQB = (TB ? 2 * VEC : 16 * VEC) * ldb * (int)sizeof(T);
-  // scalar k-position of the next fetch
-  int ld_kt = it.kt_beg, ld_k0 = 0, ld_K = 0;
-  __amdgpu_buffer_rsrc_t ra_rs = mk_rsrc(A), rb_rs = mk_rsrc(B);
-  auto set_kt = [&]() {
-    const KPair kp = kps[ld_kt];
-    ld_K = kp.k;
-    ra_rs = mk_rsrc(A + kp.a_off + (TA ? (long long)m0 * lda : (long long)m0));
-    rb_rs = mk_rsrc(B + kp.b_off + (TB ? (long long)n0 : (long long)n0 * ldb));
-  };
-  if (nsteps > 0) set_kt();
-  vec_t ra[NLD], rb[NLD];
-  // fetch(): issue the block at the current position; advance(): step it (scalar), clamped at
-  // the last block so the loop can fetch unconditionally (surplus fetches are never stored)
-  auto fetch = [&]() {
-    const int sa = (TA ? ld_k0 : ld_k0 * lda) * (int)sizeof(T);
-    const int sb = (TB ? ld_k0 * ldb : ld_k0) * (int)sizeof(T);
-#pragma unroll
-    for (int q = 0; q < NLD; ++q) {
-      ra[q] = BufLd<T>::ld(ra_rs, voa, sa + q * GQA);
-      rb[q] = BufLd<T>::ld(rb_rs, vob, sb + q * GQB);
-    }
-  };
-  auto advance = [&]() {
-    if (ld_k0 + GBK < ld_K) {
-      ld_k0 += GBK;
-    } else if (ld_kt + 1 < it.kt_beg + it.kt_cnt) {
-      ++ld_kt;
-      ld_k0 = 0;
-      set_kt();
-    }
-  };
-  auto load = [&]() {
-    fetch();
-    advance();
-  };
-  auto store = [&](int buf) {
-    T* sa = sm + (2 * buf) * OPB_;
-    T* sb = sa + OPB_;
-#pragma unroll
-    for (int q = 0; q < NLD; ++q) {
-      if (!TA) {
-        *(vec_t*)&sa[lda0 + q * LQA] = ra[q];
-      } else {
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) sa[lda0 + q * LQA + e * FLS] = ra[q][e];
-      }
-      if (TB) {
-        *(vec_t*)&sb[ldb0 + q * LQB] = rb[q];
-      } else {
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) sb[ldb0 + q * LQB + e * FLS] = rb[q][e];
-      }
-    }
-  };
-  auto frag = [&](int buf, int kq, T* a, T* b) {
-    const T* sa = sm + (2 * buf) * OPB_;
-    const T* sb = sa + OPB_;
-    const int kr = kq * 4 + (l >> 4);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = sa[kr * FLS + wm * 64 + i * 16 + (l & 15)];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = sb[kr * FLS + wn * 64 + j * 16 + (l & 15)];
-  };
-
-  if (nsteps > 0) load();
-  // ---- C prologue: acc = (beta/alpha) C, finished by one multiply with alpha in the epilogue
-  const int mrow = m0 + wm * 64 + (l & 15);
-  const int ncol = n0 + wn * 64;
-  T* cp = Cb + mrow + (long long)ncol * ldc;
-  acc_t acc[4][4];
-  if (beta == T(0)) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = T(0);
-  } else {
-    const T bs = beta / alpha;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = cp[i * 16 + (long long)(j * 16 + M_::drow(l, r)) * ldc];
-    // consume the C values here so the waitcnt pass drains them before the loop (vmcnt is a counter)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] *= bs;
-  }
-  if (nsteps > 0) store(0);
-  if (nsteps > 1) load();
-  // One basic block per k-step: barrier, then the step's 64 MFMAs/wave with the LDS writes of
-  // block s+1, the buffer fetches of block s+2 and the fragment reads of quads 1..3 interleaved
-  // one memory instruction per MFMA (sched_group_barrier), then the scalar advance.
-  constexpr int NW = (TA ? NLD * VEC : NLD) + (TB ? NLD : NLD * VEC);  // LDS stores per step
-  for (int s = 0; s < nsteps; ++s) {
-    const int cur = s & 1;
-    __syncthreads();
-    T a[3][4], b[3][4];
-    frag(cur, 0, a[0], b[0]);
-    store(cur ^ 1);
-    frag(cur, 1, a[1], b[1]);
-    fetch();
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = M_::mma(b[0][j], a[0][i], acc[i][j]);
-    frag(cur, 2, a[2], b[2]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = M_::mma(b[1][j], a[1][i], acc[i][j]);
-    frag(cur, 3, a[0], b[0]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = M_::mma(b[2][j], a[2][i], acc[i][j]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = M_::mma(b[0][j], a[0][i], acc[i][j]);
-    // schedule: [quad-0 reads] then MFMA-paced: NW stores, 4 reads (q1), 2*NLD fetches,
-    // pad to 24, 4 reads (q2), pad to 40, 4 reads (q3), rest
-    constexpr int M1 = NW + 4 + 2 * NLD;            // MFMAs paced by stores / q1 reads / fetches
-    constexpr int P1 = M1 < 24 ? 24 - M1 : 0;
-    constexpr int M2 = M1 + P1 + 4;
-    constexpr int P2 = M2 < 40 ? 40 - M2 : 0;
-    constexpr int M3 = M2 + P2 + 4;
-    static_assert(M3 < 64, "schedule overflows the step's MFMAs");
-    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-#pragma unroll
-    for (int v = 0; v < 2 * NLD; ++v) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-    }
-    if (P1 > 0) __builtin_amdgcn_sched_group_barrier(0x008, P1, 0);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-    if (P2 > 0) __builtin_amdgcn_sched_group_barrier(0x008, P2, 0);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x008, 64 - M3, 0);
-    advance();
-  }
-
-  const bool diag = (uplo == 1 && n0 + GBN > m0) || (uplo == 2 && m0 + GBM > n0);
-  if (!diag) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) cp[i * 16 + (long long)(j * 16 + M_::drow(l, r)) * ldc] = alpha * acc[i][j][r];
-  } else {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int mm = mrow + i * 16, nn = ncol + j * 16 + M_::drow(l, r);
-          const bool ok = (uplo == 1) ? (mm >= nn) : (mm <= nn);
-          if (ok) Cb[mm + (long long)nn * ldc] = alpha * acc[i][j][r];
-        }
-  }
+  const KPair* kp = kps + it.kt_beg;
+  gemm_subtile<T, TA, TB>(sm, [kp](int t) { return kp[t]; }, it.kt_cnt, m0, n0, uplo, alpha, A, lda, B, ldb, beta,
+                          C + it.c_off, ldc);
 }
 
 // One 128x128 output sub-tile per workgroup (PERSIST = false: grid = every sub-tile), or a capped

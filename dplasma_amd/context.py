@@ -81,6 +81,10 @@ class Context:
         else:
             self.streams = {}
         self._groups_built = False
+        # loopback rehearsal (parallel.comm.loopback): a world-1 group whose algorithms route their
+        # would-be remote tile edges through RCCL sends / receives to the rank itself
+        from .parallel import comm as _comm
+        self.loopback = _comm.loopback()
         self.row_group = None
         self.col_group = None
         self.urgent_group = None
@@ -207,7 +211,7 @@ class Context:
 
     # ------------------------------------------------------------------ comms
     def _build_groups(self):
-        if not self.distributed or self.world == 1:
+        if not self.distributed or (self.world == 1 and not self.loopback):
             return
         # every rank must create every group, in the same order.  On RCCL the panel traffic
         # (broadcasts / all-gathers of the factorisations' critical path) runs on high-priority
@@ -224,10 +228,10 @@ class Context:
         rows, cols = [], []
         for r in range(self.P):
             ranks = [r * self.Q + c for c in range(self.Q)]
-            rows.append(dist.new_group(ranks, **kw) if self.Q > 1 else None)
+            rows.append(dist.new_group(ranks, **kw) if self.Q > 1 or self.loopback else None)
         for c in range(self.Q):
             ranks = [r * self.Q + c for r in range(self.P)]
-            cols.append(dist.new_group(ranks, **kw) if self.P > 1 else None)
+            cols.append(dist.new_group(ranks, **kw) if self.P > 1 or self.loopback else None)
         self.row_group = rows[self.myrow]
         self.col_group = cols[self.mycol]
         # world-wide communicators of the dataflow tile transport (parallel.comm.start_p2p): one for
@@ -266,6 +270,7 @@ class Context:
         c = object.__new__(Context)
         c.__dict__.update(self.__dict__)
         c.distributed, c.rank, c.world = False, 0, 1
+        c.loopback = False
         c.P, c.Q, c.myrow, c.mycol = 1, 1, 0, 0
         c.row_group = c.col_group = None
         c.urgent_group, c.bulk_groups = None, []

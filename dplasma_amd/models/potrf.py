@@ -94,7 +94,7 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                            or ctx.info.get_int("DPLASMA:GPU:number_of_blocks", 0) > 0):
         from .potrf_ooc import potrf_ooc_New
         return potrf_ooc_New(ctx, uplo, A)
-    if ctx.world > 1 and os.environ.get("DPLASMA_POTRF_DIST", "p2p") != "collective":
+    if (ctx.world > 1 or getattr(ctx, "loopback", False)) and os.environ.get("DPLASMA_POTRF_DIST", "p2p") != "collective":
         # distributed: point-to-point dataflow panel transport (models/potrf_dist.py);
         # DPLASMA_POTRF_DIST=collective keeps the row-broadcast + column-all-gather schedule below
         from .potrf_dist import potrf_dist_New

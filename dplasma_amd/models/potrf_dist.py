@@ -138,11 +138,17 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     SG, SX = maxcnt * nbe, nlines * maxsub * nbe
     slab = SG + SX
     GX = torch.zeros(nslab * D * slab, dtype=A.dtype, device=dev)
+    # loopback rehearsal (parallel.comm.loopback, world 1): the root packs its piece into LB and sends
+    # it to itself into G, and the diagonal triangle goes to itself too -- the exchanges a real grid
+    # has, through the same RCCL calls, with the receive-side paths (DRECV unpack, PREP) taken
+    loop = bool(getattr(ctx, "loopback", False))
+    me = ctx.rank
+    LB = torch.zeros(nslab * D * SG if loop else 1, dtype=A.dtype, device=dev)
     ntri = A.mb * (A.mb + 1) // 2
     dsend = torch.zeros(2 * ntri, dtype=A.dtype, device=dev)
     drecv = torch.zeros(2 * ntri, dtype=A.dtype, device=dev)
     dbuf = torch.zeros(2 * nbe, dtype=A.dtype, device=dev)
-    tp._buffers = (GX, dsend, drecv, dbuf)
+    tp._buffers = (GX, dsend, drecv, dbuf, LB)
 
     use_rb = ops.rb_ok(A.data, A.mb) and A.mb == A.nb
     # panel TRSM: "rb" (register-resident strips, k_trsm_rb) or "gemm" (the batched TRSM engine: blocked
@@ -221,6 +227,7 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                 t_potrf = tp.task(f"POTRF({k})", s_tile, f_potrf, [gate], prio=3, comm=False)
             # ---------------- diagonal triangle to the other roots of the panel column
             tri_src = None
+            t_dsend = None
             if in_pc and mine and not own_diag:
                 src = rank_lc(diag_line, pc)
                 par2 = k % 2
@@ -234,16 +241,26 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                 tri_src = (t_dr, par2)
             if own_diag:
                 dests = [rank_lc(l, pc) for l in range(nlines) if l != my_line and per[l]]
-                if dests:
+                self_rx = loop and bool(mine)
+                if dests or self_rx:
                     par2 = k % 2
 
-                    def f_dsend(dests=dests, par2=par2, off=A.offset(*dk), kb=kb):
+                    def f_dsend(dests=dests, par2=par2, off=A.offset(*dk), kb=kb, k=k, self_rx=self_rx):
                         comm.finish(dsend_pend.get(par2))
                         buf = dsend[par2 * ntri:(par2 + 1) * ntri]
                         buf[: kb * (kb + 1) // 2].copy_(A.data.view(-1)[off + comm._tri_index(kb, A.ld, lower, dev)])
-                        h = comm.start_p2p(sends=[(buf, d) for d in dests], group=urgent_g)
+                        if self_rx:   # loopback: the triangle to myself, received like a remote root's
+                            h = comm.start_p2p(sends=[(buf, me)], recvs=[(drecv[par2 * ntri:(par2 + 1) * ntri], me)],
+                                               group=urgent_g)
+                            pend.setdefault(k, {})["d"] = h
+                        else:
+                            h = comm.start_p2p(sends=[(buf, d) for d in dests], group=urgent_g)
                         dsend_pend[par2] = h
-                    tp.task(f"DSEND({k})", s_tile, f_dsend, [t_potrf], prio=3)
+                    # (loopback: the receive buffer pair alternates as for DRECV)
+                    t_dsend = tp.task(f"DSEND({k})", s_tile, f_dsend,
+                                      [t_potrf] + ([last_trsm.get(k - 2)] if self_rx and k >= 2 else []), prio=3)
+                    if self_rx:
+                        tri_src = (t_dsend, par2)
             # ---------------- TRSM of my tiles of panel k
             t_trsm = None
             if mine:
@@ -326,6 +343,10 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                         kind = "u" if c_ in ucross else "b"
                         sends[kind].append((G + js[0] * nbe, len(js), rank_lc(l, c_)))
             kind_me = "u" if me_urgent else "b"
+            if loop and mine:
+                # loopback: packed into LB, sent to myself into G (same batch: one group call)
+                sends[kind_me].append((-1 - slot * SG, len(mine), me))
+                recvs[kind_me].append((G, len(mine), me))
             if not in_pc and per[my_line]:
                 recvs[kind_me].append((G, len(per[my_line]), rank_lc(my_line, pc)))
             for l in range(nlines):
@@ -337,9 +358,10 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
             pack = None
             if mine:
                 pb = TileBatch()
+                pk0 = slot * SG if loop else G
                 for j, i in enumerate(mine):
                     cc = tcoord(i, k)
-                    pb.add(A.offset(*cc), A.tile_rows(cc[0]), A.tile_cols(cc[1]), b_off=G + j * nbe)
+                    pb.add(A.offset(*cc), A.tile_rows(cc[0]), A.tile_cols(cc[1]), b_off=pk0 + j * nbe)
                 pack = pb.finalize()
             bg = bulk_gs[k % len(bulk_gs)]
             hint_row = ("trsm", len(per[my_line]), kb)
@@ -348,10 +370,11 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                 for h in send_pend.pop(slot, []):   # the slab's previous sends have read it
                     comm.finish(h)
                 if pack is not None:
-                    ops.geadd(0, dplasmaNoTrans, 1.0, A.data, A.ld, 0.0, GX, A.mb, pack, copy=True)
+                    ops.geadd(0, dplasmaNoTrans, 1.0, A.data, A.ld, 0.0, LB if loop else GX, A.mb, pack, copy=True)
                 hs = {}
                 for kind, grp in (("u", urgent_g), ("b", bg)):
-                    s_ = [(GX[a: a + n * nbe], r) for a, n, r in sends[kind]]
+                    # a < 0: offset -1 - a in the loopback slab LB
+                    s_ = [((LB[-1 - a: -1 - a + n * nbe] if a < 0 else GX[a: a + n * nbe]), r) for a, n, r in sends[kind]]
                     r_ = [(GX[a: a + n * nbe], r) for a, n, r in recvs[kind]]
                     if s_ or r_:
                         h = comm.start_p2p(s_, r_, group=grp, hint=hint_row)

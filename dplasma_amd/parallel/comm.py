@@ -12,9 +12,22 @@ Patterns used by the algorithms (SURVEY.md §2.10 collective inventory):
                     algorithm per message size);
 * ``allgather``  -- panel pieces across a process column (in place);
 * ``allreduce``  -- info / norm reductions.
+
+Loopback rehearsal (``DPLASMA_LOOPBACK=1`` on a world-1 process group): the algorithms plan
+their exchanges as if the rank's own tiles lived on another rank -- every tile edge that would
+cross ranks on a real grid (and, for tile DAGs / tile programs, every operand edge) becomes a
+send to and a receive from the rank itself.  On RCCL those are real ``ncclSend`` / ``ncclRecv``
+pairs in one group (NCCL supports self-sends; only torch's Python front end refuses them,
+``_check_not_self_rank``, which :func:`self_p2p` lifts for the duration of the call), so every
+RCCL branch of the transport (grouped p2p batches, the urgent / bulk communicators, the
+dataflow ``Transport`` of tile DAGs, all-to-all exchanges) executes on a one-GPU box with
+results that must equal the exchange-free path.  gloo cannot connect a rank to itself: there
+the self pairs are completed by a local copy (the CPU tests check the planning).
 """
 from __future__ import annotations
 
+import contextlib
+import os
 from typing import Optional
 
 import torch
@@ -23,6 +36,39 @@ import torch.distributed as dist
 
 def _nbytes(t: torch.Tensor) -> int:
     return t.numel() * t.element_size()
+
+
+def loopback() -> bool:
+    """True when the loopback rehearsal is on: DPLASMA_LOOPBACK=1 and a world-1 process group."""
+    return (os.environ.get("DPLASMA_LOOPBACK", "0") == "1" and dist.is_available() and dist.is_initialized()
+            and dist.get_world_size() == 1)
+
+
+@contextlib.contextmanager
+def self_p2p():
+    """Let torch.distributed post sends / receives whose peer is this rank (loopback only)."""
+    if not loopback():
+        yield
+        return
+    import torch.distributed.distributed_c10d as c10d
+    orig = c10d._check_not_self_rank
+    c10d._check_not_self_rank = lambda *a, **k: None
+    try:
+        yield
+    finally:
+        c10d._check_not_self_rank = orig
+
+
+def _split_self(sends, recvs):
+    """gloo loopback: complete the self pairs (in order) with local copies; returns the rest."""
+    me = dist.get_rank() if dist.is_initialized() else 0
+    ss = [t for t, p in sends if p == me]
+    rs = [t for t, p in recvs if p == me]
+    if len(ss) != len(rs):
+        raise RuntimeError(f"loopback: {len(ss)} self-sends but {len(rs)} self-receives in one batch")
+    for a, b in zip(ss, rs):
+        b.copy_(a.view(-1)[: b.numel()].view_as(b))
+    return [(t, p) for t, p in sends if p != me], [(t, p) for t, p in recvs if p != me]
 
 
 def bcast(t: torch.Tensor, src_global: int, group, world: bool = False) -> None:
@@ -83,9 +129,12 @@ def p2p(sends=(), recvs=()) -> None:
         return _BACKEND.sync("p2p", max(per.values()), None)
     if _nccl():
         ops = [dist.P2POp(dist.isend, t, p) for t, p in sends] + [dist.P2POp(dist.irecv, t, p) for t, p in recvs]
-        for w in dist.batch_isend_irecv(ops) or ():
-            w.wait()
+        with self_p2p():
+            for w in dist.batch_isend_irecv(ops) or ():
+                w.wait()
         return
+    if loopback():
+        sends, recvs = _split_self(sends, recvs)
     host_r = [(t, t.cpu() if t.device.type != "cpu" else t) for t, _ in recvs]
     works = [dist.isend(t.cpu() if t.device.type != "cpu" else t, p) for t, p in sends]
     works += [dist.irecv(h, p) for (_, h), (_, p) in zip(host_r, recvs)]
@@ -134,7 +183,10 @@ def start_p2p(sends=(), recvs=(), group=None, hint=None) -> Optional[Pending]:
     if _nccl() and any(t.device.type == "cuda" for t, _ in sends + recvs):
         ops = [dist.P2POp(dist.isend, t, p, group=group) for t, p in sends]
         ops += [dist.P2POp(dist.irecv, t, p, group=group) for t, p in recvs]
-        return Pending(dist.batch_isend_irecv(ops) or (), device=True)
+        with self_p2p():
+            return Pending(dist.batch_isend_irecv(ops) or (), device=True)
+    if loopback():
+        sends, recvs = _split_self(sends, recvs)
     host_s = [(t.cpu() if t.device.type != "cpu" else t, p) for t, p in sends]
     host_r = [(t, t.cpu() if t.device.type != "cpu" else t, p) for t, p in recvs]
     works = [dist.isend(h, p, group=group) for h, p in host_s]

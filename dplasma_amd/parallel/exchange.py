@@ -42,22 +42,25 @@ class ExchangePlan:
         self.nbe = nbe = mb * nb
         self.ld = mb
         mine = needs.get(me, [])
+        # loopback rehearsal (parallel.comm.loopback): my own tiles go through the all-to-all as well
+        self.loop = loop = bool(getattr(ctx, "loopback", False))
         by_src: List[List[TileKey]] = [[] for _ in range(world)]
         for key in mine:
             mid, m, n = key
             by_src[mats[mid].rank_of(m, n)].append(key)
-        self.recv_counts = [len(x) if s != me else 0 for s, x in enumerate(by_src)]
+        self.recv_counts = [len(x) if (s != me or loop) else 0 for s, x in enumerate(by_src)]
         self.slot: Dict[TileKey, int] = {}
         pos = 0
-        for s in [x for x in range(world) if x != me] + [me]:
+        order = list(range(world)) if loop else [x for x in range(world) if x != me] + [me]
+        for s in order:
             for key in by_src[s]:
                 self.slot[key] = pos * nbe
                 pos += 1
         self.nrecv = pos
-        self.nremote = pos - len(by_src[me])
+        self.nremote = pos if loop else pos - len(by_src[me])
         # my own tiles: matrix -> receive slot, one batch per source matrix
         self.local: Dict[int, TileBatch] = {}
-        for (mid, m, n) in by_src[me]:
+        for (mid, m, n) in ([] if loop else by_src[me]):
             M = mats[mid]
             self.local.setdefault(mid, TileBatch()).add(M.offset(m, n), M.tile_rows(m), M.tile_cols(n),
                                                         b_off=self.slot[(mid, m, n)])
@@ -66,7 +69,8 @@ class ExchangePlan:
         # send layout: by destination rank (never myself), in the destination's need order
         send_lists: List[List[TileKey]] = []
         for d in range(world):
-            lst = [] if d == me else [key for key in needs.get(d, []) if mats[key[0]].rank_of(key[1], key[2]) == me]
+            lst = [] if (d == me and not loop) else \
+                [key for key in needs.get(d, []) if mats[key[0]].rank_of(key[1], key[2]) == me]
             send_lists.append(lst)
         self.send_counts = [len(x) for x in send_lists]
         self.nsend = sum(self.send_counts)
@@ -98,7 +102,7 @@ class ExchangePlan:
         for mid, tb in self.local.items():
             M = self.mats[mid]
             ops.geadd(0, dplasmaNoTrans, 1.0, M.data, M.ld, 0.0, recv, self.ld, tb, copy=True)
-        if self.ctx.world == 1:
+        if self.ctx.world == 1 and not self.loop:
             return
         if sendbuf is None or sendbuf.numel() < self.nsend * nbe:
             sendbuf = self.new_send_buffer()

@@ -41,6 +41,7 @@ import torch.distributed as dist
 from ..constants import dplasmaNoTrans
 from ..ops.batch import TileBatch
 from ..utils import trace
+from . import comm
 
 # tile reference on this rank: (base index, element offset, ld, rows, cols, staging ld)
 TileRef = Tuple[int, int, int, int, int, int]
@@ -267,8 +268,9 @@ class Transport:
                     pe.record(cs)
                     self._packed[x.xid] = pe
                     rt = x.recv_target(self._bases, rb)
-                    for w in dist.batch_isend_irecv(x.p2p_ops(sb, rt)) or ():
-                        w.wait()
+                    with comm.self_p2p():
+                        for w in dist.batch_isend_irecv(x.p2p_ops(sb, rt)) or ():
+                            w.wait()
                     x.do_unpack(rt, self._bases)
                     de = torch.cuda.Event()
                     de.record(cs)
@@ -290,8 +292,14 @@ class Transport:
             rb = torch.empty(max(1, x.nrecv * x.nbe), dtype=x.dtype)
             if x.recv_into is not None and dev.type == "cpu":
                 rb = x.recv_target(self._bases, rb)   # receive in place
+            p2p = x.p2p_ops(sb, rb)
+            if comm.loopback():   # gloo cannot reach the rank itself: self pairs become local copies
+                comm._split_self([(o.tensor, o.peer) for o in p2p if o.op is dist.isend],
+                                 [(o.tensor, o.peer) for o in p2p if o.op is dist.irecv])
+                me = dist.get_rank()
+                p2p = [o for o in p2p if o.peer != me]
             works = [dist.isend(op.tensor, op.peer, tag=x.xid) if op.op is dist.isend
-                     else dist.irecv(op.tensor, op.peer, tag=x.xid) for op in x.p2p_ops(sb, rb)]
+                     else dist.irecv(op.tensor, op.peer, tag=x.xid) for op in p2p]
         self._inflight.append((x, works, (sb, rb)))
         self._count(x)
 

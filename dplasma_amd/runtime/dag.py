@@ -328,6 +328,11 @@ class TileDAG:
     def compile(self) -> Taskpool:
         ctx = self.ctx
         me, world = ctx.rank, ctx.world
+        # loopback rehearsal (parallel.comm.loopback, one rank): every tile access is planned as a remote
+        # one -- operands fetched from their home (myself) into the slot arena, written tiles written
+        # back -- so the dataflow transport's RCCL path runs with self as the peer
+        loop = bool(getattr(ctx, "loopback", False))
+        dist_plan = world > 1 or loop
         if PTG_TO_DTD[0] and not self.no_dtd and self._chunks:
             tp = self._ptg_to_dtd()
             if tp is not None:
@@ -369,7 +374,7 @@ class TileDAG:
         tp.simulation_date = lambda cost=None: simulation_date(ops, modes, kid, names, cost)
         rt = _lib_rt()
         # single process on a GPU: dataflow over two streams (critical path / bulk)
-        multistream = world == 1 and ctx.device.type == "cuda" and rt is not None and MULTISTREAM
+        multistream = world == 1 and not loop and ctx.device.type == "cuda" and rt is not None and MULTISTREAM
         crit = None
         if multistream:
             level, blevel, esrc, edst = rt.dag_schedule(ops, modes)
@@ -395,7 +400,7 @@ class TileDAG:
         # remote executor that produced it), and write-backs of remotely written tiles to their home
         xrows = None
         slot_of: Dict[int, int] = {}
-        if world > 1:
+        if dist_plan:
             used = modes > 0
             t_idx, r_idx = np.nonzero(used)
             akeys = ops[t_idx, r_idx]
@@ -403,7 +408,7 @@ class TileDAG:
             aexe = exe[t_idx]
             alev = level[t_idx].astype(np.int64)
             awr = (modes[t_idx, r_idx] & 2) > 0
-            rem = home != aexe
+            rem = (home != aexe) | loop
             self._local_access = (akeys[aexe == me], alev[aexe == me], awr[aexe == me])
             if rem.any():
                 ver = rt.dag_versions(ops, modes) if rt is not None else _versions_py(ops, modes)
@@ -444,7 +449,9 @@ class TileDAG:
                     src[sel] = we[ow][pos]
                 point = np.maximum(prod_l, prev_l[fi])
                 dst = e_r[fi]
-                direct = src != dst   # the producer itself is the executor: its slot already holds it
+                # the producer itself is the executor: its slot already holds it (an initial fetch from
+                # home always moves: on a real grid home != executor; loopback fetches from itself)
+                direct = (src != dst) | (prod_l < 0)
                 f_rows = np.stack([src, dst, fk, fl, point, np.zeros(len(fi), np.int64)], 1)[direct]
                 wi = np.nonzero(w_r)[0]
                 w_rows = np.stack([e_r[wi], h_r[wi], k_r[wi], l_r[wi], l_r[wi], np.ones(len(wi), np.int64)], 1)
@@ -475,14 +482,20 @@ class TileDAG:
         mat_dt = [M.dtype for M in self.mats]
         dtype = self.mats[0].dtype
 
-        def resolve(keys):
-            """keys (n,) -> (base index, element offset, ld) arrays for this rank."""
+        def resolve(keys, home=False):
+            """keys (n,) -> (base index, element offset, ld) arrays for this rank (home: the tiles' own
+            storage -- the loopback transport's home side)."""
             keys = np.asarray(keys, dtype=np.int64)
             mid = (keys >> _MID_SHIFT).astype(np.int64)
             bidx = mid.copy()
             off = np.zeros(len(keys), dtype=np.int64)
             ld = np.zeros(len(keys), dtype=np.int32)
-            loc = (self._home(keys) == me) if world > 1 else np.ones(len(keys), dtype=bool)
+            if home:
+                loc = np.ones(len(keys), dtype=bool)
+            elif loop:
+                loc = np.zeros(len(keys), dtype=bool)   # every operand in the slot arena
+            else:
+                loc = (self._home(keys) == me) if world > 1 else np.ones(len(keys), dtype=bool)
             if loc.any():
                 off[loc] = self._local_offsets(keys[loc])
                 ld[loc] = np.array([self.mats[i].ld for i in range(len(self.mats))], dtype=np.int32)[mid[loc]]
@@ -596,8 +609,8 @@ class TileDAG:
             lk, ll, lw = self._local_access
             wk_me, wl_me = lk[lw], ll[lw]
 
-            def tref(keys):
-                b, o, l = resolve(np.asarray(keys, dtype=np.int64))
+            def tref(keys, home=False):
+                b, o, l = resolve(np.asarray(keys, dtype=np.int64), home)
                 out = []
                 for i, k in enumerate(keys):
                     M = self.mats[int(k) >> _MID_SHIFT]
@@ -631,11 +644,12 @@ class TileDAG:
                 point = int(gkey[a, 0])
                 wb = gkey[a, 1] == 0
                 sends, recvs = defaultdict(list), defaultdict(list)
+                # loopback: a fetch is sent from the home storage, a write-back received into it
                 if len(sm):
-                    for (dst_r, k), ref in zip(sm[:, [1, 2]].tolist(), tref(sm[:, 2])):
+                    for (dst_r, k), ref in zip(sm[:, [1, 2]].tolist(), tref(sm[:, 2], loop and not wb)):
                         sends[dst_r].append(ref)
                 if len(rm):
-                    for (src_r, k), ref in zip(rm[:, [0, 2]].tolist(), tref(rm[:, 2])):
+                    for (src_r, k), ref in zip(rm[:, [0, 2]].tolist(), tref(rm[:, 2], loop and wb)):
                         recvs[src_r].append(ref)
                 x = Xfer(xid, dt, nbe_of[dt], sends, recvs, label=f"{'w' if wb else 'f'}@{point}")
                 need = None

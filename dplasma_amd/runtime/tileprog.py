@@ -138,7 +138,9 @@ class TileProgram:
         me = ctx.rank
         tp = Taskpool(self.name, ctx)
         tp.flops = self.flops
-        distributed = ctx.world > 1
+        # loopback rehearsal (parallel.comm.loopback): one rank, every operand edge through the transport
+        self._loop = bool(getattr(ctx, "loopback", False))
+        distributed = ctx.world > 1 or self._loop
         dtype = self.mats[0].dtype if self.mats else torch.float64
         stages = [st for st in self.stages if st.ops]
         self.transport = None
@@ -198,7 +200,7 @@ class TileProgram:
             for op in st.ops:
                 o = self._owner(op.out)
                 for k in op.ins:
-                    if self._owner(k) != o and k not in seen[o]:
+                    if (self._owner(k) != o or (self._loop and k != op.out)) and k not in seen[o]:
                         seen[o].add(k)
                         needs[o].append(k)
                         ready = max(ready, last_w.get(k, -1))
@@ -220,7 +222,7 @@ class TileProgram:
             sends = defaultdict(list)
             for d in range(world):
                 for key in needs.get(d, []):
-                    if self._owner(key) == me and d != me:
+                    if self._owner(key) == me and (d != me or self._loop):
                         M = self.mats[key[0]]
                         sends[d].append((key[0], M.offset(key[1], key[2]), M.ld, M.tile_rows(key[1]),
                                          M.tile_cols(key[2]), mb))
@@ -281,7 +283,7 @@ class _StageRunner:
 
         def loc(key: Key):
             M = mats[key[0]]
-            if M.rank_of(key[1], key[2]) == prog.ctx.rank:
+            if plan is None or key not in plan.slot:   # local (the receive plan holds every remote operand)
                 return ("L", key[0]), M.offset(key[1], key[2]), M.ld
             return ("R", 0), plan.offset(*key), plan.ld
 
