@@ -39,6 +39,30 @@ PyObject* dpl_arg_real(double v);
 PyObject* dpl_arg_cplx(dplasma_complex64_t v);
 PyObject* dpl_arg_cplx(dplasma_complex32_t v);
 
+// QR reduction tree handle (same layout as dplasma.h / the reference's qr_param.h struct)
+typedef struct dplasma_qrtree_s dplasma_qrtree_t;
+#ifndef DPLASMA_QRTREE_DEFINED
+#define DPLASMA_QRTREE_DEFINED
+struct dplasma_qrtree_s {
+  int (*getnbgeqrf)(const dplasma_qrtree_t*, int);
+  int (*getm)(const dplasma_qrtree_t*, int, int);
+  int (*geti)(const dplasma_qrtree_t*, int, int);
+  int (*gettype)(const dplasma_qrtree_t*, int, int);
+  int (*currpiv)(const dplasma_qrtree_t*, int, int);
+  int (*nextpiv)(const dplasma_qrtree_t*, int, int, int);
+  int (*prevpiv)(const dplasma_qrtree_t*, int, int, int);
+  int mt, nt, a, p;
+  void* args;   // PyObject* of the framework's tree (a strong reference)
+};
+#endif
+PyObject* dpl_arg_qrtree(const dplasma_qrtree_t* q);
+// an opaque framework object handed to C earlier (butterfly vectors): a new reference to it
+PyObject* dpl_arg_obj(const void* h);
+// "call" returning an object: stored as a new reference in *out (0), or -1
+int dpl_call_obj_out(dplasma_context_t* ctx, const char* name, void** out, std::initializer_list<PyObject*> args);
+// tp_setter(tp, name, v): a taskpool parameter (dplasma_<p>potrf_setrecursive, ...)
+void dpl_tp_setter(dplasma_taskpool_t* tp, const char* name, int v);
+
 PyObject* dpl_arg_ptr(const void* p);
 PyObject* dpl_arg_str(const char* s, int len);
 void dpl_keep_error();

@@ -140,6 +140,156 @@ PyObject* dpl_call_fn(const char* fname, std::initializer_list<PyObject*> args) 
   return call_obj(nullptr, fname, nullptr, args);
 }
 
+PyObject* dpl_arg_qrtree(const dplasma_qrtree_t* q) {
+  PyObject* o = q && q->args ? (PyObject*)q->args : Py_None;
+  Py_INCREF(o);
+  return o;
+}
+
+PyObject* dpl_arg_obj(const void* h) {
+  PyObject* o = h ? (PyObject*)h : Py_None;
+  Py_INCREF(o);
+  return o;
+}
+
+int dpl_call_obj_out(dplasma_context_t* ctx, const char* name, void** out, std::initializer_list<PyObject*> args) {
+  g_err.clear();
+  PyObject* r = call_obj(ctx, "call_obj", name, args);
+  if (!r) return -1;
+  if (out) *out = r;   // the caller owns the reference (dplasma_but_free)
+  else Py_DECREF(r);
+  return 0;
+}
+
+void dpl_tp_setter(dplasma_taskpool_t* tp, const char* name, int v) {
+  if (!tp || !tp->obj) return;   // native taskpools have no recursive sub-DAGs to size
+  DplGil g;
+  g_err.clear();
+  PyObject* r = call_obj(nullptr, "tp_setter", nullptr, {(Py_INCREF(tp->obj), tp->obj), PyUnicode_FromString(name),
+                                                          PyLong_FromLong(v)});
+  Py_XDECREF(r);
+}
+
+// ---- QR reduction trees (qr_param.h): the tree object lives in the framework; the query functions of
+// the C handle ask it (each call takes the GIL)
+static int qt_call(const dplasma_qrtree_t* q, const char* meth, std::initializer_list<int> a) {
+  if (!q || !q->args) return -1;
+  DplGil g;
+  PyObject* tup = PyTuple_New((Py_ssize_t)a.size());
+  Py_ssize_t i = 0;
+  for (int v : a) PyTuple_SET_ITEM(tup, i++, PyLong_FromLong(v));
+  PyObject* f = PyObject_GetAttrString((PyObject*)q->args, meth);
+  PyObject* r = f ? PyObject_CallObject(f, tup) : nullptr;
+  Py_XDECREF(f);
+  Py_DECREF(tup);
+  int v = -1;
+  if (r) v = (int)PyLong_AsLong(r);
+  else keep_error();
+  Py_XDECREF(r);
+  return v;
+}
+static int qt_getnbgeqrf(const dplasma_qrtree_t* q, int k) { return qt_call(q, "getnbgeqrf", {k}); }
+static int qt_getm(const dplasma_qrtree_t* q, int k, int i) { return qt_call(q, "getm", {k, i}); }
+static int qt_geti(const dplasma_qrtree_t* q, int k, int m) { return qt_call(q, "geti", {k, m}); }
+static int qt_gettype(const dplasma_qrtree_t* q, int k, int m) { return qt_call(q, "gettype", {k, m}); }
+static int qt_currpiv(const dplasma_qrtree_t* q, int k, int m) { return qt_call(q, "currpiv", {k, m}); }
+static int qt_nextpiv(const dplasma_qrtree_t* q, int k, int p, int m) { return qt_call(q, "nextpiv", {k, p, m}); }
+static int qt_prevpiv(const dplasma_qrtree_t* q, int k, int p, int m) { return qt_call(q, "prevpiv", {k, p, m}); }
+
+// kind: "hqr" / "systolic" / "svd"; ints: that init's integer parameters (capi.qrtree_init)
+static int qt_init(dplasma_qrtree_t* q, const char* kind, int trans, dplasma_desc_t* A, std::initializer_list<int> ints) {
+  if (!q || !A) return -1;
+  if (!A->obj) {
+    g_err = "QR trees need a framework (Python) descriptor; native contexts have no tree-based QR";
+    return -1;
+  }
+  DplGil g;
+  g_err.clear();
+  PyObject* il = PyTuple_New((Py_ssize_t)ints.size());
+  Py_ssize_t i = 0;
+  for (int v : ints) PyTuple_SET_ITEM(il, i++, PyLong_FromLong(v));
+  PyObject* r = call_obj(nullptr, "qrtree_init", nullptr,
+                         {PyUnicode_FromString(kind), PyLong_FromLong(trans), (Py_INCREF(A->obj), A->obj), il});
+  if (!r) return -1;
+  q->args = r;   // new reference, released by *_finalize
+  q->getnbgeqrf = qt_getnbgeqrf;
+  q->getm = qt_getm;
+  q->geti = qt_geti;
+  q->gettype = qt_gettype;
+  q->currpiv = qt_currpiv;
+  q->nextpiv = qt_nextpiv;
+  q->prevpiv = qt_prevpiv;
+  auto attr = [&](const char* n) {
+    PyObject* v = PyObject_GetAttrString(r, n);
+    const int x = v ? (int)PyLong_AsLong(v) : 0;
+    Py_XDECREF(v);
+    return x;
+  };
+  q->mt = attr("mt");
+  q->nt = attr("nt");
+  q->a = attr("a");
+  q->p = attr("p");
+  return 0;
+}
+
+static void qt_fini(dplasma_qrtree_t* q) {
+  if (!q || !q->args) return;
+  DplGil g;
+  Py_DECREF((PyObject*)q->args);
+  q->args = nullptr;
+}
+
+static void qt_print(dplasma_desc_t* A, dplasma_qrtree_t* q, const char* what, int k, int* perm, const char* file) {
+  (void)A;
+  if (!q || !q->args) return;
+  DplGil g;
+  PyObject* r = call_obj(nullptr, "qrtree_print", nullptr,
+                         {(Py_INCREF((PyObject*)q->args), (PyObject*)q->args), PyUnicode_FromString(what),
+                          PyLong_FromLong(k), PyLong_FromUnsignedLongLong((unsigned long long)(uintptr_t)perm),
+                          PyUnicode_FromString(file ? file : "")});
+  Py_XDECREF(r);
+}
+
+extern "C" {
+DPL_CAPI int dplasma_hqr_init(dplasma_qrtree_t* q, int trans, dplasma_desc_t* A, int type_llvl, int type_hlvl, int a,
+                              int p, int domino, int tsrr) {
+  return qt_init(q, "hqr", trans, A, {type_llvl, type_hlvl, a, p, domino, tsrr});
+}
+DPL_CAPI void dplasma_hqr_finalize(dplasma_qrtree_t* q) { qt_fini(q); }
+DPL_CAPI int dplasma_systolic_init(dplasma_qrtree_t* q, int trans, dplasma_desc_t* A, int p, int qq) {
+  return qt_init(q, "systolic", trans, A, {p, qq});
+}
+DPL_CAPI void dplasma_systolic_finalize(dplasma_qrtree_t* q) { qt_fini(q); }
+DPL_CAPI int dplasma_svd_init(dplasma_qrtree_t* q, int trans, dplasma_desc_t* A, int type_hlvl, int p,
+                              int nbcores_per_node, int ratio) {
+  return qt_init(q, "svd", trans, A, {type_hlvl, p, nbcores_per_node, ratio});
+}
+DPL_CAPI void dplasma_svd_finalize(dplasma_qrtree_t* q) { qt_fini(q); }
+DPL_CAPI int dplasma_qrtree_check(dplasma_desc_t* A, dplasma_qrtree_t* q) {
+  (void)A;
+  if (!q || !q->args) return -1;
+  DplGil g;
+  g_err.clear();
+  PyObject* r = call_obj(nullptr, "qrtree_check", nullptr, {(Py_INCREF((PyObject*)q->args), (PyObject*)q->args)});
+  const int v = r ? (int)PyLong_AsLong(r) : 1;
+  Py_XDECREF(r);
+  return v;
+}
+DPL_CAPI void dplasma_qrtree_print_dag(dplasma_desc_t* A, dplasma_qrtree_t* q, char* f) { qt_print(A, q, "dag", -1, nullptr, f); }
+DPL_CAPI void dplasma_qrtree_print_type(dplasma_desc_t* A, dplasma_qrtree_t* q) { qt_print(A, q, "type", -1, nullptr, nullptr); }
+DPL_CAPI void dplasma_qrtree_print_pivot(dplasma_desc_t* A, dplasma_qrtree_t* q) { qt_print(A, q, "pivot", -1, nullptr, nullptr); }
+DPL_CAPI void dplasma_qrtree_print_nbgeqrt(dplasma_desc_t* A, dplasma_qrtree_t* q) { qt_print(A, q, "nbgeqrt", -1, nullptr, nullptr); }
+DPL_CAPI void dplasma_qrtree_print_perm(dplasma_desc_t* A, dplasma_qrtree_t* q, int* perm) { qt_print(A, q, "perm", -1, perm, nullptr); }
+DPL_CAPI void dplasma_qrtree_print_next_k(dplasma_desc_t* A, dplasma_qrtree_t* q, int k) { qt_print(A, q, "next_k", k, nullptr, nullptr); }
+DPL_CAPI void dplasma_qrtree_print_prev_k(dplasma_desc_t* A, dplasma_qrtree_t* q, int k) { qt_print(A, q, "prev_k", k, nullptr, nullptr); }
+DPL_CAPI void dplasma_qrtree_print_geqrt_k(dplasma_desc_t* A, dplasma_qrtree_t* q, int k) { qt_print(A, q, "geqrt_k", k, nullptr, nullptr); }
+DPL_CAPI void dplasma_but_free(void* h) {
+  if (!h) return;
+  DplGil g;
+  Py_DECREF((PyObject*)h);
+}
+}  // extern "C"
+
 dplasma_taskpool_t* dpl_call_new(dplasma_context_t* ctx, const char* name, std::initializer_list<PyObject*> args) {
   g_err.clear();
   PyObject* o = call_obj(ctx, "new", name, args);

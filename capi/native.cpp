@@ -622,21 +622,29 @@ NatProgram* nat_laset(dplasma_context_t* ctx, int prec, int uplo, const void* al
   return P;
 }
 
+// A := alpha A on this rank's tiles of the uplo part, appended to P after everything already in it
+// (also the beta scaling of a grid GEMM with an empty k range, native_dist.cpp)
+bool nat_add_lascal(NatProgram& P, int uplo, const Scalar& al, NatDesc& A) {
+  auto mb = std::make_shared<MapBatch>();
+  mb->build(A, uplo, nullptr, NOTRANS);
+  if (!mb->upload(P)) return false;
+  const int prec = A.prec, part = part_of(uplo), lda = A.lld;
+  char* a = A.data;
+  int deps[NAT_NSTREAM];
+  for (int q = 0; q < NAT_NSTREAM; ++q) deps[q] = last_on(P, q);
+  P.task(1, [=](hipStream_t s) {
+    if (mb->n() == 0) return 0;
+    return dpl_lascal(prec, part, mb->n(), mb->items(), mb->mm, mb->nn, al.ptr(), a, lda, s);
+  }, {deps[0], deps[1], deps[2]});
+  return true;
+}
+
 NatProgram* nat_lascal(dplasma_context_t* ctx, int prec, int uplo, const void* alpha, dplasma_desc_t* dA) {
   NatCtx* c = ctx->nat;
   NatDesc* A = dA ? dA->nat : nullptr;
   if (!same_ctx_dist(c, {A}, prec)) return fail(nullptr, "lascal: descriptor of another context");
   NatProgram* P = new_program(c, "lascal", false);
-  auto mb = std::make_shared<MapBatch>();
-  mb->build(*A, uplo, nullptr, NOTRANS);
-  if (!mb->upload(*P)) return fail(P, "lascal: device allocation failed");
-  const Scalar al(prec, alpha);
-  const int part = part_of(uplo), lda = A->lld;
-  char* a = A->data;
-  P->task(1, [=](hipStream_t s) {
-    if (mb->n() == 0) return 0;
-    return dpl_lascal(prec, part, mb->n(), mb->items(), mb->mm, mb->nn, al.ptr(), a, lda, s);
-  }, {});
+  if (!nat_add_lascal(*P, uplo, Scalar(prec, alpha), *A)) return fail(P, "lascal: device allocation failed");
   return P;
 }
 
@@ -855,7 +863,9 @@ DPL_CAPI dplasma_context_t* dplasma_init_native_dist(int device, int rank, int w
   c->Q = world / P;
   c->myrow = rank / c->Q;
   c->mycol = rank % c->Q;
-  if (world > 1) {
+  const char* lb = std::getenv("DPLASMA_LOOPBACK");
+  c->loop = world == 1 && lb && *lb == '1';
+  if (world > 1 || c->loop) {
     std::string err;
     c->comm = nat_comm_create(rank, world, device, rdv_dir, err);
     if (!c->comm) {
@@ -1511,11 +1521,16 @@ bool add_getrf(NatProgram& P, NatDesc& A, NatDesc& IP, int& last) {
 // device, 0-based within the panel) applied to every local tile column of B on a grid: planned on the host
 // at run time (one synchronisation), rows that cross process rows travel point to point within the process
 // column, every source row read before any destination is written.  RB: scratch for 2 x (mb + 16) rows.
-int add_rowmoves_dist(NatProgram& P, NatDesc& B, const int* piv, int r0, int kmin, const DevPtr& RB, int prev) {
+// IT: item staging allocated once per program (3 regions of 2 (mb + 16) TileItems: pack / local unpack /
+// remote unpack), so a panel step neither allocates nor frees device memory (hipFree synchronises the device)
+int add_rowmoves_dist(NatProgram& P, NatDesc& B, const int* piv, int r0, int kmin, const DevPtr& RB, const DevPtr& IT,
+                      int prev) {
   NatComm* comm = P.ctx->comm;
   const int prec = B.prec, mb = B.mb, ld = B.lld, es = B.es, Pg = B.P, Q = B.Q, ln = B.ln;
   const int myrow = B.myrow, mycol = B.mycol;
   char *a = B.data, *rb = (char*)RB->p;
+  TileItem* itb = (TileItem*)IT->p;
+  const size_t itr = (size_t)2 * (mb + 16);   // items per region
   const Scalar one(prec, 1.0), zero(prec, 0.0);
   auto lrow = [=](int r) { return (long long)((r / mb) / Pg) * mb + r % mb; };   // local row of a global row
   return P.task(1, [=](hipStream_t s) {
@@ -1549,20 +1564,19 @@ int add_rowmoves_dist(NatProgram& P, NatDesc& B, const int* piv, int r0, int kmi
         ++nr;
       }
     }
-    auto launch = [&](const std::vector<TileItem>& it, const char* src, int lds, char* dst, int ldd) -> int {
+    // each list has its own item region (the task began with a stream synchronisation, so no launch of
+    // the previous step still reads them); the host copies are synchronous (pageable sources)
+    auto launch = [&](const std::vector<TileItem>& it, int region, const char* src, int lds, char* dst, int ldd) -> int {
       if (it.empty()) return 0;
-      void* d = nullptr;
-      if (hipMalloc(&d, it.size() * sizeof(TileItem)) != hipSuccess) return -1;
-      int rc = hipMemcpy(d, it.data(), it.size() * sizeof(TileItem), hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
-      if (rc == 0) rc = dpl_geadd(prec, 0, NOTRANS, (int)it.size(), d, 1, ln, one.ptr(), src, lds, zero.ptr(), dst, ldd, 1, s);
-      if (rc == 0 && hipStreamSynchronize(s) != hipSuccess) rc = -1;
-      (void)hipFree(d);
-      return rc;
+      if (it.size() > itr) return -1;
+      TileItem* d = itb + region * itr;
+      if (hipMemcpy(d, it.data(), it.size() * sizeof(TileItem), hipMemcpyHostToDevice) != hipSuccess) return -1;
+      return dpl_geadd(prec, 0, NOTRANS, (int)it.size(), d, 1, ln, one.ptr(), src, lds, zero.ptr(), dst, ldd, 1, s);
     };
-    int rc = launch(pack, a, ld, sbuf, 1);
+    int rc = launch(pack, 0, a, ld, sbuf, 1);
     if (rc == 0) rc = comm->exchange(snd, rcv, s);
-    if (rc == 0) rc = launch(ul, sbuf, 1, a, ld);
-    if (rc == 0) rc = launch(ur, rbuf, 1, a, ld);
+    if (rc == 0) rc = launch(ul, 1, sbuf, 1, a, ld);
+    if (rc == 0) rc = launch(ur, 2, rbuf, 1, a, ld);
     return rc;
   }, {prev});
 }
@@ -1572,9 +1586,11 @@ bool add_getrs_dist(NatProgram& P, NatDesc& A, NatDesc& IP, NatDesc& B) {
   const int kt = std::min(A.mt, A.nt), mb = A.mb;
   DevPtr RB = dev_alloc((size_t)2 * 2 * (mb + 16) * std::max(1, B.ln) * B.es, false);
   DevPtr PV = dev_alloc(sizeof(int) * (mb + 16), false);
-  if (!RB || !PV) return false;
+  DevPtr IT = dev_alloc(sizeof(TileItem) * 3 * 2 * (mb + 16), false);
+  if (!RB || !PV || !IT) return false;
   P.keep.push_back(RB);
   P.keep.push_back(PV);
+  P.keep.push_back(IT);
   const int* ipg = (const int*)IP.data;
   int* pv = (int*)PV->p;
   int prev = (int)P.tasks.size() - 1;   // after everything so far (a factorisation)
@@ -1583,7 +1599,7 @@ bool add_getrs_dist(NatProgram& P, NatDesc& A, NatDesc& IP, NatDesc& B) {
     // IPIV holds 1-based global rows: back to 0-based within the panel for the planner
     prev = P.task(1, [=](hipStream_t s) { return dpl_ipiv_shift(ipg + r0, pv, kmin, -(r0 + 1), s); },
                   {prev, last_on(P, 0), last_on(P, 2)});
-    prev = add_rowmoves_dist(P, B, pv, r0, kmin, RB, prev);
+    prev = add_rowmoves_dist(P, B, pv, r0, kmin, RB, IT, prev);
   }
   const Scalar one(B.prec, 1.0);
   return nat_dist_trsm_into(P, LEFT, LOWER, NOTRANS, UNIT, one, A, B) &&
@@ -1608,8 +1624,9 @@ bool add_getrf_dist(NatProgram& P, NatDesc& A, NatDesc& IP) {
   const size_t st = (size_t)mb * A.nb;
   DevPtr TS = dev_alloc((size_t)std::max(1, A.mt) * st * es, false), US = dev_alloc((size_t)std::max(1, A.nt) * st * es, false);
   DevPtr RB = dev_alloc((size_t)2 * 2 * (mb + 16) * std::max(1, ln) * es, false);   // row-move send / receive rows
-  if (!TS || !US || !RB) return false;
-  for (const DevPtr& d : {TS, US, RB}) P.keep.push_back(d);
+  DevPtr IT = dev_alloc(sizeof(TileItem) * 3 * 2 * (mb + 16), false);                 // their copy items
+  if (!TS || !US || !RB || !IT) return false;
+  for (const DevPtr& d : {TS, US, RB, IT}) P.keep.push_back(d);
   char *a = A.data, *pvb = (char*)S.pv->p, *ts = (char*)TS->p, *us = (char*)US->p, *rb = (char*)RB->p;
   int* info = (int*)P.info->p;
   int* ipg = (int*)IP.data;
@@ -1659,7 +1676,7 @@ bool add_getrf_dist(NatProgram& P, NatDesc& A, NatDesc& IP) {
     }
     prev = P.task(1, [=](hipStream_t s) { return dpl_ipiv_shift(piv, ipg + r0, kmin, r0 + 1, s); }, {prev});
     // ---- 3. net row interchanges on this rank's tile columns, planned from the pivots
-    prev = add_rowmoves_dist(P, A, piv, r0, kmin, RB, prev);
+    prev = add_rowmoves_dist(P, A, piv, r0, kmin, RB, IT, prev);
     // ---- 4. my tiles of the factored panel back into A
     prev = P.task(1, [=](hipStream_t s) {
       if (back->n() == 0) return 0;

@@ -3,6 +3,7 @@
 // with the copy a Python process may already hold) and the node-local file transport.
 #include "native_comm.h"
 
+#include <dirent.h>
 #include <dlfcn.h>
 #include <fcntl.h>
 #include <rccl/rccl.h>
@@ -59,18 +60,20 @@ bool debug() {
 
 class FileComm final : public NatComm {
  public:
-  std::string dir;
+  std::string dir, token;   // token: this job's session (see nat_comm_create), prefix of every message
   std::vector<long long> sseq, rseq;   // per-peer message counters (pairs match in issue order)
   std::vector<char> stage;
 
   const char* name() const override { return "file"; }
 
   bool send_host(int peer, const void* p, size_t bytes) {
-    const std::string n = "m." + std::to_string(rank) + "." + std::to_string(peer) + "." + std::to_string(sseq[peer]++);
+    const std::string n = "m." + token + "." + std::to_string(rank) + "." + std::to_string(peer) + "." +
+                          std::to_string(sseq[peer]++);
     return write_file(dir, n, p, bytes);
   }
   bool recv_host(int peer, void* p, size_t bytes) {
-    const std::string n = "m." + std::to_string(peer) + "." + std::to_string(rank) + "." + std::to_string(rseq[peer]++);
+    const std::string n = "m." + token + "." + std::to_string(peer) + "." + std::to_string(rank) + "." +
+                          std::to_string(rseq[peer]++);
     return read_file(dir, n, p, bytes, true);
   }
 
@@ -167,6 +170,8 @@ class RcclComm final : public NatComm {
 
   int exchange(const std::vector<NatMsg>& sends, const std::vector<NatMsg>& recvs, hipStream_t s) override {
     if (sends.empty() && recvs.empty()) return 0;
+    if (debug())
+      std::fprintf(stderr, "[native rank %d] rccl exchange: %zu sends, %zu recvs\n", rank, sends.size(), recvs.size());
     if (r.groupStart() != ncclSuccess) return -1;
     ncclResult_t e = ncclSuccess;
     for (const NatMsg& m : sends)
@@ -197,6 +202,143 @@ class RcclComm final : public NatComm {
 
 }  // namespace
 
+// ------------------------------------------------------------------------------------------ session
+// Rendezvous in a node-local directory, safe against files an earlier (crashed) job left there:
+//   rank 0 removes every stale rendezvous file, draws a random session token T and publishes it
+//   ("session"); every other rank draws a random nonce, reads T and answers "hello.T.r" = {nonce, its
+//   transport preference}; rank 0, once it has every hello, decides the transport for everyone (RCCL
+//   only if every rank sees enough GPUs and DPLASMA_NATIVE_TRANSPORT at rank 0 does not say "file")
+//   and publishes "go.T" = {transport, every rank's nonce, the RCCL unique id}.  A rank accepts a go
+//   file only if it carries its own nonce, and re-answers if the session token changes while it
+//   waits -- a stale session, hello or go file is never taken for this job's.  Message files are
+//   named m.T.src.dst.seq.
+namespace {
+
+unsigned long long rnd64() {
+  unsigned long long v = 0;
+  if (FILE* f = std::fopen("/dev/urandom", "rb")) {
+    if (std::fread(&v, sizeof v, 1, f) != 1) v = 0;
+    std::fclose(f);
+  }
+  if (v == 0)
+    v = (unsigned long long)std::chrono::steady_clock::now().time_since_epoch().count() ^
+        ((unsigned long long)getpid() << 32);
+  return v;
+}
+
+std::string hex(unsigned long long v) {
+  char b[17];
+  std::snprintf(b, sizeof b, "%016llx", v);
+  return b;
+}
+
+struct Session {
+  unsigned long long token;
+  int world;
+};
+struct Hello {
+  unsigned long long nonce;
+  int pref_rccl;
+  int pad;
+};
+struct GoHead {
+  int rccl;
+  int world;
+  ncclUniqueId id;
+};
+
+bool try_read(const std::string& path, void* data, size_t bytes) {
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) return false;
+  const bool ok = std::fread(data, 1, bytes, f) == bytes;
+  std::fclose(f);
+  return ok;
+}
+
+void remove_stale(const std::string& dir) {
+  if (DIR* d = opendir(dir.c_str())) {
+    while (dirent* e = readdir(d)) {
+      const std::string n = e->d_name;
+      if (n == "session" || n.rfind("hello.", 0) == 0 || n.rfind("go.", 0) == 0 || n.rfind("m.", 0) == 0 ||
+          n.rfind(".tmp.", 0) == 0)
+        std::remove((dir + "/" + n).c_str());
+    }
+    closedir(d);
+  }
+}
+
+// establishes the session; returns false (err set) on timeout
+bool rendezvous(const std::string& dir, int rank, int world, bool pref_rccl, const Rccl* rccl, std::string& token,
+                bool& use_rccl, ncclUniqueId& id, std::string& err) {
+  const auto t0 = std::chrono::steady_clock::now();
+  auto expired = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s(); };
+  if (rank == 0) {
+    remove_stale(dir);
+    const Session ss{rnd64(), world};
+    token = hex(ss.token);
+    if (!write_file(dir, "session", &ss, sizeof ss)) { err = "cannot write the session file in " + dir; return false; }
+    std::vector<unsigned long long> nonces(world, 0);
+    bool all_rccl = pref_rccl;
+    for (int r = 1; r < world; ++r) {
+      Hello h{};
+      if (!read_file(dir, "hello." + token + "." + std::to_string(r), &h, sizeof h, true)) {
+        err = "native rendezvous: rank " + std::to_string(r) + " did not answer in " + dir;
+        return false;
+      }
+      nonces[r] = h.nonce;
+      all_rccl = all_rccl && h.pref_rccl;
+    }
+    const char* tv = std::getenv("DPLASMA_NATIVE_TRANSPORT");
+    use_rccl = tv && *tv ? std::string(tv) == "rccl" : all_rccl;
+    GoHead gh{};
+    gh.rccl = use_rccl ? 1 : 0;
+    gh.world = world;
+    if (use_rccl && (!rccl || rccl->getUniqueId(&gh.id) != ncclSuccess)) { err = "RCCL unique id"; return false; }
+    id = gh.id;
+    std::vector<char> buf(sizeof gh + sizeof(unsigned long long) * world);
+    std::memcpy(buf.data(), &gh, sizeof gh);
+    std::memcpy(buf.data() + sizeof gh, nonces.data(), sizeof(unsigned long long) * world);
+    if (!write_file(dir, "go." + token, buf.data(), buf.size())) { err = "cannot write the go file"; return false; }
+    return true;
+  }
+  const unsigned long long nonce = rnd64();
+  std::string cur_tok;
+  int us = 50;
+  while (!expired()) {
+    Session ss{};
+    if (!try_read(dir + "/session", &ss, sizeof ss) || ss.world != world) {
+      std::this_thread::sleep_for(std::chrono::microseconds(us));
+      us = std::min(2 * us, 5000);
+      continue;
+    }
+    const std::string tok = hex(ss.token);
+    if (tok != cur_tok) {   // (re)answer this session
+      const Hello h{nonce, pref_rccl ? 1 : 0, 0};
+      if (!write_file(dir, "hello." + tok + "." + std::to_string(rank), &h, sizeof h)) { err = "cannot write hello"; return false; }
+      cur_tok = tok;
+    }
+    std::vector<char> buf(sizeof(GoHead) + sizeof(unsigned long long) * world);
+    if (try_read(dir + "/go." + tok, buf.data(), buf.size())) {
+      GoHead gh;
+      std::memcpy(&gh, buf.data(), sizeof gh);
+      unsigned long long mine = 0;
+      std::memcpy(&mine, buf.data() + sizeof gh + sizeof(unsigned long long) * rank, sizeof mine);
+      if (gh.world == world && mine == nonce) {
+        token = tok;
+        use_rccl = gh.rccl != 0;
+        id = gh.id;
+        return true;
+      }
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(us));
+    us = std::min(2 * us, 5000);
+  }
+  err = "native rendezvous timed out in " + dir;
+  return false;
+}
+
+}  // namespace
+
 NatComm* nat_comm_create(int rank, int world, int device, const char* rdv_dir, std::string& err) {
   const char* env_dir = std::getenv("DPLASMA_NATIVE_RDV");
   const std::string dir = rdv_dir && *rdv_dir ? rdv_dir : env_dir ? env_dir : "";
@@ -205,35 +347,37 @@ NatComm* nat_comm_create(int rank, int world, int device, const char* rdv_dir, s
   int ndev = 0;
   (void)hipGetDeviceCount(&ndev);
   const char* tv = std::getenv("DPLASMA_NATIVE_TRANSPORT");
-  const std::string t = tv && *tv ? tv : (ndev >= world ? "rccl" : "file");
-  if (t == "file") {
+  const std::string want = tv && *tv ? tv : "";
+  if (!want.empty() && want != "rccl" && want != "file") { err = "DPLASMA_NATIVE_TRANSPORT must be rccl or file"; return nullptr; }
+  // this rank's preference; rank 0 decides for everyone (a per-rank choice could split the job)
+  const bool pref_rccl = want.empty() ? ndev >= world : want == "rccl";
+  Rccl rccl;
+  std::string rerr;
+  const bool have_rccl = rccl.load(rerr);
+  std::string token;
+  bool use_rccl = false;
+  ncclUniqueId id{};
+  if (!rendezvous(dir, rank, world, pref_rccl && have_rccl, have_rccl ? &rccl : nullptr, token, use_rccl, id, err))
+    return nullptr;
+  if (!use_rccl) {
     auto* c = new FileComm;
     c->rank = rank;
     c->world = world;
     c->dir = dir;
+    c->token = token;
+    c->session_token = token;
     c->sseq.assign(world, 0);
     c->rseq.assign(world, 0);
     double x = 0.0;   // every rank present before the first exchange
     if (c->allreduce(&x, 1, false) != 0) { err = "file transport: rendezvous timed out in " + dir; delete c; return nullptr; }
+    c->session_dir = dir;
     return c;
   }
-  if (t != "rccl") { err = "DPLASMA_NATIVE_TRANSPORT must be rccl or file"; return nullptr; }
+  if (!have_rccl) { err = "rank 0 chose RCCL but " + rerr; return nullptr; }
   auto* c = new RcclComm;
   c->rank = rank;
   c->world = world;
-  if (!c->r.load(err)) { delete c; return nullptr; }
-  ncclUniqueId id;
-  if (rank == 0) {
-    if (c->r.getUniqueId(&id) != ncclSuccess || !write_file(dir, "ncclid", &id, sizeof id)) {
-      err = "RCCL unique id";
-      delete c;
-      return nullptr;
-    }
-  } else if (!read_file(dir, "ncclid", &id, sizeof id, false)) {
-    err = "RCCL rendezvous timed out in " + dir;
-    delete c;
-    return nullptr;
-  }
+  c->r = rccl;
   (void)hipSetDevice(device);
   int lo = 0, hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
@@ -243,15 +387,20 @@ NatComm* nat_comm_create(int rank, int world, int device, const char* rdv_dir, s
     delete c;
     return nullptr;
   }
-  double x = 0.0;   // everyone has read the id: rank 0 removes it
+  double x = 0.0;
   if (c->allreduce(&x, 1, false) != 0) { err = "RCCL all-reduce failed"; delete c; return nullptr; }
-  if (rank == 0) std::remove((dir + "/ncclid").c_str());
+  c->session_dir = dir;
+  c->session_token = token;
   return c;
 }
 
 void nat_comm_destroy(NatComm* c) {
   double x = 0.0;   // nobody leaves while a peer may still read its messages
   (void)c->allreduce(&x, 1, false);
+  if (c->rank == 0 && !c->session_dir.empty()) {   // the session's files: nobody reads them any more
+    std::remove((c->session_dir + "/session").c_str());
+    if (!c->session_token.empty()) std::remove((c->session_dir + "/go." + c->session_token).c_str());
+  }
   delete c;
 }
 

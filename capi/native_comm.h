@@ -26,6 +26,7 @@ struct NatMsg {
 class NatComm {
  public:
   int rank = 0, world = 1;
+  std::string session_dir, session_token;   // rendezvous session (native_comm.cpp), cleaned up by rank 0
   virtual ~NatComm() = default;
   virtual const char* name() const = 0;
   // every send and receive of one step, issued on stream st after the work already queued there

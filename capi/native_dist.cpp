@@ -79,6 +79,15 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
   if (!W) return fail(Pr, "potrf: panel slots: device allocation failed");
   Pr->keep.push_back(W);
   char* Wb[2] = {(char*)W->p, (char*)W->p + (size_t)nt * slot_elems * es};
+  // loopback (NatCtx::loop): the owner stages what it sends to itself in LB (double-buffered like W)
+  const bool loop = c->loop;
+  DevPtr LBw;
+  if (loop) {
+    LBw = dev_alloc(2 * (size_t)std::max(1, nt) * slot_elems * es, false);
+    if (!LBw) return fail(Pr, "potrf: loopback slots: device allocation failed");
+    Pr->keep.push_back(LBw);
+  }
+  char* LBb[2] = {loop ? (char*)LBw->p : nullptr, loop ? (char*)LBw->p + (size_t)nt * slot_elems * es : nullptr};
   auto slot = [&](int i) { return (long long)i * (long long)slot_elems; };
   auto tc = [&](int i, int k) { return lower ? std::make_pair(i, k) : std::make_pair(k, i); };
   auto own = [&](int i, int k) { const auto t = tc(i, k); return A.owner(t.first, t.second); };
@@ -118,6 +127,7 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
     const int xch_km2 = k >= 2 ? xch[k - 2] : -1;
     const int own_k = A.owner(k, k);
     char* wb = Wb[b];
+    char* sb = loop ? LBb[b] : wb;   // where this rank's outgoing panel data is staged
     // POTRF(k): the diagonal tile has every update of steps < k (NEXT(k-1) and REST(k-2))
     int t_diag = -1;
     if (me == own_k) {
@@ -127,7 +137,7 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
         return rb ? dpl_potrf_tile_rbz(uplo, kb, (double*)base + dk, ld, info, k * mb, zk, s)
                   : dpl_potrf_tile(prec, uplo, kb, base, dk, ld, info, k * mb, s);
       }, {next_prev, rest_km2});
-      char* dst = wb + slot(k) * es;   // (run-time lambdas capture values only)
+      char* dst = sb + slot(k) * es;   // (run-time lambdas capture values only)
       t_diag = Pr->task(0, [=](hipStream_t s) {
         return hipMemcpy2DAsync(dst, (size_t)mb * es, base + dk * es, (size_t)ld * es, (size_t)kb * es, kb,
                                 hipMemcpyDeviceToDevice, s) == hipSuccess ? 0 : -1;
@@ -136,10 +146,10 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
     // DIAG exchange: the factor to every other rank holding a panel tile of step k
     std::set<int> drc;
     for (int i = k + 1; i < std::min(nt, k + 1 + (lower ? Pg : Qg)); ++i) drc.insert(own(i, k));
-    drc.erase(own_k);
+    if (!loop) drc.erase(own_k);
     std::vector<NatMsg> ds, dr;
     if (me == own_k)
-      for (int r : drc) ds.push_back(NatMsg{r, wb + slot(k) * es, sbytes});
+      for (int r : drc) ds.push_back(NatMsg{r, sb + slot(k) * es, sbytes});
     if (drc.count(me)) dr.push_back(NatMsg{own_k, wb + slot(k) * es, sbytes});
     const int t_xd = add_exchange(*Pr, ds, dr, {t_diag, rest_km2, next_prev, xch_km2});
     // TRSM of this rank's panel tiles against the factor in slot k, then pack them into their slots
@@ -167,7 +177,7 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
       Pr->keep.push_back(d);
       const int nrb = (int)strips.size();
       double* zk = (double*)zb->p + (size_t)(k % 2) * zsz;
-      const bool own = me == own_k;
+      const bool own = me == own_k && !loop;
       const double* L = own ? (const double*)base + A.off(k, k) : (const double*)wb + slot(k);
       const int ldl = own ? ld : mb;
       const int t_trsm = Pr->task(0, [=](hipStream_t s) {
@@ -177,13 +187,13 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
         }
         return dpl_trsm_rb(uplo, kb, L, ldl, zk, nrb, d->p, (double*)base, ld, s);
       }, {either(t_xd, t_diag), next_prev, rest_km2});
-      t_pack = Pr->task(0, [=](hipStream_t s) { return pk->launch(prec, base, ld, wb, mb, s); }, {t_trsm, xch_km2});
+      t_pack = Pr->task(0, [=](hipStream_t s) { return pk->launch(prec, base, ld, sb, mb, s); }, {t_trsm, xch_km2});
     } else if (!tr->it.empty()) {
       if (!tr->upload(*Pr, prec, side) || !pk->upload(*Pr)) return fail(Pr, "potrf: device allocation failed");
       const int t_trsm = Pr->task(0, [=](hipStream_t s) {
         return tr->launch(prec, side, uplo, CONJTRANS, NONUNIT, one, wb, mb, base, ld, s);
       }, {either(t_xd, t_diag), next_prev, rest_km2});
-      t_pack = Pr->task(0, [=](hipStream_t s) { return pk->launch(prec, base, ld, wb, mb, s); }, {t_trsm, xch_km2});
+      t_pack = Pr->task(0, [=](hipStream_t s) { return pk->launch(prec, base, ld, sb, mb, s); }, {t_trsm, xch_km2});
     }
     // PANEL exchange: tile i from its owner to the ranks whose trailing tiles read it (ascending i:
     // both sides of a pair enumerate their messages in the same order)
@@ -191,10 +201,10 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
     for (int i = k + 1; i < nt; ++i) {
       const int src = own(i, k);
       std::set<int> cs = consumers(k, i);
-      cs.erase(src);
+      if (!loop) cs.erase(src);
       if (src == me)
-        for (int r : cs) ps.push_back(NatMsg{r, wb + slot(i) * es, sbytes});
-      else if (cs.count(me))
+        for (int r : cs) ps.push_back(NatMsg{r, sb + slot(i) * es, sbytes});
+      if (cs.count(me) && (src != me || loop))
         pr.push_back(NatMsg{src, wb + slot(i) * es, sbytes});
     }
     const int t_xp = add_exchange(*Pr, ps, pr, {t_pack, t_xd, rest_km2, next_prev});
@@ -246,7 +256,8 @@ bool nat_dist_gemm_into(NatProgram& PrR, int prec, int tA, int tB, const Scalar&
   const int es = C.es, me = c->rank;
   const bool an = tA == NOTRANS, bn = tB == NOTRANS;
   const int kt = an ? A.nt : A.mt;
-  if (kt == 0) return true;
+  if (kt == 0)   // C := beta C (restricted to C's triangle when tri says so); no exchange at all
+    return nat_add_lascal(*Pr, tri, beta, C);
   const int j0 = last_task_on(*Pr, 0), j1 = last_task_on(*Pr, 1), j2 = last_task_on(*Pr, 2);
   const int kc = std::max(1, std::min(kt, env_int("DPLASMA_NATIVE_SUMMA_K", 4)));
   const size_t sa = (size_t)A.mb * A.nb, sb = (size_t)B.mb * B.nb;   // slots: stored tiles, ld mb
@@ -254,6 +265,16 @@ bool nat_dist_gemm_into(NatProgram& PrR, int prec, int tA, int tB, const Scalar&
   if (!WA || !WB) return false;
   Pr->keep.push_back(WA);
   Pr->keep.push_back(WB);
+  // loopback (NatCtx::loop): owners pack into LA / LB and send to themselves into WA / WB
+  const bool loop = c->loop;
+  DevPtr LA, LB;
+  if (loop) {
+    LA = dev_alloc(2 * (size_t)kc * C.mt * sa * es, false);
+    LB = dev_alloc(2 * (size_t)kc * C.nt * sb * es, false);
+    if (!LA || !LB) return false;
+    Pr->keep.push_back(LA);
+    Pr->keep.push_back(LB);
+  }
   auto aslot = [&](int kk, int m) { return ((long long)kk * C.mt + m) * (long long)sa; };
   auto bslot = [&](int kk, int n) { return ((long long)kk * C.nt + n) * (long long)sb; };
   // ranks holding a C tile of block row m / block column n
@@ -267,6 +288,8 @@ bool nat_dist_gemm_into(NatProgram& PrR, int prec, int tA, int tB, const Scalar&
     const int k0 = ch * kc, k1 = std::min(kt, k0 + kc), b = ch % 2;
     char* wa = (char*)WA->p + (size_t)b * kc * C.mt * sa * es;
     char* wb = (char*)WB->p + (size_t)b * kc * C.nt * sb * es;
+    char* pa_dst = loop ? (char*)LA->p + (size_t)b * kc * C.mt * sa * es : wa;   // packing targets
+    char* pb_dst = loop ? (char*)LB->p + (size_t)b * kc * C.nt * sb * es : wb;
     const int g2 = ch >= 2 ? gem[ch - 2] : -1, x2 = ch >= 2 ? xch[ch - 2] : -1;
     auto pa = std::make_shared<CopyBatch>(), pb = std::make_shared<CopyBatch>();
     std::vector<NatMsg> snd, rcv;
@@ -278,11 +301,10 @@ bool nat_dist_gemm_into(NatProgram& PrR, int prec, int tA, int tB, const Scalar&
           pa->add(A.off(si, sj), aslot(k - k0, m), A.rows(si), A.cols(sj));
           for (int q : qs) {
             const int r = (m % C.P) * C.Q + q;
-            if (r != me) snd.push_back(NatMsg{r, p, sa * es});
+            if (r != me || loop) snd.push_back(NatMsg{r, pa_dst + aslot(k - k0, m) * es, sa * es});
           }
-        } else if (m % C.P == C.myrow && qs.count(C.mycol)) {
-          rcv.push_back(NatMsg{src, p, sa * es});
         }
+        if ((src != me || loop) && m % C.P == C.myrow && qs.count(C.mycol)) rcv.push_back(NatMsg{src, p, sa * es});
       }
     for (int k = k0; k < k1; ++k)
       for (int n = 0; n < C.nt; ++n) {   // op(B)(k, n): stored tile (k, n) or (n, k)
@@ -292,11 +314,10 @@ bool nat_dist_gemm_into(NatProgram& PrR, int prec, int tA, int tB, const Scalar&
           pb->add(B.off(si, sj), bslot(k - k0, n), B.rows(si), B.cols(sj));
           for (int pr : ps) {
             const int r = pr * C.Q + n % C.Q;
-            if (r != me) snd.push_back(NatMsg{r, p, sb * es});
+            if (r != me || loop) snd.push_back(NatMsg{r, pb_dst + bslot(k - k0, n) * es, sb * es});
           }
-        } else if (n % C.Q == C.mycol && ps.count(C.myrow)) {
-          rcv.push_back(NatMsg{src, p, sb * es});
         }
+        if ((src != me || loop) && n % C.Q == C.mycol && ps.count(C.myrow)) rcv.push_back(NatMsg{src, p, sb * es});
       }
     if (!pa->upload(*Pr) || !pb->upload(*Pr)) return false;
     const char *a = A.data, *bb = B.data;
@@ -304,8 +325,8 @@ bool nat_dist_gemm_into(NatProgram& PrR, int prec, int tA, int tB, const Scalar&
     int t_pack = -1;
     if (!pa->it.empty() || !pb->it.empty())
       t_pack = Pr->task(0, [=](hipStream_t s) {
-        const int rc = pa->launch(prec, a, lda, wa, amb, s);
-        return rc ? rc : pb->launch(prec, bb, ldb, wb, bmb, s);
+        const int rc = pa->launch(prec, a, lda, pa_dst, amb, s);
+        return rc ? rc : pb->launch(prec, bb, ldb, pb_dst, bmb, s);
       }, {g2, x2, j0, j1, j2});
     const int t_x = add_exchange(*Pr, snd, rcv, {t_pack, g2, j0, j1, j2});
     xch[ch] = either(t_x, ch >= 1 ? xch[ch - 1] : -1);

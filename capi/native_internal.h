@@ -155,7 +155,10 @@ struct NatCtx {
   // multi-process context (dplasma_init_native_dist): rank = myrow * Q + mycol on a P x Q grid
   int rank = 0, world = 1, P = 1, Q = 1, myrow = 0, mycol = 0;
   NatComm* comm = nullptr;
-  bool dist() const { return world > 1; }
+  // loopback rehearsal (DPLASMA_LOOPBACK=1 on a world-1 dist context): the grid builders run with the
+  // rank as the peer of its own tile edges, so the transport (RCCL self send / receive) really executes
+  bool loop = false;
+  bool dist() const { return world > 1 || loop; }
 };
 
 struct NatDesc {
@@ -383,3 +386,6 @@ bool nat_dist_gemm_into(NatProgram& Pr, int prec, int tA, int tB, const Scalar& 
 bool nat_dist_mirror_into(NatProgram& Pr, const NatDesc& A, int uplo, int mtrans, NatDesc& W);
 bool nat_dist_trsm_into(NatProgram& Pr, int side, int uplo, int trans, int diag, const Scalar& alpha, NatDesc& A,
                         NatDesc& B);
+
+// A := al A on this rank's tiles of the uplo part, appended after everything already in P (native.cpp)
+bool nat_add_lascal(NatProgram& P, int uplo, const Scalar& al, NatDesc& A);

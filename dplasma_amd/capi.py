@@ -83,6 +83,8 @@ def desc_get_lapack(desc, addr: int, lda: int) -> int:
 # ----------------------------------------------------------------------------- taskpools
 def new(ctx, name: str, *args):
     """dplasma_<p><op>_New(ctx, args...) -> the taskpool (nothing runs yet)."""
+    if name.startswith("x:"):
+        return _ext(name[2:], True)(ctx, *args)
     return getattr(_api, name + "_New")(ctx, *args)
 
 
@@ -303,9 +305,195 @@ def f77(name: str, *args) -> int:
     raise ValueError(f"unknown ScaLAPACK entry point {name}")
 
 
+# ----------------------------------------------------------------------------- extended entry points
+# (tools/gen_capi.py EXT: QR-tree handles, caller int arrays, butterfly handles, taskpool setters)
+class _CInts:
+    """A caller's int array (int *) as a mutable sequence: reads and writes go to the C memory."""
+
+    def __init__(self, addr: int, n: int):
+        self._a = (ctypes.c_int * max(1, n)).from_address(addr)
+        self._n = n
+
+    def __len__(self):
+        return self._n
+
+    def __getitem__(self, i):
+        if not -self._n <= i < self._n:
+            raise IndexError(i)
+        return self._a[i % self._n]
+
+    def __setitem__(self, i, v):
+        if not -self._n <= i < self._n:
+            raise IndexError(i)
+        self._a[i % self._n] = int(v)
+
+    def __iter__(self):
+        return (self._a[i] for i in range(self._n))
+
+
+def _ints(addr: int, n: int):
+    return _CInts(addr, n) if addr else None
+
+
+def _minmnt(A):
+    return min(A.mt, A.nt)
+
+
+def _x_getrf_qrf(new, p):
+    def f(ctx, tree, A, IPIV, TS, TT, criteria, alpha, lu_tab, INFO):
+        fn = getattr(_api, f"{p}getrf_qrf" + ("_New" if new else ""))
+        r = fn(ctx, tree, A, IPIV, TS, TT, criteria, alpha, _ints(lu_tab, _minmnt(A)), _ints(INFO, 1))
+        return r
+    return f
+
+
+def _x_trsmpl_qrf(new, p):
+    def f(ctx, tree, A, IPIV, B, TS, TT, lu_tab):
+        fn = getattr(_api, f"{p}trsmpl_qrf" + ("_New" if new else ""))
+        return fn(ctx, tree, A, IPIV, B, TS, TT, _ints(lu_tab, _minmnt(A)))
+    return f
+
+
+def _x_hebut(new, p):
+    def f(ctx, A, level):
+        return getattr(_api, f"{p}hebut")(ctx, A, levels=int(level))
+    return f
+
+
+def _x_hetrs(new, p):
+    def f(ctx, uplo, A, B, U_but, level):   # uplo / level: the butterfly carries its own depth
+        return getattr(_api, f"{p}hetrs")(ctx, A, B, U_but=U_but)
+    return f
+
+
+def _x_gebut(new, p):
+    def f(ctx, A, U_but, level):
+        return getattr(_api, f"{p}gebut")(ctx, A, U_but)
+    return f
+
+
+def _x_gebmm(new, p):
+    def f(ctx, A, U_but, level, trans):
+        return getattr(_api, f"{p}gebmm")(ctx, A, U_but, trans)
+    return f
+
+
+def _x_gebrd_ge2gbx(new, p):
+    # the reference's R-bidiag pre-QR (qrtre0, TS0 / TT0) is not performed here: TS0 / TT0 hold the QR
+    # block factors and TS / TT the LQ ones (models/eigen.py gebrd_ge2gbx_New)
+    def f(ctx, ib, qrtre0, qrtree, lqtree, A, TS0, TT0, TS, TT, Band):
+        fn = getattr(_api, f"{p}gebrd_ge2gbx" + ("_New" if new else ""))
+        r = fn(ctx, ib, qrtree if qrtree is not None else qrtre0, lqtree, A, TS0, TT0, TS, TT, Band)
+        return r if new else 0
+    return f
+
+
+def _x_lanm2(new, p):
+    def f(ctx, A, info):   # *info: the power iterations run (negative: not converged)
+        lst = []
+        v = float(getattr(_api, f"{p}lanm2")(ctx, A, info=lst))
+        iv = _ints(info, 1)
+        if iv is not None and lst:
+            iv[0] = lst[0]
+        return v
+    return f
+
+
+def _x_print(new, p):
+    def f(ctx, uplo, A):
+        return getattr(_api, f"{p}print")(ctx, uplo, A)
+    return f
+
+
+_EXT_ADAPT = {"getrf_qrf": _x_getrf_qrf, "trsmpl_qrf": _x_trsmpl_qrf, "hebut": _x_hebut, "hetrs": _x_hetrs,
+              "gebut": _x_gebut, "gebmm": _x_gebmm, "gebrd_ge2gbx": _x_gebrd_ge2gbx, "lanm2": _x_lanm2,
+              "print": _x_print}
+
+
+def _ext(pname: str, new: bool):
+    p, op = pname[0], pname[1:]
+    ad = _EXT_ADAPT.get(op)
+    if ad is not None:
+        return ad(new, p)
+    return getattr(_api, pname + ("_New" if new else ""))
+
+
+def call_obj(ctx, name: str, *args):
+    """An extended entry point returning a framework object to C (an opaque handle)."""
+    return _ext(name[2:] if name.startswith("x:") else name, False)(ctx, *args)
+
+
+def tp_setter(tp, name: str, v: int) -> int:
+    """dplasma_<p>potrf_setrecursive / geqrf_setrecursive on a framework taskpool."""
+    op = name[2:] if name.startswith("x:") else name
+    getattr(_api, op)(tp, int(v))
+    return 0
+
+
+def qrtree_init(kind: str, trans: int, A, ints):
+    """dplasma_hqr_init / systolic_init / svd_init (qr_param.h:120-148) -> the tree object."""
+    from .models import qrtree as qt
+    ints = [int(x) for x in ints]
+    if kind == "hqr":
+        llvl, hlvl, a, p, domino, tsrr = ints
+        return qt.hqr_init(trans, A, llvl=llvl, hlvl=hlvl, a=a, p=p if p > 0 else None, domino=bool(domino),
+                           tsrr=bool(tsrr))
+    if kind == "systolic":
+        return qt.systolic_init(trans, A, p=ints[0], q=ints[1])
+    if kind == "svd":
+        return qt.svd_init(trans, A, hlvl=ints[0], p=ints[1], nbcores_per_node=ints[2], ratio=ints[3])
+    raise ValueError(kind)
+
+
+def qrtree_check(tree) -> int:
+    try:
+        return int(tree.check())
+    except AssertionError as e:
+        print(f"dplasma_qrtree_check: {e}", flush=True)
+        return 1
+
+
+def qrtree_print(tree, what: str, k: int, perm_addr: int, filename: str) -> int:
+    """dplasma_qrtree_print_* (qr_param.h debugging functions): text on stdout, DOT to a file."""
+    kk = range(min(tree.mt, tree.nt))
+    if what == "dag":
+        with open(filename or "qrtree.dot", "w") as f:
+            f.write(tree.dot())
+        return 0
+    if what == "type":
+        out = tree.print_type()
+    elif what == "pivot":
+        out = tree.print_pivot()
+    elif what == "nbgeqrt":
+        out = tree.print_nbgeqrt()
+    elif what == "perm":
+        # the order in which rows are killed at each step (perm[k * mt + i])
+        arr = (ctypes.c_int * (tree.mt * max(1, len(kk)))).from_address(perm_addr) if perm_addr else None
+        lines = []
+        for k_ in kk:
+            order = [k_] + [m for (_, m, _) in reversed(tree.kills(k_))]
+            if arr is not None:
+                for i, m in enumerate(order):
+                    arr[k_ * tree.mt + i] = m
+            lines.append(" ".join(str(m) for m in order))
+        out = "\n".join(lines)
+    elif what in ("next_k", "prev_k"):
+        lines = []
+        for p_ in range(k, tree.mt):
+            f = tree.nextpiv if what == "next_k" else tree.prevpiv
+            lines.append(" ".join("%3d" % f(k, p_, m) for m in range(k, tree.mt + 1)))
+        out = "\n".join(lines)
+    elif what == "geqrt_k":
+        out = " ".join(str(m) for m in tree.heads(k))
+    else:
+        raise ValueError(what)
+    print(out, flush=True)
+    return 0
+
+
 def call(ctx, name: str, *args):
     """Forward one C call: dplasma_<prec><op>(ctx, args...) -> dplasma_amd.<prec><op>(ctx, *args)."""
-    fn = getattr(_api, name)
+    fn = _ext(name[2:], False) if name.startswith("x:") else getattr(_api, name)
     r = fn(ctx, *args)
     if isinstance(r, bool):
         return int(r)

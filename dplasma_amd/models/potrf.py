@@ -94,6 +94,15 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                            or ctx.info.get_int("DPLASMA:GPU:number_of_blocks", 0) > 0):
         from .potrf_ooc import potrf_ooc_New
         return potrf_ooc_New(ctx, uplo, A)
+    # one process, lower, fp64, NB = 512: the whole factorisation as one persistent launch of the device
+    # task runtime (panel work prioritised inside the bulk update's workgroups, models/potrf_dtr.py)
+    eng = os.environ.get("DPLASMA_POTRF_ENGINE", "stream")
+    if eng in ("dtr", "auto"):
+        from . import potrf_dtr
+        if potrf_dtr.supported(ctx, uplo, A):
+            return potrf_dtr.potrf_dtr_New(ctx, uplo, A, info_out)
+        if eng == "dtr":
+            raise ValueError("DPLASMA_POTRF_ENGINE=dtr: needs one GPU process, lower, fp64, NB = 512, N % 512 == 0")
     if (ctx.world > 1 or getattr(ctx, "loopback", False)) and os.environ.get("DPLASMA_POTRF_DIST", "p2p") != "collective":
         # distributed: point-to-point dataflow panel transport (models/potrf_dist.py);
         # DPLASMA_POTRF_DIST=collective keeps the row-broadcast + column-all-gather schedule below

@@ -1,0 +1,329 @@
+"""Cholesky as ONE persistent launch of the device task runtime (``csrc/kernels/dtr.hip``).
+
+The reference's Cholesky is a PTG whose POTRF / TRSM / HERK / GEMM task classes are scheduled by
+PaRSEC with priorities: the panel classes are ``high_priority`` (``src/zpotrf_L.jdf:58-69, 93, 194,
+306``), so a freed core or GPU stream takes panel work before trailing updates.  Stream priorities
+cannot do that on MI355X: the bulk update GEMM holds every CU's VGPRs and LDS, and a panel kernel on a
+high-priority stream is not even dispatched until the GEMM drains (``profiles/r4_prio_probe.txt``).
+This builder compiles the factorisation into a device task table instead:
+
+* tasks (one 256-thread workgroup each): ``POTRF(k, b)`` (row block b of the dataflow tile Cholesky
+  of tile (k, k), then block column b of ``W_k = L_kk^{-T}``; 16 cooperating workgroups),
+  ``TRSM(i, k, r)`` (128-row strip r of L(i, k) = A(i, k) W_k, a GEMM solved in place) and
+  ``UPD(i, j, r, c, k0, nk)`` (128x128 sub-tile of the trailing update by a run of ``nk`` panels);
+* panels are grouped in blocks of ``D`` (the deferred update of ``models/potrf.py``): inside a block
+  each panel updates the block's remaining columns (``NEAR``), and the block then updates every later
+  column with one k-run of ``D`` panels (``BULK``);
+* dependencies are version counters of 128x128 sub-tiles (this builder simulates the sequential
+  program once to know which version each task needs);
+* the high-priority list (ordered by target column, then: the diagonal tile's updates, POTRF, the
+  column's other updates, its TRSM strips) holds every panel task and the updates of the next block's
+  columns; the low-priority lists (one per XCD, tiles of column j on XCD j mod 8, ordered by block
+  then column) hold the rest of the bulk update.  Every workgroup takes the next ready high-priority
+  task before any low-priority one.
+
+One process, lower, fp64, NB = 512, N a multiple of 512 (``supported``); ``models/potrf.py`` uses it
+when ``DPLASMA_POTRF_ENGINE=dtr`` (or ``auto`` and supported).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List
+
+import numpy as np
+import torch
+
+from ..constants import dplasmaLower
+from ..runtime.taskpool import Taskpool
+from ..utils.flops import flops
+
+NBT = 512
+MAXB = 16
+BLK = 32 * 32
+RB = 32
+
+TASK_DT = np.dtype([("type", "<i4"), ("i", "<i4"), ("j", "<i4"), ("k0", "<i4"), ("req_beg", "<i4"),
+                    ("inc", "<i4"), ("r", "<i2"), ("c", "<i2"), ("nk", "<i2"), ("nreq", "<i2")])
+assert TASK_DT.itemsize == 32
+T_UPD, T_TRSM, T_POTRF = 0, 1, 2
+
+
+def supported(ctx, uplo, A) -> bool:
+    if not (ctx.is_gpu and ctx.world == 1 and not getattr(ctx, "loopback", False)):
+        return False
+    if uplo != dplasmaLower or A.dtype != torch.float64 or A.mb != NBT or A.nb != NBT:
+        return False
+    if A.m != A.n or A.m % NBT or A.m == 0 or A.data.device.type != "cuda":
+        return False
+    if getattr(A, "it0", 0) or getattr(A, "jt0", 0):
+        return False
+    si, sj = _strides(A)
+    return si is not None
+
+
+def _strides(A):
+    """(si, sj) with A.offset(i, j) == i * si + j * sj for every tile, or (None, None)."""
+    nt = A.nt
+    si = A.offset(1, 0) - A.offset(0, 0) if nt > 1 else NBT
+    sj = A.offset(0, 1) - A.offset(0, 0) if nt > 1 else NBT * A.ld
+    if A.offset(0, 0) != 0:
+        return None, None
+    for (i, j) in ((nt - 1, 0), (0, nt - 1), (nt - 1, nt - 1), (nt // 2, nt // 3)):
+        if A.offset(i, j) != i * si + j * sj:
+            return None, None
+    return si, sj
+
+
+class _Plan:
+    """The task table of one factorisation (identical for every run of the same shape)."""
+
+    def __init__(self, nt: int, D: int):
+        S = 4 * nt
+        self.nt, self.S, self.D = nt, S, D
+        WB = S * S                      # counter index of W_k's "block columns done" count
+        self.ncnt = WB + nt
+        ver = np.zeros(S * S, dtype=np.int32)
+        F = np.zeros((S, nt), dtype=np.int32)   # strip (I, k) solved: the value of its marker counter
+        chunks, hi_parts, lo_parts = [], [], []
+        ntask = [0]
+
+        def sc(I, J):
+            return np.asarray(I, dtype=np.int64) + np.asarray(J, dtype=np.int64) * S
+
+        def emit(typ, i, j, k0, r, c, nk, inc, reqs, nreq, prio, key=None, xcd=None):
+            n = len(i)
+            t = np.zeros(n, dtype=TASK_DT)
+            t["type"], t["i"], t["j"], t["k0"] = typ, i, j, k0
+            t["r"], t["c"], t["nk"], t["inc"] = r, c, nk, inc
+            ids = np.arange(ntask[0], ntask[0] + n, dtype=np.int64)
+            ntask[0] += n
+            chunks.append((t, reqs, nreq))
+            if prio == "hi":
+                hi_parts.append((key, ids))
+            else:
+                lo_parts.append((xcd, key, ids))
+            return ids
+
+        # sub-tile enumeration of tiles (i, j), i >= j: every (r, c), diagonal tiles only r >= c
+        rr, cc = np.meshgrid(np.arange(4), np.arange(4), indexing="ij")
+        rr, cc = rr.ravel(), cc.ravel()
+        low = rr >= cc
+
+        def subtiles(i, j):
+            """i, j: tile index arrays -> (i, j, r, c) per sub-tile."""
+            i, j = np.asarray(i), np.asarray(j)
+            n = len(i)
+            I = np.repeat(i, 16)
+            J = np.repeat(j, 16)
+            R = np.tile(rr, n)
+            C = np.tile(cc, n)
+            keep = (I != J) | np.tile(low, n)
+            return I[keep], J[keep], R[keep], C[keep]
+
+        def upd(i, j, r, c, k0, nk, prio_hi):
+            """update tasks (arrays) by panels [k0, k0+nk); bumps the sub-tile versions."""
+            n = len(i)
+            width = 1 + 2 * nk
+            reqs = np.full((n, width, 2), -1, dtype=np.int64)
+            Ci = sc(4 * i + r, 4 * j + c)
+            reqs[:, 0, 0], reqs[:, 0, 1] = Ci, ver[Ci]
+            diag = (i == j) & (r == c)
+            for q in range(nk):
+                k = k0 + q
+                a = sc(4 * i + r, 4 * k)
+                b = sc(4 * j + c, 4 * k)
+                reqs[:, 1 + 2 * q, 0], reqs[:, 1 + 2 * q, 1] = a, F[4 * i + r, k]
+                reqs[:, 2 + 2 * q, 0] = np.where(diag, -1, b)
+                reqs[:, 2 + 2 * q, 1] = np.where(diag, -1, F[4 * j + c, k])
+            ver[Ci] += 1
+            kl = k0 + nk - 1
+            if prio_hi:
+                # key: column, phase (0 diagonal tile, 2 other rows), last panel, row, sub-tile
+                key = np.stack([j, np.where(i == j, 0, 2), np.full(n, kl), i, r, c], 1)
+                return emit(T_UPD, i, j, k0, r, c, nk, Ci, reqs, None, "hi", key=key)
+            key = np.stack([np.full(n, kl), j, i, r, c], 1)
+            return emit(T_UPD, i, j, k0, r, c, nk, Ci, reqs, None, "lo", key=key, xcd=j % 8)
+
+        blocks = [(b0, min(nt, b0 + D)) for b0 in range(0, nt, D)]
+        for bi, (k0b, k1b) in enumerate(blocks):
+            for k in range(k0b, k1b):
+                # POTRF(k, b): the diagonal tile's final versions (every update of it precedes)
+                dI, dJ = np.meshgrid(np.arange(4), np.arange(4), indexing="ij")
+                sel = dI >= dJ
+                dsc = sc(4 * k + dI[sel], 4 * k + dJ[sel])
+                reqs = np.full((MAXB, len(dsc), 2), -1, dtype=np.int64)
+                reqs[:, :, 0] = dsc
+                reqs[:, :, 1] = ver[dsc]
+                b = np.arange(MAXB)
+                key = np.stack([np.full(MAXB, k), np.ones(MAXB, int), np.zeros(MAXB, int), b, b * 0, b * 0], 1)
+                emit(T_POTRF, np.full(MAXB, k), np.full(MAXB, k), k, b, 0, 0, WB + k, reqs, None, "hi", key=key)
+                if k + 1 < nt:
+                    # TRSM(i, k, r): W_k complete and every update of strip r of tile (i, k)
+                    ii = np.repeat(np.arange(k + 1, nt), 4)
+                    r = np.tile(np.arange(4), nt - k - 1)
+                    n = len(ii)
+                    reqs = np.full((n, 5, 2), -1, dtype=np.int64)
+                    reqs[:, 0, 0], reqs[:, 0, 1] = WB + k, MAXB
+                    for c in range(4):
+                        s_ = sc(4 * ii + r, 4 * k + c)
+                        reqs[:, 1 + c, 0], reqs[:, 1 + c, 1] = s_, ver[s_]
+                    mark = sc(4 * ii + r, 4 * k)
+                    ver[mark] += 1
+                    F[4 * ii + r, k] = ver[mark]
+                    key = np.stack([np.full(n, k), np.full(n, 3), np.zeros(n, int), ii, r, r * 0], 1)
+                    emit(T_TRSM, ii, np.full(n, k), k, r, 0, 0, mark, reqs, None, "hi", key=key)
+                # NEAR(k): the rest of this block's columns, panel k alone
+                for j in range(k + 1, k1b):
+                    I, J, R, C = subtiles(np.arange(j, nt), np.full(nt - j, j))
+                    upd(I, J, R, C, k, 1, True)
+            if k1b >= nt:
+                continue
+            # BULK(b): every later column, panels of the block as one k-run; the next block's columns
+            # are high priority (the look-ahead), the rest low
+            nk = k1b - k0b
+            hi_end = min(nt, k1b + D)
+            for j in range(k1b, nt):
+                I, J, R, C = subtiles(np.arange(j, nt), np.full(nt - j, j))
+                upd(I, J, R, C, k0b, nk, j < hi_end)
+        # ---- flatten: tasks, requirement pairs (compacted), lists
+        tasks = np.concatenate([c[0] for c in chunks])
+        reqs_all, nreq_all = [], []
+        for t, reqs, _ in chunks:
+            valid = reqs[:, :, 0] >= 0
+            nreq_all.append(valid.sum(1))
+            reqs_all.append(reqs[valid])
+        nreq = np.concatenate(nreq_all)
+        tasks["nreq"] = nreq
+        beg = np.zeros(len(tasks), dtype=np.int64)
+        beg[1:] = np.cumsum(nreq)[:-1]
+        tasks["req_beg"] = beg
+        self.tasks = tasks
+        self.reqs = np.concatenate(reqs_all).astype(np.int32)
+        hk = np.concatenate([k for k, _ in hi_parts])
+        hid = np.concatenate([i for _, i in hi_parts])
+        order = np.lexsort(tuple(hk[:, q] for q in reversed(range(hk.shape[1]))))
+        self.hi = hid[order].astype(np.int32)
+        lo_lists: List[np.ndarray] = []
+        if lo_parts:
+            lx = np.concatenate([np.broadcast_to(x, len(i)) for x, _, i in lo_parts])
+            lk = np.concatenate([k for _, k, _ in lo_parts])
+            lid = np.concatenate([i for _, _, i in lo_parts])
+            for x in range(8):
+                m = lx == x
+                kk = lk[m]
+                o = np.lexsort(tuple(kk[:, q] for q in reversed(range(kk.shape[1]))))
+                lo_lists.append(lid[m][o].astype(np.int32))
+        else:
+            lo_lists = [np.zeros(0, dtype=np.int32) for _ in range(8)]
+        self.lo = np.concatenate(lo_lists) if lo_lists else np.zeros(0, dtype=np.int32)
+        self.lo_off = np.zeros(9, dtype=np.int64)
+        self.lo_off[1:] = np.cumsum([len(x) for x in lo_lists])
+        self.final_ver = ver
+
+
+class _DtrArgs(ctypes.Structure):
+    _fields_ = [("A", ctypes.c_void_p), ("ld", ctypes.c_longlong), ("si", ctypes.c_longlong),
+                ("sj", ctypes.c_longlong), ("nt", ctypes.c_int), ("tasks", ctypes.c_void_p),
+                ("reqs", ctypes.c_void_p), ("cnt", ctypes.c_void_p), ("cur", ctypes.c_void_p),
+                ("hi", ctypes.c_void_p), ("nhi", ctypes.c_int), ("lo", ctypes.c_void_p),
+                ("lo_off", ctypes.c_int * 9), ("W", ctypes.c_void_p), ("Mw", ctypes.c_void_p),
+                ("Sw", ctypes.c_void_p), ("Lp", ctypes.c_void_p), ("Wp", ctypes.c_void_p),
+                ("prog", ctypes.c_void_p), ("epoch", ctypes.c_int), ("info", ctypes.c_void_p)]
+
+
+def _check_layout(lib):
+    """The ctypes image must match the compiled DtrArgs (offsets reported by the library)."""
+    off = (ctypes.c_longlong * 32)()
+    n = lib.dpl_dtr_args_layout(off, 32)
+    names = ["A", "ld", "si", "sj", "nt", "tasks", "reqs", None, "cnt", "cur", "hi", "nhi", "lo", "lo_off", "W",
+             "Mw", "Sw", "Lp", "Wp", "prog", "epoch", "info"]
+    for q, nm in enumerate(names):
+        if nm is None:
+            if off[q] != TASK_DT.itemsize:
+                raise RuntimeError("dtr: DtrTask layout mismatch")
+            continue
+        if getattr(_DtrArgs, nm).offset != off[q]:
+            raise RuntimeError(f"dtr: DtrArgs.{nm} at {getattr(_DtrArgs, nm).offset}, library says {off[q]}")
+    if ctypes.sizeof(_DtrArgs) != off[len(names)]:
+        raise RuntimeError("dtr: DtrArgs size mismatch")
+    PST = int(off[len(names) + 4])
+    return PST
+
+
+_PLANS = {}
+
+
+def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
+    from ..ops import _lib
+    if not supported(ctx, uplo, A):
+        raise ValueError("potrf_dtr: one process, lower, fp64, NB = 512, N a multiple of 512, GPU")
+    lib = _lib.load()
+    PST = _check_layout(lib)
+    nt = A.nt
+    D = max(1, int(os.environ.get("DPLASMA_DTR_DEFER", "4")))
+    key = (nt, D)
+    plan = _PLANS.get(key)
+    if plan is None:
+        plan = _PLANS[key] = _Plan(nt, D)
+    dev = A.device
+    tp = Taskpool("potrf", ctx)
+    tp.flops = flops(A.prec, "potrf", A.n)
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    tp.info = info
+
+    def up(x):
+        return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+    tasks_d = up(plan.tasks.view(np.uint8))
+    reqs_d = up(plan.reqs)
+    hi_d = up(plan.hi)
+    lo_d = up(plan.lo if len(plan.lo) else np.zeros(1, dtype=np.int32))
+    cnt = torch.zeros(plan.ncnt, dtype=torch.int32, device=dev)
+    cur = torch.zeros(9 * PST, dtype=torch.int32, device=dev)
+    # per-panel workspaces (HBM is plentiful: ~6 MB per panel, nothing recycled, no WAR edges)
+    W = torch.zeros(nt * NBT * NBT, dtype=torch.float64, device=dev)
+    Mw = torch.zeros(nt * MAXB * BLK, dtype=torch.float64, device=dev)
+    Sw = torch.zeros(nt * MAXB * RB, dtype=torch.float64, device=dev)
+    Lp = torch.zeros(nt * MAXB * MAXB * BLK, dtype=torch.float64, device=dev)
+    Wp = torch.zeros(nt * MAXB * MAXB * BLK, dtype=torch.float64, device=dev)
+    prog = torch.zeros(nt * 2 * MAXB * PST, dtype=torch.int32, device=dev)
+    si, sj = _strides(A)
+    args = _DtrArgs()
+    args.A, args.ld, args.si, args.sj, args.nt = A.data.data_ptr(), A.ld, si, sj, nt
+    args.tasks, args.reqs, args.cnt, args.cur = tasks_d.data_ptr(), reqs_d.data_ptr(), cnt.data_ptr(), cur.data_ptr()
+    args.hi, args.nhi, args.lo = hi_d.data_ptr(), len(plan.hi), lo_d.data_ptr()
+    for q in range(9):
+        args.lo_off[q] = int(plan.lo_off[q])
+    args.W, args.Mw, args.Sw, args.Lp, args.Wp, args.prog = (W.data_ptr(), Mw.data_ptr(), Sw.data_ptr(),
+                                                             Lp.data_ptr(), Wp.data_ptr(), prog.data_ptr())
+    args.info = info.data_ptr()
+    nbytes = ctypes.sizeof(_DtrArgs)
+    host = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    args_d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    epoch_off = _DtrArgs.epoch.offset
+    state = {"epoch": 0}
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    nwg = int(os.environ.get("DPLASMA_DTR_WG", 2 * ncu))
+    tp._keep = (tasks_d, reqs_d, hi_d, lo_d, cnt, cur, W, Mw, Sw, Lp, Wp, prog, host, args_d)
+    tp.dtr_plan = plan
+
+    def f_run():
+        state["epoch"] = state["epoch"] % ((1 << 25) - 1) + 1
+        args.epoch = state["epoch"]
+        ctypes.memmove(host.data_ptr(), ctypes.addressof(args), nbytes)
+        args_d.copy_(host, non_blocking=True)
+        cnt.zero_()
+        cur.zero_()
+        _lib.check(lib.dpl_dtr_potrf(args_d.data_ptr(), nwg, _lib.stream_ptr()), "dtr_potrf")
+
+    tp.task("DTR_POTRF", "update", f_run)
+
+    def _done():
+        r = int(info.item())
+        if r < 0:
+            raise RuntimeError(f"potrf: device task runtime failure (info {r})")
+        if info_out is not None:
+            info_out[0] = r
+        return r
+    tp.on_complete(_done)
+    return tp.finish_build()

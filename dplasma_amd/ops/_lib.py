@@ -23,6 +23,10 @@ _LOCK = threading.Lock()
 c_int, c_ll, c_ull, c_vp = ctypes.c_int, ctypes.c_longlong, ctypes.c_ulonglong, ctypes.c_void_p
 
 _SIGS = {
+    # device task runtime (dtr.hip): DtrArgs image in device memory, workgroups, stream
+    "dpl_dtr_potrf": [c_vp, c_int, c_vp],
+    "dpl_dtr_args_size": [],
+    "dpl_dtr_args_layout": [c_vp, c_int],
     # prec, transA, transB, nitems, items, kpairs, max_m, max_n, alpha*, A, lda, B, ldb, beta*, C, ldc, vec_ok, generic, stream
     "dpl_gemm_batched": [c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_int, c_vp,
                          c_vp, c_int, c_int, c_int, c_vp],

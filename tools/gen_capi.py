@@ -119,6 +119,174 @@ NATIVE_ALIAS = {
 }
 
 
+# Entry points of the reference API with arguments the main table cannot express (QR-tree handles,
+# caller arrays, butterfly handles, taskpool setters): src/include/dplasma/dplasma_z.h:106-349 and
+# qr_param.h:120-148.  Codes as OPS plus Q (dplasma_qrtree_t *), P (int * of the caller, written back),
+# B (butterfly handle: {T} * in, {T} ** out) and K (dplasma_taskpool_t *).  Each forwards to the
+# framework (dplasma_amd.capi.call "x:<p><op>" / new); native contexts refuse them (no native builder).
+# (op, return, [(code, name)], precisions, has _New, C name override)
+EXT = [
+    ("geqrf_param", "i", [("Q", "qrtree"), ("D", "A"), ("D", "TS"), ("D", "TT")], "sdcz", True),
+    ("gelqf_param", "i", [("Q", "qrtree"), ("D", "A"), ("D", "TS"), ("D", "TT")], "sdcz", True),
+    ("unmqr_param", "i", [("E", "side"), ("E", "trans"), ("Q", "qrtree"), ("D", "A"), ("D", "TS"), ("D", "TT"),
+                          ("D", "C")], "sdcz", True),
+    ("unmlq_param", "i", [("E", "side"), ("E", "trans"), ("Q", "qrtree"), ("D", "A"), ("D", "TS"), ("D", "TT"),
+                          ("D", "C")], "sdcz", True),
+    ("ungqr_param", "i", [("Q", "qrtree"), ("D", "A"), ("D", "TS"), ("D", "TT"), ("D", "Q")], "sdcz", True),
+    ("unglq_param", "i", [("Q", "qrtree"), ("D", "A"), ("D", "TS"), ("D", "TT"), ("D", "Q")], "sdcz", True),
+    ("geqrs_param", "i", [("Q", "qrtree"), ("D", "A"), ("D", "TS"), ("D", "TT"), ("D", "B")], "sdcz", False),
+    ("gelqs_param", "i", [("Q", "qrtree"), ("D", "A"), ("D", "TS"), ("D", "TT"), ("D", "B")], "sdcz", False),
+    ("getrf_qrf", "i", [("Q", "qrtree"), ("D", "A"), ("D", "IPIV"), ("D", "TS"), ("D", "TT"), ("I", "criteria"),
+                        ("R", "alpha"), ("P", "lu_tab"), ("P", "INFO")], "sdcz", True),
+    ("trsmpl_qrf", "i", [("Q", "qrtree"), ("D", "A"), ("D", "IPIV"), ("D", "B"), ("D", "TS"), ("D", "TT"),
+                         ("P", "lu_tab")], "sdcz", True),
+    ("trsmpl_incpiv", "i", [("D", "A"), ("D", "L"), ("D", "IPIV"), ("D", "B")], "sdcz", True),
+    ("trsmpl_ptgpanel", "i", [("D", "A"), ("D", "IPIV"), ("D", "B")], "sdcz", False),
+    ("hebut", "i", [("D", "A"), ("B", "U_but_ptr"), ("I", "level")], "sdcz", False),
+    ("hetrf", "i", [("D", "A")], "sdcz", True),
+    ("hetrs", "i", [("E", "uplo"), ("D", "A"), ("D", "B"), ("B", "U_but_vec"), ("I", "level")], "sdcz", False),
+    ("gebut", "i", [("D", "A"), ("B", "U_but_vec"), ("I", "level")], "sdcz", False),
+    ("gebmm", "i", [("D", "A"), ("B", "U_but_vec"), ("I", "level"), ("E", "trans")], "sdcz", False),
+    ("trdsm", "i", [("D", "A"), ("D", "B")], "sdcz", True),
+    ("trmdm", "i", [("D", "A")], "sdcz", True),
+    ("heev", "i", [("E", "jobz"), ("E", "uplo"), ("D", "A"), ("D", "W"), ("D", "Z")], "sdcz", True),
+    ("herbt", "i", [("E", "uplo"), ("I", "ib"), ("D", "A"), ("D", "T")], "sdcz", True),
+    ("hbrdt", "i", [("D", "A")], "sdcz", False),
+    ("gebrd_ge2gb", "i", [("I", "ib"), ("D", "A"), ("D", "Band")], "sdcz", True),
+    ("gebrd_ge2gbx", "i", [("I", "ib"), ("Q", "qrtre0"), ("Q", "qrtree"), ("Q", "lqtree"), ("D", "A"),
+                           ("D", "TS0"), ("D", "TT0"), ("D", "TS"), ("D", "TT"), ("D", "Band")], "sdcz", True),
+    ("geru", "i", [("S", "alpha"), ("D", "X"), ("D", "Y"), ("D", "A")], "sdcz", True),
+    ("gerc", "i", [("S", "alpha"), ("D", "X"), ("D", "Y"), ("D", "A")], "sdcz", True),
+    ("laswp", "i", [("D", "A"), ("D", "IPIV"), ("I", "inc")], "sdcz", False),
+    ("lanm2", "r", [("D", "A"), ("P", "info")], "sdcz", False),
+    ("pltmg", "i", [("E", "mtxtype"), ("D", "A"), ("U", "seed")], "sdcz", False),
+    ("latms", "i", [("E", "mtxtype"), ("R", "cond"), ("D", "A"), ("U", "seed")], "sdcz", False),
+    ("print", "i", [("E", "uplo"), ("D", "A")], "sdcz", False),
+    ("potrf_setrecursive", "v", [("K", "tp"), ("I", "hmb")], "sdcz", False),
+    ("geqrf_setrecursive", "v", [("K", "tp"), ("I", "hnb")], "sdcz", False),
+]
+
+
+def ext_ctype(code, p):
+    T = CTYPE[p]
+    return {"E": "dplasma_enum_t", "D": "dplasma_desc_t *", "S": T, "R": "double", "I": "int",
+            "U": "unsigned long long", "Q": "dplasma_qrtree_t *", "P": "int *", "B": T + " *",
+            "K": "dplasma_taskpool_t *"}[code]
+
+
+def ext_conv(code, nm, p):
+    if code == "D":
+        return f"dpl_arg_desc({nm})"
+    if code in "EI":
+        return f"dpl_arg_int({nm})"
+    if code == "U":
+        return f"dpl_arg_u64({nm})"
+    if code == "R":
+        return f"dpl_arg_real({nm})"
+    if code == "S":
+        return f"dpl_arg_{'cplx' if p in 'cz' else 'real'}({nm})"
+    if code == "Q":
+        return f"dpl_arg_qrtree({nm})"
+    if code == "P":
+        return f"dpl_arg_ptr({nm})"
+    if code == "B":
+        return f"dpl_arg_obj((const void *){nm})"
+    raise ValueError(code)
+
+
+def gen_ext(h, cpp):
+    """prototypes into h, wrappers into cpp (see EXT)"""
+    h += ["", "/* ---- QR reduction trees (qr_param.h): caller-allocated, filled by an init function; the query",
+          " * functions answer for the tree built by the framework (models/qrtree.py) */",
+          "#define DPLASMA_QR_KILLED_BY_TS 0", "#define DPLASMA_QR_KILLED_BY_LOCALTREE 1",
+          "#define DPLASMA_QR_KILLED_BY_DOMINO 2", "#define DPLASMA_QR_KILLED_BY_DISTTREE 3",
+          "#define DPLASMA_FLAT_TREE 0", "#define DPLASMA_GREEDY_TREE 1", "#define DPLASMA_FIBONACCI_TREE 2",
+          "#define DPLASMA_BINARY_TREE 3", "#define DPLASMA_GREEDY1P_TREE 4",
+          "typedef struct dplasma_qrtree_s dplasma_qrtree_t;",
+          "#ifndef DPLASMA_QRTREE_DEFINED",
+          "#define DPLASMA_QRTREE_DEFINED",
+          "struct dplasma_qrtree_s {",
+          "    int (*getnbgeqrf)(const dplasma_qrtree_t *qrtree, int k);",
+          "    int (*getm)(const dplasma_qrtree_t *qrtree, int k, int i);",
+          "    int (*geti)(const dplasma_qrtree_t *qrtree, int k, int m);",
+          "    int (*gettype)(const dplasma_qrtree_t *qrtree, int k, int m);",
+          "    int (*currpiv)(const dplasma_qrtree_t *qrtree, int k, int m);",
+          "    int (*nextpiv)(const dplasma_qrtree_t *qrtree, int k, int p, int m);",
+          "    int (*prevpiv)(const dplasma_qrtree_t *qrtree, int k, int p, int m);",
+          "    int mt, nt, a, p;",
+          "    void *args;   /* the framework's tree */",
+          "};",
+          "#endif",
+          "int  dplasma_hqr_init(dplasma_qrtree_t *qrtree, dplasma_enum_t trans, dplasma_desc_t *A, int type_llvl,",
+          "                      int type_hlvl, int a, int p, int domino, int tsrr);",
+          "void dplasma_hqr_finalize(dplasma_qrtree_t *qrtree);",
+          "int  dplasma_systolic_init(dplasma_qrtree_t *qrtree, dplasma_enum_t trans, dplasma_desc_t *A, int p, int q);",
+          "void dplasma_systolic_finalize(dplasma_qrtree_t *qrtree);",
+          "int  dplasma_svd_init(dplasma_qrtree_t *qrtree, dplasma_enum_t trans, dplasma_desc_t *A, int type_hlvl,",
+          "                      int p, int nbcores_per_node, int ratio);",
+          "void dplasma_svd_finalize(dplasma_qrtree_t *qrtree);",
+          "int  dplasma_qrtree_check(dplasma_desc_t *A, dplasma_qrtree_t *qrtree);",
+          "void dplasma_qrtree_print_dag(dplasma_desc_t *A, dplasma_qrtree_t *qrtree, char *filename);",
+          "void dplasma_qrtree_print_type(dplasma_desc_t *A, dplasma_qrtree_t *qrtree);",
+          "void dplasma_qrtree_print_pivot(dplasma_desc_t *A, dplasma_qrtree_t *qrtree);",
+          "void dplasma_qrtree_print_nbgeqrt(dplasma_desc_t *A, dplasma_qrtree_t *qrtree);",
+          "void dplasma_qrtree_print_perm(dplasma_desc_t *A, dplasma_qrtree_t *qrtree, int *perm);",
+          "void dplasma_qrtree_print_next_k(dplasma_desc_t *A, dplasma_qrtree_t *qrtree, int k);",
+          "void dplasma_qrtree_print_prev_k(dplasma_desc_t *A, dplasma_qrtree_t *qrtree, int k);",
+          "void dplasma_qrtree_print_geqrt_k(dplasma_desc_t *A, dplasma_qrtree_t *qrtree, int k);",
+          "/* LDL^H butterflies: hebut returns an opaque handle (not the reference's raw vector) that hetrs /",
+          " * gebut / gebmm take; release it with dplasma_but_free */",
+          "void dplasma_but_free(void *U_but_vec);",
+          "/* ---- further entry points (dplasma_z.h:106-349); on a native context they return an error */"]
+    for op, ret, args, precs, has_new, *_ in EXT:
+        for p in precs:
+            cargs = ", ".join(("dplasma_taskpool_t *tp" if c == "K" else
+                               f"{ext_ctype(c, p)}{'*' if c == 'B' and op == 'hebut' else ''}"
+                               f"{'' if ext_ctype(c, p).endswith('*') else ' '}{nm}") for c, nm in args)
+            rt = {"i": "int", "r": "double", "v": "void"}[ret]
+            if args[0][0] == "K":
+                proto = f"{rt} dplasma_{p}{op}({cargs})"
+            else:
+                proto = f"{rt} dplasma_{p}{op}(dplasma_context_t *ctx, {cargs})"
+            h.append(proto + ";")
+            if has_new:
+                nargs = cargs
+                h.append(f"dplasma_taskpool_t *dplasma_{p}{op}_New(dplasma_context_t *ctx, {nargs});")
+                h.append(f"void dplasma_{p}{op}_Destruct(dplasma_taskpool_t *tp);")
+            # ---- wrappers
+            conv = ", ".join(ext_conv(c, nm, p) for c, nm in args if c != "K")
+            if op == "hebut":   # handle out: the framework returns the butterfly object
+                cpp.append(f'extern "C" DPL_CAPI {proto} {{ if (dpl_native(ctx)) return nat_unsupported("{p}{op}"); '
+                           f'DplGil g; return dpl_call_obj_out(ctx, "x:{p}{op}", (void **)U_but_ptr, '
+                           f'{{dpl_arg_desc(A), dpl_arg_int(level)}}); }}')
+                continue
+            if args[0][0] == "K":
+                cpp.append(f'extern "C" DPL_CAPI {proto} {{ dpl_tp_setter(tp, "x:{p}{op}", {args[1][1]}); }}')
+                continue
+            if ret == "r":
+                call = f'dpl_call_real(ctx, "x:{p}{op}", {{{conv}}})'
+                cpp.append(f'extern "C" DPL_CAPI {proto} {{ if (dpl_native(ctx)) return (nat_unsupported("{p}{op}"), NAN); '
+                           f'DplGil g; return {call}; }}')
+            else:
+                call = f'dpl_call_int(ctx, "x:{p}{op}", {{{conv}}})'
+                cpp.append(f'extern "C" DPL_CAPI {proto} {{ if (dpl_native(ctx)) return nat_unsupported("{p}{op}"); '
+                           f'DplGil g; return {call}; }}')
+            if has_new:
+                cpp.append(f'extern "C" DPL_CAPI dplasma_taskpool_t *dplasma_{p}{op}_New(dplasma_context_t *ctx, {cargs}) '
+                           f'{{ if (dpl_native(ctx)) {{ nat_unsupported("{p}{op}"); return nullptr; }} '
+                           f'DplGil g; return dpl_call_new(ctx, "x:{p}{op}", {{{conv}}}); }}')
+                cpp.append(f'extern "C" DPL_CAPI void dplasma_{p}{op}_Destruct(dplasma_taskpool_t *tp) '
+                           '{ dplasma_taskpool_free(tp); }')
+
+
+# blocking solves run as two programs: the solve only when the factorisation returned info == 0, so a
+# failed factorisation leaves B untouched (reference: src/zposv_wrapper.c:102-104, zgesv_1d_wrapper.c)
+TWO_PHASE = {
+    "posv": ("potrf", "uplo, A", "potrs", "uplo, A, B"),
+    "gesv_1d": ("getrf_1d", "A, IPIV", "getrs", "111 /* NoTrans */, A, IPIV, B"),
+}
+
+
 def enums():
     from dplasma_amd import constants as C
     out = []
@@ -275,6 +443,10 @@ def main():
                 nat_call = f"nat_{nop}(ctx, {PCODE[p]}, {nat})"
                 pre = f"if (dpl_native(ctx)) return nat_execute(ctx, {nat_call}); "
                 pre_new = f"if (dpl_native(ctx)) return nat_wrap({nat_call}); "
+                if op in TWO_PHASE:
+                    f1, a1, f2, a2 = TWO_PHASE[op]
+                    pre = (f"if (dpl_native(ctx)) {{ const int info = nat_execute(ctx, nat_{f1}(ctx, {PCODE[p]}, {a1})); "
+                           f"return info != 0 ? info : nat_execute(ctx, nat_{f2}(ctx, {PCODE[p]}, {a2})); }} ")
             else:
                 miss = f'nat_unsupported("{p}{op}")'
                 pre = (f"if (dpl_native(ctx)) return {miss}; " if ret == "i"
@@ -289,6 +461,12 @@ def main():
                            f"{{ {pre_new}DplGil g; return dpl_call_new(ctx, \"{p}{op}\", {{{', '.join(conv)}}}); }}")
                 cpp.append(f"extern \"C\" DPL_CAPI void dplasma_{p}{op}_Destruct(dplasma_taskpool_t *tp) "
                            "{ dplasma_taskpool_free(tp); }")
+    ext_cpp = ['// Generated by tools/gen_capi.py: the EXT entry points (QR-tree handles, caller arrays, butterfly',
+               '// handles, taskpool setters) forwarded to dplasma_amd.capi ("x:<p><op>").',
+               '#include "capi_bridge.h"', "#include <cmath>", "",
+               'extern "C" void dplasma_taskpool_free(dplasma_taskpool_t *tp);']
+    gen_ext(h, ext_cpp)
+    (ROOT / "capi" / "dplasma_ext.cpp").write_text("\n".join(ext_cpp) + "\n")
     h += ["", "#ifdef __cplusplus", "}", "#endif", "#endif", ""]
     (inc / "dplasma.h").write_text("\n".join(h))
     cpp = cpp[:4] + cpp_head + cpp[4:]
