@@ -76,6 +76,7 @@ struct DtrArgs {
   int* prog;                // nt x 2 x MAXB x PSTRIDE: tile-step flags, then W-column flags
   int epoch;
   int* info;
+  long long* trace;         // optional (DPLASMA_DTR_TRACE): per task {start, end, wg << 8 | xcd}, 100 MHz ticks
 };
 
 constexpr int NBT = 512;    // tile size
@@ -353,6 +354,8 @@ __global__ __launch_bounds__(256, 2) void k_dtr_potrf(const DtrArgs* __restrict_
       continue;
     }
     nap = 1;
+    long long t_start = 0;
+    if (g.trace && tid == 0) t_start = (long long)__builtin_amdgcn_s_memrealtime();
     const DtrTask tk = g.tasks[t];
     if (tk.type == T_UPD) run_upd(gp, t);
     else if (tk.type == T_TRSM) run_trsm(gp, t);
@@ -360,6 +363,12 @@ __global__ __launch_bounds__(256, 2) void k_dtr_potrf(const DtrArgs* __restrict_
     // release: every wave's stores drained, then one agent-scope release and the counter bump
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (tid == 0 && g.trace) {
+      long long* tr = g.trace + 3 * (size_t)t;
+      tr[0] = t_start;
+      tr[1] = (long long)__builtin_amdgcn_s_memrealtime();
+      tr[2] = ((long long)blockIdx.x << 8) | xcd;
+    }
     if (tid == 0 && tk.inc >= 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -391,7 +400,8 @@ DPL_API int dpl_dtr_args_layout(long long* off, int n) {
       (long long)offsetof(DtrArgs, nhi),    (long long)offsetof(DtrArgs, lo),     (long long)offsetof(DtrArgs, lo_off),
       (long long)offsetof(DtrArgs, W),      (long long)offsetof(DtrArgs, Mw),     (long long)offsetof(DtrArgs, Sw),
       (long long)offsetof(DtrArgs, Lp),     (long long)offsetof(DtrArgs, Wp),     (long long)offsetof(DtrArgs, prog),
-      (long long)offsetof(DtrArgs, epoch),  (long long)offsetof(DtrArgs, info),   (long long)sizeof(DtrArgs),
+      (long long)offsetof(DtrArgs, epoch),  (long long)offsetof(DtrArgs, info),   (long long)offsetof(DtrArgs, trace),
+      (long long)sizeof(DtrArgs),
       (long long)MAXB, (long long)BLK, (long long)RB, (long long)PSTRIDE};
   const int m = (int)(sizeof(v) / sizeof(v[0]));
   for (int q = 0; q < n && q < m; ++q) off[q] = v[q];

@@ -168,9 +168,12 @@ class _GetrfDev:
       "percol" -- the distributed pivoting driven from the host (one all-gather and two host
                syncs per column; kept as the transport-independent reference of "dist")."""
 
-    def __init__(self, ctx, A, info, pivot: bool = True):
+    def __init__(self, ctx, A, info, pivot: bool = True, trailing_only: bool = False):
         self.ctx, self.A, self.info = ctx, A, info
         self.pivot = pivot   # False: getrf_nopiv (same task structure, no interchanges)
+        # trailing_only: step k's interchanges touch tile columns >= k only (the hybrid LU-QR keeps every
+        # earlier step's factor in its own row order, models/lu_qr.py)
+        self.trailing_only = trailing_only
         dev = self.dev = A.device
         mb, nb = A.mb, A.nb
         g = A.grid
@@ -529,11 +532,11 @@ class _GetrfDev:
             par = k & 1
             mdst, msrc, mcnt = self.mdst[par], self.msrc[par], self.mcnt[par]
             ldb = 2 * A.nb
-            nl = self.nleft[k] if self.side is not None else 0
+            nl = self.nleft[k] if (self.side is not None or self.trailing_only) else 0
             cur = torch.cuda.current_stream() if self.side is not None else None
             if cur is not None and self.ev_side[par] is not None:
                 cur.wait_event(self.ev_side[par])      # step k-2's side moves have read these lists
-            if nl:
+            if nl and self.side is not None:
                 ev = torch.cuda.Event()
                 ev.record(cur)                           # lists ready, left columns final (back(k-1))
                 with torch.cuda.stream(self.side):

@@ -40,6 +40,8 @@ TSMQR / TTMQR batched kernels, models/qr.py).
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -135,7 +137,53 @@ class _GetrfQrf(Taskpool):
         self.flops = flops(A.prec, "getrf", A.m, A.n)
         if criteria == RANDOM_CRITERIUM:
             genrandom_lutab(self.lu_tab, 0, self.minMNT - 1, int(round(self.minMNT * self.alpha / 100.0)), 0)
+        # Device-resident path (one process, domain = the whole panel column, a criterion that does not
+        # read the matrix): every step is issued without a host synchronisation -- LU steps on the
+        # partial-pivoting engine of getrf_1d (models/lu.py _GetrfDev: device pivot search, device row
+        # moves, MFMA updates; interchanges restricted to the trailing columns), QR steps on the
+        # stacked-domain engine -- and no LU is factored for a step that will be QR.  An exactly singular
+        # diagonal domain is reported through info at completion instead of turning that step into QR
+        # (DPLASMA_LUQR_SYNC=1 keeps the reference's per-step host decision).
+        self.fast = None
+        fast_env = os.environ.get("DPLASMA_LUQR_FAST", "auto")   # auto: on GPU; 1: also on CPU; 0: never
+        if (ctx.world == 1 and self.p == 1 and fast_env != "0" and (A.device.type == "cuda" or fast_env == "1")
+                and self._a_priori(0) is not None and os.environ.get("DPLASMA_LUQR_SYNC", "0") != "1"):
+            from .lu import _GetrfDev
+            self.fast_info = torch.zeros(1, dtype=torch.int32, device=A.device)
+            self.fast = _GetrfDev(ctx, A, self.fast_info, pivot=True, trailing_only=True)
         self.finish_build()
+
+    def _a_priori(self, k):
+        """The step's choice when it does not depend on the data (1 LU, 0 QR), else None."""
+        if self.alpha == 0:
+            return 0
+        if self.alpha >= 9999999999:
+            return 1
+        c = self.criteria
+        if c == LU_ONLY_CRITERIUM:
+            return 1
+        if c == QR_ONLY_CRITERIUM:
+            return 0
+        if c == RANDOM_CRITERIUM:
+            return int(self.lu_tab[k])
+        if c in _HIGHAMS or c == MUMPS_CRITERIUM:
+            return None
+        return k % 2
+
+    def _run_fast(self):
+        A, dev = self.A, self.fast
+        for k in range(self.minMNT):
+            cond = self._a_priori(k)
+            self.lu_tab[k] = cond
+            if cond:
+                dev.step(k)
+                kmin = dev.plan[k]["kmin"]
+                if self.IPIV.is_local(k, k):
+                    t = self.IPIV.tile(k, k)
+                    t.zero_()
+                    t[:kmin, 0] = dev.piv_dev[:kmin] + 1
+            else:
+                self._qr_step(_Step(A, k, self.p))
 
     # ------------------------------------------------------------------ one panel
     def _domain_lu(self, st: _Step):
@@ -350,6 +398,11 @@ class _GetrfQrf(Taskpool):
         self._t_run = time.perf_counter()
         A = self.A
         ctx = self.ctx
+        if self.fast is not None:
+            self._run_fast()
+            if self.info_out is not None:
+                self.info_out[0] = 0
+            return
         for k in range(self.minMNT):
             st = _Step(A, k, self.p)
             mine = self._domain_lu(st) if ctx.rank == st.owner else None
@@ -367,8 +420,11 @@ class _GetrfQrf(Taskpool):
             torch.cuda.current_stream(self.ctx.device).synchronize()
         if self.qpf is not None and int(self.qpf.info.item()) != 0:
             raise RuntimeError(f"getrf_qrf: QR panel kernel reported {int(self.qpf.info.item())}")
-        self._result = 0
-        return 0
+        r = int(self.fast_info.item()) if self.fast is not None else 0
+        if self.info_out is not None:
+            self.info_out[0] = r
+        self._result = r
+        return r
 
 
 def getrf_qrf_New(ctx, qrtree_, A, IPIV, TS, TT, criteria=DEFAULT_CRITERIUM, alpha=1.0, lu_tab=None, INFO=None,

@@ -229,7 +229,8 @@ class _DtrArgs(ctypes.Structure):
                 ("hi", ctypes.c_void_p), ("nhi", ctypes.c_int), ("lo", ctypes.c_void_p),
                 ("lo_off", ctypes.c_int * 9), ("W", ctypes.c_void_p), ("Mw", ctypes.c_void_p),
                 ("Sw", ctypes.c_void_p), ("Lp", ctypes.c_void_p), ("Wp", ctypes.c_void_p),
-                ("prog", ctypes.c_void_p), ("epoch", ctypes.c_int), ("info", ctypes.c_void_p)]
+                ("prog", ctypes.c_void_p), ("epoch", ctypes.c_int), ("info", ctypes.c_void_p),
+                ("trace", ctypes.c_void_p)]
 
 
 def _check_layout(lib):
@@ -237,7 +238,7 @@ def _check_layout(lib):
     off = (ctypes.c_longlong * 32)()
     n = lib.dpl_dtr_args_layout(off, 32)
     names = ["A", "ld", "si", "sj", "nt", "tasks", "reqs", None, "cnt", "cur", "hi", "nhi", "lo", "lo_off", "W",
-             "Mw", "Sw", "Lp", "Wp", "prog", "epoch", "info"]
+             "Mw", "Sw", "Lp", "Wp", "prog", "epoch", "info", "trace"]
     for q, nm in enumerate(names):
         if nm is None:
             if off[q] != TASK_DT.itemsize:
@@ -297,6 +298,12 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     args.W, args.Mw, args.Sw, args.Lp, args.Wp, args.prog = (W.data_ptr(), Mw.data_ptr(), Sw.data_ptr(),
                                                              Lp.data_ptr(), Wp.data_ptr(), prog.data_ptr())
     args.info = info.data_ptr()
+    # DPLASMA_DTR_TRACE=1: per-task {start, end, workgroup << 8 | xcd} (s_memrealtime, 100 MHz) in tp.dtr_trace
+    trace = None
+    if os.environ.get("DPLASMA_DTR_TRACE", "0") == "1":
+        trace = torch.zeros(3 * len(plan.tasks), dtype=torch.int64, device=dev)
+        args.trace = trace.data_ptr()
+    tp.dtr_trace = trace
     nbytes = ctypes.sizeof(_DtrArgs)
     host = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
     args_d = torch.empty(nbytes, dtype=torch.uint8, device=dev)

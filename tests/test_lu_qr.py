@@ -96,3 +96,25 @@ def test_gpu_getrf_qrf(crit):
     g = dp.init(device="cuda:0")
     a0, b0, B, lu_tab = _solve(g, torch.float64, 1000, 128, 32, crit, 1.0, 2)
     assert _resid(a0.cpu(), b0.cpu(), B.to_dense_local().cpu(), "d") < 60
+
+
+@pytest.mark.parametrize("crit,alpha", [(dp.DEFAULT_CRITERIUM, 1.0), (dp.RANDOM_CRITERIUM, 50.0),
+                                        (dp.LU_ONLY_CRITERIUM, 1.0), (dp.HIGHAM_SUM_CRITERIUM, 0.0)])
+def test_getrf_qrf_device_path_cpu(ctx, monkeypatch, crit, alpha):
+    """The host-sync-free path (p = 1, a criterion fixed in advance): LU steps on the getrf_1d engine with
+    trailing-only interchanges, QR steps on the tree; same solve accuracy and the same lu_tab as the
+    per-step path."""
+    monkeypatch.setenv("DPLASMA_LUQR_FAST", "1")
+    a0, b0, B, lu_tab = _solve(ctx, torch.float64, 300, 64, 16, crit, alpha, 1)
+    assert _resid(a0, b0, B.to_dense_local(), "d") < 60
+    monkeypatch.setenv("DPLASMA_LUQR_FAST", "0")
+    _, _, _, lu_tab2 = _solve(ctx, torch.float64, 300, 64, 16, crit, alpha, 1)
+    assert lu_tab == lu_tab2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("crit,alpha", [(dp.DEFAULT_CRITERIUM, 1.0), (dp.RANDOM_CRITERIUM, 50.0)])
+def test_gpu_getrf_qrf_device_path(crit, alpha):
+    g = dp.init(device="cuda:0")
+    a0, b0, B, lu_tab = _solve(g, torch.float64, 1536, 256, 32, crit, alpha, 1)
+    assert _resid(a0.cpu(), b0.cpu(), B.to_dense_local().cpu(), "d") < 60

@@ -1,0 +1,73 @@
+"""Per-task timeline of the device task runtime Cholesky (DPLASMA_DTR_TRACE=1).
+
+  python tools/gpu/dtr_trace_run.py N [out.npz]
+
+Prints, per task kind, the count and the mean / total duration; the workgroup occupancy (busy time
+over 2 x #CUs workgroups x span); and per panel k the critical chain: POTRF(k) span (first start of
+its 16 workgroups -> last end), its TRSM strips' span, and the gap from the last update of column k+1
+to POTRF(k+1)'s start.
+"""
+import os
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
+os.environ["DPLASMA_DTR_TRACE"] = "1"
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import dplasma_amd as dp  # noqa: E402
+from dplasma_amd.models import potrf_dtr as D  # noqa: E402
+
+
+def main():
+    N = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+    out = sys.argv[2] if len(sys.argv) > 2 else None
+    ctx = dp.init()
+    A = dp.block_cyclic(ctx, torch.float64, 512, 512, N, N)
+    dp.dplghe(ctx, float(N), dp.dplasmaLower, A, 3872)
+    A0 = A.data.clone()
+    tp = D.potrf_dtr_New(ctx, dp.dplasmaLower, A)
+    for _ in range(2):
+        A.data.copy_(A0)
+        tp.execute(ctx)
+    torch.cuda.synchronize()
+    tr = tp.dtr_trace.view(-1, 3).cpu().numpy()
+    plan = tp.dtr_plan
+    T = plan.tasks
+    s, e, who = tr[:, 0], tr[:, 1], tr[:, 2]
+    t0 = s.min()
+    span = (e.max() - t0) / 100.0   # us
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    nwg = 2 * ncu
+    dur = (e - s) / 100.0
+    print(f"N={N} tasks={len(T)} span={span / 1e3:.2f} ms  ({tp.flops / (span * 1e-6) / 1e12:.2f} TF/s)")
+    names = {D.T_UPD: "UPD", D.T_TRSM: "TRSM", D.T_POTRF: "POTRF"}
+    busy = dur.sum()
+    print(f"workgroup occupancy: {busy / (nwg * span) * 100:.1f} % of {nwg} workgroups x span")
+    for ty, nm in names.items():
+        m = T["type"] == ty
+        if ty == D.T_UPD:
+            for nk in sorted(set(T["nk"][m].tolist())):
+                mm = m & (T["nk"] == nk)
+                print(f"  {nm}(nk={nk}): {mm.sum():8d} tasks  mean {dur[mm].mean():8.1f} us  total {dur[mm].sum() / 1e3:9.1f} ms")
+        else:
+            print(f"  {nm:9s}: {m.sum():8d} tasks  mean {dur[m].mean():8.1f} us  total {dur[m].sum() / 1e3:9.1f} ms")
+    # per-panel chain
+    nt = plan.nt
+    print(" k | POTRF start..end (us from t0) | TRSM first..last end | wait before POTRF")
+    prev_end = 0.0
+    for k in range(min(nt, 24)):
+        mp = (T["type"] == D.T_POTRF) & (T["k0"] == k)
+        mt_ = (T["type"] == D.T_TRSM) & (T["k0"] == k)
+        ps, pe = (s[mp].min() - t0) / 100.0, (e[mp].max() - t0) / 100.0
+        ts_, te = ((s[mt_].min() - t0) / 100.0, (e[mt_].max() - t0) / 100.0) if mt_.any() else (pe, pe)
+        print(f"{k:3d} | {ps:10.1f} .. {pe:10.1f} ({pe - ps:7.1f}) | {ts_:10.1f} .. {te:10.1f} ({te - ts_:7.1f}) | "
+              f"{ps - prev_end:8.1f}")
+        prev_end = te
+    if out:
+        np.savez(out, trace=tr, tasks=T.view(np.uint8), nt=nt)
+
+
+if __name__ == "__main__":
+    main()
