@@ -138,6 +138,12 @@ NatProgram* nat_ungqr(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplas
 NatProgram* nat_geqrs(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* T, dplasma_desc_t* B);
 NatProgram* nat_gels(dplasma_context_t* ctx, int prec, int trans, dplasma_desc_t* A, dplasma_desc_t* T,
                      dplasma_desc_t* B);
+NatProgram* nat_getrf_nopiv(dplasma_context_t* ctx, int prec, dplasma_desc_t* A);
+NatProgram* nat_gelqf(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* T);
+NatProgram* nat_unmlq(dplasma_context_t* ctx, int prec, int side, int trans, dplasma_desc_t* A, dplasma_desc_t* T,
+                      dplasma_desc_t* C);
+NatProgram* nat_unglq(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* T, dplasma_desc_t* Q);
+NatProgram* nat_gelqs(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* T, dplasma_desc_t* B);
 int nat_execute(dplasma_context_t* ctx, NatProgram* P);     // run + wait + info, frees P
 dplasma_taskpool_t* nat_wrap(NatProgram* P);
 void nat_fini(dplasma_context_t* ctx);

@@ -1369,20 +1369,21 @@ struct LuScratch {
 
 // the dgetrf2 recursion of ops.PanelLU on the panel pv (m x n, ld): tasks on stream 1 after prev
 int add_panel_lu(NatProgram& P, int prec, char* pv, int ld, int m, int c0, int n, const LuScratch& S, int* info,
-                 int info_base, int prev) {
+                 int info_base, int prev, bool pivot = true) {
   const Scalar one(prec, 1.0), m_one(prec, -1.0);
   int* piv = (int*)S.piv->p;
   void* ws = S.ws->p;
   int* cnt = (int*)S.cnt->p;
   if (n <= LU_BW) {
     return P.task(1, [=](hipStream_t s) {
-      return dpl_lu_block(prec, pv, ld, m, c0, c0 + n, piv, ws, cnt, info, info_base, 1, s);
+      return dpl_lu_block(prec, pv, ld, m, c0, c0 + n, piv, ws, cnt, info, info_base, pivot ? 1 : 0, s);
     }, {prev});
   }
   const int n1 = (n / 2 + 15) / 16 * 16, c1 = c0 + n1;
-  prev = add_panel_lu(P, prec, pv, ld, m, c0, n1, S, info, info_base, prev);
+  prev = add_panel_lu(P, prec, pv, ld, m, c0, n1, S, info, info_base, prev, pivot);
   if (prev < 0) return prev;
-  prev = P.task(1, [=](hipStream_t s) { return dpl_laswp_panel(prec, pv, ld, c1, c0 + n, piv, c0, c1, s); }, {prev});
+  if (pivot)
+    prev = P.task(1, [=](hipStream_t s) { return dpl_laswp_panel(prec, pv, ld, c1, c0 + n, piv, c0, c1, s); }, {prev});
   auto tr = std::make_shared<Trsm1>();
   tr->tri = c0 + (long long)c0 * ld;
   tr->add(c0 + (long long)c1 * ld, n1, n - n1);
@@ -1399,8 +1400,8 @@ int add_panel_lu(NatProgram& P, int prec, char* pv, int ld, int m, int c0, int n
       return g->launch(prec, NOTRANS, NOTRANS, m_one, pv, ld, pv, ld, one, pv, ld, s);
     }, {prev});
   }
-  prev = add_panel_lu(P, prec, pv, ld, m, c1, n - n1, S, info, info_base, prev);
-  if (prev < 0) return prev;
+  prev = add_panel_lu(P, prec, pv, ld, m, c1, n - n1, S, info, info_base, prev, pivot);
+  if (prev < 0 || !pivot) return prev;
   return P.task(1, [=](hipStream_t s) { return dpl_laswp_panel(prec, pv, ld, c0, c1, piv, c1, c0 + n, s); }, {prev});
 }
 
@@ -1446,7 +1447,9 @@ int add_row_moves(NatProgram& P, const NatDesc& B, const LuScratch& S, const Dev
   }, {prev});
 }
 
-bool add_getrf(NatProgram& P, NatDesc& A, NatDesc& IP, int& last) {
+// IP == nullptr: getrf_nopiv (the same panel recursion and updates without interchanges)
+bool add_getrf(NatProgram& P, NatDesc& A, NatDesc* IP, int& last) {
+  const bool pivot = IP != nullptr;
   const int prec = A.prec, mb = A.mb, ld = A.lld;
   const int kt = std::min(A.mt, A.nt);
   LuScratch S;
@@ -1454,7 +1457,7 @@ bool add_getrf(NatProgram& P, NatDesc& A, NatDesc& IP, int& last) {
   char* a = A.data;
   char* pvb = (char*)S.pv->p;
   int* info = (int*)P.info->p;
-  int* ipg = (int*)IP.data;
+  int* ipg = pivot ? (int*)IP->data : nullptr;
   const Scalar one(prec, 1.0), m_one(prec, -1.0), zero(prec, 0.0);
   int prev = last;
   for (int k = 0; k < kt; ++k) {
@@ -1472,12 +1475,13 @@ bool add_getrf(NatProgram& P, NatDesc& A, NatDesc& IP, int& last) {
       return dpl_geadd(prec, 0, NOTRANS, gat->n(), gat->items(), gat->mm, gat->nn, one.ptr(), a, ld, zero.ptr(), pvb,
                        mp, 1, s);
     }, {prev});
-    prev = add_panel_lu(P, prec, pvb, mp, mp, 0, kmin, S, info, r0, prev);
+    prev = add_panel_lu(P, prec, pvb, mp, mp, 0, kmin, S, info, r0, prev, pivot);
     if (prev < 0) return false;
     if (kb > kmin) {   // wide last panel: the columns past the last row get the swaps and U = L^-1 A
       const int* piv = (const int*)S.piv->p;
-      prev = P.task(1, [=](hipStream_t s) { return dpl_laswp_panel(prec, pvb, mp, kmin, kb, piv, 0, kmin, s); },
-                    {prev});
+      if (pivot)
+        prev = P.task(1, [=](hipStream_t s) { return dpl_laswp_panel(prec, pvb, mp, kmin, kb, piv, 0, kmin, s); },
+                      {prev});
       auto tr = std::make_shared<Trsm1>();
       tr->tri = 0;
       tr->add((long long)kmin * mp, kmin, kb - kmin);
@@ -1488,8 +1492,10 @@ bool add_getrf(NatProgram& P, NatDesc& A, NatDesc& IP, int& last) {
     }
     // pivots -> IPIV (1-based, global); net row moves on every tile column; factored panel back
     const int* piv = (const int*)S.piv->p;
-    prev = P.task(1, [=](hipStream_t s) { return dpl_ipiv_shift(piv, ipg + r0, kmin, r0 + 1, s); }, {prev});
-    prev = add_row_moves(P, A, S, S.rowoff, S.coloff, S.ncols, r0, kmin, false, prev);
+    if (pivot) {
+      prev = P.task(1, [=](hipStream_t s) { return dpl_ipiv_shift(piv, ipg + r0, kmin, r0 + 1, s); }, {prev});
+      prev = add_row_moves(P, A, S, S.rowoff, S.coloff, S.ncols, r0, kmin, false, prev);
+    }
     prev = P.task(1, [=](hipStream_t s) {
       return dpl_geadd(prec, 0, NOTRANS, back->n(), back->items(), back->mm, back->nn, one.ptr(), pvb, mp, zero.ptr(),
                        a, ld, 1, s);
@@ -1793,7 +1799,7 @@ NatProgram* nat_getrf_1d(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, d
   if (!lu_conform(A, IP)) return fail(nullptr, "getrf_1d: square tiles <= 512 and an IPIV of min(M, N) entries");
   NatProgram* P = new_program(c, "getrf_1d", true);
   int last = -1;
-  if (!P->info || !(c->dist() ? add_getrf_dist(*P, *A, *IP) : add_getrf(*P, *A, *IP, last)))
+  if (!P->info || !(c->dist() ? add_getrf_dist(*P, *A, *IP) : add_getrf(*P, *A, IP, last)))
     return fail(P, "getrf_1d: device allocation failed");
   return P;
 }
@@ -1825,8 +1831,20 @@ NatProgram* nat_gesv_1d(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dp
   NatProgram* P = new_program(c, "gesv_1d", true);
   int last = -1;
   const bool ok = c->dist() ? add_getrf_dist(*P, *A, *IP) && add_getrs_dist(*P, *A, *IP, *B)
-                            : add_getrf(*P, *A, *IP, last) && add_getrs(*P, NOTRANS, *A, *IP, *B, last);
+                            : add_getrf(*P, *A, IP, last) && add_getrs(*P, NOTRANS, *A, *IP, *B, last);
   if (!P->info || !ok) return fail(P, "gesv_1d: device allocation failed");
+  return P;
+}
+
+// LU without pivoting (models/lu.py getrf_nopiv; reference src/zgetrf_nopiv.jdf): one process
+NatProgram* nat_getrf_nopiv(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA) {
+  NatCtx* c = ctx->nat;
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!same_ctx(c, {A}, prec)) return fail(nullptr, "getrf_nopiv: a descriptor of another context or precision");
+  if (A->mb != A->nb || A->mb > 512) return fail(nullptr, "getrf_nopiv: square tiles <= 512");
+  NatProgram* P = new_program(c, "getrf_nopiv", true);
+  int last = -1;
+  if (!P->info || !add_getrf(*P, *A, nullptr, last)) return fail(P, "getrf_nopiv: device allocation failed");
   return P;
 }
 
@@ -2128,16 +2146,178 @@ NatProgram* nat_geqrs(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dpla
   return P;
 }
 
+// ----------------------------------------------------------------------------- LQ (flat tree)
+// A = L Q is the conjugate transpose of the QR factorization A^H = Q_r R (L = R^H, Q = Q_r^H, the same
+// reflectors and T factors; LAPACK's row-stored conj(v) is exactly column v of Q_r conjugate-transposed).
+// So the LQ family runs the QR engine above on W = A^H, one process: gelqf transposes A into W, factors W,
+// transposes back; unmlq / unglq / gelqs rebuild W from the factored A and apply Q_r with the side and
+// the transposition flipped.  The two O(MN) transposes are one launch each beside the O(MN min(M, N))
+// factorization.  (models/lq.py is the tile-DAG version; reference src/zgelqf.jdf, zunmlq*.jdf.)
+namespace {
+
+// W := op-shaped work matrix of S^H (S.n x S.m, square tiles)
+std::shared_ptr<NatDesc> ctrans_desc(NatProgram& P, const NatDesc& S) {
+  auto w = std::make_shared<NatDesc>();
+  w->ctx = S.ctx;
+  w->prec = S.prec;
+  w->es = S.es;
+  w->mb = S.nb;
+  w->nb = S.mb;
+  w->m = S.n;
+  w->n = S.m;
+  w->mt = S.nt;
+  w->nt = S.mt;
+  w->lm = w->m;
+  w->ln = w->n;
+  w->lld = std::max(16, (w->m + 15) / 16 * 16);
+  void* p = nullptr;
+  if (hipMalloc(&p, (size_t)w->lld * std::max(1, w->n) * S.es) != hipSuccess) return nullptr;
+  w->data = (char*)p;
+  w->owned = true;
+  P.wdesc.push_back(w);
+  return w;
+}
+
+// D := S^H (D is S.n x S.m), on stream 1 after prev
+int add_ctrans(NatProgram& P, const NatDesc& S, NatDesc& D, int prev) {
+  auto mb = std::make_shared<MapBatch>();
+  mb->build(D, UPPERLOWER, &S, CONJTRANS);
+  if (!mb->upload(P)) return -2;
+  const int prec = S.prec, lds = S.lld, ldd = D.lld;
+  const char* s = S.data;
+  char* d = D.data;
+  const Scalar one(prec, 1.0), zero(prec, 0.0);
+  return P.task(1, [=](hipStream_t st) {
+    return dpl_geadd(prec, 0, CONJTRANS, mb->n(), mb->items(), mb->mm, mb->nn, one.ptr(), s, lds, zero.ptr(), d, ldd,
+                     1, st);
+  }, {prev});
+}
+
+bool lq_conform(const NatDesc* A, const NatDesc* T) {
+  const int kt = std::min(A->mt, A->nt);
+  return A->mb == A->nb && A->nb <= 256 && T->nb == A->nb && T->mt >= kt && T->nt >= kt && T->mb >= 1 &&
+         T->mb <= A->nb;
+}
+
+bool add_gelqf(NatProgram& P, NatDesc& A, NatDesc& T, int& last) {
+  auto W = ctrans_desc(P, A);
+  if (!W) return false;
+  last = add_ctrans(P, A, *W, last);
+  if (last < -1 || !add_geqrf(P, *W, T, last)) return false;
+  last = add_ctrans(P, *W, A, last);
+  return last >= -1;
+}
+
+// C := op(Q) C or C op(Q) with Q = Q_r^H from the native gelqf of A
+bool add_unmlq(NatProgram& P, int side, int trans, NatDesc& A, NatDesc& T, NatDesc& C, int& last) {
+  auto W = ctrans_desc(P, A);
+  if (!W) return false;
+  last = add_ctrans(P, A, *W, last);
+  if (last < -1) return false;
+  return add_unmqr(P, side, trans == NOTRANS ? CONJTRANS : NOTRANS, *W, T, C, last);
+}
+
+bool has_fullT_lq(const NatDesc& A, const NatDesc& T) {
+  return T.fullT && T.fullT_nb == A.nb && T.fullT_kt >= std::min(A.mt, A.nt);
+}
+
+}  // namespace
+
+NatProgram* nat_gelqf(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dplasma_desc_t* dT) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *T = dT ? dT->nat : nullptr;
+  if (!same_ctx(c, {A, T}, prec)) return fail(nullptr, "gelqf: descriptors of another context or precision");
+  if (!lq_conform(A, T)) return fail(nullptr, "gelqf: square tiles <= 256 and a T of (IB x NB) tiles covering A");
+  NatProgram* P = new_program(c, "gelqf", true);
+  int last = -1;
+  if (!P->info || !add_gelqf(*P, *A, *T, last)) return fail(P, "gelqf: device allocation failed");
+  return P;
+}
+
+NatProgram* nat_unmlq(dplasma_context_t* ctx, int prec, int side, int trans, dplasma_desc_t* dA, dplasma_desc_t* dT,
+                      dplasma_desc_t* dC) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *T = dT ? dT->nat : nullptr, *C = dC ? dC->nat : nullptr;
+  if (!same_ctx(c, {A, T, C}, prec)) return fail(nullptr, "unmlq: descriptors of another context or precision");
+  if (!lq_conform(A, T) || !has_fullT_lq(*A, *T)) return fail(nullptr, "unmlq: T must come from the native gelqf of A");
+  if ((side == LEFT && (C->m != A->n || C->mb != A->nb)) || (side == RIGHT && (C->n != A->n || C->nb != A->nb)))
+    return fail(nullptr, "unmlq: C does not conform to Q");
+  NatProgram* P = new_program(c, "unmlq", false);
+  int last = -1;
+  if (!add_unmlq(*P, side, trans, *A, *T, *C, last)) return fail(P, "unmlq: device allocation failed");
+  return P;
+}
+
+// Q (K x N) := the first K rows of the LQ orthogonal factor = (the first K columns of Q_r)^H
+NatProgram* nat_unglq(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dplasma_desc_t* dT, dplasma_desc_t* dQ) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *T = dT ? dT->nat : nullptr, *Q = dQ ? dQ->nat : nullptr;
+  if (!same_ctx(c, {A, T, Q}, prec)) return fail(nullptr, "unglq: descriptors of another context or precision");
+  if (!lq_conform(A, T) || !has_fullT_lq(*A, *T) || Q->n != A->n || Q->nb != A->nb || Q->mb != A->mb || Q->m > A->n)
+    return fail(nullptr, "unglq: T from the native gelqf of A, Q with A's columns");
+  NatProgram* P = new_program(c, "unglq", false);
+  auto W = ctrans_desc(*P, *A), Qt = ctrans_desc(*P, *Q);
+  if (!W || !Qt) return fail(P, "unglq: device allocation failed");
+  std::vector<TileItem> it;
+  for (int i = 0; i < Qt->mt; ++i)
+    for (int j = 0; j < Qt->nt; ++j) it.push_back(TileItem{Qt->off(i, j), 0, Qt->rows(i), Qt->cols(j), i * Qt->mb, j * Qt->nb});
+  auto d_it = dev_upload(it);
+  if (!d_it) return fail(P, "unglq: device allocation failed");
+  P->keep.push_back(d_it);
+  const int n = (int)it.size(), mb = Qt->mb, nb = Qt->nb, ldq = Qt->lld;
+  char* q = Qt->data;
+  const Scalar zero(prec, 0.0), one(prec, 1.0);
+  int last = P->task(1, [=](hipStream_t s) {
+    return dpl_laset(prec, 0, n, d_it->p, mb, nb, zero.ptr(), one.ptr(), q, ldq, s);
+  }, {});
+  last = add_ctrans(*P, *A, *W, last);
+  if (last < -1 || !add_unmqr(*P, LEFT, NOTRANS, *W, *T, *Qt, last)) return fail(P, "unglq: device allocation failed");
+  if (add_ctrans(*P, *Qt, *Q, last) < -1) return fail(P, "unglq: device allocation failed");
+  return P;
+}
+
+// minimum-norm solution of an M <= N system (reference src/zgelqs_wrapper.c): B(0:M) := L^-1 B(0:M), then
+// B := Q^H B (B's N rows receive X)
+static bool add_gelqs(NatProgram& P, NatDesc& A, NatDesc& T, NatDesc& B, int& last) {
+  auto L = lead_view(A, A.m, A.m), Y = lead_view(B, A.m, B.n);
+  P.wdesc.push_back(L);
+  P.wdesc.push_back(Y);
+  if (!add_trsm(P, LEFT, LOWER, NOTRANS, NONUNIT, Scalar(A.prec, 1.0), *L, *Y, 1, last)) return false;
+  last = last_on(P, 1);
+  return add_unmlq(P, LEFT, CONJTRANS, A, T, B, last);
+}
+
+NatProgram* nat_gelqs(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dplasma_desc_t* dT, dplasma_desc_t* dB) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *T = dT ? dT->nat : nullptr, *B = dB ? dB->nat : nullptr;
+  if (!same_ctx(c, {A, T, B}, prec)) return fail(nullptr, "gelqs: descriptors of another context or precision");
+  if (!lq_conform(A, T) || !has_fullT_lq(*A, *T) || A->m > A->n || B->m < A->n || B->mb != A->nb)
+    return fail(nullptr, "gelqs: T from the native gelqf of an M <= N matrix A, B with N rows");
+  NatProgram* P = new_program(c, "gelqs", false);
+  int last = -1;
+  if (!add_gelqs(*P, *A, *T, *B, last)) return fail(P, "gelqs: device allocation failed");
+  return P;
+}
+
+// least squares (M >= N: QR) or minimum norm (M < N: LQ), NoTrans (reference src/zgels_wrapper.c)
 NatProgram* nat_gels(dplasma_context_t* ctx, int prec, int trans, dplasma_desc_t* dA, dplasma_desc_t* dT,
                      dplasma_desc_t* dB) {
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *T = dT ? dT->nat : nullptr, *B = dB ? dB->nat : nullptr;
   if (!same_ctx(c, {A, T, B}, prec)) return fail(nullptr, "gels: descriptors of another context or precision");
-  if (trans != NOTRANS || !qr_conform(A, T) || A->m < A->n || B->m != A->m || B->mb != A->mb)
-    return fail(nullptr, "gels: NoTrans least squares of an M >= N matrix (native engine)");
+  if (trans != NOTRANS) return fail(nullptr, "gels: NoTrans (native engine)");
   NatProgram* P = new_program(c, "gels", true);
   int last = -1;
-  if (!P->info || !add_geqrf(*P, *A, *T, last) || !add_geqrs(*P, *A, *T, *B, last))
-    return fail(P, "gels: device allocation failed");
+  if (A->m >= A->n) {
+    if (!qr_conform(A, T) || B->m != A->m || B->mb != A->mb)
+      return fail(P, "gels: T of (IB x NB) tiles covering A, B with A's rows");
+    if (!P->info || !add_geqrf(*P, *A, *T, last) || !add_geqrs(*P, *A, *T, *B, last))
+      return fail(P, "gels: device allocation failed");
+  } else {
+    if (!lq_conform(A, T) || B->m < A->n || B->mb != A->nb)
+      return fail(P, "gels: T of (IB x NB) tiles covering A, B with N rows");
+    if (!P->info || !add_gelqf(*P, *A, *T, last) || !add_gelqs(*P, *A, *T, *B, last))
+      return fail(P, "gels: device allocation failed");
+  }
   return P;
 }

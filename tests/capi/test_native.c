@@ -597,6 +597,157 @@ static void test_dgetrf(dplasma_context_t *ctx) {
   dplasma_desc_destroy(A), dplasma_desc_destroy(B), dplasma_desc_destroy(IP);
 }
 
+/* dgetrf_nopiv on a diagonally dominant ragged matrix: L U = A (L unit lower, U upper, in place) */
+static void test_dgetrf_nopiv(dplasma_context_t *ctx) {
+  const int n = 600, nb = 128;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, n, n);
+  double *a = malloc(sizeof(double) * n * n), *lu = malloc(sizeof(double) * n * n);
+  unsigned sd = 5;
+  rnd_fill(a, (size_t)n * n, &sd);
+  for (int i = 0; i < n; ++i) a[i + (size_t)i * n] += n;
+  dplasma_desc_set_lapack(A, a, n);
+  const int info = dplasma_dgetrf_nopiv(ctx, A);
+  CHECK(info == 0, "dgetrf_nopiv info %d (%s)", info, dplasma_last_error());
+  dplasma_desc_get_lapack(A, lu, n);
+  double err = 0, an = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < n; ++i) {
+      double s = 0;
+      const int kk = i < j ? i : j;
+      for (int k = 0; k <= kk; ++k) s += (k == i ? 1.0 : lu[i + (size_t)k * n]) * lu[k + (size_t)j * n];
+      err = fmax(err, fabs(s - a[i + (size_t)j * n]));
+      an = fmax(an, fabs(a[i + (size_t)j * n]));
+    }
+  printf("dgetrf_nopiv n=%d nb=%d: ||LU - A|| / ||A|| %.3e\n", n, nb, err / an);
+  CHECK(err / an < 1e-13, "getrf_nopiv residual %.3e", err / an);
+  free(a), free(lu);
+  dplasma_desc_destroy(A);
+}
+
+/* flat-tree LQ family on a wide matrix: gelqf, unglq (Q Q^T = I, L Q = A), unmlq (left Q x, right A Q^T = [L 0]),
+ * minimum-norm gels / gelqs (A x = b) */
+static void test_dgelqf(dplasma_context_t *ctx) {
+  const int m = 400, n = 700, nb = 128, ib = 32, nrhs = 3;
+  const int mt = (m + nb - 1) / nb, nt = (n + nb - 1) / nb;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, m, n);
+  dplasma_desc_t *T = dplasma_desc_block_cyclic(ctx, dplasmaRealDouble, ib, nb, mt * ib, nt * nb, 1, 1,
+                                               dplasmaUpperLower);
+  dplasma_desc_t *Q = dmat(ctx, dplasmaRealDouble, nb, m, n), *C = dmat(ctx, dplasmaRealDouble, nb, m, n);
+  dplasma_desc_t *X = dmat(ctx, dplasmaRealDouble, nb, n, nrhs), *B = dmat(ctx, dplasmaRealDouble, nb, n, nrhs);
+  CHECK(T && Q && C && X && B, "descriptors: %s", dplasma_last_error());
+  double *a = malloc(sizeof(double) * m * n), *f = malloc(sizeof(double) * m * n), *q = malloc(sizeof(double) * m * n);
+  double *c = malloc(sizeof(double) * m * n), *x = malloc(sizeof(double) * n * nrhs), *y = malloc(sizeof(double) * n * nrhs);
+  double *b = malloc(sizeof(double) * n * nrhs);
+  unsigned sd = 91;
+  rnd_fill(a, (size_t)m * n, &sd), rnd_fill(x, (size_t)n * nrhs, &sd), rnd_fill(b, (size_t)n * nrhs, &sd);
+  dplasma_desc_set_lapack(A, a, m);
+  int info = dplasma_dgelqf(ctx, A, T);
+  CHECK(info == 0, "dgelqf info %d (%s)", info, dplasma_last_error());
+  dplasma_desc_get_lapack(A, f, m);
+  CHECK(dplasma_dunglq(ctx, A, T, Q) == 0, "dunglq: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(Q, q, m);
+  double orth = 0, res = 0, an = 0;
+  for (int j = 0; j < m; ++j)
+    for (int i = 0; i < m; ++i) {
+      double s = 0;
+      for (int k = 0; k < n; ++k) s += q[i + (size_t)k * m] * q[j + (size_t)k * m];
+      orth = fmax(orth, fabs(s - (i == j)));
+    }
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < m; ++i) {
+      double s = 0;
+      for (int k = 0; k <= i; ++k) s += f[i + (size_t)k * m] * q[k + (size_t)j * m];
+      res = fmax(res, fabs(s - a[i + (size_t)j * m]));
+      an = fmax(an, fabs(a[i + (size_t)j * m]));
+    }
+  printf("dgelqf m=%d n=%d nb=%d ib=%d: ||Q Q^T - I|| %.3e  ||LQ - A||/||A|| %.3e\n", m, n, nb, ib, orth, res / an);
+  CHECK(orth < 1e-12 && res / an < 1e-12, "gelqf / unglq residuals");
+  /* A0 Q^T = [L 0] (right, transposed) */
+  dplasma_desc_set_lapack(C, a, m);
+  CHECK(dplasma_dunmlq(ctx, dplasmaRight, dplasmaTrans, A, T, C) == 0, "dunmlq R T: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(C, c, m);
+  double e1 = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < m; ++i) e1 = fmax(e1, fabs(c[i + (size_t)j * m] - (j <= i ? f[i + (size_t)j * m] : 0.0)));
+  /* Q^T x (left, transposed): the first m entries are (Q x-rows) = q x */
+  dplasma_desc_set_lapack(X, x, n);
+  CHECK(dplasma_dunmlq(ctx, dplasmaLeft, dplasmaNoTrans, A, T, X) == 0, "dunmlq L N: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(X, y, n);
+  double e2 = 0;
+  for (int r = 0; r < nrhs; ++r)
+    for (int i = 0; i < m; ++i) {
+      double s = 0;
+      for (int k = 0; k < n; ++k) s += q[i + (size_t)k * m] * x[k + (size_t)r * n];
+      e2 = fmax(e2, fabs(s - y[i + (size_t)r * n]));
+    }
+  printf("dunmlq: ||A Q^T - [L 0]|| / ||A|| %.3e   ||(Q x)(0:m) - Q1 x|| %.3e\n", e1 / an, e2);
+  CHECK(e1 / an < 1e-12 && e2 < 1e-11, "unmlq residuals");
+  /* minimum norm: A x = b(0:m) */
+  dplasma_desc_set_lapack(A, a, m);
+  dplasma_desc_set_lapack(B, b, n);
+  info = dplasma_dgels(ctx, dplasmaNoTrans, A, T, B);
+  CHECK(info == 0, "dgels (M < N) info %d (%s)", info, dplasma_last_error());
+  dplasma_desc_get_lapack(B, y, n);
+  double ge = 0;
+  for (int r = 0; r < nrhs; ++r)
+    for (int i = 0; i < m; ++i) {
+      double s = 0;
+      for (int k = 0; k < n; ++k) s += a[i + (size_t)k * m] * y[k + (size_t)r * n];
+      ge = fmax(ge, fabs(s - b[i + (size_t)r * n]));
+    }
+  /* gelqs on the factored A (from the gels call) with fresh b: same solution */
+  dplasma_desc_set_lapack(B, b, n);
+  CHECK(dplasma_dgelqs(ctx, A, T, B) == 0, "dgelqs: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(B, c, n);
+  double de = 0;
+  for (int r = 0; r < nrhs; ++r)
+    for (int i = 0; i < n; ++i) de = fmax(de, fabs(c[i + (size_t)r * n] - y[i + (size_t)r * n]));
+  printf("dgels min-norm m=%d n=%d: ||A x - b|| %.3e  gelqs vs gels %.3e\n", m, n, ge, de);
+  CHECK(ge < 1e-10 && de < 1e-12, "gels / gelqs residuals");
+  free(a), free(f), free(q), free(c), free(x), free(y), free(b);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(T), dplasma_desc_destroy(Q), dplasma_desc_destroy(C);
+  dplasma_desc_destroy(X), dplasma_desc_destroy(B);
+}
+
+/* complex LQ: the conjugate-transpose construction must give L Q = A with Q Q^H = I */
+static void test_zgelqf(dplasma_context_t *ctx) {
+  const int m = 200, n = 330, nb = 64, ib = 16;
+  const int mt = (m + nb - 1) / nb, nt = (n + nb - 1) / nb;
+  dplasma_desc_t *A = dmat(ctx, dplasmaComplexDouble, nb, m, n), *Q = dmat(ctx, dplasmaComplexDouble, nb, m, n);
+  dplasma_desc_t *T = dplasma_desc_block_cyclic(ctx, dplasmaComplexDouble, ib, nb, mt * ib, nt * nb, 1, 1,
+                                               dplasmaUpperLower);
+  CHECK(A && Q && T, "descriptors: %s", dplasma_last_error());
+  double complex *a = malloc(sizeof(double complex) * m * n), *f = malloc(sizeof(double complex) * m * n);
+  double complex *q = malloc(sizeof(double complex) * m * n);
+  double *re = malloc(sizeof(double) * 2 * m * n);
+  unsigned sd = 17;
+  rnd_fill(re, (size_t)2 * m * n, &sd);
+  for (size_t i = 0; i < (size_t)m * n; ++i) a[i] = re[2 * i] + I * re[2 * i + 1];
+  dplasma_desc_set_lapack(A, a, m);
+  CHECK(dplasma_zgelqf(ctx, A, T) == 0, "zgelqf: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(A, f, m);
+  CHECK(dplasma_zunglq(ctx, A, T, Q) == 0, "zunglq: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(Q, q, m);
+  double orth = 0, res = 0, an = 0;
+  for (int j = 0; j < m; ++j)
+    for (int i = 0; i < m; ++i) {
+      double complex s = 0;
+      for (int k = 0; k < n; ++k) s += q[i + (size_t)k * m] * conj(q[j + (size_t)k * m]);
+      orth = fmax(orth, cabs(s - (i == j)));
+    }
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < m; ++i) {
+      double complex s = 0;
+      for (int k = 0; k <= i; ++k) s += f[i + (size_t)k * m] * q[k + (size_t)j * m];
+      res = fmax(res, cabs(s - a[i + (size_t)j * m]));
+      an = fmax(an, cabs(a[i + (size_t)j * m]));
+    }
+  printf("zgelqf m=%d n=%d: ||Q Q^H - I|| %.3e  ||LQ - A||/||A|| %.3e\n", m, n, orth, res / an);
+  CHECK(orth < 1e-12 && res / an < 1e-12, "zgelqf / zunglq residuals");
+  free(a), free(f), free(q), free(re);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(Q), dplasma_desc_destroy(T);
+}
+
 /* flat-tree QR family: geqrf, ungqr (thin and full Q), unmqr (left Q^T, right Q), gels */
 static void test_dgeqrf(dplasma_context_t *ctx) {
   const int m = 700, n = 400, nb = 128, ib = 32, nrhs = 3, p = 50;
@@ -839,12 +990,15 @@ int main(int argc, char **argv) {
   test_symm_hemm(ctx);
   test_dgetrf(ctx);
   test_dgeqrf(ctx);
+  test_dgetrf_nopiv(ctx);
+  test_dgelqf(ctx);
+  test_zgelqf(ctx);
   test_inverse_family(ctx);
   test_rank_2k(ctx);
   test_aliases(ctx);
   /* an operation without a native implementation fails cleanly */
   dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
-  CHECK(dplasma_dgelqf(ctx, A, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");
+  CHECK(dplasma_dgetrf_incpiv(ctx, A, A, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");
   dplasma_desc_destroy(A);
   if (argc > 1 && atoi(argv[1]) > 0) bench(ctx, atoi(argv[1]));
   CHECK(dplasma_python_active() == 0, "the interpreter was started");

@@ -108,6 +108,11 @@ NATIVE = {
     "lauum": "uplo, A",
     "potri": "uplo, A",
     "poinv": "uplo, A",
+    "getrf_nopiv": "A",
+    "gelqf": "A, T",
+    "unmlq": "side, trans, A, T, C",
+    "unglq": "A, T, Q",
+    "gelqs": "A, T, B",
 }
 # same operation natively under another name: the recursive-size hint only changes the reference's CPU
 # task granularity; a 1 x 1 ptgpanel grid is the 1-D LU; the _sync variant is the blocking call
