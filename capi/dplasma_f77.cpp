@@ -94,6 +94,8 @@ dplasma_context_t* native_ctx() {
   return g_nctx;
 }
 
+dplasma_context_t* native_ctx_any() { return g_nctx; }
+
 bool native_grid(const int* desc) { return f77_native() && desc && desc[1] == NATIVE_CTXT; }
 
 bool on_device(const void* p) {
@@ -114,6 +116,13 @@ struct Wrapped {
   bool copy = false;
   void* dev = nullptr;          // multi-process grids: device copy of a host local array (lm x ln, lld)
   int lm = 0, ln = 0, es = 0;
+  // multi-process grids, an operand off (1, 1) or distributed from another process than (0, 0): the
+  // aligned copy (host image + device matrix) and the source array's host image
+  bool redist = false, src_dev = false;
+  void* src = nullptr;
+  std::vector<char> hsrc, hw;
+  int slld = 0, mb = 0, nb = 0, rsrc = 0, csrc = 0, ia = 1, ja = 1, m = 0, n = 0, wlld = 0;
+  size_t sbytes = 0;
 };
 constexpr int NAT_TILE = 256;
 
@@ -125,15 +134,44 @@ Wrapped wrap(int prec, int es, void* a, int ia, int ja, const int* desc, int m, 
   if (dplasma_context_world(c) > 1) {
     // P x Q grid: the local array IS this rank's tiles in ScaLAPACK local layout when the operand starts
     // at (1, 1) of a matrix distributed from process (0, 0) with mb x nb blocks (the tiles)
-    if (ia != 1 || ja != 1 || desc[6] != 0 || desc[7] != 0) {
-      dpl_set_error("native multi-process F77: operands at IA = JA = 1 of matrices distributed from process (0, 0)");
-      return w;
-    }
     const int mb = desc[4], nb = desc[5], me = dplasma_context_rank(c);
     const int myrow = me / g_npcol, mycol = me % g_npcol;
     int zero = 0;
     int mm = m, nn = n, mbv = mb, nbv = nb, pr = g_nprow, pc = g_npcol, r = myrow, q = mycol;
     const int lm = numroc_(&mm, &mbv, &r, &zero, &pr), ln = numroc_(&nn, &nbv, &q, &zero, &pc);
+    if (ia != 1 || ja != 1 || desc[6] != 0 || desc[7] != 0) {
+      // not tile aligned: redistribute into an aligned copy (reference scalapack_wrappers/common.c:27-128)
+      w.redist = true;
+      w.es = es;
+      w.src = a;
+      w.slld = w.lld, w.mb = mb, w.nb = nb, w.rsrc = desc[6], w.csrc = desc[7], w.ia = ia, w.ja = ja, w.m = m, w.n = n;
+      int gm = desc[2], gn = desc[3], rs = desc[6], cs = desc[7];
+      const int slm = numroc_(&gm, &mbv, &r, &rs, &pr), sln = numroc_(&gn, &nbv, &q, &cs, &pc);
+      (void)slm;
+      w.sbytes = (size_t)w.slld * std::max(0, sln) * es;
+      w.src_dev = on_device(a);
+      char* hs = (char*)a;
+      if (w.src_dev) {
+        w.hsrc.resize(std::max<size_t>(w.sbytes, 1));
+        if (w.sbytes && hipMemcpy(w.hsrc.data(), a, w.sbytes, hipMemcpyDeviceToHost) != hipSuccess) return w;
+        hs = w.hsrc.data();
+      }
+      w.wlld = std::max(1, lm);
+      w.hw.assign((size_t)w.wlld * std::max(1, ln) * es, 0);
+      if (nat_redistribute(c, es, hs, w.slld, mb, nb, desc[6], desc[7], ia, ja, m, n, w.hw.data(), w.wlld, true) != 0) {
+        dpl_set_error("native multi-process F77: redistribution of an unaligned operand failed");
+        return w;
+      }
+      void* d = nullptr;
+      if (hipMalloc(&d, w.hw.size()) != hipSuccess) return w;
+      if (hipMemcpy(d, w.hw.data(), w.hw.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return w;
+      }
+      w.dev = d;
+      w.d = dplasma_desc_block_cyclic_lapack(c, prec, mb, nb, m, n, 0, 0, 0, 0, d, w.wlld, 1);
+      return w;
+    }
     void* dev = a;
     if (!on_device(a)) {   // host local array: through a device copy, written back by unwrap
       dev = nullptr;
@@ -170,6 +208,21 @@ Wrapped wrap(int prec, int es, void* a, int ia, int ja, const int* desc, int m, 
 }
 
 void unwrap(Wrapped& w, bool write_back) {
+  if (w.redist) {   // aligned copy -> the caller's (unaligned) operand
+    if (write_back && w.d && w.dev &&
+        hipMemcpy(w.hw.data(), w.dev, w.hw.size(), hipMemcpyDeviceToHost) == hipSuccess) {
+      char* hs = w.src_dev ? w.hsrc.data() : (char*)w.src;
+      if (nat_redistribute(native_ctx_any(), w.es, hs, w.slld, w.mb, w.nb, w.rsrc, w.csrc, w.ia, w.ja, w.m, w.n,
+                           w.hw.data(), w.wlld, false) == 0 &&
+          w.src_dev && w.sbytes)
+        (void)hipMemcpy(w.src, hs, w.sbytes, hipMemcpyHostToDevice);
+    }
+    if (w.d) dplasma_desc_destroy(w.d);
+    if (w.dev) (void)hipFree(w.dev);
+    w.d = nullptr;
+    w.dev = nullptr;
+    return;
+  }
   if (w.dev) {   // multi-process host local array
     if (write_back && w.d && w.lm > 0 && w.ln > 0)
       (void)hipMemcpy2D(w.host, (size_t)w.lld * w.es, w.dev, (size_t)w.lld * w.es, (size_t)w.lm * w.es, w.ln,
@@ -354,12 +407,14 @@ static int latsqr_work(const int* desca) {
       std::vector<int> p(k);                                                                                      \
       if (dplasma_desc_get_lapack(IP, p.data(), 1) == 0) {                                                        \
         if (dplasma_context_world(native_ctx()) > 1) {   /* ScaLAPACK layout: the entries of my local rows */  \
+          /* (local row li of the whole local array -> global row gi; rows ia-1 .. ia-1+k of the operand */     \
+          /*  hold the operand's pivots, as global rows of the whole matrix) */                                 \
           const int mbv = da[4], me = dplasma_context_rank(native_ctx()), myrow = me / g_npcol;                  \
-          int mm = m, mbb = mbv, r = myrow, z = 0, pr = g_nprow;                                                  \
-          const int lm = numroc_(&mm, &mbb, &r, &z, &pr);                                                         \
+          int gm = da[2], mbb = mbv, r = myrow, rs = da[6], pr = g_nprow;                                         \
+          const int lm = numroc_(&gm, &mbb, &r, &rs, &pr), d = (myrow - rs + g_nprow) % g_nprow;                  \
           for (int li = 0; li < lm; ++li) {                                                                       \
-            const int gi = ((li / mbv) * g_nprow + myrow) * mbv + li % mbv;                                       \
-            if (gi < k) ipiv[li] = p[gi];                                                                         \
+            const int gi = ((li / mbv) * g_nprow + d) * mbv + li % mbv - (ia - 1);                                \
+            if (gi >= 0 && gi < k) ipiv[li] = p[gi] + ia - 1;                                                     \
           }                                                                                                       \
         } else {                                                                                                  \
           for (int i = 0; i < k; ++i) ipiv[i] = p[i] + ia - 1;   /* global row of the whole array */           \

@@ -19,6 +19,7 @@
 //   its block row / column, and one GEMM launch covers every local C tile with k-runs over the chunk;
 //   chunk c+1's pack and exchange overlap chunk c's GEMM (double-buffered).
 #include <algorithm>
+#include <cstring>
 #include <set>
 
 #include "native_comm.h"
@@ -584,4 +585,127 @@ bool nat_dist_mirror_into(NatProgram& Pr, const NatDesc& A, int uplo, int mtrans
   int last = Pr.task(1, tcopy(loc, a, lda), {j0, j1, j2});
   if (!rc->it.empty()) last = Pr.task(1, tcopy(rc, sb, mb), {last, t_x});
   return true;
+}
+
+// ----------------------------------------------------------------------------- F77 redistribution
+// A ScaLAPACK operand that does not start at IA = JA = 1 of a matrix distributed from process (0, 0)
+// is not a tile-aligned block-cyclic matrix: the reference wrappers redistribute it into an aligned copy
+// before running and back afterwards (src/scalapack_wrappers/common.c:27-128).  Same here, between HOST
+// local arrays: global rows (columns) of the operand split into runs on which both the source block and
+// the aligned copy's block are constant; the message from rank s to rank d is every (column run, column,
+// row run) piece owned by s and destined to d, enumerated in the same order on both sides, packed on the
+// host, moved in ONE exchange of the context's transport and unpacked (own pieces are copied directly).
+namespace {
+struct RdRun { int sp, sl, dp, dl, len; };
+
+// runs of global indices [i0, i0 + n) (0-based): source blocks of nbk from process src, aligned copy
+// blocks of nbk from process 0, over np processes
+std::vector<RdRun> rd_runs(int i0, int n, int nbk, int src, int np) {
+  std::vector<RdRun> r;
+  int I = i0;
+  while (I < i0 + n) {
+    const int i = I - i0;
+    const int len = std::min({nbk - I % nbk, nbk - i % nbk, i0 + n - I});
+    const int bs = I / nbk, bd = i / nbk;
+    r.push_back(RdRun{(src + bs) % np, (bs / np) * nbk + I % nbk, bd % np, (bd / np) * nbk + i % nbk, len});
+    I += len;
+  }
+  return r;
+}
+}  // namespace
+
+int nat_redistribute(dplasma_context_t* ctx, int es, char* src, int slld, int mb, int nb, int rsrc, int csrc, int ia,
+                     int ja, int m, int n, char* dst, int dlld, bool to_aligned) {
+  NatCtx* c = ctx ? ctx->nat : nullptr;
+  if (!c || m <= 0 || n <= 0) return 0;
+  const int P = c->P, Q = c->Q, me = c->rank, myrow = c->myrow, mycol = c->mycol;
+  const std::vector<RdRun> rr = rd_runs(ia - 1, m, mb, rsrc, P), cr = rd_runs(ja - 1, n, nb, csrc, Q);
+  // the orientation of this call: data flows from "from" layout to "to" layout
+  auto from_row = [&](const RdRun& x) { return to_aligned ? x.sp : x.dp; };
+  auto to_row = [&](const RdRun& x) { return to_aligned ? x.dp : x.sp; };
+  auto from_l = [&](const RdRun& x) { return to_aligned ? x.sl : x.dl; };
+  auto to_l = [&](const RdRun& x) { return to_aligned ? x.dl : x.sl; };
+  char* fbuf = to_aligned ? src : dst;
+  char* tbuf = to_aligned ? dst : src;
+  const int flld = to_aligned ? slld : dlld, tlld = to_aligned ? dlld : slld;
+  // bytes of the message from (fr, fc) to (tr, tc)
+  auto msg_elems = [&](int fr, int fc, int tr, int tc) {
+    long long rows = 0, cols = 0;
+    for (const RdRun& x : rr)
+      if (from_row(x) == fr && to_row(x) == tr) rows += x.len;
+    for (const RdRun& y : cr)
+      if (from_row(y) == fc && to_row(y) == tc) cols += y.len;
+    return rows * cols;
+  };
+  // walk the pieces of one message: f(from_offset, to_offset, len) in elements
+  auto walk = [&](int fr, int fc, int tr, int tc, auto&& f) {
+    for (const RdRun& y : cr) {
+      if (from_row(y) != fc || to_row(y) != tc) continue;
+      for (int jj = 0; jj < y.len; ++jj)
+        for (const RdRun& x : rr) {
+          if (from_row(x) != fr || to_row(x) != tr) continue;
+          f((long long)from_l(x) + (long long)(from_l(y) + jj) * flld, (long long)to_l(x) + (long long)(to_l(y) + jj) * tlld,
+            x.len);
+        }
+    }
+  };
+  std::vector<NatMsg> sends, recvs;
+  std::vector<std::vector<char>> hs, hr;
+  std::vector<int> speer, rpeer;
+  for (int d = 0; d < P * Q; ++d) {
+    const int dr = d / Q, dc = d % Q;
+    if (d == me) {   // own pieces: direct host copies
+      walk(myrow, mycol, myrow, mycol, [&](long long fo, long long to, int len) {
+        std::memcpy(tbuf + to * es, fbuf + fo * es, (size_t)len * es);
+      });
+      continue;
+    }
+    const long long ns = msg_elems(myrow, mycol, dr, dc), nr = msg_elems(dr, dc, myrow, mycol);
+    if (ns > 0) {
+      std::vector<char> b((size_t)ns * es);
+      size_t p = 0;
+      walk(myrow, mycol, dr, dc, [&](long long fo, long long, int len) {
+        std::memcpy(b.data() + p, fbuf + fo * es, (size_t)len * es);
+        p += (size_t)len * es;
+      });
+      hs.push_back(std::move(b));
+      speer.push_back(d);
+    }
+    if (nr > 0) {
+      hr.emplace_back((size_t)nr * es);
+      rpeer.push_back(d);
+    }
+  }
+  std::vector<void*> dbufs;
+  auto dev = [&](size_t bytes) -> void* {
+    void* p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(bytes, 16)) != hipSuccess) return nullptr;
+    dbufs.push_back(p);
+    return p;
+  };
+  int rc = 0;
+  for (size_t q = 0; q < hs.size() && rc == 0; ++q) {
+    void* p = dev(hs[q].size());
+    if (!p || hipMemcpy(p, hs[q].data(), hs[q].size(), hipMemcpyHostToDevice) != hipSuccess) rc = -1;
+    else sends.push_back(NatMsg{speer[q], p, hs[q].size()});
+  }
+  for (size_t q = 0; q < hr.size() && rc == 0; ++q) {
+    void* p = dev(hr[q].size());
+    if (!p) rc = -1;
+    else recvs.push_back(NatMsg{rpeer[q], p, hr[q].size()});
+  }
+  hipStream_t st = c->st[0];
+  if (rc == 0 && (!sends.empty() || !recvs.empty())) rc = c->comm->exchange(sends, recvs, st);
+  if (rc == 0 && hipStreamSynchronize(st) != hipSuccess) rc = -1;
+  for (size_t q = 0; q < hr.size() && rc == 0; ++q) {
+    if (hipMemcpy(hr[q].data(), recvs[q].buf, hr[q].size(), hipMemcpyDeviceToHost) != hipSuccess) { rc = -1; break; }
+    const int s = rpeer[q];
+    size_t p = 0;
+    walk(s / Q, s % Q, myrow, mycol, [&](long long, long long to, int len) {
+      std::memcpy(tbuf + to * es, hr[q].data() + p, (size_t)len * es);
+      p += (size_t)len * es;
+    });
+  }
+  for (void* p : dbufs) (void)hipFree(p);
+  return rc;
 }

@@ -302,6 +302,33 @@ __device__ __forceinline__ void gemm_full_tile(const int wg, const GemmItemK* __
 // kernels on a high-priority stream find free CUs at once instead of queueing behind ~0.5 ms
 // GEMM workgroups (profiles/r2_potrf16k_timeline.txt).  The cap is a multiple of the 8 XCDs, so a
 // workgroup keeps its XCD's share of xcd_remap's tile order on every pass.
+// wave-uniform copy of a value that a non-inlined call passed in VGPRs (any trivially copyable type)
+template <typename V>
+__device__ __forceinline__ V rfl_any(V v) {
+  static_assert(sizeof(V) % 4 == 0, "32-bit words");
+  unsigned w[sizeof(V) / 4];
+  __builtin_memcpy(w, &v, sizeof(V));
+#pragma unroll
+  for (int q = 0; q < (int)(sizeof(V) / 4); ++q) w[q] = __builtin_amdgcn_readfirstlane(w[q]);
+  V r;
+  __builtin_memcpy(&r, w, sizeof(V));
+  return r;
+}
+
+// One sub-tile of the capped (grid-stride) launch as a separate function: inlined into the
+// grid-stride loop the body kept loop-invariant addressing live across iterations and spilled 63
+// VGPRs to scratch (hipcc -Rpass-analysis=kernel-resource-usage), which is what made every capped
+// bulk update slower than the uncapped one (profiles/r3_lu_rest_cap.txt).  Called, it is allocated on
+// its own; the arguments arrive in VGPRs and are made wave-uniform again (buffer resources need SGPRs).
+template <typename T, bool TA, bool TB>
+__device__ __attribute__((noinline)) void gemm_full_tile_call(int wg, const GemmItemK* items, const KPair* kps,
+                                                               int nsm, int nsn, T alpha, const T* A, int lda,
+                                                               const T* B, int ldb, T beta, T* C, int ldc) {
+  gemm_full_tile<T, TA, TB>(rfl_any(wg), rfl_any(items), rfl_any(kps), rfl_any(nsm), rfl_any(nsn), rfl_any(alpha),
+                            rfl_any(A), rfl_any(lda), rfl_any(B), rfl_any(ldb), rfl_any(beta), rfl_any(C),
+                            rfl_any(ldc));
+}
+
 template <typename T, bool TA, bool TB, bool PERSIST>
 __global__ __launch_bounds__(256, 2) void k_gemm_full(const GemmItemK* __restrict__ items,
                                                       const KPair* __restrict__ kps, int nsm, int nsn,
@@ -314,7 +341,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_full(const GemmItemK* __restric
     return;
   }
   for (int b = blockIdx.x; b < nwg; b += gridDim.x) {
-    gemm_full_tile<T, TA, TB>(xcd_remap(b, nwg), items, kps, nsm, nsn, alpha, A, lda, B, ldb, beta, C, ldc);
+    gemm_full_tile_call<T, TA, TB>(xcd_remap(b, nwg), items, kps, nsm, nsn, alpha, A, lda, B, ldb, beta, C, ldc);
     __syncthreads();   // the next sub-tile's first LDS stores must not overtake this one's last reads
   }
 }

@@ -167,7 +167,17 @@ class _GetrfQrf(Taskpool):
         if c == RANDOM_CRITERIUM:
             return int(self.lu_tab[k])
         if c in _HIGHAMS or c == MUMPS_CRITERIUM:
-            return None
+            if self.p != 1:
+                return None
+            # p = 1: the domain is the whole panel column, so no tile is off-domain: the off-domain
+            # sum / max / column maxima are 0 and the decision does not depend on the data --
+            # alpha * w0 > 0 (w0 > 0 for a non-singular domain), alpha * colmax >= 0; the mean over zero
+            # off-domain tiles is 0 / 0 in the reference (src/zgetrf_qrf.jdf:1125-1135), NaN: never LU
+            if c == HIGHAM_MOY_CRITERIUM:
+                return 0
+            if c == MUMPS_CRITERIUM:
+                return 1 if self.alpha >= 0 else None
+            return 1 if self.alpha > 0 else None
         return k % 2
 
     def _run_fast(self):
@@ -282,7 +292,7 @@ class _GetrfQrf(Taskpool):
         elif crit == HIGHAM_MOY_CRITERIUM:
             nt_ = A.mt - k
             nout = nt_ - (nt_ + self.p - 1) // self.p
-            cond = int(alpha * w0 > (offsum / nout if nout else 0.0))
+            cond = int(alpha * w0 > (offsum / nout if nout else float("nan")))   # 0 / 0: the reference's NaN
         elif crit == MUMPS_CRITERIUM:
             diag = vs[3 + nb:3 + nb + st.ncol].numpy()
             off = vm[1:1 + st.ncol].numpy()

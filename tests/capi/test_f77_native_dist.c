@@ -64,6 +64,8 @@ int main(int argc, char **argv) {
     for (int li = 0; li < lm; ++li) a[li + (size_t)lj * lld] = S[gi[li] + (size_t)gj[lj] * N];
   pdpotrf_("L", &n, a, &one, &one, desc, &info);
   CHECK(info == 0, "pdpotrf_ info %d: %s", info, dplasma_last_error());
+  double *S0 = malloc(sizeof(double) * N * N);
+  memcpy(S0, S, sizeof(double) * N * N);
   /* host Cholesky of S (in place, lower) */
   for (int k = 0; k < N; ++k) {
     double d = sqrt(S[k + (size_t)k * N]);
@@ -165,6 +167,69 @@ int main(int argc, char **argv) {
   printf("rank %d: pdgetrf_ %dx%d grid, pivots %s, local max rel diff %.3e\n", me, P, Q, piv_ok ? "equal" : "DIFFER",
          e / nrm);
   CHECK(piv_ok && e / nrm < 1e-10, "pdgetrf_ pivots %d, local entries differ by %.3e", piv_ok, e / nrm);
+  /* ---- unaligned operands (redistributed into an aligned copy and back, reference
+   * scalapack_wrappers/common.c:27-128): the SPD matrix and a product at IA = JA = 38 of an (N + 37)^2
+   * matrix distributed from process row P - 1; entries outside the operand must not change */
+  {
+    const int off = 37, N2 = N + off, rs = P - 1;
+    int n2 = N2, rsv = rs, ia = off + 1;
+    const int lm2 = numroc_(&n2, &nbv, &myrow, &rsv, &P), ln2 = numroc_(&n2, &nbv, &mycol, &zero, &Q);
+    int lld2 = lm2 > 1 ? lm2 : 1, desc2[9];
+    descinit_(desc2, &n2, &n2, &nbv, &nbv, &rsv, &zero, &ictxt, &lld2, &info);
+    int *gi2 = malloc(sizeof(int) * (lm2 + 1)), *gj2 = malloc(sizeof(int) * (ln2 + 1));
+    for (int l = 0; l < lm2; ++l) gi2[l] = ((l / nb) * P + (myrow - rs + P) % P) * nb + l % nb;
+    for (int l = 0; l < ln2; ++l) gj2[l] = ((l / nb) * Q + mycol) * nb + l % nb;
+    const size_t sz2 = (size_t)lld2 * (ln2 > 0 ? ln2 : 1);
+    double *a2 = malloc(sizeof(double) * sz2), *c2 = malloc(sizeof(double) * sz2), *x2 = malloc(sizeof(double) * sz2);
+    for (int lj = 0; lj < ln2; ++lj)
+      for (int li = 0; li < lm2; ++li) {
+        const int gI = gi2[li], gJ = gj2[lj];
+        const int in = gI >= off && gJ >= off;
+        a2[li + (size_t)lj * lld2] = in ? S0[(gI - off) + (size_t)(gJ - off) * N] : 100.0 + fa(gI, gJ);
+        c2[li + (size_t)lj * lld2] = in ? fc(gI - off, gJ - off) : -100.0 - fb(gI, gJ);
+        x2[li + (size_t)lj * lld2] = fa(gI, gJ);   /* the A operand of the product: rows/cols 38.. of x2 */
+      }
+    pdpotrf_("L", &n, a2, &ia, &ia, desc2, &info);
+    CHECK(info == 0, "unaligned pdpotrf_ info %d: %s", info, dplasma_last_error());
+    double e2 = 0, n2m = 0;
+    int outside_ok = 1;
+    for (int lj = 0; lj < ln2; ++lj)
+      for (int li = 0; li < lm2; ++li) {
+        const int gI = gi2[li], gJ = gj2[lj];
+        const double v = a2[li + (size_t)lj * lld2];
+        if (gI < off || gJ < off) {
+          outside_ok = outside_ok && v == 100.0 + fa(gI, gJ);
+        } else if (gI >= gJ) {
+          const double y = S[(gI - off) + (size_t)(gJ - off) * N];
+          e2 = fmax(e2, fabs(v - y));
+          n2m = fmax(n2m, fabs(y));
+        }
+      }
+    printf("rank %d: unaligned pdpotrf_ (IA=JA=%d, RSRC=%d) local max rel diff %.3e, outside %s\n", me, ia, rs,
+           n2m > 0 ? e2 / n2m : 0.0, outside_ok ? "untouched" : "CHANGED");
+    CHECK(outside_ok && (n2m == 0 || e2 / n2m < 1e-12), "unaligned pdpotrf_ diff %.3e", n2m > 0 ? e2 / n2m : 0.0);
+    /* C(38.., 38..) = 0.5 X(38.., 38..) B^T + 2 C with B the aligned fb matrix of the first part */
+    pdgemm_("N", "T", &n, &n, &n, &al, x2, &ia, &ia, desc2, B, &one, &one, desc, &be, c2, &ia, &ia, desc2);
+    e2 = 0, n2m = 0, outside_ok = 1;
+    for (int lj = 0; lj < ln2; ++lj)
+      for (int li = 0; li < lm2; ++li) {
+        const int gI = gi2[li], gJ = gj2[lj];
+        const double v = c2[li + (size_t)lj * lld2];
+        if (gI < off || gJ < off) {
+          outside_ok = outside_ok && v == -100.0 - fb(gI, gJ);
+          continue;
+        }
+        double sacc = 0;
+        for (int k = 0; k < N; ++k) sacc += fa(gI, k + off) * fb(gJ - off, k);
+        const double y = al * sacc + be * fc(gI - off, gJ - off);
+        e2 = fmax(e2, fabs(v - y));
+        n2m = fmax(n2m, fabs(y));
+      }
+    printf("rank %d: unaligned pdgemm_ local max rel diff %.3e, outside %s\n", me, n2m > 0 ? e2 / n2m : 0.0,
+           outside_ok ? "untouched" : "CHANGED");
+    CHECK(outside_ok && (n2m == 0 || e2 / n2m < 1e-12), "unaligned pdgemm_ diff %.3e", n2m > 0 ? e2 / n2m : 0.0);
+    free(a2), free(c2), free(x2), free(gi2), free(gj2);
+  }
   CHECK(!dplasma_python_active(), "the embedded interpreter was started");
   parsec_fini_wrapper_();
   if (fails) {

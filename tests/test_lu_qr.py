@@ -99,7 +99,10 @@ def test_gpu_getrf_qrf(crit):
 
 
 @pytest.mark.parametrize("crit,alpha", [(dp.DEFAULT_CRITERIUM, 1.0), (dp.RANDOM_CRITERIUM, 50.0),
-                                        (dp.LU_ONLY_CRITERIUM, 1.0), (dp.HIGHAM_SUM_CRITERIUM, 0.0)])
+                                        (dp.LU_ONLY_CRITERIUM, 1.0), (dp.HIGHAM_SUM_CRITERIUM, 0.0),
+                                        (dp.HIGHAM_SUM_CRITERIUM, 1.0), (dp.HIGHAM_CRITERIUM, 1.0),
+                                        (dp.HIGHAM_MAX_CRITERIUM, 1.0), (dp.HIGHAM_MOY_CRITERIUM, 1.0),
+                                        (dp.MUMPS_CRITERIUM, 1.0)])
 def test_getrf_qrf_device_path_cpu(ctx, monkeypatch, crit, alpha):
     """The host-sync-free path (p = 1, a criterion fixed in advance): LU steps on the getrf_1d engine with
     trailing-only interchanges, QR steps on the tree; same solve accuracy and the same lu_tab as the
