@@ -440,6 +440,17 @@ static int latsqr_work(const int* desca) {
                                 A.d, B.d);                                                                        \
     }                                                                                                             \
     unwrap(A, false), unwrap(B, true);                                                                            \
+  }                                                                                                               \
+  static int nat_p##P##latsqr(int m, int n, T* a, int ia, int ja, const int* da, T* tau) {                        \
+    Wrapped A = wrap(C, sizeof(T), a, ia, ja, da, m, n);                                                          \
+    if (!A.d) { unwrap(A, false); return -1; }                                                                    \
+    const int nb = da[4], ib = nb < 32 ? nb : 32, mt = (m + nb - 1) / nb, nt = (n + nb - 1) / nb;                \
+    dplasma_desc_t* Td = dplasma_desc_block_cyclic(native_ctx(), C, ib, nb, mt * ib, nt * nb, 0, 0, 123);        \
+    int info = Td ? dplasma_##P##geqrf(native_ctx(), A.d, Td) : -1;                                               \
+    if (info == 0 && tau) info = nat_qr_tau(Td, tau, m < n ? m : n);                                              \
+    if (Td) dplasma_desc_destroy(Td);                                                                             \
+    unwrap(A, true);                                                                                              \
+    return info;                                                                                                  \
   }
 
 DPL_F77_NATIVE(s, float, 2)
@@ -508,9 +519,10 @@ DPL_F77_NATIVE(z, dplasma_complex64_t, 5)
     const int lw = latsqr_work(desca);                                                                           \
     if (work) work[0] = (T)lw;                                                                                   \
     if (*lwork == -1) return;                                                                                    \
-    if (native_grid(desca) && job_world() > 1) {   /* no native QR on a multi-process grid */                   \
-      dpl_set_error("p?latsqr_: not available on a multi-process native grid");                                   \
-      *info = -1;                                                                                                \
+    if (native_grid(desca) && job_world() > 1) {                                                                 \
+      /* a multi-process grid: the native flat-tree QR of the grid (native_dist.cpp), R above and V below    */   \
+      /* the diagonal in LAPACK's layout, TAU (replicated, MIN(M, N) entries) = the T factors' diagonal     */   \
+      *info = nat_p##P##latsqr(*m, *n, a, *ia, *ja, desca, tau);                                                 \
       return;                                                                                                    \
     }                                                                                                            \
     DplGil g;                                                                                                    \

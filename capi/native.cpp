@@ -523,32 +523,7 @@ NatProgram* nat_syr2k(dplasma_context_t* ctx, int prec, int uplo, int trans, con
 // tile is cut at the matrix diagonal exactly as the reference's map2 LOWER / UPPER tasks do.
 static int part_of(int uplo) { return uplo == LOWER ? 1 : uplo == UPPER ? 2 : 0; }
 
-struct MapBatch {
-  std::vector<TileItem> it;
-  int mm = 0, nn = 0;
-  DevPtr d;
-  // the tiles of B (optionally paired with op(A)'s source tile) touching the uplo part
-  void build(const NatDesc& B, int uplo, const NatDesc* A, int trans) {
-    for (int n = 0; n < B.nt; ++n)
-      for (int m = 0; m < B.mt; ++m) {
-        if ((uplo == LOWER && m < n) || (uplo == UPPER && m > n)) continue;
-        if (!B.local(m, n)) continue;   // (a multi-process context: this rank's tiles)
-        const long long ao = A ? (trans == NOTRANS ? A->off(m, n) : A->off(n, m)) : B.off(m, n);
-        it.push_back(TileItem{A ? ao : B.off(m, n), B.off(m, n), B.rows(m), B.cols(n), m * B.mb, n * B.nb});
-        mm = std::max(mm, B.rows(m));
-        nn = std::max(nn, B.cols(n));
-      }
-  }
-  bool upload(NatProgram& P) {
-    if (it.empty()) return true;
-    d = dev_upload(it);
-    if (!d) return false;
-    P.keep.push_back(d);
-    return true;
-  }
-  int n() const { return (int)it.size(); }
-  const void* items() const { return d ? d->p : nullptr; }
-};
+
 
 namespace {
 std::shared_ptr<NatDesc> work_desc(NatProgram& P, const NatDesc& A);
@@ -2079,8 +2054,9 @@ bool has_fullT(const NatDesc& A, const NatDesc& T) {
 NatProgram* nat_geqrf(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dplasma_desc_t* dT) {
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *T = dT ? dT->nat : nullptr;
-  if (!same_ctx(c, {A, T}, prec)) return fail(nullptr, "geqrf: descriptors of another context or precision");
+  if (!same_ctx_dist(c, {A, T}, prec)) return fail(nullptr, "geqrf: descriptors of another context or precision");
   if (!qr_conform(A, T)) return fail(nullptr, "geqrf: square tiles <= 256 and a T of (IB x NB) tiles covering A");
+  if (c->dist()) return nat_dist_geqrf(c, *A, *T);
   NatProgram* P = new_program(c, "geqrf", true);
   int last = -1;
   if (!P->info || !add_geqrf(*P, *A, *T, last)) return fail(P, "geqrf: device allocation failed");
@@ -2091,10 +2067,14 @@ NatProgram* nat_unmqr(dplasma_context_t* ctx, int prec, int side, int trans, dpl
                       dplasma_desc_t* dC) {
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *T = dT ? dT->nat : nullptr, *C = dC ? dC->nat : nullptr;
-  if (!same_ctx(c, {A, T, C}, prec)) return fail(nullptr, "unmqr: descriptors of another context or precision");
+  if (!same_ctx_dist(c, {A, T, C}, prec)) return fail(nullptr, "unmqr: descriptors of another context or precision");
   if (!qr_conform(A, T) || !has_fullT(*A, *T)) return fail(nullptr, "unmqr: T must come from the native geqrf of A");
   if ((side == LEFT && (C->m != A->m || C->mb != A->mb)) || (side == RIGHT && (C->n != A->m || C->nb != A->mb)))
     return fail(nullptr, "unmqr: C does not conform to Q");
+  if (c->dist()) {
+    if (side != LEFT) return fail(nullptr, "unmqr: a multi-process context applies Q from the left");
+    return nat_dist_unmqr(c, trans, *A, *T, *C);
+  }
   NatProgram* P = new_program(c, "unmqr", false);
   int last = -1;
   if (!add_unmqr(*P, side, trans, *A, *T, *C, last)) return fail(P, "unmqr: device allocation failed");
@@ -2304,8 +2284,13 @@ NatProgram* nat_gels(dplasma_context_t* ctx, int prec, int trans, dplasma_desc_t
                      dplasma_desc_t* dB) {
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *T = dT ? dT->nat : nullptr, *B = dB ? dB->nat : nullptr;
-  if (!same_ctx(c, {A, T, B}, prec)) return fail(nullptr, "gels: descriptors of another context or precision");
+  if (!same_ctx_dist(c, {A, T, B}, prec)) return fail(nullptr, "gels: descriptors of another context or precision");
   if (trans != NOTRANS) return fail(nullptr, "gels: NoTrans (native engine)");
+  if (c->dist()) {
+    if (A->m < A->n || !qr_conform(A, T) || B->m != A->m || B->mb != A->mb)
+      return fail(nullptr, "gels: a multi-process context solves M >= N least squares (T of IB x NB tiles, B with A's rows)");
+    return nat_dist_gels(c, *A, *T, *B);
+  }
   NatProgram* P = new_program(c, "gels", true);
   int last = -1;
   if (A->m >= A->n) {
@@ -2320,4 +2305,19 @@ NatProgram* nat_gels(dplasma_context_t* ctx, int prec, int trans, dplasma_desc_t
       return fail(P, "gels: device allocation failed");
   }
   return P;
+}
+
+// tau_j = T_k(j, j) of a native geqrf's T (the compact-WY diagonal: LAPACK's tau), j < k, to host memory
+int nat_qr_tau(dplasma_desc_t* dT, void* tau, int k) {
+  NatDesc* T = dT ? dT->nat : nullptr;
+  if (!T || !T->fullT || k <= 0) return -1;
+  const int nb = T->fullT_nb, es = T->es;
+  if ((k + nb - 1) / nb > T->fullT_kt) return -1;
+  for (int p = 0; p * nb < k; ++p) {
+    const int c = std::min(nb, k - p * nb);
+    if (hipMemcpy2D((char*)tau + (size_t)p * nb * es, es, (const char*)T->fullT->p + (size_t)p * nb * nb * es,
+                    (size_t)(nb + 1) * es, es, c, hipMemcpyDefault) != hipSuccess)
+      return -1;
+  }
+  return 0;
 }

@@ -709,3 +709,302 @@ int nat_redistribute(dplasma_context_t* ctx, int es, char* src, int slld, int mb
   for (void* p : dbufs) (void)hipFree(p);
   return rc;
 }
+
+// ------------------------------------------------------------------------------------------------- QR
+// Flat-tree Householder QR, Q application and least squares on the grid (reference: src/zgeqrf.jdf,
+// zunmqr_LC.jdf and zgels_wrapper.c on a P x Q process grid; the data movement of ScaLAPACK's pdgeqrf:
+// a panel factorisation, then the block reflector applied as C -= V T^H (V^H C) with V^H C summed over
+// each process column).  Step k:
+//   1. the panel (tile column k, rows k..) goes to every rank (owners pack, one exchange) and every rank
+//      factors it redundantly with the persistent panel kernel (dpl_qr_panel: deterministic, so R, V and T
+//      come out identical everywhere, the distributed LU's scheme) -- T_k is kept on every rank (fullT);
+//   2. this rank's tiles of the factored panel go back into A (R above, V below the diagonal: LAPACK's
+//      layout, tau_j = T_k(j, j)); T(k, k)'s owner stores the reference-layout IB x IB diagonal blocks;
+//   3. this rank's rows of V are packed in local row order (Vloc); W = Vloc^H C_loc over its trailing tiles
+//      (one MFMA GEMM), the partial W goes to the process column's other ranks (one exchange) and theirs
+//      are added; C_loc -= Vloc (T^H W) (two GEMMs).
+// unmqr (left): V_k of tile column k is rebuilt from A by the ranks of that process column and sent
+// along the process rows; then step 3 on C's tiles.  gels: geqrf, Q^H B, R X = (Q^H B)(0:N).
+namespace {
+
+// a view of the leading r x c part of a distributed matrix (same storage)
+std::shared_ptr<NatDesc> dist_view(const NatDesc& D, int r, int c) {
+  auto v = std::make_shared<NatDesc>();
+  v->ctx = D.ctx;
+  v->prec = D.prec, v->es = D.es, v->mb = D.mb, v->nb = D.nb, v->m = r, v->n = c;
+  v->mt = (r + D.mb - 1) / D.mb;
+  v->nt = (c + D.nb - 1) / D.nb;
+  v->P = D.P, v->Q = D.Q, v->myrow = D.myrow, v->mycol = D.mycol;
+  auto loc = [](int n, int b, int p, int np) {   // numroc from process 0
+    const int nbl = n / b, ext = nbl % np;
+    int x = (nbl / np) * b;
+    if (p < ext) x += b;
+    else if (p == ext) x += n % b;
+    return x;
+  };
+  v->lm = loc(r, D.mb, D.myrow, D.P);
+  v->ln = loc(c, D.nb, D.mycol, D.Q);
+  v->lld = D.lld;
+  v->data = D.data;
+  v->owned = false;
+  return v;
+}
+
+// first local row (tile row) >= k and first local column (tile column) >= j0 of D on this rank
+long long first_local_row(const NatDesc& D, int k) {
+  for (int m = k; m < D.mt; ++m)
+    if (m % D.P == D.myrow) return (long long)(m / D.P) * D.mb;
+  return D.lm;
+}
+long long first_local_col(const NatDesc& D, int j0) {
+  for (int n = j0; n < D.nt; ++n)
+    if (n % D.Q == D.mycol) return (long long)(n / D.Q) * D.nb;
+  return D.ln;
+}
+
+struct DistQrWork {
+  DevPtr pan, V, ws, Vl, W, W2, Wr, slots;
+  int ldv = 0, ldvl = 0, wcols = 0;
+};
+
+bool dist_qr_work(NatProgram& P, const NatDesc& A, const NatDesc& C, DistQrWork& w) {
+  const int es = A.es, nb = A.nb;
+  w.ldv = std::max(16, (A.m + 15) / 16 * 16);
+  w.ldvl = std::max(16, (A.lm + 15) / 16 * 16);
+  w.wcols = std::max(1, C.ln);
+  w.pan = dev_alloc((size_t)w.ldv * nb * es, false);
+  w.V = dev_alloc((size_t)w.ldv * nb * es, true);
+  w.ws = dev_alloc((size_t)dpl_qr_panel_ws_bytes(A.prec, nb, nb) + 256, true);
+  w.Vl = dev_alloc((size_t)w.ldvl * nb * es, true);
+  w.W = dev_alloc((size_t)nb * w.wcols * es, true);
+  w.W2 = dev_alloc((size_t)nb * w.wcols * es, true);
+  w.Wr = dev_alloc((size_t)std::max(1, A.P - 1) * nb * w.wcols * es, true);
+  w.slots = dev_alloc((size_t)std::max(1, A.mt) * A.mb * nb * es, false);
+  for (const DevPtr& d : {w.pan, w.V, w.ws, w.Vl, w.W, w.W2, w.Wr, w.slots}) {
+    if (!d) return false;
+    P.keep.push_back(d);
+  }
+  return true;
+}
+
+// step 3: C_loc (tile rows >= k, local columns from lc0) := op(I - V T V^H) C_loc, V = Vloc (ldvl, rows in
+// C's local row order starting at lr0); reduction over the process column.  Tasks on stream 1 after prev.
+int add_dist_left_apply(NatProgram& P, NatDesc& C, const DistQrWork& w, long long lr0, long long lc0, int kf,
+                        const char* Tk, int ldt, bool qt, int prev) {
+  NatComm* comm = P.ctx->comm;
+  const int prec = C.prec, es = C.es, ldc = C.lld, Pg = C.P, Q = C.Q, me = P.ctx->rank;
+  const int rows = (int)(C.lm - lr0), cols = (int)(C.ln - lc0);
+  if (cols <= 0 || kf <= 0) return prev;
+  const Scalar one(prec, 1.0), zero(prec, 0.0), m_one(prec, -1.0);
+  char *c = C.data, *vl = (char*)w.Vl->p, *W = (char*)w.W->p, *W2 = (char*)w.W2->p, *Wr = (char*)w.Wr->p;
+  const int ldvl = w.ldvl;
+  auto g1 = std::make_shared<Gemm>(), g2 = std::make_shared<Gemm>(), g3 = std::make_shared<Gemm>();
+  // one item per local tile column (the engine's 128 x 128 sub-tiles), W column offset = local column
+  for (long long j = lc0; j < C.ln; j += C.nb) {
+    const int nj = (int)std::min<long long>(C.nb, C.ln - j);
+    const long long wo = (j - lc0) * kf;
+    if (rows > 0) g1->add(wo, kf, nj, {KPair{0, lr0 + j * ldc, rows, 0}}, 0);
+    g2->add(wo, kf, nj, {KPair{0, wo, kf, 0}}, 0);
+    if (rows > 0) g3->add(lr0 + j * ldc, rows, nj, {KPair{0, wo, kf, 0}}, 0);
+  }
+  if ((!g1->empty() && !g1->upload(P)) || !g2->upload(P) || (!g3->empty() && !g3->upload(P))) return -2;
+  const size_t wbytes = (size_t)kf * cols * es;
+  auto sends = std::make_shared<std::vector<NatMsg>>(), recvs = std::make_shared<std::vector<NatMsg>>();
+  int slot = 0;
+  for (int r = 0; r < Pg; ++r) {
+    const int peer = r * Q + C.mycol;
+    if (peer == me) continue;
+    sends->push_back(NatMsg{peer, W, wbytes});
+    recvs->push_back(NatMsg{peer, Wr + (size_t)slot * wbytes, wbytes});
+    ++slot;
+  }
+  const int nsl = slot;
+  std::vector<TileItem> sum_it{TileItem{0, 0, kf, cols, 0, 0}};
+  DevPtr d_sum = dev_upload(sum_it);
+  if (!d_sum) return -2;
+  P.keep.push_back(d_sum);
+  return P.task(1, [=](hipStream_t s) {
+    int rc = 0;
+    if (g1->empty()) rc = hipMemsetAsync(W, 0, wbytes, s) == hipSuccess ? 0 : -1;
+    else rc = g1->launch(prec, CONJTRANS, NOTRANS, one, vl, ldvl, c, ldc, zero, W, kf, s);
+    if (rc == 0 && nsl) rc = comm->exchange(*sends, *recvs, s);
+    for (int q = 0; q < nsl && rc == 0; ++q)   // W += the column's other partials
+      rc = dpl_geadd(prec, 0, NOTRANS, 1, d_sum->p, kf, cols, one.ptr(), Wr + (size_t)q * wbytes, kf, one.ptr(), W, kf,
+                     0, s);
+    if (rc == 0) rc = g2->launch(prec, qt ? CONJTRANS : NOTRANS, NOTRANS, one, Tk, ldt, W, kf, zero, W2, kf, s);
+    if (rc == 0 && !g3->empty()) rc = g3->launch(prec, NOTRANS, NOTRANS, m_one, vl, ldvl, W2, kf, one, c, ldc, s);
+    return rc;
+  }, {prev});
+}
+
+}  // namespace
+
+bool nat_dist_geqrf_into(NatProgram& P, NatDesc& A, NatDesc& T) {
+  NatCtx* c = P.ctx;
+  NatComm* comm = c->comm;
+  const int prec = A.prec, mb = A.mb, nb = A.nb, ld = A.lld, es = A.es, me = c->rank;
+  const int kt = std::min(A.mt, A.nt);
+  DistQrWork w;
+  if (!dist_qr_work(P, A, A, w)) return false;
+  T.fullT = dev_alloc((size_t)std::max(1, kt) * nb * nb * es, true);
+  if (!T.fullT) return false;
+  T.fullT_nb = nb;
+  T.fullT_kt = kt;
+  P.keep.push_back(T.fullT);
+  char *a = A.data, *pan = (char*)w.pan->p, *V = (char*)w.V->p, *ws = (char*)w.ws->p, *vl = (char*)w.Vl->p;
+  char *tf = (char*)T.fullT->p, *sl = (char*)w.slots->p, *t = T.data;
+  int* info = (int*)P.info->p;
+  const int ldv = w.ldv, ldvl = w.ldvl, ldT = T.lld, ib = T.mb;
+  const size_t st = (size_t)mb * nb;
+  const Scalar one(prec, 1.0), zero(prec, 0.0);
+  int prev = -1;
+  for (int k = 0; k < kt; ++k) {
+    const int M = A.m - k * mb, kb = A.cols(k), kf = std::min(M, kb);
+    // ---- 1. the panel to every rank, packed tile by tile into the contiguous panel (ld ldv)
+    auto pk = std::make_shared<MapBatch>(), sc = std::make_shared<MapBatch>(), back = std::make_shared<MapBatch>();
+    auto vpk = std::make_shared<MapBatch>();
+    auto sends = std::make_shared<std::vector<NatMsg>>(), recvs = std::make_shared<std::vector<NatMsg>>();
+    long long vrow = 0;   // Vloc row of the next local tile
+    for (int m = k; m < A.mt; ++m) {
+      const int src = A.owner(m, k);
+      char* slot = sl + (size_t)m * st * es;
+      if (src == me) {
+        pk->it.push_back(TileItem{A.off(m, k), (long long)m * (long long)st, A.rows(m), kb, 0, 0});
+        back->it.push_back(TileItem{(long long)(m - k) * mb, A.off(m, k), A.rows(m), kb, 0, 0});
+        for (int r = 0; r < c->world; ++r)
+          if (r != me) sends->push_back(NatMsg{r, slot, st * es});
+      } else {
+        recvs->push_back(NatMsg{src, slot, st * es});
+      }
+      if (m % A.P == A.myrow) {   // my rows of V, local order
+        vpk->it.push_back(TileItem{(long long)(m - k) * mb, vrow, A.rows(m), kf, 0, 0});
+        vrow += A.rows(m);
+        vpk->mm = std::max(vpk->mm, A.rows(m));
+      }
+      sc->it.push_back(TileItem{(long long)m * (long long)st, (long long)(m - k) * mb, A.rows(m), kb, 0, 0});
+      pk->mm = sc->mm = back->mm = std::max(pk->mm, A.rows(m));
+    }
+    pk->nn = sc->nn = back->nn = kb;
+    vpk->nn = kf;
+    if (!pk->upload(P) || !sc->upload(P) || !back->upload(P) || !vpk->upload(P)) return false;
+    char* Tk = tf + (size_t)k * nb * nb * es;
+    prev = P.task(1, [=](hipStream_t s) {
+      int rc = pk->n() ? dpl_geadd(prec, 0, NOTRANS, pk->n(), pk->items(), pk->mm, pk->nn, one.ptr(), a, ld, zero.ptr(),
+                                   sl, mb, 1, s) : 0;
+      if (rc == 0 && (!sends->empty() || !recvs->empty())) rc = comm->exchange(*sends, *recvs, s);
+      if (rc == 0)
+        rc = dpl_geadd(prec, 0, NOTRANS, sc->n(), sc->items(), sc->mm, sc->nn, one.ptr(), sl, mb, zero.ptr(), pan, ldv, 1, s);
+      // ---- the factorisation, redundantly on every rank
+      if (rc == 0) rc = dpl_qr_panel(prec, pan, ldv, 0, 0, M, kb, kf, V, ldv, Tk, nb, ws, info, s);
+      // ---- 2. my tiles back; 3. my rows of V
+      if (rc == 0 && back->n())
+        rc = dpl_geadd(prec, 0, NOTRANS, back->n(), back->items(), back->mm, back->nn, one.ptr(), pan, ldv, zero.ptr(), a, ld,
+                       1, s);
+      if (rc == 0 && vpk->n())
+        rc = dpl_geadd(prec, 0, NOTRANS, vpk->n(), vpk->items(), vpk->mm, vpk->nn, one.ptr(), V, ldv, zero.ptr(), vl, ldvl,
+                       1, s);
+      return rc;
+    }, {prev});
+    if (T.local(k, k)) {   // the reference layout: IB x IB diagonal blocks of T_k into tile T(k, k)
+      std::vector<TileItem> ti;
+      for (int b0 = 0; b0 < kf; b0 += ib) {
+        const int bs = std::min(ib, kf - b0);
+        ti.push_back(TileItem{(long long)k * nb * nb + b0 + (long long)b0 * nb, T.off(k, k) + (long long)b0 * ldT, bs, bs, 0, 0});
+      }
+      DevPtr d_ti = dev_upload(ti);
+      if (!d_ti) return false;
+      P.keep.push_back(d_ti);
+      const int nti = (int)ti.size();
+      prev = P.task(1, [=](hipStream_t s) {
+        return dpl_geadd(prec, 0, NOTRANS, nti, d_ti->p, ib, ib, one.ptr(), tf, nb, zero.ptr(), t, ldT, 1, s);
+      }, {prev});
+    }
+    if (k + 1 >= A.nt) continue;
+    prev = add_dist_left_apply(P, A, w, first_local_row(A, k), first_local_col(A, k + 1), kf, Tk, nb, true, prev);
+    if (prev < -1) return false;
+  }
+  return true;
+}
+
+// C := op(Q) C with Q from nat_dist_geqrf_into (left side; C distributed like A's rows)
+bool nat_dist_unmqr_into(NatProgram& P, int trans, NatDesc& A, NatDesc& T, NatDesc& C) {
+  NatCtx* c = P.ctx;
+  NatComm* comm = c->comm;
+  const int prec = A.prec, mb = A.mb, nb = A.nb, ld = A.lld, es = A.es, me = c->rank, Q = A.Q;
+  const int kt = std::min(A.mt, A.nt);
+  DistQrWork w;
+  if (!dist_qr_work(P, A, C, w)) return false;
+  const bool qt = trans != NOTRANS;
+  char *a = A.data, *vl = (char*)w.Vl->p, *raw = (char*)w.pan->p, *tf = (char*)T.fullT->p;
+  const int ldvl = w.ldvl;
+  const Scalar one(prec, 1.0), zero(prec, 0.0);
+  int prev = last_task_on(P, 1);
+  for (int s = 0; s < kt; ++s) {
+    const int k = qt ? s : kt - 1 - s;   // Q^H C: panel 0 first; Q C: the last first
+    const int M = A.m - k * mb, kb = A.cols(k), kf = std::min(M, kb), pc = k % Q;
+    const long long lr0 = first_local_row(A, k), rows = A.lm - lr0;
+    // V_k rows of this process row: the column-k owner in my process row packs them (raw, ld ldvl) and
+    // sends them along the row; every rank builds Vloc (unit diagonal, zeros above it) from raw
+    auto sends = std::make_shared<std::vector<NatMsg>>(), recvs = std::make_shared<std::vector<NatMsg>>();
+    const size_t rbytes = (size_t)ldvl * kb * es;
+    if (rows > 0) {
+      if (A.mycol == pc) {
+        for (int q = 0; q < Q; ++q)
+          if (q != A.mycol) sends->push_back(NatMsg{A.myrow * Q + q, raw, rbytes});
+      } else {
+        recvs->push_back(NatMsg{A.myrow * Q + pc, raw, rbytes});
+      }
+    }
+    auto lt = std::make_shared<MapBatch>(), cp = std::make_shared<MapBatch>();
+    long long vrow = 0;
+    for (int m = k; m < A.mt; ++m) {
+      if (m % A.P != A.myrow) continue;
+      lt->it.push_back(TileItem{vrow, vrow, A.rows(m), kf, (m - k) * mb, 0});
+      cp->it.push_back(TileItem{vrow, vrow, A.rows(m), kf, (m - k) * mb, 0});
+      vrow += A.rows(m);
+      lt->mm = cp->mm = std::max(lt->mm, A.rows(m));
+    }
+    lt->nn = cp->nn = kf;
+    if (!lt->upload(P) || !cp->upload(P)) return false;
+    const bool mine = A.mycol == pc && rows > 0;
+    const long long coff = lr0 + (long long)(k / Q) * nb * ld;   // my column-k rows in A (when mine)
+    prev = P.task(1, [=](hipStream_t st) {
+      int rc = 0;
+      if (mine && hipMemcpy2DAsync(raw, (size_t)ldvl * es, a + coff * es, (size_t)ld * es, (size_t)rows * es, kb,
+                                   hipMemcpyDeviceToDevice, st) != hipSuccess)
+        rc = -1;
+      if (rc == 0 && (!sends->empty() || !recvs->empty())) rc = comm->exchange(*sends, *recvs, st);
+      if (rc == 0 && lt->n()) rc = dpl_laset(prec, 0, lt->n(), lt->items(), lt->mm, lt->nn, zero.ptr(), one.ptr(), vl, ldvl, st);
+      if (rc == 0 && cp->n())   // part 3: strictly below the panel's diagonal
+        rc = dpl_geadd(prec, 3, NOTRANS, cp->n(), cp->items(), cp->mm, cp->nn, one.ptr(), raw, ldvl, zero.ptr(), vl, ldvl, 1, st);
+      return rc;
+    }, {prev});
+    prev = add_dist_left_apply(P, C, w, first_local_row(C, k), 0, kf, tf + (size_t)k * nb * nb * es, nb, qt, prev);
+    if (prev < -1) return false;
+  }
+  return true;
+}
+
+NatProgram* nat_dist_geqrf(NatCtx* c, NatDesc& A, NatDesc& T) {
+  NatProgram* P = new_program(c, "geqrf", true);
+  if (!P->info || !nat_dist_geqrf_into(*P, A, T)) return fail(P, "geqrf: device allocation failed");
+  return P;
+}
+
+NatProgram* nat_dist_unmqr(NatCtx* c, int trans, NatDesc& A, NatDesc& T, NatDesc& C) {
+  NatProgram* P = new_program(c, "unmqr", false);
+  if (!nat_dist_unmqr_into(*P, trans, A, T, C)) return fail(P, "unmqr: device allocation failed");
+  return P;
+}
+
+NatProgram* nat_dist_gels(NatCtx* c, NatDesc& A, NatDesc& T, NatDesc& B) {
+  NatProgram* P = new_program(c, "gels", true);
+  if (!P->info || !nat_dist_geqrf_into(*P, A, T) || !nat_dist_unmqr_into(*P, CONJTRANS, A, T, B))
+    return fail(P, "gels: device allocation failed");
+  auto R = dist_view(A, A.n, A.n), X = dist_view(B, A.n, B.n);
+  P->wdesc.push_back(R);
+  P->wdesc.push_back(X);
+  if (!nat_dist_trsm_into(*P, LEFT, UPPER, NOTRANS, NONUNIT, Scalar(A.prec, 1.0), *R, *X))
+    return fail(P, "gels: device allocation failed");
+  return P;
+}

@@ -272,6 +272,34 @@ struct NatProgram {
 
 namespace natk {
 
+// tile-wise maps / copies: one item per tile of B (paired with op(A)'s source tile), one dpl_geadd / dpl_laset launch
+struct MapBatch {
+  std::vector<TileItem> it;
+  int mm = 0, nn = 0;
+  DevPtr d;
+  // the tiles of B (optionally paired with op(A)'s source tile) touching the uplo part
+  void build(const NatDesc& B, int uplo, const NatDesc* A, int trans) {
+    for (int n = 0; n < B.nt; ++n)
+      for (int m = 0; m < B.mt; ++m) {
+        if ((uplo == LOWER && m < n) || (uplo == UPPER && m > n)) continue;
+        if (!B.local(m, n)) continue;   // (a multi-process context: this rank's tiles)
+        const long long ao = A ? (trans == NOTRANS ? A->off(m, n) : A->off(n, m)) : B.off(m, n);
+        it.push_back(TileItem{A ? ao : B.off(m, n), B.off(m, n), B.rows(m), B.cols(n), m * B.mb, n * B.nb});
+        mm = std::max(mm, B.rows(m));
+        nn = std::max(nn, B.cols(n));
+      }
+  }
+  bool upload(NatProgram& P) {
+    if (it.empty()) return true;
+    d = dev_upload(it);
+    if (!d) return false;
+    P.keep.push_back(d);
+    return true;
+  }
+  int n() const { return (int)it.size(); }
+  const void* items() const { return d ? d->p : nullptr; }
+};
+
 struct Gemm {
   std::vector<GemmItemK> it;
   std::vector<KPair> kp;
@@ -386,6 +414,11 @@ bool nat_dist_gemm_into(NatProgram& Pr, int prec, int tA, int tB, const Scalar& 
 bool nat_dist_mirror_into(NatProgram& Pr, const NatDesc& A, int uplo, int mtrans, NatDesc& W);
 bool nat_dist_trsm_into(NatProgram& Pr, int side, int uplo, int trans, int diag, const Scalar& alpha, NatDesc& A,
                         NatDesc& B);
+bool nat_dist_geqrf_into(NatProgram& P, NatDesc& A, NatDesc& T);
+bool nat_dist_unmqr_into(NatProgram& P, int trans, NatDesc& A, NatDesc& T, NatDesc& C);
+NatProgram* nat_dist_geqrf(NatCtx* c, NatDesc& A, NatDesc& T);
+NatProgram* nat_dist_unmqr(NatCtx* c, int trans, NatDesc& A, NatDesc& T, NatDesc& C);
+NatProgram* nat_dist_gels(NatCtx* c, NatDesc& A, NatDesc& T, NatDesc& B);
 
 // A := al A on this rank's tiles of the uplo part, appended after everything already in P (native.cpp)
 bool nat_add_lascal(NatProgram& P, int uplo, const Scalar& al, NatDesc& A);

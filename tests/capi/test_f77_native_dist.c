@@ -230,6 +230,52 @@ int main(int argc, char **argv) {
     CHECK(outside_ok && (n2m == 0 || e2 / n2m < 1e-12), "unaligned pdgemm_ diff %.3e", n2m > 0 ? e2 / n2m : 0.0);
     free(a2), free(c2), free(x2), free(gi2), free(gj2);
   }
+  /* ---- pdlatsqr_: tall-skinny QR of fa (N x NS) on the grid; |R| = |chol(A^T A)^T| entry by entry (R's rows
+   * are determined up to sign), tau in [1, 2] (real Householder) */
+  {
+    const int NS = 150;
+    int ns = NS, lwork = -1;
+    const int lnq = numroc_(&ns, &nbv, &mycol, &zero, &Q);
+    int descq[9];
+    descinit_(descq, &n, &ns, &nbv, &nbv, &zero, &zero, &ictxt, &lld, &info);
+    double *q = malloc(sizeof(double) * lld * (lnq > 0 ? lnq : 1)), *tau = malloc(sizeof(double) * NS), wq = 0;
+    for (int lj = 0; lj < lnq; ++lj)
+      for (int li = 0; li < lm; ++li) q[li + (size_t)lj * lld] = fa(gi[li], gj[lj]);
+    pdlatsqr_(&n, &ns, q, &one, &one, descq, tau, &wq, &lwork, &info);
+    CHECK(info == 0 && wq > 0, "pdlatsqr_ workspace query: info %d work %g", info, wq);
+    lwork = (int)wq;
+    double *work = malloc(sizeof(double) * (lwork > 0 ? lwork : 1));
+    pdlatsqr_(&n, &ns, q, &one, &one, descq, tau, work, &lwork, &info);
+    CHECK(info == 0, "pdlatsqr_ info %d: %s", info, dplasma_last_error());
+    double *G2 = malloc(sizeof(double) * NS * NS);   /* host Cholesky of A^T A (lower) */
+    for (int j = 0; j < NS; ++j)
+      for (int i = 0; i < NS; ++i) {
+        double acc = 0;
+        for (int k = 0; k < N; ++k) acc += fa(k, i) * fa(k, j);
+        G2[i + (size_t)j * NS] = acc;
+      }
+    for (int k = 0; k < NS; ++k) {
+      const double d = sqrt(G2[k + (size_t)k * NS]);
+      G2[k + (size_t)k * NS] = d;
+      for (int i = k + 1; i < NS; ++i) G2[i + (size_t)k * NS] /= d;
+      for (int j = k + 1; j < NS; ++j)
+        for (int i = j; i < NS; ++i) G2[i + (size_t)j * NS] -= G2[i + (size_t)k * NS] * G2[j + (size_t)k * NS];
+    }
+    double eq = 0, nq = 0;
+    for (int lj = 0; lj < lnq; ++lj)
+      for (int li = 0; li < lm; ++li)
+        if (gi[li] <= gj[lj]) {   /* R(i, j) = +-L(j, i) */
+          const double y = fabs(G2[gj[lj] + (size_t)gi[li] * NS]);
+          eq = fmax(eq, fabs(fabs(q[li + (size_t)lj * lld]) - y));
+          nq = fmax(nq, y);
+        }
+    int tau_ok = 1;
+    for (int j = 0; j < NS; ++j) tau_ok = tau_ok && tau[j] >= 1.0 - 1e-12 && tau[j] <= 2.0 + 1e-12;
+    printf("rank %d: pdlatsqr_ %dx%d on %dx%d grid: local max rel diff |R| %.3e, tau %s\n", me, N, NS, P, Q,
+           nq > 0 ? eq / nq : 0.0, tau_ok ? "in [1, 2]" : "OUT OF RANGE");
+    CHECK(tau_ok && (nq == 0 || eq / nq < 1e-11), "pdlatsqr_ |R| differs by %.3e", nq > 0 ? eq / nq : 0.0);
+    free(q), free(tau), free(work), free(G2);
+  }
   CHECK(!dplasma_python_active(), "the embedded interpreter was started");
   parsec_fini_wrapper_();
   if (fails) {

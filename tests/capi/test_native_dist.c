@@ -312,6 +312,53 @@ static void test_lu(int prec, int m, int n, int nrhs, int nb) {
   free(X), free(Y), free(p0), free(p1);
 }
 
+/* flat QR on the grid (geqrf, Q^H B, gels) against the one-process engine on the whole matrix: R / V
+ * tiles, the T blocks' owner tile, Q^H B and the least-squares solution, each rank on its tiles */
+static void test_qr(int m, int n, int nrhs, int nb, int ib) {
+  const int mt = (m + nb - 1) / nb, nt = (n + nb - 1) / nb;
+  dplasma_desc_t *A[2], *T[2], *B[2], *B2[2];
+  dplasma_context_t *cx[2] = {cd, c1};
+  int ok = 1;
+  for (int s = 0; s < 2; ++s) {
+    A[s] = mat(cx[s], dplasmaRealDouble, nb, m, n);
+    B[s] = mat(cx[s], dplasmaRealDouble, nb, m, nrhs);
+    B2[s] = mat(cx[s], dplasmaRealDouble, nb, m, nrhs);
+    T[s] = dplasma_desc_block_cyclic(cx[s], dplasmaRealDouble, ib, nb, mt * ib, nt * nb, 0, 0, dplasmaUpperLower);
+    ok = ok && A[s] && B[s] && B2[s] && T[s];
+  }
+  CHECK(ok, "qr descriptors: %s", dplasma_last_error());
+  if (!ok) return;
+  for (int s = 0; s < 2; ++s) {
+    int rc = dplasma_dplrnt(cx[s], 0, A[s], 71) | dplasma_dplrnt(cx[s], 0, B[s], 72) | dplasma_dplrnt(cx[s], 0, B2[s], 72);
+    const int info = dplasma_dgeqrf(cx[s], A[s], T[s]);
+    rc |= dplasma_dunmqr(cx[s], dplasmaLeft, dplasmaTrans, A[s], T[s], B[s]);
+    CHECK(rc == 0 && info == 0, "geqrf / unmqr (%s context): info %d rc %d %s", s ? "one-process" : "distributed", info,
+          rc, dplasma_last_error());
+  }
+  double *X = calloc((size_t)m * n, 8), *Y = calloc((size_t)m * n, 8);
+  double *U = calloc((size_t)m * nrhs, 8), *V = calloc((size_t)m * nrhs, 8);
+  CHECK(dplasma_desc_get_lapack(A[0], X, m) == 0 && dplasma_desc_get_lapack(A[1], Y, m) == 0, "get_lapack");
+  const double ea = cmp_local(X, Y, 0, m, n, nb, 'A');
+  CHECK(dplasma_desc_get_lapack(B[0], U, m) == 0 && dplasma_desc_get_lapack(B[1], V, m) == 0, "get_lapack");
+  const double eb = cmp_local(U, V, 0, m, nrhs, nb, 'A');
+  /* least squares on fresh copies */
+  for (int s = 0; s < 2; ++s) {
+    int rc = dplasma_dplrnt(cx[s], 0, A[s], 71);
+    const int info = dplasma_dgels(cx[s], dplasmaNoTrans, A[s], T[s], B2[s]);
+    CHECK(rc == 0 && info == 0, "gels (%s context): info %d %s", s ? "one-process" : "distributed", info,
+          dplasma_last_error());
+  }
+  CHECK(dplasma_desc_get_lapack(B2[0], U, m) == 0 && dplasma_desc_get_lapack(B2[1], V, m) == 0, "get_lapack");
+  const double ex = cmp_local(U, V, 0, m, nrhs, nb, 'A');
+  if (rank == 0)
+    printf("dgeqrf / dunmqr / dgels %dx%d nrhs=%d grid %dx%d: max rel diff R,V %.2e  Q^T B %.2e  X %.2e\n", m, n, nrhs, P, Q,
+           ea, eb, ex);
+  CHECK(ea < 1e-12 && eb < 1e-12 && ex < 1e-10, "distributed QR differs: %.2e %.2e %.2e", ea, eb, ex);
+  for (int s = 0; s < 2; ++s)
+    dplasma_desc_destroy(A[s]), dplasma_desc_destroy(T[s]), dplasma_desc_destroy(B[s]), dplasma_desc_destroy(B2[s]);
+  free(X), free(Y), free(U), free(V);
+}
+
 /* transposed maps on the grid (a tile-by-tile distributed transpose): geadd / tradd with op(A) */
 static void test_trans_maps(int cplx, int uplo, int m, int n, int nb) {
   const int prec = cplx ? dplasmaComplexDouble : dplasmaRealDouble, es = cplx ? 16 : 8;
@@ -440,9 +487,9 @@ static void test_taskpool_and_refusal(void) {
     CHECK(dplasma_taskpool_result(tp) == 0, "taskpool info %d", dplasma_taskpool_result(tp));
     dplasma_dpotrf_Destruct(tp);
   }
-  /* no distributed QR builder: a clean error on every rank, the context stays usable */
-  const int rc = dplasma_dgeqrf(cd, A, B);
-  CHECK(rc != 0 && strstr(dplasma_last_error(), "multi-process"), "dgeqrf on a multi-process context: rc %d '%s'", rc,
+  /* no distributed LQ builder: a clean error on every rank, the context stays usable */
+  const int rc = dplasma_dgelqf(cd, A, B);
+  CHECK(rc != 0 && strstr(dplasma_last_error(), "multi-process"), "dgelqf on a multi-process context: rc %d '%s'", rc,
         dplasma_last_error());
   CHECK(dplasma_dlange(cd, dplasmaMaxNorm, A) > 0, "context usable after a refused call");
   dplasma_desc_destroy(A), dplasma_desc_destroy(B);
@@ -504,6 +551,8 @@ int main(int argc, char **argv) {
   test_posv(dplasmaRealDouble, dplasmaLower, 900, 130, 128);
   test_posv(dplasmaRealDouble, dplasmaUpper, 900, 130, 128);
   test_posv(dplasmaComplexDouble, dplasmaLower, 400, 70, 64);
+  test_qr(700, 450, 30, 64, 16);
+  test_qr(512, 512, 64, 128, 32);
   test_trans_maps(0, dplasmaUpperLower, 530, 410, 64);
   test_trans_maps(1, dplasmaLower, 330, 330, 64);
   test_failing_potrf();
