@@ -70,25 +70,48 @@ int last_task_on(const NatProgram& P, int stream) {
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------- POTRF
+// The schedule of models/potrf_dist.py (the one tools/replay_potrf.py chose: profiles/r3_replay_*), in C++:
+// panels in blocks of D (DPLASMA_POTRF_DEFER, default 2; D = 1 once fewer than 24 columns remain), and
+// per panel k of block b = [c0, c1):
+//   POTRF(k) on the diagonal owner (panel stream 0)
+//   -> DIAG exchange: the factor to the other ranks holding panel tiles (communication stream 2)
+//   -> TRSM of this rank's panel tiles (one launch), packed into panel k's slab
+//   -> PANEL exchange: each tile from its owner straight to the ranks whose trailing tiles read it
+//   -> NEAR(k): the rest of block b's columns (panel stream)
+// and per block b, with every panel of the block in the k-runs (GEMM K = D x NB):
+//   NEXT(b)  the columns of block b+1 (panel stream: the critical path),
+//   NEXT2(b) the columns of block b+2 and REST2(b) everything beyond (update stream 1)
+// -- look-ahead 2: block b+1's panels run beside REST2(b-1) / NEXT2(b), the role of the reference's
+// high_priority POTRF / TRSM classes (src/zpotrf_L.jdf:58-69).  Panel slabs rotate over 3 blocks.
 NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
   const int prec = A.prec, nt = A.nt, mb = A.mb, es = A.es, me = c->rank, Pg = A.P, Qg = A.Q;
   const bool lower = uplo == LOWER;
   NatProgram* Pr = new_program(c, "potrf", true);
   if (!Pr->info) return fail(Pr, "potrf: device allocation failed");
-  const size_t slot_elems = (size_t)mb * mb;
-  DevPtr W = dev_alloc(2 * (size_t)std::max(1, nt) * slot_elems * es, false);
-  if (!W) return fail(Pr, "potrf: panel slots: device allocation failed");
+  const int D = std::max(1, env_int("DPLASMA_POTRF_DEFER", 2)), min_tiles = env_int("DPLASMA_POTRF_DEFER_MIN_TILES", 24);
+  std::vector<std::pair<int, int>> blocks;
+  for (int c0 = 0; c0 < nt;) {
+    const int d = nt - c0 >= min_tiles ? D : 1;
+    blocks.push_back({c0, std::min(nt, c0 + d)});
+    c0 += d;
+  }
+  const int NSLAB = 3;
+  const size_t slot_elems = (size_t)mb * mb, slab_elems = (size_t)D * std::max(1, nt) * slot_elems;
+  DevPtr W = dev_alloc(NSLAB * slab_elems * es, false);
+  if (!W) return fail(Pr, "potrf: panel slabs: device allocation failed");
   Pr->keep.push_back(W);
-  char* Wb[2] = {(char*)W->p, (char*)W->p + (size_t)nt * slot_elems * es};
-  // loopback (NatCtx::loop): the owner stages what it sends to itself in LB (double-buffered like W)
+  // loopback (NatCtx::loop): the owner stages what it sends to itself in LB (laid out like W)
   const bool loop = c->loop;
   DevPtr LBw;
   if (loop) {
-    LBw = dev_alloc(2 * (size_t)std::max(1, nt) * slot_elems * es, false);
-    if (!LBw) return fail(Pr, "potrf: loopback slots: device allocation failed");
+    LBw = dev_alloc(NSLAB * slab_elems * es, false);
+    if (!LBw) return fail(Pr, "potrf: loopback slabs: device allocation failed");
     Pr->keep.push_back(LBw);
   }
-  char* LBb[2] = {loop ? (char*)LBw->p : nullptr, loop ? (char*)LBw->p + (size_t)nt * slot_elems * es : nullptr};
+  // panel k's slab: (block parity, position in the block); tile i of the panel at slot i of it
+  auto slab = [&](char* base, int b, int k) {
+    return base + ((size_t)(b % NSLAB) * D + (k - blocks[b].first)) * std::max(1, nt) * slot_elems * es;
+  };
   auto slot = [&](int i) { return (long long)i * (long long)slot_elems; };
   auto tc = [&](int i, int k) { return lower ? std::make_pair(i, k) : std::make_pair(k, i); };
   auto own = [&](int i, int k) { const auto t = tc(i, k); return A.owner(t.first, t.second); };
@@ -106,11 +129,11 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
   const int side = lower ? RIGHT : LEFT, tri_mask = lower ? 1 : 2;
   const Scalar one(prec, 1.0), m_one(prec, -1.0);
   char* base = A.data;
+  char* wbase = (char*)W->p;
+  char* lbase = loop ? (char*)LBw->p : nullptr;
   const int ld = A.lld;
   int* info = (int*)Pr->info->p;
   const size_t sbytes = slot_elems * es;
-  // fp64 tiles <= 512: the dataflow tile kernel and the register-resident panel solve on its inverted 32-blocks
-  // (potrf_rb.hip, as the one-process engine); receivers invert the received factor's blocks themselves
   const bool rb = prec == P_D && A.mb == A.nb && A.mb <= 512 && env_int("DPLASMA_NATIVE_RB", 1) == 1;
   const int zsz = rb ? dpl_potrf_zbuf_size() : 0;
   DevPtr zb;
@@ -119,122 +142,152 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
     if (!zb) return fail(Pr, "potrf: device allocation failed");
     Pr->keep.push_back(zb);
   }
-
-  int next_prev = -1;                    // NEXT(k-1) (or the last panel-stream task of step k-1)
-  std::vector<int> rest(nt, -1), xch(nt, -1);   // latest update-stream / communication task after step k
-  for (int k = 0; k < nt; ++k) {
-    const int b = k % 2, kb = A.rows(k);
-    const int rest_km1 = k >= 1 ? rest[k - 1] : -1, rest_km2 = k >= 2 ? rest[k - 2] : -1;
-    const int xch_km2 = k >= 2 ? xch[k - 2] : -1;
-    const int own_k = A.owner(k, k);
-    char* wb = Wb[b];
-    char* sb = loop ? LBb[b] : wb;   // where this rank's outgoing panel data is staged
-    // POTRF(k): the diagonal tile has every update of steps < k (NEXT(k-1) and REST(k-2))
-    int t_diag = -1;
-    if (me == own_k) {
-      const long long dk = A.off(k, k);
-      double* zk = rb ? (double*)zb->p + (size_t)(k % 2) * zsz : nullptr;
-      const int t_potrf = Pr->task(0, [=](hipStream_t s) {
-        return rb ? dpl_potrf_tile_rbz(uplo, kb, (double*)base + dk, ld, info, k * mb, zk, s)
-                  : dpl_potrf_tile(prec, uplo, kb, base, dk, ld, info, k * mb, s);
-      }, {next_prev, rest_km2});
-      char* dst = sb + slot(k) * es;   // (run-time lambdas capture values only)
-      t_diag = Pr->task(0, [=](hipStream_t s) {
-        return hipMemcpy2DAsync(dst, (size_t)mb * es, base + dk * es, (size_t)ld * es, (size_t)kb * es, kb,
-                                hipMemcpyDeviceToDevice, s) == hipSuccess ? 0 : -1;
-      }, {t_potrf, xch_km2});
-    }
-    // DIAG exchange: the factor to every other rank holding a panel tile of step k
-    std::set<int> drc;
-    for (int i = k + 1; i < std::min(nt, k + 1 + (lower ? Pg : Qg)); ++i) drc.insert(own(i, k));
-    if (!loop) drc.erase(own_k);
-    std::vector<NatMsg> ds, dr;
-    if (me == own_k)
-      for (int r : drc) ds.push_back(NatMsg{r, sb + slot(k) * es, sbytes});
-    if (drc.count(me)) dr.push_back(NatMsg{own_k, wb + slot(k) * es, sbytes});
-    const int t_xd = add_exchange(*Pr, ds, dr, {t_diag, rest_km2, next_prev, xch_km2});
-    // TRSM of this rank's panel tiles against the factor in slot k, then pack them into their slots
-    auto tr = std::make_shared<Trsm1>();
-    auto pk = std::make_shared<CopyBatch>();
-    tr->tri = slot(k);
-    for (int i = k + 1; i < nt; ++i) {
-      const auto t = tc(i, k);
-      if (!A.local(t.first, t.second)) continue;
-      tr->add(A.off(t.first, t.second), A.rows(t.first), A.cols(t.second));
-      pk->add(A.off(t.first, t.second), slot(i), A.rows(t.first), A.cols(t.second));
-    }
-    int t_pack = -1;
-    if (!tr->it.empty() && rb) {
-      std::vector<RbItem> strips;   // 16-row strips of this rank's panel tiles (rows of L(i,k) / columns of U(k,i))
+  // GEMM batch of the trailing tiles in columns [n0, n1) (local), k-runs over panels ks (their slabs)
+  auto upd = [&](int b, const std::vector<int>& ks, int n0, int n1) {
+    auto g = std::make_shared<Gemm>();
+    for (int n_ = n0; n_ < n1; ++n_)
+      for (int m_ = n_; m_ < nt; ++m_) {
+        const int m = lower ? m_ : n_, n = lower ? n_ : m_;
+        if (!A.local(m, n)) continue;
+        std::vector<KPair> kp;
+        for (int k : ks) {
+          const long long so = (long long)(slab(wbase, b, k) - wbase) / es;
+          kp.push_back(KPair{so + slot(m), so + slot(n), A.rows(k), 0});
+        }
+        g->add(A.off(m, n), A.rows(m), A.cols(n), kp, m == n ? tri_mask : 0);
+      }
+    return g;
+  };
+  auto gemm_task = [&](int stream, std::shared_ptr<Gemm> g, std::initializer_list<int> deps) {
+    if (g->empty()) return -1;
+    if (!g->upload(*Pr)) return -2;
+    return Pr->task(stream, [=](hipStream_t s) {
+      return g->launch(prec, tA, tB, m_one, wbase, mb, wbase, mb, one, base, ld, s);
+    }, deps);
+  };
+  const int nbk = (int)blocks.size();
+  std::vector<int> next_of(nbk, -1), nxt2_of(nbk, -1), rest_of(nbk, -1), last_xch_of(nbk, -1);
+  int xch_prev = -1;   // the latest communication-stream task
+  for (int b = 0; b < nbk; ++b) {
+    const int c0 = blocks[b].first, c1 = blocks[b].second;
+    // every update of block b's columns from earlier blocks: NEXT(b-1) (panel stream, in order), NEXT2(b-2)
+    // and REST2(<= b-3) (update stream: REST2(b-3) precedes NEXT2(b-2) there)
+    const int upd_in = b >= 2 ? nxt2_of[b - 2] : -1;
+    // the slabs of block b were last read by block b-3's updates and sent by its exchanges
+    const int slab_free = b >= NSLAB ? rest_of[b - NSLAB] : -1;
+    const int slab_sent = b >= NSLAB ? last_xch_of[b - NSLAB] : -1;
+    for (int k = c0; k < c1; ++k) {
+      const int kb = A.rows(k), own_k = A.owner(k, k);
+      char* wb = slab(wbase, b, k);
+      char* sb = loop ? slab(lbase, b, k) : wb;   // where this rank's outgoing panel data is staged
+      int t_diag = -1;
+      if (me == own_k) {
+        const long long dk = A.off(k, k);
+        double* zk = rb ? (double*)zb->p + (size_t)(k % 2) * zsz : nullptr;
+        const int t_potrf = Pr->task(0, [=](hipStream_t s) {
+          return rb ? dpl_potrf_tile_rbz(uplo, kb, (double*)base + dk, ld, info, k * mb, zk, s)
+                    : dpl_potrf_tile(prec, uplo, kb, base, dk, ld, info, k * mb, s);
+        }, {upd_in});
+        char* dst = sb + slot(k) * es;
+        t_diag = Pr->task(0, [=](hipStream_t s) {
+          return hipMemcpy2DAsync(dst, (size_t)mb * es, base + dk * es, (size_t)ld * es, (size_t)kb * es, kb,
+                                  hipMemcpyDeviceToDevice, s) == hipSuccess ? 0 : -1;
+        }, {t_potrf, slab_free, slab_sent});
+      }
+      // DIAG exchange: the factor to every other rank holding a panel tile of step k
+      std::set<int> drc;
+      for (int i = k + 1; i < std::min(nt, k + 1 + (lower ? Pg : Qg)); ++i) drc.insert(own(i, k));
+      if (!loop) drc.erase(own_k);
+      std::vector<NatMsg> ds, dr;
+      if (me == own_k)
+        for (int r : drc) ds.push_back(NatMsg{r, sb + slot(k) * es, sbytes});
+      if (drc.count(me)) dr.push_back(NatMsg{own_k, wb + slot(k) * es, sbytes});
+      const int t_xd = add_exchange(*Pr, ds, dr, {t_diag, slab_free, slab_sent, xch_prev});
+      if (t_xd >= 0) xch_prev = t_xd;
+      // TRSM of this rank's panel tiles against the factor, then pack them into their slots
+      auto tr = std::make_shared<Trsm1>();
+      auto pk = std::make_shared<CopyBatch>();
+      tr->tri = slot(k);
       for (int i = k + 1; i < nt; ++i) {
         const auto t = tc(i, k);
         if (!A.local(t.first, t.second)) continue;
-        const int ext = lower ? A.rows(i) : A.cols(i);
-        for (int r0 = 0; r0 < ext; r0 += 16)
-          strips.push_back(RbItem{A.off(t.first, t.second) + (lower ? r0 : (long long)r0 * ld), std::min(16, ext - r0), 0});
+        tr->add(A.off(t.first, t.second), A.rows(t.first), A.cols(t.second));
+        pk->add(A.off(t.first, t.second), slot(i), A.rows(t.first), A.cols(t.second));
       }
-      DevPtr d = dev_upload(strips);
-      if (!d || !pk->upload(*Pr)) return fail(Pr, "potrf: device allocation failed");
-      Pr->keep.push_back(d);
-      const int nrb = (int)strips.size();
-      double* zk = (double*)zb->p + (size_t)(k % 2) * zsz;
-      const bool own = me == own_k && !loop;
-      const double* L = own ? (const double*)base + A.off(k, k) : (const double*)wb + slot(k);
-      const int ldl = own ? ld : mb;
-      const int t_trsm = Pr->task(0, [=](hipStream_t s) {
-        if (!own) {   // the factor came by exchange: invert its 32-blocks here
-          const int rc = dpl_trsm_rb_prep(uplo, kb, L, ldl, zk, s);
-          if (rc) return rc;
+      int t_pack = -1;
+      if (!tr->it.empty() && rb) {
+        std::vector<RbItem> strips;   // 16-row strips of this rank's panel tiles
+        for (int i = k + 1; i < nt; ++i) {
+          const auto t = tc(i, k);
+          if (!A.local(t.first, t.second)) continue;
+          const int ext = lower ? A.rows(i) : A.cols(i);
+          for (int r0 = 0; r0 < ext; r0 += 16)
+            strips.push_back(RbItem{A.off(t.first, t.second) + (lower ? r0 : (long long)r0 * ld), std::min(16, ext - r0), 0});
         }
-        return dpl_trsm_rb(uplo, kb, L, ldl, zk, nrb, d->p, (double*)base, ld, s);
-      }, {either(t_xd, t_diag), next_prev, rest_km2});
-      t_pack = Pr->task(0, [=](hipStream_t s) { return pk->launch(prec, base, ld, sb, mb, s); }, {t_trsm, xch_km2});
-    } else if (!tr->it.empty()) {
-      if (!tr->upload(*Pr, prec, side) || !pk->upload(*Pr)) return fail(Pr, "potrf: device allocation failed");
-      const int t_trsm = Pr->task(0, [=](hipStream_t s) {
-        return tr->launch(prec, side, uplo, CONJTRANS, NONUNIT, one, wb, mb, base, ld, s);
-      }, {either(t_xd, t_diag), next_prev, rest_km2});
-      t_pack = Pr->task(0, [=](hipStream_t s) { return pk->launch(prec, base, ld, sb, mb, s); }, {t_trsm, xch_km2});
-    }
-    // PANEL exchange: tile i from its owner to the ranks whose trailing tiles read it (ascending i:
-    // both sides of a pair enumerate their messages in the same order)
-    std::vector<NatMsg> ps, pr;
-    for (int i = k + 1; i < nt; ++i) {
-      const int src = own(i, k);
-      std::set<int> cs = consumers(k, i);
-      if (!loop) cs.erase(src);
-      if (src == me)
-        for (int r : cs) ps.push_back(NatMsg{r, sb + slot(i) * es, sbytes});
-      if (cs.count(me) && (src != me || loop))
-        pr.push_back(NatMsg{src, wb + slot(i) * es, sbytes});
-    }
-    const int t_xp = add_exchange(*Pr, ps, pr, {t_pack, t_xd, rest_km2, next_prev});
-    // trailing update: NEXT (column / row k+1) on the panel stream, REST on the update stream
-    auto gn = std::make_shared<Gemm>(), gr = std::make_shared<Gemm>();
-    for (int n_ = k + 1; n_ < nt; ++n_)
-      for (int m_ = n_; m_ < nt; ++m_) {
-        const int m = lower ? m_ : n_, n = lower ? n_ : m_;   // C(m, n) in the stored triangle
-        if (!A.local(m, n)) continue;
-        auto& g = (n_ == k + 1) ? gn : gr;
-        g->add(A.off(m, n), A.rows(m), A.cols(n), {KPair{slot(m), slot(n), kb, 0}}, m == n ? tri_mask : 0);
+        DevPtr d = dev_upload(strips);
+        if (!d || !pk->upload(*Pr)) return fail(Pr, "potrf: device allocation failed");
+        Pr->keep.push_back(d);
+        const int nrb = (int)strips.size();
+        double* zk = (double*)zb->p + (size_t)(k % 2) * zsz;
+        const bool ownf = me == own_k && !loop;
+        const double* L = ownf ? (const double*)base + A.off(k, k) : (const double*)(wb + slot(k) * es);
+        const int ldl = ownf ? ld : mb;
+        const int t_trsm = Pr->task(0, [=](hipStream_t s) {
+          if (!ownf) {   // the factor came by exchange: invert its 32-blocks here
+            const int rc = dpl_trsm_rb_prep(uplo, kb, L, ldl, zk, s);
+            if (rc) return rc;
+          }
+          return dpl_trsm_rb(uplo, kb, L, ldl, zk, nrb, d->p, (double*)base, ld, s);
+        }, {either(t_xd, t_diag), upd_in});
+        t_pack = Pr->task(0, [=](hipStream_t s) { return pk->launch(prec, base, ld, sb, mb, s); },
+                          {t_trsm, slab_free, slab_sent});
+      } else if (!tr->it.empty()) {
+        // the factor from the slab (the owner's copy or the received one), offset relative to the slabs' base
+        const long long to = (long long)((wb - wbase) / es) + slot(k);
+        for (TileItem& x : tr->it) x.a_off = to;
+        tr->tri = to;
+        if (!tr->upload(*Pr, prec, side) || !pk->upload(*Pr)) return fail(Pr, "potrf: device allocation failed");
+        const int t_trsm = Pr->task(0, [=](hipStream_t s) {
+          return tr->launch(prec, side, uplo, CONJTRANS, NONUNIT, one, wbase, mb, base, ld, s);
+        }, {either(t_xd, t_diag), upd_in});
+        t_pack = Pr->task(0, [=](hipStream_t s) { return pk->launch(prec, base, ld, sb, mb, s); },
+                          {t_trsm, slab_free, slab_sent});
       }
-    const int t_in = either(t_xp, either(t_pack, t_xd));
-    auto gemm = [=](std::shared_ptr<Gemm> g) {
-      return [=](hipStream_t s) { return g->launch(prec, tA, tB, m_one, wb, mb, wb, mb, one, base, ld, s); };
-    };
-    int t_next = -1;
-    if (!gn->empty()) {
-      if (!gn->upload(*Pr)) return fail(Pr, "potrf: device allocation failed");
-      t_next = Pr->task(0, gemm(gn), {t_in, rest_km1});
+      // PANEL exchange: tile i from its owner to the ranks whose trailing tiles read it (ascending i:
+      // both sides of a pair enumerate their messages in the same order)
+      std::vector<NatMsg> ps, pr;
+      for (int i = k + 1; i < nt; ++i) {
+        const int src = own(i, k);
+        std::set<int> cs = consumers(k, i);
+        if (!loop) cs.erase(src);
+        if (src == me)
+          for (int r : cs) ps.push_back(NatMsg{r, sb + slot(i) * es, sbytes});
+        if (cs.count(me) && (src != me || loop)) pr.push_back(NatMsg{src, wb + slot(i) * es, sbytes});
+      }
+      const int t_xp = add_exchange(*Pr, ps, pr, {t_pack, t_xd, slab_free, slab_sent, xch_prev});
+      if (t_xp >= 0) xch_prev = t_xp;
+      last_xch_of[b] = xch_prev;
+      // NEAR(k): the rest of this block with panel k (panel stream)
+      const int t_in = either(t_xp, either(t_pack, t_xd));
+      const int t_near = gemm_task(0, upd(b, {k}, k + 1, c1), {t_in});
+      if (t_near == -2) return fail(Pr, "potrf: device allocation failed");
     }
-    int t_rest = -1;
-    if (!gr->empty()) {
-      if (!gr->upload(*Pr)) return fail(Pr, "potrf: device allocation failed");
-      t_rest = Pr->task(1, gemm(gr), {t_in, rest_km1});
-    }
-    next_prev = either(t_next, either(t_pack, either(t_diag, next_prev)));
-    rest[k] = either(t_rest, rest_km1);
-    xch[k] = either(t_xp, either(t_xd, k >= 1 ? xch[k - 1] : -1));
+    if (c1 >= nt) break;
+    std::vector<int> ks;
+    for (int k = c0; k < c1; ++k) ks.push_back(k);
+    const int n1 = blocks[b + 1].second, n2 = b + 2 < nbk ? blocks[b + 2].second : nt;
+    const int t_in = xch_prev;
+    // NEXT(b) (critical): block b+1's columns; they are also written by NEXT2(b-1) and REST2(b-2)
+    next_of[b] = gemm_task(0, upd(b, ks, c1, n1), {t_in, b >= 1 ? nxt2_of[b - 1] : -1, b >= 2 ? rest_of[b - 2] : -1});
+    if (next_of[b] == -2) return fail(Pr, "potrf: device allocation failed");
+    nxt2_of[b] = gemm_task(1, upd(b, ks, n1, n2), {t_in});
+    if (nxt2_of[b] == -2) return fail(Pr, "potrf: device allocation failed");
+    rest_of[b] = gemm_task(1, upd(b, ks, n2, nt), {t_in});
+    if (rest_of[b] == -2) return fail(Pr, "potrf: device allocation failed");
+    // (an empty NEXT2 / REST2: the latest update-stream task stands for it)
+    const int last1 = last_task_on(*Pr, 1);
+    if (nxt2_of[b] < 0) nxt2_of[b] = last1;
+    if (rest_of[b] < 0) rest_of[b] = last1;
   }
   return Pr;
 }
