@@ -339,7 +339,54 @@ bool rendezvous(const std::string& dir, int rank, int world, bool pref_rccl, con
 
 }  // namespace
 
+// Rank replay on one GPU (DPLASMA_NATIVE_TRANSPORT=replay; tools/replay_native.py): this process is rank
+// `rank` of a `world`-rank grid with no peers.  An exchange moves no data: it is one busy-wait kernel on the
+// communication stream lasting lat + (the busiest peer link's bytes) / bw -- the timing model of
+// tools/replay_potrf.py's ReplayBackend without producer proxies (DPLASMA_REPLAY_BW GB/s per link,
+// DPLASMA_REPLAY_LAT us per exchange, DPLASMA_REPLAY_WG workgroups).  Host all-reduces return the local value.
+extern "C" int dpl_delay(double us, int nwg, hipStream_t st);
+class ReplayComm final : public NatComm {
+ public:
+  double bw = 50e3, lat = 15.0;   // bytes per us, us
+  int nwg = 4;
+  long long batches = 0;
+  double total_us = 0;
+  const char* name() const override { return "replay"; }
+  int exchange(const std::vector<NatMsg>& sends, const std::vector<NatMsg>& recvs, hipStream_t s) override {
+    if (sends.empty() && recvs.empty()) return 0;
+    std::vector<double> per(world, 0.0);
+    for (const NatMsg& m : sends) per[m.peer] += (double)m.bytes;
+    for (const NatMsg& m : recvs) per[m.peer] += (double)m.bytes;
+    double mx = 0;
+    for (double v : per) mx = std::max(mx, v);
+    const double us = lat + mx / bw;
+    ++batches;
+    total_us += us;
+    return dpl_delay(us, nwg, s);
+  }
+  int allreduce(double*, int, bool) override { return 0; }
+  ~ReplayComm() override {
+    if (std::getenv("DPLASMA_REPLAY_STATS"))
+      std::fprintf(stderr, "[replay rank %d] %lld exchanges, %.1f us modelled\n", rank, batches, total_us);
+  }
+};
+
 NatComm* nat_comm_create(int rank, int world, int device, const char* rdv_dir, std::string& err) {
+  {
+    const char* tv = std::getenv("DPLASMA_NATIVE_TRANSPORT");
+    if (tv && std::string(tv) == "replay") {
+      auto* c = new ReplayComm;
+      c->rank = rank;
+      c->world = world;
+      const char* v;
+      if ((v = std::getenv("DPLASMA_REPLAY_BW")) && *v) c->bw = std::atof(v) * 1e3;
+      if ((v = std::getenv("DPLASMA_REPLAY_LAT")) && *v) c->lat = std::atof(v);
+      if ((v = std::getenv("DPLASMA_REPLAY_WG")) && *v) c->nwg = std::max(1, std::atoi(v));
+      (void)device;
+      (void)rdv_dir;
+      return c;
+    }
+  }
   const char* env_dir = std::getenv("DPLASMA_NATIVE_RDV");
   const std::string dir = rdv_dir && *rdv_dir ? rdv_dir : env_dir ? env_dir : "";
   if (dir.empty()) { err = "no rendezvous directory (argument or DPLASMA_NATIVE_RDV)"; return nullptr; }
@@ -348,7 +395,7 @@ NatComm* nat_comm_create(int rank, int world, int device, const char* rdv_dir, s
   (void)hipGetDeviceCount(&ndev);
   const char* tv = std::getenv("DPLASMA_NATIVE_TRANSPORT");
   const std::string want = tv && *tv ? tv : "";
-  if (!want.empty() && want != "rccl" && want != "file") { err = "DPLASMA_NATIVE_TRANSPORT must be rccl or file"; return nullptr; }
+  if (!want.empty() && want != "rccl" && want != "file") { err = "DPLASMA_NATIVE_TRANSPORT must be rccl, file or replay"; return nullptr; }
   // this rank's preference; rank 0 decides for everyone (a per-rank choice could split the job)
   const bool pref_rccl = want.empty() ? ndev >= world : want == "rccl";
   Rccl rccl;
