@@ -94,36 +94,41 @@ __device__ inline int xcc_id() {
 
 __device__ inline long long toff(long long si, long long sj, int i, int j) { return (long long)i * si + (long long)j * sj; }
 
-__device__ inline bool ready(const DtrArgs& g, int t) {
-  const DtrTask tk = g.tasks[t];
-  for (int q = 0; q < tk.nreq; ++q) {
-    const int2 rq = g.reqs[tk.req_beg + q];
-    if (ld_sc1(g.cnt + rq.x) < rq.y) return false;
+// readiness of task t, checked by a whole wave: lane q < nreq tests requirement q (one round trip for
+// the requirement records and one for the counters, instead of nreq serial ones on one lane)
+__device__ inline bool ready_wave(const DtrArgs& g, int t) {
+  const int l = threadIdx.x & 63;
+  const int rb = __builtin_amdgcn_readfirstlane(g.tasks[t].req_beg);
+  const int nr = __builtin_amdgcn_readfirstlane((int)g.tasks[t].nreq);
+  bool ok = true;
+  if (l < nr) {
+    const int2 rq = g.reqs[rb + l];
+    ok = ld_sc1(g.cnt + rq.x) >= rq.y;
   }
-  return true;
+  return __builtin_amdgcn_ballot_w64(!ok) == 0;
 }
 
-// one claim attempt on a list; returns the task, -1 (head not ready), -2 (list exhausted)
+// one CAS claim attempt on a low list (wave 0): the task, -1 (head not ready), -2 (list exhausted)
 __device__ inline int try_list(const DtrArgs& g, int* cur, const int* list, int n) {
   for (int tries = 0; tries < 4; ++tries) {
-    const int h = ld_sc1(cur);
+    const int h = __builtin_amdgcn_readfirstlane(ld_sc1(cur));
     if (h >= n) return -2;
-    const int t = list[h];
-    if (!ready(g, t)) return -1;
-    if (atomicCAS(cur, h, h + 1) == h) return t;
+    const int t = __builtin_amdgcn_readfirstlane(list[h]);
+    if (!ready_wave(g, t)) return -1;
+    int won = 0;
+    if ((threadIdx.x & 63) == 0) won = atomicCAS(cur, h, h + 1) == h;
+    if (__builtin_amdgcn_readfirstlane(won)) return t;
   }
   return -1;
 }
 
-// lane 0: next task for this workgroup (-1 none ready yet, -2 everything claimed)
-__device__ inline int claim(const DtrArgs& g, int xcd) {
-  const int th = try_list(g, g.cur, g.hi, g.nhi);
-  if (th >= 0) return th;
-  bool all_done = th == -2;
+// wave 0: a ready task of the low lists -- its own XCD's list, another XCD's only once its own is
+// exhausted (-1 none ready yet, -2 every low list exhausted)
+__device__ inline int claim_low(const DtrArgs& g, int xcd) {
   const int own = try_list(g, g.cur + PSTRIDE * (1 + xcd), g.lo + g.lo_off[xcd], g.lo_off[xcd + 1] - g.lo_off[xcd]);
-  if (own >= 0) return own;
-  if (own == -1) return -1;   // own low list not exhausted: wait for its head
-  for (int d = 1; d < 8; ++d) {   // own list empty: help another XCD's
+  if (own != -2) return own;
+  bool all_done = true;
+  for (int d = 1; d < 8; ++d) {
     const int x = (xcd + d) & 7;
     const int t = try_list(g, g.cur + PSTRIDE * (1 + x), g.lo + g.lo_off[x], g.lo_off[x + 1] - g.lo_off[x]);
     if (t >= 0) return t;
@@ -318,23 +323,68 @@ __device__ __attribute__((noinline)) void run_potrf(const DtrArgs* __restrict__ 
 // The arguments live in device memory and are re-read through a laundered pointer every iteration:
 // hoisting all of DtrArgs into SGPRs across the task loop (what a by-value kernel argument invites)
 // leaves the GEMM body too few SGPRs and spills it to scratch.
+// The high list is handed out by TICKET (one atomic add per workgroup, no compare-and-swap retries on a
+// cursor that 512 workgroups contend for): a workgroup takes the next ticket, and while its task is not
+// ready yet it runs ready low-list tasks (a POTRF ticket only after 50 us: its 16 cooperating workgroups
+// should start together) -- the high list's claim rate no longer bounds the critical path (profiles/
+// r4_dtr_trace.txt: one CAS cursor gave ~4 us per claim, 86k claims).  Progress: tickets go out in list
+// order, so the earliest unfinished task in the topological order is ready and either held by a ticket
+// (its holder comes back to it) or the head of its low list (claimable by every workgroup that has
+// waited 50 us).
 __global__ __launch_bounds__(256, 2) void k_dtr_potrf(const DtrArgs* __restrict__ gargs) {
   __shared__ int s_task;
   const int tid = threadIdx.x;
   const int xcd = xcc_id();
   unsigned long long idle0 = 0;
-  int nap = 1;   // idle back-off (s_sleep units of 64 clocks), doubled up to ~1 us
+  int nap = 1;        // idle back-off (s_sleep units of 64 clocks), doubled up to ~1 us
+  int ticket = -1;    // held high-list position (wave 0's copy)
+  unsigned long long ticket_t0 = 0;
+  bool hi_done = false, lo_done = false;
   for (;;) {
     const DtrArgs* gp = gargs;
     asm volatile("" : "+s"(gp));
     const DtrArgs& g = *gp;
-    if (tid == 0) {
-      int t = ld_sc1(g.info) == -1000 ? -2 : claim(g, xcd);
+    if (tid < 64) {
+      int t = -1;
+      if (ld_sc1(g.info) == -1000) {
+        t = -2;
+      } else {
+        if (ticket < 0 && !hi_done) {
+          int tk = 0;
+          if (tid == 0) tk = atomicAdd(g.cur, 1);
+          tk = __builtin_amdgcn_readfirstlane(tk);
+          if (tk < g.nhi) {
+            ticket = tk;
+            ticket_t0 = __builtin_amdgcn_s_memrealtime();
+          } else {
+            hi_done = true;
+          }
+        }
+        bool help = true;
+        if (ticket >= 0) {
+          const int th = __builtin_amdgcn_readfirstlane(g.hi[ticket]);
+          if (ready_wave(g, th)) {
+            t = th;
+            ticket = -1;
+          } else if (__builtin_amdgcn_readfirstlane(g.tasks[th].type) == T_POTRF &&
+                     __builtin_amdgcn_s_memrealtime() - ticket_t0 < 5000ULL) {
+            help = false;   // a POTRF ticket polls for its first 50 us (the group starts together), then helps
+          }
+        }
+        if (t < 0 && help && !lo_done) {
+          t = claim_low(g, xcd);
+          if (t == -2) {
+            lo_done = true;
+            t = -1;
+          }
+        }
+        if (t < 0) t = (hi_done && lo_done && ticket < 0) ? -2 : -1;
+      }
       if (t >= 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the predecessors' bytes, fresh in this CU
+        if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the predecessors' bytes, fresh in this CU
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         idle0 = 0;
-      } else if (t == -1) {
+      } else if (t == -1 && tid == 0) {
         const unsigned long long now = __builtin_amdgcn_s_memrealtime();
         if (idle0 == 0) idle0 = now;
         else if (now - idle0 > 400000000ULL) {   // 4 s without a ready task: broken schedule, drain
@@ -342,7 +392,7 @@ __global__ __launch_bounds__(256, 2) void k_dtr_potrf(const DtrArgs* __restrict_
           t = -2;
         }
       }
-      s_task = t;
+      if (tid == 0) s_task = t;
     }
     __syncthreads();
     const int t = __builtin_amdgcn_readfirstlane(s_task);   // wave-uniform: task fields load to SGPRs

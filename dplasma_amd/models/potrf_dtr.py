@@ -311,6 +311,9 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     state = {"epoch": 0}
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     nwg = int(os.environ.get("DPLASMA_DTR_WG", 2 * ncu))
+    # progress needs a workgroup on every XCD (a low list is another XCD's to steal only once that XCD's
+    # own list is exhausted) and the 16 cooperating POTRF workgroups co-resident: at least 64 of them
+    nwg = max(64, min(nwg, 2 * ncu))
     tp._keep = (tasks_d, reqs_d, hi_d, lo_d, cnt, cur, W, Mw, Sw, Lp, Wp, prog, host, args_d)
     tp.dtr_plan = plan
 

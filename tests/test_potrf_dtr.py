@@ -17,14 +17,14 @@ T_UPD, T_TRSM, T_POTRF = D.T_UPD, D.T_TRSM, D.T_POTRF
 
 
 def _emulate(plan, A=None, nb=None, P=8, seed=0):
-    """Run the plan's claim protocol with random completion order; optional numpy math on A (lower,
-    nt x nt tiles of nb, sub-tiles of nb / 4).  Returns the claim order."""
+    """Run the plan's claim protocol with P workers and random completion order; optional numpy math on A
+    (lower, nt x nt tiles of nb, sub-tiles of nb / 4).  Returns the claim order."""
     rng = np.random.default_rng(seed)
     tasks, reqs = plan.tasks, plan.reqs
     cnt = np.zeros(plan.ncnt, dtype=np.int64)
     lists = [plan.hi] + [plan.lo[plan.lo_off[x]:plan.lo_off[x + 1]] for x in range(8)]
     cur = [0] * 9
-    inflight = []
+    inflight = []    # (task, start value, worker)
     claimed = np.zeros(len(tasks), dtype=bool)
     order = []
     s = nb // 4 if nb else None
@@ -72,30 +72,67 @@ def _emulate(plan, A=None, nb=None, P=8, seed=0):
         if tk["inc"] >= 0:
             cnt[tk["inc"]] += 1
 
+    # the kernel's claim protocol: high list by ticket (in order; a holder starts its task once ready and
+    # meanwhile helps with ready low-list heads -- a POTRF holder only after a while), low lists per XCD
+    # (own list first, another XCD's only once the own one is exhausted)
+    hi = lists[0]
+    hcur = 0
+    ticket = [None] * P
+    age = [0] * P
+    busy = [False] * P
+    owner = {}
     stall = 0
+
+    def try_low(wk):
+        x = wk % 8
+        order = [x] + ([(x + d) % 8 for d in range(1, 8)] if cur[1 + x] >= len(lists[1 + x]) else [])
+        for xx in order:
+            li = 1 + xx
+            lst = lists[li]
+            if cur[li] < len(lst) and ready(lst[cur[li]]):
+                t = int(lst[cur[li]])
+                cur[li] += 1
+                return t
+        return None
+
     while True:
         progressed = False
-        if len(inflight) < P:
-            for li in range(9):
-                lst = lists[li]
-                if cur[li] < len(lst) and ready(lst[cur[li]]):
-                    t = int(lst[cur[li]])
-                    cur[li] += 1
-                    claimed[t] = True
-                    order.append(t)
-                    inflight.append((t, start(t)))
-                    progressed = True
-                    break
+        for wk in rng.permutation(P):
+            if busy[wk]:
+                continue
+            if ticket[wk] is None and hcur < len(hi):
+                ticket[wk], age[wk] = hcur, 0
+                hcur += 1
+            t = None
+            if ticket[wk] is not None:
+                th = int(hi[ticket[wk]])
+                if ready(th):
+                    t, ticket[wk] = th, None
+                else:
+                    age[wk] += 1
+            if t is None and (ticket[wk] is None or tasks["type"][hi[ticket[wk]]] != T_POTRF or age[wk] > 3
+                              or stall):
+                t = try_low(wk)
+            if t is None:
+                continue
+            claimed[t] = True
+            order.append(t)
+            inflight.append((t, start(t), wk))
+            busy[wk] = True
+            progressed = True
         if not progressed and inflight:
             q = int(rng.integers(len(inflight)))
-            t, v = inflight.pop(q)
+            t, v, wk = inflight.pop(q)
+            busy[wk] = False
             finish(t, v)
             progressed = True
         if not progressed:
-            if all(cur[li] >= len(lists[li]) for li in range(9)):
+            if hcur >= len(hi) and all(x is None for x in ticket) and all(cur[li] >= len(lists[li]) for li in range(1, 9)):
                 break
             stall += 1
-            assert stall < 3, f"schedule stalled with heads {[cur[li] for li in range(9)]}"
+            assert stall < 50, f"schedule stalled: tickets {ticket}, heads {[cur[li] for li in range(9)]}"
+        else:
+            stall = 0
     assert claimed.all()
     return order
 
@@ -109,7 +146,7 @@ def test_dtr_plan_lists_and_progress(nt, defer):
     n_potrf = (plan.tasks["type"] == T_POTRF).sum()
     assert n_potrf == 16 * nt
     for seed in range(3):
-        _emulate(plan, P=1 + 7 * seed, seed=seed)
+        _emulate(plan, P=(8, 13, 40)[seed], seed=seed)   # >= 1 worker per XCD, as the kernel's grid has
 
 
 @pytest.mark.parametrize("nt,defer", [(5, 2), (7, 4)])
@@ -121,7 +158,7 @@ def test_dtr_plan_numerics(nt, defer):
     S = M @ M.T + n * np.eye(n)
     A = S.copy()
     plan = D._Plan(nt, defer)
-    _emulate(plan, A=A, nb=nb, P=6, seed=3)
+    _emulate(plan, A=A, nb=nb, P=8, seed=3)
     L = np.tril(A)
     assert np.abs(L - np.linalg.cholesky(S)).max() < 1e-10
 
