@@ -27,6 +27,7 @@ Two transports, the same semantics (ties resolved by the smallest position, LAPA
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 
@@ -136,6 +137,31 @@ def release_all():
     """Unmap and free every cached exchange buffer (call on every rank, e.g. before fini)."""
     for key in list(_XCHG):
         _XCHG.pop(key).close()
+
+
+def _at_exit():
+    """Interpreter exit with exchange buffers still cached (a script that never called release_all):
+    the peers' IPC mappings must be closed before the HIP runtime's own static teardown runs, or that
+    teardown can fault in __cxa_finalize -- what ended a 2-rank rehearsal under rocprofv3 with SIGSEGV
+    after its SUCCESS line (round 3, gpurun_out/b2_lud_r0.log).  Collective release while the process
+    group lives; otherwise only the local unmapping (my exported buffer goes with the process)."""
+    if not _XCHG:
+        return
+    try:
+        if dist.is_available() and dist.is_initialized():
+            release_all()
+            return
+    except Exception:   # a peer already gone: fall through to the local cleanup
+        pass
+    lib = _lib.load()
+    for xc in list(_XCHG.values()):
+        for p in xc._opened:
+            lib.dpl_xchg_close(ctypes.c_void_p(p))
+        xc._opened = []
+    _XCHG.clear()
+
+
+atexit.register(_at_exit)
 
 
 def _block_host(P, ld, m, c0, cend, kbw, tr, diag, pos, ipiv, info, info_base, xc: PanelXchg):

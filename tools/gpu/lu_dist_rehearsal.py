@@ -87,6 +87,8 @@ def main():
           f"no host sync inside a panel: {mode == 'ipc'}, "
           f"pivots identical to one process: {same}, max |factor diff| {diff:.2e} : "
           f"{'SUCCESS' if ok else 'FAIL'}", flush=True)
+    from dplasma_amd.ops import lu_dist_ops
+    lu_dist_ops.release_all()   # IPC mappings closed before the runtime's teardown (see lu_dist_ops._at_exit)
     dist.destroy_process_group()
     sys.exit(0 if int(flags[0]) == 1 else 1)
 
