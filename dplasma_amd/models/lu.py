@@ -556,7 +556,7 @@ class _GetrfDev:
                 ops.rows_move(True, A.data, A.ld, A.mb, r0, self.rowoff, cr, nr, A.nb, msrc, mcnt, ldb, self.tmp,
                               ldb)
                 if g.P > 1:
-                    dist.all_reduce(self.tmp, group=ctx.col_group)
+                    comm.allreduce(self.tmp, group=ctx.col_group)
                 ops.rows_move(False, A.data, A.ld, A.mb, r0, self.rowoff, cr, nr, A.nb, mdst, mcnt, ldb, self.tmp,
                               ldb)
             if cur is not None and k == self.kt - 1:

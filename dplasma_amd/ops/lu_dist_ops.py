@@ -263,6 +263,9 @@ class DistPanelLU:
                                                _lib.stream_ptr())
                     _lib.check(rc, "lu_block_dist")
                     xc.epoch += cend - c0
+                    us = getattr(xc, "model_us_per_col", 0.0)
+                    if us > 0:   # rank replay (tools/replay_lu.py): the cross-rank hand-offs as modelled latency
+                        _lib.check(lib.dpl_delay(float(us * (cend - c0)), 1, _lib.stream_ptr()), "delay")
                 else:
                     _block_host(Pb, ld, m, c0, cend, self.kb, self.tr, self.diag, self.pos, ipiv, info, info_base,
                                 xc)

@@ -1,0 +1,119 @@
+#!/usr/bin/env python3
+"""Rank replay of the distributed partial-pivoting LU (getrf_ptgpanel, BASELINE config 5) on ONE GPU.
+
+Builds the exact ``getrf_ptgpanel_New`` program of rank r of a P x Q grid (models/lu.py _GetrfDev: its
+local tiles, panel buffers, row moves, U broadcasts, trailing GEMMs) and runs it on the visible GPU with
+the transport replaced by the timing model of tools/replay_potrf.py (every collective / point-to-point
+exchange = one busy-wait kernel of lat + bytes / bw on a communication stream, no data moved).  The
+distributed panel kernel (csrc/kernels/lu_dist.hip) runs on this rank's rows plus the diagonal replica
+with a one-rank exchange group, and each column's cross-rank hand-off -- IPC stores over xGMI on a real
+grid -- is modelled as ``--xlat`` microseconds per column on the panel's stream.
+
+usage: python tools/replay_lu.py -N 65536 --nb 512 --grid 2x4 [--ranks all] [--steps 1] [--bw 50]
+       [--lat 15] [--xlat 6]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import dplasma_amd as dp  # noqa: E402
+from dplasma_amd.ops import lu_dist_ops  # noqa: E402
+from dplasma_amd.parallel import comm  # noqa: E402
+from replay_potrf import ReplayBackend, fake_rank_context  # noqa: E402
+
+
+class ReplayXchg:
+    """A one-rank exchange group for the distributed panel kernel (its own slot is the only peer), with
+    the per-column cross-rank hand-off modelled as a delay (lu_dist_ops.PanelLU.run)."""
+
+    def __init__(self, kbw, dtype, device, xlat_us):
+        from dplasma_amd.ops import _lib
+        lib = _lib.load()
+        self.group, self.me, self.P = None, 0, 1
+        self.slot_bytes = int(lib.dpl_lu_dist_slot_bytes(_lib.prec_code(dtype), kbw))
+        self.buf = torch.zeros(2 * self.slot_bytes // 8 + 8, dtype=torch.float64, device=device)
+        self.peers = torch.tensor([self.buf.data_ptr()], dtype=torch.int64, device=device)
+        self.epoch = 1
+        self.ok = True
+        self.model_us_per_col = xlat_us
+
+    def close(self):
+        pass
+
+
+def replay_rank(base, P, Q, rank, N, NB, steps, xlat):
+    ctx = fake_rank_context(base, P, Q, rank)
+    orig = lu_dist_ops.panel_xchg
+    lu_dist_ops.panel_xchg = lambda group, me, P_, kbw, dtype, device, max_rows=0: ReplayXchg(kbw, dtype, device, xlat)
+    try:
+        A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N, name="A")
+        dp.plrnt(ctx, A, 3872)
+        A0 = A.data.clone()
+        IP = dp.ptgpanel_ipiv_descriptor(ctx, A)
+        t0 = time.perf_counter()
+        tp = dp.getrf_ptgpanel_New(ctx, A, IP)
+        enq = time.perf_counter() - t0
+        times = []
+        for s in range(steps + 1):
+            A.data.copy_(A0)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            tp.run(ctx)
+            torch.cuda.synchronize()
+            if s > 0:
+                times.append(time.perf_counter() - t0)
+        del A, A0, tp
+        torch.cuda.empty_cache()
+    finally:
+        lu_dist_ops.panel_xchg = orig
+    return min(times), enq
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-N", type=int, default=65536)
+    ap.add_argument("--nb", type=int, default=512)
+    ap.add_argument("--grid", default="2x4")
+    ap.add_argument("--ranks", default="all")
+    ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--bw", type=float, default=50.0)
+    ap.add_argument("--lat", type=float, default=15.0)
+    ap.add_argument("--comm-wg", type=int, default=4)
+    ap.add_argument("--xlat", type=float, default=6.0, help="us per panel column (cross-rank pivot hand-off)")
+    args = ap.parse_args()
+    P, Q = map(int, args.grid.lower().split("x"))
+    base = dp.init(device="cuda:0")
+    be = ReplayBackend(base.device, args.bw, args.lat, args.comm_wg, proxies=False)
+    comm.set_backend(be)
+    ranks = range(P * Q) if args.ranks == "all" else [int(x) for x in args.ranks.split(",")]
+    from dplasma_amd.utils.flops import flops
+    fl = flops("d", "getrf", args.N, args.N)
+    res = {}
+    for r in ranks:
+        t, enq = replay_rank(base, P, Q, r, args.N, args.nb, args.steps, args.xlat)
+        res[r] = t
+        print(f"rank {r} ({r // Q},{r % Q}): {t * 1e3:9.2f} ms   enq {enq:.2f} s", flush=True)
+    worst = max(res.values())
+    ideal = fl / (78.6e12 * P * Q)
+    print(json.dumps({"op": "getrf_ptgpanel", "N": args.N, "NB": args.nb, "grid": f"{P}x{Q}", "bw_GBs": args.bw,
+                      "lat_us": args.lat, "xlat_us_per_col": args.xlat, "worst_ms": round(worst * 1e3, 2),
+                      "ideal_ms": round(ideal * 1e3, 2), "pct_peak": round(100 * ideal / worst, 1),
+                      "tflops_job": round(fl / worst / 1e12, 1),
+                      "per_rank_ms": {str(k): round(v * 1e3, 2) for k, v in res.items()},
+                      "knobs": {k: v for k, v in os.environ.items() if k.startswith("DPLASMA_")},
+                      "comm": {k: (round(v, 1) if isinstance(v, float) else v) for k, v in be.stats.items()}}),
+          flush=True)
+
+
+if __name__ == "__main__":
+    main()
