@@ -78,7 +78,15 @@ def _strides(A):
 class _Plan:
     """The task table of one factorisation (identical for every run of the same shape)."""
 
-    def __init__(self, nt: int, D: int):
+    def __init__(self, nt: int, D: int, lo_order: str = None):
+        # low-list order: "panel" -- (last panel block, column, ...): the bulk runs breadth-first, block by
+        # block; "column" -- (column block, last panel block, column, ...): a column block's remaining old
+        # updates before the next column block's, so the first panel of a block does not wait behind the
+        # whole previous bulk.  Both are subsequences of one topological order (column blocks ascending; in
+        # a block, its low-list updates, then its high-list tasks), which the deadlock argument needs.
+        lo_order = lo_order or os.environ.get("DPLASMA_DTR_LO_ORDER", "column")
+        if lo_order not in ("panel", "column"):
+            raise ValueError("DPLASMA_DTR_LO_ORDER must be panel or column")
         S = 4 * nt
         self.nt, self.S, self.D = nt, S, D
         WB = S * S                      # counter index of W_k's "block columns done" count
@@ -142,7 +150,10 @@ class _Plan:
                 # key: column, phase (0 diagonal tile, 2 other rows), last panel, row, sub-tile
                 key = np.stack([j, np.where(i == j, 0, 2), np.full(n, kl), i, r, c], 1)
                 return emit(T_UPD, i, j, k0, r, c, nk, Ci, reqs, None, "hi", key=key)
-            key = np.stack([np.full(n, kl), j, i, r, c], 1)
+            if lo_order == "column":
+                key = np.stack([j // D, np.full(n, kl), j, i, r, c], 1)
+            else:
+                key = np.stack([np.full(n, kl), j, i, r, c], 1)
             return emit(T_UPD, i, j, k0, r, c, nk, Ci, reqs, None, "lo", key=key, xcd=j % 8)
 
         blocks = [(b0, min(nt, b0 + D)) for b0 in range(0, nt, D)]
@@ -263,10 +274,11 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     PST = _check_layout(lib)
     nt = A.nt
     D = max(1, int(os.environ.get("DPLASMA_DTR_DEFER", "4")))
-    key = (nt, D)
+    lo_order = os.environ.get("DPLASMA_DTR_LO_ORDER", "column")
+    key = (nt, D, lo_order)
     plan = _PLANS.get(key)
     if plan is None:
-        plan = _PLANS[key] = _Plan(nt, D)
+        plan = _PLANS[key] = _Plan(nt, D, lo_order)
     dev = A.device
     tp = Taskpool("potrf", ctx)
     tp.flops = flops(A.prec, "potrf", A.n)

@@ -137,9 +137,10 @@ def _emulate(plan, A=None, nb=None, P=8, seed=0):
     return order
 
 
+@pytest.mark.parametrize("lo_order", ["column", "panel"])
 @pytest.mark.parametrize("nt,defer", [(1, 4), (3, 4), (9, 4), (12, 2), (10, 3)])
-def test_dtr_plan_lists_and_progress(nt, defer):
-    plan = D._Plan(nt, defer)
+def test_dtr_plan_lists_and_progress(nt, defer, lo_order):
+    plan = D._Plan(nt, defer, lo_order)
     ids = np.concatenate([plan.hi, plan.lo])
     assert len(ids) == len(plan.tasks) and len(np.unique(ids)) == len(ids)
     assert (plan.tasks["nreq"] <= 10).all()
@@ -149,15 +150,16 @@ def test_dtr_plan_lists_and_progress(nt, defer):
         _emulate(plan, P=(8, 13, 40)[seed], seed=seed)   # >= 1 worker per XCD, as the kernel's grid has
 
 
+@pytest.mark.parametrize("lo_order", ["column", "panel"])
 @pytest.mark.parametrize("nt,defer", [(5, 2), (7, 4)])
-def test_dtr_plan_numerics(nt, defer):
+def test_dtr_plan_numerics(nt, defer, lo_order):
     nb = 16
     n = nt * nb
     rng = np.random.default_rng(7)
     M = rng.standard_normal((n, n))
     S = M @ M.T + n * np.eye(n)
     A = S.copy()
-    plan = D._Plan(nt, defer)
+    plan = D._Plan(nt, defer, lo_order)
     _emulate(plan, A=A, nb=nb, P=8, seed=3)
     L = np.tril(A)
     assert np.abs(L - np.linalg.cholesky(S)).max() < 1e-10
