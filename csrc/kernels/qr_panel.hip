@@ -141,13 +141,23 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
         v[0] += __shfl_xor(v[0], 1, 64);
         if ((l & 1) == 0) red[wv][l >> 1] = v[0];
         if (rowok && grow == j) {
-          T* rj = rowj + par * QP_B;
+          if (G == 1) {   // one workgroup: row j's snapshot through LDS
 #pragma unroll
-          for (int s = 0; s < QP_B; ++s)
-            if (s < sh) st_sc1(&rj[s], a[s]);
+            for (int s = 0; s < QP_B; ++s) fin[QP_B + s] = s < sh ? a[s] : T(0);
+          } else {
+            T* rj = rowj + par * QP_B;
+#pragma unroll
+            for (int s = 0; s < QP_B; ++s)
+              if (s < sh) st_sc1(&rj[s], a[s]);
+          }
         }
       }
       __syncthreads();
+      if (G == 1) {
+        // one workgroup: the four waves' partials are the whole sum -- no global round trip
+        if (tid < QP_B) fin[tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+        __syncthreads();
+      } else {
       if (tid < QP_B) {
         const T d = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
         st_sc1(&part1[((long long)par * G + w) * QP_B + tid], d);
@@ -189,6 +199,7 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
         fin[tid] = d;
       }
       __syncthreads();
+      }
       QP_TICK(2);
       // dlarfg (every thread derives the same scalars); slot 0 is column jj
       const T alpha = fin[QP_B], x2 = fin[0];
@@ -244,7 +255,7 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
     const long long E = (long long)QP_B * nX;
     for (int x0 = 0; x0 < nX; x0 += QP_B) {
       const int cw = min(QP_B, nX - x0);
-      T* pw = part2 + (long long)w * E;
+      T* pw = G == 1 ? Yg : part2 + (long long)w * E;   // one workgroup: its partial IS Y
       if (act) {
         if (tid < R16) {
           // chunks never straddle the V_b | V_prev | A_rest boundaries (b0 is a multiple of 32)
@@ -277,7 +288,12 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int p = pt * 16 + MM::drow(l, r), q = qt * 16 + (l & 15);
-          if (q < cw) st_sc1(&pw[(long long)p * nX + x0 + q], (a0[r] + a1[r]) + (a2[r] + a3[r]));
+          if (q < cw) {
+            const T y = (a0[r] + a1[r]) + (a2[r] + a3[r]);
+            st_sc1(&pw[(long long)p * nX + x0 + q], y);
+            const int xc = x0 + q;
+            if (G == 1 && xc >= QP_B && xc < QP_B + b0) st_sc1(&Xc[((long long)b * QP_B + p) * kf + xc - QP_B], y);
+          }
         }
         __syncthreads();
       } else {
@@ -286,6 +302,10 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
       }
     }
     QP_TICK(3);
+    if (G == 1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    } else {
     ++nsync;
     grid_sync_counter(cnt, nsync * G, info);
     // ------------------------------------------------------------ Y = sum of partials
@@ -324,6 +344,7 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
     }
     ++nsync;
     grid_sync_counter(cnt, nsync * G, info);
+    }
     // ------------------------------------------------------------ T_b from taus and the Gram block
     for (int e = tid; e < QP_B * QP_B; e += 256) {
       const int c = e >> 5, k = e & 31;
@@ -411,13 +432,18 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
     QP_TICK(5);
   }
   // ------------------------------------------------------------ off-diagonal T blocks
-  // T(i, blk) = -T(i, 0:b0) Z, Z = X_b T_b, X_b = V_prev^T V_b; workgroup w owns T rows w, w+G, ...
+  // T(0:b0, blk) = -T(0:b0, 0:b0) Z, Z = X_b T_b, X_b = V_prev^T V_b.  Workgroup w owns the 16-row tiles
+  // w, w+G, ... of T for every block, so besides the diagonal blocks (final before the barrier) it reads
+  // only T rows it wrote itself.  Two row tiles at a time are staged in LDS and multiplied by Z with
+  // MFMA (the k-range of a row tile starts at its diagonal: T is upper triangular) -- was a scalar
+  // row-by-row loop whose global round trips cost ~0.7 ms per 256-column panel on one workgroup.
   if (nblk > 1) {
     ++nsync;
     grid_sync_counter(cnt, nsync * G, info);
     for (int b = 1; b < nblk; ++b) {
       const int b0 = b * QP_B, bw = min(QP_B, kf - b0);
-      if (w >= b0) continue;
+      const int nrt = b0 / 16;
+      if (w >= nrt) continue;
       for (int e = tid; e < QP_B * QP_B; e += 256) {
         const int c = e >> 5, k = e & 31;
         Ts[c][k] = (k <= c && c < bw) ? ld_sc1(&Tm[(b0 + k) + (long long)(b0 + c) * ldt]) : T(0);
@@ -432,29 +458,31 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
           Xs[c][tid] = z;   // Z(j = tid, c)
         }
       __syncthreads();
-      // own rows, 4 at a time: stage T(i, 0:b0) in LDS, then thread (c, row, half) sums over j
-      const int nown = (b0 - w + G - 1) / G;
-      T* trow = &Ws[0][0];   // [4][b0]
-      for (int o0 = 0; o0 < nown; o0 += 4) {
-        for (int e = tid; e < 4 * b0; e += 256) {
-          const int oi = e / b0, jx = e - oi * b0;
-          const int i = w + (o0 + oi) * G;
-          trow[e] = (o0 + oi < nown && jx >= i) ? ld_sc1(&Tm[i + (long long)jx * ldt]) : T(0);
+      T* trow = &Ab[0][0];   // [32][b0]: the staged T rows of two own row tiles
+      const int own_rt = (nrt - w + G - 1) / G;
+      for (int o0 = 0; o0 < own_rt; o0 += 2) {
+        for (int e = tid; e < 32 * b0; e += 256) {
+          const int rl = e / b0, k = e - rl * b0;
+          const int ot = o0 + (rl >> 4);
+          const int i = (w + ot * G) * 16 + (rl & 15);
+          trow[e] = (ot < own_rt && k >= i) ? ld_sc1(&Tm[i + (long long)k * ldt]) : T(0);
         }
         __syncthreads();
-        {
-          const int c = tid & 31, oi = (tid >> 5) & 3, hh = tid >> 7;
-          const int i = w + (o0 + oi) * G;
-          T s = T(0);
-          if (o0 + oi < nown)
-            for (int jx = i + hh; jx < b0; jx += 2) s += trow[oi * b0 + jx] * Xs[c][jx];
-          red[hh * 4 + oi][c] = s;
-        }
-        __syncthreads();
-        if (tid < 128) {
-          const int c = tid & 31, oi = tid >> 5;
-          const int i = w + (o0 + oi) * G;
-          if (o0 + oi < nown && c < bw) st_sc1(&Tm[i + (long long)(b0 + c) * ldt], -(red[oi][c] + red[4 + oi][c]));
+        const int ot = o0 + (wv >> 1), ch = wv & 1;
+        if (ot < own_rt) {
+          const int rt = w + ot * G, rl0 = (wv >> 1) * 16;
+          acc_t acc;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[r] = T(0);
+          for (int k0 = rt * 16; k0 < b0; k0 += 4) {
+            const int k = k0 + (l >> 4);
+            acc = MM::mma(trow[(rl0 + (l & 15)) * b0 + k], Xs[ch * 16 + (l & 15)][k], acc);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int c = ch * 16 + (l & 15);
+            if (c < bw) st_sc1(&Tm[(rt * 16 + MM::drow(l, r)) + (long long)(b0 + c) * ldt], -acc[r]);
+          }
         }
         __syncthreads();
       }
