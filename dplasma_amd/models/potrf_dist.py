@@ -189,6 +189,21 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     def f_upd(batch, base, ld):
         ops.gemm(tA, tB, -1.0, base, ld, base, ld, 1.0, A.data, A.ld, batch)
 
+    # DPLASMA_POTRF_BULK_CAP=c: the bulk updates (NEXT2 / REST2) as capped grid-stride GEMM launches of
+    # 2 x (CUs - c) workgroups (ops.gemm_wg_cap; the capped kernel no longer spills), so the panel chain's
+    # kernels find free workgroup slots at once -- the single-process engine's DPLASMA_POTRF_RESERVE
+    bulk_cap = 0
+    cap_res = int(env.get("DPLASMA_POTRF_BULK_CAP", "0"))
+    if cap_res > 0 and ctx.is_gpu:
+        bulk_cap = 2 * max(8, torch.cuda.get_device_properties(dev).multi_processor_count - cap_res)
+
+    def f_bulk(batch, base, ld):
+        if bulk_cap:
+            with ops.gemm_wg_cap(bulk_cap):
+                f_upd(batch, base, ld)
+        else:
+            f_upd(batch, base, ld)
+
     def wait_panels(ks):
         # the consumer's stream waits for the receives of panels ks (never for this rank's sends)
         for k in ks:
@@ -445,13 +460,13 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
         if len(nxt2):
             def f_nxt2(bt=nxt2, ks=ks):
                 wait_panels(ks)
-                f_upd(bt, GX, A.mb)
+                f_bulk(bt, GX, A.mb)
             nxt2_of[b] = tp.task(f"NEXT2({b})", upd_stream, f_nxt2, [gate, last_panel, prev_bulk], prio=1,
                                  comm=False)
         if len(rest):
             def f_rest(bt=rest, ks=ks):
                 wait_panels(ks)
-                f_upd(bt, GX, A.mb)
+                f_bulk(bt, GX, A.mb)
             rest_of[b] = tp.task(f"REST2({b})", upd_stream, f_rest, [gate, last_panel, prev_bulk, nxt2_of.get(b)],
                                  prio=0, comm=False)
         else:

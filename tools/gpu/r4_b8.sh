@@ -17,6 +17,9 @@ step() {
 step capi_native 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_capi.py -m gpu -k "native" || exit 1
 step replay_native_2x4 400 python tools/replay_native.py -N 65536 --nb 512 --grid 2x4 --steps 1 || exit 1
 step replay_python_2x4_noproxy 500 python tools/replay_potrf.py -N 65536 --nb 512 --grid 2x4 --steps 1 --no-proxy || exit 1
+step replay_python_2x4 500 python tools/replay_potrf.py -N 65536 --nb 512 --grid 2x4 --steps 1 || exit 1
+step replay_python_2x4_cap16 500 env DPLASMA_POTRF_BULK_CAP=16 python tools/replay_potrf.py -N 65536 --nb 512 --grid 2x4 --steps 1 || exit 1
+step replay_python_2x4_cap32 500 env DPLASMA_POTRF_BULK_CAP=32 python tools/replay_potrf.py -N 65536 --nb 512 --grid 2x4 --steps 1 || exit 1
 step replay_lu_2x4_x16 600 python tools/replay_lu.py -N 65536 --nb 512 --grid 2x4 --ranks 0,1,4,5 --xlat 16 || exit 1
 step replay_lu_2x4_x6 600 python tools/replay_lu.py -N 65536 --nb 512 --grid 2x4 --ranks 0,1,4,5 --xlat 6 || exit 1
 exit 0
