@@ -324,8 +324,8 @@ __device__ __attribute__((noinline)) void run_potrf(const DtrArgs* __restrict__ 
 // hoisting all of DtrArgs into SGPRs across the task loop (what a by-value kernel argument invites)
 // leaves the GEMM body too few SGPRs and spills it to scratch.
 // The high list is handed out by TICKET (one atomic add per workgroup, no compare-and-swap retries on a
-// cursor that 512 workgroups contend for): a workgroup takes the next ticket, and while its task is not
-// ready yet it runs ready low-list tasks (a POTRF ticket only after 50 us: its 16 cooperating workgroups
+// cursor that 512 workgroups contend for): a workgroup takes the next ticket when the list's head is
+// ready, and while a ticket's task is not ready yet (a race) it runs ready low-list tasks (a POTRF ticket only after 50 us: its 16 cooperating workgroups
 // should start together) -- the high list's claim rate no longer bounds the critical path (profiles/
 // r4_dtr_trace.txt: one CAS cursor gave ~4 us per claim, 86k claims).  Progress: tickets go out in list
 // order, so the earliest unfinished task in the topological order is ready and either held by a ticket
@@ -350,14 +350,22 @@ __global__ __launch_bounds__(256, 2) void k_dtr_potrf(const DtrArgs* __restrict_
         t = -2;
       } else {
         if (ticket < 0 && !hi_done) {
-          int tk = 0;
-          if (tid == 0) tk = atomicAdd(g.cur, 1);
-          tk = __builtin_amdgcn_readfirstlane(tk);
-          if (tk < g.nhi) {
-            ticket = tk;
-            ticket_t0 = __builtin_amdgcn_s_memrealtime();
-          } else {
+          // a ticket only for a ready head: a workgroup holding a not-yet-ready critical task would run
+          // low-list tasks meanwhile and come back up to one bulk task late -- the 16 POTRF workgroups of
+          // a tile would then start spread over ~0.4 ms and wait for each other
+          const int h = __builtin_amdgcn_readfirstlane(ld_sc1(g.cur));
+          if (h >= g.nhi) {
             hi_done = true;
+          } else if (ready_wave(g, __builtin_amdgcn_readfirstlane(g.hi[h]))) {
+            int tk = 0;
+            if (tid == 0) tk = atomicAdd(g.cur, 1);
+            tk = __builtin_amdgcn_readfirstlane(tk);
+            if (tk < g.nhi) {
+              ticket = tk;
+              ticket_t0 = __builtin_amdgcn_s_memrealtime();
+            } else {
+              hi_done = true;
+            }
           }
         }
         bool help = true;

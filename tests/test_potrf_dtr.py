@@ -72,8 +72,9 @@ def _emulate(plan, A=None, nb=None, P=8, seed=0):
         if tk["inc"] >= 0:
             cnt[tk["inc"]] += 1
 
-    # the kernel's claim protocol: high list by ticket (in order; a holder starts its task once ready and
-    # meanwhile helps with ready low-list heads -- a POTRF holder only after a while), low lists per XCD
+    # the kernel's claim protocol: high list by ticket (in order, taken when the head is ready; a holder
+    # whose task is not ready yet helps with ready low-list heads -- a POTRF holder only after a while),
+    # low lists per XCD
     # (own list first, another XCD's only once the own one is exhausted)
     hi = lists[0]
     hcur = 0
@@ -100,7 +101,8 @@ def _emulate(plan, A=None, nb=None, P=8, seed=0):
         for wk in rng.permutation(P):
             if busy[wk]:
                 continue
-            if ticket[wk] is None and hcur < len(hi):
+            if ticket[wk] is None and hcur < len(hi) and (ready(int(hi[hcur])) or rng.random() < 0.05):
+                # a ticket for a ready head (and, rarely, a raced one whose task is not ready yet)
                 ticket[wk], age[wk] = hcur, 0
                 hcur += 1
             t = None
