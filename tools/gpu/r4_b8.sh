@@ -20,6 +20,4 @@ step replay_python_2x4_noproxy 500 python tools/replay_potrf.py -N 65536 --nb 51
 step replay_python_2x4 500 python tools/replay_potrf.py -N 65536 --nb 512 --grid 2x4 --steps 1 || exit 1
 step replay_python_2x4_cap16 500 env DPLASMA_POTRF_BULK_CAP=16 python tools/replay_potrf.py -N 65536 --nb 512 --grid 2x4 --steps 1 || exit 1
 step replay_python_2x4_cap32 500 env DPLASMA_POTRF_BULK_CAP=32 python tools/replay_potrf.py -N 65536 --nb 512 --grid 2x4 --steps 1 || exit 1
-step replay_lu_2x4_x16 600 python tools/replay_lu.py -N 65536 --nb 512 --grid 2x4 --ranks 0,1,4,5 --xlat 16 || exit 1
-step replay_lu_2x4_x6 600 python tools/replay_lu.py -N 65536 --nb 512 --grid 2x4 --ranks 0,1,4,5 --xlat 6 || exit 1
 exit 0
