@@ -78,7 +78,7 @@ def _strides(A):
 class _Plan:
     """The task table of one factorisation (identical for every run of the same shape)."""
 
-    def __init__(self, nt: int, D: int, lo_order: str = None):
+    def __init__(self, nt: int, D: int, lo_order: str = None, min_tiles: int = None):
         # low-list order: "panel" -- (last panel block, column, ...): the bulk runs breadth-first, block by
         # block; "column" -- (column block, last panel block, column, ...): a column block's remaining old
         # updates before the next column block's, so the first panel of a block does not wait behind the
@@ -89,6 +89,20 @@ class _Plan:
             raise ValueError("DPLASMA_DTR_LO_ORDER must be panel or column")
         S = 4 * nt
         self.nt, self.S, self.D = nt, S, D
+        # blocks of D panels; single panels once fewer than min_tiles columns remain (the chain-bound tail:
+        # the stream engine's POTRF_DEFER_MIN_TILES rule)
+        if min_tiles is None:
+            min_tiles = int(os.environ.get("DPLASMA_DTR_DEFER_MIN_TILES", "0"))
+        blocks = []
+        b0 = 0
+        while b0 < nt:
+            d = D if nt - b0 >= min_tiles else 1
+            blocks.append((b0, min(nt, b0 + d)))
+            b0 += d
+        block_of = np.zeros(nt, dtype=np.int64)
+        for bi, (x0, x1) in enumerate(blocks):
+            block_of[x0:x1] = bi
+        self.blocks = blocks
         WB = S * S                      # counter index of W_k's "block columns done" count
         self.ncnt = WB + nt
         ver = np.zeros(S * S, dtype=np.int32)
@@ -151,12 +165,11 @@ class _Plan:
                 key = np.stack([j, np.where(i == j, 0, 2), np.full(n, kl), i, r, c], 1)
                 return emit(T_UPD, i, j, k0, r, c, nk, Ci, reqs, None, "hi", key=key)
             if lo_order == "column":
-                key = np.stack([j // D, np.full(n, kl), j, i, r, c], 1)
+                key = np.stack([block_of[j], np.full(n, kl), j, i, r, c], 1)
             else:
                 key = np.stack([np.full(n, kl), j, i, r, c], 1)
             return emit(T_UPD, i, j, k0, r, c, nk, Ci, reqs, None, "lo", key=key, xcd=j % 8)
 
-        blocks = [(b0, min(nt, b0 + D)) for b0 in range(0, nt, D)]
         for bi, (k0b, k1b) in enumerate(blocks):
             for k in range(k0b, k1b):
                 # POTRF(k, b): the diagonal tile's final versions (every update of it precedes)
@@ -193,7 +206,7 @@ class _Plan:
             # BULK(b): every later column, panels of the block as one k-run; the next block's columns
             # are high priority (the look-ahead), the rest low
             nk = k1b - k0b
-            hi_end = min(nt, k1b + D)
+            hi_end = blocks[bi + 1][1]
             for j in range(k1b, nt):
                 I, J, R, C = subtiles(np.arange(j, nt), np.full(nt - j, j))
                 upd(I, J, R, C, k0b, nk, j < hi_end)
@@ -275,10 +288,11 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     nt = A.nt
     D = max(1, int(os.environ.get("DPLASMA_DTR_DEFER", "4")))
     lo_order = os.environ.get("DPLASMA_DTR_LO_ORDER", "column")
-    key = (nt, D, lo_order)
+    min_tiles = int(os.environ.get("DPLASMA_DTR_DEFER_MIN_TILES", "0"))
+    key = (nt, D, lo_order, min_tiles)
     plan = _PLANS.get(key)
     if plan is None:
-        plan = _PLANS[key] = _Plan(nt, D, lo_order)
+        plan = _PLANS[key] = _Plan(nt, D, lo_order, min_tiles)
     dev = A.device
     tp = Taskpool("potrf", ctx)
     tp.flops = flops(A.prec, "potrf", A.n)

@@ -153,15 +153,15 @@ def test_dtr_plan_lists_and_progress(nt, defer, lo_order):
 
 
 @pytest.mark.parametrize("lo_order", ["column", "panel"])
-@pytest.mark.parametrize("nt,defer", [(5, 2), (7, 4)])
-def test_dtr_plan_numerics(nt, defer, lo_order):
+@pytest.mark.parametrize("nt,defer,min_tiles", [(5, 2, 0), (7, 4, 0), (11, 4, 6)])
+def test_dtr_plan_numerics(nt, defer, min_tiles, lo_order):
     nb = 16
     n = nt * nb
     rng = np.random.default_rng(7)
     M = rng.standard_normal((n, n))
     S = M @ M.T + n * np.eye(n)
     A = S.copy()
-    plan = D._Plan(nt, defer, lo_order)
+    plan = D._Plan(nt, defer, lo_order, min_tiles)
     _emulate(plan, A=A, nb=nb, P=8, seed=3)
     L = np.tril(A)
     assert np.abs(L - np.linalg.cholesky(S)).max() < 1e-10
