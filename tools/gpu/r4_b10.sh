@@ -22,6 +22,4 @@ step geqrf32k_flat 200 python tools/bench_algo.py geqrf -N 32768 --nb 256 --ib 3
 step hqr32k_a4 300 python tools/bench_algo.py geqrf -N 32768 --nb 256 --ib 32 --runs 2 --tree hqr --qr-llvl 1 --qr-hlvl 0 --qr-a -1 || exit 1
 step hqr32k_a16 300 python tools/bench_algo.py geqrf -N 32768 --nb 256 --ib 32 --runs 2 --tree hqr --qr-llvl 1 --qr-hlvl 0 --qr-a 16 || exit 1
 step luqr_sync32k 400 python tools/gpu/luqr_syncdebug.py 32768 256 || exit 1
-step replay_lu_2x4_x16 600 python tools/replay_lu.py -N 65536 --nb 512 --grid 2x4 --ranks 0,1,4,5 --xlat 16 || exit 1
-step replay_lu_2x4_x6 600 python tools/replay_lu.py -N 65536 --nb 512 --grid 2x4 --ranks 0,1,4,5 --xlat 6 || exit 1
 exit 0

@@ -51,10 +51,29 @@ class ReplayXchg:
         pass
 
 
+def _valid_pivots_panel(orig):
+    """The replay moves no data: a rank outside panel k's process column keeps a STALE pivot vector after the
+    modelled broadcast -- positions of an earlier, taller panel, which would send the row moves beyond this
+    panel's rows (the illegal memory access of round 4's first LU replay).  Clamp them into [j, mp) so the
+    moves stay a valid interchange sequence of the right size."""
+    def panel(self, k):
+        orig(self, k)
+        st = self.plan[k]
+        kmin, mp = st["kmin"], st["mp"]
+        if kmin > 0 and self.pivot:
+            j = torch.arange(kmin, dtype=torch.int32, device=self.piv_dev.device)
+            p = self.piv_dev[:kmin]
+            self.piv_dev[:kmin] = torch.maximum(torch.minimum(p, torch.full_like(p, mp - 1)), j)
+    return panel
+
+
 def replay_rank(base, P, Q, rank, N, NB, steps, xlat):
+    from dplasma_amd.models import lu as lu_mod
     ctx = fake_rank_context(base, P, Q, rank)
     orig = lu_dist_ops.panel_xchg
+    orig_panel = lu_mod._GetrfDev.panel
     lu_dist_ops.panel_xchg = lambda group, me, P_, kbw, dtype, device, max_rows=0: ReplayXchg(kbw, dtype, device, xlat)
+    lu_mod._GetrfDev.panel = _valid_pivots_panel(orig_panel)
     try:
         A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N, name="A")
         dp.plrnt(ctx, A, 3872)
@@ -76,6 +95,7 @@ def replay_rank(base, P, Q, rank, N, NB, steps, xlat):
         torch.cuda.empty_cache()
     finally:
         lu_dist_ops.panel_xchg = orig
+        lu_mod._GetrfDev.panel = orig_panel
     return min(times), enq
 
 
