@@ -65,6 +65,16 @@ def main():
         print(f"{k:3d} | {ps:10.1f} .. {pe:10.1f} ({pe - ps:7.1f}) | {ts_:10.1f} .. {te:10.1f} ({te - ts_:7.1f}) | "
               f"{ps - prev_end:8.1f}")
         prev_end = te
+    # occupancy over time (20 bins) and the share of idle workgroup-time in the first / last fifth
+    nb_ = 20
+    edges = np.linspace(0, span, nb_ + 1)
+    ss, ee = (s - t0) / 100.0, (e - t0) / 100.0
+    occ = []
+    for q in range(nb_):
+        lo, hi = edges[q], edges[q + 1]
+        busy_q = np.clip(np.minimum(ee, hi) - np.maximum(ss, lo), 0, None).sum()
+        occ.append(int(round(100 * busy_q / (nwg * (hi - lo)))))
+    print("occupancy per 5 % of the span:", occ)
     if out:
         np.savez(out, trace=tr, tasks=T.view(np.uint8), nt=nt)
 
