@@ -18,6 +18,9 @@ step dtr_trace64k 240 python tools/gpu/dtr_trace_run.py 65536 || exit 1
 for T in 16 32; do
   step dtr_tail$T 400 env DPLASMA_DTR_DEFER_MIN_TILES=$T python tools/gpu/dtr_bench.py 32768 65536 || exit 1
 done
-step replay_lu_2x4_x16 600 python tools/replay_lu.py -N 65536 --nb 512 --grid 2x4 --ranks 0,1,4,5 --xlat 16 || exit 1
-step replay_lu_2x4_x6 600 python tools/replay_lu.py -N 65536 --nb 512 --grid 2x4 --ranks 0,1,4,5 --xlat 6 || exit 1
+step replay_python_2x4_bw65 500 python tools/replay_potrf.py -N 65536 --nb 512 --grid 2x4 --steps 2 --bw 65 --lat 10 || exit 1
+step replay_python_2x4_bw65_noproxy 500 python tools/replay_potrf.py -N 65536 --nb 512 --grid 2x4 --steps 2 --bw 65 --lat 10 --no-proxy || exit 1
+step replay_native_2x4_bw65 400 python tools/replay_native.py -N 65536 --nb 512 --grid 2x4 --steps 2 --bw 65 --lat 10 || exit 1
+step replay_lu_2x4_x16 600 python tools/replay_lu.py -N 65536 --nb 512 --grid 2x4 --ranks 0,1,4,5 --bw 65 --lat 10 --xlat 16 || exit 1
+step replay_lu_2x4_x6 600 python tools/replay_lu.py -N 65536 --nb 512 --grid 2x4 --ranks 0,1,4,5 --bw 65 --lat 10 --xlat 6 || exit 1
 exit 0
