@@ -21,6 +21,4 @@ done
 step replay_python_2x4_bw65 500 python tools/replay_potrf.py -N 65536 --nb 512 --grid 2x4 --steps 2 --bw 65 --lat 10 || exit 1
 step replay_python_2x4_bw65_noproxy 500 python tools/replay_potrf.py -N 65536 --nb 512 --grid 2x4 --steps 2 --bw 65 --lat 10 --no-proxy || exit 1
 step replay_native_2x4_bw65 400 python tools/replay_native.py -N 65536 --nb 512 --grid 2x4 --steps 2 --bw 65 --lat 10 || exit 1
-step replay_lu_2x4_x16 600 python tools/replay_lu.py -N 65536 --nb 512 --grid 2x4 --ranks 0,1,4,5 --bw 65 --lat 10 --xlat 16 || exit 1
-step replay_lu_2x4_x6 600 python tools/replay_lu.py -N 65536 --nb 512 --grid 2x4 --ranks 0,1,4,5 --bw 65 --lat 10 --xlat 6 || exit 1
 exit 0
