@@ -75,6 +75,26 @@ def main():
         busy_q = np.clip(np.minimum(ee, hi) - np.maximum(ss, lo), 0, None).sum()
         occ.append(int(round(100 * busy_q / (nwg * (hi - lo)))))
     print("occupancy per 5 % of the span:", occ)
+    # gaps between consecutive tasks of each workgroup: many small ones = per-task overhead, few large ones =
+    # stalls; split by the kind of the task that follows the gap and by XCD
+    wg_of, xcd_of = who >> 8, who & 0xff
+    order = np.lexsort((ss, wg_of))
+    wo, so, eo = wg_of[order], ss[order], ee[order]
+    same = wo[1:] == wo[:-1]
+    gaps = (so[1:] - eo[:-1])[same]
+    nxt = order[1:][same]
+    tot = gaps.sum()
+    print(f"gaps: n={len(gaps)} total {tot / 1e3:.1f} WG-ms ({100 * tot / (nwg * span):.1f} % of WG x span)  mean {gaps.mean():.1f} us"
+          f"  p50 {np.percentile(gaps, 50):.1f}  p90 {np.percentile(gaps, 90):.1f}  p99 {np.percentile(gaps, 99):.1f}")
+    for lo_, hi_ in ((0, 5), (5, 20), (20, 100), (100, 1000), (1000, 1e12)):
+        m = (gaps >= lo_) & (gaps < hi_)
+        print(f"  gaps in [{lo_}, {hi_}) us: {m.sum():8d}  sum {gaps[m].sum() / 1e3:9.1f} WG-ms")
+    hi_set = np.zeros(len(T), dtype=bool)
+    hi_set[plan.hi] = True
+    for nm, m in (("next task from the high list", hi_set[nxt]), ("next task from a low list", ~hi_set[nxt])):
+        print(f"  {nm}: {m.sum()} gaps, {gaps[m].sum() / 1e3:.1f} WG-ms")
+    xb = [(ee[xcd_of == x] - ss[xcd_of == x]).sum() / ((nwg / 8) * span) * 100 for x in range(8)]
+    print("busy % per XCD:", [int(round(v)) for v in xb])
     if out:
         np.savez(out, trace=tr, tasks=T.view(np.uint8), nt=nt)
 
