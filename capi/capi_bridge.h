@@ -143,6 +143,13 @@ NatProgram* nat_gels(dplasma_context_t* ctx, int prec, int trans, dplasma_desc_t
 int nat_redistribute(dplasma_context_t* ctx, int es, char* src, int slld, int mb, int nb, int rsrc, int csrc, int ia,
                      int ja, int m, int n, char* dst, int dlld, bool to_aligned);
 int nat_qr_tau(dplasma_desc_t* T, void* tau, int k);
+NatProgram* nat_getrf_incpiv(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* L, dplasma_desc_t* IPIV);
+NatProgram* nat_trsmpl_incpiv(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* L,
+                              dplasma_desc_t* IPIV, dplasma_desc_t* B);
+NatProgram* nat_getrs_incpiv(dplasma_context_t* ctx, int prec, int trans, dplasma_desc_t* A, dplasma_desc_t* L,
+                             dplasma_desc_t* IPIV, dplasma_desc_t* B);
+NatProgram* nat_gesv_incpiv(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* L,
+                            dplasma_desc_t* IPIV, dplasma_desc_t* B);
 NatProgram* nat_getrf_nopiv(dplasma_context_t* ctx, int prec, dplasma_desc_t* A);
 NatProgram* nat_gelqf(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* T);
 NatProgram* nat_unmlq(dplasma_context_t* ctx, int prec, int side, int trans, dplasma_desc_t* A, dplasma_desc_t* T,

@@ -1823,6 +1823,187 @@ NatProgram* nat_getrf_nopiv(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA
   return P;
 }
 
+// ----------------------------------------------------------------------------- LU, incremental pivoting
+// The tile algorithm of src/zgetrf_incpiv.jdf (GETRF(k) -> GESSM(k, n) -> TSTRF(k, m) -> SSSSM(k, m, n)) on the
+// tile kernels of csrc/kernels/lu_incpiv.hip, one batched launch per task class and step (GESSM over the
+// row, SSSSM over the row for each m): TSTRF(k, m) on the panel stream, SSSSM(k, m, *) on the update stream
+// (TSTRF(k, m+1) overlaps SSSSM(k, m, *)).  L: (MT*IB) x N of IB x NB tiles, IPIV: M x NT of MB x 1 tiles
+// (tests/testing_zgetrf_incpiv.c:51-62).  One process.
+namespace {
+
+struct IncItem {   // = lu_incpiv.hip LuItem (96 bytes)
+  long long p0, p1, p2, p3;
+  int ld0, ld1, ld2, ld3;
+  int m, n, k, pad;
+  long long p4, p5;
+  int ld4, ld5, aux0, aux1;
+};
+static_assert(sizeof(IncItem) == 96, "LuItem layout");
+
+bool incpiv_conform(const NatDesc* A, const NatDesc* L, const NatDesc* IP) {
+  return A && L && IP && A->mb == A->nb && A->nb <= 256 && L->mb >= 1 && L->mb <= 32 && L->nb == A->nb &&
+         L->mt >= A->mt && L->nt >= A->nt && IP->prec == P_I && IP->mb == A->mb && IP->m >= A->m && IP->n >= A->nt;
+}
+
+struct IncBatch {
+  std::vector<IncItem> it;
+  int max_m = 0, max_n = 0;
+  DevPtr d;
+  void add(const IncItem& x) {
+    it.push_back(x);
+    max_m = std::max(max_m, x.m);
+    max_n = std::max(max_n, x.n);
+  }
+  bool upload(NatProgram& P) {
+    if (it.empty()) return true;
+    d = dev_upload(it);
+    if (!d) return false;
+    P.keep.push_back(d);
+    return true;
+  }
+};
+
+// B := L^-1 P B with the factors of add_getrf_incpiv (GESSM on block row k, SSSSM down the rows); stream 1
+bool add_trsmpl_incpiv(NatProgram& P, NatDesc& A, NatDesc& L, NatDesc& IP, NatDesc& B, int& last) {
+  const int prec = A.prec, es = A.es, ib = L.mb, kt = std::min(A.mt, A.nt);
+  auto ad = [&](NatDesc& D, int i, int j) { return (long long)(D.data + D.off(i, j) * D.es); };
+  int prev = last;
+  for (int k = 0; k < kt; ++k) {
+    auto g = std::make_shared<IncBatch>();
+    for (int n = 0; n < B.nt; ++n)
+      g->add(IncItem{0, ad(B, k, n), ad(A, k, k), ad(IP, k, k), 0, B.lld, A.lld, 0, B.rows(k), B.cols(n),
+                     std::min(A.rows(k), A.cols(k)), 0, 0, 0, 0, 0, 0, 0});
+    if (!g->upload(P)) return false;
+    prev = P.task(1, [=](hipStream_t s) { return dpl_gessm(prec, (int)g->it.size(), g->d->p, g->max_n, s); }, {prev});
+    for (int m = k + 1; m < A.mt; ++m) {
+      auto q = std::make_shared<IncBatch>();
+      for (int n = 0; n < B.nt; ++n)
+        q->add(IncItem{ad(B, k, n), ad(B, m, n), ad(L, m, k), ad(IP, m, k), B.lld, B.lld, L.lld, 0, B.rows(m), B.cols(n),
+                       A.cols(k), 0, ad(A, m, k), 0, A.lld, 0, 0, 0});
+      if (!q->upload(P)) return false;
+      const int NB = A.nb;
+      prev = P.task(1, [=](hipStream_t s) { return dpl_ssssm(prec, (int)q->it.size(), q->d->p, q->max_n, ib, NB, s); },
+                    {prev});
+    }
+  }
+  (void)es;
+  last = prev;
+  return true;
+}
+
+bool add_getrf_incpiv(NatProgram& P, NatDesc& A, NatDesc& L, NatDesc& IP, int& last) {
+  const int prec = A.prec, ib = L.mb, NB = A.nb, kt = std::min(A.mt, A.nt);
+  int* info = (int*)P.info->p;
+  auto ad = [&](NatDesc& D, int i, int j) { return (long long)(D.data + D.off(i, j) * D.es); };
+  int prev_pan = last, prev_upd = last;
+  for (int k = 0; k < kt; ++k) {
+    auto gf = std::make_shared<IncBatch>();
+    gf->add(IncItem{0, ad(A, k, k), 0, ad(IP, k, k), 0, A.lld, 0, 0, A.rows(k), A.cols(k), k * A.nb, 0, 0, 0, 0, 0, 0, 0});
+    if (!gf->upload(P)) return false;
+    // the diagonal tile is final once every SSSSM of step k-1 has run (update stream)
+    int pan = P.task(0, [=](hipStream_t s) { return dpl_getrf_tile(prec, 1, gf->d->p, info, s); }, {prev_pan, prev_upd});
+    int upd = prev_upd;
+    if (k + 1 < A.nt) {
+      auto g = std::make_shared<IncBatch>();
+      for (int n = k + 1; n < A.nt; ++n)
+        g->add(IncItem{0, ad(A, k, n), ad(A, k, k), ad(IP, k, k), 0, A.lld, A.lld, 0, A.rows(k), A.cols(n),
+                       std::min(A.rows(k), A.cols(k)), 0, 0, 0, 0, 0, 0, 0});
+      if (!g->upload(P)) return false;
+      upd = P.task(1, [=](hipStream_t s) { return dpl_gessm(prec, (int)g->it.size(), g->d->p, g->max_n, s); }, {pan, upd});
+    }
+    for (int m = k + 1; m < A.mt; ++m) {
+      auto t = std::make_shared<IncBatch>();
+      t->add(IncItem{ad(A, k, k), ad(A, m, k), ad(L, m, k), ad(IP, m, k), A.lld, A.lld, L.lld, 0, A.rows(m), A.cols(k),
+                     k * A.nb, 0, 0, 0, 0, 0, 0, 0});
+      if (!t->upload(P)) return false;
+      const int mm = t->max_m;
+      // TSTRF(k, m) needs only TSTRF(k, m-1) (the U tile, panel stream order); SSSSM(k, m, *) reads its L / IPIV
+      pan = P.task(0, [=](hipStream_t s) { return dpl_tstrf(prec, 1, t->d->p, ib, NB, mm, info, s); }, {pan});
+      if (k + 1 < A.nt) {
+        auto q = std::make_shared<IncBatch>();
+        for (int n = k + 1; n < A.nt; ++n)
+          q->add(IncItem{ad(A, k, n), ad(A, m, n), ad(L, m, k), ad(IP, m, k), A.lld, A.lld, L.lld, 0, A.rows(m), A.cols(n),
+                         A.cols(k), 0, ad(A, m, k), 0, A.lld, 0, 0, 0});
+        if (!q->upload(P)) return false;
+        upd = P.task(1, [=](hipStream_t s) { return dpl_ssssm(prec, (int)q->it.size(), q->d->p, q->max_n, ib, NB, s); },
+                     {pan, upd});
+      }
+    }
+    prev_pan = pan;
+    prev_upd = upd;
+  }
+  last = P.task(1, [](hipStream_t) { return 0; }, {prev_pan, prev_upd});
+  return true;
+}
+
+}  // namespace
+
+NatProgram* nat_getrf_incpiv(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dplasma_desc_t* dL,
+                             dplasma_desc_t* dIP) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *L = dL ? dL->nat : nullptr, *IP = dIP ? dIP->nat : nullptr;
+  if (!same_ctx(c, {A, L}, prec) || !IP || IP->ctx != c)
+    return fail(nullptr, "getrf_incpiv: descriptors of another context or precision");
+  if (!incpiv_conform(A, L, IP))
+    return fail(nullptr, "getrf_incpiv: square tiles <= 256, L of (IB <= 32) x NB tiles, IPIV of MB x 1 tiles");
+  NatProgram* P = new_program(c, "getrf_incpiv", true);
+  int last = -1;
+  if (!P->info || !add_getrf_incpiv(*P, *A, *L, *IP, last)) return fail(P, "getrf_incpiv: device allocation failed");
+  return P;
+}
+
+static bool incpiv_solve_ok(const NatDesc* A, const NatDesc* B) {
+  return B && A->m == A->n && B->m == A->m && B->mb == A->mb;
+}
+
+NatProgram* nat_trsmpl_incpiv(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dplasma_desc_t* dL,
+                              dplasma_desc_t* dIP, dplasma_desc_t* dB) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *L = dL ? dL->nat : nullptr, *IP = dIP ? dIP->nat : nullptr,
+          *B = dB ? dB->nat : nullptr;
+  if (!same_ctx(c, {A, L, B}, prec) || !IP || IP->ctx != c)
+    return fail(nullptr, "trsmpl_incpiv: descriptors of another context or precision");
+  if (!incpiv_conform(A, L, IP) || !incpiv_solve_ok(A, B)) return fail(nullptr, "trsmpl_incpiv: operands do not conform");
+  NatProgram* P = new_program(c, "trsmpl_incpiv", false);
+  int last = -1;
+  if (!add_trsmpl_incpiv(*P, *A, *L, *IP, *B, last)) return fail(P, "trsmpl_incpiv: device allocation failed");
+  return P;
+}
+
+// op(A) X = B, NoTrans (the reference getrs_incpiv: trsmpl + the upper solve)
+NatProgram* nat_getrs_incpiv(dplasma_context_t* ctx, int prec, int trans, dplasma_desc_t* dA, dplasma_desc_t* dL,
+                             dplasma_desc_t* dIP, dplasma_desc_t* dB) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *L = dL ? dL->nat : nullptr, *IP = dIP ? dIP->nat : nullptr,
+          *B = dB ? dB->nat : nullptr;
+  if (!same_ctx(c, {A, L, B}, prec) || !IP || IP->ctx != c)
+    return fail(nullptr, "getrs_incpiv: descriptors of another context or precision");
+  if (trans != NOTRANS) return fail(nullptr, "getrs_incpiv: NoTrans only (as the reference)");
+  if (!incpiv_conform(A, L, IP) || !incpiv_solve_ok(A, B)) return fail(nullptr, "getrs_incpiv: operands do not conform");
+  NatProgram* P = new_program(c, "getrs_incpiv", false);
+  int last = -1;
+  if (!add_trsmpl_incpiv(*P, *A, *L, *IP, *B, last) ||
+      !add_trsm(*P, LEFT, UPPER, NOTRANS, NONUNIT, Scalar(prec, 1.0), *A, *B, 1, last))
+    return fail(P, "getrs_incpiv: device allocation failed");
+  return P;
+}
+
+NatProgram* nat_gesv_incpiv(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dplasma_desc_t* dL,
+                            dplasma_desc_t* dIP, dplasma_desc_t* dB) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *L = dL ? dL->nat : nullptr, *IP = dIP ? dIP->nat : nullptr,
+          *B = dB ? dB->nat : nullptr;
+  if (!same_ctx(c, {A, L, B}, prec) || !IP || IP->ctx != c)
+    return fail(nullptr, "gesv_incpiv: descriptors of another context or precision");
+  if (!incpiv_conform(A, L, IP) || !incpiv_solve_ok(A, B)) return fail(nullptr, "gesv_incpiv: operands do not conform");
+  NatProgram* P = new_program(c, "gesv_incpiv", true);
+  int last = -1;
+  if (!P->info || !add_getrf_incpiv(*P, *A, *L, *IP, last) || !add_trsmpl_incpiv(*P, *A, *L, *IP, *B, last) ||
+      !add_trsm(*P, LEFT, UPPER, NOTRANS, NONUNIT, Scalar(prec, 1.0), *A, *B, 1, last))
+    return fail(P, "gesv_incpiv: device allocation failed");
+  return P;
+}
+
 dplasma_desc_t* nat_desc_int(dplasma_context_t* ctx, int mb, int nb, int m, int n) {
   return nat_desc(ctx, P_I, mb, nb, m, n, 1, 1, nullptr, 0, 1);
 }

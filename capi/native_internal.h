@@ -40,6 +40,10 @@ int dpl_lascal(int prec, int part, int nitems, const void* items, int mmax, int 
 int dpl_tile_norm(int prec, int kind, int part, int unit, int nitems, const void* items, const void* A, int lda,
                   double* out, int ostride, hipStream_t st);
 long long dpl_lu_block_ws_bytes(int m);
+int dpl_getrf_tile(int prec, int nitems, const void* items, int* info, hipStream_t st);
+int dpl_gessm(int prec, int nitems, const void* items, int max_n, hipStream_t st);
+int dpl_ssssm(int prec, int nitems, const void* items, int max_n, int ib, int NB, hipStream_t st);
+int dpl_tstrf(int prec, int nitems, const void* items, int ib, int NB, int max_m, int* info, hipStream_t st);
 int dpl_lu_block(int prec, void* A, int ld, int m, int c0, int cend, int* ipiv, void* ws, int* cnt, int* info,
                  int info_base, int pivot, hipStream_t st);
 int dpl_laswp_panel(int prec, void* A, int ld, int ca, int cb, const int* ipiv, int i0, int i1, hipStream_t st);

@@ -748,6 +748,36 @@ static void test_zgelqf(dplasma_context_t *ctx) {
   dplasma_desc_destroy(A), dplasma_desc_destroy(Q), dplasma_desc_destroy(T);
 }
 
+/* incremental-pivoting LU (tile GETRF / GESSM / TSTRF / SSSSM) + gesv_incpiv on a ragged matrix: A x = b */
+static void test_dgesv_incpiv(dplasma_context_t *ctx) {
+  const int n = 500, nb = 128, ib = 32, nrhs = 4;
+  const int mt = (n + nb - 1) / nb, nt = mt;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, n, n), *B = dmat(ctx, dplasmaRealDouble, nb, n, nrhs);
+  dplasma_desc_t *L = dplasma_desc_block_cyclic(ctx, dplasmaRealDouble, ib, nb, mt * ib, n, 1, 1, dplasmaUpperLower);
+  dplasma_desc_t *IP = dplasma_desc_ipiv(ctx, nb, 1, n, nt, 1, 1);
+  CHECK(A && B && L && IP, "incpiv descriptors: %s", dplasma_last_error());
+  double *a = malloc(sizeof(double) * n * n), *b = malloc(sizeof(double) * n * nrhs), *x = malloc(sizeof(double) * n * nrhs);
+  unsigned sd = 404;
+  rnd_fill(a, (size_t)n * n, &sd), rnd_fill(b, (size_t)n * nrhs, &sd);
+  dplasma_desc_set_lapack(A, a, n);
+  dplasma_desc_set_lapack(B, b, n);
+  const int info = dplasma_dgesv_incpiv(ctx, A, L, IP, B);
+  CHECK(info == 0, "dgesv_incpiv info %d (%s)", info, dplasma_last_error());
+  dplasma_desc_get_lapack(B, x, n);
+  double err = 0, bn = 0;
+  for (int c = 0; c < nrhs; ++c)
+    for (int i = 0; i < n; ++i) {
+      double s = 0;
+      for (int k = 0; k < n; ++k) s += a[i + (size_t)k * n] * x[k + (size_t)c * n];
+      err = fmax(err, fabs(s - b[i + (size_t)c * n]));
+      bn = fmax(bn, fabs(b[i + (size_t)c * n]));
+    }
+  printf("dgesv_incpiv n=%d nb=%d ib=%d: ||Ax-b||/||b|| %.3e\n", n, nb, ib, err / bn);
+  CHECK(err / bn < 1e-9, "gesv_incpiv residual %.3e", err / bn);
+  free(a), free(b), free(x);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(B), dplasma_desc_destroy(L), dplasma_desc_destroy(IP);
+}
+
 /* flat-tree QR family: geqrf, ungqr (thin and full Q), unmqr (left Q^T, right Q), gels */
 static void test_dgeqrf(dplasma_context_t *ctx) {
   const int m = 700, n = 400, nb = 128, ib = 32, nrhs = 3, p = 50;
@@ -991,6 +1021,7 @@ int main(int argc, char **argv) {
   test_dgetrf(ctx);
   test_dgeqrf(ctx);
   test_dgetrf_nopiv(ctx);
+  test_dgesv_incpiv(ctx);
   test_dgelqf(ctx);
   test_zgelqf(ctx);
   test_inverse_family(ctx);
@@ -998,7 +1029,7 @@ int main(int argc, char **argv) {
   test_aliases(ctx);
   /* an operation without a native implementation fails cleanly */
   dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
-  CHECK(dplasma_dgetrf_incpiv(ctx, A, A, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");
+  CHECK(dplasma_dtrmdm(ctx, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");
   dplasma_desc_destroy(A);
   if (argc > 1 && atoi(argv[1]) > 0) bench(ctx, atoi(argv[1]));
   CHECK(dplasma_python_active() == 0, "the interpreter was started");

@@ -113,6 +113,9 @@ NATIVE = {
     "unmlq": "side, trans, A, T, C",
     "unglq": "A, T, Q",
     "gelqs": "A, T, B",
+    "getrf_incpiv": "A, L, IPIV",
+    "getrs_incpiv": "trans, A, L, IPIV, B",
+    "gesv_incpiv": "A, L, IPIV, B",
 }
 # same operation natively under another name: the recursive-size hint only changes the reference's CPU
 # task granularity; a 1 x 1 ptgpanel grid is the 1-D LU; the _sync variant is the blocking call
