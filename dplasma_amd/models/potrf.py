@@ -64,6 +64,10 @@ POTRF_TRSM = "rb"   # "fused": the diagonal owner factors its tile and solves it
 # launches of 2 x (CUs - reserve) workgroups, ops.gemm_wg_cap): the panel chain's kernels find idle
 # CUs instead of waiting for GEMM workgroups to retire.  (single process, distributed)
 POTRF_RESERVE = (0, 0)
+# one GPU process: "stream" (the stream-program engine below), "dtr" (the device task runtime,
+# models/potrf_dtr.py) or "auto" (dtr from POTRF_DTR_MIN_N up when it supports the operand)
+POTRF_ENGINE = "stream"
+POTRF_DTR_MIN_N = 24576
 
 
 def _defer_depth(nt_left: int, D: int, min_tiles: int) -> int:
@@ -96,10 +100,13 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
         return potrf_ooc_New(ctx, uplo, A)
     # one process, lower, fp64, NB = 512: the whole factorisation as one persistent launch of the device
     # task runtime (panel work prioritised inside the bulk update's workgroups, models/potrf_dtr.py)
-    eng = os.environ.get("DPLASMA_POTRF_ENGINE", "stream")
+    eng = os.environ.get("DPLASMA_POTRF_ENGINE", POTRF_ENGINE)
     if eng in ("dtr", "auto"):
         from . import potrf_dtr
-        if potrf_dtr.supported(ctx, uplo, A):
+        # auto: the device task runtime from POTRF_DTR_MIN_N up (below it the panel chain dominates and the
+        # stream engine's register-resident panel solve is faster: profiles/r4_dtr_*.txt)
+        big = A.n >= int(os.environ.get("DPLASMA_POTRF_DTR_MIN_N", POTRF_DTR_MIN_N))
+        if potrf_dtr.supported(ctx, uplo, A) and (eng == "dtr" or big):
             return potrf_dtr.potrf_dtr_New(ctx, uplo, A, info_out)
         if eng == "dtr":
             raise ValueError("DPLASMA_POTRF_ENGINE=dtr: needs one GPU process, lower, fp64, NB = 512, N % 512 == 0")
