@@ -1,0 +1,20 @@
+#!/bin/bash
+# r4 batch 15: DTR bulk-update XCD assignment (tile row vs column) with the combined-peek claim; 64k gaps each.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/r4b15
+mkdir -p $O
+export PYTHONUNBUFFERED=1
+step() {
+  local name=$1 to=$2; shift 2
+  echo "== $name" | tee -a $O/summary.log
+  timeout -k 10 $to "$@" > $O/$name.log 2>&1
+  local rc=$?
+  grep -E "passed|failed|error|Error|TF/s|TIME|span=|occupancy|gaps|next task|busy %" $O/$name.log | grep -v amdgpu.ids | tail -14 | tee -a $O/summary.log
+  echo "rc=$rc" | tee -a $O/summary.log
+  return $rc
+}
+step dtr_tests 240 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_potrf_dtr.py -m gpu || exit 1
+step trace64k_col 240 env DPLASMA_DTR_XCD_KEY=col python tools/gpu/dtr_trace_run.py 65536 || exit 1
+step trace64k_row 240 env DPLASMA_DTR_XCD_KEY=row python tools/gpu/dtr_trace_run.py 65536 || exit 1
+step bench_col 400 env DPLASMA_DTR_XCD_KEY=col python tools/gpu/dtr_bench.py 32768 65536 || exit 1
+exit 0
