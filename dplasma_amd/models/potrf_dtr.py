@@ -85,9 +85,6 @@ class _Plan:
         # whole previous bulk.  Both are subsequences of one topological order (column blocks ascending; in
         # a block, its low-list updates, then its high-list tasks), which the deadlock argument needs.
         lo_order = lo_order or os.environ.get("DPLASMA_DTR_LO_ORDER", "column")
-        xcd_key = os.environ.get("DPLASMA_DTR_XCD_KEY", "row")
-        if xcd_key not in ("row", "col"):
-            raise ValueError("DPLASMA_DTR_XCD_KEY must be row or col")
         if lo_order not in ("panel", "column"):
             raise ValueError("DPLASMA_DTR_LO_ORDER must be panel or column")
         S = 4 * nt
@@ -171,11 +168,7 @@ class _Plan:
                 key = np.stack([block_of[j], np.full(n, kl), j, i, r, c], 1)
             else:
                 key = np.stack([np.full(n, kl), j, i, r, c], 1)
-            # XCD of a bulk update: by tile row (default) -- every column block's work spread over the 8
-            # lists, the 16 sub-tiles of a tile and its row's L strips on one L2; by column, a column block
-            # (D columns) fed only D of the 8 XCDs and the others idled (profiles/r4_dtr_colorder.txt)
-            xk = (i if xcd_key == "row" else j) % 8
-            return emit(T_UPD, i, j, k0, r, c, nk, Ci, reqs, None, "lo", key=key, xcd=xk)
+            return emit(T_UPD, i, j, k0, r, c, nk, Ci, reqs, None, "lo", key=key, xcd=j % 8)
 
         for bi, (k0b, k1b) in enumerate(blocks):
             for k in range(k0b, k1b):
@@ -296,7 +289,7 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     D = max(1, int(os.environ.get("DPLASMA_DTR_DEFER", "4")))
     lo_order = os.environ.get("DPLASMA_DTR_LO_ORDER", "column")
     min_tiles = int(os.environ.get("DPLASMA_DTR_DEFER_MIN_TILES", "0"))
-    key = (nt, D, lo_order, min_tiles, os.environ.get("DPLASMA_DTR_XCD_KEY", "row"))
+    key = (nt, D, lo_order, min_tiles)
     plan = _PLANS.get(key)
     if plan is None:
         plan = _PLANS[key] = _Plan(nt, D, lo_order, min_tiles)
