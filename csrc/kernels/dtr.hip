@@ -320,50 +320,6 @@ __device__ __attribute__((noinline)) void run_potrf(const DtrArgs* __restrict__ 
   w_column(g, k, b, g_lds);
 }
 
-// One claim round for the high list's head and this XCD's low-list head TOGETHER (wave 0): lane 0 walks the
-// high list, lane 1 the low list -- cursor, list entry, task record, then lanes 0-31 / 32-63 test the two
-// requirement sets -- so both peeks cost the round trips of one (profiles/r4_s13_suite_bench_dtrgaps.txt:
-// the median gap between a workgroup's tasks was ~23 us, most of it serial round trips of sequential peeks).
-struct Peek2 {
-  int hh, th, hl, tl, nlo;
-  bool hr, lr;
-};
-__device__ inline Peek2 peek2(const DtrArgs& g, int xcd, bool want_hi, bool want_lo) {
-  const int l = threadIdx.x & 63;
-  int* lcur = g.cur + PSTRIDE * (1 + xcd);
-  const int lbeg = g.lo_off[xcd], nlo = g.lo_off[xcd + 1] - g.lo_off[xcd];
-  int v = 0x7fffffff;
-  if (l == 0 && want_hi) v = ld_sc1(g.cur);
-  if (l == 1 && want_lo) v = ld_sc1(lcur);
-  Peek2 p;
-  p.nlo = nlo;
-  p.hh = __builtin_amdgcn_readlane(v, 0);
-  p.hl = __builtin_amdgcn_readlane(v, 1);
-  int t = -1;
-  if (l == 0 && want_hi && p.hh < g.nhi) t = g.hi[p.hh];
-  if (l == 1 && want_lo && p.hl < nlo) t = g.lo[lbeg + p.hl];
-  p.th = __builtin_amdgcn_readlane(t, 0);
-  p.tl = __builtin_amdgcn_readlane(t, 1);
-  int rb = 0, nr = 0;
-  if (l < 2 && t >= 0) {
-    rb = g.tasks[t].req_beg;
-    nr = g.tasks[t].nreq;
-  }
-  const int rbh = __builtin_amdgcn_readlane(rb, 0), nrh = __builtin_amdgcn_readlane(nr, 0);
-  const int rbl = __builtin_amdgcn_readlane(rb, 1), nrl = __builtin_amdgcn_readlane(nr, 1);
-  bool ok = true;
-  const int q = l & 31;
-  const int rbase = l < 32 ? rbh : rbl, rn = l < 32 ? nrh : nrl;
-  if (q < rn) {
-    const int2 rq = g.reqs[rbase + q];
-    ok = ld_sc1(g.cnt + rq.x) >= rq.y;
-  }
-  const unsigned long long bad = __builtin_amdgcn_ballot_w64(!ok);
-  p.hr = p.th >= 0 && (bad & 0xffffffffULL) == 0;
-  p.lr = p.tl >= 0 && (bad >> 32) == 0;
-  return p;
-}
-
 // The arguments live in device memory and are re-read through a laundered pointer every iteration:
 // hoisting all of DtrArgs into SGPRs across the task loop (what a by-value kernel argument invites)
 // leaves the GEMM body too few SGPRs and spills it to scratch.
@@ -393,33 +349,27 @@ __global__ __launch_bounds__(256, 2) void k_dtr_potrf(const DtrArgs* __restrict_
       if (ld_sc1(g.info) == -1000) {
         t = -2;
       } else {
-        const bool want_hi = ticket < 0 && !hi_done;
-        const Peek2 pk = peek2(g, xcd, want_hi, !lo_done);
-        int fresh = -1;   // a ticket just taken for the ready head pk.th
-        if (want_hi) {
+        if (ticket < 0 && !hi_done) {
           // a ticket only for a ready head: a workgroup holding a not-yet-ready critical task would run
           // low-list tasks meanwhile and come back up to one bulk task late -- the 16 POTRF workgroups of
           // a tile would then start spread over ~0.4 ms and wait for each other
-          if (pk.hh >= g.nhi) {
+          const int h = __builtin_amdgcn_readfirstlane(ld_sc1(g.cur));
+          if (h >= g.nhi) {
             hi_done = true;
-          } else if (pk.hr) {
+          } else if (ready_wave(g, __builtin_amdgcn_readfirstlane(g.hi[h]))) {
             int tk = 0;
             if (tid == 0) tk = atomicAdd(g.cur, 1);
             tk = __builtin_amdgcn_readfirstlane(tk);
             if (tk < g.nhi) {
               ticket = tk;
               ticket_t0 = __builtin_amdgcn_s_memrealtime();
-              if (tk == pk.hh) fresh = pk.th;
             } else {
               hi_done = true;
             }
           }
         }
         bool help = true;
-        if (fresh >= 0) {
-          t = fresh;
-          ticket = -1;
-        } else if (ticket >= 0) {
+        if (ticket >= 0) {
           const int th = __builtin_amdgcn_readfirstlane(g.hi[ticket]);
           if (ready_wave(g, th)) {
             t = th;
@@ -430,19 +380,10 @@ __global__ __launch_bounds__(256, 2) void k_dtr_potrf(const DtrArgs* __restrict_
           }
         }
         if (t < 0 && help && !lo_done) {
-          if (pk.hl < pk.nlo) {
-            // own list: claim the peeked head if it was ready (one CAS; a lost race waits for the next round)
-            if (pk.lr) {
-              int won = 0;
-              if (tid == 0) won = atomicCAS(g.cur + PSTRIDE * (1 + xcd), pk.hl, pk.hl + 1) == pk.hl;
-              if (__builtin_amdgcn_readfirstlane(won)) t = pk.tl;
-            }
-          } else {
-            t = claim_low(g, xcd);   // own list exhausted: another XCD's
-            if (t == -2) {
-              lo_done = true;
-              t = -1;
-            }
+          t = claim_low(g, xcd);
+          if (t == -2) {
+            lo_done = true;
+            t = -1;
           }
         }
         if (t < 0) t = (hi_done && lo_done && ticket < 0) ? -2 : -1;
