@@ -9,11 +9,19 @@
 //  * rows are partitioned once: workgroup w owns rows [w*R, w*R+R) (R <= 256, one row per
 //    thread in the column steps) for the whole launch, so every cross-workgroup hand-off is a
 //    small reduction (grid_sync.h) and the matrix itself never crosses workgroups;
-//  * 32-column blocks live in LDS.  Column j: every workgroup forms 32 partial dot products of
-//    its part of x = A(j+1:, j) with the block columns (c < j: the T column, c == j: ||x||^2,
-//    c > j: the reflector's effect) plus a snapshot of row j; ONE grid barrier; every
-//    workgroup reduces the partials redundantly, derives beta/tau/scale (dlarfg) and applies
-//    the reflector to its rows;
+//  * 32-column blocks live in LDS.  At the start of a block every workgroup forms the block's
+//    Gram matrix G = A_b(rows >= b0)^T A_b(rows >= b0) (MFMA partials, ONE grid barrier) and a
+//    replica of the block's top 32 rows.  Column j then needs no cross-row reduction at all:
+//    G(j, j) = ||A(j:, j)||^2 gives beta / tau, G(j, c) - A(j, j) A(j, c) = x^T A(j+1:, c)
+//    gives the reflector's effect on column c, and after the reflector (orthogonal on rows
+//    >= j, so the Gram matrix of rows >= j is unchanged) G is downdated by the new row j:
+//    G -= r_j^T r_j.  Every workgroup keeps G and the top rows in LDS and updates them
+//    redundantly (identical arithmetic -> identical scalars everywhere), so a column costs one
+//    workgroup barrier instead of a grid barrier + a 32-value reduction.  When the downdated
+//    ||x||^2 falls below 1/8 of the column's block-start norm (cancellation: a nearly
+//    dependent column, or the last rows of a square panel) that column takes the exact path:
+//    32 partial dot products per workgroup, one grid barrier, redundant reduction (the
+//    norm-downdating safeguard of LAPACK dgeqp3, here for the reflector itself);
 //  * after a block: Y = V_b^T [V_prev | A_rest] is formed with fp64 MFMA (K = the workgroup's
 //    rows), reduced in two barriers (each workgroup sums a slice), then A_rest -= V_b T_b^T Y
 //    with MFMA, rows stay resident per workgroup; Y's V_prev part is the T coupling input;
@@ -48,14 +56,15 @@ template <> struct QPM<float> {
 
 // mma(x, y, acc): D(p, q) += sum_k x(p, k) y(q, k); input lane l carries p (resp. q) = l & 15,
 // k = l >> 4; output acc[r] of lane l is D(drow(l, r), l & 15).
-// Workspace layout for a G-workgroup panel (bytes, 256-aligned parts): part1 [2][G][32], rowj [2][32],
-// part2 [G][32*(nc+32)], Yg [32*(nc+32)], Xc [nblk][32][kf] elements of the precision, then the barrier counter.
+// Workspace layout for a G-workgroup panel (bytes, 256-aligned parts): part1 [2][G][32],
+// rowj [2][32] + top rows [32][32] + summed Gram [32][32], part2 [G][32*(nc+32)] (also the Gram partials
+// [G][32][32]), Yg [32*(nc+32)], Xc [nblk][32][kf] elements of the precision, then the barrier counter.
 __host__ __device__ static inline long long qp_align(long long x) { return (x + 255) & ~255LL; }
 __host__ __device__ static inline void qp_layout_g(long long es, int nc, int kf, int G, long long off[6]) {
   const long long nblk = (kf + QP_B - 1) / QP_B;
   off[0] = 0;
   off[1] = off[0] + qp_align(es * 2 * G * QP_B);
-  off[2] = off[1] + qp_align(es * 2 * QP_B);
+  off[2] = off[1] + qp_align(es * (2 * QP_B + 2 * QP_B * QP_B));
   off[3] = off[2] + qp_align(es * (long long)G * QP_B * (nc + QP_B));
   off[4] = off[3] + qp_align(es * QP_B * (nc + QP_B));
   off[5] = off[4] + qp_align(es * nblk * QP_B * kf);
@@ -92,6 +101,8 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
   // 2 partial reduction, 3 Y partials, 4 Y barriers + reduction + T_b, 5 trailing update, 6 T coupling
   const bool tprof = prof != nullptr && w == 0 && tid == 0;
   unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long nfast = 0, nexact = 0, first_exact = -1;
+  double fe_x2 = 0.0, fe_g0 = 0.0;
   unsigned long long tlast = tprof ? __builtin_amdgcn_s_memrealtime() : 0;
 #define QP_TICK(slot)                                                \
   if (tprof) {                                                       \
@@ -99,6 +110,14 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
     tacc[slot] += tn_ - tlast;                                       \
     tlast = tn_;                                                     \
   }
+
+  // top-rows replica / summed Gram in the workspace (G > 1), Gram partials in part2
+  T* const topw = rowj + 2 * QP_B;
+  T* const gsum = topw + QP_B * QP_B;
+  // LDS replicas of the column steps, aliased on T_b / the Y chunk (both idle during the steps)
+  T (*const Gm)[QP_B + 1] = Ts;   // Gram of the block columns over rows >= the active row
+  T (*const Tp)[QP_WL] = Ws;      // the block's top 32 rows (Tp[r][c] = A(b0 + r, b0 + c))
+  __shared__ T g0[QP_B];          // block-start diagonal of G (cancellation test)
 
   for (int b = 0; b < nblk; ++b) {
     const int b0 = b * QP_B;
@@ -109,18 +128,128 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
     T a[QP_B];
 #pragma unroll
     for (int c = 0; c < QP_B; ++c) a[c] = (rowok && c < cb) ? P[grow + (long long)(b0 + c) * ldp] : T(0);
+    QP_TICK(7);
+    // ------------------------------------------------------------ block Gram + top-row replica
     for (int e = tid; e < QP_B * QP_LD; e += 256) {
       (&Xs[0][0])[e] = T(0);
       (&Ab[0][0])[e] = T(0);
     }
-    for (int e = tid; e < QP_B * (QP_B + 1); e += 256) (&Ts[0][0])[e] = T(0);
+    for (int e = tid; e < QP_B * QP_WL; e += 256) (&Tp[0][0])[e] = T(0);
     __syncthreads();
+    if (rowok && grow >= b0) {
+#pragma unroll
+      for (int c = 0; c < QP_B; ++c) Xs[c][tid] = a[c];
+    }
+    const bool top = rowok && grow >= b0 && grow < b0 + QP_B;
+    if (top) {
+      if (G == 1) {
+#pragma unroll
+        for (int c = 0; c < QP_B; ++c) Tp[grow - b0][c] = a[c];
+      } else {
+#pragma unroll
+        for (int c = 0; c < QP_B; ++c) st_sc1(&topw[(grow - b0) * QP_B + c], a[c]);
+      }
+    }
+    __syncthreads();
+    {
+      const int pt = wv & 1, qt = wv >> 1;
+      acc_t a0, a1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a0[r] = a1[r] = T(0);
+      for (int r0 = 0; r0 < R16; r0 += 8) {
+        const int rr = r0 + (l >> 4);
+        a0 = MM::mma(Xs[pt * 16 + (l & 15)][rr], Xs[qt * 16 + (l & 15)][rr], a0);
+        a1 = MM::mma(Xs[pt * 16 + (l & 15)][rr + 4], Xs[qt * 16 + (l & 15)][rr + 4], a1);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = pt * 16 + MM::drow(l, r), q = qt * 16 + (l & 15);
+        const T y = a0[r] + a1[r];
+        if (G == 1) Gm[p][q] = y;
+        else st_sc1(&part2[(long long)w * QP_B * QP_B + p * QP_B + q], y);
+      }
+    }
+    if (G > 1) {
+      ++nsync;
+      grid_sync_counter(cnt, nsync * G, info);
+      if (G <= 16) {
+        // every workgroup sums the partials itself (same order everywhere: identical G)
+        for (int e = tid; e < QP_B * QP_B; e += 256) {
+          T s = T(0);
+          for (int bb = 0; bb < G; ++bb) s += ld_sc1(&part2[(long long)bb * QP_B * QP_B + e]);
+          Gm[e >> 5][e & 31] = s;
+        }
+      } else {
+        // workgroup w sums a slice, one more barrier, everyone reads the sum
+        const int epw = (QP_B * QP_B + G - 1) / G;
+        const int e_beg = w * epw, e_end = min(QP_B * QP_B, e_beg + epw);
+        for (int base = e_beg; base < e_end; base += 32) {
+          const int e = base + (tid & 31), g = tid >> 5;
+          T s = T(0);
+          if (e < e_end)
+            for (int bb = g; bb < G; bb += 8) s += ld_sc1(&part2[(long long)bb * QP_B * QP_B + e]);
+          red[g][tid & 31] = s;
+          __syncthreads();
+          if (tid < 32 && e < e_end) {
+            T y = T(0);
+#pragma unroll
+            for (int gg = 0; gg < 8; ++gg) y += red[gg][tid];
+            st_sc1(&gsum[e], y);
+          }
+          __syncthreads();
+        }
+        ++nsync;
+        grid_sync_counter(cnt, nsync * G, info);
+        for (int e = tid; e < QP_B * QP_B; e += 256) Gm[e >> 5][e & 31] = ld_sc1(&gsum[e]);
+      }
+      for (int e = tid; e < QP_B * QP_B; e += 256) {
+        const int r = e >> 5, c = e & 31;
+        Tp[r][c] = b0 + r < M ? ld_sc1(&topw[e]) : T(0);
+      }
+    }
+    __syncthreads();
+    if (tid < QP_B) g0[tid] = Gm[tid][tid];
+    for (int e = tid; e < QP_B * QP_LD; e += 256) (&Xs[0][0])[e] = T(0);
+    __syncthreads();
+    QP_TICK(0);
     // ------------------------------------------------------------ column steps
     for (int jj = 0; jj < bw; ++jj) {
       const int j = b0 + jj;
-      const int par = nsync & 1;
       const int sh = QP_B - jj;  // live slots: slot s is column jj + s
-      QP_TICK(7);
+      const T alpha = Tp[jj][jj], gjj = Gm[jj][jj];
+      const T x2f = gjj - alpha * alpha;
+      // uniform over the whole grid: every workgroup holds the same replicas
+      const bool fast = x2f > T(0.125) * g0[jj];
+      if (tprof) {
+        if (fast) ++nfast;
+        else {
+          if (nexact++ == 0) { first_exact = j; fe_x2 = (double)x2f; fe_g0 = (double)g0[jj]; }
+        }
+      }
+      T beta, tau, scale;
+      const T* fw;   // slot-indexed reflector effects ff(s) = tau (A(j, jj+s) + scale x^T A(j+1:, jj+s))
+      if (fast) {
+        const T nrm = sqrt(gjj);
+        beta = alpha >= T(0) ? -nrm : nrm;
+        tau = (beta - alpha) / beta;
+        scale = T(1) / (alpha - beta);
+        // each wave derives the 32 effects itself (no workgroup barrier): lane s -> column jj + s
+        if (l < QP_B) {
+          const int c = jj + l;
+          T f = T(0);
+          if (l >= 1 && c < cb) {
+            const T tj = Tp[jj][c];
+            f = tau * (tj + scale * (Gm[jj][c] - alpha * tj));
+          }
+          red[wv][l] = f;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        fw = red[wv];
+        QP_TICK(1);
+      } else {
+      const int par = nsync & 1;
       {
         // x = A(r > j, j) against every live column, then a wave transpose-reduction:
         // lane l ends with the wave's sum for slot l >> 1
@@ -162,15 +291,8 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
         const T d = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
         st_sc1(&part1[((long long)par * G + w) * QP_B + tid], d);
       }
-      QP_TICK(0);
-      if (G > 1) {
-        ++nsync;
-        grid_sync_counter(cnt, nsync * G, info);
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-      }
-      QP_TICK(1);
+      ++nsync;
+      grid_sync_counter(cnt, nsync * G, info);
       {
         // thread (slot s, group q) sums partials q, q+8, ... (up to 16 loads in flight)
         const int s = tid & 31, q = tid >> 5;
@@ -200,37 +322,50 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
       }
       __syncthreads();
       }
-      QP_TICK(2);
       // dlarfg (every thread derives the same scalars); slot 0 is column jj
-      const T alpha = fin[QP_B], x2 = fin[0];
-      T beta, tau, scale;
+      const T ea = fin[QP_B], x2 = fin[0];
       if (x2 == T(0)) {
-        beta = alpha;
+        beta = ea;
         tau = T(0);
         scale = T(0);
       } else {
-        const T nrm = sqrt(alpha * alpha + x2);
-        beta = alpha >= T(0) ? -nrm : nrm;
-        tau = (beta - alpha) / beta;
-        scale = T(1) / (alpha - beta);
+        const T nrm = sqrt(ea * ea + x2);
+        beta = ea >= T(0) ? -nrm : nrm;
+        tau = (beta - ea) / beta;
+        scale = T(1) / (ea - beta);
       }
-      if (tid < QP_B) {
+      if (tid < QP_B)
         ff[tid] = (tid >= 1 && tid < sh && jj + tid < cb) ? tau * (fin[QP_B + tid] + scale * fin[tid]) : T(0);
-        if (tid == 0) taus[jj] = tau;
-      }
       __syncthreads();
+      fw = ff;
+      QP_TICK(2);
+      }
+      if (tid == 0) taus[jj] = tau;
       if (rowok) {
         const T x = a[0];
         const T vr = grow > j ? scale * x : (grow == j ? T(1) : T(0));
 #pragma unroll
-        for (int s = 1; s < QP_B; ++s) a[s] -= vr * ff[s];
+        for (int s = 1; s < QP_B; ++s) a[s] -= vr * fw[s];
         Ab[jj][tid] = grow < j ? x : (grow == j ? beta : vr);
         Xs[jj][tid] = vr;
+      }
+      // replicas: rows r > jj of the top block take the reflector like any row; the Gram matrix
+      // of rows > j is the (unchanged) one of rows >= j minus the new row j's outer product
+      for (int e = tid; e < QP_B * QP_B; e += 256) {
+        const int r = e >> 5, c = e & 31;
+        if (r > jj && c > jj) {
+          const T fc = fw[c - jj];
+          Tp[r][c] -= (scale * Tp[r][jj]) * fc;
+          Gm[r][c] -= (Tp[jj][r] - fw[r - jj]) * (Tp[jj][c] - fc);
+        }
       }
 #pragma unroll
       for (int s = 0; s < QP_B - 1; ++s) a[s] = a[s + 1];
       a[QP_B - 1] = T(0);
+      __syncthreads();
+      QP_TICK(1);
     }
+    for (int e = tid; e < QP_B * (QP_B + 1); e += 256) (&Ts[0][0])[e] = T(0);
     // non-reflector block columns (kf < nc): still in registers, rotated by bw
     if (rowok)
 #pragma unroll
@@ -491,6 +626,13 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
   QP_TICK(6);
   if (tprof)
     for (int i = 0; i < 8; ++i) prof[i] += (long long)tacc[i];
+  if (tprof) {   // column-path counters (the prof buffer holds 16 slots)
+    prof[8] += nfast;
+    prof[9] += nexact;
+    prof[10] = first_exact;
+    prof[11] = __double_as_longlong(fe_x2);
+    prof[12] = __double_as_longlong(fe_g0);
+  }
 #undef QP_TICK
 }
 

@@ -75,20 +75,63 @@ def _rup(x, m):
 
 
 # ----------------------------------------------------------------------------- plans
-def step_plan(tree, k):
-    """(domains, tt_kills) of panel k: domains = [[head, ts victims...], ...], tt = [(p, m), ...];
-    None when a TS kill's pivot is not a head (not expressible as stacked domains)."""
+def step_plan(tree, k, merge=False):
+    """(domains, tt_stacks) of panel k: domains = [[head, ts victims...], ...], tt_stacks =
+    [(p, [m, ...]), ...]; None when a TS kill's pivot is not a head (not expressible as stacked
+    domains).
+
+    merge=False: one stack per TT kill (p, [m]) in the tree's kill order.  merge=True (one process
+    row): the step's TT kills reduce every domain head to one survivor, so the whole TT subtree is
+    factored as ONE stacked panel of triangles [R_root; R_m1; R_m2; ...] (victims in kill order),
+    the way a TS domain is one stacked panel: V stays upper triangular in each victim's tile, R
+    lands in the survivor's, one T for the stack.  Mathematically the same reduction (an
+    orthogonal Q, the same R up to row signs); what changes is the launch count -- the trees are
+    shaped for a tile DAG that pipelines kills across panels, and executed round by round their
+    depth is paid in launches (the greedy tree at 32k, a = 4: up to 15 dependent rounds per step,
+    1864 panel launches in all; merged: 2 per step).  A kill set without a unique survivor falls
+    back to one stack per pivot at level 1 + its deepest victim's level.  Stacks come in level order."""
     heads = list(tree.heads(k))
     doms = {h: [h] for h in heads}
-    tts = []
+    kills = []
     for (p, m, t) in tree.kills(k):
         if t == qrtree.KILLED_BY_TS:
             if p not in doms:
                 return None
             doms[p].append(m)
         else:
-            tts.append((p, m))
+            kills.append((p, m))
+    if not merge:
+        return [doms[h] for h in heads], [(p, [m]) for (p, m) in kills]
+    victims = [m for (_, m) in kills]
+    roots = {p for (p, _) in kills} - set(victims)
+    if len(roots) == 1:
+        return [doms[h] for h in heads], [(roots.pop(), victims)]
+    stacks, order = {}, []
+    for (p, m) in kills:
+        if p not in stacks:
+            stacks[p] = []
+            order.append(p)
+        stacks[p].append(m)
+    lev = {}
+
+    def level(x):
+        if x not in stacks:
+            return 0
+        if x not in lev:
+            lev[x] = 1 + max(level(m) for m in stacks[x])
+        return lev[x]
+    rank = {p: i for i, p in enumerate(order)}
+    tts = sorted(((p, stacks[p]) for p in order), key=lambda e: (level(e[0]), rank[e[0]]))
     return [doms[h] for h in heads], tts
+
+
+def _merge_tt(A, tree):
+    """TT stacks merge per pivot on one process row with a one-row tree (cross-row kills stay pairwise,
+    and a tree built for P process rows keeps the pairwise layout a P-row grid run produces);
+    DPLASMA_QR_MERGE_TT=0 keeps every kill pairwise."""
+    if os.environ.get("DPLASMA_QR_MERGE_TT", "1") == "0":
+        return False
+    return A.grid.P == 1 and int(getattr(tree, "p", 1) or 1) == 1
 
 
 def _prow(A, m):
@@ -117,12 +160,12 @@ def usable(A, tree=None) -> bool:
 
 
 def _sequence(A, tree):
-    """Factorisation order: [("dom", k, rows) | ("tt", k, p, m)] over all panels."""
+    """Factorisation order: [("dom", k, rows) | ("tt", k, p, [m, ...])] over all panels."""
     seq = []
     for k in range(min(A.mt, A.nt)):
-        doms, tts = step_plan(tree, k)
+        doms, tts = step_plan(tree, k, _merge_tt(A, tree))
         seq += [("dom", k, d) for d in doms]
-        seq += [("tt", k, p, m) for (p, m) in tts]
+        seq += [("tt", k, p, ms) for (p, ms) in tts]
     return seq
 
 
@@ -372,13 +415,13 @@ class _Factor:
         # distributed: V and T travel along the process row(s) of the reflector rows (RCCL);
         # TT kills across process rows exchange R / V2 / T and the partial W between the two rows
         self.dist = ctx.world > 1
-        self.plans = [step_plan(tree, k) for k in range(self.kt)]
+        self.plans = [step_plan(tree, k, _merge_tt(A, tree)) for k in range(self.kt)]
         for k, (doms, tts) in enumerate(self.plans):
             for d in doms:
                 if TS.rank_of(d[0], k) != A.rank_of(d[0], k):
                     raise ValueError("geqrf: TS must be distributed like A (tile rows and columns)")
-            for (pp, m) in tts:
-                if TT.rank_of(m, k) != A.rank_of(m, k):
+            for (pp, ms) in tts:
+                if TT.rank_of(ms[0], k) != A.rank_of(ms[0], k):
                     raise ValueError("geqrf: TT must be distributed like A (tile rows and columns)")
         self.simple = all(len(d) == 1 and not t for d, t in self.plans) and A.grid.P == 1
         # one process, a tree with several domains / TT rounds per panel: every domain of a panel step in
@@ -426,10 +469,10 @@ class _Factor:
         for k in range(self.kt):
             doms, tts = self.plans[k]
             lev, rounds = {}, {}
-            for (p_, m_) in tts:
-                L = max(lev.get(p_, 0), lev.get(m_, 0)) + 1
+            for (p_, ms) in tts:
+                L = max([lev.get(p_, 0)] + [lev.get(m_, 0) for m_ in ms]) + 1
                 lev[p_] = L
-                rounds.setdefault(L, []).append([p_, m_])
+                rounds.setdefault(L, []).append([p_] + list(ms))
             cols = list(range(k + 1, A.nt))
             kgroups = []
             for kind, members in [("dom", doms)] + [("tt", rounds[L]) for L in sorted(rounds)]:
@@ -447,23 +490,42 @@ class _Factor:
                     kgroups.append((k, kind, cur, cols))
             specs.append(kgroups)
         # buffer sizes over every group
-        need_p = need_w = need_t = 1
+        need_p = need_v = need_w = need_t = 1
         ncol_el = lambda cols: sum(A.tile_cols(n) for n in cols)  # noqa: E731
+        # V / T of every group of a step at their own offsets (look-ahead applies them after all the
+        # step's panels); the gather buffer is reused group after group
+        self._vt_base = []
         for kgroups in specs:
+            vbase = tbase = 0
+            bases = []
             for (k, kind, ents, cols) in kgroups:
                 ld = max(e["ld"] for e in ents)
+                bases.append((vbase, tbase))
+                vbase += len(ents) * ld * nb
+                tbase += len(ents) * nb * nb
                 need_p = max(need_p, len(ents) * ld * nb)
-                need_t = max(need_t, len(ents) * nb * nb)
                 need_w = max(need_w, len(ents) * ents[0]["kf"] * max(1, ncol_el(cols)))
+            self._vt_base.append(bases)
+            need_v, need_t = max(need_v, vbase), max(need_t, tbase)
+        # look-ahead (DPLASMA_QR_LOOKAHEAD, default on): every group's update is split into column k+1
+        # (panel stream, right after the panels) and the rest (update stream), so the panel chain of step
+        # k+1 -- the TS launch and every TT round -- overlaps the bulk update of step k; V / T double-buffered
+        self.bla = os.environ.get("DPLASMA_QR_LOOKAHEAD", "1") != "0"
+        nbuf = 2 if self.bla else 1
         self.Pb = torch.zeros(need_p, dtype=dt, device=dev)
-        self.Vb = torch.zeros(need_p, dtype=dt, device=dev)
-        self.Tb = torch.zeros(need_t, dtype=dt, device=dev)
+        self.Vbs = [torch.zeros(need_v, dtype=dt, device=dev) for _ in range(nbuf)]
+        self.Tbs = [torch.zeros(need_t, dtype=dt, device=dev) for _ in range(nbuf)]
         self.Wb = torch.zeros(need_w, dtype=dt, device=dev)
         self.W2b = torch.zeros(need_w, dtype=dt, device=dev)
+        if self.bla:
+            need_n = max([len(ents) * ents[0]["kf"] * nb for kg in specs for (_, _, ents, _) in kg] + [1])
+            self.Wn = torch.zeros(need_n, dtype=dt, device=dev)
+            self.W2n = torch.zeros(need_n, dtype=dt, device=dev)
         self.info = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.bsteps = [[self._group(*gspec) for gspec in kgroups] for kgroups in specs]
+        self.bsteps = [[self._group(*gspec, *self._vt_base[i][gi]) for gi, gspec in enumerate(kgroups)]
+                       for i, kgroups in enumerate(specs)]
 
-    def _group(self, k, kind, ents, cols):
+    def _group(self, k, kind, ents, cols, vbase=0, tbase=0):
         A = self.A
         nb, kb = A.nb, A.tile_cols(k)
         tt = kind == "tt"
@@ -472,12 +534,13 @@ class _Factor:
         kf = ents[0]["kf"]
         ld = max(e["ld"] for e in ents)
         wcols = sum(A.tile_cols(n) for n in cols)
+        Vb, Tb = self.Vbs[k % len(self.Vbs)], self.Tbs[k % len(self.Tbs)]
         gi, bi, panels, parts, ti = [], [], [], [], []
         for j, e in enumerate(ents):
-            pb, vb, tb = j * ld * nb, j * ld * nb, j * nb * nb
+            pb, vb, tb = j * ld * nb, vbase + j * ld * nb, tbase + j * nb * nb
             if e["direct"] is not None:
                 ldp, rbl, rstride, poff = e["direct"]
-                panels.append((A.data, poff, ldp, rbl, rstride, e["M"], kb, kf, self.Vb, vb, ld, self.Tb, tb, nb))
+                panels.append((A.data, poff, ldp, rbl, rstride, e["M"], kb, kf, Vb, vb, ld, Tb, tb, nb))
             else:
                 g_ = e["gather"].items.copy()
                 g_["b_off"] += pb
@@ -485,7 +548,7 @@ class _Factor:
                 b_["a_off"] += pb
                 gi.append(g_)
                 bi.append(b_)
-                panels.append((self.Pb, pb, ld, 0, 0, e["M"], kb, kf, self.Vb, vb, ld, self.Tb, tb, nb))
+                panels.append((self.Pb, pb, ld, 0, 0, e["M"], kb, kf, Vb, vb, ld, Tb, tb, nb))
             parts.append((e["rows"], vb + np.asarray(e["voff"], dtype=np.int64), j * kf * wcols, tb))
             row = e["rows"][1] if tt else e["rows"][0]
             for b0 in range(0, kf, ib):
@@ -507,32 +570,61 @@ class _Factor:
             store = Td.full_T = {}
         for j, e in enumerate(ents):
             store[((e["rows"][1] if tt else e["rows"][0]), k)] = keep[j * kf * kf:(j + 1) * kf * kf]
-        return {"tt": tt, "n": len(ents), "ld": ld, "kf": kf, "zero": tt and bool(gi),
-                "plen": len(ents) * ld * nb, "gather": _tb(gi), "back": _tb(bi), "part": PART_UPPER if tt else PART_FULL,
-                "multi": ops.QrPanelMulti(panels, A.dtype, A.device), "Td": Td, "tstore": tst.finalize(),
-                "keep": keep, "upd": _LeftMulti(A, parts, kf, cols)}
+        g = {"tt": tt, "n": len(ents), "ld": ld, "kf": kf, "zero": tt and bool(gi), "Vb": Vb, "Tb": Tb, "tb0": tbase,
+             "plen": len(ents) * ld * nb, "gather": _tb(gi), "back": _tb(bi), "part": PART_UPPER if tt else PART_FULL,
+             "multi": ops.QrPanelMulti(panels, A.dtype, A.device), "Td": Td, "tstore": tst.finalize(), "keep": keep}
+        if self.bla:
+            g["next"] = _LeftMulti(A, [(r, v, j * kf * nb, t) for j, (r, v, _, t) in enumerate(parts)], kf,
+                                   [n for n in cols if n == k + 1])
+            g["rest"] = _LeftMulti(A, parts, kf, [n for n in cols if n != k + 1])
+        else:
+            g["upd"] = _LeftMulti(A, parts, kf, cols)
+        return g
 
-    def step_batched(self, k):
+    def _panel_group(self, g):
         A = self.A
         nb = A.nb
+        Tb = g["Tb"]
+        if g["zero"]:
+            self.Pb[: g["plen"]].zero_()
+        if g["gather"] is not None:
+            ops.geadd(g["part"], N_, 1.0, A.data, A.ld, 0.0, self.Pb, g["ld"], g["gather"], copy=True)
+        g["multi"].run(self.info)
+        if g["back"] is not None:
+            ops.geadd(g["part"], N_, 1.0, self.Pb, g["ld"], 0.0, A.data, A.ld, g["back"], copy=True)
+        Td = g["Td"]
+        ops.geadd(PART_FULL, N_, 1.0, Tb, nb, 0.0, Td.data, Td.ld, g["tstore"], copy=True)
+        n, kf, t0 = g["n"], g["kf"], g["tb0"]
+        if kf == nb:
+            g["keep"].view(n, kf * kf).copy_(Tb[t0: t0 + n * nb * nb].view(n, nb * nb))
+        else:
+            for j in range(n):
+                torch.as_strided(g["keep"], (kf, kf), (1, kf), j * kf * kf).copy_(
+                    torch.as_strided(Tb, (kf, kf), (1, nb), t0 + j * nb * nb))
+
+    def step_batched(self, k):
+        """One panel step in order (no look-ahead, or LU-QR's QR steps)."""
+        if self.bla:
+            self.panels_b(k)
+            self.nexts_b(k)
+            self.rests_b(k)
+            return
         for g in self.bsteps[k]:
-            if g["zero"]:
-                self.Pb[: g["plen"]].zero_()
-            if g["gather"] is not None:
-                ops.geadd(g["part"], N_, 1.0, A.data, A.ld, 0.0, self.Pb, g["ld"], g["gather"], copy=True)
-            g["multi"].run(self.info)
-            if g["back"] is not None:
-                ops.geadd(g["part"], N_, 1.0, self.Pb, g["ld"], 0.0, A.data, A.ld, g["back"], copy=True)
-            Td = g["Td"]
-            ops.geadd(PART_FULL, N_, 1.0, self.Tb, nb, 0.0, Td.data, Td.ld, g["tstore"], copy=True)
-            n, kf = g["n"], g["kf"]
-            if kf == nb:
-                g["keep"].view(n, kf * kf).copy_(self.Tb[: n * nb * nb].view(n, nb * nb))
-            else:
-                for j in range(n):
-                    torch.as_strided(g["keep"], (kf, kf), (1, kf), j * kf * kf).copy_(
-                        torch.as_strided(self.Tb, (kf, kf), (1, nb), j * nb * nb))
-            g["upd"].run(A, self.Vb, g["ld"], self.Tb, nb, self.Wb, self.W2b, qt=True)
+            self._panel_group(g)
+            g["upd"].run(self.A, g["Vb"], g["ld"], g["Tb"], self.A.nb, self.Wb, self.W2b, qt=True)
+
+    # ---- batched look-ahead: panels of every group (TS launch, then each TT round) on the panel stream
+    def panels_b(self, k):
+        for g in self.bsteps[k]:
+            self._panel_group(g)
+
+    def nexts_b(self, k):
+        for g in self.bsteps[k]:
+            g["next"].run(self.A, g["Vb"], g["ld"], g["Tb"], self.A.nb, self.Wn, self.W2n, qt=True)
+
+    def rests_b(self, k):
+        for g in self.bsteps[k]:
+            g["rest"].run(self.A, g["Vb"], g["ld"], g["Tb"], self.A.nb, self.Wb, self.W2b, qt=True)
 
     def _entry(self, k, rows, tt):
         A = self.A
@@ -602,13 +694,13 @@ class _Factor:
             else:
                 e["upd"] = _Left(A, d, e["voff"], e["kf"], cols) if (cols and e["myline"]) else None
             out.append(e)
-        for (p, m) in tts:
-            e = self._entry(k, [p, m], True)
+        for (p, ms) in tts:
+            e = self._entry(k, [p] + list(ms), True)
             if e["cross"] and e["myline"]:   # only my process row's reflector row: partial W summed with the peer
                 j = 0 if A.myrow == e["rp"] else 1
                 rows, voff = [e["rows"][j]], [e["voff"][j]]
             else:
-                rows, voff = [p, m], e["voff"]
+                rows, voff = e["rows"], e["voff"]
             if self.la:
                 # a cross-row kill sums partial W with the peer: both rows must issue the exchange, so the
                 # next / rest parts exist on both rows whenever the other one has columns there
@@ -729,6 +821,13 @@ def factor_New(ctx, A, TS, TT, tree, name="geqrf") -> Taskpool:
                 rst = tp.task(f"qr_rest({k})", "update", (lambda e=e, b=buf: st.apply(e, e["rest"], b, st.wr)),
                               [pan, prev_rest])
             prev_next, prev_rest2, prev_rest = nxt or pan, prev_rest, rst or prev_rest
+    elif st.batched and st.bla:
+        prev_next = prev_rest = prev_rest2 = None
+        for k in range(st.kt):
+            pan = tp.task(f"qr_panels({k})", "panel", (lambda k=k: st.panels_b(k)), [prev_next, prev_rest2])
+            nxt = tp.task(f"qr_next({k})", "panel", (lambda k=k: st.nexts_b(k)), [pan, prev_rest])
+            rst = tp.task(f"qr_rest({k})", "update", (lambda k=k: st.rests_b(k)), [pan, prev_rest])
+            prev_next, prev_rest2, prev_rest = nxt, prev_rest, rst
     elif st.batched:
         prev = None
         for k in range(st.kt):
@@ -791,7 +890,7 @@ class _Apply:
         g = A.grid
         k = s[1]
         tt = s[0] == "tt"
-        rows = [s[2], s[3]] if tt else s[2]
+        rows = [s[2]] + list(s[3]) if tt else s[2]
         kb = A.tile_cols(k)
         voff, c = [], 0
         for r in rows:
@@ -826,7 +925,8 @@ class _Apply:
         cp, dg = TileBatch(), TileBatch()
         if tt:
             dg.add(0, A.tile_rows(rows[0]), kf)
-            cp.add(A.offset(rows[1], k), A.tile_rows(rows[1]), kf, b_off=voff[1])
+            for r, o in zip(rows[1:], voff[1:]):
+                cp.add(A.offset(r, k), A.tile_rows(r), kf, b_off=o)
             it["cp"] = [(PART_UPPER, cp.finalize())]
         else:
             dg.add(0, A.tile_rows(rows[0]), kf)

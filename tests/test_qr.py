@@ -379,6 +379,49 @@ def test_hqr_distributed(world, P, engine):
         assert rel_err(sum(out[k][i] for k in range(world)), r[i]) < 1e-12, i
 
 
+# one-row trees: every pivot's TT kills of a step are ONE stacked panel of triangles (qr_panel.step_plan)
+ONE_ROW_TREES = [(0, 0, 1, 1), (1, 0, 2, 1), (3, 0, 1, 1), (1, 0, -1, 1)]
+
+
+def test_tt_stack_merge_plan():
+    """Merged stacks: each pivot once per step, victims in kill order, never more rounds than the
+    pairwise plan, and the greedy chains collapse."""
+    ctx_ = dp.init(device="cpu")
+    A = dp.block_cyclic(ctx_, torch.float64, 2, 2, 64, 64)
+    for ta in ONE_ROW_TREES:
+        tree = dp.hqr_init(dp.dplasmaNoTrans, A, *ta)
+        n_pair = n_merged = 0
+        for k in range(A.nt):
+            d1, pairs = qr_panel.step_plan(tree, k, merge=False)
+            d2, stacks = qr_panel.step_plan(tree, k, merge=True)
+            assert d1 == d2
+            assert sorted(m for _, ms in stacks for m in ms) == sorted(ms[0] for _, ms in pairs)
+            assert len(stacks) <= 1 and (not pairs or stacks[0][0] == d1[0][0])   # one survivor: the step's head
+            n_pair += len(pairs)
+            n_merged += len(stacks)
+        assert n_merged <= n_pair
+
+
+@pytest.mark.parametrize("prec", list("dz"))
+@pytest.mark.parametrize("treeargs", ONE_ROW_TREES)
+def test_hqr_one_row_tree(ctx, prec, treeargs):
+    M, N = 70, 40
+    e1, e2, *_ = _hqr_run(ctx, DTYPES[prec], False, treeargs, M, N, 8, 4)
+    assert e1 < 1e-13 and e2 < 1e-13
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", list("ds"))
+@pytest.mark.parametrize("treeargs", ONE_ROW_TREES)
+def test_gpu_hqr_one_row_tree(gctx, ctx, prec, treeargs):
+    """Merged TT stacks through the GPU panel kernel vs the same plan on the CPU."""
+    dt = DTYPES[prec]
+    res = [_hqr_run(c, dt, False, treeargs, 600, 320, 32, 8) for c in (gctx, ctx)]
+    lim = 1e-4 if prec == "s" else 1e-12
+    assert res[0][0] < lim and res[0][1] < lim
+    assert rel_err(_dense(res[0][2]), _dense(res[1][2])) < lim * 10
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("prec", list("sdcz"))
 @pytest.mark.parametrize("lq", [False, True])
@@ -475,6 +518,40 @@ def test_gpu_qr_panel_kernel(prec, M, nc, kf):
     tol = 1e-10 if prec == "d" else 2e-3
     for i, (x, y) in enumerate(zip(g, c)):
         assert rel_err(x, y) < tol, i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,nc", [(700, 96), (256, 256), (3000, 128)])
+def test_gpu_qr_panel_kernel_rank_deficient(M, nc):
+    """Columns that make the kernel's Gram-downdated norms cancel (exact copies, 1e-10
+    perturbations, zero columns, the last rows of a square panel) take the exact reduction path:
+    Q = I - V T V^T stays orthogonal and Q^T P0 = [R; 0] to working precision."""
+    from dplasma_amd.ops import tile_ops as ops
+    dev, dt = "cuda", torch.float64
+    g = torch.Generator().manual_seed(7)
+    P0 = torch.randn(M, nc, generator=g, dtype=dt)
+    P0[:, 5] = P0[:, 3]
+    P0[:, 9] = P0[:, 2] + 1e-10 * torch.randn(M, generator=g, dtype=dt)
+    P0[:, 40] = 0.0
+    P0[:, 41] = 1e-3 * P0[:, 0] - 2.0 * P0[:, 33]
+    ld = M + 3
+    P = torch.zeros(ld * nc, dtype=dt, device=dev)
+    torch.as_strided(P, (M, nc), (1, ld), 0).copy_(P0.to(dev))
+    V = torch.zeros(ld * nc, dtype=dt, device=dev)
+    Tm = torch.zeros(nc * nc, dtype=dt, device=dev)
+    ws = ops.qr_panel_workspace(nc, nc, dt, dev)
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    ops.qr_panel(P, ld, M, nc, nc, V, ld, Tm, nc, ws, info)
+    assert int(info.item()) == 0
+    Pf = torch.as_strided(P, (M, nc), (1, ld), 0).cpu()
+    Vf = torch.as_strided(V, (M, nc), (1, ld), 0).cpu()
+    Tf = torch.as_strided(Tm, (nc, nc), (1, nc), 0).cpu()
+    Q = torch.eye(M, dtype=dt) - Vf @ Tf @ Vf.T
+    assert (Q.T @ Q - torch.eye(M, dtype=dt)).abs().max() < 1e-13
+    ref = Q.T @ P0
+    assert rel_err(torch.triu(ref[:nc]), torch.triu(Pf[:nc])) < 1e-13
+    if M > nc:
+        assert ref[nc:].abs().max() < 1e-12 * P0.abs().max()
 
 
 def _qrp_worker(rank, world, P):
