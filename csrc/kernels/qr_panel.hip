@@ -128,6 +128,9 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
     T a[QP_B];
 #pragma unroll
     for (int c = 0; c < QP_B; ++c) a[c] = (rowok && c < cb) ? P[grow + (long long)(b0 + c) * ldp] : T(0);
+    // rows above b0 take no part in the block (zeros of the Gram staging and of V_b): the MFMA K loops
+    // start at the first 16-row group that reaches b0
+    const int rs16 = max(0, min(R16, b0 - rbase)) & ~15;
     QP_TICK(7);
     // ------------------------------------------------------------ block Gram + top-row replica
     for (int e = tid; e < QP_B * QP_LD; e += 256) {
@@ -156,7 +159,7 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
       acc_t a0, a1;
 #pragma unroll
       for (int r = 0; r < 4; ++r) a0[r] = a1[r] = T(0);
-      for (int r0 = 0; r0 < R16; r0 += 8) {
+      for (int r0 = rs16; r0 < R16; r0 += 8) {
         const int rr = r0 + (l >> 4);
         a0 = MM::mma(Xs[pt * 16 + (l & 15)][rr], Xs[qt * 16 + (l & 15)][rr], a0);
         a1 = MM::mma(Xs[pt * 16 + (l & 15)][rr + 4], Xs[qt * 16 + (l & 15)][rr + 4], a1);
@@ -388,32 +391,38 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
     const int nX = QP_B + b0 + nA;
     const bool act = rbase + nr > b0;
     const long long E = (long long)QP_B * nX;
+    // the next global chunk's loads are issued before the current chunk's MFMA (in flight during it)
+    T t[QP_B];
+    auto fetch_y = [&](int x0) {
+      const int cw = min(QP_B, nX - x0);
+      const bool live = act && tid < R16 && rowok && grow >= b0;
+      // chunks never straddle the V_b | V_prev | A_rest boundaries (b0 is a multiple of 32)
+      const T* src = x0 < QP_B + b0 ? V + grow + (long long)(x0 - QP_B) * ldv
+                                    : P + grow + (long long)(cb + x0 - QP_B) * ldp;
+      const long long ld = x0 < QP_B + b0 ? ldv : ldp;
+#pragma unroll
+      for (int c = 0; c < QP_B; ++c) t[c] = (live && c < cw) ? src[c * ld] : T(0);
+    };
+    if (nX > QP_B) fetch_y(QP_B);
     for (int x0 = 0; x0 < nX; x0 += QP_B) {
       const int cw = min(QP_B, nX - x0);
       T* pw = G == 1 ? Yg : part2 + (long long)w * E;   // one workgroup: its partial IS Y
       if (act) {
         if (tid < R16) {
-          // chunks never straddle the V_b | V_prev | A_rest boundaries (b0 is a multiple of 32)
-          const bool live = rowok && grow >= b0;
           if (x0 < QP_B) {
             for (int c = 0; c < QP_B; ++c) Xs[c][tid] = Ab[c][tid];
           } else {
-            const T* src = x0 < QP_B + b0 ? V + grow + (long long)(x0 - QP_B) * ldv
-                                          : P + grow + (long long)(cb + x0 - QP_B) * ldp;
-            const long long ld = x0 < QP_B + b0 ? ldv : ldp;
-            T t[QP_B];
-#pragma unroll
-            for (int c = 0; c < QP_B; ++c) t[c] = (live && c < cw) ? src[c * ld] : T(0);
 #pragma unroll
             for (int c = 0; c < QP_B; ++c) Xs[c][tid] = t[c];
           }
         }
         __syncthreads();
+        if (x0 >= QP_B && x0 + QP_B < nX) fetch_y(x0 + QP_B);
         const int pt = wv & 1, qt = wv >> 1;
         acc_t a0, a1, a2, a3;
 #pragma unroll
         for (int r = 0; r < 4; ++r) a0[r] = a1[r] = a2[r] = a3[r] = T(0);
-        for (int r0 = 0; r0 < R16; r0 += 16) {
+        for (int r0 = rs16; r0 < R16; r0 += 16) {
           const int rr = r0 + (l >> 4);
           a0 = MM::mma(Ab[pt * 16 + (l & 15)][rr], Xs[qt * 16 + (l & 15)][rr], a0);
           a1 = MM::mma(Ab[pt * 16 + (l & 15)][rr + 4], Xs[qt * 16 + (l & 15)][rr + 4], a1);
@@ -506,6 +515,14 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
     // ------------------------------------------------------------ A_rest -= V_b (T_b^T Y)
     if (nA > 0 && act) {
       const int ycol0 = QP_B + b0;
+      const bool live = tid < R16 && rowok && grow >= b0;
+      auto fetch_a = [&](int a0) {
+        const int cw = min(QP_B, nA - a0);
+        const T* src = P + grow + (long long)(b0 + cb + a0) * ldp;
+#pragma unroll
+        for (int c = 0; c < QP_B; ++c) t[c] = (live && c < cw) ? src[(long long)c * ldp] : T(0);
+      };
+      fetch_a(0);
       for (int a0 = 0; a0 < nA; a0 += QP_B) {
         const int cw = min(QP_B, nA - a0);
         for (int e = tid; e < QP_B * QP_B; e += 256) {
@@ -513,36 +530,30 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
           Ws[q][i] = q < cw ? ld_sc1(&Yg[(long long)i * nX + ycol0 + a0 + q]) : T(0);
         }
         if (tid < R16) {
-          const bool live = rowok && grow >= b0;
-          const T* src = P + grow + (long long)(b0 + cb + a0) * ldp;
-          T t[QP_B];
-#pragma unroll
-          for (int c = 0; c < QP_B; ++c) t[c] = (live && c < cw) ? src[(long long)c * ldp] : T(0);
 #pragma unroll
           for (int c = 0; c < QP_B; ++c) Xs[c][tid] = t[c];
         }
         __syncthreads();
-        T o[4];
+        if (a0 + QP_B < nA) fetch_a(a0 + QP_B);   // next chunk in flight during this one
         {
-          const int q = tid & 31, kg = tid >> 5;
+          // W' = T_b^T Y_chunk on MFMA: wave (pt, qt) forms the 16 x 16 tile W'(pt, qt), K = 32
+          const int pt = wv & 1, qt = wv >> 1;
+          acc_t acc;
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int k = kg * 4 + u;
-            T z = T(0);
-            for (int i = 0; i <= k; ++i) z += Ts[k][i] * Ws[q][i];
-            o[u] = z;
+          for (int r = 0; r < 4; ++r) acc[r] = T(0);
+#pragma unroll
+          for (int i0 = 0; i0 < QP_B; i0 += 4) {
+            const int i = i0 + (l >> 4);
+            acc = MM::mma(Ts[pt * 16 + (l & 15)][i], Ws[qt * 16 + (l & 15)][i], acc);
           }
-        }
-        __syncthreads();
-        {
-          const int q = tid & 31, kg = tid >> 5;
+          __syncthreads();
 #pragma unroll
-          for (int u = 0; u < 4; ++u) Ws[q][kg * 4 + u] = o[u];
+          for (int r = 0; r < 4; ++r) Ws[qt * 16 + (l & 15)][pt * 16 + MM::drow(l, r)] = acc[r];
         }
         __syncthreads();
         const int RT = R16 / 16;
-        for (int t = wv; t < RT * 2; t += 4) {
-          const int rt = t >> 1, qt = t & 1;
+        for (int tt = rs16 / 16 * 2 + wv; tt < RT * 2; tt += 4) {
+          const int rt = tt >> 1, qt = tt & 1;
           acc_t acc;
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[r] = Xs[qt * 16 + (l & 15)][rt * 16 + MM::drow(l, r)];

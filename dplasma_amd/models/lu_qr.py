@@ -151,7 +151,63 @@ class _GetrfQrf(Taskpool):
             from .lu import _GetrfDev
             self.fast_info = torch.zeros(1, dtype=torch.int32, device=A.device)
             self.fast = _GetrfDev(ctx, A, self.fast_info, pivot=True, trailing_only=True)
+            if os.environ.get("DPLASMA_LUQR_LOOKAHEAD", "1") != "0":
+                self._fast_tasks()
         self.finish_build()
+
+    def _fast_tasks(self):
+        """Look-ahead across LU and QR steps (device path): every step is PANEL / NEXT on the panel
+        stream and the bulk REST on the update stream, so step k+1's panel -- a pivoting LU panel or the
+        QR step's TS + TT launches -- runs beside step k's trailing update.  LU: PANEL(k) -> SWAP(k)
+        (after REST(k-1): the interchanges touch every trailing column) -> NEXT(k) || REST(k);
+        QR: PANELS(k) -> NEXT(k) (after REST(k-1)) || REST(k) (V / T double-buffered by step parity)."""
+        f, dev = self.qpf, self.fast
+        if f is None or not (f.simple or (f.batched and f.bla)):
+            return
+        prev_next = prev_rest = None
+        for k in range(self.minMNT):
+            cond = self._a_priori(k)
+            self.lu_tab[k] = cond
+            if cond:
+                pn = self.task(f"LU_PANEL({k})", "panel", (lambda k=k: self._lu_panel_fast(k)), [prev_next], prio=3)
+                sw = self.task(f"LU_SWAP({k})", "update", (lambda k=k: dev.swap(k)), [pn, prev_rest], prio=2)
+                prev_next = self.task(f"LU_NEXT({k})", "panel", (lambda k=k: dev.next(k)), [sw], prio=2)
+                prev_rest = self.task(f"LU_REST({k})", "update", (lambda k=k: dev.rest(k)), [sw], prio=1)
+            else:
+                pn = self.task(f"QR_PANELS({k})", "panel", (lambda k=k: self._qr_panels_fast(k)), [prev_next], prio=3)
+                nx = self.task(f"QR_NEXT({k})", "panel", (lambda k=k: self._qr_part_fast(k, "next")),
+                               [pn, prev_rest], prio=2)
+                prev_rest = self.task(f"QR_REST({k})", "update", (lambda k=k: self._qr_part_fast(k, "rest")),
+                                      [pn, prev_rest], prio=1)
+                prev_next = nx
+
+    def _lu_panel_fast(self, k):
+        dev = self.fast
+        dev.panel(k)
+        if self.IPIV.is_local(k, k):
+            kmin = dev.plan[k]["kmin"]
+            t = self.IPIV.tile(k, k)
+            t.zero_()
+            t[:kmin, 0] = dev.piv_dev[:kmin] + 1
+
+    def _qr_panels_fast(self, k):
+        f = self.qpf
+        if self.IPIV.is_local(k, k):
+            self.IPIV.tile(k, k).zero_()
+        if f.simple:
+            f.panel(k, f.steps[k][0], k % 2)
+        else:
+            f.panels_b(k)
+
+    def _qr_part_fast(self, k, part):
+        f = self.qpf
+        if f.simple:
+            e = f.steps[k][0]
+            f.apply(e, e.get(part), k % 2, f.wn if part == "next" else f.wr)
+        elif part == "next":
+            f.nexts_b(k)
+        else:
+            f.rests_b(k)
 
     def _a_priori(self, k):
         """The step's choice when it does not depend on the data (1 LU, 0 QR), else None."""
@@ -409,7 +465,10 @@ class _GetrfQrf(Taskpool):
         A = self.A
         ctx = self.ctx
         if self.fast is not None:
-            self._run_fast()
+            if self.tasks:
+                Taskpool.run(self, ctx)
+            else:
+                self._run_fast()
             if self.info_out is not None:
                 self.info_out[0] = 0
             return
