@@ -162,3 +162,7 @@ static inline hipError_t dpl_zero_sync(void* p, size_t bytes) {
   (void)hipStreamDestroy(s);
   return e != hipSuccess ? e : e2;
 }
+
+// Pivot-search magnitude: |x| with NaN mapped to 0, so an eligible row always beats the "no candidate" marker
+// (-1) and a NaN column still yields an in-range pivot (the row j itself) instead of the sentinel index.
+template <typename R> __device__ inline R piv_mag(R v) { return v >= R(0) ? v : R(0); }

@@ -104,7 +104,7 @@ __global__ __launch_bounds__(DLR) void k_lu_block_dist(T* __restrict__ A, int ld
     __syncthreads();
     // ---- 2. local candidate: T rows only on the diagonal owner (the replicas must not nominate)
     const bool elig = own && g >= j && (g >= tr || diag);
-    block_argmax(elig ? (double)abs1(tile[cj * R + r]) : -1.0, elig ? g : 0x7fffffff, sv, si);
+    block_argmax(elig ? piv_mag((double)abs1(tile[cj * R + r])) : -1.0, elig ? g : 0x7fffffff, sv, si);
     if (tid == 0) {
       st_sc1(&pval[par * G + w], sv[0]);
       st_sc1(&pidx[par * G + w], si[0]);

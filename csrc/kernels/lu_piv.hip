@@ -85,7 +85,7 @@ __global__ __launch_bounds__(LUR) void k_lu_col(T* __restrict__ A, int ld, int m
   // ---- 2. workgroup |max| of column j (ties -> smallest row, LAPACK i?amax)
   __shared__ R sv[LUR];
   __shared__ int si[LUR];
-  sv[tid] = in ? abs1(A[r + (long long)j * ld]) : R(-1);
+  sv[tid] = in ? piv_mag(abs1(A[r + (long long)j * ld])) : R(-1);
   si[tid] = in ? r : 0x7fffffff;
   __syncthreads();
   for (int s = LUR / 2; s > 0; s >>= 1) {
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(PLR) void k_lu_block_persist(T* __restrict__ A, int
     }
     __syncthreads();
     // ---- 2. local |max| of column cj over rows >= j; publish it with its row, and row j
-    double v = (own && g >= j) ? (double)abs1(tile[cj * R + r]) : -1.0;
+    double v = (own && g >= j) ? piv_mag((double)abs1(tile[cj * R + r])) : -1.0;
     int vi = (own && g >= j) ? g : 0x7fffffff;
     wave_argmax(v, vi);
     if ((tid & 63) == 0) { sv[tid >> 6] = v; si[tid >> 6] = vi; }
@@ -497,7 +497,7 @@ __global__ __launch_bounds__(PLR) void k_lu_block_reg(T* __restrict__ A, int ld,
         if (c < BW) v[c] = sub(v[c], mul(l, prow[c]));
     }
     // ---- 2. workgroup |max| of column cj over rows >= j
-    double val = (own && g >= j) ? (double)abs1(v[cj]) : -1.0;
+    double val = (own && g >= j) ? piv_mag((double)abs1(v[cj])) : -1.0;
     int vi = (own && g >= j) ? g : 0x7fffffff;
     wave_argmax(val, vi);
     if ((tid & 63) == 0) { sv[tid >> 6] = val; si[tid >> 6] = vi; }

@@ -168,7 +168,7 @@ class _GetrfDev:
       "percol" -- the distributed pivoting driven from the host (one all-gather and two host
                syncs per column; kept as the transport-independent reference of "dist")."""
 
-    def __init__(self, ctx, A, info, pivot: bool = True, trailing_only: bool = False):
+    def __init__(self, ctx, A, info, pivot: bool = True, trailing_only: bool = False, lookahead=None):
         self.ctx, self.A, self.info = ctx, A, info
         self.pivot = pivot   # False: getrf_nopiv (same task structure, no interchanges)
         # trailing_only: step k's interchanges touch tile columns >= k only (the hybrid LU-QR keeps every
@@ -182,7 +182,9 @@ class _GetrfDev:
         # grid-barrier panel kernel beside the REST GEMM slows from ~0.5 to ~1.2 ms per 64-column
         # block (its workgroups share CUs with GEMM waves), which eats the overlap: DGETRF 32k
         # 28.2 -> 27.1 TF/s, 64k 48.1 -> 47.2 TF/s with look-ahead on
-        self.lookahead = os.environ.get("DPLASMA_LU_LOOKAHEAD", "0") == "1"
+        # (lookahead=True: a caller that issues PANEL(k+1) beside REST(k) itself -- the hybrid LU-QR -- needs the
+        # parity-alternating panel buffers whatever the environment says)
+        self.lookahead = (os.environ.get("DPLASMA_LU_LOOKAHEAD", "0") == "1") if lookahead is None else bool(lookahead)
         self.pbufs = [torch.zeros(max(1, A.m * nb), dtype=A.dtype, device=dev)
                       for _ in range(2 if self.lookahead else 1)]
         self.piv_dev = torch.zeros(nb, dtype=torch.int32, device=dev)

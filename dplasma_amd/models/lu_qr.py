@@ -150,8 +150,10 @@ class _GetrfQrf(Taskpool):
                 and self._a_priori(0) is not None and os.environ.get("DPLASMA_LUQR_SYNC", "0") != "1"):
             from .lu import _GetrfDev
             self.fast_info = torch.zeros(1, dtype=torch.int32, device=A.device)
-            self.fast = _GetrfDev(ctx, A, self.fast_info, pivot=True, trailing_only=True)
-            if os.environ.get("DPLASMA_LUQR_LOOKAHEAD", "1") != "0":
+            la = os.environ.get("DPLASMA_LUQR_LOOKAHEAD", "1") != "0"
+            # look-ahead issues PANEL(k+1) beside REST(k): the LU engine alternates its panel buffers
+            self.fast = _GetrfDev(ctx, A, self.fast_info, pivot=True, trailing_only=True, lookahead=la)
+            if la:
                 self._fast_tasks()
         self.finish_build()
 

@@ -115,8 +115,52 @@ def test_getrf_qrf_device_path_cpu(ctx, monkeypatch, crit, alpha):
     assert lu_tab == lu_tab2
 
 
+@pytest.mark.parametrize("crit,alpha", [(dp.DEFAULT_CRITERIUM, 1.0), (dp.LU_ONLY_CRITERIUM, 1.0),
+                                        (dp.QR_ONLY_CRITERIUM, 1.0), (dp.RANDOM_CRITERIUM, 50.0)])
+def test_getrf_qrf_lookahead_hazards(ctx, monkeypatch, crit, alpha):
+    """The device path's look-ahead task graph (PANEL / NEXT on the panel stream, SWAP / REST on the
+    update stream): every buffer a step reuses two steps later is released first -- PANEL(k+2) (panel
+    buffer k % 2, QR V / T buffer k % 2) and every step's SWAP / NEXT / REST after REST(k) -- and the LU
+    engine alternates its panel buffers."""
+    monkeypatch.setenv("DPLASMA_LUQR_FAST", "1")
+    N, NB, IB = 256, 32, 8
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+    dp.plrnt(ctx, A, 3)
+    TS = dp.block_cyclic(ctx, torch.float64, IB, NB, A.mt * IB, N)
+    TT = dp.block_cyclic(ctx, torch.float64, IB, NB, A.mt * IB, N)
+    IP = dp.qrf_ipiv_descriptor(ctx, A)
+    tree = dp.hqr_init(dp.dplasmaNoTrans, A, 1, -1, -1, 1, -1, 0)
+    tp = dp.getrf_qrf_New(ctx, tree, A, IP, TS, TT, crit, alpha, [0] * A.mt)
+    assert tp.fast is not None and tp.fast.lookahead and len(tp.fast.pbufs) == 2 and tp.tasks
+    anc = []
+    for t in tp.tasks:
+        a = set(t.deps)
+        for d in t.deps:
+            a |= anc[d]
+        anc.append(a)
+    by = {t.name: t.tid for t in tp.tasks}
+
+    def tid(kind, k):
+        for pre in ("LU_", "QR_"):
+            n = f"{pre}{kind}({k})"
+            if n in by:
+                return by[n]
+        return by.get(f"QR_PANELS({k})") if kind == "PANEL" else None
+    for k in range(A.mt - 2):
+        r = tid("REST", k)
+        for kind in ("PANEL", "SWAP", "NEXT", "REST"):
+            t2 = tid(kind, k + 2)
+            if t2 is not None:
+                assert r in anc[t2], (kind, k)
+        t1 = tid("REST", k + 1)
+        assert r in anc[t1]
+    tp.run(ctx)
+    assert tp.complete(ctx) == 0
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("crit,alpha", [(dp.DEFAULT_CRITERIUM, 1.0), (dp.RANDOM_CRITERIUM, 50.0)])
+@pytest.mark.parametrize("crit,alpha", [(dp.DEFAULT_CRITERIUM, 1.0), (dp.RANDOM_CRITERIUM, 50.0),
+                                        (dp.LU_ONLY_CRITERIUM, 1.0)])
 def test_gpu_getrf_qrf_device_path(crit, alpha):
     g = dp.init(device="cuda:0")
     a0, b0, B, lu_tab = _solve(g, torch.float64, 1536, 256, 32, crit, alpha, 1)

@@ -1,5 +1,6 @@
 #!/bin/bash
 # r4 batch 20: where LU-QR's time goes -- LU-only / QR-only criteria, getrf_1d at NB=256, kernel split of DEFAULT.
+# (rerun after the fix of the first attempt's fault: the LU engine's single panel buffer under LU-QR look-ahead)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 R=$(pwd)
 O=$R/gpurun_out/r4b20
@@ -14,6 +15,7 @@ step() {
   echo "rc=$rc" | tee -a $O/summary.log
   return $rc
 }
+step luqr_tests 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_lu_qr.py -m gpu || exit 1
 step luqr_lu_only 300 python tools/gpu/luqr_syncdebug.py 32768 256 3 || exit 1
 step luqr_qr_only 300 python tools/gpu/luqr_syncdebug.py 32768 256 4 || exit 1
 step getrf32k_nb256 200 python tools/bench_algo.py getrf_1d -N 32768 --nb 256 --runs 2 || exit 1
