@@ -354,12 +354,31 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
       }
       // replicas: rows r > jj of the top block take the reflector like any row; the Gram matrix
       // of rows > j is the (unchanged) one of rows >= j minus the new row j's outer product
-      for (int e = tid; e < QP_B * QP_B; e += 256) {
-        const int r = e >> 5, c = e & 31;
-        if (r > jj && c > jj) {
+      {
+        // thread (c, r0) owns entries (r0 + 8u, c), u < 4: every operand is loaded before any store
+        const int c = tid & 31, r0 = tid >> 5;
+        if (c > jj) {
           const T fc = fw[c - jj];
-          Tp[r][c] -= (scale * Tp[r][jj]) * fc;
-          Gm[r][c] -= (Tp[jj][r] - fw[r - jj]) * (Tp[jj][c] - fc);
+          const T njc = Tp[jj][c] - fc;
+          T trj[4], nrj[4], tpv[4], gmv[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int r = r0 + 8 * u;
+            if (r > jj) {
+              trj[u] = Tp[r][jj];
+              nrj[u] = Tp[jj][r] - fw[r - jj];
+              tpv[u] = Tp[r][c];
+              gmv[u] = Gm[r][c];
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int r = r0 + 8 * u;
+            if (r > jj) {
+              Tp[r][c] = tpv[u] - (scale * trj[u]) * fc;
+              Gm[r][c] = gmv[u] - nrj[u] * njc;
+            }
+          }
         }
       }
 #pragma unroll
@@ -597,12 +616,21 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
       if (tid < b0)
         for (int k = 0; k < QP_B; ++k) Ab[k][tid] = k < bw ? ld_sc1(&Xc[((long long)b * QP_B + k) * kf + tid]) : T(0);
       __syncthreads();
-      if (tid < b0)
-        for (int c = 0; c < QP_B; ++c) {
-          T z = T(0);
-          for (int k = 0; k <= c; ++k) z += Ab[k][tid] * Ts[c][k];
-          Xs[c][tid] = z;   // Z(j = tid, c)
+      // Z = X_b T_b on MFMA (b0 x 32 times 32 x 32, T_b upper triangular with zeros below): wave wv forms the
+      // 16 x 16 tiles wv, wv + 4, ... of Z -- was a scalar 32 x 32 loop per row (~0.2 ms per panel on G = 1)
+      for (int zt = wv; zt < (b0 / 16) * 2; zt += 4) {
+        const int pt = zt >> 1, qt = zt & 1;
+        acc_t acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = T(0);
+#pragma unroll
+        for (int k0 = 0; k0 < QP_B; k0 += 4) {
+          const int k = k0 + (l >> 4);
+          acc = MM::mma(Ab[k][pt * 16 + (l & 15)], Ts[qt * 16 + (l & 15)][k], acc);
         }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Xs[qt * 16 + (l & 15)][pt * 16 + MM::drow(l, r)] = acc[r];   // Z(j, c)
+      }
       __syncthreads();
       T* trow = &Ab[0][0];   // [32][b0]: the staged T rows of two own row tiles
       const int own_rt = (nrt - w + G - 1) / G;

@@ -65,9 +65,13 @@ POTRF_TRSM = "rb"   # "fused": the diagonal owner factors its tile and solves it
 # CUs instead of waiting for GEMM workgroups to retire.  (single process, distributed)
 POTRF_RESERVE = (0, 0)
 # one GPU process: "stream" (the stream-program engine below), "dtr" (the device task runtime,
-# models/potrf_dtr.py) or "auto" (dtr from POTRF_DTR_MIN_N up when it supports the operand)
-POTRF_ENGINE = "stream"
+# models/potrf_dtr.py) or "auto" (dtr for POTRF_DTR_MIN_N <= N < POTRF_DTR_MAX_N when it supports the
+# operand).  Measured (profiles/r4_dtr_colorder.txt, r4_b16): 32k dtr 63-64 vs stream 61-62 TF/s; 64k dtr
+# 68.4-69.3 vs stream 69.4-70.1 (the stream engine's D = 2 deferred updates run the GEMMs at their
+# large-k rate, which the DTR's 128 x 128 x 512 update tasks do not reach); 16k dtr 38 vs 47.
+POTRF_ENGINE = "auto"
 POTRF_DTR_MIN_N = 24576
+POTRF_DTR_MAX_N = 49152
 
 
 def _defer_depth(nt_left: int, D: int, min_tiles: int) -> int:
@@ -103,10 +107,12 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
     eng = os.environ.get("DPLASMA_POTRF_ENGINE", POTRF_ENGINE)
     if eng in ("dtr", "auto"):
         from . import potrf_dtr
-        # auto: the device task runtime from POTRF_DTR_MIN_N up (below it the panel chain dominates and the
-        # stream engine's register-resident panel solve is faster: profiles/r4_dtr_*.txt)
-        big = A.n >= int(os.environ.get("DPLASMA_POTRF_DTR_MIN_N", POTRF_DTR_MIN_N))
-        if potrf_dtr.supported(ctx, uplo, A) and (eng == "dtr" or big):
+        # auto: the device task runtime in its measured window (below it the panel chain dominates and the
+        # stream engine's register-resident panel solve is faster; above it the stream engine's deferred
+        # large-k updates win: profiles/r4_dtr_*.txt)
+        win = (int(os.environ.get("DPLASMA_POTRF_DTR_MIN_N", POTRF_DTR_MIN_N)) <= A.n
+               < int(os.environ.get("DPLASMA_POTRF_DTR_MAX_N", POTRF_DTR_MAX_N)))
+        if potrf_dtr.supported(ctx, uplo, A) and (eng == "dtr" or win):
             return potrf_dtr.potrf_dtr_New(ctx, uplo, A, info_out)
         if eng == "dtr":
             raise ValueError("DPLASMA_POTRF_ENGINE=dtr: needs one GPU process, lower, fp64, NB = 512, N % 512 == 0")
