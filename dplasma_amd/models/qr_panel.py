@@ -265,11 +265,16 @@ class _LeftMulti:
             self.wlen = max(self.wlen, int(wbase + kf * wn.sum()))
         self.g1, self.g2, self.g3 = g1.finalize(), g2.finalize(), g3.finalize()
 
-    def run(self, C, V, ldv, Tm, ldt, W, W2, qt: bool):
+    def run(self, C, V, ldv, Tm, ldt, W, W2, qt: bool, Yv=None):
+        """Yv (optional) = V op(T), formed once per reflector set: C -= Yv (V^T C) -- two GEMM launches,
+        and no T^T W product whose cost grows with the trailing width (9 % of an a = 4 HQR step's flops)."""
         if self.empty:
             return
         kf = self.kf
         ops.gemm(T_, N_, 1.0, V, ldv, C.data, C.ld, 0.0, W, kf, self.g1)
+        if Yv is not None:
+            ops.gemm(N_, N_, -1.0, Yv, ldv, W, kf, 1.0, C.data, C.ld, self.g3)
+            return
         ops.gemm(T_ if qt else N_, N_, 1.0, Tm, ldt, W, kf, 0.0, W2, kf, self.g2)
         ops.gemm(N_, N_, -1.0, V, ldv, W2, kf, 1.0, C.data, C.ld, self.g3)
 
@@ -514,6 +519,9 @@ class _Factor:
         nbuf = 2 if self.bla else 1
         self.Pb = torch.zeros(need_p, dtype=dt, device=dev)
         self.Vbs = [torch.zeros(need_v, dtype=dt, device=dev) for _ in range(nbuf)]
+        # Y = V op(T) of every group (DPLASMA_QR_VT=0: apply T to W instead)
+        self.use_vt = os.environ.get("DPLASMA_QR_VT", "1") != "0"
+        self.Ybs = [torch.zeros(need_v, dtype=dt, device=dev) for _ in range(nbuf)] if self.use_vt else None
         self.Tbs = [torch.zeros(need_t, dtype=dt, device=dev) for _ in range(nbuf)]
         self.Wb = torch.zeros(need_w, dtype=dt, device=dev)
         self.W2b = torch.zeros(need_w, dtype=dt, device=dev)
@@ -535,6 +543,8 @@ class _Factor:
         ld = max(e["ld"] for e in ents)
         wcols = sum(A.tile_cols(n) for n in cols)
         Vb, Tb = self.Vbs[k % len(self.Vbs)], self.Tbs[k % len(self.Tbs)]
+        Yb = self.Ybs[k % len(self.Ybs)] if self.use_vt else None
+        ygemm = GemmBatch() if self.use_vt else None
         gi, bi, panels, parts, ti = [], [], [], [], []
         for j, e in enumerate(ents):
             pb, vb, tb = j * ld * nb, vbase + j * ld * nb, tbase + j * nb * nb
@@ -550,6 +560,8 @@ class _Factor:
                 bi.append(b_)
                 panels.append((self.Pb, pb, ld, 0, 0, e["M"], kb, kf, Vb, vb, ld, Tb, tb, nb))
             parts.append((e["rows"], vb + np.asarray(e["voff"], dtype=np.int64), j * kf * wcols, tb))
+            if ygemm is not None:
+                ygemm.add(vb, e["M"], kf, [(vb, tb, kf)])     # Y(entry) = V(entry) T(entry)^T
             row = e["rows"][1] if tt else e["rows"][0]
             for b0 in range(0, kf, ib):
                 bs = min(ib, kf - b0)
@@ -572,7 +584,8 @@ class _Factor:
             store[((e["rows"][1] if tt else e["rows"][0]), k)] = keep[j * kf * kf:(j + 1) * kf * kf]
         g = {"tt": tt, "n": len(ents), "ld": ld, "kf": kf, "zero": tt and bool(gi), "Vb": Vb, "Tb": Tb, "tb0": tbase,
              "plen": len(ents) * ld * nb, "gather": _tb(gi), "back": _tb(bi), "part": PART_UPPER if tt else PART_FULL,
-             "multi": ops.QrPanelMulti(panels, A.dtype, A.device), "Td": Td, "tstore": tst.finalize(), "keep": keep}
+             "multi": ops.QrPanelMulti(panels, A.dtype, A.device), "Td": Td, "tstore": tst.finalize(), "keep": keep,
+             "Yb": Yb, "ygemm": ygemm.finalize() if ygemm is not None else None}
         if self.bla:
             g["next"] = _LeftMulti(A, [(r, v, j * kf * nb, t) for j, (r, v, _, t) in enumerate(parts)], kf,
                                    [n for n in cols if n == k + 1])
@@ -594,6 +607,8 @@ class _Factor:
             ops.geadd(g["part"], N_, 1.0, self.Pb, g["ld"], 0.0, A.data, A.ld, g["back"], copy=True)
         Td = g["Td"]
         ops.geadd(PART_FULL, N_, 1.0, Tb, nb, 0.0, Td.data, Td.ld, g["tstore"], copy=True)
+        if g["ygemm"] is not None:
+            ops.gemm(N_, T_, 1.0, g["Vb"], g["ld"], Tb, nb, 0.0, g["Yb"], g["ld"], g["ygemm"])
         n, kf, t0 = g["n"], g["kf"], g["tb0"]
         if kf == nb:
             g["keep"].view(n, kf * kf).copy_(Tb[t0: t0 + n * nb * nb].view(n, nb * nb))
@@ -611,7 +626,7 @@ class _Factor:
             return
         for g in self.bsteps[k]:
             self._panel_group(g)
-            g["upd"].run(self.A, g["Vb"], g["ld"], g["Tb"], self.A.nb, self.Wb, self.W2b, qt=True)
+            g["upd"].run(self.A, g["Vb"], g["ld"], g["Tb"], self.A.nb, self.Wb, self.W2b, qt=True, Yv=g["Yb"])
 
     # ---- batched look-ahead: panels of every group (TS launch, then each TT round) on the panel stream
     def panels_b(self, k):
@@ -620,11 +635,11 @@ class _Factor:
 
     def nexts_b(self, k):
         for g in self.bsteps[k]:
-            g["next"].run(self.A, g["Vb"], g["ld"], g["Tb"], self.A.nb, self.Wn, self.W2n, qt=True)
+            g["next"].run(self.A, g["Vb"], g["ld"], g["Tb"], self.A.nb, self.Wn, self.W2n, qt=True, Yv=g["Yb"])
 
     def rests_b(self, k):
         for g in self.bsteps[k]:
-            g["rest"].run(self.A, g["Vb"], g["ld"], g["Tb"], self.A.nb, self.Wb, self.W2b, qt=True)
+            g["rest"].run(self.A, g["Vb"], g["ld"], g["Tb"], self.A.nb, self.Wb, self.W2b, qt=True, Yv=g["Yb"])
 
     def _entry(self, k, rows, tt):
         A = self.A
