@@ -374,7 +374,8 @@ __global__ __launch_bounds__(PLR) void k_lu_block_persist(T* __restrict__ A, int
   for (int cj = 0; cj < BW; ++cj) {
     const int j = c0 + cj;
     const int par = cj & 1;
-    // ---- 1. apply column cj-1 (pivot row in prow)
+    // ---- 1. apply column cj-1 (pivot row in prow); each thread touches only its own row, so the local
+    //         pivot search below needs no barrier after it
     if (cj > 0 && own && g >= j) {
       const T d = prow[cj - 1];
       T l = tile[(cj - 1) * R + r];
@@ -382,23 +383,24 @@ __global__ __launch_bounds__(PLR) void k_lu_block_persist(T* __restrict__ A, int
       tile[(cj - 1) * R + r] = l;
       for (int c = cj; c < BW; ++c) tile[c * R + r] = sub(tile[c * R + r], mul(l, prow[c]));
     }
-    __syncthreads();
-    // ---- 2. local |max| of column cj over rows >= j; publish it with its row, and row j
+    // ---- 2. local |max| of column cj over rows >= j; publish it with its row, and row j.  The four waves'
+    //         winners meet in LDS and every thread reduces them itself (one barrier, no second round).
     double v = (own && g >= j) ? piv_mag((double)abs1(tile[cj * R + r])) : -1.0;
     int vi = (own && g >= j) ? g : 0x7fffffff;
     wave_argmax(v, vi);
-    if ((tid & 63) == 0) { sv[tid >> 6] = v; si[tid >> 6] = vi; }
+    if ((tid & 63) == 0) { sv[(tid >> 6) + 4 * par] = v; si[(tid >> 6) + 4 * par] = vi; }
     __syncthreads();
-    if (tid < 64) {
-      v = tid < PLR / 64 ? sv[tid] : -1.0;
-      vi = tid < PLR / 64 ? si[tid] : 0x7fffffff;
-      wave_argmax(v, vi);
-      if (tid == 0) { sv[0] = v; si[0] = vi; }
+    v = sv[4 * par];
+    vi = si[4 * par];
+#pragma unroll
+    for (int q = 1; q < PLR / 64; ++q) {
+      const double v2 = sv[q + 4 * par];
+      const int i2 = si[q + 4 * par];
+      if (v2 > v || (v2 == v && i2 < vi)) { v = v2; vi = i2; }
     }
-    __syncthreads();
-    const int lw = si[0];
+    const int lw = vi;
     if (tid == 0) {
-      st_sc1(&pval[par * G + w], sv[0]);
+      st_sc1(&pval[par * G + w], v);
       st_sc1(&pidx[par * G + w], lw);
     }
     if (lw != 0x7fffffff && tid < BW) st_sc1(&cand[((long long)par * G + w) * PBW + tid], tile[tid * R + (lw - rbase)]);
@@ -414,19 +416,21 @@ __global__ __launch_bounds__(PLR) void k_lu_block_persist(T* __restrict__ A, int
         const int pi_ = ld_sc1(&pidx[par * G + b]);
         if (pv_ > best || (pv_ == best && pi_ < bi)) { best = pv_; bi = pi_; bw = b; }
       }
-      // the winning workgroup travels with the row index (row -> owner is rbase arithmetic)
+      // the winning workgroup travels with the row index (row -> owner is rbase arithmetic); the waves'
+      // winners in LDS slots 8..11 (slots 0..7 hold the local search of this and the previous column)
       wave_argmax(best, bi);
-      if ((tid & 63) == 0) { sv[tid >> 6] = best; si[tid >> 6] = bi; }
+      if ((tid & 63) == 0) { sv[8 + (tid >> 6)] = best; si[8 + (tid >> 6)] = bi; }
       __syncthreads();
-      if (tid < 64) {
-        best = tid < PLR / 64 ? sv[tid] : -1.0;
-        bi = tid < PLR / 64 ? si[tid] : 0x7fffffff;
-        wave_argmax(best, bi);
-        if (tid == 0) { sv[0] = best; si[0] = bi; }
+      best = sv[8];
+      bi = si[8];
+#pragma unroll
+      for (int q = 1; q < PLR / 64; ++q) {
+        const double v2 = sv[8 + q];
+        const int i2 = si[8 + q];
+        if (v2 > best || (v2 == best && i2 < bi)) { best = v2; bi = i2; }
       }
-      __syncthreads();
       (void)bw;
-      const int p = si[0], pw = (p - c0) / R;
+      const int p = bi, pw = (p - c0) / R;
       if (tid < BW) {
         prow[tid] = ld_sc1(&cand[((long long)par * G + pw) * PBW + tid]);
         oldj[tid] = ld_sc1(&cand[((long long)2 * G + par) * PBW + tid]);
@@ -439,7 +443,7 @@ __global__ __launch_bounds__(PLR) void k_lu_block_persist(T* __restrict__ A, int
       }
       if (w == 0 && tid == 0) {
         ipiv[j] = p;
-        if (sv[0] == 0.0 && info) atomicCAS(info, 0, info_base + j + 1);
+        if (best == 0.0 && info) atomicCAS(info, 0, info_base + j + 1);
       }
       __syncthreads();
     }
