@@ -49,19 +49,22 @@ __device__ inline void wave_argmax_d(double& v, int& i) {
   }
 }
 
-// (|v|, key) argmax over the 256 threads of a workgroup; result in sv[0] / si[0]
-__device__ inline void block_argmax(double v, int i, double* sv, int* si) {
+// (|v|, key) argmax over the 256 threads of a workgroup, returned to every thread: the four waves' winners
+// meet in sv[0..3] / si[0..3] behind ONE barrier and every thread reduces them itself.  The caller must pass
+// a barrier before the next call reuses the slots (every call site below is separated by one).
+__device__ inline void block_argmax(double& v, int& i, double* sv, int* si) {
   const int tid = threadIdx.x;
   wave_argmax_d(v, i);
   if ((tid & 63) == 0) { sv[tid >> 6] = v; si[tid >> 6] = i; }
   __syncthreads();
-  if (tid < 64) {
-    v = tid < DLR / 64 ? sv[tid] : -1.0;
-    i = tid < DLR / 64 ? si[tid] : 0x7fffffff;
-    wave_argmax_d(v, i);
-    if (tid == 0) { sv[0] = v; si[0] = i; }
+  v = sv[0];
+  i = si[0];
+#pragma unroll
+  for (int q = 1; q < DLR / 64; ++q) {
+    const double v2 = sv[q];
+    const int i2 = si[q];
+    if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
   }
-  __syncthreads();
 }
 
 template <typename T>
@@ -101,13 +104,16 @@ __global__ __launch_bounds__(DLR) void k_lu_block_dist(T* __restrict__ A, int ld
       tile[(cj - 1) * R + r] = l;
       for (int c = cj; c < BW; ++c) tile[c * R + r] = sub(tile[c * R + r], mul(l, prow[c]));
     }
-    __syncthreads();
-    // ---- 2. local candidate: T rows only on the diagonal owner (the replicas must not nominate)
+    // ---- 2. local candidate: T rows only on the diagonal owner (the replicas must not nominate); the search
+    //         reads only the thread's own row, and block_argmax's barrier orders the update before the row
+    //         reads of the publication below
     const bool elig = own && g >= j && (g >= tr || diag);
-    block_argmax(elig ? piv_mag((double)abs1(tile[cj * R + r])) : -1.0, elig ? g : 0x7fffffff, sv, si);
+    double cv = elig ? piv_mag((double)abs1(tile[cj * R + r])) : -1.0;
+    int ci = elig ? g : 0x7fffffff;
+    block_argmax(cv, ci, sv, si);
     if (tid == 0) {
-      st_sc1(&pval[par * G + w], sv[0]);
-      st_sc1(&pidx[par * G + w], si[0]);
+      st_sc1(&pval[par * G + w], cv);
+      st_sc1(&pidx[par * G + w], ci);
     }
     // the owner of row j publishes the FULL old row j (block part from LDS, the rest from memory)
     if (j >= rbase && j < rbase + nr) {
@@ -117,19 +123,15 @@ __global__ __launch_bounds__(DLR) void k_lu_block_dist(T* __restrict__ A, int ld
       }
     }
     grid_sync_counter(cnt, (cj + 1) * G, info);
-    // ---- 3. local winner (same answer in every WG): local row index, key = local row
-    {
-      double best = -1.0;
-      int bi = 0x7fffffff;
-      for (int b = tid; b < G; b += DLR) {
-        const double v = ld_sc1(&pval[par * G + b]);
-        const int i = ld_sc1(&pidx[par * G + b]);
-        if (v > best || (v == best && i < bi)) { best = v; bi = i; }
-      }
-      block_argmax(best, bi, sv, si);
+    // ---- 3. local winner (same answer in every WG and every thread): local row index, key = local row
+    double lval = -1.0;
+    int lw = 0x7fffffff;                        // local row of the local winner (or 0x7fffffff)
+    for (int b = tid; b < G; b += DLR) {
+      const double v = ld_sc1(&pval[par * G + b]);
+      const int i = ld_sc1(&pidx[par * G + b]);
+      if (v > lval || (v == lval && i < lw)) { lval = v; lw = i; }
     }
-    const double lval = sv[0];
-    const int lw = si[0];                       // local row of the local winner (or 0x7fffffff)
+    block_argmax(lval, lw, sv, si);
     const bool have = lw != 0x7fffffff;
     const int sender = have ? (lw - c0) / R : 0;
     // ---- 4. the sender publishes {|v|, position, row} into slot [par][me] of every rank
