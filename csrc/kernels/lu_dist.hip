@@ -81,6 +81,7 @@ __global__ __launch_bounds__(DLR) void k_lu_block_dist(T* __restrict__ A, int ld
   __shared__ int si[DLR];
   __shared__ int s_win[4];
   const int G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
+  __builtin_amdgcn_s_setprio(3);   // critical-path panel: VALU issue priority over co-resident update waves
   const int BW = cend - c0;
   const int rbase = c0 + w * R;
   const int nr = max(0, min(R, m - rbase));

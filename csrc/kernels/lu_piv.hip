@@ -360,6 +360,9 @@ __global__ __launch_bounds__(PLR) void k_lu_block_persist(T* __restrict__ A, int
   __shared__ double sv[PLR];
   __shared__ int si[PLR];
   const int G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
+  // the panel is the critical path: its waves win VALU issue over a co-resident trailing-update GEMM wave
+  // (a 32-column block leaves room on a CU for one GEMM workgroup beside it; MI355X_MICROARCH.md, wave priority)
+  __builtin_amdgcn_s_setprio(3);
   const int BW = cend - c0;
   const int rbase = c0 + w * R;
   const int nr = max(0, min(R, m - rbase));   // rows owned

@@ -87,6 +87,7 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
   __shared__ T fin[2 * QP_B];
   __shared__ T ff[QP_B], taus[QP_B];
   const int G = G_, w = w_, tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
+  __builtin_amdgcn_s_setprio(3);   // critical-path panel: VALU issue priority over co-resident update waves
   const int rbase = w * R;
   const int nr = max(0, min(R, M - rbase));
   const int R16 = (nr + 15) & ~15;
