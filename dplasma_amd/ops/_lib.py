@@ -124,7 +124,9 @@ _OPTIONAL = set()
 
 
 def lib_path() -> Path:
-    return _LIBDIR / "libdplasma_kernels.so"
+    # DPLASMA_KERNELS_LIB: an alternative build of the kernel library (A/B measurements of kernel variants)
+    alt = os.environ.get("DPLASMA_KERNELS_LIB")
+    return Path(alt) if alt else _LIBDIR / "libdplasma_kernels.so"
 
 
 def load(build_if_missing: bool = True):
