@@ -168,7 +168,8 @@ class _GetrfDev:
       "percol" -- the distributed pivoting driven from the host (one all-gather and two host
                syncs per column; kept as the transport-independent reference of "dist")."""
 
-    def __init__(self, ctx, A, info, pivot: bool = True, trailing_only: bool = False, lookahead=None):
+    def __init__(self, ctx, A, info, pivot: bool = True, trailing_only: bool = False, lookahead=None,
+                 panel_bw=None):
         self.ctx, self.A, self.info = ctx, A, info
         self.pivot = pivot   # False: getrf_nopiv (same task structure, no interchanges)
         # trailing_only: step k's interchanges touch tile columns >= k only (the hybrid LU-QR keeps every
@@ -185,6 +186,7 @@ class _GetrfDev:
         # (lookahead=True: a caller that issues PANEL(k+1) beside REST(k) itself -- the hybrid LU-QR -- needs the
         # parity-alternating panel buffers whatever the environment says)
         self.lookahead = (os.environ.get("DPLASMA_LU_LOOKAHEAD", "0") == "1") if lookahead is None else bool(lookahead)
+        self.panel_bw = panel_bw   # base block width of the recursive panel (None: ops.LU_BW)
         self.pbufs = [torch.zeros(max(1, A.m * nb), dtype=A.dtype, device=dev)
                       for _ in range(2 if self.lookahead else 1)]
         self.piv_dev = torch.zeros(nb, dtype=torch.int32, device=dev)
@@ -332,7 +334,7 @@ class _GetrfDev:
                 st["gunpack"] = unpack.finalize()
                 st["gsent"] = sent
             if self.pivot:
-                st["plu"] = ops.PanelLU(st["pv"], mp, mp, kb, pivot=True)
+                st["plu"] = ops.PanelLU(st["pv"], mp, mp, kb, pivot=True, bw=self.panel_bw)
             else:
                 # no pivoting: only the diagonal block needs the recursive LU; the rows below are
                 # L21 = A21 U11^-1, one TRSM launch (no grid barrier over the tall panel)

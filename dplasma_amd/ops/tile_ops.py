@@ -1060,8 +1060,11 @@ class PanelLU:
     (the dgetrf2 recursion; reference CORE_zgetrf_rectil's role).  The TRSM / GEMM batches of
     every recursion node are built once here and re-used by every run."""
 
-    def __init__(self, buf: torch.Tensor, ld: int, m: int, n: int, pivot: bool = True):
+    def __init__(self, buf: torch.Tensor, ld: int, m: int, n: int, pivot: bool = True, bw: int = None):
         self.buf, self.ld, self.m, self.n, self.pivot = buf, ld, m, n, pivot
+        # base block width: <= 32 columns select the 64 KiB LDS block kernel, which leaves room on a CU for a
+        # trailing-update GEMM workgroup beside it (callers that overlap the panel with updates)
+        self.bw = int(bw) if bw else LU_BW
         self.plan = []
         kf = min(m, n)
         self._rec(0, kf)
@@ -1071,7 +1074,7 @@ class PanelLU:
 
     def _rec(self, c0: int, n: int):
         ld, m = self.ld, self.m
-        if n <= LU_BW:
+        if n <= self.bw:
             self.plan.append(("block", c0, c0 + n))
             return
         n1 = (n // 2 + 15) // 16 * 16
