@@ -638,8 +638,12 @@ class _Factor:
             g["next"].run(self.A, g["Vb"], g["ld"], g["Tb"], self.A.nb, self.Wn, self.W2n, qt=True, Yv=g["Yb"])
 
     def rests_b(self, k):
-        for g in self.bsteps[k]:
-            g["rest"].run(self.A, g["Vb"], g["ld"], g["Tb"], self.A.nb, self.Wb, self.W2b, qt=True, Yv=g["Yb"])
+        # DPLASMA_QR_REST_CAP=n: the bulk update as grid-stride GEMM launches of at most n workgroups, leaving
+        # CUs to the next step's panel launches beside it (measurement knob; 0 = uncapped)
+        cap = int(os.environ.get("DPLASMA_QR_REST_CAP", "0"))
+        with (ops.gemm_wg_cap(cap) if cap > 0 else contextlib.nullcontext()):
+            for g in self.bsteps[k]:
+                g["rest"].run(self.A, g["Vb"], g["ld"], g["Tb"], self.A.nb, self.Wb, self.W2b, qt=True, Yv=g["Yb"])
 
     def _entry(self, k, rows, tt):
         A = self.A
