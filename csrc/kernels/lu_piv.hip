@@ -272,7 +272,8 @@ __global__ __launch_bounds__(256) void k_rows_move(T* __restrict__ A, int ld, in
   if (tin) {
     R = r0 + rows[t];
     rt = R / mb;
-    ro = (rt < nrt) ? rowoff[rt] : -1;
+    // a row outside the view (a corrupt or stale pivot) is skipped, never dereferenced
+    ro = (R >= 0 && rt < nrt) ? rowoff[rt] : -1;
   }
   const long long rbase = ro + (R % mb);
   const int W = nct * nb;
@@ -305,7 +306,7 @@ __global__ __launch_bounds__(256) void k_rows_permute(T* __restrict__ A, int ld,
   for (int t = threadIdx.x; t < n; t += 256) {
     const int Rs = r0 + src[t], Rd = r0 + dst[t];
     const int ts = Rs / mb, td = Rd / mb;
-    const long long bs = ts < nrt ? rowoff[ts] : -1, bd = td < nrt ? rowoff[td] : -1;
+    const long long bs = (Rs >= 0 && ts < nrt) ? rowoff[ts] : -1, bd = (Rd >= 0 && td < nrt) ? rowoff[td] : -1;
     const bool ok = bs >= 0 && bd >= 0;
     so[t] = ok ? bs + Rs % mb : -1;
     dof[t] = ok ? bd + Rd % mb : -1;
