@@ -75,6 +75,7 @@ struct DtrArgs {
   double* Wp;               // nt x MAXB x MAXB x BLK  (published W blocks, T-layout)
   int* prog;                // nt x 2 x MAXB x PSTRIDE: tile-step flags, then W-column flags
   int epoch;
+  int flags;                // bit 0: steal a ready head of another XCD's list when the own head is not ready
   int* info;
   long long* trace;         // optional (DPLASMA_DTR_TRACE): per task {start, end, wg << 8 | xcd}, 100 MHz ticks
 };
@@ -126,7 +127,18 @@ __device__ inline int try_list(const DtrArgs& g, int* cur, const int* list, int 
 // exhausted (-1 none ready yet, -2 every low list exhausted)
 __device__ inline int claim_low(const DtrArgs& g, int xcd) {
   const int own = try_list(g, g.cur + PSTRIDE * (1 + xcd), g.lo + g.lo_off[xcd], g.lo_off[xcd + 1] - g.lo_off[xcd]);
-  if (own != -2) return own;
+  if (own >= 0) return own;
+  if (own == -1) {
+    if (!(g.flags & 1)) return -1;
+    // flags bit 0: the own head waits on a dependency -- take a READY head of another XCD's list instead
+    // (any claimed task is ready, so the deadlock-freedom argument is unchanged; L2 locality is traded away)
+    for (int d = 1; d < 8; ++d) {
+      const int x = (xcd + d) & 7;
+      const int t = try_list(g, g.cur + PSTRIDE * (1 + x), g.lo + g.lo_off[x], g.lo_off[x + 1] - g.lo_off[x]);
+      if (t >= 0) return t;
+    }
+    return -1;
+  }
   bool all_done = true;
   for (int d = 1; d < 8; ++d) {
     const int x = (xcd + d) & 7;
@@ -460,7 +472,7 @@ DPL_API int dpl_dtr_args_layout(long long* off, int n) {
       (long long)offsetof(DtrArgs, Lp),     (long long)offsetof(DtrArgs, Wp),     (long long)offsetof(DtrArgs, prog),
       (long long)offsetof(DtrArgs, epoch),  (long long)offsetof(DtrArgs, info),   (long long)offsetof(DtrArgs, trace),
       (long long)sizeof(DtrArgs),
-      (long long)MAXB, (long long)BLK, (long long)RB, (long long)PSTRIDE};
+      (long long)MAXB, (long long)BLK, (long long)RB, (long long)PSTRIDE, (long long)offsetof(DtrArgs, flags)};
   const int m = (int)(sizeof(v) / sizeof(v[0]));
   for (int q = 0; q < n && q < m; ++q) off[q] = v[q];
   return m;

@@ -253,7 +253,7 @@ class _DtrArgs(ctypes.Structure):
                 ("hi", ctypes.c_void_p), ("nhi", ctypes.c_int), ("lo", ctypes.c_void_p),
                 ("lo_off", ctypes.c_int * 9), ("W", ctypes.c_void_p), ("Mw", ctypes.c_void_p),
                 ("Sw", ctypes.c_void_p), ("Lp", ctypes.c_void_p), ("Wp", ctypes.c_void_p),
-                ("prog", ctypes.c_void_p), ("epoch", ctypes.c_int), ("info", ctypes.c_void_p),
+                ("prog", ctypes.c_void_p), ("epoch", ctypes.c_int), ("flags", ctypes.c_int), ("info", ctypes.c_void_p),
                 ("trace", ctypes.c_void_p)]
 
 
@@ -273,6 +273,8 @@ def _check_layout(lib):
     if ctypes.sizeof(_DtrArgs) != off[len(names)]:
         raise RuntimeError("dtr: DtrArgs size mismatch")
     PST = int(off[len(names) + 4])
+    if n <= len(names) + 5 or off[len(names) + 5] != _DtrArgs.flags.offset:
+        raise RuntimeError("dtr: DtrArgs.flags offset mismatch")
     return PST
 
 
@@ -324,6 +326,9 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     args.W, args.Mw, args.Sw, args.Lp, args.Wp, args.prog = (W.data_ptr(), Mw.data_ptr(), Sw.data_ptr(),
                                                              Lp.data_ptr(), Wp.data_ptr(), prog.data_ptr())
     args.info = info.data_ptr()
+    # DPLASMA_DTR_STEAL=1: a workgroup whose own XCD list head waits on a dependency takes a ready head of
+    # another XCD's list (measurement knob; default: steal only from exhausted lists)
+    args.flags = 1 if os.environ.get("DPLASMA_DTR_STEAL", "0") == "1" else 0
     # DPLASMA_DTR_TRACE=1: per-task {start, end, workgroup << 8 | xcd} (s_memrealtime, 100 MHz) in tp.dtr_trace
     trace = None
     if os.environ.get("DPLASMA_DTR_TRACE", "0") == "1":
