@@ -16,7 +16,7 @@ from dplasma_amd.models import potrf_dtr as D
 T_UPD, T_TRSM, T_POTRF = D.T_UPD, D.T_TRSM, D.T_POTRF
 
 
-def _emulate(plan, A=None, nb=None, P=8, seed=0):
+def _emulate(plan, A=None, nb=None, P=8, seed=0, steal=False):
     """Run the plan's claim protocol with P workers and random completion order; optional numpy math on A
     (lower, nt x nt tiles of nb, sub-tiles of nb / 4).  Returns the claim order."""
     rng = np.random.default_rng(seed)
@@ -85,8 +85,11 @@ def _emulate(plan, A=None, nb=None, P=8, seed=0):
     stall = 0
 
     def try_low(wk):
+        # steal=True (the kernel's DtrArgs.flags bit 0): another XCD's ready head also when the own head
+        # waits on a dependency, not only once the own list is exhausted
         x = wk % 8
-        order = [x] + ([(x + d) % 8 for d in range(1, 8)] if cur[1 + x] >= len(lists[1 + x]) else [])
+        own_done = cur[1 + x] >= len(lists[1 + x])
+        order = [x] + ([(x + d) % 8 for d in range(1, 8)] if (own_done or steal) else [])
         for xx in order:
             li = 1 + xx
             lst = lists[li]
@@ -150,6 +153,7 @@ def test_dtr_plan_lists_and_progress(nt, defer, lo_order):
     assert n_potrf == 16 * nt
     for seed in range(3):
         _emulate(plan, P=(8, 13, 40)[seed], seed=seed)   # >= 1 worker per XCD, as the kernel's grid has
+        _emulate(plan, P=(8, 13, 40)[seed], seed=seed, steal=True)
 
 
 @pytest.mark.parametrize("lo_order", ["column", "panel"])
@@ -162,7 +166,7 @@ def test_dtr_plan_numerics(nt, defer, min_tiles, lo_order):
     S = M @ M.T + n * np.eye(n)
     A = S.copy()
     plan = D._Plan(nt, defer, lo_order, min_tiles)
-    _emulate(plan, A=A, nb=nb, P=8, seed=3)
+    _emulate(plan, A=A, nb=nb, P=8, seed=3, steal=(lo_order == "panel"))
     L = np.tril(A)
     assert np.abs(L - np.linalg.cholesky(S)).max() < 1e-10
 
