@@ -410,6 +410,23 @@ def test_hqr_one_row_tree(ctx, prec, treeargs):
     assert e1 < 1e-13 and e2 < 1e-13
 
 
+@pytest.mark.parametrize("knobs", [{"DPLASMA_QR_MERGE_TT": "0"}, {"DPLASMA_QR_VT": "0"},
+                                   {"DPLASMA_QR_LOOKAHEAD": "0"}, {"DPLASMA_QR_BATCHED": "0"}])
+def test_hqr_engine_knobs(ctx, monkeypatch, knobs):
+    """The stacked-domain engine's alternatives (pairwise TT kills, T applied to W, no look-ahead, entry by
+    entry) factor the same matrix as the default path (same R up to row signs, orthogonal Q)."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    for ta in ONE_ROW_TREES[:2]:
+        e1, e2, A, *_ = _hqr_run(ctx, torch.float64, False, ta, 70, 40, 8, 4)
+        assert e1 < 1e-13 and e2 < 1e-13
+        monkeypatch.delenv(next(iter(knobs)))
+        _, _, B, *_ = _hqr_run(ctx, torch.float64, False, ta, 70, 40, 8, 4)
+        monkeypatch.setenv(*next(iter(knobs.items())))
+        ra, rb = torch.triu(_dense(A)[:40]).abs(), torch.triu(_dense(B)[:40]).abs()
+        assert rel_err(ra, rb) < 1e-12
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("prec", list("ds"))
 @pytest.mark.parametrize("treeargs", ONE_ROW_TREES)
