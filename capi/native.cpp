@@ -335,6 +335,17 @@ NatProgram* nat_posv(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t*
   return P;
 }
 
+// A := alpha x y^T + A (geru) or alpha x y^H + A (gerc): X is M x 1, Y is N x 1 -- a K = 1 GEMM on the same
+// engine (reference: dplasma_zgeru / zgerc, src/zger.jdf); one process or a grid
+NatProgram* nat_ger(dplasma_context_t* ctx, int prec, int conj, const void* alpha, dplasma_desc_t* dX,
+                    dplasma_desc_t* dY, dplasma_desc_t* dA) {
+  double one[2] = {1.0, 0.0};
+  float onef[2] = {1.0f, 0.0f};
+  const void* beta = (prec == P_D || prec == P_Z) ? (const void*)one : (const void*)onef;
+  const bool cplx = prec == P_C || prec == P_Z;
+  return nat_gemm(ctx, prec, NOTRANS, (conj && cplx) ? CONJTRANS : TRANS, alpha, dX, dY, beta, dA);
+}
+
 NatProgram* nat_gemm(dplasma_context_t* ctx, int prec, int tA, int tB, const void* alpha, dplasma_desc_t* dA,
                      dplasma_desc_t* dB, const void* beta, dplasma_desc_t* dC) {
   NatCtx* c = ctx->nat;

@@ -991,6 +991,52 @@ static void test_aliases(dplasma_context_t *ctx) {
   dplasma_desc_destroy(IP);
 }
 
+/* dgeru / zgerc natively (a K = 1 GEMM): A := alpha x y^T + A, A := alpha x y^H + A, ragged 300 x 200, nb 128 */
+static void test_ger(dplasma_context_t *ctx) {
+  const int M = 300, N = 200, nb = 128;
+  dplasma_desc_t *X = dmat(ctx, dplasmaRealDouble, nb, M, 1), *Y = dmat(ctx, dplasmaRealDouble, nb, N, 1);
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, M, N);
+  dplasma_dplrnt(ctx, 0, X, 11);
+  dplasma_dplrnt(ctx, 0, Y, 12);
+  dplasma_dplrnt(ctx, 0, A, 13);
+  double *x = malloc(sizeof(double) * M), *y = malloc(sizeof(double) * N);
+  double *a = malloc(sizeof(double) * M * N), *r = malloc(sizeof(double) * M * N);
+  dplasma_desc_get_lapack(X, x, M);
+  dplasma_desc_get_lapack(Y, y, N);
+  dplasma_desc_get_lapack(A, a, M);
+  CHECK(dplasma_dgeru(ctx, 0.75, X, Y, A) == 0, "dgeru: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(A, r, M);
+  double err = 0;
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i < M; ++i) err = fmax(err, fabs(a[i + (size_t)j * M] + 0.75 * x[i] * y[j] - r[i + (size_t)j * M]));
+  printf("dgeru %dx%d max error %.3e\n", M, N, err);
+  CHECK(err < 1e-13, "dgeru error %.3e", err);
+  free(x), free(y), free(a), free(r);
+  dplasma_desc_destroy(X), dplasma_desc_destroy(Y), dplasma_desc_destroy(A);
+  /* zgerc: the conjugate of y */
+  dplasma_desc_t *Xz = dmat(ctx, dplasmaComplexDouble, nb, M, 1), *Yz = dmat(ctx, dplasmaComplexDouble, nb, N, 1);
+  dplasma_desc_t *Az = dmat(ctx, dplasmaComplexDouble, nb, M, N);
+  dplasma_zplrnt(ctx, 0, Xz, 21);
+  dplasma_zplrnt(ctx, 0, Yz, 22);
+  dplasma_zplrnt(ctx, 0, Az, 23);
+  double complex *xz = malloc(sizeof(double complex) * M), *yz = malloc(sizeof(double complex) * N);
+  double complex *az = malloc(sizeof(double complex) * M * N), *rz = malloc(sizeof(double complex) * M * N);
+  dplasma_desc_get_lapack(Xz, xz, M);
+  dplasma_desc_get_lapack(Yz, yz, N);
+  dplasma_desc_get_lapack(Az, az, M);
+  const double complex alpha = 0.5 - 0.25 * _Complex_I;
+  CHECK(dplasma_zgerc(ctx, alpha, Xz, Yz, Az) == 0, "zgerc: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(Az, rz, M);
+  err = 0;
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i < M; ++i)
+      err = fmax(err, cabs(az[i + (size_t)j * M] + alpha * xz[i] * conj(yz[j]) - rz[i + (size_t)j * M]));
+  printf("zgerc %dx%d max error %.3e\n", M, N, err);
+  CHECK(err < 1e-13, "zgerc error %.3e", err);
+  free(xz), free(yz), free(az), free(rz);
+  dplasma_desc_destroy(Xz), dplasma_desc_destroy(Yz), dplasma_desc_destroy(Az);
+}
+
 int main(int argc, char **argv) {
   setvbuf(stdout, NULL, _IONBF, 0);
   signal(SIGSEGV, on_fault);
@@ -1027,6 +1073,7 @@ int main(int argc, char **argv) {
   test_inverse_family(ctx);
   test_rank_2k(ctx);
   test_aliases(ctx);
+  test_ger(ctx);
   /* an operation without a native implementation fails cleanly */
   dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
   CHECK(dplasma_dtrmdm(ctx, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");

@@ -175,6 +175,13 @@ EXT = [
 ]
 
 
+# EXT entry points the interpreter-free engine also runs: op -> native call for precision code pc
+NATIVE_EXT = {
+    "geru": lambda pc: f"nat_ger(ctx, {pc}, 0, &alpha, X, Y, A)",
+    "gerc": lambda pc: f"nat_ger(ctx, {pc}, 1, &alpha, X, Y, A)",
+}
+
+
 def ext_ctype(code, p):
     T = CTYPE[p]
     return {"E": "dplasma_enum_t", "D": "dplasma_desc_t *", "S": T, "R": "double", "I": "int",
@@ -245,7 +252,8 @@ def gen_ext(h, cpp):
           "/* LDL^H butterflies: hebut returns an opaque handle (not the reference's raw vector) that hetrs /",
           " * gebut / gebmm take; release it with dplasma_but_free */",
           "void dplasma_but_free(void *U_but_vec);",
-          "/* ---- further entry points (dplasma_z.h:106-349); on a native context they return an error */"]
+          "/* ---- further entry points (dplasma_z.h:106-349); on a native context they return an error, except",
+          " * geru / gerc (run natively) */"]
     for op, ret, args, precs, has_new, *_ in EXT:
         for p in precs:
             cargs = ", ".join(("dplasma_taskpool_t *tp" if c == "K" else
@@ -270,6 +278,17 @@ def gen_ext(h, cpp):
                 continue
             if args[0][0] == "K":
                 cpp.append(f'extern "C" DPL_CAPI {proto} {{ dpl_tp_setter(tp, "x:{p}{op}", {args[1][1]}); }}')
+                continue
+            if op in NATIVE_EXT:   # the interpreter-free engine runs it (capi/native.cpp)
+                nat_call = NATIVE_EXT[op](PCODE[p])
+                cpp.append(f'extern "C" DPL_CAPI {proto} {{ if (dpl_native(ctx)) return nat_execute(ctx, {nat_call}); '
+                           f'DplGil g; return dpl_call_int(ctx, "x:{p}{op}", {{{conv}}}); }}')
+                if has_new:
+                    cpp.append(f'extern "C" DPL_CAPI dplasma_taskpool_t *dplasma_{p}{op}_New(dplasma_context_t *ctx, '
+                               f'{cargs}) {{ if (dpl_native(ctx)) return nat_wrap({nat_call}); '
+                               f'DplGil g; return dpl_call_new(ctx, "x:{p}{op}", {{{conv}}}); }}')
+                    cpp.append(f'extern "C" DPL_CAPI void dplasma_{p}{op}_Destruct(dplasma_taskpool_t *tp) '
+                               '{ dplasma_taskpool_free(tp); }')
                 continue
             if ret == "r":
                 call = f'dpl_call_real(ctx, "x:{p}{op}", {{{conv}}})'
