@@ -1725,13 +1725,12 @@ bool add_getrf_dist(NatProgram& P, NatDesc& A, NatDesc& IP) {
   return true;
 }
 
-// op(A) X = B with A = P L U from add_getrf (reference getrs: laswp + two TRSM, or the transposed order)
-bool add_getrs(NatProgram& P, int trans, NatDesc& A, NatDesc& IP, NatDesc& B, int& last) {
-  const int kt = std::min(A.mt, A.nt);
-  LuScratch S;
-  S.piv = dev_alloc(sizeof(int) * (A.nb + 16), true);
-  S.mdst = dev_alloc(sizeof(int) * 2 * (A.mb + 16), true);
-  S.msrc = dev_alloc(sizeof(int) * 2 * (A.mb + 16), true);
+// Row-interchange scratch for the rows of B (relative pivots, net move lists, B's tile offset tables): the
+// laswp of getrs and of laswp itself
+bool row_swap_scratch(NatProgram& P, NatDesc& B, int blk, LuScratch& S) {
+  S.piv = dev_alloc(sizeof(int) * (blk + 16), true);
+  S.mdst = dev_alloc(sizeof(int) * 2 * (blk + 16), true);
+  S.msrc = dev_alloc(sizeof(int) * 2 * (blk + 16), true);
   S.mcnt = dev_alloc(64, true);
   std::vector<long long> ro(B.mt), co(B.nt);
   std::vector<int> nc(B.nt);
@@ -1740,19 +1739,35 @@ bool add_getrs(NatProgram& P, int trans, NatDesc& A, NatDesc& IP, NatDesc& B, in
     co[n] = B.off(0, n);
     nc[n] = B.cols(n);
   }
-  DevPtr rowoff = dev_upload(ro), coloff = dev_upload(co), ncols = dev_upload(nc);
-  for (const DevPtr& d : {S.piv, S.mdst, S.msrc, S.mcnt, rowoff, coloff, ncols}) {
+  S.rowoff = dev_upload(ro);
+  S.coloff = dev_upload(co);
+  S.ncols = dev_upload(nc);
+  for (const DevPtr& d : {S.piv, S.mdst, S.msrc, S.mcnt, S.rowoff, S.coloff, S.ncols}) {
     if (!d) return false;
     P.keep.push_back(d);
   }
-  const int* ipg = (const int*)IP.data;
+  return true;
+}
+
+// the interchanges ipg[r0 .. r0 + kmin) (global, 1-based, sequential) on the rows of B (inverse: undone)
+int add_swap_block(NatProgram& P, NatDesc& B, const LuScratch& S, const int* ipg, int r0, int kmin, bool inverse,
+                   int prev) {
   int* piv = (int*)S.piv->p;
+  prev = P.task(1, [=](hipStream_t s) { return dpl_ipiv_shift(ipg + r0, piv, kmin, -(r0 + 1), s); }, {prev});
+  return add_row_moves(P, B, S, S.rowoff, S.coloff, S.ncols, r0, kmin, inverse, prev);
+}
+
+// op(A) X = B with A = P L U from add_getrf (reference getrs: laswp + two TRSM, or the transposed order)
+bool add_getrs(NatProgram& P, int trans, NatDesc& A, NatDesc& IP, NatDesc& B, int& last) {
+  const int kt = std::min(A.mt, A.nt);
+  LuScratch S;
+  if (!row_swap_scratch(P, B, std::max(A.mb, A.nb), S)) return false;
+  const int* ipg = (const int*)IP.data;
   const Scalar one(B.prec, 1.0);
   int prev = last;
   auto swaps = [&](int k, bool inverse) {
     const int r0 = k * A.mb, kmin = std::min(A.m - r0, A.cols(k));
-    prev = P.task(1, [=](hipStream_t s) { return dpl_ipiv_shift(ipg + r0, piv, kmin, -(r0 + 1), s); }, {prev});
-    prev = add_row_moves(P, B, S, rowoff, coloff, ncols, r0, kmin, inverse, prev);
+    prev = add_swap_block(P, B, S, ipg, r0, kmin, inverse, prev);
   };
   auto solve = [&](int uplo, int tr, int diag) {
     if (!add_trsm(P, LEFT, uplo, tr, diag, one, A, B, 1, prev)) return false;
@@ -1776,6 +1791,30 @@ bool lu_conform(const NatDesc* A, const NatDesc* IP) {
 }
 
 }  // namespace
+
+// A := P A with the interchanges of IPIV (1-based, sequential; dplasma_zlaswp): inc > 0 in order, inc < 0
+// undone in reverse order -- blocks of A's tile height on the device row-move kernels (one process)
+NatProgram* nat_laswp(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dplasma_desc_t* dIP, int inc) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *IP = dIP ? dIP->nat : nullptr;
+  if (!same_ctx_dist(c, {A}, prec) || !IP || IP->ctx != c)
+    return fail(nullptr, "laswp: descriptors of another context or precision");
+  if (c->dist()) return fail(nullptr, "laswp: one process only on a native context");
+  if (IP->prec != P_I || IP->m != 1 || IP->lld != 1 || A->mb > 512)
+    return fail(nullptr, "laswp: IPIV must be a 1 x n int descriptor, A tiles of at most 512 rows");
+  NatProgram* P = new_program(c, "laswp", false);
+  LuScratch S;
+  if (!row_swap_scratch(*P, *A, A->mb, S)) return fail(P, "laswp: device allocation failed");
+  const int np = std::min(IP->n, A->m), nblk = (np + A->mb - 1) / A->mb;
+  const int* ipg = (const int*)IP->data;
+  int prev = -1;
+  for (int q = 0; q < nblk; ++q) {
+    const int k = inc > 0 ? q : nblk - 1 - q;
+    const int r0 = k * A->mb, kmin = std::min(np - r0, A->mb);
+    prev = add_swap_block(*P, *A, S, ipg, r0, kmin, inc < 0, prev);
+  }
+  return P;
+}
 
 NatProgram* nat_getrf_1d(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dplasma_desc_t* dIP) {
   NatCtx* c = ctx->nat;

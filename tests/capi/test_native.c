@@ -1037,6 +1037,46 @@ static void test_ger(dplasma_context_t *ctx) {
   dplasma_desc_destroy(Xz), dplasma_desc_destroy(Yz), dplasma_desc_destroy(Az);
 }
 
+/* dlaswp natively: the pivots of a getrf applied forward to a 700 x 9 matrix (vs the same swaps on the host),
+ * then undone (inc = -1) back to the original */
+static void test_laswp(dplasma_context_t *ctx) {
+  const int n = 700, nb = 256, nc = 9;
+  dplasma_desc_t *G = dmat(ctx, dplasmaRealDouble, nb, n, n), *B = dmat(ctx, dplasmaRealDouble, nb, n, nc);
+  dplasma_desc_t *IP = dplasma_desc_ipiv(ctx, 1, nb, 1, n, 1, 1);
+  double *g = malloc(sizeof(double) * n * n), *b = malloc(sizeof(double) * n * nc), *r = malloc(sizeof(double) * n * nc);
+  int *ipiv = malloc(sizeof(int) * n);
+  unsigned sd = 77;
+  rnd_fill(g, (size_t)n * n, &sd), rnd_fill(b, (size_t)n * nc, &sd);
+  dplasma_desc_set_lapack(G, g, n);
+  CHECK(dplasma_dgetrf_1d(ctx, G, IP) == 0, "laswp: getrf %s", dplasma_last_error());
+  dplasma_desc_get_lapack(IP, ipiv, 1);
+  dplasma_desc_set_lapack(B, b, n);
+  CHECK(dplasma_dlaswp(ctx, B, IP, 1) == 0, "dlaswp: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(B, r, n);
+  for (int i = 0; i < n; ++i) {   /* host reference: LAPACK dlaswp, k1 = 1 .. n, incx = 1 */
+    const int p = ipiv[i] - 1;
+    if (p != i)
+      for (int c = 0; c < nc; ++c) {
+        const double t = b[i + (size_t)c * n];
+        b[i + (size_t)c * n] = b[p + (size_t)c * n];
+        b[p + (size_t)c * n] = t;
+      }
+  }
+  double err = 0;
+  for (size_t e = 0; e < (size_t)n * nc; ++e) err = fmax(err, fabs(r[e] - b[e]));
+  CHECK(err == 0.0, "dlaswp forward differs (%.3e)", err);
+  CHECK(dplasma_dlaswp(ctx, B, IP, -1) == 0, "dlaswp back: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(B, r, n);
+  unsigned sd2 = 77;
+  rnd_fill(g, (size_t)n * n, &sd2), rnd_fill(b, (size_t)n * nc, &sd2);   /* the original B again */
+  err = 0;
+  for (size_t e = 0; e < (size_t)n * nc; ++e) err = fmax(err, fabs(r[e] - b[e]));
+  printf("dlaswp %d x %d forward exact, undone: max diff %.3e\n", n, nc, err);
+  CHECK(err == 0.0, "dlaswp inc -1 did not undo (%.3e)", err);
+  free(g), free(b), free(r), free(ipiv);
+  dplasma_desc_destroy(G), dplasma_desc_destroy(B), dplasma_desc_destroy(IP);
+}
+
 int main(int argc, char **argv) {
   setvbuf(stdout, NULL, _IONBF, 0);
   signal(SIGSEGV, on_fault);
@@ -1074,6 +1114,7 @@ int main(int argc, char **argv) {
   test_rank_2k(ctx);
   test_aliases(ctx);
   test_ger(ctx);
+  test_laswp(ctx);
   /* an operation without a native implementation fails cleanly */
   dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
   CHECK(dplasma_dtrmdm(ctx, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");

@@ -179,6 +179,7 @@ EXT = [
 NATIVE_EXT = {
     "geru": lambda pc: f"nat_ger(ctx, {pc}, 0, &alpha, X, Y, A)",
     "gerc": lambda pc: f"nat_ger(ctx, {pc}, 1, &alpha, X, Y, A)",
+    "laswp": lambda pc: f"nat_laswp(ctx, {pc}, A, IPIV, inc)",
 }
 
 
@@ -253,7 +254,7 @@ def gen_ext(h, cpp):
           " * gebut / gebmm take; release it with dplasma_but_free */",
           "void dplasma_but_free(void *U_but_vec);",
           "/* ---- further entry points (dplasma_z.h:106-349); on a native context they return an error, except",
-          " * geru / gerc (run natively) */"]
+          " * geru / gerc / laswp (run natively) */"]
     for op, ret, args, precs, has_new, *_ in EXT:
         for p in precs:
             cargs = ", ".join(("dplasma_taskpool_t *tp" if c == "K" else
