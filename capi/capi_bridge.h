@@ -159,6 +159,7 @@ NatProgram* nat_gelqs(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplas
 NatProgram* nat_ger(dplasma_context_t* ctx, int prec, int conj, const void* alpha, dplasma_desc_t* X, dplasma_desc_t* Y,
                     dplasma_desc_t* A);
 NatProgram* nat_laswp(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* IPIV, int inc);
+double nat_lanm2(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, int* info);
 int nat_execute(dplasma_context_t* ctx, NatProgram* P);     // run + wait + info, frees P
 dplasma_taskpool_t* nat_wrap(NatProgram* P);
 void nat_fini(dplasma_context_t* ctx);

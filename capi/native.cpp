@@ -2552,3 +2552,57 @@ int nat_qr_tau(dplasma_desc_t* dT, void* tau, int k) {
   }
   return 0;
 }
+
+// ||A||_2 estimate by power iteration on A^H A (dplasma_zlanm2, src/zlanm2.jdf; the same loop as
+// models/aux.lanm2): x = n^-1/2 (1, .., 1); y = A x; x = A^H y; e = ||x|| / ||y||; x /= ||x||, until e moves by
+// less than 1e-10 relatively (at most 500 products).  *info: the iteration count, negative if not converged.
+double nat_lanm2(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, int* info) {
+  NatCtx* c = ctx->nat;
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!same_ctx_dist(c, {A}, prec)) return (fail(nullptr, "lanm2: descriptor of another context or precision"), NAN);
+  if (c->dist()) return (fail(nullptr, "lanm2: one process only on a native context"), NAN);
+  dplasma_desc_t* X = nat_desc(ctx, prec, A->nb, A->nb, A->n, 1, 1, 1, nullptr, 0, 1);
+  dplasma_desc_t* Y = nat_desc(ctx, prec, A->mb, A->nb, A->m, 1, 1, 1, nullptr, 0, 1);
+  if (!X || !Y) {
+    if (X) nat_desc_free(X);
+    if (Y) nat_desc_free(Y);
+    return (fail(nullptr, "lanm2: device allocation failed"), NAN);
+  }
+  const bool cplx = prec == P_C || prec == P_Z;
+  auto scal = [&](double v, double buf[2], float fbuf[2]) -> const void* {
+    buf[0] = v, buf[1] = 0.0, fbuf[0] = (float)v, fbuf[1] = 0.0f;
+    return (prec == P_D || prec == P_Z) ? (const void*)buf : (const void*)fbuf;
+  };
+  double b1[2], b0[2], bs[2];
+  float f1[2], f0[2], fs[2];
+  const void* one = scal(1.0, b1, f1);
+  const void* zero = scal(0.0, b0, f0);
+  const double x0 = 1.0 / std::sqrt((double)std::max(A->n, 1));
+  double bx[2];
+  float fx[2];
+  const void* xv = scal(x0, bx, fx);
+  int rc = nat_execute(ctx, nat_laset(ctx, prec, UPPERLOWER, xv, xv, X));
+  if (rc == 0) rc = nat_execute(ctx, nat_laset(ctx, prec, UPPERLOWER, zero, zero, Y));
+  double e = 0.0, e0 = -1.0;
+  int it = 0;
+  bool ok = rc == 0;
+  while (ok && it < 500 && std::fabs(e - e0) > 1e-10 * std::max(e, 1e-300)) {
+    e0 = e;
+    ok = nat_execute(ctx, nat_gemm(ctx, prec, NOTRANS, NOTRANS, one, dA, X, zero, Y)) == 0 &&
+         nat_execute(ctx, nat_gemm(ctx, prec, cplx ? CONJTRANS : TRANS, NOTRANS, one, dA, Y, zero, X)) == 0;
+    if (!ok) break;
+    const double nx = nat_lange(ctx, prec, 174 /* Frobenius */, X), ny = nat_lange(ctx, prec, 174, Y);
+    if (!(nx > 0.0) || !(ny > 0.0)) {
+      e = 0.0;
+      break;
+    }
+    e = nx / ny;
+    ok = nat_execute(ctx, nat_lascal(ctx, prec, UPPERLOWER, scal(1.0 / nx, bs, fs), X)) == 0;
+    ++it;
+  }
+  nat_desc_free(X);
+  nat_desc_free(Y);
+  if (!ok) return NAN;
+  if (info) *info = std::fabs(e - e0) <= 1e-10 * std::max(e, 1e-300) ? it : -it;
+  return e;
+}

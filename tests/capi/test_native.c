@@ -1077,6 +1077,34 @@ static void test_laswp(dplasma_context_t *ctx) {
   dplasma_desc_destroy(G), dplasma_desc_destroy(B), dplasma_desc_destroy(IP);
 }
 
+/* dlanm2 natively: ||u v^T||_2 = ||u|| ||v|| (the rank-one matrix built with dgeru on a zero matrix), and a
+ * diagonal matrix diag(3n, 2, .., n) whose 2-norm is 3n (a separated top singular value: fast convergence) */
+static void test_lanm2(dplasma_context_t *ctx) {
+  const int M = 300, N = 200, nb = 128;
+  dplasma_desc_t *X = dmat(ctx, dplasmaRealDouble, nb, M, 1), *Y = dmat(ctx, dplasmaRealDouble, nb, N, 1);
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, M, N);
+  dplasma_dplrnt(ctx, 0, X, 41);
+  dplasma_dplrnt(ctx, 0, Y, 42);
+  dplasma_dlaset(ctx, dplasmaUpperLower, 0.0, 0.0, A);
+  CHECK(dplasma_dgeru(ctx, 1.0, X, Y, A) == 0, "lanm2: dgeru %s", dplasma_last_error());
+  const double nu = dplasma_dlange(ctx, dplasmaFrobeniusNorm, X), nv = dplasma_dlange(ctx, dplasmaFrobeniusNorm, Y);
+  int info = 0;
+  const double e = dplasma_dlanm2(ctx, A, &info);
+  printf("dlanm2 rank-one %dx%d: %.15g vs %.15g (info %d)\n", M, N, e, nu * nv, info);
+  CHECK(fabs(e - nu * nv) <= 1e-12 * nu * nv && info > 0, "dlanm2 rank one: %.15g vs %.15g (info %d, %s)", e,
+        nu * nv, info, dplasma_last_error());
+  const int n = 257;
+  dplasma_desc_t *D = dmat(ctx, dplasmaRealDouble, nb, n, n);
+  double *d = calloc((size_t)n * n, sizeof(double));
+  for (int i = 0; i < n; ++i) d[i + (size_t)i * n] = i == 0 ? 3.0 * n : i + 1;
+  dplasma_desc_set_lapack(D, d, n);
+  const double e2 = dplasma_dlanm2(ctx, D, &info);
+  printf("dlanm2 diag(3n, 2..%d): %.12g (info %d)\n", n, e2, info);
+  CHECK(fabs(e2 - 3.0 * n) <= 1e-8 * n, "dlanm2 diagonal: %.12g vs %d", e2, 3 * n);
+  free(d);
+  dplasma_desc_destroy(X), dplasma_desc_destroy(Y), dplasma_desc_destroy(A), dplasma_desc_destroy(D);
+}
+
 int main(int argc, char **argv) {
   setvbuf(stdout, NULL, _IONBF, 0);
   signal(SIGSEGV, on_fault);
@@ -1115,6 +1143,7 @@ int main(int argc, char **argv) {
   test_aliases(ctx);
   test_ger(ctx);
   test_laswp(ctx);
+  test_lanm2(ctx);
   /* an operation without a native implementation fails cleanly */
   dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
   CHECK(dplasma_dtrmdm(ctx, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");

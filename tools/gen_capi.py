@@ -181,6 +181,10 @@ NATIVE_EXT = {
     "gerc": lambda pc: f"nat_ger(ctx, {pc}, 1, &alpha, X, Y, A)",
     "laswp": lambda pc: f"nat_laswp(ctx, {pc}, A, IPIV, inc)",
 }
+# EXT entry points the engine answers directly (a value, no program)
+NATIVE_EXT_DIRECT = {
+    "lanm2": lambda pc: f"nat_lanm2(ctx, {pc}, A, info)",
+}
 
 
 def ext_ctype(code, p):
@@ -254,7 +258,7 @@ def gen_ext(h, cpp):
           " * gebut / gebmm take; release it with dplasma_but_free */",
           "void dplasma_but_free(void *U_but_vec);",
           "/* ---- further entry points (dplasma_z.h:106-349); on a native context they return an error, except",
-          " * geru / gerc / laswp (run natively) */"]
+          " * geru / gerc / laswp / lanm2 (run natively) */"]
     for op, ret, args, precs, has_new, *_ in EXT:
         for p in precs:
             cargs = ", ".join(("dplasma_taskpool_t *tp" if c == "K" else
@@ -279,6 +283,12 @@ def gen_ext(h, cpp):
                 continue
             if args[0][0] == "K":
                 cpp.append(f'extern "C" DPL_CAPI {proto} {{ dpl_tp_setter(tp, "x:{p}{op}", {args[1][1]}); }}')
+                continue
+            if op in NATIVE_EXT_DIRECT:
+                call = (f'dpl_call_real(ctx, "x:{p}{op}", {{{conv}}})' if ret == "r"
+                        else f'dpl_call_int(ctx, "x:{p}{op}", {{{conv}}})')
+                cpp.append(f'extern "C" DPL_CAPI {proto} {{ if (dpl_native(ctx)) return {NATIVE_EXT_DIRECT[op](PCODE[p])}; '
+                           f'DplGil g; return {call}; }}')
                 continue
             if op in NATIVE_EXT:   # the interpreter-free engine runs it (capi/native.cpp)
                 nat_call = NATIVE_EXT[op](PCODE[p])
