@@ -160,6 +160,11 @@ NatProgram* nat_ger(dplasma_context_t* ctx, int prec, int conj, const void* alph
                     dplasma_desc_t* A);
 NatProgram* nat_laswp(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* IPIV, int inc);
 double nat_lanm2(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, int* info);
+NatProgram* nat_trsmpl_ptgpanel(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* IPIV,
+                                dplasma_desc_t* B);
+NatProgram* nat_trdsm(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* B);
+NatProgram* nat_trmdm(dplasma_context_t* ctx, int prec, dplasma_desc_t* A);
+int nat_print(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* A);
 int nat_execute(dplasma_context_t* ctx, NatProgram* P);     // run + wait + info, frees P
 dplasma_taskpool_t* nat_wrap(NatProgram* P);
 void nat_fini(dplasma_context_t* ctx);

@@ -1816,6 +1816,120 @@ NatProgram* nat_laswp(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dpla
   return P;
 }
 
+// B := L^-1 P B with the getrf_1d factors (dplasma_ztrsmpl_ptgpanel; models/lu.py trsmpl_ptgpanel): the
+// forward interchanges of getrs and its unit-lower TRSM, no upper solve
+NatProgram* nat_trsmpl_ptgpanel(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dplasma_desc_t* dIP,
+                                dplasma_desc_t* dB) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *IP = dIP ? dIP->nat : nullptr, *B = dB ? dB->nat : nullptr;
+  if (!same_ctx(c, {A, B}, prec) || !IP || IP->ctx != c)
+    return fail(nullptr, "trsmpl_ptgpanel: descriptors of another context or precision (one process)");
+  if (!lu_conform(A, IP) || A->m != A->n || B->m != A->n || B->mb != A->mb)
+    return fail(nullptr, "trsmpl_ptgpanel: operands do not conform");
+  NatProgram* P = new_program(c, "trsmpl_ptgpanel", false);
+  LuScratch S;
+  if (!row_swap_scratch(*P, *B, A->mb, S)) return fail(P, "trsmpl_ptgpanel: device allocation failed");
+  const int* ipg = (const int*)IP->data;
+  int prev = -1;
+  for (int k = 0; k < std::min(A->mt, A->nt); ++k) {
+    const int r0 = k * A->mb, kmin = std::min(A->m - r0, A->cols(k));
+    prev = add_swap_block(*P, *B, S, ipg, r0, kmin, false, prev);
+  }
+  if (!add_trsm(*P, LEFT, LOWER, NOTRANS, UNIT, Scalar(prec, 1.0), *A, *B, 1, prev))
+    return fail(P, "trsmpl_ptgpanel: device allocation failed");
+  return P;
+}
+
+// The diagonal scalings of the LDL^H family (models/ldl.py; reference src/ztrdsm.jdf, src/ztrmdm.jdf), one
+// dpl_diag_scale launch each: trdsm B := D^-1 B (row i of tile (k, n) divided by D(i, i) of A's tile (k, k));
+// trmdm: the strictly lower part of A := L D^-1 (column j of tile (m, k), m >= k, divided by D(j, j)).  D
+// itself is never written, so every tile reads it in the same launch.
+static NatProgram* diag_scale(NatCtx* c, int prec, const char* name, NatDesc& A, NatDesc& B, bool trmdm) {
+  std::vector<TileItem> it;
+  int mm = 0, nn = 0;
+  auto add = [&](int k, int m, int n) {
+    it.push_back(TileItem{A.off(k, k), B.off(m, n), B.rows(m), B.cols(n), m * B.mb, n * B.nb});
+    mm = std::max(mm, B.rows(m));
+    nn = std::max(nn, B.cols(n));
+  };
+  if (trmdm) {
+    for (int k = 0; k < std::min(A.mt, A.nt); ++k)
+      for (int m = k; m < A.mt; ++m) add(k, m, k);
+  } else {
+    for (int k = 0; k < B.mt; ++k)
+      for (int n = 0; n < B.nt; ++n) add(k, k, n);
+  }
+  NatProgram* P = new_program(c, name, false);
+  if (it.empty()) return P;
+  DevPtr d = dev_upload(it);
+  if (!d) return fail(P, "diagonal scaling: device allocation failed");
+  P->keep.push_back(d);
+  const int n = (int)it.size(), part = trmdm ? 3 : 0, lda = A.lld, ldb = B.lld;
+  const char* a = A.data;
+  char* b = B.data;
+  P->task(1, [=](hipStream_t s) {
+    return dpl_diag_scale(prec, part, trmdm ? 1 : 0, n, d->p, mm, nn, a, lda, b, ldb, s);
+  }, {});
+  return P;
+}
+
+NatProgram* nat_trdsm(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dplasma_desc_t* dB) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *B = dB ? dB->nat : nullptr;
+  if (!same_ctx(c, {A, B}, prec)) return fail(nullptr, "trdsm: descriptors of another context or precision (one process)");
+  if (A->mb != A->nb || B->mb != A->mb || A->m < B->m || A->n < B->m)
+    return fail(nullptr, "trdsm: operands do not conform");
+  return diag_scale(c, prec, "trdsm", *A, *B, false);
+}
+
+NatProgram* nat_trmdm(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA) {
+  NatCtx* c = ctx->nat;
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!same_ctx(c, {A}, prec)) return fail(nullptr, "trmdm: a descriptor of another context or precision (one process)");
+  if (A->mb != A->nb) return fail(nullptr, "trmdm: square tiles");
+  return diag_scale(c, prec, "trmdm", *A, *A, true);
+}
+
+// dplasma_zprint (src/zprint.jdf; models/aux.py print_matrix): the uplo part of A tile by tile, in the
+// Python layer's format, from a host copy (one process)
+int nat_print(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* dA) {
+  NatCtx* c = ctx->nat;
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!same_ctx(c, {A}, prec)) return nat_unsupported("print: a descriptor of another context (one process)");
+  std::vector<char> h((size_t)std::max(1, A->m) * std::max(1, A->n) * A->es);
+  if (nat_desc_io(dA, h.data(), std::max(1, A->m), false) != 0) return -1;
+  const bool cplx = prec == P_C || prec == P_Z;
+  auto at = [&](long long i, long long j, double& re, double& im) {
+    const size_t e = (size_t)(i + j * A->m);
+    im = 0.0;
+    switch (prec) {
+      case P_S: re = ((const float*)h.data())[e]; break;
+      case P_D: re = ((const double*)h.data())[e]; break;
+      case P_C: re = ((const float*)h.data())[2 * e]; im = ((const float*)h.data())[2 * e + 1]; break;
+      default: re = ((const double*)h.data())[2 * e]; im = ((const double*)h.data())[2 * e + 1]; break;
+    }
+  };
+  for (int n = 0; n < A->nt; ++n)
+    for (int m = 0; m < A->mt; ++m) {
+      if ((uplo == LOWER && m < n) || (uplo == UPPER && m > n)) continue;
+      std::printf("A(%d,%d) [%dx%d]\n", m, n, A->rows(m), A->cols(n));
+      for (int i = 0; i < A->rows(m); ++i) {
+        std::printf(" ");
+        for (int j = 0; j < A->cols(n); ++j) {
+          double re, im;
+          at((long long)m * A->mb + i, (long long)n * A->nb + j, re, im);
+          if (cplx)
+            std::printf(" %.6g%+.6gj", re, im);
+          else
+            std::printf(" % .6e", re);
+        }
+        std::printf("\n");
+      }
+    }
+  std::fflush(stdout);
+  return 0;
+}
+
 NatProgram* nat_getrf_1d(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, dplasma_desc_t* dIP) {
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *IP = dIP ? dIP->nat : nullptr;

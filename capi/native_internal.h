@@ -37,6 +37,8 @@ int dpl_geadd(int prec, int part, int trans, int nitems, const void* items, int 
               const void* A, int lda, const void* beta, void* B, int ldb, int copy, hipStream_t st);
 int dpl_lascal(int prec, int part, int nitems, const void* items, int mmax, int nmax, const void* alpha, void* A,
                int lda, hipStream_t st);
+int dpl_diag_scale(int prec, int part, int cols, int nitems, const void* items, int mmax, int nmax,
+                   const void* D, int ldd, void* B, int ldb, hipStream_t st);
 int dpl_tile_norm(int prec, int kind, int part, int unit, int nitems, const void* items, const void* A, int lda,
                   double* out, int ostride, hipStream_t st);
 long long dpl_lu_block_ws_bytes(int m);

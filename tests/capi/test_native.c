@@ -1105,6 +1105,73 @@ static void test_lanm2(dplasma_context_t *ctx) {
   dplasma_desc_destroy(X), dplasma_desc_destroy(Y), dplasma_desc_destroy(A), dplasma_desc_destroy(D);
 }
 
+/* the solve-side EXT ops natively: dtrsmpl_ptgpanel (B := L^-1 P B with the getrf_1d factors, checked as
+ * L Y = P B on the host), dtrdsm (B := D^-1 B), dtrmdm (strict lower part := L D^-1) and dprint */
+static void test_trsmpl_diag(dplasma_context_t *ctx) {
+  const int n = 600, nb = 256, nc = 7;
+  dplasma_desc_t *G = dmat(ctx, dplasmaRealDouble, nb, n, n), *B = dmat(ctx, dplasmaRealDouble, nb, n, nc);
+  dplasma_desc_t *IP = dplasma_desc_ipiv(ctx, 1, nb, 1, n, 1, 1);
+  double *g = malloc(sizeof(double) * n * n), *b = malloc(sizeof(double) * n * nc), *y = malloc(sizeof(double) * n * nc);
+  int *ipiv = malloc(sizeof(int) * n);
+  unsigned sd = 91;
+  rnd_fill(g, (size_t)n * n, &sd), rnd_fill(b, (size_t)n * nc, &sd);
+  dplasma_desc_set_lapack(G, g, n);
+  dplasma_desc_set_lapack(B, b, n);
+  CHECK(dplasma_dgetrf_1d(ctx, G, IP) == 0, "trsmpl: getrf %s", dplasma_last_error());
+  CHECK(dplasma_dtrsmpl_ptgpanel(ctx, G, IP, B) == 0, "dtrsmpl_ptgpanel: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(G, g, n);
+  dplasma_desc_get_lapack(IP, ipiv, 1);
+  dplasma_desc_get_lapack(B, y, n);
+  for (int i = 0; i < n; ++i) {   /* P b on the host */
+    const int p = ipiv[i] - 1;
+    if (p != i)
+      for (int c = 0; c < nc; ++c) {
+        const double t = b[i + (size_t)c * n];
+        b[i + (size_t)c * n] = b[p + (size_t)c * n];
+        b[p + (size_t)c * n] = t;
+      }
+  }
+  double err = 0, scale = 0;
+  for (int c = 0; c < nc; ++c)
+    for (int i = 0; i < n; ++i) {
+      double s = y[i + (size_t)c * n];   /* unit diagonal */
+      for (int k = 0; k < i; ++k) s += g[i + (size_t)k * n] * y[k + (size_t)c * n];
+      err = fmax(err, fabs(s - b[i + (size_t)c * n]));
+      scale = fmax(scale, fabs(b[i + (size_t)c * n]));
+    }
+  printf("dtrsmpl_ptgpanel %d x %d: max |L Y - P B| %.3e\n", n, nc, err);
+  CHECK(err < 1e-11 * fmax(1.0, scale) * n, "dtrsmpl_ptgpanel error %.3e", err);
+  /* trdsm / trmdm on a matrix with a nonzero diagonal */
+  for (int i = 0; i < n; ++i) g[i + (size_t)i * n] = 2.0 + 0.01 * i;
+  rnd_fill(b, (size_t)n * nc, &sd);
+  dplasma_desc_set_lapack(G, g, n);
+  dplasma_desc_set_lapack(B, b, n);
+  CHECK(dplasma_dtrdsm(ctx, G, B) == 0, "dtrdsm: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(B, y, n);
+  err = 0;
+  for (int c = 0; c < nc; ++c)
+    for (int i = 0; i < n; ++i) err = fmax(err, fabs(y[i + (size_t)c * n] - b[i + (size_t)c * n] / g[i + (size_t)i * n]));
+  printf("dtrdsm %d x %d: max diff %.3e\n", n, nc, err);
+  CHECK(err < 1e-15, "dtrdsm differs (%.3e)", err);
+  double *r = malloc(sizeof(double) * n * n);
+  CHECK(dplasma_dtrmdm(ctx, G) == 0, "dtrmdm: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(G, r, n);
+  err = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < n; ++i) {
+      const double want = i > j ? g[i + (size_t)j * n] / g[j + (size_t)j * n] : g[i + (size_t)j * n];
+      err = fmax(err, fabs(r[i + (size_t)j * n] - want));
+    }
+  printf("dtrmdm %d x %d: max diff %.3e\n", n, n, err);
+  CHECK(err < 1e-15, "dtrmdm differs (%.3e)", err);
+  dplasma_desc_t *S = dmat(ctx, dplasmaRealDouble, 2, 3, 3);
+  double s9[9] = {1, 2, 3, 4, 5, 6, 7, 8, 9};
+  dplasma_desc_set_lapack(S, s9, 3);
+  CHECK(dplasma_dprint(ctx, dplasmaLower, S) == 0, "dprint: %s", dplasma_last_error());
+  free(g), free(b), free(y), free(r), free(ipiv);
+  dplasma_desc_destroy(G), dplasma_desc_destroy(B), dplasma_desc_destroy(IP), dplasma_desc_destroy(S);
+}
+
 int main(int argc, char **argv) {
   setvbuf(stdout, NULL, _IONBF, 0);
   signal(SIGSEGV, on_fault);
@@ -1144,9 +1211,10 @@ int main(int argc, char **argv) {
   test_ger(ctx);
   test_laswp(ctx);
   test_lanm2(ctx);
+  test_trsmpl_diag(ctx);
   /* an operation without a native implementation fails cleanly */
   dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
-  CHECK(dplasma_dtrmdm(ctx, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");
+  CHECK(dplasma_dhetrf(ctx, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");
   dplasma_desc_destroy(A);
   if (argc > 1 && atoi(argv[1]) > 0) bench(ctx, atoi(argv[1]));
   CHECK(dplasma_python_active() == 0, "the interpreter was started");

@@ -180,10 +180,14 @@ NATIVE_EXT = {
     "geru": lambda pc: f"nat_ger(ctx, {pc}, 0, &alpha, X, Y, A)",
     "gerc": lambda pc: f"nat_ger(ctx, {pc}, 1, &alpha, X, Y, A)",
     "laswp": lambda pc: f"nat_laswp(ctx, {pc}, A, IPIV, inc)",
+    "trsmpl_ptgpanel": lambda pc: f"nat_trsmpl_ptgpanel(ctx, {pc}, A, IPIV, B)",
+    "trdsm": lambda pc: f"nat_trdsm(ctx, {pc}, A, B)",
+    "trmdm": lambda pc: f"nat_trmdm(ctx, {pc}, A)",
 }
 # EXT entry points the engine answers directly (a value, no program)
 NATIVE_EXT_DIRECT = {
     "lanm2": lambda pc: f"nat_lanm2(ctx, {pc}, A, info)",
+    "print": lambda pc: f"nat_print(ctx, {pc}, uplo, A)",
 }
 
 
