@@ -774,7 +774,18 @@ static void test_dgesv_incpiv(dplasma_context_t *ctx) {
     }
   printf("dgesv_incpiv n=%d nb=%d ib=%d: ||Ax-b||/||b|| %.3e\n", n, nb, ib, err / bn);
   CHECK(err / bn < 1e-9, "gesv_incpiv residual %.3e", err / bn);
-  free(a), free(b), free(x);
+  /* the same solve in two halves: trsmpl_incpiv (L^-1 P b) and the upper TRSM */
+  double *x2 = malloc(sizeof(double) * n * nrhs);
+  dplasma_desc_set_lapack(B, b, n);
+  CHECK(dplasma_dtrsmpl_incpiv(ctx, A, L, IP, B) == 0, "dtrsmpl_incpiv: %s", dplasma_last_error());
+  CHECK(dplasma_dtrsm(ctx, dplasmaLeft, dplasmaUpper, dplasmaNoTrans, dplasmaNonUnit, 1.0, A, B) == 0, "trsm: %s",
+        dplasma_last_error());
+  dplasma_desc_get_lapack(B, x2, n);
+  double d2 = 0, xn = 0;
+  for (size_t e = 0; e < (size_t)n * nrhs; ++e) d2 = fmax(d2, fabs(x2[e] - x[e])), xn = fmax(xn, fabs(x[e]));
+  printf("dtrsmpl_incpiv + dtrsm vs gesv_incpiv: max diff %.3e (|x| %.3e)\n", d2, xn);
+  CHECK(d2 <= 1e-12 * xn, "dtrsmpl_incpiv differs (%.3e)", d2);
+  free(a), free(b), free(x), free(x2);
   dplasma_desc_destroy(A), dplasma_desc_destroy(B), dplasma_desc_destroy(L), dplasma_desc_destroy(IP);
 }
 

@@ -181,6 +181,7 @@ NATIVE_EXT = {
     "gerc": lambda pc: f"nat_ger(ctx, {pc}, 1, &alpha, X, Y, A)",
     "laswp": lambda pc: f"nat_laswp(ctx, {pc}, A, IPIV, inc)",
     "trsmpl_ptgpanel": lambda pc: f"nat_trsmpl_ptgpanel(ctx, {pc}, A, IPIV, B)",
+    "trsmpl_incpiv": lambda pc: f"nat_trsmpl_incpiv(ctx, {pc}, A, L, IPIV, B)",
     "trdsm": lambda pc: f"nat_trdsm(ctx, {pc}, A, B)",
     "trmdm": lambda pc: f"nat_trmdm(ctx, {pc}, A)",
 }
