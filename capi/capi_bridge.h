@@ -162,6 +162,9 @@ NatProgram* nat_laswp(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplas
 double nat_lanm2(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, int* info);
 NatProgram* nat_trsmpl_ptgpanel(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* IPIV,
                                 dplasma_desc_t* B);
+NatProgram* nat_hetrf(dplasma_context_t* ctx, int prec, dplasma_desc_t* A);
+NatProgram* nat_hetrs(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* A, dplasma_desc_t* B,
+                      const void* U_but_vec, int level);
 NatProgram* nat_trdsm(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* B);
 NatProgram* nat_trmdm(dplasma_context_t* ctx, int prec, dplasma_desc_t* A);
 int nat_print(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* A);

@@ -1890,6 +1890,111 @@ NatProgram* nat_trmdm(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA) {
   return diag_scale(c, prec, "trmdm", *A, *A, true);
 }
 
+// LDL^H without pivoting (dplasma_zhetrf; models/ldl.py hetrf_New; reference src/zhetrf.jdf), one process.  Step
+// k: the Hermitian diagonal tile is completed from its lower triangle into a scratch tile and factored by the
+// no-pivot LU recursion (U = D L^H); its lower triangle (L_kk, D_k) goes back to A(k, k).  The column below is
+// solved against L_kk^H (giving L D), kept as W, divided by D, and the trailing lower triangle is updated
+// A(m, n) -= W(m, k) L(n, k)^H by one batched MFMA GEMM (diagonal tiles masked to their lower part).
+NatProgram* nat_hetrf(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA) {
+  NatCtx* c = ctx->nat;
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!same_ctx(c, {A}, prec)) return fail(nullptr, "hetrf: a descriptor of another context or precision (one process)");
+  if (A->mb != A->nb || A->m != A->n || A->mb > 512) return fail(nullptr, "hetrf: a square matrix of square tiles <= 512");
+  NatProgram* P = new_program(c, "hetrf", true);
+  LuScratch S;
+  DevPtr dt = dev_alloc((size_t)A->nb * A->nb * A->es, false);
+  if (!P->info || !dt || !lu_scratch(*P, *A, S)) return fail(P, "hetrf: device allocation failed");
+  P->keep.push_back(dt);
+  const int ct = (prec == P_C || prec == P_Z) ? CONJTRANS : TRANS;
+  const int mb = A->mb, ld = A->lld;
+  char* a = A->data;
+  char* t = (char*)dt->p;
+  char* w = (char*)S.pv->p;
+  int* info = (int*)P->info->p;
+  const Scalar one(prec, 1.0), m_one(prec, -1.0), zero(prec, 0.0);
+  int prev = -1;
+  for (int k = 0; k < A->mt; ++k) {
+    const int kb = A->cols(k), r0 = k * mb;
+    auto in = std::make_shared<MapBatch>(), out = std::make_shared<MapBatch>();
+    in->it.push_back(TileItem{A->off(k, k), 0, kb, kb, r0, r0});
+    out->it.push_back(TileItem{0, A->off(k, k), kb, kb, r0, r0});
+    in->mm = in->nn = out->mm = out->nn = kb;
+    if (!in->upload(*P) || !out->upload(*P)) return fail(P, "hetrf: device allocation failed");
+    prev = P->task(1, [=](hipStream_t s) {   // lower triangle, then strictly upper := (strictly lower)^H
+      int e = dpl_geadd(prec, 1, NOTRANS, 1, in->items(), kb, kb, one.ptr(), a, ld, zero.ptr(), t, kb, 1, s);
+      return e ? e : dpl_geadd(prec, 4, ct, 1, in->items(), kb, kb, one.ptr(), a, ld, zero.ptr(), t, kb, 1, s);
+    }, {prev});
+    prev = add_panel_lu(*P, prec, t, kb, kb, 0, kb, S, info, r0, prev, false);
+    if (prev < 0) return fail(P, "hetrf: device allocation failed");
+    prev = P->task(1, [=](hipStream_t s) {
+      return dpl_geadd(prec, 1, NOTRANS, 1, out->items(), kb, kb, one.ptr(), t, kb, zero.ptr(), a, ld, 1, s);
+    }, {prev});
+    if (k + 1 >= A->mt) continue;
+    const int ldw = A->m - (k + 1) * mb;
+    auto tr = std::make_shared<Trsm1>();
+    auto keep = std::make_shared<MapBatch>(), sc = std::make_shared<MapBatch>();
+    auto g = std::make_shared<Gemm>();
+    for (int m = k + 1; m < A->mt; ++m) {
+      tr->add(A->off(m, k), A->rows(m), kb);
+      keep->it.push_back(TileItem{A->off(m, k), (long long)(m - k - 1) * mb, A->rows(m), kb, 0, 0});
+      sc->it.push_back(TileItem{A->off(k, k), A->off(m, k), A->rows(m), kb, m * mb, r0});
+      keep->mm = sc->mm = std::max(keep->mm, A->rows(m));
+      for (int n = k + 1; n <= m; ++n)
+        g->add(A->off(m, n), A->rows(m), A->cols(n), {KPair{(long long)(m - k - 1) * mb, A->off(n, k), kb, 0}},
+               m == n ? 1 : 0);
+    }
+    keep->nn = sc->nn = kb;
+    if (!tr->upload(*P, prec, RIGHT) || !keep->upload(*P) || !sc->upload(*P) || !g->upload(*P))
+      return fail(P, "hetrf: device allocation failed");
+    prev = P->task(1, [=](hipStream_t s) {   // A(m, k) := A(m, k) L_kk^-H = L(m, k) D_k
+      return tr->launch(prec, RIGHT, LOWER, ct, UNIT, one, t, kb, a, ld, s);
+    }, {prev});
+    prev = P->task(1, [=](hipStream_t s) {   // W := L D; A(m, k) := L(m, k)
+      int e = dpl_geadd(prec, 0, NOTRANS, keep->n(), keep->items(), keep->mm, keep->nn, one.ptr(), a, ld, zero.ptr(),
+                        w, ldw, 1, s);
+      return e ? e : dpl_diag_scale(prec, 0, 1, sc->n(), sc->items(), sc->mm, sc->nn, a, ld, a, ld, s);
+    }, {prev});
+    prev = P->task(1, [=](hipStream_t s) {
+      return g->launch(prec, NOTRANS, ct, m_one, w, ldw, a, ld, one, a, ld, s);
+    }, {prev});
+  }
+  return P;
+}
+
+// x := (L D L^H)^-1 b with the hetrf factors (dplasma_zhetrs without butterflies; models/ldl.py hetrs): two
+// unit-lower TRSMs around trdsm.  The butterfly form (U_but_vec) stays with the Python layer.
+NatProgram* nat_hetrs(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* dA, dplasma_desc_t* dB,
+                      const void* U_but_vec, int level) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *B = dB ? dB->nat : nullptr;
+  if (!same_ctx(c, {A, B}, prec)) return fail(nullptr, "hetrs: descriptors of another context or precision (one process)");
+  if (U_but_vec && level > 0) return fail(nullptr, "hetrs: butterfly-transformed solves need the Python layer (native: U_but_vec = NULL)");
+  if (uplo != LOWER || A->mb != A->nb || A->m != A->n || B->m != A->n || B->mb != A->mb)
+    return fail(nullptr, "hetrs: operands do not conform (lower factors, square tiles)");
+  const int ct = (prec == P_C || prec == P_Z) ? CONJTRANS : TRANS;
+  NatProgram* P = new_program(c, "hetrs", false);
+  const Scalar one(prec, 1.0);
+  std::vector<TileItem> it;
+  int mm = 0, nn = 0;
+  for (int k = 0; k < B->mt; ++k)
+    for (int n = 0; n < B->nt; ++n) {
+      it.push_back(TileItem{A->off(k, k), B->off(k, n), B->rows(k), B->cols(n), k * B->mb, n * B->nb});
+      mm = std::max(mm, B->rows(k));
+      nn = std::max(nn, B->cols(n));
+    }
+  DevPtr d = dev_upload(it);
+  if (!d || !add_trsm(*P, LEFT, LOWER, NOTRANS, UNIT, one, *A, *B, 1, -1)) return fail(P, "hetrs: device allocation failed");
+  P->keep.push_back(d);
+  const int n = (int)it.size(), lda = A->lld, ldb = B->lld;
+  const char* a = A->data;
+  char* b = B->data;
+  const int t = P->task(1, [=](hipStream_t s) {
+    return dpl_diag_scale(prec, 0, 0, n, d->p, mm, nn, a, lda, b, ldb, s);
+  }, {last_on(*P, 1)});
+  if (!add_trsm(*P, LEFT, LOWER, ct, UNIT, one, *A, *B, 1, t)) return fail(P, "hetrs: device allocation failed");
+  return P;
+}
+
 // dplasma_zprint (src/zprint.jdf; models/aux.py print_matrix): the uplo part of A tile by tile, in the
 // Python layer's format, from a host copy (one process)
 int nat_print(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* dA) {

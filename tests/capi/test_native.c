@@ -1183,6 +1183,57 @@ static void test_trsmpl_diag(dplasma_context_t *ctx) {
   dplasma_desc_destroy(G), dplasma_desc_destroy(B), dplasma_desc_destroy(IP), dplasma_desc_destroy(S);
 }
 
+/* LDL^H without pivoting natively: dhetrf + dhetrs on a symmetric diagonally dominant matrix (plgsy) and zhetrf +
+ * zhetrs on a Hermitian one (plghe), the residual checked against the host copy of the full matrix */
+static void test_hetrf(dplasma_context_t *ctx) {
+  const int n = 600, nb = 256, nrhs = 3;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, n, n), *B = dmat(ctx, dplasmaRealDouble, nb, n, nrhs);
+  dplasma_dplgsy(ctx, (double)n, dplasmaUpperLower, A, 51);
+  dplasma_dplrnt(ctx, 0, B, 52);
+  double *a = malloc(sizeof(double) * n * n), *b = malloc(sizeof(double) * n * nrhs), *x = malloc(sizeof(double) * n * nrhs);
+  dplasma_desc_get_lapack(A, a, n);
+  dplasma_desc_get_lapack(B, b, n);
+  int info = dplasma_dhetrf(ctx, A);
+  CHECK(info == 0, "dhetrf info %d (%s)", info, dplasma_last_error());
+  CHECK(dplasma_dhetrs(ctx, dplasmaLower, A, B, NULL, 0) == 0, "dhetrs: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(B, x, n);
+  double err = 0, bn = 0;
+  for (int c = 0; c < nrhs; ++c)
+    for (int i = 0; i < n; ++i) {
+      double s = 0;
+      for (int k = 0; k < n; ++k) s += a[i + (size_t)k * n] * x[k + (size_t)c * n];
+      err = fmax(err, fabs(s - b[i + (size_t)c * n]));
+      bn = fmax(bn, fabs(b[i + (size_t)c * n]));
+    }
+  printf("dhetrf + dhetrs n=%d nb=%d: ||Ax-b||/||b|| %.3e\n", n, nb, err / bn);
+  CHECK(err / bn < 1e-10, "dhetrf/dhetrs residual %.3e", err / bn);
+  free(a), free(b), free(x);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(B);
+  dplasma_desc_t *Az = dmat(ctx, dplasmaComplexDouble, nb, n, n), *Bz = dmat(ctx, dplasmaComplexDouble, nb, n, nrhs);
+  dplasma_zplghe(ctx, (double)n, dplasmaUpperLower, Az, 61);
+  dplasma_zplrnt(ctx, 0, Bz, 62);
+  double complex *az = malloc(sizeof(double complex) * n * n), *bz = malloc(sizeof(double complex) * n * nrhs);
+  double complex *xz = malloc(sizeof(double complex) * n * nrhs);
+  dplasma_desc_get_lapack(Az, az, n);
+  dplasma_desc_get_lapack(Bz, bz, n);
+  info = dplasma_zhetrf(ctx, Az);
+  CHECK(info == 0, "zhetrf info %d (%s)", info, dplasma_last_error());
+  CHECK(dplasma_zhetrs(ctx, dplasmaLower, Az, Bz, NULL, 0) == 0, "zhetrs: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(Bz, xz, n);
+  err = 0, bn = 0;
+  for (int c = 0; c < nrhs; ++c)
+    for (int i = 0; i < n; ++i) {
+      double complex s = 0;
+      for (int k = 0; k < n; ++k) s += az[i + (size_t)k * n] * xz[k + (size_t)c * n];
+      err = fmax(err, cabs(s - bz[i + (size_t)c * n]));
+      bn = fmax(bn, cabs(bz[i + (size_t)c * n]));
+    }
+  printf("zhetrf + zhetrs n=%d nb=%d: ||Ax-b||/||b|| %.3e\n", n, nb, err / bn);
+  CHECK(err / bn < 1e-10, "zhetrf/zhetrs residual %.3e", err / bn);
+  free(az), free(bz), free(xz);
+  dplasma_desc_destroy(Az), dplasma_desc_destroy(Bz);
+}
+
 int main(int argc, char **argv) {
   setvbuf(stdout, NULL, _IONBF, 0);
   signal(SIGSEGV, on_fault);
@@ -1223,9 +1274,10 @@ int main(int argc, char **argv) {
   test_laswp(ctx);
   test_lanm2(ctx);
   test_trsmpl_diag(ctx);
+  test_hetrf(ctx);
   /* an operation without a native implementation fails cleanly */
   dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
-  CHECK(dplasma_dhetrf(ctx, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");
+  CHECK(dplasma_dhbrdt(ctx, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");
   dplasma_desc_destroy(A);
   if (argc > 1 && atoi(argv[1]) > 0) bench(ctx, atoi(argv[1]));
   CHECK(dplasma_python_active() == 0, "the interpreter was started");

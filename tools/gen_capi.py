@@ -182,6 +182,8 @@ NATIVE_EXT = {
     "laswp": lambda pc: f"nat_laswp(ctx, {pc}, A, IPIV, inc)",
     "trsmpl_ptgpanel": lambda pc: f"nat_trsmpl_ptgpanel(ctx, {pc}, A, IPIV, B)",
     "trsmpl_incpiv": lambda pc: f"nat_trsmpl_incpiv(ctx, {pc}, A, L, IPIV, B)",
+    "hetrf": lambda pc: f"nat_hetrf(ctx, {pc}, A)",
+    "hetrs": lambda pc: f"nat_hetrs(ctx, {pc}, uplo, A, B, U_but_vec, level)",
     "trdsm": lambda pc: f"nat_trdsm(ctx, {pc}, A, B)",
     "trmdm": lambda pc: f"nat_trmdm(ctx, {pc}, A)",
 }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# r4 batch 32: native C ABI additions (geru / gerc, laswp, lanm2, trsmpl_ptgpanel, trdsm, trmdm, print) and the getrs swap refactor under the native tests.
+# r4 batch 32: native C ABI additions (geru / gerc, laswp, lanm2, trsmpl_ptgpanel, trsmpl_incpiv, trdsm, trmdm, hetrf, hetrs, print) and the getrs swap refactor under the native tests.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/r4b32
 mkdir -p $O
@@ -9,7 +9,7 @@ step() {
   echo "== $name" | tee -a $O/summary.log
   timeout -k 10 $to "$@" > $O/$name.log 2>&1
   local rc=$?
-  grep -E "passed|failed|error|Error|FAIL|dgeru|zgerc|dlaswp|dlanm2|dtrsmpl|dtrdsm|dtrmdm|A\(|dgetrs|dgesv|native C ABI" $O/$name.log | grep -v amdgpu.ids | tail -12 | tee -a $O/summary.log
+  grep -E "passed|failed|error|Error|FAIL|dgeru|zgerc|dlaswp|dlanm2|dtrsmpl|dtrdsm|dtrmdm|hetrf|incpiv|A\(|dgetrs|dgesv|native C ABI" $O/$name.log | grep -v amdgpu.ids | tail -12 | tee -a $O/summary.log
   echo "rc=$rc" | tee -a $O/summary.log
   return $rc
 }
