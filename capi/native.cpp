@@ -2775,6 +2775,65 @@ int nat_qr_tau(dplasma_desc_t* dT, void* tau, int k) {
 // ||A||_2 estimate by power iteration on A^H A (dplasma_zlanm2, src/zlanm2.jdf; the same loop as
 // models/aux.lanm2): x = n^-1/2 (1, .., 1); y = A x; x = A^H y; e = ||x|| / ||y||; x /= ||x||, until e moves by
 // less than 1e-10 relatively (at most 500 products).  *info: the iteration count, negative if not converged.
+// dplasma_zlatms (models/generators.py latms): singular values D(i) = 1 - i/(N-1) (1 - 1/cond) (D(0) = 1) on
+// the diagonal, then A = Q1 D Q2 (General) or Q D Q^H (symmetric / Hermitian) with the random unitary factors of
+// native geqrf's of plrnt matrices (seeds seed, seed + 1), applied by native unmqr.  One process.
+int nat_latms(dplasma_context_t* ctx, int prec, int mtxtype, double cond, dplasma_desc_t* dA, unsigned long long seed) {
+  NatCtx* c = ctx->nat;
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!same_ctx(c, {A}, prec)) return (fail(nullptr, "latms: a descriptor of another context (one process)"), -1);
+  if (A->mb != A->nb || A->nb > 256 || !(cond > 0.0))
+    return (fail(nullptr, "latms: square tiles <= 256 (the native geqrf) and cond > 0"), -1);
+  const int n = A->n;
+  const double tmp = 1.0 / cond, alp = n > 1 ? (1.0 - tmp) / (n - 1) : 0.0;
+  double z2[2] = {0.0, 0.0};
+  float zf[2] = {0.0f, 0.0f};
+  const void* zero = (prec == P_D || prec == P_Z) ? (const void*)z2 : (const void*)zf;
+  int rc = nat_execute(ctx, nat_laset(ctx, prec, UPPERLOWER, zero, zero, dA));
+  if (rc != 0) return rc;
+  // the diagonal: one strided host-to-device copy per diagonal tile (pitch lld + 1 elements)
+  const int kd = std::min(A->m, A->n);
+  std::vector<char> hd((size_t)std::max(kd, 1) * A->es, 0);
+  for (int i = 0; i < kd; ++i) {
+    const double d = i == 0 ? 1.0 : (n - i - 1) * alp + tmp;
+    if (prec == P_S || prec == P_C) {
+      const float f = (float)d;
+      std::memcpy(&hd[(size_t)i * A->es], &f, sizeof f);
+    } else {
+      std::memcpy(&hd[(size_t)i * A->es], &d, sizeof d);
+    }
+  }
+  for (int k = 0; k * A->mb < kd; ++k) {
+    const int len = std::min(A->mb, kd - k * A->mb);
+    if (hipMemcpy2D(A->data + A->off(k, k) * A->es, (size_t)(A->lld + 1) * A->es, &hd[(size_t)k * A->mb * A->es], A->es,
+                    A->es, len, hipMemcpyHostToDevice) != hipSuccess)
+      return (fail(nullptr, "latms: diagonal copy failed"), -1);
+  }
+  const int ib = std::min(32, A->nb);
+  auto qfactor = [&](int rows, unsigned long long sd, dplasma_desc_t*& Q, dplasma_desc_t*& T) {
+    Q = nat_desc(ctx, prec, A->nb, A->nb, rows, rows, 1, 1, nullptr, 0, 1);
+    const int mt = (rows + A->nb - 1) / A->nb;
+    T = nat_desc(ctx, prec, ib, A->nb, mt * ib, rows, 1, 1, nullptr, 0, 1);
+    if (!Q || !T) return -1;
+    int e = nat_execute(ctx, nat_plrnt(ctx, prec, 0, Q, sd));
+    return e ? e : nat_execute(ctx, nat_geqrf(ctx, prec, Q, T));
+  };
+  dplasma_desc_t *Q1 = nullptr, *T1 = nullptr, *Q2 = nullptr, *T2 = nullptr;
+  rc = qfactor(A->m, seed, Q1, T1);
+  if (rc == 0) rc = nat_execute(ctx, nat_unmqr(ctx, prec, LEFT, NOTRANS, Q1, T1, dA));
+  if (rc == 0) {
+    if (mtxtype == 231 /* dplasmaGeneral */) {
+      rc = qfactor(A->n, seed + 1, Q2, T2);
+      if (rc == 0) rc = nat_execute(ctx, nat_unmqr(ctx, prec, RIGHT, NOTRANS, Q2, T2, dA));
+    } else {
+      rc = nat_execute(ctx, nat_unmqr(ctx, prec, RIGHT, (prec == P_C || prec == P_Z) ? CONJTRANS : TRANS, Q1, T1, dA));
+    }
+  }
+  for (dplasma_desc_t* d : {Q1, T1, Q2, T2})
+    if (d) nat_desc_free(d), delete d;
+  return rc;
+}
+
 double nat_lanm2(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, int* info) {
   NatCtx* c = ctx->nat;
   NatDesc* A = dA ? dA->nat : nullptr;
@@ -2783,8 +2842,8 @@ double nat_lanm2(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, int* info
   dplasma_desc_t* X = nat_desc(ctx, prec, A->nb, A->nb, A->n, 1, 1, 1, nullptr, 0, 1);
   dplasma_desc_t* Y = nat_desc(ctx, prec, A->mb, A->nb, A->m, 1, 1, 1, nullptr, 0, 1);
   if (!X || !Y) {
-    if (X) nat_desc_free(X);
-    if (Y) nat_desc_free(Y);
+    if (X) nat_desc_free(X), delete X;
+    if (Y) nat_desc_free(Y), delete Y;
     return (fail(nullptr, "lanm2: device allocation failed"), NAN);
   }
   const bool cplx = prec == P_C || prec == P_Z;
@@ -2819,8 +2878,8 @@ double nat_lanm2(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, int* info
     ok = nat_execute(ctx, nat_lascal(ctx, prec, UPPERLOWER, scal(1.0 / nx, bs, fs), X)) == 0;
     ++it;
   }
-  nat_desc_free(X);
-  nat_desc_free(Y);
+  nat_desc_free(X), delete X;
+  nat_desc_free(Y), delete Y;
   if (!ok) return NAN;
   if (info) *info = std::fabs(e - e0) <= 1e-10 * std::max(e, 1e-300) ? it : -it;
   return e;

@@ -1234,6 +1234,36 @@ static void test_hetrf(dplasma_context_t *ctx) {
   dplasma_desc_destroy(Az), dplasma_desc_destroy(Bz);
 }
 
+/* dlatms natively: ||A||_F^2 = sum D(i)^2 (unitary invariance), and the symmetric form is symmetric */
+static void test_latms(dplasma_context_t *ctx) {
+  const int n = 400, nb = 128;
+  const double cond = 1e3, tmp = 1.0 / cond, alp = (1.0 - tmp) / (n - 1);
+  double f2 = 0;
+  for (int i = 0; i < n; ++i) {
+    const double d = i == 0 ? 1.0 : (n - i - 1) * alp + tmp;
+    f2 += d * d;
+  }
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, n, n);
+  CHECK(dplasma_dlatms(ctx, dplasmaGeneral, cond, A, 3872) == 0, "dlatms general: %s", dplasma_last_error());
+  const double fg = dplasma_dlange(ctx, dplasmaFrobeniusNorm, A);
+  CHECK(dplasma_dlatms(ctx, dplasmaSymmetric, cond, A, 3872) == 0, "dlatms symmetric: %s", dplasma_last_error());
+  const double fs = dplasma_dlange(ctx, dplasmaFrobeniusNorm, A);
+  double *a = malloc(sizeof(double) * n * n);
+  dplasma_desc_get_lapack(A, a, n);
+  double asym = 0, amax = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < n; ++i) {
+      asym = fmax(asym, fabs(a[i + (size_t)j * n] - a[j + (size_t)i * n]));
+      amax = fmax(amax, fabs(a[i + (size_t)j * n]));
+    }
+  printf("dlatms n=%d cond=%g: ||A||_F %.15g / %.15g vs %.15g, symmetric form |A - A^T| %.3e\n", n, cond, fg, fs,
+         sqrt(f2), asym);
+  CHECK(fabs(fg - sqrt(f2)) < 1e-12 * sqrt(f2) && fabs(fs - sqrt(f2)) < 1e-12 * sqrt(f2), "dlatms Frobenius");
+  CHECK(asym < 1e-13 * fmax(amax, 1e-300) * n, "dlatms symmetric form not symmetric (%.3e)", asym);
+  free(a);
+  dplasma_desc_destroy(A);
+}
+
 int main(int argc, char **argv) {
   setvbuf(stdout, NULL, _IONBF, 0);
   signal(SIGSEGV, on_fault);
@@ -1275,6 +1305,7 @@ int main(int argc, char **argv) {
   test_lanm2(ctx);
   test_trsmpl_diag(ctx);
   test_hetrf(ctx);
+  test_latms(ctx);
   /* an operation without a native implementation fails cleanly */
   dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
   CHECK(dplasma_dhbrdt(ctx, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");
