@@ -327,6 +327,7 @@ NatProgram* nat_posv(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t*
   NatDesc *A = dA->nat, *B = dB ? dB->nat : nullptr;
   if (!same_ctx_dist(ctx->nat, {B}, prec) || B->m != A->n || B->mb != A->nb)
     return fail(P, "posv: right-hand side does not conform");
+  P->gate = (int)P->tasks.size();   // B is left unchanged when A is not positive definite
   if (ctx->nat->dist())   // the solves follow the whole factorisation (every stream)
     return add_potrs_dist(*P, uplo, *A, *B) ? P : fail(P, "posv: device allocation failed");
   // the solves (update stream) start after the factorisation's last panel-stream task (POTRF / TRSM /

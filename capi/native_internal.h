@@ -211,6 +211,9 @@ struct NatProgram {
   DevPtr info;                   // device int: first failing column (LAPACK info), 0 if none
   int result = 0;
   bool enqueued = false;
+  // gate >= 0: tasks from index gate on are enqueued only if the factorisation before them left info == 0
+  // (blocking posv: the reference's zposv_wrapper runs potrs only then); run() synchronises at the gate
+  int gate = -1;
 
   int task(int stream, std::function<int(hipStream_t)> fn, std::initializer_list<int> deps) {
     NatTask t;
@@ -242,6 +245,14 @@ struct NatProgram {
     // info is written by panel-stream tasks only (tile factorisations)
     if (info && hipMemsetAsync(info->p, 0, sizeof(int), ctx->st[0]) != hipSuccess) return -1;
     for (size_t i = 0; i < tasks.size(); ++i) {
+      if (info && (int)i == gate) {
+        int v = 0;
+        for (int q = 0; q < NAT_NSTREAM; ++q)
+          if (hipStreamSynchronize(ctx->st[q]) != hipSuccess) return -1;
+        if (hipMemcpy(&v, info->p, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        if (ctx->comm && nat_comm_reduce_info(ctx->comm, v) != 0) return -1;   // every rank takes the same branch
+        if (v != 0) break;
+      }
       NatTask& t = tasks[i];
       hipStream_t s = ctx->st[t.stream];
       for (int d : t.deps)

@@ -1264,6 +1264,25 @@ static void test_latms(dplasma_context_t *ctx) {
   dplasma_desc_destroy(A);
 }
 
+/* dposv on a matrix that is not positive definite: info > 0 and B left unchanged (zposv_wrapper.c runs potrs
+ * only when info == 0) */
+static void test_posv_not_spd(dplasma_context_t *ctx) {
+  const int n = 300, nb = 128, nrhs = 2;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, n, n), *B = dmat(ctx, dplasmaRealDouble, nb, n, nrhs);
+  dplasma_dplgsy(ctx, 0.0, dplasmaUpperLower, A, 71);   /* no diagonal bump: indefinite */
+  dplasma_dplrnt(ctx, 0, B, 72);
+  double *b = malloc(sizeof(double) * n * nrhs), *r = malloc(sizeof(double) * n * nrhs);
+  dplasma_desc_get_lapack(B, b, n);
+  const int info = dplasma_dposv(ctx, dplasmaLower, A, B);
+  dplasma_desc_get_lapack(B, r, n);
+  double d = 0;
+  for (size_t e = 0; e < (size_t)n * nrhs; ++e) d = fmax(d, fabs(r[e] - b[e]));
+  printf("dposv on an indefinite matrix: info %d, B changed by %.3e\n", info, d);
+  CHECK(info > 0 && d == 0.0, "dposv indefinite: info %d, B changed by %.3e", info, d);
+  free(b), free(r);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(B);
+}
+
 int main(int argc, char **argv) {
   setvbuf(stdout, NULL, _IONBF, 0);
   signal(SIGSEGV, on_fault);
@@ -1306,6 +1325,7 @@ int main(int argc, char **argv) {
   test_trsmpl_diag(ctx);
   test_hetrf(ctx);
   test_latms(ctx);
+  test_posv_not_spd(ctx);
   /* an operation without a native implementation fails cleanly */
   dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
   CHECK(dplasma_dhbrdt(ctx, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");
