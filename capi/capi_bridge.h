@@ -168,6 +168,7 @@ NatProgram* nat_hetrs(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t
 NatProgram* nat_trdsm(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* B);
 NatProgram* nat_trmdm(dplasma_context_t* ctx, int prec, dplasma_desc_t* A);
 int nat_latms(dplasma_context_t* ctx, int prec, int mtxtype, double cond, dplasma_desc_t* A, unsigned long long seed);
+int nat_pltmg(dplasma_context_t* ctx, int prec, int mtxtype, dplasma_desc_t* A, unsigned long long seed);
 int nat_print(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* A);
 int nat_execute(dplasma_context_t* ctx, NatProgram* P);     // run + wait + info, frees P
 dplasma_taskpool_t* nat_wrap(NatProgram* P);

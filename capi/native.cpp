@@ -2776,6 +2776,119 @@ int nat_qr_tau(dplasma_desc_t* dT, void* tau, int k) {
 // ||A||_2 estimate by power iteration on A^H A (dplasma_zlanm2, src/zlanm2.jdf; the same loop as
 // models/aux.lanm2): x = n^-1/2 (1, .., 1); y = A x; x = A^H y; e = ||x|| / ||y||; x /= ||x||, until e moves by
 // less than 1e-10 relatively (at most 500 products).  *info: the iteration count, negative if not converged.
+// dplasma_zpltmg (models/generators.py pltmg; reference src/cores/core_zpltmg.c): the closed-form LAWN-263
+// types, evaluated per tile on the host from GLOBAL indices (identical for any tiling) and copied into the tile;
+// Random is the native plrnt.  The random-vector types (house, circul, hankel, compan, fiedler, toeppd, condex,
+// demmel, langou) and those the reference lacks return -2 / an error: they stay with the Python layer.
+static bool pltmg_value(int t, long long I, long long J, long long gM, long long gN, double& v) {
+  const double If = (double)I, Jf = (double)J, Ii = If + 1.0, Ji = Jf + 1.0;
+  switch (t) {
+    case 1: {   // hadamard
+      long long x = I & J;
+      int pc = 0;
+      while (x > 0) pc += (int)(x & 1), x >>= 1;
+      v = 1.0 - 2.0 * (pc % 2);
+      return true;
+    }
+    case 3: v = 1.0 / (If - Jf + 0.5); return true;                          // parter
+    case 4: v = 0.5 / ((double)gM - If - Jf - 0.5); return true;             // ris
+    case 5: v = std::pow(0.5, std::fabs(If - Jf)); return true;              // kms
+    case 8: v = I == J ? If + 1.0 : std::min(If, Jf) - 1.0; return true;     // moler
+    case 18: v = (J + 2) % (I + 2) == 0 ? (double)(I + 1) : -1.0; return true;   // riemann
+    case 22: v = Jf >= If ? Ii / Ji : Ji / Ii; return true;                  // lehmer
+    case 24: v = std::min(Ii, Ji); return true;                              // minij
+    case 31: v = Ji <= Ii ? Ji : -Ii; return true;                           // invhess
+    case 34: v = 1.0 / (Ii + Ji); return true;                               // cauchy
+    case 35: v = 1.0 / (If + Jf + 1.0); return true;                         // hilb
+    case 36: v = I == 0 ? 1.0 : 1.0 / (If + Jf + 1.0); return true;          // lotkin
+    case 38: {                                                               // orthog
+      const double sc = M_PI / ((double)gN + 1.0);
+      v = std::sqrt(2.0 / ((double)gN + 1.0)) * std::sin(Ii * Ji * sc);
+      return true;
+    }
+    case 39: {                                                               // wilkinson
+      const double dist = (double)std::min(gN - 1 - I, I);
+      v = I == J ? ((double)gN - 2.0 * dist - 1.0) / 2.0 : (std::llabs(I - J) == 1 ? 1.0 : 0.0);
+      return true;
+    }
+    case 40: {                                                               // foster (k = h = c = 1)
+      const double k = 1.0, h = 1.0, c = 1.0;
+      if (I == J) v = J == 0 ? 1.0 : J == gN - 1 ? 1 - 1 / c - k * h / 2 : 1 - k * h / 2;
+      else v = J == 0 ? -k * h / 2 : J == gN - 1 ? -1 / c : I > J ? -k * h : 0.0;
+      return true;
+    }
+    case 41: {                                                               // wright
+      v = I == J ? 1.0 : 0.0;
+      const bool even = J % 2 == 0;
+      if (I == J + 2) v = even ? -0.9048 : -0.8270;
+      if (I == J + 3) v = even ? -1.2092 : -1.3499;
+      if (J == gM - 2 && I == 0) v = 1.0;
+      if (J == gM - 1 && I == 1) v = 1.0;
+      return true;
+    }
+    case 28: {                                                               // dorr
+      const double theta = 0.01, h = 1.0 / ((double)gN + 1.0), term = theta / (h * h);
+      const long long half = (gN + 1) / 2;
+      const bool lo = J < half;
+      if (I == J) v = lo ? 2 * term + (0.5 - (Jf + 1) * h) / h : 2 * term - (0.5 - (Jf + 1) * h) / h;
+      else if (I == J - 1) v = (lo || J == half) ? -term - (0.5 - Jf * h) / h : -term;
+      else if (I == J + 1) v = lo ? (J + 1 == half ? -term + (0.5 - (Jf + 2) * h) / h : -term)
+                                  : -term + (0.5 - (Jf + 2) * h) / h;
+      else v = 0.0;
+      return true;
+    }
+    case 30: {                                                               // chebvand
+      const double p = Jf * (gN > 1 ? 1.0 / ((double)gN - 1.0) : 0.0);
+      double T0 = 1.0, T1 = p;
+      if (I == 0) { v = T0; return true; }
+      for (long long k = 2; k <= I; ++k) {
+        const double T2 = 2 * p * T1 - T0;
+        T0 = T1, T1 = T2;
+      }
+      v = T1;
+      return true;
+    }
+    default: return false;
+  }
+}
+
+int nat_pltmg(dplasma_context_t* ctx, int prec, int mtxtype, dplasma_desc_t* dA, unsigned long long seed) {
+  NatCtx* c = ctx->nat;
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!same_ctx_dist(c, {A}, prec)) return (fail(nullptr, "pltmg: a descriptor of another context or precision"), -1);
+  if (mtxtype == 0) return nat_execute(ctx, nat_plrnt(ctx, prec, 0, dA, seed));
+  double probe;
+  if (!pltmg_value(mtxtype, 0, 0, std::max(A->m, 1), std::max(A->n, 1), probe))
+    return (fail(nullptr, "pltmg: this matrix type needs the Python layer on a native context (closed-form types "
+                          "and Random only)"), -2);
+  if (mtxtype == 1 && (A->m != A->n || (A->m & (A->m - 1)))) return -2;   // hadamard: n a power of two
+  for (int q = 0; q < NAT_NSTREAM; ++q)
+    if (hipStreamSynchronize(c->st[q]) != hipSuccess) return -1;
+  std::vector<char> h((size_t)A->mb * A->nb * A->es);
+  for (int j = 0; j < A->nt; ++j)
+    for (int i = 0; i < A->mt; ++i) {
+      if (!A->local(i, j)) continue;
+      const int r = A->rows(i), cc = A->cols(j);
+      std::fill(h.begin(), h.end(), 0);
+      for (int jj = 0; jj < cc; ++jj)
+        for (int ii = 0; ii < r; ++ii) {
+          double v = 0.0;
+          pltmg_value(mtxtype, (long long)i * A->mb + ii, (long long)j * A->nb + jj, A->m, A->n, v);
+          char* e = &h[((size_t)ii + (size_t)jj * r) * A->es];
+          if (prec == P_S || prec == P_C) {
+            const float f = (float)v;
+            std::memcpy(e, &f, sizeof f);
+          } else {
+            std::memcpy(e, &v, sizeof v);
+          }
+        }
+      if (hipMemcpy2D(A->data + A->off(i, j) * A->es, (size_t)A->lld * A->es, h.data(), (size_t)r * A->es,
+                      (size_t)r * A->es, cc, hipMemcpyHostToDevice) != hipSuccess)
+        return (fail(nullptr, "pltmg: copy to the device failed"), -1);
+    }
+  return 0;
+}
+
 // dplasma_zlatms (models/generators.py latms): singular values D(i) = 1 - i/(N-1) (1 - 1/cond) (D(0) = 1) on
 // the diagonal, then A = Q1 D Q2 (General) or Q D Q^H (symmetric / Hermitian) with the random unitary factors of
 // native geqrf's of plrnt matrices (seeds seed, seed + 1), applied by native unmqr.  One process.

@@ -1283,6 +1283,37 @@ static void test_posv_not_spd(dplasma_context_t *ctx) {
   dplasma_desc_destroy(A), dplasma_desc_destroy(B);
 }
 
+/* dpltmg natively (closed-form types): hilb / minij element values, hadamard H H^T = n I, a random-vector type
+ * (house) refused with -2 */
+static void test_pltmg(dplasma_context_t *ctx) {
+  const int n = 256, nb = 96;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, n, n);
+  double *a = malloc(sizeof(double) * n * n);
+  CHECK(dplasma_dpltmg(ctx, dplasmaMatrixHilb, A, 3872) == 0, "dpltmg hilb: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(A, a, n);
+  double err = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < n; ++i) err = fmax(err, fabs(a[i + (size_t)j * n] - 1.0 / (i + j + 1.0)));
+  CHECK(dplasma_dpltmg(ctx, dplasmaMatrixMinij, A, 3872) == 0, "dpltmg minij: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(A, a, n);
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < n; ++i) err = fmax(err, fabs(a[i + (size_t)j * n] - (double)(i < j ? i + 1 : j + 1)));
+  CHECK(dplasma_dpltmg(ctx, dplasmaMatrixHadamard, A, 3872) == 0, "dpltmg hadamard: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(A, a, n);
+  double orth = 0;
+  for (int j = 0; j < n; j += 17)
+    for (int i = 0; i < n; i += 13) {
+      double s = 0;
+      for (int k = 0; k < n; ++k) s += a[i + (size_t)k * n] * a[j + (size_t)k * n];
+      orth = fmax(orth, fabs(s - (i == j ? n : 0)));
+    }
+  const int rh = dplasma_dpltmg(ctx, dplasmaMatrixHouse, A, 3872);
+  printf("dpltmg hilb / minij max error %.3e, hadamard |H H^T - n I| %.3e, house -> %d\n", err, orth, rh);
+  CHECK(err == 0.0 && orth == 0.0 && rh == -2, "dpltmg: err %.3e orth %.3e house %d", err, orth, rh);
+  free(a);
+  dplasma_desc_destroy(A);
+}
+
 int main(int argc, char **argv) {
   setvbuf(stdout, NULL, _IONBF, 0);
   signal(SIGSEGV, on_fault);
@@ -1326,6 +1357,7 @@ int main(int argc, char **argv) {
   test_hetrf(ctx);
   test_latms(ctx);
   test_posv_not_spd(ctx);
+  test_pltmg(ctx);
   /* an operation without a native implementation fails cleanly */
   dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
   CHECK(dplasma_dhbrdt(ctx, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");

@@ -191,6 +191,7 @@ NATIVE_EXT = {
 NATIVE_EXT_DIRECT = {
     "lanm2": lambda pc: f"nat_lanm2(ctx, {pc}, A, info)",
     "print": lambda pc: f"nat_print(ctx, {pc}, uplo, A)",
+    "pltmg": lambda pc: f"nat_pltmg(ctx, {pc}, mtxtype, A, seed)",
     "latms": lambda pc: f"nat_latms(ctx, {pc}, mtxtype, cond, A, seed)",
 }
 
