@@ -163,8 +163,11 @@ double nat_lanm2(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, int* info)
 NatProgram* nat_trsmpl_ptgpanel(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* IPIV,
                                 dplasma_desc_t* B);
 NatProgram* nat_hetrf(dplasma_context_t* ctx, int prec, dplasma_desc_t* A);
-NatProgram* nat_hetrs(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* A, dplasma_desc_t* B,
-                      const void* U_but_vec, int level);
+int nat_hetrs(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* A, dplasma_desc_t* B, const void* U_but_vec,
+              int level);
+int nat_gebmm(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, const void* U, int level, int trans);
+int nat_gebut(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, const void* U, int level);
+int nat_hebut(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, void** U_out, int level);
 NatProgram* nat_trdsm(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* B);
 NatProgram* nat_trmdm(dplasma_context_t* ctx, int prec, dplasma_desc_t* A);
 int nat_latms(dplasma_context_t* ctx, int prec, int mtxtype, double cond, dplasma_desc_t* A, unsigned long long seed);

@@ -1962,14 +1962,12 @@ NatProgram* nat_hetrf(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA) {
   return P;
 }
 
-// x := (L D L^H)^-1 b with the hetrf factors (dplasma_zhetrs without butterflies; models/ldl.py hetrs): two
-// unit-lower TRSMs around trdsm.  The butterfly form (U_but_vec) stays with the Python layer.
-NatProgram* nat_hetrs(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* dA, dplasma_desc_t* dB,
-                      const void* U_but_vec, int level) {
+// x := (L D L^H)^-1 b with the hetrf factors (dplasma_zhetrs; models/ldl.py hetrs): two unit-lower TRSMs around
+// trdsm; with a butterfly (hebut's U_but_vec, level > 0) x := U (L D L^H)^-1 U^T b
+static NatProgram* hetrs_solve(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* dA, dplasma_desc_t* dB) {
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *B = dB ? dB->nat : nullptr;
   if (!same_ctx(c, {A, B}, prec)) return fail(nullptr, "hetrs: descriptors of another context or precision (one process)");
-  if (U_but_vec && level > 0) return fail(nullptr, "hetrs: butterfly-transformed solves need the Python layer (native: U_but_vec = NULL)");
   if (uplo != LOWER || A->mb != A->nb || A->m != A->n || B->m != A->n || B->mb != A->mb)
     return fail(nullptr, "hetrs: operands do not conform (lower factors, square tiles)");
   const int ct = (prec == P_C || prec == P_Z) ? CONJTRANS : TRANS;
@@ -1994,6 +1992,134 @@ NatProgram* nat_hetrs(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t
   }, {last_on(*P, 1)});
   if (!add_trsm(*P, LEFT, LOWER, ct, UNIT, one, *A, *B, 1, t)) return fail(P, "hetrs: device allocation failed");
   return P;
+}
+
+int nat_hetrs(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* dA, dplasma_desc_t* dB, const void* U_but_vec,
+              int level) {
+  int nat_gebmm(dplasma_context_t*, int, dplasma_desc_t*, const void*, int, int);
+  const bool but = U_but_vec && level > 0;
+  const int ct = (prec == P_C || prec == P_Z) ? CONJTRANS : TRANS;
+  if (but)
+    if (int rc = nat_gebmm(ctx, prec, dB, U_but_vec, level, ct)) return rc;
+  if (int rc = nat_execute(ctx, hetrs_solve(ctx, prec, uplo, dA, dB))) return rc;
+  return but ? nat_gebmm(ctx, prec, dB, U_but_vec, level, NOTRANS) : 0;
+}
+
+// ----------------------------------------------------------------------------- random butterflies (RBT)
+// models/ldl.py gebmm / gebut / hebut; reference src/zhebut.jdf, zgebut.jdf, zgebmm.jdf.  On a native context the
+// butterfly is a HOST array of levels x n values of A's precision (row l = the random diagonal R of level l,
+// entries exp(u / 10), u the plrnt values of seed 3872), as hebut returns it (malloc; the caller frees it).
+// Level l is block diagonal with 2^l butterflies W = 1/sqrt(2) [R0 R1; R0 -R1] of order n / 2^l; each level is
+// applied as one native GEMM with the (sparse) butterfly matrix stored dense.  One process.
+static double but_val(const void* U, int prec, size_t e) {
+  switch (prec) {
+    case P_S: return ((const float*)U)[e];
+    case P_D: return ((const double*)U)[e];
+    case P_C: return ((const float*)U)[2 * e];
+    default: return ((const double*)U)[2 * e];
+  }
+}
+
+// A := B_l A (side LEFT) or A B_l (RIGHT), B_l transposed when tr
+static int but_apply(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, const void* U, int l, bool tr, int side) {
+  NatDesc* A = dA->nat;
+  const int n = side == LEFT ? A->m : A->n;
+  const int size = n >> l, h = size / 2;
+  const double s2 = 1.0 / std::sqrt(2.0);
+  std::vector<char> hb((size_t)n * n * A->es, 0);
+  auto put = [&](long long I, long long J, double v) {
+    if (tr) std::swap(I, J);
+    char* e = &hb[((size_t)I + (size_t)J * n) * A->es];
+    if (prec == P_S || prec == P_C) {
+      const float f = (float)v;
+      std::memcpy(e, &f, sizeof f);
+    } else {
+      std::memcpy(e, &v, sizeof v);
+    }
+  };
+  const size_t row = (size_t)l * n;
+  for (long long I = 0; I < n; ++I) {
+    const long long base = (I / size) * size, li = I % size;
+    const bool top = li < h;
+    const long long p = top ? li : li - h;
+    put(I, base + p, but_val(U, prec, row + std::min<long long>(base + p, n - 1)) * s2);
+    const double r1 = but_val(U, prec, row + std::min<long long>(base + h + p, n - 1)) * s2;
+    put(I, base + h + p, top ? r1 : -r1);
+  }
+  dplasma_desc_t* B = nat_desc(ctx, prec, A->mb, A->mb, n, n, 1, 1, nullptr, 0, 1);
+  dplasma_desc_t* T = nat_desc(ctx, prec, A->mb, A->nb, A->m, A->n, 1, 1, nullptr, 0, 1);
+  int rc = (B && T) ? 0 : -1;
+  double o2[2] = {1.0, 0.0}, z2[2] = {0.0, 0.0};
+  float of[2] = {1.0f, 0.0f}, zf[2] = {0.0f, 0.0f};
+  const bool dbl = prec == P_D || prec == P_Z;
+  const void* one = dbl ? (const void*)o2 : (const void*)of;
+  const void* zero = dbl ? (const void*)z2 : (const void*)zf;
+  if (rc == 0) rc = nat_desc_io(B, hb.data(), n, true);
+  if (rc == 0)
+    rc = nat_execute(ctx, side == LEFT ? nat_gemm(ctx, prec, NOTRANS, NOTRANS, one, B, dA, zero, T)
+                                       : nat_gemm(ctx, prec, NOTRANS, NOTRANS, one, dA, B, zero, T));
+  if (rc == 0) rc = nat_execute(ctx, nat_lacpy(ctx, prec, UPPERLOWER, T, dA));
+  for (dplasma_desc_t* d : {B, T})
+    if (d) nat_desc_free(d), delete d;
+  return rc;
+}
+
+static bool but_ok(NatCtx* c, int prec, NatDesc* A, int n, const void* U, int level, const char* op) {
+  if (!same_ctx(c, {A}, prec)) return (fail(nullptr, std::string(op) + ": a descriptor of another context (one process)"), false);
+  if (!U || level < 0 || level > 30 || n % (1 << level))
+    return (fail(nullptr, std::string(op) + ": a butterfly vector and an order that is a multiple of 2^level"), false);
+  return true;
+}
+
+int nat_gebmm(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, const void* U, int level, int trans) {
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!A || !but_ok(ctx->nat, prec, A, A->m, U, level, "gebmm")) return -1;
+  for (int q = 0; q < level; ++q) {   // U A = B_0 (B_1 (... B_{L-1} A)); U^T A = B_{L-1}^T (... B_0^T A)
+    const int l = trans == NOTRANS ? level - 1 - q : q;
+    if (int rc = but_apply(ctx, prec, dA, U, l, trans != NOTRANS, LEFT)) return rc;
+  }
+  return 0;
+}
+
+int nat_gebut(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, const void* U, int level) {
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!A || !but_ok(ctx->nat, prec, A, A->n, U, level, "gebut") || A->m != A->n)
+    return A ? (fail(nullptr, "gebut: a square matrix"), -1) : -1;
+  if (int rc = nat_gebmm(ctx, prec, dA, U, level, TRANS)) return rc;
+  for (int l = 0; l < level; ++l)   // (U^T A) U = ((U^T A) B_0) B_1 ...
+    if (int rc = but_apply(ctx, prec, dA, U, l, false, RIGHT)) return rc;
+  return 0;
+}
+
+int nat_hebut(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, void** U_out, int level) {
+  NatDesc* A = dA ? dA->nat : nullptr;
+  if (!U_out || !A) return (fail(nullptr, "hebut: U_but_ptr and A"), -1);
+  if (!same_ctx(ctx->nat, {A}, prec)) return (fail(nullptr, "hebut: a descriptor of another context (one process)"), -1);
+  const int n = A->n;
+  if (A->m != n || level < 0 || level > 30 || n % (1 << level))
+    return (fail(nullptr, "hebut: a square matrix whose order is a multiple of 2^level"), -1);
+  // the random diagonals: plrnt values of an (n * level) x 1 real matrix, seed 3872 (ldl.butterfly_vectors)
+  const int len = std::max(1, n * level);
+  dplasma_desc_t* R = nat_desc(ctx, P_D, std::min(len, 4096), 1, len, 1, 1, 1, nullptr, 0, 1);
+  std::vector<double> u(len);
+  int rc = R ? nat_execute(ctx, nat_plrnt(ctx, P_D, 0, R, 3872)) : -1;
+  if (rc == 0) rc = nat_desc_io(R, u.data(), len, false);
+  if (R) nat_desc_free(R), delete R;
+  if (rc != 0) return rc;
+  void* U = std::calloc((size_t)len, A->es);
+  if (!U) return (fail(nullptr, "hebut: host allocation failed"), -1);
+  for (int e = 0; e < n * level; ++e) {
+    const double v = std::exp(u[e] / 10.0);
+    if (prec == P_S || prec == P_C) ((float*)U)[(prec == P_C ? 2 : 1) * e] = (float)v;
+    else ((double*)U)[(prec == P_Z ? 2 : 1) * e] = v;
+  }
+  rc = nat_gebut(ctx, prec, dA, U, level);
+  if (rc != 0) {
+    std::free(U);
+    return rc;
+  }
+  *U_out = U;
+  return 0;
 }
 
 // dplasma_zprint (src/zprint.jdf; models/aux.py print_matrix): the uplo part of A tile by tile, in the

@@ -1314,6 +1314,37 @@ static void test_pltmg(dplasma_context_t *ctx) {
   dplasma_desc_destroy(A);
 }
 
+/* random butterflies natively: hebut (A := U^T A U, U returned on the host), hetrf without pivoting on the
+ * transformed matrix, hetrs with the butterfly (x = U (L D L^T)^-1 U^T b) -- the residual on the original A */
+static void test_butterfly(dplasma_context_t *ctx) {
+  const int n = 512, nb = 128, nrhs = 2, level = 2;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, n, n), *B = dmat(ctx, dplasmaRealDouble, nb, n, nrhs);
+  dplasma_dplgsy(ctx, 1.0, dplasmaUpperLower, A, 81);   /* symmetric, small bump: indefinite */
+  dplasma_dplrnt(ctx, 0, B, 82);
+  double *a = malloc(sizeof(double) * n * n), *b = malloc(sizeof(double) * n * nrhs), *x = malloc(sizeof(double) * n * nrhs);
+  dplasma_desc_get_lapack(A, a, n);
+  dplasma_desc_get_lapack(B, b, n);
+  double *U = NULL;
+  CHECK(dplasma_dhebut(ctx, A, &U, level) == 0 && U != NULL, "dhebut: %s", dplasma_last_error());
+  int info = dplasma_dhetrf(ctx, A);
+  CHECK(info == 0, "dhetrf after hebut: info %d (%s)", info, dplasma_last_error());
+  CHECK(dplasma_dhetrs(ctx, dplasmaLower, A, B, U, level) == 0, "dhetrs with butterfly: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(B, x, n);
+  double err = 0, bn = 0, xn = 0;
+  for (int c = 0; c < nrhs; ++c)
+    for (int i = 0; i < n; ++i) {
+      double s = 0;
+      for (int k = 0; k < n; ++k) s += a[i + (size_t)k * n] * x[k + (size_t)c * n];
+      err = fmax(err, fabs(s - b[i + (size_t)c * n]));
+      bn = fmax(bn, fabs(b[i + (size_t)c * n]));
+      xn = fmax(xn, fabs(x[i + (size_t)c * n]));
+    }
+  printf("dhebut + dhetrf + dhetrs (butterfly depth %d) n=%d: ||Ax-b||/||b|| %.3e (|x| %.3e)\n", level, n, err / bn, xn);
+  CHECK(err / bn < 1e-8, "butterfly solve residual %.3e", err / bn);
+  free(U), free(a), free(b), free(x);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(B);
+}
+
 int main(int argc, char **argv) {
   setvbuf(stdout, NULL, _IONBF, 0);
   signal(SIGSEGV, on_fault);
@@ -1358,6 +1389,7 @@ int main(int argc, char **argv) {
   test_latms(ctx);
   test_posv_not_spd(ctx);
   test_pltmg(ctx);
+  test_butterfly(ctx);
   /* an operation without a native implementation fails cleanly */
   dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
   CHECK(dplasma_dhbrdt(ctx, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");

@@ -183,7 +183,6 @@ NATIVE_EXT = {
     "trsmpl_ptgpanel": lambda pc: f"nat_trsmpl_ptgpanel(ctx, {pc}, A, IPIV, B)",
     "trsmpl_incpiv": lambda pc: f"nat_trsmpl_incpiv(ctx, {pc}, A, L, IPIV, B)",
     "hetrf": lambda pc: f"nat_hetrf(ctx, {pc}, A)",
-    "hetrs": lambda pc: f"nat_hetrs(ctx, {pc}, uplo, A, B, U_but_vec, level)",
     "trdsm": lambda pc: f"nat_trdsm(ctx, {pc}, A, B)",
     "trmdm": lambda pc: f"nat_trmdm(ctx, {pc}, A)",
 }
@@ -191,6 +190,9 @@ NATIVE_EXT = {
 NATIVE_EXT_DIRECT = {
     "lanm2": lambda pc: f"nat_lanm2(ctx, {pc}, A, info)",
     "print": lambda pc: f"nat_print(ctx, {pc}, uplo, A)",
+    "hetrs": lambda pc: f"nat_hetrs(ctx, {pc}, uplo, A, B, U_but_vec, level)",
+    "gebmm": lambda pc: f"nat_gebmm(ctx, {pc}, A, U_but_vec, level, trans)",
+    "gebut": lambda pc: f"nat_gebut(ctx, {pc}, A, U_but_vec, level)",
     "pltmg": lambda pc: f"nat_pltmg(ctx, {pc}, mtxtype, A, seed)",
     "latms": lambda pc: f"nat_latms(ctx, {pc}, mtxtype, cond, A, seed)",
 }
@@ -286,7 +288,8 @@ def gen_ext(h, cpp):
             # ---- wrappers
             conv = ", ".join(ext_conv(c, nm, p) for c, nm in args if c != "K")
             if op == "hebut":   # handle out: the framework returns the butterfly object
-                cpp.append(f'extern "C" DPL_CAPI {proto} {{ if (dpl_native(ctx)) return nat_unsupported("{p}{op}"); '
+                cpp.append(f'extern "C" DPL_CAPI {proto} {{ if (dpl_native(ctx)) return nat_hebut(ctx, {PCODE[p]}, A, '
+                           f'(void **)U_but_ptr, level); '
                            f'DplGil g; return dpl_call_obj_out(ctx, "x:{p}{op}", (void **)U_but_ptr, '
                            f'{{dpl_arg_desc(A), dpl_arg_int(level)}}); }}')
                 continue

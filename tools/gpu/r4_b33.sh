@@ -9,7 +9,7 @@ step() {
   echo "== $name" | tee -a $O/summary.log
   timeout -k 10 $to "$@" > $O/$name.log 2>&1
   local rc=$?
-  grep -E "passed|failed|error|Error|FAIL|dgeru|zgerc|dlaswp|dlanm2|dpltmg|dtrsmpl|dtrdsm|dtrmdm|hetrf|incpiv|A\(|dgetrs|dgesv|native C ABI" $O/$name.log | grep -v amdgpu.ids | tail -12 | tee -a $O/summary.log
+  grep -E "passed|failed|error|Error|FAIL|dgeru|zgerc|dlaswp|dlanm2|dpltmg|hebut|dtrsmpl|dtrdsm|dtrmdm|hetrf|incpiv|A\(|dgetrs|dgesv|native C ABI" $O/$name.log | grep -v amdgpu.ids | tail -12 | tee -a $O/summary.log
   echo "rc=$rc" | tee -a $O/summary.log
   return $rc
 }
