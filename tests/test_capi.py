@@ -298,3 +298,23 @@ def test_native_dist_example_gpu(tmp_path):
     print("\n".join(outs))
     assert all(p.returncode == 0 for p in procs), "\n".join(outs)
     assert "(ok)" in outs[0] and "[****] TIME(s)" in outs[0]
+
+
+def test_capi_ext_native_routing():
+    """Every EXT entry point the interpreter-free engine implements (tools/gen_capi.py NATIVE_EXT /
+    NATIVE_EXT_DIRECT, and hebut) dispatches to capi/native.cpp on a native context in the generated wrappers,
+    in all four precisions; the others refuse a native context by name."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        import gen_capi
+    finally:
+        sys.path.pop(0)
+    src = open(os.path.join(ROOT, "capi", "dplasma_ext.cpp")).read()
+    lines = {ln.split("(", 1)[0].split()[-1]: ln for ln in src.splitlines() if ln.startswith('extern "C"')}
+    native = set(gen_capi.NATIVE_EXT) | set(gen_capi.NATIVE_EXT_DIRECT) | {"hebut"}
+    for p in "sdcz":
+        for op in native:
+            ln = lines[f"dplasma_{p}{op}"]
+            assert "if (dpl_native(ctx)) return nat_" in ln and "nat_unsupported" not in ln, (p, op)
+        for op in ("heev", "getrf_qrf", "geqrf_param"):
+            assert f'nat_unsupported("{p}{op}")' in lines[f"dplasma_{p}{op}"], (p, op)
