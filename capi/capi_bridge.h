@@ -59,7 +59,7 @@ PyObject* dpl_arg_qrtree(const dplasma_qrtree_t* q);
 // an opaque framework object handed to C earlier (butterfly vectors): a new reference to it
 PyObject* dpl_arg_obj(const void* h);
 // "call" returning an object: stored as a new reference in *out (0), or -1
-int dpl_call_obj_out(dplasma_context_t* ctx, const char* name, void** out, std::initializer_list<PyObject*> args);
+int dpl_call_bytes_out(dplasma_context_t* ctx, const char* name, void** out, std::initializer_list<PyObject*> args);
 // tp_setter(tp, name, v): a taskpool parameter (dplasma_<p>potrf_setrecursive, ...)
 void dpl_tp_setter(dplasma_taskpool_t* tp, const char* name, int v);
 

@@ -11,6 +11,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 
 static PyObject* g_capi = nullptr;   // module dplasma_amd.capi
@@ -152,12 +153,29 @@ PyObject* dpl_arg_obj(const void* h) {
   return o;
 }
 
-int dpl_call_obj_out(dplasma_context_t* ctx, const char* name, void** out, std::initializer_list<PyObject*> args) {
+// a framework call that returns bytes: copied into a malloc'd array the caller owns (free / dplasma_but_free)
+int dpl_call_bytes_out(dplasma_context_t* ctx, const char* name, void** out, std::initializer_list<PyObject*> args) {
   g_err.clear();
   PyObject* r = call_obj(ctx, "call_obj", name, args);
   if (!r) return -1;
-  if (out) *out = r;   // the caller owns the reference (dplasma_but_free)
-  else Py_DECREF(r);
+  char* src = nullptr;
+  Py_ssize_t len = 0;
+  if (PyBytes_AsStringAndSize(r, &src, &len) != 0) {
+    PyErr_Clear();
+    Py_DECREF(r);
+    g_err = std::string(name) + ": the framework did not return a byte vector";
+    return -1;
+  }
+  void* v = std::malloc(len > 0 ? (size_t)len : 1);
+  if (!v) {
+    Py_DECREF(r);
+    g_err = std::string(name) + ": host allocation failed";
+    return -1;
+  }
+  std::memcpy(v, src, (size_t)len);
+  Py_DECREF(r);
+  if (out) *out = v;
+  else std::free(v);
   return 0;
 }
 
@@ -283,11 +301,8 @@ DPL_CAPI void dplasma_qrtree_print_perm(dplasma_desc_t* A, dplasma_qrtree_t* q, 
 DPL_CAPI void dplasma_qrtree_print_next_k(dplasma_desc_t* A, dplasma_qrtree_t* q, int k) { qt_print(A, q, "next_k", k, nullptr, nullptr); }
 DPL_CAPI void dplasma_qrtree_print_prev_k(dplasma_desc_t* A, dplasma_qrtree_t* q, int k) { qt_print(A, q, "prev_k", k, nullptr, nullptr); }
 DPL_CAPI void dplasma_qrtree_print_geqrt_k(dplasma_desc_t* A, dplasma_qrtree_t* q, int k) { qt_print(A, q, "geqrt_k", k, nullptr, nullptr); }
-DPL_CAPI void dplasma_but_free(void* h) {
-  if (!h) return;
-  DplGil g;
-  Py_DECREF((PyObject*)h);
-}
+// hebut's vector is a plain malloc'd array on native and framework contexts alike
+DPL_CAPI void dplasma_but_free(void* h) { std::free(h); }
 }  // extern "C"
 
 dplasma_taskpool_t* dpl_call_new(dplasma_context_t* ctx, const char* name, std::initializer_list<PyObject*> args) {

@@ -1370,7 +1370,7 @@ int add_panel_lu(NatProgram& P, int prec, char* pv, int ld, int m, int c0, int n
   prev = add_panel_lu(P, prec, pv, ld, m, c0, n1, S, info, info_base, prev, pivot);
   if (prev < 0) return prev;
   if (pivot)
-    prev = P.task(1, [=](hipStream_t s) { return dpl_laswp_panel(prec, pv, ld, c1, c0 + n, piv, c0, c1, s); }, {prev});
+    prev = P.task(1, [=](hipStream_t s) { return dpl_laswp_panel(prec, pv, ld, m, c1, c0 + n, piv, c0, c1, info, s); }, {prev});
   auto tr = std::make_shared<Trsm1>();
   tr->tri = c0 + (long long)c0 * ld;
   tr->add(c0 + (long long)c1 * ld, n1, n - n1);
@@ -1389,7 +1389,7 @@ int add_panel_lu(NatProgram& P, int prec, char* pv, int ld, int m, int c0, int n
   }
   prev = add_panel_lu(P, prec, pv, ld, m, c1, n - n1, S, info, info_base, prev, pivot);
   if (prev < 0 || !pivot) return prev;
-  return P.task(1, [=](hipStream_t s) { return dpl_laswp_panel(prec, pv, ld, c0, c1, piv, c1, c0 + n, s); }, {prev});
+  return P.task(1, [=](hipStream_t s) { return dpl_laswp_panel(prec, pv, ld, m, c0, c1, piv, c1, c0 + n, info, s); }, {prev});
 }
 
 bool lu_scratch(NatProgram& P, const NatDesc& A, LuScratch& S) {
@@ -1427,10 +1427,16 @@ int add_row_moves(NatProgram& P, const NatDesc& B, const LuScratch& S, const Dev
   int *dst = (int*)S.mdst->p, *src = (int*)S.msrc->p, *cnt = (int*)S.mcnt->p;
   const long long *ro = (const long long*)rowoff->p, *co = (const long long*)coloff->p;
   const int* nc = (const int*)ncols->p;
-  prev = P.task(1, [=](hipStream_t s) { return dpl_piv_moves(piv, kmin, dst, src, cnt, s); }, {prev});
+  // an out-of-range pivot: info -1001 (lu_piv.hip report_bad_pivot), nothing moved -- a solve program (getrs,
+  // laswp) gets an info word for it, so the caller sees a failure instead of a silently wrong result
+  if (!P.info) P.info = dev_alloc(sizeof(int), true);
+  if (!P.info) return -2;
+  int* info = (int*)P.info->p;
+  const int mrel = B.m - r0;
+  prev = P.task(1, [=](hipStream_t s) { return dpl_piv_moves(piv, kmin, mrel, dst, src, cnt, info, s); }, {prev});
   return P.task(1, [=](hipStream_t s) {
     return dpl_rows_permute(prec, b, ld, mb, r0, ro, mt, co, nc, nt, nb, inverse ? src : dst, inverse ? dst : src, cnt,
-                            maxcnt, s);
+                            maxcnt, info, s);
   }, {prev});
 }
 
@@ -1467,7 +1473,7 @@ bool add_getrf(NatProgram& P, NatDesc& A, NatDesc* IP, int& last) {
     if (kb > kmin) {   // wide last panel: the columns past the last row get the swaps and U = L^-1 A
       const int* piv = (const int*)S.piv->p;
       if (pivot)
-        prev = P.task(1, [=](hipStream_t s) { return dpl_laswp_panel(prec, pvb, mp, kmin, kb, piv, 0, kmin, s); },
+        prev = P.task(1, [=](hipStream_t s) { return dpl_laswp_panel(prec, pvb, mp, mp, kmin, kb, piv, 0, kmin, info, s); },
                       {prev});
       auto tr = std::make_shared<Trsm1>();
       tr->tri = 0;
@@ -1659,7 +1665,7 @@ bool add_getrf_dist(NatProgram& P, NatDesc& A, NatDesc& IP) {
     prev = add_panel_lu(P, prec, pvb, mp, mp, 0, kmin, S, info, r0, prev);
     if (prev < 0) return false;
     if (kb > kmin) {
-      prev = P.task(1, [=](hipStream_t s) { return dpl_laswp_panel(prec, pvb, mp, kmin, kb, piv, 0, kmin, s); }, {prev});
+      prev = P.task(1, [=](hipStream_t s) { return dpl_laswp_panel(prec, pvb, mp, mp, kmin, kb, piv, 0, kmin, info, s); }, {prev});
       auto tr = std::make_shared<Trsm1>();
       tr->tri = 0;
       tr->add((long long)kmin * mp, kmin, kb - kmin);
@@ -2010,7 +2016,7 @@ int nat_hetrs(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* dA, dp
 // butterfly is a HOST array of levels x n values of A's precision (row l = the random diagonal R of level l,
 // entries exp(u / 10), u the plrnt values of seed 3872), as hebut returns it (malloc; the caller frees it).
 // Level l is block diagonal with 2^l butterflies W = 1/sqrt(2) [R0 R1; R0 -R1] of order n / 2^l; each level is
-// applied as one native GEMM with the (sparse) butterfly matrix stored dense.  One process.
+// one element-wise device pass (dpl_butterfly).  One process.
 static double but_val(const void* U, int prec, size_t e) {
   switch (prec) {
     case P_S: return ((const float*)U)[e];
@@ -2020,48 +2026,27 @@ static double but_val(const void* U, int prec, size_t e) {
   }
 }
 
-// A := B_l A (side LEFT) or A B_l (RIGHT), B_l transposed when tr
+// A := B_l A (side LEFT) or A B_l (RIGHT), B_l transposed when tr: one element-wise pass over A on the device
+// (csrc/kernels/butterfly.hip, O(m n); the reference's segment updates, src/cores/core_zhebut.c:21-46)
 static int but_apply(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA, const void* U, int l, bool tr, int side) {
   NatDesc* A = dA->nat;
   const int n = side == LEFT ? A->m : A->n;
-  const int size = n >> l, h = size / 2;
-  const double s2 = 1.0 / std::sqrt(2.0);
-  std::vector<char> hb((size_t)n * n * A->es, 0);
-  auto put = [&](long long I, long long J, double v) {
-    if (tr) std::swap(I, J);
-    char* e = &hb[((size_t)I + (size_t)J * n) * A->es];
-    if (prec == P_S || prec == P_C) {
-      const float f = (float)v;
-      std::memcpy(e, &f, sizeof f);
-    } else {
-      std::memcpy(e, &v, sizeof v);
-    }
-  };
+  const int size = n >> l;
+  if (size < 2) return 0;   // order / 2^l < 2: the level is the identity scaled by nothing -- reject upstream
+  std::vector<double> r(n);
   const size_t row = (size_t)l * n;
-  for (long long I = 0; I < n; ++I) {
-    const long long base = (I / size) * size, li = I % size;
-    const bool top = li < h;
-    const long long p = top ? li : li - h;
-    put(I, base + p, but_val(U, prec, row + std::min<long long>(base + p, n - 1)) * s2);
-    const double r1 = but_val(U, prec, row + std::min<long long>(base + h + p, n - 1)) * s2;
-    put(I, base + h + p, top ? r1 : -r1);
-  }
-  dplasma_desc_t* B = nat_desc(ctx, prec, A->mb, A->mb, n, n, 1, 1, nullptr, 0, 1);
-  dplasma_desc_t* T = nat_desc(ctx, prec, A->mb, A->nb, A->m, A->n, 1, 1, nullptr, 0, 1);
-  int rc = (B && T) ? 0 : -1;
-  double o2[2] = {1.0, 0.0}, z2[2] = {0.0, 0.0};
-  float of[2] = {1.0f, 0.0f}, zf[2] = {0.0f, 0.0f};
-  const bool dbl = prec == P_D || prec == P_Z;
-  const void* one = dbl ? (const void*)o2 : (const void*)of;
-  const void* zero = dbl ? (const void*)z2 : (const void*)zf;
-  if (rc == 0) rc = nat_desc_io(B, hb.data(), n, true);
-  if (rc == 0)
-    rc = nat_execute(ctx, side == LEFT ? nat_gemm(ctx, prec, NOTRANS, NOTRANS, one, B, dA, zero, T)
-                                       : nat_gemm(ctx, prec, NOTRANS, NOTRANS, one, dA, B, zero, T));
-  if (rc == 0) rc = nat_execute(ctx, nat_lacpy(ctx, prec, UPPERLOWER, T, dA));
-  for (dplasma_desc_t* d : {B, T})
-    if (d) nat_desc_free(d), delete d;
-  return rc;
+  for (int e = 0; e < n; ++e) r[e] = but_val(U, prec, row + e);
+  DevPtr rd = dev_upload(r);
+  if (!rd) return (fail(nullptr, "butterfly: device allocation failed"), -1);
+  NatCtx* c = ctx->nat;
+  hipStream_t st = c->st[0];
+  const int big = 1 << 30;
+  const int rc = dpl_butterfly(prec, side, tr ? TRANS : NOTRANS, A->m, A->n, size, (const double*)rd->p, A->data, 0,
+                               0, big, big, A->lld, st);
+  if (rc != 0) return (fail(nullptr, "butterfly: launch failed"), -1);
+  if (hipStreamSynchronize(st) != hipSuccess) return (fail(nullptr, "butterfly: device error"), -1);
+  (void)ctx;
+  return 0;
 }
 
 static bool but_ok(NatCtx* c, int prec, NatDesc* A, int n, const void* U, int level, const char* op) {

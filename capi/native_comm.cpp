@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <thread>
 #include <type_traits>
 
@@ -255,13 +256,22 @@ bool try_read(const std::string& path, void* data, size_t bytes) {
   return ok;
 }
 
+// Removes rendezvous files older than the transport timeout only: every hello / go / message file is named
+// by its session token, so a younger file (another job sharing the directory, or a peer of a restarted job
+// still draining) can never be taken for this session's and is left alone; "session" itself is rewritten
+// atomically, which a running job no longer reads.
 void remove_stale(const std::string& dir) {
+  const double max_age = timeout_s();
+  const time_t now = time(nullptr);
   if (DIR* d = opendir(dir.c_str())) {
     while (dirent* e = readdir(d)) {
       const std::string n = e->d_name;
-      if (n == "session" || n.rfind("hello.", 0) == 0 || n.rfind("go.", 0) == 0 || n.rfind("m.", 0) == 0 ||
-          n.rfind(".tmp.", 0) == 0)
-        std::remove((dir + "/" + n).c_str());
+      if (!(n == "session" || n.rfind("hello.", 0) == 0 || n.rfind("go.", 0) == 0 || n.rfind("m.", 0) == 0 ||
+            n.rfind(".tmp.", 0) == 0))
+        continue;
+      struct stat st {};
+      const std::string path = dir + "/" + n;
+      if (stat(path.c_str(), &st) == 0 && difftime(now, st.st_mtime) > max_age) std::remove(path.c_str());
     }
     closedir(d);
   }

@@ -166,7 +166,7 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
     }, deps);
   };
   const int nbk = (int)blocks.size();
-  std::vector<int> next_of(nbk, -1), nxt2_of(nbk, -1), rest_of(nbk, -1), last_xch_of(nbk, -1);
+  std::vector<int> next_of(nbk, -1), nxt2_of(nbk, -1), rest_of(nbk, -1), last_xch_of(nbk, -1), last0_of(nbk, -1);
   int xch_prev = -1;   // the latest communication-stream task
   for (int b = 0; b < nbk; ++b) {
     const int c0 = blocks[b].first, c1 = blocks[b].second;
@@ -176,6 +176,9 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
     // the slabs of block b were last read by block b-3's updates and sent by its exchanges
     const int slab_free = b >= NSLAB ? rest_of[b - NSLAB] : -1;
     const int slab_sent = b >= NSLAB ? last_xch_of[b - NSLAB] : -1;
+    // ... and by its panel-stream tasks (NEAR / NEXT of block b-3 read the same slabs): a rank with no panel or
+    // diagonal tile in blocks b-2 and b-1 has no other ordering between those reads and a write into the slab
+    const int slab_read = b >= NSLAB ? last0_of[b - NSLAB] : -1;
     for (int k = c0; k < c1; ++k) {
       const int kb = A.rows(k), own_k = A.owner(k, k);
       char* wb = slab(wbase, b, k);
@@ -192,7 +195,7 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
         t_diag = Pr->task(0, [=](hipStream_t s) {
           return hipMemcpy2DAsync(dst, (size_t)mb * es, base + dk * es, (size_t)ld * es, (size_t)kb * es, kb,
                                   hipMemcpyDeviceToDevice, s) == hipSuccess ? 0 : -1;
-        }, {t_potrf, slab_free, slab_sent});
+        }, {t_potrf, slab_free, slab_sent, slab_read});
       }
       // DIAG exchange: the factor to every other rank holding a panel tile of step k
       std::set<int> drc;
@@ -202,7 +205,7 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
       if (me == own_k)
         for (int r : drc) ds.push_back(NatMsg{r, sb + slot(k) * es, sbytes});
       if (drc.count(me)) dr.push_back(NatMsg{own_k, wb + slot(k) * es, sbytes});
-      const int t_xd = add_exchange(*Pr, ds, dr, {t_diag, slab_free, slab_sent, xch_prev});
+      const int t_xd = add_exchange(*Pr, ds, dr, {t_diag, slab_free, slab_sent, slab_read, xch_prev});
       if (t_xd >= 0) xch_prev = t_xd;
       // TRSM of this rank's panel tiles against the factor, then pack them into their slots
       auto tr = std::make_shared<Trsm1>();
@@ -240,7 +243,7 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
           return dpl_trsm_rb(uplo, kb, L, ldl, zk, nrb, d->p, (double*)base, ld, s);
         }, {either(t_xd, t_diag), upd_in});
         t_pack = Pr->task(0, [=](hipStream_t s) { return pk->launch(prec, base, ld, sb, mb, s); },
-                          {t_trsm, slab_free, slab_sent});
+                          {t_trsm, slab_free, slab_sent, slab_read});
       } else if (!tr->it.empty()) {
         // the factor from the slab (the owner's copy or the received one), offset relative to the slabs' base
         const long long to = (long long)((wb - wbase) / es) + slot(k);
@@ -251,7 +254,7 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
           return tr->launch(prec, side, uplo, CONJTRANS, NONUNIT, one, wbase, mb, base, ld, s);
         }, {either(t_xd, t_diag), upd_in});
         t_pack = Pr->task(0, [=](hipStream_t s) { return pk->launch(prec, base, ld, sb, mb, s); },
-                          {t_trsm, slab_free, slab_sent});
+                          {t_trsm, slab_free, slab_sent, slab_read});
       }
       // PANEL exchange: tile i from its owner to the ranks whose trailing tiles read it (ascending i:
       // both sides of a pair enumerate their messages in the same order)
@@ -264,7 +267,7 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
           for (int r : cs) ps.push_back(NatMsg{r, sb + slot(i) * es, sbytes});
         if (cs.count(me) && (src != me || loop)) pr.push_back(NatMsg{src, wb + slot(i) * es, sbytes});
       }
-      const int t_xp = add_exchange(*Pr, ps, pr, {t_pack, t_xd, slab_free, slab_sent, xch_prev});
+      const int t_xp = add_exchange(*Pr, ps, pr, {t_pack, t_xd, slab_free, slab_sent, slab_read, xch_prev});
       if (t_xp >= 0) xch_prev = t_xp;
       last_xch_of[b] = xch_prev;
       // NEAR(k): the rest of this block with panel k (panel stream)
@@ -280,6 +283,7 @@ NatProgram* nat_dist_potrf(NatCtx* c, int uplo, NatDesc& A) {
     // NEXT(b) (critical): block b+1's columns; they are also written by NEXT2(b-1) and REST2(b-2)
     next_of[b] = gemm_task(0, upd(b, ks, c1, n1), {t_in, b >= 1 ? nxt2_of[b - 1] : -1, b >= 2 ? rest_of[b - 2] : -1});
     if (next_of[b] == -2) return fail(Pr, "potrf: device allocation failed");
+    last0_of[b] = last_task_on(*Pr, 0);   // the last panel-stream reader of block b's slabs
     nxt2_of[b] = gemm_task(1, upd(b, ks, n1, n2), {t_in});
     if (nxt2_of[b] == -2) return fail(Pr, "potrf: device allocation failed");
     rest_of[b] = gemm_task(1, upd(b, ks, n2, nt), {t_in});

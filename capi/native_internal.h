@@ -48,11 +48,14 @@ int dpl_ssssm(int prec, int nitems, const void* items, int max_n, int ib, int NB
 int dpl_tstrf(int prec, int nitems, const void* items, int ib, int NB, int max_m, int* info, hipStream_t st);
 int dpl_lu_block(int prec, void* A, int ld, int m, int c0, int cend, int* ipiv, void* ws, int* cnt, int* info,
                  int info_base, int pivot, hipStream_t st);
-int dpl_laswp_panel(int prec, void* A, int ld, int ca, int cb, const int* ipiv, int i0, int i1, hipStream_t st);
-int dpl_piv_moves(const int* ipiv, int kb, int* dst, int* src, int* cnt, hipStream_t st);
+int dpl_butterfly(int prec, int side, int trans, int m, int n, int size, const double* r, void* A, long long si,
+                  long long sj, int mb, int nb, int ld, hipStream_t st);
+int dpl_laswp_panel(int prec, void* A, int ld, int m, int ca, int cb, const int* ipiv, int i0, int i1, int* info,
+                    hipStream_t st);
+int dpl_piv_moves(const int* ipiv, int kb, int mrel, int* dst, int* src, int* cnt, int* info, hipStream_t st);
 int dpl_rows_permute(int prec, void* A, int ld, int mb, int r0, const long long* rowoff, int nrt,
                      const long long* coloff, const int* ncols, int nct, int nb, const int* dst, const int* src,
-                     const int* cnt, int maxcnt, hipStream_t st);
+                     const int* cnt, int maxcnt, int* info, hipStream_t st);
 int dpl_ipiv_shift(const int* in, int* out, int n, int delta, hipStream_t st);
 long long dpl_qr_panel_ws_bytes(int prec, int nc, int kf);
 int dpl_qr_panel(int prec, void* P, int ldp, int rbl, long long rstride, int M, int nc, int kf, void* V, int ldv,
@@ -237,13 +240,14 @@ struct NatProgram {
       for (size_t i = 0; i < tasks.size(); ++i)
         if (tasks[i].event && hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) return -1;
     }
+    // info is cleared before the join, so a task on any stream that writes it (tile factorisations, row
+    // moves reporting an out-of-range pivot) is ordered after the clear
+    if (info && hipMemsetAsync(info->p, 0, sizeof(int), ctx->st[0]) != hipSuccess) return -1;
     for (int s = 0; s < NAT_NSTREAM; ++s)
       if (hipEventRecord(ctx->join[s], ctx->st[s]) != hipSuccess) return -1;
     for (int s = 0; s < NAT_NSTREAM; ++s)
       for (int o = 0; o < NAT_NSTREAM; ++o)
         if (o != s && hipStreamWaitEvent(ctx->st[s], ctx->join[o], 0) != hipSuccess) return -1;
-    // info is written by panel-stream tasks only (tile factorisations)
-    if (info && hipMemsetAsync(info->p, 0, sizeof(int), ctx->st[0]) != hipSuccess) return -1;
     for (size_t i = 0; i < tasks.size(); ++i) {
       if (info && (int)i == gate) {
         int v = 0;

@@ -95,18 +95,22 @@ __device__ inline int xcc_id() {
 
 __device__ inline long long toff(long long si, long long sj, int i, int j) { return (long long)i * si + (long long)j * sj; }
 
-// readiness of task t, checked by a whole wave: lane q < nreq tests requirement q (one round trip for
-// the requirement records and one for the counters, instead of nreq serial ones on one lane)
+// readiness of task t, checked by a whole wave: lane q tests requirements q, q + 64, ... (one round trip
+// for the requirement records and one for the counters per 64 of them, instead of nreq serial ones on one
+// lane; an update by a run of nk panels has 1 + 2 nk requirements, so deep runs take several rounds)
 __device__ inline bool ready_wave(const DtrArgs& g, int t) {
   const int l = threadIdx.x & 63;
   const int rb = __builtin_amdgcn_readfirstlane(g.tasks[t].req_beg);
   const int nr = __builtin_amdgcn_readfirstlane((int)g.tasks[t].nreq);
-  bool ok = true;
-  if (l < nr) {
-    const int2 rq = g.reqs[rb + l];
-    ok = ld_sc1(g.cnt + rq.x) >= rq.y;
+  for (int q0 = 0; q0 < nr; q0 += 64) {
+    bool ok = true;
+    if (q0 + l < nr) {
+      const int2 rq = g.reqs[rb + q0 + l];
+      ok = ld_sc1(g.cnt + rq.x) >= rq.y;
+    }
+    if (__builtin_amdgcn_ballot_w64(!ok) != 0) return false;
   }
-  return __builtin_amdgcn_ballot_w64(!ok) == 0;
+  return true;
 }
 
 // one CAS claim attempt on a low list (wave 0): the task, -1 (head not ready), -2 (list exhausted)

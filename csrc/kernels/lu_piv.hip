@@ -198,10 +198,37 @@ __device__ int net_moves(const int* pv, int i0, int k, int* dst, int* src, int* 
   return n;
 }
 
+// An out-of-range pivot (a corrupt or stale ipiv entry) is never dereferenced: the launch that sees it
+// moves nothing and reports DPL_INFO_BAD_PIVOT through info (over 0 or a positive singular-column index,
+// never over another failure code) -- a silently skipped row would give a wrong factor with info 0.
+#define DPL_INFO_BAD_PIVOT (-1001)
+__device__ inline void report_bad_pivot(int* info) {
+  if (!info) return;
+  int old = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while (old >= 0) {
+    const int prev = atomicCAS(info, old, DPL_INFO_BAD_PIVOT);
+    if (prev == old) break;
+    old = prev;
+  }
+}
+
 // Sequential interchanges (fallback for i1 - i0 > 512): one thread per column replays the swaps.
 template <typename T>
-__global__ __launch_bounds__(64) void k_laswp_seq(T* __restrict__ A, int ld, int ca, int cb,
-                                                  const int* __restrict__ ipiv, int i0, int i1) {
+__global__ __launch_bounds__(64) void k_laswp_seq(T* __restrict__ A, int ld, int m, int ca, int cb,
+                                                  const int* __restrict__ ipiv, int i0, int i1, int* __restrict__ info) {
+  // every pivot is validated (i <= ipiv[i] < m) before any column moves: one bad entry -> no moves at all
+  __shared__ int bad;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  for (int i = i0 + threadIdx.x; i < i1; i += 64) {
+    const int p = ipiv[i];
+    if (p < i || p >= m) bad = 1;
+  }
+  __syncthreads();
+  if (bad) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) report_bad_pivot(info);
+    return;
+  }
   const int c = ca + blockIdx.x * 64 + threadIdx.x;
   if (c >= cb) return;
   T* col = A + (long long)c * ld;
@@ -218,15 +245,25 @@ __global__ __launch_bounds__(64) void k_laswp_seq(T* __restrict__ A, int ld, int
 // Interchanges rows i <-> ipiv[i], i in [i0, i1) (i1 - i0 <= 512), on columns [ca, cb) of the
 // panel: every workgroup derives the net moves in LDS (net_moves), then each wave moves its
 // columns -- all reads of a column land in LDS before its writes (no chain through memory).
+// Rows: [0, m); a pivot outside [i, m) stops the launch (report_bad_pivot).
 #define LSW_COLS 16
 template <typename T>
-__global__ __launch_bounds__(512) void k_laswp_panel(T* __restrict__ A, int ld, int ca, int cb,
-                                                     const int* __restrict__ ipiv, int i0, int i1) {
+__global__ __launch_bounds__(512) void k_laswp_panel(T* __restrict__ A, int ld, int m, int ca, int cb,
+                                                     const int* __restrict__ ipiv, int i0, int i1,
+                                                     int* __restrict__ info) {
   __shared__ int pv[512], mdst[1024], msrc[1024], wtot[8];
   __shared__ T vals[4][1024];
   const int k = i1 - i0, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < k; i += 512) pv[i] = ipiv[i0 + i];
-  __syncthreads();
+  int badl = 0;
+  for (int i = threadIdx.x; i < k; i += 512) {
+    const int p = ipiv[i0 + i];
+    pv[i] = p;
+    badl |= (p < i0 + i || p >= m);
+  }
+  if (__syncthreads_or(badl)) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) report_bad_pivot(info);
+    return;
+  }
   const int n = net_moves<512, 2>(pv, i0, k, mdst, msrc, wtot);
   if (w >= 4) return;
   for (int cc = w; cc < LSW_COLS; cc += 4) {
@@ -239,12 +276,25 @@ __global__ __launch_bounds__(512) void k_laswp_panel(T* __restrict__ A, int ld, 
 }
 
 // Net row moves of the sequential interchanges ipiv[0..kb) (panel-relative rows, kb <= 1024):
-// row dst[t] holds the former row src[t]; cnt[0] = number of moved rows (<= 2 kb).
-__global__ __launch_bounds__(1024) void k_piv_moves(const int* __restrict__ ipiv, int kb, int* __restrict__ dst,
-                                                    int* __restrict__ src, int* __restrict__ cnt) {
+// row dst[t] holds the former row src[t]; cnt[0] = number of moved rows (<= 2 kb).  Pivots must lie in
+// [i, mrel) (mrel: the rows below the panel's first one); otherwise cnt[0] = 0 (no moves) and info reports it.
+__global__ __launch_bounds__(1024) void k_piv_moves(const int* __restrict__ ipiv, int kb, int mrel,
+                                                    int* __restrict__ dst, int* __restrict__ src,
+                                                    int* __restrict__ cnt, int* __restrict__ info) {
   __shared__ int pv[1024], wtot[16];
-  for (int i = threadIdx.x; i < kb; i += 1024) pv[i] = ipiv[i];
-  __syncthreads();
+  int badl = 0;
+  for (int i = threadIdx.x; i < kb; i += 1024) {
+    const int p = ipiv[i];
+    pv[i] = p;
+    badl |= (p < i || p >= mrel);
+  }
+  if (__syncthreads_or(badl)) {
+    if (threadIdx.x == 0) {
+      cnt[0] = 0;
+      report_bad_pivot(info);
+    }
+    return;
+  }
   const int n = net_moves<1024, 2>(pv, 0, kb, dst, src, wtot);
   if (threadIdx.x == 0) cnt[0] = n;
 }
@@ -259,7 +309,8 @@ __global__ __launch_bounds__(256) void k_rows_move(T* __restrict__ A, int ld, in
                                                    const long long* __restrict__ rowoff, int nrt,
                                                    const long long* __restrict__ coloff, const int* __restrict__ ncols,
                                                    int nct, int nb, const int* __restrict__ rows,
-                                                   const int* __restrict__ cnt, T* __restrict__ buf, int ldb) {
+                                                   const int* __restrict__ cnt, T* __restrict__ buf, int ldb,
+                                                   int* __restrict__ info) {
   // lanes run along the move list (64 moves per wave): the staging buffer is column-major in t
   // and the moved rows are mostly runs of consecutive rows (the top kb rows), so both sides of
   // the copy coalesce; the 4 waves of a workgroup take different columns.
@@ -272,8 +323,10 @@ __global__ __launch_bounds__(256) void k_rows_move(T* __restrict__ A, int ld, in
   if (tin) {
     R = r0 + rows[t];
     rt = R / mb;
-    // a row outside the view (a corrupt or stale pivot) is skipped, never dereferenced
-    ro = (R >= 0 && rt < nrt) ? rowoff[rt] : -1;
+    // a row outside the view (a corrupt or stale pivot) is never dereferenced, and reported
+    const bool inview = R >= 0 && rt < nrt;
+    ro = inview ? rowoff[rt] : -1;
+    if (!inview && blockIdx.x == 0) report_bad_pivot(info);
   }
   const long long rbase = ro + (R % mb);
   const int W = nct * nb;
@@ -299,19 +352,25 @@ __global__ __launch_bounds__(256) void k_rows_permute(T* __restrict__ A, int ld,
                                                       const long long* __restrict__ coloff,
                                                       const int* __restrict__ ncols, int nct, int nb,
                                                       const int* __restrict__ dst, const int* __restrict__ src,
-                                                      const int* __restrict__ cnt) {
+                                                      const int* __restrict__ cnt, int* __restrict__ info) {
   __shared__ long long so[1024], dof[1024];
   __shared__ T vals[4][1024];
   const int n = min(cnt[0], 1024);
+  int badl = 0;
   for (int t = threadIdx.x; t < n; t += 256) {
     const int Rs = r0 + src[t], Rd = r0 + dst[t];
     const int ts = Rs / mb, td = Rd / mb;
     const long long bs = (Rs >= 0 && ts < nrt) ? rowoff[ts] : -1, bd = (Rd >= 0 && td < nrt) ? rowoff[td] : -1;
     const bool ok = bs >= 0 && bd >= 0;
+    badl |= !ok;
     so[t] = ok ? bs + Rs % mb : -1;
     dof[t] = ok ? bd + Rd % mb : -1;
   }
-  __syncthreads();
+  // one process: every moved row is local, so a missing one is a corrupt move list -- nothing moves
+  if (__syncthreads_or(badl)) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) report_bad_pivot(info);
+    return;
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int W = nct * nb;
   for (int c = blockIdx.x * 4 + w; c < W; c += gridDim.x * 4) {
@@ -742,50 +801,50 @@ DPL_API int dpl_lu_block(int prec, void* A, int ld, int m, int c0, int cend, int
   return (int)hipGetLastError();
 }
 
-DPL_API int dpl_laswp_panel(int prec, void* A, int ld, int ca, int cb, const int* ipiv, int i0, int i1,
-                            hipStream_t st) {
+DPL_API int dpl_laswp_panel(int prec, void* A, int ld, int m, int ca, int cb, const int* ipiv, int i0, int i1,
+                            int* info, hipStream_t st) {
   if (cb <= ca || i1 <= i0) return 0;
   if (i1 - i0 > 512) {
-    DISPATCH(prec, hipLaunchKernelGGL((k_laswp_seq<T>), dim3((cb - ca + 63) / 64), dim3(64), 0, st, (T*)A, ld, ca,
-                                      cb, ipiv, i0, i1));
+    DISPATCH(prec, hipLaunchKernelGGL((k_laswp_seq<T>), dim3((cb - ca + 63) / 64), dim3(64), 0, st, (T*)A, ld, m, ca,
+                                      cb, ipiv, i0, i1, info));
     return (int)hipGetLastError();
   }
   DISPATCH(prec, hipLaunchKernelGGL((k_laswp_panel<T>), dim3((cb - ca + LSW_COLS - 1) / LSW_COLS), dim3(512), 0, st,
-                                    (T*)A, ld, ca, cb, ipiv, i0, i1));
+                                    (T*)A, ld, m, ca, cb, ipiv, i0, i1, info));
   return (int)hipGetLastError();
 }
 
-DPL_API int dpl_piv_moves(const int* ipiv, int kb, int* dst, int* src, int* cnt, hipStream_t st) {
+DPL_API int dpl_piv_moves(const int* ipiv, int kb, int mrel, int* dst, int* src, int* cnt, int* info, hipStream_t st) {
   if (kb > 1024) return -3;
-  hipLaunchKernelGGL(k_piv_moves, dim3(1), dim3(1024), 0, st, ipiv, kb, dst, src, cnt);
+  hipLaunchKernelGGL(k_piv_moves, dim3(1), dim3(1024), 0, st, ipiv, kb, mrel, dst, src, cnt, info);
   return (int)hipGetLastError();
 }
 
 DPL_API int dpl_rows_move(int prec, int gather, void* A, int ld, int mb, int r0, const long long* rowoff, int nrt,
                           const long long* coloff, const int* ncols, int nct, int nb, const int* rows,
-                          const int* cnt, int maxcnt, void* buf, int ldb, hipStream_t st) {
+                          const int* cnt, int maxcnt, void* buf, int ldb, int* info, hipStream_t st) {
   if (nct <= 0 || maxcnt <= 0) return 0;
   const int W = nct * nb;
   const int gx = (W + 3) / 4 > 2048 ? 2048 : (W + 3) / 4;
   dim3 g(gx, (maxcnt + 63) / 64);
   if (gather) {
     DISPATCH(prec, hipLaunchKernelGGL((k_rows_move<T, true>), g, dim3(256), 0, st, (T*)A, ld, mb, r0, rowoff, nrt,
-                                      coloff, ncols, nct, nb, rows, cnt, (T*)buf, ldb));
+                                      coloff, ncols, nct, nb, rows, cnt, (T*)buf, ldb, info));
   } else {
     DISPATCH(prec, hipLaunchKernelGGL((k_rows_move<T, false>), g, dim3(256), 0, st, (T*)A, ld, mb, r0, rowoff, nrt,
-                                      coloff, ncols, nct, nb, rows, cnt, (T*)buf, ldb));
+                                      coloff, ncols, nct, nb, rows, cnt, (T*)buf, ldb, info));
   }
   return (int)hipGetLastError();
 }
 
 DPL_API int dpl_rows_permute(int prec, void* A, int ld, int mb, int r0, const long long* rowoff, int nrt,
                              const long long* coloff, const int* ncols, int nct, int nb, const int* dst,
-                             const int* src, const int* cnt, int maxcnt, hipStream_t st) {
+                             const int* src, const int* cnt, int maxcnt, int* info, hipStream_t st) {
   if (nct <= 0 || maxcnt <= 0) return 0;
   if (maxcnt > 1024) return -3;
   const int W = nct * nb;
   const int gx = (W + 3) / 4 > 4096 ? 4096 : (W + 3) / 4;
   DISPATCH(prec, hipLaunchKernelGGL((k_rows_permute<T>), dim3(gx), dim3(256), 0, st, (T*)A, ld, mb, r0, rowoff, nrt,
-                                    coloff, ncols, nct, nb, dst, src, cnt));
+                                    coloff, ncols, nct, nb, dst, src, cnt, info));
   return (int)hipGetLastError();
 }

@@ -354,27 +354,49 @@ def _x_trsmpl_qrf(new, p):
     return f
 
 
+# butterfly vectors cross the C ABI as the reference's raw host arrays: level x n values of the precision
+# (complex: (re, im) pairs, im = 0), malloc'd by the C side; the framework's own form is a (level, n) real tensor
+_BUT_CT = {"s": (ctypes.c_float, 1), "d": (ctypes.c_double, 1), "c": (ctypes.c_float, 2), "z": (ctypes.c_double, 2)}
+
+
+def _but_in(p, addr, level, n):
+    """The (level, n) float64 tensor of a caller's butterfly vector at address addr (None: no butterfly)."""
+    if not addr or level <= 0:
+        return None
+    ct, comp = _BUT_CT[p]
+    raw = np.ctypeslib.as_array((ct * (level * n * comp)).from_address(int(addr)))
+    return torch.from_numpy(raw[::comp].astype(np.float64).reshape(level, n).copy())
+
+
+def _but_out(p, U):
+    ct, comp = _BUT_CT[p]
+    v = U.detach().cpu().to(torch.float64).numpy().reshape(-1)
+    out = np.zeros(v.size * comp, dtype=np.float32 if ct is ctypes.c_float else np.float64)
+    out[::comp] = v
+    return out.tobytes()
+
+
 def _x_hebut(new, p):
     def f(ctx, A, level):
-        return getattr(_api, f"{p}hebut")(ctx, A, levels=int(level))
+        return _but_out(p, getattr(_api, f"{p}hebut")(ctx, A, levels=int(level)))
     return f
 
 
 def _x_hetrs(new, p):
-    def f(ctx, uplo, A, B, U_but, level):   # uplo / level: the butterfly carries its own depth
-        return getattr(_api, f"{p}hetrs")(ctx, A, B, U_but=U_but)
+    def f(ctx, uplo, A, B, U_but, level):
+        return getattr(_api, f"{p}hetrs")(ctx, A, B, U_but=_but_in(p, U_but, int(level), B.m))
     return f
 
 
 def _x_gebut(new, p):
     def f(ctx, A, U_but, level):
-        return getattr(_api, f"{p}gebut")(ctx, A, U_but)
+        return getattr(_api, f"{p}gebut")(ctx, A, _but_in(p, U_but, int(level), A.n))
     return f
 
 
 def _x_gebmm(new, p):
     def f(ctx, A, U_but, level, trans):
-        return getattr(_api, f"{p}gebmm")(ctx, A, U_but, trans)
+        return getattr(_api, f"{p}gebmm")(ctx, A, _but_in(p, U_but, int(level), A.m), trans)
     return f
 
 

@@ -14,8 +14,8 @@ panel kernel on a copy (U = D L^H), TRSM against L_kk^H, the rows of D are
 divided out by the diagonal-scaling kernel (``k_diag_scale``) while a copy
 W = L D feeds the MFMA GEMM update A(m,n) -= W(m,k) L(n,k)^H.  Butterflies are
 applied as distributed products with per-tile generated butterfly matrices
-(2 nonzeros per row) -- simple and grid-agnostic; ``N`` must be a multiple of
-2^levels.
+(2 nonzeros per row) on P x Q grids; on one process each level is one element-wise
+O(n^2) pass (``csrc/kernels/butterfly.hip``); ``N`` must be a multiple of 2^levels.
 """
 from __future__ import annotations
 
@@ -204,12 +204,24 @@ def _butterfly_descriptor(like, n, level, r, transpose=False):
     return Bm
 
 
+def _elementwise(A) -> bool:
+    """One process: each level is one element-wise pass (O(n^2), ops.butterfly -- the reference's HEBUT /
+    GEBUT / GEBMM segment updates, src/cores/core_zhebut.c:21-46).  On a P x Q grid the row / column
+    partners of a level live on other ranks; there the level is a distributed product with the
+    generated butterfly matrix (2 nonzeros per row)."""
+    return A.grid.P * A.grid.Q == 1
+
+
 def gebmm(ctx, A, U_but, trans=N_):
     """A := U A (trans = NoTrans) or U^T A (Trans/ConjTrans), U = B_0 B_1 ... B_{d-1} from U_but (dplasma_zgebmm)."""
     levels, n = U_but.shape
     if A.m != n:
         raise ValueError("butterfly order does not match A")
     order = range(levels - 1, -1, -1) if trans == N_ else range(levels)
+    if _elementwise(A):
+        for l in order:
+            ops.butterfly(A, U_but[l], n >> l, dplasmaLeft, trans)
+        return 0
     for l in order:
         Bm = _butterfly_descriptor(A, n, l, U_but[l], transpose=(trans != N_))
         T = A.like(name="T")
@@ -223,6 +235,10 @@ def gebut(ctx, A, U_but, V_but=None):
     V_but = U_but if V_but is None else V_but
     gebmm(ctx, A, U_but, dplasmaTrans)
     levels, n = V_but.shape
+    if _elementwise(A):
+        for l in range(levels):
+            ops.butterfly(A, V_but[l], n >> l, dplasmaRight, N_)
+        return 0
     for l in range(levels):
         Bm = _butterfly_descriptor(A, n, l, V_but[l])
         T = A.like(name="T")

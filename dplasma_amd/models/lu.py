@@ -430,7 +430,8 @@ class _GetrfDev:
         self.ipiv_all[r0: r0 + kmin].copy_(self.piv_dev[:kmin] + (r0 + 1))
         if self.tmp is not None:   # net moves of this step's interchanges (lists double-buffered by parity)
             par = k & 1
-            ops.piv_moves(self.piv_dev, kmin, self.mdst[par], self.msrc[par], self.mcnt[par])
+            ops.piv_moves(self.piv_dev, kmin, self.mdst[par], self.msrc[par], self.mcnt[par], mrel=self.A.m - r0,
+                          info=self.info)
 
     def _panel_dist(self, k):
         """Distributed partial pivoting of panel k on the GPUs of its process column (see panel_mode):
@@ -547,22 +548,22 @@ class _GetrfDev:
                     self.side.wait_event(ev)
                     cl, nc = self.coloff[:nl], self.ncols[:nl]
                     ops.rows_move(True, A.data, A.ld, A.mb, r0, self.rowoff, cl, nc, A.nb, msrc, mcnt, ldb,
-                                  self.tmp_l, ldb)
+                                  self.tmp_l, ldb, self.info)
                     ops.rows_move(False, A.data, A.ld, A.mb, r0, self.rowoff, cl, nc, A.nb, mdst, mcnt, ldb,
-                                  self.tmp_l, ldb)
+                                  self.tmp_l, ldb, self.info)
                     self.ev_side[par] = torch.cuda.Event()
                     self.ev_side[par].record(self.side)
             cr, nr = self.coloff[nl:], self.ncols[nl:]
             if g.P == 1 and self.inplace_moves and ldb <= 1024:
                 # one process: in-place permutation, no staging round trip through HBM
-                ops.rows_permute(A.data, A.ld, A.mb, r0, self.rowoff, cr, nr, A.nb, mdst, msrc, mcnt, ldb)
+                ops.rows_permute(A.data, A.ld, A.mb, r0, self.rowoff, cr, nr, A.nb, mdst, msrc, mcnt, ldb, self.info)
             else:
                 ops.rows_move(True, A.data, A.ld, A.mb, r0, self.rowoff, cr, nr, A.nb, msrc, mcnt, ldb, self.tmp,
-                              ldb)
+                              ldb, self.info)
                 if g.P > 1:
                     comm.allreduce(self.tmp, group=ctx.col_group)
                 ops.rows_move(False, A.data, A.ld, A.mb, r0, self.rowoff, cr, nr, A.nb, mdst, mcnt, ldb, self.tmp,
-                              ldb)
+                              ldb, self.info)
             if cur is not None and k == self.kt - 1:
                 for e in self.ev_side:                   # join: the factorisation ends with L final
                     if e is not None:
@@ -708,7 +709,11 @@ def _reduce_info(info: torch.Tensor) -> int:
     neg = torch.where(v < 0, v, torch.zeros_like(v))
     comm.allreduce(neg, op=torch.distributed.ReduceOp.MIN)
     if int(neg.item()) < 0:
-        raise RuntimeError(f"getrf: panel kernel failed on some rank (info={int(neg.item())}): the grid of "
+        code = int(neg.item())
+        if code == ops.BAD_PIVOT:
+            raise RuntimeError(f"getrf: an out-of-range pivot reached the row interchanges on some rank (info={code}):"
+                               " no row was moved by that step, the factorisation is invalid")
+        raise RuntimeError(f"getrf: panel kernel failed on some rank (info={code}): the grid of "
                            "the persistent panel kernel was not co-resident")
     big = torch.iinfo(torch.int64).max
     pos = torch.where(v > 0, v, torch.full_like(v, big))
@@ -806,6 +811,9 @@ def laswp(ctx, A, IPIV, inc=1):
     Any P x Q grid: rows crossing process rows move with one all-to-all per
     process column (_permute_rows_2d)."""
     piv = _gather_ipiv(ctx, IPIV) - 1
+    # an out-of-range pivot (i <= piv[i] < m violated) moves nothing and is reported, never wrapped around
+    if len(piv) > A.m or np.any(piv < np.arange(len(piv))) or np.any(piv >= A.m):
+        return ops.BAD_PIVOT
     perm = np.arange(A.m)
     seq = range(len(piv)) if inc > 0 else range(len(piv) - 1, -1, -1)
     for i in seq:
@@ -822,7 +830,9 @@ def laswp(ctx, A, IPIV, inc=1):
 
 def trsmpl_ptgpanel(ctx, A, IPIV, B):
     """B := L^-1 P B with the getrf_ptgpanel factors (dplasma_ztrsmpl_ptgpanel)."""
-    laswp(ctx, B, IPIV, 1)
+    rc = laswp(ctx, B, IPIV, 1)
+    if rc:
+        return rc
     blas3.trsm(ctx, dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, A, B)
     return 0
 
@@ -843,13 +853,18 @@ def gerfs(ctx, A, LU, IPIV, B, X, iters=2):
 def getrs(ctx, trans, A, IPIV, B):
     """Solve op(A) X = B with the getrf_1d factorization (A = P L U)."""
     if trans == N_:
-        laswp(ctx, B, IPIV, 1)
+        rc = laswp(ctx, B, IPIV, 1)
+        if rc:
+            return rc
         blas3.trsm(ctx, dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, A, B)
         blas3.trsm(ctx, dplasmaLeft, dplasmaUpper, N_, dplasmaNonUnit, 1.0, A, B)
     else:
+        piv = _gather_ipiv(ctx, IPIV) - 1
+        if len(piv) > B.m or np.any(piv < np.arange(len(piv))) or np.any(piv >= B.m):
+            return ops.BAD_PIVOT   # checked before the solves: B is left unchanged
         blas3.trsm(ctx, dplasmaLeft, dplasmaUpper, trans, dplasmaNonUnit, 1.0, A, B)
         blas3.trsm(ctx, dplasmaLeft, dplasmaLower, trans, dplasmaUnit, 1.0, A, B)
-        laswp(ctx, B, IPIV, -1)
+        return laswp(ctx, B, IPIV, -1)
     return 0
 
 

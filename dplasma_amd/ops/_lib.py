@@ -75,7 +75,8 @@ _SIGS = {
     # prec, A, ld, m, c0, cend, ipiv, ws, cnt, info, info_base, pivot, stream
     "dpl_lu_block": [c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp],
     # prec, A, ld, ca, cb, ipiv, i0, i1, stream
-    "dpl_laswp_panel": [c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp],
+    # prec, A, ld, m, ca, cb, ipiv, i0, i1, info (an out-of-range pivot: -1001, nothing moved), stream
+    "dpl_laswp_panel": [c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp],
     "dpl_lu_block_ws_bytes": [c_int],
     "dpl_debug_set_phase_mask": [c_int],
     "dpl_potrf_tile_set_kind": [c_int],
@@ -95,15 +96,17 @@ _SIGS = {
     "dpl_qr_panel_ws_bytes": [c_int, c_int, c_int],
     "dpl_qr_panel_max_rows": [],
     "dpl_qr_panel_set_prof": [c_vp],
-    # ipiv, kb, dst, src, cnt, stream
-    "dpl_piv_moves": [c_vp, c_int, c_vp, c_vp, c_vp, c_vp],
-    # prec, gather, A, ld, mb, r0, rowoff, nrt, coloff, ncols, nct, nb, rows, cnt, maxcnt, buf, ldb, stream
+    # ipiv, kb, mrel, dst, src, cnt, info, stream
+    "dpl_piv_moves": [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp],
+    # prec, gather, A, ld, mb, r0, rowoff, nrt, coloff, ncols, nct, nb, rows, cnt, maxcnt, buf, ldb, info, stream
     "dpl_rows_move": [c_int, c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp,
-                      c_int, c_vp, c_int, c_vp],
+                      c_int, c_vp, c_int, c_vp, c_vp],
     "dpl_stream_cumask": [c_vp, c_int, c_vp],
     "dpl_stream_destroy": [c_vp],
     "dpl_delay": [ctypes.c_double, c_int, c_vp],
     "dpl_ipiv_shift": [c_vp, c_vp, c_int, c_int, c_vp],
+    # random butterfly level (butterfly.hip): prec, side, trans, m, n, size, r, A, si, sj, mb, nb, ld, stream
+    "dpl_butterfly": [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp],
     "dpl_gemm_set_wg_cap": [c_int],
     "dpl_lu_block_set_kind": [c_int],   # pivoting block kernel: 1 register-resident rows, 0 LDS tile
     # distributed pivoting panel (lu_dist.hip): prec, A, ld, m, c0, cend, kbw, tr, diag, lrel, ipiv, ws, cnt,
@@ -118,7 +121,7 @@ _SIGS = {
     "dpl_xchg_free": [c_vp],
     "dpl_ipc_handle_bytes": [],
     "dpl_rows_permute": [c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp,
-                         c_int, c_vp],
+                         c_int, c_vp, c_vp],
 }
 _OPTIONAL = set()
 

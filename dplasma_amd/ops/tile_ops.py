@@ -14,6 +14,8 @@ raises.
 """
 from __future__ import annotations
 
+import math
+
 import numpy as np
 import torch
 
@@ -759,6 +761,49 @@ def diag_scale(part: int, cols: bool, D: torch.Tensor, ldd: int, B: torch.Tensor
         b.copy_(torch.where(_part_mask(it, m, n, p), new, b))
 
 
+# ----------------------------------------------------------------------------- random butterflies
+def butterfly(A, r: torch.Tensor, size: int, side: int, trans: int):
+    """One butterfly level on a one-process descriptor, element-wise O(m n) (csrc/kernels/butterfly.hip):
+    A := B A / B^T A (side Left) or A B / A B^T (Right), B block diagonal with blocks
+    1/sqrt(2) [R0 R1; R0 -R1] of order ``size``, R the real vector ``r`` (length = the order)."""
+    from ..descriptor import STORAGE_TILE
+    left = side == dplasmaLeft
+    m, n = A.m, A.n
+    order = m if left else n
+    if size < 2 or size % 2 or order % size:
+        raise ValueError("butterfly: size must be even and divide the order")
+    form = 0 if left == (trans == dplasmaNoTrans) else 1
+    if _is_gpu(A.data):
+        if A.storage == STORAGE_TILE:
+            si, sj = A.mb * A.nb, A.llmt * A.mb * A.nb
+        else:
+            si, sj = A.mb, A.nb * A.ld
+        base = A.offset(0, 0) if (A.mt and A.nt) else 0
+        rd = r.to(device=A.data.device, dtype=torch.float64).contiguous()
+        buf = A.data[base:]
+        rc = _lib.load().dpl_butterfly(_lib.prec_code(A.dtype), side, trans, m, n, size, rd.data_ptr(), buf.data_ptr(),
+                                       si, sj, A.mb, A.nb, A.ld, _lib.stream_ptr())
+        _lib.check(rc, "butterfly")
+        return
+    D = A.to_dense_local()
+    X = D if left else D.t()
+    h = size // 2
+    idx = torch.arange(order // 2)
+    i0 = (idx // h) * size + idx % h
+    i1 = i0 + h
+    rr = r.to(torch.float64).cpu()
+    s = 1.0 / math.sqrt(2.0)
+    r0 = rr[i0].to(D.dtype).view(-1, 1)
+    r1 = rr[i1].to(D.dtype).view(-1, 1)
+    x0, x1 = X[i0].clone(), X[i1].clone()
+    if form == 0:
+        a, b = r0 * x0, r1 * x1
+        X[i0], X[i1] = s * (a + b), s * (a - b)
+    else:
+        X[i0], X[i1] = s * r0 * (x0 + x1), s * r1 * (x0 - x1)
+    A.from_dense(D)
+
+
 # ----------------------------------------------------------------------------- device-pivoting LU
 QR_PANEL_MAXW = 256   # widest panel of the single-launch Householder panel kernel (qr_panel.hip QP_R)
 
@@ -961,16 +1006,36 @@ def lu_block(P: torch.Tensor, ld: int, m: int, c0: int, cend: int, ipiv: torch.T
             A[j + 1:, j + 1:cend] -= torch.outer(A[j + 1:, j], A[j, j + 1:cend])
 
 
-def laswp_panel(P: torch.Tensor, ld: int, ca: int, cb: int, ipiv: torch.Tensor, i0: int, i1: int):
-    """Sequential row interchanges i <-> ipiv[i] (i in [i0, i1)) on columns [ca, cb) of panel P."""
+BAD_PIVOT = -1001   # info code of an out-of-range pivot (csrc/kernels/lu_piv.hip report_bad_pivot)
+
+
+def _bad_pivot(info):
+    """Record BAD_PIVOT in info over 0 or a positive singular-column index (never over another failure)."""
+    if info is not None and int(info[0]) >= 0:
+        info[0] = BAD_PIVOT
+
+
+def _iptr(t):
+    return t.data_ptr() if t is not None else None
+
+
+def laswp_panel(P: torch.Tensor, ld: int, ca: int, cb: int, ipiv: torch.Tensor, i0: int, i1: int, m: int = None,
+                info: torch.Tensor = None):
+    """Sequential row interchanges i <-> ipiv[i] (i in [i0, i1)) on columns [ca, cb) of panel P (m rows).
+    A pivot outside [i, m) moves nothing and sets info to BAD_PIVOT."""
     if cb <= ca or i1 <= i0:
         return
+    m = (1 << 31) - 1 if m is None else int(m)
     if _is_gpu(P):
-        rc = _lib.load().dpl_laswp_panel(_lib.prec_code(P.dtype), P.data_ptr(), ld, ca, cb, ipiv.data_ptr(), i0, i1,
-                                         _lib.stream_ptr())
+        rc = _lib.load().dpl_laswp_panel(_lib.prec_code(P.dtype), P.data_ptr(), ld, m, ca, cb, ipiv.data_ptr(), i0, i1,
+                                         _iptr(info), _lib.stream_ptr())
         _lib.check(rc, "laswp_panel")
         return
-    nrow = int(ipiv[i0:i1].max()) + 1 if i1 > i0 else 0
+    pv = [int(x) for x in ipiv[i0:i1]]
+    if any(p < i0 + q or p >= m for q, p in enumerate(pv)):
+        _bad_pivot(info)
+        return
+    nrow = max(pv) + 1
     A = torch.as_strided(P, (max(nrow, i1), cb - ca), (1, ld), ca * ld)
     for i in range(i0, i1):
         p = int(ipiv[i])
@@ -980,12 +1045,19 @@ def laswp_panel(P: torch.Tensor, ld: int, ca: int, cb: int, ipiv: torch.Tensor, 
             A[p] = t
 
 
-def piv_moves(ipiv: torch.Tensor, kb: int, dst: torch.Tensor, src: torch.Tensor, cnt: torch.Tensor):
-    """Net row moves of the sequential interchanges ipiv[:kb]: row dst[t] receives former row src[t]."""
+def piv_moves(ipiv: torch.Tensor, kb: int, dst: torch.Tensor, src: torch.Tensor, cnt: torch.Tensor, mrel: int = None,
+              info: torch.Tensor = None):
+    """Net row moves of the sequential interchanges ipiv[:kb]: row dst[t] receives former row src[t].
+    Pivots must lie in [i, mrel); otherwise no moves (cnt = 0) and info = BAD_PIVOT."""
+    mrel = (1 << 31) - 1 if mrel is None else int(mrel)
     if _is_gpu(ipiv):
-        rc = _lib.load().dpl_piv_moves(ipiv.data_ptr(), kb, dst.data_ptr(), src.data_ptr(), cnt.data_ptr(),
-                                       _lib.stream_ptr())
+        rc = _lib.load().dpl_piv_moves(ipiv.data_ptr(), kb, mrel, dst.data_ptr(), src.data_ptr(), cnt.data_ptr(),
+                                       _iptr(info), _lib.stream_ptr())
         _lib.check(rc, "piv_moves")
+        return
+    if any(int(ipiv[i]) < i or int(ipiv[i]) >= mrel for i in range(kb)):
+        cnt[0] = 0
+        _bad_pivot(info)
         return
     cur = {}
     for i in range(kb):
@@ -1001,7 +1073,8 @@ def piv_moves(ipiv: torch.Tensor, kb: int, dst: torch.Tensor, src: torch.Tensor,
 
 
 def rows_permute(A: torch.Tensor, ld: int, mb: int, r0: int, rowoff: torch.Tensor, coloff: torch.Tensor,
-                 ncols: torch.Tensor, nb: int, dst: torch.Tensor, src: torch.Tensor, cnt: torch.Tensor, maxcnt: int):
+                 ncols: torch.Tensor, nb: int, dst: torch.Tensor, src: torch.Tensor, cnt: torch.Tensor, maxcnt: int,
+                 info: torch.Tensor = None):
     """In place, one process: A[r0 + dst[t], col c] := old A[r0 + src[t], col c] on the flattened local
     tile columns (coloff[j], ncols[j]) -- rows_move gather + scatter without the staging buffer."""
     nct = int(coloff.numel())
@@ -1010,17 +1083,23 @@ def rows_permute(A: torch.Tensor, ld: int, mb: int, r0: int, rowoff: torch.Tenso
     if _is_gpu(A):
         rc = _lib.load().dpl_rows_permute(_lib.prec_code(A.dtype), A.data_ptr(), ld, mb, r0, rowoff.data_ptr(),
                                           int(rowoff.numel()), coloff.data_ptr(), ncols.data_ptr(), nct, nb,
-                                          dst.data_ptr(), src.data_ptr(), cnt.data_ptr(), maxcnt, _lib.stream_ptr())
+                                          dst.data_ptr(), src.data_ptr(), cnt.data_ptr(), maxcnt, _iptr(info),
+                                          _lib.stream_ptr())
         _lib.check(rc, "rows_permute")
         return
+    n = int(cnt[0])
+    R = [r0 + int(x) for x in list(src[:n]) + list(dst[:n])]
+    if any(r < 0 or r // mb >= rowoff.numel() or int(rowoff[r // mb]) < 0 for r in R):
+        _bad_pivot(info)   # a corrupt move list: nothing moves (as the kernel)
+        return
     buf = torch.zeros(maxcnt * nct * nb, dtype=A.dtype, device=A.device)
-    rows_move(True, A, ld, mb, r0, rowoff, coloff, ncols, nb, src, cnt, maxcnt, buf, maxcnt)
-    rows_move(False, A, ld, mb, r0, rowoff, coloff, ncols, nb, dst, cnt, maxcnt, buf, maxcnt)
+    rows_move(True, A, ld, mb, r0, rowoff, coloff, ncols, nb, src, cnt, maxcnt, buf, maxcnt, info)
+    rows_move(False, A, ld, mb, r0, rowoff, coloff, ncols, nb, dst, cnt, maxcnt, buf, maxcnt, info)
 
 
 def rows_move(gather: bool, A: torch.Tensor, ld: int, mb: int, r0: int, rowoff: torch.Tensor, coloff: torch.Tensor,
               ncols: torch.Tensor, nb: int, rows: torch.Tensor, cnt: torch.Tensor, maxcnt: int, buf: torch.Tensor,
-              ldb: int):
+              ldb: int, info: torch.Tensor = None):
     """gather: buf[t, c] = A[r0 + rows[t], col c] (0 where the row is not local);
     scatter: A[r0 + rows[t], col c] = buf[t, c] where local.  Columns: the flattened local tile
     columns (coloff[j], ncols[j]); buf is column-major with leading dimension ldb."""
@@ -1031,13 +1110,16 @@ def rows_move(gather: bool, A: torch.Tensor, ld: int, mb: int, r0: int, rowoff: 
         rc = _lib.load().dpl_rows_move(_lib.prec_code(A.dtype), int(gather), A.data_ptr(), ld, mb, r0,
                                        rowoff.data_ptr(), int(rowoff.numel()), coloff.data_ptr(), ncols.data_ptr(),
                                        nct, nb, rows.data_ptr(), cnt.data_ptr(), maxcnt, buf.data_ptr(), ldb,
-                                       _lib.stream_ptr())
+                                       _iptr(info), _lib.stream_ptr())
         _lib.check(rc, "rows_move")
         return
     n = int(cnt[0])
     for t in range(n):
         R = r0 + int(rows[t])
-        ro = int(rowoff[R // mb]) if R // mb < rowoff.numel() else -1
+        inview = 0 <= R and R // mb < rowoff.numel()
+        if not inview:   # a corrupt move list: reported, never dereferenced
+            _bad_pivot(info)
+        ro = int(rowoff[R // mb]) if inview else -1
         for j in range(nct):
             w = int(ncols[j])
             if w == 0:
@@ -1096,7 +1178,7 @@ class PanelLU:
                 lu_block(P, ld, m, op[1], op[2], ipiv, ws, cnt, info, info_base, self.pivot)
             elif op[0] == "laswp":
                 if self.pivot:
-                    laswp_panel(P, ld, op[1], op[2], ipiv, op[3], op[4])
+                    laswp_panel(P, ld, op[1], op[2], ipiv, op[3], op[4], m=m, info=info)
             elif op[0] == "trsm":
                 trsm(dplasmaLeft, dplasmaLower, dplasmaNoTrans, dplasmaUnit, 1.0, P, ld, P, ld, op[1])
             else:

@@ -593,6 +593,15 @@ static void test_dgetrf(dplasma_context_t *ctx) {
            n, nb, err / bn);
     CHECK(err / bn < 1e-9, "getrf/getrs residual %.3e", err / bn);
   }
+  /* a corrupt pivot (past the last row) is reported by the row-move kernels (info -1001), never dereferenced:
+   * dgetrs fails and names it */
+  ipiv[300] = n + 40;
+  dplasma_desc_set_lapack(IP, ipiv, 1);
+  dplasma_desc_set_lapack(B, b, n);
+  CHECK(dplasma_dgetrs(ctx, dplasmaNoTrans, A, IP, B) != 0, "dgetrs accepted a pivot past the last row");
+  CHECK(strstr(dplasma_last_error(), "-1001") != NULL, "dgetrs corrupt pivot: unexpected error '%s'",
+        dplasma_last_error());
+  printf("dgetrs corrupt pivot -> %s\n", dplasma_last_error());
   free(a), free(lu), free(b), free(x), free(ipiv);
   dplasma_desc_destroy(A), dplasma_desc_destroy(B), dplasma_desc_destroy(IP);
 }

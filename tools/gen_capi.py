@@ -220,8 +220,8 @@ def ext_conv(code, nm, p):
         return f"dpl_arg_qrtree({nm})"
     if code == "P":
         return f"dpl_arg_ptr({nm})"
-    if code == "B":
-        return f"dpl_arg_obj((const void *){nm})"
+    if code == "B":   # the caller's host butterfly vector (level x n values of the precision), by address
+        return f"dpl_arg_u64((unsigned long long)(uintptr_t){nm})"
     raise ValueError(code)
 
 
@@ -265,8 +265,9 @@ def gen_ext(h, cpp):
           "void dplasma_qrtree_print_next_k(dplasma_desc_t *A, dplasma_qrtree_t *qrtree, int k);",
           "void dplasma_qrtree_print_prev_k(dplasma_desc_t *A, dplasma_qrtree_t *qrtree, int k);",
           "void dplasma_qrtree_print_geqrt_k(dplasma_desc_t *A, dplasma_qrtree_t *qrtree, int k);",
-          "/* LDL^H butterflies: hebut returns an opaque handle (not the reference's raw vector) that hetrs /",
-          " * gebut / gebmm take; release it with dplasma_but_free */",
+          "/* LDL^H butterflies: hebut returns, as the reference does, a malloc'd host vector of level x N values of",
+          " * the precision (row l = the random diagonal of level l; complex: imaginary parts 0) that hetrs / gebut /",
+          " * gebmm take, on native and framework contexts alike; release it with free() or dplasma_but_free */",
           "void dplasma_but_free(void *U_but_vec);",
           "/* ---- further entry points (dplasma_z.h:106-349); on a native context they return an error, except",
           " * geru / gerc / laswp / lanm2 (run natively) */"]
@@ -287,10 +288,10 @@ def gen_ext(h, cpp):
                 h.append(f"void dplasma_{p}{op}_Destruct(dplasma_taskpool_t *tp);")
             # ---- wrappers
             conv = ", ".join(ext_conv(c, nm, p) for c, nm in args if c != "K")
-            if op == "hebut":   # handle out: the framework returns the butterfly object
+            if op == "hebut":   # vector out: the framework returns its bytes, copied into a malloc'd array
                 cpp.append(f'extern "C" DPL_CAPI {proto} {{ if (dpl_native(ctx)) return nat_hebut(ctx, {PCODE[p]}, A, '
                            f'(void **)U_but_ptr, level); '
-                           f'DplGil g; return dpl_call_obj_out(ctx, "x:{p}{op}", (void **)U_but_ptr, '
+                           f'DplGil g; return dpl_call_bytes_out(ctx, "x:{p}{op}", (void **)U_but_ptr, '
                            f'{{dpl_arg_desc(A), dpl_arg_int(level)}}); }}')
                 continue
             if args[0][0] == "K":
@@ -512,8 +513,8 @@ def main():
                 cpp.append(f"extern \"C\" DPL_CAPI void dplasma_{p}{op}_Destruct(dplasma_taskpool_t *tp) "
                            "{ dplasma_taskpool_free(tp); }")
     ext_cpp = ['// Generated by tools/gen_capi.py: the EXT entry points (QR-tree handles, caller arrays, butterfly',
-               '// handles, taskpool setters) forwarded to dplasma_amd.capi ("x:<p><op>").',
-               '#include "capi_bridge.h"', "#include <cmath>", "",
+               '// vectors, taskpool setters) forwarded to dplasma_amd.capi ("x:<p><op>").',
+               '#include "capi_bridge.h"', "#include <cmath>", "#include <cstdint>", "",
                'extern "C" void dplasma_taskpool_free(dplasma_taskpool_t *tp);']
     gen_ext(h, ext_cpp)
     (ROOT / "capi" / "dplasma_ext.cpp").write_text("\n".join(ext_cpp) + "\n")
