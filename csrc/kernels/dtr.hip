@@ -6,8 +6,9 @@
 // Why: a HIP stream priority does not give a kernel CU resources that another kernel holds.  Beside
 // the bulk trailing-update GEMM (2 workgroups x 72 KB LDS + 2 x 128 VGPR waves per SIMD on every CU),
 // the register-resident panel solve (256-VGPR waves) is not dispatched until the GEMM has drained
-// (tools/gpu/prio_probe.py, profiles/r4_prio_probe.txt: 0.30 ms alone, 15.7 ms beside a 15.3 ms
-// GEMM -- also with the GEMM capped to its resident 512 workgroups, so it is not the dispatch queue).
+// (tools/gpu/prio_probe.py, profiles/r4_prio_probe.txt: the panel TRSM takes 0.43 ms alone and 34.5 ms
+// beside a 34.3 ms GEMM -- also with the GEMM capped to its resident 512 workgroups, so it is not the
+// dispatch queue).
 // Here the panel work runs INSIDE the GEMM's resident workgroups: every workgroup, when it finishes a
 // task, takes the next ready task of the high-priority list (diagonal tile factorisation + inverse,
 // panel solve, look-ahead updates) before any bulk update.
