@@ -22,6 +22,9 @@
 //       the sequence overwrites)
 //   POTRF(k, b): row block b (32 rows) of the dataflow tile Cholesky (potrf_tile.h; 16 cooperating
 //       workgroups), then block column b of W_k (TRTRI below, same dataflow).
+//   SEND(i, k, r, dest) / SENDW(k, c, dest) (P x Q grids, models/potrf_dtr_dist.py): strip r of the
+//       solved panel tile (i, k) / column block c of W_k into rank dest's receive buffer / W, then one
+//       bump of dest's counter -- a remote strip is an arrival requirement of the consumer's tasks.
 // Dependencies are tile-version counters, not successor lists: each task lists (counter, target)
 // requirements (a 128x128 sub-tile's number of completed writes, a panel strip's "solved" mark, the
 // number of finished W_k block columns) and bumps one counter when done.  A list's head is claimed
@@ -36,47 +39,73 @@
 // Hand-offs between tasks (MI355X_MICROARCH.md, inter-workgroup visibility): producer -- every wave
 // s_waitcnt vmcnt(0), barrier, lane 0 agent release fence, s_waitcnt, relaxed agent atomic add;
 // consumer -- relaxed sc1 polls of the requirement counters, the claim, lane 0 agent acquire fence
-// + s_waitcnt, barrier.  Every wait is bounded (info = -1000, all workgroups drain).
+// + s_waitcnt, barrier.  Every wait is bounded (info = -1000, all workgroups drain).  Between processes
+// (one rank per GPU, peers' buffers IPC-mapped) the same with system scope: sc0 sc1 stores of the sent
+// bytes, a system release, a system-scope counter add on the peer; system-scope polls and acquire.
+//
+// Multi-rank modes (DtrArgs.nranks > 1): rank >= 0 -- this launch is one rank of a P x Q grid; rank = -1
+// -- EMULATION of the grid on one GPU: XCD x is rank x * nranks / 8's "GPU", every rank has its own tile
+// storage, receive buffers, W and counters, and time is dilated by nranks (a task's completion becomes
+// visible (nranks - 1) x its duration after it ends, through a per-counter visibility time; a send is
+// visible nranks x (lat + bytes / bw) after its rank pair's link frees up), so the span / nranks models
+// the grid's run on nranks GPUs (tools/emulate_potrf.py).
+#include <cstddef>
+#include <cstring>
+
 #include "gemm_tile.h"
 #include "potrf_tile.h"
 
 namespace {
 using namespace rbk;
 
-enum : int { T_UPD = 0, T_TRSM = 1, T_POTRF = 2 };
+enum : int { T_UPD = 0, T_TRSM = 1, T_POTRF = 2, T_SEND = 3, T_SENDW = 4 };
+constexpr int MAXR = 8;     // ranks of one launch (emulation) / of a grid (process mode)
 
 struct DtrTask {      // 32 bytes
   int type;
-  int i, j;           // UPD: tile (i, j); TRSM: tile (i, k0); POTRF: -
-  int k0;             // first panel (TRSM / POTRF: the panel)
+  int i, j;           // UPD: tile (i, j); TRSM: tile (i, k0); POTRF: -; SEND: tile row i, j = destination rank
+  int k0;             // first panel (TRSM / POTRF / SEND / SENDW: the panel)
   int req_beg;        // requirements [req_beg, req_beg + nreq): (counter, target) pairs
-  int inc;            // counter bumped on completion (-1: none)
-  short r, c;         // UPD: sub-tile; TRSM: strip r; POTRF: block row r
+  int inc;            // counter bumped on completion (-1: none); SEND / SENDW: on the destination rank
+  short r, c;         // UPD: sub-tile; TRSM / SEND: strip r; POTRF: block row r; SENDW: column block r
   short nk, nreq;     // UPD: panels in the run
 };
 static_assert(sizeof(DtrTask) == 32, "DtrTask layout");
 
 struct DtrArgs {
-  double* A;
-  long long ld;             // leading dimension of the tiles
-  long long si, sj;         // element offset of tile (i, j) = i * si + j * sj (LAPACK or TILE storage)
+  long long ld;             // leading dimension of every tile (local, received) -- 512: TILE storage
   int nt;
+  int nranks;               // 1: one process, one rank; > 1: grid (process mode or emulation)
+  int rank;                 // >= 0: this launch's rank; -1: emulation (rank from the XCD)
+  int epoch;
+  int flags;                // bit 0: steal a ready head of another XCD's list when the own head is not ready;
+                            // bit 1: WINDOWED high-list claims (see claim_hi_window), else tickets;
+                            // bits 8-15 / 16-23: how long a ticket holder polls before helping (see below)
+  int dil;                  // emulation: time dilation (= nranks); 1 otherwise
+  long long ncnt;           // counters per rank
   const DtrTask* tasks;
   const int2* reqs;
-  int* cnt;                 // version counters (zeroed per launch)
-  int* cur;                 // list cursors: [0] high, [1 + x] low list of XCD x; PSTRIDE ints apart
-  const int* hi;            // high list (task ids)
-  int nhi;
-  const int* lo;            // low lists, concatenated
+  const long long* tab;     // per rank nt x nt: element offset (from the rank's A) of tile (i, j) at i + j nt
+  const long long* xoff;    // per task: SEND / SENDW destination element offset (receive buffer / W)
+  int* cur;                 // cursors: [r] high list of rank r, [MAXR + x] low list of XCD x; PSTRIDE ints apart
+  int* claimed;             // windowed high-list claims (flags bit 1): one int per high-list position
+  const int* hi;            // high lists (task ids), rank r's at [hi_off[r], hi_off[r + 1])
+  int hi_off[MAXR + 1];
+  const int* lo;            // low lists, XCD x's at [lo_off[x], lo_off[x + 1])
   int lo_off[9];
-  double* W;                // nt x (512 x 512): W_k = L_kk^{-T}
+  double* A[MAXR];          // rank r's tile storage base (process mode: [rank] only)
+  double* recv[MAXR];       // rank r's receive buffer (process mode: IPC-mapped peers)
+  double* W[MAXR];          // rank r's W: nt x (512 x 512), W_k = L_kk^{-T}
+  int* cnt[MAXR];           // rank r's version / arrival counters (zeroed per launch)
+  unsigned long long* vis;  // emulation: per rank ncnt visibility times (100 MHz ticks)
+  unsigned long long* link; // emulation: MAXR x MAXR "link free at" times
+  long long bw_bpt;         // emulation: link bytes per tick (GB/s x 10)
+  long long lat_t;          // emulation: link latency (ticks)
   double* Mw;               // nt x MAXB x BLK     (M_k of the 32-blocks, potrf_tile.h)
   double* Sw;               // nt x MAXB x RB
   double* Lp;               // nt x MAXB x MAXB x BLK  (published L(b, m) blocks, T-layout)
   double* Wp;               // nt x MAXB x MAXB x BLK  (published W blocks, T-layout)
   int* prog;                // nt x 2 x MAXB x PSTRIDE: tile-step flags, then W-column flags
-  int epoch;
-  int flags;                // bit 0: steal a ready head of another XCD's list when the own head is not ready
   int* info;
   long long* trace;         // optional (DPLASMA_DTR_TRACE): per task {start, end, wg << 8 | xcd}, 100 MHz ticks
 };
@@ -94,20 +123,31 @@ __device__ inline int xcc_id() {
   return v & 7;
 }
 
-__device__ inline long long toff(long long si, long long sj, int i, int j) { return (long long)i * si + (long long)j * sj; }
+__device__ inline bool emul(const DtrArgs& g) { return g.rank < 0; }
+__device__ inline bool sysmode(const DtrArgs& g) { return g.rank >= 0 && g.nranks > 1; }
+template <typename T> __device__ inline T ld_sys(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ inline unsigned long long now_t() { return __builtin_amdgcn_s_memrealtime(); }
 
-// readiness of task t, checked by a whole wave: lane q tests requirements q, q + 64, ... (one round trip
-// for the requirement records and one for the counters per 64 of them, instead of nreq serial ones on one
-// lane; an update by a run of nk panels has 1 + 2 nk requirements, so deep runs take several rounds)
-__device__ inline bool ready_wave(const DtrArgs& g, int t) {
+// readiness of task t on rank rk, checked by a whole wave: lane q tests requirements q, q + 64, ... (one
+// round trip for the requirement records and one for the counters per 64 of them, instead of nreq serial
+// ones on one lane; an update by a run of nk panels has 1 + 2 nk requirements, so deep runs take several
+// rounds).  Emulation: a counter AT its target also needs that version's visibility time to have passed.
+__device__ inline bool ready_wave(const DtrArgs& g, int t, int rk) {
   const int l = threadIdx.x & 63;
   const int rb = __builtin_amdgcn_readfirstlane(g.tasks[t].req_beg);
   const int nr = __builtin_amdgcn_readfirstlane((int)g.tasks[t].nreq);
+  const int* cnt = g.cnt[rk];
+  const bool em = emul(g), sy = sysmode(g);
+  const unsigned long long now = em ? now_t() : 0;
   for (int q0 = 0; q0 < nr; q0 += 64) {
     bool ok = true;
     if (q0 + l < nr) {
       const int2 rq = g.reqs[rb + q0 + l];
-      ok = ld_sc1(g.cnt + rq.x) >= rq.y;
+      const int v = sy ? ld_sys(cnt + rq.x) : ld_sc1(cnt + rq.x);
+      ok = v >= rq.y;
+      if (ok && em && v == rq.y) ok = ld_sc1(g.vis + (size_t)rk * g.ncnt + rq.x) <= now;
     }
     if (__builtin_amdgcn_ballot_w64(!ok) != 0) return false;
   }
@@ -115,12 +155,12 @@ __device__ inline bool ready_wave(const DtrArgs& g, int t) {
 }
 
 // one CAS claim attempt on a low list (wave 0): the task, -1 (head not ready), -2 (list exhausted)
-__device__ inline int try_list(const DtrArgs& g, int* cur, const int* list, int n) {
+__device__ inline int try_list(const DtrArgs& g, int* cur, const int* list, int n, int rk) {
   for (int tries = 0; tries < 4; ++tries) {
     const int h = __builtin_amdgcn_readfirstlane(ld_sc1(cur));
     if (h >= n) return -2;
     const int t = __builtin_amdgcn_readfirstlane(list[h]);
-    if (!ready_wave(g, t)) return -1;
+    if (!ready_wave(g, t, rk)) return -1;
     int won = 0;
     if ((threadIdx.x & 63) == 0) won = atomicCAS(cur, h, h + 1) == h;
     if (__builtin_amdgcn_readfirstlane(won)) return t;
@@ -128,39 +168,132 @@ __device__ inline int try_list(const DtrArgs& g, int* cur, const int* list, int 
   return -1;
 }
 
-// wave 0: a ready task of the low lists -- its own XCD's list, another XCD's only once its own is
-// exhausted (-1 none ready yet, -2 every low list exhausted)
-__device__ inline int claim_low(const DtrArgs& g, int xcd) {
-  const int own = try_list(g, g.cur + PSTRIDE * (1 + xcd), g.lo + g.lo_off[xcd], g.lo_off[xcd + 1] - g.lo_off[xcd]);
+__device__ inline int try_xcd(const DtrArgs& g, int x, int rk) {
+  return try_list(g, g.cur + PSTRIDE * (MAXR + x), g.lo + g.lo_off[x], g.lo_off[x + 1] - g.lo_off[x], rk);
+}
+
+// wave 0: a ready task of the rank's low lists -- its own XCD's list, another of the rank's XCDs' only once
+// its own is exhausted (-1 none ready yet, -2 every low list of the rank exhausted).  x0, nx: the rank's XCDs.
+__device__ inline int claim_low(const DtrArgs& g, int xcd, int x0, int nx, int rk) {
+  const int own = try_xcd(g, xcd, rk);
   if (own >= 0) return own;
   if (own == -1) {
     if (!(g.flags & 1)) return -1;
     // flags bit 0: the own head waits on a dependency -- take a READY head of another XCD's list instead
     // (any claimed task is ready, so the deadlock-freedom argument is unchanged; L2 locality is traded away)
-    for (int d = 1; d < 8; ++d) {
-      const int x = (xcd + d) & 7;
-      const int t = try_list(g, g.cur + PSTRIDE * (1 + x), g.lo + g.lo_off[x], g.lo_off[x + 1] - g.lo_off[x]);
+    for (int d = 1; d < nx; ++d) {
+      const int t = try_xcd(g, x0 + (xcd - x0 + d) % nx, rk);
       if (t >= 0) return t;
     }
     return -1;
   }
   bool all_done = true;
-  for (int d = 1; d < 8; ++d) {
-    const int x = (xcd + d) & 7;
-    const int t = try_list(g, g.cur + PSTRIDE * (1 + x), g.lo + g.lo_off[x], g.lo_off[x + 1] - g.lo_off[x]);
+  for (int d = 1; d < nx; ++d) {
+    const int t = try_xcd(g, x0 + (xcd - x0 + d) % nx, rk);
     if (t >= 0) return t;
     if (t == -1) all_done = false;
   }
   return all_done ? -2 : -1;
 }
 
+// readiness of task t checked by ONE lane (its requirements one after the other): the windowed claim
+// evaluates 64 candidate tasks at once, one per lane
+__device__ inline bool ready_lane(const DtrArgs& g, int t, int rk) {
+  const DtrTask* tp = g.tasks + t;
+  const int rb = tp->req_beg, nr = tp->nreq;
+  const int* cnt = g.cnt[rk];
+  const bool em = emul(g), sy = sysmode(g);
+  const unsigned long long now = em ? now_t() : 0;
+  for (int q = 0; q < nr; ++q) {
+    const int2 rq = g.reqs[rb + q];
+    const int v = sy ? ld_sys(cnt + rq.x) : ld_sc1(cnt + rq.x);
+    if (v < rq.y) return false;
+    if (em && v == rq.y && ld_sc1(g.vis + (size_t)rk * g.ncnt + rq.x) > now) return false;
+  }
+  return true;
+}
+
+// WINDOWED claim on rank rk's high list (wave 0; flags bit 1): lane l looks at list position head + l and
+// the wave takes the FIRST unclaimed, ready one (CAS on its claim word), so a head that waits on a
+// dependency no longer holds up ready critical tasks behind it (the ticket scheme hands positions out in
+// order and only for a ready head).  A POTRF(k, b > 0) is eligible only once the entry before it -- its
+// group's block b - 1 -- is claimed: the 16 cooperating workgroups start in block order, so a running
+// block only ever waits for running blocks.  The head cursor skips the claimed prefix.  Progress: the
+// earliest unclaimed task of the topological order is the head of its list once its predecessors are
+// claimed, hence in the window.  Returns the task, -1 (nothing ready) or -2 (list exhausted).
+__device__ inline int claim_hi_window(const DtrArgs& g, int rk) {
+  const int l = threadIdx.x & 63;
+  int* hcur = g.cur + PSTRIDE * rk;
+  const int hbeg = g.hi_off[rk], hn = g.hi_off[rk + 1] - hbeg;
+  int* cl = g.claimed + hbeg;
+  const int* lst = g.hi + hbeg;
+  const int h = __builtin_amdgcn_readfirstlane(ld_sc1(hcur));
+  if (h >= hn) return -2;
+  const int q = h + l;
+  const bool in = q < hn;
+  const int t = in ? lst[q] : -1;
+  int c = in ? ld_sc1(cl + q) : 1;
+  const int cprev = __shfl_up(c, 1, 64);
+  bool rdy = in && c == 0 && ready_lane(g, t, rk);
+  if (rdy && g.tasks[t].type == T_POTRF && g.tasks[t].r > 0 && l > 0 && cprev == 0) rdy = false;
+  unsigned long long m = __builtin_amdgcn_ballot_w64(rdy);
+  int got = -1, gotl = -1;
+  while (m) {
+    const int L = __builtin_ctzll(m);
+    int won = 0;
+    if (l == L) won = atomicCAS(cl + q, 0, 1) == 0;
+    won = __builtin_amdgcn_readlane(won, L);
+    if (won) {
+      got = __builtin_amdgcn_readlane(t, L);
+      gotl = L;
+      break;
+    }
+    m &= m - 1;
+  }
+  // advance the head over the claimed prefix of the window
+  if (l == gotl) c = 1;
+  const unsigned long long un = __builtin_amdgcn_ballot_w64(c == 0);
+  const int f = un ? __builtin_ctzll(un) : 64;
+  if (f > 0 && l == 0) atomicCAS(hcur, h, h + f);
+  return got;
+}
+
+// tile offsets of rank rk (element offsets from g.A[rk]): local tiles and received copies
+__device__ inline long long tile_at(const long long* tab, int nt, int i, int j) { return tab[i + (long long)j * nt]; }
+
 struct UpdKs {   // k-run of an update: L(i,k) strip r, L(j,k) strip c, k in [k0, k0+nk)
-  long long si, sj;
-  int i, j, r, c, k0;
+  // the first four panels' operand offsets are looked up once, before the GEMM (scalar registers, selected
+  // by the uniform run index): a table load inside the software pipeline would stall it at every k-tile
+  // switch; deeper runs read the table for the rest
+  long long a0, a1, a2, a3, b0, b1, b2, b3;
+  const long long* tab;
+  int nt, i, j, r, c, k0;
+  __device__ void init(int nk) {
+    const long long ra = 128 * r, rb = 128 * c;
+    a0 = tile_at(tab, nt, i, k0) + ra;
+    b0 = tile_at(tab, nt, j, k0) + rb;
+    a1 = nk > 1 ? tile_at(tab, nt, i, k0 + 1) + ra : 0;
+    b1 = nk > 1 ? tile_at(tab, nt, j, k0 + 1) + rb : 0;
+    a2 = nk > 2 ? tile_at(tab, nt, i, k0 + 2) + ra : 0;
+    b2 = nk > 2 ? tile_at(tab, nt, j, k0 + 2) + rb : 0;
+    a3 = nk > 3 ? tile_at(tab, nt, i, k0 + 3) + ra : 0;
+    b3 = nk > 3 ? tile_at(tab, nt, j, k0 + 3) + rb : 0;
+    a0 = rfl64_(a0), a1 = rfl64_(a1), a2 = rfl64_(a2), a3 = rfl64_(a3);
+    b0 = rfl64_(b0), b1 = rfl64_(b1), b2 = rfl64_(b2), b3 = rfl64_(b3);
+  }
+  static __device__ long long rfl64_(long long v) {
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return (long long)(((unsigned long long)hi << 32) | lo);
+  }
   __device__ KPair operator()(int t) const {
     KPair p;
-    p.a_off = toff(si, sj, i, k0 + t) + 128 * r;
-    p.b_off = toff(si, sj, j, k0 + t) + 128 * c;
+    if (t < 4) {
+      p.a_off = t == 0 ? a0 : t == 1 ? a1 : t == 2 ? a2 : a3;
+      p.b_off = t == 0 ? b0 : t == 1 ? b1 : t == 2 ? b2 : b3;
+    } else {
+      p.a_off = tile_at(tab, nt, i, k0 + t) + 128 * r;
+      p.b_off = tile_at(tab, nt, j, k0 + t) + 128 * c;
+    }
     p.k = NBT;
     p.pad = 0;
     return p;
@@ -185,7 +318,7 @@ struct TrsmKs {  // strip r of tile (i, k) times column block c of W_k (rows [0,
 // for j = b-1 .. 0  (rows of L^{-1}: R_b = Z_b (E_b - sum_{m<b} L(b,m) R_m), transposed), Z_b = diag(S_b) M_b.
 // W_{j,m} comes from workgroup m, which publishes its block column in the order j = m, m-1, ..
 // (flag = epoch * 64 + blocks published), so the 16 workgroups run as a wavefront.
-__device__ void w_column(const DtrArgs& g, int k, int b, double* Vb) {
+__device__ void w_column(const DtrArgs& g, double* Wr, int k, int b, double* Vb) {
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int a = w >> 1, bh = w & 1;        // this wave's quadrant (row half a, column half bh)
   const int base = g.epoch * 64;
@@ -194,7 +327,7 @@ __device__ void w_column(const DtrArgs& g, int k, int b, double* Vb) {
   double* Lpk = g.Lp + (size_t)k * MAXB * MAXB * BLK;
   double* Wpk = g.Wp + (size_t)k * MAXB * MAXB * BLK;
   int* wprog = g.prog + ((size_t)k * 2 + 1) * MAXB * PSTRIDE;
-  double* Wk = g.W + (size_t)k * NBT * NBT;
+  double* Wk = Wr + (size_t)k * NBT * NBT;
   const int rho = 16 * a + (l & 15);
   // Z_b^T operand rows (M_b rows of the bh half) and the column scale S_b
   double ym[8], sc[4];
@@ -273,10 +406,11 @@ template <typename P> __device__ inline P* rflp(P* p) { return (P*)rfl64((long l
 
 // the task record and the argument fields a body uses, as wave-uniform (SGPR) values
 struct TaskU {
-  int i, j, k0, r, c, nk;
+  int i, j, k0, r, c, nk, nt;
   double* A;
-  long long ld, si, sj;
-  __device__ TaskU(const DtrArgs& g, int t) {
+  const long long* tab;
+  long long ld;
+  __device__ TaskU(const DtrArgs& g, int t, int rk) {
     const DtrTask tk = g.tasks[t];
     i = rfl(tk.i);
     j = rfl(tk.j);
@@ -284,32 +418,35 @@ struct TaskU {
     r = rfl(tk.r);
     c = rfl(tk.c);
     nk = rfl(tk.nk);
-    A = rflp(g.A);
+    nt = rfl(g.nt);
+    A = rflp(g.A[rk]);
+    tab = rflp(g.tab) + (size_t)rk * nt * nt;
     ld = rfl64(g.ld);
-    si = rfl64(g.si);
-    sj = rfl64(g.sj);
   }
 };
 
 // Task bodies: each is a separate (non-inlined) function, so its registers are allocated on its own
 // -- the GEMM body inlined into the task loop spilled (the capped persistent k_gemm_full spills the
 // same way: hipcc -Rpass-analysis=kernel-resource-usage, profiles/r4_dtr_regs.txt).
-__device__ __attribute__((noinline)) void run_upd(const DtrArgs* __restrict__ gp, int t) {
+__device__ __attribute__((noinline)) void run_upd(const DtrArgs* __restrict__ gp, int t, int rk) {
   const DtrArgs& g = *uni(gp);
-  const TaskU u(g, rfl(t));
+  const TaskU u(g, rfl(t), rfl(rk));
   __builtin_amdgcn_s_setprio(0);
-  const UpdKs ks{u.si, u.sj, u.i, u.j, u.r, u.c, u.k0};
+  UpdKs ks;
+  ks.tab = u.tab;
+  ks.nt = u.nt, ks.i = u.i, ks.j = u.j, ks.r = u.r, ks.c = u.c, ks.k0 = u.k0;
+  ks.init(u.nk);
   const int uplo = (u.i == u.j && u.r == u.c) ? 1 : 0;
   gemm_subtile<double, false, true>(g_lds, ks, u.nk, 0, 0, uplo, -1.0, u.A, (int)u.ld, u.A, (int)u.ld, 1.0,
-                                    u.A + toff(u.si, u.sj, u.i, u.j) + 128 * u.r + 128LL * u.c * u.ld, (int)u.ld);
+                                    u.A + tile_at(u.tab, u.nt, u.i, u.j) + 128 * u.r + 128LL * u.c * u.ld, (int)u.ld);
 }
 
-__device__ __attribute__((noinline)) void run_trsm(const DtrArgs* __restrict__ gp, int t) {
+__device__ __attribute__((noinline)) void run_trsm(const DtrArgs* __restrict__ gp, int t, int rk) {
   const DtrArgs& g = *uni(gp);
-  const TaskU u(g, rfl(t));
+  const TaskU u(g, rfl(t), rfl(rk));
   __builtin_amdgcn_s_setprio(2);
-  const long long ao = toff(u.si, u.sj, u.i, u.k0) + 128 * u.r;
-  const double* Wk = rflp(g.W) + (size_t)u.k0 * NBT * NBT;
+  const long long ao = tile_at(u.tab, u.nt, u.i, u.k0) + 128 * u.r;
+  const double* Wk = rflp(g.W[rfl(rk)]) + (size_t)u.k0 * NBT * NBT;
   for (int c = 3; c >= 0; --c) {
     const TrsmKs ks{ao, c};
     gemm_subtile<double, false, false>(g_lds, ks, 1, 0, 0, 0, 1.0, u.A, (int)u.ld, Wk, NBT, 0.0,
@@ -318,9 +455,10 @@ __device__ __attribute__((noinline)) void run_trsm(const DtrArgs* __restrict__ g
   }
 }
 
-__device__ __attribute__((noinline)) void run_potrf(const DtrArgs* __restrict__ gp, int t) {
+__device__ __attribute__((noinline)) void run_potrf(const DtrArgs* __restrict__ gp, int t, int rk) {
   const DtrArgs& g = *uni(gp);
   t = __builtin_amdgcn_readfirstlane(t);
+  rk = __builtin_amdgcn_readfirstlane(rk);
   const DtrTask tk = g.tasks[t];
   __builtin_amdgcn_s_setprio(RB_PRIO);
   const int k = tk.k0, b = tk.r;
@@ -331,10 +469,90 @@ __device__ __attribute__((noinline)) void run_potrf(const DtrArgs* __restrict__ 
   ws.prog = g.prog + (size_t)k * 2 * MAXB * PSTRIDE;
   ws.ticket = nullptr;
   ws.tbase = 0;
-  rb_tile_body<true>(g.A + toff(g.si, g.sj, k, k), NBT, (int)g.ld, g.info, k * NBT, ws, g.epoch, nullptr, b, g_lds,
-                     g_lds + BLK);
+  const long long* tab = g.tab + (size_t)rk * g.nt * g.nt;
+  rb_tile_body<true>(g.A[rk] + tile_at(tab, g.nt, k, k), NBT, (int)g.ld, g.info, k * NBT, ws, g.epoch, nullptr, b,
+                     g_lds, g_lds + BLK);
   __syncthreads();
-  w_column(g, k, b, g_lds);
+  w_column(g, g.W[rk], k, b, g_lds);
+}
+
+// 16-byte system-scope store (global_store_dwordx4 sc0 sc1: written through to the peer's memory)
+__device__ inline void st_sys_x2(double* p, double a, double b) {
+  typedef double d2_t __attribute__((ext_vector_type(2)));
+  const d2_t v = {a, b};
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+// copy rows x cols (column-major, both ld 512) from src to dst with the whole workgroup: 16-byte loads /
+// stores, 4 x 16 B in flight per thread; system-scope stores when the destination is a peer's memory
+__device__ inline void copy_block(double* __restrict__ dst, const double* __restrict__ src, int rows, int cols,
+                                  bool sys) {
+  typedef double d2_t __attribute__((ext_vector_type(2)));
+  const int tid = threadIdx.x;
+  const int hr = rows >> 1;                 // 16-byte pairs per column
+  const int n = hr * cols;
+  for (int e0 = tid; e0 < n; e0 += 4 * 256) {
+    d2_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * 256;
+      if (e < n) {
+        const int cc = e / hr, rr = 2 * (e % hr);
+        v[u] = *(const d2_t*)(src + rr + (long long)cc * NBT);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * 256;
+      if (e < n) {
+        const int cc = e / hr, rr = 2 * (e % hr);
+        double* d = dst + rr + (long long)cc * NBT;
+        if (sys) st_sys_x2(d, v[u][0], v[u][1]);
+        else *(d2_t*)d = v[u];
+      }
+    }
+  }
+}
+
+// SEND: strip r (128 x 512) of the solved panel tile (i, k0) into the destination's receive slot
+__device__ __attribute__((noinline)) void run_send(const DtrArgs* __restrict__ gp, int t, int rk) {
+  const DtrArgs& g = *uni(gp);
+  const TaskU u(g, rfl(t), rfl(rk));
+  __builtin_amdgcn_s_setprio(2);
+  const double* src = u.A + tile_at(u.tab, u.nt, u.i, u.k0) + 128 * u.r;
+  double* dst = rflp(g.recv[u.j]) + rfl64(g.xoff[rfl(t)]);
+  copy_block(dst, src, 128, NBT, sysmode(g));
+}
+
+// SENDW: column block c of W_k (rows [0, 128 (c + 1)), upper triangle + the zeros below it in the
+// diagonal block) into the destination's W
+__device__ __attribute__((noinline)) void run_sendw(const DtrArgs* __restrict__ gp, int t, int rk) {
+  const DtrArgs& g = *uni(gp);
+  const TaskU u(g, rfl(t), rfl(rk));
+  __builtin_amdgcn_s_setprio(2);
+  const long long o = rfl64(g.xoff[rfl(t)]);
+  const double* src = rflp(g.W[rfl(rk)]) + o;
+  double* dst = rflp(g.W[u.j]) + o;
+  copy_block(dst, src, 128 * (u.r + 1), 128, sysmode(g));
+}
+
+// Emulation: when the completion of task t (ran [t0, t1)) becomes visible -- (dil - 1) x its duration after
+// it ended; a send: dil x (lat + bytes / bw) after the (src, dst) link frees up (FIFO per ordered pair)
+__device__ inline unsigned long long emul_due(const DtrArgs& g, const DtrTask& tk, int rk, unsigned long long t0,
+                                              unsigned long long t1) {
+  if (tk.type != T_SEND && tk.type != T_SENDW)
+    return t1 + (unsigned long long)(g.dil - 1) * (t1 - t0);
+  const long long bytes = tk.type == T_SEND ? 128LL * NBT * 8 : 128LL * 128 * (tk.r + 1) * 8;
+  const unsigned long long dur = (unsigned long long)g.dil * (unsigned long long)(g.lat_t + bytes / g.bw_bpt);
+  unsigned long long* lk = g.link + rk * MAXR + tk.j;
+  unsigned long long old = __hip_atomic_load(lk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    const unsigned long long st = old > t1 ? old : t1;
+    const unsigned long long fin = st + dur;
+    if (__hip_atomic_compare_exchange_strong(lk, &old, fin, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT))
+      return fin;
+  }
 }
 
 // The arguments live in device memory and are re-read through a laundered pointer every iteration:
@@ -357,6 +575,22 @@ __global__ __launch_bounds__(256, 2) void k_dtr_potrf(const DtrArgs* __restrict_
   int ticket = -1;    // held high-list position (wave 0's copy)
   unsigned long long ticket_t0 = 0;
   bool hi_done = false, lo_done = false;
+  // this workgroup's rank and that rank's XCDs [x0, x0 + nx)
+  int rk, x0, nx;
+  {
+    const DtrArgs* gp = gargs;
+    asm volatile("" : "+s"(gp));
+    const int nr = gp->nranks, rr = gp->rank;
+    if (rr >= 0) {
+      rk = nr > 1 ? rr : 0;
+      x0 = 0;
+      nx = 8;
+    } else {
+      rk = xcd * nr / 8;
+      nx = 8 / nr;
+      x0 = rk * nx;
+    }
+  }
   for (;;) {
     const DtrArgs* gp = gargs;
     asm volatile("" : "+s"(gp));
@@ -366,38 +600,52 @@ __global__ __launch_bounds__(256, 2) void k_dtr_potrf(const DtrArgs* __restrict_
       if (ld_sc1(g.info) == -1000) {
         t = -2;
       } else {
-        if (ticket < 0 && !hi_done) {
+        int* hcur = g.cur + PSTRIDE * rk;
+        const int hbeg = g.hi_off[rk], hn = g.hi_off[rk + 1] - hbeg;
+        if ((g.flags & 2) && !hi_done) {
+          t = claim_hi_window(g, rk);
+          if (t == -2) {
+            hi_done = true;
+            t = -1;
+          }
+        } else if (ticket < 0 && !hi_done) {
           // a ticket only for a ready head: a workgroup holding a not-yet-ready critical task would run
           // low-list tasks meanwhile and come back up to one bulk task late -- the 16 POTRF workgroups of
           // a tile would then start spread over ~0.4 ms and wait for each other
-          const int h = __builtin_amdgcn_readfirstlane(ld_sc1(g.cur));
-          if (h >= g.nhi) {
+          const int h = __builtin_amdgcn_readfirstlane(ld_sc1(hcur));
+          if (h >= hn) {
             hi_done = true;
-          } else if (ready_wave(g, __builtin_amdgcn_readfirstlane(g.hi[h]))) {
+          } else if (ready_wave(g, __builtin_amdgcn_readfirstlane(g.hi[hbeg + h]), rk)) {
             int tk = 0;
-            if (tid == 0) tk = atomicAdd(g.cur, 1);
+            if (tid == 0) tk = atomicAdd(hcur, 1);
             tk = __builtin_amdgcn_readfirstlane(tk);
-            if (tk < g.nhi) {
+            if (tk < hn) {
               ticket = tk;
-              ticket_t0 = __builtin_amdgcn_s_memrealtime();
+              ticket_t0 = now_t();
             } else {
               hi_done = true;
             }
           }
         }
         bool help = true;
-        if (ticket >= 0) {
-          const int th = __builtin_amdgcn_readfirstlane(g.hi[ticket]);
-          if (ready_wave(g, th)) {
+        if (t < 0 && ticket >= 0) {
+          const int th = __builtin_amdgcn_readfirstlane(g.hi[hbeg + ticket]);
+          if (ready_wave(g, th, rk)) {
             t = th;
             ticket = -1;
-          } else if (__builtin_amdgcn_readfirstlane(g.tasks[th].type) == T_POTRF &&
-                     __builtin_amdgcn_s_memrealtime() - ticket_t0 < 5000ULL) {
-            help = false;   // a POTRF ticket polls for its first 50 us (the group starts together), then helps
+          } else {
+            // a ticket whose task is not ready yet polls for a while before it helps with a low-list task
+            // (which can hold it for a whole bulk update): POTRF tickets 50 us by default (the group starts
+            // together), other tickets not at all; flags bits 16-23 / 8-15 override (units of 10 us)
+            const unsigned fl = (unsigned)g.flags;
+            const bool is_potrf = __builtin_amdgcn_readfirstlane(g.tasks[th].type) == T_POTRF;
+            unsigned long long hold = is_potrf ? ((fl >> 16) & 255u) : ((fl >> 8) & 255u);
+            if (is_potrf && hold == 0) hold = 5;
+            if (now_t() - ticket_t0 < hold * 1000ULL * (unsigned long long)g.dil) help = false;
           }
         }
         if (t < 0 && help && !lo_done) {
-          t = claim_low(g, xcd);
+          t = claim_low(g, xcd, x0, nx, rk);
           if (t == -2) {
             lo_done = true;
             t = -1;
@@ -406,13 +654,17 @@ __global__ __launch_bounds__(256, 2) void k_dtr_potrf(const DtrArgs* __restrict_
         if (t < 0) t = (hi_done && lo_done && ticket < 0) ? -2 : -1;
       }
       if (t >= 0) {
-        if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the predecessors' bytes, fresh in this CU
+        // the predecessors' bytes, fresh in this CU (system scope: a peer process wrote some of them)
+        if (tid == 0) {
+          if (sysmode(g)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+          else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         idle0 = 0;
       } else if (t == -1 && tid == 0) {
-        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long now = now_t();
         if (idle0 == 0) idle0 = now;
-        else if (now - idle0 > 400000000ULL) {   // 4 s without a ready task: broken schedule, drain
+        else if (now - idle0 > 400000000ULL * (unsigned long long)g.dil) {   // 4 s (dilated) without a ready task: drain
           atomicExch(g.info, -1000);
           t = -2;
         }
@@ -429,25 +681,38 @@ __global__ __launch_bounds__(256, 2) void k_dtr_potrf(const DtrArgs* __restrict_
       continue;
     }
     nap = 1;
-    long long t_start = 0;
-    if (g.trace && tid == 0) t_start = (long long)__builtin_amdgcn_s_memrealtime();
+    const unsigned long long t_start = now_t();
     const DtrTask tk = g.tasks[t];
-    if (tk.type == T_UPD) run_upd(gp, t);
-    else if (tk.type == T_TRSM) run_trsm(gp, t);
-    else run_potrf(gp, t);
+    if (tk.type == T_UPD) run_upd(gp, t, rk);
+    else if (tk.type == T_TRSM) run_trsm(gp, t, rk);
+    else if (tk.type == T_POTRF) run_potrf(gp, t, rk);
+    else if (tk.type == T_SEND) run_send(gp, t, rk);
+    else run_sendw(gp, t, rk);
     // release: every wave's stores drained, then one agent-scope release and the counter bump
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0 && g.trace) {
       long long* tr = g.trace + 3 * (size_t)t;
-      tr[0] = t_start;
-      tr[1] = (long long)__builtin_amdgcn_s_memrealtime();
+      tr[0] = (long long)t_start;
+      tr[1] = (long long)now_t();
       tr[2] = ((long long)blockIdx.x << 8) | xcd;
     }
     if (tid == 0 && tk.inc >= 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(g.cnt + tk.inc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool remote = tk.type == T_SEND || tk.type == T_SENDW;
+      const int tr_ = remote ? tk.j : rk;
+      if (emul(g)) {
+        const unsigned long long due = emul_due(g, tk, rk, t_start, now_t());
+        __hip_atomic_fetch_max(g.vis + (size_t)tr_ * g.ncnt + tk.inc, due, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (remote && sysmode(g)) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(g.cnt[tr_] + tk.inc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(g.cnt[tr_] + tk.inc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
   __builtin_amdgcn_s_setprio(0);
@@ -465,20 +730,23 @@ DPL_API int dpl_dtr_potrf(const void* args_dev, int nwg, hipStream_t st) {
   hipLaunchKernelGGL(k_dtr_potrf, dim3(nwg), dim3(256), 0, st, (const DtrArgs*)args_dev);
   return (int)hipGetLastError();
 }
-// offsets of DtrArgs fields (the host packs the struct without a C compiler)
-DPL_API int dpl_dtr_args_layout(long long* off, int n) {
-  const long long v[] = {
-      (long long)offsetof(DtrArgs, A),      (long long)offsetof(DtrArgs, ld),     (long long)offsetof(DtrArgs, si),
-      (long long)offsetof(DtrArgs, sj),     (long long)offsetof(DtrArgs, nt),
-      (long long)offsetof(DtrArgs, tasks),  (long long)offsetof(DtrArgs, reqs),   (long long)sizeof(DtrTask),
-      (long long)offsetof(DtrArgs, cnt),    (long long)offsetof(DtrArgs, cur),    (long long)offsetof(DtrArgs, hi),
-      (long long)offsetof(DtrArgs, nhi),    (long long)offsetof(DtrArgs, lo),     (long long)offsetof(DtrArgs, lo_off),
-      (long long)offsetof(DtrArgs, W),      (long long)offsetof(DtrArgs, Mw),     (long long)offsetof(DtrArgs, Sw),
-      (long long)offsetof(DtrArgs, Lp),     (long long)offsetof(DtrArgs, Wp),     (long long)offsetof(DtrArgs, prog),
-      (long long)offsetof(DtrArgs, epoch),  (long long)offsetof(DtrArgs, info),   (long long)offsetof(DtrArgs, trace),
-      (long long)sizeof(DtrArgs),
-      (long long)MAXB, (long long)BLK, (long long)RB, (long long)PSTRIDE, (long long)offsetof(DtrArgs, flags)};
-  const int m = (int)(sizeof(v) / sizeof(v[0]));
-  for (int q = 0; q < n && q < m; ++q) off[q] = v[q];
-  return m;
+// offsets of DtrArgs fields by name (the host packs the struct without a C compiler): returns the offset of
+// field `name`, sizeof(DtrArgs) for "size", the layout constants for "MAXB" / "BLK" / "RB" / "PSTRIDE" /
+// "MAXR" / "task", or -1
+#define DTR_FIELD(f) if (!std::strcmp(name, #f)) return (long long)offsetof(DtrArgs, f);
+DPL_API long long dpl_dtr_field(const char* name) {
+  DTR_FIELD(ld) DTR_FIELD(nt) DTR_FIELD(nranks) DTR_FIELD(rank) DTR_FIELD(epoch) DTR_FIELD(flags) DTR_FIELD(dil)
+  DTR_FIELD(ncnt) DTR_FIELD(tasks) DTR_FIELD(reqs) DTR_FIELD(tab) DTR_FIELD(xoff) DTR_FIELD(cur) DTR_FIELD(hi)
+  DTR_FIELD(claimed)
+  DTR_FIELD(hi_off) DTR_FIELD(lo) DTR_FIELD(lo_off) DTR_FIELD(A) DTR_FIELD(recv) DTR_FIELD(W) DTR_FIELD(cnt)
+  DTR_FIELD(vis) DTR_FIELD(link) DTR_FIELD(bw_bpt) DTR_FIELD(lat_t) DTR_FIELD(Mw) DTR_FIELD(Sw) DTR_FIELD(Lp)
+  DTR_FIELD(Wp) DTR_FIELD(prog) DTR_FIELD(info) DTR_FIELD(trace)
+  if (!std::strcmp(name, "size")) return (long long)sizeof(DtrArgs);
+  if (!std::strcmp(name, "task")) return (long long)sizeof(DtrTask);
+  if (!std::strcmp(name, "MAXB")) return MAXB;
+  if (!std::strcmp(name, "BLK")) return BLK;
+  if (!std::strcmp(name, "RB")) return RB;
+  if (!std::strcmp(name, "PSTRIDE")) return PSTRIDE;
+  if (!std::strcmp(name, "MAXR")) return MAXR;
+  return -1;
 }

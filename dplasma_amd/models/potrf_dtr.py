@@ -27,8 +27,8 @@ when ``DPLASMA_POTRF_ENGINE=dtr`` (or ``auto`` and supported).
 """
 from __future__ import annotations
 
-import ctypes
 import os
+import struct
 from typing import List
 
 import numpy as np
@@ -84,9 +84,18 @@ class _Plan:
         # updates before the next column block's, so the first panel of a block does not wait behind the
         # whole previous bulk.  Both are subsequences of one topological order (column blocks ascending; in
         # a block, its low-list updates, then its high-list tasks), which the deadlock argument needs.
+        # "deadline": BOTH lists ordered by the step at which a task's output is first needed on the critical
+        # chain -- tile row i: an update of (i, j), i > j, and TRSM(i, k) feed TRSM(i, i-1) at step i - 1, the
+        # diagonal tile's updates feed POTRF(i) at step i -- then column, phase (diagonal updates, POTRF,
+        # other updates, TRSM), last panel.  One key for both lists, and a topological order: each task's
+        # inputs have a smaller deadline, or the same deadline and a smaller column or phase.  The column-
+        # major high list hands the tickets of a whole column's updates out before that column's first TRSM,
+        # which puts every row of a column on the critical chain (profiles/r5_dtr_dist_emulation.txt).
         lo_order = lo_order or os.environ.get("DPLASMA_DTR_LO_ORDER", "column")
-        if lo_order not in ("panel", "column"):
-            raise ValueError("DPLASMA_DTR_LO_ORDER must be panel or column")
+        if lo_order not in ("panel", "column", "deadline"):
+            raise ValueError("DPLASMA_DTR_LO_ORDER must be panel, column or deadline")
+        self.order = lo_order
+        dl = lo_order == "deadline"
         S = 4 * nt
         self.nt, self.S, self.D = nt, S, D
         # blocks of D panels; single panels once fewer than min_tiles columns remain (the chain-bound tail:
@@ -108,6 +117,7 @@ class _Plan:
         ver = np.zeros(S * S, dtype=np.int32)
         F = np.zeros((S, nt), dtype=np.int32)   # strip (I, k) solved: the value of its marker counter
         chunks, hi_parts, lo_parts = [], [], []
+        key_parts = []      # (ids, key padded to 6 columns): the list order key of every task
         ntask = [0]
 
         def sc(I, J):
@@ -121,6 +131,9 @@ class _Plan:
             ids = np.arange(ntask[0], ntask[0] + n, dtype=np.int64)
             ntask[0] += n
             chunks.append((t, reqs, nreq))
+            kk = np.zeros((n, 6), dtype=np.int64)
+            kk[:, :key.shape[1]] = key
+            key_parts.append(kk)
             if prio == "hi":
                 hi_parts.append((key, ids))
             else:
@@ -160,6 +173,11 @@ class _Plan:
                 reqs[:, 2 + 2 * q, 1] = np.where(diag, -1, F[4 * j + c, k])
             ver[Ci] += 1
             kl = k0 + nk - 1
+            if dl:
+                key = np.stack([np.where(i == j, i, i - 1), j, np.where(i == j, 0, 2), np.full(n, kl), r, c], 1)
+                if prio_hi:
+                    return emit(T_UPD, i, j, k0, r, c, nk, Ci, reqs, None, "hi", key=key)
+                return emit(T_UPD, i, j, k0, r, c, nk, Ci, reqs, None, "lo", key=key, xcd=j % 8)
             if prio_hi:
                 # key: column, phase (0 diagonal tile, 2 other rows), last panel, row, sub-tile
                 key = np.stack([j, np.where(i == j, 0, 2), np.full(n, kl), i, r, c], 1)
@@ -180,7 +198,10 @@ class _Plan:
                 reqs[:, :, 0] = dsc
                 reqs[:, :, 1] = ver[dsc]
                 b = np.arange(MAXB)
-                key = np.stack([np.full(MAXB, k), np.ones(MAXB, int), np.zeros(MAXB, int), b, b * 0, b * 0], 1)
+                if dl:
+                    key = np.stack([np.full(MAXB, k), np.full(MAXB, k), np.ones(MAXB, int), b * 0, b, b * 0], 1)
+                else:
+                    key = np.stack([np.full(MAXB, k), np.ones(MAXB, int), np.zeros(MAXB, int), b, b * 0, b * 0], 1)
                 emit(T_POTRF, np.full(MAXB, k), np.full(MAXB, k), k, b, 0, 0, WB + k, reqs, None, "hi", key=key)
                 if k + 1 < nt:
                     # TRSM(i, k, r): W_k complete and every update of strip r of tile (i, k)
@@ -195,7 +216,10 @@ class _Plan:
                     mark = sc(4 * ii + r, 4 * k)
                     ver[mark] += 1
                     F[4 * ii + r, k] = ver[mark]
-                    key = np.stack([np.full(n, k), np.full(n, 3), np.zeros(n, int), ii, r, r * 0], 1)
+                    if dl:
+                        key = np.stack([ii - 1, np.full(n, k), np.full(n, 3), np.zeros(n, int), r, r * 0], 1)
+                    else:
+                        key = np.stack([np.full(n, k), np.full(n, 3), np.zeros(n, int), ii, r, r * 0], 1)
                     emit(T_TRSM, ii, np.full(n, k), k, r, 0, 0, mark, reqs, None, "hi", key=key)
                 # NEAR(k): the rest of this block's columns, panel k alone
                 for j in range(k + 1, k1b):
@@ -244,38 +268,95 @@ class _Plan:
         self.lo_off = np.zeros(9, dtype=np.int64)
         self.lo_off[1:] = np.cumsum([len(x) for x in lo_lists])
         self.final_ver = ver
+        self.F = F                                   # strip (I, k) solved: the value of its marker counter
+        self.WB = WB
+        self.key = np.concatenate(key_parts)         # list order key per task (hi: column-major; lo: its list's)
+        self.is_hi = np.zeros(len(tasks), dtype=bool)
+        self.is_hi[self.hi] = True
+        self.block_of = block_of
 
 
-class _DtrArgs(ctypes.Structure):
-    _fields_ = [("A", ctypes.c_void_p), ("ld", ctypes.c_longlong), ("si", ctypes.c_longlong),
-                ("sj", ctypes.c_longlong), ("nt", ctypes.c_int), ("tasks", ctypes.c_void_p),
-                ("reqs", ctypes.c_void_p), ("cnt", ctypes.c_void_p), ("cur", ctypes.c_void_p),
-                ("hi", ctypes.c_void_p), ("nhi", ctypes.c_int), ("lo", ctypes.c_void_p),
-                ("lo_off", ctypes.c_int * 9), ("W", ctypes.c_void_p), ("Mw", ctypes.c_void_p),
-                ("Sw", ctypes.c_void_p), ("Lp", ctypes.c_void_p), ("Wp", ctypes.c_void_p),
-                ("prog", ctypes.c_void_p), ("epoch", ctypes.c_int), ("flags", ctypes.c_int), ("info", ctypes.c_void_p),
-                ("trace", ctypes.c_void_p)]
+class ArgsImage:
+    """Host image of the kernel's DtrArgs, packed by field name (offsets from dpl_dtr_field: the struct is
+    laid out by the device compiler, not mirrored here)."""
+
+    _LL = ("ld", "ncnt", "bw_bpt", "lat_t")
+    _INT = ("nt", "nranks", "rank", "epoch", "flags", "dil")
+    _PTR = ("tasks", "reqs", "tab", "xoff", "cur", "claimed", "hi", "lo", "vis", "link", "Mw", "Sw", "Lp", "Wp",
+            "prog", "info", "trace")
+    _PARR = ("A", "recv", "W", "cnt")
+    _IARR = ("hi_off", "lo_off")
+
+    def __init__(self, lib):
+        self.lib = lib
+        f = lambda n: int(lib.dpl_dtr_field(n.encode()))   # noqa: E731
+        self.size = f("size")
+        if f("task") != TASK_DT.itemsize:
+            raise RuntimeError("dtr: DtrTask layout mismatch")
+        self.off = {n: f(n) for n in self._LL + self._INT + self._PTR + self._PARR + self._IARR}
+        if min(self.off.values()) < 0:
+            raise RuntimeError("dtr: the kernel library lacks a DtrArgs field")
+        self.maxr = f("MAXR")
+        self.pstride = f("PSTRIDE")
+        self.buf = bytearray(self.size)
+
+    def set(self, name, v):
+        o = self.off[name]
+        if name in self._LL:
+            struct.pack_into("<q", self.buf, o, int(v))
+        elif name in self._INT:
+            struct.pack_into("<i", self.buf, o, int(v))
+        elif name in self._PTR:
+            struct.pack_into("<Q", self.buf, o, int(v or 0))
+        elif name in self._PARR:
+            vals = list(v) + [0] * (self.maxr - len(v))
+            struct.pack_into(f"<{self.maxr}Q", self.buf, o, *[int(x or 0) for x in vals])
+        else:
+            n = self.maxr + 1 if name == "hi_off" else 9
+            vals = list(v) + [v[-1]] * (n - len(v))
+            struct.pack_into(f"<{n}i", self.buf, o, *[int(x) for x in vals])
 
 
-def _check_layout(lib):
-    """The ctypes image must match the compiled DtrArgs (offsets reported by the library)."""
-    off = (ctypes.c_longlong * 32)()
-    n = lib.dpl_dtr_args_layout(off, 32)
-    names = ["A", "ld", "si", "sj", "nt", "tasks", "reqs", None, "cnt", "cur", "hi", "nhi", "lo", "lo_off", "W",
-             "Mw", "Sw", "Lp", "Wp", "prog", "epoch", "info", "trace"]
-    for q, nm in enumerate(names):
-        if nm is None:
-            if off[q] != TASK_DT.itemsize:
-                raise RuntimeError("dtr: DtrTask layout mismatch")
-            continue
-        if getattr(_DtrArgs, nm).offset != off[q]:
-            raise RuntimeError(f"dtr: DtrArgs.{nm} at {getattr(_DtrArgs, nm).offset}, library says {off[q]}")
-    if ctypes.sizeof(_DtrArgs) != off[len(names)]:
-        raise RuntimeError("dtr: DtrArgs size mismatch")
-    PST = int(off[len(names) + 4])
-    if n <= len(names) + 5 or off[len(names) + 5] != _DtrArgs.flags.offset:
-        raise RuntimeError("dtr: DtrArgs.flags offset mismatch")
-    return PST
+def flags_from_env() -> int:
+    # DPLASMA_DTR_STEAL=1: a workgroup whose own XCD list head waits on a dependency takes a ready head of
+    # another XCD's list (measurement knob; default: steal only from exhausted lists)
+    fl = 1 if os.environ.get("DPLASMA_DTR_STEAL", "0") == "1" else 0
+    # DPLASMA_DTR_HOLD="potrf_us,other_us": how long a high-list ticket whose task is not ready yet polls before
+    # it runs a low-list task meanwhile (measurement knob; default 50 us for POTRF tickets, 0 for the others)
+    # DPLASMA_DTR_CLAIM=window: windowed high-list claims (the first ready task among the next 64 positions)
+    # instead of in-order tickets
+    if os.environ.get("DPLASMA_DTR_CLAIM", "ticket") == "window":
+        fl |= 2
+    hold = os.environ.get("DPLASMA_DTR_HOLD")
+    if hold:
+        hp, ho = (int(x) for x in hold.split(","))
+        fl |= (min(255, max(0, ho // 10)) << 8) | (min(255, max(1, hp // 10)) << 16)
+    return fl
+
+
+def tile_offsets(A, nt):
+    """nt x nt table (i + j nt) of A's tile element offsets for i >= j (local tiles only), -1 elsewhere."""
+    tab = np.full(nt * nt, -1, dtype=np.int64)
+    for j in range(nt):
+        for i in range(j, nt):
+            if A.is_local(i, j):
+                tab[i + j * nt] = A.offset(i, j)
+    return tab
+
+
+class PotrfScratch:
+    """Per-panel POTRF workspaces of one launch (indexed by panel: disjoint across the ranks of an emulation)."""
+
+    def __init__(self, nt, dev, pstride):
+        self.Mw = torch.zeros(nt * MAXB * BLK, dtype=torch.float64, device=dev)
+        self.Sw = torch.zeros(nt * MAXB * RB, dtype=torch.float64, device=dev)
+        self.Lp = torch.zeros(nt * MAXB * MAXB * BLK, dtype=torch.float64, device=dev)
+        self.Wp = torch.zeros(nt * MAXB * MAXB * BLK, dtype=torch.float64, device=dev)
+        self.prog = torch.zeros(nt * 2 * MAXB * pstride, dtype=torch.int32, device=dev)
+
+    def fill(self, img):
+        for n in ("Mw", "Sw", "Lp", "Wp", "prog"):
+            img.set(n, getattr(self, n).data_ptr())
 
 
 _PLANS = {}
@@ -286,7 +367,8 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     if not supported(ctx, uplo, A):
         raise ValueError("potrf_dtr: one process, lower, fp64, NB = 512, N a multiple of 512, GPU")
     lib = _lib.load()
-    PST = _check_layout(lib)
+    img = ArgsImage(lib)
+    PST = img.pstride
     nt = A.nt
     D = max(1, int(os.environ.get("DPLASMA_DTR_DEFER", "4")))
     lo_order = os.environ.get("DPLASMA_DTR_LO_ORDER", "column")
@@ -307,54 +389,64 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     reqs_d = up(plan.reqs)
     hi_d = up(plan.hi)
     lo_d = up(plan.lo if len(plan.lo) else np.zeros(1, dtype=np.int32))
+    si, sj = _strides(A)
+    tab = np.full(nt * nt, -1, dtype=np.int64)
+    for j in range(nt):
+        tab[j * nt + j: (j + 1) * nt] = np.arange(j, nt, dtype=np.int64) * si + j * sj
+    tab_d = up(tab)
     cnt = torch.zeros(plan.ncnt, dtype=torch.int32, device=dev)
-    cur = torch.zeros(9 * PST, dtype=torch.int32, device=dev)
+    cur = torch.zeros((img.maxr + 8) * PST, dtype=torch.int32, device=dev)
+    claimed = torch.zeros(len(plan.hi) + 1, dtype=torch.int32, device=dev)
     # per-panel workspaces (HBM is plentiful: ~6 MB per panel, nothing recycled, no WAR edges)
     W = torch.zeros(nt * NBT * NBT, dtype=torch.float64, device=dev)
-    Mw = torch.zeros(nt * MAXB * BLK, dtype=torch.float64, device=dev)
-    Sw = torch.zeros(nt * MAXB * RB, dtype=torch.float64, device=dev)
-    Lp = torch.zeros(nt * MAXB * MAXB * BLK, dtype=torch.float64, device=dev)
-    Wp = torch.zeros(nt * MAXB * MAXB * BLK, dtype=torch.float64, device=dev)
-    prog = torch.zeros(nt * 2 * MAXB * PST, dtype=torch.int32, device=dev)
-    si, sj = _strides(A)
-    args = _DtrArgs()
-    args.A, args.ld, args.si, args.sj, args.nt = A.data.data_ptr(), A.ld, si, sj, nt
-    args.tasks, args.reqs, args.cnt, args.cur = tasks_d.data_ptr(), reqs_d.data_ptr(), cnt.data_ptr(), cur.data_ptr()
-    args.hi, args.nhi, args.lo = hi_d.data_ptr(), len(plan.hi), lo_d.data_ptr()
-    for q in range(9):
-        args.lo_off[q] = int(plan.lo_off[q])
-    args.W, args.Mw, args.Sw, args.Lp, args.Wp, args.prog = (W.data_ptr(), Mw.data_ptr(), Sw.data_ptr(),
-                                                             Lp.data_ptr(), Wp.data_ptr(), prog.data_ptr())
-    args.info = info.data_ptr()
-    # DPLASMA_DTR_STEAL=1: a workgroup whose own XCD list head waits on a dependency takes a ready head of
-    # another XCD's list (measurement knob; default: steal only from exhausted lists)
-    args.flags = 1 if os.environ.get("DPLASMA_DTR_STEAL", "0") == "1" else 0
+    scr = PotrfScratch(nt, dev, PST)
+    img.set("ld", A.ld)
+    img.set("nt", nt)
+    img.set("nranks", 1)
+    img.set("rank", 0)
+    img.set("dil", 1)
+    img.set("ncnt", plan.ncnt)
+    img.set("tasks", tasks_d.data_ptr())
+    img.set("reqs", reqs_d.data_ptr())
+    img.set("tab", tab_d.data_ptr())
+    img.set("cur", cur.data_ptr())
+    img.set("claimed", claimed.data_ptr())
+    img.set("hi", hi_d.data_ptr())
+    img.set("hi_off", [0, len(plan.hi)])
+    img.set("lo", lo_d.data_ptr())
+    img.set("lo_off", plan.lo_off)
+    img.set("A", [A.data.data_ptr()])
+    img.set("W", [W.data_ptr()])
+    img.set("cnt", [cnt.data_ptr()])
+    scr.fill(img)
+    img.set("info", info.data_ptr())
+    img.set("flags", flags_from_env())
     # DPLASMA_DTR_TRACE=1: per-task {start, end, workgroup << 8 | xcd} (s_memrealtime, 100 MHz) in tp.dtr_trace
     trace = None
     if os.environ.get("DPLASMA_DTR_TRACE", "0") == "1":
         trace = torch.zeros(3 * len(plan.tasks), dtype=torch.int64, device=dev)
-        args.trace = trace.data_ptr()
+        img.set("trace", trace.data_ptr())
     tp.dtr_trace = trace
-    nbytes = ctypes.sizeof(_DtrArgs)
+    nbytes = img.size
     host = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
     args_d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    epoch_off = _DtrArgs.epoch.offset
     state = {"epoch": 0}
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     nwg = int(os.environ.get("DPLASMA_DTR_WG", 2 * ncu))
     # progress needs a workgroup on every XCD (a low list is another XCD's to steal only once that XCD's
     # own list is exhausted) and the 16 cooperating POTRF workgroups co-resident: at least 64 of them
     nwg = max(64, min(nwg, 2 * ncu))
-    tp._keep = (tasks_d, reqs_d, hi_d, lo_d, cnt, cur, W, Mw, Sw, Lp, Wp, prog, host, args_d)
+    tp._keep = (tasks_d, reqs_d, hi_d, lo_d, tab_d, cnt, cur, claimed, W, scr, host, args_d)
     tp.dtr_plan = plan
 
     def f_run():
         state["epoch"] = state["epoch"] % ((1 << 25) - 1) + 1
-        args.epoch = state["epoch"]
-        ctypes.memmove(host.data_ptr(), ctypes.addressof(args), nbytes)
+        img.set("epoch", state["epoch"])
+        host.numpy()[:] = np.frombuffer(bytes(img.buf), dtype=np.uint8)
         args_d.copy_(host, non_blocking=True)
         cnt.zero_()
         cur.zero_()
+        claimed.zero_()
         _lib.check(lib.dpl_dtr_potrf(args_d.data_ptr(), nwg, _lib.stream_ptr()), "dtr_potrf")
 
     tp.task("DTR_POTRF", "update", f_run)

@@ -1,0 +1,328 @@
+"""Distributed device task runtime Cholesky: every rank of a P x Q grid runs the DTR on its own tiles.
+
+The reference schedules the Cholesky PTG on every rank with priorities, and a task whose input is a
+remote tile waits for the remote-dependency engine to deliver it (``src/zpotrf_L.jdf:58-69``
+priorities, ``high_priority`` at ``:93, 194, 306``; the flows ``A <- A potrf_ztrsm(k, m)`` of the
+update classes cross ranks).  Here the same happens inside ONE persistent launch per rank
+(``csrc/kernels/dtr.hip``): a remote panel strip is a task *requirement* -- an arrival counter on the
+consumer rank -- and the producer's ``SEND`` task (high priority, right behind the ``TRSM`` that
+solved the strip) stores the strip into the consumer's receive buffer and bumps that counter; no
+separate transport kernel competes for the CUs the persistent kernel holds.
+
+Plan (this module), from the one-process plan of ``models/potrf_dtr.py``:
+
+* every task runs on the owner of the tile it writes (``UPD(i, j, ..)`` and ``TRSM(i, k, r)`` on
+  owner(i, j) / owner(i, k), ``POTRF(k, b)`` on owner(k, k));
+* an update's requirement on a strip of a remote panel tile becomes "arrival counter >= 1" on its
+  rank; a ``SEND(i, k, r, dest)`` task per (strip, consumer rank) requires the strip solved on the
+  producer and bumps the consumer's counter (same counter index on every rank: the strip's marker);
+* a ``TRSM(i, k, r)`` away from owner(k, k) needs ``W_k = L_kk^-T``: ``SENDW(k, c, dest)`` tasks copy
+  its four 128-column blocks (upper triangle only) into the consumer's ``W``; the consumer's TRSM
+  requires 4 arrivals instead of the 16 POTRF block columns;
+* every remote tile a rank reads gets its own receive slot (HBM is plentiful: ~0.75 nt^2 / 2 / (P Q)
+  tiles per rank, nothing recycled, so no write-after-read hazards);
+* lists: each rank's high list is the one-process high order restricted to its tasks, with ``SEND``
+  right behind its ``TRSM`` and ``SENDW`` right behind POTRF(k); its low tasks are split over the
+  XCDs it runs on by column, each list in the one-process low order.  Every list is a subsequence of
+  the one-process topological order extended by the sends, so the earliest unfinished task of that
+  order is always claimable on its rank: the distributed schedule cannot deadlock either
+  (``tests/test_potrf_dtr.py`` runs the protocol over ranks with random completion orders).
+
+Two execution modes share the kernel: one process per GPU (``rank >= 0``; peers' receive buffers,
+``W`` and counters IPC-mapped, system-scope stores + release) and the *emulation* of a grid on one
+GPU (``rank = -1``): each XCD is a rank's "GPU" (8 ranks: one XCD each), the sends are copies inside
+HBM, and time is dilated by the number of ranks -- every task's completion becomes visible
+(nranks - 1) x its duration late and a send lands ``nranks x (lat + bytes / bw)`` after its link
+(one per ordered rank pair, FIFO) frees up -- so the launch's span / nranks models the P x Q run
+(``tools/emulate_potrf.py``).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import potrf_dtr as D
+
+T_UPD, T_TRSM, T_POTRF = D.T_UPD, D.T_TRSM, D.T_POTRF
+T_SEND, T_SENDW = 3, 4
+NBT, MAXB = D.NBT, D.MAXB
+STRIP = 128 * NBT                     # elements of a 128-row strip of a 512 x 512 tile
+
+
+class DistPlan:
+    """Per-rank task lists, requirement targets, sends and receive slots of a P x Q grid."""
+
+    def __init__(self, nt: int, Dd: int, P: int, Q: int, lo_order: str = None, min_tiles: int = None,
+                 base: "D._Plan" = None):
+        base = base or D._Plan(nt, Dd, lo_order, min_tiles)
+        self.base, self.nt, self.P, self.Q, self.nranks = base, nt, P, Q, P * Q
+        S, WB = base.S, base.WB
+        self.S, self.WB, self.ncnt = S, WB, base.ncnt
+        tasks = base.tasks.copy()
+        reqs = base.reqs.copy()
+        ntask0 = len(tasks)
+        own = self._owner(tasks["i"].astype(np.int64), tasks["j"].astype(np.int64))
+        # ---- requirement translation (remote strips / remote W_k)
+        nreq = tasks["nreq"].astype(np.int64)
+        rtask = np.repeat(np.arange(ntask0), nreq)
+        rpos = np.arange(len(reqs)) - np.repeat(tasks["req_beg"].astype(np.int64), nreq)
+        ttype = tasks["type"][rtask]
+        towner = own[rtask]
+        idx = reqs[:, 0].astype(np.int64)
+        strip_req = (ttype == T_UPD) & (rpos >= 1)
+        I, J = idx % S, idx // S
+        powner = self._owner(I // 4, J // 4)
+        remote_strip = strip_req & (powner != towner)
+        # consumers of remote strips: unique (counter, consumer rank)
+        cons = np.unique(np.stack([idx[remote_strip], towner[remote_strip]], 1), axis=0) if remote_strip.any() \
+            else np.zeros((0, 2), dtype=np.int64)
+        reqs[remote_strip, 1] = 1
+        w_req = (ttype == T_TRSM) & (rpos == 0)
+        kW = idx - WB
+        wowner = self._owner(kW, kW)
+        remote_w = w_req & (wowner != towner)
+        wcons = np.unique(np.stack([kW[remote_w], towner[remote_w]], 1), axis=0) if remote_w.any() \
+            else np.zeros((0, 2), dtype=np.int64)
+        reqs[remote_w, 1] = 4
+        # ---- send tasks
+        ns, nw = len(cons), 4 * len(wcons)
+        st = np.zeros(ns + nw, dtype=D.TASK_DT)
+        sreq = np.zeros((ns + nw, 2), dtype=np.int64)
+        keys = np.zeros((ns + nw, 6), dtype=np.int64)
+        sown = np.zeros(ns + nw, dtype=np.int64)
+        if ns:
+            c_idx, dest = cons[:, 0], cons[:, 1]
+            Is, ks = c_idx % S, c_idx // S // 4
+            st["type"][:ns], st["i"][:ns], st["j"][:ns], st["k0"][:ns] = T_SEND, Is // 4, dest, ks
+            st["r"][:ns], st["inc"][:ns] = Is % 4, c_idx
+            sreq[:ns, 0] = c_idx
+            sreq[:ns, 1] = base.F[Is, ks]            # the strip's "solved" marker value on the producer
+            if base.order == "deadline":
+                keys[:ns] = np.stack([Is // 4 - 1, ks, np.full(ns, 3), np.zeros(ns, int), Is % 4, 1 + dest], 1)
+            else:
+                keys[:ns] = np.stack([ks, np.full(ns, 3), np.zeros(ns, int), Is // 4, Is % 4, 1 + dest], 1)
+            sown[:ns] = self._owner(Is // 4, ks)
+        if nw:
+            kk = np.repeat(wcons[:, 0], 4)
+            dest = np.repeat(wcons[:, 1], 4)
+            cb = np.tile(np.arange(4), len(wcons))
+            sl = slice(ns, ns + nw)
+            st["type"][sl], st["i"][sl], st["j"][sl], st["k0"][sl] = T_SENDW, kk, dest, kk
+            st["r"][sl], st["inc"][sl] = cb, WB + kk
+            sreq[sl, 0], sreq[sl, 1] = WB + kk, MAXB
+            if base.order == "deadline":
+                keys[sl] = np.stack([kk, kk, np.ones(nw, int), np.ones(nw, int), MAXB + cb, dest], 1)
+            else:
+                keys[sl] = np.stack([kk, np.ones(nw, int), np.zeros(nw, int), MAXB + cb, dest, np.zeros(nw, int)], 1)
+            sown[sl] = self._owner(kk, kk)
+        st["nreq"] = 1
+        st["req_beg"] = len(reqs) + np.arange(ns + nw)
+        self.tasks = np.concatenate([tasks, st])
+        self.reqs = np.concatenate([reqs, sreq]).astype(np.int32)
+        self.owner = np.concatenate([own, sown])
+        self.key = np.concatenate([base.key, keys])
+        self.is_hi = np.concatenate([base.is_hi, np.ones(ns + nw, dtype=bool)])
+        self.nsend, self.nsendw = ns, nw
+        # ---- receive slots: every remote panel tile a rank reads
+        self.recv_tiles = []
+        self.recv_slot = []
+        for r in range(self.nranks):
+            sel = cons[:, 1] == r if ns else np.zeros(0, dtype=bool)
+            tl = np.unique(np.stack([(cons[sel, 0] % S) // 4, cons[sel, 0] // S // 4], 1), axis=0) \
+                if ns and sel.any() else np.zeros((0, 2), dtype=np.int64)
+            self.recv_tiles.append(tl)
+            self.recv_slot.append({(int(i), int(k)): q for q, (i, k) in enumerate(tl)})
+        # send destinations: element offset in the destination's receive buffer (SEND) or W (SENDW)
+        self.xoff = np.zeros(len(self.tasks), dtype=np.int64)
+        for q in range(ns):
+            t = self.tasks[ntask0 + q]
+            slot = self.recv_slot[int(t["j"])][(int(t["i"]), int(t["k0"]))]
+            self.xoff[ntask0 + q] = slot * NBT * NBT + 128 * int(t["r"])
+        if nw:
+            tw = self.tasks[ntask0 + ns:]
+            self.xoff[ntask0 + ns:] = tw["k0"].astype(np.int64) * NBT * NBT + tw["r"].astype(np.int64) * 128 * NBT
+
+    def _owner(self, i, j):
+        return (np.asarray(i) % self.P) * self.Q + (np.asarray(j) % self.Q)
+
+    # ------------------------------------------------------------------ lists
+    def lists(self, xcds_of: dict):
+        """xcds_of: rank -> the XCD ids its workgroups run on (a process: all 8; the emulation: its own).
+        Returns (hi, hi_off[nranks + 1], lo, lo_off[9]): each rank's high list (in the one-process high order
+        with the sends inserted) and one low list per XCD (the rank's low tasks by column, one-process order)."""
+        hi_parts, hi_off = [], [0]
+        lo_lists = [np.zeros(0, dtype=np.int32) for _ in range(8)]
+        nr = self.nranks
+        for r in range(nr):
+            mine = self.owner == r
+            h = np.nonzero(mine & self.is_hi)[0]
+            kk = self.key[h]
+            o = np.lexsort(tuple([h] + [kk[:, q] for q in reversed(range(6))]))
+            hi_parts.append(h[o].astype(np.int32))
+            hi_off.append(hi_off[-1] + len(h))
+            xs = list(xcds_of.get(r, []))
+            if not xs:
+                continue
+            lo = np.nonzero(mine & ~self.is_hi)[0]
+            kk = self.key[lo]
+            o = np.lexsort(tuple([lo] + [kk[:, q] for q in reversed(range(6))]))
+            lo = lo[o]
+            col = self.tasks["j"][lo].astype(np.int64)
+            pick = (col // self.Q) % len(xs)
+            for q, x in enumerate(xs):
+                lo_lists[x] = np.concatenate([lo_lists[x], lo[pick == q].astype(np.int32)])
+        hi = np.concatenate(hi_parts) if hi_parts else np.zeros(0, dtype=np.int32)
+        lo_off = np.zeros(9, dtype=np.int64)
+        lo_off[1:] = np.cumsum([len(x) for x in lo_lists])
+        return hi, np.asarray(hi_off + [hi_off[-1]] * (8 - nr), dtype=np.int64), np.concatenate(lo_lists), lo_off
+
+    def recv_elems(self, r: int) -> int:
+        return max(1, len(self.recv_tiles[r])) * NBT * NBT
+
+    def tile_table(self, r: int, tile_off, recv_base_off: int) -> np.ndarray:
+        """nt x nt element offsets (relative to rank r's A base; column-major by (i, j)): r's local tiles
+        (tile_off(i, j)) and its received copies (recv_base_off + slot * NB^2); -1 elsewhere."""
+        nt = self.nt
+        tab = np.full(nt * nt, -1, dtype=np.int64)
+        for j in range(nt):
+            for i in range(j, nt):
+                if self._owner(i, j) == r:
+                    tab[i + j * nt] = tile_off(i, j)
+        for (i, k), q in self.recv_slot[r].items():
+            tab[i + k * nt] = recv_base_off + q * NBT * NBT
+        return tab
+
+
+# ------------------------------------------------------------------------------------------ emulation
+class Emulation:
+    """A P x Q grid's DTR Cholesky emulated on ONE GPU (see the module docstring): every rank's tiles in its
+    own TILE-storage descriptor, receive buffer, W and counters; one launch of 2 x #CUs workgroups whose
+    XCD picks their rank; time dilated by P Q.  ``run()`` returns the launch span (s); the modelled P x Q
+    time is span / (P Q)."""
+
+    def __init__(self, ctx, N: int, P: int, Q: int, bw_gbs: float = 50.0, lat_us: float = 10.0, Dd: int = None,
+                 seed: int = 3872, trace: bool = False, order: str = None):
+        import os
+
+        import torch
+
+        from .. import descriptor as dsc
+        from ..ops import _lib
+        nr = P * Q
+        if 8 % nr or N % NBT:
+            raise ValueError("emulation: P Q must divide 8 (one or more XCDs per rank) and N a multiple of 512")
+        self.ctx, self.N, self.P, self.Q, self.nr = ctx, N, P, Q, nr
+        nt = N // NBT
+        Dd = Dd or max(1, int(os.environ.get("DPLASMA_DTR_DEFER", "4")))
+        self.plan = plan = DistPlan(nt, Dd, P, Q, lo_order=order or os.environ.get("DPLASMA_DTR_LO_ORDER", "deadline"))
+        lib = _lib.load()
+        self.lib = lib
+        img = D.ArgsImage(lib)
+        self.img = img
+        dev = ctx.device
+        X = 8 // nr
+        hi, hi_off, lo, lo_off = plan.lists({r: list(range(r * X, (r + 1) * X)) for r in range(nr)})
+
+        def up(x):
+            return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+        # per-rank storage: the P x Q block-cyclic descriptors of rank r (TILE storage, 512 x 512 tiles)
+        self.A = [dsc.TiledMatrix(torch.float64, NBT, NBT, N, N, P=P, Q=Q, rank=r, device=dev) for r in range(nr)]
+        from .aux import plghe
+        for Ar in self.A:
+            plghe(ctx, float(N), 123, Ar, seed)      # dplasmaUpperLower: bit-identical for any distribution
+        self.A0 = [Ar.data.clone() for Ar in self.A]
+        self.recv = [torch.zeros(plan.recv_elems(r), dtype=torch.float64, device=dev) for r in range(nr)]
+        self.W = [torch.zeros(nt * NBT * NBT, dtype=torch.float64, device=dev) for _ in range(nr)]
+        self.cnt = torch.zeros(nr * plan.ncnt, dtype=torch.int32, device=dev)
+        self.vis = torch.zeros(nr * plan.ncnt, dtype=torch.int64, device=dev)
+        self.link = torch.zeros(img.maxr * img.maxr, dtype=torch.int64, device=dev)
+        self.cur = torch.zeros((img.maxr + 8) * img.pstride, dtype=torch.int32, device=dev)
+        self.claimed = torch.zeros(len(hi) + 1, dtype=torch.int32, device=dev)
+        tabs = []
+        for r in range(nr):
+            rb = (self.recv[r].data_ptr() - self.A[r].data.data_ptr())
+            assert rb % 8 == 0
+            tabs.append(plan.tile_table(r, self.A[r].offset, rb // 8))
+        self.tab_d = up(np.concatenate(tabs))
+        self.tasks_d = up(plan.tasks.view(np.uint8))
+        self.reqs_d = up(plan.reqs)
+        self.xoff_d = up(plan.xoff)
+        self.hi_d = up(hi if len(hi) else np.zeros(1, dtype=np.int32))
+        self.lo_d = up(lo if len(lo) else np.zeros(1, dtype=np.int32))
+        self.info = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.scr = D.PotrfScratch(nt, dev, img.pstride)
+        self.trace = torch.zeros(3 * len(plan.tasks), dtype=torch.int64, device=dev) if trace else None
+        img.set("ld", NBT)
+        img.set("nt", nt)
+        img.set("nranks", nr)
+        img.set("rank", -1)
+        img.set("dil", nr)
+        img.set("ncnt", plan.ncnt)
+        img.set("tasks", self.tasks_d.data_ptr())
+        img.set("reqs", self.reqs_d.data_ptr())
+        img.set("tab", self.tab_d.data_ptr())
+        img.set("xoff", self.xoff_d.data_ptr())
+        img.set("cur", self.cur.data_ptr())
+        img.set("claimed", self.claimed.data_ptr())
+        img.set("hi", self.hi_d.data_ptr())
+        img.set("hi_off", hi_off)
+        img.set("lo", self.lo_d.data_ptr())
+        img.set("lo_off", lo_off)
+        img.set("A", [a.data.data_ptr() for a in self.A])
+        img.set("recv", [b.data_ptr() for b in self.recv])
+        img.set("W", [w.data_ptr() for w in self.W])
+        img.set("cnt", [self.cnt.data_ptr() + 4 * r * plan.ncnt for r in range(nr)])
+        img.set("vis", self.vis.data_ptr())
+        img.set("link", self.link.data_ptr())
+        img.set("bw_bpt", max(1, int(round(bw_gbs * 10))))
+        img.set("lat_t", int(round(lat_us * 100)))
+        self.scr.fill(img)
+        img.set("info", self.info.data_ptr())
+        img.set("flags", D.flags_from_env())
+        if trace:
+            img.set("trace", self.trace.data_ptr())
+        self.args_d = torch.empty(img.size, dtype=torch.uint8, device=dev)
+        self.epoch = 0
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        self.nwg = 2 * ncu
+
+    def reset(self):
+        for Ar, a0 in zip(self.A, self.A0):
+            Ar.data.copy_(a0)
+
+    def run(self) -> float:
+        import time
+
+        import torch
+
+        from ..ops import _lib
+        self.epoch = self.epoch % ((1 << 25) - 1) + 1
+        self.img.set("epoch", self.epoch)
+        self.args_d.copy_(torch.frombuffer(bytearray(self.img.buf), dtype=torch.uint8))
+        for t in (self.cnt, self.vis, self.link, self.cur, self.claimed, self.info):
+            t.zero_()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        _lib.check(self.lib.dpl_dtr_potrf(self.args_d.data_ptr(), self.nwg, _lib.stream_ptr()), "dtr_potrf (emulation)")
+        torch.cuda.synchronize()
+        span = time.perf_counter() - t0
+        r = int(self.info.item())
+        if r != 0:
+            raise RuntimeError(f"emulated potrf: info {r}")
+        return span
+
+    def assemble(self):
+        """The factor as one one-process descriptor (lower tiles from their owners)."""
+        import torch
+
+        from .. import descriptor as dsc
+        N, nt = self.N, self.N // NBT
+        L = dsc.TiledMatrix(torch.float64, NBT, NBT, N, N, device=self.ctx.device)
+        A0 = dsc.TiledMatrix(torch.float64, NBT, NBT, N, N, device=self.ctx.device)
+        for j in range(nt):
+            for i in range(j, nt):
+                r = self.plan._owner(i, j)
+                Ar = self.A[r]
+                o = Ar.offset(i, j)
+                L.data[L.offset(i, j): L.offset(i, j) + NBT * NBT].copy_(Ar.data[o:o + NBT * NBT])
+                A0.data[A0.offset(i, j): A0.offset(i, j) + NBT * NBT].copy_(self.A0[r][o:o + NBT * NBT])
+        return L, A0

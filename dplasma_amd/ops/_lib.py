@@ -26,7 +26,7 @@ _SIGS = {
     # device task runtime (dtr.hip): DtrArgs image in device memory, workgroups, stream
     "dpl_dtr_potrf": [c_vp, c_int, c_vp],
     "dpl_dtr_args_size": [],
-    "dpl_dtr_args_layout": [c_vp, c_int],
+    "dpl_dtr_field": [ctypes.c_char_p],
     # prec, transA, transB, nitems, items, kpairs, max_m, max_n, alpha*, A, lda, B, ldb, beta*, C, ldc, vec_ok, generic, stream
     "dpl_gemm_batched": [c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_int, c_vp,
                          c_vp, c_int, c_int, c_int, c_vp],
@@ -124,6 +124,7 @@ _SIGS = {
                          c_int, c_vp, c_vp],
 }
 _OPTIONAL = set()
+_RESTYPE = {"dpl_dtr_field": c_ll}
 
 
 def lib_path() -> Path:
@@ -156,7 +157,7 @@ def load(build_if_missing: bool = True):
                     continue
                 raise
             f.argtypes = args
-            f.restype = c_int
+            f.restype = _RESTYPE.get(name, c_int)
         _LIB = _Declared(lib)
         # pivoting block kernel: LDS tile (default) or register-resident rows (DPLASMA_LU_BLOCK=reg,
         # measured slower: profiles/r3_lu_block_reg.txt)

@@ -12,6 +12,7 @@ import pytest
 import torch
 
 from dplasma_amd.models import potrf_dtr as D
+from dplasma_amd.models import potrf_dtr_dist as DD
 
 T_UPD, T_TRSM, T_POTRF = D.T_UPD, D.T_TRSM, D.T_POTRF
 
@@ -142,7 +143,7 @@ def _emulate(plan, A=None, nb=None, P=8, seed=0, steal=False):
     return order
 
 
-@pytest.mark.parametrize("lo_order", ["column", "panel"])
+@pytest.mark.parametrize("lo_order", ["column", "panel", "deadline"])
 @pytest.mark.parametrize("nt,defer", [(1, 4), (3, 4), (9, 4), (12, 2), (10, 3)])
 def test_dtr_plan_lists_and_progress(nt, defer, lo_order):
     plan = D._Plan(nt, defer, lo_order)
@@ -156,7 +157,7 @@ def test_dtr_plan_lists_and_progress(nt, defer, lo_order):
         _emulate(plan, P=(8, 13, 40)[seed], seed=seed, steal=True)
 
 
-@pytest.mark.parametrize("lo_order", ["column", "panel"])
+@pytest.mark.parametrize("lo_order", ["column", "panel", "deadline"])
 @pytest.mark.parametrize("nt,defer,min_tiles", [(5, 2, 0), (7, 4, 0), (11, 4, 6)])
 def test_dtr_plan_numerics(nt, defer, min_tiles, lo_order):
     nb = 16
@@ -169,6 +170,224 @@ def test_dtr_plan_numerics(nt, defer, min_tiles, lo_order):
     _emulate(plan, A=A, nb=nb, P=8, seed=3, steal=(lo_order == "panel"))
     L = np.tril(A)
     assert np.abs(L - np.linalg.cholesky(S)).max() < 1e-10
+
+
+# ------------------------------------------------------------------------------- distributed DTR
+def _emulate_dist(dplan, xcds_of, A=None, nb=None, wpx=2, seed=0, window=False):
+    """The claim protocol of every rank of a P x Q grid (models/potrf_dtr_dist.py), with wpx workers per
+    XCD, random completion order and, with A, per-rank storage: a rank reads its own tiles, its receive
+    slots (written only by SEND tasks) and its own W_k (computed by POTRF, or written by SENDW) -- a
+    missing requirement shows up as a wrong factor.  Returns the assembled factor (or None)."""
+    rng = np.random.default_rng(seed)
+    tasks, reqs, nr, nt = dplan.tasks, dplan.reqs, dplan.nranks, dplan.nt
+    hi, hi_off, lo, lo_off = dplan.lists(xcds_of)
+    cnt = np.zeros((nr, dplan.ncnt), dtype=np.int64)
+    hcur = [hi_off[r] for r in range(nr)]
+    lcur = [lo_off[x] for x in range(8)]
+    s = nb // 4 if nb else None
+    store = [A.copy() if A is not None else None for _ in range(nr)]     # rank r's view (its tiles valid)
+    if A is not None:
+        for r in range(nr):
+            for i in range(nt):
+                for j in range(nt):
+                    if dplan._owner(i, j) != r:
+                        store[r][i * nb:(i + 1) * nb, j * nb:(j + 1) * nb] = np.nan
+    recv = [dict() for _ in range(nr)]
+    W = [dict() for _ in range(nr)]
+    workers = [(r, x) for r in range(nr) for x in xcds_of[r] for _ in range(wpx)]
+    busy = [False] * len(workers)
+    ticket = [None] * len(workers)
+    inflight = []
+    done = np.zeros(len(tasks), dtype=bool)
+
+    def ready(t, r):
+        b, n = tasks["req_beg"][t], tasks["nreq"][t]
+        return all(cnt[r, reqs[b + q, 0]] >= reqs[b + q, 1] for q in range(n))
+
+    def panel(r, i, k):
+        if dplan._owner(i, k) == r:
+            return store[r][i * nb:(i + 1) * nb, k * nb:(k + 1) * nb]
+        return recv[r][(i, k)]
+
+    def start(t, r):
+        if A is None:
+            return None
+        tk = tasks[t]
+        ty, i, j, k0, rr, c, nk = (int(tk[f]) for f in ("type", "i", "j", "k0", "r", "c", "nk"))
+        X = store[r]
+        if ty == T_UPD:
+            acc = X[i * nb + rr * s: i * nb + (rr + 1) * s, j * nb + c * s: j * nb + (c + 1) * s].copy()
+            for k in range(k0, k0 + nk):
+                acc -= panel(r, i, k)[rr * s:(rr + 1) * s] @ panel(r, j, k)[c * s:(c + 1) * s].T
+            return acc
+        if ty == T_TRSM:
+            return X[i * nb + rr * s: i * nb + (rr + 1) * s, k0 * nb:(k0 + 1) * nb] @ W[r][k0]
+        if ty == T_POTRF and rr == 0:
+            return np.linalg.cholesky(X[k0 * nb:(k0 + 1) * nb, k0 * nb:(k0 + 1) * nb])
+        if ty == DD.T_SEND:
+            return X[i * nb + rr * s: i * nb + (rr + 1) * s, k0 * nb:(k0 + 1) * nb].copy()
+        if ty == DD.T_SENDW:
+            return W[r][k0][:, rr * s:(rr + 1) * s].copy()
+        return None
+
+    def finish(t, r, val):
+        tk = tasks[t]
+        ty, i, j, k0, rr, c = (int(tk[f]) for f in ("type", "i", "j", "k0", "r", "c"))
+        tgt = r
+        if A is not None and val is not None:
+            X = store[r]
+            if ty == T_UPD:
+                blk = X[i * nb + rr * s: i * nb + (rr + 1) * s, j * nb + c * s: j * nb + (c + 1) * s]
+                if i == j and rr == c:
+                    val = np.tril(val) + np.triu(blk, 1)
+                blk[:] = val
+            elif ty == T_TRSM:
+                X[i * nb + rr * s: i * nb + (rr + 1) * s, k0 * nb:(k0 + 1) * nb] = val
+            elif ty == T_POTRF:
+                X[k0 * nb:(k0 + 1) * nb, k0 * nb:(k0 + 1) * nb] = np.tril(val)
+                W[r][k0] = np.linalg.inv(val).T
+            elif ty == DD.T_SEND:
+                recv[j].setdefault((i, k0), np.full((nb, nb), np.nan))[rr * s:(rr + 1) * s] = val
+            else:
+                W[j].setdefault(k0, np.zeros((nb, nb)))[:, rr * s:(rr + 1) * s] = val
+        if ty in (DD.T_SEND, DD.T_SENDW):
+            tgt = j
+        if tk["inc"] >= 0:
+            cnt[tgt, tk["inc"]] += 1
+        done[t] = True
+
+    def try_low(r, x):
+        xs = [x] + [y for y in xcds_of[r] if y != x]
+        for y in xs:
+            if lcur[y] < lo_off[y + 1]:
+                t = int(lo[lcur[y]])
+                if ready(t, r):
+                    lcur[y] += 1
+                    return t
+                if y == x:
+                    return None        # the own head waits: no stealing while the own list lasts
+        return None
+
+    hclaimed = np.zeros(len(hi) + 1, dtype=bool)
+
+    def claim_window(r):
+        # the kernel's windowed claim (DtrArgs.flags bit 1): the first unclaimed ready task among the next 64
+        # positions; POTRF(k, b > 0) only once the entry before it is claimed; the head skips the claimed prefix
+        h = hcur[r]
+        end = min(h + 64, hi_off[r + 1])
+        got = None
+        for q in range(h, end):
+            t = int(hi[q])
+            if hclaimed[q] or not ready(t, r):
+                continue
+            if tasks["type"][t] == T_POTRF and tasks["r"][t] > 0 and q > h and not hclaimed[q - 1]:
+                continue
+            hclaimed[q] = True
+            got = t
+            break
+        while hcur[r] < hi_off[r + 1] and hclaimed[hcur[r]]:
+            hcur[r] += 1
+        return got
+
+    stall = 0
+    while True:
+        progressed = False
+        for w in rng.permutation(len(workers)):
+            if busy[w]:
+                continue
+            r, x = workers[w]
+            if window:
+                t = claim_window(r)
+                if t is None:
+                    t = try_low(r, x)
+                if t is None:
+                    continue
+                inflight.append((t, r, start(t, r), w))
+                busy[w] = True
+                progressed = True
+                continue
+            if ticket[w] is None and hcur[r] < hi_off[r + 1] and (ready(int(hi[hcur[r]]), r) or rng.random() < 0.05):
+                ticket[w] = hcur[r]
+                hcur[r] += 1
+            t = None
+            if ticket[w] is not None:
+                th = int(hi[ticket[w]])
+                if ready(th, r):
+                    t, ticket[w] = th, None
+            if t is None and (ticket[w] is None or tasks["type"][hi[ticket[w]]] != T_POTRF or stall):
+                t = try_low(r, x)
+            if t is None:
+                continue
+            inflight.append((t, r, start(t, r), w))
+            busy[w] = True
+            progressed = True
+        if not progressed and inflight:
+            q = int(rng.integers(len(inflight)))
+            t, r, v, w = inflight.pop(q)
+            busy[w] = False
+            finish(t, r, v)
+            progressed = True
+        if not progressed:
+            if all(hcur[r] >= hi_off[r + 1] for r in range(nr)) and all(tk is None for tk in ticket) and \
+                    all(lcur[y] >= lo_off[y + 1] for y in range(8)):
+                break
+            stall += 1
+            assert stall < 50, f"distributed schedule stalled: heads {hcur} {lcur}"
+        else:
+            stall = 0
+    assert done.all()
+    if A is None:
+        return None
+    L = np.zeros_like(A)
+    for i in range(nt):
+        for j in range(i + 1):
+            o = dplan._owner(i, j)
+            L[i * nb:(i + 1) * nb, j * nb:(j + 1) * nb] = store[o][i * nb:(i + 1) * nb, j * nb:(j + 1) * nb]
+    return np.tril(L)
+
+
+def _xcds(nr, mode):
+    if mode == "emulate":            # every XCD a rank's GPU: rank r on XCDs [r*8/nr, (r+1)*8/nr)
+        X = 8 // nr
+        return {r: list(range(r * X, (r + 1) * X)) for r in range(nr)}
+    return {r: [r % 8] for r in range(nr)}   # (one list per rank is enough for the protocol check)
+
+
+@pytest.mark.parametrize("order", ["column", "deadline"])
+@pytest.mark.parametrize("grid", [(1, 1), (1, 2), (2, 1), (2, 2), (2, 4)])
+@pytest.mark.parametrize("nt,defer", [(4, 2), (9, 4), (12, 3)])
+def test_dtr_dist_plan_progress(grid, nt, defer, order):
+    """Every rank's lists drain with random completion orders: no distributed deadlock."""
+    P, Q = grid
+    dplan = DD.DistPlan(nt, defer, P, Q, lo_order=order)
+    nr = P * Q
+    hi, hi_off, lo, lo_off = dplan.lists(_xcds(nr, "emulate"))
+    ids = np.concatenate([hi, lo])
+    assert len(ids) == len(dplan.tasks) and len(np.unique(ids)) == len(ids)
+    # sends exactly to the ranks whose updates read a remote strip, never to the producer itself
+    snd = dplan.tasks[dplan.tasks["type"] == DD.T_SEND]
+    assert (dplan._owner(snd["i"], snd["k0"]) != snd["j"]).all()
+    for seed in range(2):
+        _emulate_dist(dplan, _xcds(nr, "emulate"), wpx=1 + seed, seed=seed)
+        _emulate_dist(dplan, _xcds(nr, "emulate"), wpx=1 + seed, seed=seed, window=True)
+
+
+@pytest.mark.parametrize("order", ["column", "deadline"])
+@pytest.mark.parametrize("grid", [(1, 2), (2, 2), (2, 4), (3, 2)])
+def test_dtr_dist_plan_numerics(grid, order):
+    """Per-rank storage, receive slots and W copies: the assembled factor equals numpy's Cholesky."""
+    P, Q = grid
+    nt, nb = 7, 16
+    n = nt * nb
+    rng = np.random.default_rng(11)
+    M = rng.standard_normal((n, n))
+    S = M @ M.T + n * np.eye(n)
+    dplan = DD.DistPlan(nt, 2, P, Q, lo_order=order)
+    nr = P * Q
+    for window in (False, True):
+        L = _emulate_dist(dplan, _xcds(nr, "emulate" if 8 % nr == 0 else "proc"), A=S.copy(), nb=nb, wpx=2, seed=5,
+                          window=window)
+        assert np.abs(L - np.linalg.cholesky(S)).max() < 1e-10
 
 
 @pytest.mark.gpu
@@ -187,4 +406,21 @@ def test_dtr_potrf_gpu(N):
     Ar = A.like()
     Ar.data.copy_(A0)
     ok, res = dp.check_potrf(ctx, dp.dplasmaLower, A, Ar)
+    assert ok, res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grid", [(1, 2), (2, 2), (2, 4)])
+def test_dtr_dist_emulation_gpu(grid):
+    """A P x Q grid emulated on the XCDs of one GPU (per-rank storage, sends as copies, dilated time): the
+    assembled factor passes the reference residual check."""
+    import dplasma_amd as dp
+    P, Q = grid
+    ctx = dp.init()
+    em = DD.Emulation(ctx, 4096, P, Q, bw_gbs=50.0, lat_us=10.0)
+    for _ in range(2):
+        em.reset()
+        em.run()
+    L, A0 = em.assemble()
+    ok, res = dp.check_potrf(ctx, dp.dplasmaLower, L, A0)
     assert ok, res
