@@ -241,6 +241,15 @@ class Context:
         nb = max(1, int(os.environ.get("DPLASMA_BULK_GROUPS", "2")))
         self.urgent_group = dist.new_group(list(range(self.world)), **kw)
         self.bulk_groups = [dist.new_group(list(range(self.world))) for _ in range(nb)]
+        # names for the communication-order recorder (parallel.comm.record): the same on every rank
+        from .parallel import comm as _comm
+        for i, g in enumerate(rows):
+            _comm.name_group(g, f"row{i}")
+        for i, g in enumerate(cols):
+            _comm.name_group(g, f"col{i}")
+        _comm.name_group(self.urgent_group, "urgent")
+        for i, g in enumerate(self.bulk_groups):
+            _comm.name_group(g, f"bulk{i}")
         if dist.get_backend() == "nccl" and self.is_gpu:
             # create every communicator now, on every rank (a point-to-point batch that involves only
             # some ranks must never be the call that initialises one)

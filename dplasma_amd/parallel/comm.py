@@ -34,6 +34,124 @@ import torch
 import torch.distributed as dist
 
 
+# ------------------------------------------------------------------ communication-order recorder
+# Every rank issues its transfers from the same SPMD program: tasks are built in the same order on every
+# rank (runtime/taskpool.py chains the communicating tasks in program order under any scheduler policy),
+# so on every communicator each pair of ranks posts its messages in one order, and the batches of all
+# communicators follow one global order of task labels -- the two conditions under which RCCL batches on
+# several communicators (urgent / bulk / row / col, each on its own stream) cannot wait on each other in
+# a cycle.  record() logs (label, communicator, op, peer, bytes) per call; check_order() verifies both
+# conditions over every rank's log (tests/test_comm_order.py).
+LABEL = ""            # the running task's name (set by the taskpool runner)
+_GROUP_NAMES = {}
+_REC = None
+
+
+def name_group(group, name: str) -> None:
+    if group is not None:
+        _GROUP_NAMES[id(group)] = name
+
+
+def _gname(group) -> str:
+    return "world" if group is None else _GROUP_NAMES.get(id(group), f"g{id(group)}")
+
+
+def record(on: bool = True):
+    """Start (on) or stop recording this process's transfers; returns the log recorded so far."""
+    global _REC
+    log = _REC
+    _REC = [] if on else None
+    return log
+
+
+def _rec_p2p(sends, recvs, group):
+    if _REC is None:
+        return
+    g = _gname(group)
+    batch = []
+    for t, p in sends:
+        batch.append(("send", int(p), _nbytes(t)))
+    for t, p in recvs:
+        batch.append(("recv", int(p), _nbytes(t)))
+    _REC.append((LABEL, g, "p2p", batch))
+
+
+def _rec_coll(kind, t, group):
+    """t None: a collective whose per-rank sizes differ by design (all-to-all): only its kind is compared."""
+    if _REC is not None:
+        _REC.append((LABEL, _gname(group), kind, [("coll", -1, _nbytes(t) if t is not None else -1)]))
+
+
+def check_order(logs: dict) -> None:
+    """logs: rank -> record() log.  Raises AssertionError unless (1) on every communicator, the messages
+    rank a sends to rank b and those b receives from a pair up in order (same sizes), (2) every member of a
+    communicator issues the same sequence of collectives on it, and (3) the batches of all ranks follow one
+    global order: merging every batch with the batches its messages pair with (the sender's DSEND(k) and the
+    receiver's DRECV(k) are one transfer), the per-rank issue orders leave no cycle -- the condition under
+    which no set of ranks can each wait, in issue order, for a batch that waits on another of them."""
+    from collections import defaultdict
+    sends, recvs, colls = defaultdict(list), defaultdict(list), defaultdict(dict)
+    for r, log in logs.items():
+        for bi, (label, g, kind, batch) in enumerate(log):
+            for op, peer, nb in batch:
+                if op == "send":
+                    sends[(g, r, peer)].append((nb, (r, bi), label))
+                elif op == "recv":
+                    recvs[(g, peer, r)].append((nb, (r, bi), label))
+                else:
+                    colls[g].setdefault(r, []).append((kind, nb, (r, bi)))
+    parent = {}
+
+    def find(x):
+        parent.setdefault(x, x)
+        while parent[x] != x:
+            parent[x] = parent[parent[x]]
+            x = parent[x]
+        return x
+
+    def union(x, y):
+        parent[find(x)] = find(y)
+    for key in set(sends) | set(recvs):
+        a, b = sends.get(key, []), recvs.get(key, [])
+        for n in range(max(len(a), len(b))):
+            if n >= len(a) or n >= len(b) or a[n][0] != b[n][0]:
+                raise AssertionError(
+                    f"communicator {key[0]}: rank {key[1]} -> {key[2]}: message {n} differs (sent "
+                    f"{a[n][::2] if n < len(a) else None}, received {b[n][::2] if n < len(b) else None})")
+            union(a[n][1], b[n][1])
+    for g, per in colls.items():
+        seqs = list(per.values())
+        if any([x[:2] for x in sq] != [x[:2] for x in seqs[0]] for sq in seqs):
+            raise AssertionError(f"communicator {g}: ranks issue different collective sequences")
+        for i in range(len(seqs[0])):
+            for sq in seqs[1:]:
+                union(sq[i][2], seqs[0][i][2])
+    succ, indeg, nodes = defaultdict(set), defaultdict(int), set()
+    for r, log in logs.items():
+        prev = None
+        for bi in range(len(log)):
+            c = find((r, bi))
+            nodes.add(c)
+            if prev is not None and prev != c and c not in succ[prev]:
+                succ[prev].add(c)
+                indeg[c] += 1
+            if prev is not None and prev == c:
+                raise AssertionError(f"rank {r}: batches {bi - 1} and {bi} pair with each other (a wait cycle)")
+            prev = c
+    ready = [n for n in nodes if indeg[n] == 0]
+    seen = 0
+    while ready:
+        n = ready.pop()
+        seen += 1
+        for m in succ[n]:
+            indeg[m] -= 1
+            if indeg[m] == 0:
+                ready.append(m)
+    if seen != len(nodes):
+        raise AssertionError("the ranks issue their batches in orders with no common global order "
+                             f"({len(nodes) - seen} transfers on a cycle)")
+
+
 def _nbytes(t: torch.Tensor) -> int:
     return t.numel() * t.element_size()
 
@@ -78,6 +196,7 @@ def bcast(t: torch.Tensor, src_global: int, group, world: bool = False) -> None:
         return _BACKEND.sync("bcast", _nbytes(t), group)
     if group is None and not world:
         return
+    _rec_coll("bcast", t, group)
     if world and not (dist.is_initialized() and dist.get_world_size() > 1):
         return
     w = dist.broadcast(t, src=src_global, group=group, async_op=True)
@@ -94,6 +213,7 @@ def allgather_inplace(out: torch.Tensor, my_index: int, group) -> None:
         return _BACKEND.sync("allgather", _nbytes(out) - _nbytes(out[my_index]), group)
     if group is None:
         return
+    _rec_coll("allgather", out, group)
     inp = out[my_index]
     if out.device.type == "cuda" and _nccl():
         w = dist.all_gather_into_tensor(out.view(-1), inp.reshape(-1),
@@ -111,6 +231,7 @@ def allreduce(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None) -> None:
         return _BACKEND.sync("allreduce", 2 * _nbytes(t), group)
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return
+    _rec_coll("allreduce", t, group)
     dist.all_reduce(t, op=op, group=group)
 
 
@@ -127,6 +248,7 @@ def p2p(sends=(), recvs=()) -> None:
         for t_, p_ in sends + recvs:
             per[p_] = per.get(p_, 0) + _nbytes(t_)
         return _BACKEND.sync("p2p", max(per.values()), None)
+    _rec_p2p(sends, recvs, None)
     if _nccl():
         ops = [dist.P2POp(dist.isend, t, p) for t, p in sends] + [dist.P2POp(dist.irecv, t, p) for t, p in recvs]
         with self_p2p():
@@ -180,6 +302,7 @@ def start_p2p(sends=(), recvs=(), group=None, hint=None) -> Optional[Pending]:
         return None
     if _BACKEND is not None:
         return _BACKEND.start_p2p(sends, recvs, group, hint)
+    _rec_p2p(sends, recvs, group)
     if _nccl() and any(t.device.type == "cuda" for t, _ in sends + recvs):
         ops = [dist.P2POp(dist.isend, t, p, group=group) for t, p in sends]
         ops += [dist.P2POp(dist.irecv, t, p, group=group) for t, p in recvs]

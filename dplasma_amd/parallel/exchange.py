@@ -19,6 +19,8 @@ from typing import Dict, List, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from . import comm
+
 from ..constants import dplasmaNoTrans
 from ..ops import tile_ops as ops
 from ..ops.batch import TileBatch
@@ -111,6 +113,7 @@ class ExchangePlan:
             ops.geadd(0, dplasmaNoTrans, 1.0, M.data, M.ld, 0.0, sendbuf, self.ld, tb, copy=True)
         out_splits = [c * nbe for c in self.recv_counts]
         in_splits = [c * nbe for c in self.send_counts]
+        comm._rec_coll("alltoall", None, None)
         w = dist.all_to_all_single(recv[: self.nremote * nbe], sendbuf[: self.nsend * nbe], out_splits,
                                    in_splits, async_op=True)
         w.wait()

@@ -268,8 +268,11 @@ class Transport:
                     pe.record(cs)
                     self._packed[x.xid] = pe
                     rt = x.recv_target(self._bases, rb)
+                    ops_ = x.p2p_ops(sb, rt)
+                    comm._rec_p2p([(o.tensor, o.peer) for o in ops_ if o.op is dist.isend],
+                                  [(o.tensor, o.peer) for o in ops_ if o.op is dist.irecv], None)
                     with comm.self_p2p():
-                        for w in dist.batch_isend_irecv(x.p2p_ops(sb, rt)) or ():
+                        for w in dist.batch_isend_irecv(ops_) or ():
                             w.wait()
                     x.do_unpack(rt, self._bases)
                     de = torch.cuda.Event()
@@ -293,6 +296,8 @@ class Transport:
             if x.recv_into is not None and dev.type == "cpu":
                 rb = x.recv_target(self._bases, rb)   # receive in place
             p2p = x.p2p_ops(sb, rb)
+            comm._rec_p2p([(o.tensor, o.peer) for o in p2p if o.op is dist.isend],
+                          [(o.tensor, o.peer) for o in p2p if o.op is dist.irecv], None)
             if comm.loopback():   # gloo cannot reach the rank itself: self pairs become local copies
                 comm._split_self([(o.tensor, o.peer) for o in p2p if o.op is dist.isend],
                                  [(o.tensor, o.peer) for o in p2p if o.op is dist.irecv])

@@ -111,8 +111,10 @@ class Taskpool:
             self._run_gpu_py(ctx)
         else:
             from ..utils import trace
+            from ..parallel import comm
             for ti in self.issue_order(ctx):
                 t = self.tasks[ti]
+                comm.LABEL = t.name
                 with trace.span(ctx, t.name, "task", gpu=False):
                     t.fn()
         self._t_run = t0
@@ -153,6 +155,7 @@ class Taskpool:
         return order
 
     def _run_gpu_py(self, ctx):
+        from ..parallel import comm
         from ..utils import trace
         cur = torch.cuda.current_stream(ctx.device)
         start = torch.cuda.Event()
@@ -167,6 +170,7 @@ class Taskpool:
             for d in t.deps:
                 if self.tasks[d].stream != t.stream:
                     s.wait_event(events[d])
+            comm.LABEL = t.name
             with torch.cuda.stream(s), trace.span(ctx, t.name, "task", s):
                 t.fn()
             if t.needs_event:
