@@ -79,18 +79,20 @@ struct DtrArgs {
   int rank;                 // >= 0: this launch's rank; -1: emulation (rank from the XCD)
   int epoch;
   int flags;                // bit 0: steal a ready head of another XCD's list when the own head is not ready;
-                            // bit 1: WINDOWED high-list claims (see claim_hi_window), else tickets;
-                            // bits 8-15 / 16-23: how long a ticket holder polls before helping (see below)
+                            // bits 8-15 / 16-23: how long a ticket holder polls before helping (see below);
+                            // bits 24-27: high-list segments scanned per claim (0: 8)
   int dil;                  // emulation: time dilation (= nranks); 1 otherwise
   long long ncnt;           // counters per rank
   const DtrTask* tasks;
   const int2* reqs;
   const long long* tab;     // per rank nt x nt: element offset (from the rank's A) of tile (i, j) at i + j nt
   const long long* xoff;    // per task: SEND / SENDW destination element offset (receive buffer / W)
-  int* cur;                 // cursors: [r] high list of rank r, [MAXR + x] low list of XCD x; PSTRIDE ints apart
-  int* claimed;             // windowed high-list claims (flags bit 1): one int per high-list position
+  int* cur;                 // cursors: [r] step low-water mark of rank r, [MAXR + x] low list of XCD x; PSTRIDE apart
   const int* hi;            // high lists (task ids), rank r's at [hi_off[r], hi_off[r + 1])
   int hi_off[MAXR + 1];
+  int nsteps;               // each rank's high list is nsteps FIFO segments (list order "step": one per panel)
+  const int* hs_off;        // per rank nsteps + 1 segment offsets (relative to hi_off[r])
+  int* scur;                // per rank x segment ticket cursors, PSTRIDE ints apart
   const int* lo;            // low lists, XCD x's at [lo_off[x], lo_off[x + 1])
   int lo_off[9];
   double* A[MAXR];          // rank r's tile storage base (process mode: [rank] only)
@@ -107,7 +109,7 @@ struct DtrArgs {
   double* Wp;               // nt x MAXB x MAXB x BLK  (published W blocks, T-layout)
   int* prog;                // nt x 2 x MAXB x PSTRIDE: tile-step flags, then W-column flags
   int* info;
-  long long* trace;         // optional (DPLASMA_DTR_TRACE): per task {start, end, wg << 8 | xcd}, 100 MHz ticks
+  long long* trace;         // optional (DPLASMA_DTR_TRACE): per task {start, end, wg << 8 | xcd, visible}, 100 MHz ticks
 };
 
 constexpr int NBT = 512;    // tile size
@@ -194,68 +196,6 @@ __device__ inline int claim_low(const DtrArgs& g, int xcd, int x0, int nx, int r
     if (t == -1) all_done = false;
   }
   return all_done ? -2 : -1;
-}
-
-// readiness of task t checked by ONE lane (its requirements one after the other): the windowed claim
-// evaluates 64 candidate tasks at once, one per lane
-__device__ inline bool ready_lane(const DtrArgs& g, int t, int rk) {
-  const DtrTask* tp = g.tasks + t;
-  const int rb = tp->req_beg, nr = tp->nreq;
-  const int* cnt = g.cnt[rk];
-  const bool em = emul(g), sy = sysmode(g);
-  const unsigned long long now = em ? now_t() : 0;
-  for (int q = 0; q < nr; ++q) {
-    const int2 rq = g.reqs[rb + q];
-    const int v = sy ? ld_sys(cnt + rq.x) : ld_sc1(cnt + rq.x);
-    if (v < rq.y) return false;
-    if (em && v == rq.y && ld_sc1(g.vis + (size_t)rk * g.ncnt + rq.x) > now) return false;
-  }
-  return true;
-}
-
-// WINDOWED claim on rank rk's high list (wave 0; flags bit 1): lane l looks at list position head + l and
-// the wave takes the FIRST unclaimed, ready one (CAS on its claim word), so a head that waits on a
-// dependency no longer holds up ready critical tasks behind it (the ticket scheme hands positions out in
-// order and only for a ready head).  A POTRF(k, b > 0) is eligible only once the entry before it -- its
-// group's block b - 1 -- is claimed: the 16 cooperating workgroups start in block order, so a running
-// block only ever waits for running blocks.  The head cursor skips the claimed prefix.  Progress: the
-// earliest unclaimed task of the topological order is the head of its list once its predecessors are
-// claimed, hence in the window.  Returns the task, -1 (nothing ready) or -2 (list exhausted).
-__device__ inline int claim_hi_window(const DtrArgs& g, int rk) {
-  const int l = threadIdx.x & 63;
-  int* hcur = g.cur + PSTRIDE * rk;
-  const int hbeg = g.hi_off[rk], hn = g.hi_off[rk + 1] - hbeg;
-  int* cl = g.claimed + hbeg;
-  const int* lst = g.hi + hbeg;
-  const int h = __builtin_amdgcn_readfirstlane(ld_sc1(hcur));
-  if (h >= hn) return -2;
-  const int q = h + l;
-  const bool in = q < hn;
-  const int t = in ? lst[q] : -1;
-  int c = in ? ld_sc1(cl + q) : 1;
-  const int cprev = __shfl_up(c, 1, 64);
-  bool rdy = in && c == 0 && ready_lane(g, t, rk);
-  if (rdy && g.tasks[t].type == T_POTRF && g.tasks[t].r > 0 && l > 0 && cprev == 0) rdy = false;
-  unsigned long long m = __builtin_amdgcn_ballot_w64(rdy);
-  int got = -1, gotl = -1;
-  while (m) {
-    const int L = __builtin_ctzll(m);
-    int won = 0;
-    if (l == L) won = atomicCAS(cl + q, 0, 1) == 0;
-    won = __builtin_amdgcn_readlane(won, L);
-    if (won) {
-      got = __builtin_amdgcn_readlane(t, L);
-      gotl = L;
-      break;
-    }
-    m &= m - 1;
-  }
-  // advance the head over the claimed prefix of the window
-  if (l == gotl) c = 1;
-  const unsigned long long un = __builtin_amdgcn_ballot_w64(c == 0);
-  const int f = un ? __builtin_ctzll(un) : 64;
-  if (f > 0 && l == 0) atomicCAS(hcur, h, h + f);
-  return got;
 }
 
 // tile offsets of rank rk (element offsets from g.A[rk]): local tiles and received copies
@@ -600,35 +540,48 @@ __global__ __launch_bounds__(256, 2) void k_dtr_potrf(const DtrArgs* __restrict_
       if (ld_sc1(g.info) == -1000) {
         t = -2;
       } else {
-        int* hcur = g.cur + PSTRIDE * rk;
-        const int hbeg = g.hi_off[rk], hn = g.hi_off[rk + 1] - hbeg;
-        if ((g.flags & 2) && !hi_done) {
-          t = claim_hi_window(g, rk);
-          if (t == -2) {
+        const int hbeg = g.hi_off[rk];
+        if (ticket < 0 && !hi_done) {
+          // the high list is nsteps FIFO segments (one per panel step with the "step" order, else one): a
+          // ticket goes out for a READY head of one of the first STEPW segments not yet handed out completely
+          // (lowest first) -- a task of step k+1 (POTRF(k+1)) is not held up behind step k's updates that wait
+          // for remote strips.  A ticket only for a ready head: a workgroup holding a not-yet-ready critical
+          // task would run low-list tasks meanwhile and come back up to one bulk task late -- the 16 POTRF
+          // workgroups of a tile would then start spread over ~0.4 ms and wait for each other.
+          // Progress: the earliest unclaimed task of the (step-major) topological order is the head of the
+          // lowest segment that is not handed out, which every scan looks at first.
+          const int stepw = ((unsigned)g.flags >> 24) & 15u ? (((unsigned)g.flags >> 24) & 15u) : 8;
+          const int ns = g.nsteps;
+          const int* so = g.hs_off + (size_t)rk * (ns + 1);
+          int* lw = g.cur + PSTRIDE * rk;
+          const int s0 = __builtin_amdgcn_readfirstlane(ld_sc1(lw));
+          if (s0 >= ns) {
             hi_done = true;
-            t = -1;
-          }
-        } else if (ticket < 0 && !hi_done) {
-          // a ticket only for a ready head: a workgroup holding a not-yet-ready critical task would run
-          // low-list tasks meanwhile and come back up to one bulk task late -- the 16 POTRF workgroups of
-          // a tile would then start spread over ~0.4 ms and wait for each other
-          const int h = __builtin_amdgcn_readfirstlane(ld_sc1(hcur));
-          if (h >= hn) {
-            hi_done = true;
-          } else if (ready_wave(g, __builtin_amdgcn_readfirstlane(g.hi[hbeg + h]), rk)) {
-            int tk = 0;
-            if (tid == 0) tk = atomicAdd(hcur, 1);
-            tk = __builtin_amdgcn_readfirstlane(tk);
-            if (tk < hn) {
-              ticket = tk;
-              ticket_t0 = now_t();
-            } else {
-              hi_done = true;
+          } else {
+            const int s1 = s0 + stepw < ns ? s0 + stepw : ns;
+            for (int sg = s0; sg < s1; ++sg) {
+              int* sc = g.scur + ((size_t)rk * ns + sg) * PSTRIDE;
+              const int b = so[sg], n = so[sg + 1] - b;
+              const int h = __builtin_amdgcn_readfirstlane(ld_sc1(sc));
+              if (h >= n) {
+                if (sg == s0 && tid == 0) atomicCAS(lw, s0, s0 + 1);   // segment handed out: raise the mark
+                continue;
+              }
+              if (ready_wave(g, __builtin_amdgcn_readfirstlane(g.hi[hbeg + b + h]), rk)) {
+                int tk = 0;
+                if (tid == 0) tk = atomicAdd(sc, 1);
+                tk = __builtin_amdgcn_readfirstlane(tk);
+                if (tk < n) {
+                  ticket = b + tk;
+                  ticket_t0 = now_t();
+                  break;
+                }
+              }
             }
           }
         }
         bool help = true;
-        if (t < 0 && ticket >= 0) {
+        if (ticket >= 0) {
           const int th = __builtin_amdgcn_readfirstlane(g.hi[hbeg + ticket]);
           if (ready_wave(g, th, rk)) {
             t = th;
@@ -655,8 +608,10 @@ __global__ __launch_bounds__(256, 2) void k_dtr_potrf(const DtrArgs* __restrict_
       }
       if (t >= 0) {
         // the predecessors' bytes, fresh in this CU (system scope: a peer process wrote some of them)
+        // (flags bit 2: the system-scope acquire also in one process -- a measurement knob: it invalidates the
+        // XCD's L2 as well, see profiles/r5_dtr_dist_emulation.txt)
         if (tid == 0) {
-          if (sysmode(g)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+          if (sysmode(g) || (g.flags & 4)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
           else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -691,19 +646,22 @@ __global__ __launch_bounds__(256, 2) void k_dtr_potrf(const DtrArgs* __restrict_
     // release: every wave's stores drained, then one agent-scope release and the counter bump
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    unsigned long long due = 0;
+    if (tid == 0 && tk.inc >= 0 && emul(g)) due = emul_due(g, tk, rk, t_start, now_t());
     if (tid == 0 && g.trace) {
-      long long* tr = g.trace + 3 * (size_t)t;
+      long long* tr = g.trace + 4 * (size_t)t;
       tr[0] = (long long)t_start;
       tr[1] = (long long)now_t();
       tr[2] = ((long long)blockIdx.x << 8) | xcd;
+      // emulation: when the completion becomes visible; otherwise the number of times the task ran (1)
+      if (emul(g)) tr[3] = (long long)due;
+      else atomicAdd((unsigned long long*)(tr + 3), 1ULL);
     }
     if (tid == 0 && tk.inc >= 0) {
       const bool remote = tk.type == T_SEND || tk.type == T_SENDW;
       const int tr_ = remote ? tk.j : rk;
-      if (emul(g)) {
-        const unsigned long long due = emul_due(g, tk, rk, t_start, now_t());
+      if (emul(g))
         __hip_atomic_fetch_max(g.vis + (size_t)tr_ * g.ncnt + tk.inc, due, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
       if (remote && sysmode(g)) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -737,8 +695,8 @@ DPL_API int dpl_dtr_potrf(const void* args_dev, int nwg, hipStream_t st) {
 DPL_API long long dpl_dtr_field(const char* name) {
   DTR_FIELD(ld) DTR_FIELD(nt) DTR_FIELD(nranks) DTR_FIELD(rank) DTR_FIELD(epoch) DTR_FIELD(flags) DTR_FIELD(dil)
   DTR_FIELD(ncnt) DTR_FIELD(tasks) DTR_FIELD(reqs) DTR_FIELD(tab) DTR_FIELD(xoff) DTR_FIELD(cur) DTR_FIELD(hi)
-  DTR_FIELD(claimed)
-  DTR_FIELD(hi_off) DTR_FIELD(lo) DTR_FIELD(lo_off) DTR_FIELD(A) DTR_FIELD(recv) DTR_FIELD(W) DTR_FIELD(cnt)
+
+  DTR_FIELD(hi_off) DTR_FIELD(nsteps) DTR_FIELD(hs_off) DTR_FIELD(scur) DTR_FIELD(lo) DTR_FIELD(lo_off) DTR_FIELD(A) DTR_FIELD(recv) DTR_FIELD(W) DTR_FIELD(cnt)
   DTR_FIELD(vis) DTR_FIELD(link) DTR_FIELD(bw_bpt) DTR_FIELD(lat_t) DTR_FIELD(Mw) DTR_FIELD(Sw) DTR_FIELD(Lp)
   DTR_FIELD(Wp) DTR_FIELD(prog) DTR_FIELD(info) DTR_FIELD(trace)
   if (!std::strcmp(name, "size")) return (long long)sizeof(DtrArgs);

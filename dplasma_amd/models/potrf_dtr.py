@@ -91,11 +91,22 @@ class _Plan:
         # inputs have a smaller deadline, or the same deadline and a smaller column or phase.  The column-
         # major high list hands the tickets of a whole column's updates out before that column's first TRSM,
         # which puts every row of a column on the critical chain (profiles/r5_dtr_dist_emulation.txt).
+        # "rowpipe": the column order, but inside a column the high list runs row by row -- the updates of
+        # tile (i, j), then its TRSM strips (and their sends) -- so TRSM(j+1, j) waits for row j+1's inputs
+        # only, not for the whole column's (a distributed grid receives the previous panel's strips row by
+        # row; the in-order tickets would otherwise put the entire previous panel on the critical chain)
+        # "step": both lists by the panel step that makes a task ready -- POTRF(k), W_k's sends, the TRSMs of
+        # panel k (row by row, each strip followed by its sends), then every update whose run ends at panel k
+        # (column by column: the next diagonal tile first).  An update is placed where its inputs appear, not
+        # under its output column (the column order parks the look-ahead update of the next block's first
+        # diagonal tile behind that block's panels: profiles/r5_dtr_dist_emulation.txt).
         lo_order = lo_order or os.environ.get("DPLASMA_DTR_LO_ORDER", "column")
-        if lo_order not in ("panel", "column", "deadline"):
-            raise ValueError("DPLASMA_DTR_LO_ORDER must be panel, column or deadline")
+        if lo_order not in ("panel", "column", "deadline", "rowpipe", "step"):
+            raise ValueError("DPLASMA_DTR_LO_ORDER must be panel, column, rowpipe, step or deadline")
         self.order = lo_order
         dl = lo_order == "deadline"
+        rp = lo_order == "rowpipe"
+        sp = lo_order == "step"
         S = 4 * nt
         self.nt, self.S, self.D = nt, S, D
         # blocks of D panels; single panels once fewer than min_tiles columns remain (the chain-bound tail:
@@ -173,16 +184,27 @@ class _Plan:
                 reqs[:, 2 + 2 * q, 1] = np.where(diag, -1, F[4 * j + c, k])
             ver[Ci] += 1
             kl = k0 + nk - 1
+            if sp:
+                key = np.stack([np.full(n, kl), np.full(n, 3), j, i, r, c], 1)
+                if prio_hi:
+                    return emit(T_UPD, i, j, k0, r, c, nk, Ci, reqs, None, "hi", key=key)
+                return emit(T_UPD, i, j, k0, r, c, nk, Ci, reqs, None, "lo", key=key, xcd=j % 8)
             if dl:
                 key = np.stack([np.where(i == j, i, i - 1), j, np.where(i == j, 0, 2), np.full(n, kl), r, c], 1)
                 if prio_hi:
                     return emit(T_UPD, i, j, k0, r, c, nk, Ci, reqs, None, "hi", key=key)
                 return emit(T_UPD, i, j, k0, r, c, nk, Ci, reqs, None, "lo", key=key, xcd=j % 8)
+            if prio_hi and rp:
+                # key: column, phase (0 diagonal tile, 2 other rows), row, 0 (before the row's TRSM), last panel,
+                # sub-tile
+                key = np.stack([j, np.where(i == j, 0, 2), np.where(i == j, 0, i), np.zeros(n, int),
+                                np.full(n, kl), 4 * r + c], 1)
+                return emit(T_UPD, i, j, k0, r, c, nk, Ci, reqs, None, "hi", key=key)
             if prio_hi:
                 # key: column, phase (0 diagonal tile, 2 other rows), last panel, row, sub-tile
                 key = np.stack([j, np.where(i == j, 0, 2), np.full(n, kl), i, r, c], 1)
                 return emit(T_UPD, i, j, k0, r, c, nk, Ci, reqs, None, "hi", key=key)
-            if lo_order == "column":
+            if lo_order in ("column", "rowpipe"):
                 key = np.stack([block_of[j], np.full(n, kl), j, i, r, c], 1)
             else:
                 key = np.stack([np.full(n, kl), j, i, r, c], 1)
@@ -198,7 +220,9 @@ class _Plan:
                 reqs[:, :, 0] = dsc
                 reqs[:, :, 1] = ver[dsc]
                 b = np.arange(MAXB)
-                if dl:
+                if sp:
+                    key = np.stack([np.full(MAXB, k), b * 0, b * 0, b * 0, b, b * 0], 1)
+                elif dl:
                     key = np.stack([np.full(MAXB, k), np.full(MAXB, k), np.ones(MAXB, int), b * 0, b, b * 0], 1)
                 else:
                     key = np.stack([np.full(MAXB, k), np.ones(MAXB, int), np.zeros(MAXB, int), b, b * 0, b * 0], 1)
@@ -216,8 +240,12 @@ class _Plan:
                     mark = sc(4 * ii + r, 4 * k)
                     ver[mark] += 1
                     F[4 * ii + r, k] = ver[mark]
-                    if dl:
+                    if sp:
+                        key = np.stack([np.full(n, k), np.full(n, 2), ii, r, r * 0, r * 0], 1)
+                    elif dl:
                         key = np.stack([ii - 1, np.full(n, k), np.full(n, 3), np.zeros(n, int), r, r * 0], 1)
+                    elif rp:
+                        key = np.stack([np.full(n, k), np.full(n, 2), ii, np.ones(n, int), r, r * 0], 1)
                     else:
                         key = np.stack([np.full(n, k), np.full(n, 3), np.zeros(n, int), ii, r, r * 0], 1)
                     emit(T_TRSM, ii, np.full(n, k), k, r, 0, 0, mark, reqs, None, "hi", key=key)
@@ -281,8 +309,8 @@ class ArgsImage:
     laid out by the device compiler, not mirrored here)."""
 
     _LL = ("ld", "ncnt", "bw_bpt", "lat_t")
-    _INT = ("nt", "nranks", "rank", "epoch", "flags", "dil")
-    _PTR = ("tasks", "reqs", "tab", "xoff", "cur", "claimed", "hi", "lo", "vis", "link", "Mw", "Sw", "Lp", "Wp",
+    _INT = ("nt", "nranks", "rank", "epoch", "flags", "dil", "nsteps")
+    _PTR = ("tasks", "reqs", "tab", "xoff", "cur", "hs_off", "scur", "hi", "lo", "vis", "link", "Mw", "Sw", "Lp", "Wp",
             "prog", "info", "trace")
     _PARR = ("A", "recv", "W", "cnt")
     _IARR = ("hi_off", "lo_off")
@@ -317,16 +345,29 @@ class ArgsImage:
             struct.pack_into(f"<{n}i", self.buf, o, *[int(x) for x in vals])
 
 
+def step_segments(keys_sorted: np.ndarray, order: str, nt: int) -> np.ndarray:
+    """Offsets (nt + 1) of the per-step FIFO segments of one rank's high list (sorted by key): with the "step"
+    order one segment per panel (key column 0), else one segment holding the whole list."""
+    n = len(keys_sorted)
+    if order != "step":
+        return np.array([0] + [n] * nt, dtype=np.int32)
+    steps = keys_sorted[:, 0] if n else np.zeros(0, dtype=np.int64)
+    return np.searchsorted(steps, np.arange(nt + 1), side="left").astype(np.int32)
+
+
 def flags_from_env() -> int:
     # DPLASMA_DTR_STEAL=1: a workgroup whose own XCD list head waits on a dependency takes a ready head of
     # another XCD's list (measurement knob; default: steal only from exhausted lists)
     fl = 1 if os.environ.get("DPLASMA_DTR_STEAL", "0") == "1" else 0
     # DPLASMA_DTR_HOLD="potrf_us,other_us": how long a high-list ticket whose task is not ready yet polls before
     # it runs a low-list task meanwhile (measurement knob; default 50 us for POTRF tickets, 0 for the others)
-    # DPLASMA_DTR_CLAIM=window: windowed high-list claims (the first ready task among the next 64 positions)
-    # instead of in-order tickets
-    if os.environ.get("DPLASMA_DTR_CLAIM", "ticket") == "window":
-        fl |= 2
+    # DPLASMA_DTR_SYSACQ=1: system-scope acquire before every task (measurement knob)
+    if os.environ.get("DPLASMA_DTR_SYSACQ", "0") == "1":
+        fl |= 4
+    # DPLASMA_DTR_STEPW=w: step segments of the high list scanned per claim (1..15; default 8)
+    sw = int(os.environ.get("DPLASMA_DTR_STEPW", "0"))
+    if sw:
+        fl |= (min(15, max(1, sw)) << 24)
     hold = os.environ.get("DPLASMA_DTR_HOLD")
     if hold:
         hp, ho = (int(x) for x in hold.split(","))
@@ -396,7 +437,9 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     tab_d = up(tab)
     cnt = torch.zeros(plan.ncnt, dtype=torch.int32, device=dev)
     cur = torch.zeros((img.maxr + 8) * PST, dtype=torch.int32, device=dev)
-    claimed = torch.zeros(len(plan.hi) + 1, dtype=torch.int32, device=dev)
+    hs = step_segments(plan.key[plan.hi], plan.order, nt)
+    hs_d = up(hs)
+    scur = torch.zeros(nt * PST, dtype=torch.int32, device=dev)
     # per-panel workspaces (HBM is plentiful: ~6 MB per panel, nothing recycled, no WAR edges)
     W = torch.zeros(nt * NBT * NBT, dtype=torch.float64, device=dev)
     scr = PotrfScratch(nt, dev, PST)
@@ -410,7 +453,9 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     img.set("reqs", reqs_d.data_ptr())
     img.set("tab", tab_d.data_ptr())
     img.set("cur", cur.data_ptr())
-    img.set("claimed", claimed.data_ptr())
+    img.set("nsteps", nt)
+    img.set("hs_off", hs_d.data_ptr())
+    img.set("scur", scur.data_ptr())
     img.set("hi", hi_d.data_ptr())
     img.set("hi_off", [0, len(plan.hi)])
     img.set("lo", lo_d.data_ptr())
@@ -424,7 +469,7 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     # DPLASMA_DTR_TRACE=1: per-task {start, end, workgroup << 8 | xcd} (s_memrealtime, 100 MHz) in tp.dtr_trace
     trace = None
     if os.environ.get("DPLASMA_DTR_TRACE", "0") == "1":
-        trace = torch.zeros(3 * len(plan.tasks), dtype=torch.int64, device=dev)
+        trace = torch.zeros(4 * len(plan.tasks), dtype=torch.int64, device=dev)
         img.set("trace", trace.data_ptr())
     tp.dtr_trace = trace
     nbytes = img.size
@@ -436,7 +481,7 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     # progress needs a workgroup on every XCD (a low list is another XCD's to steal only once that XCD's
     # own list is exhausted) and the 16 cooperating POTRF workgroups co-resident: at least 64 of them
     nwg = max(64, min(nwg, 2 * ncu))
-    tp._keep = (tasks_d, reqs_d, hi_d, lo_d, tab_d, cnt, cur, claimed, W, scr, host, args_d)
+    tp._keep = (tasks_d, reqs_d, hi_d, lo_d, tab_d, cnt, cur, hs_d, scur, W, scr, host, args_d)
     tp.dtr_plan = plan
 
     def f_run():
@@ -446,7 +491,7 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
         args_d.copy_(host, non_blocking=True)
         cnt.zero_()
         cur.zero_()
-        claimed.zero_()
+        scur.zero_()
         _lib.check(lib.dpl_dtr_potrf(args_d.data_ptr(), nwg, _lib.stream_ptr()), "dtr_potrf")
 
     tp.task("DTR_POTRF", "update", f_run)

@@ -98,6 +98,10 @@ class DistPlan:
             sreq[:ns, 1] = base.F[Is, ks]            # the strip's "solved" marker value on the producer
             if base.order == "deadline":
                 keys[:ns] = np.stack([Is // 4 - 1, ks, np.full(ns, 3), np.zeros(ns, int), Is % 4, 1 + dest], 1)
+            elif base.order == "rowpipe":
+                keys[:ns] = np.stack([ks, np.full(ns, 2), Is // 4, np.ones(ns, int), Is % 4, 1 + dest], 1)
+            elif base.order == "step":
+                keys[:ns] = np.stack([ks, np.full(ns, 2), Is // 4, Is % 4, 1 + dest, np.zeros(ns, int)], 1)
             else:
                 keys[:ns] = np.stack([ks, np.full(ns, 3), np.zeros(ns, int), Is // 4, Is % 4, 1 + dest], 1)
             sown[:ns] = self._owner(Is // 4, ks)
@@ -111,6 +115,8 @@ class DistPlan:
             sreq[sl, 0], sreq[sl, 1] = WB + kk, MAXB
             if base.order == "deadline":
                 keys[sl] = np.stack([kk, kk, np.ones(nw, int), np.ones(nw, int), MAXB + cb, dest], 1)
+            elif base.order == "step":
+                keys[sl] = np.stack([kk, np.ones(nw, int), np.zeros(nw, int), np.zeros(nw, int), cb, dest], 1)
             else:
                 keys[sl] = np.stack([kk, np.ones(nw, int), np.zeros(nw, int), MAXB + cb, dest, np.zeros(nw, int)], 1)
             sown[sl] = self._owner(kk, kk)
@@ -170,6 +176,7 @@ class DistPlan:
             pick = (col // self.Q) % len(xs)
             for q, x in enumerate(xs):
                 lo_lists[x] = np.concatenate([lo_lists[x], lo[pick == q].astype(np.int32)])
+        self.hs_off = np.concatenate([D.step_segments(self.key[h], self.base.order, self.nt) for h in hi_parts])
         hi = np.concatenate(hi_parts) if hi_parts else np.zeros(0, dtype=np.int32)
         lo_off = np.zeros(9, dtype=np.int64)
         lo_off[1:] = np.cumsum([len(x) for x in lo_lists])
@@ -213,7 +220,7 @@ class Emulation:
         self.ctx, self.N, self.P, self.Q, self.nr = ctx, N, P, Q, nr
         nt = N // NBT
         Dd = Dd or max(1, int(os.environ.get("DPLASMA_DTR_DEFER", "4")))
-        self.plan = plan = DistPlan(nt, Dd, P, Q, lo_order=order or os.environ.get("DPLASMA_DTR_LO_ORDER", "deadline"))
+        self.plan = plan = DistPlan(nt, Dd, P, Q, lo_order=order or os.environ.get("DPLASMA_DTR_LO_ORDER", "step"))
         lib = _lib.load()
         self.lib = lib
         img = D.ArgsImage(lib)
@@ -236,7 +243,8 @@ class Emulation:
         self.vis = torch.zeros(nr * plan.ncnt, dtype=torch.int64, device=dev)
         self.link = torch.zeros(img.maxr * img.maxr, dtype=torch.int64, device=dev)
         self.cur = torch.zeros((img.maxr + 8) * img.pstride, dtype=torch.int32, device=dev)
-        self.claimed = torch.zeros(len(hi) + 1, dtype=torch.int32, device=dev)
+        self.hs_d = up(plan.hs_off)
+        self.scur = torch.zeros(nr * nt * img.pstride, dtype=torch.int32, device=dev)
         tabs = []
         for r in range(nr):
             rb = (self.recv[r].data_ptr() - self.A[r].data.data_ptr())
@@ -250,7 +258,7 @@ class Emulation:
         self.lo_d = up(lo if len(lo) else np.zeros(1, dtype=np.int32))
         self.info = torch.zeros(1, dtype=torch.int32, device=dev)
         self.scr = D.PotrfScratch(nt, dev, img.pstride)
-        self.trace = torch.zeros(3 * len(plan.tasks), dtype=torch.int64, device=dev) if trace else None
+        self.trace = torch.zeros(4 * len(plan.tasks), dtype=torch.int64, device=dev) if trace else None
         img.set("ld", NBT)
         img.set("nt", nt)
         img.set("nranks", nr)
@@ -262,7 +270,9 @@ class Emulation:
         img.set("tab", self.tab_d.data_ptr())
         img.set("xoff", self.xoff_d.data_ptr())
         img.set("cur", self.cur.data_ptr())
-        img.set("claimed", self.claimed.data_ptr())
+        img.set("nsteps", nt)
+        img.set("hs_off", self.hs_d.data_ptr())
+        img.set("scur", self.scur.data_ptr())
         img.set("hi", self.hi_d.data_ptr())
         img.set("hi_off", hi_off)
         img.set("lo", self.lo_d.data_ptr())
@@ -298,7 +308,7 @@ class Emulation:
         self.epoch = self.epoch % ((1 << 25) - 1) + 1
         self.img.set("epoch", self.epoch)
         self.args_d.copy_(torch.frombuffer(bytearray(self.img.buf), dtype=torch.uint8))
-        for t in (self.cnt, self.vis, self.link, self.cur, self.claimed, self.info):
+        for t in (self.cnt, self.vis, self.link, self.cur, self.scur, self.info):
             t.zero_()
         torch.cuda.synchronize()
         t0 = time.perf_counter()

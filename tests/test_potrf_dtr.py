@@ -78,6 +78,19 @@ def _emulate(plan, A=None, nb=None, P=8, seed=0, steal=False):
     # low lists per XCD
     # (own list first, another XCD's only once the own one is exhausted)
     hi = lists[0]
+    seg = D.step_segments(plan.key[plan.hi], plan.order, plan.nt)   # the kernel's per-step FIFO segments
+    scur = [int(seg[q]) for q in range(len(seg) - 1)]
+    low = [0]
+
+    def take_ticket(force_race):
+        # a ticket for a ready head of one of the first 8 segments not handed out (lowest first)
+        while low[0] < len(scur) and scur[low[0]] >= seg[low[0] + 1]:
+            low[0] += 1
+        for q in range(low[0], min(low[0] + 8, len(scur))):
+            if scur[q] < seg[q + 1] and (ready(int(hi[scur[q]])) or (force_race and q == low[0])):
+                scur[q] += 1
+                return scur[q] - 1
+        return None
     hcur = 0
     ticket = [None] * P
     age = [0] * P
@@ -105,10 +118,11 @@ def _emulate(plan, A=None, nb=None, P=8, seed=0, steal=False):
         for wk in rng.permutation(P):
             if busy[wk]:
                 continue
-            if ticket[wk] is None and hcur < len(hi) and (ready(int(hi[hcur])) or rng.random() < 0.05):
+            if ticket[wk] is None:
                 # a ticket for a ready head (and, rarely, a raced one whose task is not ready yet)
-                ticket[wk], age[wk] = hcur, 0
-                hcur += 1
+                tk = take_ticket(rng.random() < 0.05)
+                if tk is not None:
+                    ticket[wk], age[wk] = tk, 0
             t = None
             if ticket[wk] is not None:
                 th = int(hi[ticket[wk]])
@@ -133,7 +147,8 @@ def _emulate(plan, A=None, nb=None, P=8, seed=0, steal=False):
             finish(t, v)
             progressed = True
         if not progressed:
-            if hcur >= len(hi) and all(x is None for x in ticket) and all(cur[li] >= len(lists[li]) for li in range(1, 9)):
+            if all(scur[q] >= seg[q + 1] for q in range(len(scur))) and all(x is None for x in ticket) and \
+                    all(cur[li] >= len(lists[li]) for li in range(1, 9)):
                 break
             stall += 1
             assert stall < 50, f"schedule stalled: tickets {ticket}, heads {[cur[li] for li in range(9)]}"
@@ -143,7 +158,7 @@ def _emulate(plan, A=None, nb=None, P=8, seed=0, steal=False):
     return order
 
 
-@pytest.mark.parametrize("lo_order", ["column", "panel", "deadline"])
+@pytest.mark.parametrize("lo_order", ["column", "panel", "deadline", "rowpipe", "step"])
 @pytest.mark.parametrize("nt,defer", [(1, 4), (3, 4), (9, 4), (12, 2), (10, 3)])
 def test_dtr_plan_lists_and_progress(nt, defer, lo_order):
     plan = D._Plan(nt, defer, lo_order)
@@ -157,7 +172,7 @@ def test_dtr_plan_lists_and_progress(nt, defer, lo_order):
         _emulate(plan, P=(8, 13, 40)[seed], seed=seed, steal=True)
 
 
-@pytest.mark.parametrize("lo_order", ["column", "panel", "deadline"])
+@pytest.mark.parametrize("lo_order", ["column", "panel", "deadline", "rowpipe", "step"])
 @pytest.mark.parametrize("nt,defer,min_tiles", [(5, 2, 0), (7, 4, 0), (11, 4, 6)])
 def test_dtr_plan_numerics(nt, defer, min_tiles, lo_order):
     nb = 16
@@ -173,7 +188,7 @@ def test_dtr_plan_numerics(nt, defer, min_tiles, lo_order):
 
 
 # ------------------------------------------------------------------------------- distributed DTR
-def _emulate_dist(dplan, xcds_of, A=None, nb=None, wpx=2, seed=0, window=False):
+def _emulate_dist(dplan, xcds_of, A=None, nb=None, wpx=2, seed=0):
     """The claim protocol of every rank of a P x Q grid (models/potrf_dtr_dist.py), with wpx workers per
     XCD, random completion order and, with A, per-rank storage: a rank reads its own tiles, its receive
     slots (written only by SEND tasks) and its own W_k (computed by POTRF, or written by SENDW) -- a
@@ -182,6 +197,19 @@ def _emulate_dist(dplan, xcds_of, A=None, nb=None, wpx=2, seed=0, window=False):
     tasks, reqs, nr, nt = dplan.tasks, dplan.reqs, dplan.nranks, dplan.nt
     hi, hi_off, lo, lo_off = dplan.lists(xcds_of)
     cnt = np.zeros((nr, dplan.ncnt), dtype=np.int64)
+    segs = dplan.hs_off.reshape(nr, -1)                 # per-rank step segments (relative to hi_off[r])
+    scur = [[int(hi_off[r] + segs[r][q]) for q in range(segs.shape[1] - 1)] for r in range(nr)]
+    sl = [0] * nr
+
+    def take_ticket(r, force_race):
+        end = lambda q: hi_off[r] + segs[r][q + 1]   # noqa: E731
+        while sl[r] < len(scur[r]) and scur[r][sl[r]] >= end(sl[r]):
+            sl[r] += 1
+        for q in range(sl[r], min(sl[r] + 8, len(scur[r]))):
+            if scur[r][q] < end(q) and (ready(int(hi[scur[r][q]]), r) or (force_race and q == sl[r])):
+                scur[r][q] += 1
+                return scur[r][q] - 1
+        return None
     hcur = [hi_off[r] for r in range(nr)]
     lcur = [lo_off[x] for x in range(8)]
     s = nb // 4 if nb else None
@@ -268,27 +296,6 @@ def _emulate_dist(dplan, xcds_of, A=None, nb=None, wpx=2, seed=0, window=False):
                     return None        # the own head waits: no stealing while the own list lasts
         return None
 
-    hclaimed = np.zeros(len(hi) + 1, dtype=bool)
-
-    def claim_window(r):
-        # the kernel's windowed claim (DtrArgs.flags bit 1): the first unclaimed ready task among the next 64
-        # positions; POTRF(k, b > 0) only once the entry before it is claimed; the head skips the claimed prefix
-        h = hcur[r]
-        end = min(h + 64, hi_off[r + 1])
-        got = None
-        for q in range(h, end):
-            t = int(hi[q])
-            if hclaimed[q] or not ready(t, r):
-                continue
-            if tasks["type"][t] == T_POTRF and tasks["r"][t] > 0 and q > h and not hclaimed[q - 1]:
-                continue
-            hclaimed[q] = True
-            got = t
-            break
-        while hcur[r] < hi_off[r + 1] and hclaimed[hcur[r]]:
-            hcur[r] += 1
-        return got
-
     stall = 0
     while True:
         progressed = False
@@ -296,19 +303,8 @@ def _emulate_dist(dplan, xcds_of, A=None, nb=None, wpx=2, seed=0, window=False):
             if busy[w]:
                 continue
             r, x = workers[w]
-            if window:
-                t = claim_window(r)
-                if t is None:
-                    t = try_low(r, x)
-                if t is None:
-                    continue
-                inflight.append((t, r, start(t, r), w))
-                busy[w] = True
-                progressed = True
-                continue
-            if ticket[w] is None and hcur[r] < hi_off[r + 1] and (ready(int(hi[hcur[r]]), r) or rng.random() < 0.05):
-                ticket[w] = hcur[r]
-                hcur[r] += 1
+            if ticket[w] is None:
+                ticket[w] = take_ticket(r, rng.random() < 0.05)
             t = None
             if ticket[w] is not None:
                 th = int(hi[ticket[w]])
@@ -328,7 +324,8 @@ def _emulate_dist(dplan, xcds_of, A=None, nb=None, wpx=2, seed=0, window=False):
             finish(t, r, v)
             progressed = True
         if not progressed:
-            if all(hcur[r] >= hi_off[r + 1] for r in range(nr)) and all(tk is None for tk in ticket) and \
+            if all(scur[r][q] >= hi_off[r] + segs[r][q + 1] for r in range(nr) for q in range(len(scur[r]))) and \
+                    all(tk is None for tk in ticket) and \
                     all(lcur[y] >= lo_off[y + 1] for y in range(8)):
                 break
             stall += 1
@@ -353,7 +350,7 @@ def _xcds(nr, mode):
     return {r: [r % 8] for r in range(nr)}   # (one list per rank is enough for the protocol check)
 
 
-@pytest.mark.parametrize("order", ["column", "deadline"])
+@pytest.mark.parametrize("order", ["column", "rowpipe", "step"])
 @pytest.mark.parametrize("grid", [(1, 1), (1, 2), (2, 1), (2, 2), (2, 4)])
 @pytest.mark.parametrize("nt,defer", [(4, 2), (9, 4), (12, 3)])
 def test_dtr_dist_plan_progress(grid, nt, defer, order):
@@ -369,10 +366,9 @@ def test_dtr_dist_plan_progress(grid, nt, defer, order):
     assert (dplan._owner(snd["i"], snd["k0"]) != snd["j"]).all()
     for seed in range(2):
         _emulate_dist(dplan, _xcds(nr, "emulate"), wpx=1 + seed, seed=seed)
-        _emulate_dist(dplan, _xcds(nr, "emulate"), wpx=1 + seed, seed=seed, window=True)
 
 
-@pytest.mark.parametrize("order", ["column", "deadline"])
+@pytest.mark.parametrize("order", ["column", "rowpipe", "step"])
 @pytest.mark.parametrize("grid", [(1, 2), (2, 2), (2, 4), (3, 2)])
 def test_dtr_dist_plan_numerics(grid, order):
     """Per-rank storage, receive slots and W copies: the assembled factor equals numpy's Cholesky."""
@@ -384,10 +380,8 @@ def test_dtr_dist_plan_numerics(grid, order):
     S = M @ M.T + n * np.eye(n)
     dplan = DD.DistPlan(nt, 2, P, Q, lo_order=order)
     nr = P * Q
-    for window in (False, True):
-        L = _emulate_dist(dplan, _xcds(nr, "emulate" if 8 % nr == 0 else "proc"), A=S.copy(), nb=nb, wpx=2, seed=5,
-                          window=window)
-        assert np.abs(L - np.linalg.cholesky(S)).max() < 1e-10
+    L = _emulate_dist(dplan, _xcds(nr, "emulate" if 8 % nr == 0 else "proc"), A=S.copy(), nb=nb, wpx=2, seed=5)
+    assert np.abs(L - np.linalg.cholesky(S)).max() < 1e-10
 
 
 @pytest.mark.gpu

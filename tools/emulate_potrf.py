@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--trace", default=None, help="write the per-task trace (npz)")
-    ap.add_argument("--order", default="deadline", choices=["deadline", "column", "panel"])
+    ap.add_argument("--order", default="step", choices=["deadline", "column", "panel", "rowpipe", "step"])
     ap.add_argument("--defer", type=int, default=None)
     a = ap.parse_args()
     P, Q = (int(x) for x in a.grid.lower().split("x"))
@@ -62,8 +62,9 @@ def main():
           f"{100 * f / best / (nr * PEAK):.1f} % of peak", flush=True)
     if a.trace:
         import numpy as np
-        np.savez(a.trace, trace=em.trace.view(-1, 3).cpu().numpy(), owner=pl.owner, type=pl.tasks["type"],
-                 k0=pl.tasks["k0"], i=pl.tasks["i"], j=pl.tasks["j"], nk=pl.tasks["nk"])
+        np.savez(a.trace, trace=em.trace.view(-1, 4).cpu().numpy(), owner=pl.owner, type=pl.tasks["type"],
+                 k0=pl.tasks["k0"], i=pl.tasks["i"], j=pl.tasks["j"], nk=pl.tasks["nk"], inc=pl.tasks["inc"],
+                 req_beg=pl.tasks["req_beg"], nreq=pl.tasks["nreq"], reqs=pl.reqs, nranks=nr)
     if a.check:
         L, A0 = em.assemble()
         ok, res = dp.check_potrf(ctx, dp.dplasmaLower, L, A0)

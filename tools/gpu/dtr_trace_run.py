@@ -28,11 +28,21 @@ def main():
     dp.dplghe(ctx, float(N), dp.dplasmaLower, A, 3872)
     A0 = A.data.clone()
     tp = D.potrf_dtr_New(ctx, dp.dplasmaLower, A)
-    for _ in range(2):
+    # DTR_TRACE_RUNS=n: up to n runs, stopping at the first whose residual check fails (that run's trace is kept)
+    runs = int(os.environ.get("DTR_TRACE_RUNS", "2"))
+    for rep in range(runs):
         A.data.copy_(A0)
+        tp.dtr_trace.zero_()
         tp.execute(ctx)
+        if runs > 2:
+            Ar = A.like()
+            Ar.data.copy_(A0)
+            ok, res = dp.check_potrf(ctx, dp.dplasmaLower, A, Ar)
+            print(f"run {rep}: check={ok} res={res:.2e}", flush=True)
+            if not ok:
+                break
     torch.cuda.synchronize()
-    tr = tp.dtr_trace.view(-1, 3).cpu().numpy()
+    tr = tp.dtr_trace.view(-1, 4).cpu().numpy()
     plan = tp.dtr_plan
     T = plan.tasks
     s, e, who = tr[:, 0], tr[:, 1], tr[:, 2]
@@ -96,7 +106,9 @@ def main():
     xb = [(ee[xcd_of == x] - ss[xcd_of == x]).sum() / ((nwg / 8) * span) * 100 for x in range(8)]
     print("busy % per XCD:", [int(round(v)) for v in xb])
     if out:
-        np.savez(out, trace=tr, tasks=T.view(np.uint8), nt=nt)
+        np.savez(out, trace=tr, tasks=T.view(np.uint8), nt=nt, owner=np.zeros(len(T), dtype=np.int64),
+                 type=T["type"], k0=T["k0"], i=T["i"], j=T["j"], r=T["r"], nk=T["nk"], inc=T["inc"], req_beg=T["req_beg"],
+                 nreq=T["nreq"], reqs=plan.reqs, nranks=1)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,29 @@
+#!/bin/bash
+# r5 batch 11: step-major order with per-step FIFO segments (DPLASMA_DTR_LO_ORDER=step) -- 1-GPU DTR, 2x4 emulation, critical paths
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/r5b11
+mkdir -p $O
+export PYTHONUNBUFFERED=1
+step() {
+  local name=$1 to=$2; shift 2
+  echo "== $name" | tee -a $O/summary.log
+  timeout -k 10 $to "$@" > $O/$name.log 2>&1
+  local rc=$?
+  grep -E "passed|failed|Error|error|TIME|EMUL|residual|span" $O/$name.log | grep -v amdgpu.ids | tail -8 | tee -a $O/summary.log
+  echo "rc=$rc" | tee -a $O/summary.log
+  return $rc
+}
+export DPLASMA_DTR_LO_ORDER=step
+step tests 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_potrf_dtr.py || exit 1
+step perf_step 400 python -c "
+import sys; sys.path.insert(0, 'tools/gpu'); import dtr_bench as b
+for N in (16384, 32768, 65536): b.run(N, 'dtr')" || exit 1
+step tr1_16k 300 python tools/gpu/dtr_trace_run.py 16384 $O/g16.npz || exit 1
+python tools/emul_critical.py $O/g16.npz 1 40 > $O/g16_critical.txt 2>&1
+step em16_2x4 200 python tools/emulate_potrf.py -N 16384 --grid 2x4 --order step --reps 1 --check --trace $O/em16.npz || exit 1
+python tools/emul_critical.py $O/em16.npz 8 60 > $O/em16_critical.txt 2>&1
+step em32_2x4 300 python tools/emulate_potrf.py -N 32768 --grid 2x4 --order step --reps 1 --trace $O/em32.npz || exit 1
+python tools/emul_critical.py $O/em32.npz 8 60 > $O/em32_critical.txt 2>&1
+step em64_2x4 400 python tools/emulate_potrf.py -N 65536 --grid 2x4 --order step --reps 1 || exit 1
+rm -f $O/*.npz
+exit 0

@@ -51,29 +51,42 @@ class ReplayXchg:
         pass
 
 
-def _valid_pivots_panel(orig):
-    """The replay moves no data: a rank outside panel k's process column keeps a STALE pivot vector after the
-    modelled broadcast -- positions of an earlier, taller panel, which would send the row moves beyond this
-    panel's rows (the illegal memory access of round 4's first LU replay).  Clamp them into [j, mp) so the
-    moves stay a valid interchange sequence of the right size."""
+def true_pivots(base, N, NB):
+    """The pivots of the whole factorisation, from a one-process getrf_ptgpanel of the same matrix
+    (plrnt seed 3872, identical for every distribution): what each panel's broadcast delivers on the grid."""
+    A = dp.block_cyclic(base, torch.float64, NB, NB, N, N, name="A")
+    dp.plrnt(base, A, 3872)
+    IP = dp.ptgpanel_ipiv_descriptor(base, A)
+    tp = dp.getrf_ptgpanel_New(base, A, IP)
+    info = tp.execute(base)
+    ipiv = tp.ipiv_all.clone()            # global, 1-based
+    del A, IP, tp
+    torch.cuda.empty_cache()
+    return ipiv, info
+
+
+def _delivered_pivots_panel(orig, ipiv):
+    """The replay moves no data, so the pivots a rank computes or receives for panel k are not the grid's
+    (a rank outside the panel's process column keeps an earlier panel's vector; a rank inside searched its
+    own rows only).  The modelled broadcast instead DELIVERS the true pivots of panel k (from a one-process
+    factorisation of the same matrix, ``true_pivots``), as the root's broadcast does on the grid: the row
+    moves then carry the real interchange pattern and always stay inside the panel's rows."""
     def panel(self, k):
         orig(self, k)
         st = self.plan[k]
-        kmin, mp = st["kmin"], st["mp"]
+        kmin, r0 = st["kmin"], st["r0"]
         if kmin > 0 and self.pivot:
-            j = torch.arange(kmin, dtype=torch.int32, device=self.piv_dev.device)
-            p = self.piv_dev[:kmin]
-            self.piv_dev[:kmin] = torch.maximum(torch.minimum(p, torch.full_like(p, mp - 1)), j)
+            self.piv_dev[:kmin] = ipiv[r0:r0 + kmin] - (r0 + 1)
     return panel
 
 
-def replay_rank(base, P, Q, rank, N, NB, steps, xlat):
+def replay_rank(base, P, Q, rank, N, NB, steps, xlat, ipiv):
     from dplasma_amd.models import lu as lu_mod
     ctx = fake_rank_context(base, P, Q, rank)
     orig = lu_dist_ops.panel_xchg
     orig_panel = lu_mod._GetrfDev.panel
     lu_dist_ops.panel_xchg = lambda group, me, P_, kbw, dtype, device, max_rows=0: ReplayXchg(kbw, dtype, device, xlat)
-    lu_mod._GetrfDev.panel = _valid_pivots_panel(orig_panel)
+    lu_mod._GetrfDev.panel = _delivered_pivots_panel(orig_panel, ipiv)
     try:
         A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N, name="A")
         dp.plrnt(ctx, A, 3872)
@@ -113,6 +126,10 @@ def main():
     args = ap.parse_args()
     P, Q = map(int, args.grid.lower().split("x"))
     base = dp.init(device="cuda:0")
+    t0 = time.perf_counter()
+    ipiv, info0 = true_pivots(base, args.N, args.nb)
+    print(f"true pivots: one-process getrf_ptgpanel N={args.N} info={info0} ({time.perf_counter() - t0:.1f} s)",
+          flush=True)
     be = ReplayBackend(base.device, args.bw, args.lat, args.comm_wg, proxies=False)
     comm.set_backend(be)
     ranks = range(P * Q) if args.ranks == "all" else [int(x) for x in args.ranks.split(",")]
@@ -120,7 +137,7 @@ def main():
     fl = flops("d", "getrf", args.N, args.N)
     res = {}
     for r in ranks:
-        t, enq = replay_rank(base, P, Q, r, args.N, args.nb, args.steps, args.xlat)
+        t, enq = replay_rank(base, P, Q, r, args.N, args.nb, args.steps, args.xlat, ipiv)
         res[r] = t
         print(f"rank {r} ({r // Q},{r % Q}): {t * 1e3:9.2f} ms   enq {enq:.2f} s", flush=True)
     worst = max(res.values())
