@@ -199,7 +199,13 @@ __device__ inline int claim_low(const DtrArgs& g, int xcd, int x0, int nx, int r
 }
 
 // tile offsets of rank rk (element offsets from g.A[rk]): local tiles and received copies
-__device__ inline long long tile_at(const long long* tab, int nt, int i, int j) { return tab[i + (long long)j * nt]; }
+// (wave-uniform: the loaded value is made scalar again, or every buffer resource built from it -- the GEMM's
+// operand and C addresses -- would be wrapped in a waterfall loop inside the software pipeline)
+__device__ inline long long tile_at(const long long* tab, int nt, int i, int j) {
+  const long long v = tab[i + (long long)j * nt];
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (long long)(((unsigned long long)hi << 32) | lo);
+}
 
 struct UpdKs {   // k-run of an update: L(i,k) strip r, L(j,k) strip c, k in [k0, k0+nk)
   // the first four panels' operand offsets are looked up once, before the GEMM (scalar registers, selected
@@ -228,8 +234,9 @@ struct UpdKs {   // k-run of an update: L(i,k) strip r, L(j,k) strip c, k in [k0
   __device__ KPair operator()(int t) const {
     KPair p;
     if (t < 4) {
-      p.a_off = t == 0 ? a0 : t == 1 ? a1 : t == 2 ? a2 : a3;
-      p.b_off = t == 0 ? b0 : t == 1 ? b1 : t == 2 ? b2 : b3;
+      // (readfirstlane: the functor may live in memory, which makes its fields look divergent)
+      p.a_off = rfl64_(t == 0 ? a0 : t == 1 ? a1 : t == 2 ? a2 : a3);
+      p.b_off = rfl64_(t == 0 ? b0 : t == 1 ? b1 : t == 2 ? b2 : b3);
     } else {
       p.a_off = tile_at(tab, nt, i, k0 + t) + 128 * r;
       p.b_off = tile_at(tab, nt, j, k0 + t) + 128 * c;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# r5 batch 16: is the segmented step order's intermittent wrong factor an L2 staleness? system-scope acquire A/B
+# r5 batch 16: DTR after removing the operand waterfall loops; is the segmented step order's intermittent wrong factor an L2 staleness? system-scope acquire A/B
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/r5b16
 mkdir -p $O
@@ -13,6 +13,8 @@ run() {
   echo "rc=$rc" | tee -a $O/summary.log
   return $rc
 }
+echo "== perf column (after the waterfall fix)" | tee -a $O/summary.log
+timeout -k 10 300 python tools/gpu/dtr_bench.py 16384 32768 65536 2>&1 | grep TIME | tee -a $O/summary.log
 run step_w8_sysacq DPLASMA_DTR_LO_ORDER=step DPLASMA_DTR_STEPW=8 DPLASMA_DTR_SYSACQ=1 || exit 1
 run step_w8 DPLASMA_DTR_LO_ORDER=step DPLASMA_DTR_STEPW=8 || exit 1
 run step_w2 DPLASMA_DTR_LO_ORDER=step DPLASMA_DTR_STEPW=2 || exit 1
