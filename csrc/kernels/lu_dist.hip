@@ -302,6 +302,33 @@ DPL_API int dpl_xchg_alloc(long long bytes, void** ptr, void* handle) {
   return 0;
 }
 
+// Zero-filled device memory exported as an IPC handle: cached (hipMalloc: data a peer stores into with
+// system-scope stores and this process reads with plain loads after a system acquire -- the distributed
+// DTR's receive buffers and W) or uncached (flags and counters polled across processes).
+DPL_API int dpl_ipc_alloc(long long bytes, int cached, void** ptr, void* handle) {
+  if (!cached) return dpl_xchg_alloc(bytes, ptr, handle);
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, (size_t)bytes);
+  if (e != hipSuccess) return (int)e;
+  e = dpl_zero_sync(p, (size_t)bytes);
+  if (e != hipSuccess) return (int)e;
+  hipIpcMemHandle_t h;
+  e = hipIpcGetMemHandle(&h, p);
+  if (e != hipSuccess) {
+    (void)hipFree(p);
+    return (int)e;
+  }
+  std::memcpy(handle, &h, sizeof(h));
+  *ptr = p;
+  return 0;
+}
+
+// clear device memory and return once the zeros have landed (value: the byte)
+DPL_API int dpl_memset_sync(void* ptr, int value, long long bytes) {
+  if (value != 0) return -2;
+  return (int)dpl_zero_sync(ptr, (size_t)bytes);
+}
+
 DPL_API int dpl_xchg_open(const void* handle, void** ptr) {
   hipIpcMemHandle_t h;
   std::memcpy(&h, handle, sizeof(h));

@@ -114,8 +114,14 @@ def potrf_New(ctx, uplo: int, A, info_out=None, defer: int = None) -> Taskpool:
                < int(os.environ.get("DPLASMA_POTRF_DTR_MAX_N", POTRF_DTR_MAX_N)))
         if potrf_dtr.supported(ctx, uplo, A) and (eng == "dtr" or win):
             return potrf_dtr.potrf_dtr_New(ctx, uplo, A, info_out)
+        if eng == "dtr" and ctx.world > 1:
+            # one rank of a P x Q grid: the distributed device task runtime (models/potrf_dtr_dist.py)
+            from . import potrf_dtr_dist
+            if potrf_dtr_dist.supported(ctx, uplo, A):
+                return potrf_dtr_dist.potrf_dtr_dist_New(ctx, uplo, A, info_out)
         if eng == "dtr":
-            raise ValueError("DPLASMA_POTRF_ENGINE=dtr: needs one GPU process, lower, fp64, NB = 512, N % 512 == 0")
+            raise ValueError("DPLASMA_POTRF_ENGINE=dtr: needs lower, fp64, NB = 512, N % 512 == 0 (one GPU process, or a "
+                             "P x Q grid of <= 8 GPU processes with TILE storage)")
     if (ctx.world > 1 or getattr(ctx, "loopback", False)) and os.environ.get("DPLASMA_POTRF_DIST", "p2p") != "collective":
         # distributed: point-to-point dataflow panel transport (models/potrf_dist.py);
         # DPLASMA_POTRF_DIST=collective keeps the row-broadcast + column-all-gather schedule below

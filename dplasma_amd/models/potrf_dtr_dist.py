@@ -336,3 +336,212 @@ class Emulation:
                 L.data[L.offset(i, j): L.offset(i, j) + NBT * NBT].copy_(Ar.data[o:o + NBT * NBT])
                 A0.data[A0.offset(i, j): A0.offset(i, j) + NBT * NBT].copy_(self.A0[r][o:o + NBT * NBT])
         return L, A0
+
+
+# ------------------------------------------------------------------------------------ process mode
+class _Peers:
+    """This rank's receive buffer, W and counters, exported over IPC, and every peer's mapped into this
+    process (one process per GPU; ranks sharing a GPU -- the rehearsal -- work the same way)."""
+
+    def __init__(self, ctx, specs):
+        import ctypes
+
+        import torch.distributed as dist
+
+        from ..ops import _lib
+        lib = _lib.load()
+        self.lib = lib
+        self.local, self.opened = [], []
+        hb = int(lib.dpl_ipc_handle_bytes())
+        mine = []
+        for nbytes, cached in specs:
+            h = (ctypes.c_char * hb)()
+            ptr = ctypes.c_void_p()
+            rc = lib.dpl_ipc_alloc(int(nbytes), int(cached), ctypes.byref(ptr), h)
+            if rc != 0:
+                raise RuntimeError(f"distributed DTR: IPC allocation of {nbytes} bytes failed ({rc})")
+            self.local.append(ptr.value)
+            mine.append(bytes(h))
+        allh = [None] * ctx.world
+        dist.all_gather_object(allh, mine)
+        self.ptrs = []          # [buffer][rank] -> device pointer in this process
+        for b in range(len(specs)):
+            row = []
+            for r in range(ctx.world):
+                if r == ctx.rank:
+                    row.append(self.local[b])
+                    continue
+                p = ctypes.c_void_p()
+                rc = lib.dpl_xchg_open(ctypes.create_string_buffer(allh[r][b], hb), ctypes.byref(p))
+                if rc != 0:
+                    raise RuntimeError(f"distributed DTR: cannot map rank {r}'s buffer {b} ({rc})")
+                self.opened.append(p.value)
+                row.append(p.value)
+            self.ptrs.append(row)
+        _PEERS.append(self)
+
+    def close(self):
+        import ctypes
+
+        import torch
+        import torch.distributed as dist
+        if self.local is None:
+            return
+        torch.cuda.synchronize()
+        if dist.is_initialized():
+            dist.barrier()
+        for p in self.opened:
+            self.lib.dpl_xchg_close(ctypes.c_void_p(p))
+        if dist.is_initialized():
+            dist.barrier()
+        for p in self.local:
+            self.lib.dpl_xchg_free(ctypes.c_void_p(p))
+        self.local, self.opened = None, []
+
+
+_PEERS = []
+
+
+def release_all():
+    """Unmap and free the distributed DTR's IPC buffers (every rank; collective)."""
+    while _PEERS:
+        _PEERS.pop().close()
+
+
+def _at_exit():
+    try:
+        import torch.distributed as dist
+        if _PEERS and dist.is_available() and dist.is_initialized():
+            release_all()
+    except Exception:   # pragma: no cover - teardown best effort
+        pass
+
+
+import atexit  # noqa: E402
+atexit.register(_at_exit)
+
+
+def supported(ctx, uplo, A) -> bool:
+    from ..constants import dplasmaLower
+    from ..descriptor import STORAGE_TILE
+    import torch
+    if not (ctx.is_gpu and ctx.world > 1 and ctx.world <= 8 and not getattr(ctx, "loopback", False)):
+        return False
+    if uplo != dplasmaLower or A.dtype != torch.float64 or A.mb != NBT or A.nb != NBT:
+        return False
+    if A.m != A.n or A.m % NBT or A.storage != STORAGE_TILE or A.grid.P * A.grid.Q != ctx.world:
+        return False
+    return not (A.it0 or A.jt0 or A.grid.kp != 1 or A.grid.kq != 1 or A.grid.ip or A.grid.jq)
+
+
+_DPLANS = {}
+
+
+def potrf_dtr_dist_New(ctx, uplo: int, A, info_out=None):
+    """The distributed DTR Cholesky of this rank's tiles (one process per GPU, every rank calls it).
+    Each run: counters cleared, a barrier (no peer may send into a counter before it is cleared), one
+    persistent launch; info all-reduced."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from ..ops import _lib
+    from ..parallel import comm
+    from ..runtime.taskpool import Taskpool
+    from ..utils.flops import flops
+    if not supported(ctx, uplo, A):
+        raise ValueError("distributed DTR: lower, fp64, NB = 512 TILE storage on the context's P x Q grid (<= 8 GPUs)")
+    P, Q, me = A.grid.P, A.grid.Q, ctx.rank
+    nt = A.nt
+    Dd = max(1, int(os.environ.get("DPLASMA_DTR_DEFER", "4")))
+    order = os.environ.get("DPLASMA_DTR_LO_ORDER", "column")
+    key = (nt, Dd, P, Q, order)
+    plan = _DPLANS.get(key)
+    if plan is None:
+        plan = _DPLANS[key] = DistPlan(nt, Dd, P, Q, lo_order=order)
+    lib = _lib.load()
+    img = D.ArgsImage(lib)
+    PST = img.pstride
+    dev = A.device
+    hi, hi_off, lo, lo_off = plan.lists({me: list(range(8))})
+    peers = _Peers(ctx, [(plan.recv_elems(me) * 8, True), (nt * NBT * NBT * 8, True), (plan.ncnt * 4, False)])
+    recv_p, W_p, cnt_p = peers.ptrs
+
+    def up(x):
+        return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+    tab = plan.tile_table(me, A.offset, (recv_p[me] - A.data.data_ptr()) // 8)
+    assert (recv_p[me] - A.data.data_ptr()) % 8 == 0
+    tabs = np.full(plan.nranks * nt * nt, -1, dtype=np.int64)
+    tabs[me * nt * nt:(me + 1) * nt * nt] = tab
+    keep = dict(tasks=up(plan.tasks.view(np.uint8)), reqs=up(plan.reqs), tab=up(tabs), xoff=up(plan.xoff),
+                hi=up(hi if len(hi) else np.zeros(1, dtype=np.int32)), lo=up(lo if len(lo) else np.zeros(1, dtype=np.int32)),
+                hs=up(plan.hs_off))
+    cur = torch.zeros((img.maxr + 8) * PST, dtype=torch.int32, device=dev)
+    scur = torch.zeros(plan.nranks * nt * PST, dtype=torch.int32, device=dev)
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    scr = D.PotrfScratch(nt, dev, PST)
+    img.set("ld", NBT)
+    img.set("nt", nt)
+    img.set("nranks", plan.nranks)
+    img.set("rank", me)
+    img.set("dil", 1)
+    img.set("ncnt", plan.ncnt)
+    for f in ("tasks", "reqs", "tab", "xoff", "hi", "lo"):
+        img.set(f, keep[f].data_ptr())
+    img.set("hs_off", keep["hs"].data_ptr())
+    img.set("nsteps", nt)
+    img.set("scur", scur.data_ptr())
+    img.set("cur", cur.data_ptr())
+    img.set("hi_off", hi_off)
+    img.set("lo_off", lo_off)
+    img.set("A", [A.data.data_ptr() if r == me else 0 for r in range(plan.nranks)])
+    img.set("recv", recv_p)
+    img.set("W", W_p)
+    img.set("cnt", cnt_p)
+    scr.fill(img)
+    img.set("info", info.data_ptr())
+    img.set("flags", D.flags_from_env())
+    args_d = torch.empty(img.size, dtype=torch.uint8, device=dev)
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    nwg = int(os.environ.get("DPLASMA_DTR_WG", 2 * ncu))
+    nwg = max(64, min(nwg, 2 * ncu))
+    cnt_local = torch.empty(0)   # (the counters live in the IPC buffer: cleared by a memset kernel below)
+    tp = Taskpool("potrf", ctx)
+    tp.flops = flops(A.prec, "potrf", A.n)
+    tp.info = info
+    state = {"epoch": 0}
+    tp._keep = (keep, cur, scur, info, scr, args_d, peers, cnt_local)
+    tp.dtr_plan = plan
+
+    def f_run():
+        state["epoch"] = state["epoch"] % ((1 << 25) - 1) + 1
+        img.set("epoch", state["epoch"])
+        args_d.copy_(torch.frombuffer(bytearray(img.buf), dtype=torch.uint8))
+        cur.zero_()
+        scur.zero_()
+        torch.cuda.current_stream().synchronize()
+        _lib.check(lib.dpl_memset_sync(cnt_p[me], 0, plan.ncnt * 4), "dtr counters")
+        # every rank's counters are cleared before any rank's kernel can send into them
+        comm.barrier_world()
+        _lib.check(lib.dpl_dtr_potrf(args_d.data_ptr(), nwg, _lib.stream_ptr()), "dtr_potrf (distributed)")
+
+    tp.task("DTR_POTRF", "update", f_run)
+
+    def _done():
+        v = info.to(torch.int64)
+        if dist.get_backend() != "nccl":
+            v = v.cpu()
+        neg = torch.where(v < 0, v, torch.zeros_like(v))
+        dist.all_reduce(neg, op=dist.ReduceOp.MIN)
+        if int(neg.item()) < 0:
+            raise RuntimeError(f"potrf: distributed device task runtime failure (info {int(neg.item())})")
+        pos = torch.where(v > 0, v, torch.full_like(v, 1 << 40))
+        dist.all_reduce(pos, op=dist.ReduceOp.MIN)
+        r = int(pos.item())
+        r = 0 if r == 1 << 40 else r
+        if info_out is not None:
+            info_out[0] = r
+        return r
+    tp.on_complete(_done)
+    return tp.finish_build()

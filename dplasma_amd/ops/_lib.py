@@ -116,6 +116,8 @@ _SIGS = {
     "dpl_lu_dist_ws_bytes": [c_int],
     "dpl_lu_dist_slot_bytes": [c_int, c_int],
     "dpl_xchg_alloc": [c_ll, c_vp, c_vp],
+    "dpl_ipc_alloc": [c_ll, c_int, c_vp, c_vp],
+    "dpl_memset_sync": [c_vp, c_int, c_ll],
     "dpl_xchg_open": [c_vp, c_vp],
     "dpl_xchg_close": [c_vp],
     "dpl_xchg_free": [c_vp],

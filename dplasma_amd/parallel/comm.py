@@ -203,6 +203,18 @@ def bcast(t: torch.Tensor, src_global: int, group, world: bool = False) -> None:
     w.wait()
 
 
+def barrier_world() -> None:
+    """A host-side barrier over every rank (the host returns once every rank has reached it)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return
+    if _nccl():
+        t = torch.zeros(1, device=torch.device("cuda", torch.cuda.current_device()))
+        dist.all_reduce(t)
+        torch.cuda.current_stream().synchronize()
+    else:
+        dist.barrier()
+
+
 def _nccl() -> bool:
     return dist.get_backend() == "nccl"
 

@@ -22,4 +22,9 @@ timeout -k 10 200 python -c "
 import os, sys; os.environ['DPLASMA_DTR_LO_ORDER']='step'; os.environ['DPLASMA_DTR_STEPW']='8'; os.environ['DPLASMA_DTR_SYSACQ']='1'
 sys.path.insert(0, 'tools/gpu'); import dtr_bench as b
 for N in (16384, 32768, 65536): b.run(N, 'dtr')" 2>&1 | grep TIME | tee -a $O/summary.log
+echo "== dtr_dist rehearsal 2 ranks" | tee -a $O/summary.log
+DPLASMA_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \
+  --master-port 29517 tools/gpu/dtr_dist_rehearsal.py 8192 1 2 > $O/rehearsal2.log 2>&1
+echo "rc=$?" | tee -a $O/summary.log
+grep -E "run |DTR-DIST|Error|error" $O/rehearsal2.log | head -12 | tee -a $O/summary.log
 exit 0
