@@ -385,7 +385,8 @@ __device__ __attribute__((noinline)) void run_upd(const DtrArgs* __restrict__ gp
   ks.init(u.nk);
   const int uplo = (u.i == u.j && u.r == u.c) ? 1 : 0;
   gemm_subtile<double, false, true>(g_lds, ks, u.nk, 0, 0, uplo, -1.0, u.A, (int)u.ld, u.A, (int)u.ld, 1.0,
-                                    u.A + tile_at(u.tab, u.nt, u.i, u.j) + 128 * u.r + 128LL * u.c * u.ld, (int)u.ld);
+                                    u.A + tile_at(u.tab, u.nt, u.i, u.j) + 128 * u.r + 128LL * u.c * u.ld, (int)u.ld,
+                                    -1, (rfl(g.flags) & 16) != 0);
 }
 
 __device__ __attribute__((noinline)) void run_trsm(const DtrArgs* __restrict__ gp, int t, int rk) {
@@ -397,7 +398,7 @@ __device__ __attribute__((noinline)) void run_trsm(const DtrArgs* __restrict__ g
   for (int c = 3; c >= 0; --c) {
     const TrsmKs ks{ao, c};
     gemm_subtile<double, false, false>(g_lds, ks, 1, 0, 0, 0, 1.0, u.A, (int)u.ld, Wk, NBT, 0.0,
-                                       u.A + ao + 128LL * c * u.ld, (int)u.ld);
+                                       u.A + ao + 128LL * c * u.ld, (int)u.ld, -1, (rfl(g.flags) & 16) != 0);
     __syncthreads();   // LDS image reuse (block c-1 never reads the columns block c wrote)
   }
 }
@@ -669,7 +670,9 @@ __global__ __launch_bounds__(256, 2) void k_dtr_potrf(const DtrArgs* __restrict_
       const int tr_ = remote ? tk.j : rk;
       if (emul(g))
         __hip_atomic_fetch_max(g.vis + (size_t)tr_ * g.ncnt + tk.inc, due, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (remote && sysmode(g)) {
+      // (flags bit 3: the system-scope release for every task -- a measurement knob, DPLASMA_DTR_SYSREL; it
+      // does not remove the two-workgroups-per-CU failure, profiles/r5_dtr_coresidency.txt)
+      if ((remote && sysmode(g)) || (g.flags & 8)) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_fetch_add(g.cnt[tr_] + tk.inc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

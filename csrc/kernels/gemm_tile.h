@@ -91,7 +91,7 @@ template <typename T, bool TA, bool TB, typename KS>
 __device__ __forceinline__ void gemm_subtile(T* __restrict__ sm, const KS& ks, const int kt_cnt, const int m0,
                                              const int n0, const int uplo, T alpha, const T* __restrict__ A,
                                              int lda, const T* __restrict__ B, int ldb, T beta,
-                                             T* __restrict__ Cb, int ldc, int tid_in = -1) {
+                                             T* __restrict__ Cb, int ldc, int tid_in = -1, bool wt = false) {
   typedef MF<T> M_;
   typedef typename M_::acc_t acc_t;
   typedef typename M_::vec_t vec_t;
@@ -303,7 +303,20 @@ __device__ __forceinline__ void gemm_subtile(T* __restrict__ sm, const KS& ks, c
   }
 
   const bool diag = (uplo == 1 && n0 + GBN > m0) || (uplo == 2 && m0 + GBM > n0);
-  if (!diag) {
+  if (wt) {
+    // write-through to memory (system scope) -- a measurement knob of the device task runtime
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int mm = mrow + i * 16, nn = ncol + j * 16 + M_::drow(l, r);
+          const bool ok = !diag || ((uplo == 1) ? (mm >= nn) : (mm <= nn));
+          if (ok) __hip_atomic_store(Cb + mm + (long long)nn * ldc, alpha * acc[i][j][r], __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+  } else if (!diag) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll

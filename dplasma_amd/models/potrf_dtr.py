@@ -364,6 +364,12 @@ def flags_from_env() -> int:
     # DPLASMA_DTR_SYSACQ=1: system-scope acquire before every task (measurement knob)
     if os.environ.get("DPLASMA_DTR_SYSACQ", "0") == "1":
         fl |= 4
+    # DPLASMA_DTR_SYSREL=1: system-scope release after every task (measurement knob)
+    if os.environ.get("DPLASMA_DTR_SYSREL", "0") == "1":
+        fl |= 8
+    # DPLASMA_DTR_WT=1: update / TRSM results stored write-through at system scope (measurement knob)
+    if os.environ.get("DPLASMA_DTR_WT", "0") == "1":
+        fl |= 16
     # DPLASMA_DTR_STEPW=w: step segments of the high list scanned per claim (1..15; default 8)
     sw = int(os.environ.get("DPLASMA_DTR_STEPW", "0"))
     if sw:
@@ -474,21 +480,32 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     tp.dtr_trace = trace
     nbytes = img.size
     host = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    hosts = [[host, None], [torch.empty(nbytes, dtype=torch.uint8).pin_memory(), None]]
     args_d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     state = {"epoch": 0}
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    nwg = int(os.environ.get("DPLASMA_DTR_WG", 2 * ncu))
+    # one workgroup per CU by default: with two per CU the factor came out wrong in a few % of runs under
+    # stress, for reasons not found (profiles/r5_dtr_coresidency.txt); DPLASMA_DTR_WG=512 re-enables two
+    nwg = int(os.environ.get("DPLASMA_DTR_WG", ncu))
     # progress needs a workgroup on every XCD (a low list is another XCD's to steal only once that XCD's
     # own list is exhausted) and the 16 cooperating POTRF workgroups co-resident: at least 64 of them
     nwg = max(64, min(nwg, 2 * ncu))
-    tp._keep = (tasks_d, reqs_d, hi_d, lo_d, tab_d, cnt, cur, hs_d, scur, W, scr, host, args_d)
+    tp._keep = (tasks_d, reqs_d, hi_d, lo_d, tab_d, cnt, cur, hs_d, scur, W, scr, hosts, args_d)
     tp.dtr_plan = plan
 
     def f_run():
         state["epoch"] = state["epoch"] % ((1 << 25) - 1) + 1
         img.set("epoch", state["epoch"])
-        host.numpy()[:] = np.frombuffer(bytes(img.buf), dtype=np.uint8)
-        args_d.copy_(host, non_blocking=True)
+        # a pinned staging buffer per run slot: a non-blocking copy still pending from an earlier run (runs
+        # issued back to back, no host sync between them) must not see this run's epoch
+        slot = hosts[state["epoch"] % len(hosts)]
+        if slot[1] is not None:
+            slot[1].synchronize()
+        slot[0].numpy()[:] = np.frombuffer(bytes(img.buf), dtype=np.uint8)
+        args_d.copy_(slot[0], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        slot[1] = ev
         cnt.zero_()
         cur.zero_()
         scur.zero_()

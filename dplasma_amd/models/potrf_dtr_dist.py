@@ -504,7 +504,7 @@ def potrf_dtr_dist_New(ctx, uplo: int, A, info_out=None):
     img.set("flags", D.flags_from_env())
     args_d = torch.empty(img.size, dtype=torch.uint8, device=dev)
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    nwg = int(os.environ.get("DPLASMA_DTR_WG", 2 * ncu))
+    nwg = int(os.environ.get("DPLASMA_DTR_WG", ncu))   # one per CU (see models/potrf_dtr.py)
     nwg = max(64, min(nwg, 2 * ncu))
     cnt_local = torch.empty(0)   # (the counters live in the IPC buffer: cleared by a memset kernel below)
     tp = Taskpool("potrf", ctx)

@@ -28,7 +28,7 @@ def main():
     world = dist.get_world_size()
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
     # the ranks share the GPU: each launch gets its share of the 2 x #CUs resident workgroups
-    os.environ.setdefault("DPLASMA_DTR_WG", str(max(64, 2 * ncu // world)))
+    os.environ.setdefault("DPLASMA_DTR_WG", str(max(64, ncu // world)))
     os.environ["DPLASMA_POTRF_ENGINE"] = "dtr"
     import dplasma_amd as dp
     ctx = dp.init(P=P)

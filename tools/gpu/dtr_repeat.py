@@ -6,6 +6,7 @@ import sys
 from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import dplasma_amd as dp  # noqa: E402
@@ -21,14 +22,33 @@ def main():
     tp = D.potrf_dtr_New(ctx, dp.dplasmaLower, A)
     Ar = A.like()
     bad = 0
+    good = None
+    nt = N // 512
     for rep in range(runs):
         A.data.copy_(A0)
         tp.info.zero_()
         tp.execute(ctx)
+        info = int(tp.info.item())
+        # every counter at its final value (a task run twice would leave one above it)
+        plan = tp.dtr_plan
+        cnt = tp._keep[5].cpu().numpy()
+        exp = np.concatenate([plan.final_ver, np.full(plan.nt, 16)]).astype(np.int64)
+        over = np.nonzero(cnt.astype(np.int64) != exp)[0]
+        cmsg = f" counters off: {len(over)} e.g. {[(int(q), int(cnt[q]), int(exp[q])) for q in over[:6]]}" if len(over) else ""
+        L = torch.tril(A.to_dense_local())
         Ar.data.copy_(A0)
         ok, res = dp.check_potrf(ctx, dp.dplasmaLower, A, Ar)
         bad += not ok
-        print(f"run {rep}: check={ok} res={res:.2e}", flush=True)
+        msg = ""
+        if ok and good is None:
+            good = L.clone()
+        elif not ok and good is not None:
+            # 128 x 128 sub-tiles that differ from a good run's factor, in factorisation order (k, i, r, c)
+            d = (L - good).abs().view(nt, 4, 128, nt, 4, 128).amax(dim=(2, 5))   # [i, r, j, c]
+            idx = torch.nonzero(d > 1e-9)
+            lst = sorted((int(j), int(i), int(r), int(c), float(d[i, r, j, c])) for i, r, j, c in idx.tolist())
+            msg = f" info={info} bad sub-tiles {len(lst)} first (j, i, r, c, err): {lst[:8]}"
+        print(f"run {rep}: check={ok} res={res:.2e}{msg}{cmsg}", flush=True)
     print(f"FAILED {bad} / {runs}", flush=True)
 
 
