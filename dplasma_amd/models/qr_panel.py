@@ -75,7 +75,7 @@ def _rup(x, m):
 
 
 # ----------------------------------------------------------------------------- plans
-def step_plan(tree, k, merge=False):
+def step_plan(tree, k, merge=False, prow=None):
     """(domains, tt_stacks) of panel k: domains = [[head, ts victims...], ...], tt_stacks =
     [(p, [m, ...]), ...]; None when a TS kill's pivot is not a head (not expressible as stacked
     domains).
@@ -102,6 +102,8 @@ def step_plan(tree, k, merge=False):
             kills.append((p, m))
     if not merge:
         return [doms[h] for h in heads], [(p, [m]) for (p, m) in kills]
+    if merge == "row":
+        return [doms[h] for h in heads], _row_stacks(kills, prow)
     victims = [m for (_, m) in kills]
     roots = {p for (p, _) in kills} - set(victims)
     if len(roots) == 1:
@@ -125,13 +127,64 @@ def step_plan(tree, k, merge=False):
     return [doms[h] for h in heads], tts
 
 
+def _row_stacks(kills, prow):
+    """merge="row" (trees over several process rows): the kills inside one process row become stacked panels
+    -- every local subtree of a step is ONE stack [R_root; R_v1; R_v2; ...] factored by the row's owner of the
+    panel column, the one-process-row trick applied per row -- while the kills that cross process rows stay
+    pairwise (R / V2 / T and the partial W exchanged between the two rows).  Kills are taken in tree order; a
+    local kill whose victim leads an open stack absorbs that stack (its triangles join the killer's stack
+    unreduced: the same QR of the union), and a cross-row kill first closes (emits) the open stacks of both
+    its tiles, so every entry sees its tiles' R as the tree order has them.  The trees' low-level rounds
+    inside a row (greedy at 2 x 4: up to ~6 per step) collapse to one launch; src/dplasma_hqr.c:1670-1948
+    lays out the same two-level reduction (local trees, then the distributed high-level tree)."""
+    open_, order, out = {}, [], []
+
+    def close(x):
+        if x in open_:
+            out.append((x, open_.pop(x)))
+            order.remove(x)
+    for (p, m) in kills:
+        if prow(p) == prow(m):
+            vict = [m] + (open_.pop(m) if m in open_ else [])
+            if m in order:
+                order.remove(m)
+            if p in open_:
+                open_[p] += vict
+            else:
+                open_[p] = vict
+                order.append(p)
+        else:
+            close(p)
+            close(m)
+            out.append((p, [m]))
+    for x in list(order):
+        close(x)
+    return out
+
+
 def _merge_tt(A, tree):
-    """TT stacks merge per pivot on one process row with a one-row tree (cross-row kills stay pairwise,
-    and a tree built for P process rows keeps the pairwise layout a P-row grid run produces);
-    DPLASMA_QR_MERGE_TT=0 keeps every kill pairwise."""
-    if os.environ.get("DPLASMA_QR_MERGE_TT", "1") == "0":
+    """How a step's TT kills are grouped: one process row and a one-row tree -> every pivot's kills one
+    stack (True); several process rows (a P x Q grid, or one process running a tree built for p rows, which
+    must lay its factors out as the grid run does) -> stacks per process row, cross-row kills pairwise
+    ("row"); DPLASMA_QR_MERGE_TT=0 keeps every kill pairwise, =1 limits merging to one-row trees."""
+    env = os.environ.get("DPLASMA_QR_MERGE_TT", "row")
+    if env == "0":
         return False
-    return A.grid.P == 1 and int(getattr(tree, "p", 1) or 1) == 1
+    if A.grid.P == 1 and int(getattr(tree, "p", 1) or 1) == 1:
+        return True
+    return "row" if env == "row" else False
+
+
+def _tree_prow(A, tree):
+    """Process row of tile row m as the step plans see it: the grid's (P > 1), else the tree's p rows."""
+    if A.grid.P > 1:
+        return lambda m: _prow(A, m)
+    p = max(1, int(getattr(tree, "p", 1) or 1))
+    return lambda m: m % p
+
+
+def _plan(A, tree, k):
+    return step_plan(tree, k, _merge_tt(A, tree), _tree_prow(A, tree))
 
 
 def _prow(A, m):
@@ -163,7 +216,7 @@ def _sequence(A, tree):
     """Factorisation order: [("dom", k, rows) | ("tt", k, p, [m, ...])] over all panels."""
     seq = []
     for k in range(min(A.mt, A.nt)):
-        doms, tts = step_plan(tree, k, _merge_tt(A, tree))
+        doms, tts = _plan(A, tree, k)
         seq += [("dom", k, d) for d in doms]
         seq += [("tt", k, p, ms) for (p, ms) in tts]
     return seq
@@ -420,7 +473,7 @@ class _Factor:
         # distributed: V and T travel along the process row(s) of the reflector rows (RCCL);
         # TT kills across process rows exchange R / V2 / T and the partial W between the two rows
         self.dist = ctx.world > 1
-        self.plans = [step_plan(tree, k, _merge_tt(A, tree)) for k in range(self.kt)]
+        self.plans = [_plan(A, tree, k) for k in range(self.kt)]
         for k, (doms, tts) in enumerate(self.plans):
             for d in doms:
                 if TS.rank_of(d[0], k) != A.rank_of(d[0], k):

@@ -402,6 +402,34 @@ def test_tt_stack_merge_plan():
         assert n_merged <= n_pair
 
 
+@pytest.mark.parametrize("treeargs", [(0, 0, 2, 2), (1, 1, 2, 2), (1, 0, 4, 2), (3, 1, 2, 4), (2, 1, 3, 3)])
+def test_tt_row_stack_plan(treeargs):
+    """Trees over p process rows (merge="row"): every local stack lies in ONE process row, cross-row kills stay
+    pairwise, each victim appears once, the tree's tile pairs are all reduced, and a stack only ever comes
+    after the cross-row kills it must follow (its root's and victims' last cross-row use precedes it or none)."""
+    ctx_ = dp.init(device="cpu")
+    A = dp.block_cyclic(ctx_, torch.float64, 2, 2, 96, 64)
+    tree = dp.hqr_init(dp.dplasmaNoTrans, A, *treeargs)
+    p = treeargs[3]
+    prow = lambda m: m % p  # noqa: E731
+    n_pair = n_row = 0
+    for k in range(A.nt):
+        d1, pairs = qr_panel.step_plan(tree, k, merge=False)
+        d2, stacks = qr_panel.step_plan(tree, k, merge="row", prow=prow)
+        assert d1 == d2
+        assert sorted(m for _, ms in stacks for m in ms) == sorted(ms[0] for _, ms in pairs)
+        for (r, ms) in stacks:
+            rows = {prow(r)} | {prow(m) for m in ms}
+            assert len(rows) == 1 or len(ms) == 1          # cross-row entries are pairs
+        dead = set()
+        for (r, ms) in stacks:                               # nothing used after it was killed
+            assert r not in dead and not (set(ms) & dead)
+            dead |= set(ms)
+        n_pair += len(pairs)
+        n_row += len(stacks)
+    assert n_row <= n_pair
+
+
 @pytest.mark.parametrize("prec", list("dz"))
 @pytest.mark.parametrize("treeargs", ONE_ROW_TREES)
 def test_hqr_one_row_tree(ctx, prec, treeargs):
