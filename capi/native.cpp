@@ -18,6 +18,7 @@
 // variants), herk / syrk, the element-wise maps (geadd, tradd, lacpy, laset, lascal), the norms lange /
 // lantr, plghe, plgsy, plrnt.
 // Every other entry point returns an error on a native context.
+#include <complex>
 #include <map>
 #include <set>
 
@@ -2889,8 +2890,9 @@ int nat_qr_tau(dplasma_desc_t* dT, void* tau, int k) {
 // less than 1e-10 relatively (at most 500 products).  *info: the iteration count, negative if not converged.
 // dplasma_zpltmg (models/generators.py pltmg; reference src/cores/core_zpltmg.c): the closed-form LAWN-263
 // types, evaluated per tile on the host from GLOBAL indices (identical for any tiling) and copied into the tile;
-// Random is the native plrnt.  The random-vector types (house, circul, hankel, compan, fiedler, toeppd, condex,
-// demmel, langou) and those the reference lacks return -2 / an error: they stay with the Python layer.
+// Random is the native plrnt; the random-vector types (house, circul, hankel, compan, fiedler, toeppd, condex,
+// demmel, langou: core_zpltmg_{circul,condex,fiedler,hankel,toeppd}.c, zpltmg_*.jdf) build their O(n) vectors
+// once from the same 64-bit LCG stream as plrnt (PltmgVec below); the types the reference lacks return -2.
 static bool pltmg_value(int t, long long I, long long J, long long gM, long long gN, double& v) {
   const double If = (double)I, Jf = (double)J, Ii = If + 1.0, Ji = Jf + 1.0;
   switch (t) {
@@ -2963,15 +2965,148 @@ static bool pltmg_value(int t, long long I, long long J, long long gM, long long
   }
 }
 
+// the plrnt stream on the host (csrc/kernels/aux.hip, utils/lcg.py): element (I, J) of a gM-row matrix is the
+// LCG state after I + J gM (complex: 2 (I + J gM)) steps from the seed, value 0.5f - ran * 2^-64 in float
+static unsigned long long lcg_jump(unsigned long long n, unsigned long long seed) {
+  unsigned long long a = 6364136223846793005ULL, c = 1ULL, ran = seed;
+  while (n) {
+    if (n & 1ULL) ran = a * ran + c;
+    c *= a + 1ULL;
+    a *= a;
+    n >>= 1;
+  }
+  return ran;
+}
+static double lcg_val(unsigned long long ran) { return (double)(0.5f - (float)ran * 5.4210108624275222e-20f); }
+static std::complex<double> plrnt_at(unsigned long long idx, unsigned long long seed, bool cplx) {
+  if (!cplx) return lcg_val(lcg_jump(idx, seed));
+  const unsigned long long r = lcg_jump(2ULL * idx, seed);
+  return {lcg_val(r), lcg_val(6364136223846793005ULL * r + 1ULL)};
+}
+
+// per-call state of the random-vector types (models/generators.py _formula, the same definitions)
+struct PltmgVec {
+  int t = 0;
+  long long gM = 0, gN = 0;
+  bool cplx = false;
+  double eps = 0, tau = 0;
+  unsigned long long seed = 0;
+  std::vector<std::complex<double>> v;   // the random vector (circul / fiedler / hankel / house / compan)
+  std::vector<double> tv;                // toeppd: t(d), d = -(n-1) .. n-1
+  long long z = 0;
+  std::vector<std::complex<double>> Q;   // condex: orthonormal basis (gM x 3, column-major)
+
+  bool init(int type, long long m, long long n, int prec, unsigned long long sd) {
+    t = type, gM = m, gN = n, seed = sd;
+    cplx = prec == P_C || prec == P_Z;
+    eps = (prec == P_S || prec == P_C) ? 1.1920928955078125e-07 : 2.220446049250313e-16;
+    auto rv = [&](long long len) {            // the first column of a len-row plrnt matrix
+      v.resize((size_t)len);
+      for (long long i = 0; i < len; ++i) v[(size_t)i] = plrnt_at((unsigned long long)i, seed, cplx);
+    };
+    switch (t) {
+      case 9: rv(gN); return true;                          // circul
+      case 27: rv(std::max(gM, gN)); return true;           // fiedler
+      case 12: rv(gM + gN); return true;                    // hankel
+      case 2: {                                             // house: I - tau v v^H, tau = 2 / ||v||^2
+        rv(gM);
+        double s2 = 0;
+        for (auto& x : v) s2 += std::norm(x);
+        tau = 2.0 / s2;
+        return true;
+      }
+      case 14: {                                            // compan: first row r / r(0)
+        rv(gN);
+        const std::complex<double> v0 = v[0];
+        for (auto& x : v) x /= v0;
+        return true;
+      }
+      case 23: {                                            // toeppd: t(d) = sum_k w_k cos(theta_k d)
+        std::vector<double> w((size_t)gM), th((size_t)gM);
+        for (long long k = 0; k < gM; ++k) {                // a 2-row plrnt matrix: row 0 -> w, row 1 -> theta
+          w[(size_t)k] = plrnt_at((unsigned long long)(2 * k), seed, cplx).real() + 0.5;
+          th[(size_t)k] = 2.0 * M_PI * (plrnt_at((unsigned long long)(1 + 2 * k), seed, cplx).real() + 0.5);
+        }
+        const long long nn = std::max(gM, gN);
+        z = nn - 1;
+        tv.assign((size_t)(2 * nn - 1), 0.0);
+        for (long long d = 0; d < nn; ++d) {
+          double acc = 0;
+          for (long long k = 0; k < gM; ++k) acc += w[(size_t)k] * std::cos(th[(size_t)k] * (double)d);
+          tv[(size_t)(z + d)] = tv[(size_t)(z - d)] = acc;   // cos is even
+        }
+        return true;
+      }
+      case 7: {                                             // condex: Q = orth([1, e_1, x]), x_i = (-1)^i (1 + i/(n-1))
+        const long long n_ = gM;
+        Q.assign((size_t)(3 * n_), 0.0);
+        for (long long i = 0; i < n_; ++i) {
+          Q[(size_t)i] = 1.0;
+          Q[(size_t)(2 * n_ + i)] = ((i & 1) ? -1.0 : 1.0) * (1.0 + (double)i / (double)std::max<long long>(gN - 1, 1));
+        }
+        Q[(size_t)n_] = 1.0;
+        for (int c = 0; c < 3; ++c)                          // modified Gram-Schmidt, twice: the projector
+          for (int pass = 0; pass < 2; ++pass) {             // Q Q^H is what the formula uses (sign-free)
+            std::complex<double>* qc = &Q[(size_t)c * n_];
+            for (int b = 0; b < c; ++b) {
+              const std::complex<double>* qb = &Q[(size_t)b * n_];
+              std::complex<double> d = 0;
+              for (long long i = 0; i < n_; ++i) d += std::conj(qb[i]) * qc[i];
+              for (long long i = 0; i < n_; ++i) qc[i] -= d * qb[i];
+            }
+            double nr = 0;
+            for (long long i = 0; i < n_; ++i) nr += std::norm(qc[i]);
+            nr = std::sqrt(nr);
+            if (!(nr > 0)) return false;
+            for (long long i = 0; i < n_; ++i) qc[i] /= nr;
+          }
+        return true;
+      }
+      case 29: case 42: return true;                        // demmel, langou: the plrnt base per element
+      default: return false;
+    }
+  }
+
+  std::complex<double> at(long long I, long long J) const {
+    switch (t) {
+      case 9: return v[(size_t)(((J - I) % gN + gN) % gN)];
+      case 27: return std::abs(v[(size_t)I] - v[(size_t)J]);
+      case 12: return v[(size_t)(I + J)];
+      case 2: return (I == J ? 1.0 : 0.0) - tau * v[(size_t)I] * std::conj(v[(size_t)J]);
+      case 14:
+        if (I == 0) return J == 0 ? std::complex<double>(0.0) : v[(size_t)std::min(J, gN - 1)];
+        return I == J + 1 ? 1.0 : 0.0;
+      case 23: return tv[(size_t)(I - J + z)];
+      case 7: {
+        const double theta = 100.0;
+        std::complex<double> s = 0;
+        for (int c = 0; c < 3; ++c) s += Q[(size_t)c * gM + I] * std::conj(Q[(size_t)c * gM + J]);
+        return (I == J ? 1.0 + theta : 0.0) - theta * s;
+      }
+      case 29: {
+        const std::complex<double> b = plrnt_at((unsigned long long)(I + J * gM), seed, cplx);
+        return b * (std::pow(10.0, 14.0 * (double)I / (double)gM) * (I == J ? 1.0 : 1e-7));
+      }
+      case 42: {
+        const std::complex<double> b = plrnt_at((unsigned long long)(I + J * gM), seed, cplx);
+        const long long mn = std::min(gM, gN);
+        return (J >= mn / 4 && J < mn / 2 && I >= J) ? b * eps : b;
+      }
+      default: return 0.0;
+    }
+  }
+};
+
 int nat_pltmg(dplasma_context_t* ctx, int prec, int mtxtype, dplasma_desc_t* dA, unsigned long long seed) {
   NatCtx* c = ctx->nat;
   NatDesc* A = dA ? dA->nat : nullptr;
   if (!same_ctx_dist(c, {A}, prec)) return (fail(nullptr, "pltmg: a descriptor of another context or precision"), -1);
   if (mtxtype == 0) return nat_execute(ctx, nat_plrnt(ctx, prec, 0, dA, seed));
   double probe;
-  if (!pltmg_value(mtxtype, 0, 0, std::max(A->m, 1), std::max(A->n, 1), probe))
-    return (fail(nullptr, "pltmg: this matrix type needs the Python layer on a native context (closed-form types "
-                          "and Random only)"), -2);
+  PltmgVec pv;
+  const bool closed = pltmg_value(mtxtype, 0, 0, std::max(A->m, 1), std::max(A->n, 1), probe);
+  if (!closed && !(A->m > 0 && A->n > 0 && pv.init(mtxtype, A->m, A->n, prec, seed)))
+    return (fail(nullptr, "pltmg: matrix type not available (the reference lacks it)"), -2);
   if (mtxtype == 1 && (A->m != A->n || (A->m & (A->m - 1)))) return -2;   // hadamard: n a power of two
   for (int q = 0; q < NAT_NSTREAM; ++q)
     if (hipStreamSynchronize(c->st[q]) != hipSuccess) return -1;
@@ -2983,14 +3118,22 @@ int nat_pltmg(dplasma_context_t* ctx, int prec, int mtxtype, dplasma_desc_t* dA,
       std::fill(h.begin(), h.end(), 0);
       for (int jj = 0; jj < cc; ++jj)
         for (int ii = 0; ii < r; ++ii) {
-          double v = 0.0;
-          pltmg_value(mtxtype, (long long)i * A->mb + ii, (long long)j * A->nb + jj, A->m, A->n, v);
+          const long long I = (long long)i * A->mb + ii, J = (long long)j * A->nb + jj;
+          std::complex<double> z = 0.0;
+          if (closed) {
+            double v = 0.0;
+            pltmg_value(mtxtype, I, J, A->m, A->n, v);
+            z = v;
+          } else {
+            z = pv.at(I, J);
+          }
           char* e = &h[((size_t)ii + (size_t)jj * r) * A->es];
           if (prec == P_S || prec == P_C) {
-            const float f = (float)v;
-            std::memcpy(e, &f, sizeof f);
+            const float f[2] = {(float)z.real(), (float)z.imag()};
+            std::memcpy(e, f, (prec == P_C ? 2 : 1) * sizeof(float));
           } else {
-            std::memcpy(e, &v, sizeof v);
+            const double d[2] = {z.real(), z.imag()};
+            std::memcpy(e, d, (prec == P_Z ? 2 : 1) * sizeof(double));
           }
         }
       if (hipMemcpy2D(A->data + A->off(i, j) * A->es, (size_t)A->lld * A->es, h.data(), (size_t)r * A->es,

@@ -1316,9 +1316,51 @@ static void test_pltmg(dplasma_context_t *ctx) {
       for (int k = 0; k < n; ++k) s += a[i + (size_t)k * n] * a[j + (size_t)k * n];
       orth = fmax(orth, fabs(s - (i == j ? n : 0)));
     }
-  const int rh = dplasma_dpltmg(ctx, dplasmaMatrixHouse, A, 3872);
-  printf("dpltmg hilb / minij max error %.3e, hadamard |H H^T - n I| %.3e, house -> %d\n", err, orth, rh);
-  CHECK(err == 0.0 && orth == 0.0 && rh == -2, "dpltmg: err %.3e orth %.3e house %d", err, orth, rh);
+  /* house: a symmetric orthogonal reflector, H H = I */
+  CHECK(dplasma_dpltmg(ctx, dplasmaMatrixHouse, A, 3872) == 0, "dpltmg house: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(A, a, n);
+  double hh = 0;
+  for (int j = 0; j < n; j += 11)
+    for (int i = 0; i < n; i += 7) {
+      double s = 0;
+      for (int k = 0; k < n; ++k) s += a[i + (size_t)k * n] * a[k + (size_t)j * n];
+      hh = fmax(hh, fabs(s - (i == j ? 1.0 : 0.0)));
+      hh = fmax(hh, fabs(a[i + (size_t)j * n] - a[j + (size_t)i * n]));
+    }
+  /* circul: A(i, j) = A(i + 1, j + 1) (mod n) */
+  CHECK(dplasma_dpltmg(ctx, dplasmaMatrixCircul, A, 3872) == 0, "dpltmg circul: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(A, a, n);
+  double circ = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < n; ++i) circ = fmax(circ, fabs(a[i + (size_t)j * n] - a[(i + 1) % n + (size_t)((j + 1) % n) * n]));
+  const int rx = dplasma_dpltmg(ctx, 6 /* toeppen: not in the reference */, A, 3872);
+  printf("dpltmg hilb / minij max error %.3e, hadamard |H H^T - n I| %.3e, house |H H - I| %.3e, circulant %.3e, "
+         "toeppen -> %d\n", err, orth, hh, circ, rx);
+  CHECK(err == 0.0 && orth == 0.0 && hh < 1e-13 && circ == 0.0 && rx == -2, "dpltmg: err %.3e orth %.3e house %.3e "
+        "circ %.3e toeppen %d", err, orth, hh, circ, rx);
+  /* DPLASMA_TEST_DUMP=dir: every random-vector type (d and z) for tests/test_capi.py to compare with the Python layer */
+  const char *dump = getenv("DPLASMA_TEST_DUMP");
+  if (dump) {
+    const int m2 = 40, n2 = 36, nb2 = 16;
+    const int types[] = {2, 7, 9, 12, 14, 23, 27, 29, 42};
+    for (int z = 0; z < 2; ++z) {
+      dplasma_desc_t *B = dmat(ctx, z ? dplasmaComplexDouble : dplasmaRealDouble, nb2, m2, n2);
+      double *b = malloc(sizeof(double) * 2 * m2 * n2);
+      for (unsigned q = 0; q < sizeof types / sizeof types[0]; ++q) {
+        const int r = z ? dplasma_zpltmg(ctx, types[q], B, 3872) : dplasma_dpltmg(ctx, types[q], B, 3872);
+        CHECK(r == 0, "%cpltmg type %d: %d (%s)", z ? 'z' : 'd', types[q], r, dplasma_last_error());
+        dplasma_desc_get_lapack(B, b, m2);
+        char path[4096];
+        snprintf(path, sizeof path, "%s/pltmg_%c_%d.bin", dump, z ? 'z' : 'd', types[q]);
+        FILE *f = fopen(path, "wb");
+        CHECK(f != NULL, "cannot write %s", path);
+        fwrite(b, sizeof(double) * (z ? 2 : 1), (size_t)m2 * n2, f);
+        fclose(f);
+      }
+      free(b);
+      dplasma_desc_destroy(B);
+    }
+  }
   free(a);
   dplasma_desc_destroy(A);
 }

@@ -162,6 +162,33 @@ def test_capi_native_gpu(tmp_path):
 
 
 @pytest.mark.gpu
+def test_capi_native_pltmg_matches_python(tmp_path):
+    """The native random-vector pltmg types (house, condex, circul, hankel, compan, toeppd, fiedler, demmel,
+    langou; capi/native.cpp PltmgVec) equal the Python layer's (models/generators.py) in d and z: the same LCG
+    stream, the same formulas (condex: the same projector, toeppd: the same cosine sums)."""
+    import numpy as np
+    import torch
+    env = dict(os.environ)
+    env.pop("PYTHONPATH", None)
+    env["DPLASMA_TEST_DUMP"] = str(tmp_path)
+    r = subprocess.run([_build_native(tmp_path)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    import dplasma_amd as dp
+    ctx = dp.init(device="cpu")
+    m, n = 40, 36
+    for z, dt in ((False, torch.float64), (True, torch.complex128)):
+        for t in (2, 7, 9, 12, 14, 23, 27, 29, 42):
+            raw = np.fromfile(str(tmp_path / f"pltmg_{'z' if z else 'd'}_{t}.bin"), dtype=np.float64)
+            got = raw.view(np.complex128) if z else raw
+            got = torch.from_numpy(got.reshape(n, m).T.copy())
+            A = dp.block_cyclic(ctx, dt, 16, 16, m, n)
+            assert dp.pltmg(ctx, t, A, 3872) == 0
+            ref = A.to_dense_local()
+            err = (got - ref).abs().max().item() / max(1.0, ref.abs().max().item())
+            assert err < 1e-12, (z, t, err)
+
+
+@pytest.mark.gpu
 def test_capi_f77_native_gpu(tmp_path):
     """ScaLAPACK F77 entry points without Python (one process, 1 x 1 BLACS grid -> the native engine):
     pdpotrf_ / pdgemm_ / pdgetrf_ / pdtrsm_ / pdtrmm_ on submatrices of host local arrays
