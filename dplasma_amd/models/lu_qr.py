@@ -51,6 +51,7 @@ from ..descriptor import TiledMatrix
 from ..ops import qr_ops
 from ..ops import tile_ops as ops
 from ..ops.batch import GemmBatch, TileBatch
+from ..ops.batch import unpredicated as ops_batch_unpredicated
 from ..parallel import comm
 from ..runtime.dag import TileDAG
 from ..runtime.taskpool import Taskpool
@@ -91,9 +92,22 @@ def genrandom_lutab(lu_tab, deb, fin, nb_lu, rec_depth=0):
     genrandom_lutab(lu_tab, new_fin + 1, fin, nb_lu - new_nb, rec_depth + 1)
 
 
-def _lapack(name, arr):
-    from scipy.linalg import lapack
-    return lapack.get_lapack_funcs((name,), (arr,))[0]
+def _w0(lu: torch.Tensor, crit: int) -> torch.Tensor:
+    """The criterion's measure of the domain's square LU (a 0-d tensor on lu's device, no host sync):
+    HIGHAM: cond_1(U) = ||U||_1 ||U^-1||_1; HIGHAM_SUM / MAX / MOY: 1 / ||(L U)^-1||_1.  Exact norms from
+    the triangular inverses (the reference estimates them with LAPACK's trcon / gecon,
+    src/zgetrf_qrf.jdf:739-846 -- the same quantities; a decision exactly at the estimate's error margin is
+    parity unpinned)."""
+    n = lu.shape[0]
+    eye = torch.eye(n, dtype=lu.dtype, device=lu.device)
+    U = torch.triu(lu)
+    if crit == HIGHAM_CRITERIUM:
+        Ui = torch.linalg.solve_triangular(U, eye, upper=True)
+        return U.abs().sum(0).max() * Ui.abs().sum(0).max()
+    L = torch.tril(lu, -1) + eye
+    X = torch.linalg.solve_triangular(L, eye, upper=False, unitriangular=True)
+    X = torch.linalg.solve_triangular(U, X, upper=True)
+    return 1.0 / X.abs().sum(0).max()
 
 
 class _Step:
@@ -130,7 +144,11 @@ class _GetrfQrf(Taskpool):
         # tree; T factors then live in its ("panel") format and trsmpl_qrf applies them the same way
         self.qpf = None
         if qr_panel.usable(A, tree):
-            self.qpf = qr_panel._Factor(ctx, A, TS, TT, tree)
+            # a data-dependent criterion may run device-decided (below): its QR panels then run under a predicate
+            # they do not see, so none may factor in place in A
+            maybe_dev = (ctx.world == 1 and A.device.type == "cuda" and (criteria in _HIGHAMS or criteria == MUMPS_CRITERIUM)
+                         and os.environ.get("DPLASMA_LUQR_DEVCRIT", "1") != "0")
+            self.qpf = qr_panel._Factor(ctx, A, TS, TT, tree, inplace=not maybe_dev)
             TS.qr_format = TT.qr_format = "panel"
         else:
             TS.qr_format = TT.qr_format = "tile"
@@ -145,6 +163,25 @@ class _GetrfQrf(Taskpool):
         # diagonal domain is reported through info at completion instead of turning that step into QR
         # (DPLASMA_LUQR_SYNC=1 keeps the reference's per-step host decision).
         self.fast = None
+        # Device-decided steps (one GPU process, a criterion that reads the matrix, p > 1): every step's domain
+        # LU, criterion and decision stay on the device and BOTH branches are issued predicated on the decision
+        # flag (ops/batch.py predicated: the untaken branch's batched launches run with empty items) -- no
+        # host synchronisation in the step loop; lu_tab is read back once at completion.
+        # DPLASMA_LUQR_DEVCRIT=0 keeps the per-step host decision.
+        self.devcrit = (ctx.world == 1 and A.device.type == "cuda" and self.qpf is not None and self.qpf.batched
+                        and (criteria in _HIGHAMS or criteria == MUMPS_CRITERIUM) and self.alpha != 0
+                        and self.alpha < 9999999999 and os.environ.get("DPLASMA_LUQR_DEVCRIT", "1") != "0"
+                        and os.environ.get("DPLASMA_LUQR_SYNC", "0") != "1")
+        self._dec = []
+        if self.devcrit:
+            # every step's tables, panel plans and workspaces now: the run issues no host round trip at all
+            for k in range(self.minMNT):
+                st = _Step(A, k, self.p)
+                self._dev_step(st)
+                key = (st.M, st.ncol)
+                if key not in self._panel_ws:
+                    self._panel_ws[key] = (ops.lu_workspace(st.M, A.device),
+                                           torch.zeros(1, dtype=torch.int32, device=A.device))
         fast_env = os.environ.get("DPLASMA_LUQR_FAST", "auto")   # auto: on GPU; 1: also on CPU; 0: never
         if (ctx.world == 1 and self.p == 1 and fast_env != "0" and (A.device.type == "cuda" or fast_env == "1")
                 and self._a_priori(0) is not None and os.environ.get("DPLASMA_LUQR_SYNC", "0") != "1"):
@@ -255,6 +292,131 @@ class _GetrfQrf(Taskpool):
             else:
                 self._qr_step(_Step(A, k, self.p))
 
+    # ------------------------------------------------------------------ device-decided steps
+    def _run_devcrit(self):
+        from ..ops import batch as B
+        A = self.A
+        self._dec = []
+        for k in range(self.minMNT):
+            st = _Step(A, k, self.p)
+            buf, view, ipiv, info, colmax = self._domain_lu_dev(st)
+            flag = self._criterion_dev(st, view, info, colmax)
+            self._dec.append(flag)
+            with B.predicated(flag):
+                self._lu_step_dev(st, buf, ipiv, flag)
+            with B.predicated(1 - flag):
+                self._qr_step(st, zero_ipiv=False)   # (the LU branch wrote IPIV(k, k) = flag * pivots)
+
+    def _domain_lu_dev(self, st: _Step):
+        """The stacked domain's LU on the device (a copy: A is untouched until the decision)."""
+        A = self.A
+        if self._pbuf is None:
+            self._pbuf = torch.empty(max(1, A.m * A.nb), dtype=A.dtype, device=A.device)
+        buf = self._pbuf[: st.ncol * st.M]
+        view = torch.as_strided(buf, (st.M, st.ncol), (1, st.M))
+        dv = self._dev_step(st)
+        ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, buf, st.M, dv["gather"], copy=True)
+        colmax = None
+        if self.criteria == MUMPS_CRITERIUM:
+            colmax = A.tile(st.k, st.k)[:st.ncol, :st.ncol].abs().amax(0)
+        ipiv = torch.zeros(max(st.kmax, 1), dtype=torch.int32, device=A.device)
+        info = torch.zeros(1, dtype=torch.int32, device=A.device)
+        key = (st.M, st.ncol)
+        ws = self._panel_ws.get(key)
+        if ws is None:
+            ws = self._panel_ws[key] = (ops.lu_workspace(st.M, A.device),
+                                        torch.zeros(1, dtype=torch.int32, device=A.device))
+        plu = self._plu.get(st.k)
+        if plu is None:
+            plu = self._plu[st.k] = ops.PanelLU(buf, st.M, st.M, st.ncol, pivot=True)
+        plu.run(ipiv, ws[0], ws[1], info, 0)
+        return buf, view, ipiv, info, colmax
+
+    def _criterion_dev(self, st: _Step, view, info, colmax):
+        """The step's decision as a device int32 flag [1] (1 = LU): _decide's formulas on device tensors."""
+        A, crit, alpha = self.A, self.criteria, self.alpha
+        bad = info[0] != 0
+        offs = [A.tile(m, st.k) for m in st.off]
+        if crit == MUMPS_CRITERIUM:
+            if offs:
+                off = torch.stack([t.abs().amax(0) for t in offs]).amax(0)[:st.ncol]
+                cond = (alpha * colmax >= off).all()
+            else:
+                cond = torch.ones((), dtype=torch.bool, device=A.device)
+        else:
+            lu = view[:st.ncol, :st.ncol]
+            w0 = torch.nan_to_num(_w0(lu, crit).to(torch.float64), nan=0.0, posinf=float("inf"))
+            n1 = torch.stack([t.abs().sum(0).max() for t in offs]).to(torch.float64) if offs else None
+            if crit in (HIGHAM_CRITERIUM, HIGHAM_SUM_CRITERIUM):
+                thr = n1.sum() if offs else torch.zeros((), dtype=torch.float64, device=A.device)
+                cond = alpha * w0 > thr
+            elif crit == HIGHAM_MAX_CRITERIUM:
+                thr = n1.max() if offs else torch.zeros((), dtype=torch.float64, device=A.device)
+                cond = alpha * w0 > thr
+            else:
+                nt_ = A.mt - st.k
+                nout = nt_ - (nt_ + self.p - 1) // self.p
+                if nout == 0:
+                    cond = torch.zeros((), dtype=torch.bool, device=A.device)   # 0 / 0: the reference's NaN
+                else:
+                    cond = alpha * w0 > n1.sum() / nout
+        return (cond & ~bad).to(torch.int32).view(1)
+
+    def _dev_step(self, st: _Step):
+        """Per-step batches of the device-decided path (built once, cached): domain gather / write-back and the
+        stacked-row table of the trailing row interchanges."""
+        d = self.__dict__.setdefault("_devb", {}).get(st.k)
+        if d is not None:
+            return d
+        A, k = self.A, st.k
+        g, back = TileBatch(), TileBatch()
+        r0 = 0
+        for m, r in zip(st.dom, st.rows):
+            g.add(A.offset(m, k), r, st.ncol, b_off=r0)
+            back.add(r0, r, st.ncol, b_off=A.offset(m, k))
+            r0 += r
+        d = {"gather": g.finalize(), "back": back.finalize()}
+        trail = list(range(k + 1, A.nt))
+        if trail:
+            base = A.offset(st.dom[0], trail[0])
+            d["rowoff"] = torch.tensor([A.offset(m, trail[0]) - base for m in st.dom], dtype=torch.int64,
+                                       device=A.device)
+            d["coloff"] = torch.tensor([A.offset(st.dom[0], n) for n in trail], dtype=torch.int64, device=A.device)
+            d["ncols"] = torch.tensor([A.tile_cols(n) for n in trail], dtype=torch.int32, device=A.device)
+            nb = A.nb
+            d["mv"] = (torch.zeros(2 * nb, dtype=torch.int32, device=A.device),
+                       torch.zeros(2 * nb, dtype=torch.int32, device=A.device),
+                       torch.zeros(1, dtype=torch.int32, device=A.device))
+        self._devb[k] = d
+        return d
+
+    def _lu_step_dev(self, st: _Step, buf, ipiv, flag):
+        """The LU branch, issued under the step's predicate: factored domain back into A, the pivots into IPIV,
+        the interchanges inside the domain stack of every trailing column (device move list, its count
+        multiplied by the flag), then the solves and the update (batched: predicated)."""
+        A, k = self.A, st.k
+        d = self._dev_step(st)
+        ops.geadd(0, N_, 1.0, buf, st.M, 0.0, A.data, A.ld, d["back"], copy=True)
+        if self.IPIV.is_local(k, k):
+            t = self.IPIV.tile(k, k)
+            new = torch.zeros_like(t)
+            new[:st.kmax, 0] = ipiv[:st.kmax] + 1
+            t.copy_(new * flag.to(t.dtype))
+        if "rowoff" in d:
+            mdst, msrc, mcnt = d["mv"]
+            with ops_batch_unpredicated():
+                ops.piv_moves(ipiv, st.kmax, mdst, msrc, mcnt, mrel=st.M, info=self._devinfo())
+            mcnt.mul_(flag)
+            ops.rows_permute(A.data, A.ld, A.mb, 0, d["rowoff"], d["coloff"], d["ncols"], A.nb, mdst, msrc, mcnt,
+                             2 * A.nb, self._devinfo())
+        self._lu_update_local(st)
+
+    def _devinfo(self):
+        t = self.__dict__.get("_dinfo")
+        if t is None:
+            t = self._dinfo = torch.zeros(1, dtype=torch.int32, device=self.A.device)
+        return t
+
     # ------------------------------------------------------------------ one panel
     def _domain_lu(self, st: _Step):
         """Stacked LU of the domain on the diagonal owner -> (buffer, ipiv, info, W0, colmax)."""
@@ -289,14 +451,8 @@ class _GetrfQrf(Taskpool):
         w0 = 0.0
         bad = int(info.item()) != 0
         if not bad and self.criteria in _HIGHAMS:
-            lu = view[:st.ncol, :st.ncol].cpu().numpy()
-            lu = np.asfortranarray(lu.astype(np.complex128 if A.dtype.is_complex else np.float64))
-            if self.criteria == HIGHAM_CRITERIUM:
-                rc, _ = _lapack("trcon", lu)(lu, norm="1", uplo="U", diag="N")
-                w0 = 1.0 / rc if rc > 0 else np.inf
-            else:
-                rc, _ = _lapack("gecon", lu)(lu, 1.0, norm="1")
-                w0 = float(rc)
+            lu = view[:st.ncol, :st.ncol].cpu().to(torch.complex128 if A.dtype.is_complex else torch.float64)
+            w0 = float(_w0(lu, self.criteria))
         return buf, view, ipiv, bad, w0, colmax
 
     def _offdomain_norms(self, st: _Step):
@@ -443,9 +599,9 @@ class _GetrfQrf(Taskpool):
         if gb is not None:
             ops.gemm(N_, N_, -1.0, A.data, A.ld, A.data, A.ld, 1.0, A.data, A.ld, gb)
 
-    def _qr_step(self, st: _Step):
+    def _qr_step(self, st: _Step, zero_ipiv: bool = True):
         A, ctx, k = self.A, self.ctx, st.k
-        if self.IPIV.is_local(k, k):
+        if zero_ipiv and self.IPIV.is_local(k, k):
             self.IPIV.tile(k, k).zero_()
         f = self.qpf
         if f is not None:
@@ -476,6 +632,11 @@ class _GetrfQrf(Taskpool):
             if self.info_out is not None:
                 self.info_out[0] = 0
             return
+        if self.devcrit:
+            self._run_devcrit()
+            if self.info_out is not None:
+                self.info_out[0] = 0
+            return
         for k in range(self.minMNT):
             st = _Step(A, k, self.p)
             mine = self._domain_lu(st) if ctx.rank == st.owner else None
@@ -494,6 +655,13 @@ class _GetrfQrf(Taskpool):
         if self.qpf is not None and int(self.qpf.info.item()) != 0:
             raise RuntimeError(f"getrf_qrf: QR panel kernel reported {int(self.qpf.info.item())}")
         r = int(self.fast_info.item()) if self.fast is not None else 0
+        if self.devcrit and self._dec:
+            # the decisions, read back once for the whole factorisation
+            dec = torch.cat(self._dec).cpu().tolist()
+            for k, c in enumerate(dec):
+                self.lu_tab[k] = int(c)
+            if "_dinfo" in self.__dict__ and int(self._dinfo.item()) != 0:
+                raise RuntimeError(f"getrf_qrf: row interchanges reported {int(self._dinfo.item())}")
         if self.info_out is not None:
             self.info_out[0] = r
         self._result = r

@@ -45,7 +45,7 @@ import torch
 
 from ..constants import dplasmaConjTrans, dplasmaLeft, dplasmaNoTrans, dplasmaTrans
 from ..ops import tile_ops as ops
-from ..ops.batch import GemmBatch, TileBatch
+from ..ops.batch import GemmBatch, TileBatch, unpredicated
 from ..parallel import comm
 from ..runtime.taskpool import Taskpool
 from ..utils.flops import flops
@@ -465,8 +465,11 @@ def _rebuild_T(V, ldv, M, kf, Td, row, k, out, ldt):
 
 # ----------------------------------------------------------------------------- factorisation
 class _Factor:
-    def __init__(self, ctx, A, TS, TT, tree):
+    def __init__(self, ctx, A, TS, TT, tree, inplace=True):
         self.ctx, self.A, self.TS, self.TT = ctx, A, TS, TT
+        # inplace=False: every domain is gathered into the panel buffer, none factored in place in A (a caller
+        # that issues the panel kernels beside a predicate they ignore -- models/lu_qr.py -- needs A untouched)
+        self.inplace = inplace
         dev, dt = A.device, A.dtype
         nb = A.nb
         self.kt = min(A.mt, A.nt)
@@ -651,11 +654,14 @@ class _Factor:
         A = self.A
         nb = A.nb
         Tb = g["Tb"]
-        if g["zero"]:
-            self.Pb[: g["plen"]].zero_()
-        if g["gather"] is not None:
-            ops.geadd(g["part"], N_, 1.0, A.data, A.ld, 0.0, self.Pb, g["ld"], g["gather"], copy=True)
-        g["multi"].run(self.info)
+        # (a predicated step -- models/lu_qr.py -- still factors its panel: only scratch buffers are written
+        # here, and the kernel must see a whole panel either way)
+        with unpredicated():
+            if g["zero"]:
+                self.Pb[: g["plen"]].zero_()
+            if g["gather"] is not None:
+                ops.geadd(g["part"], N_, 1.0, A.data, A.ld, 0.0, self.Pb, g["ld"], g["gather"], copy=True)
+            g["multi"].run(self.info)
         if g["back"] is not None:
             ops.geadd(g["part"], N_, 1.0, self.Pb, g["ld"], 0.0, A.data, A.ld, g["back"], copy=True)
         Td = g["Td"]
@@ -740,7 +746,7 @@ class _Factor:
             rin = TileBatch().add(0, A.tile_rows(rows[1]), kb, b_off=voff[1])
             e["r_in"] = rin.finalize()   # R buffer -> P (upper part)
         # a domain of consecutive tile rows stored contiguously is factored in place
-        if not tt and list(rows) == list(range(rows[0], rows[0] + len(rows))) and g.P == 1:
+        if not tt and self.inplace and list(rows) == list(range(rows[0], rows[0] + len(rows))) and g.P == 1:
             if A.storage == "tile" or A.ld == A.mb:
                 e["direct"] = (A.mb, A.mb, A.mb * A.nb, A.offset(rows[0], k))
             else:

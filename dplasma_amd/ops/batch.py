@@ -7,6 +7,8 @@ PyTorch tile operations on the CPU reference path.  The record layouts match
 """
 from __future__ import annotations
 
+import contextlib
+
 import numpy as np
 import torch
 
@@ -17,6 +19,45 @@ TILE_ITEM = np.dtype([("a_off", "<i8"), ("b_off", "<i8"), ("m", "<i4"), ("n", "<
 assert GEMM_ITEM.itemsize == 32 and KPAIR.itemsize == 24 and TILE_ITEM.itemsize == 32
 
 MASK_FULL, MASK_LOWER, MASK_UPPER = 0, 1, 2
+
+# Predicated issue (models/lu_qr.py's device-decided steps): while a device flag is set, every batch handed to a
+# kernel is a copy whose item sizes (m, n: int32 words 4 and 5 of both 32-byte records) are multiplied by the
+# flag on the device -- flag 0 turns every launch of the branch into workgroups that exit at once, without the
+# host ever reading the flag.  Nested predicates multiply.
+_PRED = [None]
+
+
+@contextlib.contextmanager
+def predicated(flag):
+    """Issue the enclosed batch launches under a device int32 flag (shape [1]): 1 runs them, 0 skips them."""
+    old = _PRED[0]
+    _PRED[0] = flag if old is None else old * flag
+    try:
+        yield
+    finally:
+        _PRED[0] = old
+
+
+@contextlib.contextmanager
+def unpredicated():
+    """Launches that must run whatever the enclosing predicate (e.g. work whose result only feeds predicated
+    launches, and which must not see skipped inputs)."""
+    old = _PRED[0]
+    _PRED[0] = None
+    try:
+        yield
+    finally:
+        _PRED[0] = old
+
+
+def _pred(t: torch.Tensor) -> torch.Tensor:
+    f = _PRED[0]
+    if f is None or t.numel() == 0:
+        return t
+    p = t.clone()
+    v = p.view(torch.int32).view(-1, 8)
+    v[:, 4:6] *= f.to(device=p.device, dtype=torch.int32)
+    return p
 
 
 class _Uploadable:
@@ -139,7 +180,7 @@ class GemmBatch(_Uploadable):
 
     def device_arrays(self, device):
         self.finalize()
-        return self._upload(self.items, device), self._upload(self.kpairs, device)
+        return _pred(self._upload(self.items, device)), self._upload(self.kpairs, device)
 
 
 class TileBatch(_Uploadable):
@@ -168,4 +209,4 @@ class TileBatch(_Uploadable):
 
     def device_array(self, device):
         self.finalize()
-        return self._upload(self.items, device)
+        return _pred(self._upload(self.items, device))

@@ -23,6 +23,7 @@ from ..constants import (dplasmaConjTrans, dplasmaLeft, dplasmaLower, dplasmaNon
                          dplasmaTrans, dplasmaUnit, dplasmaUpper)
 from ..utils import lcg
 from . import _lib
+from .batch import _pred as _pred_items
 from .batch import MASK_LOWER, MASK_UPPER, GemmBatch, TileBatch
 
 FORCE_GENERIC_GEMM = False  # testing knob: route real GEMMs through the FMA kernel
@@ -396,7 +397,7 @@ def trsm_strip(side, uplo, trans, diag, alpha, A, lda, B, ldb, batch):
     for sub in _trsm_groups(batch, side, B):
         sa = _lib.Scalar(alpha, B.dtype)
         rc = lib.dpl_trsm_batched(_lib.prec_code(B.dtype), side, uplo, trans, diag, len(sub.items),
-                                  sub.items_dev.data_ptr(), sub.max_m, sub.max_n, sa.ptr, A.data_ptr(), lda,
+                                  _pred_items(sub.items_dev).data_ptr(), sub.max_m, sub.max_n, sa.ptr, A.data_ptr(), lda,
                                   B.data_ptr(), ldb, sub.ntri, sub.tri_dev.data_ptr(), sub.work.data_ptr(),
                                   _lib.stream_ptr())
         _lib.check(rc, "trsm_batched")
@@ -418,7 +419,7 @@ def trsm(side: int, uplo: int, trans: int, diag: int, alpha, A: torch.Tensor, ld
         for sub in _trsm_groups(batch, side, B):
             sa = _lib.Scalar(alpha, B.dtype)
             rc = lib.dpl_trsm_batched(_lib.prec_code(B.dtype), side, uplo, trans, diag, len(sub.items),
-                                      sub.items_dev.data_ptr(), sub.max_m, sub.max_n, sa.ptr, A.data_ptr(), lda,
+                                      _pred_items(sub.items_dev).data_ptr(), sub.max_m, sub.max_n, sa.ptr, A.data_ptr(), lda,
                                       B.data_ptr(), ldb, sub.ntri, sub.tri_dev.data_ptr(), sub.work.data_ptr(),
                                       _lib.stream_ptr())
             _lib.check(rc, "trsm_batched")

@@ -73,9 +73,9 @@ def test_random_lutab():
     assert sum(t) == 0
 
 
-def _worker(rank, world, P):
+def _worker(rank, world, P, crit=dp.DEFAULT_CRITERIUM, alpha=1.0):
     ctx = dp.init(device="cpu", P=P)
-    a0, b0, B, lu_tab = _solve(ctx, torch.float64, 96, 16, 4, dp.DEFAULT_CRITERIUM, 1.0, None)
+    a0, b0, B, lu_tab = _solve(ctx, torch.float64, 96, 16, 4, crit, alpha, None)
     x = B.to_dense_local()
     import torch.distributed as dist
     for t in (x, a0, b0):
@@ -88,6 +88,19 @@ def test_getrf_qrf_distributed(ctx):
     tabs = [out[r][1] for r in range(4)]
     assert all(t == tabs[0] for t in tabs)
     assert all(out[r][0] < 60 for r in range(4))
+
+
+@pytest.mark.parametrize("crit,alpha", [(dp.HIGHAM_CRITERIUM, 0.02), (dp.HIGHAM_SUM_CRITERIUM, 1.0),
+                                        (dp.MUMPS_CRITERIUM, 1.0)])
+def test_getrf_qrf_distributed_data_criteria(ctx, crit, alpha):
+    """Data-dependent criteria on a 2 x 1 grid (p = 2): the criterion's pieces are reduced across the ranks, every
+    rank takes the same decisions, and they are the one-process decisions for the same matrix."""
+    out = run_distributed(_worker, 2, 2, crit, alpha)
+    tabs = [out[r][1] for r in range(2)]
+    assert tabs[0] == tabs[1]
+    assert all(out[r][0] < 60 for r in range(2))
+    _, _, _, tab1 = _solve(ctx, torch.float64, 96, 16, 4, crit, alpha, 2)
+    assert tabs[0] == tab1
 
 
 @pytest.mark.gpu
@@ -165,3 +178,56 @@ def test_gpu_getrf_qrf_device_path(crit, alpha):
     g = dp.init(device="cuda:0")
     a0, b0, B, lu_tab = _solve(g, torch.float64, 1536, 256, 32, crit, alpha, 1)
     assert _resid(a0.cpu(), b0.cpu(), B.to_dense_local().cpu(), "d") < 60
+
+
+def _luqr_run(g, crit, alpha, devcrit, monkeypatch, N=1536, NB=256, p=2, sync_error=False):
+    monkeypatch.setenv("DPLASMA_LUQR_DEVCRIT", "1" if devcrit else "0")
+    dt = torch.float64
+    A = dp.block_cyclic(g, dt, NB, NB, N, N)
+    dp.plrnt(g, A, 7)
+    TS = dp.block_cyclic(g, dt, 32, NB, A.mt * 32, N)
+    TT = dp.block_cyclic(g, dt, 32, NB, A.mt * 32, N)
+    IP = dp.qrf_ipiv_descriptor(g, A)
+    tree = qrtree.hqr_init(dp.dplasmaNoTrans, A, qrtree.GREEDY_TREE, qrtree.FLAT_TREE, 2, p)
+    tab = [0] * A.mt
+    tp = dp.getrf_qrf_New(g, tree, A, IP, TS, TT, crit, alpha, tab, p=p)
+    assert tp.devcrit == devcrit
+    torch.cuda.synchronize()
+    if sync_error:
+        torch.cuda.set_sync_debug_mode("error")   # any host synchronisation in the step loop raises
+    try:
+        tp.run(g)
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    tp.complete(g)
+    return tab, A.to_dense_local().cpu(), IP.to_dense_local().cpu()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("crit,alpha", [(dp.HIGHAM_CRITERIUM, 0.02), (dp.HIGHAM_SUM_CRITERIUM, 1.0),
+                                        (dp.HIGHAM_MAX_CRITERIUM, 2.0), (dp.HIGHAM_MOY_CRITERIUM, 4.0),
+                                        (dp.MUMPS_CRITERIUM, 1.0), (dp.MUMPS_CRITERIUM, 3.0)])
+def test_gpu_luqr_device_criterion(monkeypatch, crit, alpha):
+    """Data-dependent criteria with p = 2 on one GPU: the domain LU, the criterion (exact 1-norm measures,
+    off-domain norms / column maxima) and the decision stay on the device and both branches are issued
+    predicated on it -- the run raises under sync-debug "error" if anything synchronises -- and the result
+    (lu_tab, factors, pivots) is the host-decided path's."""
+    g = dp.init(device="cuda:0")
+    tab_d, a_d, ip_d = _luqr_run(g, crit, alpha, True, monkeypatch, sync_error=True)
+    tab_h, a_h, ip_h = _luqr_run(g, crit, alpha, False, monkeypatch)
+    print(crit, alpha, "lu_tab", tab_d)
+    assert tab_d == tab_h
+    assert torch.equal(ip_d, ip_h)
+    assert (a_d - a_h).abs().max().item() < 1e-9 * max(1.0, a_h.abs().max().item())
+
+
+def test_luqr_w0_exact_norms():
+    """_w0: cond_1(U) and 1 / ||(L U)^-1||_1 from the triangular inverses match dense numpy inverses."""
+    rng = np.random.default_rng(3)
+    lu = torch.from_numpy(rng.standard_normal((24, 24)) + 6 * np.eye(24))
+    U = np.triu(lu.numpy())
+    L = np.tril(lu.numpy(), -1) + np.eye(24)
+    c = np.abs(U).sum(0).max() * np.abs(np.linalg.inv(U)).sum(0).max()
+    assert abs(float(lu_qr._w0(lu, dp.HIGHAM_CRITERIUM)) - c) < 1e-10 * c
+    r = 1.0 / np.abs(np.linalg.inv(L @ U)).sum(0).max()
+    assert abs(float(lu_qr._w0(lu, dp.HIGHAM_SUM_CRITERIUM)) - r) < 1e-10 * r
