@@ -110,6 +110,17 @@ struct DtrArgs {
   int* prog;                // nt x 2 x MAXB x PSTRIDE: tile-step flags, then W-column flags
   int* info;
   long long* trace;         // optional (DPLASMA_DTR_TRACE): per task {start, end, wg << 8 | xcd, visible}, 100 MHz ticks
+  // ---- push scheduling (k_dtr_q): per-task pending-predecessor counts, successor lists, ready rings
+  int ntask;
+  int nclass;               // priority classes (ring r = class * 8 + XCD; lower class first)
+  int* pend;                // per task: predecessors not yet complete (reset per launch)
+  const int* succ_off;      // ntask + 1
+  const int* succ;          // successor task ids
+  const int* ring_of;       // per task: the ready ring it is pushed to
+  const int* qbase;         // nclass * 8 + 1 slot offsets
+  int* qctl;                // per ring: head at [2 r PSTRIDE], tail at [(2 r + 1) PSTRIDE] (reset per launch)
+  int* qslot;               // ring slots: task id + 1, 0 = reserved but not yet written (reset per launch)
+  int* done;                // completed tasks
 };
 
 constexpr int NBT = 512;    // tile size
@@ -686,11 +697,146 @@ __global__ __launch_bounds__(256, 2) void k_dtr_potrf(const DtrArgs* __restrict_
   __builtin_amdgcn_s_setprio(0);
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Push scheduling: a task becomes READY when its last predecessor completes -- that predecessor's workgroup
+// decrements the pending count of each successor (64 lanes at once) and pushes the one it brought to zero into
+// a ready ring: one FIFO per (priority class, XCD), sized for every task that will ever enter it (pushes
+// never wrap).  Workers pop the lowest non-empty class, own XCD first: the ready critical-path task (a POTRF
+// block, a panel TRSM, a look-ahead update) is the next one any idle workgroup takes, with no list position to
+// wait behind -- what the reference's priority-ordered ready queues do on every rank (src/zpotrf_L.jdf:58-69).
+// The lists + version counters of k_dtr_potrf make a ready task wait behind its list's head; its traces showed
+// that wait as the critical path (profiles/r5_dtr_queue.txt).
+// A push reserves a slot (tail atomic) and then stores the id (sc1): a popper that finds the reserved slot still
+// 0 treats the ring as empty for now.  Completion order: release (every wave's stores drained, agent release)
+// before the decrements, so a pushed task's inputs are visible to the popper's acquire.
+__device__ inline int q_pop(const DtrArgs& g, int r) {
+  int* head = g.qctl + (size_t)(2 * r) * PSTRIDE;
+  int* tail = head + PSTRIDE;
+  for (int tries = 0; tries < 2; ++tries) {
+    const int h = __builtin_amdgcn_readfirstlane(ld_sc1(head));
+    const int tl = __builtin_amdgcn_readfirstlane(ld_sc1(tail));
+    if (h >= tl) return -1;
+    const int s = __builtin_amdgcn_readfirstlane(ld_sc1(g.qslot + g.qbase[r] + h));
+    if (s == 0) return -1;
+    int won = 0;
+    if ((threadIdx.x & 63) == 0) won = atomicCAS(head, h, h + 1) == h;
+    if (__builtin_amdgcn_readfirstlane(won)) return s - 1;
+  }
+  return -1;
+}
+
+__device__ inline void q_push(const DtrArgs& g, int t) {   // one lane
+  const int r = g.ring_of[t];
+  int* tail = g.qctl + (size_t)(2 * r + 1) * PSTRIDE;
+  const int pos = atomicAdd(tail, 1);
+  st_sc1(g.qslot + g.qbase[r] + pos, t + 1);
+}
+
+__global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ gargs) {
+  __shared__ int s_task;
+  const int tid = threadIdx.x;
+  const int xcd = xcc_id();
+  unsigned long long idle0 = 0;
+  int nap = 1;
+  for (;;) {
+    const DtrArgs* gp = gargs;
+    asm volatile("" : "+s"(gp));
+    const DtrArgs& g = *gp;
+    if (tid < 64) {
+      int t = -1;
+      if (ld_sc1(g.info) == -1000) {
+        t = -2;
+      } else {
+        // every ring's emptiness at once (lane l: scan position l + 64 w, class-major, own XCD first inside a
+        // class), then a pop of the first non-empty one in that order; a lost race rescans
+        const int nr = g.nclass * 8;
+        const int l = tid & 63;
+        for (int tries = 0; tries < 4 && t < 0; ++tries) {
+          int best = -1;
+          for (int w0 = 0; w0 < nr && best < 0; w0 += 64) {
+            const int pos = w0 + l;
+            bool ne = false;
+            int r = 0;
+            if (pos < nr) {
+              r = (pos & ~7) + ((xcd + pos) & 7);
+              const int* hd = g.qctl + (size_t)(2 * r) * PSTRIDE;
+              ne = ld_sc1(hd) < ld_sc1(hd + PSTRIDE);
+            }
+            const unsigned long long bal = __builtin_amdgcn_ballot_w64(ne);
+            if (bal) {
+              const int first = __builtin_ctzll(bal);
+              best = __builtin_amdgcn_readlane(r, first);
+            }
+          }
+          if (best < 0) break;
+          t = q_pop(g, best);
+        }
+        if (t < 0 && __builtin_amdgcn_readfirstlane(ld_sc1(g.done)) >= g.ntask) t = -2;
+      }
+      if (t >= 0) {
+        if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        idle0 = 0;
+      } else if (t == -1 && tid == 0) {
+        const unsigned long long now = now_t();
+        if (idle0 == 0) idle0 = now;
+        else if (now - idle0 > 400000000ULL) {   // 4 s without a ready task: drain
+          atomicExch(g.info, -1000);
+          t = -2;
+        }
+      }
+      if (tid == 0) s_task = t;
+    }
+    __syncthreads();
+    const int t = __builtin_amdgcn_readfirstlane(s_task);
+    __syncthreads();
+    if (t == -2) break;
+    if (t == -1) {
+      for (int q = 0; q < nap; ++q) __builtin_amdgcn_s_sleep(1);
+      nap = nap < 16 ? 2 * nap : 16;
+      continue;
+    }
+    nap = 1;
+    const unsigned long long t_start = now_t();
+    const DtrTask tk = g.tasks[t];
+    if (tk.type == T_UPD) run_upd(gp, t, 0);
+    else if (tk.type == T_TRSM) run_trsm(gp, t, 0);
+    else run_potrf(gp, t, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0 && g.trace) {
+      long long* tr = g.trace + 4 * (size_t)t;
+      tr[0] = (long long)t_start;
+      tr[1] = (long long)now_t();
+      tr[2] = ((long long)blockIdx.x << 8) | xcd;
+      atomicAdd((unsigned long long*)(tr + 3), 1ULL);
+    }
+    if (tid < 64) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int sb = g.succ_off[t], se = g.succ_off[t + 1];
+      for (int q = sb + tid; q < se; q += 64) {
+        const int sx = g.succ[q];
+        if (atomicSub(g.pend + sx, 1) == 1) q_push(g, sx);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (tid == 0) atomicAdd(g.done, 1);
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
+}
+
 }  // namespace
 
 // One DTR Cholesky launch (see the header).  args: a DtrArgs image built by the host (models/potrf_dtr.py
 // fills it through dpl_dtr_args_size / the field offsets below), grid = 2 x #CUs workgroups.
 DPL_API int dpl_dtr_args_size() { return (int)sizeof(DtrArgs); }
+// the push-scheduled launch (k_dtr_q): one process, one rank
+DPL_API int dpl_dtr_potrf_q(const void* args_dev, int nwg, hipStream_t st) {
+  if (nwg <= 0 || !args_dev) return -3;
+  hipLaunchKernelGGL(k_dtr_q, dim3(nwg), dim3(256), 0, st, (const DtrArgs*)args_dev);
+  return (int)hipGetLastError();
+}
 DPL_API int dpl_dtr_lds_doubles() { return LDS_D; }
 // args_dev: the DtrArgs image in device memory (uploaded by the host before the launch)
 DPL_API int dpl_dtr_potrf(const void* args_dev, int nwg, hipStream_t st) {
@@ -708,7 +854,9 @@ DPL_API long long dpl_dtr_field(const char* name) {
 
   DTR_FIELD(hi_off) DTR_FIELD(nsteps) DTR_FIELD(hs_off) DTR_FIELD(scur) DTR_FIELD(lo) DTR_FIELD(lo_off) DTR_FIELD(A) DTR_FIELD(recv) DTR_FIELD(W) DTR_FIELD(cnt)
   DTR_FIELD(vis) DTR_FIELD(link) DTR_FIELD(bw_bpt) DTR_FIELD(lat_t) DTR_FIELD(Mw) DTR_FIELD(Sw) DTR_FIELD(Lp)
-  DTR_FIELD(Wp) DTR_FIELD(prog) DTR_FIELD(info) DTR_FIELD(trace)
+  DTR_FIELD(Wp) DTR_FIELD(prog) DTR_FIELD(info) DTR_FIELD(trace) DTR_FIELD(ntask) DTR_FIELD(nclass) DTR_FIELD(pend)
+  DTR_FIELD(succ_off) DTR_FIELD(succ) DTR_FIELD(ring_of) DTR_FIELD(qbase) DTR_FIELD(qctl) DTR_FIELD(qslot)
+  DTR_FIELD(done)
   if (!std::strcmp(name, "size")) return (long long)sizeof(DtrArgs);
   if (!std::strcmp(name, "task")) return (long long)sizeof(DtrTask);
   if (!std::strcmp(name, "MAXB")) return MAXB;

@@ -304,14 +304,83 @@ class _Plan:
         self.block_of = block_of
 
 
+# push scheduling classes: 0 POTRF blocks, 1 panel TRSM strips, then the updates by output column j (the step that
+# needs them), in at most UPD_BUCKETS buckets
+UPD_BUCKETS = 22
+NCLASS = 2 + UPD_BUCKETS
+
+
+def queue_plan(plan):
+    """Push scheduling (k_dtr_q) of a _Plan: the requirement lists turned into task edges, and the ready rings.
+
+    Requirement (c, v) on a sub-tile version / strip marker counter (c < WB) names the task that made its v-th
+    increment -- those counters are bumped in emission order, each bump depending on the previous one -- and a
+    W_k requirement (c = WB + k, all 16 blocks) names POTRF(k)'s 16 block tasks.  Returns a dict of int32 arrays:
+    ndeps, succ_off, succ, ring_of, qbase, qinit (the initially ready tasks' slots) and tinit (initial tails)."""
+    tasks, reqs, WB = plan.tasks, plan.reqs, plan.WB
+    n = len(tasks)
+    inc = tasks["inc"].astype(np.int64)
+    # the increments of every counter in emission order: sorted (counter, task id)
+    has = np.nonzero(inc >= 0)[0]
+    srt = has[np.lexsort((has, inc[has]))]
+    sc = inc[srt]
+    ncnt = int(max(inc.max(), int(reqs[:, 0].max()) if len(reqs) else 0)) + 1
+    cstart = np.searchsorted(sc, np.arange(ncnt + 1))
+    ccount = np.diff(cstart)
+    # requirement records: consumer, counter, value
+    nr = tasks["nreq"].astype(np.int64)
+    rt = np.repeat(np.arange(n, dtype=np.int64), nr)
+    rb = np.repeat(tasks["req_beg"].astype(np.int64), nr) + (np.arange(int(nr.sum())) - np.repeat(np.cumsum(nr) - nr, nr))
+    rc, rv = reqs[rb, 0].astype(np.int64), reqs[rb, 1].astype(np.int64)
+    keep = rv > 0
+    rt, rc, rv = rt[keep], rc[keep], rv[keep]
+    if np.any(ccount[rc] < rv):
+        raise RuntimeError("queue_plan: a requirement names an increment that never happens")
+    ver = rc < WB
+    cons = [rt[ver]]
+    prod = [srt[cstart[rc[ver]] + rv[ver] - 1]]
+    w = ~ver                                           # W_k: every POTRF block of panel k
+    if w.any():
+        m = ccount[rc[w]]
+        cons.append(np.repeat(rt[w], m))
+        prod.append(srt[np.repeat(cstart[rc[w]], m) + (np.arange(int(m.sum())) - np.repeat(np.cumsum(m) - m, m))])
+    cons, prod = np.concatenate(cons), np.concatenate(prod)
+    pair = np.unique(prod * n + cons)
+    prod, cons = pair // n, pair % n
+    ndeps = np.bincount(cons, minlength=n).astype(np.int32)
+    succ_off = np.zeros(n + 1, dtype=np.int32)
+    succ_off[1:] = np.cumsum(np.bincount(prod, minlength=n))
+    succ = cons.astype(np.int32) if len(cons) else np.zeros(1, dtype=np.int32)   # pairs sorted by producer
+    typ = tasks["type"]
+    nbk = max(1, min(plan.nt, UPD_BUCKETS))
+    ucls = 2 + np.minimum(nbk - 1, tasks["j"].astype(np.int64) * nbk // max(1, plan.nt))
+    cls = np.where(typ == T_POTRF, 0, np.where(typ == T_TRSM, 1, ucls))
+    # XCD of the ring: the POTRF blocks spread over all eight (the 16 cooperate and must start together), TRSM by
+    # tile row, updates by output column (the low lists' L2 locality)
+    xcd = np.where(typ == T_POTRF, tasks["r"] % 8, np.where(typ == T_TRSM, tasks["i"] % 8, tasks["j"] % 8))
+    ring_of = (cls * 8 + xcd).astype(np.int32)
+    nring = NCLASS * 8
+    cap = np.bincount(ring_of, minlength=nring)
+    qbase = np.zeros(nring + 1, dtype=np.int32)
+    qbase[1:] = np.cumsum(cap)
+    qinit = np.zeros(max(1, n), dtype=np.int32)
+    tinit = np.zeros(nring, dtype=np.int32)
+    for t in np.nonzero(ndeps == 0)[0]:
+        r = ring_of[t]
+        qinit[qbase[r] + tinit[r]] = t + 1
+        tinit[r] += 1
+    return {"ndeps": ndeps, "succ_off": succ_off, "succ": succ, "ring_of": ring_of, "qbase": qbase,
+            "qinit": qinit, "tinit": tinit, "cls": cls}
+
+
 class ArgsImage:
     """Host image of the kernel's DtrArgs, packed by field name (offsets from dpl_dtr_field: the struct is
     laid out by the device compiler, not mirrored here)."""
 
     _LL = ("ld", "ncnt", "bw_bpt", "lat_t")
-    _INT = ("nt", "nranks", "rank", "epoch", "flags", "dil", "nsteps")
+    _INT = ("nt", "nranks", "rank", "epoch", "flags", "dil", "nsteps", "ntask", "nclass")
     _PTR = ("tasks", "reqs", "tab", "xoff", "cur", "hs_off", "scur", "hi", "lo", "vis", "link", "Mw", "Sw", "Lp", "Wp",
-            "prog", "info", "trace")
+            "prog", "info", "trace", "pend", "succ_off", "succ", "ring_of", "qbase", "qctl", "qslot", "done")
     _PARR = ("A", "recv", "W", "cnt")
     _IARR = ("hi_off", "lo_off")
 
@@ -490,8 +559,33 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     # progress needs a workgroup on every XCD (a low list is another XCD's to steal only once that XCD's
     # own list is exhausted) and the 16 cooperating POTRF workgroups co-resident: at least 64 of them
     nwg = max(64, min(nwg, 2 * ncu))
-    tp._keep = (tasks_d, reqs_d, hi_d, lo_d, tab_d, cnt, cur, hs_d, scur, W, scr, hosts, args_d)
+    # scheduling: "queue" (default) -- push scheduling, a task is pushed into its priority class's ready ring by
+    # the completion of its last predecessor (k_dtr_q, queue_plan); "lists" -- the static high / low lists with
+    # version-counter readiness (k_dtr_potrf)
+    sched = os.environ.get("DPLASMA_DTR_SCHED", "queue")
+    if sched not in ("queue", "lists"):
+        raise ValueError("DPLASMA_DTR_SCHED must be queue or lists")
+    qk = None
+    if sched == "queue":
+        qp = getattr(plan, "_queue", None)
+        if qp is None:
+            qp = plan._queue = queue_plan(plan)
+        nring = NCLASS * 8
+        qctl_init = torch.zeros(2 * nring * PST, dtype=torch.int32)
+        qctl_init.view(nring, 2, PST)[:, 1, 0] = torch.from_numpy(qp["tinit"])
+        qk = {"pend0": up(qp["ndeps"]), "pend": torch.empty(len(qp["ndeps"]), dtype=torch.int32, device=dev),
+              "succ_off": up(qp["succ_off"]), "succ": up(qp["succ"]), "ring_of": up(qp["ring_of"]),
+              "qbase": up(qp["qbase"]), "qctl0": qctl_init.to(dev), "qctl": torch.empty(2 * nring * PST, dtype=torch.int32,
+                                                                                          device=dev),
+              "qslot0": up(qp["qinit"]), "qslot": torch.empty(len(qp["qinit"]), dtype=torch.int32, device=dev),
+              "done": torch.zeros(1, dtype=torch.int32, device=dev)}
+        img.set("ntask", len(plan.tasks))
+        img.set("nclass", NCLASS)
+        for f in ("pend", "succ_off", "succ", "ring_of", "qbase", "qctl", "qslot", "done"):
+            img.set(f, qk[f].data_ptr())
+    tp._keep = (tasks_d, reqs_d, hi_d, lo_d, tab_d, cnt, cur, hs_d, scur, W, scr, hosts, args_d, qk)
     tp.dtr_plan = plan
+    tp.dtr_sched = sched
 
     def f_run():
         state["epoch"] = state["epoch"] % ((1 << 25) - 1) + 1
@@ -506,6 +600,13 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
         ev = torch.cuda.Event()
         ev.record()
         slot[1] = ev
+        if qk is not None:
+            qk["pend"].copy_(qk["pend0"])
+            qk["qctl"].copy_(qk["qctl0"])
+            qk["qslot"].copy_(qk["qslot0"])
+            qk["done"].zero_()
+            _lib.check(lib.dpl_dtr_potrf_q(args_d.data_ptr(), nwg, _lib.stream_ptr()), "dtr_potrf_q")
+            return
         cnt.zero_()
         cur.zero_()
         scur.zero_()

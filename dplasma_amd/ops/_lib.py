@@ -25,6 +25,7 @@ c_int, c_ll, c_ull, c_vp = ctypes.c_int, ctypes.c_longlong, ctypes.c_ulonglong, 
 _SIGS = {
     # device task runtime (dtr.hip): DtrArgs image in device memory, workgroups, stream
     "dpl_dtr_potrf": [c_vp, c_int, c_vp],
+    "dpl_dtr_potrf_q": [c_vp, c_int, c_vp],
     "dpl_dtr_args_size": [],
     "dpl_dtr_field": [ctypes.c_char_p],
     # prec, transA, transB, nitems, items, kpairs, max_m, max_n, alpha*, A, lda, B, ldb, beta*, C, ldc, vec_ok, generic, stream

@@ -187,6 +187,85 @@ def test_dtr_plan_numerics(nt, defer, min_tiles, lo_order):
     assert np.abs(L - np.linalg.cholesky(S)).max() < 1e-10
 
 
+def _emulate_q(plan, A, nb, P=8, seed=0):
+    """The push protocol of k_dtr_q (potrf_dtr.queue_plan): a completed task decrements its successors' pending
+    counts and pushes the ones it brings to zero into their class's ring; P workers pop the lowest class (FIFO
+    inside a class); completions in random order; numpy math on A as _emulate does."""
+    q = D.queue_plan(plan)
+    rng = np.random.default_rng(seed)
+    tasks = plan.tasks
+    s = nb // 4
+    pend = q["ndeps"].astype(np.int64).copy()
+    rings = [[] for _ in range(D.NCLASS)]
+    for t in np.nonzero(pend == 0)[0]:
+        rings[q["cls"][t]].append(int(t))
+    W = {}
+
+    def blk(i, j, r, c):
+        return A[i * nb + r * s: i * nb + (r + 1) * s, j * nb + c * s: j * nb + (c + 1) * s]
+
+    def start(t):
+        ty, i, j, k0, r, c, nk = (int(tasks[t][f]) for f in ("type", "i", "j", "k0", "r", "c", "nk"))
+        if ty == T_UPD:
+            acc = blk(i, j, r, c).copy()
+            for k in range(k0, k0 + nk):
+                acc -= A[i * nb + r * s: i * nb + (r + 1) * s, k * nb:(k + 1) * nb] @ \
+                    A[j * nb + c * s: j * nb + (c + 1) * s, k * nb:(k + 1) * nb].T
+            return acc
+        if ty == T_TRSM:
+            return A[i * nb + r * s: i * nb + (r + 1) * s, k0 * nb:(k0 + 1) * nb] @ W[k0]
+        if ty == T_POTRF and r == 0:
+            return np.linalg.cholesky(A[k0 * nb:(k0 + 1) * nb, k0 * nb:(k0 + 1) * nb])
+        return None
+
+    def finish(t, val):
+        ty, i, j, k0, r, c = (int(tasks[t][f]) for f in ("type", "i", "j", "k0", "r", "c"))
+        if val is not None:
+            if ty == T_UPD:
+                if i == j and r == c:
+                    val = np.tril(val) + np.triu(blk(i, j, r, c), 1)
+                blk(i, j, r, c)[:] = val
+            elif ty == T_TRSM:
+                A[i * nb + r * s: i * nb + (r + 1) * s, k0 * nb:(k0 + 1) * nb] = val
+            else:
+                A[k0 * nb:(k0 + 1) * nb, k0 * nb:(k0 + 1) * nb] = np.tril(val)
+                W[k0] = np.linalg.inv(val).T
+        for x in q["succ"][q["succ_off"][t]:q["succ_off"][t + 1]]:
+            pend[x] -= 1
+            if pend[x] == 0:
+                rings[q["cls"][x]].append(int(x))
+    inflight, done = [], 0
+    while done < len(tasks):
+        while len(inflight) < P:
+            ring = next((r_ for r_ in rings if r_), None)
+            if ring is None:
+                break
+            t = ring.pop(0)
+            inflight.append((t, start(t)))
+        assert inflight, "push protocol stalled"
+        t, v = inflight.pop(int(rng.integers(len(inflight))))
+        finish(t, v)
+        done += 1
+    assert (pend == 0).all()
+
+
+@pytest.mark.parametrize("lo_order", ["column", "step"])
+@pytest.mark.parametrize("nt,defer,min_tiles", [(5, 2, 0), (7, 4, 0), (11, 4, 6)])
+def test_dtr_queue_plan_numerics(nt, defer, min_tiles, lo_order):
+    """Push scheduling: the requirement lists turned into task edges give the Cholesky factor for random
+    completion orders, and every task is pushed exactly once."""
+    nb = 16
+    n = nt * nb
+    rng = np.random.default_rng(7)
+    M = rng.standard_normal((n, n))
+    S = M @ M.T + n * np.eye(n)
+    for seed in range(3):
+        A = S.copy()
+        plan = D._Plan(nt, defer, lo_order, min_tiles)
+        _emulate_q(plan, A, nb, P=(8, 24, 64)[seed], seed=seed)
+        assert np.abs(np.tril(A) - np.linalg.cholesky(S)).max() < 1e-10
+
+
 # ------------------------------------------------------------------------------- distributed DTR
 def _emulate_dist(dplan, xcds_of, A=None, nb=None, wpx=2, seed=0):
     """The claim protocol of every rank of a P x Q grid (models/potrf_dtr_dist.py), with wpx workers per
