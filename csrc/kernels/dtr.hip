@@ -111,16 +111,17 @@ struct DtrArgs {
   int* info;
   long long* trace;         // optional (DPLASMA_DTR_TRACE): per task {start, end, wg << 8 | xcd, visible}, 100 MHz ticks
   // ---- push scheduling (k_dtr_q): per-task pending-predecessor counts, successor lists, ready rings
-  int ntask;
+  int ntask;                // tasks this launch runs (this rank's)
   int nclass;               // priority classes (ring r = class * 8 + XCD; lower class first)
-  int* pend;                // per task: predecessors not yet complete (reset per launch)
-  const int* succ_off;      // ntask + 1
-  const int* succ;          // successor task ids
-  const int* ring_of;       // per task: the ready ring it is pushed to
-  const int* qbase;         // nclass * 8 + 1 slot offsets
-  int* qctl;                // per ring: head at [2 r PSTRIDE], tail at [(2 r + 1) PSTRIDE] (reset per launch)
-  int* qslot;               // ring slots: task id + 1, 0 = reserved but not yet written (reset per launch)
-  int* done;                // completed tasks
+  int* pend[MAXR];          // rank r's per-task (global ids) predecessors not yet complete (reset per launch)
+  const int* succ_off;      // global task ids: successors [succ_off[t], succ_off[t + 1])
+  const int* succ;
+  const int* ring_of;       // per task: the ready ring it is pushed to (on its owner)
+  const int* town;          // per task: owner rank (null: one rank)
+  const int* qbase;         // per rank nclass * 8 + 1 slot offsets
+  int* qctl[MAXR];          // rank r's rings: head at [2 q PSTRIDE], tail at [(2 q + 1) PSTRIDE] (reset per launch)
+  int* qslot[MAXR];         // rank r's ring slots: task id + 1, 0 = reserved but not yet written (reset per launch)
+  int* done;                // tasks completed by this launch
 };
 
 constexpr int NBT = 512;    // tile size
@@ -709,27 +710,42 @@ __global__ __launch_bounds__(256, 2) void k_dtr_potrf(const DtrArgs* __restrict_
 // A push reserves a slot (tail atomic) and then stores the id (sc1): a popper that finds the reserved slot still
 // 0 treats the ring as empty for now.  Completion order: release (every wave's stores drained, agent release)
 // before the decrements, so a pushed task's inputs are visible to the popper's acquire.
-__device__ inline int q_pop(const DtrArgs& g, int r) {
-  int* head = g.qctl + (size_t)(2 * r) * PSTRIDE;
+template <typename T> __device__ inline T ld_q(const T* p, bool sy) { return sy ? ld_sys(p) : ld_sc1(p); }
+
+__device__ inline int q_pop(const DtrArgs& g, int r, int rk, bool sy) {
+  int* head = g.qctl[rk] + (size_t)(2 * r) * PSTRIDE;
   int* tail = head + PSTRIDE;
+  const int* qb = g.qbase + (size_t)rk * (g.nclass * 8 + 1);
   for (int tries = 0; tries < 2; ++tries) {
-    const int h = __builtin_amdgcn_readfirstlane(ld_sc1(head));
-    const int tl = __builtin_amdgcn_readfirstlane(ld_sc1(tail));
+    const int h = __builtin_amdgcn_readfirstlane(ld_q(head, sy));
+    const int tl = __builtin_amdgcn_readfirstlane(ld_q(tail, sy));
     if (h >= tl) return -1;
-    const int s = __builtin_amdgcn_readfirstlane(ld_sc1(g.qslot + g.qbase[r] + h));
+    const int s = __builtin_amdgcn_readfirstlane(ld_q(g.qslot[rk] + qb[r] + h, sy));
     if (s == 0) return -1;
     int won = 0;
-    if ((threadIdx.x & 63) == 0) won = atomicCAS(head, h, h + 1) == h;
+    if ((threadIdx.x & 63) == 0) {
+      int e = h;
+      won = sy ? __hip_atomic_compare_exchange_strong(head, &e, h + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_SYSTEM)
+               : atomicCAS(head, h, h + 1) == h;
+    }
     if (__builtin_amdgcn_readfirstlane(won)) return s - 1;
   }
   return -1;
 }
 
-__device__ inline void q_push(const DtrArgs& g, int t) {   // one lane
+// push task t into its ring on rank d (one lane); process mode: the peer's rings through its IPC mapping
+__device__ inline void q_push(const DtrArgs& g, int t, int d, bool sy) {
   const int r = g.ring_of[t];
-  int* tail = g.qctl + (size_t)(2 * r + 1) * PSTRIDE;
-  const int pos = atomicAdd(tail, 1);
-  st_sc1(g.qslot + g.qbase[r] + pos, t + 1);
+  int* tail = g.qctl[d] + (size_t)(2 * r + 1) * PSTRIDE;
+  const int* qb = g.qbase + (size_t)d * (g.nclass * 8 + 1);
+  if (sy) {
+    const int pos = __hip_atomic_fetch_add(tail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(g.qslot[d] + qb[r] + pos, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+    const int pos = atomicAdd(tail, 1);
+    st_sc1(g.qslot[d] + qb[r] + pos, t + 1);
+  }
 }
 
 __global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ gargs) {
@@ -738,6 +754,14 @@ __global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ ga
   const int xcd = xcc_id();
   unsigned long long idle0 = 0;
   int nap = 1;
+  int rk;
+  bool sy;
+  {
+    const DtrArgs* gp = gargs;
+    asm volatile("" : "+s"(gp));
+    sy = sysmode(*gp);
+    rk = sy ? gp->rank : 0;
+  }
   for (;;) {
     const DtrArgs* gp = gargs;
     asm volatile("" : "+s"(gp));
@@ -759,8 +783,8 @@ __global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ ga
             int r = 0;
             if (pos < nr) {
               r = (pos & ~7) + ((xcd + pos) & 7);
-              const int* hd = g.qctl + (size_t)(2 * r) * PSTRIDE;
-              ne = ld_sc1(hd) < ld_sc1(hd + PSTRIDE);
+              const int* hd = g.qctl[rk] + (size_t)(2 * r) * PSTRIDE;
+              ne = ld_q(hd, sy) < ld_q(hd + PSTRIDE, sy);
             }
             const unsigned long long bal = __builtin_amdgcn_ballot_w64(ne);
             if (bal) {
@@ -769,12 +793,15 @@ __global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ ga
             }
           }
           if (best < 0) break;
-          t = q_pop(g, best);
+          t = q_pop(g, best, rk, sy);
         }
         if (t < 0 && __builtin_amdgcn_readfirstlane(ld_sc1(g.done)) >= g.ntask) t = -2;
       }
       if (t >= 0) {
-        if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (tid == 0) {
+          if (sy) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // a peer's strips / W may be among the inputs
+          else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         idle0 = 0;
       } else if (t == -1 && tid == 0) {
@@ -799,9 +826,11 @@ __global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ ga
     nap = 1;
     const unsigned long long t_start = now_t();
     const DtrTask tk = g.tasks[t];
-    if (tk.type == T_UPD) run_upd(gp, t, 0);
-    else if (tk.type == T_TRSM) run_trsm(gp, t, 0);
-    else run_potrf(gp, t, 0);
+    if (tk.type == T_UPD) run_upd(gp, t, rk);
+    else if (tk.type == T_TRSM) run_trsm(gp, t, rk);
+    else if (tk.type == T_POTRF) run_potrf(gp, t, rk);
+    else if (tk.type == T_SEND) run_send(gp, t, rk);
+    else run_sendw(gp, t, rk);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0 && g.trace) {
@@ -812,12 +841,16 @@ __global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ ga
       atomicAdd((unsigned long long*)(tr + 3), 1ULL);
     }
     if (tid < 64) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      if (sy) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int sb = g.succ_off[t], se = g.succ_off[t + 1];
       for (int q = sb + tid; q < se; q += 64) {
         const int sx = g.succ[q];
-        if (atomicSub(g.pend + sx, 1) == 1) q_push(g, sx);
+        const int d = g.town ? g.town[sx] : 0;
+        const int left = sy ? __hip_atomic_fetch_sub(g.pend[d] + sx, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                            : atomicSub(g.pend[d] + sx, 1);
+        if (left == 1) q_push(g, sx, d, sy);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (tid == 0) atomicAdd(g.done, 1);
@@ -855,8 +888,8 @@ DPL_API long long dpl_dtr_field(const char* name) {
   DTR_FIELD(hi_off) DTR_FIELD(nsteps) DTR_FIELD(hs_off) DTR_FIELD(scur) DTR_FIELD(lo) DTR_FIELD(lo_off) DTR_FIELD(A) DTR_FIELD(recv) DTR_FIELD(W) DTR_FIELD(cnt)
   DTR_FIELD(vis) DTR_FIELD(link) DTR_FIELD(bw_bpt) DTR_FIELD(lat_t) DTR_FIELD(Mw) DTR_FIELD(Sw) DTR_FIELD(Lp)
   DTR_FIELD(Wp) DTR_FIELD(prog) DTR_FIELD(info) DTR_FIELD(trace) DTR_FIELD(ntask) DTR_FIELD(nclass) DTR_FIELD(pend)
-  DTR_FIELD(succ_off) DTR_FIELD(succ) DTR_FIELD(ring_of) DTR_FIELD(qbase) DTR_FIELD(qctl) DTR_FIELD(qslot)
-  DTR_FIELD(done)
+  DTR_FIELD(succ_off) DTR_FIELD(succ) DTR_FIELD(ring_of) DTR_FIELD(town) DTR_FIELD(qbase) DTR_FIELD(qctl)
+  DTR_FIELD(qslot) DTR_FIELD(done)
   if (!std::strcmp(name, "size")) return (long long)sizeof(DtrArgs);
   if (!std::strcmp(name, "task")) return (long long)sizeof(DtrTask);
   if (!std::strcmp(name, "MAXB")) return MAXB;

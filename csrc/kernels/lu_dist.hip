@@ -324,6 +324,13 @@ DPL_API int dpl_ipc_alloc(long long bytes, int cached, void** ptr, void* handle)
 }
 
 // clear device memory and return once the zeros have landed (value: the byte)
+// device-to-device copy, completed on return (used on IPC-mapped buffers before a cross-process barrier)
+DPL_API int dpl_memcpy_sync(void* dst, const void* src, long long bytes) {
+  if (bytes <= 0) return 0;
+  if (hipMemcpy(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice) != hipSuccess) return -1;
+  return (int)hipDeviceSynchronize();
+}
+
 DPL_API int dpl_memset_sync(void* ptr, int value, long long bytes) {
   if (value != 0) return -2;
   return (int)dpl_zero_sync(ptr, (size_t)bytes);

@@ -310,40 +310,45 @@ UPD_BUCKETS = 22
 NCLASS = 2 + UPD_BUCKETS
 
 
-def queue_plan(plan):
-    """Push scheduling (k_dtr_q) of a _Plan: the requirement lists turned into task edges, and the ready rings.
+def queue_edges(tasks, reqs, WB, owner=None, inc_rank=None):
+    """Task edges of a requirement-list plan (push scheduling, k_dtr_q).
 
-    Requirement (c, v) on a sub-tile version / strip marker counter (c < WB) names the task that made its v-th
-    increment -- those counters are bumped in emission order, each bump depending on the previous one -- and a
-    W_k requirement (c = WB + k, all 16 blocks) names POTRF(k)'s 16 block tasks.  Returns a dict of int32 arrays:
-    ndeps, succ_off, succ, ring_of, qbase, qinit (the initially ready tasks' slots) and tinit (initial tails)."""
-    tasks, reqs, WB = plan.tasks, plan.reqs, plan.WB
+    Counters live per rank: task t's requirement (c, v) is on rank owner[t]'s counter c; its increment (inc) lands
+    on rank inc_rank[t] (its destination for a send).  A requirement on a sub-tile version / strip marker counter
+    (c < WB, bumped in emission order, each bump depending on the previous one; a remote strip's arrival counter
+    has its single send) names the task of its v-th increment; a W counter (c >= WB: the 16 POTRF blocks of panel
+    k, or W_k's 4 arriving column blocks) names all of them.  Returns (ndeps, succ_off, succ)."""
     n = len(tasks)
+    owner = np.zeros(n, dtype=np.int64) if owner is None else np.asarray(owner, dtype=np.int64)
+    inc_rank = owner if inc_rank is None else np.asarray(inc_rank, dtype=np.int64)
     inc = tasks["inc"].astype(np.int64)
-    # the increments of every counter in emission order: sorted (counter, task id)
+    ncnt = int(max(inc.max(initial=0), int(reqs[:, 0].max()) if len(reqs) else 0)) + 1
+    # the increments of every (rank, counter) in emission order
     has = np.nonzero(inc >= 0)[0]
-    srt = has[np.lexsort((has, inc[has]))]
-    sc = inc[srt]
-    ncnt = int(max(inc.max(), int(reqs[:, 0].max()) if len(reqs) else 0)) + 1
-    cstart = np.searchsorted(sc, np.arange(ncnt + 1))
+    key = inc_rank[has] * ncnt + inc[has]
+    srt = has[np.lexsort((has, key))]
+    skey = inc_rank[srt] * ncnt + inc[srt]
+    nkey = (int(max(owner.max(initial=0), inc_rank.max(initial=0))) + 1) * ncnt
+    cstart = np.searchsorted(skey, np.arange(nkey + 1))
     ccount = np.diff(cstart)
-    # requirement records: consumer, counter, value
+    # requirement records: consumer, (rank, counter), value
     nr = tasks["nreq"].astype(np.int64)
     rt = np.repeat(np.arange(n, dtype=np.int64), nr)
     rb = np.repeat(tasks["req_beg"].astype(np.int64), nr) + (np.arange(int(nr.sum())) - np.repeat(np.cumsum(nr) - nr, nr))
     rc, rv = reqs[rb, 0].astype(np.int64), reqs[rb, 1].astype(np.int64)
     keep = rv > 0
     rt, rc, rv = rt[keep], rc[keep], rv[keep]
-    if np.any(ccount[rc] < rv):
-        raise RuntimeError("queue_plan: a requirement names an increment that never happens")
+    rk = owner[rt] * ncnt + rc
+    if np.any(ccount[rk] < rv):
+        raise RuntimeError("queue_edges: a requirement names an increment that never happens")
     ver = rc < WB
     cons = [rt[ver]]
-    prod = [srt[cstart[rc[ver]] + rv[ver] - 1]]
-    w = ~ver                                           # W_k: every POTRF block of panel k
+    prod = [srt[cstart[rk[ver]] + rv[ver] - 1]]
+    w = ~ver
     if w.any():
-        m = ccount[rc[w]]
+        m = ccount[rk[w]]
         cons.append(np.repeat(rt[w], m))
-        prod.append(srt[np.repeat(cstart[rc[w]], m) + (np.arange(int(m.sum())) - np.repeat(np.cumsum(m) - m, m))])
+        prod.append(srt[np.repeat(cstart[rk[w]], m) + (np.arange(int(m.sum())) - np.repeat(np.cumsum(m) - m, m))])
     cons, prod = np.concatenate(cons), np.concatenate(prod)
     pair = np.unique(prod * n + cons)
     prod, cons = pair // n, pair % n
@@ -351,24 +356,43 @@ def queue_plan(plan):
     succ_off = np.zeros(n + 1, dtype=np.int32)
     succ_off[1:] = np.cumsum(np.bincount(prod, minlength=n))
     succ = cons.astype(np.int32) if len(cons) else np.zeros(1, dtype=np.int32)   # pairs sorted by producer
+    return ndeps, succ_off, succ
+
+
+def queue_classes(tasks, nt, is_hi=None):
+    """(class, XCD) of every task's ready ring: 0 POTRF blocks (spread over the eight XCDs: the 16 cooperate and
+    must start together), 1 panel TRSM strips and sends (by tile row), then updates by output column j -- the step
+    that needs them -- in at most UPD_BUCKETS buckets (by output column: the low lists' L2 locality)."""
     typ = tasks["type"]
-    nbk = max(1, min(plan.nt, UPD_BUCKETS))
-    ucls = 2 + np.minimum(nbk - 1, tasks["j"].astype(np.int64) * nbk // max(1, plan.nt))
-    cls = np.where(typ == T_POTRF, 0, np.where(typ == T_TRSM, 1, ucls))
-    # XCD of the ring: the POTRF blocks spread over all eight (the 16 cooperate and must start together), TRSM by
-    # tile row, updates by output column (the low lists' L2 locality)
-    xcd = np.where(typ == T_POTRF, tasks["r"] % 8, np.where(typ == T_TRSM, tasks["i"] % 8, tasks["j"] % 8))
-    ring_of = (cls * 8 + xcd).astype(np.int32)
+    nbk = max(1, min(nt, UPD_BUCKETS))
+    ucls = 2 + np.minimum(nbk - 1, tasks["j"].astype(np.int64) * nbk // max(1, nt))
+    cls = np.where(typ == T_POTRF, 0, np.where(typ == T_UPD, ucls, 1))
+    xcd = np.where(typ == T_POTRF, tasks["r"] % 8, np.where(typ == T_UPD, tasks["j"] % 8, tasks["i"] % 8))
+    return cls.astype(np.int64), xcd.astype(np.int64)
+
+
+def queue_rings(ring_of, mine, ndeps):
+    """One rank's rings: slot offsets per ring (its tasks only) and the initially ready tasks' slots / tails."""
     nring = NCLASS * 8
-    cap = np.bincount(ring_of, minlength=nring)
+    cap = np.bincount(ring_of[mine], minlength=nring)
     qbase = np.zeros(nring + 1, dtype=np.int32)
     qbase[1:] = np.cumsum(cap)
-    qinit = np.zeros(max(1, n), dtype=np.int32)
+    qinit = np.zeros(max(1, int(qbase[-1])), dtype=np.int32)
     tinit = np.zeros(nring, dtype=np.int32)
-    for t in np.nonzero(ndeps == 0)[0]:
+    for t in np.nonzero(mine & (ndeps == 0))[0]:
         r = ring_of[t]
         qinit[qbase[r] + tinit[r]] = t + 1
         tinit[r] += 1
+    return qbase, qinit, tinit
+
+
+def queue_plan(plan):
+    """Push scheduling (k_dtr_q) of a one-process _Plan: queue_edges + one rank's rings.  Returns a dict of arrays:
+    ndeps, succ_off, succ, ring_of, qbase, qinit (the initially ready tasks' slots), tinit (initial tails), cls."""
+    ndeps, succ_off, succ = queue_edges(plan.tasks, plan.reqs, plan.WB)
+    cls, xcd = queue_classes(plan.tasks, plan.nt)
+    ring_of = (cls * 8 + xcd).astype(np.int32)
+    qbase, qinit, tinit = queue_rings(ring_of, np.ones(len(plan.tasks), dtype=bool), ndeps)
     return {"ndeps": ndeps, "succ_off": succ_off, "succ": succ, "ring_of": ring_of, "qbase": qbase,
             "qinit": qinit, "tinit": tinit, "cls": cls}
 
@@ -380,8 +404,8 @@ class ArgsImage:
     _LL = ("ld", "ncnt", "bw_bpt", "lat_t")
     _INT = ("nt", "nranks", "rank", "epoch", "flags", "dil", "nsteps", "ntask", "nclass")
     _PTR = ("tasks", "reqs", "tab", "xoff", "cur", "hs_off", "scur", "hi", "lo", "vis", "link", "Mw", "Sw", "Lp", "Wp",
-            "prog", "info", "trace", "pend", "succ_off", "succ", "ring_of", "qbase", "qctl", "qslot", "done")
-    _PARR = ("A", "recv", "W", "cnt")
+            "prog", "info", "trace", "succ_off", "succ", "ring_of", "town", "qbase", "done")
+    _PARR = ("A", "recv", "W", "cnt", "pend", "qctl", "qslot")
     _IARR = ("hi_off", "lo_off")
 
     def __init__(self, lib):
@@ -581,8 +605,10 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
               "done": torch.zeros(1, dtype=torch.int32, device=dev)}
         img.set("ntask", len(plan.tasks))
         img.set("nclass", NCLASS)
-        for f in ("pend", "succ_off", "succ", "ring_of", "qbase", "qctl", "qslot", "done"):
+        for f in ("succ_off", "succ", "ring_of", "qbase", "done"):
             img.set(f, qk[f].data_ptr())
+        for f in ("pend", "qctl", "qslot"):
+            img.set(f, [qk[f].data_ptr()])
     tp._keep = (tasks_d, reqs_d, hi_d, lo_d, tab_d, cnt, cur, hs_d, scur, W, scr, hosts, args_d, qk)
     tp.dtr_plan = plan
     tp.dtr_sched = sched

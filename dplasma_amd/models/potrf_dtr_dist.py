@@ -147,6 +147,31 @@ class DistPlan:
             tw = self.tasks[ntask0 + ns:]
             self.xoff[ntask0 + ns:] = tw["k0"].astype(np.int64) * NBT * NBT + tw["r"].astype(np.int64) * 128 * NBT
 
+    def queue(self):
+        """Push scheduling over the grid (k_dtr_q in process mode): global task edges -- a send's successors live
+        on its destination rank, whose pending counts and rings it updates through the IPC mapping -- and every
+        rank's rings (cached)."""
+        q = getattr(self, "_queue", None)
+        if q is not None:
+            return q
+        typ = self.tasks["type"]
+        inc_rank = np.where((typ == T_SEND) | (typ == T_SENDW), self.tasks["j"].astype(np.int64), self.owner)
+        ndeps, succ_off, succ = D.queue_edges(self.tasks, self.reqs, self.WB, self.owner, inc_rank)
+        cls, xcd = D.queue_classes(self.tasks, self.nt)
+        ring_of = (cls * 8 + xcd).astype(np.int32)
+        qbase, qinit, tinit, nown = [], [], [], []
+        for r in range(self.nranks):
+            mine = self.owner == r
+            b, qi, ti = D.queue_rings(ring_of, mine, ndeps)
+            qbase.append(b)
+            qinit.append(qi)
+            tinit.append(ti)
+            nown.append(int(mine.sum()))
+        self._queue = q = {"ndeps": ndeps, "succ_off": succ_off, "succ": succ, "ring_of": ring_of, "cls": cls,
+                           "town": self.owner.astype(np.int32), "qbase": np.concatenate(qbase), "qinit": qinit,
+                           "tinit": tinit, "nown": nown}
+        return q
+
     def _owner(self, i, j):
         return (np.asarray(i) % self.P) * self.Q + (np.asarray(j) % self.Q)
 
@@ -465,8 +490,15 @@ def potrf_dtr_dist_New(ctx, uplo: int, A, info_out=None):
     PST = img.pstride
     dev = A.device
     hi, hi_off, lo, lo_off = plan.lists({me: list(range(8))})
-    peers = _Peers(ctx, [(plan.recv_elems(me) * 8, True), (nt * NBT * NBT * 8, True), (plan.ncnt * 4, False)])
-    recv_p, W_p, cnt_p = peers.ptrs
+    sched = os.environ.get("DPLASMA_DTR_SCHED", "queue")
+    specs = [(plan.recv_elems(me) * 8, True), (nt * NBT * NBT * 8, True), (plan.ncnt * 4, False)]
+    qp = None
+    if sched == "queue":
+        qp = plan.queue()
+        nring = D.NCLASS * 8
+        specs += [(len(plan.tasks) * 4, False), (2 * nring * PST * 4, False), (len(qp["qinit"][me]) * 4, False)]
+    peers = _Peers(ctx, specs)
+    recv_p, W_p, cnt_p = peers.ptrs[:3]
 
     def up(x):
         return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
@@ -502,6 +534,22 @@ def potrf_dtr_dist_New(ctx, uplo: int, A, info_out=None):
     scr.fill(img)
     img.set("info", info.data_ptr())
     img.set("flags", D.flags_from_env())
+    qk = None
+    if qp is not None:
+        pend_p, qctl_p, qslot_p = peers.ptrs[3:6]
+        qctl0 = torch.zeros(2 * nring * PST, dtype=torch.int32)
+        qctl0.view(nring, 2, PST)[:, 1, 0] = torch.from_numpy(qp["tinit"][me])
+        qk = {"pend0": up(qp["ndeps"]), "qctl0": qctl0.to(dev), "qslot0": up(qp["qinit"][me]),
+              "succ_off": up(qp["succ_off"]), "succ": up(qp["succ"]), "ring_of": up(qp["ring_of"]),
+              "town": up(qp["town"]), "qbase": up(qp["qbase"]), "done": torch.zeros(1, dtype=torch.int32, device=dev)}
+        img.set("ntask", qp["nown"][me])
+        img.set("nclass", D.NCLASS)
+        for f in ("succ_off", "succ", "ring_of", "town", "qbase", "done"):
+            img.set(f, qk[f].data_ptr())
+        img.set("pend", pend_p)
+        img.set("qctl", qctl_p)
+        img.set("qslot", qslot_p)
+        keep["q"] = qk
     args_d = torch.empty(img.size, dtype=torch.uint8, device=dev)
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     nwg = int(os.environ.get("DPLASMA_DTR_WG", ncu))   # one per CU (see models/potrf_dtr.py)
@@ -522,8 +570,17 @@ def potrf_dtr_dist_New(ctx, uplo: int, A, info_out=None):
         scur.zero_()
         torch.cuda.current_stream().synchronize()
         _lib.check(lib.dpl_memset_sync(cnt_p[me], 0, plan.ncnt * 4), "dtr counters")
+        if qk is not None:
+            # this rank's pending counts and rings from their templates (peers push into them after the barrier)
+            for dst, src in ((pend_p[me], qk["pend0"]), (qctl_p[me], qk["qctl0"]), (qslot_p[me], qk["qslot0"])):
+                _lib.check(lib.dpl_memcpy_sync(dst, src.data_ptr(), src.numel() * 4), "dtr queue reset")
+            qk["done"].zero_()
+            torch.cuda.current_stream().synchronize()
         # every rank's counters are cleared before any rank's kernel can send into them
         comm.barrier_world()
+        if qk is not None:
+            _lib.check(lib.dpl_dtr_potrf_q(args_d.data_ptr(), nwg, _lib.stream_ptr()), "dtr_potrf_q (distributed)")
+            return
         _lib.check(lib.dpl_dtr_potrf(args_d.data_ptr(), nwg, _lib.stream_ptr()), "dtr_potrf (distributed)")
 
     tp.task("DTR_POTRF", "update", f_run)

@@ -119,6 +119,7 @@ _SIGS = {
     "dpl_xchg_alloc": [c_ll, c_vp, c_vp],
     "dpl_ipc_alloc": [c_ll, c_int, c_vp, c_vp],
     "dpl_memset_sync": [c_vp, c_int, c_ll],
+    "dpl_memcpy_sync": [c_vp, c_vp, c_ll],
     "dpl_xchg_open": [c_vp, c_vp],
     "dpl_xchg_close": [c_vp],
     "dpl_xchg_free": [c_vp],

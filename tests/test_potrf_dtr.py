@@ -187,17 +187,17 @@ def test_dtr_plan_numerics(nt, defer, min_tiles, lo_order):
     assert np.abs(L - np.linalg.cholesky(S)).max() < 1e-10
 
 
-def _emulate_q(plan, A, nb, P=8, seed=0):
+def _emulate_q(plan, A, nb, P=8, seed=0, q=None):
     """The push protocol of k_dtr_q (potrf_dtr.queue_plan): a completed task decrements its successors' pending
     counts and pushes the ones it brings to zero into their class's ring; P workers pop the lowest class (FIFO
     inside a class); completions in random order; numpy math on A as _emulate does."""
-    q = D.queue_plan(plan)
+    q = q or D.queue_plan(plan)
     rng = np.random.default_rng(seed)
     tasks = plan.tasks
     s = nb // 4
     pend = q["ndeps"].astype(np.int64).copy()
     rings = [[] for _ in range(D.NCLASS)]
-    for t in np.nonzero(pend == 0)[0]:
+    for t in np.nonzero(pend == 0)[0]:   # (the sends of a grid plan are no-ops here: one global matrix)
         rings[q["cls"][t]].append(int(t))
     W = {}
 
@@ -247,6 +247,29 @@ def _emulate_q(plan, A, nb, P=8, seed=0):
         finish(t, v)
         done += 1
     assert (pend == 0).all()
+
+
+@pytest.mark.parametrize("grid", [(1, 2), (2, 2), (2, 4)])
+@pytest.mark.parametrize("nt", [6, 9])
+def test_dtr_dist_queue_numerics(grid, nt):
+    """Push scheduling over a grid (DistPlan.queue): the cross-rank edges (send -> remote consumers) order every
+    task after its inputs -- random completion orders over all ranks' tasks give the factor -- and every rank's
+    rings hold exactly its tasks."""
+    nb = 16
+    n = nt * nb
+    rng = np.random.default_rng(5)
+    M = rng.standard_normal((n, n))
+    S = M @ M.T + n * np.eye(n)
+    dplan = DD.DistPlan(nt, 4, *grid)
+    q = dplan.queue()
+    nring = D.NCLASS * 8
+    for r in range(dplan.nranks):
+        b = q["qbase"][r * (nring + 1):(r + 1) * (nring + 1)]
+        assert b[-1] == q["nown"][r] == int((dplan.owner == r).sum())
+    for seed in range(2):
+        A = S.copy()
+        _emulate_q(dplan, A, nb, P=(16, 48)[seed], seed=seed, q=q)
+        assert np.abs(np.tril(A) - np.linalg.cholesky(S)).max() < 1e-10
 
 
 @pytest.mark.parametrize("lo_order", ["column", "step"])
