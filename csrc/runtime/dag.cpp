@@ -102,9 +102,51 @@ py::array_t<int64_t> dag_list_schedule(I64 pred_ptr, I64 pred_idx, py::array_t<i
   return out;
 }
 
+// Bottom level (longest weighted path to a sink, the task's own weight included) of a DAG given by successor
+// lists (CSR): Kahn's order, then one backward pass.  The device task runtime's push scheduler ranks its ready
+// rings by it (models/potrf_dtr.py queue_classes).
+py::array_t<double> dag_bottom_level(py::array_t<int32_t, py::array::c_style | py::array::forcecast> succ_off,
+                                     py::array_t<int32_t, py::array::c_style | py::array::forcecast> succ,
+                                     py::array_t<double, py::array::c_style | py::array::forcecast> w) {
+  const int64_t n = w.shape(0);
+  if (succ_off.ndim() != 1 || succ_off.shape(0) != n + 1)
+    throw std::invalid_argument("dag_bottom_level: succ_off must have n + 1 entries");
+  const int32_t* so = succ_off.data();
+  const int32_t* sc = succ.data();
+  const double* wt = w.data();
+  for (int64_t e = 0; e < so[n]; ++e)
+    if (sc[e] < 0 || sc[e] >= n) throw std::invalid_argument("dag_bottom_level: successor out of range");
+  py::array_t<double> out(n);
+  double* bl = out.mutable_data();
+  bool cyc = false;
+  {
+    py::gil_scoped_release rel;
+    std::vector<int32_t> indeg(n, 0), order;
+    order.reserve(n);
+    for (int64_t e = 0; e < so[n]; ++e) ++indeg[sc[e]];
+    for (int64_t t = 0; t < n; ++t)
+      if (!indeg[t]) order.push_back((int32_t)t);
+    for (size_t h = 0; h < order.size(); ++h)
+      for (int32_t e = so[order[h]]; e < so[order[h] + 1]; ++e)
+        if (--indeg[sc[e]] == 0) order.push_back(sc[e]);
+    cyc = (int64_t)order.size() != n;
+    if (!cyc)
+      for (int64_t h = n - 1; h >= 0; --h) {
+        const int32_t t = order[h];
+        double m = 0;
+        for (int32_t e = so[t]; e < so[t + 1]; ++e) m = std::max(m, bl[sc[e]]);
+        bl[t] = wt[t] + m;
+      }
+  }
+  if (cyc) throw std::invalid_argument("dag_bottom_level: the graph has a cycle");
+  return out;
+}
+
 }  // namespace
 
 void register_dag(py::module_& m) {
+  m.def("dag_bottom_level", &dag_bottom_level, py::arg("succ_off"), py::arg("succ"), py::arg("w"),
+        "Longest weighted path from each task to a sink (its own weight included)");
   m.def("dag_list_schedule", &dag_list_schedule, py::arg("pred_ptr"), py::arg("pred_idx"), py::arg("prio"),
         py::arg("policy"), py::arg("seed") = 0,
         "Issue order of a task graph under a ready-queue policy (0 program, 1 priority, 2 inverse "

@@ -359,14 +359,43 @@ def queue_edges(tasks, reqs, WB, owner=None, inc_rank=None):
     return ndeps, succ_off, succ
 
 
-def queue_classes(tasks, nt, is_hi=None):
-    """(class, XCD) of every task's ready ring: 0 POTRF blocks (spread over the eight XCDs: the 16 cooperate and
-    must start together), 1 panel TRSM strips and sends (by tile row), then updates by output column j -- the step
-    that needs them -- in at most UPD_BUCKETS buckets (by output column: the low lists' L2 locality)."""
+# measured mean task durations at one workgroup per CU (us; profiles/r5_dtr_queue.txt): the weights of the
+# bottom-level priorities
+TASK_US = {"upd1": 75.0, "upd_k": 65.0, "trsm": 175.0, "potrf": 300.0, "send": 20.0}
+
+
+def task_weights(tasks):
     typ = tasks["type"]
-    nbk = max(1, min(nt, UPD_BUCKETS))
-    ucls = 2 + np.minimum(nbk - 1, tasks["j"].astype(np.int64) * nbk // max(1, nt))
-    cls = np.where(typ == T_POTRF, 0, np.where(typ == T_UPD, ucls, 1))
+    nk = tasks["nk"].astype(np.float64)
+    return np.where(typ == T_UPD, np.maximum(TASK_US["upd1"], TASK_US["upd_k"] * nk),
+                    np.where(typ == T_TRSM, TASK_US["trsm"], np.where(typ == T_POTRF, TASK_US["potrf"],
+                                                                      TASK_US["send"]))).astype(np.float64)
+
+
+def bottom_levels(succ_off, succ, w):
+    """Longest weighted path from every task to the end of the factorisation (native, runtime/dag.cpp)."""
+    from ..runtime.dag import _lib_rt
+    rt = _lib_rt()
+    if rt is None or not hasattr(rt, "dag_bottom_level"):
+        raise RuntimeError("dtr: the native runtime module (_dplasma_rt) with dag_bottom_level is needed")
+    return np.asarray(rt.dag_bottom_level(succ_off, succ, w))
+
+
+def queue_classes(tasks, nt, succ_off=None, succ=None):
+    """(class, XCD) of every task's ready ring.  Class 0: the POTRF blocks (spread over the eight XCDs: the 16
+    cooperate and must start together); then every other task by its bottom level -- the longest path of task
+    durations from it to the end, the list-scheduling priority of critical-path schedulers -- in UPD_BUCKETS + 1
+    buckets, longest first (a tile's chain of deferred updates and the panels behind it rank by what they still
+    hold up, not by their output column: ranking by column starved the last columns' update chains, r5_b32).
+    XCD: POTRF block % 8, TRSM / sends by tile row, updates by output column (the low lists' L2 locality)."""
+    typ = tasks["type"]
+    if succ_off is None:
+        cls = np.where(typ == T_POTRF, 0, np.where(typ == T_UPD, 2, 1))
+    else:
+        bl = bottom_levels(succ_off, succ, task_weights(tasks))
+        nb_ = NCLASS - 1
+        top = max(float(bl.max()), 1e-9)
+        cls = np.where(typ == T_POTRF, 0, 1 + np.minimum(nb_ - 1, ((1.0 - bl / top) * nb_).astype(np.int64)))
     xcd = np.where(typ == T_POTRF, tasks["r"] % 8, np.where(typ == T_UPD, tasks["j"] % 8, tasks["i"] % 8))
     return cls.astype(np.int64), xcd.astype(np.int64)
 
@@ -390,7 +419,7 @@ def queue_plan(plan):
     """Push scheduling (k_dtr_q) of a one-process _Plan: queue_edges + one rank's rings.  Returns a dict of arrays:
     ndeps, succ_off, succ, ring_of, qbase, qinit (the initially ready tasks' slots), tinit (initial tails), cls."""
     ndeps, succ_off, succ = queue_edges(plan.tasks, plan.reqs, plan.WB)
-    cls, xcd = queue_classes(plan.tasks, plan.nt)
+    cls, xcd = queue_classes(plan.tasks, plan.nt, succ_off, succ)
     ring_of = (cls * 8 + xcd).astype(np.int32)
     qbase, qinit, tinit = queue_rings(ring_of, np.ones(len(plan.tasks), dtype=bool), ndeps)
     return {"ndeps": ndeps, "succ_off": succ_off, "succ": succ, "ring_of": ring_of, "qbase": qbase,

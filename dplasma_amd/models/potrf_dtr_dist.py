@@ -157,7 +157,7 @@ class DistPlan:
         typ = self.tasks["type"]
         inc_rank = np.where((typ == T_SEND) | (typ == T_SENDW), self.tasks["j"].astype(np.int64), self.owner)
         ndeps, succ_off, succ = D.queue_edges(self.tasks, self.reqs, self.WB, self.owner, inc_rank)
-        cls, xcd = D.queue_classes(self.tasks, self.nt)
+        cls, xcd = D.queue_classes(self.tasks, self.nt, succ_off, succ)
         ring_of = (cls * 8 + xcd).astype(np.int32)
         qbase, qinit, tinit, nown = [], [], [], []
         for r in range(self.nranks):

@@ -28,4 +28,14 @@ timeout -k 10 300 python tools/gpu/dtr_trace_run.py 16384 $O/trace16k_q.npz > $O
 head -8 $O/trace16k.log | tee -a $O/summary.log
 timeout -k 10 300 python tools/emul_critical.py $O/trace16k_q.npz 1 30 > $O/crit16k.log 2>&1
 head -40 $O/crit16k.log | tee -a $O/summary.log
+echo "== dist rehearsal queue 2 ranks 1x2 16k" | tee -a $O/summary.log
+DPLASMA_DTR_SCHED=queue DPLASMA_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nproc-per-node 2 \
+  --master-addr 127.0.0.1 --master-port 29519 tools/gpu/dtr_dist_rehearsal.py 16384 1 3 > $O/reh12.log 2>&1
+echo "rc=$?" | tee -a $O/summary.log
+grep -E "run |DTR-DIST|Error|error" $O/reh12.log | head -8 | tee -a $O/summary.log
+echo "== dist rehearsal queue 4 ranks 2x2 16k" | tee -a $O/summary.log
+DPLASMA_DTR_SCHED=queue DPLASMA_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nproc-per-node 4 \
+  --master-addr 127.0.0.1 --master-port 29521 tools/gpu/dtr_dist_rehearsal.py 16384 2 3 > $O/reh22.log 2>&1
+echo "rc=$?" | tee -a $O/summary.log
+grep -E "run |DTR-DIST|Error|error" $O/reh22.log | head -8 | tee -a $O/summary.log
 exit 0
