@@ -69,13 +69,13 @@ POTRF_RESERVE = (0, 0)
 # operand).  Measured (profiles/r4_dtr_colorder.txt, r4_b16): 32k dtr 63-64 vs stream 61-62 TF/s; 64k dtr
 # 68.4-69.3 vs stream 69.4-70.1 (the stream engine's D = 2 deferred updates run the GEMMs at their
 # large-k rate, which the DTR's 128 x 128 x 512 update tasks do not reach); 16k dtr 38 vs 47.
-# Round 5: the DTR runs one workgroup per CU by default (two per CU gave an intermittent wrong factor under
-# stress, profiles/r5_dtr_coresidency.txt), which measures 16k 44.2 / 32k 60.3 / 64k 63.3 against the stream
-# engine's 46.0 / 59.5-61.2 / 67.0-69.2: no window left where it wins clearly, so "auto" selects nothing by
-# default (DPLASMA_POTRF_DTR_MIN_N / _MAX_N re-open one).
+# Round 5: the DTR runs one workgroup per CU (two per CU gave an intermittent wrong factor under stress,
+# profiles/r5_dtr_coresidency.txt) and push-schedules its tasks by bottom level (profiles/r5_dtr_queue.txt):
+# 16k 48.8 / 32k 62.0 / 64k 65.2 TF/s against the stream engine's 46.0 / 59.5-61.2 / 67.0-69.2 -> "auto" takes
+# the DTR below 48k.
 POTRF_ENGINE = "auto"
-POTRF_DTR_MIN_N = 1 << 62
-POTRF_DTR_MAX_N = 1 << 62
+POTRF_DTR_MIN_N = 12288
+POTRF_DTR_MAX_N = 49152
 
 
 def _defer_depth(nt_left: int, D: int, min_tiles: int) -> int:
