@@ -122,6 +122,7 @@ struct DtrArgs {
   int* qctl[MAXR];          // rank r's rings: head at [2 q PSTRIDE], tail at [(2 q + 1) PSTRIDE] (reset per launch)
   int* qslot[MAXR];         // rank r's ring slots: task id + 1, 0 = reserved but not yet written (reset per launch)
   int* done;                // tasks completed by this launch
+  unsigned long long* rdy;  // emulation: per task, when its last input becomes visible (max over predecessors)
 };
 
 constexpr int NBT = 512;    // tile size
@@ -754,13 +755,17 @@ __global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ ga
   const int xcd = xcc_id();
   unsigned long long idle0 = 0;
   int nap = 1;
-  int rk;
-  bool sy;
+  int rk, x0, nx;
+  bool sy, em;
   {
     const DtrArgs* gp = gargs;
     asm volatile("" : "+s"(gp));
     sy = sysmode(*gp);
-    rk = sy ? gp->rank : 0;
+    em = emul(*gp);
+    // emulation: XCD x runs rank x nr / 8 (its rings live on that rank's XCDs [x0, x0 + nx))
+    nx = em ? 8 / gp->nranks : 8;
+    rk = sy ? gp->rank : em ? xcd / nx : 0;
+    x0 = em ? rk * nx : 0;
   }
   for (;;) {
     const DtrArgs* gp = gargs;
@@ -773,8 +778,9 @@ __global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ ga
       } else {
         // every ring's emptiness at once (lane l: scan position l + 64 w, class-major, own XCD first inside a
         // class), then a pop of the first non-empty one in that order; a lost race rescans
-        const int nr = g.nclass * 8;
+        const int nr = g.nclass * nx;
         const int l = tid & 63;
+        const unsigned long long now = em ? now_t() : 0;
         for (int tries = 0; tries < 4 && t < 0; ++tries) {
           int best = -1;
           for (int w0 = 0; w0 < nr && best < 0; w0 += 64) {
@@ -782,9 +788,14 @@ __global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ ga
             bool ne = false;
             int r = 0;
             if (pos < nr) {
-              r = (pos & ~7) + ((xcd + pos) & 7);
+              r = (pos / nx) * 8 + x0 + (xcd - x0 + pos) % nx;
               const int* hd = g.qctl[rk] + (size_t)(2 * r) * PSTRIDE;
-              ne = ld_q(hd, sy) < ld_q(hd + PSTRIDE, sy);
+              const int h = ld_q(hd, sy);
+              ne = h < ld_q(hd + PSTRIDE, sy);
+              if (ne && em) {   // emulation: a head whose inputs are not visible yet does not count
+                const int sx = ld_sc1(g.qslot[rk] + g.qbase[(size_t)rk * (g.nclass * 8 + 1) + r] + h);
+                ne = sx != 0 && ld_sc1(g.rdy + sx - 1) <= now;
+              }
             }
             const unsigned long long bal = __builtin_amdgcn_ballot_w64(ne);
             if (bal) {
@@ -794,6 +805,10 @@ __global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ ga
           }
           if (best < 0) break;
           t = q_pop(g, best, rk, sy);
+        }
+        if (t >= 0 && em && ld_sc1(g.rdy + t) > now_t()) {
+          // (a race: the popped head was replaced by one not visible yet) -- wait for it, it is ours now
+          while (ld_sc1(g.rdy + t) > now_t()) __builtin_amdgcn_s_sleep(2);
         }
         if (t < 0 && __builtin_amdgcn_readfirstlane(ld_sc1(g.done)) >= g.ntask) t = -2;
       }
@@ -840,6 +855,10 @@ __global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ ga
       tr[2] = ((long long)blockIdx.x << 8) | xcd;
       atomicAdd((unsigned long long*)(tr + 3), 1ULL);
     }
+    unsigned long long due = 0;
+    if (tid == 0 && em) due = emul_due(g, tk, rk, t_start, now_t());
+    if (em) due = __builtin_amdgcn_readfirstlane((unsigned)due) | ((unsigned long long)__builtin_amdgcn_readfirstlane(
+                      (unsigned)(due >> 32)) << 32);
     if (tid < 64) {
       if (sy) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -848,6 +867,10 @@ __global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ ga
       for (int q = sb + tid; q < se; q += 64) {
         const int sx = g.succ[q];
         const int d = g.town ? g.town[sx] : 0;
+        if (em) {   // the successor's visibility: the latest of its predecessors' (before the decrement)
+          __hip_atomic_fetch_max(g.rdy + sx, due, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         const int left = sy ? __hip_atomic_fetch_sub(g.pend[d] + sx, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                             : atomicSub(g.pend[d] + sx, 1);
         if (left == 1) q_push(g, sx, d, sy);
@@ -889,7 +912,7 @@ DPL_API long long dpl_dtr_field(const char* name) {
   DTR_FIELD(vis) DTR_FIELD(link) DTR_FIELD(bw_bpt) DTR_FIELD(lat_t) DTR_FIELD(Mw) DTR_FIELD(Sw) DTR_FIELD(Lp)
   DTR_FIELD(Wp) DTR_FIELD(prog) DTR_FIELD(info) DTR_FIELD(trace) DTR_FIELD(ntask) DTR_FIELD(nclass) DTR_FIELD(pend)
   DTR_FIELD(succ_off) DTR_FIELD(succ) DTR_FIELD(ring_of) DTR_FIELD(town) DTR_FIELD(qbase) DTR_FIELD(qctl)
-  DTR_FIELD(qslot) DTR_FIELD(done)
+  DTR_FIELD(qslot) DTR_FIELD(done) DTR_FIELD(rdy)
   if (!std::strcmp(name, "size")) return (long long)sizeof(DtrArgs);
   if (!std::strcmp(name, "task")) return (long long)sizeof(DtrTask);
   if (!std::strcmp(name, "MAXB")) return MAXB;

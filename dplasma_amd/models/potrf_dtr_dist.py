@@ -315,10 +315,41 @@ class Emulation:
         img.set("flags", D.flags_from_env())
         if trace:
             img.set("trace", self.trace.data_ptr())
+        # scheduling (DPLASMA_DTR_SCHED): "queue" -- push scheduling (k_dtr_q; every rank's rings on its own XCDs,
+        # a successor's visibility the latest of its predecessors' dilated completions), "lists" -- k_dtr_potrf
+        self.sched = os.environ.get("DPLASMA_DTR_SCHED", "queue")
+        self.qk = None
+        if self.sched == "queue":
+            qp = plan.queue()
+            nring = D.NCLASS * 8
+            own = plan.owner.astype(np.int64)
+            xr = (own * X + (qp["ring_of"] % 8) % X)                     # the owner rank's XCDs
+            ring_of = ((qp["ring_of"] // 8) * 8 + xr).astype(np.int32)
+            bases, qctl0, qslot0 = [], [], []
+            for r in range(nr):
+                b, qi, ti = D.queue_rings(ring_of, own == r, qp["ndeps"])
+                bases.append(b)
+                c0 = torch.zeros(2 * nring * img.pstride, dtype=torch.int32)
+                c0.view(nring, 2, img.pstride)[:, 1, 0] = torch.from_numpy(ti)
+                qctl0.append(c0.to(dev))
+                qslot0.append(up(qi))
+            self.qk = qk = {"pend0": up(qp["ndeps"]), "qctl0": qctl0, "qslot0": qslot0,
+                            "pend": [torch.empty(len(plan.tasks), dtype=torch.int32, device=dev) for _ in range(nr)],
+                            "qctl": [torch.empty_like(c) for c in qctl0], "qslot": [torch.empty_like(q_) for q_ in qslot0],
+                            "succ_off": up(qp["succ_off"]), "succ": up(qp["succ"]), "ring_of": up(ring_of),
+                            "town": up(qp["town"]), "qbase": up(np.concatenate(bases)),
+                            "done": torch.zeros(1, dtype=torch.int32, device=dev),
+                            "rdy": torch.zeros(len(plan.tasks), dtype=torch.int64, device=dev)}
+            img.set("ntask", len(plan.tasks))
+            img.set("nclass", D.NCLASS)
+            for f in ("succ_off", "succ", "ring_of", "town", "qbase", "done", "rdy"):
+                img.set(f, qk[f].data_ptr())
+            for f in ("pend", "qctl", "qslot"):
+                img.set(f, [t_.data_ptr() for t_ in qk[f]])
         self.args_d = torch.empty(img.size, dtype=torch.uint8, device=dev)
         self.epoch = 0
         ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-        self.nwg = 2 * ncu
+        self.nwg = int(os.environ.get("DPLASMA_DTR_WG", 2 * ncu))
 
     def reset(self):
         for Ar, a0 in zip(self.A, self.A0):
@@ -335,9 +366,22 @@ class Emulation:
         self.args_d.copy_(torch.frombuffer(bytearray(self.img.buf), dtype=torch.uint8))
         for t in (self.cnt, self.vis, self.link, self.cur, self.scur, self.info):
             t.zero_()
+        qk = self.qk
+        if qk is not None:
+            for r in range(self.nr):
+                qk["pend"][r].copy_(qk["pend0"])
+                qk["qctl"][r].copy_(qk["qctl0"][r])
+                qk["qslot"][r].copy_(qk["qslot0"][r])
+            qk["done"].zero_()
+            qk["rdy"].zero_()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        _lib.check(self.lib.dpl_dtr_potrf(self.args_d.data_ptr(), self.nwg, _lib.stream_ptr()), "dtr_potrf (emulation)")
+        if qk is not None:
+            _lib.check(self.lib.dpl_dtr_potrf_q(self.args_d.data_ptr(), self.nwg, _lib.stream_ptr()),
+                       "dtr_potrf_q (emulation)")
+        else:
+            _lib.check(self.lib.dpl_dtr_potrf(self.args_d.data_ptr(), self.nwg, _lib.stream_ptr()),
+                       "dtr_potrf (emulation)")
         torch.cuda.synchronize()
         span = time.perf_counter() - t0
         r = int(self.info.item())
