@@ -433,7 +433,7 @@ class ArgsImage:
     _LL = ("ld", "ncnt", "bw_bpt", "lat_t")
     _INT = ("nt", "nranks", "rank", "epoch", "flags", "dil", "nsteps", "ntask", "nclass")
     _PTR = ("tasks", "reqs", "tab", "xoff", "cur", "hs_off", "scur", "hi", "lo", "vis", "link", "Mw", "Sw", "Lp", "Wp",
-            "prog", "info", "trace", "succ_off", "succ", "ring_of", "town", "qbase", "done")
+            "prog", "info", "trace", "succ_off", "succ", "ring_of", "town", "qbase", "done", "rdy")
     _PARR = ("A", "recv", "W", "cnt", "pend", "qctl", "qslot")
     _IARR = ("hi_off", "lo_off")
 
