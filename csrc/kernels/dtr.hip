@@ -857,8 +857,10 @@ __global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ ga
     }
     unsigned long long due = 0;
     if (tid == 0 && em) due = emul_due(g, tk, rk, t_start, now_t());
-    if (em) due = __builtin_amdgcn_readfirstlane((unsigned)due) | ((unsigned long long)__builtin_amdgcn_readfirstlane(
-                      (unsigned)(due >> 32)) << 32);
+    if (em) {   // (unsigned words: a signed low word would sign-extend into the high one)
+      const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)due), hi = __builtin_amdgcn_readfirstlane((unsigned)(due >> 32));
+      due = ((unsigned long long)hi << 32) | lo;
+    }
     if (tid < 64) {
       if (sy) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
