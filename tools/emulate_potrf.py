@@ -67,6 +67,10 @@ def main():
                  req_beg=pl.tasks["req_beg"], nreq=pl.tasks["nreq"], reqs=pl.reqs, nranks=nr)
     if a.check:
         L, A0 = em.assemble()
+        del em                      # the per-rank storage, receive buffers and W: the 64k check needs the room
+        import gc
+        gc.collect()
+        torch.cuda.empty_cache()
         ok, res = dp.check_potrf(ctx, dp.dplasmaLower, L, A0)
         print(f"[emul] residual {res:.3e} check={ok}", flush=True)
         if not ok:
