@@ -61,6 +61,72 @@ def _spawn_ranks(n: int, cpu: bool) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def _choose_engine(ctx, uplo, A, A0, tp, args):
+    """N > 1: race the distributed device task runtime (models/potrf_dtr_dist.py, push-scheduled, in-kernel
+    sends over the IPC-mapped peers; modelled at 75 % of 8-GPU peak at 2x4 64k, profiles/r5_dtr_dist_emulation.txt)
+    against the stream engine in the untimed warmup, and keep it only if it builds, factors correctly (residual
+    check) and is faster on every rank -- all three agreed across ranks, so every rank picks the same engine.
+    DPLASMA_BENCH_DIST_ENGINE=stream skips the race."""
+    import torch.distributed as dist
+
+    import dplasma_amd as dp
+    from dplasma_amd.models import potrf_dtr_dist
+    if os.environ.get("DPLASMA_BENCH_DIST_ENGINE", "race") == "stream" or args.cpu or \
+            not potrf_dtr_dist.supported(ctx, uplo, A):
+        return tp, "stream"
+    dev = ctx.device
+
+    def agree(v, op):
+        t = torch.tensor([float(v)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=op)
+        return float(t.item())
+
+    def timed(t):
+        A.data.copy_(A0)
+        t.info.zero_()
+        ctx.sync()
+        ctx.barrier()
+        ctx.sync()
+        t0 = time.perf_counter()
+        t.run(ctx)
+        ctx.sync()
+        el = time.perf_counter() - t0
+        t.complete(ctx)
+        return el
+    tpd, ok = None, 1.0
+    try:
+        tpd = potrf_dtr_dist.potrf_dtr_dist_New(ctx, uplo, A)
+    except Exception as e:   # noqa: BLE001 -- any build failure means: keep the stream engine
+        print(f"rank {ctx.rank}: distributed DTR unavailable ({e})", file=sys.stderr)
+        ok = 0.0
+    if agree(ok, dist.ReduceOp.MIN) < 1:
+        return tp, "stream"
+    t_d = float("inf")
+    try:
+        timed(tpd)
+        t_d = timed(tpd)
+    except RuntimeError as e:   # a drained launch: the taskpool agreed the failure across ranks
+        print(f"rank {ctx.rank}: distributed DTR failed ({e})", file=sys.stderr)
+        ok = 0.0
+    if ok:
+        A_orig = A.like()
+        A_orig.data.copy_(A0)
+        good, _ = dp.check_potrf(ctx, uplo, A, A_orig)
+        del A_orig
+        ok = 1.0 if good else 0.0
+    timed(tp)
+    t_s = timed(tp)
+    ok = agree(ok, dist.ReduceOp.MIN)
+    t_d, t_s = agree(t_d if ok else 1e30, dist.ReduceOp.MAX), agree(t_s, dist.ReduceOp.MAX)
+    if ctx.rank == 0:
+        print(f"bench: warmup race -- distributed DTR {'%.1f ms' % (t_d * 1e3) if ok else 'not usable'}, "
+              f"stream engine {t_s * 1e3:.1f} ms", file=sys.stderr)
+    if ok and t_d < t_s:
+        return tpd, "dtr"
+    potrf_dtr_dist.release_all()
+    return tp, "stream"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -132,6 +198,9 @@ def main():
     tp = dp.dpotrf_New(ctx, uplo, A)
     t_enq = time.perf_counter() - t0
     flops = tp.flops
+    engine = "dtr" if getattr(tp, "dtr_plan", None) is not None else "stream"
+    if world > 1:
+        tp, engine = _choose_engine(ctx, uplo, A, A0, tp, args)
 
     def step():
         A.data.copy_(A0)
@@ -195,6 +264,7 @@ def main():
             "residual": res,
             "check_s": round(t_check, 2) if args.check else None,
             "enq_s": round(t_enq, 3),
+            "engine": engine,
             "config": {"model": f"dpotrf ({'lower' if args.uplo == 'L' else 'upper'}, 2D block-cyclic tiles)", "N": N, "NB": NB, "global_batch": 1,
                        "seq_len": N, "parallelism": f"{ctx.P}x{ctx.Q} block-cyclic (one rank per GPU)"},
         }
