@@ -535,7 +535,10 @@ def potrf_dtr_dist_New(ctx, uplo: int, A, info_out=None):
     dev = A.device
     hi, hi_off, lo, lo_off = plan.lists({me: list(range(8))})
     sched = os.environ.get("DPLASMA_DTR_SCHED", "queue")
-    specs = [(plan.recv_elems(me) * 8, True), (nt * NBT * NBT * 8, True), (plan.ncnt * 4, False)]
+    # receive buffer and W: cached device memory (operands of many update tasks); DPLASMA_DTR_RECV_UNCACHED=1 puts
+    # them in uncached memory instead (a diagnostic for peers whose stores a consumer might read stale)
+    rc_ = os.environ.get("DPLASMA_DTR_RECV_UNCACHED", "0") != "1"
+    specs = [(plan.recv_elems(me) * 8, rc_), (nt * NBT * NBT * 8, rc_), (plan.ncnt * 4, False)]
     qp = None
     if sched == "queue":
         qp = plan.queue()
