@@ -365,6 +365,11 @@ TASK_US = {"upd1": 75.0, "upd_k": 65.0, "trsm": 175.0, "potrf": 300.0, "send": 2
 
 
 def task_weights(tasks):
+    # DPLASMA_DTR_BL_W="upd1,upd_k,trsm,potrf" overrides the weights (measurement knob)
+    w = os.environ.get("DPLASMA_DTR_BL_W")
+    if w:
+        for k_, v in zip(("upd1", "upd_k", "trsm", "potrf"), w.split(",")):
+            TASK_US[k_] = float(v)
     typ = tasks["type"]
     nk = tasks["nk"].astype(np.float64)
     return np.where(typ == T_UPD, np.maximum(TASK_US["upd1"], TASK_US["upd_k"] * nk),
