@@ -48,6 +48,15 @@ NBT, MAXB = D.NBT, D.MAXB
 STRIP = 128 * NBT                     # elements of a 128-row strip of a 512 x 512 tile
 
 
+def _unique_pairs(a, b):
+    """np.unique(np.stack([a, b], 1), axis=0) for non-negative integer columns, through one 1-D key (the row-wise
+    unique sorts structured rows: 14 s of a 64k 2 x 4 plan)."""
+    a, b = np.asarray(a, dtype=np.int64), np.asarray(b, dtype=np.int64)
+    m = int(b.max()) + 1 if len(b) else 1
+    k = np.unique(a * m + b)
+    return np.stack([k // m, k % m], 1)
+
+
 class DistPlan:
     """Per-rank task lists, requirement targets, sends and receive slots of a P x Q grid."""
 
@@ -73,14 +82,14 @@ class DistPlan:
         powner = self._owner(I // 4, J // 4)
         remote_strip = strip_req & (powner != towner)
         # consumers of remote strips: unique (counter, consumer rank)
-        cons = np.unique(np.stack([idx[remote_strip], towner[remote_strip]], 1), axis=0) if remote_strip.any() \
+        cons = _unique_pairs(idx[remote_strip], towner[remote_strip]) if remote_strip.any() \
             else np.zeros((0, 2), dtype=np.int64)
         reqs[remote_strip, 1] = 1
         w_req = (ttype == T_TRSM) & (rpos == 0)
         kW = idx - WB
         wowner = self._owner(kW, kW)
         remote_w = w_req & (wowner != towner)
-        wcons = np.unique(np.stack([kW[remote_w], towner[remote_w]], 1), axis=0) if remote_w.any() \
+        wcons = _unique_pairs(kW[remote_w], towner[remote_w]) if remote_w.any() \
             else np.zeros((0, 2), dtype=np.int64)
         reqs[remote_w, 1] = 4
         # ---- send tasks
@@ -133,7 +142,7 @@ class DistPlan:
         self.recv_slot = []
         for r in range(self.nranks):
             sel = cons[:, 1] == r if ns else np.zeros(0, dtype=bool)
-            tl = np.unique(np.stack([(cons[sel, 0] % S) // 4, cons[sel, 0] // S // 4], 1), axis=0) \
+            tl = _unique_pairs((cons[sel, 0] % S) // 4, cons[sel, 0] // S // 4) \
                 if ns and sel.any() else np.zeros((0, 2), dtype=np.int64)
             self.recv_tiles.append(tl)
             self.recv_slot.append({(int(i), int(k)): q for q, (i, k) in enumerate(tl)})
