@@ -16,4 +16,13 @@ perf panel_heavy DPLASMA_DTR_BL_W=75,65,400,800
 perf trsm_heavy DPLASMA_DTR_BL_W=75,65,600,300
 perf flat DPLASMA_DTR_BL_W=60,60,60,60
 perf chain_light DPLASMA_DTR_BL_W=75,65,100,150
+emu() {
+  echo "== emul 2x4 64k $1" | tee -a $O/summary.log
+  shift
+  env DPLASMA_DTR_WG=256 "$@" timeout -k 10 300 python tools/emulate_potrf.py -N 65536 --grid 2x4 --bw 50 --lat 10 --reps 2 \
+    2>&1 | grep EMUL | tee -a $O/summary.log
+}
+emu default DPLASMA_DTR_SCHED=queue
+emu panel_heavy DPLASMA_DTR_BL_W=75,65,400,800
+emu chain_light DPLASMA_DTR_BL_W=75,65,100,150
 exit 0
