@@ -25,7 +25,16 @@
 //   SEND(i, k, r, dest) / SENDW(k, c, dest) (P x Q grids, models/potrf_dtr_dist.py): strip r of the
 //       solved panel tile (i, k) / column block c of W_k into rank dest's receive buffer / W, then one
 //       bump of dest's counter -- a remote strip is an arrival requirement of the consumer's tasks.
-// Dependencies are tile-version counters, not successor lists: each task lists (counter, target)
+// Two schedulers share the task bodies:
+//  * k_dtr_q (default, DPLASMA_DTR_SCHED=queue): PUSH scheduling.  The host turns the requirement lists into
+//    task edges (models/potrf_dtr.py queue_edges); a task is pushed into a ready ring -- one FIFO per (class,
+//    XCD), class = its bottom level (longest path of task durations to the end) bucketed, POTRF blocks first --
+//    by the workgroup that completes its last predecessor; idle workgroups scan all rings with one ballot per 64
+//    and pop the best.  Across ranks a send decrements its remote consumers' pending counts and pushes them into
+//    the peer's rings through the IPC mapping (system scope).  No ready task waits behind a list head
+//    (profiles/r5_dtr_queue.txt: 16k 45.8 -> 48.8 TF/s; 2x4 64k emulated 17-30 % -> 74.8 %).
+//  * k_dtr_potrf (DPLASMA_DTR_SCHED=lists): the static lists below.
+// Dependencies of the list scheduler are tile-version counters, not successor lists: each task lists (counter, target)
 // requirements (a 128x128 sub-tile's number of completed writes, a panel strip's "solved" mark, the
 // number of finished W_k block columns) and bumps one counter when done.  A list's head is claimed
 // (CAS on the list cursor) only when ready, so tasks start in list order and nobody ever waits
