@@ -359,22 +359,25 @@ def queue_edges(tasks, reqs, WB, owner=None, inc_rank=None):
     return ndeps, succ_off, succ
 
 
-# measured mean task durations at one workgroup per CU (us; profiles/r5_dtr_queue.txt): the weights of the
-# bottom-level priorities
-TASK_US = {"upd1": 75.0, "upd_k": 65.0, "trsm": 175.0, "potrf": 300.0, "send": 20.0}
+# weights of the bottom-level priorities (us).  Start: measured mean task durations at one workgroup per CU
+# (profiles/r5_dtr_queue.txt: trsm 175, potrf 300); the critical-path tasks are weighted above their mean
+# duration -- the sweep in profiles/r5_dtr_bl_weights.txt found trsm 400 / potrf 800 best or tied at 16k, 32k and
+# on the emulated 2x4 grid at 64k (75.5 % vs 74.4 %)
+TASK_US = {"upd1": 75.0, "upd_k": 65.0, "trsm": 400.0, "potrf": 800.0, "send": 20.0}
 
 
 def task_weights(tasks):
     # DPLASMA_DTR_BL_W="upd1,upd_k,trsm,potrf" overrides the weights (measurement knob)
+    us = dict(TASK_US)
     w = os.environ.get("DPLASMA_DTR_BL_W")
     if w:
         for k_, v in zip(("upd1", "upd_k", "trsm", "potrf"), w.split(",")):
-            TASK_US[k_] = float(v)
+            us[k_] = float(v)
     typ = tasks["type"]
     nk = tasks["nk"].astype(np.float64)
-    return np.where(typ == T_UPD, np.maximum(TASK_US["upd1"], TASK_US["upd_k"] * nk),
-                    np.where(typ == T_TRSM, TASK_US["trsm"], np.where(typ == T_POTRF, TASK_US["potrf"],
-                                                                      TASK_US["send"]))).astype(np.float64)
+    return np.where(typ == T_UPD, np.maximum(us["upd1"], us["upd_k"] * nk),
+                    np.where(typ == T_TRSM, us["trsm"], np.where(typ == T_POTRF, us["potrf"],
+                                                                 us["send"]))).astype(np.float64)
 
 
 def bottom_levels(succ_off, succ, w):
