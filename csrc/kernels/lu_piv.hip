@@ -407,13 +407,109 @@ __device__ inline void wave_argmax(double& v, int& i) {
   }
 }
 
+// Pivot of one column across the G workgroups: every workgroup has published its local winner (v at
+// pval[par G + w], row at pidx[par G + w]) and its candidate row; returns the global winner (largest
+// magnitude, lowest row on ties) in every thread.
+//  HIER (default): XCD-sharded fan-in -- workgroup w arrives on the counter of group w % 8 (the hardware
+//    dispatches blockIdx round-robin over the 8 XCDs, so a group is an XCD; correctness never depends on it),
+//    the group's LAST arriver (told by the value its add returned) reduces the group's candidates, publishes
+//    the group winner and arrives on the top counter; every workgroup polls the top counter and reduces <= 8
+//    group winners.  ~32 + 8 serialised atomics and 8 candidate loads per workgroup instead of 256 + 256
+//    (MI355X_MICROARCH.md barrier-counter 7.4 us vs barrier-xcd 4.1 us at 256 workgroups).
+//  flat: one counter, every workgroup reduces all G candidates (the former path; dpl_lu_block_set_kind(2)).
+// ctr: 9 counters, 32 ints apart (zeroed before the launch); gval / gidx: [2][8] group winners.
+// sv / si: >= 13 LDS slots.  Everything crossing workgroups is an sc1 store drained before the arrival and
+// an sc1 load after the poll (grid_sync.h).
+template <bool HIER>
+__device__ inline void lu_pick(double v, int vi, int par, int cj, int G, int w, double* pval, int* pidx, int* ctr,
+                               double* gval, int* gidx, int* info, double* sv, int* si, double& best, int& bi) {
+  const int tid = threadIdx.x;
+  if (!HIER) {
+    grid_sync_counter(ctr, (cj + 1) * G, info);
+    best = -1.0;
+    bi = 0x7fffffff;
+    for (int b = tid; b < G; b += PLR) {
+      const double pv_ = ld_sc1(&pval[par * G + b]);
+      const int pi_ = ld_sc1(&pidx[par * G + b]);
+      if (pv_ > best || (pv_ == best && pi_ < bi)) { best = pv_; bi = pi_; }
+    }
+    wave_argmax(best, bi);
+    if ((tid & 63) == 0) { sv[8 + (tid >> 6)] = best; si[8 + (tid >> 6)] = bi; }
+    __syncthreads();
+    best = sv[8];
+    bi = si[8];
+#pragma unroll
+    for (int q = 1; q < PLR / 64; ++q)
+      if (sv[8 + q] > best || (sv[8 + q] == best && si[8 + q] < bi)) { best = sv[8 + q]; bi = si[8 + q]; }
+    return;
+  }
+  (void)v;
+  (void)vi;
+  const int ng = G < 8 ? G : 8;
+  const int x = w % ng;
+  const int gx = (G - x + ng - 1) / ng;        // workgroups of group x: x, x + ng, ...
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(&ctr[32 * x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    si[12] = (old + 1 == (cj + 1) * gx);
+  }
+  __syncthreads();
+  if (si[12]) {                                 // uniform: the group's last arriver reduces it
+    double gv = -1.0;
+    int gi = 0x7fffffff;
+    for (int t = tid; t < gx; t += PLR) {
+      const int b = x + t * ng;
+      const double pv_ = ld_sc1(&pval[par * G + b]);
+      const int pi_ = ld_sc1(&pidx[par * G + b]);
+      if (pv_ > gv || (pv_ == gv && pi_ < gi)) { gv = pv_; gi = pi_; }
+    }
+    wave_argmax(gv, gi);
+    if ((tid & 63) == 0) { sv[8 + (tid >> 6)] = gv; si[8 + (tid >> 6)] = gi; }
+    __syncthreads();
+    if (tid == 0) {
+      gv = sv[8];
+      gi = si[8];
+#pragma unroll
+      for (int q = 1; q < PLR / 64; ++q)
+        if (sv[8 + q] > gv || (sv[8 + q] == gv && si[8 + q] < gi)) { gv = sv[8 + q]; gi = si[8 + q]; }
+      st_sc1(&gval[par * 8 + x], gv);
+      st_sc1(&gidx[par * 8 + x], gi);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(&ctr[32 * 8], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (tid == 0) {
+    const int target = (cj + 1) * ng;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(&ctr[32 * 8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ULL) {  // 100 MHz clock: 2 s (grid not co-resident)
+        if (info) atomicExch(info, -1000);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    best = tid < ng ? ld_sc1(&gval[par * 8 + tid]) : -1.0;
+    bi = tid < ng ? ld_sc1(&gidx[par * 8 + tid]) : 0x7fffffff;
+    wave_argmax(best, bi);
+    if (tid == 0) { sv[12] = best; si[13] = bi; }
+  }
+  __syncthreads();
+  best = sv[12];
+  bi = si[13];
+}
+
 // BWT: the widest block this instantiation holds (64: 128 KiB LDS tile for fp64; 32: 64 KiB, which leaves
 // room on the CU for one trailing-update GEMM workgroup -- DPLASMA_LU_BW=32, the recursion's base width)
-template <typename T, int BWT>
+template <typename T, int BWT, bool HIER>
 __global__ __launch_bounds__(PLR) void k_lu_block_persist(T* __restrict__ A, int ld, int m, int c0, int cend, int R,
                                                           int* __restrict__ ipiv, T* __restrict__ cand,
                                                           double* __restrict__ pval, int* __restrict__ pidx,
-                                                          int* __restrict__ cnt, int* __restrict__ info,
+                                                          int* __restrict__ cnt, double* __restrict__ gval,
+                                                          int* __restrict__ gidx, int* __restrict__ info,
                                                           int info_base) {
   __shared__ T tile[BWT * PLR];      // column-major: tile[c * R + r]
   __shared__ T prow[PBW], oldj[PBW];
@@ -469,30 +565,12 @@ __global__ __launch_bounds__(PLR) void k_lu_block_persist(T* __restrict__ A, int
     if (lw != 0x7fffffff && tid < BW) st_sc1(&cand[((long long)par * G + w) * PBW + tid], tile[tid * R + (lw - rbase)]);
     if (j >= rbase && j < rbase + nr && tid < BW)
       st_sc1(&cand[((long long)2 * G + par) * PBW + tid], tile[tid * R + (j - rbase)]);
-    grid_sync_counter(cnt, (cj + 1) * G, info);
-    // ---- 3. global pivot (every workgroup reduces the same G candidates)
+    // ---- 3. global pivot (the winning workgroup travels with the row index: row -> owner is rbase
+    //         arithmetic; LDS slots 8..13 are the exchange's, 0..7 hold this and the previous column's search)
     {
-      double best = -1.0;
-      int bi = 0x7fffffff, bw = 0;
-      for (int b = tid; b < G; b += PLR) {
-        const double pv_ = ld_sc1(&pval[par * G + b]);
-        const int pi_ = ld_sc1(&pidx[par * G + b]);
-        if (pv_ > best || (pv_ == best && pi_ < bi)) { best = pv_; bi = pi_; bw = b; }
-      }
-      // the winning workgroup travels with the row index (row -> owner is rbase arithmetic); the waves'
-      // winners in LDS slots 8..11 (slots 0..7 hold the local search of this and the previous column)
-      wave_argmax(best, bi);
-      if ((tid & 63) == 0) { sv[8 + (tid >> 6)] = best; si[8 + (tid >> 6)] = bi; }
-      __syncthreads();
-      best = sv[8];
-      bi = si[8];
-#pragma unroll
-      for (int q = 1; q < PLR / 64; ++q) {
-        const double v2 = sv[8 + q];
-        const int i2 = si[8 + q];
-        if (v2 > best || (v2 == best && i2 < bi)) { best = v2; bi = i2; }
-      }
-      (void)bw;
+      double best;
+      int bi;
+      lu_pick<HIER>(v, lw, par, cj, G, w, pval, pidx, cnt, gval, gidx, info, sv, si, best, bi);
       const int p = bi, pw = (p - c0) / R;
       if (tid < BW) {
         prow[tid] = ld_sc1(&cand[((long long)par * G + pw) * PBW + tid]);
@@ -525,6 +603,170 @@ __global__ __launch_bounds__(PLR) void k_lu_block_persist(T* __restrict__ A, int
   }
 }
 
+// ---------------------------------------------------------------- tagged-granule block LU (default)
+// k_lu_block_persist with the pivot exchange done through self-validating granules instead of a counter:
+// every value that crosses workgroups travels as one 8-byte {32-bit payload, 32-bit tag} word written by ONE
+// sc1 store, tag = launch epoch << 7 | (column + 1).  A reader polls the words themselves until every tag
+// matches -- no drain before an arrival, no counter round trip, no poll on a separate flag (MI355X_MICROARCH.md
+// handoff-1to1 ~0.8-1 us vs barrier-counter 7.4 us): one column costs the local search, one record read
+// (value hi / lo, row) of every workgroup, and one read of the winning row and the old row j.
+// Records, candidate rows and row j are double-buffered by column parity: a workgroup publishes column cj + 2
+// only after it has read every workgroup's column cj + 1, which each of them published after reading cj.
+// Layout (8-byte words): rec[2][G][4] = {value hi, value lo, row}, rows[2][G][PBW * NW], jrow[2][PBW * NW]
+// (NW = 32-bit words per element).
+__device__ inline bool tag_poll(const unsigned long long* p, unsigned tag, unsigned long long& x, int* info) {
+  x = ld_sc1(p);
+  if ((unsigned)x == tag) return true;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  do {
+    __builtin_amdgcn_s_sleep(1);
+    x = ld_sc1(p);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ULL) {  // 100 MHz clock: 2 s (grid not co-resident)
+      if (info) atomicExch(info, -1000);
+      return false;
+    }
+  } while ((unsigned)x != tag);
+  return true;
+}
+
+// one element as NW tagged words (payload in the high half) / back, polling stale words
+template <typename T> __device__ inline void tag_put(unsigned long long* p, T x, unsigned tag) {
+  constexpr int NW = sizeof(T) / 4;
+  unsigned u[NW];
+  __builtin_memcpy(u, &x, sizeof(T));
+#pragma unroll
+  for (int q = 0; q < NW; ++q) st_sc1(&p[q], ((unsigned long long)u[q] << 32) | tag);
+}
+template <typename T> __device__ inline T tag_get(const unsigned long long* p, unsigned tag, int* info) {
+  constexpr int NW = sizeof(T) / 4;
+  unsigned long long x[NW];
+#pragma unroll
+  for (int q = 0; q < NW; ++q) x[q] = ld_sc1(&p[q]);
+  unsigned u[NW];
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    if ((unsigned)x[q] != tag) tag_poll(&p[q], tag, x[q], info);
+    u[q] = (unsigned)(x[q] >> 32);
+  }
+  T v;
+  __builtin_memcpy(&v, u, sizeof(T));
+  return v;
+}
+
+template <typename T, int BWT>
+__global__ __launch_bounds__(PLR) void k_lu_block_tag(T* __restrict__ A, int ld, int m, int c0, int cend, int R,
+                                                      int* __restrict__ ipiv, unsigned long long* __restrict__ rec,
+                                                      unsigned long long* __restrict__ rows,
+                                                      unsigned long long* __restrict__ jrow, unsigned tag0,
+                                                      int* __restrict__ info, int info_base) {
+  constexpr int NW = sizeof(T) / 4;
+  __shared__ T tile[BWT * PLR];      // column-major: tile[c * R + r]
+  __shared__ T prow[PBW], oldj[PBW];
+  __shared__ double sv[16];
+  __shared__ int si[16];
+  const int G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
+  __builtin_amdgcn_s_setprio(3);
+  const int BW = cend - c0;
+  const int rbase = c0 + w * R;
+  const int nr = max(0, min(R, m - rbase));
+  for (int e = tid; e < BW * R; e += PLR) {
+    const int c = e / R, r = e % R;
+    if (r < nr) tile[c * R + r] = A[(rbase + r) + (long long)(c0 + c) * ld];
+  }
+  __syncthreads();
+  const int r = tid, g = rbase + tid;
+  const bool own = r < nr;
+  for (int cj = 0; cj < BW; ++cj) {
+    const int j = c0 + cj;
+    const int par = cj & 1;
+    const unsigned tag = tag0 | (unsigned)(cj + 1);
+    // ---- 1. apply column cj-1 (pivot row in prow)
+    if (cj > 0 && own && g >= j) {
+      const T d = prow[cj - 1];
+      T l = tile[(cj - 1) * R + r];
+      if (!is_zero(d)) l = divv(l, d);
+      tile[(cj - 1) * R + r] = l;
+      for (int c = cj; c < BW; ++c) tile[c * R + r] = sub(tile[c * R + r], mul(l, prow[c]));
+    }
+    // ---- 2. local |max| of column cj over rows >= j
+    double v = (own && g >= j) ? piv_mag((double)abs1(tile[cj * R + r])) : -1.0;
+    int vi = (own && g >= j) ? g : 0x7fffffff;
+    wave_argmax(v, vi);
+    if ((tid & 63) == 0) { sv[(tid >> 6) + 4 * par] = v; si[(tid >> 6) + 4 * par] = vi; }
+    __syncthreads();
+    v = sv[4 * par];
+    vi = si[4 * par];
+#pragma unroll
+    for (int q = 1; q < PLR / 64; ++q) {
+      const double v2 = sv[q + 4 * par];
+      const int i2 = si[q + 4 * par];
+      if (v2 > v || (v2 == v && i2 < vi)) { v = v2; vi = i2; }
+    }
+    // ---- publish: record, candidate row, and row j by its owner (tagged words, no drain, no counter)
+    if (tid == 0) {
+      const unsigned long long vb = (unsigned long long)__double_as_longlong(v);
+      unsigned long long* rc = rec + ((long long)par * G + w) * 4;
+      st_sc1(&rc[0], ((vb >> 32) << 32) | tag);
+      st_sc1(&rc[1], (vb << 32) | tag);
+      st_sc1(&rc[2], ((unsigned long long)(unsigned)vi << 32) | tag);
+    }
+    // candidate row by threads [0, 64), row j by threads [64, 128): one element (NW words) per thread
+    if (tid < BW && vi != 0x7fffffff)
+      tag_put<T>(&rows[((long long)par * G + w) * (PBW * NW) + tid * NW], tile[tid * R + (vi - rbase)], tag);
+    if (tid >= 64 && tid - 64 < BW && j >= rbase && j < rbase + nr)
+      tag_put<T>(&jrow[(long long)par * (PBW * NW) + (tid - 64) * NW], tile[(tid - 64) * R + (j - rbase)], tag);
+    // ---- 3. every workgroup's record -> global pivot (same answer everywhere)
+    double best = -1.0;
+    int bi = 0x7fffffff;
+    for (int b = tid; b < G; b += PLR) {
+      const unsigned long long* rc = rec + ((long long)par * G + b) * 4;
+      // the three words issued together; only a stale one is polled again
+      unsigned long long x0 = ld_sc1(&rc[0]), x1 = ld_sc1(&rc[1]), x2 = ld_sc1(&rc[2]);
+      if ((unsigned)x0 != tag) tag_poll(&rc[0], tag, x0, info);
+      if ((unsigned)x1 != tag) tag_poll(&rc[1], tag, x1, info);
+      if ((unsigned)x2 != tag) tag_poll(&rc[2], tag, x2, info);
+      const double pv_ = __longlong_as_double((long long)(((x0 >> 32) << 32) | (x1 >> 32)));
+      const int pi_ = (int)(unsigned)(x2 >> 32);
+      if (pv_ > best || (pv_ == best && pi_ < bi)) { best = pv_; bi = pi_; }
+    }
+    wave_argmax(best, bi);
+    if ((tid & 63) == 0) { sv[8 + (tid >> 6)] = best; si[8 + (tid >> 6)] = bi; }
+    __syncthreads();
+    best = sv[8];
+    bi = si[8];
+#pragma unroll
+    for (int q = 1; q < PLR / 64; ++q)
+      if (sv[8 + q] > best || (sv[8 + q] == best && si[8 + q] < bi)) { best = sv[8 + q]; bi = si[8 + q]; }
+    const bool any = bi != 0x7fffffff;           // no eligible row (j >= m): nothing to pivot
+    const int p = bi, pw = any ? (p - c0) / R : 0;
+    // ---- 4. the winning row (threads [0, 64)) and the old row j (threads [64, 128))
+    if (any && tid < BW) prow[tid] = tag_get<T>(&rows[((long long)par * G + pw) * (PBW * NW) + tid * NW], tag, info);
+    if (j < m && tid >= 64 && tid - 64 < BW)
+      oldj[tid - 64] = tag_get<T>(&jrow[(long long)par * (PBW * NW) + (tid - 64) * NW], tag, info);
+    __syncthreads();
+    if (any && tid < BW) {
+      if (j >= rbase && j < rbase + nr) tile[tid * R + (j - rbase)] = prow[tid];
+      if (p != j && p >= rbase && p < rbase + nr) tile[tid * R + (p - rbase)] = oldj[tid];
+    }
+    if (w == 0 && tid == 0 && any) {
+      ipiv[j] = p;
+      if (best == 0.0 && info) atomicCAS(info, 0, info_base + j + 1);
+    }
+    __syncthreads();
+  }
+  if (own && g >= cend) {
+    const T d = prow[BW - 1];
+    T l = tile[(BW - 1) * R + r];
+    if (!is_zero(d)) l = divv(l, d);
+    tile[(BW - 1) * R + r] = l;
+  }
+  __syncthreads();
+  for (int e = tid; e < BW * R; e += PLR) {
+    const int c = e / R, rr = e % R;
+    if (rr < nr) A[(rbase + rr) + (long long)(c0 + c) * ld] = tile[c * R + rr];
+  }
+}
+
 // ---------------------------------------------------------------- register-resident block LU
 // Same algorithm and hand-offs as k_lu_block_persist, but every thread keeps ITS ROW of the block in
 // registers (v[c], c < 64, the column loop fully unrolled so every index is static) instead of a
@@ -535,10 +777,11 @@ template <typename T>
 __global__ __launch_bounds__(PLR) void k_lu_block_reg(T* __restrict__ A, int ld, int m, int c0, int cend, int R,
                                                       int* __restrict__ ipiv, T* __restrict__ cand,
                                                       double* __restrict__ pval, int* __restrict__ pidx,
-                                                      int* __restrict__ cnt, int* __restrict__ info, int info_base) {
+                                                      int* __restrict__ cnt, double* __restrict__ gval,
+                                                      int* __restrict__ gidx, int* __restrict__ info, int info_base) {
   __shared__ T prow[PBW], oldj[PBW];
-  __shared__ double sv[PLR / 64];
-  __shared__ int si[PLR / 64];
+  __shared__ double sv[16];
+  __shared__ int si[16];
   const int G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
   const int BW = cend - c0;
   const int rbase = c0 + w * R;
@@ -588,23 +831,10 @@ __global__ __launch_bounds__(PLR) void k_lu_block_reg(T* __restrict__ A, int ld,
       for (int c = 0; c < PBW; ++c)
         if (c < BW) st_sc1(&cand[((long long)2 * G + par) * PBW + c], v[c]);
     }
-    grid_sync_counter(cnt, (cj + 1) * G, info);
-    // ---- 3. global pivot (every workgroup reduces the same G candidates)
-    double best = -1.0;
-    int bix = 0x7fffffff;
-    for (int b = tid; b < G; b += PLR) {
-      const double pv_ = ld_sc1(&pval[par * G + b]);
-      const int pi_ = ld_sc1(&pidx[par * G + b]);
-      if (pv_ > best || (pv_ == best && pi_ < bix)) { best = pv_; bix = pi_; }
-    }
-    wave_argmax(best, bix);
-    if ((tid & 63) == 0) { sv[tid >> 6] = best; si[tid >> 6] = bix; }
-    __syncthreads();
-    best = sv[0];
-    bix = si[0];
-#pragma unroll
-    for (int q = 1; q < PLR / 64; ++q)
-      if (sv[q] > best || (sv[q] == best && si[q] < bix)) { best = sv[q]; bix = si[q]; }
+    // ---- 3. global pivot
+    double best;
+    int bix;
+    lu_pick<true>(bv, bi, par, cj, G, w, pval, pidx, cnt, gval, gidx, info, sv, si, best, bix);
     const int p = bix, pw = (p - c0) / R;
     if (tid < BW) {
       prow[tid] = ld_sc1(&cand[((long long)par * G + pw) * PBW + tid]);
@@ -636,7 +866,9 @@ __global__ __launch_bounds__(PLR) void k_lu_block_reg(T* __restrict__ A, int ld,
     if (own && c < BW) A[g + (long long)(c0 + c) * ld] = v[c];
 }
 
-// block kernel choice for the pivoting persistent path: 0 = LDS tile (default), 1 = register-resident rows.
+// block kernel choice for the pivoting persistent path: 0 = LDS tile, tagged-granule exchange (default),
+// 1 = register-resident rows, 2 = LDS tile with the flat one-counter exchange (the former default), 3 = LDS tile
+// with the XCD-sharded counter exchange (profiles/r5_lu_pivot_exchange.txt).
 // Measured on one MI355X (profiles/r3_lu_block_reg.txt): the register variant is 30 % slower per column
 // (64 fully unrolled column steps: ~100 KiB of code per launch, instruction-cache bound) and look-ahead
 // does not recover it -- kept opt-in (DPLASMA_LU_BLOCK=reg) as the measured alternative.
@@ -663,10 +895,15 @@ static int g_num_cus = 0;
 
 // ws layout (bytes): [0, 8*2*G) pval, then 4*2*G pidx, then 8-aligned candidate rows
 // (3 * G * PBW * sizeof(T) <= 3 * 256 * 64 * 16 B); callers size it with dpl_lu_block_ws_bytes.
+// + the tagged-exchange area (k_lu_block_tag) at LU_TAG_OFF: rec 2 x 256 x 32 B, rows 2 x 256 x PBW x 2 x 8 B,
+// jrow 2 x PBW x 2 x 8 B.
+#define LU_TAG_OFF (1LL << 20)
 DPL_API long long dpl_lu_block_ws_bytes(int m) {
   const int maxwg = (m + LUR - 1) / LUR;
   long long a = 16LL * (maxwg > 256 ? maxwg : 256) + 64;
-  return a + 3LL * 256 * PBW * 16 + 64;
+  a += 3LL * 256 * PBW * 16 + 64;
+  const long long tag_end = LU_TAG_OFF + 2LL * 256 * 32 + 2LL * 256 * PBW * 2 * 8 + 2LL * PBW * 2 * 8;
+  return a > tag_end ? a : tag_end;
 }
 
 // ------------------------------------------------------------------ no-pivot block LU
@@ -756,27 +993,55 @@ DPL_API int dpl_lu_block(int prec, void* A, int ld, int m, int c0, int cend, int
       double* pval = (double*)b;
       int* pidx = (int*)(b + 8LL * 2 * 256);
       void* cand = (void*)(b + 8LL * 2 * 256 + 4LL * 2 * 256 + 64);
-      hipMemsetAsync(cnt, 0, sizeof(int), st);
+      // exchange counters (9 x 128 B) and group winners behind the candidate rows (real types: 8-B elements)
+      char* xb = b + ((8LL * 2 * 256 + 4LL * 2 * 256 + 64 + 3LL * 256 * PBW * 8 + 127) & ~127LL);
+      int* ctr = (int*)xb;
+      double* gval = (double*)(xb + 9 * 128);
+      int* gidx = (int*)(xb + 9 * 128 + 8 * 16);
+      if (g_lu_kind == 0) {
+        static unsigned epoch = 0;
+        epoch = (epoch + 1) & 0x1ffffffu;
+        const unsigned tag0 = epoch << 7;
+        unsigned long long* rec = (unsigned long long*)(b + LU_TAG_OFF);
+        unsigned long long* rws = rec + 2 * 256 * 4;
+        unsigned long long* jrw = rws + 2LL * 256 * PBW * 2;
+#define LUT_ARGS(T) (T*)A, ld, m, c0, cend, R, ipiv, rec, rws, jrw, tag0, info, info_base
+        if (cend - c0 <= 32) {
+          if (prec == DPL_D) hipLaunchKernelGGL((k_lu_block_tag<double, 32>), dim3(G), dim3(PLR), 0, st, LUT_ARGS(double));
+          else hipLaunchKernelGGL((k_lu_block_tag<float, 32>), dim3(G), dim3(PLR), 0, st, LUT_ARGS(float));
+        } else if (prec == DPL_D) {
+          hipLaunchKernelGGL((k_lu_block_tag<double, 64>), dim3(G), dim3(PLR), 0, st, LUT_ARGS(double));
+        } else {
+          hipLaunchKernelGGL((k_lu_block_tag<float, 64>), dim3(G), dim3(PLR), 0, st, LUT_ARGS(float));
+        }
+#undef LUT_ARGS
+        return (int)hipGetLastError();
+      }
+      const bool flat = g_lu_kind == 2;
+      if (flat) ctr = cnt;
+      hipMemsetAsync(ctr, 0, flat ? sizeof(int) : 9 * 128, st);
+#define LUB_ARGS(T) (T*)A, ld, m, c0, cend, R, ipiv, (T*)cand, pval, pidx, ctr, gval, gidx, info, info_base
       if (g_lu_kind == 1) {
         if (prec == DPL_D)
-          hipLaunchKernelGGL((k_lu_block_reg<double>), dim3(G), dim3(PLR), 0, st, (double*)A, ld, m, c0, cend, R,
-                             ipiv, (double*)cand, pval, pidx, cnt, info, info_base);
+          hipLaunchKernelGGL((k_lu_block_reg<double>), dim3(G), dim3(PLR), 0, st, LUB_ARGS(double));
         else
-          hipLaunchKernelGGL((k_lu_block_reg<float>), dim3(G), dim3(PLR), 0, st, (float*)A, ld, m, c0, cend, R,
-                             ipiv, (float*)cand, pval, pidx, cnt, info, info_base);
+          hipLaunchKernelGGL((k_lu_block_reg<float>), dim3(G), dim3(PLR), 0, st, LUB_ARGS(float));
       } else if (cend - c0 <= 32) {
-        if (prec == DPL_D)
-          hipLaunchKernelGGL((k_lu_block_persist<double, 32>), dim3(G), dim3(PLR), 0, st, (double*)A, ld, m, c0, cend,
-                             R, ipiv, (double*)cand, pval, pidx, cnt, info, info_base);
-        else
-          hipLaunchKernelGGL((k_lu_block_persist<float, 32>), dim3(G), dim3(PLR), 0, st, (float*)A, ld, m, c0, cend,
-                             R, ipiv, (float*)cand, pval, pidx, cnt, info, info_base);
-      } else if (prec == DPL_D)
-        hipLaunchKernelGGL((k_lu_block_persist<double, 64>), dim3(G), dim3(PLR), 0, st, (double*)A, ld, m, c0, cend, R,
-                           ipiv, (double*)cand, pval, pidx, cnt, info, info_base);
-      else
-        hipLaunchKernelGGL((k_lu_block_persist<float, 64>), dim3(G), dim3(PLR), 0, st, (float*)A, ld, m, c0, cend, R,
-                           ipiv, (float*)cand, pval, pidx, cnt, info, info_base);
+        if (prec == DPL_D) {
+          if (flat) hipLaunchKernelGGL((k_lu_block_persist<double, 32, false>), dim3(G), dim3(PLR), 0, st, LUB_ARGS(double));
+          else hipLaunchKernelGGL((k_lu_block_persist<double, 32, true>), dim3(G), dim3(PLR), 0, st, LUB_ARGS(double));
+        } else {
+          if (flat) hipLaunchKernelGGL((k_lu_block_persist<float, 32, false>), dim3(G), dim3(PLR), 0, st, LUB_ARGS(float));
+          else hipLaunchKernelGGL((k_lu_block_persist<float, 32, true>), dim3(G), dim3(PLR), 0, st, LUB_ARGS(float));
+        }
+      } else if (prec == DPL_D) {
+        if (flat) hipLaunchKernelGGL((k_lu_block_persist<double, 64, false>), dim3(G), dim3(PLR), 0, st, LUB_ARGS(double));
+        else hipLaunchKernelGGL((k_lu_block_persist<double, 64, true>), dim3(G), dim3(PLR), 0, st, LUB_ARGS(double));
+      } else {
+        if (flat) hipLaunchKernelGGL((k_lu_block_persist<float, 64, false>), dim3(G), dim3(PLR), 0, st, LUB_ARGS(float));
+        else hipLaunchKernelGGL((k_lu_block_persist<float, 64, true>), dim3(G), dim3(PLR), 0, st, LUB_ARGS(float));
+      }
+#undef LUB_ARGS
       return (int)hipGetLastError();
     }
   }

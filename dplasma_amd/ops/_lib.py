@@ -109,7 +109,7 @@ _SIGS = {
     # random butterfly level (butterfly.hip): prec, side, trans, m, n, size, r, A, si, sj, mb, nb, ld, stream
     "dpl_butterfly": [c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp],
     "dpl_gemm_set_wg_cap": [c_int],
-    "dpl_lu_block_set_kind": [c_int],   # pivoting block kernel: 1 register-resident rows, 0 LDS tile
+    "dpl_lu_block_set_kind": [c_int],   # pivoting block kernel: 0 tagged exchange, 1 register rows, 2 flat, 3 xcd counters
     # distributed pivoting panel (lu_dist.hip): prec, A, ld, m, c0, cend, kbw, tr, diag, lrel, ipiv, ws, cnt,
     # peers, P, me, slot_bytes, epoch0, info, info_base, stream
     "dpl_lu_block_dist": [c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -165,7 +165,7 @@ def load(build_if_missing: bool = True):
         _LIB = _Declared(lib)
         # pivoting block kernel: LDS tile (default) or register-resident rows (DPLASMA_LU_BLOCK=reg,
         # measured slower: profiles/r3_lu_block_reg.txt)
-        _LIB.dpl_lu_block_set_kind(1 if os.environ.get("DPLASMA_LU_BLOCK", "lds") == "reg" else 0)
+        _LIB.dpl_lu_block_set_kind({"reg": 1, "flat": 2, "xcd": 3}.get(os.environ.get("DPLASMA_LU_BLOCK", "lds"), 0))
         return _LIB
 
 

@@ -32,8 +32,18 @@ def main():
             if r:
                 ts.append(e0.elapsed_time(e1) * 1e3)
         ts.sort()
+        # check against torch's LU of the same M x 64 panel (column-major buffer = transposed view)
+        LU, piv = torch.linalg.lu_factor(P0.view(bw, M).T)
+        same_piv = bool(torch.equal(ipiv[:bw].long() + 1, piv.long()))
+        err = float((P.view(bw, M).T - LU).abs().max())
         print(f"M={M:6d} G={-(-M // 256):4d}: {ts[len(ts) // 2]:8.1f} us per 64-column block = "
-              f"{ts[len(ts) // 2] / bw:6.2f} us/column  info={int(info.item())}", flush=True)
+              f"{ts[len(ts) // 2] / bw:6.2f} us/column  info={int(info.item())} pivots_match={same_piv} "
+              f"max|LU-ref|={err:.1e}", flush=True)
+        if not same_piv or err > 1e-8 or int(info.item()) != 0:
+            bad = (ipiv[:bw].long() + 1 != piv.long()).nonzero()
+            print("  first pivot mismatch at column", bad[:4].flatten().tolist(), "ours", ipiv[:8].tolist(),
+                  "ref", (piv[:8] - 1).tolist(), "nan", bool(P.isnan().any()), flush=True)
+            sys.exit(1)
 
 
 if __name__ == "__main__":
