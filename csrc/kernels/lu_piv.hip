@@ -614,45 +614,6 @@ __global__ __launch_bounds__(PLR) void k_lu_block_persist(T* __restrict__ A, int
 // only after it has read every workgroup's column cj + 1, which each of them published after reading cj.
 // Layout (8-byte words): rec[2][G][4] = {value hi, value lo, row}, rows[2][G][PBW * NW], jrow[2][PBW * NW]
 // (NW = 32-bit words per element).
-__device__ inline bool tag_poll(const unsigned long long* p, unsigned tag, unsigned long long& x, int* info) {
-  x = ld_sc1(p);
-  if ((unsigned)x == tag) return true;
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  do {
-    __builtin_amdgcn_s_sleep(1);
-    x = ld_sc1(p);
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ULL) {  // 100 MHz clock: 2 s (grid not co-resident)
-      if (info) atomicExch(info, -1000);
-      return false;
-    }
-  } while ((unsigned)x != tag);
-  return true;
-}
-
-// one element as NW tagged words (payload in the high half) / back, polling stale words
-template <typename T> __device__ inline void tag_put(unsigned long long* p, T x, unsigned tag) {
-  constexpr int NW = sizeof(T) / 4;
-  unsigned u[NW];
-  __builtin_memcpy(u, &x, sizeof(T));
-#pragma unroll
-  for (int q = 0; q < NW; ++q) st_sc1(&p[q], ((unsigned long long)u[q] << 32) | tag);
-}
-template <typename T> __device__ inline T tag_get(const unsigned long long* p, unsigned tag, int* info) {
-  constexpr int NW = sizeof(T) / 4;
-  unsigned long long x[NW];
-#pragma unroll
-  for (int q = 0; q < NW; ++q) x[q] = ld_sc1(&p[q]);
-  unsigned u[NW];
-#pragma unroll
-  for (int q = 0; q < NW; ++q) {
-    if ((unsigned)x[q] != tag) tag_poll(&p[q], tag, x[q], info);
-    u[q] = (unsigned)(x[q] >> 32);
-  }
-  T v;
-  __builtin_memcpy(&v, u, sizeof(T));
-  return v;
-}
-
 template <typename T, int BWT>
 __global__ __launch_bounds__(PLR) void k_lu_block_tag(T* __restrict__ A, int ld, int m, int c0, int cend, int R,
                                                       int* __restrict__ ipiv, unsigned long long* __restrict__ rec,
