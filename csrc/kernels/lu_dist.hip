@@ -7,10 +7,9 @@
 // MI355X design.  Every rank of the panel's process column keeps, in one column-major buffer,
 //   rows [0, tr)      T: a replica of the diagonal tile rows (every pivot destination is one of them),
 //   rows [tr, m)      its own panel rows (panel-relative positions in lrel[]),
-// and factors it with the persistent block kernel of lu_piv.hip (rows LDS-resident), extended by ONE
-// cross-process hand-off per column:
-//   1. local exchange through tagged granules (grid_sync.h, as k_lu_block_tag -- no grid barrier): every WG
-//      reads every WG's {|v|, position} record, so the local winner (|v| desc, position asc) is known to all;
+// and factors it with the persistent block kernel of lu_piv.hip (rows LDS-resident, one grid barrier
+// per column), extended by ONE cross-process hand-off per column:
+//   1. local grid barrier (agent scope): the local winner (|v| desc, position asc) is known to every WG;
 //   2. the WG that owns it writes {|v|, position, the whole kbw-wide row} into slot [parity][me] of
 //      every peer's exchange buffer (IPC-mapped device memory, system-scope stores over xGMI), then
 //      a system-scope release and the slot's epoch flag;
@@ -71,12 +70,11 @@ __device__ inline void block_argmax(double& v, int& i, double* sv, int* si) {
 template <typename T>
 __global__ __launch_bounds__(DLR) void k_lu_block_dist(T* __restrict__ A, int ld, int m, int c0, int cend, int R,
                                                        int kbw, int tr, int diag, const int* __restrict__ lrel,
-                                                       int* __restrict__ ipiv, unsigned long long* __restrict__ rec,
-                                                       unsigned long long* __restrict__ oldrow, unsigned tag0,
+                                                       int* __restrict__ ipiv, double* __restrict__ pval, int* __restrict__ pidx,
+                                                       T* __restrict__ oldrow, int* __restrict__ cnt,
                                                        const unsigned long long* __restrict__ peers, int P, int me,
                                                        int slot_bytes, int epoch0, int* __restrict__ info,
                                                        int info_base) {
-  constexpr int NW = sizeof(T) / 4;
   __shared__ T tile[DBW * DLR];      // column-major: tile[c * R + r]
   __shared__ T prow[DBW];
   __shared__ double sv[DLR];
@@ -114,34 +112,24 @@ __global__ __launch_bounds__(DLR) void k_lu_block_dist(T* __restrict__ A, int ld
     double cv = elig ? piv_mag((double)abs1(tile[cj * R + r])) : -1.0;
     int ci = elig ? g : 0x7fffffff;
     block_argmax(cv, ci, sv, si);
-    // local exchange through tagged granules (grid_sync.h; no grid barrier): record {|v| hi, |v| lo, row}
-    const unsigned tag = tag0 | (unsigned)(cj + 1);
-    const int lpar = cj & 1;
     if (tid == 0) {
-      const unsigned long long vb = (unsigned long long)__double_as_longlong(cv);
-      unsigned long long* rc = rec + ((long long)lpar * G + w) * 4;
-      st_sc1(&rc[0], ((vb >> 32) << 32) | tag);
-      st_sc1(&rc[1], (vb << 32) | tag);
-      st_sc1(&rc[2], ((unsigned long long)(unsigned)ci << 32) | tag);
+      st_sc1(&pval[par * G + w], cv);
+      st_sc1(&pidx[par * G + w], ci);
     }
     // the owner of row j publishes the FULL old row j (block part from LDS, the rest from memory)
     if (j >= rbase && j < rbase + nr) {
       for (int c = tid; c < kbw; c += DLR) {
         const T v = (c >= c0 && c < cend) ? tile[(c - c0) * R + (j - rbase)] : A[j + (long long)c * ld];
-        tag_put<T>(&oldrow[((long long)lpar * kbw + c) * NW], v, tag);
+        st_sc1(&oldrow[(long long)par * kbw + c], v);
       }
     }
+    grid_sync_counter(cnt, (cj + 1) * G, info);
     // ---- 3. local winner (same answer in every WG and every thread): local row index, key = local row
     double lval = -1.0;
     int lw = 0x7fffffff;                        // local row of the local winner (or 0x7fffffff)
     for (int b = tid; b < G; b += DLR) {
-      const unsigned long long* rc = rec + ((long long)lpar * G + b) * 4;
-      unsigned long long x0 = ld_sc1(&rc[0]), x1 = ld_sc1(&rc[1]), x2 = ld_sc1(&rc[2]);
-      if ((unsigned)x0 != tag) tag_poll(&rc[0], tag, x0, info);
-      if ((unsigned)x1 != tag) tag_poll(&rc[1], tag, x1, info);
-      if ((unsigned)x2 != tag) tag_poll(&rc[2], tag, x2, info);
-      const double v = __longlong_as_double((long long)(((x0 >> 32) << 32) | (x1 >> 32)));
-      const int i = (int)(unsigned)(x2 >> 32);
+      const double v = ld_sc1(&pval[par * G + b]);
+      const int i = ld_sc1(&pidx[par * G + b]);
       if (v > lval || (v == lval && i < lw)) { lval = v; lw = i; }
     }
     block_argmax(lval, lw, sv, si);
@@ -216,7 +204,7 @@ __global__ __launch_bounds__(DLR) void k_lu_block_dist(T* __restrict__ A, int ld
       }
       if (dest >= 0 && dest >= rbase && dest < rbase + nr) {
         for (int c = tid; c < kbw; c += DLR) {
-          const T v = tag_get<T>(&oldrow[((long long)lpar * kbw + c) * NW], tag, info);
+          const T v = ld_sc1(&oldrow[(long long)par * kbw + c]);
           if (c >= c0 && c < cend) tile[(c - c0) * R + (dest - rbase)] = v;
           else A[dest + (long long)c * ld] = v;
         }
@@ -245,8 +233,8 @@ __global__ __launch_bounds__(DLR) void k_lu_block_dist(T* __restrict__ A, int ld
 static int g_cus = 0;
 
 DPL_API int dpl_lu_dist_ws_bytes(int kbw) {
-  // tagged records [2 x 256 x 4] words, tagged old row j [2 x kbw x 2] words (8 B each)
-  return 8 * 2 * 256 * 4 + 8 * 2 * kbw * 2 + 64;
+  // pval [2 x 256] doubles, pidx [2 x 256] ints, old row j [2 x kbw] (<= 16 B elements)
+  return 16 * 2 * 256 + 64 + 2 * kbw * 16 + 64;
 }
 
 DPL_API int dpl_lu_dist_slot_bytes(int prec, int kbw) {
@@ -274,18 +262,19 @@ DPL_API int dpl_lu_block_dist(int prec, void* A, int ld, int m, int c0, int cend
   if (G < 1) G = 1;
   const int R = (rows + G - 1) / G;
   if (R > DLR) return -4;   // more local rows than one per thread on every CU
-  (void)cnt;
-  unsigned long long* rec = (unsigned long long*)ws;
-  unsigned long long* old = rec + 2 * 256 * 4;
-  static unsigned launch = 0;                  // local tags: launch << 7 | column + 1 (never 0, never stale)
-  launch = (launch + 1) & 0x1ffffffu;
-  const unsigned tag0 = launch << 7;
+  char* b = (char*)ws;
+  double* pval = (double*)b;
+  int* pidx = (int*)(b + 8LL * 2 * 256);
+  char* old = b + 16LL * 2 * 256 + 64;
+  (void)hipMemsetAsync(cnt, 0, sizeof(int), st);
   if (prec == DPL_D)
     hipLaunchKernelGGL((k_lu_block_dist<double>), dim3(G), dim3(DLR), 0, st, (double*)A, ld, m, c0, cend, R, kbw, tr,
-                       diag, lrel, ipiv, rec, old, tag0, peers, P, me, slot_bytes, epoch0, info, info_base);
+                       diag, lrel, ipiv, pval, pidx, (double*)old, cnt, peers, P, me, slot_bytes,
+                       epoch0, info, info_base);
   else
     hipLaunchKernelGGL((k_lu_block_dist<float>), dim3(G), dim3(DLR), 0, st, (float*)A, ld, m, c0, cend, R, kbw, tr,
-                       diag, lrel, ipiv, rec, old, tag0, peers, P, me, slot_bytes, epoch0, info, info_base);
+                       diag, lrel, ipiv, pval, pidx, (float*)old, cnt, peers, P, me, slot_bytes,
+                       epoch0, info, info_base);
   return (int)hipGetLastError();
 }
 

@@ -938,8 +938,8 @@ DPL_API int dpl_lu_block(int prec, void* A, int ld, int m, int c0, int cend, int
   // persistent single-launch path: real precisions, rows fit one per thread in <= #CU workgroups
   if (g_num_cus == 0) {
     int dev = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (g_num_cus <= 0) g_num_cus = 1;
   }
   const int rows = m - c0;
@@ -980,7 +980,7 @@ DPL_API int dpl_lu_block(int prec, void* A, int ld, int m, int c0, int cend, int
       }
       const bool flat = g_lu_kind == 2;
       if (flat) ctr = cnt;
-      hipMemsetAsync(ctr, 0, flat ? sizeof(int) : 9 * 128, st);
+      (void)hipMemsetAsync(ctr, 0, flat ? sizeof(int) : 9 * 128, st);
 #define LUB_ARGS(T) (T*)A, ld, m, c0, cend, R, ipiv, (T*)cand, pval, pidx, ctr, gval, gidx, info, info_base
       if (g_lu_kind == 1) {
         if (prec == DPL_D)
