@@ -641,13 +641,16 @@ __global__ __launch_bounds__(PLR) void k_lu_block_tag(T* __restrict__ A, int ld,
     const int j = c0 + cj;
     const int par = cj & 1;
     const unsigned tag = tag0 | (unsigned)(cj + 1);
-    // ---- 1. apply column cj-1 (pivot row in prow)
-    if (cj > 0 && own && g >= j) {
+    // ---- 1. apply column cj-1 (pivot row in prow) to column cj only: the search needs nothing more, and the
+    //         rest of the rank-1 update (3b) runs while the record travels
+    const bool upd = cj > 0 && own && g >= j;
+    T l = ST<T>::zero();
+    if (upd) {
       const T d = prow[cj - 1];
-      T l = tile[(cj - 1) * R + r];
+      l = tile[(cj - 1) * R + r];
       if (!is_zero(d)) l = divv(l, d);
       tile[(cj - 1) * R + r] = l;
-      for (int c = cj; c < BW; ++c) tile[c * R + r] = sub(tile[c * R + r], mul(l, prow[c]));
+      tile[cj * R + r] = sub(tile[cj * R + r], mul(l, prow[cj]));
     }
     // ---- 2. local |max| of column cj over rows >= j
     double v = (own && g >= j) ? piv_mag((double)abs1(tile[cj * R + r])) : -1.0;
@@ -671,6 +674,10 @@ __global__ __launch_bounds__(PLR) void k_lu_block_tag(T* __restrict__ A, int ld,
       st_sc1(&rc[1], (vb << 32) | tag);
       st_sc1(&rc[2], ((unsigned long long)(unsigned)vi << 32) | tag);
     }
+    // ---- 3b. the rest of column cj-1's rank-1 update (own row only), then the rows are complete
+    if (upd)
+      for (int c = cj + 1; c < BW; ++c) tile[c * R + r] = sub(tile[c * R + r], mul(l, prow[c]));
+    __syncthreads();
     // candidate row by threads [0, 64), row j by threads [64, 128): one element (NW words) per thread
     if (tid < BW && vi != 0x7fffffff)
       tag_put<T>(&rows[((long long)par * G + w) * (PBW * NW) + tid * NW], tile[tid * R + (vi - rbase)], tag);
