@@ -8,9 +8,12 @@
 // MI355X design:
 //  * The tall panel (m up to 64k rows x NB columns, column-major, one buffer) is factored by a
 //    recursive LU (host-side recursion in dplasma_amd.ops: halves -> laswp + TRSM + MFMA GEMM);
-//    its base case is a column block of <= 64 columns handled by dpl_lu_block, which issues one
-//    launch per column.  Launch j, over every row of the panel (256 rows per workgroup, one row
-//    per thread, coalesced column-major reads):
+//    its base case is a column block of <= 64 columns handled by dpl_lu_block.  Real precisions run
+//    it as ONE persistent launch with the block's rows in LDS and the per-column pivot chosen through
+//    tagged granules (k_lu_block_tag, the default -- see there; the grid-barrier and register variants
+//    stay selectable).  The fallback (complex, or panels taller than 256 rows x #CU) issues one launch
+//    per column.  Launch j, over every row of the panel (256 rows per workgroup, one row per thread,
+//    coalesced column-major reads):
 //      1. applies column j-1: l = a(r, j-1) / a(j-1, j-1); a(r, j-1) = l;
 //         a(r, c) -= l * a(j-1, c) for the block's columns c > j-1   (rank-1 update)
 //      2. computes the workgroup's |max| of column j over its rows,
