@@ -61,11 +61,53 @@ def _spawn_ranks(n: int, cpu: bool) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def race_engines(agree_min, agree_max, build_dtr, run_dtr, check_dtr, run_stream, log=None):
+    """The engine race's decision, with every collective injected (agree_min / agree_max: all-reduce of one float
+    over the ranks): build the DTR, run it twice (warm, then timed and checked), time the stream engine twice, and
+    keep the DTR only if it built, ran and passed the check on EVERY rank and was faster (max over ranks).  A
+    failure on one rank -- an exception from build_dtr / run_dtr / check_dtr -- is agreed, never skipped, so
+    every rank takes the same branch and no collective is left unmatched.  Returns ("dtr" | "stream", t_dtr,
+    t_stream, dtr_handle)."""
+    tpd, ok = None, 1.0
+    try:
+        tpd = build_dtr()
+    except Exception as e:   # noqa: BLE001 -- any build failure means: keep the stream engine
+        if log:
+            log(f"distributed DTR unavailable ({e})")
+        ok = 0.0
+    if agree_min(ok) < 1:
+        return "stream", None, None, None
+    t_d = float("inf")
+    try:
+        run_dtr(tpd, poison=False)
+        t_d = run_dtr(tpd, poison=True)
+    except Exception as e:   # noqa: BLE001 -- a drained launch: the taskpool agreed the failure across ranks
+        if log:
+            log(f"distributed DTR failed ({e})")
+        ok = 0.0
+    if ok:
+        try:
+            ok = 1.0 if check_dtr(tpd) else 0.0
+        except Exception as e:   # noqa: BLE001
+            if log:
+                log(f"distributed DTR check failed ({e})")
+            ok = 0.0
+    run_stream()
+    t_s = run_stream()
+    ok = agree_min(ok)
+    t_d, t_s = agree_max(t_d if ok else 1e30), agree_max(t_s)
+    if ok and t_d < t_s:
+        return "dtr", t_d, t_s, tpd
+    return "stream", (t_d if ok else None), t_s, tpd
+
+
 def _choose_engine(ctx, uplo, A, A0, tp, args):
     """N > 1: race the distributed device task runtime (models/potrf_dtr_dist.py, push-scheduled, in-kernel
     sends over the IPC-mapped peers; modelled at 75 % of 8-GPU peak at 2x4 64k, profiles/r5_dtr_dist_emulation.txt)
     against the stream engine in the untimed warmup, and keep it only if it builds, factors correctly (residual
     check) and is faster on every rank -- all three agreed across ranks, so every rank picks the same engine.
+    The checked run starts from POISONED receive slots and peer W blocks (NaN): a strip read before its bytes
+    crossed xGMI fails the check instead of reproducing the previous run's bit-identical values.
     DPLASMA_BENCH_DIST_ENGINE=stream skips the race."""
     import torch.distributed as dist
 
@@ -81,9 +123,11 @@ def _choose_engine(ctx, uplo, A, A0, tp, args):
         dist.all_reduce(t, op=op)
         return float(t.item())
 
-    def timed(t):
+    def timed(t, poison=False):
         A.data.copy_(A0)
         t.info.zero_()
+        if poison:
+            t.poison()
         ctx.sync()
         ctx.barrier()
         ctx.sync()
@@ -93,35 +137,23 @@ def _choose_engine(ctx, uplo, A, A0, tp, args):
         el = time.perf_counter() - t0
         t.complete(ctx)
         return el
-    tpd, ok = None, 1.0
-    try:
-        tpd = potrf_dtr_dist.potrf_dtr_dist_New(ctx, uplo, A)
-    except Exception as e:   # noqa: BLE001 -- any build failure means: keep the stream engine
-        print(f"rank {ctx.rank}: distributed DTR unavailable ({e})", file=sys.stderr)
-        ok = 0.0
-    if agree(ok, dist.ReduceOp.MIN) < 1:
-        return tp, "stream"
-    t_d = float("inf")
-    try:
-        timed(tpd)
-        t_d = timed(tpd)
-    except RuntimeError as e:   # a drained launch: the taskpool agreed the failure across ranks
-        print(f"rank {ctx.rank}: distributed DTR failed ({e})", file=sys.stderr)
-        ok = 0.0
-    if ok:
+
+    def check(_t):
         A_orig = A.like()
         A_orig.data.copy_(A0)
         good, _ = dp.check_potrf(ctx, uplo, A, A_orig)
         del A_orig
-        ok = 1.0 if good else 0.0
-    timed(tp)
-    t_s = timed(tp)
-    ok = agree(ok, dist.ReduceOp.MIN)
-    t_d, t_s = agree(t_d if ok else 1e30, dist.ReduceOp.MAX), agree(t_s, dist.ReduceOp.MAX)
+        return good
+
+    engine, t_d, t_s, tpd = race_engines(
+        lambda v: agree(v, dist.ReduceOp.MIN), lambda v: agree(v, dist.ReduceOp.MAX),
+        lambda: potrf_dtr_dist.potrf_dtr_dist_New(ctx, uplo, A), timed, check, lambda: timed(tp),
+        log=lambda m: print(f"rank {ctx.rank}: {m}", file=sys.stderr))
     if ctx.rank == 0:
-        print(f"bench: warmup race -- distributed DTR {'%.1f ms' % (t_d * 1e3) if ok else 'not usable'}, "
-              f"stream engine {t_s * 1e3:.1f} ms", file=sys.stderr)
-    if ok and t_d < t_s:
+        print(f"bench: warmup race -- distributed DTR {'%.1f ms' % (t_d * 1e3) if t_d else 'not usable'}, "
+              f"stream engine {'%.1f ms' % (t_s * 1e3) if t_s else '-'} (checked run from poisoned receive slots)",
+              file=sys.stderr)
+    if engine == "dtr":
         return tpd, "dtr"
     potrf_dtr_dist.release_all()
     return tp, "stream"
@@ -213,7 +245,9 @@ def main():
     ctx.barrier()
     ctx.sync()
     total = 0.0
-    for _ in range(args.steps):
+    # DPLASMA_BENCH_STEPLOG=1: every rank prints each timed step's time (stderr) -- the per-step view behind the max
+    steplog = os.environ.get("DPLASMA_BENCH_STEPLOG") == "1"
+    for si in range(args.steps):
         A.data.copy_(A0)
         tp.info.zero_()
         ctx.sync()
@@ -224,7 +258,10 @@ def main():
         ctx.sync()
         ctx.barrier()
         ctx.sync()
-        total += time.perf_counter() - t0
+        dt = time.perf_counter() - t0
+        total += dt
+        if steplog:
+            print(f"bench: rank {rank} step {si}: {dt * 1e3:.1f} ms", file=sys.stderr)
     info = tp.complete(ctx)
     el = torch.tensor([total], dtype=torch.float64, device=ctx.device)
     if world > 1:

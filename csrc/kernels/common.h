@@ -153,15 +153,16 @@ static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 // stream and hipStreamSynchronize -- not hipMemset on the null stream + hipDeviceSynchronize, which
 // a rocprofv3 trace showed completing after a later kernel on a non-blocking stream had started
 // (profiles/r4_potrf_rb_race.txt).
-static inline hipError_t dpl_zero_sync(void* p, size_t bytes) {
+static inline hipError_t dpl_fill_sync(void* p, int byte, size_t bytes) {
   hipStream_t s = nullptr;
   hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
   if (e != hipSuccess) return e;
-  e = hipMemsetAsync(p, 0, bytes, s);
+  e = hipMemsetAsync(p, byte & 255, bytes, s);
   const hipError_t e2 = hipStreamSynchronize(s);
   (void)hipStreamDestroy(s);
   return e != hipSuccess ? e : e2;
 }
+static inline hipError_t dpl_zero_sync(void* p, size_t bytes) { return dpl_fill_sync(p, 0, bytes); }
 
 // Pivot-search magnitude: |x| with NaN mapped to 0, so an eligible row always beats the "no candidate" marker
 // (-1) and a NaN column still yields an in-range pivot (the row j itself) instead of the sentinel index.

@@ -331,9 +331,11 @@ DPL_API int dpl_memcpy_sync(void* dst, const void* src, long long bytes) {
   return (int)hipDeviceSynchronize();
 }
 
+// (value: any byte -- 0xFF fills doubles with NaN: the poisoned receive slots of bench.py's engine race)
 DPL_API int dpl_memset_sync(void* ptr, int value, long long bytes) {
-  if (value != 0) return -2;
-  return (int)dpl_zero_sync(ptr, (size_t)bytes);
+  if (value < 0 || value > 255) return -2;
+  if (bytes <= 0) return 0;
+  return (int)dpl_fill_sync(ptr, value, (size_t)bytes);
 }
 
 DPL_API int dpl_xchg_open(const void* handle, void** ptr) {

@@ -431,32 +431,46 @@ class _Peers:
         self.lib = lib
         self.local, self.opened = [], []
         hb = int(lib.dpl_ipc_handle_bytes())
-        mine = []
+        mine, err = [], None
+        # A failure on one rank (allocation, mapping) is agreed through the gathers below, never raised before
+        # them: every rank reaches the same collectives and raises together, and close() (collective) runs on
+        # every rank because the object is registered before anything can raise.
+        _PEERS.append(self)
         for nbytes, cached in specs:
             h = (ctypes.c_char * hb)()
             ptr = ctypes.c_void_p()
             rc = lib.dpl_ipc_alloc(int(nbytes), int(cached), ctypes.byref(ptr), h)
             if rc != 0:
-                raise RuntimeError(f"distributed DTR: IPC allocation of {nbytes} bytes failed ({rc})")
+                err = f"rank {ctx.rank}: IPC allocation of {nbytes} bytes failed ({rc})"
+                break
             self.local.append(ptr.value)
             mine.append(bytes(h))
         allh = [None] * ctx.world
-        dist.all_gather_object(allh, mine)
+        dist.all_gather_object(allh, (err, mine))
+        errs = [e for e, _ in allh if e]
+        if errs:
+            raise RuntimeError("distributed DTR: " + "; ".join(errs))
         self.ptrs = []          # [buffer][rank] -> device pointer in this process
         for b in range(len(specs)):
             row = []
             for r in range(ctx.world):
-                if r == ctx.rank:
-                    row.append(self.local[b])
+                if r == ctx.rank or err:
+                    row.append(self.local[b] if r == ctx.rank else 0)
                     continue
                 p = ctypes.c_void_p()
-                rc = lib.dpl_xchg_open(ctypes.create_string_buffer(allh[r][b], hb), ctypes.byref(p))
+                rc = lib.dpl_xchg_open(ctypes.create_string_buffer(allh[r][1][b], hb), ctypes.byref(p))
                 if rc != 0:
-                    raise RuntimeError(f"distributed DTR: cannot map rank {r}'s buffer {b} ({rc})")
+                    err = f"rank {ctx.rank}: cannot map rank {r}'s buffer {b} ({rc})"
+                    row.append(0)
+                    continue
                 self.opened.append(p.value)
                 row.append(p.value)
             self.ptrs.append(row)
-        _PEERS.append(self)
+        errs = [None] * ctx.world
+        dist.all_gather_object(errs, err)
+        errs = [e for e in errs if e]
+        if errs:
+            raise RuntimeError("distributed DTR: " + "; ".join(errs))
 
     def close(self):
         import ctypes
@@ -640,6 +654,27 @@ def potrf_dtr_dist_New(ctx, uplo: int, A, info_out=None):
         _lib.check(lib.dpl_dtr_potrf(args_d.data_ptr(), nwg, _lib.stream_ptr()), "dtr_potrf (distributed)")
 
     tp.task("DTR_POTRF", "update", f_run)
+
+    def poison():
+        """NaN-fill (0xFF bytes) this rank's receive slots and every W_k it does not compute itself, so a consumer
+        that reads a peer's strip or W block before it has arrived gets NaN -- a residual failure -- instead of the
+        bit-identical values an earlier factorisation of the same matrix left there (bench.py's engine race).  W_k
+        of a diagonal tile this rank owns stays as it is: w_column writes its upper blocks only, the zeros below
+        the diagonal come from the allocation."""
+        torch.cuda.current_stream().synchronize()
+        _lib.check(lib.dpl_memset_sync(recv_p[me], 0xFF, plan.recv_elems(me) * 8), "dtr poison recv")
+        blk = NBT * NBT * 8
+        k = 0
+        while k < nt:
+            if A.rank_of(k, k) == me:
+                k += 1
+                continue
+            k1 = k
+            while k1 < nt and A.rank_of(k1, k1) != me:
+                k1 += 1
+            _lib.check(lib.dpl_memset_sync(W_p[me] + k * blk, 0xFF, (k1 - k) * blk), "dtr poison W")
+            k = k1
+    tp.poison = poison
 
     def _done():
         v = info.to(torch.int64)

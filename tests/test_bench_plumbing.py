@@ -54,3 +54,60 @@ def test_bench_refuses_missing_gpus():
     assert r.returncode != 0
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert "GPU" in r.stderr
+
+
+def _race_worker(rank, world, scenario):
+    """bench.race_engines on gloo ranks with injected failures: every rank must take the same branch."""
+    import importlib.util
+
+    import torch
+    import torch.distributed as dist
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+
+    def agree(v, op):
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        dist.all_reduce(t, op=op)
+        return float(t.item())
+    calls = {"poisoned": 0, "stream": 0}
+
+    def build():
+        if scenario == "build_fails" and rank == 1:
+            raise RuntimeError("IPC allocation failed")
+        return "dtr-handle"
+
+    def run_dtr(tpd, poison=False):
+        assert tpd == "dtr-handle"
+        calls["poisoned"] += int(poison)
+        if scenario == "launch_fails" and rank == world - 1:
+            raise RuntimeError("potrf: distributed device task runtime failure (info -1000)")
+        # rank 0 slower than the stream engine in "dtr_slow_on_one_rank": the MAX over ranks decides
+        return 5.0 if (scenario == "dtr_slow_on_one_rank" and rank == 0) else 1.0
+
+    def check(tpd):
+        # a stale cross-GPU read shows up as NaN -> residual failure on that rank only
+        return not (scenario == "check_fails" and rank == 1)
+
+    def run_stream():
+        calls["stream"] += 1
+        return 2.0
+    eng, t_d, t_s, _ = bench.race_engines(lambda v: agree(v, dist.ReduceOp.MIN), lambda v: agree(v, dist.ReduceOp.MAX),
+                                          build, run_dtr, check, run_stream)
+    dist.barrier()   # every collective matched: this returns on every rank
+    return eng, calls
+
+
+@pytest.mark.parametrize("scenario,expect", [("ok", "dtr"), ("build_fails", "stream"), ("launch_fails", "stream"),
+                                             ("check_fails", "stream"), ("dtr_slow_on_one_rank", "stream")])
+def test_bench_engine_race_falls_back(scenario, expect):
+    """The N > 1 warmup race keeps the distributed DTR only if it built, ran and passed the (poisoned-slot)
+    residual check on EVERY rank and was faster on the slowest rank; one rank's failure sends all to `stream`."""
+    from helpers import run_distributed
+    out = run_distributed(_race_worker, 3, scenario)
+    engines = {r: v[0] for r, v in out.items()}
+    assert set(engines.values()) == {expect}, engines
+    for r, (_, calls) in out.items():
+        if scenario not in ("build_fails", "launch_fails"):
+            assert calls["poisoned"] == 1      # the checked run starts from poisoned receive slots
+        assert calls["stream"] == (2 if scenario != "build_fails" else 0)
