@@ -132,6 +132,10 @@ struct DtrArgs {
   int* qslot[MAXR];         // rank r's ring slots: task id + 1, 0 = reserved but not yet written (reset per launch)
   int* done;                // tasks completed by this launch
   unsigned long long* rdy;  // emulation: per task, when its last input becomes visible (max over predecessors)
+  // optional hazard probe (DPLASMA_DTR_PROBE=1, the two-workgroups-per-CU hunt, profiles/r6_dtr_probe.txt):
+  // [0] record count, [8, 8 + 4 nt * nt) per strip (4 i + r, k) the epoch stamped by its TRSM before its release,
+  // then 8-word records of every diagonal-tile update that saw a strip operand stale (see probe_strips)
+  long long* probe;
 };
 
 constexpr int NBT = 512;    // tile size
@@ -394,6 +398,80 @@ struct TaskU {
   }
 };
 
+// Hazard probe of one strip operand (thread 0): its TRSM's stamp must be this launch's epoch, and two elements of it
+// -- row 0 of the strip in column 511 (the in-place TRSM's first-written block) and column 0 (its last) -- must
+// read the same through this CU's caches (a plain load) and from memory (a system-scope load).  A mismatch is
+// recorded: {task, k << 16 | strip << 8 | phase << 4 | kind, wg << 8 | xcd, stamp, plain511, mem511, plain0, mem0},
+// kind 1 = stamp not this epoch (the task started before the TRSM's release), 2 = stale cache line.
+__device__ __attribute__((noinline)) void probe_strip(const DtrArgs* __restrict__ gp, int t, int rk, int ti, int k,
+                                                      int strip, int phase) {
+  const DtrArgs& g = *gp;
+  long long* pr = g.probe;
+  const int nt = g.nt;
+  const long long st = __hip_atomic_load(pr + 8 + (long long)(4 * ti + strip) * nt + k, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+  const long long* tab = g.tab + (size_t)rk * nt * nt;
+  const double* base = g.A[rk] + tab[ti + (long long)k * nt] + 128 * strip;
+  const double* p511 = base + 511LL * g.ld;
+  const double n511 = *(volatile const double*)p511, n0 = *(volatile const double*)base;
+  const double m511 = __hip_atomic_load(const_cast<double*>(p511), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const double m0 = __hip_atomic_load(const_cast<double*>(base), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const int kind = st != g.epoch ? 1 : ((__double_as_longlong(n511) != __double_as_longlong(m511) ||
+                                         __double_as_longlong(n0) != __double_as_longlong(m0)) ? 2 : 0);
+  if (!kind) return;
+  const long long q = atomicAdd((unsigned long long*)pr, 1ULL);
+  if (q >= 4096) return;
+  long long* rec = pr + 8 + 4LL * nt * nt + 8 * q;
+  rec[0] = t;
+  rec[1] = ((long long)k << 16) | (strip << 8) | (phase << 4) | kind;
+  rec[2] = ((long long)blockIdx.x << 8) | xcc_id();
+  rec[3] = st;
+  rec[4] = __double_as_longlong(n511);
+  rec[5] = __double_as_longlong(m511);
+  rec[6] = __double_as_longlong(n0);
+  rec[7] = __double_as_longlong(m0);
+}
+
+// sub-tile (r, c) of diagonal tile (i, i): its stamp (epoch << 12 | panel the last update run ended at) and one element
+// through the caches vs memory.  want: the expected stamp (< 0: no check); kinds 3 / 4 (an update's C operand) and
+// 5 / 6 (a POTRF block's input), stamp / cache.
+__device__ __attribute__((noinline)) void probe_sub(const DtrArgs* __restrict__ gp, int t, int rk, int i, int r, int c,
+                                                    long long want, int row, int kst) {
+  const DtrArgs& g = *gp;
+  long long* pr = g.probe;
+  const int nt = g.nt;
+  long long* sst = pr + 8 + 4LL * nt * nt;
+  const long long st = __hip_atomic_load(sst + ((long long)i * nt + i) * 16 + 4 * r + c, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+  const long long* tab = g.tab + (size_t)rk * nt * nt;
+  const double* e = g.A[rk] + tab[i + (long long)i * nt] + row + 128LL * c * g.ld;
+  const double n0 = *(volatile const double*)e;
+  const double m0 = __hip_atomic_load(const_cast<double*>(e), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const int kind = (want >= 0 && st != want) ? kst : (__double_as_longlong(n0) != __double_as_longlong(m0) ? kst + 1 : 0);
+  if (!kind) return;
+  const long long q = atomicAdd((unsigned long long*)pr, 1ULL);
+  if (q >= 4096) return;
+  long long* rec = pr + 8 + 20LL * nt * nt + 8 * q;
+  rec[0] = t;
+  rec[1] = ((long long)i << 16) | ((4 * r + c) << 8) | kind;
+  rec[2] = ((long long)blockIdx.x << 8) | xcc_id();
+  rec[3] = st;
+  rec[4] = __double_as_longlong(n0);
+  rec[5] = __double_as_longlong(m0);
+  rec[6] = want;
+  rec[7] = row;
+}
+
+__device__ inline void probe_upd(const DtrArgs* __restrict__ gp, int t, int rk, int i, int j, int r, int c, int k0,
+                                 int nk, int phase) {
+  if (threadIdx.x != 0) return;
+  for (int q = 0; q < nk; ++q) {
+    probe_strip(gp, t, rk, i, k0 + q, r, phase);
+    if (c != r) probe_strip(gp, t, rk, j, k0 + q, c, phase);
+  }
+  if (phase == 0) probe_sub(gp, t, rk, i, r, c, k0 > 0 ? ((long long)gp->epoch << 12) + k0 : -1, 128 * r, 3);
+}
+
 // Task bodies: each is a separate (non-inlined) function, so its registers are allocated on its own
 // -- the GEMM body inlined into the task loop spilled (the capped persistent k_gemm_full spills the
 // same way: hipcc -Rpass-analysis=kernel-resource-usage, profiles/r4_dtr_regs.txt).
@@ -406,9 +484,12 @@ __device__ __attribute__((noinline)) void run_upd(const DtrArgs* __restrict__ gp
   ks.nt = u.nt, ks.i = u.i, ks.j = u.j, ks.r = u.r, ks.c = u.c, ks.k0 = u.k0;
   ks.init(u.nk);
   const int uplo = (u.i == u.j && u.r == u.c) ? 1 : 0;
+  const bool prb = g.probe != nullptr && u.i == u.j;
+  if (prb) probe_upd(gp, rfl(t), rfl(rk), u.i, u.j, u.r, u.c, u.k0, u.nk, 0);
   gemm_subtile<double, false, true>(g_lds, ks, u.nk, 0, 0, uplo, -1.0, u.A, (int)u.ld, u.A, (int)u.ld, 1.0,
                                     u.A + tile_at(u.tab, u.nt, u.i, u.j) + 128 * u.r + 128LL * u.c * u.ld, (int)u.ld,
                                     -1, (rfl(g.flags) & 16) != 0);
+  if (prb) probe_upd(gp, rfl(t), rfl(rk), u.i, u.j, u.r, u.c, u.k0, u.nk, 1);
 }
 
 __device__ __attribute__((noinline)) void run_trsm(const DtrArgs* __restrict__ gp, int t, int rk) {
@@ -440,6 +521,9 @@ __device__ __attribute__((noinline)) void run_potrf(const DtrArgs* __restrict__ 
   ws.ticket = nullptr;
   ws.tbase = 0;
   const long long* tab = g.tab + (size_t)rk * g.nt * g.nt;
+  if (g.probe && threadIdx.x == 0)   // hazard probe: the row block's input sub-tiles (final versions, fresh)
+    for (int c = 0; c <= b / 4; ++c)
+      probe_sub(gp, t, rk, k, b / 4, c, k > 0 ? ((long long)g.epoch << 12) + k : -1, 32 * b, 5);
   rb_tile_body<true>(g.A[rk] + tile_at(tab, g.nt, k, k), NBT, (int)g.ld, g.info, k * NBT, ws, g.epoch, nullptr, b,
                      g_lds, g_lds + BLK);
   __syncthreads();
@@ -687,6 +771,12 @@ __global__ __launch_bounds__(256, 2) void k_dtr_potrf(const DtrArgs* __restrict_
       if (emul(g)) tr[3] = (long long)due;
       else atomicAdd((unsigned long long*)(tr + 3), 1ULL);
     }
+    if (tid == 0 && g.probe && tk.type == T_TRSM)   // hazard probe: the strip's stamp, ordered by the release below
+      __hip_atomic_store(g.probe + 8 + (long long)(4 * tk.i + tk.r) * g.nt + tk.k0, (long long)g.epoch,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0 && g.probe && tk.type == T_UPD && tk.i == tk.j)   // ... and a diagonal sub-tile's version stamp
+      __hip_atomic_store(g.probe + 8 + 4LL * g.nt * g.nt + ((long long)tk.i * g.nt + tk.i) * 16 + 4 * tk.r + tk.c,
+                         ((long long)g.epoch << 12) + tk.k0 + tk.nk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid == 0 && tk.inc >= 0) {
       const bool remote = tk.type == T_SEND || tk.type == T_SENDW;
       const int tr_ = remote ? tk.j : rk;
@@ -870,6 +960,12 @@ __global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ ga
       const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)due), hi = __builtin_amdgcn_readfirstlane((unsigned)(due >> 32));
       due = ((unsigned long long)hi << 32) | lo;
     }
+    if (tid == 0 && g.probe && tk.type == T_TRSM)   // hazard probe: the strip's stamp, ordered by the release below
+      __hip_atomic_store(g.probe + 8 + (long long)(4 * tk.i + tk.r) * g.nt + tk.k0, (long long)g.epoch,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0 && g.probe && tk.type == T_UPD && tk.i == tk.j)   // ... and a diagonal sub-tile's version stamp
+      __hip_atomic_store(g.probe + 8 + 4LL * g.nt * g.nt + ((long long)tk.i * g.nt + tk.i) * 16 + 4 * tk.r + tk.c,
+                         ((long long)g.epoch << 12) + tk.k0 + tk.nk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid < 64) {
       if (sy) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -923,7 +1019,7 @@ DPL_API long long dpl_dtr_field(const char* name) {
   DTR_FIELD(vis) DTR_FIELD(link) DTR_FIELD(bw_bpt) DTR_FIELD(lat_t) DTR_FIELD(Mw) DTR_FIELD(Sw) DTR_FIELD(Lp)
   DTR_FIELD(Wp) DTR_FIELD(prog) DTR_FIELD(info) DTR_FIELD(trace) DTR_FIELD(ntask) DTR_FIELD(nclass) DTR_FIELD(pend)
   DTR_FIELD(succ_off) DTR_FIELD(succ) DTR_FIELD(ring_of) DTR_FIELD(town) DTR_FIELD(qbase) DTR_FIELD(qctl)
-  DTR_FIELD(qslot) DTR_FIELD(done) DTR_FIELD(rdy)
+  DTR_FIELD(qslot) DTR_FIELD(done) DTR_FIELD(rdy) DTR_FIELD(probe)
   if (!std::strcmp(name, "size")) return (long long)sizeof(DtrArgs);
   if (!std::strcmp(name, "task")) return (long long)sizeof(DtrTask);
   if (!std::strcmp(name, "MAXB")) return MAXB;

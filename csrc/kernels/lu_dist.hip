@@ -231,6 +231,15 @@ __global__ __launch_bounds__(DLR) void k_lu_block_dist(T* __restrict__ A, int ld
 }
 
 static int g_cus = 0;
+static int g_maxwg = 0;   // > 0: at most this many workgroups per launch (a rank confined to a CU-masked stream)
+
+// Cap the persistent panel's grid (0: one workgroup per CU of the device).  A launch on a CU-masked stream must not
+// exceed the CUs of its mask: its grid barrier needs every workgroup co-resident (tools/gpu/lu_xlat_probe.py runs two
+// emulated ranks on the two halves of one GPU).
+DPL_API int dpl_lu_dist_set_maxwg(int n) {
+  g_maxwg = n > 0 ? n : 0;
+  return 0;
+}
 
 DPL_API int dpl_lu_dist_ws_bytes(int kbw) {
   // pval [2 x 256] doubles, pidx [2 x 256] ints, old row j [2 x kbw] (<= 16 B elements)
@@ -256,7 +265,8 @@ DPL_API int dpl_lu_block_dist(int prec, void* A, int ld, int m, int c0, int cend
     if (g_cus <= 0) g_cus = 1;
   }
   const int rows = m - c0;
-  const int gmax = g_cus < 256 ? g_cus : 256;
+  int gmax = g_cus < 256 ? g_cus : 256;
+  if (g_maxwg > 0 && g_maxwg < gmax) gmax = g_maxwg;
   int G = (rows + DLR - 1) / DLR;
   if (G > gmax) G = gmax;
   if (G < 1) G = 1;

@@ -1084,3 +1084,99 @@ DPL_API int dpl_rows_permute(int prec, void* A, int ld, int mb, int r0, const lo
                                     coloff, ncols, nct, nb, dst, src, cnt, info));
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------- cross-process-row interchanges (P > 1)
+// The reference's SWAP_COLLECT / SWAP_SND (src/zgetrf_ptgpanel.jdf:825-984): only the moved rows whose source and
+// destination live on DIFFERENT process rows travel, point to point between those two rows of the process column.
+// Every rank holds the same net move list (identical pivots), so every rank classifies every move the same way:
+//   pack   (s_own == me, d_own == q != me): my staged source row goes into my send buffer for q,
+//   unpack (d_own == me, s_own == q != me): q's row arrives in my receive buffer from q,
+// at the move's ordinal inside its (source row, destination row) class -- computed identically on both sides, so
+// no index travels with the rows.  A class holds at most kb moves (the moves either fill the top block's kb rows or
+// empty them), so the buffers are kb rows wide.  xo[t] = (1 << 30 | q << 16 | ord) for pack, (1 << 29 | q << 16 |
+// ord) for unpack, -1 for a move that stays on this process row (or is not mine).
+__device__ inline int xscan_1024(bool f, int* wsum) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long b = __builtin_amdgcn_ballot_w64(f);
+  const int in = __builtin_popcountll(b & ((1ULL << lane) - 1ULL));
+  if (lane == 0) wsum[w] = __builtin_popcountll(b);
+  __syncthreads();
+  int off = 0;
+  for (int q = 0; q < w; ++q) off += wsum[q];
+  __syncthreads();
+  return off + in;
+}
+
+__global__ __launch_bounds__(1024) void k_rows_xord(const int* __restrict__ dst, const int* __restrict__ src,
+                                                    const int* __restrict__ cnt, int r0, int mb,
+                                                    const int* __restrict__ prow, int nrt, int me, int P, int ldx,
+                                                    int* __restrict__ xo, int* __restrict__ info) {
+  __shared__ int wsum[16];
+  const int n = cnt[0];
+  const int t = threadIdx.x;
+  int so = -1, dd = -1;
+  if (t < n) {
+    const int Rs = r0 + src[t], Rd = r0 + dst[t];
+    if (Rs >= 0 && Rd >= 0 && Rs / mb < nrt && Rd / mb < nrt) {
+      so = prow[Rs / mb];
+      dd = prow[Rd / mb];
+    } else {
+      report_bad_pivot(info);
+    }
+  }
+  int out = -1;
+  for (int q = 0; q < P; ++q) {   // uniform loop: every thread takes part in every scan
+    if (q == me) continue;
+    const bool fp = so == me && dd == q;
+    const int op = xscan_1024(fp, wsum);
+    const bool fu = dd == me && so == q;
+    const int ou = xscan_1024(fu, wsum);
+    if (fp) out = op < ldx ? ((1 << 30) | (q << 16) | op) : -1;
+    if (fu) out = ou < ldx ? ((1 << 29) | (q << 16) | ou) : -1;
+    if ((fp && op >= ldx) || (fu && ou >= ldx)) report_bad_pivot(info);
+  }
+  xo[t] = out;
+}
+
+// pack: bufs[q][ord + c ldx] = tmp[t + c ldb]; unpack: tmp[t + c ldb] = bufs[q][ord + c ldx] (W columns).  Lanes run
+// along the move list, the 4 waves of a workgroup over columns (k_rows_move's shape).
+template <typename T, bool PACK>
+__global__ __launch_bounds__(256) void k_rows_xcopy(T* __restrict__ tmp, int ldb, int W, const int* __restrict__ xo,
+                                                    const int* __restrict__ cnt, T* const* __restrict__ bufs, int ldx) {
+  const int n = cnt[0];
+  if (blockIdx.y * 64 >= n) return;
+  const int t = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int x = t < n ? xo[t] : -1;
+  const bool act = x >= 0 && ((x >> (PACK ? 30 : 29)) & 1);
+  if (__builtin_amdgcn_ballot_w64(act) == 0) return;
+  const int q = (x >> 16) & 0x1fff, o = x & 0xffff;
+  T* b = act ? bufs[q] : nullptr;
+  for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < W; c += gridDim.x * 4) {
+    if (!act) continue;
+    if (PACK) b[o + (long long)c * ldx] = tmp[t + (long long)c * ldb];
+    else tmp[t + (long long)c * ldb] = b[o + (long long)c * ldx];
+  }
+}
+
+DPL_API int dpl_rows_xord(const int* dst, const int* src, const int* cnt, int r0, int mb, const int* prow, int nrt,
+                          int me, int P, int ldx, int* xo, int* info, hipStream_t st) {
+  if (P < 2 || P > 8192 || ldx <= 0 || ldx > 65535) return -3;
+  hipLaunchKernelGGL(k_rows_xord, dim3(1), dim3(1024), 0, st, dst, src, cnt, r0, mb, prow, nrt, me, P, ldx, xo, info);
+  return (int)hipGetLastError();
+}
+
+DPL_API int dpl_rows_xcopy(int prec, int pack, void* tmp, int ldb, int W, const int* xo, const int* cnt, int maxcnt,
+                           void* const* bufs, int ldx, hipStream_t st) {
+  if (W <= 0 || maxcnt <= 0) return 0;
+  if (maxcnt > 1024) return -3;
+  const int gx = (W + 3) / 4 > 2048 ? 2048 : (W + 3) / 4;
+  dim3 g(gx, (maxcnt + 63) / 64);
+  if (pack) {
+    DISPATCH(prec, hipLaunchKernelGGL((k_rows_xcopy<T, true>), g, dim3(256), 0, st, (T*)tmp, ldb, W, xo, cnt,
+                                      (T* const*)bufs, ldx));
+  } else {
+    DISPATCH(prec, hipLaunchKernelGGL((k_rows_xcopy<T, false>), g, dim3(256), 0, st, (T*)tmp, ldb, W, xo, cnt,
+                                      (T* const*)bufs, ldx));
+  }
+  return (int)hipGetLastError();
+}

@@ -185,7 +185,11 @@ class _GetrfDev:
         # 28.2 -> 27.1 TF/s, 64k 48.1 -> 47.2 TF/s with look-ahead on
         # (lookahead=True: a caller that issues PANEL(k+1) beside REST(k) itself -- the hybrid LU-QR -- needs the
         # parity-alternating panel buffers whatever the environment says)
-        self.lookahead = (os.environ.get("DPLASMA_LU_LOOKAHEAD", "0") == "1") if lookahead is None else bool(lookahead)
+        # P > 1 with the point-to-point interchanges: look-ahead on by default -- the distributed panel's per-column
+        # cross-process hand-offs are latency, not CU time, so they belong beside the bulk update (tools/replay_lu.py)
+        la_def = "1" if (g.P > 1 and pivot and os.environ.get("DPLASMA_LU_PANEL", "dist") != "percol"
+                         and os.environ.get("DPLASMA_LU_XROWS", "p2p") != "allreduce") else "0"
+        self.lookahead = (os.environ.get("DPLASMA_LU_LOOKAHEAD", la_def) == "1") if lookahead is None else bool(lookahead)
         self.panel_bw = panel_bw   # base block width of the recursive panel (None: ops.LU_BW)
         self.pbufs = [torch.zeros(max(1, A.m * nb), dtype=A.dtype, device=dev)
                       for _ in range(2 if self.lookahead else 1)]
@@ -244,6 +248,38 @@ class _GetrfDev:
             self.tmp_l = torch.zeros_like(self.tmp)
             self.ev_side = [None, None]
         self.nleft = [bisect.bisect_left(lcols, k) for k in range(min(A.mt, A.nt))]
+        # P > 1 (DPLASMA_LU_XROWS=p2p, the default): the interchanges move only the rows whose source and destination
+        # lie on different process rows, point to point inside the process column (the reference's SWAP_COLLECT /
+        # SWAP_SND, src/zgetrf_ptgpanel.jdf:825-984), classified on the device from the move list (no host pivots),
+        # and split by urgency: the next panel's column (panel stream, urgent communicator), the rest of the trailing
+        # columns (update stream) and the already factored columns (low-priority side stream -- only the final L
+        # needs them).  "allreduce" keeps round 5's summed exchange of the whole 2 NB-row staging buffer.
+        self.xmode = (g.P > 1 and pivot and not self.percol and bool(lcols) and
+                      os.environ.get("DPLASMA_LU_XROWS", "p2p") != "allreduce")
+        if self.xmode:
+            self.xpeers = [q for q in range(g.P) if q != A.myrow]
+            self.prow_t = torch.tensor([g.prow(m + A.it0) for m in range(A.mt)], dtype=torch.int32, device=dev)
+            self.xo = torch.full((2, 2 * nb), -1, dtype=torch.int32, device=dev)
+            wtot = len(lcols) * nb
+
+            def xbufs(W):
+                sb = {q: torch.zeros(max(1, nb * W), dtype=A.dtype, device=dev) for q in self.xpeers}
+                rb = {q: torch.zeros(max(1, nb * W), dtype=A.dtype, device=dev) for q in self.xpeers}
+                if dev.type == "cuda":
+                    sp = torch.tensor([sb[q].data_ptr() if q in sb else 0 for q in range(g.P)], dtype=torch.int64,
+                                      device=dev)
+                    rp = torch.tensor([rb[q].data_ptr() if q in rb else 0 for q in range(g.P)], dtype=torch.int64,
+                                      device=dev)
+                else:
+                    sp, rp = [sb.get(q) for q in range(g.P)], [rb.get(q) for q in range(g.P)]
+                return {"send": sb, "recv": rb, "sp": sp, "rp": rp}
+            self.xb = {"next": xbufs(nb), "rest": xbufs(wtot)}
+            if not trailing_only:
+                self.xb["left"] = xbufs(wtot)
+                self.tmp_x = torch.zeros_like(self.tmp) if self.tmp is not None else None
+            self.g_next = ctx.urgent_group if ctx.urgent_group is not None else ctx.col_group
+            bulk = list(ctx.bulk_groups) or [ctx.col_group]
+            self.g_rest, self.g_left = bulk[0], bulk[-1]
         ncol_loc = sum(A.tile_cols(n) for n in lcols)
         self.ubuf = torch.zeros(max(1, nb * max(ncol_loc, 1)), dtype=A.dtype, device=dev)
         # P > 1: per-step panel gather buffer [P][maxrows x nb] (every process row's panel tiles)
@@ -262,6 +298,8 @@ class _GetrfDev:
         # local candidates (value, row, candidate row, current diagonal row) and only the two rows of
         # an interchange move; O(NB (NB + P)) elements per panel instead of O(M NB / P)
         self.plan = [self._build(k) for k in range(self.kt)]
+        rl = max([st.get("rlen", 0) for st in self.plan] + [0])
+        self.rbuf = torch.zeros(max(1, rl), dtype=A.dtype, device=dev) if rl else None
         self.bytes_panel = [0] * self.kt   # elements this rank sends per step (panel exchange)
         if self.percol:
             mlmax = max([st.get("Ml", 0) for st in self.plan] + [1])
@@ -291,6 +329,18 @@ class _GetrfDev:
         else:
             lay = {m: (m - k) * mb for m in range(k, A.mt)}
             st["pld"] = mp
+            if g.P > 1 and g.Q > 1 and self.gbuf is not None:
+                # the row broadcast of the factored panel carries this process row's tiles only (the row peers'
+                # trailing updates read nothing else): packed by the root, unpacked at the same place by the others
+                mine_r = [m for m in range(k, A.mt) if A.row_is_local(m)]
+                pk, upk, r = TileBatch(), TileBatch(), 0
+                for m in mine_r:
+                    pk.add(lay[m], A.tile_rows(m), kb, b_off=r)
+                    upk.add(r, A.tile_rows(m), kb, b_off=lay[m])
+                    r += A.tile_rows(m)
+                st["rlen"], st["rld"] = r * kb, max(1, r)
+                if r:
+                    st["rpack"], st["runpack"] = pk.finalize(), upk.finalize()
         if A.col_is_local(k) and self.dist:
             diag = A.row_is_local(k)
             tb, back = TileBatch(), TileBatch()
@@ -360,22 +410,32 @@ class _GetrfDev:
                 st["grow"] = grow
         trail = [n for n in range(k + 1, A.nt) if A.col_is_local(n)]
         st["trail"] = trail
+        lcols = self.lcols
+        st["jl"] = bisect.bisect_left(lcols, k)                       # local columns left of the panel
+        st["jk"] = 1 if A.col_is_local(k) else 0                        # the panel column itself (rewritten by back)
+        st["jn"] = 1 if (k + 1 < A.nt and A.col_is_local(k + 1)) else 0   # the next panel's column
+        parts = {"": trail, "_n": trail[:st["jn"]], "_r": trail[st["jn"]:]}
         if trail and A.row_is_local(k):
-            tb = TileBatch()
-            for n in trail:
-                tb.add(0, kb, A.tile_cols(n), b_off=A.offset(k, n))
-            st["trsm"] = tb.finalize()
+            for sfx, cols in parts.items():
+                if cols:
+                    tb = TileBatch()
+                    for n in cols:
+                        tb.add(0, kb, A.tile_cols(n), b_off=A.offset(k, n))
+                    st["trsm" + sfx] = tb.finalize()
         if trail and k + 1 < A.mt:
             uoff, c = {}, 0
             for n in trail:
                 uoff[n] = c * kb
                 c += A.tile_cols(n)
             st["ulen"] = c * kb
+            st["ulen_n"] = (A.tile_cols(k + 1) * kb) if st["jn"] else 0   # the next column's U leads the buffer
             if A.row_is_local(k):
-                tb = TileBatch()
-                for n in trail:
-                    tb.add(A.offset(k, n), kb, A.tile_cols(n), b_off=uoff[n])
-                st["upack"] = tb.finalize()
+                for sfx, cols in parts.items():
+                    if cols:
+                        tb = TileBatch()
+                        for n in cols:
+                            tb.add(A.offset(k, n), kb, A.tile_cols(n), b_off=uoff[n])
+                        st["upack" + sfx] = tb.finalize()
             rows = [m for m in range(k + 1, A.mt) if A.row_is_local(m)]
             if rows:
                 nxt, rest = GemmBatch(), GemmBatch()
@@ -390,6 +450,13 @@ class _GetrfDev:
     def step(self, k):
         """The whole step in order (no look-ahead)."""
         self.panel(k)
+        if self.xmode:
+            self.swap_next(k)
+            self.next(k)
+            self.swap_rest(k)
+            self.rest(k)
+            self.swap_left(k)
+            return
         self.swap(k)
         self.next(k)
         self.rest(k)
@@ -422,7 +489,15 @@ class _GetrfDev:
         # --- factored panel + pivots along process rows
         if g.Q > 1:
             root = g.rank(A.myrow, pc)
-            comm.bcast(pv, root, ctx.row_group)
+            if "rlen" in st:        # gather mode, P > 1: only this process row's tiles travel
+                rb = self.rbuf[: st["rlen"]]
+                if A.col_is_local(k) and "rpack" in st:
+                    ops.geadd(0, N_, 1.0, pv, st["pld"], 0.0, self.rbuf, st["rld"], st["rpack"], copy=True)
+                comm.bcast(rb, root, ctx.row_group)
+                if not A.col_is_local(k) and "runpack" in st:
+                    ops.geadd(0, N_, 1.0, self.rbuf, st["rld"], 0.0, pv, st["pld"], st["runpack"], copy=True)
+            else:
+                comm.bcast(pv, root, ctx.row_group)
             if self.pivot:
                 comm.bcast(self.piv_dev, root, ctx.row_group)
         if not self.pivot:
@@ -432,6 +507,9 @@ class _GetrfDev:
             par = k & 1
             ops.piv_moves(self.piv_dev, kmin, self.mdst[par], self.msrc[par], self.mcnt[par], mrel=self.A.m - r0,
                           info=self.info)
+            if self.xmode:
+                ops.rows_xord(self.mdst[par], self.msrc[par], self.mcnt[par], r0, A.mb, self.prow_t, A.myrow, g.P,
+                              A.nb, self.xo[par], self.info)
 
     def _panel_dist(self, k):
         """Distributed partial pivoting of panel k on the GPUs of its process column (see panel_mode):
@@ -584,6 +662,82 @@ class _GetrfDev:
         if g.P > 1:
             comm.bcast(ub[: st["ulen"]], g.rank(g.prow(k + A.it0), A.mycol), ctx.col_group)
 
+    # ---- P > 1 interchanges, point to point (xmode) ------------------------------------------------------
+    def _xswap(self, k, j0, j1, tmp, key, group):
+        """Step k's net row moves on the local tile columns lcols[j0:j1]: my source rows are staged (gather), the
+        ones whose destination lies on another process row go into that row's send buffer at their class ordinal
+        (rows_xord / rows_xcopy), one grouped point-to-point exchange with the other process rows of my column
+        (fixed NB-row buffers: a class never holds more than NB moves), the arriving rows are unpacked into their
+        staging slots and every slot is scattered to its local destination row."""
+        if j1 <= j0:
+            return
+        A = self.A
+        g = A.grid
+        st = self.plan[k]
+        par = k & 1
+        nb = A.nb
+        ldb = 2 * nb
+        W = (j1 - j0) * nb
+        xb = self.xb[key]
+        rows = tmp is not None
+        if rows:
+            cr, nr = self.coloff[j0:j1], self.ncols[j0:j1]
+            ops.rows_move(True, A.data, A.ld, A.mb, st["r0"], self.rowoff, cr, nr, nb, self.msrc[par], self.mcnt[par],
+                          ldb, tmp, ldb, self.info)
+            ops.rows_xcopy(True, tmp, ldb, W, self.xo[par], self.mcnt[par], ldb, xb["sp"], nb)
+        sends = [(xb["send"][q][: nb * W], g.rank(q, A.mycol)) for q in self.xpeers]
+        recvs = [(xb["recv"][q][: nb * W], g.rank(q, A.mycol)) for q in self.xpeers]
+        comm.p2p(sends, recvs, group=group)
+        if rows:
+            ops.rows_xcopy(False, tmp, ldb, W, self.xo[par], self.mcnt[par], ldb, xb["rp"], nb)
+            ops.rows_move(False, A.data, A.ld, A.mb, st["r0"], self.rowoff, cr, nr, nb, self.mdst[par], self.mcnt[par],
+                          ldb, tmp, ldb, self.info)
+
+    def _u_bcast(self, k, sfx, lo, hi, group):
+        """U block row part [lo, hi) of ubuf (packed where row k lives) down the process column, point to point
+        from the diagonal process row on ``group``."""
+        A, st = self.A, self.plan[k]
+        if hi <= lo:
+            return
+        g = A.grid
+        ub = self.ubuf[lo:hi]
+        if "upack" + sfx in st:
+            ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, self.ubuf, st["kb"], st["upack" + sfx], copy=True)
+        root_p = g.prow(k + A.it0)
+        if A.myrow == root_p:
+            comm.p2p([(ub, g.rank(q, A.mycol)) for q in range(g.P) if q != root_p], (), group=group)
+        else:
+            comm.p2p((), [(ub, g.rank(root_p, A.mycol))], group=group)
+
+    def swap_next(self, k):
+        """The next panel's column (k + 1) only: interchanges, panel write-back, its U block and broadcast -- the
+        critical path of the look-ahead (panel stream)."""
+        A, st = self.A, self.plan[k]
+        j0 = st["jl"] + st["jk"]
+        self._xswap(k, j0, j0 + st["jn"], self.tmp, "next", self.g_next)
+        if "back" in st:
+            ops.geadd(0, N_, 1.0, st["pv"], st["pld"], 0.0, A.data, A.ld, st["back"], copy=True)
+        if "trsm_n" in st:
+            ops.trsm(dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, st["pv"], st["pld"], A.data, A.ld, st["trsm_n"])
+        if "ulen" in st:
+            self._u_bcast(k, "_n", 0, st["ulen_n"], self.g_next)
+
+    def swap_rest(self, k):
+        """Every later trailing column: interchanges, U blocks, broadcast (update stream)."""
+        A, st = self.A, self.plan[k]
+        j0 = st["jl"] + st["jk"] + st["jn"]
+        self._xswap(k, j0, len(self.lcols), self.tmp, "rest", self.g_rest)
+        if "trsm_r" in st:
+            ops.trsm(dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, st["pv"], st["pld"], A.data, A.ld, st["trsm_r"])
+        if "ulen" in st:
+            self._u_bcast(k, "_r", st["ulen_n"], st["ulen"], self.g_rest)
+
+    def swap_left(self, k):
+        """The already factored columns (< k): only the final L needs these moves (side stream)."""
+        if self.trailing_only:
+            return
+        self._xswap(k, 0, self.plan[k]["jl"], getattr(self, "tmp_x", None), "left", self.g_left)
+
     def _update(self, k, key):
         st = self.plan[k]
         gb = st.get(key)
@@ -611,6 +765,24 @@ class _GetrfDev:
                 prev = tp.task(f"{tag}({k})", "update", (lambda k=k: self.step(k)), [prev])
             return
         nxt = rest = None
+        if self.xmode:
+            # PANEL(k+1) waits for NEXT(k) only; SWAPN(k+1) for REST(k) (column k+2 carries step k's update);
+            # LEFT(k) on the low-priority side stream after PANEL(k) (move lists; panel k-1 written back before
+            # PANEL(k) by SWAPN(k-1) on the panel stream) -- PANEL(k+2) re-fills step k's lists, so it waits for LEFT(k)
+            lefts = {}
+            for k in range(self.kt):
+                t_p = tp.task(f"PANEL({k})", "panel", (lambda k=k: self.panel(k)), [nxt, lefts.get(k - 2)], prio=3)
+                t_n = tp.task(f"SWAPN({k})", "panel", (lambda k=k: self.swap_next(k)), [t_p, rest], prio=3)
+                nxt = tp.task(f"NEXT({k})", "panel", (lambda k=k: self.next(k)), [t_n], prio=2)
+                t_s = tp.task(f"SWAPR({k})", "update", (lambda k=k: self.swap_rest(k)), [t_p, rest], prio=2)
+                rest = tp.task(f"REST({k})", "update", (lambda k=k: self.rest(k)), [t_s], prio=1)
+                if not self.trailing_only and self.plan[k]["jl"] > 0:
+                    lefts[k] = tp.task(f"LEFT({k})", "aux", (lambda k=k: self.swap_left(k)),
+                                       [t_p, lefts.get(k - 1)], prio=0)
+            tail = [t for t in lefts.values()]
+            if tail:   # the factorisation ends with L final
+                tp.task("LEFT_JOIN", "update", (lambda: None), [rest] + tail, prio=0)
+            return
         for k in range(self.kt):
             t_p = tp.task(f"PANEL({k})", "panel", (lambda k=k: self.panel(k)), [nxt], prio=3)
             t_s = tp.task(f"SWAP({k})", "update", (lambda k=k: self.swap(k)), [t_p, rest], prio=2)

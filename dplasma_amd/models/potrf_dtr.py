@@ -441,7 +441,7 @@ class ArgsImage:
     _LL = ("ld", "ncnt", "bw_bpt", "lat_t")
     _INT = ("nt", "nranks", "rank", "epoch", "flags", "dil", "nsteps", "ntask", "nclass")
     _PTR = ("tasks", "reqs", "tab", "xoff", "cur", "hs_off", "scur", "hi", "lo", "vis", "link", "Mw", "Sw", "Lp", "Wp",
-            "prog", "info", "trace", "succ_off", "succ", "ring_of", "town", "qbase", "done", "rdy")
+            "prog", "info", "trace", "succ_off", "succ", "ring_of", "town", "qbase", "done", "rdy", "probe")
     _PARR = ("A", "recv", "W", "cnt", "pend", "qctl", "qslot")
     _IARR = ("hi_off", "lo_off")
 
@@ -608,6 +608,12 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
         trace = torch.zeros(4 * len(plan.tasks), dtype=torch.int64, device=dev)
         img.set("trace", trace.data_ptr())
     tp.dtr_trace = trace
+    # DPLASMA_DTR_PROBE=1: the strip-hazard probe of the diagonal-tile updates (tp.dtr_probe; dtr.hip probe_strip)
+    probe = None
+    if os.environ.get("DPLASMA_DTR_PROBE", "0") == "1":
+        probe = torch.zeros(8 + 20 * nt * nt + 8 * 4096, dtype=torch.int64, device=dev)
+        img.set("probe", probe.data_ptr())
+    tp.dtr_probe = probe
     nbytes = img.size
     host = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
     hosts = [[host, None], [torch.empty(nbytes, dtype=torch.uint8).pin_memory(), None]]
@@ -646,7 +652,7 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
             img.set(f, qk[f].data_ptr())
         for f in ("pend", "qctl", "qslot"):
             img.set(f, [qk[f].data_ptr()])
-    tp._keep = (tasks_d, reqs_d, hi_d, lo_d, tab_d, cnt, cur, hs_d, scur, W, scr, hosts, args_d, qk)
+    tp._keep = (tasks_d, reqs_d, hi_d, lo_d, tab_d, cnt, cur, hs_d, scur, W, scr, hosts, args_d, qk, probe)
     tp.dtr_plan = plan
     tp.dtr_sched = sched
 

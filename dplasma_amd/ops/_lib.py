@@ -115,6 +115,7 @@ _SIGS = {
     "dpl_lu_block_dist": [c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                           c_int, c_int, c_int, c_int, c_vp, c_int, c_vp],
     "dpl_lu_dist_ws_bytes": [c_int],
+    "dpl_lu_dist_set_maxwg": [c_int],
     "dpl_lu_dist_slot_bytes": [c_int, c_int],
     "dpl_xchg_alloc": [c_ll, c_vp, c_vp],
     "dpl_ipc_alloc": [c_ll, c_int, c_vp, c_vp],
@@ -126,6 +127,10 @@ _SIGS = {
     "dpl_ipc_handle_bytes": [],
     "dpl_rows_permute": [c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp,
                          c_int, c_vp, c_vp],
+    # cross-process-row interchanges: dst, src, cnt, r0, mb, prow, nrt, me, P, ldx, xo, info, stream
+    "dpl_rows_xord": [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp],
+    # prec, pack, tmp, ldb, W, xo, cnt, maxcnt, bufs, ldx, stream
+    "dpl_rows_xcopy": [c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_int, c_vp],
 }
 _OPTIONAL = set()
 _RESTYPE = {"dpl_dtr_field": c_ll}

@@ -1098,6 +1098,66 @@ def rows_permute(A: torch.Tensor, ld: int, mb: int, r0: int, rowoff: torch.Tenso
     rows_move(False, A, ld, mb, r0, rowoff, coloff, ncols, nb, dst, cnt, maxcnt, buf, maxcnt, info)
 
 
+def rows_xord(dst: torch.Tensor, src: torch.Tensor, cnt: torch.Tensor, r0: int, mb: int, prow: torch.Tensor, me: int,
+              P: int, ldx: int, xo: torch.Tensor, info: torch.Tensor = None):
+    """Classify the net moves (dst[t] <- src[t], rows r0 + ...) for the point-to-point exchange between process rows
+    (the reference's SWAP_COLLECT / SWAP_SND, src/zgetrf_ptgpanel.jdf:825-984): xo[t] = 1<<30 | q<<16 | ord when my
+    staged source row goes to process row q, 1<<29 | q<<16 | ord when it arrives from q, -1 otherwise; ord is the
+    move's rank inside its (source row, destination row) class -- the same on both sides.  prow[view tile row] =
+    its process row."""
+    if _is_gpu(dst):
+        rc = _lib.load().dpl_rows_xord(dst.data_ptr(), src.data_ptr(), cnt.data_ptr(), r0, mb, prow.data_ptr(),
+                                       int(prow.numel()), me, P, ldx, xo.data_ptr(), _iptr(info), _lib.stream_ptr())
+        _lib.check(rc, "rows_xord")
+        return
+    n = int(cnt[0])
+    nrt = int(prow.numel())
+    nxt = {}
+    xo.fill_(-1)
+    for t in range(n):
+        Rs, Rd = r0 + int(src[t]), r0 + int(dst[t])
+        if not (0 <= Rs and 0 <= Rd and Rs // mb < nrt and Rd // mb < nrt):
+            _bad_pivot(info)
+            continue
+        so, dd = int(prow[Rs // mb]), int(prow[Rd // mb])
+        if so == dd or (so != me and dd != me):
+            continue
+        key = (so, dd)
+        o = nxt.get(key, 0)
+        nxt[key] = o + 1
+        if o >= ldx:
+            _bad_pivot(info)
+            continue
+        xo[t] = ((1 << 30) | (dd << 16) | o) if so == me else ((1 << 29) | (so << 16) | o)
+
+
+def rows_xcopy(pack: bool, tmp: torch.Tensor, ldb: int, W: int, xo: torch.Tensor, cnt: torch.Tensor, maxcnt: int,
+               bufs, ldx: int):
+    """pack: bufs[q][ord + c ldx] = tmp[t + c ldb] for my moves leaving for process row q; unpack: the reverse for
+    the moves arriving from q (c < W).  bufs: a device int64 tensor of buffer addresses (GPU) or a list of tensors
+    indexed by process row (CPU)."""
+    if W <= 0 or maxcnt <= 0:
+        return
+    if _is_gpu(tmp):
+        rc = _lib.load().dpl_rows_xcopy(_lib.prec_code(tmp.dtype), int(pack), tmp.data_ptr(), ldb, W, xo.data_ptr(),
+                                        cnt.data_ptr(), maxcnt, bufs.data_ptr(), ldx, _lib.stream_ptr())
+        _lib.check(rc, "rows_xcopy")
+        return
+    n = int(cnt[0])
+    bit = 30 if pack else 29
+    for t in range(n):
+        x = int(xo[t])
+        if x < 0 or not (x >> bit) & 1:
+            continue
+        q, o = (x >> 16) & 0x1FFF, x & 0xFFFF
+        tv = torch.as_strided(tmp, (W,), (ldb,), t)
+        bv = torch.as_strided(bufs[q], (W,), (ldx,), o)
+        if pack:
+            bv.copy_(tv)
+        else:
+            tv.copy_(bv)
+
+
 def rows_move(gather: bool, A: torch.Tensor, ld: int, mb: int, r0: int, rowoff: torch.Tensor, coloff: torch.Tensor,
               ncols: torch.Tensor, nb: int, rows: torch.Tensor, cnt: torch.Tensor, maxcnt: int, buf: torch.Tensor,
               ldb: int, info: torch.Tensor = None):

@@ -247,8 +247,9 @@ def allreduce(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None) -> None:
     dist.all_reduce(t, op=op, group=group)
 
 
-def p2p(sends=(), recvs=()) -> None:
-    """Grouped point-to-point transfer: sends / recvs are lists of (tensor, global peer rank).
+def p2p(sends=(), recvs=(), group=None) -> None:
+    """Grouped point-to-point transfer: sends / recvs are lists of (tensor, global peer rank), on the
+    communicator of ``group`` (None: the world's).
 
     RCCL: one grouped send/recv call (every pair on its own xGMI link); the current stream waits
     for the transfer.  gloo: CUDA tensors are staged through host memory (gloo moves host buffers)."""
@@ -259,10 +260,11 @@ def p2p(sends=(), recvs=()) -> None:
         per = {}
         for t_, p_ in sends + recvs:
             per[p_] = per.get(p_, 0) + _nbytes(t_)
-        return _BACKEND.sync("p2p", max(per.values()), None)
-    _rec_p2p(sends, recvs, None)
+        return _BACKEND.sync("p2p", max(per.values()), group)
+    _rec_p2p(sends, recvs, group)
     if _nccl():
-        ops = [dist.P2POp(dist.isend, t, p) for t, p in sends] + [dist.P2POp(dist.irecv, t, p) for t, p in recvs]
+        ops = [dist.P2POp(dist.isend, t, p, group=group) for t, p in sends]
+        ops += [dist.P2POp(dist.irecv, t, p, group=group) for t, p in recvs]
         with self_p2p():
             for w in dist.batch_isend_irecv(ops) or ():
                 w.wait()
@@ -270,8 +272,8 @@ def p2p(sends=(), recvs=()) -> None:
     if loopback():
         sends, recvs = _split_self(sends, recvs)
     host_r = [(t, t.cpu() if t.device.type != "cpu" else t) for t, _ in recvs]
-    works = [dist.isend(t.cpu() if t.device.type != "cpu" else t, p) for t, p in sends]
-    works += [dist.irecv(h, p) for (_, h), (_, p) in zip(host_r, recvs)]
+    works = [dist.isend(t.cpu() if t.device.type != "cpu" else t, p, group=group) for t, p in sends]
+    works += [dist.irecv(h, p, group=group) for (_, h), (_, p) in zip(host_r, recvs)]
     for w in works:
         w.wait()
     for t, h in host_r:

@@ -63,27 +63,47 @@ def _hqr_w(rank, world):
     return 0, c.record(False)
 
 
+def _getrf_w(rank, world):
+    """getrf_ptgpanel on 2 x 4 with the point-to-point interchanges (next column / rest / left on three
+    communicators, look-ahead): the recorded order must satisfy the same three conditions."""
+    import dplasma_amd as dp
+    from dplasma_amd.parallel import comm as c
+    ctx = dp.init(device="cpu", P=2)
+    A = dp.block_cyclic(ctx, torch.float64, 16, 16, 128, 128)
+    dp.plrnt(ctx, A, 3872)
+    IP = dp.ptgpanel_ipiv_descriptor(ctx, A)
+    c.record(True)
+    info = dp.getrf_ptgpanel(ctx, A, IP)
+    return info, c.record(False)
+
+
 @pytest.fixture(scope="module")
 def logs():
     out = {}
-    for name, fn in (("potrf", _potrf_w), ("gemm", _gemm_w), ("hqr", _hqr_w)):
+    for name, fn in (("potrf", _potrf_w), ("gemm", _gemm_w), ("hqr", _hqr_w), ("getrf", _getrf_w)):
         res = run_distributed(fn, 8)
         assert all(res[r][0] == 0 for r in range(8))
         out[name] = {r: res[r][1] for r in range(8)}
     return out
 
 
-@pytest.mark.parametrize("alg", ["potrf", "gemm", "hqr"])
+@pytest.mark.parametrize("alg", ["potrf", "gemm", "hqr", "getrf"])
 def test_comm_order_consistent(logs, alg):
     log = logs[alg]
     assert sum(len(v) for v in log.values()) > 0
     comms = {g for v in log.values() for _, g, _, _ in v}
     if alg == "potrf":     # the dataflow transport really uses several communicators
         assert len(comms) >= 2, comms
+    if alg == "getrf":
+        # rows cross process rows point to point (next column urgent, rest / left on the bulk communicators);
+        # no all-reduce of the staging buffer is left
+        kinds = {(g, k) for v in log.values() for _, g, k, _ in v}
+        assert ("urgent", "p2p") in kinds and ("bulk0", "p2p") in kinds and ("bulk1", "p2p") in kinds, kinds
+        assert not any(k == "allreduce" and g.startswith("col") for g, k in kinds), kinds
     comm.check_order(log)
 
 
-@pytest.mark.parametrize("alg", ["potrf", "gemm", "hqr"])
+@pytest.mark.parametrize("alg", ["potrf", "gemm", "hqr", "getrf"])
 def test_comm_order_detects_permutation(logs, alg):
     """Swapping two point-to-point batches of one rank (different tasks) must fail the check: either the
     messages no longer pair up in order on their communicator, or the swap creates a wait cycle."""
@@ -96,6 +116,8 @@ def test_comm_order_detects_permutation(logs, alg):
                 i, j = idx[a], idx[b]
                 if seq[i][0] == seq[j][0]:
                     continue
+                if seq[i][1:] == seq[j][1:]:
+                    continue   # same communicator, same peers and sizes: a swap no transport could tell apart
                 bad = copy.deepcopy(log)
                 bad[r][i], bad[r][j] = bad[r][j], bad[r][i]
                 with pytest.raises(AssertionError):

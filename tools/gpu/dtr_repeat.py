@@ -1,6 +1,10 @@
 """Repeat one DTR Cholesky configuration and residual-check every run (intermittent-failure hunt).
 
   python tools/gpu/dtr_repeat.py N runs
+
+DPLASMA_DTR_PROBE=1: also print the strip-hazard probe's records of every run (csrc/kernels/dtr.hip probe_strip:
+kind 1 = a diagonal-tile update started before its strip's TRSM stamp, kind 2 = a strip read differently through
+the CU's caches than from memory).
 """
 import sys
 from pathlib import Path
@@ -24,9 +28,13 @@ def main():
     bad = 0
     good = None
     nt = N // 512
+    probe = getattr(tp, "dtr_probe", None)
+    nprobe = [0] * 7
     for rep in range(runs):
         A.data.copy_(A0)
         tp.info.zero_()
+        if probe is not None:
+            probe[0] = 0
         tp.execute(ctx)
         info = int(tp.info.item())
         # every counter at its final value (a task run twice would leave one above it)
@@ -48,8 +56,25 @@ def main():
             idx = torch.nonzero(d > 1e-9)
             lst = sorted((int(j), int(i), int(r), int(c), float(d[i, r, j, c])) for i, r, j, c in idx.tolist())
             msg = f" info={info} bad sub-tiles {len(lst)} first (j, i, r, c, err): {lst[:8]}"
-        print(f"run {rep}: check={ok} res={res:.2e}{msg}{cmsg}", flush=True)
-    print(f"FAILED {bad} / {runs}", flush=True)
+        pmsg = ""
+        if probe is not None:
+            pr = probe.cpu().numpy()
+            n = int(min(pr[0], 4096))
+            recs = pr[8 + 20 * nt * nt: 8 + 20 * nt * nt + 8 * n].reshape(n, 8)
+            kinds = [int(x & 15) for x in recs[:, 1]]
+            for kd in range(1, 7):
+                nprobe[kd] += kinds.count(kd)
+            if n:
+                show = [(int(r_[0]), int(r_[1] >> 16), int((r_[1] >> 8) & 255), int((r_[1] >> 4) & 15), int(r_[1] & 15),
+                         int(r_[2] >> 8), int(r_[2] & 255), int(r_[3]),
+                         float(np.frombuffer(np.int64(r_[4]).tobytes())[0]), float(np.frombuffer(np.int64(r_[5]).tobytes())[0]))
+                        for r_ in recs[:6]]
+                pmsg = (f" probe: {n} records by kind {[kinds.count(kd) for kd in range(1, 7)]}; first (task, "
+                        f"k|tile, strip|sub, phase, kind, wg, xcd, stamp, plain, mem): {show}")
+        print(f"run {rep}: check={ok} res={res:.2e}{msg}{cmsg}{pmsg}", flush=True)
+    print(f"FAILED {bad} / {runs}" + (f"; probe records by kind (1 strip stamp, 2 strip cache, 3 C stamp, 4 C cache, "
+                                      f"5 POTRF-input stamp, 6 POTRF-input cache): {nprobe[1:]}"
+                                      if probe is not None else ""), flush=True)
 
 
 if __name__ == "__main__":

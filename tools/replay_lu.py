@@ -7,10 +7,17 @@ the transport replaced by the timing model of tools/replay_potrf.py (every colle
 exchange = one busy-wait kernel of lat + bytes / bw on a communication stream, no data moved).  The
 distributed panel kernel (csrc/kernels/lu_dist.hip) runs on this rank's rows plus the diagonal replica
 with a one-rank exchange group, and each column's cross-rank hand-off -- IPC stores over xGMI on a real
-grid -- is modelled as ``--xlat`` microseconds per column on the panel's stream.
+grid -- is modelled as ``--xlat`` + ``--xgmi`` microseconds per column on the panel's stream: ``--xlat`` is the
+MEASURED cost of a real peer (tools/gpu/lu_xlat_probe.py: two emulated ranks on the two CU halves of one GPU
+exchanging through memory, minus one rank alone -- profiles/r6_lu_xlat_probe.txt), ``--xgmi`` the extra one-way
+latency of an xGMI hop over an on-package one (an assumption, reported with the result).
+
+Communicators are modelled separately (one delay stream each): the row / column groups of the panel and
+diagonal-tile broadcasts, the urgent communicator of the next column's interchanges and U block, the bulk ones of
+the rest of the trailing columns and of the deferred left-column interchanges (models/lu.py _xswap).
 
 usage: python tools/replay_lu.py -N 65536 --nb 512 --grid 2x4 [--ranks all] [--steps 1] [--bw 50]
-       [--lat 15] [--xlat 6]
+       [--lat 15] [--xlat 2.4] [--xgmi 2]
 """
 from __future__ import annotations
 
@@ -83,6 +90,7 @@ def _delivered_pivots_panel(orig, ipiv):
 def replay_rank(base, P, Q, rank, N, NB, steps, xlat, ipiv):
     from dplasma_amd.models import lu as lu_mod
     ctx = fake_rank_context(base, P, Q, rank)
+    ctx.row_group, ctx.col_group = "row", "col"      # one modelled link stream per communicator
     orig = lu_dist_ops.panel_xchg
     orig_panel = lu_mod._GetrfDev.panel
     lu_dist_ops.panel_xchg = lambda group, me, P_, kbw, dtype, device, max_rows=0: ReplayXchg(kbw, dtype, device, xlat)
@@ -122,7 +130,8 @@ def main():
     ap.add_argument("--bw", type=float, default=50.0)
     ap.add_argument("--lat", type=float, default=15.0)
     ap.add_argument("--comm-wg", type=int, default=4)
-    ap.add_argument("--xlat", type=float, default=6.0, help="us per panel column (cross-rank pivot hand-off)")
+    ap.add_argument("--xlat", type=float, default=6.0, help="us per panel column (cross-rank pivot hand-off, measured)")
+    ap.add_argument("--xgmi", type=float, default=0.0, help="extra us per panel column for the xGMI hop (assumed)")
     args = ap.parse_args()
     P, Q = map(int, args.grid.lower().split("x"))
     base = dp.init(device="cuda:0")
@@ -137,13 +146,13 @@ def main():
     fl = flops("d", "getrf", args.N, args.N)
     res = {}
     for r in ranks:
-        t, enq = replay_rank(base, P, Q, r, args.N, args.nb, args.steps, args.xlat, ipiv)
+        t, enq = replay_rank(base, P, Q, r, args.N, args.nb, args.steps, args.xlat + args.xgmi, ipiv)
         res[r] = t
         print(f"rank {r} ({r // Q},{r % Q}): {t * 1e3:9.2f} ms   enq {enq:.2f} s", flush=True)
     worst = max(res.values())
     ideal = fl / (78.6e12 * P * Q)
     print(json.dumps({"op": "getrf_ptgpanel", "N": args.N, "NB": args.nb, "grid": f"{P}x{Q}", "bw_GBs": args.bw,
-                      "lat_us": args.lat, "xlat_us_per_col": args.xlat, "worst_ms": round(worst * 1e3, 2),
+                      "lat_us": args.lat, "xlat_us_per_col": args.xlat, "xgmi_us_per_col": args.xgmi, "worst_ms": round(worst * 1e3, 2),
                       "ideal_ms": round(ideal * 1e3, 2), "pct_peak": round(100 * ideal / worst, 1),
                       "tflops_job": round(fl / worst / 1e12, 1),
                       "per_rank_ms": {str(k): round(v * 1e3, 2) for k, v in res.items()},
