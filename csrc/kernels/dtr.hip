@@ -136,6 +136,7 @@ struct DtrArgs {
   // [0] record count, [8, 8 + 4 nt * nt) per strip (4 i + r, k) the epoch stamped by its TRSM before its release,
   // then 8-word records of every diagonal-tile update that saw a strip operand stale (see probe_strips)
   long long* probe;
+  double* snap;             // optional (with probe): nt x 512 x 512 copy of every diagonal tile's POTRF input
 };
 
 constexpr int NBT = 512;    // tile size
@@ -524,6 +525,15 @@ __device__ __attribute__((noinline)) void run_potrf(const DtrArgs* __restrict__ 
   if (g.probe && threadIdx.x == 0)   // hazard probe: the row block's input sub-tiles (final versions, fresh)
     for (int c = 0; c <= b / 4; ++c)
       probe_sub(gp, t, rk, k, b / 4, c, k > 0 ? ((long long)g.epoch << 12) + k : -1, 32 * b, 5);
+  if (g.snap) {   // ... and a copy of the row block's input as this workgroup reads it (host: chol(input) vs output)
+    const double* src = g.A[rk] + tile_at(tab, g.nt, k, k);
+    double* dst = g.snap + (size_t)k * NBT * NBT;
+    for (int e = threadIdx.x; e < 32 * (32 * b + 32); e += 256) {
+      const int rr = 32 * b + e % 32, cc = e / 32;
+      dst[rr + (long long)cc * NBT] = src[rr + (long long)cc * g.ld];
+    }
+    __syncthreads();
+  }
   rb_tile_body<true>(g.A[rk] + tile_at(tab, g.nt, k, k), NBT, (int)g.ld, g.info, k * NBT, ws, g.epoch, nullptr, b,
                      g_lds, g_lds + BLK);
   __syncthreads();
@@ -1019,7 +1029,7 @@ DPL_API long long dpl_dtr_field(const char* name) {
   DTR_FIELD(vis) DTR_FIELD(link) DTR_FIELD(bw_bpt) DTR_FIELD(lat_t) DTR_FIELD(Mw) DTR_FIELD(Sw) DTR_FIELD(Lp)
   DTR_FIELD(Wp) DTR_FIELD(prog) DTR_FIELD(info) DTR_FIELD(trace) DTR_FIELD(ntask) DTR_FIELD(nclass) DTR_FIELD(pend)
   DTR_FIELD(succ_off) DTR_FIELD(succ) DTR_FIELD(ring_of) DTR_FIELD(town) DTR_FIELD(qbase) DTR_FIELD(qctl)
-  DTR_FIELD(qslot) DTR_FIELD(done) DTR_FIELD(rdy) DTR_FIELD(probe)
+  DTR_FIELD(qslot) DTR_FIELD(done) DTR_FIELD(rdy) DTR_FIELD(probe) DTR_FIELD(snap)
   if (!std::strcmp(name, "size")) return (long long)sizeof(DtrArgs);
   if (!std::strcmp(name, "task")) return (long long)sizeof(DtrTask);
   if (!std::strcmp(name, "MAXB")) return MAXB;

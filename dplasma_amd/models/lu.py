@@ -256,7 +256,19 @@ class _GetrfDev:
         # needs them).  "allreduce" keeps round 5's summed exchange of the whole 2 NB-row staging buffer.
         self.xmode = (g.P > 1 and pivot and not self.percol and bool(lcols) and
                       os.environ.get("DPLASMA_LU_XROWS", "p2p") != "allreduce")
+        self.nch = 1
+        # gather-mode panels on P x Q grids: the panel's tiles travel point to point with the exact per-step sizes
+        # (packed slots; an all-gather would move the largest step's slot every step), and with DPLASMA_LU_RNF=1
+        # (default) the ranks of the NEXT panel's process column receive them too and factor panel k redundantly --
+        # the factored panel then never travels on the critical path: NEXT(k) runs on the column that factored it
+        self.gxp2p = g.P > 1 and pivot and self.panel_mode == "gather"
+        self.rnf = (self.gxp2p and self.xmode and g.Q > 1 and os.environ.get("DPLASMA_LU_RNF", "1") == "1")
         if self.xmode:
+            # the rest of the trailing columns in DPLASMA_LU_CHUNKS column chunks: chunk c's interchanges / U block of
+            # step k+1 (exchange stream) overlap the update of chunk c+1 of step k (update stream)
+            self.nch = max(1, int(os.environ.get("DPLASMA_LU_CHUNKS", "2")))
+            if dev.type == "cuda" and "xch" not in ctx.streams:
+                ctx.streams["xch"] = torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1])
             self.xpeers = [q for q in range(g.P) if q != A.myrow]
             self.prow_t = torch.tensor([g.prow(m + A.it0) for m in range(A.mt)], dtype=torch.int32, device=dev)
             self.xo = torch.full((2, 2 * nb), -1, dtype=torch.int32, device=dev)
@@ -282,6 +294,8 @@ class _GetrfDev:
             self.g_rest, self.g_left = bulk[0], bulk[-1]
         ncol_loc = sum(A.tile_cols(n) for n in lcols)
         self.ubuf = torch.zeros(max(1, nb * max(ncol_loc, 1)), dtype=A.dtype, device=dev)
+        # xmode: U blocks double-buffered by step parity (step k+1's exchanges run while step k's update chunks read)
+        self.ubufs = [self.ubuf, torch.zeros_like(self.ubuf) if self.xmode else self.ubuf]
         # P > 1: per-step panel gather buffer [P][maxrows x nb] (every process row's panel tiles)
         self.gbuf = None
         if g.P > 1 and not self.dist and not self.percol:
@@ -356,15 +370,33 @@ class _GetrfDev:
             st["kmin"] = min(st["kmin"], tr)
             self.bytes_panel_plan = getattr(self, "bytes_panel_plan", {})
             self.bytes_panel_plan[k] = st["kmin"] * (2 + kb) * (g.P - 1)
-        elif A.col_is_local(k):
+        elif A.col_is_local(k) or (self.rnf and k + 1 < A.nt and A.col_is_local(k + 1)):
+            own_col = A.col_is_local(k)
+            st["fac"] = True
             mine = [m for m in range(k, A.mt) if A.row_is_local(m)]
-            if mine:
+            if mine and own_col:
                 tb, back = TileBatch(), TileBatch()
                 for m in mine:
                     tb.add(A.offset(m, k), A.tile_rows(m), kb, b_off=(m - k) * mb)
                     back.add((m - k) * mb, A.tile_rows(m), kb, b_off=A.offset(m, k))
                 st["gather"], st["back"] = tb.finalize(), back.finalize()
-            if g.P > 1 and self.gbuf is not None:
+            if self.gxp2p:
+                # exact slots: process row q's tiles of the panel, packed (ld = its row count) one after another
+                rows_q = [sum(A.tile_rows(m) for m in range(k, A.mt) if g.prow(m + A.it0) == q) for q in range(g.P)]
+                off_q = [sum(rows_q[:q]) * kb for q in range(g.P)]
+                pack, unpack = TileBatch(), [TileBatch() for _ in range(g.P)]
+                rq = [0] * g.P
+                for m in range(k, A.mt):
+                    q = g.prow(m + A.it0)
+                    if q == A.myrow and own_col:
+                        pack.add(A.offset(m, k), A.tile_rows(m), kb, b_off=rq[q])
+                    unpack[q].add(rq[q], A.tile_rows(m), kb, b_off=(m - k) * mb)
+                    rq[q] += A.tile_rows(m)
+                st["xslots"] = [(off_q[q], rows_q[q] * kb, max(1, rows_q[q])) for q in range(g.P)]
+                st["gpack"] = pack.finalize() if len(pack) else None
+                st["gunpack"] = [u.finalize() if len(u) else None for u in unpack]
+                st["gsent"] = rows_q[A.myrow] * kb if own_col else 0
+            elif g.P > 1 and self.gbuf is not None:
                 # pack my panel tiles into my slot of the gather buffer, unpack every slot into the panel
                 gm, slot = self.gmax, g.P
                 pack, unpack = TileBatch(), TileBatch()
@@ -394,7 +426,7 @@ class _GetrfDev:
                     for r in range(kb, mp, mb):
                         tb.add(0, min(mb, mp - r), kb, b_off=r)
                     st["l21"] = tb.finalize()
-            if g.P > 1:
+            if g.P > 1 and own_col:
                 # percol mode: my panel rows, contiguous (ld = Ml), and their global row indices
                 lg, lu_ = TileBatch(), TileBatch()
                 grow, r = [], 0
@@ -445,6 +477,37 @@ class _GetrfDev:
                                                           [(lay[m], uoff[n], kb)])
                 st["gemm_next"] = nxt.finalize() if len(nxt) else None
                 st["gemm_rest"] = rest.finalize() if len(rest) else None
+        # xmode: the rest columns in chunks -- (first, end) local column index, columns, U range; per chunk its TRSM,
+        # U pack and update batch
+        rest_cols = trail[st["jn"]:]
+        j0r = st["jl"] + st["jk"] + st["jn"]
+        bnd = [round(c * len(rest_cols) / self.nch) for c in range(self.nch + 1)]
+        st["chunks"] = []
+        for c in range(self.nch):
+            cols = rest_cols[bnd[c]:bnd[c + 1]]
+            ch = {"j0": j0r + bnd[c], "j1": j0r + bnd[c + 1], "cols": cols}
+            if cols and "ulen" in st:
+                ch["ulo"] = uoff[cols[0]]
+                ch["uhi"] = uoff[cols[-1]] + A.tile_cols(cols[-1]) * kb
+                if A.row_is_local(k):
+                    tb, up = TileBatch(), TileBatch()
+                    for n in cols:
+                        tb.add(0, kb, A.tile_cols(n), b_off=A.offset(k, n))
+                        up.add(A.offset(k, n), kb, A.tile_cols(n), b_off=uoff[n])
+                    ch["trsm"], ch["upack"] = tb.finalize(), up.finalize()
+                rows = [m for m in range(k + 1, A.mt) if A.row_is_local(m)]
+                if rows:
+                    gb = GemmBatch()
+                    for n in cols:
+                        for m in rows:
+                            gb.add(A.offset(m, n), A.tile_rows(m), A.tile_cols(n), [(lay[m], uoff[n], kb)])
+                    ch["gemm"] = gb.finalize()
+            elif cols and A.row_is_local(k):
+                tb = TileBatch()
+                for n in cols:
+                    tb.add(0, kb, A.tile_cols(n), b_off=A.offset(k, n))
+                ch["trsm"] = tb.finalize()
+            st["chunks"].append(ch)
         return st
 
     def step(self, k):
@@ -453,8 +516,9 @@ class _GetrfDev:
         if self.xmode:
             self.swap_next(k)
             self.next(k)
-            self.swap_rest(k)
-            self.rest(k)
+            for c in range(len(self.plan[k]["chunks"])):
+                self.swap_rest(k, c)
+                self.rest_chunk(k, c)
             self.swap_left(k)
             return
         self.swap(k)
@@ -473,6 +537,9 @@ class _GetrfDev:
             self._panel_dist(k)
         elif A.col_is_local(k) and self.percol:
             self._panel_percol(k)
+        elif self.gxp2p:
+            self._panel_gx(k)
+            return self._panel_tail(k, pv)
         elif A.col_is_local(k):
             if g.P > 1:
                 gv = self.gbuf[: g.P * self.gmax * kb].view(g.P, self.gmax * kb)
@@ -486,8 +553,16 @@ class _GetrfDev:
             st["plu"].run(self.piv_dev, self.ws, self.cnt, self.info, r0)
             if "l21" in st:
                 ops.trsm(dplasmaRight, dplasmaUpper, N_, dplasmaNonUnit, 1.0, pv, mp, pv, mp, st["l21"])
+        return self._panel_tail(k, pv, bcast=True)
+
+    def _panel_tail(self, k, pv, bcast=False):
+        A, ctx = self.A, self.ctx
+        g = A.grid
+        st = self.plan[k]
+        kb, r0, kmin = st["kb"], st["r0"], st["kmin"]
+        pc = g.pcol(k + A.jt0)
         # --- factored panel + pivots along process rows
-        if g.Q > 1:
+        if bcast and g.Q > 1:
             root = g.rank(A.myrow, pc)
             if "rlen" in st:        # gather mode, P > 1: only this process row's tiles travel
                 rb = self.rbuf[: st["rlen"]]
@@ -510,6 +585,61 @@ class _GetrfDev:
             if self.xmode:
                 ops.rows_xord(self.mdst[par], self.msrc[par], self.mcnt[par], r0, A.mb, self.prow_t, A.myrow, g.P,
                               A.nb, self.xo[par], self.info)
+
+    def _panel_gx(self, k):
+        """Gather-mode panel on P x Q with point-to-point transfers of the exact per-step slots.  The ranks of the
+        panel's process column exchange their tiles; with RNF the ranks of the next panel's column receive every
+        slot too, and all of them factor the panel redundantly (identical pivots).  The other ranks of each process
+        row get that row's tiles of the factored panel and the pivots from the panel's column, point to point on the
+        row communicator."""
+        A, ctx = self.A, self.ctx
+        g = A.grid
+        st = self.plan[k]
+        kb = st["kb"]
+        pv = st["pv"]
+        kc = g.pcol(k + A.jt0)
+        kc1 = g.pcol(k + 1 + A.jt0) if (self.rnf and k + 1 < A.nt) else None
+        in_k = A.col_is_local(k)
+        in_k1 = kc1 is not None and A.mycol == kc1 and not in_k
+        if st.get("fac"):
+            sl = st["xslots"]
+            gb = self.gbuf
+            if in_k and st["gpack"] is not None:
+                o, n, ldq = sl[A.myrow]
+                ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, gb[o:], ldq, st["gpack"], copy=True)
+            sends, recvs = [], []
+            if in_k:
+                o, n, _ = sl[A.myrow]
+                dst = [g.rank(q, kc) for q in range(g.P) if q != A.myrow]
+                if kc1 is not None:
+                    dst += [g.rank(q, kc1) for q in range(g.P)]
+                sends = [(gb[o:o + n], d) for d in dst] if n else []
+                recvs = [(gb[sl[q][0]:sl[q][0] + sl[q][1]], g.rank(q, kc)) for q in range(g.P)
+                         if q != A.myrow and sl[q][1]]
+            else:
+                recvs = [(gb[sl[q][0]:sl[q][0] + sl[q][1]], g.rank(q, kc)) for q in range(g.P) if sl[q][1]]
+            comm.p2p(sends, recvs, group=self.g_next)
+            for q in range(g.P):   # every slot into the full panel (mine too: the pack read it from A)
+                if st["gunpack"][q] is not None:
+                    ops.geadd(0, N_, 1.0, gb[sl[q][0]:], sl[q][2], 0.0, pv, st["mp"], st["gunpack"][q], copy=True)
+            self.bytes_panel[k] = st["gsent"]
+            st["plu"].run(self.piv_dev, self.ws, self.cnt, self.info, st["r0"])
+        if g.Q > 1:
+            others = [c for c in range(g.Q) if c != kc and c != kc1]
+            mine = g.rank(A.myrow, kc)
+            if in_k and others:
+                sends = [(self.piv_dev, g.rank(A.myrow, c)) for c in others]
+                if "rlen" in st and st["rlen"]:
+                    ops.geadd(0, N_, 1.0, pv, st["pld"], 0.0, self.rbuf, st["rld"], st["rpack"], copy=True)
+                    sends += [(self.rbuf[: st["rlen"]], g.rank(A.myrow, c)) for c in others]
+                comm.p2p(sends, (), group=ctx.row_group)
+            elif not st.get("fac"):
+                recvs = [(self.piv_dev, mine)]
+                if "rlen" in st and st["rlen"]:
+                    recvs.append((self.rbuf[: st["rlen"]], mine))
+                comm.p2p((), recvs, group=ctx.row_group)
+                if "rlen" in st and st["rlen"]:
+                    ops.geadd(0, N_, 1.0, self.rbuf, st["rld"], 0.0, pv, st["pld"], st["runpack"], copy=True)
 
     def _panel_dist(self, k):
         """Distributed partial pivoting of panel k on the GPUs of its process column (see panel_mode):
@@ -700,9 +830,11 @@ class _GetrfDev:
         if hi <= lo:
             return
         g = A.grid
-        ub = self.ubuf[lo:hi]
-        if "upack" + sfx in st:
-            ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, self.ubuf, st["kb"], st["upack" + sfx], copy=True)
+        ubuf = self.ubufs[k & 1]
+        ub = ubuf[lo:hi]
+        pk = st.get("upack" + sfx) if isinstance(sfx, str) else sfx.get("upack")
+        if pk is not None:
+            ops.geadd(0, N_, 1.0, A.data, A.ld, 0.0, ubuf, st["kb"], pk, copy=True)
         root_p = g.prow(k + A.it0)
         if A.myrow == root_p:
             comm.p2p([(ub, g.rank(q, A.mycol)) for q in range(g.P) if q != root_p], (), group=group)
@@ -722,15 +854,21 @@ class _GetrfDev:
         if "ulen" in st:
             self._u_bcast(k, "_n", 0, st["ulen_n"], self.g_next)
 
-    def swap_rest(self, k):
-        """Every later trailing column: interchanges, U blocks, broadcast (update stream)."""
+    def swap_rest(self, k, c):
+        """Chunk c of the later trailing columns: interchanges, U blocks, broadcast (exchange stream)."""
         A, st = self.A, self.plan[k]
-        j0 = st["jl"] + st["jk"] + st["jn"]
-        self._xswap(k, j0, len(self.lcols), self.tmp, "rest", self.g_rest)
-        if "trsm_r" in st:
-            ops.trsm(dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, st["pv"], st["pld"], A.data, A.ld, st["trsm_r"])
-        if "ulen" in st:
-            self._u_bcast(k, "_r", st["ulen_n"], st["ulen"], self.g_rest)
+        ch = st["chunks"][c]
+        self._xswap(k, ch["j0"], ch["j1"], self.tmp, "rest", self.g_rest)
+        if "trsm" in ch:
+            ops.trsm(dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, st["pv"], st["pld"], A.data, A.ld, ch["trsm"])
+        if "ulo" in ch:
+            self._u_bcast(k, ch, ch["ulo"], ch["uhi"], self.g_rest)
+
+    def rest_chunk(self, k, c):
+        st = self.plan[k]
+        gb = st["chunks"][c].get("gemm")
+        if gb is not None:
+            ops.gemm(N_, N_, -1.0, st["pv"], st["pld"], self.ubufs[k & 1], st["kb"], 1.0, self.A.data, self.A.ld, gb)
 
     def swap_left(self, k):
         """The already factored columns (< k): only the final L needs these moves (side stream)."""
@@ -742,7 +880,7 @@ class _GetrfDev:
         st = self.plan[k]
         gb = st.get(key)
         if gb is not None:   # trailing update A(m, n) -= L(m, k) U(k, n)
-            ops.gemm(N_, N_, -1.0, st["pv"], st["pld"], self.ubuf, st["kb"], 1.0, self.A.data, self.A.ld, gb)
+            ops.gemm(N_, N_, -1.0, st["pv"], st["pld"], self.ubufs[k & 1], st["kb"], 1.0, self.A.data, self.A.ld, gb)
 
     def next(self, k):
         self._update(k, "gemm_next")
@@ -769,19 +907,34 @@ class _GetrfDev:
             # PANEL(k+1) waits for NEXT(k) only; SWAPN(k+1) for REST(k) (column k+2 carries step k's update);
             # LEFT(k) on the low-priority side stream after PANEL(k) (move lists; panel k-1 written back before
             # PANEL(k) by SWAPN(k-1) on the panel stream) -- PANEL(k+2) re-fills step k's lists, so it waits for LEFT(k)
-            lefts = {}
+            # REST(k) runs in column chunks on the update stream; SWAPR(k) chunk c (exchange stream) waits only for
+            # the chunks of REST(k-1) that updated its columns, so its transfers overlap the update of the others;
+            # SWAPN(k) waits for the chunk of REST(k-1) that updated column k+1.  PANEL(k) re-fills step k-2's panel
+            # buffer, move lists and U buffer: it waits for all of REST(k-2) and LEFT(k-2).
+            lefts, rest_of, col_chunk = {}, {}, {}
+            xs = "xch" if self.dev.type == "cuda" else "update"
             for k in range(self.kt):
-                t_p = tp.task(f"PANEL({k})", "panel", (lambda k=k: self.panel(k)), [nxt, lefts.get(k - 2)], prio=3)
-                t_n = tp.task(f"SWAPN({k})", "panel", (lambda k=k: self.swap_next(k)), [t_p, rest], prio=3)
+                st = self.plan[k]
+                t_p = tp.task(f"PANEL({k})", "panel", (lambda k=k: self.panel(k)),
+                              [nxt, lefts.get(k - 2)] + rest_of.get(k - 2, []), prio=3)
+                t_n = tp.task(f"SWAPN({k})", "panel", (lambda k=k: self.swap_next(k)),
+                              [t_p, col_chunk.get((k - 1, k + 1))], prio=3)
                 nxt = tp.task(f"NEXT({k})", "panel", (lambda k=k: self.next(k)), [t_n], prio=2)
-                t_s = tp.task(f"SWAPR({k})", "update", (lambda k=k: self.swap_rest(k)), [t_p, rest], prio=2)
-                rest = tp.task(f"REST({k})", "update", (lambda k=k: self.rest(k)), [t_s], prio=1)
-                if not self.trailing_only and self.plan[k]["jl"] > 0:
+                rest_of[k] = []
+                for c, ch in enumerate(st["chunks"]):
+                    if not ch["cols"]:
+                        continue
+                    dr = [t_p] + sorted({col_chunk[(k - 1, n)] for n in ch["cols"] if (k - 1, n) in col_chunk})
+                    t_x = tp.task(f"SWAPR{c}({k})", xs, (lambda k=k, c=c: self.swap_rest(k, c)), dr, prio=2)
+                    t_r = tp.task(f"REST{c}({k})", "update", (lambda k=k, c=c: self.rest_chunk(k, c)), [t_x], prio=1)
+                    for n in ch["cols"]:
+                        col_chunk[(k, n)] = t_r
+                    rest_of[k].append(t_r)
+                if not self.trailing_only and st["jl"] > 0:
                     lefts[k] = tp.task(f"LEFT({k})", "aux", (lambda k=k: self.swap_left(k)),
                                        [t_p, lefts.get(k - 1)], prio=0)
-            tail = [t for t in lefts.values()]
-            if tail:   # the factorisation ends with L final
-                tp.task("LEFT_JOIN", "update", (lambda: None), [rest] + tail, prio=0)
+            tail = [t for t in lefts.values()] + [t for v in rest_of.values() for t in v[-1:]] + [nxt]
+            tp.task("JOIN", "update", (lambda: None), tail, prio=0)   # the factorisation ends with L final
             return
         for k in range(self.kt):
             t_p = tp.task(f"PANEL({k})", "panel", (lambda k=k: self.panel(k)), [nxt], prio=3)

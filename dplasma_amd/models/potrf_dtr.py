@@ -441,7 +441,7 @@ class ArgsImage:
     _LL = ("ld", "ncnt", "bw_bpt", "lat_t")
     _INT = ("nt", "nranks", "rank", "epoch", "flags", "dil", "nsteps", "ntask", "nclass")
     _PTR = ("tasks", "reqs", "tab", "xoff", "cur", "hs_off", "scur", "hi", "lo", "vis", "link", "Mw", "Sw", "Lp", "Wp",
-            "prog", "info", "trace", "succ_off", "succ", "ring_of", "town", "qbase", "done", "rdy", "probe")
+            "prog", "info", "trace", "succ_off", "succ", "ring_of", "town", "qbase", "done", "rdy", "probe", "snap")
     _PARR = ("A", "recv", "W", "cnt", "pend", "qctl", "qslot")
     _IARR = ("hi_off", "lo_off")
 
@@ -614,6 +614,11 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
         probe = torch.zeros(8 + 20 * nt * nt + 8 * 4096, dtype=torch.int64, device=dev)
         img.set("probe", probe.data_ptr())
     tp.dtr_probe = probe
+    snap = None
+    if os.environ.get("DPLASMA_DTR_SNAP", "0") == "1":
+        snap = torch.zeros(nt * NBT * NBT, dtype=torch.float64, device=dev)
+        img.set("snap", snap.data_ptr())
+    tp.dtr_snap = snap
     nbytes = img.size
     host = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
     hosts = [[host, None], [torch.empty(nbytes, dtype=torch.uint8).pin_memory(), None]]
@@ -652,7 +657,7 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
             img.set(f, qk[f].data_ptr())
         for f in ("pend", "qctl", "qslot"):
             img.set(f, [qk[f].data_ptr()])
-    tp._keep = (tasks_d, reqs_d, hi_d, lo_d, tab_d, cnt, cur, hs_d, scur, W, scr, hosts, args_d, qk, probe)
+    tp._keep = (tasks_d, reqs_d, hi_d, lo_d, tab_d, cnt, cur, hs_d, scur, W, scr, hosts, args_d, qk, probe, snap)
     tp.dtr_plan = plan
     tp.dtr_sched = sched
 

@@ -56,6 +56,17 @@ def main():
             idx = torch.nonzero(d > 1e-9)
             lst = sorted((int(j), int(i), int(r), int(c), float(d[i, r, j, c])) for i, r, j, c in idx.tolist())
             msg = f" info={info} bad sub-tiles {len(lst)} first (j, i, r, c, err): {lst[:8]}"
+            snap = getattr(tp, "dtr_snap", None)
+            if snap is not None and lst:
+                # the first wrong diagonal tile: was POTRF's input wrong, or its factorisation of that input?
+                j0 = lst[0][0]
+                inp = torch.tril(snap[j0 * 512 * 512:(j0 + 1) * 512 * 512].view(512, 512).t()).cpu()
+                lj = L[j0 * 512:(j0 + 1) * 512, j0 * 512:(j0 + 1) * 512].cpu()
+                lh = torch.linalg.cholesky(inp + torch.tril(inp, -1).t())
+                gin = good[j0 * 512:(j0 + 1) * 512, j0 * 512:(j0 + 1) * 512].cpu()
+                msg += (f" | tile {j0}: |out - chol(input)| = {float((lj - lh).abs().max()):.2e}, "
+                        f"|out - good| = {float((lj - gin).abs().max()):.2e}, |chol(input) - good| = "
+                        f"{float((lh - gin).abs().max()):.2e}")
         pmsg = ""
         if probe is not None:
             pr = probe.cpu().numpy()
