@@ -540,11 +540,12 @@ __device__ __attribute__((noinline)) void run_potrf(const DtrArgs* __restrict__ 
   w_column(g, g.W[rk], k, b, g_lds);
 }
 
-// 16-byte system-scope store (global_store_dwordx4 sc0 sc1: written through to the peer's memory)
+// system-scope stores (sc0 sc1: written through to the peer's memory), two 8-byte ones -- compiler-generated, not
+// inline asm (an inline-asm dwordx4 store hides its VGPR operands from the hazard recognizer: see st_sc1_x2 in
+// potrf_tile.h and profiles/r6_dtr_coresidency_rootcause.txt)
 __device__ inline void st_sys_x2(double* p, double a, double b) {
-  typedef double d2_t __attribute__((ext_vector_type(2)));
-  const d2_t v = {a, b};
-  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+  __hip_atomic_store(p, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(p + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // copy rows x cols (column-major, both ld 512) from src to dst with the whole workgroup: 16-byte loads /

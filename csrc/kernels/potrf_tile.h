@@ -77,11 +77,14 @@ __device__ inline void spin_until(const int* flag, int target, int* info) {
 
 __device__ inline void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// 16-byte write-through store (global_store_dwordx4 sc1); drained by drain_stores()
+// two 8-byte agent-scope stores (sc1, write-through); drained by drain_stores().  Compiler-generated on purpose:
+// the former inline-asm global_store_dwordx4 was invisible to the compiler's hazard recognizer, which then let the
+// next VALU rewrite the store's address VGPRs in the following instruction -- with two workgroups per CU (two waves
+// per SIMD interleaving) the published M_k came out wrong in a few % of DTR runs while everything the workgroup kept
+// for itself was right (profiles/r6_dtr_coresidency_rootcause.txt: post-mortem of the published blocks).
 __device__ inline void st_sc1_x2(double* p, double a, double b) {
-  typedef double d2_t __attribute__((ext_vector_type(2)));
-  const d2_t v = {a, b};
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  __hip_atomic_store(p, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(p + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // acc += sum_u Y(u) X(u): A operand Y, B operand X (T-layout chunks)

@@ -12,13 +12,13 @@ import pytest
 ROOT = Path(__file__).resolve().parents[1]
 
 
-def _run(world, N, NB, extra_env=None, timeout=240):
+def _run(world, N, NB, extra_env=None, timeout=240, P=None):
     env = dict(os.environ, DPLASMA_DIST_BACKEND="gloo", PYTHONUNBUFFERED="1")
     env.update(extra_env or {})
     port = 29600 + world + (N // NB) % 50
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), str(ROOT / "tools/gpu/lu_dist_rehearsal.py"),
-           str(N), str(NB), str(world)]
+           str(N), str(NB), str(P or world)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
     out = r.stdout + r.stderr
     return r.returncode, out
@@ -39,3 +39,14 @@ def test_lu_dist_host_exchange_on_gpu():
     rc, out = _run(2, 1024, 128, {"DPLASMA_LU_XCHG": "host"})
     assert rc == 0, out[-3000:]
     assert out.count("SUCCESS") == 2 and "exchange=host" in out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("panel", ["gather", "dist"])
+def test_lu_grid_2x4_rehearsal(panel):
+    """The whole P x Q program on a 2 x 4 grid of eight processes sharing the GPU: point-to-point interchanges of the
+    rows crossing process rows, chunked trailing exchanges, look-ahead and -- gather panels -- the redundant
+    factorisation of each panel on the next panel's column (RNF).  Pivots and factors equal one process."""
+    rc, out = _run(8, 4096, 256, {"DPLASMA_LU_PANEL": panel}, timeout=400, P=2)
+    assert rc == 0, out[-3000:]
+    assert out.count("SUCCESS") == 8 and "2x4" in out

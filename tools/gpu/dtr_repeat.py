@@ -67,6 +67,40 @@ def main():
                 msg += (f" | tile {j0}: |out - chol(input)| = {float((lj - lh).abs().max()):.2e}, "
                         f"|out - good| = {float((lj - gin).abs().max()):.2e}, |chol(input) - good| = "
                         f"{float((lh - gin).abs().max()):.2e}")
+                # which 32 x 32 blocks (row block i, column block k) of the tile's factor are wrong, in dataflow order
+                e32 = (torch.tril(lj) - lh).abs().view(16, 32, 16, 32).amax(dim=(1, 3))
+                bad32 = sorted((int(k_), int(i_), float(e32[i_, k_])) for i_, k_ in torch.nonzero(e32 > 1e-9).tolist())
+                msg += f"; wrong 32-blocks (k, i, err) {[(a_, b_, f'{c_:.1e}') for a_, b_, c_ in bad32[:10]]}"
+                # post mortem of the tile's published hand-off blocks (PotrfScratch, per tile, intact after the run):
+                # Lp(i, k) (L(i,k) as published for the row blocks below) vs the factor's own L(i,k) in A, and
+                # Z_k = diag(S_k) M_k vs inv(L(k,k))
+                scr = tp._keep[10]
+                MAXB, BLK = 16, 1024
+                w_, r_, l_ = np.meshgrid(np.arange(16) // 4, np.arange(16) % 4, np.arange(64), indexing="ij")
+                e_idx = (np.arange(16)[:, None] * 64 + np.arange(64)[None, :]).ravel()
+                ww, rr, ll = (np.arange(16) // 4)[:, None].repeat(64, 1).ravel(), (np.arange(16) % 4)[:, None].repeat(64, 1).ravel(), np.tile(np.arange(64), 16)
+                rho = 16 * (ww >> 1) + (ll & 15)
+                gam = 16 * (ww & 1) + (ll >> 4) + 4 * rr
+                Lp = scr.Lp[j0 * MAXB * MAXB * BLK:(j0 + 1) * MAXB * MAXB * BLK].view(MAXB, MAXB, BLK).cpu()
+                lpbad = []
+                for i_ in range(1, 16):
+                    for k_ in range(i_):
+                        blk = torch.zeros(32, 32, dtype=torch.float64)
+                        blk[rho, gam] = Lp[i_, k_][e_idx]
+                        ref = lj[32 * i_:32 * i_ + 32, 32 * k_:32 * k_ + 32]
+                        d_ = float((blk - ref).abs().max())
+                        if d_ > 1e-9:
+                            lpbad.append((i_, k_, f"{d_:.1e}"))
+                Mw = scr.Mw[j0 * MAXB * BLK:(j0 + 1) * MAXB * BLK].view(MAXB, 32, 32).cpu()   # [k][col][row]
+                Sw = scr.Sw[j0 * MAXB * 32:(j0 + 1) * MAXB * 32].view(MAXB, 32).cpu()
+                zbad = []
+                for k_ in range(16):
+                    Z = torch.diag(Sw[k_]) @ Mw[k_].t()
+                    Lkk = lj[32 * k_:32 * k_ + 32, 32 * k_:32 * k_ + 32]
+                    d_ = float((Z @ Lkk - torch.eye(32, dtype=torch.float64)).abs().max())
+                    if d_ > 1e-8:
+                        zbad.append((k_, f"{d_:.1e}"))
+                msg += f"; published L blocks wrong (i, k, err) {lpbad[:8]} of {len(lpbad)}; Z_k wrong {zbad[:6]}"
         pmsg = ""
         if probe is not None:
             pr = probe.cpu().numpy()

@@ -4,7 +4,7 @@ the processes exactly as between GPUs of a node (gloo only carries the host-side
 tile replica and the trailing row moves):
 
   DPLASMA_DIST_BACKEND=gloo python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \\
-      tools/gpu/lu_dist_rehearsal.py [N] [NB] [P]
+      tools/gpu/lu_dist_rehearsal.py [N] [NB] [P]      (P < world: a P x world/P grid)
 
 Checks: the exchange is device-side (``ipc``), pivots are identical to the one-process factorisation
 of the same matrix on the same GPU, and the factors agree.  Prints the factorisation time and the mean
@@ -78,8 +78,10 @@ def main():
     piv1 = _gather_ipiv(lctx, IP1)
     same = bool(np.array_equal(piv, piv1))
     diff = (fac - B.to_dense_local().cpu()).abs().max().item()
-    ok = info == 0 and info1 == 0 and same and diff < 1e-8 and (mode == "ipc" or
-                                                                  os.environ.get("DPLASMA_LU_XCHG") == "host")
+    # the device exchange is required of the distributed-pivoting panel only (gather-mode panels -- factored whole
+    # by the ranks that need them, DPLASMA_LU_PANEL=gather -- have no per-column exchange)
+    need_ipc = os.environ.get("DPLASMA_LU_PANEL") == "dist" and os.environ.get("DPLASMA_LU_XCHG") != "host"
+    ok = info == 0 and info1 == 0 and same and diff < 1e-8 and (mode == "ipc" or not need_ipc)
     flags = torch.tensor([int(ok)])
     dist.all_reduce(flags, op=dist.ReduceOp.MIN)
     print(f"rank {ctx.rank}: lu dist {ctx.P}x{ctx.Q} N={N} NB={NB} exchange={mode}: {t:.3f} s, panels on this rank "

@@ -27,6 +27,14 @@ import os
 import sys
 import time
 
+# one hardware queue per modelled link stream: with HIP's default of 4 queues per process the delay streams of
+# the five communicators (and the program's panel / update / exchange / side streams) share queues, which
+# serialises transfers that run on different links (--hw-queues, default 16; set before HIP starts)
+if "--hw-queues" in sys.argv:
+    os.environ["GPU_MAX_HW_QUEUES"] = sys.argv[sys.argv.index("--hw-queues") + 1]
+else:
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -132,6 +140,7 @@ def main():
     ap.add_argument("--comm-wg", type=int, default=4)
     ap.add_argument("--xlat", type=float, default=6.0, help="us per panel column (cross-rank pivot hand-off, measured)")
     ap.add_argument("--xgmi", type=float, default=0.0, help="extra us per panel column for the xGMI hop (assumed)")
+    ap.add_argument("--hw-queues", type=int, default=16, help="GPU_MAX_HW_QUEUES for this process")
     args = ap.parse_args()
     P, Q = map(int, args.grid.lower().split("x"))
     base = dp.init(device="cuda:0")
@@ -156,7 +165,7 @@ def main():
                       "ideal_ms": round(ideal * 1e3, 2), "pct_peak": round(100 * ideal / worst, 1),
                       "tflops_job": round(fl / worst / 1e12, 1),
                       "per_rank_ms": {str(k): round(v * 1e3, 2) for k, v in res.items()},
-                      "knobs": {k: v for k, v in os.environ.items() if k.startswith("DPLASMA_")},
+                      "knobs": {k: v for k, v in os.environ.items() if k.startswith("DPLASMA_") or k == "GPU_MAX_HW_QUEUES"},
                       "comm": {k: (round(v, 1) if isinstance(v, float) else v) for k, v in be.stats.items()}}),
           flush=True)
 
