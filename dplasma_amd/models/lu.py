@@ -314,6 +314,12 @@ class _GetrfDev:
         self.plan = [self._build(k) for k in range(self.kt)]
         rl = max([st.get("rlen", 0) for st in self.plan] + [0])
         self.rbuf = torch.zeros(max(1, rl), dtype=A.dtype, device=dev) if rl else None
+        # LSEND: the panel's row transfers as a task of their own (look-ahead, gather panels on P x Q); the pivots
+        # travel from a copy (piv_dev is re-filled by the next panel while the send may still be in flight)
+        self.lsend_task = bool(self.lookahead and self.xmode and self.gxp2p and g.Q > 1)
+        self.piv_send = [torch.zeros_like(self.piv_dev), torch.zeros_like(self.piv_dev)]
+        if self.lsend_task and dev.type == "cuda" and "lsend" not in ctx.streams:
+            ctx.streams["lsend"] = torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1])
         self.bytes_panel = [0] * self.kt   # elements this rank sends per step (panel exchange)
         if self.percol:
             mlmax = max([st.get("Ml", 0) for st in self.plan] + [1])
@@ -624,22 +630,40 @@ class _GetrfDev:
                     ops.geadd(0, N_, 1.0, gb[sl[q][0]:], sl[q][2], 0.0, pv, st["mp"], st["gunpack"][q], copy=True)
             self.bytes_panel[k] = st["gsent"]
             st["plu"].run(self.piv_dev, self.ws, self.cnt, self.info, st["r0"])
+            if self.lsend_task and in_k:   # (panel stream: PANEL(k+1) re-fills piv_dev before LSEND(k) may run)
+                self.piv_send[k & 1].copy_(self.piv_dev)
         if g.Q > 1:
             others = [c for c in range(g.Q) if c != kc and c != kc1]
             mine = g.rank(A.myrow, kc)
-            if in_k and others:
-                sends = [(self.piv_dev, g.rank(A.myrow, c)) for c in others]
-                if "rlen" in st and st["rlen"]:
-                    ops.geadd(0, N_, 1.0, pv, st["pld"], 0.0, self.rbuf, st["rld"], st["rpack"], copy=True)
-                    sends += [(self.rbuf[: st["rlen"]], g.rank(A.myrow, c)) for c in others]
-                comm.p2p(sends, (), group=ctx.row_group)
-            elif not st.get("fac"):
+            if in_k and others and not self.lsend_task:
+                self._lsend(k)
+            elif not in_k and not st.get("fac"):
                 recvs = [(self.piv_dev, mine)]
                 if "rlen" in st and st["rlen"]:
                     recvs.append((self.rbuf[: st["rlen"]], mine))
                 comm.p2p((), recvs, group=ctx.row_group)
                 if "rlen" in st and st["rlen"]:
                     ops.geadd(0, N_, 1.0, self.rbuf, st["rld"], 0.0, pv, st["pld"], st["runpack"], copy=True)
+
+    def _lsend(self, k):
+        """The factored panel's rows of my process row and the pivots, from the panel's column to the other ranks of
+        the row (point to point on the row communicator).  With look-ahead a task of its own (LSEND, own stream):
+        neither the panel owner's next steps nor its trailing updates wait for these transfers."""
+        A, ctx = self.A, self.ctx
+        g = A.grid
+        if not (self.gxp2p and g.Q > 1 and A.col_is_local(k)):
+            return
+        st = self.plan[k]
+        kc = g.pcol(k + A.jt0)
+        kc1 = g.pcol(k + 1 + A.jt0) if (self.rnf and k + 1 < A.nt) else None
+        others = [c for c in range(g.Q) if c != kc and c != kc1]
+        if not others:
+            return
+        sends = [(self.piv_send[k & 1], g.rank(A.myrow, c)) for c in others]
+        if "rlen" in st and st["rlen"]:
+            ops.geadd(0, N_, 1.0, st["pv"], st["pld"], 0.0, self.rbuf, st["rld"], st["rpack"], copy=True)
+            sends += [(self.rbuf[: st["rlen"]], g.rank(A.myrow, c)) for c in others]
+        comm.p2p(sends, (), group=ctx.row_group)
 
     def _panel_dist(self, k):
         """Distributed partial pivoting of panel k on the GPUs of its process column (see panel_mode):
@@ -911,12 +935,15 @@ class _GetrfDev:
             # the chunks of REST(k-1) that updated its columns, so its transfers overlap the update of the others;
             # SWAPN(k) waits for the chunk of REST(k-1) that updated column k+1.  PANEL(k) re-fills step k-2's panel
             # buffer, move lists and U buffer: it waits for all of REST(k-2) and LEFT(k-2).
-            lefts, rest_of, col_chunk = {}, {}, {}
+            lefts, rest_of, col_chunk, lsends = {}, {}, {}, {}
             xs = "xch" if self.dev.type == "cuda" else "update"
             for k in range(self.kt):
                 st = self.plan[k]
                 t_p = tp.task(f"PANEL({k})", "panel", (lambda k=k: self.panel(k)),
-                              [nxt, lefts.get(k - 2)] + rest_of.get(k - 2, []), prio=3)
+                              [nxt, lefts.get(k - 2)] + rest_of.get(k - 2, []) + [lsends.get(k - 2)], prio=3)
+                if self.lsend_task:
+                    ls_s = "lsend" if self.dev.type == "cuda" else "update"
+                    lsends[k] = tp.task(f"LSEND({k})", ls_s, (lambda k=k: self._lsend(k)), [t_p], prio=3)
                 t_n = tp.task(f"SWAPN({k})", "panel", (lambda k=k: self.swap_next(k)),
                               [t_p, col_chunk.get((k - 1, k + 1))], prio=3)
                 nxt = tp.task(f"NEXT({k})", "panel", (lambda k=k: self.next(k)), [t_n], prio=2)
@@ -933,7 +960,8 @@ class _GetrfDev:
                 if not self.trailing_only and st["jl"] > 0:
                     lefts[k] = tp.task(f"LEFT({k})", "aux", (lambda k=k: self.swap_left(k)),
                                        [t_p, lefts.get(k - 1)], prio=0)
-            tail = [t for t in lefts.values()] + [t for v in rest_of.values() for t in v[-1:]] + [nxt]
+            tail = ([t for t in lefts.values()] + [t for v in rest_of.values() for t in v[-1:]] + [nxt]
+                    + [t for t in lsends.values()][-1:])
             tp.task("JOIN", "update", (lambda: None), tail, prio=0)   # the factorisation ends with L final
             return
         for k in range(self.kt):

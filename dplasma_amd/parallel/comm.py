@@ -257,10 +257,15 @@ def p2p(sends=(), recvs=(), group=None) -> None:
     if not sends and not recvs:
         return
     if _BACKEND is not None and hasattr(_BACKEND, "sync"):
-        per = {}
-        for t_, p_ in sends + recvs:
-            per[p_] = per.get(p_, 0) + _nbytes(t_)
-        return _BACKEND.sync("p2p", max(per.values()), group)
+        # critical link: per peer the larger direction (an xGMI link is full duplex: what I send to a peer and what
+        # it sends me travel at the same time)
+        out_b, in_b = {}, {}
+        for t_, p_ in sends:
+            out_b[p_] = out_b.get(p_, 0) + _nbytes(t_)
+        for t_, p_ in recvs:
+            in_b[p_] = in_b.get(p_, 0) + _nbytes(t_)
+        crit = max(max(out_b.get(p_, 0), in_b.get(p_, 0)) for p_ in set(out_b) | set(in_b))
+        return _BACKEND.sync("p2p", crit, group)
     _rec_p2p(sends, recvs, group)
     if _nccl():
         ops = [dist.P2POp(dist.isend, t, p, group=group) for t, p in sends]

@@ -104,9 +104,13 @@ class ReplayBackend:
         gs = self._stream(group)
         ev = torch.cuda.Event()
         ev.record(cur)
-        per_peer = {}
-        for t, p in list(sends) + list(recvs):
-            per_peer[p] = per_peer.get(p, 0) + t.numel() * t.element_size()
+        # critical link: per peer the larger direction (full-duplex xGMI links)
+        out_b, in_b = {}, {}
+        for t, p in sends:
+            out_b[p] = out_b.get(p, 0) + t.numel() * t.element_size()
+        for t, p in recvs:
+            in_b[p] = in_b.get(p, 0) + t.numel() * t.element_size()
+        per_peer = {p: max(out_b.get(p, 0), in_b.get(p, 0)) for p in set(out_b) | set(in_b)}
         if self.proxies and recvs and not sends and hint is not None:
             rs = self.remote_potrf if hint[0] == "potrf" else self.remote_trsm
             rs.wait_event(ev)
