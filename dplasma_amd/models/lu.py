@@ -158,13 +158,14 @@ class _GetrfDev:
     factorisation overlaps REST(k) -- the reference's lookahead through priorities.  Panel buffers alternate with k's parity (REST(k) still reads panel k).
 
     Panel modes for P > 1 (``DPLASMA_LU_PANEL``):
-      "dist" (default) -- the reference's distributed pivoting on the GPUs (ops.lu_dist_ops): each
+      "dist" -- the reference's distributed pivoting on the GPUs (ops.lu_dist_ops): each
                process row keeps its own panel rows plus a replica of the diagonal tile rows, and
                every column's pivot is chosen inside the persistent panel kernel through one
                cross-process hand-off (IPC-mapped exchange buffers over xGMI, epoch flags): O(NB^2)
                elements per rank and panel instead of the whole panel, no host round trip;
-      "gather" -- the panel's process column all-gathers the tall panel and every process row
-               factors it redundantly (one collective per panel, O(M NB / P) elements per rank);
+      "gather" (default) -- the panel's process column exchanges its tiles point to point (exact per-step
+               sizes) and every process row factors the tall panel redundantly with the one-process tagged
+               panel kernel (O(M NB / P) elements per rank, no per-column cross-process hand-off);
       "percol" -- the distributed pivoting driven from the host (one all-gather and two host
                syncs per column; kept as the transport-independent reference of "dist")."""
 
@@ -187,7 +188,7 @@ class _GetrfDev:
         # parity-alternating panel buffers whatever the environment says)
         # P > 1 with the point-to-point interchanges: look-ahead on by default -- the distributed panel's per-column
         # cross-process hand-offs are latency, not CU time, so they belong beside the bulk update (tools/replay_lu.py)
-        la_def = "1" if (g.P > 1 and pivot and os.environ.get("DPLASMA_LU_PANEL", "dist") != "percol"
+        la_def = "1" if (g.P > 1 and pivot and os.environ.get("DPLASMA_LU_PANEL", "gather") != "percol"
                          and os.environ.get("DPLASMA_LU_XROWS", "p2p") != "allreduce") else "0"
         self.lookahead = (os.environ.get("DPLASMA_LU_LOOKAHEAD", la_def) == "1") if lookahead is None else bool(lookahead)
         self.panel_bw = panel_bw   # base block width of the recursive panel (None: ops.LU_BW)
@@ -196,7 +197,10 @@ class _GetrfDev:
         self.piv_dev = torch.zeros(nb, dtype=torch.int32, device=dev)
         self.ipiv_all = torch.zeros(max(1, min(A.m, A.n)), dtype=torch.int32, device=dev)
         self.ws = ops.lu_workspace(A.m, dev)
-        self.panel_mode = os.environ.get("DPLASMA_LU_PANEL", "dist")
+        # gather (default): measured in the 2 x 4 rank replay against the distributed-pivoting kernel (its per-column
+        # grid barrier + cross-rank hand-off is 12-17 us per column against the one-process tagged panel's ~5,
+        # tools/gpu/lu_xlat_probe.py, profiles/r6_lu_config5.txt); the pivots are the same
+        self.panel_mode = os.environ.get("DPLASMA_LU_PANEL", "gather")
         if self.panel_mode not in ("dist", "gather", "percol"):
             raise ValueError(f"DPLASMA_LU_PANEL={self.panel_mode!r}: expected dist, gather or percol")
         self.percol = self.panel_mode == "percol" and g.P > 1 and pivot
@@ -259,10 +263,12 @@ class _GetrfDev:
         self.nch = 1
         # gather-mode panels on P x Q grids: the panel's tiles travel point to point with the exact per-step sizes
         # (packed slots; an all-gather would move the largest step's slot every step), and with DPLASMA_LU_RNF=1
-        # (default) the ranks of the NEXT panel's process column receive them too and factor panel k redundantly --
-        # the factored panel then never travels on the critical path: NEXT(k) runs on the column that factored it
+        # the ranks of the NEXT panel's process column receive them too and factor panel k redundantly -- the
+        # factored panel then never travels on the critical path, NEXT(k) runs on a column that factored it (off by
+        # default: the rank replay charges the extra factorisation and cannot credit the cross-rank chain it
+        # shortens, profiles/r6_lu_config5.txt)
         self.gxp2p = g.P > 1 and pivot and self.panel_mode == "gather"
-        self.rnf = (self.gxp2p and self.xmode and g.Q > 1 and os.environ.get("DPLASMA_LU_RNF", "1") == "1")
+        self.rnf = (self.gxp2p and self.xmode and g.Q > 1 and os.environ.get("DPLASMA_LU_RNF", "0") == "1")
         if self.xmode:
             # the rest of the trailing columns in DPLASMA_LU_CHUNKS column chunks: chunk c's interchanges / U block of
             # step k+1 (exchange stream) overlap the update of chunk c+1 of step k (update stream)

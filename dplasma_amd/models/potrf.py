@@ -69,8 +69,9 @@ POTRF_RESERVE = (0, 0)
 # operand).  Measured (profiles/r4_dtr_colorder.txt, r4_b16): 32k dtr 63-64 vs stream 61-62 TF/s; 64k dtr
 # 68.4-69.3 vs stream 69.4-70.1 (the stream engine's D = 2 deferred updates run the GEMMs at their
 # large-k rate, which the DTR's 128 x 128 x 512 update tasks do not reach); 16k dtr 38 vs 47.
-# Round 5: the DTR runs one workgroup per CU (two per CU gave an intermittent wrong factor under stress,
-# profiles/r5_dtr_coresidency.txt) and push-schedules its tasks by bottom level (profiles/r5_dtr_queue.txt):
+# Round 5: the DTR runs one workgroup per CU (two per CU gave an intermittent wrong factor under stress --
+# round 6 found and fixed the cause, an inline-asm store, profiles/r6_dtr_coresidency_rootcause.txt; one per CU
+# stays the default because it is faster) and push-schedules its tasks by bottom level (profiles/r5_dtr_queue.txt):
 # 16k 48.8 / 32k 62.0 / 64k 65.2 TF/s against the stream engine's 46.0 / 59.5-61.2 / 67.0-69.2 -> "auto" takes
 # the DTR below 48k.
 POTRF_ENGINE = "auto"

@@ -625,8 +625,9 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     args_d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     state = {"epoch": 0}
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    # one workgroup per CU by default: with two per CU the factor came out wrong in a few % of runs under
-    # stress, for reasons not found (profiles/r5_dtr_coresidency.txt); DPLASMA_DTR_WG=512 re-enables two
+    # one workgroup per CU by default: faster than two with the push scheduler at 16k / 32k / 64k (48.0 / 61.8 / 64.9
+    # vs 28.4 / 55.8 / 62.6 TF/s).  Two per CU (DPLASMA_DTR_WG=512) are correct since round 6: the intermittent wrong
+    # factor of round 5 was an inline-asm store in the tile POTRF (profiles/r6_dtr_coresidency_rootcause.txt)
     nwg = int(os.environ.get("DPLASMA_DTR_WG", ncu))
     # progress needs a workgroup on every XCD (a low list is another XCD's to steal only once that XCD's
     # own list is exhausted) and the 16 cooperating POTRF workgroups co-resident: at least 64 of them

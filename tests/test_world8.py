@@ -184,7 +184,7 @@ def test_getrf_ptgpanel_percol(world, P, prec):
 
 @pytest.mark.parametrize("world,P,prec", [(2, 2, "d"), (4, 2, "d"), (8, 4, "d"), (4, 4, "z"), (3, 3, "s"), (2, 1, "d")])
 def test_getrf_ptgpanel_dist(world, P, prec):
-    """Default P > 1 panel (ops.lu_dist_ops, zgetrf_ptgpanel.jdf GETRF_MAX / RDC / SND): every process
+    """Distributed-pivoting P > 1 panel (ops.lu_dist_ops, zgetrf_ptgpanel.jdf GETRF_MAX / RDC / SND): every process
     row keeps its own panel rows plus a replica of the diagonal tile; each column's pivot and the
     winner's whole row travel in one exchange of P candidates.  Pivots are identical to one process;
     a rank sends kmin x (2 + NB) elements to each of its P - 1 peers per panel, independent of M."""
