@@ -508,6 +508,14 @@ class _Factor:
         self.ws = ops.qr_panel_workspace(nb, nb, dt, dev)
         self.info = torch.zeros(1, dtype=torch.int32, device=dev)
         self.steps = [self._build(k) for k in range(self.kt)]
+        # VSEND (look-ahead on P x Q): the broadcasts whose root is this rank run as a task of their own after the
+        # step's panels (own stream) -- the root's next-column update does not wait for its V / T to reach the row
+        # (every root of a step on one row communicator is that row's rank of the panel column, so deferring all of
+        # them keeps each communicator's order)
+        self.vsend_task = (self.la and self.dist and A.grid.Q > 1 and os.environ.get("DPLASMA_QR_VSEND", "1") != "0")
+        self._vq, self._cur_k = {}, None
+        if self.vsend_task and dev.type == "cuda" and "vsend" not in ctx.streams:
+            ctx.streams["vsend"] = torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1])
         ups = [u for st in self.steps for e in st for u in (e.get("next"), e.get("rest"), e.get("upd")) if u]
         if self.simple or self.la:
             nx = [e["next"] for st in self.steps for e in st if e.get("next")]
@@ -837,6 +845,9 @@ class _Factor:
     def _bcast(self, e, V, Tm, root):
         """V and T along my process row (from the rank of my row that holds them); T is upper
         triangular and only its triangle travels."""
+        if self.vsend_task and self._cur_k is not None and self.A.rank == root:
+            self._vq.setdefault(self._cur_k, []).append((e, V, Tm, root))
+            return
         if self.dist and self.A.grid.Q > 1:
             comm.bcast(V[: e["ld"] * e["kf"]], root, self.ctx.row_group)
             nb = self.A.nb
@@ -854,8 +865,17 @@ class _Factor:
 
     # ---- general trees with look-ahead (self.la): V / T of entry i of step k in buffer (k % 2) * nent + i
     def panels_la(self, k):
-        for i, e in enumerate(self.steps[k]):
-            self.panel(k, e, (k % 2) * self.nent + i, pbuf=0)
+        self._cur_k = k
+        try:
+            for i, e in enumerate(self.steps[k]):
+                self.panel(k, e, (k % 2) * self.nent + i, pbuf=0)
+        finally:
+            self._cur_k = None
+
+    def vsend(self, k):
+        """The root broadcasts deferred by panels_la(k), in their order."""
+        for e, V, Tm, root in self._vq.pop(k, []):
+            self._bcast(e, V, Tm, root)
 
     def nexts_la(self, k):
         for i, e in enumerate(self.steps[k]):
@@ -912,11 +932,18 @@ def factor_New(ctx, A, TS, TT, tree, name="geqrf") -> Taskpool:
             prev = tp.task(f"qr_step({k})", "update", (lambda k=k: st.step_batched(k)), [prev])
     elif st.la:
         prev_next = prev_rest = prev_rest2 = None
+        vs = {}
         for k in range(st.kt):
-            pan = tp.task(f"qr_panel({k})", "panel", (lambda k=k: st.panels_la(k)), [prev_next, prev_rest2])
+            # V / T buffers alternate with k's parity: step k+2's panels wait for step k's deferred broadcasts too
+            pan = tp.task(f"qr_panel({k})", "panel", (lambda k=k: st.panels_la(k)), [prev_next, prev_rest2, vs.get(k - 2)])
+            if st.vsend_task:
+                vs[k] = tp.task(f"qr_vsend({k})", "vsend" if A.device.type == "cuda" else "update",
+                                (lambda k=k: st.vsend(k)), [pan])
             nxt = tp.task(f"qr_next({k})", "panel", (lambda k=k: st.nexts_la(k)), [pan, prev_rest])
             rst = tp.task(f"qr_rest({k})", "update", (lambda k=k: st.rests_la(k)), [pan, prev_rest])
             prev_next, prev_rest2, prev_rest = nxt, prev_rest, rst
+        if vs:
+            tp.task("qr_vsend_join", "update", (lambda: None), [rst] + list(vs.values())[-2:])
     else:
         prev = None
         for k in range(st.kt):
