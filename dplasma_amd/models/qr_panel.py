@@ -508,11 +508,12 @@ class _Factor:
         self.ws = ops.qr_panel_workspace(nb, nb, dt, dev)
         self.info = torch.zeros(1, dtype=torch.int32, device=dev)
         self.steps = [self._build(k) for k in range(self.kt)]
-        # VSEND (look-ahead on P x Q): the broadcasts whose root is this rank run as a task of their own after the
-        # step's panels (own stream) -- the root's next-column update does not wait for its V / T to reach the row
-        # (every root of a step on one row communicator is that row's rank of the panel column, so deferring all of
-        # them keeps each communicator's order)
-        self.vsend_task = (self.la and self.dist and A.grid.Q > 1 and os.environ.get("DPLASMA_QR_VSEND", "1") != "0")
+        # VSEND (look-ahead on P x Q, DPLASMA_QR_VSEND=1): the broadcasts whose root is this rank run as a task of
+        # their own after the step's panels (own stream) -- the root's next-column update does not wait for its V / T
+        # to reach the row (every root of a step on one row communicator is that row's rank of the panel column, so
+        # deferring all of them keeps each communicator's order).  Off by default: 2 x 4 64k rank replay 41.1 % with,
+        # 43.6 % without (profiles/r6_hqr_config4.txt)
+        self.vsend_task = (self.la and self.dist and A.grid.Q > 1 and os.environ.get("DPLASMA_QR_VSEND", "0") == "1")
         self._vq, self._cur_k = {}, None
         if self.vsend_task and dev.type == "cuda" and "vsend" not in ctx.streams:
             ctx.streams["vsend"] = torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1])

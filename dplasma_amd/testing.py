@@ -84,6 +84,12 @@ class Harness:
         self.a = a
         world = int(os.environ.get("WORLD_SIZE", "1"))
         import torch.distributed as dist
+        if world > 1:
+            # P x Q stream programs (LU / QR / Cholesky look-ahead) keep panel, update, exchange and side streams plus
+            # one stream per communicator busy at once: one hardware queue each, or HIP's default of 4 per process
+            # serialises them (2 x 4 LU rank replay: 32.5 % with 4 queues, 40.2 % with 16 -- profiles/r6_lu_config5.txt).
+            # Must be set before HIP starts (torch.cuda.is_available() below starts it).
+            os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
         use_gpu = torch.cuda.is_available() and a.gpus != 0
         if world > 1 and not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
