@@ -56,6 +56,14 @@ struct dplasma_qrtree_s {
 };
 #endif
 PyObject* dpl_arg_qrtree(const dplasma_qrtree_t* q);
+// trees of native descriptors (native_qrtree.cpp): q->args is the C++ tree, the queries answer from it
+namespace nq { class Tree; }
+bool nat_qrtree_is(const dplasma_qrtree_t* q);
+nq::Tree* nat_qrtree(const dplasma_qrtree_t* q);
+int nat_qrtree_init(dplasma_qrtree_t* q, const char* kind, int trans, dplasma_desc_t* A, std::initializer_list<int> ints);
+void nat_qrtree_fini(dplasma_qrtree_t* q);
+int nat_qrtree_check(const dplasma_qrtree_t* q);
+void nat_qrtree_print(const dplasma_qrtree_t* q, const char* what, int k, int* perm, const char* file);
 // an opaque framework object handed to C earlier (butterfly vectors): a new reference to it
 PyObject* dpl_arg_obj(const void* h);
 // "call" returning an object: stored as a new reference in *out (0), or -1

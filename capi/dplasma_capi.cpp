@@ -217,10 +217,7 @@ static int qt_prevpiv(const dplasma_qrtree_t* q, int k, int p, int m) { return q
 // kind: "hqr" / "systolic" / "svd"; ints: that init's integer parameters (capi.qrtree_init)
 static int qt_init(dplasma_qrtree_t* q, const char* kind, int trans, dplasma_desc_t* A, std::initializer_list<int> ints) {
   if (!q || !A) return -1;
-  if (!A->obj) {
-    g_err = "QR trees need a framework (Python) descriptor; native contexts have no tree-based QR";
-    return -1;
-  }
+  if (!A->obj) return nat_qrtree_init(q, kind, trans, A, ints);   // a native descriptor: the C++ tree (native_qrtree.cpp)
   DplGil g;
   g_err.clear();
   PyObject* il = PyTuple_New((Py_ssize_t)ints.size());
@@ -251,6 +248,7 @@ static int qt_init(dplasma_qrtree_t* q, const char* kind, int trans, dplasma_des
 }
 
 static void qt_fini(dplasma_qrtree_t* q) {
+  if (nat_qrtree_is(q)) return nat_qrtree_fini(q);
   if (!q || !q->args) return;
   DplGil g;
   Py_DECREF((PyObject*)q->args);
@@ -259,6 +257,7 @@ static void qt_fini(dplasma_qrtree_t* q) {
 
 static void qt_print(dplasma_desc_t* A, dplasma_qrtree_t* q, const char* what, int k, int* perm, const char* file) {
   (void)A;
+  if (nat_qrtree_is(q)) return nat_qrtree_print(q, what, k, perm, file);
   if (!q || !q->args) return;
   DplGil g;
   PyObject* r = call_obj(nullptr, "qrtree_print", nullptr,
@@ -285,6 +284,7 @@ DPL_CAPI int dplasma_svd_init(dplasma_qrtree_t* q, int trans, dplasma_desc_t* A,
 DPL_CAPI void dplasma_svd_finalize(dplasma_qrtree_t* q) { qt_fini(q); }
 DPL_CAPI int dplasma_qrtree_check(dplasma_desc_t* A, dplasma_qrtree_t* q) {
   (void)A;
+  if (nat_qrtree_is(q)) return nat_qrtree_check(q);
   if (!q || !q->args) return -1;
   DplGil g;
   g_err.clear();
