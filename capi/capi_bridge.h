@@ -176,6 +176,22 @@ int nat_hetrs(dplasma_context_t* ctx, int prec, int uplo, dplasma_desc_t* A, dpl
 int nat_gebmm(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, const void* U, int level, int trans);
 int nat_gebut(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, const void* U, int level);
 int nat_hebut(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, void** U_out, int level);
+NatProgram* nat_geqrf_param(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* A, dplasma_desc_t* TS,
+                            dplasma_desc_t* TT);
+NatProgram* nat_gelqf_param(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* A, dplasma_desc_t* TS,
+                            dplasma_desc_t* TT);
+NatProgram* nat_unmqr_param(dplasma_context_t* ctx, int prec, int side, int trans, dplasma_qrtree_t* q, dplasma_desc_t* A,
+                            dplasma_desc_t* TS, dplasma_desc_t* TT, dplasma_desc_t* C);
+NatProgram* nat_unmlq_param(dplasma_context_t* ctx, int prec, int side, int trans, dplasma_qrtree_t* q, dplasma_desc_t* A,
+                            dplasma_desc_t* TS, dplasma_desc_t* TT, dplasma_desc_t* C);
+NatProgram* nat_ungqr_param(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* A, dplasma_desc_t* TS,
+                            dplasma_desc_t* TT, dplasma_desc_t* Q);
+NatProgram* nat_unglq_param(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* A, dplasma_desc_t* TS,
+                            dplasma_desc_t* TT, dplasma_desc_t* Q);
+NatProgram* nat_geqrs_param(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* A, dplasma_desc_t* TS,
+                            dplasma_desc_t* TT, dplasma_desc_t* B);
+NatProgram* nat_gelqs_param(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* A, dplasma_desc_t* TS,
+                            dplasma_desc_t* TT, dplasma_desc_t* B);
 NatProgram* nat_trdsm(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* B);
 NatProgram* nat_trmdm(dplasma_context_t* ctx, int prec, dplasma_desc_t* A);
 int nat_latms(dplasma_context_t* ctx, int prec, int mtxtype, double cond, dplasma_desc_t* A, unsigned long long seed);

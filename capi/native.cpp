@@ -24,6 +24,7 @@
 
 #include "native_comm.h"
 #include "native_internal.h"
+#include "native_qrtree.h"
 
 
 namespace {
@@ -2867,6 +2868,541 @@ NatProgram* nat_gels(dplasma_context_t* ctx, int prec, int trans, dplasma_desc_t
     if (!P->info || !add_gelqf(*P, *A, *T, last) || !add_gelqs(*P, *A, *T, *B, last))
       return fail(P, "gels: device allocation failed");
   }
+  return P;
+}
+
+// ----------------------------------------------------------------------------- tree-driven QR / LQ (*_param)
+// dplasma_zgeqrf_param and its family (reference src/zgeqrf_param.jdf, zunmqr_param*.jdf, zungqr_param.jdf) on
+// one process, driven by a native reduction tree (native_qrtree.cpp).  Each panel step k follows the tree's
+// plan: every TS domain (a GEQRT head with the rows it TS-kills) is ONE stacked Householder panel (rows
+// gathered into a panel buffer, dpl_qr_panel, written back: R in the head tile, V below the diagonal and in
+// the killed tiles), then every TT kill (p, m) in plan order is the panel of the two stacked triangles
+// [R_p; R_m] (V = [I; V2], V2 upper triangular into A(m, k)'s upper part, A(p, k)'s R replaced) -- the
+// stacked-domain design of models/qr_panel.py, with the same trailing update C -= V op(T) (V^H C) as three
+// batched MFMA GEMM launches per entry.  T: the full nb x nb compact-WY factor of every entry in a slot of the
+// TS (domains) / TT (kills) descriptor's side buffer, its IB x IB diagonal blocks in the reference-layout
+// tile TS(head, k) / TT(m, k) (LQ: tile (k, row)).  The apply rebuilds each entry's V from A and replays the
+// entries forward (Q^H) or backward (Q).  The LQ variants run the QR engine on A^H (native gelqf's scheme).
+namespace {
+
+struct QpEntry {
+  bool tt = false;
+  std::vector<int> rows, voff;   // tile rows (rows[0]: head / annihilator) and their offsets in the stack
+  int M = 0, kf = 0, k = 0;
+  int trow = 0;                  // T slot row: the domain head / the TT-killed row
+};
+
+// the entries of every panel step, in execution order
+std::vector<std::vector<QpEntry>> qp_entries(const nq::Tree& t, const NatDesc& A) {
+  const int kt = std::min(A.mt, A.nt);
+  std::vector<std::vector<QpEntry>> out(kt);
+  for (int k = 0; k < kt; ++k) {
+    std::vector<int> heads;
+    std::vector<nq::Kill> kills;
+    t.plan(k, heads, kills);
+    const int kb = A.cols(k);
+    for (int h : heads) {
+      QpEntry e;
+      e.k = k;
+      e.rows.push_back(h);
+      for (const nq::Kill& x : kills)
+        if (x.type == nq::KILLED_BY_TS && x.piv == h) e.rows.push_back(x.m);
+      e.trow = h;
+      out[k].push_back(e);
+    }
+    for (const nq::Kill& x : kills) {
+      if (x.type == nq::KILLED_BY_TS) continue;
+      QpEntry e;
+      e.tt = true;
+      e.k = k;
+      e.rows = {x.piv, x.m};
+      e.trow = x.m;
+      out[k].push_back(e);
+    }
+    for (QpEntry& e : out[k]) {
+      int c = 0;
+      for (int r : e.rows) {
+        e.voff.push_back(c);
+        c += A.rows(r);
+      }
+      e.M = c;
+      e.kf = std::min(c, kb);
+    }
+  }
+  return out;
+}
+
+bool tree_fits(const nq::Tree* t, const NatDesc& A) { return t && t->mt == A.mt && t->nt == A.nt; }
+
+// C(rows_i, cols) := op(H) C(rows_i, cols), H = I - V T V^H, V rows = the stacked rows (row tile i at voff_i of V)
+bool add_left_apply_rows(NatProgram& P, int prec, NatDesc& C, const std::vector<int>& rows, const std::vector<int>& voff,
+                         int kf, char* V, int ldv, char* Tk, int ldt, bool qt, char* W, char* W2,
+                         const std::vector<int>& cols, int stream, int dep, int& out) {
+  out = dep;
+  if (cols.empty() || kf <= 0) return true;
+  const Scalar one(prec, 1.0), zero(prec, 0.0), m_one(prec, -1.0);
+  auto g1 = std::make_shared<Gemm>(), g2 = std::make_shared<Gemm>(), g3 = std::make_shared<Gemm>();
+  long long wo = 0;
+  for (int j : cols) {
+    const int nj = C.cols(j);
+    std::vector<KPair> kp;
+    for (size_t i = 0; i < rows.size(); ++i) kp.push_back(KPair{voff[i], C.off(rows[i], j), C.rows(rows[i]), 0});
+    g1->add(wo, kf, nj, kp, 0);
+    g2->add(wo, kf, nj, {KPair{0, wo, kf, 0}}, 0);
+    for (size_t i = 0; i < rows.size(); ++i)
+      g3->add(C.off(rows[i], j), C.rows(rows[i]), nj, {KPair{voff[i], wo, kf, 0}}, 0);
+    wo += (long long)kf * nj;
+  }
+  if (!g1->upload(P) || !g2->upload(P) || !g3->upload(P)) return false;
+  char* c = C.data;
+  const int ldc = C.lld;
+  int t = P.task(stream, [=](hipStream_t s) { return g1->launch(prec, CONJTRANS, NOTRANS, one, V, ldv, c, ldc, zero, W, kf, s); },
+                 {dep});
+  t = P.task(stream, [=](hipStream_t s) {
+    return g2->launch(prec, qt ? CONJTRANS : NOTRANS, NOTRANS, one, Tk, ldt, W, kf, zero, W2, kf, s);
+  }, {t});
+  out = P.task(stream, [=](hipStream_t s) { return g3->launch(prec, NOTRANS, NOTRANS, m_one, V, ldv, W2, kf, one, c, ldc, s); },
+               {t});
+  return true;
+}
+
+// C(:, cols_i) := C(:, cols_i) op(H) (right; C's column tile cols_i pairs with V's row tile i): W = sum C V_i,
+// W2 = W op(T), C(:, cols_i) -= W2 V_i^H
+bool add_right_apply_rows(NatProgram& P, int prec, NatDesc& C, const std::vector<int>& rows, const std::vector<int>& voff,
+                          int kf, char* V, int ldv, char* Tk, int ldt, bool qt, char* W, char* W2, int ldw, int stream,
+                          int dep, int& out) {
+  out = dep;
+  if (kf <= 0 || C.mt == 0) return true;
+  const Scalar one(prec, 1.0), zero(prec, 0.0), m_one(prec, -1.0);
+  auto g1 = std::make_shared<Gemm>(), g2 = std::make_shared<Gemm>(), g3 = std::make_shared<Gemm>();
+  for (int i = 0; i < C.mt; ++i) {
+    const long long wo = (long long)i * C.mb;
+    std::vector<KPair> kp;
+    for (size_t r = 0; r < rows.size(); ++r) kp.push_back(KPair{C.off(i, rows[r]), voff[r], C.cols(rows[r]), 0});
+    g1->add(wo, C.rows(i), kf, kp, 0);
+    g2->add(wo, C.rows(i), kf, {KPair{wo, 0, kf, 0}}, 0);
+    for (size_t r = 0; r < rows.size(); ++r)
+      g3->add(C.off(i, rows[r]), C.rows(i), C.cols(rows[r]), {KPair{wo, voff[r], kf, 0}}, 0);
+  }
+  if (!g1->upload(P) || !g2->upload(P) || !g3->upload(P)) return false;
+  char* c = C.data;
+  const int ldc = C.lld;
+  int t = P.task(stream, [=](hipStream_t s) { return g1->launch(prec, NOTRANS, NOTRANS, one, c, ldc, V, ldv, zero, W, ldw, s); },
+                 {dep});
+  t = P.task(stream, [=](hipStream_t s) {
+    return g2->launch(prec, NOTRANS, qt ? CONJTRANS : NOTRANS, one, W, ldw, Tk, ldt, zero, W2, ldw, s);
+  }, {t});
+  out = P.task(stream, [=](hipStream_t s) {
+    return g3->launch(prec, NOTRANS, CONJTRANS, m_one, W2, ldw, V, ldv, one, c, ldc, s);
+  }, {t});
+  return true;
+}
+
+// tile copies between A(rows_i, k) and the stack (part: 0 full, 2 upper incl. the diagonal, tile coordinates)
+int add_stack_copy(NatProgram& P, const NatDesc& A, const QpEntry& e, char* buf, int ldb, bool to_stack, int part,
+                   int stream, int dep) {
+  std::vector<TileItem> it;
+  const int kb = A.cols(e.k);
+  for (size_t i = 0; i < e.rows.size(); ++i) {
+    const long long ao = A.off(e.rows[i], e.k), so = e.voff[i];
+    it.push_back(to_stack ? TileItem{ao, so, A.rows(e.rows[i]), kb, 0, 0} : TileItem{so, ao, A.rows(e.rows[i]), kb, 0, 0});
+  }
+  auto d = dev_upload(it);
+  if (!d) return -2;
+  P.keep.push_back(d);
+  const int n = (int)it.size(), prec = A.prec, lda = A.lld, mb = A.mb;
+  char* a = A.data;
+  const Scalar one(prec, 1.0), zero(prec, 0.0);
+  return P.task(stream, [=](hipStream_t s) {
+    return to_stack ? dpl_geadd(prec, part, NOTRANS, n, d->p, mb, kb, one.ptr(), a, lda, zero.ptr(), buf, ldb, 1, s)
+                    : dpl_geadd(prec, part, NOTRANS, n, d->p, mb, kb, one.ptr(), buf, ldb, zero.ptr(), a, lda, 1, s);
+  }, {dep});
+}
+
+// an entry's explicit V (unit diagonal, zeros above) rebuilt from the factored A into V (ld ldv)
+int add_entry_v(NatProgram& P, const NatDesc& A, const QpEntry& e, char* V, int ldv, int stream, int dep) {
+  const int prec = A.prec, kb = A.cols(e.k), mb = A.mb, lda = A.lld;
+  std::vector<TileItem> lt, ct;
+  for (size_t i = 0; i < e.rows.size(); ++i) {
+    const int r = e.rows[i];
+    lt.push_back(TileItem{0, e.voff[i], A.rows(r), kb, e.voff[i], 0});   // stacked diagonal ones, zeros elsewhere
+    if (e.tt) {
+      if (i == 1) ct.push_back(TileItem{A.off(r, e.k), e.voff[i], A.rows(r), kb, 0, 0});   // V2: the upper part
+    } else {
+      ct.push_back(TileItem{A.off(r, e.k), e.voff[i], A.rows(r), kb, e.voff[i], 0});       // strictly below the stacked diagonal
+    }
+  }
+  for (TileItem& x : lt) std::swap(x.a_off, x.b_off);   // laset items address B through a_off
+  auto dl = dev_upload(lt), dc = dev_upload(ct);
+  if (!dl || !dc) return -2;
+  P.keep.push_back(dl);
+  P.keep.push_back(dc);
+  const int nl = (int)lt.size(), nc = (int)ct.size(), part = e.tt ? 2 : 3;
+  char* a = A.data;
+  const Scalar zero(prec, 0.0), one(prec, 1.0);
+  const int t = P.task(stream, [=](hipStream_t s) {
+    return dpl_laset(prec, 0, nl, dl->p, mb, kb, zero.ptr(), one.ptr(), V, ldv, s);
+  }, {dep});
+  return P.task(stream, [=](hipStream_t s) {
+    return dpl_geadd(prec, part, NOTRANS, nc, dc->p, mb, kb, one.ptr(), a, lda, zero.ptr(), V, ldv, 1, s);
+  }, {t});
+}
+
+struct QpBufs {
+  DevPtr P, V, W, W2, ws;
+  int ld = 0;
+};
+
+bool qp_bufs(NatProgram& P, const NatDesc& A, const std::vector<std::vector<QpEntry>>& ents, size_t wlen, QpBufs& b) {
+  int maxM = 16;
+  for (const auto& st : ents)
+    for (const QpEntry& e : st) maxM = std::max(maxM, e.M);
+  b.ld = (maxM + 15) / 16 * 16;
+  const int es = A.es, nb = A.nb;
+  b.P = dev_alloc((size_t)b.ld * nb * es, true);
+  b.V = dev_alloc((size_t)b.ld * nb * es, true);
+  b.W = dev_alloc(wlen * es, false);
+  b.W2 = dev_alloc(wlen * es, false);
+  b.ws = dev_alloc((size_t)dpl_qr_panel_ws_bytes(A.prec, nb, nb) + 256, true);
+  for (const DevPtr& d : {b.P, b.V, b.W, b.W2, b.ws}) {
+    if (!d) return false;
+    P.keep.push_back(d);
+  }
+  return true;
+}
+
+// T slots: one nb x nb factor per (trow, k) of the entries of one kind, in the descriptor's side buffer
+bool qp_slots(NatProgram& P, NatDesc& T, const NatDesc& A, const std::vector<std::vector<QpEntry>>& ents, bool tt) {
+  const int kt = (int)ents.size(), nb = A.nb;
+  T.tidx.assign((size_t)kt * A.mt, -1);
+  T.tidx_mt = A.mt;
+  long long n = 0;
+  for (const auto& st : ents)
+    for (const QpEntry& e : st)
+      if (e.tt == tt) T.tidx[(size_t)e.k * A.mt + e.trow] = n++;
+  T.fullT = dev_alloc((size_t)std::max(1LL, n) * nb * nb * A.es, true);
+  T.fullT_nb = nb;
+  T.fullT_kt = -1;   // not a flat-tree T: the plain unmqr / ungqr refuse it
+  if (!T.fullT) return false;
+  P.keep.push_back(T.fullT);
+  return true;
+}
+
+char* qp_slot(const NatDesc& T, const QpEntry& e) {
+  const long long s = T.tidx[(size_t)e.k * T.tidx_mt + e.trow];
+  return s < 0 ? nullptr : (char*)T.fullT->p + (size_t)s * T.fullT_nb * T.fullT_nb * T.es;
+}
+
+bool tree_T_ok(const NatDesc& T, const NatDesc& A, const std::vector<std::vector<QpEntry>>& ents, bool tt) {
+  if (!T.fullT || T.fullT_nb != A.nb || T.tidx_mt != A.mt || T.tidx.size() < ents.size() * (size_t)A.mt) return false;
+  for (const auto& st : ents)
+    for (const QpEntry& e : st)
+      if (e.tt == tt && T.tidx[(size_t)e.k * A.mt + e.trow] < 0) return false;
+  return true;
+}
+
+// lq: the reference-layout diagonal blocks go to tile (k, trow) of the T descriptor (the LQ T layout)
+bool add_geqrf_param(NatProgram& P, const nq::Tree& tree, NatDesc& A, NatDesc& TS, NatDesc& TT, bool lq, int& last) {
+  const int prec = A.prec, nb = A.nb, es = A.es;
+  const auto ents = qp_entries(tree, A);
+  QpBufs b;
+  if (!qp_bufs(P, A, ents, (size_t)nb * std::max(1, A.n), b) || !qp_slots(P, TS, A, ents, false) ||
+      !qp_slots(P, TT, A, ents, true))
+    return false;
+  int* info = (int*)P.info->p;
+  char *pb = (char*)b.P->p, *vb = (char*)b.V->p, *ws = (char*)b.ws->p;
+  const int ld = b.ld;
+  int prev = last;
+  for (const auto& st : ents) {
+    for (const QpEntry& e : st) {
+      const int k = e.k, kb = A.cols(k), M = e.M, kf = e.kf;
+      NatDesc& Td = e.tt ? TT : TS;
+      char* Tk = qp_slot(Td, e);
+      if (e.tt) {   // the stack of two triangles: zeros below them
+        prev = P.task(0, [=](hipStream_t s) { return (int)hipMemsetAsync(pb, 0, (size_t)ld * kb * es, s); }, {prev});
+      }
+      prev = add_stack_copy(P, A, e, pb, ld, true, e.tt ? 2 : 0, 0, prev);
+      if (prev < -1) return false;
+      prev = P.task(0, [=](hipStream_t s) { return dpl_qr_panel(prec, pb, ld, 0, 0, M, kb, kf, vb, ld, Tk, nb, ws, info, s); },
+                    {prev});
+      prev = add_stack_copy(P, A, e, pb, ld, false, e.tt ? 2 : 0, 0, prev);
+      if (prev < -1) return false;
+      // reference layout: the IB x IB diagonal blocks of T into tile (trow, k) (LQ: (k, trow)) when it exists
+      const int ti = lq ? k : e.trow, tj = lq ? e.trow : k;
+      if (ti < Td.mt && tj < Td.nt) {
+        const int ib = Td.mb;
+        std::vector<TileItem> it;
+        for (int b0 = 0; b0 < kf; b0 += ib) {
+          const int bs = std::min(ib, kf - b0);
+          it.push_back(TileItem{b0 + (long long)b0 * nb, Td.off(ti, tj) + (long long)b0 * Td.lld, bs, bs, 0, 0});
+        }
+        auto d = dev_upload(it);
+        if (!d) return false;
+        P.keep.push_back(d);
+        const int n = (int)it.size(), ldT = Td.lld;
+        char* td = Td.data;
+        const Scalar one(prec, 1.0), zero(prec, 0.0);
+        prev = P.task(0, [=](hipStream_t s) {
+          return dpl_geadd(prec, 0, NOTRANS, n, d->p, ib, ib, one.ptr(), Tk, nb, zero.ptr(), td, ldT, 1, s);
+        }, {prev});
+      }
+      std::vector<int> cols;
+      for (int j = k + 1; j < A.nt; ++j) cols.push_back(j);
+      int out = prev;
+      if (!add_left_apply_rows(P, prec, A, e.rows, e.voff, kf, vb, ld, Tk, nb, true, (char*)b.W->p, (char*)b.W2->p, cols, 0,
+                               prev, out))
+        return false;
+      prev = out;
+    }
+  }
+  last = prev;
+  return true;
+}
+
+// C := op(Q) C (left) or C op(Q) (right), Q from add_geqrf_param of A with the same tree
+bool add_unmqr_param(NatProgram& P, const nq::Tree& tree, int side, int trans, NatDesc& A, NatDesc& TS, NatDesc& TT,
+                     NatDesc& C, int& last) {
+  const int prec = A.prec, nb = A.nb;
+  const bool left = side == LEFT, qt = trans != NOTRANS;
+  const auto ents = qp_entries(tree, A);
+  if (!tree_T_ok(TS, A, ents, false) || !tree_T_ok(TT, A, ents, true)) return false;
+  std::vector<const QpEntry*> order;
+  for (const auto& st : ents)
+    for (const QpEntry& e : st) order.push_back(&e);
+  // left: Q^H C replays the factorisation order, Q C the reverse; right: C Q in order, C Q^H reversed
+  if (left ? !qt : qt) std::reverse(order.begin(), order.end());
+  const int ldw = std::max(16, (C.m + 15) / 16 * 16);
+  const size_t wlen = left ? (size_t)nb * std::max(1, C.n) : (size_t)ldw * nb;
+  QpBufs b;
+  if (!qp_bufs(P, A, ents, wlen, b)) return false;
+  char* vb = (char*)b.V->p;
+  int prev = last;
+  for (const QpEntry* e : order) {
+    prev = add_entry_v(P, A, *e, vb, b.ld, 1, prev);
+    if (prev < -1) return false;
+    char* Tk = qp_slot(e->tt ? TT : TS, *e);
+    int out = prev;
+    bool ok;
+    if (left) {
+      std::vector<int> cols;
+      for (int j = 0; j < C.nt; ++j) cols.push_back(j);
+      ok = add_left_apply_rows(P, prec, C, e->rows, e->voff, e->kf, vb, b.ld, Tk, nb, qt, (char*)b.W->p, (char*)b.W2->p,
+                               cols, 1, prev, out);
+    } else {
+      ok = add_right_apply_rows(P, prec, C, e->rows, e->voff, e->kf, vb, b.ld, Tk, nb, qt, (char*)b.W->p,
+                                (char*)b.W2->p, ldw, 1, prev, out);
+    }
+    if (!ok) return false;
+    prev = out;
+  }
+  last = prev;
+  return true;
+}
+
+bool param_conform(const NatDesc* A, const NatDesc* TS, const NatDesc* TT) {
+  return A && TS && TT && A->mb == A->nb && A->nb <= 256 && TS->nb == A->nb && TT->nb == A->nb && TS->mb >= 1 &&
+         TT->mb >= 1 && TS->mb <= A->nb && TT->mb <= A->nb;
+}
+
+}  // namespace
+
+NatProgram* nat_geqrf_param(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* dA,
+                            dplasma_desc_t* dTS, dplasma_desc_t* dTT) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *TS = dTS ? dTS->nat : nullptr, *TT = dTT ? dTT->nat : nullptr;
+  const nq::Tree* t = nat_qrtree(q);
+  if (!same_ctx(c, {A, TS, TT}, prec)) return fail(nullptr, "geqrf_param: descriptors of another context or precision");
+  if (!param_conform(A, TS, TT)) return fail(nullptr, "geqrf_param: square tiles <= 256 and TS / TT of (IB x NB) tiles");
+  if (!tree_fits(t, *A)) return fail(nullptr, "geqrf_param: a native tree built for A's tile rows and columns");
+  NatProgram* P = new_program(c, "geqrf_param", true);
+  int last = -1;
+  if (!P->info || !add_geqrf_param(*P, *t, *A, *TS, *TT, false, last)) return fail(P, "geqrf_param: device allocation failed");
+  return P;
+}
+
+NatProgram* nat_unmqr_param(dplasma_context_t* ctx, int prec, int side, int trans, dplasma_qrtree_t* q,
+                            dplasma_desc_t* dA, dplasma_desc_t* dTS, dplasma_desc_t* dTT, dplasma_desc_t* dC) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *TS = dTS ? dTS->nat : nullptr, *TT = dTT ? dTT->nat : nullptr,
+          *C = dC ? dC->nat : nullptr;
+  const nq::Tree* t = nat_qrtree(q);
+  if (!same_ctx(c, {A, TS, TT, C}, prec)) return fail(nullptr, "unmqr_param: descriptors of another context or precision");
+  if (!param_conform(A, TS, TT) || !tree_fits(t, *A)) return fail(nullptr, "unmqr_param: operands of geqrf_param");
+  if ((side == LEFT && (C->m != A->m || C->mb != A->mb)) || (side == RIGHT && (C->n != A->m || C->nb != A->mb)))
+    return fail(nullptr, "unmqr_param: C does not conform to Q");
+  NatProgram* P = new_program(c, "unmqr_param", false);
+  int last = -1;
+  if (!add_unmqr_param(*P, *t, side, trans, *A, *TS, *TT, *C, last))
+    return fail(P, "unmqr_param: TS / TT must come from the native geqrf_param of A with this tree");
+  return P;
+}
+
+NatProgram* nat_ungqr_param(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* dA,
+                            dplasma_desc_t* dTS, dplasma_desc_t* dTT, dplasma_desc_t* dQ) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *TS = dTS ? dTS->nat : nullptr, *TT = dTT ? dTT->nat : nullptr,
+          *Q = dQ ? dQ->nat : nullptr;
+  const nq::Tree* t = nat_qrtree(q);
+  if (!same_ctx(c, {A, TS, TT, Q}, prec)) return fail(nullptr, "ungqr_param: descriptors of another context or precision");
+  if (!param_conform(A, TS, TT) || !tree_fits(t, *A) || Q->m != A->m || Q->mb != A->mb || Q->n > A->m)
+    return fail(nullptr, "ungqr_param: operands of geqrf_param, Q with A's rows");
+  NatProgram* P = new_program(c, "ungqr_param", false);
+  std::vector<TileItem> it;
+  for (int i = 0; i < Q->mt; ++i)
+    for (int j = 0; j < Q->nt; ++j) it.push_back(TileItem{Q->off(i, j), 0, Q->rows(i), Q->cols(j), i * Q->mb, j * Q->nb});
+  auto d_it = dev_upload(it);
+  if (!d_it) return fail(P, "ungqr_param: device allocation failed");
+  P->keep.push_back(d_it);
+  const int n = (int)it.size(), mb = Q->mb, nb = Q->nb, ldq = Q->lld;
+  char* qd = Q->data;
+  const Scalar zero(prec, 0.0), one(prec, 1.0);
+  int last = P->task(1, [=](hipStream_t s) { return dpl_laset(prec, 0, n, d_it->p, mb, nb, zero.ptr(), one.ptr(), qd, ldq, s); },
+                     {});
+  if (!add_unmqr_param(*P, *t, LEFT, NOTRANS, *A, *TS, *TT, *Q, last))
+    return fail(P, "ungqr_param: TS / TT must come from the native geqrf_param of A with this tree");
+  return P;
+}
+
+NatProgram* nat_geqrs_param(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* dA,
+                            dplasma_desc_t* dTS, dplasma_desc_t* dTT, dplasma_desc_t* dB) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *TS = dTS ? dTS->nat : nullptr, *TT = dTT ? dTT->nat : nullptr,
+          *B = dB ? dB->nat : nullptr;
+  const nq::Tree* t = nat_qrtree(q);
+  if (!same_ctx(c, {A, TS, TT, B}, prec)) return fail(nullptr, "geqrs_param: descriptors of another context or precision");
+  if (!param_conform(A, TS, TT) || !tree_fits(t, *A) || A->m < A->n || B->m != A->m || B->mb != A->mb)
+    return fail(nullptr, "geqrs_param: operands of geqrf_param of an M >= N matrix, B with A's rows");
+  NatProgram* P = new_program(c, "geqrs_param", false);
+  int last = -1;
+  if (!add_unmqr_param(*P, *t, LEFT, CONJTRANS, *A, *TS, *TT, *B, last))
+    return fail(P, "geqrs_param: TS / TT must come from the native geqrf_param of A with this tree");
+  auto R = lead_view(*A, A->n, A->n), X = lead_view(*B, A->n, B->n);
+  P->wdesc.push_back(R);
+  P->wdesc.push_back(X);
+  if (!add_trsm(*P, LEFT, UPPER, NOTRANS, NONUNIT, Scalar(prec, 1.0), *R, *X, 1, last))
+    return fail(P, "geqrs_param: device allocation failed");
+  return P;
+}
+
+// ---- LQ: the QR engine on W = A^H with the tree built for A^H (trans = ConjTrans: its rows are A's tile columns)
+NatProgram* nat_gelqf_param(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* dA,
+                            dplasma_desc_t* dTS, dplasma_desc_t* dTT) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *TS = dTS ? dTS->nat : nullptr, *TT = dTT ? dTT->nat : nullptr;
+  const nq::Tree* t = nat_qrtree(q);
+  if (!same_ctx(c, {A, TS, TT}, prec)) return fail(nullptr, "gelqf_param: descriptors of another context or precision");
+  if (!param_conform(A, TS, TT)) return fail(nullptr, "gelqf_param: square tiles <= 256 and TS / TT of (IB x NB) tiles");
+  if (!t || t->mt != A->nt || t->nt != A->mt) return fail(nullptr, "gelqf_param: a native tree built with trans = ConjTrans");
+  NatProgram* P = new_program(c, "gelqf_param", true);
+  auto W = ctrans_desc(*P, *A);
+  if (!W) return fail(P, "gelqf_param: device allocation failed");
+  int last = add_ctrans(*P, *A, *W, -1);
+  if (last < -1 || !P->info || !add_geqrf_param(*P, *t, *W, *TS, *TT, true, last))
+    return fail(P, "gelqf_param: device allocation failed");
+  if (add_ctrans(*P, *W, *A, last) < -1) return fail(P, "gelqf_param: device allocation failed");
+  return P;
+}
+
+namespace {
+bool add_unmlq_param(NatProgram& P, const nq::Tree& t, int side, int trans, NatDesc& A, NatDesc& TS, NatDesc& TT,
+                     NatDesc& C, int& last) {
+  auto W = ctrans_desc(P, A);
+  if (!W) return false;
+  last = add_ctrans(P, A, *W, last);
+  if (last < -1) return false;
+  return add_unmqr_param(P, t, side, trans == NOTRANS ? CONJTRANS : NOTRANS, *W, TS, TT, C, last);
+}
+}  // namespace
+
+NatProgram* nat_unmlq_param(dplasma_context_t* ctx, int prec, int side, int trans, dplasma_qrtree_t* q,
+                            dplasma_desc_t* dA, dplasma_desc_t* dTS, dplasma_desc_t* dTT, dplasma_desc_t* dC) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *TS = dTS ? dTS->nat : nullptr, *TT = dTT ? dTT->nat : nullptr,
+          *C = dC ? dC->nat : nullptr;
+  const nq::Tree* t = nat_qrtree(q);
+  if (!same_ctx(c, {A, TS, TT, C}, prec)) return fail(nullptr, "unmlq_param: descriptors of another context or precision");
+  if (!param_conform(A, TS, TT) || !t || t->mt != A->nt || t->nt != A->mt)
+    return fail(nullptr, "unmlq_param: operands of gelqf_param");
+  if ((side == LEFT && (C->m != A->n || C->mb != A->nb)) || (side == RIGHT && (C->n != A->n || C->nb != A->nb)))
+    return fail(nullptr, "unmlq_param: C does not conform to Q");
+  NatProgram* P = new_program(c, "unmlq_param", false);
+  int last = -1;
+  if (!add_unmlq_param(*P, *t, side, trans, *A, *TS, *TT, *C, last))
+    return fail(P, "unmlq_param: TS / TT must come from the native gelqf_param of A with this tree");
+  return P;
+}
+
+NatProgram* nat_unglq_param(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* dA,
+                            dplasma_desc_t* dTS, dplasma_desc_t* dTT, dplasma_desc_t* dQ) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *TS = dTS ? dTS->nat : nullptr, *TT = dTT ? dTT->nat : nullptr,
+          *Q = dQ ? dQ->nat : nullptr;
+  const nq::Tree* t = nat_qrtree(q);
+  if (!same_ctx(c, {A, TS, TT, Q}, prec)) return fail(nullptr, "unglq_param: descriptors of another context or precision");
+  if (!param_conform(A, TS, TT) || !t || t->mt != A->nt || t->nt != A->mt || Q->n != A->n || Q->nb != A->nb ||
+      Q->mb != A->mb || Q->m > A->n)
+    return fail(nullptr, "unglq_param: operands of gelqf_param, Q with A's columns");
+  NatProgram* P = new_program(c, "unglq_param", false);
+  auto W = ctrans_desc(*P, *A), Qt = ctrans_desc(*P, *Q);
+  if (!W || !Qt) return fail(P, "unglq_param: device allocation failed");
+  std::vector<TileItem> it;
+  for (int i = 0; i < Qt->mt; ++i)
+    for (int j = 0; j < Qt->nt; ++j) it.push_back(TileItem{Qt->off(i, j), 0, Qt->rows(i), Qt->cols(j), i * Qt->mb, j * Qt->nb});
+  auto d_it = dev_upload(it);
+  if (!d_it) return fail(P, "unglq_param: device allocation failed");
+  P->keep.push_back(d_it);
+  const int n = (int)it.size(), mb = Qt->mb, nb = Qt->nb, ldq = Qt->lld;
+  char* qd = Qt->data;
+  const Scalar zero(prec, 0.0), one(prec, 1.0);
+  int last = P->task(1, [=](hipStream_t s) { return dpl_laset(prec, 0, n, d_it->p, mb, nb, zero.ptr(), one.ptr(), qd, ldq, s); },
+                     {});
+  last = add_ctrans(*P, *A, *W, last);
+  if (last < -1 || !add_unmqr_param(*P, *t, LEFT, NOTRANS, *W, *TS, *TT, *Qt, last))
+    return fail(P, "unglq_param: TS / TT must come from the native gelqf_param of A with this tree");
+  if (add_ctrans(*P, *Qt, *Q, last) < -1) return fail(P, "unglq_param: device allocation failed");
+  return P;
+}
+
+NatProgram* nat_gelqs_param(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* dA,
+                            dplasma_desc_t* dTS, dplasma_desc_t* dTT, dplasma_desc_t* dB) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *TS = dTS ? dTS->nat : nullptr, *TT = dTT ? dTT->nat : nullptr,
+          *B = dB ? dB->nat : nullptr;
+  const nq::Tree* t = nat_qrtree(q);
+  if (!same_ctx(c, {A, TS, TT, B}, prec)) return fail(nullptr, "gelqs_param: descriptors of another context or precision");
+  if (!param_conform(A, TS, TT) || !t || t->mt != A->nt || t->nt != A->mt || A->m > A->n || B->m < A->n ||
+      B->mb != A->nb)
+    return fail(nullptr, "gelqs_param: operands of gelqf_param of an M <= N matrix, B with N rows");
+  NatProgram* P = new_program(c, "gelqs_param", false);
+  auto L = lead_view(*A, A->m, A->m), Y = lead_view(*B, A->m, B->n);
+  P->wdesc.push_back(L);
+  P->wdesc.push_back(Y);
+  int last = -1;
+  if (!add_trsm(*P, LEFT, LOWER, NOTRANS, NONUNIT, Scalar(prec, 1.0), *L, *Y, 1, last))
+    return fail(P, "gelqs_param: device allocation failed");
+  last = last_on(*P, 1);
+  if (A->n > A->m) {   // B(M:N) := 0
+    std::vector<TileItem> it;
+    for (int i = 0; i < B->mt; ++i) {
+      const int top = i * B->mb, rows = B->rows(i);
+      if (top + rows <= A->m) continue;
+      const int skip = std::max(0, A->m - top);
+      for (int j = 0; j < B->nt; ++j)
+        it.push_back(TileItem{B->off(i, j) + skip, 0, rows - skip, B->cols(j), 0, 0});
+    }
+    if (!it.empty()) {
+      auto d = dev_upload(it);
+      if (!d) return fail(P, "gelqs_param: device allocation failed");
+      P->keep.push_back(d);
+      const int n = (int)it.size(), mb = B->mb, nb = B->nb, ldb = B->lld;
+      char* bd = B->data;
+      const Scalar zero(prec, 0.0);
+      last = P->task(1, [=](hipStream_t s) { return dpl_laset(prec, 0, n, d->p, mb, nb, zero.ptr(), zero.ptr(), bd, ldb, s); },
+                     {last});
+    }
+  }
+  if (!add_unmlq_param(*P, *t, LEFT, CONJTRANS, *A, *TS, *TT, *B, last))
+    return fail(P, "gelqs_param: TS / TT must come from the native gelqf_param of A with this tree");
   return P;
 }
 

@@ -182,6 +182,10 @@ struct NatDesc {
   // reference-layout IB x IB diagonal blocks being in the tiles themselves (unmqr / ungqr / gels read it)
   DevPtr fullT;
   int fullT_nb = 0, fullT_kt = 0;
+  // written by the native tree-driven geqrf_param (TS: one slot per TS domain head, TT: one per TT-killed
+  // row): slot of (row, k) at tidx[k * tidx_mt + row] (-1: none), each an nb x nb T in fullT
+  std::vector<long long> tidx;
+  int tidx_mt = 0;
   NatDesc() = default;
   NatDesc(const NatDesc&) = delete;             // owns its buffer: never copied (nor captured by value)
   NatDesc& operator=(const NatDesc&) = delete;

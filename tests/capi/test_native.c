@@ -886,6 +886,180 @@ static void test_dgeqrf(dplasma_context_t *ctx) {
 }
 
 
+/* tree-driven QR / LQ (native_qrtree.cpp trees + native.cpp *_param builders) on ragged matrices.  Trees: HQR with
+ * a greedy low tree over TS domains of a = 2 tiles and a flat high tree over p = 3 virtual process rows (TS, local
+ * TT and distributed TT kills), HQR binary/greedy with domino, systolic, adaptive SVD.  Checks: ||Q^T Q - I||,
+ * ||QR - A|| (ungqr_param), |R| equal to the flat geqrf's |R| (R is unique up to row signs), Q^T A0 = [R; 0] and
+ * D Q against the host product (unmqr_param), the least-squares normal equations (geqrs_param). */
+static void test_dgeqrf_param(dplasma_context_t *ctx) {
+  const int m = 900, n = 500, nb = 128, ib = 32, nrhs = 2, p = 40;
+  const int mt = (m + nb - 1) / nb, nt = (n + nb - 1) / nb;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, m, n), *F = dmat(ctx, dplasmaRealDouble, nb, m, n);
+  dplasma_desc_t *TS = dplasma_desc_block_cyclic(ctx, dplasmaRealDouble, ib, nb, mt * ib, nt * nb, 1, 1, dplasmaUpperLower);
+  dplasma_desc_t *TT = dplasma_desc_block_cyclic(ctx, dplasmaRealDouble, ib, nb, mt * ib, nt * nb, 1, 1, dplasmaUpperLower);
+  dplasma_desc_t *T0 = dplasma_desc_block_cyclic(ctx, dplasmaRealDouble, ib, nb, mt * ib, nt * nb, 1, 1, dplasmaUpperLower);
+  dplasma_desc_t *Q = dmat(ctx, dplasmaRealDouble, nb, m, n), *Qf = dmat(ctx, dplasmaRealDouble, nb, m, m);
+  dplasma_desc_t *C = dmat(ctx, dplasmaRealDouble, nb, m, n), *D = dmat(ctx, dplasmaRealDouble, nb, p, m);
+  dplasma_desc_t *B = dmat(ctx, dplasmaRealDouble, nb, m, nrhs);
+  CHECK(A && F && TS && TT && T0 && Q && Qf && C && D && B, "param descriptors: %s", dplasma_last_error());
+  double *a = malloc(sizeof(double) * m * n), *f = malloc(sizeof(double) * m * n), *f0 = malloc(sizeof(double) * m * n);
+  double *q = malloc(sizeof(double) * m * n), *qf = malloc(sizeof(double) * m * m), *c = malloc(sizeof(double) * m * n);
+  double *d = malloc(sizeof(double) * p * m), *dq = malloc(sizeof(double) * p * m);
+  double *b = malloc(sizeof(double) * m * nrhs), *x = malloc(sizeof(double) * m * nrhs);
+  unsigned sd = 313;
+  rnd_fill(a, (size_t)m * n, &sd), rnd_fill(d, (size_t)p * m, &sd), rnd_fill(b, (size_t)m * nrhs, &sd);
+  dplasma_desc_set_lapack(F, a, m);
+  CHECK(dplasma_dgeqrf(ctx, F, T0) == 0, "flat dgeqrf: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(F, f0, m);
+  double an = 0;
+  for (size_t e = 0; e < (size_t)m * n; ++e) an = fmax(an, fabs(a[e]));
+  for (int kind = 0; kind < 4; ++kind) {
+    dplasma_qrtree_t qt;
+    memset(&qt, 0, sizeof qt);
+    int rc;
+    const char *nm;
+    if (kind == 0) rc = dplasma_hqr_init(&qt, dplasmaNoTrans, A, DPLASMA_GREEDY_TREE, DPLASMA_FLAT_TREE, 2, 3, 0, 0), nm = "hqr greedy/flat a=2 p=3";
+    else if (kind == 1) rc = dplasma_hqr_init(&qt, dplasmaNoTrans, A, 3, DPLASMA_GREEDY_TREE, 1, 2, 1, 0), nm = "hqr binary/greedy p=2 domino";
+    else if (kind == 2) rc = dplasma_systolic_init(&qt, dplasmaNoTrans, A, 2, 2), nm = "systolic 2x2";
+    else rc = dplasma_svd_init(&qt, dplasmaNoTrans, A, 2, 2, 2, 1), nm = "svd fibonacci p=2";
+    CHECK(rc == 0, "%s init: %s", nm, dplasma_last_error());
+    if (rc) continue;
+    CHECK(qt.mt == mt && qt.nt == nt, "%s dims %d x %d", nm, qt.mt, qt.nt);
+    CHECK(dplasma_qrtree_check(A, &qt) == 0, "%s check: %s", nm, dplasma_last_error());
+    dplasma_desc_set_lapack(A, a, m);
+    int info = dplasma_dgeqrf_param(ctx, &qt, A, TS, TT);
+    CHECK(info == 0, "%s dgeqrf_param info %d (%s)", nm, info, dplasma_last_error());
+    dplasma_desc_get_lapack(A, f, m);
+    CHECK(dplasma_dungqr_param(ctx, &qt, A, TS, TT, Q) == 0, "%s dungqr_param: %s", nm, dplasma_last_error());
+    CHECK(dplasma_dungqr_param(ctx, &qt, A, TS, TT, Qf) == 0, "%s dungqr_param full: %s", nm, dplasma_last_error());
+    dplasma_desc_get_lapack(Q, q, m);
+    dplasma_desc_get_lapack(Qf, qf, m);
+    double orth = 0, res = 0, rd = 0;
+    for (int j = 0; j < n; ++j)
+      for (int i = 0; i < n; ++i) {
+        double s = 0;
+        for (int k = 0; k < m; ++k) s += q[k + (size_t)i * m] * q[k + (size_t)j * m];
+        orth = fmax(orth, fabs(s - (i == j)));
+      }
+    for (int j = 0; j < n; ++j)
+      for (int i = 0; i < m; ++i) {
+        double s = 0;
+        for (int k = 0; k <= j && k < n; ++k) s += q[i + (size_t)k * m] * f[k + (size_t)j * m];
+        res = fmax(res, fabs(s - a[i + (size_t)j * m]));
+        if (i <= j) rd = fmax(rd, fabs(fabs(f[i + (size_t)j * m]) - fabs(f0[i + (size_t)j * m])));
+      }
+    /* Q^T A0 = [R; 0] and D Q against the host product with the full Q */
+    dplasma_desc_set_lapack(C, a, m);
+    CHECK(dplasma_dunmqr_param(ctx, dplasmaLeft, dplasmaTrans, &qt, A, TS, TT, C) == 0, "%s dunmqr_param L T: %s", nm,
+          dplasma_last_error());
+    dplasma_desc_get_lapack(C, c, m);
+    double e1 = 0, e2 = 0;
+    for (int j = 0; j < n; ++j)
+      for (int i = 0; i < m; ++i) e1 = fmax(e1, fabs(c[i + (size_t)j * m] - (i <= j ? f[i + (size_t)j * m] : 0.0)));
+    dplasma_desc_set_lapack(D, d, p);
+    CHECK(dplasma_dunmqr_param(ctx, dplasmaRight, dplasmaNoTrans, &qt, A, TS, TT, D) == 0, "%s dunmqr_param R N: %s", nm,
+          dplasma_last_error());
+    dplasma_desc_get_lapack(D, dq, p);
+    for (int j = 0; j < m; ++j)
+      for (int i = 0; i < p; ++i) {
+        double s = 0;
+        for (int k = 0; k < m; ++k) s += d[i + (size_t)k * p] * qf[k + (size_t)j * m];
+        e2 = fmax(e2, fabs(s - dq[i + (size_t)j * p]));
+      }
+    /* least squares on the factored A: A^T (A x - b) = 0 */
+    dplasma_desc_set_lapack(B, b, m);
+    CHECK(dplasma_dgeqrs_param(ctx, &qt, A, TS, TT, B) == 0, "%s dgeqrs_param: %s", nm, dplasma_last_error());
+    dplasma_desc_get_lapack(B, x, m);
+    double ne = 0, bn = 0;
+    for (int r = 0; r < nrhs; ++r) {
+      for (int j = 0; j < n; ++j) {
+        double s = 0;
+        for (int i = 0; i < m; ++i) {
+          double ax = 0;
+          for (int k = 0; k < n; ++k) ax += a[i + (size_t)k * m] * x[k + (size_t)r * m];
+          s += a[i + (size_t)j * m] * (ax - b[i + (size_t)r * m]);
+        }
+        ne = fmax(ne, fabs(s));
+      }
+      for (int i = 0; i < m; ++i) bn = fmax(bn, fabs(b[i + (size_t)r * m]));
+    }
+    printf("dgeqrf_param %-30s ||Q^T Q - I|| %.2e ||QR - A||/||A|| %.2e | |R| - |R_flat| | %.2e  Q^T A %.2e  D Q %.2e  "
+           "geqrs %.2e\n", nm, orth, res / an, rd / an, e1 / an, e2, ne / (m * an * bn));
+    CHECK(orth < 1e-12 && res / an < 1e-12 && rd / an < 1e-11 && e1 / an < 1e-12 && e2 < 1e-11 &&
+          ne / (m * an * bn) < 1e-12, "%s residuals", nm);
+    dplasma_hqr_finalize(&qt);   /* (every init's finalize releases the native tree) */
+  }
+  free(a), free(f), free(f0), free(q), free(qf), free(c), free(d), free(dq), free(b), free(x);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(F), dplasma_desc_destroy(TS), dplasma_desc_destroy(TT);
+  dplasma_desc_destroy(T0), dplasma_desc_destroy(Q), dplasma_desc_destroy(Qf), dplasma_desc_destroy(C);
+  dplasma_desc_destroy(D), dplasma_desc_destroy(B);
+}
+
+/* tree-driven LQ on a wide ragged matrix (tree built with trans = Trans: over A's tile columns): gelqf_param,
+ * unglq_param (Q Q^T = I, LQ = A), unmlq_param (A0 Q^T = [L 0]), gelqs_param (minimum-norm A x = b) */
+static void test_dgelqf_param(dplasma_context_t *ctx) {
+  const int m = 300, n = 800, nb = 128, ib = 32, nrhs = 2;
+  const int mt = (m + nb - 1) / nb, nt = (n + nb - 1) / nb;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, m, n), *Q = dmat(ctx, dplasmaRealDouble, nb, m, n);
+  dplasma_desc_t *C = dmat(ctx, dplasmaRealDouble, nb, m, n), *B = dmat(ctx, dplasmaRealDouble, nb, n, nrhs);
+  dplasma_desc_t *TS = dplasma_desc_block_cyclic(ctx, dplasmaRealDouble, ib, nb, mt * ib, nt * nb, 1, 1, dplasmaUpperLower);
+  dplasma_desc_t *TT = dplasma_desc_block_cyclic(ctx, dplasmaRealDouble, ib, nb, mt * ib, nt * nb, 1, 1, dplasmaUpperLower);
+  CHECK(A && Q && C && B && TS && TT, "lq param descriptors: %s", dplasma_last_error());
+  double *a = malloc(sizeof(double) * m * n), *f = malloc(sizeof(double) * m * n), *q = malloc(sizeof(double) * m * n);
+  double *c = malloc(sizeof(double) * m * n), *b = malloc(sizeof(double) * n * nrhs), *y = malloc(sizeof(double) * n * nrhs);
+  unsigned sd = 515;
+  rnd_fill(a, (size_t)m * n, &sd), rnd_fill(b, (size_t)n * nrhs, &sd);
+  dplasma_qrtree_t qt;
+  memset(&qt, 0, sizeof qt);
+  CHECK(dplasma_hqr_init(&qt, dplasmaTrans, A, DPLASMA_GREEDY_TREE, DPLASMA_FLAT_TREE, 2, 2, 0, 1) == 0, "lq tree: %s",
+        dplasma_last_error());
+  CHECK(qt.mt == nt && qt.nt == mt, "lq tree dims %d x %d", qt.mt, qt.nt);
+  dplasma_desc_set_lapack(A, a, m);
+  int info = dplasma_dgelqf_param(ctx, &qt, A, TS, TT);
+  CHECK(info == 0, "dgelqf_param info %d (%s)", info, dplasma_last_error());
+  dplasma_desc_get_lapack(A, f, m);
+  CHECK(dplasma_dunglq_param(ctx, &qt, A, TS, TT, Q) == 0, "dunglq_param: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(Q, q, m);
+  double orth = 0, res = 0, an = 0;
+  for (int j = 0; j < m; ++j)
+    for (int i = 0; i < m; ++i) {
+      double s = 0;
+      for (int k = 0; k < n; ++k) s += q[i + (size_t)k * m] * q[j + (size_t)k * m];
+      orth = fmax(orth, fabs(s - (i == j)));
+    }
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < m; ++i) {
+      double s = 0;
+      for (int k = 0; k <= i; ++k) s += f[i + (size_t)k * m] * q[k + (size_t)j * m];
+      res = fmax(res, fabs(s - a[i + (size_t)j * m]));
+      an = fmax(an, fabs(a[i + (size_t)j * m]));
+    }
+  dplasma_desc_set_lapack(C, a, m);
+  CHECK(dplasma_dunmlq_param(ctx, dplasmaRight, dplasmaTrans, &qt, A, TS, TT, C) == 0, "dunmlq_param R T: %s",
+        dplasma_last_error());
+  dplasma_desc_get_lapack(C, c, m);
+  double e1 = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < m; ++i) e1 = fmax(e1, fabs(c[i + (size_t)j * m] - (j <= i ? f[i + (size_t)j * m] : 0.0)));
+  dplasma_desc_set_lapack(B, b, n);
+  CHECK(dplasma_dgelqs_param(ctx, &qt, A, TS, TT, B) == 0, "dgelqs_param: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(B, y, n);
+  double ge = 0;
+  for (int r = 0; r < nrhs; ++r)
+    for (int i = 0; i < m; ++i) {
+      double s = 0;
+      for (int k = 0; k < n; ++k) s += a[i + (size_t)k * m] * y[k + (size_t)r * n];
+      ge = fmax(ge, fabs(s - b[i + (size_t)r * n]));
+    }
+  printf("dgelqf_param hqr greedy/flat tsrr: ||Q Q^T - I|| %.2e ||LQ - A||/||A|| %.2e  A Q^T %.2e  gelqs ||Ax-b|| %.2e\n",
+         orth, res / an, e1 / an, ge);
+  CHECK(orth < 1e-12 && res / an < 1e-12 && e1 / an < 1e-12 && ge < 1e-10, "gelqf_param residuals");
+  dplasma_hqr_finalize(&qt);
+  free(a), free(f), free(q), free(c), free(b), free(y);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(Q), dplasma_desc_destroy(C), dplasma_desc_destroy(B);
+  dplasma_desc_destroy(TS), dplasma_desc_destroy(TT);
+}
+
 /* trtri / lauum / potri / poinv natively: A := inv(A) checked as ||A0 inv(A) - I||; lauum against host
    L^T L; her2k / syr2k against host rank-2k; the alias entry points (ptgpanel on 1x1, potrf_rec). */
 static void test_inverse_family(dplasma_context_t *ctx) {
@@ -1429,6 +1603,8 @@ int main(int argc, char **argv) {
   test_dgesv_incpiv(ctx);
   test_dgelqf(ctx);
   test_zgelqf(ctx);
+  test_dgeqrf_param(ctx);
+  test_dgelqf_param(ctx);
   test_inverse_family(ctx);
   test_rank_2k(ctx);
   test_aliases(ctx);

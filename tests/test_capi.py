@@ -343,5 +343,5 @@ def test_capi_ext_native_routing():
         for op in native:
             ln = lines[f"dplasma_{p}{op}"]
             assert "if (dpl_native(ctx)) return nat_" in ln and "nat_unsupported" not in ln, (p, op)
-        for op in ("heev", "getrf_qrf", "geqrf_param"):
+        for op in ("heev", "getrf_qrf", "hbrdt"):
             assert f'nat_unsupported("{p}{op}")' in lines[f"dplasma_{p}{op}"], (p, op)

@@ -185,6 +185,15 @@ NATIVE_EXT = {
     "hetrf": lambda pc: f"nat_hetrf(ctx, {pc}, A)",
     "trdsm": lambda pc: f"nat_trdsm(ctx, {pc}, A, B)",
     "trmdm": lambda pc: f"nat_trmdm(ctx, {pc}, A)",
+    # tree-driven QR / LQ (native_qrtree.cpp trees, native.cpp *_param builders)
+    "geqrf_param": lambda pc: f"nat_geqrf_param(ctx, {pc}, qrtree, A, TS, TT)",
+    "gelqf_param": lambda pc: f"nat_gelqf_param(ctx, {pc}, qrtree, A, TS, TT)",
+    "unmqr_param": lambda pc: f"nat_unmqr_param(ctx, {pc}, side, trans, qrtree, A, TS, TT, C)",
+    "unmlq_param": lambda pc: f"nat_unmlq_param(ctx, {pc}, side, trans, qrtree, A, TS, TT, C)",
+    "ungqr_param": lambda pc: f"nat_ungqr_param(ctx, {pc}, qrtree, A, TS, TT, Q)",
+    "unglq_param": lambda pc: f"nat_unglq_param(ctx, {pc}, qrtree, A, TS, TT, Q)",
+    "geqrs_param": lambda pc: f"nat_geqrs_param(ctx, {pc}, qrtree, A, TS, TT, B)",
+    "gelqs_param": lambda pc: f"nat_gelqs_param(ctx, {pc}, qrtree, A, TS, TT, B)",
 }
 # EXT entry points the engine answers directly (a value, no program)
 NATIVE_EXT_DIRECT = {
