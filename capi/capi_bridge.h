@@ -192,6 +192,10 @@ NatProgram* nat_geqrs_param(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* 
                             dplasma_desc_t* TT, dplasma_desc_t* B);
 NatProgram* nat_gelqs_param(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* A, dplasma_desc_t* TS,
                             dplasma_desc_t* TT, dplasma_desc_t* B);
+NatProgram* nat_getrf_qrf(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* A, dplasma_desc_t* IPIV,
+                          dplasma_desc_t* TS, dplasma_desc_t* TT, int criteria, double alpha, int* lu_tab, int* INFO);
+NatProgram* nat_trsmpl_qrf(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* A, dplasma_desc_t* IPIV,
+                           dplasma_desc_t* B, dplasma_desc_t* TS, dplasma_desc_t* TT, int* lu_tab);
 NatProgram* nat_trdsm(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* B);
 NatProgram* nat_trmdm(dplasma_context_t* ctx, int prec, dplasma_desc_t* A);
 int nat_latms(dplasma_context_t* ctx, int prec, int mtxtype, double cond, dplasma_desc_t* A, unsigned long long seed);

@@ -3101,60 +3101,64 @@ bool tree_T_ok(const NatDesc& T, const NatDesc& A, const std::vector<std::vector
   return true;
 }
 
-// lq: the reference-layout diagonal blocks go to tile (k, trow) of the T descriptor (the LQ T layout)
-bool add_geqrf_param(NatProgram& P, const nq::Tree& tree, NatDesc& A, NatDesc& TS, NatDesc& TT, bool lq, int& last) {
+// one entry of a tree step: stack, factor (T into its slot), write back, reference-layout T blocks (LQ: tile
+// (k, trow)), trailing update of columns k+1..; tasks on `stream` after prev; returns the last task (< -1: failure)
+int add_qp_factor_entry(NatProgram& P, NatDesc& A, NatDesc& TS, NatDesc& TT, const QpEntry& e, const QpBufs& b, bool lq,
+                        int stream, int prev) {
   const int prec = A.prec, nb = A.nb, es = A.es;
-  const auto ents = qp_entries(tree, A);
-  QpBufs b;
-  if (!qp_bufs(P, A, ents, (size_t)nb * std::max(1, A.n), b) || !qp_slots(P, TS, A, ents, false) ||
-      !qp_slots(P, TT, A, ents, true))
-    return false;
   int* info = (int*)P.info->p;
   char *pb = (char*)b.P->p, *vb = (char*)b.V->p, *ws = (char*)b.ws->p;
   const int ld = b.ld;
-  int prev = last;
-  for (const auto& st : ents) {
-    for (const QpEntry& e : st) {
-      const int k = e.k, kb = A.cols(k), M = e.M, kf = e.kf;
-      NatDesc& Td = e.tt ? TT : TS;
-      char* Tk = qp_slot(Td, e);
-      if (e.tt) {   // the stack of two triangles: zeros below them
-        prev = P.task(0, [=](hipStream_t s) { return (int)hipMemsetAsync(pb, 0, (size_t)ld * kb * es, s); }, {prev});
-      }
-      prev = add_stack_copy(P, A, e, pb, ld, true, e.tt ? 2 : 0, 0, prev);
-      if (prev < -1) return false;
-      prev = P.task(0, [=](hipStream_t s) { return dpl_qr_panel(prec, pb, ld, 0, 0, M, kb, kf, vb, ld, Tk, nb, ws, info, s); },
-                    {prev});
-      prev = add_stack_copy(P, A, e, pb, ld, false, e.tt ? 2 : 0, 0, prev);
-      if (prev < -1) return false;
-      // reference layout: the IB x IB diagonal blocks of T into tile (trow, k) (LQ: (k, trow)) when it exists
-      const int ti = lq ? k : e.trow, tj = lq ? e.trow : k;
-      if (ti < Td.mt && tj < Td.nt) {
-        const int ib = Td.mb;
-        std::vector<TileItem> it;
-        for (int b0 = 0; b0 < kf; b0 += ib) {
-          const int bs = std::min(ib, kf - b0);
-          it.push_back(TileItem{b0 + (long long)b0 * nb, Td.off(ti, tj) + (long long)b0 * Td.lld, bs, bs, 0, 0});
-        }
-        auto d = dev_upload(it);
-        if (!d) return false;
-        P.keep.push_back(d);
-        const int n = (int)it.size(), ldT = Td.lld;
-        char* td = Td.data;
-        const Scalar one(prec, 1.0), zero(prec, 0.0);
-        prev = P.task(0, [=](hipStream_t s) {
-          return dpl_geadd(prec, 0, NOTRANS, n, d->p, ib, ib, one.ptr(), Tk, nb, zero.ptr(), td, ldT, 1, s);
-        }, {prev});
-      }
-      std::vector<int> cols;
-      for (int j = k + 1; j < A.nt; ++j) cols.push_back(j);
-      int out = prev;
-      if (!add_left_apply_rows(P, prec, A, e.rows, e.voff, kf, vb, ld, Tk, nb, true, (char*)b.W->p, (char*)b.W2->p, cols, 0,
-                               prev, out))
-        return false;
-      prev = out;
+  const int k = e.k, kb = A.cols(k), M = e.M, kf = e.kf;
+  NatDesc& Td = e.tt ? TT : TS;
+  char* Tk = qp_slot(Td, e);
+  if (e.tt)   // the stack of two triangles: zeros below them
+    prev = P.task(stream, [=](hipStream_t s) { return (int)hipMemsetAsync(pb, 0, (size_t)ld * kb * es, s); }, {prev});
+  prev = add_stack_copy(P, A, e, pb, ld, true, e.tt ? 2 : 0, stream, prev);
+  if (prev < -1) return prev;
+  prev = P.task(stream, [=](hipStream_t s) { return dpl_qr_panel(prec, pb, ld, 0, 0, M, kb, kf, vb, ld, Tk, nb, ws, info, s); },
+                {prev});
+  prev = add_stack_copy(P, A, e, pb, ld, false, e.tt ? 2 : 0, stream, prev);
+  if (prev < -1) return prev;
+  const int ti = lq ? k : e.trow, tj = lq ? e.trow : k;
+  if (ti < Td.mt && tj < Td.nt) {
+    const int ib = Td.mb;
+    std::vector<TileItem> it;
+    for (int b0 = 0; b0 < kf; b0 += ib) {
+      const int bs = std::min(ib, kf - b0);
+      it.push_back(TileItem{b0 + (long long)b0 * nb, Td.off(ti, tj) + (long long)b0 * Td.lld, bs, bs, 0, 0});
     }
+    auto d = dev_upload(it);
+    if (!d) return -2;
+    P.keep.push_back(d);
+    const int n = (int)it.size(), ldT = Td.lld;
+    char* td = Td.data;
+    const Scalar one(prec, 1.0), zero(prec, 0.0);
+    prev = P.task(stream, [=](hipStream_t s) {
+      return dpl_geadd(prec, 0, NOTRANS, n, d->p, ib, ib, one.ptr(), Tk, nb, zero.ptr(), td, ldT, 1, s);
+    }, {prev});
   }
+  std::vector<int> cols;
+  for (int j = k + 1; j < A.nt; ++j) cols.push_back(j);
+  int out = prev;
+  if (!add_left_apply_rows(P, prec, A, e.rows, e.voff, kf, vb, ld, Tk, nb, true, (char*)b.W->p, (char*)b.W2->p, cols,
+                           stream, prev, out))
+    return -2;
+  return out;
+}
+
+bool add_geqrf_param(NatProgram& P, const nq::Tree& tree, NatDesc& A, NatDesc& TS, NatDesc& TT, bool lq, int& last) {
+  const auto ents = qp_entries(tree, A);
+  QpBufs b;
+  if (!qp_bufs(P, A, ents, (size_t)A.nb * std::max(1, A.n), b) || !qp_slots(P, TS, A, ents, false) ||
+      !qp_slots(P, TT, A, ents, true))
+    return false;
+  int prev = last;
+  for (const auto& st : ents)
+    for (const QpEntry& e : st) {
+      prev = add_qp_factor_entry(P, A, TS, TT, e, b, lq, 0, prev);
+      if (prev < -1) return false;
+    }
   last = prev;
   return true;
 }
@@ -3403,6 +3407,428 @@ NatProgram* nat_gelqs_param(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* 
   }
   if (!add_unmlq_param(*P, *t, LEFT, CONJTRANS, *A, *TS, *TT, *B, last))
     return fail(P, "gelqs_param: TS / TT must come from the native gelqf_param of A with this tree");
+  return P;
+}
+
+// ----------------------------------------------------------------------------- hybrid LU-QR (getrf_qrf, trsmpl_qrf)
+// dplasma_zgetrf_qrf / ztrsmpl_qrf (reference src/zgetrf_qrf.jdf, ztrsmpl_qrf.jdf; models/lu_qr.py) on one
+// process.  Step k: the diagonal domain -- panel tiles k, k+p, k+2p, ... (p = the grid rows) -- is stacked into a
+// contiguous buffer and factored by the device partial-pivoting recursion (A untouched); a host DECIDE task
+// (one stream synchronisation) evaluates the criterion from that LU and the off-domain tiles and records it in
+// lu_tab[k]; both branches are in the program as predicated tasks (NatTask::guard): LU -- the stacked factors
+// written back, IPIV(k, k) := the 1-based stack pivots, the domain rows of the trailing columns interchanged,
+// TRSM of row k with L_kk and of the off-domain tiles with U_kk, one MFMA GEMM batch; QR -- the tree's step k
+// (stacked TS-domain / TT panels, as geqrf_param).  Criteria as models/lu_qr.py (HIGHAM: alpha cond_1(U_kk) >
+// sum ||A_ik||_1, SUM / MAX / MOY: alpha / ||(L U)_kk^-1||_1 against the sum / max / mean, MUMPS column maxima,
+// LU_ONLY, QR_ONLY, RANDOM (balanced table), DEFAULT alternating); alpha = 0 forces QR, >= 9999999999 LU, a
+// singular domain QR.  Norms are exact (the reference estimates them with trcon / gecon: a decision exactly at
+// the estimate's margin is parity unpinned).
+namespace {
+
+enum { LQ_DEFAULT = 0, LQ_HIGHAM = 1, LQ_MUMPS = 2, LQ_LU_ONLY = 3, LQ_QR_ONLY = 4, LQ_RANDOM = 5, LQ_HSUM = 6,
+       LQ_HMAX = 7, LQ_HMOY = 8 };
+
+// balanced recursive split of nb_lu LU steps over [deb, fin] (dplasma_genrandom_lutab, models/lu_qr.py)
+void genrandom_lutab(std::vector<int>& t, int deb, int fin, int nb_lu, int depth) {
+  if (deb == fin) {
+    t[deb] = nb_lu != 0;
+    return;
+  }
+  const int n = fin - deb + 1;
+  const int new_fin = n % 2 == 0 ? deb - 1 + n / 2 : deb - 1 + (fin - deb) / 2 + (depth % 2);
+  const int new_nb = nb_lu % 2 == 0 ? nb_lu / 2 : (nb_lu - 1) / 2 + (depth % 2);
+  genrandom_lutab(t, deb, new_fin, new_nb, depth + 1);
+  genrandom_lutab(t, new_fin + 1, fin, nb_lu - new_nb, depth + 1);
+}
+
+using cplx = std::complex<double>;
+
+// host copy of an r x c block (element ld) of a device matrix of precision prec, widened to complex<double>
+bool host_block(int prec, const char* src, int ld, int r, int c, std::vector<cplx>& out) {
+  const int es = esize(prec);
+  std::vector<unsigned char> raw((size_t)r * c * es);
+  if (r > 0 && c > 0 &&
+      hipMemcpy2D(raw.data(), (size_t)r * es, src, (size_t)ld * es, (size_t)r * es, c, hipMemcpyDeviceToHost) != hipSuccess)
+    return false;
+  out.resize((size_t)r * c);
+  for (size_t i = 0; i < out.size(); ++i) {
+    const unsigned char* p = raw.data() + i * es;
+    if (prec == P_S) out[i] = *(const float*)p;
+    else if (prec == P_D) out[i] = *(const double*)p;
+    else if (prec == P_C) out[i] = cplx(((const float*)p)[0], ((const float*)p)[1]);
+    else out[i] = cplx(((const double*)p)[0], ((const double*)p)[1]);
+  }
+  return true;
+}
+
+// inverse of an n x n triangular matrix (column-major, ld n); unit: implicit unit diagonal
+std::vector<cplx> tri_inverse(const std::vector<cplx>& T, int n, bool upper, bool unit) {
+  std::vector<cplx> X((size_t)n * n, 0.0);
+  for (int j = 0; j < n; ++j) {   // column j of X solves T x = e_j
+    std::vector<cplx> x(n, 0.0);
+    x[j] = 1.0;
+    if (upper) {
+      for (int i = n - 1; i >= 0; --i) {
+        cplx s = x[i];
+        for (int c = i + 1; c < n; ++c) s -= T[i + (size_t)c * n] * x[c];
+        x[i] = unit ? s : s / T[i + (size_t)i * n];
+      }
+    } else {
+      for (int i = 0; i < n; ++i) {
+        cplx s = x[i];
+        for (int c = 0; c < i; ++c) s -= T[i + (size_t)c * n] * x[c];
+        x[i] = unit ? s : s / T[i + (size_t)i * n];
+      }
+    }
+    for (int i = 0; i < n; ++i) X[i + (size_t)j * n] = x[i];
+  }
+  return X;
+}
+
+double norm1(const std::vector<cplx>& X, int r, int c, int ld) {
+  double m = 0;
+  for (int j = 0; j < c; ++j) {
+    double s = 0;
+    for (int i = 0; i < r; ++i) s += std::abs(X[i + (size_t)j * ld]);
+    m = std::max(m, s);
+  }
+  return m;
+}
+
+struct LuqrState {
+  std::vector<std::shared_ptr<int>> dec;   // per step: 1 LU, 0 QR (set by the DECIDE task)
+  std::vector<int> table;                  // RANDOM criterion's lu_tab
+};
+
+bool luqr_conform(const NatDesc* A, const NatDesc* IP, const NatDesc* TS, const NatDesc* TT) {
+  return A && IP && param_conform(A, TS, TT) && IP->prec == P_I && IP->mb == A->mb && IP->nb == 1 && IP->mt >= A->mt &&
+         IP->nt >= std::min(A->mt, A->nt);
+}
+
+}  // namespace
+
+NatProgram* nat_getrf_qrf(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* dA, dplasma_desc_t* dIP,
+                          dplasma_desc_t* dTS, dplasma_desc_t* dTT, int criteria, double alpha, int* lu_tab, int* INFO) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *IP = dIP ? dIP->nat : nullptr, *TS = dTS ? dTS->nat : nullptr,
+          *TT = dTT ? dTT->nat : nullptr;
+  const nq::Tree* t = nat_qrtree(q);
+  if (!same_ctx(c, {A, TS, TT}, prec) || !IP || IP->ctx != c)
+    return fail(nullptr, "getrf_qrf: descriptors of another context or precision");
+  if (!luqr_conform(A, IP, TS, TT))
+    return fail(nullptr, "getrf_qrf: square tiles <= 256, TS / TT of (IB x NB) tiles, IPIV of (MB x 1) int tiles");
+  if (!tree_fits(t, *A)) return fail(nullptr, "getrf_qrf: a native tree built for A's tile rows and columns");
+  if (criteria < LQ_DEFAULT || criteria > LQ_HMOY) return fail(nullptr, "getrf_qrf: unknown criterion");
+  NatProgram* P = new_program(c, "getrf_qrf", true);
+  // the domain period: the grid rows (DPLASMA_LUQR_P overrides it, as models/lu_qr.py's p argument)
+  const int kt = std::min(A->mt, A->nt), mb = A->mb, nb = A->nb, es = A->es, ld = A->lld,
+            pgrid = std::max(1, env_int("DPLASMA_LUQR_P", A->P));
+  const auto ents = qp_entries(*t, *A);
+  QpBufs qb;
+  LuScratch S;
+  if (!P->info || !qp_bufs(*P, *A, ents, (size_t)nb * std::max(1, A->n), qb) || !qp_slots(*P, *TS, *A, ents, false) ||
+      !qp_slots(*P, *TT, *A, ents, true) || !lu_scratch(*P, *A, S))
+    return fail(P, "getrf_qrf: device allocation failed");
+  // the trailing domain rows during the interchanges (stack order), the domain LU's info
+  DevPtr WT = dev_alloc((size_t)std::max(1, A->m) * std::max(1, A->n) * es, false);
+  DevPtr DI = dev_alloc(sizeof(int), true);
+  if (!WT || !DI) return fail(P, "getrf_qrf: device allocation failed");
+  P->keep.push_back(WT);
+  P->keep.push_back(DI);
+  auto state = std::make_shared<LuqrState>();
+  if (criteria == LQ_RANDOM) {
+    state->table.assign(kt, 0);
+    if (kt > 0) genrandom_lutab(state->table, 0, kt - 1, (int)std::lround(kt * alpha / 100.0), 0);
+  }
+  char* a = A->data;
+  char* buf = (char*)S.pv->p;
+  char* wt = (char*)WT->p;
+  int* dinfo = (int*)DI->p;
+  int* ipg = (int*)IP->data;
+  const Scalar one(prec, 1.0), m_one(prec, -1.0), zero(prec, 0.0);
+  int prev = P->task(1, [=](hipStream_t) {
+    if (INFO) *INFO = 0;
+    return 0;
+  }, {});
+  for (int k = 0; k < kt; ++k) {
+    std::vector<int> dom, off;
+    for (int m = k; m < A->mt; m += pgrid) dom.push_back(m);
+    for (int m = k + 1; m < A->mt; ++m)
+      if ((m - k) % pgrid) off.push_back(m);
+    int M = 0;
+    std::vector<int> soff;
+    for (int m : dom) {
+      soff.push_back(M);
+      M += A->rows(m);
+    }
+    const int ncol = A->cols(k), kmax = std::min(M, ncol);
+    // ---- domain LU on the stacked copy (A untouched)
+    auto gat = std::make_shared<MapBatch>(), back = std::make_shared<MapBatch>();
+    for (size_t i = 0; i < dom.size(); ++i) {
+      gat->it.push_back(TileItem{A->off(dom[i], k), soff[i], A->rows(dom[i]), ncol, 0, 0});
+      back->it.push_back(TileItem{soff[i], A->off(dom[i], k), A->rows(dom[i]), ncol, 0, 0});
+      gat->mm = back->mm = std::max(gat->mm, A->rows(dom[i]));
+    }
+    gat->nn = back->nn = ncol;
+    if (!gat->upload(*P) || !back->upload(*P)) return fail(P, "getrf_qrf: device allocation failed");
+    prev = P->task(1, [=](hipStream_t s) {
+      if (hipMemsetAsync(dinfo, 0, sizeof(int), s) != hipSuccess) return -1;
+      return dpl_geadd(prec, 0, NOTRANS, gat->n(), gat->items(), gat->mm, gat->nn, one.ptr(), a, ld, zero.ptr(), buf, M, 1, s);
+    }, {prev});
+    prev = add_panel_lu(*P, prec, buf, M, M, 0, kmax, S, dinfo, 0, prev, true);
+    if (prev < 0) return fail(P, "getrf_qrf: device allocation failed");
+    const int* piv = (const int*)S.piv->p;
+    if (ncol > kmax) {   // fewer domain rows than columns: the last columns take the swaps and L^-1
+      prev = P->task(1, [=](hipStream_t s) { return dpl_laswp_panel(prec, buf, M, M, kmax, ncol, piv, 0, kmax, dinfo, s); },
+                     {prev});
+      auto tr = std::make_shared<Trsm1>();
+      tr->tri = 0;
+      tr->add((long long)kmax * M, kmax, ncol - kmax);
+      if (!tr->upload(*P, prec, LEFT)) return fail(P, "getrf_qrf: device allocation failed");
+      prev = P->task(1, [=](hipStream_t s) { return tr->launch(prec, LEFT, LOWER, NOTRANS, UNIT, one, buf, M, buf, M, s); },
+                     {prev});
+    }
+    // ---- DECIDE (host, one synchronisation): the criterion from the domain LU and the untouched column k
+    auto dec = std::make_shared<int>(0);
+    state->dec.push_back(dec);
+    const int r0 = k * mb, mrows = A->m - r0;
+    const std::vector<int> off_c = off, dom_c = dom;
+    prev = P->task(1, [=](hipStream_t s) {
+      if (hipStreamSynchronize(s) != hipSuccess) return -1;
+      int bad = 0;
+      if (hipMemcpy(&bad, dinfo, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+      std::vector<cplx> col, lu;
+      const bool need_col = criteria == LQ_MUMPS || criteria == LQ_HIGHAM || criteria == LQ_HSUM ||
+                            criteria == LQ_HMAX || criteria == LQ_HMOY;
+      if (need_col && !host_block(prec, a + A->off(k, k) * es, ld, mrows, ncol, col)) return -1;
+      double w0 = 0.0, offsum = 0.0, offmax = 0.0;
+      std::vector<double> cm_off(ncol, 0.0), cm_diag(ncol, 0.0);
+      if (need_col) {
+        for (int m : off_c) {   // 1-norms / column maxima of the off-domain tiles of column k
+          const int rr = A->rows(m), base = (m - k) * mb;
+          double tn = 0;
+          for (int j = 0; j < ncol; ++j) {
+            double sj = 0, mj = 0;
+            for (int i = 0; i < rr; ++i) {
+              const double v = std::abs(col[base + i + (size_t)j * mrows]);
+              sj += v;
+              mj = std::max(mj, v);
+            }
+            tn = std::max(tn, sj);
+            cm_off[j] = std::max(cm_off[j], mj);
+          }
+          offsum += tn;
+          offmax = std::max(offmax, tn);
+        }
+        for (int j = 0; j < ncol; ++j)
+          for (int i = 0; i < std::min(ncol, A->rows(k)); ++i) cm_diag[j] = std::max(cm_diag[j], std::abs(col[i + (size_t)j * mrows]));
+      }
+      if (!bad && (criteria == LQ_HIGHAM || criteria == LQ_HSUM || criteria == LQ_HMAX || criteria == LQ_HMOY)) {
+        const int n = kmax;
+        if (!host_block(prec, buf, M, n, n, lu)) return -1;
+        std::vector<cplx> U((size_t)n * n, 0.0), L((size_t)n * n, 0.0);
+        for (int j = 0; j < n; ++j)
+          for (int i = 0; i < n; ++i) {
+            if (i <= j) U[i + (size_t)j * n] = lu[i + (size_t)j * n];
+            if (i > j) L[i + (size_t)j * n] = lu[i + (size_t)j * n];
+          }
+        const std::vector<cplx> Ui = tri_inverse(U, n, true, false);
+        if (criteria == LQ_HIGHAM) {
+          w0 = norm1(U, n, n, n) * norm1(Ui, n, n, n);
+        } else {   // 1 / ||U^-1 L^-1||_1
+          const std::vector<cplx> Li = tri_inverse(L, n, false, true);
+          std::vector<cplx> X((size_t)n * n, 0.0);
+          for (int j = 0; j < n; ++j)
+            for (int l = j; l < n; ++l) {   // Li is unit lower: column j nonzero from row j
+              const cplx x = Li[l + (size_t)j * n];
+              if (x == 0.0) continue;
+              for (int i = 0; i <= l; ++i) X[i + (size_t)j * n] += Ui[i + (size_t)l * n] * x;
+            }
+          w0 = 1.0 / norm1(X, n, n, n);
+        }
+      }
+      int cond;
+      if (bad) cond = 0;
+      else if (criteria == LQ_HIGHAM || criteria == LQ_HSUM) cond = alpha * w0 > offsum;
+      else if (criteria == LQ_HMAX) cond = alpha * w0 > offmax;
+      else if (criteria == LQ_HMOY) {
+        const int ntk = A->mt - k, nout = ntk - (ntk + pgrid - 1) / pgrid;
+        cond = nout ? alpha * w0 > offsum / nout : 0;   // 0 / 0: the reference's NaN comparison
+      } else if (criteria == LQ_MUMPS) {
+        cond = 1;
+        for (int j = 0; j < ncol; ++j)
+          if (!(alpha * cm_diag[j] >= cm_off[j])) cond = 0;
+      } else if (criteria == LQ_LU_ONLY) cond = 1;
+      else if (criteria == LQ_QR_ONLY) cond = 0;
+      else if (criteria == LQ_RANDOM) cond = state->table[k];
+      else cond = k % 2;
+      if (!bad) {
+        if (alpha == 0) cond = 0;
+        if (alpha >= 9999999999.0) cond = 1;
+      }
+      *dec = cond;
+      if (lu_tab) lu_tab[k] = cond;
+      return 0;
+    }, {prev});
+    // ---- LU branch (predicated on *dec == 1)
+    P->cur_guard = dec;
+    P->cur_want = 1;
+    prev = P->task(1, [=](hipStream_t s) {
+      return dpl_geadd(prec, 0, NOTRANS, back->n(), back->items(), back->mm, back->nn, one.ptr(), buf, M, zero.ptr(), a, ld, 1, s);
+    }, {prev});
+    int* ipk = ipg + IP->off(k, k);
+    const int rk = A->rows(k);
+    prev = P->task(1, [=](hipStream_t s) {
+      if (hipMemsetAsync(ipk, 0, sizeof(int) * rk, s) != hipSuccess) return -1;
+      return dpl_ipiv_shift(piv, ipk, kmax, 1, s);
+    }, {prev});
+    // interchanges inside the domain stack of the trailing columns: gather, laswp, scatter
+    const int ntc = A->n - (k + 1) * nb;
+    if (ntc > 0) {
+      auto tg = std::make_shared<MapBatch>(), ts = std::make_shared<MapBatch>();
+      for (size_t i = 0; i < dom.size(); ++i)
+        for (int n = k + 1; n < A->nt; ++n) {
+          const long long so = soff[i] + (long long)(n - k - 1) * nb * M;
+          tg->it.push_back(TileItem{A->off(dom[i], n), so, A->rows(dom[i]), A->cols(n), 0, 0});
+          ts->it.push_back(TileItem{so, A->off(dom[i], n), A->rows(dom[i]), A->cols(n), 0, 0});
+        }
+      tg->mm = ts->mm = mb;
+      tg->nn = ts->nn = nb;
+      if (!tg->upload(*P) || !ts->upload(*P)) return fail(P, "getrf_qrf: device allocation failed");
+      prev = P->task(1, [=](hipStream_t s) {
+        int rc = dpl_geadd(prec, 0, NOTRANS, tg->n(), tg->items(), tg->mm, tg->nn, one.ptr(), a, ld, zero.ptr(), wt, M, 1, s);
+        if (rc == 0) rc = dpl_laswp_panel(prec, wt, M, M, 0, ntc, piv, 0, kmax, dinfo, s);
+        if (rc == 0)
+          rc = dpl_geadd(prec, 0, NOTRANS, ts->n(), ts->items(), ts->mm, ts->nn, one.ptr(), wt, M, zero.ptr(), a, ld, 1, s);
+        return rc;
+      }, {prev});
+      // U row: A(k, n) := L_kk^-1 A(k, n)
+      auto tr = std::make_shared<Trsm1>();
+      tr->tri = A->off(k, k);
+      for (int n = k + 1; n < A->nt; ++n) tr->add(A->off(k, n), kmax, A->cols(n));
+      if (!tr->upload(*P, prec, LEFT)) return fail(P, "getrf_qrf: device allocation failed");
+      prev = P->task(1, [=](hipStream_t s) { return tr->launch(prec, LEFT, LOWER, NOTRANS, UNIT, one, a, ld, a, ld, s); },
+                     {prev});
+    }
+    if (!off.empty()) {   // off-domain tiles: A(m, k) := A(m, k) U_kk^-1
+      auto tr = std::make_shared<Trsm1>();
+      tr->tri = A->off(k, k);
+      for (int m : off) tr->add(A->off(m, k), A->rows(m), ncol);
+      if (!tr->upload(*P, prec, RIGHT)) return fail(P, "getrf_qrf: device allocation failed");
+      prev = P->task(1, [=](hipStream_t s) { return tr->launch(prec, RIGHT, UPPER, NOTRANS, NONUNIT, one, a, ld, a, ld, s); },
+                     {prev});
+    }
+    if (k + 1 < A->mt && k + 1 < A->nt) {
+      auto g = std::make_shared<Gemm>();
+      for (int n = k + 1; n < A->nt; ++n)
+        for (int m = k + 1; m < A->mt; ++m) g->add(A->off(m, n), A->rows(m), A->cols(n), {KPair{A->off(m, k), A->off(k, n), kmax, 0}}, 0);
+      if (!g->upload(*P)) return fail(P, "getrf_qrf: device allocation failed");
+      prev = P->task(1, [=](hipStream_t s) { return g->launch(prec, NOTRANS, NOTRANS, m_one, a, ld, a, ld, one, a, ld, s); },
+                     {prev});
+    }
+    // ---- QR branch (predicated on *dec == 0): the tree's step k
+    P->cur_want = 0;
+    prev = P->task(1, [=](hipStream_t s) { return (int)hipMemsetAsync(ipk, 0, sizeof(int) * rk, s); }, {prev});
+    for (const QpEntry& e : ents[k]) {
+      prev = add_qp_factor_entry(*P, *A, *TS, *TT, e, qb, false, 1, prev);
+      if (prev < -1) return fail(P, "getrf_qrf: device allocation failed");
+    }
+    P->cur_guard.reset();
+    P->cur_want = 1;
+  }
+  return P;
+}
+
+// B := the hybrid factorization's L_k^-1 P_k / Q_k^H applied in step order (lu_tab from getrf_qrf); the solve
+// x = U^-1 (that B) is the caller's trsm with A's upper triangle (tests/testing_zgetrf_qrf.c)
+NatProgram* nat_trsmpl_qrf(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* dA, dplasma_desc_t* dIP,
+                           dplasma_desc_t* dB, dplasma_desc_t* dTS, dplasma_desc_t* dTT, int* lu_tab) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *IP = dIP ? dIP->nat : nullptr, *B = dB ? dB->nat : nullptr,
+          *TS = dTS ? dTS->nat : nullptr, *TT = dTT ? dTT->nat : nullptr;
+  const nq::Tree* t = nat_qrtree(q);
+  if (!same_ctx(c, {A, B, TS, TT}, prec) || !IP || IP->ctx != c)
+    return fail(nullptr, "trsmpl_qrf: descriptors of another context or precision");
+  if (!luqr_conform(A, IP, TS, TT) || !tree_fits(t, *A) || !lu_tab || B->m != A->m || B->mb != A->mb)
+    return fail(nullptr, "trsmpl_qrf: operands of getrf_qrf (with its lu_tab), B with A's rows");
+  const auto ents = qp_entries(*t, *A);
+  if (!tree_T_ok(*TS, *A, ents, false) || !tree_T_ok(*TT, *A, ents, true))
+    return fail(nullptr, "trsmpl_qrf: TS / TT must come from the native getrf_qrf of A with this tree");
+  NatProgram* P = new_program(c, "trsmpl_qrf", true);
+  const int kt = std::min(A->mt, A->nt), mb = A->mb, es = A->es, pgrid = std::max(1, env_int("DPLASMA_LUQR_P", A->P));
+  QpBufs qb;
+  if (!qp_bufs(*P, *A, ents, (size_t)A->nb * std::max(1, B->n), qb)) return fail(P, "trsmpl_qrf: device allocation failed");
+  DevPtr WT = dev_alloc((size_t)std::max(1, A->m) * std::max(1, B->n) * es, false);
+  DevPtr PV = dev_alloc(sizeof(int) * (mb + 16), true);
+  if (!WT || !PV) return fail(P, "trsmpl_qrf: device allocation failed");
+  P->keep.push_back(WT);
+  P->keep.push_back(PV);
+  char *a = A->data, *b = B->data, *wt = (char*)WT->p;
+  int* pv = (int*)PV->p;
+  int* info = (int*)P->info->p;
+  const int lda = A->lld, ldb = B->lld;
+  const Scalar one(prec, 1.0), m_one(prec, -1.0), zero(prec, 0.0);
+  int prev = -1;
+  for (int k = 0; k < kt; ++k) {
+    if (!lu_tab[k]) {
+      for (const QpEntry& e : ents[k]) {
+        prev = add_entry_v(*P, *A, e, (char*)qb.V->p, qb.ld, 1, prev);
+        if (prev < -1) return fail(P, "trsmpl_qrf: device allocation failed");
+        std::vector<int> cols;
+        for (int j = 0; j < B->nt; ++j) cols.push_back(j);
+        int out = prev;
+        if (!add_left_apply_rows(*P, prec, *B, e.rows, e.voff, e.kf, (char*)qb.V->p, qb.ld, qp_slot(e.tt ? *TT : *TS, e),
+                                 A->nb, true, (char*)qb.W->p, (char*)qb.W2->p, cols, 1, prev, out))
+          return fail(P, "trsmpl_qrf: device allocation failed");
+        prev = out;
+      }
+      continue;
+    }
+    std::vector<int> dom;
+    std::vector<long long> soff;
+    int M = 0;
+    for (int m = k; m < A->mt; m += pgrid) {
+      dom.push_back(m);
+      soff.push_back(M);
+      M += A->rows(m);
+    }
+    const int kmax = std::min(M, A->cols(k));
+    const int* ipk = (const int*)IP->data + IP->off(k, k);
+    auto tg = std::make_shared<MapBatch>(), ts = std::make_shared<MapBatch>();
+    for (size_t i = 0; i < dom.size(); ++i)
+      for (int n = 0; n < B->nt; ++n) {
+        const long long so = soff[i] + (long long)n * B->nb * M;
+        tg->it.push_back(TileItem{B->off(dom[i], n), so, B->rows(dom[i]), B->cols(n), 0, 0});
+        ts->it.push_back(TileItem{so, B->off(dom[i], n), B->rows(dom[i]), B->cols(n), 0, 0});
+      }
+    tg->mm = ts->mm = mb;
+    tg->nn = ts->nn = B->nb;
+    if (!tg->upload(*P) || !ts->upload(*P)) return fail(P, "trsmpl_qrf: device allocation failed");
+    const int bn = B->n;
+    prev = P->task(1, [=](hipStream_t s) {   // the domain rows of B interchanged with the step's 1-based stack pivots
+      int rc = dpl_ipiv_shift(ipk, pv, kmax, -1, s);
+      if (rc == 0)
+        rc = dpl_geadd(prec, 0, NOTRANS, tg->n(), tg->items(), tg->mm, tg->nn, one.ptr(), b, ldb, zero.ptr(), wt, M, 1, s);
+      if (rc == 0) rc = dpl_laswp_panel(prec, wt, M, M, 0, bn, pv, 0, kmax, info, s);
+      if (rc == 0)
+        rc = dpl_geadd(prec, 0, NOTRANS, ts->n(), ts->items(), ts->mm, ts->nn, one.ptr(), wt, M, zero.ptr(), b, ldb, 1, s);
+      return rc;
+    }, {prev});
+    auto tr = std::make_shared<Trsm1>();
+    tr->tri = A->off(k, k);
+    for (int n = 0; n < B->nt; ++n) tr->add(B->off(k, n), kmax, B->cols(n));
+    if (!tr->upload(*P, prec, LEFT)) return fail(P, "trsmpl_qrf: device allocation failed");
+    prev = P->task(1, [=](hipStream_t s) { return tr->launch(prec, LEFT, LOWER, NOTRANS, UNIT, one, a, lda, b, ldb, s); },
+                   {prev});
+    if (k + 1 < B->mt) {
+      auto g = std::make_shared<Gemm>();
+      for (int n = 0; n < B->nt; ++n)
+        for (int m = k + 1; m < B->mt; ++m) g->add(B->off(m, n), B->rows(m), B->cols(n), {KPair{A->off(m, k), B->off(k, n), kmax, 0}}, 0);
+      if (!g->upload(*P)) return fail(P, "trsmpl_qrf: device allocation failed");
+      prev = P->task(1, [=](hipStream_t s) { return g->launch(prec, NOTRANS, NOTRANS, m_one, a, lda, b, ldb, one, b, ldb, s); },
+                     {prev});
+    }
+  }
   return P;
 }
 

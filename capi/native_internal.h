@@ -206,6 +206,10 @@ struct NatTask {
   std::vector<int> deps;
   std::function<int(hipStream_t)> fn;
   bool event = false;
+  // predicated task (a data-dependent branch decided by an earlier task at enqueue time): fn runs only if
+  // *guard == want; otherwise the task launches nothing (its event, if any, is still recorded)
+  std::shared_ptr<int> guard;
+  int want = 1;
 };
 
 struct NatProgram {
@@ -222,10 +226,16 @@ struct NatProgram {
   // (blocking posv: the reference's zposv_wrapper runs potrs only then); run() synchronises at the gate
   int gate = -1;
 
+  // tasks added while cur_guard is set are predicated on *cur_guard == cur_want
+  std::shared_ptr<int> cur_guard;
+  int cur_want = 1;
+
   int task(int stream, std::function<int(hipStream_t)> fn, std::initializer_list<int> deps) {
     NatTask t;
     t.stream = stream;
     t.fn = std::move(fn);
+    t.guard = cur_guard;
+    t.want = cur_want;
     const int id = (int)tasks.size();
     for (int d : deps) {
       if (d < 0 || d >= id) continue;
@@ -265,7 +275,7 @@ struct NatProgram {
       hipStream_t s = ctx->st[t.stream];
       for (int d : t.deps)
         if (tasks[d].stream != t.stream && hipStreamWaitEvent(s, ev[d], 0) != hipSuccess) return -1;
-      const int rc = t.fn(s);
+      const int rc = (t.guard && *t.guard != t.want) ? 0 : t.fn(s);
       if (rc != 0) {
         if (const char* e = std::getenv("DPLASMA_NATIVE_DEBUG"); e && *e == '1')
           std::fprintf(stderr, "[native] %s: task %zu of %zu (stream %d) failed: %d\n", name.c_str(), i, tasks.size(),

@@ -913,7 +913,7 @@ static void test_dgeqrf_param(dplasma_context_t *ctx) {
   dplasma_desc_get_lapack(F, f0, m);
   double an = 0;
   for (size_t e = 0; e < (size_t)m * n; ++e) an = fmax(an, fabs(a[e]));
-  for (int kind = 0; kind < 4; ++kind) {
+  for (int kind = 0; kind < 5; ++kind) {
     dplasma_qrtree_t qt;
     memset(&qt, 0, sizeof qt);
     int rc;
@@ -921,7 +921,8 @@ static void test_dgeqrf_param(dplasma_context_t *ctx) {
     if (kind == 0) rc = dplasma_hqr_init(&qt, dplasmaNoTrans, A, DPLASMA_GREEDY_TREE, DPLASMA_FLAT_TREE, 2, 3, 0, 0), nm = "hqr greedy/flat a=2 p=3";
     else if (kind == 1) rc = dplasma_hqr_init(&qt, dplasmaNoTrans, A, 3, DPLASMA_GREEDY_TREE, 1, 2, 1, 0), nm = "hqr binary/greedy p=2 domino";
     else if (kind == 2) rc = dplasma_systolic_init(&qt, dplasmaNoTrans, A, 2, 2), nm = "systolic 2x2";
-    else rc = dplasma_svd_init(&qt, dplasmaNoTrans, A, 2, 2, 2, 1), nm = "svd fibonacci p=2";
+    else if (kind == 3) rc = dplasma_svd_init(&qt, dplasmaNoTrans, A, 2, 2, 2, 1), nm = "svd fibonacci p=2";
+    else rc = dplasma_hqr_init(&qt, dplasmaNoTrans, A, DPLASMA_GREEDY_TREE, DPLASMA_FLAT_TREE, 4, 1, 0, 0), nm = "hqr greedy a=4";
     CHECK(rc == 0, "%s init: %s", nm, dplasma_last_error());
     if (rc) continue;
     CHECK(qt.mt == mt && qt.nt == nt, "%s dims %d x %d", nm, qt.mt, qt.nt);
@@ -1058,6 +1059,132 @@ static void test_dgelqf_param(dplasma_context_t *ctx) {
   free(a), free(f), free(q), free(c), free(b), free(y);
   dplasma_desc_destroy(A), dplasma_desc_destroy(Q), dplasma_desc_destroy(C), dplasma_desc_destroy(B);
   dplasma_desc_destroy(TS), dplasma_desc_destroy(TT);
+}
+
+/* hybrid LU-QR (native getrf_qrf + trsmpl_qrf, HQR greedy tree a = 4): per criterion the lu_tab pattern (DEFAULT
+ * alternates, LU_ONLY / QR_ONLY, RANDOM balanced, HIGHAM / MUMPS on one process row: LU unless singular) and the
+ * solve x = U^-1 trsmpl_qrf(b) checked as ||A x - b|| / (||A|| ||x|| n) (tests/testing_zgetrf_qrf.c) */
+static void test_dgetrf_qrf(dplasma_context_t *ctx) {
+  const int n = 900, nb = 128, ib = 32, nrhs = 3;
+  const int mt = (n + nb - 1) / nb;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, n, n), *B = dmat(ctx, dplasmaRealDouble, nb, n, nrhs);
+  dplasma_desc_t *TS = dplasma_desc_block_cyclic(ctx, dplasmaRealDouble, ib, nb, mt * ib, mt * nb, 1, 1, dplasmaUpperLower);
+  dplasma_desc_t *TT = dplasma_desc_block_cyclic(ctx, dplasmaRealDouble, ib, nb, mt * ib, mt * nb, 1, 1, dplasmaUpperLower);
+  dplasma_desc_t *IP = dplasma_desc_ipiv(ctx, nb, 1, mt * nb, mt, 1, 1);
+  CHECK(A && B && TS && TT && IP, "getrf_qrf descriptors: %s", dplasma_last_error());
+  double *a = malloc(sizeof(double) * n * n), *b = malloc(sizeof(double) * n * nrhs), *x = malloc(sizeof(double) * n * nrhs);
+  unsigned sd = 733;
+  rnd_fill(a, (size_t)n * n, &sd), rnd_fill(b, (size_t)n * nrhs, &sd);
+  dplasma_qrtree_t qt;
+  memset(&qt, 0, sizeof qt);
+  CHECK(dplasma_hqr_init(&qt, dplasmaNoTrans, A, DPLASMA_GREEDY_TREE, DPLASMA_FLAT_TREE, 4, 1, 0, 0) == 0, "tree: %s",
+        dplasma_last_error());
+  const int crit[] = {0, 3, 4, 5, 1, 2};
+  const double alph[] = {1.0, 1.0, 1.0, 50.0, 1.0, 1.0};
+  const char *names[] = {"DEFAULT", "LU_ONLY", "QR_ONLY", "RANDOM 50%", "HIGHAM", "MUMPS"};
+  for (int c = 0; c < 6; ++c) {
+    int lu_tab[64], info = -7;
+    memset(lu_tab, 0xff, sizeof lu_tab);
+    dplasma_desc_set_lapack(A, a, n);
+    int rc = dplasma_dgetrf_qrf(ctx, &qt, A, IP, TS, TT, crit[c], alph[c], lu_tab, &info);
+    CHECK(rc == 0 && info == 0, "dgetrf_qrf %s rc %d info %d (%s)", names[c], rc, info, dplasma_last_error());
+    int nlu = 0, pat = 1;
+    char tab[80];
+    for (int k = 0; k < mt; ++k) {
+      nlu += lu_tab[k] == 1;
+      tab[k] = lu_tab[k] == 1 ? 'L' : (lu_tab[k] == 0 ? 'Q' : '?');
+      if (crit[c] == 0 && lu_tab[k] != k % 2) pat = 0;
+      if ((crit[c] == 3 || crit[c] == 1 || crit[c] == 2) && lu_tab[k] != 1) pat = 0;
+      if (crit[c] == 4 && lu_tab[k] != 0) pat = 0;
+    }
+    tab[mt] = 0;
+    if (crit[c] == 5 && nlu != (int)lround(mt * 0.5)) pat = 0;
+    dplasma_desc_set_lapack(B, b, n);
+    CHECK(dplasma_dtrsmpl_qrf(ctx, &qt, A, IP, B, TS, TT, lu_tab) == 0, "dtrsmpl_qrf %s: %s", names[c], dplasma_last_error());
+    CHECK(dplasma_dtrsm(ctx, dplasmaLeft, dplasmaUpper, dplasmaNoTrans, dplasmaNonUnit, 1.0, A, B) == 0, "trsm: %s",
+          dplasma_last_error());
+    dplasma_desc_get_lapack(B, x, n);
+    double err = 0, an = 0, xn = 0;
+    for (size_t e = 0; e < (size_t)n * n; ++e) an = fmax(an, fabs(a[e]));
+    for (int r = 0; r < nrhs; ++r)
+      for (int i = 0; i < n; ++i) {
+        double s = 0;
+        for (int k = 0; k < n; ++k) s += a[i + (size_t)k * n] * x[k + (size_t)r * n];
+        err = fmax(err, fabs(s - b[i + (size_t)r * n]));
+        xn = fmax(xn, fabs(x[i + (size_t)r * n]));
+      }
+    const double rel = err / (an * xn * n);
+    printf("dgetrf_qrf %-10s lu_tab %s  ||Ax-b||/(||A|| ||x|| n) %.2e\n", names[c], tab, rel);
+    CHECK(pat && rel < 1e-15, "getrf_qrf %s: pattern %d residual %.3e", names[c], pat, rel);
+  }
+  dplasma_hqr_finalize(&qt);
+  free(a), free(b), free(x);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(B), dplasma_desc_destroy(TS), dplasma_desc_destroy(TT);
+  dplasma_desc_destroy(IP);
+}
+
+/* getrf_qrf with data-dependent criteria on a p = 2 domain period (DPLASMA_LUQR_P): the same matrix as
+ * tests/test_lu_qr.py _luqr_run (plrnt seed 7, N 1536, NB 256, HQR greedy/flat a = 2 p = 2); prints lu_tab per
+ * (criterion, alpha) and dumps the factors under DPLASMA_TEST_DUMP for tests/test_capi.py to compare with the Python
+ * engine; solve residual checked here */
+static void test_dgetrf_qrf_criteria(dplasma_context_t *ctx) {
+  const int n = 1536, nb = 256, ib = 32, nrhs = 2;
+  const int mt = n / nb;
+  setenv("DPLASMA_LUQR_P", "2", 1);
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, n, n), *B = dmat(ctx, dplasmaRealDouble, nb, n, nrhs);
+  dplasma_desc_t *TS = dplasma_desc_block_cyclic(ctx, dplasmaRealDouble, ib, nb, mt * ib, n, 1, 1, dplasmaUpperLower);
+  dplasma_desc_t *TT = dplasma_desc_block_cyclic(ctx, dplasmaRealDouble, ib, nb, mt * ib, n, 1, 1, dplasmaUpperLower);
+  dplasma_desc_t *IP = dplasma_desc_ipiv(ctx, nb, 1, n, mt, 1, 1);
+  CHECK(A && B && TS && TT && IP, "getrf_qrf criteria descriptors: %s", dplasma_last_error());
+  double *a = malloc(sizeof(double) * n * n), *f = malloc(sizeof(double) * n * n);
+  double *b = malloc(sizeof(double) * n * nrhs), *x = malloc(sizeof(double) * n * nrhs);
+  CHECK(dplasma_dplrnt(ctx, 0, A, 7) == 0 && dplasma_dplrnt(ctx, 0, B, 8) == 0, "plrnt: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(A, a, n);
+  dplasma_desc_get_lapack(B, b, n);
+  dplasma_qrtree_t qt;
+  memset(&qt, 0, sizeof qt);
+  CHECK(dplasma_hqr_init(&qt, dplasmaNoTrans, A, DPLASMA_GREEDY_TREE, DPLASMA_FLAT_TREE, 2, 2, 0, 0) == 0, "tree: %s",
+        dplasma_last_error());
+  const int crit[] = {1, 6, 7, 8, 2, 2};
+  const double alph[] = {0.02, 1.0, 2.0, 4.0, 1.0, 3.0};
+  const char *dump = getenv("DPLASMA_TEST_DUMP");
+  for (int c = 0; c < 6; ++c) {
+    int lu_tab[16], info = -7;
+    dplasma_desc_set_lapack(A, a, n);
+    int rc = dplasma_dgetrf_qrf(ctx, &qt, A, IP, TS, TT, crit[c], alph[c], lu_tab, &info);
+    CHECK(rc == 0 && info == 0, "dgetrf_qrf crit %d rc %d info %d (%s)", crit[c], rc, info, dplasma_last_error());
+    char tab[32];
+    for (int k = 0; k < mt; ++k) tab[k] = lu_tab[k] ? 'L' : 'Q';
+    tab[mt] = 0;
+    dplasma_desc_get_lapack(A, f, n);
+    if (dump) {
+      char path[512];
+      snprintf(path, sizeof path, "%s/luqr_%d_%g.bin", dump, crit[c], alph[c]);
+      FILE *fp = fopen(path, "wb");
+      if (fp) fwrite(f, sizeof(double), (size_t)n * n, fp), fclose(fp);
+    }
+    dplasma_desc_set_lapack(B, b, n);
+    CHECK(dplasma_dtrsmpl_qrf(ctx, &qt, A, IP, B, TS, TT, lu_tab) == 0, "dtrsmpl_qrf: %s", dplasma_last_error());
+    CHECK(dplasma_dtrsm(ctx, dplasmaLeft, dplasmaUpper, dplasmaNoTrans, dplasmaNonUnit, 1.0, A, B) == 0, "trsm: %s",
+          dplasma_last_error());
+    dplasma_desc_get_lapack(B, x, n);
+    double err = 0, an = 0, xn = 0;
+    for (size_t e = 0; e < (size_t)n * n; ++e) an = fmax(an, fabs(a[e]));
+    for (int r = 0; r < nrhs; ++r)
+      for (int i = 0; i < n; ++i) {
+        double s = 0;
+        for (int k = 0; k < n; ++k) s += a[i + (size_t)k * n] * x[k + (size_t)r * n];
+        err = fmax(err, fabs(s - b[i + (size_t)r * n]));
+        xn = fmax(xn, fabs(x[i + (size_t)r * n]));
+      }
+    printf("luqr_criteria crit=%d alpha=%g lu_tab=%s resid=%.2e\n", crit[c], alph[c], tab, err / (an * xn * n));
+    CHECK(err / (an * xn * n) < 1e-15, "getrf_qrf crit %d residual", crit[c]);
+  }
+  unsetenv("DPLASMA_LUQR_P");
+  dplasma_hqr_finalize(&qt);
+  free(a), free(f), free(b), free(x);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(B), dplasma_desc_destroy(TS), dplasma_desc_destroy(TT);
+  dplasma_desc_destroy(IP);
 }
 
 /* trtri / lauum / potri / poinv natively: A := inv(A) checked as ||A0 inv(A) - I||; lauum against host
@@ -1605,6 +1732,8 @@ int main(int argc, char **argv) {
   test_zgelqf(ctx);
   test_dgeqrf_param(ctx);
   test_dgelqf_param(ctx);
+  test_dgetrf_qrf(ctx);
+  test_dgetrf_qrf_criteria(ctx);
   test_inverse_family(ctx);
   test_rank_2k(ctx);
   test_aliases(ctx);

@@ -189,6 +189,47 @@ def test_capi_native_pltmg_matches_python(tmp_path):
 
 
 @pytest.mark.gpu
+def test_capi_native_luqr_matches_python(tmp_path):
+    """Native getrf_qrf (capi/native.cpp) against the Python engine (models/lu_qr.py) with data-dependent criteria
+    on a p = 2 domain period: the same plrnt matrix (seed 7, N 1536, NB 256) and HQR tree (greedy / flat, a = 2,
+    p = 2) give the same lu_tab for HIGHAM / SUM / MAX / MOY / MUMPS and the same factors (the QR steps' updates
+    round differently: V (T^T (V^T C)) natively, (V T) (V^T C) in Python)."""
+    import numpy as np
+    import torch
+    env = dict(os.environ)
+    env.pop("PYTHONPATH", None)
+    env["DPLASMA_TEST_DUMP"] = str(tmp_path)
+    r = subprocess.run([_build_native(tmp_path)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    native = {}
+    for ln in r.stdout.splitlines():
+        if ln.startswith("luqr_criteria"):
+            kv = dict(x.split("=") for x in ln.split()[1:])
+            native[(int(kv["crit"]), float(kv["alpha"]))] = kv["lu_tab"]
+    assert len(native) == 6, r.stdout
+    import dplasma_amd as dp
+    from dplasma_amd.models import qrtree
+    g = dp.init(device="cuda:0")
+    N, NB = 1536, 256
+    for (crit, alpha), tab_n in sorted(native.items()):
+        A = dp.block_cyclic(g, torch.float64, NB, NB, N, N)
+        dp.plrnt(g, A, 7)
+        TS = dp.block_cyclic(g, torch.float64, 32, NB, A.mt * 32, N)
+        TT = dp.block_cyclic(g, torch.float64, 32, NB, A.mt * 32, N)
+        IP = dp.qrf_ipiv_descriptor(g, A)
+        tree = qrtree.hqr_init(dp.dplasmaNoTrans, A, qrtree.GREEDY_TREE, qrtree.FLAT_TREE, 2, 2)
+        tab = [0] * A.mt
+        dp.getrf_qrf(g, tree, A, IP, TS, TT, crit, alpha, tab, p=2)
+        tab_p = "".join("L" if t else "Q" for t in tab)
+        print(crit, alpha, "native", tab_n, "python", tab_p)
+        assert tab_n == tab_p, (crit, alpha)
+        got = np.fromfile(str(tmp_path / f"luqr_{crit}_{alpha:g}.bin"), dtype=np.float64).reshape(N, N).T
+        ref = A.to_dense_local().cpu().numpy()
+        err = np.abs(got - ref).max() / max(1.0, np.abs(ref).max())
+        assert err < 1e-9, (crit, alpha, err)
+
+
+@pytest.mark.gpu
 def test_capi_f77_native_gpu(tmp_path):
     """ScaLAPACK F77 entry points without Python (one process, 1 x 1 BLACS grid -> the native engine):
     pdpotrf_ / pdgemm_ / pdgetrf_ / pdtrsm_ / pdtrmm_ on submatrices of host local arrays
@@ -343,5 +384,5 @@ def test_capi_ext_native_routing():
         for op in native:
             ln = lines[f"dplasma_{p}{op}"]
             assert "if (dpl_native(ctx)) return nat_" in ln and "nat_unsupported" not in ln, (p, op)
-        for op in ("heev", "getrf_qrf", "hbrdt"):
+        for op in ("heev", "herbt", "hbrdt"):
             assert f'nat_unsupported("{p}{op}")' in lines[f"dplasma_{p}{op}"], (p, op)

@@ -194,6 +194,9 @@ NATIVE_EXT = {
     "unglq_param": lambda pc: f"nat_unglq_param(ctx, {pc}, qrtree, A, TS, TT, Q)",
     "geqrs_param": lambda pc: f"nat_geqrs_param(ctx, {pc}, qrtree, A, TS, TT, B)",
     "gelqs_param": lambda pc: f"nat_gelqs_param(ctx, {pc}, qrtree, A, TS, TT, B)",
+    # hybrid LU-QR (native.cpp nat_getrf_qrf: predicated LU / QR branches after a host decision per step)
+    "getrf_qrf": lambda pc: f"nat_getrf_qrf(ctx, {pc}, qrtree, A, IPIV, TS, TT, criteria, alpha, lu_tab, INFO)",
+    "trsmpl_qrf": lambda pc: f"nat_trsmpl_qrf(ctx, {pc}, qrtree, A, IPIV, B, TS, TT, lu_tab)",
 }
 # EXT entry points the engine answers directly (a value, no program)
 NATIVE_EXT_DIRECT = {
