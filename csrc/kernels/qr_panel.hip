@@ -179,8 +179,12 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
       if (G <= 16) {
         // every workgroup sums the partials itself (same order everywhere: identical G)
         for (int e = tid; e < QP_B * QP_B; e += 256) {
+          T t16[16];
+#pragma unroll
+          for (int bb = 0; bb < 16; ++bb) t16[bb] = bb < G ? ld_sc1(&part2[(long long)bb * QP_B * QP_B + e]) : T(0);
           T s = T(0);
-          for (int bb = 0; bb < G; ++bb) s += ld_sc1(&part2[(long long)bb * QP_B * QP_B + e]);
+#pragma unroll
+          for (int bb = 0; bb < 16; ++bb) s += t16[bb];
           Gm[e >> 5][e & 31] = s;
         }
       } else {
@@ -191,7 +195,16 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
           const int e = base + (tid & 31), g = tid >> 5;
           T s = T(0);
           if (e < e_end)
-            for (int bb = g; bb < G; bb += 8) s += ld_sc1(&part2[(long long)bb * QP_B * QP_B + e]);
+            for (int bb0 = g; bb0 < G; bb0 += 64) {   // 8 partials in flight per thread
+              T t8[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                const int bb = bb0 + 8 * u;
+                t8[u] = bb < G ? ld_sc1(&part2[(long long)bb * QP_B * QP_B + e]) : T(0);
+              }
+#pragma unroll
+              for (int u = 0; u < 8; ++u) s += t8[u];
+            }
           red[g][tid & 31] = s;
           __syncthreads();
           if (tid < 32 && e < e_end) {
@@ -478,8 +491,12 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
       const long long epw = (E + G - 1) / G;
       const long long e_beg = (long long)w * epw, e_end = min(E, e_beg + epw);
       for (long long e = e_beg + tid; e < e_end; e += 256) {
+        T t8[8];
+#pragma unroll
+        for (int bb = 0; bb < 8; ++bb) t8[bb] = bb < G ? ld_sc1(&part2[(long long)bb * E + e]) : T(0);
         T y = T(0);
-        for (int bb = 0; bb < G; ++bb) y += ld_sc1(&part2[(long long)bb * E + e]);
+#pragma unroll
+        for (int bb = 0; bb < 8; ++bb) y += t8[bb];
         st_sc1(&Yg[e], y);
         const int p = (int)(e / nX), xc = (int)(e - (long long)p * nX);
         if (xc >= QP_B && xc < QP_B + b0) st_sc1(&Xc[((long long)b * QP_B + p) * kf + xc - QP_B], y);
@@ -492,7 +509,16 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
         const int g = tid >> 5;
         T s = T(0);
         if (e < e_end)
-          for (int bb = g; bb < G; bb += 8) s += ld_sc1(&part2[(long long)bb * E + e]);
+          for (int bb0 = g; bb0 < G; bb0 += 64) {   // 8 partials in flight per thread
+            T t8[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const int bb = bb0 + 8 * u;
+              t8[u] = bb < G ? ld_sc1(&part2[(long long)bb * E + e]) : T(0);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += t8[u];
+          }
         red[g][tid & 31] = s;
         __syncthreads();
         if (tid < 32 && e < e_end) {
@@ -516,16 +542,34 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
     }
     __syncthreads();
     if (tid < bw) {
-      // lane i builds row i of T_b: T(i, j) = -tau_j sum_{k=i}^{j-1} T(i, k) G(k, j)
-      const int i = tid;
+      // T_b in two 16-reflector halves: lane i builds row i of T11 (i < 16) or of T22 (the compact-WY factor of
+      // reflectors 16..31 alone) by the dlarft recurrence T(i, j) = -tau_j sum_{k=i}^{j-1} T(i, k) G(k, j) --
+      // a quarter of the 32-long recurrence's sequential work (~20 us of LDS round trips per block before)
+      const int i = tid, h1 = min(bw, (i < 16 ? 0 : 16) + 16);
       Ts[i][i] = taus[i];
-      for (int jc = i + 1; jc < bw; ++jc) {
+      for (int jc = i + 1; jc < h1; ++jc) {
         T z = T(0);
         for (int k = i; k < jc; ++k) z += Ts[k][i] * Ws[jc][k];
         Ts[jc][i] = -taus[jc] * z;
       }
     }
     __syncthreads();
+    if (bw > 16) {
+      // T12 = -T11 (V1^T V2) T22: X = G12 T22 then T11 X, a thread per entry (16 x 16 = 256 threads); Xs is idle
+      // between the column steps and the trailing update
+      const int i = tid & 15, j = 16 + (tid >> 4);
+      T x = T(0);
+      if (j < bw)
+        for (int k = 16; k <= j; ++k) x += Ws[k][i] * Ts[j][k];   // G(i, k) T22(k, j)
+      Xs[j - 16][i] = x;
+      __syncthreads();
+      if (j < bw) {
+        T y = T(0);
+        for (int k = i; k < 16; ++k) y += Ts[k][i] * Xs[j - 16][k];
+        Ts[j][i] = -y;
+      }
+      __syncthreads();
+    }
     if (w == 0)
       for (int e = tid; e < bw * bw; e += 256) {
         const int c = e / bw, i = e - c * bw;
