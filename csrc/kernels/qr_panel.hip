@@ -45,6 +45,11 @@ template <> struct QPM<double> {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, c, 0, 0, 0);
   }
   static __device__ inline int drow(int l, int r) { return (l >> 4) + 4 * r; }
+  static __device__ inline double rcp(double d) {   // 1/d: hardware estimate + 2 Newton steps
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(fma(-d, r, 1.0), r, r);
+    return fma(fma(-d, r, 1.0), r, r);
+  }
 };
 template <> struct QPM<float> {
   typedef f4_t acc_t;
@@ -52,6 +57,7 @@ template <> struct QPM<float> {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(x, y, c, 0, 0, 0);
   }
   static __device__ inline int drow(int l, int r) { return (l >> 4) * 4 + r; }
+  static __device__ inline float rcp(float d) { return 1.0f / d; }
 };
 
 // mma(x, y, acc): D(p, q) += sum_k x(p, k) y(q, k); input lane l carries p (resp. q) = l & 15,
@@ -101,7 +107,7 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
   // optional phase timers (workgroup 0, 100 MHz ticks): 0 column-step compute, 1 column barrier,
   // 2 partial reduction, 3 Y partials, 4 Y barriers + reduction + T_b, 5 trailing update, 6 T coupling
   const bool tprof = prof != nullptr && w == 0 && tid == 0;
-  unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tacc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};   // slot 8: column steps up to the reflector effects
   long long nfast = 0, nexact = 0, first_exact = -1;
   double fe_x2 = 0.0, fe_g0 = 0.0;
   unsigned long long tlast = tprof ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -233,6 +239,19 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
     for (int jj = 0; jj < bw; ++jj) {
       const int j = b0 + jj;
       const int sh = QP_B - jj;  // live slots: slot s is column jj + s
+      // this thread's replica operands (entries (r0 + 8u, c) below): they do not depend on the column's
+      // reflector, so their LDS loads are issued first and overlap its computation
+      const int rc_c = tid & 31, rc_r0 = tid >> 5;
+      T p_trj[4], p_tjr[4], p_tpv[4], p_gmv[4];
+      const T p_tjc = Tp[jj][rc_c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = rc_r0 + 8 * u;
+        p_trj[u] = Tp[r][jj];
+        p_tjr[u] = Tp[jj][r];
+        p_tpv[u] = Tp[r][rc_c];
+        p_gmv[u] = Gm[r][rc_c];
+      }
       const T alpha = Tp[jj][jj], gjj = Gm[jj][jj];
       const T x2f = gjj - alpha * alpha;
       // uniform over the whole grid: every workgroup holds the same replicas
@@ -248,8 +267,10 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
       if (fast) {
         const T nrm = sqrt(gjj);
         beta = alpha >= T(0) ? -nrm : nrm;
-        tau = (beta - alpha) / beta;
-        scale = T(1) / (alpha - beta);
+        // reciprocals by the hardware estimate + Newton steps (full precision) instead of two IEEE divisions on
+        // the column's dependent chain
+        tau = (beta - alpha) * MM::rcp(beta);
+        scale = MM::rcp(alpha - beta);
         // each wave derives the 32 effects itself (no workgroup barrier): lane s -> column jj + s
         if (l < QP_B) {
           const int c = jj + l;
@@ -264,7 +285,7 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         fw = red[wv];
-        QP_TICK(1);
+        QP_TICK(8);
       } else {
       const int par = nsync & 1;
       {
@@ -369,28 +390,18 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
       // replicas: rows r > jj of the top block take the reflector like any row; the Gram matrix
       // of rows > j is the (unchanged) one of rows >= j minus the new row j's outer product
       {
-        // thread (c, r0) owns entries (r0 + 8u, c), u < 4: every operand is loaded before any store
-        const int c = tid & 31, r0 = tid >> 5;
+        // thread (c, r0) owns entries (r0 + 8u, c), u < 4: every operand was loaded at the top of the step
+        const int c = rc_c, r0 = rc_r0;
         if (c > jj) {
           const T fc = fw[c - jj];
-          const T njc = Tp[jj][c] - fc;
-          T trj[4], nrj[4], tpv[4], gmv[4];
+          const T njc = p_tjc - fc;
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int r = r0 + 8 * u;
             if (r > jj) {
-              trj[u] = Tp[r][jj];
-              nrj[u] = Tp[jj][r] - fw[r - jj];
-              tpv[u] = Tp[r][c];
-              gmv[u] = Gm[r][c];
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int r = r0 + 8 * u;
-            if (r > jj) {
-              Tp[r][c] = tpv[u] - (scale * trj[u]) * fc;
-              Gm[r][c] = gmv[u] - nrj[u] * njc;
+              const T nrj = p_tjr[u] - fw[r - jj];
+              Tp[r][c] = p_tpv[u] - (scale * p_trj[u]) * fc;
+              Gm[r][c] = p_gmv[u] - nrj * njc;
             }
           }
         }
@@ -710,6 +721,7 @@ __device__ __forceinline__ void qr_panel_body(T* __restrict__ P0, int ldp, int r
   QP_TICK(6);
   if (tprof)
     for (int i = 0; i < 8; ++i) prof[i] += (long long)tacc[i];
+  if (tprof) prof[13] += (long long)tacc[8];
   if (tprof) {   // column-path counters (the prof buffer holds 16 slots)
     prof[8] += nfast;
     prof[9] += nexact;

@@ -54,6 +54,8 @@ def run(M, nb, tt, reps=5):
     p = prof.cpu().tolist()
     tot = sum(p[:8]) or 1
     phases = ", ".join(f"{PH[i]} {p[i] / 100:.0f}us" for i in range(8) if p[i])
+    if p[13]:
+        phases += f", (col-effects {p[13] / 100:.0f}us)"
     print(f"M={M:6d} {('TTr' if tt == 'real' else 'TT') if tt else 'TS'} G={-(-M // 256):3d}  {min(ts):7.3f} ms  fast {p[8]} exact {p[9]} "
           f"first_exact {p[10]}  |R| err {err:.1e}\n    {phases}", flush=True)
 
