@@ -3210,17 +3210,295 @@ bool param_conform(const NatDesc* A, const NatDesc* TS, const NatDesc* TT) {
 
 }  // namespace
 
+// ----------------------------------------------------------------------------- tree-driven QR on a P x Q grid
+// geqrf_param / unmqr_param (left) / ungqr_param / geqrs_param on a multi-process native context (the native
+// flat geqrf's data movement, native_dist.cpp, generalised to a reduction tree).  Step k: tile column k (rows
+// k..) goes to every rank in one exchange and every rank runs the tree's entries of the step on its copy, in
+// plan order -- each TS domain / TT kill one stacked panel (dpl_qr_panel: deterministic, so every rank holds the
+// same R, V and T, replicated T slots as on one process) -- and after each entry the reflector is applied to
+// this rank's trailing tiles: W = V_e(local rows)^H C_loc, the partial W summed over the process column (one
+// exchange), C_loc -= V_e (T_e^H W).  The apply (unmqr_param) rebuilds V_e's local rows from column k's tiles
+// of this process row (sent along the row by the column's owner) and replays the entries forward (Q^H) or
+// backward (Q) the same way.
+namespace {
+
+struct DistQp {
+  DevPtr slots, pan, P, V, ws, W, W2, Wr, raw;
+  int ldv = 0, ldp = 0, ldr = 0;
+};
+
+bool dist_qp_bufs(NatProgram& P, const NatDesc& A, const NatDesc& C, const std::vector<std::vector<QpEntry>>& ents,
+                  DistQp& b) {
+  const int es = A.es, nb = A.nb, mb = A.mb;
+  int maxM = 16;
+  for (const auto& st : ents)
+    for (const QpEntry& e : st) maxM = std::max(maxM, e.M);
+  b.ldv = std::max(16, (A.m + 15) / 16 * 16);
+  b.ldp = (maxM + 15) / 16 * 16;
+  b.ldr = std::max(16, (A.lm + 15) / 16 * 16);
+  const size_t wlen = (size_t)nb * std::max(1, C.ln);
+  b.slots = dev_alloc((size_t)std::max(1, A.mt) * mb * nb * es, false);
+  b.pan = dev_alloc((size_t)b.ldv * nb * es, true);
+  b.P = dev_alloc((size_t)b.ldp * nb * es, true);
+  b.V = dev_alloc((size_t)b.ldp * nb * es, true);
+  b.ws = dev_alloc((size_t)dpl_qr_panel_ws_bytes(A.prec, nb, nb) + 256, true);
+  b.W = dev_alloc(wlen * es, true);
+  b.W2 = dev_alloc(wlen * es, true);
+  b.Wr = dev_alloc((size_t)std::max(1, A.P - 1) * wlen * es, true);
+  b.raw = dev_alloc((size_t)b.ldr * nb * es, true);
+  for (const DevPtr& d : {b.slots, b.pan, b.P, b.V, b.ws, b.W, b.W2, b.Wr, b.raw}) {
+    if (!d) return false;
+    P.keep.push_back(d);
+  }
+  return true;
+}
+
+// C(local rows of e, local columns j >= j0) := op(H_e) C, V_e rows at voff (ld ldv) of V; partial W summed over
+// the process column.  Stream 1 after prev.
+int add_dist_entry_apply(NatProgram& P, NatDesc& C, const QpEntry& e, char* V, int ldv, const char* Tk, int ldt, bool qt,
+                         int j0, const DistQp& b, int prev) {
+  NatComm* comm = P.ctx->comm;
+  const int prec = C.prec, es = C.es, ldc = C.lld, me = P.ctx->rank, kf = e.kf;
+  std::vector<int> cols;
+  for (int j = j0; j < C.nt; ++j)
+    if (j % C.Q == C.mycol) cols.push_back(j);
+  if (cols.empty() || kf <= 0) return prev;
+  std::vector<size_t> lr;   // indices of e's rows that are mine
+  for (size_t i = 0; i < e.rows.size(); ++i)
+    if (e.rows[i] % C.P == C.myrow) lr.push_back(i);
+  auto g1 = std::make_shared<Gemm>(), g2 = std::make_shared<Gemm>(), g3 = std::make_shared<Gemm>();
+  long long wo = 0;
+  for (int j : cols) {
+    const int nj = C.cols(j);
+    std::vector<KPair> kp;
+    for (size_t i : lr) kp.push_back(KPair{e.voff[i], C.off(e.rows[i], j), C.rows(e.rows[i]), 0});
+    if (!kp.empty()) g1->add(wo, kf, nj, kp, 0);
+    g2->add(wo, kf, nj, {KPair{0, wo, kf, 0}}, 0);
+    for (size_t i : lr) g3->add(C.off(e.rows[i], j), C.rows(e.rows[i]), nj, {KPair{e.voff[i], wo, kf, 0}}, 0);
+    wo += (long long)kf * nj;
+  }
+  if ((!g1->empty() && !g1->upload(P)) || !g2->upload(P) || (!g3->empty() && !g3->upload(P))) return -2;
+  const size_t wbytes = (size_t)wo * es;
+  char *W = (char*)b.W->p, *W2 = (char*)b.W2->p, *Wr = (char*)b.Wr->p, *c = C.data;
+  auto sends = std::make_shared<std::vector<NatMsg>>(), recvs = std::make_shared<std::vector<NatMsg>>();
+  int slot = 0;
+  for (int r = 0; r < C.P; ++r) {
+    const int peer = r * C.Q + C.mycol;
+    if (peer == me) continue;
+    sends->push_back(NatMsg{peer, W, wbytes});
+    recvs->push_back(NatMsg{peer, Wr + (size_t)slot * wbytes, wbytes});
+    ++slot;
+  }
+  const int nsl = slot;
+  std::vector<TileItem> sum_it{TileItem{0, 0, kf, (int)(wo / kf), 0, 0}};
+  DevPtr d_sum = dev_upload(sum_it);
+  if (!d_sum) return -2;
+  P.keep.push_back(d_sum);
+  const int wcols = (int)(wo / kf);
+  const Scalar one(prec, 1.0), zero(prec, 0.0), m_one(prec, -1.0);
+  return P.task(1, [=](hipStream_t s) {
+    int rc = 0;
+    if (g1->empty()) rc = hipMemsetAsync(W, 0, wbytes, s) == hipSuccess ? 0 : -1;
+    else rc = g1->launch(prec, CONJTRANS, NOTRANS, one, V, ldv, c, ldc, zero, W, kf, s);
+    if (rc == 0 && nsl) rc = comm->exchange(*sends, *recvs, s);
+    for (int q = 0; q < nsl && rc == 0; ++q)
+      rc = dpl_geadd(prec, 0, NOTRANS, 1, d_sum->p, kf, wcols, one.ptr(), Wr + (size_t)q * wbytes, kf, one.ptr(), W, kf, 0, s);
+    if (rc == 0) rc = g2->launch(prec, qt ? CONJTRANS : NOTRANS, NOTRANS, one, Tk, ldt, W, kf, zero, W2, kf, s);
+    if (rc == 0 && !g3->empty()) rc = g3->launch(prec, NOTRANS, NOTRANS, m_one, V, ldv, W2, kf, one, c, ldc, s);
+    return rc;
+  }, {prev});
+}
+
+bool dist_geqrf_param(NatProgram& P, const nq::Tree& tree, NatDesc& A, NatDesc& TS, NatDesc& TT) {
+  NatComm* comm = P.ctx->comm;
+  const int prec = A.prec, mb = A.mb, nb = A.nb, ld = A.lld, es = A.es, me = P.ctx->rank;
+  const auto ents = qp_entries(tree, A);
+  DistQp b;
+  if (!dist_qp_bufs(P, A, A, ents, b) || !qp_slots(P, TS, A, ents, false) || !qp_slots(P, TT, A, ents, true)) return false;
+  char *a = A.data, *sl = (char*)b.slots->p, *pan = (char*)b.pan->p, *pb = (char*)b.P->p, *vb = (char*)b.V->p;
+  char* ws = (char*)b.ws->p;
+  int* info = (int*)P.info->p;
+  const int ldv = b.ldv, ldp = b.ldp;
+  const size_t st = (size_t)mb * nb;
+  const Scalar one(prec, 1.0), zero(prec, 0.0);
+  int prev = -1;
+  for (const auto& step : ents) {
+    if (step.empty()) continue;
+    const int k = step[0].k, kb = A.cols(k);
+    // ---- tile column k (rows k..) to every rank, unpacked into the contiguous panel (tile m at row (m - k) mb)
+    auto pk = std::make_shared<MapBatch>(), sc = std::make_shared<MapBatch>(), back = std::make_shared<MapBatch>();
+    auto sends = std::make_shared<std::vector<NatMsg>>(), recvs = std::make_shared<std::vector<NatMsg>>();
+    for (int m = k; m < A.mt; ++m) {
+      const int src = A.owner(m, k);
+      char* slot = sl + (size_t)m * st * es;
+      if (src == me) {
+        pk->it.push_back(TileItem{A.off(m, k), (long long)m * (long long)st, A.rows(m), kb, 0, 0});
+        back->it.push_back(TileItem{(long long)(m - k) * mb, A.off(m, k), A.rows(m), kb, 0, 0});
+        for (int r = 0; r < P.ctx->world; ++r)
+          if (r != me) sends->push_back(NatMsg{r, slot, st * es});
+      } else {
+        recvs->push_back(NatMsg{src, slot, st * es});
+      }
+      sc->it.push_back(TileItem{(long long)m * (long long)st, (long long)(m - k) * mb, A.rows(m), kb, 0, 0});
+      pk->mm = sc->mm = back->mm = std::max(pk->mm, A.rows(m));
+    }
+    pk->nn = sc->nn = back->nn = kb;
+    if (!pk->upload(P) || !sc->upload(P) || !back->upload(P)) return false;
+    prev = P.task(1, [=](hipStream_t s) {
+      int rc = pk->n() ? dpl_geadd(prec, 0, NOTRANS, pk->n(), pk->items(), pk->mm, pk->nn, one.ptr(), a, ld, zero.ptr(), sl,
+                                   mb, 1, s) : 0;
+      if (rc == 0 && (!sends->empty() || !recvs->empty())) rc = comm->exchange(*sends, *recvs, s);
+      if (rc == 0)
+        rc = dpl_geadd(prec, 0, NOTRANS, sc->n(), sc->items(), sc->mm, sc->nn, one.ptr(), sl, mb, zero.ptr(), pan, ldv, 1, s);
+      return rc;
+    }, {prev});
+    // ---- the step's entries, each factored on every rank's panel copy, then applied to this rank's trailing tiles
+    for (const QpEntry& e : step) {
+      NatDesc& Td = e.tt ? TT : TS;
+      char* Tk = qp_slot(Td, e);
+      const int M = e.M, kf = e.kf, part = e.tt ? 2 : 0;
+      auto g = std::make_shared<MapBatch>(), w = std::make_shared<MapBatch>();
+      for (size_t i = 0; i < e.rows.size(); ++i) {
+        const long long po = (long long)(e.rows[i] - k) * mb;
+        g->it.push_back(TileItem{po, e.voff[i], A.rows(e.rows[i]), kb, 0, 0});
+        w->it.push_back(TileItem{e.voff[i], po, A.rows(e.rows[i]), kb, 0, 0});
+        g->mm = w->mm = std::max(g->mm, A.rows(e.rows[i]));
+      }
+      g->nn = w->nn = kb;
+      if (!g->upload(P) || !w->upload(P)) return false;
+      const bool tt = e.tt;
+      prev = P.task(1, [=](hipStream_t s) {
+        int rc = tt ? (hipMemsetAsync(pb, 0, (size_t)ldp * kb * es, s) == hipSuccess ? 0 : -1) : 0;
+        if (rc == 0)
+          rc = dpl_geadd(prec, part, NOTRANS, g->n(), g->items(), g->mm, g->nn, one.ptr(), pan, ldv, zero.ptr(), pb, ldp, 1, s);
+        if (rc == 0) rc = dpl_qr_panel(prec, pb, ldp, 0, 0, M, kb, kf, vb, ldp, Tk, nb, ws, info, s);
+        if (rc == 0)
+          rc = dpl_geadd(prec, part, NOTRANS, w->n(), w->items(), w->mm, w->nn, one.ptr(), pb, ldp, zero.ptr(), pan, ldv, 1, s);
+        return rc;
+      }, {prev});
+      if (Td.local(e.trow, k)) {   // reference layout: IB x IB diagonal blocks of T into tile (trow, k)
+        const int ib = Td.mb;
+        std::vector<TileItem> it;
+        for (int b0 = 0; b0 < kf; b0 += ib) {
+          const int bs = std::min(ib, kf - b0);
+          it.push_back(TileItem{b0 + (long long)b0 * nb, Td.off(e.trow, k) + (long long)b0 * Td.lld, bs, bs, 0, 0});
+        }
+        auto d = dev_upload(it);
+        if (!d) return false;
+        P.keep.push_back(d);
+        const int n = (int)it.size(), ldT = Td.lld;
+        char* td = Td.data;
+        prev = P.task(1, [=](hipStream_t s) {
+          return dpl_geadd(prec, 0, NOTRANS, n, d->p, ib, ib, one.ptr(), Tk, nb, zero.ptr(), td, ldT, 1, s);
+        }, {prev});
+      }
+      prev = add_dist_entry_apply(P, A, e, vb, ldp, Tk, nb, true, k + 1, b, prev);
+      if (prev < -1) return false;
+    }
+    // ---- this rank's tiles of the factored column back into A
+    if (back->n())
+      prev = P.task(1, [=](hipStream_t s) {
+        return dpl_geadd(prec, 0, NOTRANS, back->n(), back->items(), back->mm, back->nn, one.ptr(), pan, ldv, zero.ptr(), a, ld,
+                         1, s);
+      }, {prev});
+  }
+  return true;
+}
+
+// C := op(Q) C (left), Q from dist_geqrf_param of A with the same tree; C distributed like A's rows
+bool dist_unmqr_param(NatProgram& P, const nq::Tree& tree, int trans, NatDesc& A, NatDesc& TS, NatDesc& TT, NatDesc& C) {
+  NatComm* comm = P.ctx->comm;
+  const int prec = A.prec, mb = A.mb, ld = A.lld, es = A.es, Q = A.Q;
+  const bool qt = trans != NOTRANS;
+  const auto ents = qp_entries(tree, A);
+  if (!tree_T_ok(TS, A, ents, false) || !tree_T_ok(TT, A, ents, true)) return false;
+  DistQp b;
+  if (!dist_qp_bufs(P, A, C, ents, b)) return false;
+  char *a = A.data, *raw = (char*)b.raw->p, *vb = (char*)b.V->p;
+  const int ldr = b.ldr, ldp = b.ldp;
+  const Scalar one(prec, 1.0), zero(prec, 0.0);
+  const int kt = (int)ents.size();
+  int prev = -1;
+  for (int s = 0; s < kt; ++s) {
+    const int k = qt ? s : kt - 1 - s;   // Q^H C: step 0 first; Q C: the last first
+    if (ents[k].empty()) continue;
+    const int kb = A.cols(k), pc = k % Q;
+    // my process row's rows of column k (local tile rows >= k) from the column's owner in this row
+    long long lr0 = A.lm;
+    for (int m = k; m < A.mt; ++m)
+      if (m % A.P == A.myrow) {
+        lr0 = (long long)(m / A.P) * mb;
+        break;
+      }
+    const long long rows = A.lm - lr0;
+    auto sends = std::make_shared<std::vector<NatMsg>>(), recvs = std::make_shared<std::vector<NatMsg>>();
+    const size_t rbytes = (size_t)ldr * kb * es;
+    if (rows > 0) {
+      if (A.mycol == pc) {
+        for (int q = 0; q < Q; ++q)
+          if (q != A.mycol) sends->push_back(NatMsg{A.myrow * Q + q, raw, rbytes});
+      } else {
+        recvs->push_back(NatMsg{A.myrow * Q + pc, raw, rbytes});
+      }
+    }
+    const bool mine = A.mycol == pc && rows > 0;
+    const long long coff = lr0 + (long long)(k / Q) * A.nb * ld;
+    prev = P.task(1, [=](hipStream_t st) {
+      int rc = 0;
+      if (mine && hipMemcpy2DAsync(raw, (size_t)ldr * es, a + coff * es, (size_t)ld * es, (size_t)rows * es, kb,
+                                   hipMemcpyDeviceToDevice, st) != hipSuccess)
+        rc = -1;
+      if (rc == 0 && (!sends->empty() || !recvs->empty())) rc = comm->exchange(*sends, *recvs, st);
+      return rc;
+    }, {prev});
+    std::vector<const QpEntry*> order;
+    for (const QpEntry& e : ents[k]) order.push_back(&e);
+    if (!qt) std::reverse(order.begin(), order.end());
+    for (const QpEntry* ep : order) {
+      const QpEntry& e = *ep;
+      // V_e's local rows (stack coordinates at voff) from raw: TS domain -- strictly below the stacked diagonal with
+      // a unit diagonal; TT kill -- identity on the survivor's rows, the upper part of the victim's tile
+      auto lt = std::make_shared<MapBatch>(), cp = std::make_shared<MapBatch>();
+      for (size_t i = 0; i < e.rows.size(); ++i) {
+        const int r = e.rows[i];
+        if (r % A.P != A.myrow) continue;
+        const long long ro = (long long)(r / A.P) * mb - lr0;
+        lt->it.push_back(TileItem{e.voff[i], 0, A.rows(r), kb, e.voff[i], 0});
+        if (!e.tt) cp->it.push_back(TileItem{ro, e.voff[i], A.rows(r), kb, e.voff[i], 0});
+        else if (i == 1) cp->it.push_back(TileItem{ro, e.voff[i], A.rows(r), kb, 0, 0});
+        lt->mm = cp->mm = std::max(lt->mm, A.rows(r));
+      }
+      lt->nn = cp->nn = kb;
+      if (!lt->upload(P) || !cp->upload(P)) return false;
+      const int part = e.tt ? 2 : 3;
+      prev = P.task(1, [=](hipStream_t st) {
+        int rc = lt->n() ? dpl_laset(prec, 0, lt->n(), lt->items(), lt->mm, lt->nn, zero.ptr(), one.ptr(), vb, ldp, st) : 0;
+        if (rc == 0 && cp->n())
+          rc = dpl_geadd(prec, part, NOTRANS, cp->n(), cp->items(), cp->mm, cp->nn, one.ptr(), raw, ldr, zero.ptr(), vb, ldp, 1,
+                         st);
+        return rc;
+      }, {prev});
+      prev = add_dist_entry_apply(P, C, e, vb, ldp, qp_slot(e.tt ? TT : TS, e), A.nb, qt, 0, b, prev);
+      if (prev < -1) return false;
+    }
+  }
+  return true;
+}
+
+}  // namespace
+
 NatProgram* nat_geqrf_param(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* dA,
                             dplasma_desc_t* dTS, dplasma_desc_t* dTT) {
   NatCtx* c = ctx->nat;
   NatDesc *A = dA ? dA->nat : nullptr, *TS = dTS ? dTS->nat : nullptr, *TT = dTT ? dTT->nat : nullptr;
   const nq::Tree* t = nat_qrtree(q);
-  if (!same_ctx(c, {A, TS, TT}, prec)) return fail(nullptr, "geqrf_param: descriptors of another context or precision");
+  if (!same_ctx_dist(c, {A, TS, TT}, prec)) return fail(nullptr, "geqrf_param: descriptors of another context or precision");
   if (!param_conform(A, TS, TT)) return fail(nullptr, "geqrf_param: square tiles <= 256 and TS / TT of (IB x NB) tiles");
   if (!tree_fits(t, *A)) return fail(nullptr, "geqrf_param: a native tree built for A's tile rows and columns");
   NatProgram* P = new_program(c, "geqrf_param", true);
   int last = -1;
-  if (!P->info || !add_geqrf_param(*P, *t, *A, *TS, *TT, false, last)) return fail(P, "geqrf_param: device allocation failed");
+  if (!P->info || !(c->dist() ? dist_geqrf_param(*P, *t, *A, *TS, *TT) : add_geqrf_param(*P, *t, *A, *TS, *TT, false, last)))
+    return fail(P, "geqrf_param: device allocation failed");
   return P;
 }
 
@@ -3230,13 +3508,14 @@ NatProgram* nat_unmqr_param(dplasma_context_t* ctx, int prec, int side, int tran
   NatDesc *A = dA ? dA->nat : nullptr, *TS = dTS ? dTS->nat : nullptr, *TT = dTT ? dTT->nat : nullptr,
           *C = dC ? dC->nat : nullptr;
   const nq::Tree* t = nat_qrtree(q);
-  if (!same_ctx(c, {A, TS, TT, C}, prec)) return fail(nullptr, "unmqr_param: descriptors of another context or precision");
+  if (!same_ctx_dist(c, {A, TS, TT, C}, prec)) return fail(nullptr, "unmqr_param: descriptors of another context or precision");
   if (!param_conform(A, TS, TT) || !tree_fits(t, *A)) return fail(nullptr, "unmqr_param: operands of geqrf_param");
   if ((side == LEFT && (C->m != A->m || C->mb != A->mb)) || (side == RIGHT && (C->n != A->m || C->nb != A->mb)))
     return fail(nullptr, "unmqr_param: C does not conform to Q");
+  if (c->dist() && side != LEFT) return fail(nullptr, "unmqr_param: a multi-process context applies Q from the left");
   NatProgram* P = new_program(c, "unmqr_param", false);
   int last = -1;
-  if (!add_unmqr_param(*P, *t, side, trans, *A, *TS, *TT, *C, last))
+  if (!(c->dist() ? dist_unmqr_param(*P, *t, trans, *A, *TS, *TT, *C) : add_unmqr_param(*P, *t, side, trans, *A, *TS, *TT, *C, last)))
     return fail(P, "unmqr_param: TS / TT must come from the native geqrf_param of A with this tree");
   return P;
 }
@@ -3247,22 +3526,24 @@ NatProgram* nat_ungqr_param(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* 
   NatDesc *A = dA ? dA->nat : nullptr, *TS = dTS ? dTS->nat : nullptr, *TT = dTT ? dTT->nat : nullptr,
           *Q = dQ ? dQ->nat : nullptr;
   const nq::Tree* t = nat_qrtree(q);
-  if (!same_ctx(c, {A, TS, TT, Q}, prec)) return fail(nullptr, "ungqr_param: descriptors of another context or precision");
+  if (!same_ctx_dist(c, {A, TS, TT, Q}, prec)) return fail(nullptr, "ungqr_param: descriptors of another context or precision");
   if (!param_conform(A, TS, TT) || !tree_fits(t, *A) || Q->m != A->m || Q->mb != A->mb || Q->n > A->m)
     return fail(nullptr, "ungqr_param: operands of geqrf_param, Q with A's rows");
   NatProgram* P = new_program(c, "ungqr_param", false);
   std::vector<TileItem> it;
   for (int i = 0; i < Q->mt; ++i)
-    for (int j = 0; j < Q->nt; ++j) it.push_back(TileItem{Q->off(i, j), 0, Q->rows(i), Q->cols(j), i * Q->mb, j * Q->nb});
+    for (int j = 0; j < Q->nt; ++j)
+      if (Q->local(i, j)) it.push_back(TileItem{Q->off(i, j), 0, Q->rows(i), Q->cols(j), i * Q->mb, j * Q->nb});
   auto d_it = dev_upload(it);
   if (!d_it) return fail(P, "ungqr_param: device allocation failed");
   P->keep.push_back(d_it);
   const int n = (int)it.size(), mb = Q->mb, nb = Q->nb, ldq = Q->lld;
   char* qd = Q->data;
   const Scalar zero(prec, 0.0), one(prec, 1.0);
-  int last = P->task(1, [=](hipStream_t s) { return dpl_laset(prec, 0, n, d_it->p, mb, nb, zero.ptr(), one.ptr(), qd, ldq, s); },
-                     {});
-  if (!add_unmqr_param(*P, *t, LEFT, NOTRANS, *A, *TS, *TT, *Q, last))
+  int last = P->task(1, [=](hipStream_t s) {
+    return n ? dpl_laset(prec, 0, n, d_it->p, mb, nb, zero.ptr(), one.ptr(), qd, ldq, s) : 0;
+  }, {});
+  if (!(c->dist() ? dist_unmqr_param(*P, *t, NOTRANS, *A, *TS, *TT, *Q) : add_unmqr_param(*P, *t, LEFT, NOTRANS, *A, *TS, *TT, *Q, last)))
     return fail(P, "ungqr_param: TS / TT must come from the native geqrf_param of A with this tree");
   return P;
 }
@@ -3273,13 +3554,31 @@ NatProgram* nat_geqrs_param(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* 
   NatDesc *A = dA ? dA->nat : nullptr, *TS = dTS ? dTS->nat : nullptr, *TT = dTT ? dTT->nat : nullptr,
           *B = dB ? dB->nat : nullptr;
   const nq::Tree* t = nat_qrtree(q);
-  if (!same_ctx(c, {A, TS, TT, B}, prec)) return fail(nullptr, "geqrs_param: descriptors of another context or precision");
+  if (!same_ctx_dist(c, {A, TS, TT, B}, prec)) return fail(nullptr, "geqrs_param: descriptors of another context or precision");
   if (!param_conform(A, TS, TT) || !tree_fits(t, *A) || A->m < A->n || B->m != A->m || B->mb != A->mb)
     return fail(nullptr, "geqrs_param: operands of geqrf_param of an M >= N matrix, B with A's rows");
   NatProgram* P = new_program(c, "geqrs_param", false);
   int last = -1;
-  if (!add_unmqr_param(*P, *t, LEFT, CONJTRANS, *A, *TS, *TT, *B, last))
+  if (!(c->dist() ? dist_unmqr_param(*P, *t, CONJTRANS, *A, *TS, *TT, *B)
+                  : add_unmqr_param(*P, *t, LEFT, CONJTRANS, *A, *TS, *TT, *B, last)))
     return fail(P, "geqrs_param: TS / TT must come from the native geqrf_param of A with this tree");
+  if (c->dist()) {   // R X = (Q^H B)(0:N) on the grid
+    auto dv = [](const NatDesc& D, int r, int cc) {
+      auto v = std::make_shared<NatDesc>();
+      v->ctx = D.ctx, v->prec = D.prec, v->es = D.es, v->mb = D.mb, v->nb = D.nb, v->m = r, v->n = cc;
+      v->mt = (r + D.mb - 1) / D.mb, v->nt = (cc + D.nb - 1) / D.nb;
+      v->P = D.P, v->Q = D.Q, v->myrow = D.myrow, v->mycol = D.mycol;
+      v->lm = nat_numroc(r, D.mb, D.myrow, D.P), v->ln = nat_numroc(cc, D.nb, D.mycol, D.Q);
+      v->lld = D.lld, v->data = D.data, v->owned = false;
+      return v;
+    };
+    auto R = dv(*A, A->n, A->n), X = dv(*B, A->n, B->n);
+    P->wdesc.push_back(R);
+    P->wdesc.push_back(X);
+    if (!nat_dist_trsm_into(*P, LEFT, UPPER, NOTRANS, NONUNIT, Scalar(prec, 1.0), *R, *X))
+      return fail(P, "geqrs_param: device allocation failed");
+    return P;
+  }
   auto R = lead_view(*A, A->n, A->n), X = lead_view(*B, A->n, B->n);
   P->wdesc.push_back(R);
   P->wdesc.push_back(X);

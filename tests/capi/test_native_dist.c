@@ -359,6 +359,60 @@ static void test_qr(int m, int n, int nrhs, int nb, int ib) {
   free(X), free(Y), free(U), free(V);
 }
 
+/* tree-driven QR on the grid (geqrf_param, unmqr_param Q^H B, ungqr_param, geqrs_param; HQR greedy / greedy with
+ * TS domains of a = 2 tiles over p = P process rows) against the one-process native engine with the same tree:
+ * R / V tiles, Q^H B, Q and the least-squares solution, each rank on its tiles */
+static void test_qr_param(int m, int n, int nrhs, int nb, int ib, int llvl, int hlvl, int a) {
+  const int mt = (m + nb - 1) / nb, nt = (n + nb - 1) / nb;
+  dplasma_desc_t *A[2], *TS[2], *TT[2], *B[2], *B2[2], *Qm[2];
+  dplasma_context_t *cx[2] = {cd, c1};
+  dplasma_qrtree_t qt[2];
+  int ok = 1;
+  for (int s = 0; s < 2; ++s) {
+    A[s] = mat(cx[s], dplasmaRealDouble, nb, m, n);
+    B[s] = mat(cx[s], dplasmaRealDouble, nb, m, nrhs);
+    B2[s] = mat(cx[s], dplasmaRealDouble, nb, m, nrhs);
+    Qm[s] = mat(cx[s], dplasmaRealDouble, nb, m, n);
+    TS[s] = dplasma_desc_block_cyclic(cx[s], dplasmaRealDouble, ib, nb, mt * ib, nt * nb, 0, 0, dplasmaUpperLower);
+    TT[s] = dplasma_desc_block_cyclic(cx[s], dplasmaRealDouble, ib, nb, mt * ib, nt * nb, 0, 0, dplasmaUpperLower);
+    ok = ok && A[s] && B[s] && B2[s] && Qm[s] && TS[s] && TT[s];
+    memset(&qt[s], 0, sizeof qt[s]);
+    if (ok) ok = dplasma_hqr_init(&qt[s], dplasmaNoTrans, A[s], llvl, hlvl, a, P, 0, 0) == 0;
+  }
+  CHECK(ok, "qr_param descriptors / trees: %s", dplasma_last_error());
+  if (!ok) return;
+  for (int s = 0; s < 2; ++s) {
+    int rc = dplasma_dplrnt(cx[s], 0, A[s], 81) | dplasma_dplrnt(cx[s], 0, B[s], 82) | dplasma_dplrnt(cx[s], 0, B2[s], 82);
+    const int info = dplasma_dgeqrf_param(cx[s], &qt[s], A[s], TS[s], TT[s]);
+    rc |= dplasma_dunmqr_param(cx[s], dplasmaLeft, dplasmaTrans, &qt[s], A[s], TS[s], TT[s], B[s]);
+    rc |= dplasma_dungqr_param(cx[s], &qt[s], A[s], TS[s], TT[s], Qm[s]);
+    rc |= dplasma_dgeqrs_param(cx[s], &qt[s], A[s], TS[s], TT[s], B2[s]);
+    CHECK(rc == 0 && info == 0, "geqrf_param family (%s context): info %d rc %d %s", s ? "one-process" : "distributed", info,
+          rc, dplasma_last_error());
+  }
+  double *X = calloc((size_t)m * n, 8), *Y = calloc((size_t)m * n, 8);
+  double *U = calloc((size_t)m * nrhs, 8), *V = calloc((size_t)m * nrhs, 8);
+  CHECK(dplasma_desc_get_lapack(A[0], X, m) == 0 && dplasma_desc_get_lapack(A[1], Y, m) == 0, "get_lapack");
+  const double ea = cmp_local(X, Y, 0, m, n, nb, 'A');
+  CHECK(dplasma_desc_get_lapack(Qm[0], X, m) == 0 && dplasma_desc_get_lapack(Qm[1], Y, m) == 0, "get_lapack");
+  const double eq = cmp_local(X, Y, 0, m, n, nb, 'A');
+  CHECK(dplasma_desc_get_lapack(B[0], U, m) == 0 && dplasma_desc_get_lapack(B[1], V, m) == 0, "get_lapack");
+  const double eb = cmp_local(U, V, 0, m, nrhs, nb, 'A');
+  CHECK(dplasma_desc_get_lapack(B2[0], U, m) == 0 && dplasma_desc_get_lapack(B2[1], V, m) == 0, "get_lapack");
+  const double ex = cmp_local(U, V, 0, m, nrhs, nb, 'A');
+  if (rank == 0)
+    printf("dgeqrf_param family %dx%d tree (%d, %d, a=%d, p=%d) grid %dx%d: max rel diff R,V %.2e  Q %.2e  Q^T B %.2e  X %.2e\n",
+           m, n, llvl, hlvl, a, P, P, Q, ea, eq, eb, ex);
+  CHECK(ea < 1e-12 && eq < 1e-12 && eb < 1e-12 && ex < 1e-10, "distributed tree QR differs: %.2e %.2e %.2e %.2e", ea, eq,
+        eb, ex);
+  for (int s = 0; s < 2; ++s) {
+    dplasma_hqr_finalize(&qt[s]);
+    dplasma_desc_destroy(A[s]), dplasma_desc_destroy(TS[s]), dplasma_desc_destroy(TT[s]), dplasma_desc_destroy(B[s]);
+    dplasma_desc_destroy(B2[s]), dplasma_desc_destroy(Qm[s]);
+  }
+  free(X), free(Y), free(U), free(V);
+}
+
 /* transposed maps on the grid (a tile-by-tile distributed transpose): geadd / tradd with op(A) */
 static void test_trans_maps(int cplx, int uplo, int m, int n, int nb) {
   const int prec = cplx ? dplasmaComplexDouble : dplasmaRealDouble, es = cplx ? 16 : 8;
@@ -553,6 +607,8 @@ int main(int argc, char **argv) {
   test_posv(dplasmaComplexDouble, dplasmaLower, 400, 70, 64);
   test_qr(700, 450, 30, 64, 16);
   test_qr(512, 512, 64, 128, 32);
+  test_qr_param(700, 450, 30, 64, 16, 1, 1, 2);
+  test_qr_param(520, 520, 20, 64, 16, 3, 0, 1);
   test_trans_maps(0, dplasmaUpperLower, 530, 410, 64);
   test_trans_maps(1, dplasmaLower, 330, 330, 64);
   test_failing_potrf();
