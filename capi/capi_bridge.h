@@ -196,6 +196,10 @@ NatProgram* nat_getrf_qrf(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q,
                           dplasma_desc_t* TS, dplasma_desc_t* TT, int criteria, double alpha, int* lu_tab, int* INFO);
 NatProgram* nat_trsmpl_qrf(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q, dplasma_desc_t* A, dplasma_desc_t* IPIV,
                            dplasma_desc_t* B, dplasma_desc_t* TS, dplasma_desc_t* TT, int* lu_tab);
+NatProgram* nat_herbt(dplasma_context_t* ctx, int prec, int uplo, int ib, dplasma_desc_t* A, dplasma_desc_t* T);
+NatProgram* nat_hbrdt(dplasma_context_t* ctx, int prec, dplasma_desc_t* A);
+NatProgram* nat_heev(dplasma_context_t* ctx, int prec, int jobz, int uplo, dplasma_desc_t* A, dplasma_desc_t* W,
+                     dplasma_desc_t* Z);
 NatProgram* nat_trdsm(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* B);
 NatProgram* nat_trmdm(dplasma_context_t* ctx, int prec, dplasma_desc_t* A);
 int nat_latms(dplasma_context_t* ctx, int prec, int mtxtype, double cond, dplasma_desc_t* A, unsigned long long seed);

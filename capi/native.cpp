@@ -19,12 +19,15 @@
 // lantr, plghe, plgsy, plrnt.
 // Every other entry point returns an error on a native context.
 #include <complex>
+#include <limits>
+#include <thread>
 #include <map>
 #include <set>
 
 #include "native_comm.h"
 #include "native_internal.h"
 #include "native_qrtree.h"
+#include "../csrc/runtime/band_core.h"
 
 
 namespace {
@@ -4128,6 +4131,312 @@ NatProgram* nat_trsmpl_qrf(dplasma_context_t* ctx, int prec, dplasma_qrtree_t* q
                      {prev});
     }
   }
+  return P;
+}
+
+// ----------------------------------------------------------------------------- eigenvalues (herbt, hbrdt, heev)
+// dplasma_zherbt / zhbrdt / zheev (reference src/zherbt_L.jdf, zhbrdt.jdf, zheev_wrapper.c; models/eigen.py) on one
+// process.  herbt: the uplo triangle mirrored into full Hermitian storage, then per panel k the tile column k below
+// the diagonal block (rows k+1..) factored in place as one Householder panel (dpl_qr_panel) and applied from both
+// sides to the trailing block A(k+1:, k+1:) -- Q^H from the left (columns k+1..), Q from the right (rows k+1..) --
+// with the batched MFMA GEMM engine; T's IB x IB diagonal blocks into tile T(k+1, k); Upper: the band mirrored
+// back.  hbrdt: the Hermitian band -> real tridiagonal bulge chase of csrc/runtime/band_core.h on the host;
+// eigenvalues of the tridiagonal by implicit QL with Wilkinson-type shifts (the role of LAPACK dsterf).
+namespace {
+
+// dst := the conjugate transpose of the uplo triangle (full Hermitian storage); band_only: the first
+// sub/super-diagonal tiles only.  Stream 1 after prev.
+int add_mirror(NatProgram& P, NatDesc& A, int uplo, bool band_only, int prev) {
+  auto off = std::make_shared<MapBatch>(), dia = std::make_shared<MapBatch>();
+  for (int n = 0; n < A.nt; ++n) {
+    const int mend = band_only ? std::min(A.mt, n + 2) : A.mt;
+    for (int m = n + 1; m < mend; ++m) {
+      if (uplo == LOWER) off->it.push_back(TileItem{A.off(m, n), A.off(n, m), A.rows(n), A.cols(m), 0, 0});
+      else off->it.push_back(TileItem{A.off(n, m), A.off(m, n), A.rows(m), A.cols(n), 0, 0});
+    }
+    if (n < A.mt) dia->it.push_back(TileItem{A.off(n, n), A.off(n, n), A.rows(n), A.cols(n), 0, 0});
+  }
+  for (auto* b : {off.get(), dia.get()}) {
+    for (const TileItem& x : b->it) {
+      b->mm = std::max(b->mm, x.m);
+      b->nn = std::max(b->nn, x.n);
+    }
+  }
+  if (!off->upload(P) || !dia->upload(P)) return -2;
+  const int prec = A.prec, ld = A.lld, dpart = uplo == LOWER ? 4 : 3;   // the other triangle of the diagonal tiles
+  char* a = A.data;
+  const Scalar one(prec, 1.0), zero(prec, 0.0);
+  return P.task(1, [=](hipStream_t s) {
+    int rc = off->n() ? dpl_geadd(prec, 0, CONJTRANS, off->n(), off->items(), off->mm, off->nn, one.ptr(), a, ld, zero.ptr(),
+                                  a, ld, 1, s) : 0;
+    if (rc == 0 && dia->n())
+      rc = dpl_geadd(prec, dpart, CONJTRANS, dia->n(), dia->items(), dia->mm, dia->nn, one.ptr(), a, ld, zero.ptr(), a, ld, 1, s);
+    return rc;
+  }, {prev});
+}
+
+bool add_herbt(NatProgram& P, int uplo, NatDesc& A, NatDesc& T, int& last) {
+  const int prec = A.prec, nb = A.nb, es = A.es, ld = A.lld, mb = A.mb;
+  int prev = add_mirror(P, A, uplo, false, last);
+  if (prev < -1) return false;
+  if (A.mt > 1) {
+    const int ldv = std::max(16, (A.m + 15) / 16 * 16);
+    DevPtr V = dev_alloc((size_t)ldv * nb * es, true), Tk = dev_alloc((size_t)nb * nb * es, true);
+    DevPtr W = dev_alloc((size_t)std::max(ldv, nb * std::max(1, A.nt)) * nb * es, false);
+    DevPtr W2 = dev_alloc((size_t)std::max(ldv, nb * std::max(1, A.nt)) * nb * es, false);
+    DevPtr ws = dev_alloc((size_t)dpl_qr_panel_ws_bytes(prec, nb, nb) + 256, true);
+    for (const DevPtr& d : {V, Tk, W, W2, ws}) {
+      if (!d) return false;
+      P.keep.push_back(d);
+    }
+    char *a = A.data, *v = (char*)V->p, *tk = (char*)Tk->p, *w = (char*)W->p, *w2 = (char*)W2->p, *wsp = (char*)ws->p;
+    int* info = (int*)P.info->p;
+    const Scalar one(prec, 1.0), zero(prec, 0.0), m_one(prec, -1.0);
+    for (int k = 0; k + 1 < A.mt && k < A.nt; ++k) {
+      const int r0 = k + 1, M = A.m - r0 * mb, kb = A.cols(k), kf = std::min(M, kb);
+      char* pk = a + A.off(r0, k) * es;
+      prev = P.task(1, [=](hipStream_t s) { return dpl_qr_panel(prec, pk, ld, 0, 0, M, kb, kf, v, ldv, tk, nb, wsp, info, s); },
+                    {prev});
+      if (r0 < T.mt && k < T.nt) {   // reference layout: T's IB x IB diagonal blocks into tile T(k+1, k)
+        const int ib = T.mb;
+        std::vector<TileItem> it;
+        for (int b0 = 0; b0 < kf; b0 += ib) {
+          const int bs = std::min(ib, kf - b0);
+          it.push_back(TileItem{b0 + (long long)b0 * nb, T.off(r0, k) + (long long)b0 * T.lld, bs, bs, 0, 0});
+        }
+        auto d = dev_upload(it);
+        if (!d) return false;
+        P.keep.push_back(d);
+        const int n = (int)it.size(), ldT = T.lld;
+        char* td = T.data;
+        prev = P.task(1, [=](hipStream_t s) {
+          return dpl_geadd(prec, 0, NOTRANS, n, d->p, ib, ib, one.ptr(), tk, nb, zero.ptr(), td, ldT, 1, s);
+        }, {prev});
+      }
+      // left: A(k+1:, k+1:) := Q^H A(k+1:, k+1:)
+      std::vector<int> cols;
+      for (int j = r0; j < A.nt; ++j) cols.push_back(j);
+      int out = prev;
+      if (!add_left_apply(P, prec, A, r0, M, kf, v, ldv, tk, nb, true, w, w2, cols, 1, prev, out)) return false;
+      prev = out;
+      // right: A(k+1:, k+1:) := A(k+1:, k+1:) Q  (W = C V, W2 = W T, C -= W2 V^H; rows k+1.. only)
+      auto g1 = std::make_shared<Gemm>(), g2 = std::make_shared<Gemm>(), g3 = std::make_shared<Gemm>();
+      const int ldw = ldv;
+      for (int i = r0; i < A.mt; ++i) {
+        const long long wo = (long long)(i - r0) * mb;
+        std::vector<KPair> kp;
+        for (int j = r0; j < A.nt; ++j) kp.push_back(KPair{A.off(i, j), (long long)(j - r0) * mb, A.cols(j), 0});
+        g1->add(wo, A.rows(i), kf, kp, 0);
+        g2->add(wo, A.rows(i), kf, {KPair{wo, 0, kf, 0}}, 0);
+        for (int j = r0; j < A.nt; ++j) g3->add(A.off(i, j), A.rows(i), A.cols(j), {KPair{wo, (long long)(j - r0) * mb, kf, 0}}, 0);
+      }
+      if (!g1->upload(P) || !g2->upload(P) || !g3->upload(P)) return false;
+      prev = P.task(1, [=](hipStream_t s) {
+        int rc = g1->launch(prec, NOTRANS, NOTRANS, one, a, ld, v, ldv, zero, w, ldw, s);
+        if (rc == 0) rc = g2->launch(prec, NOTRANS, NOTRANS, one, w, ldw, tk, nb, zero, w2, ldw, s);
+        if (rc == 0) rc = g3->launch(prec, NOTRANS, CONJTRANS, m_one, w2, ldw, v, ldv, one, a, ld, s);
+        return rc;
+      }, {prev});
+    }
+  }
+  if (uplo == UPPER) {   // the reduced band back into the upper triangle
+    prev = add_mirror(P, A, LOWER, true, prev);
+    if (prev < -1) return false;
+  }
+  last = prev;
+  return true;
+}
+
+// eigenvalues (ascending) of the symmetric tridiagonal (d, e) by implicit QL: false if an eigenvalue took more
+// than 64 sweeps
+bool tridiag_eigenvalues(std::vector<double>& d, std::vector<double> e) {
+  const int n = (int)d.size();
+  e.resize(std::max(n, 1), 0.0);
+  if (n > 0) e[n - 1] = 0.0;
+  const double eps = std::numeric_limits<double>::epsilon();
+  for (int l = 0; l < n; ++l) {
+    int iter = 0, m;
+    do {
+      for (m = l; m < n - 1; ++m) {
+        const double dd = std::fabs(d[m]) + std::fabs(d[m + 1]);
+        if (std::fabs(e[m]) <= eps * dd) break;
+      }
+      if (m != l) {
+        if (iter++ == 64) return false;
+        double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
+        double r = std::hypot(g, 1.0);
+        g = d[m] - d[l] + e[l] / (g + (g >= 0 ? std::fabs(r) : -std::fabs(r)));
+        double s = 1.0, c = 1.0, p = 0.0;
+        bool deflated = false;
+        for (int i = m - 1; i >= l; --i) {
+          double f = s * e[i];
+          const double b = c * e[i];
+          r = std::hypot(f, g);
+          e[i + 1] = r;
+          if (r == 0.0) {   // underflow: split here and restart the sweep
+            d[i + 1] -= p;
+            e[m] = 0.0;
+            deflated = true;
+            break;
+          }
+          s = f / r;
+          c = g / r;
+          g = d[i + 1] - p;
+          r = (d[i] - g) * s + 2.0 * c * b;
+          p = s * r;
+          d[i + 1] = g + p;
+          g = c * r - b;
+        }
+        if (deflated) continue;
+        d[l] -= p;
+        e[l] = g;
+        e[m] = 0.0;
+      }
+    } while (m != l);
+  }
+  std::sort(d.begin(), d.end());
+  return true;
+}
+
+template <typename TT>
+void band_chase(const std::vector<unsigned char>& raw, int ldab, int n, int b, std::vector<double>& d, std::vector<double>& e) {
+  using R = typename dpl_band::real_of<TT>::type;
+  std::vector<R> dr(n), er(std::max(n - 1, 0));
+  int nth = env_int("OMP_NUM_THREADS", 0);
+  if (nth <= 0) nth = (int)std::thread::hardware_concurrency();
+  nth = std::max(1, std::min(nth, 16));
+  dpl_band::hbrdt_core<TT>((const TT*)raw.data(), ldab, n, b, nth, dr.data(), er.data());
+  d.assign(dr.begin(), dr.end());
+  e.assign(er.begin(), er.end());
+}
+
+// the lower nb-band of A (after herbt) in LAPACK band storage AB(i - j, j), ldab = nb + 1, on the host
+bool host_lower_band(const NatDesc& A, std::vector<unsigned char>& ab) {
+  const int nb = A.nb, N = std::min(A.m, A.n), es = A.es, ldab = nb + 1;
+  ab.assign((size_t)ldab * std::max(N, 1) * es, 0);
+  std::vector<unsigned char> col((size_t)2 * nb * es);
+  for (int j = 0; j < N; ++j) {
+    const int rows = std::min(nb + 1, N - j);
+    if (hipMemcpy(col.data(), A.data + ((size_t)j * A.lld + j) * es, (size_t)rows * es, hipMemcpyDeviceToHost) != hipSuccess)
+      return false;
+    std::memcpy(ab.data() + (size_t)j * ldab * es, col.data(), (size_t)rows * es);
+  }
+  return true;
+}
+
+bool chase_and_solve(int prec, const std::vector<unsigned char>& ab, int ldab, int n, int b, std::vector<double>& w,
+                     std::vector<double>* e_out = nullptr) {
+  std::vector<double> d, e;
+  switch (prec) {
+    case P_S: band_chase<float>(ab, ldab, n, b, d, e); break;
+    case P_D: band_chase<double>(ab, ldab, n, b, d, e); break;
+    case P_C: band_chase<std::complex<float>>(ab, ldab, n, b, d, e); break;
+    default: band_chase<std::complex<double>>(ab, ldab, n, b, d, e); break;
+  }
+  if (e_out) {
+    w = d;
+    *e_out = e;
+    return true;
+  }
+  w = d;
+  return tridiag_eigenvalues(w, e);
+}
+
+}  // namespace
+
+NatProgram* nat_herbt(dplasma_context_t* ctx, int prec, int uplo, int ib, dplasma_desc_t* dA, dplasma_desc_t* dT) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *T = dT ? dT->nat : nullptr;
+  if (!same_ctx(c, {A, T}, prec)) return fail(nullptr, "herbt: descriptors of another context or precision");
+  if (A->m != A->n || A->mb != A->nb || A->nb > 256 || T->mb != ib || T->nb != A->nb || T->mt < A->mt || T->nt < A->nt)
+    return fail(nullptr, "herbt: square A of square tiles <= 256, T of mt x nt tiles of ib x nb");
+  if (uplo != LOWER && uplo != UPPER) return fail(nullptr, "herbt: illegal uplo");
+  NatProgram* P = new_program(c, "herbt", true);
+  int last = -1;
+  if (!P->info || !add_herbt(*P, uplo, *A, *T, last)) return fail(P, "herbt: device allocation failed");
+  return P;
+}
+
+// band -> tridiagonal in place on a band descriptor ((nb+1) x N, LAPACK lower band storage): on exit row 0 holds d,
+// row 1 holds e, the rest is zero (models/eigen.py hetrd_b2s); one host task
+NatProgram* nat_hbrdt(dplasma_context_t* ctx, int prec, dplasma_desc_t* dA) {
+  NatCtx* c = ctx->nat;
+  NatDesc* B = dA ? dA->nat : nullptr;
+  if (!same_ctx(c, {B}, prec)) return fail(nullptr, "hbrdt: a descriptor of this context and precision");
+  if (B->m < 2) return fail(nullptr, "hbrdt: a band of at least 2 rows");
+  NatProgram* P = new_program(c, "hbrdt", false);
+  NatDesc* Bp = B;
+  P->task(1, [=](hipStream_t s) {
+    if (hipStreamSynchronize(s) != hipSuccess) return -1;
+    const int es = Bp->es, ldab = Bp->m, n = Bp->n;
+    std::vector<unsigned char> ab((size_t)ldab * std::max(n, 1) * es);
+    if (hipMemcpy2D(ab.data(), (size_t)ldab * es, Bp->data, (size_t)Bp->lld * es, (size_t)ldab * es, n,
+                    hipMemcpyDeviceToHost) != hipSuccess)
+      return -1;
+    std::vector<double> d, e;
+    chase_and_solve(prec, ab, ldab, n, ldab - 1, d, &e);
+    std::vector<unsigned char> out(ab.size(), 0);
+    auto put = [&](int r, int j, double v) {
+      unsigned char* p = out.data() + ((size_t)j * ldab + r) * es;
+      if (prec == P_S || prec == P_C) {
+        const float f = (float)v;
+        std::memcpy(p, &f, sizeof f);
+      } else {
+        std::memcpy(p, &v, sizeof v);
+      }
+    };
+    for (int j = 0; j < n; ++j) put(0, j, d[j]);
+    for (int j = 0; j + 1 < n; ++j) put(1, j, e[j]);
+    return hipMemcpy2D(Bp->data, (size_t)Bp->lld * es, out.data(), (size_t)ldab * es, (size_t)ldab * es, n,
+                       hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+  }, {});
+  return P;
+}
+
+// eigenvalues of Hermitian A (NoVec, as the reference): herbt, then one host task -- the band to the host, the chase,
+// QL; W (N x 1, A's precision or its real counterpart) receives them in ascending order
+NatProgram* nat_heev(dplasma_context_t* ctx, int prec, int jobz, int uplo, dplasma_desc_t* dA, dplasma_desc_t* dW,
+                     dplasma_desc_t*) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *W = dW ? dW->nat : nullptr;
+  if (jobz != 301 /* NoVec */) return fail(nullptr, "heev: only jobz = NoVec (as the reference)");
+  if (!same_ctx(c, {A}, prec) || !W || W->ctx != c) return fail(nullptr, "heev: descriptors of this context");
+  const int rprec = prec == P_C ? P_S : (prec == P_Z ? P_D : prec);
+  if (W->prec != prec && W->prec != rprec) return fail(nullptr, "heev: W of A's precision or its real counterpart");
+  if (W->m < A->n || A->m != A->n || A->mb != A->nb || A->nb > 256) return fail(nullptr, "heev: square A of square tiles <= 256, W with N rows");
+  const int ib = std::min(32, A->nb);
+  auto T = std::make_shared<NatDesc>();   // block-reflector scratch (mt x nt tiles of ib x nb)
+  T->ctx = c, T->prec = prec, T->es = A->es, T->mb = ib, T->nb = A->nb, T->m = A->mt * ib, T->n = A->n;
+  T->mt = A->mt, T->nt = A->nt, T->lm = T->m, T->ln = T->n, T->lld = std::max(16, (T->m + 15) / 16 * 16);
+  void* tp = nullptr;
+  if (hipMalloc(&tp, (size_t)T->lld * std::max(1, T->n) * A->es) != hipSuccess) return fail(nullptr, "heev: device allocation failed");
+  T->data = (char*)tp;
+  T->owned = true;
+  NatProgram* P = new_program(c, "heev", true);
+  P->wdesc.push_back(T);
+  int last = -1;
+  if (!P->info || !add_herbt(*P, uplo, *A, *T, last)) return fail(P, "heev: device allocation failed");
+  NatDesc* Ap = A;
+  NatDesc* Wp = W;
+  P->task(1, [=](hipStream_t s) {
+    if (hipStreamSynchronize(s) != hipSuccess) return -1;
+    std::vector<unsigned char> ab;
+    if (!host_lower_band(*Ap, ab)) return -1;
+    std::vector<double> w;
+    if (!chase_and_solve(prec, ab, Ap->nb + 1, Ap->n, Ap->nb, w)) return -3;   // QL did not converge
+    const int wes = Wp->es;
+    std::vector<unsigned char> wv((size_t)Ap->n * wes, 0);
+    for (int i = 0; i < Ap->n; ++i) {
+      unsigned char* p = wv.data() + (size_t)i * wes;
+      if (Wp->prec == P_S || Wp->prec == P_C) {
+        const float f = (float)w[i];
+        std::memcpy(p, &f, sizeof f);
+      } else {
+        std::memcpy(p, &w[i], sizeof(double));
+      }
+    }
+    return hipMemcpy(Wp->data, wv.data(), wv.size(), hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+  }, {last});
   return P;
 }
 

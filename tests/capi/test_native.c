@@ -1187,6 +1187,116 @@ static void test_dgetrf_qrf_criteria(dplasma_context_t *ctx) {
   dplasma_desc_destroy(IP);
 }
 
+/* eigenvalues natively: heev (herbt two-sided panel reduction to band + host bulge chase + QL) on the 1-D Laplacian
+ * (known spectrum 2 - 2 cos(k pi / (n + 1))), on random symmetric / Hermitian matrices (trace and Frobenius invariants,
+ * Lower and Upper agree), and hbrdt on a band descriptor (d, e similar to the band: the same invariants) */
+static void test_heev(dplasma_context_t *ctx) {
+  const int n = 600, nb = 64;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, n, n), *W = dmat(ctx, dplasmaRealDouble, nb, n, 1);
+  double *a = malloc(sizeof(double) * n * n), *w = malloc(sizeof(double) * n), *w2 = malloc(sizeof(double) * n);
+  /* 1-D Laplacian */
+  memset(a, 0, sizeof(double) * n * n);
+  for (int i = 0; i < n; ++i) {
+    a[i + (size_t)i * n] = 2.0;
+    if (i + 1 < n) a[i + 1 + (size_t)i * n] = a[i + (size_t)(i + 1) * n] = -1.0;
+  }
+  dplasma_desc_set_lapack(A, a, n);
+  CHECK(dplasma_dheev(ctx, dplasmaNoVec, dplasmaLower, A, W, NULL) == 0, "dheev: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(W, w, n);
+  double el = 0;
+  for (int k = 0; k < n; ++k) el = fmax(el, fabs(w[k] - (2.0 - 2.0 * cos((k + 1) * M_PI / (n + 1)))));
+  /* random symmetric: trace / Frobenius invariants, Lower vs Upper */
+  unsigned sd = 919;
+  rnd_fill(a, (size_t)n * n, &sd);
+  double tr = 0, fr = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < j; ++i) a[i + (size_t)j * n] = a[j + (size_t)i * n];
+  for (int j = 0; j < n; ++j) {
+    tr += a[j + (size_t)j * n];
+    for (int i = 0; i < n; ++i) fr += a[i + (size_t)j * n] * a[i + (size_t)j * n];
+  }
+  dplasma_desc_set_lapack(A, a, n);
+  CHECK(dplasma_dheev(ctx, dplasmaNoVec, dplasmaLower, A, W, NULL) == 0, "dheev L: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(W, w, n);
+  dplasma_desc_set_lapack(A, a, n);
+  CHECK(dplasma_dheev(ctx, dplasmaNoVec, dplasmaUpper, A, W, NULL) == 0, "dheev U: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(W, w2, n);
+  double s1 = 0, s2 = 0, lu = 0, wmax = 0;
+  int sorted = 1;
+  for (int k = 0; k < n; ++k) {
+    s1 += w[k], s2 += w[k] * w[k];
+    lu = fmax(lu, fabs(w[k] - w2[k]));
+    wmax = fmax(wmax, fabs(w[k]));
+    if (k && w[k] < w[k - 1]) sorted = 0;
+  }
+  printf("dheev n=%d nb=%d: Laplacian max err %.2e  random: |sum l - tr| %.2e  |sum l^2 - ||A||_F^2|/||A||_F^2 %.2e  L vs U %.2e\n",
+         n, nb, el, fabs(s1 - tr) / (n * wmax), fabs(s2 - fr) / fr, lu / wmax);
+  CHECK(el < 1e-12 && fabs(s1 - tr) / (n * wmax) < 1e-13 && fabs(s2 - fr) / fr < 1e-12 && lu / wmax < 1e-12 && sorted,
+        "dheev residuals");
+  /* complex Hermitian */
+  {
+    const int nz = 300, nbz = 48;
+    dplasma_desc_t *Z = dmat(ctx, dplasmaComplexDouble, nbz, nz, nz), *Wz = dmat(ctx, dplasmaRealDouble, nbz, nz, 1);
+    double complex *z = malloc(sizeof(double complex) * nz * nz);
+    double *re = malloc(sizeof(double) * 2 * nz * nz), *wz = malloc(sizeof(double) * nz);
+    rnd_fill(re, (size_t)2 * nz * nz, &sd);
+    for (int j = 0; j < nz; ++j)
+      for (int i = 0; i < nz; ++i) z[i + (size_t)j * nz] = re[2 * (i + (size_t)j * nz)] + I * re[2 * (i + (size_t)j * nz) + 1];
+    double trz = 0, frz = 0;
+    for (int j = 0; j < nz; ++j) {
+      z[j + (size_t)j * nz] = creal(z[j + (size_t)j * nz]);
+      for (int i = 0; i < j; ++i) z[i + (size_t)j * nz] = conj(z[j + (size_t)i * nz]);
+    }
+    for (int j = 0; j < nz; ++j) {
+      trz += creal(z[j + (size_t)j * nz]);
+      for (int i = 0; i < nz; ++i) frz += creal(z[i + (size_t)j * nz] * conj(z[i + (size_t)j * nz]));
+    }
+    dplasma_desc_set_lapack(Z, z, nz);
+    CHECK(dplasma_zheev(ctx, dplasmaNoVec, dplasmaLower, Z, Wz, NULL) == 0, "zheev: %s", dplasma_last_error());
+    dplasma_desc_get_lapack(Wz, wz, nz);
+    double t1 = 0, t2 = 0, wm = 0;
+    for (int k = 0; k < nz; ++k) t1 += wz[k], t2 += wz[k] * wz[k], wm = fmax(wm, fabs(wz[k]));
+    printf("zheev n=%d: |sum l - tr| %.2e  |sum l^2 - ||A||_F^2|/||A||_F^2 %.2e\n", nz, fabs(t1 - trz) / (nz * wm),
+           fabs(t2 - frz) / frz);
+    CHECK(fabs(t1 - trz) / (nz * wm) < 1e-13 && fabs(t2 - frz) / frz < 1e-12, "zheev invariants");
+    free(z), free(re), free(wz);
+    dplasma_desc_destroy(Z), dplasma_desc_destroy(Wz);
+  }
+  /* hbrdt on a band descriptor ((b+1) x n, lower band storage of a random symmetric band matrix) */
+  {
+    const int b = 16, nn = 400;
+    dplasma_desc_t *Bd = dmat(ctx, dplasmaRealDouble, 64, b + 1, nn);
+    double *ab = malloc(sizeof(double) * (b + 1) * nn), *out = malloc(sizeof(double) * (b + 1) * nn);
+    rnd_fill(ab, (size_t)(b + 1) * nn, &sd);
+    for (int j = 0; j < nn; ++j)
+      for (int r = 0; r <= b; ++r)
+        if (j + r >= nn) ab[r + (size_t)j * (b + 1)] = 0;
+    double tb = 0, fb = 0;
+    for (int j = 0; j < nn; ++j) {
+      tb += ab[(size_t)j * (b + 1)];
+      fb += ab[(size_t)j * (b + 1)] * ab[(size_t)j * (b + 1)];
+      for (int r = 1; r <= b; ++r) fb += 2 * ab[r + (size_t)j * (b + 1)] * ab[r + (size_t)j * (b + 1)];
+    }
+    dplasma_desc_set_lapack(Bd, ab, b + 1);
+    CHECK(dplasma_dhbrdt(ctx, Bd) == 0, "dhbrdt: %s", dplasma_last_error());
+    dplasma_desc_get_lapack(Bd, out, b + 1);
+    double td = 0, fd = 0, rest = 0;
+    for (int j = 0; j < nn; ++j) {
+      td += out[(size_t)j * (b + 1)];
+      fd += out[(size_t)j * (b + 1)] * out[(size_t)j * (b + 1)];
+      if (j + 1 < nn) fd += 2 * out[1 + (size_t)j * (b + 1)] * out[1 + (size_t)j * (b + 1)];
+      for (int r = 2; r <= b; ++r) rest = fmax(rest, fabs(out[r + (size_t)j * (b + 1)]));
+    }
+    printf("dhbrdt b=%d n=%d: |trace d - trace| %.2e  |fro(d,e)^2 - fro^2|/fro^2 %.2e  rows >= 2 max %.1e\n", b, nn,
+           fabs(td - tb), fabs(fd - fb) / fb, rest);
+    CHECK(fabs(td - tb) < 1e-10 && fabs(fd - fb) / fb < 1e-12 && rest == 0, "hbrdt invariants");
+    free(ab), free(out);
+    dplasma_desc_destroy(Bd);
+  }
+  free(a), free(w), free(w2);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(W);
+}
+
 /* trtri / lauum / potri / poinv natively: A := inv(A) checked as ||A0 inv(A) - I||; lauum against host
    L^T L; her2k / syr2k against host rank-2k; the alias entry points (ptgpanel on 1x1, potrf_rec). */
 static void test_inverse_family(dplasma_context_t *ctx) {
@@ -1734,6 +1844,7 @@ int main(int argc, char **argv) {
   test_dgelqf_param(ctx);
   test_dgetrf_qrf(ctx);
   test_dgetrf_qrf_criteria(ctx);
+  test_heev(ctx);
   test_inverse_family(ctx);
   test_rank_2k(ctx);
   test_aliases(ctx);
@@ -1748,7 +1859,7 @@ int main(int argc, char **argv) {
   test_butterfly(ctx);
   /* an operation without a native implementation fails cleanly */
   dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
-  CHECK(dplasma_dhbrdt(ctx, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");
+  CHECK(dplasma_dgebrd_ge2gb(ctx, 32, A, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");
   dplasma_desc_destroy(A);
   if (argc > 1 && atoi(argv[1]) > 0) bench(ctx, atoi(argv[1]));
   CHECK(dplasma_python_active() == 0, "the interpreter was started");

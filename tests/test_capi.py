@@ -384,5 +384,5 @@ def test_capi_ext_native_routing():
         for op in native:
             ln = lines[f"dplasma_{p}{op}"]
             assert "if (dpl_native(ctx)) return nat_" in ln and "nat_unsupported" not in ln, (p, op)
-        for op in ("heev", "herbt", "hbrdt"):
+        for op in ("gebrd_ge2gb", "gebrd_ge2gbx"):
             assert f'nat_unsupported("{p}{op}")' in lines[f"dplasma_{p}{op}"], (p, op)

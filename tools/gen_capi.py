@@ -197,6 +197,10 @@ NATIVE_EXT = {
     # hybrid LU-QR (native.cpp nat_getrf_qrf: predicated LU / QR branches after a host decision per step)
     "getrf_qrf": lambda pc: f"nat_getrf_qrf(ctx, {pc}, qrtree, A, IPIV, TS, TT, criteria, alpha, lu_tab, INFO)",
     "trsmpl_qrf": lambda pc: f"nat_trsmpl_qrf(ctx, {pc}, qrtree, A, IPIV, B, TS, TT, lu_tab)",
+    # eigenvalues (native.cpp: two-sided panel reduction to band, host bulge chase + QL)
+    "herbt": lambda pc: f"nat_herbt(ctx, {pc}, uplo, ib, A, T)",
+    "hbrdt": lambda pc: f"nat_hbrdt(ctx, {pc}, A)",
+    "heev": lambda pc: f"nat_heev(ctx, {pc}, jobz, uplo, A, W, Z)",
 }
 # EXT entry points the engine answers directly (a value, no program)
 NATIVE_EXT_DIRECT = {
