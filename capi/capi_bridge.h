@@ -200,6 +200,10 @@ NatProgram* nat_herbt(dplasma_context_t* ctx, int prec, int uplo, int ib, dplasm
 NatProgram* nat_hbrdt(dplasma_context_t* ctx, int prec, dplasma_desc_t* A);
 NatProgram* nat_heev(dplasma_context_t* ctx, int prec, int jobz, int uplo, dplasma_desc_t* A, dplasma_desc_t* W,
                      dplasma_desc_t* Z);
+NatProgram* nat_gebrd_ge2gb(dplasma_context_t* ctx, int prec, int ib, dplasma_desc_t* A, dplasma_desc_t* Band);
+NatProgram* nat_gebrd_ge2gbx(dplasma_context_t* ctx, int prec, int ib, dplasma_qrtree_t* qt0, dplasma_qrtree_t* qt,
+                             dplasma_qrtree_t* lqt, dplasma_desc_t* A, dplasma_desc_t* TS0, dplasma_desc_t* TT0,
+                             dplasma_desc_t* TS, dplasma_desc_t* TT, dplasma_desc_t* Band);
 NatProgram* nat_trdsm(dplasma_context_t* ctx, int prec, dplasma_desc_t* A, dplasma_desc_t* B);
 NatProgram* nat_trmdm(dplasma_context_t* ctx, int prec, dplasma_desc_t* A);
 int nat_latms(dplasma_context_t* ctx, int prec, int mtxtype, double cond, dplasma_desc_t* A, unsigned long long seed);

@@ -4440,6 +4440,197 @@ NatProgram* nat_heev(dplasma_context_t* ctx, int prec, int jobz, int uplo, dplas
   return P;
 }
 
+// ----------------------------------------------------------------------------- general -> band bidiagonal (ge2gb)
+// dplasma_zgebrd_ge2gb / ge2gbx (reference src/zgebrd_ge2gb.jdf; models/eigen.py gebrd_ge2gbx_New) on one process,
+// flat trees: per k a QR step (tile column k, rows k.., one in-place Householder panel, Q^H applied to columns
+// k+1..) and, for k < nt - 1, an LQ step on tile row k, columns k+1.. (its conjugate transpose factored as one panel
+// in a scratch buffer and written back -- L in A(k, k+1), the conj(V) rows beside it, LAPACK's LQ layout -- then Q
+// applied from the right to rows k+1..).  Band: (nb + 1) x N upper band storage AB(nb + i - j, j).
+namespace {
+
+struct Ge2gbBufs {
+  DevPtr V, Tk, W, W2, ws, Bt;
+  int ldv = 0, ldb = 0;
+};
+
+// C(i0.., j0..) := C(i0.., j0..) op(H), H = I - V T V^H, V rows <-> C columns from j0 (nb each)
+int add_right_from(NatProgram& P, NatDesc& A, int i0, int j0, int kf, char* V, int ldv, char* Tk, bool qt, char* W, char* W2,
+                   int ldw, int prev) {
+  if (i0 >= A.mt || j0 >= A.nt || kf <= 0) return prev;
+  const int prec = A.prec, mb = A.mb, nb = A.nb, ld = A.lld;
+  auto g1 = std::make_shared<Gemm>(), g2 = std::make_shared<Gemm>(), g3 = std::make_shared<Gemm>();
+  for (int i = i0; i < A.mt; ++i) {
+    const long long wo = (long long)(i - i0) * mb;
+    std::vector<KPair> kp;
+    for (int j = j0; j < A.nt; ++j) kp.push_back(KPair{A.off(i, j), (long long)(j - j0) * nb, A.cols(j), 0});
+    g1->add(wo, A.rows(i), kf, kp, 0);
+    g2->add(wo, A.rows(i), kf, {KPair{wo, 0, kf, 0}}, 0);
+    for (int j = j0; j < A.nt; ++j) g3->add(A.off(i, j), A.rows(i), A.cols(j), {KPair{wo, (long long)(j - j0) * nb, kf, 0}}, 0);
+  }
+  if (!g1->upload(P) || !g2->upload(P) || !g3->upload(P)) return -2;
+  char* a = A.data;
+  const Scalar one(prec, 1.0), zero(prec, 0.0), m_one(prec, -1.0);
+  return P.task(1, [=](hipStream_t s) {
+    int rc = g1->launch(prec, NOTRANS, NOTRANS, one, a, ld, V, ldv, zero, W, ldw, s);
+    if (rc == 0) rc = g2->launch(prec, NOTRANS, qt ? CONJTRANS : NOTRANS, one, W, ldw, Tk, nb, zero, W2, ldw, s);
+    if (rc == 0) rc = g3->launch(prec, NOTRANS, CONJTRANS, m_one, W2, ldw, V, ldv, one, a, ld, s);
+    return rc;
+  }, {prev});
+}
+
+// IB x IB diagonal blocks of the nb x nb T (ld nb) into tile (ti, tj) of Td
+int add_T_blocks(NatProgram& P, const NatDesc& Td, int ti, int tj, int kf, char* Tk, int nb, int prev) {
+  if (ti >= Td.mt || tj >= Td.nt) return prev;
+  const int ib = Td.mb, prec = Td.prec;
+  std::vector<TileItem> it;
+  for (int b0 = 0; b0 < kf; b0 += ib) {
+    const int bs = std::min(ib, kf - b0);
+    it.push_back(TileItem{b0 + (long long)b0 * nb, Td.off(ti, tj) + (long long)b0 * Td.lld, bs, bs, 0, 0});
+  }
+  auto d = dev_upload(it);
+  if (!d) return -2;
+  P.keep.push_back(d);
+  const int n = (int)it.size(), ldT = Td.lld;
+  char* td = Td.data;
+  const Scalar one(prec, 1.0), zero(prec, 0.0);
+  return P.task(1, [=](hipStream_t s) {
+    return dpl_geadd(prec, 0, NOTRANS, n, d->p, ib, ib, one.ptr(), Tk, nb, zero.ptr(), td, ldT, 1, s);
+  }, {prev});
+}
+
+bool add_ge2gb(NatProgram& P, NatDesc& A, const NatDesc* TSq, const NatDesc* TSl, NatDesc* Band, int& last) {
+  const int prec = A.prec, nb = A.nb, mb = A.mb, es = A.es, ld = A.lld;
+  Ge2gbBufs b;
+  b.ldv = std::max(16, (std::max(A.m, A.n) + 15) / 16 * 16);
+  b.ldb = std::max(16, (A.n + 15) / 16 * 16);
+  b.V = dev_alloc((size_t)b.ldv * nb * es, true);
+  b.Tk = dev_alloc((size_t)nb * nb * es, true);
+  const size_t wl = (size_t)std::max(b.ldv, nb * std::max(1, A.nt)) * nb;
+  b.W = dev_alloc(wl * es, false);
+  b.W2 = dev_alloc(wl * es, false);
+  b.ws = dev_alloc((size_t)dpl_qr_panel_ws_bytes(prec, nb, nb) + 256, true);
+  b.Bt = dev_alloc((size_t)b.ldb * nb * es, true);
+  for (const DevPtr& d : {b.V, b.Tk, b.W, b.W2, b.ws, b.Bt}) {
+    if (!d) return false;
+    P.keep.push_back(d);
+  }
+  char *a = A.data, *v = (char*)b.V->p, *tk = (char*)b.Tk->p, *w = (char*)b.W->p, *w2 = (char*)b.W2->p;
+  char *ws = (char*)b.ws->p, *bt = (char*)b.Bt->p;
+  const int ldv = b.ldv, ldb = b.ldb;
+  int* info = (int*)P.info->p;
+  const Scalar one(prec, 1.0), zero(prec, 0.0);
+  int prev = last;
+  for (int k = 0; k < A.nt; ++k) {
+    // ---- QR step: column k, rows k..
+    const int M = A.m - k * mb, kb = A.cols(k), kf = std::min(M, kb);
+    char* pk = a + A.off(k, k) * es;
+    prev = P.task(1, [=](hipStream_t s) { return dpl_qr_panel(prec, pk, ld, 0, 0, M, kb, kf, v, ldv, tk, nb, ws, info, s); },
+                  {prev});
+    if (TSq) prev = add_T_blocks(P, *TSq, k, k, kf, tk, nb, prev);
+    if (prev < -1) return false;
+    std::vector<int> cols;
+    for (int j = k + 1; j < A.nt; ++j) cols.push_back(j);
+    int out = prev;
+    if (!add_left_apply(P, prec, A, k, M, kf, v, ldv, tk, nb, true, w, w2, cols, 1, prev, out)) return false;
+    prev = out;
+    if (k + 1 >= A.nt) break;
+    // ---- LQ step: row k, columns k+1.. (its conjugate transpose as one panel)
+    const int Nl = A.n - (k + 1) * nb, rk = A.rows(k), kfl = std::min(Nl, rk);
+    auto to = std::make_shared<MapBatch>(), fro = std::make_shared<MapBatch>();
+    for (int j = k + 1; j < A.nt; ++j) {
+      const long long bo = (long long)(j - k - 1) * nb;
+      to->it.push_back(TileItem{A.off(k, j), bo, A.cols(j), rk, 0, 0});     // Bt(j-block) := A(k, j)^H
+      fro->it.push_back(TileItem{bo, A.off(k, j), rk, A.cols(j), 0, 0});    // A(k, j) := Bt(j-block)^H
+    }
+    to->mm = nb, to->nn = rk;
+    fro->mm = rk, fro->nn = nb;
+    if (!to->upload(P) || !fro->upload(P)) return false;
+    prev = P.task(1, [=](hipStream_t s) {
+      int rc = dpl_geadd(prec, 0, CONJTRANS, to->n(), to->items(), to->mm, to->nn, one.ptr(), a, ld, zero.ptr(), bt, ldb, 1, s);
+      if (rc == 0) rc = dpl_qr_panel(prec, bt, ldb, 0, 0, Nl, rk, kfl, v, ldv, tk, nb, ws, info, s);
+      if (rc == 0)
+        rc = dpl_geadd(prec, 0, CONJTRANS, fro->n(), fro->items(), fro->mm, fro->nn, one.ptr(), bt, ldb, zero.ptr(), a, ld, 1, s);
+      return rc;
+    }, {prev});
+    if (TSl) prev = add_T_blocks(P, *TSl, k, k + 1, kfl, tk, nb, prev);
+    if (prev < -1) return false;
+    // rows k+1.. of columns k+1..: C := C Q_r (A(k, k+1:) = R^H Q_r^H)
+    prev = add_right_from(P, A, k + 1, k + 1, kfl, v, ldv, tk, false, w, w2, ldv, prev);
+    if (prev < -1) return false;
+  }
+  if (Band) {   // upper band storage: Band(nb + i - j, j) = A(i, j), max(0, j - nb) <= i <= j
+    const int N = std::min(A.m, A.n), ldB = Band->lld;
+    char* bd = Band->data;
+    prev = P.task(1, [=](hipStream_t s) {
+      if (hipMemsetAsync(bd, 0, (size_t)ldB * std::max(1, Band->n) * es, s) != hipSuccess) return -1;
+      for (int j = 0; j < std::min(N, nb); ++j)
+        if (hipMemcpyAsync(bd + ((size_t)j * ldB + (nb - j)) * es, a + (size_t)j * ld * es, (size_t)(j + 1) * es,
+                           hipMemcpyDeviceToDevice, s) != hipSuccess)
+          return -1;
+      if (N > nb &&
+          hipMemcpy2DAsync(bd + (size_t)nb * ldB * es, (size_t)ldB * es, a + ((size_t)nb * ld) * es, (size_t)(ld + 1) * es,
+                           (size_t)(nb + 1) * es, N - nb, hipMemcpyDeviceToDevice, s) != hipSuccess)
+        return -1;
+      return 0;
+    }, {prev});
+  }
+  last = prev;
+  return true;
+}
+
+bool tree_is_flat(const nq::Tree* t) {
+  if (!t) return true;
+  for (int k = 0; k < std::min(t->mt, t->nt); ++k) {
+    std::vector<int> h;
+    std::vector<nq::Kill> kl;
+    t->plan(k, h, kl);
+    if (h.size() != 1 || h[0] != k) return false;
+    for (const nq::Kill& x : kl)
+      if (x.piv != k || x.type != nq::KILLED_BY_TS) return false;
+  }
+  return true;
+}
+
+bool band_ok(const NatDesc* A, const NatDesc* Band) {
+  return !Band || (Band->m >= A->nb + 1 && Band->n >= std::min(A->m, A->n) && Band->prec == A->prec);
+}
+
+}  // namespace
+
+NatProgram* nat_gebrd_ge2gb(dplasma_context_t* ctx, int prec, int ib, dplasma_desc_t* dA, dplasma_desc_t* dBand) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *Band = dBand ? dBand->nat : nullptr;
+  if (!same_ctx(c, {A}, prec) || (Band && Band->ctx != c)) return fail(nullptr, "gebrd_ge2gb: descriptors of this context");
+  if (A->m < A->n || A->mb != A->nb || A->nb > 256 || ib <= 0 || !band_ok(A, Band))
+    return fail(nullptr, "gebrd_ge2gb: M >= N, square tiles <= 256, Band of (nb + 1) x N");
+  NatProgram* P = new_program(c, "gebrd_ge2gb", true);
+  int last = -1;
+  if (!P->info || !add_ge2gb(*P, *A, nullptr, nullptr, Band, last)) return fail(P, "gebrd_ge2gb: device allocation failed");
+  return P;
+}
+
+// ge2gbx: the trees must be flat (every panel one TS domain: the engine above); TS0 receives the QR steps' T blocks
+// (tile (k, k)), TS the LQ steps' (tile (k, k + 1)); TT0 / TT stay untouched (no TT kills in a flat tree)
+NatProgram* nat_gebrd_ge2gbx(dplasma_context_t* ctx, int prec, int ib, dplasma_qrtree_t* qt0, dplasma_qrtree_t* qt,
+                             dplasma_qrtree_t* lqt, dplasma_desc_t* dA, dplasma_desc_t* dTS0, dplasma_desc_t*,
+                             dplasma_desc_t* dTS, dplasma_desc_t*, dplasma_desc_t* dBand) {
+  NatCtx* c = ctx->nat;
+  NatDesc *A = dA ? dA->nat : nullptr, *Band = dBand ? dBand->nat : nullptr;
+  NatDesc *TS0 = dTS0 ? dTS0->nat : nullptr, *TS = dTS ? dTS->nat : nullptr;
+  if (!same_ctx(c, {A}, prec) || (Band && Band->ctx != c)) return fail(nullptr, "gebrd_ge2gbx: descriptors of this context");
+  const nq::Tree* tq = nat_qrtree(qt ? qt : qt0);
+  const nq::Tree* tl = nat_qrtree(lqt);
+  if ((qt || qt0) && !tq) return fail(nullptr, "gebrd_ge2gbx: native trees (dplasma_hqr_init on a native descriptor)");
+  if (!tree_is_flat(tq) || !tree_is_flat(tl))
+    return fail(nullptr, "gebrd_ge2gbx: the native engine reduces with flat trees (one TS domain per panel)");
+  if (A->m < A->n || A->mb != A->nb || A->nb > 256 || ib <= 0 || !band_ok(A, Band))
+    return fail(nullptr, "gebrd_ge2gbx: M >= N, square tiles <= 256, Band of (nb + 1) x N");
+  NatProgram* P = new_program(c, "gebrd_ge2gbx", true);
+  int last = -1;
+  if (!P->info || !add_ge2gb(*P, *A, TS0, TS, Band, last)) return fail(P, "gebrd_ge2gbx: device allocation failed");
+  return P;
+}
+
 // tau_j = T_k(j, j) of a native geqrf's T (the compact-WY diagonal: LAPACK's tau), j < k, to host memory
 int nat_qr_tau(dplasma_desc_t* dT, void* tau, int k) {
   NatDesc* T = dT ? dT->nat : nullptr;

@@ -1297,6 +1297,61 @@ static void test_heev(dplasma_context_t *ctx) {
   dplasma_desc_destroy(A), dplasma_desc_destroy(W);
 }
 
+/* general -> upper band bidiagonal natively (gebrd_ge2gb; ge2gbx with flat native trees gives the same band): the
+ * band keeps the Frobenius norm and holds nothing outside its nb + 1 diagonals; A and the band are dumped under
+ * DPLASMA_TEST_DUMP for tests/test_capi.py to compare singular values with numpy */
+static void test_ge2gb(dplasma_context_t *ctx) {
+  const int m = 600, n = 400, nb = 64, ib = 16;
+  const int mt = (m + nb - 1) / nb, nt = (n + nb - 1) / nb;
+  dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, nb, m, n), *Bd = dmat(ctx, dplasmaRealDouble, nb, nb + 1, n);
+  dplasma_desc_t *B2 = dmat(ctx, dplasmaRealDouble, nb, nb + 1, n);
+  dplasma_desc_t *TS0 = dplasma_desc_block_cyclic(ctx, dplasmaRealDouble, ib, nb, mt * ib, nt * nb, 1, 1, dplasmaUpperLower);
+  dplasma_desc_t *TS = dplasma_desc_block_cyclic(ctx, dplasmaRealDouble, ib, nb, mt * ib, nt * nb, 1, 1, dplasmaUpperLower);
+  CHECK(A && Bd && B2 && TS0 && TS, "ge2gb descriptors: %s", dplasma_last_error());
+  double *a = malloc(sizeof(double) * m * n), *band = malloc(sizeof(double) * (nb + 1) * n);
+  double *band2 = malloc(sizeof(double) * (nb + 1) * n);
+  unsigned sd = 4242;
+  rnd_fill(a, (size_t)m * n, &sd);
+  double fa = 0;
+  for (size_t e = 0; e < (size_t)m * n; ++e) fa += a[e] * a[e];
+  dplasma_desc_set_lapack(A, a, m);
+  CHECK(dplasma_dgebrd_ge2gb(ctx, ib, A, Bd) == 0, "dgebrd_ge2gb: %s", dplasma_last_error());
+  dplasma_desc_get_lapack(Bd, band, nb + 1);
+  dplasma_qrtree_t tq, tl;
+  memset(&tq, 0, sizeof tq), memset(&tl, 0, sizeof tl);
+  CHECK(dplasma_hqr_init(&tq, dplasmaNoTrans, A, DPLASMA_FLAT_TREE, DPLASMA_FLAT_TREE, mt, 1, 0, 0) == 0 &&
+        dplasma_hqr_init(&tl, dplasmaTrans, A, DPLASMA_FLAT_TREE, DPLASMA_FLAT_TREE, nt, 1, 0, 0) == 0, "flat trees: %s",
+        dplasma_last_error());
+  dplasma_desc_set_lapack(A, a, m);
+  CHECK(dplasma_dgebrd_ge2gbx(ctx, ib, NULL, &tq, &tl, A, TS0, NULL, TS, NULL, B2) == 0, "dgebrd_ge2gbx: %s",
+        dplasma_last_error());
+  dplasma_desc_get_lapack(B2, band2, nb + 1);
+  double fb = 0, dx = 0;
+  for (int j = 0; j < n; ++j)
+    for (int r = 0; r <= nb; ++r) {
+      const double x = band[r + (size_t)j * (nb + 1)];
+      fb += x * x;
+      dx = fmax(dx, fabs(x - band2[r + (size_t)j * (nb + 1)]));
+    }
+  const char *dump = getenv("DPLASMA_TEST_DUMP");
+  if (dump) {
+    char path[512];
+    snprintf(path, sizeof path, "%s/ge2gb_a.bin", dump);
+    FILE *fp = fopen(path, "wb");
+    if (fp) fwrite(a, sizeof(double), (size_t)m * n, fp), fclose(fp);
+    snprintf(path, sizeof path, "%s/ge2gb_band.bin", dump);
+    fp = fopen(path, "wb");
+    if (fp) fwrite(band, sizeof(double), (size_t)(nb + 1) * n, fp), fclose(fp);
+  }
+  printf("dgebrd_ge2gb %dx%d nb=%d: | ||band||_F^2 - ||A||_F^2 | / ||A||_F^2 %.2e  ge2gbx (flat trees) vs ge2gb %.1e\n", m, n,
+         nb, fabs(fb - fa) / fa, dx);
+  CHECK(fabs(fb - fa) / fa < 1e-12 && dx == 0, "ge2gb band");
+  dplasma_hqr_finalize(&tq), dplasma_hqr_finalize(&tl);
+  free(a), free(band), free(band2);
+  dplasma_desc_destroy(A), dplasma_desc_destroy(Bd), dplasma_desc_destroy(B2), dplasma_desc_destroy(TS0);
+  dplasma_desc_destroy(TS);
+}
+
 /* trtri / lauum / potri / poinv natively: A := inv(A) checked as ||A0 inv(A) - I||; lauum against host
    L^T L; her2k / syr2k against host rank-2k; the alias entry points (ptgpanel on 1x1, potrf_rec). */
 static void test_inverse_family(dplasma_context_t *ctx) {
@@ -1845,6 +1900,7 @@ int main(int argc, char **argv) {
   test_dgetrf_qrf(ctx);
   test_dgetrf_qrf_criteria(ctx);
   test_heev(ctx);
+  test_ge2gb(ctx);
   test_inverse_family(ctx);
   test_rank_2k(ctx);
   test_aliases(ctx);
@@ -1857,9 +1913,10 @@ int main(int argc, char **argv) {
   test_posv_not_spd(ctx);
   test_pltmg(ctx);
   test_butterfly(ctx);
-  /* an operation without a native implementation fails cleanly */
+  /* a request outside the native engine's scope fails cleanly (heev computes eigenvalues only, as the reference) */
   dplasma_desc_t *A = dmat(ctx, dplasmaRealDouble, 64, 128, 128);
-  CHECK(dplasma_dgebrd_ge2gb(ctx, 32, A, A) == -1 && strstr(dplasma_last_error(), "native") != NULL, "unsupported op");
+  CHECK(dplasma_dheev(ctx, dplasmaVec, dplasmaLower, A, A, NULL) != 0 && strstr(dplasma_last_error(), "NoVec") != NULL,
+        "refused request: '%s'", dplasma_last_error());
   dplasma_desc_destroy(A);
   if (argc > 1 && atoi(argv[1]) > 0) bench(ctx, atoi(argv[1]));
   CHECK(dplasma_python_active() == 0, "the interpreter was started");

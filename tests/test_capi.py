@@ -230,6 +230,30 @@ def test_capi_native_luqr_matches_python(tmp_path):
 
 
 @pytest.mark.gpu
+def test_capi_native_ge2gb_singular_values(tmp_path):
+    """Native gebrd_ge2gb (capi/native.cpp): the singular values of the upper band it returns equal numpy's of the
+    input (tests/capi/test_native.c dumps both)."""
+    import numpy as np
+    env = dict(os.environ)
+    env.pop("PYTHONPATH", None)
+    env["DPLASMA_TEST_DUMP"] = str(tmp_path)
+    r = subprocess.run([_build_native(tmp_path)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    m, n, nb = 600, 400, 64
+    a = np.fromfile(str(tmp_path / "ge2gb_a.bin"), dtype=np.float64).reshape(n, m).T
+    ab = np.fromfile(str(tmp_path / "ge2gb_band.bin"), dtype=np.float64).reshape(n, nb + 1).T
+    B = np.zeros((n, n))
+    for j in range(n):
+        for i in range(max(0, j - nb), j + 1):
+            B[i, j] = ab[nb + i - j, j]
+    s_ref = np.linalg.svd(a, compute_uv=False)
+    s_band = np.linalg.svd(B, compute_uv=False)
+    err = np.abs(s_ref - s_band).max() / s_ref.max()
+    print("ge2gb singular values max rel err", err)
+    assert err < 1e-12, err
+
+
+@pytest.mark.gpu
 def test_capi_f77_native_gpu(tmp_path):
     """ScaLAPACK F77 entry points without Python (one process, 1 x 1 BLACS grid -> the native engine):
     pdpotrf_ / pdgemm_ / pdgetrf_ / pdtrsm_ / pdtrmm_ on submatrices of host local arrays
@@ -371,7 +395,7 @@ def test_native_dist_example_gpu(tmp_path):
 def test_capi_ext_native_routing():
     """Every EXT entry point the interpreter-free engine implements (tools/gen_capi.py NATIVE_EXT /
     NATIVE_EXT_DIRECT, and hebut) dispatches to capi/native.cpp on a native context in the generated wrappers,
-    in all four precisions; the others refuse a native context by name."""
+    in all four precisions (none refuses a native context any more)."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     try:
         import gen_capi
@@ -384,5 +408,5 @@ def test_capi_ext_native_routing():
         for op in native:
             ln = lines[f"dplasma_{p}{op}"]
             assert "if (dpl_native(ctx)) return nat_" in ln and "nat_unsupported" not in ln, (p, op)
-        for op in ("gebrd_ge2gb", "gebrd_ge2gbx"):
-            assert f'nat_unsupported("{p}{op}")' in lines[f"dplasma_{p}{op}"], (p, op)
+    # every EXT entry point has a native builder now
+    assert 'nat_unsupported("' not in src

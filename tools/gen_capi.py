@@ -201,6 +201,8 @@ NATIVE_EXT = {
     "herbt": lambda pc: f"nat_herbt(ctx, {pc}, uplo, ib, A, T)",
     "hbrdt": lambda pc: f"nat_hbrdt(ctx, {pc}, A)",
     "heev": lambda pc: f"nat_heev(ctx, {pc}, jobz, uplo, A, W, Z)",
+    "gebrd_ge2gb": lambda pc: f"nat_gebrd_ge2gb(ctx, {pc}, ib, A, Band)",
+    "gebrd_ge2gbx": lambda pc: f"nat_gebrd_ge2gbx(ctx, {pc}, ib, qrtre0, qrtree, lqtree, A, TS0, TT0, TS, TT, Band)",
 }
 # EXT entry points the engine answers directly (a value, no program)
 NATIVE_EXT_DIRECT = {
