@@ -534,10 +534,14 @@ __device__ __attribute__((noinline)) void run_potrf(const DtrArgs* __restrict__ 
     }
     __syncthreads();
   }
-  rb_tile_body<true>(g.A[rk] + tile_at(tab, g.nt, k, k), NBT, (int)g.ld, g.info, k * NBT, ws, g.epoch, nullptr, b,
+  // with the task trace on: the tile body's phase stamps of every block (64 per block, after the task records)
+  unsigned long long* ph = g.trace ? (unsigned long long*)(g.trace + 4LL * g.ntask) + (size_t)k * MAXB * 64 : nullptr;
+  rb_tile_body<true>(g.A[rk] + tile_at(tab, g.nt, k, k), NBT, (int)g.ld, g.info, k * NBT, ws, g.epoch, ph, b,
                      g_lds, g_lds + BLK);
   __syncthreads();
+  if (ph && threadIdx.x == 0) ph[64 * b + 52] = __builtin_amdgcn_s_memrealtime();
   w_column(g, g.W[rk], k, b, g_lds);
+  if (ph && threadIdx.x == 0) ph[64 * b + 53] = __builtin_amdgcn_s_memrealtime();
 }
 
 // system-scope stores (sc0 sc1: written through to the peer's memory), two 8-byte ones -- compiler-generated, not
@@ -944,8 +948,13 @@ __global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ ga
     __syncthreads();
     if (t == -2) break;
     if (t == -1) {
+      // idle back-off: every scan is 2 x nclass x 8 coherent loads, and ~150 idle workgroups rescanning after 1-16
+      // sleeps slowed the POTRF blocks' hand-offs in the early steps (POTRF(1..3) 814-919 us against ~380: phase
+      // stamps, dtr_trace_run.py 16k); cap = 2^(flags >> 28) sleeps (DPLASMA_DTR_NAP; 0: 16)
+      const unsigned napl = ((unsigned)g.flags >> 28) & 15u;
+      const int napmax = napl ? (1 << napl) : 16;
       for (int q = 0; q < nap; ++q) __builtin_amdgcn_s_sleep(1);
-      nap = nap < 16 ? 2 * nap : 16;
+      nap = nap < napmax ? 2 * nap : napmax;
       continue;
     }
     nap = 1;

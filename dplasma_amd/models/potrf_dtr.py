@@ -75,10 +75,16 @@ def _strides(A):
     return si, sj
 
 
+def _head_env(default: str = "") -> tuple:
+    """DPLASMA_DTR_HEAD: comma-separated widths of the first panel blocks (then DPLASMA_DTR_DEFER)."""
+    s = os.environ.get("DPLASMA_DTR_HEAD", default).strip()
+    return tuple(int(x) for x in s.split(",") if x.strip())
+
+
 class _Plan:
     """The task table of one factorisation (identical for every run of the same shape)."""
 
-    def __init__(self, nt: int, D: int, lo_order: str = None, min_tiles: int = None):
+    def __init__(self, nt: int, D: int, lo_order: str = None, min_tiles: int = None, head=None):
         # low-list order: "panel" -- (last panel block, column, ...): the bulk runs breadth-first, block by
         # block; "column" -- (column block, last panel block, column, ...): a column block's remaining old
         # updates before the next column block's, so the first panel of a block does not wait behind the
@@ -113,10 +119,18 @@ class _Plan:
         # the stream engine's POTRF_DEFER_MIN_TILES rule)
         if min_tiles is None:
             min_tiles = int(os.environ.get("DPLASMA_DTR_DEFER_MIN_TILES", "0"))
+        # head: the widths of the first blocks (then D).  A block's bulk update of the later columns waits for its
+        # last panel, so with D = 4 from the start the first ~4 panels run with only their look-ahead work beside
+        # them (dtr_trace_run.py 16k: ~1/3 of the workgroups busy over the first 15 % of the span)
+        if head is None:
+            head = _head_env()
+        head = [max(1, int(h)) for h in head]
         blocks = []
         b0 = 0
         while b0 < nt:
             d = D if nt - b0 >= min_tiles else 1
+            if len(blocks) < len(head):
+                d = head[len(blocks)]
             blocks.append((b0, min(nt, b0 + d)))
             b0 += d
         block_of = np.zeros(nt, dtype=np.int64)
@@ -306,7 +320,7 @@ class _Plan:
 
 # push scheduling classes: 0 POTRF blocks, 1 panel TRSM strips, then the updates by output column j (the step that
 # needs them), in at most UPD_BUCKETS buckets
-UPD_BUCKETS = 22
+UPD_BUCKETS = int(os.environ.get("DPLASMA_DTR_BUCKETS", "22"))
 NCLASS = 2 + UPD_BUCKETS
 
 
@@ -504,6 +518,10 @@ def flags_from_env() -> int:
     sw = int(os.environ.get("DPLASMA_DTR_STEPW", "0"))
     if sw:
         fl |= (min(15, max(1, sw)) << 24)
+    # DPLASMA_DTR_NAP=n: the push scheduler's idle back-off cap, n = 2^e sleeps (default 16)
+    nap = int(os.environ.get("DPLASMA_DTR_NAP", "0"))
+    if nap > 0:
+        fl |= (min(7, max(1, nap.bit_length() - 1)) << 28)   # (a signed 32-bit field: e <= 7)
     hold = os.environ.get("DPLASMA_DTR_HOLD")
     if hold:
         hp, ho = (int(x) for x in hold.split(","))
@@ -550,10 +568,11 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     D = max(1, int(os.environ.get("DPLASMA_DTR_DEFER", "4")))
     lo_order = os.environ.get("DPLASMA_DTR_LO_ORDER", "column")
     min_tiles = int(os.environ.get("DPLASMA_DTR_DEFER_MIN_TILES", "0"))
-    key = (nt, D, lo_order, min_tiles)
+    head = _head_env()
+    key = (nt, D, lo_order, min_tiles, head)
     plan = _PLANS.get(key)
     if plan is None:
-        plan = _PLANS[key] = _Plan(nt, D, lo_order, min_tiles)
+        plan = _PLANS[key] = _Plan(nt, D, lo_order, min_tiles, head)
     dev = A.device
     tp = Taskpool("potrf", ctx)
     tp.flops = flops(A.prec, "potrf", A.n)
@@ -605,7 +624,8 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     # DPLASMA_DTR_TRACE=1: per-task {start, end, workgroup << 8 | xcd} (s_memrealtime, 100 MHz) in tp.dtr_trace
     trace = None
     if os.environ.get("DPLASMA_DTR_TRACE", "0") == "1":
-        trace = torch.zeros(4 * len(plan.tasks), dtype=torch.int64, device=dev)
+        # + the POTRF blocks' phase stamps (dtr.hip run_potrf: 64 per block, nt x 16 blocks)
+        trace = torch.zeros(4 * len(plan.tasks) + nt * MAXB * 64, dtype=torch.int64, device=dev)
         img.set("trace", trace.data_ptr())
     tp.dtr_trace = trace
     # DPLASMA_DTR_PROBE=1: the strip-hazard probe of the diagonal-tile updates (tp.dtr_probe; dtr.hip probe_strip)

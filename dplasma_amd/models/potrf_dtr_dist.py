@@ -292,7 +292,9 @@ class Emulation:
         self.lo_d = up(lo if len(lo) else np.zeros(1, dtype=np.int32))
         self.info = torch.zeros(1, dtype=torch.int32, device=dev)
         self.scr = D.PotrfScratch(nt, dev, img.pstride)
-        self.trace = torch.zeros(4 * len(plan.tasks), dtype=torch.int64, device=dev) if trace else None
+        # (+ the POTRF blocks' phase stamps, dtr.hip run_potrf)
+        self.trace = (torch.zeros(4 * len(plan.tasks) + nt * D.MAXB * 64, dtype=torch.int64, device=dev)
+                      if trace else None)
         img.set("ld", NBT)
         img.set("nt", nt)
         img.set("nranks", nr)

@@ -62,7 +62,7 @@ def main():
           f"{100 * f / best / (nr * PEAK):.1f} % of peak", flush=True)
     if a.trace:
         import numpy as np
-        np.savez(a.trace, trace=em.trace.view(-1, 4).cpu().numpy(), owner=pl.owner, type=pl.tasks["type"],
+        np.savez(a.trace, trace=em.trace[:4 * len(pl.tasks)].view(-1, 4).cpu().numpy(), owner=pl.owner, type=pl.tasks["type"],
                  k0=pl.tasks["k0"], i=pl.tasks["i"], j=pl.tasks["j"], nk=pl.tasks["nk"], inc=pl.tasks["inc"],
                  req_beg=pl.tasks["req_beg"], nreq=pl.tasks["nreq"], reqs=pl.reqs, nranks=nr)
     if a.check:

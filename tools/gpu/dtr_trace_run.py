@@ -42,7 +42,8 @@ def main():
             if not ok:
                 break
     torch.cuda.synchronize()
-    tr = tp.dtr_trace.view(-1, 4).cpu().numpy()
+    tr = tp.dtr_trace[:4 * len(tp.dtr_plan.tasks)].view(-1, 4).cpu().numpy()
+    ph = tp.dtr_trace[4 * len(tp.dtr_plan.tasks):].view(-1, 16, 64).cpu().numpy()
     plan = tp.dtr_plan
     T = plan.tasks
     s, e, who = tr[:, 0], tr[:, 1], tr[:, 2]
@@ -108,7 +109,20 @@ def main():
     if out:
         np.savez(out, trace=tr, tasks=T.view(np.uint8), nt=nt, owner=np.zeros(len(T), dtype=np.int64),
                  type=T["type"], k0=T["k0"], i=T["i"], j=T["j"], r=T["r"], nk=T["nk"], inc=T["inc"], req_beg=T["req_beg"],
-                 nreq=T["nreq"], reqs=plan.reqs, nranks=1)
+                 nreq=T["nreq"], reqs=plan.reqs, nranks=1, phase=ph)
+
+    # POTRF(k) phases per block (us from the step's first block start): factor chain end (slot 51), W column end (53)
+    for k in list(range(min(6, nt))) + [nt // 2, nt - 1]:
+        p = ph[k].astype(np.float64)
+        b0 = p[:, 0].min()
+        st = (p[:, 0] - b0) / 100.0
+        dg = (p[:, 49] - b0) / 100.0
+        fe = (p[:, 51] - b0) / 100.0
+        we = (p[:, 53] - b0) / 100.0
+        print(f"POTRF({k}) block start " + " ".join(f"{x:.0f}" for x in st))
+        print(f"   diag start  " + " ".join(f"{x:.0f}" for x in dg))
+        print(f"   factor end  " + " ".join(f"{x:.0f}" for x in fe))
+        print(f"   W end       " + " ".join(f"{x:.0f}" for x in we))
 
 
 if __name__ == "__main__":
