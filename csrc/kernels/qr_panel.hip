@@ -739,7 +739,11 @@ __global__ __launch_bounds__(256, 1) void k_qr_panel_persist(T* __restrict__ P0,
                                                              T* __restrict__ part1, T* __restrict__ rowj,
                                                              T* __restrict__ part2, T* __restrict__ Yg,
                                                              T* __restrict__ Xc, int* __restrict__ cnt,
-                                                             int* __restrict__ info, long long* __restrict__ prof) {
+                                                             int* __restrict__ info, long long* __restrict__ prof,
+                                                             const int* __restrict__ pred) {
+  // predicated issue (a device-decided branch, dpl_qr_panel_set_pred): every workgroup reads the same flag before
+  // any hand-off, so a skipped launch exits whole
+  if (pred && __builtin_amdgcn_readfirstlane(*pred) == 0) return;
   qr_panel_body<T>(P0, ldp, rbl, rstride, M, nc, kf, R, V, ldv, Tm, ldt, part1, rowj, part2, Yg, Xc, cnt, info, prof,
                    gridDim.x, blockIdx.x);
 }
@@ -759,7 +763,8 @@ struct QpItem {
 
 template <typename T>
 __global__ __launch_bounds__(256, 1) void k_qr_panel_multi(const QpItem* __restrict__ items, int nitems,
-                                                           int* __restrict__ info) {
+                                                           int* __restrict__ info, const int* __restrict__ pred) {
+  if (pred && __builtin_amdgcn_readfirstlane(*pred) == 0) return;
   int e = 0;
   while (e + 1 < nitems && items[e + 1].wbase <= (int)blockIdx.x) ++e;
   const QpItem it = items[e];
@@ -784,6 +789,14 @@ static int qp_cus() {
 }
 
 static long long* g_qp_prof = nullptr;
+// Predicate of the next launches (device int32, 0 = skip; nullptr: none): models/lu_qr.py's device-decided steps
+// issue the QR branch under the decision flag (ops/batch.py predicated), and the real-precision panel kernels honour
+// it like the batched launches (complex panels run and their results are discarded by the predicated write-back)
+static const int* g_qp_pred = nullptr;
+DPL_API int dpl_qr_panel_set_pred(const void* dev_ptr) {
+  g_qp_pred = (const int*)dev_ptr;
+  return 0;
+}
 // Debug: accumulate workgroup 0's phase timers (8 x int64, 100 MHz ticks) into dev_ptr (nullptr: off).
 DPL_API int dpl_qr_panel_set_prof(void* dev_ptr) {
   g_qp_prof = (long long*)dev_ptr;
@@ -837,11 +850,11 @@ DPL_API int dpl_qr_panel(int prec, void* P, int ldp, int rbl, long long rstride,
   if (prec == DPL_D)
     hipLaunchKernelGGL((k_qr_panel_persist<double>), dim3(G), dim3(256), 0, st, (double*)P, ldp, rbl, rstride, M, nc, kf, R,
                        (double*)V, ldv, (double*)Tm, ldt, (double*)part1, (double*)rowj, (double*)part2, (double*)Yg, (double*)Xc,
-                       cnt, info, g_qp_prof);
+                       cnt, info, g_qp_prof, g_qp_pred);
   else
     hipLaunchKernelGGL((k_qr_panel_persist<float>), dim3(G), dim3(256), 0, st, (float*)P, ldp, rbl, rstride, M, nc, kf, R,
                        (float*)V, ldv, (float*)Tm, ldt, (float*)part1, (float*)rowj, (float*)part2, (float*)Yg, (float*)Xc, cnt,
-                       info, g_qp_prof);
+                       info, g_qp_prof, g_qp_pred);
   return (int)hipGetLastError();
 }
 
@@ -909,9 +922,9 @@ DPL_API int dpl_qr_panel_multi(int prec, int n, int total, const void* items, in
   if (total <= 0 || total > qp_cus()) return -4;
   HIP_CHECK_RET(hipMemsetAsync(cnt0, 0, sizeof(int) * n, st));
   if (prec == DPL_D)
-    hipLaunchKernelGGL((k_qr_panel_multi<double>), dim3(total), dim3(256), 0, st, (const QpItem*)items, n, info);
+    hipLaunchKernelGGL((k_qr_panel_multi<double>), dim3(total), dim3(256), 0, st, (const QpItem*)items, n, info, g_qp_pred);
   else
-    hipLaunchKernelGGL((k_qr_panel_multi<float>), dim3(total), dim3(256), 0, st, (const QpItem*)items, n, info);
+    hipLaunchKernelGGL((k_qr_panel_multi<float>), dim3(total), dim3(256), 0, st, (const QpItem*)items, n, info, g_qp_pred);
   return (int)hipGetLastError();
 }
 

@@ -146,7 +146,9 @@ class _GetrfQrf(Taskpool):
         if qr_panel.usable(A, tree):
             # a data-dependent criterion may run device-decided (below): its QR panels then run under a predicate
             # they do not see, so none may factor in place in A
-            maybe_dev = (ctx.world == 1 and A.device.type == "cuda" and (criteria in _HIGHAMS or criteria == MUMPS_CRITERIUM)
+            maybe_dev = (((ctx.world == 1 and A.device.type == "cuda") or
+                          (ctx.world > 1 and (p or A.grid.P) % A.grid.P == 0))
+                         and (criteria in _HIGHAMS or criteria == MUMPS_CRITERIUM)
                          and os.environ.get("DPLASMA_LUQR_DEVCRIT", "1") != "0")
             self.qpf = qr_panel._Factor(ctx, A, TS, TT, tree, inplace=not maybe_dev)
             TS.qr_format = TT.qr_format = "panel"
@@ -172,6 +174,19 @@ class _GetrfQrf(Taskpool):
                         and (criteria in _HIGHAMS or criteria == MUMPS_CRITERIUM) and self.alpha != 0
                         and self.alpha < 9999999999 and os.environ.get("DPLASMA_LUQR_DEVCRIT", "1") != "0"
                         and os.environ.get("DPLASMA_LUQR_SYNC", "0") != "1")
+        # Several processes (the reference reduces the criterion inside the DAG: zlufacto -> reduce_norm ->
+        # setchoice, src/zgetrf_qrf.jdf:739-1156): the diagonal owner's domain LU, w0 and pivots, every rank's
+        # off-domain norms, the cross-rank reduction (device all-reduce: RCCL on GPUs) and the decision flag stay
+        # on the device, and both branches are issued under the flag -- the LU branch's interchanges from a
+        # device move list (the domain lives on one process row when p is a multiple of P), its solves and
+        # update as a predicated tile program; the QR branch on the stacked-domain engine (no in-place panels).
+        # On the CPU the batched fallbacks loop over host records and cannot see a predicate: there the flag is
+        # read (no device to synchronise) and only the taken branch runs.
+        self.devcrit_dist = (ctx.world > 1 and self.qpf is not None and not self.qpf.inplace
+                             and (criteria in _HIGHAMS or criteria == MUMPS_CRITERIUM) and self.alpha != 0
+                             and self.alpha < 9999999999 and self.p % A.grid.P == 0
+                             and os.environ.get("DPLASMA_LUQR_DEVCRIT", "1") != "0"
+                             and os.environ.get("DPLASMA_LUQR_SYNC", "0") != "1")
         self._dec = []
         if self.devcrit:
             # every step's tables, panel plans and workspaces now: the run issues no host round trip at all
@@ -369,14 +384,17 @@ class _GetrfQrf(Taskpool):
         if d is not None:
             return d
         A, k = self.A, st.k
-        g, back = TileBatch(), TileBatch()
-        r0 = 0
-        for m, r in zip(st.dom, st.rows):
-            g.add(A.offset(m, k), r, st.ncol, b_off=r0)
-            back.add(r0, r, st.ncol, b_off=A.offset(m, k))
-            r0 += r
-        d = {"gather": g.finalize(), "back": back.finalize()}
-        trail = list(range(k + 1, A.nt))
+        d = {}
+        if A.rank == st.owner:   # the domain's tiles (all of column k's domain rows live with the diagonal tile)
+            g, back = TileBatch(), TileBatch()
+            r0 = 0
+            for m, r in zip(st.dom, st.rows):
+                g.add(A.offset(m, k), r, st.ncol, b_off=r0)
+                back.add(r0, r, st.ncol, b_off=A.offset(m, k))
+                r0 += r
+            d["gather"], d["back"] = g.finalize(), back.finalize()
+        # the trailing interchanges: my local trailing columns, when the domain rows are on my process row
+        trail = [n for n in range(k + 1, A.nt) if A.col_is_local(n)] if A.row_is_local(k) else []
         if trail:
             base = A.offset(st.dom[0], trail[0])
             d["rowoff"] = torch.tensor([A.offset(m, trail[0]) - base for m in st.dom], dtype=torch.int64,
@@ -416,6 +434,111 @@ class _GetrfQrf(Taskpool):
         if t is None:
             t = self._dinfo = torch.zeros(1, dtype=torch.int32, device=self.A.device)
         return t
+
+    # ------------------------------------------------------------------ device-decided steps, several processes
+    def _run_devcrit_dist(self):
+        from ..ops import batch as B
+        A, ctx = self.A, self.ctx
+        gpu = A.device.type == "cuda"
+        self._dec = []
+        for k in range(self.minMNT):
+            st = _Step(A, k, self.p)
+            mine = self._domain_lu_dev(st) if ctx.rank == st.owner else None
+            flag, ipiv = self._decide_dev(st, mine)
+            self._dec.append(flag)
+            if gpu:
+                with B.predicated(flag):
+                    self._lu_step_dist_dev(st, mine, ipiv, flag)
+                with B.predicated(1 - flag):
+                    self._qr_step(st, zero_ipiv=False)   # (the LU branch wrote IPIV(k, k) = flag * pivots)
+            elif int(flag[0]):
+                self._lu_step_dist_dev(st, mine, ipiv, flag)
+            else:
+                self._qr_step(st)
+
+    def _decide_dev(self, st: _Step, mine):
+        """_decide on the device: the SUM vector [w0, bad, offsum, ipiv(nb), colmax_diag(nb)] and the MAX vector
+        [offmax, colmax_off(nb)] filled by device ops, all-reduced on the device, the flag computed from them.
+        Returns (flag int32 [1], pivots int32 [kmax]) -- the same on every rank, nothing read by the host."""
+        A, crit, alpha = self.A, self.criteria, self.alpha
+        dev, nb, k = A.device, A.nb, st.k
+        f64 = torch.float64
+        vs = torch.zeros(3 + 2 * nb, dtype=f64, device=dev)
+        vm = torch.zeros(1 + nb, dtype=f64, device=dev)
+        if mine is not None:
+            _, view, ipiv, info, colmax = mine
+            bad = info[0] != 0
+            vs[1] = bad.to(f64)
+            if crit in _HIGHAMS:
+                w0 = torch.nan_to_num(_w0(view[:st.ncol, :st.ncol], crit).to(f64), nan=0.0, posinf=float("inf"))
+                vs[0] = torch.where(bad, torch.zeros((), dtype=f64, device=dev), w0)
+            vs[3:3 + st.kmax] = ipiv[:st.kmax].to(f64)
+            if colmax is not None:
+                vs[3 + nb:3 + nb + colmax.numel()] = colmax.to(f64)
+        offs = [A.tile(m, k) for m in st.off if A.is_local(m, k)]
+        if offs:
+            if crit == MUMPS_CRITERIUM:
+                cm = torch.stack([t.abs().amax(0) for t in offs]).amax(0).to(f64)
+                vm[1:1 + cm.numel()] = cm
+            else:
+                n1 = torch.stack([t.abs().sum(0).max() for t in offs]).to(f64)
+                vs[2] = n1.sum()
+                vm[0] = n1.max()
+        comm.allreduce(vs)
+        comm.allreduce(vm, op=torch.distributed.ReduceOp.MAX)
+        w0, offsum, offmax = vs[0], vs[2], vm[0]
+        bad = vs[1] > 0
+        if crit in (HIGHAM_CRITERIUM, HIGHAM_SUM_CRITERIUM):
+            cond = alpha * w0 > offsum
+        elif crit == HIGHAM_MAX_CRITERIUM:
+            cond = alpha * w0 > offmax
+        elif crit == HIGHAM_MOY_CRITERIUM:
+            nt_ = A.mt - k
+            nout = nt_ - (nt_ + self.p - 1) // self.p
+            cond = (alpha * w0 > offsum / nout) if nout else torch.zeros((), dtype=torch.bool, device=dev)
+        else:   # MUMPS
+            cond = (alpha * vs[3 + nb:3 + nb + st.ncol] >= vm[1:1 + st.ncol]).all()
+        flag = (cond & ~bad).to(torch.int32).view(1)
+        return flag, vs[3:3 + st.kmax].round().to(torch.int32)
+
+    def _lu_step_dist_dev(self, st: _Step, mine, ipiv, flag):
+        """The LU branch on a P x Q grid, issued under the step's predicate: the owner writes the factored domain
+        back, IPIV(k, k) = flag x pivots, the domain's process row permutes its local trailing columns from the
+        device move list (count multiplied by the flag), then the solves and the update (tile program: batched
+        launches, predicated; its operand transfers run whatever the flag -- they only read)."""
+        A, k = self.A, st.k
+        d = self._dev_step(st)
+        if mine is not None:
+            ops.geadd(0, N_, 1.0, mine[0], st.M, 0.0, A.data, A.ld, d["back"], copy=True)
+        if self.IPIV.is_local(k, k):
+            t = self.IPIV.tile(k, k)
+            new = torch.zeros_like(t)
+            new[:st.kmax, 0] = ipiv[:st.kmax] + 1
+            t.copy_(new * flag.to(t.dtype))
+        if "rowoff" in d:
+            mdst, msrc, mcnt = d["mv"]
+            with ops_batch_unpredicated():
+                ops.piv_moves(ipiv, st.kmax, mdst, msrc, mcnt, mrel=st.M, info=self._devinfo())
+            mcnt.mul_(flag)
+            ops.rows_permute(A.data, A.ld, A.mb, 0, d["rowoff"], d["coloff"], d["ncols"], A.nb, mdst, msrc, mcnt,
+                             2 * A.nb, self._devinfo())
+        self._lu_update_prog(st)
+
+    def _lu_update_prog(self, st: _Step):
+        """The LU step's solves and trailing update on a P x Q grid (one tile program)."""
+        A, ctx, k = self.A, self.ctx, st.k
+        prog = TileProgram(ctx, f"getrf_qrf_lu({k})")
+        s = prog.stage("trsm")
+        for n in range(k + 1, A.nt):
+            s.trsm(dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, (A, k, k), (A, k, n))
+        for m in st.off:
+            s.trsm(dplasmaRight, dplasmaUpper, N_, dplasmaNonUnit, 1.0, (A, k, k), (A, m, k))
+        if k + 1 < A.nt:
+            s = prog.stage("gemm")
+            for m in range(k + 1, A.mt):
+                for n in range(k + 1, A.nt):
+                    s.gemm((A, m, n), [((A, m, k), N_, (A, k, n), N_)], alpha=-1.0, beta=1.0)
+        prog.compile().execute(ctx)
 
     # ------------------------------------------------------------------ one panel
     def _domain_lu(self, st: _Step):
@@ -548,18 +671,7 @@ class _GetrfQrf(Taskpool):
         if ctx.world == 1:
             self._lu_update_local(st)
             return
-        prog = TileProgram(ctx, f"getrf_qrf_lu({k})")
-        s = prog.stage("trsm")
-        for n in range(k + 1, A.nt):
-            s.trsm(dplasmaLeft, dplasmaLower, N_, dplasmaUnit, 1.0, (A, k, k), (A, k, n))
-        for m in st.off:
-            s.trsm(dplasmaRight, dplasmaUpper, N_, dplasmaNonUnit, 1.0, (A, k, k), (A, m, k))
-        if k + 1 < A.nt:
-            s = prog.stage("gemm")
-            for m in range(k + 1, A.mt):
-                for n in range(k + 1, A.nt):
-                    s.gemm((A, m, n), [((A, m, k), N_, (A, k, n), N_)], alpha=-1.0, beta=1.0)
-        prog.compile().execute(ctx)
+        self._lu_update_prog(st)
 
     def _lu_update_local(self, st: _Step):
         """One process: the LU step's solves and trailing update as three batched launches (TRSM of
@@ -637,6 +749,11 @@ class _GetrfQrf(Taskpool):
             if self.info_out is not None:
                 self.info_out[0] = 0
             return
+        if self.devcrit_dist:
+            self._run_devcrit_dist()
+            if self.info_out is not None:
+                self.info_out[0] = 0
+            return
         for k in range(self.minMNT):
             st = _Step(A, k, self.p)
             mine = self._domain_lu(st) if ctx.rank == st.owner else None
@@ -655,7 +772,7 @@ class _GetrfQrf(Taskpool):
         if self.qpf is not None and int(self.qpf.info.item()) != 0:
             raise RuntimeError(f"getrf_qrf: QR panel kernel reported {int(self.qpf.info.item())}")
         r = int(self.fast_info.item()) if self.fast is not None else 0
-        if self.devcrit and self._dec:
+        if (self.devcrit or self.devcrit_dist) and self._dec:
             # the decisions, read back once for the whole factorisation
             dec = torch.cat(self._dec).cpu().tolist()
             for k, c in enumerate(dec):

@@ -97,6 +97,7 @@ _SIGS = {
     "dpl_qr_panel_ws_bytes": [c_int, c_int, c_int],
     "dpl_qr_panel_max_rows": [],
     "dpl_qr_panel_set_prof": [c_vp],
+    "dpl_qr_panel_set_pred": [c_vp],
     # ipiv, kb, mrel, dst, src, cnt, info, stream
     "dpl_piv_moves": [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp],
     # prec, gather, A, ld, mb, r0, rowoff, nrt, coloff, ncols, nct, nb, rows, cnt, maxcnt, buf, ldb, info, stream

@@ -14,6 +14,7 @@ raises.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import numpy as np
@@ -809,6 +810,17 @@ def butterfly(A, r: torch.Tensor, size: int, side: int, trans: int):
 QR_PANEL_MAXW = 256   # widest panel of the single-launch Householder panel kernel (qr_panel.hip QP_R)
 
 
+def _qp_pred(lib):
+    """Hand the enclosing batch predicate (ops/batch.py predicated) to the next panel launch: a device-decided
+    branch's panels then exit at once when the flag is 0, like its batched launches."""
+    from . import batch as _b
+    f = _b._PRED[0]
+    if f is None or not f.is_cuda:
+        return False
+    lib.dpl_qr_panel_set_pred(ctypes.c_void_p(f.data_ptr()))
+    return True
+
+
 def qr_panel_max_rows(device) -> int:
     """Tallest panel the persistent QR panel kernel factors in one launch (one workgroup per CU)."""
     if torch.device(device).type == "cuda":
@@ -889,9 +901,12 @@ class QrPanelMulti:
                 V[voff: voff + ldv * kf] = vt
                 Tm[toff: toff + ldt * kf] = tt
             return
-        rc = _lib.load().dpl_qr_panel_multi(_lib.prec_code(self.dtype), len(self.panels), self.total,
-                                            self.items.data_ptr(), self.cnt.data_ptr(), info.data_ptr(),
-                                            _lib.stream_ptr())
+        lib = _lib.load()
+        pr = _qp_pred(lib)
+        rc = lib.dpl_qr_panel_multi(_lib.prec_code(self.dtype), len(self.panels), self.total,
+                                    self.items.data_ptr(), self.cnt.data_ptr(), info.data_ptr(), _lib.stream_ptr())
+        if pr:
+            lib.dpl_qr_panel_set_pred(ctypes.c_void_p(0))
         _lib.check(rc, "qr_panel_multi")
 
 
@@ -930,9 +945,13 @@ def qr_panel(P: torch.Tensor, ldp: int, M: int, nc: int, kf: int, V: torch.Tenso
     if kf <= 0:
         return
     if _is_gpu(P):
-        rc = _lib.load().dpl_qr_panel(_lib.prec_code(P.dtype), P.data_ptr() + poff * P.element_size(), ldp, int(rbl),
-                                      int(rstride), M, nc, kf, V.data_ptr(), ldv, Tm.data_ptr(), ldt, ws.data_ptr(),
-                                      info.data_ptr(), _lib.stream_ptr())
+        lib = _lib.load()
+        pr = _qp_pred(lib)
+        rc = lib.dpl_qr_panel(_lib.prec_code(P.dtype), P.data_ptr() + poff * P.element_size(), ldp, int(rbl),
+                              int(rstride), M, nc, kf, V.data_ptr(), ldv, Tm.data_ptr(), ldt, ws.data_ptr(),
+                              info.data_ptr(), _lib.stream_ptr())
+        if pr:
+            lib.dpl_qr_panel_set_pred(ctypes.c_void_p(0))   # (the library's other callers launch unpredicated)
         _lib.check(rc, "qr_panel")
         return
     if 0 < rbl < M or poff:

@@ -103,6 +103,41 @@ def test_getrf_qrf_distributed_data_criteria(ctx, crit, alpha):
     assert tabs[0] == tab1
 
 
+def _worker_devcrit(rank, world, P, crit, alpha, devcrit):
+    import os
+    os.environ["DPLASMA_LUQR_DEVCRIT"] = devcrit
+    ctx = dp.init(device="cpu", P=P)
+    N, NB, ib = 96, 16, 4
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+    dp.plrnt(ctx, A, 7)
+    TS = dp.block_cyclic(ctx, torch.float64, ib, NB, A.mt * ib, N)
+    TT = dp.block_cyclic(ctx, torch.float64, ib, NB, A.mt * ib, N)
+    IP = dp.qrf_ipiv_descriptor(ctx, A)
+    tree = qrtree.hqr_init(dp.dplasmaNoTrans, A, qrtree.GREEDY_TREE, qrtree.FLAT_TREE, 2, None)
+    tp = lu_qr.getrf_qrf_New(ctx, tree, A, IP, TS, TT, crit, alpha)
+    tp.execute(ctx)
+    import torch.distributed as dist
+    x, ip = A.to_dense_local(), IP.to_dense_local()
+    dist.all_reduce(x)
+    dist.all_reduce(ip)
+    return tp.devcrit_dist, list(tp.lu_tab), x, ip
+
+
+@pytest.mark.parametrize("crit,alpha,P,world", [(dp.HIGHAM_CRITERIUM, 0.02, 2, 2), (dp.MUMPS_CRITERIUM, 1.0, 2, 4),
+                                                (dp.HIGHAM_MAX_CRITERIUM, 2.0, 1, 2)])
+def test_getrf_qrf_distributed_device_decision(crit, alpha, P, world):
+    """Several processes, data-dependent criterion: the decision is reduced and taken on the device (the
+    reference's zlufacto -> reduce_norm -> setchoice inside the DAG) -- same lu_tab, pivots and factors as the
+    host-decided path (DPLASMA_LUQR_DEVCRIT=0), with both LU and QR steps among the decisions."""
+    dev = run_distributed(_worker_devcrit, world, P, crit, alpha, "1")
+    host = run_distributed(_worker_devcrit, world, P, crit, alpha, "0")
+    assert all(dev[r][0] for r in range(world)) and not any(host[r][0] for r in range(world))
+    assert all(dev[r][1] == dev[0][1] for r in range(world))
+    assert dev[0][1] == host[0][1]
+    assert bool((dev[0][3] == host[0][3]).all())
+    assert float((dev[0][2] - host[0][2]).abs().max()) < 1e-12 * float(host[0][2].abs().max())
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("crit", [dp.DEFAULT_CRITERIUM, dp.HIGHAM_SUM_CRITERIUM])
 def test_gpu_getrf_qrf(crit):
