@@ -869,6 +869,7 @@ __global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ ga
   const int xcd = xcc_id();
   unsigned long long idle0 = 0;
   int nap = 1;
+  int seen_done = -1;   // g.done read before this workgroup's last empty scan (-1: none)
   int rk, x0, nx;
   bool sy, em;
   {
@@ -887,8 +888,17 @@ __global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ ga
     const DtrArgs& g = *gp;
     if (tid < 64) {
       int t = -1;
+      // one process: a task is pushed only by a completion, and every completion bumps g.done after its pushes --
+      // so when g.done has not moved since this workgroup's last empty scan, no ring can have gained a task and
+      // the 2 x nclass x 8 coherent loads of a scan are skipped (with ~160 idle workgroups rescanning, the early
+      // steps' POTRF hand-offs ran 2x slower: profiles/r6_dtr16k_analysis.txt).  Not with remote pushes (peers)
+      // or emulated visibility times.  DPLASMA_DTR_SCANSKIP=0 (flags bit 5) turns it off.
+      const bool can_skip = !sy && !em && !(g.flags & 32);
+      const int dnow = can_skip ? __builtin_amdgcn_readfirstlane(ld_sc1(g.done)) : 0;
       if (ld_sc1(g.info) == -1000) {
         t = -2;
+      } else if (can_skip && dnow == seen_done) {
+        if (dnow >= g.ntask) t = -2;
       } else {
         // every ring's emptiness at once (lane l: scan position l + 64 w, class-major, own XCD first inside a
         // class), then a pop of the first non-empty one in that order; a lost race rescans
@@ -924,6 +934,7 @@ __global__ __launch_bounds__(256, 2) void k_dtr_q(const DtrArgs* __restrict__ ga
           // (a race: the popped head was replaced by one not visible yet) -- wait for it, it is ours now
           while (ld_sc1(g.rdy + t) > now_t()) __builtin_amdgcn_s_sleep(2);
         }
+        seen_done = (t < 0 && can_skip) ? dnow : -1;
         if (t < 0 && __builtin_amdgcn_readfirstlane(ld_sc1(g.done)) >= g.ntask) t = -2;
       }
       if (t >= 0) {

@@ -518,6 +518,10 @@ def flags_from_env() -> int:
     sw = int(os.environ.get("DPLASMA_DTR_STEPW", "0"))
     if sw:
         fl |= (min(15, max(1, sw)) << 24)
+    # DPLASMA_DTR_SCANSKIP=0: idle workgroups rescan every ready ring even when no task completed since their last
+    # empty scan (measurement knob; default: skip)
+    if os.environ.get("DPLASMA_DTR_SCANSKIP", "1") == "0":
+        fl |= 32
     # DPLASMA_DTR_NAP=n: the push scheduler's idle back-off cap, n = 2^e sleeps (default 16)
     nap = int(os.environ.get("DPLASMA_DTR_NAP", "0"))
     if nap > 0:

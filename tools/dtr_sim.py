@@ -22,13 +22,15 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 DUR = {"upd1": 76.0, "upd4_per_k": 64.0, "trsm": 177.0, "potrf_blk": 23.0, "pop": 4.0}
 
 
-def simulate(plan, q, nwg=256, dur=DUR, prio=None):
+def simulate(plan, q, nwg=256, dur=DUR, prio=None, override=None):
     from dplasma_amd.models import potrf_dtr as D
     T = plan.tasks
     n = len(T)
     typ, nk, k0, blk = T["type"], T["nk"].astype(float), T["k0"], T["r"]
     d = np.where(typ == D.T_UPD, np.where(nk <= 1, dur["upd1"], dur["upd4_per_k"] * nk),
                  np.where(typ == D.T_TRSM, dur["trsm"], 0.0))
+    if override is not None:   # (mask, duration): what-if durations of selected tasks
+        d = np.where(override[0], override[1], d)
     pend = q["ndeps"].astype(np.int64).copy()
     so, su = q["succ_off"], q["succ"]
     ring = q["ring_of"] if prio is None else prio
