@@ -200,8 +200,16 @@ class Context:
         """Destroy the HIP streams this context created itself (CU-masked ones)."""
         owned = getattr(self, "_owned_streams", [])
         if owned:
+            import gc
+
             from .ops import _lib
+            # tensors the caching allocator handed out on these streams must go back to it while the streams
+            # still exist: task pools hold reference cycles (closures), so without a collection here their
+            # tensors were freed by a LATER garbage collection, onto destroyed streams -- a segfault inside an
+            # unrelated test's import (GPU suite, round 6)
+            gc.collect()
             torch.cuda.synchronize(self.device)
+            torch.cuda.empty_cache()
             for name in ("diag", "potrf_update", *getattr(self, "_owned_names", [])):
                 self.streams.pop(name, None)
             for s in owned:

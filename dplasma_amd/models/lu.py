@@ -268,7 +268,13 @@ class _GetrfDev:
         # default: the rank replay charges the extra factorisation and cannot credit the cross-rank chain it
         # shortens, profiles/r6_lu_config5.txt)
         self.gxp2p = g.P > 1 and pivot and self.panel_mode == "gather"
-        self.rnf = (self.gxp2p and self.xmode and g.Q > 1 and os.environ.get("DPLASMA_LU_RNF", "0") == "1")
+        # RNF is switched off: the 2 x 4 one-GPU rehearsal gives wrong factors (correct pivots) with it, before and after
+        # the round-6 LSEND buffer fix (tools/gpu/r6_b27.sh) -- DPLASMA_LU_RNF=1 is ignored with a warning until fixed
+        self.rnf = False
+        if self.gxp2p and self.xmode and g.Q > 1 and os.environ.get("DPLASMA_LU_RNF", "0") == "1":
+            import warnings
+            warnings.warn("DPLASMA_LU_RNF=1 ignored: the redundant next-column panel factorisation is disabled "
+                          "(wrong factors in the 2x4 rehearsal)")
         if self.xmode:
             # the rest of the trailing columns in DPLASMA_LU_CHUNKS column chunks: chunk c's interchanges / U block of
             # step k+1 (exchange stream) overlap the update of chunk c+1 of step k (update stream)
@@ -298,6 +304,10 @@ class _GetrfDev:
             self.g_next = ctx.urgent_group if ctx.urgent_group is not None else ctx.col_group
             bulk = list(ctx.bulk_groups) or [ctx.col_group]
             self.g_rest, self.g_left = bulk[0], bulk[-1]
+        elif self.gxp2p:
+            # gather panels with the summed row exchange (DPLASMA_LU_XROWS=allreduce): the panel slots still travel
+            # point to point, on the urgent communicator
+            self.g_next = ctx.urgent_group if ctx.urgent_group is not None else ctx.col_group
         ncol_loc = sum(A.tile_cols(n) for n in lcols)
         self.ubuf = torch.zeros(max(1, nb * max(ncol_loc, 1)), dtype=A.dtype, device=dev)
         # xmode: U blocks double-buffered by step parity (step k+1's exchanges run while step k's update chunks read)
@@ -324,6 +334,11 @@ class _GetrfDev:
         # travel from a copy (piv_dev is re-filled by the next panel while the send may still be in flight)
         self.lsend_task = bool(self.lookahead and self.xmode and self.gxp2p and g.Q > 1)
         self.piv_send = [torch.zeros_like(self.piv_dev), torch.zeros_like(self.piv_dev)]
+        # ... and the rows from their own buffers (by step parity): rbuf is this rank's RECEIVE buffer of the next steps
+        # (PANEL(k+1) on a rank of panel k's column receives there while LSEND(k) may still be packing / sending --
+        # no task edge orders the two; sharing rbuf gave intermittently wrong factors with correct pivots)
+        self.rbuf_send = ([torch.zeros_like(self.rbuf), torch.zeros_like(self.rbuf)]
+                          if (self.lsend_task and self.rbuf is not None) else None)
         if self.lsend_task and dev.type == "cuda" and "lsend" not in ctx.streams:
             ctx.streams["lsend"] = torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1])
         self.bytes_panel = [0] * self.kt   # elements this rank sends per step (panel exchange)
@@ -636,7 +651,7 @@ class _GetrfDev:
                     ops.geadd(0, N_, 1.0, gb[sl[q][0]:], sl[q][2], 0.0, pv, st["mp"], st["gunpack"][q], copy=True)
             self.bytes_panel[k] = st["gsent"]
             st["plu"].run(self.piv_dev, self.ws, self.cnt, self.info, st["r0"])
-            if self.lsend_task and in_k:   # (panel stream: PANEL(k+1) re-fills piv_dev before LSEND(k) may run)
+            if in_k:   # (LSEND task: PANEL(k+1) re-fills piv_dev before LSEND(k) may run)
                 self.piv_send[k & 1].copy_(self.piv_dev)
         if g.Q > 1:
             others = [c for c in range(g.Q) if c != kc and c != kc1]
@@ -667,8 +682,9 @@ class _GetrfDev:
             return
         sends = [(self.piv_send[k & 1], g.rank(A.myrow, c)) for c in others]
         if "rlen" in st and st["rlen"]:
-            ops.geadd(0, N_, 1.0, st["pv"], st["pld"], 0.0, self.rbuf, st["rld"], st["rpack"], copy=True)
-            sends += [(self.rbuf[: st["rlen"]], g.rank(A.myrow, c)) for c in others]
+            rb = self.rbuf_send[k & 1] if self.rbuf_send is not None else self.rbuf
+            ops.geadd(0, N_, 1.0, st["pv"], st["pld"], 0.0, rb, st["rld"], st["rpack"], copy=True)
+            sends += [(rb[: st["rlen"]], g.rank(A.myrow, c)) for c in others]
         comm.p2p(sends, (), group=ctx.row_group)
 
     def _panel_dist(self, k):

@@ -45,8 +45,18 @@ def test_lu_dist_host_exchange_on_gpu():
 @pytest.mark.parametrize("panel", ["gather", "dist"])
 def test_lu_grid_2x4_rehearsal(panel):
     """The whole P x Q program on a 2 x 4 grid of eight processes sharing the GPU: point-to-point interchanges of the
-    rows crossing process rows, chunked trailing exchanges, look-ahead and -- gather panels -- the redundant
-    factorisation of each panel on the next panel's column (RNF).  Pivots and factors equal one process."""
+    rows crossing process rows, chunked trailing exchanges, look-ahead, the panel rows' own LSEND buffers (the shared
+    receive buffer gave intermittently wrong factors).  Pivots and factors equal one process."""
     rc, out = _run(8, 4096, 256, {"DPLASMA_LU_PANEL": panel}, timeout=400, P=2)
     assert rc == 0, out[-3000:]
     assert out.count("SUCCESS") == 8 and "2x4" in out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{"DPLASMA_LU_LOOKAHEAD": "0"}, {"DPLASMA_LU_XROWS": "allreduce"}])
+def test_lu_grid_2x4_gather_modes(env):
+    """Gather panels without look-ahead (the panel column sends the pivots inline) and with the summed row exchange
+    (the panel slots still travel point to point): both were broken before round 6's fixes."""
+    rc, out = _run(8, 4096, 256, dict(env, DPLASMA_LU_PANEL="gather"), timeout=400, P=2)
+    assert rc == 0, out[-3000:]
+    assert out.count("SUCCESS") == 8
