@@ -1085,6 +1085,43 @@ DPL_API int dpl_rows_permute(int prec, void* A, int ld, int mb, int r0, const lo
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------- deferred left interchanges (one process row)
+// getrf_1d with DPLASMA_LU_DEFER_LEFT: every step's interchanges touch the trailing columns only, and each factored
+// tile column receives, once at the end, the composition of all later steps' interchanges (a permutation of its rows
+// [r0, m), host-composed: dplasma_amd.lib._dplasma_rt.piv_compose_left).  GATHER: buf(i, c) = A(src[i], c), the
+// reads scattered, the writes coalesced; then A(r0 + i, c) = buf(i, c), coalesced both ways.  Same element moves
+// as applying the swaps step by step, each element once (the per-step moves sweep every left column every step).
+template <typename T, bool GATHER>
+__global__ __launch_bounds__(256) void k_rows_perm_col(T* __restrict__ A, int ld, int mb,
+                                                       const long long* __restrict__ rowoff, int nrt, long long coff,
+                                                       int ncols, const int* __restrict__ src, int r0, int cnt,
+                                                       T* __restrict__ buf, int* __restrict__ info) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= cnt) return;
+  const int R = GATHER ? src[i] : r0 + i;
+  const int rt = R / mb;
+  if (R < r0 || rt >= nrt || rowoff[rt] < 0) {   // a row outside [r0, m): a corrupt composition, nothing moves
+    if (GATHER) report_bad_pivot(info);
+    return;
+  }
+  const long long base = rowoff[rt] + (R % mb) + coff;
+  for (int c = blockIdx.y; c < ncols; c += gridDim.y) {
+    if (GATHER) buf[i + (long long)c * cnt] = A[base + (long long)c * ld];
+    else A[base + (long long)c * ld] = buf[i + (long long)c * cnt];
+  }
+}
+
+DPL_API int dpl_rows_perm_col(int prec, void* A, int ld, int mb, const long long* rowoff, int nrt, long long coff,
+                              int ncols, const int* src, int r0, int cnt, void* buf, int* info, hipStream_t st) {
+  if (cnt <= 0 || ncols <= 0) return 0;
+  const dim3 grid((cnt + 255) / 256, ncols < 64 ? ncols : 64);
+  DISPATCH(prec, hipLaunchKernelGGL((k_rows_perm_col<T, true>), grid, dim3(256), 0, st, (T*)A, ld, mb, rowoff, nrt,
+                                    coff, ncols, src, r0, cnt, (T*)buf, info));
+  DISPATCH(prec, hipLaunchKernelGGL((k_rows_perm_col<T, false>), grid, dim3(256), 0, st, (T*)A, ld, mb, rowoff, nrt,
+                                    coff, ncols, src, r0, cnt, (T*)buf, info));
+  return (int)hipGetLastError();
+}
+
 // ---------------------------------------------------------------- cross-process-row interchanges (P > 1)
 // The reference's SWAP_COLLECT / SWAP_SND (src/zgetrf_ptgpanel.jdf:825-984): only the moved rows whose source and
 // destination live on DIFFERENT process rows travel, point to point between those two rows of the process column.

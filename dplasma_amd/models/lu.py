@@ -180,7 +180,7 @@ class _GetrfDev:
         mb, nb = A.mb, A.nb
         g = A.grid
         self.kt = min(A.mt, A.nt)
-        # look-ahead is opt-in: measured on one MI355X (profiles/r2_lu_lookahead.txt) the persistent
+        # round 2: look-ahead opt-in -- measured on one MI355X (profiles/r2_lu_lookahead.txt) the persistent
         # grid-barrier panel kernel beside the REST GEMM slows from ~0.5 to ~1.2 ms per 64-column
         # block (its workgroups share CUs with GEMM waves), which eats the overlap: DGETRF 32k
         # 28.2 -> 27.1 TF/s, 64k 48.1 -> 47.2 TF/s with look-ahead on
@@ -190,6 +190,14 @@ class _GetrfDev:
         # cross-process hand-offs are latency, not CU time, so they belong beside the bulk update (tools/replay_lu.py)
         la_def = "1" if (g.P > 1 and pivot and os.environ.get("DPLASMA_LU_PANEL", "gather") != "percol"
                          and os.environ.get("DPLASMA_LU_XROWS", "p2p") != "allreduce") else "0"
+        # one process, round 6: re-measured with the tagged pivoting kernel and the deferred left interchanges, look-ahead
+        # with 32-column pivoting blocks (64 KB of LDS: room for a GEMM workgroup beside it) now wins -- 32k 35.1-35.2
+        # -> 36.0, 64k 53.7 -> 54.0 TF/s (tools/gpu/r6_b29.sh; r6_b19 without the deferral: 34.2 -> 35.3, 53.2 -> 53.6)
+        la_p1 = g.P == 1 and g.Q == 1 and pivot and lookahead is None and "DPLASMA_LU_LOOKAHEAD" not in os.environ
+        if la_p1:
+            la_def = "1"
+            if panel_bw is None and "DPLASMA_LU_BW" not in os.environ:
+                panel_bw = 32
         self.lookahead = (os.environ.get("DPLASMA_LU_LOOKAHEAD", la_def) == "1") if lookahead is None else bool(lookahead)
         self.panel_bw = panel_bw   # base block width of the recursive panel (None: ops.LU_BW)
         self.pbufs = [torch.zeros(max(1, A.m * nb), dtype=A.dtype, device=dev)
@@ -245,6 +253,14 @@ class _GetrfDev:
         # row-move time grows 82 -> 132 ms at N=32k and the factorisation is no faster, so the
         # default keeps one exchange per step.  P > 1 always keeps one summed exchange.
         self.inplace_moves = os.environ.get("DPLASMA_LU_INPLACE_MOVES", "1") != "0"
+        # P == 1 (DPLASMA_LU_DEFER_LEFT, default on: 32k 34.4 -> 35.1, 64k 52.7 -> 53.6 TF/s, r6_b28): every step's interchanges touch the trailing columns only, and each factored
+        # tile column gets the composition of all later steps' interchanges once, at the end (piv_compose_left +
+        # rows_perm_col): each left element moves once instead of once per later step, off the steps' critical path
+        self.defer_left = (self.tmp is not None and A.grid.P == 1 and pivot and not trailing_only
+                           and os.environ.get("DPLASMA_LU_DEFER_LEFT", "1") == "1")
+        if self.defer_left:
+            self.trailing_only = True
+            self.coloff_h = [A.offset(lrows[0], n) for n in lcols]
         self.side = None
         if self.tmp is not None and A.grid.P == 1 and dev.type == "cuda" and \
                 os.environ.get("DPLASMA_LU_SIDE_SWAPS", "0") == "1":
@@ -941,12 +957,38 @@ class _GetrfDev:
         else:
             self._update(k, "gemm_rest")
 
+    def left_all(self):
+        """The deferred left interchanges (defer_left): column n's rows below its diagonal block take the composition
+        of steps n+1 .. kt-1's interchanges.  One host read of the pivots, after the last step."""
+        if not self.defer_left or self.kt < 2:
+            return
+        from ..runtime.dag import _lib_rt
+        A = self.A
+        mb = A.mb
+        ip = self.ipiv_all[: min(A.m, A.n)].cpu().numpy()
+        src, off = _lib_rt().piv_compose_left(ip, A.m, mb, self.kt)
+        srcd = torch.from_numpy(src).to(self.dev)
+        buf = self.__dict__.get("_lbuf")
+        need = max(1, (A.m - mb) * A.nb)
+        if buf is None or buf.numel() < need:
+            buf = self._lbuf = torch.empty(need, dtype=A.dtype, device=self.dev)
+        for j, n in enumerate(self.lcols):
+            if n >= self.kt - 1:
+                break
+            s0 = (n + 1) * mb
+            cnt = A.m - s0
+            o = int(off[n])
+            ops.rows_perm_col(A.data, A.ld, mb, self.rowoff, self.coloff_h[j], A.tile_cols(n), srcd[o:o + cnt], s0, cnt,
+                              buf, self.info)
+
     def add_tasks(self, tp, tag):
         """PANEL/SWAP/NEXT/REST tasks of every step; with look-ahead PANEL(k+1) overlaps REST(k)."""
         if not self.lookahead:
             prev = None
             for k in range(self.kt):
                 prev = tp.task(f"{tag}({k})", "update", (lambda k=k: self.step(k)), [prev])
+            if self.defer_left:
+                tp.task("LEFTALL", "update", self.left_all, [prev])
             return
         nxt = rest = None
         if self.xmode:
@@ -991,6 +1033,8 @@ class _GetrfDev:
             t_s = tp.task(f"SWAP({k})", "update", (lambda k=k: self.swap(k)), [t_p, rest], prio=2)
             nxt = tp.task(f"NEXT({k})", "panel", (lambda k=k: self.next(k)), [t_s], prio=2)
             rest = tp.task(f"REST({k})", "update", (lambda k=k: self.rest(k)), [t_s], prio=1)
+        if self.defer_left:
+            tp.task("LEFTALL", "update", self.left_all, [nxt, rest], prio=0)
 
 
 def _permute_rows_2d(ctx, A, dst_rows, src_rows, coltiles):

@@ -126,6 +126,8 @@ _SIGS = {
     "dpl_xchg_close": [c_vp],
     "dpl_xchg_free": [c_vp],
     "dpl_ipc_handle_bytes": [],
+    "dpl_rows_perm_col": [c_int, c_vp, c_int, c_int, c_vp, c_int, c_ll, c_int, c_vp, c_int, c_int, c_vp, c_vp,
+                          c_vp],
     "dpl_rows_permute": [c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp,
                          c_int, c_vp, c_vp],
     # cross-process-row interchanges: dst, src, cnt, r0, mb, prow, nrt, me, P, ldx, xo, info, stream

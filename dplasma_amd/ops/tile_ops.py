@@ -1092,6 +1092,28 @@ def piv_moves(ipiv: torch.Tensor, kb: int, dst: torch.Tensor, src: torch.Tensor,
     cnt[0] = len(moves)
 
 
+def rows_perm_col(A: torch.Tensor, ld: int, mb: int, rowoff: torch.Tensor, coff: int, ncols: int, src: torch.Tensor,
+                  r0: int, cnt: int, buf: torch.Tensor, info: torch.Tensor = None):
+    """One tile column's rows [r0, r0 + cnt) take the former rows src[0:cnt) (element (r, c) at
+    rowoff[r // mb] + r % mb + coff + c * ld): the deferred left interchanges of getrf_1d.  buf: cnt x ncols scratch."""
+    if cnt <= 0 or ncols <= 0:
+        return
+    if _is_gpu(A):
+        rc = _lib.load().dpl_rows_perm_col(_lib.prec_code(A.dtype), A.data_ptr(), ld, mb, rowoff.data_ptr(),
+                                           int(rowoff.numel()), int(coff), int(ncols), src.data_ptr(), int(r0), int(cnt),
+                                           buf.data_ptr(), _iptr(info), _lib.stream_ptr())
+        _lib.check(rc, "rows_perm_col")
+        return
+    ro = rowoff.to(torch.int64)
+    cols = torch.arange(ncols, dtype=torch.int64) * ld + int(coff)
+
+    def addr(rows):
+        rows = rows.to(torch.int64)
+        return (ro[rows // mb] + rows % mb)[:, None] + cols[None, :]
+    vals = A[addr(src[:cnt])].clone()
+    A[addr(torch.arange(r0, r0 + cnt))] = vals
+
+
 def rows_permute(A: torch.Tensor, ld: int, mb: int, r0: int, rowoff: torch.Tensor, coloff: torch.Tensor,
                  ncols: torch.Tensor, nb: int, dst: torch.Tensor, src: torch.Tensor, cnt: torch.Tensor, maxcnt: int,
                  info: torch.Tensor = None):

@@ -195,3 +195,39 @@ def test_gpu_getrf_nopiv(prec, N, NB):
     L = torch.tril(lu, -1) + torch.eye(N, dtype=a.dtype)
     err = ((L @ torch.triu(lu) - a).abs().max() / a.abs().max()).item()
     assert err < (1e-4 if prec in "sc" else 1e-12), err
+
+
+@pytest.mark.parametrize("M,N,NB", [(300, 160, 32), (160, 300, 32), (257, 257, 64)])
+def test_getrf_1d_deferred_left_interchanges(monkeypatch, M, N, NB):
+    """DPLASMA_LU_DEFER_LEFT=1: trailing-only interchanges per step + one composed permutation per factored column at
+    the end (piv_compose_left / rows_perm_col) -- the same element moves, so factors and pivots are bit-identical."""
+    import dplasma_amd as dp
+    ctx = dp.init(device="cpu")
+    out = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DPLASMA_LU_DEFER_LEFT", mode)
+        A = dp.block_cyclic(ctx, torch.float64, NB, NB, M, N)
+        dp.plrnt(ctx, A, 5)
+        IP = dp.ipiv_descriptor(ctx, A)
+        tp = dp.getrf_1d_New(ctx, A, IP)
+        assert tp._state.defer_left == (mode == "1")
+        tp.execute(ctx)
+        out.append((A.to_dense_local().clone(), IP.to_dense_local().clone()))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+
+
+def test_piv_compose_left_matches_sequential_swaps():
+    import numpy as np
+    from dplasma_amd.runtime.dag import _lib_rt
+    rng = np.random.default_rng(1)
+    for (m, nb, K) in [(100, 16, 100), (257, 32, 200), (300, 32, 96)]:
+        kt = -(-K // nb)
+        ip = np.array([rng.integers(i, m) + 1 for i in range(K)], dtype=np.int32)
+        src, off = _lib_rt().piv_compose_left(ip, m, nb, kt)
+        for n in range(kt - 1):
+            s = (n + 1) * nb
+            perm = np.arange(m)
+            for i in range(s, K):
+                q = ip[i] - 1
+                perm[[i, q]] = perm[[q, i]]
+            assert (src[off[n]:off[n] + m - s] == perm[s:]).all()
