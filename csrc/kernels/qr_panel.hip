@@ -30,6 +30,8 @@
 // Output: P holds R (upper) and V (strictly below the diagonal), V holds V explicitly (unit
 // diagonal, zeros above) for the trailing GEMMs, Tm the full upper-triangular kf x kf T
 // (its strictly-lower part is left untouched: callers keep it zero).
+#include <cstdlib>
+
 #include "common.h"
 #include "grid_sync.h"
 
@@ -840,6 +842,19 @@ DPL_API int dpl_qr_panel(int prec, void* P, int ldp, int rbl, long long rstride,
   int G = (M + QP_R - 1) / QP_R;
   if (G > cus) return -4;
   if (G < 1) G = 1;
+  {  // DPLASMA_QP_GMIN=g (measurement knob): at least g workgroups -- short panels (TT kills: 2 x nb rows) get more
+     // hands for their Y partials and T coupling, at the price of wider per-column reductions
+    static int gmin = -1, rmax = -1;
+    if (gmin < 0) {
+      const char* e = getenv("DPLASMA_QP_GMIN");
+      gmin = e ? atoi(e) : 0;
+      const char* r = getenv("DPLASMA_QP_RMAX");   // at most this many rows per workgroup (measurement knob)
+      rmax = r ? atoi(r) : 0;
+    }
+    int want = gmin;
+    if (rmax > 0 && (M + rmax - 1) / rmax > want) want = (M + rmax - 1) / rmax;
+    if (want > G) G = want < cus ? (want < M ? want : M) : cus;
+  }
   const int R = (M + G - 1) / G;
   long long off[6];
   qp_layout(prec == DPL_D ? 8 : 4, nc, kf, off);

@@ -51,13 +51,24 @@ def run(M, nb, tt, reps=5):
     R = torch.triu(P.view(nb, M).t()[:nb])
     ref = torch.linalg.qr(P0, mode="r")[1]
     err = (R.abs() - ref.abs()).abs().max().item() / ref.abs().max().item()
+    # Q R with Q = I - V T V^T from the kernel's explicit V and T: the factorisation itself, not only |R|
+    Vm = V.view(nb, ld).t()[:M]
+    Tt = torch.triu(Tm.view(nb, nb).t())
+    X = torch.zeros(M, nb, dtype=torch.float64, device=dev)
+    X[:nb] = R
+    rec = X - Vm @ (Tt @ (Vm.t() @ X))
+    qerr = ((rec - P0).abs().max() / P0.abs().max()).item()
     p = prof.cpu().tolist()
     tot = sum(p[:8]) or 1
     phases = ", ".join(f"{PH[i]} {p[i] / 100:.0f}us" for i in range(8) if p[i])
     if p[13]:
         phases += f", (col-effects {p[13] / 100:.0f}us)"
-    print(f"M={M:6d} {('TTr' if tt == 'real' else 'TT') if tt else 'TS'} G={-(-M // 256):3d}  {min(ts):7.3f} ms  fast {p[8]} exact {p[9]} "
-          f"first_exact {p[10]}  |R| err {err:.1e}\n    {phases}", flush=True)
+    import os
+    gm = int(os.environ.get("DPLASMA_QP_GMIN", "0"))
+    rm = int(os.environ.get("DPLASMA_QP_RMAX", "0"))
+    gq = max(-(-M // 256), min(gm, M), -(-M // rm) if rm else 0)
+    print(f"M={M:6d} {('TTr' if tt == 'real' else 'TT') if tt else 'TS'} G={min(gq, 256):3d}  {min(ts):7.3f} ms  fast {p[8]} exact {p[9]} "
+          f"first_exact {p[10]}  |R| err {err:.1e}  QR err {qerr:.1e}\n    {phases}", flush=True)
 
 
 if __name__ == "__main__":
