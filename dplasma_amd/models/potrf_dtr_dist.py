@@ -360,7 +360,9 @@ class Emulation:
         self.args_d = torch.empty(img.size, dtype=torch.uint8, device=dev)
         self.epoch = 0
         ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-        self.nwg = int(os.environ.get("DPLASMA_DTR_WG", 2 * ncu))
+        # one workgroup per CU, as the process mode and the one-GPU DTR (the round-5 figures were taken with
+        # DPLASMA_DTR_WG=256; two per CU models the grid ~2x slower at 32k: 22 % vs 39 %, r6_b39 / r6_b41)
+        self.nwg = int(os.environ.get("DPLASMA_DTR_WG", ncu))
 
     def reset(self):
         for Ar, a0 in zip(self.A, self.A0):
