@@ -288,6 +288,8 @@ class _GetrfDev:
         self.gxp2p = g.P > 1 and pivot and self.panel_mode == "gather"
         # RNF is switched off: the 2 x 4 one-GPU rehearsal gives wrong factors (correct pivots) with it, before and after
         # the round-6 LSEND buffer fix (tools/gpu/r6_b27.sh) -- DPLASMA_LU_RNF=1 is ignored with a warning until fixed
+        # (r6 debug run: the wrong tiles are the left (already factored) columns of the redundant-factorising process
+        # column, rows moved by late steps -- its LEFT interchanges)
         self.rnf = False
         if self.gxp2p and self.xmode and g.Q > 1 and os.environ.get("DPLASMA_LU_RNF", "0") == "1":
             import warnings

@@ -82,6 +82,12 @@ def main():
     # by the ranks that need them, DPLASMA_LU_PANEL=gather -- have no per-column exchange)
     need_ipc = os.environ.get("DPLASMA_LU_PANEL") == "dist" and os.environ.get("DPLASMA_LU_XCHG") != "host"
     ok = info == 0 and info1 == 0 and same and diff < 1e-8 and (mode == "ipc" or not need_ipc)
+    if not ok and ctx.rank == 0:   # which tiles differ (tile row, tile column, max |diff|), first ones
+        dd = (fac - B.to_dense_local().cpu()).abs()
+        bad = [(m, n, dd[m * NB:(m + 1) * NB, n * NB:(n + 1) * NB].max().item())
+               for m in range(-(-N // NB)) for n in range(-(-N // NB))]
+        bad = [b for b in bad if b[2] > 1e-8]
+        print(f"rank 0: {len(bad)} tiles differ; first: {bad[:24]}", flush=True)
     flags = torch.tensor([int(ok)])
     dist.all_reduce(flags, op=dist.ReduceOp.MIN)
     print(f"rank {ctx.rank}: lu dist {ctx.P}x{ctx.Q} N={N} NB={NB} exchange={mode}: {t:.3f} s, panels on this rank "
