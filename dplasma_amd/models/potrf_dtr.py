@@ -561,6 +561,76 @@ class PotrfScratch:
 _PLANS = {}
 
 
+def _plan_cache_path(nt, D, lo_order, min_tiles, head):
+    """On-disk cache of a one-process plan and its push-scheduling arrays (the 64k plan: 1.57 M tasks, 13 M edges,
+    ~6.5 s of host time to build).  Keyed by the plan parameters, the priority knobs and a hash of this module's
+    source, so an edited planner never reads an old plan.  DPLASMA_DTR_PLAN_CACHE: directory (default
+    ~/.cache/dplasma_amd), "0" disables."""
+    import hashlib
+    d = os.environ.get("DPLASMA_DTR_PLAN_CACHE", os.path.join(os.path.expanduser("~"), ".cache", "dplasma_amd"))
+    if d == "0" or nt < 48:   # (small plans build in well under a second)
+        return None
+    with open(__file__, "rb") as f:
+        src = hashlib.sha1(f.read()).hexdigest()[:12]
+    knobs = f"{UPD_BUCKETS}_{os.environ.get('DPLASMA_DTR_BL_W', '')}"
+    tag = hashlib.sha1(f"{nt}_{D}_{lo_order}_{min_tiles}_{head}_{knobs}_{src}".encode()).hexdigest()[:16]
+    return os.path.join(d, f"dtr_plan_{nt}_{tag}.npz")
+
+
+_PLAN_ARR = ("reqs", "hi", "lo", "lo_off", "final_ver", "F", "key", "is_hi", "block_of")
+_PLAN_INT = ("nt", "S", "D", "ncnt", "WB")
+
+
+def _plan_load(path):
+    """A cached plan (None when absent or unreadable); plain arrays only (allow_pickle=False)."""
+    try:
+        with np.load(path, allow_pickle=False) as z:
+            pl = _Plan.__new__(_Plan)
+            pl.tasks = z["tasks"].view(TASK_DT).reshape(-1)
+            for n in _PLAN_ARR:
+                setattr(pl, n, z[n])
+            for n in _PLAN_INT:
+                setattr(pl, n, int(z[n]))
+            pl.order = str(z["order"])
+            pl.blocks = [tuple(int(x) for x in b) for b in z["blocks"]]
+            pl._queue = {n[2:]: z[n] for n in z.files if n.startswith("q_")}
+        return pl
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def _plan_save(path, pl):
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        arrs = {n: getattr(pl, n) for n in _PLAN_ARR}
+        arrs.update({n: np.int64(getattr(pl, n)) for n in _PLAN_INT})
+        arrs["tasks"] = pl.tasks.view(np.uint8)
+        arrs["order"] = np.array(pl.order)
+        arrs["blocks"] = np.array(pl.blocks, dtype=np.int64).reshape(-1, 2)
+        arrs.update({f"q_{n}": v for n, v in pl._queue.items()})
+        tmp = f"{path}.{os.getpid()}.tmp.npz"
+        np.savez(tmp, **arrs)
+        os.replace(tmp, path)   # (atomic: a concurrent reader sees the old file or the whole new one)
+    except OSError:
+        pass
+
+
+def _get_plan(nt, D, lo_order, min_tiles, head):
+    key = (nt, D, lo_order, min_tiles, head)
+    plan = _PLANS.get(key)
+    if plan is not None:
+        return plan
+    path = _plan_cache_path(nt, D, lo_order, min_tiles, head)
+    plan = _plan_load(path) if path and os.path.exists(path) else None
+    if plan is None:
+        plan = _Plan(nt, D, lo_order, min_tiles, head)
+        if path:
+            plan._queue = queue_plan(plan)
+            _plan_save(path, plan)
+    _PLANS[key] = plan
+    return plan
+
+
 def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     from ..ops import _lib
     if not supported(ctx, uplo, A):
@@ -573,10 +643,7 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     lo_order = os.environ.get("DPLASMA_DTR_LO_ORDER", "column")
     min_tiles = int(os.environ.get("DPLASMA_DTR_DEFER_MIN_TILES", "0"))
     head = _head_env()
-    key = (nt, D, lo_order, min_tiles, head)
-    plan = _PLANS.get(key)
-    if plan is None:
-        plan = _PLANS[key] = _Plan(nt, D, lo_order, min_tiles, head)
+    plan = _get_plan(nt, D, lo_order, min_tiles, head)
     dev = A.device
     tp = Taskpool("potrf", ctx)
     tp.flops = flops(A.prec, "potrf", A.n)
