@@ -1,7 +1,8 @@
 // Composition of LU row interchanges for the deferred left-column pass of getrf_1d (DPLASMA_LU_DEFER_LEFT): for
 // every factored tile column n, the permutation that all later steps' interchanges apply to its rows [(n+1) nb, m).
 // Backward over the LAPACK pivot sequence with the map and its inverse, one O(1) update per swap -- O(K + m kt) in
-// total, where applying the swaps per column would be O(K kt).
+// total, where applying the swaps per column would be O(K kt).  Reference role: the swpback(k, n) tasks of
+// src/zgetrf_1d.jdf:360-409 (step k's interchanges applied to left column n, off the critical path).
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 

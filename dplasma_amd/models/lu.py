@@ -256,6 +256,7 @@ class _GetrfDev:
         # P == 1 (DPLASMA_LU_DEFER_LEFT, default on: 32k 34.4 -> 35.1, 64k 52.7 -> 53.6 TF/s, r6_b28): every step's interchanges touch the trailing columns only, and each factored
         # tile column gets the composition of all later steps' interchanges once, at the end (piv_compose_left +
         # rows_perm_col): each left element moves once instead of once per later step, off the steps' critical path
+        # (the reference's swpback(k, n) tasks, priority 0, chained per left column: src/zgetrf_1d.jdf:360-409)
         # (not with DPLASMA_LU_SIDE_SWAPS=1, which applies the same left moves step by step on a side stream)
         self.defer_left = (self.tmp is not None and A.grid.P == 1 and pivot and not trailing_only
                            and os.environ.get("DPLASMA_LU_SIDE_SWAPS", "0") != "1"
