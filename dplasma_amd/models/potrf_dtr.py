@@ -723,6 +723,11 @@ def potrf_dtr_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
     # progress needs a workgroup on every XCD (a low list is another XCD's to steal only once that XCD's
     # own list is exhausted) and the 16 cooperating POTRF workgroups co-resident: at least 64 of them
     nwg = max(64, min(nwg, 2 * ncu))
+    if nwg > ncu:
+        # two per CU: the idle scan skip was only exercised at one per CU (a box was lost during the first 512-
+        # workgroup run with it, cause not established), so this configuration keeps the full rescan it was
+        # validated with (0 / 100 wrong factors, profiles/r6_dtr_coresidency_rootcause.txt)
+        img.set("flags", flags_from_env() | 32)
     # scheduling: "queue" (default) -- push scheduling, a task is pushed into its priority class's ready ring by
     # the completion of its last predecessor (k_dtr_q, queue_plan); "lists" -- the static high / low lists with
     # version-counter readiness (k_dtr_potrf)
