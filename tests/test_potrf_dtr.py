@@ -520,3 +520,66 @@ def test_dtr_dist_emulation_gpu(grid):
     L, A0 = em.assemble()
     ok, res = dp.check_potrf(ctx, dp.dplasmaLower, L, A0)
     assert ok, res
+
+
+def _emulate_q_interleaved(plan, P, seed, skip=True):
+    """k_dtr_q's idle-worker protocol at the granularity of its memory operations, in random interleavings: an idle
+    worker (1) reads g.done, (2) skips the ring scan when g.done still equals the value read before its last empty scan
+    (the scan skip), else scans and pops -- and a completion (a) pushes the successors it readies, then (b) bumps
+    g.done.  Returns the number of scheduling steps; raises when every worker idles on a skipped scan while a ring
+    holds a task (the deadlock the skip must not introduce)."""
+    q = D.queue_plan(plan)
+    rng = np.random.default_rng(seed)
+    pend = q["ndeps"].astype(np.int64).copy()
+    rings = [[] for _ in range(D.NCLASS)]
+    for t in np.nonzero(pend == 0)[0]:
+        rings[q["cls"][t]].append(int(t))
+    done = 0
+    # worker: [state, task, dnow, seen]; states: "read" (about to read g.done), "scan", "run", "pushed"
+    W = [["read", -1, 0, -1] for _ in range(P)]
+    steps = 0
+    n = len(plan.tasks)
+    while done < n:
+        steps += 1
+        w = W[int(rng.integers(P))]
+        if w[0] == "read":
+            w[2] = done
+            w[0] = "scan"
+        elif w[0] == "scan":
+            if skip and w[2] == w[3]:
+                w[0] = "read"          # skipped: nothing completed since the last empty scan
+            else:
+                ring = next((r_ for r_ in rings if r_), None)
+                if ring is None:
+                    w[3] = w[2]
+                    w[0] = "read"
+                else:
+                    w[1] = ring.pop(0)
+                    w[3] = -1
+                    w[0] = "run"
+        elif w[0] == "run":
+            t = w[1]
+            for x in q["succ"][q["succ_off"][t]:q["succ_off"][t + 1]]:
+                pend[x] -= 1
+                if pend[x] == 0:
+                    rings[q["cls"][x]].append(int(x))
+            w[0] = "pushed"
+        else:   # "pushed": the completion's g.done bump, after its pushes
+            done += 1
+            w[0], w[1] = "read", -1
+        if all(x[0] in ("read", "scan") and x[2] == x[3] == done for x in W) and any(rings):
+            raise AssertionError("scan skip deadlock: every worker skips while a task is ready")
+        if steps > 200 * n * P:
+            raise AssertionError("no progress")
+    assert (pend == 0).all() and not any(rings)
+    return steps
+
+
+@pytest.mark.parametrize("nt,P", [(6, 4), (9, 16), (12, 64)])
+def test_dtr_scan_skip_protocol(nt, P):
+    """The idle scan skip (dtr.hip k_dtr_q, one process): a worker skips scanning while g.done has not moved since its
+    last empty scan; completions push before they bump g.done -- every task is popped exactly once and no interleaving
+    leaves a ready task behind sleeping workers."""
+    plan = D._Plan(nt, 4, "column", 0)
+    for seed in range(4):
+        _emulate_q_interleaved(plan, P, seed)
