@@ -583,3 +583,28 @@ def test_dtr_scan_skip_protocol(nt, P):
     plan = D._Plan(nt, 4, "column", 0)
     for seed in range(4):
         _emulate_q_interleaved(plan, P, seed)
+
+
+def test_dtr_plan_disk_cache(tmp_path, monkeypatch):
+    """The on-disk plan cache (potrf_dtr._get_plan): a second process-level lookup loads exactly the plan and push
+    arrays the first one built; a different planner source or knob misses; DPLASMA_DTR_PLAN_CACHE=0 disables it."""
+    monkeypatch.setenv("DPLASMA_DTR_PLAN_CACHE", str(tmp_path))
+    D._PLANS.clear()
+    p1 = D._get_plan(48, 4, "column", 0, ())
+    files = list(tmp_path.iterdir())
+    assert len(files) == 1 and files[0].suffix == ".npz"
+    D._PLANS.clear()
+    p2 = D._get_plan(48, 4, "column", 0, ())
+    assert p2 is not p1 and p2.tasks.dtype == p1.tasks.dtype and np.array_equal(p1.tasks, p2.tasks)
+    for n in D._PLAN_ARR:
+        assert np.array_equal(getattr(p1, n), getattr(p2, n)), n
+    assert (p1.nt, p1.S, p1.D, p1.ncnt, p1.WB, p1.order, p1.blocks) == (p2.nt, p2.S, p2.D, p2.ncnt, p2.WB, p2.order,
+                                                                        p2.blocks)
+    assert set(p1._queue) == set(p2._queue)
+    for k, v in p1._queue.items():
+        assert np.array_equal(v, p2._queue[k]), k
+    monkeypatch.setenv("DPLASMA_DTR_BL_W", "75,65,250,500")   # another priority knob: another file
+    assert D._plan_cache_path(48, 4, "column", 0, ()) != str(files[0])
+    monkeypatch.setenv("DPLASMA_DTR_PLAN_CACHE", "0")
+    assert D._plan_cache_path(48, 4, "column", 0, ()) is None
+    D._PLANS.clear()
