@@ -319,6 +319,10 @@ class _GetrfDev:
                     sp, rp = [sb.get(q) for q in range(g.P)], [rb.get(q) for q in range(g.P)]
                 return {"send": sb, "recv": rb, "sp": sp, "rp": rp}
             self.xb = {"next": xbufs(nb), "rest": xbufs(wtot)}
+            # SWAPN (panel stream) stages the next column's moved rows in a buffer of its own: sharing self.tmp with
+            # the SWAPR chunks (exchange stream) let a chunk's gather overwrite rows SWAPN had not scattered yet --
+            # the two tasks of a step have no edge between them
+            self.tmp_n = torch.zeros(2 * nb * nb, dtype=A.dtype, device=dev) if self.tmp is not None else None
             if not trailing_only:
                 self.xb["left"] = xbufs(wtot)
                 self.tmp_x = torch.zeros_like(self.tmp) if self.tmp is not None else None
@@ -913,7 +917,7 @@ class _GetrfDev:
         critical path of the look-ahead (panel stream)."""
         A, st = self.A, self.plan[k]
         j0 = st["jl"] + st["jk"]
-        self._xswap(k, j0, j0 + st["jn"], self.tmp, "next", self.g_next)
+        self._xswap(k, j0, j0 + st["jn"], self.tmp_n, "next", self.g_next)
         if "back" in st:
             ops.geadd(0, N_, 1.0, st["pv"], st["pld"], 0.0, A.data, A.ld, st["back"], copy=True)
         if "trsm_n" in st:
