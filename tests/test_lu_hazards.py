@@ -18,8 +18,8 @@ STREAM = (("PANEL(", "panel"), ("SWAPN(", "panel"), ("NEXT(", "panel"), ("LSEND(
           ("REST", "update"), ("LEFT(", "aux"), ("JOIN", "update"))
 
 
-def _gpu_stream(name):
-    for pre, s in STREAM:
+def _gpu_stream(name, streams=STREAM):
+    for pre, s in streams:
         if name.startswith(pre):
             return s
     return "update"
@@ -29,8 +29,6 @@ def _worker(rank, world, N, NB, share):
     import os
     os.environ["DPLASMA_LU_PANEL"] = "gather"
     import dplasma_amd as dp
-    from dplasma_amd.ops import tile_ops as ops
-    from dplasma_amd.parallel import comm
     ctx = dp.init(device="cpu", P=2)
     A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
     dp.plrnt(ctx, A, 3872)
@@ -43,6 +41,16 @@ def _worker(rank, world, N, NB, share):
     elif share == "rsend":       # ... and LSEND packing into the receive buffer of the next panel
         assert st.lsend_task and st.rbuf_send is not None
         st.rbuf_send = [st.rbuf, st.rbuf]
+    info, graph, acc = instrumented_run(ctx, tp, st, A)
+    return info, graph, acc
+
+
+def instrumented_run(ctx, tp, st, A):
+    """Run taskpool tp with every scratch-buffer access of its tasks recorded: (info, graph, {task: (reads,
+    writes)}), an access being (buffer name, first element, end element).  st: the engine object whose tensors are
+    the scratch buffers (the matrix A is excluded)."""
+    from dplasma_amd.ops import tile_ops as ops
+    from dplasma_amd.parallel import comm
     # tracked scratch storages: every tensor the engine owns except the matrix
     names = {}
 
@@ -142,6 +150,11 @@ def _worker(rank, world, N, NB, share):
                            ([t for t, _ in sends], [t for t, _ in recvs]))),
         (comm, "bcast", wrap(comm, "bcast", lambda t, *r, **k: ([], [t]))),
         (comm, "allreduce", wrap(comm, "allreduce", lambda t, *r, **k: ([], [t]))),
+        (comm, "exchange_add", wrap(comm, "exchange_add", lambda t, peer, tmp: ([t], [t, tmp]))),
+        (comm, "bcast_tri", wrap(comm, "bcast_tri", lambda dst, do, src, so, *r, **k: (tens(src), [dst]))),
+        (ops, "sum_partials", wrap(ops, "sum_partials", lambda src, stride, S, L, dst: ([src], [(dst, 0, L)]))),
+        (ops, "qr_panel", wrap(ops, "qr_panel", lambda P, ldp, M, nc, kf, V, ldv, Tm, ldt, ws, info, *r, **k:
+                               ([P], [P, V, Tm, ws]))),
     ]
     run0 = ops.PanelLU.run
 
@@ -176,7 +189,7 @@ def _worker(rank, world, N, NB, share):
     return info, graph, {k: (sorted(v[0]), sorted(v[1])) for k, v in acc.items()}
 
 
-def _hazards(graph, acc):
+def _hazards(graph, acc, streams=STREAM):
     anc = []
     for _, deps in graph:
         a = set(deps)
@@ -196,7 +209,7 @@ def _hazards(graph, acc):
                 if t1 == t2 or not (w1 or w2) or h1 <= l2 or h2 <= l1:
                     continue
                 a, c = min(t1, t2), max(t1, t2)
-                if _gpu_stream(graph[a][0]) == _gpu_stream(graph[c][0]):
+                if _gpu_stream(graph[a][0], streams) == _gpu_stream(graph[c][0], streams):
                     continue
                 if a not in anc[c]:
                     out.add((b, graph[a][0], graph[c][0]))
