@@ -145,6 +145,8 @@ def instrumented_run(ctx, tp, st, A):
                                  (([(tmp, 0, W * ldb), xo, cnt], tens(ptrs)) if g
                                   else (tens(ptrs) + [xo, cnt], [(tmp, 0, W * ldb)])))),
         (ops, "piv_moves", wrap(ops, "piv_moves", lambda ip, kb, d, s_, c, *r, **k: ([ip], [d, s_, c]))),
+        (ops, "rows_permute", wrap(ops, "rows_permute", lambda Ax, ld, mb, r0, ro, co, nc, nb, d, s_, c, *r, **k:
+                                   ([d, s_, c], [Ax]))),
         (ops, "rows_xord", wrap(ops, "rows_xord", lambda md, ms, mc, *r, **k: ([md, ms, mc], [r[-2]]))),
         (comm, "p2p", wrap(comm, "p2p", lambda sends=(), recvs=(), group=None, **k:
                            ([t for t, _ in sends], [t for t, _ in recvs]))),
@@ -230,3 +232,25 @@ def test_lu_2x4_cross_stream_buffer_hazards(share):
         assert any(h[1] == "rbuf" and {h[2][:5], h[3][:5]} == {"LSEND", "PANEL"} for h in found), found[:10]
     else:
         assert not found, found[:20]
+
+
+P1_STREAMS = (("PANEL(", "panel"), ("NEXT(", "panel"), ("SWAP(", "update"), ("REST(", "update"), ("LEFTALL", "update"))
+
+
+@pytest.mark.parametrize("M,N", [(256, 256), (320, 192)])
+def test_lu_one_process_lookahead_hazards(M, N):
+    """The one-process DGETRF defaults of round 6 (look-ahead PANEL / NEXT on the panel stream beside SWAP / REST, the
+    deferred left pass at the end): no unordered cross-stream conflict on a scratch buffer."""
+    import dplasma_amd as dp
+    ctx = dp.init(device="cpu")
+    A = dp.block_cyclic(ctx, torch.float64, 32, 32, M, N)
+    dp.plrnt(ctx, A, 11)
+    IP = dp.ipiv_descriptor(ctx, A)
+    tp = dp.getrf_1d_New(ctx, A, IP)
+    st = tp._state
+    assert st.lookahead and st.defer_left and len(st.pbufs) == 2
+    info, graph, acc = instrumented_run(ctx, tp, st, A)
+    assert info == 0
+    assert any(n == "LEFTALL" for n, _ in graph)
+    found = _hazards(graph, acc, P1_STREAMS)
+    assert not found, found[:20]
