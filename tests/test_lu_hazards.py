@@ -254,3 +254,35 @@ def test_lu_one_process_lookahead_hazards(M, N):
     assert any(n == "LEFTALL" for n, _ in graph)
     found = _hazards(graph, acc, P1_STREAMS)
     assert not found, found[:20]
+
+
+LUQR_STREAMS = (("LU_PANEL(", "panel"), ("LU_NEXT(", "panel"), ("QR_PANELS(", "panel"), ("QR_NEXT(", "panel"),
+                ("LU_SWAP(", "update"), ("LU_REST(", "update"), ("QR_REST(", "update"))
+
+
+@pytest.mark.parametrize("crit,alpha", [(0, 1.0), (5, 50.0)])
+def test_luqr_lookahead_hazards(monkeypatch, crit, alpha):
+    """The hybrid LU-QR device path (one process, p = 1): LU and QR steps interleaved with look-ahead across them --
+    no unordered cross-stream conflict on the LU engine's or the QR engine's scratch buffers."""
+    import types
+
+    import dplasma_amd as dp
+    monkeypatch.setenv("DPLASMA_LUQR_FAST", "1")
+    ctx = dp.init(device="cpu")
+    N, NB, IB = 256, 32, 8
+    A = dp.block_cyclic(ctx, torch.float64, NB, NB, N, N)
+    dp.plrnt(ctx, A, 3)
+    TS = dp.block_cyclic(ctx, torch.float64, IB, NB, A.mt * IB, N)
+    TT = dp.block_cyclic(ctx, torch.float64, IB, NB, A.mt * IB, N)
+    IP = dp.qrf_ipiv_descriptor(ctx, A)
+    tree = dp.hqr_init(dp.dplasmaNoTrans, A, 1, -1, -1, 1, -1, 0)
+    tp = dp.getrf_qrf_New(ctx, tree, A, IP, TS, TT, crit, alpha, [0] * A.mt)
+    assert tp.fast is not None and tp.fast.lookahead and tp.tasks
+    st = types.SimpleNamespace(**{f"lu_{k}": v for k, v in tp.fast.__dict__.items() if k not in ("A", "ctx", "plan")},
+                               **{f"qr_{k}": v for k, v in tp.qpf.__dict__.items() if k not in ("A", "ctx")})
+    info, graph, acc = instrumented_run(ctx, tp, st, A)
+    assert tp.complete(ctx) == 0
+    kinds = {n.split("(")[0] for n, _ in graph}
+    assert {"LU_PANEL", "QR_PANELS"} <= kinds, kinds
+    found = _hazards(graph, acc, LUQR_STREAMS)
+    assert not found, found[:20]
