@@ -608,3 +608,25 @@ def test_dtr_plan_disk_cache(tmp_path, monkeypatch):
     monkeypatch.setenv("DPLASMA_DTR_PLAN_CACHE", "0")
     assert D._plan_cache_path(48, 4, "column", 0, ()) is None
     D._PLANS.clear()
+
+
+def test_dtr_scheduler_model_bounds():
+    """tools/dtr_sim.py (the CPU model of the push scheduler used to rank priority schemes): every task runs once, no
+    task starts before its predecessors end, and the modelled span lies between the DAG's critical path and the
+    serial sum of the work."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "tools"))
+    import dtr_sim as S
+    plan = D._Plan(12, 4, "column", 0)
+    q = D.queue_plan(plan)
+    s, e = S.simulate(plan, q, 32)
+    assert (s >= 0).all() and (e >= s).all()
+    for t in range(len(plan.tasks)):
+        for x in q["succ"][q["succ_off"][t]:q["succ_off"][t + 1]]:
+            assert s[x] >= e[t] - 1e-9
+    T = plan.tasks
+    w = np.where(T["type"] == D.T_UPD, np.where(T["nk"] <= 1, S.DUR["upd1"], S.DUR["upd4_per_k"] * T["nk"]),
+                 np.where(T["type"] == D.T_TRSM, S.DUR["trsm"], S.DUR["potrf_blk"]))
+    cp = D.bottom_levels(q["succ_off"], q["succ"], w.astype(np.float64)).max()
+    assert cp * 0.99 <= e.max() <= (w.sum() + len(T) * 10) * 1.01
