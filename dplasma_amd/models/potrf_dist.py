@@ -171,7 +171,11 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
         return {cross(j) for j in window(k)}
 
     panels = {}
-    last_trsm = {}     # k -> TRSM(k) task (the reader of the diagonal receive buffer k % 2)
+    last_trsm = {}     # k -> TRSM(k) task
+    # parity -> the last task of this rank that read the diagonal receive buffer of that parity: the next DRECV into it
+    # waits for that reader (panel k-2 is another process column's when Q > 2, so "TRSM(k-2)" would not exist here --
+    # found by tests/test_potrf_hazards.py)
+    drecv_reader = {}
     pend = {}          # k -> {"u": Pending, "b": Pending} (this rank's batches of panel k)
     send_pend = {}     # slot -> list of Pending whose sends read that slab
     dsend_pend = {}    # k % 2 -> Pending of the diag send reading dsend[k % 2]
@@ -252,7 +256,7 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                                        hint=("potrf", kb))
                     pend.setdefault(k, {})["d"] = h
                 # the buffer pair alternates: panel k-2's TRSM must have read it (deps)
-                t_dr = tp.task(f"DRECV({k})", "comm", f_drecv, [last_trsm.get(k - 2)] if k >= 2 else [], prio=3)
+                t_dr = tp.task(f"DRECV({k})", "comm", f_drecv, [drecv_reader.get(par2)], prio=3)
                 tri_src = (t_dr, par2)
             if own_diag:
                 dests = [rank_lc(l, pc) for l in range(nlines) if l != my_line and per[l]]
@@ -273,7 +277,7 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                         dsend_pend[par2] = h
                     # (loopback: the receive buffer pair alternates as for DRECV)
                     t_dsend = tp.task(f"DSEND({k})", s_tile, f_dsend,
-                                      [t_potrf] + ([last_trsm.get(k - 2)] if self_rx and k >= 2 else []), prio=3)
+                                      [t_potrf] + ([drecv_reader.get(par2)] if self_rx else []), prio=3)
                     if self_rx:
                         tri_src = (t_dsend, par2)
             # ---------------- TRSM of my tiles of panel k
@@ -322,6 +326,8 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                     deps = [t_potrf, gate] + [t for _, t in pre]
                 t_trsm = tp.task(f"TRSM({k})", s_pan, f_trsm, deps, prio=2, comm=False)
                 last_trsm[k] = t_trsm
+                if tri_src is not None:
+                    drecv_reader[tri_src[1]] = t_trsm
             if k == nt - 1:
                 break
             # ---------------- panel k's transport
@@ -614,6 +620,7 @@ def potrf_pipelined_New(ctx, uplo: int, A, info_out=None, chunk: int = 8) -> Tas
     nxt2 = {}          # k -> NEXT2(k)
     rest2 = {}         # k -> REST2(k)
     last_trsm = {}
+    drecv_reader = {}   # parity -> the last reader of that diagonal receive buffer on this rank (see potrf_dist_New)
     slot_readers = {}
     for k in range(nt):
         kb = A.tile_rows(k)
@@ -650,7 +657,7 @@ def potrf_pipelined_New(ctx, uplo: int, A, info_out=None, chunk: int = 8) -> Tas
             def f_drecv(src=src, par2=par2, k=k, kb=kb):
                 pend[(k, "d")] = comm.start_p2p(recvs=[(drecv[par2 * ntri:(par2 + 1) * ntri], src)], group=urgent_g,
                                                 hint=("potrf", kb))
-            t_dr = tp.task(f"DRECV({k})", "comm", f_drecv, [last_trsm.get(k - 2)], prio=3)
+            t_dr = tp.task(f"DRECV({k})", "comm", f_drecv, [drecv_reader.get(par2)], prio=3)
         if own_diag:
             dests = [rank_lc(l, pc) for l in range(nlines) if l != my_line and piece(k, l)]
             if dests:
@@ -760,6 +767,8 @@ def potrf_pipelined_New(ctx, uplo: int, A, info_out=None, chunk: int = 8) -> Tas
                 trsm_tasks.append(t_tc)
                 trsm_of[c] = t_tc
                 last_trsm[k] = t_tc
+                if t_dr is not None:
+                    drecv_reader[k % 2] = t_tc
                 if first:
                     t_first = t_tc
                 first = False

@@ -158,6 +158,27 @@ def instrumented_run(ctx, tp, st, A):
         (ops, "qr_panel", wrap(ops, "qr_panel", lambda P, ldp, M, nc, kf, V, ldv, Tm, ldt, ws, info, *r, **k:
                                ([P], [P, V, Tm, ws]))),
     ]
+    pend = {}
+    start0, finish0 = comm.start_p2p, comm.finish
+
+    def start_p2p(sends=(), recvs=(), group=None, hint=None):
+        # an asynchronous exchange writes its receive buffers (and reads its send buffers) from where it starts; the
+        # tasks that finish it read them
+        sd, rv = [t for t, _ in sends], [t for t, _ in recvs]
+        note(sd, False)
+        note(rv, True)
+        h = start0(sends, recvs, group=group, hint=hint)
+        if h is not None:
+            pend[id(h)] = (sd, rv)
+        return h
+
+    def finish(h):
+        if h is not None and id(h) in pend:   # a consumer observes the data (several consumers may finish one)
+            sd, rv = pend[id(h)]
+            note(sd + rv, False)
+        return finish0(h)
+    comm.start_p2p, comm.finish = start_p2p, finish
+    saved += [(comm, "start_p2p", start0), (comm, "finish", finish0)]
     run0 = ops.PanelLU.run
 
     def run(self, ipiv, ws, cnt, info, base, *r, **k):
@@ -187,13 +208,13 @@ def instrumented_run(ctx, tp, st, A):
         ops.PanelLU.run = run0
         for mod, fname, f in saved:
             setattr(mod, fname, f)
-    graph = [(t.name, list(t.deps)) for t in tp.tasks]
+    graph = [(t.name, list(t.deps), t.stream) for t in tp.tasks]
     return info, graph, {k: (sorted(v[0]), sorted(v[1])) for k, v in acc.items()}
 
 
 def _hazards(graph, acc, streams=STREAM):
     anc = []
-    for _, deps in graph:
+    for _, deps, *_ in graph:
         a = set(deps)
         for d in deps:
             a |= anc[d]
@@ -211,7 +232,9 @@ def _hazards(graph, acc, streams=STREAM):
                 if t1 == t2 or not (w1 or w2) or h1 <= l2 or h2 <= l1:
                     continue
                 a, c = min(t1, t2), max(t1, t2)
-                if _gpu_stream(graph[a][0], streams) == _gpu_stream(graph[c][0], streams):
+                sa = _gpu_stream(graph[a][0], streams) if streams is not None else graph[a][2]
+                sc = _gpu_stream(graph[c][0], streams) if streams is not None else graph[c][2]
+                if sa == sc:
                     continue
                 if a not in anc[c]:
                     out.add((b, graph[a][0], graph[c][0]))
@@ -251,7 +274,7 @@ def test_lu_one_process_lookahead_hazards(M, N):
     assert st.lookahead and st.defer_left and len(st.pbufs) == 2
     info, graph, acc = instrumented_run(ctx, tp, st, A)
     assert info == 0
-    assert any(n == "LEFTALL" for n, _ in graph)
+    assert any(g[0] == "LEFTALL" for g in graph)
     found = _hazards(graph, acc, P1_STREAMS)
     assert not found, found[:20]
 
@@ -282,7 +305,7 @@ def test_luqr_lookahead_hazards(monkeypatch, crit, alpha):
                                **{f"qr_{k}": v for k, v in tp.qpf.__dict__.items() if k not in ("A", "ctx")})
     info, graph, acc = instrumented_run(ctx, tp, st, A)
     assert tp.complete(ctx) == 0
-    kinds = {n.split("(")[0] for n, _ in graph}
+    kinds = {g[0].split("(")[0] for g in graph}
     assert {"LU_PANEL", "QR_PANELS"} <= kinds, kinds
     found = _hazards(graph, acc, LUQR_STREAMS)
     assert not found, found[:20]
