@@ -171,7 +171,6 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
         return {cross(j) for j in window(k)}
 
     panels = {}
-    last_trsm = {}     # k -> TRSM(k) task
     # parity -> the last task of this rank that read the diagonal receive buffer of that parity: the next DRECV into it
     # waits for that reader (panel k-2 is another process column's when Q > 2, so "TRSM(k-2)" would not exist here --
     # found by tests/test_potrf_hazards.py)
@@ -325,7 +324,6 @@ def potrf_dist_New(ctx, uplo: int, A, info_out=None) -> Taskpool:
                         ops.trsm(side, uplo, dplasmaConjTrans, dplasmaNonUnit, 1.0, tb_, tl, A.data, A.ld, tb)
                     deps = [t_potrf, gate] + [t for _, t in pre]
                 t_trsm = tp.task(f"TRSM({k})", s_pan, f_trsm, deps, prio=2, comm=False)
-                last_trsm[k] = t_trsm
                 if tri_src is not None:
                     drecv_reader[tri_src[1]] = t_trsm
             if k == nt - 1:
@@ -619,7 +617,6 @@ def potrf_pipelined_New(ctx, uplo: int, A, info_out=None, chunk: int = 8) -> Tas
     nxt_chunk = {}     # (k, chunk) -> NEXT(k, chunk) task on this rank
     nxt2 = {}          # k -> NEXT2(k)
     rest2 = {}         # k -> REST2(k)
-    last_trsm = {}
     drecv_reader = {}   # parity -> the last reader of that diagonal receive buffer on this rank (see potrf_dist_New)
     slot_readers = {}
     for k in range(nt):
@@ -766,7 +763,6 @@ def potrf_pipelined_New(ctx, uplo: int, A, info_out=None, chunk: int = 8) -> Tas
                 t_tc = tp.task(f"TRSM({k},{c})", "panel", f_tc, deps, prio=2, comm=False)
                 trsm_tasks.append(t_tc)
                 trsm_of[c] = t_tc
-                last_trsm[k] = t_tc
                 if t_dr is not None:
                     drecv_reader[k % 2] = t_tc
                 if first:
