@@ -290,7 +290,9 @@ class _GetrfDev:
         # RNF is switched off: the 2 x 4 one-GPU rehearsal gives wrong factors (correct pivots) with it, before and after
         # the round-6 LSEND buffer fix (tools/gpu/r6_b27.sh) -- DPLASMA_LU_RNF=1 is ignored with a warning until fixed
         # (r6 debug run: the wrong tiles are the left (already factored) columns of the redundant-factorising process
-        # column, rows moved by late steps -- its LEFT interchanges)
+        # column, rows moved by late steps -- its LEFT interchanges).  The cross-stream hazard checker
+        # (tests/test_lu_hazards.py) finds no scratch-buffer race with RNF forced on; tracking the matrix storage by
+        # element span flags the same pairs with and without RNF (tile spans overlap), so the cause is still open
         self.rnf = False
         if self.gxp2p and self.xmode and g.Q > 1 and os.environ.get("DPLASMA_LU_RNF", "0") == "1":
             import warnings
